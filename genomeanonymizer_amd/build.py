@@ -1,0 +1,86 @@
+"""In-tree build of the native libraries (no JIT cache: the .so files travel with the repo
+snapshot to the GPU box).
+
+* ``genomeanonymizer_amd/libganon_hip.so``  — HIP kernels + C ABI (include/ganon.h), gfx950
+* ``genomeanonymizer_amd/libganon_host.so`` — BAM decoder + FASTQ formatter (include/ganon_host.h)
+* ``oracle/build/libganon_oracle.so``       — CPU restatement used by tests/bench only
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+HIP_LIB = os.path.join(PKG, "libganon_hip.so")
+HOST_LIB = os.path.join(PKG, "libganon_host.so")
+ORACLE_LIB = os.path.join(REPO, "oracle", "build", "libganon_oracle.so")
+ARCH = "gfx950"
+
+
+def _hipcc() -> str:
+    for cand in (shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found: the HIP library cannot be built")
+
+
+def _stale(target: str, sources) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(s) > t for s in sources)
+
+
+def _run(cmd) -> None:
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        sys.stderr.write(res.stdout + res.stderr)
+        raise RuntimeError(f"build failed: {' '.join(cmd)}")
+
+
+def build_hip(force: bool = False) -> str:
+    src = os.path.join(CSRC, "ganon_hip.hip")
+    hdr = os.path.join(REPO, "include", "ganon.h")
+    if force or _stale(HIP_LIB, [src, hdr, __file__]):
+        tmp = HIP_LIB + ".tmp"
+        _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+              "-fvisibility=hidden", "-Wno-unused-result", "-o", tmp, src])
+        os.replace(tmp, HIP_LIB)
+    return HIP_LIB
+
+
+def build_host(force: bool = False) -> str:
+    src = os.path.join(CSRC, "ganon_host.cpp")
+    hdr = os.path.join(REPO, "include", "ganon_host.h")
+    if force or _stale(HOST_LIB, [src, hdr, __file__]):
+        tmp = HOST_LIB + ".tmp"
+        _run(["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-fvisibility=hidden", "-pthread",
+              "-o", tmp, src, "-lz"])
+        os.replace(tmp, HOST_LIB)
+    return HOST_LIB
+
+
+def build_oracle(force: bool = False) -> str:
+    src = os.path.join(REPO, "oracle", "ganon_oracle.c")
+    hdr = os.path.join(REPO, "include", "ganon.h")
+    os.makedirs(os.path.dirname(ORACLE_LIB), exist_ok=True)
+    if force or _stale(ORACLE_LIB, [src, hdr, __file__]):
+        tmp = ORACLE_LIB + ".tmp"
+        _run(["gcc", "-O2", "-std=c11", "-fPIC", "-shared", "-o", tmp, src])
+        os.replace(tmp, ORACLE_LIB)
+    return ORACLE_LIB
+
+
+def build_all(force: bool = False) -> None:
+    build_host(force)
+    build_oracle(force)
+    build_hip(force)
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv)
+    print("built:", HIP_LIB, HOST_LIB, ORACLE_LIB)

@@ -1,0 +1,961 @@
+// ganon_hip.hip — MI355X (gfx950) germline-variant masking kernels + the C ABI of
+// include/ganon.h (libganon_hip.so).
+//
+// Reference semantics (per scope = one CompleteGermlineAnonymizer.anonymize call,
+// anonymizer_methods.py:431-535):
+//   tally     process_snv for every aligned base of every scope read
+//             (variation_classifier.py:144-182, :185-215): base != 'N', base != ref,
+//             ref in ACGT -> observation (pos, allele, tumor|normal);
+//   classify  SomaticVariationType state machine (variants.py:33-39): a call ends in
+//             TUMORAL_NORMAL_VARIANT iff it was observed in >=1 tumor AND >=1 normal read;
+//   mask      at the normal column: every supporting read of a TN call other than the
+//             kept window variant gets the reference base (anonymizer_methods.py:537-556,
+//             :170-176); the call is counted for the statistics (:555-556).
+//
+// Design: integer/byte work, HBM-bound — no MFMA. One workgroup owns one
+// scope (or a 16 Ki-position tile of a wide scope). The scope's reference slice and a
+// per-position tally live in LDS: 1 byte per position (tumor ACGT nibble | normal ACGT
+// nibble, updated with ds_or_b32 on the containing dword). nt16 codes of A, C, G, T are
+// one-hot (1, 2, 4, 8), so a nibble IS the allele set and TN = tumor & normal.
+// Non-ACGTN read bases ("=" and IUPAC codes) are rare; a scope that meets one is re-run
+// on a 16-code tally (4 bytes per position: tumor code mask | normal code mask << 16).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <numeric>
+#include <string>
+#include <type_traits>
+#include <vector>
+
+#include "../../include/ganon.h"
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kWaves = kBlock / 64;
+constexpr int kSmallCap0 = 4096;    // positions, class 0
+constexpr int kSmallCap1 = 16384;   // positions, class 1 (= wide cap)
+constexpr int kTile = 16384;        // positions per tile of a large scope
+constexpr int kPersistGrid = 1024;  // grid of the device-counted (rare) re-run kernels
+
+struct Tile {
+  int32_t scope;
+  int32_t a;      // tile covers [a, b) (contig positions)
+  int32_t b;
+  int32_t pad;
+  int64_t lo;     // candidate range in large_incid
+  int64_t hi;
+};
+
+// Device view of a batch (all pointers device-resident).
+struct DevBatch {
+  const int32_t *ref_start, *read_len, *read_end, *n_cig, *write_scope;
+  const int64_t *seq_off, *cig_off;
+  const uint8_t *seq, *dataset;
+  const uint32_t *cigar;
+  const int64_t *incid_off;
+  const int32_t *incid_read;
+  const int32_t *span_start, *span_len, *keep_pos;
+  const int64_t *ref_off;
+  const uint8_t *ref, *keep_code;
+};
+
+__device__ __forceinline__ int nib_at(const uint8_t *__restrict__ buf, int64_t i) {
+  const uint8_t b = buf[i >> 1];
+  return (i & 1) ? (b & 0xF) : (b >> 4);
+}
+
+__device__ __forceinline__ bool is_acgt(int c) { return c != 0 && (c & (c - 1)) == 0 && c <= 8; }
+
+// Per-lane monotone walk over a read's CIGAR: query positions visited in increasing order.
+struct CigarCursor {
+  const uint32_t *cig;
+  int n, k;
+  int q0;        // first query position of op k
+  int r0;        // first reference position of op k
+  int qlen, rlen, op;
+
+  __device__ __forceinline__ void load() {
+    if (k < n) {
+      const uint32_t w = cig[k];
+      op = w & 0xF;
+      const int len = (int)(w >> 4);
+      qlen = (op == 0 || op == 1 || op == 4 || op == 7 || op == 8) ? len : 0;
+      rlen = (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) ? len : 0;
+    }
+  }
+  __device__ __forceinline__ void init(const uint32_t *c, int nc, int ref_start) {
+    cig = c; n = nc; k = 0; q0 = 0; r0 = ref_start; qlen = rlen = 0; op = 0;
+    load();
+  }
+  // Returns the reference position aligned to query position q (M/=/X), or -1 when q sits
+  // in an I/S op or beyond the CIGAR. q must not decrease between calls.
+  __device__ __forceinline__ int ref_of(int q) {
+    while (k < n && q >= q0 + qlen) {
+      q0 += qlen; r0 += rlen; ++k;
+      load();
+    }
+    if (k >= n) return -1;
+    if (op == 0 || op == 7 || op == 8) return r0 + (q - q0);
+    return -1;
+  }
+};
+
+__device__ __forceinline__ int block_sum(int v, int *scratch) {
+  // wave reduction then LDS across waves; scratch holds kWaves ints.
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) scratch[wave] = v;
+  __syncthreads();
+  int t = 0;
+#pragma unroll
+  for (int w = 0; w < kWaves; ++w) t += scratch[w];
+  return t;
+}
+
+// ---- tally of one read into the LDS table covering [a, b) ------------------------------
+// TB = bytes per position: 1 (ACGT nibbles) or 4 (16-code masks). Returns true when a
+// non-ACGTN base that would be a call was seen (only meaningful for TB == 1).
+template <int TB>
+__device__ __forceinline__ bool tally_read(const DevBatch &B, int r, int a, int b,
+                                           uint32_t *tab, const uint8_t *refb, int lane) {
+  const int L = B.read_len[r];
+  const int ds = B.dataset[r];
+  const int64_t sq = B.seq_off[r] * 2;
+  CigarCursor cur;
+  cur.init(B.cigar + B.cig_off[r], B.n_cig[r], B.ref_start[r]);
+  bool rare = false;
+  for (int q = lane; q < L; q += 64) {
+    const int p = cur.ref_of(q);
+    if (p < a || p >= b) continue;
+    const int c = nib_at(B.seq, sq + q);
+    const int off = p - a;
+    const int rc = (refb[off >> 1] >> ((off & 1) ? 0 : 4)) & 0xF;
+    if (c == 15 || c == rc || !is_acgt(rc)) continue;
+    if (TB == 1) {
+      if (is_acgt(c)) atomicOr(&tab[off >> 2], (uint32_t)c << (ds * 4 + (off & 3) * 8));
+      else rare = true;
+    } else {
+      atomicOr(&tab[off], (1u << c) << (16 * ds));
+    }
+  }
+  return rare;
+}
+
+template <int TB>
+__device__ __forceinline__ uint32_t tn_mask(const uint32_t *tab, int off) {
+  if (TB == 1) {
+    const uint32_t byte = (tab[off >> 2] >> ((off & 3) * 8)) & 0xFF;
+    return byte & (byte >> 4) & 0xF;                  // ACGT one-hot codes
+  } else {
+    const uint32_t w = tab[off];
+    return w & (w >> 16) & 0xFFFF;                    // bit c = code c
+  }
+}
+
+template <int TB>
+__device__ __forceinline__ bool tn_hit(uint32_t tn, int c) {
+  if (TB == 1) return is_acgt(c) && (tn & (uint32_t)c);
+  return (tn >> c) & 1u;
+}
+
+template <int TB>
+__device__ __forceinline__ int tn_count(uint32_t tn) { return __popc(tn); }
+
+// Stage the reference nibbles of [a, a + span) into LDS (packed, nibble 0 = position a).
+__device__ __forceinline__ void stage_ref(const DevBatch &B, int64_t nib0, int span, uint8_t *refb) {
+  const int nbytes = (span + 1) >> 1;
+  for (int j = threadIdx.x; j < nbytes; j += kBlock) {
+    const int64_t n0 = nib0 + 2 * (int64_t)j;
+    const int hi = nib_at(B.ref, n0);
+    const int lo = (2 * j + 1 < span) ? nib_at(B.ref, n0 + 1) : 0;
+    refb[j] = (uint8_t)((hi << 4) | lo);
+  }
+}
+
+// Clear the tumor bit of the kept allele so the kept call is neither masked nor counted.
+template <int TB>
+__device__ __forceinline__ void clear_keep(const DevBatch &B, int s, int a, int b, uint32_t *tab) {
+  if (threadIdx.x != 0) return;
+  const int kp = B.keep_pos[s];
+  if (kp < a || kp >= b) return;
+  const int kc = B.keep_code[s];
+  const int off = kp - a;
+  if (TB == 1) {
+    if (is_acgt(kc)) atomicAnd(&tab[off >> 2], ~((uint32_t)kc << ((off & 3) * 8)));
+  } else {
+    atomicAnd(&tab[off], ~(1u << kc));
+  }
+}
+
+// Write the masked copy of read r (all bytes) using the LDS tally of [a, b).
+template <int TB>
+__device__ __forceinline__ int mask_read_lds(const DevBatch &B, int r, int a, const uint32_t *tab,
+                                             const uint8_t *refb, uint8_t *__restrict__ out, int lane) {
+  const int L = B.read_len[r];
+  const int64_t so = B.seq_off[r];
+  CigarCursor cur;
+  cur.init(B.cigar + B.cig_off[r], B.n_cig[r], B.ref_start[r]);
+  int masked = 0;
+  const int nbytes = (L + 1) >> 1;
+  for (int j = lane; j < nbytes; j += 64) {
+    const uint8_t in = B.seq[so + j];
+    int nb[2] = {in >> 4, in & 0xF};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int q = 2 * j + h;
+      if (q >= L) break;
+      const int p = cur.ref_of(q);
+      if (p < 0) continue;
+      const int off = p - a;
+      const uint32_t tn = tn_mask<TB>(tab, off);
+      if (tn && tn_hit<TB>(tn, nb[h])) {
+        nb[h] = (refb[off >> 1] >> ((off & 1) ? 0 : 4)) & 0xF;
+        ++masked;
+      }
+    }
+    out[so + j] = (uint8_t)((nb[0] << 4) | nb[1]);
+  }
+  return masked;
+}
+
+// ---- kernels ---------------------------------------------------------------------------
+
+// Reads written unmasked (write_scope == -1): plain copy.
+__global__ void __launch_bounds__(kBlock) k_passthrough(const DevBatch B, const int32_t *__restrict__ list,
+                                                        int n, uint8_t *__restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int gw = (blockIdx.x * kBlock + threadIdx.x) >> 6;
+  const int nw = (gridDim.x * kBlock) >> 6;
+  for (int i = gw; i < n; i += nw) {
+    const int r = list[i];
+    const int64_t so = B.seq_off[r];
+    const int nbytes = (B.read_len[r] + 1) >> 1;
+    for (int j = lane; j < nbytes; j += 64) out[so + j] = B.seq[so + j];
+  }
+}
+
+// One workgroup per small scope (span <= cap): tally -> classify -> mask, all in LDS.
+// count_ptr != nullptr: the list length lives on the device (re-run of rare scopes).
+template <int TB>
+__global__ void __launch_bounds__(kBlock) k_scope_small(const DevBatch B, const int32_t *__restrict__ list,
+                                                        int n_static, const int32_t *count_ptr, int cap,
+                                                        uint8_t *__restrict__ out, int32_t *scope_calls,
+                                                        int32_t *scope_bases, int32_t *rare_list,
+                                                        int32_t *rare_count) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  const int tab_words = cap * TB / 4;
+  uint32_t *tab = smem;
+  uint8_t *refb = reinterpret_cast<uint8_t *>(smem + tab_words);
+  int *scratch = reinterpret_cast<int *>(refb + ((cap / 2 + 15) & ~15));
+  const int n = count_ptr ? *count_ptr : n_static;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int li = blockIdx.x; li < n; li += gridDim.x) {
+    const int s = list[li];
+    const int a = B.span_start[s];
+    const int span = B.span_len[s];
+    const int b = a + span;
+    const int words = (span * TB + 3) >> 2;
+    for (int w = threadIdx.x; w < words; w += kBlock) tab[w] = 0;
+    stage_ref(B, B.ref_off[s], span, refb);
+    if (threadIdx.x == 0) scratch[kWaves] = 0;
+    __syncthreads();
+    const int64_t i0 = B.incid_off[s], i1 = B.incid_off[s + 1];
+    bool rare = false;
+    for (int64_t i = i0 + wave; i < i1; i += kWaves) rare |= tally_read<TB>(B, B.incid_read[i], a, b, tab, refb, lane);
+    if (TB == 1 && rare) scratch[kWaves] = 1;
+    __syncthreads();
+    clear_keep<TB>(B, s, a, b, tab);
+    __syncthreads();
+    int calls = 0;
+    for (int off = threadIdx.x; off < span; off += kBlock) calls += tn_count<TB>(tn_mask<TB>(tab, off));
+    calls = block_sum(calls, scratch);
+    int bases = 0;
+    for (int64_t i = i0 + wave; i < i1; i += kWaves) {
+      const int r = B.incid_read[i];
+      if (B.write_scope[r] != s) continue;
+      bases += mask_read_lds<TB>(B, r, a, tab, refb, out, lane);
+    }
+    bases = block_sum(bases, scratch);
+    if (threadIdx.x == 0) {
+      scope_calls[s] = calls;
+      scope_bases[s] = bases;
+      if (TB == 1 && scratch[kWaves]) rare_list[atomicAdd(rare_count, 1)] = s;
+    }
+    __syncthreads();
+  }
+}
+
+// One workgroup per 16 Ki-position tile of a large scope: tally -> TN table (global).
+template <int TB>
+__global__ void __launch_bounds__(kBlock) k_tile_large(const DevBatch B, const Tile *__restrict__ tiles,
+                                                       const int32_t *__restrict__ tile_list, int n_static,
+                                                       const int32_t *count_ptr, const int32_t *__restrict__ large_incid,
+                                                       const int64_t *__restrict__ tab_off, uint16_t *__restrict__ tn_tab,
+                                                       int32_t *scope_calls, int32_t *rare_list, int32_t *rare_count) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  const int tab_words = kTile * TB / 4;
+  uint32_t *tab = smem;
+  uint8_t *refb = reinterpret_cast<uint8_t *>(smem + tab_words);
+  int *scratch = reinterpret_cast<int *>(refb + kTile / 2);
+  const int n = count_ptr ? *count_ptr : n_static;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int li = blockIdx.x; li < n; li += gridDim.x) {
+    const int ti = tile_list ? tile_list[li] : li;
+    const Tile t = tiles[ti];
+    const int s = t.scope;
+    const int span = t.b - t.a;
+    const int words = (span * TB + 3) >> 2;
+    for (int w = threadIdx.x; w < words; w += kBlock) tab[w] = 0;
+    stage_ref(B, B.ref_off[s] + (t.a - B.span_start[s]), span, refb);
+    if (threadIdx.x == 0) scratch[kWaves] = 0;
+    __syncthreads();
+    bool rare = false;
+    for (int64_t i = t.lo + wave; i < t.hi; i += kWaves) {
+      const int r = large_incid[i];
+      if (B.read_end[r] <= t.a || B.ref_start[r] >= t.b) continue;
+      rare |= tally_read<TB>(B, r, t.a, t.b, tab, refb, lane);
+    }
+    if (TB == 1 && rare) scratch[kWaves] = 1;
+    __syncthreads();
+    clear_keep<TB>(B, s, t.a, t.b, tab);
+    __syncthreads();
+    int calls = 0;
+    uint16_t *dst = tn_tab + tab_off[s] + (t.a - B.span_start[s]);
+    for (int off = threadIdx.x; off < span; off += kBlock) {
+      const uint32_t tn = tn_mask<TB>(tab, off);
+      uint32_t m16;
+      if (TB == 1) m16 = ((tn & 1u) << 1) | ((tn & 2u) << 1) | ((tn & 4u) << 2) | ((tn & 8u) << 5);
+      else m16 = tn;
+      dst[off] = (uint16_t)m16;
+      calls += tn_count<TB>(tn);
+    }
+    calls = block_sum(calls, scratch);
+    if (threadIdx.x == 0) {
+      const bool is_rare = (TB == 1) && scratch[kWaves];
+      if (is_rare) rare_list[atomicAdd(rare_count, 1)] = ti;
+      else if (calls) atomicAdd(&scope_calls[s], calls);
+    }
+    __syncthreads();
+  }
+}
+
+// Reads written from large scopes: one wave per read, TN table lookups in global memory.
+__global__ void __launch_bounds__(kBlock) k_mask_large(const DevBatch B, const int32_t *__restrict__ list, int n,
+                                                       const int64_t *__restrict__ tab_off,
+                                                       const uint16_t *__restrict__ tn_tab,
+                                                       uint8_t *__restrict__ out, int32_t *scope_bases) {
+  const int lane = threadIdx.x & 63;
+  const int gw = (blockIdx.x * kBlock + threadIdx.x) >> 6;
+  const int nw = (gridDim.x * kBlock) >> 6;
+  for (int i = gw; i < n; i += nw) {
+    const int r = list[i];
+    const int s = B.write_scope[r];
+    const int a = B.span_start[s];
+    const int64_t to = tab_off[s];
+    const int64_t rnib = B.ref_off[s];
+    const int L = B.read_len[r];
+    const int64_t so = B.seq_off[r];
+    CigarCursor cur;
+    cur.init(B.cigar + B.cig_off[r], B.n_cig[r], B.ref_start[r]);
+    int masked = 0;
+    for (int j = lane; j < ((L + 1) >> 1); j += 64) {
+      const uint8_t in = B.seq[so + j];
+      int nb[2] = {in >> 4, in & 0xF};
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int q = 2 * j + h;
+        if (q >= L) break;
+        const int p = cur.ref_of(q);
+        if (p < 0) continue;
+        const uint32_t tn = tn_tab[to + (p - a)];
+        if ((tn >> nb[h]) & 1u) {
+          nb[h] = nib_at(B.ref, rnib + (p - a));
+          ++masked;
+        }
+      }
+      out[so + j] = (uint8_t)((nb[0] << 4) | nb[1]);
+    }
+    for (int o = 32; o > 0; o >>= 1) masked += __shfl_xor(masked, o);
+    if (lane == 0 && masked) atomicAdd(&scope_bases[s], masked);
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_totals(const int32_t *__restrict__ calls, const int32_t *__restrict__ bases,
+                                                   int n, const int32_t *rare_small, const int32_t *rare_tiles,
+                                                   unsigned long long *totals) {
+  long long c = 0, b = 0;
+  for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+    c += calls[i];
+    b += bases[i];
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    c += __shfl_xor(c, o);
+    b += __shfl_xor(b, o);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (c) atomicAdd(&totals[GANON_T_MASKED_SNV_CALLS], (unsigned long long)c);
+    if (b) atomicAdd(&totals[GANON_T_MASKED_BASES], (unsigned long long)b);
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    atomicAdd(&totals[GANON_T_RARE_SCOPES], (unsigned long long)(*rare_small + *rare_tiles));
+}
+
+}  // namespace
+
+// ---- host side ---------------------------------------------------------------------------
+
+struct ganon_ctx {
+  int device = 0;
+  hipStream_t own = nullptr;
+  hipStream_t stream = nullptr;
+  bool profiling = false;
+  std::string err;
+  struct Rec { std::string name; hipEvent_t e0, e1; };
+  std::vector<Rec> recs;
+  std::vector<hipEvent_t> pool;
+  std::vector<ganon_kernel_time> last_times;
+};
+
+struct ganon_dbatch {
+  DevBatch B{};
+  std::vector<void *> allocs;
+  int32_t n_reads = 0, n_scopes = 0;
+  int64_t seq_bytes = 0;
+  uint8_t *out = nullptr;
+  int32_t *scope_calls = nullptr, *scope_bases = nullptr;
+  unsigned long long *totals = nullptr, *static_totals = nullptr;
+  int32_t *counters = nullptr;  // [0] rare small count, [1] rare tile count
+  int32_t *small_list[2] = {nullptr, nullptr};
+  int32_t n_small[2] = {0, 0};
+  int32_t *pt_list = nullptr;
+  int32_t n_pt = 0;
+  Tile *tiles = nullptr;
+  int32_t n_tiles = 0;
+  int32_t *large_incid = nullptr;
+  int64_t *tab_off = nullptr;
+  uint16_t *tn_tab = nullptr;
+  int64_t tn_entries = 0;
+  int32_t *large_written = nullptr;
+  int32_t n_large_written = 0;
+  int32_t n_large_scopes = 0;
+  int32_t *rare_small_list = nullptr, *rare_tile_list = nullptr;
+  int32_t max_small_span = 0;
+  bool ran = false;
+};
+
+namespace {
+
+int fail(ganon_ctx *ctx, int code, const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (ctx) ctx->err = buf;
+  return code;
+}
+
+#define HIP_OR_FAIL(call)                                                                  \
+  do {                                                                                     \
+    hipError_t e_ = (call);                                                                \
+    if (e_ != hipSuccess)                                                                  \
+      return fail(ctx, GANON_E_DEVICE, "%s failed: %s", #call, hipGetErrorString(e_));     \
+  } while (0)
+
+template <typename T>
+int dev_alloc(ganon_ctx *ctx, ganon_dbatch *db, T **p, size_t count) {
+  *p = nullptr;
+  size_t bytes = std::max<size_t>(count, 1) * sizeof(T);
+  hipError_t e = hipMalloc(reinterpret_cast<void **>(p), bytes);
+  if (e != hipSuccess) return fail(ctx, GANON_E_NOMEM, "hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
+  db->allocs.push_back(*p);
+  return GANON_OK;
+}
+
+template <typename T>
+int dev_copy(ganon_ctx *ctx, ganon_dbatch *db, T **p, const T *src, size_t count) {
+  int rc = dev_alloc(ctx, db, p, count);
+  if (rc) return rc;
+  if (count) {
+    hipError_t e = hipMemcpyAsync(*p, src, count * sizeof(T), hipMemcpyHostToDevice, ctx->stream);
+    if (e != hipSuccess) return fail(ctx, GANON_E_DEVICE, "hipMemcpyAsync H2D failed: %s", hipGetErrorString(e));
+  }
+  return GANON_OK;
+}
+
+void free_batch(ganon_dbatch *db) {
+  for (void *p : db->allocs) hipFree(p);
+  db->allocs.clear();
+}
+
+size_t small_lds_bytes(int tb, int cap) {
+  return (size_t)cap * tb + (((size_t)cap / 2 + 15) & ~(size_t)15) + 16 * sizeof(int);
+}
+
+size_t tile_lds_bytes(int tb) { return (size_t)kTile * tb + kTile / 2 + 16 * sizeof(int); }
+
+hipEvent_t get_event(ganon_ctx *ctx) {
+  if (!ctx->pool.empty()) {
+    hipEvent_t e = ctx->pool.back();
+    ctx->pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  hipEventCreate(&e);
+  return e;
+}
+
+struct KernelScope {
+  ganon_ctx *ctx;
+  ganon_ctx::Rec rec;
+  KernelScope(ganon_ctx *c, const char *name) : ctx(c) {
+    if (!ctx->profiling) return;
+    rec.name = name;
+    rec.e0 = get_event(ctx);
+    rec.e1 = get_event(ctx);
+    hipEventRecord(rec.e0, ctx->stream);
+  }
+  ~KernelScope() {
+    if (!ctx->profiling) return;
+    hipEventRecord(rec.e1, ctx->stream);
+    ctx->recs.push_back(rec);
+  }
+};
+
+int check_launch(ganon_ctx *ctx, const char *what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(ctx, GANON_E_DEVICE, "launch of %s failed: %s", what, hipGetErrorString(e));
+  return GANON_OK;
+}
+
+}  // namespace
+
+GANON_API int ganon_abi_version(void) { return GANON_ABI_VERSION; }
+
+GANON_API int ganon_ctx_create(int device, ganon_ctx **out) {
+  if (!out) return GANON_E_ARG;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0 || device < 0 || device >= n) return GANON_E_DEVICE;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return GANON_E_DEVICE;
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return GANON_E_DEVICE;
+  if (hipSetDevice(device) != hipSuccess) return GANON_E_DEVICE;
+  ganon_ctx *ctx = new ganon_ctx();
+  ctx->device = device;
+  if (hipStreamCreateWithFlags(&ctx->own, hipStreamNonBlocking) != hipSuccess) {
+    delete ctx;
+    return GANON_E_DEVICE;
+  }
+  ctx->stream = ctx->own;
+  // Every kernel gets the LDS its worst class needs.
+  hipFuncSetAttribute(reinterpret_cast<const void *>(k_scope_small<1>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                      (int)small_lds_bytes(1, kSmallCap1));
+  hipFuncSetAttribute(reinterpret_cast<const void *>(k_scope_small<4>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                      (int)small_lds_bytes(4, kSmallCap1));
+  hipFuncSetAttribute(reinterpret_cast<const void *>(k_tile_large<1>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                      (int)tile_lds_bytes(1));
+  hipFuncSetAttribute(reinterpret_cast<const void *>(k_tile_large<4>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                      (int)tile_lds_bytes(4));
+  *out = ctx;
+  return GANON_OK;
+}
+
+GANON_API int ganon_ctx_destroy(ganon_ctx *ctx) {
+  if (!ctx) return GANON_E_ARG;
+  hipSetDevice(ctx->device);
+  if (ctx->own) {
+    hipStreamSynchronize(ctx->own);
+    hipStreamDestroy(ctx->own);
+  }
+  for (auto &r : ctx->recs) {
+    hipEventDestroy(r.e0);
+    hipEventDestroy(r.e1);
+  }
+  for (auto e : ctx->pool) hipEventDestroy(e);
+  delete ctx;
+  return GANON_OK;
+}
+
+GANON_API const char *ganon_last_error(ganon_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+GANON_API int ganon_ctx_set_stream(ganon_ctx *ctx, void *hip_stream) {
+  if (!ctx) return GANON_E_ARG;
+  ctx->stream = hip_stream ? reinterpret_cast<hipStream_t>(hip_stream) : ctx->own;
+  return GANON_OK;
+}
+
+GANON_API int ganon_ctx_set_profiling(ganon_ctx *ctx, int enabled) {
+  if (!ctx) return GANON_E_ARG;
+  ctx->profiling = enabled != 0;
+  return GANON_OK;
+}
+
+static int validate(ganon_ctx *ctx, const ganon_batch *b, std::vector<int32_t> &read_end) {
+  if (b->n_reads < 0 || b->n_scopes < 0 || b->n_incid < 0 || b->seq_bytes < 0 || b->n_cigar_ops < 0 ||
+      b->ref_bytes < 0)
+    return fail(ctx, GANON_E_ARG, "negative size in batch");
+  if (b->n_reads > 0 && (!b->ref_start || !b->read_len || !b->seq_off || !b->cig_off || !b->n_cig ||
+                         !b->dataset || !b->write_scope))
+    return fail(ctx, GANON_E_ARG, "null read array");
+  if (b->seq_bytes > 0 && !b->seq_nt16) return fail(ctx, GANON_E_ARG, "null seq_nt16");
+  if (b->n_cigar_ops > 0 && !b->cigar) return fail(ctx, GANON_E_ARG, "null cigar");
+  if (!b->scope_incid_off) return fail(ctx, GANON_E_ARG, "null scope_incid_off");
+  if (b->n_scopes > 0 && (!b->scope_span_start || !b->scope_span_len || !b->scope_ref_off || !b->keep_pos ||
+                          !b->keep_code))
+    return fail(ctx, GANON_E_ARG, "null scope array");
+  if (b->n_incid > 0 && !b->incid_read) return fail(ctx, GANON_E_ARG, "null incid_read");
+  if (b->ref_bytes > 0 && !b->ref_nt16) return fail(ctx, GANON_E_ARG, "null ref_nt16");
+  read_end.assign(b->n_reads, 0);
+  for (int32_t r = 0; r < b->n_reads; ++r) {
+    const int64_t L = b->read_len[r];
+    if (L < 0 || b->seq_off[r] < 0 || b->seq_off[r] + (L + 1) / 2 > b->seq_bytes)
+      return fail(ctx, GANON_E_ARG, "read %d: sequence out of range", r);
+    if (b->n_cig[r] < 0 || b->cig_off[r] < 0 || b->cig_off[r] + b->n_cig[r] > b->n_cigar_ops)
+      return fail(ctx, GANON_E_ARG, "read %d: cigar out of range", r);
+    if (b->dataset[r] > 1) return fail(ctx, GANON_E_ARG, "read %d: dataset must be 0 or 1", r);
+    if (b->write_scope[r] < -1 || b->write_scope[r] >= b->n_scopes)
+      return fail(ctx, GANON_E_ARG, "read %d: write_scope out of range", r);
+    int64_t rl = 0;
+    for (int k = 0; k < b->n_cig[r]; ++k) {
+      const uint32_t w = b->cigar[b->cig_off[r] + k];
+      const int op = w & 0xF;
+      if (op > 8) return fail(ctx, GANON_E_ARG, "read %d: bad cigar op %d", r, op);
+      if (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) rl += w >> 4;
+    }
+    if (b->ref_start[r] < 0 || b->ref_start[r] + rl > INT32_MAX) return fail(ctx, GANON_E_ARG, "read %d: bad position", r);
+    read_end[r] = (int32_t)(b->ref_start[r] + (rl > 0 ? rl : 1));
+  }
+  if (b->scope_incid_off[0] != 0 || b->scope_incid_off[b->n_scopes] != b->n_incid)
+    return fail(ctx, GANON_E_ARG, "scope_incid_off must start at 0 and end at n_incid");
+  std::vector<uint8_t> seen(b->n_reads, 0);
+  for (int32_t s = 0; s < b->n_scopes; ++s) {
+    const int64_t i0 = b->scope_incid_off[s], i1 = b->scope_incid_off[s + 1];
+    if (i1 < i0) return fail(ctx, GANON_E_ARG, "scope %d: decreasing incidence offsets", s);
+    const int64_t ss = b->scope_span_start[s], sl = b->scope_span_len[s];
+    if (sl < 0 || ss < 0) return fail(ctx, GANON_E_ARG, "scope %d: bad span", s);
+    if (b->scope_ref_off[s] < 0 || b->scope_ref_off[s] + sl > 2 * b->ref_bytes)
+      return fail(ctx, GANON_E_ARG, "scope %d: reference slice out of range", s);
+    if (b->keep_code[s] > 15) return fail(ctx, GANON_E_ARG, "scope %d: keep_code > 15", s);
+    for (int64_t i = i0; i < i1; ++i) {
+      const int32_t r = b->incid_read[i];
+      if (r < 0 || r >= b->n_reads) return fail(ctx, GANON_E_ARG, "incidence %lld: read out of range", (long long)i);
+      if (b->ref_start[r] < ss || read_end[r] > ss + sl)
+        return fail(ctx, GANON_E_ARG, "scope %d: read %d [%d,%d) outside span [%lld,%lld)", s, r, b->ref_start[r],
+                    read_end[r], (long long)ss, (long long)(ss + sl));
+      if (b->write_scope[r] == s) seen[r] = 1;
+    }
+  }
+  for (int32_t r = 0; r < b->n_reads; ++r)
+    if (b->write_scope[r] >= 0 && !seen[r])
+      return fail(ctx, GANON_E_ARG, "read %d: write_scope %d does not contain it", r, b->write_scope[r]);
+  return GANON_OK;
+}
+
+GANON_API int ganon_batch_upload(ganon_ctx *ctx, const ganon_batch *b, ganon_dbatch **out) {
+  if (!ctx || !b || !out) return fail(ctx, GANON_E_ARG, "null argument");
+  *out = nullptr;
+  HIP_OR_FAIL(hipSetDevice(ctx->device));
+  std::vector<int32_t> read_end;
+  int rc = validate(ctx, b, read_end);
+  if (rc) return rc;
+  ganon_dbatch *db = new ganon_dbatch();
+  db->n_reads = b->n_reads;
+  db->n_scopes = b->n_scopes;
+  db->seq_bytes = b->seq_bytes;
+  auto bail = [&](int code) {
+    hipStreamSynchronize(ctx->stream);
+    free_batch(db);
+    delete db;
+    return code;
+  };
+  // ---- work lists (host) ----
+  std::vector<int32_t> small[2], pt, large_written, large_incid, large_scopes;
+  std::vector<int64_t> tab_off(b->n_scopes, -1);
+  std::vector<Tile> tiles;
+  int64_t tn_entries = 0;
+  for (int32_t s = 0; s < b->n_scopes; ++s) {
+    const int32_t sl = b->scope_span_len[s];
+    if (sl <= kSmallCap0) small[0].push_back(s);
+    else if (sl <= kSmallCap1) small[1].push_back(s);
+    else {
+      large_scopes.push_back(s);
+      tab_off[s] = tn_entries;
+      tn_entries += sl;
+      const int64_t i0 = b->scope_incid_off[s], i1 = b->scope_incid_off[s + 1];
+      const int64_t base = (int64_t)large_incid.size();
+      for (int64_t i = i0; i < i1; ++i) large_incid.push_back(b->incid_read[i]);
+      std::stable_sort(large_incid.begin() + base, large_incid.end(),
+                       [&](int32_t x, int32_t y) { return b->ref_start[x] < b->ref_start[y]; });
+      int32_t maxspan = 1;
+      for (int64_t i = base; i < (int64_t)large_incid.size(); ++i) {
+        const int32_t r = large_incid[i];
+        maxspan = std::max(maxspan, read_end[r] - b->ref_start[r]);
+      }
+      const int32_t ss = b->scope_span_start[s];
+      for (int64_t a = ss; a < (int64_t)ss + sl; a += kTile) {
+        Tile t{};
+        t.scope = s;
+        t.a = (int32_t)a;
+        t.b = (int32_t)std::min<int64_t>(a + kTile, (int64_t)ss + sl);
+        auto first = large_incid.begin() + base;
+        auto last = large_incid.end();
+        const int64_t lo_key = (int64_t)t.a - maxspan;
+        t.lo = std::lower_bound(first, last, lo_key,
+                                [&](int32_t r, int64_t key) { return (int64_t)b->ref_start[r] < key; }) -
+               large_incid.begin();
+        t.hi = std::lower_bound(first, last, (int64_t)t.b,
+                                [&](int32_t r, int64_t key) { return (int64_t)b->ref_start[r] < key; }) -
+               large_incid.begin();
+        tiles.push_back(t);
+      }
+    }
+  }
+  for (int32_t r = 0; r < b->n_reads; ++r) {
+    const int32_t ws = b->write_scope[r];
+    if (ws < 0) pt.push_back(r);
+    else if (tab_off[ws] >= 0) large_written.push_back(r);
+  }
+  int32_t max_small = 0;
+  for (auto s : small[0]) max_small = std::max(max_small, b->scope_span_len[s]);
+  for (auto s : small[1]) max_small = std::max(max_small, b->scope_span_len[s]);
+  // ---- device copies ----
+  DevBatch &D = db->B;
+#define COPY(field, src, n)                                                                       \
+  do {                                                                                            \
+    using T_ = std::remove_const_t<std::remove_pointer_t<decltype(D.field)>>;                     \
+    T_ *q_ = nullptr;                                                                             \
+    if ((rc = dev_copy(ctx, db, &q_, reinterpret_cast<const T_ *>(src), (size_t)(n)))) return bail(rc); \
+    D.field = q_;                                                                                 \
+  } while (0)
+  COPY(ref_start, b->ref_start, b->n_reads);
+  COPY(read_len, b->read_len, b->n_reads);
+  COPY(read_end, read_end.data(), b->n_reads);
+  COPY(n_cig, b->n_cig, b->n_reads);
+  COPY(write_scope, b->write_scope, b->n_reads);
+  COPY(seq_off, b->seq_off, b->n_reads);
+  COPY(cig_off, b->cig_off, b->n_reads);
+  COPY(seq, b->seq_nt16, b->seq_bytes);
+  COPY(dataset, b->dataset, b->n_reads);
+  COPY(cigar, b->cigar, b->n_cigar_ops);
+  COPY(incid_off, b->scope_incid_off, (size_t)b->n_scopes + 1);
+  COPY(incid_read, b->incid_read, b->n_incid);
+  COPY(span_start, b->scope_span_start, b->n_scopes);
+  COPY(span_len, b->scope_span_len, b->n_scopes);
+  COPY(keep_pos, b->keep_pos, b->n_scopes);
+  COPY(ref_off, b->scope_ref_off, b->n_scopes);
+  COPY(ref, b->ref_nt16, b->ref_bytes);
+  COPY(keep_code, b->keep_code, b->n_scopes);
+#undef COPY
+  for (int k = 0; k < 2; ++k) {
+    if ((rc = dev_copy(ctx, db, &db->small_list[k], small[k].data(), small[k].size()))) return bail(rc);
+    db->n_small[k] = (int32_t)small[k].size();
+  }
+  if ((rc = dev_copy(ctx, db, &db->pt_list, pt.data(), pt.size()))) return bail(rc);
+  db->n_pt = (int32_t)pt.size();
+  if ((rc = dev_copy(ctx, db, &db->tiles, tiles.data(), tiles.size()))) return bail(rc);
+  db->n_tiles = (int32_t)tiles.size();
+  if ((rc = dev_copy(ctx, db, &db->large_incid, large_incid.data(), large_incid.size()))) return bail(rc);
+  if ((rc = dev_copy(ctx, db, &db->tab_off, tab_off.data(), tab_off.size()))) return bail(rc);
+  if ((rc = dev_alloc(ctx, db, &db->tn_tab, (size_t)tn_entries))) return bail(rc);
+  db->tn_entries = tn_entries;
+  if ((rc = dev_copy(ctx, db, &db->large_written, large_written.data(), large_written.size()))) return bail(rc);
+  db->n_large_written = (int32_t)large_written.size();
+  db->n_large_scopes = (int32_t)large_scopes.size();
+  db->max_small_span = max_small;
+  if ((rc = dev_alloc(ctx, db, &db->out, (size_t)b->seq_bytes))) return bail(rc);
+  if ((rc = dev_alloc(ctx, db, &db->scope_calls, (size_t)b->n_scopes))) return bail(rc);
+  if ((rc = dev_alloc(ctx, db, &db->scope_bases, (size_t)b->n_scopes))) return bail(rc);
+  if ((rc = dev_alloc(ctx, db, &db->totals, GANON_N_TOTALS))) return bail(rc);
+  if ((rc = dev_alloc(ctx, db, &db->counters, 4))) return bail(rc);
+  if ((rc = dev_alloc(ctx, db, &db->rare_small_list, small[0].size() + small[1].size()))) return bail(rc);
+  if ((rc = dev_alloc(ctx, db, &db->rare_tile_list, tiles.size()))) return bail(rc);
+  unsigned long long st[GANON_N_TOTALS] = {0};
+  int64_t written = 0;
+  for (int32_t r = 0; r < b->n_reads; ++r) written += b->write_scope[r] >= 0;
+  st[GANON_T_READS_IN] = (unsigned long long)b->n_reads;
+  st[GANON_T_READS_WRITTEN] = (unsigned long long)written;
+  st[GANON_T_SCOPES] = (unsigned long long)b->n_scopes;
+  st[GANON_T_LARGE_TILES] = (unsigned long long)tiles.size();
+  if ((rc = dev_copy(ctx, db, &db->static_totals, st, GANON_N_TOTALS))) return bail(rc);
+  hipError_t e = hipStreamSynchronize(ctx->stream);
+  if (e != hipSuccess) {
+    fail(ctx, GANON_E_DEVICE, "upload sync failed: %s", hipGetErrorString(e));
+    return bail(GANON_E_DEVICE);
+  }
+  *out = db;
+  return GANON_OK;
+}
+
+GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
+  if (!ctx || !db) return fail(ctx, GANON_E_ARG, "null argument");
+  HIP_OR_FAIL(hipSetDevice(ctx->device));
+  for (auto &r : ctx->recs) {
+    ctx->pool.push_back(r.e0);
+    ctx->pool.push_back(r.e1);
+  }
+  ctx->recs.clear();
+  hipStream_t st = ctx->stream;
+  const DevBatch &B = db->B;
+  int rc;
+  HIP_OR_FAIL(hipMemsetAsync(db->counters, 0, 4 * sizeof(int32_t), st));
+  HIP_OR_FAIL(hipMemcpyAsync(db->totals, db->static_totals, GANON_N_TOTALS * sizeof(unsigned long long),
+                             hipMemcpyDeviceToDevice, st));
+  if (db->n_large_scopes) {
+    HIP_OR_FAIL(hipMemsetAsync(db->scope_calls, 0, (size_t)db->n_scopes * sizeof(int32_t), st));
+    HIP_OR_FAIL(hipMemsetAsync(db->scope_bases, 0, (size_t)db->n_scopes * sizeof(int32_t), st));
+  }
+  if (db->n_pt) {
+    KernelScope ks(ctx, "k_passthrough");
+    const int grid = std::min<int>((db->n_pt + kWaves - 1) / kWaves, 8192);
+    k_passthrough<<<grid, kBlock, 0, st>>>(B, db->pt_list, db->n_pt, db->out);
+    if ((rc = check_launch(ctx, "k_passthrough"))) return rc;
+  }
+  const int caps[2] = {kSmallCap0, kSmallCap1};
+  for (int k = 0; k < 2; ++k) {
+    if (!db->n_small[k]) continue;
+    KernelScope ks(ctx, k == 0 ? "k_scope_small<1>/4K" : "k_scope_small<1>/16K");
+    k_scope_small<1><<<db->n_small[k], kBlock, small_lds_bytes(1, caps[k]), st>>>(
+        B, db->small_list[k], db->n_small[k], nullptr, caps[k], db->out, db->scope_calls, db->scope_bases,
+        db->rare_small_list, db->counters + 0);
+    if ((rc = check_launch(ctx, "k_scope_small<1>"))) return rc;
+  }
+  if (db->n_tiles) {
+    KernelScope ks(ctx, "k_tile_large<1>");
+    k_tile_large<1><<<db->n_tiles, kBlock, tile_lds_bytes(1), st>>>(
+        B, db->tiles, nullptr, db->n_tiles, nullptr, db->large_incid, db->tab_off, db->tn_tab, db->scope_calls,
+        db->rare_tile_list, db->counters + 1);
+    if ((rc = check_launch(ctx, "k_tile_large<1>"))) return rc;
+  }
+  // Re-runs on the 16-code tally; list lengths stay on the device (no host sync).
+  if (db->n_small[0] + db->n_small[1]) {
+    KernelScope ks(ctx, "k_scope_small<4>/rare");
+    const int grid = std::min<int>(db->n_small[0] + db->n_small[1], kPersistGrid);
+    k_scope_small<4><<<grid, kBlock, small_lds_bytes(4, kSmallCap1), st>>>(
+        B, db->rare_small_list, 0, db->counters + 0, kSmallCap1, db->out, db->scope_calls, db->scope_bases,
+        nullptr, nullptr);
+    if ((rc = check_launch(ctx, "k_scope_small<4>"))) return rc;
+  }
+  if (db->n_tiles) {
+    KernelScope ks(ctx, "k_tile_large<4>/rare");
+    const int grid = std::min<int>(db->n_tiles, kPersistGrid);
+    k_tile_large<4><<<grid, kBlock, tile_lds_bytes(4), st>>>(
+        B, db->tiles, db->rare_tile_list, 0, db->counters + 1, db->large_incid, db->tab_off, db->tn_tab,
+        db->scope_calls, nullptr, nullptr);
+    if ((rc = check_launch(ctx, "k_tile_large<4>"))) return rc;
+  }
+  if (db->n_large_written) {
+    KernelScope ks(ctx, "k_mask_large");
+    const int grid = std::min<int>((db->n_large_written + kWaves - 1) / kWaves, 8192);
+    k_mask_large<<<grid, kBlock, 0, st>>>(B, db->large_written, db->n_large_written, db->tab_off, db->tn_tab,
+                                          db->out, db->scope_bases);
+    if ((rc = check_launch(ctx, "k_mask_large"))) return rc;
+  }
+  {
+    KernelScope ks(ctx, "k_totals");
+    const int grid = std::max(1, std::min<int>((db->n_scopes + kBlock - 1) / kBlock, 256));
+    k_totals<<<grid, kBlock, 0, st>>>(db->scope_calls, db->scope_bases, db->n_scopes, db->counters + 0,
+                                      db->counters + 1, db->totals);
+    if ((rc = check_launch(ctx, "k_totals"))) return rc;
+  }
+  db->ran = true;
+  return GANON_OK;
+}
+
+GANON_API int ganon_batch_sync(ganon_ctx *ctx) {
+  if (!ctx) return GANON_E_ARG;
+  HIP_OR_FAIL(hipStreamSynchronize(ctx->stream));
+  if (ctx->profiling) {
+    ctx->last_times.clear();
+    for (auto &r : ctx->recs) {
+      float ms = 0.f;
+      hipEventElapsedTime(&ms, r.e0, r.e1);
+      auto it = std::find_if(ctx->last_times.begin(), ctx->last_times.end(),
+                             [&](const ganon_kernel_time &t) { return r.name == t.name; });
+      if (it == ctx->last_times.end()) {
+        ganon_kernel_time t{};
+        std::snprintf(t.name, sizeof t.name, "%s", r.name.c_str());
+        t.launches = 1;
+        t.ms = ms;
+        ctx->last_times.push_back(t);
+      } else {
+        it->launches += 1;
+        it->ms += ms;
+      }
+    }
+  }
+  return GANON_OK;
+}
+
+GANON_API int ganon_last_kernel_times(ganon_ctx *ctx, ganon_kernel_time *out, int max_k) {
+  if (!ctx) return GANON_E_ARG;
+  const int n = (int)ctx->last_times.size();
+  for (int i = 0; i < n && i < max_k && out; ++i) out[i] = ctx->last_times[i];
+  return n;
+}
+
+GANON_API int ganon_batch_download(ganon_ctx *ctx, ganon_dbatch *db, uint8_t *seq_out, int32_t *scope_calls_out,
+                                   int32_t *scope_bases_out, int64_t *totals_out) {
+  if (!ctx || !db) return fail(ctx, GANON_E_ARG, "null argument");
+  if (!db->ran) return fail(ctx, GANON_E_STATE, "download before run");
+  HIP_OR_FAIL(hipSetDevice(ctx->device));
+  hipStream_t st = ctx->stream;
+  if (seq_out && db->seq_bytes)
+    HIP_OR_FAIL(hipMemcpyAsync(seq_out, db->out, (size_t)db->seq_bytes, hipMemcpyDeviceToHost, st));
+  if (scope_calls_out && db->n_scopes)
+    HIP_OR_FAIL(hipMemcpyAsync(scope_calls_out, db->scope_calls, (size_t)db->n_scopes * 4, hipMemcpyDeviceToHost, st));
+  if (scope_bases_out && db->n_scopes)
+    HIP_OR_FAIL(hipMemcpyAsync(scope_bases_out, db->scope_bases, (size_t)db->n_scopes * 4, hipMemcpyDeviceToHost, st));
+  if (totals_out)
+    HIP_OR_FAIL(hipMemcpyAsync(totals_out, db->totals, GANON_N_TOTALS * 8, hipMemcpyDeviceToHost, st));
+  HIP_OR_FAIL(hipStreamSynchronize(st));
+  return GANON_OK;
+}
+
+GANON_API int ganon_batch_free(ganon_ctx *ctx, ganon_dbatch *db) {
+  if (!db) return GANON_E_ARG;
+  if (ctx) {
+    hipSetDevice(ctx->device);
+    hipStreamSynchronize(ctx->stream);
+  }
+  free_batch(db);
+  delete db;
+  return GANON_OK;
+}
+
+GANON_API int ganon_batch_device_totals(ganon_dbatch *db, void **dev_ptr) {
+  if (!db || !dev_ptr) return GANON_E_ARG;
+  *dev_ptr = db->totals;
+  return GANON_OK;
+}
+
+GANON_API int ganon_batch_info(ganon_dbatch *db, int64_t *info) {
+  if (!db || !info) return GANON_E_ARG;
+  info[0] = db->n_small[0];
+  info[1] = db->n_small[1];
+  info[2] = db->n_large_scopes;
+  info[3] = db->n_tiles;
+  info[4] = db->n_pt;
+  info[5] = db->n_large_written;
+  info[6] = db->max_small_span;
+  info[7] = db->tn_entries;
+  return GANON_OK;
+}
+
+GANON_API int ganon_mask_batch(ganon_ctx *ctx, const ganon_batch *batch, uint8_t *seq_out, int32_t *scope_calls_out,
+                               int32_t *scope_bases_out, int64_t *totals_out) {
+  if (!ctx || !batch || (!seq_out && batch->seq_bytes)) return fail(ctx, GANON_E_ARG, "null argument");
+  ganon_dbatch *db = nullptr;
+  int rc = ganon_batch_upload(ctx, batch, &db);
+  if (rc) return rc;
+  rc = ganon_batch_run(ctx, db);
+  if (!rc) rc = ganon_batch_sync(ctx);
+  if (!rc) rc = ganon_batch_download(ctx, db, seq_out, scope_calls_out, scope_bases_out, totals_out);
+  ganon_batch_free(ctx, db);
+  return rc;
+}

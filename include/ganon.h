@@ -1,0 +1,133 @@
+/*
+ * ganon.h — C ABI of the MI355X germline-variant masking path (libganon_hip.so).
+ *
+ * Drop-in boundary for the reference's per-scope anonymizer plugin:
+ *   CompleteGermlineAnonymizer.anonymize(variant_to_keep, tumor_normal_pileup, ref_genome,
+ *                                        stats_recorder)      anonymizer_methods.py:431-535
+ * called once per scope by anonymize_window (short_read_tumor_normal_anonymizer.py:289-293).
+ * Inside one call the reference classifies every aligned base of every tumor/normal read
+ * of the scope (variation_classifier.py:144-215, SomaticVariationType state machine
+ * variants.py:33-39) and overwrites, in every supporting read, each SNV seen in >=1 tumor
+ * AND >=1 normal read with the reference base (mask_germline_variants,
+ * anonymizer_methods.py:537-556 -> mask_or_modify_base_pair :170-176), except the window's
+ * own VCF variant (:546-547). This ABI processes MANY scopes per call: the host scheduler
+ * (genomeanonymizer_amd/planner.py) lays the scopes of a contig out as one batch.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only; all coordinates are 0-based and contig-relative.
+ *  - Bases are BAM nt16 codes ("=ACMGRSVTWYHKDBN"), packed two per byte, high nibble
+ *    first, exactly as stored in a BAM record; every read starts at a byte boundary.
+ *  - CIGAR ops are BAM u32 words (len << 4 | op), op in MIDNSHP=X.
+ *  - Return value 0 on success, a negative GANON_E* code otherwise; the message is in
+ *    ganon_last_error(ctx). No C++ exception or abort crosses the ABI.
+ *  - One ctx per GPU per host thread; a ctx is not thread-safe.
+ *  - There is no CPU implementation behind this ABI: without a usable gfx950 device
+ *    ganon_ctx_create fails with GANON_E_DEVICE.
+ */
+#ifndef GANON_H
+#define GANON_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+#define GANON_API extern "C" __attribute__((visibility("default")))
+#else
+#define GANON_API __attribute__((visibility("default")))
+#endif
+
+#define GANON_ABI_VERSION 1
+
+enum {
+  GANON_OK = 0,
+  GANON_E_ARG = -1,      /* invalid argument / inconsistent batch (message says which) */
+  GANON_E_DEVICE = -2,   /* no device, wrong architecture, HIP runtime error */
+  GANON_E_NOMEM = -3,    /* device or host allocation failed */
+  GANON_E_STATE = -4     /* call out of order (e.g. download before run) */
+};
+
+/* Totals written by ganon_batch_download / ganon_mask_batch (int64 each). */
+enum {
+  GANON_T_MASKED_SNV_CALLS = 0, /* TN SNV calls masked, summed over scopes (stats #SNV) */
+  GANON_T_MASKED_BASES = 1,     /* bases overwritten in written reads                   */
+  GANON_T_READS_IN = 2,         /* reads presented to the kernels                      */
+  GANON_T_READS_WRITTEN = 3,    /* reads with write_scope >= 0                          */
+  GANON_T_SCOPES = 4,           /* scopes in the batch                                  */
+  GANON_T_RARE_SCOPES = 5,      /* scopes re-run on the 16-code tally (non-ACGTN bases) */
+  GANON_T_LARGE_TILES = 6,      /* position tiles of scopes wider than the LDS cap      */
+  GANON_N_TOTALS = 8
+};
+
+typedef struct ganon_ctx ganon_ctx;
+typedef struct ganon_dbatch ganon_dbatch;
+
+typedef struct ganon_batch {
+  int32_t n_reads;
+  int32_t n_scopes;
+  int64_t n_incid;
+  int64_t seq_bytes;              /* size of seq_nt16 (and of the output buffer)          */
+  int64_t n_cigar_ops;            /* size of cigar                                        */
+  int64_t ref_bytes;              /* size of ref_nt16                                     */
+  /* reads (BAM order) */
+  const int32_t *ref_start;       /* [n_reads] BAM pos                                    */
+  const int32_t *read_len;        /* [n_reads] l_seq                                      */
+  const int64_t *seq_off;         /* [n_reads] byte offset of the read in seq_nt16        */
+  const uint8_t *seq_nt16;        /* [seq_bytes]                                          */
+  const int64_t *cig_off;         /* [n_reads] first op of the read in cigar              */
+  const int32_t *n_cig;           /* [n_reads]                                            */
+  const uint32_t *cigar;          /* [n_cigar_ops]                                        */
+  const uint8_t *dataset;         /* [n_reads] 0 tumor, 1 normal                          */
+  const int32_t *write_scope;     /* [n_reads] scope whose tally masks this read, -1 none */
+  /* scopes: CSR over incidences (a read may belong to several scopes) */
+  const int64_t *scope_incid_off; /* [n_scopes + 1]                                       */
+  const int32_t *incid_read;      /* [n_incid]                                            */
+  const int32_t *scope_span_start;/* [n_scopes] first position covered by the scope reads */
+  const int32_t *scope_span_len;  /* [n_scopes] covered extent (max end - span_start)     */
+  const int64_t *scope_ref_off;   /* [n_scopes] nibble index of span_start in ref_nt16    */
+  const uint8_t *ref_nt16;        /* [ref_bytes] upper-cased reference, nt16, 2 per byte  */
+  const int32_t *keep_pos;        /* [n_scopes] kept SNV position, -1 none (AM:546-547)   */
+  const uint8_t *keep_code;       /* [n_scopes] nt16 code of the kept alt allele          */
+} ganon_batch;
+
+/* Context: one device, one HIP stream, device scratch. */
+GANON_API int ganon_ctx_create(int device, ganon_ctx **out);
+GANON_API int ganon_ctx_destroy(ganon_ctx *ctx);
+GANON_API const char *ganon_last_error(ganon_ctx *ctx);
+GANON_API int ganon_abi_version(void);
+/* Use an external hipStream_t (e.g. torch's current stream); NULL = the ctx's own. */
+GANON_API int ganon_ctx_set_stream(ganon_ctx *ctx, void *hip_stream);
+/* When on, ganon_batch_run records a HIP event pair around each kernel it launches. */
+GANON_API int ganon_ctx_set_profiling(ganon_ctx *ctx, int enabled);
+
+/* One-shot: upload, run, download, free (synchronous). seq_out has seq_bytes bytes;
+ * scope_calls_out / scope_bases_out ([n_scopes] each) and totals_out ([GANON_N_TOTALS])
+ * may be NULL. */
+GANON_API int ganon_mask_batch(ganon_ctx *ctx, const ganon_batch *batch, uint8_t *seq_out_nt16,
+                               int32_t *scope_calls_out, int32_t *scope_bases_out,
+                               int64_t *totals_out);
+
+/* Device-resident path (benchmarks, multi-GPU shards): the batch is copied to HBM once and
+ * its scope work lists are built at upload; ganon_batch_run only launches kernels. */
+GANON_API int ganon_batch_upload(ganon_ctx *ctx, const ganon_batch *batch, ganon_dbatch **out);
+GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db);      /* async on the stream */
+GANON_API int ganon_batch_sync(ganon_ctx *ctx);
+GANON_API int ganon_batch_download(ganon_ctx *ctx, ganon_dbatch *db, uint8_t *seq_out_nt16,
+                                   int32_t *scope_calls_out, int32_t *scope_bases_out,
+                                   int64_t *totals_out);
+GANON_API int ganon_batch_free(ganon_ctx *ctx, ganon_dbatch *db);
+/* Device pointer of the device-side totals ([GANON_N_TOTALS] int64), valid after run. */
+GANON_API int ganon_batch_device_totals(ganon_dbatch *db, void **dev_ptr);
+
+/* Kernel timing of the last profiled run: up to max_k entries of
+ * (name, launches, total milliseconds). Returns the number of distinct kernels. */
+typedef struct ganon_kernel_time {
+  char name[48];
+  int32_t launches;
+  float ms;
+} ganon_kernel_time;
+GANON_API int ganon_last_kernel_times(ganon_ctx *ctx, ganon_kernel_time *out, int max_k);
+
+/* Work-list summary of an uploaded batch: [small_scopes, wide?, large_scopes, large_tiles,
+ * passthrough_reads, large_written_reads, max_small_span, 0]. */
+GANON_API int ganon_batch_info(ganon_dbatch *db, int64_t *info8);
+
+#endif /* GANON_H */

@@ -1,0 +1,142 @@
+#!/usr/bin/env python3
+"""Run the UNMODIFIED reference GenomeAnonymizer on a synthetic scenario and store its
+outputs as golden fixtures under ``tests/golden/<scenario>/``.
+
+TEST INFRASTRUCTURE ONLY (oracle/). Runs in the build container only: it imports the
+reference from ``/root/reference/src`` at run time, supplies the missing third-party
+packages through ``oracle/stubs`` (pysam, variant_extractor) and builds a plain-Python
+``pileup_io`` module from ``pileup_io.pyx`` into a temporary directory by stripping the
+Cython type declarations (``cimport`` statements, ``cdef:`` blocks, ``cdef`` on function
+definitions). Nothing derived from the reference's source is written into the repository:
+only the inputs' digests and the reference's output files (FASTQ + statistics) are kept.
+
+Entry point exercised: ``run_short_read_tumor_normal_anonymizer``
+(short_read_tumor_normal_anonymizer.py:889-967) with ``CompleteGermlineAnonymizer``
+(anonymizer_methods.py:422-556), record_statistics=True, cpus=1, no enhanced mode —
+i.e. exactly what ``genome_anonymizer -m complete_germline --record_statistics`` runs
+(genome_anonymizer.py:57-112).
+
+usage: python oracle/run_reference.py tiny edge config1
+"""
+from __future__ import annotations
+
+import gzip
+import hashlib
+import json
+import os
+import re
+import shutil
+import sys
+import tempfile
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REFERENCE = "/root/reference"
+PYX = os.path.join(REFERENCE, "src", "GenomeAnonymizer", "pileup_io.pyx")
+
+
+def _detype_pyx(src: str) -> str:
+    """Mechanical Cython -> Python: drop cimports and cdef declaration blocks."""
+    out = []
+    lines = src.splitlines()
+    i = 0
+    while i < len(lines):
+        line = lines[i]
+        s = line.strip()
+        if s.startswith("cimport ") or (s.startswith("from ") and " cimport " in s):
+            while lines[i].rstrip().endswith("\\"):
+                i += 1
+            i += 1
+            continue
+        if s == "cdef:":
+            ind = len(line) - len(line.lstrip())
+            i += 1
+            while i < len(lines) and (not lines[i].strip() or
+                                      len(lines[i]) - len(lines[i].lstrip()) > ind):
+                i += 1
+            continue
+        line = re.sub(r"^(\s*)cdef (\w+\()", r"\1def \2", line)
+        line = line.replace("from pysam.libcalignedsegment import AlignedSegment",
+                            "from pysam import AlignedSegment")
+        out.append(line)
+        i += 1
+    return "\n".join(out) + "\n"
+
+
+def _digest_inputs(paths) -> dict:
+    d = {}
+    for key in ("ref", "vcf"):
+        with open(paths[key], "rb") as fh:
+            d[key] = hashlib.sha256(fh.read()).hexdigest()
+    for key in ("T", "N"):
+        with gzip.open(paths[key], "rb") as fh:
+            d[key] = hashlib.sha256(fh.read()).hexdigest()
+    return d
+
+
+def run_reference(scenario_name: str, golden_root: str) -> dict:
+    sys.path.insert(0, REPO)
+    from genomeanonymizer_amd.synth.generate import generate, scenario
+
+    work = tempfile.mkdtemp(prefix=f"ganon_ref_{scenario_name}_")
+    mod_dir = os.path.join(work, "_mods")
+    os.makedirs(mod_dir)
+    with open(PYX) as fh:
+        with open(os.path.join(mod_dir, "pileup_io.py"), "w") as out:
+            out.write(_detype_pyx(fh.read()))
+    for p in (REFERENCE, mod_dir, os.path.join(REPO, "oracle", "stubs")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+
+    inputs = os.path.join(work, "in")
+    paths = generate(scenario(scenario_name), inputs)
+
+    from src.GenomeAnonymizer.anonymizer_methods import CompleteGermlineAnonymizer
+    from src.GenomeAnonymizer.short_read_tumor_normal_anonymizer import (
+        name_output, run_short_read_tumor_normal_anonymizer)
+
+    t_out, n_out = name_output(paths["T"]), name_output(paths["N"])
+    cwd = os.getcwd()
+    os.chdir(work)  # the reference writes a *.mem_debug file into the CWD (SR:633)
+    t0 = time.time()
+    try:
+        run_short_read_tumor_normal_anonymizer(
+            [paths["vcf"]], [(paths["T"], paths["N"])], paths["ref"],
+            CompleteGermlineAnonymizer(), [(t_out, n_out)], True, 1, False)
+    finally:
+        os.chdir(cwd)
+    elapsed = time.time() - t0
+
+    dest = os.path.join(golden_root, scenario_name)
+    os.makedirs(dest, exist_ok=True)
+    files = {}
+    for tag, prefix in (("tumor", t_out), ("normal", n_out)):
+        for suffix in (".1.fastq", ".2.fastq", ".single_end.fastq"):
+            src = prefix + suffix
+            if os.path.exists(src):
+                name = f"{tag}{suffix}.gz"
+                with open(src, "rb") as fi, gzip.GzipFile(os.path.join(dest, name), "wb", mtime=0) as fo:
+                    shutil.copyfileobj(fi, fo)
+                with open(src, "rb") as fi:
+                    files[name] = hashlib.sha256(fi.read()).hexdigest()
+    stats = paths["N"] + ".statistics.txt"
+    shutil.copy(stats, os.path.join(dest, "normal.statistics.txt"))
+    with open(stats, "rb") as fi:
+        files["normal.statistics.txt"] = hashlib.sha256(fi.read()).hexdigest()
+    meta = {"scenario": scenario_name, "inputs_sha256": _digest_inputs(paths),
+            "outputs_sha256": files, "reference_seconds": round(elapsed, 2),
+            "generator": "genomeanonymizer_amd.synth.generate.scenario(%r)" % scenario_name,
+            "entry": "run_short_read_tumor_normal_anonymizer(..., CompleteGermlineAnonymizer(), "
+                     "record_statistics=True, cpus=1, enhance_parallelization=False)"}
+    with open(os.path.join(dest, "meta.json"), "w") as fh:
+        json.dump(meta, fh, indent=1, sort_keys=True)
+    shutil.rmtree(work, ignore_errors=True)
+    return meta
+
+
+if __name__ == "__main__":
+    root = os.path.join(REPO, "tests", "golden")
+    for name in sys.argv[1:] or ["tiny", "edge", "config1"]:
+        m = run_reference(name, root)
+        print(json.dumps({"scenario": name, "seconds": m["reference_seconds"],
+                          "files": sorted(m["outputs_sha256"])}))

@@ -1,0 +1,138 @@
+"""The anonymizer plugin, MI355X edition.
+
+Reference interface: the ``Anonymizer`` protocol selected with ``-m complete_germline``
+(anonymizer_methods.py:290-309, genome_anonymizer.py:9-13, :73) and its one
+implementation ``CompleteGermlineAnonymizer`` (anonymizer_methods.py:422-556), called once
+per scope with a merged tumor/normal pileup and yielding anonymized read pairs.
+
+Here the plugin receives the whole plan of a sample (all scopes, planner.py) and masks
+every scope in ONE device batch through the C ABI of include/ganon.h (libganon_hip.so):
+SNV tally -> TN classification -> overwrite, per scope, on the GPU. Germline indels (rare,
+variable-length edits) stay on the host (indels.py). There is no CPU masking path: a
+missing HIP library or device raises ``GanonError``.
+"""
+from __future__ import annotations
+
+import dataclasses
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+
+from . import native
+from .indels import apply_leftovers, has_indel_ops, query_sequence, scope_indels
+from .io.bam import ReadTable
+from .io.fasta import FastaRef
+from .planner import Plan, SamplePlanner
+from .variants import VariantType, kept_snv
+
+
+@dataclasses.dataclass
+class MaskResult:
+    seq_out: np.ndarray                    # masked copy of the batch's seq blob
+    seq_base: Tuple[int, int]              # byte offset of the tumor / normal blob in seq_out
+    batch_index: Dict[Tuple[int, int], int]
+    scope_snv_calls: np.ndarray            # [n_scopes] masked TN SNV calls
+    scope_masked_bases: np.ndarray         # [n_scopes]
+    scope_indel_counts: Dict[int, Dict[VariantType, int]]
+    leftovers: Dict[Tuple[int, int, int], list]   # (ds, row, scope) -> indel edits
+    totals: np.ndarray
+    arrays: dict                           # the device batch (kept for tests/bench)
+
+
+def build_batch(plan: Plan, tables: Tuple[ReadTable, ReadTable], fasta: FastaRef) -> Tuple[dict, dict]:
+    """Lay the plan's scopes out as one ganon_batch (include/ganon.h)."""
+    T, N = tables
+    packed, nib_off = fasta.packed()
+    # batch reads: every read of every scope, tumor rows then normal rows
+    in_scope = [np.zeros(T.n, bool), np.zeros(N.n, bool)]
+    for sc in plan.scopes:
+        in_scope[0][sc.t_rows] = True
+        in_scope[1][sc.n_rows] = True
+    rows = [np.nonzero(in_scope[0])[0], np.nonzero(in_scope[1])[0]]
+    bidx = [np.full(T.n, -1, np.int64), np.full(N.n, -1, np.int64)]
+    bidx[0][rows[0]] = np.arange(len(rows[0]))
+    bidx[1][rows[1]] = len(rows[0]) + np.arange(len(rows[1]))
+    n_reads = len(rows[0]) + len(rows[1])
+    seq_base = (0, len(T.seq))
+    cig_base = (0, len(T.cigar))
+    arr = {}
+    cat = lambda f, dt: np.concatenate([getattr(T, f)[rows[0]], getattr(N, f)[rows[1]]]).astype(dt)
+    arr["ref_start"] = cat("pos", np.int32)
+    arr["read_len"] = cat("l_seq", np.int32)
+    arr["seq_off"] = np.concatenate([T.seq_off[rows[0]] + seq_base[0], N.seq_off[rows[1]] + seq_base[1]]).astype(np.int64)
+    arr["seq_nt16"] = np.ascontiguousarray(np.concatenate([T.seq, N.seq]).astype(np.uint8))
+    arr["cig_off"] = np.concatenate([T.cig_off[rows[0]] + cig_base[0], N.cig_off[rows[1]] + cig_base[1]]).astype(np.int64)
+    arr["n_cig"] = cat("n_cigar", np.int32)
+    arr["cigar"] = np.ascontiguousarray(np.concatenate([T.cigar, N.cigar]).astype(np.uint32))
+    arr["dataset"] = np.concatenate([np.zeros(len(rows[0]), np.uint8), np.ones(len(rows[1]), np.uint8)])
+    ws = np.full(n_reads, -1, np.int32)
+    for ds, row, s in plan.written_instances():
+        if s >= 0:
+            ws[bidx[ds][row]] = s
+    arr["write_scope"] = ws
+    counts = np.array([len(sc.t_rows) + len(sc.n_rows) for sc in plan.scopes], np.int64)
+    arr["scope_incid_off"] = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+    arr["incid_read"] = (np.concatenate([np.concatenate([bidx[0][sc.t_rows], bidx[1][sc.n_rows]])
+                                         for sc in plan.scopes]).astype(np.int32)
+                         if plan.scopes else np.zeros(0, np.int32))
+    arr["scope_span_start"] = np.array([sc.span_start for sc in plan.scopes], np.int32)
+    arr["scope_span_len"] = np.array([sc.span_end - sc.span_start for sc in plan.scopes], np.int32)
+    arr["scope_ref_off"] = np.array([nib_off[sc.contig] + sc.span_start for sc in plan.scopes], np.int64)
+    arr["ref_nt16"] = np.ascontiguousarray(packed)
+    keep = [kept_snv(sc.keep) if sc.is_variant_window else (-1, 0) for sc in plan.scopes]
+    arr["keep_pos"] = np.array([k[0] for k in keep], np.int32)
+    arr["keep_code"] = np.array([k[1] for k in keep], np.uint8)
+    meta = {"bidx": bidx, "seq_base": seq_base}
+    return arr, meta
+
+
+class CompleteGermlineAnonymizer:
+    """Masks every germline (tumor AND normal) SNV of every scope on the GPU; keeps the
+    window's own variant; defers indels to the host path like the reference does
+    (left-overs applied when a pair is yielded)."""
+
+    name = "complete_germline"
+
+    def __init__(self, device: int = 0, engine=None):
+        self.device = device
+        self._engine = engine
+
+    @property
+    def engine(self):
+        if self._engine is None:
+            self._engine = native.HipMasker(self.device)
+        return self._engine
+
+    def anonymize(self, planner: SamplePlanner, plan: Plan) -> MaskResult:
+        tables = planner.tables
+        fasta = planner.fasta
+        arrays, meta = build_batch(plan, tables, fasta)
+        out, calls, bases, totals = self.engine.mask(arrays)
+        # host indel path, only for scopes that contain a read with an I/D op
+        written = {}
+        for ds, row, s in plan.written_instances():
+            if s >= 0:
+                written[(ds, row)] = s
+        indel_counts: Dict[int, Dict[VariantType, int]] = {}
+        leftovers: Dict[Tuple[int, int, int], list] = {}
+        for sc in plan.scopes:
+            if not any(has_indel_ops(tables[0], r) for r in sc.t_rows.tolist()) and \
+                    not any(has_indel_ops(tables[1], r) for r in sc.n_rows.tolist()):
+                continue
+            reg = planner.registration_order(sc)
+            N = tables[1]
+            ns, ne = N.pos[sc.n_rows], N.end[sc.n_rows]
+
+            def cover(p, ns=ns, ne=ne):
+                return bool(np.any((ns <= p) & (ne > p)))
+
+            keep = sc.keep if sc.is_variant_window else None
+            counts, left = scope_indels(sc.contig, reg, tables, fasta, cover, keep)
+            indel_counts[sc.id] = counts
+            for key, edits in left.items():
+                if written.get(key) == sc.id:
+                    leftovers[(key[0], key[1], sc.id)] = edits
+        return MaskResult(out, meta["seq_base"], {}, calls, bases, indel_counts, leftovers, totals, arrays)
+
+
+ANONYMIZER_ALGORITHMS = {CompleteGermlineAnonymizer.name: CompleteGermlineAnonymizer}

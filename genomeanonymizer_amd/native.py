@@ -1,0 +1,273 @@
+"""ctypes bindings of the two in-tree native libraries.
+
+* ``libganon_hip.so`` (include/ganon.h): the HIP masking kernels. There is no CPU
+  implementation behind it; loading or creating a context fails loudly without a gfx950
+  device (``GanonError``), never falls back.
+* ``libganon_host.so`` (include/ganon_host.h): BAM decoder and FASTQ formatter.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Optional
+
+import numpy as np
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+HIP_LIB_PATH = os.path.join(_PKG, "libganon_hip.so")
+HOST_LIB_PATH = os.path.join(_PKG, "libganon_host.so")
+
+GANON_N_TOTALS = 8
+TOTAL_NAMES = ("masked_snv_calls", "masked_bases", "reads_in", "reads_written", "scopes",
+               "rare_scopes", "large_tiles", "reserved")
+
+
+class GanonError(RuntimeError):
+    pass
+
+
+_p = C.c_void_p
+_i32p = C.POINTER(C.c_int32)
+_i64p = C.POINTER(C.c_int64)
+_u8p = C.POINTER(C.c_uint8)
+_u32p = C.POINTER(C.c_uint32)
+
+
+class GanonBatch(C.Structure):
+    """Mirror of ``ganon_batch`` (include/ganon.h)."""
+    _fields_ = [
+        ("n_reads", C.c_int32), ("n_scopes", C.c_int32), ("n_incid", C.c_int64),
+        ("seq_bytes", C.c_int64), ("n_cigar_ops", C.c_int64), ("ref_bytes", C.c_int64),
+        ("ref_start", _i32p), ("read_len", _i32p), ("seq_off", _i64p), ("seq_nt16", _u8p),
+        ("cig_off", _i64p), ("n_cig", _i32p), ("cigar", _u32p), ("dataset", _u8p),
+        ("write_scope", _i32p),
+        ("scope_incid_off", _i64p), ("incid_read", _i32p), ("scope_span_start", _i32p),
+        ("scope_span_len", _i32p), ("scope_ref_off", _i64p), ("ref_nt16", _u8p),
+        ("keep_pos", _i32p), ("keep_code", _u8p),
+    ]
+
+
+class KernelTime(C.Structure):
+    _fields_ = [("name", C.c_char * 48), ("launches", C.c_int32), ("ms", C.c_float)]
+
+
+# numpy field spec of a batch: name -> dtype
+BATCH_ARRAYS = {
+    "ref_start": np.int32, "read_len": np.int32, "seq_off": np.int64, "seq_nt16": np.uint8,
+    "cig_off": np.int64, "n_cig": np.int32, "cigar": np.uint32, "dataset": np.uint8,
+    "write_scope": np.int32, "scope_incid_off": np.int64, "incid_read": np.int32,
+    "scope_span_start": np.int32, "scope_span_len": np.int32, "scope_ref_off": np.int64,
+    "ref_nt16": np.uint8, "keep_pos": np.int32, "keep_code": np.uint8,
+}
+
+
+_PTR_OF = {np.int32: _i32p, np.int64: _i64p, np.uint8: _u8p, np.uint32: _u32p}
+
+
+def make_c_batch(arrays: dict) -> GanonBatch:
+    """Build a GanonBatch over numpy arrays (kept alive by the caller's dict)."""
+    b = GanonBatch()
+    for name, dt in BATCH_ARRAYS.items():
+        a = arrays[name]
+        if a.dtype != dt or not a.flags["C_CONTIGUOUS"]:
+            raise GanonError(f"batch array {name} must be C-contiguous {np.dtype(dt)}")
+        setattr(b, name, a.ctypes.data_as(_PTR_OF[dt]))
+    b.n_reads = len(arrays["read_len"])
+    b.n_scopes = len(arrays["scope_span_len"])
+    b.n_incid = len(arrays["incid_read"])
+    b.seq_bytes = len(arrays["seq_nt16"])
+    b.n_cigar_ops = len(arrays["cigar"])
+    b.ref_bytes = len(arrays["ref_nt16"])
+    return b
+
+
+_hip = None
+_host = None
+
+
+def hip_lib():
+    """Load libganon_hip.so (raises GanonError if it is missing)."""
+    global _hip
+    if _hip is not None:
+        return _hip
+    if not os.path.exists(HIP_LIB_PATH):
+        raise GanonError(f"{HIP_LIB_PATH} is missing: run __graft_entry__.build() (hipcc, gfx950)")
+    lib = C.CDLL(HIP_LIB_PATH)
+    lib.ganon_abi_version.restype = C.c_int
+    lib.ganon_ctx_create.argtypes = [C.c_int, C.POINTER(_p)]
+    lib.ganon_ctx_destroy.argtypes = [_p]
+    lib.ganon_last_error.argtypes = [_p]
+    lib.ganon_last_error.restype = C.c_char_p
+    lib.ganon_ctx_set_stream.argtypes = [_p, _p]
+    lib.ganon_ctx_set_profiling.argtypes = [_p, C.c_int]
+    lib.ganon_mask_batch.argtypes = [_p, C.POINTER(GanonBatch), _u8p, _i32p, _i32p, _i64p]
+    lib.ganon_batch_upload.argtypes = [_p, C.POINTER(GanonBatch), C.POINTER(_p)]
+    lib.ganon_batch_run.argtypes = [_p, _p]
+    lib.ganon_batch_sync.argtypes = [_p]
+    lib.ganon_batch_download.argtypes = [_p, _p, _u8p, _i32p, _i32p, _i64p]
+    lib.ganon_batch_free.argtypes = [_p, _p]
+    lib.ganon_batch_device_totals.argtypes = [_p, C.POINTER(_p)]
+    lib.ganon_last_kernel_times.argtypes = [_p, C.POINTER(KernelTime), C.c_int]
+    lib.ganon_batch_info.argtypes = [_p, _i64p]
+    if lib.ganon_abi_version() != 1:
+        raise GanonError("libganon_hip.so ABI version mismatch")
+    _hip = lib
+    return lib
+
+
+EXPORTED_HIP_SYMBOLS = (
+    "ganon_ctx_create", "ganon_ctx_destroy", "ganon_last_error", "ganon_abi_version",
+    "ganon_ctx_set_stream", "ganon_ctx_set_profiling", "ganon_mask_batch", "ganon_batch_upload",
+    "ganon_batch_run", "ganon_batch_sync", "ganon_batch_download", "ganon_batch_free",
+    "ganon_batch_device_totals", "ganon_last_kernel_times", "ganon_batch_info",
+)
+EXPORTED_HOST_SYMBOLS = (
+    "ganon_bam_open", "ganon_bam_view_get", "ganon_bam_error", "ganon_bam_close",
+    "ganon_host_last_error", "ganon_fastq_format", "ganon_pack_nt16",
+)
+
+
+def _ptr(a: np.ndarray, ty):
+    return a.ctypes.data_as(ty) if a is not None else None
+
+
+class HipMasker:
+    """One device context (one GPU, one HIP stream) of libganon_hip.so."""
+
+    def __init__(self, device: int = 0):
+        lib = hip_lib()
+        self._lib = lib
+        h = _p()
+        rc = lib.ganon_ctx_create(int(device), C.byref(h))
+        if rc != 0:
+            raise GanonError(f"ganon_ctx_create(device={device}) failed with {rc}: "
+                             "no usable gfx950 device (there is no CPU fallback)")
+        self._h = h
+        self.device = device
+
+    def _check(self, rc: int, what: str) -> None:
+        if rc != 0:
+            msg = self._lib.ganon_last_error(self._h).decode(errors="replace")
+            raise GanonError(f"{what} failed ({rc}): {msg}")
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._lib.ganon_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, hip_stream_ptr: Optional[int]) -> None:
+        self._check(self._lib.ganon_ctx_set_stream(self._h, _p(hip_stream_ptr or 0)), "set_stream")
+
+    def set_profiling(self, on: bool) -> None:
+        self._check(self._lib.ganon_ctx_set_profiling(self._h, 1 if on else 0), "set_profiling")
+
+    def mask(self, arrays: dict):
+        """Synchronous one-shot: returns (seq_out, scope_calls, scope_bases, totals)."""
+        b = make_c_batch(arrays)
+        out = np.empty(b.seq_bytes, np.uint8)
+        calls = np.zeros(b.n_scopes, np.int32)
+        bases = np.zeros(b.n_scopes, np.int32)
+        tot = np.zeros(GANON_N_TOTALS, np.int64)
+        self._check(self._lib.ganon_mask_batch(self._h, C.byref(b), _ptr(out, _u8p), _ptr(calls, _i32p),
+                                               _ptr(bases, _i32p), _ptr(tot, _i64p)), "ganon_mask_batch")
+        return out, calls, bases, tot
+
+    # -- device-resident path ------------------------------------------------------------
+    def upload(self, arrays: dict) -> "DeviceBatch":
+        b = make_c_batch(arrays)
+        h = _p()
+        self._check(self._lib.ganon_batch_upload(self._h, C.byref(b), C.byref(h)), "ganon_batch_upload")
+        return DeviceBatch(self, h, b.seq_bytes, b.n_scopes)
+
+
+class DeviceBatch:
+    def __init__(self, masker: HipMasker, handle, seq_bytes: int, n_scopes: int):
+        self.m = masker
+        self.h = handle
+        self.seq_bytes = seq_bytes
+        self.n_scopes = n_scopes
+
+    def run(self) -> None:
+        self.m._check(self.m._lib.ganon_batch_run(self.m._h, self.h), "ganon_batch_run")
+
+    def sync(self) -> None:
+        self.m._check(self.m._lib.ganon_batch_sync(self.m._h), "ganon_batch_sync")
+
+    def download(self):
+        out = np.empty(self.seq_bytes, np.uint8)
+        calls = np.zeros(self.n_scopes, np.int32)
+        bases = np.zeros(self.n_scopes, np.int32)
+        tot = np.zeros(GANON_N_TOTALS, np.int64)
+        self.m._check(self.m._lib.ganon_batch_download(self.m._h, self.h, _ptr(out, _u8p), _ptr(calls, _i32p),
+                                                       _ptr(bases, _i32p), _ptr(tot, _i64p)), "download")
+        return out, calls, bases, tot
+
+    def totals(self) -> np.ndarray:
+        tot = np.zeros(GANON_N_TOTALS, np.int64)
+        self.m._check(self.m._lib.ganon_batch_download(self.m._h, self.h, None, None, None, _ptr(tot, _i64p)),
+                      "download totals")
+        return tot
+
+    def device_totals_ptr(self) -> int:
+        p = _p()
+        self.m._check(self.m._lib.ganon_batch_device_totals(self.h, C.byref(p)), "device_totals")
+        return p.value
+
+    def info(self) -> dict:
+        a = np.zeros(8, np.int64)
+        self.m._check(self.m._lib.ganon_batch_info(self.h, _ptr(a, _i64p)), "batch_info")
+        keys = ("small4k_scopes", "small16k_scopes", "large_scopes", "large_tiles", "passthrough_reads",
+                "large_written_reads", "max_small_span", "tn_table_entries")
+        return dict(zip(keys, a.tolist()))
+
+    def kernel_times(self) -> list:
+        arr = (KernelTime * 32)()
+        n = self.m._lib.ganon_last_kernel_times(self.m._h, arr, 32)
+        return [(arr[i].name.decode(), int(arr[i].launches), float(arr[i].ms)) for i in range(min(n, 32))]
+
+    def free(self) -> None:
+        if self.h:
+            self.m._lib.ganon_batch_free(self.m._h, self.h)
+            self.h = None
+
+
+# ---- host library ---------------------------------------------------------------------
+
+class BamView(C.Structure):
+    _fields_ = [
+        ("n_records", C.c_int64), ("n_ref", C.c_int32), ("ref_names", _p),
+        ("ref_name_off", _i64p), ("ref_len", _i64p),
+        ("tid", _i32p), ("pos", _i32p), ("end", _i32p), ("flag", _i32p), ("mapq", _i32p),
+        ("l_seq", _i32p), ("n_cigar", _i32p), ("mate_tid", _i32p), ("mate_pos", _i32p), ("tlen", _i32p),
+        ("name_off", _i64p), ("name_len", _i32p), ("cig_off", _i64p), ("seq_off", _i64p),
+        ("qual_off", _i64p), ("aux_off", _i64p), ("aux_len", _i32p),
+        ("names", _p), ("names_bytes", C.c_int64), ("cigar", _u32p), ("cigar_ops", C.c_int64),
+        ("seq", _u8p), ("seq_bytes", C.c_int64), ("qual", _u8p), ("qual_bytes", C.c_int64),
+        ("aux", _u8p), ("aux_bytes", C.c_int64),
+    ]
+
+
+def host_lib():
+    global _host
+    if _host is not None:
+        return _host
+    if not os.path.exists(HOST_LIB_PATH):
+        raise GanonError(f"{HOST_LIB_PATH} is missing: run __graft_entry__.build()")
+    lib = C.CDLL(HOST_LIB_PATH)
+    lib.ganon_bam_open.argtypes = [C.c_char_p, C.c_int, C.POINTER(_p)]
+    lib.ganon_bam_view_get.argtypes = [_p, C.POINTER(BamView)]
+    lib.ganon_bam_close.argtypes = [_p]
+    lib.ganon_host_last_error.restype = C.c_char_p
+    lib.ganon_fastq_format.restype = C.c_int64
+    lib.ganon_fastq_format.argtypes = [C.c_int64, C.POINTER(_u8p), _u8p, _i64p, _i32p, _u8p, C.POINTER(_u8p),
+                                       _u8p, _i64p, _i32p, _u8p, C.c_char_p, _i64p, _i32p, _u8p, C.c_char_p,
+                                       C.c_int64]
+    lib.ganon_pack_nt16.argtypes = [C.c_char_p, C.c_int64, _u8p]
+    _host = lib
+    return lib

@@ -1,0 +1,512 @@
+"""Host scope scheduler: which reads meet in which scope, and which scope's masked copy of
+each read is written where, in the reference's exact output order.
+
+Restates (without masking anything) the control flow of
+``anonymize_genome`` (short_read_tumor_normal_anonymizer.py:625-760) for one tumor/normal
+pair:
+
+* windows and sections: ``get_windows`` (SR:71-131), ``get_genome_sections`` (SR:245-276);
+* variant windows: ``anonymize_window`` (SR:279-372) over a pileup of [first, last)
+  (pileup_io.pyx:8-41, htslib ``nofilter`` stepper, ``truncate=False``);
+* inter-window gaps: ``anonymize_inter_window_region`` (SR:498-558) driven by
+  ``iter_fetch_pair`` (pileup_io.pyx:124-298) with its cluster rules;
+* the yield order of ``CompleteGermlineAnonymizer.anonymize`` (anonymizer_methods.py:
+  472-532) computed from coordinates: a complete pair is yielded at the first
+  normal column beyond its rightmost end, pairs at one column in first-appearance order,
+  leftovers at scope end in first-appearance order;
+* pairing and de-duplication: ``write_pair``/``written_read_ids`` (SR:134-165),
+  ``to_pair_anonymized_reads`` with first-object-wins (AM:320-389),
+  ``pair_unmapped_or_non_pileup_pairs_and_write`` (SR:375-406), ``pair_unmapped_mates``
+  (SR:561-600) and ``write_single_end_reads`` (SR:603-622);
+* statistics bookkeeping (SR:175-242): the window rows and which scope counts into which.
+
+The masking itself (the hot path) happens later, in one device batch over all scopes
+(genomeanonymizer_amd/anonymizer_methods.py -> include/ganon.h). An output record is an
+``Instance`` = (dataset, read row, scope): the read as masked by that scope's tally, or
+unmasked when scope == -1 (reads written from a fetch pass-through).
+"""
+from __future__ import annotations
+
+import dataclasses
+from typing import Dict, Iterator, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from .io.bam import FLAG_SECONDARY, FLAG_SUPPLEMENTARY, ReadTable
+from .io.fasta import FastaRef
+from .variants import VariantRecord, VariantType, WindowVariant
+
+DATASET_TUMORAL = 0
+DATASET_NORMAL = 1
+WINDOW_SIZE = 2000
+LONG_SV = 100_000
+
+Instance = Tuple[int, int, int]  # (dataset, row, scope id or -1)
+
+
+class UnsupportedInput(NotImplementedError):
+    """Input the reference handles through code paths this build does not restate yet."""
+
+
+@dataclasses.dataclass
+class Window:
+    """SR:35-52."""
+    sequence: str
+    first: int
+    last: int
+    variant: Optional[WindowVariant] = None
+
+    def is_variant_window(self) -> bool:
+        return self.variant is not None
+
+    def __str__(self) -> str:
+        if self.variant is None:
+            return ",".join(map(str, (self.sequence, self.first, self.last)))
+        return ",".join(map(str, (self.sequence, self.first, self.last, self.variant)))
+
+
+def get_windows(records: Sequence[VariantRecord], ref_index: Dict[str, int],
+                window_size: int = WINDOW_SIZE) -> List[Window]:
+    """One window (two for INV/TRA/long SVs) of +-window_size/2 around each record (SR:71-131)."""
+    half = int(window_size / 2)
+    windows: List[Window] = []
+    for r in records:
+        called = WindowVariant.from_record(r)
+        end = r.end
+        end_chrom = r.contig
+        if r.alt_sv_breakend:
+            end_chrom = r.alt_sv_breakend[0]
+            if r.contig != end_chrom:
+                end = r.alt_sv_breakend[1]
+        vt = r.variant_type
+        if vt is VariantType.INV:
+            if r.pos + half > r.end - half:
+                windows.append(Window(r.contig, r.pos - half, r.end + half + 1, called))
+            else:
+                windows.append(Window(r.contig, r.pos - half, r.pos + half + 1, called))
+                windows.append(Window(r.contig, r.end - half, r.end + half + 1, called))
+        elif vt is VariantType.TRA:
+            windows.append(Window(r.contig, r.pos - half, r.pos + half + 1, called))
+            windows.append(Window(end_chrom, end - half, end + half + 1, called))
+        elif vt is VariantType.SNV:
+            windows.append(Window(r.contig, r.pos - half, r.pos + half + 1, called))
+        else:
+            if r.length < LONG_SV:
+                windows.append(Window(r.contig, r.pos - half, r.end + half + 1, called))
+            else:
+                windows.append(Window(r.contig, r.pos - half, r.pos + half + 1, called))
+                windows.append(Window(end_chrom, end - half, end + half + 1, called))
+    for w in windows:
+        if w.sequence not in ref_index:
+            raise ValueError(f"variant contig {w.sequence!r} is not in the reference FASTA")
+    windows.sort(key=lambda w: (ref_index[w.sequence], w.first, w.last))
+    return windows
+
+
+def get_genome_sections(windows: Sequence[Window], fasta: FastaRef) -> List[Window]:
+    """Alternating inter-window gaps and windows per contig; whole contigs without windows
+    become Window(seq, 0, 0) (SR:245-276)."""
+    sections: List[Window] = []
+    by_seq: Dict[str, List[Window]] = {k: [] for k in fasta.references}
+    for w in windows:
+        by_seq[w.sequence].append(w)
+    for seq, length in zip(fasta.references, fasta.lengths):
+        ws = by_seq[seq]
+        if not ws:
+            sections.append(Window(seq, 0, 0))
+            continue
+        first = 1
+        for w in ws:
+            sections.append(Window(seq, first, w.first - 1))
+            first = w.last + 1
+            sections.append(w)
+        sections.append(Window(seq, first, length - 1))
+    idx = fasta.index
+    sections.sort(key=lambda w: (idx[w.sequence], w.first, w.last))
+    return sections
+
+
+@dataclasses.dataclass
+class Scope:
+    """One pileup scope = one CompleteGermlineAnonymizer.anonymize call."""
+    id: int
+    contig: str
+    tid_t: int
+    tid_n: int
+    first: int
+    last: int
+    t_rows: np.ndarray        # mapped tumor reads of the pileup, file order
+    n_rows: np.ndarray        # mapped normal reads of the pileup, file order
+    keep: Optional[WindowVariant]
+    is_variant_window: bool
+    span_start: int = 0
+    span_end: int = 0
+
+
+@dataclasses.dataclass
+class Plan:
+    scopes: List[Scope]
+    io_log: List[tuple]            # ('open', hid) | ('write', hid, dataset, slot, Instance) | ('close', hid)
+    single_end: Dict[int, List[Instance]]               # dataset -> records
+    stats_events: List[Tuple[str, object]]              # ('window', key) | ('scope', id) | ('outside', None)
+    write_single_end: bool
+
+    @property
+    def streams(self) -> Dict[Tuple[int, int], List[Instance]]:
+        """Records per (dataset, mate slot) in the order write_pair is called."""
+        out: Dict[Tuple[int, int], List[Instance]] = {(d, s): [] for d in (0, 1) for s in (0, 1)}
+        for ev in self.io_log:
+            if ev[0] == "write":
+                out[(ev[2], ev[3])].append(ev[4])
+        return out
+
+    def written_instances(self):
+        for ev in self.io_log:
+            if ev[0] == "write":
+                yield ev[4]
+        for recs in self.single_end.values():
+            yield from recs
+
+
+class SamplePlanner:
+    """Plans one tumor/normal pair. Reads are referred to by (dataset, row)."""
+
+    def __init__(self, tumor: ReadTable, normal: ReadTable, fasta: FastaRef, windows: Sequence[Window]):
+        self.tables = (tumor, normal)
+        self.fasta = fasta
+        self.windows = list(windows)
+        self.scopes: List[Scope] = []
+        self.to_pair: Dict[str, List[Optional[Instance]]] = {}
+        self.written: set = set()
+        self.io_log: List[tuple] = []
+        self._next_hid = 0
+        self.stats_events: List[Tuple[str, object]] = []
+        self._check_supported()
+
+    # ---- input checks --------------------------------------------------------------------
+    def _check_supported(self) -> None:
+        for ds, t in enumerate(self.tables):
+            if np.any(t.flag & (FLAG_SECONDARY | FLAG_SUPPLEMENTARY)):
+                raise UnsupportedInput("secondary/supplementary alignments are not supported yet "
+                                       "(reference: AnonymizedRead supplementary bookkeeping, AM:98-137)")
+            if b"SAZ" in t.aux.tobytes():
+                rows = [i for i in range(t.n) if t.has_tag(i, b"SA")]
+                if rows:
+                    raise UnsupportedInput("reads with an SA tag are not supported yet (AM:100-108)")
+        tn = set(self.tables[0].names) & set(self.tables[1].names)
+        if tn:
+            raise ValueError(f"{len(tn)} read names occur in both the tumor and the normal BAM; the "
+                             "reference keys reads by name only and mixes such reads (SURVEY Q10)")
+
+    # ---- read helpers ----------------------------------------------------------------------
+    def name(self, ds: int, row: int) -> str:
+        return self.tables[ds].names[row]
+
+    def slot(self, ds: int, row: int) -> int:
+        s = int(self.tables[ds].mate_idx[row])
+        if s < 0:
+            # list[None] in the reference (AM:119-123)
+            raise TypeError(f"read {self.name(ds, row)!r} has neither the READ1 nor the READ2 flag; "
+                            "the reference cannot store it (SURVEY Q8)")
+        return s
+
+    def _ref_end(self, ds: int, row: int) -> Optional[int]:
+        t = self.tables[ds]
+        if t.is_unmapped[row] or t.n_cigar[row] == 0:
+            return None
+        return int(t.end[row])
+
+    # ---- pairing / writing (SR:134-165, AM:320-389, SR:375-406) ----------------------------
+    # Each reference function that writes opens its own four append-mode handles and closes
+    # them when it returns (SR:297-299/366, SR:516-518/558, SR:564-566/600); with Python's
+    # buffered text I/O the records of nested handles land in the files in flush order, so
+    # the opens, writes and closes are logged and replayed by writer.py.
+    def _open(self) -> int:
+        hid = self._next_hid
+        self._next_hid += 1
+        self.io_log.append(("open", hid))
+        return hid
+
+    def _close(self, hid: int) -> None:
+        self.io_log.append(("close", hid))
+
+    def write_pair(self, i0: Instance, i1: Instance, hid: int) -> None:
+        name = self.name(i0[0], i0[1])
+        if name in self.written:
+            return
+        self.written.add(name)
+        ds = i0[0]
+        self.io_log.append(("write", hid, ds, 0, i0))
+        self.io_log.append(("write", hid, ds, 1, i1))
+
+    def _store_first(self, inst: Instance) -> List[Optional[Instance]]:
+        name = self.name(inst[0], inst[1])
+        slot = self.slot(inst[0], inst[1])
+        pair = self.to_pair.get(name)
+        if pair is None:
+            pair = [None, None]
+            self.to_pair[name] = pair
+        if pair[slot] is None:
+            pair[slot] = inst
+        return pair
+
+    def passthrough(self, ds: int, row: int, hid: int) -> None:
+        """pair_unmapped_or_non_pileup_pairs_and_write: unmasked instance, first stored wins,
+        write when both mates are known (never popped from to_pair)."""
+        t = self.tables[ds]
+        if t.l_seq[row] == 0:
+            raise TypeError(f"read {t.names[row]!r} has no SEQ; the reference cannot upper-case it")
+        pair = self._store_first((ds, row, -1))
+        if pair[0] is not None and pair[1] is not None:
+            self.write_pair(pair[0], pair[1], hid)
+
+    # ---- scopes ------------------------------------------------------------------------------
+    def _pileup_reads(self, ds: int, contig: str, first: int, last: int) -> np.ndarray:
+        t = self.tables[ds]
+        rows = t.fetch(contig, first, last)
+        rows = rows[~t.is_unmapped[rows]]
+        if len(rows) and np.any(t.n_cigar[rows] == 0):
+            raise TypeError("mapped read without CIGAR in a pileup (reference_end is None)")
+        return rows
+
+    def new_scope(self, contig: str, first: int, last: int, keep: Optional[WindowVariant],
+                  is_variant_window: bool) -> Scope:
+        t_rows = self._pileup_reads(0, contig, first, last)
+        n_rows = self._pileup_reads(1, contig, first, last)
+        sc = Scope(len(self.scopes), contig, self.tables[0].tid_of(contig), self.tables[1].tid_of(contig),
+                   first, last, t_rows, n_rows, keep, is_variant_window)
+        starts, ends = [], []
+        for ds, rows in ((0, t_rows), (1, n_rows)):
+            if len(rows):
+                starts.append(int(self.tables[ds].pos[rows].min()))
+                ends.append(int(self.tables[ds].end[rows].max()))
+        sc.span_start = min(starts) if starts else 0
+        sc.span_end = max(ends) if ends else 0
+        self.scopes.append(sc)
+        self.stats_events.append(("scope", sc.id))
+        return sc
+
+    def registration_order(self, sc: Scope) -> List[Tuple[int, int]]:
+        """(dataset, row) in the order the reference first meets each read: pileup columns by
+        position, the tumor column before the normal one, reads in file order."""
+        T, N = self.tables
+        pos = np.concatenate([T.pos[sc.t_rows], N.pos[sc.n_rows]]).astype(np.int64)
+        ds = np.concatenate([np.zeros(len(sc.t_rows), np.int64), np.ones(len(sc.n_rows), np.int64)])
+        fo = np.concatenate([np.arange(len(sc.t_rows)), np.arange(len(sc.n_rows))])
+        rows = np.concatenate([sc.t_rows, sc.n_rows]).astype(np.int64)
+        order = np.lexsort((fo, ds, pos))
+        return list(zip(ds[order].tolist(), rows[order].tolist()))
+
+    def yield_sequence(self, sc: Scope) -> List[List[Optional[Instance]]]:
+        """Pairs in the order CompleteGermlineAnonymizer.anonymize yields them (AM:472-532)."""
+        reg = self.registration_order(sc)
+        pairs: Dict[str, List[Optional[Instance]]] = {}
+        max_end: Dict[str, int] = {}
+        for ds, row in reg:
+            name = self.name(ds, row)
+            slot = self.slot(ds, row)
+            p = pairs.get(name)
+            if p is None:
+                p = [None, None]
+                pairs[name] = p
+                max_end[name] = int(self.tables[ds].end[row])
+            else:
+                max_end[name] = max(max_end[name], int(self.tables[ds].end[row]))
+            if p[slot] is not None:
+                raise UnsupportedInput(f"two alignments of {name!r} with the same mate flag in one scope")
+            p[slot] = (ds, row, sc.id)
+        # normal columns: union of the normal reads' [pos, end)
+        N = self.tables[1]
+        if len(sc.n_rows):
+            s = N.pos[sc.n_rows].astype(np.int64)
+            e = N.end[sc.n_rows].astype(np.int64)
+            o = np.argsort(s, kind="stable")
+            s, e = s[o], e[o]
+            run_end = np.maximum.accumulate(e)
+            brk = np.nonzero(s[1:] > run_end[:-1])[0] + 1
+            m_start = s[np.concatenate([[0], brk])]
+            m_end = run_end[np.concatenate([brk - 1, [len(s) - 1]])]
+        else:
+            m_start = m_end = np.zeros(0, np.int64)
+        scan, rest = [], []
+        for rank, (name, p) in enumerate(pairs.items()):
+            if p[0] is not None and p[1] is not None:
+                x = max_end[name] + 1                      # first column with right_most_end < pos
+                k = int(np.searchsorted(m_end, x, side="right"))
+                if k < len(m_end):
+                    scan.append((max(x, int(m_start[k])), rank, p))
+                    continue
+            rest.append(p)
+        scan.sort(key=lambda t: (t[0], t[1]))
+        return [t[2] for t in scan] + rest
+
+    def anonymize_window(self, contig: str, first: int, last: int, keep: Optional[WindowVariant],
+                         is_variant_window: bool) -> None:
+        """SR:279-372 with the yielded pairs consumed as SR:304-361 does."""
+        sc = self.new_scope(contig, first, last, keep, is_variant_window)
+        hid = self._open()
+        for p0, p1 in self.yield_sequence(sc):
+            if p0 is not None and p1 is not None:
+                self.write_pair(p0, p1, hid)
+                continue
+            name = None
+            for inst in (p0, p1):
+                if inst is not None:
+                    self._store_first(inst)
+                    name = self.name(inst[0], inst[1])
+            upd = self.to_pair[name]
+            if upd[0] is not None and upd[1] is not None:
+                self.write_pair(upd[0], upd[1], hid)
+                del self.to_pair[name]
+        self._close(hid)
+
+    # ---- inter-window clustering (pileup_io.pyx:124-298) --------------------------------------
+    def iter_fetch_pair(self, contig: str, first: Optional[int], last: Optional[int]) -> Iterator[tuple]:
+        T, N = self.tables
+        it = [iter(T.fetch(contig, first, last).tolist()), iter(N.fetch(contig, first, last).tolist())]
+        tabs = (T, N)
+
+        def mapped(ds, r):
+            return not tabs[ds].is_unmapped[r]
+
+        def end_of(ds, r):
+            return self._ref_end(ds, r)
+
+        def cmp_reads(ds, a, b):
+            ta = tabs[ds]
+            fa, fb = int(ta.pos[a]), int(ta.pos[b])
+            la = end_of(ds, a) if mapped(ds, a) else fa
+            lb = end_of(ds, b) if mapped(ds, b) else fb
+            from .variants import compare
+            return compare(int(ta.tid[a]), fa, la, int(ta.tid[b]), fb, lb)
+
+        def collect(ds, arr, unmapped):
+            while True:
+                nxt = next(it[ds], None)
+                if nxt is None:
+                    return None
+                if not mapped(ds, nxt):
+                    unmapped.append(nxt)
+                    continue
+                if not (-1 <= cmp_reads(ds, arr[-1], nxt) <= 1):
+                    return nxt
+                arr.append(nxt)
+
+        def rightmost(ds, arr, prev):
+            right = 0 if prev is None else prev
+            for r in arr:
+                if mapped(ds, r):
+                    e = end_of(ds, r)
+                    if e is None:
+                        raise TypeError("mapped read without reference_end")
+                    right = max(right, e)
+            return right
+
+        from .variants import compare
+        arrs = [[], []]
+        unm = [[], []]
+        cur = [next(it[0], None), next(it[1], None)]
+        yielded = [True, True]
+        seqi = [None, None]
+        left = [None, None]
+        right = [None, None]
+        if cur[0] is None and cur[1] is None:
+            return
+        for ds in (0, 1):
+            if cur[ds] is not None:
+                r = cur[ds]
+                seqi[ds] = int(tabs[ds].tid[r])
+                left[ds] = int(tabs[ds].pos[r])
+                right[ds] = end_of(ds, r)
+                arrs[ds].append(r)
+
+        def restart(ds):
+            r = cur[ds]
+            yielded[ds] = True
+            arrs[ds] = [r]
+            seqi[ds] = int(tabs[ds].tid[r])
+            left[ds] = int(tabs[ds].pos[r])
+            right[ds] = end_of(ds, r)
+
+        while True:
+            for ds in (0, 1):
+                if yielded[ds] and cur[ds] is not None:
+                    cur[ds] = collect(ds, arrs[ds], unm[ds])
+                    right[ds] = rightmost(ds, arrs[ds], right[ds])
+                    yielded[ds] = False
+            if cur[0] is None and cur[1] is None:
+                yield arrs[0], None, None
+                yield None, arrs[1], None
+                break
+            if cur[0] is not None and cur[1] is not None:
+                c = compare(seqi[0], left[0], right[0], seqi[1], left[1], right[1])
+                if c < -1:
+                    yield arrs[0], None, None
+                    restart(0)
+                elif c > 1:
+                    yield None, arrs[1], None
+                    restart(1)
+                else:
+                    yield arrs[0], arrs[1], (contig, min(left[0], left[1]), max(right[0], right[1]))
+                    restart(0)
+                    restart(1)
+            else:
+                if cur[0] is not None:
+                    yield arrs[0], None, None
+                    restart(0)
+                if cur[1] is not None:
+                    yield None, arrs[1], None
+                    restart(1)
+        yield None, None, (unm[0], unm[1])
+
+    def anonymize_inter_window_region(self, w: Window) -> None:
+        """SR:498-558."""
+        first, last = w.first, w.last
+        if first + last == 0:
+            first = last = None
+        events = self.iter_fetch_pair(w.sequence, first, last)
+        hid = self._open()
+        for t_arr, n_arr, extra in events:
+            if t_arr is not None and n_arr is not None:
+                seq, lo, hi = extra
+                self.anonymize_window(seq, lo, hi, None, False)
+            elif t_arr is None and n_arr is None:
+                for ds in (0, 1):
+                    for r in extra[ds]:
+                        self.passthrough(ds, r, hid)
+            else:
+                ds = 0 if t_arr is not None else 1
+                for r in (t_arr if ds == 0 else n_arr):
+                    self.passthrough(ds, r, hid)
+        self._close(hid)
+
+    def pair_unmapped_mates(self) -> None:
+        """SR:561-600: re-fetch every window for placed-unmapped mates of unpaired reads."""
+        hid = self._open()
+        for w in self.windows:
+            for ds in (0, 1):
+                t = self.tables[ds]
+                for r in t.fetch(w.sequence, w.first - 1, w.last).tolist():
+                    if t.is_unmapped[r] and t.names[r] in self.to_pair:
+                        self.passthrough(ds, r, hid)
+        self._close(hid)
+
+    # ---- whole sample (SR:625-760) -----------------------------------------------------------
+    def run(self) -> Plan:
+        sections = get_genome_sections(self.windows, self.fasta)
+        for w in sections:
+            if w.is_variant_window():
+                self.stats_events.append(("window", str(w)))
+                self.anonymize_window(w.sequence, w.first, w.last, w.variant, True)
+            else:
+                self.stats_events.append(("outside", None))
+                self.anonymize_inter_window_region(w)
+        if self.to_pair:
+            self.pair_unmapped_mates()
+        for k in self.written:
+            self.to_pair.pop(k, None)
+        single: Dict[int, List[Instance]] = {0: [], 1: []}
+        for name, pair in self.to_pair.items():
+            inst = pair[0] if pair[0] is not None else pair[1]
+            single[inst[0]].append(inst)
+        return Plan(self.scopes, self.io_log, single, self.stats_events, bool(self.to_pair))

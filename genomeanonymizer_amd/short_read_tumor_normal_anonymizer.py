@@ -1,0 +1,83 @@
+"""Sample driver: tumor/normal pairs -> anonymized FASTQ (+ statistics).
+
+Mirrors the reference module of the same name (short_read_tumor_normal_anonymizer.py):
+``name_output`` (:55-58), ``get_windows`` (:71-131, in planner.py), ``anonymize_genome``
+(:625-760) and ``run_short_read_tumor_normal_anonymizer`` (:889-967) with the same
+arguments and output files:
+  {tumor/normal prefix}.1.fastq / .2.fastq, .single_end.fastq when mates stay unpaired,
+  {normal_bam}.statistics.txt with --record_statistics.
+Per sample the host plans all scopes (planner.py), the GPU masks them in one batch
+(anonymizer_methods.py -> libganon_hip.so) and the host writes the records in the
+reference's order (writer.py).
+"""
+from __future__ import annotations
+
+import logging
+import re
+import time
+from typing import Dict, List, Sequence, Tuple
+
+from .anonymizer_methods import CompleteGermlineAnonymizer
+from .io.bam import ReadTable
+from .io.fasta import FastaRef
+from .io.vcf import read_vcf
+from .planner import SamplePlanner, Window, get_windows
+from .writer import statistics_rows, write_fastqs, write_statistics
+
+log = logging.getLogger("genomeanonymizer_amd")
+
+
+def name_output(sample: str) -> str:
+    """SR:55-58 (note: the pattern's '.' matches any character, as in the reference)."""
+    return re.sub(".bam|.sam|.cram", ".anonymized", sample)
+
+
+def get_ref_idxs(fasta: FastaRef) -> Dict[str, int]:
+    return dict(fasta.index)
+
+
+def anonymize_genome(windows_in_sample: List[Window], tumor_bam_file: str, normal_bam_file: str,
+                     ref_genome_file: str, anonymizer: CompleteGermlineAnonymizer, tumor_output_fastq: str,
+                     normal_output_fastq: str, record_statistics: bool, available_threads: int = 8,
+                     fasta: FastaRef = None) -> dict:
+    t0 = time.time()
+    fasta = fasta or FastaRef(ref_genome_file)
+    tumor = ReadTable(tumor_bam_file, threads=available_threads)
+    normal = ReadTable(normal_bam_file, threads=available_threads)
+    t1 = time.time()
+    planner = SamplePlanner(tumor, normal, fasta, windows_in_sample)
+    plan = planner.run()
+    t2 = time.time()
+    res = anonymizer.anonymize(planner, plan)
+    t3 = time.time()
+    write_fastqs(plan, res, (tumor, normal), (tumor_output_fastq, normal_output_fastq))
+    if record_statistics:
+        write_statistics(f"{normal_bam_file}.statistics.txt", statistics_rows(plan, res))
+    t4 = time.time()
+    timing = {"decode_s": t1 - t0, "plan_s": t2 - t1, "mask_s": t3 - t2, "write_s": t4 - t3,
+              "reads": int(tumor.n + normal.n), "scopes": len(plan.scopes)}
+    log.info("Anonymization complete for samples %s and %s: %s", tumor_output_fastq, normal_output_fastq, timing)
+    return timing
+
+
+def run_short_read_tumor_normal_anonymizer(vcf_variants_per_sample: Sequence[str],
+                                           tumor_normal_samples: Sequence[Tuple[str, str]],
+                                           ref_genome_file: str, anonymizer: CompleteGermlineAnonymizer,
+                                           output_filenames: Sequence[Tuple[str, str]], record_statistics: bool,
+                                           cpus: int = 1, enhance_parallelization: bool = False) -> List[dict]:
+    """SR:889-967. Samples run one after another on the GPU (each is one device batch);
+    ``cpus`` sets the host decode threads. The reference's enhanced mode crashes whenever a
+    sample is split; here it is accepted and has no effect."""
+    if enhance_parallelization:
+        log.warning("--enhanced_multiprocessing has no effect in this build (the reference's mode is broken, "
+                    "SURVEY Q12)")
+    fasta = FastaRef(ref_genome_file)
+    ref_idx = get_ref_idxs(fasta)
+    inputs = []
+    for vcf, samples, outs in zip(vcf_variants_per_sample, tumor_normal_samples, output_filenames):
+        inputs.append((get_windows(read_vcf(vcf), ref_idx), samples, outs))
+    timings = []
+    for windows, (t_bam, n_bam), (t_out, n_out) in inputs:
+        timings.append(anonymize_genome(windows, t_bam, n_bam, ref_genome_file, anonymizer, t_out, n_out,
+                                        record_statistics, max(1, int(cpus)), fasta=fasta))
+    return timings

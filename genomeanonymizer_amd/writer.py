@@ -1,0 +1,305 @@
+"""FASTQ and statistics output.
+
+* FASTQ records as ``write_pair`` / ``write_single_end_reads`` write them
+  (short_read_tumor_normal_anonymizer.py:134-165, :603-622) with the per-read encoding of
+  ``AnonymizedRead.get_anonymized_fastq_record`` (anonymizer_methods.py:205-243):
+  ``@name/1|2``, the upper-cased (masked) sequence, reverse-complemented for reverse reads,
+  and the qualities printed in the BAM's stored order for every read (they are
+  loaded forward-oriented and reversed once more on output). Bulk formatting runs in
+  libganon_host.so; the rare indel-edited records are formatted here.
+* the statistics file of ``AnonymizedVariantsStatistics.write_statistics`` (SR:175-242).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import itertools
+from typing import Dict, List, Sequence, Tuple
+
+import numpy as np
+
+from . import native
+from .anonymizer_methods import MaskResult
+from .indels import apply_leftovers
+from .io.bam import ReadTable
+from .planner import Plan
+
+NT16 = "=ACMGRSVTWYHKDBN"
+_REVERSES = {ord("A"): ord("T"), ord("C"): ord("G"), ord("G"): ord("C"), ord("T"): ord("A"), ord("N"): ord("N")}
+OUTSIDE_WINDOWS = "outside_windows,-,-,-"
+STAT_HEADER = ["#SEQ", "#FIRST", "#LAST", "#SNV", "#DEL", "#INS", "#DUP", "#INV", "#CNV", "#TRA", "#SGL"]
+
+
+_NT16_BYTES = np.frombuffer(NT16.encode(), np.uint8)
+
+
+def _decode(buf: np.ndarray, nib0: int, n: int) -> bytearray:
+    i = nib0 + np.arange(n, dtype=np.int64)
+    b = buf[i >> 1]
+    c = np.where(i & 1, b & 0xF, b >> 4)
+    return bytearray(_NT16_BYTES[c].tobytes())
+
+
+class FastqFormatter:
+    def __init__(self, tables: Tuple[ReadTable, ReadTable], res: MaskResult):
+        self.tables = tables
+        self.res = res
+        self.lib = native.host_lib()
+        # buffers: 0 = device output, 1 = tumor BAM seq, 2 = normal BAM seq
+        self._seq_bufs = [res.seq_out, tables[0].seq, tables[1].seq]
+        self._qual_bufs = [tables[0].qual, tables[1].qual]
+
+    def _native(self, recs: Sequence[Tuple[int, int, int]]) -> bytes:
+        n = len(recs)
+        if n == 0:
+            return b""
+        T, N = self.tables
+        ds = np.fromiter((r[0] for r in recs), np.int64, n)
+        row = np.fromiter((r[1] for r in recs), np.int64, n)
+        sc = np.fromiter((r[2] for r in recs), np.int64, n)
+        seq_sel = np.where(sc >= 0, 0, 1 + ds).astype(np.uint8)
+        seq_off_t = np.where(ds == 0, T.seq_off[np.where(ds == 0, row, 0)], N.seq_off[np.where(ds == 1, row, 0)])
+        base = np.where(ds == 0, self.res.seq_base[0], self.res.seq_base[1])
+        byte_off = np.where(sc >= 0, base + seq_off_t, seq_off_t)
+        nib_off = (2 * byte_off).astype(np.int64)
+        pick = lambda f, dt: np.where(ds == 0, getattr(T, f)[np.where(ds == 0, row, 0)],
+                                      getattr(N, f)[np.where(ds == 1, row, 0)]).astype(dt)
+        seq_len = pick("l_seq", np.int32)
+        reverse = pick("is_reverse", np.uint8)
+        qual_off = pick("qual_off", np.int64)
+        flag = pick("flag", np.int64)
+        mate = np.where(flag & 0x40, 1, 2).astype(np.uint8)
+        qual_sel = ds.astype(np.uint8)
+        qual_rev = np.zeros(n, np.uint8)
+        # names: one blob for this call
+        names = [self.tables[d].names[r] for d, r, _ in recs]
+        enc = [s.encode() for s in names]
+        name_len = np.array([len(e) for e in enc], np.int32)
+        name_off = np.concatenate([[0], np.cumsum(name_len)[:-1]]).astype(np.int64)
+        blob = b"".join(enc)
+        cap = int(np.sum(name_len) + 2 * np.sum(seq_len) + 8 * n + 16)
+        out = C.create_string_buffer(cap)
+        u8p = C.POINTER(C.c_uint8)
+        seq_ptrs = (u8p * 3)(*[b.ctypes.data_as(u8p) for b in self._seq_bufs])
+        qual_ptrs = (u8p * 2)(*[b.ctypes.data_as(u8p) for b in self._qual_bufs])
+        P = lambda a, t: a.ctypes.data_as(C.POINTER(t))
+        w = self.lib.ganon_fastq_format(
+            n, seq_ptrs, P(seq_sel, C.c_uint8), P(nib_off, C.c_int64), P(seq_len, C.c_int32),
+            P(reverse, C.c_uint8), qual_ptrs, P(qual_sel, C.c_uint8), P(qual_off, C.c_int64),
+            P(seq_len, C.c_int32), P(qual_rev, C.c_uint8), blob, P(name_off, C.c_int64),
+            P(name_len, C.c_int32), P(mate, C.c_uint8), out, cap)
+        if w < 0:
+            if w == -(1 << 63):
+                raise RuntimeError("FASTQ buffer too small")
+            i = -w - 1
+            d, r, _ = recs[i]
+            raise TypeError(f"reverse read {self.tables[d].names[r]!r} has a base outside ACGTN: the "
+                            "reference's reverse complement fails on it (SURVEY Q7)")
+        return out.raw[:w]
+
+    def _edited(self, inst, edits) -> bytes:
+        ds, row, sc = inst
+        t = self.tables[ds]
+        L = int(t.l_seq[row])
+        if sc >= 0:
+            nib0 = 2 * (self.res.seq_base[ds] + int(t.seq_off[row]))
+            seq = _decode(self.res.seq_out, nib0, L)
+        else:
+            seq = _decode(t.seq, 2 * int(t.seq_off[row]), L)
+        q = t.qual[int(t.qual_off[row]):int(t.qual_off[row]) + L].tolist()
+        rev = bool(t.is_reverse[row])
+        qual_fwd = q[::-1] if rev else q
+        seq, qual_fwd = apply_leftovers(seq, qual_fwd, edits)
+        if rev:
+            try:
+                seq = bytearray(_REVERSES[c] for c in reversed(seq))
+            except KeyError:
+                raise TypeError(f"reverse read {t.names[row]!r} has a base outside ACGTN (SURVEY Q7)")
+            qual = qual_fwd[::-1]
+        else:
+            qual = qual_fwd
+        mate = 1 if t.flag[row] & 0x40 else 2
+        return (f"@{t.names[row]}/{mate}\n".encode() + bytes(seq) + b"\n+\n" +
+                bytes(x + 33 for x in qual) + b"\n")
+
+    def format(self, recs: Sequence[Tuple[int, int, int]]) -> bytes:
+        parts: List[bytes] = []
+        run: List[Tuple[int, int, int]] = []
+        left = self.res.leftovers
+        for inst in recs:
+            edits = left.get(inst)
+            if edits is None:
+                run.append(inst)
+                continue
+            parts.append(self._native(run))
+            run = []
+            parts.append(self._edited(inst, edits))
+        parts.append(self._native(run))
+        return b"".join(parts)
+
+
+TEXT_CHUNK = 8192  # TextIOWrapper._CHUNK_SIZE of CPython
+
+
+class AppendHandle:
+    """One ``open(path, 'a')`` text handle of CPython (TextIOWrapper over a BufferedWriter
+    of ``block`` = st_blksize bytes) writing into a shared O_APPEND file: records become
+    visible in the file only when a flush reaches the raw layer. The reference opens a
+    fresh set of such handles in every scope / section function (SR:297-299, :516-518,
+    :564-566), so nested handles interleave in the files at flush granularity."""
+
+    def __init__(self, sink: list, block: int):
+        self.sink = sink
+        self.block = block
+        self.pending: list = []
+        self.pending_len = 0
+        self.buf: list = []
+        self.buf_len = 0
+
+    def write(self, rec, n: int) -> None:
+        # textio.c write(): never concatenate more than chunk_size, flush once >= chunk_size
+        if self.pending_len + n > TEXT_CHUNK:
+            self._text_flush()
+            self.pending = [rec]
+            self.pending_len = n
+        else:
+            self.pending.append(rec)
+            self.pending_len += n
+        if self.pending_len >= TEXT_CHUNK:
+            self._text_flush()
+
+    def _text_flush(self) -> None:
+        if not self.pending:
+            return
+        recs, n = self.pending, self.pending_len
+        self.pending, self.pending_len = [], 0
+        # bufferedio.c write(): buffer if it fits, else flush the buffer and write through
+        if n <= self.block - self.buf_len:
+            self.buf.extend(recs)
+            self.buf_len += n
+            return
+        self._raw_flush()
+        if n > self.block:
+            self.sink.extend(recs)
+        else:
+            self.buf, self.buf_len = list(recs), n
+
+    def _raw_flush(self) -> None:
+        if self.buf:
+            self.sink.extend(self.buf)
+            self.buf, self.buf_len = [], 0
+
+    def close(self) -> None:
+        self._text_flush()
+        self._raw_flush()
+
+
+def replay_io(io_log, rec_len, block: int) -> Dict[Tuple[int, int], list]:
+    """Order in which the records of each output file reach the disk."""
+    files: Dict[Tuple[int, int], list] = {(d, s): [] for d in (0, 1) for s in (0, 1)}
+    handles: Dict[int, Dict[Tuple[int, int], AppendHandle]] = {}
+    for ev in io_log:
+        if ev[0] == "open":
+            handles[ev[1]] = {k: AppendHandle(files[k], block) for k in files}
+        elif ev[0] == "write":
+            inst = ev[4]
+            handles[ev[1]][(ev[2], ev[3])].write(inst, rec_len(inst))
+        else:
+            for h in handles.pop(ev[1]).values():
+                h.close()
+    if handles:
+        raise RuntimeError("unclosed handles in the I/O log")
+    return files
+
+
+def io_block_size(directory: str) -> int:
+    """st_blksize CPython would use for a buffered file in ``directory``."""
+    import os
+    try:
+        st = os.stat(directory).st_blksize
+        return st if st > 1 else 8192
+    except OSError:
+        return 8192
+
+
+def write_fastqs(plan: Plan, res: MaskResult, tables, prefixes: Tuple[str, str],
+                 block_size: int = None) -> Dict[str, int]:
+    import os
+    fmt = FastqFormatter(tables, res)
+    if block_size is None:
+        block_size = io_block_size(os.path.dirname(os.path.abspath(prefixes[0])))
+    edited = {inst: fmt._edited(inst, e) for inst, e in res.leftovers.items()}
+
+    def rec_len(inst):
+        b = edited.get(inst)
+        if b is not None:
+            return len(b)
+        t = tables[inst[0]]
+        return int(t.name_len[inst[1]]) + 8 + 2 * int(t.l_seq[inst[1]])
+
+    order = replay_io(plan.io_log, rec_len, block_size)
+    sizes = {}
+    for ds in (0, 1):
+        for slot in (0, 1):
+            path = f"{prefixes[ds]}.{slot + 1}.fastq"
+            data = fmt.format(order[(ds, slot)])
+            with open(path, "wb") as fh:
+                fh.write(data)
+            sizes[path] = len(data)
+    if plan.write_single_end:
+        for ds in (0, 1):
+            path = f"{prefixes[ds]}.single_end.fastq"
+            data = fmt.format(plan.single_end[ds])
+            with open(path, "wb") as fh:
+                fh.write(data)
+            sizes[path] = len(data)
+    return sizes
+
+
+def statistics_rows(plan: Plan, res: MaskResult) -> Dict[str, List[int]]:
+    """Replay the recorder events (SR:175-210) with the per-scope counts."""
+    from .variants import VariantType
+    rows: Dict[str, List[int]] = {OUTSIDE_WINDOWS: [0] * 8}
+    current = ""
+    for kind, val in plan.stats_events:
+        if kind == "window":
+            rows[val] = [0] * 8
+            current = val
+        elif kind == "outside":
+            current = OUTSIDE_WINDOWS
+        else:
+            s = int(val)
+            ic = res.scope_indel_counts.get(s, {})
+            add = [int(res.scope_snv_calls[s]), ic.get(VariantType.DEL, 0), ic.get(VariantType.INS, 0)]
+            if any(add):
+                row = rows[current]
+                for k in range(3):
+                    row[k] += add[k]
+    return rows
+
+
+def write_statistics(path: str, rows: Dict[str, List[int]]) -> None:
+    """AnonymizedVariantsStatistics.write_statistics (SR:212-242)."""
+    cols = [[] for _ in range(8)]
+    with open(path, "w") as fh:
+        fh.write("\t".join(STAT_HEADER) + "\n")
+        for key, counts in rows.items():
+            fields = key.split(",")[:-1]
+            fh.write("\t".join(map(str, itertools.chain(fields, counts))) + "\n")
+            for k, v in enumerate(counts):
+                cols[k].append(v)
+        fh.write("### Overall statistics:\n")
+        fh.write("\t".join(STAT_HEADER[3:]) + "\n")
+        arrays = [np.array(c, dtype=np.int64) for c in cols]
+        for stat in ("total_counts", "average_counts", "median_counts", "max_counts", "min_counts"):
+            fh.write(f"#{stat}\t")
+            if stat == "total_counts":
+                vals = [np.sum(a) for a in arrays]
+            elif stat == "average_counts":
+                vals = [a.mean() for a in arrays]
+            elif stat == "median_counts":
+                vals = [np.median(a) for a in arrays]
+            elif stat == "max_counts":
+                vals = [a.max() for a in arrays]
+            else:
+                vals = [a.min() for a in arrays]
+            fh.write("\t".join(map(str, vals)) + "\n")

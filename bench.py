@@ -1,0 +1,234 @@
+#!/usr/bin/env python3
+"""Benchmark of the germline-masking hot path on BASELINE.json configs[1].
+
+One step = one pass of the masking kernels over one resident batch: the config-2 layout
+(10 M synthetic 150 bp tumor+normal reads on a 3.0 Gb genome with 1 M germline SNPs and a
+1 M-window VCF; genomeanonymizer_amd/synth/batch.py) uploaded to HBM once, then
+``ganon_batch_run`` = SNV tally -> TN classification -> overwrite for every scope, plus the
+pass-through copies, exactly what ``ganon_mask_batch`` does minus the PCIe copies.
+Multi-GPU (torchrun): every rank owns its own config-2 shard (per-contig sharding makes
+shards independent; weak scaling) and the only collective is the int64 totals all-reduce
+over RCCL at the end of each step.
+
+Prints one JSON line (rank 0). ``roofline`` is for the dominant kernel: the algorithmic
+bytes it processes per launch (SURVEY §8(d) figures, attributed per kernel)
+over its average duration measured with HIP events on the launch stream.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+SMALL_CAP0, SMALL_CAP1 = 4096, 16384
+
+
+def kernel_bytes(arr) -> dict:
+    """Algorithmic bytes per launch of each kernel (SURVEY §8(d) per-unit figures).
+
+    Per read: ceil(L/2) in + ceil(L/2) out + 4*n_cigar + 16, charged to the kernel that
+    writes the read; each further scope incidence ceil(L/2) + 4*n_cigar + 8, charged to
+    that scope's kernel; each scope ceil(span/2) of reference, charged to its kernel."""
+    L = arr["read_len"].astype(np.int64)
+    h = (L + 1) // 2
+    nc = arr["n_cig"].astype(np.int64)
+    span = arr["scope_span_len"].astype(np.int64)
+    cls = np.where(span <= SMALL_CAP0, 0, np.where(span <= SMALL_CAP1, 1, 2))
+    names = ["k_scope_small<1>/4K", "k_scope_small<1>/16K", "large"]
+    out = {n: 0 for n in names}
+    out["k_passthrough"] = 0
+    ws = arr["write_scope"].astype(np.int64)
+    base = 2 * h + 4 * nc + 16
+    wcls = np.where(ws >= 0, cls[np.maximum(ws, 0)], 3)
+    for k, n in enumerate(names + ["k_passthrough"]):
+        out[n] += int(base[wcls == k].sum())
+    offs = arr["scope_incid_off"]
+    scope_of_inc = np.repeat(np.arange(len(span)), np.diff(offs))
+    r = arr["incid_read"].astype(np.int64)
+    # the first incidence of every read is covered by its base cost
+    first = np.zeros(len(r), bool)
+    is_ws = scope_of_inc == ws[r]
+    order = np.lexsort((~is_ws, r))
+    rs = r[order]
+    firsts = np.ones(len(rs), bool)
+    firsts[1:] = rs[1:] != rs[:-1]
+    first[order[firsts]] = True
+    extra = ~first
+    cost = (h + 4 * nc + 8)[r]
+    for k, n in enumerate(names):
+        out[n] += int(cost[extra & (cls[scope_of_inc] == k)].sum())
+        out[n] += int(((span + 1) // 2)[cls == k].sum())
+    return out
+
+
+def cpu_baseline(arr, n_reads: int, budget_s: float = 10.0) -> dict:
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    from pyoracle import OracleEngine
+    eng = OracleEngine()
+    runs, t0 = 0, time.perf_counter()
+    while True:
+        eng.mask(arr)
+        runs += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or runs >= 3:
+            break
+    return {"value": round(n_reads * runs / el, 1), "unit": "reads/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/ganon_oracle.c (C restatement of the reference's per-scope classify+mask, "
+                      f"single thread) over the whole {n_reads}-read batch x{runs} ({el:.1f} s); "
+                      f"reference Python calibration: 1,196 reads/s (BASELINE.md §2)"}
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--reads", type=int, default=10_000_000)
+    ap.add_argument("--genome", type=int, default=3_000_000_000)
+    ap.add_argument("--windows", type=int, default=1_000_000)
+    ap.add_argument("--germline", type=int, default=1_000_000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_r01.json"),
+                    help="PMC summary (tools/pmc_summary.py) for the traffic field, if present")
+    args = ap.parse_args()
+
+    import torch
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from genomeanonymizer_amd import native
+    from genomeanonymizer_amd.synth.batch import algorithmic_bytes, config2_batch
+
+    t_gen = time.perf_counter()
+    arr, info = config2_batch(n_reads=args.reads, genome=args.genome, n_windows=args.windows,
+                              n_germline=args.germline, seed=2 + rank)
+    t_gen = time.perf_counter() - t_gen
+    masker = native.HipMasker(local)
+    stream = torch.cuda.current_stream()
+    masker.set_stream(stream.cuda_stream)
+    t_up = time.perf_counter()
+    db = masker.upload(arr)
+    t_up = time.perf_counter() - t_up
+    tot_t = torch.zeros(8, dtype=torch.int64, device="cuda")
+
+    def step():
+        db.run()
+        if dist is not None:
+            db.copy_totals_to(tot_t.data_ptr())
+            dist.all_reduce(tot_t)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    dt_t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+    if dist is not None:
+        dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
+    dt = float(dt_t.item())
+
+    # per-kernel durations: the same steps again with a HIP event pair around each launch
+    masker.set_profiling(True)
+    ktimes: dict = {}
+    for _ in range(args.steps):
+        db.run()
+        db.sync()
+        for name, launches, ms in db.kernel_times():
+            k = ktimes.setdefault(name, [0, 0.0])
+            k[0] += launches
+            k[1] += ms
+    masker.set_profiling(False)
+    totals = db.totals()
+    batch_info = db.info()
+    if dist is not None:
+        db.copy_totals_to(tot_t.data_ptr())
+        dist.all_reduce(tot_t)
+        torch.cuda.synchronize()
+        job_totals = tot_t.cpu().numpy()
+    else:
+        job_totals = totals
+    db.free()
+
+    kb = kernel_bytes(arr)
+    per_kernel = {n: {"launches": c, "avg_ms": ms / c} for n, (c, ms) in ktimes.items()}
+    dom = max(per_kernel, key=lambda n: per_kernel[n]["avg_ms"] * per_kernel[n]["launches"])
+    dom_bytes = kb.get(dom, kb.get("large", 0) if dom.startswith("k_tile") else 0)
+    dom_ms = per_kernel[dom]["avg_ms"]
+    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
+    pass_ms = sum(v["avg_ms"] * v["launches"] for v in per_kernel.values()) / args.steps
+    alg_total = algorithmic_bytes(arr)
+    traffic = None
+    if os.path.exists(args.pmc):
+        try:
+            pmc = json.load(open(args.pmc))
+            if pmc.get("kernel") == dom and pmc.get("reads") == args.reads:
+                traffic = pmc.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    reads_total = info["reads"] * world
+    value = reads_total * args.steps / dt
+    result = {
+        "metric": "reads/sec + bases/sec anonymized, 150 bp paired BAM, 1/2/4/8 MI355X",
+        "value": round(value, 1),
+        "unit": "reads/s",
+        "bases_per_sec": round(value * info["read_len"], 1),
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (genomeanonymizer_amd.synth.batch.config2_batch, seed 2+rank)",
+        "config": {"workload": "BASELINE configs[1]: 10M-read 150 bp tumor+normal batch, 1M germline SNPs, "
+                               "1M-window VCF, 3.0 Gb / 24 contigs, resident in HBM",
+                   "reads_per_gpu": info["reads"], "scopes_per_gpu": info["scopes"],
+                   "window_scopes": info["window_scopes"], "union_scopes": info["union_scopes"],
+                   "passthrough_reads": info["passthrough_reads"], "parallelism": f"contig-shard x{world}"},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                     "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_ms": round(dom_ms, 5)},
+        "pass": {"kernel_ms": round(pass_ms, 4), "algorithmic_bytes": alg_total,
+                 "achieved_GBps": round(alg_total / (pass_ms * 1e-3) / 1e9, 1),
+                 "kernels": {n: {"avg_ms": round(v["avg_ms"], 5), "launches_per_step": v["launches"] // args.steps,
+                                 "alg_bytes": kb.get(n)} for n, v in per_kernel.items()}},
+        "totals": {k: int(v) for k, v in zip(native.TOTAL_NAMES, job_totals)},
+        "batch": batch_info,
+        "setup_s": {"generate": round(t_gen, 1), "upload_pcie": round(t_up, 2)},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(arr, info["reads"])
+    elif rank == 0:
+        result["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -934,6 +934,14 @@ GANON_API int ganon_batch_device_totals(ganon_dbatch *db, void **dev_ptr) {
   return GANON_OK;
 }
 
+GANON_API int ganon_batch_copy_totals(ganon_ctx *ctx, ganon_dbatch *db, void *dev_dst) {
+  if (!ctx || !db || !dev_dst) return fail(ctx, GANON_E_ARG, "null argument");
+  HIP_OR_FAIL(hipSetDevice(ctx->device));
+  HIP_OR_FAIL(hipMemcpyAsync(dev_dst, db->totals, GANON_N_TOTALS * sizeof(int64_t), hipMemcpyDeviceToDevice,
+                             ctx->stream));
+  return GANON_OK;
+}
+
 GANON_API int ganon_batch_info(ganon_dbatch *db, int64_t *info) {
   if (!db || !info) return GANON_E_ARG;
   info[0] = db->n_small[0];

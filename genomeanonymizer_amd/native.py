@@ -107,6 +107,7 @@ def hip_lib():
     lib.ganon_batch_download.argtypes = [_p, _p, _u8p, _i32p, _i32p, _i64p]
     lib.ganon_batch_free.argtypes = [_p, _p]
     lib.ganon_batch_device_totals.argtypes = [_p, C.POINTER(_p)]
+    lib.ganon_batch_copy_totals.argtypes = [_p, _p, _p]
     lib.ganon_last_kernel_times.argtypes = [_p, C.POINTER(KernelTime), C.c_int]
     lib.ganon_batch_info.argtypes = [_p, _i64p]
     if lib.ganon_abi_version() != 1:
@@ -119,7 +120,7 @@ EXPORTED_HIP_SYMBOLS = (
     "ganon_ctx_create", "ganon_ctx_destroy", "ganon_last_error", "ganon_abi_version",
     "ganon_ctx_set_stream", "ganon_ctx_set_profiling", "ganon_mask_batch", "ganon_batch_upload",
     "ganon_batch_run", "ganon_batch_sync", "ganon_batch_download", "ganon_batch_free",
-    "ganon_batch_device_totals", "ganon_last_kernel_times", "ganon_batch_info",
+    "ganon_batch_device_totals", "ganon_batch_copy_totals", "ganon_last_kernel_times", "ganon_batch_info",
 )
 EXPORTED_HOST_SYMBOLS = (
     "ganon_bam_open", "ganon_bam_view_get", "ganon_bam_error", "ganon_bam_close",
@@ -213,6 +214,9 @@ class DeviceBatch:
         self.m._check(self.m._lib.ganon_batch_download(self.m._h, self.h, None, None, None, _ptr(tot, _i64p)),
                       "download totals")
         return tot
+
+    def copy_totals_to(self, dev_ptr: int) -> None:
+        self.m._check(self.m._lib.ganon_batch_copy_totals(self.m._h, self.h, _p(dev_ptr)), "copy_totals")
 
     def device_totals_ptr(self) -> int:
         p = _p()

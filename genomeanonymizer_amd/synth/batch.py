@@ -1,0 +1,406 @@
+"""Synthetic device batches (include/ganon.h layout) built directly in numpy, for kernel
+parity tests and the benchmark — no BAM round trip.
+
+* ``random_batch``: small batches full of edge cases (soft clips, I/D/N/H/=/X CIGAR ops,
+  N / IUPAC / '=' read bases, kept variants on TN sites, empty scopes, zero-length reads,
+  reads shared by several scopes, pass-through reads, scopes wider than the LDS cap).
+* ``config2_batch``: BASELINE.json configs[1] — 10 M 150 bp reads (tumor + normal, FR
+  pairs, insert N(300, 30)) on a 3.0 Gb 24-contig random genome with 1 M germline het SNPs,
+  0.1 % errors, quals irrelevant to the kernel, and a window VCF of 1 M somatic SNVs spaced
+  >= 2.5 kb (windows cover ~67 % of the genome). Scopes follow the
+  planner's rules: one scope per window (reads overlapping [pos-1000, pos+1001)), and in
+  the gaps one scope per chain of overlapping reads that holds both tumor and normal reads
+  (iter_fetch_pair's union scopes, approximated by read chaining over both samples);
+  reads in no scope are pass-through (write_scope -1); a read in two scopes is written
+  from the first one (the first-writer rule).
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Tuple
+
+import numpy as np
+
+ACGT = np.array([1, 2, 4, 8], np.uint8)     # nt16 codes
+IUPAC = np.array([3, 5, 6, 7, 9, 10, 11, 12, 13, 14], np.uint8)
+
+
+def pack_nibbles(codes: np.ndarray) -> np.ndarray:
+    c = codes.astype(np.uint8)
+    if len(c) & 1:
+        c = np.concatenate([c, np.zeros(1, np.uint8)])
+    return ((c[0::2] << 4) | c[1::2]).astype(np.uint8)
+
+
+def unpack_nibbles(packed: np.ndarray, n: int) -> np.ndarray:
+    out = np.empty(2 * len(packed), np.uint8)
+    out[0::2] = packed >> 4
+    out[1::2] = packed & 0xF
+    return out[:n]
+
+
+def _cigar_word(op: str, n: int) -> int:
+    return (n << 4) | "MIDNSHP=X".index(op)
+
+
+def random_batch(seed: int, n_scopes: int = 64, max_reads: int = 40, read_len=(0, 220),
+                 wide_scopes: int = 2, rare_frac: float = 0.02) -> Dict[str, np.ndarray]:
+    """Edge-case batch. Every scope owns a private contig region so spans never collide."""
+    rng = np.random.default_rng(seed)
+    scopes = []
+    region_len = []
+    for s in range(n_scopes):
+        wide = s < wide_scopes
+        span = int(rng.integers(20000, 40000)) if wide else int(rng.integers(50, 3000))
+        region_len.append(span + 1200)
+        scopes.append(wide)
+    # reference: one contig per scope region, each starting on a byte boundary
+    ref_codes, ref_nib_off = [], []
+    nib = 0
+    for L in region_len:
+        r = ACGT[rng.integers(0, 4, L)]
+        ns = rng.random(L) < 0.01
+        r[ns] = 15                                   # N in the reference: never a call
+        iu = rng.random(L) < 0.003
+        r[iu] = IUPAC[rng.integers(0, len(IUPAC), int(iu.sum()))]
+        ref_codes.append(r)
+        ref_nib_off.append(nib)
+        nib += L + (L & 1)
+    ref_packed = np.concatenate([pack_nibbles(r) for r in ref_codes])
+    reads: List[Tuple[int, int, list, np.ndarray, int]] = []   # (scope, pos, cigar, seq, dataset)
+    scope_reads: List[List[int]] = []
+    for s, wide in enumerate(scopes):
+        ref = ref_codes[s]
+        L = len(ref)
+        # germline sites: alt alleles shared by tumor and normal reads
+        n_sites = max(1, L // 60)
+        sites = np.unique(rng.integers(300, L - 300, n_sites))
+        alt = {int(p): int(ACGT[rng.integers(0, 4)]) for p in sites}
+        rare_sites = {int(p): int(IUPAC[rng.integers(0, len(IUPAC))]) if rng.random() < 0.7 else 0
+                      for p in sites[rng.random(len(sites)) < rare_frac * 10]}
+        nr = int(rng.integers(0, max_reads + 1)) if not wide else int(rng.integers(150, 400))
+        ids = []
+        for _ in range(nr):
+            ds = int(rng.integers(0, 2))
+            rl = int(rng.integers(read_len[0], read_len[1] + 1))
+            pos = int(rng.integers(250, max(251, L - 300 - min(rl, 200))))
+            if wide and rng.random() < 0.3:
+                rl = int(rng.integers(1000, 6000))       # long reads crossing tile borders
+                pos = int(rng.integers(250, max(251, L - rl - 300)))
+            cig, seq = _make_read(rng, ref, pos, rl, alt, rare_sites, ds)
+            if cig is None:
+                continue
+            reads.append((s, pos, cig, seq, ds))
+            ids.append(len(reads) - 1)
+        scope_reads.append(ids)
+    # a few reads also join the next scope's incidence list when regions allow it: skip,
+    # spans are private; instead add cross-scope incidence by duplicating scope membership
+    # for reads that lie in both (none here) — shared membership is covered in config2.
+    n = len(reads)
+    ref_start = np.array([r[1] for r in reads], np.int64)
+    seq_parts, cig_parts = [], []
+    seq_off = np.zeros(n, np.int64)
+    cig_off = np.zeros(n, np.int64)
+    so = co = 0
+    for i, (_, _, cig, seq, _) in enumerate(reads):
+        p = pack_nibbles(seq)
+        seq_parts.append(p)
+        seq_off[i] = so
+        so += len(p)
+        cig_parts.append(np.array(cig, np.uint32))
+        cig_off[i] = co
+        co += len(cig)
+    arr = {
+        "read_len": np.array([len(r[3]) for r in reads], np.int32),
+        "seq_off": seq_off,
+        "seq_nt16": np.concatenate(seq_parts) if seq_parts else np.zeros(0, np.uint8),
+        "cig_off": cig_off,
+        "n_cig": np.array([len(r[2]) for r in reads], np.int32),
+        "cigar": np.concatenate(cig_parts) if cig_parts else np.zeros(0, np.uint32),
+        "dataset": np.array([r[4] for r in reads], np.uint8),
+        "ref_nt16": ref_packed,
+    }
+    # scope spans from their reads; the contig coordinate of scope s is the region offset
+    ends = np.array([_ref_end(r[1], r[2]) for r in reads], np.int64)
+    span_start, span_len, ref_off, incid, offs = [], [], [], [], [0]
+    keep_pos, keep_code = [], []
+    for s, ids in enumerate(scope_reads):
+        if ids:
+            a = int(ref_start[ids].min())
+            b = int(ends[ids].max())
+        else:
+            a = b = 0
+        span_start.append(a)
+        span_len.append(b - a)
+        ref_off.append(ref_nib_off[s] + a)
+        order = rng.permutation(len(ids))
+        incid.extend([ids[k] for k in order])
+        offs.append(len(incid))
+        # keep: half of the scopes keep one (alt) allele at a germline-ish site
+        if ids and rng.random() < 0.5:
+            r = reads[ids[0]]
+            kp = r[1] + int(rng.integers(0, 30))
+            keep_pos.append(kp)
+            keep_code.append(int(ACGT[rng.integers(0, 4)]) if rng.random() < 0.8 else 5)
+        else:
+            keep_pos.append(-1)
+            keep_code.append(0)
+    arr["ref_start"] = ref_start.astype(np.int32)
+    arr["scope_incid_off"] = np.array(offs, np.int64)
+    arr["incid_read"] = np.array(incid, np.int32)
+    arr["scope_span_start"] = np.array(span_start, np.int32)
+    arr["scope_span_len"] = np.array(span_len, np.int32)
+    arr["scope_ref_off"] = np.array(ref_off, np.int64)
+    arr["keep_pos"] = np.array(keep_pos, np.int32)
+    arr["keep_code"] = np.array(keep_code, np.uint8)
+    ws = np.full(n, -1, np.int32)
+    for s, ids in enumerate(scope_reads):
+        for i in ids:
+            if rng.random() < 0.85:
+                ws[i] = s
+    arr["write_scope"] = ws
+    return arr
+
+
+def _ref_end(pos: int, cig: list) -> int:
+    rl = sum(w >> 4 for w in cig if (w & 0xF) in (0, 2, 3, 7, 8))
+    return pos + (rl if rl > 0 else 1)
+
+
+def _make_read(rng, ref, pos, rl, alt, rare_sites, ds):
+    """Build (cigar words, nt16 codes) for a read of rl query bases starting at ref pos."""
+    if rl == 0:
+        return [_cigar_word("M", 0)] if rng.random() < 0.5 else [], np.zeros(0, np.uint8)
+    ops = []
+    left = rl
+    if rng.random() < 0.1:
+        k = int(rng.integers(1, min(20, left) + 1))
+        ops.append(("S", k)); left -= k
+    if rng.random() < 0.05:
+        ops.insert(0, ("H", int(rng.integers(1, 10))))
+    while left > 0:
+        k = int(rng.integers(1, left + 1)) if rng.random() < 0.3 else left
+        op = "M"
+        u = rng.random()
+        if u < 0.05:
+            op = "="
+        elif u < 0.1:
+            op = "X"
+        ops.append((op, k)); left -= k
+        if left > 0:
+            v = rng.random()
+            if v < 0.3:
+                n = int(rng.integers(1, min(8, left) + 1))
+                ops.append(("I", n)); left -= n
+            elif v < 0.6:
+                ops.append(("D", int(rng.integers(1, 6))))
+            elif v < 0.7:
+                ops.append(("N", int(rng.integers(5, 60))))
+    if rng.random() < 0.05:
+        ops.append(("H", int(rng.integers(1, 10))))
+    seq = []
+    rp = pos
+    for op, n in ops:
+        if op in "M=X":
+            for i in range(n):
+                p = rp + i
+                if p >= len(ref):
+                    return None, None
+                b = int(ref[p])
+                if p in alt and rng.random() < 0.6:
+                    b = alt[p]
+                if p in rare_sites and rng.random() < 0.5:
+                    b = rare_sites[p]
+                u = rng.random()
+                if u < 0.002:
+                    b = int(ACGT[rng.integers(0, 4)])
+                elif u < 0.004:
+                    b = 15
+                seq.append(b)
+            rp += n
+        elif op in "IS":
+            seq.extend(int(x) for x in ACGT[rng.integers(0, 4, n)])
+        elif op in "DN":
+            rp += n
+    if rp >= len(ref) - 1:
+        return None, None
+    return [_cigar_word(o, n) for o, n in ops], np.array(seq, np.uint8)
+
+
+# ---------------------------------------------------------------------------------------
+# BASELINE.json configs[1]
+# ---------------------------------------------------------------------------------------
+
+def _random_genome(rng, total: int) -> np.ndarray:
+    """Packed nt16 genome of random ACGT (2 bases per byte)."""
+    nbytes = (total + 1) // 2
+    raw = np.frombuffer(rng.bytes(nbytes), np.uint8)
+    lut = np.zeros(256, np.uint8)
+    for v in range(256):
+        lut[v] = (ACGT[v & 3] << 4) | ACGT[(v >> 2) & 3]
+    return lut[raw]
+
+
+def config2_batch(n_reads: int = 10_000_000, genome: int = 3_000_000_000, n_contigs: int = 24,
+                  n_windows: int = 1_000_000, n_germline: int = 1_000_000, read_len: int = 150,
+                  seed: int = 2, window_spacing: int = 2500) -> Tuple[Dict[str, np.ndarray], dict]:
+    """Vectorised BASELINE configs[1] batch. Returns (arrays, info)."""
+    rng = np.random.default_rng(seed)
+    L = read_len
+    # contigs: 24 of decreasing length summing to `genome`, each starting on a byte boundary
+    w = np.linspace(2.0, 1.0, n_contigs)
+    clen = np.floor(w / w.sum() * genome).astype(np.int64)
+    clen -= clen % 2
+    cstart = np.concatenate([[0], np.cumsum(clen)[:-1]])      # nibble offsets (even)
+    ref = _random_genome(rng, int(clen.sum()))
+
+    def ref_codes(gpos: np.ndarray) -> np.ndarray:
+        b = ref[gpos >> 1]
+        return np.where(gpos & 1, b & 0xF, b >> 4).astype(np.uint8)
+
+    # germline het SNPs (global positions) and their alt codes
+    gsnp = np.unique(rng.integers(0, int(clen.sum()), n_germline))
+    galt = ACGT[(np.searchsorted(ACGT, ref_codes(gsnp)) + rng.integers(1, 4, len(gsnp))) % 4]
+    # windows: evenly spaced per contig (>= window_spacing apart), 1-based pos >= 1002
+    per = np.maximum(1, (clen / clen.sum() * n_windows).astype(np.int64))
+    win_contig, win_pos = [], []
+    for c in range(n_contigs):
+        k = min(int(per[c]), max(0, (int(clen[c]) - 4000) // window_spacing))
+        pos = 1002 + np.arange(k, dtype=np.int64) * window_spacing + rng.integers(0, window_spacing - 2003 + 1, k)
+        pos = pos[pos <= clen[c] - 1003]
+        win_contig.append(np.full(len(pos), c, np.int64))
+        win_pos.append(pos)
+    win_contig = np.concatenate(win_contig)
+    win_pos = np.concatenate(win_pos)
+    # reads: FR pairs, half tumor half normal
+    n_pairs = n_reads // 2
+    pc = rng.choice(n_contigs, size=n_pairs, p=clen / clen.sum())
+    flen = np.clip(np.round(rng.normal(300, 30, n_pairs)).astype(np.int64), L + 10, None)
+    fstart = (rng.random(n_pairs) * (clen[pc] - flen - 2)).astype(np.int64)
+    ds_pair = (np.arange(n_pairs) >= n_pairs // 2).astype(np.uint8)      # 0 tumor, 1 normal
+    rc = np.concatenate([pc, pc])
+    rpos = np.concatenate([fstart, fstart + flen - L]).astype(np.int64)
+    rds = np.concatenate([ds_pair, ds_pair])
+    hap = np.concatenate([rng.integers(0, 2, n_pairs)] * 2).astype(bool)
+    # order reads like a coordinate-sorted pair of BAMs: by (contig, pos)
+    order = np.lexsort((rpos, rc))
+    rc, rpos, rds, hap = rc[order], rpos[order], rds[order], hap[order]
+    gstart = cstart[rc] + rpos
+    n = len(rpos)
+    # bases: reference + germline het alts on haplotype 1 + 0.1 % errors
+    codes = np.empty((n, L), np.uint8)
+    step = 1_000_000
+    offs = np.arange(L, dtype=np.int64)
+    for a in range(0, n, step):
+        b = min(n, a + step)
+        codes[a:b] = ref_codes(gstart[a:b, None] + offs[None, :])
+    lo = np.searchsorted(gsnp, gstart)
+    hi = np.searchsorted(gsnp, gstart + L)
+    cnt = hi - lo
+    rid = np.repeat(np.arange(n), cnt)
+    k = np.arange(int(cnt.sum())) - np.repeat(np.cumsum(cnt) - cnt, cnt)
+    sidx = lo[rid] + k
+    carry = hap[rid]
+    codes[rid[carry], (gsnp[sidx] - gstart[rid])[carry]] = galt[sidx][carry]
+    n_err = int(n * L * 0.001)
+    er = rng.integers(0, n, n_err)
+    eo = rng.integers(0, L, n_err)
+    codes[er, eo] = ACGT[rng.integers(0, 4, n_err)]
+    seq = ((codes[:, 0::2] << 4) | codes[:, 1::2]).reshape(-1)
+    del codes
+    # scopes: windows first (in contig/position order), then gap union scopes
+    rend = rpos + L
+    key = rc * (1 << 40) + rpos
+    span = L
+    wkey_lo = win_contig * (1 << 40) + (win_pos - 1000 - span)
+    wkey_hi = win_contig * (1 << 40) + (win_pos + 1001)
+    wlo = np.searchsorted(key, wkey_lo, side="left")
+    whi = np.searchsorted(key, wkey_hi, side="left")
+    wcnt = whi - wlo
+    w_rid = np.repeat(np.arange(len(win_pos)), wcnt)
+    w_k = np.arange(int(wcnt.sum())) - np.repeat(np.cumsum(wcnt) - wcnt, wcnt)
+    w_read = wlo[w_rid] + w_k
+    keep_hit = rend[w_read] > (win_pos[w_rid] - 1000)
+    w_rid, w_read = w_rid[keep_hit], w_read[keep_hit]
+    in_window = np.zeros(n, bool)
+    in_window[w_read] = True
+    # gap chains over reads that are in no window: consecutive overlapping reads (same contig)
+    g = np.nonzero(~in_window)[0]
+    gc, gp, ge = rc[g], rpos[g], rend[g]
+    run_end = np.maximum.accumulate(gc * (1 << 40) + ge)
+    new_chain = np.ones(len(g), bool)
+    new_chain[1:] = (gc[1:] != gc[:-1]) | (gc[1:] * (1 << 40) + gp[1:] > run_end[:-1])
+    chain = np.cumsum(new_chain) - 1
+    n_chain = int(chain[-1]) + 1 if len(g) else 0
+    has_t = np.zeros(n_chain, bool)
+    has_n = np.zeros(n_chain, bool)
+    has_t[chain[rds[g] == 0]] = True
+    has_n[chain[rds[g] == 1]] = True
+    union = has_t & has_n
+    u_ids = np.nonzero(union)[0]
+    u_map = np.full(n_chain, -1, np.int64)
+    u_map[u_ids] = np.arange(len(u_ids))
+    g_scope = u_map[chain]
+    g_sel = g_scope >= 0
+    n_win = len(win_pos)
+    n_scopes = n_win + len(u_ids)
+    inc_scope = np.concatenate([w_rid, n_win + g_scope[g_sel]])
+    inc_read = np.concatenate([w_read, g[g_sel]])
+    o = np.argsort(inc_scope, kind="stable")
+    inc_scope, inc_read = inc_scope[o], inc_read[o]
+    counts = np.bincount(inc_scope, minlength=n_scopes)
+    incid_off = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+    # spans and reference offsets
+    s_start = np.full(n_scopes, np.iinfo(np.int64).max, np.int64)
+    s_end = np.zeros(n_scopes, np.int64)
+    np.minimum.at(s_start, inc_scope, rpos[inc_read])
+    np.maximum.at(s_end, inc_scope, rend[inc_read])
+    empty = counts == 0
+    s_start[empty] = 0
+    s_end[empty] = 0
+    s_contig = np.concatenate([win_contig, np.zeros(len(u_ids), np.int64)])
+    first_read = np.full(n_scopes, -1, np.int64)
+    first_read[inc_scope[::-1]] = inc_read[::-1]
+    has_read = first_read >= 0
+    s_contig[has_read] = rc[first_read[has_read]]
+    # first-writer rule: the earliest scope (lowest id) a read belongs to writes it
+    first_scope = np.full(n, n_scopes, np.int64)
+    np.minimum.at(first_scope, inc_read, inc_scope)
+    ws = np.where(first_scope < n_scopes, first_scope, -1).astype(np.int32)
+    arr = {
+        "ref_start": rpos.astype(np.int32),
+        "read_len": np.full(n, L, np.int32),
+        "seq_off": (np.arange(n, dtype=np.int64) * (L // 2)),
+        "seq_nt16": seq,
+        "cig_off": np.arange(n, dtype=np.int64),
+        "n_cig": np.ones(n, np.int32),
+        "cigar": np.full(n, (L << 4) | 0, np.uint32),
+        "dataset": rds.astype(np.uint8),
+        "write_scope": ws,
+        "scope_incid_off": incid_off,
+        "incid_read": inc_read.astype(np.int32),
+        "scope_span_start": s_start.astype(np.int32),
+        "scope_span_len": (s_end - s_start).astype(np.int32),
+        "scope_ref_off": (cstart[s_contig] + s_start).astype(np.int64),
+        "ref_nt16": ref,
+        "keep_pos": np.concatenate([win_pos - 1, np.full(len(u_ids), -1, np.int64)]).astype(np.int32),
+        "keep_code": np.concatenate([ACGT[rng.integers(0, 4, n_win)], np.zeros(len(u_ids), np.uint8)]),
+    }
+    info = {"reads": n, "read_len": L, "scopes": n_scopes, "window_scopes": n_win,
+            "union_scopes": int(len(u_ids)), "incidences": int(len(inc_read)),
+            "passthrough_reads": int((ws < 0).sum()), "genome": int(clen.sum()), "contigs": n_contigs,
+            "germline_snps": int(len(gsnp))}
+    return arr, info
+
+
+def algorithmic_bytes(arr: Dict[str, np.ndarray]) -> int:
+    """SURVEY §8(d) bytes of one launch over the batch: per read ceil(L/2) in + ceil(L/2)
+    out + 4*n_cigar + 16; per extra scope incidence ceil(L/2) + 4*n_cigar + 8; per scope
+    ceil(span/2) reference bytes."""
+    L = arr["read_len"].astype(np.int64)
+    half = (L + 1) // 2
+    nc = arr["n_cig"].astype(np.int64)
+    per_read = 2 * half + 4 * nc + 16
+    inc = np.bincount(arr["incid_read"], minlength=len(L)).astype(np.int64)
+    extra = np.maximum(inc - 1, 0) * (half + 4 * nc + 8)
+    ref = (arr["scope_span_len"].astype(np.int64) + 1) // 2
+    return int(per_read.sum() + extra.sum() + ref.sum())

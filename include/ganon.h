@@ -116,6 +116,8 @@ GANON_API int ganon_batch_download(ganon_ctx *ctx, ganon_dbatch *db, uint8_t *se
 GANON_API int ganon_batch_free(ganon_ctx *ctx, ganon_dbatch *db);
 /* Device pointer of the device-side totals ([GANON_N_TOTALS] int64), valid after run. */
 GANON_API int ganon_batch_device_totals(ganon_dbatch *db, void **dev_ptr);
+/* Enqueue a device-to-device copy of the totals into dev_dst (e.g. an RCCL buffer). */
+GANON_API int ganon_batch_copy_totals(ganon_ctx *ctx, ganon_dbatch *db, void *dev_dst);
 
 /* Kernel timing of the last profiled run: up to max_k entries of
  * (name, launches, total milliseconds). Returns the number of distinct kernels. */

@@ -1,0 +1,142 @@
+"""Parity of the HIP path (libganon_hip.so through the C ABI) — needs an MI355X.
+
+Bit-exact for every written read's packed bases and for the per-scope counts, against
+(1) the reference's own per-scope outputs (tests/golden/scopes, made by
+oracle/make_scope_golden.py), (2) the CPU oracle on seeded edge-case and config-2 batches,
+(3) the reference's end-to-end FASTQ/statistics files (tests/golden/<scenario>).
+"""
+import numpy as np
+import pytest
+
+from helpers import load_scope_golden, run_pipeline_vs_golden, written_reads_equal
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def masker(hip_built):
+    from genomeanonymizer_amd import native
+    m = native.HipMasker(0)
+    yield m
+    m.close()
+
+
+@pytest.fixture(scope="module")
+def oracle():
+    from pyoracle import OracleEngine
+    return OracleEngine()
+
+
+def _all_reads_equal(arr, a, b):
+    """Written reads and pass-through reads (write_scope -1 in the batch: plain copies)."""
+    L = (arr["read_len"].astype(np.int64) + 1) // 2
+    bad = []
+    for r in range(len(L)):
+        o, n = int(arr["seq_off"][r]), int(L[r])
+        if not np.array_equal(a[o:o + n], b[o:o + n]):
+            bad.append(r)
+    return bad
+
+
+@pytest.mark.parametrize("seed", [101, 202, 303])
+def test_hip_matches_reference_scopes(masker, seed):
+    arr, exp_seq, exp_calls = load_scope_golden(seed)
+    out, calls, bases, tot = masker.mask(arr)
+    assert written_reads_equal(arr, out, exp_seq) == []
+    assert np.array_equal(calls, exp_calls)
+
+
+@pytest.mark.parametrize("seed", list(range(1, 13)))
+def test_hip_matches_oracle_edge_batches(masker, oracle, seed):
+    from genomeanonymizer_amd.synth.batch import random_batch
+    kw = {}
+    if seed % 3 == 0:
+        kw["rare_frac"] = 0.3
+    if seed % 4 == 0:
+        kw["wide_scopes"] = 4
+    arr = random_batch(seed, n_scopes=40, **kw)
+    out, calls, bases, tot = masker.mask(arr)
+    o_out, o_calls, o_bases, o_tot = oracle.mask(arr)
+    in_batch = np.zeros(len(arr["read_len"]), bool)
+    in_batch[arr["incid_read"]] = True
+    bad = [r for r in _all_reads_equal(arr, out, o_out) if in_batch[r] or arr["write_scope"][r] >= 0]
+    assert bad == []
+    assert np.array_equal(calls, o_calls) and np.array_equal(bases, o_bases)
+    assert tot[0] == o_tot[0] and tot[1] == o_tot[1]
+
+
+def test_hip_rare_and_wide_paths_exercised(masker):
+    from genomeanonymizer_amd.synth.batch import random_batch
+    arr = random_batch(8, n_scopes=30, rare_frac=0.3, wide_scopes=4)
+    db = masker.upload(arr)
+    db.run()
+    db.sync()
+    info = db.info()
+    tot = db.totals()
+    db.free()
+    assert info["large_scopes"] >= 1 and info["large_tiles"] >= 2
+    assert tot[5] >= 1, "no scope went through the 16-code re-run"
+
+
+@pytest.mark.parametrize("name", ["tiny", "edge", "config1"])
+def test_hip_pipeline_matches_reference(name, tmp_path, hip_built):
+    from genomeanonymizer_amd.anonymizer_methods import CompleteGermlineAnonymizer
+    bad = run_pipeline_vs_golden(name, str(tmp_path / name), CompleteGermlineAnonymizer(device=0))
+    assert bad == {}
+
+
+def test_hip_config2_matches_oracle(masker, oracle):
+    """BASELINE configs[1] layout at 2 M reads: every byte and count equal to the oracle."""
+    from genomeanonymizer_amd.synth.batch import config2_batch
+    arr, info = config2_batch(n_reads=2_000_000, genome=600_000_000, n_windows=200_000, n_germline=200_000)
+    out, calls, bases, tot = masker.mask(arr)
+    o_out, o_calls, o_bases, o_tot = oracle.mask(arr)
+    assert np.array_equal(calls, o_calls)
+    assert np.array_equal(bases, o_bases)
+    L = (arr["read_len"].astype(np.int64) + 1) // 2
+    assert np.all(L == 75)
+    assert np.array_equal(out, o_out)
+    assert tot[2] == info["reads"]
+
+
+def test_hip_device_path_is_idempotent_and_deterministic(masker):
+    """Running the same uploaded batch twice gives identical bytes and totals; masking the
+    masked output again changes nothing for TN-masked bases (they now equal the ref)."""
+    from genomeanonymizer_amd.synth.batch import config2_batch
+    arr, _ = config2_batch(n_reads=200_000, genome=60_000_000, n_windows=20_000, n_germline=40_000)
+    db = masker.upload(arr)
+    db.run()
+    db.sync()
+    a = db.download()
+    db.run()
+    db.sync()
+    b = db.download()
+    db.free()
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[3], b[3])
+    arr2 = dict(arr)
+    arr2["seq_nt16"] = a[0]
+    out2, calls2, bases2, _ = masker.mask(arr2)
+    assert bases2.sum() == 0
+
+
+def test_hip_empty_and_degenerate_batches(masker):
+    from genomeanonymizer_amd.synth.batch import random_batch
+    from genomeanonymizer_amd import native
+    z = lambda dt: np.zeros(0, dt)
+    empty = {"ref_start": z(np.int32), "read_len": z(np.int32), "seq_off": z(np.int64), "seq_nt16": z(np.uint8),
+             "cig_off": z(np.int64), "n_cig": z(np.int32), "cigar": z(np.uint32), "dataset": z(np.uint8),
+             "write_scope": z(np.int32), "scope_incid_off": np.zeros(1, np.int64), "incid_read": z(np.int32),
+             "scope_span_start": z(np.int32), "scope_span_len": z(np.int32), "scope_ref_off": z(np.int64),
+             "ref_nt16": z(np.uint8), "keep_pos": z(np.int32), "keep_code": z(np.uint8)}
+    out, calls, bases, tot = masker.mask(empty)
+    assert len(out) == 0 and tot[2] == 0
+    arr = random_batch(3, n_scopes=10)
+    bad = dict(arr)
+    bad["write_scope"] = arr["write_scope"].copy()
+    bad["write_scope"][0] = len(arr["scope_span_len"]) + 5
+    with pytest.raises(native.GanonError):
+        masker.mask(bad)
+    bad = dict(arr)
+    bad["scope_span_len"] = np.maximum(arr["scope_span_len"] - 10, 0).astype(np.int32)
+    with pytest.raises(native.GanonError):
+        masker.mask(bad)

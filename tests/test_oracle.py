@@ -1,0 +1,76 @@
+"""The oracle (oracle/ganon_oracle.c + the host pipeline) pinned against the reference's
+own outputs, generated in the build container by oracle/run_reference.py and
+oracle/make_scope_golden.py (the reference has no tests or fixtures of its own).
+
+The pipeline tests run the product's host planner and writer with the CPU oracle standing
+in for the device: they check the host logic on machines without a GPU. The product never
+uses the oracle (HipMasker is its only masking engine); the GPU tests repeat these checks
+through libganon_hip.so.
+"""
+import numpy as np
+import pytest
+
+from helpers import load_scope_golden, run_pipeline_vs_golden, written_reads_equal
+
+
+@pytest.mark.parametrize("seed", [101, 202, 303])
+def test_oracle_matches_reference_per_scope(seed):
+    from pyoracle import OracleEngine
+    arr, exp_seq, exp_calls = load_scope_golden(seed)
+    out, calls, bases, tot = OracleEngine().mask(arr)
+    assert written_reads_equal(arr, out, exp_seq) == []
+    assert np.array_equal(calls, exp_calls)
+    assert tot[0] == exp_calls.sum()
+
+
+@pytest.mark.parametrize("name", ["tiny", "edge", "config1"])
+def test_pipeline_with_oracle_matches_reference(name, tmp_path):
+    from pyoracle import OracleEngine
+    from genomeanonymizer_amd.anonymizer_methods import CompleteGermlineAnonymizer
+    bad = run_pipeline_vs_golden(name, str(tmp_path / name), CompleteGermlineAnonymizer(engine=OracleEngine()))
+    assert bad == {}
+
+
+def test_oracle_known_answers():
+    """Hand-built scope: TN SNV masked, T-only kept, N base ignored, kept variant kept."""
+    from pyoracle import OracleEngine
+    from genomeanonymizer_amd.synth.batch import pack_nibbles
+    A, C, G, T, N = 1, 2, 4, 8, 15
+    ref = np.array([A, C, G, T] * 5, np.uint8)               # 20 positions
+    reads = [  # (dataset, pos, bases)
+        (0, 0, [A, C, T, T, A, C]),      # T: pos2 G->T
+        (1, 1, [C, T, T, A, C, G]),      # N: pos2 G->T  => TN at pos 2
+        (0, 4, [A, C, G, G, A]),         # T: pos7 T->G (tumor only)
+        (1, 5, [C, G, T, A, N]),         # N: pos9 N ignored
+        (0, 8, [A, C, T, T]),            # T: pos10 G->T
+        (1, 8, [A, C, T, T]),            # N: pos10 G->T => TN but kept
+    ]
+    seq, offs = [], []
+    o = 0
+    for _, _, b in reads:
+        p = pack_nibbles(np.array(b, np.uint8))
+        seq.append(p)
+        offs.append(o)
+        o += len(p)
+    arr = {
+        "ref_start": np.array([r[1] for r in reads], np.int32),
+        "read_len": np.array([len(r[2]) for r in reads], np.int32),
+        "seq_off": np.array(offs, np.int64), "seq_nt16": np.concatenate(seq),
+        "cig_off": np.arange(len(reads), dtype=np.int64), "n_cig": np.ones(len(reads), np.int32),
+        "cigar": np.array([(len(r[2]) << 4) for r in reads], np.uint32),
+        "dataset": np.array([r[0] for r in reads], np.uint8),
+        "write_scope": np.zeros(len(reads), np.int32),
+        "scope_incid_off": np.array([0, len(reads)], np.int64),
+        "incid_read": np.arange(len(reads), dtype=np.int32),
+        "scope_span_start": np.array([0], np.int32), "scope_span_len": np.array([16], np.int32),
+        "scope_ref_off": np.array([0], np.int64), "ref_nt16": pack_nibbles(ref),
+        "keep_pos": np.array([10], np.int32), "keep_code": np.array([T], np.uint8),
+    }
+    out, calls, bases, tot = OracleEngine().mask(arr)
+    assert calls.tolist() == [1] and bases.tolist() == [2]
+    from genomeanonymizer_amd.synth.batch import unpack_nibbles
+    r0 = unpack_nibbles(out[offs[0]:offs[0] + 3], 6).tolist()
+    r1 = unpack_nibbles(out[offs[1]:offs[1] + 3], 6).tolist()
+    assert r0 == [A, C, G, T, A, C] and r1 == [C, G, T, A, C, G]
+    r2 = unpack_nibbles(out[offs[2]:offs[2] + 3], 5).tolist()
+    assert r2 == [A, C, G, G, A]

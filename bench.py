@@ -28,7 +28,19 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
-SMALL_CAP0, SMALL_CAP1 = 4096, 16384
+SMALL_CAP0, SMALL_CAP1 = 2560, 16384    # scope classes of ganon_hip.hip (kSmallCap0/1)
+
+
+def kernel_class(name: str) -> str:
+    if name.startswith("k_passthrough"):
+        return "k_passthrough"
+    if name.endswith("/2.5K"):
+        return "small2.5K"
+    if name.endswith("/16K"):
+        return "small16K"
+    if name.startswith("k_tile_large<1>") or name.startswith("k_mask_large"):
+        return "large"
+    return ""
 
 
 def kernel_bytes(arr) -> dict:
@@ -42,7 +54,7 @@ def kernel_bytes(arr) -> dict:
     nc = arr["n_cig"].astype(np.int64)
     span = arr["scope_span_len"].astype(np.int64)
     cls = np.where(span <= SMALL_CAP0, 0, np.where(span <= SMALL_CAP1, 1, 2))
-    names = ["k_scope_small<1>/4K", "k_scope_small<1>/16K", "large"]
+    names = ["small2.5K", "small16K", "large"]
     out = {n: 0 for n in names}
     out["k_passthrough"] = 0
     ws = arr["write_scope"].astype(np.int64)
@@ -96,6 +108,8 @@ def main() -> None:
     ap.add_argument("--windows", type=int, default=1_000_000)
     ap.add_argument("--germline", type=int, default=1_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--variant", type=int, default=0, help="0 wave-per-scope (default), 1 block-per-scope")
+    ap.add_argument("--ab", action="store_true", help="also time the other small-scope variant, interleaved")
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_r01.json"),
                     help="PMC summary (tools/pmc_summary.py) for the traffic field, if present")
     args = ap.parse_args()
@@ -118,6 +132,7 @@ def main() -> None:
                               n_germline=args.germline, seed=2 + rank)
     t_gen = time.perf_counter() - t_gen
     masker = native.HipMasker(local)
+    masker.set_variant(args.variant)
     stream = torch.cuda.current_stream()
     masker.set_stream(stream.cuda_stream)
     t_up = time.perf_counter()
@@ -160,6 +175,23 @@ def main() -> None:
             k[0] += launches
             k[1] += ms
     masker.set_profiling(False)
+    ab = None
+    if args.ab:
+        # interleaved rounds in one process (cdna_hip_programming.md §5.4 rule 24)
+        samples = {0: [], 1: []}
+        for _ in range(5):
+            for v in (0, 1):
+                masker.set_variant(v)
+                db.run()
+                torch.cuda.synchronize()
+                t = time.perf_counter()
+                for _ in range(args.steps):
+                    db.run()
+                torch.cuda.synchronize()
+                samples[v].append((time.perf_counter() - t) / args.steps * 1e3)
+        masker.set_variant(args.variant)
+        ab = {("wave" if v == 0 else "block"): {"median_ms": round(float(np.median(x)), 4),
+                                                "min_ms": round(float(np.min(x)), 4)} for v, x in samples.items()}
     totals = db.totals()
     batch_info = db.info()
     if dist is not None:
@@ -174,7 +206,7 @@ def main() -> None:
     kb = kernel_bytes(arr)
     per_kernel = {n: {"launches": c, "avg_ms": ms / c} for n, (c, ms) in ktimes.items()}
     dom = max(per_kernel, key=lambda n: per_kernel[n]["avg_ms"] * per_kernel[n]["launches"])
-    dom_bytes = kb.get(dom, kb.get("large", 0) if dom.startswith("k_tile") else 0)
+    dom_bytes = kb.get(kernel_class(dom), 0)
     dom_ms = per_kernel[dom]["avg_ms"]
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     pass_ms = sum(v["avg_ms"] * v["launches"] for v in per_kernel.values()) / args.steps
@@ -215,7 +247,8 @@ def main() -> None:
         "pass": {"kernel_ms": round(pass_ms, 4), "algorithmic_bytes": alg_total,
                  "achieved_GBps": round(alg_total / (pass_ms * 1e-3) / 1e9, 1),
                  "kernels": {n: {"avg_ms": round(v["avg_ms"], 5), "launches_per_step": v["launches"] // args.steps,
-                                 "alg_bytes": kb.get(n)} for n, v in per_kernel.items()}},
+                                 "alg_bytes": kb.get(kernel_class(n))} for n, v in per_kernel.items()}},
+        "ab_small_scope_kernel": ab,
         "totals": {k: int(v) for k, v in zip(native.TOTAL_NAMES, job_totals)},
         "batch": batch_info,
         "setup_s": {"generate": round(t_gen, 1), "upload_pcie": round(t_up, 2)},

@@ -36,7 +36,7 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / 64;
-constexpr int kSmallCap0 = 4096;    // positions, class 0
+constexpr int kSmallCap0 = 2560;    // positions, class 0 (window scopes: 2001 + read overhang)
 constexpr int kSmallCap1 = 16384;   // positions, class 1 (= wide cap)
 constexpr int kTile = 16384;        // positions per tile of a large scope
 constexpr int kPersistGrid = 1024;  // grid of the device-counted (rare) re-run kernels
@@ -120,9 +120,25 @@ __device__ __forceinline__ int block_sum(int v, int *scratch) {
 // ---- tally of one read into the LDS table covering [a, b) ------------------------------
 // TB = bytes per position: 1 (ACGT nibbles) or 4 (16-code masks). Returns true when a
 // non-ACGTN base that would be a call was seen (only meaningful for TB == 1).
-template <int TB>
+// Reference nibble of contig position p: staged in LDS (nibble 0 = position a) ...
+struct LdsRef {
+  const uint8_t *refb;
+  int a;
+  __device__ __forceinline__ int operator()(int p) const {
+    const int off = p - a;
+    return (refb[off >> 1] >> ((off & 1) ? 0 : 4)) & 0xF;
+  }
+};
+// ... or read straight from the packed genome (nib0 = nibble index of position 0).
+struct GlobalRef {
+  const uint8_t *ref;
+  int64_t nib0;
+  __device__ __forceinline__ int operator()(int p) const { return nib_at(ref, nib0 + p); }
+};
+
+template <int TB, typename RefFn>
 __device__ __forceinline__ bool tally_read(const DevBatch &B, int r, int a, int b,
-                                           uint32_t *tab, const uint8_t *refb, int lane) {
+                                           uint32_t *tab, const RefFn &refn, int lane) {
   const int L = B.read_len[r];
   const int ds = B.dataset[r];
   const int64_t sq = B.seq_off[r] * 2;
@@ -134,7 +150,7 @@ __device__ __forceinline__ bool tally_read(const DevBatch &B, int r, int a, int 
     if (p < a || p >= b) continue;
     const int c = nib_at(B.seq, sq + q);
     const int off = p - a;
-    const int rc = (refb[off >> 1] >> ((off & 1) ? 0 : 4)) & 0xF;
+    const int rc = refn(p);
     if (c == 15 || c == rc || !is_acgt(rc)) continue;
     if (TB == 1) {
       if (is_acgt(c)) atomicOr(&tab[off >> 2], (uint32_t)c << (ds * 4 + (off & 3) * 8));
@@ -193,9 +209,9 @@ __device__ __forceinline__ void clear_keep(const DevBatch &B, int s, int a, int 
 }
 
 // Write the masked copy of read r (all bytes) using the LDS tally of [a, b).
-template <int TB>
+template <int TB, typename RefFn>
 __device__ __forceinline__ int mask_read_lds(const DevBatch &B, int r, int a, const uint32_t *tab,
-                                             const uint8_t *refb, uint8_t *__restrict__ out, int lane) {
+                                             const RefFn &refn, uint8_t *__restrict__ out, int lane) {
   const int L = B.read_len[r];
   const int64_t so = B.seq_off[r];
   CigarCursor cur;
@@ -214,7 +230,7 @@ __device__ __forceinline__ int mask_read_lds(const DevBatch &B, int r, int a, co
       const int off = p - a;
       const uint32_t tn = tn_mask<TB>(tab, off);
       if (tn && tn_hit<TB>(tn, nb[h])) {
-        nb[h] = (refb[off >> 1] >> ((off & 1) ? 0 : 4)) & 0xF;
+        nb[h] = refn(p);
         ++masked;
       }
     }
@@ -266,7 +282,8 @@ __global__ void __launch_bounds__(kBlock) k_scope_small(const DevBatch B, const 
     __syncthreads();
     const int64_t i0 = B.incid_off[s], i1 = B.incid_off[s + 1];
     bool rare = false;
-    for (int64_t i = i0 + wave; i < i1; i += kWaves) rare |= tally_read<TB>(B, B.incid_read[i], a, b, tab, refb, lane);
+    const LdsRef refn{refb, a};
+    for (int64_t i = i0 + wave; i < i1; i += kWaves) rare |= tally_read<TB>(B, B.incid_read[i], a, b, tab, refn, lane);
     if (TB == 1 && rare) scratch[kWaves] = 1;
     __syncthreads();
     clear_keep<TB>(B, s, a, b, tab);
@@ -278,13 +295,188 @@ __global__ void __launch_bounds__(kBlock) k_scope_small(const DevBatch B, const 
     for (int64_t i = i0 + wave; i < i1; i += kWaves) {
       const int r = B.incid_read[i];
       if (B.write_scope[r] != s) continue;
-      bases += mask_read_lds<TB>(B, r, a, tab, refb, out, lane);
+      bases += mask_read_lds<TB>(B, r, a, tab, refn, out, lane);
     }
     bases = block_sum(bases, scratch);
     if (threadIdx.x == 0) {
       scope_calls[s] = calls;
       scope_bases[s] = bases;
       if (TB == 1 && scratch[kWaves]) rare_list[atomicAdd(rare_count, 1)] = s;
+    }
+    __syncthreads();
+  }
+}
+
+// One WAVE per small scope (the common case: ~2.3 kb spans, a handful to a few hundred
+// reads). Reads are taken 64 at a time: each lane loads one read's metadata, reads with a
+// single M/=/X op covering the whole sequence ("simple", ~all short reads) are compacted
+// into LDS and processed four at a time by 16-lane groups (one packed byte = two bases
+// per lane step); reads with any other CIGAR go through the per-read cursor walk. The
+// reference nibbles come straight from the packed genome (no staging), the tally is the
+// 1-byte-per-position LDS table. Same results as k_scope_small<1>.
+constexpr int kMetaLds = 64 * (4 * 4 + 8);
+
+__device__ __forceinline__ uint64_t lanes_below(int lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
+
+__global__ void __launch_bounds__(64) k_scope_wave(const DevBatch B, const int32_t *__restrict__ list, int n,
+                                                   int cap, uint8_t *__restrict__ out, int32_t *scope_calls,
+                                                   int32_t *scope_bases, int32_t *rare_list, int32_t *rare_count) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  uint32_t *tab = smem;
+  int *m_start = reinterpret_cast<int *>(smem + cap / 4);
+  int *m_len = m_start + 64;
+  int *m_ds = m_len + 64;
+  int64_t *m_off = reinterpret_cast<int64_t *>(m_ds + 128);
+  const int lane = threadIdx.x;
+  for (int li = blockIdx.x; li < n; li += gridDim.x) {
+    const int s = list[li];
+    const int a = B.span_start[s];
+    const int span = B.span_len[s];
+    const int b = a + span;
+    const GlobalRef refn{B.ref, B.ref_off[s] - a};
+    uint4 *t4 = reinterpret_cast<uint4 *>(tab);
+    for (int k = lane; k < ((span + 15) >> 4); k += 64) t4[k] = make_uint4(0u, 0u, 0u, 0u);
+    __syncthreads();
+    const int64_t i0 = B.incid_off[s], i1 = B.incid_off[s + 1];
+    bool rare = false;
+    // ---- tally ------------------------------------------------------------------------
+    for (int64_t c0 = i0; c0 < i1; c0 += 64) {
+      const int nh = (int)((i1 - c0) < 64 ? (i1 - c0) : 64);
+      int r = 0;
+      bool simple = false, cplx = false;
+      if (lane < nh) {
+        r = B.incid_read[c0 + lane];
+        const int L = B.read_len[r];
+        const int nc = B.n_cig[r];
+        if (nc == 1) {
+          const uint32_t w = B.cigar[B.cig_off[r]];
+          const int op = w & 15;
+          simple = (op == 0 || op == 7 || op == 8) && (int)(w >> 4) == L && L > 0;
+        }
+        cplx = !simple && nc > 0 && L > 0;
+      }
+      const uint64_t sm = __ballot(simple);
+      if (simple) {
+        const int idx = __popcll(sm & lanes_below(lane));
+        m_start[idx] = B.ref_start[r];
+        m_len[idx] = B.read_len[r];
+        m_ds[idx] = B.dataset[r];
+        m_off[idx] = B.seq_off[r];
+      }
+      __syncthreads();
+      const int ns = __popcll(sm);
+      for (int j0 = 0; j0 < ns; j0 += 4) {
+        const int j = j0 + (lane >> 4);
+        if (j >= ns) continue;
+        const int st = m_start[j], L = m_len[j], d = m_ds[j];
+        const int64_t so = m_off[j];
+        const int nb = (L + 1) >> 1;
+        for (int bi = lane & 15; bi < nb; bi += 16) {
+          const uint32_t byte = B.seq[so + bi];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int q = 2 * bi + h;
+            if (q >= L) break;
+            const int c = h ? (byte & 15) : (byte >> 4);
+            const int p = st + q;
+            const int rc = refn(p);
+            if (c == 15 || c == rc || !is_acgt(rc)) continue;
+            if (is_acgt(c)) {
+              const int off = p - a;
+              atomicOr(&tab[off >> 2], (uint32_t)c << (d * 4 + (off & 3) * 8));
+            } else {
+              rare = true;
+            }
+          }
+        }
+      }
+      uint64_t cm = __ballot(cplx);
+      while (cm) {
+        const int l = __ffsll((unsigned long long)cm) - 1;
+        cm &= cm - 1;
+        const int rr = __shfl(r, l);
+        rare |= tally_read<1>(B, rr, a, b, tab, refn, lane);
+      }
+      __syncthreads();
+    }
+    // ---- classify: kept allele out, count TN calls --------------------------------------
+    clear_keep<1>(B, s, a, b, tab);
+    __syncthreads();
+    int calls = 0;
+    for (int k = lane; k < ((span + 3) >> 2); k += 64) {
+      const uint32_t w = tab[k];
+      calls += __popc(w & (w >> 4) & 0x0F0F0F0Fu);
+    }
+    // ---- mask the reads this scope writes -------------------------------------------------
+    int bases = 0;
+    for (int64_t c0 = i0; c0 < i1; c0 += 64) {
+      const int nh = (int)((i1 - c0) < 64 ? (i1 - c0) : 64);
+      int r = 0;
+      bool simple = false, cplx = false;
+      if (lane < nh) {
+        r = B.incid_read[c0 + lane];
+        if (B.write_scope[r] == s) {
+          const int L = B.read_len[r];
+          const int nc = B.n_cig[r];
+          if (nc == 1) {
+            const uint32_t w = B.cigar[B.cig_off[r]];
+            const int op = w & 15;
+            simple = (op == 0 || op == 7 || op == 8) && (int)(w >> 4) == L && L > 0;
+          }
+          cplx = !simple && L > 0;
+        }
+      }
+      const uint64_t sm = __ballot(simple);
+      if (simple) {
+        const int idx = __popcll(sm & lanes_below(lane));
+        m_start[idx] = B.ref_start[r];
+        m_len[idx] = B.read_len[r];
+        m_off[idx] = B.seq_off[r];
+      }
+      __syncthreads();
+      const int ns = __popcll(sm);
+      for (int j0 = 0; j0 < ns; j0 += 4) {
+        const int j = j0 + (lane >> 4);
+        if (j >= ns) continue;
+        const int st = m_start[j], L = m_len[j];
+        const int64_t so = m_off[j];
+        const int nb = (L + 1) >> 1;
+        for (int bi = lane & 15; bi < nb; bi += 16) {
+          const uint32_t byte = B.seq[so + bi];
+          int nib[2] = {(int)(byte >> 4), (int)(byte & 15)};
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int q = 2 * bi + h;
+            if (q >= L) break;
+            const int off = st + q - a;
+            const uint32_t t = (tab[off >> 2] >> ((off & 3) * 8)) & 0xFF;
+            const uint32_t tn = t & (t >> 4) & 15;
+            if (tn && is_acgt(nib[h]) && (tn & (uint32_t)nib[h])) {
+              nib[h] = refn(st + q);
+              ++bases;
+            }
+          }
+          out[so + bi] = (uint8_t)((nib[0] << 4) | nib[1]);
+        }
+      }
+      uint64_t cm = __ballot(cplx);
+      while (cm) {
+        const int l = __ffsll((unsigned long long)cm) - 1;
+        cm &= cm - 1;
+        const int rr = __shfl(r, l);
+        bases += mask_read_lds<1>(B, rr, a, tab, refn, out, lane);
+      }
+      __syncthreads();
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      calls += __shfl_xor(calls, o);
+      bases += __shfl_xor(bases, o);
+    }
+    const bool any_rare = __ballot(rare) != 0;
+    if (lane == 0) {
+      scope_calls[s] = calls;
+      scope_bases[s] = bases;
+      if (any_rare) rare_list[atomicAdd(rare_count, 1)] = s;
     }
     __syncthreads();
   }
@@ -318,7 +510,7 @@ __global__ void __launch_bounds__(kBlock) k_tile_large(const DevBatch B, const T
     for (int64_t i = t.lo + wave; i < t.hi; i += kWaves) {
       const int r = large_incid[i];
       if (B.read_end[r] <= t.a || B.ref_start[r] >= t.b) continue;
-      rare |= tally_read<TB>(B, r, t.a, t.b, tab, refb, lane);
+      rare |= tally_read<TB>(B, r, t.a, t.b, tab, LdsRef{refb, t.a}, lane);
     }
     if (TB == 1 && rare) scratch[kWaves] = 1;
     __syncthreads();
@@ -414,6 +606,7 @@ struct ganon_ctx {
   hipStream_t own = nullptr;
   hipStream_t stream = nullptr;
   bool profiling = false;
+  int variant = GANON_VARIANT_DEFAULT;
   std::string err;
   struct Rec { std::string name; hipEvent_t e0, e1; };
   std::vector<Rec> recs;
@@ -587,6 +780,13 @@ GANON_API const char *ganon_last_error(ganon_ctx *ctx) { return ctx ? ctx->err.c
 GANON_API int ganon_ctx_set_stream(ganon_ctx *ctx, void *hip_stream) {
   if (!ctx) return GANON_E_ARG;
   ctx->stream = hip_stream ? reinterpret_cast<hipStream_t>(hip_stream) : ctx->own;
+  return GANON_OK;
+}
+
+GANON_API int ganon_ctx_set_variant(ganon_ctx *ctx, int variant) {
+  if (!ctx || variant < GANON_VARIANT_DEFAULT || variant > GANON_VARIANT_BLOCK)
+    return fail(ctx, GANON_E_ARG, "unknown kernel variant %d", variant);
+  ctx->variant = variant;
   return GANON_OK;
 }
 
@@ -819,11 +1019,19 @@ GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
   const int caps[2] = {kSmallCap0, kSmallCap1};
   for (int k = 0; k < 2; ++k) {
     if (!db->n_small[k]) continue;
-    KernelScope ks(ctx, k == 0 ? "k_scope_small<1>/4K" : "k_scope_small<1>/16K");
-    k_scope_small<1><<<db->n_small[k], kBlock, small_lds_bytes(1, caps[k]), st>>>(
-        B, db->small_list[k], db->n_small[k], nullptr, caps[k], db->out, db->scope_calls, db->scope_bases,
-        db->rare_small_list, db->counters + 0);
-    if ((rc = check_launch(ctx, "k_scope_small<1>"))) return rc;
+    if (ctx->variant == GANON_VARIANT_BLOCK) {
+      KernelScope ks(ctx, k == 0 ? "k_scope_small<1>/2.5K" : "k_scope_small<1>/16K");
+      k_scope_small<1><<<db->n_small[k], kBlock, small_lds_bytes(1, caps[k]), st>>>(
+          B, db->small_list[k], db->n_small[k], nullptr, caps[k], db->out, db->scope_calls, db->scope_bases,
+          db->rare_small_list, db->counters + 0);
+      if ((rc = check_launch(ctx, "k_scope_small<1>"))) return rc;
+    } else {
+      KernelScope ks(ctx, k == 0 ? "k_scope_wave/2.5K" : "k_scope_wave/16K");
+      k_scope_wave<<<db->n_small[k], 64, (size_t)caps[k] + kMetaLds, st>>>(
+          B, db->small_list[k], db->n_small[k], caps[k], db->out, db->scope_calls, db->scope_bases,
+          db->rare_small_list, db->counters + 0);
+      if ((rc = check_launch(ctx, "k_scope_wave"))) return rc;
+    }
   }
   if (db->n_tiles) {
     KernelScope ks(ctx, "k_tile_large<1>");

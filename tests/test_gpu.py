@@ -65,6 +65,21 @@ def test_hip_matches_oracle_edge_batches(masker, oracle, seed):
     assert tot[0] == o_tot[0] and tot[1] == o_tot[1]
 
 
+@pytest.mark.parametrize("seed", [21, 22, 23])
+def test_block_variant_matches_wave_variant(masker, seed):
+    """The first (workgroup-per-scope) kernel and the wave-per-scope kernel agree."""
+    from genomeanonymizer_amd.synth.batch import config2_batch, random_batch
+    arr = random_batch(seed, n_scopes=40, rare_frac=0.1, wide_scopes=1) if seed != 23 else \
+        config2_batch(n_reads=300_000, genome=90_000_000, n_windows=30_000, n_germline=60_000)[0]
+    res = []
+    for v in (0, 1):
+        masker.set_variant(v)
+        res.append(masker.mask(arr))
+    masker.set_variant(0)
+    for k in range(3):
+        assert np.array_equal(res[0][k], res[1][k])
+
+
 def test_hip_rare_and_wide_paths_exercised(masker):
     from genomeanonymizer_amd.synth.batch import random_batch
     arr = random_batch(8, n_scopes=30, rare_frac=0.3, wide_scopes=4)

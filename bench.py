@@ -34,6 +34,8 @@ SMALL_CAP0, SMALL_CAP1 = 2560, 16384    # scope classes of ganon_hip.hip (kSmall
 def kernel_class(name: str) -> str:
     if name.startswith("k_passthrough"):
         return "k_passthrough"
+    if name == "copy_seq":
+        return "k_passthrough"
     if name.endswith("/2.5K"):
         return "small2.5K"
     if name.endswith("/16K"):
@@ -178,9 +180,9 @@ def main() -> None:
     ab = None
     if args.ab:
         # interleaved rounds in one process (cdna_hip_programming.md §5.4 rule 24)
-        samples = {0: [], 1: []}
+        samples = {0: [], 1: [], 2: []}
         for _ in range(5):
-            for v in (0, 1):
+            for v in (0, 1, 2):
                 masker.set_variant(v)
                 db.run()
                 torch.cuda.synchronize()
@@ -190,7 +192,7 @@ def main() -> None:
                 torch.cuda.synchronize()
                 samples[v].append((time.perf_counter() - t) / args.steps * 1e3)
         masker.set_variant(args.variant)
-        ab = {("wave" if v == 0 else "block"): {"median_ms": round(float(np.median(x)), 4),
+        ab = {("v2_copy_patch", "v0_block", "v1_wave")[v]: {"median_ms": round(float(np.median(x)), 4),
                                                 "min_ms": round(float(np.min(x)), 4)} for v, x in samples.items()}
     totals = db.totals()
     batch_info = db.info()

@@ -482,6 +482,212 @@ __global__ void __launch_bounds__(64) k_scope_wave(const DevBatch B, const int32
   }
 }
 
+// ---- v2: copy-then-patch ----------------------------------------------------------------
+// The output starts as a device copy of the input bases (one streaming memcpy); the scope
+// kernel only reads. Per incidence a 16-byte record (built at upload, scope-major, so a
+// scope's records are one coalesced load) says where the read is and whether this scope
+// writes it. Simple reads are taken 16 nibbles per lane (three aligned dword loads each for
+// the read and the reference, nibble-swapped so nibble k sits at bits 4k), mismatches go
+// to the LDS tally AND to a short LDS observation list; after classification only the
+// observations that hit a TN call in a read this scope writes are patched in place
+// (atomicXor on the containing dword: neighbouring reads' bytes are untouched).
+constexpr int kObsCap = 256;
+constexpr uint32_t kRecSimple = 1u << 25, kRecMine = 1u << 26, kRecCplx = 1u << 27;
+
+__device__ __forceinline__ uint32_t nib_swap(uint32_t d) { return ((d >> 4) & 0x0F0F0F0Fu) | ((d & 0x0F0F0F0Fu) << 4); }
+
+// 16 consecutive nibbles starting at nibble index n of a packed buffer (padded by 12 bytes):
+// nibble k of the result at bits [4k, 4k+4).
+__device__ __forceinline__ uint64_t load16(const uint8_t *__restrict__ buf, int64_t n) {
+  const uint32_t *p = reinterpret_cast<const uint32_t *>(buf) + (n >> 3);
+  const uint32_t d0 = nib_swap(p[0]), d1 = nib_swap(p[1]), d2 = nib_swap(p[2]);
+  const uint64_t x0 = (uint64_t)d0 | ((uint64_t)d1 << 32);
+  const uint64_t x1 = (uint64_t)d1 | ((uint64_t)d2 << 32);
+  const int sh = 4 * (int)(n & 7);
+  return (uint64_t)(uint32_t)(x0 >> sh) | ((uint64_t)(uint32_t)(x1 >> sh) << 32);
+}
+
+struct ObsList {
+  uint32_t *meta;   // off | c << 16 | ds << 20 | mine << 21
+  int64_t *nib;     // nibble index of the base in the sequence buffer
+  int *count;       // [0] entries, [1] overflow flag
+  __device__ __forceinline__ void add(int off, int c, int ds, bool mine, int64_t nib_index) {
+    const int k = atomicAdd(count, 1);
+    if (k < kObsCap) {
+      meta[k] = (uint32_t)off | ((uint32_t)c << 16) | ((uint32_t)ds << 20) | ((uint32_t)mine << 21);
+      nib[k] = nib_index;
+    } else {
+      count[1] = 1;
+    }
+  }
+};
+
+__device__ __forceinline__ void patch_nibble(uint8_t *out, int64_t nib_index, int from, int to) {
+  const int64_t byte = nib_index >> 1;
+  const int sh = 8 * (int)(byte & 3) + ((nib_index & 1) ? 0 : 4);
+  atomicXor(reinterpret_cast<uint32_t *>(out) + (byte >> 2), (uint32_t)(from ^ to) << sh);
+}
+
+// One observation of base c at position p (offset off in the table) of dataset ds.
+__device__ __forceinline__ bool observe(uint32_t *tab, ObsList &obs, int off, int c, int rc, int ds, bool mine,
+                                        int64_t nib_index) {
+  if (c == 15 || c == rc || !is_acgt(rc)) return false;
+  if (!is_acgt(c)) return true;                       // rare: 16-code re-run
+  atomicOr(&tab[off >> 2], (uint32_t)c << (ds * 4 + (off & 3) * 8));
+  obs.add(off, c, ds, mine, nib_index);
+  return false;
+}
+
+__global__ void __launch_bounds__(64) k_scope_v2(const DevBatch B, const int4 *__restrict__ inc_rec,
+                                                 const int32_t *__restrict__ list, int n, int cap,
+                                                 uint8_t *__restrict__ out, int32_t *scope_calls,
+                                                 int32_t *scope_bases, int32_t *rare_list, int32_t *rare_count) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  uint32_t *tab = smem;
+  int *m_start = reinterpret_cast<int *>(smem + cap / 4);
+  int *m_len = m_start + 64;
+  int *m_ds = m_len + 64;
+  int *m_mine = m_ds + 64;
+  int64_t *m_off = reinterpret_cast<int64_t *>(m_mine + 64);
+  ObsList obs;
+  obs.meta = reinterpret_cast<uint32_t *>(m_off + 64);
+  obs.nib = reinterpret_cast<int64_t *>(obs.meta + kObsCap);
+  obs.count = reinterpret_cast<int *>(obs.nib + kObsCap);
+  const int lane = threadIdx.x;
+  for (int li = blockIdx.x; li < n; li += gridDim.x) {
+    const int s = list[li];
+    const int a = B.span_start[s];
+    const int span = B.span_len[s];
+    const int b = a + span;
+    const int64_t rnib0 = B.ref_off[s] - a;            // nibble index of contig position 0
+    const GlobalRef refn{B.ref, rnib0};
+    uint4 *t4 = reinterpret_cast<uint4 *>(tab);
+    for (int k = lane; k < ((span + 15) >> 4); k += 64) t4[k] = make_uint4(0u, 0u, 0u, 0u);
+    if (lane < 2) obs.count[lane] = 0;
+    __syncthreads();
+    const int64_t i0 = B.incid_off[s], i1 = B.incid_off[s + 1];
+    bool rare = false;
+    for (int64_t c0 = i0; c0 < i1; c0 += 64) {
+      const int nh = (int)((i1 - c0) < 64 ? (i1 - c0) : 64);
+      int4 rec = make_int4(0, 0, 0, 0);
+      if (lane < nh) rec = inc_rec[c0 + lane];
+      const uint32_t fl = (uint32_t)rec.y;
+      const bool simple = (fl & kRecSimple) != 0;
+      const bool cplx = (fl & kRecCplx) != 0;
+      const uint64_t sm = __ballot(simple);
+      if (simple) {
+        const int idx = __popcll(sm & lanes_below(lane));
+        m_start[idx] = rec.x;
+        m_len[idx] = (int)(fl & 0xFFFFFF);
+        m_ds[idx] = (int)((fl >> 24) & 1);
+        m_mine[idx] = (fl & kRecMine) ? 1 : 0;
+        m_off[idx] = (int64_t)(((uint64_t)(uint32_t)rec.w << 32) | (uint32_t)rec.z);
+      }
+      __syncthreads();
+      const int ns = __popcll(sm);
+      for (int j0 = 0; j0 < ns; j0 += 4) {
+        const int j = j0 + (lane >> 4);
+        if (j >= ns) continue;
+        const int st = m_start[j], L = m_len[j], d = m_ds[j];
+        const bool mine = m_mine[j] != 0;
+        const int64_t snib = 2 * m_off[j];
+        for (int q0 = 16 * (lane & 15); q0 < L; q0 += 256) {
+          const uint64_t sv = load16(B.seq, snib + q0);
+          const uint64_t rv = load16(B.ref, rnib0 + st + q0);
+          const int nb = (L - q0) < 16 ? (L - q0) : 16;
+          // nibbles that differ from the reference (cheap pre-filter: usually none)
+          uint64_t diff = sv ^ rv;
+          diff = (diff | (diff >> 1) | (diff >> 2) | (diff >> 3)) & 0x1111111111111111ull;
+          if (nb < 16) diff &= (1ull << (4 * nb)) - 1;
+          while (diff) {
+            const int k = __builtin_ctzll(diff) >> 2;
+            diff &= diff - 1;
+            const int c = (int)((sv >> (4 * k)) & 15);
+            const int rc = (int)((rv >> (4 * k)) & 15);
+            rare |= observe(tab, obs, st + q0 + k - a, c, rc, d, mine, snib + q0 + k);
+          }
+        }
+      }
+      uint64_t cm = __ballot(cplx);
+      while (cm) {
+        const int l = __ffsll((unsigned long long)cm) - 1;
+        cm &= cm - 1;
+        const int r = __shfl(rec.x, l);
+        const bool mine = (__shfl((int)fl, l) & kRecMine) != 0;
+        const int L = B.read_len[r];
+        const int ds = B.dataset[r];
+        const int64_t snib = 2 * B.seq_off[r];
+        CigarCursor cur;
+        cur.init(B.cigar + B.cig_off[r], B.n_cig[r], B.ref_start[r]);
+        for (int q = lane; q < L; q += 64) {
+          const int p = cur.ref_of(q);
+          if (p < a || p >= b) continue;
+          rare |= observe(tab, obs, p - a, nib_at(B.seq, snib + q), refn(p), ds, mine, snib + q);
+        }
+      }
+      __syncthreads();
+    }
+    clear_keep<1>(B, s, a, b, tab);
+    __syncthreads();
+    int calls = 0;
+    for (int k = lane; k < ((span + 3) >> 2); k += 64) {
+      const uint32_t w = tab[k];
+      calls += __popc(w & (w >> 4) & 0x0F0F0F0Fu);
+    }
+    int bases = 0;
+    const int n_obs = obs.count[0] < kObsCap ? obs.count[0] : kObsCap;
+    if (!obs.count[1]) {
+      for (int e = lane; e < n_obs; e += 64) {
+        const uint32_t m = obs.meta[e];
+        if (!(m & (1u << 21))) continue;
+        const int off = (int)(m & 0xFFFF), c = (int)((m >> 16) & 15);
+        const uint32_t t = (tab[off >> 2] >> ((off & 3) * 8)) & 0xFF;
+        if (t & (t >> 4) & (uint32_t)c) {
+          patch_nibble(out, obs.nib[e], c, refn(a + off));
+          ++bases;
+        }
+      }
+    } else {
+      // more mismatches than the list holds: walk the reads this scope writes again
+      for (int64_t i = i0; i < i1; ++i) {
+        const int4 rec = inc_rec[i];
+        if (!(rec.y & kRecMine)) continue;
+        const int r = B.incid_read[i];
+        const int L = B.read_len[r];
+        const int64_t snib = 2 * B.seq_off[r];
+        CigarCursor cur;
+        cur.init(B.cigar + B.cig_off[r], B.n_cig[r], B.ref_start[r]);
+        for (int q = lane; q < L; q += 64) {
+          const int p = cur.ref_of(q);
+          if (p < a || p >= b) continue;
+          const int c = nib_at(B.seq, snib + q);
+          const int off = p - a;
+          const uint32_t t = (tab[off >> 2] >> ((off & 3) * 8)) & 0xFF;
+          if (is_acgt(c) && (t & (t >> 4) & (uint32_t)c)) {
+            patch_nibble(out, snib + q, c, refn(p));
+            ++bases;
+          }
+        }
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      calls += __shfl_xor(calls, o);
+      bases += __shfl_xor(bases, o);
+    }
+    const bool any_rare = __ballot(rare) != 0;
+    if (lane == 0) {
+      scope_calls[s] = calls;
+      scope_bases[s] = bases;
+      if (any_rare) rare_list[atomicAdd(rare_count, 1)] = s;
+    }
+    __syncthreads();
+  }
+}
+
+size_t v2_lds_bytes(int cap) {
+  return (size_t)cap + 64 * (4 * 4 + 8) + kObsCap * (4 + 8) + 16;
+}
+
 // One workgroup per 16 Ki-position tile of a large scope: tally -> TN table (global).
 template <int TB>
 __global__ void __launch_bounds__(kBlock) k_tile_large(const DevBatch B, const Tile *__restrict__ tiles,
@@ -638,6 +844,7 @@ struct ganon_dbatch {
   int32_t n_large_scopes = 0;
   int32_t *rare_small_list = nullptr, *rare_tile_list = nullptr;
   int32_t max_small_span = 0;
+  int4 *inc_rec = nullptr;      // per incidence, scope-major: {start|read, len|flags, seq_off lo, hi}
   bool ran = false;
 };
 
@@ -663,7 +870,9 @@ int fail(ganon_ctx *ctx, int code, const char *fmt, ...) {
 template <typename T>
 int dev_alloc(ganon_ctx *ctx, ganon_dbatch *db, T **p, size_t count) {
   *p = nullptr;
-  size_t bytes = std::max<size_t>(count, 1) * sizeof(T);
+  // +16 bytes: load16() reads up to 12 bytes past a buffer's last nibble, and the patch
+  // atomics touch whole dwords
+  size_t bytes = std::max<size_t>(count, 1) * sizeof(T) + 16;
   hipError_t e = hipMalloc(reinterpret_cast<void **>(p), bytes);
   if (e != hipSuccess) return fail(ctx, GANON_E_NOMEM, "hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
   db->allocs.push_back(*p);
@@ -784,7 +993,7 @@ GANON_API int ganon_ctx_set_stream(ganon_ctx *ctx, void *hip_stream) {
 }
 
 GANON_API int ganon_ctx_set_variant(ganon_ctx *ctx, int variant) {
-  if (!ctx || variant < GANON_VARIANT_DEFAULT || variant > GANON_VARIANT_BLOCK)
+  if (!ctx || variant < GANON_VARIANT_DEFAULT || variant > GANON_VARIANT_WAVE)
     return fail(ctx, GANON_E_ARG, "unknown kernel variant %d", variant);
   ctx->variant = variant;
   return GANON_OK;
@@ -968,6 +1177,31 @@ GANON_API int ganon_batch_upload(ganon_ctx *ctx, const ganon_batch *b, ganon_dba
   db->n_large_written = (int32_t)large_written.size();
   db->n_large_scopes = (int32_t)large_scopes.size();
   db->max_small_span = max_small;
+  {
+    // per-incidence records for the v2 scope kernel (scope-major, one int4 each)
+    std::vector<int4> rec((size_t)b->n_incid);
+    for (int32_t s = 0; s < b->n_scopes; ++s) {
+      for (int64_t i = b->scope_incid_off[s]; i < b->scope_incid_off[s + 1]; ++i) {
+        const int32_t r = b->incid_read[i];
+        const int32_t L = b->read_len[r];
+        bool simple = false;
+        if (b->n_cig[r] == 1) {
+          const uint32_t w = b->cigar[b->cig_off[r]];
+          const int op = w & 0xF;
+          simple = (op == 0 || op == 7 || op == 8) && (int64_t)(w >> 4) == L && L > 0;
+        }
+        const bool cplx = !simple && b->n_cig[r] > 0 && L > 0;
+        if (L >= (1 << 24)) return bail(fail(ctx, GANON_E_ARG, "read %d longer than 16 Mb", r));
+        uint32_t fl = (uint32_t)L | ((uint32_t)b->dataset[r] << 24);
+        if (simple) fl |= kRecSimple;
+        if (cplx) fl |= kRecCplx;
+        if (b->write_scope[r] == s) fl |= kRecMine;
+        const uint64_t so = (uint64_t)b->seq_off[r];
+        rec[i] = make_int4(simple ? b->ref_start[r] : r, (int)fl, (int)(uint32_t)so, (int)(uint32_t)(so >> 32));
+      }
+    }
+    if ((rc = dev_copy(ctx, db, &db->inc_rec, rec.data(), rec.size()))) return bail(rc);
+  }
   if ((rc = dev_alloc(ctx, db, &db->out, (size_t)b->seq_bytes))) return bail(rc);
   if ((rc = dev_alloc(ctx, db, &db->scope_calls, (size_t)b->n_scopes))) return bail(rc);
   if ((rc = dev_alloc(ctx, db, &db->scope_bases, (size_t)b->n_scopes))) return bail(rc);
@@ -1010,7 +1244,12 @@ GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
     HIP_OR_FAIL(hipMemsetAsync(db->scope_calls, 0, (size_t)db->n_scopes * sizeof(int32_t), st));
     HIP_OR_FAIL(hipMemsetAsync(db->scope_bases, 0, (size_t)db->n_scopes * sizeof(int32_t), st));
   }
-  if (db->n_pt) {
+  const bool v2 = ctx->variant == GANON_VARIANT_DEFAULT;
+  if (v2) {
+    // copy-then-patch: every read's bytes first, the scope kernels patch masked nibbles
+    KernelScope ks(ctx, "copy_seq");
+    if (db->seq_bytes) HIP_OR_FAIL(hipMemcpyAsync(db->out, B.seq, (size_t)db->seq_bytes, hipMemcpyDeviceToDevice, st));
+  } else if (db->n_pt) {
     KernelScope ks(ctx, "k_passthrough");
     const int grid = std::min<int>((db->n_pt + kWaves - 1) / kWaves, 8192);
     k_passthrough<<<grid, kBlock, 0, st>>>(B, db->pt_list, db->n_pt, db->out);
@@ -1019,7 +1258,13 @@ GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
   const int caps[2] = {kSmallCap0, kSmallCap1};
   for (int k = 0; k < 2; ++k) {
     if (!db->n_small[k]) continue;
-    if (ctx->variant == GANON_VARIANT_BLOCK) {
+    if (v2) {
+      KernelScope ks(ctx, k == 0 ? "k_scope_v2/2.5K" : "k_scope_v2/16K");
+      k_scope_v2<<<db->n_small[k], 64, v2_lds_bytes(caps[k]), st>>>(
+          B, db->inc_rec, db->small_list[k], db->n_small[k], caps[k], db->out, db->scope_calls, db->scope_bases,
+          db->rare_small_list, db->counters + 0);
+      if ((rc = check_launch(ctx, "k_scope_v2"))) return rc;
+    } else if (ctx->variant == GANON_VARIANT_BLOCK) {
       KernelScope ks(ctx, k == 0 ? "k_scope_small<1>/2.5K" : "k_scope_small<1>/16K");
       k_scope_small<1><<<db->n_small[k], kBlock, small_lds_bytes(1, caps[k]), st>>>(
           B, db->small_list[k], db->n_small[k], nullptr, caps[k], db->out, db->scope_calls, db->scope_bases,

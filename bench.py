@@ -180,9 +180,9 @@ def main() -> None:
     ab = None
     if args.ab:
         # interleaved rounds in one process (cdna_hip_programming.md §5.4 rule 24)
-        samples = {0: [], 1: [], 2: []}
+        samples = {0: [], 1: [], 2: [], 3: []}
         for _ in range(5):
-            for v in (0, 1, 2):
+            for v in (0, 1, 2, 3):
                 masker.set_variant(v)
                 db.run()
                 torch.cuda.synchronize()
@@ -192,7 +192,7 @@ def main() -> None:
                 torch.cuda.synchronize()
                 samples[v].append((time.perf_counter() - t) / args.steps * 1e3)
         masker.set_variant(args.variant)
-        ab = {("v2_copy_patch", "v0_block", "v1_wave")[v]: {"median_ms": round(float(np.median(x)), 4),
+        ab = {("v3_persistent", "v0_block", "v1_wave", "v2_copy_patch")[v]: {"median_ms": round(float(np.median(x)), 4),
                                                 "min_ms": round(float(np.min(x)), 4)} for v, x in samples.items()}
     totals = db.totals()
     batch_info = db.info()

@@ -511,9 +511,10 @@ struct ObsList {
   uint32_t *meta;   // off | c << 16 | ds << 20 | mine << 21
   int64_t *nib;     // nibble index of the base in the sequence buffer
   int *count;       // [0] entries, [1] overflow flag
+  int cap = kObsCap;
   __device__ __forceinline__ void add(int off, int c, int ds, bool mine, int64_t nib_index) {
     const int k = atomicAdd(count, 1);
-    if (k < kObsCap) {
+    if (k < cap) {
       meta[k] = (uint32_t)off | ((uint32_t)c << 16) | ((uint32_t)ds << 20) | ((uint32_t)mine << 21);
       nib[k] = nib_index;
     } else {
@@ -688,6 +689,199 @@ size_t v2_lds_bytes(int cap) {
   return (size_t)cap + 64 * (4 * 4 + 8) + kObsCap * (4 + 8) + 16;
 }
 
+// ---- v3: persistent waves ------------------------------------------------------------------
+// v2's algorithm with the latency chain cut down: 256-thread workgroups whose four waves
+// work independently (wave-level sync only), a persistent grid in which every wave walks
+// its own stream of scopes and prefetches the next scope's 48-byte record while it works
+// on the current one, and simple reads spread over the lanes chunk by chunk (16 bases per
+// lane, chunk -> read by binary search over an LDS prefix array) so six 150 bp reads fill
+// one 64-lane pass. LDS per wave stays under 5 KB for the 2.5 K class (32 waves per CU).
+constexpr int kV3Obs = 96;
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__host__ __device__ inline size_t v3_wave_lds_bytes(int cap) {
+  return (size_t)cap + 64 * 16 + 68 * 4 + kV3Obs * (4 + 8) + 16;
+}
+
+__device__ __forceinline__ int64_t i64_of(int lo, int hi) {
+  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+__global__ void __launch_bounds__(256) k_scope_v3(const DevBatch B, const int4 *__restrict__ srec, int n, int cap,
+                                                  const int4 *__restrict__ inc_rec, uint8_t *__restrict__ out,
+                                                  int32_t *scope_calls, int32_t *scope_bases, int32_t *rare_list,
+                                                  int32_t *rare_count) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  // wave index made provably wave-uniform: scope records then live in SGPRs (s_load)
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  uint32_t *base = smem + wave * (v3_wave_lds_bytes(cap) / 4);
+  uint32_t *tab = base;
+  int4 *mrec = reinterpret_cast<int4 *>(base + cap / 4);
+  int *mcs = reinterpret_cast<int *>(mrec + 64);
+  ObsList obs;
+  obs.meta = reinterpret_cast<uint32_t *>(mcs + 68);
+  obs.nib = reinterpret_cast<int64_t *>(obs.meta + kV3Obs);
+  obs.count = reinterpret_cast<int *>(obs.nib + kV3Obs);
+  obs.cap = kV3Obs;
+  const int nw = gridDim.x * 4;
+  int li = blockIdx.x * 4 + wave;
+  int4 ra = make_int4(0, 0, 0, 0), rb = ra, rc = ra;
+  if (li < n) {
+    ra = srec[3 * li];
+    rb = srec[3 * li + 1];
+    rc = srec[3 * li + 2];
+  }
+  while (li < n) {
+    const int nli = li + nw;
+    int4 na = make_int4(0, 0, 0, 0), nb = na, nc = na;
+    if (nli < n) {                                   // prefetch the next scope's record
+      na = srec[3 * nli];
+      nb = srec[3 * nli + 1];
+      nc = srec[3 * nli + 2];
+    }
+    const int s = ra.x, a = ra.y, span = ra.z, keep_pos = ra.w;
+    const int64_t i0 = i64_of(rb.x, rb.y);
+    const int ninc = rb.z, keep_code = rb.w;
+    const int64_t rnib0 = i64_of(rc.x, rc.y);      // nibble index of contig position 0
+    const int b = a + span;
+    const GlobalRef refn{B.ref, rnib0};
+    uint4 *t4 = reinterpret_cast<uint4 *>(tab);
+    for (int k = lane; k < ((span + 15) >> 4); k += 64) t4[k] = make_uint4(0u, 0u, 0u, 0u);
+    if (lane < 2) obs.count[lane] = 0;
+    wave_sync();
+    bool rare = false;
+    for (int c0 = 0; c0 < ninc; c0 += 64) {
+      const int nh = (ninc - c0) < 64 ? (ninc - c0) : 64;
+      int4 rec = make_int4(0, 0, 0, 0);
+      if (lane < nh) rec = inc_rec[i0 + c0 + lane];
+      const uint32_t fl = (uint32_t)rec.y;
+      const bool simple = (fl & kRecSimple) != 0;
+      const bool cplx = (fl & kRecCplx) != 0;
+      const int nck = simple ? (int)(((fl & 0xFFFFFF) + 15) >> 4) : 0;
+      int incl = nck;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(incl, o);
+        if (lane >= o) incl += t;
+      }
+      const int total = __shfl(incl, 63);
+      mrec[lane] = rec;
+      mcs[lane] = incl - nck;
+      wave_sync();
+      for (int t = lane; t < total; t += 64) {
+        int lo = 0, hi = 63;                         // largest j with mcs[j] <= t
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (mcs[mid] <= t) lo = mid;
+          else hi = mid - 1;
+        }
+        const int4 r = mrec[lo];
+        const int q0 = 16 * (t - mcs[lo]);
+        const uint32_t rf = (uint32_t)r.y;
+        const int L = (int)(rf & 0xFFFFFF), d = (int)((rf >> 24) & 1);
+        const bool mine = (rf & kRecMine) != 0;
+        const int64_t snib = 2 * i64_of(r.z, r.w);
+        const uint64_t sv = load16(B.seq, snib + q0);
+        const uint64_t rv = load16(B.ref, rnib0 + r.x + q0);
+        const int nbase = (L - q0) < 16 ? (L - q0) : 16;
+        uint64_t diff = sv ^ rv;
+        diff = (diff | (diff >> 1) | (diff >> 2) | (diff >> 3)) & 0x1111111111111111ull;
+        if (nbase < 16) diff &= (1ull << (4 * nbase)) - 1;
+        while (diff) {
+          const int k = __builtin_ctzll(diff) >> 2;
+          diff &= diff - 1;
+          rare |= observe(tab, obs, r.x + q0 + k - a, (int)((sv >> (4 * k)) & 15), (int)((rv >> (4 * k)) & 15), d,
+                          mine, snib + q0 + k);
+        }
+      }
+      uint64_t cm = __ballot(cplx);
+      while (cm) {
+        const int l = __ffsll((unsigned long long)cm) - 1;
+        cm &= cm - 1;
+        const int r = __shfl(rec.x, l);
+        const bool mine = (__shfl((int)fl, l) & kRecMine) != 0;
+        const int L = B.read_len[r];
+        const int ds = B.dataset[r];
+        const int64_t snib = 2 * B.seq_off[r];
+        CigarCursor cur;
+        cur.init(B.cigar + B.cig_off[r], B.n_cig[r], B.ref_start[r]);
+        for (int q = lane; q < L; q += 64) {
+          const int p = cur.ref_of(q);
+          if (p < a || p >= b) continue;
+          rare |= observe(tab, obs, p - a, nib_at(B.seq, snib + q), refn(p), ds, mine, snib + q);
+        }
+      }
+      wave_sync();
+    }
+    if (lane == 0 && keep_pos >= a && keep_pos < b && is_acgt(keep_code)) {
+      const int off = keep_pos - a;
+      atomicAnd(&tab[off >> 2], ~((uint32_t)keep_code << ((off & 3) * 8)));
+    }
+    wave_sync();
+    int calls = 0;
+    for (int k = lane; k < ((span + 3) >> 2); k += 64) {
+      const uint32_t w = tab[k];
+      calls += __popc(w & (w >> 4) & 0x0F0F0F0Fu);
+    }
+    int bases = 0;
+    const int n_obs = obs.count[0] < kV3Obs ? obs.count[0] : kV3Obs;
+    if (obs.count[0] <= kV3Obs) {
+      for (int e = lane; e < n_obs; e += 64) {
+        const uint32_t m = obs.meta[e];
+        if (!(m & (1u << 21))) continue;
+        const int off = (int)(m & 0xFFFF), c = (int)((m >> 16) & 15);
+        const uint32_t t = (tab[off >> 2] >> ((off & 3) * 8)) & 0xFF;
+        if (t & (t >> 4) & (uint32_t)c) {
+          patch_nibble(out, obs.nib[e], c, refn(a + off));
+          ++bases;
+        }
+      }
+    } else {
+      // more mismatches than the list holds: walk the reads this scope writes again
+      for (int64_t i = i0; i < i0 + ninc; ++i) {
+        const int4 rec = inc_rec[i];
+        if (!(rec.y & kRecMine)) continue;
+        const int r = B.incid_read[i];
+        const int L = B.read_len[r];
+        const int64_t snib = 2 * B.seq_off[r];
+        CigarCursor cur;
+        cur.init(B.cigar + B.cig_off[r], B.n_cig[r], B.ref_start[r]);
+        for (int q = lane; q < L; q += 64) {
+          const int p = cur.ref_of(q);
+          if (p < a || p >= b) continue;
+          const int c = nib_at(B.seq, snib + q);
+          const int off = p - a;
+          const uint32_t t = (tab[off >> 2] >> ((off & 3) * 8)) & 0xFF;
+          if (is_acgt(c) && (t & (t >> 4) & (uint32_t)c)) {
+            patch_nibble(out, snib + q, c, refn(p));
+            ++bases;
+          }
+        }
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      calls += __shfl_xor(calls, o);
+      bases += __shfl_xor(bases, o);
+    }
+    const bool any_rare = __ballot(rare) != 0;
+    if (lane == 0) {
+      scope_calls[s] = calls;
+      scope_bases[s] = bases;
+      if (any_rare) rare_list[atomicAdd(rare_count, 1)] = s;
+    }
+    wave_sync();
+    ra = na;
+    rb = nb;
+    rc = nc;
+    li = nli;
+  }
+}
+
 // One workgroup per 16 Ki-position tile of a large scope: tally -> TN table (global).
 template <int TB>
 __global__ void __launch_bounds__(kBlock) k_tile_large(const DevBatch B, const Tile *__restrict__ tiles,
@@ -813,6 +1007,7 @@ struct ganon_ctx {
   hipStream_t stream = nullptr;
   bool profiling = false;
   int variant = GANON_VARIANT_DEFAULT;
+  int v3_blocks[2] = {1, 1};   // resident grid of k_scope_v3 per class (occupancy x CUs)
   std::string err;
   struct Rec { std::string name; hipEvent_t e0, e1; };
   std::vector<Rec> recs;
@@ -845,6 +1040,7 @@ struct ganon_dbatch {
   int32_t *rare_small_list = nullptr, *rare_tile_list = nullptr;
   int32_t max_small_span = 0;
   int4 *inc_rec = nullptr;      // per incidence, scope-major: {start|read, len|flags, seq_off lo, hi}
+  int4 *srec[2] = {nullptr, nullptr};   // per small scope of each class: 3 x int4 (k_scope_v3)
   bool ran = false;
 };
 
@@ -964,6 +1160,18 @@ GANON_API int ganon_ctx_create(int device, ganon_ctx **out) {
                       (int)tile_lds_bytes(1));
   hipFuncSetAttribute(reinterpret_cast<const void *>(k_tile_large<4>), hipFuncAttributeMaxDynamicSharedMemorySize,
                       (int)tile_lds_bytes(4));
+  hipFuncSetAttribute(reinterpret_cast<const void *>(k_scope_v3), hipFuncAttributeMaxDynamicSharedMemorySize,
+                      (int)(4 * v3_wave_lds_bytes(kSmallCap1)));
+  // persistent grid of k_scope_v3: every resident workgroup slot, no more
+  const int caps[2] = {kSmallCap0, kSmallCap1};
+  for (int k = 0; k < 2; ++k) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_scope_v3, kBlock, 4 * v3_wave_lds_bytes(caps[k])) !=
+            hipSuccess ||
+        per_cu < 1)
+      per_cu = 1;
+    ctx->v3_blocks[k] = per_cu * prop.multiProcessorCount;
+  }
   *out = ctx;
   return GANON_OK;
 }
@@ -993,7 +1201,7 @@ GANON_API int ganon_ctx_set_stream(ganon_ctx *ctx, void *hip_stream) {
 }
 
 GANON_API int ganon_ctx_set_variant(ganon_ctx *ctx, int variant) {
-  if (!ctx || variant < GANON_VARIANT_DEFAULT || variant > GANON_VARIANT_WAVE)
+  if (!ctx || variant < GANON_VARIANT_DEFAULT || variant > GANON_VARIANT_COPYPATCH)
     return fail(ctx, GANON_E_ARG, "unknown kernel variant %d", variant);
   ctx->variant = variant;
   return GANON_OK;
@@ -1201,6 +1409,20 @@ GANON_API int ganon_batch_upload(ganon_ctx *ctx, const ganon_batch *b, ganon_dba
       }
     }
     if ((rc = dev_copy(ctx, db, &db->inc_rec, rec.data(), rec.size()))) return bail(rc);
+    for (int k = 0; k < 2; ++k) {
+      std::vector<int4> sr(3 * small[k].size());
+      for (size_t j = 0; j < small[k].size(); ++j) {
+        const int32_t s = small[k][j];
+        const int64_t i0 = b->scope_incid_off[s];
+        const int64_t ni = b->scope_incid_off[s + 1] - i0;
+        if (ni >= INT32_MAX) return bail(fail(ctx, GANON_E_ARG, "scope %d has too many reads", s));
+        const int64_t nib0 = b->scope_ref_off[s] - b->scope_span_start[s];
+        sr[3 * j] = make_int4(s, b->scope_span_start[s], b->scope_span_len[s], b->keep_pos[s]);
+        sr[3 * j + 1] = make_int4((int)(uint32_t)i0, (int)(uint32_t)((uint64_t)i0 >> 32), (int)ni, b->keep_code[s]);
+        sr[3 * j + 2] = make_int4((int)(uint32_t)nib0, (int)(uint32_t)((uint64_t)nib0 >> 32), 0, 0);
+      }
+      if ((rc = dev_copy(ctx, db, &db->srec[k], sr.data(), sr.size()))) return bail(rc);
+    }
   }
   if ((rc = dev_alloc(ctx, db, &db->out, (size_t)b->seq_bytes))) return bail(rc);
   if ((rc = dev_alloc(ctx, db, &db->scope_calls, (size_t)b->n_scopes))) return bail(rc);
@@ -1244,8 +1466,9 @@ GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
     HIP_OR_FAIL(hipMemsetAsync(db->scope_calls, 0, (size_t)db->n_scopes * sizeof(int32_t), st));
     HIP_OR_FAIL(hipMemsetAsync(db->scope_bases, 0, (size_t)db->n_scopes * sizeof(int32_t), st));
   }
-  const bool v2 = ctx->variant == GANON_VARIANT_DEFAULT;
-  if (v2) {
+  const bool v3 = ctx->variant == GANON_VARIANT_DEFAULT;
+  const bool v2 = ctx->variant == GANON_VARIANT_COPYPATCH;
+  if (v2 || v3) {
     // copy-then-patch: every read's bytes first, the scope kernels patch masked nibbles
     KernelScope ks(ctx, "copy_seq");
     if (db->seq_bytes) HIP_OR_FAIL(hipMemcpyAsync(db->out, B.seq, (size_t)db->seq_bytes, hipMemcpyDeviceToDevice, st));
@@ -1258,7 +1481,15 @@ GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
   const int caps[2] = {kSmallCap0, kSmallCap1};
   for (int k = 0; k < 2; ++k) {
     if (!db->n_small[k]) continue;
-    if (v2) {
+    if (v3) {
+      KernelScope ks(ctx, k == 0 ? "k_scope_v3/2.5K" : "k_scope_v3/16K");
+      const size_t lds = 4 * v3_wave_lds_bytes(caps[k]);
+      const int grid = std::max(1, std::min((db->n_small[k] + 3) / 4, ctx->v3_blocks[k]));
+      k_scope_v3<<<grid, kBlock, lds, st>>>(B, db->srec[k], db->n_small[k], caps[k], db->inc_rec, db->out,
+                                            db->scope_calls, db->scope_bases, db->rare_small_list,
+                                            db->counters + 0);
+      if ((rc = check_launch(ctx, "k_scope_v3"))) return rc;
+    } else if (v2) {
       KernelScope ks(ctx, k == 0 ? "k_scope_v2/2.5K" : "k_scope_v2/16K");
       k_scope_v2<<<db->n_small[k], 64, v2_lds_bytes(caps[k]), st>>>(
           B, db->inc_rec, db->small_list[k], db->n_small[k], caps[k], db->out, db->scope_calls, db->scope_bases,

@@ -72,11 +72,11 @@ def test_block_variant_matches_wave_variant(masker, seed):
     arr = random_batch(seed, n_scopes=40, rare_frac=0.1, wide_scopes=1) if seed != 23 else \
         config2_batch(n_reads=300_000, genome=90_000_000, n_windows=30_000, n_germline=60_000)[0]
     res = []
-    for v in (0, 1, 2):
+    for v in (0, 1, 2, 3):
         masker.set_variant(v)
         res.append(masker.mask(arr))
     masker.set_variant(0)
-    for v in (1, 2):
+    for v in (1, 2, 3):
         for k in range(3):
             assert np.array_equal(res[0][k], res[v][k]), (v, k)
 

@@ -45,12 +45,15 @@ def kernel_class(name: str) -> str:
     return ""
 
 
-def kernel_bytes(arr) -> dict:
+def kernel_bytes(arr, copy_patch: bool = True) -> dict:
     """Algorithmic bytes per launch of each kernel (SURVEY §8(d) per-unit figures).
 
-    Per read: ceil(L/2) in + ceil(L/2) out + 4*n_cigar + 16, charged to the kernel that
-    writes the read; each further scope incidence ceil(L/2) + 4*n_cigar + 8, charged to
-    that scope's kernel; each scope ceil(span/2) of reference, charged to its kernel."""
+    Per read: ceil(L/2) in + ceil(L/2) out + 4*n_cigar + 16; each further scope incidence
+    ceil(L/2) + 4*n_cigar + 8; each scope ceil(span/2) of reference. Attribution: with
+    copy-then-patch (default variant) the device copy owns every read's in + out bytes and
+    the scope kernel of the read's write scope owns its 4*n_cigar + 16; otherwise the
+    kernel that writes a read owns all of its bytes. Extra incidences and the reference
+    bytes go to the kernel of their scope. The per-kernel figures sum to the formula."""
     L = arr["read_len"].astype(np.int64)
     h = (L + 1) // 2
     nc = arr["n_cig"].astype(np.int64)
@@ -60,8 +63,12 @@ def kernel_bytes(arr) -> dict:
     out = {n: 0 for n in names}
     out["k_passthrough"] = 0
     ws = arr["write_scope"].astype(np.int64)
-    base = 2 * h + 4 * nc + 16
     wcls = np.where(ws >= 0, cls[np.maximum(ws, 0)], 3)
+    if copy_patch:
+        out["k_passthrough"] += int((2 * h).sum())
+        base = 4 * nc + 16
+    else:
+        base = 2 * h + 4 * nc + 16
     for k, n in enumerate(names + ["k_passthrough"]):
         out[n] += int(base[wcls == k].sum())
     offs = arr["scope_incid_off"]
@@ -205,7 +212,7 @@ def main() -> None:
         job_totals = totals
     db.free()
 
-    kb = kernel_bytes(arr)
+    kb = kernel_bytes(arr, copy_patch=args.variant in (0, 3))
     per_kernel = {n: {"launches": c, "avg_ms": ms / c} for n, (c, ms) in ktimes.items()}
     dom = max(per_kernel, key=lambda n: per_kernel[n]["avg_ms"] * per_kernel[n]["launches"])
     dom_bytes = kb.get(kernel_class(dom), 0)

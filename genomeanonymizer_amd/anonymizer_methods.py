@@ -39,13 +39,17 @@ class MaskResult:
     arrays: dict                           # the device batch (kept for tests/bench)
 
 
-def build_batch(plan: Plan, tables: Tuple[ReadTable, ReadTable], fasta: FastaRef) -> Tuple[dict, dict]:
-    """Lay the plan's scopes out as one ganon_batch (include/ganon.h)."""
+def build_batch(plan: Plan, tables: Tuple[ReadTable, ReadTable], fasta: FastaRef,
+                scope_ids=None) -> Tuple[dict, dict]:
+    """Lay the plan's scopes (all, or the subset ``scope_ids`` of one contig shard) out as
+    one ganon_batch (include/ganon.h). Batch scope k is plan scope ``meta['scope_ids'][k]``."""
     T, N = tables
     packed, nib_off = fasta.packed()
+    scopes = plan.scopes if scope_ids is None else [plan.scopes[i] for i in scope_ids]
+    local = {sc.id: k for k, sc in enumerate(scopes)}
     # batch reads: every read of every scope, tumor rows then normal rows
     in_scope = [np.zeros(T.n, bool), np.zeros(N.n, bool)]
-    for sc in plan.scopes:
+    for sc in scopes:
         in_scope[0][sc.t_rows] = True
         in_scope[1][sc.n_rows] = True
     rows = [np.nonzero(in_scope[0])[0], np.nonzero(in_scope[1])[0]]
@@ -67,22 +71,22 @@ def build_batch(plan: Plan, tables: Tuple[ReadTable, ReadTable], fasta: FastaRef
     arr["dataset"] = np.concatenate([np.zeros(len(rows[0]), np.uint8), np.ones(len(rows[1]), np.uint8)])
     ws = np.full(n_reads, -1, np.int32)
     for ds, row, s in plan.written_instances():
-        if s >= 0:
-            ws[bidx[ds][row]] = s
+        if s >= 0 and s in local:
+            ws[bidx[ds][row]] = local[s]
     arr["write_scope"] = ws
-    counts = np.array([len(sc.t_rows) + len(sc.n_rows) for sc in plan.scopes], np.int64)
+    counts = np.array([len(sc.t_rows) + len(sc.n_rows) for sc in scopes], np.int64)
     arr["scope_incid_off"] = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
     arr["incid_read"] = (np.concatenate([np.concatenate([bidx[0][sc.t_rows], bidx[1][sc.n_rows]])
-                                         for sc in plan.scopes]).astype(np.int32)
-                         if plan.scopes else np.zeros(0, np.int32))
-    arr["scope_span_start"] = np.array([sc.span_start for sc in plan.scopes], np.int32)
-    arr["scope_span_len"] = np.array([sc.span_end - sc.span_start for sc in plan.scopes], np.int32)
-    arr["scope_ref_off"] = np.array([nib_off[sc.contig] + sc.span_start for sc in plan.scopes], np.int64)
+                                         for sc in scopes]).astype(np.int32)
+                         if scopes else np.zeros(0, np.int32))
+    arr["scope_span_start"] = np.array([sc.span_start for sc in scopes], np.int32)
+    arr["scope_span_len"] = np.array([sc.span_end - sc.span_start for sc in scopes], np.int32)
+    arr["scope_ref_off"] = np.array([nib_off[sc.contig] + sc.span_start for sc in scopes], np.int64)
     arr["ref_nt16"] = np.ascontiguousarray(packed)
-    keep = [kept_snv(sc.keep) if sc.is_variant_window else (-1, 0) for sc in plan.scopes]
+    keep = [kept_snv(sc.keep) if sc.is_variant_window else (-1, 0) for sc in scopes]
     arr["keep_pos"] = np.array([k[0] for k in keep], np.int32)
     arr["keep_code"] = np.array([k[1] for k in keep], np.uint8)
-    meta = {"bidx": bidx, "seq_base": seq_base}
+    meta = {"bidx": bidx, "seq_base": seq_base, "scope_ids": np.array([sc.id for sc in scopes], np.int64)}
     return arr, meta
 
 
@@ -103,11 +107,18 @@ class CompleteGermlineAnonymizer:
             self._engine = native.HipMasker(self.device)
         return self._engine
 
-    def anonymize(self, planner: SamplePlanner, plan: Plan) -> MaskResult:
+    def anonymize(self, planner: SamplePlanner, plan: Plan, scope_ids=None) -> MaskResult:
+        """Mask all scopes of ``plan`` (or the contig shard ``scope_ids``) in one device batch.
+        Per-scope counts come back indexed by plan scope id (zero outside the shard)."""
         tables = planner.tables
         fasta = planner.fasta
-        arrays, meta = build_batch(plan, tables, fasta)
-        out, calls, bases, totals = self.engine.mask(arrays)
+        arrays, meta = build_batch(plan, tables, fasta, scope_ids)
+        out, b_calls, b_bases, totals = self.engine.mask(arrays)
+        calls = np.zeros(len(plan.scopes), np.int32)
+        bases = np.zeros(len(plan.scopes), np.int32)
+        calls[meta["scope_ids"]] = b_calls
+        bases[meta["scope_ids"]] = b_bases
+        mine = set(meta["scope_ids"].tolist())
         # host indel path, only for scopes that contain a read with an I/D op
         written = {}
         for ds, row, s in plan.written_instances():
@@ -116,6 +127,8 @@ class CompleteGermlineAnonymizer:
         indel_counts: Dict[int, Dict[VariantType, int]] = {}
         leftovers: Dict[Tuple[int, int, int], list] = {}
         for sc in plan.scopes:
+            if sc.id not in mine:
+                continue
             if not any(has_indel_ops(tables[0], r) for r in sc.t_rows.tolist()) and \
                     not any(has_indel_ops(tables[1], r) for r in sc.n_rows.tolist()):
                 continue

@@ -1,0 +1,113 @@
+"""Command line, same flags as the reference (genome_anonymizer.py:16-112):
+
+  python -m genomeanonymizer_amd.genome_anonymizer -d DIR -s samples.tsv -r ref.fa \\
+      [-m complete_germline] [-c CPUS] [--record_statistics] [--enhanced_multiprocessing] [-v N]
+
+samples.tsv: tumor<TAB>normal<TAB>vcf per line, paths relative to DIR, '#' lines skipped.
+Outputs next to the inputs: re.sub('.bam|.sam|.cram', '.anonymized', path) + .1/.2.fastq
+(+ .single_end.fastq), and {normal_bam}.statistics.txt with --record_statistics.
+
+Multi-GPU: launch under ``torchrun --nproc-per-node N`` (or set WORLD_SIZE/RANK/LOCAL_RANK):
+contigs are sharded over the ranks (distributed.py); rank 0 writes the files.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import sys
+import time
+from argparse import ArgumentParser, BooleanOptionalAction
+from typing import List, Tuple
+
+from .anonymizer_methods import ANONYMIZER_ALGORITHMS, CompleteGermlineAnonymizer
+from .short_read_tumor_normal_anonymizer import name_output, run_short_read_tumor_normal_anonymizer
+
+COMPLETE_GERMLINE_ANONYMIZER_ALGORITHM = "complete_germline"
+
+
+def exec_parser(argv=None):
+    parser = ArgumentParser(prog="GenomeAnonymizer",
+                            description="Anonymization of sequencing data by removing germline variation "
+                                        "(MI355X build)")
+    parser.add_argument("-d", "--directory", type=str, required=True,
+                        help="Directory in which the tumor-normal sample pairs and the samples text file are stored")
+    parser.add_argument("-s", "--samples", type=str, required=True,
+                        help="Text file with the tumor, normal and vcf file names of each sample, tab separated")
+    parser.add_argument("-r", "--reference", type=str, required=True,
+                        help="reference genome to which the reads are mapped")
+    parser.add_argument("-m", "--method", type=str, required=False, default="complete_germline",
+                        choices=["complete_germline"],
+                        help="anonymization method: complete_germline masks all germline SNVs in the reads")
+    parser.add_argument("-c", "--cpu", type=int, required=False, default=1,
+                        help="Number of CPUs available (host BAM decode threads)")
+    parser.add_argument("--record_statistics", action=BooleanOptionalAction,
+                        help="Record statistics about the number of anonymized variants by region and type")
+    parser.add_argument("--enhanced_multiprocessing", action=BooleanOptionalAction,
+                        help="Accepted for compatibility; no effect (see SURVEY Q12)")
+    parser.add_argument("-v", "--verbose", type=int, required=False, default=2, help="Verbosity of logging")
+    parser.add_argument("--device", type=int, default=None, help="GPU index (default: LOCAL_RANK or 0)")
+    return parser.parse_args(argv)
+
+
+def join_dir_file(directory: str, param: str) -> str:
+    return "".join((directory, "/", param)) if not directory.endswith("/") else "".join((directory, param))
+
+
+def read_samples(path_to_samples: str, directory: str):
+    samples: List[Tuple[str, str]] = []
+    outputs: List[Tuple[str, str]] = []
+    vcfs: List[str] = []
+    with open(path_to_samples) as fh:
+        for line in fh:
+            if line.startswith("#"):
+                continue
+            f = line.strip().split("\t")
+            t, n, v = (join_dir_file(directory, x) for x in f[:3])
+            samples.append((t, n))
+            vcfs.append(v)
+            outputs.append((name_output(t), name_output(n)))
+    return vcfs, samples, outputs
+
+
+def run_anonymizer(argv=None) -> None:
+    config = exec_parser(argv)
+    logging.basicConfig(level=config.verbose * 10)
+    t0 = time.time()
+    logging.info("Beginning execution of GenomeAnonymizer (MI355X build)")
+    if config.method not in ANONYMIZER_ALGORITHMS:
+        logging.error("Anonymizer algorithm %s is not a valid option", config.method)
+        sys.exit(1)
+    vcfs, samples, outputs = read_samples(join_dir_file(config.directory, config.samples), config.directory)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    device = config.device if config.device is not None else local
+    anonymizer = CompleteGermlineAnonymizer(device=device)
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        from .distributed import anonymize_genome_sharded
+        from .io.fasta import FastaRef
+        from .io.vcf import read_vcf
+        from .planner import get_windows
+        torch.cuda.set_device(device)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        rank = dist.get_rank()
+        fa = FastaRef(config.reference)
+        for vcf, (t, n), (to, no) in zip(vcfs, samples, outputs):
+            windows = get_windows(read_vcf(vcf), fa.index)
+            work = os.path.join(os.path.dirname(os.path.abspath(no)), ".ganon_shards")
+            tot = anonymize_genome_sharded(windows, t, n, config.reference, to, no, bool(config.record_statistics),
+                                           rank, world, work, anonymizer, dist, threads=max(1, config.cpu))
+            if rank == 0:
+                logging.info("sample %s/%s totals %s", t, n, tot)
+        dist.destroy_process_group()
+    else:
+        run_short_read_tumor_normal_anonymizer(vcfs, samples, config.reference, anonymizer, outputs,
+                                               bool(config.record_statistics), config.cpu,
+                                               bool(config.enhanced_multiprocessing))
+    logging.info("Finished execution of GenomeAnonymizer successfully")
+    logging.debug("Total execution time: %s s", time.time() - t0)
+
+
+if __name__ == "__main__":
+    run_anonymizer()

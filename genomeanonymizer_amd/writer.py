@@ -212,8 +212,11 @@ def replay_io(io_log, rec_len, block: int) -> Dict[Tuple[int, int], list]:
 
 
 def io_block_size(directory: str) -> int:
-    """st_blksize CPython would use for a buffered file in ``directory``."""
+    """st_blksize CPython would use for a buffered file in ``directory`` (override with the
+    environment variable GANON_IO_BLOCK to reproduce files written on another filesystem)."""
     import os
+    if os.environ.get("GANON_IO_BLOCK"):
+        return int(os.environ["GANON_IO_BLOCK"])
     try:
         st = os.stat(directory).st_blksize
         return st if st > 1 else 8192

@@ -1,0 +1,73 @@
+"""The N>1 path (contig shards, one process per rank, totals all-reduce) on CPU with gloo:
+two ranks must write exactly the reference's files. The CPU oracle stands in for the GPU
+(test infrastructure); the GPU variant of this path is exercised by bench.py under torchrun."""
+import os
+import socket
+
+import pytest
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, name, workdir, policy, q):
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [repo, os.path.join(repo, "oracle"), os.path.join(repo, "tests")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from pyoracle import OracleEngine
+        from genomeanonymizer_amd.anonymizer_methods import CompleteGermlineAnonymizer
+        from genomeanonymizer_amd.distributed import anonymize_genome_sharded
+        from genomeanonymizer_amd.io.fasta import FastaRef
+        from genomeanonymizer_amd.io.vcf import read_vcf
+        from genomeanonymizer_amd.planner import get_windows
+        from genomeanonymizer_amd.short_read_tumor_normal_anonymizer import name_output
+        from genomeanonymizer_amd import writer
+        writer.io_block_size = lambda d: 4096
+        inp = os.path.join(workdir, "in")
+        paths = {"T": os.path.join(inp, "tumor.bam"), "N": os.path.join(inp, "normal.bam"),
+                 "ref": os.path.join(inp, "ref.fa"), "vcf": os.path.join(inp, "variants.vcf")}
+        fa = FastaRef(paths["ref"])
+        windows = get_windows(read_vcf(paths["vcf"]), fa.index)
+        tot = anonymize_genome_sharded(windows, paths["T"], paths["N"], paths["ref"], name_output(paths["T"]),
+                                       name_output(paths["N"]), True, rank, world, os.path.join(workdir, "shards"),
+                                       CompleteGermlineAnonymizer(engine=OracleEngine()), dist, policy)
+        q.put((rank, tot))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name,policy", [("edge", "lpt"), ("tiny", "round_robin")])
+def test_two_rank_contig_shards_match_reference(name, policy, tmp_path):
+    from helpers import GOLDEN, run_pipeline_vs_golden
+    from genomeanonymizer_amd.synth.generate import generate, scenario
+    import gzip
+    workdir = str(tmp_path / name)
+    paths = generate(scenario(name), os.path.join(workdir, "in"))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, name, workdir, policy, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(300)
+    assert all(p.exitcode == 0 for p in procs)
+    results = dict(q.get() for _ in range(2))
+    assert results[0] == results[1]            # totals are all-reduced
+    from genomeanonymizer_amd.short_read_tumor_normal_anonymizer import name_output
+    for tag, pre in (("tumor", name_output(paths["T"])), ("normal", name_output(paths["N"]))):
+        for suf in (".1.fastq", ".2.fastq", ".single_end.fastq"):
+            gp = os.path.join(GOLDEN, name, f"{tag}{suf}.gz")
+            if os.path.exists(gp):
+                assert open(pre + suf, "rb").read() == gzip.open(gp).read(), tag + suf
+    assert open(paths["N"] + ".statistics.txt").read() == open(os.path.join(GOLDEN, name, "normal.statistics.txt")).read()

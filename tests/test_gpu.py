@@ -101,6 +101,28 @@ def test_hip_pipeline_matches_reference(name, tmp_path, hip_built):
     assert bad == {}
 
 
+def test_cli_matches_reference(tmp_path, hip_built):
+    """python -m genomeanonymizer_amd.genome_anonymizer with the reference's flags."""
+    import gzip
+    import os
+    import subprocess
+    import sys
+    from helpers import GOLDEN, REPO
+    from genomeanonymizer_amd.synth.generate import generate, scenario
+    d = str(tmp_path / "cli")
+    paths = generate(scenario("edge"), d)
+    env = dict(os.environ, PYTHONPATH=REPO, GANON_IO_BLOCK="4096")   # the fixtures' st_blksize
+    r = subprocess.run([sys.executable, "-m", "genomeanonymizer_amd.genome_anonymizer", "-d", d, "-s", "samples.tsv",
+                        "-r", paths["ref"], "--record_statistics", "-c", "4"], env=env, capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    for tag, stem in (("tumor", "tumor"), ("normal", "normal")):
+        for suf in (".1.fastq", ".2.fastq", ".single_end.fastq"):
+            gp = os.path.join(GOLDEN, "edge", f"{tag}{suf}.gz")
+            assert open(os.path.join(d, f"{stem}.anonymized{suf}"), "rb").read() == gzip.open(gp).read()
+    assert open(paths["N"] + ".statistics.txt").read() == open(os.path.join(GOLDEN, "edge", "normal.statistics.txt")).read()
+
+
 def test_hip_config2_matches_oracle(masker, oracle):
     """BASELINE configs[1] layout at 2 M reads: every byte and count equal to the oracle."""
     from genomeanonymizer_amd.synth.batch import config2_batch

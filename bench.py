@@ -29,6 +29,7 @@ sys.path.insert(0, REPO)
 
 HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 SMALL_CAP0, SMALL_CAP1 = 2560, 16384    # scope classes of ganon_hip.hip (kSmallCap0/1)
+VARIANT_NAMES = {0: "v3_persistent", 1: "v0_block", 2: "v1_wave", 3: "v2_copy_patch", 4: "v4_group"}
 
 
 def kernel_class(name: str) -> str:
@@ -42,6 +43,8 @@ def kernel_class(name: str) -> str:
         return "small16K"
     if name.startswith("k_tile_large<1>") or name.startswith("k_mask_large"):
         return "large"
+    if name.startswith("k_group"):
+        return "group"
     return ""
 
 
@@ -87,6 +90,7 @@ def kernel_bytes(arr, copy_patch: bool = True) -> dict:
     for k, n in enumerate(names):
         out[n] += int(cost[extra & (cls[scope_of_inc] == k)].sum())
         out[n] += int(((span + 1) // 2)[cls == k].sum())
+    out["group"] = out["small2.5K"] + out["small16K"]    # k_group_v4 covers both classes
     return out
 
 
@@ -117,8 +121,9 @@ def main() -> None:
     ap.add_argument("--windows", type=int, default=1_000_000)
     ap.add_argument("--germline", type=int, default=1_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--variant", type=int, default=0, help="0 wave-per-scope (default), 1 block-per-scope")
-    ap.add_argument("--ab", action="store_true", help="also time the other small-scope variant, interleaved")
+    ap.add_argument("--variant", type=int, default=0,
+                    help="include/ganon.h GANON_VARIANT_*: 0 default, 1 block, 2 wave, 3 copy-patch, 4 group")
+    ap.add_argument("--ab", action="store_true", help="also time every small-scope variant, interleaved")
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_r01.json"),
                     help="PMC summary (tools/pmc_summary.py) for the traffic field, if present")
     args = ap.parse_args()
@@ -187,9 +192,9 @@ def main() -> None:
     ab = None
     if args.ab:
         # interleaved rounds in one process (cdna_hip_programming.md §5.4 rule 24)
-        samples = {0: [], 1: [], 2: [], 3: []}
+        samples = {v: [] for v in VARIANT_NAMES}
         for _ in range(5):
-            for v in (0, 1, 2, 3):
+            for v in VARIANT_NAMES:
                 masker.set_variant(v)
                 db.run()
                 torch.cuda.synchronize()
@@ -199,7 +204,7 @@ def main() -> None:
                 torch.cuda.synchronize()
                 samples[v].append((time.perf_counter() - t) / args.steps * 1e3)
         masker.set_variant(args.variant)
-        ab = {("v3_persistent", "v0_block", "v1_wave", "v2_copy_patch")[v]: {"median_ms": round(float(np.median(x)), 4),
+        ab = {VARIANT_NAMES[v]: {"median_ms": round(float(np.median(x)), 4),
                                                 "min_ms": round(float(np.min(x)), 4)} for v, x in samples.items()}
     totals = db.totals()
     batch_info = db.info()
@@ -212,7 +217,7 @@ def main() -> None:
         job_totals = totals
     db.free()
 
-    kb = kernel_bytes(arr, copy_patch=args.variant in (0, 3))
+    kb = kernel_bytes(arr, copy_patch=args.variant in (0, 3, 4))
     per_kernel = {n: {"launches": c, "avg_ms": ms / c} for n, (c, ms) in ktimes.items()}
     dom = max(per_kernel, key=lambda n: per_kernel[n]["avg_ms"] * per_kernel[n]["launches"])
     dom_bytes = kb.get(kernel_class(dom), 0)

@@ -882,6 +882,271 @@ __global__ void __launch_bounds__(256) k_scope_v3(const DevBatch B, const int4 *
   }
 }
 
+// ---- v4: scope groups, observation sort -------------------------------------------------
+// No per-scope table and no per-scope serialization. At upload every read of a small scope is
+// cut into segments (one per aligned M/=/X run: query nibble index, reference nibble index,
+// length) and consecutive scopes are packed into groups of ~kGrpTarget segments. One 256-thread
+// workgroup streams all 16-base chunks of all segments of its group at once (memory-level
+// parallelism across scopes instead of one scope at a time), and every base that differs from
+// an ACGT reference base becomes an observation in LDS:
+//   key = scope_local:12 | (pos - span_start):48 | allele:4
+//   payload = nibble index:48 | ref:4 | dataset:1 | mine:1
+// The list is sorted (bitonic, in LDS); a run of equal keys is one call (pos, allele) of one
+// scope, TN iff the run holds a tumor and a normal observation — the end state of the
+// reference's per-position state machine (variants.py:33-39) — and not the
+// window's kept variant. Run heads count the call and patch the run's observations in reads
+// the scope writes. All 16 codes are handled alike (no re-run). A group whose observations
+// overflow the list is re-scanned over halves of its observed key range; a single key that
+// overflows on its own (very deep coverage at one site) is resolved by a flags scan and a
+// patch scan.
+constexpr int kGrpThreads = 256;
+constexpr int kGrpTile = 256;        // segment records staged per tile
+constexpr int kGrpTarget = 256;      // segments per group (a larger scope forms its own group)
+constexpr int kGrpObs = 512;         // observations per LDS list
+constexpr int kGrpMaxScopes = 4096;  // scopes per group (12-bit local index)
+constexpr int kGrpStack = 80;        // key ranges pending (bisection depth <= 64)
+constexpr uint32_t kSegMine = 1u << 26;
+enum { kModeCollect = 0, kModeFlags = 1, kModePatch = 2 };
+
+struct GrpShared {
+  int4 rec[kGrpTile];               // {query nibble lo, hi, reference nibble lo, hi}
+  int2 rec2[kGrpTile];              // {length | dataset << 24 | mine << 26, scope_local}
+  int pre[kGrpTile];
+  int wsum[kGrpThreads / 64];
+  unsigned long long key[kGrpObs];
+  unsigned long long pay[kGrpObs];
+  unsigned long long stk_lo[kGrpStack], stk_hi[kGrpStack];
+  int stk_mode[kGrpStack];
+  unsigned long long kmin, kmax;
+  int top, n_obs, flags, masked;
+};
+
+struct GrpRange {
+  unsigned long long lo, hi;
+  int mode;
+};
+
+__device__ __forceinline__ void grp_observe(GrpShared &sh, const GrpRange &R, uint8_t *out, unsigned long long key,
+                                            int64_t nib, int c, int rc, int ds, bool mine) {
+  if (key < R.lo || key >= R.hi) return;
+  if (R.mode == kModeCollect) {
+    atomicMin(&sh.kmin, key);
+    atomicMax(&sh.kmax, key);
+    const int k = atomicAdd(&sh.n_obs, 1);
+    if (k < kGrpObs) {
+      sh.key[k] = key;
+      sh.pay[k] = (unsigned long long)nib | ((unsigned long long)rc << 48) | ((unsigned long long)ds << 52) |
+                  ((unsigned long long)(mine ? 1 : 0) << 53);
+    }
+  } else if (R.mode == kModeFlags) {
+    atomicOr(&sh.flags, 1 << ds);
+  } else if (mine) {
+    patch_nibble(out, nib, c, rc);
+    atomicAdd(&sh.masked, 1);
+  }
+}
+
+// Is (scope s, pos_off, allele c) the window's kept variant? (clear_keep's rule)
+__device__ __forceinline__ bool grp_kept(const DevBatch &B, int s, int64_t pos_off, int c) {
+  const int kp = B.keep_pos[s];
+  return kp >= 0 && B.keep_code[s] == c && (int64_t)kp - B.span_start[s] == pos_off;
+}
+
+// Stream every chunk of every segment of the group, feeding observations in range R.
+__device__ __forceinline__ void grp_scan(const DevBatch &B, GrpShared &sh, const GrpRange &R, int s_begin,
+                                         int64_t i_begin, int64_t i_end, const int4 *__restrict__ rec4,
+                                         const int2 *__restrict__ rec2, uint8_t *out) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int64_t c0 = i_begin; c0 < i_end; c0 += kGrpTile) {
+    const int nh = (int)((i_end - c0) < kGrpTile ? (i_end - c0) : kGrpTile);
+    int nck = 0;
+    if (tid < nh) {
+      const int4 r = rec4[c0 + tid];
+      const int2 r2 = rec2[c0 + tid];
+      sh.rec[tid] = r;
+      sh.rec2[tid] = r2;
+      nck = ((r2.x & 0xFFFFFF) + 15) >> 4;
+    }
+    int incl = nck;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int t = __shfl_up(incl, o);
+      if (lane >= o) incl += t;
+    }
+    if (lane == 63) sh.wsum[wave] = incl;
+    __syncthreads();
+    int wbase = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < kGrpThreads / 64; ++w) {
+      const int v = sh.wsum[w];
+      wbase += w < wave ? v : 0;
+      total += v;
+    }
+    sh.pre[tid] = wbase + incl - nck;
+    __syncthreads();
+    for (int t = tid; t < total; t += kGrpThreads) {
+      int lo = 0, hi = nh - 1;                      // the segment owning chunk t
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (sh.pre[mid] <= t) lo = mid;
+        else hi = mid - 1;
+      }
+      const int4 r = sh.rec[lo];
+      const int2 r2 = sh.rec2[lo];
+      const int L = r2.x & 0xFFFFFF;
+      const int q0 = 16 * (t - sh.pre[lo]);
+      const int64_t snib = i64_of(r.x, r.y) + q0;
+      const int64_t rnib = i64_of(r.z, r.w) + q0;
+      const uint64_t sv = load16(B.seq, snib);
+      const uint64_t rv = load16(B.ref, rnib);
+      const int nb = (L - q0) < 16 ? (L - q0) : 16;
+      uint64_t diff = sv ^ rv;
+      diff = (diff | (diff >> 1) | (diff >> 2) | (diff >> 3)) & 0x1111111111111111ull;
+      if (nb < 16) diff &= (1ull << (4 * nb)) - 1;
+      if (!diff) continue;
+      const int s = s_begin + r2.y;
+      const int ds = (r2.x >> 24) & 1;
+      const bool mine = (r2.x & kSegMine) != 0;
+      const int64_t pos0 = rnib - B.ref_off[s];     // pos - span_start of the chunk's first base
+      do {
+        const int k = __builtin_ctzll(diff) >> 2;
+        diff &= diff - 1;
+        const int c = (int)((sv >> (4 * k)) & 15);
+        const int rc = (int)((rv >> (4 * k)) & 15);
+        if (c == 15 || !is_acgt(rc)) continue;
+        const unsigned long long key =
+            ((unsigned long long)r2.y << 52) | ((unsigned long long)(pos0 + k) << 4) | (unsigned long long)c;
+        grp_observe(sh, R, out, key, snib + k, c, rc, ds, mine);
+      } while (diff);
+    }
+    __syncthreads();
+  }
+}
+
+// Sorted list -> calls: one thread per run of equal keys.
+__device__ __forceinline__ void grp_classify(const DevBatch &B, GrpShared &sh, int n, int s_begin, uint8_t *out,
+                                             int32_t *scope_calls, int32_t *scope_bases) {
+  const int tid = threadIdx.x;
+  int n2 = 1;
+  while (n2 < n) n2 <<= 1;
+  for (int i = n + tid; i < n2; i += kGrpThreads) sh.key[i] = ~0ull;
+  __syncthreads();
+  for (int k = 2; k <= n2; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = tid; i < n2; i += kGrpThreads) {
+        const int ixj = i ^ j;
+        if (ixj <= i) continue;
+        const unsigned long long a = sh.key[i], b = sh.key[ixj];
+        if ((a > b) == ((i & k) == 0)) {
+          sh.key[i] = b;
+          sh.key[ixj] = a;
+          const unsigned long long p = sh.pay[i];
+          sh.pay[i] = sh.pay[ixj];
+          sh.pay[ixj] = p;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = tid; i < n; i += kGrpThreads) {
+    const unsigned long long key = sh.key[i];
+    if (i > 0 && sh.key[i - 1] == key) continue;
+    int e = i, seen = 0;
+    while (e < n && sh.key[e] == key) seen |= 1 << ((sh.pay[e++] >> 52) & 1);
+    if (seen != 3) continue;
+    const int s = s_begin + (int)(key >> 52);
+    const int c = (int)(key & 15);
+    if (grp_kept(B, s, (int64_t)((key >> 4) & ((1ull << 48) - 1)), c)) continue;
+    atomicAdd(&scope_calls[s], 1);
+    int masked = 0;
+    for (int x = i; x < e; ++x) {
+      const unsigned long long p = sh.pay[x];
+      if (!((p >> 53) & 1)) continue;
+      patch_nibble(out, (int64_t)(p & ((1ull << 48) - 1)), c, (int)((p >> 48) & 15));
+      ++masked;
+    }
+    if (masked) atomicAdd(&scope_bases[s], masked);
+  }
+}
+
+// groups: 2 x int4 per group {s_begin, s_end, seg_begin lo, hi}, {seg_end lo, hi, 0, 0}
+__global__ void __launch_bounds__(kGrpThreads) k_group_v4(const DevBatch B, const int4 *__restrict__ groups,
+                                                          const int4 *__restrict__ rec4, const int2 *__restrict__ rec2,
+                                                          uint8_t *__restrict__ out, int32_t *scope_calls,
+                                                          int32_t *scope_bases) {
+  __shared__ GrpShared sh;
+  const int tid = threadIdx.x;
+  const int4 g0 = groups[2 * blockIdx.x];
+  const int4 g1 = groups[2 * blockIdx.x + 1];
+  const int s_begin = g0.x;
+  const int64_t i_begin = i64_of(g0.z, g0.w), i_end = i64_of(g1.x, g1.y);
+  if (tid == 0) {
+    sh.top = 0;
+    sh.stk_lo[0] = 0ull;
+    sh.stk_hi[0] = ~0ull;
+    sh.stk_mode[0] = kModeCollect;
+  }
+  for (;;) {
+    __syncthreads();
+    const int top = sh.top;
+    if (top < 0) break;
+    const GrpRange R{sh.stk_lo[top], sh.stk_hi[top], sh.stk_mode[top]};
+    __syncthreads();
+    if (tid == 0) {
+      sh.top = top - 1;
+      sh.n_obs = 0;
+      sh.kmin = ~0ull;
+      sh.kmax = 0ull;
+      sh.flags = 0;
+      sh.masked = 0;
+    }
+    __syncthreads();
+    grp_scan(B, sh, R, s_begin, i_begin, i_end, rec4, rec2, out);
+    // (grp_scan ends on a barrier)
+    const int s = s_begin + (int)(R.lo >> 52);
+    if (R.mode == kModeFlags) {
+      if (tid == 0 && sh.flags == 3 && !grp_kept(B, s, (int64_t)((R.lo >> 4) & ((1ull << 48) - 1)), (int)(R.lo & 15))) {
+        atomicAdd(&scope_calls[s], 1);
+        const int t = ++sh.top;
+        sh.stk_lo[t] = R.lo;
+        sh.stk_hi[t] = R.hi;
+        sh.stk_mode[t] = kModePatch;
+      }
+      continue;
+    }
+    if (R.mode == kModePatch) {
+      if (tid == 0 && sh.masked) atomicAdd(&scope_bases[s], sh.masked);
+      continue;
+    }
+    const int n = sh.n_obs;
+    if (n > kGrpObs) {
+      if (tid == 0) {
+        const unsigned long long a = sh.kmin, b = sh.kmax;
+        int t = sh.top;
+        if (a == b) {
+          ++t;
+          sh.stk_lo[t] = a;
+          sh.stk_hi[t] = a + 1;
+          sh.stk_mode[t] = kModeFlags;
+        } else if (t + 2 < kGrpStack) {
+          const unsigned long long mid = a + (b - a) / 2;
+          ++t;
+          sh.stk_lo[t] = mid + 1;
+          sh.stk_hi[t] = b + 1;
+          sh.stk_mode[t] = kModeCollect;
+          ++t;
+          sh.stk_lo[t] = a;
+          sh.stk_hi[t] = mid + 1;
+          sh.stk_mode[t] = kModeCollect;
+        }
+        sh.top = t;
+      }
+      continue;
+    }
+    grp_classify(B, sh, n, s_begin, out, scope_calls, scope_bases);
+  }
+}
+
 // One workgroup per 16 Ki-position tile of a large scope: tally -> TN table (global).
 template <int TB>
 __global__ void __launch_bounds__(kBlock) k_tile_large(const DevBatch B, const Tile *__restrict__ tiles,
@@ -1041,6 +1306,11 @@ struct ganon_dbatch {
   int32_t max_small_span = 0;
   int4 *inc_rec = nullptr;      // per incidence, scope-major: {start|read, len|flags, seq_off lo, hi}
   int4 *srec[2] = {nullptr, nullptr};   // per small scope of each class: 3 x int4 (k_scope_v3)
+  int4 *groups = nullptr;               // k_group_v4: 2 x int4 per group
+  int4 *seg4 = nullptr;                 // k_group_v4: per segment {query nibble, reference nibble}
+  int2 *seg2 = nullptr;                 // k_group_v4: per segment {length | flags, scope_local}
+  int32_t n_groups = 0;
+  int64_t n_seg = 0;
   bool ran = false;
 };
 
@@ -1201,7 +1471,7 @@ GANON_API int ganon_ctx_set_stream(ganon_ctx *ctx, void *hip_stream) {
 }
 
 GANON_API int ganon_ctx_set_variant(ganon_ctx *ctx, int variant) {
-  if (!ctx || variant < GANON_VARIANT_DEFAULT || variant > GANON_VARIANT_COPYPATCH)
+  if (!ctx || variant < GANON_VARIANT_DEFAULT || variant > GANON_VARIANT_GROUP)
     return fail(ctx, GANON_E_ARG, "unknown kernel variant %d", variant);
   ctx->variant = variant;
   return GANON_OK;
@@ -1424,6 +1694,72 @@ GANON_API int ganon_batch_upload(ganon_ctx *ctx, const ganon_batch *b, ganon_dba
       if ((rc = dev_copy(ctx, db, &db->srec[k], sr.data(), sr.size()))) return bail(rc);
     }
   }
+  {
+    // k_group_v4: aligned segments of every read of every small scope, scope-major, packed
+    // into groups of consecutive scopes
+    std::vector<int4> s4, grp;
+    std::vector<int2> s2;
+    s4.reserve((size_t)b->n_incid);
+    s2.reserve((size_t)b->n_incid);
+    auto lo32 = [](int64_t v) { return (int)(uint32_t)(uint64_t)v; };
+    auto hi32 = [](int64_t v) { return (int)(uint32_t)((uint64_t)v >> 32); };
+    int32_t g_s0 = -1;
+    int64_t g_i0 = 0;
+    auto close_group = [&](int32_t s_end) {
+      if (g_s0 < 0) return;
+      const int64_t i1 = (int64_t)s4.size();
+      grp.push_back(make_int4(g_s0, s_end, lo32(g_i0), hi32(g_i0)));
+      grp.push_back(make_int4(lo32(i1), hi32(i1), 0, 0));
+      g_s0 = -1;
+    };
+    auto segments_of = [&](int32_t r, auto &&emit) {
+      const int64_t L = b->read_len[r];
+      int64_t q = 0, p = b->ref_start[r];
+      for (int k = 0; k < b->n_cig[r] && q < L; ++k) {
+        const uint32_t w = b->cigar[b->cig_off[r] + k];
+        const int op = w & 0xF;
+        const int64_t len = w >> 4;
+        if (op == 0 || op == 7 || op == 8) {
+          const int64_t n = std::min(len, L - q);
+          if (n > 0) emit(q, p, n);
+          q += len;
+          p += len;
+        } else if (op == 1 || op == 4) {
+          q += len;
+        } else if (op == 2 || op == 3) {
+          p += len;
+        }
+      }
+    };
+    for (int32_t s = 0; s < b->n_scopes; ++s) {
+      if (tab_off[s] >= 0) continue;   // wide scope: tile path
+      const int64_t i0 = b->scope_incid_off[s], i1 = b->scope_incid_off[s + 1];
+      int64_t nseg = 0;
+      for (int64_t i = i0; i < i1; ++i) segments_of(b->incid_read[i], [&](int64_t, int64_t, int64_t) { ++nseg; });
+      if (g_s0 >= 0 && ((int64_t)s4.size() - g_i0 + nseg > kGrpTarget || s - g_s0 >= kGrpMaxScopes)) close_group(s);
+      if (g_s0 < 0) {
+        g_s0 = s;
+        g_i0 = (int64_t)s4.size();
+      }
+      const int64_t ref0 = b->scope_ref_off[s] - b->scope_span_start[s];
+      for (int64_t i = i0; i < i1; ++i) {
+        const int32_t r = b->incid_read[i];
+        if (b->read_len[r] >= (1 << 24)) return bail(fail(ctx, GANON_E_ARG, "read %d longer than 16 Mb", r));
+        const uint32_t fl = ((uint32_t)b->dataset[r] << 24) | (b->write_scope[r] == s ? kSegMine : 0u);
+        const int64_t qnib = 2 * b->seq_off[r];
+        segments_of(r, [&](int64_t q, int64_t p, int64_t n) {
+          s4.push_back(make_int4(lo32(qnib + q), hi32(qnib + q), lo32(ref0 + p), hi32(ref0 + p)));
+          s2.push_back(make_int2((int)((uint32_t)n | fl), s - g_s0));
+        });
+      }
+    }
+    close_group(b->n_scopes);
+    if ((rc = dev_copy(ctx, db, &db->groups, grp.data(), grp.size()))) return bail(rc);
+    if ((rc = dev_copy(ctx, db, &db->seg4, s4.data(), s4.size()))) return bail(rc);
+    if ((rc = dev_copy(ctx, db, &db->seg2, s2.data(), s2.size()))) return bail(rc);
+    db->n_groups = (int32_t)(grp.size() / 2);
+    db->n_seg = (int64_t)s4.size();
+  }
   if ((rc = dev_alloc(ctx, db, &db->out, (size_t)b->seq_bytes))) return bail(rc);
   if ((rc = dev_alloc(ctx, db, &db->scope_calls, (size_t)b->n_scopes))) return bail(rc);
   if ((rc = dev_alloc(ctx, db, &db->scope_bases, (size_t)b->n_scopes))) return bail(rc);
@@ -1462,13 +1798,15 @@ GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
   HIP_OR_FAIL(hipMemsetAsync(db->counters, 0, 4 * sizeof(int32_t), st));
   HIP_OR_FAIL(hipMemcpyAsync(db->totals, db->static_totals, GANON_N_TOTALS * sizeof(unsigned long long),
                              hipMemcpyDeviceToDevice, st));
-  if (db->n_large_scopes) {
+  const bool v3 = ctx->variant == GANON_VARIANT_DEFAULT;
+  const bool v2 = ctx->variant == GANON_VARIANT_COPYPATCH;
+  const bool v4 = ctx->variant == GANON_VARIANT_GROUP;
+  if (db->n_large_scopes || v4) {
+    // counted with atomics (tiles of wide scopes; v4 run heads)
     HIP_OR_FAIL(hipMemsetAsync(db->scope_calls, 0, (size_t)db->n_scopes * sizeof(int32_t), st));
     HIP_OR_FAIL(hipMemsetAsync(db->scope_bases, 0, (size_t)db->n_scopes * sizeof(int32_t), st));
   }
-  const bool v3 = ctx->variant == GANON_VARIANT_DEFAULT;
-  const bool v2 = ctx->variant == GANON_VARIANT_COPYPATCH;
-  if (v2 || v3) {
+  if (v2 || v3 || v4) {
     // copy-then-patch: every read's bytes first, the scope kernels patch masked nibbles
     KernelScope ks(ctx, "copy_seq");
     if (db->seq_bytes) HIP_OR_FAIL(hipMemcpyAsync(db->out, B.seq, (size_t)db->seq_bytes, hipMemcpyDeviceToDevice, st));
@@ -1478,8 +1816,14 @@ GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
     k_passthrough<<<grid, kBlock, 0, st>>>(B, db->pt_list, db->n_pt, db->out);
     if ((rc = check_launch(ctx, "k_passthrough"))) return rc;
   }
+  if (v4 && db->n_groups) {
+    KernelScope ks(ctx, "k_group_v4");
+    k_group_v4<<<db->n_groups, kGrpThreads, 0, st>>>(B, db->groups, db->seg4, db->seg2, db->out, db->scope_calls,
+                                                     db->scope_bases);
+    if ((rc = check_launch(ctx, "k_group_v4"))) return rc;
+  }
   const int caps[2] = {kSmallCap0, kSmallCap1};
-  for (int k = 0; k < 2; ++k) {
+  for (int k = 0; k < 2 && !v4; ++k) {
     if (!db->n_small[k]) continue;
     if (v3) {
       KernelScope ks(ctx, k == 0 ? "k_scope_v3/2.5K" : "k_scope_v3/16K");
@@ -1517,7 +1861,7 @@ GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
     if ((rc = check_launch(ctx, "k_tile_large<1>"))) return rc;
   }
   // Re-runs on the 16-code tally; list lengths stay on the device (no host sync).
-  if (db->n_small[0] + db->n_small[1]) {
+  if (db->n_small[0] + db->n_small[1] && !v4) {
     KernelScope ks(ctx, "k_scope_small<4>/rare");
     const int grid = std::min<int>(db->n_small[0] + db->n_small[1], kPersistGrid);
     k_scope_small<4><<<grid, kBlock, small_lds_bytes(4, kSmallCap1), st>>>(

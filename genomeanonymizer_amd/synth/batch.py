@@ -161,6 +161,81 @@ def random_batch(seed: int, n_scopes: int = 64, max_reads: int = 40, read_len=(0
     return arr
 
 
+def dense_batch(seed: int, reads_per_scope=(8000, 400, 1200), span: int = 2200, read_len: int = 150,
+                error_rate: float = 0.02, keep_hot_site: bool = False) -> Dict[str, np.ndarray]:
+    """Very deep, error-rich scopes: thousands of observations per scope and one germline
+    site carried by every read over it (one call seen thousands of times). Exercises the
+    overflow handling of observation-list kernels; simple 150M reads only."""
+    rng = np.random.default_rng(seed)
+    n_s = len(reads_per_scope)
+    region = span + 2 * read_len
+    ref_codes = ACGT[rng.integers(0, 4, region * n_s)]
+    reads, scope_reads = [], []
+    keep_pos, keep_code = [], []
+    for s, nr in enumerate(reads_per_scope):
+        base = s * region
+        hot = read_len + span // 2                   # every read over it carries hot_alt
+        hot_alt = int(ACGT[(int(np.log2(ref_codes[base + hot])) + 1) % 4])
+        het = read_len + span // 3
+        het_alt = int(ACGT[(int(np.log2(ref_codes[base + het])) + 2) % 4])
+        ids = []
+        for _ in range(nr):
+            pos = int(rng.integers(read_len // 2, read_len // 2 + span - read_len))
+            seq = ref_codes[base + pos: base + pos + read_len].copy()
+            err = rng.random(read_len) < error_rate
+            seq[err] = ACGT[rng.integers(0, 4, int(err.sum()))]
+            if pos <= hot < pos + read_len:
+                seq[hot - pos] = hot_alt
+            if pos <= het < pos + read_len and rng.random() < 0.5:
+                seq[het - pos] = het_alt
+            reads.append((base + pos, seq, int(rng.integers(0, 2))))
+            ids.append(len(reads) - 1)
+        scope_reads.append(ids)
+        if keep_hot_site and s == 0:
+            keep_pos.append(base + hot)
+            keep_code.append(hot_alt)
+        else:
+            keep_pos.append(-1)
+            keep_code.append(0)
+    n = len(reads)
+    L = np.full(n, read_len, np.int32)
+    h = (read_len + 1) // 2
+    arr = {
+        "ref_start": np.array([r[0] for r in reads], np.int32),
+        "read_len": L,
+        "seq_off": np.arange(n, dtype=np.int64) * h,
+        "seq_nt16": np.concatenate([pack_nibbles(r[1]) for r in reads]),
+        "cig_off": np.arange(n, dtype=np.int64),
+        "n_cig": np.ones(n, np.int32),
+        "cigar": np.full(n, _cigar_word("M", read_len), np.uint32),
+        "dataset": np.array([r[2] for r in reads], np.uint8),
+        "ref_nt16": pack_nibbles(ref_codes),
+    }
+    starts = arr["ref_start"].astype(np.int64)
+    span_start, span_len, incid, offs = [], [], [], [0]
+    for s, ids in enumerate(scope_reads):
+        a = int(starts[ids].min())
+        b = int(starts[ids].max()) + read_len
+        span_start.append(a)
+        span_len.append(b - a)
+        incid.extend(rng.permutation(ids).tolist())
+        offs.append(len(incid))
+    arr["scope_incid_off"] = np.array(offs, np.int64)
+    arr["incid_read"] = np.array(incid, np.int32)
+    arr["scope_span_start"] = np.array(span_start, np.int32)
+    arr["scope_span_len"] = np.array(span_len, np.int32)
+    arr["scope_ref_off"] = np.array(span_start, np.int64)      # one contig: nibble = position
+    arr["keep_pos"] = np.array(keep_pos, np.int32)
+    arr["keep_code"] = np.array(keep_code, np.uint8)
+    ws = np.full(n, -1, np.int32)
+    for s, ids in enumerate(scope_reads):
+        for i in ids:
+            if rng.random() < 0.9:
+                ws[i] = s
+    arr["write_scope"] = ws
+    return arr
+
+
 def _ref_end(pos: int, cig: list) -> int:
     rl = sum(w >> 4 for w in cig if (w & 0xF) in (0, 2, 3, 7, 8))
     return pos + (rl if rl > 0 else 1)

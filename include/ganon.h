@@ -98,9 +98,16 @@ GANON_API int ganon_ctx_set_stream(ganon_ctx *ctx, void *hip_stream);
 /* Small-scope kernel: GANON_VARIANT_DEFAULT (copy-then-patch, persistent waves),
  * GANON_VARIANT_BLOCK (one 256-thread workgroup per scope, the first version),
  * GANON_VARIANT_WAVE (one wave per scope writing whole reads) or GANON_VARIANT_COPYPATCH
- * (copy-then-patch, one 64-thread workgroup per scope). The non-default ones are kept for
- * A/B runs and cross-checks; all give identical results. */
-enum { GANON_VARIANT_DEFAULT = 0, GANON_VARIANT_BLOCK = 1, GANON_VARIANT_WAVE = 2, GANON_VARIANT_COPYPATCH = 3 };
+ * (copy-then-patch, one 64-thread workgroup per scope), GANON_VARIANT_GROUP (copy-then-patch,
+ * one workgroup per group of consecutive scopes, calls from a sorted observation list). The
+ * non-default ones are kept for A/B runs and cross-checks; all give identical results. */
+enum {
+  GANON_VARIANT_DEFAULT = 0,
+  GANON_VARIANT_BLOCK = 1,
+  GANON_VARIANT_WAVE = 2,
+  GANON_VARIANT_COPYPATCH = 3,
+  GANON_VARIANT_GROUP = 4
+};
 GANON_API int ganon_ctx_set_variant(ganon_ctx *ctx, int variant);
 /* When on, ganon_batch_run records a HIP event pair around each kernel it launches. */
 GANON_API int ganon_ctx_set_profiling(ganon_ctx *ctx, int enabled);

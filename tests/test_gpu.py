@@ -12,6 +12,8 @@ from helpers import load_scope_golden, run_pipeline_vs_golden, written_reads_equ
 
 pytestmark = pytest.mark.gpu
 
+VARIANTS = (0, 1, 2, 3, 4)   # include/ganon.h GANON_VARIANT_*
+
 
 @pytest.fixture(scope="module")
 def masker(hip_built):
@@ -41,9 +43,12 @@ def _all_reads_equal(arr, a, b):
 @pytest.mark.parametrize("seed", [101, 202, 303])
 def test_hip_matches_reference_scopes(masker, seed):
     arr, exp_seq, exp_calls = load_scope_golden(seed)
-    out, calls, bases, tot = masker.mask(arr)
-    assert written_reads_equal(arr, out, exp_seq) == []
-    assert np.array_equal(calls, exp_calls)
+    for v in (0, 4):
+        masker.set_variant(v)
+        out, calls, bases, tot = masker.mask(arr)
+        assert written_reads_equal(arr, out, exp_seq) == [], v
+        assert np.array_equal(calls, exp_calls), v
+    masker.set_variant(0)
 
 
 @pytest.mark.parametrize("seed", list(range(1, 13)))
@@ -55,14 +60,17 @@ def test_hip_matches_oracle_edge_batches(masker, oracle, seed):
     if seed % 4 == 0:
         kw["wide_scopes"] = 4
     arr = random_batch(seed, n_scopes=40, **kw)
-    out, calls, bases, tot = masker.mask(arr)
     o_out, o_calls, o_bases, o_tot = oracle.mask(arr)
     in_batch = np.zeros(len(arr["read_len"]), bool)
     in_batch[arr["incid_read"]] = True
-    bad = [r for r in _all_reads_equal(arr, out, o_out) if in_batch[r] or arr["write_scope"][r] >= 0]
-    assert bad == []
-    assert np.array_equal(calls, o_calls) and np.array_equal(bases, o_bases)
-    assert tot[0] == o_tot[0] and tot[1] == o_tot[1]
+    for v in (0, 4):
+        masker.set_variant(v)
+        out, calls, bases, tot = masker.mask(arr)
+        bad = [r for r in _all_reads_equal(arr, out, o_out) if in_batch[r] or arr["write_scope"][r] >= 0]
+        assert bad == [], v
+        assert np.array_equal(calls, o_calls) and np.array_equal(bases, o_bases), v
+        assert tot[0] == o_tot[0] and tot[1] == o_tot[1], v
+    masker.set_variant(0)
 
 
 @pytest.mark.parametrize("seed", [21, 22, 23])
@@ -72,13 +80,30 @@ def test_block_variant_matches_wave_variant(masker, seed):
     arr = random_batch(seed, n_scopes=40, rare_frac=0.1, wide_scopes=1) if seed != 23 else \
         config2_batch(n_reads=300_000, genome=90_000_000, n_windows=30_000, n_germline=60_000)[0]
     res = []
-    for v in (0, 1, 2, 3):
+    for v in VARIANTS:
         masker.set_variant(v)
         res.append(masker.mask(arr))
     masker.set_variant(0)
-    for v in (1, 2, 3):
+    for v in VARIANTS[1:]:
         for k in range(3):
             assert np.array_equal(res[0][k], res[v][k]), (v, k)
+
+
+@pytest.mark.parametrize("seed,keep", [(5, False), (6, True)])
+def test_dense_scopes_all_variants_match_oracle(masker, oracle, seed, keep):
+    """Thousands of observations per scope and one site seen by ~600 reads: the group
+    kernel's list overflows (key-range bisection, single-key flags/patch scans)."""
+    from genomeanonymizer_amd.synth.batch import dense_batch
+    arr = dense_batch(seed, keep_hot_site=keep)
+    o_out, o_calls, o_bases, _ = oracle.mask(arr)
+    assert o_calls[0] > 1000
+    for v in VARIANTS:
+        masker.set_variant(v)
+        out, calls, bases, _ = masker.mask(arr)
+        assert np.array_equal(calls, o_calls), v
+        assert np.array_equal(bases, o_bases), v
+        assert np.array_equal(out, o_out), v
+    masker.set_variant(0)
 
 
 def test_hip_rare_and_wide_paths_exercised(masker):
@@ -127,14 +152,17 @@ def test_hip_config2_matches_oracle(masker, oracle):
     """BASELINE configs[1] layout at 2 M reads: every byte and count equal to the oracle."""
     from genomeanonymizer_amd.synth.batch import config2_batch
     arr, info = config2_batch(n_reads=2_000_000, genome=600_000_000, n_windows=200_000, n_germline=200_000)
-    out, calls, bases, tot = masker.mask(arr)
     o_out, o_calls, o_bases, o_tot = oracle.mask(arr)
-    assert np.array_equal(calls, o_calls)
-    assert np.array_equal(bases, o_bases)
     L = (arr["read_len"].astype(np.int64) + 1) // 2
     assert np.all(L == 75)
-    assert np.array_equal(out, o_out)
-    assert tot[2] == info["reads"]
+    for v in (0, 4):
+        masker.set_variant(v)
+        out, calls, bases, tot = masker.mask(arr)
+        assert np.array_equal(calls, o_calls), v
+        assert np.array_equal(bases, o_bases), v
+        assert np.array_equal(out, o_out), v
+        assert tot[2] == info["reads"]
+    masker.set_variant(0)
 
 
 def test_hip_device_path_is_idempotent_and_deterministic(masker):

@@ -29,14 +29,19 @@ sys.path.insert(0, REPO)
 
 HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 SMALL_CAP0, SMALL_CAP1 = 2560, 16384    # scope classes of ganon_hip.hip (kSmallCap0/1)
-VARIANT_NAMES = {0: "v3_persistent", 1: "v0_block", 2: "v1_wave", 3: "v2_copy_patch", 4: "v4_group"}
+VARIANT_NAMES = {0: "default", 1: "v0_block", 2: "v1_wave", 3: "v2_copy_patch", 4: "v4_group",
+                 5: "v5_group_fused", 6: "v3_persistent"}
+# how each variant writes reads (kernel_bytes attribution)
+VARIANT_WRITE = {0: "copy_patch", 1: "whole", 2: "whole", 3: "copy_patch", 4: "copy_patch", 5: "fused",
+                 6: "copy_patch"}
+# A/B configurations: (name, variant, group-kernel unroll)
+AB_CONFIGS = [(VARIANT_NAMES[v], v, 1) for v in (1, 2, 3, 6)] + \
+    [(f"v4_group_u{u}", 4, u) for u in (1, 2)] + [(f"v5_group_fused_u{u}", 5, u) for u in (1, 2, 4)]
 
 
 def kernel_class(name: str) -> str:
-    if name.startswith("k_passthrough"):
-        return "k_passthrough"
-    if name == "copy_seq":
-        return "k_passthrough"
+    if name in ("copy_seq", "k_copy_ranges") or name.startswith("k_passthrough"):
+        return "copy"
     if name.endswith("/2.5K"):
         return "small2.5K"
     if name.endswith("/16K"):
@@ -48,15 +53,17 @@ def kernel_class(name: str) -> str:
     return ""
 
 
-def kernel_bytes(arr, copy_patch: bool = True) -> dict:
-    """Algorithmic bytes per launch of each kernel (SURVEY §8(d) per-unit figures).
+def kernel_bytes(arr, mode: str = "fused") -> dict:
+    """Algorithmic bytes per launch of each kernel class (SURVEY §8(d) per-unit figures).
 
     Per read: ceil(L/2) in + ceil(L/2) out + 4*n_cigar + 16; each further scope incidence
-    ceil(L/2) + 4*n_cigar + 8; each scope ceil(span/2) of reference. Attribution: with
-    copy-then-patch (default variant) the device copy owns every read's in + out bytes and
-    the scope kernel of the read's write scope owns its 4*n_cigar + 16; otherwise the
-    kernel that writes a read owns all of its bytes. Extra incidences and the reference
-    bytes go to the kernel of their scope. The per-kernel figures sum to the formula."""
+    ceil(L/2) + 4*n_cigar + 8; each scope ceil(span/2) of reference. A read's own cost goes
+    to the kernel that writes it: mode "whole" — the scope kernel of its write scope, or the
+    pass-through copy; "copy_patch" — the device copy owns every read's in + out bytes and the
+    scope kernel its 4*n_cigar + 16; "fused" — the group kernel for the simple reads it stores,
+    the range copy for pass-through and clipped/indel reads, the wide-scope kernels for theirs.
+    Extra incidences and reference bytes go to the kernel of their scope; "group" (both small
+    classes) is what the group kernels own. The per-class figures sum to the formula."""
     L = arr["read_len"].astype(np.int64)
     h = (L + 1) // 2
     nc = arr["n_cig"].astype(np.int64)
@@ -64,15 +71,19 @@ def kernel_bytes(arr, copy_patch: bool = True) -> dict:
     cls = np.where(span <= SMALL_CAP0, 0, np.where(span <= SMALL_CAP1, 1, 2))
     names = ["small2.5K", "small16K", "large"]
     out = {n: 0 for n in names}
-    out["k_passthrough"] = 0
+    out["copy"] = 0
     ws = arr["write_scope"].astype(np.int64)
     wcls = np.where(ws >= 0, cls[np.maximum(ws, 0)], 3)
-    if copy_patch:
-        out["k_passthrough"] += int((2 * h).sum())
+    base = 2 * h + 4 * nc + 16
+    if mode == "copy_patch":
+        out["copy"] += int((2 * h).sum())
         base = 4 * nc + 16
-    else:
-        base = 2 * h + 4 * nc + 16
-    for k, n in enumerate(names + ["k_passthrough"]):
+    elif mode == "fused":
+        w = arr["cigar"][np.minimum(arr["cig_off"], max(len(arr["cigar"]) - 1, 0))].astype(np.int64) \
+            if len(arr["cigar"]) else np.zeros(len(L), np.int64)
+        simple = (nc == 1) & np.isin(w & 0xF, (0, 7, 8)) & ((w >> 4) == L) & (L > 0)
+        wcls = np.where((wcls < 2) & ~simple, 3, wcls)     # copied by k_copy_ranges
+    for k, n in enumerate(names + ["copy"]):
         out[n] += int(base[wcls == k].sum())
     offs = arr["scope_incid_off"]
     scope_of_inc = np.repeat(np.arange(len(span)), np.diff(offs))
@@ -90,7 +101,7 @@ def kernel_bytes(arr, copy_patch: bool = True) -> dict:
     for k, n in enumerate(names):
         out[n] += int(cost[extra & (cls[scope_of_inc] == k)].sum())
         out[n] += int(((span + 1) // 2)[cls == k].sum())
-    out["group"] = out["small2.5K"] + out["small16K"]    # k_group_v4 covers both classes
+    out["group"] = out["small2.5K"] + out["small16K"]
     return out
 
 
@@ -122,7 +133,9 @@ def main() -> None:
     ap.add_argument("--germline", type=int, default=1_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--variant", type=int, default=0,
-                    help="include/ganon.h GANON_VARIANT_*: 0 default, 1 block, 2 wave, 3 copy-patch, 4 group")
+                    help="include/ganon.h GANON_VARIANT_*: 0 default (= 4), 1 block, 2 wave, 3 copy-patch, "
+                         "4 group, 5 group fused, 6 persistent")
+    ap.add_argument("--unroll", type=int, default=1, help="group kernel chunks in flight per thread (1/2/4/8)")
     ap.add_argument("--ab", action="store_true", help="also time every small-scope variant, interleaved")
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_r01.json"),
                     help="PMC summary (tools/pmc_summary.py) for the traffic field, if present")
@@ -147,6 +160,7 @@ def main() -> None:
     t_gen = time.perf_counter() - t_gen
     masker = native.HipMasker(local)
     masker.set_variant(args.variant)
+    masker.set_param(native.PARAM_GROUP_UNROLL, args.unroll)
     stream = torch.cuda.current_stream()
     masker.set_stream(stream.cuda_stream)
     t_up = time.perf_counter()
@@ -192,20 +206,22 @@ def main() -> None:
     ab = None
     if args.ab:
         # interleaved rounds in one process (cdna_hip_programming.md §5.4 rule 24)
-        samples = {v: [] for v in VARIANT_NAMES}
+        samples = {name: [] for name, _, _ in AB_CONFIGS}
         for _ in range(5):
-            for v in VARIANT_NAMES:
+            for name, v, u in AB_CONFIGS:
                 masker.set_variant(v)
+                masker.set_param(native.PARAM_GROUP_UNROLL, u)
                 db.run()
                 torch.cuda.synchronize()
                 t = time.perf_counter()
                 for _ in range(args.steps):
                     db.run()
                 torch.cuda.synchronize()
-                samples[v].append((time.perf_counter() - t) / args.steps * 1e3)
+                samples[name].append((time.perf_counter() - t) / args.steps * 1e3)
         masker.set_variant(args.variant)
-        ab = {VARIANT_NAMES[v]: {"median_ms": round(float(np.median(x)), 4),
-                                                "min_ms": round(float(np.min(x)), 4)} for v, x in samples.items()}
+        masker.set_param(native.PARAM_GROUP_UNROLL, args.unroll)
+        ab = {name: {"median_ms": round(float(np.median(x)), 4),
+                     "min_ms": round(float(np.min(x)), 4)} for name, x in samples.items()}
     totals = db.totals()
     batch_info = db.info()
     if dist is not None:
@@ -217,7 +233,7 @@ def main() -> None:
         job_totals = totals
     db.free()
 
-    kb = kernel_bytes(arr, copy_patch=args.variant in (0, 3, 4))
+    kb = kernel_bytes(arr, VARIANT_WRITE[args.variant])
     per_kernel = {n: {"launches": c, "avg_ms": ms / c} for n, (c, ms) in ktimes.items()}
     dom = max(per_kernel, key=lambda n: per_kernel[n]["avg_ms"] * per_kernel[n]["launches"])
     dom_bytes = kb.get(kernel_class(dom), 0)

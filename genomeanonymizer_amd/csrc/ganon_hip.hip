@@ -905,20 +905,33 @@ constexpr int kGrpTarget = 256;      // segments per group (a larger scope forms
 constexpr int kGrpObs = 512;         // observations per LDS list
 constexpr int kGrpMaxScopes = 4096;  // scopes per group (12-bit local index)
 constexpr int kGrpStack = 80;        // key ranges pending (bisection depth <= 64)
-constexpr uint32_t kSegMine = 1u << 26;
+constexpr int kGrpPatch = 256;       // patches applied in registers by the fused write pass
+constexpr uint32_t kSegMine = 1u << 26;   // the segment's read is written by this scope
+constexpr uint32_t kSegWrite = 1u << 27;  // ... and the fused write pass stores it (simple read)
+constexpr unsigned long long kNibMask = (1ull << 48) - 1;
 enum { kModeCollect = 0, kModeFlags = 1, kModePatch = 2 };
+// GANON_PARAM_GROUP_SKIP (profiling only, results invalid): phases left out
+enum { kSkipClassify = 1, kSkipChunks = 2 };
+// grp_classify: count calls/bases; put patches of stored segments in the LDS list (others are
+// patched at once); or only patch stored segments' observations, atomically
+enum { kClsCount = 1, kClsList = 2, kClsStoredAtomic = 4 };
+constexpr int kGrpMap = 4096;        // chunk -> segment map entries (larger tiles binary-search)
+static_assert(kGrpTile == kGrpThreads && kGrpTile <= 256, "one staged record per thread, 8-bit map");
 
 struct GrpShared {
   int4 rec[kGrpTile];               // {query nibble lo, hi, reference nibble lo, hi}
-  int2 rec2[kGrpTile];              // {length | dataset << 24 | mine << 26, scope_local}
+  int2 rec2[kGrpTile];              // {length | dataset << 24 | mine << 26 | write << 27,
+                                    //  scope_local | (segment pos - span_start) << 12}
   int pre[kGrpTile];
+  uint8_t cmap[kGrpMap];            // staged segment of each chunk (tiles of <= kGrpMap chunks)
   int wsum[kGrpThreads / 64];
   unsigned long long key[kGrpObs];
   unsigned long long pay[kGrpObs];
+  unsigned long long patch[kGrpPatch];   // nibble index << 4 | (from ^ to)
   unsigned long long stk_lo[kGrpStack], stk_hi[kGrpStack];
   int stk_mode[kGrpStack];
   unsigned long long kmin, kmax;
-  int top, n_obs, flags, masked;
+  int top, n_obs, flags, masked, n_patch;
 };
 
 struct GrpRange {
@@ -926,17 +939,21 @@ struct GrpRange {
   int mode;
 };
 
+// payload: nibble index:48 | ref:4 | dataset:1 | mine:1 | stored:1
 __device__ __forceinline__ void grp_observe(GrpShared &sh, const GrpRange &R, uint8_t *out, unsigned long long key,
-                                            int64_t nib, int c, int rc, int ds, bool mine) {
+                                            int64_t nib, int c, int rc, int ds, uint32_t fl) {
   if (key < R.lo || key >= R.hi) return;
+  const bool mine = (fl & kSegMine) != 0;
   if (R.mode == kModeCollect) {
-    atomicMin(&sh.kmin, key);
-    atomicMax(&sh.kmax, key);
     const int k = atomicAdd(&sh.n_obs, 1);
     if (k < kGrpObs) {
       sh.key[k] = key;
       sh.pay[k] = (unsigned long long)nib | ((unsigned long long)rc << 48) | ((unsigned long long)ds << 52) |
-                  ((unsigned long long)(mine ? 1 : 0) << 53);
+                  ((unsigned long long)(mine ? 1 : 0) << 53) | ((unsigned long long)((fl >> 27) & 1) << 54);
+    } else {
+      // key range of the overflow (the stored part is folded in by grp_key_range)
+      atomicMin(&sh.kmin, key);
+      atomicMax(&sh.kmax, key);
     }
   } else if (R.mode == kModeFlags) {
     atomicOr(&sh.flags, 1 << ds);
@@ -952,102 +969,146 @@ __device__ __forceinline__ bool grp_kept(const DevBatch &B, int s, int64_t pos_o
   return kp >= 0 && B.keep_code[s] == c && (int64_t)kp - B.span_start[s] == pos_off;
 }
 
+// Stage records [c0, c0 + nh) in LDS with the exclusive prefix of their 16-base chunk counts
+// (only segments flagged kSegWrite when stored_only); returns the tile's chunk total.
+__device__ __forceinline__ int grp_tile(GrpShared &sh, const int4 *__restrict__ rec4, const int2 *__restrict__ rec2,
+                                        int64_t c0, int nh, bool stored_only) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t ix = c0 + (tid < nh ? tid : nh - 1);
+  const int4 r = rec4[ix];
+  const int2 r2 = rec2[ix];
+  int nck = 0;
+  if (tid < nh) {
+    sh.rec[tid] = r;
+    sh.rec2[tid] = r2;
+    if (!stored_only || (r2.x & kSegWrite)) nck = ((r2.x & 0xFFFFFF) + 15) >> 4;
+  }
+  int incl = nck;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(incl, o);
+    if (lane >= o) incl += t;
+  }
+  if (lane == 63) sh.wsum[wave] = incl;
+  __syncthreads();
+  int wbase = 0, total = 0;
+#pragma unroll
+  for (int w = 0; w < kGrpThreads / 64; ++w) {
+    const int v = sh.wsum[w];
+    wbase += w < wave ? v : 0;
+    total += v;
+  }
+  const int pre = wbase + incl - nck;
+  sh.pre[tid] = pre;
+  if (total <= kGrpMap)
+    for (int k = 0; k < nck; ++k) sh.cmap[pre + k] = (uint8_t)tid;
+  __syncthreads();
+  return total;
+}
+
+// The staged segment owning chunk t (largest j with pre[j] <= t).
+__device__ __forceinline__ int grp_find(const GrpShared &sh, int nh, int total, int t) {
+  if (total <= kGrpMap) return sh.cmap[t];
+  int lo = 0, hi = nh - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (sh.pre[mid] <= t) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
 // Stream every chunk of every segment of the group, feeding observations in range R.
+template <int kGrpUnroll>   // chunks in flight per thread
 __device__ __forceinline__ void grp_scan(const DevBatch &B, GrpShared &sh, const GrpRange &R, int s_begin,
                                          int64_t i_begin, int64_t i_end, const int4 *__restrict__ rec4,
-                                         const int2 *__restrict__ rec2, uint8_t *out) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+                                         const int2 *__restrict__ rec2, uint8_t *out, int skip) {
+  const int tid = threadIdx.x;
   for (int64_t c0 = i_begin; c0 < i_end; c0 += kGrpTile) {
     const int nh = (int)((i_end - c0) < kGrpTile ? (i_end - c0) : kGrpTile);
-    int nck = 0;
-    if (tid < nh) {
-      const int4 r = rec4[c0 + tid];
-      const int2 r2 = rec2[c0 + tid];
-      sh.rec[tid] = r;
-      sh.rec2[tid] = r2;
-      nck = ((r2.x & 0xFFFFFF) + 15) >> 4;
-    }
-    int incl = nck;
+    int total = grp_tile(sh, rec4, rec2, c0, nh, false);
+    if (skip & kSkipChunks) total = 0;
+    // kGrpUnroll chunks per thread per iteration: all their loads are issued before any is used
+    for (int t0 = tid; t0 < total; t0 += kGrpUnroll * kGrpThreads) {
+      int seg[kGrpUnroll], q0[kGrpUnroll];
+      uint64_t sv[kGrpUnroll], rv[kGrpUnroll];
+      int64_t sn[kGrpUnroll], rn[kGrpUnroll];
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int t = __shfl_up(incl, o);
-      if (lane >= o) incl += t;
-    }
-    if (lane == 63) sh.wsum[wave] = incl;
-    __syncthreads();
-    int wbase = 0, total = 0;
-#pragma unroll
-    for (int w = 0; w < kGrpThreads / 64; ++w) {
-      const int v = sh.wsum[w];
-      wbase += w < wave ? v : 0;
-      total += v;
-    }
-    sh.pre[tid] = wbase + incl - nck;
-    __syncthreads();
-    for (int t = tid; t < total; t += kGrpThreads) {
-      int lo = 0, hi = nh - 1;                      // the segment owning chunk t
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (sh.pre[mid] <= t) lo = mid;
-        else hi = mid - 1;
+      for (int u = 0; u < kGrpUnroll; ++u) {
+        const int t = min(t0 + u * kGrpThreads, total - 1);
+        const int j = grp_find(sh, nh, total, t);
+        seg[u] = j;
+        q0[u] = 16 * (t - sh.pre[j]);
+        const int4 r = sh.rec[j];
+        sn[u] = i64_of(r.x, r.y) + q0[u];
+        rn[u] = i64_of(r.z, r.w) + q0[u];
       }
-      const int4 r = sh.rec[lo];
-      const int2 r2 = sh.rec2[lo];
-      const int L = r2.x & 0xFFFFFF;
-      const int q0 = 16 * (t - sh.pre[lo]);
-      const int64_t snib = i64_of(r.x, r.y) + q0;
-      const int64_t rnib = i64_of(r.z, r.w) + q0;
-      const uint64_t sv = load16(B.seq, snib);
-      const uint64_t rv = load16(B.ref, rnib);
-      const int nb = (L - q0) < 16 ? (L - q0) : 16;
-      uint64_t diff = sv ^ rv;
-      diff = (diff | (diff >> 1) | (diff >> 2) | (diff >> 3)) & 0x1111111111111111ull;
-      if (nb < 16) diff &= (1ull << (4 * nb)) - 1;
-      if (!diff) continue;
-      const int s = s_begin + r2.y;
-      const int ds = (r2.x >> 24) & 1;
-      const bool mine = (r2.x & kSegMine) != 0;
-      const int64_t pos0 = rnib - B.ref_off[s];     // pos - span_start of the chunk's first base
-      do {
-        const int k = __builtin_ctzll(diff) >> 2;
-        diff &= diff - 1;
-        const int c = (int)((sv >> (4 * k)) & 15);
-        const int rc = (int)((rv >> (4 * k)) & 15);
-        if (c == 15 || !is_acgt(rc)) continue;
-        const unsigned long long key =
-            ((unsigned long long)r2.y << 52) | ((unsigned long long)(pos0 + k) << 4) | (unsigned long long)c;
-        grp_observe(sh, R, out, key, snib + k, c, rc, ds, mine);
-      } while (diff);
+#pragma unroll
+      for (int u = 0; u < kGrpUnroll; ++u) {
+        sv[u] = load16(B.seq, sn[u]);
+        rv[u] = load16(B.ref, rn[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < kGrpUnroll; ++u) {
+        if (t0 + u * kGrpThreads >= total) break;
+        const int2 r2 = sh.rec2[seg[u]];
+        const int L = r2.x & 0xFFFFFF;
+        const int nb = (L - q0[u]) < 16 ? (L - q0[u]) : 16;
+        uint64_t diff = sv[u] ^ rv[u];
+        diff = (diff | (diff >> 1) | (diff >> 2) | (diff >> 3)) & 0x1111111111111111ull;
+        if (nb < 16) diff &= (1ull << (4 * nb)) - 1;
+        if (!diff) continue;
+        const int ds = (r2.x >> 24) & 1;
+        const int pos0 = (int)((uint32_t)r2.y >> 12) + q0[u];   // pos - span_start, first base
+        const unsigned long long sk = (unsigned long long)(r2.y & 0xFFF) << 52;
+        do {
+          const int k = __builtin_ctzll(diff) >> 2;
+          diff &= diff - 1;
+          const int c = (int)((sv[u] >> (4 * k)) & 15);
+          const int rc = (int)((rv[u] >> (4 * k)) & 15);
+          if (c == 15 || !is_acgt(rc)) continue;
+          const unsigned long long key = sk | ((unsigned long long)(pos0 + k) << 4) | (unsigned long long)c;
+          grp_observe(sh, R, out, key, sn[u] + k, c, rc, ds, (uint32_t)r2.x);
+        } while (diff);
+      }
     }
     __syncthreads();
   }
 }
 
-// Sorted list -> calls: one thread per run of equal keys.
-__device__ __forceinline__ void grp_classify(const DevBatch &B, GrpShared &sh, int n, int s_begin, uint8_t *out,
-                                             int32_t *scope_calls, int32_t *scope_bases) {
+// In-LDS bitonic sort of n keys (n <= capacity rounded to a power of two); optional payload.
+__device__ __forceinline__ void lds_bitonic(unsigned long long *key, unsigned long long *pay, int n) {
   const int tid = threadIdx.x;
   int n2 = 1;
   while (n2 < n) n2 <<= 1;
-  for (int i = n + tid; i < n2; i += kGrpThreads) sh.key[i] = ~0ull;
+  for (int i = n + tid; i < n2; i += kGrpThreads) key[i] = ~0ull;
   __syncthreads();
   for (int k = 2; k <= n2; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {
       for (int i = tid; i < n2; i += kGrpThreads) {
         const int ixj = i ^ j;
         if (ixj <= i) continue;
-        const unsigned long long a = sh.key[i], b = sh.key[ixj];
+        const unsigned long long a = key[i], b = key[ixj];
         if ((a > b) == ((i & k) == 0)) {
-          sh.key[i] = b;
-          sh.key[ixj] = a;
-          const unsigned long long p = sh.pay[i];
-          sh.pay[i] = sh.pay[ixj];
-          sh.pay[ixj] = p;
+          key[i] = b;
+          key[ixj] = a;
+          if (pay) {
+            const unsigned long long p = pay[i];
+            pay[i] = pay[ixj];
+            pay[ixj] = p;
+          }
         }
       }
       __syncthreads();
     }
   }
+}
+
+// Sorted list -> calls: one thread per run of equal keys (how: kCls* bits).
+__device__ __forceinline__ void grp_classify(const DevBatch &B, GrpShared &sh, int n, int s_begin, uint8_t *out,
+                                             int32_t *scope_calls, int32_t *scope_bases, int how) {
+  const int tid = threadIdx.x;
+  lds_bitonic(sh.key, sh.pay, n);
   for (int i = tid; i < n; i += kGrpThreads) {
     const unsigned long long key = sh.key[i];
     if (i > 0 && sh.key[i - 1] == key) continue;
@@ -1056,24 +1117,100 @@ __device__ __forceinline__ void grp_classify(const DevBatch &B, GrpShared &sh, i
     if (seen != 3) continue;
     const int s = s_begin + (int)(key >> 52);
     const int c = (int)(key & 15);
-    if (grp_kept(B, s, (int64_t)((key >> 4) & ((1ull << 48) - 1)), c)) continue;
-    atomicAdd(&scope_calls[s], 1);
+    if (grp_kept(B, s, (int64_t)((key >> 4) & kNibMask), c)) continue;
+    if (how & kClsCount) atomicAdd(&scope_calls[s], 1);
     int masked = 0;
     for (int x = i; x < e; ++x) {
       const unsigned long long p = sh.pay[x];
       if (!((p >> 53) & 1)) continue;
-      patch_nibble(out, (int64_t)(p & ((1ull << 48) - 1)), c, (int)((p >> 48) & 15));
       ++masked;
+      const bool stored = (p >> 54) & 1;
+      const int64_t nib = (int64_t)(p & kNibMask);
+      const int rc = (int)((p >> 48) & 15);
+      if ((how & kClsList) && stored) {
+        const int k = atomicAdd(&sh.n_patch, 1);
+        if (k < kGrpPatch) sh.patch[k] = ((unsigned long long)nib << 4) | (unsigned long long)(c ^ rc);
+      } else if (!(how & kClsStoredAtomic) || stored) {
+        patch_nibble(out, nib, c, rc);
+      }
     }
-    if (masked) atomicAdd(&scope_bases[s], masked);
+    if ((how & kClsCount) && masked) atomicAdd(&scope_bases[s], masked);
   }
 }
 
+// Fused write pass: every read stored by this group (segments flagged kSegWrite: one segment =
+// the whole read) is copied from seq to out with the group's patches applied in registers.
+// Dwords inside the read are stored whole, the read's partial edge dwords byte by byte, so no
+// other workgroup's bytes are touched and no atomics are needed.
+__device__ __forceinline__ void grp_store_dword(uint8_t *out, int64_t D, uint32_t w, int64_t R0, int64_t R1) {
+  const int64_t lo = D > R0 ? D : R0, hi = (D + 4) < R1 ? (D + 4) : R1;
+  if (lo >= hi) return;
+  if (lo == D && hi == D + 4) {
+    *reinterpret_cast<uint32_t *>(out + D) = w;
+  } else {
+    for (int64_t b = lo; b < hi; ++b) out[b] = (uint8_t)(w >> (8 * (int)(b - D)));
+  }
+}
+
+__device__ __forceinline__ void grp_write(const DevBatch &B, GrpShared &sh, int64_t i_begin, int64_t i_end,
+                                          const int4 *__restrict__ rec4, const int2 *__restrict__ rec2, uint8_t *out,
+                                          int np) {
+  const int tid = threadIdx.x;
+  for (int64_t c0 = i_begin; c0 < i_end; c0 += kGrpTile) {
+    const int nh = (int)((i_end - c0) < kGrpTile ? (i_end - c0) : kGrpTile);
+    const int total = grp_tile(sh, rec4, rec2, c0, nh, true);
+    for (int t = tid; t < total; t += kGrpThreads) {
+      const int j = grp_find(sh, nh, total, t);
+      const int4 r = sh.rec[j];
+      const int L = sh.rec2[j].x & 0xFFFFFF;
+      const int q0 = 16 * (t - sh.pre[j]);
+      const int64_t R0 = i64_of(r.x, r.y) >> 1, R1 = R0 + ((L + 1) >> 1);
+      const int64_t B0 = R0 + (q0 >> 1), A = B0 & ~(int64_t)3;
+      const uint32_t *src = reinterpret_cast<const uint32_t *>(B.seq) + (A >> 2);
+      uint32_t w0 = src[0], w1 = src[1], w2 = src[2];
+      if (np) {
+        const unsigned long long lo_key = (unsigned long long)(2 * A) << 4;
+        int lo = 0, hi = np;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (sh.patch[mid] < lo_key) lo = mid + 1;
+          else hi = mid;
+        }
+        for (int k = lo; k < np; ++k) {
+          const unsigned long long e = sh.patch[k];
+          const int64_t nib = (int64_t)(e >> 4);
+          if (nib >= 2 * A + 24) break;
+          const int off = (int)((nib >> 1) - A);
+          const uint32_t x = (uint32_t)(e & 15) << (8 * (off & 3) + ((nib & 1) ? 0 : 4));
+          if (off < 4) w0 ^= x;
+          else if (off < 8) w1 ^= x;
+          else w2 ^= x;
+        }
+      }
+      // dwords starting in [B0, B0 + 8), plus the read's leading partial dword for chunk 0
+      if (A >= B0 || (q0 == 0 && A < R0)) grp_store_dword(out, A, w0, R0, R1);
+      if (A + 4 >= B0) grp_store_dword(out, A + 4, w1, R0, R1);
+      if (A + 8 < B0 + 8) grp_store_dword(out, A + 8, w2, R0, R1);
+    }
+    __syncthreads();
+  }
+}
+
+// The raw write pass done, make its stores visible at the memory side before atomics patch
+// the same bytes (device atomics execute beyond the XCD's L2).
+__device__ __forceinline__ void grp_release() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __syncthreads();
+}
+
 // groups: 2 x int4 per group {s_begin, s_end, seg_begin lo, hi}, {seg_end lo, hi, 0, 0}
-__global__ void __launch_bounds__(kGrpThreads) k_group_v4(const DevBatch B, const int4 *__restrict__ groups,
-                                                          const int4 *__restrict__ rec4, const int2 *__restrict__ rec2,
-                                                          uint8_t *__restrict__ out, int32_t *scope_calls,
-                                                          int32_t *scope_bases) {
+// FUSED: the group also stores its simple reads (grp_write); otherwise out is a prior copy of
+// seq and every patch is an atomic XOR.
+template <int U, bool FUSED>
+__global__ void __launch_bounds__(kGrpThreads) k_group(const DevBatch B, const int4 *__restrict__ groups,
+                                                       const int4 *__restrict__ rec4, const int2 *__restrict__ rec2,
+                                                       uint8_t *__restrict__ out, int32_t *scope_calls,
+                                                       int32_t *scope_bases, int skip) {
   __shared__ GrpShared sh;
   const int tid = threadIdx.x;
   const int4 g0 = groups[2 * blockIdx.x];
@@ -1085,7 +1222,9 @@ __global__ void __launch_bounds__(kGrpThreads) k_group_v4(const DevBatch B, cons
     sh.stk_lo[0] = 0ull;
     sh.stk_hi[0] = ~0ull;
     sh.stk_mode[0] = kModeCollect;
+    sh.n_patch = 0;
   }
+  bool atomic_mode = !FUSED;   // out already holds raw bytes: patches are atomic XORs
   for (;;) {
     __syncthreads();
     const int top = sh.top;
@@ -1101,11 +1240,12 @@ __global__ void __launch_bounds__(kGrpThreads) k_group_v4(const DevBatch B, cons
       sh.masked = 0;
     }
     __syncthreads();
-    grp_scan(B, sh, R, s_begin, i_begin, i_end, rec4, rec2, out);
+    grp_scan<U>(B, sh, R, s_begin, i_begin, i_end, rec4, rec2, out, skip);
     // (grp_scan ends on a barrier)
+    if (skip & kSkipClassify) continue;
     const int s = s_begin + (int)(R.lo >> 52);
     if (R.mode == kModeFlags) {
-      if (tid == 0 && sh.flags == 3 && !grp_kept(B, s, (int64_t)((R.lo >> 4) & ((1ull << 48) - 1)), (int)(R.lo & 15))) {
+      if (tid == 0 && sh.flags == 3 && !grp_kept(B, s, (int64_t)((R.lo >> 4) & kNibMask), (int)(R.lo & 15))) {
         atomicAdd(&scope_calls[s], 1);
         const int t = ++sh.top;
         sh.stk_lo[t] = R.lo;
@@ -1120,6 +1260,16 @@ __global__ void __launch_bounds__(kGrpThreads) k_group_v4(const DevBatch B, cons
     }
     const int n = sh.n_obs;
     if (n > kGrpObs) {
+      for (int i = tid; i < kGrpObs; i += kGrpThreads) {
+        atomicMin(&sh.kmin, sh.key[i]);
+        atomicMax(&sh.kmax, sh.key[i]);
+      }
+      __syncthreads();
+      if (!atomic_mode) {
+        grp_write(B, sh, i_begin, i_end, rec4, rec2, out, 0);
+        grp_release();
+        atomic_mode = true;
+      }
       if (tid == 0) {
         const unsigned long long a = sh.kmin, b = sh.kmax;
         int t = sh.top;
@@ -1143,7 +1293,39 @@ __global__ void __launch_bounds__(kGrpThreads) k_group_v4(const DevBatch B, cons
       }
       continue;
     }
-    grp_classify(B, sh, n, s_begin, out, scope_calls, scope_bases);
+    if (atomic_mode) {
+      grp_classify(B, sh, n, s_begin, out, scope_calls, scope_bases, kClsCount);
+      continue;
+    }
+    // fused, whole group in one list: patches in registers during the write pass
+    grp_classify(B, sh, n, s_begin, out, scope_calls, scope_bases, kClsCount | kClsList);
+    __syncthreads();
+    const int np = sh.n_patch;
+    if (np <= kGrpPatch) {
+      lds_bitonic(sh.patch, nullptr, np);
+      grp_write(B, sh, i_begin, i_end, rec4, rec2, out, np);
+    } else {
+      grp_write(B, sh, i_begin, i_end, rec4, rec2, out, 0);
+      grp_release();
+      grp_classify(B, sh, n, s_begin, out, scope_calls, scope_bases, kClsStoredAtomic);
+    }
+  }
+}
+
+// Byte ranges of reads no group stores (pass-through reads, reads with clips or indels): one
+// wave per range, whole dwords inside it, its partial edge dwords byte by byte.
+__global__ void __launch_bounds__(kBlock) k_copy_ranges(const uint8_t *__restrict__ seq,
+                                                        const int64_t *__restrict__ rng, int n,
+                                                        uint8_t *__restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int gw = (blockIdx.x * kBlock + threadIdx.x) >> 6;
+  const int nw = (gridDim.x * kBlock) >> 6;
+  for (int i = gw; i < n; i += nw) {
+    const int64_t b = rng[2 * i], e = rng[2 * i + 1];
+    for (int64_t D = (b & ~(int64_t)3) + 4 * lane; D < e; D += 256) {
+      const uint32_t w = *reinterpret_cast<const uint32_t *>(seq + D);
+      grp_store_dword(out, D, w, b, e);
+    }
   }
 }
 
@@ -1250,11 +1432,23 @@ __global__ void __launch_bounds__(kBlock) k_totals(const int32_t *__restrict__ c
     c += calls[i];
     b += bases[i];
   }
+  // one same-address atomic per workgroup: they serialize at the memory side
+  __shared__ long long part[2][kWaves];
   for (int o = 32; o > 0; o >>= 1) {
     c += __shfl_xor(c, o);
     b += __shfl_xor(b, o);
   }
   if ((threadIdx.x & 63) == 0) {
+    part[0][threadIdx.x >> 6] = c;
+    part[1][threadIdx.x >> 6] = b;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    c = b = 0;
+    for (int w = 0; w < kWaves; ++w) {
+      c += part[0][w];
+      b += part[1][w];
+    }
     if (c) atomicAdd(&totals[GANON_T_MASKED_SNV_CALLS], (unsigned long long)c);
     if (b) atomicAdd(&totals[GANON_T_MASKED_BASES], (unsigned long long)b);
   }
@@ -1273,6 +1467,8 @@ struct ganon_ctx {
   bool profiling = false;
   int variant = GANON_VARIANT_DEFAULT;
   int v3_blocks[2] = {1, 1};   // resident grid of k_scope_v3 per class (occupancy x CUs)
+  int group_unroll = 1;        // GANON_PARAM_GROUP_UNROLL
+  int group_skip = 0;          // GANON_PARAM_GROUP_SKIP (profiling only)
   std::string err;
   struct Rec { std::string name; hipEvent_t e0, e1; };
   std::vector<Rec> recs;
@@ -1306,11 +1502,13 @@ struct ganon_dbatch {
   int32_t max_small_span = 0;
   int4 *inc_rec = nullptr;      // per incidence, scope-major: {start|read, len|flags, seq_off lo, hi}
   int4 *srec[2] = {nullptr, nullptr};   // per small scope of each class: 3 x int4 (k_scope_v3)
-  int4 *groups = nullptr;               // k_group_v4: 2 x int4 per group
-  int4 *seg4 = nullptr;                 // k_group_v4: per segment {query nibble, reference nibble}
-  int2 *seg2 = nullptr;                 // k_group_v4: per segment {length | flags, scope_local}
+  int4 *groups = nullptr;               // k_group: 2 x int4 per group
+  int4 *seg4 = nullptr;                 // k_group: per segment {query nibble, reference nibble}
+  int2 *seg2 = nullptr;                 // k_group: per segment {length | flags, scope_local}
   int32_t n_groups = 0;
   int64_t n_seg = 0;
+  int64_t *copy_ranges = nullptr;       // k_copy_ranges: [begin, end) byte pairs
+  int32_t n_copy_ranges = 0;
   bool ran = false;
 };
 
@@ -1471,10 +1669,25 @@ GANON_API int ganon_ctx_set_stream(ganon_ctx *ctx, void *hip_stream) {
 }
 
 GANON_API int ganon_ctx_set_variant(ganon_ctx *ctx, int variant) {
-  if (!ctx || variant < GANON_VARIANT_DEFAULT || variant > GANON_VARIANT_GROUP)
+  if (!ctx || variant < GANON_VARIANT_DEFAULT || variant > GANON_VARIANT_PERSIST)
     return fail(ctx, GANON_E_ARG, "unknown kernel variant %d", variant);
   ctx->variant = variant;
   return GANON_OK;
+}
+
+GANON_API int ganon_ctx_set_param(ganon_ctx *ctx, int param, int value) {
+  if (!ctx) return GANON_E_ARG;
+  if (param == GANON_PARAM_GROUP_UNROLL) {
+    if (value != 1 && value != 2 && value != 4 && value != 8)
+      return fail(ctx, GANON_E_ARG, "group unroll must be 1, 2, 4 or 8 (got %d)", value);
+    ctx->group_unroll = value;
+    return GANON_OK;
+  }
+  if (param == GANON_PARAM_GROUP_SKIP) {
+    ctx->group_skip = value & (kSkipClassify | kSkipChunks);
+    return GANON_OK;
+  }
+  return fail(ctx, GANON_E_ARG, "unknown parameter %d", param);
 }
 
 GANON_API int ganon_ctx_set_profiling(ganon_ctx *ctx, int enabled) {
@@ -1703,6 +1916,13 @@ GANON_API int ganon_batch_upload(ganon_ctx *ctx, const ganon_batch *b, ganon_dba
     s2.reserve((size_t)b->n_incid);
     auto lo32 = [](int64_t v) { return (int)(uint32_t)(uint64_t)v; };
     auto hi32 = [](int64_t v) { return (int)(uint32_t)((uint64_t)v >> 32); };
+    // one M/=/X op over the whole read: a single segment, stored by the fused write pass
+    auto simple_read = [&](int32_t r) {
+      if (b->n_cig[r] != 1 || b->read_len[r] <= 0) return false;
+      const uint32_t w = b->cigar[b->cig_off[r]];
+      const int op = w & 0xF;
+      return (op == 0 || op == 7 || op == 8) && (int64_t)(w >> 4) == b->read_len[r];
+    };
     int32_t g_s0 = -1;
     int64_t g_i0 = 0;
     auto close_group = [&](int32_t s_end) {
@@ -1745,11 +1965,14 @@ GANON_API int ganon_batch_upload(ganon_ctx *ctx, const ganon_batch *b, ganon_dba
       for (int64_t i = i0; i < i1; ++i) {
         const int32_t r = b->incid_read[i];
         if (b->read_len[r] >= (1 << 24)) return bail(fail(ctx, GANON_E_ARG, "read %d longer than 16 Mb", r));
-        const uint32_t fl = ((uint32_t)b->dataset[r] << 24) | (b->write_scope[r] == s ? kSegMine : 0u);
+        uint32_t fl = (uint32_t)b->dataset[r] << 24;
+        if (b->write_scope[r] == s) fl |= kSegMine | (simple_read(r) ? kSegWrite : 0u);
         const int64_t qnib = 2 * b->seq_off[r];
         segments_of(r, [&](int64_t q, int64_t p, int64_t n) {
           s4.push_back(make_int4(lo32(qnib + q), hi32(qnib + q), lo32(ref0 + p), hi32(ref0 + p)));
-          s2.push_back(make_int2((int)((uint32_t)n | fl), s - g_s0));
+          // small scope: span <= kSmallCap1 < 2^20 positions
+          const uint32_t pos_off = (uint32_t)(p - b->scope_span_start[s]);
+          s2.push_back(make_int2((int)((uint32_t)n | fl), (int)((uint32_t)(s - g_s0) | (pos_off << 12))));
         });
       }
     }
@@ -1759,8 +1982,31 @@ GANON_API int ganon_batch_upload(ganon_ctx *ctx, const ganon_batch *b, ganon_dba
     if ((rc = dev_copy(ctx, db, &db->seg2, s2.data(), s2.size()))) return bail(rc);
     db->n_groups = (int32_t)(grp.size() / 2);
     db->n_seg = (int64_t)s4.size();
+    // byte ranges no fused group stores: reads out of every scope, reads with clips or indels
+    // (wide-scope reads are written whole by k_mask_large); adjacent ranges merged
+    std::vector<std::pair<int64_t, int64_t>> rs;
+    for (int32_t r = 0; r < b->n_reads; ++r) {
+      const int64_t h = ((int64_t)b->read_len[r] + 1) / 2;
+      const int32_t ws = b->write_scope[r];
+      if (h == 0 || (ws >= 0 && (tab_off[ws] >= 0 || simple_read(r)))) continue;
+      rs.emplace_back(b->seq_off[r], b->seq_off[r] + h);
+    }
+    std::sort(rs.begin(), rs.end());
+    std::vector<int64_t> ranges;
+    for (const auto &x : rs) {
+      if (!ranges.empty() && x.first <= ranges.back()) ranges.back() = std::max(ranges.back(), x.second);
+      else {
+        ranges.push_back(x.first);
+        ranges.push_back(x.second);
+      }
+    }
+    if ((rc = dev_copy(ctx, db, &db->copy_ranges, ranges.data(), ranges.size()))) return bail(rc);
+    db->n_copy_ranges = (int32_t)(ranges.size() / 2);
   }
   if ((rc = dev_alloc(ctx, db, &db->out, (size_t)b->seq_bytes))) return bail(rc);
+  // bytes outside every read are never written by the fused variant: make them defined
+  if (hipMemsetAsync(db->out, 0, (size_t)b->seq_bytes + 16, ctx->stream) != hipSuccess)
+    return bail(fail(ctx, GANON_E_DEVICE, "hipMemsetAsync(out) failed"));
   if ((rc = dev_alloc(ctx, db, &db->scope_calls, (size_t)b->n_scopes))) return bail(rc);
   if ((rc = dev_alloc(ctx, db, &db->scope_bases, (size_t)b->n_scopes))) return bail(rc);
   if ((rc = dev_alloc(ctx, db, &db->totals, GANON_N_TOTALS))) return bail(rc);
@@ -1798,15 +2044,25 @@ GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
   HIP_OR_FAIL(hipMemsetAsync(db->counters, 0, 4 * sizeof(int32_t), st));
   HIP_OR_FAIL(hipMemcpyAsync(db->totals, db->static_totals, GANON_N_TOTALS * sizeof(unsigned long long),
                              hipMemcpyDeviceToDevice, st));
-  const bool v3 = ctx->variant == GANON_VARIANT_DEFAULT;
+  const bool v3 = ctx->variant == GANON_VARIANT_PERSIST;
   const bool v2 = ctx->variant == GANON_VARIANT_COPYPATCH;
-  const bool v4 = ctx->variant == GANON_VARIANT_GROUP;
+  const bool v5 = ctx->variant == GANON_VARIANT_GROUP_FUSED;
+  const bool v4 = ctx->variant == GANON_VARIANT_DEFAULT || ctx->variant == GANON_VARIANT_GROUP || v5;
   if (db->n_large_scopes || v4) {
-    // counted with atomics (tiles of wide scopes; v4 run heads)
+    // counted with atomics (tiles of wide scopes; group run heads)
     HIP_OR_FAIL(hipMemsetAsync(db->scope_calls, 0, (size_t)db->n_scopes * sizeof(int32_t), st));
     HIP_OR_FAIL(hipMemsetAsync(db->scope_bases, 0, (size_t)db->n_scopes * sizeof(int32_t), st));
   }
-  if (v2 || v3 || v4) {
+  if (v5) {
+    // reads no group stores, copied first (a separate kernel: its stores are complete and
+    // visible before the group kernel patches any of those bytes atomically)
+    if (db->n_copy_ranges) {
+      KernelScope ks(ctx, "k_copy_ranges");
+      const int grid = std::min<int>((db->n_copy_ranges + kWaves - 1) / kWaves, 8192);
+      k_copy_ranges<<<grid, kBlock, 0, st>>>(B.seq, db->copy_ranges, db->n_copy_ranges, db->out);
+      if ((rc = check_launch(ctx, "k_copy_ranges"))) return rc;
+    }
+  } else if (v2 || v3 || v4) {
     // copy-then-patch: every read's bytes first, the scope kernels patch masked nibbles
     KernelScope ks(ctx, "copy_seq");
     if (db->seq_bytes) HIP_OR_FAIL(hipMemcpyAsync(db->out, B.seq, (size_t)db->seq_bytes, hipMemcpyDeviceToDevice, st));
@@ -1817,10 +2073,15 @@ GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
     if ((rc = check_launch(ctx, "k_passthrough"))) return rc;
   }
   if (v4 && db->n_groups) {
-    KernelScope ks(ctx, "k_group_v4");
-    k_group_v4<<<db->n_groups, kGrpThreads, 0, st>>>(B, db->groups, db->seg4, db->seg2, db->out, db->scope_calls,
-                                                     db->scope_bases);
-    if ((rc = check_launch(ctx, "k_group_v4"))) return rc;
+    KernelScope ks(ctx, v5 ? "k_group_fused" : "k_group");
+    const int u = ctx->group_unroll;
+    auto kern = v5 ? (u == 2 ? k_group<2, true> : u == 4 ? k_group<4, true> : u == 8 ? k_group<8, true>
+                                                                                     : k_group<1, true>)
+                   : (u == 2 ? k_group<2, false> : u == 4 ? k_group<4, false> : u == 8 ? k_group<8, false>
+                                                                                       : k_group<1, false>);
+    kern<<<db->n_groups, kGrpThreads, 0, st>>>(B, db->groups, db->seg4, db->seg2, db->out, db->scope_calls,
+                                               db->scope_bases, ctx->group_skip);
+    if ((rc = check_launch(ctx, "k_group"))) return rc;
   }
   const int caps[2] = {kSmallCap0, kSmallCap1};
   for (int k = 0; k < 2 && !v4; ++k) {
@@ -1886,7 +2147,7 @@ GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
   }
   {
     KernelScope ks(ctx, "k_totals");
-    const int grid = std::max(1, std::min<int>((db->n_scopes + kBlock - 1) / kBlock, 256));
+    const int grid = std::max(1, std::min<int>((db->n_scopes + kBlock - 1) / kBlock, 128));
     k_totals<<<grid, kBlock, 0, st>>>(db->scope_calls, db->scope_bases, db->n_scopes, db->counters + 0,
                                       db->counters + 1, db->totals);
     if ((rc = check_launch(ctx, "k_totals"))) return rc;

@@ -101,6 +101,7 @@ def hip_lib():
     lib.ganon_ctx_set_stream.argtypes = [_p, _p]
     lib.ganon_ctx_set_profiling.argtypes = [_p, C.c_int]
     lib.ganon_ctx_set_variant.argtypes = [_p, C.c_int]
+    lib.ganon_ctx_set_param.argtypes = [_p, C.c_int, C.c_int]
     lib.ganon_mask_batch.argtypes = [_p, C.POINTER(GanonBatch), _u8p, _i32p, _i32p, _i64p]
     lib.ganon_batch_upload.argtypes = [_p, C.POINTER(GanonBatch), C.POINTER(_p)]
     lib.ganon_batch_run.argtypes = [_p, _p]
@@ -117,9 +118,12 @@ def hip_lib():
     return lib
 
 
+PARAM_GROUP_UNROLL = 1   # include/ganon.h GANON_PARAM_GROUP_UNROLL
+PARAM_GROUP_SKIP = 2     # include/ganon.h GANON_PARAM_GROUP_SKIP (phase timing only)
+
 EXPORTED_HIP_SYMBOLS = (
     "ganon_ctx_create", "ganon_ctx_destroy", "ganon_last_error", "ganon_abi_version",
-    "ganon_ctx_set_stream", "ganon_ctx_set_profiling", "ganon_ctx_set_variant", "ganon_mask_batch", "ganon_batch_upload",
+    "ganon_ctx_set_stream", "ganon_ctx_set_profiling", "ganon_ctx_set_variant", "ganon_ctx_set_param", "ganon_mask_batch", "ganon_batch_upload",
     "ganon_batch_run", "ganon_batch_sync", "ganon_batch_download", "ganon_batch_free",
     "ganon_batch_device_totals", "ganon_batch_copy_totals", "ganon_last_kernel_times", "ganon_batch_info",
 )
@@ -167,8 +171,12 @@ class HipMasker:
         self._check(self._lib.ganon_ctx_set_stream(self._h, _p(hip_stream_ptr or 0)), "set_stream")
 
     def set_variant(self, variant: int) -> None:
-        """0 = one wave per small scope (default), 1 = one 256-thread workgroup per scope."""
+        """include/ganon.h GANON_VARIANT_*: 0 default, 1 block, 2 wave, 3 copy-patch, 4 group."""
         self._check(self._lib.ganon_ctx_set_variant(self._h, int(variant)), "set_variant")
+
+    def set_param(self, param: int, value: int) -> None:
+        """include/ganon.h GANON_PARAM_* tuning knob (never changes results)."""
+        self._check(self._lib.ganon_ctx_set_param(self._h, int(param), int(value)), "set_param")
 
     def set_profiling(self, on: bool) -> None:
         self._check(self._lib.ganon_ctx_set_profiling(self._h, 1 if on else 0), "set_profiling")

@@ -95,20 +95,32 @@ GANON_API const char *ganon_last_error(ganon_ctx *ctx);
 GANON_API int ganon_abi_version(void);
 /* Use an external hipStream_t (e.g. torch's current stream); NULL = the ctx's own. */
 GANON_API int ganon_ctx_set_stream(ganon_ctx *ctx, void *hip_stream);
-/* Small-scope kernel: GANON_VARIANT_DEFAULT (copy-then-patch, persistent waves),
+/* Small-scope kernel: GANON_VARIANT_DEFAULT (= GROUP),
  * GANON_VARIANT_BLOCK (one 256-thread workgroup per scope, the first version),
- * GANON_VARIANT_WAVE (one wave per scope writing whole reads) or GANON_VARIANT_COPYPATCH
+ * GANON_VARIANT_WAVE (one wave per scope writing whole reads), GANON_VARIANT_COPYPATCH
  * (copy-then-patch, one 64-thread workgroup per scope), GANON_VARIANT_GROUP (copy-then-patch,
- * one workgroup per group of consecutive scopes, calls from a sorted observation list). The
- * non-default ones are kept for A/B runs and cross-checks; all give identical results. */
+ * one workgroup per group of consecutive scopes, calls from a sorted observation list),
+ * GANON_VARIANT_GROUP_FUSED (the group kernel also stores its reads, patched in registers: no
+ * separate copy), GANON_VARIANT_PERSIST (copy-then-patch, persistent waves, one scope per
+ * wave). The non-default ones are kept for A/B runs and cross-checks; all give identical
+ * results for every byte that belongs to a read (bytes of seq_out outside every read's
+ * [seq_off, seq_off + ceil(len/2)) are left untouched by GROUP_FUSED). */
 enum {
   GANON_VARIANT_DEFAULT = 0,
   GANON_VARIANT_BLOCK = 1,
   GANON_VARIANT_WAVE = 2,
   GANON_VARIANT_COPYPATCH = 3,
-  GANON_VARIANT_GROUP = 4
+  GANON_VARIANT_GROUP = 4,
+  GANON_VARIANT_GROUP_FUSED = 5,
+  GANON_VARIANT_PERSIST = 6
 };
 GANON_API int ganon_ctx_set_variant(ganon_ctx *ctx, int variant);
+/* Tuning knobs (results never depend on them). GANON_PARAM_GROUP_UNROLL: 16-base chunks each
+ * thread of the group kernels keeps in flight, 1 (default), 2, 4 or 8.
+ * GANON_PARAM_GROUP_SKIP is for phase timing only and DOES change results: bit 0 leaves out
+ * the classification, bit 1 the chunk scan of the group kernel. Keep it 0 in production. */
+enum { GANON_PARAM_GROUP_UNROLL = 1, GANON_PARAM_GROUP_SKIP = 2 };
+GANON_API int ganon_ctx_set_param(ganon_ctx *ctx, int param, int value);
 /* When on, ganon_batch_run records a HIP event pair around each kernel it launches. */
 GANON_API int ganon_ctx_set_profiling(ganon_ctx *ctx, int enabled);
 

@@ -12,7 +12,8 @@ from helpers import load_scope_golden, run_pipeline_vs_golden, written_reads_equ
 
 pytestmark = pytest.mark.gpu
 
-VARIANTS = (0, 1, 2, 3, 4)   # include/ganon.h GANON_VARIANT_*
+VARIANTS = (0, 1, 2, 3, 4, 5, 6)   # include/ganon.h GANON_VARIANT_*
+MAIN = (0, 5, 6)                  # default (group + copy), fused group, persistent waves
 
 
 @pytest.fixture(scope="module")
@@ -43,7 +44,7 @@ def _all_reads_equal(arr, a, b):
 @pytest.mark.parametrize("seed", [101, 202, 303])
 def test_hip_matches_reference_scopes(masker, seed):
     arr, exp_seq, exp_calls = load_scope_golden(seed)
-    for v in (0, 4):
+    for v in MAIN:
         masker.set_variant(v)
         out, calls, bases, tot = masker.mask(arr)
         assert written_reads_equal(arr, out, exp_seq) == [], v
@@ -63,7 +64,7 @@ def test_hip_matches_oracle_edge_batches(masker, oracle, seed):
     o_out, o_calls, o_bases, o_tot = oracle.mask(arr)
     in_batch = np.zeros(len(arr["read_len"]), bool)
     in_batch[arr["incid_read"]] = True
-    for v in (0, 4):
+    for v in MAIN:
         masker.set_variant(v)
         out, calls, bases, tot = masker.mask(arr)
         bad = [r for r in _all_reads_equal(arr, out, o_out) if in_batch[r] or arr["write_scope"][r] >= 0]
@@ -109,12 +110,14 @@ def test_dense_scopes_all_variants_match_oracle(masker, oracle, seed, keep):
 def test_hip_rare_and_wide_paths_exercised(masker):
     from genomeanonymizer_amd.synth.batch import random_batch
     arr = random_batch(8, n_scopes=30, rare_frac=0.3, wide_scopes=4)
+    masker.set_variant(6)     # the persistent-wave kernel re-runs rare scopes on a 16-code tally
     db = masker.upload(arr)
     db.run()
     db.sync()
     info = db.info()
     tot = db.totals()
     db.free()
+    masker.set_variant(0)
     assert info["large_scopes"] >= 1 and info["large_tiles"] >= 2
     assert tot[5] >= 1, "no scope went through the 16-code re-run"
 
@@ -155,7 +158,7 @@ def test_hip_config2_matches_oracle(masker, oracle):
     o_out, o_calls, o_bases, o_tot = oracle.mask(arr)
     L = (arr["read_len"].astype(np.int64) + 1) // 2
     assert np.all(L == 75)
-    for v in (0, 4):
+    for v in MAIN:
         masker.set_variant(v)
         out, calls, bases, tot = masker.mask(arr)
         assert np.array_equal(calls, o_calls), v

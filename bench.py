@@ -32,11 +32,10 @@ SMALL_CAP0, SMALL_CAP1 = 2560, 16384    # scope classes of ganon_hip.hip (kSmall
 VARIANT_NAMES = {0: "default", 1: "v0_block", 2: "v1_wave", 3: "v2_copy_patch", 4: "v4_group",
                  5: "v5_group_fused", 6: "v3_persistent"}
 # how each variant writes reads (kernel_bytes attribution)
-VARIANT_WRITE = {0: "copy_patch", 1: "whole", 2: "whole", 3: "copy_patch", 4: "copy_patch", 5: "fused",
+VARIANT_WRITE = {0: "fused", 1: "whole", 2: "whole", 3: "copy_patch", 4: "copy_patch", 5: "fused",
                  6: "copy_patch"}
 # A/B configurations: (name, variant, group-kernel unroll)
-AB_CONFIGS = [(VARIANT_NAMES[v], v, 1) for v in (1, 2, 3, 6)] + \
-    [(f"v4_group_u{u}", 4, u) for u in (1, 2)] + [(f"v5_group_fused_u{u}", 5, u) for u in (1, 2, 4)]
+AB_CONFIGS = [(VARIANT_NAMES[v], v, 1) for v in (1, 2, 3, 6, 4)] + [(f"v5_group_fused_u{u}", 5, u) for u in (1, 2)]
 
 
 def kernel_class(name: str) -> str:
@@ -60,8 +59,8 @@ def kernel_bytes(arr, mode: str = "fused") -> dict:
     ceil(L/2) + 4*n_cigar + 8; each scope ceil(span/2) of reference. A read's own cost goes
     to the kernel that writes it: mode "whole" — the scope kernel of its write scope, or the
     pass-through copy; "copy_patch" — the device copy owns every read's in + out bytes and the
-    scope kernel its 4*n_cigar + 16; "fused" — the group kernel for the simple reads it stores,
-    the range copy for pass-through and clipped/indel reads, the wide-scope kernels for theirs.
+    scope kernel its 4*n_cigar + 16; "fused" — the group kernel (it copies the whole buffer
+    partition by partition) except the reads the wide-scope kernels write.
     Extra incidences and reference bytes go to the kernel of their scope; "group" (both small
     classes) is what the group kernels own. The per-class figures sum to the formula."""
     L = arr["read_len"].astype(np.int64)
@@ -79,10 +78,7 @@ def kernel_bytes(arr, mode: str = "fused") -> dict:
         out["copy"] += int((2 * h).sum())
         base = 4 * nc + 16
     elif mode == "fused":
-        w = arr["cigar"][np.minimum(arr["cig_off"], max(len(arr["cigar"]) - 1, 0))].astype(np.int64) \
-            if len(arr["cigar"]) else np.zeros(len(L), np.int64)
-        simple = (nc == 1) & np.isin(w & 0xF, (0, 7, 8)) & ((w >> 4) == L) & (L > 0)
-        wcls = np.where((wcls < 2) & ~simple, 3, wcls)     # copied by k_copy_ranges
+        wcls = np.where(wcls == 2, 2, 0)     # the group kernel copies every byte it does not leave to k_mask_large
     for k, n in enumerate(names + ["copy"]):
         out[n] += int(base[wcls == k].sum())
     offs = arr["scope_incid_off"]
@@ -133,7 +129,7 @@ def main() -> None:
     ap.add_argument("--germline", type=int, default=1_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--variant", type=int, default=0,
-                    help="include/ganon.h GANON_VARIANT_*: 0 default (= 4), 1 block, 2 wave, 3 copy-patch, "
+                    help="include/ganon.h GANON_VARIANT_*: 0 default (= 5), 1 block, 2 wave, 3 copy-patch, "
                          "4 group, 5 group fused, 6 persistent")
     ap.add_argument("--unroll", type=int, default=1, help="group kernel chunks in flight per thread (1/2/4/8)")
     ap.add_argument("--ab", action="store_true", help="also time every small-scope variant, interleaved")

@@ -48,7 +48,7 @@ def build_hip(force: bool = False) -> str:
     if force or _stale(HIP_LIB, [src, hdr, __file__]):
         tmp = HIP_LIB + ".tmp"
         _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-              "-fvisibility=hidden", "-Wno-unused-result", "-o", tmp, src])
+              "-fvisibility=hidden", "-Wno-unused-result", "-Wno-unused-value", "-o", tmp, src])
         os.replace(tmp, HIP_LIB)
     return HIP_LIB
 

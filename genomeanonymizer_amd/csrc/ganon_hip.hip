@@ -882,7 +882,7 @@ __global__ void __launch_bounds__(256) k_scope_v3(const DevBatch B, const int4 *
   }
 }
 
-// ---- v4: scope groups, observation sort -------------------------------------------------
+// ---- group kernels: scope groups, observation lists ---------------------------------------
 // No per-scope table and no per-scope serialization. At upload every read of a small scope is
 // cut into segments (one per aligned M/=/X run: query nibble index, reference nibble index,
 // length) and consecutive scopes are packed into groups of ~kGrpTarget segments. One 256-thread
@@ -891,36 +891,42 @@ __global__ void __launch_bounds__(256) k_scope_v3(const DevBatch B, const int4 *
 // an ACGT reference base becomes an observation in LDS:
 //   key = scope_local:12 | (pos - span_start):48 | allele:4
 //   payload = nibble index:48 | ref:4 | dataset:1 | mine:1
-// The list is sorted (bitonic, in LDS); a run of equal keys is one call (pos, allele) of one
-// scope, TN iff the run holds a tumor and a normal observation — the end state of the
-// reference's per-position state machine (variants.py:33-39) — and not the
-// window's kept variant. Run heads count the call and patch the run's observations in reads
-// the scope writes. All 16 codes are handled alike (no re-run). A group whose observations
-// overflow the list is re-scanned over halves of its observed key range; a single key that
-// overflows on its own (very deep coverage at one site) is resolved by a flags scan and a
-// patch scan.
+// A set of equal keys is one call (pos, allele) of one scope, TN iff it holds a tumor and a
+// normal observation — the end state of the reference's per-position state machine
+// (variants.py:33-39) — and not the window's kept variant. TN calls are counted
+// and their observations in reads the scope writes are masked. All 16 codes are handled
+// alike (no re-run). A group whose observations overflow the list is re-scanned over halves
+// of its observed key range; a single key that overflows on its own (very deep coverage at one
+// site) is resolved by a flags scan and a patch scan.
+//
+// Output. GROUP: a device copy of seq precedes the kernel, masks are atomic XORs. GROUP_FUSED:
+// groups are launched in the order of their reads in the sequence buffer and each workgroup
+// owns a 128-byte-aligned partition [p0, p1) of the output, which it copies with whole-line
+// 16-byte stores before scanning (its reads' bases are then L2-hot for the scan). Masks inside
+// the partition are plain byte stores seq[b] ^ mask after the copy has drained; masks of
+// bytes in another workgroup's partition (a read crossing a partition boundary) go to a
+// global list applied by k_far_patches after the kernel. Partial-line stores from different
+// workgroups cost ~4x whole-line stores on MI355X (tools/membench.hip), hence partitions.
 constexpr int kGrpThreads = 256;
 constexpr int kGrpTile = 256;        // segment records staged per tile
 constexpr int kGrpTarget = 256;      // segments per group (a larger scope forms its own group)
 constexpr int kGrpObs = 512;         // observations per LDS list
 constexpr int kGrpMaxScopes = 4096;  // scopes per group (12-bit local index)
 constexpr int kGrpStack = 80;        // key ranges pending (bisection depth <= 64)
-constexpr int kGrpPatch = 256;       // patches applied in registers by the fused write pass
+constexpr int kGrpPatch = 256;       // in-partition masks of a fused workgroup, sorted in LDS
+constexpr int kGrpMap = 4096;        // chunk -> segment map entries (larger tiles binary-search)
+constexpr int kGrpQuad = 256;        // lists up to this size are matched without sorting
+constexpr int64_t kPartAlign = 128;  // partition boundaries fall on whole lines
 constexpr uint32_t kSegMine = 1u << 26;   // the segment's read is written by this scope
-constexpr uint32_t kSegWrite = 1u << 27;  // ... and the fused write pass stores it (simple read)
 constexpr unsigned long long kNibMask = (1ull << 48) - 1;
 enum { kModeCollect = 0, kModeFlags = 1, kModePatch = 2 };
 // GANON_PARAM_GROUP_SKIP (profiling only, results invalid): phases left out
-enum { kSkipClassify = 1, kSkipChunks = 2 };
-// grp_classify: count calls/bases; put patches of stored segments in the LDS list (others are
-// patched at once); or only patch stored segments' observations, atomically
-enum { kClsCount = 1, kClsList = 2, kClsStoredAtomic = 4 };
-constexpr int kGrpMap = 4096;        // chunk -> segment map entries (larger tiles binary-search)
+enum { kSkipClassify = 1, kSkipChunks = 2, kSkipCopy = 4 };
 static_assert(kGrpTile == kGrpThreads && kGrpTile <= 256, "one staged record per thread, 8-bit map");
 
 struct GrpShared {
   int4 rec[kGrpTile];               // {query nibble lo, hi, reference nibble lo, hi}
-  int2 rec2[kGrpTile];              // {length | dataset << 24 | mine << 26 | write << 27,
+  int2 rec2[kGrpTile];              // {length | dataset << 24 | mine << 26,
                                     //  scope_local | (segment pos - span_start) << 12}
   int pre[kGrpTile];
   uint8_t cmap[kGrpMap];            // staged segment of each chunk (tiles of <= kGrpMap chunks)
@@ -932,6 +938,7 @@ struct GrpShared {
   int stk_mode[kGrpStack];
   unsigned long long kmin, kmax;
   int top, n_obs, flags, masked, n_patch;
+  int blk_calls, blk_bases;         // this workgroup's contribution to the totals
 };
 
 struct GrpRange {
@@ -939,9 +946,40 @@ struct GrpRange {
   int mode;
 };
 
-// payload: nibble index:48 | ref:4 | dataset:1 | mine:1 | stored:1
-__device__ __forceinline__ void grp_observe(GrpShared &sh, const GrpRange &R, uint8_t *out, unsigned long long key,
-                                            int64_t nib, int c, int rc, int ds, uint32_t fl) {
+// Where a masked base goes.
+struct PatchSink {
+  uint8_t *out;
+  int64_t p0, p1;                   // fused: this workgroup's partition of out (bytes)
+  unsigned long long *far;          // fused: masks of bytes outside the partition
+  int *far_count;
+  int64_t far_cap;
+  bool fused;
+  bool lds;                         // fused, in-partition masks into the LDS list
+  bool in_only;                     // fused re-run after an LDS list overflow: in-partition only
+};
+
+__device__ __forceinline__ void sink_patch(GrpShared &sh, const PatchSink &k, int64_t nib, int c, int rc) {
+  const unsigned long long e = ((unsigned long long)nib << 4) | (unsigned long long)(c ^ rc);
+  if (k.fused) {
+    const int64_t byte = nib >> 1;
+    if (byte < k.p0 || byte >= k.p1) {
+      if (k.in_only) return;
+      const int i = atomicAdd(k.far_count, 1);
+      if (i < k.far_cap) k.far[i] = e;
+      return;
+    }
+    if (k.lds) {
+      const int i = atomicAdd(&sh.n_patch, 1);
+      if (i < kGrpPatch) sh.patch[i] = e;
+      return;
+    }
+  }
+  patch_nibble(k.out, nib, c, rc);
+}
+
+// payload: nibble index:48 | ref:4 | dataset:1 | mine:1
+__device__ __forceinline__ void grp_observe(GrpShared &sh, const GrpRange &R, const PatchSink &sink,
+                                            unsigned long long key, int64_t nib, int c, int rc, int ds, uint32_t fl) {
   if (key < R.lo || key >= R.hi) return;
   const bool mine = (fl & kSegMine) != 0;
   if (R.mode == kModeCollect) {
@@ -949,16 +987,16 @@ __device__ __forceinline__ void grp_observe(GrpShared &sh, const GrpRange &R, ui
     if (k < kGrpObs) {
       sh.key[k] = key;
       sh.pay[k] = (unsigned long long)nib | ((unsigned long long)rc << 48) | ((unsigned long long)ds << 52) |
-                  ((unsigned long long)(mine ? 1 : 0) << 53) | ((unsigned long long)((fl >> 27) & 1) << 54);
+                  ((unsigned long long)(mine ? 1 : 0) << 53);
     } else {
-      // key range of the overflow (the stored part is folded in by grp_key_range)
+      // key range of the overflow (the stored part is folded in after the scan)
       atomicMin(&sh.kmin, key);
       atomicMax(&sh.kmax, key);
     }
   } else if (R.mode == kModeFlags) {
     atomicOr(&sh.flags, 1 << ds);
   } else if (mine) {
-    patch_nibble(out, nib, c, rc);
+    sink_patch(sh, sink, nib, c, rc);
     atomicAdd(&sh.masked, 1);
   }
 }
@@ -969,10 +1007,10 @@ __device__ __forceinline__ bool grp_kept(const DevBatch &B, int s, int64_t pos_o
   return kp >= 0 && B.keep_code[s] == c && (int64_t)kp - B.span_start[s] == pos_off;
 }
 
-// Stage records [c0, c0 + nh) in LDS with the exclusive prefix of their 16-base chunk counts
-// (only segments flagged kSegWrite when stored_only); returns the tile's chunk total.
+// Stage records [c0, c0 + nh) in LDS with the exclusive prefix of their 16-base chunk counts;
+// returns the tile's chunk total.
 __device__ __forceinline__ int grp_tile(GrpShared &sh, const int4 *__restrict__ rec4, const int2 *__restrict__ rec2,
-                                        int64_t c0, int nh, bool stored_only) {
+                                        int64_t c0, int nh) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t ix = c0 + (tid < nh ? tid : nh - 1);
   const int4 r = rec4[ix];
@@ -981,7 +1019,7 @@ __device__ __forceinline__ int grp_tile(GrpShared &sh, const int4 *__restrict__ 
   if (tid < nh) {
     sh.rec[tid] = r;
     sh.rec2[tid] = r2;
-    if (!stored_only || (r2.x & kSegWrite)) nck = ((r2.x & 0xFFFFFF) + 15) >> 4;
+    nck = ((r2.x & 0xFFFFFF) + 15) >> 4;
   }
   int incl = nck;
 #pragma unroll
@@ -1020,13 +1058,13 @@ __device__ __forceinline__ int grp_find(const GrpShared &sh, int nh, int total, 
 
 // Stream every chunk of every segment of the group, feeding observations in range R.
 template <int kGrpUnroll>   // chunks in flight per thread
-__device__ __forceinline__ void grp_scan(const DevBatch &B, GrpShared &sh, const GrpRange &R, int s_begin,
+__device__ __forceinline__ void grp_scan(const DevBatch &B, GrpShared &sh, const GrpRange &R, const PatchSink &sink,
                                          int64_t i_begin, int64_t i_end, const int4 *__restrict__ rec4,
-                                         const int2 *__restrict__ rec2, uint8_t *out, int skip) {
+                                         const int2 *__restrict__ rec2, int skip) {
   const int tid = threadIdx.x;
   for (int64_t c0 = i_begin; c0 < i_end; c0 += kGrpTile) {
     const int nh = (int)((i_end - c0) < kGrpTile ? (i_end - c0) : kGrpTile);
-    int total = grp_tile(sh, rec4, rec2, c0, nh, false);
+    int total = grp_tile(sh, rec4, rec2, c0, nh);
     if (skip & kSkipChunks) total = 0;
     // kGrpUnroll chunks per thread per iteration: all their loads are issued before any is used
     for (int t0 = tid; t0 < total; t0 += kGrpUnroll * kGrpThreads) {
@@ -1068,7 +1106,7 @@ __device__ __forceinline__ void grp_scan(const DevBatch &B, GrpShared &sh, const
           const int rc = (int)((rv[u] >> (4 * k)) & 15);
           if (c == 15 || !is_acgt(rc)) continue;
           const unsigned long long key = sk | ((unsigned long long)(pos0 + k) << 4) | (unsigned long long)c;
-          grp_observe(sh, R, out, key, sn[u] + k, c, rc, ds, (uint32_t)r2.x);
+          grp_observe(sh, R, sink, key, sn[u] + k, c, rc, ds, (uint32_t)r2.x);
         } while (diff);
       }
     }
@@ -1104,10 +1142,42 @@ __device__ __forceinline__ void lds_bitonic(unsigned long long *key, unsigned lo
   }
 }
 
-// Sorted list -> calls: one thread per run of equal keys (how: kCls* bits).
-__device__ __forceinline__ void grp_classify(const DevBatch &B, GrpShared &sh, int n, int s_begin, uint8_t *out,
-                                             int32_t *scope_calls, int32_t *scope_bases, int how) {
+// Observation list -> calls. Up to kGrpQuad observations every thread matches its own
+// observation against the whole list (no sort, no barrier); longer lists are sorted and one
+// thread takes each run of equal keys. count: add calls/bases to the per-scope and workgroup
+// totals (off for a re-run that only re-applies masks).
+__device__ __forceinline__ void grp_classify(const DevBatch &B, GrpShared &sh, int n, int s_begin,
+                                             const PatchSink &sink, int32_t *scope_calls, int32_t *scope_bases,
+                                             bool count) {
   const int tid = threadIdx.x;
+  if (n <= kGrpQuad) {
+    if (tid >= n) return;
+    const unsigned long long key = sh.key[tid];
+    int seen = 0;
+    bool head = true;
+    for (int j = 0; j < n; ++j) {
+      if (sh.key[j] != key) continue;
+      seen |= 1 << ((sh.pay[j] >> 52) & 1);
+      head &= j >= tid;
+    }
+    if (seen != 3) return;
+    const int s = s_begin + (int)(key >> 52);
+    const int c = (int)(key & 15);
+    if (grp_kept(B, s, (int64_t)((key >> 4) & kNibMask), c)) return;
+    if (count && head) {
+      atomicAdd(&scope_calls[s], 1);
+      atomicAdd(&sh.blk_calls, 1);
+    }
+    const unsigned long long p = sh.pay[tid];
+    if ((p >> 53) & 1) {
+      sink_patch(sh, sink, (int64_t)(p & kNibMask), c, (int)((p >> 48) & 15));
+      if (count) {
+        atomicAdd(&scope_bases[s], 1);
+        atomicAdd(&sh.blk_bases, 1);
+      }
+    }
+    return;
+  }
   lds_bitonic(sh.key, sh.pay, n);
   for (int i = tid; i < n; i += kGrpThreads) {
     const unsigned long long key = sh.key[i];
@@ -1118,117 +1188,89 @@ __device__ __forceinline__ void grp_classify(const DevBatch &B, GrpShared &sh, i
     const int s = s_begin + (int)(key >> 52);
     const int c = (int)(key & 15);
     if (grp_kept(B, s, (int64_t)((key >> 4) & kNibMask), c)) continue;
-    if (how & kClsCount) atomicAdd(&scope_calls[s], 1);
     int masked = 0;
     for (int x = i; x < e; ++x) {
       const unsigned long long p = sh.pay[x];
       if (!((p >> 53) & 1)) continue;
+      sink_patch(sh, sink, (int64_t)(p & kNibMask), c, (int)((p >> 48) & 15));
       ++masked;
-      const bool stored = (p >> 54) & 1;
-      const int64_t nib = (int64_t)(p & kNibMask);
-      const int rc = (int)((p >> 48) & 15);
-      if ((how & kClsList) && stored) {
-        const int k = atomicAdd(&sh.n_patch, 1);
-        if (k < kGrpPatch) sh.patch[k] = ((unsigned long long)nib << 4) | (unsigned long long)(c ^ rc);
-      } else if (!(how & kClsStoredAtomic) || stored) {
-        patch_nibble(out, nib, c, rc);
+    }
+    if (count) {
+      atomicAdd(&scope_calls[s], 1);
+      atomicAdd(&sh.blk_calls, 1);
+      if (masked) {
+        atomicAdd(&scope_bases[s], masked);
+        atomicAdd(&sh.blk_bases, masked);
       }
     }
-    if ((how & kClsCount) && masked) atomicAdd(&scope_bases[s], masked);
   }
 }
 
-// Fused write pass: every read stored by this group (segments flagged kSegWrite: one segment =
-// the whole read) is copied from seq to out with the group's patches applied in registers.
-// Dwords inside the read are stored whole, the read's partial edge dwords byte by byte, so no
-// other workgroup's bytes are touched and no atomics are needed.
-__device__ __forceinline__ void grp_store_dword(uint8_t *out, int64_t D, uint32_t w, int64_t R0, int64_t R1) {
-  const int64_t lo = D > R0 ? D : R0, hi = (D + 4) < R1 ? (D + 4) : R1;
-  if (lo >= hi) return;
-  if (lo == D && hi == D + 4) {
-    *reinterpret_cast<uint32_t *>(out + D) = w;
-  } else {
-    for (int64_t b = lo; b < hi; ++b) out[b] = (uint8_t)(w >> (8 * (int)(b - D)));
-  }
-}
-
-__device__ __forceinline__ void grp_write(const DevBatch &B, GrpShared &sh, int64_t i_begin, int64_t i_end,
-                                          const int4 *__restrict__ rec4, const int2 *__restrict__ rec2, uint8_t *out,
-                                          int np) {
-  const int tid = threadIdx.x;
-  for (int64_t c0 = i_begin; c0 < i_end; c0 += kGrpTile) {
-    const int nh = (int)((i_end - c0) < kGrpTile ? (i_end - c0) : kGrpTile);
-    const int total = grp_tile(sh, rec4, rec2, c0, nh, true);
-    for (int t = tid; t < total; t += kGrpThreads) {
-      const int j = grp_find(sh, nh, total, t);
-      const int4 r = sh.rec[j];
-      const int L = sh.rec2[j].x & 0xFFFFFF;
-      const int q0 = 16 * (t - sh.pre[j]);
-      const int64_t R0 = i64_of(r.x, r.y) >> 1, R1 = R0 + ((L + 1) >> 1);
-      const int64_t B0 = R0 + (q0 >> 1), A = B0 & ~(int64_t)3;
-      const uint32_t *src = reinterpret_cast<const uint32_t *>(B.seq) + (A >> 2);
-      uint32_t w0 = src[0], w1 = src[1], w2 = src[2];
-      if (np) {
-        const unsigned long long lo_key = (unsigned long long)(2 * A) << 4;
-        int lo = 0, hi = np;
-        while (lo < hi) {
-          const int mid = (lo + hi) >> 1;
-          if (sh.patch[mid] < lo_key) lo = mid + 1;
-          else hi = mid;
-        }
-        for (int k = lo; k < np; ++k) {
-          const unsigned long long e = sh.patch[k];
-          const int64_t nib = (int64_t)(e >> 4);
-          if (nib >= 2 * A + 24) break;
-          const int off = (int)((nib >> 1) - A);
-          const uint32_t x = (uint32_t)(e & 15) << (8 * (off & 3) + ((nib & 1) ? 0 : 4));
-          if (off < 4) w0 ^= x;
-          else if (off < 8) w1 ^= x;
-          else w2 ^= x;
-        }
-      }
-      // dwords starting in [B0, B0 + 8), plus the read's leading partial dword for chunk 0
-      if (A >= B0 || (q0 == 0 && A < R0)) grp_store_dword(out, A, w0, R0, R1);
-      if (A + 4 >= B0) grp_store_dword(out, A + 4, w1, R0, R1);
-      if (A + 8 < B0 + 8) grp_store_dword(out, A + 8, w2, R0, R1);
+// Fused: apply the sorted in-partition list (nibble << 4 | from ^ to) with one plain byte store
+// per masked byte, seq[b] ^ mask — the partition copy of that byte has drained before.
+__device__ __forceinline__ void grp_patch_bytes(const DevBatch &B, GrpShared &sh, int np, uint8_t *out) {
+  for (int i = threadIdx.x; i < np; i += kGrpThreads) {
+    const unsigned long long e = sh.patch[i];
+    const int64_t byte = (int64_t)(e >> 5);
+    if (i > 0 && (int64_t)(sh.patch[i - 1] >> 5) == byte) continue;
+    uint32_t x = 0;
+    for (int k = i; k < np && (int64_t)(sh.patch[k] >> 5) == byte; ++k) {
+      const unsigned long long f = sh.patch[k];
+      x ^= (uint32_t)(f & 15) << (((f >> 4) & 1) ? 0 : 4);
     }
-    __syncthreads();
+    out[byte] = (uint8_t)(B.seq[byte] ^ x);
   }
 }
 
-// The raw write pass done, make its stores visible at the memory side before atomics patch
-// the same bytes (device atomics execute beyond the XCD's L2).
+// Make this workgroup's stores visible at the memory side before device atomics (which execute
+// beyond the XCD's L2) patch the same bytes.
 __device__ __forceinline__ void grp_release() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
   __syncthreads();
 }
 
-// groups: 2 x int4 per group {s_begin, s_end, seg_begin lo, hi}, {seg_end lo, hi, 0, 0}
-// FUSED: the group also stores its simple reads (grp_write); otherwise out is a prior copy of
-// seq and every patch is an atomic XOR.
+// groups: 3 x int4 per group, in launch order: {s_begin, s_end, seg_begin lo, hi},
+// {seg_end lo, hi, 0, 0}, {partition begin lo, hi, end lo, hi} (bytes; fused only).
 template <int U, bool FUSED>
 __global__ void __launch_bounds__(kGrpThreads) k_group(const DevBatch B, const int4 *__restrict__ groups,
                                                        const int4 *__restrict__ rec4, const int2 *__restrict__ rec2,
                                                        uint8_t *__restrict__ out, int32_t *scope_calls,
-                                                       int32_t *scope_bases, int skip) {
+                                                       int32_t *scope_bases, int32_t *part,
+                                                       unsigned long long *far, int *far_count, int64_t far_cap,
+                                                       int skip) {
   __shared__ GrpShared sh;
   const int tid = threadIdx.x;
-  const int4 g0 = groups[2 * blockIdx.x];
-  const int4 g1 = groups[2 * blockIdx.x + 1];
+  const int4 g0 = groups[3 * blockIdx.x];
+  const int4 g1 = groups[3 * blockIdx.x + 1];
+  const int4 g2 = groups[3 * blockIdx.x + 2];
   const int s_begin = g0.x;
   const int64_t i_begin = i64_of(g0.z, g0.w), i_end = i64_of(g1.x, g1.y);
+  PatchSink sink{out, i64_of(g2.x, g2.y), i64_of(g2.z, g2.w), far, far_count, far_cap, FUSED, FUSED, false};
+  if (FUSED && !(skip & kSkipCopy)) {
+    // the partition: whole 16-byte windows (the buffers are padded past seq_bytes)
+    for (int64_t D = sink.p0 + 16 * tid; D < sink.p1; D += 16 * kGrpThreads)
+      *reinterpret_cast<uint4 *>(out + D) = *reinterpret_cast<const uint4 *>(B.seq + D);
+    __builtin_amdgcn_s_waitcnt(0);   // drained before any mask store of this workgroup
+  }
   if (tid == 0) {
     sh.top = 0;
     sh.stk_lo[0] = 0ull;
     sh.stk_hi[0] = ~0ull;
     sh.stk_mode[0] = kModeCollect;
     sh.n_patch = 0;
+    sh.blk_calls = 0;
+    sh.blk_bases = 0;
   }
-  bool atomic_mode = !FUSED;   // out already holds raw bytes: patches are atomic XORs
   for (;;) {
     __syncthreads();
     const int top = sh.top;
-    if (top < 0) break;
+    if (top < 0) {
+      if (tid == 0) {   // per-workgroup partial totals (k_totals sums them)
+        part[2 * blockIdx.x] = sh.blk_calls;
+        part[2 * blockIdx.x + 1] = sh.blk_bases;
+      }
+      break;
+    }
     const GrpRange R{sh.stk_lo[top], sh.stk_hi[top], sh.stk_mode[top]};
     __syncthreads();
     if (tid == 0) {
@@ -1240,13 +1282,14 @@ __global__ void __launch_bounds__(kGrpThreads) k_group(const DevBatch B, const i
       sh.masked = 0;
     }
     __syncthreads();
-    grp_scan<U>(B, sh, R, s_begin, i_begin, i_end, rec4, rec2, out, skip);
+    grp_scan<U>(B, sh, R, sink, i_begin, i_end, rec4, rec2, skip);
     // (grp_scan ends on a barrier)
     if (skip & kSkipClassify) continue;
     const int s = s_begin + (int)(R.lo >> 52);
     if (R.mode == kModeFlags) {
       if (tid == 0 && sh.flags == 3 && !grp_kept(B, s, (int64_t)((R.lo >> 4) & kNibMask), (int)(R.lo & 15))) {
         atomicAdd(&scope_calls[s], 1);
+        sh.blk_calls += 1;
         const int t = ++sh.top;
         sh.stk_lo[t] = R.lo;
         sh.stk_hi[t] = R.hi;
@@ -1255,7 +1298,10 @@ __global__ void __launch_bounds__(kGrpThreads) k_group(const DevBatch B, const i
       continue;
     }
     if (R.mode == kModePatch) {
-      if (tid == 0 && sh.masked) atomicAdd(&scope_bases[s], sh.masked);
+      if (tid == 0 && sh.masked) {
+        atomicAdd(&scope_bases[s], sh.masked);
+        sh.blk_bases += sh.masked;
+      }
       continue;
     }
     const int n = sh.n_obs;
@@ -1264,12 +1310,12 @@ __global__ void __launch_bounds__(kGrpThreads) k_group(const DevBatch B, const i
         atomicMin(&sh.kmin, sh.key[i]);
         atomicMax(&sh.kmax, sh.key[i]);
       }
-      __syncthreads();
-      if (!atomic_mode) {
-        grp_write(B, sh, i_begin, i_end, rec4, rec2, out, 0);
+      if (sink.lds) {
+        // bisection from here on: in-partition masks become atomics after a release
         grp_release();
-        atomic_mode = true;
+        sink.lds = false;
       }
+      __syncthreads();
       if (tid == 0) {
         const unsigned long long a = sh.kmin, b = sh.kmax;
         int t = sh.top;
@@ -1293,39 +1339,38 @@ __global__ void __launch_bounds__(kGrpThreads) k_group(const DevBatch B, const i
       }
       continue;
     }
-    if (atomic_mode) {
-      grp_classify(B, sh, n, s_begin, out, scope_calls, scope_bases, kClsCount);
-      continue;
-    }
-    // fused, whole group in one list: patches in registers during the write pass
-    grp_classify(B, sh, n, s_begin, out, scope_calls, scope_bases, kClsCount | kClsList);
+    grp_classify(B, sh, n, s_begin, sink, scope_calls, scope_bases, true);
+    if (!sink.lds) continue;
+    // fused, whole group in one list: in-partition masks as byte stores
     __syncthreads();
     const int np = sh.n_patch;
     if (np <= kGrpPatch) {
-      lds_bitonic(sh.patch, nullptr, np);
-      grp_write(B, sh, i_begin, i_end, rec4, rec2, out, np);
+      if (np) {
+        lds_bitonic(sh.patch, nullptr, np);
+        grp_patch_bytes(B, sh, np, out);
+      }
     } else {
-      grp_write(B, sh, i_begin, i_end, rec4, rec2, out, 0);
       grp_release();
-      grp_classify(B, sh, n, s_begin, out, scope_calls, scope_bases, kClsStoredAtomic);
+      PatchSink again = sink;
+      again.lds = false;
+      again.in_only = true;
+      grp_classify(B, sh, n, s_begin, again, scope_calls, scope_bases, false);
     }
   }
 }
 
-// Byte ranges of reads no group stores (pass-through reads, reads with clips or indels): one
-// wave per range, whole dwords inside it, its partial edge dwords byte by byte.
-__global__ void __launch_bounds__(kBlock) k_copy_ranges(const uint8_t *__restrict__ seq,
-                                                        const int64_t *__restrict__ rng, int n,
+// Fused: masks of bytes outside the masking workgroup's partition, after every partition is
+// written (a later kernel).
+__global__ void __launch_bounds__(kBlock) k_far_patches(const unsigned long long *__restrict__ far,
+                                                        const int *__restrict__ far_count, int64_t cap,
                                                         uint8_t *__restrict__ out) {
-  const int lane = threadIdx.x & 63;
-  const int gw = (blockIdx.x * kBlock + threadIdx.x) >> 6;
-  const int nw = (gridDim.x * kBlock) >> 6;
-  for (int i = gw; i < n; i += nw) {
-    const int64_t b = rng[2 * i], e = rng[2 * i + 1];
-    for (int64_t D = (b & ~(int64_t)3) + 4 * lane; D < e; D += 256) {
-      const uint32_t w = *reinterpret_cast<const uint32_t *>(seq + D);
-      grp_store_dword(out, D, w, b, e);
-    }
+  const int64_t n = min((int64_t)*far_count, cap);
+  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+    const unsigned long long e = far[i];
+    const int64_t nib = (int64_t)(e >> 4);
+    const int64_t byte = nib >> 1;
+    const int sh = 8 * (int)(byte & 3) + ((nib & 1) ? 0 : 4);
+    atomicXor(reinterpret_cast<uint32_t *>(out) + (byte >> 2), (uint32_t)(e & 15) << sh);
   }
 }
 
@@ -1424,13 +1469,22 @@ __global__ void __launch_bounds__(kBlock) k_mask_large(const DevBatch B, const i
   }
 }
 
+// Totals: per-scope counts of the scopes in ids (all n scopes when ids is null) plus the
+// (calls, bases) partials of the group kernel's workgroups.
 __global__ void __launch_bounds__(kBlock) k_totals(const int32_t *__restrict__ calls, const int32_t *__restrict__ bases,
-                                                   int n, const int32_t *rare_small, const int32_t *rare_tiles,
+                                                   const int32_t *__restrict__ ids, int n,
+                                                   const int32_t *__restrict__ grp_part, int n_part,
+                                                   const int32_t *rare_small, const int32_t *rare_tiles,
                                                    unsigned long long *totals) {
   long long c = 0, b = 0;
   for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
-    c += calls[i];
-    b += bases[i];
+    const int s = ids ? ids[i] : i;
+    c += calls[s];
+    b += bases[s];
+  }
+  for (int i = blockIdx.x * kBlock + threadIdx.x; i < n_part; i += gridDim.x * kBlock) {
+    c += grp_part[2 * i];
+    b += grp_part[2 * i + 1];
   }
   // one same-address atomic per workgroup: they serialize at the memory side
   __shared__ long long part[2][kWaves];
@@ -1507,8 +1561,10 @@ struct ganon_dbatch {
   int2 *seg2 = nullptr;                 // k_group: per segment {length | flags, scope_local}
   int32_t n_groups = 0;
   int64_t n_seg = 0;
-  int64_t *copy_ranges = nullptr;       // k_copy_ranges: [begin, end) byte pairs
-  int32_t n_copy_ranges = 0;
+  unsigned long long *far = nullptr;    // fused: masks outside the masking group's partition
+  int64_t far_cap = 0;
+  int32_t *grp_part = nullptr;          // k_group: (calls, bases) per workgroup
+  int32_t *large_ids = nullptr;         // scopes of the tile path
   bool ran = false;
 };
 
@@ -1684,7 +1740,7 @@ GANON_API int ganon_ctx_set_param(ganon_ctx *ctx, int param, int value) {
     return GANON_OK;
   }
   if (param == GANON_PARAM_GROUP_SKIP) {
-    ctx->group_skip = value & (kSkipClassify | kSkipChunks);
+    ctx->group_skip = value & (kSkipClassify | kSkipChunks | kSkipCopy);
     return GANON_OK;
   }
   return fail(ctx, GANON_E_ARG, "unknown parameter %d", param);
@@ -1867,6 +1923,7 @@ GANON_API int ganon_batch_upload(ganon_ctx *ctx, const ganon_batch *b, ganon_dba
   if ((rc = dev_copy(ctx, db, &db->large_written, large_written.data(), large_written.size()))) return bail(rc);
   db->n_large_written = (int32_t)large_written.size();
   db->n_large_scopes = (int32_t)large_scopes.size();
+  if ((rc = dev_copy(ctx, db, &db->large_ids, large_scopes.data(), large_scopes.size()))) return bail(rc);
   db->max_small_span = max_small;
   {
     // per-incidence records for the v2 scope kernel (scope-major, one int4 each)
@@ -1908,29 +1965,28 @@ GANON_API int ganon_batch_upload(ganon_ctx *ctx, const ganon_batch *b, ganon_dba
     }
   }
   {
-    // k_group_v4: aligned segments of every read of every small scope, scope-major, packed
-    // into groups of consecutive scopes
-    std::vector<int4> s4, grp;
+    // group kernels: aligned segments of every read of every small scope, scope-major, packed
+    // into groups of consecutive scopes; groups launch in the order of their written reads in
+    // the sequence buffer, each owning the 128-byte-aligned partition of out from its first
+    // written read to the next group's (fused variant)
+    std::vector<int4> s4;
     std::vector<int2> s2;
     s4.reserve((size_t)b->n_incid);
     s2.reserve((size_t)b->n_incid);
     auto lo32 = [](int64_t v) { return (int)(uint32_t)(uint64_t)v; };
     auto hi32 = [](int64_t v) { return (int)(uint32_t)((uint64_t)v >> 32); };
-    // one M/=/X op over the whole read: a single segment, stored by the fused write pass
-    auto simple_read = [&](int32_t r) {
-      if (b->n_cig[r] != 1 || b->read_len[r] <= 0) return false;
-      const uint32_t w = b->cigar[b->cig_off[r]];
-      const int op = w & 0xF;
-      return (op == 0 || op == 7 || op == 8) && (int64_t)(w >> 4) == b->read_len[r];
+    struct G {
+      int32_t s0, s1;
+      int64_t i0, i1, first;   // first: lowest seq_off of a read the group writes
     };
+    std::vector<G> gs;
     int32_t g_s0 = -1;
-    int64_t g_i0 = 0;
+    int64_t g_i0 = 0, g_first = INT64_MAX;
     auto close_group = [&](int32_t s_end) {
       if (g_s0 < 0) return;
-      const int64_t i1 = (int64_t)s4.size();
-      grp.push_back(make_int4(g_s0, s_end, lo32(g_i0), hi32(g_i0)));
-      grp.push_back(make_int4(lo32(i1), hi32(i1), 0, 0));
+      gs.push_back(G{g_s0, s_end, g_i0, (int64_t)s4.size(), g_first});
       g_s0 = -1;
+      g_first = INT64_MAX;
     };
     auto segments_of = [&](int32_t r, auto &&emit) {
       const int64_t L = b->read_len[r];
@@ -1966,7 +2022,10 @@ GANON_API int ganon_batch_upload(ganon_ctx *ctx, const ganon_batch *b, ganon_dba
         const int32_t r = b->incid_read[i];
         if (b->read_len[r] >= (1 << 24)) return bail(fail(ctx, GANON_E_ARG, "read %d longer than 16 Mb", r));
         uint32_t fl = (uint32_t)b->dataset[r] << 24;
-        if (b->write_scope[r] == s) fl |= kSegMine | (simple_read(r) ? kSegWrite : 0u);
+        if (b->write_scope[r] == s) {
+          fl |= kSegMine;
+          g_first = std::min(g_first, b->seq_off[r]);
+        }
         const int64_t qnib = 2 * b->seq_off[r];
         segments_of(r, [&](int64_t q, int64_t p, int64_t n) {
           s4.push_back(make_int4(lo32(qnib + q), hi32(qnib + q), lo32(ref0 + p), hi32(ref0 + p)));
@@ -1977,31 +2036,46 @@ GANON_API int ganon_batch_upload(ganon_ctx *ctx, const ganon_batch *b, ganon_dba
       }
     }
     close_group(b->n_scopes);
+    const int32_t ng = (int32_t)gs.size();
+    std::vector<int32_t> order(ng);
+    for (int32_t k = 0; k < ng; ++k) order[k] = k;
+    std::stable_sort(order.begin(), order.end(), [&](int32_t x, int32_t y) { return gs[x].first < gs[y].first; });
+    // partitions: [part[k], part[k + 1]) for the k-th group launched
+    std::vector<int64_t> part(ng + 1), rank(ng);
+    part[0] = 0;
+    for (int32_t k = 1; k < ng; ++k) {
+      const int64_t f = std::min(gs[order[k]].first, b->seq_bytes);
+      part[k] = std::max(part[k - 1], f / kPartAlign * kPartAlign);
+    }
+    if (ng) part[ng] = b->seq_bytes;
+    for (int32_t k = 0; k < ng; ++k) rank[order[k]] = k;
+    // exact bound on masks landing outside the masking group's partition: every nibble of a
+    // written read that lies outside it
+    int64_t far_cap = 0;
+    for (int32_t r = 0; r < b->n_reads; ++r) {
+      const int32_t ws = b->write_scope[r];
+      if (ws < 0 || tab_off[ws] >= 0 || b->read_len[r] == 0) continue;
+      const int64_t k = rank[std::upper_bound(gs.begin(), gs.end(), ws,
+                                              [](int32_t v, const G &g) { return v < g.s0; }) - gs.begin() - 1];
+      const int64_t r0 = b->seq_off[r], r1 = r0 + ((int64_t)b->read_len[r] + 1) / 2;
+      const int64_t in = std::max<int64_t>(0, std::min(r1, part[k + 1]) - std::max(r0, part[k]));
+      far_cap += 2 * ((r1 - r0) - in);
+    }
+    std::vector<int4> grp(3 * (size_t)ng);
+    for (int32_t k = 0; k < ng; ++k) {
+      const G &g = gs[order[k]];
+      grp[3 * k] = make_int4(g.s0, g.s1, lo32(g.i0), hi32(g.i0));
+      grp[3 * k + 1] = make_int4(lo32(g.i1), hi32(g.i1), 0, 0);
+      grp[3 * k + 2] = make_int4(lo32(part[k]), hi32(part[k]), lo32(part[k + 1]), hi32(part[k + 1]));
+    }
     if ((rc = dev_copy(ctx, db, &db->groups, grp.data(), grp.size()))) return bail(rc);
     if ((rc = dev_copy(ctx, db, &db->seg4, s4.data(), s4.size()))) return bail(rc);
     if ((rc = dev_copy(ctx, db, &db->seg2, s2.data(), s2.size()))) return bail(rc);
-    db->n_groups = (int32_t)(grp.size() / 2);
+    db->n_groups = ng;
+    if ((rc = dev_alloc(ctx, db, &db->grp_part, 2 * (size_t)ng))) return bail(rc);
     db->n_seg = (int64_t)s4.size();
-    // byte ranges no fused group stores: reads out of every scope, reads with clips or indels
-    // (wide-scope reads are written whole by k_mask_large); adjacent ranges merged
-    std::vector<std::pair<int64_t, int64_t>> rs;
-    for (int32_t r = 0; r < b->n_reads; ++r) {
-      const int64_t h = ((int64_t)b->read_len[r] + 1) / 2;
-      const int32_t ws = b->write_scope[r];
-      if (h == 0 || (ws >= 0 && (tab_off[ws] >= 0 || simple_read(r)))) continue;
-      rs.emplace_back(b->seq_off[r], b->seq_off[r] + h);
-    }
-    std::sort(rs.begin(), rs.end());
-    std::vector<int64_t> ranges;
-    for (const auto &x : rs) {
-      if (!ranges.empty() && x.first <= ranges.back()) ranges.back() = std::max(ranges.back(), x.second);
-      else {
-        ranges.push_back(x.first);
-        ranges.push_back(x.second);
-      }
-    }
-    if ((rc = dev_copy(ctx, db, &db->copy_ranges, ranges.data(), ranges.size()))) return bail(rc);
-    db->n_copy_ranges = (int32_t)(ranges.size() / 2);
+    db->far_cap = far_cap;
+    if ((rc = dev_alloc(ctx, db, &db->far, (size_t)far_cap))) return bail(rc);
   }
   if ((rc = dev_alloc(ctx, db, &db->out, (size_t)b->seq_bytes))) return bail(rc);
   // bytes outside every read are never written by the fused variant: make them defined
@@ -2046,22 +2120,15 @@ GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
                              hipMemcpyDeviceToDevice, st));
   const bool v3 = ctx->variant == GANON_VARIANT_PERSIST;
   const bool v2 = ctx->variant == GANON_VARIANT_COPYPATCH;
-  const bool v5 = ctx->variant == GANON_VARIANT_GROUP_FUSED;
-  const bool v4 = ctx->variant == GANON_VARIANT_DEFAULT || ctx->variant == GANON_VARIANT_GROUP || v5;
+  const bool v5 = ctx->variant == GANON_VARIANT_DEFAULT || ctx->variant == GANON_VARIANT_GROUP_FUSED;
+  const bool v4 = ctx->variant == GANON_VARIANT_GROUP || v5;   // group kernels
   if (db->n_large_scopes || v4) {
     // counted with atomics (tiles of wide scopes; group run heads)
     HIP_OR_FAIL(hipMemsetAsync(db->scope_calls, 0, (size_t)db->n_scopes * sizeof(int32_t), st));
     HIP_OR_FAIL(hipMemsetAsync(db->scope_bases, 0, (size_t)db->n_scopes * sizeof(int32_t), st));
   }
-  if (v5) {
-    // reads no group stores, copied first (a separate kernel: its stores are complete and
-    // visible before the group kernel patches any of those bytes atomically)
-    if (db->n_copy_ranges) {
-      KernelScope ks(ctx, "k_copy_ranges");
-      const int grid = std::min<int>((db->n_copy_ranges + kWaves - 1) / kWaves, 8192);
-      k_copy_ranges<<<grid, kBlock, 0, st>>>(B.seq, db->copy_ranges, db->n_copy_ranges, db->out);
-      if ((rc = check_launch(ctx, "k_copy_ranges"))) return rc;
-    }
+  if (v5 && db->n_groups) {
+    // the fused group kernel writes every byte of out (its partitions tile [0, seq_bytes))
   } else if (v2 || v3 || v4) {
     // copy-then-patch: every read's bytes first, the scope kernels patch masked nibbles
     KernelScope ks(ctx, "copy_seq");
@@ -2080,8 +2147,14 @@ GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
                    : (u == 2 ? k_group<2, false> : u == 4 ? k_group<4, false> : u == 8 ? k_group<8, false>
                                                                                        : k_group<1, false>);
     kern<<<db->n_groups, kGrpThreads, 0, st>>>(B, db->groups, db->seg4, db->seg2, db->out, db->scope_calls,
-                                               db->scope_bases, ctx->group_skip);
+                                               db->scope_bases, db->grp_part, db->far, db->counters + 2,
+                                               db->far_cap, ctx->group_skip);
     if ((rc = check_launch(ctx, "k_group"))) return rc;
+  }
+  if (v5 && db->far_cap) {
+    KernelScope ks(ctx, "k_far_patches");
+    k_far_patches<<<64, kBlock, 0, st>>>(db->far, db->counters + 2, db->far_cap, db->out);
+    if ((rc = check_launch(ctx, "k_far_patches"))) return rc;
   }
   const int caps[2] = {kSmallCap0, kSmallCap1};
   for (int k = 0; k < 2 && !v4; ++k) {
@@ -2148,8 +2221,13 @@ GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
   {
     KernelScope ks(ctx, "k_totals");
     const int grid = std::max(1, std::min<int>((db->n_scopes + kBlock - 1) / kBlock, 128));
-    k_totals<<<grid, kBlock, 0, st>>>(db->scope_calls, db->scope_bases, db->n_scopes, db->counters + 0,
-                                      db->counters + 1, db->totals);
+    // group variants: their workgroups' partials plus the wide scopes' own counts
+    if (v4 && db->n_groups)
+      k_totals<<<grid, kBlock, 0, st>>>(db->scope_calls, db->scope_bases, db->large_ids, db->n_large_scopes,
+                                        db->grp_part, db->n_groups, db->counters + 0, db->counters + 1, db->totals);
+    else
+      k_totals<<<grid, kBlock, 0, st>>>(db->scope_calls, db->scope_bases, nullptr, db->n_scopes, nullptr, 0,
+                                        db->counters + 0, db->counters + 1, db->totals);
     if ((rc = check_launch(ctx, "k_totals"))) return rc;
   }
   db->ran = true;

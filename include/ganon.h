@@ -95,16 +95,15 @@ GANON_API const char *ganon_last_error(ganon_ctx *ctx);
 GANON_API int ganon_abi_version(void);
 /* Use an external hipStream_t (e.g. torch's current stream); NULL = the ctx's own. */
 GANON_API int ganon_ctx_set_stream(ganon_ctx *ctx, void *hip_stream);
-/* Small-scope kernel: GANON_VARIANT_DEFAULT (= GROUP),
+/* Small-scope kernel: GANON_VARIANT_DEFAULT (= GROUP_FUSED),
  * GANON_VARIANT_BLOCK (one 256-thread workgroup per scope, the first version),
  * GANON_VARIANT_WAVE (one wave per scope writing whole reads), GANON_VARIANT_COPYPATCH
  * (copy-then-patch, one 64-thread workgroup per scope), GANON_VARIANT_GROUP (copy-then-patch,
  * one workgroup per group of consecutive scopes, calls from a sorted observation list),
- * GANON_VARIANT_GROUP_FUSED (the group kernel also stores its reads, patched in registers: no
- * separate copy), GANON_VARIANT_PERSIST (copy-then-patch, persistent waves, one scope per
- * wave). The non-default ones are kept for A/B runs and cross-checks; all give identical
- * results for every byte that belongs to a read (bytes of seq_out outside every read's
- * [seq_off, seq_off + ceil(len/2)) are left untouched by GROUP_FUSED). */
+ * GANON_VARIANT_GROUP_FUSED (no separate copy: each group workgroup copies its own line-aligned
+ * partition of the output and masks with byte stores), GANON_VARIANT_PERSIST (copy-then-patch,
+ * persistent waves, one scope per wave). The non-default ones are kept for A/B runs and
+ * cross-checks; all give identical results. */
 enum {
   GANON_VARIANT_DEFAULT = 0,
   GANON_VARIANT_BLOCK = 1,

@@ -13,7 +13,7 @@ from helpers import load_scope_golden, run_pipeline_vs_golden, written_reads_equ
 pytestmark = pytest.mark.gpu
 
 VARIANTS = (0, 1, 2, 3, 4, 5, 6)   # include/ganon.h GANON_VARIANT_*
-MAIN = (0, 5, 6)                  # default (group + copy), fused group, persistent waves
+MAIN = (0, 4, 6)                  # default (fused group), group + copy, persistent waves
 
 
 @pytest.fixture(scope="module")

@@ -905,13 +905,13 @@ __global__ void __launch_bounds__(256) k_scope_v3(const DevBatch B, const int4 *
 // 16-byte stores before scanning (its reads' bases are then L2-hot for the scan). Masks inside
 // the partition are plain byte stores seq[b] ^ mask after the copy has drained; masks of
 // bytes in another workgroup's partition (a read crossing a partition boundary) go to a
-// global list applied by k_far_patches after the kernel. Partial-line stores from different
+// global list applied by k_finish after the kernel. Partial-line stores from different
 // workgroups cost ~4x whole-line stores on MI355X (tools/membench.hip), hence partitions.
 constexpr int kGrpThreads = 256;
 constexpr int kGrpTile = 256;        // segment records staged per tile
 constexpr int kGrpTarget = 256;      // segments per group (a larger scope forms its own group)
 constexpr int kGrpObs = 512;         // observations per LDS list
-constexpr int kGrpMaxScopes = 4096;  // scopes per group (12-bit local index)
+constexpr int kGrpMaxScopes = 256;   // scopes per group (12-bit local index field)
 constexpr int kGrpStack = 80;        // key ranges pending (bisection depth <= 64)
 constexpr int kGrpPatch = 256;       // in-partition masks of a fused workgroup, sorted in LDS
 constexpr int kGrpMap = 4096;        // chunk -> segment map entries (larger tiles binary-search)
@@ -939,6 +939,8 @@ struct GrpShared {
   unsigned long long kmin, kmax;
   int top, n_obs, flags, masked, n_patch;
   int blk_calls, blk_bases;         // this workgroup's contribution to the totals
+  int cnt_calls[kGrpMaxScopes];     // per-scope counts, written out once at the end
+  int cnt_bases[kGrpMaxScopes];
 };
 
 struct GrpRange {
@@ -1146,9 +1148,19 @@ __device__ __forceinline__ void lds_bitonic(unsigned long long *key, unsigned lo
 // observation against the whole list (no sort, no barrier); longer lists are sorted and one
 // thread takes each run of equal keys. count: add calls/bases to the per-scope and workgroup
 // totals (off for a re-run that only re-applies masks).
+__device__ __forceinline__ void grp_count(GrpShared &sh, int s_local, int calls, int bases) {
+  if (calls) {
+    atomicAdd(&sh.cnt_calls[s_local], calls);
+    atomicAdd(&sh.blk_calls, calls);
+  }
+  if (bases) {
+    atomicAdd(&sh.cnt_bases[s_local], bases);
+    atomicAdd(&sh.blk_bases, bases);
+  }
+}
+
 __device__ __forceinline__ void grp_classify(const DevBatch &B, GrpShared &sh, int n, int s_begin,
-                                             const PatchSink &sink, int32_t *scope_calls, int32_t *scope_bases,
-                                             bool count) {
+                                             const PatchSink &sink, bool count) {
   const int tid = threadIdx.x;
   if (n <= kGrpQuad) {
     if (tid >= n) return;
@@ -1164,18 +1176,10 @@ __device__ __forceinline__ void grp_classify(const DevBatch &B, GrpShared &sh, i
     const int s = s_begin + (int)(key >> 52);
     const int c = (int)(key & 15);
     if (grp_kept(B, s, (int64_t)((key >> 4) & kNibMask), c)) return;
-    if (count && head) {
-      atomicAdd(&scope_calls[s], 1);
-      atomicAdd(&sh.blk_calls, 1);
-    }
     const unsigned long long p = sh.pay[tid];
-    if ((p >> 53) & 1) {
-      sink_patch(sh, sink, (int64_t)(p & kNibMask), c, (int)((p >> 48) & 15));
-      if (count) {
-        atomicAdd(&scope_bases[s], 1);
-        atomicAdd(&sh.blk_bases, 1);
-      }
-    }
+    const int mine = (int)((p >> 53) & 1);
+    if (mine) sink_patch(sh, sink, (int64_t)(p & kNibMask), c, (int)((p >> 48) & 15));
+    if (count) grp_count(sh, s - s_begin, head ? 1 : 0, mine);
     return;
   }
   lds_bitonic(sh.key, sh.pay, n);
@@ -1195,14 +1199,7 @@ __device__ __forceinline__ void grp_classify(const DevBatch &B, GrpShared &sh, i
       sink_patch(sh, sink, (int64_t)(p & kNibMask), c, (int)((p >> 48) & 15));
       ++masked;
     }
-    if (count) {
-      atomicAdd(&scope_calls[s], 1);
-      atomicAdd(&sh.blk_calls, 1);
-      if (masked) {
-        atomicAdd(&scope_bases[s], masked);
-        atomicAdd(&sh.blk_bases, masked);
-      }
-    }
+    if (count) grp_count(sh, s - s_begin, 1, masked);
   }
 }
 
@@ -1232,25 +1229,31 @@ __device__ __forceinline__ void grp_release() {
 // groups: 3 x int4 per group, in launch order: {s_begin, s_end, seg_begin lo, hi},
 // {seg_end lo, hi, 0, 0}, {partition begin lo, hi, end lo, hi} (bytes; fused only).
 template <int U, bool FUSED>
-__global__ void __launch_bounds__(kGrpThreads) k_group(const DevBatch B, const int4 *__restrict__ groups,
+__global__ void __launch_bounds__(kGrpThreads, 6) k_group(const DevBatch B, const int4 *__restrict__ groups,
                                                        const int4 *__restrict__ rec4, const int2 *__restrict__ rec2,
                                                        uint8_t *__restrict__ out, int32_t *scope_calls,
                                                        int32_t *scope_bases, int32_t *part,
                                                        unsigned long long *far, int *far_count, int64_t far_cap,
-                                                       int skip) {
+                                                       int skip, int nt_copy) {
   __shared__ GrpShared sh;
   const int tid = threadIdx.x;
   const int4 g0 = groups[3 * blockIdx.x];
   const int4 g1 = groups[3 * blockIdx.x + 1];
   const int4 g2 = groups[3 * blockIdx.x + 2];
-  const int s_begin = g0.x;
+  const int s_begin = g0.x, s_end = g0.y;
   const int64_t i_begin = i64_of(g0.z, g0.w), i_end = i64_of(g1.x, g1.y);
   PatchSink sink{out, i64_of(g2.x, g2.y), i64_of(g2.z, g2.w), far, far_count, far_cap, FUSED, FUSED, false};
   if (FUSED && !(skip & kSkipCopy)) {
-    // the partition: whole 16-byte windows (the buffers are padded past seq_bytes)
-    for (int64_t D = sink.p0 + 16 * tid; D < sink.p1; D += 16 * kGrpThreads)
-      *reinterpret_cast<uint4 *>(out + D) = *reinterpret_cast<const uint4 *>(B.seq + D);
-    __builtin_amdgcn_s_waitcnt(0);   // drained before any mask store of this workgroup
+    // the partition: whole 16-byte windows (the buffers are padded past seq_bytes); the stores
+    // drain while the scan runs (s_waitcnt before the mask stores)
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    if (nt_copy) {
+      for (int64_t D = sink.p0 + 16 * tid; D < sink.p1; D += 16 * kGrpThreads)
+        __builtin_nontemporal_store(*reinterpret_cast<const u32x4 *>(B.seq + D), reinterpret_cast<u32x4 *>(out + D));
+    } else {
+      for (int64_t D = sink.p0 + 16 * tid; D < sink.p1; D += 16 * kGrpThreads)
+        *reinterpret_cast<u32x4 *>(out + D) = *reinterpret_cast<const u32x4 *>(B.seq + D);
+    }
   }
   if (tid == 0) {
     sh.top = 0;
@@ -1261,11 +1264,22 @@ __global__ void __launch_bounds__(kGrpThreads) k_group(const DevBatch B, const i
     sh.blk_calls = 0;
     sh.blk_bases = 0;
   }
+  for (int i = tid; i < kGrpMaxScopes; i += kGrpThreads) {
+    sh.cnt_calls[i] = 0;
+    sh.cnt_bases[i] = 0;
+  }
   for (;;) {
     __syncthreads();
     const int top = sh.top;
     if (top < 0) {
-      if (tid == 0) {   // per-workgroup partial totals (k_totals sums them)
+      // per-scope counts (wide scopes in the id range belong to the tile path) and the
+      // workgroup's partial totals (k_finish sums them)
+      for (int i = tid; i < s_end - s_begin; i += kGrpThreads) {
+        if (B.span_len[s_begin + i] > kSmallCap1) continue;
+        scope_calls[s_begin + i] = sh.cnt_calls[i];
+        scope_bases[s_begin + i] = sh.cnt_bases[i];
+      }
+      if (tid == 0) {
         part[2 * blockIdx.x] = sh.blk_calls;
         part[2 * blockIdx.x + 1] = sh.blk_bases;
       }
@@ -1288,8 +1302,7 @@ __global__ void __launch_bounds__(kGrpThreads) k_group(const DevBatch B, const i
     const int s = s_begin + (int)(R.lo >> 52);
     if (R.mode == kModeFlags) {
       if (tid == 0 && sh.flags == 3 && !grp_kept(B, s, (int64_t)((R.lo >> 4) & kNibMask), (int)(R.lo & 15))) {
-        atomicAdd(&scope_calls[s], 1);
-        sh.blk_calls += 1;
+        grp_count(sh, s - s_begin, 1, 0);
         const int t = ++sh.top;
         sh.stk_lo[t] = R.lo;
         sh.stk_hi[t] = R.hi;
@@ -1298,10 +1311,7 @@ __global__ void __launch_bounds__(kGrpThreads) k_group(const DevBatch B, const i
       continue;
     }
     if (R.mode == kModePatch) {
-      if (tid == 0 && sh.masked) {
-        atomicAdd(&scope_bases[s], sh.masked);
-        sh.blk_bases += sh.masked;
-      }
+      if (tid == 0) grp_count(sh, s - s_begin, 0, sh.masked);
       continue;
     }
     const int n = sh.n_obs;
@@ -1339,9 +1349,11 @@ __global__ void __launch_bounds__(kGrpThreads) k_group(const DevBatch B, const i
       }
       continue;
     }
-    grp_classify(B, sh, n, s_begin, sink, scope_calls, scope_bases, true);
+    grp_classify(B, sh, n, s_begin, sink, true);
     if (!sink.lds) continue;
-    // fused, whole group in one list: in-partition masks as byte stores
+    // fused, whole group in one list: in-partition masks as byte stores, after every wave's
+    // partition stores have drained
+    __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     const int np = sh.n_patch;
     if (np <= kGrpPatch) {
@@ -1354,24 +1366,75 @@ __global__ void __launch_bounds__(kGrpThreads) k_group(const DevBatch B, const i
       PatchSink again = sink;
       again.lds = false;
       again.in_only = true;
-      grp_classify(B, sh, n, s_begin, again, scope_calls, scope_bases, false);
+      grp_classify(B, sh, n, s_begin, again, false);
     }
   }
 }
 
-// Fused: masks of bytes outside the masking workgroup's partition, after every partition is
-// written (a later kernel).
-__global__ void __launch_bounds__(kBlock) k_far_patches(const unsigned long long *__restrict__ far,
-                                                        const int *__restrict__ far_count, int64_t cap,
-                                                        uint8_t *__restrict__ out) {
-  const int64_t n = min((int64_t)*far_count, cap);
-  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+// Last kernel of a group-variant run. (1) Fused: masks of bytes outside the masking
+// workgroup's partition (every partition is written by now). (2) Totals: the group
+// workgroups' partials plus the wide scopes' counts, reduced per workgroup into acc; the last
+// workgroup to finish (ticket acc[2]) writes totals = static values + sums + rare counts and
+// resets acc and counters for the next run — no memset or copy is launched per run.
+// counters: [0] rare small scopes, [1] rare tiles, [2] far masks.
+__global__ void __launch_bounds__(kBlock) k_finish(const unsigned long long *__restrict__ far, int64_t far_cap,
+                                                   uint8_t *__restrict__ out, const int32_t *__restrict__ grp_part,
+                                                   int n_groups, const int32_t *__restrict__ large_ids, int n_large,
+                                                   const int32_t *__restrict__ scope_calls,
+                                                   const int32_t *__restrict__ scope_bases,
+                                                   const unsigned long long *__restrict__ static_totals,
+                                                   int32_t *counters, unsigned long long *acc,
+                                                   unsigned long long *totals) {
+  const int64_t gtid = blockIdx.x * (int64_t)kBlock + threadIdx.x, gstride = (int64_t)gridDim.x * kBlock;
+  const int64_t n_far = min((int64_t)counters[2], far_cap);
+  for (int64_t i = gtid; i < n_far; i += gstride) {
     const unsigned long long e = far[i];
     const int64_t nib = (int64_t)(e >> 4);
     const int64_t byte = nib >> 1;
     const int sh = 8 * (int)(byte & 3) + ((nib & 1) ? 0 : 4);
     atomicXor(reinterpret_cast<uint32_t *>(out) + (byte >> 2), (uint32_t)(e & 15) << sh);
   }
+  long long c = 0, b = 0;
+  for (int64_t i = gtid; i < n_groups; i += gstride) {
+    c += grp_part[2 * i];
+    b += grp_part[2 * i + 1];
+  }
+  for (int64_t i = gtid; i < n_large; i += gstride) {
+    c += scope_calls[large_ids[i]];
+    b += scope_bases[large_ids[i]];
+  }
+  __shared__ long long part[2][kWaves];
+  __shared__ int last;
+  for (int o = 32; o > 0; o >>= 1) {
+    c += __shfl_xor(c, o);
+    b += __shfl_xor(b, o);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    part[0][threadIdx.x >> 6] = c;
+    part[1][threadIdx.x >> 6] = b;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    c = b = 0;
+    for (int w = 0; w < kWaves; ++w) {
+      c += part[0][w];
+      b += part[1][w];
+    }
+    if (c) atomicAdd(&acc[0], (unsigned long long)c);
+    if (b) atomicAdd(&acc[1], (unsigned long long)b);
+    __threadfence();
+    last = atomicAdd(&acc[2], 1ull) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last || threadIdx.x != 0) return;
+  __threadfence();
+  const unsigned long long sc = atomicExch(&acc[0], 0ull), sb = atomicExch(&acc[1], 0ull);
+  atomicExch(&acc[2], 0ull);
+  for (int k = 0; k < GANON_N_TOTALS; ++k) totals[k] = static_totals[k];
+  totals[GANON_T_MASKED_SNV_CALLS] += sc;
+  totals[GANON_T_MASKED_BASES] += sb;
+  totals[GANON_T_RARE_SCOPES] += (unsigned long long)(atomicExch(&counters[0], 0) + atomicExch(&counters[1], 0));
+  atomicExch(&counters[2], 0);
 }
 
 // One workgroup per 16 Ki-position tile of a large scope: tally -> TN table (global).
@@ -1523,6 +1586,8 @@ struct ganon_ctx {
   int v3_blocks[2] = {1, 1};   // resident grid of k_scope_v3 per class (occupancy x CUs)
   int group_unroll = 1;        // GANON_PARAM_GROUP_UNROLL
   int group_skip = 0;          // GANON_PARAM_GROUP_SKIP (profiling only)
+  int group_target = kGrpTarget;   // GANON_PARAM_GROUP_TARGET
+  int nt_copy = 1;             // GANON_PARAM_NT_COPY
   std::string err;
   struct Rec { std::string name; hipEvent_t e0, e1; };
   std::vector<Rec> recs;
@@ -1561,6 +1626,7 @@ struct ganon_dbatch {
   int2 *seg2 = nullptr;                 // k_group: per segment {length | flags, scope_local}
   int32_t n_groups = 0;
   int64_t n_seg = 0;
+  unsigned long long *acc = nullptr;    // k_finish: calls, bases, workgroup ticket
   unsigned long long *far = nullptr;    // fused: masks outside the masking group's partition
   int64_t far_cap = 0;
   int32_t *grp_part = nullptr;          // k_group: (calls, bases) per workgroup
@@ -1737,6 +1803,15 @@ GANON_API int ganon_ctx_set_param(ganon_ctx *ctx, int param, int value) {
     if (value != 1 && value != 2 && value != 4 && value != 8)
       return fail(ctx, GANON_E_ARG, "group unroll must be 1, 2, 4 or 8 (got %d)", value);
     ctx->group_unroll = value;
+    return GANON_OK;
+  }
+  if (param == GANON_PARAM_GROUP_TARGET) {
+    if (value < 16 || value > 65536) return fail(ctx, GANON_E_ARG, "group target must be in [16, 65536] (got %d)", value);
+    ctx->group_target = value;
+    return GANON_OK;
+  }
+  if (param == GANON_PARAM_NT_COPY) {
+    ctx->nt_copy = value != 0;
     return GANON_OK;
   }
   if (param == GANON_PARAM_GROUP_SKIP) {
@@ -2012,7 +2087,8 @@ GANON_API int ganon_batch_upload(ganon_ctx *ctx, const ganon_batch *b, ganon_dba
       const int64_t i0 = b->scope_incid_off[s], i1 = b->scope_incid_off[s + 1];
       int64_t nseg = 0;
       for (int64_t i = i0; i < i1; ++i) segments_of(b->incid_read[i], [&](int64_t, int64_t, int64_t) { ++nseg; });
-      if (g_s0 >= 0 && ((int64_t)s4.size() - g_i0 + nseg > kGrpTarget || s - g_s0 >= kGrpMaxScopes)) close_group(s);
+      if (g_s0 >= 0 && ((int64_t)s4.size() - g_i0 + nseg > ctx->group_target || s - g_s0 >= kGrpMaxScopes))
+        close_group(s);
       if (g_s0 < 0) {
         g_s0 = s;
         g_i0 = (int64_t)s4.size();
@@ -2085,6 +2161,11 @@ GANON_API int ganon_batch_upload(ganon_ctx *ctx, const ganon_batch *b, ganon_dba
   if ((rc = dev_alloc(ctx, db, &db->scope_bases, (size_t)b->n_scopes))) return bail(rc);
   if ((rc = dev_alloc(ctx, db, &db->totals, GANON_N_TOTALS))) return bail(rc);
   if ((rc = dev_alloc(ctx, db, &db->counters, 4))) return bail(rc);
+  if ((rc = dev_alloc(ctx, db, &db->acc, 3))) return bail(rc);
+  // k_finish keeps these zero between runs
+  if (hipMemsetAsync(db->counters, 0, 4 * sizeof(int32_t), ctx->stream) != hipSuccess ||
+      hipMemsetAsync(db->acc, 0, 3 * sizeof(unsigned long long), ctx->stream) != hipSuccess)
+    return bail(fail(ctx, GANON_E_DEVICE, "hipMemsetAsync(counters) failed"));
   if ((rc = dev_alloc(ctx, db, &db->rare_small_list, small[0].size() + small[1].size()))) return bail(rc);
   if ((rc = dev_alloc(ctx, db, &db->rare_tile_list, tiles.size()))) return bail(rc);
   unsigned long long st[GANON_N_TOTALS] = {0};
@@ -2115,15 +2196,18 @@ GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
   hipStream_t st = ctx->stream;
   const DevBatch &B = db->B;
   int rc;
-  HIP_OR_FAIL(hipMemsetAsync(db->counters, 0, 4 * sizeof(int32_t), st));
-  HIP_OR_FAIL(hipMemcpyAsync(db->totals, db->static_totals, GANON_N_TOTALS * sizeof(unsigned long long),
-                             hipMemcpyDeviceToDevice, st));
   const bool v3 = ctx->variant == GANON_VARIANT_PERSIST;
   const bool v2 = ctx->variant == GANON_VARIANT_COPYPATCH;
   const bool v5 = ctx->variant == GANON_VARIANT_DEFAULT || ctx->variant == GANON_VARIANT_GROUP_FUSED;
   const bool v4 = ctx->variant == GANON_VARIANT_GROUP || v5;   // group kernels
-  if (db->n_large_scopes || v4) {
-    // counted with atomics (tiles of wide scopes; group run heads)
+  if (!v4) {
+    // group variants leave counters zero and write totals in k_finish
+    HIP_OR_FAIL(hipMemsetAsync(db->counters, 0, 4 * sizeof(int32_t), st));
+    HIP_OR_FAIL(hipMemcpyAsync(db->totals, db->static_totals, GANON_N_TOTALS * sizeof(unsigned long long),
+                               hipMemcpyDeviceToDevice, st));
+  }
+  if (db->n_large_scopes) {
+    // wide scopes are counted with atomics (tiles)
     HIP_OR_FAIL(hipMemsetAsync(db->scope_calls, 0, (size_t)db->n_scopes * sizeof(int32_t), st));
     HIP_OR_FAIL(hipMemsetAsync(db->scope_bases, 0, (size_t)db->n_scopes * sizeof(int32_t), st));
   }
@@ -2148,13 +2232,8 @@ GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
                                                                                        : k_group<1, false>);
     kern<<<db->n_groups, kGrpThreads, 0, st>>>(B, db->groups, db->seg4, db->seg2, db->out, db->scope_calls,
                                                db->scope_bases, db->grp_part, db->far, db->counters + 2,
-                                               db->far_cap, ctx->group_skip);
+                                               db->far_cap, ctx->group_skip, ctx->nt_copy);
     if ((rc = check_launch(ctx, "k_group"))) return rc;
-  }
-  if (v5 && db->far_cap) {
-    KernelScope ks(ctx, "k_far_patches");
-    k_far_patches<<<64, kBlock, 0, st>>>(db->far, db->counters + 2, db->far_cap, db->out);
-    if ((rc = check_launch(ctx, "k_far_patches"))) return rc;
   }
   const int caps[2] = {kSmallCap0, kSmallCap1};
   for (int k = 0; k < 2 && !v4; ++k) {
@@ -2219,16 +2298,20 @@ GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
     if ((rc = check_launch(ctx, "k_mask_large"))) return rc;
   }
   {
-    KernelScope ks(ctx, "k_totals");
-    const int grid = std::max(1, std::min<int>((db->n_scopes + kBlock - 1) / kBlock, 128));
-    // group variants: their workgroups' partials plus the wide scopes' own counts
-    if (v4 && db->n_groups)
-      k_totals<<<grid, kBlock, 0, st>>>(db->scope_calls, db->scope_bases, db->large_ids, db->n_large_scopes,
-                                        db->grp_part, db->n_groups, db->counters + 0, db->counters + 1, db->totals);
-    else
+    if (v4) {
+      // far masks (fused), totals from the group partials and the wide scopes, counter reset
+      KernelScope ks(ctx, "k_finish");
+      k_finish<<<64, kBlock, 0, st>>>(db->far, v5 && db->n_groups ? db->far_cap : 0, db->out, db->grp_part,
+                                      db->n_groups, db->large_ids, db->n_large_scopes, db->scope_calls,
+                                      db->scope_bases, db->static_totals, db->counters, db->acc, db->totals);
+      if ((rc = check_launch(ctx, "k_finish"))) return rc;
+    } else {
+      KernelScope ks(ctx, "k_totals");
+      const int grid = std::max(1, std::min<int>((db->n_scopes + kBlock - 1) / kBlock, 128));
       k_totals<<<grid, kBlock, 0, st>>>(db->scope_calls, db->scope_bases, nullptr, db->n_scopes, nullptr, 0,
                                         db->counters + 0, db->counters + 1, db->totals);
-    if ((rc = check_launch(ctx, "k_totals"))) return rc;
+      if ((rc = check_launch(ctx, "k_totals"))) return rc;
+    }
   }
   db->ran = true;
   return GANON_OK;

@@ -117,8 +117,12 @@ GANON_API int ganon_ctx_set_variant(ganon_ctx *ctx, int variant);
 /* Tuning knobs (results never depend on them). GANON_PARAM_GROUP_UNROLL: 16-base chunks each
  * thread of the group kernels keeps in flight, 1 (default), 2, 4 or 8.
  * GANON_PARAM_GROUP_SKIP is for phase timing only and DOES change results: bit 0 leaves out
- * the classification, bit 1 the chunk scan of the group kernel. Keep it 0 in production. */
-enum { GANON_PARAM_GROUP_UNROLL = 1, GANON_PARAM_GROUP_SKIP = 2 };
+ * the classification, bit 1 the chunk scan, bit 2 the partition copy of the group kernels.
+ * Keep it 0 in production. GANON_PARAM_GROUP_TARGET: segments per scope group (read at
+ * upload; default 256). GANON_PARAM_NT_COPY: non-temporal stores for the fused partition copy
+ * (default 1). */
+enum { GANON_PARAM_GROUP_UNROLL = 1, GANON_PARAM_GROUP_SKIP = 2, GANON_PARAM_GROUP_TARGET = 3,
+       GANON_PARAM_NT_COPY = 4 };
 GANON_API int ganon_ctx_set_param(ganon_ctx *ctx, int param, int value);
 /* When on, ganon_batch_run records a HIP event pair around each kernel it launches. */
 GANON_API int ganon_ctx_set_profiling(ganon_ctx *ctx, int enabled);

@@ -1,9 +1,11 @@
 #!/usr/bin/env python3
-"""Phase timing of the group kernel on the config-2 batch (profiling aid, not a test).
+"""Phase timing of the group kernels on the config-2 batch (profiling aid, not a test).
 
-Runs ganon_batch_run with HIP-event timing for each (variant, unroll, skip) configuration,
-interleaved over several rounds, and prints one JSON object of median per-kernel times.
-skip != 0 leaves phases out (GANON_PARAM_GROUP_SKIP) and gives invalid results: timing only.
+Runs ganon_batch_run with HIP-event timing for each configuration
+variant:unroll:skip[:group_target[:nt_copy]], interleaved over several rounds, and prints one
+JSON object of median per-kernel times. skip != 0 leaves phases out (GANON_PARAM_GROUP_SKIP)
+and gives invalid results: timing only. group_target is applied at upload (one upload per
+distinct target).
 """
 import argparse
 import json
@@ -22,33 +24,44 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--configs", default="0:1:0,0:1:1,0:1:2,0:2:0,5:1:0,5:2:0",
-                    help="comma list of variant:unroll:skip")
+                    help="comma list of variant:unroll:skip[:group_target[:nt_copy]]")
     args = ap.parse_args()
     from genomeanonymizer_amd import native
     from genomeanonymizer_amd.synth.batch import config2_batch
     arr, info = config2_batch(n_reads=args.reads, genome=args.genome,
                               n_windows=args.reads // 10, n_germline=args.reads // 10, seed=2)
     m = native.HipMasker(0)
-    db = m.upload(arr)
+    cfgs = []
+    for c in args.configs.split(","):
+        f = [int(x) for x in c.split(":")]
+        f += [256, 0][len(f) - 3:] if len(f) < 5 else []
+        cfgs.append(tuple(f[:5]))
+    dbs = {}
+    for c in cfgs:
+        if c[3] not in dbs:
+            m.set_param(native.PARAM_GROUP_TARGET, c[3])
+            dbs[c[3]] = m.upload(arr)
     m.set_profiling(True)
-    cfgs = [tuple(int(x) for x in c.split(":")) for c in args.configs.split(",")]
     res = {c: {} for c in cfgs}
     for _ in range(args.rounds):
         for c in cfgs:
-            v, u, sk = c
+            v, u, sk, tgt, nt = c
             m.set_variant(v)
             m.set_param(native.PARAM_GROUP_UNROLL, u)
             m.set_param(native.PARAM_GROUP_SKIP, sk)
+            m.set_param(native.PARAM_NT_COPY, nt)
+            db = dbs[tgt]
             for _ in range(args.steps):
                 db.run()
                 db.sync()
                 for name, launches, ms in db.kernel_times():
                     res[c].setdefault(name, []).append(ms / launches)
     m.set_param(native.PARAM_GROUP_SKIP, 0)
-    out = {f"v{v}_u{u}_skip{sk}": {n: round(float(np.median(x)), 5) for n, x in d.items()}
-           for (v, u, sk), d in res.items()}
-    out["batch"] = db.info()
-    db.free()
+    out = {f"v{v}_u{u}_skip{sk}_t{tgt}_nt{nt}": {n: round(float(np.median(x)), 5) for n, x in d.items()}
+           for (v, u, sk, tgt, nt), d in res.items()}
+    out["batch"] = next(iter(dbs.values())).info()
+    for db in dbs.values():
+        db.free()
     m.close()
     print(json.dumps(out), flush=True)
 

@@ -1246,13 +1246,23 @@ __global__ void __launch_bounds__(kGrpThreads, 6) k_group(const DevBatch B, cons
   if (FUSED && !(skip & kSkipCopy)) {
     // the partition: whole 16-byte windows (the buffers are padded past seq_bytes); the stores
     // drain while the scan runs (s_waitcnt before the mask stores)
+    // 8 windows in flight per thread: all loads issue before the first store waits on them
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    if (nt_copy) {
-      for (int64_t D = sink.p0 + 16 * tid; D < sink.p1; D += 16 * kGrpThreads)
-        __builtin_nontemporal_store(*reinterpret_cast<const u32x4 *>(B.seq + D), reinterpret_cast<u32x4 *>(out + D));
-    } else {
-      for (int64_t D = sink.p0 + 16 * tid; D < sink.p1; D += 16 * kGrpThreads)
-        *reinterpret_cast<u32x4 *>(out + D) = *reinterpret_cast<const u32x4 *>(B.seq + D);
+    constexpr int kCopyUnroll = 8;
+    for (int64_t D0 = sink.p0 + 16 * tid; D0 < sink.p1; D0 += 16 * kGrpThreads * kCopyUnroll) {
+      u32x4 v[kCopyUnroll];
+#pragma unroll
+      for (int k = 0; k < kCopyUnroll; ++k) {
+        const int64_t D = D0 + 16 * kGrpThreads * k;
+        if (D < sink.p1) v[k] = *reinterpret_cast<const u32x4 *>(B.seq + D);
+      }
+#pragma unroll
+      for (int k = 0; k < kCopyUnroll; ++k) {
+        const int64_t D = D0 + 16 * kGrpThreads * k;
+        if (D >= sink.p1) break;
+        if (nt_copy) __builtin_nontemporal_store(v[k], reinterpret_cast<u32x4 *>(out + D));
+        else *reinterpret_cast<u32x4 *>(out + D) = v[k];
+      }
     }
   }
   if (tid == 0) {

@@ -35,7 +35,7 @@ VARIANT_NAMES = {0: "default", 1: "v0_block", 2: "v1_wave", 3: "v2_copy_patch", 
 VARIANT_WRITE = {0: "fused", 1: "whole", 2: "whole", 3: "copy_patch", 4: "copy_patch", 5: "fused",
                  6: "copy_patch"}
 # A/B configurations: (name, variant, group-kernel unroll)
-AB_CONFIGS = [(VARIANT_NAMES[v], v, 1) for v in (1, 2, 3, 6, 4)] + [(f"v5_group_fused_u{u}", 5, u) for u in (1, 2)]
+AB_CONFIGS = [(VARIANT_NAMES[v], v, 2) for v in (1, 2, 3, 6, 4)] + [(f"v5_group_fused_k{u}", 5, u) for u in (1, 2, 4)]
 
 
 def kernel_class(name: str) -> str:
@@ -131,7 +131,7 @@ def main() -> None:
     ap.add_argument("--variant", type=int, default=0,
                     help="include/ganon.h GANON_VARIANT_*: 0 default (= 5), 1 block, 2 wave, 3 copy-patch, "
                          "4 group, 5 group fused, 6 persistent")
-    ap.add_argument("--unroll", type=int, default=1, help="group kernel chunks in flight per thread (1/2/4/8)")
+    ap.add_argument("--unroll", type=int, default=2, help="group kernel chunk width in 16-base blocks (1/2/4/8)")
     ap.add_argument("--ab", action="store_true", help="also time every small-scope variant, interleaved")
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_r01.json"),
                     help="PMC summary (tools/pmc_summary.py) for the traffic field, if present")

@@ -1009,10 +1009,10 @@ __device__ __forceinline__ bool grp_kept(const DevBatch &B, int s, int64_t pos_o
   return kp >= 0 && B.keep_code[s] == c && (int64_t)kp - B.span_start[s] == pos_off;
 }
 
-// Stage records [c0, c0 + nh) in LDS with the exclusive prefix of their 16-base chunk counts;
+// Stage records [c0, c0 + nh) in LDS with the exclusive prefix of their chunk counts;
 // returns the tile's chunk total.
 __device__ __forceinline__ int grp_tile(GrpShared &sh, const int4 *__restrict__ rec4, const int2 *__restrict__ rec2,
-                                        int64_t c0, int nh) {
+                                        int64_t c0, int nh, int chunk) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t ix = c0 + (tid < nh ? tid : nh - 1);
   const int4 r = rec4[ix];
@@ -1021,7 +1021,7 @@ __device__ __forceinline__ int grp_tile(GrpShared &sh, const int4 *__restrict__ 
   if (tid < nh) {
     sh.rec[tid] = r;
     sh.rec2[tid] = r2;
-    nck = ((r2.x & 0xFFFFFF) + 15) >> 4;
+    nck = ((r2.x & 0xFFFFFF) + chunk - 1) / chunk;
   }
   int incl = nck;
 #pragma unroll
@@ -1058,58 +1058,66 @@ __device__ __forceinline__ int grp_find(const GrpShared &sh, int nh, int total, 
   return lo;
 }
 
-// Stream every chunk of every segment of the group, feeding observations in range R.
-template <int kGrpUnroll>   // chunks in flight per thread
+// Stream every chunk of every segment of the group, feeding observations in range R. A chunk
+// is 16 * K bases: each thread loads the 2K + 1 sequence dwords and 2K + 1 reference dwords
+// covering its chunk at once (one memory round trip per chunk), then takes the K 16-base
+// windows out of registers with static indices.
+template <int K>
 __device__ __forceinline__ void grp_scan(const DevBatch &B, GrpShared &sh, const GrpRange &R, const PatchSink &sink,
                                          int64_t i_begin, int64_t i_end, const int4 *__restrict__ rec4,
                                          const int2 *__restrict__ rec2, int skip) {
   const int tid = threadIdx.x;
   for (int64_t c0 = i_begin; c0 < i_end; c0 += kGrpTile) {
     const int nh = (int)((i_end - c0) < kGrpTile ? (i_end - c0) : kGrpTile);
-    int total = grp_tile(sh, rec4, rec2, c0, nh);
+    int total = grp_tile(sh, rec4, rec2, c0, nh, 16 * K);
     if (skip & kSkipChunks) total = 0;
-    // kGrpUnroll chunks per thread per iteration: all their loads are issued before any is used
-    for (int t0 = tid; t0 < total; t0 += kGrpUnroll * kGrpThreads) {
-      int seg[kGrpUnroll], q0[kGrpUnroll];
-      uint64_t sv[kGrpUnroll], rv[kGrpUnroll];
-      int64_t sn[kGrpUnroll], rn[kGrpUnroll];
+    for (int t = tid; t < total; t += kGrpThreads) {
+      const int j = grp_find(sh, nh, total, t);
+      const int4 r = sh.rec[j];
+      const int2 r2 = sh.rec2[j];
+      const int L = r2.x & 0xFFFFFF;
+      const int q0 = 16 * K * (t - sh.pre[j]);
+      const int64_t sn = i64_of(r.x, r.y) + q0, rn = i64_of(r.z, r.w) + q0;
+      const uint32_t *ps = reinterpret_cast<const uint32_t *>(B.seq) + (sn >> 3);
+      const uint32_t *pr = reinterpret_cast<const uint32_t *>(B.ref) + (rn >> 3);
+      uint32_t ds[2 * K + 1], dr[2 * K + 1];
 #pragma unroll
-      for (int u = 0; u < kGrpUnroll; ++u) {
-        const int t = min(t0 + u * kGrpThreads, total - 1);
-        const int j = grp_find(sh, nh, total, t);
-        seg[u] = j;
-        q0[u] = 16 * (t - sh.pre[j]);
-        const int4 r = sh.rec[j];
-        sn[u] = i64_of(r.x, r.y) + q0[u];
-        rn[u] = i64_of(r.z, r.w) + q0[u];
+      for (int i = 0; i < 2 * K + 1; ++i) {
+        ds[i] = ps[i];
+        dr[i] = pr[i];
       }
 #pragma unroll
-      for (int u = 0; u < kGrpUnroll; ++u) {
-        sv[u] = load16(B.seq, sn[u]);
-        rv[u] = load16(B.ref, rn[u]);
+      for (int i = 0; i < 2 * K + 1; ++i) {
+        ds[i] = nib_swap(ds[i]);
+        dr[i] = nib_swap(dr[i]);
       }
+      const int shs = 4 * (int)(sn & 7), shr = 4 * (int)(rn & 7);
+      const int ds_ = (r2.x >> 24) & 1;
+      const unsigned long long sk = (unsigned long long)(r2.y & 0xFFF) << 52;
+      const int pos_seg = (int)((uint32_t)r2.y >> 12);
 #pragma unroll
-      for (int u = 0; u < kGrpUnroll; ++u) {
-        if (t0 + u * kGrpThreads >= total) break;
-        const int2 r2 = sh.rec2[seg[u]];
-        const int L = r2.x & 0xFFFFFF;
-        const int nb = (L - q0[u]) < 16 ? (L - q0[u]) : 16;
-        uint64_t diff = sv[u] ^ rv[u];
+      for (int i = 0; i < K; ++i) {
+        const int qi = q0 + 16 * i;
+        if (qi >= L) break;
+        const uint64_t xs0 = (uint64_t)ds[2 * i] | ((uint64_t)ds[2 * i + 1] << 32);
+        const uint64_t xs1 = (uint64_t)ds[2 * i + 1] | ((uint64_t)ds[2 * i + 2] << 32);
+        const uint64_t xr0 = (uint64_t)dr[2 * i] | ((uint64_t)dr[2 * i + 1] << 32);
+        const uint64_t xr1 = (uint64_t)dr[2 * i + 1] | ((uint64_t)dr[2 * i + 2] << 32);
+        const uint64_t sv = (uint64_t)(uint32_t)(xs0 >> shs) | ((uint64_t)(uint32_t)(xs1 >> shs) << 32);
+        const uint64_t rv = (uint64_t)(uint32_t)(xr0 >> shr) | ((uint64_t)(uint32_t)(xr1 >> shr) << 32);
+        const int nb = (L - qi) < 16 ? (L - qi) : 16;
+        uint64_t diff = sv ^ rv;
         diff = (diff | (diff >> 1) | (diff >> 2) | (diff >> 3)) & 0x1111111111111111ull;
         if (nb < 16) diff &= (1ull << (4 * nb)) - 1;
-        if (!diff) continue;
-        const int ds = (r2.x >> 24) & 1;
-        const int pos0 = (int)((uint32_t)r2.y >> 12) + q0[u];   // pos - span_start, first base
-        const unsigned long long sk = (unsigned long long)(r2.y & 0xFFF) << 52;
-        do {
+        while (diff) {
           const int k = __builtin_ctzll(diff) >> 2;
           diff &= diff - 1;
-          const int c = (int)((sv[u] >> (4 * k)) & 15);
-          const int rc = (int)((rv[u] >> (4 * k)) & 15);
+          const int c = (int)((sv >> (4 * k)) & 15);
+          const int rc = (int)((rv >> (4 * k)) & 15);
           if (c == 15 || !is_acgt(rc)) continue;
-          const unsigned long long key = sk | ((unsigned long long)(pos0 + k) << 4) | (unsigned long long)c;
-          grp_observe(sh, R, sink, key, sn[u] + k, c, rc, ds, (uint32_t)r2.x);
-        } while (diff);
+          const unsigned long long key = sk | ((unsigned long long)(pos_seg + qi + k) << 4) | (unsigned long long)c;
+          grp_observe(sh, R, sink, key, sn + 16 * i + k, c, rc, ds_, (uint32_t)r2.x);
+        }
       }
     }
     __syncthreads();
@@ -1229,7 +1237,7 @@ __device__ __forceinline__ void grp_release() {
 // groups: 3 x int4 per group, in launch order: {s_begin, s_end, seg_begin lo, hi},
 // {seg_end lo, hi, 0, 0}, {partition begin lo, hi, end lo, hi} (bytes; fused only).
 template <int U, bool FUSED>
-__global__ void __launch_bounds__(kGrpThreads, 6) k_group(const DevBatch B, const int4 *__restrict__ groups,
+__global__ void __launch_bounds__(kGrpThreads, (U <= 2 ? 6 : U == 4 ? 5 : 4)) k_group(const DevBatch B, const int4 *__restrict__ groups,
                                                        const int4 *__restrict__ rec4, const int2 *__restrict__ rec2,
                                                        uint8_t *__restrict__ out, int32_t *scope_calls,
                                                        int32_t *scope_bases, int32_t *part,
@@ -1594,7 +1602,7 @@ struct ganon_ctx {
   bool profiling = false;
   int variant = GANON_VARIANT_DEFAULT;
   int v3_blocks[2] = {1, 1};   // resident grid of k_scope_v3 per class (occupancy x CUs)
-  int group_unroll = 1;        // GANON_PARAM_GROUP_UNROLL
+  int group_unroll = 2;        // GANON_PARAM_GROUP_UNROLL
   int group_skip = 0;          // GANON_PARAM_GROUP_SKIP (profiling only)
   int group_target = kGrpTarget;   // GANON_PARAM_GROUP_TARGET
   int nt_copy = 1;             // GANON_PARAM_NT_COPY
@@ -1666,9 +1674,10 @@ int fail(ganon_ctx *ctx, int code, const char *fmt, ...) {
 template <typename T>
 int dev_alloc(ganon_ctx *ctx, ganon_dbatch *db, T **p, size_t count) {
   *p = nullptr;
-  // +16 bytes: load16() reads up to 12 bytes past a buffer's last nibble, and the patch
+  // +128 bytes: the group kernels load up to 68 bytes from a chunk start past a buffer's last nibble,
+  // and the patch
   // atomics touch whole dwords
-  size_t bytes = std::max<size_t>(count, 1) * sizeof(T) + 16;
+  size_t bytes = std::max<size_t>(count, 1) * sizeof(T) + 128;
   hipError_t e = hipMalloc(reinterpret_cast<void **>(p), bytes);
   if (e != hipSuccess) return fail(ctx, GANON_E_NOMEM, "hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
   db->allocs.push_back(*p);

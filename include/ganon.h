@@ -115,7 +115,7 @@ enum {
 };
 GANON_API int ganon_ctx_set_variant(ganon_ctx *ctx, int variant);
 /* Tuning knobs (results never depend on them). GANON_PARAM_GROUP_UNROLL: 16-base chunks each
- * thread of the group kernels keeps in flight, 1 (default), 2, 4 or 8.
+ * thread of the group kernels loads at once (chunk = 16 x value bases): 1, 2 (default), 4 or 8.
  * GANON_PARAM_GROUP_SKIP is for phase timing only and DOES change results: bit 0 leaves out
  * the classification, bit 1 the chunk scan, bit 2 the partition copy of the group kernels.
  * Keep it 0 in production. GANON_PARAM_GROUP_TARGET: segments per scope group (read at

@@ -28,6 +28,7 @@
 #include <numeric>
 #include <string>
 #include <type_traits>
+#include <thread>
 #include <vector>
 
 #include "../../include/ganon.h"
@@ -61,6 +62,7 @@ struct DevBatch {
   const int32_t *span_start, *span_len, *keep_pos;
   const int64_t *ref_off;
   const uint8_t *ref, *keep_code;
+  const uint32_t *ref2;   // 2-bit reference (k_ref2) for the group kernels, null = nt16 only
 };
 
 __device__ __forceinline__ int nib_at(const uint8_t *__restrict__ buf, int64_t i) {
@@ -882,6 +884,37 @@ __global__ void __launch_bounds__(256) k_scope_v3(const DevBatch B, const int4 *
   }
 }
 
+// ---- 2-bit reference ----------------------------------------------------------------------
+// Word w = bases [16w, 16w + 16) of ref_nt16 as 2-bit codes (A0 C1 G2 T3; base i at bits
+// 2 * (i & 15)). Non-ACGT bases get code 0: only segments whose reference range is all ACGT
+// (ordered first in their group at upload) read this copy — half the bytes, fewer lines.
+__global__ void __launch_bounds__(kBlock) k_ref2(const uint8_t *__restrict__ ref, int64_t n_words,
+                                                 uint32_t *__restrict__ ref2) {
+  for (int64_t w = blockIdx.x * (int64_t)kBlock + threadIdx.x; w < n_words; w += (int64_t)gridDim.x * kBlock) {
+    const uint64_t v = load16(ref, 16 * w);
+    uint32_t code = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int c = (int)((v >> (4 * k)) & 15);
+      if (is_acgt(c)) code |= (uint32_t)__builtin_ctz(c) << (2 * k);
+    }
+    ref2[w] = code;
+  }
+}
+
+// 16 codes of a 2-bit window (code k at bits 2k) as one-hot nt16 nibbles (nibble k).
+__device__ __forceinline__ uint64_t expand2(uint32_t x) {
+  uint64_t y = x;
+  y = (y | (y << 16)) & 0x0000FFFF0000FFFFull;
+  y = (y | (y << 8)) & 0x00FF00FF00FF00FFull;
+  y = (y | (y << 4)) & 0x0F0F0F0F0F0F0F0Full;
+  y = (y | (y << 2)) & 0x3333333333333333ull;        // code k in nibble k
+  const uint64_t lo = y & 0x1111111111111111ull, hi = (y >> 1) & 0x1111111111111111ull;
+  const uint64_t v = lo + 0x1111111111111111ull;     // 1 (A) or 2 (C) ...
+  const uint64_t m = hi * 15;                         // ... shifted to 4 (G) or 8 (T)
+  return (v & ~m) | ((v << 2) & m);
+}
+
 // ---- group kernels: scope groups, observation lists ---------------------------------------
 // No per-scope table and no per-scope serialization. At upload every read of a small scope is
 // cut into segments (one per aligned M/=/X run: query nibble index, reference nibble index,
@@ -1062,7 +1095,7 @@ __device__ __forceinline__ int grp_find(const GrpShared &sh, int nh, int total, 
 // is 16 * K bases: each thread loads the 2K + 1 sequence dwords and 2K + 1 reference dwords
 // covering its chunk at once (one memory round trip per chunk), then takes the K 16-base
 // windows out of registers with static indices.
-template <int K>
+template <int K, bool REF2>
 __device__ __forceinline__ void grp_scan(const DevBatch &B, GrpShared &sh, const GrpRange &R, const PatchSink &sink,
                                          int64_t i_begin, int64_t i_end, const int4 *__restrict__ rec4,
                                          const int2 *__restrict__ rec2, int skip) {
@@ -1079,19 +1112,20 @@ __device__ __forceinline__ void grp_scan(const DevBatch &B, GrpShared &sh, const
       const int q0 = 16 * K * (t - sh.pre[j]);
       const int64_t sn = i64_of(r.x, r.y) + q0, rn = i64_of(r.z, r.w) + q0;
       const uint32_t *ps = reinterpret_cast<const uint32_t *>(B.seq) + (sn >> 3);
-      const uint32_t *pr = reinterpret_cast<const uint32_t *>(B.ref) + (rn >> 3);
-      uint32_t ds[2 * K + 1], dr[2 * K + 1];
+      const uint32_t *pr = REF2 ? B.ref2 + (rn >> 4) : reinterpret_cast<const uint32_t *>(B.ref) + (rn >> 3);
+      constexpr int NR = REF2 ? K + 1 : 2 * K + 1;   // reference words covering the chunk
+      uint32_t ds[2 * K + 1], dr[NR];
 #pragma unroll
-      for (int i = 0; i < 2 * K + 1; ++i) {
-        ds[i] = ps[i];
-        dr[i] = pr[i];
-      }
+      for (int i = 0; i < 2 * K + 1; ++i) ds[i] = ps[i];
 #pragma unroll
-      for (int i = 0; i < 2 * K + 1; ++i) {
-        ds[i] = nib_swap(ds[i]);
-        dr[i] = nib_swap(dr[i]);
+      for (int i = 0; i < NR; ++i) dr[i] = pr[i];
+#pragma unroll
+      for (int i = 0; i < 2 * K + 1; ++i) ds[i] = nib_swap(ds[i]);
+      if (!REF2) {
+#pragma unroll
+        for (int i = 0; i < NR; ++i) dr[i] = nib_swap(dr[i]);
       }
-      const int shs = 4 * (int)(sn & 7), shr = 4 * (int)(rn & 7);
+      const int shs = 4 * (int)(sn & 7), shr = REF2 ? 2 * (int)(rn & 15) : 4 * (int)(rn & 7);
       const int ds_ = (r2.x >> 24) & 1;
       const unsigned long long sk = (unsigned long long)(r2.y & 0xFFF) << 52;
       const int pos_seg = (int)((uint32_t)r2.y >> 12);
@@ -1101,10 +1135,15 @@ __device__ __forceinline__ void grp_scan(const DevBatch &B, GrpShared &sh, const
         if (qi >= L) break;
         const uint64_t xs0 = (uint64_t)ds[2 * i] | ((uint64_t)ds[2 * i + 1] << 32);
         const uint64_t xs1 = (uint64_t)ds[2 * i + 1] | ((uint64_t)ds[2 * i + 2] << 32);
-        const uint64_t xr0 = (uint64_t)dr[2 * i] | ((uint64_t)dr[2 * i + 1] << 32);
-        const uint64_t xr1 = (uint64_t)dr[2 * i + 1] | ((uint64_t)dr[2 * i + 2] << 32);
         const uint64_t sv = (uint64_t)(uint32_t)(xs0 >> shs) | ((uint64_t)(uint32_t)(xs1 >> shs) << 32);
-        const uint64_t rv = (uint64_t)(uint32_t)(xr0 >> shr) | ((uint64_t)(uint32_t)(xr1 >> shr) << 32);
+        uint64_t rv;
+        if (REF2) {
+          rv = expand2((uint32_t)((((uint64_t)dr[i]) | ((uint64_t)dr[i + 1] << 32)) >> shr));
+        } else {
+          const uint64_t xr0 = (uint64_t)dr[2 * i] | ((uint64_t)dr[2 * i + 1] << 32);
+          const uint64_t xr1 = (uint64_t)dr[2 * i + 1] | ((uint64_t)dr[2 * i + 2] << 32);
+          rv = (uint64_t)(uint32_t)(xr0 >> shr) | ((uint64_t)(uint32_t)(xr1 >> shr) << 32);
+        }
         const int nb = (L - qi) < 16 ? (L - qi) : 16;
         uint64_t diff = sv ^ rv;
         diff = (diff | (diff >> 1) | (diff >> 2) | (diff >> 3)) & 0x1111111111111111ull;
@@ -1235,7 +1274,8 @@ __device__ __forceinline__ void grp_release() {
 }
 
 // groups: 3 x int4 per group, in launch order: {s_begin, s_end, seg_begin lo, hi},
-// {seg_end lo, hi, 0, 0}, {partition begin lo, hi, end lo, hi} (bytes; fused only).
+// {seg_end lo, hi, seg_mid lo, hi}, {partition begin lo, hi, end lo, hi} (bytes; fused only);
+// segments [seg_begin, seg_mid) have an all-ACGT reference range (2-bit reference).
 template <int U, bool FUSED>
 __global__ void __launch_bounds__(kGrpThreads, (U <= 2 ? 6 : U == 4 ? 5 : 4)) k_group(const DevBatch B, const int4 *__restrict__ groups,
                                                        const int4 *__restrict__ rec4, const int2 *__restrict__ rec2,
@@ -1249,7 +1289,7 @@ __global__ void __launch_bounds__(kGrpThreads, (U <= 2 ? 6 : U == 4 ? 5 : 4)) k_
   const int4 g1 = groups[3 * blockIdx.x + 1];
   const int4 g2 = groups[3 * blockIdx.x + 2];
   const int s_begin = g0.x, s_end = g0.y;
-  const int64_t i_begin = i64_of(g0.z, g0.w), i_end = i64_of(g1.x, g1.y);
+  const int64_t i_begin = i64_of(g0.z, g0.w), i_end = i64_of(g1.x, g1.y), i_mid = i64_of(g1.z, g1.w);
   PatchSink sink{out, i64_of(g2.x, g2.y), i64_of(g2.z, g2.w), far, far_count, far_cap, FUSED, FUSED, false};
   if (FUSED && !(skip & kSkipCopy)) {
     // the partition: whole 16-byte windows (the buffers are padded past seq_bytes); the stores
@@ -1314,7 +1354,12 @@ __global__ void __launch_bounds__(kGrpThreads, (U <= 2 ? 6 : U == 4 ? 5 : 4)) k_
       sh.masked = 0;
     }
     __syncthreads();
-    grp_scan<U>(B, sh, R, sink, i_begin, i_end, rec4, rec2, skip);
+    if (B.ref2) {
+      grp_scan<U, true>(B, sh, R, sink, i_begin, i_mid, rec4, rec2, skip);
+      grp_scan<U, false>(B, sh, R, sink, i_mid, i_end, rec4, rec2, skip);
+    } else {
+      grp_scan<U, false>(B, sh, R, sink, i_begin, i_end, rec4, rec2, skip);
+    }
     // (grp_scan ends on a barrier)
     if (skip & kSkipClassify) continue;
     const int s = s_begin + (int)(R.lo >> 52);
@@ -1606,6 +1651,7 @@ struct ganon_ctx {
   int group_skip = 0;          // GANON_PARAM_GROUP_SKIP (profiling only)
   int group_target = kGrpTarget;   // GANON_PARAM_GROUP_TARGET
   int nt_copy = 1;             // GANON_PARAM_NT_COPY
+  int ref2 = 1;                // GANON_PARAM_REF2
   std::string err;
   struct Rec { std::string name; hipEvent_t e0, e1; };
   std::vector<Rec> recs;
@@ -1645,6 +1691,7 @@ struct ganon_dbatch {
   int32_t n_groups = 0;
   int64_t n_seg = 0;
   unsigned long long *acc = nullptr;    // k_finish: calls, bases, workgroup ticket
+  uint32_t *ref2 = nullptr;             // 2-bit reference (k_ref2)
   unsigned long long *far = nullptr;    // fused: masks outside the masking group's partition
   int64_t far_cap = 0;
   int32_t *grp_part = nullptr;          // k_group: (calls, bases) per workgroup
@@ -1827,6 +1874,10 @@ GANON_API int ganon_ctx_set_param(ganon_ctx *ctx, int param, int value) {
   if (param == GANON_PARAM_GROUP_TARGET) {
     if (value < 16 || value > 65536) return fail(ctx, GANON_E_ARG, "group target must be in [16, 65536] (got %d)", value);
     ctx->group_target = value;
+    return GANON_OK;
+  }
+  if (param == GANON_PARAM_REF2) {
+    ctx->ref2 = value != 0;
     return GANON_OK;
   }
   if (param == GANON_PARAM_NT_COPY) {
@@ -2072,13 +2123,49 @@ GANON_API int ganon_batch_upload(ganon_ctx *ctx, const ganon_batch *b, ganon_dba
     struct G {
       int32_t s0, s1;
       int64_t i0, i1, first;   // first: lowest seq_off of a read the group writes
+      int64_t mid;             // segments [i0, mid) have an all-ACGT reference range
     };
     std::vector<G> gs;
     int32_t g_s0 = -1;
     int64_t g_i0 = 0, g_first = INT64_MAX;
+    // 64-base reference blocks holding a non-ACGT code (N, IUPAC, '='), for the clean/dirty split
+    const int64_t n_blk = (b->ref_bytes + 31) / 32;
+    std::vector<uint8_t> bad_blk((size_t)n_blk, 0);
+    {
+      uint8_t ok[256];
+      for (int v = 0; v < 256; ++v) ok[v] = ((0x116 >> (v >> 4)) & 1) && ((0x116 >> (v & 15)) & 1);
+      const int nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+      std::vector<std::thread> th;
+      for (int t = 0; t < nt; ++t)
+        th.emplace_back([&, t] {
+          for (int64_t k = t; k < n_blk; k += nt) {
+            const int64_t e = std::min<int64_t>(32 * k + 32, b->ref_bytes);
+            uint8_t bad = 0;
+            for (int64_t x = 32 * k; x < e; ++x) bad |= !ok[b->ref_nt16[x]];
+            bad_blk[k] = bad;
+          }
+        });
+      for (auto &x : th) x.join();
+    }
+    auto ref_clean = [&](int64_t rnib, int64_t n) {
+      for (int64_t k = rnib >> 6; k <= (rnib + n - 1) >> 6; ++k)
+        if (k >= n_blk || bad_blk[k]) return false;
+      return true;
+    };
+    std::vector<int4> c4, d4;   // the open group's segments: clean, dirty reference
+    std::vector<int2> c2, d2;
     auto close_group = [&](int32_t s_end) {
       if (g_s0 < 0) return;
-      gs.push_back(G{g_s0, s_end, g_i0, (int64_t)s4.size(), g_first});
+      s4.insert(s4.end(), c4.begin(), c4.end());
+      s2.insert(s2.end(), c2.begin(), c2.end());
+      const int64_t mid = (int64_t)s4.size();
+      s4.insert(s4.end(), d4.begin(), d4.end());
+      s2.insert(s2.end(), d2.begin(), d2.end());
+      c4.clear();
+      c2.clear();
+      d4.clear();
+      d2.clear();
+      gs.push_back(G{g_s0, s_end, g_i0, (int64_t)s4.size(), g_first, mid});
       g_s0 = -1;
       g_first = INT64_MAX;
     };
@@ -2106,7 +2193,7 @@ GANON_API int ganon_batch_upload(ganon_ctx *ctx, const ganon_batch *b, ganon_dba
       const int64_t i0 = b->scope_incid_off[s], i1 = b->scope_incid_off[s + 1];
       int64_t nseg = 0;
       for (int64_t i = i0; i < i1; ++i) segments_of(b->incid_read[i], [&](int64_t, int64_t, int64_t) { ++nseg; });
-      if (g_s0 >= 0 && ((int64_t)s4.size() - g_i0 + nseg > ctx->group_target || s - g_s0 >= kGrpMaxScopes))
+      if (g_s0 >= 0 && ((int64_t)(c4.size() + d4.size()) + nseg > ctx->group_target || s - g_s0 >= kGrpMaxScopes))
         close_group(s);
       if (g_s0 < 0) {
         g_s0 = s;
@@ -2123,10 +2210,11 @@ GANON_API int ganon_batch_upload(ganon_ctx *ctx, const ganon_batch *b, ganon_dba
         }
         const int64_t qnib = 2 * b->seq_off[r];
         segments_of(r, [&](int64_t q, int64_t p, int64_t n) {
-          s4.push_back(make_int4(lo32(qnib + q), hi32(qnib + q), lo32(ref0 + p), hi32(ref0 + p)));
+          const bool clean = ref_clean(ref0 + p, n);
+          (clean ? c4 : d4).push_back(make_int4(lo32(qnib + q), hi32(qnib + q), lo32(ref0 + p), hi32(ref0 + p)));
           // small scope: span <= kSmallCap1 < 2^20 positions
           const uint32_t pos_off = (uint32_t)(p - b->scope_span_start[s]);
-          s2.push_back(make_int2((int)((uint32_t)n | fl), (int)((uint32_t)(s - g_s0) | (pos_off << 12))));
+          (clean ? c2 : d2).push_back(make_int2((int)((uint32_t)n | fl), (int)((uint32_t)(s - g_s0) | (pos_off << 12))));
         });
       }
     }
@@ -2160,7 +2248,7 @@ GANON_API int ganon_batch_upload(ganon_ctx *ctx, const ganon_batch *b, ganon_dba
     for (int32_t k = 0; k < ng; ++k) {
       const G &g = gs[order[k]];
       grp[3 * k] = make_int4(g.s0, g.s1, lo32(g.i0), hi32(g.i0));
-      grp[3 * k + 1] = make_int4(lo32(g.i1), hi32(g.i1), 0, 0);
+      grp[3 * k + 1] = make_int4(lo32(g.i1), hi32(g.i1), lo32(g.mid), hi32(g.mid));
       grp[3 * k + 2] = make_int4(lo32(part[k]), hi32(part[k]), lo32(part[k + 1]), hi32(part[k + 1]));
     }
     if ((rc = dev_copy(ctx, db, &db->groups, grp.data(), grp.size()))) return bail(rc);
@@ -2171,6 +2259,14 @@ GANON_API int ganon_batch_upload(ganon_ctx *ctx, const ganon_batch *b, ganon_dba
     db->n_seg = (int64_t)s4.size();
     db->far_cap = far_cap;
     if ((rc = dev_alloc(ctx, db, &db->far, (size_t)far_cap))) return bail(rc);
+    const int64_t n_words = (2 * b->ref_bytes + 15) / 16;
+    if ((rc = dev_alloc(ctx, db, &db->ref2, (size_t)n_words + 2))) return bail(rc);
+    if (n_words) {
+      k_ref2<<<(int)std::min<int64_t>((n_words + kBlock - 1) / kBlock, 16384), kBlock, 0, ctx->stream>>>(
+          D.ref, n_words, db->ref2);
+      if ((rc = check_launch(ctx, "k_ref2"))) return bail(rc);
+    }
+    D.ref2 = db->ref2;
   }
   if ((rc = dev_alloc(ctx, db, &db->out, (size_t)b->seq_bytes))) return bail(rc);
   // bytes outside every read are never written by the fused variant: make them defined
@@ -2213,7 +2309,8 @@ GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
   }
   ctx->recs.clear();
   hipStream_t st = ctx->stream;
-  const DevBatch &B = db->B;
+  DevBatch B = db->B;
+  if (!ctx->ref2) B.ref2 = nullptr;   // group kernels then read the nt16 reference only
   int rc;
   const bool v3 = ctx->variant == GANON_VARIANT_PERSIST;
   const bool v2 = ctx->variant == GANON_VARIANT_COPYPATCH;

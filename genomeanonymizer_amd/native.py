@@ -122,6 +122,7 @@ PARAM_GROUP_UNROLL = 1   # include/ganon.h GANON_PARAM_GROUP_UNROLL
 PARAM_GROUP_SKIP = 2     # include/ganon.h GANON_PARAM_GROUP_SKIP (phase timing only)
 PARAM_GROUP_TARGET = 3   # include/ganon.h GANON_PARAM_GROUP_TARGET (segments per group, at upload)
 PARAM_NT_COPY = 4        # include/ganon.h GANON_PARAM_NT_COPY
+PARAM_REF2 = 5           # include/ganon.h GANON_PARAM_REF2
 
 EXPORTED_HIP_SYMBOLS = (
     "ganon_ctx_create", "ganon_ctx_destroy", "ganon_last_error", "ganon_abi_version",

@@ -120,9 +120,10 @@ GANON_API int ganon_ctx_set_variant(ganon_ctx *ctx, int variant);
  * the classification, bit 1 the chunk scan, bit 2 the partition copy of the group kernels.
  * Keep it 0 in production. GANON_PARAM_GROUP_TARGET: segments per scope group (read at
  * upload; default 256). GANON_PARAM_NT_COPY: non-temporal stores for the fused partition copy
- * (default 1). */
+ * (default 1). GANON_PARAM_REF2: group kernels read a 2-bit copy of the reference for segments
+ * whose reference range is all ACGT (1, default) or the nt16 reference only (0). */
 enum { GANON_PARAM_GROUP_UNROLL = 1, GANON_PARAM_GROUP_SKIP = 2, GANON_PARAM_GROUP_TARGET = 3,
-       GANON_PARAM_NT_COPY = 4 };
+       GANON_PARAM_NT_COPY = 4, GANON_PARAM_REF2 = 5 };
 GANON_API int ganon_ctx_set_param(ganon_ctx *ctx, int param, int value);
 /* When on, ganon_batch_run records a HIP event pair around each kernel it launches. */
 GANON_API int ganon_ctx_set_profiling(ganon_ctx *ctx, int enabled);

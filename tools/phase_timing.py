@@ -2,7 +2,7 @@
 """Phase timing of the group kernels on the config-2 batch (profiling aid, not a test).
 
 Runs ganon_batch_run with HIP-event timing for each configuration
-variant:unroll:skip[:group_target[:nt_copy]], interleaved over several rounds, and prints one
+variant:unroll:skip[:group_target[:nt_copy[:ref2]]], interleaved over several rounds, and prints one
 JSON object of median per-kernel times. skip != 0 leaves phases out (GANON_PARAM_GROUP_SKIP)
 and gives invalid results: timing only. group_target is applied at upload (one upload per
 distinct target).
@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--configs", default="0:1:0,0:1:1,0:1:2,0:2:0,5:1:0,5:2:0",
-                    help="comma list of variant:unroll:skip[:group_target[:nt_copy]]")
+                    help="comma list of variant:unroll:skip[:group_target[:nt_copy[:ref2]]]")
     args = ap.parse_args()
     from genomeanonymizer_amd import native
     from genomeanonymizer_amd.synth.batch import config2_batch
@@ -34,8 +34,8 @@ def main():
     cfgs = []
     for c in args.configs.split(","):
         f = [int(x) for x in c.split(":")]
-        f += [256, 0][len(f) - 3:] if len(f) < 5 else []
-        cfgs.append(tuple(f[:5]))
+        f += [256, 1, 1][len(f) - 3:] if len(f) < 6 else []
+        cfgs.append(tuple(f[:6]))
     dbs = {}
     for c in cfgs:
         if c[3] not in dbs:
@@ -45,11 +45,12 @@ def main():
     res = {c: {} for c in cfgs}
     for _ in range(args.rounds):
         for c in cfgs:
-            v, u, sk, tgt, nt = c
+            v, u, sk, tgt, nt, r2 = c
             m.set_variant(v)
             m.set_param(native.PARAM_GROUP_UNROLL, u)
             m.set_param(native.PARAM_GROUP_SKIP, sk)
             m.set_param(native.PARAM_NT_COPY, nt)
+            m.set_param(native.PARAM_REF2, r2)
             db = dbs[tgt]
             for _ in range(args.steps):
                 db.run()
@@ -57,8 +58,8 @@ def main():
                 for name, launches, ms in db.kernel_times():
                     res[c].setdefault(name, []).append(ms / launches)
     m.set_param(native.PARAM_GROUP_SKIP, 0)
-    out = {f"v{v}_u{u}_skip{sk}_t{tgt}_nt{nt}": {n: round(float(np.median(x)), 5) for n, x in d.items()}
-           for (v, u, sk, tgt, nt), d in res.items()}
+    out = {f"v{v}_k{u}_skip{sk}_t{tgt}_nt{nt}_ref2{r2}": {n: round(float(np.median(x)), 5) for n, x in d.items()}
+           for (v, u, sk, tgt, nt, r2), d in res.items()}
     out["batch"] = next(iter(dbs.values())).info()
     for db in dbs.values():
         db.free()

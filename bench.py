@@ -118,15 +118,46 @@ def cpu_baseline(arr, n_reads: int, budget_s: float = 10.0) -> dict:
                       f"reference Python calibration: 1,196 reads/s (BASELINE.md §2)"}
 
 
+CONFIGS = {
+    "c2": {"defaults": {"reads": 10_000_000, "genome": 3_000_000_000, "windows": 1_000_000, "germline": 1_000_000},
+           "generator": "genomeanonymizer_amd.synth.batch.config2_batch", "seed": 2,
+           "workload": "BASELINE configs[1]: {reads}-read 150 bp tumor+normal batch, {germline} germline SNPs, "
+                       "{windows}-window VCF, {genome} bp / 24 contigs, resident in HBM"},
+    "c3": {"defaults": {"reads": 40_000_000, "genome": 100_000_000, "windows": 10_000, "germline": 100_000},
+           "generator": "genomeanonymizer_amd.synth.batch.config2_batch", "seed": 3,
+           "workload": "SURVEY C3 density: {reads} 150 bp reads (~60x tumor+normal) on {genome} bp, "
+                       "1 germline het SNP per kb, a window every 10 kb, resident in HBM"},
+    "c5": {"defaults": {"reads": 20_000, "genome": 200_000_000, "windows": 0, "germline": 0},
+           "generator": "genomeanonymizer_amd.synth.batch.longread_batch", "seed": 7,
+           "workload": "SURVEY C5: {reads} ONT-like reads 10-100 kb (5 % indels, soft clips) on {genome} bp, "
+                       "germline het SNP per kb, a window every 10 kb (scopes to ~200 kb), resident in HBM"},
+}
+
+
+def make_batch(args, rank: int):
+    from genomeanonymizer_amd.synth.batch import config2_batch, longread_batch
+    if args.config == "c5":
+        return longread_batch(seed=7 + rank, n_reads=args.reads, genome=args.genome)
+    seed = CONFIGS[args.config]["seed"] + rank
+    if args.config == "c3":
+        return config2_batch(n_reads=args.reads, genome=args.genome, n_contigs=4, n_windows=args.windows,
+                             n_germline=args.germline, seed=seed, window_spacing=10_000)
+    return config2_batch(n_reads=args.reads, genome=args.genome, n_windows=args.windows,
+                         n_germline=args.germline, seed=seed)
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--reads", type=int, default=10_000_000)
-    ap.add_argument("--genome", type=int, default=3_000_000_000)
-    ap.add_argument("--windows", type=int, default=1_000_000)
-    ap.add_argument("--germline", type=int, default=1_000_000)
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="c2",
+                    help="c2 = BASELINE configs[1] (the metric's workload); c3 / c5 = SURVEY §8(d) density and "
+                         "long-read shapes, for their own lines")
+    ap.add_argument("--reads", type=int, default=None)
+    ap.add_argument("--genome", type=int, default=None)
+    ap.add_argument("--windows", type=int, default=None)
+    ap.add_argument("--germline", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--variant", type=int, default=0,
                     help="include/ganon.h GANON_VARIANT_*: 0 default (= 5), 1 block, 2 wave, 3 copy-patch, "
@@ -136,6 +167,9 @@ def main() -> None:
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_r01.json"),
                     help="PMC summary (tools/pmc_summary.py) for the traffic field, if present")
     args = ap.parse_args()
+    for k, v in CONFIGS[args.config]["defaults"].items():
+        if getattr(args, k) is None:
+            setattr(args, k, v)
 
     import torch
     rank = int(os.environ.get("RANK", 0))
@@ -148,11 +182,10 @@ def main() -> None:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from genomeanonymizer_amd import native
-    from genomeanonymizer_amd.synth.batch import algorithmic_bytes, config2_batch
+    from genomeanonymizer_amd.synth.batch import algorithmic_bytes
 
     t_gen = time.perf_counter()
-    arr, info = config2_batch(n_reads=args.reads, genome=args.genome, n_windows=args.windows,
-                              n_germline=args.germline, seed=2 + rank)
+    arr, info = make_batch(args, rank)
     t_gen = time.perf_counter() - t_gen
     masker = native.HipMasker(local)
     masker.set_variant(args.variant)
@@ -248,11 +281,13 @@ def main() -> None:
 
     reads_total = info["reads"] * world
     value = reads_total * args.steps / dt
+    mean_len = float(arr["read_len"].astype(np.int64).mean()) if len(arr["read_len"]) else 0.0
+    cfg = CONFIGS[args.config]
     result = {
         "metric": "reads/sec + bases/sec anonymized, 150 bp paired BAM, 1/2/4/8 MI355X",
         "value": round(value, 1),
         "unit": "reads/s",
-        "bases_per_sec": round(value * info["read_len"], 1),
+        "bases_per_sec": round(value * mean_len, 1),
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
@@ -261,12 +296,12 @@ def main() -> None:
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (genomeanonymizer_amd.synth.batch.config2_batch, seed 2+rank)",
-        "config": {"workload": "BASELINE configs[1]: 10M-read 150 bp tumor+normal batch, 1M germline SNPs, "
-                               "1M-window VCF, 3.0 Gb / 24 contigs, resident in HBM",
-                   "reads_per_gpu": info["reads"], "scopes_per_gpu": info["scopes"],
-                   "window_scopes": info["window_scopes"], "union_scopes": info["union_scopes"],
-                   "passthrough_reads": info["passthrough_reads"], "parallelism": f"contig-shard x{world}"},
+        "data": f"synthetic ({cfg['generator']}, seed {cfg['seed']}+rank)",
+        "config": {"workload": cfg["workload"].format(**vars(args)), "name": args.config,
+                   "reads_per_gpu": info["reads"], "mean_read_len": round(mean_len, 1),
+                   "scopes_per_gpu": info["scopes"], "incidences_per_gpu": info.get("incidences"),
+                   "window_scopes": info.get("window_scopes"), "union_scopes": info.get("union_scopes"),
+                   "passthrough_reads": info.get("passthrough_reads"), "parallelism": f"contig-shard x{world}"},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                      "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_ms": round(dom_ms, 5)},

@@ -302,6 +302,141 @@ def _make_read(rng, ref, pos, rl, alt, rare_sites, ds):
 
 
 # ---------------------------------------------------------------------------------------
+# long reads
+# ---------------------------------------------------------------------------------------
+
+def longread_batch(seed: int = 5, n_reads: int = 200, genome: int = 2_000_000, len_range=(10_000, 100_000),
+                   indel_rate: float = 0.05, sub_rate: float = 0.01, clip_max: int = 2000,
+                   window_spacing: int = 10_000, germline_every: int = 1000) -> Tuple[Dict[str, np.ndarray], dict]:
+    """C5-like batch: ONT-style reads (log-uniform lengths, ~indel_rate 1-3 bp I/D ops, soft clips
+    at both ends, substitutions), tumor and normal halves, het germline SNPs every
+    ~germline_every bp, reference N runs and IUPAC codes, and a window scope every
+    window_spacing bp (reads overlapping [pos - 1000, pos + 1001); scope spans reach ~200 kb).
+    A read is written by the first window it overlaps; reads in no window pass through."""
+    rng = np.random.default_rng(seed)
+    ref = ACGT[rng.integers(0, 4, genome)]
+    for a in range(250_000, genome - 1000, 700_000):          # N runs
+        ref[a:a + 500] = 15
+    iu = rng.random(genome) < 2e-5
+    ref[iu] = IUPAC[rng.integers(0, len(IUPAC), int(iu.sum()))]
+    gsnp = np.arange(500, genome - 500, germline_every) + rng.integers(-200, 200, (genome - 1000) // germline_every)
+    gsnp = np.unique(gsnp[(gsnp > 0) & (gsnp < genome)])
+    galt = ACGT[rng.integers(0, 4, len(gsnp))]
+    lo, hi = np.log(len_range[0]), np.log(len_range[1])
+    starts, cigars, seqs, dss = [], [], [], []
+    for r in range(n_reads):
+        span = int(np.exp(rng.uniform(lo, hi)))
+        pos = int(rng.integers(0, max(1, genome - span - 10)))
+        hap = rng.random() < 0.5
+        # M runs (geometric) separated by 1-3 bp insertions/deletions, built vectorised
+        runs = rng.geometric(indel_rate, size=int(span * indel_rate * 2) + 8).astype(np.int64)
+        runs = runs[np.cumsum(runs) <= span]
+        if not len(runs):
+            continue
+        nr = len(runs)
+        ins = rng.random(nr) < 0.5                                # indel after run k: insertion?
+        ilen = rng.integers(1, 4, nr).astype(np.int64)
+        ins[-1] = False
+        ilen[-1] = 0                                              # nothing after the last run
+        c0 = int(rng.integers(0, clip_max + 1)) if rng.random() < 0.7 else 0
+        c1 = int(rng.integers(0, clip_max + 1)) if rng.random() < 0.7 else 0
+        radv = runs + np.where(ins, 0, ilen)
+        qadv = runs + np.where(ins, ilen, 0)
+        rstart = pos + np.concatenate([[0], np.cumsum(radv)[:-1]])
+        qstart = c0 + np.concatenate([[0], np.cumsum(qadv)[:-1]])
+        keep = rstart + runs < genome - 1
+        if not keep.all():
+            k = int(np.argmin(keep))
+            if k == 0:
+                continue
+            runs, ins, ilen, rstart, qstart = runs[:k], ins[:k], ilen[:k], rstart[:k], qstart[:k]
+            ins[-1] = False
+            ilen[-1] = 0
+        lq = int(c0 + runs.sum() + ilen[ins].sum() + c1)
+        seq = ACGT[rng.integers(0, 4, lq)]                         # clips and insertions random
+        tot = int(runs.sum())
+        off = np.arange(tot, dtype=np.int64) - np.repeat(np.cumsum(runs) - runs, runs)
+        ridx = np.repeat(rstart, runs) + off
+        b = ref[ridx].copy()
+        if hap:
+            gi = np.minimum(np.searchsorted(gsnp, ridx), len(gsnp) - 1)
+            hit = gsnp[gi] == ridx
+            b[hit] = galt[gi[hit]]
+        err = rng.random(tot) < sub_rate
+        b[err] = ACGT[rng.integers(0, 4, int(err.sum()))]
+        seq[np.repeat(qstart, runs) + off] = b
+        words = [np.full(1, (c0 << 4) | 4, np.int64)] if c0 else []
+        mid = np.empty(2 * len(runs), np.int64)
+        mid[0::2] = runs << 4                                    # M
+        mid[1::2] = (ilen << 4) | np.where(ins, 1, 2)            # I / D
+        mid = mid[:-1]                                           # no indel after the last run
+        words.append(mid)
+        if c1:
+            words.append(np.full(1, (c1 << 4) | 4, np.int64))
+        starts.append(pos)
+        cigars.append(np.concatenate(words).astype(np.uint32))
+        seqs.append(seq.astype(np.uint8))
+        dss.append(r % 2)
+    order = np.argsort(np.array(starts), kind="stable")     # coordinate-sorted, like a BAM
+    starts = [starts[i] for i in order]
+    cigars = [cigars[i] for i in order]
+    seqs = [seqs[i] for i in order]
+    dss = [dss[i] for i in order]
+    n = len(starts)
+    packed = [pack_nibbles(x) for x in seqs]
+    seq_off = np.zeros(n, np.int64)
+    seq_off[1:] = np.cumsum([len(x) for x in packed])[:-1]
+    cig_off = np.zeros(n, np.int64)
+    cig_off[1:] = np.cumsum([len(c) for c in cigars])[:-1]
+    ends = np.array([_ref_end(starts[i], cigars[i].tolist()) for i in range(n)], np.int64)
+    st = np.array(starts, np.int64)
+    # window scopes
+    wpos = np.arange(1002, genome - 1002, window_spacing, dtype=np.int64)
+    max_span = int((ends - st).max()) if n else 0
+    incid, offs, span_start, span_len, keep_pos, keep_code = [], [0], [], [], [], []
+    ws = np.full(n, -1, np.int32)
+    for w, wp in enumerate(wpos):
+        a, b = wp - 1000, wp + 1001
+        cand = np.arange(np.searchsorted(st, a - max_span), np.searchsorted(st, b))
+        ids = cand[(st[cand] < b) & (ends[cand] > a)]
+        incid.extend(ids.tolist())
+        offs.append(len(incid))
+        if len(ids):
+            s0, s1 = int(st[ids].min()), int(ends[ids].max())
+        else:
+            s0 = s1 = 0
+        span_start.append(s0)
+        span_len.append(s1 - s0)
+        keep_pos.append(int(wp - 1))
+        keep_code.append(int(ACGT[rng.integers(0, 4)]))
+        new = ids[ws[ids] < 0]
+        ws[new] = w
+    arr = {
+        "ref_start": st.astype(np.int32),
+        "read_len": np.array([len(x) for x in seqs], np.int32),
+        "seq_off": seq_off,
+        "seq_nt16": np.concatenate(packed) if packed else np.zeros(0, np.uint8),
+        "cig_off": cig_off,
+        "n_cig": np.array([len(c) for c in cigars], np.int32),
+        "cigar": np.concatenate(cigars) if cigars else np.zeros(0, np.uint32),
+        "dataset": np.array(dss, np.uint8),
+        "write_scope": ws,
+        "scope_incid_off": np.array(offs, np.int64),
+        "incid_read": np.array(incid, np.int32),
+        "scope_span_start": np.array(span_start, np.int32),
+        "scope_span_len": np.array(span_len, np.int32),
+        "scope_ref_off": np.array(span_start, np.int64),      # one contig: nibble = position
+        "ref_nt16": pack_nibbles(ref),
+        "keep_pos": np.array(keep_pos, np.int32),
+        "keep_code": np.array(keep_code, np.uint8),
+    }
+    info = {"reads": n, "bases": int(arr["read_len"].astype(np.int64).sum()), "scopes": len(wpos),
+            "incidences": len(incid), "max_span": int(max(span_len) if span_len else 0),
+            "cigar_ops": int(len(arr["cigar"]))}
+    return arr, info
+
+
+# ---------------------------------------------------------------------------------------
 # BASELINE.json configs[1]
 # ---------------------------------------------------------------------------------------
 

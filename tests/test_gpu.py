@@ -107,6 +107,39 @@ def test_dense_scopes_all_variants_match_oracle(masker, oracle, seed, keep):
     masker.set_variant(0)
 
 
+@pytest.mark.parametrize("seed", [5, 6])
+def test_long_reads_match_oracle(masker, oracle, seed):
+    """SURVEY §8(d) C5 shape: 10-100 kb reads with ~5 % 1-3 bp indels, soft clips, N runs and
+    IUPAC codes in the reference; window scopes span up to ~200 kb (the LDS tile path)."""
+    from genomeanonymizer_amd.synth.batch import longread_batch
+    arr, info = longread_batch(seed, n_reads=120)
+    assert info["max_span"] > 16384
+    o_out, o_calls, o_bases, o_tot = oracle.mask(arr)
+    assert o_calls.sum() > 100
+    for v in MAIN:
+        masker.set_variant(v)
+        out, calls, bases, tot = masker.mask(arr)
+        assert np.array_equal(calls, o_calls), v
+        assert np.array_equal(bases, o_bases), v
+        assert np.array_equal(out, o_out), v
+    masker.set_variant(0)
+
+
+def test_deep_coverage_short_reads_match_oracle(masker, oracle):
+    """SURVEY §8(d) C3 density (~60x tumor+normal) on a small genome: window scopes of ~800
+    reads, observation lists near and over their LDS capacity."""
+    from genomeanonymizer_amd.synth.batch import config2_batch
+    arr, info = config2_batch(n_reads=800_000, genome=2_000_000, n_contigs=2, n_windows=600, n_germline=2_000)
+    o_out, o_calls, o_bases, _ = oracle.mask(arr)
+    for v in MAIN:
+        masker.set_variant(v)
+        out, calls, bases, tot = masker.mask(arr)
+        assert np.array_equal(calls, o_calls), v
+        assert np.array_equal(bases, o_bases), v
+        assert np.array_equal(out, o_out), v
+    masker.set_variant(0)
+
+
 def test_hip_rare_and_wide_paths_exercised(masker):
     from genomeanonymizer_amd.synth.batch import random_batch
     arr = random_batch(8, n_scopes=30, rare_frac=0.3, wide_scopes=4)

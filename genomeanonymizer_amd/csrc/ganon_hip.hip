@@ -928,9 +928,11 @@ __device__ __forceinline__ uint64_t expand2(uint32_t x) {
 // normal observation — the end state of the reference's per-position state machine
 // (variants.py:33-39) — and not the window's kept variant. TN calls are counted
 // and their observations in reads the scope writes are masked. All 16 codes are handled
-// alike (no re-run). A group whose observations overflow the list is re-scanned over halves
-// of its observed key range; a single key that overflows on its own (very deep coverage at one
-// site) is resolved by a flags scan and a patch scan.
+// alike (no re-run). A group whose observations overflow the LDS list (deep coverage, long
+// reads) is re-scanned once into its own global observation region (sized at upload, L2-hot),
+// aggregated in a global hash table of distinct keys (workgroup-scope atomics: only this
+// workgroup touches it), classified, and masked from the observation region — the reads are
+// not scanned again. A region that overflows too is split over halves of its key range.
 //
 // Output. GROUP: a device copy of seq precedes the kernel, masks are atomic XORs. GROUP_FUSED:
 // groups are launched in the order of their reads in the sequence buffer and each workgroup
@@ -949,10 +951,13 @@ constexpr int kGrpStack = 80;        // key ranges pending (bisection depth <= 6
 constexpr int kGrpPatch = 256;       // in-partition masks of a fused workgroup, sorted in LDS
 constexpr int kGrpMap = 4096;        // chunk -> segment map entries (larger tiles binary-search)
 constexpr int kGrpQuad = 256;        // lists up to this size are matched without sorting
+constexpr int kGrpMaxSpan = 1 << 20; // widest scope of the group kernels (20-bit position field)
+constexpr unsigned long long kEmpty = ~0ull;
 constexpr int64_t kPartAlign = 128;  // partition boundaries fall on whole lines
 constexpr uint32_t kSegMine = 1u << 26;   // the segment's read is written by this scope
 constexpr unsigned long long kNibMask = (1ull << 48) - 1;
-enum { kModeCollect = 0, kModeFlags = 1, kModePatch = 2 };
+// key-range passes: LDS observation list; the group's global observation region
+enum { kModeCollect = 0, kModeGlobal = 1 };
 // GANON_PARAM_GROUP_SKIP (profiling only, results invalid): phases left out
 enum { kSkipClassify = 1, kSkipChunks = 2, kSkipCopy = 4 };
 static_assert(kGrpTile == kGrpThreads && kGrpTile <= 256, "one staged record per thread, 8-bit map");
@@ -964,13 +969,13 @@ struct GrpShared {
   int pre[kGrpTile];
   uint8_t cmap[kGrpMap];            // staged segment of each chunk (tiles of <= kGrpMap chunks)
   int wsum[kGrpThreads / 64];
-  unsigned long long key[kGrpObs];
+  unsigned long long key[kGrpObs];   // observation list
   unsigned long long pay[kGrpObs];
   unsigned long long patch[kGrpPatch];   // nibble index << 4 | (from ^ to)
   unsigned long long stk_lo[kGrpStack], stk_hi[kGrpStack];
   int stk_mode[kGrpStack];
   unsigned long long kmin, kmax;
-  int top, n_obs, flags, masked, n_patch;
+  int top, n_obs, n_patch;
   int blk_calls, blk_bases;         // this workgroup's contribution to the totals
   int cnt_calls[kGrpMaxScopes];     // per-scope counts, written out once at the end
   int cnt_bases[kGrpMaxScopes];
@@ -1012,27 +1017,49 @@ __device__ __forceinline__ void sink_patch(GrpShared &sh, const PatchSink &k, in
   patch_nibble(k.out, nib, c, rc);
 }
 
+// A group's global observation region (overflow path): cap observations (key, payload) at
+// obs + off, and a hash table of up to 2 * cap distinct keys (key, 2-bit tumor/normal flags)
+// at tkey/tflag + 2 * off. Only the owning workgroup touches it.
+struct GrpGlobal {
+  unsigned long long *okey, *opay, *tkey;
+  unsigned int *tflag;
+  int64_t off;
+  int cap;
+};
+
+__device__ __forceinline__ unsigned long long ld_l2(const unsigned long long *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // sc1: past the CU's L1
+}
+__device__ __forceinline__ unsigned int ld_l2(const unsigned int *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ unsigned gtab_home(unsigned long long key, int tsize) {
+  const unsigned long long h = key * 0x9E3779B97F4A7C15ull;
+  return (unsigned)(((h >> 32) * (unsigned long long)tsize) >> 32);
+}
+
+__device__ __forceinline__ void grp_count(GrpShared &sh, int s_local, int calls, int bases);
+
 // payload: nibble index:48 | ref:4 | dataset:1 | mine:1
-__device__ __forceinline__ void grp_observe(GrpShared &sh, const GrpRange &R, const PatchSink &sink,
-                                            unsigned long long key, int64_t nib, int c, int rc, int ds, uint32_t fl) {
+__device__ __forceinline__ void grp_observe(GrpShared &sh, const GrpRange &R, const GrpGlobal &gg,
+                                            unsigned long long key, int64_t nib, int rc, int ds, uint32_t fl) {
   if (key < R.lo || key >= R.hi) return;
-  const bool mine = (fl & kSegMine) != 0;
+  const unsigned long long pay = (unsigned long long)nib | ((unsigned long long)rc << 48) |
+                                 ((unsigned long long)ds << 52) | ((unsigned long long)((fl >> 26) & 1) << 53);
+  const int k = atomicAdd(&sh.n_obs, 1);
   if (R.mode == kModeCollect) {
-    const int k = atomicAdd(&sh.n_obs, 1);
     if (k < kGrpObs) {
       sh.key[k] = key;
-      sh.pay[k] = (unsigned long long)nib | ((unsigned long long)rc << 48) | ((unsigned long long)ds << 52) |
-                  ((unsigned long long)(mine ? 1 : 0) << 53);
-    } else {
-      // key range of the overflow (the stored part is folded in after the scan)
-      atomicMin(&sh.kmin, key);
-      atomicMax(&sh.kmax, key);
+      sh.pay[k] = pay;
     }
-  } else if (R.mode == kModeFlags) {
-    atomicOr(&sh.flags, 1 << ds);
-  } else if (mine) {
-    sink_patch(sh, sink, nib, c, rc);
-    atomicAdd(&sh.masked, 1);
+  } else {
+    atomicMin(&sh.kmin, key);
+    atomicMax(&sh.kmax, key);
+    if (k < gg.cap) {
+      gg.okey[gg.off + k] = key;
+      gg.opay[gg.off + k] = pay;
+    }
   }
 }
 
@@ -1096,7 +1123,7 @@ __device__ __forceinline__ int grp_find(const GrpShared &sh, int nh, int total, 
 // covering its chunk at once (one memory round trip per chunk), then takes the K 16-base
 // windows out of registers with static indices.
 template <int K, bool REF2>
-__device__ __forceinline__ void grp_scan(const DevBatch &B, GrpShared &sh, const GrpRange &R, const PatchSink &sink,
+__device__ __forceinline__ void grp_scan(const DevBatch &B, GrpShared &sh, const GrpRange &R, const GrpGlobal &gg,
                                          int64_t i_begin, int64_t i_end, const int4 *__restrict__ rec4,
                                          const int2 *__restrict__ rec2, int skip) {
   const int tid = threadIdx.x;
@@ -1155,10 +1182,11 @@ __device__ __forceinline__ void grp_scan(const DevBatch &B, GrpShared &sh, const
           const int rc = (int)((rv >> (4 * k)) & 15);
           if (c == 15 || !is_acgt(rc)) continue;
           const unsigned long long key = sk | ((unsigned long long)(pos_seg + qi + k) << 4) | (unsigned long long)c;
-          grp_observe(sh, R, sink, key, sn + 16 * i + k, c, rc, ds_, (uint32_t)r2.x);
+          grp_observe(sh, R, gg, key, sn + 16 * i + k, rc, ds_, (uint32_t)r2.x);
         }
       }
     }
+    if (R.mode == kModeGlobal) __builtin_amdgcn_s_waitcnt(0);   // region stores at L2 before the barrier
     __syncthreads();
   }
 }
@@ -1250,6 +1278,70 @@ __device__ __forceinline__ void grp_classify(const DevBatch &B, GrpShared &sh, i
   }
 }
 
+// Overflow path: n observations of one key range sit in the group's global region. Aggregate
+// them in a hash table of distinct keys (workgroup-scope atomics in L2), count the TN calls
+// (minus the kept variant), and mask the observations of reads the scopes write.
+__device__ __forceinline__ void grp_global(const DevBatch &B, GrpShared &sh, const GrpGlobal &gg, int n,
+                                           int s_begin, const PatchSink &sink) {
+  const int tid = threadIdx.x;
+  const int tsize = max(2 * n, 64);
+  unsigned long long *tk = gg.tkey + 2 * gg.off;
+  unsigned int *tf = gg.tflag + 2 * gg.off;
+  for (int i = tid; i < tsize; i += kGrpThreads) {
+    tk[i] = kEmpty;
+    tf[i] = 0;
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  for (int i = tid; i < n; i += kGrpThreads) {
+    const unsigned long long key = ld_l2(gg.okey + gg.off + i);
+    const int ds = (int)((ld_l2(gg.opay + gg.off + i) >> 52) & 1);
+    unsigned slot = gtab_home(key, tsize);
+    for (int probe = 0; probe < tsize; ++probe) {
+      unsigned long long expected = kEmpty;
+      __hip_atomic_compare_exchange_strong(tk + slot, &expected, key, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (expected == kEmpty || expected == key) {
+        __hip_atomic_fetch_or(tf + slot, 1u << ds, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        break;
+      }
+      if (++slot == (unsigned)tsize) slot = 0;
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  // calls: one per TN slot
+  for (int i = tid; i < tsize; i += kGrpThreads) {
+    const unsigned long long key = ld_l2(tk + i);
+    if (key == kEmpty || ld_l2(tf + i) != 3) continue;
+    const int c = (int)(key & 15);
+    if (grp_kept(B, s_begin + (int)(key >> 52), (int64_t)((key >> 4) & kNibMask), c)) continue;
+    grp_count(sh, (int)(key >> 52), 1, 0);
+  }
+  // masks: every observation of a read the scope writes whose key is TN
+  for (int i = tid; i < n; i += kGrpThreads) {
+    const unsigned long long pay = ld_l2(gg.opay + gg.off + i);
+    if (!((pay >> 53) & 1)) continue;
+    const unsigned long long key = ld_l2(gg.okey + gg.off + i);
+    unsigned slot = gtab_home(key, tsize);
+    unsigned int f = 0;
+    for (int probe = 0; probe < tsize; ++probe) {
+      const unsigned long long k = ld_l2(tk + slot);
+      if (k == key) {
+        f = ld_l2(tf + slot);
+        break;
+      }
+      if (k == kEmpty) break;
+      if (++slot == (unsigned)tsize) slot = 0;
+    }
+    if (f != 3) continue;
+    const int c = (int)(key & 15);
+    if (grp_kept(B, s_begin + (int)(key >> 52), (int64_t)((key >> 4) & kNibMask), c)) continue;
+    sink_patch(sh, sink, (int64_t)(pay & kNibMask), c, (int)((pay >> 48) & 15));
+    grp_count(sh, (int)(key >> 52), 0, 1);
+  }
+}
+
 // Fused: apply the sorted in-partition list (nibble << 4 | from ^ to) with one plain byte store
 // per masked byte, seq[b] ^ mask — the partition copy of that byte has drained before.
 __device__ __forceinline__ void grp_patch_bytes(const DevBatch &B, GrpShared &sh, int np, uint8_t *out) {
@@ -1273,21 +1365,26 @@ __device__ __forceinline__ void grp_release() {
   __syncthreads();
 }
 
-// groups: 3 x int4 per group, in launch order: {s_begin, s_end, seg_begin lo, hi},
-// {seg_end lo, hi, seg_mid lo, hi}, {partition begin lo, hi, end lo, hi} (bytes; fused only);
-// segments [seg_begin, seg_mid) have an all-ACGT reference range (2-bit reference).
+// groups: 4 x int4 per group, in launch order: {s_begin, s_end, seg_begin lo, hi},
+// {seg_end lo, hi, seg_mid lo, hi}, {partition begin lo, hi, end lo, hi} (bytes; fused only),
+// {global region offset lo, hi, capacity, 0}; segments [seg_begin, seg_mid) have an all-ACGT
+// reference range (2-bit reference).
 template <int U, bool FUSED>
 __global__ void __launch_bounds__(kGrpThreads, (U <= 2 ? 6 : U == 4 ? 5 : 4)) k_group(const DevBatch B, const int4 *__restrict__ groups,
                                                        const int4 *__restrict__ rec4, const int2 *__restrict__ rec2,
                                                        uint8_t *__restrict__ out, int32_t *scope_calls,
                                                        int32_t *scope_bases, int32_t *part,
                                                        unsigned long long *far, int *far_count, int64_t far_cap,
+                                                       unsigned long long *gokey, unsigned long long *gopay,
+                                                       unsigned long long *gtkey, unsigned int *gtflag,
                                                        int skip, int nt_copy) {
   __shared__ GrpShared sh;
   const int tid = threadIdx.x;
-  const int4 g0 = groups[3 * blockIdx.x];
-  const int4 g1 = groups[3 * blockIdx.x + 1];
-  const int4 g2 = groups[3 * blockIdx.x + 2];
+  const int4 g0 = groups[4 * blockIdx.x];
+  const int4 g1 = groups[4 * blockIdx.x + 1];
+  const int4 g2 = groups[4 * blockIdx.x + 2];
+  const int4 g3 = groups[4 * blockIdx.x + 3];
+  const GrpGlobal gg{gokey, gopay, gtkey, gtflag, i64_of(g3.x, g3.y), g3.z};
   const int s_begin = g0.x, s_end = g0.y;
   const int64_t i_begin = i64_of(g0.z, g0.w), i_end = i64_of(g1.x, g1.y), i_mid = i64_of(g1.z, g1.w);
   PatchSink sink{out, i64_of(g2.x, g2.y), i64_of(g2.z, g2.w), far, far_count, far_cap, FUSED, FUSED, false};
@@ -1333,7 +1430,7 @@ __global__ void __launch_bounds__(kGrpThreads, (U <= 2 ? 6 : U == 4 ? 5 : 4)) k_
       // per-scope counts (wide scopes in the id range belong to the tile path) and the
       // workgroup's partial totals (k_finish sums them)
       for (int i = tid; i < s_end - s_begin; i += kGrpThreads) {
-        if (B.span_len[s_begin + i] > kSmallCap1) continue;
+        if (B.span_len[s_begin + i] > kGrpMaxSpan) continue;
         scope_calls[s_begin + i] = sh.cnt_calls[i];
         scope_bases[s_begin + i] = sh.cnt_bases[i];
       }
@@ -1350,55 +1447,27 @@ __global__ void __launch_bounds__(kGrpThreads, (U <= 2 ? 6 : U == 4 ? 5 : 4)) k_
       sh.n_obs = 0;
       sh.kmin = ~0ull;
       sh.kmax = 0ull;
-      sh.flags = 0;
-      sh.masked = 0;
     }
     __syncthreads();
     if (B.ref2) {
-      grp_scan<U, true>(B, sh, R, sink, i_begin, i_mid, rec4, rec2, skip);
-      grp_scan<U, false>(B, sh, R, sink, i_mid, i_end, rec4, rec2, skip);
+      grp_scan<U, true>(B, sh, R, gg, i_begin, i_mid, rec4, rec2, skip);
+      grp_scan<U, false>(B, sh, R, gg, i_mid, i_end, rec4, rec2, skip);
     } else {
-      grp_scan<U, false>(B, sh, R, sink, i_begin, i_end, rec4, rec2, skip);
+      grp_scan<U, false>(B, sh, R, gg, i_begin, i_end, rec4, rec2, skip);
     }
     // (grp_scan ends on a barrier)
     if (skip & kSkipClassify) continue;
-    const int s = s_begin + (int)(R.lo >> 52);
-    if (R.mode == kModeFlags) {
-      if (tid == 0 && sh.flags == 3 && !grp_kept(B, s, (int64_t)((R.lo >> 4) & kNibMask), (int)(R.lo & 15))) {
-        grp_count(sh, s - s_begin, 1, 0);
-        const int t = ++sh.top;
-        sh.stk_lo[t] = R.lo;
-        sh.stk_hi[t] = R.hi;
-        sh.stk_mode[t] = kModePatch;
+    if (R.mode == kModeGlobal) {
+      const int n = sh.n_obs;
+      if (n <= gg.cap) {
+        grp_global(B, sh, gg, n, s_begin, sink);
+        continue;
       }
-      continue;
-    }
-    if (R.mode == kModePatch) {
-      if (tid == 0) grp_count(sh, s - s_begin, 0, sh.masked);
-      continue;
-    }
-    const int n = sh.n_obs;
-    if (n > kGrpObs) {
-      for (int i = tid; i < kGrpObs; i += kGrpThreads) {
-        atomicMin(&sh.kmin, sh.key[i]);
-        atomicMax(&sh.kmax, sh.key[i]);
-      }
-      if (sink.lds) {
-        // bisection from here on: in-partition masks become atomics after a release
-        grp_release();
-        sink.lds = false;
-      }
-      __syncthreads();
+      // the region overflowed too: halves of the observed key range, each from the list again
       if (tid == 0) {
-        const unsigned long long a = sh.kmin, b = sh.kmax;
+        const unsigned long long a = sh.kmin, b = sh.kmax, mid = a + (b - a) / 2;
         int t = sh.top;
-        if (a == b) {
-          ++t;
-          sh.stk_lo[t] = a;
-          sh.stk_hi[t] = a + 1;
-          sh.stk_mode[t] = kModeFlags;
-        } else if (t + 2 < kGrpStack) {
-          const unsigned long long mid = a + (b - a) / 2;
+        if (a < b && t + 2 < kGrpStack) {
           ++t;
           sh.stk_lo[t] = mid + 1;
           sh.stk_hi[t] = b + 1;
@@ -1409,6 +1478,21 @@ __global__ void __launch_bounds__(kGrpThreads, (U <= 2 ? 6 : U == 4 ? 5 : 4)) k_
           sh.stk_mode[t] = kModeCollect;
         }
         sh.top = t;
+      }
+      continue;
+    }
+    const int n = sh.n_obs;
+    if (n > kGrpObs) {
+      if (sink.lds) {
+        // masks from here on are atomic XORs, after a release of the partition copy
+        grp_release();
+        sink.lds = false;
+      }
+      if (tid == 0) {   // the same key range again, into the global region
+        const int t = ++sh.top;
+        sh.stk_lo[t] = R.lo;
+        sh.stk_hi[t] = R.hi;
+        sh.stk_mode[t] = kModeGlobal;
       }
       continue;
     }
@@ -1695,7 +1779,12 @@ struct ganon_dbatch {
   unsigned long long *far = nullptr;    // fused: masks outside the masking group's partition
   int64_t far_cap = 0;
   int32_t *grp_part = nullptr;          // k_group: (calls, bases) per workgroup
-  int32_t *large_ids = nullptr;         // scopes of the tile path
+  int32_t *large_ids = nullptr;         // scopes of the tile path under the group variants (huge)
+  unsigned long long *gokey = nullptr, *gopay = nullptr, *gtkey = nullptr;   // group overflow regions
+  unsigned int *gtflag = nullptr;
+  Tile *tiles_h = nullptr;              // tiles / written reads of huge scopes (group variants)
+  int32_t *large_written_h = nullptr;
+  int32_t n_tiles_h = 0, n_large_written_h = 0, n_huge_scopes = 0;
   bool ran = false;
 };
 
@@ -2068,7 +2157,24 @@ GANON_API int ganon_batch_upload(ganon_ctx *ctx, const ganon_batch *b, ganon_dba
   if ((rc = dev_copy(ctx, db, &db->large_written, large_written.data(), large_written.size()))) return bail(rc);
   db->n_large_written = (int32_t)large_written.size();
   db->n_large_scopes = (int32_t)large_scopes.size();
-  if ((rc = dev_copy(ctx, db, &db->large_ids, large_scopes.data(), large_scopes.size()))) return bail(rc);
+  {
+    // the group kernels take every scope up to kGrpMaxSpan positions; only wider ("huge")
+    // scopes keep the tile path under the group variants
+    std::vector<Tile> tiles_h;
+    std::vector<int32_t> written_h, ids_h;
+    for (const Tile &t : tiles)
+      if (b->scope_span_len[t.scope] > kGrpMaxSpan) tiles_h.push_back(t);
+    for (int32_t r : large_written)
+      if (b->scope_span_len[b->write_scope[r]] > kGrpMaxSpan) written_h.push_back(r);
+    for (int32_t x : large_scopes)
+      if (b->scope_span_len[x] > kGrpMaxSpan) ids_h.push_back(x);
+    if ((rc = dev_copy(ctx, db, &db->tiles_h, tiles_h.data(), tiles_h.size()))) return bail(rc);
+    if ((rc = dev_copy(ctx, db, &db->large_written_h, written_h.data(), written_h.size()))) return bail(rc);
+    if ((rc = dev_copy(ctx, db, &db->large_ids, ids_h.data(), ids_h.size()))) return bail(rc);
+    db->n_tiles_h = (int32_t)tiles_h.size();
+    db->n_large_written_h = (int32_t)written_h.size();
+    db->n_huge_scopes = (int32_t)ids_h.size();
+  }
   db->max_small_span = max_small;
   {
     // per-incidence records for the v2 scope kernel (scope-major, one int4 each)
@@ -2124,6 +2230,7 @@ GANON_API int ganon_batch_upload(ganon_ctx *ctx, const ganon_batch *b, ganon_dba
       int32_t s0, s1;
       int64_t i0, i1, first;   // first: lowest seq_off of a read the group writes
       int64_t mid;             // segments [i0, mid) have an all-ACGT reference range
+      int64_t bases;           // aligned bases of its segments (sizes the overflow region)
     };
     std::vector<G> gs;
     int32_t g_s0 = -1;
@@ -2156,6 +2263,9 @@ GANON_API int ganon_batch_upload(ganon_ctx *ctx, const ganon_batch *b, ganon_dba
     std::vector<int2> c2, d2;
     auto close_group = [&](int32_t s_end) {
       if (g_s0 < 0) return;
+      int64_t bases = 0;
+      for (const int2 &x : c2) bases += x.x & 0xFFFFFF;
+      for (const int2 &x : d2) bases += x.x & 0xFFFFFF;
       s4.insert(s4.end(), c4.begin(), c4.end());
       s2.insert(s2.end(), c2.begin(), c2.end());
       const int64_t mid = (int64_t)s4.size();
@@ -2165,7 +2275,7 @@ GANON_API int ganon_batch_upload(ganon_ctx *ctx, const ganon_batch *b, ganon_dba
       c2.clear();
       d4.clear();
       d2.clear();
-      gs.push_back(G{g_s0, s_end, g_i0, (int64_t)s4.size(), g_first, mid});
+      gs.push_back(G{g_s0, s_end, g_i0, (int64_t)s4.size(), g_first, mid, bases});
       g_s0 = -1;
       g_first = INT64_MAX;
     };
@@ -2189,7 +2299,7 @@ GANON_API int ganon_batch_upload(ganon_ctx *ctx, const ganon_batch *b, ganon_dba
       }
     };
     for (int32_t s = 0; s < b->n_scopes; ++s) {
-      if (tab_off[s] >= 0) continue;   // wide scope: tile path
+      if (b->scope_span_len[s] > kGrpMaxSpan) continue;   // huge scope: tile path
       const int64_t i0 = b->scope_incid_off[s], i1 = b->scope_incid_off[s + 1];
       int64_t nseg = 0;
       for (int64_t i = i0; i < i1; ++i) segments_of(b->incid_read[i], [&](int64_t, int64_t, int64_t) { ++nseg; });
@@ -2237,20 +2347,30 @@ GANON_API int ganon_batch_upload(ganon_ctx *ctx, const ganon_batch *b, ganon_dba
     int64_t far_cap = 0;
     for (int32_t r = 0; r < b->n_reads; ++r) {
       const int32_t ws = b->write_scope[r];
-      if (ws < 0 || tab_off[ws] >= 0 || b->read_len[r] == 0) continue;
+      if (ws < 0 || b->scope_span_len[ws] > kGrpMaxSpan || b->read_len[r] == 0) continue;
       const int64_t k = rank[std::upper_bound(gs.begin(), gs.end(), ws,
                                               [](int32_t v, const G &g) { return v < g.s0; }) - gs.begin() - 1];
       const int64_t r0 = b->seq_off[r], r1 = r0 + ((int64_t)b->read_len[r] + 1) / 2;
       const int64_t in = std::max<int64_t>(0, std::min(r1, part[k + 1]) - std::max(r0, part[k]));
       far_cap += 2 * ((r1 - r0) - in);
     }
-    std::vector<int4> grp(3 * (size_t)ng);
+    // overflow regions: (bases / 48 + 256) observations per group, i.e. up to ~2 % of its
+    // aligned bases mismatching (more: key-range halving)
+    std::vector<int4> grp(4 * (size_t)ng);
+    int64_t region = 0;
     for (int32_t k = 0; k < ng; ++k) {
       const G &g = gs[order[k]];
-      grp[3 * k] = make_int4(g.s0, g.s1, lo32(g.i0), hi32(g.i0));
-      grp[3 * k + 1] = make_int4(lo32(g.i1), hi32(g.i1), lo32(g.mid), hi32(g.mid));
-      grp[3 * k + 2] = make_int4(lo32(part[k]), hi32(part[k]), lo32(part[k + 1]), hi32(part[k + 1]));
+      const int64_t cap = std::min<int64_t>(g.bases / 48 + 256, INT32_MAX / 2);
+      grp[4 * k] = make_int4(g.s0, g.s1, lo32(g.i0), hi32(g.i0));
+      grp[4 * k + 1] = make_int4(lo32(g.i1), hi32(g.i1), lo32(g.mid), hi32(g.mid));
+      grp[4 * k + 2] = make_int4(lo32(part[k]), hi32(part[k]), lo32(part[k + 1]), hi32(part[k + 1]));
+      grp[4 * k + 3] = make_int4(lo32(region), hi32(region), (int)cap, 0);
+      region += cap;
     }
+    if ((rc = dev_alloc(ctx, db, &db->gokey, (size_t)region))) return bail(rc);
+    if ((rc = dev_alloc(ctx, db, &db->gopay, (size_t)region))) return bail(rc);
+    if ((rc = dev_alloc(ctx, db, &db->gtkey, 2 * (size_t)region + 64))) return bail(rc);
+    if ((rc = dev_alloc(ctx, db, &db->gtflag, 2 * (size_t)region + 64))) return bail(rc);
     if ((rc = dev_copy(ctx, db, &db->groups, grp.data(), grp.size()))) return bail(rc);
     if ((rc = dev_copy(ctx, db, &db->seg4, s4.data(), s4.size()))) return bail(rc);
     if ((rc = dev_copy(ctx, db, &db->seg2, s2.data(), s2.size()))) return bail(rc);
@@ -2322,7 +2442,11 @@ GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
     HIP_OR_FAIL(hipMemcpyAsync(db->totals, db->static_totals, GANON_N_TOTALS * sizeof(unsigned long long),
                                hipMemcpyDeviceToDevice, st));
   }
-  if (db->n_large_scopes) {
+  const Tile *tiles = v4 ? db->tiles_h : db->tiles;
+  const int32_t n_tiles = v4 ? db->n_tiles_h : db->n_tiles;
+  const int32_t *large_written = v4 ? db->large_written_h : db->large_written;
+  const int32_t n_large_written = v4 ? db->n_large_written_h : db->n_large_written;
+  if (v4 ? db->n_huge_scopes : db->n_large_scopes) {
     // wide scopes are counted with atomics (tiles)
     HIP_OR_FAIL(hipMemsetAsync(db->scope_calls, 0, (size_t)db->n_scopes * sizeof(int32_t), st));
     HIP_OR_FAIL(hipMemsetAsync(db->scope_bases, 0, (size_t)db->n_scopes * sizeof(int32_t), st));
@@ -2348,7 +2472,8 @@ GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
                                                                                        : k_group<1, false>);
     kern<<<db->n_groups, kGrpThreads, 0, st>>>(B, db->groups, db->seg4, db->seg2, db->out, db->scope_calls,
                                                db->scope_bases, db->grp_part, db->far, db->counters + 2,
-                                               db->far_cap, ctx->group_skip, ctx->nt_copy);
+                                               db->far_cap, db->gokey, db->gopay, db->gtkey, db->gtflag,
+                                               ctx->group_skip, ctx->nt_copy);
     if ((rc = check_launch(ctx, "k_group"))) return rc;
   }
   const int caps[2] = {kSmallCap0, kSmallCap1};
@@ -2382,10 +2507,10 @@ GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
       if ((rc = check_launch(ctx, "k_scope_wave"))) return rc;
     }
   }
-  if (db->n_tiles) {
+  if (n_tiles) {
     KernelScope ks(ctx, "k_tile_large<1>");
-    k_tile_large<1><<<db->n_tiles, kBlock, tile_lds_bytes(1), st>>>(
-        B, db->tiles, nullptr, db->n_tiles, nullptr, db->large_incid, db->tab_off, db->tn_tab, db->scope_calls,
+    k_tile_large<1><<<n_tiles, kBlock, tile_lds_bytes(1), st>>>(
+        B, tiles, nullptr, n_tiles, nullptr, db->large_incid, db->tab_off, db->tn_tab, db->scope_calls,
         db->rare_tile_list, db->counters + 1);
     if ((rc = check_launch(ctx, "k_tile_large<1>"))) return rc;
   }
@@ -2398,18 +2523,18 @@ GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
         nullptr, nullptr);
     if ((rc = check_launch(ctx, "k_scope_small<4>"))) return rc;
   }
-  if (db->n_tiles) {
+  if (n_tiles) {
     KernelScope ks(ctx, "k_tile_large<4>/rare");
-    const int grid = std::min<int>(db->n_tiles, kPersistGrid);
+    const int grid = std::min<int>(n_tiles, kPersistGrid);
     k_tile_large<4><<<grid, kBlock, tile_lds_bytes(4), st>>>(
-        B, db->tiles, db->rare_tile_list, 0, db->counters + 1, db->large_incid, db->tab_off, db->tn_tab,
+        B, tiles, db->rare_tile_list, 0, db->counters + 1, db->large_incid, db->tab_off, db->tn_tab,
         db->scope_calls, nullptr, nullptr);
     if ((rc = check_launch(ctx, "k_tile_large<4>"))) return rc;
   }
-  if (db->n_large_written) {
+  if (n_large_written) {
     KernelScope ks(ctx, "k_mask_large");
-    const int grid = std::min<int>((db->n_large_written + kWaves - 1) / kWaves, 8192);
-    k_mask_large<<<grid, kBlock, 0, st>>>(B, db->large_written, db->n_large_written, db->tab_off, db->tn_tab,
+    const int grid = std::min<int>((n_large_written + kWaves - 1) / kWaves, 8192);
+    k_mask_large<<<grid, kBlock, 0, st>>>(B, large_written, n_large_written, db->tab_off, db->tn_tab,
                                           db->out, db->scope_bases);
     if ((rc = check_launch(ctx, "k_mask_large"))) return rc;
   }
@@ -2418,7 +2543,7 @@ GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
       // far masks (fused), totals from the group partials and the wide scopes, counter reset
       KernelScope ks(ctx, "k_finish");
       k_finish<<<64, kBlock, 0, st>>>(db->far, v5 && db->n_groups ? db->far_cap : 0, db->out, db->grp_part,
-                                      db->n_groups, db->large_ids, db->n_large_scopes, db->scope_calls,
+                                      db->n_groups, db->large_ids, db->n_huge_scopes, db->scope_calls,
                                       db->scope_bases, db->static_totals, db->counters, db->acc, db->totals);
       if ((rc = check_launch(ctx, "k_finish"))) return rc;
     } else {

@@ -29,10 +29,11 @@ sys.path.insert(0, REPO)
 
 HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 SMALL_CAP0, SMALL_CAP1 = 2560, 16384    # scope classes of ganon_hip.hip (kSmallCap0/1)
+GROUP_MAX_SPAN = 1 << 20                # kGrpMaxSpan: widest scope of the group kernels
 VARIANT_NAMES = {0: "default", 1: "v0_block", 2: "v1_wave", 3: "v2_copy_patch", 4: "v4_group",
                  5: "v5_group_fused", 6: "v3_persistent"}
 # how each variant writes reads (kernel_bytes attribution)
-VARIANT_WRITE = {0: "fused", 1: "whole", 2: "whole", 3: "copy_patch", 4: "copy_patch", 5: "fused",
+VARIANT_WRITE = {0: "fused", 1: "whole", 2: "whole", 3: "copy_patch", 4: "group", 5: "fused",
                  6: "copy_patch"}
 # A/B configurations: (name, variant, group-kernel unroll)
 AB_CONFIGS = [(VARIANT_NAMES[v], v, 2) for v in (1, 2, 3, 6, 4)] + [(f"v5_group_fused_k{u}", 5, u) for u in (1, 2, 4)]
@@ -59,8 +60,9 @@ def kernel_bytes(arr, mode: str = "fused") -> dict:
     ceil(L/2) + 4*n_cigar + 8; each scope ceil(span/2) of reference. A read's own cost goes
     to the kernel that writes it: mode "whole" — the scope kernel of its write scope, or the
     pass-through copy; "copy_patch" — the device copy owns every read's in + out bytes and the
-    scope kernel its 4*n_cigar + 16; "fused" — the group kernel (it copies the whole buffer
-    partition by partition) except the reads the wide-scope kernels write.
+    scope kernel its 4*n_cigar + 16 ("group": the same with the group kernel owning every scope up
+    to 1 Mi positions); "fused" — the group kernel (it copies the whole buffer partition by
+    partition) except the reads the wide-scope kernels write.
     Extra incidences and reference bytes go to the kernel of their scope; "group" (both small
     classes) is what the group kernels own. The per-class figures sum to the formula."""
     L = arr["read_len"].astype(np.int64)
@@ -68,13 +70,15 @@ def kernel_bytes(arr, mode: str = "fused") -> dict:
     nc = arr["n_cig"].astype(np.int64)
     span = arr["scope_span_len"].astype(np.int64)
     cls = np.where(span <= SMALL_CAP0, 0, np.where(span <= SMALL_CAP1, 1, 2))
+    if mode in ("fused", "group"):
+        cls = np.where(span <= GROUP_MAX_SPAN, 0, 2)     # group kernels take every scope up to 1 Mi positions
     names = ["small2.5K", "small16K", "large"]
     out = {n: 0 for n in names}
     out["copy"] = 0
     ws = arr["write_scope"].astype(np.int64)
     wcls = np.where(ws >= 0, cls[np.maximum(ws, 0)], 3)
     base = 2 * h + 4 * nc + 16
-    if mode == "copy_patch":
+    if mode in ("copy_patch", "group"):
         out["copy"] += int((2 * h).sum())
         base = 4 * nc + 16
     elif mode == "fused":

@@ -943,6 +943,9 @@ __device__ __forceinline__ uint64_t expand2(uint32_t x) {
 // global list applied by k_finish after the kernel. Partial-line stores from different
 // workgroups cost ~4x whole-line stores on MI355X (tools/membench.hip), hence partitions.
 constexpr int kGrpThreads = 256;
+#ifndef GANON_K2_BLOCKS
+#define GANON_K2_BLOCKS 6   // resident workgroups per CU the K = 2 instance is compiled for
+#endif
 constexpr int kGrpTile = 256;        // segment records staged per tile
 constexpr int kGrpTarget = 256;      // segments per group (a larger scope forms its own group)
 constexpr int kGrpObs = 512;         // observations per LDS list
@@ -954,18 +957,27 @@ constexpr int kGrpQuad = 256;        // lists up to this size are matched withou
 constexpr int kGrpMaxSpan = 1 << 20; // widest scope of the group kernels (20-bit position field)
 constexpr unsigned long long kEmpty = ~0ull;
 constexpr int64_t kPartAlign = 128;  // partition boundaries fall on whole lines
-constexpr uint32_t kSegMine = 1u << 26;   // the segment's read is written by this scope
+// segment record (int4, 16 bytes): x = query nibble bits 0-31, y = reference nibble bits 0-31,
+// z = query nibble bits 32-39 | reference nibble bits 32-39 << 8 | length << 16 (14 bits) |
+// dataset << 30 | mine << 31, w = scope_local | (pos - span_start) << 12
+constexpr int kSegMaxLen = (1 << 14) - 1;   // longer aligned runs are cut into pieces at upload
+constexpr uint32_t kSegMine = 1u << 31;     // the segment's read is written by this scope
 constexpr unsigned long long kNibMask = (1ull << 48) - 1;
-// key-range passes: LDS observation list; the group's global observation region
-enum { kModeCollect = 0, kModeGlobal = 1 };
+// key-range pass: observations to the LDS list, overflow to the group's global region
+enum { kModeCollect = 0 };
 // GANON_PARAM_GROUP_SKIP (profiling only, results invalid): phases left out
 enum { kSkipClassify = 1, kSkipChunks = 2, kSkipCopy = 4 };
 static_assert(kGrpTile == kGrpThreads && kGrpTile <= 256, "one staged record per thread, 8-bit map");
 
+// The few batch arrays the group kernels read (a slim kernel argument keeps SGPRs free).
+struct GrpBatch {
+  const uint8_t *seq, *ref, *keep_code;
+  const uint32_t *ref2;
+  const int32_t *keep_pos, *span_start, *span_len;
+};
+
 struct GrpShared {
-  int4 rec[kGrpTile];               // {query nibble lo, hi, reference nibble lo, hi}
-  int2 rec2[kGrpTile];              // {length | dataset << 24 | mine << 26,
-                                    //  scope_local | (segment pos - span_start) << 12}
+  int4 rec[kGrpTile];               // segment records (layout at kSegMine)
   int pre[kGrpTile];
   uint8_t cmap[kGrpMap];            // staged segment of each chunk (tiles of <= kGrpMap chunks)
   int wsum[kGrpThreads / 64];
@@ -987,12 +999,21 @@ struct GrpRange {
 };
 
 // Where a masked base goes.
+// Rarely used outputs and scratch of the group kernels, read through one pointer (device
+// memory) so that their addresses do not occupy scalar registers for the whole kernel.
+struct GrpAux {
+  int32_t *scope_calls, *scope_bases, *part;   // per-scope counts; per-workgroup partial totals
+  unsigned long long *far;                      // fused: masks of bytes outside the partition
+  int *far_count;
+  int64_t far_cap;
+  unsigned long long *okey, *opay, *tkey;       // overflow regions (GrpGlobal)
+  unsigned int *tflag;
+};
+
 struct PatchSink {
   uint8_t *out;
   int64_t p0, p1;                   // fused: this workgroup's partition of out (bytes)
-  unsigned long long *far;          // fused: masks of bytes outside the partition
-  int *far_count;
-  int64_t far_cap;
+  const GrpAux *aux;                // far-mask list
   bool fused;
   bool lds;                         // fused, in-partition masks into the LDS list
   bool in_only;                     // fused re-run after an LDS list overflow: in-partition only
@@ -1004,8 +1025,8 @@ __device__ __forceinline__ void sink_patch(GrpShared &sh, const PatchSink &k, in
     const int64_t byte = nib >> 1;
     if (byte < k.p0 || byte >= k.p1) {
       if (k.in_only) return;
-      const int i = atomicAdd(k.far_count, 1);
-      if (i < k.far_cap) k.far[i] = e;
+      const int i = atomicAdd(k.aux->far_count, 1);
+      if (i < k.aux->far_cap) k.aux->far[i] = e;
       return;
     }
     if (k.lds) {
@@ -1021,8 +1042,7 @@ __device__ __forceinline__ void sink_patch(GrpShared &sh, const PatchSink &k, in
 // obs + off, and a hash table of up to 2 * cap distinct keys (key, 2-bit tumor/normal flags)
 // at tkey/tflag + 2 * off. Only the owning workgroup touches it.
 struct GrpGlobal {
-  unsigned long long *okey, *opay, *tkey;
-  unsigned int *tflag;
+  const GrpAux *aux;
   int64_t off;
   int cap;
 };
@@ -1043,45 +1063,40 @@ __device__ __forceinline__ void grp_count(GrpShared &sh, int s_local, int calls,
 
 // payload: nibble index:48 | ref:4 | dataset:1 | mine:1
 __device__ __forceinline__ void grp_observe(GrpShared &sh, const GrpRange &R, const GrpGlobal &gg,
-                                            unsigned long long key, int64_t nib, int rc, int ds, uint32_t fl) {
+                                            unsigned long long key, int64_t nib, int rc, int ds, uint32_t mine) {
   if (key < R.lo || key >= R.hi) return;
   const unsigned long long pay = (unsigned long long)nib | ((unsigned long long)rc << 48) |
-                                 ((unsigned long long)ds << 52) | ((unsigned long long)((fl >> 26) & 1) << 53);
+                                 ((unsigned long long)ds << 52) | ((unsigned long long)mine << 53);
   const int k = atomicAdd(&sh.n_obs, 1);
-  if (R.mode == kModeCollect) {
-    if (k < kGrpObs) {
-      sh.key[k] = key;
-      sh.pay[k] = pay;
-    }
+  if (k < kGrpObs) {
+    sh.key[k] = key;
+    sh.pay[k] = pay;
   } else {
-    atomicMin(&sh.kmin, key);
-    atomicMax(&sh.kmax, key);
-    if (k < gg.cap) {
-      gg.okey[gg.off + k] = key;
-      gg.opay[gg.off + k] = pay;
+    // past the LDS list: straight into the group's global region (no second scan)
+    if (k - kGrpObs < gg.cap - kGrpObs) {
+      gg.aux->okey[gg.off + (k - kGrpObs)] = key;
+      gg.aux->opay[gg.off + (k - kGrpObs)] = pay;
     }
   }
 }
 
 // Is (scope s, pos_off, allele c) the window's kept variant? (clear_keep's rule)
-__device__ __forceinline__ bool grp_kept(const DevBatch &B, int s, int64_t pos_off, int c) {
+__device__ __forceinline__ bool grp_kept(const GrpBatch &B, int s, int64_t pos_off, int c) {
   const int kp = B.keep_pos[s];
   return kp >= 0 && B.keep_code[s] == c && (int64_t)kp - B.span_start[s] == pos_off;
 }
 
 // Stage records [c0, c0 + nh) in LDS with the exclusive prefix of their chunk counts;
 // returns the tile's chunk total.
-__device__ __forceinline__ int grp_tile(GrpShared &sh, const int4 *__restrict__ rec4, const int2 *__restrict__ rec2,
-                                        int64_t c0, int nh, int chunk) {
+__device__ __forceinline__ int grp_tile(GrpShared &sh, const int4 *__restrict__ rec4, int64_t c0, int nh,
+                                        int chunk) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t ix = c0 + (tid < nh ? tid : nh - 1);
   const int4 r = rec4[ix];
-  const int2 r2 = rec2[ix];
   int nck = 0;
   if (tid < nh) {
     sh.rec[tid] = r;
-    sh.rec2[tid] = r2;
-    nck = ((r2.x & 0xFFFFFF) + chunk - 1) / chunk;
+    nck = ((((uint32_t)r.z >> 16) & kSegMaxLen) + chunk - 1) / chunk;
   }
   int incl = nck;
 #pragma unroll
@@ -1123,21 +1138,21 @@ __device__ __forceinline__ int grp_find(const GrpShared &sh, int nh, int total, 
 // covering its chunk at once (one memory round trip per chunk), then takes the K 16-base
 // windows out of registers with static indices.
 template <int K, bool REF2>
-__device__ __forceinline__ void grp_scan(const DevBatch &B, GrpShared &sh, const GrpRange &R, const GrpGlobal &gg,
-                                         int64_t i_begin, int64_t i_end, const int4 *__restrict__ rec4,
-                                         const int2 *__restrict__ rec2, int skip) {
+__device__ __forceinline__ void grp_scan(const GrpBatch &B, GrpShared &sh, const GrpRange &R, const GrpGlobal &gg,
+                                         int64_t i_begin, int64_t i_end, const int4 *__restrict__ rec4, int skip) {
   const int tid = threadIdx.x;
   for (int64_t c0 = i_begin; c0 < i_end; c0 += kGrpTile) {
     const int nh = (int)((i_end - c0) < kGrpTile ? (i_end - c0) : kGrpTile);
-    int total = grp_tile(sh, rec4, rec2, c0, nh, 16 * K);
+    int total = grp_tile(sh, rec4, c0, nh, 16 * K);
     if (skip & kSkipChunks) total = 0;
     for (int t = tid; t < total; t += kGrpThreads) {
       const int j = grp_find(sh, nh, total, t);
       const int4 r = sh.rec[j];
-      const int2 r2 = sh.rec2[j];
-      const int L = r2.x & 0xFFFFFF;
+      const uint32_t rz = (uint32_t)r.z;
+      const int L = (int)((rz >> 16) & kSegMaxLen);
       const int q0 = 16 * K * (t - sh.pre[j]);
-      const int64_t sn = i64_of(r.x, r.y) + q0, rn = i64_of(r.z, r.w) + q0;
+      const int64_t sn = (int64_t)((uint64_t)(uint32_t)r.x | ((uint64_t)(rz & 0xFF) << 32)) + q0;
+      const int64_t rn = (int64_t)((uint64_t)(uint32_t)r.y | ((uint64_t)((rz >> 8) & 0xFF) << 32)) + q0;
       const uint32_t *ps = reinterpret_cast<const uint32_t *>(B.seq) + (sn >> 3);
       const uint32_t *pr = REF2 ? B.ref2 + (rn >> 4) : reinterpret_cast<const uint32_t *>(B.ref) + (rn >> 3);
       constexpr int NR = REF2 ? K + 1 : 2 * K + 1;   // reference words covering the chunk
@@ -1153,9 +1168,9 @@ __device__ __forceinline__ void grp_scan(const DevBatch &B, GrpShared &sh, const
         for (int i = 0; i < NR; ++i) dr[i] = nib_swap(dr[i]);
       }
       const int shs = 4 * (int)(sn & 7), shr = REF2 ? 2 * (int)(rn & 15) : 4 * (int)(rn & 7);
-      const int ds_ = (r2.x >> 24) & 1;
-      const unsigned long long sk = (unsigned long long)(r2.y & 0xFFF) << 52;
-      const int pos_seg = (int)((uint32_t)r2.y >> 12);
+      const int ds_ = (int)((rz >> 30) & 1);
+      const unsigned long long sk = (unsigned long long)(r.w & 0xFFF) << 52;
+      const int pos_seg = (int)((uint32_t)r.w >> 12);
 #pragma unroll
       for (int i = 0; i < K; ++i) {
         const int qi = q0 + 16 * i;
@@ -1182,11 +1197,10 @@ __device__ __forceinline__ void grp_scan(const DevBatch &B, GrpShared &sh, const
           const int rc = (int)((rv >> (4 * k)) & 15);
           if (c == 15 || !is_acgt(rc)) continue;
           const unsigned long long key = sk | ((unsigned long long)(pos_seg + qi + k) << 4) | (unsigned long long)c;
-          grp_observe(sh, R, gg, key, sn + 16 * i + k, rc, ds_, (uint32_t)r2.x);
+          grp_observe(sh, R, gg, key, sn + 16 * i + k, rc, ds_, rz >> 31);
         }
       }
     }
-    if (R.mode == kModeGlobal) __builtin_amdgcn_s_waitcnt(0);   // region stores at L2 before the barrier
     __syncthreads();
   }
 }
@@ -1234,7 +1248,7 @@ __device__ __forceinline__ void grp_count(GrpShared &sh, int s_local, int calls,
   }
 }
 
-__device__ __forceinline__ void grp_classify(const DevBatch &B, GrpShared &sh, int n, int s_begin,
+__device__ __forceinline__ void grp_classify(const GrpBatch &B, GrpShared &sh, int n, int s_begin,
                                              const PatchSink &sink, bool count) {
   const int tid = threadIdx.x;
   if (n <= kGrpQuad) {
@@ -1281,12 +1295,13 @@ __device__ __forceinline__ void grp_classify(const DevBatch &B, GrpShared &sh, i
 // Overflow path: n observations of one key range sit in the group's global region. Aggregate
 // them in a hash table of distinct keys (workgroup-scope atomics in L2), count the TN calls
 // (minus the kept variant), and mask the observations of reads the scopes write.
-__device__ __forceinline__ void grp_global(const DevBatch &B, GrpShared &sh, const GrpGlobal &gg, int n,
+__device__ __forceinline__ void grp_global(const GrpBatch &B, GrpShared &sh, const GrpGlobal &gg, int n,
                                            int s_begin, const PatchSink &sink) {
   const int tid = threadIdx.x;
   const int tsize = max(2 * n, 64);
-  unsigned long long *tk = gg.tkey + 2 * gg.off;
-  unsigned int *tf = gg.tflag + 2 * gg.off;
+  unsigned long long *tk = gg.aux->tkey + 2 * gg.off;
+  unsigned int *tf = gg.aux->tflag + 2 * gg.off;
+  const unsigned long long *okey = gg.aux->okey + gg.off, *opay = gg.aux->opay + gg.off;
   for (int i = tid; i < tsize; i += kGrpThreads) {
     tk[i] = kEmpty;
     tf[i] = 0;
@@ -1294,8 +1309,8 @@ __device__ __forceinline__ void grp_global(const DevBatch &B, GrpShared &sh, con
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
   for (int i = tid; i < n; i += kGrpThreads) {
-    const unsigned long long key = ld_l2(gg.okey + gg.off + i);
-    const int ds = (int)((ld_l2(gg.opay + gg.off + i) >> 52) & 1);
+    const unsigned long long key = ld_l2(okey + i);
+    const int ds = (int)((ld_l2(opay + i) >> 52) & 1);
     unsigned slot = gtab_home(key, tsize);
     for (int probe = 0; probe < tsize; ++probe) {
       unsigned long long expected = kEmpty;
@@ -1320,9 +1335,9 @@ __device__ __forceinline__ void grp_global(const DevBatch &B, GrpShared &sh, con
   }
   // masks: every observation of a read the scope writes whose key is TN
   for (int i = tid; i < n; i += kGrpThreads) {
-    const unsigned long long pay = ld_l2(gg.opay + gg.off + i);
+    const unsigned long long pay = ld_l2(opay + i);
     if (!((pay >> 53) & 1)) continue;
-    const unsigned long long key = ld_l2(gg.okey + gg.off + i);
+    const unsigned long long key = ld_l2(okey + i);
     unsigned slot = gtab_home(key, tsize);
     unsigned int f = 0;
     for (int probe = 0; probe < tsize; ++probe) {
@@ -1344,7 +1359,7 @@ __device__ __forceinline__ void grp_global(const DevBatch &B, GrpShared &sh, con
 
 // Fused: apply the sorted in-partition list (nibble << 4 | from ^ to) with one plain byte store
 // per masked byte, seq[b] ^ mask — the partition copy of that byte has drained before.
-__device__ __forceinline__ void grp_patch_bytes(const DevBatch &B, GrpShared &sh, int np, uint8_t *out) {
+__device__ __forceinline__ void grp_patch_bytes(const GrpBatch &B, GrpShared &sh, int np, uint8_t *out) {
   for (int i = threadIdx.x; i < np; i += kGrpThreads) {
     const unsigned long long e = sh.patch[i];
     const int64_t byte = (int64_t)(e >> 5);
@@ -1370,13 +1385,9 @@ __device__ __forceinline__ void grp_release() {
 // {global region offset lo, hi, capacity, 0}; segments [seg_begin, seg_mid) have an all-ACGT
 // reference range (2-bit reference).
 template <int U, bool FUSED>
-__global__ void __launch_bounds__(kGrpThreads, (U <= 2 ? 6 : U == 4 ? 5 : 4)) k_group(const DevBatch B, const int4 *__restrict__ groups,
-                                                       const int4 *__restrict__ rec4, const int2 *__restrict__ rec2,
-                                                       uint8_t *__restrict__ out, int32_t *scope_calls,
-                                                       int32_t *scope_bases, int32_t *part,
-                                                       unsigned long long *far, int *far_count, int64_t far_cap,
-                                                       unsigned long long *gokey, unsigned long long *gopay,
-                                                       unsigned long long *gtkey, unsigned int *gtflag,
+__global__ void __launch_bounds__(kGrpThreads, (U == 1 ? 6 : U == 2 ? GANON_K2_BLOCKS : U == 4 ? 5 : 4)) k_group(const GrpBatch B, const int4 *__restrict__ groups,
+                                                       const int4 *__restrict__ rec4,
+                                                       uint8_t *__restrict__ out, const GrpAux *__restrict__ aux,
                                                        int skip, int nt_copy) {
   __shared__ GrpShared sh;
   const int tid = threadIdx.x;
@@ -1384,10 +1395,10 @@ __global__ void __launch_bounds__(kGrpThreads, (U <= 2 ? 6 : U == 4 ? 5 : 4)) k_
   const int4 g1 = groups[4 * blockIdx.x + 1];
   const int4 g2 = groups[4 * blockIdx.x + 2];
   const int4 g3 = groups[4 * blockIdx.x + 3];
-  const GrpGlobal gg{gokey, gopay, gtkey, gtflag, i64_of(g3.x, g3.y), g3.z};
+  const GrpGlobal gg{aux, i64_of(g3.x, g3.y), g3.z};
   const int s_begin = g0.x, s_end = g0.y;
   const int64_t i_begin = i64_of(g0.z, g0.w), i_end = i64_of(g1.x, g1.y), i_mid = i64_of(g1.z, g1.w);
-  PatchSink sink{out, i64_of(g2.x, g2.y), i64_of(g2.z, g2.w), far, far_count, far_cap, FUSED, FUSED, false};
+  PatchSink sink{out, i64_of(g2.x, g2.y), i64_of(g2.z, g2.w), aux, FUSED, FUSED, false};
   if (FUSED && !(skip & kSkipCopy)) {
     // the partition: whole 16-byte windows (the buffers are padded past seq_bytes); the stores
     // drain while the scan runs (s_waitcnt before the mask stores)
@@ -1431,12 +1442,12 @@ __global__ void __launch_bounds__(kGrpThreads, (U <= 2 ? 6 : U == 4 ? 5 : 4)) k_
       // workgroup's partial totals (k_finish sums them)
       for (int i = tid; i < s_end - s_begin; i += kGrpThreads) {
         if (B.span_len[s_begin + i] > kGrpMaxSpan) continue;
-        scope_calls[s_begin + i] = sh.cnt_calls[i];
-        scope_bases[s_begin + i] = sh.cnt_bases[i];
+        aux->scope_calls[s_begin + i] = sh.cnt_calls[i];
+        aux->scope_bases[s_begin + i] = sh.cnt_bases[i];
       }
       if (tid == 0) {
-        part[2 * blockIdx.x] = sh.blk_calls;
-        part[2 * blockIdx.x + 1] = sh.blk_bases;
+        aux->part[2 * blockIdx.x] = sh.blk_calls;
+        aux->part[2 * blockIdx.x + 1] = sh.blk_bases;
       }
       break;
     }
@@ -1450,49 +1461,56 @@ __global__ void __launch_bounds__(kGrpThreads, (U <= 2 ? 6 : U == 4 ? 5 : 4)) k_
     }
     __syncthreads();
     if (B.ref2) {
-      grp_scan<U, true>(B, sh, R, gg, i_begin, i_mid, rec4, rec2, skip);
-      grp_scan<U, false>(B, sh, R, gg, i_mid, i_end, rec4, rec2, skip);
+      grp_scan<U, true>(B, sh, R, gg, i_begin, i_mid, rec4, skip);
+      grp_scan<U, false>(B, sh, R, gg, i_mid, i_end, rec4, skip);
     } else {
-      grp_scan<U, false>(B, sh, R, gg, i_begin, i_end, rec4, rec2, skip);
+      grp_scan<U, false>(B, sh, R, gg, i_begin, i_end, rec4, skip);
     }
     // (grp_scan ends on a barrier)
     if (skip & kSkipClassify) continue;
-    if (R.mode == kModeGlobal) {
-      const int n = sh.n_obs;
+    const int n = sh.n_obs;
+    if (n > kGrpObs) {
       if (n <= gg.cap) {
+        // the list joins the region's tail: n observations contiguous in the region
+        for (int i = tid; i < kGrpObs; i += kGrpThreads) {
+          aux->okey[gg.off + (n - kGrpObs) + i] = sh.key[i];
+          aux->opay[gg.off + (n - kGrpObs) + i] = sh.pay[i];
+        }
+        if (sink.lds) {
+          // masks from here on are atomic XORs, after a release of the partition copy
+          grp_release();
+          sink.lds = false;
+        }
+        __builtin_amdgcn_s_waitcnt(0);   // region stores at L2 before the barrier
+        __syncthreads();
         grp_global(B, sh, gg, n, s_begin, sink);
         continue;
       }
-      // the region overflowed too: halves of the observed key range, each from the list again
+      // the region overflowed too (more than ~2 % of the bases mismatch): split [R.lo, R.hi)
+      // at the middle of the stored keys' range — both halves keep stored keys, and a single key
+      // never fills a region (capacity > 3 x the group's reads)
+      __builtin_amdgcn_s_waitcnt(0);
+      __syncthreads();
+      for (int i = tid; i < gg.cap; i += kGrpThreads) {
+        const unsigned long long k = i < kGrpObs ? sh.key[i] : ld_l2(aux->okey + gg.off + (i - kGrpObs));
+        atomicMin(&sh.kmin, k);
+        atomicMax(&sh.kmax, k);
+      }
+      __syncthreads();
       if (tid == 0) {
-        const unsigned long long a = sh.kmin, b = sh.kmax, mid = a + (b - a) / 2;
+        const unsigned long long a = sh.kmin, b = sh.kmax, mid = a + (b - a) / 2 + 1;
         int t = sh.top;
         if (a < b && t + 2 < kGrpStack) {
           ++t;
-          sh.stk_lo[t] = mid + 1;
-          sh.stk_hi[t] = b + 1;
+          sh.stk_lo[t] = mid;
+          sh.stk_hi[t] = R.hi;
           sh.stk_mode[t] = kModeCollect;
           ++t;
-          sh.stk_lo[t] = a;
-          sh.stk_hi[t] = mid + 1;
+          sh.stk_lo[t] = R.lo;
+          sh.stk_hi[t] = mid;
           sh.stk_mode[t] = kModeCollect;
         }
         sh.top = t;
-      }
-      continue;
-    }
-    const int n = sh.n_obs;
-    if (n > kGrpObs) {
-      if (sink.lds) {
-        // masks from here on are atomic XORs, after a release of the partition copy
-        grp_release();
-        sink.lds = false;
-      }
-      if (tid == 0) {   // the same key range again, into the global region
-        const int t = ++sh.top;
-        sh.stk_lo[t] = R.lo;
-        sh.stk_hi[t] = R.hi;
-        sh.stk_mode[t] = kModeGlobal;
       }
       continue;
     }
@@ -1770,8 +1788,7 @@ struct ganon_dbatch {
   int4 *inc_rec = nullptr;      // per incidence, scope-major: {start|read, len|flags, seq_off lo, hi}
   int4 *srec[2] = {nullptr, nullptr};   // per small scope of each class: 3 x int4 (k_scope_v3)
   int4 *groups = nullptr;               // k_group: 2 x int4 per group
-  int4 *seg4 = nullptr;                 // k_group: per segment {query nibble, reference nibble}
-  int2 *seg2 = nullptr;                 // k_group: per segment {length | flags, scope_local}
+  int4 *seg4 = nullptr;                 // k_group: segment records (16 bytes, layout at kSegMine)
   int32_t n_groups = 0;
   int64_t n_seg = 0;
   unsigned long long *acc = nullptr;    // k_finish: calls, bases, workgroup ticket
@@ -1780,6 +1797,7 @@ struct ganon_dbatch {
   int64_t far_cap = 0;
   int32_t *grp_part = nullptr;          // k_group: (calls, bases) per workgroup
   int32_t *large_ids = nullptr;         // scopes of the tile path under the group variants (huge)
+  GrpAux *aux = nullptr;                // k_group's rarely used pointers (device copy)
   unsigned long long *gokey = nullptr, *gopay = nullptr, *gtkey = nullptr;   // group overflow regions
   unsigned int *gtflag = nullptr;
   Tile *tiles_h = nullptr;              // tiles / written reads of huge scopes (group variants)
@@ -2220,10 +2238,10 @@ GANON_API int ganon_batch_upload(ganon_ctx *ctx, const ganon_batch *b, ganon_dba
     // into groups of consecutive scopes; groups launch in the order of their written reads in
     // the sequence buffer, each owning the 128-byte-aligned partition of out from its first
     // written read to the next group's (fused variant)
+    if (2 * b->seq_bytes >= (int64_t(1) << 40) || 2 * b->ref_bytes >= (int64_t(1) << 40))
+      return bail(fail(ctx, GANON_E_ARG, "sequence or reference over 2^40 bases"));
     std::vector<int4> s4;
-    std::vector<int2> s2;
     s4.reserve((size_t)b->n_incid);
-    s2.reserve((size_t)b->n_incid);
     auto lo32 = [](int64_t v) { return (int)(uint32_t)(uint64_t)v; };
     auto hi32 = [](int64_t v) { return (int)(uint32_t)((uint64_t)v >> 32); };
     struct G {
@@ -2260,21 +2278,16 @@ GANON_API int ganon_batch_upload(ganon_ctx *ctx, const ganon_batch *b, ganon_dba
       return true;
     };
     std::vector<int4> c4, d4;   // the open group's segments: clean, dirty reference
-    std::vector<int2> c2, d2;
     auto close_group = [&](int32_t s_end) {
       if (g_s0 < 0) return;
       int64_t bases = 0;
-      for (const int2 &x : c2) bases += x.x & 0xFFFFFF;
-      for (const int2 &x : d2) bases += x.x & 0xFFFFFF;
+      for (const int4 &x : c4) bases += ((uint32_t)x.z >> 16) & kSegMaxLen;
+      for (const int4 &x : d4) bases += ((uint32_t)x.z >> 16) & kSegMaxLen;
       s4.insert(s4.end(), c4.begin(), c4.end());
-      s2.insert(s2.end(), c2.begin(), c2.end());
       const int64_t mid = (int64_t)s4.size();
       s4.insert(s4.end(), d4.begin(), d4.end());
-      s2.insert(s2.end(), d2.begin(), d2.end());
       c4.clear();
-      c2.clear();
       d4.clear();
-      d2.clear();
       gs.push_back(G{g_s0, s_end, g_i0, (int64_t)s4.size(), g_first, mid, bases});
       g_s0 = -1;
       g_first = INT64_MAX;
@@ -2288,7 +2301,7 @@ GANON_API int ganon_batch_upload(ganon_ctx *ctx, const ganon_batch *b, ganon_dba
         const int64_t len = w >> 4;
         if (op == 0 || op == 7 || op == 8) {
           const int64_t n = std::min(len, L - q);
-          if (n > 0) emit(q, p, n);
+          for (int64_t o = 0; o < n; o += kSegMaxLen) emit(q + o, p + o, std::min<int64_t>(kSegMaxLen, n - o));
           q += len;
           p += len;
         } else if (op == 1 || op == 4) {
@@ -2313,7 +2326,7 @@ GANON_API int ganon_batch_upload(ganon_ctx *ctx, const ganon_batch *b, ganon_dba
       for (int64_t i = i0; i < i1; ++i) {
         const int32_t r = b->incid_read[i];
         if (b->read_len[r] >= (1 << 24)) return bail(fail(ctx, GANON_E_ARG, "read %d longer than 16 Mb", r));
-        uint32_t fl = (uint32_t)b->dataset[r] << 24;
+        uint32_t fl = (uint32_t)b->dataset[r] << 30;
         if (b->write_scope[r] == s) {
           fl |= kSegMine;
           g_first = std::min(g_first, b->seq_off[r]);
@@ -2321,10 +2334,13 @@ GANON_API int ganon_batch_upload(ganon_ctx *ctx, const ganon_batch *b, ganon_dba
         const int64_t qnib = 2 * b->seq_off[r];
         segments_of(r, [&](int64_t q, int64_t p, int64_t n) {
           const bool clean = ref_clean(ref0 + p, n);
-          (clean ? c4 : d4).push_back(make_int4(lo32(qnib + q), hi32(qnib + q), lo32(ref0 + p), hi32(ref0 + p)));
-          // small scope: span <= kSmallCap1 < 2^20 positions
+          const uint64_t sq = (uint64_t)(qnib + q), rf = (uint64_t)(ref0 + p);
+          const uint32_t z = (uint32_t)((sq >> 32) & 0xFF) | ((uint32_t)((rf >> 32) & 0xFF) << 8) |
+                             ((uint32_t)n << 16) | fl;
+          // scope span <= kGrpMaxSpan = 2^20 positions
           const uint32_t pos_off = (uint32_t)(p - b->scope_span_start[s]);
-          (clean ? c2 : d2).push_back(make_int2((int)((uint32_t)n | fl), (int)((uint32_t)(s - g_s0) | (pos_off << 12))));
+          (clean ? c4 : d4).push_back(make_int4((int)(uint32_t)sq, (int)(uint32_t)rf, (int)z,
+                                                (int)((uint32_t)(s - g_s0) | (pos_off << 12))));
         });
       }
     }
@@ -2354,13 +2370,13 @@ GANON_API int ganon_batch_upload(ganon_ctx *ctx, const ganon_batch *b, ganon_dba
       const int64_t in = std::max<int64_t>(0, std::min(r1, part[k + 1]) - std::max(r0, part[k]));
       far_cap += 2 * ((r1 - r0) - in);
     }
-    // overflow regions: (bases / 48 + 256) observations per group, i.e. up to ~2 % of its
+    // overflow regions: (bases / 48 + kGrpObs) observations per group, i.e. up to ~2 % of its
     // aligned bases mismatching (more: key-range halving)
     std::vector<int4> grp(4 * (size_t)ng);
     int64_t region = 0;
     for (int32_t k = 0; k < ng; ++k) {
       const G &g = gs[order[k]];
-      const int64_t cap = std::min<int64_t>(g.bases / 48 + 256, INT32_MAX / 2);
+      const int64_t cap = std::min<int64_t>(g.bases / 48 + kGrpObs, INT32_MAX / 2);
       grp[4 * k] = make_int4(g.s0, g.s1, lo32(g.i0), hi32(g.i0));
       grp[4 * k + 1] = make_int4(lo32(g.i1), hi32(g.i1), lo32(g.mid), hi32(g.mid));
       grp[4 * k + 2] = make_int4(lo32(part[k]), hi32(part[k]), lo32(part[k + 1]), hi32(part[k + 1]));
@@ -2373,7 +2389,6 @@ GANON_API int ganon_batch_upload(ganon_ctx *ctx, const ganon_batch *b, ganon_dba
     if ((rc = dev_alloc(ctx, db, &db->gtflag, 2 * (size_t)region + 64))) return bail(rc);
     if ((rc = dev_copy(ctx, db, &db->groups, grp.data(), grp.size()))) return bail(rc);
     if ((rc = dev_copy(ctx, db, &db->seg4, s4.data(), s4.size()))) return bail(rc);
-    if ((rc = dev_copy(ctx, db, &db->seg2, s2.data(), s2.size()))) return bail(rc);
     db->n_groups = ng;
     if ((rc = dev_alloc(ctx, db, &db->grp_part, 2 * (size_t)ng))) return bail(rc);
     db->n_seg = (int64_t)s4.size();
@@ -2397,6 +2412,11 @@ GANON_API int ganon_batch_upload(ganon_ctx *ctx, const ganon_batch *b, ganon_dba
   if ((rc = dev_alloc(ctx, db, &db->totals, GANON_N_TOTALS))) return bail(rc);
   if ((rc = dev_alloc(ctx, db, &db->counters, 4))) return bail(rc);
   if ((rc = dev_alloc(ctx, db, &db->acc, 3))) return bail(rc);
+  {
+    const GrpAux a{db->scope_calls, db->scope_bases, db->grp_part, db->far, db->counters + 2, db->far_cap,
+                   db->gokey, db->gopay, db->gtkey, db->gtflag};
+    if ((rc = dev_copy(ctx, db, &db->aux, &a, 1))) return bail(rc);
+  }
   // k_finish keeps these zero between runs
   if (hipMemsetAsync(db->counters, 0, 4 * sizeof(int32_t), ctx->stream) != hipSuccess ||
       hipMemsetAsync(db->acc, 0, 3 * sizeof(unsigned long long), ctx->stream) != hipSuccess)
@@ -2470,10 +2490,9 @@ GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
                                                                                      : k_group<1, true>)
                    : (u == 2 ? k_group<2, false> : u == 4 ? k_group<4, false> : u == 8 ? k_group<8, false>
                                                                                        : k_group<1, false>);
-    kern<<<db->n_groups, kGrpThreads, 0, st>>>(B, db->groups, db->seg4, db->seg2, db->out, db->scope_calls,
-                                               db->scope_bases, db->grp_part, db->far, db->counters + 2,
-                                               db->far_cap, db->gokey, db->gopay, db->gtkey, db->gtflag,
-                                               ctx->group_skip, ctx->nt_copy);
+    const GrpBatch GB{B.seq, B.ref, B.keep_code, B.ref2, B.keep_pos, B.span_start, B.span_len};
+    kern<<<db->n_groups, kGrpThreads, 0, st>>>(GB, db->groups, db->seg4, db->out, db->aux, ctx->group_skip,
+                                               ctx->nt_copy);
     if ((rc = check_launch(ctx, "k_group"))) return rc;
   }
   const int caps[2] = {kSmallCap0, kSmallCap1};

@@ -14,7 +14,8 @@ from typing import Optional
 import numpy as np
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-HIP_LIB_PATH = os.path.join(_PKG, "libganon_hip.so")
+# GANON_HIP_LIB: another in-tree build of the same sources (compile-time tuning A/B only)
+HIP_LIB_PATH = os.environ.get("GANON_HIP_LIB") or os.path.join(_PKG, "libganon_hip.so")
 HOST_LIB_PATH = os.path.join(_PKG, "libganon_host.so")
 
 GANON_N_TOTALS = 8

@@ -951,7 +951,7 @@ constexpr int kGrpTarget = 256;      // segments per group (a larger scope forms
 constexpr int kGrpObs = 512;         // observations per LDS list
 constexpr int kGrpMaxScopes = 256;   // scopes per group (12-bit local index field)
 constexpr int kGrpStack = 80;        // key ranges pending (bisection depth <= 64)
-constexpr int kGrpPatch = 256;       // in-partition masks of a fused workgroup, sorted in LDS
+constexpr int kGrpPatch = 512;       // in-partition masks of one list pass (<= its observations)
 constexpr int kGrpMap = 4096;        // chunk -> segment map entries (larger tiles binary-search)
 constexpr int kGrpQuad = 256;        // lists up to this size are matched without sorting
 constexpr int kGrpMaxSpan = 1 << 20; // widest scope of the group kernels (20-bit position field)
@@ -1015,8 +1015,7 @@ struct PatchSink {
   int64_t p0, p1;                   // fused: this workgroup's partition of out (bytes)
   const GrpAux *aux;                // far-mask list
   bool fused;
-  bool lds;                         // fused, in-partition masks into the LDS list
-  bool in_only;                     // fused re-run after an LDS list overflow: in-partition only
+  bool lds;                         // fused: in-partition masks into the LDS list
 };
 
 __device__ __forceinline__ void sink_patch(GrpShared &sh, const PatchSink &k, int64_t nib, int c, int rc) {
@@ -1024,7 +1023,6 @@ __device__ __forceinline__ void sink_patch(GrpShared &sh, const PatchSink &k, in
   if (k.fused) {
     const int64_t byte = nib >> 1;
     if (byte < k.p0 || byte >= k.p1) {
-      if (k.in_only) return;
       const int i = atomicAdd(k.aux->far_count, 1);
       if (i < k.aux->far_cap) k.aux->far[i] = e;
       return;
@@ -1301,7 +1299,7 @@ __device__ __forceinline__ void grp_global(const GrpBatch &B, GrpShared &sh, con
   const int tsize = max(2 * n, 64);
   unsigned long long *tk = gg.aux->tkey + 2 * gg.off;
   unsigned int *tf = gg.aux->tflag + 2 * gg.off;
-  const unsigned long long *okey = gg.aux->okey + gg.off, *opay = gg.aux->opay + gg.off;
+  unsigned long long *okey = gg.aux->okey + gg.off, *opay = gg.aux->opay + gg.off;
   for (int i = tid; i < tsize; i += kGrpThreads) {
     tk[i] = kEmpty;
     tf[i] = 0;
@@ -1352,13 +1350,59 @@ __device__ __forceinline__ void grp_global(const GrpBatch &B, GrpShared &sh, con
     if (f != 3) continue;
     const int c = (int)(key & 15);
     if (grp_kept(B, s_begin + (int)(key >> 52), (int64_t)((key >> 4) & kNibMask), c)) continue;
-    sink_patch(sh, sink, (int64_t)(pay & kNibMask), c, (int)((pay >> 48) & 15));
     grp_count(sh, (int)(key >> 52), 0, 1);
+    const int64_t nib = (int64_t)(pay & kNibMask);
+    const int rc = (int)((pay >> 48) & 15);
+    if (!sink.fused || (nib >> 1) < sink.p0 || (nib >> 1) >= sink.p1) {
+      sink_patch(sh, PatchSink{sink.out, sink.p0, sink.p1, sink.aux, sink.fused, false}, nib, c, rc);
+      continue;
+    }
+    okey[i] = ((unsigned long long)nib << 4) | (unsigned long long)(c ^ rc);   // in-partition mask
+    opay[i] = pay | (1ull << 54);
   }
+  if (!sink.fused) return;
+  // fused: merge the in-partition masks per byte (the table area again, keyed by byte) and
+  // apply each byte once, out[b] ^= mask — only this workgroup writes its partition
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  for (int i = tid; i < tsize; i += kGrpThreads) {
+    tk[i] = kEmpty;
+    tf[i] = 0;
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  for (int i = tid; i < n; i += kGrpThreads) {
+    const unsigned long long e = ld_l2(okey + i);
+    const unsigned long long pay = ld_l2(opay + i);
+    if (!((pay >> 54) & 1)) continue;                       // no in-partition mask
+    const unsigned long long byte = e >> 5;
+    unsigned slot = gtab_home(byte, tsize);
+    for (int probe = 0; probe < tsize; ++probe) {
+      unsigned long long expected = kEmpty;
+      __hip_atomic_compare_exchange_strong(tk + slot, &expected, byte, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (expected == kEmpty || expected == byte) {
+        __hip_atomic_fetch_xor(tf + slot, (unsigned)(e & 15) << (((e >> 4) & 1) ? 0 : 4), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+        break;
+      }
+      if (++slot == (unsigned)tsize) slot = 0;
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  for (int i = tid; i < tsize; i += kGrpThreads) {
+    const unsigned long long byte = ld_l2(tk + i);
+    if (byte == kEmpty) continue;
+    const unsigned w = ld_l2(reinterpret_cast<const unsigned int *>(sink.out) + (byte >> 2));
+    sink.out[byte] = (uint8_t)((w >> (8 * (byte & 3))) ^ ld_l2(tf + i));
+  }
+  __builtin_amdgcn_s_waitcnt(0);
 }
 
 // Fused: apply the sorted in-partition list (nibble << 4 | from ^ to) with one plain byte store
-// per masked byte, seq[b] ^ mask — the partition copy of that byte has drained before.
+// per masked byte, out[b] ^ mask — the partition copy and earlier masks of that byte were
+// stored by this workgroup and have drained (read back from L2).
 __device__ __forceinline__ void grp_patch_bytes(const GrpBatch &B, GrpShared &sh, int np, uint8_t *out) {
   for (int i = threadIdx.x; i < np; i += kGrpThreads) {
     const unsigned long long e = sh.patch[i];
@@ -1369,15 +1413,9 @@ __device__ __forceinline__ void grp_patch_bytes(const GrpBatch &B, GrpShared &sh
       const unsigned long long f = sh.patch[k];
       x ^= (uint32_t)(f & 15) << (((f >> 4) & 1) ? 0 : 4);
     }
-    out[byte] = (uint8_t)(B.seq[byte] ^ x);
+    const unsigned w = ld_l2(reinterpret_cast<const unsigned int *>(out) + (byte >> 2));
+    out[byte] = (uint8_t)((w >> (8 * (byte & 3))) ^ x);
   }
-}
-
-// Make this workgroup's stores visible at the memory side before device atomics (which execute
-// beyond the XCD's L2) patch the same bytes.
-__device__ __forceinline__ void grp_release() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  __syncthreads();
 }
 
 // groups: 4 x int4 per group, in launch order: {s_begin, s_end, seg_begin lo, hi},
@@ -1398,7 +1436,7 @@ __global__ void __launch_bounds__(kGrpThreads, (U == 1 ? 6 : U == 2 ? GANON_K2_B
   const GrpGlobal gg{aux, i64_of(g3.x, g3.y), g3.z};
   const int s_begin = g0.x, s_end = g0.y;
   const int64_t i_begin = i64_of(g0.z, g0.w), i_end = i64_of(g1.x, g1.y), i_mid = i64_of(g1.z, g1.w);
-  PatchSink sink{out, i64_of(g2.x, g2.y), i64_of(g2.z, g2.w), aux, FUSED, FUSED, false};
+  const PatchSink sink{out, i64_of(g2.x, g2.y), i64_of(g2.z, g2.w), aux, FUSED, FUSED};
   if (FUSED && !(skip & kSkipCopy)) {
     // the partition: whole 16-byte windows (the buffers are padded past seq_bytes); the stores
     // drain while the scan runs (s_waitcnt before the mask stores)
@@ -1476,11 +1514,6 @@ __global__ void __launch_bounds__(kGrpThreads, (U == 1 ? 6 : U == 2 ? GANON_K2_B
           aux->okey[gg.off + (n - kGrpObs) + i] = sh.key[i];
           aux->opay[gg.off + (n - kGrpObs) + i] = sh.pay[i];
         }
-        if (sink.lds) {
-          // masks from here on are atomic XORs, after a release of the partition copy
-          grp_release();
-          sink.lds = false;
-        }
         __builtin_amdgcn_s_waitcnt(0);   // region stores at L2 before the barrier
         __syncthreads();
         grp_global(B, sh, gg, n, s_begin, sink);
@@ -1516,23 +1549,17 @@ __global__ void __launch_bounds__(kGrpThreads, (U == 1 ? 6 : U == 2 ? GANON_K2_B
     }
     grp_classify(B, sh, n, s_begin, sink, true);
     if (!sink.lds) continue;
-    // fused, whole group in one list: in-partition masks as byte stores, after every wave's
-    // partition stores have drained
+    // fused: in-partition masks (at most one per observation of this list) as byte stores, after
+    // every wave's earlier stores have drained
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     const int np = sh.n_patch;
-    if (np <= kGrpPatch) {
-      if (np) {
-        lds_bitonic(sh.patch, nullptr, np);
-        grp_patch_bytes(B, sh, np, out);
-      }
-    } else {
-      grp_release();
-      PatchSink again = sink;
-      again.lds = false;
-      again.in_only = true;
-      grp_classify(B, sh, n, s_begin, again, false);
+    if (np) {
+      lds_bitonic(sh.patch, nullptr, np);
+      grp_patch_bytes(B, sh, np, out);
+      __builtin_amdgcn_s_waitcnt(0);
     }
+    if (tid == 0) sh.n_patch = 0;
   }
 }
 

@@ -19,17 +19,21 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--reads", type=int, default=10_000_000)
-    ap.add_argument("--genome", type=int, default=3_000_000_000)
+    ap.add_argument("--config", default="c2", help="bench.py workload (c2, c3, c5)")
+    ap.add_argument("--reads", type=int, default=None)
+    ap.add_argument("--genome", type=int, default=None)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--configs", default="0:1:0,0:1:1,0:1:2,0:2:0,5:1:0,5:2:0",
                     help="comma list of variant:unroll:skip[:group_target[:nt_copy[:ref2]]]")
     args = ap.parse_args()
     from genomeanonymizer_amd import native
-    from genomeanonymizer_amd.synth.batch import config2_batch
-    arr, info = config2_batch(n_reads=args.reads, genome=args.genome,
-                              n_windows=args.reads // 10, n_germline=args.reads // 10, seed=2)
+    import bench
+    args.windows = args.germline = None
+    for k, v in bench.CONFIGS[args.config]["defaults"].items():
+        if getattr(args, k) is None:
+            setattr(args, k, v)
+    arr, info = bench.make_batch(args, 0)
     m = native.HipMasker(0)
     cfgs = []
     for c in args.configs.split(","):

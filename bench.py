@@ -153,8 +153,8 @@ def make_batch(args, rank: int):
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", choices=sorted(CONFIGS), default="c2",
                     help="c2 = BASELINE configs[1] (the metric's workload); c3 / c5 = SURVEY §8(d) density and "
                          "long-read shapes, for their own lines")

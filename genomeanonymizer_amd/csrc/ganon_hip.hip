@@ -2197,7 +2197,8 @@ GANON_API int ganon_batch_upload(ganon_ctx *ctx, const ganon_batch *b, ganon_dba
   db->n_tiles = (int32_t)tiles.size();
   if ((rc = dev_copy(ctx, db, &db->large_incid, large_incid.data(), large_incid.size()))) return bail(rc);
   if ((rc = dev_copy(ctx, db, &db->tab_off, tab_off.data(), tab_off.size()))) return bail(rc);
-  if ((rc = dev_alloc(ctx, db, &db->tn_tab, (size_t)tn_entries))) return bail(rc);
+  // the tile path's TN table (2 bytes per position of every wide scope) is allocated on the
+  // first run that uses it: under the group variants only scopes over kGrpMaxSpan tile
   db->tn_entries = tn_entries;
   if ((rc = dev_copy(ctx, db, &db->large_written, large_written.data(), large_written.size()))) return bail(rc);
   db->n_large_written = (int32_t)large_written.size();
@@ -2553,6 +2554,7 @@ GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
       if ((rc = check_launch(ctx, "k_scope_wave"))) return rc;
     }
   }
+  if (n_tiles && !db->tn_tab && (rc = dev_alloc(ctx, db, &db->tn_tab, (size_t)db->tn_entries))) return rc;
   if (n_tiles) {
     KernelScope ks(ctx, "k_tile_large<1>");
     k_tile_large<1><<<n_tiles, kBlock, tile_lds_bytes(1), st>>>(

@@ -7,9 +7,9 @@ mkdir -p gpurun_out
 rocm-smi --showproductname > gpurun_out/gpu_info.txt 2>&1 || true
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 \
  && timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 \
- && timeout -k 10 600 python bench.py --steps ${STEPS:-10} --warmup 3 ${BENCH_ARGS:-} > gpurun_out/bench.json 2> gpurun_out/bench.err
+ && timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.json 2> gpurun_out/bench.err
 rc=$?
 echo "exit=$rc"
-tail -3 gpurun_out/smoke.log gpurun_out/pytest_gpu.log 2>/dev/null
+tail -n 3 gpurun_out/smoke.log gpurun_out/pytest_gpu.log 2>/dev/null
 cat gpurun_out/bench.json 2>/dev/null | head -c 3000
 exit $rc

@@ -150,6 +150,77 @@ def make_batch(args, rank: int):
                          n_germline=args.germline, seed=seed)
 
 
+def fastq_bench(masker, db, arr, args, torch, rank: int) -> dict:
+    """the FASTQ records of every read of the batch, formatted on the
+    device straight from the masked output (ganon_fastq_*, no copy of the bases). Reported
+    beside the masking line: formatter ms per run, its roofline, mask + format per step, and
+    the host formatter (libganon_host.so, one thread) on a bounded sample."""
+    from genomeanonymizer_amd import native
+    from genomeanonymizer_amd.synth.fastq import algorithmic_bytes as fq_bytes, fastq_records
+    # c2 reads are ACGT only: every read may be reverse (a bad one would fail the download)
+    recs = fastq_records(arr, seed=11 + rank, reverse_frac=0.5, name_len=(30, 45), check_bad=False)
+    f = masker.fastq_upload(recs, seq_batch=db)
+    for _ in range(args.warmup):
+        f.run()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(args.steps):
+        f.run()
+    torch.cuda.synchronize()
+    fmt_ms = (time.perf_counter() - t) / args.steps * 1e3
+    t = time.perf_counter()
+    for _ in range(args.steps):
+        db.run()
+        f.run()
+    torch.cuda.synchronize()
+    both_ms = (time.perf_counter() - t) / args.steps * 1e3
+    masker.set_profiling(True)
+    kt: dict = {}
+    for _ in range(args.steps):
+        f.run()
+        f.sync()
+        for name, launches, ms in f.kernel_times():
+            k = kt.setdefault(name, [0, 0.0])
+            k[0] += launches
+            k[1] += ms
+    masker.set_profiling(False)
+    head = f.download()[:64]   # also checks the error slot (no bad record)
+    f.free()
+    n = len(recs["seq_len"])
+    alg = fq_bytes(recs)
+    fmt_k = kt.get("k_fq_format", [1, float("nan")])
+    k_ms = fmt_k[1] / fmt_k[0]
+    # bytes the format kernel alone moves per launch: all but the length scan's inputs/outputs
+    k_alg = alg - 4 * n
+    # host formatter, one thread, bounded sample
+    m = min(n, 400_000)
+    sample = {k: (v[:m] if isinstance(v, np.ndarray) and len(v) == n else v) for k, v in recs.items()}
+    sample["seq_bufs"] = [arr["seq_nt16"]]
+    t = time.perf_counter()
+    reps = 0
+    while True:
+        native.host_format_fastq(sample)
+        reps += 1
+        if time.perf_counter() - t > 3.0:
+            break
+    host_rps = m * reps / (time.perf_counter() - t)
+    return {
+        "records": n, "bytes_out": native.fastq_bytes(recs), "ms_per_run": round(fmt_ms, 4),
+        "records_per_s": round(n / (fmt_ms * 1e-3), 1), "mask_plus_format_ms_per_step": round(both_ms, 4),
+        "mask_plus_format_reads_per_s": round(n / (both_ms * 1e-3), 1),
+        "kernels": {k: {"avg_ms": round(v[1] / v[0], 5), "launches": v[0] // args.steps} for k, v in kt.items()},
+        "algorithmic_bytes_per_run": alg,
+        "roofline": {"bound": "hbm", "kernel": "k_fq_format", "achieved": round(k_alg / (k_ms * 1e-3) / 1e9, 1),
+                     "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": round(k_alg / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                     "algorithmic_bytes_per_launch": k_alg, "avg_launch_ms": round(k_ms, 5)},
+        "cpu_host_formatter": {"value": round(host_rps, 1), "unit": "records/s", "cores": 1,
+                               "kind": "host C++ (libganon_host.so ganon_fastq_format)",
+                               "sample": f"first {m} records, {reps} passes"},
+        "head": head.decode(errors="replace"),
+    }
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -168,6 +239,7 @@ def main() -> None:
                          "4 group, 5 group fused, 6 persistent")
     ap.add_argument("--unroll", type=int, default=2, help="group kernel chunk width in 16-base blocks (1/2/4/8)")
     ap.add_argument("--ab", action="store_true", help="also time every small-scope variant, interleaved")
+    ap.add_argument("--no-fastq", action="store_true", help="skip the FASTQ formatter measurement")
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_r01.json"),
                     help="PMC summary (tools/pmc_summary.py) for the traffic field, if present")
     args = ap.parse_args()
@@ -255,6 +327,7 @@ def main() -> None:
         masker.set_param(native.PARAM_GROUP_UNROLL, args.unroll)
         ab = {name: {"median_ms": round(float(np.median(x)), 4),
                      "min_ms": round(float(np.min(x)), 4)} for name, x in samples.items()}
+    fastq = None if args.no_fastq else fastq_bench(masker, db, arr, args, torch, rank)
     totals = db.totals()
     batch_info = db.info()
     if dist is not None:
@@ -314,6 +387,7 @@ def main() -> None:
                  "kernels": {n: {"avg_ms": round(v["avg_ms"], 5), "launches_per_step": v["launches"] // args.steps,
                                  "alg_bytes": kb.get(kernel_class(n))} for n, v in per_kernel.items()}},
         "ab_small_scope_kernel": ab,
+        "fastq": fastq,
         "totals": {k: int(v) for k, v in zip(native.TOTAL_NAMES, job_totals)},
         "batch": batch_info,
         "setup_s": {"generate": round(t_gen, 1), "upload_pcie": round(t_up, 2)},

@@ -107,6 +107,12 @@ class CompleteGermlineAnonymizer:
             self._engine = native.HipMasker(self.device)
         return self._engine
 
+    def format_fastq(self, recs: dict) -> bytes:
+        """FASTQ records on the masking engine's device (``ganon_fastq_format_hip``); an engine
+        without a formatter (none in the product) leaves them to libganon_host.so."""
+        fmt = getattr(self.engine, "format_fastq", None)
+        return fmt(recs) if fmt is not None else native.host_format_fastq(recs)
+
     def anonymize(self, planner: SamplePlanner, plan: Plan, scope_ids=None) -> MaskResult:
         """Mask all scopes of ``plan`` (or the contig shard ``scope_ids``) in one device batch.
         Per-scope counts come back indexed by plan scope id (zero outside the shard)."""

@@ -1,7 +1,8 @@
 """In-tree build of the native libraries (no JIT cache: the .so files travel with the repo
 snapshot to the GPU box).
 
-* ``genomeanonymizer_amd/libganon_hip.so``  — HIP kernels + C ABI (include/ganon.h), gfx950
+* ``genomeanonymizer_amd/libganon_hip.so``  — HIP kernels (masking, FASTQ formatter) + C ABI
+  (include/ganon.h), gfx950
 * ``genomeanonymizer_amd/libganon_host.so`` — BAM decoder + FASTQ formatter (include/ganon_host.h)
 * ``oracle/build/libganon_oracle.so``       — CPU restatement used by tests/bench only
 """
@@ -42,13 +43,16 @@ def _run(cmd) -> None:
         raise RuntimeError(f"build failed: {' '.join(cmd)}")
 
 
+HIP_SOURCES = ("ganon_hip.hip", "ganon_fastq.hip")
+
+
 def build_hip(force: bool = False) -> str:
-    src = os.path.join(CSRC, "ganon_hip.hip")
-    hdr = os.path.join(REPO, "include", "ganon.h")
-    if force or _stale(HIP_LIB, [src, hdr, __file__]):
+    srcs = [os.path.join(CSRC, s) for s in HIP_SOURCES]
+    deps = srcs + [os.path.join(REPO, "include", "ganon.h"), os.path.join(CSRC, "ganon_ctx.h"), __file__]
+    if force or _stale(HIP_LIB, deps):
         tmp = HIP_LIB + ".tmp"
         _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-              "-fvisibility=hidden", "-Wno-unused-result", "-Wno-unused-value", "-o", tmp, src])
+              "-fvisibility=hidden", "-Wno-unused-result", "-Wno-unused-value", "-o", tmp] + srcs)
         os.replace(tmp, HIP_LIB)
     return HIP_LIB
 

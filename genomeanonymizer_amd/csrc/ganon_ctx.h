@@ -1,0 +1,98 @@
+// ganon_ctx.h — internal to libganon_hip.so: the context shared by the masking kernels
+// (ganon_hip.hip) and the FASTQ formatter (ganon_fastq.hip), error/launch helpers and the
+// per-kernel event timer. Not part of the C ABI (include/ganon.h is).
+#ifndef GANON_CTX_H
+#define GANON_CTX_H
+
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "../../include/ganon.h"
+
+struct ganon_ctx {
+  int device = 0;
+  hipStream_t own = nullptr;
+  hipStream_t stream = nullptr;
+  bool profiling = false;
+  int variant = GANON_VARIANT_DEFAULT;
+  int v3_blocks[2] = {1, 1};   // resident grid of k_scope_v3 per class (occupancy x CUs)
+  int group_unroll = 2;        // GANON_PARAM_GROUP_UNROLL
+  int group_skip = 0;          // GANON_PARAM_GROUP_SKIP (profiling only)
+  int group_target = 256;      // GANON_PARAM_GROUP_TARGET
+  int nt_copy = 1;             // GANON_PARAM_NT_COPY
+  int ref2 = 1;                // GANON_PARAM_REF2
+  int fq_skip = 0;             // GANON_PARAM_FASTQ_SKIP (profiling only)
+  int fq_kd = 4;               // GANON_PARAM_FASTQ_KD
+  std::string err;
+  struct Rec { std::string name; hipEvent_t e0, e1; };
+  std::vector<Rec> recs;
+  std::vector<hipEvent_t> pool;
+  std::vector<ganon_kernel_time> last_times;
+};
+
+// Device sequence buffers of an uploaded masking batch (defined in ganon_hip.hip): the input
+// (BAM nt16 layout) and the masked output, both `bytes` long.
+int ganon_dbatch_seq_buffers(const ganon_dbatch *db, const uint8_t **in, const uint8_t **out, int64_t *bytes);
+
+namespace ganon_detail {
+
+inline int fail(ganon_ctx *ctx, int code, const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (ctx) ctx->err = buf;
+  return code;
+}
+
+inline hipEvent_t get_event(ganon_ctx *ctx) {
+  if (!ctx->pool.empty()) {
+    hipEvent_t e = ctx->pool.back();
+    ctx->pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  hipEventCreate(&e);
+  return e;
+}
+
+// HIP event pair around the launches of its lifetime when profiling is on
+// (ganon_last_kernel_times).
+struct KernelScope {
+  ganon_ctx *ctx;
+  ganon_ctx::Rec rec;
+  KernelScope(ganon_ctx *c, const char *name) : ctx(c) {
+    if (!ctx->profiling) return;
+    rec.name = name;
+    rec.e0 = get_event(ctx);
+    rec.e1 = get_event(ctx);
+    hipEventRecord(rec.e0, ctx->stream);
+  }
+  ~KernelScope() {
+    if (!ctx->profiling) return;
+    hipEventRecord(rec.e1, ctx->stream);
+    ctx->recs.push_back(rec);
+  }
+};
+
+inline int check_launch(ganon_ctx *ctx, const char *what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(ctx, GANON_E_DEVICE, "launch of %s failed: %s", what, hipGetErrorString(e));
+  return GANON_OK;
+}
+
+}  // namespace ganon_detail
+
+#define HIP_OR_FAIL(call)                                                                          \
+  do {                                                                                             \
+    hipError_t e_ = (call);                                                                        \
+    if (e_ != hipSuccess)                                                                          \
+      return ganon_detail::fail(ctx, GANON_E_DEVICE, "%s failed: %s", #call, hipGetErrorString(e_)); \
+  } while (0)
+
+#endif  // GANON_CTX_H

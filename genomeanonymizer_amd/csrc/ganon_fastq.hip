@@ -1,0 +1,1008 @@
+// ganon_fastq.hip — MI355X (gfx950) FASTQ record formatter, part of
+// libganon_hip.so; C ABI in include/ganon.h (ganon_fastq_*).
+//
+// Reference: AnonymizedRead.get_anonymized_fastq_record (anonymizer_methods.py:215-243) with
+// reverse_complement (:205-213; table `reverses`, :22: A<->T, C<->G, N->N, any other base a
+// KeyError — SURVEY Q7) and write_pair's record framing (short_read_tumor_normal_anonymizer.py
+// :134-165): '@' name '/' mate '\n' SEQ '\n' '+' '\n' QUAL '\n', qualities printed in the order
+// they are stored in the BAM for every read. Same contract as the host formatter
+// ganon_fastq_format (include/ganon_host.h), which the parity tests compare byte for byte.
+//
+// Design: byte work, HBM-bound. A run is four launches:
+//   k_fq_bsum   record-length sums per block of 2048 records
+//   k_fq_bscan  one workgroup: exclusive scan of the block sums (also resets the error slot)
+//   k_fq_off    record output offsets (u64) + for every 16 KiB output tile the record that
+//               holds its first byte
+//   k_fq_format one workgroup per 16 KiB output tile, records staged in LDS. Lanes own
+//               consecutive output dwords (every store instruction writes 256 contiguous
+//               bytes, each line once); a per-lane record cursor walks forward. A dword inside
+//               one field is built from two aligned dword loads: names as they are,
+//               qualities + 33 per byte (SWAR, byte-reversed for reversed qualities), bases
+//               as four nibbles through two v_perm table lookups (reverse complement likewise,
+//               with a zero-byte test for the Q7 error); dwords across fields are built byte
+//               by byte. KD dwords per lane are loaded before any is used.
+#include "ganon_ctx.h"
+
+#include <algorithm>
+#include <climits>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+namespace {
+
+using ganon_detail::check_launch;
+using ganon_detail::fail;
+using ganon_detail::KernelScope;
+
+constexpr int kFqThreads = 256;
+constexpr int kFqTile = 8192;                                 // output bytes per workgroup
+constexpr int kFqStage = 64;                                  // records per tile of the main kernel (more: k_fq_dense)
+constexpr int kFqDenseGrid = 512;                             // workgroups of k_fq_dense
+constexpr int kFqScanPer = 8;                                 // records per thread in the offset scan
+constexpr int kFqScanBlock = kFqThreads * kFqScanPer;         // 2048 records per scan block
+constexpr int kFqScanThreads = 1024;
+constexpr int kFqMaxBufs = GANON_FASTQ_MAX_BUFS;
+
+constexpr uint64_t kOff56 = (1ull << 56) - 1;
+constexpr uint64_t kOff48 = (1ull << 48) - 1;
+
+// One record, 32 bytes:
+//   seq  = nibble offset (56 bits) | seq buffer << 56 (2 bits) | reverse << 58 | qual_rev << 59
+//   qual = byte offset (48 bits) | mate byte << 48 | qual buffer << 56 (2 bits)
+//   name = byte offset (48 bits) | name length << 48 (16 bits)
+struct FqRec {
+  uint64_t seq, qual, name;
+  uint32_t len, qlen;
+};
+static_assert(sizeof(FqRec) == 32, "FqRec is two 16-byte words");
+
+struct FqBufs {
+  const uint8_t *seq[kFqMaxBufs];
+  const uint8_t *qual[kFqMaxBufs];
+  const uint8_t *names;
+};
+
+// "=ACMGRSVTWYHKDBN" and its reverse complement per reverse_complement (0 = no mapping).
+constexpr uint64_t kFwdLo = 0x565352474D43413Dull;   // = A C M G R S V   (codes 0..7)
+constexpr uint64_t kFwdHi = 0x4E42444B48595754ull;   // T W Y H K D B N   (codes 8..15)
+constexpr uint64_t kRevLo = 0x0000004300475400ull;   // A->T, C->G, G->C  (codes 1, 2, 4)
+constexpr uint64_t kRevHi = 0x4E00000000000041ull;   // T->A (8), N->N (15)
+
+__device__ __forceinline__ uint32_t tab16(uint64_t lo, uint64_t hi, uint32_t c) {
+  const uint64_t w = c < 8 ? lo : hi;
+  return (uint32_t)(w >> (8 * (c & 7))) & 0xFF;
+}
+
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+__device__ __forceinline__ unsigned long long wave_incl_scan(unsigned long long v) {
+  const int lane = threadIdx.x & 63;
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long t = __shfl_up(v, o);
+    if (lane >= o) v += t;
+  }
+  return v;
+}
+
+__global__ void __launch_bounds__(kFqThreads) k_fq_bsum(const uint32_t *__restrict__ len,
+                                                        unsigned long long *__restrict__ bsum) {
+  __shared__ unsigned long long s[kFqThreads / 64];
+  const uint4 *p = reinterpret_cast<const uint4 *>(len + (int64_t)blockIdx.x * kFqScanBlock) + 2 * threadIdx.x;
+  const uint4 a = p[0], b = p[1];
+  unsigned long long v = (unsigned long long)a.x + a.y + a.z + a.w + b.x + b.y + b.z + b.w;
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) bsum[blockIdx.x] = s[0] + s[1] + s[2] + s[3];
+}
+
+__global__ void __launch_bounds__(kFqScanThreads) k_fq_bscan(unsigned long long *__restrict__ bsum, int64_t nb,
+                                                             unsigned long long *__restrict__ err,
+                                                             unsigned int *__restrict__ dense_count) {
+  __shared__ unsigned long long s[kFqScanThreads / 64];
+  __shared__ unsigned long long s_carry;
+  if (threadIdx.x == 0) {
+    s_carry = 0;
+    *err = ~0ull;
+    *dense_count = 0;
+  }
+  __syncthreads();
+  for (int64_t base = 0; base < nb; base += kFqScanThreads) {
+    const int64_t i = base + threadIdx.x;
+    const unsigned long long v = i < nb ? bsum[i] : 0;
+    const unsigned long long w = wave_incl_scan(v);
+    if ((threadIdx.x & 63) == 63) s[threadIdx.x >> 6] = w;
+    __syncthreads();
+    unsigned long long pre = s_carry;
+    for (int k = 0; k < (int)(threadIdx.x >> 6); ++k) pre += s[k];
+    if (i < nb) bsum[i] = pre + w - v;   // exclusive
+    __syncthreads();
+    if (threadIdx.x == kFqScanThreads - 1) s_carry = pre + w;
+    __syncthreads();
+  }
+}
+
+__global__ void __launch_bounds__(kFqThreads) k_fq_off(const uint32_t *__restrict__ len,
+                                                       const unsigned long long *__restrict__ boff, int64_t n,
+                                                       uint64_t *__restrict__ off, int64_t *__restrict__ tile_first) {
+  __shared__ unsigned long long s[kFqThreads / 64];
+  const int64_t r0 = (int64_t)blockIdx.x * kFqScanBlock + kFqScanPer * threadIdx.x;
+  const uint4 *p = reinterpret_cast<const uint4 *>(len + r0);
+  const uint4 a = p[0], b = p[1];
+  const uint32_t l[kFqScanPer] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  unsigned long long v = 0;
+#pragma unroll
+  for (int k = 0; k < kFqScanPer; ++k) v += l[k];
+  const unsigned long long w = wave_incl_scan(v);
+  if ((threadIdx.x & 63) == 63) s[threadIdx.x >> 6] = w;
+  __syncthreads();
+  unsigned long long o = boff[blockIdx.x] + w - v;
+  for (int k = 0; k < (int)(threadIdx.x >> 6); ++k) o += s[k];
+#pragma unroll
+  for (int k = 0; k < kFqScanPer; ++k) {
+    const int64_t r = r0 + k;
+    if (r >= n) break;
+    const unsigned long long e = o + l[k];
+    off[r] = o;
+    // tiles whose first byte lies in [o, e)
+    for (unsigned long long t = (o + kFqTile - 1) / kFqTile; t * kFqTile < e; ++t) tile_first[t] = r;
+    if (r == n - 1) off[n] = e;
+    o = e;
+  }
+}
+
+__device__ __forceinline__ const uint8_t *pick4(const uint8_t *const (&p)[kFqMaxBufs], uint32_t sel) {
+  // per-lane choice among kernel-argument pointers without indexing the argument block
+  const uint8_t *a = (sel & 1) ? p[1] : p[0];
+  const uint8_t *b = (sel & 1) ? p[3] : p[2];
+  return (sel & 2) ? b : a;
+}
+
+// Per output byte (record offset o of record R): its source and how it is transformed.
+// info = constant value | kind << 8 (0 const, 1 raw name byte, 2 nt16 nibble, 3 quality) |
+//        low nibble << 10 | reverse << 11
+struct FqSrc {
+  const uint8_t *addr;
+  uint32_t info;
+};
+
+__device__ __forceinline__ FqSrc fq_src(const FqRec &R, uint32_t o, const FqBufs &bufs) {
+  const uint32_t NL = (uint32_t)(R.name >> 48), L = R.len, Q = R.qlen;
+  FqSrc s{bufs.names, 0u};
+  if (o == 0) {
+    s.info = '@';
+    return s;
+  }
+  o -= 1;
+  if (o < NL) {
+    s.addr = bufs.names + (R.name & kOff48) + o;
+    s.info = 1u << 8;
+    return s;
+  }
+  o -= NL;
+  if (o < 3) {
+    s.info = o == 0 ? '/' : o == 1 ? (((uint32_t)(R.qual >> 48) & 0xFF) + '0') & 0xFF : '\n';
+    return s;
+  }
+  o -= 3;
+  if (o < L) {
+    const uint32_t rev = (uint32_t)(R.seq >> 58) & 1;
+    const uint64_t nib = (R.seq & kOff56) + (rev ? L - 1 - o : o);
+    s.addr = pick4(bufs.seq, (uint32_t)(R.seq >> 56) & 3) + (nib >> 1);
+    s.info = (2u << 8) | ((uint32_t)(nib & 1) << 10) | (rev << 11);
+    return s;
+  }
+  o -= L;
+  if (o < 3) {
+    s.info = o == 1 ? '+' : '\n';
+    return s;
+  }
+  o -= 3;
+  if (o < Q) {
+    const uint32_t qrev = (uint32_t)(R.seq >> 59) & 1;
+    s.addr = pick4(bufs.qual, (uint32_t)(R.qual >> 56) & 3) + (R.qual & kOff48) + (qrev ? Q - 1 - o : o);
+    s.info = 3u << 8;
+    return s;
+  }
+  s.info = '\n';
+  return s;
+}
+
+__device__ __forceinline__ uint32_t fq_val(uint32_t info, uint32_t byte, bool &bad) {
+  const uint32_t kind = (info >> 8) & 3;
+  if (kind == 1) return byte;
+  if (kind == 3) return (byte + 33) & 0xFF;
+  if (kind == 2) {
+    const uint32_t c = (info >> 10) & 1 ? (byte & 0xF) : (byte >> 4);
+    if ((info >> 11) & 1) {
+      const uint32_t x = tab16(kRevLo, kRevHi, c);
+      bad |= x == 0;
+      return x;
+    }
+    return tab16(kFwdLo, kFwdHi, c);
+  }
+  return info & 0xFF;
+}
+
+// nt16 codes (one per byte of c, 0..15) -> table bytes, two v_perm over the 16-byte table.
+__device__ __forceinline__ uint32_t nt16_lut(uint32_t c, uint64_t lo, uint64_t hi) {
+  const uint32_t sel = c & 0x07070707u;
+  const uint32_t a = __builtin_amdgcn_perm((uint32_t)(lo >> 32), (uint32_t)lo, sel);
+  const uint32_t b = __builtin_amdgcn_perm((uint32_t)(hi >> 32), (uint32_t)hi, sel);
+  const uint32_t m = ((c >> 3) & 0x01010101u) * 0xFFu;
+  return (b & m) | (a & ~m);
+}
+
+__device__ __forceinline__ uint32_t add33(uint32_t x) {   // per byte (x + 33) & 0xFF
+  return ((x & 0x7F7F7F7Fu) + 0x21212121u) ^ (x & 0x80808080u);
+}
+
+// Field f of a record (0 name, 1 bases, 2 qualities) clipped to the tile, in tile bytes:
+// [a, b); aligned interior dwords [ia, ib) (empty when ia >= ib: then every byte is an edge).
+struct FqField {
+  int a, b, ia, ib;
+};
+
+__device__ __forceinline__ FqField fq_field(int64_t P0, uint32_t fa, uint32_t len) {
+  FqField F;
+  const int64_t a = max<int64_t>(P0 + fa, 0), b = min<int64_t>(P0 + fa + len, kFqTile);
+  F.a = (int)min<int64_t>(a, kFqTile);
+  F.b = (int)max<int64_t>(b, (int64_t)F.a);
+  F.ia = (F.a + 3) & ~3;
+  F.ib = F.b & ~3;
+  return F;
+}
+
+// Edge byte e (0..5) of a field: tile position, or -1.
+__device__ __forceinline__ int fq_edge(const FqField &F, int e) {
+  if (F.ia >= F.ib) return F.a + e < F.b ? F.a + e : -1;
+  if (e < 3) return F.a + e < F.ia ? F.a + e : -1;
+  return F.ib + (e - 3) < F.b ? F.ib + (e - 3) : -1;
+}
+
+// One record into the tile image by one wave, in three phases so that a wave can keep the
+// loads of several records in flight (k_fq_format batches NB records): prep computes every
+// source address, load issues the loads, finish transforms and writes. Every branch is
+// wave-uniform except the lane-range guards: name / base / quality interiors as aligned dwords
+// (two dword loads, a v_perm or SWAR transform, ds_write_b32), the <= 6 edge bytes of each
+// field and the 8 constant bytes on lanes 0..25 (one byte load each, ds_write_b8). Fields
+// longer than 256 bytes take several passes (ps); edges and constants go with pass 0.
+struct FqWork {
+  int64_t r;
+  const uint32_t *an, *as, *aq;
+  const uint8_t *eaddr;
+  int tn, ts, tq, et;
+  uint32_t shn, shs, shq, par, flags;   // flags: hn | hs << 1 | hq << 2 | rev << 3 | qrev << 4 | ekind << 5 | elow << 8
+  uint32_t econst;
+  uint32_t n0, n1, s0w, s1w, q0, q1, ev;
+};
+
+__device__ __forceinline__ int fq_passes(const FqRec &R, int64_t P0) {
+  const uint32_t NL = (uint32_t)(R.name >> 48), L = R.len, Q = R.qlen;
+  const FqField Fn = fq_field(P0, 1, NL), Fs = fq_field(P0, NL + 4, L), Fq = fq_field(P0, NL + 7 + L, Q);
+  const int nmax = max(max(Fn.ib - Fn.ia, Fs.ib - Fs.ia), Fq.ib - Fq.ia) >> 2;
+  return max(1, (nmax + 63) >> 6);
+}
+
+__device__ __forceinline__ void fq_prep(FqWork &w, const FqRec &R, int64_t r, int64_t P0, int ps,
+                                        const FqBufs &bufs, int lane) {
+  const uint32_t NL = (uint32_t)(R.name >> 48), L = R.len, Q = R.qlen;
+  const FqField Fn = fq_field(P0, 1, NL), Fs = fq_field(P0, NL + 4, L), Fq = fq_field(P0, NL + 7 + L, Q);
+  const uint8_t *nm = bufs.names + (R.name & kOff48);
+  const uint32_t rev = (uint32_t)(R.seq >> 58) & 1, qrev = (uint32_t)(R.seq >> 59) & 1;
+  const uint8_t *sb = pick4(bufs.seq, (uint32_t)(R.seq >> 56) & 3);
+  const uint64_t s0 = R.seq & kOff56;
+  const uint8_t *qb = pick4(bufs.qual, (uint32_t)(R.qual >> 56) & 3) + (R.qual & kOff48);
+  const int64_t bn = P0 + 1, bs = P0 + NL + 4, bq = P0 + NL + 7 + L;   // tile position of each field's byte 0
+  w.r = r;
+  // interiors
+  const int d = 64 * ps + lane;
+  const uint32_t hn = d < ((Fn.ib - Fn.ia) >> 2), hs = d < ((Fs.ib - Fs.ia) >> 2), hq = d < ((Fq.ib - Fq.ia) >> 2);
+  w.tn = Fn.ia + 4 * d;
+  w.ts = Fs.ia + 4 * d;
+  w.tq = Fq.ia + 4 * d;
+  const uint8_t *pn = nm + (uint32_t)(w.tn - bn);
+  const uint32_t js = (uint32_t)(w.ts - bs);
+  const uint64_t nbs = s0 + (rev ? L - 4 - js : js);
+  const uint8_t *psq = sb + (nbs >> 1);
+  const uint32_t jq = (uint32_t)(w.tq - bq);
+  const uint8_t *pq = qb + (qrev ? Q - 4 - jq : jq);
+  w.an = reinterpret_cast<const uint32_t *>((uintptr_t)pn & ~(uintptr_t)3);
+  w.as = reinterpret_cast<const uint32_t *>((uintptr_t)psq & ~(uintptr_t)3);
+  w.aq = reinterpret_cast<const uint32_t *>((uintptr_t)pq & ~(uintptr_t)3);
+  w.shn = (uint32_t)(uintptr_t)pn & 3;
+  w.shs = (uint32_t)(uintptr_t)psq & 3;
+  w.shq = (uint32_t)(uintptr_t)pq & 3;
+  w.par = (uint32_t)(nbs & 1);
+  // edge / constant lane: one byte (pass 0 only)
+  int et = -1;
+  uint32_t ekind = 0, elow = 0;
+  w.econst = 0;
+  w.eaddr = nm;
+  if (ps == 0 && lane < 18) {
+    const int f = lane / 6, e = lane - 6 * f;
+    const FqField &F = f == 0 ? Fn : f == 1 ? Fs : Fq;
+    et = fq_edge(F, e);
+    if (et >= 0) {
+      const uint32_t j = (uint32_t)(et - (f == 0 ? bn : f == 1 ? bs : bq));
+      ekind = f + 1;
+      if (f == 0) {
+        w.eaddr = nm + j;
+      } else if (f == 1) {
+        const uint64_t nib = s0 + (rev ? L - 1 - j : j);
+        w.eaddr = sb + (nib >> 1);
+        elow = (uint32_t)(nib & 1);
+      } else {
+        w.eaddr = qb + (qrev ? Q - 1 - j : j);
+      }
+    }
+  } else if (ps == 0 && lane < 26) {
+    int64_t o;
+    switch (lane - 18) {
+      case 0: o = 0; w.econst = '@'; break;
+      case 1: o = NL + 1; w.econst = '/'; break;
+      case 2: o = NL + 2; w.econst = ((uint32_t)(R.qual >> 48) + '0') & 0xFF; break;
+      case 3: o = NL + 3; w.econst = '\n'; break;
+      case 4: o = NL + 4 + L; w.econst = '\n'; break;
+      case 5: o = NL + 5 + L; w.econst = '+'; break;
+      case 6: o = NL + 6 + L; w.econst = '\n'; break;
+      default: o = NL + 7 + L + Q; w.econst = '\n'; break;
+    }
+    const int64_t t = P0 + o;
+    et = (t >= 0 && t < kFqTile) ? (int)t : -1;
+  }
+  w.et = et;
+  w.flags = hn | (hs << 1) | (hq << 2) | (rev << 3) | (qrev << 4) | (ekind << 5) | (elow << 8);
+}
+
+__device__ __forceinline__ void fq_load(FqWork &w) {
+  w.n0 = w.n1 = w.s0w = w.s1w = w.q0 = w.q1 = w.ev = 0;
+  if (w.flags & 1) { w.n0 = w.an[0]; w.n1 = w.an[1]; }
+  if (w.flags & 2) { w.s0w = w.as[0]; w.s1w = w.as[1]; }
+  if (w.flags & 4) { w.q0 = w.aq[0]; w.q1 = w.aq[1]; }
+  if (w.et >= 0 && (w.flags >> 5) & 3) w.ev = *w.eaddr;
+}
+
+__device__ __forceinline__ void fq_finish(const FqWork &w, uint8_t *tile, unsigned long long &bad) {
+  uint32_t *tile32 = reinterpret_cast<uint32_t *>(tile);
+  const bool rev = (w.flags >> 3) & 1, qrev = (w.flags >> 4) & 1;
+  if (w.flags & 1) tile32[w.tn >> 2] = __builtin_amdgcn_alignbyte(w.n1, w.n0, w.shn);
+  if (w.flags & 2) {
+    const uint32_t x0 = __builtin_amdgcn_alignbyte(w.s1w, w.s0w, w.shs);
+    const uint32_t hiN = (x0 >> 4) & 0x0F0F0F0Fu, loN = x0 & 0x0F0F0F0Fu;
+    // codes in output order: forward [H0 L0 H1 L1] / [L0 H1 L1 H2], reverse the mirror
+    const uint32_t sel = rev ? (w.par ? 0x04010502u : 0x00040105u) : (w.par ? 0x02050104u : 0x05010400u);
+    const uint32_t cc = __builtin_amdgcn_perm(loN, hiN, sel);
+    const uint32_t x = rev ? nt16_lut(cc, kRevLo, kRevHi) : nt16_lut(cc, kFwdLo, kFwdHi);
+    if (rev && ((x - 0x01010101u) & ~x & 0x80808080u)) bad = min(bad, (unsigned long long)w.r);
+    tile32[w.ts >> 2] = x;
+  }
+  if (w.flags & 4) {
+    const uint32_t x0 = __builtin_amdgcn_alignbyte(w.q1, w.q0, w.shq);
+    tile32[w.tq >> 2] = add33(qrev ? __builtin_bswap32(x0) : x0);
+  }
+  if (w.et >= 0) {
+    const uint32_t ekind = (w.flags >> 5) & 3;
+    uint32_t x = w.econst;
+    if (ekind == 1) {
+      x = w.ev;
+    } else if (ekind == 2) {
+      const uint32_t c = (w.flags >> 8) & 1 ? (w.ev & 0xF) : (w.ev >> 4);
+      x = rev ? tab16(kRevLo, kRevHi, c) : tab16(kFwdLo, kFwdHi, c);
+      if (x == 0) bad = min(bad, (unsigned long long)w.r);
+    } else if (ekind == 3) {
+      x = (w.ev + 33) & 0xFF;
+    }
+    tile[w.et] = (uint8_t)x;
+  }
+}
+
+// Tile image of a dense tile (k_fq_dense): built in LDS record by record, one wave per record.
+__device__ __forceinline__ void fq_tile_by_records(uint8_t *smem, const FqBufs &bufs, const FqRec *__restrict__ recs,
+                                                   const uint64_t *__restrict__ off, int64_t r0, int64_t rl,
+                                                   uint64_t t0, unsigned long long &bad) {
+  uint8_t *tile = smem;
+  FqRec *s_rec = reinterpret_cast<FqRec *>(smem + kFqTile);
+  uint64_t *s_off = reinterpret_cast<uint64_t *>(smem + kFqTile + kFqStage * sizeof(FqRec));
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int64_t sb = r0; sb <= rl; sb += kFqStage) {
+    const int ns = (int)min<int64_t>(kFqStage, rl - sb + 1);
+    if (sb != r0) __syncthreads();   // the previous batch of staged records is done
+    for (int k = threadIdx.x; k < ns; k += kFqThreads) s_rec[k] = recs[sb + k];
+    for (int k = threadIdx.x; k <= ns; k += kFqThreads) s_off[k] = off[sb + k];
+    __syncthreads();
+    for (int k = wave; k < ns; k += kFqThreads / 64) {
+      const FqRec R = s_rec[k];
+      const int64_t P0 = (int64_t)s_off[k] - (int64_t)t0;
+      const int np = fq_passes(R, P0);
+      for (int ps = 0; ps < np; ++ps) {
+        FqWork w;
+        fq_prep(w, R, sb + k, P0, ps, bufs, lane);
+        fq_load(w);
+        fq_finish(w, tile, bad);
+      }
+    }
+  }
+}
+
+// Per-tile record descriptors (LDS), one entry per record touching the tile, computed once
+// per record by one thread. Field f: 0 bases, 1 qualities, 2 name.
+struct FqDescs {
+  int64_t P0[kFqStage];              // tile position of the record's byte 0 (may be negative)
+  uint32_t NL[kFqStage], L[kFqStage], Q[kFqStage], fl[kFqStage];   // fl: rev | qrev << 1 | mate << 8
+  const uint8_t *nm[kFqStage], *sb[kFqStage], *qb[kFqStage];
+  uint64_t s0[kFqStage];             // first nibble of the bases in sb
+  int32_t td0[3][kFqStage];          // first interior tile dword of field f
+  uint16_t vs[3][kFqStage];          // first virtual dword of field f's interior
+};
+constexpr int kFqDw = kFqTile / 4;   // dwords per tile
+constexpr size_t kFqSmemA = kFqTile + kFqStage * sizeof(FqRec) + (kFqStage + 1) * sizeof(uint64_t);
+constexpr size_t kFqSmemB = kFqTile + kFqDw * sizeof(uint16_t) + sizeof(FqDescs);
+constexpr int kFqSpecial = 26;       // per record: 8 constant bytes + up to 6 edge bytes per field
+
+// Block-wide exclusive scan of a u64 (packed counters), 256 threads; returns the total too.
+__device__ __forceinline__ unsigned long long block_excl_scan(unsigned long long v, unsigned long long *s_w,
+                                                              unsigned long long &total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  unsigned long long inc = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long u = __shfl_up(inc, o);
+    if (lane >= o) inc += u;
+  }
+  if (lane == 63) s_w[w] = inc;
+  __syncthreads();
+  unsigned long long pre = inc - v;
+  total = 0;
+  for (int k = 0; k < kFqThreads / 64; ++k) {
+    if (k < w) pre += s_w[k];
+    total += s_w[k];
+  }
+  return pre;
+}
+
+template <int KD>
+__global__ void __launch_bounds__(kFqThreads) k_fq_format(const FqBufs bufs, const FqRec *__restrict__ recs,
+                                                          const uint64_t *__restrict__ off,
+                                                          const int64_t *__restrict__ tile_first, int64_t n,
+                                                          uint64_t total, uint8_t *__restrict__ out,
+                                                          unsigned long long *__restrict__ err, int skip,
+                                                          int *__restrict__ dense_list,
+                                                          unsigned int *__restrict__ dense_count) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[kFqSmemB];
+  __shared__ unsigned long long s_w[kFqThreads / 64];
+  const uint64_t t0 = (uint64_t)blockIdx.x * kFqTile;
+  const int64_t r0 = tile_first[blockIdx.x];
+  const int64_t rl = (t0 + kFqTile < total) ? tile_first[blockIdx.x + 1] : n - 1;   // last record touching the tile
+  const int t = threadIdx.x;
+  unsigned long long bad = ~0ull;
+  uint8_t *tile = smem;
+  uint32_t *tile32 = reinterpret_cast<uint32_t *>(smem);
+  if (rl - r0 + 1 > kFqStage) {   // left to k_fq_dense
+    if (t == 0) dense_list[atomicAdd(dense_count, 1u)] = (int)blockIdx.x;
+    return;
+  }
+  {
+    const int ns = (int)(rl - r0 + 1);
+    uint16_t *map = reinterpret_cast<uint16_t *>(smem + kFqTile);   // virtual dword -> f << 8 | record
+    FqDescs &D = *reinterpret_cast<FqDescs *>(smem + kFqTile + kFqDw * sizeof(uint16_t));
+    // 1. descriptors, one thread per record, and the interior dword counts per field
+    reinterpret_cast<uint4 *>(map)[t] = make_uint4(0, 0, 0, 0);
+    unsigned long long cnt = 0;   // interior dwords: bases | qualities << 16 | name << 32
+    int td[3] = {0, 0, 0};
+    if (t < ns) {
+      const FqRec R = recs[r0 + t];
+      const int64_t P0 = (int64_t)off[r0 + t] - (int64_t)t0;
+      const uint32_t NL = (uint32_t)(R.name >> 48), L = R.len, Q = R.qlen;
+      D.P0[t] = P0;
+      D.NL[t] = NL;
+      D.L[t] = L;
+      D.Q[t] = Q;
+      D.fl[t] = (uint32_t)((R.seq >> 58) & 1) | ((uint32_t)((R.seq >> 59) & 1) << 1) |
+                ((uint32_t)((R.qual >> 48) & 0xFF) << 8);
+      D.nm[t] = bufs.names + (R.name & kOff48);
+      D.sb[t] = pick4(bufs.seq, (uint32_t)(R.seq >> 56) & 3);
+      D.s0[t] = R.seq & kOff56;
+      D.qb[t] = pick4(bufs.qual, (uint32_t)(R.qual >> 56) & 3) + (R.qual & kOff48);
+      const FqField Fs = fq_field(P0, NL + 4, L), Fq = fq_field(P0, NL + 7 + L, Q), Fn = fq_field(P0, 1, NL);
+      const int cs = max(0, (Fs.ib - Fs.ia) >> 2), cq = max(0, (Fq.ib - Fq.ia) >> 2), cn = max(0, (Fn.ib - Fn.ia) >> 2);
+      td[0] = Fs.ia >> 2;
+      td[1] = Fq.ia >> 2;
+      td[2] = Fn.ia >> 2;
+      cnt = (unsigned long long)cs | ((unsigned long long)cq << 16) | ((unsigned long long)cn << 32);
+    }
+    unsigned long long tot;
+    const unsigned long long pre = block_excl_scan(cnt, s_w, tot);
+    const int V0 = (int)(tot & 0xFFFF), V1 = V0 + (int)((tot >> 16) & 0xFFFF), V = V1 + (int)((tot >> 32) & 0xFFFF);
+    if (t < ns) {
+      const int base[3] = {0, V0, V1};
+#pragma unroll
+      for (int f = 0; f < 3; ++f) {
+        const int c = (int)((cnt >> (16 * f)) & 0xFFFF);
+        const int v = base[f] + (int)((pre >> (16 * f)) & 0xFFFF);
+        D.td0[f][t] = td[f];
+        D.vs[f][t] = (uint16_t)v;
+        if (c > 0) map[v] = (uint16_t)(f << 8 | t);
+      }
+    }
+    __syncthreads();
+    // 2. fill forward (prefix max over f << 8 | record, increasing along the virtual dwords):
+    //    thread t owns map[8t, 8t + 8)
+    {
+      static_assert(kFqDw == 8 * kFqThreads, "one uint4 of the map per thread");
+      uint4 *m4 = reinterpret_cast<uint4 *>(map) + t;
+      const uint4 a = m4[0];
+      uint32_t v[8] = {a.x & 0xFFFF, a.x >> 16, a.y & 0xFFFF, a.y >> 16, a.z & 0xFFFF, a.z >> 16, a.w & 0xFFFF, a.w >> 16};
+      uint32_t mx = 0;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) mx = max(mx, v[i]);
+      uint32_t inc = mx;
+      const int lane = t & 63;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t u = __shfl_up(inc, o);
+        if (lane >= o) inc = max(inc, u);
+      }
+      __syncthreads();   // s_w reused
+      if (lane == 63) s_w[t >> 6] = inc;
+      __syncthreads();
+      uint32_t pm = __shfl_up(inc, 1);
+      if (lane == 0) pm = 0;
+      for (int w = 0; w < (t >> 6); ++w) pm = max(pm, (uint32_t)s_w[w]);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        pm = max(pm, v[i]);
+        v[i] = pm;
+      }
+      m4[0] = make_uint4(v[0] | v[1] << 16, v[2] | v[3] << 16, v[4] | v[5] << 16, v[6] | v[7] << 16);
+    }
+    __syncthreads();
+    // 3. interiors: virtual dwords on consecutive lanes (one field type per wave but at the two
+    //    type changes), KD per lane at a time, two aligned dword loads each
+#pragma unroll 1
+    for (int vb = 0; vb < V; vb += kFqThreads * KD) {
+      uint32_t key[KD], sh[KD], par[KD], v0[KD], v1[KD];
+      int td[KD];
+      const uint32_t *a0[KD];
+#pragma unroll
+      for (int j = 0; j < KD; ++j) {
+        const int v = vb + j * kFqThreads + t;
+        key[j] = 0xFFFFu;
+        a0[j] = reinterpret_cast<const uint32_t *>(bufs.names);
+        sh[j] = par[j] = 0;
+        td[j] = 0;
+        if (v >= V) continue;
+        const uint32_t kf = map[v];
+        const int f = kf >> 8, k = kf & 0xFF;
+        key[j] = kf;
+        const int tdw = D.td0[f][k] + (v - D.vs[f][k]);
+        td[j] = tdw;
+        const int64_t P0 = D.P0[k];
+        const uint32_t NL = D.NL[k], L = D.L[k], Q = D.Q[k], fl = D.fl[k];
+        const uint8_t *src;
+        if (f == 0) {
+          const uint32_t jb = (uint32_t)(4 * (int64_t)tdw - (P0 + NL + 4));
+          const bool rev = fl & 1;
+          const uint64_t nb = D.s0[k] + (rev ? L - 4 - jb : jb);
+          src = D.sb[k] + (nb >> 1);
+          par[j] = (uint32_t)(nb & 1);
+        } else if (f == 1) {
+          const uint32_t jb = (uint32_t)(4 * (int64_t)tdw - (P0 + NL + 7 + L));
+          src = D.qb[k] + (((fl >> 1) & 1) ? Q - 4 - jb : jb);
+        } else {
+          src = D.nm[k] + (uint32_t)(4 * (int64_t)tdw - (P0 + 1));
+        }
+        sh[j] = (uint32_t)((uintptr_t)src & 3);
+        a0[j] = reinterpret_cast<const uint32_t *>((uintptr_t)src & ~(uintptr_t)3);
+      }
+      if (!(skip & 1)) {
+#pragma unroll
+        for (int j = 0; j < KD; ++j) {
+          v0[j] = __builtin_nontemporal_load(a0[j]);
+          v1[j] = __builtin_nontemporal_load(a0[j] + 1);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < KD; ++j) v0[j] = v1[j] = 0x11111111u;
+      }
+#pragma unroll
+      for (int j = 0; j < KD; ++j) {
+        if (key[j] == 0xFFFFu) continue;
+        const int f = key[j] >> 8, k = key[j] & 0xFF;
+        const uint32_t w = __builtin_amdgcn_alignbyte(v1[j], v0[j], sh[j]);
+        const uint32_t fl = D.fl[k];
+        uint32_t x;
+        if (f == 0) {
+          const uint32_t hiN = (w >> 4) & 0x0F0F0F0Fu, loN = w & 0x0F0F0F0Fu;
+          // codes in output order: forward [H0 L0 H1 L1] / [L0 H1 L1 H2], reverse the mirror
+          const bool rev = fl & 1;
+          const uint32_t sel = rev ? (par[j] ? 0x04010502u : 0x00040105u) : (par[j] ? 0x02050104u : 0x05010400u);
+          const uint32_t cc = __builtin_amdgcn_perm(loN, hiN, sel);
+          x = rev ? nt16_lut(cc, kRevLo, kRevHi) : nt16_lut(cc, kFwdLo, kFwdHi);
+          if (rev && ((x - 0x01010101u) & ~x & 0x80808080u)) bad = min(bad, (unsigned long long)(r0 + k));
+        } else if (f == 1) {
+          x = add33(((fl >> 1) & 1) ? __builtin_bswap32(w) : w);
+        } else {
+          x = w;
+        }
+        tile32[td[j]] = x;
+      }
+    }
+    // 4. constant and edge bytes: kFqSpecial slots per record, one thread each
+#pragma unroll 1
+    for (int s = t; s < ns * kFqSpecial; s += kFqThreads) {
+      const int k = s / kFqSpecial, e = s - k * kFqSpecial;
+      const int64_t P0 = D.P0[k];
+      const uint32_t NL = D.NL[k], L = D.L[k], Q = D.Q[k], fl = D.fl[k];
+      int pos = -1;
+      uint32_t x = 0;
+      if (e < 8) {
+        int64_t o;
+        switch (e) {
+          case 0: o = 0; x = '@'; break;
+          case 1: o = NL + 1; x = '/'; break;
+          case 2: o = NL + 2; x = ((fl >> 8) + '0') & 0xFF; break;
+          case 3: o = NL + 3; x = '\n'; break;
+          case 4: o = NL + 4 + L; x = '\n'; break;
+          case 5: o = NL + 5 + L; x = '+'; break;
+          case 6: o = NL + 6 + L; x = '\n'; break;
+          default: o = NL + 7 + L + Q; x = '\n'; break;
+        }
+        const int64_t p = P0 + o;
+        pos = (p >= 0 && p < kFqTile) ? (int)p : -1;
+      } else {
+        const int f = (e - 8) / 6, ee = (e - 8) - 6 * f;   // 0 bases, 1 qualities, 2 name
+        const uint32_t fa = f == 0 ? NL + 4 : f == 1 ? NL + 7 + L : 1, len = f == 0 ? L : f == 1 ? Q : NL;
+        pos = fq_edge(fq_field(P0, fa, len), ee);
+        if (pos >= 0) {
+          const uint32_t jb = (uint32_t)(pos - (P0 + fa));
+          if (f == 0) {
+            const bool rev = fl & 1;
+            const uint64_t nib = D.s0[k] + (rev ? L - 1 - jb : jb);
+            const uint32_t byte = (skip & 1) ? 0x11u : D.sb[k][nib >> 1];
+            const uint32_t c = (nib & 1) ? (byte & 0xF) : (byte >> 4);
+            x = rev ? tab16(kRevLo, kRevHi, c) : tab16(kFwdLo, kFwdHi, c);
+            if (rev && x == 0) bad = min(bad, (unsigned long long)(r0 + k));
+          } else if (f == 1) {
+            x = (((skip & 1) ? 0x11u : D.qb[k][((fl >> 1) & 1) ? Q - 1 - jb : jb]) + 33) & 0xFF;
+          } else {
+            x = (skip & 1) ? 0x41u : D.nm[k][jb];
+          }
+        }
+      }
+      if (pos >= 0) tile[pos] = (uint8_t)x;
+    }
+  }
+  if (bad != ~0ull && !(skip & 1)) atomicMin(err, bad);
+  __syncthreads();
+  if (skip & 2) return;
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int q = 0; q < kFqTile / (16 * kFqThreads); ++q) {
+    const int p = (q * kFqThreads + t) * 16;
+    if (t0 + p >= total) break;
+    __builtin_nontemporal_store(*reinterpret_cast<const u32x4 *>(tile + p), reinterpret_cast<u32x4 *>(out + t0 + p));
+  }
+}
+
+// Tiles touched by more than kFqStage records (records of a few dozen bytes), listed by
+// k_fq_format: built in LDS record by record (one wave per record), a fixed grid looping over
+// the list.
+__global__ void __launch_bounds__(kFqThreads) k_fq_dense(const FqBufs bufs, const FqRec *__restrict__ recs,
+                                                         const uint64_t *__restrict__ off,
+                                                         const int64_t *__restrict__ tile_first, int64_t n,
+                                                         uint64_t total, uint8_t *__restrict__ out,
+                                                         unsigned long long *__restrict__ err,
+                                                         const int *__restrict__ dense_list,
+                                                         const unsigned int *__restrict__ dense_count) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[kFqSmemA];
+  const unsigned int cnt = *dense_count;
+  unsigned long long bad = ~0ull;
+  for (unsigned int i = blockIdx.x; i < cnt; i += gridDim.x) {
+    const int tl = dense_list[i];
+    const uint64_t t0 = (uint64_t)tl * kFqTile;
+    const int64_t r0 = tile_first[tl];
+    const int64_t rl = (t0 + kFqTile < total) ? tile_first[tl + 1] : n - 1;
+    __syncthreads();   // the previous tile's image has been stored
+    fq_tile_by_records(smem, bufs, recs, off, r0, rl, t0, bad);
+    __syncthreads();
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int q = 0; q < kFqTile / (16 * kFqThreads); ++q) {
+      const int p = (q * kFqThreads + threadIdx.x) * 16;
+      if (t0 + p >= total) break;
+      __builtin_nontemporal_store(*reinterpret_cast<const u32x4 *>(smem + p), reinterpret_cast<u32x4 *>(out + t0 + p));
+    }
+  }
+  if (bad != ~0ull) atomicMin(err, bad);
+}
+
+}  // namespace
+
+// ---- host side ---------------------------------------------------------------------------
+
+struct ganon_fastq {
+  std::vector<void *> allocs;
+  int64_t n = 0, nb = 0, n_tiles = 0;
+  uint64_t total = 0;
+  FqBufs bufs{};
+  FqRec *recs = nullptr;
+  uint32_t *len = nullptr;
+  uint64_t *off = nullptr;
+  int64_t *tile_first = nullptr;
+  unsigned long long *bsum = nullptr, *err = nullptr;
+  int *dense_list = nullptr;          // tiles left to k_fq_dense
+  unsigned int *dense_count = nullptr;
+  uint8_t *out = nullptr;
+};
+
+namespace {
+
+template <typename T>
+int fq_alloc(ganon_ctx *ctx, ganon_fastq *f, T **p, size_t count) {
+  *p = nullptr;
+  const size_t bytes = std::max<size_t>(count, 1) * sizeof(T) + 128;
+  hipError_t e = hipMalloc(reinterpret_cast<void **>(p), bytes);
+  if (e != hipSuccess) return fail(ctx, GANON_E_NOMEM, "hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
+  f->allocs.push_back(*p);
+  return GANON_OK;
+}
+
+void fq_release(ganon_fastq *f) {
+  for (void *p : f->allocs) hipFree(p);
+  f->allocs.clear();
+}
+
+// Parallel loop over [0, n) in contiguous slices (host packing of the record array).
+template <typename F>
+void host_parallel(int64_t n, F fn) {
+  const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(std::thread::hardware_concurrency(),
+                                                               std::min<int64_t>(16, n / 65536 + 1)));
+  std::vector<std::thread> pool;
+  for (int t = 0; t < nt; ++t)
+    pool.emplace_back([&, t] { fn(n * t / nt, n * (t + 1) / nt); });
+  for (auto &th : pool) th.join();
+}
+
+}  // namespace
+
+GANON_API int ganon_fastq_upload(ganon_ctx *ctx, const ganon_fastq_records *in, ganon_fastq **out) {
+  if (!ctx || !in || !out) return GANON_E_ARG;
+  *out = nullptr;
+  const int64_t n = in->n;
+  if (n < 0 || n > (int64_t)INT32_MAX * 64) return fail(ctx, GANON_E_ARG, "bad record count %lld", (long long)n);
+  const int nsb = in->n_seq_bufs, nqb = in->n_qual_bufs;
+  if (nsb < 1 || nsb > kFqMaxBufs || nqb < 1 || nqb > kFqMaxBufs)
+    return fail(ctx, GANON_E_ARG, "1..%d sequence and quality buffers", kFqMaxBufs);
+  if (n && (!in->seq_sel || !in->seq_nib_off || !in->seq_len || !in->reverse || !in->qual_sel || !in->qual_off ||
+            !in->qual_len || !in->qual_rev || !in->name_off || !in->name_len || !in->mate))
+    return fail(ctx, GANON_E_ARG, "null record array");
+  if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, GANON_E_DEVICE, "hipSetDevice failed");
+  ganon_fastq *f = new ganon_fastq();
+  f->n = n;
+  auto bail = [&](int rc) {
+    fq_release(f);
+    delete f;
+    return rc;
+  };
+  // extents of every source buffer the records use
+  struct Ext { int64_t lo = INT64_MAX, hi = 0; };
+  std::vector<Ext> se(kFqMaxBufs), qe(kFqMaxBufs);
+  Ext ne;
+  uint64_t total = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    const int s = in->seq_sel[i], q = in->qual_sel[i];
+    const int64_t L = in->seq_len[i], Q = in->qual_len[i], NL = in->name_len[i];
+    if (s >= nsb || q >= nqb || L < 0 || Q < 0 || NL < 0 || NL > 0xFFFF || in->seq_nib_off[i] < 0 ||
+        in->qual_off[i] < 0 || in->name_off[i] < 0)
+      return bail(fail(ctx, GANON_E_ARG, "record %lld: bad buffer, length or offset", (long long)i));
+    if (L) {
+      se[s].lo = std::min(se[s].lo, in->seq_nib_off[i] >> 1);
+      se[s].hi = std::max(se[s].hi, (in->seq_nib_off[i] + L + 1) >> 1);
+    }
+    if (Q) {
+      qe[q].lo = std::min(qe[q].lo, in->qual_off[i]);
+      qe[q].hi = std::max(qe[q].hi, in->qual_off[i] + Q);
+    }
+    if (NL) {
+      ne.lo = std::min(ne.lo, in->name_off[i]);
+      ne.hi = std::max(ne.hi, in->name_off[i] + NL);
+    }
+    const uint64_t rl = (uint64_t)(8 + NL + L + Q);
+    if (rl > UINT32_MAX) return bail(fail(ctx, GANON_E_ARG, "record %lld longer than 4 GiB", (long long)i));
+    total += rl;
+  }
+  if (ne.lo == INT64_MAX) ne.lo = ne.hi = 0;
+  for (auto &e : se) if (e.lo == INT64_MAX) e.lo = e.hi = 0;
+  for (auto &e : qe) if (e.lo == INT64_MAX) e.lo = e.hi = 0;
+  int rc;
+  // sources: device batch buffers (no copy) or the used slice of each host buffer
+  int64_t seq_base[kFqMaxBufs] = {0, 0, 0, 0};
+  if (in->seq_batch) {
+    const uint8_t *din = nullptr, *dout = nullptr;
+    int64_t bytes = 0;
+    if ((rc = ganon_dbatch_seq_buffers(in->seq_batch, &din, &dout, &bytes))) return bail(fail(ctx, rc, "bad batch"));
+    if (nsb > 2) return bail(fail(ctx, GANON_E_ARG, "a device batch provides two sequence buffers"));
+    for (int s = 0; s < nsb; ++s)
+      if (se[s].hi > bytes) return bail(fail(ctx, GANON_E_ARG, "sequence offset past the batch buffer"));
+    f->bufs.seq[0] = dout;
+    f->bufs.seq[1] = din;
+  } else {
+    if (!in->seq_buf) return bail(fail(ctx, GANON_E_ARG, "no sequence buffers"));
+    for (int s = 0; s < nsb; ++s) {
+      uint8_t *d = nullptr;
+      const int64_t sz = se[s].hi - se[s].lo;
+      if (sz && !in->seq_buf[s]) return bail(fail(ctx, GANON_E_ARG, "null sequence buffer %d", s));
+      if ((rc = fq_alloc(ctx, f, &d, (size_t)sz))) return bail(rc);
+      if (sz) HIP_OR_FAIL(hipMemcpyAsync(d, in->seq_buf[s] + se[s].lo, sz, hipMemcpyHostToDevice, ctx->stream));
+      f->bufs.seq[s] = d;
+      seq_base[s] = se[s].lo;
+    }
+  }
+  if (!in->qual_buf) return bail(fail(ctx, GANON_E_ARG, "no quality buffers"));
+  for (int q = 0; q < nqb; ++q) {
+    uint8_t *d = nullptr;
+    const int64_t sz = qe[q].hi - qe[q].lo;
+    if (sz && !in->qual_buf[q]) return bail(fail(ctx, GANON_E_ARG, "null quality buffer %d", q));
+    if ((rc = fq_alloc(ctx, f, &d, (size_t)sz))) return bail(rc);
+    if (sz) HIP_OR_FAIL(hipMemcpyAsync(d, in->qual_buf[q] + qe[q].lo, sz, hipMemcpyHostToDevice, ctx->stream));
+    f->bufs.qual[q] = d;
+  }
+  {
+    uint8_t *d = nullptr;
+    const int64_t sz = ne.hi - ne.lo;
+    if (sz && !in->names) return bail(fail(ctx, GANON_E_ARG, "null name blob"));
+    if ((rc = fq_alloc(ctx, f, &d, (size_t)sz))) return bail(rc);
+    if (sz) HIP_OR_FAIL(hipMemcpyAsync(d, in->names + ne.lo, sz, hipMemcpyHostToDevice, ctx->stream));
+    f->bufs.names = d;
+  }
+  for (int s = nsb; s < kFqMaxBufs; ++s) f->bufs.seq[s] = f->bufs.seq[0];
+  for (int q = nqb; q < kFqMaxBufs; ++q) f->bufs.qual[q] = f->bufs.qual[0];
+  // packed records and lengths (lengths padded to whole scan blocks with zeros)
+  f->nb = (n + kFqScanBlock - 1) / kFqScanBlock;
+  f->total = total;
+  f->n_tiles = (int64_t)((total + kFqTile - 1) / kFqTile);
+  std::vector<FqRec> rec((size_t)n);
+  std::vector<uint32_t> len((size_t)(f->nb * kFqScanBlock), 0u);
+  host_parallel(n, [&](int64_t a, int64_t b) {
+    for (int64_t i = a; i < b; ++i) {
+      const int s = in->seq_sel[i], q = in->qual_sel[i];
+      FqRec &R = rec[i];
+      R.seq = (uint64_t)(in->seq_nib_off[i] - 2 * seq_base[s]) | ((uint64_t)s << 56) |
+              ((uint64_t)(in->reverse[i] != 0) << 58) | ((uint64_t)(in->qual_rev[i] != 0) << 59);
+      R.qual = (uint64_t)(in->qual_off[i] - qe[q].lo) | ((uint64_t)in->mate[i] << 48) | ((uint64_t)q << 56);
+      R.name = (uint64_t)(in->name_len[i] ? in->name_off[i] - ne.lo : 0) | ((uint64_t)in->name_len[i] << 48);
+      R.len = (uint32_t)in->seq_len[i];
+      R.qlen = (uint32_t)in->qual_len[i];
+      len[i] = (uint32_t)(8 + in->name_len[i] + in->seq_len[i] + in->qual_len[i]);
+    }
+  });
+  if ((rc = fq_alloc(ctx, f, &f->recs, (size_t)n))) return bail(rc);
+  if ((rc = fq_alloc(ctx, f, &f->len, len.size()))) return bail(rc);
+  if ((rc = fq_alloc(ctx, f, &f->off, (size_t)n + 1))) return bail(rc);
+  if ((rc = fq_alloc(ctx, f, &f->tile_first, (size_t)f->n_tiles + 1))) return bail(rc);
+  if ((rc = fq_alloc(ctx, f, &f->bsum, (size_t)f->nb))) return bail(rc);
+  if ((rc = fq_alloc(ctx, f, &f->err, 1))) return bail(rc);
+  if ((rc = fq_alloc(ctx, f, &f->dense_list, (size_t)f->n_tiles))) return bail(rc);
+  if ((rc = fq_alloc(ctx, f, &f->dense_count, 1))) return bail(rc);
+  if ((rc = fq_alloc(ctx, f, &f->out, (size_t)f->n_tiles * kFqTile))) return bail(rc);
+  if (n) {
+    HIP_OR_FAIL(hipMemcpyAsync(f->recs, rec.data(), rec.size() * sizeof(FqRec), hipMemcpyHostToDevice, ctx->stream));
+    HIP_OR_FAIL(hipMemcpyAsync(f->len, len.data(), len.size() * sizeof(uint32_t), hipMemcpyHostToDevice, ctx->stream));
+  }
+  HIP_OR_FAIL(hipMemsetAsync(f->err, 0xFF, sizeof(unsigned long long), ctx->stream));
+  HIP_OR_FAIL(hipStreamSynchronize(ctx->stream));   // the host staging vectors die here
+  *out = f;
+  return GANON_OK;
+}
+
+GANON_API int ganon_fastq_run(ganon_ctx *ctx, ganon_fastq *f) {
+  if (!ctx || !f) return GANON_E_ARG;
+  if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, GANON_E_DEVICE, "hipSetDevice failed");
+  if (ctx->profiling) {
+    for (auto &r : ctx->recs) {
+      ctx->pool.push_back(r.e0);
+      ctx->pool.push_back(r.e1);
+    }
+    ctx->recs.clear();
+  }
+  if (f->n == 0) return GANON_OK;
+  int rc;
+  {
+    KernelScope ks(ctx, "k_fq_scan");
+    hipLaunchKernelGGL(k_fq_bsum, dim3((unsigned)f->nb), dim3(kFqThreads), 0, ctx->stream, f->len, f->bsum);
+    hipLaunchKernelGGL(k_fq_bscan, dim3(1), dim3(kFqScanThreads), 0, ctx->stream, f->bsum, f->nb, f->err,
+                       f->dense_count);
+    hipLaunchKernelGGL(k_fq_off, dim3((unsigned)f->nb), dim3(kFqThreads), 0, ctx->stream, f->len, f->bsum, f->n,
+                       f->off, f->tile_first);
+    if ((rc = check_launch(ctx, "k_fq_scan"))) return rc;
+  }
+  {
+    KernelScope ks(ctx, "k_fq_format");
+    auto kern = ctx->fq_kd == 1 ? k_fq_format<1> : ctx->fq_kd == 2 ? k_fq_format<2> : k_fq_format<4>;   // records per batch
+    hipLaunchKernelGGL(kern, dim3((unsigned)f->n_tiles), dim3(kFqThreads), 0, ctx->stream, f->bufs, f->recs,
+                       f->off, f->tile_first, f->n, f->total, f->out, f->err, ctx->fq_skip, f->dense_list,
+                       f->dense_count);
+    hipLaunchKernelGGL(k_fq_dense, dim3(kFqDenseGrid), dim3(kFqThreads), 0, ctx->stream, f->bufs, f->recs, f->off,
+                       f->tile_first, f->n, f->total, f->out, f->err, f->dense_list, f->dense_count);
+    if ((rc = check_launch(ctx, "k_fq_format"))) return rc;
+  }
+  return GANON_OK;
+}
+
+GANON_API int64_t ganon_fastq_bytes(const ganon_fastq *f) { return f ? (int64_t)f->total : -1; }
+
+GANON_API int ganon_fastq_device_output(const ganon_fastq *f, void **dev_ptr) {
+  if (!f || !dev_ptr) return GANON_E_ARG;
+  *dev_ptr = f->out;
+  return GANON_OK;
+}
+
+GANON_API int64_t ganon_fastq_download(ganon_ctx *ctx, ganon_fastq *f, char *out, int64_t cap) {
+  constexpr int64_t kFailed = GANON_FASTQ_FAILED;
+  if (!ctx || !f || (!out && f->total)) return kFailed;
+  if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, GANON_E_DEVICE, "hipSetDevice failed"), kFailed;
+  unsigned long long bad = ~0ull;
+  if (f->n && hipMemcpyAsync(&bad, f->err, sizeof bad, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess)
+    return fail(ctx, GANON_E_DEVICE, "error-slot copy failed"), kFailed;
+  if (hipStreamSynchronize(ctx->stream) != hipSuccess) return fail(ctx, GANON_E_DEVICE, "formatter run failed"), kFailed;
+  if (bad != ~0ull) {
+    fail(ctx, GANON_E_ARG, "record %llu: reverse read with a base outside ACGTN (SURVEY Q7)", bad);
+    return -(int64_t)bad - 1;
+  }
+  if ((int64_t)f->total > cap) {
+    fail(ctx, GANON_E_ARG, "output buffer too small (%llu bytes needed)", (unsigned long long)f->total);
+    return INT64_MIN;
+  }
+  if (f->total && (hipMemcpyAsync(out, f->out, f->total, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+                   hipStreamSynchronize(ctx->stream) != hipSuccess))
+    return fail(ctx, GANON_E_DEVICE, "output copy failed"), kFailed;
+  return (int64_t)f->total;
+}
+
+GANON_API int ganon_fastq_free(ganon_ctx *ctx, ganon_fastq *f) {
+  if (!f) return GANON_E_ARG;
+  if (ctx) hipSetDevice(ctx->device);
+  fq_release(f);
+  delete f;
+  return GANON_OK;
+}
+
+GANON_API int64_t ganon_fastq_format_hip(ganon_ctx *ctx, int64_t n, const uint8_t *const *seq_buf,
+                                         const uint8_t *seq_sel, const int64_t *seq_nib_off, const int32_t *seq_len,
+                                         const uint8_t *reverse, const uint8_t *const *qual_buf,
+                                         const uint8_t *qual_sel, const int64_t *qual_off, const int32_t *qual_len,
+                                         const uint8_t *qual_rev, const char *names, const int64_t *name_off,
+                                         const int32_t *name_len, const uint8_t *mate, char *out, int64_t cap) {
+  if (!ctx || n < 0) return GANON_FASTQ_FAILED;
+  ganon_fastq_records r{};
+  r.n = n;
+  int ms = 0, mq = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    ms = std::max<int>(ms, seq_sel[i]);
+    mq = std::max<int>(mq, qual_sel[i]);
+  }
+  r.n_seq_bufs = ms + 1;
+  r.n_qual_bufs = mq + 1;
+  r.seq_buf = seq_buf;
+  r.seq_sel = seq_sel;
+  r.seq_nib_off = seq_nib_off;
+  r.seq_len = seq_len;
+  r.reverse = reverse;
+  r.qual_buf = qual_buf;
+  r.qual_sel = qual_sel;
+  r.qual_off = qual_off;
+  r.qual_len = qual_len;
+  r.qual_rev = qual_rev;
+  r.names = names;
+  r.name_off = name_off;
+  r.name_len = name_len;
+  r.mate = mate;
+  ganon_fastq *f = nullptr;
+  if (ganon_fastq_upload(ctx, &r, &f)) return GANON_FASTQ_FAILED;
+  const int64_t w = ganon_fastq_run(ctx, f) ? GANON_FASTQ_FAILED : ganon_fastq_download(ctx, f, out, cap);
+  ganon_fastq_free(ctx, f);
+  return w;
+}

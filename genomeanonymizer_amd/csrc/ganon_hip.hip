@@ -32,6 +32,7 @@
 #include <vector>
 
 #include "../../include/ganon.h"
+#include "ganon_ctx.h"
 
 namespace {
 
@@ -1769,24 +1770,9 @@ __global__ void __launch_bounds__(kBlock) k_totals(const int32_t *__restrict__ c
 
 // ---- host side ---------------------------------------------------------------------------
 
-struct ganon_ctx {
-  int device = 0;
-  hipStream_t own = nullptr;
-  hipStream_t stream = nullptr;
-  bool profiling = false;
-  int variant = GANON_VARIANT_DEFAULT;
-  int v3_blocks[2] = {1, 1};   // resident grid of k_scope_v3 per class (occupancy x CUs)
-  int group_unroll = 2;        // GANON_PARAM_GROUP_UNROLL
-  int group_skip = 0;          // GANON_PARAM_GROUP_SKIP (profiling only)
-  int group_target = kGrpTarget;   // GANON_PARAM_GROUP_TARGET
-  int nt_copy = 1;             // GANON_PARAM_NT_COPY
-  int ref2 = 1;                // GANON_PARAM_REF2
-  std::string err;
-  struct Rec { std::string name; hipEvent_t e0, e1; };
-  std::vector<Rec> recs;
-  std::vector<hipEvent_t> pool;
-  std::vector<ganon_kernel_time> last_times;
-};
+using ganon_detail::check_launch;
+using ganon_detail::fail;
+using ganon_detail::KernelScope;
 
 struct ganon_dbatch {
   DevBatch B{};
@@ -1835,22 +1821,6 @@ struct ganon_dbatch {
 
 namespace {
 
-int fail(ganon_ctx *ctx, int code, const char *fmt, ...) {
-  char buf[512];
-  va_list ap;
-  va_start(ap, fmt);
-  vsnprintf(buf, sizeof buf, fmt, ap);
-  va_end(ap);
-  if (ctx) ctx->err = buf;
-  return code;
-}
-
-#define HIP_OR_FAIL(call)                                                                  \
-  do {                                                                                     \
-    hipError_t e_ = (call);                                                                \
-    if (e_ != hipSuccess)                                                                  \
-      return fail(ctx, GANON_E_DEVICE, "%s failed: %s", #call, hipGetErrorString(e_));     \
-  } while (0)
 
 template <typename T>
 int dev_alloc(ganon_ctx *ctx, ganon_dbatch *db, T **p, size_t count) {
@@ -1886,40 +1856,6 @@ size_t small_lds_bytes(int tb, int cap) {
 }
 
 size_t tile_lds_bytes(int tb) { return (size_t)kTile * tb + kTile / 2 + 16 * sizeof(int); }
-
-hipEvent_t get_event(ganon_ctx *ctx) {
-  if (!ctx->pool.empty()) {
-    hipEvent_t e = ctx->pool.back();
-    ctx->pool.pop_back();
-    return e;
-  }
-  hipEvent_t e = nullptr;
-  hipEventCreate(&e);
-  return e;
-}
-
-struct KernelScope {
-  ganon_ctx *ctx;
-  ganon_ctx::Rec rec;
-  KernelScope(ganon_ctx *c, const char *name) : ctx(c) {
-    if (!ctx->profiling) return;
-    rec.name = name;
-    rec.e0 = get_event(ctx);
-    rec.e1 = get_event(ctx);
-    hipEventRecord(rec.e0, ctx->stream);
-  }
-  ~KernelScope() {
-    if (!ctx->profiling) return;
-    hipEventRecord(rec.e1, ctx->stream);
-    ctx->recs.push_back(rec);
-  }
-};
-
-int check_launch(ganon_ctx *ctx, const char *what) {
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return fail(ctx, GANON_E_DEVICE, "launch of %s failed: %s", what, hipGetErrorString(e));
-  return GANON_OK;
-}
 
 }  // namespace
 
@@ -2012,6 +1948,15 @@ GANON_API int ganon_ctx_set_param(ganon_ctx *ctx, int param, int value) {
   }
   if (param == GANON_PARAM_REF2) {
     ctx->ref2 = value != 0;
+    return GANON_OK;
+  }
+  if (param == GANON_PARAM_FASTQ_SKIP) {
+    ctx->fq_skip = value & 31;
+    return GANON_OK;
+  }
+  if (param == GANON_PARAM_FASTQ_KD) {
+    if (value != 1 && value != 2 && value != 4) return fail(ctx, GANON_E_ARG, "FASTQ dwords per lane: 1, 2 or 4");
+    ctx->fq_kd = value;
     return GANON_OK;
   }
   if (param == GANON_PARAM_NT_COPY) {
@@ -2691,6 +2636,14 @@ GANON_API int ganon_batch_info(ganon_dbatch *db, int64_t *info) {
   info[5] = db->n_large_written;
   info[6] = db->max_small_span;
   info[7] = db->tn_entries;
+  return GANON_OK;
+}
+
+int ganon_dbatch_seq_buffers(const ganon_dbatch *db, const uint8_t **in, const uint8_t **out, int64_t *bytes) {
+  if (!db) return GANON_E_ARG;
+  *in = db->B.seq;
+  *out = db->out;
+  *bytes = db->seq_bytes;
   return GANON_OK;
 }
 

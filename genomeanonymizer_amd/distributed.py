@@ -94,7 +94,7 @@ def anonymize_genome_sharded(windows: List[Window], tumor_bam: str, normal_bam: 
         dist.barrier()
     if rank == 0:
         merged = _merge_shards(plan, tables, res, workdir, world)
-        write_fastqs(plan, merged, tables, (tumor_out, normal_out))
+        write_fastqs(plan, merged, tables, (tumor_out, normal_out), backend=anonymizer.format_fastq)
         if record_statistics:
             write_statistics(f"{normal_bam}.statistics.txt", statistics_rows(plan, merged))
     if dist is not None:

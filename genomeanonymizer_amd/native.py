@@ -1,6 +1,7 @@
 """ctypes bindings of the two in-tree native libraries.
 
-* ``libganon_hip.so`` (include/ganon.h): the HIP masking kernels. There is no CPU
+* ``libganon_hip.so`` (include/ganon.h): the HIP masking kernels and the HIP FASTQ
+  formatter (``ganon_fastq_*``). There is no CPU
   implementation behind it; loading or creating a context fails loudly without a gfx950
   device (``GanonError``), never falls back.
 * ``libganon_host.so`` (include/ganon_host.h): BAM decoder and FASTQ formatter.
@@ -45,6 +46,17 @@ class GanonBatch(C.Structure):
         ("scope_incid_off", _i64p), ("incid_read", _i32p), ("scope_span_start", _i32p),
         ("scope_span_len", _i32p), ("scope_ref_off", _i64p), ("ref_nt16", _u8p),
         ("keep_pos", _i32p), ("keep_code", _u8p),
+    ]
+
+
+class GanonFastqRecords(C.Structure):
+    """Mirror of ``ganon_fastq_records`` (include/ganon.h)."""
+    _fields_ = [
+        ("n", C.c_int64), ("n_seq_bufs", C.c_int32), ("n_qual_bufs", C.c_int32),
+        ("seq_buf", C.POINTER(_u8p)), ("seq_batch", _p), ("seq_sel", _u8p), ("seq_nib_off", _i64p),
+        ("seq_len", _i32p), ("reverse", _u8p), ("qual_buf", C.POINTER(_u8p)), ("qual_sel", _u8p),
+        ("qual_off", _i64p), ("qual_len", _i32p), ("qual_rev", _u8p), ("names", C.c_char_p),
+        ("name_off", _i64p), ("name_len", _i32p), ("mate", _u8p),
     ]
 
 
@@ -113,7 +125,19 @@ def hip_lib():
     lib.ganon_batch_copy_totals.argtypes = [_p, _p, _p]
     lib.ganon_last_kernel_times.argtypes = [_p, C.POINTER(KernelTime), C.c_int]
     lib.ganon_batch_info.argtypes = [_p, _i64p]
-    if lib.ganon_abi_version() != 1:
+    lib.ganon_fastq_upload.argtypes = [_p, C.POINTER(GanonFastqRecords), C.POINTER(_p)]
+    lib.ganon_fastq_run.argtypes = [_p, _p]
+    lib.ganon_fastq_bytes.argtypes = [_p]
+    lib.ganon_fastq_bytes.restype = C.c_int64
+    lib.ganon_fastq_device_output.argtypes = [_p, C.POINTER(_p)]
+    lib.ganon_fastq_download.argtypes = [_p, _p, C.c_char_p, C.c_int64]
+    lib.ganon_fastq_download.restype = C.c_int64
+    lib.ganon_fastq_free.argtypes = [_p, _p]
+    lib.ganon_fastq_format_hip.restype = C.c_int64
+    lib.ganon_fastq_format_hip.argtypes = [_p, C.c_int64, C.POINTER(_u8p), _u8p, _i64p, _i32p, _u8p,
+                                           C.POINTER(_u8p), _u8p, _i64p, _i32p, _u8p, C.c_char_p, _i64p,
+                                           _i32p, _u8p, C.c_char_p, C.c_int64]
+    if lib.ganon_abi_version() != 2:
         raise GanonError("libganon_hip.so ABI version mismatch")
     _hip = lib
     return lib
@@ -124,12 +148,16 @@ PARAM_GROUP_SKIP = 2     # include/ganon.h GANON_PARAM_GROUP_SKIP (phase timing 
 PARAM_GROUP_TARGET = 3   # include/ganon.h GANON_PARAM_GROUP_TARGET (segments per group, at upload)
 PARAM_NT_COPY = 4        # include/ganon.h GANON_PARAM_NT_COPY
 PARAM_REF2 = 5           # include/ganon.h GANON_PARAM_REF2
+PARAM_FASTQ_SKIP = 6     # include/ganon.h GANON_PARAM_FASTQ_SKIP (phase timing only)
+PARAM_FASTQ_KD = 7       # include/ganon.h GANON_PARAM_FASTQ_KD
 
 EXPORTED_HIP_SYMBOLS = (
     "ganon_ctx_create", "ganon_ctx_destroy", "ganon_last_error", "ganon_abi_version",
     "ganon_ctx_set_stream", "ganon_ctx_set_profiling", "ganon_ctx_set_variant", "ganon_ctx_set_param", "ganon_mask_batch", "ganon_batch_upload",
     "ganon_batch_run", "ganon_batch_sync", "ganon_batch_download", "ganon_batch_free",
     "ganon_batch_device_totals", "ganon_batch_copy_totals", "ganon_last_kernel_times", "ganon_batch_info",
+    "ganon_fastq_upload", "ganon_fastq_run", "ganon_fastq_bytes", "ganon_fastq_device_output",
+    "ganon_fastq_download", "ganon_fastq_free", "ganon_fastq_format_hip",
 )
 EXPORTED_HOST_SYMBOLS = (
     "ganon_bam_open", "ganon_bam_view_get", "ganon_bam_error", "ganon_bam_close",
@@ -202,6 +230,142 @@ class HipMasker:
         h = _p()
         self._check(self._lib.ganon_batch_upload(self._h, C.byref(b), C.byref(h)), "ganon_batch_upload")
         return DeviceBatch(self, h, b.seq_bytes, b.n_scopes)
+
+    # -- FASTQ formatter -------------------------------------------------------------------
+    def fastq_upload(self, recs: dict, seq_batch: "DeviceBatch" = None) -> "DeviceFastq":
+        """Upload a record set (``fastq_records`` layout); with ``seq_batch`` the sequences are
+        read from that device batch (buffer 0 = masked output, 1 = input) without a copy."""
+        c, keep = _c_fastq_records(recs, seq_batch)
+        h = _p()
+        self._check(self._lib.ganon_fastq_upload(self._h, C.byref(c), C.byref(h)), "ganon_fastq_upload")
+        del keep
+        return DeviceFastq(self, h)
+
+    def format_fastq(self, recs: dict) -> bytes:
+        """One-shot ``ganon_fastq_format_hip`` (the host formatter's arguments)."""
+        a = _fastq_args(recs)
+        n_bytes = fastq_bytes(recs)
+        out = C.create_string_buffer(max(n_bytes, 1))
+        w = self._lib.ganon_fastq_format_hip(self._h, *a, out, n_bytes)
+        return out.raw[:_fastq_result(w, lambda: self._lib.ganon_last_error(self._h).decode(errors="replace"))]
+
+
+class FastqBadRecord(GanonError):
+    """A reverse read with a base outside ACGTN (the reference's KeyError)."""
+
+    def __init__(self, index: int, msg: str):
+        super().__init__(msg)
+        self.index = index
+
+
+FASTQ_FAILED = -(1 << 63) + 1   # include/ganon.h GANON_FASTQ_FAILED
+
+
+def _fastq_result(w: int, err) -> int:
+    if w >= 0:
+        return w
+    if w == -(1 << 63):
+        raise GanonError("FASTQ output buffer too small")
+    if w == FASTQ_FAILED:
+        raise GanonError(f"FASTQ formatter failed: {err()}")
+    raise FastqBadRecord(-w - 1, f"record {-w - 1}: reverse read with a base outside ACGTN (SURVEY Q7)")
+
+
+FASTQ_ARRAYS = {"seq_sel": np.uint8, "seq_nib_off": np.int64, "seq_len": np.int32, "reverse": np.uint8,
+                "qual_sel": np.uint8, "qual_off": np.int64, "qual_len": np.int32, "qual_rev": np.uint8,
+                "name_off": np.int64, "name_len": np.int32, "mate": np.uint8}
+
+
+def fastq_bytes(recs: dict) -> int:
+    return int(8 * len(recs["seq_len"]) + recs["name_len"].sum(dtype=np.int64) +
+               recs["seq_len"].sum(dtype=np.int64) + recs["qual_len"].sum(dtype=np.int64))
+
+
+def _check_fastq(recs: dict) -> None:
+    for k, dt in FASTQ_ARRAYS.items():
+        a = recs[k]
+        if a.dtype != dt or not a.flags["C_CONTIGUOUS"]:
+            raise GanonError(f"FASTQ record array {k} must be C-contiguous {np.dtype(dt)}")
+
+
+def _fastq_args(recs: dict) -> tuple:
+    """The host formatter's argument list (minus out/cap) over a ``fastq_records`` dict."""
+    _check_fastq(recs)
+    seq_ptrs = (_u8p * len(recs["seq_bufs"]))(*[b.ctypes.data_as(_u8p) for b in recs["seq_bufs"]])
+    qual_ptrs = (_u8p * len(recs["qual_bufs"]))(*[b.ctypes.data_as(_u8p) for b in recs["qual_bufs"]])
+    P = lambda k, t: recs[k].ctypes.data_as(t)
+    return (len(recs["seq_len"]), seq_ptrs, P("seq_sel", _u8p), P("seq_nib_off", _i64p), P("seq_len", _i32p),
+            P("reverse", _u8p), qual_ptrs, P("qual_sel", _u8p), P("qual_off", _i64p), P("qual_len", _i32p),
+            P("qual_rev", _u8p), bytes(recs["names"]), P("name_off", _i64p), P("name_len", _i32p),
+            P("mate", _u8p))
+
+
+def _c_fastq_records(recs: dict, seq_batch=None):
+    _check_fastq(recs)
+    c = GanonFastqRecords()
+    c.n = len(recs["seq_len"])
+    nsb = 2 if seq_batch is not None else len(recs["seq_bufs"])
+    c.n_seq_bufs, c.n_qual_bufs = nsb, len(recs["qual_bufs"])
+    keep = []
+    if seq_batch is None:
+        sp = (_u8p * nsb)(*[b.ctypes.data_as(_u8p) for b in recs["seq_bufs"]])
+        keep.append(sp)
+        c.seq_buf = sp
+    else:
+        c.seq_batch = seq_batch.h
+    qp = (_u8p * len(recs["qual_bufs"]))(*[b.ctypes.data_as(_u8p) for b in recs["qual_bufs"]])
+    keep.append(qp)
+    c.qual_buf = qp
+    names = bytes(recs["names"])
+    keep.append(names)
+    c.names = names
+    for k, dt in FASTQ_ARRAYS.items():
+        setattr(c, k, recs[k].ctypes.data_as(_PTR_OF[dt]))
+    return c, keep
+
+
+def host_format_fastq(recs: dict) -> bytes:
+    """libganon_host.so ganon_fastq_format over a ``fastq_records`` dict (same contract)."""
+    a = _fastq_args(recs)
+    n_bytes = fastq_bytes(recs)
+    out = C.create_string_buffer(max(n_bytes, 1))
+    w = host_lib().ganon_fastq_format(*a, out, n_bytes)
+    return out.raw[:_fastq_result(w, lambda: "host formatter")]
+
+
+class DeviceFastq:
+    """A record set resident on the device (ganon_fastq_upload)."""
+
+    def __init__(self, masker: HipMasker, handle):
+        self.m = masker
+        self.h = handle
+        self.n_bytes = int(masker._lib.ganon_fastq_bytes(handle))
+
+    def run(self) -> None:
+        self.m._check(self.m._lib.ganon_fastq_run(self.m._h, self.h), "ganon_fastq_run")
+
+    def sync(self) -> None:
+        self.m._check(self.m._lib.ganon_batch_sync(self.m._h), "ganon_batch_sync")
+
+    def device_output_ptr(self) -> int:
+        p = _p()
+        self.m._check(self.m._lib.ganon_fastq_device_output(self.h, C.byref(p)), "fastq_device_output")
+        return p.value
+
+    def download(self) -> bytes:
+        out = C.create_string_buffer(max(self.n_bytes, 1))
+        w = self.m._lib.ganon_fastq_download(self.m._h, self.h, out, self.n_bytes)
+        return out.raw[:_fastq_result(w, lambda: self.m._lib.ganon_last_error(self.m._h).decode(errors="replace"))]
+
+    def kernel_times(self) -> list:
+        arr = (KernelTime * 32)()
+        n = self.m._lib.ganon_last_kernel_times(self.m._h, arr, 32)
+        return [(arr[i].name.decode(), int(arr[i].launches), float(arr[i].ms)) for i in range(min(n, 32))]
+
+    def free(self) -> None:
+        if self.h:
+            self.m._lib.ganon_fastq_free(self.m._h, self.h)
+            self.h = None
 
 
 class DeviceBatch:

@@ -50,7 +50,8 @@ def anonymize_genome(windows_in_sample: List[Window], tumor_bam_file: str, norma
     t2 = time.time()
     res = anonymizer.anonymize(planner, plan)
     t3 = time.time()
-    write_fastqs(plan, res, (tumor, normal), (tumor_output_fastq, normal_output_fastq))
+    write_fastqs(plan, res, (tumor, normal), (tumor_output_fastq, normal_output_fastq),
+                 backend=anonymizer.format_fastq)
     if record_statistics:
         write_statistics(f"{normal_bam_file}.statistics.txt", statistics_rows(plan, res))
     t4 = time.time()

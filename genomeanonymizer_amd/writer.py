@@ -5,13 +5,13 @@
   ``AnonymizedRead.get_anonymized_fastq_record`` (anonymizer_methods.py:205-243):
   ``@name/1|2``, the upper-cased (masked) sequence, reverse-complemented for reverse reads,
   and the qualities printed in the BAM's stored order for every read (they are
-  loaded forward-oriented and reversed once more on output). Bulk formatting runs in
-  libganon_host.so; the rare indel-edited records are formatted here.
+  loaded forward-oriented and reversed once more on output). Bulk formatting runs on the
+  GPU (``ganon_fastq_format_hip`` through the masking engine) or in libganon_host.so; the
+  rare indel-edited records are formatted here.
 * the statistics file of ``AnonymizedVariantsStatistics.write_statistics`` (SR:175-242).
 """
 from __future__ import annotations
 
-import ctypes as C
 import itertools
 from typing import Dict, List, Sequence, Tuple
 
@@ -40,18 +40,21 @@ def _decode(buf: np.ndarray, nib0: int, n: int) -> bytearray:
 
 
 class FastqFormatter:
-    def __init__(self, tables: Tuple[ReadTable, ReadTable], res: MaskResult):
+    """Formats record runs through ``backend`` (a ``native.fastq_records`` dict -> bytes): the
+    HIP formatter of the masking engine's device (``HipMasker.format_fastq``) in the product,
+    the host library's ``ganon_fastq_format`` when no engine formatter is given."""
+
+    def __init__(self, tables: Tuple[ReadTable, ReadTable], res: MaskResult, backend=None):
         self.tables = tables
         self.res = res
-        self.lib = native.host_lib()
+        self.backend = backend or native.host_format_fastq
         # buffers: 0 = device output, 1 = tumor BAM seq, 2 = normal BAM seq
         self._seq_bufs = [res.seq_out, tables[0].seq, tables[1].seq]
         self._qual_bufs = [tables[0].qual, tables[1].qual]
 
-    def _native(self, recs: Sequence[Tuple[int, int, int]]) -> bytes:
+    def records(self, recs: Sequence[Tuple[int, int, int]]) -> dict:
+        """The record arrays of instances ``(dataset, row, write scope | -1)``."""
         n = len(recs)
-        if n == 0:
-            return b""
         T, N = self.tables
         ds = np.fromiter((r[0] for r in recs), np.int64, n)
         row = np.fromiter((r[1] for r in recs), np.int64, n)
@@ -60,41 +63,31 @@ class FastqFormatter:
         seq_off_t = np.where(ds == 0, T.seq_off[np.where(ds == 0, row, 0)], N.seq_off[np.where(ds == 1, row, 0)])
         base = np.where(ds == 0, self.res.seq_base[0], self.res.seq_base[1])
         byte_off = np.where(sc >= 0, base + seq_off_t, seq_off_t)
-        nib_off = (2 * byte_off).astype(np.int64)
         pick = lambda f, dt: np.where(ds == 0, getattr(T, f)[np.where(ds == 0, row, 0)],
                                       getattr(N, f)[np.where(ds == 1, row, 0)]).astype(dt)
         seq_len = pick("l_seq", np.int32)
-        reverse = pick("is_reverse", np.uint8)
-        qual_off = pick("qual_off", np.int64)
         flag = pick("flag", np.int64)
-        mate = np.where(flag & 0x40, 1, 2).astype(np.uint8)
-        qual_sel = ds.astype(np.uint8)
-        qual_rev = np.zeros(n, np.uint8)
-        # names: one blob for this call
-        names = [self.tables[d].names[r] for d, r, _ in recs]
-        enc = [s.encode() for s in names]
+        enc = [self.tables[d].names[r].encode() for d, r, _ in recs]
         name_len = np.array([len(e) for e in enc], np.int32)
-        name_off = np.concatenate([[0], np.cumsum(name_len)[:-1]]).astype(np.int64)
-        blob = b"".join(enc)
-        cap = int(np.sum(name_len) + 2 * np.sum(seq_len) + 8 * n + 16)
-        out = C.create_string_buffer(cap)
-        u8p = C.POINTER(C.c_uint8)
-        seq_ptrs = (u8p * 3)(*[b.ctypes.data_as(u8p) for b in self._seq_bufs])
-        qual_ptrs = (u8p * 2)(*[b.ctypes.data_as(u8p) for b in self._qual_bufs])
-        P = lambda a, t: a.ctypes.data_as(C.POINTER(t))
-        w = self.lib.ganon_fastq_format(
-            n, seq_ptrs, P(seq_sel, C.c_uint8), P(nib_off, C.c_int64), P(seq_len, C.c_int32),
-            P(reverse, C.c_uint8), qual_ptrs, P(qual_sel, C.c_uint8), P(qual_off, C.c_int64),
-            P(seq_len, C.c_int32), P(qual_rev, C.c_uint8), blob, P(name_off, C.c_int64),
-            P(name_len, C.c_int32), P(mate, C.c_uint8), out, cap)
-        if w < 0:
-            if w == -(1 << 63):
-                raise RuntimeError("FASTQ buffer too small")
-            i = -w - 1
-            d, r, _ = recs[i]
+        return {
+            "seq_bufs": self._seq_bufs, "seq_sel": seq_sel, "seq_nib_off": (2 * byte_off).astype(np.int64),
+            "seq_len": seq_len, "reverse": pick("is_reverse", np.uint8),
+            "qual_bufs": self._qual_bufs, "qual_sel": ds.astype(np.uint8), "qual_off": pick("qual_off", np.int64),
+            "qual_len": seq_len.copy(), "qual_rev": np.zeros(n, np.uint8),   # stored order for every read (Q1)
+            "names": b"".join(enc), "name_len": name_len,
+            "name_off": np.concatenate([[0], np.cumsum(name_len)[:-1]]).astype(np.int64),
+            "mate": np.where(flag & 0x40, 1, 2).astype(np.uint8),
+        }
+
+    def _native(self, recs: Sequence[Tuple[int, int, int]]) -> bytes:
+        if len(recs) == 0:
+            return b""
+        try:
+            return self.backend(self.records(recs))
+        except native.FastqBadRecord as e:
+            d, r, _ = recs[e.index]
             raise TypeError(f"reverse read {self.tables[d].names[r]!r} has a base outside ACGTN: the "
-                            "reference's reverse complement fails on it (SURVEY Q7)")
-        return out.raw[:w]
+                            "reference's reverse complement fails on it (SURVEY Q7)") from None
 
     def _edited(self, inst, edits) -> bytes:
         ds, row, sc = inst
@@ -225,9 +218,9 @@ def io_block_size(directory: str) -> int:
 
 
 def write_fastqs(plan: Plan, res: MaskResult, tables, prefixes: Tuple[str, str],
-                 block_size: int = None) -> Dict[str, int]:
+                 block_size: int = None, backend=None) -> Dict[str, int]:
     import os
-    fmt = FastqFormatter(tables, res)
+    fmt = FastqFormatter(tables, res, backend)
     if block_size is None:
         block_size = io_block_size(os.path.dirname(os.path.abspath(prefixes[0])))
     edited = {inst: fmt._edited(inst, e) for inst, e in res.leftovers.items()}

@@ -35,7 +35,7 @@
 #define GANON_API __attribute__((visibility("default")))
 #endif
 
-#define GANON_ABI_VERSION 1
+#define GANON_ABI_VERSION 2
 
 enum {
   GANON_OK = 0,
@@ -121,9 +121,12 @@ GANON_API int ganon_ctx_set_variant(ganon_ctx *ctx, int variant);
  * Keep it 0 in production. GANON_PARAM_GROUP_TARGET: segments per scope group (read at
  * upload; default 256). GANON_PARAM_NT_COPY: non-temporal stores for the fused partition copy
  * (default 1). GANON_PARAM_REF2: group kernels read a 2-bit copy of the reference for segments
- * whose reference range is all ACGT (1, default) or the nt16 reference only (0). */
+ * whose reference range is all ACGT (1, default) or the nt16 reference only (0).
+ * GANON_PARAM_FASTQ_KD: output dwords per lane the FASTQ formatter loads at once (1, 2, 4).
+ * GANON_PARAM_FASTQ_SKIP (phase timing only, changes results): bit 0 leaves out the
+ * formatter's source loads, bit 1 its stores, bit 2 its tile writes in LDS. */
 enum { GANON_PARAM_GROUP_UNROLL = 1, GANON_PARAM_GROUP_SKIP = 2, GANON_PARAM_GROUP_TARGET = 3,
-       GANON_PARAM_NT_COPY = 4, GANON_PARAM_REF2 = 5 };
+       GANON_PARAM_NT_COPY = 4, GANON_PARAM_REF2 = 5, GANON_PARAM_FASTQ_SKIP = 6, GANON_PARAM_FASTQ_KD = 7 };
 GANON_API int ganon_ctx_set_param(ganon_ctx *ctx, int param, int value);
 /* When on, ganon_batch_run records a HIP event pair around each kernel it launches. */
 GANON_API int ganon_ctx_set_profiling(ganon_ctx *ctx, int enabled);
@@ -161,5 +164,63 @@ GANON_API int ganon_last_kernel_times(ganon_ctx *ctx, ganon_kernel_time *out, in
 /* Work-list summary of an uploaded batch: [small_scopes, wide?, large_scopes, large_tiles,
  * passthrough_reads, large_written_reads, max_small_span, 0]. */
 GANON_API int ganon_batch_info(ganon_dbatch *db, int64_t *info8);
+
+/* ---- FASTQ record formatter ------------------------------------------
+ * Replaces, for many reads at once, AnonymizedRead.get_anonymized_fastq_record
+ * (anonymizer_methods.py:215-243, with reverse_complement :205-213) and write_pair's record
+ * framing (short_read_tumor_normal_anonymizer.py:134-165). Record i is
+ *   '@' name '/' ('0' + mate) '\n' SEQ '\n' '+' '\n' QUAL '\n'
+ * SEQ: seq_len[i] nt16 nibbles from nibble seq_nib_off[i] of sequence buffer seq_sel[i], printed
+ *      as "=ACMGRSVTWYHKDBN"; when reverse[i], reverse-complemented with the reference's table
+ *      {A<->T, C<->G, N->N} — any other code is the reference's KeyError.
+ * QUAL: qual_len[i] bytes from qual_off[i] of quality buffer qual_sel[i], each + 33, in stored
+ *      order (qual_rev[i] == 0; the reference's output for every read) or reversed.
+ * Byte-identical to the host formatter ganon_fastq_format (include/ganon_host.h). */
+#define GANON_FASTQ_MAX_BUFS 4
+#define GANON_FASTQ_FAILED (INT64_MIN + 1)   /* device/argument failure, see ganon_last_error */
+typedef struct ganon_fastq ganon_fastq;   /* device-resident record batch */
+typedef struct ganon_fastq_records {
+  int64_t n;
+  int32_t n_seq_bufs, n_qual_bufs;           /* 1..GANON_FASTQ_MAX_BUFS each */
+  const uint8_t *const *seq_buf;             /* host nt16 buffers (ignored with seq_batch) */
+  const ganon_dbatch *seq_batch;             /* or: buffer 0 = the batch's masked output,
+                                                buffer 1 = its input, no copy */
+  const uint8_t *seq_sel;
+  const int64_t *seq_nib_off;
+  const int32_t *seq_len;
+  const uint8_t *reverse;
+  const uint8_t *const *qual_buf;            /* host raw phred buffers */
+  const uint8_t *qual_sel;
+  const int64_t *qual_off;
+  const int32_t *qual_len;
+  const uint8_t *qual_rev;
+  const char *names;                         /* host name blob */
+  const int64_t *name_off;
+  const int32_t *name_len;                   /* <= 65535 */
+  const uint8_t *mate;
+} ganon_fastq_records;
+/* Upload the records (and the used slices of the host buffers); synchronous. */
+GANON_API int ganon_fastq_upload(ganon_ctx *ctx, const ganon_fastq_records *records, ganon_fastq **out);
+/* Format on the device (async on the stream): offsets scan + one workgroup per 16 KiB tile. */
+GANON_API int ganon_fastq_run(ganon_ctx *ctx, ganon_fastq *f);
+/* Output size in bytes (sum of 8 + name + seq + qual lengths). */
+GANON_API int64_t ganon_fastq_bytes(const ganon_fastq *f);
+/* Device pointer of the formatted bytes (valid after run). */
+GANON_API int ganon_fastq_device_output(const ganon_fastq *f, void **dev_ptr);
+/* Synchronize and copy the output: returns the byte count, -(i+1) for the first bad record i
+ * (Q7), INT64_MIN when cap is too small, GANON_FASTQ_FAILED on other errors. */
+GANON_API int64_t ganon_fastq_download(ganon_ctx *ctx, ganon_fastq *f, char *out, int64_t cap);
+GANON_API int ganon_fastq_free(ganon_ctx *ctx, ganon_fastq *f);
+/* One-shot with exactly the arguments of the host formatter ganon_fastq_format
+ * (include/ganon_host.h): upload, run, download, free. Same return convention as
+ * ganon_fastq_download. */
+GANON_API int64_t ganon_fastq_format_hip(ganon_ctx *ctx, int64_t n, const uint8_t *const *seq_buf,
+                                         const uint8_t *seq_sel, const int64_t *seq_nib_off,
+                                         const int32_t *seq_len, const uint8_t *reverse,
+                                         const uint8_t *const *qual_buf, const uint8_t *qual_sel,
+                                         const int64_t *qual_off, const int32_t *qual_len,
+                                         const uint8_t *qual_rev, const char *names,
+                                         const int64_t *name_off, const int32_t *name_len,
+                                         const uint8_t *mate, char *out, int64_t cap);
 
 #endif /* GANON_H */

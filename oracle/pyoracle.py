@@ -30,6 +30,15 @@ class OracleEngine:
                                                 C.POINTER(C.c_int32), C.POINTER(C.c_int32),
                                                 C.POINTER(C.c_int64)]
 
+    def format_fastq(self, recs: dict) -> bytes:
+        """The FASTQ restatement (fastq_oracle.py) with HipMasker.format_fastq's contract."""
+        import fastq_oracle
+        from genomeanonymizer_amd.native import FastqBadRecord
+        try:
+            return fastq_oracle.format_records(recs)
+        except fastq_oracle.BadRecord as e:
+            raise FastqBadRecord(e.index, str(e)) from None
+
     def mask(self, arrays: dict):
         from genomeanonymizer_amd.native import make_c_batch
         b = make_c_batch(arrays)

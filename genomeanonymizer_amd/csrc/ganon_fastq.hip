@@ -429,20 +429,22 @@ __device__ __forceinline__ void fq_tile_by_records(uint8_t *smem, const FqBufs &
   }
 }
 
-// Per-tile record descriptors (LDS), one entry per record touching the tile, computed once
-// per record by one thread. Field f: 0 bases, 1 qualities, 2 name.
-struct FqDescs {
-  int64_t P0[kFqStage];              // tile position of the record's byte 0 (may be negative)
-  uint32_t NL[kFqStage], L[kFqStage], Q[kFqStage], fl[kFqStage];   // fl: rev | qrev << 1 | mate << 8
-  const uint8_t *nm[kFqStage], *sb[kFqStage], *qb[kFqStage];
-  uint64_t s0[kFqStage];             // first nibble of the bases in sb
-  int32_t td0[3][kFqStage];          // first interior tile dword of field f
-  uint16_t vs[3][kFqStage];          // first virtual dword of field f's interior
+// Per-tile field spans (LDS): field f (0 bases, 1 qualities, 2 name) of staged record k is
+// span f * kFqStage + k, written once by the record's thread.
+struct FqSpan {
+  uint64_t src;    // name / qualities: address of field byte 0; bases: 2 * buffer address + first nibble
+  int32_t j0;      // field index of byte 0 of the span's first tile dword (-3..)
+  uint32_t len;    // field length
+  uint16_t td0;    // first tile dword
+  uint16_t vs;     // first virtual dword
+  uint32_t flags;  // reverse | f << 1
 };
+static_assert(sizeof(FqSpan) == 24, "FqSpan layout");
 constexpr int kFqDw = kFqTile / 4;   // dwords per tile
+constexpr int kFqMap = 4096;         // virtual dwords: tile dwords + up to 3 shared edge dwords per record
+static_assert(kFqMap >= kFqDw + 3 * kFqStage, "virtual dword map");
 constexpr size_t kFqSmemA = kFqTile + kFqStage * sizeof(FqRec) + (kFqStage + 1) * sizeof(uint64_t);
-constexpr size_t kFqSmemB = kFqTile + kFqDw * sizeof(uint16_t) + sizeof(FqDescs);
-constexpr int kFqSpecial = 26;       // per record: 8 constant bytes + up to 6 edge bytes per field
+constexpr size_t kFqSmemB = kFqTile + kFqMap * sizeof(uint16_t) + 3 * kFqStage * sizeof(FqSpan);
 
 // Block-wide exclusive scan of a u64 (packed counters), 256 threads; returns the total too.
 __device__ __forceinline__ unsigned long long block_excl_scan(unsigned long long v, unsigned long long *s_w,
@@ -487,35 +489,46 @@ __global__ void __launch_bounds__(kFqThreads) k_fq_format(const FqBufs bufs, con
   }
   {
     const int ns = (int)(rl - r0 + 1);
-    uint16_t *map = reinterpret_cast<uint16_t *>(smem + kFqTile);   // virtual dword -> f << 8 | record
-    FqDescs &D = *reinterpret_cast<FqDescs *>(smem + kFqTile + kFqDw * sizeof(uint16_t));
-    // 1. descriptors, one thread per record, and the interior dword counts per field
+    uint16_t *map = reinterpret_cast<uint16_t *>(smem + kFqTile);   // virtual dword -> span
+    FqSpan *spans = reinterpret_cast<FqSpan *>(smem + kFqTile + kFqMap * sizeof(uint16_t));
+    // 1. zero tile and map; one thread per record: its three field spans (the tile dwords each
+    //    field touches — neighbouring fields share edge dwords, OR-ed together) and, once the
+    //    tile is zero, its 8 constant bytes
+    reinterpret_cast<uint4 *>(tile)[t] = make_uint4(0, 0, 0, 0);
+    reinterpret_cast<uint4 *>(tile)[t + kFqThreads] = make_uint4(0, 0, 0, 0);
     reinterpret_cast<uint4 *>(map)[t] = make_uint4(0, 0, 0, 0);
-    unsigned long long cnt = 0;   // interior dwords: bases | qualities << 16 | name << 32
-    int td[3] = {0, 0, 0};
+    reinterpret_cast<uint4 *>(map)[t + kFqThreads] = make_uint4(0, 0, 0, 0);
+    unsigned long long cnt = 0;   // dwords touched: bases | qualities << 16 | name << 32
+    FqSpan sp[3];
+    int64_t P0 = 0;
+    uint32_t NL = 0, L = 0, Q = 0, mate = 0;
     if (t < ns) {
       const FqRec R = recs[r0 + t];
-      const int64_t P0 = (int64_t)off[r0 + t] - (int64_t)t0;
-      const uint32_t NL = (uint32_t)(R.name >> 48), L = R.len, Q = R.qlen;
-      D.P0[t] = P0;
-      D.NL[t] = NL;
-      D.L[t] = L;
-      D.Q[t] = Q;
-      D.fl[t] = (uint32_t)((R.seq >> 58) & 1) | ((uint32_t)((R.seq >> 59) & 1) << 1) |
-                ((uint32_t)((R.qual >> 48) & 0xFF) << 8);
-      D.nm[t] = bufs.names + (R.name & kOff48);
-      D.sb[t] = pick4(bufs.seq, (uint32_t)(R.seq >> 56) & 3);
-      D.s0[t] = R.seq & kOff56;
-      D.qb[t] = pick4(bufs.qual, (uint32_t)(R.qual >> 56) & 3) + (R.qual & kOff48);
-      const FqField Fs = fq_field(P0, NL + 4, L), Fq = fq_field(P0, NL + 7 + L, Q), Fn = fq_field(P0, 1, NL);
-      const int cs = max(0, (Fs.ib - Fs.ia) >> 2), cq = max(0, (Fq.ib - Fq.ia) >> 2), cn = max(0, (Fn.ib - Fn.ia) >> 2);
-      td[0] = Fs.ia >> 2;
-      td[1] = Fq.ia >> 2;
-      td[2] = Fn.ia >> 2;
-      cnt = (unsigned long long)cs | ((unsigned long long)cq << 16) | ((unsigned long long)cn << 32);
+      P0 = (int64_t)off[r0 + t] - (int64_t)t0;
+      NL = (uint32_t)(R.name >> 48);
+      L = R.len;
+      Q = R.qlen;
+      mate = (uint32_t)((R.qual >> 48) & 0xFF);
+      const uint32_t fa[3] = {NL + 4, NL + 7 + L, 1u}, len[3] = {L, Q, NL};
+      const uint32_t rev[3] = {(uint32_t)(R.seq >> 58) & 1, (uint32_t)(R.seq >> 59) & 1, 0u};
+      const uint64_t src[3] = {2 * (uint64_t)(uintptr_t)pick4(bufs.seq, (uint32_t)(R.seq >> 56) & 3) + (R.seq & kOff56),
+                               (uint64_t)(uintptr_t)(pick4(bufs.qual, (uint32_t)(R.qual >> 56) & 3) + (R.qual & kOff48)),
+                               (uint64_t)(uintptr_t)(bufs.names + (R.name & kOff48))};
+#pragma unroll
+      for (int f = 0; f < 3; ++f) {
+        const FqField F = fq_field(P0, fa[f], len[f]);
+        const int d0 = F.a >> 2, d1 = (F.b + 3) >> 2;
+        sp[f].src = src[f];
+        sp[f].j0 = (int)(4 * (int64_t)d0 - (P0 + fa[f]));
+        sp[f].len = len[f];
+        sp[f].td0 = (uint16_t)d0;
+        sp[f].flags = rev[f] | (f << 1);
+        cnt |= (unsigned long long)(F.b > F.a ? d1 - d0 : 0) << (16 * f);
+      }
     }
     unsigned long long tot;
-    const unsigned long long pre = block_excl_scan(cnt, s_w, tot);
+    const unsigned long long pre = block_excl_scan(cnt, s_w, tot);   // (its barrier: tile and map are zero)
+    if (skip & 8) return;
     const int V0 = (int)(tot & 0xFFFF), V1 = V0 + (int)((tot >> 16) & 0xFFFF), V = V1 + (int)((tot >> 32) & 0xFFFF);
     if (t < ns) {
       const int base[3] = {0, V0, V1};
@@ -523,22 +536,32 @@ __global__ void __launch_bounds__(kFqThreads) k_fq_format(const FqBufs bufs, con
       for (int f = 0; f < 3; ++f) {
         const int c = (int)((cnt >> (16 * f)) & 0xFFFF);
         const int v = base[f] + (int)((pre >> (16 * f)) & 0xFFFF);
-        D.td0[f][t] = td[f];
-        D.vs[f][t] = (uint16_t)v;
-        if (c > 0) map[v] = (uint16_t)(f << 8 | t);
+        sp[f].vs = (uint16_t)v;
+        spans[f * kFqStage + t] = sp[f];
+        if (c > 0) map[v] = (uint16_t)(f * kFqStage + t);
+      }
+      if (!(skip & 64)) {
+        const int64_t o[8] = {0, NL + 1, NL + 2, NL + 3, NL + 4 + L, NL + 5 + L, NL + 6 + L, NL + 7 + L + Q};
+        const uint32_t x[8] = {'@', '/', (mate + '0') & 0xFF, '\n', '\n', '+', '\n', '\n'};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int64_t p = P0 + o[e];
+          if (p >= 0 && p < kFqTile) atomicOr(&tile32[p >> 2], x[e] << (8 * (p & 3)));
+        }
       }
     }
     __syncthreads();
     // 2. fill forward (prefix max over f << 8 | record, increasing along the virtual dwords):
-    //    thread t owns map[8t, 8t + 8)
+    //    thread t owns map[16t, 16t + 16)
     {
-      static_assert(kFqDw == 8 * kFqThreads, "one uint4 of the map per thread");
-      uint4 *m4 = reinterpret_cast<uint4 *>(map) + t;
-      const uint4 a = m4[0];
-      uint32_t v[8] = {a.x & 0xFFFF, a.x >> 16, a.y & 0xFFFF, a.y >> 16, a.z & 0xFFFF, a.z >> 16, a.w & 0xFFFF, a.w >> 16};
+      static_assert(kFqMap == 16 * kFqThreads, "two uint4 of the map per thread");
+      uint4 *m4 = reinterpret_cast<uint4 *>(map) + 2 * t;
+      const uint4 a = m4[0], b = m4[1];
+      uint32_t v[16] = {a.x & 0xFFFF, a.x >> 16, a.y & 0xFFFF, a.y >> 16, a.z & 0xFFFF, a.z >> 16, a.w & 0xFFFF, a.w >> 16,
+                        b.x & 0xFFFF, b.x >> 16, b.y & 0xFFFF, b.y >> 16, b.z & 0xFFFF, b.z >> 16, b.w & 0xFFFF, b.w >> 16};
       uint32_t mx = 0;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) mx = max(mx, v[i]);
+      for (int i = 0; i < 16; ++i) mx = max(mx, v[i]);
       uint32_t inc = mx;
       const int lane = t & 63;
       for (int o = 1; o < 64; o <<= 1) {
@@ -552,19 +575,24 @@ __global__ void __launch_bounds__(kFqThreads) k_fq_format(const FqBufs bufs, con
       if (lane == 0) pm = 0;
       for (int w = 0; w < (t >> 6); ++w) pm = max(pm, (uint32_t)s_w[w]);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
+      for (int i = 0; i < 16; ++i) {
         pm = max(pm, v[i]);
         v[i] = pm;
       }
       m4[0] = make_uint4(v[0] | v[1] << 16, v[2] | v[3] << 16, v[4] | v[5] << 16, v[6] | v[7] << 16);
+      m4[1] = make_uint4(v[8] | v[9] << 16, v[10] | v[11] << 16, v[12] | v[13] << 16, v[14] | v[15] << 16);
     }
     __syncthreads();
-    // 3. interiors: virtual dwords on consecutive lanes (one field type per wave but at the two
-    //    type changes), KD per lane at a time, two aligned dword loads each
+    if (skip & 16) return;
+    // 3. field dwords: virtual dwords on consecutive lanes (one field type per wave but at the
+    //    two type changes), KD per lane at a time. The 4-byte source window is clamped inside the
+    //    field (never before a buffer's start), shifted into place and masked to the field's
+    //    bytes; whole dwords are written, edge dwords OR-ed into the zeroed tile.
 #pragma unroll 1
-    for (int vb = 0; vb < V; vb += kFqThreads * KD) {
-      uint32_t key[KD], sh[KD], par[KD], v0[KD], v1[KD];
-      int td[KD];
+    for (int vb = 0; vb < ((skip & 32) ? 0 : V); vb += kFqThreads * KD) {
+      uint32_t key[KD], sh[KD], par[KD], v0[KD], v1[KD], flg[KD];
+      int td_[KD], dsh[KD];   // dsh: byte shift from the clamped window to the wanted one
+      uint32_t msk[KD];
       const uint32_t *a0[KD];
 #pragma unroll
       for (int j = 0; j < KD; ++j) {
@@ -572,28 +600,35 @@ __global__ void __launch_bounds__(kFqThreads) k_fq_format(const FqBufs bufs, con
         key[j] = 0xFFFFu;
         a0[j] = reinterpret_cast<const uint32_t *>(bufs.names);
         sh[j] = par[j] = 0;
-        td[j] = 0;
+        td_[j] = 0;
+        dsh[j] = 0;
+        msk[j] = 0;
+        flg[j] = 0;
         if (v >= V) continue;
         const uint32_t kf = map[v];
-        const int f = kf >> 8, k = kf & 0xFF;
         key[j] = kf;
-        const int tdw = D.td0[f][k] + (v - D.vs[f][k]);
-        td[j] = tdw;
-        const int64_t P0 = D.P0[k];
-        const uint32_t NL = D.NL[k], L = D.L[k], Q = D.Q[k], fl = D.fl[k];
+        const FqSpan S = spans[kf];
+        const int i = v - S.vs;
+        td_[j] = S.td0 + i;
+        const int j0 = S.j0 + 4 * i;   // field index of the dword's byte 0
+        const int len = (int)S.len;
+        // bytes i with 0 <= j0 + i < len
+        const int lo = max(0, -j0), hi = min(4, len - j0);
+        msk[j] = hi > lo ? (0xFFFFFFFFu >> (8 * (4 - (hi - lo)))) << (8 * lo) : 0u;
+        const bool rev = S.flags & 1;
+        // wanted source window start m (ascending source order), clamped into [0, max(0, len - 4)]
+        const int m = rev ? len - 4 - j0 : j0;
+        const int c = min(max(m, 0), max(0, len - 4));
+        dsh[j] = rev ? c - m : m - c;   // > 0: shift right, < 0: shift left (bytes)
         const uint8_t *src;
-        if (f == 0) {
-          const uint32_t jb = (uint32_t)(4 * (int64_t)tdw - (P0 + NL + 4));
-          const bool rev = fl & 1;
-          const uint64_t nb = D.s0[k] + (rev ? L - 4 - jb : jb);
-          src = D.sb[k] + (nb >> 1);
+        if ((S.flags >> 1) == 0) {
+          const uint64_t nb = S.src + (uint64_t)c;
+          src = reinterpret_cast<const uint8_t *>(nb >> 1);
           par[j] = (uint32_t)(nb & 1);
-        } else if (f == 1) {
-          const uint32_t jb = (uint32_t)(4 * (int64_t)tdw - (P0 + NL + 7 + L));
-          src = D.qb[k] + (((fl >> 1) & 1) ? Q - 4 - jb : jb);
         } else {
-          src = D.nm[k] + (uint32_t)(4 * (int64_t)tdw - (P0 + 1));
+          src = reinterpret_cast<const uint8_t *>(S.src + (uint64_t)c);
         }
+        flg[j] = S.flags;
         sh[j] = (uint32_t)((uintptr_t)src & 3);
         a0[j] = reinterpret_cast<const uint32_t *>((uintptr_t)src & ~(uintptr_t)3);
       }
@@ -609,70 +644,31 @@ __global__ void __launch_bounds__(kFqThreads) k_fq_format(const FqBufs bufs, con
       }
 #pragma unroll
       for (int j = 0; j < KD; ++j) {
-        if (key[j] == 0xFFFFu) continue;
-        const int f = key[j] >> 8, k = key[j] & 0xFF;
+        if (key[j] == 0xFFFFu || msk[j] == 0) continue;
+        const int f = flg[j] >> 1, k = key[j] % kFqStage;
+        const bool rev = flg[j] & 1;
         const uint32_t w = __builtin_amdgcn_alignbyte(v1[j], v0[j], sh[j]);
-        const uint32_t fl = D.fl[k];
+        const int ds = dsh[j];
+        auto place = [&](uint32_t y) {   // clamped window -> wanted window
+          return ds >= 0 ? y >> (8 * ds) : y << (8 * -ds);
+        };
         uint32_t x;
         if (f == 0) {
           const uint32_t hiN = (w >> 4) & 0x0F0F0F0Fu, loN = w & 0x0F0F0F0Fu;
           // codes in output order: forward [H0 L0 H1 L1] / [L0 H1 L1 H2], reverse the mirror
-          const bool rev = fl & 1;
           const uint32_t sel = rev ? (par[j] ? 0x04010502u : 0x00040105u) : (par[j] ? 0x02050104u : 0x05010400u);
-          const uint32_t cc = __builtin_amdgcn_perm(loN, hiN, sel);
+          const uint32_t cc = place(__builtin_amdgcn_perm(loN, hiN, sel));
           x = rev ? nt16_lut(cc, kRevLo, kRevHi) : nt16_lut(cc, kFwdLo, kFwdHi);
-          if (rev && ((x - 0x01010101u) & ~x & 0x80808080u)) bad = min(bad, (unsigned long long)(r0 + k));
+          const uint32_t y = x | ~msk[j];
+          if (rev && ((y - 0x01010101u) & ~y & 0x80808080u)) bad = min(bad, (unsigned long long)(r0 + k));
         } else if (f == 1) {
-          x = add33(((fl >> 1) & 1) ? __builtin_bswap32(w) : w);
+          x = add33(place(rev ? __builtin_bswap32(w) : w));
         } else {
-          x = w;
+          x = place(w);
         }
-        tile32[td[j]] = x;
+        if (msk[j] == 0xFFFFFFFFu) tile32[td_[j]] = x;
+        else atomicOr(&tile32[td_[j]], x & msk[j]);
       }
-    }
-    // 4. constant and edge bytes: kFqSpecial slots per record, one thread each
-#pragma unroll 1
-    for (int s = t; s < ns * kFqSpecial; s += kFqThreads) {
-      const int k = s / kFqSpecial, e = s - k * kFqSpecial;
-      const int64_t P0 = D.P0[k];
-      const uint32_t NL = D.NL[k], L = D.L[k], Q = D.Q[k], fl = D.fl[k];
-      int pos = -1;
-      uint32_t x = 0;
-      if (e < 8) {
-        int64_t o;
-        switch (e) {
-          case 0: o = 0; x = '@'; break;
-          case 1: o = NL + 1; x = '/'; break;
-          case 2: o = NL + 2; x = ((fl >> 8) + '0') & 0xFF; break;
-          case 3: o = NL + 3; x = '\n'; break;
-          case 4: o = NL + 4 + L; x = '\n'; break;
-          case 5: o = NL + 5 + L; x = '+'; break;
-          case 6: o = NL + 6 + L; x = '\n'; break;
-          default: o = NL + 7 + L + Q; x = '\n'; break;
-        }
-        const int64_t p = P0 + o;
-        pos = (p >= 0 && p < kFqTile) ? (int)p : -1;
-      } else {
-        const int f = (e - 8) / 6, ee = (e - 8) - 6 * f;   // 0 bases, 1 qualities, 2 name
-        const uint32_t fa = f == 0 ? NL + 4 : f == 1 ? NL + 7 + L : 1, len = f == 0 ? L : f == 1 ? Q : NL;
-        pos = fq_edge(fq_field(P0, fa, len), ee);
-        if (pos >= 0) {
-          const uint32_t jb = (uint32_t)(pos - (P0 + fa));
-          if (f == 0) {
-            const bool rev = fl & 1;
-            const uint64_t nib = D.s0[k] + (rev ? L - 1 - jb : jb);
-            const uint32_t byte = (skip & 1) ? 0x11u : D.sb[k][nib >> 1];
-            const uint32_t c = (nib & 1) ? (byte & 0xF) : (byte >> 4);
-            x = rev ? tab16(kRevLo, kRevHi, c) : tab16(kFwdLo, kFwdHi, c);
-            if (rev && x == 0) bad = min(bad, (unsigned long long)(r0 + k));
-          } else if (f == 1) {
-            x = (((skip & 1) ? 0x11u : D.qb[k][((fl >> 1) & 1) ? Q - 1 - jb : jb]) + 33) & 0xFF;
-          } else {
-            x = (skip & 1) ? 0x41u : D.nm[k][jb];
-          }
-        }
-      }
-      if (pos >= 0) tile[pos] = (uint8_t)x;
     }
   }
   if (bad != ~0ull && !(skip & 1)) atomicMin(err, bad);

@@ -1951,7 +1951,7 @@ GANON_API int ganon_ctx_set_param(ganon_ctx *ctx, int param, int value) {
     return GANON_OK;
   }
   if (param == GANON_PARAM_FASTQ_SKIP) {
-    ctx->fq_skip = value & 31;
+    ctx->fq_skip = value & 127;
     return GANON_OK;
   }
   if (param == GANON_PARAM_FASTQ_KD) {

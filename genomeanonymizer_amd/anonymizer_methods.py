@@ -7,9 +7,11 @@ per scope with a merged tumor/normal pileup and yielding anonymized read pairs.
 
 Here the plugin receives the whole plan of a sample (all scopes, planner.py) and masks
 every scope in ONE device batch through the C ABI of include/ganon.h (libganon_hip.so):
-SNV tally -> TN classification -> overwrite, per scope, on the GPU. Germline indels (rare,
-variable-length edits) stay on the host (indels.py). There is no CPU masking path: a
-missing HIP library or device raises ``GanonError``.
+SNV tally -> TN classification -> overwrite, per scope, on the GPU; the germline indel tally
+(process_indels + TN classification + normal-column check) runs on the GPU too
+(``ganon_indel_*``), and its records become the reference's left-over edits, applied by the
+host when a record is formatted (variable-length output, indels.py). There is no CPU
+masking path: a missing HIP library or device raises ``GanonError``.
 """
 from __future__ import annotations
 
@@ -19,7 +21,7 @@ from typing import Dict, List, Optional, Tuple
 import numpy as np
 
 from . import native
-from .indels import apply_leftovers, has_indel_ops, query_sequence, scope_indels
+from .indels import IndelCall, query_sequence
 from .io.bam import ReadTable
 from .io.fasta import FastaRef
 from .planner import Plan, SamplePlanner
@@ -86,14 +88,56 @@ def build_batch(plan: Plan, tables: Tuple[ReadTable, ReadTable], fasta: FastaRef
     keep = [kept_snv(sc.keep) if sc.is_variant_window else (-1, 0) for sc in scopes]
     arr["keep_pos"] = np.array([k[0] for k in keep], np.int32)
     arr["keep_code"] = np.array([k[1] for k in keep], np.uint8)
-    meta = {"bidx": bidx, "seq_base": seq_base, "scope_ids": np.array([sc.id for sc in scopes], np.int64)}
+    meta = {"bidx": bidx, "rows": rows, "seq_base": seq_base,
+            "scope_ids": np.array([sc.id for sc in scopes], np.int64)}
     return arr, meta
 
 
+def indel_results(recs: np.ndarray, meta: dict, plan: Plan, tables: Tuple[ReadTable, ReadTable],
+                  fasta: FastaRef):
+    """Device indel records (``native.INDEL_REC``, sorted by scope, pos, rank) -> the reference's
+    per-scope statistics counts (``stats_recorder.count_variant``, anonymizer_methods.py:555-556)
+    and left-over lists ``(ds, row, scope) -> [(in_read_pos, IndelCall)]`` in the order
+    ``mask_germline_variants`` appends them (by normal column, then call order at the column).
+    The kept window variant (AM:546-547) is excluded here: its identity includes the allele."""
+    rows = meta["rows"]
+    n_t = len(rows[0])
+
+    def ds_row(r: int) -> Tuple[int, int]:
+        return (0, int(rows[0][r])) if r < n_t else (1, int(rows[1][r - n_t]))
+
+    indel_counts: Dict[int, Dict[VariantType, int]] = {}
+    leftovers: Dict[Tuple[int, int, int], list] = {}
+    live: Dict[Tuple[int, int, int], Optional[IndelCall]] = {}
+    for rec in recs.tolist():
+        b_scope, pos, length, vtype, rank, kind, read, irp = rec
+        sid = int(meta["scope_ids"][b_scope])
+        key = (sid, pos, rank)
+        ds, row = ds_row(read)
+        if kind == native.INDEL_CALL:
+            sc = plan.scopes[sid]
+            vt = VariantType(vtype)
+            end = pos + 1 if vt is VariantType.INS else pos + length - 1
+            alen = length if vt is VariantType.INS else 2
+            allele = query_sequence(tables[ds], row)[irp:irp + alen]
+            if sc.is_variant_window and sc.keep is not None and \
+                    (sc.contig, vt, pos, end, length, allele) == sc.keep.identity():
+                live[key] = None
+                continue
+            counts = indel_counts.setdefault(sid, {VariantType.DEL: 0, VariantType.INS: 0})
+            counts[vt] += 1
+            live[key] = IndelCall(pos, end, vt, length, allele, fasta.fetch(sc.contig, pos, end + 1).upper())
+        else:
+            call = live[key]
+            if call is not None:
+                leftovers.setdefault((ds, row, sid), []).append((irp, call))
+    return indel_counts, leftovers
+
+
 class CompleteGermlineAnonymizer:
-    """Masks every germline (tumor AND normal) SNV of every scope on the GPU; keeps the
-    window's own variant; defers indels to the host path like the reference does
-    (left-overs applied when a pair is yielded)."""
+    """Masks every germline (tumor AND normal) SNV of every scope on the GPU and tallies its
+    germline indels there; keeps the window's own variant; indel edits are left-overs applied
+    when a pair is yielded, like the reference."""
 
     name = "complete_germline"
 
@@ -119,38 +163,12 @@ class CompleteGermlineAnonymizer:
         tables = planner.tables
         fasta = planner.fasta
         arrays, meta = build_batch(plan, tables, fasta, scope_ids)
-        out, b_calls, b_bases, totals = self.engine.mask(arrays)
+        out, b_calls, b_bases, totals, irecs = self.engine.mask(arrays, indels=True)
         calls = np.zeros(len(plan.scopes), np.int32)
         bases = np.zeros(len(plan.scopes), np.int32)
         calls[meta["scope_ids"]] = b_calls
         bases[meta["scope_ids"]] = b_bases
-        mine = set(meta["scope_ids"].tolist())
-        # host indel path, only for scopes that contain a read with an I/D op
-        written = {}
-        for ds, row, s in plan.written_instances():
-            if s >= 0:
-                written[(ds, row)] = s
-        indel_counts: Dict[int, Dict[VariantType, int]] = {}
-        leftovers: Dict[Tuple[int, int, int], list] = {}
-        for sc in plan.scopes:
-            if sc.id not in mine:
-                continue
-            if not any(has_indel_ops(tables[0], r) for r in sc.t_rows.tolist()) and \
-                    not any(has_indel_ops(tables[1], r) for r in sc.n_rows.tolist()):
-                continue
-            reg = planner.registration_order(sc)
-            N = tables[1]
-            ns, ne = N.pos[sc.n_rows], N.end[sc.n_rows]
-
-            def cover(p, ns=ns, ne=ne):
-                return bool(np.any((ns <= p) & (ne > p)))
-
-            keep = sc.keep if sc.is_variant_window else None
-            counts, left = scope_indels(sc.contig, reg, tables, fasta, cover, keep)
-            indel_counts[sc.id] = counts
-            for key, edits in left.items():
-                if written.get(key) == sc.id:
-                    leftovers[(key[0], key[1], sc.id)] = edits
+        indel_counts, leftovers = indel_results(irecs, meta, plan, tables, fasta)
         return MaskResult(out, meta["seq_base"], {}, calls, bases, indel_counts, leftovers, totals, arrays)
 
 

@@ -38,6 +38,21 @@ struct ganon_ctx {
 // (BAM nt16 layout) and the masked output, both `bytes` long.
 int ganon_dbatch_seq_buffers(const ganon_dbatch *db, const uint8_t **in, const uint8_t **out, int64_t *bytes);
 
+// Device read/scope arrays of an uploaded masking batch (defined in ganon_hip.hip), for the
+// germline indel tally (ganon_indel.hip). read_end = bam_endpos (pos + reference length, or
+// pos + 1 for a zero-length alignment).
+struct GanonReadView {
+  const int32_t *ref_start, *read_len, *read_end, *n_cig, *write_scope;
+  const int64_t *seq_off, *cig_off;
+  const uint8_t *seq, *dataset;
+  const uint32_t *cigar;
+  const int64_t *incid_off;
+  const int32_t *incid_read;
+  const int32_t *span_start, *span_len;
+  int32_t n_reads, n_scopes;
+};
+int ganon_dbatch_read_view(const ganon_dbatch *db, GanonReadView *v);
+
 namespace ganon_detail {
 
 inline int fail(ganon_ctx *ctx, int code, const char *fmt, ...) {

@@ -2647,6 +2647,28 @@ int ganon_dbatch_seq_buffers(const ganon_dbatch *db, const uint8_t **in, const u
   return GANON_OK;
 }
 
+int ganon_dbatch_read_view(const ganon_dbatch *db, GanonReadView *v) {
+  if (!db || !v) return GANON_E_ARG;
+  const DevBatch &B = db->B;
+  v->ref_start = B.ref_start;
+  v->read_len = B.read_len;
+  v->read_end = B.read_end;
+  v->n_cig = B.n_cig;
+  v->write_scope = B.write_scope;
+  v->seq_off = B.seq_off;
+  v->cig_off = B.cig_off;
+  v->seq = B.seq;
+  v->dataset = B.dataset;
+  v->cigar = B.cigar;
+  v->incid_off = B.incid_off;
+  v->incid_read = B.incid_read;
+  v->span_start = B.span_start;
+  v->span_len = B.span_len;
+  v->n_reads = db->n_reads;
+  v->n_scopes = db->n_scopes;
+  return GANON_OK;
+}
+
 GANON_API int ganon_mask_batch(ganon_ctx *ctx, const ganon_batch *batch, uint8_t *seq_out, int32_t *scope_calls_out,
                                int32_t *scope_bases_out, int64_t *totals_out) {
   if (!ctx || !batch || (!seq_out && batch->seq_bytes)) return fail(ctx, GANON_E_ARG, "null argument");

@@ -1,0 +1,478 @@
+// ganon_indel.hip — germline indel tally on MI355X (gfx950); C ABI in
+// include/ganon.h (ganon_indel_*), part of libganon_hip.so.
+//
+// Reference semantics, per scope (= one CompleteGermlineAnonymizer.anonymize call):
+//   process_indels (variation_classifier.py:52-141) registers every I/D CIGAR op of every read
+//   the scope's pileup meets, once per read (seen_read_alns, :208-215), as a call keyed by
+//   (pos, end, type, length, allele) (CalledGenomicVariant.__eq__, variants.py:83-96; end is a
+//   function of pos/type/length); the tumor/normal state machine (variants.py:33-39) makes it
+//   TUMORAL_NORMAL once a tumor AND a normal read support it; at the normal pileup column `pos`
+//   every TN call other than the kept window variant is counted and handed to each supporting
+//   read as a left-over edit (anonymizer_methods.py:537-556, :245-252).
+//
+// Design: integer work, no MFMA. Observations are rare in short-read batches and
+// dense in long-read ones (5 % indel errors: ~10^8 per C5 batch), so the tally is a sort rather
+// than an LDS table:
+//   k_indel_emit      one wave per (scope, read) incidence with an I/D op; lanes take 64 CIGAR ops
+//                     at a time, wave prefix sums give each op its reference position and read
+//                     offset, I/D lanes write a 16-byte observation and the sort key
+//                     scope << pos_bits | (pos - span_start) at ballot-compacted slots
+//                     (slots fixed at upload by a host scan, so the output order — and the stable
+//                     sort below — is deterministic);
+//   radix sort        hipcub pairs (key, observation index), key bits = scope bits + pos bits;
+//   k_indel_classify  the first thread of each (scope, pos) run resolves the run: exact allele
+//                     comparison groups observations into calls, tumor+normal presence, normal
+//                     coverage of pos (the scope's normal reads), registration rank among the
+//                     calls at pos, and which observations become output records;
+//   scan + k_indel_write  compaction of the records (deterministic order).
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "../../include/ganon.h"
+#include "ganon_ctx.h"
+
+using ganon_detail::check_launch;
+using ganon_detail::fail;
+using ganon_detail::KernelScope;
+
+namespace {
+
+struct IndelInc {       // one incidence with an I/D op (host plan)
+  int32_t read;
+  int32_t scope;
+  int64_t obs_off;      // first observation slot
+};
+
+struct IndelObs {       // one I/D op of one incidence
+  int32_t read;
+  int32_t irp;          // in_read_pos (reference arithmetic)
+  int32_t pos;          // contig position
+  int32_t type_len;     // length << 1 | is_insertion
+};
+
+constexpr int kIndelWaves = 4;
+constexpr int kIndelThreads = 64 * kIndelWaves;
+
+__device__ __forceinline__ int nib(const uint8_t *__restrict__ seq, int64_t byte_off, int i) {
+  const uint8_t b = seq[byte_off + (i >> 1)];
+  return (i & 1) ? (b & 0xF) : (b >> 4);
+}
+
+__device__ __forceinline__ int wave_excl_scan(int v, int lane) {
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  return x - v;
+}
+
+__global__ void __launch_bounds__(kIndelThreads) k_indel_emit(const GanonReadView V, const IndelInc *__restrict__ list,
+                                                              int64_t n_list, int pos_bits, IndelObs *__restrict__ obs,
+                                                              unsigned long long *__restrict__ keys,
+                                                              uint32_t *__restrict__ vals) {
+  const int lane = threadIdx.x & 63;
+  const int64_t w = (int64_t)blockIdx.x * kIndelWaves + (threadIdx.x >> 6);
+  if (w >= n_list) return;
+  const IndelInc e = list[w];
+  const int r = e.read;
+  const int nc = V.n_cig[r];
+  const uint32_t *__restrict__ cig = V.cigar + V.cig_off[r];
+  const unsigned long long kscope = (unsigned long long)e.scope << pos_bits;
+  const int span0 = V.span_start[e.scope];
+  int rcarry = V.ref_start[r], qcarry = 0;
+  int64_t slot = e.obs_off;
+  for (int k0 = 0; k0 < nc; k0 += 64) {
+    const int k = k0 + lane;
+    const uint32_t word = k < nc ? cig[k] : 0u;
+    const int op = (int)(word & 0xF), len = (int)(word >> 4);
+    // reference-consuming M D N = X; the reference's read offset advances on M N = X S H I
+    const int radv = (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) ? len : 0;
+    const int qadv = (op == 0 || op == 1 || op == 3 || op == 4 || op == 5 || op == 7 || op == 8) ? len : 0;
+    const bool is_id = k < nc && (op == 1 || op == 2);
+    const int pos = rcarry + wave_excl_scan(radv, lane);
+    const int irp = qcarry + wave_excl_scan(qadv, lane);
+    const unsigned long long m = __ballot(is_id);
+    if (is_id) {
+      const int64_t o = slot + __popcll(m & ((1ull << lane) - 1ull));
+      IndelObs ob;
+      ob.read = r;
+      ob.irp = irp;
+      ob.pos = pos;
+      ob.type_len = (len << 1) | (op == 1 ? 1 : 0);
+      obs[o] = ob;
+      keys[o] = kscope | (unsigned long long)(uint32_t)(pos - span0);
+      vals[o] = (uint32_t)o;
+    }
+    slot += __popcll(m);
+    rcarry = __shfl(pos + radv, 63);
+    qcarry = __shfl(irp + qadv, 63);
+  }
+}
+
+// Exact call identity of two observations at the same (scope, pos): type, length, allele.
+__device__ bool same_call(const GanonReadView &V, const IndelObs &a, const IndelObs &b) {
+  if (a.type_len != b.type_len) return false;
+  const int len = a.type_len >> 1;
+  const int alen = (a.type_len & 1) ? len : 2;
+  const int La = V.read_len[a.read], Lb = V.read_len[b.read];
+  // python slice [irp, irp + alen) clipped to the read
+  const int na = max(0, min(La, a.irp + alen) - a.irp);
+  const int nb = max(0, min(Lb, b.irp + alen) - b.irp);
+  if (na != nb) return false;
+  const int64_t oa = V.seq_off[a.read], ob = V.seq_off[b.read];
+  for (int i = 0; i < na; ++i)
+    if (nib(V.seq, oa, a.irp + i) != nib(V.seq, ob, b.irp + i)) return false;
+  return true;
+}
+
+// Registration order key of an observation: the reference meets reads by first pileup column
+// (ref_start), tumor before normal, file order — the incidence order of the scope — and a read's
+// ops in CIGAR order; observation slots follow incidence then op order.
+__device__ __forceinline__ unsigned long long reg_key(const GanonReadView &V, const IndelObs &o, uint32_t idx) {
+  return ((unsigned long long)(uint32_t)V.ref_start[o.read] << 32) | idx;
+}
+
+__device__ bool normal_covers(const GanonReadView &V, int scope, int pos) {
+  const int64_t i1 = V.incid_off[scope + 1];
+  for (int64_t i = V.incid_off[scope]; i < i1; ++i) {
+    const int r = V.incid_read[i];
+    if (V.dataset[r] == 1 && V.ref_start[r] <= pos && pos < V.read_end[r]) return true;
+  }
+  return false;
+}
+
+// flags per sorted element: bit 0 = call record (first registered support of a masked TN call),
+// bit 1 = support record (a read the scope writes); rank = the call's registration rank at pos.
+// repk: scratch, registration key of each call's first support (UINT64_MAX = not a call head).
+__global__ void __launch_bounds__(256) k_indel_classify(const GanonReadView V, const unsigned long long *__restrict__ keys,
+                                                        const uint32_t *__restrict__ vals, int64_t n, int pos_bits,
+                                                        const IndelObs *__restrict__ obs, uint8_t *__restrict__ flags,
+                                                        int32_t *__restrict__ rank,
+                                                        unsigned long long *__restrict__ repk) {
+  const int64_t j0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j0 >= n) return;
+  const unsigned long long key = keys[j0];
+  if (j0 > 0 && keys[j0 - 1] == key) return;
+  int64_t j1 = j0 + 1;
+  while (j1 < n && keys[j1] == key) ++j1;
+  const int scope = (int)(key >> pos_bits);
+  const int pos = obs[vals[j0]].pos;
+  const unsigned long long kNone = ~0ull;
+  // pass 1: call heads (first element of each distinct call, in sorted = slot order), TN state,
+  // first registered support
+  for (int64_t a = j0; a < j1; ++a) {
+    flags[a] = 0;
+    repk[a] = kNone;
+    const IndelObs oa = obs[vals[a]];
+    bool head = true;
+    for (int64_t b = j0; b < a && head; ++b)
+      if (same_call(V, obs[vals[b]], oa)) head = false;
+    if (!head) continue;
+    bool t = false, nn = false;
+    unsigned long long best = kNone;
+    for (int64_t c = a; c < j1; ++c) {
+      const uint32_t ic = vals[c];
+      const IndelObs oc = obs[ic];
+      if (c != a && !same_call(V, oa, oc)) continue;
+      if (V.dataset[oc.read] == 0) t = true; else nn = true;
+      best = min(best, reg_key(V, oc, ic));
+    }
+    repk[a] = best;
+    // TN and a normal column at pos: bit 7 marks a masked call head until pass 2
+    if (t && nn && normal_covers(V, scope, pos)) flags[a] = 0x80;
+  }
+  // pass 2: ranks and records of the masked calls
+  for (int64_t a = j0; a < j1; ++a) {
+    if (!(flags[a] & 0x80)) continue;
+    const unsigned long long ka = repk[a];
+    int rk = 0;
+    for (int64_t b = j0; b < j1; ++b)
+      if (repk[b] < ka) ++rk;   // every call head has a distinct first support
+    const IndelObs oa = obs[vals[a]];
+    for (int64_t c = a; c < j1; ++c) {
+      const uint32_t ic = vals[c];
+      const IndelObs oc = obs[ic];
+      if (c != a && !same_call(V, oa, oc)) continue;
+      uint8_t f = (reg_key(V, oc, ic) == ka) ? 1 : 0;
+      if (V.write_scope[oc.read] == scope) {
+        // a read supporting the call twice keeps its last offset (dict assignment)
+        bool last = true;
+        for (int64_t d = c + 1; d < j1 && last; ++d) {
+          const IndelObs od = obs[vals[d]];
+          if (od.read == oc.read && same_call(V, oa, od)) last = false;
+        }
+        if (last) f |= 2;
+      }
+      if (f) {
+        flags[c] = (uint8_t)((flags[c] & 0x80) | f);
+        rank[c] = rk;
+      }
+    }
+  }
+  for (int64_t a = j0; a < j1; ++a) flags[a] &= 3;
+}
+
+struct RecCount {
+  const uint8_t *flags;
+  int64_t n;
+  __host__ __device__ int64_t operator()(int64_t j) const {
+    if (j >= n) return 0;
+    const uint8_t f = flags[j];
+    return (int64_t)((f & 1) + ((f >> 1) & 1));
+  }
+};
+
+__global__ void __launch_bounds__(256) k_indel_write(const unsigned long long *__restrict__ keys,
+                                                     const uint32_t *__restrict__ vals, int64_t n, int pos_bits,
+                                                     const IndelObs *__restrict__ obs, const uint8_t *__restrict__ flags,
+                                                     const int32_t *__restrict__ rank, const int64_t *__restrict__ offs,
+                                                     ganon_indel_rec *__restrict__ out) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const uint8_t f = flags[j];
+  if (!f) return;
+  const IndelObs o = obs[vals[j]];
+  ganon_indel_rec rec;
+  rec.scope = (int32_t)(keys[j] >> pos_bits);
+  rec.pos = o.pos;
+  rec.length = o.type_len >> 1;
+  rec.type = (o.type_len & 1) ? GANON_INDEL_INS : GANON_INDEL_DEL;
+  rec.rank = rank[j];
+  rec.read = o.read;
+  rec.in_read_pos = o.irp;
+  int64_t w = offs[j];
+  if (f & 1) {
+    rec.kind = GANON_INDEL_CALL;
+    out[w++] = rec;
+  }
+  if (f & 2) {
+    rec.kind = GANON_INDEL_SUPPORT;
+    out[w] = rec;
+  }
+}
+
+int bits_for(int64_t v) {   // bits to hold 0..v
+  int b = 1;
+  while (b < 62 && (v >> b) != 0) ++b;
+  return b;
+}
+
+}  // namespace
+
+struct ganon_indels {
+  std::vector<void *> allocs;
+  GanonReadView V{};
+  int64_t n_obs = 0, n_list = 0, n_records = -1;
+  int pos_bits = 1, key_bits = 2;
+  IndelInc *list = nullptr;
+  IndelObs *obs = nullptr;
+  unsigned long long *keys[2] = {nullptr, nullptr};
+  uint32_t *vals[2] = {nullptr, nullptr};
+  int sorted_sel = 0;                 // which half of the double buffers holds the sorted pairs
+  uint8_t *flags = nullptr;
+  int32_t *rank = nullptr;
+  unsigned long long *repk = nullptr;
+  int64_t *offs = nullptr;            // [n_obs + 1]
+  void *temp = nullptr;
+  size_t temp_bytes = 0;
+  ganon_indel_rec *recs = nullptr;
+  int64_t recs_cap = 0;
+  bool ran = false;
+};
+
+namespace {
+
+template <typename T>
+int ind_alloc(ganon_ctx *ctx, ganon_indels *t, T **p, size_t count) {
+  *p = nullptr;
+  const size_t bytes = std::max<size_t>(count, 1) * sizeof(T) + 128;
+  hipError_t e = hipMalloc(reinterpret_cast<void **>(p), bytes);
+  if (e != hipSuccess) return fail(ctx, GANON_E_NOMEM, "hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
+  t->allocs.push_back(*p);
+  return GANON_OK;
+}
+
+void ind_release(ganon_indels *t) {
+  for (void *p : t->allocs) hipFree(p);
+  t->allocs.clear();
+}
+
+}  // namespace
+
+GANON_API int ganon_indel_upload(ganon_ctx *ctx, const ganon_batch *b, const ganon_dbatch *db, ganon_indels **out) {
+  if (!ctx || !b || !db || !out) return fail(ctx, GANON_E_ARG, "null argument");
+  *out = nullptr;
+  HIP_OR_FAIL(hipSetDevice(ctx->device));
+  GanonReadView V{};
+  if (ganon_dbatch_read_view(db, &V) || V.n_reads != b->n_reads || V.n_scopes != b->n_scopes)
+    return fail(ctx, GANON_E_ARG, "indel upload: host batch does not match the device batch");
+  // per read: I/D ops (the host CIGARs were validated by ganon_batch_upload)
+  std::vector<int32_t> nid(b->n_reads, 0);
+  for (int32_t r = 0; r < b->n_reads; ++r) {
+    const uint32_t *c = b->cigar + b->cig_off[r];
+    int32_t k = 0;
+    for (int32_t i = 0; i < b->n_cig[r]; ++i) {
+      const uint32_t op = c[i] & 0xF;
+      k += (op == 1 || op == 2);
+    }
+    nid[r] = k;
+  }
+  std::vector<IndelInc> list;
+  int64_t n_obs = 0;
+  int32_t max_span = 0;
+  for (int32_t s = 0; s < b->n_scopes; ++s) {
+    max_span = std::max(max_span, b->scope_span_len[s]);
+    for (int64_t i = b->scope_incid_off[s]; i < b->scope_incid_off[s + 1]; ++i) {
+      const int32_t r = b->incid_read[i];
+      if (!nid[r]) continue;
+      list.push_back(IndelInc{r, s, n_obs});
+      n_obs += nid[r];
+    }
+  }
+  if (n_obs >= (int64_t)INT32_MAX) return fail(ctx, GANON_E_ARG, "indel upload: %lld observations (max 2^31-1)", (long long)n_obs);
+  ganon_indels *t = new ganon_indels();
+  t->V = V;
+  t->n_obs = n_obs;
+  t->n_list = (int64_t)list.size();
+  t->pos_bits = bits_for((int64_t)max_span);
+  t->key_bits = t->pos_bits + bits_for(std::max<int64_t>((int64_t)b->n_scopes - 1, 1));
+  int rc = GANON_OK;
+  auto bail = [&](int code) {
+    ind_release(t);
+    delete t;
+    return code;
+  };
+  if (t->key_bits > 64) return bail(fail(ctx, GANON_E_ARG, "indel upload: sort key needs %d bits", t->key_bits));
+  if (n_obs > 0) {
+    if ((rc = ind_alloc(ctx, t, &t->list, list.size()))) return bail(rc);
+    if ((rc = ind_alloc(ctx, t, &t->obs, (size_t)n_obs))) return bail(rc);
+    for (int h = 0; h < 2; ++h) {
+      if ((rc = ind_alloc(ctx, t, &t->keys[h], (size_t)n_obs))) return bail(rc);
+      if ((rc = ind_alloc(ctx, t, &t->vals[h], (size_t)n_obs))) return bail(rc);
+    }
+    if ((rc = ind_alloc(ctx, t, &t->flags, (size_t)n_obs))) return bail(rc);
+    if ((rc = ind_alloc(ctx, t, &t->rank, (size_t)n_obs))) return bail(rc);
+    if ((rc = ind_alloc(ctx, t, &t->repk, (size_t)n_obs))) return bail(rc);
+    if ((rc = ind_alloc(ctx, t, &t->offs, (size_t)n_obs + 1))) return bail(rc);
+    // temp storage: max of the sort's and the scan's
+    size_t sort_bytes = 0, scan_bytes = 0;
+    hipcub::DoubleBuffer<unsigned long long> K(t->keys[0], t->keys[1]);
+    hipcub::DoubleBuffer<uint32_t> Vb(t->vals[0], t->vals[1]);
+    if (hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, K, Vb, (int)n_obs, 0, t->key_bits, ctx->stream) !=
+        hipSuccess)
+      return bail(fail(ctx, GANON_E_DEVICE, "indel upload: radix sort sizing failed"));
+    hipcub::CountingInputIterator<int64_t> cnt(0);
+    hipcub::TransformInputIterator<int64_t, RecCount, hipcub::CountingInputIterator<int64_t>> it(cnt, RecCount{t->flags, n_obs});
+    if (hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, it, t->offs, (int)(n_obs + 1), ctx->stream) != hipSuccess)
+      return bail(fail(ctx, GANON_E_DEVICE, "indel upload: scan sizing failed"));
+    t->temp_bytes = std::max(sort_bytes, scan_bytes);
+    if ((rc = ind_alloc(ctx, t, reinterpret_cast<uint8_t **>(&t->temp), t->temp_bytes))) return bail(rc);
+    hipError_t e = hipMemcpyAsync(t->list, list.data(), list.size() * sizeof(IndelInc), hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) return bail(fail(ctx, GANON_E_DEVICE, "indel upload copy failed: %s", hipGetErrorString(e)));
+  }
+  *out = t;
+  return GANON_OK;
+}
+
+GANON_API int ganon_indel_run(ganon_ctx *ctx, ganon_indels *t) {
+  if (!ctx || !t) return fail(ctx, GANON_E_ARG, "null argument");
+  HIP_OR_FAIL(hipSetDevice(ctx->device));
+  t->ran = true;
+  t->n_records = -1;
+  if (t->n_obs == 0) return GANON_OK;
+  int rc;
+  const int64_t n = t->n_obs;
+  {
+    KernelScope ks(ctx, "k_indel_emit");
+    const unsigned grid = (unsigned)((t->n_list + kIndelWaves - 1) / kIndelWaves);
+    hipLaunchKernelGGL(k_indel_emit, dim3(grid), dim3(kIndelThreads), 0, ctx->stream, t->V, t->list, t->n_list,
+                       t->pos_bits, t->obs, t->keys[0], t->vals[0]);
+    if ((rc = check_launch(ctx, "k_indel_emit"))) return rc;
+  }
+  {
+    KernelScope ks(ctx, "indel_sort");
+    hipcub::DoubleBuffer<unsigned long long> K(t->keys[0], t->keys[1]);
+    hipcub::DoubleBuffer<uint32_t> Vb(t->vals[0], t->vals[1]);
+    size_t bytes = t->temp_bytes;
+    if (hipcub::DeviceRadixSort::SortPairs(t->temp, bytes, K, Vb, (int)n, 0, t->key_bits, ctx->stream) != hipSuccess)
+      return fail(ctx, GANON_E_DEVICE, "indel radix sort failed");
+    t->sorted_sel = K.selector;
+    if (Vb.selector != K.selector) return fail(ctx, GANON_E_DEVICE, "indel radix sort: key/value buffers diverged");
+  }
+  const unsigned long long *keys = t->keys[t->sorted_sel];
+  const uint32_t *vals = t->vals[t->sorted_sel];
+  const unsigned grid = (unsigned)((n + 255) / 256);
+  {
+    KernelScope ks(ctx, "k_indel_classify");
+    hipLaunchKernelGGL(k_indel_classify, dim3(grid), dim3(256), 0, ctx->stream, t->V, keys, vals, n, t->pos_bits,
+                       t->obs, t->flags, t->rank, t->repk);
+    if ((rc = check_launch(ctx, "k_indel_classify"))) return rc;
+  }
+  {
+    KernelScope ks(ctx, "indel_scan");
+    hipcub::CountingInputIterator<int64_t> cnt(0);
+    hipcub::TransformInputIterator<int64_t, RecCount, hipcub::CountingInputIterator<int64_t>> it(cnt, RecCount{t->flags, n});
+    size_t bytes = t->temp_bytes;
+    if (hipcub::DeviceScan::ExclusiveSum(t->temp, bytes, it, t->offs, (int)(n + 1), ctx->stream) != hipSuccess)
+      return fail(ctx, GANON_E_DEVICE, "indel scan failed");
+  }
+  return GANON_OK;
+}
+
+GANON_API int64_t ganon_indel_download(ganon_ctx *ctx, ganon_indels *t, ganon_indel_rec *out, int64_t cap) {
+  if (!ctx || !t) return fail(ctx, GANON_E_ARG, "null argument");
+  if (!t->ran) return fail(ctx, GANON_E_STATE, "indel download before run");
+  if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, GANON_E_DEVICE, "hipSetDevice failed");
+  if (t->n_obs == 0) {
+    t->n_records = 0;
+    return 0;
+  }
+  int64_t total = 0;
+  hipError_t e = hipMemcpyAsync(&total, t->offs + t->n_obs, sizeof total, hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (e != hipSuccess) return fail(ctx, GANON_E_DEVICE, "indel download: %s", hipGetErrorString(e));
+  t->n_records = total;
+  if (!out || cap < total || total == 0) return total;
+  if (t->recs_cap < total) {
+    int rc = ind_alloc(ctx, t, &t->recs, (size_t)total);
+    if (rc) return rc;
+    t->recs_cap = total;
+  }
+  const int64_t n = t->n_obs;
+  hipLaunchKernelGGL(k_indel_write, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream,
+                     t->keys[t->sorted_sel], t->vals[t->sorted_sel], n, t->pos_bits, t->obs, t->flags, t->rank,
+                     t->offs, t->recs);
+  int rc = check_launch(ctx, "k_indel_write");
+  if (rc) return rc;
+  e = hipMemcpyAsync(out, t->recs, (size_t)total * sizeof(ganon_indel_rec), hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (e != hipSuccess) return fail(ctx, GANON_E_DEVICE, "indel download: %s", hipGetErrorString(e));
+  return total;
+}
+
+GANON_API int ganon_indel_info(const ganon_indels *t, int64_t *info4) {
+  if (!t || !info4) return GANON_E_ARG;
+  info4[0] = t->n_obs;
+  info4[1] = t->n_list;
+  info4[2] = t->key_bits;
+  info4[3] = t->n_records;
+  return GANON_OK;
+}
+
+GANON_API int ganon_indel_free(ganon_ctx *ctx, ganon_indels *t) {
+  if (!t) return GANON_OK;
+  if (ctx) {
+    hipSetDevice(ctx->device);
+    hipStreamSynchronize(ctx->stream);
+  }
+  ind_release(t);
+  delete t;
+  return GANON_OK;
+}

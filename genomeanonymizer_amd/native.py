@@ -60,6 +60,24 @@ class GanonFastqRecords(C.Structure):
     ]
 
 
+# ganon_indel_rec (include/ganon.h): one masked TN indel call (kind 0) or one support of it by
+# a read its scope writes (kind 1)
+INDEL_REC = np.dtype([("scope", np.int32), ("pos", np.int32), ("length", np.int32), ("type", np.int32),
+                      ("rank", np.int32), ("kind", np.int32), ("read", np.int32), ("in_read_pos", np.int32)])
+INDEL_DEL, INDEL_INS = 2, 3
+INDEL_CALL, INDEL_SUPPORT = 0, 1
+
+
+def indel_records_array(rows) -> np.ndarray:
+    """Records as a structured array sorted by (scope, pos, rank, kind, read): the device's order
+    is not part of the contract."""
+    a = np.array([tuple(r) for r in rows], INDEL_REC) if not isinstance(rows, np.ndarray) else rows
+    if len(a) == 0:
+        return np.zeros(0, INDEL_REC)
+    o = np.lexsort((a["in_read_pos"], a["read"], a["kind"], a["rank"], a["pos"], a["scope"]))
+    return a[o]
+
+
 class KernelTime(C.Structure):
     _fields_ = [("name", C.c_char * 48), ("launches", C.c_int32), ("ms", C.c_float)]
 
@@ -137,6 +155,12 @@ def hip_lib():
     lib.ganon_fastq_format_hip.argtypes = [_p, C.c_int64, C.POINTER(_u8p), _u8p, _i64p, _i32p, _u8p,
                                            C.POINTER(_u8p), _u8p, _i64p, _i32p, _u8p, C.c_char_p, _i64p,
                                            _i32p, _u8p, C.c_char_p, C.c_int64]
+    lib.ganon_indel_upload.argtypes = [_p, C.POINTER(GanonBatch), _p, C.POINTER(_p)]
+    lib.ganon_indel_run.argtypes = [_p, _p]
+    lib.ganon_indel_download.argtypes = [_p, _p, _p, C.c_int64]
+    lib.ganon_indel_download.restype = C.c_int64
+    lib.ganon_indel_info.argtypes = [_p, _i64p]
+    lib.ganon_indel_free.argtypes = [_p, _p]
     if lib.ganon_abi_version() != 2:
         raise GanonError("libganon_hip.so ABI version mismatch")
     _hip = lib
@@ -158,6 +182,7 @@ EXPORTED_HIP_SYMBOLS = (
     "ganon_batch_device_totals", "ganon_batch_copy_totals", "ganon_last_kernel_times", "ganon_batch_info",
     "ganon_fastq_upload", "ganon_fastq_run", "ganon_fastq_bytes", "ganon_fastq_device_output",
     "ganon_fastq_download", "ganon_fastq_free", "ganon_fastq_format_hip",
+    "ganon_indel_upload", "ganon_indel_run", "ganon_indel_download", "ganon_indel_info", "ganon_indel_free",
 )
 EXPORTED_HOST_SYMBOLS = (
     "ganon_bam_open", "ganon_bam_view_get", "ganon_bam_error", "ganon_bam_close",
@@ -213,8 +238,23 @@ class HipMasker:
     def set_profiling(self, on: bool) -> None:
         self._check(self._lib.ganon_ctx_set_profiling(self._h, 1 if on else 0), "set_profiling")
 
-    def mask(self, arrays: dict):
-        """Synchronous one-shot: returns (seq_out, scope_calls, scope_bases, totals)."""
+    def mask(self, arrays: dict, indels: bool = False):
+        """Synchronous one-shot: returns (seq_out, scope_calls, scope_bases, totals), plus the
+        germline indel records (``INDEL_REC``, sorted) when ``indels``."""
+        if indels:
+            db = self.upload(arrays)
+            try:
+                t = db.indel_tally(arrays)
+                try:
+                    db.run()
+                    t.run()
+                    res = db.download()
+                    recs = t.download()
+                finally:
+                    t.free()
+            finally:
+                db.free()
+            return res + (recs,)
         b = make_c_batch(arrays)
         out = np.empty(b.seq_bytes, np.uint8)
         calls = np.zeros(b.n_scopes, np.int32)
@@ -416,9 +456,49 @@ class DeviceBatch:
         n = self.m._lib.ganon_last_kernel_times(self.m._h, arr, 32)
         return [(arr[i].name.decode(), int(arr[i].launches), float(arr[i].ms)) for i in range(min(n, 32))]
 
+    def indel_tally(self, arrays: dict) -> "DeviceIndels":
+        """Plan the germline indel tally of this batch (``arrays`` = the batch it was uploaded from)."""
+        b = make_c_batch(arrays)
+        h = _p()
+        self.m._check(self.m._lib.ganon_indel_upload(self.m._h, C.byref(b), self.h, C.byref(h)), "ganon_indel_upload")
+        return DeviceIndels(self.m, h)
+
     def free(self) -> None:
         if self.h:
             self.m._lib.ganon_batch_free(self.m._h, self.h)
+            self.h = None
+
+
+class DeviceIndels:
+    """ganon_indel_* handle: observation emission, sort and classification on the device."""
+
+    def __init__(self, masker: HipMasker, handle):
+        self.m = masker
+        self.h = handle
+
+    def run(self) -> None:
+        self.m._check(self.m._lib.ganon_indel_run(self.m._h, self.h), "ganon_indel_run")
+
+    def download(self) -> np.ndarray:
+        lib = self.m._lib
+        n = lib.ganon_indel_download(self.m._h, self.h, None, 0)
+        if n < 0:
+            self.m._check(int(n), "ganon_indel_download")
+        out = np.zeros(n, INDEL_REC)
+        if n:
+            w = lib.ganon_indel_download(self.m._h, self.h, out.ctypes.data_as(_p), n)
+            if w != n:
+                self.m._check(int(w) if w < 0 else -4, "ganon_indel_download")
+        return indel_records_array(out)
+
+    def info(self) -> dict:
+        a = np.zeros(4, np.int64)
+        self.m._check(self.m._lib.ganon_indel_info(self.h, _ptr(a, _i64p)), "ganon_indel_info")
+        return dict(zip(("observations", "incidences", "key_bits", "records"), a.tolist()))
+
+    def free(self) -> None:
+        if self.h:
+            self.m._lib.ganon_indel_free(self.m._h, self.h)
             self.h = None
 
 

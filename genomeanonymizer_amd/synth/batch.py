@@ -161,6 +161,160 @@ def random_batch(seed: int, n_scopes: int = 64, max_reads: int = 40, read_len=(0
     return arr
 
 
+def indel_batch(seed: int, n_scopes: int = 40, reads_per_scope=(2, 40), read_len=(20, 200),
+                indel_per_kb: float = 10.0, noise: float = 0.01) -> Dict[str, np.ndarray]:
+    """Germline-indel batch for the indel tally: one contig, overlapping scope
+    windows (a read may join the next scope's incidence list), germline INS/DEL alleles carried by
+    tumor and normal reads, random indel noise, and the CIGAR corner cases of process_indels
+    (variation_classifier.py:52-141): leading/trailing I and D, back-to-back I ops at one position,
+    S/H clips (H counts toward in_read_pos), N skips. Incidences list tumor reads, then
+    normal reads, in file order, as build_batch does."""
+    rng = np.random.default_rng(seed)
+    step, win = 1500, 2600
+    Lc = n_scopes * step + win + 2000
+    ref = ACGT[rng.integers(0, 4, Lc)]
+    planted = {}
+    for p in np.unique(rng.integers(50, Lc - 50, int(Lc * indel_per_kb / 1000))).tolist():
+        if rng.random() < 0.5:
+            k = int(rng.integers(1, 6))
+            planted[p] = ("I", k, ACGT[rng.integers(0, 4, k)])
+        else:
+            planted[p] = ("D", int(rng.integers(1, 6)), None)
+    reads = []        # (home scope, pos, cigar words, seq codes, dataset)
+
+    def make(pos, rl):
+        ops, seq = [], []
+
+        def put(op, n, codes=None):
+            if op == "M" and ops and ops[-1][0] == "M":
+                ops[-1] = ("M", ops[-1][1] + n)
+            else:
+                ops.append((op, n))
+            if codes is not None:
+                seq.extend(int(c) for c in codes)
+
+        if rng.random() < 0.15:
+            put("H", int(rng.integers(1, 20)))
+        if rng.random() < 0.2:
+            k = int(rng.integers(1, 30))
+            put("S", k, ACGT[rng.integers(0, 4, k)])
+        if rng.random() < 0.05:
+            k = int(rng.integers(1, 4))
+            put("I", k, ACGT[rng.integers(0, 4, k)])
+        p = pos
+        left = rl - len(seq)
+        while left > 0 and p < Lc - 10:
+            pl = planted.get(p)
+            if pl is not None and rng.random() < 0.8:
+                if pl[0] == "I":
+                    n = min(pl[1], left)
+                    put("I", n, pl[2][:n])
+                    left -= n
+                    if left > 3 and rng.random() < 0.05:      # a second I op at the same position
+                        put("I", 1, ACGT[rng.integers(0, 4, 1)])
+                        left -= 1
+                else:
+                    put("D", pl[1])
+                    p += pl[1]
+                if left > 0:
+                    put("M", 1, [ref[p]])
+                    p += 1
+                    left -= 1
+                continue
+            u = rng.random()
+            if u < noise / 2:
+                n = min(int(rng.integers(1, 4)), left)
+                put("I", n, ACGT[rng.integers(0, 4, n)])
+                left -= n
+            elif u < noise:
+                n = int(rng.integers(1, 4))
+                put("D", n)
+                p += n
+            elif u < noise + 0.002:
+                n = int(rng.integers(5, 30))
+                put("N", n)
+                p += n
+            else:
+                c = ref[p] if rng.random() > 0.01 else ACGT[rng.integers(0, 4)]
+                put("M", 1, [c])
+                p += 1
+                left -= 1
+        if left > 0:
+            put("S", left, ACGT[rng.integers(0, 4, left)])
+        u = rng.random()
+        if u < 0.04:
+            k = int(rng.integers(1, 4))
+            put("I", k, ACGT[rng.integers(0, 4, k)])
+        elif u < 0.08:
+            put("D", int(rng.integers(1, 4)))
+        if rng.random() < 0.1:
+            put("H", int(rng.integers(1, 20)))
+        if not any(o in ("M",) for o, _ in ops):
+            return None, None
+        return [_cigar_word(o, n) for o, n in ops], np.array(seq, np.uint8)
+
+    for s in range(n_scopes):
+        for _ in range(int(rng.integers(reads_per_scope[0], reads_per_scope[1] + 1))):
+            rl = int(rng.integers(read_len[0], read_len[1] + 1))
+            pos = int(rng.integers(s * step + 50, s * step + win - 400))
+            cig, seq = make(pos, rl)
+            if cig is not None:
+                reads.append((s, pos, cig, seq, int(rng.integers(0, 2))))
+    n = len(reads)
+    ends = np.array([_ref_end(r[1], r[2]) for r in reads], np.int64)
+    members = [[] for _ in range(n_scopes)]
+    for i, (s, pos, _, _, _) in enumerate(reads):
+        members[s].append(i)
+        if s + 1 < n_scopes and ends[i] > (s + 1) * step and rng.random() < 0.5:
+            members[s + 1].append(i)
+    ws = np.full(n, -1, np.int32)
+    for i, (s, _, _, _, _) in enumerate(reads):
+        if rng.random() < 0.85:
+            ws[i] = s
+    seq_parts, cig_parts = [], []
+    seq_off = np.zeros(n, np.int64)
+    cig_off = np.zeros(n, np.int64)
+    so = co = 0
+    for i, (_, _, cig, seq, _) in enumerate(reads):
+        pk = pack_nibbles(seq)
+        seq_parts.append(pk)
+        seq_off[i] = so
+        so += len(pk)
+        cig_parts.append(np.array(cig, np.uint32))
+        cig_off[i] = co
+        co += len(cig)
+    ref_start = np.array([r[1] for r in reads], np.int64)
+    dataset = np.array([r[4] for r in reads], np.uint8)
+    span_start, span_len, incid, offs = [], [], [], [0]
+    for s in range(n_scopes):
+        ids = sorted(members[s], key=lambda i: (int(dataset[i]), i))
+        a = int(ref_start[ids].min()) if ids else 0
+        b = int(ends[ids].max()) if ids else 0
+        span_start.append(a)
+        span_len.append(b - a)
+        incid.extend(ids)
+        offs.append(len(incid))
+    return {
+        "ref_start": ref_start.astype(np.int32),
+        "read_len": np.array([len(r[3]) for r in reads], np.int32),
+        "seq_off": seq_off,
+        "seq_nt16": np.concatenate(seq_parts) if seq_parts else np.zeros(0, np.uint8),
+        "cig_off": cig_off,
+        "n_cig": np.array([len(r[2]) for r in reads], np.int32),
+        "cigar": np.concatenate(cig_parts) if cig_parts else np.zeros(0, np.uint32),
+        "dataset": dataset,
+        "write_scope": ws,
+        "scope_incid_off": np.array(offs, np.int64),
+        "incid_read": np.array(incid, np.int32),
+        "scope_span_start": np.array(span_start, np.int32),
+        "scope_span_len": np.array(span_len, np.int32),
+        "scope_ref_off": np.array(span_start, np.int64),
+        "ref_nt16": pack_nibbles(ref),
+        "keep_pos": np.full(n_scopes, -1, np.int32),
+        "keep_code": np.zeros(n_scopes, np.uint8),
+    }
+
+
 def dense_batch(seed: int, reads_per_scope=(8000, 400, 1200), span: int = 2200, read_len: int = 150,
                 error_rate: float = 0.02, keep_hot_site: bool = False) -> Dict[str, np.ndarray]:
     """Very deep, error-rich scopes: thousands of observations per scope and one germline

@@ -224,4 +224,52 @@ GANON_API int64_t ganon_fastq_format_hip(ganon_ctx *ctx, int64_t n, const uint8_
                                          const int64_t *name_off, const int32_t *name_len,
                                          const uint8_t *mate, char *out, int64_t cap);
 
+/* ---- Germline indel tally ----------------------------------------------
+ * Replaces, for every scope of an uploaded batch at once, process_indels
+ * (variation_classifier.py:52-141: every I/D CIGAR op of every scope read is a call keyed by
+ * (pos, type, length, allele) with the reference's read-offset arithmetic), the
+ * tumor/normal state machine (variants.py:33-39) and the indel half of mask_germline_variants
+ * (anonymizer_methods.py:537-556 -> add_left_over_variant :245-252): a call seen in >=1 tumor and
+ * >=1 normal read of the scope, at a position some normal read of the scope covers (a normal
+ * pileup column exists there), is a masked TN indel call. The variable-length edits themselves
+ * (mask_or_modify_indel, anonymizer_methods.py:178-203) are applied by the host when the record
+ * is formatted, as the reference applies left-overs when a pair is yielded.
+ *   pos          = ref_start + sum of M/D/N/=/X lengths before the op
+ *   in_read_pos  = sum of M/N/=/X/S/H/I lengths before the op (the reference's counter adds S/H/I
+ *                  and subtracts D from a sum that includes D and N)
+ *   allele       = read bases [in_read_pos, in_read_pos + (INS ? length : 2)) clipped to the read
+ * Registration order (which call at a position came first, needed for the order of a read's
+ * left-overs) assumes each scope's incidences list its tumor reads in file order, then its normal
+ * reads in file order (the reference meets reads column by column, tumor before normal).
+ * Output: one record per masked TN call (kind GANON_INDEL_CALL: read/in_read_pos = its first
+ * registered support, for the host's kept-variant check) and one per support by a read whose
+ * write_scope is that scope (kind GANON_INDEL_SUPPORT; a read supporting a call twice keeps its
+ * last offset, like the reference's supporting_reads dict). Records are in device order; a call
+ * is identified by (scope, pos, rank), rank = its registration order among the calls at pos. */
+enum { GANON_INDEL_DEL = 2, GANON_INDEL_INS = 3 };          /* VariantType values */
+enum { GANON_INDEL_CALL = 0, GANON_INDEL_SUPPORT = 1 };
+typedef struct ganon_indel_rec {
+  int32_t scope;        /* batch scope                                   */
+  int32_t pos;          /* contig position of the call                   */
+  int32_t length;       /* CIGAR op length                               */
+  int32_t type;         /* GANON_INDEL_DEL / GANON_INDEL_INS             */
+  int32_t rank;         /* registration order among the calls at pos     */
+  int32_t kind;         /* GANON_INDEL_CALL / GANON_INDEL_SUPPORT        */
+  int32_t read;         /* batch read                                    */
+  int32_t in_read_pos;  /* offset of the op in the read (see above)      */
+} ganon_indel_rec;
+typedef struct ganon_indels ganon_indels;
+/* Plan the tally of an uploaded batch: b must be the host batch db was uploaded from (CIGARs are
+ * scanned on the host to size the observation buffers). db must outlive the handle. */
+GANON_API int ganon_indel_upload(ganon_ctx *ctx, const ganon_batch *b, const ganon_dbatch *db,
+                                 ganon_indels **out);
+/* Observation emission, sort and classification on the device (async on the stream). */
+GANON_API int ganon_indel_run(ganon_ctx *ctx, ganon_indels *t);
+/* Synchronize and copy the records: returns their count; copies only when out != NULL and
+ * cap >= count (call again with a larger buffer otherwise); negative GANON_E* on failure. */
+GANON_API int64_t ganon_indel_download(ganon_ctx *ctx, ganon_indels *t, ganon_indel_rec *out, int64_t cap);
+/* [observations, incidences with an I/D op, sort key bits, records (after download, else -1)] */
+GANON_API int ganon_indel_info(const ganon_indels *t, int64_t *info4);
+GANON_API int ganon_indel_free(ganon_ctx *ctx, ganon_indels *t);
+
 #endif /* GANON_H */

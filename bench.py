@@ -5,7 +5,9 @@ One step = one pass of the masking kernels over one resident batch: the config-2
 (10 M synthetic 150 bp tumor+normal reads on a 3.0 Gb genome with 1 M germline SNPs and a
 1 M-window VCF; genomeanonymizer_amd/synth/batch.py) uploaded to HBM once, then
 ``ganon_batch_run`` = SNV tally -> TN classification -> overwrite for every scope, plus the
-pass-through copies, exactly what ``ganon_mask_batch`` does minus the PCIe copies.
+pass-through copies, exactly what ``ganon_mask_batch`` does minus the PCIe copies, then
+``ganon_indel_run`` = the germline indel tally (a no-op launch-free pass when no read of the
+batch has an I/D op, as in the config-2 synthetic reads).
 Multi-GPU (torchrun): every rank owns its own config-2 shard (per-contig sharding makes
 shards independent; weak scaling) and the only collective is the int64 totals all-reduce
 over RCCL at the end of each step.
@@ -50,7 +52,25 @@ def kernel_class(name: str) -> str:
         return "large"
     if name.startswith("k_group"):
         return "group"
+    if name in ("k_indel_emit", "indel_sort", "k_indel_classify", "indel_scan"):
+        return name
     return ""
+
+
+def indel_bytes(arr, n_obs: int) -> dict:
+    """Algorithmic bytes per launch of the indel tally (ganon_indel.hip): the emission reads the
+    CIGARs of the incidences whose read has an I/D op and writes a 16-byte observation + 8-byte key
+    + 4-byte index per op; the sort reads and writes each (key, index) pair once; the
+    classification reads key, index and observation and writes flags, rank and the 8-byte
+    registration key of every element; the scan reads the flags and writes 8-byte offsets."""
+    ops = arr["cigar"] & 0xF
+    has = np.zeros(len(arr["read_len"]), bool)
+    rid = np.repeat(np.arange(len(arr["read_len"])), arr["n_cig"].astype(np.int64))
+    has[np.unique(rid[(ops == 1) | (ops == 2)])] = True
+    r = arr["incid_read"].astype(np.int64)
+    cig = int((4 * arr["n_cig"].astype(np.int64)[r])[has[r]].sum())
+    return {"k_indel_emit": cig + 28 * n_obs, "indel_sort": 24 * n_obs,
+            "k_indel_classify": 41 * n_obs, "indel_scan": 9 * n_obs}
 
 
 def kernel_bytes(arr, mode: str = "fused") -> dict:
@@ -240,6 +260,7 @@ def main() -> None:
     ap.add_argument("--unroll", type=int, default=2, help="group kernel chunk width in 16-base blocks (1/2/4/8)")
     ap.add_argument("--ab", action="store_true", help="also time every small-scope variant, interleaved")
     ap.add_argument("--no-fastq", action="store_true", help="skip the FASTQ formatter measurement")
+    ap.add_argument("--indel-sort", type=int, default=0, help="GANON_PARAM_INDEL_SORT: 0 segmented, 1 global")
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_r01.json"),
                     help="PMC summary (tools/pmc_summary.py) for the traffic field, if present")
     args = ap.parse_args()
@@ -266,15 +287,18 @@ def main() -> None:
     masker = native.HipMasker(local)
     masker.set_variant(args.variant)
     masker.set_param(native.PARAM_GROUP_UNROLL, args.unroll)
+    masker.set_param(native.PARAM_INDEL_SORT, args.indel_sort)
     stream = torch.cuda.current_stream()
     masker.set_stream(stream.cuda_stream)
     t_up = time.perf_counter()
     db = masker.upload(arr)
+    ind = db.indel_tally(arr)      # germline indel tally, part of every step
     t_up = time.perf_counter() - t_up
     tot_t = torch.zeros(8, dtype=torch.int64, device="cuda")
 
     def step():
         db.run()
+        ind.run()
         if dist is not None:
             db.copy_totals_to(tot_t.data_ptr())
             dist.all_reduce(tot_t)
@@ -302,6 +326,7 @@ def main() -> None:
     ktimes: dict = {}
     for _ in range(args.steps):
         db.run()
+        ind.run()
         db.sync()
         for name, launches, ms in db.kernel_times():
             k = ktimes.setdefault(name, [0, 0.0])
@@ -330,6 +355,9 @@ def main() -> None:
     fastq = None if args.no_fastq else fastq_bench(masker, db, arr, args, torch, rank)
     totals = db.totals()
     batch_info = db.info()
+    irecs = ind.download()
+    indel_info = ind.info()
+    ind.free()
     if dist is not None:
         db.copy_totals_to(tot_t.data_ptr())
         dist.all_reduce(tot_t)
@@ -340,8 +368,10 @@ def main() -> None:
     db.free()
 
     kb = kernel_bytes(arr, VARIANT_WRITE[args.variant])
+    kb.update(indel_bytes(arr, indel_info["observations"]))
     per_kernel = {n: {"launches": c, "avg_ms": ms / c} for n, (c, ms) in ktimes.items()}
     dom = max(per_kernel, key=lambda n: per_kernel[n]["avg_ms"] * per_kernel[n]["launches"])
+    indel_ms = sum(v["avg_ms"] * v["launches"] for n, v in per_kernel.items() if "indel" in n) / args.steps
     dom_bytes = kb.get(kernel_class(dom), 0)
     dom_ms = per_kernel[dom]["avg_ms"]
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
@@ -386,6 +416,10 @@ def main() -> None:
                  "achieved_GBps": round(alg_total / (pass_ms * 1e-3) / 1e9, 1),
                  "kernels": {n: {"avg_ms": round(v["avg_ms"], 5), "launches_per_step": v["launches"] // args.steps,
                                  "alg_bytes": kb.get(kernel_class(n))} for n, v in per_kernel.items()}},
+        "indel": {"observations": indel_info["observations"], "incidences": indel_info["incidences"],
+                  "masked_calls": int((irecs["kind"] == native.INDEL_CALL).sum()),
+                  "support_records": int((irecs["kind"] == native.INDEL_SUPPORT).sum()),
+                  "ms_per_step": round(indel_ms, 4)},
         "ab_small_scope_kernel": ab,
         "fastq": fastq,
         "totals": {k: int(v) for k, v in zip(native.TOTAL_NAMES, job_totals)},

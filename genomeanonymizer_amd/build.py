@@ -47,13 +47,37 @@ HIP_SOURCES = ("ganon_hip.hip", "ganon_fastq.hip", "ganon_indel.hip")
 
 
 def build_hip(force: bool = False) -> str:
+    """One object per source, compiled in parallel, then linked (the hipcub sort in
+    ganon_indel.hip is the slowest unit)."""
     srcs = [os.path.join(CSRC, s) for s in HIP_SOURCES]
-    deps = srcs + [os.path.join(REPO, "include", "ganon.h"), os.path.join(CSRC, "ganon_ctx.h"), __file__]
-    if force or _stale(HIP_LIB, deps):
-        tmp = HIP_LIB + ".tmp"
-        _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-              "-fvisibility=hidden", "-Wno-unused-result", "-Wno-unused-value", "-o", tmp] + srcs)
-        os.replace(tmp, HIP_LIB)
+    hdrs = [os.path.join(REPO, "include", "ganon.h"), os.path.join(CSRC, "ganon_ctx.h"), __file__]
+    if not (force or _stale(HIP_LIB, srcs + hdrs)):
+        return HIP_LIB
+    objdir = os.path.join(PKG, "build")
+    os.makedirs(objdir, exist_ok=True)
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden",
+             "-Wno-unused-result", "-Wno-unused-value"]
+    objs, procs = [], []
+    for src in srcs:
+        obj = os.path.join(objdir, os.path.basename(src) + ".o")
+        objs.append(obj)
+        if force or _stale(obj, [src] + hdrs):
+            cmd = [_hipcc()] + flags + ["-c", "-o", obj + ".tmp", src]
+            procs.append((cmd, obj, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                                                     text=True)))
+    failed = None
+    for cmd, obj, p in procs:
+        out, _ = p.communicate()
+        if p.returncode != 0:
+            sys.stderr.write(out)
+            failed = failed or cmd
+        else:
+            os.replace(obj + ".tmp", obj)
+    if failed:
+        raise RuntimeError(f"build failed: {' '.join(failed)}")
+    tmp = HIP_LIB + ".tmp"
+    _run([_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs)
+    os.replace(tmp, HIP_LIB)
     return HIP_LIB
 
 

@@ -27,6 +27,7 @@ struct ganon_ctx {
   int ref2 = 1;                // GANON_PARAM_REF2
   int fq_skip = 0;             // GANON_PARAM_FASTQ_SKIP (profiling only)
   int fq_kd = 4;               // GANON_PARAM_FASTQ_KD
+  int indel_sort = 0;          // GANON_PARAM_INDEL_SORT
   std::string err;
   struct Rec { std::string name; hipEvent_t e0, e1; };
   std::vector<Rec> recs;

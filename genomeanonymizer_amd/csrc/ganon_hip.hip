@@ -1954,6 +1954,11 @@ GANON_API int ganon_ctx_set_param(ganon_ctx *ctx, int param, int value) {
     ctx->fq_skip = value & 127;
     return GANON_OK;
   }
+  if (param == GANON_PARAM_INDEL_SORT) {
+    if (value != 0 && value != 1) return fail(ctx, GANON_E_ARG, "indel sort: 0 (segmented) or 1 (global)");
+    ctx->indel_sort = value;
+    return GANON_OK;
+  }
   if (param == GANON_PARAM_FASTQ_KD) {
     if (value != 1 && value != 2 && value != 4) return fail(ctx, GANON_E_ARG, "FASTQ dwords per lane: 1, 2 or 4");
     ctx->fq_kd = value;

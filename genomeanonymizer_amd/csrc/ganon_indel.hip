@@ -15,16 +15,19 @@
 // than an LDS table:
 //   k_indel_emit      one wave per (scope, read) incidence with an I/D op; lanes take 64 CIGAR ops
 //                     at a time, wave prefix sums give each op its reference position and read
-//                     offset, I/D lanes write a 16-byte observation and the sort key
-//                     scope << pos_bits | (pos - span_start) at ballot-compacted slots
-//                     (slots fixed at upload by a host scan, so the output order — and the stable
-//                     sort below — is deterministic);
-//   radix sort        hipcub pairs (key, observation index), key bits = scope bits + pos bits;
-//   k_indel_classify  the first thread of each (scope, pos) run resolves the run: exact allele
-//                     comparison groups observations into calls, tumor+normal presence, normal
-//                     coverage of pos (the scope's normal reads), registration rank among the
-//                     calls at pos, and which observations become output records;
-//   scan + k_indel_write  compaction of the records (deterministic order).
+//                     offset, I/D lanes write a 16-byte observation and a 32-bit sort key
+//                     (pos - span_start, plus the scope segment's parity in bit 31) at
+//                     ballot-compacted slots fixed at upload by a host scan (scope-major);
+//   radix sort        hipcub segmented pairs (key, observation index), one segment per scope
+//                     with observations, position bits only (GANON_PARAM_INDEL_SORT 1: one
+//                     global sort of 64-bit scope|position keys instead);
+//   k_indel_classify  the first thread of each (scope, pos) run resolves the run — singletons
+//                     leave at once: exact allele comparison groups observations into calls,
+//                     tumor+normal presence, normal coverage of pos (the scope's normal reads),
+//                     registration rank among the calls at pos, the observations that become
+//                     output records, one atomic add of the record count per run;
+//   k_indel_write     (download) records at atomic slots; results do not depend on slot order
+//                     (a call is (scope, pos, rank); the host sorts the records).
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -43,16 +46,25 @@ namespace {
 
 struct IndelInc {       // one incidence with an I/D op (host plan)
   int32_t read;
-  int32_t scope;
+  uint32_t scope_par;   // scope | (index of the scope among scopes with observations & 1) << 31
   int64_t obs_off;      // first observation slot
 };
 
 struct IndelObs {       // one I/D op of one incidence
   int32_t read;
   int32_t irp;          // in_read_pos (reference arithmetic)
-  int32_t pos;          // contig position
+  int32_t scope;
   int32_t type_len;     // length << 1 | is_insertion
 };
+
+// Sort keys. Segmented (default): one segment per scope, 32-bit key = segment parity << 31 |
+// (pos - span_start), sorted on the position bits only — the parity bit still tells adjacent
+// scopes apart in the sorted array. Global (A/B): 64-bit key = scope << pos_bits | (pos - span_start).
+template <typename KeyT>
+__device__ __forceinline__ KeyT make_key(uint32_t scope_par, int pos_bits, uint32_t rel) {
+  if constexpr (sizeof(KeyT) == 4) return (scope_par & 0x80000000u) | rel;
+  else return ((unsigned long long)(scope_par & 0x7FFFFFFFu) << pos_bits) | rel;
+}
 
 constexpr int kIndelWaves = 4;
 constexpr int kIndelThreads = 64 * kIndelWaves;
@@ -72,10 +84,10 @@ __device__ __forceinline__ int wave_excl_scan(int v, int lane) {
   return x - v;
 }
 
+template <typename KeyT>
 __global__ void __launch_bounds__(kIndelThreads) k_indel_emit(const GanonReadView V, const IndelInc *__restrict__ list,
                                                               int64_t n_list, int pos_bits, IndelObs *__restrict__ obs,
-                                                              unsigned long long *__restrict__ keys,
-                                                              uint32_t *__restrict__ vals) {
+                                                              KeyT *__restrict__ keys, uint32_t *__restrict__ vals) {
   const int lane = threadIdx.x & 63;
   const int64_t w = (int64_t)blockIdx.x * kIndelWaves + (threadIdx.x >> 6);
   if (w >= n_list) return;
@@ -83,8 +95,8 @@ __global__ void __launch_bounds__(kIndelThreads) k_indel_emit(const GanonReadVie
   const int r = e.read;
   const int nc = V.n_cig[r];
   const uint32_t *__restrict__ cig = V.cigar + V.cig_off[r];
-  const unsigned long long kscope = (unsigned long long)e.scope << pos_bits;
-  const int span0 = V.span_start[e.scope];
+  const int scope = (int)(e.scope_par & 0x7FFFFFFFu);
+  const int span0 = V.span_start[scope];
   int rcarry = V.ref_start[r], qcarry = 0;
   int64_t slot = e.obs_off;
   for (int k0 = 0; k0 < nc; k0 += 64) {
@@ -103,10 +115,10 @@ __global__ void __launch_bounds__(kIndelThreads) k_indel_emit(const GanonReadVie
       IndelObs ob;
       ob.read = r;
       ob.irp = irp;
-      ob.pos = pos;
+      ob.scope = scope;
       ob.type_len = (len << 1) | (op == 1 ? 1 : 0);
       obs[o] = ob;
-      keys[o] = kscope | (unsigned long long)(uint32_t)(pos - span0);
+      keys[o] = make_key<KeyT>(e.scope_par, pos_bits, (uint32_t)(pos - span0));
       vals[o] = (uint32_t)o;
     }
     slot += __popcll(m);
@@ -147,23 +159,17 @@ __device__ bool normal_covers(const GanonReadView &V, int scope, int pos) {
   return false;
 }
 
-// flags per sorted element: bit 0 = call record (first registered support of a masked TN call),
-// bit 1 = support record (a read the scope writes); rank = the call's registration rank at pos.
-// repk: scratch, registration key of each call's first support (UINT64_MAX = not a call head).
-__global__ void __launch_bounds__(256) k_indel_classify(const GanonReadView V, const unsigned long long *__restrict__ keys,
-                                                        const uint32_t *__restrict__ vals, int64_t n, int pos_bits,
-                                                        const IndelObs *__restrict__ obs, uint8_t *__restrict__ flags,
-                                                        int32_t *__restrict__ rank,
-                                                        unsigned long long *__restrict__ repk) {
-  const int64_t j0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j0 >= n) return;
-  const unsigned long long key = keys[j0];
-  if (j0 > 0 && keys[j0 - 1] == key) return;
+template <typename KeyT>
+__device__ void classify_run(const GanonReadView &V, const KeyT *__restrict__ keys, const uint32_t *__restrict__ vals,
+                             int64_t n, int pos_bits, const IndelObs *__restrict__ obs, uint8_t *__restrict__ flags,
+                             int32_t *__restrict__ rank, unsigned long long *__restrict__ repk, int64_t j0,
+                             unsigned long long *__restrict__ n_rec) {
+  const KeyT key = keys[j0];
   int64_t j1 = j0 + 1;
   while (j1 < n && keys[j1] == key) ++j1;
-  const int scope = (int)(key >> pos_bits);
-  const int pos = obs[vals[j0]].pos;
+  const int scope = obs[vals[j0]].scope;
   const unsigned long long kNone = ~0ull;
+  bool any_tn = false;
   // pass 1: call heads (first element of each distinct call, in sorted = slot order), TN state,
   // first registered support
   for (int64_t a = j0; a < j1; ++a) {
@@ -184,10 +190,19 @@ __global__ void __launch_bounds__(256) k_indel_classify(const GanonReadView V, c
       best = min(best, reg_key(V, oc, ic));
     }
     repk[a] = best;
-    // TN and a normal column at pos: bit 7 marks a masked call head until pass 2
-    if (t && nn && normal_covers(V, scope, pos)) flags[a] = 0x80;
+    if (t && nn) {
+      flags[a] = 0x80;         // TN call head; the normal column is checked once per run below
+      any_tn = true;
+    }
+  }
+  if (!any_tn) return;
+  const int pos = V.span_start[scope] + (int)((unsigned long long)key & ((1ull << pos_bits) - 1ull));
+  if (!normal_covers(V, scope, pos)) {
+    for (int64_t a = j0; a < j1; ++a) flags[a] = 0;
+    return;
   }
   // pass 2: ranks and records of the masked calls
+  unsigned long long recs = 0;
   for (int64_t a = j0; a < j1; ++a) {
     if (!(flags[a] & 0x80)) continue;
     const unsigned long long ka = repk[a];
@@ -212,26 +227,90 @@ __global__ void __launch_bounds__(256) k_indel_classify(const GanonReadView V, c
       if (f) {
         flags[c] = (uint8_t)((flags[c] & 0x80) | f);
         rank[c] = rk;
+        recs += (f & 1) + (f >> 1);
       }
     }
   }
   for (int64_t a = j0; a < j1; ++a) flags[a] &= 3;
+  if (recs) atomicAdd(n_rec, recs);
 }
 
-struct RecCount {
-  const uint8_t *flags;
-  int64_t n;
-  __host__ __device__ int64_t operator()(int64_t j) const {
-    if (j >= n) return 0;
-    const uint8_t f = flags[j];
-    return (int64_t)((f & 1) + ((f >> 1) & 1));
-  }
-};
+// Runs of equal keys = observations at one (scope, pos). Every element's flags start at 0; the
+// first element of each run with more than one observation goes to run_list. A workgroup covers
+// kRunChunk elements (coalesced, kRunPer per thread) and takes its list slots with ONE atomic add:
+// a single global counter hit once per wave serialises (~10 ns per add at the L2).
+constexpr int kRunPer = 16;
+constexpr int kRunChunk = 256 * kRunPer;
 
-__global__ void __launch_bounds__(256) k_indel_write(const unsigned long long *__restrict__ keys,
+template <typename KeyT>
+__global__ void __launch_bounds__(256) k_indel_runs(const KeyT *__restrict__ keys, int64_t n,
+                                                    uint8_t *__restrict__ flags, int32_t *__restrict__ run_list,
+                                                    unsigned int *__restrict__ run_count) {
+  __shared__ unsigned int wsum[4];
+  __shared__ unsigned int base;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t c0 = (int64_t)blockIdx.x * kRunChunk;
+  unsigned int heads = 0;   // bit i: element c0 + i * 256 + tid is a run head
+#pragma unroll
+  for (int i = 0; i < kRunPer; ++i) {
+    const int64_t j = c0 + (int64_t)i * 256 + threadIdx.x;
+    if (j < n) {
+      flags[j] = 0;
+      const KeyT k = keys[j];
+      if ((j == 0 || keys[j - 1] != k) && j + 1 < n && keys[j + 1] == k) heads |= 1u << i;
+    }
+  }
+  const unsigned int cnt = __popc(heads);
+  // block exclusive scan of cnt
+  unsigned int x = cnt;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned int y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[wave] = x;
+  __syncthreads();
+  unsigned int wbase = 0, total = 0;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    wbase += (w < wave) ? wsum[w] : 0u;
+    total += wsum[w];
+  }
+  if (threadIdx.x == 0) base = total ? atomicAdd(run_count, total) : 0u;
+  __syncthreads();
+  unsigned int o = base + wbase + x - cnt;
+#pragma unroll
+  for (int i = 0; i < kRunPer; ++i)
+    if (heads & (1u << i)) run_list[o++] = (int32_t)(c0 + (int64_t)i * 256 + threadIdx.x);
+}
+
+// One thread per run of k_indel_runs (grid-stride over the device-side count). flags per element:
+// bit 0 = call record (first registered support of a masked TN call), bit 1 = support record (a
+// read the scope writes); rank = the call's registration rank at pos. repk: scratch, registration
+// key of each call's first support (UINT64_MAX = not a call head). n_rec: records of the whole
+// batch (one atomic add per run that has any).
+template <typename KeyT>
+__global__ void __launch_bounds__(256) k_indel_classify(const GanonReadView V, const KeyT *__restrict__ keys,
+                                                        const uint32_t *__restrict__ vals, int64_t n, int pos_bits,
+                                                        const IndelObs *__restrict__ obs, uint8_t *__restrict__ flags,
+                                                        int32_t *__restrict__ rank,
+                                                        unsigned long long *__restrict__ repk,
+                                                        const int32_t *__restrict__ run_list,
+                                                        const unsigned int *__restrict__ run_count,
+                                                        unsigned long long *__restrict__ n_rec) {
+  const unsigned int n_runs = *run_count;
+  for (unsigned int ri = blockIdx.x * blockDim.x + threadIdx.x; ri < n_runs; ri += gridDim.x * blockDim.x)
+    classify_run<KeyT>(V, keys, vals, n, pos_bits, obs, flags, rank, repk, run_list[ri], n_rec);
+}
+
+
+// Records in device order (slots from an atomic counter; the host sorts them).
+template <typename KeyT>
+__global__ void __launch_bounds__(256) k_indel_write(const GanonReadView V, const KeyT *__restrict__ keys,
                                                      const uint32_t *__restrict__ vals, int64_t n, int pos_bits,
                                                      const IndelObs *__restrict__ obs, const uint8_t *__restrict__ flags,
-                                                     const int32_t *__restrict__ rank, const int64_t *__restrict__ offs,
+                                                     const int32_t *__restrict__ rank,
+                                                     unsigned long long *__restrict__ slot,
                                                      ganon_indel_rec *__restrict__ out) {
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
@@ -239,14 +318,14 @@ __global__ void __launch_bounds__(256) k_indel_write(const unsigned long long *_
   if (!f) return;
   const IndelObs o = obs[vals[j]];
   ganon_indel_rec rec;
-  rec.scope = (int32_t)(keys[j] >> pos_bits);
-  rec.pos = o.pos;
+  rec.scope = o.scope;
+  rec.pos = V.span_start[o.scope] + (int)((unsigned long long)keys[j] & ((1ull << pos_bits) - 1ull));
   rec.length = o.type_len >> 1;
   rec.type = (o.type_len & 1) ? GANON_INDEL_INS : GANON_INDEL_DEL;
   rec.rank = rank[j];
   rec.read = o.read;
   rec.in_read_pos = o.irp;
-  int64_t w = offs[j];
+  unsigned long long w = atomicAdd(slot, (unsigned long long)((f & 1) + (f >> 1)));
   if (f & 1) {
     rec.kind = GANON_INDEL_CALL;
     out[w++] = rec;
@@ -269,16 +348,21 @@ struct ganon_indels {
   std::vector<void *> allocs;
   GanonReadView V{};
   int64_t n_obs = 0, n_list = 0, n_records = -1;
+  int32_t n_seg = 0;                  // scopes with observations (segments of the sort)
   int pos_bits = 1, key_bits = 2;
+  bool global = false;                // sort strategy of the last run (GANON_PARAM_INDEL_SORT)
   IndelInc *list = nullptr;
   IndelObs *obs = nullptr;
-  unsigned long long *keys[2] = {nullptr, nullptr};
+  int32_t *seg_off = nullptr;         // [n_seg + 1] observation offsets of the segments
+  void *keys[2] = {nullptr, nullptr}; // 8 bytes per observation (either key width)
   uint32_t *vals[2] = {nullptr, nullptr};
   int sorted_sel = 0;                 // which half of the double buffers holds the sorted pairs
   uint8_t *flags = nullptr;
   int32_t *rank = nullptr;
   unsigned long long *repk = nullptr;
-  int64_t *offs = nullptr;            // [n_obs + 1]
+  unsigned long long *counters = nullptr;   // [0] records (classify), [1] write slots
+  int32_t *run_list = nullptr;        // first element of each run of >1 observations
+  unsigned int *run_count = nullptr;
   void *temp = nullptr;
   size_t temp_bytes = 0;
   ganon_indel_rec *recs = nullptr;
@@ -303,6 +387,58 @@ void ind_release(ganon_indels *t) {
   t->allocs.clear();
 }
 
+template <typename KeyT>
+hipError_t sort_pairs(ganon_indels *t, void *temp, size_t &bytes, bool global, hipStream_t st, int *sel) {
+  hipcub::DoubleBuffer<KeyT> K(static_cast<KeyT *>(t->keys[0]), static_cast<KeyT *>(t->keys[1]));
+  hipcub::DoubleBuffer<uint32_t> Vb(t->vals[0], t->vals[1]);
+  hipError_t e;
+  if (global)
+    e = hipcub::DeviceRadixSort::SortPairs(temp, bytes, K, Vb, (int)t->n_obs, 0, t->key_bits, st);
+  else
+    e = hipcub::DeviceSegmentedRadixSort::SortPairs(temp, bytes, K, Vb, (int)t->n_obs, t->n_seg, t->seg_off,
+                                                     t->seg_off + 1, 0, t->pos_bits, st);
+  if (sel) *sel = (K.selector == Vb.selector) ? K.selector : -1;
+  return e;
+}
+
+template <typename KeyT>
+int run_tally(ganon_ctx *ctx, ganon_indels *t) {
+  int rc;
+  const int64_t n = t->n_obs;
+  HIP_OR_FAIL(hipMemsetAsync(t->counters, 0, 2 * sizeof(unsigned long long), ctx->stream));
+  HIP_OR_FAIL(hipMemsetAsync(t->run_count, 0, sizeof(unsigned int), ctx->stream));
+  {
+    KernelScope ks(ctx, "k_indel_emit");
+    const unsigned grid = (unsigned)((t->n_list + kIndelWaves - 1) / kIndelWaves);
+    hipLaunchKernelGGL(k_indel_emit<KeyT>, dim3(grid), dim3(kIndelThreads), 0, ctx->stream, t->V, t->list, t->n_list,
+                       t->pos_bits, t->obs, static_cast<KeyT *>(t->keys[0]), t->vals[0]);
+    if ((rc = check_launch(ctx, "k_indel_emit"))) return rc;
+  }
+  {
+    KernelScope ks(ctx, "indel_sort");
+    size_t bytes = t->temp_bytes;
+    int sel = 0;
+    if (sort_pairs<KeyT>(t, t->temp, bytes, t->global, ctx->stream, &sel) != hipSuccess)
+      return fail(ctx, GANON_E_DEVICE, "indel radix sort failed");
+    if (sel < 0) return fail(ctx, GANON_E_DEVICE, "indel radix sort: key/value buffers diverged");
+    t->sorted_sel = sel;
+  }
+  {
+    KernelScope ks(ctx, "k_indel_classify");
+    const KeyT *keys = static_cast<const KeyT *>(t->keys[t->sorted_sel]);
+    hipLaunchKernelGGL(k_indel_runs<KeyT>, dim3((unsigned)((n + kRunChunk - 1) / kRunChunk)), dim3(256), 0,
+                       ctx->stream, keys, n, t->flags, t->run_list, t->run_count);
+    // runs <= n / 2 (the count stays on the device): one thread per possible run, the threads past
+    // the count leave at once
+    const unsigned grid = (unsigned)((n / 2 + 255) / 256);
+    hipLaunchKernelGGL(k_indel_classify<KeyT>, dim3(grid), dim3(256), 0, ctx->stream, t->V, keys,
+                       t->vals[t->sorted_sel], n, t->pos_bits, t->obs, t->flags, t->rank, t->repk, t->run_list,
+                       t->run_count, t->counters);
+    if ((rc = check_launch(ctx, "k_indel_classify"))) return rc;
+  }
+  return GANON_OK;
+}
+
 }  // namespace
 
 GANON_API int ganon_indel_upload(ganon_ctx *ctx, const ganon_batch *b, const ganon_dbatch *db, ganon_indels **out) {
@@ -324,22 +460,27 @@ GANON_API int ganon_indel_upload(ganon_ctx *ctx, const ganon_batch *b, const gan
     nid[r] = k;
   }
   std::vector<IndelInc> list;
+  std::vector<int32_t> seg_off(1, 0);
   int64_t n_obs = 0;
   int32_t max_span = 0;
   for (int32_t s = 0; s < b->n_scopes; ++s) {
     max_span = std::max(max_span, b->scope_span_len[s]);
+    const uint32_t par = (uint32_t)((seg_off.size() - 1) & 1) << 31;
+    const int64_t before = n_obs;
     for (int64_t i = b->scope_incid_off[s]; i < b->scope_incid_off[s + 1]; ++i) {
       const int32_t r = b->incid_read[i];
       if (!nid[r]) continue;
-      list.push_back(IndelInc{r, s, n_obs});
+      list.push_back(IndelInc{r, (uint32_t)s | par, n_obs});
       n_obs += nid[r];
     }
+    if (n_obs > before) seg_off.push_back((int32_t)std::min<int64_t>(n_obs, INT32_MAX));
   }
   if (n_obs >= (int64_t)INT32_MAX) return fail(ctx, GANON_E_ARG, "indel upload: %lld observations (max 2^31-1)", (long long)n_obs);
   ganon_indels *t = new ganon_indels();
   t->V = V;
   t->n_obs = n_obs;
   t->n_list = (int64_t)list.size();
+  t->n_seg = (int32_t)seg_off.size() - 1;
   t->pos_bits = bits_for((int64_t)max_span);
   t->key_bits = t->pos_bits + bits_for(std::max<int64_t>((int64_t)b->n_scopes - 1, 1));
   int rc = GANON_OK;
@@ -348,32 +489,31 @@ GANON_API int ganon_indel_upload(ganon_ctx *ctx, const ganon_batch *b, const gan
     delete t;
     return code;
   };
-  if (t->key_bits > 64) return bail(fail(ctx, GANON_E_ARG, "indel upload: sort key needs %d bits", t->key_bits));
+  if (t->pos_bits > 31 || t->key_bits > 64) return bail(fail(ctx, GANON_E_ARG, "indel upload: sort key needs %d bits", t->key_bits));
   if (n_obs > 0) {
     if ((rc = ind_alloc(ctx, t, &t->list, list.size()))) return bail(rc);
     if ((rc = ind_alloc(ctx, t, &t->obs, (size_t)n_obs))) return bail(rc);
+    if ((rc = ind_alloc(ctx, t, &t->seg_off, seg_off.size()))) return bail(rc);
     for (int h = 0; h < 2; ++h) {
-      if ((rc = ind_alloc(ctx, t, &t->keys[h], (size_t)n_obs))) return bail(rc);
+      if ((rc = ind_alloc(ctx, t, reinterpret_cast<unsigned long long **>(&t->keys[h]), (size_t)n_obs))) return bail(rc);
       if ((rc = ind_alloc(ctx, t, &t->vals[h], (size_t)n_obs))) return bail(rc);
     }
     if ((rc = ind_alloc(ctx, t, &t->flags, (size_t)n_obs))) return bail(rc);
     if ((rc = ind_alloc(ctx, t, &t->rank, (size_t)n_obs))) return bail(rc);
     if ((rc = ind_alloc(ctx, t, &t->repk, (size_t)n_obs))) return bail(rc);
-    if ((rc = ind_alloc(ctx, t, &t->offs, (size_t)n_obs + 1))) return bail(rc);
-    // temp storage: max of the sort's and the scan's
-    size_t sort_bytes = 0, scan_bytes = 0;
-    hipcub::DoubleBuffer<unsigned long long> K(t->keys[0], t->keys[1]);
-    hipcub::DoubleBuffer<uint32_t> Vb(t->vals[0], t->vals[1]);
-    if (hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, K, Vb, (int)n_obs, 0, t->key_bits, ctx->stream) !=
-        hipSuccess)
+    if ((rc = ind_alloc(ctx, t, &t->counters, 2))) return bail(rc);
+    if ((rc = ind_alloc(ctx, t, &t->run_list, (size_t)n_obs / 2 + 1))) return bail(rc);
+    if ((rc = ind_alloc(ctx, t, &t->run_count, 1))) return bail(rc);
+    // temp storage: the larger of the two sort strategies
+    size_t seg_bytes = 0, glob_bytes = 0;
+    if (sort_pairs<uint32_t>(t, nullptr, seg_bytes, false, ctx->stream, nullptr) != hipSuccess ||
+        sort_pairs<unsigned long long>(t, nullptr, glob_bytes, true, ctx->stream, nullptr) != hipSuccess)
       return bail(fail(ctx, GANON_E_DEVICE, "indel upload: radix sort sizing failed"));
-    hipcub::CountingInputIterator<int64_t> cnt(0);
-    hipcub::TransformInputIterator<int64_t, RecCount, hipcub::CountingInputIterator<int64_t>> it(cnt, RecCount{t->flags, n_obs});
-    if (hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, it, t->offs, (int)(n_obs + 1), ctx->stream) != hipSuccess)
-      return bail(fail(ctx, GANON_E_DEVICE, "indel upload: scan sizing failed"));
-    t->temp_bytes = std::max(sort_bytes, scan_bytes);
+    t->temp_bytes = std::max(seg_bytes, glob_bytes);
     if ((rc = ind_alloc(ctx, t, reinterpret_cast<uint8_t **>(&t->temp), t->temp_bytes))) return bail(rc);
     hipError_t e = hipMemcpyAsync(t->list, list.data(), list.size() * sizeof(IndelInc), hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(t->seg_off, seg_off.data(), seg_off.size() * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     if (e != hipSuccess) return bail(fail(ctx, GANON_E_DEVICE, "indel upload copy failed: %s", hipGetErrorString(e)));
   }
@@ -387,43 +527,8 @@ GANON_API int ganon_indel_run(ganon_ctx *ctx, ganon_indels *t) {
   t->ran = true;
   t->n_records = -1;
   if (t->n_obs == 0) return GANON_OK;
-  int rc;
-  const int64_t n = t->n_obs;
-  {
-    KernelScope ks(ctx, "k_indel_emit");
-    const unsigned grid = (unsigned)((t->n_list + kIndelWaves - 1) / kIndelWaves);
-    hipLaunchKernelGGL(k_indel_emit, dim3(grid), dim3(kIndelThreads), 0, ctx->stream, t->V, t->list, t->n_list,
-                       t->pos_bits, t->obs, t->keys[0], t->vals[0]);
-    if ((rc = check_launch(ctx, "k_indel_emit"))) return rc;
-  }
-  {
-    KernelScope ks(ctx, "indel_sort");
-    hipcub::DoubleBuffer<unsigned long long> K(t->keys[0], t->keys[1]);
-    hipcub::DoubleBuffer<uint32_t> Vb(t->vals[0], t->vals[1]);
-    size_t bytes = t->temp_bytes;
-    if (hipcub::DeviceRadixSort::SortPairs(t->temp, bytes, K, Vb, (int)n, 0, t->key_bits, ctx->stream) != hipSuccess)
-      return fail(ctx, GANON_E_DEVICE, "indel radix sort failed");
-    t->sorted_sel = K.selector;
-    if (Vb.selector != K.selector) return fail(ctx, GANON_E_DEVICE, "indel radix sort: key/value buffers diverged");
-  }
-  const unsigned long long *keys = t->keys[t->sorted_sel];
-  const uint32_t *vals = t->vals[t->sorted_sel];
-  const unsigned grid = (unsigned)((n + 255) / 256);
-  {
-    KernelScope ks(ctx, "k_indel_classify");
-    hipLaunchKernelGGL(k_indel_classify, dim3(grid), dim3(256), 0, ctx->stream, t->V, keys, vals, n, t->pos_bits,
-                       t->obs, t->flags, t->rank, t->repk);
-    if ((rc = check_launch(ctx, "k_indel_classify"))) return rc;
-  }
-  {
-    KernelScope ks(ctx, "indel_scan");
-    hipcub::CountingInputIterator<int64_t> cnt(0);
-    hipcub::TransformInputIterator<int64_t, RecCount, hipcub::CountingInputIterator<int64_t>> it(cnt, RecCount{t->flags, n});
-    size_t bytes = t->temp_bytes;
-    if (hipcub::DeviceScan::ExclusiveSum(t->temp, bytes, it, t->offs, (int)(n + 1), ctx->stream) != hipSuccess)
-      return fail(ctx, GANON_E_DEVICE, "indel scan failed");
-  }
-  return GANON_OK;
+  t->global = ctx->indel_sort != 0;
+  return t->global ? run_tally<unsigned long long>(ctx, t) : run_tally<uint32_t>(ctx, t);
 }
 
 GANON_API int64_t ganon_indel_download(ganon_ctx *ctx, ganon_indels *t, ganon_indel_rec *out, int64_t cap) {
@@ -434,34 +539,42 @@ GANON_API int64_t ganon_indel_download(ganon_ctx *ctx, ganon_indels *t, ganon_in
     t->n_records = 0;
     return 0;
   }
-  int64_t total = 0;
-  hipError_t e = hipMemcpyAsync(&total, t->offs + t->n_obs, sizeof total, hipMemcpyDeviceToHost, ctx->stream);
+  unsigned long long total = 0;
+  hipError_t e = hipMemcpyAsync(&total, t->counters, sizeof total, hipMemcpyDeviceToHost, ctx->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
   if (e != hipSuccess) return fail(ctx, GANON_E_DEVICE, "indel download: %s", hipGetErrorString(e));
-  t->n_records = total;
-  if (!out || cap < total || total == 0) return total;
-  if (t->recs_cap < total) {
+  t->n_records = (int64_t)total;
+  if (!out || cap < (int64_t)total || total == 0) return (int64_t)total;
+  if (t->recs_cap < (int64_t)total) {
     int rc = ind_alloc(ctx, t, &t->recs, (size_t)total);
     if (rc) return rc;
-    t->recs_cap = total;
+    t->recs_cap = (int64_t)total;
   }
   const int64_t n = t->n_obs;
-  hipLaunchKernelGGL(k_indel_write, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream,
-                     t->keys[t->sorted_sel], t->vals[t->sorted_sel], n, t->pos_bits, t->obs, t->flags, t->rank,
-                     t->offs, t->recs);
+  const unsigned grid = (unsigned)((n + 255) / 256);
+  e = hipMemsetAsync(t->counters + 1, 0, sizeof(unsigned long long), ctx->stream);
+  if (e != hipSuccess) return fail(ctx, GANON_E_DEVICE, "indel download: %s", hipGetErrorString(e));
+  if (t->global)
+    hipLaunchKernelGGL(k_indel_write<unsigned long long>, dim3(grid), dim3(256), 0, ctx->stream, t->V,
+                       static_cast<const unsigned long long *>(t->keys[t->sorted_sel]), t->vals[t->sorted_sel], n,
+                       t->pos_bits, t->obs, t->flags, t->rank, t->counters + 1, t->recs);
+  else
+    hipLaunchKernelGGL(k_indel_write<uint32_t>, dim3(grid), dim3(256), 0, ctx->stream, t->V,
+                       static_cast<const uint32_t *>(t->keys[t->sorted_sel]), t->vals[t->sorted_sel], n, t->pos_bits,
+                       t->obs, t->flags, t->rank, t->counters + 1, t->recs);
   int rc = check_launch(ctx, "k_indel_write");
   if (rc) return rc;
   e = hipMemcpyAsync(out, t->recs, (size_t)total * sizeof(ganon_indel_rec), hipMemcpyDeviceToHost, ctx->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
   if (e != hipSuccess) return fail(ctx, GANON_E_DEVICE, "indel download: %s", hipGetErrorString(e));
-  return total;
+  return (int64_t)total;
 }
 
 GANON_API int ganon_indel_info(const ganon_indels *t, int64_t *info4) {
   if (!t || !info4) return GANON_E_ARG;
   info4[0] = t->n_obs;
   info4[1] = t->n_list;
-  info4[2] = t->key_bits;
+  info4[2] = t->global ? t->key_bits : t->pos_bits;
   info4[3] = t->n_records;
   return GANON_OK;
 }

@@ -125,9 +125,12 @@ GANON_API int ganon_ctx_set_variant(ganon_ctx *ctx, int variant);
  * GANON_PARAM_FASTQ_KD: output dwords per lane the FASTQ formatter loads at once (1, 2, 4).
  * GANON_PARAM_FASTQ_SKIP (phase timing only, changes results): bit 0 leaves out the
  * formatter's source loads, bit 1 its stores; bits 3-6 stop after the descriptor scan / after the
- * dword map / leave out the interior pass / leave out the edge and constant bytes. */
+ * dword map / leave out the interior pass / leave out the edge and constant bytes.
+ * GANON_PARAM_INDEL_SORT: the indel tally sorts its observations per scope (0, default: segmented,
+ * 32-bit position keys) or in one global sort of 64-bit scope|position keys (1). */
 enum { GANON_PARAM_GROUP_UNROLL = 1, GANON_PARAM_GROUP_SKIP = 2, GANON_PARAM_GROUP_TARGET = 3,
-       GANON_PARAM_NT_COPY = 4, GANON_PARAM_REF2 = 5, GANON_PARAM_FASTQ_SKIP = 6, GANON_PARAM_FASTQ_KD = 7 };
+       GANON_PARAM_NT_COPY = 4, GANON_PARAM_REF2 = 5, GANON_PARAM_FASTQ_SKIP = 6, GANON_PARAM_FASTQ_KD = 7,
+       GANON_PARAM_INDEL_SORT = 8 };
 GANON_API int ganon_ctx_set_param(ganon_ctx *ctx, int param, int value);
 /* When on, ganon_batch_run records a HIP event pair around each kernel it launches. */
 GANON_API int ganon_ctx_set_profiling(ganon_ctx *ctx, int enabled);

@@ -143,9 +143,12 @@ def test_hip_indel_tally_matches_oracle(seed, hip_built):
     m = native.HipMasker(0)
     try:
         *_, got = m.mask(arr, indels=True)
+        m.set_param(native.PARAM_INDEL_SORT, 1)
+        *_, got_global = m.mask(arr, indels=True)
     finally:
         m.close()
     assert np.array_equal(got, want)
+    assert np.array_equal(got_global, want)
 
 
 @pytest.mark.gpu
@@ -175,12 +178,15 @@ def test_hip_indel_long_reads_match_oracle(hip_built):
     try:
         db = m.upload(arr)
         t = db.indel_tally(arr)
-        t.run()
-        got = t.download()
-        info = t.info()
+        for mode in (0, 1):     # segmented per-scope sort (default), one global sort
+            m.set_param(native.PARAM_INDEL_SORT, mode)
+            t.run()
+            got = t.download()
+            info = t.info()
+            assert info["observations"] > 10_000
+            assert np.array_equal(got, want), mode
+        m.set_param(native.PARAM_INDEL_SORT, 0)
         t.free()
         db.free()
     finally:
         m.close()
-    assert info["observations"] > 10_000
-    assert np.array_equal(got, want)

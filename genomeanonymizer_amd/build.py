@@ -81,13 +81,16 @@ def build_hip(force: bool = False) -> str:
     return HIP_LIB
 
 
+HOST_SOURCES = ("ganon_host.cpp", "ganon_plan.cpp")
+
+
 def build_host(force: bool = False) -> str:
-    src = os.path.join(CSRC, "ganon_host.cpp")
+    srcs = [os.path.join(CSRC, s) for s in HOST_SOURCES]
     hdr = os.path.join(REPO, "include", "ganon_host.h")
-    if force or _stale(HOST_LIB, [src, hdr, __file__]):
+    if force or _stale(HOST_LIB, srcs + [hdr, __file__]):
         tmp = HOST_LIB + ".tmp"
         _run(["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-fvisibility=hidden", "-pthread",
-              "-o", tmp, src, "-lz"])
+              "-o", tmp] + srcs + ["-lz"])
         os.replace(tmp, HOST_LIB)
     return HOST_LIB
 

@@ -1,0 +1,737 @@
+// ganon_plan.cpp — native host scope scheduler, part of libganon_host.so;
+// C ABI in include/ganon_host.h (ganon_plan_*).
+//
+// The same plan as genomeanonymizer_amd/planner.py (SamplePlanner.run), at native speed: it
+// restates, without masking anything, the control flow of anonymize_genome
+// (short_read_tumor_normal_anonymizer.py:625-760) for one tumor/normal pair —
+//   sections           get_genome_sections (SR:245-276)
+//   variant windows    anonymize_window (SR:279-372) over a pileup of [first, last)
+//                      (pileup_io.pyx:8-41: mapped reads overlapping the region, file order)
+//   gaps               anonymize_inter_window_region (SR:498-558) driven by iter_fetch_pair
+//                      (pileup_io.pyx:124-298) and its cluster rules
+//   yield order        CompleteGermlineAnonymizer.anonymize (anonymizer_methods.py:472-532,
+//                      SURVEY Q11): a complete pair at the first normal column past its rightmost
+//                      end, pairs at one column in first-appearance order, the rest at scope end
+//   pairing            write_pair / written_read_ids (SR:134-165), to_pair_anonymized_reads
+//                      first-object-wins (AM:320-389), pair_unmapped_or_non_pileup_pairs_and_write
+//                      (SR:375-406), pair_unmapped_mates (SR:561-600), write_single_end_reads
+//                      (SR:603-622)
+//   statistics         the recorder's window/outside/scope events (SR:175-242)
+// and the reference's errors (region errors Q4, unflagged mates Q8, reads without SEQ, names in
+// both samples Q10) as error codes + messages. The output is column arrays; the Python planner
+// stays as a second implementation the tests compare against.
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <string_view>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+#include "../../include/ganon_host.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+struct PlanError {
+  int code;
+  std::string msg;
+};
+
+[[noreturn]] void raise(int code, const std::string &msg) { throw PlanError{code, msg}; }
+
+struct Inst {
+  int32_t ds;
+  int32_t scope;   // -1 = unmasked
+  int64_t row;
+};
+
+constexpr int32_t kFlagUnmap = 0x4, kFlagRead1 = 0x40, kFlagRead2 = 0x80;
+
+struct Table {
+  const ganon_plan_table *t = nullptr;
+  struct Ix {
+    bool built = false;
+    std::vector<int64_t> rows, pos;
+    int64_t span = 1;
+  };
+  std::vector<Ix> index;   // per BAM tid
+
+  bool unmapped(int64_t r) const { return (t->flag[r] & kFlagUnmap) != 0; }
+  int mate_idx(int64_t r) const {
+    return (t->flag[r] & kFlagRead1) ? 0 : (t->flag[r] & kFlagRead2) ? 1 : -1;
+  }
+  std::string name(int64_t r) const { return std::string(t->names + t->name_off[r], (size_t)t->name_len[r]); }
+};
+
+struct PairSlot {
+  Inst p[2];
+  bool has[2] = {false, false};
+  uint64_t seq = 0;   // insertion order (dict order: a deleted key re-inserted goes last)
+};
+
+struct ScopeRec {
+  int32_t contig, window;
+  int64_t first, last, span_start, span_end;
+  int64_t t0, t1, n0, n1;   // ranges in t_rows / n_rows
+};
+
+class Planner {
+ public:
+  Planner(const ganon_plan_input *in) : in_(in) {
+    for (int d = 0; d < 2; ++d) {
+      tab_[d].t = &in->tables[d];
+      tab_[d].index.resize((size_t)std::max(in->tables[d].n_ref, 0));
+    }
+  }
+
+  void run() {
+    name_ids();
+    const std::vector<Section> secs = sections();
+    for (const Section &w : secs) {
+      if (w.window >= 0) {
+        stats_.push_back(0);
+        stats_.push_back(w.window);
+        anonymize_window(w.contig, w.first, w.last, w.window, true);
+      } else {
+        stats_.push_back(1);
+        stats_.push_back(-1);
+        inter_window(w);
+      }
+    }
+    if (!to_pair_.empty()) pair_unmapped_mates();
+    for (int64_t k : written_) to_pair_.erase(k);
+    std::vector<std::pair<uint64_t, const PairSlot *>> rest;
+    rest.reserve(to_pair_.size());
+    for (const auto &kv : to_pair_) rest.emplace_back(kv.second.seq, &kv.second);
+    std::sort(rest.begin(), rest.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
+    for (const auto &e : rest) {
+      const Inst &i = e.second->has[0] ? e.second->p[0] : e.second->p[1];
+      single_[i.ds].push_back(i.row);
+      single_[i.ds].push_back(i.scope);
+    }
+    write_single_end_ = !to_pair_.empty();
+  }
+
+  // results
+  std::vector<ScopeRec> scopes_;
+  std::vector<int64_t> t_rows_, n_rows_;
+  std::vector<int32_t> events_;       // 7 per event: kind, hid, ds, slot, inst ds, inst scope, 0
+  std::vector<int64_t> event_rows_;   // inst row per event (write) or -1
+  std::vector<int32_t> stats_;        // 2 per event: kind (0 window, 1 outside, 2 scope), value
+  std::vector<int64_t> single_[2];    // (row, scope) pairs
+  bool write_single_end_ = false;
+
+ private:
+  struct Section {
+    int32_t contig;
+    int64_t first, last;
+    int32_t window;   // -1 = gap / whole contig
+  };
+
+  const ganon_plan_input *in_;
+  Table tab_[2];
+  std::vector<int64_t> nid_[2];       // name id per row
+  std::unordered_map<int64_t, PairSlot> to_pair_;
+  uint64_t pair_seq_ = 0;
+  std::unordered_set<int64_t> written_;
+  int32_t next_hid_ = 0;
+
+  std::string contig_name(int32_t c) const {
+    return std::string(in_->contig_names + in_->contig_name_off[c]);
+  }
+
+  // names -> ids; the same name in both samples is the reference's silent mix-up (Q10)
+  void name_ids() {
+    std::unordered_map<std::string_view, int64_t> ids;
+    ids.reserve((size_t)(in_->tables[0].n + in_->tables[1].n));
+    int64_t tumor_ids = 0;
+    for (int d = 0; d < 2; ++d) {
+      const ganon_plan_table &t = in_->tables[d];
+      nid_[d].resize((size_t)t.n);
+      int64_t shared = 0;
+      for (int64_t r = 0; r < t.n; ++r) {
+        std::string_view nm(t.names + t.name_off[r], (size_t)t.name_len[r]);
+        auto it = ids.find(nm);
+        if (it == ids.end()) {
+          const int64_t id = (int64_t)ids.size();
+          ids.emplace(nm, id);
+          nid_[d][r] = id;
+        } else {
+          nid_[d][r] = it->second;
+          if (d == 1 && it->second < tumor_ids) ++shared;
+        }
+      }
+      if (d == 0) tumor_ids = (int64_t)ids.size();
+      else if (shared) {
+        // count distinct shared names like the Python set intersection
+        std::unordered_set<int64_t> s;
+        for (int64_t r = 0; r < t.n; ++r)
+          if (nid_[1][r] < tumor_ids) s.insert(nid_[1][r]);
+        raise(GANON_PLAN_E_VALUE, std::to_string(s.size()) +
+                                      " read names occur in both the tumor and the normal BAM; the reference keys "
+                                      "reads by name only and mixes such reads (SURVEY Q10)");
+      }
+    }
+  }
+
+  // ---- sections (SR:245-276) ----
+  std::vector<Section> sections() const {
+    std::vector<std::vector<int32_t>> by_seq((size_t)in_->n_contigs);
+    for (int32_t w = 0; w < in_->n_windows; ++w) by_seq[(size_t)in_->win_contig[w]].push_back(w);
+    std::vector<Section> out;
+    for (int32_t c = 0; c < in_->n_contigs; ++c) {
+      const auto &ws = by_seq[(size_t)c];
+      if (ws.empty()) {
+        out.push_back(Section{c, 0, 0, -1});
+        continue;
+      }
+      int64_t first = 1;
+      for (int32_t w : ws) {
+        out.push_back(Section{c, first, in_->win_first[w] - 1, -1});
+        first = in_->win_last[w] + 1;
+        out.push_back(Section{c, in_->win_first[w], in_->win_last[w], w});
+      }
+      out.push_back(Section{c, first, in_->contig_len[c] - 1, -1});
+    }
+    std::stable_sort(out.begin(), out.end(), [](const Section &a, const Section &b) {
+      if (a.contig != b.contig) return a.contig < b.contig;
+      if (a.first != b.first) return a.first < b.first;
+      return a.last < b.last;
+    });
+    return out;
+  }
+
+  // ---- htslib-style region query (io/bam.py ReadTable.fetch) ----
+  int32_t tid_of(int ds, int32_t contig) const {
+    const int32_t tid = in_->tables[ds].tid_of_contig[contig];
+    if (tid < 0) raise(GANON_PLAN_E_VALUE, "invalid contig `" + contig_name(contig) + "`");
+    return tid;
+  }
+
+  const Table::Ix &tid_index(int ds, int32_t tid) {
+    Table &T = tab_[ds];
+    Table::Ix &ix = T.index[(size_t)tid];
+    if (ix.built) return ix;
+    const ganon_plan_table &t = *T.t;
+    int64_t span = 0;
+    bool any = false;
+    for (int64_t r = 0; r < t.n; ++r) {
+      if (t.tid[r] != tid) continue;
+      if (!ix.pos.empty() && t.pos[r] < ix.pos.back())
+        raise(GANON_PLAN_E_VALUE, "records of contig " + std::to_string(tid) + " are not coordinate sorted");
+      ix.rows.push_back(r);
+      ix.pos.push_back(t.pos[r]);
+      span = any ? std::max(span, (int64_t)t.end[r] - t.pos[r]) : (int64_t)t.end[r] - t.pos[r];
+      any = true;
+    }
+    ix.span = any ? span : 1;
+    ix.built = true;
+    return ix;
+  }
+
+  // rows overlapping [start, stop) (whole contig when has_* is false), file order
+  void fetch(int ds, int32_t contig, bool has_start, int64_t start, bool has_stop, int64_t stop,
+             std::vector<int64_t> &out) {
+    out.clear();
+    const int32_t tid = tid_of(ds, contig);
+    const int64_t length = in_->tables[ds].ref_len[tid];
+    const int64_t rstart = has_start ? start : 0;
+    const int64_t rstop = has_stop ? stop : length;
+    if (rstart > rstop)
+      raise(GANON_PLAN_E_VALUE, "invalid coordinates: start (" + std::to_string(rstart) + ") > stop (" +
+                                    std::to_string(rstop) + ")");
+    if (rstart < 0) raise(GANON_PLAN_E_VALUE, "start out of range (" + std::to_string(rstart) + ")");
+    const Table::Ix &ix = tid_index(ds, tid);
+    const size_t lo = (size_t)(std::lower_bound(ix.pos.begin(), ix.pos.end(), rstart - ix.span) - ix.pos.begin());
+    const size_t hi = (size_t)(std::lower_bound(ix.pos.begin(), ix.pos.end(), rstop) - ix.pos.begin());
+    const int32_t *end = in_->tables[ds].end;
+    for (size_t i = lo; i < hi; ++i)
+      if (end[ix.rows[i]] > rstart) out.push_back(ix.rows[i]);
+  }
+
+  // ---- read helpers ----
+  int slot(int ds, int64_t row) const {
+    const int s = tab_[ds].mate_idx(row);
+    if (s < 0)
+      raise(GANON_PLAN_E_TYPE, "read '" + tab_[ds].name(row) +
+                                   "' has neither the READ1 nor the READ2 flag; the reference cannot store it (SURVEY Q8)");
+    return s;
+  }
+
+  // reference_end, or -1 for None (unmapped / no CIGAR)
+  int64_t ref_end(int ds, int64_t row) const {
+    const ganon_plan_table &t = in_->tables[ds];
+    if ((t.flag[row] & kFlagUnmap) || t.n_cigar[row] == 0) return -1;
+    return t.end[row];
+  }
+
+  // ---- pairing / writing ----
+  int32_t open_handle() {
+    const int32_t h = next_hid_++;
+    events_.insert(events_.end(), {0, h, 0, 0, 0, 0, 0});
+    event_rows_.push_back(-1);
+    return h;
+  }
+  void close_handle(int32_t h) {
+    events_.insert(events_.end(), {2, h, 0, 0, 0, 0, 0});
+    event_rows_.push_back(-1);
+  }
+  void log_write(int32_t h, int ds, int sl, const Inst &i) {
+    events_.insert(events_.end(), {1, h, ds, sl, i.ds, i.scope, 0});
+    event_rows_.push_back(i.row);
+  }
+
+  void write_pair(const Inst &i0, const Inst &i1, int32_t hid) {
+    const int64_t name = nid_[i0.ds][(size_t)i0.row];
+    if (!written_.insert(name).second) return;
+    log_write(hid, i0.ds, 0, i0);
+    log_write(hid, i0.ds, 1, i1);
+  }
+
+  PairSlot &store_first(const Inst &inst) {
+    const int64_t name = nid_[inst.ds][(size_t)inst.row];
+    const int sl = slot(inst.ds, inst.row);
+    auto it = to_pair_.find(name);
+    if (it == to_pair_.end()) {
+      it = to_pair_.emplace(name, PairSlot{}).first;
+      it->second.seq = pair_seq_++;
+    }
+    PairSlot &p = it->second;
+    if (!p.has[sl]) {
+      p.p[sl] = inst;
+      p.has[sl] = true;
+    }
+    return p;
+  }
+
+  void passthrough(int ds, int64_t row, int32_t hid) {
+    if (in_->tables[ds].l_seq[row] == 0)
+      raise(GANON_PLAN_E_TYPE, "read '" + tab_[ds].name(row) + "' has no SEQ; the reference cannot upper-case it");
+    PairSlot &p = store_first(Inst{ds, -1, row});
+    if (p.has[0] && p.has[1]) write_pair(p.p[0], p.p[1], hid);
+  }
+
+  // ---- scopes ----
+  void pileup_reads(int ds, int32_t contig, int64_t first, int64_t last, std::vector<int64_t> &out) {
+    std::vector<int64_t> rows;
+    fetch(ds, contig, true, first, true, last, rows);
+    out.clear();
+    const ganon_plan_table &t = in_->tables[ds];
+    for (int64_t r : rows) {
+      if (t.flag[r] & kFlagUnmap) continue;
+      if (t.n_cigar[r] == 0) raise(GANON_PLAN_E_TYPE, "mapped read without CIGAR in a pileup (reference_end is None)");
+      out.push_back(r);
+    }
+  }
+
+  int32_t new_scope(int32_t contig, int64_t first, int64_t last, int32_t window) {
+    std::vector<int64_t> tr, nr;
+    pileup_reads(0, contig, first, last, tr);
+    pileup_reads(1, contig, first, last, nr);
+    tid_of(0, contig);
+    tid_of(1, contig);
+    ScopeRec sc{};
+    sc.contig = contig;
+    sc.window = window;
+    sc.first = first;
+    sc.last = last;
+    bool any = false;
+    int64_t s0 = 0, s1 = 0;
+    for (int d = 0; d < 2; ++d) {
+      const ganon_plan_table &t = in_->tables[d];
+      for (int64_t r : (d == 0 ? tr : nr)) {
+        s0 = any ? std::min<int64_t>(s0, t.pos[r]) : t.pos[r];
+        s1 = any ? std::max<int64_t>(s1, t.end[r]) : t.end[r];
+        any = true;
+      }
+    }
+    sc.span_start = any ? s0 : 0;
+    sc.span_end = any ? s1 : 0;
+    sc.t0 = (int64_t)t_rows_.size();
+    t_rows_.insert(t_rows_.end(), tr.begin(), tr.end());
+    sc.t1 = (int64_t)t_rows_.size();
+    sc.n0 = (int64_t)n_rows_.size();
+    n_rows_.insert(n_rows_.end(), nr.begin(), nr.end());
+    sc.n1 = (int64_t)n_rows_.size();
+    const int32_t id = (int32_t)scopes_.size();
+    scopes_.push_back(sc);
+    stats_.push_back(2);
+    stats_.push_back(id);
+    return id;
+  }
+
+  struct YPair {
+    int64_t name;
+    Inst p[2];
+    bool has[2];
+    int64_t max_end;
+  };
+
+  // pairs in the order CompleteGermlineAnonymizer.anonymize yields them (AM:472-532)
+  void yield_sequence(int32_t sid, std::vector<YPair> &pairs, std::vector<int32_t> &order) {
+    const ScopeRec &sc = scopes_[(size_t)sid];
+    struct Reg {
+      int64_t pos;
+      int32_t ds;
+      int64_t fo, row;
+    };
+    std::vector<Reg> reg;
+    reg.reserve((size_t)(sc.t1 - sc.t0 + sc.n1 - sc.n0));
+    for (int64_t i = sc.t0; i < sc.t1; ++i) reg.push_back(Reg{in_->tables[0].pos[t_rows_[i]], 0, i - sc.t0, t_rows_[i]});
+    for (int64_t i = sc.n0; i < sc.n1; ++i) reg.push_back(Reg{in_->tables[1].pos[n_rows_[i]], 1, i - sc.n0, n_rows_[i]});
+    std::sort(reg.begin(), reg.end(), [](const Reg &a, const Reg &b) {
+      if (a.pos != b.pos) return a.pos < b.pos;
+      if (a.ds != b.ds) return a.ds < b.ds;
+      return a.fo < b.fo;
+    });
+    pairs.clear();
+    std::unordered_map<int64_t, int32_t> where;
+    where.reserve(reg.size());
+    for (const Reg &g : reg) {
+      const int64_t name = nid_[g.ds][(size_t)g.row];
+      const int sl = slot(g.ds, g.row);
+      const int64_t e = in_->tables[g.ds].end[g.row];
+      auto it = where.find(name);
+      YPair *p;
+      if (it == where.end()) {
+        where.emplace(name, (int32_t)pairs.size());
+        pairs.push_back(YPair{name, {}, {false, false}, e});
+        p = &pairs.back();
+      } else {
+        p = &pairs[(size_t)it->second];
+        p->max_end = std::max(p->max_end, e);
+      }
+      if (p->has[sl])
+        raise(GANON_PLAN_E_UNSUPPORTED, "two alignments of '" + tab_[g.ds].name(g.row) +
+                                            "' with the same mate flag in one scope");
+      p->p[sl] = Inst{g.ds, sid, g.row};
+      p->has[sl] = true;
+    }
+    // normal columns: union of the normal reads' [pos, end)
+    std::vector<int64_t> m_start, m_end;
+    if (sc.n1 > sc.n0) {
+      std::vector<std::pair<int64_t, int64_t>> iv;
+      iv.reserve((size_t)(sc.n1 - sc.n0));
+      for (int64_t i = sc.n0; i < sc.n1; ++i)
+        iv.emplace_back(in_->tables[1].pos[n_rows_[i]], in_->tables[1].end[n_rows_[i]]);
+      std::stable_sort(iv.begin(), iv.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
+      int64_t run_end = iv[0].second;
+      m_start.push_back(iv[0].first);
+      for (size_t i = 1; i < iv.size(); ++i) {
+        if (iv[i].first > run_end) {
+          m_end.push_back(run_end);
+          m_start.push_back(iv[i].first);
+        }
+        run_end = std::max(run_end, iv[i].second);
+      }
+      m_end.push_back(run_end);
+    }
+    struct Scan {
+      int64_t col;
+      int32_t rank;
+    };
+    std::vector<Scan> scan;
+    std::vector<int32_t> rest;
+    for (int32_t rank = 0; rank < (int32_t)pairs.size(); ++rank) {
+      const YPair &p = pairs[(size_t)rank];
+      if (p.has[0] && p.has[1]) {
+        const int64_t x = p.max_end + 1;   // first column with right_most_end < pos
+        const size_t k = (size_t)(std::upper_bound(m_end.begin(), m_end.end(), x) - m_end.begin());
+        if (k < m_end.size()) {
+          scan.push_back(Scan{std::max(x, m_start[k]), rank});
+          continue;
+        }
+      }
+      rest.push_back(rank);
+    }
+    std::sort(scan.begin(), scan.end(), [](const Scan &a, const Scan &b) {
+      return a.col != b.col ? a.col < b.col : a.rank < b.rank;
+    });
+    order.clear();
+    for (const Scan &s : scan) order.push_back(s.rank);
+    order.insert(order.end(), rest.begin(), rest.end());
+  }
+
+  void anonymize_window(int32_t contig, int64_t first, int64_t last, int32_t window, bool /*variant*/) {
+    const int32_t sid = new_scope(contig, first, last, window);
+    const int32_t hid = open_handle();
+    std::vector<YPair> pairs;
+    std::vector<int32_t> order;
+    yield_sequence(sid, pairs, order);
+    for (int32_t k : order) {
+      const YPair &p = pairs[(size_t)k];
+      if (p.has[0] && p.has[1]) {
+        write_pair(p.p[0], p.p[1], hid);
+        continue;
+      }
+      const Inst &inst = p.has[0] ? p.p[0] : p.p[1];
+      store_first(inst);
+      const int64_t name = nid_[inst.ds][(size_t)inst.row];
+      auto it = to_pair_.find(name);
+      if (it->second.has[0] && it->second.has[1]) {
+        const Inst a = it->second.p[0], b = it->second.p[1];
+        write_pair(a, b, hid);
+        to_pair_.erase(it);
+      }
+    }
+    close_handle(hid);
+  }
+
+  // ---- inter-window clustering (pileup_io.pyx:124-298) ----
+  static int compare(int64_t s1, int64_t f1, int64_t l1, int64_t s2, int64_t f2, int64_t l2) {
+    const bool overlap = f2 <= l1 && l2 >= f1;
+    if (s1 != s2) return s1 < s2 ? -3 : 3;
+    if (l1 != l2) {
+      if (l1 < l2) return overlap ? -1 : -2;
+      return overlap ? 1 : 2;
+    }
+    if (f1 != f2) return f1 < f2 ? -1 : 1;
+    return 0;
+  }
+
+  void inter_window(const Section &w) {
+    bool has = true;
+    int64_t first = w.first, last = w.last;
+    if (first + last == 0) has = false;   // whole contig (fetch without a region)
+    std::vector<int64_t> it[2];
+    fetch(0, w.contig, has, first, has, last, it[0]);
+    fetch(1, w.contig, has, first, has, last, it[1]);
+    size_t ip[2] = {0, 0};
+    const int32_t hid = open_handle();
+    auto mapped = [&](int ds, int64_t r) { return !tab_[ds].unmapped(r); };
+    auto need_end = [&](int ds, int64_t r) {
+      const int64_t e = ref_end(ds, r);
+      if (e < 0) raise(GANON_PLAN_E_TYPE, "mapped read without reference_end");
+      return e;
+    };
+    auto next = [&](int ds, int64_t &r) {
+      if (ip[ds] >= it[ds].size()) return false;
+      r = it[ds][ip[ds]++];
+      return true;
+    };
+    std::vector<int64_t> arrs[2], unm[2];
+    int64_t cur[2];
+    bool has_cur[2];
+    bool yielded[2] = {true, true};
+    int64_t seqi[2] = {0, 0}, left[2] = {0, 0}, right[2] = {-1, -1};   // right -1 = None
+    has_cur[0] = next(0, cur[0]);
+    has_cur[1] = next(1, cur[1]);
+    auto passthrough_all = [&](int ds, const std::vector<int64_t> &rows) {
+      for (int64_t r : rows) passthrough(ds, r, hid);
+    };
+    if (has_cur[0] || has_cur[1]) {
+      for (int ds = 0; ds < 2; ++ds)
+        if (has_cur[ds]) {
+          const int64_t r = cur[ds];
+          seqi[ds] = in_->tables[ds].tid[r];
+          left[ds] = in_->tables[ds].pos[r];
+          right[ds] = ref_end(ds, r);
+          arrs[ds].push_back(r);
+        }
+      auto collect = [&](int ds) {
+        for (;;) {
+          int64_t nxt;
+          if (!next(ds, nxt)) return false;
+          if (!mapped(ds, nxt)) {
+            unm[ds].push_back(nxt);
+            continue;
+          }
+          const int64_t a = arrs[ds].back();
+          const ganon_plan_table &t = in_->tables[ds];
+          const int64_t fa = t.pos[a], fb = t.pos[nxt];
+          const int64_t la = mapped(ds, a) ? need_end(ds, a) : fa;
+          const int64_t lb = need_end(ds, nxt);
+          const int c = compare(t.tid[a], fa, la, t.tid[nxt], fb, lb);
+          if (!(-1 <= c && c <= 1)) {
+            cur[ds] = nxt;
+            return true;
+          }
+          arrs[ds].push_back(nxt);
+        }
+      };
+      auto rightmost = [&](int ds) {
+        int64_t r = right[ds] < 0 ? 0 : right[ds];
+        for (int64_t x : arrs[ds])
+          if (mapped(ds, x)) r = std::max(r, need_end(ds, x));
+        right[ds] = r;
+      };
+      auto restart = [&](int ds) {
+        const int64_t r = cur[ds];
+        yielded[ds] = true;
+        arrs[ds].assign(1, r);
+        seqi[ds] = in_->tables[ds].tid[r];
+        left[ds] = in_->tables[ds].pos[r];
+        right[ds] = ref_end(ds, r);
+      };
+      for (;;) {
+        for (int ds = 0; ds < 2; ++ds)
+          if (yielded[ds] && has_cur[ds]) {
+            has_cur[ds] = collect(ds);
+            rightmost(ds);
+            yielded[ds] = false;
+          }
+        if (!has_cur[0] && !has_cur[1]) {
+          passthrough_all(0, arrs[0]);
+          passthrough_all(1, arrs[1]);
+          break;
+        }
+        if (has_cur[0] && has_cur[1]) {
+          if (right[0] < 0 || right[1] < 0) raise(GANON_PLAN_E_TYPE, "mapped read without reference_end");
+          const int c = compare(seqi[0], left[0], right[0], seqi[1], left[1], right[1]);
+          if (c < -1) {
+            passthrough_all(0, arrs[0]);
+            restart(0);
+          } else if (c > 1) {
+            passthrough_all(1, arrs[1]);
+            restart(1);
+          } else {
+            anonymize_window(w.contig, std::min(left[0], left[1]), std::max(right[0], right[1]), -1, false);
+            restart(0);
+            restart(1);
+          }
+        } else {
+          if (has_cur[0]) {
+            passthrough_all(0, arrs[0]);
+            restart(0);
+          }
+          if (has_cur[1]) {
+            passthrough_all(1, arrs[1]);
+            restart(1);
+          }
+        }
+      }
+      passthrough_all(0, unm[0]);
+      passthrough_all(1, unm[1]);
+    }
+    close_handle(hid);
+  }
+
+  // ---- SR:561-600 ----
+  void pair_unmapped_mates() {
+    const int32_t hid = open_handle();
+    std::vector<int64_t> rows;
+    for (int32_t w = 0; w < in_->n_windows; ++w)
+      for (int ds = 0; ds < 2; ++ds) {
+        fetch(ds, in_->win_contig[w], true, in_->win_first[w] - 1, true, in_->win_last[w], rows);
+        for (int64_t r : rows)
+          if (tab_[ds].unmapped(r) && to_pair_.count(nid_[ds][(size_t)r])) passthrough(ds, r, hid);
+      }
+    close_handle(hid);
+  }
+};
+
+}  // namespace
+
+struct ganon_plan {
+  Planner *p = nullptr;
+  std::vector<int32_t> sc_contig, sc_window;
+  std::vector<int64_t> sc_first, sc_last, sc_span_start, sc_span_end, sc_t_off, sc_n_off;
+};
+
+GANON_HOST_API int ganon_plan_run(const ganon_plan_input *in, ganon_plan **out) {
+  if (!in || !out) {
+    g_err = "null argument";
+    return GANON_PLAN_E_ARG;
+  }
+  *out = nullptr;
+  for (int d = 0; d < 2; ++d) {
+    const ganon_plan_table &t = in->tables[d];
+    if (t.n < 0 || (t.n > 0 && (!t.tid || !t.pos || !t.end || !t.flag || !t.l_seq || !t.n_cigar || !t.names ||
+                                !t.name_off || !t.name_len)) ||
+        !t.tid_of_contig || (t.n_ref > 0 && !t.ref_len)) {
+      g_err = "bad read table";
+      return GANON_PLAN_E_ARG;
+    }
+    for (int32_t c = 0; c < in->n_contigs; ++c)
+      if (t.tid_of_contig[c] >= t.n_ref) {
+        g_err = "tid_of_contig out of range";
+        return GANON_PLAN_E_ARG;
+      }
+    for (int64_t r = 0; r < t.n; ++r)
+      if (t.tid[r] >= t.n_ref) {
+        g_err = "read tid out of range";
+        return GANON_PLAN_E_ARG;
+      }
+  }
+  for (int32_t w = 0; w < in->n_windows; ++w)
+    if (in->win_contig[w] < 0 || in->win_contig[w] >= in->n_contigs) {
+      g_err = "window contig out of range";
+      return GANON_PLAN_E_ARG;
+    }
+  ganon_plan *pl = new ganon_plan();
+  pl->p = new Planner(in);
+  try {
+    pl->p->run();
+  } catch (const PlanError &e) {
+    g_err = e.msg;
+    ganon_plan_free(pl);
+    return e.code;
+  } catch (const std::bad_alloc &) {
+    g_err = "out of memory";
+    ganon_plan_free(pl);
+    return GANON_PLAN_E_NOMEM;
+  }
+  const auto &S = pl->p->scopes_;
+  const size_t n = S.size();
+  pl->sc_contig.resize(n);
+  pl->sc_window.resize(n);
+  pl->sc_first.resize(n);
+  pl->sc_last.resize(n);
+  pl->sc_span_start.resize(n);
+  pl->sc_span_end.resize(n);
+  pl->sc_t_off.resize(n + 1);
+  pl->sc_n_off.resize(n + 1);
+  for (size_t i = 0; i < n; ++i) {
+    pl->sc_contig[i] = S[i].contig;
+    pl->sc_window[i] = S[i].window;
+    pl->sc_first[i] = S[i].first;
+    pl->sc_last[i] = S[i].last;
+    pl->sc_span_start[i] = S[i].span_start;
+    pl->sc_span_end[i] = S[i].span_end;
+    pl->sc_t_off[i] = S[i].t0;
+    pl->sc_n_off[i] = S[i].n0;
+  }
+  pl->sc_t_off[n] = (int64_t)pl->p->t_rows_.size();
+  pl->sc_n_off[n] = (int64_t)pl->p->n_rows_.size();
+  *out = pl;
+  return GANON_PLAN_OK;
+}
+
+GANON_HOST_API int ganon_plan_view_get(const ganon_plan *pl, ganon_plan_view *v) {
+  if (!pl || !v) return GANON_PLAN_E_ARG;
+  const Planner &p = *pl->p;
+  v->n_scopes = (int32_t)p.scopes_.size();
+  v->scope_contig = pl->sc_contig.data();
+  v->scope_window = pl->sc_window.data();
+  v->scope_first = pl->sc_first.data();
+  v->scope_last = pl->sc_last.data();
+  v->scope_span_start = pl->sc_span_start.data();
+  v->scope_span_end = pl->sc_span_end.data();
+  v->scope_t_off = pl->sc_t_off.data();
+  v->scope_n_off = pl->sc_n_off.data();
+  v->t_rows = p.t_rows_.data();
+  v->n_rows = p.n_rows_.data();
+  v->n_events = (int64_t)p.event_rows_.size();
+  v->events = p.events_.data();
+  v->event_rows = p.event_rows_.data();
+  v->n_stats = (int64_t)p.stats_.size() / 2;
+  v->stats = p.stats_.data();
+  for (int d = 0; d < 2; ++d) {
+    v->n_single[d] = (int64_t)p.single_[d].size() / 2;
+    v->single[d] = p.single_[d].data();
+  }
+  v->write_single_end = p.write_single_end_ ? 1 : 0;
+  return GANON_PLAN_OK;
+}
+
+GANON_HOST_API void ganon_plan_free(ganon_plan *pl) {
+  if (!pl) return;
+  delete pl->p;
+  delete pl;
+}
+
+GANON_HOST_API const char *ganon_plan_last_error(void) { return g_err.c_str(); }

@@ -24,7 +24,7 @@ from .anonymizer_methods import CompleteGermlineAnonymizer, MaskResult
 from .indels import IndelCall
 from .io.bam import ReadTable
 from .io.fasta import FastaRef
-from .planner import Plan, SamplePlanner, Window
+from .planner import Plan, SamplePlanner, Window, make_planner
 from .variants import VariantType
 from .writer import statistics_rows, write_fastqs, write_statistics
 
@@ -61,7 +61,7 @@ def anonymize_genome_sharded(windows: List[Window], tumor_bam: str, normal_bam: 
     anonymizer = anonymizer or CompleteGermlineAnonymizer(device=int(os.environ.get("LOCAL_RANK", 0)))
     fasta = FastaRef(ref_file)
     tables = (ReadTable(tumor_bam, threads=threads), ReadTable(normal_bam, threads=threads))
-    planner = SamplePlanner(tables[0], tables[1], fasta, windows)
+    planner = make_planner(tables[0], tables[1], fasta, windows)
     plan = planner.run()
     owner = contig_owner(plan, list(fasta.references), world, policy)
     mine = [sc.id for sc in plan.scopes if owner[sc.contig] == rank]

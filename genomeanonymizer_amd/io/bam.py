@@ -98,7 +98,8 @@ class ReadTable:
         ix = self._index.get(tid)
         if ix is None:
             rows = np.nonzero(self.tid == tid)[0].astype(np.int64)
-            pos = self.pos[rows]
+            # int64: searchsorted with a Python int would cast an int32 array on every call
+            pos = self.pos[rows].astype(np.int64)
             if len(pos) > 1 and np.any(np.diff(pos) < 0):
                 raise ValueError(f"{self.path}: records of contig {tid} are not coordinate sorted")
             span = int((self.end[rows] - pos).max()) if len(rows) else 1

@@ -188,6 +188,7 @@ EXPORTED_HIP_SYMBOLS = (
 EXPORTED_HOST_SYMBOLS = (
     "ganon_bam_open", "ganon_bam_view_get", "ganon_bam_error", "ganon_bam_close",
     "ganon_host_last_error", "ganon_fastq_format", "ganon_pack_nt16",
+    "ganon_plan_run", "ganon_plan_view_get", "ganon_plan_free", "ganon_plan_last_error",
 )
 
 
@@ -519,6 +520,115 @@ class BamView(C.Structure):
     ]
 
 
+class PlanTable(C.Structure):
+    """Mirror of ``ganon_plan_table`` (include/ganon_host.h)."""
+    _fields_ = [("n", C.c_int64), ("tid", _i32p), ("pos", _i32p), ("end", _i32p), ("flag", _i32p),
+                ("l_seq", _i32p), ("n_cigar", _i32p), ("names", _p), ("name_off", _i64p), ("name_len", _i32p),
+                ("n_ref", C.c_int32), ("ref_len", _i64p), ("tid_of_contig", _i32p)]
+
+
+class PlanInput(C.Structure):
+    _fields_ = [("tables", PlanTable * 2), ("n_contigs", C.c_int32), ("contig_len", _i64p),
+                ("contig_names", _p), ("contig_name_off", _i64p), ("n_windows", C.c_int32),
+                ("win_contig", _i32p), ("win_first", _i64p), ("win_last", _i64p)]
+
+
+class PlanView(C.Structure):
+    _fields_ = [("n_scopes", C.c_int32), ("scope_contig", _i32p), ("scope_window", _i32p),
+                ("scope_first", _i64p), ("scope_last", _i64p), ("scope_span_start", _i64p),
+                ("scope_span_end", _i64p), ("scope_t_off", _i64p), ("scope_n_off", _i64p),
+                ("t_rows", _i64p), ("n_rows", _i64p), ("n_events", C.c_int64), ("events", _i32p),
+                ("event_rows", _i64p), ("n_stats", C.c_int64), ("stats", _i32p),
+                ("n_single", C.c_int64 * 2), ("single", _i64p * 2), ("write_single_end", C.c_int32)]
+
+
+PLAN_E_VALUE, PLAN_E_TYPE, PLAN_E_UNSUPPORTED = -10, -11, -12
+
+
+def _np_copy(ptr, n: int, dtype) -> np.ndarray:
+    if n <= 0:
+        return np.zeros(0, dtype)
+    return np.ctypeslib.as_array(ptr, shape=(int(n),)).astype(dtype, copy=True)
+
+
+def plan_sample(tables, contig_names, contig_lens, win_contig, win_first, win_last) -> dict:
+    """``ganon_plan_run`` over two ReadTables (io/bam.py) and the variant windows. Returns the
+    plan's column arrays (copies); raises ValueError / TypeError / planner.UnsupportedInput as
+    the reference's own code would (message from the library)."""
+    lib = host_lib()
+    keep = []
+
+    def arr(a, dt):
+        a = np.ascontiguousarray(a, dtype=dt)
+        keep.append(a)
+        return a.ctypes.data_as(_PTR_OF[dt])
+
+    inp = PlanInput()
+    for d, t in enumerate(tables):
+        pt = inp.tables[d]
+        pt.n = t.n
+        for f in ("tid", "pos", "end", "flag", "l_seq", "n_cigar"):
+            setattr(pt, f, arr(getattr(t, f), np.int32))
+        nb = np.ascontiguousarray(t.names_blob)
+        keep.append(nb)
+        pt.names = nb.ctypes.data_as(_p)
+        pt.name_off = arr(t.name_off, np.int64)
+        pt.name_len = arr(t.name_len, np.int32)
+        pt.n_ref = len(t.ref_names)
+        pt.ref_len = arr(t.ref_lens, np.int64)
+        idx = {nm: i for i, nm in enumerate(t.ref_names)}
+        pt.tid_of_contig = arr([idx.get(c, -1) for c in contig_names], np.int32)
+    inp.n_contigs = len(contig_names)
+    inp.contig_len = arr(contig_lens, np.int64)
+    blob = b"".join(c.encode() + b"\0" for c in contig_names) or b"\0"
+    cb = np.frombuffer(blob, np.uint8).copy()
+    keep.append(cb)
+    inp.contig_names = cb.ctypes.data_as(_p)
+    offs = np.cumsum([0] + [len(c.encode()) + 1 for c in contig_names])[:-1] if contig_names else [0]
+    inp.contig_name_off = arr(offs, np.int64)
+    inp.n_windows = len(win_contig)
+    inp.win_contig = arr(win_contig, np.int32)
+    inp.win_first = arr(win_first, np.int64)
+    inp.win_last = arr(win_last, np.int64)
+    h = _p()
+    rc = lib.ganon_plan_run(C.byref(inp), C.byref(h))
+    if rc != 0:
+        msg = lib.ganon_plan_last_error().decode(errors="replace")
+        if rc == PLAN_E_VALUE:
+            raise ValueError(msg)
+        if rc == PLAN_E_TYPE:
+            raise TypeError(msg)
+        if rc == PLAN_E_UNSUPPORTED:
+            from .planner import UnsupportedInput
+            raise UnsupportedInput(msg)
+        raise GanonError(f"ganon_plan_run failed ({rc}): {msg}")
+    try:
+        v = PlanView()
+        lib.ganon_plan_view_get(h, C.byref(v))
+        ns = int(v.n_scopes)
+        out = {
+            "scope_contig": _np_copy(v.scope_contig, ns, np.int32),
+            "scope_window": _np_copy(v.scope_window, ns, np.int32),
+            "scope_first": _np_copy(v.scope_first, ns, np.int64),
+            "scope_last": _np_copy(v.scope_last, ns, np.int64),
+            "scope_span_start": _np_copy(v.scope_span_start, ns, np.int64),
+            "scope_span_end": _np_copy(v.scope_span_end, ns, np.int64),
+            "scope_t_off": _np_copy(v.scope_t_off, ns + 1, np.int64),
+            "scope_n_off": _np_copy(v.scope_n_off, ns + 1, np.int64),
+        }
+        out["t_rows"] = _np_copy(v.t_rows, int(out["scope_t_off"][-1]), np.int64)
+        out["n_rows"] = _np_copy(v.n_rows, int(out["scope_n_off"][-1]), np.int64)
+        ne = int(v.n_events)
+        out["events"] = _np_copy(v.events, 7 * ne, np.int32).reshape(ne, 7)
+        out["event_rows"] = _np_copy(v.event_rows, ne, np.int64)
+        out["stats"] = _np_copy(v.stats, 2 * int(v.n_stats), np.int32).reshape(-1, 2)
+        out["single"] = [_np_copy(v.single[d], 2 * int(v.n_single[d]), np.int64).reshape(-1, 2) for d in (0, 1)]
+        out["write_single_end"] = bool(v.write_single_end)
+    finally:
+        lib.ganon_plan_free(h)
+    return out
+
+
 def host_lib():
     global _host
     if _host is not None:
@@ -535,5 +645,9 @@ def host_lib():
                                        _u8p, _i64p, _i32p, _u8p, C.c_char_p, _i64p, _i32p, _u8p, C.c_char_p,
                                        C.c_int64]
     lib.ganon_pack_nt16.argtypes = [C.c_char_p, C.c_int64, _u8p]
+    lib.ganon_plan_run.argtypes = [C.POINTER(PlanInput), C.POINTER(_p)]
+    lib.ganon_plan_view_get.argtypes = [_p, C.POINTER(PlanView)]
+    lib.ganon_plan_free.argtypes = [_p]
+    lib.ganon_plan_last_error.restype = C.c_char_p
     _host = lib
     return lib

@@ -181,10 +181,11 @@ class SamplePlanner:
         self.io_log: List[tuple] = []
         self._next_hid = 0
         self.stats_events: List[Tuple[str, object]] = []
-        self._check_supported()
+        self._check_supported(names=not self.native)
 
+    native = False
     # ---- input checks --------------------------------------------------------------------
-    def _check_supported(self) -> None:
+    def _check_supported(self, names: bool = True) -> None:
         for ds, t in enumerate(self.tables):
             if np.any(t.flag & (FLAG_SECONDARY | FLAG_SUPPLEMENTARY)):
                 raise UnsupportedInput("secondary/supplementary alignments are not supported yet "
@@ -193,7 +194,7 @@ class SamplePlanner:
                 rows = [i for i in range(t.n) if t.has_tag(i, b"SA")]
                 if rows:
                     raise UnsupportedInput("reads with an SA tag are not supported yet (AM:100-108)")
-        tn = set(self.tables[0].names) & set(self.tables[1].names)
+        tn = set(self.tables[0].names) & set(self.tables[1].names) if names else None
         if tn:
             raise ValueError(f"{len(tn)} read names occur in both the tumor and the normal BAM; the "
                              "reference keys reads by name only and mixes such reads (SURVEY Q10)")
@@ -510,3 +511,57 @@ class SamplePlanner:
             inst = pair[0] if pair[0] is not None else pair[1]
             single[inst[0]].append(inst)
         return Plan(self.scopes, self.io_log, single, self.stats_events, bool(self.to_pair))
+
+
+class NativeSamplePlanner(SamplePlanner):
+    """The same plan from libganon_host.so (``ganon_plan_run``, csrc/ganon_plan.cpp): the
+    control flow above restated in C++ over the read tables' columns. The product's planner;
+    SamplePlanner (pure Python) is the second implementation the tests compare it with."""
+
+    native = True
+
+    def run(self) -> Plan:
+        from . import native
+        refs = list(self.fasta.references)
+        cidx = {c: i for i, c in enumerate(refs)}
+        w = self.windows
+        res = native.plan_sample(self.tables, refs, list(self.fasta.lengths),
+                                 [cidx[x.sequence] for x in w], [x.first for x in w], [x.last for x in w])
+        T, N = self.tables
+        t_rows, n_rows = res["t_rows"], res["n_rows"]
+        to, no = res["scope_t_off"], res["scope_n_off"]
+        for k in range(len(res["scope_contig"])):
+            contig = refs[int(res["scope_contig"][k])]
+            wi = int(res["scope_window"][k])
+            sc = Scope(k, contig, T.tid_of(contig), N.tid_of(contig), int(res["scope_first"][k]),
+                       int(res["scope_last"][k]), t_rows[to[k]:to[k + 1]], n_rows[no[k]:no[k + 1]],
+                       w[wi].variant if wi >= 0 else None, wi >= 0)
+            sc.span_start = int(res["scope_span_start"][k])
+            sc.span_end = int(res["scope_span_end"][k])
+            self.scopes.append(sc)
+        ev = res["events"].tolist()
+        rows = res["event_rows"].tolist()
+        log = self.io_log
+        for e, r in zip(ev, rows):
+            if e[0] == 1:
+                log.append(("write", e[1], e[2], e[3], (e[4], r, e[5])))
+            elif e[0] == 0:
+                log.append(("open", e[1]))
+            else:
+                log.append(("close", e[1]))
+        for kind, val in res["stats"].tolist():
+            if kind == 0:
+                self.stats_events.append(("window", str(w[val])))
+            elif kind == 1:
+                self.stats_events.append(("outside", None))
+            else:
+                self.stats_events.append(("scope", val))
+        single = {d: [(d, r, s) for r, s in res["single"][d].tolist()] for d in (0, 1)}
+        return Plan(self.scopes, self.io_log, single, self.stats_events, res["write_single_end"])
+
+
+def make_planner(tumor: ReadTable, normal: ReadTable, fasta: FastaRef, windows: Sequence[Window]) -> SamplePlanner:
+    """The native planner; GANON_PLANNER=python selects the pure-Python one."""
+    import os
+    cls = SamplePlanner if os.environ.get("GANON_PLANNER") == "python" else NativeSamplePlanner
+    return cls(tumor, normal, fasta, windows)

@@ -21,7 +21,7 @@ from .anonymizer_methods import CompleteGermlineAnonymizer
 from .io.bam import ReadTable
 from .io.fasta import FastaRef
 from .io.vcf import read_vcf
-from .planner import SamplePlanner, Window, get_windows
+from .planner import Window, get_windows, make_planner
 from .writer import statistics_rows, write_fastqs, write_statistics
 
 log = logging.getLogger("genomeanonymizer_amd")
@@ -45,7 +45,7 @@ def anonymize_genome(windows_in_sample: List[Window], tumor_bam_file: str, norma
     tumor = ReadTable(tumor_bam_file, threads=available_threads)
     normal = ReadTable(normal_bam_file, threads=available_threads)
     t1 = time.time()
-    planner = SamplePlanner(tumor, normal, fasta, windows_in_sample)
+    planner = make_planner(tumor, normal, fasta, windows_in_sample)
     plan = planner.run()
     t2 = time.time()
     res = anonymizer.anonymize(planner, plan)

@@ -81,4 +81,64 @@ GANON_HOST_API int64_t ganon_fastq_format(int64_t n, const uint8_t *const *seq_b
  * outside "=ACMGRSVTWYHKDBN" (after upper-casing) become N (15). `out` has (n+1)/2 bytes. */
 GANON_HOST_API void ganon_pack_nt16(const char *ascii, int64_t n, uint8_t *out);
 
+/* ---- Scope planner -------------------------------------------------------
+ * Replaces, for one tumor/normal pair, the control flow of anonymize_genome
+ * (short_read_tumor_normal_anonymizer.py:625-760) that decides which reads meet in which pileup
+ * scope and which scope's masked copy of each read is written, in which order: sections
+ * (SR:245-276), anonymize_window (SR:279-372), anonymize_inter_window_region + iter_fetch_pair
+ * (SR:498-558, pileup_io.pyx:124-298), the yield order of CompleteGermlineAnonymizer.anonymize
+ * (anonymizer_methods.py:472-532), write_pair / to_pair_anonymized_reads / unmapped-mate pairing /
+ * single ends (SR:134-165, :375-406, :561-622, AM:320-389) and the statistics recorder's events.
+ * Same results as genomeanonymizer_amd/planner.py (SamplePlanner.run). */
+enum {
+  GANON_PLAN_OK = 0,
+  GANON_PLAN_E_ARG = -1,
+  GANON_PLAN_E_NOMEM = -3,
+  GANON_PLAN_E_VALUE = -10,        /* the reference raises ValueError (region errors Q4, Q10, ...) */
+  GANON_PLAN_E_TYPE = -11,         /* the reference raises TypeError (Q8, reads without SEQ, ...)  */
+  GANON_PLAN_E_UNSUPPORTED = -12   /* input this build does not restate                           */
+};
+typedef struct ganon_plan_table {  /* one sample, file order (columns of a ganon_bam_view) */
+  int64_t n;
+  const int32_t *tid, *pos, *end, *flag, *l_seq, *n_cigar;
+  const char *names;
+  const int64_t *name_off;
+  const int32_t *name_len;
+  int32_t n_ref;
+  const int64_t *ref_len;          /* [n_ref] BAM header lengths                            */
+  const int32_t *tid_of_contig;    /* [n_contigs] this BAM's tid of each FASTA contig, -1 none */
+} ganon_plan_table;
+typedef struct ganon_plan_input {
+  ganon_plan_table tables[2];      /* 0 tumor, 1 normal                                      */
+  int32_t n_contigs;               /* FASTA contigs, FASTA order                              */
+  const int64_t *contig_len;
+  const char *contig_names;        /* NUL-terminated names at contig_name_off (messages)      */
+  const int64_t *contig_name_off;
+  int32_t n_windows;               /* variant windows in get_windows order (SR:71-131)        */
+  const int32_t *win_contig;
+  const int64_t *win_first, *win_last;
+} ganon_plan_input;
+typedef struct ganon_plan ganon_plan;
+typedef struct ganon_plan_view {
+  int32_t n_scopes;
+  const int32_t *scope_contig, *scope_window;      /* window -1: a gap cluster scope      */
+  const int64_t *scope_first, *scope_last, *scope_span_start, *scope_span_end;
+  const int64_t *scope_t_off, *scope_n_off;        /* [n_scopes + 1] CSR into t_rows/n_rows */
+  const int64_t *t_rows, *n_rows;                  /* mapped pileup reads, file order      */
+  int64_t n_events;                                /* I/O log                              */
+  const int32_t *events;     /* 7 per event: kind (0 open, 1 write, 2 close), handle, file dataset,
+                                file mate slot, instance dataset, instance scope (-1 unmasked), 0 */
+  const int64_t *event_rows; /* instance row of a write event, -1 otherwise                 */
+  int64_t n_stats;
+  const int32_t *stats;      /* 2 per event: kind (0 window -> window index, 1 outside, 2 scope id) */
+  int64_t n_single[2];
+  const int64_t *single[2];  /* per dataset: (row, scope) pairs of the single-end records    */
+  int32_t write_single_end;
+} ganon_plan_view;
+/* Returns GANON_PLAN_OK or a GANON_PLAN_E_* code (message: ganon_plan_last_error()). */
+GANON_HOST_API int ganon_plan_run(const ganon_plan_input *in, ganon_plan **out);
+GANON_HOST_API int ganon_plan_view_get(const ganon_plan *plan, ganon_plan_view *view);
+GANON_HOST_API void ganon_plan_free(ganon_plan *plan);
+GANON_HOST_API const char *ganon_plan_last_error(void);
+
 #endif /* GANON_HOST_H */

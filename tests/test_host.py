@@ -112,3 +112,81 @@ def test_config2_batch_small():
     out, calls, bases, tot = OracleEngine().mask(arr)
     assert tot[2] == 20000
     assert algorithmic_bytes(arr) / info["reads"] > 170
+
+
+def _plans(paths):
+    from genomeanonymizer_amd.io.bam import ReadTable
+    from genomeanonymizer_amd.io.fasta import FastaRef
+    from genomeanonymizer_amd.io.vcf import read_vcf
+    from genomeanonymizer_amd.planner import NativeSamplePlanner, SamplePlanner, get_windows
+    fa = FastaRef(paths["ref"])
+    ws = get_windows(read_vcf(paths["vcf"]), dict(fa.index))
+    out = []
+    for cls in (SamplePlanner, NativeSamplePlanner):
+        t = (ReadTable(paths["T"]), ReadTable(paths["N"]))
+        try:
+            out.append(cls(t[0], t[1], fa, ws).run())
+        except Exception as e:      # both must fail the same way
+            out.append((type(e).__name__,))
+    return out
+
+
+def _same_plan(a, b):
+    if isinstance(a, tuple) or isinstance(b, tuple):
+        assert a == b
+        return
+    assert len(a.scopes) == len(b.scopes)
+    for x, y in zip(a.scopes, b.scopes):
+        assert (x.contig, x.first, x.last, x.span_start, x.span_end, x.is_variant_window, x.keep) == \
+               (y.contig, y.first, y.last, y.span_start, y.span_end, y.is_variant_window, y.keep)
+        assert np.array_equal(x.t_rows, y.t_rows) and np.array_equal(x.n_rows, y.n_rows)
+    norm = lambda log: [tuple(int(v) if not isinstance(v, (str, tuple)) else
+                              (tuple(int(u) for u in v) if isinstance(v, tuple) else v) for v in e) for e in log]
+    assert norm(a.io_log) == norm(b.io_log)
+    assert {d: [tuple(map(int, i)) for i in r] for d, r in a.single_end.items()} == \
+           {d: [tuple(map(int, i)) for i in r] for d, r in b.single_end.items()}
+    assert a.stats_events == b.stats_events
+    assert a.write_single_end == b.write_single_end
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_native_planner_matches_python_planner(seed, tmp_path):
+    """ganon_plan_run (csrc/ganon_plan.cpp) against SamplePlanner on randomized scenarios with
+    unmapped/unplaced mates, cross-contig pairs, coverage holes, windows near contig ends."""
+    from genomeanonymizer_amd.synth.generate import ContigSpec, ScenarioConfig, generate
+    rng = np.random.default_rng(seed)
+    contigs = []
+    for c in range(3):
+        L = int(rng.integers(8_000, 30_000))
+        nw = int(rng.integers(0, 5))
+        wins = sorted(set(int(x) for x in rng.integers(1001, L - 1200, nw)))
+        spaced = []
+        for x in wins:                       # the reference needs >= 2003 bp between windows (Q4)
+            if not spaced or x - spaced[-1] >= 2003:
+                spaced.append(x)
+        holes = [("T" if rng.random() < 0.5 else "N", int(h), int(h) + 500) for h in rng.integers(0, L - 600, 2)]
+        contigs.append(ContigSpec(f"c{c}", L, int(rng.integers(50, 600)), windows=spaced,
+                                  keep_windows=int(rng.integers(0, 2)), holes=holes))
+    cfg = ScenarioConfig(name=f"r{seed}", seed=seed, contigs=contigs, germline_snp_per_kb=4.0,
+                         germline_indel_per_kb=0.5, softclip_frac=0.05, unmapped_mate_frac=0.05,
+                         unplaced_frac=0.4, cross_contig_pairs=10)
+    paths = generate(cfg, str(tmp_path / "in"))
+    a, b = _plans(paths)
+    _same_plan(a, b)
+
+
+@pytest.mark.parametrize("name", ["tiny", "edge"])
+def test_native_planner_matches_python_planner_on_golden_inputs(name, tmp_path):
+    from genomeanonymizer_amd.synth.generate import generate, scenario
+    a, b = _plans(generate(scenario(name), str(tmp_path / "in")))
+    _same_plan(a, b)
+
+
+def test_native_planner_raises_like_python_planner(tmp_path):
+    """Windows 1.5 kb apart: the gap between them has first > last and the region query raises
+    ValueError in both planners, as pysam does in the reference."""
+    from genomeanonymizer_amd.synth.generate import ContigSpec, ScenarioConfig, generate
+    cfg = ScenarioConfig(name="q4", seed=9, contigs=[ContigSpec("c0", 20000, 300, windows=[3000, 4500, 9000]),
+                                                     ContigSpec("c1", 5000, 100)])
+    a, b = _plans(generate(cfg, str(tmp_path / "in")))
+    assert a == b == ("ValueError",)

@@ -72,9 +72,13 @@ def build_batch(plan: Plan, tables: Tuple[ReadTable, ReadTable], fasta: FastaRef
     arr["cigar"] = np.ascontiguousarray(np.concatenate([T.cigar, N.cigar]).astype(np.uint32))
     arr["dataset"] = np.concatenate([np.zeros(len(rows[0]), np.uint8), np.ones(len(rows[1]), np.uint8)])
     ws = np.full(n_reads, -1, np.int32)
-    for ds, row, s in plan.written_instances():
-        if s >= 0 and s in local:
-            ws[bidx[ds][row]] = local[s]
+    w_ds, w_row, w_sc = plan.written_arrays()
+    loc = np.full(len(plan.scopes) + 1, -1, np.int64)
+    loc[[sc.id for sc in scopes]] = np.arange(len(scopes))
+    sel = (w_sc >= 0) & (loc[np.where(w_sc >= 0, w_sc, len(plan.scopes))] >= 0)
+    b = np.where(w_ds[sel] == 0, bidx[0][np.where(w_ds[sel] == 0, w_row[sel], 0)],
+                 bidx[1][np.where(w_ds[sel] == 1, w_row[sel], 0)])
+    ws[b] = loc[w_sc[sel]]
     arr["write_scope"] = ws
     counts = np.array([len(sc.t_rows) + len(sc.n_rows) for sc in scopes], np.int64)
     arr["scope_incid_off"] = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)

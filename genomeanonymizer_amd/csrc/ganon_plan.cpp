@@ -735,3 +735,109 @@ GANON_HOST_API void ganon_plan_free(ganon_plan *pl) {
 }
 
 GANON_HOST_API const char *ganon_plan_last_error(void) { return g_err.c_str(); }
+
+// ---- I/O replay (writer.py AppendHandle / replay_io) --------------------------------------------
+// Every reference function that writes opens its own append-mode text handles on the four FASTQ
+// files (SR:297-299, 516-518, 564-566); CPython's TextIOWrapper gathers writes up to 8 KiB
+// (_CHUNK_SIZE) and its BufferedWriter holds `block` = st_blksize bytes, so the records of nested
+// handles reach the files in flush order. This replays the plan's I/O log.
+namespace {
+
+constexpr int64_t kTextChunk = 8192;
+
+struct Handle {
+  std::vector<int64_t> *sink = nullptr;
+  int64_t block = 8192;
+  std::vector<int64_t> pending, buf;
+  int64_t pending_len = 0, buf_len = 0;
+
+  void raw_flush() {
+    if (!buf.empty()) {
+      sink->insert(sink->end(), buf.begin(), buf.end());
+      buf.clear();
+      buf_len = 0;
+    }
+  }
+  void text_flush() {
+    if (pending.empty()) return;
+    const int64_t n = pending_len;
+    if (n <= block - buf_len) {
+      buf.insert(buf.end(), pending.begin(), pending.end());
+      buf_len += n;
+    } else {
+      raw_flush();
+      if (n > block) {
+        sink->insert(sink->end(), pending.begin(), pending.end());
+      } else {
+        buf = pending;
+        buf_len = n;
+      }
+    }
+    pending.clear();
+    pending_len = 0;
+  }
+  void write(int64_t rec, int64_t n) {
+    if (pending_len + n > kTextChunk) {
+      text_flush();
+      pending.assign(1, rec);
+      pending_len = n;
+    } else {
+      pending.push_back(rec);
+      pending_len += n;
+    }
+    if (pending_len >= kTextChunk) text_flush();
+  }
+  void close() {
+    text_flush();
+    raw_flush();
+  }
+};
+
+}  // namespace
+
+GANON_HOST_API int64_t ganon_io_replay(int64_t n_events, const int32_t *events, const int64_t *rec_len, int64_t block,
+                                       int64_t *order, int64_t *file_count) {
+  if (n_events < 0 || (n_events > 0 && (!events || !rec_len || !order)) || !file_count || block < 1) {
+    g_err = "io_replay: bad argument";
+    return GANON_PLAN_E_ARG;
+  }
+  std::vector<int64_t> files[4];
+  std::unordered_map<int32_t, std::vector<Handle>> open;
+  for (int64_t i = 0; i < n_events; ++i) {
+    const int32_t *e = events + 7 * i;
+    if (e[0] == 0) {
+      std::vector<Handle> hs(4);
+      for (int f = 0; f < 4; ++f) {
+        hs[(size_t)f].sink = &files[f];
+        hs[(size_t)f].block = block;
+      }
+      open[e[1]] = std::move(hs);
+    } else if (e[0] == 1) {
+      auto it = open.find(e[1]);
+      const int f = e[2] * 2 + e[3];
+      if (it == open.end() || f < 0 || f > 3) {
+        g_err = "io_replay: write to a handle that is not open";
+        return GANON_PLAN_E_ARG;
+      }
+      it->second[(size_t)f].write(i, rec_len[i]);
+    } else {
+      auto it = open.find(e[1]);
+      if (it == open.end()) {
+        g_err = "io_replay: close of a handle that is not open";
+        return GANON_PLAN_E_ARG;
+      }
+      for (Handle &h : it->second) h.close();
+      open.erase(it);
+    }
+  }
+  if (!open.empty()) {
+    g_err = "unclosed handles in the I/O log";
+    return GANON_PLAN_E_ARG;
+  }
+  int64_t k = 0;
+  for (int f = 0; f < 4; ++f) {
+    file_count[f] = (int64_t)files[f].size();
+    for (int64_t x : files[f]) order[k++] = x;
+  }
+  return k;
+}

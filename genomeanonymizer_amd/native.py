@@ -188,7 +188,7 @@ EXPORTED_HIP_SYMBOLS = (
 EXPORTED_HOST_SYMBOLS = (
     "ganon_bam_open", "ganon_bam_view_get", "ganon_bam_error", "ganon_bam_close",
     "ganon_host_last_error", "ganon_fastq_format", "ganon_pack_nt16",
-    "ganon_plan_run", "ganon_plan_view_get", "ganon_plan_free", "ganon_plan_last_error",
+    "ganon_plan_run", "ganon_plan_view_get", "ganon_plan_free", "ganon_plan_last_error", "ganon_io_replay",
 )
 
 
@@ -629,6 +629,22 @@ def plan_sample(tables, contig_names, contig_lens, win_contig, win_first, win_la
     return out
 
 
+def io_replay(events: np.ndarray, rec_len: np.ndarray, block: int):
+    """``ganon_io_replay``: per output file (dataset * 2 + slot) the write-event indices in the
+    order they reach the file."""
+    lib = host_lib()
+    ev = np.ascontiguousarray(events, np.int32).reshape(-1, 7)
+    rl = np.ascontiguousarray(rec_len, np.int64)
+    order = np.zeros(max(len(ev), 1), np.int64)
+    cnt = np.zeros(4, np.int64)
+    k = lib.ganon_io_replay(len(ev), ev.ctypes.data_as(_i32p), rl.ctypes.data_as(_i64p), int(block),
+                            order.ctypes.data_as(_i64p), cnt.ctypes.data_as(_i64p))
+    if k < 0:
+        raise RuntimeError(lib.ganon_plan_last_error().decode(errors="replace"))
+    bounds = np.concatenate([[0], np.cumsum(cnt)])
+    return [order[bounds[f]:bounds[f + 1]] for f in range(4)]
+
+
 def host_lib():
     global _host
     if _host is not None:
@@ -649,5 +665,7 @@ def host_lib():
     lib.ganon_plan_view_get.argtypes = [_p, C.POINTER(PlanView)]
     lib.ganon_plan_free.argtypes = [_p]
     lib.ganon_plan_last_error.restype = C.c_char_p
+    lib.ganon_io_replay.argtypes = [C.c_int64, _i32p, _i64p, C.c_int64, _i64p, _i64p]
+    lib.ganon_io_replay.restype = C.c_int64
     _host = lib
     return lib

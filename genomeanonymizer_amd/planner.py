@@ -143,13 +143,61 @@ class Scope:
     span_end: int = 0
 
 
-@dataclasses.dataclass
 class Plan:
-    scopes: List[Scope]
-    io_log: List[tuple]            # ('open', hid) | ('write', hid, dataset, slot, Instance) | ('close', hid)
-    single_end: Dict[int, List[Instance]]               # dataset -> records
-    stats_events: List[Tuple[str, object]]              # ('window', key) | ('scope', id) | ('outside', None)
-    write_single_end: bool
+    """A sample's plan. The I/O log is kept as columns (``events``: kind 0 open / 1 write /
+    2 close, handle, file dataset, file slot, instance dataset, instance scope, 0;
+    ``event_rows``: instance row) by the native planner and as tuples by the Python one; each
+    form is derived from the other on first use."""
+
+    def __init__(self, scopes: List[Scope], io_log: Optional[List[tuple]], single_end: Dict[int, List[Instance]],
+                 stats_events: List[Tuple[str, object]], write_single_end: bool,
+                 events: Optional[np.ndarray] = None, event_rows: Optional[np.ndarray] = None):
+        self.scopes = scopes
+        self._io_log = io_log
+        self.single_end = single_end
+        self.stats_events = stats_events
+        self.write_single_end = write_single_end
+        self._events = events
+        self._event_rows = event_rows
+
+    @property
+    def io_log(self) -> List[tuple]:
+        # ('open', hid) | ('write', hid, dataset, slot, Instance) | ('close', hid)
+        if self._io_log is None:
+            log = []
+            for e, r in zip(self._events.tolist(), self._event_rows.tolist()):
+                if e[0] == 1:
+                    log.append(("write", e[1], e[2], e[3], (e[4], r, e[5])))
+                elif e[0] == 0:
+                    log.append(("open", e[1]))
+                else:
+                    log.append(("close", e[1]))
+            self._io_log = log
+        return self._io_log
+
+    def io_arrays(self) -> Tuple[np.ndarray, np.ndarray]:
+        if self._events is None:
+            n = len(self._io_log)
+            ev = np.zeros((n, 7), np.int32)
+            rows = np.full(n, -1, np.int64)
+            for i, e in enumerate(self._io_log):
+                if e[0] == "write":
+                    ev[i, :6] = (1, e[1], e[2], e[3], e[4][0], e[4][2])
+                    rows[i] = e[4][1]
+                else:
+                    ev[i, :2] = (0 if e[0] == "open" else 2, e[1])
+            self._events, self._event_rows = ev, rows
+        return self._events, self._event_rows
+
+    def written_arrays(self) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+        """(dataset, row, scope) of every written record: pair writes, then single ends."""
+        ev, rows = self.io_arrays()
+        w = ev[:, 0] == 1
+        se = [np.array(self.single_end[d], np.int64).reshape(-1, 3) for d in (0, 1)]
+        ds = np.concatenate([ev[w, 4].astype(np.int64)] + [x[:, 0] for x in se])
+        row = np.concatenate([rows[w]] + [x[:, 1] for x in se])
+        sc = np.concatenate([ev[w, 5].astype(np.int64)] + [x[:, 2] for x in se])
+        return ds, row, sc
 
     @property
     def streams(self) -> Dict[Tuple[int, int], List[Instance]]:
@@ -539,16 +587,6 @@ class NativeSamplePlanner(SamplePlanner):
             sc.span_start = int(res["scope_span_start"][k])
             sc.span_end = int(res["scope_span_end"][k])
             self.scopes.append(sc)
-        ev = res["events"].tolist()
-        rows = res["event_rows"].tolist()
-        log = self.io_log
-        for e, r in zip(ev, rows):
-            if e[0] == 1:
-                log.append(("write", e[1], e[2], e[3], (e[4], r, e[5])))
-            elif e[0] == 0:
-                log.append(("open", e[1]))
-            else:
-                log.append(("close", e[1]))
         for kind, val in res["stats"].tolist():
             if kind == 0:
                 self.stats_events.append(("window", str(w[val])))
@@ -557,7 +595,8 @@ class NativeSamplePlanner(SamplePlanner):
             else:
                 self.stats_events.append(("scope", val))
         single = {d: [(d, r, s) for r, s in res["single"][d].tolist()] for d in (0, 1)}
-        return Plan(self.scopes, self.io_log, single, self.stats_events, res["write_single_end"])
+        return Plan(self.scopes, None, single, self.stats_events, res["write_single_end"],
+                    events=res["events"], event_rows=res["event_rows"])
 
 
 def make_planner(tumor: ReadTable, normal: ReadTable, fasta: FastaRef, windows: Sequence[Window]) -> SamplePlanner:

@@ -51,41 +51,51 @@ class FastqFormatter:
         # buffers: 0 = device output, 1 = tumor BAM seq, 2 = normal BAM seq
         self._seq_bufs = [res.seq_out, tables[0].seq, tables[1].seq]
         self._qual_bufs = [tables[0].qual, tables[1].qual]
+        self._names = tables[0].names_blob.tobytes() + tables[1].names_blob.tobytes()
+        self._name_base = (0, len(tables[0].names_blob))
+        self.edited: Dict[Tuple[int, int, int], bytes] = {}   # indel-edited records (write_fastqs)
 
-    def records(self, recs: Sequence[Tuple[int, int, int]]) -> dict:
+    @staticmethod
+    def _key(ds, row, sc):
+        return ((np.asarray(sc, np.int64) + 1) << 33) | (np.asarray(ds, np.int64) << 32) | np.asarray(row, np.int64)
+
+    def records_arrays(self, ds: np.ndarray, row: np.ndarray, sc: np.ndarray) -> dict:
         """The record arrays of instances ``(dataset, row, write scope | -1)``."""
-        n = len(recs)
+        n = len(ds)
         T, N = self.tables
-        ds = np.fromiter((r[0] for r in recs), np.int64, n)
-        row = np.fromiter((r[1] for r in recs), np.int64, n)
-        sc = np.fromiter((r[2] for r in recs), np.int64, n)
+        ds = np.asarray(ds, np.int64)
+        row = np.asarray(row, np.int64)
+        sc = np.asarray(sc, np.int64)
+        t0, t1 = ds == 0, ds == 1
+        r0, r1 = np.where(t0, row, 0), np.where(t1, row, 0)
+        pick = lambda f, dt: np.where(t0, getattr(T, f)[r0], getattr(N, f)[r1]).astype(dt)
         seq_sel = np.where(sc >= 0, 0, 1 + ds).astype(np.uint8)
-        seq_off_t = np.where(ds == 0, T.seq_off[np.where(ds == 0, row, 0)], N.seq_off[np.where(ds == 1, row, 0)])
-        base = np.where(ds == 0, self.res.seq_base[0], self.res.seq_base[1])
+        seq_off_t = pick("seq_off", np.int64)
+        base = np.where(t0, self.res.seq_base[0], self.res.seq_base[1])
         byte_off = np.where(sc >= 0, base + seq_off_t, seq_off_t)
-        pick = lambda f, dt: np.where(ds == 0, getattr(T, f)[np.where(ds == 0, row, 0)],
-                                      getattr(N, f)[np.where(ds == 1, row, 0)]).astype(dt)
         seq_len = pick("l_seq", np.int32)
         flag = pick("flag", np.int64)
-        enc = [self.tables[d].names[r].encode() for d, r, _ in recs]
-        name_len = np.array([len(e) for e in enc], np.int32)
+        name_off = pick("name_off", np.int64) + np.where(t0, self._name_base[0], self._name_base[1])
         return {
             "seq_bufs": self._seq_bufs, "seq_sel": seq_sel, "seq_nib_off": (2 * byte_off).astype(np.int64),
             "seq_len": seq_len, "reverse": pick("is_reverse", np.uint8),
             "qual_bufs": self._qual_bufs, "qual_sel": ds.astype(np.uint8), "qual_off": pick("qual_off", np.int64),
             "qual_len": seq_len.copy(), "qual_rev": np.zeros(n, np.uint8),   # stored order for every read (Q1)
-            "names": b"".join(enc), "name_len": name_len,
-            "name_off": np.concatenate([[0], np.cumsum(name_len)[:-1]]).astype(np.int64),
+            "names": self._names, "name_len": pick("name_len", np.int32), "name_off": name_off,
             "mate": np.where(flag & 0x40, 1, 2).astype(np.uint8),
         }
 
-    def _native(self, recs: Sequence[Tuple[int, int, int]]) -> bytes:
-        if len(recs) == 0:
+    def records(self, recs: Sequence[Tuple[int, int, int]]) -> dict:
+        a = np.array(recs, np.int64).reshape(-1, 3)
+        return self.records_arrays(a[:, 0], a[:, 1], a[:, 2])
+
+    def _native(self, ds, row, sc) -> bytes:
+        if len(ds) == 0:
             return b""
         try:
-            return self.backend(self.records(recs))
+            return self.backend(self.records_arrays(ds, row, sc))
         except native.FastqBadRecord as e:
-            d, r, _ = recs[e.index]
+            d, r = int(ds[e.index]), int(row[e.index])
             raise TypeError(f"reverse read {self.tables[d].names[r]!r} has a base outside ACGTN: the "
                             "reference's reverse complement fails on it (SURVEY Q7)") from None
 
@@ -114,20 +124,41 @@ class FastqFormatter:
         return (f"@{t.names[row]}/{mate}\n".encode() + bytes(seq) + b"\n+\n" +
                 bytes(x + 33 for x in qual) + b"\n")
 
-    def format(self, recs: Sequence[Tuple[int, int, int]]) -> bytes:
-        parts: List[bytes] = []
-        run: List[Tuple[int, int, int]] = []
+    def format_arrays(self, ds: np.ndarray, row: np.ndarray, sc: np.ndarray) -> bytes:
+        """Records in the given order: every unedited record in ONE formatter call, the rare
+        indel-edited ones (variable length, formatted on the host) spliced in."""
+        ds = np.asarray(ds, np.int64)
+        row = np.asarray(row, np.int64)
+        sc = np.asarray(sc, np.int64)
         left = self.res.leftovers
-        for inst in recs:
-            edits = left.get(inst)
-            if edits is None:
-                run.append(inst)
-                continue
-            parts.append(self._native(run))
-            run = []
-            parts.append(self._edited(inst, edits))
-        parts.append(self._native(run))
+        if not left:
+            return self._native(ds, row, sc)
+        keys = self._key(ds, row, sc)
+        lk = self._key(*zip(*left.keys()))
+        ed = np.nonzero(np.isin(keys, lk))[0]
+        if len(ed) == 0:
+            return self._native(ds, row, sc)
+        keep = np.ones(len(ds), bool)
+        keep[ed] = False
+        data = self._native(ds[keep], row[keep], sc[keep])
+        T, N = self.tables
+        nl = np.where(ds == 0, T.name_len[np.where(ds == 0, row, 0)], N.name_len[np.where(ds == 1, row, 0)])
+        ls = np.where(ds == 0, T.l_seq[np.where(ds == 0, row, 0)], N.l_seq[np.where(ds == 1, row, 0)])
+        rl = np.where(keep, nl.astype(np.int64) + 8 + 2 * ls.astype(np.int64), 0)
+        off = np.concatenate([[0], np.cumsum(rl)])      # byte offset in `data` of each record
+        parts, prev = [], 0
+        for i in ed.tolist():
+            parts.append(data[off[prev]:off[i]])
+            inst = (int(ds[i]), int(row[i]), int(sc[i]))
+            b = self.edited.get(inst)
+            parts.append(b if b is not None else self._edited(inst, left[inst]))
+            prev = i + 1
+        parts.append(data[off[prev]:])
         return b"".join(parts)
+
+    def format(self, recs: Sequence[Tuple[int, int, int]]) -> bytes:
+        a = np.array(recs, np.int64).reshape(-1, 3)
+        return self.format_arrays(a[:, 0], a[:, 1], a[:, 2])
 
 
 TEXT_CHUNK = 8192  # TextIOWrapper._CHUNK_SIZE of CPython
@@ -223,21 +254,32 @@ def write_fastqs(plan: Plan, res: MaskResult, tables, prefixes: Tuple[str, str],
     fmt = FastqFormatter(tables, res, backend)
     if block_size is None:
         block_size = io_block_size(os.path.dirname(os.path.abspath(prefixes[0])))
-    edited = {inst: fmt._edited(inst, e) for inst, e in res.leftovers.items()}
-
-    def rec_len(inst):
-        b = edited.get(inst)
-        if b is not None:
-            return len(b)
-        t = tables[inst[0]]
-        return int(t.name_len[inst[1]]) + 8 + 2 * int(t.l_seq[inst[1]])
-
-    order = replay_io(plan.io_log, rec_len, block_size)
+    fmt.edited = {inst: fmt._edited(inst, e) for inst, e in res.leftovers.items()}
+    ev, rows = plan.io_arrays()
+    ids = ev[:, 4].astype(np.int64)
+    isc = ev[:, 5].astype(np.int64)
+    T, N = tables
+    wr = ev[:, 0] == 1
+    r0 = np.where(wr & (ids == 0), rows, 0)
+    r1 = np.where(wr & (ids == 1), rows, 0)
+    rec_len = np.where(ids == 0, T.name_len[r0].astype(np.int64) + 8 + 2 * T.l_seq[r0].astype(np.int64),
+                       N.name_len[r1].astype(np.int64) + 8 + 2 * N.l_seq[r1].astype(np.int64))
+    if fmt.edited:
+        keys = np.where(wr, FastqFormatter._key(ids, rows, isc), -1)
+        ek = FastqFormatter._key(*zip(*fmt.edited.keys()))
+        el = np.array([len(b) for b in fmt.edited.values()], np.int64)
+        o = np.argsort(ek)
+        ek, el = ek[o], el[o]
+        j = np.minimum(np.searchsorted(ek, keys), len(ek) - 1)
+        hit = ek[j] == keys
+        rec_len[hit] = el[j[hit]]
+    order = native.io_replay(ev, np.where(wr, rec_len, 0), block_size)
     sizes = {}
     for ds in (0, 1):
         for slot in (0, 1):
             path = f"{prefixes[ds]}.{slot + 1}.fastq"
-            data = fmt.format(order[(ds, slot)])
+            e = order[2 * ds + slot]
+            data = fmt.format_arrays(ids[e], rows[e], isc[e])
             with open(path, "wb") as fh:
                 fh.write(data)
             sizes[path] = len(data)

@@ -140,5 +140,14 @@ GANON_HOST_API int ganon_plan_run(const ganon_plan_input *in, ganon_plan **out);
 GANON_HOST_API int ganon_plan_view_get(const ganon_plan *plan, ganon_plan_view *view);
 GANON_HOST_API void ganon_plan_free(ganon_plan *plan);
 GANON_HOST_API const char *ganon_plan_last_error(void);
+/* Order in which the write events of an I/O log (ganon_plan_view.events layout, 7 ints each)
+ * reach the four FASTQ files (tumor .1, tumor .2, normal .1, normal .2 = file dataset * 2 + slot):
+ * every "open" creates four CPython append-mode text handles (8 KiB TextIOWrapper chunks over a
+ * BufferedWriter of `block` bytes), records become visible when a flush reaches the raw layer
+ * (SR:297-299, 516-518, 564-566). rec_len[i]: byte length of write event i's record.
+ * order (>= number of write events) receives event indices, file by file; file_count[4] their
+ * counts. Returns the number written or GANON_PLAN_E_ARG (unbalanced log). */
+GANON_HOST_API int64_t ganon_io_replay(int64_t n_events, const int32_t *events, const int64_t *rec_len,
+                                       int64_t block, int64_t *order, int64_t *file_count);
 
 #endif /* GANON_HOST_H */

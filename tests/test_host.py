@@ -190,3 +190,35 @@ def test_native_planner_raises_like_python_planner(tmp_path):
                                                      ContigSpec("c1", 5000, 100)])
     a, b = _plans(generate(cfg, str(tmp_path / "in")))
     assert a == b == ("ValueError",)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_native_io_replay_matches_python_model(seed):
+    """ganon_io_replay against writer.replay_io (the CPython buffering model checked above) on
+    random nested open/write/close logs with record sizes around the 8 KiB chunk and block."""
+    from genomeanonymizer_amd import native, writer
+    rng = random.Random(seed)
+    log, open_h, nxt = [], [], 0
+    for _ in range(3000):
+        u = rng.random()
+        if u < 0.08 or not open_h:
+            log.append(("open", nxt))
+            open_h.append(nxt)
+            nxt += 1
+        elif u < 0.14 and len(open_h) > 1:
+            h = open_h.pop(rng.randrange(len(open_h)))
+            log.append(("close", h))
+        else:
+            h = rng.choice(open_h)
+            ds, sl = rng.randrange(2), rng.randrange(2)
+            log.append(("write", h, ds, sl, (ds, len(log), -1)))
+    for h in reversed(open_h):
+        log.append(("close", h))
+    sizes = {i: rng.choice([40, 300, 2000, 5000, 9000]) for i in range(len(log))}
+    block = rng.choice([4096, 8192, 65536])
+    want = writer.replay_io(log, lambda inst: sizes[inst[1]], block)
+    from genomeanonymizer_amd.planner import Plan
+    ev, rows = Plan([], log, {0: [], 1: []}, [], False).io_arrays()
+    got = native.io_replay(ev, np.array([sizes[i] for i in range(len(log))], np.int64), block)
+    for f in range(4):
+        assert [i[1] for i in want[(f // 2, f % 2)]] == rows[got[f]].tolist()

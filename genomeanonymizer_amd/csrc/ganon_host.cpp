@@ -148,64 +148,122 @@ GANON_HOST_API int ganon_bam_open(const char *path, int threads, ganon_bam **out
     p += 4;
     bam->ref_len.push_back(l_ref);
   }
-  // ---- records ----
+  // ---- records: boundaries (sequential), sizes + offsets, then columns in parallel ----
+  std::vector<int64_t> rec;   // offset of each record's block_size field
   while (p < n) {
     int32_t bs;
     if (p + 4 > n) return die("truncated record size");
     std::memcpy(&bs, d + p, 4);
     if (bs < 32 || p + 4 + bs > n) return die("bad record size");
-    const uint8_t *r = d + p + 4;
-    int32_t rtid, rpos, mtid, mpos, rtlen, lseq;
-    uint16_t ncig, rflag;
-    std::memcpy(&rtid, r + 0, 4);
-    std::memcpy(&rpos, r + 4, 4);
-    const uint8_t l_rn = r[8], rmapq = r[9];
-    std::memcpy(&ncig, r + 12, 2);
-    std::memcpy(&rflag, r + 14, 2);
-    std::memcpy(&lseq, r + 16, 4);
-    std::memcpy(&mtid, r + 20, 4);
-    std::memcpy(&mpos, r + 24, 4);
-    std::memcpy(&rtlen, r + 28, 4);
-    int64_t q = 32;
-    const int64_t need = q + l_rn + 4LL * ncig + (lseq + 1) / 2 + lseq;
-    if (lseq < 0 || need > bs) return die("record fields exceed block size");
-    bam->tid.push_back(rtid);
-    bam->pos.push_back(rpos);
-    bam->flag.push_back(rflag);
-    bam->mapq.push_back(rmapq);
-    bam->l_seq.push_back(lseq);
-    bam->n_cigar.push_back(ncig);
-    bam->mate_tid.push_back(mtid);
-    bam->mate_pos.push_back(mpos);
-    bam->tlen.push_back(rtlen);
-    bam->name_off.push_back((int64_t)bam->names.size());
-    bam->name_len.push_back(l_rn > 0 ? l_rn - 1 : 0);
-    bam->names.insert(bam->names.end(), r + q, r + q + l_rn);
-    if (l_rn == 0 || bam->names.back() != '\0') bam->names.push_back('\0');
-    q += l_rn;
-    bam->cig_off.push_back((int64_t)bam->cigar.size());
-    int64_t rlen = 0;
-    for (int k = 0; k < ncig; ++k) {
-      uint32_t w;
-      std::memcpy(&w, r + q + 4 * k, 4);
-      bam->cigar.push_back(w);
-      const int op = w & 0xF;
-      if (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) rlen += w >> 4;
-    }
-    q += 4LL * ncig;
-    if (rflag & 4) rlen = 0;
-    bam->end.push_back((int32_t)(rpos + (rlen > 0 ? rlen : 1)));
-    bam->seq_off.push_back((int64_t)bam->seq.size());
-    bam->seq.insert(bam->seq.end(), r + q, r + q + (lseq + 1) / 2);
-    q += (lseq + 1) / 2;
-    bam->qual_off.push_back((int64_t)bam->qual.size());
-    bam->qual.insert(bam->qual.end(), r + q, r + q + lseq);
-    q += lseq;
-    bam->aux_off.push_back((int64_t)bam->aux.size());
-    bam->aux_len.push_back((int32_t)(bs - q));
-    bam->aux.insert(bam->aux.end(), r + q, r + bs);
+    rec.push_back(p);
     p += 4 + bs;
   }
+  const int64_t nr = (int64_t)rec.size();
+  // per record: name bytes kept, CIGAR ops, sequence length, aux bytes
+  std::vector<int64_t> o_name(nr + 1), o_cig(nr + 1), o_seq(nr + 1), o_qual(nr + 1), o_aux(nr + 1);
+  std::atomic<int64_t> first_bad{INT64_MAX};
+  auto run_chunks = [&](auto &&fn) {
+    std::vector<std::thread> ts;
+    const int64_t per = (nr + nt - 1) / std::max(nt, 1);
+    for (int t = 1; t < nt; ++t) ts.emplace_back([&, t] { fn(std::min(nr, t * per), std::min(nr, (t + 1) * per)); });
+    fn((int64_t)0, std::min(nr, per));
+    for (auto &th : ts) th.join();
+  };
+  run_chunks([&](int64_t i0, int64_t i1) {
+    for (int64_t i = i0; i < i1; ++i) {
+      const uint8_t *r = d + rec[i] + 4;
+      int32_t bs, lseq;
+      uint16_t ncig;
+      std::memcpy(&bs, d + rec[i], 4);
+      std::memcpy(&ncig, r + 12, 2);
+      std::memcpy(&lseq, r + 16, 4);
+      const uint8_t l_rn = r[8];
+      const int64_t need = 32 + (int64_t)l_rn + 4LL * ncig + (lseq + 1) / 2 + lseq;
+      if (lseq < 0 || need > bs) {
+        int64_t cur = first_bad.load();
+        while (i < cur && !first_bad.compare_exchange_weak(cur, i)) {
+        }
+        o_name[i + 1] = o_cig[i + 1] = o_seq[i + 1] = o_qual[i + 1] = o_aux[i + 1] = 0;
+        continue;
+      }
+      o_name[i + 1] = l_rn + ((l_rn == 0 || r[32 + l_rn - 1] != 0) ? 1 : 0);
+      o_cig[i + 1] = ncig;
+      o_seq[i + 1] = (lseq + 1) / 2;
+      o_qual[i + 1] = lseq;
+      o_aux[i + 1] = bs - need;
+    }
+  });
+  if (first_bad.load() != INT64_MAX) return die("record fields exceed block size");
+  for (int64_t i = 0; i < nr; ++i) {
+    o_name[i + 1] += o_name[i];
+    o_cig[i + 1] += o_cig[i];
+    o_seq[i + 1] += o_seq[i];
+    o_qual[i + 1] += o_qual[i];
+    o_aux[i + 1] += o_aux[i];
+  }
+  for (auto *v : {&bam->tid, &bam->pos, &bam->end, &bam->flag, &bam->mapq, &bam->l_seq, &bam->n_cigar, &bam->mate_tid,
+                  &bam->mate_pos, &bam->tlen, &bam->name_len, &bam->aux_len})
+    v->resize((size_t)nr);
+  for (auto *v : {&bam->name_off, &bam->cig_off, &bam->seq_off, &bam->qual_off, &bam->aux_off}) v->resize((size_t)nr);
+  bam->names.resize((size_t)o_name[nr]);
+  bam->cigar.resize((size_t)o_cig[nr]);
+  bam->seq.resize((size_t)o_seq[nr]);
+  bam->qual.resize((size_t)o_qual[nr]);
+  bam->aux.resize((size_t)o_aux[nr]);
+  run_chunks([&](int64_t i0, int64_t i1) {
+    for (int64_t i = i0; i < i1; ++i) {
+      const uint8_t *r = d + rec[i] + 4;
+      int32_t bs, rtid, rpos, mtid, mpos, rtlen, lseq;
+      uint16_t ncig, rflag;
+      std::memcpy(&bs, d + rec[i], 4);
+      std::memcpy(&rtid, r + 0, 4);
+      std::memcpy(&rpos, r + 4, 4);
+      const uint8_t l_rn = r[8], rmapq = r[9];
+      std::memcpy(&ncig, r + 12, 2);
+      std::memcpy(&rflag, r + 14, 2);
+      std::memcpy(&lseq, r + 16, 4);
+      std::memcpy(&mtid, r + 20, 4);
+      std::memcpy(&mpos, r + 24, 4);
+      std::memcpy(&rtlen, r + 28, 4);
+      bam->tid[i] = rtid;
+      bam->pos[i] = rpos;
+      bam->flag[i] = rflag;
+      bam->mapq[i] = rmapq;
+      bam->l_seq[i] = lseq;
+      bam->n_cigar[i] = ncig;
+      bam->mate_tid[i] = mtid;
+      bam->mate_pos[i] = mpos;
+      bam->tlen[i] = rtlen;
+      int64_t q = 32;
+      bam->name_off[i] = o_name[i];
+      bam->name_len[i] = l_rn > 0 ? l_rn - 1 : 0;
+      char *nm = bam->names.data() + o_name[i];
+      std::memcpy(nm, r + q, l_rn);
+      if (o_name[i + 1] - o_name[i] > l_rn) nm[l_rn] = '\0';
+      q += l_rn;
+      bam->cig_off[i] = o_cig[i];
+      int64_t rlen = 0;
+      uint32_t *cg = bam->cigar.data() + o_cig[i];
+      std::memcpy(cg, r + q, 4LL * ncig);
+      for (int k = 0; k < ncig; ++k) {
+        const uint32_t w = cg[k];
+        const int op = w & 0xF;
+        if (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) rlen += w >> 4;
+      }
+      q += 4LL * ncig;
+      if (rflag & 4) rlen = 0;
+      bam->end[i] = (int32_t)(rpos + (rlen > 0 ? rlen : 1));
+      bam->seq_off[i] = o_seq[i];
+      std::memcpy(bam->seq.data() + o_seq[i], r + q, (size_t)((lseq + 1) / 2));
+      q += (lseq + 1) / 2;
+      bam->qual_off[i] = o_qual[i];
+      std::memcpy(bam->qual.data() + o_qual[i], r + q, (size_t)lseq);
+      q += lseq;
+      bam->aux_off[i] = o_aux[i];
+      bam->aux_len[i] = (int32_t)(bs - q);
+      std::memcpy(bam->aux.data() + o_aux[i], r + q, (size_t)(bs - q));
+    }
+  });
   *out = bam;
   return 0;
 }

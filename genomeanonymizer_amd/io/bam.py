@@ -84,14 +84,26 @@ class ReadTable:
             self.aux = _blob(v.aux, int(v.aux_bytes)).copy()
         finally:
             lib.ganon_bam_close(h)
-        nb = self.names_blob.tobytes()
-        self.names: List[str] = [nb[o:o + l].decode() for o, l in zip(self.name_off.tolist(), self.name_len.tolist())]
+        self._names: Optional[List[str]] = None
         self.is_unmapped = (self.flag & FLAG_UNMAP) != 0
         self.is_reverse = (self.flag & FLAG_REVERSE) != 0
         # pair slot as AnonymizedRead.get_pair_idx (anonymizer_methods.py:119-123): -1 = neither flag
         self.mate_idx = np.where(self.flag & FLAG_READ1, 0, np.where(self.flag & FLAG_READ2, 1, -1)).astype(np.int8)
         self.has_cigar = self.n_cigar > 0
         self._index: Dict[int, tuple] = {}
+
+    @property
+    def names(self) -> List[str]:
+        """Read names as str (built on first use: the native planner and the formatters work on
+        ``names_blob`` / ``name_off`` / ``name_len`` directly)."""
+        if self._names is None:
+            nb = self.names_blob.tobytes()
+            self._names = [nb[o:o + l].decode() for o, l in zip(self.name_off.tolist(), self.name_len.tolist())]
+        return self._names
+
+    def name(self, i: int) -> str:
+        o = int(self.name_off[i])
+        return self.names_blob[o:o + int(self.name_len[i])].tobytes().decode()
 
     # -- htslib-style region query -----------------------------------------------------
     def _tid_index(self, tid: int):

@@ -96,7 +96,7 @@ class FastqFormatter:
             return self.backend(self.records_arrays(ds, row, sc))
         except native.FastqBadRecord as e:
             d, r = int(ds[e.index]), int(row[e.index])
-            raise TypeError(f"reverse read {self.tables[d].names[r]!r} has a base outside ACGTN: the "
+            raise TypeError(f"reverse read {self.tables[d].name(r)!r} has a base outside ACGTN: the "
                             "reference's reverse complement fails on it (SURVEY Q7)") from None
 
     def _edited(self, inst, edits) -> bytes:
@@ -116,12 +116,12 @@ class FastqFormatter:
             try:
                 seq = bytearray(_REVERSES[c] for c in reversed(seq))
             except KeyError:
-                raise TypeError(f"reverse read {t.names[row]!r} has a base outside ACGTN (SURVEY Q7)")
+                raise TypeError(f"reverse read {t.name(row)!r} has a base outside ACGTN (SURVEY Q7)")
             qual = qual_fwd[::-1]
         else:
             qual = qual_fwd
         mate = 1 if t.flag[row] & 0x40 else 2
-        return (f"@{t.names[row]}/{mate}\n".encode() + bytes(seq) + b"\n+\n" +
+        return (f"@{t.name(row)}/{mate}\n".encode() + bytes(seq) + b"\n+\n" +
                 bytes(x + 33 for x in qual) + b"\n")
 
     def format_arrays(self, ds: np.ndarray, row: np.ndarray, sc: np.ndarray) -> bytes:

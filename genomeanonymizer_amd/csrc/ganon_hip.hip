@@ -967,7 +967,7 @@ constexpr unsigned long long kNibMask = (1ull << 48) - 1;
 // key-range pass: observations to the LDS list, overflow to the group's global region
 enum { kModeCollect = 0 };
 // GANON_PARAM_GROUP_SKIP (profiling only, results invalid): phases left out
-enum { kSkipClassify = 1, kSkipChunks = 2, kSkipCopy = 4 };
+enum { kSkipClassify = 1, kSkipChunks = 2, kSkipCopy = 4, kSkipCounts = 8 };
 static_assert(kGrpTile == kGrpThreads && kGrpTile <= 256, "one staged record per thread, 8-bit map");
 
 // The few batch arrays the group kernels read (a slim kernel argument keeps SGPRs free).
@@ -1479,7 +1479,7 @@ __global__ void __launch_bounds__(kGrpThreads, (U == 1 ? 6 : U == 2 ? GANON_K2_B
     if (top < 0) {
       // per-scope counts (wide scopes in the id range belong to the tile path) and the
       // workgroup's partial totals (k_finish sums them)
-      for (int i = tid; i < s_end - s_begin; i += kGrpThreads) {
+      for (int i = tid; i < ((skip & kSkipCounts) ? 0 : s_end - s_begin); i += kGrpThreads) {
         if (B.span_len[s_begin + i] > kGrpMaxSpan) continue;
         aux->scope_calls[s_begin + i] = sh.cnt_calls[i];
         aux->scope_bases[s_begin + i] = sh.cnt_bases[i];
@@ -1969,7 +1969,7 @@ GANON_API int ganon_ctx_set_param(ganon_ctx *ctx, int param, int value) {
     return GANON_OK;
   }
   if (param == GANON_PARAM_GROUP_SKIP) {
-    ctx->group_skip = value & (kSkipClassify | kSkipChunks | kSkipCopy);
+    ctx->group_skip = value & (kSkipClassify | kSkipChunks | kSkipCopy | kSkipCounts);
     return GANON_OK;
   }
   return fail(ctx, GANON_E_ARG, "unknown parameter %d", param);

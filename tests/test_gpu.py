@@ -242,3 +242,42 @@ def test_hip_empty_and_degenerate_batches(masker):
     bad["scope_span_len"] = np.maximum(arr["scope_span_len"] - 10, 0).astype(np.int32)
     with pytest.raises(native.GanonError):
         masker.mask(bad)
+
+
+@pytest.fixture(scope="module")
+def c2_full():
+    """BASELINE configs[1] at full size: the bench workload (10 M reads, 3.0 Gb, 1 M windows)."""
+    from genomeanonymizer_amd.synth.batch import config2_batch
+    arr, info = config2_batch()
+    return arr, info
+
+
+def test_hip_config2_full_size_matches_oracle_and_is_idempotent(masker, oracle, c2_full):
+    """Full BASELINE configs[1] batch: every byte and count equal to the C oracle, and masking
+    the masked output again masks nothing (each masked base now equals the reference)."""
+    arr, info = c2_full
+    assert info["reads"] == 10_000_000
+    out, calls, bases, tot = masker.mask(arr)
+    o_out, o_calls, o_bases, _ = oracle.mask(arr)
+    assert np.array_equal(calls, o_calls)
+    assert np.array_equal(bases, o_bases)
+    assert np.array_equal(out, o_out)
+    assert tot[1] == bases.sum() > 0
+    del o_out
+    arr2 = dict(arr)
+    arr2["seq_nt16"] = out
+    out2, calls2, bases2, _ = masker.mask(arr2)
+    assert bases2.sum() == 0 and calls2.sum() == 0
+    assert np.array_equal(out2, out)
+
+
+def test_hip_fastq_full_size_matches_host_formatter(masker, c2_full):
+    """10 M FASTQ records formatted on the device equal libganon_host.so's byte for byte."""
+    from genomeanonymizer_amd import native
+    from genomeanonymizer_amd.synth.fastq import fastq_records
+    arr, _ = c2_full
+    recs = fastq_records(arr, seed=11, reverse_frac=0.5, name_len=(30, 45), check_bad=False)
+    got = masker.format_fastq(recs)
+    want = native.host_format_fastq(recs)
+    assert len(got) == native.fastq_bytes(recs) == len(want)
+    assert got == want

@@ -120,7 +120,7 @@ GANON_API int ganon_ctx_set_variant(ganon_ctx *ctx, int variant);
  * the classification, bit 1 the chunk scan, bit 2 the partition copy of the group kernels, bit 3
  * the per-scope count stores.
  * Keep it 0 in production. GANON_PARAM_GROUP_TARGET: segments per scope group (read at
- * upload; default 256). GANON_PARAM_NT_COPY: non-temporal stores for the fused partition copy
+ * upload; default 512). GANON_PARAM_NT_COPY: non-temporal stores for the fused partition copy
  * (default 1). GANON_PARAM_REF2: group kernels read a 2-bit copy of the reference for segments
  * whose reference range is all ACGT (1, default) or the nt16 reference only (0).
  * GANON_PARAM_FASTQ_KD: output dwords per lane the FASTQ formatter loads at once (1, 2, 4).

@@ -52,12 +52,12 @@ def kernel_class(name: str) -> str:
         return "large"
     if name.startswith("k_group"):
         return "group"
-    if name in ("k_indel_emit", "indel_sort", "k_indel_classify", "indel_scan"):
+    if name in ("indel_candidates", "k_indel_emit", "indel_sort", "k_indel_classify"):
         return name
     return ""
 
 
-def indel_bytes(arr, n_obs: int) -> dict:
+def indel_bytes(arr, n_obs: int, n_emit: int = None) -> dict:
     """Algorithmic bytes per launch of the indel tally (ganon_indel.hip): the emission reads the
     CIGARs of the incidences whose read has an I/D op and writes a 16-byte observation + 8-byte key
     + 4-byte index per op; the sort reads and writes each (key, index) pair once; the
@@ -69,8 +69,9 @@ def indel_bytes(arr, n_obs: int) -> dict:
     has[np.unique(rid[(ops == 1) | (ops == 2)])] = True
     r = arr["incid_read"].astype(np.int64)
     cig = int((4 * arr["n_cig"].astype(np.int64)[r])[has[r]].sum())
-    return {"k_indel_emit": cig + 28 * n_obs, "indel_sort": 24 * n_obs,
-            "k_indel_classify": 41 * n_obs, "indel_scan": 9 * n_obs}
+    n_emit = n_obs if n_emit is None or n_emit < 0 else n_emit
+    return {"indel_candidates": 2 * cig, "k_indel_emit": cig + 32 * n_emit, "indel_sort": 24 * n_emit,
+            "k_indel_classify": 45 * n_emit}
 
 
 def kernel_bytes(arr, mode: str = "fused") -> dict:
@@ -368,7 +369,7 @@ def main() -> None:
     db.free()
 
     kb = kernel_bytes(arr, VARIANT_WRITE[args.variant])
-    kb.update(indel_bytes(arr, indel_info["observations"]))
+    kb.update(indel_bytes(arr, indel_info["observations"], indel_info["emitted"]))
     per_kernel = {n: {"launches": c, "avg_ms": ms / c} for n, (c, ms) in ktimes.items()}
     dom = max(per_kernel, key=lambda n: per_kernel[n]["avg_ms"] * per_kernel[n]["launches"])
     indel_ms = sum(v["avg_ms"] * v["launches"] for n, v in per_kernel.items() if "indel" in n) / args.steps
@@ -416,7 +417,8 @@ def main() -> None:
                  "achieved_GBps": round(alg_total / (pass_ms * 1e-3) / 1e9, 1),
                  "kernels": {n: {"avg_ms": round(v["avg_ms"], 5), "launches_per_step": v["launches"] // args.steps,
                                  "alg_bytes": kb.get(kernel_class(n))} for n, v in per_kernel.items()}},
-        "indel": {"observations": indel_info["observations"], "incidences": indel_info["incidences"],
+        "indel": {"observations": indel_info["observations"], "emitted": indel_info["emitted"],
+                  "incidences": indel_info["incidences"],
                   "masked_calls": int((irecs["kind"] == native.INDEL_CALL).sum()),
                   "support_records": int((irecs["kind"] == native.INDEL_SUPPORT).sum()),
                   "ms_per_step": round(indel_ms, 4)},

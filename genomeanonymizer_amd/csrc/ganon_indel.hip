@@ -44,10 +44,25 @@ using ganon_detail::KernelScope;
 
 namespace {
 
-struct IndelInc {       // one incidence with an I/D op (host plan)
+// Work items are blocks of kWalkOps CIGAR ops (long-read CIGARs hold thousands of ops), each with
+// the reference's running offsets at its first op computed on the host, so that every block is an
+// independent wave.
+constexpr int kWalkJ = 4;
+constexpr int kWalkOps = 64 * kWalkJ;
+
+struct IndelInc {       // one block of one incidence with an I/D op (host plan)
   int32_t read;
   uint32_t scope_par;   // scope | (index of the scope among scopes with observations & 1) << 31
-  int64_t obs_off;      // first observation slot
+  int32_t k0;           // first CIGAR op of the block
+  int32_t pos0, irp0;   // reference position / in_read_pos at op k0
+  int32_t pad;
+  int64_t obs_off;      // slot of the block's first I/D op (unfiltered numbering = registration order)
+  int64_t cbase;        // genome nibble index of the read's contig start (candidate map)
+};
+
+struct IndelRead {      // one block of one read with an I/D op (candidate marking)
+  int32_t read, k0, pos0, pad;
+  int64_t cbase;
 };
 
 struct IndelObs {       // one I/D op of one incidence
@@ -55,7 +70,14 @@ struct IndelObs {       // one I/D op of one incidence
   int32_t irp;          // in_read_pos (reference arithmetic)
   int32_t scope;
   int32_t type_len;     // length << 1 | is_insertion
+  uint32_t ord;         // unfiltered slot: incidence order, then op order (registration order)
 };
+
+// Candidate map: 2 bits per genome position (bit 0: one read has an I/D op there, bit 1: two or
+// more). An observation at a position with bit 1 clear is alone at its (scope, position) in every
+// scope, so it cannot be part of a tumor AND normal call or change the rank of one: it is not
+// emitted (GANON_PARAM_INDEL_SORT 0).
+
 
 // Sort keys. Segmented (default): one segment per scope, 32-bit key = segment parity << 31 |
 // (pos - span_start), sorted on the position bits only — the parity bit still tells adjacent
@@ -84,47 +106,147 @@ __device__ __forceinline__ int wave_excl_scan(int v, int lane) {
   return x - v;
 }
 
-template <typename KeyT>
+// The reference's offsets of a read's ops, 64 CIGAR ops per step of one wave: pos = reference
+// start + M/D/N/=/X lengths before the op; irp = M/N/=/X/S/H/I lengths before it.
+struct CigarStep {
+  int op, len, pos, irp;
+  bool is_id;
+};
+
+// One block: every lane loads kWalkJ CIGAR words before any is used, and the callback gets the
+// kWalkJ steps of 64 ops together so that it can issue its own loads (the candidate map) for all of
+// them at once.
+template <typename F>
+__device__ __forceinline__ void walk_block(const GanonReadView &V, int r, int k0, int pos0, int irp0, int lane, F &&f) {
+  const int nc = min(V.n_cig[r], k0 + kWalkOps);
+  const uint32_t *__restrict__ cig = V.cigar + V.cig_off[r];
+  int rcarry = pos0, qcarry = irp0;
+  uint32_t word[kWalkJ];
+#pragma unroll
+  for (int j = 0; j < kWalkJ; ++j) {
+    const int k = k0 + 64 * j + lane;
+    word[j] = k < nc ? cig[k] : 0u;
+  }
+  CigarStep c[kWalkJ];
+#pragma unroll
+  for (int j = 0; j < kWalkJ; ++j) {
+    const int k = k0 + 64 * j + lane;
+    c[j].op = (int)(word[j] & 0xF);
+    c[j].len = (int)(word[j] >> 4);
+    const int op = c[j].op, len = c[j].len;
+    const int radv = (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) ? len : 0;
+    const int qadv = (op == 0 || op == 1 || op == 3 || op == 4 || op == 5 || op == 7 || op == 8) ? len : 0;
+    c[j].is_id = k < nc && (op == 1 || op == 2);
+    c[j].pos = rcarry + wave_excl_scan(radv, lane);
+    c[j].irp = qcarry + wave_excl_scan(qadv, lane);
+    rcarry = __shfl(c[j].pos + radv, 63);
+    qcarry = __shfl(c[j].irp + qadv, 63);
+  }
+  f(c);
+}
+
+// Candidate marking: one wave per block of a read with an I/D op (each read once, whatever its scopes).
+__global__ void __launch_bounds__(kIndelThreads) k_indel_mark(const GanonReadView V, const IndelRead *__restrict__ reads,
+                                                              int64_t n_reads, uint32_t *__restrict__ map) {
+  const int lane = threadIdx.x & 63;
+  const int64_t w = (int64_t)blockIdx.x * kIndelWaves + (threadIdx.x >> 6);
+  if (w >= n_reads) return;
+  const IndelRead e = reads[w];
+  walk_block(V, e.read, e.k0, e.pos0, 0, lane, [&](const CigarStep (&c)[kWalkJ]) {
+    uint32_t old[kWalkJ], bit[kWalkJ];
+    int64_t word[kWalkJ];
+#pragma unroll
+    for (int j = 0; j < kWalkJ; ++j) {
+      const int64_t g = e.cbase + c[j].pos;
+      word[j] = g >> 4;
+      bit[j] = 1u << (2 * (g & 15));
+      old[j] = c[j].is_id ? atomicOr(map + word[j], bit[j]) : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < kWalkJ; ++j)
+      if (c[j].is_id && (old[j] & bit[j])) atomicOr(map + word[j], bit[j] << 1);
+  });
+}
+
+// Candidate bits of kWalkJ steps, their map words loaded together.
+__device__ __forceinline__ void cand_bits(const uint32_t *__restrict__ map, int64_t cbase,
+                                          const CigarStep (&c)[kWalkJ], bool (&hit)[kWalkJ]) {
+  uint32_t mw[kWalkJ];
+#pragma unroll
+  for (int j = 0; j < kWalkJ; ++j) mw[j] = c[j].is_id ? map[(cbase + c[j].pos) >> 4] : 0u;
+#pragma unroll
+  for (int j = 0; j < kWalkJ; ++j)
+    hit[j] = c[j].is_id && ((mw[j] >> (2 * ((cbase + c[j].pos) & 15) + 1)) & 1);
+}
+
+// Candidate observations per listed incidence (filtered emission slots come from their scan).
+__global__ void __launch_bounds__(kIndelThreads) k_indel_count(const GanonReadView V, const IndelInc *__restrict__ list,
+                                                               int64_t n_list, const uint32_t *__restrict__ map,
+                                                               int32_t *__restrict__ cnt) {
+  const int lane = threadIdx.x & 63;
+  const int64_t w = (int64_t)blockIdx.x * kIndelWaves + (threadIdx.x >> 6);
+  if (w >= n_list) return;
+  const IndelInc e = list[w];
+  int total = 0;
+  walk_block(V, e.read, e.k0, e.pos0, e.irp0, lane, [&](const CigarStep (&c)[kWalkJ]) {
+    bool hit[kWalkJ];
+    cand_bits(map, e.cbase, c, hit);
+#pragma unroll
+    for (int j = 0; j < kWalkJ; ++j) total += __popcll(__ballot(hit[j]));
+  });
+  if (lane == 0) cnt[w] = total;
+}
+
+// FILTER: slots from the candidate scan (off[w]), only candidate ops; else the host's slots.
+template <typename KeyT, bool FILTER>
 __global__ void __launch_bounds__(kIndelThreads) k_indel_emit(const GanonReadView V, const IndelInc *__restrict__ list,
-                                                              int64_t n_list, int pos_bits, IndelObs *__restrict__ obs,
+                                                              int64_t n_list, int pos_bits, const uint32_t *__restrict__ map,
+                                                              const int32_t *__restrict__ off, IndelObs *__restrict__ obs,
                                                               KeyT *__restrict__ keys, uint32_t *__restrict__ vals) {
   const int lane = threadIdx.x & 63;
   const int64_t w = (int64_t)blockIdx.x * kIndelWaves + (threadIdx.x >> 6);
   if (w >= n_list) return;
   const IndelInc e = list[w];
-  const int r = e.read;
-  const int nc = V.n_cig[r];
-  const uint32_t *__restrict__ cig = V.cigar + V.cig_off[r];
   const int scope = (int)(e.scope_par & 0x7FFFFFFFu);
   const int span0 = V.span_start[scope];
-  int rcarry = V.ref_start[r], qcarry = 0;
-  int64_t slot = e.obs_off;
-  for (int k0 = 0; k0 < nc; k0 += 64) {
-    const int k = k0 + lane;
-    const uint32_t word = k < nc ? cig[k] : 0u;
-    const int op = (int)(word & 0xF), len = (int)(word >> 4);
-    // reference-consuming M D N = X; the reference's read offset advances on M N = X S H I
-    const int radv = (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) ? len : 0;
-    const int qadv = (op == 0 || op == 1 || op == 3 || op == 4 || op == 5 || op == 7 || op == 8) ? len : 0;
-    const bool is_id = k < nc && (op == 1 || op == 2);
-    const int pos = rcarry + wave_excl_scan(radv, lane);
-    const int irp = qcarry + wave_excl_scan(qadv, lane);
-    const unsigned long long m = __ballot(is_id);
-    if (is_id) {
-      const int64_t o = slot + __popcll(m & ((1ull << lane) - 1ull));
-      IndelObs ob;
-      ob.read = r;
-      ob.irp = irp;
-      ob.scope = scope;
-      ob.type_len = (len << 1) | (op == 1 ? 1 : 0);
-      obs[o] = ob;
-      keys[o] = make_key<KeyT>(e.scope_par, pos_bits, (uint32_t)(pos - span0));
-      vals[o] = (uint32_t)o;
+  int64_t slot = FILTER ? (int64_t)off[w] : e.obs_off;
+  int64_t ord = e.obs_off;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  walk_block(V, e.read, e.k0, e.pos0, e.irp0, lane, [&](const CigarStep (&c)[kWalkJ]) {
+    bool keep[kWalkJ];
+    if (FILTER) {
+      cand_bits(map, e.cbase, c, keep);
+    } else {
+#pragma unroll
+      for (int j = 0; j < kWalkJ; ++j) keep[j] = c[j].is_id;
     }
-    slot += __popcll(m);
-    rcarry = __shfl(pos + radv, 63);
-    qcarry = __shfl(irp + qadv, 63);
-  }
+#pragma unroll
+    for (int j = 0; j < kWalkJ; ++j) {
+      const unsigned long long m_all = __ballot(c[j].is_id);
+      const unsigned long long m = __ballot(keep[j]);
+      if (keep[j]) {
+        const int64_t o = slot + __popcll(m & below);
+        IndelObs ob;
+        ob.read = e.read;
+        ob.irp = c[j].irp;
+        ob.scope = scope;
+        ob.type_len = (c[j].len << 1) | (c[j].op == 1 ? 1 : 0);
+        ob.ord = (uint32_t)(ord + __popcll(m_all & below));
+        obs[o] = ob;
+        keys[o] = make_key<KeyT>(e.scope_par, pos_bits, (uint32_t)(c[j].pos - span0));
+        vals[o] = (uint32_t)o;
+      }
+      slot += __popcll(m);
+      ord += __popcll(m_all);
+    }
+  });
+}
+
+// Segment offsets of the filtered observations: seg_off[k] = off[first listed incidence of k].
+__global__ void k_indel_segs(const int32_t *__restrict__ seg_first, int32_t n_seg, const int32_t *__restrict__ off,
+                             int32_t *__restrict__ seg_off) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k <= n_seg) seg_off[k] = off[seg_first[k]];
 }
 
 // Exact call identity of two observations at the same (scope, pos): type, length, allele.
@@ -146,8 +268,8 @@ __device__ bool same_call(const GanonReadView &V, const IndelObs &a, const Indel
 // Registration order key of an observation: the reference meets reads by first pileup column
 // (ref_start), tumor before normal, file order — the incidence order of the scope — and a read's
 // ops in CIGAR order; observation slots follow incidence then op order.
-__device__ __forceinline__ unsigned long long reg_key(const GanonReadView &V, const IndelObs &o, uint32_t idx) {
-  return ((unsigned long long)(uint32_t)V.ref_start[o.read] << 32) | idx;
+__device__ __forceinline__ unsigned long long reg_key(const GanonReadView &V, const IndelObs &o) {
+  return ((unsigned long long)(uint32_t)V.ref_start[o.read] << 32) | o.ord;
 }
 
 __device__ bool normal_covers(const GanonReadView &V, int scope, int pos) {
@@ -187,7 +309,7 @@ __device__ void classify_run(const GanonReadView &V, const KeyT *__restrict__ ke
       const IndelObs oc = obs[ic];
       if (c != a && !same_call(V, oa, oc)) continue;
       if (V.dataset[oc.read] == 0) t = true; else nn = true;
-      best = min(best, reg_key(V, oc, ic));
+      best = min(best, reg_key(V, oc));
     }
     repk[a] = best;
     if (t && nn) {
@@ -214,7 +336,7 @@ __device__ void classify_run(const GanonReadView &V, const KeyT *__restrict__ ke
       const uint32_t ic = vals[c];
       const IndelObs oc = obs[ic];
       if (c != a && !same_call(V, oa, oc)) continue;
-      uint8_t f = (reg_key(V, oc, ic) == ka) ? 1 : 0;
+      uint8_t f = (reg_key(V, oc) == ka) ? 1 : 0;
       if (V.write_scope[oc.read] == scope) {
         // a read supporting the call twice keeps its last offset (dict assignment)
         bool last = true;
@@ -243,9 +365,10 @@ constexpr int kRunPer = 16;
 constexpr int kRunChunk = 256 * kRunPer;
 
 template <typename KeyT>
-__global__ void __launch_bounds__(256) k_indel_runs(const KeyT *__restrict__ keys, int64_t n,
+__global__ void __launch_bounds__(256) k_indel_runs(const KeyT *__restrict__ keys, const int32_t *__restrict__ n_dev,
                                                     uint8_t *__restrict__ flags, int32_t *__restrict__ run_list,
                                                     unsigned int *__restrict__ run_count) {
+  const int64_t n = *n_dev;
   __shared__ unsigned int wsum[4];
   __shared__ unsigned int base;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -291,13 +414,14 @@ __global__ void __launch_bounds__(256) k_indel_runs(const KeyT *__restrict__ key
 // batch (one atomic add per run that has any).
 template <typename KeyT>
 __global__ void __launch_bounds__(256) k_indel_classify(const GanonReadView V, const KeyT *__restrict__ keys,
-                                                        const uint32_t *__restrict__ vals, int64_t n, int pos_bits,
-                                                        const IndelObs *__restrict__ obs, uint8_t *__restrict__ flags,
-                                                        int32_t *__restrict__ rank,
+                                                        const uint32_t *__restrict__ vals, const int32_t *__restrict__ n_dev,
+                                                        int pos_bits, const IndelObs *__restrict__ obs,
+                                                        uint8_t *__restrict__ flags, int32_t *__restrict__ rank,
                                                         unsigned long long *__restrict__ repk,
                                                         const int32_t *__restrict__ run_list,
                                                         const unsigned int *__restrict__ run_count,
                                                         unsigned long long *__restrict__ n_rec) {
+  const int64_t n = *n_dev;
   const unsigned int n_runs = *run_count;
   for (unsigned int ri = blockIdx.x * blockDim.x + threadIdx.x; ri < n_runs; ri += gridDim.x * blockDim.x)
     classify_run<KeyT>(V, keys, vals, n, pos_bits, obs, flags, rank, repk, run_list[ri], n_rec);
@@ -307,13 +431,13 @@ __global__ void __launch_bounds__(256) k_indel_classify(const GanonReadView V, c
 // Records in device order (slots from an atomic counter; the host sorts them).
 template <typename KeyT>
 __global__ void __launch_bounds__(256) k_indel_write(const GanonReadView V, const KeyT *__restrict__ keys,
-                                                     const uint32_t *__restrict__ vals, int64_t n, int pos_bits,
-                                                     const IndelObs *__restrict__ obs, const uint8_t *__restrict__ flags,
-                                                     const int32_t *__restrict__ rank,
+                                                     const uint32_t *__restrict__ vals, const int32_t *__restrict__ n_dev,
+                                                     int pos_bits, const IndelObs *__restrict__ obs,
+                                                     const uint8_t *__restrict__ flags, const int32_t *__restrict__ rank,
                                                      unsigned long long *__restrict__ slot,
                                                      ganon_indel_rec *__restrict__ out) {
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n) return;
+  if (j >= *n_dev) return;
   const uint8_t f = flags[j];
   if (!f) return;
   const IndelObs o = obs[vals[j]];
@@ -347,13 +471,20 @@ int bits_for(int64_t v) {   // bits to hold 0..v
 struct ganon_indels {
   std::vector<void *> allocs;
   GanonReadView V{};
-  int64_t n_obs = 0, n_list = 0, n_records = -1;
+  int64_t n_obs = 0, n_list = 0, n_rdist = 0, n_records = -1, n_candidates = -1;
   int32_t n_seg = 0;                  // scopes with observations (segments of the sort)
   int pos_bits = 1, key_bits = 2;
-  bool global = false;                // sort strategy of the last run (GANON_PARAM_INDEL_SORT)
+  bool global = false;                // strategy of the last run (GANON_PARAM_INDEL_SORT 1)
   IndelInc *list = nullptr;
-  IndelObs *obs = nullptr;
+  IndelRead *rdist = nullptr;         // distinct reads with an I/D op (candidate marking)
+  uint32_t *map = nullptr;            // candidate map, 2 bits per genome position
+  int64_t map_words = 0;
+  int32_t *cnt = nullptr;             // [n_list + 1] candidate observations per listed incidence
+  int32_t *off = nullptr;             // [n_list + 1] their exclusive scan; off[n_list] = count
+  int32_t *seg_first = nullptr;       // [n_seg + 1] first listed incidence of each segment
   int32_t *seg_off = nullptr;         // [n_seg + 1] observation offsets of the segments
+  int32_t *nval = nullptr;            // [1] n_obs (unfiltered runs)
+  IndelObs *obs = nullptr;
   void *keys[2] = {nullptr, nullptr}; // 8 bytes per observation (either key width)
   uint32_t *vals[2] = {nullptr, nullptr};
   int sorted_sel = 0;                 // which half of the double buffers holds the sorted pairs
@@ -368,6 +499,7 @@ struct ganon_indels {
   ganon_indel_rec *recs = nullptr;
   int64_t recs_cap = 0;
   bool ran = false;
+  const int32_t *n_dev() const { return global ? nval : off + n_list; }
 };
 
 namespace {
@@ -387,6 +519,8 @@ void ind_release(ganon_indels *t) {
   t->allocs.clear();
 }
 
+// Segmented (filtered observations, device segment offsets) or one global sort (all observations).
+// num_items is the capacity: the filtered count stays on the device, the segments bound the work.
 template <typename KeyT>
 hipError_t sort_pairs(ganon_indels *t, void *temp, size_t &bytes, bool global, hipStream_t st, int *sel) {
   hipcub::DoubleBuffer<KeyT> K(static_cast<KeyT *>(t->keys[0]), static_cast<KeyT *>(t->keys[1]));
@@ -401,17 +535,39 @@ hipError_t sort_pairs(ganon_indels *t, void *temp, size_t &bytes, bool global, h
   return e;
 }
 
+hipError_t scan_counts(ganon_indels *t, void *temp, size_t &bytes, hipStream_t st) {
+  return hipcub::DeviceScan::ExclusiveSum(temp, bytes, t->cnt, t->off, (int)(t->n_list + 1), st);
+}
+
 template <typename KeyT>
 int run_tally(ganon_ctx *ctx, ganon_indels *t) {
   int rc;
-  const int64_t n = t->n_obs;
+  const int64_t n = t->n_obs;   // capacity
+  const bool filter = !t->global;
+  const unsigned lgrid = (unsigned)((t->n_list + kIndelWaves - 1) / kIndelWaves);
   HIP_OR_FAIL(hipMemsetAsync(t->counters, 0, 2 * sizeof(unsigned long long), ctx->stream));
   HIP_OR_FAIL(hipMemsetAsync(t->run_count, 0, sizeof(unsigned int), ctx->stream));
+  if (filter) {
+    KernelScope ks(ctx, "indel_candidates");
+    HIP_OR_FAIL(hipMemsetAsync(t->map, 0, (size_t)t->map_words * 4, ctx->stream));
+    hipLaunchKernelGGL(k_indel_mark, dim3((unsigned)((t->n_rdist + kIndelWaves - 1) / kIndelWaves)),
+                       dim3(kIndelThreads), 0, ctx->stream, t->V, t->rdist, t->n_rdist, t->map);
+    hipLaunchKernelGGL(k_indel_count, dim3(lgrid), dim3(kIndelThreads), 0, ctx->stream, t->V, t->list, t->n_list,
+                       t->map, t->cnt);
+    size_t bytes = t->temp_bytes;
+    if (scan_counts(t, t->temp, bytes, ctx->stream) != hipSuccess) return fail(ctx, GANON_E_DEVICE, "indel scan failed");
+    hipLaunchKernelGGL(k_indel_segs, dim3((unsigned)((t->n_seg + 256) / 256)), dim3(256), 0, ctx->stream,
+                       t->seg_first, t->n_seg, t->off, t->seg_off);
+    if ((rc = check_launch(ctx, "indel_candidates"))) return rc;
+  }
   {
     KernelScope ks(ctx, "k_indel_emit");
-    const unsigned grid = (unsigned)((t->n_list + kIndelWaves - 1) / kIndelWaves);
-    hipLaunchKernelGGL(k_indel_emit<KeyT>, dim3(grid), dim3(kIndelThreads), 0, ctx->stream, t->V, t->list, t->n_list,
-                       t->pos_bits, t->obs, static_cast<KeyT *>(t->keys[0]), t->vals[0]);
+    if (filter)
+      hipLaunchKernelGGL((k_indel_emit<KeyT, true>), dim3(lgrid), dim3(kIndelThreads), 0, ctx->stream, t->V, t->list,
+                         t->n_list, t->pos_bits, t->map, t->off, t->obs, static_cast<KeyT *>(t->keys[0]), t->vals[0]);
+    else
+      hipLaunchKernelGGL((k_indel_emit<KeyT, false>), dim3(lgrid), dim3(kIndelThreads), 0, ctx->stream, t->V, t->list,
+                         t->n_list, t->pos_bits, t->map, t->off, t->obs, static_cast<KeyT *>(t->keys[0]), t->vals[0]);
     if ((rc = check_launch(ctx, "k_indel_emit"))) return rc;
   }
   {
@@ -427,13 +583,13 @@ int run_tally(ganon_ctx *ctx, ganon_indels *t) {
     KernelScope ks(ctx, "k_indel_classify");
     const KeyT *keys = static_cast<const KeyT *>(t->keys[t->sorted_sel]);
     hipLaunchKernelGGL(k_indel_runs<KeyT>, dim3((unsigned)((n + kRunChunk - 1) / kRunChunk)), dim3(256), 0,
-                       ctx->stream, keys, n, t->flags, t->run_list, t->run_count);
-    // runs <= n / 2 (the count stays on the device): one thread per possible run, the threads past
+                       ctx->stream, keys, t->n_dev(), t->flags, t->run_list, t->run_count);
+    // runs <= n / 2 (the counts stay on the device): one thread per possible run, the threads past
     // the count leave at once
     const unsigned grid = (unsigned)((n / 2 + 255) / 256);
     hipLaunchKernelGGL(k_indel_classify<KeyT>, dim3(grid), dim3(256), 0, ctx->stream, t->V, keys,
-                       t->vals[t->sorted_sel], n, t->pos_bits, t->obs, t->flags, t->rank, t->repk, t->run_list,
-                       t->run_count, t->counters);
+                       t->vals[t->sorted_sel], t->n_dev(), t->pos_bits, t->obs, t->flags, t->rank, t->repk,
+                       t->run_list, t->run_count, t->counters);
     if ((rc = check_launch(ctx, "k_indel_classify"))) return rc;
   }
   return GANON_OK;
@@ -459,30 +615,70 @@ GANON_API int ganon_indel_upload(ganon_ctx *ctx, const ganon_batch *b, const gan
     }
     nid[r] = k;
   }
+  // per read with an I/D op: the reference's running offsets at every kWalkOps-th op, and the I/D
+  // ops before it (process_indels arithmetic, variation_classifier.py:52-141)
+  struct Blk {
+    int32_t k0, pos0, irp0, nid0;
+  };
+  std::vector<int64_t> blk_of(b->n_reads, -1);
+  std::vector<Blk> blks;
+  for (int32_t r = 0; r < b->n_reads; ++r) {
+    if (!nid[r]) continue;
+    blk_of[r] = (int64_t)blks.size();
+    const uint32_t *c = b->cigar + b->cig_off[r];
+    int64_t pos = b->ref_start[r], irp = 0;
+    int32_t k_id = 0;
+    for (int32_t k = 0; k < b->n_cig[r]; ++k) {
+      if (k % kWalkOps == 0) blks.push_back(Blk{k, (int32_t)pos, (int32_t)irp, k_id});
+      const uint32_t op = c[k] & 0xF, len = c[k] >> 4;
+      if (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) pos += len;
+      if (op == 0 || op == 1 || op == 3 || op == 4 || op == 5 || op == 7 || op == 8) irp += len;
+      k_id += (op == 1 || op == 2);
+    }
+    if (pos > INT32_MAX || irp > INT32_MAX) return fail(ctx, GANON_E_ARG, "indel upload: read %d offsets over 2^31", r);
+  }
+  auto n_blk = [&](int32_t r) { return (b->n_cig[r] + kWalkOps - 1) / kWalkOps; };
+  auto blk_ids = [&](int32_t r, int i) {   // I/D ops in block i of read r
+    const Blk &x = blks[(size_t)(blk_of[r] + i)];
+    return (i + 1 < n_blk(r) ? blks[(size_t)(blk_of[r] + i + 1)].nid0 : nid[r]) - x.nid0;
+  };
   std::vector<IndelInc> list;
-  std::vector<int32_t> seg_off(1, 0);
+  std::vector<IndelRead> rdist;          // each read with an I/D op once (first incidence's contig)
+  std::vector<uint8_t> seen(b->n_reads, 0);
+  std::vector<int32_t> seg_first;        // first list entry of each segment, then the list size
   int64_t n_obs = 0;
   int32_t max_span = 0;
   for (int32_t s = 0; s < b->n_scopes; ++s) {
     max_span = std::max(max_span, b->scope_span_len[s]);
-    const uint32_t par = (uint32_t)((seg_off.size() - 1) & 1) << 31;
-    const int64_t before = n_obs;
+    const uint32_t par = (uint32_t)(seg_first.size() & 1) << 31;
+    const int64_t cbase = b->scope_ref_off[s] - b->scope_span_start[s];   // contig start, genome nibbles
+    const size_t before = list.size();
     for (int64_t i = b->scope_incid_off[s]; i < b->scope_incid_off[s + 1]; ++i) {
       const int32_t r = b->incid_read[i];
       if (!nid[r]) continue;
-      list.push_back(IndelInc{r, (uint32_t)s | par, n_obs});
+      for (int k = 0; k < n_blk(r); ++k) {
+        const int ids = blk_ids(r, k);
+        if (!ids) continue;
+        const Blk &x = blks[(size_t)(blk_of[r] + k)];
+        list.push_back(IndelInc{r, (uint32_t)s | par, x.k0, x.pos0, x.irp0, 0, n_obs + x.nid0, cbase});
+        if (!seen[r]) rdist.push_back(IndelRead{r, x.k0, x.pos0, 0, cbase});
+      }
+      seen[r] = 1;
       n_obs += nid[r];
     }
-    if (n_obs > before) seg_off.push_back((int32_t)std::min<int64_t>(n_obs, INT32_MAX));
+    if (list.size() > before) seg_first.push_back((int32_t)before);
   }
+  seg_first.push_back((int32_t)list.size());
   if (n_obs >= (int64_t)INT32_MAX) return fail(ctx, GANON_E_ARG, "indel upload: %lld observations (max 2^31-1)", (long long)n_obs);
   ganon_indels *t = new ganon_indels();
   t->V = V;
   t->n_obs = n_obs;
   t->n_list = (int64_t)list.size();
-  t->n_seg = (int32_t)seg_off.size() - 1;
+  t->n_rdist = (int64_t)rdist.size();
+  t->n_seg = (int32_t)seg_first.size() - 1;
   t->pos_bits = bits_for((int64_t)max_span);
   t->key_bits = t->pos_bits + bits_for(std::max<int64_t>((int64_t)b->n_scopes - 1, 1));
+  t->map_words = (2 * b->ref_bytes + 64) / 16 + 1;
   int rc = GANON_OK;
   auto bail = [&](int code) {
     ind_release(t);
@@ -492,8 +688,14 @@ GANON_API int ganon_indel_upload(ganon_ctx *ctx, const ganon_batch *b, const gan
   if (t->pos_bits > 31 || t->key_bits > 64) return bail(fail(ctx, GANON_E_ARG, "indel upload: sort key needs %d bits", t->key_bits));
   if (n_obs > 0) {
     if ((rc = ind_alloc(ctx, t, &t->list, list.size()))) return bail(rc);
+    if ((rc = ind_alloc(ctx, t, &t->rdist, rdist.size()))) return bail(rc);
+    if ((rc = ind_alloc(ctx, t, &t->map, (size_t)t->map_words))) return bail(rc);
+    if ((rc = ind_alloc(ctx, t, &t->cnt, list.size() + 1))) return bail(rc);
+    if ((rc = ind_alloc(ctx, t, &t->off, list.size() + 1))) return bail(rc);
+    if ((rc = ind_alloc(ctx, t, &t->seg_first, seg_first.size()))) return bail(rc);
+    if ((rc = ind_alloc(ctx, t, &t->seg_off, seg_first.size()))) return bail(rc);
+    if ((rc = ind_alloc(ctx, t, &t->nval, 1))) return bail(rc);
     if ((rc = ind_alloc(ctx, t, &t->obs, (size_t)n_obs))) return bail(rc);
-    if ((rc = ind_alloc(ctx, t, &t->seg_off, seg_off.size()))) return bail(rc);
     for (int h = 0; h < 2; ++h) {
       if ((rc = ind_alloc(ctx, t, reinterpret_cast<unsigned long long **>(&t->keys[h]), (size_t)n_obs))) return bail(rc);
       if ((rc = ind_alloc(ctx, t, &t->vals[h], (size_t)n_obs))) return bail(rc);
@@ -504,16 +706,23 @@ GANON_API int ganon_indel_upload(ganon_ctx *ctx, const ganon_batch *b, const gan
     if ((rc = ind_alloc(ctx, t, &t->counters, 2))) return bail(rc);
     if ((rc = ind_alloc(ctx, t, &t->run_list, (size_t)n_obs / 2 + 1))) return bail(rc);
     if ((rc = ind_alloc(ctx, t, &t->run_count, 1))) return bail(rc);
-    // temp storage: the larger of the two sort strategies
-    size_t seg_bytes = 0, glob_bytes = 0;
+    // temp storage: the largest of the two sorts and the count scan
+    size_t seg_bytes = 0, glob_bytes = 0, scan_bytes = 0;
     if (sort_pairs<uint32_t>(t, nullptr, seg_bytes, false, ctx->stream, nullptr) != hipSuccess ||
-        sort_pairs<unsigned long long>(t, nullptr, glob_bytes, true, ctx->stream, nullptr) != hipSuccess)
-      return bail(fail(ctx, GANON_E_DEVICE, "indel upload: radix sort sizing failed"));
-    t->temp_bytes = std::max(seg_bytes, glob_bytes);
+        sort_pairs<unsigned long long>(t, nullptr, glob_bytes, true, ctx->stream, nullptr) != hipSuccess ||
+        scan_counts(t, nullptr, scan_bytes, ctx->stream) != hipSuccess)
+      return bail(fail(ctx, GANON_E_DEVICE, "indel upload: radix sort / scan sizing failed"));
+    t->temp_bytes = std::max(std::max(seg_bytes, glob_bytes), scan_bytes);
     if ((rc = ind_alloc(ctx, t, reinterpret_cast<uint8_t **>(&t->temp), t->temp_bytes))) return bail(rc);
+    const int32_t nv = (int32_t)n_obs;
     hipError_t e = hipMemcpyAsync(t->list, list.data(), list.size() * sizeof(IndelInc), hipMemcpyHostToDevice, ctx->stream);
     if (e == hipSuccess)
-      e = hipMemcpyAsync(t->seg_off, seg_off.data(), seg_off.size() * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream);
+      e = hipMemcpyAsync(t->rdist, rdist.data(), rdist.size() * sizeof(IndelRead), hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(t->seg_first, seg_first.data(), seg_first.size() * sizeof(int32_t), hipMemcpyHostToDevice,
+                         ctx->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(t->nval, &nv, sizeof nv, hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(t->cnt + list.size(), 0, sizeof(int32_t), ctx->stream);   // scan tail
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     if (e != hipSuccess) return bail(fail(ctx, GANON_E_DEVICE, "indel upload copy failed: %s", hipGetErrorString(e)));
   }
@@ -526,6 +735,7 @@ GANON_API int ganon_indel_run(ganon_ctx *ctx, ganon_indels *t) {
   HIP_OR_FAIL(hipSetDevice(ctx->device));
   t->ran = true;
   t->n_records = -1;
+  t->n_candidates = -1;
   if (t->n_obs == 0) return GANON_OK;
   t->global = ctx->indel_sort != 0;
   return t->global ? run_tally<unsigned long long>(ctx, t) : run_tally<uint32_t>(ctx, t);
@@ -540,8 +750,11 @@ GANON_API int64_t ganon_indel_download(ganon_ctx *ctx, ganon_indels *t, ganon_in
     return 0;
   }
   unsigned long long total = 0;
+  int32_t cand = 0;
   hipError_t e = hipMemcpyAsync(&total, t->counters, sizeof total, hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(&cand, t->n_dev(), sizeof cand, hipMemcpyDeviceToHost, ctx->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  t->n_candidates = cand;
   if (e != hipSuccess) return fail(ctx, GANON_E_DEVICE, "indel download: %s", hipGetErrorString(e));
   t->n_records = (int64_t)total;
   if (!out || cap < (int64_t)total || total == 0) return (int64_t)total;
@@ -556,12 +769,12 @@ GANON_API int64_t ganon_indel_download(ganon_ctx *ctx, ganon_indels *t, ganon_in
   if (e != hipSuccess) return fail(ctx, GANON_E_DEVICE, "indel download: %s", hipGetErrorString(e));
   if (t->global)
     hipLaunchKernelGGL(k_indel_write<unsigned long long>, dim3(grid), dim3(256), 0, ctx->stream, t->V,
-                       static_cast<const unsigned long long *>(t->keys[t->sorted_sel]), t->vals[t->sorted_sel], n,
-                       t->pos_bits, t->obs, t->flags, t->rank, t->counters + 1, t->recs);
+                       static_cast<const unsigned long long *>(t->keys[t->sorted_sel]), t->vals[t->sorted_sel],
+                       t->n_dev(), t->pos_bits, t->obs, t->flags, t->rank, t->counters + 1, t->recs);
   else
     hipLaunchKernelGGL(k_indel_write<uint32_t>, dim3(grid), dim3(256), 0, ctx->stream, t->V,
-                       static_cast<const uint32_t *>(t->keys[t->sorted_sel]), t->vals[t->sorted_sel], n, t->pos_bits,
-                       t->obs, t->flags, t->rank, t->counters + 1, t->recs);
+                       static_cast<const uint32_t *>(t->keys[t->sorted_sel]), t->vals[t->sorted_sel], t->n_dev(),
+                       t->pos_bits, t->obs, t->flags, t->rank, t->counters + 1, t->recs);
   int rc = check_launch(ctx, "k_indel_write");
   if (rc) return rc;
   e = hipMemcpyAsync(out, t->recs, (size_t)total * sizeof(ganon_indel_rec), hipMemcpyDeviceToHost, ctx->stream);
@@ -570,12 +783,16 @@ GANON_API int64_t ganon_indel_download(ganon_ctx *ctx, ganon_indels *t, ganon_in
   return (int64_t)total;
 }
 
-GANON_API int ganon_indel_info(const ganon_indels *t, int64_t *info4) {
-  if (!t || !info4) return GANON_E_ARG;
-  info4[0] = t->n_obs;
-  info4[1] = t->n_list;
-  info4[2] = t->global ? t->key_bits : t->pos_bits;
-  info4[3] = t->n_records;
+GANON_API int ganon_indel_info(const ganon_indels *t, int64_t *info8) {
+  if (!t || !info8) return GANON_E_ARG;
+  info8[0] = t->n_obs;
+  info8[1] = t->n_list;
+  info8[2] = t->global ? t->key_bits : t->pos_bits;
+  info8[3] = t->n_records;
+  info8[4] = t->n_candidates;
+  info8[5] = t->n_rdist;
+  info8[6] = t->global ? 1 : 0;
+  info8[7] = 0;
   return GANON_OK;
 }
 

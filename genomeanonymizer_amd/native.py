@@ -494,9 +494,10 @@ class DeviceIndels:
         return indel_records_array(out)
 
     def info(self) -> dict:
-        a = np.zeros(4, np.int64)
+        a = np.zeros(8, np.int64)
         self.m._check(self.m._lib.ganon_indel_info(self.h, _ptr(a, _i64p)), "ganon_indel_info")
-        return dict(zip(("observations", "incidences", "key_bits", "records"), a.tolist()))
+        return dict(zip(("observations", "incidences", "key_bits", "records", "emitted", "reads", "global_sort"),
+                        a.tolist()))
 
     def free(self) -> None:
         if self.h:

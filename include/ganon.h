@@ -127,8 +127,9 @@ GANON_API int ganon_ctx_set_variant(ganon_ctx *ctx, int variant);
  * GANON_PARAM_FASTQ_SKIP (phase timing only, changes results): bit 0 leaves out the
  * formatter's source loads, bit 1 its stores; bits 3-6 stop after the descriptor scan / after the
  * dword map / leave out the interior pass / leave out the edge and constant bytes.
- * GANON_PARAM_INDEL_SORT: the indel tally sorts its observations per scope (0, default: segmented,
- * 32-bit position keys) or in one global sort of 64-bit scope|position keys (1). */
+ * GANON_PARAM_INDEL_SORT: the indel tally keeps only observations at positions where two or more
+ * reads have an I/D op and sorts them per scope (0, default: segmented, 32-bit position keys), or
+ * sorts every observation in one global sort of 64-bit scope|position keys (1). Same records. */
 enum { GANON_PARAM_GROUP_UNROLL = 1, GANON_PARAM_GROUP_SKIP = 2, GANON_PARAM_GROUP_TARGET = 3,
        GANON_PARAM_NT_COPY = 4, GANON_PARAM_REF2 = 5, GANON_PARAM_FASTQ_SKIP = 6, GANON_PARAM_FASTQ_KD = 7,
        GANON_PARAM_INDEL_SORT = 8 };
@@ -272,8 +273,10 @@ GANON_API int ganon_indel_run(ganon_ctx *ctx, ganon_indels *t);
 /* Synchronize and copy the records: returns their count; copies only when out != NULL and
  * cap >= count (call again with a larger buffer otherwise); negative GANON_E* on failure. */
 GANON_API int64_t ganon_indel_download(ganon_ctx *ctx, ganon_indels *t, ganon_indel_rec *out, int64_t cap);
-/* [observations, incidences with an I/D op, sort key bits, records (after download, else -1)] */
-GANON_API int ganon_indel_info(const ganon_indels *t, int64_t *info4);
+/* [observations, incidences with an I/D op, sort key bits, records (after download, else -1),
+ *  observations emitted by the last run (after download, else -1: the candidate filter keeps only
+ *  positions where two or more reads have an I/D op), reads with an I/D op, sort strategy, 0] */
+GANON_API int ganon_indel_info(const ganon_indels *t, int64_t *info8);
 GANON_API int ganon_indel_free(ganon_ctx *ctx, ganon_indels *t);
 
 #endif /* GANON_H */

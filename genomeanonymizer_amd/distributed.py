@@ -44,6 +44,22 @@ def contig_owner(plan: Plan, contigs: Sequence[str], world: int, policy: str = "
     return owner
 
 
+def _read_byte_index(tables, seq_base, ds: np.ndarray, row: np.ndarray) -> np.ndarray:
+    """Indices into the batch's sequence blob of every packed byte of the reads (ds, row), read
+    after read."""
+    T, N = tables
+    ds = np.asarray(ds, np.int64)
+    row = np.asarray(row, np.int64)
+    t0 = ds == 0
+    r0, r1 = np.where(t0, row, 0), np.where(t0, 0, row)
+    start = np.where(t0, seq_base[0] + T.seq_off[r0], seq_base[1] + N.seq_off[r1]).astype(np.int64)
+    n = (np.where(t0, T.l_seq[r0], N.l_seq[r1]).astype(np.int64) + 1) // 2
+    if len(n) == 0:
+        return np.zeros(0, np.int64)
+    first = np.concatenate([[0], np.cumsum(n)[:-1]])
+    return np.repeat(start - first, n) + np.arange(int(n.sum()), dtype=np.int64)
+
+
 def _edits_to_json(edits):
     return [[irp, c.pos, c.end, c.variant_type.value, c.length, c.allele, c.ref_allele] for irp, c in edits]
 
@@ -67,18 +83,14 @@ def anonymize_genome_sharded(windows: List[Window], tumor_bam: str, normal_bam: 
     mine = [sc.id for sc in plan.scopes if owner[sc.contig] == rank]
     res = anonymizer.anonymize(planner, plan, scope_ids=mine)
     mine_set = set(mine)
-    # this rank's written reads and their masked bytes
-    T, N = tables
-    recs = [(ds, row, s) for ds, row, s in plan.written_instances() if s in mine_set]
-    chunks = []
-    for ds, row, s in recs:
-        t = tables[ds]
-        o = res.seq_base[ds] + int(t.seq_off[row])
-        chunks.append(res.seq_out[o:o + (int(t.l_seq[row]) + 1) // 2])
+    # this rank's written reads and their masked bytes (column arrays, no per-record Python)
+    w_ds, w_row, w_sc = plan.written_arrays()
+    sel = (w_sc >= 0) & np.isin(w_sc, np.fromiter(mine_set, np.int64, len(mine_set)))
+    recs = np.stack([w_ds[sel], w_row[sel], w_sc[sel]], axis=1).astype(np.int64).reshape(-1, 3)
+    idx = _read_byte_index(tables, res.seq_base, recs[:, 0], recs[:, 1])
     os.makedirs(workdir, exist_ok=True)
     shard = os.path.join(workdir, f"shard{rank}")
-    np.savez(shard + ".npz", recs=np.array(recs, np.int64).reshape(-1, 3),
-             seq=np.concatenate(chunks) if chunks else np.zeros(0, np.uint8),
+    np.savez(shard + ".npz", recs=recs, seq=res.seq_out[idx],
              calls=res.scope_snv_calls, bases=res.scope_masked_bases, totals=res.totals)
     with open(shard + ".json", "w") as fh:
         json.dump({"indel_counts": {str(s): {vt.name: n for vt, n in c.items()}
@@ -113,14 +125,8 @@ def _merge_shards(plan: Plan, tables, res0: MaskResult, workdir: str, world: int
         z = np.load(os.path.join(workdir, f"shard{r}.npz"))
         calls += z["calls"]
         bases += z["bases"]
-        o = 0
-        seq = z["seq"]
-        for ds, row, s in z["recs"].tolist():
-            t = tables[ds]
-            n = (int(t.l_seq[row]) + 1) // 2
-            dst = res0.seq_base[ds] + int(t.seq_off[row])
-            seq_out[dst:dst + n] = seq[o:o + n]
-            o += n
+        zr = z["recs"]
+        seq_out[_read_byte_index(tables, res0.seq_base, zr[:, 0], zr[:, 1])] = z["seq"]
         with open(os.path.join(workdir, f"shard{r}.json")) as fh:
             j = json.load(fh)
         for s, c in j["indel_counts"].items():

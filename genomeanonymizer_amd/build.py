@@ -101,7 +101,7 @@ def build_oracle(force: bool = False) -> str:
     os.makedirs(os.path.dirname(ORACLE_LIB), exist_ok=True)
     if force or _stale(ORACLE_LIB, [src, hdr, __file__]):
         tmp = ORACLE_LIB + ".tmp"
-        _run(["gcc", "-O2", "-std=c11", "-fPIC", "-shared", "-o", tmp, src])
+        _run(["gcc", "-O2", "-std=c11", "-fPIC", "-shared", "-pthread", "-o", tmp, src])
         os.replace(tmp, ORACLE_LIB)
     return ORACLE_LIB
 

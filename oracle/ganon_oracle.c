@@ -23,6 +23,7 @@
  * Build: make -C oracle  (plain gcc, no dependencies).
  */
 #include <stdint.h>
+#include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -106,18 +107,14 @@ static int64_t collect_obs(const ganon_batch *b, int32_t s, int32_t r, obs_t *ou
   return n;
 }
 
-int oracle_mask_batch(const ganon_batch *b, uint8_t *seq_out, int32_t *scope_calls,
-                      int32_t *scope_bases, int64_t *totals) {
-  if (!b || !seq_out) return GANON_E_ARG;
-  memcpy(seq_out, b->seq_nt16, (size_t)b->seq_bytes);
-  int64_t tot[GANON_N_TOTALS];
-  memset(tot, 0, sizeof(tot));
-  tot[GANON_T_READS_IN] = b->n_reads;
-  tot[GANON_T_SCOPES] = b->n_scopes;
-  for (int32_t r = 0; r < b->n_reads; ++r) tot[GANON_T_READS_WRITTEN] += b->write_scope[r] >= 0;
+/* Scopes [s0, s1): classify and mask (seq_out already holds the input copy). A read is masked
+ * only by its write scope and every read starts on a byte boundary, so disjoint scope ranges
+ * write disjoint bytes (the multi-threaded baseline relies on it). */
+static int mask_scopes(const ganon_batch *b, int32_t s0, int32_t s1, uint8_t *seq_out, int32_t *scope_calls,
+                       int32_t *scope_bases, int64_t *tot) {
   int64_t cap = 0;
   obs_t *obs = NULL;
-  for (int32_t s = 0; s < b->n_scopes; ++s) {
+  for (int32_t s = s0; s < s1; ++s) {
     int64_t need = 0;
     for (int64_t i = b->scope_incid_off[s]; i < b->scope_incid_off[s + 1]; ++i)
       need += b->read_len[b->incid_read[i]];
@@ -167,6 +164,72 @@ int oracle_mask_batch(const ganon_batch *b, uint8_t *seq_out, int32_t *scope_cal
     tot[GANON_T_MASKED_BASES] += bases;
   }
   free(obs);
+  return GANON_OK;
+}
+
+static void static_totals(const ganon_batch *b, int64_t *tot) {
+  memset(tot, 0, sizeof(int64_t) * GANON_N_TOTALS);
+  tot[GANON_T_READS_IN] = b->n_reads;
+  tot[GANON_T_SCOPES] = b->n_scopes;
+  for (int32_t r = 0; r < b->n_reads; ++r) tot[GANON_T_READS_WRITTEN] += b->write_scope[r] >= 0;
+}
+
+int oracle_mask_batch(const ganon_batch *b, uint8_t *seq_out, int32_t *scope_calls,
+                      int32_t *scope_bases, int64_t *totals) {
+  if (!b || !seq_out) return GANON_E_ARG;
+  memcpy(seq_out, b->seq_nt16, (size_t)b->seq_bytes);
+  int64_t tot[GANON_N_TOTALS];
+  static_totals(b, tot);
+  const int rc = mask_scopes(b, 0, b->n_scopes, seq_out, scope_calls, scope_bases, tot);
+  if (rc) return rc;
+  if (totals) memcpy(totals, tot, sizeof(tot));
+  return GANON_OK;
+}
+
+typedef struct {
+  const ganon_batch *b;
+  int32_t s0, s1;
+  uint8_t *seq_out;
+  int32_t *calls, *bases;
+  int64_t tot[GANON_N_TOTALS];
+  int rc;
+} shard_t;
+
+static void *shard_main(void *arg) {
+  shard_t *w = (shard_t *)arg;
+  memset(w->tot, 0, sizeof(w->tot));
+  w->rc = mask_scopes(w->b, w->s0, w->s1, w->seq_out, w->calls, w->bases, w->tot);
+  return NULL;
+}
+
+/* The same results on `threads` POSIX threads, each over a contiguous range of scopes (SURVEY
+ * §8(d) "ref-cpu-N": the CPU path on all of a host's cores). */
+int oracle_mask_batch_mt(const ganon_batch *b, uint8_t *seq_out, int32_t *scope_calls, int32_t *scope_bases,
+                         int64_t *totals, int threads) {
+  if (!b || !seq_out || threads < 1) return GANON_E_ARG;
+  if (threads > 256) threads = 256;
+  memcpy(seq_out, b->seq_nt16, (size_t)b->seq_bytes);
+  int64_t tot[GANON_N_TOTALS];
+  static_totals(b, tot);
+  shard_t w[256];
+  pthread_t th[256];
+  for (int t = 0; t < threads; ++t) {
+    w[t].b = b;
+    w[t].s0 = (int32_t)((int64_t)b->n_scopes * t / threads);
+    w[t].s1 = (int32_t)((int64_t)b->n_scopes * (t + 1) / threads);
+    w[t].seq_out = seq_out;
+    w[t].calls = scope_calls;
+    w[t].bases = scope_bases;
+    if (pthread_create(&th[t], NULL, shard_main, &w[t]) != 0) return GANON_E_NOMEM;
+  }
+  int rc = GANON_OK;
+  for (int t = 0; t < threads; ++t) {
+    pthread_join(th[t], NULL);
+    if (w[t].rc) rc = w[t].rc;
+    tot[GANON_T_MASKED_SNV_CALLS] += w[t].tot[GANON_T_MASKED_SNV_CALLS];
+    tot[GANON_T_MASKED_BASES] += w[t].tot[GANON_T_MASKED_BASES];
+  }
+  if (rc) return rc;
   if (totals) memcpy(totals, tot, sizeof(tot));
   return GANON_OK;
 }

@@ -29,6 +29,8 @@ class OracleEngine:
         self._lib.oracle_mask_batch.argtypes = [C.POINTER(GanonBatch), C.POINTER(C.c_uint8),
                                                 C.POINTER(C.c_int32), C.POINTER(C.c_int32),
                                                 C.POINTER(C.c_int64)]
+        self._lib.oracle_mask_batch_mt.argtypes = self._lib.oracle_mask_batch.argtypes + [C.c_int]
+        self.threads = 1
 
     def format_fastq(self, recs: dict) -> bytes:
         """The FASTQ restatement (fastq_oracle.py) with HipMasker.format_fastq's contract."""
@@ -50,10 +52,10 @@ class OracleEngine:
         calls = np.zeros(b.n_scopes, np.int32)
         bases = np.zeros(b.n_scopes, np.int32)
         tot = np.zeros(N_TOTALS, np.int64)
-        rc = self._lib.oracle_mask_batch(C.byref(b), out.ctypes.data_as(C.POINTER(C.c_uint8)),
-                                         calls.ctypes.data_as(C.POINTER(C.c_int32)),
-                                         bases.ctypes.data_as(C.POINTER(C.c_int32)),
-                                         tot.ctypes.data_as(C.POINTER(C.c_int64)))
+        args = (C.byref(b), out.ctypes.data_as(C.POINTER(C.c_uint8)), calls.ctypes.data_as(C.POINTER(C.c_int32)),
+                bases.ctypes.data_as(C.POINTER(C.c_int32)), tot.ctypes.data_as(C.POINTER(C.c_int64)))
+        rc = (self._lib.oracle_mask_batch(*args) if self.threads == 1
+              else self._lib.oracle_mask_batch_mt(*args, int(self.threads)))
         if rc != 0:
             raise RuntimeError(f"oracle_mask_batch failed: {rc}")
         return out, calls, bases, tot

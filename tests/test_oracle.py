@@ -74,3 +74,19 @@ def test_oracle_known_answers():
     assert r0 == [A, C, G, T, A, C] and r1 == [C, G, T, A, C, G]
     r2 = unpack_nibbles(out[offs[2]:offs[2] + 3], 5).tolist()
     assert r2 == [A, C, G, G, A]
+
+
+def test_oracle_threads_give_the_same_results():
+    """The multi-threaded CPU baseline (bench.py cpu_baseline) computes what the one-thread oracle
+    does: scope shards write disjoint reads."""
+    import numpy as np
+    from pyoracle import OracleEngine
+    from genomeanonymizer_amd.synth.batch import config2_batch, random_batch
+    e = OracleEngine()
+    for arr in (random_batch(4, n_scopes=40), config2_batch(n_reads=100_000, genome=30_000_000, n_windows=10_000,
+                                                            n_germline=10_000)[0]):
+        e.threads = 1
+        a = e.mask(arr)
+        e.threads = 7
+        b = e.mask(arr)
+        assert all(np.array_equal(x, y) for x, y in zip(a, b))

@@ -917,7 +917,11 @@ GANON_API int ganon_fastq_run(ganon_ctx *ctx, ganon_fastq *f) {
   }
   {
     KernelScope ks(ctx, "k_fq_format");
-    auto kern = ctx->fq_kd == 1 ? k_fq_format<1> : ctx->fq_kd == 2 ? k_fq_format<2> : k_fq_format<4>;   // records per batch
+    // virtual dwords per lane per round: a tile holds ~2,100 of them (2,048 tile dwords plus the
+    // dwords neighbouring fields share), so the width sets the number of dependent load rounds
+    const int kd = ctx->fq_kd;
+    auto kern = kd == 1 ? k_fq_format<1> : kd == 2 ? k_fq_format<2> : kd == 3 ? k_fq_format<3>
+              : kd == 5 ? k_fq_format<5> : kd == 6 ? k_fq_format<6> : kd == 8 ? k_fq_format<8> : k_fq_format<4>;
     hipLaunchKernelGGL(kern, dim3((unsigned)f->n_tiles), dim3(kFqThreads), 0, ctx->stream, f->bufs, f->recs,
                        f->off, f->tile_first, f->n, f->total, f->out, f->err, ctx->fq_skip, f->dense_list,
                        f->dense_count);

@@ -1960,7 +1960,7 @@ GANON_API int ganon_ctx_set_param(ganon_ctx *ctx, int param, int value) {
     return GANON_OK;
   }
   if (param == GANON_PARAM_FASTQ_KD) {
-    if (value != 1 && value != 2 && value != 4) return fail(ctx, GANON_E_ARG, "FASTQ dwords per lane: 1, 2 or 4");
+    if (value < 1 || value > 8 || value == 7) return fail(ctx, GANON_E_ARG, "FASTQ dwords per lane: 1-6 or 8");
     ctx->fq_kd = value;
     return GANON_OK;
   }

@@ -16,7 +16,7 @@ masking path: a missing HIP library or device raises ``GanonError``.
 from __future__ import annotations
 
 import dataclasses
-from typing import Dict, List, Optional, Tuple
+from typing import Dict, Optional, Tuple
 
 import numpy as np
 

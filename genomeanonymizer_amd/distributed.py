@@ -16,7 +16,7 @@ from __future__ import annotations
 
 import json
 import os
-from typing import Dict, List, Sequence, Tuple
+from typing import Dict, List, Sequence
 
 import numpy as np
 
@@ -24,7 +24,7 @@ from .anonymizer_methods import CompleteGermlineAnonymizer, MaskResult
 from .indels import IndelCall
 from .io.bam import ReadTable
 from .io.fasta import FastaRef
-from .planner import Plan, SamplePlanner, Window, make_planner
+from .planner import Plan, Window, make_planner
 from .variants import VariantType
 from .writer import statistics_rows, write_fastqs, write_statistics
 

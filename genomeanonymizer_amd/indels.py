@@ -11,12 +11,12 @@ edits; ``mask_or_modify_indel`` (AM:178-203) edits the sequence and 
 from __future__ import annotations
 
 import dataclasses
-from typing import Dict, List, Tuple
+from typing import List, Tuple
 
 import numpy as np
 
 from .io.bam import ReadTable
-from .variants import SomaticVariationType, VariantType
+from .variants import VariantType
 
 NT16 = "=ACMGRSVTWYHKDBN"
 
@@ -33,14 +33,14 @@ def query_sequence(t: ReadTable, row: int) -> str:
 
 @dataclasses.dataclass
 class IndelCall:
+    """A masked TN indel call as CalledGenomicVariant holds it (variants.py:40-56): 0-based pos,
+    end (pos + 1 for INS, pos + length - 1 for DEL), type, length, read allele, reference allele."""
     pos: int
     end: int
     variant_type: VariantType
     length: int
     allele: str
     ref_allele: str
-    state: SomaticVariationType = SomaticVariationType.UNCLASSIFIED
-    support: Dict[Tuple[int, int], int] = dataclasses.field(default_factory=dict)
 
 
 def apply_leftovers(seq: bytearray, qual_fwd: List[int], edits: List[Tuple[int, IndelCall]]):

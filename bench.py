@@ -10,7 +10,7 @@ pass-through copies, exactly what ``ganon_mask_batch`` does minus the PCIe copie
 batch has an I/D op, as in the config-2 synthetic reads).
 Multi-GPU (torchrun): every rank owns its own config-2 shard (per-contig sharding makes
 shards independent; weak scaling) and the only collective is the int64 totals all-reduce
-over RCCL at the end of each step.
+over RCCL of each step, overlapped with the next step's kernels (double-buffered).
 
 Prints one JSON line (rank 0). ``roofline`` is for the dominant kernel: the algorithmic
 bytes it processes per launch (SURVEY §8(d) figures, attributed per kernel)
@@ -284,11 +284,17 @@ def main() -> None:
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
-    torch.cuda.set_device(local)
+    dev = local % max(1, torch.cuda.device_count())   # == local on a node with a GPU per rank
+    torch.cuda.set_device(dev)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # GANON_BENCH_BACKEND=gloo: rehearsal of the N > 1 path on one GPU (host-side reductions)
+        backend = os.environ.get("GANON_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
 
     from genomeanonymizer_amd import native
     from genomeanonymizer_amd.synth.batch import algorithmic_bytes
@@ -296,7 +302,7 @@ def main() -> None:
     t_gen = time.perf_counter()
     arr, info = make_batch(args, rank)
     t_gen = time.perf_counter() - t_gen
-    masker = native.HipMasker(local)
+    masker = native.HipMasker(dev)
     masker.set_variant(args.variant)
     masker.set_param(native.PARAM_GROUP_UNROLL, args.unroll)
     masker.set_param(native.PARAM_INDEL_SORT, args.indel_sort)
@@ -306,29 +312,47 @@ def main() -> None:
     db = masker.upload(arr)
     ind = db.indel_tally(arr)      # germline indel tally, part of every step
     t_up = time.perf_counter() - t_up
-    tot_t = torch.zeros(8, dtype=torch.int64, device="cuda")
+    # totals all-reduce (RCCL) of every step, double-buffered: the reduction of step i runs beside
+    # step i + 1's kernels; a buffer is reused only after its previous reduction completed
+    tots = [torch.zeros(8, dtype=torch.int64, device="cuda") for _ in range(2)]
+    works = [None, None]
+    host_reduce = dist is not None and dist.get_backend() != "nccl"
 
-    def step():
+    def step(i: int):
         db.run()
         ind.run()
         if dist is not None:
-            db.copy_totals_to(tot_t.data_ptr())
-            dist.all_reduce(tot_t)
+            if host_reduce:
+                dist.all_reduce(torch.from_numpy(db.totals()))
+                return
+            b = i & 1
+            if works[b] is not None:
+                works[b].wait()
+            db.copy_totals_to(tots[b].data_ptr())
+            works[b] = dist.all_reduce(tots[b], async_op=True)
 
-    for _ in range(args.warmup):
-        step()
+    def drain():
+        for b in range(2):
+            if works[b] is not None:
+                works[b].wait()
+                works[b] = None
+
+    for i in range(args.warmup):
+        step(i)
+    drain()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    for i in range(args.steps):
+        step(i)
+    drain()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     dt = time.perf_counter() - t0
-    dt_t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+    dt_t = torch.tensor([dt], dtype=torch.float64, device="cpu" if host_reduce else "cuda")
     if dist is not None:
         dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
     dt = float(dt_t.item())
@@ -370,11 +394,15 @@ def main() -> None:
     irecs = ind.download()
     indel_info = ind.info()
     ind.free()
-    if dist is not None:
-        db.copy_totals_to(tot_t.data_ptr())
-        dist.all_reduce(tot_t)
+    if dist is not None and host_reduce:
+        t_host = torch.from_numpy(totals.copy())
+        dist.all_reduce(t_host)
+        job_totals = t_host.numpy()
+    elif dist is not None:
+        db.copy_totals_to(tots[0].data_ptr())
+        dist.all_reduce(tots[0])
         torch.cuda.synchronize()
-        job_totals = tot_t.cpu().numpy()
+        job_totals = tots[0].cpu().numpy()
     else:
         job_totals = totals
     db.free()

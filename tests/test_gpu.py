@@ -281,3 +281,51 @@ def test_hip_fastq_full_size_matches_host_formatter(masker, c2_full):
     want = native.host_format_fastq(recs)
     assert len(got) == native.fastq_bytes(recs) == len(want)
     assert got == want
+
+
+@pytest.mark.parametrize("seed", [11, 12, 13])
+def test_hip_pipeline_matches_oracle_pipeline_on_random_scenarios(seed, tmp_path, hip_built):
+    """Differential end-to-end check beyond the three golden scenarios: randomized samples with
+    germline SNPs and indels, soft clips, N bases, unmapped / unplaced mates, cross-contig pairs and
+    coverage holes, through the product (native planner, HIP masking + indel tally + HIP FASTQ) and
+    through the oracle-backed pipeline (C oracle, indel restatement, FASTQ restatement, pinned by the
+    reference's files in tests/test_oracle.py): every output file byte-identical."""
+    import os
+    from pyoracle import OracleEngine
+    from genomeanonymizer_amd import short_read_tumor_normal_anonymizer as sr
+    from genomeanonymizer_amd.anonymizer_methods import CompleteGermlineAnonymizer
+    from genomeanonymizer_amd.synth.generate import ContigSpec, ScenarioConfig, generate
+    rng = np.random.default_rng(seed)
+    contigs = []
+    for c in range(3):
+        L = int(rng.integers(10_000, 40_000))
+        wins, x = [], 1001 + int(rng.integers(0, 2000))
+        while x < L - 1500 and len(wins) < 6:
+            wins.append(x)
+            x += 2003 + int(rng.integers(0, 6000))
+        contigs.append(ContigSpec(f"chr{c}", L, int(rng.integers(100, 800)), windows=wins,
+                                  keep_windows=int(rng.integers(0, 2)),
+                                  holes=[("T" if rng.random() < 0.5 else "N", 3000, 3600)]))
+    cfg = ScenarioConfig(name=f"d{seed}", seed=seed, contigs=contigs, germline_snp_per_kb=5.0,
+                         germline_indel_per_kb=1.0, hom_fraction=0.3, softclip_frac=0.05,
+                         unmapped_mate_frac=0.03, n_base_frac=0.03, unplaced_frac=0.4, cross_contig_pairs=8)
+    paths = generate(cfg, str(tmp_path / "in"))
+    outs = {}
+    for tag, anon in (("hip", CompleteGermlineAnonymizer(device=0)),
+                      ("oracle", CompleteGermlineAnonymizer(engine=OracleEngine()))):
+        d = tmp_path / tag
+        d.mkdir()
+        t_out, n_out = str(d / "tumor"), str(d / "normal")
+        sr.run_short_read_tumor_normal_anonymizer([paths["vcf"]], [(paths["T"], paths["N"])], paths["ref"], anon,
+                                                  [(t_out, n_out)], True, 4)
+        files = {}
+        for pre in (t_out, n_out):
+            for suf in (".1.fastq", ".2.fastq", ".single_end.fastq"):
+                if os.path.exists(pre + suf):
+                    files[os.path.basename(pre) + suf] = open(pre + suf, "rb").read()
+        files["stats"] = open(paths["N"] + ".statistics.txt").read()
+        outs[tag] = files
+    assert outs["hip"].keys() == outs["oracle"].keys()
+    for k in outs["hip"]:
+        assert outs["hip"][k] == outs["oracle"][k], k
+    assert len(outs["hip"]["tumor.1.fastq"]) > 10_000

@@ -1053,6 +1053,15 @@ __device__ __forceinline__ unsigned int ld_l2(const unsigned int *p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// threadIdx.x the compiler cannot hoist out of a loop: address arithmetic of the rare overflow
+// paths is then recomputed where it is used instead of being kept live (spilled to scratch)
+// across the whole kernel.
+__device__ __forceinline__ int opaque_tid() {
+  int t = (int)threadIdx.x;
+  asm volatile("" : "+v"(t));
+  return t;
+}
+
 __device__ __forceinline__ unsigned gtab_home(unsigned long long key, int tsize) {
   const unsigned long long h = key * 0x9E3779B97F4A7C15ull;
   return (unsigned)(((h >> 32) * (unsigned long long)tsize) >> 32);
@@ -1296,7 +1305,7 @@ __device__ __forceinline__ void grp_classify(const GrpBatch &B, GrpShared &sh, i
 // (minus the kept variant), and mask the observations of reads the scopes write.
 __device__ __forceinline__ void grp_global(const GrpBatch &B, GrpShared &sh, const GrpGlobal &gg, int n,
                                            int s_begin, const PatchSink &sink) {
-  const int tid = threadIdx.x;
+  const int tid = opaque_tid();
   const int tsize = max(2 * n, 64);
   unsigned long long *tk = gg.aux->tkey + 2 * gg.off;
   unsigned int *tf = gg.aux->tflag + 2 * gg.off;
@@ -1479,7 +1488,7 @@ __global__ void __launch_bounds__(kGrpThreads, (U == 1 ? 6 : U == 2 ? GANON_K2_B
     if (top < 0) {
       // per-scope counts (wide scopes in the id range belong to the tile path) and the
       // workgroup's partial totals (k_finish sums them)
-      for (int i = tid; i < ((skip & kSkipCounts) ? 0 : s_end - s_begin); i += kGrpThreads) {
+      for (int i = opaque_tid(); i < ((skip & kSkipCounts) ? 0 : s_end - s_begin); i += kGrpThreads) {
         if (B.span_len[s_begin + i] > kGrpMaxSpan) continue;
         aux->scope_calls[s_begin + i] = sh.cnt_calls[i];
         aux->scope_bases[s_begin + i] = sh.cnt_bases[i];
@@ -1511,7 +1520,7 @@ __global__ void __launch_bounds__(kGrpThreads, (U == 1 ? 6 : U == 2 ? GANON_K2_B
     if (n > kGrpObs) {
       if (n <= gg.cap) {
         // the list joins the region's tail: n observations contiguous in the region
-        for (int i = tid; i < kGrpObs; i += kGrpThreads) {
+        for (int i = opaque_tid(); i < kGrpObs; i += kGrpThreads) {
           aux->okey[gg.off + (n - kGrpObs) + i] = sh.key[i];
           aux->opay[gg.off + (n - kGrpObs) + i] = sh.pay[i];
         }
@@ -1525,7 +1534,7 @@ __global__ void __launch_bounds__(kGrpThreads, (U == 1 ? 6 : U == 2 ? GANON_K2_B
       // never fills a region (capacity > 3 x the group's reads)
       __builtin_amdgcn_s_waitcnt(0);
       __syncthreads();
-      for (int i = tid; i < gg.cap; i += kGrpThreads) {
+      for (int i = opaque_tid(); i < gg.cap; i += kGrpThreads) {
         const unsigned long long k = i < kGrpObs ? sh.key[i] : ld_l2(aux->okey + gg.off + (i - kGrpObs));
         atomicMin(&sh.kmin, k);
         atomicMax(&sh.kmax, k);

@@ -947,6 +947,9 @@ constexpr int kGrpThreads = 256;
 #ifndef GANON_K2_BLOCKS
 #define GANON_K2_BLOCKS 6   // resident workgroups per CU the K = 2 instance is compiled for
 #endif
+#ifndef GANON_TILE_COPY
+#define GANON_TILE_COPY 0   // 1: fused partition copied tile by tile during the scan (CopyCursor)
+#endif
 constexpr int kGrpTile = 256;        // segment records staged per tile
 constexpr int kGrpTarget = 256;      // segments per group (a larger scope forms its own group)
 constexpr int kGrpObs = 512;         // observations per LDS list
@@ -958,6 +961,7 @@ constexpr int kGrpQuad = 256;        // lists up to this size are matched withou
 constexpr int kGrpMaxSpan = 1 << 20; // widest scope of the group kernels (20-bit position field)
 constexpr unsigned long long kEmpty = ~0ull;
 constexpr int64_t kPartAlign = 128;  // partition boundaries fall on whole lines
+constexpr int kGrpRec = 5;           // int4 records per group (layout at k_group)
 // segment record (int4, 16 bytes): x = query nibble bits 0-31, y = reference nibble bits 0-31,
 // z = query nibble bits 32-39 | reference nibble bits 32-39 << 8 | length << 16 (14 bits) |
 // dataset << 30 | mine << 31, w = scope_local | (pos - span_start) << 12
@@ -968,6 +972,9 @@ constexpr unsigned long long kNibMask = (1ull << 48) - 1;
 enum { kModeCollect = 0 };
 // GANON_PARAM_GROUP_SKIP (profiling only, results invalid): phases left out
 enum { kSkipClassify = 1, kSkipChunks = 2, kSkipCopy = 4, kSkipCounts = 8 };
+// GANON_PARAM_GROUP_SKIP bit 4 (A/B, same results): copy the whole partition before the scan
+// instead of tile by tile
+enum { kCopyFirst = 16 };
 static_assert(kGrpTile == kGrpThreads && kGrpTile <= 256, "one staged record per thread, 8-bit map");
 
 // The few batch arrays the group kernels read (a slim kernel argument keeps SGPRs free).
@@ -988,6 +995,7 @@ struct GrpShared {
   unsigned long long stk_lo[kGrpStack], stk_hi[kGrpStack];
   int stk_mode[kGrpStack];
   unsigned long long kmin, kmax;
+  unsigned long long cut[2];        // fused: end of the written reads staged so far, per piece
   int top, n_obs, n_patch;
   int blk_calls, blk_bases;         // this workgroup's contribution to the totals
   int cnt_calls[kGrpMaxScopes];     // per-scope counts, written out once at the end
@@ -1013,17 +1021,18 @@ struct GrpAux {
 
 struct PatchSink {
   uint8_t *out;
-  int64_t p0, p1;                   // fused: this workgroup's partition of out (bytes)
+  int64_t p0, p1, q0, q1;           // fused: this workgroup's partition pieces of out (bytes)
   const GrpAux *aux;                // far-mask list
   bool fused;
   bool lds;                         // fused: in-partition masks into the LDS list
+  __device__ bool inside(int64_t byte) const { return (byte >= p0 && byte < p1) || (byte >= q0 && byte < q1); }
 };
 
 __device__ __forceinline__ void sink_patch(GrpShared &sh, const PatchSink &k, int64_t nib, int c, int rc) {
   const unsigned long long e = ((unsigned long long)nib << 4) | (unsigned long long)(c ^ rc);
   if (k.fused) {
     const int64_t byte = nib >> 1;
-    if (byte < k.p0 || byte >= k.p1) {
+    if (!k.inside(byte)) {
       const int i = atomicAdd(k.aux->far_count, 1);
       if (i < k.aux->far_cap) k.aux->far[i] = e;
       return;
@@ -1094,10 +1103,49 @@ __device__ __forceinline__ bool grp_kept(const GrpBatch &B, int s, int64_t pos_o
   return kp >= 0 && B.keep_code[s] == c && (int64_t)kp - B.span_start[s] == pos_off;
 }
 
+// Fused partition copy, tile by tile: the pieces [beg, end) are copied up to the last byte of
+// the written reads staged so far (cur: next byte to copy), so that the scan's chunk loads that
+// follow find those lines in L2. Copying a whole ~40 KB partition first loses every line before
+// the scan reaches it (a group lives ~35 us while its XCD streams ~27 MB through a 4 MB L2).
+struct CopyCursor {
+  int64_t beg[2], cur[2], end[2];
+  uint8_t *out;
+  int nt;
+};
+
+// A workgroup-uniform 64-bit value (read from LDS) in scalar registers.
+__device__ __forceinline__ unsigned long long uniform64(unsigned long long v) {
+  return (unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)v) |
+         ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(v >> 32)) << 32);
+}
+
+// Bytes [p0, p1) of src to dst in 16-byte windows (p0 16-byte aligned; a window may end past p1
+// only at the end of the buffer, which is padded), 8 windows in flight per thread.
+__device__ __forceinline__ void copy_windows(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, int64_t p0,
+                                             int64_t p1, int nt) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  constexpr int kCopyUnroll = 8;
+  for (int64_t D0 = p0 + 16 * (int)threadIdx.x; D0 < p1; D0 += 16 * kGrpThreads * kCopyUnroll) {
+    u32x4 v[kCopyUnroll];
+#pragma unroll
+    for (int k = 0; k < kCopyUnroll; ++k) {
+      const int64_t D = D0 + 16 * kGrpThreads * k;
+      if (D < p1) v[k] = *reinterpret_cast<const u32x4 *>(src + D);
+    }
+#pragma unroll
+    for (int k = 0; k < kCopyUnroll; ++k) {
+      const int64_t D = D0 + 16 * kGrpThreads * k;
+      if (D >= p1) break;
+      if (nt) __builtin_nontemporal_store(v[k], reinterpret_cast<u32x4 *>(dst + D));
+      else *reinterpret_cast<u32x4 *>(dst + D) = v[k];
+    }
+  }
+}
+
 // Stage records [c0, c0 + nh) in LDS with the exclusive prefix of their chunk counts;
-// returns the tile's chunk total.
+// returns the tile's chunk total. docopy: raise the pieces' copy cuts to the staged written reads.
 __device__ __forceinline__ int grp_tile(GrpShared &sh, const int4 *__restrict__ rec4, int64_t c0, int nh,
-                                        int chunk) {
+                                        int chunk, const CopyCursor &cc, bool docopy) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t ix = c0 + (tid < nh ? tid : nh - 1);
   const int4 r = rec4[ix];
@@ -1125,6 +1173,14 @@ __device__ __forceinline__ int grp_tile(GrpShared &sh, const int4 *__restrict__ 
   sh.pre[tid] = pre;
   if (total <= kGrpMap)
     for (int k = 0; k < nck; ++k) sh.cmap[pre + k] = (uint8_t)tid;
+  if (docopy && tid < nh && ((uint32_t)r.z >> 31)) {
+    const uint32_t rz = (uint32_t)r.z;
+    const int64_t sn = (int64_t)((uint64_t)(uint32_t)r.x | ((uint64_t)(rz & 0xFF) << 32));
+    const int64_t b0 = sn >> 1, e = (sn + ((rz >> 16) & kSegMaxLen) + 1) >> 1;
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      if (b0 >= cc.beg[k] && b0 < cc.end[k]) atomicMax(&sh.cut[k], (unsigned long long)e);
+  }
   __syncthreads();
   return total;
 }
@@ -1147,11 +1203,23 @@ __device__ __forceinline__ int grp_find(const GrpShared &sh, int nh, int total, 
 // windows out of registers with static indices.
 template <int K, bool REF2>
 __device__ __forceinline__ void grp_scan(const GrpBatch &B, GrpShared &sh, const GrpRange &R, const GrpGlobal &gg,
-                                         int64_t i_begin, int64_t i_end, const int4 *__restrict__ rec4, int skip) {
+                                         int64_t i_begin, int64_t i_end, const int4 *__restrict__ rec4, int skip,
+                                         CopyCursor &cc, bool docopy) {
   const int tid = threadIdx.x;
   for (int64_t c0 = i_begin; c0 < i_end; c0 += kGrpTile) {
     const int nh = (int)((i_end - c0) < kGrpTile ? (i_end - c0) : kGrpTile);
-    int total = grp_tile(sh, rec4, c0, nh, 16 * K);
+    int total = grp_tile(sh, rec4, c0, nh, 16 * K, cc, docopy);
+    if (docopy) {
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int64_t c = (int64_t)((uniform64(sh.cut[k]) + 15) & ~15ull);
+        const int64_t cut = c < cc.end[k] ? c : cc.end[k];
+        if (cut > cc.cur[k]) {
+          copy_windows(B.seq, cc.out, cc.cur[k], cut, cc.nt);
+          cc.cur[k] = cut;
+        }
+      }
+    }
     if (skip & kSkipChunks) total = 0;
     for (int t = tid; t < total; t += kGrpThreads) {
       const int j = grp_find(sh, nh, total, t);
@@ -1363,8 +1431,10 @@ __device__ __forceinline__ void grp_global(const GrpBatch &B, GrpShared &sh, con
     grp_count(sh, (int)(key >> 52), 0, 1);
     const int64_t nib = (int64_t)(pay & kNibMask);
     const int rc = (int)((pay >> 48) & 15);
-    if (!sink.fused || (nib >> 1) < sink.p0 || (nib >> 1) >= sink.p1) {
-      sink_patch(sh, PatchSink{sink.out, sink.p0, sink.p1, sink.aux, sink.fused, false}, nib, c, rc);
+    if (!sink.fused || !sink.inside(nib >> 1)) {
+      PatchSink direct = sink;
+      direct.lds = false;
+      sink_patch(sh, direct, nib, c, rc);
       continue;
     }
     okey[i] = ((unsigned long long)nib << 4) | (unsigned long long)(c ^ rc);   // in-partition mask
@@ -1428,10 +1498,10 @@ __device__ __forceinline__ void grp_patch_bytes(const GrpBatch &B, GrpShared &sh
   }
 }
 
-// groups: 4 x int4 per group, in launch order: {s_begin, s_end, seg_begin lo, hi},
-// {seg_end lo, hi, seg_mid lo, hi}, {partition begin lo, hi, end lo, hi} (bytes; fused only),
-// {global region offset lo, hi, capacity, 0}; segments [seg_begin, seg_mid) have an all-ACGT
-// reference range (2-bit reference).
+// groups: kGrpRec x int4 per group, in launch order: {s_begin, s_end, seg_begin lo, hi},
+// {seg_end lo, hi, seg_mid lo, hi}, {partition piece A begin lo, hi, end lo, hi} (bytes; fused
+// only), {global region offset lo, hi, capacity, 0}, {piece B begin lo, hi, end lo, hi};
+// segments [seg_begin, seg_mid) have an all-ACGT reference range (2-bit reference).
 template <int U, bool FUSED>
 __global__ void __launch_bounds__(kGrpThreads, (U == 1 ? 6 : U == 2 ? GANON_K2_BLOCKS : U == 4 ? 5 : 4)) k_group(const GrpBatch B, const int4 *__restrict__ groups,
                                                        const int4 *__restrict__ rec4,
@@ -1439,37 +1509,31 @@ __global__ void __launch_bounds__(kGrpThreads, (U == 1 ? 6 : U == 2 ? GANON_K2_B
                                                        int skip, int nt_copy) {
   __shared__ GrpShared sh;
   const int tid = threadIdx.x;
-  const int4 g0 = groups[4 * blockIdx.x];
-  const int4 g1 = groups[4 * blockIdx.x + 1];
-  const int4 g2 = groups[4 * blockIdx.x + 2];
-  const int4 g3 = groups[4 * blockIdx.x + 3];
+  const int4 g0 = groups[kGrpRec * blockIdx.x];
+  const int4 g1 = groups[kGrpRec * blockIdx.x + 1];
+  const int4 g2 = groups[kGrpRec * blockIdx.x + 2];
+  const int4 g3 = groups[kGrpRec * blockIdx.x + 3];
+  const int4 g4 = groups[kGrpRec * blockIdx.x + 4];
   const GrpGlobal gg{aux, i64_of(g3.x, g3.y), g3.z};
   const int s_begin = g0.x, s_end = g0.y;
   const int64_t i_begin = i64_of(g0.z, g0.w), i_end = i64_of(g1.x, g1.y), i_mid = i64_of(g1.z, g1.w);
-  const PatchSink sink{out, i64_of(g2.x, g2.y), i64_of(g2.z, g2.w), aux, FUSED, FUSED};
-  if (FUSED && !(skip & kSkipCopy)) {
-    // the partition: whole 16-byte windows (the buffers are padded past seq_bytes); the stores
-    // drain while the scan runs (s_waitcnt before the mask stores)
-    // 8 windows in flight per thread: all loads issue before the first store waits on them
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    constexpr int kCopyUnroll = 8;
-    for (int64_t D0 = sink.p0 + 16 * tid; D0 < sink.p1; D0 += 16 * kGrpThreads * kCopyUnroll) {
-      u32x4 v[kCopyUnroll];
+  const PatchSink sink{out, i64_of(g2.x, g2.y), i64_of(g2.z, g2.w), i64_of(g4.x, g4.y), i64_of(g4.z, g4.w),
+                       aux, FUSED, FUSED};
+  // the partition pieces, whole 16-byte windows (the buffers are padded past seq_bytes), copied
+  // tile by tile during the first scan pass (CopyCursor); the stores drain while the scan runs
+  // (s_waitcnt before the mask stores)
+  const bool copy = FUSED && !(skip & kSkipCopy);
+  CopyCursor cc{{sink.p0, sink.q0}, {sink.p0, sink.q0}, {sink.p1, sink.q1}, out, nt_copy};
+  if (copy && (!GANON_TILE_COPY || (skip & kCopyFirst))) {
 #pragma unroll
-      for (int k = 0; k < kCopyUnroll; ++k) {
-        const int64_t D = D0 + 16 * kGrpThreads * k;
-        if (D < sink.p1) v[k] = *reinterpret_cast<const u32x4 *>(B.seq + D);
-      }
-#pragma unroll
-      for (int k = 0; k < kCopyUnroll; ++k) {
-        const int64_t D = D0 + 16 * kGrpThreads * k;
-        if (D >= sink.p1) break;
-        if (nt_copy) __builtin_nontemporal_store(v[k], reinterpret_cast<u32x4 *>(out + D));
-        else *reinterpret_cast<u32x4 *>(out + D) = v[k];
-      }
-    }
+    for (int k = 0; k < 2; ++k) copy_windows(B.seq, out, cc.beg[k], cc.end[k], nt_copy);
+    cc.cur[0] = sink.p1;
+    cc.cur[1] = sink.q1;
   }
+  bool first_pass = true;
   if (tid == 0) {
+    sh.cut[0] = (unsigned long long)sink.p0;
+    sh.cut[1] = (unsigned long long)sink.q0;
     sh.top = 0;
     sh.stk_lo[0] = 0ull;
     sh.stk_hi[0] = ~0ull;
@@ -1508,12 +1572,19 @@ __global__ void __launch_bounds__(kGrpThreads, (U == 1 ? 6 : U == 2 ? GANON_K2_B
       sh.kmax = 0ull;
     }
     __syncthreads();
+    const bool pc = GANON_TILE_COPY && copy && first_pass;
     if (B.ref2) {
-      grp_scan<U, true>(B, sh, R, gg, i_begin, i_mid, rec4, skip);
-      grp_scan<U, false>(B, sh, R, gg, i_mid, i_end, rec4, skip);
+      grp_scan<U, true>(B, sh, R, gg, i_begin, i_mid, rec4, skip, cc, pc);
+      grp_scan<U, false>(B, sh, R, gg, i_mid, i_end, rec4, skip, cc, pc);
     } else {
-      grp_scan<U, false>(B, sh, R, gg, i_begin, i_end, rec4, skip);
+      grp_scan<U, false>(B, sh, R, gg, i_begin, i_end, rec4, skip, cc, pc);
     }
+    if (pc) {   // the rest of the pieces (bytes past the last written read's segments)
+#pragma unroll
+      for (int k = 0; k < 2; ++k)
+        if (cc.cur[k] < cc.end[k]) copy_windows(B.seq, out, cc.cur[k], cc.end[k], nt_copy);
+    }
+    first_pass = false;
     // (grp_scan ends on a barrier)
     if (skip & kSkipClassify) continue;
     const int n = sh.n_obs;
@@ -1978,7 +2049,7 @@ GANON_API int ganon_ctx_set_param(ganon_ctx *ctx, int param, int value) {
     return GANON_OK;
   }
   if (param == GANON_PARAM_GROUP_SKIP) {
-    ctx->group_skip = value & (kSkipClassify | kSkipChunks | kSkipCopy | kSkipCounts);
+    ctx->group_skip = value & (kSkipClassify | kSkipChunks | kSkipCopy | kSkipCounts | kCopyFirst);
     return GANON_OK;
   }
   return fail(ctx, GANON_E_ARG, "unknown parameter %d", param);
@@ -2333,41 +2404,105 @@ GANON_API int ganon_batch_upload(ganon_ctx *ctx, const ganon_batch *b, ganon_dba
     }
     close_group(b->n_scopes);
     const int32_t ng = (int32_t)gs.size();
+    // partition pieces: the sequence buffer in byte order is a sequence of runs of written reads
+    // owned by one group (a group's written reads are contiguous per dataset when each dataset's
+    // reads are stored in position order — the product layout is every tumor read, then every
+    // normal read, so a group has one run per dataset). Each group keeps its two largest runs as
+    // pieces; any other run (a read at a group boundary) joins the piece before it. The pieces
+    // tile [0, seq_bytes) at 128-byte boundaries; bytes of a read outside its group's pieces
+    // are masked through the far list.
+    std::vector<int32_t> scope_grp((size_t)b->n_scopes, -1);
+    for (int32_t k = 0; k < ng; ++k)
+      for (int32_t s = gs[k].s0; s < gs[k].s1; ++s)
+        if (b->scope_span_len[s] <= kGrpMaxSpan) scope_grp[s] = k;
+    auto owner_of = [&](int32_t r) -> int32_t {
+      const int32_t ws = b->write_scope[r];
+      return (ws < 0 || b->read_len[r] == 0) ? -1 : scope_grp[ws];
+    };
+    std::vector<int32_t> byoff;
+    byoff.reserve((size_t)b->n_reads);
+    bool sorted = true;
+    for (int32_t r = 0; r < b->n_reads; ++r) {
+      if (owner_of(r) < 0) continue;
+      if (!byoff.empty() && b->seq_off[r] < b->seq_off[byoff.back()]) sorted = false;
+      byoff.push_back(r);
+    }
+    if (!sorted)
+      std::stable_sort(byoff.begin(), byoff.end(), [&](int32_t x, int32_t y) { return b->seq_off[x] < b->seq_off[y]; });
+    struct Run {
+      int64_t start;
+      int32_t owner;
+    };
+    std::vector<Run> runs;
+    for (int32_t r : byoff) {
+      const int32_t g = owner_of(r);
+      if (runs.empty() || runs.back().owner != g) runs.push_back(Run{b->seq_off[r], g});
+    }
+    // each group's two largest runs (bytes up to the next run)
+    auto run_len = [&](int64_t i) {
+      return ((size_t)i + 1 < runs.size() ? runs[(size_t)i + 1].start : b->seq_bytes) - runs[(size_t)i].start;
+    };
+    std::vector<int64_t> best((size_t)ng * 2, -1);
+    for (int64_t i = 0; i < (int64_t)runs.size(); ++i) {
+      int64_t *bb = &best[2 * (size_t)runs[(size_t)i].owner];
+      const int64_t len = run_len(i);
+      if (bb[0] < 0 || len > run_len(bb[0])) {
+        bb[1] = bb[0];
+        bb[0] = i;
+      } else if (bb[1] < 0 || len > run_len(bb[1])) {
+        bb[1] = i;
+      }
+    }
+    std::vector<Run> pieces;
+    for (int64_t i = 0; i < (int64_t)runs.size(); ++i) {
+      const int32_t g = runs[(size_t)i].owner;
+      if (best[2 * (size_t)g] != i && best[2 * (size_t)g + 1] != i) continue;
+      const int64_t c = pieces.empty() ? 0 : std::min(runs[(size_t)i].start, b->seq_bytes) / kPartAlign * kPartAlign;
+      if (!pieces.empty() && c <= pieces.back().start) pieces.back().owner = g;   // the previous piece is empty
+      else pieces.push_back(Run{c, g});
+    }
+    std::vector<int64_t> pc((size_t)ng * 4, 0);   // per group: piece A [0], [1); piece B [2], [3)
+    std::vector<int64_t> first((size_t)ng, INT64_MAX);
+    for (size_t i = 0; i < pieces.size(); ++i) {
+      const int32_t g = pieces[i].owner;
+      const int64_t e = i + 1 < pieces.size() ? pieces[i + 1].start : b->seq_bytes;
+      int64_t *q = &pc[4 * (size_t)g];
+      const int slot = first[g] == INT64_MAX ? 0 : 2;   // at most two pieces per group
+      q[slot] = pieces[i].start;
+      q[slot + 1] = e;
+      first[g] = std::min(first[g], pieces[i].start);
+    }
+    if (pieces.empty() && ng) {   // no written read in a small scope: the first group copies it all
+      pc[0] = 0;
+      pc[1] = b->seq_bytes;
+      first[0] = 0;
+    }
     std::vector<int32_t> order(ng);
     for (int32_t k = 0; k < ng; ++k) order[k] = k;
-    std::stable_sort(order.begin(), order.end(), [&](int32_t x, int32_t y) { return gs[x].first < gs[y].first; });
-    // partitions: [part[k], part[k + 1]) for the k-th group launched
-    std::vector<int64_t> part(ng + 1), rank(ng);
-    part[0] = 0;
-    for (int32_t k = 1; k < ng; ++k) {
-      const int64_t f = std::min(gs[order[k]].first, b->seq_bytes);
-      part[k] = std::max(part[k - 1], f / kPartAlign * kPartAlign);
-    }
-    if (ng) part[ng] = b->seq_bytes;
-    for (int32_t k = 0; k < ng; ++k) rank[order[k]] = k;
-    // exact bound on masks landing outside the masking group's partition: every nibble of a
-    // written read that lies outside it
+    std::stable_sort(order.begin(), order.end(), [&](int32_t x, int32_t y) { return first[x] < first[y]; });
+    // exact bound on masks landing outside the masking group's pieces: every nibble of a
+    // written read that lies outside them
     int64_t far_cap = 0;
-    for (int32_t r = 0; r < b->n_reads; ++r) {
-      const int32_t ws = b->write_scope[r];
-      if (ws < 0 || b->scope_span_len[ws] > kGrpMaxSpan || b->read_len[r] == 0) continue;
-      const int64_t k = rank[std::upper_bound(gs.begin(), gs.end(), ws,
-                                              [](int32_t v, const G &g) { return v < g.s0; }) - gs.begin() - 1];
+    for (int32_t r : byoff) {
+      const int64_t *q = &pc[4 * (size_t)owner_of(r)];
       const int64_t r0 = b->seq_off[r], r1 = r0 + ((int64_t)b->read_len[r] + 1) / 2;
-      const int64_t in = std::max<int64_t>(0, std::min(r1, part[k + 1]) - std::max(r0, part[k]));
+      const int64_t in = std::max<int64_t>(0, std::min(r1, q[1]) - std::max(r0, q[0])) +
+                         std::max<int64_t>(0, std::min(r1, q[3]) - std::max(r0, q[2]));
       far_cap += 2 * ((r1 - r0) - in);
     }
     // overflow regions: (bases / 48 + kGrpObs) observations per group, i.e. up to ~2 % of its
     // aligned bases mismatching (more: key-range halving)
-    std::vector<int4> grp(4 * (size_t)ng);
+    std::vector<int4> grp(kGrpRec * (size_t)ng);
     int64_t region = 0;
     for (int32_t k = 0; k < ng; ++k) {
       const G &g = gs[order[k]];
+      const int64_t *q = &pc[4 * (size_t)order[k]];
       const int64_t cap = std::min<int64_t>(g.bases / 48 + kGrpObs, INT32_MAX / 2);
-      grp[4 * k] = make_int4(g.s0, g.s1, lo32(g.i0), hi32(g.i0));
-      grp[4 * k + 1] = make_int4(lo32(g.i1), hi32(g.i1), lo32(g.mid), hi32(g.mid));
-      grp[4 * k + 2] = make_int4(lo32(part[k]), hi32(part[k]), lo32(part[k + 1]), hi32(part[k + 1]));
-      grp[4 * k + 3] = make_int4(lo32(region), hi32(region), (int)cap, 0);
+      grp[kGrpRec * k] = make_int4(g.s0, g.s1, lo32(g.i0), hi32(g.i0));
+      grp[kGrpRec * k + 1] = make_int4(lo32(g.i1), hi32(g.i1), lo32(g.mid), hi32(g.mid));
+      grp[kGrpRec * k + 2] = make_int4(lo32(q[0]), hi32(q[0]), lo32(q[1]), hi32(q[1]));
+      grp[kGrpRec * k + 3] = make_int4(lo32(region), hi32(region), (int)cap, 0);
+      grp[kGrpRec * k + 4] = make_int4(lo32(q[2]), hi32(q[2]), lo32(q[3]), hi32(q[3]));
       region += cap;
     }
     if ((rc = dev_alloc(ctx, db, &db->gokey, (size_t)region))) return bail(rc);

@@ -768,3 +768,30 @@ def algorithmic_bytes(arr: Dict[str, np.ndarray]) -> int:
     extra = np.maximum(inc - 1, 0) * (half + 4 * nc + 8)
     ref = (arr["scope_span_len"].astype(np.int64) + 1) // 2
     return int(per_read.sum() + extra.sum() + ref.sum())
+
+
+def dataset_major(arr: Dict[str, np.ndarray], chunk: int = 1 << 20) -> Dict[str, np.ndarray]:
+    """The same batch with its sequence buffer laid out as the product path builds it
+    (anonymizer_methods.build_batch): every dataset-0 read's packed bases, then every dataset-1
+    read's, each dataset in its original buffer order. Only seq_nt16 and seq_off change, so
+    results are comparable read by read with the interleaved original."""
+    ds = arr["dataset"].astype(np.int64)
+    so = arr["seq_off"].astype(np.int64)
+    nb = (arr["read_len"].astype(np.int64) + 1) // 2
+    order = np.lexsort((so, ds))
+    new_off = np.empty_like(so)
+    new_off[order] = np.concatenate([[0], np.cumsum(nb[order])[:-1]])
+    seq = arr["seq_nt16"]
+    out = np.zeros(len(seq), np.uint8)
+    for k in range(0, len(order), chunk):
+        o = order[k:k + chunk]
+        n = nb[o]
+        if n.sum() == 0:
+            continue
+        first = np.concatenate([[0], np.cumsum(n)[:-1]])
+        rel = np.arange(int(n.sum()), dtype=np.int64) - np.repeat(first, n)
+        out[np.repeat(new_off[o], n) + rel] = seq[np.repeat(so[o], n) + rel]
+    res = dict(arr)
+    res["seq_off"] = new_off
+    res["seq_nt16"] = out
+    return res

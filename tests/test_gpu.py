@@ -201,6 +201,36 @@ def test_hip_config2_matches_oracle(masker, oracle):
     masker.set_variant(0)
 
 
+def test_hip_dataset_major_layout_matches_oracle(masker, oracle):
+    """The product path's sequence layout (every tumor read, then every normal read:
+    build_batch) gives each scope group one partition piece per dataset: bytes and counts equal
+    the oracle's, and every read's masked bases equal those of the interleaved layout; the
+    copy-whole-partition-first order (GROUP_SKIP bit 4) gives the same bytes."""
+    from genomeanonymizer_amd import native
+    from genomeanonymizer_amd.synth.batch import config2_batch, dataset_major
+    arr, _ = config2_batch(n_reads=400_000, genome=120_000_000, n_windows=40_000, n_germline=40_000)
+    dm = dataset_major(arr)
+    o_out, o_calls, o_bases, _ = oracle.mask(dm)
+    out, calls, bases, tot = masker.mask(dm)
+    assert np.array_equal(calls, o_calls) and np.array_equal(bases, o_bases)
+    assert np.array_equal(out, o_out)
+    assert bases.sum() > 0
+    masker.set_param(native.PARAM_GROUP_SKIP, 16)
+    try:
+        out_cf = masker.mask(dm)[0]
+    finally:
+        masker.set_param(native.PARAM_GROUP_SKIP, 0)
+    assert np.array_equal(out_cf, out)
+    out_i, calls_i, _, _ = masker.mask(arr)
+    assert np.array_equal(calls_i, calls)
+    nb = (arr["read_len"].astype(np.int64) + 1) // 2
+    first = np.concatenate([[0], np.cumsum(nb)[:-1]])
+    rel = np.arange(int(nb.sum()), dtype=np.int64) - np.repeat(first, nb)
+    ia = np.repeat(arr["seq_off"].astype(np.int64), nb) + rel
+    idm = np.repeat(dm["seq_off"].astype(np.int64), nb) + rel
+    assert np.array_equal(out_i[ia], out[idm])
+
+
 def test_hip_device_path_is_idempotent_and_deterministic(masker):
     """Running the same uploaded batch twice gives identical bytes and totals; masking the
     masked output again changes nothing for TN-masked bases (they now equal the ref)."""

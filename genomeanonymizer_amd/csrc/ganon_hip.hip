@@ -947,16 +947,13 @@ constexpr int kGrpThreads = 256;
 #ifndef GANON_K2_BLOCKS
 #define GANON_K2_BLOCKS 6   // resident workgroups per CU the K = 2 instance is compiled for
 #endif
-#ifndef GANON_TILE_COPY
-#define GANON_TILE_COPY 0   // 1: fused partition copied tile by tile during the scan (CopyCursor)
-#endif
 constexpr int kGrpTile = 256;        // segment records staged per tile
 constexpr int kGrpTarget = 256;      // segments per group (a larger scope forms its own group)
 constexpr int kGrpObs = 512;         // observations per LDS list
 constexpr int kGrpMaxScopes = 256;   // scopes per group (12-bit local index field)
 constexpr int kGrpStack = 80;        // key ranges pending (bisection depth <= 64)
 constexpr int kGrpPatch = 512;       // in-partition masks of one list pass (<= its observations)
-constexpr int kGrpMap = 4096;        // chunk -> segment map entries (larger tiles binary-search)
+constexpr int kGrpMap = 2048;        // chunk -> segment map entries (larger tiles binary-search)
 constexpr int kGrpQuad = 256;        // lists up to this size are matched without sorting
 constexpr int kGrpMaxSpan = 1 << 20; // widest scope of the group kernels (20-bit position field)
 constexpr unsigned long long kEmpty = ~0ull;
@@ -972,9 +969,6 @@ constexpr unsigned long long kNibMask = (1ull << 48) - 1;
 enum { kModeCollect = 0 };
 // GANON_PARAM_GROUP_SKIP (profiling only, results invalid): phases left out
 enum { kSkipClassify = 1, kSkipChunks = 2, kSkipCopy = 4, kSkipCounts = 8 };
-// GANON_PARAM_GROUP_SKIP bit 4 (A/B, same results): copy the whole partition before the scan
-// instead of tile by tile
-enum { kCopyFirst = 16 };
 static_assert(kGrpTile == kGrpThreads && kGrpTile <= 256, "one staged record per thread, 8-bit map");
 
 // The few batch arrays the group kernels read (a slim kernel argument keeps SGPRs free).
@@ -995,7 +989,6 @@ struct GrpShared {
   unsigned long long stk_lo[kGrpStack], stk_hi[kGrpStack];
   int stk_mode[kGrpStack];
   unsigned long long kmin, kmax;
-  unsigned long long cut[2];        // fused: end of the written reads staged so far, per piece
   int top, n_obs, n_patch;
   int blk_calls, blk_bases;         // this workgroup's contribution to the totals
   int cnt_calls[kGrpMaxScopes];     // per-scope counts, written out once at the end
@@ -1103,24 +1096,9 @@ __device__ __forceinline__ bool grp_kept(const GrpBatch &B, int s, int64_t pos_o
   return kp >= 0 && B.keep_code[s] == c && (int64_t)kp - B.span_start[s] == pos_off;
 }
 
-// Fused partition copy, tile by tile: the pieces [beg, end) are copied up to the last byte of
-// the written reads staged so far (cur: next byte to copy), so that the scan's chunk loads that
-// follow find those lines in L2. Copying a whole ~40 KB partition first loses every line before
-// the scan reaches it (a group lives ~35 us while its XCD streams ~27 MB through a 4 MB L2).
-struct CopyCursor {
-  int64_t beg[2], cur[2], end[2];
-  uint8_t *out;
-  int nt;
-};
-
-// A workgroup-uniform 64-bit value (read from LDS) in scalar registers.
-__device__ __forceinline__ unsigned long long uniform64(unsigned long long v) {
-  return (unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)v) |
-         ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(v >> 32)) << 32);
-}
-
-// Bytes [p0, p1) of src to dst in 16-byte windows (p0 16-byte aligned; a window may end past p1
-// only at the end of the buffer, which is padded), 8 windows in flight per thread.
+// Fused partition copy: bytes [p0, p1) of src to dst in 16-byte windows (p0 16-byte aligned; a
+// window may end past p1 only at the end of the buffer, which is padded), 8 windows in flight
+// per thread: all loads issue before the first store waits on them.
 __device__ __forceinline__ void copy_windows(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, int64_t p0,
                                              int64_t p1, int nt) {
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -1143,10 +1121,11 @@ __device__ __forceinline__ void copy_windows(const uint8_t *__restrict__ src, ui
 }
 
 // Stage records [c0, c0 + nh) in LDS with the exclusive prefix of their chunk counts;
-// returns the tile's chunk total. docopy: raise the pieces' copy cuts to the staged written reads.
+// returns the tile's chunk total.
 __device__ __forceinline__ int grp_tile(GrpShared &sh, const int4 *__restrict__ rec4, int64_t c0, int nh,
-                                        int chunk, const CopyCursor &cc, bool docopy) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+                                        int chunk) {
+  const int tid = threadIdx.x, wave = tid >> 6;
+  const int lane = opaque_tid() & 63;   // shuffle sources computed here, not kept live across the kernel
   const int64_t ix = c0 + (tid < nh ? tid : nh - 1);
   const int4 r = rec4[ix];
   int nck = 0;
@@ -1157,7 +1136,7 @@ __device__ __forceinline__ int grp_tile(GrpShared &sh, const int4 *__restrict__ 
   int incl = nck;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
-    const int t = __shfl_up(incl, o);
+    const int t = __builtin_amdgcn_ds_bpermute((lane >= o ? lane - o : lane) << 2, incl);
     if (lane >= o) incl += t;
   }
   if (lane == 63) sh.wsum[wave] = incl;
@@ -1173,14 +1152,6 @@ __device__ __forceinline__ int grp_tile(GrpShared &sh, const int4 *__restrict__ 
   sh.pre[tid] = pre;
   if (total <= kGrpMap)
     for (int k = 0; k < nck; ++k) sh.cmap[pre + k] = (uint8_t)tid;
-  if (docopy && tid < nh && ((uint32_t)r.z >> 31)) {
-    const uint32_t rz = (uint32_t)r.z;
-    const int64_t sn = (int64_t)((uint64_t)(uint32_t)r.x | ((uint64_t)(rz & 0xFF) << 32));
-    const int64_t b0 = sn >> 1, e = (sn + ((rz >> 16) & kSegMaxLen) + 1) >> 1;
-#pragma unroll
-    for (int k = 0; k < 2; ++k)
-      if (b0 >= cc.beg[k] && b0 < cc.end[k]) atomicMax(&sh.cut[k], (unsigned long long)e);
-  }
   __syncthreads();
   return total;
 }
@@ -1203,23 +1174,11 @@ __device__ __forceinline__ int grp_find(const GrpShared &sh, int nh, int total, 
 // windows out of registers with static indices.
 template <int K, bool REF2>
 __device__ __forceinline__ void grp_scan(const GrpBatch &B, GrpShared &sh, const GrpRange &R, const GrpGlobal &gg,
-                                         int64_t i_begin, int64_t i_end, const int4 *__restrict__ rec4, int skip,
-                                         CopyCursor &cc, bool docopy) {
+                                         int64_t i_begin, int64_t i_end, const int4 *__restrict__ rec4, int skip) {
   const int tid = threadIdx.x;
   for (int64_t c0 = i_begin; c0 < i_end; c0 += kGrpTile) {
     const int nh = (int)((i_end - c0) < kGrpTile ? (i_end - c0) : kGrpTile);
-    int total = grp_tile(sh, rec4, c0, nh, 16 * K, cc, docopy);
-    if (docopy) {
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int64_t c = (int64_t)((uniform64(sh.cut[k]) + 15) & ~15ull);
-        const int64_t cut = c < cc.end[k] ? c : cc.end[k];
-        if (cut > cc.cur[k]) {
-          copy_windows(B.seq, cc.out, cc.cur[k], cut, cc.nt);
-          cc.cur[k] = cut;
-        }
-      }
-    }
+    int total = grp_tile(sh, rec4, c0, nh, 16 * K);
     if (skip & kSkipChunks) total = 0;
     for (int t = tid; t < total; t += kGrpThreads) {
       const int j = grp_find(sh, nh, total, t);
@@ -1519,21 +1478,15 @@ __global__ void __launch_bounds__(kGrpThreads, (U == 1 ? 6 : U == 2 ? GANON_K2_B
   const int64_t i_begin = i64_of(g0.z, g0.w), i_end = i64_of(g1.x, g1.y), i_mid = i64_of(g1.z, g1.w);
   const PatchSink sink{out, i64_of(g2.x, g2.y), i64_of(g2.z, g2.w), i64_of(g4.x, g4.y), i64_of(g4.z, g4.w),
                        aux, FUSED, FUSED};
-  // the partition pieces, whole 16-byte windows (the buffers are padded past seq_bytes), copied
-  // tile by tile during the first scan pass (CopyCursor); the stores drain while the scan runs
-  // (s_waitcnt before the mask stores)
-  const bool copy = FUSED && !(skip & kSkipCopy);
-  CopyCursor cc{{sink.p0, sink.q0}, {sink.p0, sink.q0}, {sink.p1, sink.q1}, out, nt_copy};
-  if (copy && (!GANON_TILE_COPY || (skip & kCopyFirst))) {
-#pragma unroll
-    for (int k = 0; k < 2; ++k) copy_windows(B.seq, out, cc.beg[k], cc.end[k], nt_copy);
-    cc.cur[0] = sink.p1;
-    cc.cur[1] = sink.q1;
+  // the partition pieces, whole 16-byte windows (the buffers are padded past seq_bytes); the
+  // stores drain while the scan runs (s_waitcnt before the mask stores). (Copying tile by tile,
+  // each time up to the tile's written reads so that the scan's loads hit L2, read 0.34 GB less
+  // per c2 launch but took 0.55 instead of 0.54 ms in the same build: DESIGN 5.)
+  if (FUSED && !(skip & kSkipCopy)) {
+    copy_windows(B.seq, out, sink.p0, sink.p1, nt_copy);
+    copy_windows(B.seq, out, sink.q0, sink.q1, nt_copy);
   }
-  bool first_pass = true;
   if (tid == 0) {
-    sh.cut[0] = (unsigned long long)sink.p0;
-    sh.cut[1] = (unsigned long long)sink.q0;
     sh.top = 0;
     sh.stk_lo[0] = 0ull;
     sh.stk_hi[0] = ~0ull;
@@ -1572,19 +1525,12 @@ __global__ void __launch_bounds__(kGrpThreads, (U == 1 ? 6 : U == 2 ? GANON_K2_B
       sh.kmax = 0ull;
     }
     __syncthreads();
-    const bool pc = GANON_TILE_COPY && copy && first_pass;
     if (B.ref2) {
-      grp_scan<U, true>(B, sh, R, gg, i_begin, i_mid, rec4, skip, cc, pc);
-      grp_scan<U, false>(B, sh, R, gg, i_mid, i_end, rec4, skip, cc, pc);
+      grp_scan<U, true>(B, sh, R, gg, i_begin, i_mid, rec4, skip);
+      grp_scan<U, false>(B, sh, R, gg, i_mid, i_end, rec4, skip);
     } else {
-      grp_scan<U, false>(B, sh, R, gg, i_begin, i_end, rec4, skip, cc, pc);
+      grp_scan<U, false>(B, sh, R, gg, i_begin, i_end, rec4, skip);
     }
-    if (pc) {   // the rest of the pieces (bytes past the last written read's segments)
-#pragma unroll
-      for (int k = 0; k < 2; ++k)
-        if (cc.cur[k] < cc.end[k]) copy_windows(B.seq, out, cc.cur[k], cc.end[k], nt_copy);
-    }
-    first_pass = false;
     // (grp_scan ends on a barrier)
     if (skip & kSkipClassify) continue;
     const int n = sh.n_obs;
@@ -2049,7 +1995,7 @@ GANON_API int ganon_ctx_set_param(ganon_ctx *ctx, int param, int value) {
     return GANON_OK;
   }
   if (param == GANON_PARAM_GROUP_SKIP) {
-    ctx->group_skip = value & (kSkipClassify | kSkipChunks | kSkipCopy | kSkipCounts | kCopyFirst);
+    ctx->group_skip = value & (kSkipClassify | kSkipChunks | kSkipCopy | kSkipCounts);
     return GANON_OK;
   }
   return fail(ctx, GANON_E_ARG, "unknown parameter %d", param);

@@ -118,8 +118,7 @@ GANON_API int ganon_ctx_set_variant(ganon_ctx *ctx, int variant);
  * thread of the group kernels loads at once (chunk = 16 x value bases): 1, 2 (default), 4 or 8.
  * GANON_PARAM_GROUP_SKIP is for phase timing only and DOES change results: bit 0 leaves out
  * the classification, bit 1 the chunk scan, bit 2 the partition copy of the group kernels, bit 3
- * the per-scope count stores; bit 4 (A/B, results unchanged) copies each group's whole
- * partition before its scan instead of tile by tile.
+ * the per-scope count stores.
  * Keep it 0 in production. GANON_PARAM_GROUP_TARGET: segments per scope group (read at
  * upload; default 512). GANON_PARAM_NT_COPY: non-temporal stores for the fused partition copy
  * (default 1). GANON_PARAM_REF2: group kernels read a 2-bit copy of the reference for segments

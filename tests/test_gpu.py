@@ -204,9 +204,7 @@ def test_hip_config2_matches_oracle(masker, oracle):
 def test_hip_dataset_major_layout_matches_oracle(masker, oracle):
     """The product path's sequence layout (every tumor read, then every normal read:
     build_batch) gives each scope group one partition piece per dataset: bytes and counts equal
-    the oracle's, and every read's masked bases equal those of the interleaved layout; the
-    copy-whole-partition-first order (GROUP_SKIP bit 4) gives the same bytes."""
-    from genomeanonymizer_amd import native
+    the oracle's, and every read's masked bases equal those of the interleaved layout."""
     from genomeanonymizer_amd.synth.batch import config2_batch, dataset_major
     arr, _ = config2_batch(n_reads=400_000, genome=120_000_000, n_windows=40_000, n_germline=40_000)
     dm = dataset_major(arr)
@@ -215,12 +213,6 @@ def test_hip_dataset_major_layout_matches_oracle(masker, oracle):
     assert np.array_equal(calls, o_calls) and np.array_equal(bases, o_bases)
     assert np.array_equal(out, o_out)
     assert bases.sum() > 0
-    masker.set_param(native.PARAM_GROUP_SKIP, 16)
-    try:
-        out_cf = masker.mask(dm)[0]
-    finally:
-        masker.set_param(native.PARAM_GROUP_SKIP, 0)
-    assert np.array_equal(out_cf, out)
     out_i, calls_i, _, _ = masker.mask(arr)
     assert np.array_equal(calls_i, calls)
     nb = (arr["read_len"].astype(np.int64) + 1) // 2

@@ -953,7 +953,7 @@ constexpr int kGrpObs = 512;         // observations per LDS list
 constexpr int kGrpMaxScopes = 256;   // scopes per group (12-bit local index field)
 constexpr int kGrpStack = 80;        // key ranges pending (bisection depth <= 64)
 constexpr int kGrpPatch = 512;       // in-partition masks of one list pass (<= its observations)
-constexpr int kGrpMap = 2048;        // chunk -> segment map entries (larger tiles binary-search)
+constexpr int kGrpMap = 4096;        // chunk -> segment map entries (larger tiles binary-search)
 constexpr int kGrpQuad = 256;        // lists up to this size are matched without sorting
 constexpr int kGrpMaxSpan = 1 << 20; // widest scope of the group kernels (20-bit position field)
 constexpr unsigned long long kEmpty = ~0ull;
@@ -1124,8 +1124,7 @@ __device__ __forceinline__ void copy_windows(const uint8_t *__restrict__ src, ui
 // returns the tile's chunk total.
 __device__ __forceinline__ int grp_tile(GrpShared &sh, const int4 *__restrict__ rec4, int64_t c0, int nh,
                                         int chunk) {
-  const int tid = threadIdx.x, wave = tid >> 6;
-  const int lane = opaque_tid() & 63;   // shuffle sources computed here, not kept live across the kernel
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t ix = c0 + (tid < nh ? tid : nh - 1);
   const int4 r = rec4[ix];
   int nck = 0;
@@ -1133,11 +1132,18 @@ __device__ __forceinline__ int grp_tile(GrpShared &sh, const int4 *__restrict__ 
     sh.rec[tid] = r;
     nck = ((((uint32_t)r.z >> 16) & kSegMaxLen) + chunk - 1) / chunk;
   }
+  // wave inclusive scan: DPP row_shr within each 16-lane row, then the row totals (no lane-index
+  // registers: shuffle index arithmetic hoisted out of the tile loop cost 9 VGPRs and spills)
   int incl = nck;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int t = __builtin_amdgcn_ds_bpermute((lane >= o ? lane - o : lane) << 2, incl);
-    if (lane >= o) incl += t;
+  incl += __builtin_amdgcn_update_dpp(0, incl, 0x111, 0xF, 0xF, false);   // row_shr:1
+  incl += __builtin_amdgcn_update_dpp(0, incl, 0x112, 0xF, 0xF, false);   // row_shr:2
+  incl += __builtin_amdgcn_update_dpp(0, incl, 0x114, 0xF, 0xF, false);   // row_shr:4
+  incl += __builtin_amdgcn_update_dpp(0, incl, 0x118, 0xF, 0xF, false);   // row_shr:8
+  {
+    const int r0 = __builtin_amdgcn_readlane(incl, 15), r1 = __builtin_amdgcn_readlane(incl, 31),
+              r2 = __builtin_amdgcn_readlane(incl, 47);
+    const int row = lane >> 4;
+    incl += (row >= 1 ? r0 : 0) + (row >= 2 ? r1 : 0) + (row >= 3 ? r2 : 0);
   }
   if (lane == 63) sh.wsum[wave] = incl;
   __syncthreads();

@@ -775,10 +775,16 @@ def dataset_major(arr: Dict[str, np.ndarray], chunk: int = 1 << 20) -> Dict[str,
     (anonymizer_methods.build_batch): every dataset-0 read's packed bases, then every dataset-1
     read's, each dataset in its original buffer order. Only seq_nt16 and seq_off change, so
     results are comparable read by read with the interleaved original."""
-    ds = arr["dataset"].astype(np.int64)
+    order = np.lexsort((arr["seq_off"].astype(np.int64), arr["dataset"].astype(np.int64)))
+    return relayout(arr, order, chunk)
+
+
+def relayout(arr: Dict[str, np.ndarray], order: np.ndarray, chunk: int = 1 << 20) -> Dict[str, np.ndarray]:
+    """The same batch with the reads' packed bases stored in the buffer in ``order`` (read
+    indices), back to back; only seq_nt16 and seq_off change."""
     so = arr["seq_off"].astype(np.int64)
     nb = (arr["read_len"].astype(np.int64) + 1) // 2
-    order = np.lexsort((so, ds))
+    order = np.asarray(order, np.int64)
     new_off = np.empty_like(so)
     new_off[order] = np.concatenate([[0], np.cumsum(nb[order])[:-1]])
     seq = arr["seq_nt16"]

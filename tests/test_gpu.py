@@ -201,13 +201,18 @@ def test_hip_config2_matches_oracle(masker, oracle):
     masker.set_variant(0)
 
 
-def test_hip_dataset_major_layout_matches_oracle(masker, oracle):
+@pytest.mark.parametrize("layout", ["dataset_major", "shuffled"])
+def test_hip_buffer_layouts_match_oracle(masker, oracle, layout):
     """The product path's sequence layout (every tumor read, then every normal read:
-    build_batch) gives each scope group one partition piece per dataset: bytes and counts equal
-    the oracle's, and every read's masked bases equal those of the interleaved layout."""
-    from genomeanonymizer_amd.synth.batch import config2_batch, dataset_major
+    build_batch) gives each scope group one partition piece per dataset; a shuffled buffer
+    leaves most written bytes outside their group's pieces (far-list masks). Bytes and counts
+    equal the oracle's, and every read's masked bases equal those of the interleaved layout."""
+    from genomeanonymizer_amd.synth.batch import config2_batch, dataset_major, relayout
     arr, _ = config2_batch(n_reads=400_000, genome=120_000_000, n_windows=40_000, n_germline=40_000)
-    dm = dataset_major(arr)
+    if layout == "dataset_major":
+        dm = dataset_major(arr)
+    else:
+        dm = relayout(arr, np.random.default_rng(7).permutation(len(arr["read_len"])))
     o_out, o_calls, o_bases, _ = oracle.mask(dm)
     out, calls, bases, tot = masker.mask(dm)
     assert np.array_equal(calls, o_calls) and np.array_equal(bases, o_bases)

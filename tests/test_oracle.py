@@ -90,3 +90,26 @@ def test_oracle_threads_give_the_same_results():
         e.threads = 7
         b = e.mask(arr)
         assert all(np.array_equal(x, y) for x, y in zip(a, b))
+
+
+def test_oracle_is_buffer_layout_invariant():
+    """The batches the GPU layout tests use (synth dataset_major / relayout: the product path's
+    tumor-then-normal buffer and a shuffled one) hold the same reads as the original: the oracle
+    masks every read identically and counts the same calls in all three."""
+    import numpy as np
+    from pyoracle import OracleEngine
+    from genomeanonymizer_amd.synth.batch import config2_batch, dataset_major, relayout
+    arr, _ = config2_batch(n_reads=60_000, genome=20_000_000, n_windows=6_000, n_germline=6_000)
+    nb = (arr["read_len"].astype(np.int64) + 1) // 2
+    first = np.concatenate([[0], np.cumsum(nb)[:-1]])
+    rel = np.arange(int(nb.sum()), dtype=np.int64) - np.repeat(first, nb)
+    e = OracleEngine()
+    out, calls, bases, _ = e.mask(arr)
+    assert bases.sum() > 0
+    for other in (dataset_major(arr), relayout(arr, np.random.default_rng(3).permutation(len(nb)))):
+        assert len(other["seq_nt16"]) == len(arr["seq_nt16"])
+        assert np.array_equal(other["seq_nt16"][np.repeat(other["seq_off"], nb) + rel],
+                              arr["seq_nt16"][np.repeat(arr["seq_off"], nb) + rel])
+        o2, c2, b2, _ = e.mask(other)
+        assert np.array_equal(c2, calls) and np.array_equal(b2, bases)
+        assert np.array_equal(o2[np.repeat(other["seq_off"], nb) + rel], out[np.repeat(arr["seq_off"], nb) + rel])

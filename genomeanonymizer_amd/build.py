@@ -43,14 +43,15 @@ def _run(cmd) -> None:
         raise RuntimeError(f"build failed: {' '.join(cmd)}")
 
 
-HIP_SOURCES = ("ganon_hip.hip", "ganon_fastq.hip", "ganon_indel.hip")
+HIP_SOURCES = ("ganon_hip.hip", "ganon_prep.hip", "ganon_fastq.hip", "ganon_indel.hip")
 
 
 def build_hip(force: bool = False) -> str:
     """One object per source, compiled in parallel, then linked (the hipcub sort in
     ganon_indel.hip is the slowest unit)."""
     srcs = [os.path.join(CSRC, s) for s in HIP_SOURCES]
-    hdrs = [os.path.join(REPO, "include", "ganon.h"), os.path.join(CSRC, "ganon_ctx.h"), __file__]
+    hdrs = [os.path.join(REPO, "include", "ganon.h"), os.path.join(CSRC, "ganon_ctx.h"), os.path.join(CSRC, "ganon_batch.h"),
+            __file__]
     if not (force or _stale(HIP_LIB, srcs + hdrs)):
         return HIP_LIB
     objdir = os.path.join(PKG, "build")

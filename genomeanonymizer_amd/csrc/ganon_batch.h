@@ -1,0 +1,173 @@
+// ganon_batch.h — internal to libganon_hip.so: the device batch (ganon_dbatch), the resident
+// reference (ganon_ref), the layouts the device prep kernels (ganon_prep.hip) write and the
+// masking kernels (ganon_hip.hip) read. Not part of the C ABI (include/ganon.h is).
+//
+// A batch lives in HBM in two layers:
+//   raw      the ganon_batch SoA exactly as the host hands it over (BAM nt16 bases, BAM CIGAR
+//            words, per-read/per-scope metadata, the scope->read incidence CSR) — the only
+//            bytes that cross PCIe;
+//   derived  everything the masking kernels need beyond that — per-read segment counts and
+//            read ends, scope groups, 16-byte segment records (one per aligned M/=/X run of a
+//            read in a scope), output partition pieces, overflow regions — rebuilt from the raw
+//            layer by the prep kernels on every ganon_batch_run.
+#ifndef GANON_BATCH_H
+#define GANON_BATCH_H
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <vector>
+
+#include "../../include/ganon.h"
+#include "ganon_ctx.h"
+
+namespace ganon_dev {
+
+constexpr int kBlock = 256;
+constexpr int kWaves = kBlock / 64;
+constexpr int kTile = 16384;           // positions per tile of a huge scope (tile path)
+
+// ---- group kernels (ganon_hip.hip k_group) -----------------------------------------------
+constexpr int kGrpRec = 5;             // int4 records per group (layout below)
+constexpr int kGrpObs = 512;           // observations per LDS list
+constexpr int kGrpMaxScopes = 256;     // scopes per group (8-bit LDS counters index, 12-bit field)
+constexpr int kGrpMaxSpan = 1 << 20;   // widest scope of the group kernels (20-bit position field)
+constexpr int64_t kPartAlign = 128;    // partition boundaries fall on whole lines
+constexpr int kSegMaxLen = (1 << 14) - 1;   // longer aligned runs are cut into pieces
+constexpr uint32_t kSegMine = 1u << 31;     // the segment's read is written by this scope
+// segment record (int4, 16 bytes): x = query nibble bits 0-31, y = reference nibble bits 0-31,
+// z = query nibble bits 32-39 | reference nibble bits 32-39 << 8 | length << 16 (14 bits) |
+// dataset << 30 | mine << 31, w = scope_local | (pos - span_start) << 12.
+// group record (kGrpRec x int4), one per group in launch order:
+//   [0] {s_begin, s_end, seg_begin lo, hi}      [1] {seg_end lo, hi, seg_mid lo, hi}
+//   [2] {piece A begin lo, hi, end lo, hi}       [3] {overflow region lo, hi, capacity, 0}
+//   [4] {piece B begin lo, hi, end lo, hi}
+// segments [seg_begin, seg_mid) have an all-ACGT reference range (2-bit reference).
+
+// Device view of a batch (all pointers device-resident).
+struct DevBatch {
+  const int32_t *ref_start, *read_len, *read_end, *n_cig, *write_scope;
+  const int64_t *seq_off, *cig_off;
+  const uint8_t *seq, *dataset;
+  const uint32_t *cigar;
+  const int64_t *incid_off;
+  const int32_t *incid_read;
+  const int32_t *span_start, *span_len, *keep_pos;
+  const int64_t *ref_off;
+  const uint8_t *ref, *keep_code;
+  const uint32_t *ref2;   // 2-bit reference (k_ref2), null = nt16 only
+};
+
+struct Tile {
+  int32_t scope;
+  int32_t a;      // tile covers [a, b) (contig positions)
+  int32_t b;
+  int32_t pad;
+  int64_t lo;     // candidate range in large_incid
+  int64_t hi;
+};
+
+// Rarely used outputs and scratch of the group kernels, read through one pointer (device
+// memory) so that their addresses do not occupy scalar registers for the whole kernel.
+struct GrpAux {
+  int32_t *scope_calls, *scope_bases, *part;   // per-scope counts; per-workgroup partial totals
+  unsigned long long *far;                      // masks of bytes outside the masking group's pieces
+  unsigned long long *far_count;                // 64-bit: a whole sample may be one batch
+  int64_t far_cap;
+  unsigned long long *paths;                    // [0] sorted lists, [1] region passes, [2] key-range splits
+  unsigned long long *okey, *opay, *tkey;       // overflow regions
+  unsigned int *tflag;
+};
+
+// First error the device validation found (upload only).
+struct PrepErr {
+  int code;         // 0 none, else a PrepErrKind
+  int pad;
+  long long index;  // read / scope / incidence
+  long long a, b;
+};
+enum PrepErrKind {
+  kErrReadSeq = 1, kErrReadCigar, kErrReadDataset, kErrReadWriteScope, kErrReadLong, kErrCigarOp, kErrReadPos,
+  kErrScopeOff, kErrScopeSpan, kErrScopeRef, kErrScopeKeep, kErrIncidRead, kErrIncidSpan, kErrWriteScopeMissing
+};
+
+// Grow-only device buffer (+128 bytes of padding: the group kernels load up to 68 bytes past a
+// chunk start, the patch atomics touch whole dwords).
+struct DBuf {
+  void *p = nullptr;
+  size_t bytes = 0;
+};
+
+}  // namespace ganon_dev
+
+// Resident reference: uploaded once, shared by every batch of a context (a whole genome).
+struct ganon_ref {
+  uint8_t *nt16 = nullptr;     // upper-cased reference, nt16, 2 per byte (+ padding)
+  uint32_t *ref2 = nullptr;    // 2-bit copy (A0 C1 G2 T3), 16 bases per word
+  uint64_t *bad = nullptr;     // bit k: 64-base block k holds a non-ACGT code (N, IUPAC, '=')
+  int64_t bytes = 0, n_blk = 0;
+  bool owned_by_batch = false;
+};
+
+struct ganon_dbatch {
+  ganon_dev::DevBatch B{};
+  // sizes of the current contents
+  int32_t n_reads = 0, n_scopes = 0;
+  int64_t n_incid = 0, seq_bytes = 0, n_cigar_ops = 0;
+  const ganon_ref *ref = nullptr;
+  ganon_ref *own_ref = nullptr;          // a batch uploaded without a resident reference
+  // raw layer (grow-only)
+  ganon_dev::DBuf b_ref_start, b_read_len, b_seq_off, b_cig_off, b_n_cig, b_dataset, b_write_scope, b_seq, b_cigar,
+      b_incid_off, b_incid_read, b_span_start, b_span_len, b_ref_off, b_keep_pos, b_keep_code;
+  // derived layer
+  ganon_dev::DBuf b_read_end, b_rseg, b_rbase, b_seen, b_cost, b_cost_scan, b_gid, b_gs0, b_lo, b_lo_idx, b_lo_sorted,
+      b_lo_idx_sorted, b_groups, b_seg4, b_grp_part, b_far, b_gokey, b_gopay, b_gtkey, b_gtflag, b_scan_tmp, b_out,
+      b_scope_calls, b_scope_bases, b_small;   // b_small: totals, static totals, counters, acc, status, errors
+  uint8_t *out = nullptr;
+  int32_t *scope_calls = nullptr, *scope_bases = nullptr;
+  unsigned long long *totals = nullptr, *static_totals = nullptr, *acc = nullptr, *far_count = nullptr;
+  int32_t *counters = nullptr;          // [0] rare small (unused), [1] rare tiles
+  int32_t *status = nullptr;            // sticky device error bits (1: far-mask list overflow)
+  ganon_dev::PrepErr *err = nullptr;
+  unsigned long long *plan_info = nullptr;   // [0] far nibbles, [1] huge scopes, [2] written reads
+  unsigned long long *paths = nullptr;       // GrpAux::paths (since upload)
+  ganon_dev::GrpAux *aux = nullptr;
+  // plan of the current contents (device prep, sized at upload)
+  int32_t n_groups = 0, group_target = 512;
+  int64_t n_seg = 0, region = 0, far_cap = 0, n_written = 0;
+  size_t scan_tmp_bytes = 0;
+  // huge scopes (> kGrpMaxSpan positions): tile path, planned on the host at upload
+  std::vector<void *> huge_allocs;
+  ganon_dev::Tile *tiles_h = nullptr;
+  int32_t *large_incid = nullptr, *large_written_h = nullptr, *large_ids = nullptr;
+  int64_t *tab_off = nullptr;
+  uint16_t *tn_tab = nullptr;
+  int64_t tn_entries = 0;
+  int32_t n_tiles_h = 0, n_large_written_h = 0, n_huge_scopes = 0;
+  int32_t *rare_tile_list = nullptr;
+  bool ran = false;
+};
+
+namespace ganon_prep {
+
+// Validate the raw layer on the device, plan the derived layer (group count, segment count,
+// overflow regions, far-mask capacity) and size its buffers. Synchronous (upload time).
+int plan(ganon_ctx *ctx, ganon_dbatch *db);
+// Rebuild every derived array from the raw layer (async on the stream): the first half of
+// every ganon_batch_run.
+int run(ganon_ctx *ctx, ganon_dbatch *db);
+// Grow-only allocation of count elements of T.
+int grow(ganon_ctx *ctx, ganon_dev::DBuf &b, size_t bytes);
+template <typename T>
+inline int grow_n(ganon_ctx *ctx, ganon_dev::DBuf &b, size_t count, T **out) {
+  int rc = grow(ctx, b, count * sizeof(T));
+  *out = static_cast<T *>(b.p);
+  return rc;
+}
+
+}  // namespace ganon_prep
+
+// Non-ACGT block bitmap of a resident reference (ganon_prep.hip), async on the stream.
+int ganon_ref_blocks(ganon_ctx *ctx, ganon_ref *ref);
+
+#endif  // GANON_BATCH_H

@@ -19,10 +19,10 @@ struct ganon_ctx {
   hipStream_t stream = nullptr;
   bool profiling = false;
   int variant = GANON_VARIANT_DEFAULT;
-  int v3_blocks[2] = {1, 1};   // resident grid of k_scope_v3 per class (occupancy x CUs)
   int group_unroll = 2;        // GANON_PARAM_GROUP_UNROLL
   int group_skip = 0;          // GANON_PARAM_GROUP_SKIP (profiling only)
-  int group_target = 512;      // GANON_PARAM_GROUP_TARGET (512: two full 256-record staging tiles)
+  int group_target = 704;      // GANON_PARAM_GROUP_TARGET, cost units per group (segments + a
+                               // per-scope weight of 3: ~512 segments on configs[1], two staging tiles)
   int nt_copy = 1;             // GANON_PARAM_NT_COPY
   int ref2 = 1;                // GANON_PARAM_REF2
   int fq_skip = 0;             // GANON_PARAM_FASTQ_SKIP (profiling only)

@@ -12,13 +12,14 @@
 //             kept window variant gets the reference base (anonymizer_methods.py:537-556,
 //             :170-176); the call is counted for the statistics (:555-556).
 //
-// Design: integer/byte work, HBM-bound — no MFMA. One workgroup owns one
-// scope (or a 16 Ki-position tile of a wide scope). The scope's reference slice and a
-// per-position tally live in LDS: 1 byte per position (tumor ACGT nibble | normal ACGT
-// nibble, updated with ds_or_b32 on the containing dword). nt16 codes of A, C, G, T are
-// one-hot (1, 2, 4, 8), so a nibble IS the allele set and TN = tumor & normal.
-// Non-ACGTN read bases ("=" and IUPAC codes) are rare; a scope that meets one is re-run
-// on a 16-code tally (4 bytes per position: tumor code mask | normal code mask << 16).
+// Design: integer/byte work, HBM-bound — no MFMA. A run is
+//   device prep (ganon_prep.hip): the raw SoA -> segment records, scope groups, partitions;
+//   k_group<2, true>: one 256-thread workgroup per scope group copies its partition pieces of
+//             the output and streams every aligned base of its scopes in 32-base chunks;
+//             mismatches become LDS observations, classified per (scope, position, allele);
+//   k_tile_large + k_mask_large: scopes wider than 1 Mi positions (16 Ki-position LDS tiles);
+//   k_finish: far masks, totals.
+// The reference genome is resident (ganon_ref): nt16 + a 2-bit copy + a non-ACGT block map.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -28,43 +29,15 @@
 #include <numeric>
 #include <string>
 #include <type_traits>
-#include <thread>
 #include <vector>
 
 #include "../../include/ganon.h"
+#include "ganon_batch.h"
 #include "ganon_ctx.h"
 
+using namespace ganon_dev;
+
 namespace {
-
-constexpr int kBlock = 256;
-constexpr int kWaves = kBlock / 64;
-constexpr int kSmallCap0 = 2560;    // positions, class 0 (window scopes: 2001 + read overhang)
-constexpr int kSmallCap1 = 16384;   // positions, class 1 (= wide cap)
-constexpr int kTile = 16384;        // positions per tile of a large scope
-constexpr int kPersistGrid = 1024;  // grid of the device-counted (rare) re-run kernels
-
-struct Tile {
-  int32_t scope;
-  int32_t a;      // tile covers [a, b) (contig positions)
-  int32_t b;
-  int32_t pad;
-  int64_t lo;     // candidate range in large_incid
-  int64_t hi;
-};
-
-// Device view of a batch (all pointers device-resident).
-struct DevBatch {
-  const int32_t *ref_start, *read_len, *read_end, *n_cig, *write_scope;
-  const int64_t *seq_off, *cig_off;
-  const uint8_t *seq, *dataset;
-  const uint32_t *cigar;
-  const int64_t *incid_off;
-  const int32_t *incid_read;
-  const int32_t *span_start, *span_len, *keep_pos;
-  const int64_t *ref_off;
-  const uint8_t *ref, *keep_code;
-  const uint32_t *ref2;   // 2-bit reference (k_ref2) for the group kernels, null = nt16 only
-};
 
 __device__ __forceinline__ int nib_at(const uint8_t *__restrict__ buf, int64_t i) {
   const uint8_t b = buf[i >> 1];
@@ -242,261 +215,7 @@ __device__ __forceinline__ int mask_read_lds(const DevBatch &B, int r, int a, co
   return masked;
 }
 
-// ---- kernels ---------------------------------------------------------------------------
-
-// Reads written unmasked (write_scope == -1): plain copy.
-__global__ void __launch_bounds__(kBlock) k_passthrough(const DevBatch B, const int32_t *__restrict__ list,
-                                                        int n, uint8_t *__restrict__ out) {
-  const int lane = threadIdx.x & 63;
-  const int gw = (blockIdx.x * kBlock + threadIdx.x) >> 6;
-  const int nw = (gridDim.x * kBlock) >> 6;
-  for (int i = gw; i < n; i += nw) {
-    const int r = list[i];
-    const int64_t so = B.seq_off[r];
-    const int nbytes = (B.read_len[r] + 1) >> 1;
-    for (int j = lane; j < nbytes; j += 64) out[so + j] = B.seq[so + j];
-  }
-}
-
-// One workgroup per small scope (span <= cap): tally -> classify -> mask, all in LDS.
-// count_ptr != nullptr: the list length lives on the device (re-run of rare scopes).
-template <int TB>
-__global__ void __launch_bounds__(kBlock) k_scope_small(const DevBatch B, const int32_t *__restrict__ list,
-                                                        int n_static, const int32_t *count_ptr, int cap,
-                                                        uint8_t *__restrict__ out, int32_t *scope_calls,
-                                                        int32_t *scope_bases, int32_t *rare_list,
-                                                        int32_t *rare_count) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  const int tab_words = cap * TB / 4;
-  uint32_t *tab = smem;
-  uint8_t *refb = reinterpret_cast<uint8_t *>(smem + tab_words);
-  int *scratch = reinterpret_cast<int *>(refb + ((cap / 2 + 15) & ~15));
-  const int n = count_ptr ? *count_ptr : n_static;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int li = blockIdx.x; li < n; li += gridDim.x) {
-    const int s = list[li];
-    const int a = B.span_start[s];
-    const int span = B.span_len[s];
-    const int b = a + span;
-    const int words = (span * TB + 3) >> 2;
-    for (int w = threadIdx.x; w < words; w += kBlock) tab[w] = 0;
-    stage_ref(B, B.ref_off[s], span, refb);
-    if (threadIdx.x == 0) scratch[kWaves] = 0;
-    __syncthreads();
-    const int64_t i0 = B.incid_off[s], i1 = B.incid_off[s + 1];
-    bool rare = false;
-    const LdsRef refn{refb, a};
-    for (int64_t i = i0 + wave; i < i1; i += kWaves) rare |= tally_read<TB>(B, B.incid_read[i], a, b, tab, refn, lane);
-    if (TB == 1 && rare) scratch[kWaves] = 1;
-    __syncthreads();
-    clear_keep<TB>(B, s, a, b, tab);
-    __syncthreads();
-    int calls = 0;
-    for (int off = threadIdx.x; off < span; off += kBlock) calls += tn_count<TB>(tn_mask<TB>(tab, off));
-    calls = block_sum(calls, scratch);
-    int bases = 0;
-    for (int64_t i = i0 + wave; i < i1; i += kWaves) {
-      const int r = B.incid_read[i];
-      if (B.write_scope[r] != s) continue;
-      bases += mask_read_lds<TB>(B, r, a, tab, refn, out, lane);
-    }
-    bases = block_sum(bases, scratch);
-    if (threadIdx.x == 0) {
-      scope_calls[s] = calls;
-      scope_bases[s] = bases;
-      if (TB == 1 && scratch[kWaves]) rare_list[atomicAdd(rare_count, 1)] = s;
-    }
-    __syncthreads();
-  }
-}
-
-// One WAVE per small scope (the common case: ~2.3 kb spans, a handful to a few hundred
-// reads). Reads are taken 64 at a time: each lane loads one read's metadata, reads with a
-// single M/=/X op covering the whole sequence ("simple", ~all short reads) are compacted
-// into LDS and processed four at a time by 16-lane groups (one packed byte = two bases
-// per lane step); reads with any other CIGAR go through the per-read cursor walk. The
-// reference nibbles come straight from the packed genome (no staging), the tally is the
-// 1-byte-per-position LDS table. Same results as k_scope_small<1>.
-constexpr int kMetaLds = 64 * (4 * 4 + 8);
-
-__device__ __forceinline__ uint64_t lanes_below(int lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
-
-__global__ void __launch_bounds__(64) k_scope_wave(const DevBatch B, const int32_t *__restrict__ list, int n,
-                                                   int cap, uint8_t *__restrict__ out, int32_t *scope_calls,
-                                                   int32_t *scope_bases, int32_t *rare_list, int32_t *rare_count) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  uint32_t *tab = smem;
-  int *m_start = reinterpret_cast<int *>(smem + cap / 4);
-  int *m_len = m_start + 64;
-  int *m_ds = m_len + 64;
-  int64_t *m_off = reinterpret_cast<int64_t *>(m_ds + 128);
-  const int lane = threadIdx.x;
-  for (int li = blockIdx.x; li < n; li += gridDim.x) {
-    const int s = list[li];
-    const int a = B.span_start[s];
-    const int span = B.span_len[s];
-    const int b = a + span;
-    const GlobalRef refn{B.ref, B.ref_off[s] - a};
-    uint4 *t4 = reinterpret_cast<uint4 *>(tab);
-    for (int k = lane; k < ((span + 15) >> 4); k += 64) t4[k] = make_uint4(0u, 0u, 0u, 0u);
-    __syncthreads();
-    const int64_t i0 = B.incid_off[s], i1 = B.incid_off[s + 1];
-    bool rare = false;
-    // ---- tally ------------------------------------------------------------------------
-    for (int64_t c0 = i0; c0 < i1; c0 += 64) {
-      const int nh = (int)((i1 - c0) < 64 ? (i1 - c0) : 64);
-      int r = 0;
-      bool simple = false, cplx = false;
-      if (lane < nh) {
-        r = B.incid_read[c0 + lane];
-        const int L = B.read_len[r];
-        const int nc = B.n_cig[r];
-        if (nc == 1) {
-          const uint32_t w = B.cigar[B.cig_off[r]];
-          const int op = w & 15;
-          simple = (op == 0 || op == 7 || op == 8) && (int)(w >> 4) == L && L > 0;
-        }
-        cplx = !simple && nc > 0 && L > 0;
-      }
-      const uint64_t sm = __ballot(simple);
-      if (simple) {
-        const int idx = __popcll(sm & lanes_below(lane));
-        m_start[idx] = B.ref_start[r];
-        m_len[idx] = B.read_len[r];
-        m_ds[idx] = B.dataset[r];
-        m_off[idx] = B.seq_off[r];
-      }
-      __syncthreads();
-      const int ns = __popcll(sm);
-      for (int j0 = 0; j0 < ns; j0 += 4) {
-        const int j = j0 + (lane >> 4);
-        if (j >= ns) continue;
-        const int st = m_start[j], L = m_len[j], d = m_ds[j];
-        const int64_t so = m_off[j];
-        const int nb = (L + 1) >> 1;
-        for (int bi = lane & 15; bi < nb; bi += 16) {
-          const uint32_t byte = B.seq[so + bi];
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int q = 2 * bi + h;
-            if (q >= L) break;
-            const int c = h ? (byte & 15) : (byte >> 4);
-            const int p = st + q;
-            const int rc = refn(p);
-            if (c == 15 || c == rc || !is_acgt(rc)) continue;
-            if (is_acgt(c)) {
-              const int off = p - a;
-              atomicOr(&tab[off >> 2], (uint32_t)c << (d * 4 + (off & 3) * 8));
-            } else {
-              rare = true;
-            }
-          }
-        }
-      }
-      uint64_t cm = __ballot(cplx);
-      while (cm) {
-        const int l = __ffsll((unsigned long long)cm) - 1;
-        cm &= cm - 1;
-        const int rr = __shfl(r, l);
-        rare |= tally_read<1>(B, rr, a, b, tab, refn, lane);
-      }
-      __syncthreads();
-    }
-    // ---- classify: kept allele out, count TN calls --------------------------------------
-    clear_keep<1>(B, s, a, b, tab);
-    __syncthreads();
-    int calls = 0;
-    for (int k = lane; k < ((span + 3) >> 2); k += 64) {
-      const uint32_t w = tab[k];
-      calls += __popc(w & (w >> 4) & 0x0F0F0F0Fu);
-    }
-    // ---- mask the reads this scope writes -------------------------------------------------
-    int bases = 0;
-    for (int64_t c0 = i0; c0 < i1; c0 += 64) {
-      const int nh = (int)((i1 - c0) < 64 ? (i1 - c0) : 64);
-      int r = 0;
-      bool simple = false, cplx = false;
-      if (lane < nh) {
-        r = B.incid_read[c0 + lane];
-        if (B.write_scope[r] == s) {
-          const int L = B.read_len[r];
-          const int nc = B.n_cig[r];
-          if (nc == 1) {
-            const uint32_t w = B.cigar[B.cig_off[r]];
-            const int op = w & 15;
-            simple = (op == 0 || op == 7 || op == 8) && (int)(w >> 4) == L && L > 0;
-          }
-          cplx = !simple && L > 0;
-        }
-      }
-      const uint64_t sm = __ballot(simple);
-      if (simple) {
-        const int idx = __popcll(sm & lanes_below(lane));
-        m_start[idx] = B.ref_start[r];
-        m_len[idx] = B.read_len[r];
-        m_off[idx] = B.seq_off[r];
-      }
-      __syncthreads();
-      const int ns = __popcll(sm);
-      for (int j0 = 0; j0 < ns; j0 += 4) {
-        const int j = j0 + (lane >> 4);
-        if (j >= ns) continue;
-        const int st = m_start[j], L = m_len[j];
-        const int64_t so = m_off[j];
-        const int nb = (L + 1) >> 1;
-        for (int bi = lane & 15; bi < nb; bi += 16) {
-          const uint32_t byte = B.seq[so + bi];
-          int nib[2] = {(int)(byte >> 4), (int)(byte & 15)};
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int q = 2 * bi + h;
-            if (q >= L) break;
-            const int off = st + q - a;
-            const uint32_t t = (tab[off >> 2] >> ((off & 3) * 8)) & 0xFF;
-            const uint32_t tn = t & (t >> 4) & 15;
-            if (tn && is_acgt(nib[h]) && (tn & (uint32_t)nib[h])) {
-              nib[h] = refn(st + q);
-              ++bases;
-            }
-          }
-          out[so + bi] = (uint8_t)((nib[0] << 4) | nib[1]);
-        }
-      }
-      uint64_t cm = __ballot(cplx);
-      while (cm) {
-        const int l = __ffsll((unsigned long long)cm) - 1;
-        cm &= cm - 1;
-        const int rr = __shfl(r, l);
-        bases += mask_read_lds<1>(B, rr, a, tab, refn, out, lane);
-      }
-      __syncthreads();
-    }
-    for (int o = 32; o > 0; o >>= 1) {
-      calls += __shfl_xor(calls, o);
-      bases += __shfl_xor(bases, o);
-    }
-    const bool any_rare = __ballot(rare) != 0;
-    if (lane == 0) {
-      scope_calls[s] = calls;
-      scope_bases[s] = bases;
-      if (any_rare) rare_list[atomicAdd(rare_count, 1)] = s;
-    }
-    __syncthreads();
-  }
-}
-
-// ---- v2: copy-then-patch ----------------------------------------------------------------
-// The output starts as a device copy of the input bases (one streaming memcpy); the scope
-// kernel only reads. Per incidence a 16-byte record (built at upload, scope-major, so a
-// scope's records are one coalesced load) says where the read is and whether this scope
-// writes it. Simple reads are taken 16 nibbles per lane (three aligned dword loads each for
-// the read and the reference, nibble-swapped so nibble k sits at bits 4k), mismatches go
-// to the LDS tally AND to a short LDS observation list; after classification only the
-// observations that hit a TN call in a read this scope writes are patched in place
-// (atomicXor on the containing dword: neighbouring reads' bytes are untouched).
-constexpr int kObsCap = 256;
-constexpr uint32_t kRecSimple = 1u << 25, kRecMine = 1u << 26, kRecCplx = 1u << 27;
-
+// ---- nibble helpers ------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t nib_swap(uint32_t d) { return ((d >> 4) & 0x0F0F0F0Fu) | ((d & 0x0F0F0F0Fu) << 4); }
 
 // 16 consecutive nibbles starting at nibble index n of a packed buffer (padded by 12 bytes):
@@ -510,379 +229,14 @@ __device__ __forceinline__ uint64_t load16(const uint8_t *__restrict__ buf, int6
   return (uint64_t)(uint32_t)(x0 >> sh) | ((uint64_t)(uint32_t)(x1 >> sh) << 32);
 }
 
-struct ObsList {
-  uint32_t *meta;   // off | c << 16 | ds << 20 | mine << 21
-  int64_t *nib;     // nibble index of the base in the sequence buffer
-  int *count;       // [0] entries, [1] overflow flag
-  int cap = kObsCap;
-  __device__ __forceinline__ void add(int off, int c, int ds, bool mine, int64_t nib_index) {
-    const int k = atomicAdd(count, 1);
-    if (k < cap) {
-      meta[k] = (uint32_t)off | ((uint32_t)c << 16) | ((uint32_t)ds << 20) | ((uint32_t)mine << 21);
-      nib[k] = nib_index;
-    } else {
-      count[1] = 1;
-    }
-  }
-};
-
 __device__ __forceinline__ void patch_nibble(uint8_t *out, int64_t nib_index, int from, int to) {
   const int64_t byte = nib_index >> 1;
   const int sh = 8 * (int)(byte & 3) + ((nib_index & 1) ? 0 : 4);
   atomicXor(reinterpret_cast<uint32_t *>(out) + (byte >> 2), (uint32_t)(from ^ to) << sh);
 }
 
-// One observation of base c at position p (offset off in the table) of dataset ds.
-__device__ __forceinline__ bool observe(uint32_t *tab, ObsList &obs, int off, int c, int rc, int ds, bool mine,
-                                        int64_t nib_index) {
-  if (c == 15 || c == rc || !is_acgt(rc)) return false;
-  if (!is_acgt(c)) return true;                       // rare: 16-code re-run
-  atomicOr(&tab[off >> 2], (uint32_t)c << (ds * 4 + (off & 3) * 8));
-  obs.add(off, c, ds, mine, nib_index);
-  return false;
-}
-
-__global__ void __launch_bounds__(64) k_scope_v2(const DevBatch B, const int4 *__restrict__ inc_rec,
-                                                 const int32_t *__restrict__ list, int n, int cap,
-                                                 uint8_t *__restrict__ out, int32_t *scope_calls,
-                                                 int32_t *scope_bases, int32_t *rare_list, int32_t *rare_count) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  uint32_t *tab = smem;
-  int *m_start = reinterpret_cast<int *>(smem + cap / 4);
-  int *m_len = m_start + 64;
-  int *m_ds = m_len + 64;
-  int *m_mine = m_ds + 64;
-  int64_t *m_off = reinterpret_cast<int64_t *>(m_mine + 64);
-  ObsList obs;
-  obs.meta = reinterpret_cast<uint32_t *>(m_off + 64);
-  obs.nib = reinterpret_cast<int64_t *>(obs.meta + kObsCap);
-  obs.count = reinterpret_cast<int *>(obs.nib + kObsCap);
-  const int lane = threadIdx.x;
-  for (int li = blockIdx.x; li < n; li += gridDim.x) {
-    const int s = list[li];
-    const int a = B.span_start[s];
-    const int span = B.span_len[s];
-    const int b = a + span;
-    const int64_t rnib0 = B.ref_off[s] - a;            // nibble index of contig position 0
-    const GlobalRef refn{B.ref, rnib0};
-    uint4 *t4 = reinterpret_cast<uint4 *>(tab);
-    for (int k = lane; k < ((span + 15) >> 4); k += 64) t4[k] = make_uint4(0u, 0u, 0u, 0u);
-    if (lane < 2) obs.count[lane] = 0;
-    __syncthreads();
-    const int64_t i0 = B.incid_off[s], i1 = B.incid_off[s + 1];
-    bool rare = false;
-    for (int64_t c0 = i0; c0 < i1; c0 += 64) {
-      const int nh = (int)((i1 - c0) < 64 ? (i1 - c0) : 64);
-      int4 rec = make_int4(0, 0, 0, 0);
-      if (lane < nh) rec = inc_rec[c0 + lane];
-      const uint32_t fl = (uint32_t)rec.y;
-      const bool simple = (fl & kRecSimple) != 0;
-      const bool cplx = (fl & kRecCplx) != 0;
-      const uint64_t sm = __ballot(simple);
-      if (simple) {
-        const int idx = __popcll(sm & lanes_below(lane));
-        m_start[idx] = rec.x;
-        m_len[idx] = (int)(fl & 0xFFFFFF);
-        m_ds[idx] = (int)((fl >> 24) & 1);
-        m_mine[idx] = (fl & kRecMine) ? 1 : 0;
-        m_off[idx] = (int64_t)(((uint64_t)(uint32_t)rec.w << 32) | (uint32_t)rec.z);
-      }
-      __syncthreads();
-      const int ns = __popcll(sm);
-      for (int j0 = 0; j0 < ns; j0 += 4) {
-        const int j = j0 + (lane >> 4);
-        if (j >= ns) continue;
-        const int st = m_start[j], L = m_len[j], d = m_ds[j];
-        const bool mine = m_mine[j] != 0;
-        const int64_t snib = 2 * m_off[j];
-        for (int q0 = 16 * (lane & 15); q0 < L; q0 += 256) {
-          const uint64_t sv = load16(B.seq, snib + q0);
-          const uint64_t rv = load16(B.ref, rnib0 + st + q0);
-          const int nb = (L - q0) < 16 ? (L - q0) : 16;
-          // nibbles that differ from the reference (cheap pre-filter: usually none)
-          uint64_t diff = sv ^ rv;
-          diff = (diff | (diff >> 1) | (diff >> 2) | (diff >> 3)) & 0x1111111111111111ull;
-          if (nb < 16) diff &= (1ull << (4 * nb)) - 1;
-          while (diff) {
-            const int k = __builtin_ctzll(diff) >> 2;
-            diff &= diff - 1;
-            const int c = (int)((sv >> (4 * k)) & 15);
-            const int rc = (int)((rv >> (4 * k)) & 15);
-            rare |= observe(tab, obs, st + q0 + k - a, c, rc, d, mine, snib + q0 + k);
-          }
-        }
-      }
-      uint64_t cm = __ballot(cplx);
-      while (cm) {
-        const int l = __ffsll((unsigned long long)cm) - 1;
-        cm &= cm - 1;
-        const int r = __shfl(rec.x, l);
-        const bool mine = (__shfl((int)fl, l) & kRecMine) != 0;
-        const int L = B.read_len[r];
-        const int ds = B.dataset[r];
-        const int64_t snib = 2 * B.seq_off[r];
-        CigarCursor cur;
-        cur.init(B.cigar + B.cig_off[r], B.n_cig[r], B.ref_start[r]);
-        for (int q = lane; q < L; q += 64) {
-          const int p = cur.ref_of(q);
-          if (p < a || p >= b) continue;
-          rare |= observe(tab, obs, p - a, nib_at(B.seq, snib + q), refn(p), ds, mine, snib + q);
-        }
-      }
-      __syncthreads();
-    }
-    clear_keep<1>(B, s, a, b, tab);
-    __syncthreads();
-    int calls = 0;
-    for (int k = lane; k < ((span + 3) >> 2); k += 64) {
-      const uint32_t w = tab[k];
-      calls += __popc(w & (w >> 4) & 0x0F0F0F0Fu);
-    }
-    int bases = 0;
-    const int n_obs = obs.count[0] < kObsCap ? obs.count[0] : kObsCap;
-    if (!obs.count[1]) {
-      for (int e = lane; e < n_obs; e += 64) {
-        const uint32_t m = obs.meta[e];
-        if (!(m & (1u << 21))) continue;
-        const int off = (int)(m & 0xFFFF), c = (int)((m >> 16) & 15);
-        const uint32_t t = (tab[off >> 2] >> ((off & 3) * 8)) & 0xFF;
-        if (t & (t >> 4) & (uint32_t)c) {
-          patch_nibble(out, obs.nib[e], c, refn(a + off));
-          ++bases;
-        }
-      }
-    } else {
-      // more mismatches than the list holds: walk the reads this scope writes again
-      for (int64_t i = i0; i < i1; ++i) {
-        const int4 rec = inc_rec[i];
-        if (!(rec.y & kRecMine)) continue;
-        const int r = B.incid_read[i];
-        const int L = B.read_len[r];
-        const int64_t snib = 2 * B.seq_off[r];
-        CigarCursor cur;
-        cur.init(B.cigar + B.cig_off[r], B.n_cig[r], B.ref_start[r]);
-        for (int q = lane; q < L; q += 64) {
-          const int p = cur.ref_of(q);
-          if (p < a || p >= b) continue;
-          const int c = nib_at(B.seq, snib + q);
-          const int off = p - a;
-          const uint32_t t = (tab[off >> 2] >> ((off & 3) * 8)) & 0xFF;
-          if (is_acgt(c) && (t & (t >> 4) & (uint32_t)c)) {
-            patch_nibble(out, snib + q, c, refn(p));
-            ++bases;
-          }
-        }
-      }
-    }
-    for (int o = 32; o > 0; o >>= 1) {
-      calls += __shfl_xor(calls, o);
-      bases += __shfl_xor(bases, o);
-    }
-    const bool any_rare = __ballot(rare) != 0;
-    if (lane == 0) {
-      scope_calls[s] = calls;
-      scope_bases[s] = bases;
-      if (any_rare) rare_list[atomicAdd(rare_count, 1)] = s;
-    }
-    __syncthreads();
-  }
-}
-
-size_t v2_lds_bytes(int cap) {
-  return (size_t)cap + 64 * (4 * 4 + 8) + kObsCap * (4 + 8) + 16;
-}
-
-// ---- v3: persistent waves ------------------------------------------------------------------
-// v2's algorithm with the latency chain cut down: 256-thread workgroups whose four waves
-// work independently (wave-level sync only), a persistent grid in which every wave walks
-// its own stream of scopes and prefetches the next scope's 48-byte record while it works
-// on the current one, and simple reads spread over the lanes chunk by chunk (16 bases per
-// lane, chunk -> read by binary search over an LDS prefix array) so six 150 bp reads fill
-// one 64-lane pass. LDS per wave stays under 5 KB for the 2.5 K class (32 waves per CU).
-constexpr int kV3Obs = 96;
-
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-__host__ __device__ inline size_t v3_wave_lds_bytes(int cap) {
-  return (size_t)cap + 64 * 16 + 68 * 4 + kV3Obs * (4 + 8) + 16;
-}
-
 __device__ __forceinline__ int64_t i64_of(int lo, int hi) {
   return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
-}
-
-__global__ void __launch_bounds__(256) k_scope_v3(const DevBatch B, const int4 *__restrict__ srec, int n, int cap,
-                                                  const int4 *__restrict__ inc_rec, uint8_t *__restrict__ out,
-                                                  int32_t *scope_calls, int32_t *scope_bases, int32_t *rare_list,
-                                                  int32_t *rare_count) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  // wave index made provably wave-uniform: scope records then live in SGPRs (s_load)
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  uint32_t *base = smem + wave * (v3_wave_lds_bytes(cap) / 4);
-  uint32_t *tab = base;
-  int4 *mrec = reinterpret_cast<int4 *>(base + cap / 4);
-  int *mcs = reinterpret_cast<int *>(mrec + 64);
-  ObsList obs;
-  obs.meta = reinterpret_cast<uint32_t *>(mcs + 68);
-  obs.nib = reinterpret_cast<int64_t *>(obs.meta + kV3Obs);
-  obs.count = reinterpret_cast<int *>(obs.nib + kV3Obs);
-  obs.cap = kV3Obs;
-  const int nw = gridDim.x * 4;
-  int li = blockIdx.x * 4 + wave;
-  int4 ra = make_int4(0, 0, 0, 0), rb = ra, rc = ra;
-  if (li < n) {
-    ra = srec[3 * li];
-    rb = srec[3 * li + 1];
-    rc = srec[3 * li + 2];
-  }
-  while (li < n) {
-    const int nli = li + nw;
-    int4 na = make_int4(0, 0, 0, 0), nb = na, nc = na;
-    if (nli < n) {                                   // prefetch the next scope's record
-      na = srec[3 * nli];
-      nb = srec[3 * nli + 1];
-      nc = srec[3 * nli + 2];
-    }
-    const int s = ra.x, a = ra.y, span = ra.z, keep_pos = ra.w;
-    const int64_t i0 = i64_of(rb.x, rb.y);
-    const int ninc = rb.z, keep_code = rb.w;
-    const int64_t rnib0 = i64_of(rc.x, rc.y);      // nibble index of contig position 0
-    const int b = a + span;
-    const GlobalRef refn{B.ref, rnib0};
-    uint4 *t4 = reinterpret_cast<uint4 *>(tab);
-    for (int k = lane; k < ((span + 15) >> 4); k += 64) t4[k] = make_uint4(0u, 0u, 0u, 0u);
-    if (lane < 2) obs.count[lane] = 0;
-    wave_sync();
-    bool rare = false;
-    for (int c0 = 0; c0 < ninc; c0 += 64) {
-      const int nh = (ninc - c0) < 64 ? (ninc - c0) : 64;
-      int4 rec = make_int4(0, 0, 0, 0);
-      if (lane < nh) rec = inc_rec[i0 + c0 + lane];
-      const uint32_t fl = (uint32_t)rec.y;
-      const bool simple = (fl & kRecSimple) != 0;
-      const bool cplx = (fl & kRecCplx) != 0;
-      const int nck = simple ? (int)(((fl & 0xFFFFFF) + 15) >> 4) : 0;
-      int incl = nck;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const int t = __shfl_up(incl, o);
-        if (lane >= o) incl += t;
-      }
-      const int total = __shfl(incl, 63);
-      mrec[lane] = rec;
-      mcs[lane] = incl - nck;
-      wave_sync();
-      for (int t = lane; t < total; t += 64) {
-        int lo = 0, hi = 63;                         // largest j with mcs[j] <= t
-        while (lo < hi) {
-          const int mid = (lo + hi + 1) >> 1;
-          if (mcs[mid] <= t) lo = mid;
-          else hi = mid - 1;
-        }
-        const int4 r = mrec[lo];
-        const int q0 = 16 * (t - mcs[lo]);
-        const uint32_t rf = (uint32_t)r.y;
-        const int L = (int)(rf & 0xFFFFFF), d = (int)((rf >> 24) & 1);
-        const bool mine = (rf & kRecMine) != 0;
-        const int64_t snib = 2 * i64_of(r.z, r.w);
-        const uint64_t sv = load16(B.seq, snib + q0);
-        const uint64_t rv = load16(B.ref, rnib0 + r.x + q0);
-        const int nbase = (L - q0) < 16 ? (L - q0) : 16;
-        uint64_t diff = sv ^ rv;
-        diff = (diff | (diff >> 1) | (diff >> 2) | (diff >> 3)) & 0x1111111111111111ull;
-        if (nbase < 16) diff &= (1ull << (4 * nbase)) - 1;
-        while (diff) {
-          const int k = __builtin_ctzll(diff) >> 2;
-          diff &= diff - 1;
-          rare |= observe(tab, obs, r.x + q0 + k - a, (int)((sv >> (4 * k)) & 15), (int)((rv >> (4 * k)) & 15), d,
-                          mine, snib + q0 + k);
-        }
-      }
-      uint64_t cm = __ballot(cplx);
-      while (cm) {
-        const int l = __ffsll((unsigned long long)cm) - 1;
-        cm &= cm - 1;
-        const int r = __shfl(rec.x, l);
-        const bool mine = (__shfl((int)fl, l) & kRecMine) != 0;
-        const int L = B.read_len[r];
-        const int ds = B.dataset[r];
-        const int64_t snib = 2 * B.seq_off[r];
-        CigarCursor cur;
-        cur.init(B.cigar + B.cig_off[r], B.n_cig[r], B.ref_start[r]);
-        for (int q = lane; q < L; q += 64) {
-          const int p = cur.ref_of(q);
-          if (p < a || p >= b) continue;
-          rare |= observe(tab, obs, p - a, nib_at(B.seq, snib + q), refn(p), ds, mine, snib + q);
-        }
-      }
-      wave_sync();
-    }
-    if (lane == 0 && keep_pos >= a && keep_pos < b && is_acgt(keep_code)) {
-      const int off = keep_pos - a;
-      atomicAnd(&tab[off >> 2], ~((uint32_t)keep_code << ((off & 3) * 8)));
-    }
-    wave_sync();
-    int calls = 0;
-    for (int k = lane; k < ((span + 3) >> 2); k += 64) {
-      const uint32_t w = tab[k];
-      calls += __popc(w & (w >> 4) & 0x0F0F0F0Fu);
-    }
-    int bases = 0;
-    const int n_obs = obs.count[0] < kV3Obs ? obs.count[0] : kV3Obs;
-    if (obs.count[0] <= kV3Obs) {
-      for (int e = lane; e < n_obs; e += 64) {
-        const uint32_t m = obs.meta[e];
-        if (!(m & (1u << 21))) continue;
-        const int off = (int)(m & 0xFFFF), c = (int)((m >> 16) & 15);
-        const uint32_t t = (tab[off >> 2] >> ((off & 3) * 8)) & 0xFF;
-        if (t & (t >> 4) & (uint32_t)c) {
-          patch_nibble(out, obs.nib[e], c, refn(a + off));
-          ++bases;
-        }
-      }
-    } else {
-      // more mismatches than the list holds: walk the reads this scope writes again
-      for (int64_t i = i0; i < i0 + ninc; ++i) {
-        const int4 rec = inc_rec[i];
-        if (!(rec.y & kRecMine)) continue;
-        const int r = B.incid_read[i];
-        const int L = B.read_len[r];
-        const int64_t snib = 2 * B.seq_off[r];
-        CigarCursor cur;
-        cur.init(B.cigar + B.cig_off[r], B.n_cig[r], B.ref_start[r]);
-        for (int q = lane; q < L; q += 64) {
-          const int p = cur.ref_of(q);
-          if (p < a || p >= b) continue;
-          const int c = nib_at(B.seq, snib + q);
-          const int off = p - a;
-          const uint32_t t = (tab[off >> 2] >> ((off & 3) * 8)) & 0xFF;
-          if (is_acgt(c) && (t & (t >> 4) & (uint32_t)c)) {
-            patch_nibble(out, snib + q, c, refn(p));
-            ++bases;
-          }
-        }
-      }
-    }
-    for (int o = 32; o > 0; o >>= 1) {
-      calls += __shfl_xor(calls, o);
-      bases += __shfl_xor(bases, o);
-    }
-    const bool any_rare = __ballot(rare) != 0;
-    if (lane == 0) {
-      scope_calls[s] = calls;
-      scope_bases[s] = bases;
-      if (any_rare) rare_list[atomicAdd(rare_count, 1)] = s;
-    }
-    wave_sync();
-    ra = na;
-    rb = nb;
-    rc = nc;
-    li = nli;
-  }
 }
 
 // ---- 2-bit reference ----------------------------------------------------------------------
@@ -916,6 +270,7 @@ __device__ __forceinline__ uint64_t expand2(uint32_t x) {
   return (v & ~m) | ((v << 2) & m);
 }
 
+
 // ---- group kernels: scope groups, observation lists ---------------------------------------
 // No per-scope table and no per-scope serialization. At upload every read of a small scope is
 // cut into segments (one per aligned M/=/X run: query nibble index, reference nibble index,
@@ -948,22 +303,11 @@ constexpr int kGrpThreads = 256;
 #define GANON_K2_BLOCKS 6   // resident workgroups per CU the K = 2 instance is compiled for
 #endif
 constexpr int kGrpTile = 256;        // segment records staged per tile
-constexpr int kGrpTarget = 256;      // segments per group (a larger scope forms its own group)
-constexpr int kGrpObs = 512;         // observations per LDS list
-constexpr int kGrpMaxScopes = 256;   // scopes per group (12-bit local index field)
 constexpr int kGrpStack = 80;        // key ranges pending (bisection depth <= 64)
 constexpr int kGrpPatch = 512;       // in-partition masks of one list pass (<= its observations)
 constexpr int kGrpMap = 4096;        // chunk -> segment map entries (larger tiles binary-search)
 constexpr int kGrpQuad = 256;        // lists up to this size are matched without sorting
-constexpr int kGrpMaxSpan = 1 << 20; // widest scope of the group kernels (20-bit position field)
 constexpr unsigned long long kEmpty = ~0ull;
-constexpr int64_t kPartAlign = 128;  // partition boundaries fall on whole lines
-constexpr int kGrpRec = 5;           // int4 records per group (layout at k_group)
-// segment record (int4, 16 bytes): x = query nibble bits 0-31, y = reference nibble bits 0-31,
-// z = query nibble bits 32-39 | reference nibble bits 32-39 << 8 | length << 16 (14 bits) |
-// dataset << 30 | mine << 31, w = scope_local | (pos - span_start) << 12
-constexpr int kSegMaxLen = (1 << 14) - 1;   // longer aligned runs are cut into pieces at upload
-constexpr uint32_t kSegMine = 1u << 31;     // the segment's read is written by this scope
 constexpr unsigned long long kNibMask = (1ull << 48) - 1;
 // key-range pass: observations to the LDS list, overflow to the group's global region
 enum { kModeCollect = 0 };
@@ -1000,18 +344,6 @@ struct GrpRange {
   int mode;
 };
 
-// Where a masked base goes.
-// Rarely used outputs and scratch of the group kernels, read through one pointer (device
-// memory) so that their addresses do not occupy scalar registers for the whole kernel.
-struct GrpAux {
-  int32_t *scope_calls, *scope_bases, *part;   // per-scope counts; per-workgroup partial totals
-  unsigned long long *far;                      // fused: masks of bytes outside the partition
-  int *far_count;
-  int64_t far_cap;
-  unsigned long long *okey, *opay, *tkey;       // overflow regions (GrpGlobal)
-  unsigned int *tflag;
-};
-
 struct PatchSink {
   uint8_t *out;
   int64_t p0, p1, q0, q1;           // fused: this workgroup's partition pieces of out (bytes)
@@ -1026,8 +358,8 @@ __device__ __forceinline__ void sink_patch(GrpShared &sh, const PatchSink &k, in
   if (k.fused) {
     const int64_t byte = nib >> 1;
     if (!k.inside(byte)) {
-      const int i = atomicAdd(k.aux->far_count, 1);
-      if (i < k.aux->far_cap) k.aux->far[i] = e;
+      const unsigned long long i = atomicAdd(k.aux->far_count, 1ull);
+      if (i < (unsigned long long)k.aux->far_cap) k.aux->far[i] = e;
       return;
     }
     if (k.lds) {
@@ -1540,6 +872,8 @@ __global__ void __launch_bounds__(kGrpThreads, (U == 1 ? 6 : U == 2 ? GANON_K2_B
     // (grp_scan ends on a barrier)
     if (skip & kSkipClassify) continue;
     const int n = sh.n_obs;
+    if (tid == 0 && n > kGrpQuad)   // path counters (ganon_batch_path_counts): sorted list, region, split
+      atomicAdd(&aux->paths[n <= kGrpObs ? 0 : n <= gg.cap ? 1 : 2], 1ull);
     if (n > kGrpObs) {
       if (n <= gg.cap) {
         // the list joins the region's tail: n observations contiguous in the region
@@ -1601,17 +935,19 @@ __global__ void __launch_bounds__(kGrpThreads, (U == 1 ? 6 : U == 2 ? GANON_K2_B
 // workgroups' partials plus the wide scopes' counts, reduced per workgroup into acc; the last
 // workgroup to finish (ticket acc[2]) writes totals = static values + sums + rare counts and
 // resets acc and counters for the next run — no memset or copy is launched per run.
-// counters: [0] rare small scopes, [1] rare tiles, [2] far masks.
+// counters: [0] rare small scopes (unused), [1] rare tiles; far_count: far masks.
 __global__ void __launch_bounds__(kBlock) k_finish(const unsigned long long *__restrict__ far, int64_t far_cap,
                                                    uint8_t *__restrict__ out, const int32_t *__restrict__ grp_part,
                                                    int n_groups, const int32_t *__restrict__ large_ids, int n_large,
                                                    const int32_t *__restrict__ scope_calls,
                                                    const int32_t *__restrict__ scope_bases,
                                                    const unsigned long long *__restrict__ static_totals,
-                                                   int32_t *counters, unsigned long long *acc,
+                                                   int32_t *counters, unsigned long long *far_count,
+                                                   int32_t *status, unsigned long long *acc,
                                                    unsigned long long *totals) {
   const int64_t gtid = blockIdx.x * (int64_t)kBlock + threadIdx.x, gstride = (int64_t)gridDim.x * kBlock;
-  const int64_t n_far = min((int64_t)counters[2], far_cap);
+  const unsigned long long far_n = *far_count;
+  const int64_t n_far = far_n < (unsigned long long)far_cap ? (int64_t)far_n : far_cap;
   for (int64_t i = gtid; i < n_far; i += gstride) {
     const unsigned long long e = far[i];
     const int64_t nib = (int64_t)(e >> 4);
@@ -1659,9 +995,10 @@ __global__ void __launch_bounds__(kBlock) k_finish(const unsigned long long *__r
   totals[GANON_T_MASKED_SNV_CALLS] += sc;
   totals[GANON_T_MASKED_BASES] += sb;
   totals[GANON_T_RARE_SCOPES] += (unsigned long long)(atomicExch(&counters[0], 0) + atomicExch(&counters[1], 0));
-  atomicExch(&counters[2], 0);
+  // more far masks than the planned capacity (cannot happen for a batch planned at upload): the
+  // masks past it were dropped — download reports the run as failed instead of unmasked bases
+  if (atomicExch(far_count, 0ull) > (unsigned long long)far_cap) atomicOr(status, 1);
 }
-
 // One workgroup per 16 Ki-position tile of a large scope: tally -> TN table (global).
 template <int TB>
 __global__ void __launch_bounds__(kBlock) k_tile_large(const DevBatch B, const Tile *__restrict__ tiles,
@@ -1757,137 +1094,314 @@ __global__ void __launch_bounds__(kBlock) k_mask_large(const DevBatch B, const i
   }
 }
 
-// Totals: per-scope counts of the scopes in ids (all n scopes when ids is null) plus the
-// (calls, bases) partials of the group kernel's workgroups.
-__global__ void __launch_bounds__(kBlock) k_totals(const int32_t *__restrict__ calls, const int32_t *__restrict__ bases,
-                                                   const int32_t *__restrict__ ids, int n,
-                                                   const int32_t *__restrict__ grp_part, int n_part,
-                                                   const int32_t *rare_small, const int32_t *rare_tiles,
-                                                   unsigned long long *totals) {
-  long long c = 0, b = 0;
-  for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
-    const int s = ids ? ids[i] : i;
-    c += calls[s];
-    b += bases[s];
-  }
-  for (int i = blockIdx.x * kBlock + threadIdx.x; i < n_part; i += gridDim.x * kBlock) {
-    c += grp_part[2 * i];
-    b += grp_part[2 * i + 1];
-  }
-  // one same-address atomic per workgroup: they serialize at the memory side
-  __shared__ long long part[2][kWaves];
-  for (int o = 32; o > 0; o >>= 1) {
-    c += __shfl_xor(c, o);
-    b += __shfl_xor(b, o);
-  }
-  if ((threadIdx.x & 63) == 0) {
-    part[0][threadIdx.x >> 6] = c;
-    part[1][threadIdx.x >> 6] = b;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    c = b = 0;
-    for (int w = 0; w < kWaves; ++w) {
-      c += part[0][w];
-      b += part[1][w];
-    }
-    if (c) atomicAdd(&totals[GANON_T_MASKED_SNV_CALLS], (unsigned long long)c);
-    if (b) atomicAdd(&totals[GANON_T_MASKED_BASES], (unsigned long long)b);
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0)
-    atomicAdd(&totals[GANON_T_RARE_SCOPES], (unsigned long long)(*rare_small + *rare_tiles));
-}
-
 }  // namespace
-
 // ---- host side ---------------------------------------------------------------------------
 
 using ganon_detail::check_launch;
 using ganon_detail::fail;
 using ganon_detail::KernelScope;
 
-struct ganon_dbatch {
-  DevBatch B{};
-  std::vector<void *> allocs;
-  int32_t n_reads = 0, n_scopes = 0;
-  int64_t seq_bytes = 0;
-  uint8_t *out = nullptr;
-  int32_t *scope_calls = nullptr, *scope_bases = nullptr;
-  unsigned long long *totals = nullptr, *static_totals = nullptr;
-  int32_t *counters = nullptr;  // [0] rare small count, [1] rare tile count
-  int32_t *small_list[2] = {nullptr, nullptr};
-  int32_t n_small[2] = {0, 0};
-  int32_t *pt_list = nullptr;
-  int32_t n_pt = 0;
-  Tile *tiles = nullptr;
-  int32_t n_tiles = 0;
-  int32_t *large_incid = nullptr;
-  int64_t *tab_off = nullptr;
-  uint16_t *tn_tab = nullptr;
-  int64_t tn_entries = 0;
-  int32_t *large_written = nullptr;
-  int32_t n_large_written = 0;
-  int32_t n_large_scopes = 0;
-  int32_t *rare_small_list = nullptr, *rare_tile_list = nullptr;
-  int32_t max_small_span = 0;
-  int4 *inc_rec = nullptr;      // per incidence, scope-major: {start|read, len|flags, seq_off lo, hi}
-  int4 *srec[2] = {nullptr, nullptr};   // per small scope of each class: 3 x int4 (k_scope_v3)
-  int4 *groups = nullptr;               // k_group: 2 x int4 per group
-  int4 *seg4 = nullptr;                 // k_group: segment records (16 bytes, layout at kSegMine)
-  int32_t n_groups = 0;
-  int64_t n_seg = 0;
-  unsigned long long *acc = nullptr;    // k_finish: calls, bases, workgroup ticket
-  uint32_t *ref2 = nullptr;             // 2-bit reference (k_ref2)
-  unsigned long long *far = nullptr;    // fused: masks outside the masking group's partition
-  int64_t far_cap = 0;
-  int32_t *grp_part = nullptr;          // k_group: (calls, bases) per workgroup
-  int32_t *large_ids = nullptr;         // scopes of the tile path under the group variants (huge)
-  GrpAux *aux = nullptr;                // k_group's rarely used pointers (device copy)
-  unsigned long long *gokey = nullptr, *gopay = nullptr, *gtkey = nullptr;   // group overflow regions
-  unsigned int *gtflag = nullptr;
-  Tile *tiles_h = nullptr;              // tiles / written reads of huge scopes (group variants)
-  int32_t *large_written_h = nullptr;
-  int32_t n_tiles_h = 0, n_large_written_h = 0, n_huge_scopes = 0;
-  bool ran = false;
-};
-
 namespace {
 
+size_t tile_lds_bytes(int tb) { return (size_t)kTile * tb + kTile / 2 + 16 * sizeof(int); }
 
-template <typename T>
-int dev_alloc(ganon_ctx *ctx, ganon_dbatch *db, T **p, size_t count) {
-  *p = nullptr;
-  // +128 bytes: the group kernels load up to 68 bytes from a chunk start past a buffer's last nibble,
-  // and the patch
-  // atomics touch whole dwords
-  size_t bytes = std::max<size_t>(count, 1) * sizeof(T) + 128;
-  hipError_t e = hipMalloc(reinterpret_cast<void **>(p), bytes);
-  if (e != hipSuccess) return fail(ctx, GANON_E_NOMEM, "hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
-  db->allocs.push_back(*p);
-  return GANON_OK;
+void free_buf(DBuf &b) {
+  if (b.p) hipFree(b.p);
+  b = DBuf{};
 }
 
-template <typename T>
-int dev_copy(ganon_ctx *ctx, ganon_dbatch *db, T **p, const T *src, size_t count) {
-  int rc = dev_alloc(ctx, db, p, count);
-  if (rc) return rc;
-  if (count) {
-    hipError_t e = hipMemcpyAsync(*p, src, count * sizeof(T), hipMemcpyHostToDevice, ctx->stream);
-    if (e != hipSuccess) return fail(ctx, GANON_E_DEVICE, "hipMemcpyAsync H2D failed: %s", hipGetErrorString(e));
-  }
-  return GANON_OK;
+void free_ref(ganon_ref *r) {
+  if (!r) return;
+  if (r->nt16) hipFree(r->nt16);
+  if (r->ref2) hipFree(r->ref2);
+  if (r->bad) hipFree(r->bad);
+  delete r;
+}
+
+void free_huge(ganon_dbatch *db) {
+  for (void *p : db->huge_allocs) hipFree(p);
+  db->huge_allocs.clear();
+  db->tiles_h = nullptr;
+  db->large_incid = db->large_written_h = db->large_ids = db->rare_tile_list = nullptr;
+  db->tab_off = nullptr;
+  db->tn_tab = nullptr;
+  db->n_tiles_h = db->n_large_written_h = 0;
+  db->tn_entries = 0;
 }
 
 void free_batch(ganon_dbatch *db) {
-  for (void *p : db->allocs) hipFree(p);
-  db->allocs.clear();
+  DBuf *bufs[] = {&db->b_ref_start, &db->b_read_len, &db->b_seq_off, &db->b_cig_off, &db->b_n_cig, &db->b_dataset,
+                  &db->b_write_scope, &db->b_seq, &db->b_cigar, &db->b_incid_off, &db->b_incid_read,
+                  &db->b_span_start, &db->b_span_len, &db->b_ref_off, &db->b_keep_pos, &db->b_keep_code,
+                  &db->b_read_end, &db->b_rseg, &db->b_rbase, &db->b_seen, &db->b_cost, &db->b_cost_scan, &db->b_gid,
+                  &db->b_gs0, &db->b_lo, &db->b_lo_idx, &db->b_lo_sorted, &db->b_lo_idx_sorted, &db->b_groups,
+                  &db->b_seg4, &db->b_grp_part, &db->b_far, &db->b_gokey, &db->b_gopay, &db->b_gtkey, &db->b_gtflag,
+                  &db->b_scan_tmp, &db->b_out, &db->b_scope_calls, &db->b_scope_bases, &db->b_small};
+  for (DBuf *b : bufs) free_buf(*b);
+  free_huge(db);
+  free_ref(db->own_ref);
+  db->own_ref = nullptr;
 }
 
-size_t small_lds_bytes(int tb, int cap) {
-  return (size_t)cap * tb + (((size_t)cap / 2 + 15) & ~(size_t)15) + 16 * sizeof(int);
+// Grow b to count elements and enqueue the copy of src (async on the stream).
+template <typename T>
+int h2d(ganon_ctx *ctx, DBuf &b, const T *src, size_t count, const T **field) {
+  T *p = nullptr;
+  int rc = ganon_prep::grow_n(ctx, b, count, &p);
+  if (rc) return rc;
+  if (count) {
+    hipError_t e = hipMemcpyAsync(p, src, count * sizeof(T), hipMemcpyHostToDevice, ctx->stream);
+    if (e != hipSuccess) return fail(ctx, GANON_E_DEVICE, "hipMemcpyAsync H2D failed: %s", hipGetErrorString(e));
+  }
+  *field = p;
+  return GANON_OK;
 }
 
-size_t tile_lds_bytes(int tb) { return (size_t)kTile * tb + kTile / 2 + 16 * sizeof(int); }
+template <typename T>
+int dmalloc(ganon_ctx *ctx, std::vector<void *> &allocs, T **p, size_t count) {
+  *p = nullptr;
+  const size_t bytes = std::max<size_t>(count, 1) * sizeof(T) + 128;
+  hipError_t e = hipMalloc(reinterpret_cast<void **>(p), bytes);
+  if (e != hipSuccess) return fail(ctx, GANON_E_NOMEM, "hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
+  allocs.push_back(*p);
+  return GANON_OK;
+}
+
+int ref_create(ganon_ctx *ctx, const uint8_t *nt16, int64_t bytes, ganon_ref **out) {
+  *out = nullptr;
+  if (bytes < 0 || (bytes > 0 && !nt16)) return fail(ctx, GANON_E_ARG, "bad reference buffer");
+  if (2 * bytes >= (int64_t(1) << 40)) return fail(ctx, GANON_E_ARG, "reference over 2^40 bases");
+  ganon_ref *r = new ganon_ref();
+  r->bytes = bytes;
+  r->n_blk = (bytes + 31) / 32;
+  const int64_t n_words = (2 * bytes + 15) / 16;
+  const int64_t n_bad = (r->n_blk + 63) / 64 + 1;
+  hipError_t e = hipMalloc(reinterpret_cast<void **>(&r->nt16), (size_t)bytes + 128);
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&r->ref2), (size_t)(n_words + 2) * 4 + 128);
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&r->bad), (size_t)n_bad * 8 + 128);
+  if (e != hipSuccess) {
+    free_ref(r);
+    return fail(ctx, GANON_E_NOMEM, "reference allocation failed: %s", hipGetErrorString(e));
+  }
+  if (bytes) e = hipMemcpyAsync(r->nt16, nt16, (size_t)bytes, hipMemcpyHostToDevice, ctx->stream);
+  if (e == hipSuccess) e = hipMemsetAsync(r->nt16 + bytes, 0, 128, ctx->stream);
+  if (e != hipSuccess) {
+    free_ref(r);
+    return fail(ctx, GANON_E_DEVICE, "reference copy failed: %s", hipGetErrorString(e));
+  }
+  int rc = GANON_OK;
+  if (n_words) {
+    k_ref2<<<(int)std::min<int64_t>((n_words + kBlock - 1) / kBlock, 16384), kBlock, 0, ctx->stream>>>(r->nt16, n_words,
+                                                                                                    r->ref2);
+    rc = check_launch(ctx, "k_ref2");
+  }
+  if (!rc) rc = ganon_ref_blocks(ctx, r);
+  if (!rc && hipStreamSynchronize(ctx->stream) != hipSuccess) rc = fail(ctx, GANON_E_DEVICE, "reference upload sync failed");
+  if (rc) {
+    free_ref(r);
+    return rc;
+  }
+  *out = r;
+  return GANON_OK;
+}
+
+// bam_endpos of read r from the host batch (huge-scope planning only).
+int32_t host_read_end(const ganon_batch *b, int32_t r) {
+  int64_t rl = 0;
+  for (int k = 0; k < b->n_cig[r]; ++k) {
+    const uint32_t w = b->cigar[b->cig_off[r] + k];
+    const int op = w & 0xF;
+    if (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) rl += w >> 4;
+  }
+  return (int32_t)(b->ref_start[r] + (rl > 0 ? rl : 1));
+}
+
+// Scopes wider than kGrpMaxSpan (whole-contig union scopes of very deep samples; none in the
+// benchmark configs): 16 Ki-position tiles planned on the host from the scopes' incidences.
+int plan_huge(ganon_ctx *ctx, ganon_dbatch *db, const ganon_batch *b) {
+  free_huge(db);
+  if (!db->n_huge_scopes) return GANON_OK;
+  std::vector<int32_t> large_incid, ids, written;
+  std::vector<int64_t> tab_off((size_t)b->n_scopes, -1);
+  std::vector<Tile> tiles;
+  int64_t tn_entries = 0;
+  for (int32_t s = 0; s < b->n_scopes; ++s) {
+    const int32_t sl = b->scope_span_len[s];
+    if (sl <= kGrpMaxSpan) continue;
+    ids.push_back(s);
+    tab_off[s] = tn_entries;
+    tn_entries += sl;
+    const int64_t base = (int64_t)large_incid.size();
+    for (int64_t i = b->scope_incid_off[s]; i < b->scope_incid_off[s + 1]; ++i) large_incid.push_back(b->incid_read[i]);
+    std::stable_sort(large_incid.begin() + base, large_incid.end(),
+                     [&](int32_t x, int32_t y) { return b->ref_start[x] < b->ref_start[y]; });
+    int32_t maxspan = 1;
+    for (int64_t i = base; i < (int64_t)large_incid.size(); ++i) {
+      const int32_t r = large_incid[i];
+      maxspan = std::max(maxspan, host_read_end(b, r) - b->ref_start[r]);
+    }
+    const int32_t ss = b->scope_span_start[s];
+    for (int64_t a = ss; a < (int64_t)ss + sl; a += kTile) {
+      Tile t{};
+      t.scope = s;
+      t.a = (int32_t)a;
+      t.b = (int32_t)std::min<int64_t>(a + kTile, (int64_t)ss + sl);
+      auto first = large_incid.begin() + base;
+      auto last = large_incid.end();
+      t.lo = std::lower_bound(first, last, (int64_t)t.a - maxspan,
+                              [&](int32_t r, int64_t key) { return (int64_t)b->ref_start[r] < key; }) -
+             large_incid.begin();
+      t.hi = std::lower_bound(first, last, (int64_t)t.b,
+                              [&](int32_t r, int64_t key) { return (int64_t)b->ref_start[r] < key; }) -
+             large_incid.begin();
+      tiles.push_back(t);
+    }
+  }
+  for (int32_t r = 0; r < b->n_reads; ++r) {
+    const int32_t ws = b->write_scope[r];
+    if (ws >= 0 && b->scope_span_len[ws] > kGrpMaxSpan) written.push_back(r);
+  }
+  int rc;
+  auto up = [&](auto **p, const auto &v) -> int {
+    using T = std::remove_const_t<std::remove_reference_t<decltype(v[0])>>;
+    T *q = nullptr;
+    int c = dmalloc(ctx, db->huge_allocs, &q, v.size());
+    if (c) return c;
+    if (!v.empty() && hipMemcpyAsync(q, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
+      return fail(ctx, GANON_E_DEVICE, "huge-scope plan copy failed");
+    *p = q;
+    return GANON_OK;
+  };
+  if ((rc = up(&db->tiles_h, tiles)) || (rc = up(&db->large_incid, large_incid)) || (rc = up(&db->tab_off, tab_off)) ||
+      (rc = up(&db->large_written_h, written)) || (rc = up(&db->large_ids, ids)))
+    return rc;
+  if ((rc = dmalloc(ctx, db->huge_allocs, &db->rare_tile_list, tiles.size()))) return rc;
+  db->n_tiles_h = (int32_t)tiles.size();
+  db->n_large_written_h = (int32_t)written.size();
+  db->tn_entries = tn_entries;
+  return GANON_OK;
+}
+
+// Copy a host batch into db (grow-only buffers), validate and plan it on the device.
+int load_batch(ganon_ctx *ctx, ganon_dbatch *db, const ganon_batch *b, const ganon_ref *shared) {
+  if (b->n_reads < 0 || b->n_scopes < 0 || b->n_incid < 0 || b->seq_bytes < 0 || b->n_cigar_ops < 0 || b->ref_bytes < 0)
+    return fail(ctx, GANON_E_ARG, "negative size in batch");
+  if (b->n_reads > 0 && (!b->ref_start || !b->read_len || !b->seq_off || !b->cig_off || !b->n_cig || !b->dataset ||
+                         !b->write_scope))
+    return fail(ctx, GANON_E_ARG, "null read array");
+  if (b->seq_bytes > 0 && !b->seq_nt16) return fail(ctx, GANON_E_ARG, "null seq_nt16");
+  if (b->n_cigar_ops > 0 && !b->cigar) return fail(ctx, GANON_E_ARG, "null cigar");
+  if (!b->scope_incid_off) return fail(ctx, GANON_E_ARG, "null scope_incid_off");
+  if (b->n_scopes > 0 && (!b->scope_span_start || !b->scope_span_len || !b->scope_ref_off || !b->keep_pos ||
+                          !b->keep_code))
+    return fail(ctx, GANON_E_ARG, "null scope array");
+  if (b->n_incid > 0 && !b->incid_read) return fail(ctx, GANON_E_ARG, "null incid_read");
+  if (!shared && b->ref_bytes > 0 && !b->ref_nt16) return fail(ctx, GANON_E_ARG, "null ref_nt16");
+  if (b->scope_incid_off[0] != 0 || b->scope_incid_off[b->n_scopes] != b->n_incid)
+    return fail(ctx, GANON_E_ARG, "scope_incid_off must start at 0 and end at n_incid");
+  if (2 * b->seq_bytes >= (int64_t(1) << 39)) return fail(ctx, GANON_E_ARG, "sequence over 2^39 bases");
+  if (b->n_incid >= INT32_MAX) return fail(ctx, GANON_E_ARG, "more than 2^31-1 incidences");
+  int rc;
+  HIP_OR_FAIL(hipStreamSynchronize(ctx->stream));   // a previous run of db may still read its buffers
+  db->ran = false;
+  if (shared) {
+    db->ref = shared;
+  } else {
+    free_ref(db->own_ref);
+    db->own_ref = nullptr;
+    if ((rc = ref_create(ctx, b->ref_nt16, b->ref_bytes, &db->own_ref))) return rc;
+    db->ref = db->own_ref;
+  }
+  db->n_reads = b->n_reads;
+  db->n_scopes = b->n_scopes;
+  db->n_incid = b->n_incid;
+  db->seq_bytes = b->seq_bytes;
+  db->n_cigar_ops = b->n_cigar_ops;
+  db->group_target = ctx->group_target;
+  DevBatch &D = db->B;
+  if ((rc = h2d(ctx, db->b_ref_start, b->ref_start, b->n_reads, &D.ref_start)) ||
+      (rc = h2d(ctx, db->b_read_len, b->read_len, b->n_reads, &D.read_len)) ||
+      (rc = h2d(ctx, db->b_seq_off, b->seq_off, b->n_reads, &D.seq_off)) ||
+      (rc = h2d(ctx, db->b_cig_off, b->cig_off, b->n_reads, &D.cig_off)) ||
+      (rc = h2d(ctx, db->b_n_cig, b->n_cig, b->n_reads, &D.n_cig)) ||
+      (rc = h2d(ctx, db->b_dataset, b->dataset, b->n_reads, &D.dataset)) ||
+      (rc = h2d(ctx, db->b_write_scope, b->write_scope, b->n_reads, &D.write_scope)) ||
+      (rc = h2d(ctx, db->b_seq, b->seq_nt16, b->seq_bytes, &D.seq)) ||
+      (rc = h2d(ctx, db->b_cigar, b->cigar, b->n_cigar_ops, &D.cigar)) ||
+      (rc = h2d(ctx, db->b_incid_off, b->scope_incid_off, (size_t)b->n_scopes + 1, &D.incid_off)) ||
+      (rc = h2d(ctx, db->b_incid_read, b->incid_read, b->n_incid, &D.incid_read)) ||
+      (rc = h2d(ctx, db->b_span_start, b->scope_span_start, b->n_scopes, &D.span_start)) ||
+      (rc = h2d(ctx, db->b_span_len, b->scope_span_len, b->n_scopes, &D.span_len)) ||
+      (rc = h2d(ctx, db->b_ref_off, b->scope_ref_off, b->n_scopes, &D.ref_off)) ||
+      (rc = h2d(ctx, db->b_keep_pos, b->keep_pos, b->n_scopes, &D.keep_pos)) ||
+      (rc = h2d(ctx, db->b_keep_code, b->keep_code, b->n_scopes, &D.keep_code)))
+    return rc;
+  D.ref = db->ref->nt16;
+  D.ref2 = db->ref->ref2;
+  // small device state: totals, static totals, acc, far count, plan info (u64); counters, status;
+  // the first validation error; the group kernels' aux pointers
+  constexpr size_t kU64 = 8 + 8 + 4 + 1 + 4 + 4;
+  constexpr size_t kSmallBytes = kU64 * 8 + 8 * 4 + sizeof(PrepErr) + sizeof(GrpAux) + 64;
+  uint8_t *sm = nullptr;
+  if ((rc = ganon_prep::grow_n(ctx, db->b_small, kSmallBytes, &sm))) return rc;
+  auto *u = reinterpret_cast<unsigned long long *>(sm);
+  db->totals = u;
+  db->static_totals = u + 8;
+  db->acc = u + 16;
+  db->far_count = u + 20;
+  db->plan_info = u + 21;
+  db->paths = u + 25;
+  db->counters = reinterpret_cast<int32_t *>(u + kU64);
+  db->status = db->counters + 4;
+  db->err = reinterpret_cast<PrepErr *>(sm + kU64 * 8 + 8 * 4);
+  db->aux = reinterpret_cast<GrpAux *>(sm + kU64 * 8 + 8 * 4 + sizeof(PrepErr));
+  HIP_OR_FAIL(hipMemsetAsync(sm, 0, kSmallBytes, ctx->stream));
+  if ((rc = ganon_prep::grow_n(ctx, db->b_scope_calls, b->n_scopes, &db->scope_calls)) ||
+      (rc = ganon_prep::grow_n(ctx, db->b_scope_bases, b->n_scopes, &db->scope_bases)) ||
+      (rc = ganon_prep::grow_n(ctx, db->b_out, b->seq_bytes, &db->out)))
+    return rc;
+  // bytes outside every read are never written by the masking kernels: make them defined
+  HIP_OR_FAIL(hipMemsetAsync(db->out, 0, (size_t)b->seq_bytes + 16, ctx->stream));
+  if ((rc = ganon_prep::plan(ctx, db))) return rc;
+  if ((rc = plan_huge(ctx, db, b))) return rc;
+  const GrpAux a{db->scope_calls,
+                 db->scope_bases,
+                 static_cast<int32_t *>(db->b_grp_part.p),
+                 static_cast<unsigned long long *>(db->b_far.p),
+                 db->far_count,
+                 db->far_cap,
+                 db->paths,
+                 static_cast<unsigned long long *>(db->b_gokey.p),
+                 static_cast<unsigned long long *>(db->b_gopay.p),
+                 static_cast<unsigned long long *>(db->b_gtkey.p),
+                 static_cast<unsigned int *>(db->b_gtflag.p)};
+  unsigned long long st[GANON_N_TOTALS] = {0};
+  st[GANON_T_READS_IN] = (unsigned long long)b->n_reads;
+  st[GANON_T_READS_WRITTEN] = (unsigned long long)db->n_written;
+  st[GANON_T_SCOPES] = (unsigned long long)b->n_scopes;
+  st[GANON_T_LARGE_TILES] = (unsigned long long)db->n_tiles_h;
+  // (both from stack memory: synchronized below before returning)
+  HIP_OR_FAIL(hipMemcpyAsync(db->aux, &a, sizeof a, hipMemcpyHostToDevice, ctx->stream));
+  HIP_OR_FAIL(hipMemcpyAsync(db->static_totals, st, sizeof st, hipMemcpyHostToDevice, ctx->stream));
+  HIP_OR_FAIL(hipStreamSynchronize(ctx->stream));
+  return GANON_OK;
+}
+
+int upload_common(ganon_ctx *ctx, const ganon_batch *b, const ganon_ref *ref, ganon_dbatch **out) {
+  if (!ctx || !b || !out) return fail(ctx, GANON_E_ARG, "null argument");
+  *out = nullptr;
+  HIP_OR_FAIL(hipSetDevice(ctx->device));
+  ganon_dbatch *db = new ganon_dbatch();
+  int rc = load_batch(ctx, db, b, ref);
+  if (rc) {
+    hipStreamSynchronize(ctx->stream);
+    free_batch(db);
+    delete db;
+    return rc;
+  }
+  *out = db;
+  return GANON_OK;
+}
 
 }  // namespace
 
@@ -1909,27 +1423,10 @@ GANON_API int ganon_ctx_create(int device, ganon_ctx **out) {
     return GANON_E_DEVICE;
   }
   ctx->stream = ctx->own;
-  // Every kernel gets the LDS its worst class needs.
-  hipFuncSetAttribute(reinterpret_cast<const void *>(k_scope_small<1>), hipFuncAttributeMaxDynamicSharedMemorySize,
-                      (int)small_lds_bytes(1, kSmallCap1));
-  hipFuncSetAttribute(reinterpret_cast<const void *>(k_scope_small<4>), hipFuncAttributeMaxDynamicSharedMemorySize,
-                      (int)small_lds_bytes(4, kSmallCap1));
   hipFuncSetAttribute(reinterpret_cast<const void *>(k_tile_large<1>), hipFuncAttributeMaxDynamicSharedMemorySize,
                       (int)tile_lds_bytes(1));
   hipFuncSetAttribute(reinterpret_cast<const void *>(k_tile_large<4>), hipFuncAttributeMaxDynamicSharedMemorySize,
                       (int)tile_lds_bytes(4));
-  hipFuncSetAttribute(reinterpret_cast<const void *>(k_scope_v3), hipFuncAttributeMaxDynamicSharedMemorySize,
-                      (int)(4 * v3_wave_lds_bytes(kSmallCap1)));
-  // persistent grid of k_scope_v3: every resident workgroup slot, no more
-  const int caps[2] = {kSmallCap0, kSmallCap1};
-  for (int k = 0; k < 2; ++k) {
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_scope_v3, kBlock, 4 * v3_wave_lds_bytes(caps[k])) !=
-            hipSuccess ||
-        per_cu < 1)
-      per_cu = 1;
-    ctx->v3_blocks[k] = per_cu * prop.multiProcessorCount;
-  }
   *out = ctx;
   return GANON_OK;
 }
@@ -1959,8 +1456,10 @@ GANON_API int ganon_ctx_set_stream(ganon_ctx *ctx, void *hip_stream) {
 }
 
 GANON_API int ganon_ctx_set_variant(ganon_ctx *ctx, int variant) {
-  if (!ctx || variant < GANON_VARIANT_DEFAULT || variant > GANON_VARIANT_PERSIST)
-    return fail(ctx, GANON_E_ARG, "unknown kernel variant %d", variant);
+  if (!ctx) return GANON_E_ARG;
+  if (variant != GANON_VARIANT_DEFAULT && variant != GANON_VARIANT_GROUP_FUSED)
+    return fail(ctx, GANON_E_ARG, "kernel variant %d was retired: the fused group kernel is the only small-scope path",
+                variant);
   ctx->variant = variant;
   return GANON_OK;
 }
@@ -2013,505 +1512,42 @@ GANON_API int ganon_ctx_set_profiling(ganon_ctx *ctx, int enabled) {
   return GANON_OK;
 }
 
-static int validate(ganon_ctx *ctx, const ganon_batch *b, std::vector<int32_t> &read_end) {
-  if (b->n_reads < 0 || b->n_scopes < 0 || b->n_incid < 0 || b->seq_bytes < 0 || b->n_cigar_ops < 0 ||
-      b->ref_bytes < 0)
-    return fail(ctx, GANON_E_ARG, "negative size in batch");
-  if (b->n_reads > 0 && (!b->ref_start || !b->read_len || !b->seq_off || !b->cig_off || !b->n_cig ||
-                         !b->dataset || !b->write_scope))
-    return fail(ctx, GANON_E_ARG, "null read array");
-  if (b->seq_bytes > 0 && !b->seq_nt16) return fail(ctx, GANON_E_ARG, "null seq_nt16");
-  if (b->n_cigar_ops > 0 && !b->cigar) return fail(ctx, GANON_E_ARG, "null cigar");
-  if (!b->scope_incid_off) return fail(ctx, GANON_E_ARG, "null scope_incid_off");
-  if (b->n_scopes > 0 && (!b->scope_span_start || !b->scope_span_len || !b->scope_ref_off || !b->keep_pos ||
-                          !b->keep_code))
-    return fail(ctx, GANON_E_ARG, "null scope array");
-  if (b->n_incid > 0 && !b->incid_read) return fail(ctx, GANON_E_ARG, "null incid_read");
-  if (b->ref_bytes > 0 && !b->ref_nt16) return fail(ctx, GANON_E_ARG, "null ref_nt16");
-  read_end.assign(b->n_reads, 0);
-  for (int32_t r = 0; r < b->n_reads; ++r) {
-    const int64_t L = b->read_len[r];
-    if (L < 0 || b->seq_off[r] < 0 || b->seq_off[r] + (L + 1) / 2 > b->seq_bytes)
-      return fail(ctx, GANON_E_ARG, "read %d: sequence out of range", r);
-    if (b->n_cig[r] < 0 || b->cig_off[r] < 0 || b->cig_off[r] + b->n_cig[r] > b->n_cigar_ops)
-      return fail(ctx, GANON_E_ARG, "read %d: cigar out of range", r);
-    if (b->dataset[r] > 1) return fail(ctx, GANON_E_ARG, "read %d: dataset must be 0 or 1", r);
-    if (b->write_scope[r] < -1 || b->write_scope[r] >= b->n_scopes)
-      return fail(ctx, GANON_E_ARG, "read %d: write_scope out of range", r);
-    int64_t rl = 0;
-    for (int k = 0; k < b->n_cig[r]; ++k) {
-      const uint32_t w = b->cigar[b->cig_off[r] + k];
-      const int op = w & 0xF;
-      if (op > 8) return fail(ctx, GANON_E_ARG, "read %d: bad cigar op %d", r, op);
-      if (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) rl += w >> 4;
-    }
-    if (b->ref_start[r] < 0 || b->ref_start[r] + rl > INT32_MAX) return fail(ctx, GANON_E_ARG, "read %d: bad position", r);
-    read_end[r] = (int32_t)(b->ref_start[r] + (rl > 0 ? rl : 1));
+GANON_API int ganon_ref_upload(ganon_ctx *ctx, const uint8_t *ref_nt16, int64_t ref_bytes, ganon_ref **out) {
+  if (!ctx || !out) return fail(ctx, GANON_E_ARG, "null argument");
+  HIP_OR_FAIL(hipSetDevice(ctx->device));
+  return ref_create(ctx, ref_nt16, ref_bytes, out);
+}
+
+GANON_API int ganon_ref_free(ganon_ctx *ctx, ganon_ref *ref) {
+  if (!ref) return GANON_E_ARG;
+  if (ctx) {
+    hipSetDevice(ctx->device);
+    hipStreamSynchronize(ctx->stream);
   }
-  if (b->scope_incid_off[0] != 0 || b->scope_incid_off[b->n_scopes] != b->n_incid)
-    return fail(ctx, GANON_E_ARG, "scope_incid_off must start at 0 and end at n_incid");
-  std::vector<uint8_t> seen(b->n_reads, 0);
-  for (int32_t s = 0; s < b->n_scopes; ++s) {
-    const int64_t i0 = b->scope_incid_off[s], i1 = b->scope_incid_off[s + 1];
-    if (i1 < i0) return fail(ctx, GANON_E_ARG, "scope %d: decreasing incidence offsets", s);
-    const int64_t ss = b->scope_span_start[s], sl = b->scope_span_len[s];
-    if (sl < 0 || ss < 0) return fail(ctx, GANON_E_ARG, "scope %d: bad span", s);
-    if (b->scope_ref_off[s] < 0 || b->scope_ref_off[s] + sl > 2 * b->ref_bytes)
-      return fail(ctx, GANON_E_ARG, "scope %d: reference slice out of range", s);
-    if (b->keep_code[s] > 15) return fail(ctx, GANON_E_ARG, "scope %d: keep_code > 15", s);
-    for (int64_t i = i0; i < i1; ++i) {
-      const int32_t r = b->incid_read[i];
-      if (r < 0 || r >= b->n_reads) return fail(ctx, GANON_E_ARG, "incidence %lld: read out of range", (long long)i);
-      if (b->ref_start[r] < ss || read_end[r] > ss + sl)
-        return fail(ctx, GANON_E_ARG, "scope %d: read %d [%d,%d) outside span [%lld,%lld)", s, r, b->ref_start[r],
-                    read_end[r], (long long)ss, (long long)(ss + sl));
-      if (b->write_scope[r] == s) seen[r] = 1;
-    }
-  }
-  for (int32_t r = 0; r < b->n_reads; ++r)
-    if (b->write_scope[r] >= 0 && !seen[r])
-      return fail(ctx, GANON_E_ARG, "read %d: write_scope %d does not contain it", r, b->write_scope[r]);
+  free_ref(ref);
   return GANON_OK;
 }
 
 GANON_API int ganon_batch_upload(ganon_ctx *ctx, const ganon_batch *b, ganon_dbatch **out) {
-  if (!ctx || !b || !out) return fail(ctx, GANON_E_ARG, "null argument");
-  *out = nullptr;
+  return upload_common(ctx, b, nullptr, out);
+}
+
+GANON_API int ganon_batch_upload_ref(ganon_ctx *ctx, const ganon_batch *b, const ganon_ref *ref, ganon_dbatch **out) {
+  if (!ref) return fail(ctx, GANON_E_ARG, "null reference");
+  return upload_common(ctx, b, ref, out);
+}
+
+GANON_API int ganon_batch_reload(ganon_ctx *ctx, ganon_dbatch *db, const ganon_batch *b) {
+  if (!ctx || !db || !b) return fail(ctx, GANON_E_ARG, "null argument");
   HIP_OR_FAIL(hipSetDevice(ctx->device));
-  std::vector<int32_t> read_end;
-  int rc = validate(ctx, b, read_end);
-  if (rc) return rc;
-  ganon_dbatch *db = new ganon_dbatch();
-  db->n_reads = b->n_reads;
-  db->n_scopes = b->n_scopes;
-  db->seq_bytes = b->seq_bytes;
-  auto bail = [&](int code) {
-    hipStreamSynchronize(ctx->stream);
-    free_batch(db);
-    delete db;
-    return code;
-  };
-  // ---- work lists (host) ----
-  std::vector<int32_t> small[2], pt, large_written, large_incid, large_scopes;
-  std::vector<int64_t> tab_off(b->n_scopes, -1);
-  std::vector<Tile> tiles;
-  int64_t tn_entries = 0;
-  for (int32_t s = 0; s < b->n_scopes; ++s) {
-    const int32_t sl = b->scope_span_len[s];
-    if (sl <= kSmallCap0) small[0].push_back(s);
-    else if (sl <= kSmallCap1) small[1].push_back(s);
-    else {
-      large_scopes.push_back(s);
-      tab_off[s] = tn_entries;
-      tn_entries += sl;
-      const int64_t i0 = b->scope_incid_off[s], i1 = b->scope_incid_off[s + 1];
-      const int64_t base = (int64_t)large_incid.size();
-      for (int64_t i = i0; i < i1; ++i) large_incid.push_back(b->incid_read[i]);
-      std::stable_sort(large_incid.begin() + base, large_incid.end(),
-                       [&](int32_t x, int32_t y) { return b->ref_start[x] < b->ref_start[y]; });
-      int32_t maxspan = 1;
-      for (int64_t i = base; i < (int64_t)large_incid.size(); ++i) {
-        const int32_t r = large_incid[i];
-        maxspan = std::max(maxspan, read_end[r] - b->ref_start[r]);
-      }
-      const int32_t ss = b->scope_span_start[s];
-      for (int64_t a = ss; a < (int64_t)ss + sl; a += kTile) {
-        Tile t{};
-        t.scope = s;
-        t.a = (int32_t)a;
-        t.b = (int32_t)std::min<int64_t>(a + kTile, (int64_t)ss + sl);
-        auto first = large_incid.begin() + base;
-        auto last = large_incid.end();
-        const int64_t lo_key = (int64_t)t.a - maxspan;
-        t.lo = std::lower_bound(first, last, lo_key,
-                                [&](int32_t r, int64_t key) { return (int64_t)b->ref_start[r] < key; }) -
-               large_incid.begin();
-        t.hi = std::lower_bound(first, last, (int64_t)t.b,
-                                [&](int32_t r, int64_t key) { return (int64_t)b->ref_start[r] < key; }) -
-               large_incid.begin();
-        tiles.push_back(t);
-      }
-    }
+  const ganon_ref *shared = db->own_ref ? nullptr : db->ref;
+  int rc = load_batch(ctx, db, b, shared);
+  if (rc) {
+    // the device batch holds a partial load: only free or reload is valid now
+    db->n_groups = 0;
+    db->ran = false;
   }
-  for (int32_t r = 0; r < b->n_reads; ++r) {
-    const int32_t ws = b->write_scope[r];
-    if (ws < 0) pt.push_back(r);
-    else if (tab_off[ws] >= 0) large_written.push_back(r);
-  }
-  int32_t max_small = 0;
-  for (auto s : small[0]) max_small = std::max(max_small, b->scope_span_len[s]);
-  for (auto s : small[1]) max_small = std::max(max_small, b->scope_span_len[s]);
-  // ---- device copies ----
-  DevBatch &D = db->B;
-#define COPY(field, src, n)                                                                       \
-  do {                                                                                            \
-    using T_ = std::remove_const_t<std::remove_pointer_t<decltype(D.field)>>;                     \
-    T_ *q_ = nullptr;                                                                             \
-    if ((rc = dev_copy(ctx, db, &q_, reinterpret_cast<const T_ *>(src), (size_t)(n)))) return bail(rc); \
-    D.field = q_;                                                                                 \
-  } while (0)
-  COPY(ref_start, b->ref_start, b->n_reads);
-  COPY(read_len, b->read_len, b->n_reads);
-  COPY(read_end, read_end.data(), b->n_reads);
-  COPY(n_cig, b->n_cig, b->n_reads);
-  COPY(write_scope, b->write_scope, b->n_reads);
-  COPY(seq_off, b->seq_off, b->n_reads);
-  COPY(cig_off, b->cig_off, b->n_reads);
-  COPY(seq, b->seq_nt16, b->seq_bytes);
-  COPY(dataset, b->dataset, b->n_reads);
-  COPY(cigar, b->cigar, b->n_cigar_ops);
-  COPY(incid_off, b->scope_incid_off, (size_t)b->n_scopes + 1);
-  COPY(incid_read, b->incid_read, b->n_incid);
-  COPY(span_start, b->scope_span_start, b->n_scopes);
-  COPY(span_len, b->scope_span_len, b->n_scopes);
-  COPY(keep_pos, b->keep_pos, b->n_scopes);
-  COPY(ref_off, b->scope_ref_off, b->n_scopes);
-  COPY(ref, b->ref_nt16, b->ref_bytes);
-  COPY(keep_code, b->keep_code, b->n_scopes);
-#undef COPY
-  for (int k = 0; k < 2; ++k) {
-    if ((rc = dev_copy(ctx, db, &db->small_list[k], small[k].data(), small[k].size()))) return bail(rc);
-    db->n_small[k] = (int32_t)small[k].size();
-  }
-  if ((rc = dev_copy(ctx, db, &db->pt_list, pt.data(), pt.size()))) return bail(rc);
-  db->n_pt = (int32_t)pt.size();
-  if ((rc = dev_copy(ctx, db, &db->tiles, tiles.data(), tiles.size()))) return bail(rc);
-  db->n_tiles = (int32_t)tiles.size();
-  if ((rc = dev_copy(ctx, db, &db->large_incid, large_incid.data(), large_incid.size()))) return bail(rc);
-  if ((rc = dev_copy(ctx, db, &db->tab_off, tab_off.data(), tab_off.size()))) return bail(rc);
-  // the tile path's TN table (2 bytes per position of every wide scope) is allocated on the
-  // first run that uses it: under the group variants only scopes over kGrpMaxSpan tile
-  db->tn_entries = tn_entries;
-  if ((rc = dev_copy(ctx, db, &db->large_written, large_written.data(), large_written.size()))) return bail(rc);
-  db->n_large_written = (int32_t)large_written.size();
-  db->n_large_scopes = (int32_t)large_scopes.size();
-  {
-    // the group kernels take every scope up to kGrpMaxSpan positions; only wider ("huge")
-    // scopes keep the tile path under the group variants
-    std::vector<Tile> tiles_h;
-    std::vector<int32_t> written_h, ids_h;
-    for (const Tile &t : tiles)
-      if (b->scope_span_len[t.scope] > kGrpMaxSpan) tiles_h.push_back(t);
-    for (int32_t r : large_written)
-      if (b->scope_span_len[b->write_scope[r]] > kGrpMaxSpan) written_h.push_back(r);
-    for (int32_t x : large_scopes)
-      if (b->scope_span_len[x] > kGrpMaxSpan) ids_h.push_back(x);
-    if ((rc = dev_copy(ctx, db, &db->tiles_h, tiles_h.data(), tiles_h.size()))) return bail(rc);
-    if ((rc = dev_copy(ctx, db, &db->large_written_h, written_h.data(), written_h.size()))) return bail(rc);
-    if ((rc = dev_copy(ctx, db, &db->large_ids, ids_h.data(), ids_h.size()))) return bail(rc);
-    db->n_tiles_h = (int32_t)tiles_h.size();
-    db->n_large_written_h = (int32_t)written_h.size();
-    db->n_huge_scopes = (int32_t)ids_h.size();
-  }
-  db->max_small_span = max_small;
-  {
-    // per-incidence records for the v2 scope kernel (scope-major, one int4 each)
-    std::vector<int4> rec((size_t)b->n_incid);
-    for (int32_t s = 0; s < b->n_scopes; ++s) {
-      for (int64_t i = b->scope_incid_off[s]; i < b->scope_incid_off[s + 1]; ++i) {
-        const int32_t r = b->incid_read[i];
-        const int32_t L = b->read_len[r];
-        bool simple = false;
-        if (b->n_cig[r] == 1) {
-          const uint32_t w = b->cigar[b->cig_off[r]];
-          const int op = w & 0xF;
-          simple = (op == 0 || op == 7 || op == 8) && (int64_t)(w >> 4) == L && L > 0;
-        }
-        const bool cplx = !simple && b->n_cig[r] > 0 && L > 0;
-        if (L >= (1 << 24)) return bail(fail(ctx, GANON_E_ARG, "read %d longer than 16 Mb", r));
-        uint32_t fl = (uint32_t)L | ((uint32_t)b->dataset[r] << 24);
-        if (simple) fl |= kRecSimple;
-        if (cplx) fl |= kRecCplx;
-        if (b->write_scope[r] == s) fl |= kRecMine;
-        const uint64_t so = (uint64_t)b->seq_off[r];
-        rec[i] = make_int4(simple ? b->ref_start[r] : r, (int)fl, (int)(uint32_t)so, (int)(uint32_t)(so >> 32));
-      }
-    }
-    if ((rc = dev_copy(ctx, db, &db->inc_rec, rec.data(), rec.size()))) return bail(rc);
-    for (int k = 0; k < 2; ++k) {
-      std::vector<int4> sr(3 * small[k].size());
-      for (size_t j = 0; j < small[k].size(); ++j) {
-        const int32_t s = small[k][j];
-        const int64_t i0 = b->scope_incid_off[s];
-        const int64_t ni = b->scope_incid_off[s + 1] - i0;
-        if (ni >= INT32_MAX) return bail(fail(ctx, GANON_E_ARG, "scope %d has too many reads", s));
-        const int64_t nib0 = b->scope_ref_off[s] - b->scope_span_start[s];
-        sr[3 * j] = make_int4(s, b->scope_span_start[s], b->scope_span_len[s], b->keep_pos[s]);
-        sr[3 * j + 1] = make_int4((int)(uint32_t)i0, (int)(uint32_t)((uint64_t)i0 >> 32), (int)ni, b->keep_code[s]);
-        sr[3 * j + 2] = make_int4((int)(uint32_t)nib0, (int)(uint32_t)((uint64_t)nib0 >> 32), 0, 0);
-      }
-      if ((rc = dev_copy(ctx, db, &db->srec[k], sr.data(), sr.size()))) return bail(rc);
-    }
-  }
-  {
-    // group kernels: aligned segments of every read of every small scope, scope-major, packed
-    // into groups of consecutive scopes; groups launch in the order of their written reads in
-    // the sequence buffer, each owning the 128-byte-aligned partition of out from its first
-    // written read to the next group's (fused variant)
-    if (2 * b->seq_bytes >= (int64_t(1) << 40) || 2 * b->ref_bytes >= (int64_t(1) << 40))
-      return bail(fail(ctx, GANON_E_ARG, "sequence or reference over 2^40 bases"));
-    std::vector<int4> s4;
-    s4.reserve((size_t)b->n_incid);
-    auto lo32 = [](int64_t v) { return (int)(uint32_t)(uint64_t)v; };
-    auto hi32 = [](int64_t v) { return (int)(uint32_t)((uint64_t)v >> 32); };
-    struct G {
-      int32_t s0, s1;
-      int64_t i0, i1, first;   // first: lowest seq_off of a read the group writes
-      int64_t mid;             // segments [i0, mid) have an all-ACGT reference range
-      int64_t bases;           // aligned bases of its segments (sizes the overflow region)
-    };
-    std::vector<G> gs;
-    int32_t g_s0 = -1;
-    int64_t g_i0 = 0, g_first = INT64_MAX;
-    // 64-base reference blocks holding a non-ACGT code (N, IUPAC, '='), for the clean/dirty split
-    const int64_t n_blk = (b->ref_bytes + 31) / 32;
-    std::vector<uint8_t> bad_blk((size_t)n_blk, 0);
-    {
-      uint8_t ok[256];
-      for (int v = 0; v < 256; ++v) ok[v] = ((0x116 >> (v >> 4)) & 1) && ((0x116 >> (v & 15)) & 1);
-      const int nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-      std::vector<std::thread> th;
-      for (int t = 0; t < nt; ++t)
-        th.emplace_back([&, t] {
-          for (int64_t k = t; k < n_blk; k += nt) {
-            const int64_t e = std::min<int64_t>(32 * k + 32, b->ref_bytes);
-            uint8_t bad = 0;
-            for (int64_t x = 32 * k; x < e; ++x) bad |= !ok[b->ref_nt16[x]];
-            bad_blk[k] = bad;
-          }
-        });
-      for (auto &x : th) x.join();
-    }
-    auto ref_clean = [&](int64_t rnib, int64_t n) {
-      for (int64_t k = rnib >> 6; k <= (rnib + n - 1) >> 6; ++k)
-        if (k >= n_blk || bad_blk[k]) return false;
-      return true;
-    };
-    std::vector<int4> c4, d4;   // the open group's segments: clean, dirty reference
-    auto close_group = [&](int32_t s_end) {
-      if (g_s0 < 0) return;
-      int64_t bases = 0;
-      for (const int4 &x : c4) bases += ((uint32_t)x.z >> 16) & kSegMaxLen;
-      for (const int4 &x : d4) bases += ((uint32_t)x.z >> 16) & kSegMaxLen;
-      s4.insert(s4.end(), c4.begin(), c4.end());
-      const int64_t mid = (int64_t)s4.size();
-      s4.insert(s4.end(), d4.begin(), d4.end());
-      c4.clear();
-      d4.clear();
-      gs.push_back(G{g_s0, s_end, g_i0, (int64_t)s4.size(), g_first, mid, bases});
-      g_s0 = -1;
-      g_first = INT64_MAX;
-    };
-    auto segments_of = [&](int32_t r, auto &&emit) {
-      const int64_t L = b->read_len[r];
-      int64_t q = 0, p = b->ref_start[r];
-      for (int k = 0; k < b->n_cig[r] && q < L; ++k) {
-        const uint32_t w = b->cigar[b->cig_off[r] + k];
-        const int op = w & 0xF;
-        const int64_t len = w >> 4;
-        if (op == 0 || op == 7 || op == 8) {
-          const int64_t n = std::min(len, L - q);
-          for (int64_t o = 0; o < n; o += kSegMaxLen) emit(q + o, p + o, std::min<int64_t>(kSegMaxLen, n - o));
-          q += len;
-          p += len;
-        } else if (op == 1 || op == 4) {
-          q += len;
-        } else if (op == 2 || op == 3) {
-          p += len;
-        }
-      }
-    };
-    for (int32_t s = 0; s < b->n_scopes; ++s) {
-      if (b->scope_span_len[s] > kGrpMaxSpan) continue;   // huge scope: tile path
-      const int64_t i0 = b->scope_incid_off[s], i1 = b->scope_incid_off[s + 1];
-      int64_t nseg = 0;
-      for (int64_t i = i0; i < i1; ++i) segments_of(b->incid_read[i], [&](int64_t, int64_t, int64_t) { ++nseg; });
-      if (g_s0 >= 0 && ((int64_t)(c4.size() + d4.size()) + nseg > ctx->group_target || s - g_s0 >= kGrpMaxScopes))
-        close_group(s);
-      if (g_s0 < 0) {
-        g_s0 = s;
-        g_i0 = (int64_t)s4.size();
-      }
-      const int64_t ref0 = b->scope_ref_off[s] - b->scope_span_start[s];
-      for (int64_t i = i0; i < i1; ++i) {
-        const int32_t r = b->incid_read[i];
-        if (b->read_len[r] >= (1 << 24)) return bail(fail(ctx, GANON_E_ARG, "read %d longer than 16 Mb", r));
-        uint32_t fl = (uint32_t)b->dataset[r] << 30;
-        if (b->write_scope[r] == s) {
-          fl |= kSegMine;
-          g_first = std::min(g_first, b->seq_off[r]);
-        }
-        const int64_t qnib = 2 * b->seq_off[r];
-        segments_of(r, [&](int64_t q, int64_t p, int64_t n) {
-          const bool clean = ref_clean(ref0 + p, n);
-          const uint64_t sq = (uint64_t)(qnib + q), rf = (uint64_t)(ref0 + p);
-          const uint32_t z = (uint32_t)((sq >> 32) & 0xFF) | ((uint32_t)((rf >> 32) & 0xFF) << 8) |
-                             ((uint32_t)n << 16) | fl;
-          // scope span <= kGrpMaxSpan = 2^20 positions
-          const uint32_t pos_off = (uint32_t)(p - b->scope_span_start[s]);
-          (clean ? c4 : d4).push_back(make_int4((int)(uint32_t)sq, (int)(uint32_t)rf, (int)z,
-                                                (int)((uint32_t)(s - g_s0) | (pos_off << 12))));
-        });
-      }
-    }
-    close_group(b->n_scopes);
-    const int32_t ng = (int32_t)gs.size();
-    // partition pieces: the sequence buffer in byte order is a sequence of runs of written reads
-    // owned by one group (a group's written reads are contiguous per dataset when each dataset's
-    // reads are stored in position order — the product layout is every tumor read, then every
-    // normal read, so a group has one run per dataset). Each group keeps its two largest runs as
-    // pieces; any other run (a read at a group boundary) joins the piece before it. The pieces
-    // tile [0, seq_bytes) at 128-byte boundaries; bytes of a read outside its group's pieces
-    // are masked through the far list.
-    std::vector<int32_t> scope_grp((size_t)b->n_scopes, -1);
-    for (int32_t k = 0; k < ng; ++k)
-      for (int32_t s = gs[k].s0; s < gs[k].s1; ++s)
-        if (b->scope_span_len[s] <= kGrpMaxSpan) scope_grp[s] = k;
-    auto owner_of = [&](int32_t r) -> int32_t {
-      const int32_t ws = b->write_scope[r];
-      return (ws < 0 || b->read_len[r] == 0) ? -1 : scope_grp[ws];
-    };
-    std::vector<int32_t> byoff;
-    byoff.reserve((size_t)b->n_reads);
-    bool sorted = true;
-    for (int32_t r = 0; r < b->n_reads; ++r) {
-      if (owner_of(r) < 0) continue;
-      if (!byoff.empty() && b->seq_off[r] < b->seq_off[byoff.back()]) sorted = false;
-      byoff.push_back(r);
-    }
-    if (!sorted)
-      std::stable_sort(byoff.begin(), byoff.end(), [&](int32_t x, int32_t y) { return b->seq_off[x] < b->seq_off[y]; });
-    struct Run {
-      int64_t start;
-      int32_t owner;
-    };
-    std::vector<Run> runs;
-    for (int32_t r : byoff) {
-      const int32_t g = owner_of(r);
-      if (runs.empty() || runs.back().owner != g) runs.push_back(Run{b->seq_off[r], g});
-    }
-    // each group's two largest runs (bytes up to the next run)
-    auto run_len = [&](int64_t i) {
-      return ((size_t)i + 1 < runs.size() ? runs[(size_t)i + 1].start : b->seq_bytes) - runs[(size_t)i].start;
-    };
-    std::vector<int64_t> best((size_t)ng * 2, -1);
-    for (int64_t i = 0; i < (int64_t)runs.size(); ++i) {
-      int64_t *bb = &best[2 * (size_t)runs[(size_t)i].owner];
-      const int64_t len = run_len(i);
-      if (bb[0] < 0 || len > run_len(bb[0])) {
-        bb[1] = bb[0];
-        bb[0] = i;
-      } else if (bb[1] < 0 || len > run_len(bb[1])) {
-        bb[1] = i;
-      }
-    }
-    std::vector<Run> pieces;
-    for (int64_t i = 0; i < (int64_t)runs.size(); ++i) {
-      const int32_t g = runs[(size_t)i].owner;
-      if (best[2 * (size_t)g] != i && best[2 * (size_t)g + 1] != i) continue;
-      const int64_t c = pieces.empty() ? 0 : std::min(runs[(size_t)i].start, b->seq_bytes) / kPartAlign * kPartAlign;
-      if (!pieces.empty() && c <= pieces.back().start) pieces.back().owner = g;   // the previous piece is empty
-      else pieces.push_back(Run{c, g});
-    }
-    std::vector<int64_t> pc((size_t)ng * 4, 0);   // per group: piece A [0], [1); piece B [2], [3)
-    std::vector<int64_t> first((size_t)ng, INT64_MAX);
-    for (size_t i = 0; i < pieces.size(); ++i) {
-      const int32_t g = pieces[i].owner;
-      const int64_t e = i + 1 < pieces.size() ? pieces[i + 1].start : b->seq_bytes;
-      int64_t *q = &pc[4 * (size_t)g];
-      const int slot = first[g] == INT64_MAX ? 0 : 2;   // at most two pieces per group
-      q[slot] = pieces[i].start;
-      q[slot + 1] = e;
-      first[g] = std::min(first[g], pieces[i].start);
-    }
-    if (pieces.empty() && ng) {   // no written read in a small scope: the first group copies it all
-      pc[0] = 0;
-      pc[1] = b->seq_bytes;
-      first[0] = 0;
-    }
-    std::vector<int32_t> order(ng);
-    for (int32_t k = 0; k < ng; ++k) order[k] = k;
-    std::stable_sort(order.begin(), order.end(), [&](int32_t x, int32_t y) { return first[x] < first[y]; });
-    // exact bound on masks landing outside the masking group's pieces: every nibble of a
-    // written read that lies outside them
-    int64_t far_cap = 0;
-    for (int32_t r : byoff) {
-      const int64_t *q = &pc[4 * (size_t)owner_of(r)];
-      const int64_t r0 = b->seq_off[r], r1 = r0 + ((int64_t)b->read_len[r] + 1) / 2;
-      const int64_t in = std::max<int64_t>(0, std::min(r1, q[1]) - std::max(r0, q[0])) +
-                         std::max<int64_t>(0, std::min(r1, q[3]) - std::max(r0, q[2]));
-      far_cap += 2 * ((r1 - r0) - in);
-    }
-    // overflow regions: (bases / 48 + kGrpObs) observations per group, i.e. up to ~2 % of its
-    // aligned bases mismatching (more: key-range halving)
-    std::vector<int4> grp(kGrpRec * (size_t)ng);
-    int64_t region = 0;
-    for (int32_t k = 0; k < ng; ++k) {
-      const G &g = gs[order[k]];
-      const int64_t *q = &pc[4 * (size_t)order[k]];
-      const int64_t cap = std::min<int64_t>(g.bases / 48 + kGrpObs, INT32_MAX / 2);
-      grp[kGrpRec * k] = make_int4(g.s0, g.s1, lo32(g.i0), hi32(g.i0));
-      grp[kGrpRec * k + 1] = make_int4(lo32(g.i1), hi32(g.i1), lo32(g.mid), hi32(g.mid));
-      grp[kGrpRec * k + 2] = make_int4(lo32(q[0]), hi32(q[0]), lo32(q[1]), hi32(q[1]));
-      grp[kGrpRec * k + 3] = make_int4(lo32(region), hi32(region), (int)cap, 0);
-      grp[kGrpRec * k + 4] = make_int4(lo32(q[2]), hi32(q[2]), lo32(q[3]), hi32(q[3]));
-      region += cap;
-    }
-    if ((rc = dev_alloc(ctx, db, &db->gokey, (size_t)region))) return bail(rc);
-    if ((rc = dev_alloc(ctx, db, &db->gopay, (size_t)region))) return bail(rc);
-    if ((rc = dev_alloc(ctx, db, &db->gtkey, 2 * (size_t)region + 64))) return bail(rc);
-    if ((rc = dev_alloc(ctx, db, &db->gtflag, 2 * (size_t)region + 64))) return bail(rc);
-    if ((rc = dev_copy(ctx, db, &db->groups, grp.data(), grp.size()))) return bail(rc);
-    if ((rc = dev_copy(ctx, db, &db->seg4, s4.data(), s4.size()))) return bail(rc);
-    db->n_groups = ng;
-    if ((rc = dev_alloc(ctx, db, &db->grp_part, 2 * (size_t)ng))) return bail(rc);
-    db->n_seg = (int64_t)s4.size();
-    db->far_cap = far_cap;
-    if ((rc = dev_alloc(ctx, db, &db->far, (size_t)far_cap))) return bail(rc);
-    const int64_t n_words = (2 * b->ref_bytes + 15) / 16;
-    if ((rc = dev_alloc(ctx, db, &db->ref2, (size_t)n_words + 2))) return bail(rc);
-    if (n_words) {
-      k_ref2<<<(int)std::min<int64_t>((n_words + kBlock - 1) / kBlock, 16384), kBlock, 0, ctx->stream>>>(
-          D.ref, n_words, db->ref2);
-      if ((rc = check_launch(ctx, "k_ref2"))) return bail(rc);
-    }
-    D.ref2 = db->ref2;
-  }
-  if ((rc = dev_alloc(ctx, db, &db->out, (size_t)b->seq_bytes))) return bail(rc);
-  // bytes outside every read are never written by the fused variant: make them defined
-  if (hipMemsetAsync(db->out, 0, (size_t)b->seq_bytes + 16, ctx->stream) != hipSuccess)
-    return bail(fail(ctx, GANON_E_DEVICE, "hipMemsetAsync(out) failed"));
-  if ((rc = dev_alloc(ctx, db, &db->scope_calls, (size_t)b->n_scopes))) return bail(rc);
-  if ((rc = dev_alloc(ctx, db, &db->scope_bases, (size_t)b->n_scopes))) return bail(rc);
-  if ((rc = dev_alloc(ctx, db, &db->totals, GANON_N_TOTALS))) return bail(rc);
-  if ((rc = dev_alloc(ctx, db, &db->counters, 4))) return bail(rc);
-  if ((rc = dev_alloc(ctx, db, &db->acc, 3))) return bail(rc);
-  {
-    const GrpAux a{db->scope_calls, db->scope_bases, db->grp_part, db->far, db->counters + 2, db->far_cap,
-                   db->gokey, db->gopay, db->gtkey, db->gtflag};
-    if ((rc = dev_copy(ctx, db, &db->aux, &a, 1))) return bail(rc);
-  }
-  // k_finish keeps these zero between runs
-  if (hipMemsetAsync(db->counters, 0, 4 * sizeof(int32_t), ctx->stream) != hipSuccess ||
-      hipMemsetAsync(db->acc, 0, 3 * sizeof(unsigned long long), ctx->stream) != hipSuccess)
-    return bail(fail(ctx, GANON_E_DEVICE, "hipMemsetAsync(counters) failed"));
-  if ((rc = dev_alloc(ctx, db, &db->rare_small_list, small[0].size() + small[1].size()))) return bail(rc);
-  if ((rc = dev_alloc(ctx, db, &db->rare_tile_list, tiles.size()))) return bail(rc);
-  unsigned long long st[GANON_N_TOTALS] = {0};
-  int64_t written = 0;
-  for (int32_t r = 0; r < b->n_reads; ++r) written += b->write_scope[r] >= 0;
-  st[GANON_T_READS_IN] = (unsigned long long)b->n_reads;
-  st[GANON_T_READS_WRITTEN] = (unsigned long long)written;
-  st[GANON_T_SCOPES] = (unsigned long long)b->n_scopes;
-  st[GANON_T_LARGE_TILES] = (unsigned long long)tiles.size();
-  if ((rc = dev_copy(ctx, db, &db->static_totals, st, GANON_N_TOTALS))) return bail(rc);
-  hipError_t e = hipStreamSynchronize(ctx->stream);
-  if (e != hipSuccess) {
-    fail(ctx, GANON_E_DEVICE, "upload sync failed: %s", hipGetErrorString(e));
-    return bail(GANON_E_DEVICE);
-  }
-  *out = db;
-  return GANON_OK;
+  return rc;
 }
 
 GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
@@ -2526,127 +1562,60 @@ GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
   DevBatch B = db->B;
   if (!ctx->ref2) B.ref2 = nullptr;   // group kernels then read the nt16 reference only
   int rc;
-  const bool v3 = ctx->variant == GANON_VARIANT_PERSIST;
-  const bool v2 = ctx->variant == GANON_VARIANT_COPYPATCH;
-  const bool v5 = ctx->variant == GANON_VARIANT_DEFAULT || ctx->variant == GANON_VARIANT_GROUP_FUSED;
-  const bool v4 = ctx->variant == GANON_VARIANT_GROUP || v5;   // group kernels
-  if (!v4) {
-    // group variants leave counters zero and write totals in k_finish
-    HIP_OR_FAIL(hipMemsetAsync(db->counters, 0, 4 * sizeof(int32_t), st));
-    HIP_OR_FAIL(hipMemcpyAsync(db->totals, db->static_totals, GANON_N_TOTALS * sizeof(unsigned long long),
-                               hipMemcpyDeviceToDevice, st));
-  }
-  const Tile *tiles = v4 ? db->tiles_h : db->tiles;
-  const int32_t n_tiles = v4 ? db->n_tiles_h : db->n_tiles;
-  const int32_t *large_written = v4 ? db->large_written_h : db->large_written;
-  const int32_t n_large_written = v4 ? db->n_large_written_h : db->n_large_written;
-  if (v4 ? db->n_huge_scopes : db->n_large_scopes) {
-    // wide scopes are counted with atomics (tiles)
+  // 1. derived layer from the raw SoA
+  if ((rc = ganon_prep::run(ctx, db))) return rc;
+  if (db->n_huge_scopes) {
+    // huge scopes are counted with atomics (tiles)
     HIP_OR_FAIL(hipMemsetAsync(db->scope_calls, 0, (size_t)db->n_scopes * sizeof(int32_t), st));
     HIP_OR_FAIL(hipMemsetAsync(db->scope_bases, 0, (size_t)db->n_scopes * sizeof(int32_t), st));
   }
-  if (v5 && db->n_groups) {
-    // the fused group kernel writes every byte of out (its partitions tile [0, seq_bytes))
-  } else if (v2 || v3 || v4) {
-    // copy-then-patch: every read's bytes first, the scope kernels patch masked nibbles
-    KernelScope ks(ctx, "copy_seq");
-    if (db->seq_bytes) HIP_OR_FAIL(hipMemcpyAsync(db->out, B.seq, (size_t)db->seq_bytes, hipMemcpyDeviceToDevice, st));
-  } else if (db->n_pt) {
-    KernelScope ks(ctx, "k_passthrough");
-    const int grid = std::min<int>((db->n_pt + kWaves - 1) / kWaves, 8192);
-    k_passthrough<<<grid, kBlock, 0, st>>>(B, db->pt_list, db->n_pt, db->out);
-    if ((rc = check_launch(ctx, "k_passthrough"))) return rc;
-  }
-  if (v4 && db->n_groups) {
-    KernelScope ks(ctx, v5 ? "k_group_fused" : "k_group");
+  // 2. masking: the fused group kernel writes every byte of out (its pieces tile [0, seq_bytes))
+  if (db->n_groups) {
+    KernelScope ks(ctx, "k_group_fused");
     const int u = ctx->group_unroll;
-    auto kern = v5 ? (u == 2 ? k_group<2, true> : u == 4 ? k_group<4, true> : u == 8 ? k_group<8, true>
-                                                                                     : k_group<1, true>)
-                   : (u == 2 ? k_group<2, false> : u == 4 ? k_group<4, false> : u == 8 ? k_group<8, false>
-                                                                                       : k_group<1, false>);
+    auto kern = u == 2 ? k_group<2, true> : u == 4 ? k_group<4, true> : u == 8 ? k_group<8, true> : k_group<1, true>;
     const GrpBatch GB{B.seq, B.ref, B.keep_code, B.ref2, B.keep_pos, B.span_start, B.span_len};
-    kern<<<db->n_groups, kGrpThreads, 0, st>>>(GB, db->groups, db->seg4, db->out, db->aux, ctx->group_skip,
-                                               ctx->nt_copy);
+    kern<<<db->n_groups, kGrpThreads, 0, st>>>(GB, static_cast<const int4 *>(db->b_groups.p),
+                                               static_cast<const int4 *>(db->b_seg4.p), db->out, db->aux,
+                                               ctx->group_skip, ctx->nt_copy);
     if ((rc = check_launch(ctx, "k_group"))) return rc;
+  } else if (db->seq_bytes) {
+    KernelScope ks(ctx, "copy_seq");
+    HIP_OR_FAIL(hipMemcpyAsync(db->out, B.seq, (size_t)db->seq_bytes, hipMemcpyDeviceToDevice, st));
   }
-  const int caps[2] = {kSmallCap0, kSmallCap1};
-  for (int k = 0; k < 2 && !v4; ++k) {
-    if (!db->n_small[k]) continue;
-    if (v3) {
-      KernelScope ks(ctx, k == 0 ? "k_scope_v3/2.5K" : "k_scope_v3/16K");
-      const size_t lds = 4 * v3_wave_lds_bytes(caps[k]);
-      const int grid = std::max(1, std::min((db->n_small[k] + 3) / 4, ctx->v3_blocks[k]));
-      k_scope_v3<<<grid, kBlock, lds, st>>>(B, db->srec[k], db->n_small[k], caps[k], db->inc_rec, db->out,
-                                            db->scope_calls, db->scope_bases, db->rare_small_list,
-                                            db->counters + 0);
-      if ((rc = check_launch(ctx, "k_scope_v3"))) return rc;
-    } else if (v2) {
-      KernelScope ks(ctx, k == 0 ? "k_scope_v2/2.5K" : "k_scope_v2/16K");
-      k_scope_v2<<<db->n_small[k], 64, v2_lds_bytes(caps[k]), st>>>(
-          B, db->inc_rec, db->small_list[k], db->n_small[k], caps[k], db->out, db->scope_calls, db->scope_bases,
-          db->rare_small_list, db->counters + 0);
-      if ((rc = check_launch(ctx, "k_scope_v2"))) return rc;
-    } else if (ctx->variant == GANON_VARIANT_BLOCK) {
-      KernelScope ks(ctx, k == 0 ? "k_scope_small<1>/2.5K" : "k_scope_small<1>/16K");
-      k_scope_small<1><<<db->n_small[k], kBlock, small_lds_bytes(1, caps[k]), st>>>(
-          B, db->small_list[k], db->n_small[k], nullptr, caps[k], db->out, db->scope_calls, db->scope_bases,
-          db->rare_small_list, db->counters + 0);
-      if ((rc = check_launch(ctx, "k_scope_small<1>"))) return rc;
-    } else {
-      KernelScope ks(ctx, k == 0 ? "k_scope_wave/2.5K" : "k_scope_wave/16K");
-      k_scope_wave<<<db->n_small[k], 64, (size_t)caps[k] + kMetaLds, st>>>(
-          B, db->small_list[k], db->n_small[k], caps[k], db->out, db->scope_calls, db->scope_bases,
-          db->rare_small_list, db->counters + 0);
-      if ((rc = check_launch(ctx, "k_scope_wave"))) return rc;
+  if (db->n_tiles_h) {
+    if (!db->tn_tab && (rc = dmalloc(ctx, db->huge_allocs, &db->tn_tab, (size_t)db->tn_entries))) return rc;
+    {
+      KernelScope ks(ctx, "k_tile_large<1>");
+      k_tile_large<1><<<db->n_tiles_h, kBlock, tile_lds_bytes(1), st>>>(
+          B, db->tiles_h, nullptr, db->n_tiles_h, nullptr, db->large_incid, db->tab_off, db->tn_tab, db->scope_calls,
+          db->rare_tile_list, db->counters + 1);
+      if ((rc = check_launch(ctx, "k_tile_large<1>"))) return rc;
     }
-  }
-  if (n_tiles && !db->tn_tab && (rc = dev_alloc(ctx, db, &db->tn_tab, (size_t)db->tn_entries))) return rc;
-  if (n_tiles) {
-    KernelScope ks(ctx, "k_tile_large<1>");
-    k_tile_large<1><<<n_tiles, kBlock, tile_lds_bytes(1), st>>>(
-        B, tiles, nullptr, n_tiles, nullptr, db->large_incid, db->tab_off, db->tn_tab, db->scope_calls,
-        db->rare_tile_list, db->counters + 1);
-    if ((rc = check_launch(ctx, "k_tile_large<1>"))) return rc;
-  }
-  // Re-runs on the 16-code tally; list lengths stay on the device (no host sync).
-  if (db->n_small[0] + db->n_small[1] && !v4) {
-    KernelScope ks(ctx, "k_scope_small<4>/rare");
-    const int grid = std::min<int>(db->n_small[0] + db->n_small[1], kPersistGrid);
-    k_scope_small<4><<<grid, kBlock, small_lds_bytes(4, kSmallCap1), st>>>(
-        B, db->rare_small_list, 0, db->counters + 0, kSmallCap1, db->out, db->scope_calls, db->scope_bases,
-        nullptr, nullptr);
-    if ((rc = check_launch(ctx, "k_scope_small<4>"))) return rc;
-  }
-  if (n_tiles) {
-    KernelScope ks(ctx, "k_tile_large<4>/rare");
-    const int grid = std::min<int>(n_tiles, kPersistGrid);
-    k_tile_large<4><<<grid, kBlock, tile_lds_bytes(4), st>>>(
-        B, tiles, db->rare_tile_list, 0, db->counters + 1, db->large_incid, db->tab_off, db->tn_tab,
-        db->scope_calls, nullptr, nullptr);
-    if ((rc = check_launch(ctx, "k_tile_large<4>"))) return rc;
-  }
-  if (n_large_written) {
-    KernelScope ks(ctx, "k_mask_large");
-    const int grid = std::min<int>((n_large_written + kWaves - 1) / kWaves, 8192);
-    k_mask_large<<<grid, kBlock, 0, st>>>(B, large_written, n_large_written, db->tab_off, db->tn_tab,
-                                          db->out, db->scope_bases);
-    if ((rc = check_launch(ctx, "k_mask_large"))) return rc;
+    {
+      // tiles that met a non-ACGTN base: re-run on the 16-code tally (count stays on the device)
+      KernelScope ks(ctx, "k_tile_large<4>/rare");
+      k_tile_large<4><<<std::min<int>(db->n_tiles_h, 1024), kBlock, tile_lds_bytes(4), st>>>(
+          B, db->tiles_h, db->rare_tile_list, 0, db->counters + 1, db->large_incid, db->tab_off, db->tn_tab,
+          db->scope_calls, nullptr, nullptr);
+      if ((rc = check_launch(ctx, "k_tile_large<4>"))) return rc;
+    }
+    if (db->n_large_written_h) {
+      KernelScope ks(ctx, "k_mask_large");
+      const int grid = std::min<int>((db->n_large_written_h + kWaves - 1) / kWaves, 8192);
+      k_mask_large<<<grid, kBlock, 0, st>>>(B, db->large_written_h, db->n_large_written_h, db->tab_off, db->tn_tab,
+                                            db->out, db->scope_bases);
+      if ((rc = check_launch(ctx, "k_mask_large"))) return rc;
+    }
   }
   {
-    if (v4) {
-      // far masks (fused), totals from the group partials and the wide scopes, counter reset
-      KernelScope ks(ctx, "k_finish");
-      k_finish<<<64, kBlock, 0, st>>>(db->far, v5 && db->n_groups ? db->far_cap : 0, db->out, db->grp_part,
-                                      db->n_groups, db->large_ids, db->n_huge_scopes, db->scope_calls,
-                                      db->scope_bases, db->static_totals, db->counters, db->acc, db->totals);
-      if ((rc = check_launch(ctx, "k_finish"))) return rc;
-    } else {
-      KernelScope ks(ctx, "k_totals");
-      const int grid = std::max(1, std::min<int>((db->n_scopes + kBlock - 1) / kBlock, 128));
-      k_totals<<<grid, kBlock, 0, st>>>(db->scope_calls, db->scope_bases, nullptr, db->n_scopes, nullptr, 0,
-                                        db->counters + 0, db->counters + 1, db->totals);
-      if ((rc = check_launch(ctx, "k_totals"))) return rc;
-    }
+    // far masks, totals from the group partials and the huge scopes, counter reset
+    KernelScope ks(ctx, "k_finish");
+    k_finish<<<64, kBlock, 0, st>>>(static_cast<const unsigned long long *>(db->b_far.p), db->n_groups ? db->far_cap : 0,
+                                    db->out, static_cast<const int32_t *>(db->b_grp_part.p), db->n_groups,
+                                    db->large_ids, db->n_huge_scopes, db->scope_calls, db->scope_bases,
+                                    db->static_totals, db->counters, db->far_count, db->status, db->acc, db->totals);
+    if ((rc = check_launch(ctx, "k_finish"))) return rc;
   }
   db->ran = true;
   return GANON_OK;
@@ -2690,6 +1659,8 @@ GANON_API int ganon_batch_download(ganon_ctx *ctx, ganon_dbatch *db, uint8_t *se
   if (!db->ran) return fail(ctx, GANON_E_STATE, "download before run");
   HIP_OR_FAIL(hipSetDevice(ctx->device));
   hipStream_t st = ctx->stream;
+  int32_t status = 0;
+  HIP_OR_FAIL(hipMemcpyAsync(&status, db->status, sizeof status, hipMemcpyDeviceToHost, st));
   if (seq_out && db->seq_bytes)
     HIP_OR_FAIL(hipMemcpyAsync(seq_out, db->out, (size_t)db->seq_bytes, hipMemcpyDeviceToHost, st));
   if (scope_calls_out && db->n_scopes)
@@ -2699,6 +1670,7 @@ GANON_API int ganon_batch_download(ganon_ctx *ctx, ganon_dbatch *db, uint8_t *se
   if (totals_out)
     HIP_OR_FAIL(hipMemcpyAsync(totals_out, db->totals, GANON_N_TOTALS * 8, hipMemcpyDeviceToHost, st));
   HIP_OR_FAIL(hipStreamSynchronize(st));
+  if (status & 1) return fail(ctx, GANON_E_STATE, "far-mask list overflowed its planned capacity: output invalid");
   return GANON_OK;
 }
 
@@ -2727,16 +1699,24 @@ GANON_API int ganon_batch_copy_totals(ganon_ctx *ctx, ganon_dbatch *db, void *de
   return GANON_OK;
 }
 
+GANON_API int ganon_batch_path_counts(ganon_ctx *ctx, ganon_dbatch *db, int64_t *out4) {
+  if (!ctx || !db || !out4) return fail(ctx, GANON_E_ARG, "null argument");
+  HIP_OR_FAIL(hipSetDevice(ctx->device));
+  HIP_OR_FAIL(hipMemcpyAsync(out4, db->paths, 4 * sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+  HIP_OR_FAIL(hipStreamSynchronize(ctx->stream));
+  return GANON_OK;
+}
+
 GANON_API int ganon_batch_info(ganon_dbatch *db, int64_t *info) {
   if (!db || !info) return GANON_E_ARG;
-  info[0] = db->n_small[0];
-  info[1] = db->n_small[1];
-  info[2] = db->n_large_scopes;
-  info[3] = db->n_tiles;
-  info[4] = db->n_pt;
-  info[5] = db->n_large_written;
-  info[6] = db->max_small_span;
-  info[7] = db->tn_entries;
+  info[0] = db->n_groups;
+  info[1] = db->n_seg;
+  info[2] = db->n_huge_scopes;
+  info[3] = db->n_tiles_h;
+  info[4] = db->far_cap;
+  info[5] = db->n_large_written_h;
+  info[6] = db->region;
+  info[7] = db->n_written;
   return GANON_OK;
 }
 

@@ -95,10 +95,13 @@ BATCH_ARRAYS = {
 _PTR_OF = {np.int32: _i32p, np.int64: _i64p, np.uint8: _u8p, np.uint32: _u32p}
 
 
-def make_c_batch(arrays: dict) -> GanonBatch:
-    """Build a GanonBatch over numpy arrays (kept alive by the caller's dict)."""
+def make_c_batch(arrays: dict, with_ref: bool = True) -> GanonBatch:
+    """Build a GanonBatch over numpy arrays (kept alive by the caller's dict). ``with_ref`` False:
+    the reference is resident on the device, ``ref_nt16`` may be absent."""
     b = GanonBatch()
     for name, dt in BATCH_ARRAYS.items():
+        if name == "ref_nt16" and not with_ref and name not in arrays:
+            continue
         a = arrays[name]
         if a.dtype != dt or not a.flags["C_CONTIGUOUS"]:
             raise GanonError(f"batch array {name} must be C-contiguous {np.dtype(dt)}")
@@ -108,7 +111,7 @@ def make_c_batch(arrays: dict) -> GanonBatch:
     b.n_incid = len(arrays["incid_read"])
     b.seq_bytes = len(arrays["seq_nt16"])
     b.n_cigar_ops = len(arrays["cigar"])
-    b.ref_bytes = len(arrays["ref_nt16"])
+    b.ref_bytes = len(arrays["ref_nt16"]) if "ref_nt16" in arrays else 0
     return b
 
 
@@ -135,6 +138,10 @@ def hip_lib():
     lib.ganon_ctx_set_param.argtypes = [_p, C.c_int, C.c_int]
     lib.ganon_mask_batch.argtypes = [_p, C.POINTER(GanonBatch), _u8p, _i32p, _i32p, _i64p]
     lib.ganon_batch_upload.argtypes = [_p, C.POINTER(GanonBatch), C.POINTER(_p)]
+    lib.ganon_batch_upload_ref.argtypes = [_p, C.POINTER(GanonBatch), _p, C.POINTER(_p)]
+    lib.ganon_batch_reload.argtypes = [_p, _p, C.POINTER(GanonBatch)]
+    lib.ganon_ref_upload.argtypes = [_p, _u8p, C.c_int64, C.POINTER(_p)]
+    lib.ganon_ref_free.argtypes = [_p, _p]
     lib.ganon_batch_run.argtypes = [_p, _p]
     lib.ganon_batch_sync.argtypes = [_p]
     lib.ganon_batch_download.argtypes = [_p, _p, _u8p, _i32p, _i32p, _i64p]
@@ -143,6 +150,7 @@ def hip_lib():
     lib.ganon_batch_copy_totals.argtypes = [_p, _p, _p]
     lib.ganon_last_kernel_times.argtypes = [_p, C.POINTER(KernelTime), C.c_int]
     lib.ganon_batch_info.argtypes = [_p, _i64p]
+    lib.ganon_batch_path_counts.argtypes = [_p, _p, _i64p]
     lib.ganon_fastq_upload.argtypes = [_p, C.POINTER(GanonFastqRecords), C.POINTER(_p)]
     lib.ganon_fastq_run.argtypes = [_p, _p]
     lib.ganon_fastq_bytes.argtypes = [_p]
@@ -161,7 +169,7 @@ def hip_lib():
     lib.ganon_indel_download.restype = C.c_int64
     lib.ganon_indel_info.argtypes = [_p, _i64p]
     lib.ganon_indel_free.argtypes = [_p, _p]
-    if lib.ganon_abi_version() != 2:
+    if lib.ganon_abi_version() != 3:
         raise GanonError("libganon_hip.so ABI version mismatch")
     _hip = lib
     return lib
@@ -169,7 +177,7 @@ def hip_lib():
 
 PARAM_GROUP_UNROLL = 1   # include/ganon.h GANON_PARAM_GROUP_UNROLL
 PARAM_GROUP_SKIP = 2     # include/ganon.h GANON_PARAM_GROUP_SKIP (phase timing only)
-PARAM_GROUP_TARGET = 3   # include/ganon.h GANON_PARAM_GROUP_TARGET (segments per group, at upload)
+PARAM_GROUP_TARGET = 3   # include/ganon.h GANON_PARAM_GROUP_TARGET (cost units per group, at upload)
 PARAM_NT_COPY = 4        # include/ganon.h GANON_PARAM_NT_COPY
 PARAM_REF2 = 5           # include/ganon.h GANON_PARAM_REF2
 PARAM_FASTQ_SKIP = 6     # include/ganon.h GANON_PARAM_FASTQ_SKIP (phase timing only)
@@ -178,9 +186,11 @@ PARAM_INDEL_SORT = 8     # include/ganon.h GANON_PARAM_INDEL_SORT (0 segmented, 
 
 EXPORTED_HIP_SYMBOLS = (
     "ganon_ctx_create", "ganon_ctx_destroy", "ganon_last_error", "ganon_abi_version",
-    "ganon_ctx_set_stream", "ganon_ctx_set_profiling", "ganon_ctx_set_variant", "ganon_ctx_set_param", "ganon_mask_batch", "ganon_batch_upload",
+    "ganon_ctx_set_stream", "ganon_ctx_set_profiling", "ganon_ctx_set_variant", "ganon_ctx_set_param", "ganon_mask_batch",
+    "ganon_ref_upload", "ganon_ref_free", "ganon_batch_upload", "ganon_batch_upload_ref", "ganon_batch_reload",
     "ganon_batch_run", "ganon_batch_sync", "ganon_batch_download", "ganon_batch_free",
     "ganon_batch_device_totals", "ganon_batch_copy_totals", "ganon_last_kernel_times", "ganon_batch_info",
+    "ganon_batch_path_counts",
     "ganon_fastq_upload", "ganon_fastq_run", "ganon_fastq_bytes", "ganon_fastq_device_output",
     "ganon_fastq_download", "ganon_fastq_free", "ganon_fastq_format_hip",
     "ganon_indel_upload", "ganon_indel_run", "ganon_indel_download", "ganon_indel_info", "ganon_indel_free",
@@ -230,7 +240,8 @@ class HipMasker:
         self._check(self._lib.ganon_ctx_set_stream(self._h, _p(hip_stream_ptr or 0)), "set_stream")
 
     def set_variant(self, variant: int) -> None:
-        """include/ganon.h GANON_VARIANT_*: 0 default, 1 block, 2 wave, 3 copy-patch, 4 group."""
+        """include/ganon.h GANON_VARIANT_*: 0 (default) or 5 (the same fused group kernel); the
+        round-1 A/B kernels are retired and raise GanonError."""
         self._check(self._lib.ganon_ctx_set_variant(self._h, int(variant)), "set_variant")
 
     def set_param(self, param: int, value: int) -> None:
@@ -267,11 +278,24 @@ class HipMasker:
         return out, calls, bases, tot
 
     # -- device-resident path ------------------------------------------------------------
-    def upload(self, arrays: dict) -> "DeviceBatch":
-        b = make_c_batch(arrays)
+    def upload(self, arrays: dict, ref: "DeviceRef" = None) -> "DeviceBatch":
+        """Copy the raw batch arrays to HBM; validation and planning run on the device. With
+        ``ref`` the scopes read that resident reference (the batch's ``ref_nt16`` is ignored)."""
+        b = make_c_batch(arrays, with_ref=ref is None)
         h = _p()
-        self._check(self._lib.ganon_batch_upload(self._h, C.byref(b), C.byref(h)), "ganon_batch_upload")
-        return DeviceBatch(self, h, b.seq_bytes, b.n_scopes)
+        if ref is None:
+            self._check(self._lib.ganon_batch_upload(self._h, C.byref(b), C.byref(h)), "ganon_batch_upload")
+        else:
+            self._check(self._lib.ganon_batch_upload_ref(self._h, C.byref(b), ref.h, C.byref(h)),
+                        "ganon_batch_upload_ref")
+        return DeviceBatch(self, h, b.seq_bytes, b.n_scopes, resident_ref=ref is not None)
+
+    def upload_reference(self, ref_nt16: np.ndarray) -> "DeviceRef":
+        """ganon_ref_upload: a genome resident in HBM for every batch of this context."""
+        a = np.ascontiguousarray(ref_nt16, dtype=np.uint8)
+        h = _p()
+        self._check(self._lib.ganon_ref_upload(self._h, a.ctypes.data_as(_u8p), len(a), C.byref(h)), "ganon_ref_upload")
+        return DeviceRef(self, h, len(a))
 
     # -- FASTQ formatter -------------------------------------------------------------------
     def fastq_upload(self, recs: dict, seq_batch: "DeviceBatch" = None) -> "DeviceFastq":
@@ -410,12 +434,34 @@ class DeviceFastq:
             self.h = None
 
 
+class DeviceRef:
+    """A reference genome resident on the device (ganon_ref_upload)."""
+
+    def __init__(self, masker: HipMasker, handle, n_bytes: int):
+        self.m = masker
+        self.h = handle
+        self.n_bytes = n_bytes
+
+    def free(self) -> None:
+        if self.h:
+            self.m._lib.ganon_ref_free(self.m._h, self.h)
+            self.h = None
+
+
 class DeviceBatch:
-    def __init__(self, masker: HipMasker, handle, seq_bytes: int, n_scopes: int):
+    def __init__(self, masker: HipMasker, handle, seq_bytes: int, n_scopes: int, resident_ref: bool = False):
         self.m = masker
         self.h = handle
         self.seq_bytes = seq_bytes
         self.n_scopes = n_scopes
+        self.resident_ref = resident_ref
+
+    def reload(self, arrays: dict) -> None:
+        """ganon_batch_reload: replace the contents with another host batch (device buffers reused)."""
+        b = make_c_batch(arrays, with_ref=not self.resident_ref)
+        self.m._check(self.m._lib.ganon_batch_reload(self.m._h, self.h, C.byref(b)), "ganon_batch_reload")
+        self.seq_bytes = b.seq_bytes
+        self.n_scopes = b.n_scopes
 
     def run(self) -> None:
         self.m._check(self.m._lib.ganon_batch_run(self.m._h, self.h), "ganon_batch_run")
@@ -449,14 +495,20 @@ class DeviceBatch:
     def info(self) -> dict:
         a = np.zeros(8, np.int64)
         self.m._check(self.m._lib.ganon_batch_info(self.h, _ptr(a, _i64p)), "batch_info")
-        keys = ("small4k_scopes", "small16k_scopes", "large_scopes", "large_tiles", "passthrough_reads",
-                "large_written_reads", "max_small_span", "tn_table_entries")
+        keys = ("groups", "segments", "huge_scopes", "huge_tiles", "far_capacity", "huge_written_reads",
+                "overflow_region", "written_reads")
         return dict(zip(keys, a.tolist()))
 
     def kernel_times(self) -> list:
         arr = (KernelTime * 32)()
         n = self.m._lib.ganon_last_kernel_times(self.m._h, arr, 32)
         return [(arr[i].name.decode(), int(arr[i].launches), float(arr[i].ms)) for i in range(min(n, 32))]
+
+    def path_counts(self) -> dict:
+        """ganon_batch_path_counts: the group kernel's rarer paths taken since upload."""
+        a = np.zeros(4, np.int64)
+        self.m._check(self.m._lib.ganon_batch_path_counts(self.m._h, self.h, _ptr(a, _i64p)), "path_counts")
+        return {"sorted_lists": int(a[0]), "region_passes": int(a[1]), "key_range_splits": int(a[2])}
 
     def indel_tally(self, arrays: dict) -> "DeviceIndels":
         """Plan the germline indel tally of this batch (``arrays`` = the batch it was uploaded from)."""

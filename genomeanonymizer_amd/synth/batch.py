@@ -43,14 +43,15 @@ def _cigar_word(op: str, n: int) -> int:
 
 
 def random_batch(seed: int, n_scopes: int = 64, max_reads: int = 40, read_len=(0, 220),
-                 wide_scopes: int = 2, rare_frac: float = 0.02) -> Dict[str, np.ndarray]:
-    """Edge-case batch. Every scope owns a private contig region so spans never collide."""
+                 wide_scopes: int = 2, rare_frac: float = 0.02, wide_span=(20000, 40000)) -> Dict[str, np.ndarray]:
+    """Edge-case batch. Every scope owns a private contig region so spans never collide. The
+    first ``wide_scopes`` scopes span ``wide_span`` positions (over 2^20: the huge-scope tile path)."""
     rng = np.random.default_rng(seed)
     scopes = []
     region_len = []
     for s in range(n_scopes):
         wide = s < wide_scopes
-        span = int(rng.integers(20000, 40000)) if wide else int(rng.integers(50, 3000))
+        span = int(rng.integers(*wide_span)) if wide else int(rng.integers(50, 3000))
         region_len.append(span + 1200)
         scopes.append(wide)
     # reference: one contig per scope region, each starting on a byte boundary
@@ -730,6 +731,20 @@ def config2_batch(n_reads: int = 10_000_000, genome: int = 3_000_000_000, n_cont
     first_scope = np.full(n, n_scopes, np.int64)
     np.minimum.at(first_scope, inc_read, inc_scope)
     ws = np.where(first_scope < n_scopes, first_scope, -1).astype(np.int32)
+    keep_pos = np.concatenate([win_pos - 1, np.full(len(u_ids), -1, np.int64)])
+    keep_code = np.concatenate([ACGT[rng.integers(0, 4, n_win)], np.zeros(len(u_ids), np.uint8)])
+    # scope ids in genome order, windows and gap union scopes interleaved, as the product planner
+    # lays a sample's scopes out (a read is in one scope here, so the writer is unchanged)
+    order = np.lexsort((s_start, s_contig))
+    new_id = np.empty(n_scopes, np.int64)
+    new_id[order] = np.arange(n_scopes)
+    o = np.argsort(new_id[inc_scope], kind="stable")
+    inc_scope, inc_read = new_id[inc_scope][o], inc_read[o]
+    counts = counts[order]
+    incid_off = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+    s_start, s_end, s_contig = s_start[order], s_end[order], s_contig[order]
+    keep_pos, keep_code = keep_pos[order], keep_code[order]
+    ws = np.where(ws >= 0, new_id[np.maximum(ws, 0)], -1).astype(np.int32)
     arr = {
         "ref_start": rpos.astype(np.int32),
         "read_len": np.full(n, L, np.int32),
@@ -746,8 +761,8 @@ def config2_batch(n_reads: int = 10_000_000, genome: int = 3_000_000_000, n_cont
         "scope_span_len": (s_end - s_start).astype(np.int32),
         "scope_ref_off": (cstart[s_contig] + s_start).astype(np.int64),
         "ref_nt16": ref,
-        "keep_pos": np.concatenate([win_pos - 1, np.full(len(u_ids), -1, np.int64)]).astype(np.int32),
-        "keep_code": np.concatenate([ACGT[rng.integers(0, 4, n_win)], np.zeros(len(u_ids), np.uint8)]),
+        "keep_pos": keep_pos.astype(np.int32),
+        "keep_code": keep_code.astype(np.uint8),
     }
     info = {"reads": n, "read_len": L, "scopes": n_scopes, "window_scopes": n_win,
             "union_scopes": int(len(u_ids)), "incidences": int(len(inc_read)),

@@ -35,7 +35,7 @@
 #define GANON_API __attribute__((visibility("default")))
 #endif
 
-#define GANON_ABI_VERSION 2
+#define GANON_ABI_VERSION 3
 
 enum {
   GANON_OK = 0,
@@ -59,6 +59,7 @@ enum {
 
 typedef struct ganon_ctx ganon_ctx;
 typedef struct ganon_dbatch ganon_dbatch;
+typedef struct ganon_ref ganon_ref;
 
 typedef struct ganon_batch {
   int32_t n_reads;
@@ -95,15 +96,11 @@ GANON_API const char *ganon_last_error(ganon_ctx *ctx);
 GANON_API int ganon_abi_version(void);
 /* Use an external hipStream_t (e.g. torch's current stream); NULL = the ctx's own. */
 GANON_API int ganon_ctx_set_stream(ganon_ctx *ctx, void *hip_stream);
-/* Small-scope kernel: GANON_VARIANT_DEFAULT (= GROUP_FUSED),
- * GANON_VARIANT_BLOCK (one 256-thread workgroup per scope, the first version),
- * GANON_VARIANT_WAVE (one wave per scope writing whole reads), GANON_VARIANT_COPYPATCH
- * (copy-then-patch, one 64-thread workgroup per scope), GANON_VARIANT_GROUP (copy-then-patch,
- * one workgroup per group of consecutive scopes, calls from a sorted observation list),
- * GANON_VARIANT_GROUP_FUSED (no separate copy: each group workgroup copies its own line-aligned
- * partition of the output and masks with byte stores), GANON_VARIANT_PERSIST (copy-then-patch,
- * persistent waves, one scope per wave). The non-default ones are kept for A/B runs and
- * cross-checks; all give identical results. */
+/* Small-scope kernel. Since ABI 3 the fused group kernel (GANON_VARIANT_DEFAULT =
+ * GANON_VARIANT_GROUP_FUSED: one workgroup per group of consecutive scopes copies its line-aligned
+ * pieces of the output and masks with byte stores) is the only one; the round-1 A/B kernels
+ * (BLOCK, WAVE, COPYPATCH, GROUP, PERSIST) were retired and ganon_ctx_set_variant rejects them
+ * with GANON_E_ARG. The enum values are kept so that old callers get that error, not another. */
 enum {
   GANON_VARIANT_DEFAULT = 0,
   GANON_VARIANT_BLOCK = 1,
@@ -120,7 +117,7 @@ GANON_API int ganon_ctx_set_variant(ganon_ctx *ctx, int variant);
  * the classification, bit 1 the chunk scan, bit 2 the partition copy of the group kernels, bit 3
  * the per-scope count stores.
  * Keep it 0 in production. GANON_PARAM_GROUP_TARGET: segments per scope group (read at
- * upload; default 512). GANON_PARAM_NT_COPY: non-temporal stores for the fused partition copy
+ * upload, in cost units: segments plus 3 per scope; default 704). GANON_PARAM_NT_COPY: non-temporal stores for the fused partition copy
  * (default 1). GANON_PARAM_REF2: group kernels read a 2-bit copy of the reference for segments
  * whose reference range is all ACGT (1, default) or the nt16 reference only (0).
  * GANON_PARAM_FASTQ_KD: output dwords per lane the FASTQ formatter loads at once (1-6 or 8; default 3).
@@ -144,9 +141,25 @@ GANON_API int ganon_mask_batch(ganon_ctx *ctx, const ganon_batch *batch, uint8_t
                                int32_t *scope_calls_out, int32_t *scope_bases_out,
                                int64_t *totals_out);
 
-/* Device-resident path (benchmarks, multi-GPU shards): the batch is copied to HBM once and
- * its scope work lists are built at upload; ganon_batch_run only launches kernels. */
+/* Resident reference: the genome (upper-cased nt16, 2 per byte, contigs concatenated) copied
+ * to HBM once, with a 2-bit copy and a non-ACGT block map built on the device. Batches uploaded
+ * with ganon_batch_upload_ref read it in place (their ref_nt16 / ref_bytes are ignored; scope_ref_off
+ * indexes this reference). It must outlive those batches. */
+GANON_API int ganon_ref_upload(ganon_ctx *ctx, const uint8_t *ref_nt16, int64_t ref_bytes, ganon_ref **out);
+GANON_API int ganon_ref_free(ganon_ctx *ctx, ganon_ref *ref);
+
+/* Device-resident path (streaming, benchmarks, multi-GPU shards). Upload copies only the raw
+ * ganon_batch arrays to HBM and validates and plans them on the device (synchronous). Every
+ * ganon_batch_run first rebuilds the derived layer (per-read CIGAR walk into aligned segments,
+ * scope groups, output partitions) from those raw arrays on the device, then masks: a run does
+ * all the work of anonymizing the batch. ganon_batch_upload uploads the batch's own reference;
+ * ganon_batch_upload_ref uses a resident one. ganon_batch_reload replaces the contents of an
+ * uploaded batch with another host batch, reusing its device buffers (grow-only) and its
+ * reference (resident, or the new batch's own) — the double-buffered streaming path. */
 GANON_API int ganon_batch_upload(ganon_ctx *ctx, const ganon_batch *batch, ganon_dbatch **out);
+GANON_API int ganon_batch_upload_ref(ganon_ctx *ctx, const ganon_batch *batch, const ganon_ref *ref,
+                                     ganon_dbatch **out);
+GANON_API int ganon_batch_reload(ganon_ctx *ctx, ganon_dbatch *db, const ganon_batch *batch);
 GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db);      /* async on the stream */
 GANON_API int ganon_batch_sync(ganon_ctx *ctx);
 GANON_API int ganon_batch_download(ganon_ctx *ctx, ganon_dbatch *db, uint8_t *seq_out_nt16,
@@ -167,9 +180,14 @@ typedef struct ganon_kernel_time {
 } ganon_kernel_time;
 GANON_API int ganon_last_kernel_times(ganon_ctx *ctx, ganon_kernel_time *out, int max_k);
 
-/* Work-list summary of an uploaded batch: [small_scopes, wide?, large_scopes, large_tiles,
- * passthrough_reads, large_written_reads, max_small_span, 0]. */
+/* Plan of an uploaded batch: [scope groups, segment records, huge scopes (> 2^20 positions, tile
+ * path), huge-scope tiles, far-mask capacity (nibbles), reads written by huge scopes, overflow-region
+ * entries, written reads]. */
 GANON_API int ganon_batch_info(ganon_dbatch *db, int64_t *info8);
+/* How often the group kernel took its rarer paths since upload (synchronous): [lists of more than
+ * 256 observations classified after an LDS sort, lists of more than 512 classified from the
+ * group's global overflow region, key-range splits of an overflowing region, 0]. */
+GANON_API int ganon_batch_path_counts(ganon_ctx *ctx, ganon_dbatch *db, int64_t *out4);
 
 /* ---- FASTQ record formatter ------------------------------------------
  * Replaces, for many reads at once, AnonymizedRead.get_anonymized_fastq_record

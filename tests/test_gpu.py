@@ -12,8 +12,6 @@ from helpers import load_scope_golden, run_pipeline_vs_golden, written_reads_equ
 
 pytestmark = pytest.mark.gpu
 
-VARIANTS = (0, 1, 2, 3, 4, 5, 6)   # include/ganon.h GANON_VARIANT_*
-MAIN = (0, 4, 6)                  # default (fused group), group + copy, persistent waves
 
 
 @pytest.fixture(scope="module")
@@ -44,12 +42,9 @@ def _all_reads_equal(arr, a, b):
 @pytest.mark.parametrize("seed", [101, 202, 303])
 def test_hip_matches_reference_scopes(masker, seed):
     arr, exp_seq, exp_calls = load_scope_golden(seed)
-    for v in MAIN:
-        masker.set_variant(v)
-        out, calls, bases, tot = masker.mask(arr)
-        assert written_reads_equal(arr, out, exp_seq) == [], v
-        assert np.array_equal(calls, exp_calls), v
-    masker.set_variant(0)
+    out, calls, bases, tot = masker.mask(arr)
+    assert written_reads_equal(arr, out, exp_seq) == []
+    assert np.array_equal(calls, exp_calls)
 
 
 @pytest.mark.parametrize("seed", list(range(1, 13)))
@@ -64,47 +59,88 @@ def test_hip_matches_oracle_edge_batches(masker, oracle, seed):
     o_out, o_calls, o_bases, o_tot = oracle.mask(arr)
     in_batch = np.zeros(len(arr["read_len"]), bool)
     in_batch[arr["incid_read"]] = True
-    for v in MAIN:
-        masker.set_variant(v)
-        out, calls, bases, tot = masker.mask(arr)
-        bad = [r for r in _all_reads_equal(arr, out, o_out) if in_batch[r] or arr["write_scope"][r] >= 0]
-        assert bad == [], v
-        assert np.array_equal(calls, o_calls) and np.array_equal(bases, o_bases), v
-        assert tot[0] == o_tot[0] and tot[1] == o_tot[1], v
+    out, calls, bases, tot = masker.mask(arr)
+    bad = [r for r in _all_reads_equal(arr, out, o_out) if in_batch[r] or arr["write_scope"][r] >= 0]
+    assert bad == []
+    assert np.array_equal(calls, o_calls) and np.array_equal(bases, o_bases)
+    assert tot[0] == o_tot[0] and tot[1] == o_tot[1]
+
+
+def test_retired_variants_are_rejected(masker):
+    """The round-1 A/B kernels are gone from the product library (ABI 3): asking for one is an
+    error, not a silent fallback."""
+    from genomeanonymizer_amd import native
+    for v in (1, 2, 3, 4, 6):
+        with pytest.raises(native.GanonError):
+            masker.set_variant(v)
+    masker.set_variant(5)
     masker.set_variant(0)
 
 
-@pytest.mark.parametrize("seed", [21, 22, 23])
-def test_block_variant_matches_wave_variant(masker, seed):
-    """The first (workgroup-per-scope) kernel and the wave-per-scope kernel agree."""
+def test_reload_rebuilds_every_derived_array(masker, oracle):
+    """ganon_batch_reload reuses the device buffers of another batch (grow-only): batch A, then
+    a differently shaped batch B, then A again — every run rebuilds segments, groups and pieces
+    from the raw arrays on the device, so each result equals a fresh one-shot mask."""
     from genomeanonymizer_amd.synth.batch import config2_batch, random_batch
-    arr = random_batch(seed, n_scopes=40, rare_frac=0.1, wide_scopes=1) if seed != 23 else \
-        config2_batch(n_reads=300_000, genome=90_000_000, n_windows=30_000, n_germline=60_000)[0]
-    res = []
-    for v in VARIANTS:
-        masker.set_variant(v)
-        res.append(masker.mask(arr))
-    masker.set_variant(0)
-    for v in VARIANTS[1:]:
-        for k in range(3):
-            assert np.array_equal(res[0][k], res[v][k]), (v, k)
+    a, _ = config2_batch(n_reads=120_000, genome=40_000_000, n_windows=12_000, n_germline=30_000, seed=4)
+    b = random_batch(31, n_scopes=50, rare_frac=0.2, wide_scopes=3)
+    want_a, want_b = masker.mask(a), masker.mask(b)
+    db = masker.upload(a)
+    try:
+        for arr, want in ((a, want_a), (b, want_b), (a, want_a)):
+            if arr is not a or db.seq_bytes != len(a["seq_nt16"]):
+                db.reload(arr)
+            db.run()
+            db.run()        # twice: no state of a run may leak into the next
+            got = db.download()
+            for k in range(4):
+                assert np.array_equal(got[k], want[k]), k
+    finally:
+        db.free()
+    o_out, o_calls, o_bases, _ = oracle.mask(b)
+    assert np.array_equal(want_b[1], o_calls) and np.array_equal(want_b[2], o_bases)
 
 
-@pytest.mark.parametrize("seed,keep", [(5, False), (6, True)])
-def test_dense_scopes_all_variants_match_oracle(masker, oracle, seed, keep):
-    """Thousands of observations per scope and one site seen by ~600 reads: the group
-    kernel's list overflows (key-range bisection, single-key flags/patch scans)."""
+def test_resident_reference_matches_private(masker):
+    """ganon_ref_upload: one genome resident in HBM, batches uploaded against it (no reference in
+    the batch) give the same bytes and counts as batches carrying their own reference."""
+    from genomeanonymizer_amd.synth.batch import config2_batch
+    arr, _ = config2_batch(n_reads=100_000, genome=30_000_000, n_windows=10_000, n_germline=20_000, seed=9)
+    want = masker.mask(arr)
+    ref = masker.upload_reference(arr["ref_nt16"])
+    no_ref = {k: v for k, v in arr.items() if k != "ref_nt16"}
+    db = masker.upload(no_ref, ref=ref)
+    try:
+        db.run()
+        got = db.download()
+    finally:
+        db.free()
+        ref.free()
+    for k in range(4):
+        assert np.array_equal(got[k], want[k]), k
+
+
+@pytest.mark.parametrize("seed,keep,err", [(5, False, 0.02), (6, True, 0.05)])
+def test_dense_scopes_match_oracle(masker, oracle, seed, keep, err):
+    """Thousands of observations per scope and one site seen by ~600 reads: the group kernel's
+    LDS list overflows into the group's global region; at 5 % errors (more mismatches than the
+    region holds, ~2 % of the bases) the region is split by key range."""
     from genomeanonymizer_amd.synth.batch import dense_batch
-    arr = dense_batch(seed, keep_hot_site=keep)
+    arr = dense_batch(seed, keep_hot_site=keep, error_rate=err)
     o_out, o_calls, o_bases, _ = oracle.mask(arr)
     assert o_calls[0] > 1000
-    for v in VARIANTS:
-        masker.set_variant(v)
-        out, calls, bases, _ = masker.mask(arr)
-        assert np.array_equal(calls, o_calls), v
-        assert np.array_equal(bases, o_bases), v
-        assert np.array_equal(out, o_out), v
-    masker.set_variant(0)
+    db = masker.upload(arr)
+    try:
+        db.run()
+        out, calls, bases, _ = db.download()
+        paths = db.path_counts()
+    finally:
+        db.free()
+    assert np.array_equal(calls, o_calls)
+    assert np.array_equal(bases, o_bases)
+    assert np.array_equal(out, o_out)
+    assert paths["region_passes"] > 0, paths
+    assert (paths["key_range_splits"] > 0) == (err > 0.04), paths
 
 
 @pytest.mark.parametrize("seed", [5, 6])
@@ -116,13 +152,10 @@ def test_long_reads_match_oracle(masker, oracle, seed):
     assert info["max_span"] > 16384
     o_out, o_calls, o_bases, o_tot = oracle.mask(arr)
     assert o_calls.sum() > 100
-    for v in MAIN:
-        masker.set_variant(v)
-        out, calls, bases, tot = masker.mask(arr)
-        assert np.array_equal(calls, o_calls), v
-        assert np.array_equal(bases, o_bases), v
-        assert np.array_equal(out, o_out), v
-    masker.set_variant(0)
+    out, calls, bases, tot = masker.mask(arr)
+    assert np.array_equal(calls, o_calls)
+    assert np.array_equal(bases, o_bases)
+    assert np.array_equal(out, o_out)
 
 
 def test_deep_coverage_short_reads_match_oracle(masker, oracle):
@@ -131,28 +164,57 @@ def test_deep_coverage_short_reads_match_oracle(masker, oracle):
     from genomeanonymizer_amd.synth.batch import config2_batch
     arr, info = config2_batch(n_reads=800_000, genome=2_000_000, n_contigs=2, n_windows=600, n_germline=2_000)
     o_out, o_calls, o_bases, _ = oracle.mask(arr)
-    for v in MAIN:
-        masker.set_variant(v)
-        out, calls, bases, tot = masker.mask(arr)
-        assert np.array_equal(calls, o_calls), v
-        assert np.array_equal(bases, o_bases), v
-        assert np.array_equal(out, o_out), v
-    masker.set_variant(0)
+    out, calls, bases, tot = masker.mask(arr)
+    assert np.array_equal(calls, o_calls)
+    assert np.array_equal(bases, o_bases)
+    assert np.array_equal(out, o_out)
 
 
-def test_hip_rare_and_wide_paths_exercised(masker):
+def test_hip_huge_scopes_tile_path_matches_oracle(masker, oracle):
+    """Scopes wider than 2^20 positions take the LDS tile path (k_tile_large + k_mask_large), and
+    tiles meeting IUPAC/'=' bases re-run on the 16-code tally; both equal the oracle."""
     from genomeanonymizer_amd.synth.batch import random_batch
-    arr = random_batch(8, n_scopes=30, rare_frac=0.3, wide_scopes=4)
-    masker.set_variant(6)     # the persistent-wave kernel re-runs rare scopes on a 16-code tally
+    arr = random_batch(8, n_scopes=12, rare_frac=0.3, wide_scopes=2, wide_span=(1_100_000, 1_200_000))
+    o_out, o_calls, o_bases, o_tot = oracle.mask(arr)
     db = masker.upload(arr)
-    db.run()
-    db.sync()
-    info = db.info()
-    tot = db.totals()
-    db.free()
-    masker.set_variant(0)
-    assert info["large_scopes"] >= 1 and info["large_tiles"] >= 2
-    assert tot[5] >= 1, "no scope went through the 16-code re-run"
+    try:
+        db.run()
+        out, calls, bases, tot = db.download()
+        info = db.info()
+    finally:
+        db.free()
+    assert info["huge_scopes"] == 2 and info["huge_tiles"] >= 2 * 67
+    assert tot[5] >= 1, "no tile went through the 16-code re-run"
+    assert np.array_equal(calls, o_calls) and np.array_equal(bases, o_bases)
+    written = arr["write_scope"] >= 0
+    L = (arr["read_len"].astype(np.int64) + 1) // 2
+    for r in np.nonzero(written)[0]:
+        o, n = int(arr["seq_off"][r]), int(L[r])
+        assert np.array_equal(out[o:o + n], o_out[o:o + n]), r
+
+
+def test_hip_configs2_density_matches_oracle(masker, oracle):
+    """BASELINE configs[2] density on a slice the oracle covers: 30x tumor + 30x normal 150 bp
+    reads, a germline het SNP every ~37 bp (an ~80 M-site set on 3 Gb), a window every 10 kb
+    (2.4 M reads, 6 Mb). Window scopes hold ~860 reads and ~1,700 observations, gap union scopes
+    several thousand: the group kernel's LDS lists overflow into the global region path."""
+    from genomeanonymizer_amd.synth.batch import config2_batch
+    arr, info = config2_batch(n_reads=2_400_000, genome=6_000_000, n_contigs=2, n_windows=600,
+                              n_germline=162_000, seed=12, window_spacing=10_000)
+    assert info["germline_snps"] > 150_000
+    o_out, o_calls, o_bases, o_tot = oracle.mask(arr)
+    db = masker.upload(arr)
+    try:
+        db.run()
+        out, calls, bases, tot = db.download()
+        paths = db.path_counts()
+    finally:
+        db.free()
+    assert np.array_equal(calls, o_calls)
+    assert np.array_equal(bases, o_bases)
+    assert np.array_equal(out, o_out)
+    assert o_bases.sum() > 100_000
+    assert paths["region_passes"] > 0, paths
 
 
 @pytest.mark.parametrize("name", ["tiny", "edge", "config1"])
@@ -191,14 +253,12 @@ def test_hip_config2_matches_oracle(masker, oracle):
     o_out, o_calls, o_bases, o_tot = oracle.mask(arr)
     L = (arr["read_len"].astype(np.int64) + 1) // 2
     assert np.all(L == 75)
-    for v in MAIN:
-        masker.set_variant(v)
-        out, calls, bases, tot = masker.mask(arr)
-        assert np.array_equal(calls, o_calls), v
-        assert np.array_equal(bases, o_bases), v
-        assert np.array_equal(out, o_out), v
-        assert tot[2] == info["reads"]
-    masker.set_variant(0)
+    out, calls, bases, tot = masker.mask(arr)
+    assert np.array_equal(calls, o_calls)
+    assert np.array_equal(bases, o_bases)
+    assert np.array_equal(out, o_out)
+    assert tot[2] == info["reads"]
+
 
 
 @pytest.mark.parametrize("layout", ["dataset_major", "shuffled"])

@@ -120,7 +120,7 @@ struct ganon_dbatch {
   ganon_dev::DBuf b_ref_start, b_read_len, b_seq_off, b_cig_off, b_n_cig, b_dataset, b_write_scope, b_seq, b_cigar,
       b_incid_off, b_incid_read, b_span_start, b_span_len, b_ref_off, b_keep_pos, b_keep_code;
   // derived layer
-  ganon_dev::DBuf b_read_end, b_rseg, b_rbase, b_seen, b_cost, b_cost_scan, b_gid, b_gs0, b_lo, b_lo_idx, b_lo_sorted,
+  ganon_dev::DBuf b_read_end, b_seen, b_cursor, b_gs0, b_lo, b_lo_idx, b_lo_sorted,
       b_lo_idx_sorted, b_groups, b_seg4, b_grp_part, b_far, b_gokey, b_gopay, b_gtkey, b_gtflag, b_scan_tmp, b_out,
       b_scope_calls, b_scope_bases, b_small;   // b_small: totals, static totals, counters, acc, status, errors
   uint8_t *out = nullptr;
@@ -131,6 +131,7 @@ struct ganon_dbatch {
   ganon_dev::PrepErr *err = nullptr;
   unsigned long long *plan_info = nullptr;   // [0] far nibbles, [1] huge scopes, [2] written reads
   unsigned long long *paths = nullptr;       // GrpAux::paths (since upload)
+  unsigned long long *cursor = nullptr;      // k_prep_emit allocation counters and their bases (b_cursor)
   ganon_dev::GrpAux *aux = nullptr;
   // plan of the current contents (device prep, sized at upload)
   int32_t n_groups = 0, group_target = 512;
@@ -152,7 +153,7 @@ namespace ganon_prep {
 
 // Validate the raw layer on the device, plan the derived layer (group count, segment count,
 // overflow regions, far-mask capacity) and size its buffers. Synchronous (upload time).
-int plan(ganon_ctx *ctx, ganon_dbatch *db);
+int plan(ganon_ctx *ctx, ganon_dbatch *db, const int64_t *host_incid_off);
 // Rebuild every derived array from the raw layer (async on the stream): the first half of
 // every ganon_batch_run.
 int run(ganon_ctx *ctx, ganon_dbatch *db);

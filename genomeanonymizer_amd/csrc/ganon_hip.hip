@@ -1133,8 +1133,7 @@ void free_batch(ganon_dbatch *db) {
   DBuf *bufs[] = {&db->b_ref_start, &db->b_read_len, &db->b_seq_off, &db->b_cig_off, &db->b_n_cig, &db->b_dataset,
                   &db->b_write_scope, &db->b_seq, &db->b_cigar, &db->b_incid_off, &db->b_incid_read,
                   &db->b_span_start, &db->b_span_len, &db->b_ref_off, &db->b_keep_pos, &db->b_keep_code,
-                  &db->b_read_end, &db->b_rseg, &db->b_rbase, &db->b_seen, &db->b_cost, &db->b_cost_scan, &db->b_gid,
-                  &db->b_gs0, &db->b_lo, &db->b_lo_idx, &db->b_lo_sorted, &db->b_lo_idx_sorted, &db->b_groups,
+                  &db->b_read_end, &db->b_seen, &db->b_cursor, &db->b_gs0, &db->b_lo, &db->b_lo_idx, &db->b_lo_sorted, &db->b_lo_idx_sorted, &db->b_groups,
                   &db->b_seg4, &db->b_grp_part, &db->b_far, &db->b_gokey, &db->b_gopay, &db->b_gtkey, &db->b_gtflag,
                   &db->b_scan_tmp, &db->b_out, &db->b_scope_calls, &db->b_scope_bases, &db->b_small};
   for (DBuf *b : bufs) free_buf(*b);
@@ -1362,7 +1361,7 @@ int load_batch(ganon_ctx *ctx, ganon_dbatch *db, const ganon_batch *b, const gan
     return rc;
   // bytes outside every read are never written by the masking kernels: make them defined
   HIP_OR_FAIL(hipMemsetAsync(db->out, 0, (size_t)b->seq_bytes + 16, ctx->stream));
-  if ((rc = ganon_prep::plan(ctx, db))) return rc;
+  if ((rc = ganon_prep::plan(ctx, db, b->scope_incid_off))) return rc;
   if ((rc = plan_huge(ctx, db, b))) return rc;
   const GrpAux a{db->scope_calls,
                  db->scope_bases,

@@ -11,21 +11,19 @@
 // scope writes the read) — that k_group (ganon_hip.hip) streams in 16-base chunks.
 //
 // Kernels (integer work, HBM/latency bound, no MFMA), in launch order:
-//   k_prep_reads    thread per read: CIGAR walk -> segments, aligned bases, bam_endpos; at upload
-//                   also every per-read check of the old host validation (no host loop remains);
-//   k_prep_scopes   workgroup per 256 consecutive scopes: their incidences are one contiguous
-//                   CSR range, scope of an incidence by binary search in LDS; per-scope cost
-//                   (segments + a per-scope weight that caps a group at 256 scopes) and overflow
-//                   region size, LDS 64-bit atomics;
-//   scans           rocPRIM device scans: exclusive prefix of (cost, region) over scopes, then
-//                   the group index (a group = scopes whose cost prefix falls in one bucket of
-//                   group_target units);
-//   k_prep_emit     workgroup per group: scope metadata staged in LDS, each thread walks one
-//                   incidence's CIGAR (segments of short CIGARs kept in registers, longer ones
-//                   walked again) around a block scan; segments whose reference range is all
-//                   ACGT fill the group's records from the front, the others from the back (the
-//                   group kernel reads the front half through the 2-bit reference); the lowest
-//                   buffer offset of the reads the group writes, per dataset (LDS atomicMin);
+//   (upload only) k_prep_reads / k_prep_scope_check / k_prep_incid_check / k_prep_seen_check:
+//                   every check of the round-1 host validation, on the device (no host loop);
+//   k_prep_groups   thread per scope: groups are the scopes whose (incidences + 3 per scope) prefix
+//                   — the CSR offsets themselves, no scan — falls in one bucket of group_target
+//                   units; the weight caps a group at 256 scopes;
+//   k_prep_emit     workgroup per group: scope metadata staged in LDS, each thread walks two
+//                   incidences' CIGARs (loads issued together), counts clean/dirty segments around
+//                   a block scan, takes the group's record range and overflow region from one of
+//                   256 allocation counters (bases fixed at upload), and writes the records (single-segment ones kept in registers
+//                   from the count); all-ACGT-reference segments fill the range from the front,
+//                   the others from the back (the group kernel reads the front part through the
+//                   2-bit reference); read_end; the lowest buffer offset of the reads the group
+//                   writes, per dataset (LDS atomicMin);
 //   k_prep_pieces   rocPRIM radix sort of those 2 x groups candidates; the sorted candidates,
 //                   aligned down to 128-byte lines, tile the output buffer — each group copies
 //                   at most two pieces.
@@ -46,16 +44,9 @@ using ganon_detail::KernelScope;
 namespace {
 
 constexpr int kPrepThreads = 256;
-constexpr int kScopeChunk = 256;      // scopes per k_prep_scopes workgroup
 constexpr unsigned long long kNone = ~0ull;
+constexpr int kCursors = 256;   // emit allocation counters (group g uses g % kCursors): no same-address hot spot
 constexpr int64_t kFarMax = int64_t(1) << 28;   // far-mask list entries at most
-
-struct Pair {
-  long long a, b;   // a: scope cost (segments + weight), b: overflow-region observations
-};
-struct PairPlus {
-  __host__ __device__ Pair operator()(const Pair &x, const Pair &y) const { return Pair{x.a + y.a, x.b + y.b}; }
-};
 
 // The raw arrays and sizes every prep kernel reads.
 struct Raw {
@@ -85,10 +76,11 @@ __device__ __forceinline__ bool is_aligned_op(int op) { return op == 0 || op == 
 // Aligned runs of a read (M/=/X ops, cut at kSegMaxLen, clipped to the read length): f(q, p, n)
 // with query offset q, contig position p, length n — the host planner's segments_of, round 1.
 template <typename F>
-__device__ __forceinline__ void walk_segments(const uint32_t *__restrict__ cig, int nc, int L, int ref_start, F &&f) {
+__device__ __forceinline__ void walk_segments(const uint32_t *__restrict__ cig, int nc, int L, int ref_start, uint32_t w0,
+                                              F &&f) {
   int q = 0, p = ref_start;
   for (int k = 0; k < nc && q < L; ++k) {
-    const uint32_t w = cig[k];
+    const uint32_t w = k == 0 ? w0 : cig[k];   // (the first word is loaded early by the caller)
     const int op = (int)(w & 0xF);
     const int len = (int)(w >> 4);
     if (is_aligned_op(op)) {
@@ -139,10 +131,8 @@ __global__ void __launch_bounds__(kPrepThreads) k_ref_blocks(const uint8_t *__re
   }
 }
 
-// ---- per read ------------------------------------------------------------------------------
-__global__ void __launch_bounds__(kPrepThreads) k_prep_reads(const Raw R, int validate, PrepErr *err,
-                                                             int32_t *__restrict__ rseg, int32_t *__restrict__ rbase,
-                                                             int32_t *__restrict__ read_end,
+// ---- per read (upload: validation) --------------------------------------------------------
+__global__ void __launch_bounds__(kPrepThreads) k_prep_reads(const Raw R, PrepErr *err, int32_t *__restrict__ read_end,
                                                              unsigned long long *written) {
   int n_written = 0;
   for (int64_t r = blockIdx.x * (int64_t)kPrepThreads + threadIdx.x; r < R.n_reads;
@@ -151,50 +141,29 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_reads(const Raw R, int va
     const int nc = R.n_cig[r];
     const int64_t co = R.cig_off[r];
     const int rs = R.ref_start[r];
-    if (validate) {
-      const int64_t so = R.seq_off[r];
-      const int ws = R.write_scope[r];
-      if (L < 0 || so < 0 || so + ((int64_t)L + 1) / 2 > R.seq_bytes) { report(err, kErrReadSeq, r); continue; }
-      if (nc < 0 || co < 0 || co + nc > R.n_cigar_ops) { report(err, kErrReadCigar, r); continue; }
-      if (R.dataset[r] > 1) report(err, kErrReadDataset, r);
-      if (ws < -1 || ws >= R.n_scopes) report(err, kErrReadWriteScope, r, ws);
-      if (L >= (1 << 24)) report(err, kErrReadLong, r);
-      n_written += ws >= 0;
-    }
-    int q = 0, nseg = 0, bases = 0;
+    const int64_t so = R.seq_off[r];
+    const int ws = R.write_scope[r];
+    if (L < 0 || so < 0 || so + ((int64_t)L + 1) / 2 > R.seq_bytes) { report(err, kErrReadSeq, r); continue; }
+    if (nc < 0 || co < 0 || co + nc > R.n_cigar_ops) { report(err, kErrReadCigar, r); continue; }
+    if (R.dataset[r] > 1) report(err, kErrReadDataset, r);
+    if (ws < -1 || ws >= R.n_scopes) report(err, kErrReadWriteScope, r, ws);
+    if (L >= (1 << 24)) report(err, kErrReadLong, r);
+    n_written += ws >= 0;
     int64_t rl = 0;
     for (int k = 0; k < nc; ++k) {
       const uint32_t w = R.cigar[co + k];
       const int op = (int)(w & 0xF);
-      const int len = (int)(w >> 4);
-      if (validate && op > 8) { report(err, kErrCigarOp, r, op); break; }
-      if (is_aligned_op(op)) {
-        if (q < L) {
-          const int n = min(len, L - q);
-          nseg += (n + kSegMaxLen - 1) / kSegMaxLen;
-          bases += n;
-        }
-        q += len;
-        rl += len;
-      } else if (op == 1 || op == 4) {
-        q += len;
-      } else if (op == 2 || op == 3) {
-        rl += len;
-      }
-      if (q > L) q = L;   // (the host walk stops emitting once q reaches L; clamp keeps q in int)
+      if (op > 8) { report(err, kErrCigarOp, r, op); break; }
+      if (is_aligned_op(op) || op == 2 || op == 3) rl += w >> 4;
     }
-    if (validate && (rs < 0 || rs + rl > INT32_MAX)) { report(err, kErrReadPos, r); continue; }
-    rseg[r] = nseg;
-    rbase[r] = bases;
+    if (rs < 0 || rs + rl > INT32_MAX) { report(err, kErrReadPos, r); continue; }
     read_end[r] = (int32_t)(rs + (rl > 0 ? rl : 1));
   }
-  if (validate) {
-    for (int o = 32; o > 0; o >>= 1) n_written += __shfl_xor(n_written, o);
-    if ((threadIdx.x & 63) == 0 && n_written) atomicAdd(written, (unsigned long long)n_written);
-  }
+  for (int o = 32; o > 0; o >>= 1) n_written += __shfl_xor(n_written, o);
+  if ((threadIdx.x & 63) == 0 && n_written) atomicAdd(written, (unsigned long long)n_written);
 }
 
-// ---- per scope (validation only) -----------------------------------------------------------
+// ---- per scope (upload: validation) --------------------------------------------------------
 __global__ void __launch_bounds__(kPrepThreads) k_prep_scope_check(const Raw R, PrepErr *err,
                                                                    unsigned long long *huge) {
   int n_huge = 0;
@@ -223,48 +192,6 @@ __device__ __forceinline__ int lds_upper(const long long *off, int n, long long 
   return lo;
 }
 
-// ---- per scope: cost and region size; at upload also the incidence checks --------------------
-__global__ void __launch_bounds__(kPrepThreads) k_prep_scopes(const Raw R, int validate, PrepErr *err,
-                                                              const int32_t *__restrict__ rseg,
-                                                              const int32_t *__restrict__ rbase,
-                                                              const int32_t *__restrict__ read_end,
-                                                              uint8_t *__restrict__ seen, long long weight,
-                                                              Pair *__restrict__ cost) {
-  __shared__ long long off[kScopeChunk + 1];
-  __shared__ unsigned long long lseg[kScopeChunk], lbase[kScopeChunk];
-  __shared__ int lss[kScopeChunk], lse[kScopeChunk];
-  __shared__ uint8_t lhuge[kScopeChunk];
-  const int tid = threadIdx.x;
-  const int s0 = blockIdx.x * kScopeChunk;
-  const int ns = min(kScopeChunk, R.n_scopes - s0);
-  for (int t = tid; t <= ns; t += kPrepThreads) off[t] = R.incid_off[s0 + t];
-  for (int t = tid; t < ns; t += kPrepThreads) {
-    lseg[t] = 0;
-    lbase[t] = 0;
-    lss[t] = R.span_start[s0 + t];
-    lse[t] = R.span_start[s0 + t] + R.span_len[s0 + t];
-    lhuge[t] = R.span_len[s0 + t] > kGrpMaxSpan;
-  }
-  __syncthreads();
-  const long long i0 = off[0], i1 = off[ns];
-  for (long long i = i0 + tid; i < i1; i += kPrepThreads) {
-    const int j = lds_upper(off, ns, i);
-    const int r = R.incid_read[i];
-    if (validate) {
-      if (r < 0 || r >= R.n_reads) { report(err, kErrIncidRead, i, r); continue; }
-      if (R.ref_start[r] < lss[j] || read_end[r] > lse[j]) { report(err, kErrIncidSpan, s0 + j, r); continue; }
-      if (R.write_scope[r] == s0 + j) seen[r] = 1;
-    }
-    if (!lhuge[j]) {
-      atomicAdd(&lseg[j], (unsigned long long)rseg[r]);
-      atomicAdd(&lbase[j], (unsigned long long)rbase[r]);
-    }
-  }
-  __syncthreads();
-  for (int t = tid; t < ns; t += kPrepThreads)
-    cost[s0 + t] = Pair{(long long)lseg[t] + weight, (long long)((lbase[t] + 47) / 48)};
-}
-
 __global__ void __launch_bounds__(kPrepThreads) k_prep_seen_check(const Raw R, const uint8_t *__restrict__ seen,
                                                                   PrepErr *err) {
   for (int64_t r = blockIdx.x * (int64_t)kPrepThreads + threadIdx.x; r < R.n_reads;
@@ -272,18 +199,40 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_seen_check(const Raw R, c
     if (R.write_scope[r] >= 0 && !seen[r]) report(err, kErrWriteScopeMissing, r, R.write_scope[r]);
 }
 
-// Group head flag of scope s: its cost prefix starts a new bucket of `target` units.
-struct HeadOp {
-  const Pair *P;
-  long long target;
-  __host__ __device__ int operator()(int s) const { return s == 0 || (P[s].a / target) != (P[s - 1].a / target); }
-};
+// Scope groups: the scopes whose cost prefix (incidences + `weight` per scope, no scan needed: the
+// CSR offsets are that prefix) falls in one bucket of `target` units. The weight bounds a group to
+// 256 scopes. A bucket skipped over by a scope with many incidences is an empty group.
+__device__ __forceinline__ int64_t group_of(const int64_t *__restrict__ incid_off, int64_t s, long long weight,
+                                            long long target) {
+  return (incid_off[s] + weight * s) / target;
+}
 
-// gs0[g] = first scope of group g.
-__global__ void __launch_bounds__(kPrepThreads) k_prep_groups(const Pair *__restrict__ P, const int32_t *__restrict__ gid,
-                                                              int n_scopes, long long target, int32_t *__restrict__ gs0) {
-  for (int64_t s = blockIdx.x * (int64_t)kPrepThreads + threadIdx.x; s < n_scopes; s += (int64_t)gridDim.x * kPrepThreads)
-    if (s == 0 || (P[s].a / target) != (P[s - 1].a / target)) gs0[gid[s] - 1] = (int32_t)s;
+// Upload only: every incidence's read index and span, and the write scope of every written read.
+__global__ void __launch_bounds__(kPrepThreads) k_prep_incid_check(const Raw R, const int32_t *__restrict__ read_end,
+                                                                   PrepErr *err, uint8_t *__restrict__ seen) {
+  for (int64_t s = blockIdx.x * (int64_t)kPrepThreads + threadIdx.x; s < R.n_scopes;
+       s += (int64_t)gridDim.x * kPrepThreads) {
+    const int ss = R.span_start[s], se = R.span_start[s] + R.span_len[s];
+    for (int64_t i = R.incid_off[s]; i < R.incid_off[s + 1]; ++i) {
+      const int r = R.incid_read[i];
+      if (r < 0 || r >= R.n_reads) { report(err, kErrIncidRead, i, r); continue; }
+      if (R.ref_start[r] < ss || read_end[r] > se) { report(err, kErrIncidSpan, s, r); continue; }
+      if (R.write_scope[r] == s) seen[r] = 1;
+    }
+  }
+}
+
+// gs0[b] = first scope of group b; cursors of the emit kernel's allocations reset.
+__global__ void __launch_bounds__(kPrepThreads) k_prep_groups(const Raw R, long long weight, long long target,
+                                                              int32_t *__restrict__ gs0,
+                                                              unsigned long long *__restrict__ cursor) {
+  const int64_t gt = blockIdx.x * (int64_t)kPrepThreads + threadIdx.x;
+  if (gt < 2 * kCursors) cursor[gt] = 0;
+  for (int64_t s = gt; s < R.n_scopes; s += (int64_t)gridDim.x * kPrepThreads) {
+    const int64_t b = group_of(R.incid_off, s, weight, target);
+    const int64_t bp = s == 0 ? -1 : group_of(R.incid_off, s - 1, weight, target);
+    for (int64_t x = bp + 1; x <= b; ++x) gs0[x] = (int32_t)s;
+  }
 }
 
 __device__ __forceinline__ int4 piece(int64_t a, int64_t b) {
@@ -319,7 +268,7 @@ __device__ __forceinline__ int64_t rec_lo(const int4 &x) { return (int64_t)(((ui
 __device__ __forceinline__ int64_t rec_hi(const int4 &x) { return (int64_t)(((uint64_t)(uint32_t)x.w << 32) | (uint32_t)x.z); }
 
 // Upload only: nibbles of written reads outside their group's pieces (the far-mask capacity).
-__global__ void __launch_bounds__(kPrepThreads) k_prep_farcap(const Raw R, const int32_t *__restrict__ gid,
+__global__ void __launch_bounds__(kPrepThreads) k_prep_farcap(const Raw R, long long weight, long long target,
                                                               const int4 *__restrict__ groups,
                                                               unsigned long long *far_nibs) {
   unsigned long long acc = 0;
@@ -327,7 +276,7 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_farcap(const Raw R, const
        r += (int64_t)gridDim.x * kPrepThreads) {
     const int ws = R.write_scope[r];
     if (ws < 0 || R.read_len[r] == 0 || R.span_len[ws] > kGrpMaxSpan) continue;
-    const int64_t g = gid[ws] - 1;
+    const int64_t g = group_of(R.incid_off, ws, weight, target);
     const int4 A = groups[kGrpRec * g + 2], Bp = groups[kGrpRec * g + 4];
     const int64_t r0 = R.seq_off[r], r1 = r0 + ((int64_t)R.read_len[r] + 1) / 2;
     const int64_t in = max((int64_t)0, min(r1, rec_hi(A)) - max(r0, rec_lo(A))) +
@@ -372,22 +321,63 @@ __device__ __forceinline__ void block_scan2(int a, int b, int &ea, int &eb, int 
   __syncthreads();
 }
 
-// Segment records, group records 0, 1, 3 and the partition candidates of group g: the lowest
-// buffer offset of the reads the group writes, per dataset (lo[2g + d], kNone if none; every
-// written read is "mine" in exactly one incidence, its write scope's).
-constexpr int kRegSegs = 2;   // segments of an incidence kept in registers between count and write
-__global__ void __launch_bounds__(kPrepThreads) k_prep_emit(const Raw R, const Pair *__restrict__ P,
-                                                            const int32_t *__restrict__ gs0, int n_groups,
-                                                            long long weight, const uint64_t *__restrict__ bad,
-                                                            int64_t n_blk, int4 *__restrict__ seg4,
+// Segment records, group records 0, 1, 3, read_end and the partition candidates of group g.
+// Pass 1 walks every incidence of the group (segments counted as clean/dirty, aligned bases), then
+// one atomic per group takes the group's segment range and overflow region from global cursors
+// (group ranges land in any order; results do not depend on it); pass 2 writes the records —
+// all-ACGT-reference segments from the front of the range, the others from the back. A group of at
+// most kEmitUnroll x 256 incidences (every window group of configs[1]) keeps pass 1's loads and
+// its single-segment records in registers; larger groups walk again in pass 2. `write` 0 (upload
+// plan): counts, region sizes and candidates only. The candidates are the lowest buffer offset of
+// the reads the group writes, per dataset (every written read is "mine" in one incidence).
+constexpr int kEmitUnroll = 2;   // incidences per thread and trip
+
+struct EmitInc {                 // one incidence of a trip, in registers
+  const uint32_t *cg;
+  int64_t so;
+  int r, j, ncig, L, rs, ds, wsc;
+  uint32_t w0;
+};
+
+__device__ __forceinline__ void emit_load(const Raw &R, const long long *off, const uint8_t *huge, int ns,
+                                          long long base, long long i1, EmitInc (&e)[kEmitUnroll]) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int u = 0; u < kEmitUnroll; ++u) {
+    const long long i = base + tid + kPrepThreads * u;
+    e[u].j = i < i1 ? lds_upper(off, ns, i) : 0;
+    e[u].r = i < i1 ? R.incid_read[i] : -1;
+  }
+#pragma unroll
+  for (int u = 0; u < kEmitUnroll; ++u) {
+    const int rr = e[u].r >= 0 ? e[u].r : 0;
+    e[u].cg = R.cigar + R.cig_off[rr];
+    e[u].ncig = e[u].r >= 0 ? R.n_cig[rr] : 0;
+    e[u].L = R.read_len[rr];
+    e[u].rs = R.ref_start[rr];
+    e[u].so = R.seq_off[rr];
+    e[u].ds = R.dataset[rr];
+    e[u].wsc = R.write_scope[rr];
+  }
+#pragma unroll
+  for (int u = 0; u < kEmitUnroll; ++u) e[u].w0 = e[u].ncig > 0 ? e[u].cg[0] : 0u;
+}
+
+__global__ void __launch_bounds__(kPrepThreads) k_prep_emit(const Raw R, const int32_t *__restrict__ gs0, int n_groups,
+                                                            int write, const uint64_t *__restrict__ bad, int64_t n_blk,
+                                                            int32_t *__restrict__ read_end, int4 *__restrict__ seg4,
                                                             int4 *__restrict__ groups, unsigned long long *__restrict__ lo,
-                                                            uint32_t *__restrict__ lo_idx) {
+                                                            uint32_t *__restrict__ lo_idx,
+                                                            unsigned long long *__restrict__ cursor,
+                                                            const unsigned long long *__restrict__ cursor_base) {
   __shared__ long long off[kGrpMaxScopes + 1];
   __shared__ long long ref0[kGrpMaxScopes];
   __shared__ int sstart[kGrpMaxScopes];
   __shared__ uint8_t huge[kGrpMaxScopes];
   __shared__ int ws[2 * kWaves];
-  __shared__ unsigned long long lmin[2];
+  __shared__ unsigned long long lmin[2], lbases, gbase[2];
+  __shared__ int4 stash[kPrepThreads * kEmitUnroll];       // one-trip groups: single-segment records
+  __shared__ uint8_t stash_clean[kPrepThreads * kEmitUnroll];
   const int tid = threadIdx.x;
   const int g = blockIdx.x;
   const int s0 = gs0[g];
@@ -400,91 +390,165 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_emit(const Raw R, const P
     huge[t] = R.span_len[s0 + t] > kGrpMaxSpan;
   }
   if (tid < 2) lmin[tid] = kNone;
-  const Pair p0 = P[s0], p1 = P[s1];
-  const int64_t seg_b = p0.a - weight * s0, seg_e = p1.a - weight * s1;
+  if (tid == 0) lbases = 0;
   __syncthreads();
   const long long i0 = off[0], i1 = off[ns];
-  int64_t run_c = 0, run_d = 0;   // records placed so far (clean from the front, dirty from the back)
-  for (long long base = i0; base < i1; base += kPrepThreads) {
-    const long long i = base + tid;
-    int j = 0, r = -1;
-    if (i < i1) {
-      j = lds_upper(off, ns, i);
-      r = huge[j] ? -1 : R.incid_read[i];
-    }
-    const uint32_t *cig = nullptr;
-    int ncig = 0, L = 0, rs = 0, nc = 0, nd = 0, ds = 0;
-    bool mine = false;
-    int64_t so = 0;
-    int4 keep[kRegSegs];
-    bool kclean[kRegSegs];
-    const int64_t r0 = ref0[j];
-    const int ss = sstart[j];
-    if (r >= 0) {
-      cig = R.cigar + R.cig_off[r];
-      ncig = R.n_cig[r];
-      L = R.read_len[r];
-      rs = R.ref_start[r];
-      so = R.seq_off[r];
-      ds = R.dataset[r];
-      mine = R.write_scope[r] == s0 + j;
-      if (mine && L > 0) atomicMin(&lmin[ds], (unsigned long long)so);
-      const uint32_t fl = ((uint32_t)ds << 30) | (mine ? kSegMine : 0u);
-      const int64_t qnib = 2 * so;
-      walk_segments(cig, ncig, L, rs, [&](int q, int p, int n) {
+  const bool one_trip = i1 - i0 <= (long long)kPrepThreads * kEmitUnroll;
+  int cnt[kEmitUnroll];        // (one trip) segments of this thread's incidences
+#pragma unroll
+  for (int u = 0; u < kEmitUnroll; ++u) cnt[u] = 0;   // an empty group runs no trip
+  int tot_c = 0, tot_d = 0, ec = 0, ed = 0;   // group totals; (one trip) this thread's offsets
+  unsigned long long mn0 = kNone, mn1 = kNone, bases = 0;   // this thread's candidates, aligned bases
+  // ---- pass 1: count
+  for (long long base = i0; base < i1; base += kPrepThreads * kEmitUnroll) {   // uniform trip count
+    EmitInc e[kEmitUnroll];
+    emit_load(R, off, huge, ns, base, i1, e);
+    int tnc = 0, tnd = 0;
+#pragma unroll
+    for (int u = 0; u < kEmitUnroll; ++u) {
+      cnt[u] = 0;
+      if (e[u].r < 0) continue;
+      const EmitInc &x = e[u];
+      const bool mine = x.wsc == s0 + x.j;
+      if (mine && x.L > 0) {
+        if (x.ds) mn1 = min(mn1, (unsigned long long)x.so);
+        else mn0 = min(mn0, (unsigned long long)x.so);
+      }
+      // bam_endpos (the tile path of huge scopes and the indel tally read it)
+      int64_t rl = 0;
+      for (int k = 0; k < x.ncig; ++k) {
+        const uint32_t w = k == 0 ? x.w0 : x.cg[k];
+        const int op = (int)(w & 0xF);
+        if (is_aligned_op(op) || op == 2 || op == 3) rl += w >> 4;
+      }
+      read_end[x.r] = (int32_t)(x.rs + (rl > 0 ? rl : 1));
+      if (huge[x.j]) continue;
+      const uint32_t fl = ((uint32_t)x.ds << 30) | (mine ? kSegMine : 0u);
+      const int64_t qnib = 2 * x.so, r0 = ref0[x.j];
+      const int ss = sstart[x.j], jl = x.j;
+      const int slot = tid + kPrepThreads * u;
+      int &n_ = cnt[u];
+      walk_segments(x.cg, x.ncig, x.L, x.rs, x.w0, [&](int q, int p, int n) {
         const uint64_t sq = (uint64_t)(qnib + q), rf = (uint64_t)(r0 + p);
         const bool clean = ref_clean(bad, n_blk, (int64_t)rf, n);
-        const int k = nc + nd;
-        if (k < kRegSegs) {
+        if (n_ == 0 && one_trip) {
           const uint32_t z = (uint32_t)((sq >> 32) & 0xFF) | ((uint32_t)((rf >> 32) & 0xFF) << 8) | ((uint32_t)n << 16) | fl;
-          keep[k] = make_int4((int)(uint32_t)sq, (int)(uint32_t)rf, (int)z, (int)((uint32_t)j | ((uint32_t)(p - ss) << 12)));
-          kclean[k] = clean;
+          stash[slot] = make_int4((int)(uint32_t)sq, (int)(uint32_t)rf, (int)z, (int)((uint32_t)jl | ((uint32_t)(p - ss) << 12)));
+          stash_clean[slot] = clean;
         }
-        if (clean) ++nc;
-        else ++nd;
+        ++n_;
+        if (clean) ++tnc;
+        else ++tnd;
+        bases += n;
       });
     }
-    int ec, ed, tc, td;
-    block_scan2(nc, nd, ec, ed, tc, td, ws);
-    if (r >= 0 && nc + nd) {
-      int64_t pc = seg_b + run_c + ec, pd = seg_e - 1 - (run_d + ed);
-      if (nc + nd <= kRegSegs) {
+    int tc, td;
+    block_scan2(tnc, tnd, ec, ed, tc, td, ws);
+    ec += tot_c;
+    ed += tot_d;
+    tot_c += tc;
+    tot_d += td;
+  }
+  // ---- candidates and aligned bases: wave reductions, one LDS atomic per wave
+  for (int o = 32; o > 0; o >>= 1) {
+    mn0 = min(mn0, (unsigned long long)__shfl_xor(mn0, o));
+    mn1 = min(mn1, (unsigned long long)__shfl_xor(mn1, o));
+    bases += __shfl_xor(bases, o);
+  }
+  if ((tid & 63) == 0) {
+    if (mn0 != kNone) atomicMin(&lmin[0], mn0);
+    if (mn1 != kNone) atomicMin(&lmin[1], mn1);
+    if (bases) atomicAdd(&lbases, bases);
+  }
+  __syncthreads();
+  // ---- the group's segment range and overflow region: sub-cursor g % kCursors, whose base the
+  //      upload plan fixed (the groups of a sub-cursor take their ranges in any order)
+  if (tid == 0) {
+    const int k = g % kCursors;
+    gbase[0] = cursor_base[k] + atomicAdd(&cursor[k], (unsigned long long)(tot_c + tot_d));
+    const unsigned long long cap = min((lbases + 47) / 48 + kGrpObs, (unsigned long long)(INT32_MAX / 2));
+    gbase[1] = (cursor_base[kCursors + k] + atomicAdd(&cursor[kCursors + k], cap)) | (cap << 40);
+  }
+  __syncthreads();
+  const int64_t seg_b = (int64_t)gbase[0], seg_e = seg_b + tot_c + tot_d;
+  // ---- pass 2: write (walks again where the stash does not hold the incidence's one record)
+  if (write) {
+    int64_t run_c = 0, run_d = 0;
+    for (long long base = i0; base < i1; base += kPrepThreads * kEmitUnroll) {
+      int xc = ec, xd = ed, tc = 0, td = 0;
+      int cc[kEmitUnroll], cd[kEmitUnroll];
+      EmitInc e[kEmitUnroll];
+      const bool reload = !one_trip || cnt[0] > 1 || cnt[1] > 1;
+      if (reload) emit_load(R, off, huge, ns, base, i1, e);
+      if (one_trip) {
 #pragma unroll
-        for (int k = 0; k < kRegSegs; ++k) {
-          if (k >= nc + nd) break;
-          if (kclean[k]) seg4[pc++] = keep[k];
-          else seg4[pd--] = keep[k];
+        for (int u = 0; u < kEmitUnroll; ++u) {
+          cc[u] = cnt[u] == 1 ? (int)stash_clean[tid + kPrepThreads * u] : 0;
+          cd[u] = cnt[u] == 1 ? 1 - cc[u] : 0;
+          if (cnt[u] > 1) {
+            const int64_t r0 = ref0[e[u].j];
+            int &c_ = cc[u], &d_ = cd[u];
+            walk_segments(e[u].cg, e[u].ncig, e[u].L, e[u].rs, e[u].w0, [&](int, int p, int n) {
+              if (ref_clean(bad, n_blk, r0 + p, n)) ++c_;
+              else ++d_;
+            });
+          }
         }
       } else {
-        const uint32_t fl = ((uint32_t)ds << 30) | (mine ? kSegMine : 0u);
-        const int64_t qnib = 2 * so;
-        walk_segments(cig, ncig, L, rs, [&](int q, int p, int n) {
+        int tnc = 0, tnd = 0;
+#pragma unroll
+        for (int u = 0; u < kEmitUnroll; ++u) {
+          cc[u] = cd[u] = 0;
+          if (e[u].r < 0 || huge[e[u].j]) continue;
+          const int64_t r0 = ref0[e[u].j];
+          int &c_ = cc[u], &d_ = cd[u];
+          walk_segments(e[u].cg, e[u].ncig, e[u].L, e[u].rs, e[u].w0, [&](int, int p, int n) {
+            if (ref_clean(bad, n_blk, r0 + p, n)) ++c_;
+            else ++d_;
+          });
+          tnc += c_;
+          tnd += d_;
+        }
+        block_scan2(tnc, tnd, xc, xd, tc, td, ws);
+      }
+      int64_t pc = seg_b + run_c + xc, pd = seg_e - 1 - (run_d + xd);
+#pragma unroll
+      for (int u = 0; u < kEmitUnroll; ++u) {
+        if (cc[u] + cd[u] == 0) continue;
+        if (one_trip && cnt[u] == 1) {
+          if (cc[u]) seg4[pc++] = stash[tid + kPrepThreads * u];
+          else seg4[pd--] = stash[tid + kPrepThreads * u];
+          continue;
+        }
+        const EmitInc &x = e[u];
+        const uint32_t fl = ((uint32_t)x.ds << 30) | (x.wsc == s0 + x.j ? kSegMine : 0u);
+        const int64_t qnib = 2 * x.so, r0 = ref0[x.j];
+        const int ss = sstart[x.j], jl = x.j;
+        walk_segments(x.cg, x.ncig, x.L, x.rs, x.w0, [&](int q, int p, int n) {
           const uint64_t sq = (uint64_t)(qnib + q), rf = (uint64_t)(r0 + p);
           const uint32_t z = (uint32_t)((sq >> 32) & 0xFF) | ((uint32_t)((rf >> 32) & 0xFF) << 8) | ((uint32_t)n << 16) | fl;
           const int4 rec = make_int4((int)(uint32_t)sq, (int)(uint32_t)rf, (int)z,
-                                     (int)((uint32_t)j | ((uint32_t)(p - ss) << 12)));
+                                     (int)((uint32_t)jl | ((uint32_t)(p - ss) << 12)));
           if (ref_clean(bad, n_blk, (int64_t)rf, n)) seg4[pc++] = rec;
           else seg4[pd--] = rec;
         });
       }
+      run_c += tc;
+      run_d += td;
     }
-    run_c += tc;
-    run_d += td;
   }
-  __syncthreads();
   if (tid < 2) {
     lo[2 * (int64_t)g + tid] = lmin[tid];
     lo_idx[2 * (int64_t)g + tid] = (uint32_t)(2 * g + tid);
   }
   if (tid == 0) {
-    const int64_t mid = seg_b + run_c;
-    const int64_t region = p0.b + (int64_t)kGrpObs * g;
-    const int64_t cap = min<int64_t>(p1.b - p0.b + kGrpObs, INT32_MAX / 2);
+    const int64_t mid = seg_b + tot_c;
+    const int64_t region = (int64_t)(gbase[1] & ((1ull << 40) - 1));
+    const int cap = (int)(gbase[1] >> 40);
     groups[kGrpRec * (int64_t)g] = make_int4(s0, s1, (int)(uint32_t)seg_b, (int)(uint32_t)((uint64_t)seg_b >> 32));
     groups[kGrpRec * (int64_t)g + 1] = make_int4((int)(uint32_t)seg_e, (int)(uint32_t)((uint64_t)seg_e >> 32),
                                                  (int)(uint32_t)mid, (int)(uint32_t)((uint64_t)mid >> 32));
-    groups[kGrpRec * (int64_t)g + 3] = make_int4((int)(uint32_t)region, (int)(uint32_t)((uint64_t)region >> 32),
-                                                 (int)cap, 0);
+    groups[kGrpRec * (int64_t)g + 3] = make_int4((int)(uint32_t)region, (int)(uint32_t)((uint64_t)region >> 32), cap, 0);
   }
 }
 
@@ -548,73 +612,29 @@ int check_err(ganon_ctx *ctx, ganon_dbatch *db) {
   return GANON_OK;
 }
 
-// Temp storage of the three rocPRIM calls for n scopes and c candidates.
-hipError_t scan_bytes(int64_t n, int64_t c, size_t &bytes) {
-  size_t a = 0, b = 0, d = 0;
-  hipError_t e = rocprim::exclusive_scan(nullptr, a, (Pair *)nullptr, (Pair *)nullptr, Pair{0, 0}, (size_t)n + 1,
-                                         PairPlus{}, 0);
-  if (e != hipSuccess) return e;
-  e = rocprim::inclusive_scan(nullptr, b, rocprim::make_transform_iterator(rocprim::make_counting_iterator<int>(0),
-                                                                          HeadOp{nullptr, 1}),
-                              (int32_t *)nullptr, (size_t)n, rocprim::plus<int32_t>(), 0);
-  if (e != hipSuccess) return e;
-  e = rocprim::radix_sort_pairs(nullptr, d, (unsigned long long *)nullptr, (unsigned long long *)nullptr,
-                                (uint32_t *)nullptr, (uint32_t *)nullptr, (size_t)c, 0, 40, 0);
-  bytes = std::max(std::max(a, b), d);
-  return e;
+// Temp storage of the candidate sort (c candidates).
+hipError_t sort_bytes(int64_t c, size_t &bytes) {
+  return rocprim::radix_sort_pairs(nullptr, bytes, (unsigned long long *)nullptr, (unsigned long long *)nullptr,
+                                   (uint32_t *)nullptr, (uint32_t *)nullptr, (size_t)c, 0, 40, 0);
 }
 
-// The planning kernels shared by plan() and run(): scopes -> scans -> groups -> pieces.
-int launch_scopes_groups(ganon_ctx *ctx, ganon_dbatch *db, const Raw &R, int validate) {
-  hipStream_t st = ctx->stream;
-  const long long w = weight_of(db->group_target);
-  Pair *cost = static_cast<Pair *>(db->b_cost.p);
-  Pair *P = static_cast<Pair *>(db->b_cost_scan.p);
-  int32_t *gid = static_cast<int32_t *>(db->b_gid.p);
-  {
-    KernelScope ks(ctx, "prep_scopes");
-    if (db->n_scopes) {
-      hipLaunchKernelGGL(k_prep_scopes, dim3((unsigned)((db->n_scopes + kScopeChunk - 1) / kScopeChunk)),
-                         dim3(kPrepThreads), 0, st, R, validate, db->err, static_cast<const int32_t *>(db->b_rseg.p),
-                         static_cast<const int32_t *>(db->b_rbase.p), db->B.read_end,
-                         static_cast<uint8_t *>(db->b_seen.p), w, cost);
-      int rc = check_launch(ctx, "k_prep_scopes");
-      if (rc) return rc;
-    }
-    HIP_OR_FAIL(hipMemsetAsync(cost + db->n_scopes, 0, sizeof(Pair), st));
-  }
-  if (validate) {
-    hipLaunchKernelGGL(k_prep_seen_check, dim3(grid_for(db->n_reads)), dim3(kPrepThreads), 0, st, R,
-                       static_cast<const uint8_t *>(db->b_seen.p), db->err);
-    int rc = check_err(ctx, db);
-    if (rc) return rc;
-  }
-  {
-    KernelScope ks(ctx, "prep_scan");
-    size_t bytes = db->scan_tmp_bytes;
-    if (rocprim::exclusive_scan(db->b_scan_tmp.p, bytes, cost, P, Pair{0, 0}, (size_t)db->n_scopes + 1, PairPlus{},
-                                st) != hipSuccess)
-      return fail(ctx, GANON_E_DEVICE, "prep: scope scan failed");
-    if (db->n_scopes) {
-      bytes = db->scan_tmp_bytes;
-      if (rocprim::inclusive_scan(db->b_scan_tmp.p, bytes,
-                                  rocprim::make_transform_iterator(rocprim::make_counting_iterator<int>(0),
-                                                                   HeadOp{P, (long long)db->group_target}),
-                                  gid, (size_t)db->n_scopes, rocprim::plus<int32_t>(), st) != hipSuccess)
-        return fail(ctx, GANON_E_DEVICE, "prep: group scan failed");
-    }
-  }
-  return GANON_OK;
-}
-
-// Group starts, then (after the emit kernel wrote the candidates) sort + pieces.
-int launch_groups(ganon_ctx *ctx, ganon_dbatch *db) {
-  if (!db->n_groups) return GANON_OK;
+int launch_groups(ganon_ctx *ctx, ganon_dbatch *db, const Raw &R) {
   KernelScope ks(ctx, "prep_groups");
-  hipLaunchKernelGGL(k_prep_groups, dim3(grid_for(db->n_scopes)), dim3(kPrepThreads), 0, ctx->stream,
-                     static_cast<const Pair *>(db->b_cost_scan.p), static_cast<const int32_t *>(db->b_gid.p),
-                     db->n_scopes, (long long)db->group_target, static_cast<int32_t *>(db->b_gs0.p));
+  hipLaunchKernelGGL(k_prep_groups, dim3(grid_for(std::max<int64_t>(db->n_scopes, 2 * kCursors))), dim3(kPrepThreads), 0,
+                     ctx->stream, R, weight_of(db->group_target), (long long)db->group_target,
+                     static_cast<int32_t *>(db->b_gs0.p), db->cursor);
   return check_launch(ctx, "k_prep_groups");
+}
+
+int launch_emit(ganon_ctx *ctx, ganon_dbatch *db, const Raw &R, int write) {
+  if (!db->n_groups) return GANON_OK;
+  KernelScope ks(ctx, "prep_emit");
+  hipLaunchKernelGGL(k_prep_emit, dim3((unsigned)db->n_groups), dim3(kPrepThreads), 0, ctx->stream, R,
+                     static_cast<const int32_t *>(db->b_gs0.p), db->n_groups, write, db->ref->bad, db->ref->n_blk,
+                     const_cast<int32_t *>(db->B.read_end), static_cast<int4 *>(db->b_seg4.p),
+                     static_cast<int4 *>(db->b_groups.p), static_cast<unsigned long long *>(db->b_lo.p),
+                     static_cast<uint32_t *>(db->b_lo_idx.p), db->cursor, db->cursor + 2 * kCursors);
+  return check_launch(ctx, "k_prep_emit");
 }
 
 int launch_pieces(ganon_ctx *ctx, ganon_dbatch *db) {
@@ -633,26 +653,6 @@ int launch_pieces(ganon_ctx *ctx, ganon_dbatch *db) {
   hipLaunchKernelGGL(k_prep_pieces, dim3(grid_for(n_cand)), dim3(kPrepThreads), 0, st, lo_s, idx_s, n_cand,
                      db->seq_bytes, static_cast<int4 *>(db->b_groups.p));
   return check_launch(ctx, "k_prep_pieces");
-}
-
-int launch_reads(ganon_ctx *ctx, ganon_dbatch *db, const Raw &R, int validate) {
-  KernelScope ks(ctx, "prep_reads");
-  if (!db->n_reads) return GANON_OK;
-  hipLaunchKernelGGL(k_prep_reads, dim3(grid_for(db->n_reads)), dim3(kPrepThreads), 0, ctx->stream, R, validate,
-                     db->err, static_cast<int32_t *>(db->b_rseg.p), static_cast<int32_t *>(db->b_rbase.p),
-                     const_cast<int32_t *>(db->B.read_end), db->plan_info + 2);
-  return check_launch(ctx, "k_prep_reads");
-}
-
-int launch_emit(ganon_ctx *ctx, ganon_dbatch *db, const Raw &R) {
-  if (!db->n_groups) return GANON_OK;
-  KernelScope ks(ctx, "prep_emit");
-  hipLaunchKernelGGL(k_prep_emit, dim3((unsigned)db->n_groups), dim3(kPrepThreads), 0, ctx->stream, R,
-                     static_cast<const Pair *>(db->b_cost_scan.p), static_cast<const int32_t *>(db->b_gs0.p),
-                     db->n_groups, weight_of(db->group_target), db->ref->bad, db->ref->n_blk,
-                     static_cast<int4 *>(db->b_seg4.p), static_cast<int4 *>(db->b_groups.p),
-                     static_cast<unsigned long long *>(db->b_lo.p), static_cast<uint32_t *>(db->b_lo_idx.p));
-  return check_launch(ctx, "k_prep_emit");
 }
 
 }  // namespace
@@ -678,66 +678,77 @@ int grow(ganon_ctx *ctx, DBuf &b, size_t bytes) {
   return GANON_OK;
 }
 
-int plan(ganon_ctx *ctx, ganon_dbatch *db) {
+int plan(ganon_ctx *ctx, ganon_dbatch *db, const int64_t *host_incid_off) {
   hipStream_t st = ctx->stream;
   int rc;
   const int64_t nr = db->n_reads, ns = db->n_scopes;
-  int32_t *p32 = nullptr;
-  if ((rc = grow_n(ctx, db->b_read_end, nr, &p32))) return rc;
-  db->B.read_end = p32;
-  if ((rc = grow_n(ctx, db->b_rseg, nr, &p32)) || (rc = grow_n(ctx, db->b_rbase, nr, &p32))) return rc;
+  int32_t *read_end = nullptr;
+  if ((rc = grow_n(ctx, db->b_read_end, nr, &read_end))) return rc;
+  db->B.read_end = read_end;
   uint8_t *seen = nullptr;
   if ((rc = grow_n(ctx, db->b_seen, nr, &seen))) return rc;
-  Pair *pp = nullptr;
-  if ((rc = grow_n(ctx, db->b_cost, ns + 1, &pp)) || (rc = grow_n(ctx, db->b_cost_scan, ns + 1, &pp))) return rc;
-  if ((rc = grow_n(ctx, db->b_gid, ns, &p32))) return rc;
-  // temp storage for the scans (candidates: at most one group per scope, two per group)
-  size_t tmp = 0;
-  if (scan_bytes(ns, 2 * ns, tmp) != hipSuccess) return fail(ctx, GANON_E_DEVICE, "prep: rocPRIM sizing failed");
-  uint8_t *t8 = nullptr;
-  if ((rc = grow_n(ctx, db->b_scan_tmp, tmp, &t8))) return rc;
-  db->scan_tmp_bytes = tmp;
+  if ((rc = grow_n(ctx, db->b_cursor, 4 * kCursors, &db->cursor))) return rc;   // counters, then bases
   const Raw R = raw_of(db);
   HIP_OR_FAIL(hipMemsetAsync(db->err, 0, sizeof(PrepErr), st));
   HIP_OR_FAIL(hipMemsetAsync(db->plan_info, 0, 4 * sizeof(unsigned long long), st));
   HIP_OR_FAIL(hipMemsetAsync(seen, 0, (size_t)std::max<int64_t>(nr, 1), st));
   // 1. per-read and per-scope checks (every later kernel relies on them)
-  if ((rc = launch_reads(ctx, db, R, 1))) return rc;
+  if (nr) hipLaunchKernelGGL(k_prep_reads, dim3(grid_for(nr)), dim3(kPrepThreads), 0, st, R, db->err, read_end,
+                             db->plan_info + 2);
   if (ns) hipLaunchKernelGGL(k_prep_scope_check, dim3(grid_for(ns)), dim3(kPrepThreads), 0, st, R, db->err,
                              db->plan_info + 1);
-  if ((rc = check_launch(ctx, "k_prep_scope_check")) || (rc = check_err(ctx, db))) return rc;
-  // 2. incidences (checked inside), scans
-  if ((rc = launch_scopes_groups(ctx, db, R, 1))) return rc;
-  int32_t ng = 0;
-  Pair total{0, 0};
-  if (ns) HIP_OR_FAIL(hipMemcpyAsync(&ng, static_cast<int32_t *>(db->b_gid.p) + ns - 1, 4, hipMemcpyDeviceToHost, st));
-  HIP_OR_FAIL(hipMemcpyAsync(&total, static_cast<Pair *>(db->b_cost_scan.p) + ns, sizeof total, hipMemcpyDeviceToHost, st));
-  HIP_OR_FAIL(hipStreamSynchronize(st));
-  db->n_groups = ng;
-  db->n_seg = total.a - weight_of(db->group_target) * ns;
-  db->region = total.b + (int64_t)kGrpObs * ng;
-  // 3. derived buffers sized by the scans; groups, segments, pieces, far-mask capacity
+  if ((rc = check_launch(ctx, "k_prep_reads/k_prep_scope_check")) || (rc = check_err(ctx, db))) return rc;
+  // 2. incidences, write scopes
+  if (ns) hipLaunchKernelGGL(k_prep_incid_check, dim3(grid_for(ns)), dim3(kPrepThreads), 0, st, R, read_end, db->err,
+                             seen);
+  if (nr) hipLaunchKernelGGL(k_prep_seen_check, dim3(grid_for(nr)), dim3(kPrepThreads), 0, st, R, seen, db->err);
+  if ((rc = check_launch(ctx, "k_prep_incid_check/k_prep_seen_check")) || (rc = check_err(ctx, db))) return rc;
+  // 3. groups (their number follows from the host's CSR offsets), then a counting emit pass sizes
+  //    the segment records and overflow regions
+  const long long w = weight_of(db->group_target);
+  const int64_t ng = ns ? (host_incid_off[ns - 1] + w * (ns - 1)) / db->group_target + 1 : 0;
+  if (ng > INT32_MAX / kGrpRec) return fail(ctx, GANON_E_ARG, "batch too large: %lld scope groups", (long long)ng);
+  db->n_groups = (int32_t)ng;
+  int32_t *p32 = nullptr;
   int4 *grp = nullptr;
-  if ((rc = grow_n(ctx, db->b_groups, (size_t)kGrpRec * ng, &grp))) return rc;
-  if ((rc = grow_n(ctx, db->b_gs0, ng, &p32))) return rc;
   unsigned long long *u64 = nullptr;
   uint32_t *u32 = nullptr;
-  if ((rc = grow_n(ctx, db->b_lo, 2 * (size_t)ng, &u64)) || (rc = grow_n(ctx, db->b_lo_sorted, 2 * (size_t)ng, &u64)) ||
+  if ((rc = grow_n(ctx, db->b_gs0, ng, &p32)) || (rc = grow_n(ctx, db->b_groups, (size_t)kGrpRec * ng, &grp)) ||
+      (rc = grow_n(ctx, db->b_grp_part, 2 * (size_t)ng, &p32)) ||
+      (rc = grow_n(ctx, db->b_lo, 2 * (size_t)ng, &u64)) || (rc = grow_n(ctx, db->b_lo_sorted, 2 * (size_t)ng, &u64)) ||
       (rc = grow_n(ctx, db->b_lo_idx, 2 * (size_t)ng, &u32)) ||
       (rc = grow_n(ctx, db->b_lo_idx_sorted, 2 * (size_t)ng, &u32)))
     return rc;
-  int4 *s4 = nullptr;
-  if ((rc = grow_n(ctx, db->b_seg4, (size_t)db->n_seg, &s4))) return rc;
-  if ((rc = grow_n(ctx, db->b_grp_part, 2 * (size_t)ng, &p32))) return rc;
-  if ((rc = launch_groups(ctx, db)) || (rc = launch_emit(ctx, db, R)) || (rc = launch_pieces(ctx, db))) return rc;
+  size_t tmp = 0;
+  if (sort_bytes(2 * ng, tmp) != hipSuccess) return fail(ctx, GANON_E_DEVICE, "prep: rocPRIM sizing failed");
+  uint8_t *t8 = nullptr;
+  if ((rc = grow_n(ctx, db->b_scan_tmp, tmp, &t8))) return rc;
+  db->scan_tmp_bytes = tmp;
+  HIP_OR_FAIL(hipMemsetAsync(db->cursor + 2 * kCursors, 0, 2 * kCursors * sizeof(unsigned long long), st));
+  if ((rc = launch_groups(ctx, db, R)) || (rc = launch_emit(ctx, db, R, 0)) || (rc = launch_pieces(ctx, db))) return rc;
   if (ng && nr)
-    hipLaunchKernelGGL(k_prep_farcap, dim3(grid_for(nr)), dim3(kPrepThreads), 0, st, R,
-                       static_cast<const int32_t *>(db->b_gid.p), static_cast<const int4 *>(db->b_groups.p),
-                       db->plan_info);
+    hipLaunchKernelGGL(k_prep_farcap, dim3(grid_for(nr)), dim3(kPrepThreads), 0, st, R, w, (long long)db->group_target,
+                       static_cast<const int4 *>(db->b_groups.p), db->plan_info);
   if ((rc = check_launch(ctx, "k_prep_farcap"))) return rc;
   unsigned long long info[4] = {0, 0, 0, 0};
+  std::vector<unsigned long long> cur(4 * kCursors, 0);
   HIP_OR_FAIL(hipMemcpyAsync(info, db->plan_info, sizeof info, hipMemcpyDeviceToHost, st));
+  HIP_OR_FAIL(hipMemcpyAsync(cur.data(), db->cursor, 2 * kCursors * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
   HIP_OR_FAIL(hipStreamSynchronize(st));
+  // sub-cursor bases: exclusive prefix of the counting pass's totals (deterministic per sub-cursor)
+  unsigned long long tseg = 0, treg = 0;
+  for (int k = 0; k < kCursors; ++k) {
+    cur[2 * kCursors + k] = tseg;
+    cur[3 * kCursors + k] = treg;
+    tseg += cur[k];
+    treg += cur[kCursors + k];
+  }
+  HIP_OR_FAIL(hipMemcpyAsync(db->cursor + 2 * kCursors, cur.data() + 2 * kCursors, 2 * kCursors * sizeof(unsigned long long),
+                             hipMemcpyHostToDevice, st));
+  HIP_OR_FAIL(hipStreamSynchronize(st));
+  db->n_seg = (int64_t)tseg;
+  db->region = (int64_t)treg;
+  if (treg >= (1ull << 40)) return fail(ctx, GANON_E_ARG, "batch too large: overflow regions over 2^40 entries");
   // far masks: at most one per nibble of a written read outside its group's pieces. That bound is
   // exact but loose (masks are the TN-mismatching nibbles only), and a batch whose scopes are not
   // in genome order can put most written bytes outside their pieces: the list is capped at 2^28
@@ -745,6 +756,8 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db) {
   db->far_cap = std::min<int64_t>((int64_t)info[0], kFarMax);
   db->n_huge_scopes = (int32_t)info[1];
   db->n_written = (int64_t)info[2];
+  int4 *s4 = nullptr;
+  if ((rc = grow_n(ctx, db->b_seg4, (size_t)db->n_seg, &s4))) return rc;
   if ((rc = grow_n(ctx, db->b_far, (size_t)db->far_cap, &u64))) return rc;
   if ((rc = grow_n(ctx, db->b_gokey, (size_t)db->region, &u64)) || (rc = grow_n(ctx, db->b_gopay, (size_t)db->region, &u64)) ||
       (rc = grow_n(ctx, db->b_gtkey, 2 * (size_t)db->region + 64, &u64)) ||
@@ -756,9 +769,8 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db) {
 int run(ganon_ctx *ctx, ganon_dbatch *db) {
   const Raw R = raw_of(db);
   int rc;
-  if ((rc = launch_reads(ctx, db, R, 0))) return rc;
-  if ((rc = launch_scopes_groups(ctx, db, R, 0))) return rc;
-  if ((rc = launch_groups(ctx, db)) || (rc = launch_emit(ctx, db, R))) return rc;
+  if (!db->n_groups) return GANON_OK;
+  if ((rc = launch_groups(ctx, db, R)) || (rc = launch_emit(ctx, db, R, 1))) return rc;
   return launch_pieces(ctx, db);
 }
 

@@ -17,6 +17,11 @@ namespace {
 
 thread_local std::string g_err;
 
+// memcpy of n bytes; n == 0 (an empty blob's data() may be null) copies nothing
+inline void copy_bytes(void *dst, const void *src, size_t n) {
+  if (n) std::memcpy(dst, src, n);
+}
+
 struct Block {
   int64_t in_off;   // compressed payload offset in the file buffer
   int32_t in_len;   // compressed payload length
@@ -58,9 +63,7 @@ static int set_err(const std::string &m) {
 
 GANON_HOST_API const char *ganon_host_last_error(void) { return g_err.c_str(); }
 
-GANON_HOST_API int ganon_bam_open(const char *path, int threads, ganon_bam **out) {
-  if (!path || !out) return set_err("null argument");
-  *out = nullptr;
+static int bam_open_impl(const char *path, int threads, ganon_bam **out) {
   FILE *fh = std::fopen(path, "rb");
   if (!fh) return set_err(std::string("cannot open ") + path);
   std::fseek(fh, 0, SEEK_END);
@@ -72,28 +75,36 @@ GANON_HOST_API int ganon_bam_open(const char *path, int threads, ganon_bam **out
     return set_err("short read");
   }
   std::fclose(fh);
-  // ---- BGZF block table ----
+  // ---- BGZF block table (untrusted input: every field is checked before it is used) ----
   std::vector<Block> blocks;
   int64_t off = 0, total = 0;
-  while (off < (int64_t)file.size()) {
-    if (off + 18 > (int64_t)file.size()) return set_err("truncated BGZF header");
+  const int64_t fsz = (int64_t)file.size();
+  while (off < fsz) {
+    if (off + 18 > fsz) return set_err("truncated BGZF header");
     const uint8_t *h = &file[off];
     if (h[0] != 31 || h[1] != 139 || h[2] != 8 || !(h[3] & 4)) return set_err("not a BGZF file");
     const int xlen = h[10] | (h[11] << 8);
+    // the extra field and the 8-byte CRC32/ISIZE trailer must lie inside the file
+    if (off + 12 + xlen + 8 > fsz) return set_err("truncated BGZF extra field");
     int bsize = -1;
     for (int x = 12; x < 12 + xlen;) {
+      if (x + 4 > 12 + xlen) return set_err("malformed BGZF extra subfield");
       const int slen = h[x + 2] | (h[x + 3] << 8);
+      if (x + 4 + slen > 12 + xlen) return set_err("malformed BGZF extra subfield");
       if (h[x] == 66 && h[x + 1] == 67 && slen == 2) bsize = h[x + 4] | (h[x + 5] << 8);
       x += 4 + slen;
     }
     if (bsize < 0) return set_err("BGZF block without BC subfield");
     const int64_t blen = (int64_t)bsize + 1;
-    if (off + blen > (int64_t)file.size()) return set_err("truncated BGZF block");
+    if (off + blen > fsz) return set_err("truncated BGZF block");
+    const int64_t in_len = blen - 12 - xlen - 8;
+    if (in_len < 0) return set_err("BGZF block size smaller than its header");
     Block b;
     b.in_off = off + 12 + xlen;
-    b.in_len = (int32_t)(blen - 12 - xlen - 8);
+    b.in_len = (int32_t)in_len;
     uint32_t isize;
     std::memcpy(&isize, &file[off + blen - 4], 4);
+    if (isize > 65536) return set_err("BGZF block ISIZE over 64 KiB");
     b.out_len = (int32_t)isize;
     b.out_off = total;
     total += isize;
@@ -130,10 +141,12 @@ GANON_HOST_API int ganon_bam_open(const char *path, int threads, ganon_bam **out
   if (n < 12 || std::memcmp(d, "BAM\1", 4) != 0) return die("not a BAM stream");
   int32_t l_text, n_ref;
   std::memcpy(&l_text, d + 4, 4);
+  if (l_text < 0) return die("negative header text length");
   int64_t p = 8 + (int64_t)l_text;
   if (p + 4 > n) return die("truncated header");
   std::memcpy(&n_ref, d + p, 4);
   p += 4;
+  if (n_ref < 0) return die("negative reference count");
   for (int32_t i = 0; i < n_ref; ++i) {
     int32_t l_name, l_ref;
     if (p + 4 > n) return die("truncated reference list");
@@ -238,13 +251,13 @@ GANON_HOST_API int ganon_bam_open(const char *path, int threads, ganon_bam **out
       bam->name_off[i] = o_name[i];
       bam->name_len[i] = l_rn > 0 ? l_rn - 1 : 0;
       char *nm = bam->names.data() + o_name[i];
-      std::memcpy(nm, r + q, l_rn);
+      copy_bytes(nm, r + q, l_rn);
       if (o_name[i + 1] - o_name[i] > l_rn) nm[l_rn] = '\0';
       q += l_rn;
       bam->cig_off[i] = o_cig[i];
       int64_t rlen = 0;
       uint32_t *cg = bam->cigar.data() + o_cig[i];
-      std::memcpy(cg, r + q, 4LL * ncig);
+      copy_bytes(cg, r + q, 4LL * ncig);
       for (int k = 0; k < ncig; ++k) {
         const uint32_t w = cg[k];
         const int op = w & 0xF;
@@ -254,18 +267,32 @@ GANON_HOST_API int ganon_bam_open(const char *path, int threads, ganon_bam **out
       if (rflag & 4) rlen = 0;
       bam->end[i] = (int32_t)(rpos + (rlen > 0 ? rlen : 1));
       bam->seq_off[i] = o_seq[i];
-      std::memcpy(bam->seq.data() + o_seq[i], r + q, (size_t)((lseq + 1) / 2));
+      copy_bytes(bam->seq.data() + o_seq[i], r + q, (size_t)((lseq + 1) / 2));
       q += (lseq + 1) / 2;
       bam->qual_off[i] = o_qual[i];
-      std::memcpy(bam->qual.data() + o_qual[i], r + q, (size_t)lseq);
+      copy_bytes(bam->qual.data() + o_qual[i], r + q, (size_t)lseq);
       q += lseq;
       bam->aux_off[i] = o_aux[i];
       bam->aux_len[i] = (int32_t)(bs - q);
-      std::memcpy(bam->aux.data() + o_aux[i], r + q, (size_t)(bs - q));
+      copy_bytes(bam->aux.data() + o_aux[i], r + q, (size_t)(bs - q));
     }
   });
   *out = bam;
   return 0;
+}
+
+// No C++ exception crosses the C ABI: allocation failures (a huge ISIZE total, a corrupt record
+// count) become an error code.
+GANON_HOST_API int ganon_bam_open(const char *path, int threads, ganon_bam **out) {
+  if (!path || !out) return set_err("null argument");
+  *out = nullptr;
+  try {
+    return bam_open_impl(path, threads, out);
+  } catch (const std::bad_alloc &) {
+    return set_err("out of memory decoding the BAM file");
+  } catch (const std::exception &e) {
+    return set_err(std::string("BAM decode failed: ") + e.what());
+  }
 }
 
 GANON_HOST_API int ganon_bam_view_get(ganon_bam *b, ganon_bam_view *v) {

@@ -76,34 +76,48 @@ def anonymize_genome_sharded(windows: List[Window], tumor_bam: str, normal_bam: 
     initialised) or None for a single rank. Returns the all-reduced totals."""
     anonymizer = anonymizer or CompleteGermlineAnonymizer(device=int(os.environ.get("LOCAL_RANK", 0)))
     fasta = FastaRef(ref_file)
-    tables = (ReadTable(tumor_bam, threads=threads), ReadTable(normal_bam, threads=threads))
-    planner = make_planner(tables[0], tables[1], fasta, windows)
-    plan = planner.run()
-    owner = contig_owner(plan, list(fasta.references), world, policy)
-    mine = [sc.id for sc in plan.scopes if owner[sc.contig] == rank]
-    res = anonymizer.anonymize(planner, plan, scope_ids=mine)
-    mine_set = set(mine)
-    # this rank's written reads and their masked bytes (column arrays, no per-record Python)
-    w_ds, w_row, w_sc = plan.written_arrays()
-    sel = (w_sc >= 0) & np.isin(w_sc, np.fromiter(mine_set, np.int64, len(mine_set)))
-    recs = np.stack([w_ds[sel], w_row[sel], w_sc[sel]], axis=1).astype(np.int64).reshape(-1, 3)
-    idx = _read_byte_index(tables, res.seq_base, recs[:, 0], recs[:, 1])
-    os.makedirs(workdir, exist_ok=True)
-    shard = os.path.join(workdir, f"shard{rank}")
-    np.savez(shard + ".npz", recs=recs, seq=res.seq_out[idx],
-             calls=res.scope_snv_calls, bases=res.scope_masked_bases, totals=res.totals)
-    with open(shard + ".json", "w") as fh:
-        json.dump({"indel_counts": {str(s): {vt.name: n for vt, n in c.items()}
-                                    for s, c in res.scope_indel_counts.items()},
-                   "leftovers": [[k[0], k[1], k[2], _edits_to_json(v)] for k, v in res.leftovers.items()]}, fh)
-    totals = res.totals.astype(np.int64)
+    tables = plan = res = None
+    failure = None
+    try:
+        tables = (ReadTable(tumor_bam, threads=threads), ReadTable(normal_bam, threads=threads))
+        planner = make_planner(tables[0], tables[1], fasta, windows)
+        plan = planner.run()
+        owner = contig_owner(plan, list(fasta.references), world, policy)
+        mine = [sc.id for sc in plan.scopes if owner[sc.contig] == rank]
+        res = anonymizer.anonymize(planner, plan, scope_ids=mine)
+        mine_set = set(mine)
+        # this rank's written reads and their masked bytes (column arrays, no per-record Python)
+        w_ds, w_row, w_sc = plan.written_arrays()
+        sel = (w_sc >= 0) & np.isin(w_sc, np.fromiter(mine_set, np.int64, len(mine_set)))
+        recs = np.stack([w_ds[sel], w_row[sel], w_sc[sel]], axis=1).astype(np.int64).reshape(-1, 3)
+        idx = _read_byte_index(tables, res.seq_base, recs[:, 0], recs[:, 1])
+        os.makedirs(workdir, exist_ok=True)
+        shard = os.path.join(workdir, f"shard{rank}")
+        np.savez(shard + ".npz", recs=recs, seq=res.seq_out[idx],
+                 calls=res.scope_snv_calls, bases=res.scope_masked_bases, totals=res.totals)
+        with open(shard + ".json", "w") as fh:
+            json.dump({"indel_counts": {str(s): {vt.name: n for vt, n in c.items()}
+                                        for s, c in res.scope_indel_counts.items()},
+                       "leftovers": [[k[0], k[1], k[2], _edits_to_json(v)] for k, v in res.leftovers.items()]}, fh)
+        totals = res.totals.astype(np.int64)
+    except Exception as e:   # every rank must reach the collectives below, or the others hang
+        failure = e
+        totals = np.zeros(8, np.int64)
     if dist is not None:
         import torch
         dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+        flag = torch.tensor([1 if failure is not None else 0], dtype=torch.int64, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+        if int(flag.item()):
+            if failure is not None:
+                raise failure
+            raise RuntimeError("anonymize_genome_sharded: another rank failed")
         tt = torch.from_numpy(totals.copy()).to(dev)
         dist.all_reduce(tt)
         totals = tt.cpu().numpy()
         dist.barrier()
+    elif failure is not None:
+        raise failure
     if rank == 0:
         merged = _merge_shards(plan, tables, res, workdir, world)
         write_fastqs(plan, merged, tables, (tumor_out, normal_out), backend=anonymizer.format_fastq)

@@ -16,7 +16,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, name, workdir, policy, q):
+def _worker(rank, world, port, name, workdir, policy, q, engine="oracle", fail_rank=-1):
     import sys
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [repo, os.path.join(repo, "oracle"), os.path.join(repo, "tests")]
@@ -38,9 +38,14 @@ def _worker(rank, world, port, name, workdir, policy, q):
                  "ref": os.path.join(inp, "ref.fa"), "vcf": os.path.join(inp, "variants.vcf")}
         fa = FastaRef(paths["ref"])
         windows = get_windows(read_vcf(paths["vcf"]), fa.index)
+        anon = CompleteGermlineAnonymizer(engine=OracleEngine()) if engine == "oracle" else CompleteGermlineAnonymizer(device=0)
+        if rank == fail_rank:
+            def boom(*a, **k):
+                raise RuntimeError("injected failure")
+            anon.anonymize = boom
         tot = anonymize_genome_sharded(windows, paths["T"], paths["N"], paths["ref"], name_output(paths["T"]),
                                        name_output(paths["N"]), True, rank, world, os.path.join(workdir, "shards"),
-                                       CompleteGermlineAnonymizer(engine=OracleEngine()), dist, policy)
+                                       anon, dist, policy)
         q.put((rank, tot))
     finally:
         dist.destroy_process_group()
@@ -71,3 +76,25 @@ def test_two_rank_contig_shards_match_reference(name, policy, tmp_path):
             if os.path.exists(gp):
                 assert open(pre + suf, "rb").read() == gzip.open(gp).read(), tag + suf
     assert open(paths["N"] + ".statistics.txt").read() == open(os.path.join(GOLDEN, name, "normal.statistics.txt")).read()
+
+
+def test_a_failing_rank_stops_every_rank(tmp_path):
+    """A rank that raises still reaches the error-flag all-reduce: the other rank raises too
+    instead of waiting in a collective forever (distributed.py)."""
+    from genomeanonymizer_amd.synth.generate import generate, scenario
+    workdir = str(tmp_path / "tiny")
+    generate(scenario("tiny"), os.path.join(workdir, "in"))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, "tiny", workdir, "lpt", q, "oracle", 1)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    alive = [p.is_alive() for p in procs]
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    assert alive == [False, False]
+    assert all(p.exitcode != 0 for p in procs)

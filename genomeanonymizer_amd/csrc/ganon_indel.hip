@@ -586,7 +586,7 @@ int run_tally(ganon_ctx *ctx, ganon_indels *t) {
                        ctx->stream, keys, t->n_dev(), t->flags, t->run_list, t->run_count);
     // runs <= n / 2 (the counts stay on the device): one thread per possible run, the threads past
     // the count leave at once
-    const unsigned grid = (unsigned)((n / 2 + 255) / 256);
+    const unsigned grid = (unsigned)std::max<int64_t>(1, (n / 2 + 255) / 256);   // (n = 1: one idle workgroup)
     hipLaunchKernelGGL(k_indel_classify<KeyT>, dim3(grid), dim3(256), 0, ctx->stream, t->V, keys,
                        t->vals[t->sorted_sel], t->n_dev(), t->pos_bits, t->obs, t->flags, t->rank, t->repk,
                        t->run_list, t->run_count, t->counters);

@@ -1,20 +1,25 @@
 #!/usr/bin/env python3
 """Benchmark of the germline-masking hot path on BASELINE.json configs[1].
 
-One step = one pass of the masking kernels over one resident batch: the config-2 layout
-(10 M synthetic 150 bp tumor+normal reads on a 3.0 Gb genome with 1 M germline SNPs and a
-1 M-window VCF; genomeanonymizer_amd/synth/batch.py) uploaded to HBM once, then
-``ganon_batch_run`` = SNV tally -> TN classification -> overwrite for every scope, plus the
-pass-through copies, exactly what ``ganon_mask_batch`` does minus the PCIe copies, then
-``ganon_indel_run`` = the germline indel tally (a no-op launch-free pass when no read of the
-batch has an I/D op, as in the config-2 synthetic reads).
-Multi-GPU (torchrun): every rank owns its own config-2 shard (per-contig sharding makes
-shards independent; weak scaling) and the only collective is the int64 totals all-reduce
-over RCCL of each step, overlapped with the next step's kernels (double-buffered).
+One step = everything it takes to anonymize one resident raw batch: ``ganon_batch_run`` =
+the device prep (CIGAR walk of every (scope, read) incidence into aligned segments, scope groups,
+output partition pieces — rebuilt from the raw ganon_batch arrays on every run,
+csrc/ganon_prep.hip) + SNV tally -> TN classification -> overwrite for every scope and the copy of
+every other read (k_group, k_finish), then ``ganon_indel_run`` = the germline indel tally (no
+launch when no read has an I/D op, as in the config-2 synthetic reads). The batch is the config-2
+layout (10 M synthetic 150 bp tumor+normal reads on a 3.0 Gb genome with 1 M germline SNPs and a
+1 M-window VCF; genomeanonymizer_amd/synth/batch.py) copied to HBM once as raw SoA arrays.
+Multi-GPU (torchrun): every rank owns its own config-2 shard (per-contig sharding makes shards
+independent; weak scaling) and the only collective is the int64 totals all-reduce over RCCL of
+each step, overlapped with the next step's kernels (double-buffered).
 
-Prints one JSON line (rank 0). ``roofline`` is for the dominant kernel: the algorithmic
-bytes it processes per launch (SURVEY §8(d) figures, attributed per kernel)
-over its average duration measured with HIP events on the launch stream.
+Prints one JSON line (rank 0). ``roofline`` is for the whole step (the prep kernels and the
+masking kernels, all of which a step needs): the algorithmic bytes of the batch (SURVEY §8(d):
+per read ceil(L/2) in + ceil(L/2) out + 4 n_cigar + 16, per extra incidence ceil(L/2) + 4 n_cigar +
+8, per scope ceil(span/2) of reference) over the summed average durations of the step's kernels,
+each measured with HIP events on the launch stream; ``roofline.dominant`` gives the masking kernel
+alone. ``pcie_inclusive``: the same batch re-copied from pinned host memory every step (reload =
+H2D + device validation + plan), run, and its masked bases copied back.
 """
 from __future__ import annotations
 
@@ -30,25 +35,14 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
-SMALL_CAP0, SMALL_CAP1 = 2560, 16384    # scope classes of ganon_hip.hip (kSmallCap0/1)
 GROUP_MAX_SPAN = 1 << 20                # kGrpMaxSpan: widest scope of the group kernels
-VARIANT_NAMES = {0: "default", 1: "v0_block", 2: "v1_wave", 3: "v2_copy_patch", 4: "v4_group",
-                 5: "v5_group_fused", 6: "v3_persistent"}
-# how each variant writes reads (kernel_bytes attribution)
-VARIANT_WRITE = {0: "fused", 1: "whole", 2: "whole", 3: "copy_patch", 4: "group", 5: "fused",
-                 6: "copy_patch"}
-# A/B configurations: (name, variant, group-kernel unroll)
-AB_CONFIGS = [(VARIANT_NAMES[v], v, 2) for v in (1, 2, 3, 6, 4)] + [(f"v5_group_fused_k{u}", 5, u) for u in (1, 2, 4)]
+PREP_KERNELS = ("prep_groups", "prep_emit", "prep_pieces")
 
 
 def kernel_class(name: str) -> str:
-    if name in ("copy_seq", "k_copy_ranges") or name.startswith("k_passthrough"):
+    if name == "copy_seq":
         return "copy"
-    if name.endswith("/2.5K"):
-        return "small2.5K"
-    if name.endswith("/16K"):
-        return "small16K"
-    if name.startswith("k_tile_large<1>") or name.startswith("k_mask_large"):
+    if name.startswith("k_tile_large") or name.startswith("k_mask_large"):
         return "large"
     if name.startswith("k_group"):
         return "group"
@@ -74,38 +68,25 @@ def indel_bytes(arr, n_obs: int, n_emit: int = None) -> dict:
             "k_indel_classify": 45 * n_emit}
 
 
-def kernel_bytes(arr, mode: str = "fused") -> dict:
-    """Algorithmic bytes per launch of each kernel class (SURVEY §8(d) per-unit figures).
+def kernel_bytes(arr) -> dict:
+    """Algorithmic bytes per launch of the masking kernels (SURVEY §8(d) per-unit figures).
 
     Per read: ceil(L/2) in + ceil(L/2) out + 4*n_cigar + 16; each further scope incidence
-    ceil(L/2) + 4*n_cigar + 8; each scope ceil(span/2) of reference. A read's own cost goes
-    to the kernel that writes it: mode "whole" — the scope kernel of its write scope, or the
-    pass-through copy; "copy_patch" — the device copy owns every read's in + out bytes and the
-    scope kernel its 4*n_cigar + 16 ("group": the same with the group kernel owning every scope up
-    to 1 Mi positions); "fused" — the group kernel (it copies the whole buffer partition by
-    partition) except the reads the wide-scope kernels write.
-    Extra incidences and reference bytes go to the kernel of their scope; "group" (both small
-    classes) is what the group kernels own. The per-class figures sum to the formula."""
+    ceil(L/2) + 4*n_cigar + 8; each scope ceil(span/2) of reference. The fused group kernel copies
+    every byte of the output it does not leave to the huge-scope kernels (class "large": scopes
+    over 2^20 positions, their written reads, incidences and reference). The per-class figures sum
+    to the formula."""
     L = arr["read_len"].astype(np.int64)
     h = (L + 1) // 2
     nc = arr["n_cig"].astype(np.int64)
     span = arr["scope_span_len"].astype(np.int64)
-    cls = np.where(span <= SMALL_CAP0, 0, np.where(span <= SMALL_CAP1, 1, 2))
-    if mode in ("fused", "group"):
-        cls = np.where(span <= GROUP_MAX_SPAN, 0, 2)     # group kernels take every scope up to 1 Mi positions
-    names = ["small2.5K", "small16K", "large"]
-    out = {n: 0 for n in names}
-    out["copy"] = 0
+    cls = np.where(span <= GROUP_MAX_SPAN, 0, 1)
+    out = {"group": 0, "large": 0, "copy": 0}
     ws = arr["write_scope"].astype(np.int64)
-    wcls = np.where(ws >= 0, cls[np.maximum(ws, 0)], 3)
+    wcls = np.where(ws >= 0, cls[np.maximum(ws, 0)], 0)
     base = 2 * h + 4 * nc + 16
-    if mode in ("copy_patch", "group"):
-        out["copy"] += int((2 * h).sum())
-        base = 4 * nc + 16
-    elif mode == "fused":
-        wcls = np.where(wcls == 2, 2, 0)     # the group kernel copies every byte it does not leave to k_mask_large
-    for k, n in enumerate(names + ["copy"]):
-        out[n] += int(base[wcls == k].sum())
+    out["group"] += int(base[wcls == 0].sum())
+    out["large"] += int(base[wcls == 1].sum())
     offs = arr["scope_incid_off"]
     scope_of_inc = np.repeat(np.arange(len(span)), np.diff(offs))
     r = arr["incid_read"].astype(np.int64)
@@ -119,10 +100,9 @@ def kernel_bytes(arr, mode: str = "fused") -> dict:
     first[order[firsts]] = True
     extra = ~first
     cost = (h + 4 * nc + 8)[r]
-    for k, n in enumerate(names):
+    for k, n in enumerate(("group", "large")):
         out[n] += int(cost[extra & (cls[scope_of_inc] == k)].sum())
         out[n] += int(((span + 1) // 2)[cls == k].sum())
-    out["group"] = out["small2.5K"] + out["small16K"]
     return out
 
 
@@ -255,6 +235,40 @@ def fastq_bench(masker, db, arr, args, torch, rank: int) -> dict:
     }
 
 
+def pcie_bench(masker, db, arr, args, torch) -> dict:
+    """The batch re-copied from pinned host memory every step: ganon_batch_reload (H2D of the raw
+    arrays + device validation and plan, three synchronizations), ganon_batch_run, and the masked
+    bases copied back (D2H). The same raw bytes the resident steps start from."""
+    from genomeanonymizer_amd import native
+    pinned = {}
+    for k, v in arr.items():
+        if k == "ref_nt16":   # resident on the device (ganon_ref_upload): not re-sent per batch
+            continue
+        t = torch.empty(v.nbytes, dtype=torch.uint8, pin_memory=True)
+        a = t.numpy().view(v.dtype).reshape(v.shape)
+        a[...] = v
+        pinned[k] = (t, a)
+    parr = {k: a for k, (_, a) in pinned.items()}
+    out_t = torch.empty(len(arr["seq_nt16"]), dtype=torch.uint8, pin_memory=True)
+    out = out_t.numpy()
+    n = max(2, min(args.steps, 10))
+    for _ in range(2):
+        db.reload(parr)
+        db.run()
+        db.download_seq(out)
+    t = time.perf_counter()
+    for _ in range(n):
+        db.reload(parr)
+        db.run()
+        db.download_seq(out)
+    ms = (time.perf_counter() - t) / n * 1e3
+    h2d = int(sum(v.nbytes for k, v in arr.items() if k != "ref_nt16"))
+    return {"value": round(len(arr["read_len"]) / (ms * 1e-3), 1), "unit": "reads/s", "ms_per_batch": round(ms, 3),
+            "batches": n, "h2d_bytes": h2d, "d2h_bytes": int(len(out)),
+            "note": "pinned H2D of every raw read/scope array (the reference stays resident) + device "
+                    "validation/plan + run + D2H of the masked bases, per batch"}
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -268,11 +282,9 @@ def main() -> None:
     ap.add_argument("--windows", type=int, default=None)
     ap.add_argument("--germline", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--variant", type=int, default=0,
-                    help="include/ganon.h GANON_VARIANT_*: 0 default (= 5), 1 block, 2 wave, 3 copy-patch, "
-                         "4 group, 5 group fused, 6 persistent")
     ap.add_argument("--unroll", type=int, default=2, help="group kernel chunk width in 16-base blocks (1/2/4/8)")
-    ap.add_argument("--ab", action="store_true", help="also time every small-scope variant, interleaved")
+    ap.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive measurement")
+    ap.add_argument("--target", type=int, default=None, help="GANON_PARAM_GROUP_TARGET (cost units per group)")
     ap.add_argument("--no-fastq", action="store_true", help="skip the FASTQ formatter measurement")
     ap.add_argument("--indel-sort", type=int, default=0, help="GANON_PARAM_INDEL_SORT: 0 segmented, 1 global")
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_r01.json"),
@@ -305,13 +317,15 @@ def main() -> None:
     arr, info = make_batch(args, rank)
     t_gen = time.perf_counter() - t_gen
     masker = native.HipMasker(dev)
-    masker.set_variant(args.variant)
     masker.set_param(native.PARAM_GROUP_UNROLL, args.unroll)
+    if args.target:
+        masker.set_param(native.PARAM_GROUP_TARGET, args.target)
     masker.set_param(native.PARAM_INDEL_SORT, args.indel_sort)
     stream = torch.cuda.current_stream()
     masker.set_stream(stream.cuda_stream)
     t_up = time.perf_counter()
-    db = masker.upload(arr)
+    ref = masker.upload_reference(arr["ref_nt16"])      # the genome stays resident (ganon_ref_upload)
+    db = masker.upload({k: v for k, v in arr.items() if k != "ref_nt16"}, ref=ref)
     ind = db.indel_tally(arr)      # germline indel tally, part of every step
     t_up = time.perf_counter() - t_up
     # totals all-reduce (RCCL) of every step, double-buffered: the reduction of step i runs beside
@@ -371,25 +385,7 @@ def main() -> None:
             k[0] += launches
             k[1] += ms
     masker.set_profiling(False)
-    ab = None
-    if args.ab:
-        # interleaved rounds in one process (cdna_hip_programming.md §5.4 rule 24)
-        samples = {name: [] for name, _, _ in AB_CONFIGS}
-        for _ in range(5):
-            for name, v, u in AB_CONFIGS:
-                masker.set_variant(v)
-                masker.set_param(native.PARAM_GROUP_UNROLL, u)
-                db.run()
-                torch.cuda.synchronize()
-                t = time.perf_counter()
-                for _ in range(args.steps):
-                    db.run()
-                torch.cuda.synchronize()
-                samples[name].append((time.perf_counter() - t) / args.steps * 1e3)
-        masker.set_variant(args.variant)
-        masker.set_param(native.PARAM_GROUP_UNROLL, args.unroll)
-        ab = {name: {"median_ms": round(float(np.median(x)), 4),
-                     "min_ms": round(float(np.min(x)), 4)} for name, x in samples.items()}
+    pcie = None if args.no_pcie else pcie_bench(masker, db, arr, args, torch)
     fastq = None if args.no_fastq else fastq_bench(masker, db, arr, args, torch, rank)
     totals = db.totals()
     batch_info = db.info()
@@ -408,23 +404,24 @@ def main() -> None:
     else:
         job_totals = totals
     db.free()
+    ref.free()
 
-    kb = kernel_bytes(arr, VARIANT_WRITE[args.variant])
+    kb = kernel_bytes(arr)
     kb.update(indel_bytes(arr, indel_info["observations"], indel_info["emitted"]))
     per_kernel = {n: {"launches": c, "avg_ms": ms / c} for n, (c, ms) in ktimes.items()}
     dom = max(per_kernel, key=lambda n: per_kernel[n]["avg_ms"] * per_kernel[n]["launches"])
     indel_ms = sum(v["avg_ms"] * v["launches"] for n, v in per_kernel.items() if "indel" in n) / args.steps
     dom_bytes = kb.get(kernel_class(dom), 0)
     dom_ms = per_kernel[dom]["avg_ms"]
-    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     pass_ms = sum(v["avg_ms"] * v["launches"] for v in per_kernel.values()) / args.steps
     alg_total = algorithmic_bytes(arr)
+    achieved = alg_total / (pass_ms * 1e-3) / 1e9
     traffic = None
     if os.path.exists(args.pmc):
         try:
             pmc = json.load(open(args.pmc))
-            if pmc.get("kernel") == dom and pmc.get("reads") == args.reads:
-                traffic = pmc.get("hbm_bytes_per_launch")
+            if pmc.get("reads") == args.reads and pmc.get("config") == args.config:
+                traffic = pmc.get("step_hbm_bytes")
         except Exception:
             traffic = None
 
@@ -451,11 +448,17 @@ def main() -> None:
                    "scopes_per_gpu": info["scopes"], "incidences_per_gpu": info.get("incidences"),
                    "window_scopes": info.get("window_scopes"), "union_scopes": info.get("union_scopes"),
                    "passthrough_reads": info.get("passthrough_reads"), "parallelism": f"contig-shard x{world}"},
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                     "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_ms": round(dom_ms, 5)},
+        "roofline": {"bound": "hbm", "kernel": "step: " + " + ".join(per_kernel), "achieved": round(achieved, 1),
+                     "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                     "traffic": traffic, "algorithmic_bytes_per_launch": alg_total,
+                     "avg_launch_ms": round(pass_ms, 5),
+                     "dominant": {"kernel": dom, "algorithmic_bytes_per_launch": dom_bytes,
+                                  "avg_launch_ms": round(dom_ms, 5),
+                                  "achieved": round(dom_bytes / (dom_ms * 1e-3) / 1e9, 1),
+                                  "frac": round(dom_bytes / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}},
         "pass": {"kernel_ms": round(pass_ms, 4), "algorithmic_bytes": alg_total,
-                 "achieved_GBps": round(alg_total / (pass_ms * 1e-3) / 1e9, 1),
+                 "prep_ms": round(sum(v["avg_ms"] * v["launches"] for n, v in per_kernel.items()
+                                      if n in PREP_KERNELS) / args.steps, 4),
                  "kernels": {n: {"avg_ms": round(v["avg_ms"], 5), "launches_per_step": v["launches"] // args.steps,
                                  "alg_bytes": kb.get(kernel_class(n))} for n, v in per_kernel.items()}},
         "indel": {"observations": indel_info["observations"], "emitted": indel_info["emitted"],
@@ -463,7 +466,7 @@ def main() -> None:
                   "masked_calls": int((irecs["kind"] == native.INDEL_CALL).sum()),
                   "support_records": int((irecs["kind"] == native.INDEL_SUPPORT).sum()),
                   "ms_per_step": round(indel_ms, 4)},
-        "ab_small_scope_kernel": ab,
+        "pcie_inclusive": pcie,
         "fastq": fastq,
         "totals": {k: int(v) for k, v in zip(native.TOTAL_NAMES, job_totals)},
         "batch": batch_info,

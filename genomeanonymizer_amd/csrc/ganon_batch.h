@@ -129,13 +129,13 @@ struct ganon_dbatch {
   int32_t *counters = nullptr;          // [0] rare small (unused), [1] rare tiles
   int32_t *status = nullptr;            // sticky device error bits (1: far-mask list overflow)
   ganon_dev::PrepErr *err = nullptr;
-  unsigned long long *plan_info = nullptr;   // [0] far nibbles, [1] huge scopes, [2] written reads
+  unsigned long long *plan_info = nullptr;   // [0] far nibbles, [1] huge scopes, [2] written reads, [3] longest read
   unsigned long long *paths = nullptr;       // GrpAux::paths (since upload)
   unsigned long long *cursor = nullptr;      // k_prep_emit allocation counters and their bases (b_cursor)
   ganon_dev::GrpAux *aux = nullptr;
   // plan of the current contents (device prep, sized at upload)
   int32_t n_groups = 0, group_target = 512;
-  int64_t n_seg = 0, region = 0, far_cap = 0, n_written = 0;
+  int64_t n_seg = 0, region = 0, far_cap = 0, n_written = 0, region_per_incid = 0;
   size_t scan_tmp_bytes = 0;
   // huge scopes (> kGrpMaxSpan positions): tile path, planned on the host at upload
   std::vector<void *> huge_allocs;

@@ -134,7 +134,7 @@ __global__ void __launch_bounds__(kPrepThreads) k_ref_blocks(const uint8_t *__re
 // ---- per read (upload: validation) --------------------------------------------------------
 __global__ void __launch_bounds__(kPrepThreads) k_prep_reads(const Raw R, PrepErr *err, int32_t *__restrict__ read_end,
                                                              unsigned long long *written) {
-  int n_written = 0;
+  int n_written = 0, max_len = 0;
   for (int64_t r = blockIdx.x * (int64_t)kPrepThreads + threadIdx.x; r < R.n_reads;
        r += (int64_t)gridDim.x * kPrepThreads) {
     const int L = R.read_len[r];
@@ -149,6 +149,7 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_reads(const Raw R, PrepEr
     if (ws < -1 || ws >= R.n_scopes) report(err, kErrReadWriteScope, r, ws);
     if (L >= (1 << 24)) report(err, kErrReadLong, r);
     n_written += ws >= 0;
+    max_len = max(max_len, L);
     int64_t rl = 0;
     for (int k = 0; k < nc; ++k) {
       const uint32_t w = R.cigar[co + k];
@@ -159,8 +160,12 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_reads(const Raw R, PrepEr
     if (rs < 0 || rs + rl > INT32_MAX) { report(err, kErrReadPos, r); continue; }
     read_end[r] = (int32_t)(rs + (rl > 0 ? rl : 1));
   }
-  for (int o = 32; o > 0; o >>= 1) n_written += __shfl_xor(n_written, o);
+  for (int o = 32; o > 0; o >>= 1) {
+    n_written += __shfl_xor(n_written, o);
+    max_len = max(max_len, __shfl_xor(max_len, o));
+  }
   if ((threadIdx.x & 63) == 0 && n_written) atomicAdd(written, (unsigned long long)n_written);
+  if ((threadIdx.x & 63) == 0 && max_len) atomicMax(written + 1, (unsigned long long)max_len);
 }
 
 // ---- per scope (upload: validation) --------------------------------------------------------
@@ -222,16 +227,18 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_incid_check(const Raw R, 
   }
 }
 
-// gs0[b] = first scope of group b; cursors of the emit kernel's allocations reset.
+// gmeta[b] = (first scope of group b, its first incidence); allocation counters reset.
 __global__ void __launch_bounds__(kPrepThreads) k_prep_groups(const Raw R, long long weight, long long target,
-                                                              int32_t *__restrict__ gs0,
+                                                              longlong2 *__restrict__ gmeta,
                                                               unsigned long long *__restrict__ cursor) {
   const int64_t gt = blockIdx.x * (int64_t)kPrepThreads + threadIdx.x;
-  if (gt < 2 * kCursors) cursor[gt] = 0;
+  if (gt < kCursors) cursor[gt] = 0;
   for (int64_t s = gt; s < R.n_scopes; s += (int64_t)gridDim.x * kPrepThreads) {
     const int64_t b = group_of(R.incid_off, s, weight, target);
     const int64_t bp = s == 0 ? -1 : group_of(R.incid_off, s - 1, weight, target);
-    for (int64_t x = bp + 1; x <= b; ++x) gs0[x] = (int32_t)s;
+    if (bp == b) continue;
+    const longlong2 m = make_longlong2(s, R.incid_off[s]);
+    for (int64_t x = bp + 1; x <= b; ++x) gmeta[x] = m;
   }
 }
 
@@ -322,14 +329,18 @@ __device__ __forceinline__ void block_scan2(int a, int b, int &ea, int &eb, int 
 }
 
 // Segment records, group records 0, 1, 3, read_end and the partition candidates of group g.
-// Pass 1 walks every incidence of the group (segments counted as clean/dirty, aligned bases), then
-// one atomic per group takes the group's segment range and overflow region from global cursors
-// (group ranges land in any order; results do not depend on it); pass 2 writes the records —
-// all-ACGT-reference segments from the front of the range, the others from the back. A group of at
-// most kEmitUnroll x 256 incidences (every window group of configs[1]) keeps pass 1's loads and
-// its single-segment records in registers; larger groups walk again in pass 2. `write` 0 (upload
-// plan): counts, region sizes and candidates only. The candidates are the lowest buffer offset of
-// the reads the group writes, per dataset (every written read is "mine" in one incidence).
+// Pass 1 walks every incidence of the group (segments counted as clean/dirty); pass 2 writes the
+// records — all-ACGT-reference segments from the front of the group's range, the others from the
+// back. No global allocation in the common case: a group with at most one segment per incidence
+// (every short-read group) uses the records at its own incidence indices [i0, i0 + count); a
+// group with more (long reads, split CIGARs) takes its range past n_incid from one of 256
+// allocation counters whose bases the upload plan fixed. Its overflow region is likewise a closed
+// form of its incidence range: (i1 - i0) x ceil(longest read / 48) + 512 observations from
+// i0 x ceil(longest read / 48) + 512 g. A group of at most kEmitUnroll x 256 incidences keeps
+// pass 1's loads in registers and its single-segment records in LDS; larger groups walk again.
+// `write` 0 (upload plan): counts and candidates only. The candidates are the lowest buffer
+// offset of the reads the group writes, per dataset (every written read is "mine" in one
+// incidence).
 constexpr int kEmitUnroll = 2;   // incidences per thread and trip
 
 struct EmitInc {                 // one incidence of a trip, in registers
@@ -339,13 +350,12 @@ struct EmitInc {                 // one incidence of a trip, in registers
   uint32_t w0;
 };
 
-__device__ __forceinline__ void emit_load(const Raw &R, const long long *off, const uint8_t *huge, int ns,
-                                          long long base, long long i1, EmitInc (&e)[kEmitUnroll]) {
+// The read side of a trip (needs no scope lookup: issued before the scope staging is waited for).
+__device__ __forceinline__ void emit_load_reads(const Raw &R, long long base, long long i1, EmitInc (&e)[kEmitUnroll]) {
   const int tid = threadIdx.x;
 #pragma unroll
   for (int u = 0; u < kEmitUnroll; ++u) {
     const long long i = base + tid + kPrepThreads * u;
-    e[u].j = i < i1 ? lds_upper(off, ns, i) : 0;
     e[u].r = i < i1 ? R.incid_read[i] : -1;
   }
 #pragma unroll
@@ -363,8 +373,21 @@ __device__ __forceinline__ void emit_load(const Raw &R, const long long *off, co
   for (int u = 0; u < kEmitUnroll; ++u) e[u].w0 = e[u].ncig > 0 ? e[u].cg[0] : 0u;
 }
 
-__global__ void __launch_bounds__(kPrepThreads) k_prep_emit(const Raw R, const int32_t *__restrict__ gs0, int n_groups,
-                                                            int write, const uint64_t *__restrict__ bad, int64_t n_blk,
+// The scope side: local scope index by binary search in the staged offsets; huge scopes drop out.
+__device__ __forceinline__ void emit_resolve(const long long *off, const uint8_t *huge, int ns, long long base,
+                                             EmitInc (&e)[kEmitUnroll], bool keep_huge) {
+#pragma unroll
+  for (int u = 0; u < kEmitUnroll; ++u) {
+    e[u].j = 0;
+    if (e[u].r < 0) continue;
+    e[u].j = lds_upper(off, ns, base + threadIdx.x + kPrepThreads * u);
+    if (!keep_huge && huge[e[u].j]) e[u].r = -1;
+  }
+}
+
+__global__ void __launch_bounds__(kPrepThreads) k_prep_emit(const Raw R, const longlong2 *__restrict__ gmeta,
+                                                            int n_groups, int write, const uint64_t *__restrict__ bad,
+                                                            int64_t n_blk, long long region_per_incid,
                                                             int32_t *__restrict__ read_end, int4 *__restrict__ seg4,
                                                             int4 *__restrict__ groups, unsigned long long *__restrict__ lo,
                                                             uint32_t *__restrict__ lo_idx,
@@ -375,14 +398,15 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_emit(const Raw R, const i
   __shared__ int sstart[kGrpMaxScopes];
   __shared__ uint8_t huge[kGrpMaxScopes];
   __shared__ int ws[2 * kWaves];
-  __shared__ unsigned long long lmin[2], lbases, gbase[2];
+  __shared__ unsigned long long lmin[2], gbase;
   __shared__ int4 stash[kPrepThreads * kEmitUnroll];       // one-trip groups: single-segment records
   __shared__ uint8_t stash_clean[kPrepThreads * kEmitUnroll];
   const int tid = threadIdx.x;
   const int g = blockIdx.x;
-  const int s0 = gs0[g];
-  const int s1 = g + 1 < n_groups ? gs0[g + 1] : R.n_scopes;
-  const int ns = s1 - s0;   // <= kGrpMaxScopes (the cost weight bounds a bucket)
+  const longlong2 m0 = gmeta[g];
+  const longlong2 m1 = g + 1 < n_groups ? gmeta[g + 1] : make_longlong2(R.n_scopes, R.n_incid);
+  const int s0 = (int)m0.x, s1 = (int)m1.x, ns = s1 - s0;   // ns <= kGrpMaxScopes (the cost weight)
+  const long long i0 = m0.y, i1 = m1.y;
   for (int t = tid; t <= ns; t += kPrepThreads) off[t] = R.incid_off[s0 + t];
   for (int t = tid; t < ns; t += kPrepThreads) {
     sstart[t] = R.span_start[s0 + t];
@@ -390,19 +414,18 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_emit(const Raw R, const i
     huge[t] = R.span_len[s0 + t] > kGrpMaxSpan;
   }
   if (tid < 2) lmin[tid] = kNone;
-  if (tid == 0) lbases = 0;
-  __syncthreads();
-  const long long i0 = off[0], i1 = off[ns];
   const bool one_trip = i1 - i0 <= (long long)kPrepThreads * kEmitUnroll;
   int cnt[kEmitUnroll];        // (one trip) segments of this thread's incidences
 #pragma unroll
   for (int u = 0; u < kEmitUnroll; ++u) cnt[u] = 0;   // an empty group runs no trip
   int tot_c = 0, tot_d = 0, ec = 0, ed = 0;   // group totals; (one trip) this thread's offsets
-  unsigned long long mn0 = kNone, mn1 = kNone, bases = 0;   // this thread's candidates, aligned bases
+  unsigned long long mn0 = kNone, mn1 = kNone;   // this thread's candidates
   // ---- pass 1: count
   for (long long base = i0; base < i1; base += kPrepThreads * kEmitUnroll) {   // uniform trip count
     EmitInc e[kEmitUnroll];
-    emit_load(R, off, huge, ns, base, i1, e);
+    emit_load_reads(R, base, i1, e);
+    __syncthreads();   // (first trip: the scope staging)
+    emit_resolve(off, huge, ns, base, e, true);
     int tnc = 0, tnd = 0;
 #pragma unroll
     for (int u = 0; u < kEmitUnroll; ++u) {
@@ -439,7 +462,6 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_emit(const Raw R, const i
         ++n_;
         if (clean) ++tnc;
         else ++tnd;
-        bases += n;
       });
     }
     int tc, td;
@@ -449,28 +471,28 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_emit(const Raw R, const i
     tot_c += tc;
     tot_d += td;
   }
-  // ---- candidates and aligned bases: wave reductions, one LDS atomic per wave
+  // ---- candidates: wave reductions, one LDS atomic per wave
   for (int o = 32; o > 0; o >>= 1) {
     mn0 = min(mn0, (unsigned long long)__shfl_xor(mn0, o));
     mn1 = min(mn1, (unsigned long long)__shfl_xor(mn1, o));
-    bases += __shfl_xor(bases, o);
   }
   if ((tid & 63) == 0) {
     if (mn0 != kNone) atomicMin(&lmin[0], mn0);
     if (mn1 != kNone) atomicMin(&lmin[1], mn1);
-    if (bases) atomicAdd(&lbases, bases);
   }
-  __syncthreads();
-  // ---- the group's segment range and overflow region: sub-cursor g % kCursors, whose base the
-  //      upload plan fixed (the groups of a sub-cursor take their ranges in any order)
+  // ---- the group's record range: its own incidence indices, or (more segments than incidences)
+  //      past n_incid from sub-counter g % kCursors
+  const long long count = tot_c + tot_d;
   if (tid == 0) {
-    const int k = g % kCursors;
-    gbase[0] = cursor_base[k] + atomicAdd(&cursor[k], (unsigned long long)(tot_c + tot_d));
-    const unsigned long long cap = min((lbases + 47) / 48 + kGrpObs, (unsigned long long)(INT32_MAX / 2));
-    gbase[1] = (cursor_base[kCursors + k] + atomicAdd(&cursor[kCursors + k], cap)) | (cap << 40);
+    if (count <= i1 - i0) {
+      gbase = (unsigned long long)i0;
+    } else {
+      const int k = g % kCursors;
+      gbase = (unsigned long long)R.n_incid + cursor_base[k] + atomicAdd(&cursor[k], (unsigned long long)count);
+    }
   }
   __syncthreads();
-  const int64_t seg_b = (int64_t)gbase[0], seg_e = seg_b + tot_c + tot_d;
+  const int64_t seg_b = (int64_t)gbase, seg_e = seg_b + count;
   // ---- pass 2: write (walks again where the stash does not hold the incidence's one record)
   if (write) {
     int64_t run_c = 0, run_d = 0;
@@ -479,7 +501,10 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_emit(const Raw R, const i
       int cc[kEmitUnroll], cd[kEmitUnroll];
       EmitInc e[kEmitUnroll];
       const bool reload = !one_trip || cnt[0] > 1 || cnt[1] > 1;
-      if (reload) emit_load(R, off, huge, ns, base, i1, e);
+      if (reload) {
+        emit_load_reads(R, base, i1, e);
+        emit_resolve(off, huge, ns, base, e, false);
+      }
       if (one_trip) {
 #pragma unroll
         for (int u = 0; u < kEmitUnroll; ++u) {
@@ -499,7 +524,7 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_emit(const Raw R, const i
 #pragma unroll
         for (int u = 0; u < kEmitUnroll; ++u) {
           cc[u] = cd[u] = 0;
-          if (e[u].r < 0 || huge[e[u].j]) continue;
+          if (e[u].r < 0) continue;
           const int64_t r0 = ref0[e[u].j];
           int &c_ = cc[u], &d_ = cd[u];
           walk_segments(e[u].cg, e[u].ncig, e[u].L, e[u].rs, e[u].w0, [&](int, int p, int n) {
@@ -543,8 +568,8 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_emit(const Raw R, const i
   }
   if (tid == 0) {
     const int64_t mid = seg_b + tot_c;
-    const int64_t region = (int64_t)(gbase[1] & ((1ull << 40) - 1));
-    const int cap = (int)(gbase[1] >> 40);
+    const int64_t region = i0 * region_per_incid + (int64_t)kGrpObs * g;
+    const int cap = (int)min((i1 - i0) * region_per_incid + kGrpObs, (long long)(INT32_MAX / 2));
     groups[kGrpRec * (int64_t)g] = make_int4(s0, s1, (int)(uint32_t)seg_b, (int)(uint32_t)((uint64_t)seg_b >> 32));
     groups[kGrpRec * (int64_t)g + 1] = make_int4((int)(uint32_t)seg_e, (int)(uint32_t)((uint64_t)seg_e >> 32),
                                                  (int)(uint32_t)mid, (int)(uint32_t)((uint64_t)mid >> 32));
@@ -620,9 +645,9 @@ hipError_t sort_bytes(int64_t c, size_t &bytes) {
 
 int launch_groups(ganon_ctx *ctx, ganon_dbatch *db, const Raw &R) {
   KernelScope ks(ctx, "prep_groups");
-  hipLaunchKernelGGL(k_prep_groups, dim3(grid_for(std::max<int64_t>(db->n_scopes, 2 * kCursors))), dim3(kPrepThreads), 0,
+  hipLaunchKernelGGL(k_prep_groups, dim3(grid_for(std::max<int64_t>(db->n_scopes, kCursors))), dim3(kPrepThreads), 0,
                      ctx->stream, R, weight_of(db->group_target), (long long)db->group_target,
-                     static_cast<int32_t *>(db->b_gs0.p), db->cursor);
+                     static_cast<longlong2 *>(db->b_gs0.p), db->cursor);
   return check_launch(ctx, "k_prep_groups");
 }
 
@@ -630,10 +655,11 @@ int launch_emit(ganon_ctx *ctx, ganon_dbatch *db, const Raw &R, int write) {
   if (!db->n_groups) return GANON_OK;
   KernelScope ks(ctx, "prep_emit");
   hipLaunchKernelGGL(k_prep_emit, dim3((unsigned)db->n_groups), dim3(kPrepThreads), 0, ctx->stream, R,
-                     static_cast<const int32_t *>(db->b_gs0.p), db->n_groups, write, db->ref->bad, db->ref->n_blk,
-                     const_cast<int32_t *>(db->B.read_end), static_cast<int4 *>(db->b_seg4.p),
-                     static_cast<int4 *>(db->b_groups.p), static_cast<unsigned long long *>(db->b_lo.p),
-                     static_cast<uint32_t *>(db->b_lo_idx.p), db->cursor, db->cursor + 2 * kCursors);
+                     static_cast<const longlong2 *>(db->b_gs0.p), db->n_groups, write, db->ref->bad, db->ref->n_blk,
+                     (long long)db->region_per_incid, const_cast<int32_t *>(db->B.read_end),
+                     static_cast<int4 *>(db->b_seg4.p), static_cast<int4 *>(db->b_groups.p),
+                     static_cast<unsigned long long *>(db->b_lo.p), static_cast<uint32_t *>(db->b_lo_idx.p),
+                     db->cursor, db->cursor + kCursors);
   return check_launch(ctx, "k_prep_emit");
 }
 
@@ -698,6 +724,17 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db, const int64_t *host_incid_off) {
   if (ns) hipLaunchKernelGGL(k_prep_scope_check, dim3(grid_for(ns)), dim3(kPrepThreads), 0, st, R, db->err,
                              db->plan_info + 1);
   if ((rc = check_launch(ctx, "k_prep_reads/k_prep_scope_check")) || (rc = check_err(ctx, db))) return rc;
+  {
+    // overflow-region observations per incidence: the longest read's ceil(L / 48) (>= the round-1
+    // bound of aligned bases / 48 per group)
+    unsigned long long max_len = 0;
+    HIP_OR_FAIL(hipMemcpyAsync(&max_len, db->plan_info + 3, sizeof max_len, hipMemcpyDeviceToHost, st));
+    HIP_OR_FAIL(hipStreamSynchronize(st));
+    db->region_per_incid = (int64_t)((max_len + 47) / 48);
+    if ((double)db->n_incid * (double)db->region_per_incid > 4e9)
+      return fail(ctx, GANON_E_ARG, "batch too large: %lld incidences of reads up to %llu bases (split it)",
+                  (long long)db->n_incid, max_len);
+  }
   // 2. incidences, write scopes
   if (ns) hipLaunchKernelGGL(k_prep_incid_check, dim3(grid_for(ns)), dim3(kPrepThreads), 0, st, R, read_end, db->err,
                              seen);
@@ -713,7 +750,8 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db, const int64_t *host_incid_off) {
   int4 *grp = nullptr;
   unsigned long long *u64 = nullptr;
   uint32_t *u32 = nullptr;
-  if ((rc = grow_n(ctx, db->b_gs0, ng, &p32)) || (rc = grow_n(ctx, db->b_groups, (size_t)kGrpRec * ng, &grp)) ||
+  longlong2 *gm = nullptr;
+  if ((rc = grow_n(ctx, db->b_gs0, ng, &gm)) || (rc = grow_n(ctx, db->b_groups, (size_t)kGrpRec * ng, &grp)) ||
       (rc = grow_n(ctx, db->b_grp_part, 2 * (size_t)ng, &p32)) ||
       (rc = grow_n(ctx, db->b_lo, 2 * (size_t)ng, &u64)) || (rc = grow_n(ctx, db->b_lo_sorted, 2 * (size_t)ng, &u64)) ||
       (rc = grow_n(ctx, db->b_lo_idx, 2 * (size_t)ng, &u32)) ||
@@ -724,31 +762,29 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db, const int64_t *host_incid_off) {
   uint8_t *t8 = nullptr;
   if ((rc = grow_n(ctx, db->b_scan_tmp, tmp, &t8))) return rc;
   db->scan_tmp_bytes = tmp;
-  HIP_OR_FAIL(hipMemsetAsync(db->cursor + 2 * kCursors, 0, 2 * kCursors * sizeof(unsigned long long), st));
+  HIP_OR_FAIL(hipMemsetAsync(db->cursor + kCursors, 0, kCursors * sizeof(unsigned long long), st));
   if ((rc = launch_groups(ctx, db, R)) || (rc = launch_emit(ctx, db, R, 0)) || (rc = launch_pieces(ctx, db))) return rc;
   if (ng && nr)
     hipLaunchKernelGGL(k_prep_farcap, dim3(grid_for(nr)), dim3(kPrepThreads), 0, st, R, w, (long long)db->group_target,
                        static_cast<const int4 *>(db->b_groups.p), db->plan_info);
   if ((rc = check_launch(ctx, "k_prep_farcap"))) return rc;
   unsigned long long info[4] = {0, 0, 0, 0};
-  std::vector<unsigned long long> cur(4 * kCursors, 0);
+  std::vector<unsigned long long> cur(2 * kCursors, 0);
   HIP_OR_FAIL(hipMemcpyAsync(info, db->plan_info, sizeof info, hipMemcpyDeviceToHost, st));
-  HIP_OR_FAIL(hipMemcpyAsync(cur.data(), db->cursor, 2 * kCursors * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+  HIP_OR_FAIL(hipMemcpyAsync(cur.data(), db->cursor, kCursors * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
   HIP_OR_FAIL(hipStreamSynchronize(st));
-  // sub-cursor bases: exclusive prefix of the counting pass's totals (deterministic per sub-cursor)
-  unsigned long long tseg = 0, treg = 0;
+  // sub-counter bases: exclusive prefix of the counting pass's totals (groups with more segments
+  // than incidences only; deterministic per sub-counter)
+  unsigned long long tseg = 0;
   for (int k = 0; k < kCursors; ++k) {
-    cur[2 * kCursors + k] = tseg;
-    cur[3 * kCursors + k] = treg;
+    cur[kCursors + k] = tseg;
     tseg += cur[k];
-    treg += cur[kCursors + k];
   }
-  HIP_OR_FAIL(hipMemcpyAsync(db->cursor + 2 * kCursors, cur.data() + 2 * kCursors, 2 * kCursors * sizeof(unsigned long long),
+  HIP_OR_FAIL(hipMemcpyAsync(db->cursor + kCursors, cur.data() + kCursors, kCursors * sizeof(unsigned long long),
                              hipMemcpyHostToDevice, st));
   HIP_OR_FAIL(hipStreamSynchronize(st));
-  db->n_seg = (int64_t)tseg;
-  db->region = (int64_t)treg;
-  if (treg >= (1ull << 40)) return fail(ctx, GANON_E_ARG, "batch too large: overflow regions over 2^40 entries");
+  db->n_seg = db->n_incid + (int64_t)tseg;   // record slots: one per incidence, then the long groups
+  db->region = db->n_incid * db->region_per_incid + (int64_t)kGrpObs * ng;
   // far masks: at most one per nibble of a written read outside its group's pieces. That bound is
   // exact but loose (masks are the TN-mismatching nibbles only), and a batch whose scopes are not
   // in genome order can put most written bytes outside their pieces: the list is capped at 2^28

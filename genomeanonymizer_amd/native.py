@@ -478,6 +478,13 @@ class DeviceBatch:
                                                        _ptr(bases, _i32p), _ptr(tot, _i64p)), "download")
         return out, calls, bases, tot
 
+    def download_seq(self, out: np.ndarray) -> None:
+        """The masked bases into ``out`` (uint8, seq_bytes long; pinned memory for full PCIe rate)."""
+        if out.dtype != np.uint8 or len(out) < self.seq_bytes or not out.flags["C_CONTIGUOUS"]:
+            raise GanonError("download_seq: need a C-contiguous uint8 buffer of seq_bytes")
+        self.m._check(self.m._lib.ganon_batch_download(self.m._h, self.h, _ptr(out, _u8p), None, None, None),
+                      "download")
+
     def totals(self) -> np.ndarray:
         tot = np.zeros(GANON_N_TOTALS, np.int64)
         self.m._check(self.m._lib.ganon_batch_download(self.m._h, self.h, None, None, None, _ptr(tot, _i64p)),

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Phase timing of the group kernels on the config-2 batch (profiling aid, not a test).
 
-Runs ganon_batch_run with HIP-event timing for each configuration
+Runs ganon_batch_run (device prep + masking) with HIP-event timing for each configuration
 variant:unroll:skip[:group_target[:nt_copy[:ref2]]], interleaved over several rounds, and prints one
 JSON object of median per-kernel times. skip != 0 leaves phases out (GANON_PARAM_GROUP_SKIP)
 and gives invalid results: timing only. group_target is applied at upload (one upload per
@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--genome", type=int, default=None)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--configs", default="0:1:0,0:1:1,0:1:2,0:2:0,5:1:0,5:2:0",
+    ap.add_argument("--configs", default="0:1:0,0:2:0,0:2:1,0:2:2,0:2:4",
                     help="comma list of variant:unroll:skip[:group_target[:nt_copy[:ref2]]]")
     args = ap.parse_args()
     from genomeanonymizer_amd import native
@@ -38,7 +38,7 @@ def main():
     cfgs = []
     for c in args.configs.split(","):
         f = [int(x) for x in c.split(":")]
-        f += [256, 1, 1][len(f) - 3:] if len(f) < 6 else []
+        f += [704, 1, 1][len(f) - 3:] if len(f) < 6 else []
         cfgs.append(tuple(f[:6]))
     dbs = {}
     for c in cfgs:

@@ -120,8 +120,7 @@ struct ganon_dbatch {
   ganon_dev::DBuf b_ref_start, b_read_len, b_seq_off, b_cig_off, b_n_cig, b_dataset, b_write_scope, b_seq, b_cigar,
       b_incid_off, b_incid_read, b_span_start, b_span_len, b_ref_off, b_keep_pos, b_keep_code;
   // derived layer
-  ganon_dev::DBuf b_read_end, b_seen, b_cursor, b_gs0, b_lo, b_lo_idx, b_lo_sorted,
-      b_lo_idx_sorted, b_groups, b_seg4, b_grp_part, b_far, b_gokey, b_gopay, b_gtkey, b_gtflag, b_scan_tmp, b_out,
+  ganon_dev::DBuf b_read_end, b_seen, b_cursor, b_gs0, b_lo, b_linemap, b_groups, b_seg4, b_grp_part, b_far, b_gokey, b_gopay, b_gtkey, b_gtflag, b_out,
       b_scope_calls, b_scope_bases, b_small;   // b_small: totals, static totals, counters, acc, status, errors
   uint8_t *out = nullptr;
   int32_t *scope_calls = nullptr, *scope_bases = nullptr;
@@ -136,7 +135,6 @@ struct ganon_dbatch {
   // plan of the current contents (device prep, sized at upload)
   int32_t n_groups = 0, group_target = 512;
   int64_t n_seg = 0, region = 0, far_cap = 0, n_written = 0, region_per_incid = 0;
-  size_t scan_tmp_bytes = 0;
   // huge scopes (> kGrpMaxSpan positions): tile path, planned on the host at upload
   std::vector<void *> huge_allocs;
   ganon_dev::Tile *tiles_h = nullptr;

@@ -1133,9 +1133,9 @@ void free_batch(ganon_dbatch *db) {
   DBuf *bufs[] = {&db->b_ref_start, &db->b_read_len, &db->b_seq_off, &db->b_cig_off, &db->b_n_cig, &db->b_dataset,
                   &db->b_write_scope, &db->b_seq, &db->b_cigar, &db->b_incid_off, &db->b_incid_read,
                   &db->b_span_start, &db->b_span_len, &db->b_ref_off, &db->b_keep_pos, &db->b_keep_code,
-                  &db->b_read_end, &db->b_seen, &db->b_cursor, &db->b_gs0, &db->b_lo, &db->b_lo_idx, &db->b_lo_sorted, &db->b_lo_idx_sorted, &db->b_groups,
+                  &db->b_read_end, &db->b_seen, &db->b_cursor, &db->b_gs0, &db->b_lo, &db->b_linemap, &db->b_groups,
                   &db->b_seg4, &db->b_grp_part, &db->b_far, &db->b_gokey, &db->b_gopay, &db->b_gtkey, &db->b_gtflag,
-                  &db->b_scan_tmp, &db->b_out, &db->b_scope_calls, &db->b_scope_bases, &db->b_small};
+                  &db->b_out, &db->b_scope_calls, &db->b_scope_bases, &db->b_small};
   for (DBuf *b : bufs) free_buf(*b);
   free_huge(db);
   free_ref(db->own_ref);

@@ -24,15 +24,15 @@
 //                   the others from the back (the group kernel reads the front part through the
 //                   2-bit reference); read_end; the lowest buffer offset of the reads the group
 //                   writes, per dataset (LDS atomicMin);
-//   k_prep_pieces   rocPRIM radix sort of those 2 x groups candidates; the sorted candidates,
-//                   aligned down to 128-byte lines, tile the output buffer — each group copies
-//                   at most two pieces.
+//   k_prep_linemap + k_prep_pieces  the candidates mark their 128-byte lines in a 3-level
+//                   bitmap (ties on a line through a small hash table); each candidate's piece runs
+//                   from its line to the next marked one, so the pieces tile the output buffer —
+//                   each group copies at most two pieces. No sort.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cstring>
 
-#include <rocprim/rocprim.hpp>
 
 #include "ganon_batch.h"
 
@@ -247,27 +247,120 @@ __device__ __forceinline__ int4 piece(int64_t a, int64_t b) {
                    (int)(uint32_t)((uint64_t)b >> 32));
 }
 
-// Partition pieces from the sorted candidates: candidate i starts at its offset aligned down to
-// a line (the first at 0) and ends where the next candidate starts (the last at the end of the
-// buffer); a candidate whose next one starts on the same line is empty. Slot d of group g holds
-// the piece of its dataset-d candidate. No written read at all: one group copies everything.
-__global__ void __launch_bounds__(kPrepThreads) k_prep_pieces(const unsigned long long *__restrict__ key,
-                                                              const uint32_t *__restrict__ idx, int n_cand,
-                                                              int64_t seq_bytes, int4 *__restrict__ groups) {
-  for (int64_t i = blockIdx.x * (int64_t)kPrepThreads + threadIdx.x; i < n_cand;
-       i += (int64_t)gridDim.x * kPrepThreads) {
-    const unsigned long long k = key[i];
-    const uint32_t v = idx[i];
+// ---- partition pieces (no sort) --------------------------------------------------------------
+// Every candidate (a group's lowest written offset in one dataset) starts a piece on its 128-byte
+// line; a piece runs to the next line holding a candidate (the last one to the end of the buffer,
+// the first one from 0). Several candidates on one line: the one with the largest (offset, index)
+// owns it and the others get empty pieces — exactly what sorting the candidates and cutting at
+// their aligned offsets gives (round 1's plan; the previous version sorted with rocPRIM). Lines
+// holding a candidate are a 3-level bitmap (bit per line / per level-0 word / per level-1 word),
+// so "next" and "previous" marked line are a few word loads; ties go through a small hash table
+// keyed by line with a 64-bit atomicMax of (offset << 25 | candidate index).
+struct LineMap {
+  unsigned long long *l0, *l1, *l2;   // bit per line, per nonzero l0 word, per nonzero l1 word
+  unsigned long long *hkey, *hval;    // tie table: line + 1 (0 empty), max (offset << 25 | candidate)
+  int64_t n_lines, n0, n1, n2;        // lines, words per level
+  int64_t hsize;                      // power of two
+};
+
+__device__ __forceinline__ unsigned long long bit_above(unsigned long long w, int b) {   // bits > b
+  return b >= 63 ? 0ull : w & (~0ull << (b + 1));
+}
+__device__ __forceinline__ unsigned long long bit_below(unsigned long long w, int b) {   // bits < b
+  return b <= 0 ? 0ull : w & (~0ull >> (64 - b));
+}
+
+// Smallest marked index > x at level `lv` words (n words), or -1.
+__device__ int64_t map_next(const LineMap &M, int64_t x) {
+  int64_t w = x >> 6;
+  unsigned long long m = bit_above(M.l0[w], (int)(x & 63));
+  if (m) return (w << 6) + __ffsll((long long)m) - 1;
+  int64_t w1 = w >> 6;                      // l1 word holding bit w
+  unsigned long long m1 = bit_above(M.l1[w1], (int)(w & 63));
+  if (!m1) {
+    int64_t w2 = w1 >> 6;
+    unsigned long long m2 = bit_above(M.l2[w2], (int)(w1 & 63));
+    while (!m2) {
+      if (++w2 >= M.n2) return -1;
+      m2 = M.l2[w2];
+    }
+    w1 = (w2 << 6) + __ffsll((long long)m2) - 1;
+    m1 = M.l1[w1];
+  }
+  w = (w1 << 6) + __ffsll((long long)m1) - 1;
+  return (w << 6) + __ffsll((long long)M.l0[w]) - 1;
+}
+
+// Is any index < x marked?
+__device__ bool map_any_below(const LineMap &M, int64_t x) {
+  int64_t w = x >> 6;
+  if (bit_below(M.l0[w], (int)(x & 63))) return true;
+  int64_t w1 = w >> 6;
+  if (bit_below(M.l1[w1], (int)(w & 63))) return true;
+  int64_t w2 = w1 >> 6;
+  if (bit_below(M.l2[w2], (int)(w1 & 63))) return true;
+  for (int64_t k = 0; k < w2; ++k)
+    if (M.l2[k]) return true;
+  return false;
+}
+
+__device__ __forceinline__ unsigned hash_line(int64_t line, int64_t hsize) {
+  return (unsigned)(((uint64_t)line * 0x9E3779B97F4A7C15ull) >> 32) & (unsigned)(hsize - 1);
+}
+
+// Mark candidate c (lowest offset `key`) of the emit kernel's group.
+__device__ void map_mark(const LineMap &M, unsigned long long key, uint32_t c) {
+  const int64_t line = (int64_t)(key >> 7);
+  atomicOr(&M.l0[line >> 6], 1ull << (line & 63));
+  const unsigned long long tag = (unsigned long long)line + 1, v = (key << 25) | c;
+  for (unsigned h = hash_line(line, M.hsize);; h = (h + 1) & (unsigned)(M.hsize - 1)) {
+    const unsigned long long prev = atomicCAS(&M.hkey[h], 0ull, tag);
+    if (prev == 0ull || prev == tag) {
+      atomicMax(&M.hval[h], v);
+      return;
+    }
+  }
+}
+
+// l1 / l2 from l0 (thread per l1 word).
+__global__ void __launch_bounds__(kPrepThreads) k_prep_linemap(LineMap M) {
+  for (int64_t w1 = blockIdx.x * (int64_t)kPrepThreads + threadIdx.x; w1 < M.n1; w1 += (int64_t)gridDim.x * kPrepThreads) {
+    unsigned long long b = 0;
+    for (int k = 0; k < 64; ++k) {
+      const int64_t w = (w1 << 6) + k;
+      if (w < M.n0 && M.l0[w]) b |= 1ull << k;
+    }
+    M.l1[w1] = b;
+    if (b) atomicOr(&M.l2[w1 >> 6], 1ull << (w1 & 63));
+  }
+}
+
+// Piece of candidate c: slot d = c & 1 of group c >> 1. No candidate at all: candidate 0 (group
+// 0, dataset 0) copies the whole buffer.
+__global__ void __launch_bounds__(kPrepThreads) k_prep_pieces(const unsigned long long *__restrict__ lo, int n_cand,
+                                                              LineMap M, int64_t seq_bytes, int4 *__restrict__ groups) {
+  for (int64_t c = blockIdx.x * (int64_t)kPrepThreads + threadIdx.x; c < n_cand; c += (int64_t)gridDim.x * kPrepThreads) {
+    const unsigned long long k = lo[c];
     int4 pc = piece(0, 0);
     if (k != kNone) {
-      const int64_t c = i == 0 ? 0 : (int64_t)(k & ~(unsigned long long)(kPartAlign - 1));
-      const unsigned long long kn = i + 1 < n_cand ? key[i + 1] : kNone;
-      const int64_t e = kn != kNone ? (int64_t)(kn & ~(unsigned long long)(kPartAlign - 1)) : seq_bytes;
-      if (e > c) pc = piece(c, e);
-    } else if (i == 0) {
-      pc = piece(0, seq_bytes);
+      const int64_t line = (int64_t)(k >> 7);
+      unsigned long long win = 0;
+      for (unsigned h = hash_line(line, M.hsize);; h = (h + 1) & (unsigned)(M.hsize - 1))
+        if (M.hkey[h] == (unsigned long long)line + 1) {
+          win = M.hval[h];
+          break;
+        }
+      if ((win & ((1ull << 25) - 1)) == (unsigned long long)c) {
+        const int64_t next = map_next(M, line);
+        const int64_t a = map_any_below(M, line) ? line * kPartAlign : 0;
+        pc = piece(a, next < 0 ? seq_bytes : next * kPartAlign);
+      }
+    } else if (c == 0) {
+      bool any = false;   // no candidate at all: candidate 0 copies the whole buffer
+      for (int64_t w = 0; w < M.n2 && !any; ++w) any = M.l2[w] != 0;
+      if (!any) pc = piece(0, seq_bytes);
     }
-    groups[kGrpRec * (int64_t)(v >> 1) + 2 + 2 * (v & 1)] = pc;
+    groups[kGrpRec * (c >> 1) + 2 + 2 * (c & 1)] = pc;
   }
 }
 
@@ -390,8 +483,7 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_emit(const Raw R, const l
                                                             int64_t n_blk, long long region_per_incid,
                                                             int32_t *__restrict__ read_end, int4 *__restrict__ seg4,
                                                             int4 *__restrict__ groups, unsigned long long *__restrict__ lo,
-                                                            uint32_t *__restrict__ lo_idx,
-                                                            unsigned long long *__restrict__ cursor,
+                                                            LineMap M, unsigned long long *__restrict__ cursor,
                                                             const unsigned long long *__restrict__ cursor_base) {
   __shared__ long long off[kGrpMaxScopes + 1];
   __shared__ long long ref0[kGrpMaxScopes];
@@ -564,7 +656,7 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_emit(const Raw R, const l
   }
   if (tid < 2) {
     lo[2 * (int64_t)g + tid] = lmin[tid];
-    lo_idx[2 * (int64_t)g + tid] = (uint32_t)(2 * g + tid);
+    if (lmin[tid] != kNone) map_mark(M, lmin[tid], (uint32_t)(2 * g + tid));
   }
   if (tid == 0) {
     const int64_t mid = seg_b + tot_c;
@@ -637,14 +729,34 @@ int check_err(ganon_ctx *ctx, ganon_dbatch *db) {
   return GANON_OK;
 }
 
-// Temp storage of the candidate sort (c candidates).
-hipError_t sort_bytes(int64_t c, size_t &bytes) {
-  return rocprim::radix_sort_pairs(nullptr, bytes, (unsigned long long *)nullptr, (unsigned long long *)nullptr,
-                                   (uint32_t *)nullptr, (uint32_t *)nullptr, (size_t)c, 0, 40, 0);
+// The line map over the batch's output buffer (b_linemap: l0 | l1 | l2 | hash keys | hash values).
+LineMap line_map(const ganon_dbatch *db) {
+  LineMap M;
+  M.n_lines = std::max<int64_t>(1, (db->seq_bytes + kPartAlign - 1) / kPartAlign);
+  M.n0 = (M.n_lines + 63) / 64;
+  M.n1 = (M.n0 + 63) / 64;
+  M.n2 = (M.n1 + 63) / 64;
+  int64_t h = 64;
+  while (h < 4 * 2 * (int64_t)db->n_groups) h <<= 1;
+  M.hsize = h;
+  auto *base = static_cast<unsigned long long *>(db->b_linemap.p);
+  M.l0 = base;
+  M.l1 = M.l0 + M.n0;
+  M.l2 = M.l1 + M.n1;
+  M.hkey = M.l2 + M.n2;
+  M.hval = M.hkey + M.hsize;
+  return M;
+}
+
+int64_t line_map_words(const ganon_dbatch *db) {
+  const LineMap M = line_map(db);
+  return M.n0 + M.n1 + M.n2 + 2 * M.hsize;
 }
 
 int launch_groups(ganon_ctx *ctx, ganon_dbatch *db, const Raw &R) {
   KernelScope ks(ctx, "prep_groups");
+  if (db->n_groups)   // the line map, marked by the emit kernel
+    HIP_OR_FAIL(hipMemsetAsync(db->b_linemap.p, 0, (size_t)line_map_words(db) * 8, ctx->stream));
   hipLaunchKernelGGL(k_prep_groups, dim3(grid_for(std::max<int64_t>(db->n_scopes, kCursors))), dim3(kPrepThreads), 0,
                      ctx->stream, R, weight_of(db->group_target), (long long)db->group_target,
                      static_cast<longlong2 *>(db->b_gs0.p), db->cursor);
@@ -658,8 +770,7 @@ int launch_emit(ganon_ctx *ctx, ganon_dbatch *db, const Raw &R, int write) {
                      static_cast<const longlong2 *>(db->b_gs0.p), db->n_groups, write, db->ref->bad, db->ref->n_blk,
                      (long long)db->region_per_incid, const_cast<int32_t *>(db->B.read_end),
                      static_cast<int4 *>(db->b_seg4.p), static_cast<int4 *>(db->b_groups.p),
-                     static_cast<unsigned long long *>(db->b_lo.p), static_cast<uint32_t *>(db->b_lo_idx.p),
-                     db->cursor, db->cursor + kCursors);
+                     static_cast<unsigned long long *>(db->b_lo.p), line_map(db), db->cursor, db->cursor + kCursors);
   return check_launch(ctx, "k_prep_emit");
 }
 
@@ -668,16 +779,11 @@ int launch_pieces(ganon_ctx *ctx, ganon_dbatch *db) {
   const int n_cand = 2 * db->n_groups;
   if (!db->n_groups) return GANON_OK;
   KernelScope ks(ctx, "prep_pieces");
-  auto *lo = static_cast<unsigned long long *>(db->b_lo.p);
-  auto *lo_idx = static_cast<uint32_t *>(db->b_lo_idx.p);
-  auto *lo_s = static_cast<unsigned long long *>(db->b_lo_sorted.p);
-  auto *idx_s = static_cast<uint32_t *>(db->b_lo_idx_sorted.p);
-  size_t bytes = db->scan_tmp_bytes;
-  if (rocprim::radix_sort_pairs(db->b_scan_tmp.p, bytes, lo, lo_s, lo_idx, idx_s, (size_t)n_cand, 0, 40, st) !=
-      hipSuccess)
-    return fail(ctx, GANON_E_DEVICE, "prep: candidate sort failed");
-  hipLaunchKernelGGL(k_prep_pieces, dim3(grid_for(n_cand)), dim3(kPrepThreads), 0, st, lo_s, idx_s, n_cand,
-                     db->seq_bytes, static_cast<int4 *>(db->b_groups.p));
+  const LineMap M = line_map(db);
+  hipLaunchKernelGGL(k_prep_linemap, dim3(grid_for(M.n1)), dim3(kPrepThreads), 0, st, M);
+  hipLaunchKernelGGL(k_prep_pieces, dim3(grid_for(n_cand)), dim3(kPrepThreads), 0, st,
+                     static_cast<const unsigned long long *>(db->b_lo.p), n_cand, M, db->seq_bytes,
+                     static_cast<int4 *>(db->b_groups.p));
   return check_launch(ctx, "k_prep_pieces");
 }
 
@@ -753,15 +859,9 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db, const int64_t *host_incid_off) {
   longlong2 *gm = nullptr;
   if ((rc = grow_n(ctx, db->b_gs0, ng, &gm)) || (rc = grow_n(ctx, db->b_groups, (size_t)kGrpRec * ng, &grp)) ||
       (rc = grow_n(ctx, db->b_grp_part, 2 * (size_t)ng, &p32)) ||
-      (rc = grow_n(ctx, db->b_lo, 2 * (size_t)ng, &u64)) || (rc = grow_n(ctx, db->b_lo_sorted, 2 * (size_t)ng, &u64)) ||
-      (rc = grow_n(ctx, db->b_lo_idx, 2 * (size_t)ng, &u32)) ||
-      (rc = grow_n(ctx, db->b_lo_idx_sorted, 2 * (size_t)ng, &u32)))
+      (rc = grow_n(ctx, db->b_lo, 2 * (size_t)ng, &u64)) ||
+      (rc = grow_n(ctx, db->b_linemap, (size_t)line_map_words(db), &u64)))
     return rc;
-  size_t tmp = 0;
-  if (sort_bytes(2 * ng, tmp) != hipSuccess) return fail(ctx, GANON_E_DEVICE, "prep: rocPRIM sizing failed");
-  uint8_t *t8 = nullptr;
-  if ((rc = grow_n(ctx, db->b_scan_tmp, tmp, &t8))) return rc;
-  db->scan_tmp_bytes = tmp;
   HIP_OR_FAIL(hipMemsetAsync(db->cursor + kCursors, 0, kCursors * sizeof(unsigned long long), st));
   if ((rc = launch_groups(ctx, db, R)) || (rc = launch_emit(ctx, db, R, 0)) || (rc = launch_pieces(ctx, db))) return rc;
   if (ng && nr)

@@ -42,9 +42,11 @@ class MaskResult:
 
 
 def build_batch(plan: Plan, tables: Tuple[ReadTable, ReadTable], fasta: FastaRef,
-                scope_ids=None) -> Tuple[dict, dict]:
+                scope_ids=None, written=None) -> Tuple[dict, dict]:
     """Lay the plan's scopes (all, or the subset ``scope_ids`` of one contig shard) out as
-    one ganon_batch (include/ganon.h). Batch scope k is plan scope ``meta['scope_ids'][k]``."""
+    one ganon_batch (include/ganon.h). Batch scope k is plan scope ``meta['scope_ids'][k]``.
+    ``written``: (dataset, row, scope) arrays of the instances to mask, at most one masked scope
+    per read (default: the plan's written records)."""
     T, N = tables
     packed, nib_off = fasta.packed()
     scopes = plan.scopes if scope_ids is None else [plan.scopes[i] for i in scope_ids]
@@ -72,7 +74,7 @@ def build_batch(plan: Plan, tables: Tuple[ReadTable, ReadTable], fasta: FastaRef
     arr["cigar"] = np.ascontiguousarray(np.concatenate([T.cigar, N.cigar]).astype(np.uint32))
     arr["dataset"] = np.concatenate([np.zeros(len(rows[0]), np.uint8), np.ones(len(rows[1]), np.uint8)])
     ws = np.full(n_reads, -1, np.int32)
-    w_ds, w_row, w_sc = plan.written_arrays()
+    w_ds, w_row, w_sc = plan.written_arrays() if written is None else written
     loc = np.full(len(plan.scopes) + 1, -1, np.int64)
     loc[[sc.id for sc in scopes]] = np.arange(len(scopes))
     sel = (w_sc >= 0) & (loc[np.where(w_sc >= 0, w_sc, len(plan.scopes))] >= 0)
@@ -161,12 +163,12 @@ class CompleteGermlineAnonymizer:
         fmt = getattr(self.engine, "format_fastq", None)
         return fmt(recs) if fmt is not None else native.host_format_fastq(recs)
 
-    def anonymize(self, planner: SamplePlanner, plan: Plan, scope_ids=None) -> MaskResult:
+    def anonymize(self, planner: SamplePlanner, plan: Plan, scope_ids=None, written=None) -> MaskResult:
         """Mask all scopes of ``plan`` (or the contig shard ``scope_ids``) in one device batch.
         Per-scope counts come back indexed by plan scope id (zero outside the shard)."""
         tables = planner.tables
         fasta = planner.fasta
-        arrays, meta = build_batch(plan, tables, fasta, scope_ids)
+        arrays, meta = build_batch(plan, tables, fasta, scope_ids, written)
         out, b_calls, b_bases, totals, irecs = self.engine.mask(arrays, indels=True)
         calls = np.zeros(len(plan.scopes), np.int32)
         bases = np.zeros(len(plan.scopes), np.int32)

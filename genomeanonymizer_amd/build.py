@@ -47,7 +47,7 @@ HIP_SOURCES = ("ganon_hip.hip", "ganon_prep.hip", "ganon_fastq.hip", "ganon_inde
 
 
 def build_hip(force: bool = False) -> str:
-    """One object per source, compiled in parallel, then linked (the hipcub sort in
+    """One object per source, compiled in parallel, then linked (the rocPRIM sort in
     ganon_indel.hip is the slowest unit)."""
     srcs = [os.path.join(CSRC, s) for s in HIP_SOURCES]
     hdrs = [os.path.join(REPO, "include", "ganon.h"), os.path.join(CSRC, "ganon_ctx.h"), os.path.join(CSRC, "ganon_batch.h"),

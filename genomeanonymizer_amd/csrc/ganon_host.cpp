@@ -63,96 +63,83 @@ static int set_err(const std::string &m) {
 
 GANON_HOST_API const char *ganon_host_last_error(void) { return g_err.c_str(); }
 
-static int bam_open_impl(const char *path, int threads, ganon_bam **out) {
-  FILE *fh = std::fopen(path, "rb");
-  if (!fh) return set_err(std::string("cannot open ") + path);
-  std::fseek(fh, 0, SEEK_END);
-  const long fsize = std::ftell(fh);
-  std::fseek(fh, 0, SEEK_SET);
-  std::vector<uint8_t> file((size_t)std::max(0L, fsize));
-  if (fsize > 0 && std::fread(file.data(), 1, (size_t)fsize, fh) != (size_t)fsize) {
-    std::fclose(fh);
-    return set_err("short read");
+namespace {
+
+// One BGZF block at h (avail bytes from h to the end of the buffer). Returns 1 with the block's
+// total length, payload position/length and ISIZE; 0 when the buffer ends inside the block; -1 on a
+// malformed block (message set). Untrusted input: every field is checked before it is used.
+int parse_block(const uint8_t *h, int64_t avail, int64_t &blen, int64_t &in_rel, int32_t &in_len, int32_t &isize) {
+  if (avail < 18) return 0;
+  if (h[0] != 31 || h[1] != 139 || h[2] != 8 || !(h[3] & 4)) return set_err("not a BGZF file");
+  const int xlen = h[10] | (h[11] << 8);
+  if (12 + xlen + 8 > avail) return 0;   // the extra field and the CRC32/ISIZE trailer
+  int bsize = -1;
+  for (int x = 12; x < 12 + xlen;) {
+    if (x + 4 > 12 + xlen) return set_err("malformed BGZF extra subfield");
+    const int slen = h[x + 2] | (h[x + 3] << 8);
+    if (x + 4 + slen > 12 + xlen) return set_err("malformed BGZF extra subfield");
+    if (h[x] == 66 && h[x + 1] == 67 && slen == 2) bsize = h[x + 4] | (h[x + 5] << 8);
+    x += 4 + slen;
   }
-  std::fclose(fh);
-  // ---- BGZF block table (untrusted input: every field is checked before it is used) ----
-  std::vector<Block> blocks;
-  int64_t off = 0, total = 0;
-  const int64_t fsz = (int64_t)file.size();
-  while (off < fsz) {
-    if (off + 18 > fsz) return set_err("truncated BGZF header");
-    const uint8_t *h = &file[off];
-    if (h[0] != 31 || h[1] != 139 || h[2] != 8 || !(h[3] & 4)) return set_err("not a BGZF file");
-    const int xlen = h[10] | (h[11] << 8);
-    // the extra field and the 8-byte CRC32/ISIZE trailer must lie inside the file
-    if (off + 12 + xlen + 8 > fsz) return set_err("truncated BGZF extra field");
-    int bsize = -1;
-    for (int x = 12; x < 12 + xlen;) {
-      if (x + 4 > 12 + xlen) return set_err("malformed BGZF extra subfield");
-      const int slen = h[x + 2] | (h[x + 3] << 8);
-      if (x + 4 + slen > 12 + xlen) return set_err("malformed BGZF extra subfield");
-      if (h[x] == 66 && h[x + 1] == 67 && slen == 2) bsize = h[x + 4] | (h[x + 5] << 8);
-      x += 4 + slen;
-    }
-    if (bsize < 0) return set_err("BGZF block without BC subfield");
-    const int64_t blen = (int64_t)bsize + 1;
-    if (off + blen > fsz) return set_err("truncated BGZF block");
-    const int64_t in_len = blen - 12 - xlen - 8;
-    if (in_len < 0) return set_err("BGZF block size smaller than its header");
-    Block b;
-    b.in_off = off + 12 + xlen;
-    b.in_len = (int32_t)in_len;
-    uint32_t isize;
-    std::memcpy(&isize, &file[off + blen - 4], 4);
-    if (isize > 65536) return set_err("BGZF block ISIZE over 64 KiB");
-    b.out_len = (int32_t)isize;
-    b.out_off = total;
-    total += isize;
-    if (b.out_len > 0) blocks.push_back(b);
-    off += blen;
-  }
-  std::vector<uint8_t> data((size_t)total);
-  std::atomic<int64_t> next{0};
+  if (bsize < 0) return set_err("BGZF block without BC subfield");
+  blen = (int64_t)bsize + 1;
+  if (blen > avail) return 0;
+  const int64_t il = blen - 12 - xlen - 8;
+  if (il < 0) return set_err("BGZF block size smaller than its header");
+  uint32_t is;
+  std::memcpy(&is, h + blen - 4, 4);
+  if (is > 65536) return set_err("BGZF block ISIZE over 64 KiB");
+  in_rel = 12 + xlen;
+  in_len = (int32_t)il;
+  isize = (int32_t)is;
+  return 1;
+}
+
+// Inflates blocks[b0, b1) of `file` into data (block out_off relative to blocks[b0].out_off).
+bool inflate_blocks(const uint8_t *file, const std::vector<Block> &blocks, size_t b0, size_t b1, uint8_t *data,
+                    int threads) {
+  std::atomic<size_t> next{b0};
   std::atomic<bool> bad{false};
+  const int64_t base = b0 < b1 ? blocks[b0].out_off : 0;
   const int nt = std::max(1, std::min(threads, 64));
   auto worker = [&]() {
     for (;;) {
-      const int64_t i = next.fetch_add(1);
-      if (i >= (int64_t)blocks.size() || bad.load()) return;
+      const size_t i = next.fetch_add(1);
+      if (i >= b1 || bad.load()) return;
       const Block &b = blocks[i];
-      if (!inflate_raw(&file[b.in_off], b.in_len, &data[b.out_off], b.out_len)) bad = true;
+      if (!inflate_raw(file + b.in_off, b.in_len, data + (b.out_off - base), b.out_len)) bad = true;
     }
   };
   std::vector<std::thread> pool;
-  for (int t = 1; t < nt; ++t) pool.emplace_back(worker);
+  for (int t = 1; t < nt && (size_t)t < b1 - b0; ++t) pool.emplace_back(worker);
   worker();
   for (auto &t : pool) t.join();
-  if (bad) return set_err("BGZF inflate failed");
-  file.clear();
-  file.shrink_to_fit();
-  // ---- BAM header ----
-  auto *bam = new ganon_bam();
-  auto die = [&](const char *m) {
-    delete bam;
-    return set_err(m);
-  };
-  const uint8_t *d = data.data();
-  const int64_t n = (int64_t)data.size();
-  if (n < 12 || std::memcmp(d, "BAM\1", 4) != 0) return die("not a BAM stream");
+  return !bad;
+}
+
+// BAM header (magic, text, reference list) at d[0, n). Returns 1 with p = first record offset, 0
+// when n ends inside the header, -1 on a malformed header.
+int parse_header(const uint8_t *d, int64_t n, ganon_bam *bam, int64_t &p) {
+  if (n < 12) return 0;
+  if (std::memcmp(d, "BAM\1", 4) != 0) return set_err("not a BAM stream");
   int32_t l_text, n_ref;
   std::memcpy(&l_text, d + 4, 4);
-  if (l_text < 0) return die("negative header text length");
-  int64_t p = 8 + (int64_t)l_text;
-  if (p + 4 > n) return die("truncated header");
+  if (l_text < 0) return set_err("negative header text length");
+  p = 8 + (int64_t)l_text;
+  if (p + 4 > n) return 0;
   std::memcpy(&n_ref, d + p, 4);
   p += 4;
-  if (n_ref < 0) return die("negative reference count");
+  if (n_ref < 0) return set_err("negative reference count");
+  bam->ref_names.clear();
+  bam->ref_name_off.clear();
+  bam->ref_len.clear();
   for (int32_t i = 0; i < n_ref; ++i) {
     int32_t l_name, l_ref;
-    if (p + 4 > n) return die("truncated reference list");
+    if (p + 4 > n) return 0;
     std::memcpy(&l_name, d + p, 4);
     p += 4;
-    if (l_name <= 0 || p + l_name + 4 > n) return die("bad reference name");
+    if (l_name <= 0) return set_err("bad reference name");
+    if (p + l_name + 4 > n) return 0;
     bam->ref_name_off.push_back((int64_t)bam->ref_names.size());
     bam->ref_names.insert(bam->ref_names.end(), d + p, d + p + l_name);
     bam->ref_names.back() = '\0';
@@ -161,13 +148,19 @@ static int bam_open_impl(const char *path, int threads, ganon_bam **out) {
     p += 4;
     bam->ref_len.push_back(l_ref);
   }
+  return 1;
+}
+
+// Column arrays of the records packed back to back in d[p, n) (each: block_size + body).
+int records_to_columns(const uint8_t *d, int64_t p, int64_t n, ganon_bam *bam, int threads) {
+  const int nt = std::max(1, std::min(threads, 64));
   // ---- records: boundaries (sequential), sizes + offsets, then columns in parallel ----
   std::vector<int64_t> rec;   // offset of each record's block_size field
   while (p < n) {
     int32_t bs;
-    if (p + 4 > n) return die("truncated record size");
+    if (p + 4 > n) return set_err("truncated record size");
     std::memcpy(&bs, d + p, 4);
-    if (bs < 32 || p + 4 + bs > n) return die("bad record size");
+    if (bs < 32 || p + 4 + bs > n) return set_err("bad record size");
     rec.push_back(p);
     p += 4 + bs;
   }
@@ -206,7 +199,7 @@ static int bam_open_impl(const char *path, int threads, ganon_bam **out) {
       o_aux[i + 1] = bs - need;
     }
   });
-  if (first_bad.load() != INT64_MAX) return die("record fields exceed block size");
+  if (first_bad.load() != INT64_MAX) return set_err("record fields exceed block size");
   for (int64_t i = 0; i < nr; ++i) {
     o_name[i + 1] += o_name[i];
     o_cig[i + 1] += o_cig[i];
@@ -277,6 +270,53 @@ static int bam_open_impl(const char *path, int threads, ganon_bam **out) {
       copy_bytes(bam->aux.data() + o_aux[i], r + q, (size_t)(bs - q));
     }
   });
+  return 0;
+}
+
+
+}  // namespace
+
+static int bam_open_impl(const char *path, int threads, ganon_bam **out) {
+  FILE *fh = std::fopen(path, "rb");
+  if (!fh) return set_err(std::string("cannot open ") + path);
+  std::fseek(fh, 0, SEEK_END);
+  const long fsize = std::ftell(fh);
+  std::fseek(fh, 0, SEEK_SET);
+  std::vector<uint8_t> file((size_t)std::max(0L, fsize));
+  if (fsize > 0 && std::fread(file.data(), 1, (size_t)fsize, fh) != (size_t)fsize) {
+    std::fclose(fh);
+    return set_err("short read");
+  }
+  std::fclose(fh);
+  std::vector<Block> blocks;
+  int64_t off = 0, total = 0;
+  const int64_t fsz = (int64_t)file.size();
+  while (off < fsz) {
+    int64_t blen, in_rel;
+    int32_t in_len, isize;
+    const int rc = parse_block(&file[off], fsz - off, blen, in_rel, in_len, isize);
+    if (rc < 0) return -1;
+    if (rc == 0) return set_err("truncated BGZF block");
+    if (isize > 0) blocks.push_back(Block{off + in_rel, in_len, isize, total});
+    total += isize;
+    off += blen;
+  }
+  std::vector<uint8_t> data((size_t)total);
+  if (!inflate_blocks(file.data(), blocks, 0, blocks.size(), data.data(), threads))
+    return set_err("BGZF inflate failed");
+  file.clear();
+  file.shrink_to_fit();
+  auto *bam = new ganon_bam();
+  int64_t p = 0;
+  const int hr = parse_header(data.data(), (int64_t)data.size(), bam, p);
+  if (hr <= 0) {
+    delete bam;
+    return hr < 0 ? -1 : set_err("truncated header");
+  }
+  if (records_to_columns(data.data(), p, (int64_t)data.size(), bam, threads) != 0) {
+    delete bam;
+    return -1;
+  }
   *out = bam;
   return 0;
 }
@@ -335,6 +375,289 @@ GANON_HOST_API int ganon_bam_view_get(ganon_bam *b, ganon_bam_view *v) {
 GANON_HOST_API const char *ganon_bam_error(ganon_bam *) { return g_err.c_str(); }
 
 GANON_HOST_API void ganon_bam_close(ganon_bam *b) { delete b; }
+
+// ---- contig reader (bounded-memory streaming decode) ------------------------------------------
+// The reference reads a sample through region queries (AlignmentFile.fetch / pileup per section,
+// short_read_tumor_normal_anonymizer.py:498-558, pileup_io.pyx:8-41), never the whole file at once.
+// The reader decodes the records of one reference sequence at a time: it seeks to the sequence's
+// first record through the BAM index (.bai: pseudo-bin 37450 or the smallest chunk start of its
+// bins) or, without one, streams forward from the previous sequence's end; it inflates a bounded
+// window of BGZF blocks at a time on `threads` threads and keeps only the sequence's records.
+struct ganon_bam_reader {
+  FILE *fh = nullptr;
+  int64_t fsize = 0;
+  int threads = 8;
+  int64_t chunk = 32 << 20;          // compressed bytes read per step
+  ganon_bam header;                  // reference list only
+  int64_t data_voff = 0;             // virtual offset of the first record
+  bool has_index = false;
+  std::vector<int64_t> index_beg;    // per tid: virtual offset of its first record, -1 = no records
+  int64_t cur_voff = -1;             // forward cursor: the first record not yet consumed
+  int32_t cur_tid = 0;
+};
+
+namespace {
+
+constexpr int32_t kTidEnd = INT32_MAX;
+inline int64_t tid_order(int32_t t) { return t < 0 ? (int64_t)INT32_MAX : (int64_t)t; }   // unplaced last
+
+// Reads and inflates complete BGZF blocks starting at file offset coff (at most R->chunk compressed
+// bytes). Appends the inflated bytes to data and one (data offset, file offset) pair per non-empty
+// block to bmap. Returns the file offset after the last complete block, or -1 on error.
+int64_t read_blocks(ganon_bam_reader *R, int64_t coff, std::vector<uint8_t> &data,
+                    std::vector<std::pair<int64_t, int64_t>> &bmap) {
+  const int64_t want = std::min<int64_t>(R->chunk, R->fsize - coff);
+  std::vector<uint8_t> comp((size_t)want);
+  if (std::fseek(R->fh, (long)coff, SEEK_SET) != 0 || std::fread(comp.data(), 1, (size_t)want, R->fh) != (size_t)want)
+    return set_err("short read");
+  std::vector<Block> blocks;
+  std::vector<int64_t> bcoff;
+  int64_t off = 0, total = 0;
+  while (off < want) {
+    int64_t blen, in_rel;
+    int32_t in_len, isize;
+    const int rc = parse_block(&comp[(size_t)off], want - off, blen, in_rel, in_len, isize);
+    if (rc < 0) return -1;
+    if (rc == 0) break;
+    if (isize > 0) {
+      blocks.push_back(Block{off + in_rel, in_len, isize, total});
+      bcoff.push_back(coff + off);
+    }
+    total += isize;
+    off += blen;
+  }
+  if (off == 0) return set_err("truncated BGZF block");
+  const size_t base = data.size();
+  data.resize(base + (size_t)total);
+  if (!inflate_blocks(comp.data(), blocks, 0, blocks.size(), data.data() + base, R->threads))
+    return set_err("BGZF inflate failed");
+  for (size_t i = 0; i < blocks.size(); ++i) bmap.emplace_back((int64_t)base + blocks[i].out_off, bcoff[i]);
+  return coff + off;
+}
+
+int64_t voff_at(const std::vector<std::pair<int64_t, int64_t>> &bmap, int64_t x) {
+  auto it = std::upper_bound(bmap.begin(), bmap.end(), std::make_pair(x, INT64_MAX));
+  if (it == bmap.begin()) return -1;
+  --it;
+  return (it->second << 16) | (x - it->first);
+}
+
+// Streams from virtual offset voff: keeps the records of `tid`, stops at the first record after them
+// (each tid's records are contiguous in a coordinate-sorted file). first_tid: tid of the first
+// record met (kTidEnd when none) so that an index start can be validated.
+int scan_tid(ganon_bam_reader *R, int64_t voff, int32_t tid, std::vector<uint8_t> &kept, int64_t &next_voff,
+             int32_t &next_tid, int32_t &first_tid) {
+  int64_t coff = voff >> 16;
+  std::vector<uint8_t> data;
+  std::vector<std::pair<int64_t, int64_t>> bmap;
+  int64_t dpos = (int64_t)(voff & 0xFFFF);
+  bool seen = false;
+  first_tid = kTidEnd;
+  for (;;) {
+    if (coff >= R->fsize) {
+      if (dpos != (int64_t)data.size()) return set_err("truncated BAM record");
+      next_voff = -1;
+      next_tid = kTidEnd;
+      return 0;
+    }
+    // drop consumed bytes (keep the block map entries still needed for offsets >= dpos)
+    if (dpos > 0 && !data.empty()) {
+      const int64_t cut = std::min<int64_t>(dpos, (int64_t)data.size());
+      data.erase(data.begin(), data.begin() + cut);
+      dpos -= cut;
+      for (auto &e : bmap) e.first -= cut;
+      size_t k = 0;
+      while (k + 1 < bmap.size() && bmap[k + 1].first <= 0) ++k;
+      bmap.erase(bmap.begin(), bmap.begin() + (long)k);
+    }
+    coff = read_blocks(R, coff, data, bmap);
+    if (coff < 0) return -1;
+    for (;;) {
+      if (dpos + 4 > (int64_t)data.size()) break;
+      int32_t bs, rtid;
+      std::memcpy(&bs, &data[(size_t)dpos], 4);
+      if (bs < 32) return set_err("bad record size");
+      if (dpos + 4 + bs > (int64_t)data.size()) break;
+      std::memcpy(&rtid, &data[(size_t)dpos + 4], 4);
+      if (first_tid == kTidEnd) first_tid = rtid;
+      if (rtid == tid) {
+        kept.insert(kept.end(), data.begin() + dpos, data.begin() + dpos + 4 + bs);
+        seen = true;
+      } else if (seen || tid_order(rtid) > tid_order(tid)) {
+        next_voff = voff_at(bmap, dpos);
+        next_tid = rtid;
+        return 0;
+      }
+      dpos += 4 + bs;
+    }
+  }
+}
+
+void load_index(ganon_bam_reader *R, const std::string &bam_path) {
+  std::vector<std::string> cands{bam_path + ".bai"};
+  if (bam_path.size() > 4 && bam_path.compare(bam_path.size() - 4, 4, ".bam") == 0)
+    cands.push_back(bam_path.substr(0, bam_path.size() - 4) + ".bai");
+  for (const std::string &ip : cands) {
+    FILE *f = std::fopen(ip.c_str(), "rb");
+    if (!f) continue;
+    std::vector<uint8_t> b;
+    uint8_t tmp[65536];
+    size_t k;
+    while ((k = std::fread(tmp, 1, sizeof tmp, f)) > 0) b.insert(b.end(), tmp, tmp + k);
+    std::fclose(f);
+    size_t p = 0;
+    auto rd = [&](void *dst, size_t n) {
+      if (p + n > b.size()) return false;
+      std::memcpy(dst, &b[p], n);
+      p += n;
+      return true;
+    };
+    char magic[4];
+    int32_t n_ref;
+    if (!rd(magic, 4) || std::memcmp(magic, "BAI\1", 4) != 0 || !rd(&n_ref, 4) ||
+        n_ref != (int32_t)R->header.ref_len.size())
+      continue;
+    std::vector<int64_t> beg((size_t)n_ref, -1);
+    bool ok = true;
+    for (int32_t r = 0; r < n_ref && ok; ++r) {
+      int32_t n_bin;
+      if (!rd(&n_bin, 4) || n_bin < 0) { ok = false; break; }
+      int64_t pseudo = -1, lo = -1;
+      for (int32_t i = 0; i < n_bin && ok; ++i) {
+        uint32_t bin;
+        int32_t n_chunk;
+        if (!rd(&bin, 4) || !rd(&n_chunk, 4) || n_chunk < 0) { ok = false; break; }
+        for (int32_t c = 0; c < n_chunk; ++c) {
+          uint64_t cb, ce;
+          if (!rd(&cb, 8) || !rd(&ce, 8)) { ok = false; break; }
+          if (bin == 37450) {
+            if (c == 0) pseudo = (int64_t)cb;
+          } else if (lo < 0 || (int64_t)cb < lo) {
+            lo = (int64_t)cb;
+          }
+        }
+      }
+      int32_t n_intv;
+      if (!ok || !rd(&n_intv, 4) || n_intv < 0 || p + 8ull * (size_t)n_intv > b.size()) { ok = false; break; }
+      p += 8ull * (size_t)n_intv;
+      beg[(size_t)r] = pseudo >= 0 ? pseudo : lo;
+    }
+    if (!ok) continue;
+    R->index_beg = std::move(beg);
+    R->has_index = true;
+    return;
+  }
+}
+
+int reader_open_impl(const char *path, int threads, ganon_bam_reader **out) {
+  auto *R = new ganon_bam_reader();
+  R->threads = std::max(1, std::min(threads, 64));
+  R->fh = std::fopen(path, "rb");
+  if (!R->fh) {
+    delete R;
+    return set_err(std::string("cannot open ") + path);
+  }
+  std::fseek(R->fh, 0, SEEK_END);
+  R->fsize = (int64_t)std::ftell(R->fh);
+  // header: inflate block windows until it is complete
+  std::vector<uint8_t> data;
+  std::vector<std::pair<int64_t, int64_t>> bmap;
+  int64_t coff = 0, p = 0;
+  for (;;) {
+    if (coff >= R->fsize) {
+      ganon_bam_reader_close(R);
+      return set_err("truncated header");
+    }
+    coff = read_blocks(R, coff, data, bmap);
+    if (coff < 0) {
+      ganon_bam_reader_close(R);
+      return -1;
+    }
+    const int hr = parse_header(data.data(), (int64_t)data.size(), &R->header, p);
+    if (hr < 0) {
+      ganon_bam_reader_close(R);
+      return -1;
+    }
+    if (hr > 0) break;
+  }
+  R->data_voff = p == (int64_t)data.size() ? (coff << 16) : voff_at(bmap, p);
+  R->cur_voff = R->data_voff;
+  R->cur_tid = 0;
+  load_index(R, path);
+  *out = R;
+  return 0;
+}
+
+}  // namespace
+
+GANON_HOST_API int ganon_bam_reader_open(const char *path, int threads, ganon_bam_reader **out) {
+  if (!path || !out) return set_err("null argument");
+  *out = nullptr;
+  try {
+    return reader_open_impl(path, threads, out);
+  } catch (const std::bad_alloc &) {
+    return set_err("out of memory reading the BAM header");
+  }
+}
+
+GANON_HOST_API int ganon_bam_reader_set_window(ganon_bam_reader *R, int64_t bytes) {
+  if (!R) return set_err("null argument");
+  R->chunk = std::max<int64_t>(bytes, 1 << 17);   // at least two maximal BGZF blocks
+  return 0;
+}
+
+GANON_HOST_API int ganon_bam_reader_has_index(const ganon_bam_reader *R) { return R && R->has_index ? 1 : 0; }
+
+GANON_HOST_API int ganon_bam_reader_header(ganon_bam_reader *R, ganon_bam_view *v) {
+  if (!R) return set_err("null argument");
+  return ganon_bam_view_get(&R->header, v);
+}
+
+GANON_HOST_API int ganon_bam_reader_contig(ganon_bam_reader *R, int32_t tid, ganon_bam **out) {
+  if (!R || !out) return set_err("null argument");
+  *out = nullptr;
+  if (tid < 0 || tid >= (int32_t)R->header.ref_len.size()) return set_err("tid out of range");
+  try {
+    std::vector<uint8_t> kept;
+    int64_t next_voff = -1;
+    int32_t next_tid = kTidEnd, first_tid = kTidEnd;
+    bool done = false;
+    if (R->has_index) {
+      const int64_t beg = R->index_beg[(size_t)tid];
+      if (beg < 0) {
+        done = true;   // the index lists no record of this sequence
+      } else {
+        if (scan_tid(R, beg, tid, kept, next_voff, next_tid, first_tid) != 0) return -1;
+        done = first_tid == tid;   // a stale index falls back to the forward scan
+        if (!done) kept.clear();
+      }
+    }
+    if (!done) {
+      const bool forward = R->cur_voff >= 0 && tid_order(R->cur_tid) <= tid_order(tid);
+      if (scan_tid(R, forward ? R->cur_voff : R->data_voff, tid, kept, next_voff, next_tid, first_tid) != 0) return -1;
+      R->cur_voff = next_voff;
+      R->cur_tid = next_tid;
+    }
+    auto *bam = new ganon_bam();
+    bam->ref_names = R->header.ref_names;
+    bam->ref_name_off = R->header.ref_name_off;
+    bam->ref_len = R->header.ref_len;
+    if (records_to_columns(kept.data(), 0, (int64_t)kept.size(), bam, R->threads) != 0) {
+      delete bam;
+      return -1;
+    }
+    *out = bam;
+    return 0;
+  } catch (const std::bad_alloc &) {
+    return set_err("out of memory decoding a BAM sequence");
+  }
+}
+
+GANON_HOST_API void ganon_bam_reader_close(ganon_bam_reader *R) {
+  if (!R) return;
+  if (R->fh) std::fclose(R->fh);
+  delete R;
+}
 
 GANON_HOST_API int64_t ganon_fastq_format(int64_t n, const uint8_t *const *seq_buf, const uint8_t *seq_sel,
                                           const int64_t *seq_nib_off, const int32_t *seq_len,

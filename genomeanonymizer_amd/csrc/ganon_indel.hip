@@ -18,7 +18,7 @@
 //                     offset, I/D lanes write a 16-byte observation and a 32-bit sort key
 //                     (pos - span_start, plus the scope segment's parity in bit 31) at
 //                     ballot-compacted slots fixed at upload by a host scan (scope-major);
-//   radix sort        hipcub segmented pairs (key, observation index), one segment per scope
+//   radix sort        rocPRIM segmented pairs (key, observation index), one segment per scope
 //                     with observations, position bits only (GANON_PARAM_INDEL_SORT 1: one
 //                     global sort of 64-bit scope|position keys instead);
 //   k_indel_classify  the first thread of each (scope, pos) run resolves the run — singletons
@@ -29,7 +29,9 @@
 //   k_indel_write     (download) records at atomic slots; results do not depend on slot order
 //                     (a call is (scope, pos, rank); the host sorts the records).
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+#include <rocprim/device/device_segmented_radix_sort.hpp>
 
 #include <algorithm>
 #include <cstring>
@@ -523,20 +525,25 @@ void ind_release(ganon_indels *t) {
 // num_items is the capacity: the filtered count stays on the device, the segments bound the work.
 template <typename KeyT>
 hipError_t sort_pairs(ganon_indels *t, void *temp, size_t &bytes, bool global, hipStream_t st, int *sel) {
-  hipcub::DoubleBuffer<KeyT> K(static_cast<KeyT *>(t->keys[0]), static_cast<KeyT *>(t->keys[1]));
-  hipcub::DoubleBuffer<uint32_t> Vb(t->vals[0], t->vals[1]);
+  rocprim::double_buffer<KeyT> K(static_cast<KeyT *>(t->keys[0]), static_cast<KeyT *>(t->keys[1]));
+  rocprim::double_buffer<uint32_t> Vb(t->vals[0], t->vals[1]);
   hipError_t e;
   if (global)
-    e = hipcub::DeviceRadixSort::SortPairs(temp, bytes, K, Vb, (int)t->n_obs, 0, t->key_bits, st);
+    e = rocprim::radix_sort_pairs(temp, bytes, K, Vb, (unsigned int)t->n_obs, 0u, (unsigned int)t->key_bits, st);
   else
-    e = hipcub::DeviceSegmentedRadixSort::SortPairs(temp, bytes, K, Vb, (int)t->n_obs, t->n_seg, t->seg_off,
-                                                     t->seg_off + 1, 0, t->pos_bits, st);
-  if (sel) *sel = (K.selector == Vb.selector) ? K.selector : -1;
+    e = rocprim::segmented_radix_sort_pairs(temp, bytes, K, Vb, (unsigned int)t->n_obs, (unsigned int)t->n_seg,
+                                            t->seg_off, t->seg_off + 1, 0u, (unsigned int)t->pos_bits, st);
+  if (sel) {
+    const int ks = K.current() == static_cast<KeyT *>(t->keys[0]) ? 0 : 1;
+    const int vs = Vb.current() == t->vals[0] ? 0 : 1;
+    *sel = ks == vs ? ks : -1;
+  }
   return e;
 }
 
 hipError_t scan_counts(ganon_indels *t, void *temp, size_t &bytes, hipStream_t st) {
-  return hipcub::DeviceScan::ExclusiveSum(temp, bytes, t->cnt, t->off, (int)(t->n_list + 1), st);
+  return rocprim::exclusive_scan(temp, bytes, t->cnt, t->off, 0, (size_t)(t->n_list + 1), rocprim::plus<int32_t>(),
+                                 st);
 }
 
 template <typename KeyT>

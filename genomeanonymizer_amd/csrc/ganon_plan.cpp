@@ -89,6 +89,7 @@ class Planner {
   }
 
   void run() {
+    cmode_ = in_->contig_mode != 0;
     name_ids();
     const std::vector<Section> secs = sections();
     for (const Section &w : secs) {
@@ -101,6 +102,10 @@ class Planner {
         stats_.push_back(-1);
         inter_window(w);
       }
+    }
+    if (cmode_) {
+      export_contig();
+      return;
     }
     if (!to_pair_.empty()) pair_unmapped_mates();
     for (int64_t k : written_) to_pair_.erase(k);
@@ -124,6 +129,8 @@ class Planner {
   std::vector<int32_t> stats_;        // 2 per event: kind (0 window, 1 outside, 2 scope), value
   std::vector<int64_t> single_[2];    // (row, scope) pairs
   bool write_single_end_ = false;
+  std::vector<int64_t> left_;         // contig mode: 9 per unwritten pair (include/ganon_host.h)
+  std::vector<int64_t> cand_;         // contig mode: 5 per pair_unmapped_mates candidate
 
  private:
   struct Section {
@@ -136,7 +143,9 @@ class Planner {
   Table tab_[2];
   std::vector<int64_t> nid_[2];       // name id per row
   std::unordered_map<int64_t, PairSlot> to_pair_;
-  uint64_t pair_seq_ = 0;
+  uint64_t pair_seq_ = 0;             // clock: to_pair insertions and placeholder events
+  bool cmode_ = false;
+  std::vector<uint8_t> cross_;        // per name id (contig mode)
   std::unordered_set<int64_t> written_;
   int32_t next_hid_ = 0;
 
@@ -165,6 +174,11 @@ class Planner {
           if (d == 1 && it->second < tumor_ids) ++shared;
         }
       }
+      if (cmode_) {
+        cross_.resize(ids.size(), 0);
+        for (int64_t r = 0; r < t.n; ++r)
+          if (t.tid[r] < 0 || t.mate_tid[r] != t.tid[r]) cross_[(size_t)nid_[d][r]] = 1;
+      }
       if (d == 0) tumor_ids = (int64_t)ids.size();
       else if (shared) {
         // count distinct shared names like the Python set intersection
@@ -184,6 +198,7 @@ class Planner {
     for (int32_t w = 0; w < in_->n_windows; ++w) by_seq[(size_t)in_->win_contig[w]].push_back(w);
     std::vector<Section> out;
     for (int32_t c = 0; c < in_->n_contigs; ++c) {
+      if (in_->contig_mode && c != in_->only_contig) continue;
       const auto &ws = by_seq[(size_t)c];
       if (ws.empty()) {
         out.push_back(Section{c, 0, 0, -1});
@@ -285,6 +300,15 @@ class Planner {
     event_rows_.push_back(i.row);
   }
 
+  bool cross(const Inst &i) const { return cmode_ && cross_[(size_t)nid_[i.ds][(size_t)i.row]]; }
+
+  // contig mode: an operation on a cross name's pairing state, decided by ganon_resolver_contig
+  void placeholder(int32_t kind, int32_t hid, int slot, const Inst &i) {
+    if (pair_seq_ >= (uint64_t)INT32_MAX) raise(GANON_PLAN_E_UNSUPPORTED, "contig plan clock overflow");
+    events_.insert(events_.end(), {kind, hid, i.ds, slot, i.ds, i.scope, (int32_t)pair_seq_++});
+    event_rows_.push_back(i.row);
+  }
+
   void write_pair(const Inst &i0, const Inst &i1, int32_t hid) {
     const int64_t name = nid_[i0.ds][(size_t)i0.row];
     if (!written_.insert(name).second) return;
@@ -311,7 +335,12 @@ class Planner {
   void passthrough(int ds, int64_t row, int32_t hid) {
     if (in_->tables[ds].l_seq[row] == 0)
       raise(GANON_PLAN_E_TYPE, "read '" + tab_[ds].name(row) + "' has no SEQ; the reference cannot upper-case it");
-    PairSlot &p = store_first(Inst{ds, -1, row});
+    const Inst inst{ds, -1, row};
+    if (cross(inst)) {
+      placeholder(5, hid, slot(ds, row), inst);
+      return;
+    }
+    PairSlot &p = store_first(inst);
     if (p.has[0] && p.has[1]) write_pair(p.p[0], p.p[1], hid);
   }
 
@@ -465,10 +494,19 @@ class Planner {
     for (int32_t k : order) {
       const YPair &p = pairs[(size_t)k];
       if (p.has[0] && p.has[1]) {
-        write_pair(p.p[0], p.p[1], hid);
+        if (cross(p.p[0])) {
+          placeholder(3, hid, 0, p.p[0]);
+          placeholder(3, hid, 1, p.p[1]);
+        } else {
+          write_pair(p.p[0], p.p[1], hid);
+        }
         continue;
       }
       const Inst &inst = p.has[0] ? p.p[0] : p.p[1];
+      if (cross(inst)) {
+        placeholder(4, hid, p.has[0] ? 0 : 1, inst);
+        continue;
+      }
       store_first(inst);
       const int64_t name = nid_[inst.ds][(size_t)inst.row];
       auto it = to_pair_.find(name);
@@ -610,6 +648,47 @@ class Planner {
     close_handle(hid);
   }
 
+  // ---- contig mode: what the sample-wide resolution needs from this contig ----
+  void export_contig() {
+    std::vector<std::pair<uint64_t, const PairSlot *>> rest;
+    std::unordered_set<int64_t> pending;
+    for (const auto &kv : to_pair_) {
+      if (written_.count(kv.first)) continue;   // dropped at the sample's end anyway
+      rest.emplace_back(kv.second.seq, &kv.second);
+      pending.insert(kv.first);
+    }
+    std::sort(rest.begin(), rest.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
+    for (const auto &e : rest) {
+      const PairSlot &p = *e.second;
+      left_.push_back((int64_t)p.seq);
+      for (int s = 0; s < 2; ++s) {
+        left_.push_back(p.has[s] ? 1 : 0);
+        left_.push_back(p.has[s] ? p.p[s].ds : 0);
+        left_.push_back(p.has[s] ? p.p[s].scope : 0);
+        left_.push_back(p.has[s] ? p.p[s].row : 0);
+      }
+    }
+    // placed-unmapped records of this contig's windows whose names may still be unpaired at the end
+    std::vector<int64_t> rows;
+    for (int32_t w = 0; w < in_->n_windows; ++w) {
+      if (in_->win_contig[w] != in_->only_contig) continue;
+      for (int ds = 0; ds < 2; ++ds) {
+        try {
+          fetch(ds, in_->win_contig[w], true, in_->win_first[w] - 1, true, in_->win_last[w], rows);
+        } catch (const PlanError &) {
+          cand_.insert(cand_.end(), {w, -1, in_->win_first[w] - 1, -1, 0});   // raises if reached
+          break;
+        }
+        for (int64_t r : rows) {
+          if (!tab_[ds].unmapped(r)) continue;
+          const int64_t nm = nid_[ds][(size_t)r];
+          if (!cross_[(size_t)nm] && !pending.count(nm)) continue;
+          cand_.insert(cand_.end(), {w, ds, r, tab_[ds].mate_idx(r), in_->tables[ds].l_seq[r] == 0 ? 1 : 0});
+        }
+      }
+    }
+  }
+
   // ---- SR:561-600 ----
   void pair_unmapped_mates() {
     const int32_t hid = open_handle();
@@ -656,6 +735,12 @@ GANON_HOST_API int ganon_plan_run(const ganon_plan_input *in, ganon_plan **out) 
         g_err = "read tid out of range";
         return GANON_PLAN_E_ARG;
       }
+  }
+  if (in->contig_mode && (in->only_contig < 0 || in->only_contig >= in->n_contigs ||
+                          (in->tables[0].n > 0 && !in->tables[0].mate_tid) ||
+                          (in->tables[1].n > 0 && !in->tables[1].mate_tid))) {
+    g_err = "contig mode: bad contig or missing mate_tid";
+    return GANON_PLAN_E_ARG;
   }
   for (int32_t w = 0; w < in->n_windows; ++w)
     if (in->win_contig[w] < 0 || in->win_contig[w] >= in->n_contigs) {
@@ -725,6 +810,10 @@ GANON_HOST_API int ganon_plan_view_get(const ganon_plan *pl, ganon_plan_view *v)
     v->single[d] = p.single_[d].data();
   }
   v->write_single_end = p.write_single_end_ ? 1 : 0;
+  v->n_left = (int64_t)p.left_.size() / 9;
+  v->left = p.left_.data();
+  v->n_cand = (int64_t)p.cand_.size() / 5;
+  v->cand = p.cand_.data();
   return GANON_PLAN_OK;
 }
 
@@ -735,6 +824,194 @@ GANON_HOST_API void ganon_plan_free(ganon_plan *pl) {
 }
 
 GANON_HOST_API const char *ganon_plan_last_error(void) { return g_err.c_str(); }
+
+// ---- cross-contig resolution (contig mode) -------------------------------------------------------
+// The sample-wide pairing state of the reference (to_pair_anonymized_reads, written_read_ids) for the
+// names the contig plans could not decide alone; see include/ganon_host.h.
+namespace {
+
+struct RInst {
+  int64_t job, ds, scope, row;
+};
+
+struct RSlot {
+  RInst p[2];
+  bool has[2] = {false, false};
+  int64_t seq = 0;   // (job << 32) | clock of the last insertion (dict order)
+};
+
+}  // namespace
+
+struct ganon_resolver {
+  std::unordered_map<std::string, RSlot> to_pair;
+  std::unordered_set<std::string> written;
+
+  RSlot &store_first(const std::string &name, int slot, const RInst &i, int64_t seq) {
+    auto it = to_pair.find(name);
+    if (it == to_pair.end()) {
+      it = to_pair.emplace(name, RSlot{}).first;
+      it->second.seq = seq;
+    }
+    RSlot &p = it->second;
+    if (!p.has[slot]) {
+      p.p[slot] = i;
+      p.has[slot] = true;
+    }
+    return p;
+  }
+  // write_pair (SR:134-165): both records to the first instance's dataset files, once per name
+  int write_pair(const std::string &name, const RInst &a, const RInst &b, int64_t *w) {
+    if (!written.insert(name).second) return 0;
+    const RInst *ab[2] = {&a, &b};
+    for (int s = 0; s < 2; ++s) {
+      int64_t *o = w + 6 * s;
+      o[0] = a.ds;
+      o[1] = s;
+      o[2] = ab[s]->job;
+      o[3] = ab[s]->ds;
+      o[4] = ab[s]->scope;
+      o[5] = ab[s]->row;
+    }
+    return 2;
+  }
+};
+
+GANON_HOST_API int ganon_resolver_create(ganon_resolver **out) {
+  if (!out) return GANON_PLAN_E_ARG;
+  try {
+    *out = new ganon_resolver();
+  } catch (const std::bad_alloc &) {
+    return GANON_PLAN_E_NOMEM;
+  }
+  return GANON_PLAN_OK;
+}
+
+GANON_HOST_API void ganon_resolver_free(ganon_resolver *r) { delete r; }
+
+GANON_HOST_API int ganon_resolver_contig(ganon_resolver *r, int32_t job, int64_t n_ops, const int32_t *ops,
+                                         const int64_t *op_rows, const char *op_names, const int64_t *op_name_off,
+                                         const int32_t *op_name_len, int64_t n_left, const int64_t *left,
+                                         const char *left_names, const int64_t *left_name_off,
+                                         const int32_t *left_name_len, int32_t *out_n, int64_t *out_w) {
+  if (!r || n_ops < 0 || n_left < 0 || (n_ops > 0 && (!ops || !op_rows || !op_names || !op_name_off ||
+                                                       !op_name_len || !out_n || !out_w)) ||
+      (n_left > 0 && (!left || !left_names || !left_name_off || !left_name_len))) {
+    g_err = "resolver: bad argument";
+    return GANON_PLAN_E_ARG;
+  }
+  try {
+    const int64_t base = (int64_t)job << 32;
+    for (int64_t i = 0; i < n_ops; ++i) {
+      const int32_t *e = ops + 7 * i;
+      const std::string name(op_names + op_name_off[i], (size_t)op_name_len[i]);
+      const RInst inst{job, e[4], e[5], op_rows[i]};
+      out_n[i] = 0;
+      if (e[0] == 3) {   // a complete pair in one scope: this op (slot 0) and the next (slot 1)
+        if (i + 1 >= n_ops || ops[7 * (i + 1)] != 3) {
+          g_err = "resolver: unpaired pair event";
+          return GANON_PLAN_E_ARG;
+        }
+        const RInst other{job, ops[7 * (i + 1) + 4], ops[7 * (i + 1) + 5], op_rows[i + 1]};
+        out_n[i] = r->write_pair(name, inst, other, out_w + 12 * i);
+        out_n[i + 1] = 0;
+        ++i;
+        continue;
+      }
+      if (e[0] != 4 && e[0] != 5) {
+        g_err = "resolver: not a placeholder event";
+        return GANON_PLAN_E_ARG;
+      }
+      RSlot &p = r->store_first(name, e[3], inst, base | (int64_t)(uint32_t)e[6]);
+      if (p.has[0] && p.has[1]) {
+        const RInst a = p.p[0], b = p.p[1];
+        out_n[i] = r->write_pair(name, a, b, out_w + 12 * i);
+        if (e[0] == 4) r->to_pair.erase(name);   // anonymize_window pops a written pair (SR:360)
+      }
+    }
+    for (int64_t k = 0; k < n_left; ++k) {
+      const int64_t *l = left + 9 * k;
+      const std::string name(left_names + left_name_off[k], (size_t)left_name_len[k]);
+      for (int s = 0; s < 2; ++s)
+        if (l[1 + 4 * s]) r->store_first(name, s, RInst{job, l[2 + 4 * s], l[3 + 4 * s], l[4 + 4 * s]}, base | l[0]);
+    }
+  } catch (const std::bad_alloc &) {
+    g_err = "out of memory";
+    return GANON_PLAN_E_NOMEM;
+  }
+  return GANON_PLAN_OK;
+}
+
+GANON_HOST_API int64_t ganon_resolver_pending(ganon_resolver *r, int64_t *out, int64_t cap) {
+  if (!r) return GANON_PLAN_E_ARG;
+  int64_t n = 0;
+  for (const auto &kv : r->to_pair)
+    for (int s = 0; s < 2; ++s)
+      if (kv.second.has[s]) {
+        if (out && n < cap) {
+          const RInst &i = kv.second.p[s];
+          int64_t *o = out + 4 * n;
+          o[0] = i.job;
+          o[1] = i.ds;
+          o[2] = i.scope;
+          o[3] = i.row;
+        }
+        ++n;
+      }
+  return n;
+}
+
+GANON_HOST_API int ganon_resolver_finish(ganon_resolver *r, int64_t n_cand, const int64_t *cand, const char *names,
+                                         const int64_t *name_off, const int32_t *name_len, int64_t *tail,
+                                         int64_t *n_tail, int64_t *single0, int64_t *single1, int64_t *n_single,
+                                         int32_t *write_single_end) {
+  if (!r || n_cand < 0 || !n_tail || !n_single || !write_single_end ||
+      (n_cand > 0 && (!cand || !names || !name_off || !name_len || !tail))) {
+    g_err = "resolver: bad argument";
+    return GANON_PLAN_E_ARG;
+  }
+  *n_tail = 0;
+  // pair_unmapped_mates (SR:561-600) runs only when something is left to pair (SR:752)
+  if (!r->to_pair.empty()) {
+    for (int64_t k = 0; k < n_cand; ++k) {
+      const int64_t *c = cand + 7 * k;
+      if (c[2] < 0) {   // this window's fetch(first - 1, last) raises (pysam region check)
+        g_err = "start out of range (" + std::to_string(c[3]) + ")";
+        return GANON_PLAN_E_VALUE;
+      }
+      const std::string name(names + name_off[k], (size_t)name_len[k]);
+      if (!r->to_pair.count(name)) continue;
+      if (c[5]) {
+        g_err = "read '" + name + "' has no SEQ; the reference cannot upper-case it";
+        return GANON_PLAN_E_TYPE;
+      }
+      if (c[4] < 0) {
+        g_err = "read '" + name + "' has neither the READ1 nor the READ2 flag; the reference cannot store it (SURVEY Q8)";
+        return GANON_PLAN_E_TYPE;
+      }
+      RSlot &p = r->store_first(name, (int)c[4], RInst{c[0], c[2], -1, c[3]}, INT64_MAX);
+      if (p.has[0] && p.has[1]) {
+        const RInst a = p.p[0], b = p.p[1];
+        *n_tail += r->write_pair(name, a, b, tail + 6 * *n_tail);
+      }
+    }
+  }
+  for (const std::string &k : r->written) r->to_pair.erase(k);
+  std::vector<std::pair<int64_t, const RSlot *>> rest;
+  for (const auto &kv : r->to_pair) rest.emplace_back(kv.second.seq, &kv.second);
+  std::stable_sort(rest.begin(), rest.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
+  n_single[0] = n_single[1] = 0;
+  for (const auto &e : rest) {
+    const RInst &i = e.second->has[0] ? e.second->p[0] : e.second->p[1];
+    int64_t *dst = (i.ds == 0 ? single0 : single1) + 4 * n_single[i.ds];
+    dst[0] = i.job;
+    dst[1] = i.ds;
+    dst[2] = i.scope;
+    dst[3] = i.row;
+    ++n_single[i.ds];
+  }
+  *write_single_end = r->to_pair.empty() ? 0 : 1;
+  return GANON_PLAN_OK;
+}
 
 // ---- I/O replay (writer.py AppendHandle / replay_io) --------------------------------------------
 // Every reference function that writes opens its own append-mode text handles on the four FASTQ

@@ -8,7 +8,8 @@ Outputs next to the inputs: re.sub('.bam|.sam|.cram', '.anonymized', path) + .1/
 (+ .single_end.fastq), and {normal_bam}.statistics.txt with --record_statistics.
 
 Multi-GPU: launch under ``torchrun --nproc-per-node N`` (or set WORLD_SIZE/RANK/LOCAL_RANK):
-contigs are sharded over the ranks (distributed.py); rank 0 writes the files.
+contigs are sharded round-robin over the ranks; each rank decodes, masks and writes its own
+contigs at their offsets of the shared output files (distributed.py, stream.py).
 """
 from __future__ import annotations
 
@@ -95,9 +96,8 @@ def run_anonymizer(argv=None) -> None:
         fa = FastaRef(config.reference)
         for vcf, (t, n), (to, no) in zip(vcfs, samples, outputs):
             windows = get_windows(read_vcf(vcf), fa.index)
-            work = os.path.join(os.path.dirname(os.path.abspath(no)), ".ganon_shards")
             tot = anonymize_genome_sharded(windows, t, n, config.reference, to, no, bool(config.record_statistics),
-                                           rank, world, work, anonymizer, dist, threads=max(1, config.cpu))
+                                           anonymizer, dist, threads=max(1, config.cpu))
             if rank == 0:
                 logging.info("sample %s/%s totals %s", t, n, tot)
         dist.destroy_process_group()

@@ -42,48 +42,47 @@ def _blob(ptr, n, dtype=np.uint8):
 class ReadTable:
     """All records of one BAM file, in file order."""
 
-    def __init__(self, path: str, threads: int = 8):
+    def __init__(self, path: str, threads: int = 8, handle=None):
+        """Decode the whole file, or take the records of an open ``ganon_bam`` handle (one
+        reference sequence from ``BamReader.contig``); the handle is released here."""
         lib = native.host_lib()
-        h = C.c_void_p()
-        rc = lib.ganon_bam_open(os.fsencode(path), int(threads), C.byref(h))
-        if rc != 0:
-            raise native.GanonError(f"cannot decode {path}: {lib.ganon_host_last_error().decode()}")
+        if handle is None:
+            h = C.c_void_p()
+            rc = lib.ganon_bam_open(os.fsencode(path), int(threads), C.byref(h))
+            if rc != 0:
+                raise native.GanonError(f"cannot decode {path}: {lib.ganon_host_last_error().decode()}")
+        else:
+            h = handle
         try:
             v = native.BamView()
             lib.ganon_bam_view_get(h, C.byref(v))
-            n = int(v.n_records)
-            self.path = path
-            self.n = n
-            names_blob = _blob(v.names, int(v.names_bytes))
-            self.ref_names: List[str] = []
-            ref_name_off = _arr(v.ref_name_off, v.n_ref, np.int64)
-            raw = int(v.ref_names)
-            for o in ref_name_off:
-                self.ref_names.append(C.string_at(raw + int(o)).decode())
-            self.ref_lens = _arr(v.ref_len, v.n_ref, np.int64)
-            self.tid = _arr(v.tid, n, np.int32)
-            self.pos = _arr(v.pos, n, np.int32)
-            self.end = _arr(v.end, n, np.int32)
-            self.flag = _arr(v.flag, n, np.int32)
-            self.mapq = _arr(v.mapq, n, np.int32)
-            self.l_seq = _arr(v.l_seq, n, np.int32)
-            self.n_cigar = _arr(v.n_cigar, n, np.int32)
-            self.mate_tid = _arr(v.mate_tid, n, np.int32)
-            self.mate_pos = _arr(v.mate_pos, n, np.int32)
-            self.name_off = _arr(v.name_off, n, np.int64)
-            self.name_len = _arr(v.name_len, n, np.int32)
-            self.cig_off = _arr(v.cig_off, n, np.int64)
-            self.seq_off = _arr(v.seq_off, n, np.int64)
-            self.qual_off = _arr(v.qual_off, n, np.int64)
-            self.aux_off = _arr(v.aux_off, n, np.int64)
-            self.aux_len = _arr(v.aux_len, n, np.int32)
-            self.names_blob = names_blob
-            self.cigar = _blob(v.cigar, int(v.cigar_ops), np.uint32).copy()
-            self.seq = _blob(v.seq, int(v.seq_bytes)).copy()
-            self.qual = _blob(v.qual, int(v.qual_bytes)).copy()
-            self.aux = _blob(v.aux, int(v.aux_bytes)).copy()
+            self._load(path, v)
         finally:
             lib.ganon_bam_close(h)
+        self._finish()
+
+    def _load(self, path: str, v) -> None:
+        n = int(v.n_records)
+        self.path = path
+        self.n = n
+        self.ref_names: List[str] = []
+        ref_name_off = _arr(v.ref_name_off, v.n_ref, np.int64)
+        raw = int(v.ref_names) if v.n_ref else 0
+        for o in ref_name_off:
+            self.ref_names.append(C.string_at(raw + int(o)).decode())
+        self.ref_lens = _arr(v.ref_len, v.n_ref, np.int64)
+        for f in ("tid", "pos", "end", "flag", "mapq", "l_seq", "n_cigar", "mate_tid", "mate_pos", "name_len",
+                  "aux_len"):
+            setattr(self, f, _arr(getattr(v, f), n, np.int32))
+        for f in ("name_off", "cig_off", "seq_off", "qual_off", "aux_off"):
+            setattr(self, f, _arr(getattr(v, f), n, np.int64))
+        self.names_blob = _blob(v.names, int(v.names_bytes))
+        self.cigar = _blob(v.cigar, int(v.cigar_ops), np.uint32).copy()
+        self.seq = _blob(v.seq, int(v.seq_bytes)).copy()
+        self.qual = _blob(v.qual, int(v.qual_bytes)).copy()
+        self.aux = _blob(v.aux, int(v.aux_bytes)).copy()
+
+    def _finish(self) -> None:
         self._names: Optional[List[str]] = None
         self.is_unmapped = (self.flag & FLAG_UNMAP) != 0
         self.is_reverse = (self.flag & FLAG_REVERSE) != 0
@@ -169,3 +168,75 @@ class ReadTable:
     def cigar_of(self, i: int) -> np.ndarray:
         o = int(self.cig_off[i])
         return self.cigar[o:o + int(self.n_cigar[i])]
+
+
+class BamReader:
+    """One BAM file read a reference sequence at a time (``ganon_bam_reader``, include/
+    ganon_host.h): the bounded-memory counterpart of ``ReadTable(path)``. ``contig(tid)`` returns a
+    ReadTable of that sequence's records only (file order, full reference list); the reader seeks
+    through ``<bam>.bai`` when present, else streams forward."""
+
+    def __init__(self, path: str, threads: int = 8, window: int = 0):
+        lib = native.host_lib()
+        h = C.c_void_p()
+        rc = lib.ganon_bam_reader_open(os.fsencode(path), int(threads), C.byref(h))
+        if rc != 0:
+            raise native.GanonError(f"cannot open {path}: {lib.ganon_host_last_error().decode()}")
+        self._h = h
+        self.path = path
+        if window:
+            lib.ganon_bam_reader_set_window(h, int(window))
+        v = native.BamView()
+        lib.ganon_bam_reader_header(h, C.byref(v))
+        off = _arr(v.ref_name_off, v.n_ref, np.int64)
+        raw = int(v.ref_names) if v.n_ref else 0
+        self.ref_names: List[str] = [C.string_at(raw + int(o)).decode() for o in off]
+        self.ref_lens = _arr(v.ref_len, v.n_ref, np.int64)
+        self.has_index = bool(lib.ganon_bam_reader_has_index(h))
+
+    def tid_of(self, contig: str) -> int:
+        try:
+            return self.ref_names.index(contig)
+        except ValueError:
+            return -1
+
+    def contig(self, tid: int) -> ReadTable:
+        """The records of BAM sequence ``tid`` (an empty table for tid < 0)."""
+        if tid < 0:
+            return self.empty()
+        lib = native.host_lib()
+        h = C.c_void_p()
+        rc = lib.ganon_bam_reader_contig(self._h, int(tid), C.byref(h))
+        if rc != 0:
+            raise native.GanonError(f"cannot decode {self.path} sequence {tid}: "
+                                    f"{lib.ganon_host_last_error().decode()}")
+        return ReadTable(self.path, handle=h)
+
+    def empty(self) -> ReadTable:
+        """A table with no records and this file's reference list."""
+        t = ReadTable.__new__(ReadTable)
+        t.path, t.n = self.path, 0
+        t.ref_names, t.ref_lens = list(self.ref_names), self.ref_lens.copy()
+        for f in ("tid", "pos", "end", "flag", "mapq", "l_seq", "n_cigar", "mate_tid", "mate_pos", "name_len",
+                  "aux_len"):
+            setattr(t, f, np.zeros(0, np.int32))
+        for f in ("name_off", "cig_off", "seq_off", "qual_off", "aux_off"):
+            setattr(t, f, np.zeros(0, np.int64))
+        t.names_blob = np.zeros(0, np.uint8)
+        t.cigar = np.zeros(0, np.uint32)
+        t.seq = np.zeros(0, np.uint8)
+        t.qual = np.zeros(0, np.uint8)
+        t.aux = np.zeros(0, np.uint8)
+        t._finish()
+        return t
+
+    def close(self) -> None:
+        if self._h:
+            native.host_lib().ganon_bam_reader_close(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -199,6 +199,10 @@ EXPORTED_HOST_SYMBOLS = (
     "ganon_bam_open", "ganon_bam_view_get", "ganon_bam_error", "ganon_bam_close",
     "ganon_host_last_error", "ganon_fastq_format", "ganon_pack_nt16",
     "ganon_plan_run", "ganon_plan_view_get", "ganon_plan_free", "ganon_plan_last_error", "ganon_io_replay",
+    "ganon_bam_reader_open", "ganon_bam_reader_set_window", "ganon_bam_reader_has_index", "ganon_bam_reader_header",
+    "ganon_bam_reader_contig", "ganon_bam_reader_close",
+    "ganon_resolver_create", "ganon_resolver_free", "ganon_resolver_contig", "ganon_resolver_pending",
+    "ganon_resolver_finish",
 )
 
 
@@ -219,6 +223,16 @@ class HipMasker:
                              "no usable gfx950 device (there is no CPU fallback)")
         self._h = h
         self.device = device
+        self._ref = None            # (the host array, its DeviceRef): the genome stays resident
+
+    def resident_reference(self, ref_nt16: np.ndarray) -> "DeviceRef":
+        """The packed genome in HBM, uploaded once per array object (stream.py masks one contig
+        batch after another against the same genome)."""
+        if self._ref is None or self._ref[0] is not ref_nt16:
+            if self._ref is not None:
+                self._ref[1].free()
+            self._ref = (ref_nt16, self.upload_reference(ref_nt16))
+        return self._ref[1]
 
     def _check(self, rc: int, what: str) -> None:
         if rc != 0:
@@ -226,6 +240,9 @@ class HipMasker:
             raise GanonError(f"{what} failed ({rc}): {msg}")
 
     def close(self) -> None:
+        if getattr(self, "_ref", None) is not None:
+            self._ref[1].free()
+            self._ref = None
         if getattr(self, "_h", None):
             self._lib.ganon_ctx_destroy(self._h)
             self._h = None
@@ -255,7 +272,7 @@ class HipMasker:
         """Synchronous one-shot: returns (seq_out, scope_calls, scope_bases, totals), plus the
         germline indel records (``INDEL_REC``, sorted) when ``indels``."""
         if indels:
-            db = self.upload(arrays)
+            db = self.upload(arrays, ref=self.resident_reference(arrays["ref_nt16"]))
             try:
                 t = db.indel_tally(arrays)
                 try:
@@ -584,13 +601,14 @@ class PlanTable(C.Structure):
     """Mirror of ``ganon_plan_table`` (include/ganon_host.h)."""
     _fields_ = [("n", C.c_int64), ("tid", _i32p), ("pos", _i32p), ("end", _i32p), ("flag", _i32p),
                 ("l_seq", _i32p), ("n_cigar", _i32p), ("names", _p), ("name_off", _i64p), ("name_len", _i32p),
-                ("n_ref", C.c_int32), ("ref_len", _i64p), ("tid_of_contig", _i32p)]
+                ("n_ref", C.c_int32), ("ref_len", _i64p), ("tid_of_contig", _i32p), ("mate_tid", _i32p)]
 
 
 class PlanInput(C.Structure):
     _fields_ = [("tables", PlanTable * 2), ("n_contigs", C.c_int32), ("contig_len", _i64p),
                 ("contig_names", _p), ("contig_name_off", _i64p), ("n_windows", C.c_int32),
-                ("win_contig", _i32p), ("win_first", _i64p), ("win_last", _i64p)]
+                ("win_contig", _i32p), ("win_first", _i64p), ("win_last", _i64p),
+                ("contig_mode", C.c_int32), ("only_contig", C.c_int32)]
 
 
 class PlanView(C.Structure):
@@ -599,7 +617,8 @@ class PlanView(C.Structure):
                 ("scope_span_end", _i64p), ("scope_t_off", _i64p), ("scope_n_off", _i64p),
                 ("t_rows", _i64p), ("n_rows", _i64p), ("n_events", C.c_int64), ("events", _i32p),
                 ("event_rows", _i64p), ("n_stats", C.c_int64), ("stats", _i32p),
-                ("n_single", C.c_int64 * 2), ("single", _i64p * 2), ("write_single_end", C.c_int32)]
+                ("n_single", C.c_int64 * 2), ("single", _i64p * 2), ("write_single_end", C.c_int32),
+                ("n_left", C.c_int64), ("left", _i64p), ("n_cand", C.c_int64), ("cand", _i64p)]
 
 
 PLAN_E_VALUE, PLAN_E_TYPE, PLAN_E_UNSUPPORTED = -10, -11, -12
@@ -611,10 +630,11 @@ def _np_copy(ptr, n: int, dtype) -> np.ndarray:
     return np.ctypeslib.as_array(ptr, shape=(int(n),)).astype(dtype, copy=True)
 
 
-def plan_sample(tables, contig_names, contig_lens, win_contig, win_first, win_last) -> dict:
+def plan_sample(tables, contig_names, contig_lens, win_contig, win_first, win_last, only_contig=None) -> dict:
     """``ganon_plan_run`` over two ReadTables (io/bam.py) and the variant windows. Returns the
     plan's column arrays (copies); raises ValueError / TypeError / planner.UnsupportedInput as
-    the reference's own code would (message from the library)."""
+    the reference's own code would (message from the library). ``only_contig``: contig mode for
+    that FASTA contig (tables holding its records only), see include/ganon_host.h."""
     lib = host_lib()
     keep = []
 
@@ -638,6 +658,7 @@ def plan_sample(tables, contig_names, contig_lens, win_contig, win_first, win_la
         pt.ref_len = arr(t.ref_lens, np.int64)
         idx = {nm: i for i, nm in enumerate(t.ref_names)}
         pt.tid_of_contig = arr([idx.get(c, -1) for c in contig_names], np.int32)
+        pt.mate_tid = arr(t.mate_tid, np.int32)
     inp.n_contigs = len(contig_names)
     inp.contig_len = arr(contig_lens, np.int64)
     blob = b"".join(c.encode() + b"\0" for c in contig_names) or b"\0"
@@ -650,6 +671,8 @@ def plan_sample(tables, contig_names, contig_lens, win_contig, win_first, win_la
     inp.win_contig = arr(win_contig, np.int32)
     inp.win_first = arr(win_first, np.int64)
     inp.win_last = arr(win_last, np.int64)
+    inp.contig_mode = 0 if only_contig is None else 1
+    inp.only_contig = -1 if only_contig is None else int(only_contig)
     h = _p()
     rc = lib.ganon_plan_run(C.byref(inp), C.byref(h))
     if rc != 0:
@@ -684,9 +707,97 @@ def plan_sample(tables, contig_names, contig_lens, win_contig, win_first, win_la
         out["stats"] = _np_copy(v.stats, 2 * int(v.n_stats), np.int32).reshape(-1, 2)
         out["single"] = [_np_copy(v.single[d], 2 * int(v.n_single[d]), np.int64).reshape(-1, 2) for d in (0, 1)]
         out["write_single_end"] = bool(v.write_single_end)
+        out["left"] = _np_copy(v.left, 9 * int(v.n_left), np.int64).reshape(-1, 9)
+        out["cand"] = _np_copy(v.cand, 5 * int(v.n_cand), np.int64).reshape(-1, 5)
     finally:
         lib.ganon_plan_free(h)
     return out
+
+
+def _names_args(names: list, keep: list):
+    """(blob, offsets, lengths) ctypes arguments of a list of bytes names."""
+    lens = np.array([len(x) for x in names], np.int32)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.int64)]).astype(np.int64) if len(names) else np.zeros(1, np.int64)
+    blob = np.frombuffer(b"".join(names) + b"\0", np.uint8).copy()
+    lens = lens if len(names) else np.zeros(1, np.int32)
+    keep += [blob, offs, lens]
+    return blob.ctypes.data_as(_p), offs.ctypes.data_as(_i64p), lens.ctypes.data_as(_i32p)
+
+
+class Resolver:
+    """``ganon_resolver_*`` (include/ganon_host.h): the sample-wide pairing state across contig
+    plans. Writes come back as int64 rows (file dataset, file slot, job, dataset, scope, row)."""
+
+    def __init__(self):
+        self._lib = host_lib()
+        h = _p()
+        if self._lib.ganon_resolver_create(C.byref(h)) != 0:
+            raise GanonError("ganon_resolver_create failed")
+        self._h = h
+
+    def _err(self, rc: int):
+        msg = self._lib.ganon_plan_last_error().decode(errors="replace")
+        if rc == PLAN_E_VALUE:
+            raise ValueError(msg)
+        if rc == PLAN_E_TYPE:
+            raise TypeError(msg)
+        raise GanonError(f"resolver failed ({rc}): {msg}")
+
+    def contig(self, job: int, ops: np.ndarray, op_rows: np.ndarray, op_names: list, left: np.ndarray,
+               left_names: list):
+        """Returns (n_writes per op, writes [n_ops, 2, 6])."""
+        keep = []
+        ops = np.ascontiguousarray(ops, np.int32).reshape(-1, 7)
+        rows = np.ascontiguousarray(op_rows, np.int64)
+        left = np.ascontiguousarray(left, np.int64).reshape(-1, 9)
+        n = len(ops)
+        out_n = np.zeros(max(n, 1), np.int32)
+        out_w = np.zeros((max(n, 1), 2, 6), np.int64)
+        on, oo, ol = _names_args(op_names, keep)
+        ln, lo, ll = _names_args(left_names, keep)
+        rc = self._lib.ganon_resolver_contig(self._h, int(job), n, ops.ctypes.data_as(_i32p), rows.ctypes.data_as(_i64p),
+                                             on, oo, ol, len(left), left.ctypes.data_as(_i64p), ln, lo, ll,
+                                             out_n.ctypes.data_as(_i32p), out_w.ctypes.data_as(_i64p))
+        if rc != 0:
+            self._err(rc)
+        return out_n[:n], out_w[:n]
+
+    def pending(self) -> np.ndarray:
+        k = self._lib.ganon_resolver_pending(self._h, None, 0)
+        out = np.zeros((max(k, 1), 4), np.int64)
+        self._lib.ganon_resolver_pending(self._h, out.ctypes.data_as(_i64p), k)
+        return out[:k]
+
+    def finish(self, cand: np.ndarray, names: list):
+        """Returns (tail writes [n, 6], single ends per dataset [m, 4] (job, ds, scope, row),
+        write_single_end)."""
+        keep = []
+        cand = np.ascontiguousarray(cand, np.int64).reshape(-1, 7)
+        n_pend = self._lib.ganon_resolver_pending(self._h, None, 0)
+        tail = np.zeros((max(2 * len(cand), 1), 6), np.int64)
+        s0 = np.zeros((max(n_pend, 1), 4), np.int64)
+        s1 = np.zeros((max(n_pend, 1), 4), np.int64)
+        n_tail = C.c_int64(0)
+        n_single = np.zeros(2, np.int64)
+        wse = C.c_int32(0)
+        nb, no, nl = _names_args(names, keep)
+        rc = self._lib.ganon_resolver_finish(self._h, len(cand), cand.ctypes.data_as(_i64p), nb, no, nl,
+                                             tail.ctypes.data_as(_i64p), C.byref(n_tail), s0.ctypes.data_as(_i64p),
+                                             s1.ctypes.data_as(_i64p), n_single.ctypes.data_as(_i64p), C.byref(wse))
+        if rc != 0:
+            self._err(rc)
+        return tail[:n_tail.value], [s0[:n_single[0]], s1[:n_single[1]]], bool(wse.value)
+
+    def close(self):
+        if self._h:
+            self._lib.ganon_resolver_free(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def io_replay(events: np.ndarray, rec_len: np.ndarray, block: int):
@@ -715,6 +826,12 @@ def host_lib():
     lib.ganon_bam_open.argtypes = [C.c_char_p, C.c_int, C.POINTER(_p)]
     lib.ganon_bam_view_get.argtypes = [_p, C.POINTER(BamView)]
     lib.ganon_bam_close.argtypes = [_p]
+    lib.ganon_bam_reader_open.argtypes = [C.c_char_p, C.c_int, C.POINTER(_p)]
+    lib.ganon_bam_reader_has_index.argtypes = [_p]
+    lib.ganon_bam_reader_set_window.argtypes = [_p, C.c_int64]
+    lib.ganon_bam_reader_header.argtypes = [_p, C.POINTER(BamView)]
+    lib.ganon_bam_reader_contig.argtypes = [_p, C.c_int32, C.POINTER(_p)]
+    lib.ganon_bam_reader_close.argtypes = [_p]
     lib.ganon_host_last_error.restype = C.c_char_p
     lib.ganon_fastq_format.restype = C.c_int64
     lib.ganon_fastq_format.argtypes = [C.c_int64, C.POINTER(_u8p), _u8p, _i64p, _i32p, _u8p, C.POINTER(_u8p),
@@ -726,6 +843,14 @@ def host_lib():
     lib.ganon_plan_free.argtypes = [_p]
     lib.ganon_plan_last_error.restype = C.c_char_p
     lib.ganon_io_replay.argtypes = [C.c_int64, _i32p, _i64p, C.c_int64, _i64p, _i64p]
+    lib.ganon_resolver_create.argtypes = [C.POINTER(_p)]
+    lib.ganon_resolver_free.argtypes = [_p]
+    lib.ganon_resolver_contig.argtypes = [_p, C.c_int32, C.c_int64, _i32p, _i64p, _p, _i64p, _i32p, C.c_int64, _i64p,
+                                          _p, _i64p, _i32p, _i32p, _i64p]
+    lib.ganon_resolver_pending.argtypes = [_p, _i64p, C.c_int64]
+    lib.ganon_resolver_pending.restype = C.c_int64
+    lib.ganon_resolver_finish.argtypes = [_p, C.c_int64, _i64p, _p, _i64p, _i32p, _i64p, _i64p, _i64p, _i64p,
+                                          _i64p, _i32p]
     lib.ganon_io_replay.restype = C.c_int64
     _host = lib
     return lib

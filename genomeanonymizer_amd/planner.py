@@ -567,6 +567,7 @@ class NativeSamplePlanner(SamplePlanner):
     SamplePlanner (pure Python) is the second implementation the tests compare it with."""
 
     native = True
+    only_contig: Optional[int] = None   # contig mode (ContigPlanner)
 
     def run(self) -> Plan:
         from . import native
@@ -574,7 +575,9 @@ class NativeSamplePlanner(SamplePlanner):
         cidx = {c: i for i, c in enumerate(refs)}
         w = self.windows
         res = native.plan_sample(self.tables, refs, list(self.fasta.lengths),
-                                 [cidx[x.sequence] for x in w], [x.first for x in w], [x.last for x in w])
+                                 [cidx[x.sequence] for x in w], [x.first for x in w], [x.last for x in w],
+                                 only_contig=self.only_contig)
+        self.contig_exports = {"left": res["left"], "cand": res["cand"]}
         T, N = self.tables
         t_rows, n_rows = res["t_rows"], res["n_rows"]
         to, no = res["scope_t_off"], res["scope_n_off"]
@@ -597,6 +600,18 @@ class NativeSamplePlanner(SamplePlanner):
         single = {d: [(d, r, s) for r, s in res["single"][d].tolist()] for d in (0, 1)}
         return Plan(self.scopes, None, single, self.stats_events, res["write_single_end"],
                     events=res["events"], event_rows=res["event_rows"])
+
+
+class ContigPlanner(NativeSamplePlanner):
+    """Contig mode of the native planner (include/ganon_host.h ``contig_mode``): plans one FASTA
+    contig from tables holding only that contig's records. Pairing operations on names with a
+    record on another sequence become placeholder events (kinds 3/4/5) for stream.py's resolver;
+    ``contig_exports`` holds the contig's unwritten pairs and pair_unmapped_mates candidates."""
+
+    def __init__(self, tumor: ReadTable, normal: ReadTable, fasta: FastaRef, windows: Sequence[Window],
+                 contig_index: int):
+        self.only_contig = int(contig_index)
+        super().__init__(tumor, normal, fasta, windows)
 
 
 def make_planner(tumor: ReadTable, normal: ReadTable, fasta: FastaRef, windows: Sequence[Window]) -> SamplePlanner:

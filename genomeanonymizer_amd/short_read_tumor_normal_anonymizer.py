@@ -6,13 +6,15 @@ Mirrors the reference module of the same name (short_read_tumor_normal_anonymize
 arguments and output files:
   {tumor/normal prefix}.1.fastq / .2.fastq, .single_end.fastq when mates stay unpaired,
   {normal_bam}.statistics.txt with --record_statistics.
-Per sample the host plans all scopes (planner.py), the GPU masks them in one batch
-(anonymizer_methods.py -> libganon_hip.so) and the host writes the records in the
-reference's order (writer.py).
+By default a sample streams contig by contig with bounded memory (stream.py: per-contig decode,
+plan, one device batch, cross-contig pairing resolution, output at the contig's file offsets);
+GANON_WHOLE_SAMPLE=1 selects the whole-sample path below (one plan and one device batch for the
+sample), kept as the second implementation the tests compare against.
 """
 from __future__ import annotations
 
 import logging
+import os
 import re
 import time
 from typing import Dict, List, Sequence, Tuple
@@ -39,9 +41,19 @@ def get_ref_idxs(fasta: FastaRef) -> Dict[str, int]:
 def anonymize_genome(windows_in_sample: List[Window], tumor_bam_file: str, normal_bam_file: str,
                      ref_genome_file: str, anonymizer: CompleteGermlineAnonymizer, tumor_output_fastq: str,
                      normal_output_fastq: str, record_statistics: bool, available_threads: int = 8,
-                     fasta: FastaRef = None) -> dict:
-    t0 = time.time()
+                     fasta: FastaRef = None, streaming: bool = None, dist=None) -> dict:
     fasta = fasta or FastaRef(ref_genome_file)
+    if streaming is None:
+        streaming = os.environ.get("GANON_WHOLE_SAMPLE", "0") != "1"
+    if streaming or dist is not None:
+        from .stream import anonymize_genome_streaming
+        timing = anonymize_genome_streaming(windows_in_sample, tumor_bam_file, normal_bam_file, fasta, anonymizer,
+                                            tumor_output_fastq, normal_output_fastq, record_statistics,
+                                            available_threads, dist=dist)
+        log.info("Anonymization complete for samples %s and %s: %s", tumor_output_fastq, normal_output_fastq,
+                 timing)
+        return timing
+    t0 = time.time()
     tumor = ReadTable(tumor_bam_file, threads=available_threads)
     normal = ReadTable(normal_bam_file, threads=available_threads)
     t1 = time.time()
@@ -65,7 +77,8 @@ def run_short_read_tumor_normal_anonymizer(vcf_variants_per_sample: Sequence[str
                                            tumor_normal_samples: Sequence[Tuple[str, str]],
                                            ref_genome_file: str, anonymizer: CompleteGermlineAnonymizer,
                                            output_filenames: Sequence[Tuple[str, str]], record_statistics: bool,
-                                           cpus: int = 1, enhance_parallelization: bool = False) -> List[dict]:
+                                           cpus: int = 1, enhance_parallelization: bool = False,
+                                           dist=None) -> List[dict]:
     """SR:889-967. Samples run one after another on the GPU (each is one device batch);
     ``cpus`` sets the host decode threads. The reference's enhanced mode crashes whenever a
     sample is split; here it is accepted and has no effect."""
@@ -80,5 +93,5 @@ def run_short_read_tumor_normal_anonymizer(vcf_variants_per_sample: Sequence[str
     timings = []
     for windows, (t_bam, n_bam), (t_out, n_out) in inputs:
         timings.append(anonymize_genome(windows, t_bam, n_bam, ref_genome_file, anonymizer, t_out, n_out,
-                                        record_statistics, max(1, int(cpus)), fasta=fasta))
+                                        record_statistics, max(1, int(cpus)), fasta=fasta, dist=dist))
     return timings

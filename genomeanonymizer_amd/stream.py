@@ -1,0 +1,438 @@
+"""Bounded-memory, contig-sharded anonymization of one tumor/normal pair.
+
+The reference walks a sample section by section through region queries
+(``anonymize_genome``, short_read_tumor_normal_anonymizer.py:625-760) and never holds a BAM in
+memory; its only state that outlives a contig is the pairing state — ``to_pair_anonymized_reads``,
+``written_read_ids`` (SR:134-165, :304-406, AM:351-389) — and the end-of-sample passes
+(``pair_unmapped_mates`` SR:561-600, ``write_single_end_reads`` SR:603-622). This module runs the
+same flow one FASTA contig ("job") at a time:
+
+1. decode the job's records only (``io.bam.BamReader``: .bai seek or forward stream);
+2. plan it in contig mode (``planner.ContigPlanner``): every name whose records all lie on this
+   contig is planned exactly; operations on "cross" names (a record whose mate is on another
+   sequence, or unplaced) become placeholder events;
+3. mask its scopes in one device batch (``CompleteGermlineAnonymizer``: HIP SNV + indel tally);
+4. resolve the placeholders, contig after contig in FASTA order, against the sample-wide pairing
+   state (``native.Resolver``, C++), and carry the records those names may still need (their
+   formatted FASTQ bytes) to later contigs;
+5. replay the job's I/O log (the reference's per-section append handles) and write its
+   bytes at the job's offset of each output file; the files grow in contig order.
+
+Multi-GPU: ``world`` ranks take the contigs round-robin in FASTA order (the north
+star's policy); round i processes jobs i*world .. i*world+world-1 in parallel, one per rank, each on
+its own GPU; one gather of the placeholders / carried records and one of the byte counts per round
+(gloo over the host) let every rank resolve and place its own job, so each rank decodes, plans,
+masks, formats and writes only its contigs. No data-path collective touches the masked bases.
+Memory: one job per rank plus the carried records of names still unpaired.
+"""
+from __future__ import annotations
+
+import os
+import time
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import native
+from .anonymizer_methods import CompleteGermlineAnonymizer, MaskResult
+from .io.bam import BamReader, ReadTable
+from .io.fasta import FastaRef
+from .planner import ContigPlanner, Plan, Window, UnsupportedInput
+from . import writer as _writer
+from .writer import OUTSIDE_WINDOWS, FastqFormatter, statistics_rows, write_statistics
+
+Key = Tuple[int, int, int, int]   # (job, dataset, scope, row)
+
+
+def _names(table: ReadTable, rows: np.ndarray) -> List[bytes]:
+    nb = table.names_blob
+    return [nb[o:o + n].tobytes() for o, n in zip(table.name_off[rows].tolist(), table.name_len[rows].tolist())]
+
+
+def _names_ds(tables, ds: np.ndarray, rows: np.ndarray) -> List[bytes]:
+    out: List[bytes] = [b""] * len(ds)
+    for d in (0, 1):
+        sel = np.nonzero(ds == d)[0]
+        for i, nm in zip(sel.tolist(), _names(tables[d], rows[sel])):
+            out[i] = nm
+    return out
+
+
+class Job:
+    """Phase 1 of one contig: decode, plan, mask; then, once resolved, its output bytes."""
+
+    def __init__(self, job: int, contig: str, readers, fasta: FastaRef, windows: Sequence[Window],
+                 anonymizer: CompleteGermlineAnonymizer):
+        self.job = job
+        self.contig = contig
+        t0 = time.time()
+        self.tables = tuple(r.contig(r.tid_of(contig)) for r in readers)
+        t1 = time.time()
+        planner = ContigPlanner(self.tables[0], self.tables[1], fasta, windows, job)
+        self.plan: Plan = planner.run()
+        ex = planner.contig_exports
+        t2 = time.time()
+        ev, rows = self.plan.io_arrays()
+        self.events, self.event_rows = ev, rows
+        self.ph = np.nonzero(ev[:, 0] >= 3)[0]
+        self.left = ex["left"]
+        self.cand = ex["cand"]
+        self.masked_scope = [np.full(t.n, -1, np.int64) for t in self.tables]
+        written = self._mask_instances()
+        self.res: MaskResult = anonymizer.anonymize(planner, self.plan, written=written)
+        t3 = time.time()
+        self.fmt = FastqFormatter(self.tables, self.res, anonymizer.format_fastq)
+        self.fmt.edited = {inst: self.fmt._edited(inst, e) for inst, e in self.res.leftovers.items()}
+        self.timing = {"decode_s": t1 - t0, "plan_s": t2 - t1, "mask_s": t3 - t2}
+
+    # -- which masked copy of each read the device produces --------------------------------------
+    def _mask_instances(self):
+        """One masked scope per read: its local write, else its first placeholder, else its
+        unwritten-pair entry (the instance the sample-wide state can store first)."""
+        ev, rows = self.events, self.event_rows
+        parts = []
+        w = ev[:, 0] == 1
+        parts.append((ev[w, 4].astype(np.int64), rows[w], ev[w, 5].astype(np.int64)))
+        p = self.ph
+        parts.append((ev[p, 4].astype(np.int64), rows[p], ev[p, 5].astype(np.int64)))
+        L = self.left
+        for s in (0, 1):
+            h = L[:, 1 + 4 * s] == 1 if len(L) else np.zeros(0, bool)
+            parts.append((L[h, 2 + 4 * s], L[h, 4 + 4 * s], L[h, 3 + 4 * s]))
+        ds = np.concatenate([x[0] for x in parts]).astype(np.int64)
+        rw = np.concatenate([x[1] for x in parts]).astype(np.int64)
+        sc = np.concatenate([x[2] for x in parts]).astype(np.int64)
+        m = sc >= 0
+        ds, rw, sc = ds[m], rw[m], sc[m]
+        for d in (0, 1):
+            sel = ds == d
+            r, s = rw[sel][::-1], sc[sel][::-1]        # reversed: the first occurrence wins
+            self.masked_scope[d][r] = s
+        keep = np.zeros(len(ds), bool)
+        if len(ds):
+            key = ds * (1 << 40) + rw
+            _, first = np.unique(key, return_index=True)
+            keep[first] = True
+        return ds[keep], rw[keep], sc[keep]
+
+    def check_instance(self, ds: int, row: int, scope: int) -> None:
+        if scope >= 0 and self.masked_scope[ds][row] != scope:
+            raise UnsupportedInput(
+                f"read {self.tables[ds].name(row)!r} would be written from two scopes of {self.contig!r} "
+                "(mate fields that disagree with where its records are)")
+
+    # -- exports for the resolution ---------------------------------------------------------------
+    def record_lengths(self, ds: np.ndarray, row: np.ndarray, sc: np.ndarray) -> np.ndarray:
+        T, N = self.tables
+        ds = np.asarray(ds, np.int64)
+        row = np.asarray(row, np.int64)
+        r0, r1 = np.where(ds == 0, row, 0), np.where(ds == 1, row, 0)
+        nl = np.where(ds == 0, T.name_len[r0], N.name_len[r1]).astype(np.int64)
+        ls = np.where(ds == 0, T.l_seq[r0], N.l_seq[r1]).astype(np.int64)
+        out = nl + 8 + 2 * ls
+        if self.fmt.edited and len(ds):
+            keys = FastqFormatter._key(ds, row, np.asarray(sc, np.int64))
+            ek = FastqFormatter._key(*zip(*self.fmt.edited.keys()))
+            el = np.array([len(b) for b in self.fmt.edited.values()], np.int64)
+            o = np.argsort(ek)
+            ek, el = ek[o], el[o]
+            j = np.minimum(np.searchsorted(ek, keys), len(ek) - 1)
+            hit = ek[j] == keys
+            out[hit] = el[j[hit]]
+        return out
+
+    def format_records(self, ds, row, sc) -> List[bytes]:
+        ds = np.asarray(ds, np.int64)
+        row = np.asarray(row, np.int64)
+        sc = np.asarray(sc, np.int64)
+        if len(ds) == 0:
+            return []
+        data = self.fmt.format_arrays(ds, row, sc)
+        off = np.concatenate([[0], np.cumsum(self.record_lengths(ds, row, sc))])
+        return [data[off[i]:off[i + 1]] for i in range(len(ds))]
+
+    def exports(self) -> dict:
+        ev, rows = self.events, self.event_rows
+        p = self.ph
+        ops = ev[p]
+        op_rows = rows[p]
+        op_ds = ops[:, 4].astype(np.int64)
+        L = self.left
+        left_ds = np.where(L[:, 1] == 1, L[:, 2], L[:, 6]) if len(L) else np.zeros(0, np.int64)
+        left_row = np.where(L[:, 1] == 1, L[:, 4], L[:, 8]) if len(L) else np.zeros(0, np.int64)
+        C = self.cand
+        cm = C[:, 1] >= 0 if len(C) else np.zeros(0, bool)
+        cand = np.zeros((len(C), 7), np.int64)
+        if len(C):
+            cand[:, 0] = self.job
+            cand[:, 1:6] = C
+        cand_names = [b""] * len(C)
+        idx = np.nonzero(cm)[0]
+        for i, nm in zip(idx.tolist(), _names_ds(self.tables, C[idx, 1], C[idx, 2])):
+            cand_names[i] = nm
+        # carried records: every instance the resolution may write outside this job
+        inst = [(ops[:, 4].astype(np.int64), op_rows, ops[:, 5].astype(np.int64))]
+        for s in (0, 1):
+            h = L[:, 1 + 4 * s] == 1 if len(L) else np.zeros(0, bool)
+            inst.append((L[h, 2 + 4 * s], L[h, 4 + 4 * s], L[h, 3 + 4 * s]))
+        inst.append((C[idx, 1], C[idx, 2], np.full(len(idx), -1, np.int64)))
+        ds = np.concatenate([x[0] for x in inst]).astype(np.int64)
+        rw = np.concatenate([x[1] for x in inst]).astype(np.int64)
+        sc = np.concatenate([x[2] for x in inst]).astype(np.int64)
+        carry: Dict[Key, bytes] = {}
+        if len(ds):
+            key = np.stack([ds, sc, rw], axis=1)
+            _, first = np.unique(key, axis=0, return_index=True)
+            first = np.sort(first)
+            ok = np.array([sc[i] < 0 or self.masked_scope[ds[i]][rw[i]] == sc[i] for i in first.tolist()], bool)
+            first = first[ok] if len(first) else first
+            recs = self.format_records(ds[first], rw[first], sc[first])
+            for i, b in zip(first.tolist(), recs):
+                carry[(self.job, int(ds[i]), int(sc[i]), int(rw[i]))] = b
+        return {
+            "job": self.job, "ops": ops, "op_rows": op_rows,
+            "op_names": _names_ds(self.tables, op_ds, op_rows),
+            "left": L, "left_names": _names_ds(self.tables, left_ds, left_row),
+            "cand": cand, "cand_names": cand_names, "carry": carry,
+        }
+
+    # -- output ----------------------------------------------------------------------------------
+    def output(self, out_n: np.ndarray, out_w: np.ndarray, carry: Dict[Key, bytes], block: int) -> List[bytes]:
+        """The job's bytes per output file (tumor .1, .2, normal .1, .2) with the resolved writes of
+        its placeholder events spliced into its I/O log."""
+        ev, rows = self.events, self.event_rows
+        n = len(ev)
+        is_ph = ev[:, 0] >= 3
+        k = np.ones(n, np.int64)
+        k[is_ph] = 0
+        if len(self.ph):
+            k[self.ph] = out_n
+        src = np.repeat(np.arange(n), k)                 # source event of each final event
+        nf = len(src)
+        fin = ev[src].copy()
+        frow = rows[src].copy()
+        fjob = np.full(nf, self.job, np.int64)
+        # the resolved writes: placeholder op i contributes out_w[i, :out_n[i]]
+        ph_pos = np.nonzero(is_ph[src])[0]
+        if len(ph_pos):
+            which = np.concatenate([np.arange(c) for c in out_n[out_n > 0]]) if np.any(out_n > 0) else np.zeros(0, np.int64)
+            opi = np.repeat(np.arange(len(self.ph)), out_n)
+            w = out_w[opi, which]
+            fin[ph_pos, 0] = 1
+            fin[ph_pos, 2] = w[:, 0]
+            fin[ph_pos, 3] = w[:, 1]
+            fin[ph_pos, 4] = w[:, 3]
+            fin[ph_pos, 5] = w[:, 4]
+            fin[ph_pos, 6] = 0
+            frow[ph_pos] = w[:, 5]
+            fjob[ph_pos] = w[:, 2]
+        wr = fin[:, 0] == 1
+        ext = wr & (fjob != self.job)
+        loc = wr & ~ext
+        for i in np.nonzero(loc & (fin[:, 5] >= 0))[0].tolist():
+            self.check_instance(int(fin[i, 4]), int(frow[i]), int(fin[i, 5]))
+        rec_len = np.zeros(nf, np.int64)
+        li = np.nonzero(loc)[0]
+        rec_len[li] = self.record_lengths(fin[li, 4], frow[li], fin[li, 5])
+        ext_bytes: Dict[int, bytes] = {}
+        for i in np.nonzero(ext)[0].tolist():
+            b = carry.get((int(fjob[i]), int(fin[i, 4]), int(fin[i, 5]), int(frow[i])))
+            if b is None:
+                raise UnsupportedInput("a record written across contigs was not carried (its mate fields disagree "
+                                       "with where its records are)")
+            ext_bytes[i] = b
+            rec_len[i] = len(b)
+        order = native.io_replay(fin[:, :7].astype(np.int32), np.where(wr, rec_len, 0), block)
+        out = []
+        for f in range(4):
+            e = order[f]
+            is_ext = ext[e]
+            le = e[~is_ext]
+            data = self.fmt.format_arrays(fin[le, 4], frow[le], fin[le, 5]) if len(le) else b""
+            if not np.any(is_ext):
+                out.append(data)
+                continue
+            off = np.concatenate([[0], np.cumsum(rec_len[le])])
+            parts, prev_local = [], 0
+            pos = np.nonzero(is_ext)[0]
+            for j, p in enumerate(pos.tolist()):
+                n_local_before = p - j
+                parts.append(data[off[prev_local]:off[n_local_before]])
+                parts.append(ext_bytes[int(e[p])])
+                prev_local = n_local_before
+            parts.append(data[off[prev_local]:])
+            out.append(b"".join(parts))
+        return out
+
+    def stats(self) -> Dict[str, List[int]]:
+        return statistics_rows(self.plan, self.res)
+
+
+class _Comm:
+    """Host-side gathers for the per-round exchange (gloo group over torch.distributed)."""
+
+    def __init__(self, dist=None):
+        self.dist = dist
+        self.group = None
+        self.rank, self.world = 0, 1
+        if dist is not None:
+            self.rank, self.world = dist.get_rank(), dist.get_world_size()
+            self.group = dist.new_group(backend="gloo") if dist.get_backend() != "gloo" else None
+
+    def allgather(self, obj) -> list:
+        if self.dist is None:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj, group=self.group)
+        return out
+
+    def barrier(self) -> None:
+        if self.dist is not None:
+            self.dist.barrier(group=self.group)
+
+    def allreduce_totals(self, totals: np.ndarray) -> np.ndarray:
+        """The one collective on the data path's results: int64 totals, summed over the ranks (RCCL
+        over xGMI on the default nccl group, gloo otherwise)."""
+        if self.dist is None:
+            return totals
+        import torch
+        dev = torch.device("cuda", torch.cuda.current_device()) if self.dist.get_backend() == "nccl" \
+            else torch.device("cpu")
+        t = torch.from_numpy(totals.astype(np.int64)).to(dev)
+        self.dist.all_reduce(t)
+        return t.cpu().numpy()
+
+
+def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam: str, fasta: FastaRef,
+                               anonymizer: CompleteGermlineAnonymizer, tumor_out: str, normal_out: str,
+                               record_statistics: bool, threads: int = 8, dist=None,
+                               normal_stats_path: Optional[str] = None, block_size: Optional[int] = None,
+                               window_bytes: int = 0) -> dict:
+    """One tumor/normal pair, contig by contig (single rank when ``dist`` is None, else the
+    ranks of the initialised torch.distributed world). Output files, statistics and errors are
+    the reference's (SR:625-760)."""
+    comm = _Comm(dist)
+    rank, world = comm.rank, comm.world
+    paths = [f"{tumor_out}.1.fastq", f"{tumor_out}.2.fastq", f"{normal_out}.1.fastq", f"{normal_out}.2.fastq"]
+    if block_size is None:
+        block_size = _writer.io_block_size(os.path.dirname(os.path.abspath(tumor_out)))
+    timing = {"decode_s": 0.0, "plan_s": 0.0, "mask_s": 0.0, "resolve_s": 0.0, "write_s": 0.0, "jobs": 0,
+              "reads": 0}
+    failure: Optional[BaseException] = None
+    if rank == 0:
+        for p in paths:
+            open(p, "wb").close()
+    comm.barrier()
+    fds = [os.open(p, os.O_WRONLY) for p in paths]
+    readers = (BamReader(tumor_bam, threads, window_bytes), BamReader(normal_bam, threads, window_bytes))
+    contigs = list(fasta.references)
+    resolver = native.Resolver()
+    carry: Dict[Key, bytes] = {}
+    cands: List[np.ndarray] = []
+    cand_names: List[bytes] = []
+    base = [0, 0, 0, 0]
+    stats_rows: List[Tuple[int, Dict[str, List[int]]]] = []
+    totals = np.zeros(8, np.int64)
+    n_rounds = (len(contigs) + world - 1) // world
+    try:
+        for rnd in range(n_rounds):
+            jid = rnd * world + rank
+            job = None
+            exp = None
+            err = None
+            if failure is None and jid < len(contigs):
+                try:
+                    job = Job(jid, contigs[jid], readers, fasta, windows, anonymizer)
+                    exp = job.exports()
+                    for k in ("decode_s", "plan_s", "mask_s"):
+                        timing[k] += job.timing[k]
+                    timing["jobs"] += 1
+                    timing["reads"] += int(job.tables[0].n + job.tables[1].n)
+                    totals += np.asarray(job.res.totals, np.int64)[:8]
+                except BaseException as e:   # every rank must reach the gathers
+                    failure, err = e, repr(e)
+            gathered = comm.allgather({"exp": exp, "err": err})
+            errs = [g["err"] for g in gathered if g["err"] is not None]
+            if errs:
+                if failure is not None:
+                    raise failure
+                raise RuntimeError(f"another rank failed: {errs[0]}")
+            t0 = time.time()
+            mine = None
+            for g in gathered:
+                e = g["exp"]
+                if e is None:
+                    continue
+                out_n, out_w = resolver.contig(e["job"], e["ops"], e["op_rows"], e["op_names"], e["left"],
+                                               e["left_names"])
+                carry.update(e["carry"])
+                cands.append(e["cand"])
+                cand_names.extend(e["cand_names"])
+                if job is not None and e["job"] == job.job:
+                    mine = (out_n, out_w)
+            t1 = time.time()
+            data = [b"", b"", b"", b""]
+            if job is not None:
+                try:
+                    data = job.output(mine[0], mine[1], carry, block_size)
+                    stats_rows.append((job.job, job.stats()))
+                except BaseException as e:
+                    failure, err = e, repr(e)
+            sizes = comm.allgather({"sizes": [len(d) for d in data], "err": err})
+            errs = [g["err"] for g in sizes if g["err"] is not None]
+            if errs:
+                if failure is not None:
+                    raise failure
+                raise RuntimeError(f"another rank failed: {errs[0]}")
+            for f in range(4):
+                off = base[f] + sum(sizes[r]["sizes"][f] for r in range(rank))
+                if data[f]:
+                    os.pwrite(fds[f], data[f], off)
+                base[f] += sum(g["sizes"][f] for g in sizes)
+            # carried records still reachable: pending pairs and the end-of-sample candidates
+            pend = resolver.pending()
+            live = set(map(tuple, pend.tolist()))
+            for c in cands:
+                for r in c[c[:, 2] >= 0].tolist() if len(c) else []:
+                    live.add((r[0], r[2], -1, r[3]))
+            for k in [k for k in carry if k not in live]:
+                del carry[k]
+            job = None
+            timing["resolve_s"] += t1 - t0
+            timing["write_s"] += time.time() - t1
+        # ---- end of the sample: pair_unmapped_mates, single ends (SR:561-622) ----
+        cand = np.concatenate(cands) if cands else np.zeros((0, 7), np.int64)
+        tail, single, wse = resolver.finish(cand, cand_names)
+        if rank == 0:
+            per_file: List[List[bytes]] = [[], [], [], []]
+            for w in tail.tolist():
+                per_file[2 * w[0] + w[1]].append(carry[(w[2], w[3], w[4], w[5])])
+            for f in range(4):
+                blob = b"".join(per_file[f])
+                if blob:
+                    os.pwrite(fds[f], blob, base[f])
+            if wse:
+                for d, prefix in enumerate((tumor_out, normal_out)):
+                    with open(f"{prefix}.single_end.fastq", "wb") as fh:
+                        fh.write(b"".join(carry[tuple(x)] for x in single[d].tolist()))
+        all_stats = comm.allgather(stats_rows)
+        if rank == 0 and record_statistics:
+            merged: Dict[str, List[int]] = {OUTSIDE_WINDOWS: [0] * 8}
+            for _, rows in sorted((x for part in all_stats for x in part), key=lambda t: t[0]):
+                for key, counts in rows.items():
+                    if key == OUTSIDE_WINDOWS:
+                        merged[key] = [a + b for a, b in zip(merged[key], counts)]
+                    else:
+                        merged[key] = list(counts)
+            write_statistics(normal_stats_path or f"{normal_bam}.statistics.txt", merged)
+    finally:
+        for fd in fds:
+            os.close(fd)
+        for r in readers:
+            r.close()
+        resolver.close()
+    totals = comm.allreduce_totals(totals)
+    timing["totals"] = {k: int(v) for k, v in zip(("masked_snv_calls", "masked_bases", "reads_in", "reads_written",
+                                                   "scopes", "rare_scopes", "large_tiles", "reserved"), totals)}
+    comm.barrier()
+    return timing

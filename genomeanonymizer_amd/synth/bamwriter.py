@@ -56,6 +56,11 @@ class BgzfWriter:
             self._fh.write(_bgzf_block(bytes(self._buf[:_BGZF_MAX_INPUT]), self._level))
             del self._buf[:_BGZF_MAX_INPUT]
 
+    def tell_virtual(self) -> int:
+        """BGZF virtual offset of the next byte written (compressed block offset << 16 | offset
+        in the block's uncompressed payload)."""
+        return (self._fh.tell() << 16) | len(self._buf)
+
     def close(self) -> None:
         if self._buf:
             self._fh.write(_bgzf_block(bytes(self._buf), self._level))
@@ -112,7 +117,9 @@ class BamRecord:
 
 
 def write_bam(path: str, contigs: Sequence[Tuple[str, int]], records: Iterable[BamRecord],
-              level: int = 6) -> None:
+              level: int = 6, index: bool = False) -> None:
+    """Coordinate-sorted BAM; ``index`` also writes ``path + '.bai'`` (bins with their chunks, the
+    16 kb linear index and the pseudo-bin 37450 of each reference, SAM spec §5.2)."""
     text = "@HD\tVN:1.6\tSO:coordinate\n" + "".join(
         f"@SQ\tSN:{n}\tLN:{l}\n" for n, l in contigs)
     w = BgzfWriter(path, level)
@@ -121,9 +128,57 @@ def write_bam(path: str, contigs: Sequence[Tuple[str, int]], records: Iterable[B
         nb = n.encode() + b"\x00"
         hdr += struct.pack("<i", len(nb)) + nb + struct.pack("<i", l)
     w.write(hdr)
+    spans = []   # (tid, pos, end, voff_beg, voff_end, unmapped)
     for rec in records:
-        w.write(rec.encode())
+        b = rec.encode()
+        v0 = w.tell_virtual()
+        w.write(b)
+        if index:
+            spans.append((rec.tid, rec.pos, rec.end(), v0, w.tell_virtual(), bool(rec.flag & 4)))
     w.close()
+    if index:
+        _write_bai(path + ".bai", len(contigs), spans)
+
+
+def _write_bai(path: str, n_ref: int, spans) -> None:
+    per = [[] for _ in range(n_ref)]
+    n_no_coor = 0
+    for s in spans:
+        if s[0] < 0:
+            n_no_coor += 1
+        else:
+            per[s[0]].append(s)
+    out = b"BAI\x01" + struct.pack("<i", n_ref)
+    for recs in per:
+        bins = {}
+        lin = {}
+        for tid, pos, end, v0, v1, unm in recs:
+            ch = bins.setdefault(reg2bin(pos, end), [])
+            if ch and ch[-1][1] == v0:
+                ch[-1][1] = v1
+            else:
+                ch.append([v0, v1])
+            for k in range(pos >> 14, ((end - 1) >> 14) + 1):
+                lin.setdefault(k, v0)
+        nb = len(bins) + (1 if recs else 0)
+        out += struct.pack("<i", nb)
+        for b in sorted(bins):
+            out += struct.pack("<Ii", b, len(bins[b]))
+            for v0, v1 in bins[b]:
+                out += struct.pack("<QQ", v0, v1)
+        if recs:
+            n_unm = sum(1 for r in recs if r[5])
+            out += struct.pack("<Ii", 37450, 2) + struct.pack("<QQ", recs[0][3], recs[-1][4]) + \
+                struct.pack("<QQ", len(recs) - n_unm, n_unm)
+        n_intv = (max(lin) + 1) if lin else 0
+        out += struct.pack("<i", n_intv)
+        last = 0
+        for k in range(n_intv):
+            last = lin.get(k, last)
+            out += struct.pack("<Q", last)
+    out += struct.pack("<Q", n_no_coor)
+    with open(path, "wb") as fh:
+        fh.write(out)
 
 
 def write_fasta(path: str, contigs: Sequence[Tuple[str, str]], width: int = 60) -> None:

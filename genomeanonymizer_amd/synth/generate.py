@@ -60,6 +60,7 @@ class ScenarioConfig:
     n_ref_runs: int = 0             # runs of 'N' in the reference
     unplaced_frac: float = 0.0      # of the unmapped mates: unplaced (tid -1)
     cross_contig_pairs: int = 0     # per sample: pairs with mates on two different contigs
+    bam_index: bool = False         # also write <bam>.bai
 
 
 @dataclasses.dataclass
@@ -353,7 +354,7 @@ def generate(cfg: ScenarioConfig, outdir: str) -> Dict[str, str]:
         recs.sort(key=lambda r: (r.tid if r.tid >= 0 else 1 << 30, r.pos, bool(r.flag & 4), r.name,
                                  r.flag & 0xC0))
         path = os.path.join(outdir, "tumor.bam" if sample == "T" else "normal.bam")
-        write_bam(path, contig_lens, recs)
+        write_bam(path, contig_lens, recs, index=cfg.bam_index)
         paths[sample] = path
     # window VCF: somatic SNVs + records on germline SNPs (kept-variant rule)
     vrecs = []

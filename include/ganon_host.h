@@ -60,6 +60,20 @@ GANON_HOST_API const char *ganon_bam_error(ganon_bam *bam);
 GANON_HOST_API void ganon_bam_close(ganon_bam *bam);
 GANON_HOST_API const char *ganon_host_last_error(void);
 
+/* Contig reader: bounded-memory decode of one reference sequence at a time (the records of BAM tid
+ * `tid`, file order). Seeks through the BAM index (<path>.bai or <path minus .bam>.bai) when one
+ * is present and valid, otherwise streams forward (a request for an earlier tid rescans from the
+ * first record). The returned ganon_bam carries the full reference list and is released with
+ * ganon_bam_close. The reader header view has n_records = 0. */
+typedef struct ganon_bam_reader ganon_bam_reader;
+GANON_HOST_API int ganon_bam_reader_open(const char *path, int threads, ganon_bam_reader **out);
+GANON_HOST_API int ganon_bam_reader_has_index(const ganon_bam_reader *reader);
+/* Compressed bytes read and inflated per step (default 32 MiB, at least 128 KiB). */
+GANON_HOST_API int ganon_bam_reader_set_window(ganon_bam_reader *reader, int64_t bytes);
+GANON_HOST_API int ganon_bam_reader_header(ganon_bam_reader *reader, ganon_bam_view *view);
+GANON_HOST_API int ganon_bam_reader_contig(ganon_bam_reader *reader, int32_t tid, ganon_bam **out);
+GANON_HOST_API void ganon_bam_reader_close(ganon_bam_reader *reader);
+
 /* FASTQ formatter. For record i:
  *   '@' name '/' mate '\n' SEQ '\n' '+' '\n' QUAL '\n'
  * SEQ: seq_len[i] nt16 nibbles starting at nibble seq_nib_off[i] of seq_buf[seq_sel[i]],
@@ -107,6 +121,7 @@ typedef struct ganon_plan_table {  /* one sample, file order (columns of a ganon
   int32_t n_ref;
   const int64_t *ref_len;          /* [n_ref] BAM header lengths                            */
   const int32_t *tid_of_contig;    /* [n_contigs] this BAM's tid of each FASTA contig, -1 none */
+  const int32_t *mate_tid;         /* per record; read only in contig mode                    */
 } ganon_plan_table;
 typedef struct ganon_plan_input {
   ganon_plan_table tables[2];      /* 0 tumor, 1 normal                                      */
@@ -117,6 +132,17 @@ typedef struct ganon_plan_input {
   int32_t n_windows;               /* variant windows in get_windows order (SR:71-131)        */
   const int32_t *win_contig;
   const int64_t *win_first, *win_last;
+  /* Contig mode (contig_mode != 0): plan FASTA contig only_contig alone from tables holding that
+   * contig's records (ganon_bam_reader_contig). Names with a record whose mate is on another
+   * reference sequence or unplaced (mate_tid != tid) are "cross" names: every operation of the
+   * reference's pairing state on them (write_pair of a complete pair, the to_pair store of an
+   * incomplete one, a pass-through) becomes a placeholder event (kinds 3 / 4 / 5) that
+   * ganon_resolver_contig decides with the state of the contigs before; the other names are planned
+   * here exactly. Their pairs still unwritten at the contig's end are exported (view.left), and so
+   * are the placed-unmapped records of the contig's windows that pair_unmapped_mates may need
+   * (view.cand). */
+  int32_t contig_mode;
+  int32_t only_contig;
 } ganon_plan_input;
 typedef struct ganon_plan ganon_plan;
 typedef struct ganon_plan_view {
@@ -134,12 +160,50 @@ typedef struct ganon_plan_view {
   int64_t n_single[2];
   const int64_t *single[2];  /* per dataset: (row, scope) pairs of the single-end records    */
   int32_t write_single_end;
+  /* contig mode: events may also hold kind 3 (a complete pair of a cross name: two consecutive events,
+   * slot 0 then 1), 4 (store in to_pair, write and drop when complete: anonymize_window SR:313-360),
+   * 5 (pass-through store, write when complete: SR:375-406); the 7th int is the event's clock. */
+  int64_t n_left;
+  const int64_t *left;       /* 9 per unwritten pair: clock, has0, ds0, scope0, row0, has1, ds1, scope1, row1 */
+  int64_t n_cand;
+  const int64_t *cand;       /* 5 per record: window, dataset (-1: this window's fetch raises), row,
+                                slot (-1: no READ1/READ2 flag), 1 if the record has no SEQ */
 } ganon_plan_view;
 /* Returns GANON_PLAN_OK or a GANON_PLAN_E_* code (message: ganon_plan_last_error()). */
 GANON_HOST_API int ganon_plan_run(const ganon_plan_input *in, ganon_plan **out);
 GANON_HOST_API int ganon_plan_view_get(const ganon_plan *plan, ganon_plan_view *view);
 GANON_HOST_API void ganon_plan_free(ganon_plan *plan);
 GANON_HOST_API const char *ganon_plan_last_error(void);
+/* ---- Cross-contig resolution (contig mode) -------------------------------------------------------
+ * Replays, contig after contig in FASTA order, the placeholder events of the contig plans against the
+ * sample-wide pairing state (to_pair_anonymized_reads / written_read_ids, SR:134-165, :304-406,
+ * AM:351-389), then the end of the sample: pair_unmapped_mates (SR:561-600) over the exported
+ * candidates and the single ends (SR:603-622). Instances are (job, dataset, scope, row), job = the
+ * contig plan they come from. A write is 6 int64: file dataset, file slot, job, dataset, scope, row. */
+typedef struct ganon_resolver ganon_resolver;
+GANON_HOST_API int ganon_resolver_create(ganon_resolver **out);
+GANON_HOST_API void ganon_resolver_free(ganon_resolver *r);
+/* ops: the placeholder events of job's plan (7 int32 each, plan layout) with their rows and read
+ * names; left: the plan's unwritten pairs (9 int64 each) with names. out_n[i] receives the number of
+ * writes op i makes (0 or 2), out_w 12 int64 per op. */
+GANON_HOST_API int ganon_resolver_contig(ganon_resolver *r, int32_t job, int64_t n_ops, const int32_t *ops,
+                                         const int64_t *op_rows, const char *op_names, const int64_t *op_name_off,
+                                         const int32_t *op_name_len, int64_t n_left, const int64_t *left,
+                                         const char *left_names, const int64_t *left_name_off,
+                                         const int32_t *left_name_len, int32_t *out_n, int64_t *out_w);
+/* Pending instances (4 int64 each: job, dataset, scope, row); returns the count (all of them when
+ * cap >= count, else only the count). */
+GANON_HOST_API int64_t ganon_resolver_pending(ganon_resolver *r, int64_t *out, int64_t cap);
+/* cand: 7 int64 per record (job, window, dataset, row, slot, no-SEQ flag, 0) in window order, with
+ * names. tail (12 int64 per candidate) receives the writes of pair_unmapped_mates (count n_tail);
+ * single[d] (4 int64 per record, capacity = ganon_resolver_pending count) the single ends in
+ * dictionary order (counts n_single[2]). Returns GANON_PLAN_OK or GANON_PLAN_E_VALUE / _TYPE with the
+ * reference's error (message: ganon_plan_last_error). */
+GANON_HOST_API int ganon_resolver_finish(ganon_resolver *r, int64_t n_cand, const int64_t *cand, const char *names,
+                                         const int64_t *name_off, const int32_t *name_len, int64_t *tail,
+                                         int64_t *n_tail, int64_t *single0, int64_t *single1, int64_t *n_single,
+                                         int32_t *write_single_end);
+
 /* Order in which the write events of an I/O log (ganon_plan_view.events layout, 7 ints each)
  * reach the four FASTQ files (tumor .1, tumor .2, normal .1, normal .2 = file dataset * 2 + slot):
  * every "open" creates four CPython append-mode text handles (8 KiB TextIOWrapper chunks over a

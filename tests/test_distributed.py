@@ -1,6 +1,8 @@
-"""The N>1 path (contig shards, one process per rank, totals all-reduce) on CPU with gloo:
-two ranks must write exactly the reference's files. The CPU oracle stands in for the GPU
-(test infrastructure); the GPU variant of this path is exercised by bench.py under torchrun."""
+"""The N>1 path (round-robin contig shards, one process per rank, each decoding, planning,
+masking and writing its own contigs; per-round gloo exchange of the cross-contig pairing state;
+totals all-reduce) on CPU with gloo: two ranks must write exactly the reference's files. The CPU
+oracle stands in for the GPU (test infrastructure); tests/test_gpu_distributed.py runs the HIP
+engine."""
 import os
 import socket
 
@@ -16,7 +18,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, name, workdir, policy, q, engine="oracle", fail_rank=-1):
+def _worker(rank, world, port, name, workdir, q, engine="oracle", fail_rank=-1):
     import sys
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [repo, os.path.join(repo, "oracle"), os.path.join(repo, "tests")]
@@ -44,24 +46,24 @@ def _worker(rank, world, port, name, workdir, policy, q, engine="oracle", fail_r
                 raise RuntimeError("injected failure")
             anon.anonymize = boom
         tot = anonymize_genome_sharded(windows, paths["T"], paths["N"], paths["ref"], name_output(paths["T"]),
-                                       name_output(paths["N"]), True, rank, world, os.path.join(workdir, "shards"),
-                                       anon, dist, policy)
+                                       name_output(paths["N"]), True, anon, dist)
         q.put((rank, tot))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name,policy", [("edge", "lpt"), ("tiny", "round_robin")])
-def test_two_rank_contig_shards_match_reference(name, policy, tmp_path):
+@pytest.mark.parametrize("name,index", [("edge", True), ("tiny", False)])
+def test_two_rank_contig_shards_match_reference(name, index, tmp_path):
     from helpers import GOLDEN, run_pipeline_vs_golden
     from genomeanonymizer_amd.synth.generate import generate, scenario
     import gzip
+    import dataclasses
     workdir = str(tmp_path / name)
-    paths = generate(scenario(name), os.path.join(workdir, "in"))
+    paths = generate(dataclasses.replace(scenario(name), bam_index=index), os.path.join(workdir, "in"))
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, name, workdir, policy, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, name, workdir, q)) for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:
@@ -87,7 +89,7 @@ def test_a_failing_rank_stops_every_rank(tmp_path):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, "tiny", workdir, "lpt", q, "oracle", 1)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, "tiny", workdir, q, "oracle", 1)) for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:

@@ -217,11 +217,31 @@ def test_hip_configs2_density_matches_oracle(masker, oracle):
     assert paths["region_passes"] > 0, paths
 
 
+@pytest.mark.parametrize("whole", [False, True], ids=["streaming", "whole_sample"])
 @pytest.mark.parametrize("name", ["tiny", "edge", "config1"])
-def test_hip_pipeline_matches_reference(name, tmp_path, hip_built):
+def test_hip_pipeline_matches_reference(name, whole, tmp_path, hip_built, monkeypatch):
     from genomeanonymizer_amd.anonymizer_methods import CompleteGermlineAnonymizer
+    monkeypatch.setenv("GANON_WHOLE_SAMPLE", "1" if whole else "0")
     bad = run_pipeline_vs_golden(name, str(tmp_path / name), CompleteGermlineAnonymizer(device=0))
     assert bad == {}
+
+
+def test_hip_streaming_matches_whole_sample_many_contigs(tmp_path, hip_built, monkeypatch):
+    """The streamed product (per-contig decode, contig-mode plans, one HIP batch per contig with the
+    genome resident, cross-contig resolution) against the whole-sample product on a 12-contig
+    tiled sample with cross-contig mates, unplaced mates and single ends: identical files."""
+    import os
+    from test_stream import _run
+    from genomeanonymizer_amd.anonymizer_methods import CompleteGermlineAnonymizer
+    from genomeanonymizer_amd.synth.generate import generate, scenario
+    from genomeanonymizer_amd.synth.tile import tile_sample
+    base = generate(scenario("edge"), str(tmp_path / "base"))
+    paths = tile_sample(base, 4, str(tmp_path / "in"))
+    anon = CompleteGermlineAnonymizer(device=0)
+    whole = _run(paths, str(tmp_path / "whole"), True, anon)
+    streamed = _run(paths, str(tmp_path / "stream"), False, anon)
+    assert whole == streamed
+    assert any(k.endswith(".single_end.fastq") for k in whole)
 
 
 def test_cli_matches_reference(tmp_path, hip_built):

@@ -13,8 +13,8 @@ from test_distributed import _free_port, _worker
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("name,policy", [("edge", "lpt"), ("config1", "round_robin")])
-def test_two_rank_hip_contig_shards_match_reference(name, policy, tmp_path, hip_built):
+@pytest.mark.parametrize("name", ["edge", "config1"])
+def test_two_rank_hip_contig_shards_match_reference(name, tmp_path, hip_built):
     import gzip
     from helpers import GOLDEN
     from genomeanonymizer_amd.short_read_tumor_normal_anonymizer import name_output
@@ -24,7 +24,7 @@ def test_two_rank_hip_contig_shards_match_reference(name, policy, tmp_path, hip_
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, name, workdir, policy, q, "hip")) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, name, workdir, q, "hip")) for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:

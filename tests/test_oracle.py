@@ -23,10 +23,12 @@ def test_oracle_matches_reference_per_scope(seed):
     assert tot[0] == exp_calls.sum()
 
 
+@pytest.mark.parametrize("whole", [False, True], ids=["streaming", "whole_sample"])
 @pytest.mark.parametrize("name", ["tiny", "edge", "config1"])
-def test_pipeline_with_oracle_matches_reference(name, tmp_path):
+def test_pipeline_with_oracle_matches_reference(name, whole, tmp_path, monkeypatch):
     from pyoracle import OracleEngine
     from genomeanonymizer_amd.anonymizer_methods import CompleteGermlineAnonymizer
+    monkeypatch.setenv("GANON_WHOLE_SAMPLE", "1" if whole else "0")
     bad = run_pipeline_vs_golden(name, str(tmp_path / name), CompleteGermlineAnonymizer(engine=OracleEngine()))
     assert bad == {}
 

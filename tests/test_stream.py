@@ -1,0 +1,179 @@
+"""Bounded-memory streaming (stream.py): contig reader, contig-mode planning, cross-contig
+resolution, multi-rank placement. The CPU oracle stands in for the device (test infrastructure);
+tests/test_gpu.py and tests/test_gpu_distributed.py run the same paths on the HIP engine.
+
+Parity: the streamed files must equal the whole-sample path's (planner.py/ganon_plan.cpp over the
+whole BAM, one device batch), which tests/test_oracle.py pins to the reference's own outputs."""
+import dataclasses
+import os
+import shutil
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+
+def _scenario(seed: int, n_contigs: int = 4):
+    from genomeanonymizer_amd.synth.generate import ContigSpec, ScenarioConfig
+    rng = np.random.default_rng(seed)
+    contigs = []
+    for c in range(n_contigs):
+        L = int(rng.integers(8_000, 30_000))
+        wins, x = [], 1001 + int(rng.integers(0, 2000))
+        while x < L - 1500 and len(wins) < 5:
+            wins.append(x)
+            x += 2003 + int(rng.integers(0, 6000))
+        if c == 1:
+            wins = []            # a contig without windows: one whole-contig section
+        contigs.append(ContigSpec(f"chr{c}", L, int(rng.integers(80, 500)), windows=wins,
+                                  keep_windows=int(rng.integers(0, 2)),
+                                  holes=[("T" if rng.random() < 0.5 else "N", 3000, 3600)]))
+    return ScenarioConfig(name=f"s{seed}", seed=seed, contigs=contigs, germline_snp_per_kb=5.0,
+                          germline_indel_per_kb=1.0, hom_fraction=0.3, softclip_frac=0.05,
+                          unmapped_mate_frac=0.04, n_base_frac=0.03, unplaced_frac=0.4, cross_contig_pairs=15,
+                          bam_index=bool(seed % 2))
+
+
+def _outputs(prefixes, stats_path):
+    files = {}
+    for pre in prefixes:
+        for suf in (".1.fastq", ".2.fastq", ".single_end.fastq"):
+            if os.path.exists(pre + suf):
+                files[os.path.basename(pre) + suf] = open(pre + suf, "rb").read()
+    files["stats"] = open(stats_path).read()
+    return files
+
+
+def _run(paths, outdir, whole: bool, anonymizer=None):
+    from pyoracle import OracleEngine
+    from genomeanonymizer_amd import short_read_tumor_normal_anonymizer as sr
+    from genomeanonymizer_amd.anonymizer_methods import CompleteGermlineAnonymizer
+    os.makedirs(outdir, exist_ok=True)
+    t_out, n_out = os.path.join(outdir, "tumor"), os.path.join(outdir, "normal")
+    old = os.environ.get("GANON_WHOLE_SAMPLE")
+    os.environ["GANON_WHOLE_SAMPLE"] = "1" if whole else "0"
+    try:
+        sr.run_short_read_tumor_normal_anonymizer(
+            [paths["vcf"]], [(paths["T"], paths["N"])], paths["ref"],
+            anonymizer or CompleteGermlineAnonymizer(engine=OracleEngine()), [(t_out, n_out)], True, 4)
+    finally:
+        if old is None:
+            os.environ.pop("GANON_WHOLE_SAMPLE")
+        else:
+            os.environ["GANON_WHOLE_SAMPLE"] = old
+    return _outputs((t_out, n_out), paths["N"] + ".statistics.txt")
+
+
+@pytest.mark.parametrize("index", [True, False])
+def test_contig_reader_matches_whole_file_decode(index, tmp_path):
+    from genomeanonymizer_amd.io.bam import BamReader, ReadTable
+    from genomeanonymizer_amd.synth.generate import generate, scenario
+    paths = generate(dataclasses.replace(scenario("config1"), bam_index=index), str(tmp_path / "in"))
+    for key in ("T", "N"):
+        full = ReadTable(paths[key])
+        for window in (0, 1 << 17):   # default window, and the smallest (records straddle windows)
+            R = BamReader(paths[key], threads=3, window=window)
+            assert R.has_index == index
+            assert R.ref_names == full.ref_names
+            for tid in (0, 0):           # a repeated request rescans
+                t = R.contig(tid)
+                rows = np.nonzero(full.tid == tid)[0]
+                assert t.n == len(rows)
+                for f in ("pos", "end", "flag", "l_seq", "n_cigar", "mate_tid", "mate_pos", "name_len"):
+                    assert np.array_equal(getattr(t, f), getattr(full, f)[rows]), f
+                assert t.names == [full.names[r] for r in rows]
+                lo, hi = int(full.seq_off[rows[0]]), int(full.seq_off[rows[-1]] + (full.l_seq[rows[-1]] + 1) // 2)
+                assert np.array_equal(t.seq, full.seq[lo:hi])
+                qlo = int(full.qual_off[rows[0]])
+                assert np.array_equal(t.qual, full.qual[qlo:qlo + len(t.qual)])
+            R.close()
+
+
+def test_contig_reader_multi_contig_any_order(tmp_path):
+    from genomeanonymizer_amd.io.bam import BamReader, ReadTable
+    from genomeanonymizer_amd.synth.generate import generate, scenario
+    for index in (True, False):
+        paths = generate(dataclasses.replace(scenario("edge"), bam_index=index), str(tmp_path / f"in{index}"))
+        full = ReadTable(paths["T"])
+        R = BamReader(paths["T"], threads=2)
+        for tid in (2, 0, 1, 1, 2):
+            t = R.contig(tid)
+            rows = np.nonzero(full.tid == tid)[0]
+            assert t.n == len(rows) and np.array_equal(t.pos, full.pos[rows])
+            assert t.names == [full.names[r] for r in rows]
+        assert R.contig(-1).n == 0
+        R.close()
+
+
+@pytest.mark.parametrize("seed", [21, 22])
+def test_streaming_matches_whole_sample(seed, tmp_path):
+    """Cross-contig mates, unplaced / placed unmapped mates, single ends, a contig without windows:
+    every file of the streamed run equals the whole-sample run's."""
+    from genomeanonymizer_amd.synth.generate import generate
+    paths = generate(_scenario(seed), str(tmp_path / "in"))
+    whole = _run(paths, str(tmp_path / "whole"), True)
+    streamed = _run(paths, str(tmp_path / "stream"), False)
+    assert set(whole) == set(streamed)
+    for k in whole:
+        assert whole[k] == streamed[k], k
+    assert any(k.endswith(".single_end.fastq") for k in whole)
+
+
+def test_streaming_many_contigs_matches_whole_sample(tmp_path):
+    """12 contigs (a tiled sample): per-contig offsets and the carried state over many rounds."""
+    from genomeanonymizer_amd.synth.generate import generate, scenario
+    from genomeanonymizer_amd.synth.tile import tile_sample
+    base = generate(scenario("tiny"), str(tmp_path / "base"))
+    paths = tile_sample(base, 6, str(tmp_path / "in"))
+    whole = _run(paths, str(tmp_path / "whole"), True)
+    streamed = _run(paths, str(tmp_path / "stream"), False)
+    assert whole == streamed
+
+
+def _rank_worker(rank, world, port, paths, outdir, q):
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [repo, os.path.join(repo, "oracle"), os.path.join(repo, "tests")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from pyoracle import OracleEngine
+        from genomeanonymizer_amd.anonymizer_methods import CompleteGermlineAnonymizer
+        from genomeanonymizer_amd.distributed import anonymize_genome_sharded
+        from genomeanonymizer_amd.io.fasta import FastaRef
+        from genomeanonymizer_amd.io.vcf import read_vcf
+        from genomeanonymizer_amd.planner import get_windows
+        windows = get_windows(read_vcf(paths["vcf"]), FastaRef(paths["ref"]).index)
+        tot = anonymize_genome_sharded(windows, paths["T"], paths["N"], paths["ref"], os.path.join(outdir, "tumor"),
+                                       os.path.join(outdir, "normal"), True,
+                                       CompleteGermlineAnonymizer(engine=OracleEngine()), dist)
+        q.put((rank, tot))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_three_ranks_match_one_rank(tmp_path):
+    """3 ranks over 5 contigs (the last round leaves a rank idle): the files equal one rank's."""
+    from test_distributed import _free_port
+    from genomeanonymizer_amd.synth.generate import generate
+    paths = generate(_scenario(23, n_contigs=5), str(tmp_path / "in"))
+    one = _run(paths, str(tmp_path / "one"), False)
+    stats_one = one.pop("stats")
+    os.remove(paths["N"] + ".statistics.txt")
+    out = str(tmp_path / "three")
+    os.makedirs(out)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_worker, args=(r, 3, port, paths, out, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(300)
+    assert [p.exitcode for p in procs] == [0, 0, 0]
+    tots = dict(q.get() for _ in range(3))
+    assert tots[0] == tots[1] == tots[2]
+    three = _outputs((os.path.join(out, "tumor"), os.path.join(out, "normal")), paths["N"] + ".statistics.txt")
+    assert three.pop("stats") == stats_one
+    assert three == one

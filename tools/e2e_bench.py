@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
 """End-to-end timing of the product pipeline on one tumor/normal pair (BAM decode -> native
 planner -> GPU masking + indel tally -> GPU FASTQ formatting -> files), the path a user of the
-CLI runs. Prints one JSON line with per-stage seconds and reads/s.
+CLI runs: the streamed path (per contig, bounded memory; the default) and the whole-sample path.
+Prints one JSON line with per-stage seconds, reads/s and the process's peak RSS per mode.
 
-    python tools/e2e_bench.py DIR   # DIR holds tumor.bam normal.bam ref.fa variants.vcf
+    python tools/e2e_bench.py DIR   # DIR holds tumor.bam normal.bam ref.fa variants.vcf (tools/e2e_data.py)
 """
 import json
 import os
@@ -29,18 +30,31 @@ def main():
     t_win = time.time() - t0
     anon = CompleteGermlineAnonymizer(device=0)
     anon.engine   # context creation outside the timed stages
-    runs = []
-    for _ in range(2):    # the first run pays one-time costs (module loads, device init)
-        tim = sr.anonymize_genome(windows, os.path.join(d, "tumor.bam"), os.path.join(d, "normal.bam"),
-                                  os.path.join(d, "ref.fa"), anon, os.path.join(out, "tumor"),
-                                  os.path.join(out, "normal"), True, 16, fasta=fasta)
-        runs.append(tim)
-    tim = runs[-1]
-    total = tim["decode_s"] + tim["plan_s"] + tim["mask_s"] + tim["write_s"]
-    print(json.dumps({"reads": tim["reads"], "scopes": tim["scopes"], "windows_s": round(t_win, 3),
-                      "stages_s": {k: round(v, 3) for k, v in tim.items() if k.endswith("_s")},
-                      "total_s": round(total, 3), "reads_per_s": round(tim["reads"] / total, 1),
-                      "first_run_total_s": round(sum(v for k, v in runs[0].items() if k.endswith("_s")), 3)}))
+    import resource
+    res = {"windows_s": round(t_win, 3)}
+    modes = sys.argv[3].split(",") if len(sys.argv) > 3 else ["stream", "whole"]
+    for mode in modes:
+        runs = []
+        for _ in range(2):    # the first run pays one-time costs (module loads, device init)
+            t1 = time.time()
+            tim = sr.anonymize_genome(windows, os.path.join(d, "tumor.bam"), os.path.join(d, "normal.bam"),
+                                      os.path.join(d, "ref.fa"), anon, os.path.join(out, f"tumor_{mode}"),
+                                      os.path.join(out, f"normal_{mode}"), True, 16, fasta=fasta,
+                                      streaming=(mode == "stream"))
+            tim["wall_s"] = time.time() - t1
+            runs.append(tim)
+        tim = runs[-1]
+        res[mode] = {"reads": tim["reads"], "stages_s": {k: round(v, 3) for k, v in tim.items() if k.endswith("_s")},
+                     "reads_per_s": round(tim["reads"] / tim["wall_s"], 1),
+                     "peak_rss_mb": resource.getrusage(resource.RUSAGE_SELF).ru_maxrss // 1024,
+                     "first_run_wall_s": round(runs[0]["wall_s"], 3)}
+        print(json.dumps({mode: res[mode]}), file=sys.stderr, flush=True)
+    if "stream" in res and "whole" in res:
+        same = all(open(os.path.join(out, f"{x}_stream{s}"), "rb").read() ==
+                   open(os.path.join(out, f"{x}_whole{s}"), "rb").read()
+                   for x in ("tumor", "normal") for s in (".1.fastq", ".2.fastq"))
+        res["stream_equals_whole"] = same
+    print(json.dumps(res))
 
 
 if __name__ == "__main__":

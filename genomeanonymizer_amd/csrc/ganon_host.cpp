@@ -392,6 +392,7 @@ struct ganon_bam_reader {
   int64_t data_voff = 0;             // virtual offset of the first record
   bool has_index = false;
   std::vector<int64_t> index_beg;    // per tid: virtual offset of its first record, -1 = no records
+  std::vector<int64_t> index_end;    // per tid: virtual offset past its last record (-1 unknown)
   int64_t cur_voff = -1;             // forward cursor: the first record not yet consumed
   int32_t cur_tid = 0;
 };
@@ -404,9 +405,9 @@ inline int64_t tid_order(int32_t t) { return t < 0 ? (int64_t)INT32_MAX : (int64
 // Reads and inflates complete BGZF blocks starting at file offset coff (at most R->chunk compressed
 // bytes). Appends the inflated bytes to data and one (data offset, file offset) pair per non-empty
 // block to bmap. Returns the file offset after the last complete block, or -1 on error.
-int64_t read_blocks(ganon_bam_reader *R, int64_t coff, std::vector<uint8_t> &data,
+int64_t read_blocks(ganon_bam_reader *R, int64_t coff, int64_t step, std::vector<uint8_t> &data,
                     std::vector<std::pair<int64_t, int64_t>> &bmap) {
-  const int64_t want = std::min<int64_t>(R->chunk, R->fsize - coff);
+  const int64_t want = std::min<int64_t>(std::max<int64_t>(step, 1 << 17), R->fsize - coff);
   std::vector<uint8_t> comp((size_t)want);
   if (std::fseek(R->fh, (long)coff, SEEK_SET) != 0 || std::fread(comp.data(), 1, (size_t)want, R->fh) != (size_t)want)
     return set_err("short read");
@@ -444,9 +445,12 @@ int64_t voff_at(const std::vector<std::pair<int64_t, int64_t>> &bmap, int64_t x)
 
 // Streams from virtual offset voff: keeps the records of `tid`, stops at the first record after them
 // (each tid's records are contiguous in a coordinate-sorted file). first_tid: tid of the first
-// record met (kTidEnd when none) so that an index start can be validated.
-int scan_tid(ganon_bam_reader *R, int64_t voff, int32_t tid, std::vector<uint8_t> &kept, int64_t &next_voff,
-             int32_t &next_tid, int32_t &first_tid) {
+// record met (kTidEnd when none) so that an index start can be validated. hint: expected compressed
+// bytes of the sequence (index span) or 0; the step read and inflated at a time starts there (or at
+// 1 MiB) and doubles up to the reader's window, so a small sequence never inflates a whole window.
+int scan_tid(ganon_bam_reader *R, int64_t voff, int32_t tid, int64_t hint, std::vector<uint8_t> &kept,
+             int64_t &next_voff, int32_t &next_tid, int32_t &first_tid) {
+  int64_t step = std::min<int64_t>(hint > 0 ? hint + (1 << 16) : (1 << 20), R->chunk);
   int64_t coff = voff >> 16;
   std::vector<uint8_t> data;
   std::vector<std::pair<int64_t, int64_t>> bmap;
@@ -470,8 +474,9 @@ int scan_tid(ganon_bam_reader *R, int64_t voff, int32_t tid, std::vector<uint8_t
       while (k + 1 < bmap.size() && bmap[k + 1].first <= 0) ++k;
       bmap.erase(bmap.begin(), bmap.begin() + (long)k);
     }
-    coff = read_blocks(R, coff, data, bmap);
+    coff = read_blocks(R, coff, step, data, bmap);
     if (coff < 0) return -1;
+    step = std::min<int64_t>(2 * step, R->chunk);
     for (;;) {
       if (dpos + 4 > (int64_t)data.size()) break;
       int32_t bs, rtid;
@@ -517,12 +522,12 @@ void load_index(ganon_bam_reader *R, const std::string &bam_path) {
     if (!rd(magic, 4) || std::memcmp(magic, "BAI\1", 4) != 0 || !rd(&n_ref, 4) ||
         n_ref != (int32_t)R->header.ref_len.size())
       continue;
-    std::vector<int64_t> beg((size_t)n_ref, -1);
+    std::vector<int64_t> beg((size_t)n_ref, -1), end((size_t)n_ref, -1);
     bool ok = true;
     for (int32_t r = 0; r < n_ref && ok; ++r) {
       int32_t n_bin;
       if (!rd(&n_bin, 4) || n_bin < 0) { ok = false; break; }
-      int64_t pseudo = -1, lo = -1;
+      int64_t pseudo = -1, pseudo_end = -1, lo = -1, hi = -1;
       for (int32_t i = 0; i < n_bin && ok; ++i) {
         uint32_t bin;
         int32_t n_chunk;
@@ -531,9 +536,13 @@ void load_index(ganon_bam_reader *R, const std::string &bam_path) {
           uint64_t cb, ce;
           if (!rd(&cb, 8) || !rd(&ce, 8)) { ok = false; break; }
           if (bin == 37450) {
-            if (c == 0) pseudo = (int64_t)cb;
-          } else if (lo < 0 || (int64_t)cb < lo) {
-            lo = (int64_t)cb;
+            if (c == 0) {
+              pseudo = (int64_t)cb;
+              pseudo_end = (int64_t)ce;
+            }
+          } else {
+            if (lo < 0 || (int64_t)cb < lo) lo = (int64_t)cb;
+            if ((int64_t)ce > hi) hi = (int64_t)ce;
           }
         }
       }
@@ -541,9 +550,11 @@ void load_index(ganon_bam_reader *R, const std::string &bam_path) {
       if (!ok || !rd(&n_intv, 4) || n_intv < 0 || p + 8ull * (size_t)n_intv > b.size()) { ok = false; break; }
       p += 8ull * (size_t)n_intv;
       beg[(size_t)r] = pseudo >= 0 ? pseudo : lo;
+      end[(size_t)r] = pseudo >= 0 ? pseudo_end : hi;
     }
     if (!ok) continue;
     R->index_beg = std::move(beg);
+    R->index_end = std::move(end);
     R->has_index = true;
     return;
   }
@@ -568,7 +579,7 @@ int reader_open_impl(const char *path, int threads, ganon_bam_reader **out) {
       ganon_bam_reader_close(R);
       return set_err("truncated header");
     }
-    coff = read_blocks(R, coff, data, bmap);
+    coff = read_blocks(R, coff, 1 << 20, data, bmap);
     if (coff < 0) {
       ganon_bam_reader_close(R);
       return -1;
@@ -627,14 +638,17 @@ GANON_HOST_API int ganon_bam_reader_contig(ganon_bam_reader *R, int32_t tid, gan
       if (beg < 0) {
         done = true;   // the index lists no record of this sequence
       } else {
-        if (scan_tid(R, beg, tid, kept, next_voff, next_tid, first_tid) != 0) return -1;
+        const int64_t e = R->index_end[(size_t)tid];
+        const int64_t hint = e > beg ? (e >> 16) - (beg >> 16) : 0;
+        if (scan_tid(R, beg, tid, hint, kept, next_voff, next_tid, first_tid) != 0) return -1;
         done = first_tid == tid;   // a stale index falls back to the forward scan
         if (!done) kept.clear();
       }
     }
     if (!done) {
       const bool forward = R->cur_voff >= 0 && tid_order(R->cur_tid) <= tid_order(tid);
-      if (scan_tid(R, forward ? R->cur_voff : R->data_voff, tid, kept, next_voff, next_tid, first_tid) != 0) return -1;
+      if (scan_tid(R, forward ? R->cur_voff : R->data_voff, tid, 0, kept, next_voff, next_tid, first_tid) != 0)
+        return -1;
       R->cur_voff = next_voff;
       R->cur_tid = next_tid;
     }

@@ -229,8 +229,15 @@ class Job:
         wr = fin[:, 0] == 1
         ext = wr & (fjob != self.job)
         loc = wr & ~ext
-        for i in np.nonzero(loc & (fin[:, 5] >= 0))[0].tolist():
-            self.check_instance(int(fin[i, 4]), int(frow[i]), int(fin[i, 5]))
+        chk = np.nonzero(loc & (fin[:, 5] >= 0))[0]
+        if len(chk):
+            d, r, sc = fin[chk, 4].astype(np.int64), frow[chk], fin[chk, 5].astype(np.int64)
+            ms = np.where(d == 0, self.masked_scope[0][np.where(d == 0, r, 0)] if self.tables[0].n else -1,
+                          self.masked_scope[1][np.where(d == 1, r, 0)] if self.tables[1].n else -1)
+            bad = np.nonzero(ms != sc)[0]
+            if len(bad):
+                i = int(chk[bad[0]])
+                self.check_instance(int(fin[i, 4]), int(frow[i]), int(fin[i, 5]))
         rec_len = np.zeros(nf, np.int64)
         li = np.nonzero(loc)[0]
         rec_len[li] = self.record_lengths(fin[li, 4], frow[li], fin[li, 5])

@@ -26,7 +26,7 @@ struct ganon_ctx {
   int nt_copy = 1;             // GANON_PARAM_NT_COPY
   int ref2 = 1;                // GANON_PARAM_REF2
   int fq_skip = 0;             // GANON_PARAM_FASTQ_SKIP (profiling only)
-  int fq_kd = 3;               // GANON_PARAM_FASTQ_KD (3: 2.61 ms vs 2.69 at 4 on 10 M records)
+  int fq_kd = 0;               // GANON_PARAM_FASTQ_KD (0: quad kernel, 2 quads per lane; 3: dword kernel)
   int indel_sort = 0;          // GANON_PARAM_INDEL_SORT
   std::string err;
   struct Rec { std::string name; hipEvent_t e0, e1; };

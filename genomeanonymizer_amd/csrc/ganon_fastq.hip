@@ -683,6 +683,255 @@ __global__ void __launch_bounds__(kFqThreads) k_fq_format(const FqBufs bufs, con
   }
 }
 
+// ---- quad variant (GANON_PARAM_FASTQ_KD 0 / 9 / 10) -----------------------------------------------
+// The same tile design with 16-byte units: a virtual unit is one 16-byte-aligned tile quad of one
+// field, so the map / span lookup and the address arithmetic are paid once per 16 output bytes
+// instead of once per 4 (the dword kernel above is VALU-bound: without loads and stores it still
+// takes 2.2 of its 2.6 ms on configs[1]'s 10 M records). Each unit loads the aligned dwords under its
+// 16-byte source window (3 for bases: 16 nibbles; 5 for names / qualities), every dword address
+// clamped into the field's own aligned extent (bytes outside the field are masked off anyway, so a
+// clamped dword never matters and no load leaves the field's allocation), builds the four output
+// dwords with the dword kernel's transforms and writes them with one ds_write_b128 when the quad
+// lies inside the field, else per dword (whole dwords stored, edge dwords OR-ed). The virtual map is
+// 4x smaller, so the fill-forward scan is too.
+constexpr int kFqQMap = 1024;        // virtual quads: 512 tile quads + up to 3 shared per record
+static_assert(kFqQMap >= kFqTile / 16 + 3 * kFqStage, "virtual quad map");
+constexpr size_t kFqSmemQ = kFqTile + kFqQMap * sizeof(uint16_t) + 3 * kFqStage * sizeof(FqSpan);
+
+__device__ __forceinline__ uint32_t fq_dmask(int jd, int len) {   // bytes of dword jd..jd+3 inside [0, len)
+  const int lo = max(0, -jd), hi = min(4, len - jd);
+  return hi > lo ? (0xFFFFFFFFu >> (8 * (4 - (hi - lo)))) << (8 * lo) : 0u;
+}
+
+__device__ __forceinline__ const uint32_t *fq_clamp(uintptr_t a, uintptr_t lo, uintptr_t hi) {
+  return reinterpret_cast<const uint32_t *>(a < lo ? lo : a > hi ? hi : a);
+}
+
+template <int KQ>
+__global__ void __launch_bounds__(kFqThreads) k_fq_quad(const FqBufs bufs, const FqRec *__restrict__ recs,
+                                                        const uint64_t *__restrict__ off,
+                                                        const int64_t *__restrict__ tile_first, int64_t n,
+                                                        uint64_t total, uint8_t *__restrict__ out,
+                                                        unsigned long long *__restrict__ err, int skip,
+                                                        int *__restrict__ dense_list,
+                                                        unsigned int *__restrict__ dense_count) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[kFqSmemQ];
+  __shared__ unsigned long long s_w[kFqThreads / 64];
+  const uint64_t t0 = (uint64_t)blockIdx.x * kFqTile;
+  const int64_t r0 = tile_first[blockIdx.x];
+  const int64_t rl = (t0 + kFqTile < total) ? tile_first[blockIdx.x + 1] : n - 1;
+  const int t = threadIdx.x;
+  unsigned long long bad = ~0ull;
+  uint8_t *tile = smem;
+  uint32_t *tile32 = reinterpret_cast<uint32_t *>(smem);
+  if (rl - r0 + 1 > kFqStage) {   // left to k_fq_dense
+    if (t == 0) dense_list[atomicAdd(dense_count, 1u)] = (int)blockIdx.x;
+    return;
+  }
+  const int ns = (int)(rl - r0 + 1);
+  uint16_t *map = reinterpret_cast<uint16_t *>(smem + kFqTile);
+  FqSpan *spans = reinterpret_cast<FqSpan *>(smem + kFqTile + kFqQMap * sizeof(uint16_t));
+  // 1. zero tile and map; one thread per record: its three field spans in tile quads
+  reinterpret_cast<uint4 *>(tile)[t] = make_uint4(0, 0, 0, 0);
+  reinterpret_cast<uint4 *>(tile)[t + kFqThreads] = make_uint4(0, 0, 0, 0);
+  static_assert(kFqQMap * sizeof(uint16_t) == 8 * kFqThreads, "one uint2 of the map per thread");
+  reinterpret_cast<uint2 *>(map)[t] = make_uint2(0, 0);
+  unsigned long long cnt = 0;   // quads touched: bases | qualities << 16 | name << 32
+  FqSpan sp[3];
+  int64_t P0 = 0;
+  uint32_t NL = 0, L = 0, Q = 0, mate = 0;
+  if (t < ns) {
+    const FqRec R = recs[r0 + t];
+    P0 = (int64_t)off[r0 + t] - (int64_t)t0;
+    NL = (uint32_t)(R.name >> 48);
+    L = R.len;
+    Q = R.qlen;
+    mate = (uint32_t)((R.qual >> 48) & 0xFF);
+    const uint32_t fa[3] = {NL + 4, NL + 7 + L, 1u}, len[3] = {L, Q, NL};
+    const uint32_t rev[3] = {(uint32_t)(R.seq >> 58) & 1, (uint32_t)(R.seq >> 59) & 1, 0u};
+    const uint64_t src[3] = {2 * (uint64_t)(uintptr_t)pick4(bufs.seq, (uint32_t)(R.seq >> 56) & 3) + (R.seq & kOff56),
+                             (uint64_t)(uintptr_t)(pick4(bufs.qual, (uint32_t)(R.qual >> 56) & 3) + (R.qual & kOff48)),
+                             (uint64_t)(uintptr_t)(bufs.names + (R.name & kOff48))};
+#pragma unroll
+    for (int f = 0; f < 3; ++f) {
+      const FqField F = fq_field(P0, fa[f], len[f]);
+      const int q0 = F.a >> 4, q1 = (F.b + 15) >> 4;
+      sp[f].src = src[f];
+      sp[f].j0 = (int)(16 * (int64_t)q0 - (P0 + fa[f]));
+      sp[f].len = len[f];
+      sp[f].td0 = (uint16_t)q0;
+      sp[f].flags = rev[f] | (f << 1);
+      cnt |= (unsigned long long)(F.b > F.a ? q1 - q0 : 0) << (16 * f);
+    }
+  }
+  unsigned long long tot;
+  const unsigned long long pre = block_excl_scan(cnt, s_w, tot);   // (its barrier: tile and map are zero)
+  if (skip & 8) return;
+  const int V0 = (int)(tot & 0xFFFF), V1 = V0 + (int)((tot >> 16) & 0xFFFF), V = V1 + (int)((tot >> 32) & 0xFFFF);
+  if (t < ns) {
+    const int base[3] = {0, V0, V1};
+#pragma unroll
+    for (int f = 0; f < 3; ++f) {
+      const int c = (int)((cnt >> (16 * f)) & 0xFFFF);
+      const int v = base[f] + (int)((pre >> (16 * f)) & 0xFFFF);
+      sp[f].vs = (uint16_t)v;
+      spans[f * kFqStage + t] = sp[f];
+      if (c > 0) map[v] = (uint16_t)(f * kFqStage + t);
+    }
+    const int64_t o[8] = {0, NL + 1, NL + 2, NL + 3, NL + 4 + L, NL + 5 + L, NL + 6 + L, NL + 7 + L + Q};
+    const uint32_t x[8] = {'@', '/', (mate + '0') & 0xFF, '\n', '\n', '+', '\n', '\n'};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int64_t p = P0 + o[e];
+      if (p >= 0 && p < kFqTile) atomicOr(&tile32[p >> 2], x[e] << (8 * (p & 3)));
+    }
+  }
+  __syncthreads();
+  // 2. fill forward (prefix max over the virtual quads): thread t owns map[4t, 4t + 4)
+  {
+    uint2 *m2 = reinterpret_cast<uint2 *>(map) + t;
+    const uint2 a = *m2;
+    uint32_t v[4] = {a.x & 0xFFFF, a.x >> 16, a.y & 0xFFFF, a.y >> 16};
+    const uint32_t mx = max(max(v[0], v[1]), max(v[2], v[3]));
+    uint32_t inc = mx;
+    const int lane = t & 63;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t u = __shfl_up(inc, o);
+      if (lane >= o) inc = max(inc, u);
+    }
+    __syncthreads();   // s_w reused
+    if (lane == 63) s_w[t >> 6] = inc;
+    __syncthreads();
+    uint32_t pm = __shfl_up(inc, 1);
+    if (lane == 0) pm = 0;
+    for (int w = 0; w < (t >> 6); ++w) pm = max(pm, (uint32_t)s_w[w]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      pm = max(pm, v[i]);
+      v[i] = pm;
+    }
+    *m2 = make_uint2(v[0] | v[1] << 16, v[2] | v[3] << 16);
+  }
+  __syncthreads();
+  if (skip & 16) return;
+  // 3. units: KQ virtual quads per lane at a time
+#pragma unroll 1
+  for (int vb = 0; vb < ((skip & 32) ? 0 : V); vb += kFqThreads * KQ) {
+    uint32_t key[KQ], dw[KQ][5], sh[KQ], par[KQ], flg[KQ];
+    int tq[KQ], J[KQ], len[KQ];
+    const uint32_t *ad[KQ][5];
+#pragma unroll
+    for (int j = 0; j < KQ; ++j) {
+      const int v = vb + j * kFqThreads + t;
+      key[j] = 0xFFFFu;
+      sh[j] = par[j] = flg[j] = 0;
+      tq[j] = J[j] = len[j] = 0;
+#pragma unroll
+      for (int k = 0; k < 5; ++k) ad[j][k] = reinterpret_cast<const uint32_t *>(bufs.names);
+      if (v >= V) continue;
+      const uint32_t kf = map[v];
+      key[j] = kf;
+      const FqSpan S = spans[kf];
+      const int i = v - S.vs;
+      tq[j] = S.td0 + i;
+      J[j] = S.j0 + 16 * i;
+      len[j] = (int)S.len;
+      flg[j] = S.flags;
+      const int rel = (S.flags & 1) ? len[j] - 16 - J[j] : J[j];   // window start in field units
+      // 32-bit offsets from the field's aligned base A0: the window's aligned dwords, each clamped
+      // into the field's aligned extent [0, hi]
+      int start, hi;
+      uint64_t A0;
+      if ((S.flags >> 1) == 0) {   // bases: nibble units (S.src = 2 * byte address + first nibble)
+        const int n_off = (int)(S.src & 7) + rel;
+        par[j] = (uint32_t)(n_off & 1);
+        start = n_off >> 1;
+        hi = (((int)(S.src & 7) + len[j] - 1) >> 1) & ~3;
+        A0 = (S.src >> 1) & ~(uint64_t)3;
+      } else {
+        start = (int)(S.src & 3) + rel;
+        hi = ((int)(S.src & 3) + len[j] - 1) & ~3;
+        A0 = S.src & ~(uint64_t)3;
+      }
+      sh[j] = (uint32_t)(start & 3);
+      const int a = start - (start & 3);
+#pragma unroll
+      for (int k = 0; k < 5; ++k)
+        ad[j][k] = reinterpret_cast<const uint32_t *>(A0 + (uint64_t)(uint32_t)min(max(a + 4 * k, 0), hi));
+    }
+#pragma unroll
+    for (int j = 0; j < KQ; ++j) {
+      if (skip & 1) {
+        dw[j][0] = dw[j][1] = dw[j][2] = dw[j][3] = dw[j][4] = 0x11111111u;
+        continue;
+      }
+      dw[j][0] = __builtin_nontemporal_load(ad[j][0]);
+      dw[j][1] = __builtin_nontemporal_load(ad[j][1]);
+      dw[j][2] = __builtin_nontemporal_load(ad[j][2]);
+      if ((flg[j] >> 1) != 0) {
+        dw[j][3] = __builtin_nontemporal_load(ad[j][3]);
+        dw[j][4] = __builtin_nontemporal_load(ad[j][4]);
+      } else {
+        dw[j][3] = dw[j][4] = 0;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < KQ; ++j) {
+      if (key[j] == 0xFFFFu) continue;
+      const int f = flg[j] >> 1, k = key[j] % kFqStage;
+      const bool rev = flg[j] & 1;
+      uint32_t x[4], m[4];
+      const bool full = J[j] >= 0 && J[j] + 16 <= len[j];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) m[d] = full ? 0xFFFFFFFFu : fq_dmask(J[j] + 4 * d, len[j]);
+      if (f == 0) {
+        const uint32_t sel = rev ? (par[j] ? 0x04010502u : 0x00040105u) : (par[j] ? 0x02050104u : 0x05010400u);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          const uint32_t o = sh[j] + (rev ? 6 - 2 * d : 2 * d);   // window byte offset (<= 9)
+          const uint32_t kk = o >> 2;
+          const uint32_t lo_w = kk == 0 ? dw[j][0] : kk == 1 ? dw[j][1] : dw[j][2];
+          const uint32_t hi_w = kk == 0 ? dw[j][1] : kk == 1 ? dw[j][2] : dw[j][3];
+          const uint32_t w = __builtin_amdgcn_alignbyte(hi_w, lo_w, o & 3);
+          const uint32_t hiN = (w >> 4) & 0x0F0F0F0Fu, loN = w & 0x0F0F0F0Fu;
+          const uint32_t cc = __builtin_amdgcn_perm(loN, hiN, sel);
+          x[d] = rev ? nt16_lut(cc, kRevLo, kRevHi) : nt16_lut(cc, kFwdLo, kFwdHi);
+          const uint32_t y = x[d] | ~m[d];
+          if (rev && ((y - 0x01010101u) & ~y & 0x80808080u)) bad = min(bad, (unsigned long long)(r0 + k));
+        }
+      } else {
+        uint32_t we[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) we[e] = __builtin_amdgcn_alignbyte(dw[j][e + 1], dw[j][e], sh[j]);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          const uint32_t y = rev ? __builtin_bswap32(we[3 - d]) : we[d];
+          x[d] = f == 1 ? add33(y) : y;
+        }
+      }
+      if (full) {
+        reinterpret_cast<uint4 *>(tile)[tq[j]] = make_uint4(x[0], x[1], x[2], x[3]);
+      } else {
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          if (m[d] == 0xFFFFFFFFu) tile32[4 * tq[j] + d] = x[d];
+          else if (m[d]) atomicOr(&tile32[4 * tq[j] + d], x[d] & m[d]);
+        }
+      }
+    }
+  }
+  if (bad != ~0ull) atomicMin(err, bad);
+  __syncthreads();
+  if (skip & 2) return;
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int q = 0; q < kFqTile / (16 * kFqThreads); ++q) {
+    const int p = (q * kFqThreads + t) * 16;
+    if (t0 + p >= total) break;
+    __builtin_nontemporal_store(*reinterpret_cast<const u32x4 *>(tile + p), reinterpret_cast<u32x4 *>(out + t0 + p));
+  }
+}
+
 // Tiles touched by more than kFqStage records (records of a few dozen bytes), listed by
 // k_fq_format: built in LDS record by record (one wave per record), a fixed grid looping over
 // the list.
@@ -920,7 +1169,8 @@ GANON_API int ganon_fastq_run(ganon_ctx *ctx, ganon_fastq *f) {
     // virtual dwords per lane per round: a tile holds ~2,100 of them (2,048 tile dwords plus the
     // dwords neighbouring fields share), so the width sets the number of dependent load rounds
     const int kd = ctx->fq_kd;
-    auto kern = kd == 1 ? k_fq_format<1> : kd == 2 ? k_fq_format<2> : kd == 3 ? k_fq_format<3>
+    auto kern = kd == 0 ? k_fq_quad<2> : kd == 9 ? k_fq_quad<1> : kd == 10 ? k_fq_quad<3>
+              : kd == 1 ? k_fq_format<1> : kd == 2 ? k_fq_format<2> : kd == 3 ? k_fq_format<3>
               : kd == 5 ? k_fq_format<5> : kd == 6 ? k_fq_format<6> : kd == 8 ? k_fq_format<8> : k_fq_format<4>;
     hipLaunchKernelGGL(kern, dim3((unsigned)f->n_tiles), dim3(kFqThreads), 0, ctx->stream, f->bufs, f->recs,
                        f->off, f->tile_first, f->n, f->total, f->out, f->err, ctx->fq_skip, f->dense_list,

@@ -15,7 +15,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reads", type=int, default=10_000_000)
     ap.add_argument("--runs", type=int, default=5)
-    ap.add_argument("--configs", default="4:0",
+    ap.add_argument("--configs", default="0:0",
                     help="comma list of kd:skip (GANON_PARAM_FASTQ_KD / _SKIP), timed interleaved")
     a = ap.parse_args()
     import numpy as np

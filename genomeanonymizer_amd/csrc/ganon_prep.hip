@@ -421,7 +421,7 @@ __device__ __forceinline__ void block_scan2(int a, int b, int &ea, int &eb, int 
   __syncthreads();
 }
 
-// Segment records, group records 0, 1, 3, read_end and the partition candidates of group g.
+// Segment records, group records 0, 1, 3 and the partition candidates of group g.
 // Pass 1 walks every incidence of the group (segments counted as clean/dirty); pass 2 writes the
 // records — all-ACGT-reference segments from the front of the group's range, the others from the
 // back. No global allocation in the common case: a group with at most one segment per incidence
@@ -529,14 +529,7 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_emit(const Raw R, const l
         if (x.ds) mn1 = min(mn1, (unsigned long long)x.so);
         else mn0 = min(mn0, (unsigned long long)x.so);
       }
-      // bam_endpos (the tile path of huge scopes and the indel tally read it)
-      int64_t rl = 0;
-      for (int k = 0; k < x.ncig; ++k) {
-        const uint32_t w = k == 0 ? x.w0 : x.cg[k];
-        const int op = (int)(w & 0xF);
-        if (is_aligned_op(op) || op == 2 || op == 3) rl += w >> 4;
-      }
-      read_end[x.r] = (int32_t)(x.rs + (rl > 0 ? rl : 1));
+      // (read_end, bam_endpos, is the upload's: k_prep_reads writes it once per batch)
       if (huge[x.j]) continue;
       const uint32_t fl = ((uint32_t)x.ds << 30) | (mine ? kSegMine : 0u);
       const int64_t qnib = 2 * x.so, r0 = ref0[x.j];

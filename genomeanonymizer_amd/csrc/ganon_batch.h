@@ -120,6 +120,8 @@ struct ganon_dbatch {
   ganon_dev::DBuf b_ref_start, b_read_len, b_seq_off, b_cig_off, b_n_cig, b_dataset, b_write_scope, b_seq, b_cigar,
       b_incid_off, b_incid_read, b_span_start, b_span_len, b_ref_off, b_keep_pos, b_keep_code;
   // derived layer
+  ganon_dev::DBuf b_nseg, b_scost, b_scan_tmp, b_slots, b_slot0;   // segments per read; long-read mode: group
+                                                                  // costs, dirty flags, first slot per incidence
   ganon_dev::DBuf b_read_end, b_seen, b_cursor, b_gs0, b_lo, b_linemap, b_groups, b_seg4, b_grp_part, b_far, b_gokey, b_gopay, b_gtkey, b_gtflag, b_out,
       b_scope_calls, b_scope_bases, b_small;   // b_small: totals, static totals, counters, acc, status, errors
   uint8_t *out = nullptr;
@@ -128,12 +130,17 @@ struct ganon_dbatch {
   int32_t *counters = nullptr;          // [0] rare small (unused), [1] rare tiles
   int32_t *status = nullptr;            // sticky device error bits (1: far-mask list overflow)
   ganon_dev::PrepErr *err = nullptr;
-  unsigned long long *plan_info = nullptr;   // [0] far nibbles, [1] huge scopes, [2] written reads, [3] longest read
+  unsigned long long *plan_info = nullptr;   // [0] far nibbles, [1] huge scopes, [2] written reads, [3] longest read,
+                                             // [4] most segments of one read
   unsigned long long *paths = nullptr;       // GrpAux::paths (since upload)
   unsigned long long *cursor = nullptr;      // k_prep_emit allocation counters and their bases (b_cursor)
   ganon_dev::GrpAux *aux = nullptr;
   // plan of the current contents (device prep, sized at upload)
   int32_t n_groups = 0, group_target = 512;
+  // long-read mode (a read with more than one aligned segment): groups cut on the prefix of segments
+  // per scope (scost, upload) instead of the CSR offsets, and emitted one wave per incidence
+  bool long_mode = false;
+  int64_t *scost = nullptr;
   int64_t n_seg = 0, region = 0, far_cap = 0, n_written = 0, region_per_incid = 0;
   // huge scopes (> kGrpMaxSpan positions): tile path, planned on the host at upload
   std::vector<void *> huge_allocs;

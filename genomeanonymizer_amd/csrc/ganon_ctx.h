@@ -26,6 +26,7 @@ struct ganon_ctx {
   int nt_copy = 1;             // GANON_PARAM_NT_COPY
   int ref2 = 1;                // GANON_PARAM_REF2
   int fq_skip = 0;             // GANON_PARAM_FASTQ_SKIP (profiling only)
+  int prep_long = -1;          // GANON_PARAM_PREP_LONG (-1 auto, 0 never, 1 always)
   int fq_kd = 0;               // GANON_PARAM_FASTQ_KD (0: quad kernel, 2 quads per lane; 3: dword kernel)
   int indel_sort = 0;          // GANON_PARAM_INDEL_SORT
   std::string err;

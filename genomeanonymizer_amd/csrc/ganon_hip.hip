@@ -1339,7 +1339,7 @@ int load_batch(ganon_ctx *ctx, ganon_dbatch *db, const ganon_batch *b, const gan
   D.ref2 = db->ref->ref2;
   // small device state: totals, static totals, acc, far count, plan info (u64); counters, status;
   // the first validation error; the group kernels' aux pointers
-  constexpr size_t kU64 = 8 + 8 + 4 + 1 + 4 + 4;
+  constexpr size_t kU64 = 8 + 8 + 4 + 1 + 6 + 4;
   constexpr size_t kSmallBytes = kU64 * 8 + 8 * 4 + sizeof(PrepErr) + sizeof(GrpAux) + 64;
   uint8_t *sm = nullptr;
   if ((rc = ganon_prep::grow_n(ctx, db->b_small, kSmallBytes, &sm))) return rc;
@@ -1349,7 +1349,7 @@ int load_batch(ganon_ctx *ctx, ganon_dbatch *db, const ganon_batch *b, const gan
   db->acc = u + 16;
   db->far_count = u + 20;
   db->plan_info = u + 21;
-  db->paths = u + 25;
+  db->paths = u + 27;
   db->counters = reinterpret_cast<int32_t *>(u + kU64);
   db->status = db->counters + 4;
   db->err = reinterpret_cast<PrepErr *>(sm + kU64 * 8 + 8 * 4);
@@ -1493,6 +1493,11 @@ GANON_API int ganon_ctx_set_param(ganon_ctx *ctx, int param, int value) {
     if (value < 0 || value > 10 || value == 7)
       return fail(ctx, GANON_E_ARG, "FASTQ kernel: 0 / 9 / 10 (quads, 2 / 1 / 3 per lane), dwords per lane 1-6 or 8");
     ctx->fq_kd = value;
+    return GANON_OK;
+  }
+  if (param == GANON_PARAM_PREP_LONG) {
+    if (value < -1 || value > 1) return fail(ctx, GANON_E_ARG, "prep long mode: -1 (auto), 0 or 1");
+    ctx->prep_long = value;
     return GANON_OK;
   }
   if (param == GANON_PARAM_NT_COPY) {

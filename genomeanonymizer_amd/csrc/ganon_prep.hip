@@ -24,6 +24,11 @@
 //                   the others from the back (the group kernel reads the front part through the
 //                   2-bit reference); read_end; the lowest buffer offset of the reads the group
 //                   writes, per dataset (LDS atomicMin);
+//   k_prep_emit_long (long-read mode, a read with more than one aligned segment in the batch):
+//                   groups cut on the segments-per-scope prefix computed at upload, the record count
+//                   from the segments per read, one wave per incidence over the whole batch walking
+//                   its CIGAR 64 ops at a time (wave prefix sums of the query / reference deltas and
+//                   of the record counts) into deterministic slots — one walk, no atomics;
 //   k_prep_linemap + k_prep_pieces  the candidates mark their 128-byte lines in a 3-level
 //                   bitmap (ties on a line through a small hash table); each candidate's piece runs
 //                   from its line to the next marked one, so the pieces tile the output buffer —
@@ -32,6 +37,8 @@
 
 #include <algorithm>
 #include <cstring>
+
+#include <rocprim/device/device_scan.hpp>
 
 
 #include "ganon_batch.h"
@@ -133,8 +140,8 @@ __global__ void __launch_bounds__(kPrepThreads) k_ref_blocks(const uint8_t *__re
 
 // ---- per read (upload: validation) --------------------------------------------------------
 __global__ void __launch_bounds__(kPrepThreads) k_prep_reads(const Raw R, PrepErr *err, int32_t *__restrict__ read_end,
-                                                             unsigned long long *written) {
-  int n_written = 0, max_len = 0;
+                                                             int32_t *__restrict__ nseg, unsigned long long *written) {
+  int n_written = 0, max_len = 0, max_seg = 0;
   for (int64_t r = blockIdx.x * (int64_t)kPrepThreads + threadIdx.x; r < R.n_reads;
        r += (int64_t)gridDim.x * kPrepThreads) {
     const int L = R.read_len[r];
@@ -159,13 +166,19 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_reads(const Raw R, PrepEr
     }
     if (rs < 0 || rs + rl > INT32_MAX) { report(err, kErrReadPos, r); continue; }
     read_end[r] = (int32_t)(rs + (rl > 0 ? rl : 1));
+    int ns = 0;   // segments of the read (walk_segments)
+    if (nc <= (int)(R.n_cigar_ops - co)) walk_segments(R.cigar + co, nc, L, rs, nc ? R.cigar[co] : 0u, [&](int, int, int) { ++ns; });
+    nseg[r] = ns;
+    max_seg = max(max_seg, ns);
   }
   for (int o = 32; o > 0; o >>= 1) {
     n_written += __shfl_xor(n_written, o);
     max_len = max(max_len, __shfl_xor(max_len, o));
+    max_seg = max(max_seg, __shfl_xor(max_seg, o));
   }
   if ((threadIdx.x & 63) == 0 && n_written) atomicAdd(written, (unsigned long long)n_written);
   if ((threadIdx.x & 63) == 0 && max_len) atomicMax(written + 1, (unsigned long long)max_len);
+  if ((threadIdx.x & 63) == 0 && max_seg) atomicMax(written + 2, (unsigned long long)max_seg);
 }
 
 // ---- per scope (upload: validation) --------------------------------------------------------
@@ -208,8 +221,23 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_seen_check(const Raw R, c
 // CSR offsets are that prefix) falls in one bucket of `target` units. The weight bounds a group to
 // 256 scopes. A bucket skipped over by a scope with many incidences is an empty group.
 __device__ __forceinline__ int64_t group_of(const int64_t *__restrict__ incid_off, int64_t s, long long weight,
-                                            long long target) {
-  return (incid_off[s] + weight * s) / target;
+                                            long long target, const int64_t *__restrict__ cost) {
+  return cost ? cost[s] / target : (incid_off[s] + weight * s) / target;
+}
+
+// Long-read mode (upload): cost of scope s = its incidences' segments + weight (exclusive prefix next).
+__global__ void __launch_bounds__(kPrepThreads) k_prep_scope_cost(const Raw R, const int32_t *__restrict__ nseg,
+                                                                  long long weight, int64_t *__restrict__ cost) {
+  for (int64_t s = blockIdx.x * (int64_t)kPrepThreads + threadIdx.x; s <= R.n_scopes;
+       s += (int64_t)gridDim.x * kPrepThreads) {
+    if (s == R.n_scopes) {
+      cost[s] = 0;
+      continue;
+    }
+    int64_t c = weight;
+    for (int64_t i = R.incid_off[s]; i < R.incid_off[s + 1]; ++i) c += nseg[R.incid_read[i]];
+    cost[s] = c;
+  }
 }
 
 // Upload only: every incidence's read index and span, and the write scope of every written read.
@@ -229,13 +257,14 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_incid_check(const Raw R, 
 
 // gmeta[b] = (first scope of group b, its first incidence); allocation counters reset.
 __global__ void __launch_bounds__(kPrepThreads) k_prep_groups(const Raw R, long long weight, long long target,
+                                                              const int64_t *__restrict__ cost,
                                                               longlong2 *__restrict__ gmeta,
                                                               unsigned long long *__restrict__ cursor) {
   const int64_t gt = blockIdx.x * (int64_t)kPrepThreads + threadIdx.x;
   if (gt < kCursors) cursor[gt] = 0;
   for (int64_t s = gt; s < R.n_scopes; s += (int64_t)gridDim.x * kPrepThreads) {
-    const int64_t b = group_of(R.incid_off, s, weight, target);
-    const int64_t bp = s == 0 ? -1 : group_of(R.incid_off, s - 1, weight, target);
+    const int64_t b = group_of(R.incid_off, s, weight, target, cost);
+    const int64_t bp = s == 0 ? -1 : group_of(R.incid_off, s - 1, weight, target, cost);
     if (bp == b) continue;
     const longlong2 m = make_longlong2(s, R.incid_off[s]);
     for (int64_t x = bp + 1; x <= b; ++x) gmeta[x] = m;
@@ -369,6 +398,7 @@ __device__ __forceinline__ int64_t rec_hi(const int4 &x) { return (int64_t)(((ui
 
 // Upload only: nibbles of written reads outside their group's pieces (the far-mask capacity).
 __global__ void __launch_bounds__(kPrepThreads) k_prep_farcap(const Raw R, long long weight, long long target,
+                                                              const int64_t *__restrict__ cost,
                                                               const int4 *__restrict__ groups,
                                                               unsigned long long *far_nibs) {
   unsigned long long acc = 0;
@@ -376,7 +406,7 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_farcap(const Raw R, long 
        r += (int64_t)gridDim.x * kPrepThreads) {
     const int ws = R.write_scope[r];
     if (ws < 0 || R.read_len[r] == 0 || R.span_len[ws] > kGrpMaxSpan) continue;
-    const int64_t g = group_of(R.incid_off, ws, weight, target);
+    const int64_t g = group_of(R.incid_off, ws, weight, target, cost);
     const int4 A = groups[kGrpRec * g + 2], Bp = groups[kGrpRec * g + 4];
     const int64_t r0 = R.seq_off[r], r1 = r0 + ((int64_t)R.read_len[r] + 1) / 2;
     const int64_t in = max((int64_t)0, min(r1, rec_hi(A)) - max(r0, rec_lo(A))) +
@@ -662,6 +692,172 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_emit(const Raw R, const l
   }
 }
 
+// ---- long-read mode: one wave per incidence ---------------------------------------------------
+// A read with thousands of CIGAR ops (long reads with indel errors) walked by one thread is a
+// serial chain of dependent loads; here a wave walks it 64 ops at a time: per-lane query / reference
+// deltas, wave prefix sums for each op's (q, p), the read-length clip (ops at or past the read
+// length give nothing, as walk_segments stops there), per-lane segment pieces and a wave prefix of
+// the piece counts. The slots are deterministic: the incidence's records follow the group's
+// earlier incidences (k_prep_long_groups wrote each incidence's first slot from the segments per
+// read) in op order, so the walk needs no cursor and no atomics. A group all of whose records have
+// an all-ACGT reference range is read through the 2-bit reference by the group kernel (its clean
+// part is the whole range); a group with any other record is read through the nt16 reference (its
+// clean part is empty) — the wave that finds one flags the group.
+__device__ __forceinline__ void wave_walk(const Raw &R, int r, bool mine, int jl, int ss, int64_t r0ref,
+                                          const uint64_t *__restrict__ bad, int64_t n_blk, int64_t slot0,
+                                          unsigned long long *dirty, int4 *__restrict__ seg4) {
+  const int lane = threadIdx.x & 63;
+  const int nc = R.n_cig[r], L = R.read_len[r];
+  const int64_t co = R.cig_off[r];
+  const uint32_t fl = ((uint32_t)R.dataset[r] << 30) | (mine ? kSegMine : 0u);
+  const int64_t qnib = 2 * R.seq_off[r];
+  int q = 0, p = R.ref_start[r];   // carries (wave-uniform)
+  int64_t slot = slot0;
+  bool any_dirty = false;
+  for (int base = 0; base < nc && q < L; base += 64) {
+    const int k = base + lane;
+    const uint32_t w = k < nc ? R.cigar[co + k] : 0u;
+    const int op = (int)(w & 0xF), len = (int)(w >> 4);
+    const bool al = is_aligned_op(op);
+    const int dq = (al || op == 1 || op == 4) ? len : 0;
+    const int dp = (al || op == 2 || op == 3) ? len : 0;
+    const int q_ex0 = q, p_ex0 = p;
+    int iq = dq, ip = dp;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int xq = __shfl_up(iq, o), xp = __shfl_up(ip, o);
+      if (lane >= o) {
+        iq += xq;
+        ip += xp;
+      }
+    }
+    const int q0 = q_ex0 + iq - dq, p0 = p_ex0 + ip - dp;
+    const int n = (al && q0 < L) ? min(len, L - q0) : 0;
+    const int c = (n + kSegMaxLen - 1) / kSegMaxLen;   // pieces
+    int ic = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int x = __shfl_up(ic, o);
+      if (lane >= o) ic += x;
+    }
+    int64_t pc = slot + ic - c;
+    for (int o = 0; o < n; o += kSegMaxLen) {
+      const int m = min(kSegMaxLen, n - o);
+      const uint64_t sq = (uint64_t)(qnib + q0 + o), rf = (uint64_t)(r0ref + p0 + o);
+      const uint32_t z = (uint32_t)((sq >> 32) & 0xFF) | ((uint32_t)((rf >> 32) & 0xFF) << 8) | ((uint32_t)m << 16) | fl;
+      seg4[pc++] = make_int4((int)(uint32_t)sq, (int)(uint32_t)rf, (int)z,
+                             (int)((uint32_t)jl | ((uint32_t)(p0 + o - ss) << 12)));
+      any_dirty |= !ref_clean(bad, n_blk, (int64_t)rf, m);
+    }
+    slot += __shfl(ic, 63);
+    q += __shfl(iq, 63);
+    p += __shfl(ip, 63);
+  }
+  if (__any(any_dirty) && lane == 0) atomicOr(dirty, 1ull);
+}
+
+// Long-read mode, per group (thread per group): the record count from the segments per read (no
+// walk), the record range as k_prep_emit takes it, each incidence's first slot, the candidates,
+// group records 0 and 3, and the group's dirty flag reset. Long-read groups hold few incidences.
+__global__ void __launch_bounds__(kPrepThreads) k_prep_long_groups(const Raw R, const longlong2 *__restrict__ gmeta,
+                                                                   int n_groups, long long region_per_incid,
+                                                                   const int32_t *__restrict__ nseg,
+                                                                   int4 *__restrict__ groups,
+                                                                   unsigned long long *__restrict__ lo, LineMap M,
+                                                                   unsigned long long *__restrict__ cursor,
+                                                                   const unsigned long long *__restrict__ cursor_base,
+                                                                   unsigned long long *__restrict__ dirty,
+                                                                   int64_t *__restrict__ slot0, int write) {
+  for (int64_t g = blockIdx.x * (int64_t)kPrepThreads + threadIdx.x; g < n_groups;
+       g += (int64_t)gridDim.x * kPrepThreads) {
+    const longlong2 m0 = gmeta[g];
+    const longlong2 m1 = g + 1 < n_groups ? gmeta[g + 1] : make_longlong2(R.n_scopes, R.n_incid);
+    const int s0 = (int)m0.x, s1 = (int)m1.x;
+    const long long i0 = m0.y, i1 = m1.y;
+    unsigned long long count = 0, mn[2] = {kNone, kNone};
+    for (int s = s0; s < s1; ++s) {
+      if (R.span_len[s] > kGrpMaxSpan) continue;   // huge scope: tile path
+      for (int64_t i = R.incid_off[s]; i < R.incid_off[s + 1]; ++i) {
+        const int r = R.incid_read[i];
+        count += (unsigned long long)nseg[r];
+        if (R.write_scope[r] == s && R.read_len[r] > 0) {
+          const int d = R.dataset[r];
+          mn[d] = min(mn[d], (unsigned long long)R.seq_off[r]);
+        }
+      }
+    }
+    int64_t seg_b = i0;
+    if ((long long)count > i1 - i0) {
+      const int k = (int)(g % kCursors);
+      seg_b = (int64_t)(R.n_incid + cursor_base[k] + atomicAdd(&cursor[k], count));
+    }
+    const int64_t seg_e = seg_b + (int64_t)count;
+    if (write) {
+      int64_t x = seg_b;
+      for (int s = s0; s < s1; ++s) {
+        if (R.span_len[s] > kGrpMaxSpan) continue;
+        for (int64_t i = R.incid_off[s]; i < R.incid_off[s + 1]; ++i) {
+          slot0[i] = x;
+          x += nseg[R.incid_read[i]];
+        }
+      }
+    }
+    for (int d = 0; d < 2; ++d) {
+      lo[2 * g + d] = mn[d];
+      if (mn[d] != kNone) map_mark(M, mn[d], (uint32_t)(2 * g + d));
+    }
+    const int64_t region = i0 * region_per_incid + (int64_t)kGrpObs * g;
+    const int cap = (int)min((i1 - i0) * region_per_incid + kGrpObs, (long long)(INT32_MAX / 2));
+    groups[kGrpRec * g] = make_int4(s0, s1, (int)(uint32_t)seg_b, (int)(uint32_t)((uint64_t)seg_b >> 32));
+    groups[kGrpRec * g + 1] = make_int4((int)(uint32_t)seg_e, (int)(uint32_t)((uint64_t)seg_e >> 32), 0, 0);
+    groups[kGrpRec * g + 3] = make_int4((int)(uint32_t)region, (int)(uint32_t)((uint64_t)region >> 32), cap, 0);
+    dirty[g] = 0;
+  }
+}
+
+// Long-read mode: the records, one wave per incidence over the whole batch (a long-read group holds
+// one or two incidences: waves per group would idle). The scope of incidence i by binary search in
+// the CSR offsets, its group in closed form (group_of).
+__global__ void __launch_bounds__(kPrepThreads) k_prep_emit_waves(const Raw R, const int64_t *__restrict__ cost,
+                                                                  long long target, const longlong2 *__restrict__ gmeta,
+                                                                  const uint64_t *__restrict__ bad, int64_t n_blk,
+                                                                  const int64_t *__restrict__ slot0,
+                                                                  unsigned long long *__restrict__ dirty,
+                                                                  int4 *__restrict__ seg4) {
+  const int64_t nw = (int64_t)gridDim.x * kWaves;
+  for (int64_t i = blockIdx.x * (int64_t)kWaves + (threadIdx.x >> 6); i < R.n_incid; i += nw) {
+    int64_t a = 0, b = R.n_scopes - 1;   // last scope with incid_off[s] <= i
+    while (a < b) {
+      const int64_t mid = (a + b + 1) >> 1;
+      if (R.incid_off[mid] <= i) a = mid;
+      else b = mid - 1;
+    }
+    const int s = (int)a;
+    if (R.span_len[s] > kGrpMaxSpan) continue;
+    const int64_t g = group_of(R.incid_off, s, 0, target, cost);
+    const int r = R.incid_read[i];
+    wave_walk(R, r, R.write_scope[r] == s, s - (int)gmeta[g].x, R.span_start[s], R.ref_off[s] - R.span_start[s], bad,
+              n_blk, slot0[i], dirty + g, seg4);
+  }
+}
+
+// Long-read mode: each group's clean part (group record 1's mid): the whole range, or nothing.
+__global__ void __launch_bounds__(kPrepThreads) k_prep_long_mid(int n_groups, const unsigned long long *__restrict__ dirty,
+                                                                int4 *__restrict__ groups) {
+  for (int64_t g = blockIdx.x * (int64_t)kPrepThreads + threadIdx.x; g < n_groups;
+       g += (int64_t)gridDim.x * kPrepThreads) {
+    const int4 A = groups[kGrpRec * g];
+    const int4 Bq = groups[kGrpRec * g + 1];
+    if (dirty[g]) {   // mid = seg_b
+      groups[kGrpRec * g + 1].z = A.z;
+      groups[kGrpRec * g + 1].w = A.w;
+    } else {          // mid = seg_e
+      groups[kGrpRec * g + 1].z = Bq.x;
+      groups[kGrpRec * g + 1].w = Bq.y;
+    }
+  }
+}
+
 Raw raw_of(const ganon_dbatch *db) {
   const DevBatch &B = db->B;
   Raw R;
@@ -752,13 +948,31 @@ int launch_groups(ganon_ctx *ctx, ganon_dbatch *db, const Raw &R) {
     HIP_OR_FAIL(hipMemsetAsync(db->b_linemap.p, 0, (size_t)line_map_words(db) * 8, ctx->stream));
   hipLaunchKernelGGL(k_prep_groups, dim3(grid_for(std::max<int64_t>(db->n_scopes, kCursors))), dim3(kPrepThreads), 0,
                      ctx->stream, R, weight_of(db->group_target), (long long)db->group_target,
-                     static_cast<longlong2 *>(db->b_gs0.p), db->cursor);
+                     db->long_mode ? db->scost : nullptr, static_cast<longlong2 *>(db->b_gs0.p), db->cursor);
   return check_launch(ctx, "k_prep_groups");
 }
 
 int launch_emit(ganon_ctx *ctx, ganon_dbatch *db, const Raw &R, int write) {
   if (!db->n_groups) return GANON_OK;
   KernelScope ks(ctx, "prep_emit");
+  if (db->long_mode) {
+    const unsigned gg = grid_for(db->n_groups);
+    auto *dirty = static_cast<unsigned long long *>(db->b_slots.p);
+    auto *slot0 = static_cast<int64_t *>(db->b_slot0.p);
+    hipLaunchKernelGGL(k_prep_long_groups, dim3(gg), dim3(kPrepThreads), 0, ctx->stream, R,
+                       static_cast<const longlong2 *>(db->b_gs0.p), db->n_groups, (long long)db->region_per_incid,
+                       static_cast<const int32_t *>(db->b_nseg.p), static_cast<int4 *>(db->b_groups.p),
+                       static_cast<unsigned long long *>(db->b_lo.p), line_map(db), db->cursor, db->cursor + kCursors,
+                       dirty, slot0, write);
+    if (write) {
+      hipLaunchKernelGGL(k_prep_emit_waves, dim3(grid_for(db->n_incid * 64)), dim3(kPrepThreads), 0, ctx->stream, R,
+                         db->scost, (long long)db->group_target, static_cast<const longlong2 *>(db->b_gs0.p),
+                         db->ref->bad, db->ref->n_blk, slot0, dirty, static_cast<int4 *>(db->b_seg4.p));
+      hipLaunchKernelGGL(k_prep_long_mid, dim3(gg), dim3(kPrepThreads), 0, ctx->stream, db->n_groups, dirty,
+                         static_cast<int4 *>(db->b_groups.p));
+    }
+    return check_launch(ctx, "k_prep_emit (long)");
+  }
   hipLaunchKernelGGL(k_prep_emit, dim3((unsigned)db->n_groups), dim3(kPrepThreads), 0, ctx->stream, R,
                      static_cast<const longlong2 *>(db->b_gs0.p), db->n_groups, write, db->ref->bad, db->ref->n_blk,
                      (long long)db->region_per_incid, const_cast<int32_t *>(db->B.read_end),
@@ -815,10 +1029,12 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db, const int64_t *host_incid_off) {
   if ((rc = grow_n(ctx, db->b_cursor, 4 * kCursors, &db->cursor))) return rc;   // counters, then bases
   const Raw R = raw_of(db);
   HIP_OR_FAIL(hipMemsetAsync(db->err, 0, sizeof(PrepErr), st));
-  HIP_OR_FAIL(hipMemsetAsync(db->plan_info, 0, 4 * sizeof(unsigned long long), st));
+  HIP_OR_FAIL(hipMemsetAsync(db->plan_info, 0, 6 * sizeof(unsigned long long), st));
+  int32_t *nseg = nullptr;
+  if ((rc = grow_n(ctx, db->b_nseg, nr, &nseg))) return rc;
   HIP_OR_FAIL(hipMemsetAsync(seen, 0, (size_t)std::max<int64_t>(nr, 1), st));
   // 1. per-read and per-scope checks (every later kernel relies on them)
-  if (nr) hipLaunchKernelGGL(k_prep_reads, dim3(grid_for(nr)), dim3(kPrepThreads), 0, st, R, db->err, read_end,
+  if (nr) hipLaunchKernelGGL(k_prep_reads, dim3(grid_for(nr)), dim3(kPrepThreads), 0, st, R, db->err, read_end, nseg,
                              db->plan_info + 2);
   if (ns) hipLaunchKernelGGL(k_prep_scope_check, dim3(grid_for(ns)), dim3(kPrepThreads), 0, st, R, db->err,
                              db->plan_info + 1);
@@ -826,9 +1042,12 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db, const int64_t *host_incid_off) {
   {
     // overflow-region observations per incidence: the longest read's ceil(L / 48) (>= the round-1
     // bound of aligned bases / 48 per group)
-    unsigned long long max_len = 0;
+    unsigned long long max_len = 0, max_seg = 0;
     HIP_OR_FAIL(hipMemcpyAsync(&max_len, db->plan_info + 3, sizeof max_len, hipMemcpyDeviceToHost, st));
+    HIP_OR_FAIL(hipMemcpyAsync(&max_seg, db->plan_info + 4, sizeof max_seg, hipMemcpyDeviceToHost, st));
     HIP_OR_FAIL(hipStreamSynchronize(st));
+    db->long_mode = max_seg > 1 || ctx->prep_long == 1;
+    if (ctx->prep_long == 0) db->long_mode = false;
     db->region_per_incid = (int64_t)((max_len + 47) / 48);
     if ((double)db->n_incid * (double)db->region_per_incid > 4e9)
       return fail(ctx, GANON_E_ARG, "batch too large: %lld incidences of reads up to %llu bases (split it)",
@@ -842,7 +1061,30 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db, const int64_t *host_incid_off) {
   // 3. groups (their number follows from the host's CSR offsets), then a counting emit pass sizes
   //    the segment records and overflow regions
   const long long w = weight_of(db->group_target);
-  const int64_t ng = ns ? (host_incid_off[ns - 1] + w * (ns - 1)) / db->group_target + 1 : 0;
+  int64_t ng = ns ? (host_incid_off[ns - 1] + w * (ns - 1)) / db->group_target + 1 : 0;
+  db->scost = nullptr;
+  if (db->long_mode && ns) {
+    // groups cut on the prefix of segments per scope: cost[s] = segments of its incidences + w
+    int64_t *cost = nullptr;
+    if ((rc = grow_n(ctx, db->b_scost, (size_t)ns + 1, &cost))) return rc;
+    hipLaunchKernelGGL(k_prep_scope_cost, dim3(grid_for(ns + 1)), dim3(kPrepThreads), 0, st, R, nseg, w, cost);
+    if ((rc = check_launch(ctx, "k_prep_scope_cost"))) return rc;
+    size_t tb = 0;
+    HIP_OR_FAIL(rocprim::exclusive_scan(nullptr, tb, cost, cost, (int64_t)0, (size_t)ns + 1, rocprim::plus<int64_t>(), st));
+    void *tmp = nullptr;
+    if ((rc = grow_n(ctx, db->b_scan_tmp, tb, reinterpret_cast<uint8_t **>(&tmp)))) return rc;
+    HIP_OR_FAIL(rocprim::exclusive_scan(tmp, tb, cost, cost, (int64_t)0, (size_t)ns + 1, rocprim::plus<int64_t>(), st));
+    int64_t last = 0;
+    HIP_OR_FAIL(hipMemcpyAsync(&last, cost + ns - 1, sizeof last, hipMemcpyDeviceToHost, st));
+    HIP_OR_FAIL(hipStreamSynchronize(st));
+    db->scost = cost;
+    ng = last / db->group_target + 1;
+    unsigned long long *sl = nullptr;
+    int64_t *s0p = nullptr;
+    if ((rc = grow_n(ctx, db->b_slots, (size_t)ng, &sl)) ||
+        (rc = grow_n(ctx, db->b_slot0, (size_t)std::max<int64_t>(db->n_incid, 1), &s0p)))
+      return rc;
+  }
   if (ng > INT32_MAX / kGrpRec) return fail(ctx, GANON_E_ARG, "batch too large: %lld scope groups", (long long)ng);
   db->n_groups = (int32_t)ng;
   int32_t *p32 = nullptr;
@@ -859,7 +1101,7 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db, const int64_t *host_incid_off) {
   if ((rc = launch_groups(ctx, db, R)) || (rc = launch_emit(ctx, db, R, 0)) || (rc = launch_pieces(ctx, db))) return rc;
   if (ng && nr)
     hipLaunchKernelGGL(k_prep_farcap, dim3(grid_for(nr)), dim3(kPrepThreads), 0, st, R, w, (long long)db->group_target,
-                       static_cast<const int4 *>(db->b_groups.p), db->plan_info);
+                       db->long_mode ? db->scost : nullptr, static_cast<const int4 *>(db->b_groups.p), db->plan_info);
   if ((rc = check_launch(ctx, "k_prep_farcap"))) return rc;
   unsigned long long info[4] = {0, 0, 0, 0};
   std::vector<unsigned long long> cur(2 * kCursors, 0);

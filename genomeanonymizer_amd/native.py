@@ -183,6 +183,7 @@ PARAM_REF2 = 5           # include/ganon.h GANON_PARAM_REF2
 PARAM_FASTQ_SKIP = 6     # include/ganon.h GANON_PARAM_FASTQ_SKIP (phase timing only)
 PARAM_FASTQ_KD = 7       # include/ganon.h GANON_PARAM_FASTQ_KD
 PARAM_INDEL_SORT = 8     # include/ganon.h GANON_PARAM_INDEL_SORT (0 segmented, 1 global)
+PARAM_PREP_LONG = 9      # include/ganon.h GANON_PARAM_PREP_LONG (-1 auto, 0 never, 1 always; at upload)
 
 EXPORTED_HIP_SYMBOLS = (
     "ganon_ctx_create", "ganon_ctx_destroy", "ganon_last_error", "ganon_abi_version",

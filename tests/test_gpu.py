@@ -436,3 +436,60 @@ def test_hip_pipeline_matches_oracle_pipeline_on_random_scenarios(seed, tmp_path
     for k in outs["hip"]:
         assert outs["hip"][k] == outs["oracle"][k], k
     assert len(outs["hip"]["tumor.1.fastq"]) > 10_000
+
+
+@pytest.fixture(scope="module")
+def masker_long(hip_built):
+    """A context whose uploads always take the long-read prep (GANON_PARAM_PREP_LONG 1)."""
+    from genomeanonymizer_amd import native
+    m = native.HipMasker(0)
+    m.set_param(native.PARAM_PREP_LONG, 1)
+    yield m
+    m.close()
+
+
+@pytest.mark.parametrize("seed", [1, 3, 4, 8, 12])
+def test_long_prep_on_short_batches_matches_oracle(masker_long, oracle, seed):
+    """The long-read device prep (segment-weighted groups, one wave per incidence) forced on the
+    edge-case batches: every read and count equal to the oracle, as the default prep gives."""
+    from genomeanonymizer_amd.synth.batch import random_batch
+    kw = {"rare_frac": 0.3} if seed % 3 == 0 else {}
+    if seed % 4 == 0:
+        kw["wide_scopes"] = 4
+    arr = random_batch(seed, n_scopes=40, **kw)
+    o_out, o_calls, o_bases, o_tot = oracle.mask(arr)
+    in_batch = np.zeros(len(arr["read_len"]), bool)
+    in_batch[arr["incid_read"]] = True
+    out, calls, bases, tot = masker_long.mask(arr)
+    bad = [r for r in _all_reads_equal(arr, out, o_out) if in_batch[r] or arr["write_scope"][r] >= 0]
+    assert bad == []
+    assert np.array_equal(calls, o_calls) and np.array_equal(bases, o_bases)
+
+
+def test_long_prep_config2_matches_oracle(masker_long, oracle):
+    from genomeanonymizer_amd.synth.batch import config2_batch
+    arr, info = config2_batch(n_reads=400_000, genome=100_000_000, n_windows=40_000, n_germline=40_000)
+    o_out, o_calls, o_bases, _ = oracle.mask(arr)
+    out, calls, bases, tot = masker_long.mask(arr)
+    assert np.array_equal(calls, o_calls)
+    assert np.array_equal(bases, o_bases)
+    assert np.array_equal(out, o_out)
+
+
+def test_long_reads_c5_shape_groups_are_balanced(masker, oracle):
+    """C5-shaped batch (reads of thousands of CIGAR ops): the long-read prep cuts groups on
+    segments, so no group holds more than a few times the target, and results equal the oracle."""
+    from genomeanonymizer_amd.synth.batch import longread_batch
+    arr, info = longread_batch(7, n_reads=400)
+    o_out, o_calls, o_bases, _ = oracle.mask(arr)
+    db = masker.upload(arr)
+    try:
+        bi = db.info()
+        assert bi["groups"] * 512 >= bi["segments"] // 4, bi
+        db.run()
+        out, calls, bases, tot = db.download()
+    finally:
+        db.free()
+    assert np.array_equal(calls, o_calls)
+    assert np.array_equal(bases, o_bases)
+    assert np.array_equal(out, o_out)

@@ -1496,7 +1496,7 @@ GANON_API int ganon_ctx_set_param(ganon_ctx *ctx, int param, int value) {
     return GANON_OK;
   }
   if (param == GANON_PARAM_PREP_LONG) {
-    if (value < -1 || value > 1) return fail(ctx, GANON_E_ARG, "prep long mode: -1 (auto), 0 or 1");
+    if (value < -1 || value > 2) return fail(ctx, GANON_E_ARG, "prep mode: -1 (auto), 0 (two-pass), 1 (long), 2 (one-segment)");
     ctx->prep_long = value;
     return GANON_OK;
   }

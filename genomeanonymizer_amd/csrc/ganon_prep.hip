@@ -24,6 +24,10 @@
 //                   the others from the back (the group kernel reads the front part through the
 //                   2-bit reference); read_end; the lowest buffer offset of the reads the group
 //                   writes, per dataset (LDS atomicMin);
+//   k_prep_emit_flat (every read with at most one aligned segment: short reads, the default then):
+//                   thread per incidence, its one record at the slot of its own index — no count
+//                   pass, no scan, no allocation; a group is read through the 2-bit reference unless
+//                   one of its records touches a non-ACGT block;
 //   k_prep_emit_long (long-read mode, a read with more than one aligned segment in the batch):
 //                   groups cut on the segments-per-scope prefix computed at upload, the record count
 //                   from the segments per read, one wave per incidence over the whole batch walking
@@ -692,6 +696,116 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_emit(const Raw R, const l
   }
 }
 
+// ---- one-segment mode: every read of the batch has at most one aligned segment (short reads) ----
+// Each incidence owns exactly the slot of its own index, so the records need no count pass, no
+// scan and no allocation: thread per incidence, one CIGAR walk, one record (an incidence without a
+// segment, or in a huge scope, leaves a zero-length record the group kernel skips). A group whose
+// records all have an all-ACGT reference range is read through the 2-bit reference (clean part =
+// the whole range), any other group through the nt16 reference.
+__global__ void __launch_bounds__(kPrepThreads) k_prep_emit_flat(const Raw R, const longlong2 *__restrict__ gmeta,
+                                                                 int n_groups, const uint64_t *__restrict__ bad,
+                                                                 int64_t n_blk, long long region_per_incid,
+                                                                 int4 *__restrict__ seg4, int4 *__restrict__ groups,
+                                                                 unsigned long long *__restrict__ lo, LineMap M,
+                                                                 int write) {
+  __shared__ long long off[kGrpMaxScopes + 1];
+  __shared__ long long ref0[kGrpMaxScopes];
+  __shared__ int sstart[kGrpMaxScopes];
+  __shared__ uint8_t huge[kGrpMaxScopes];
+  __shared__ unsigned long long lmin[2];
+  __shared__ int s_dirty;
+  const int tid = threadIdx.x;
+  const int g = blockIdx.x;
+  const longlong2 m0 = gmeta[g];
+  const longlong2 m1 = g + 1 < n_groups ? gmeta[g + 1] : make_longlong2(R.n_scopes, R.n_incid);
+  const int s0 = (int)m0.x, s1 = (int)m1.x, ns = s1 - s0;
+  const long long i0 = m0.y, i1 = m1.y;
+  for (int t = tid; t <= ns; t += kPrepThreads) off[t] = R.incid_off[s0 + t];
+  for (int t = tid; t < ns; t += kPrepThreads) {
+    sstart[t] = R.span_start[s0 + t];
+    ref0[t] = R.ref_off[s0 + t] - R.span_start[s0 + t];
+    huge[t] = R.span_len[s0 + t] > kGrpMaxSpan;
+  }
+  if (tid < 2) lmin[tid] = kNone;
+  if (tid == 0) s_dirty = 0;
+  __syncthreads();
+  unsigned long long mn0 = kNone, mn1 = kNone;
+  bool dirty = false;
+  // two incidences per thread and trip, their loads issued together (the chain incidence -> read
+  // fields -> CIGAR -> reference block bitmap is latency bound)
+  for (long long base = i0; base < i1; base += 2 * kPrepThreads) {
+    EmitInc e[2];
+    int jj[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const long long i = base + tid + kPrepThreads * u;
+      e[u].r = i < i1 ? R.incid_read[i] : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int rr = e[u].r >= 0 ? e[u].r : 0;
+      e[u].cg = R.cigar + R.cig_off[rr];
+      e[u].ncig = e[u].r >= 0 ? R.n_cig[rr] : 0;
+      e[u].L = R.read_len[rr];
+      e[u].rs = R.ref_start[rr];
+      e[u].so = R.seq_off[rr];
+      e[u].ds = R.dataset[rr];
+      e[u].wsc = R.write_scope[rr];
+      jj[u] = lds_upper(off, ns, base + tid + kPrepThreads * u);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) e[u].w0 = e[u].ncig > 0 ? e[u].cg[0] : 0u;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (e[u].r < 0) continue;
+      const EmitInc &x = e[u];
+      const int j = jj[u];
+      const bool mine = x.wsc == s0 + j;
+      if (mine && x.L > 0) {
+        if (x.ds) mn1 = min(mn1, (unsigned long long)x.so);
+        else mn0 = min(mn0, (unsigned long long)x.so);
+      }
+      if (!write) continue;
+      int4 rec = make_int4(0, 0, 0, j);   // zero-length: no chunks
+      if (!huge[j]) {
+        const uint32_t fl = ((uint32_t)x.ds << 30) | (mine ? kSegMine : 0u);
+        const int64_t qnib = 2 * x.so, r0 = ref0[j];
+        const int ss = sstart[j];
+        walk_segments(x.cg, x.ncig, x.L, x.rs, x.w0, [&](int q, int p, int n) {
+          const uint64_t sq = (uint64_t)(qnib + q), rf = (uint64_t)(r0 + p);
+          const uint32_t z = (uint32_t)((sq >> 32) & 0xFF) | ((uint32_t)((rf >> 32) & 0xFF) << 8) | ((uint32_t)n << 16) | fl;
+          rec = make_int4((int)(uint32_t)sq, (int)(uint32_t)rf, (int)z, (int)((uint32_t)j | ((uint32_t)(p - ss) << 12)));
+          dirty |= !ref_clean(bad, n_blk, (int64_t)rf, n);
+        });
+      }
+      seg4[base + tid + kPrepThreads * u] = rec;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    mn0 = min(mn0, (unsigned long long)__shfl_xor(mn0, o));
+    mn1 = min(mn1, (unsigned long long)__shfl_xor(mn1, o));
+  }
+  if ((tid & 63) == 0) {
+    if (mn0 != kNone) atomicMin(&lmin[0], mn0);
+    if (mn1 != kNone) atomicMin(&lmin[1], mn1);
+  }
+  if (__any(dirty) && (tid & 63) == 0) s_dirty = 1;
+  __syncthreads();
+  if (tid < 2) {
+    lo[2 * (int64_t)g + tid] = lmin[tid];
+    if (lmin[tid] != kNone) map_mark(M, lmin[tid], (uint32_t)(2 * g + tid));
+  }
+  if (tid == 0) {
+    const int64_t seg_b = i0, seg_e = i1, mid = s_dirty ? seg_b : seg_e;
+    const int64_t region = i0 * region_per_incid + (int64_t)kGrpObs * g;
+    const int cap = (int)min((i1 - i0) * region_per_incid + kGrpObs, (long long)(INT32_MAX / 2));
+    groups[kGrpRec * (int64_t)g] = make_int4(s0, s1, (int)(uint32_t)seg_b, (int)(uint32_t)((uint64_t)seg_b >> 32));
+    groups[kGrpRec * (int64_t)g + 1] = make_int4((int)(uint32_t)seg_e, (int)(uint32_t)((uint64_t)seg_e >> 32),
+                                                 (int)(uint32_t)mid, (int)(uint32_t)((uint64_t)mid >> 32));
+    groups[kGrpRec * (int64_t)g + 3] = make_int4((int)(uint32_t)region, (int)(uint32_t)((uint64_t)region >> 32), cap, 0);
+  }
+}
+
 // ---- long-read mode: one wave per incidence ---------------------------------------------------
 // A read with thousands of CIGAR ops (long reads with indel errors) walked by one thread is a
 // serial chain of dependent loads; here a wave walks it 64 ops at a time: per-lane query / reference
@@ -973,6 +1087,14 @@ int launch_emit(ganon_ctx *ctx, ganon_dbatch *db, const Raw &R, int write) {
     }
     return check_launch(ctx, "k_prep_emit (long)");
   }
+  if (db->flat_mode) {
+    hipLaunchKernelGGL(k_prep_emit_flat, dim3((unsigned)db->n_groups), dim3(kPrepThreads), 0, ctx->stream, R,
+                       static_cast<const longlong2 *>(db->b_gs0.p), db->n_groups, db->ref->bad, db->ref->n_blk,
+                       (long long)db->region_per_incid, static_cast<int4 *>(db->b_seg4.p),
+                       static_cast<int4 *>(db->b_groups.p), static_cast<unsigned long long *>(db->b_lo.p), line_map(db),
+                       write);
+    return check_launch(ctx, "k_prep_emit_flat");
+  }
   hipLaunchKernelGGL(k_prep_emit, dim3((unsigned)db->n_groups), dim3(kPrepThreads), 0, ctx->stream, R,
                      static_cast<const longlong2 *>(db->b_gs0.p), db->n_groups, write, db->ref->bad, db->ref->n_blk,
                      (long long)db->region_per_incid, const_cast<int32_t *>(db->B.read_end),
@@ -1046,8 +1168,10 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db, const int64_t *host_incid_off) {
     HIP_OR_FAIL(hipMemcpyAsync(&max_len, db->plan_info + 3, sizeof max_len, hipMemcpyDeviceToHost, st));
     HIP_OR_FAIL(hipMemcpyAsync(&max_seg, db->plan_info + 4, sizeof max_seg, hipMemcpyDeviceToHost, st));
     HIP_OR_FAIL(hipStreamSynchronize(st));
-    db->long_mode = max_seg > 1 || ctx->prep_long == 1;
-    if (ctx->prep_long == 0) db->long_mode = false;
+    // prep mode: long (a read with several segments, or forced), one-segment (every read has at most
+    // one: the default for short reads), or the two-pass short emit (GANON_PARAM_PREP_LONG 0)
+    db->long_mode = ctx->prep_long == 1 || (ctx->prep_long != 0 && max_seg > 1);
+    db->flat_mode = !db->long_mode && max_seg <= 1 && (ctx->prep_long == -1 || ctx->prep_long == 2);
     db->region_per_incid = (int64_t)((max_len + 47) / 48);
     if ((double)db->n_incid * (double)db->region_per_incid > 4e9)
       return fail(ctx, GANON_E_ARG, "batch too large: %lld incidences of reads up to %llu bases (split it)",

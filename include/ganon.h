@@ -128,9 +128,11 @@ GANON_API int ganon_ctx_set_variant(ganon_ctx *ctx, int variant);
  * GANON_PARAM_INDEL_SORT: the indel tally keeps only observations at positions where two or more
  * reads have an I/D op and sorts them per scope (0, default: segmented, 32-bit position keys), or
  * sorts every observation in one global sort of 64-bit scope|position keys (1). Same records.
- * GANON_PARAM_PREP_LONG (read at upload): the long-read device prep — groups cut on the prefix of
- * aligned segments per scope, one wave per incidence walking its CIGAR — is used when a read of the
- * batch has more than one segment (-1, default), always (1) or never (0). Same results. */
+ * GANON_PARAM_PREP_LONG (read at upload): which device prep builds the segment records. -1 (default):
+ * the long-read prep (groups cut on the prefix of aligned segments per scope, one wave per incidence
+ * walking its CIGAR) when a read of the batch has more than one segment, else the one-segment prep
+ * (one record per incidence at its own index); 1: always the long-read prep; 2: the one-segment prep
+ * when it applies; 0: the two-pass per-group emit. Same results. */
 enum { GANON_PARAM_GROUP_UNROLL = 1, GANON_PARAM_GROUP_SKIP = 2, GANON_PARAM_GROUP_TARGET = 3,
        GANON_PARAM_NT_COPY = 4, GANON_PARAM_REF2 = 5, GANON_PARAM_FASTQ_SKIP = 6, GANON_PARAM_FASTQ_KD = 7,
        GANON_PARAM_INDEL_SORT = 8, GANON_PARAM_PREP_LONG = 9 };

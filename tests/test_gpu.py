@@ -493,3 +493,31 @@ def test_long_reads_c5_shape_groups_are_balanced(masker, oracle):
     assert np.array_equal(calls, o_calls)
     assert np.array_equal(bases, o_bases)
     assert np.array_equal(out, o_out)
+
+
+@pytest.fixture(scope="module")
+def masker_twopass(hip_built):
+    """A context whose uploads take the two-pass per-group emit (GANON_PARAM_PREP_LONG 0)."""
+    from genomeanonymizer_amd import native
+    m = native.HipMasker(0)
+    m.set_param(native.PARAM_PREP_LONG, 0)
+    yield m
+    m.close()
+
+
+@pytest.mark.parametrize("seed", [2, 3, 4, 9])
+def test_two_pass_prep_matches_oracle(masker_twopass, oracle, seed):
+    """The default short-read prep is the one-segment emit; the two-pass emit stays selectable and
+    exact."""
+    from genomeanonymizer_amd.synth.batch import random_batch
+    kw = {"rare_frac": 0.3} if seed % 3 == 0 else {}
+    if seed % 4 == 0:
+        kw["wide_scopes"] = 4
+    arr = random_batch(seed, n_scopes=40, **kw)
+    o_out, o_calls, o_bases, _ = oracle.mask(arr)
+    in_batch = np.zeros(len(arr["read_len"]), bool)
+    in_batch[arr["incid_read"]] = True
+    out, calls, bases, tot = masker_twopass.mask(arr)
+    bad = [r for r in _all_reads_equal(arr, out, o_out) if in_batch[r] or arr["write_scope"][r] >= 0]
+    assert bad == []
+    assert np.array_equal(calls, o_calls) and np.array_equal(bases, o_bases)

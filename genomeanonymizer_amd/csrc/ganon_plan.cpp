@@ -70,6 +70,11 @@ struct Table {
 struct PairSlot {
   Inst p[2];
   bool has[2] = {false, false};
+  // the stored object met another of its read's objects (add_or_update_anonymized_read_from_other,
+  // AM:351-389): update_anonymized_read_from_other re-sets its left-over flag (AM:281-287), so the
+  // left-overs it already applied at its scope's end (AM:521-532) are applied once more when the
+  // pair is written from to_pair (SR:353-357) or as a single end (SR:615-616)
+  bool upd[2] = {false, false};
   uint64_t seq = 0;   // insertion order (dict order: a deleted key re-inserted goes last)
 };
 
@@ -114,9 +119,11 @@ class Planner {
     for (const auto &kv : to_pair_) rest.emplace_back(kv.second.seq, &kv.second);
     std::sort(rest.begin(), rest.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
     for (const auto &e : rest) {
-      const Inst &i = e.second->has[0] ? e.second->p[0] : e.second->p[1];
+      const int sl = e.second->has[0] ? 0 : 1;
+      const Inst &i = e.second->p[sl];
       single_[i.ds].push_back(i.row);
       single_[i.ds].push_back(i.scope);
+      single_[i.ds].push_back(e.second->upd[sl] ? 1 : 0);
     }
     write_single_end_ = !to_pair_.empty();
   }
@@ -124,12 +131,12 @@ class Planner {
   // results
   std::vector<ScopeRec> scopes_;
   std::vector<int64_t> t_rows_, n_rows_;
-  std::vector<int32_t> events_;       // 7 per event: kind, hid, ds, slot, inst ds, inst scope, 0
+  std::vector<int32_t> events_;       // 7 per event: kind, hid, ds, slot, inst ds, inst scope, reapply (write) / clock
   std::vector<int64_t> event_rows_;   // inst row per event (write) or -1
   std::vector<int32_t> stats_;        // 2 per event: kind (0 window, 1 outside, 2 scope), value
-  std::vector<int64_t> single_[2];    // (row, scope) pairs
+  std::vector<int64_t> single_[2];    // (row, scope, reapply) triples
   bool write_single_end_ = false;
-  std::vector<int64_t> left_;         // contig mode: 9 per unwritten pair (include/ganon_host.h)
+  std::vector<int64_t> left_;         // contig mode: 11 per unwritten pair (include/ganon_host.h)
   std::vector<int64_t> cand_;         // contig mode: 5 per pair_unmapped_mates candidate
 
  private:
@@ -295,8 +302,8 @@ class Planner {
     events_.insert(events_.end(), {2, h, 0, 0, 0, 0, 0});
     event_rows_.push_back(-1);
   }
-  void log_write(int32_t h, int ds, int sl, const Inst &i) {
-    events_.insert(events_.end(), {1, h, ds, sl, i.ds, i.scope, 0});
+  void log_write(int32_t h, int ds, int sl, const Inst &i, bool reapply) {
+    events_.insert(events_.end(), {1, h, ds, sl, i.ds, i.scope, reapply ? 1 : 0});
     event_rows_.push_back(i.row);
   }
 
@@ -309,14 +316,16 @@ class Planner {
     event_rows_.push_back(i.row);
   }
 
-  void write_pair(const Inst &i0, const Inst &i1, int32_t hid) {
+  void write_pair(const Inst &i0, const Inst &i1, int32_t hid, bool r0 = false, bool r1 = false) {
     const int64_t name = nid_[i0.ds][(size_t)i0.row];
     if (!written_.insert(name).second) return;
-    log_write(hid, i0.ds, 0, i0);
-    log_write(hid, i0.ds, 1, i1);
+    log_write(hid, i0.ds, 0, i0, r0);
+    log_write(hid, i0.ds, 1, i1, r1);
   }
 
-  PairSlot &store_first(const Inst &inst) {
+  // update: the consumer of a scope's yields (add_or_update_anonymized_read_from_other) rather
+  // than a pass-through (add_anonymized_read_pair_to_collection_from_alignment)
+  PairSlot &store_first(const Inst &inst, bool update = false) {
     const int64_t name = nid_[inst.ds][(size_t)inst.row];
     const int sl = slot(inst.ds, inst.row);
     auto it = to_pair_.find(name);
@@ -328,6 +337,8 @@ class Planner {
     if (!p.has[sl]) {
       p.p[sl] = inst;
       p.has[sl] = true;
+    } else if (update) {
+      p.upd[sl] = true;
     }
     return p;
   }
@@ -341,7 +352,7 @@ class Planner {
       return;
     }
     PairSlot &p = store_first(inst);
-    if (p.has[0] && p.has[1]) write_pair(p.p[0], p.p[1], hid);
+    if (p.has[0] && p.has[1]) write_pair(p.p[0], p.p[1], hid, p.upd[0], p.upd[1]);
   }
 
   // ---- scopes ----
@@ -507,12 +518,12 @@ class Planner {
         placeholder(4, hid, p.has[0] ? 0 : 1, inst);
         continue;
       }
-      store_first(inst);
+      store_first(inst, true);
       const int64_t name = nid_[inst.ds][(size_t)inst.row];
       auto it = to_pair_.find(name);
       if (it->second.has[0] && it->second.has[1]) {
         const Inst a = it->second.p[0], b = it->second.p[1];
-        write_pair(a, b, hid);
+        write_pair(a, b, hid, it->second.upd[0], it->second.upd[1]);
         to_pair_.erase(it);
       }
     }
@@ -667,6 +678,8 @@ class Planner {
         left_.push_back(p.has[s] ? p.p[s].scope : 0);
         left_.push_back(p.has[s] ? p.p[s].row : 0);
       }
+      left_.push_back(p.upd[0] ? 1 : 0);
+      left_.push_back(p.upd[1] ? 1 : 0);
     }
     // placed-unmapped records of this contig's windows whose names may still be unpaired at the end
     std::vector<int64_t> rows;
@@ -806,11 +819,11 @@ GANON_HOST_API int ganon_plan_view_get(const ganon_plan *pl, ganon_plan_view *v)
   v->n_stats = (int64_t)p.stats_.size() / 2;
   v->stats = p.stats_.data();
   for (int d = 0; d < 2; ++d) {
-    v->n_single[d] = (int64_t)p.single_[d].size() / 2;
+    v->n_single[d] = (int64_t)p.single_[d].size() / 3;
     v->single[d] = p.single_[d].data();
   }
   v->write_single_end = p.write_single_end_ ? 1 : 0;
-  v->n_left = (int64_t)p.left_.size() / 9;
+  v->n_left = (int64_t)p.left_.size() / 11;
   v->left = p.left_.data();
   v->n_cand = (int64_t)p.cand_.size() / 5;
   v->cand = p.cand_.data();
@@ -837,6 +850,7 @@ struct RInst {
 struct RSlot {
   RInst p[2];
   bool has[2] = {false, false};
+  bool upd[2] = {false, false};   // PairSlot::upd
   int64_t seq = 0;   // (job << 32) | clock of the last insertion (dict order)
 };
 
@@ -846,7 +860,7 @@ struct ganon_resolver {
   std::unordered_map<std::string, RSlot> to_pair;
   std::unordered_set<std::string> written;
 
-  RSlot &store_first(const std::string &name, int slot, const RInst &i, int64_t seq) {
+  RSlot &store_first(const std::string &name, int slot, const RInst &i, int64_t seq, bool update = false) {
     auto it = to_pair.find(name);
     if (it == to_pair.end()) {
       it = to_pair.emplace(name, RSlot{}).first;
@@ -856,21 +870,26 @@ struct ganon_resolver {
     if (!p.has[slot]) {
       p.p[slot] = i;
       p.has[slot] = true;
+    } else if (update) {
+      p.upd[slot] = true;
     }
     return p;
   }
   // write_pair (SR:134-165): both records to the first instance's dataset files, once per name
-  int write_pair(const std::string &name, const RInst &a, const RInst &b, int64_t *w) {
+  int write_pair(const std::string &name, const RInst &a, const RInst &b, int64_t *w, bool ra = false,
+                 bool rb = false) {
     if (!written.insert(name).second) return 0;
     const RInst *ab[2] = {&a, &b};
+    const bool re[2] = {ra, rb};
     for (int s = 0; s < 2; ++s) {
-      int64_t *o = w + 6 * s;
+      int64_t *o = w + 7 * s;
       o[0] = a.ds;
       o[1] = s;
       o[2] = ab[s]->job;
       o[3] = ab[s]->ds;
       o[4] = ab[s]->scope;
       o[5] = ab[s]->row;
+      o[6] = re[s] ? 1 : 0;
     }
     return 2;
   }
@@ -912,7 +931,7 @@ GANON_HOST_API int ganon_resolver_contig(ganon_resolver *r, int32_t job, int64_t
           return GANON_PLAN_E_ARG;
         }
         const RInst other{job, ops[7 * (i + 1) + 4], ops[7 * (i + 1) + 5], op_rows[i + 1]};
-        out_n[i] = r->write_pair(name, inst, other, out_w + 12 * i);
+        out_n[i] = r->write_pair(name, inst, other, out_w + 14 * i);
         out_n[i + 1] = 0;
         ++i;
         continue;
@@ -921,18 +940,21 @@ GANON_HOST_API int ganon_resolver_contig(ganon_resolver *r, int32_t job, int64_t
         g_err = "resolver: not a placeholder event";
         return GANON_PLAN_E_ARG;
       }
-      RSlot &p = r->store_first(name, e[3], inst, base | (int64_t)(uint32_t)e[6]);
+      RSlot &p = r->store_first(name, e[3], inst, base | (int64_t)(uint32_t)e[6], e[0] == 4);
       if (p.has[0] && p.has[1]) {
         const RInst a = p.p[0], b = p.p[1];
-        out_n[i] = r->write_pair(name, a, b, out_w + 12 * i);
+        out_n[i] = r->write_pair(name, a, b, out_w + 14 * i, p.upd[0], p.upd[1]);
         if (e[0] == 4) r->to_pair.erase(name);   // anonymize_window pops a written pair (SR:360)
       }
     }
     for (int64_t k = 0; k < n_left; ++k) {
-      const int64_t *l = left + 9 * k;
+      const int64_t *l = left + 11 * k;
       const std::string name(left_names + left_name_off[k], (size_t)left_name_len[k]);
       for (int s = 0; s < 2; ++s)
-        if (l[1 + 4 * s]) r->store_first(name, s, RInst{job, l[2 + 4 * s], l[3 + 4 * s], l[4 + 4 * s]}, base | l[0]);
+        if (l[1 + 4 * s]) {
+          RSlot &p = r->store_first(name, s, RInst{job, l[2 + 4 * s], l[3 + 4 * s], l[4 + 4 * s]}, base | l[0]);
+          if (l[9 + s]) p.upd[s] = true;
+        }
     }
   } catch (const std::bad_alloc &) {
     g_err = "out of memory";
@@ -991,7 +1013,7 @@ GANON_HOST_API int ganon_resolver_finish(ganon_resolver *r, int64_t n_cand, cons
       RSlot &p = r->store_first(name, (int)c[4], RInst{c[0], c[2], -1, c[3]}, INT64_MAX);
       if (p.has[0] && p.has[1]) {
         const RInst a = p.p[0], b = p.p[1];
-        *n_tail += r->write_pair(name, a, b, tail + 6 * *n_tail);
+        *n_tail += r->write_pair(name, a, b, tail + 7 * *n_tail, p.upd[0], p.upd[1]);
       }
     }
   }
@@ -1001,12 +1023,14 @@ GANON_HOST_API int ganon_resolver_finish(ganon_resolver *r, int64_t n_cand, cons
   std::stable_sort(rest.begin(), rest.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
   n_single[0] = n_single[1] = 0;
   for (const auto &e : rest) {
-    const RInst &i = e.second->has[0] ? e.second->p[0] : e.second->p[1];
-    int64_t *dst = (i.ds == 0 ? single0 : single1) + 4 * n_single[i.ds];
+    const int sl = e.second->has[0] ? 0 : 1;
+    const RInst &i = e.second->p[sl];
+    int64_t *dst = (i.ds == 0 ? single0 : single1) + 5 * n_single[i.ds];
     dst[0] = i.job;
     dst[1] = i.ds;
     dst[2] = i.scope;
     dst[3] = i.row;
+    dst[4] = e.second->upd[sl] ? 1 : 0;
     ++n_single[i.ds];
   }
   *write_single_end = r->to_pair.empty() ? 0 : 1;

@@ -706,9 +706,9 @@ def plan_sample(tables, contig_names, contig_lens, win_contig, win_first, win_la
         out["events"] = _np_copy(v.events, 7 * ne, np.int32).reshape(ne, 7)
         out["event_rows"] = _np_copy(v.event_rows, ne, np.int64)
         out["stats"] = _np_copy(v.stats, 2 * int(v.n_stats), np.int32).reshape(-1, 2)
-        out["single"] = [_np_copy(v.single[d], 2 * int(v.n_single[d]), np.int64).reshape(-1, 2) for d in (0, 1)]
+        out["single"] = [_np_copy(v.single[d], 3 * int(v.n_single[d]), np.int64).reshape(-1, 3) for d in (0, 1)]
         out["write_single_end"] = bool(v.write_single_end)
-        out["left"] = _np_copy(v.left, 9 * int(v.n_left), np.int64).reshape(-1, 9)
+        out["left"] = _np_copy(v.left, 11 * int(v.n_left), np.int64).reshape(-1, 11)
         out["cand"] = _np_copy(v.cand, 5 * int(v.n_cand), np.int64).reshape(-1, 5)
     finally:
         lib.ganon_plan_free(h)
@@ -746,14 +746,14 @@ class Resolver:
 
     def contig(self, job: int, ops: np.ndarray, op_rows: np.ndarray, op_names: list, left: np.ndarray,
                left_names: list):
-        """Returns (n_writes per op, writes [n_ops, 2, 6])."""
+        """Returns (n_writes per op, writes [n_ops, 2, 7])."""
         keep = []
         ops = np.ascontiguousarray(ops, np.int32).reshape(-1, 7)
         rows = np.ascontiguousarray(op_rows, np.int64)
-        left = np.ascontiguousarray(left, np.int64).reshape(-1, 9)
+        left = np.ascontiguousarray(left, np.int64).reshape(-1, 11)
         n = len(ops)
         out_n = np.zeros(max(n, 1), np.int32)
-        out_w = np.zeros((max(n, 1), 2, 6), np.int64)
+        out_w = np.zeros((max(n, 1), 2, 7), np.int64)
         on, oo, ol = _names_args(op_names, keep)
         ln, lo, ll = _names_args(left_names, keep)
         rc = self._lib.ganon_resolver_contig(self._h, int(job), n, ops.ctypes.data_as(_i32p), rows.ctypes.data_as(_i64p),
@@ -770,14 +770,14 @@ class Resolver:
         return out[:k]
 
     def finish(self, cand: np.ndarray, names: list):
-        """Returns (tail writes [n, 6], single ends per dataset [m, 4] (job, ds, scope, row),
-        write_single_end)."""
+        """Returns (tail writes [n, 7], single ends per dataset [m, 5] (job, ds, scope, row,
+        reapply), write_single_end)."""
         keep = []
         cand = np.ascontiguousarray(cand, np.int64).reshape(-1, 7)
         n_pend = self._lib.ganon_resolver_pending(self._h, None, 0)
-        tail = np.zeros((max(2 * len(cand), 1), 6), np.int64)
-        s0 = np.zeros((max(n_pend, 1), 4), np.int64)
-        s1 = np.zeros((max(n_pend, 1), 4), np.int64)
+        tail = np.zeros((max(2 * len(cand), 1), 7), np.int64)
+        s0 = np.zeros((max(n_pend, 1), 5), np.int64)
+        s1 = np.zeros((max(n_pend, 1), 5), np.int64)
         n_tail = C.c_int64(0)
         n_single = np.zeros(2, np.int64)
         wse = C.c_int32(0)

@@ -151,10 +151,13 @@ class Plan:
 
     def __init__(self, scopes: List[Scope], io_log: Optional[List[tuple]], single_end: Dict[int, List[Instance]],
                  stats_events: List[Tuple[str, object]], write_single_end: bool,
-                 events: Optional[np.ndarray] = None, event_rows: Optional[np.ndarray] = None):
+                 events: Optional[np.ndarray] = None, event_rows: Optional[np.ndarray] = None,
+                 single_reapply: Optional[Dict[int, List[int]]] = None):
         self.scopes = scopes
         self._io_log = io_log
         self.single_end = single_end
+        # per single end: 1 when its left-overs are applied a second time (PairSlot::upd, ganon_plan.cpp)
+        self.single_reapply = single_reapply or {d: [0] * len(single_end[d]) for d in (0, 1)}
         self.stats_events = stats_events
         self.write_single_end = write_single_end
         self._events = events
@@ -162,12 +165,12 @@ class Plan:
 
     @property
     def io_log(self) -> List[tuple]:
-        # ('open', hid) | ('write', hid, dataset, slot, Instance) | ('close', hid)
+        # ('open', hid) | ('write', hid, dataset, slot, Instance, reapply) | ('close', hid)
         if self._io_log is None:
             log = []
             for e, r in zip(self._events.tolist(), self._event_rows.tolist()):
                 if e[0] == 1:
-                    log.append(("write", e[1], e[2], e[3], (e[4], r, e[5])))
+                    log.append(("write", e[1], e[2], e[3], (e[4], r, e[5]), e[6]))
                 elif e[0] == 0:
                     log.append(("open", e[1]))
                 else:
@@ -182,7 +185,7 @@ class Plan:
             rows = np.full(n, -1, np.int64)
             for i, e in enumerate(self._io_log):
                 if e[0] == "write":
-                    ev[i, :6] = (1, e[1], e[2], e[3], e[4][0], e[4][2])
+                    ev[i, :7] = (1, e[1], e[2], e[3], e[4][0], e[4][2], e[5] if len(e) > 5 else 0)
                     rows[i] = e[4][1]
                 else:
                     ev[i, :2] = (0 if e[0] == "open" else 2, e[1])
@@ -279,24 +282,30 @@ class SamplePlanner:
     def _close(self, hid: int) -> None:
         self.io_log.append(("close", hid))
 
-    def write_pair(self, i0: Instance, i1: Instance, hid: int) -> None:
+    def write_pair(self, i0: Instance, i1: Instance, hid: int, r0: int = 0, r1: int = 0) -> None:
         name = self.name(i0[0], i0[1])
         if name in self.written:
             return
         self.written.add(name)
         ds = i0[0]
-        self.io_log.append(("write", hid, ds, 0, i0))
-        self.io_log.append(("write", hid, ds, 1, i1))
+        self.io_log.append(("write", hid, ds, 0, i0, r0))
+        self.io_log.append(("write", hid, ds, 1, i1, r1))
 
-    def _store_first(self, inst: Instance) -> List[Optional[Instance]]:
+    def _store_first(self, inst: Instance, update: bool = False) -> List[Optional[Instance]]:
+        """to_pair store; ``update``: from a scope's consumer (add_or_update_anonymized_read_from_other,
+        AM:351-389), whose update_anonymized_read_from_other re-sets the stored object's left-over
+        flag (AM:281-287): its already-applied left-overs are applied once more when it is written
+        from to_pair or as a single end. pair = [inst0, inst1, reapply0, reapply1]."""
         name = self.name(inst[0], inst[1])
         slot = self.slot(inst[0], inst[1])
         pair = self.to_pair.get(name)
         if pair is None:
-            pair = [None, None]
+            pair = [None, None, 0, 0]
             self.to_pair[name] = pair
         if pair[slot] is None:
             pair[slot] = inst
+        elif update:
+            pair[2 + slot] = 1
         return pair
 
     def passthrough(self, ds: int, row: int, hid: int) -> None:
@@ -307,7 +316,7 @@ class SamplePlanner:
             raise TypeError(f"read {t.names[row]!r} has no SEQ; the reference cannot upper-case it")
         pair = self._store_first((ds, row, -1))
         if pair[0] is not None and pair[1] is not None:
-            self.write_pair(pair[0], pair[1], hid)
+            self.write_pair(pair[0], pair[1], hid, pair[2], pair[3])
 
     # ---- scopes ------------------------------------------------------------------------------
     def _pileup_reads(self, ds: int, contig: str, first: int, last: int) -> np.ndarray:
@@ -401,11 +410,11 @@ class SamplePlanner:
             name = None
             for inst in (p0, p1):
                 if inst is not None:
-                    self._store_first(inst)
+                    self._store_first(inst, update=True)
                     name = self.name(inst[0], inst[1])
             upd = self.to_pair[name]
             if upd[0] is not None and upd[1] is not None:
-                self.write_pair(upd[0], upd[1], hid)
+                self.write_pair(upd[0], upd[1], hid, upd[2], upd[3])
                 del self.to_pair[name]
         self._close(hid)
 
@@ -555,10 +564,13 @@ class SamplePlanner:
         for k in self.written:
             self.to_pair.pop(k, None)
         single: Dict[int, List[Instance]] = {0: [], 1: []}
+        reapply: Dict[int, List[int]] = {0: [], 1: []}
         for name, pair in self.to_pair.items():
-            inst = pair[0] if pair[0] is not None else pair[1]
+            sl = 0 if pair[0] is not None else 1
+            inst = pair[sl]
             single[inst[0]].append(inst)
-        return Plan(self.scopes, self.io_log, single, self.stats_events, bool(self.to_pair))
+            reapply[inst[0]].append(pair[2 + sl])
+        return Plan(self.scopes, self.io_log, single, self.stats_events, bool(self.to_pair), single_reapply=reapply)
 
 
 class NativeSamplePlanner(SamplePlanner):
@@ -597,8 +609,9 @@ class NativeSamplePlanner(SamplePlanner):
                 self.stats_events.append(("outside", None))
             else:
                 self.stats_events.append(("scope", val))
-        single = {d: [(d, r, s) for r, s in res["single"][d].tolist()] for d in (0, 1)}
-        return Plan(self.scopes, None, single, self.stats_events, res["write_single_end"],
+        single = {d: [(d, r, s) for r, s, _ in res["single"][d].tolist()] for d in (0, 1)}
+        reapply = {d: [x for _, _, x in res["single"][d].tolist()] for d in (0, 1)}
+        return Plan(self.scopes, None, single, self.stats_events, res["write_single_end"], single_reapply=reapply,
                     events=res["events"], event_rows=res["event_rows"])
 
 

@@ -41,7 +41,7 @@ from .planner import ContigPlanner, Plan, Window, UnsupportedInput
 from . import writer as _writer
 from .writer import OUTSIDE_WINDOWS, FastqFormatter, statistics_rows, write_statistics
 
-Key = Tuple[int, int, int, int]   # (job, dataset, scope, row)
+Key = Tuple[int, int, int, int, int]   # (job, dataset, scope, row, reapply)
 
 
 def _names(table: ReadTable, rows: np.ndarray) -> List[bytes]:
@@ -82,7 +82,6 @@ class Job:
         self.res: MaskResult = anonymizer.anonymize(planner, self.plan, written=written)
         t3 = time.time()
         self.fmt = FastqFormatter(self.tables, self.res, anonymizer.format_fastq)
-        self.fmt.edited = {inst: self.fmt._edited(inst, e) for inst, e in self.res.leftovers.items()}
         self.timing = {"decode_s": t1 - t0, "plan_s": t2 - t1, "mask_s": t3 - t2}
 
     # -- which masked copy of each read the device produces --------------------------------------
@@ -122,33 +121,17 @@ class Job:
                 "(mate fields that disagree with where its records are)")
 
     # -- exports for the resolution ---------------------------------------------------------------
-    def record_lengths(self, ds: np.ndarray, row: np.ndarray, sc: np.ndarray) -> np.ndarray:
-        T, N = self.tables
-        ds = np.asarray(ds, np.int64)
-        row = np.asarray(row, np.int64)
-        r0, r1 = np.where(ds == 0, row, 0), np.where(ds == 1, row, 0)
-        nl = np.where(ds == 0, T.name_len[r0], N.name_len[r1]).astype(np.int64)
-        ls = np.where(ds == 0, T.l_seq[r0], N.l_seq[r1]).astype(np.int64)
-        out = nl + 8 + 2 * ls
-        if self.fmt.edited and len(ds):
-            keys = FastqFormatter._key(ds, row, np.asarray(sc, np.int64))
-            ek = FastqFormatter._key(*zip(*self.fmt.edited.keys()))
-            el = np.array([len(b) for b in self.fmt.edited.values()], np.int64)
-            o = np.argsort(ek)
-            ek, el = ek[o], el[o]
-            j = np.minimum(np.searchsorted(ek, keys), len(ek) - 1)
-            hit = ek[j] == keys
-            out[hit] = el[j[hit]]
-        return out
+    def record_lengths(self, ds, row, sc, reapply=None) -> np.ndarray:
+        return self.fmt.record_lengths(ds, row, sc, reapply)
 
-    def format_records(self, ds, row, sc) -> List[bytes]:
+    def format_records(self, ds, row, sc, reapply=None) -> List[bytes]:
         ds = np.asarray(ds, np.int64)
         row = np.asarray(row, np.int64)
         sc = np.asarray(sc, np.int64)
         if len(ds) == 0:
             return []
-        data = self.fmt.format_arrays(ds, row, sc)
-        off = np.concatenate([[0], np.cumsum(self.record_lengths(ds, row, sc))])
+        data = self.fmt.format_arrays(ds, row, sc, reapply)
+        off = np.concatenate([[0], np.cumsum(self.record_lengths(ds, row, sc, reapply))])
         return [data[off[i]:off[i + 1]] for i in range(len(ds))]
 
     def exports(self) -> dict:
@@ -188,7 +171,10 @@ class Job:
             first = first[ok] if len(first) else first
             recs = self.format_records(ds[first], rw[first], sc[first])
             for i, b in zip(first.tolist(), recs):
-                carry[(self.job, int(ds[i]), int(sc[i]), int(rw[i]))] = b
+                inst = (int(ds[i]), int(rw[i]), int(sc[i]))
+                carry[(self.job, inst[0], inst[2], inst[1], 0)] = b
+                if inst in self.res.leftovers:   # written later with its left-overs applied twice
+                    carry[(self.job, inst[0], inst[2], inst[1], 1)] = self.fmt.edited_bytes(inst, 1)
         return {
             "job": self.job, "ops": ops, "op_rows": op_rows,
             "op_names": _names_ds(self.tables, op_ds, op_rows),
@@ -223,10 +209,12 @@ class Job:
             fin[ph_pos, 3] = w[:, 1]
             fin[ph_pos, 4] = w[:, 3]
             fin[ph_pos, 5] = w[:, 4]
-            fin[ph_pos, 6] = 0
+            fin[ph_pos, 6] = w[:, 6]
             frow[ph_pos] = w[:, 5]
             fjob[ph_pos] = w[:, 2]
         wr = fin[:, 0] == 1
+        fin[~wr, 6] = 0
+        reap = fin[:, 6].astype(np.int64)
         ext = wr & (fjob != self.job)
         loc = wr & ~ext
         chk = np.nonzero(loc & (fin[:, 5] >= 0))[0]
@@ -240,10 +228,12 @@ class Job:
                 self.check_instance(int(fin[i, 4]), int(frow[i]), int(fin[i, 5]))
         rec_len = np.zeros(nf, np.int64)
         li = np.nonzero(loc)[0]
-        rec_len[li] = self.record_lengths(fin[li, 4], frow[li], fin[li, 5])
+        rec_len[li] = self.record_lengths(fin[li, 4], frow[li], fin[li, 5], reap[li])
         ext_bytes: Dict[int, bytes] = {}
         for i in np.nonzero(ext)[0].tolist():
-            b = carry.get((int(fjob[i]), int(fin[i, 4]), int(fin[i, 5]), int(frow[i])))
+            b = carry.get((int(fjob[i]), int(fin[i, 4]), int(fin[i, 5]), int(frow[i]), int(reap[i])))
+            if b is None and reap[i]:   # a carried record without left-overs: the same bytes
+                b = carry.get((int(fjob[i]), int(fin[i, 4]), int(fin[i, 5]), int(frow[i]), 0))
             if b is None:
                 raise UnsupportedInput("a record written across contigs was not carried (its mate fields disagree "
                                        "with where its records are)")
@@ -255,7 +245,7 @@ class Job:
             e = order[f]
             is_ext = ext[e]
             le = e[~is_ext]
-            data = self.fmt.format_arrays(fin[le, 4], frow[le], fin[le, 5]) if len(le) else b""
+            data = self.fmt.format_arrays(fin[le, 4], frow[le], fin[le, 5], reap[le]) if len(le) else b""
             if not np.any(is_ext):
                 out.append(data)
                 continue
@@ -402,7 +392,7 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
             for c in cands:
                 for r in c[c[:, 2] >= 0].tolist() if len(c) else []:
                     live.add((r[0], r[2], -1, r[3]))
-            for k in [k for k in carry if k not in live]:
+            for k in [k for k in carry if k[:4] not in live]:
                 del carry[k]
             job = None
             timing["resolve_s"] += t1 - t0
@@ -412,8 +402,11 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
         tail, single, wse = resolver.finish(cand, cand_names)
         if rank == 0:
             per_file: List[List[bytes]] = [[], [], [], []]
+            def carried(k):
+                b = carry.get(k)
+                return b if b is not None else carry[k[:4] + (0,)]
             for w in tail.tolist():
-                per_file[2 * w[0] + w[1]].append(carry[(w[2], w[3], w[4], w[5])])
+                per_file[2 * w[0] + w[1]].append(carried((w[2], w[3], w[4], w[5], w[6])))
             for f in range(4):
                 blob = b"".join(per_file[f])
                 if blob:
@@ -421,7 +414,7 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
             if wse:
                 for d, prefix in enumerate((tumor_out, normal_out)):
                     with open(f"{prefix}.single_end.fastq", "wb") as fh:
-                        fh.write(b"".join(carry[tuple(x)] for x in single[d].tolist()))
+                        fh.write(b"".join(carried(tuple(x)) for x in single[d].tolist()))
         all_stats = comm.allgather(stats_rows)
         if rank == 0 and record_statistics:
             merged: Dict[str, List[int]] = {OUTSIDE_WINDOWS: [0] * 8}

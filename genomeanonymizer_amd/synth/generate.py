@@ -384,7 +384,28 @@ def generate(cfg: ScenarioConfig, outdir: str) -> Dict[str, str]:
 # Named scenarios used by the golden fixtures and the tests
 # ---------------------------------------------------------------------------------------
 
+def fuzz_scenario(seed: int) -> ScenarioConfig:
+    """Random small multi-contig pair (oracle/fuzz_reference.py; goldens tests/golden/fuzz<seed>)."""
+    rng = np.random.default_rng(seed)
+    contigs = []
+    for c in range(int(rng.integers(2, 4))):
+        L = int(rng.integers(6_000, 14_000))
+        wins, x = [], 1001 + int(rng.integers(0, 1500))
+        while x < L - 1200 and len(wins) < 4:
+            wins.append(x)
+            x += 2003 + int(rng.integers(0, 3000))
+        contigs.append(ContigSpec(f"c{c}", L, int(rng.integers(60, 260)), windows=wins,
+                                  keep_windows=int(rng.integers(0, 2))))
+    return ScenarioConfig(name=f"fuzz{seed}", seed=seed, contigs=contigs,
+                          germline_snp_per_kb=float(rng.uniform(3, 10)),
+                          germline_indel_per_kb=float(rng.uniform(1, 4)), hom_fraction=0.3,
+                          softclip_frac=0.05, unmapped_mate_frac=0.05, n_base_frac=0.03,
+                          unplaced_frac=0.4, cross_contig_pairs=int(rng.integers(5, 30)))
+
+
 def scenario(name: str) -> ScenarioConfig:
+    if name.startswith("fuzz"):
+        return fuzz_scenario(int(name[4:]))
     if name == "config1":
         # BASELINE.json configs[0] / SURVEY §8(d) C1: chr20 1 Mb, 5,000 pairs per sample,
         # 1,000 germline het SNPs, 100 windows at 5,000 + 10,000*i (1-based).

@@ -54,6 +54,7 @@ class FastqFormatter:
         self._names = tables[0].names_blob.tobytes() + tables[1].names_blob.tobytes()
         self._name_base = (0, len(tables[0].names_blob))
         self.edited: Dict[Tuple[int, int, int], bytes] = {}   # indel-edited records (write_fastqs)
+        self.edited2: Dict[Tuple[int, int, int], bytes] = {}  # the same with the left-overs applied twice
 
     @staticmethod
     def _key(ds, row, sc):
@@ -99,7 +100,16 @@ class FastqFormatter:
             raise TypeError(f"reverse read {self.tables[d].name(r)!r} has a base outside ACGTN: the "
                             "reference's reverse complement fails on it (SURVEY Q7)") from None
 
-    def _edited(self, inst, edits) -> bytes:
+    def edited_bytes(self, inst, reapply: int = 0) -> bytes:
+        """Record of an instance with left-over edits, applied once or (reapply) twice (cached)."""
+        cache = self.edited2 if reapply else self.edited
+        b = cache.get(inst)
+        if b is None:
+            b = self._edited(inst, self.res.leftovers[inst], 2 if reapply else 1)
+            cache[inst] = b
+        return b
+
+    def _edited(self, inst, edits, times: int = 1) -> bytes:
         ds, row, sc = inst
         t = self.tables[ds]
         L = int(t.l_seq[row])
@@ -111,7 +121,8 @@ class FastqFormatter:
         q = t.qual[int(t.qual_off[row]):int(t.qual_off[row]) + L].tolist()
         rev = bool(t.is_reverse[row])
         qual_fwd = q[::-1] if rev else q
-        seq, qual_fwd = apply_leftovers(seq, qual_fwd, edits)
+        for _ in range(times):   # mask_or_anonymize_left_over_variants, once more when re-flagged
+            seq, qual_fwd = apply_leftovers(seq, qual_fwd, edits)
         if rev:
             try:
                 seq = bytearray(_REVERSES[c] for c in reversed(seq))
@@ -124,12 +135,14 @@ class FastqFormatter:
         return (f"@{t.name(row)}/{mate}\n".encode() + bytes(seq) + b"\n+\n" +
                 bytes(x + 33 for x in qual) + b"\n")
 
-    def format_arrays(self, ds: np.ndarray, row: np.ndarray, sc: np.ndarray) -> bytes:
+    def format_arrays(self, ds: np.ndarray, row: np.ndarray, sc: np.ndarray, reapply=None) -> bytes:
         """Records in the given order: every unedited record in ONE formatter call, the rare
-        indel-edited ones (variable length, formatted on the host) spliced in."""
+        indel-edited ones (variable length, formatted on the host; ``reapply``: left-overs applied
+        twice) spliced in."""
         ds = np.asarray(ds, np.int64)
         row = np.asarray(row, np.int64)
         sc = np.asarray(sc, np.int64)
+        reapply = np.zeros(len(ds), np.int64) if reapply is None else np.asarray(reapply, np.int64)
         left = self.res.leftovers
         if not left:
             return self._native(ds, row, sc)
@@ -149,16 +162,33 @@ class FastqFormatter:
         parts, prev = [], 0
         for i in ed.tolist():
             parts.append(data[off[prev]:off[i]])
-            inst = (int(ds[i]), int(row[i]), int(sc[i]))
-            b = self.edited.get(inst)
-            parts.append(b if b is not None else self._edited(inst, left[inst]))
+            parts.append(self.edited_bytes((int(ds[i]), int(row[i]), int(sc[i])), int(reapply[i])))
             prev = i + 1
         parts.append(data[off[prev]:])
         return b"".join(parts)
 
-    def format(self, recs: Sequence[Tuple[int, int, int]]) -> bytes:
+    def format(self, recs: Sequence[Tuple[int, int, int]], reapply=None) -> bytes:
         a = np.array(recs, np.int64).reshape(-1, 3)
-        return self.format_arrays(a[:, 0], a[:, 1], a[:, 2])
+        return self.format_arrays(a[:, 0], a[:, 1], a[:, 2], reapply)
+
+    def record_lengths(self, ds, row, sc, reapply=None) -> np.ndarray:
+        """Byte length of each record (edited ones included)."""
+        T, N = self.tables
+        ds = np.asarray(ds, np.int64)
+        row = np.asarray(row, np.int64)
+        sc = np.asarray(sc, np.int64)
+        r0, r1 = np.where(ds == 0, row, 0), np.where(ds == 1, row, 0)
+        nl = np.where(ds == 0, T.name_len[r0] if T.n else 0, N.name_len[r1] if N.n else 0).astype(np.int64)
+        ls = np.where(ds == 0, T.l_seq[r0] if T.n else 0, N.l_seq[r1] if N.n else 0).astype(np.int64)
+        out = nl + 8 + 2 * ls
+        left = self.res.leftovers
+        if left and len(ds):
+            keys = self._key(ds, row, sc)
+            lk = self._key(*zip(*left.keys()))
+            re_ = np.zeros(len(ds), np.int64) if reapply is None else np.asarray(reapply, np.int64)
+            for i in np.nonzero(np.isin(keys, lk))[0].tolist():
+                out[i] = len(self.edited_bytes((int(ds[i]), int(row[i]), int(sc[i])), int(re_[i])))
+        return out
 
 
 TEXT_CHUNK = 8192  # TextIOWrapper._CHUNK_SIZE of CPython
@@ -254,39 +284,28 @@ def write_fastqs(plan: Plan, res: MaskResult, tables, prefixes: Tuple[str, str],
     fmt = FastqFormatter(tables, res, backend)
     if block_size is None:
         block_size = io_block_size(os.path.dirname(os.path.abspath(prefixes[0])))
-    fmt.edited = {inst: fmt._edited(inst, e) for inst, e in res.leftovers.items()}
     ev, rows = plan.io_arrays()
     ids = ev[:, 4].astype(np.int64)
     isc = ev[:, 5].astype(np.int64)
-    T, N = tables
     wr = ev[:, 0] == 1
-    r0 = np.where(wr & (ids == 0), rows, 0)
-    r1 = np.where(wr & (ids == 1), rows, 0)
-    rec_len = np.where(ids == 0, T.name_len[r0].astype(np.int64) + 8 + 2 * T.l_seq[r0].astype(np.int64),
-                       N.name_len[r1].astype(np.int64) + 8 + 2 * N.l_seq[r1].astype(np.int64))
-    if fmt.edited:
-        keys = np.where(wr, FastqFormatter._key(ids, rows, isc), -1)
-        ek = FastqFormatter._key(*zip(*fmt.edited.keys()))
-        el = np.array([len(b) for b in fmt.edited.values()], np.int64)
-        o = np.argsort(ek)
-        ek, el = ek[o], el[o]
-        j = np.minimum(np.searchsorted(ek, keys), len(ek) - 1)
-        hit = ek[j] == keys
-        rec_len[hit] = el[j[hit]]
-    order = native.io_replay(ev, np.where(wr, rec_len, 0), block_size)
+    reapply = np.where(wr, ev[:, 6], 0).astype(np.int64)
+    rec_len = np.zeros(len(ev), np.int64)
+    wi = np.nonzero(wr)[0]
+    rec_len[wi] = fmt.record_lengths(ids[wi], rows[wi], isc[wi], reapply[wi])
+    order = native.io_replay(ev, rec_len, block_size)
     sizes = {}
     for ds in (0, 1):
         for slot in (0, 1):
             path = f"{prefixes[ds]}.{slot + 1}.fastq"
             e = order[2 * ds + slot]
-            data = fmt.format_arrays(ids[e], rows[e], isc[e])
+            data = fmt.format_arrays(ids[e], rows[e], isc[e], reapply[e])
             with open(path, "wb") as fh:
                 fh.write(data)
             sizes[path] = len(data)
     if plan.write_single_end:
         for ds in (0, 1):
             path = f"{prefixes[ds]}.single_end.fastq"
-            data = fmt.format(plan.single_end[ds])
+            data = fmt.format(plan.single_end[ds], plan.single_reapply[ds])
             with open(path, "wb") as fh:
                 fh.write(data)
             sizes[path] = len(data)

@@ -153,18 +153,22 @@ typedef struct ganon_plan_view {
   const int64_t *t_rows, *n_rows;                  /* mapped pileup reads, file order      */
   int64_t n_events;                                /* I/O log                              */
   const int32_t *events;     /* 7 per event: kind (0 open, 1 write, 2 close), handle, file dataset,
-                                file mate slot, instance dataset, instance scope (-1 unmasked), 0 */
+                                file mate slot, instance dataset, instance scope (-1 unmasked),
+                                reapply: 1 when the written object's left-overs are applied a second
+                                time (its left-over flag re-set by update_anonymized_read_from_other,
+                                AM:281-287) */
   const int64_t *event_rows; /* instance row of a write event, -1 otherwise                 */
   int64_t n_stats;
   const int32_t *stats;      /* 2 per event: kind (0 window -> window index, 1 outside, 2 scope id) */
   int64_t n_single[2];
-  const int64_t *single[2];  /* per dataset: (row, scope) pairs of the single-end records    */
+  const int64_t *single[2];  /* per dataset: (row, scope, reapply) of the single-end records  */
   int32_t write_single_end;
   /* contig mode: events may also hold kind 3 (a complete pair of a cross name: two consecutive events,
    * slot 0 then 1), 4 (store in to_pair, write and drop when complete: anonymize_window SR:313-360),
    * 5 (pass-through store, write when complete: SR:375-406); the 7th int is the event's clock. */
   int64_t n_left;
-  const int64_t *left;       /* 9 per unwritten pair: clock, has0, ds0, scope0, row0, has1, ds1, scope1, row1 */
+  const int64_t *left;       /* 11 per unwritten pair: clock, has0, ds0, scope0, row0, has1, ds1, scope1, row1,
+                                reapply0, reapply1 */
   int64_t n_cand;
   const int64_t *cand;       /* 5 per record: window, dataset (-1: this window's fetch raises), row,
                                 slot (-1: no READ1/READ2 flag), 1 if the record has no SEQ */
@@ -179,13 +183,14 @@ GANON_HOST_API const char *ganon_plan_last_error(void);
  * sample-wide pairing state (to_pair_anonymized_reads / written_read_ids, SR:134-165, :304-406,
  * AM:351-389), then the end of the sample: pair_unmapped_mates (SR:561-600) over the exported
  * candidates and the single ends (SR:603-622). Instances are (job, dataset, scope, row), job = the
- * contig plan they come from. A write is 6 int64: file dataset, file slot, job, dataset, scope, row. */
+ * contig plan they come from. A write is 7 int64: file dataset, file slot, job, dataset, scope, row,
+ * reapply (see ganon_plan_view.events). */
 typedef struct ganon_resolver ganon_resolver;
 GANON_HOST_API int ganon_resolver_create(ganon_resolver **out);
 GANON_HOST_API void ganon_resolver_free(ganon_resolver *r);
 /* ops: the placeholder events of job's plan (7 int32 each, plan layout) with their rows and read
- * names; left: the plan's unwritten pairs (9 int64 each) with names. out_n[i] receives the number of
- * writes op i makes (0 or 2), out_w 12 int64 per op. */
+ * names; left: the plan's unwritten pairs (11 int64 each) with names. out_n[i] receives the number of
+ * writes op i makes (0 or 2), out_w 14 int64 per op. */
 GANON_HOST_API int ganon_resolver_contig(ganon_resolver *r, int32_t job, int64_t n_ops, const int32_t *ops,
                                          const int64_t *op_rows, const char *op_names, const int64_t *op_name_off,
                                          const int32_t *op_name_len, int64_t n_left, const int64_t *left,
@@ -195,9 +200,9 @@ GANON_HOST_API int ganon_resolver_contig(ganon_resolver *r, int32_t job, int64_t
  * cap >= count, else only the count). */
 GANON_HOST_API int64_t ganon_resolver_pending(ganon_resolver *r, int64_t *out, int64_t cap);
 /* cand: 7 int64 per record (job, window, dataset, row, slot, no-SEQ flag, 0) in window order, with
- * names. tail (12 int64 per candidate) receives the writes of pair_unmapped_mates (count n_tail);
- * single[d] (4 int64 per record, capacity = ganon_resolver_pending count) the single ends in
- * dictionary order (counts n_single[2]). Returns GANON_PLAN_OK or GANON_PLAN_E_VALUE / _TYPE with the
+ * names. tail (14 int64 per candidate) receives the writes of pair_unmapped_mates (count n_tail);
+ * single[d] (5 int64 per record: job, dataset, scope, row, reapply; capacity = ganon_resolver_pending
+ * count) the single ends in dictionary order (counts n_single[2]). Returns GANON_PLAN_OK or GANON_PLAN_E_VALUE / _TYPE with the
  * reference's error (message: ganon_plan_last_error). */
 GANON_HOST_API int ganon_resolver_finish(ganon_resolver *r, int64_t n_cand, const int64_t *cand, const char *names,
                                          const int64_t *name_off, const int32_t *name_len, int64_t *tail,

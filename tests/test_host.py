@@ -147,6 +147,7 @@ def _same_plan(a, b):
            {d: [tuple(map(int, i)) for i in r] for d, r in b.single_end.items()}
     assert a.stats_events == b.stats_events
     assert a.write_single_end == b.write_single_end
+    assert a.single_reapply == b.single_reapply
 
 
 @pytest.mark.parametrize("seed", [1, 2, 3])

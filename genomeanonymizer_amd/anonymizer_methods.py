@@ -39,18 +39,26 @@ class MaskResult:
     leftovers: Dict[Tuple[int, int, int], list]   # (ds, row, scope) -> indel edits
     totals: np.ndarray
     arrays: dict                           # the device batch (kept for tests/bench)
+    dup_off: Dict[Tuple[int, int, int], int] = dataclasses.field(default_factory=dict)
+
+    def masked_nib(self, tables, ds: int, row: int, scope: int) -> int:
+        """Nibble offset in seq_out of read (ds, row) as masked by ``scope``."""
+        o = self.dup_off.get((ds, row, scope))
+        if o is None:
+            o = self.seq_base[ds] + int(tables[ds].seq_off[row])
+        return 2 * o
 
 
 def build_batch(plan: Plan, tables: Tuple[ReadTable, ReadTable], fasta: FastaRef,
                 scope_ids=None, written=None) -> Tuple[dict, dict]:
     """Lay the plan's scopes (all, or the subset ``scope_ids`` of one contig shard) out as
     one ganon_batch (include/ganon.h). Batch scope k is plan scope ``meta['scope_ids'][k]``.
-    ``written``: (dataset, row, scope) arrays of the instances to mask, at most one masked scope
-    per read (default: the plan's written records)."""
+    ``written``: (dataset, row, scope) arrays of the instances to mask (default: the plan's written
+    records). A read masked in a second scope (the alignments of complex names, objects.py) gets a
+    copy of its record in the batch, the one that scope's incidence points at."""
     T, N = tables
     packed, nib_off = fasta.packed()
     scopes = plan.scopes if scope_ids is None else [plan.scopes[i] for i in scope_ids]
-    local = {sc.id: k for k, sc in enumerate(scopes)}
     # batch reads: every read of every scope, tumor rows then normal rows
     in_scope = [np.zeros(T.n, bool), np.zeros(N.n, bool)]
     for sc in scopes:
@@ -68,25 +76,80 @@ def build_batch(plan: Plan, tables: Tuple[ReadTable, ReadTable], fasta: FastaRef
     arr["ref_start"] = cat("pos", np.int32)
     arr["read_len"] = cat("l_seq", np.int32)
     arr["seq_off"] = np.concatenate([T.seq_off[rows[0]] + seq_base[0], N.seq_off[rows[1]] + seq_base[1]]).astype(np.int64)
-    arr["seq_nt16"] = np.ascontiguousarray(np.concatenate([T.seq, N.seq]).astype(np.uint8))
     arr["cig_off"] = np.concatenate([T.cig_off[rows[0]] + cig_base[0], N.cig_off[rows[1]] + cig_base[1]]).astype(np.int64)
     arr["n_cig"] = cat("n_cigar", np.int32)
     arr["cigar"] = np.ascontiguousarray(np.concatenate([T.cigar, N.cigar]).astype(np.uint32))
     arr["dataset"] = np.concatenate([np.zeros(len(rows[0]), np.uint8), np.ones(len(rows[1]), np.uint8)])
     ws = np.full(n_reads, -1, np.int32)
     w_ds, w_row, w_sc = plan.written_arrays() if written is None else written
+    w_ds, w_row, w_sc = (np.asarray(x, np.int64) for x in (w_ds, w_row, w_sc))
     loc = np.full(len(plan.scopes) + 1, -1, np.int64)
     loc[[sc.id for sc in scopes]] = np.arange(len(scopes))
     sel = (w_sc >= 0) & (loc[np.where(w_sc >= 0, w_sc, len(plan.scopes))] >= 0)
-    b = np.where(w_ds[sel] == 0, bidx[0][np.where(w_ds[sel] == 0, w_row[sel], 0)],
-                 bidx[1][np.where(w_ds[sel] == 1, w_row[sel], 0)])
-    ws[b] = loc[w_sc[sel]]
-    arr["write_scope"] = ws
+    w_ds, w_row, w_sc = w_ds[sel], w_row[sel], w_sc[sel]
+    b = np.where(w_ds == 0, bidx[0][np.where(w_ds == 0, w_row, 0)], bidx[1][np.where(w_ds == 1, w_row, 0)])
+    first = np.ones(len(b), bool)
+    if len(b):
+        _, fi = np.unique(b, return_index=True)
+        first[:] = False
+        first[fi] = True
+    ws[b[first]] = loc[w_sc[first]]
     counts = np.array([len(sc.t_rows) + len(sc.n_rows) for sc in scopes], np.int64)
-    arr["scope_incid_off"] = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
-    arr["incid_read"] = (np.concatenate([np.concatenate([bidx[0][sc.t_rows], bidx[1][sc.n_rows]])
-                                         for sc in scopes]).astype(np.int32)
-                         if scopes else np.zeros(0, np.int32))
+    incid_off = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+    incid = (np.concatenate([np.concatenate([bidx[0][sc.t_rows], bidx[1][sc.n_rows]]) for sc in scopes]).astype(np.int32)
+             if scopes else np.zeros(0, np.int32))
+    seq_parts = [T.seq, N.seq]
+    dup_off: Dict[Tuple[int, int, int], int] = {}
+    dup_rows = []
+    extra = {k: [] for k in ("ref_start", "read_len", "seq_off", "cig_off", "n_cig", "dataset")}
+    n_seq = len(T.seq) + len(N.seq)
+    ex_ws = []
+    for i in np.nonzero(~first)[0].tolist():        # the same read masked in another scope
+        d, r, sid = int(w_ds[i]), int(w_row[i]), int(w_sc[i])
+        if (d, r, sid) in dup_off or ws[b[i]] == loc[sid]:
+            continue
+        t = tables[d]
+        nbytes = (int(t.l_seq[r]) + 1) // 2
+        o = int(t.seq_off[r])
+        seq_parts.append(t.seq[o:o + nbytes])
+        dup_off[(d, r, sid)] = n_seq
+        k = int(loc[sid])
+        seg = incid[incid_off[k]:incid_off[k + 1]]
+        hit = np.nonzero(seg == b[i])[0]
+        seg[hit] = n_reads + len(dup_rows)
+        extra["ref_start"].append(int(t.pos[r]))
+        extra["read_len"].append(int(t.l_seq[r]))
+        extra["seq_off"].append(n_seq)
+        extra["cig_off"].append(int(t.cig_off[r]) + cig_base[d])
+        extra["n_cig"].append(int(t.n_cigar[r]))
+        extra["dataset"].append(d)
+        ex_ws.append(k)
+        dup_rows.append((d, r))
+        n_seq += nbytes
+    if dup_rows:
+        for f, dt in (("ref_start", np.int32), ("read_len", np.int32), ("seq_off", np.int64), ("cig_off", np.int64),
+                      ("n_cig", np.int32), ("dataset", np.uint8)):
+            arr[f] = np.concatenate([arr[f], np.array(extra[f], dt)])
+        ws = np.concatenate([ws, np.array(ex_ws, np.int32)])
+    arr["seq_nt16"] = np.ascontiguousarray(np.concatenate(seq_parts).astype(np.uint8))
+    arr["write_scope"] = ws
+    arr["scope_incid_off"] = incid_off
+    arr["incid_read"] = incid
+    skip = getattr(plan, "skip", None)
+    if skip is not None and len(skip):
+        # seen_read_alns (variation_classifier.py:196-207): later alignments of a read in a scope
+        # are tallied for SNVs but not for indels
+        drop = np.zeros(len(incid), bool)
+        for sid, d, r in skip.tolist():
+            k = int(loc[sid]) if sid < len(plan.scopes) else -1
+            if k < 0:
+                continue
+            br = n_reads + dup_rows.index((d, r)) if (d, r, sid) in dup_off else int(bidx[d][r])
+            seg = incid[incid_off[k]:incid_off[k + 1]]
+            drop[incid_off[k] + np.nonzero(seg == br)[0]] = True
+        kept = np.diff(np.concatenate([[0], np.cumsum(~drop)])[incid_off])
+        arr["indel_incid_off"] = np.concatenate([[0], np.cumsum(kept)]).astype(np.int64)
+        arr["indel_incid_read"] = incid[~drop]
     arr["scope_span_start"] = np.array([sc.span_start for sc in scopes], np.int32)
     arr["scope_span_len"] = np.array([sc.span_end - sc.span_start for sc in scopes], np.int32)
     arr["scope_ref_off"] = np.array([nib_off[sc.contig] + sc.span_start for sc in scopes], np.int64)
@@ -94,7 +157,7 @@ def build_batch(plan: Plan, tables: Tuple[ReadTable, ReadTable], fasta: FastaRef
     keep = [kept_snv(sc.keep) if sc.is_variant_window else (-1, 0) for sc in scopes]
     arr["keep_pos"] = np.array([k[0] for k in keep], np.int32)
     arr["keep_code"] = np.array([k[1] for k in keep], np.uint8)
-    meta = {"bidx": bidx, "rows": rows, "seq_base": seq_base,
+    meta = {"bidx": bidx, "rows": rows, "seq_base": seq_base, "dup_off": dup_off, "dup_rows": dup_rows,
             "scope_ids": np.array([sc.id for sc in scopes], np.int64)}
     return arr, meta
 
@@ -108,8 +171,12 @@ def indel_results(recs: np.ndarray, meta: dict, plan: Plan, tables: Tuple[ReadTa
     The kept window variant (AM:546-547) is excluded here: its identity includes the allele."""
     rows = meta["rows"]
     n_t = len(rows[0])
+    n_p = n_t + len(rows[1])
+    dups = meta.get("dup_rows", [])
 
     def ds_row(r: int) -> Tuple[int, int]:
+        if r >= n_p:
+            return dups[r - n_p]
         return (0, int(rows[0][r])) if r < n_t else (1, int(rows[1][r - n_t]))
 
     indel_counts: Dict[int, Dict[VariantType, int]] = {}
@@ -175,7 +242,8 @@ class CompleteGermlineAnonymizer:
         calls[meta["scope_ids"]] = b_calls
         bases[meta["scope_ids"]] = b_bases
         indel_counts, leftovers = indel_results(irecs, meta, plan, tables, fasta)
-        return MaskResult(out, meta["seq_base"], {}, calls, bases, indel_counts, leftovers, totals, arrays)
+        return MaskResult(out, meta["seq_base"], {}, calls, bases, indel_counts, leftovers, totals, arrays,
+                          meta["dup_off"])
 
 
 ANONYMIZER_ALGORITHMS = {CompleteGermlineAnonymizer.name: CompleteGermlineAnonymizer}

@@ -49,7 +49,8 @@ struct Inst {
   int64_t row;
 };
 
-constexpr int32_t kFlagUnmap = 0x4, kFlagRead1 = 0x40, kFlagRead2 = 0x80;
+constexpr int32_t kFlagUnmap = 0x4, kFlagReverse = 0x10, kFlagRead1 = 0x40, kFlagRead2 = 0x80,
+                  kFlagSecondary = 0x100, kFlagSupplementary = 0x800;
 
 struct Table {
   const ganon_plan_table *t = nullptr;
@@ -138,6 +139,9 @@ class Planner {
   bool write_single_end_ = false;
   std::vector<int64_t> left_;         // contig mode: 11 per unwritten pair (include/ganon_host.h)
   std::vector<int64_t> cand_;         // contig mode: 5 per pair_unmapped_mates candidate
+  std::vector<int64_t> objs_;         // contig mode: 10 per object of a complex name
+  std::vector<int64_t> obj_rows_;
+  std::vector<int64_t> skip_;         // (scope, ds, row) left out of the indel tally
 
  private:
   struct Section {
@@ -153,6 +157,7 @@ class Planner {
   uint64_t pair_seq_ = 0;             // clock: to_pair insertions and placeholder events
   bool cmode_ = false;
   std::vector<uint8_t> cross_;        // per name id (contig mode)
+  std::vector<uint8_t> cx_;           // per name id: complex (SA tag / secondary / supplementary record)
   std::unordered_set<int64_t> written_;
   int32_t next_hid_ = 0;
 
@@ -183,8 +188,25 @@ class Planner {
       }
       if (cmode_) {
         cross_.resize(ids.size(), 0);
+        cx_.resize(ids.size(), 0);
+        for (int64_t r = 0; r < t.n; ++r) {
+          const size_t nm = (size_t)nid_[d][r];
+          if (t.tid[r] < 0 || t.mate_tid[r] != t.tid[r]) cross_[nm] = 1;
+          if (complex_rec(d, r)) {
+            // a secondary alignment off its mate's contig: the name's other records may be planned
+            // as local elsewhere, where nothing tells that this object exists
+            if ((t.flag[r] & kFlagSecondary) && t.mate_tid[r] >= 0 && t.mate_tid[r] != t.tid[r])
+              raise(GANON_PLAN_E_UNSUPPORTED, "secondary alignment of '" + tab_[d].name(r) +
+                                                  "' on another reference sequence than its mate");
+            cx_[nm] = 1;
+            cross_[nm] = 1;
+          }
+        }
+      } else {
         for (int64_t r = 0; r < t.n; ++r)
-          if (t.tid[r] < 0 || t.mate_tid[r] != t.tid[r]) cross_[(size_t)nid_[d][r]] = 1;
+          if (complex_rec(d, r))
+            raise(GANON_PLAN_E_UNSUPPORTED, "secondary / supplementary alignments and SA tags are planned by the "
+                                            "streaming (contig) path only (record '" + tab_[d].name(r) + "')");
       }
       if (d == 0) tumor_ids = (int64_t)ids.size();
       else if (shared) {
@@ -308,6 +330,37 @@ class Planner {
   }
 
   bool cross(const Inst &i) const { return cmode_ && cross_[(size_t)nid_[i.ds][(size_t)i.row]]; }
+  bool cx(int ds, int64_t row) const { return cmode_ && cx_[(size_t)nid_[ds][(size_t)row]]; }
+  bool complex_rec(int ds, int64_t r) const {
+    const ganon_plan_table &t = in_->tables[ds];
+    return (t.flag[r] & (kFlagSecondary | kFlagSupplementary)) || (t.n_sa && t.n_sa[r] >= 0);
+  }
+  bool supp_rec(int ds, int64_t r) const { return (in_->tables[ds].flag[r] & kFlagSupplementary) != 0; }
+  int32_t n_sa(int ds, int64_t r) const { return in_->tables[ds].n_sa ? in_->tables[ds].n_sa[r] : -1; }
+
+  // an AnonymizedRead of a complex name (include/ganon_host.h ganon_plan_view.objs)
+  int64_t add_object(int32_t scope, int ds, int sl, const std::vector<int64_t> &al, const std::vector<int64_t> &hashes) {
+    const int64_t idx = (int64_t)objs_.size() / 10;
+    const int64_t c = al[0];
+    int64_t base = -1;
+    for (int64_t r : al)
+      if (!supp_rec(ds, r)) {
+        base = r;
+        break;
+      }
+    const int32_t nsa = n_sa(ds, c);
+    const int64_t info = (supp_rec(ds, c) ? 1 : 0) | (nsa >= 0 ? 2 : 0) | ((int64_t)std::max(nsa, 0) << 8);
+    objs_.insert(objs_.end(), {(int64_t)scope, (int64_t)ds, (int64_t)sl, c, base, (int64_t)obj_rows_.size(),
+                               (int64_t)al.size(), (int64_t)(obj_rows_.size() + al.size()), (int64_t)hashes.size(), info});
+    obj_rows_.insert(obj_rows_.end(), al.begin(), al.end());
+    obj_rows_.insert(obj_rows_.end(), hashes.begin(), hashes.end());
+    return idx;
+  }
+  void object_event(int32_t kind, int32_t hid, int32_t flags, int sl, int ds, int32_t scope, int64_t obj) {
+    if (pair_seq_ >= (uint64_t)INT32_MAX) raise(GANON_PLAN_E_UNSUPPORTED, "contig plan clock overflow");
+    events_.insert(events_.end(), {kind, hid, flags, sl, ds, scope, (int32_t)pair_seq_++});
+    event_rows_.push_back(obj);
+  }
 
   // contig mode: an operation on a cross name's pairing state, decided by ganon_resolver_contig
   void placeholder(int32_t kind, int32_t hid, int slot, const Inst &i) {
@@ -347,6 +400,13 @@ class Planner {
     if (in_->tables[ds].l_seq[row] == 0)
       raise(GANON_PLAN_E_TYPE, "read '" + tab_[ds].name(row) + "' has no SEQ; the reference cannot upper-case it");
     const Inst inst{ds, -1, row};
+    if (cx(ds, row)) {   // add_anonymized_read_pair_to_collection_from_alignment on a complex name
+      const int sl = slot(ds, row);
+      std::vector<int64_t> h;
+      if (supp_rec(ds, row) && n_sa(ds, row) >= 0) h.push_back(row);
+      object_event(7, hid, 0, sl, ds, -1, add_object(-1, ds, sl, {row}, h));
+      return;
+    }
     if (cross(inst)) {
       placeholder(5, hid, slot(ds, row), inst);
       return;
@@ -410,9 +470,22 @@ class Planner {
     bool has[2];
     int64_t max_end;
   };
+  // the objects one yield of a complex name carries: alignments per slot since the name (re)entered
+  // the anonymizer's dictionary, in registration order
+  struct Episode {
+    int32_t ds;
+    std::vector<int64_t> al[2];
+    std::vector<int64_t> hashes[2];
+  };
+  struct YItem {
+    int64_t col;    // yield column, or INT64_MAX = at the scope's end
+    int64_t rank;   // registration index of the dictionary entry (dict order)
+    int32_t kind;   // 0 plain pair, 1 complex episode
+    int32_t idx;
+  };
 
   // pairs in the order CompleteGermlineAnonymizer.anonymize yields them (AM:472-532)
-  void yield_sequence(int32_t sid, std::vector<YPair> &pairs, std::vector<int32_t> &order) {
+  void yield_sequence(int32_t sid, std::vector<YPair> &pairs, std::vector<Episode> &eps, std::vector<YItem> &order) {
     const ScopeRec &sc = scopes_[(size_t)sid];
     struct Reg {
       int64_t pos;
@@ -428,29 +501,6 @@ class Planner {
       if (a.ds != b.ds) return a.ds < b.ds;
       return a.fo < b.fo;
     });
-    pairs.clear();
-    std::unordered_map<int64_t, int32_t> where;
-    where.reserve(reg.size());
-    for (const Reg &g : reg) {
-      const int64_t name = nid_[g.ds][(size_t)g.row];
-      const int sl = slot(g.ds, g.row);
-      const int64_t e = in_->tables[g.ds].end[g.row];
-      auto it = where.find(name);
-      YPair *p;
-      if (it == where.end()) {
-        where.emplace(name, (int32_t)pairs.size());
-        pairs.push_back(YPair{name, {}, {false, false}, e});
-        p = &pairs.back();
-      } else {
-        p = &pairs[(size_t)it->second];
-        p->max_end = std::max(p->max_end, e);
-      }
-      if (p->has[sl])
-        raise(GANON_PLAN_E_UNSUPPORTED, "two alignments of '" + tab_[g.ds].name(g.row) +
-                                            "' with the same mate flag in one scope");
-      p->p[sl] = Inst{g.ds, sid, g.row};
-      p->has[sl] = true;
-    }
     // normal columns: union of the normal reads' [pos, end)
     std::vector<int64_t> m_start, m_end;
     if (sc.n1 > sc.n0) {
@@ -470,40 +520,149 @@ class Planner {
       }
       m_end.push_back(run_end);
     }
-    struct Scan {
-      int64_t col;
-      int32_t rank;
+    // first normal column at or after x (mask + yield loop of AM:477-512), INT64_MAX if none
+    auto yield_col = [&](int64_t x) {
+      const size_t k = (size_t)(std::upper_bound(m_end.begin(), m_end.end(), x) - m_end.begin());
+      return k < m_end.size() ? std::max(x, m_start[k]) : INT64_MAX;
     };
-    std::vector<Scan> scan;
-    std::vector<int32_t> rest;
-    for (int32_t rank = 0; rank < (int32_t)pairs.size(); ++rank) {
-      const YPair &p = pairs[(size_t)rank];
-      if (p.has[0] && p.has[1]) {
-        const int64_t x = p.max_end + 1;   // first column with right_most_end < pos
-        const size_t k = (size_t)(std::upper_bound(m_end.begin(), m_end.end(), x) - m_end.begin());
-        if (k < m_end.size()) {
-          scan.push_back(Scan{std::max(x, m_start[k]), rank});
-          continue;
+    pairs.clear();
+    eps.clear();
+    order.clear();
+    std::vector<int64_t> pair_rank;
+    std::unordered_map<int64_t, int32_t> where;
+    std::unordered_map<int64_t, int32_t> cx_where;
+    std::vector<std::vector<int32_t>> cx_regs;
+    where.reserve(reg.size());
+    for (int32_t gi = 0; gi < (int32_t)reg.size(); ++gi) {
+      const Reg &g = reg[(size_t)gi];
+      const int64_t name = nid_[g.ds][(size_t)g.row];
+      const int sl = slot(g.ds, g.row);
+      if (cx(g.ds, g.row)) {
+        auto it = cx_where.find(name);
+        if (it == cx_where.end()) {
+          cx_where.emplace(name, (int32_t)cx_regs.size());
+          cx_regs.emplace_back();
+          cx_regs.back().push_back(gi);
+        } else {
+          std::vector<int32_t> &v = cx_regs[(size_t)it->second];
+          // seen_read_alns: only a read's first alignment in the scope contributes indels
+          bool seen = false;
+          for (int32_t x : v) seen = seen || slot(reg[(size_t)x].ds, reg[(size_t)x].row) == sl;
+          if (seen) skip_.insert(skip_.end(), {(int64_t)sid, (int64_t)g.ds, g.row});
+          v.push_back(gi);
+        }
+        continue;
+      }
+      const int64_t e = in_->tables[g.ds].end[g.row];
+      auto it = where.find(name);
+      YPair *p;
+      if (it == where.end()) {
+        where.emplace(name, (int32_t)pairs.size());
+        pairs.push_back(YPair{name, {}, {false, false}, e});
+        pair_rank.push_back(gi);
+        p = &pairs.back();
+      } else {
+        p = &pairs[(size_t)it->second];
+        p->max_end = std::max(p->max_end, e);
+      }
+      if (p->has[sl])
+        raise(GANON_PLAN_E_UNSUPPORTED, "two alignments of '" + tab_[g.ds].name(g.row) +
+                                            "' with the same mate flag in one scope");
+      p->p[sl] = Inst{g.ds, sid, g.row};
+      p->has[sl] = true;
+    }
+    std::vector<YItem> items;
+    for (int32_t k = 0; k < (int32_t)pairs.size(); ++k) {
+      const YPair &p = pairs[(size_t)k];
+      const int64_t col = (p.has[0] && p.has[1]) ? yield_col(p.max_end + 1) : INT64_MAX;
+      items.push_back(YItem{col, pair_rank[(size_t)k], 0, k});
+    }
+    // complex names: the object state after each registration; a writeable pair is yielded at the
+    // first normal column past its rightmost end that comes before the name's next registration
+    for (const std::vector<int32_t> &v : cx_regs) {
+      bool open = false;
+      bool ex[2], supp[2], has_sa[2];
+      int32_t nsa[2];
+      int64_t max_end = 0, rank = 0;
+      Episode cur;
+      for (size_t k = 0; k < v.size(); ++k) {
+        const Reg &g = reg[(size_t)v[k]];
+        const int ds = g.ds;
+        const int sl = slot(ds, g.row);
+        const bool sp = supp_rec(ds, g.row);
+        if (!open) {
+          open = true;
+          ex[0] = ex[1] = false;
+          cur = Episode{};
+          cur.ds = ds;
+          rank = v[k];
+          max_end = 0;
+        }
+        cur.al[sl].push_back(g.row);
+        auto add_hash = [&](int s, int64_t row) {
+          if (std::find(cur.hashes[s].begin(), cur.hashes[s].end(), row) == cur.hashes[s].end())
+            cur.hashes[s].push_back(row);
+        };
+        if (!ex[sl]) {   // AnonymizedRead.__init__ (AM:85-117); the creator's own hash when the name is
+                         // known already or at its second column (AM:333-342)
+          ex[sl] = true;
+          supp[sl] = sp;
+          nsa[sl] = n_sa(ds, g.row);
+          has_sa[sl] = nsa[sl] >= 0;
+          if (sp && (has_sa[sl] || ex[1 - sl] || in_->tables[ds].end[g.row] - g.pos >= 2)) add_hash(sl, g.row);
+        } else {
+          if (!sp && supp[sl]) supp[sl] = false;   // update_from_primary_mapping
+          if (sp) add_hash(sl, g.row);
+        }
+        max_end = std::max<int64_t>(max_end, in_->tables[ds].end[g.row]);
+        auto complete = [&](int s) {
+          return !supp[s] && (!has_sa[s] || (int64_t)cur.hashes[s].size() >= nsa[s]);
+        };
+        if (ex[0] && ex[1] && complete(0) && complete(1)) {
+          const int64_t next_pos = k + 1 < v.size() ? reg[(size_t)v[k + 1]].pos : INT64_MAX;
+          const int64_t col = yield_col(max_end + 1);
+          if (col < next_pos) {
+            items.push_back(YItem{col, rank, 1, (int32_t)eps.size()});
+            eps.push_back(std::move(cur));
+            open = false;
+          }
         }
       }
-      rest.push_back(rank);
+      if (open) {
+        items.push_back(YItem{INT64_MAX, rank, 1, (int32_t)eps.size()});
+        eps.push_back(std::move(cur));
+      }
     }
-    std::sort(scan.begin(), scan.end(), [](const Scan &a, const Scan &b) {
+    std::sort(items.begin(), items.end(), [](const YItem &a, const YItem &b) {
       return a.col != b.col ? a.col < b.col : a.rank < b.rank;
     });
-    order.clear();
-    for (const Scan &s : scan) order.push_back(s.rank);
-    order.insert(order.end(), rest.begin(), rest.end());
+    order = std::move(items);
+  }
+
+  void complex_yield(int32_t sid, int32_t hid, const Episode &ep) {
+    const int n = (ep.al[0].empty() ? 0 : 1) + (ep.al[1].empty() ? 0 : 1);
+    bool first = true;
+    for (int s = 0; s < 2; ++s) {
+      if (ep.al[s].empty()) continue;
+      const int64_t obj = add_object(sid, ep.ds, s, ep.al[s], ep.hashes[s]);
+      object_event(6, hid, first ? (1 | (n << 1)) : 0, s, ep.ds, sid, obj);
+      first = false;
+    }
   }
 
   void anonymize_window(int32_t contig, int64_t first, int64_t last, int32_t window, bool /*variant*/) {
     const int32_t sid = new_scope(contig, first, last, window);
     const int32_t hid = open_handle();
     std::vector<YPair> pairs;
-    std::vector<int32_t> order;
-    yield_sequence(sid, pairs, order);
-    for (int32_t k : order) {
-      const YPair &p = pairs[(size_t)k];
+    std::vector<Episode> eps;
+    std::vector<YItem> order;
+    yield_sequence(sid, pairs, eps, order);
+    for (const YItem &y : order) {
+      if (y.kind == 1) {
+        complex_yield(sid, hid, eps[(size_t)y.idx]);
+        continue;
+      }
+      const YPair &p = pairs[(size_t)y.idx];
       if (p.has[0] && p.has[1]) {
         if (cross(p.p[0])) {
           placeholder(3, hid, 0, p.p[0]);
@@ -696,6 +855,9 @@ class Planner {
           if (!tab_[ds].unmapped(r)) continue;
           const int64_t nm = nid_[ds][(size_t)r];
           if (!cross_[(size_t)nm] && !pending.count(nm)) continue;
+          if (complex_rec(ds, r))
+            raise(GANON_PLAN_E_UNSUPPORTED, "unmapped secondary / supplementary record or SA tag ('" +
+                                                tab_[ds].name(r) + "')");
           cand_.insert(cand_.end(), {w, ds, r, tab_[ds].mate_idx(r), in_->tables[ds].l_seq[r] == 0 ? 1 : 0});
         }
       }
@@ -827,6 +989,12 @@ GANON_HOST_API int ganon_plan_view_get(const ganon_plan *pl, ganon_plan_view *v)
   v->left = p.left_.data();
   v->n_cand = (int64_t)p.cand_.size() / 5;
   v->cand = p.cand_.data();
+  v->n_objs = (int64_t)p.objs_.size() / 10;
+  v->objs = p.objs_.data();
+  v->n_obj_rows = (int64_t)p.obj_rows_.size();
+  v->obj_rows = p.obj_rows_.data();
+  v->n_skip = (int64_t)p.skip_.size() / 3;
+  v->skip = p.skip_.data();
   return GANON_PLAN_OK;
 }
 
@@ -847,51 +1015,150 @@ struct RInst {
   int64_t job, ds, scope, row;
 };
 
+// One AnonymizedRead of the sample-wide state: a plain instance (its masked copy in one scope and
+// the re-set left-over flag, as the cross names of round 2 had it) or an object whose content the
+// caller replays from the log (complex names, and plain instances that met one).
+struct RObj {
+  bool general = false;
+  int64_t id = 0;
+  RInst inst{};
+  bool upd = false;     // plain: PairSlot::upd
+  int32_t ds = 0;
+  bool supp = false, has_sa = false;
+  int32_t n_sa = 0;
+  std::vector<int64_t> hashes;   // supplementary records recorded (record ids)
+
+  bool complete() const {   // AnonymizedRead.anonymized_read_is_complete (AM:125-137)
+    return !supp && (!has_sa || (int64_t)hashes.size() >= n_sa);
+  }
+  void add_hash(int64_t h) {
+    if (std::find(hashes.begin(), hashes.end(), h) == hashes.end()) hashes.push_back(h);
+  }
+};
+
+RObj plain_obj(const RInst &i) {
+  RObj o;
+  o.inst = i;
+  o.ds = (int32_t)i.ds;
+  return o;
+}
+
 struct RSlot {
-  RInst p[2];
+  RObj o[2];
   bool has[2] = {false, false};
-  bool upd[2] = {false, false};   // PairSlot::upd
   int64_t seq = 0;   // (job << 32) | clock of the last insertion (dict order)
 };
+
+int64_t record_id(int64_t job, int64_t ds, int64_t row) { return (job << 40) | (ds << 39) | row; }
 
 }  // namespace
 
 struct ganon_resolver {
   std::unordered_map<std::string, RSlot> to_pair;
   std::unordered_set<std::string> written;
+  std::vector<int64_t> log;     // 8 per entry (include/ganon_host.h)
+  int64_t next_gid = (int64_t)1 << 62;
+  int64_t next_serial = 0;
 
-  RSlot &store_first(const std::string &name, int slot, const RInst &i, int64_t seq, bool update = false) {
+  void emit(int64_t op, int64_t id, int64_t a = 0, int64_t b = 0, int64_t c = 0, int64_t d = 0, int64_t e = 0) {
+    log.insert(log.end(), {op, id, a, b, c, d, e, 0});
+  }
+  void generalize(RObj &o) {
+    if (o.general) return;
+    o.id = next_gid++;
+    emit(1, o.id, o.inst.job, o.inst.ds, o.inst.scope, o.inst.row, o.upd ? 1 : 0);
+    o.general = true;
+  }
+  void apply(RObj &o) {   // "if has_left_overs_to_mask: mask_or_anonymize_left_over_variants()"
+    if (o.general) emit(3, o.id);
+  }
+  void out_obj(RObj &o, int64_t file_ds, int s, int64_t *w) {
+    w[0] = file_ds;
+    w[1] = s;
+    if (o.general) {
+      const int64_t serial = next_serial++;
+      emit(5, o.id, serial);
+      w[2] = -1;
+      w[3] = o.ds;
+      w[4] = -2;
+      w[5] = serial;
+      w[6] = 0;
+    } else {
+      w[2] = o.inst.job;
+      w[3] = o.inst.ds;
+      w[4] = o.inst.scope;
+      w[5] = o.inst.row;
+      w[6] = o.upd ? 1 : 0;
+    }
+  }
+  // write_pair (SR:134-165): both records to the first object's dataset files, once per name
+  int write_pair(const std::string &name, RObj &a, RObj &b, int64_t *w) {
+    if (!written.insert(name).second) return 0;
+    const int64_t fds = a.ds;
+    out_obj(a, fds, 0, w);
+    out_obj(b, fds, 1, w + 7);
+    return 2;
+  }
+  RSlot &entry(const std::string &name, int64_t seq) {
     auto it = to_pair.find(name);
     if (it == to_pair.end()) {
       it = to_pair.emplace(name, RSlot{}).first;
       it->second.seq = seq;
     }
-    RSlot &p = it->second;
-    if (!p.has[slot]) {
-      p.p[slot] = i;
-      p.has[slot] = true;
-    } else if (update) {
-      p.upd[slot] = true;
+    return it->second;
+  }
+  // add_or_update_anonymized_read_from_other (AM:351-389)
+  RSlot &add_or_update(const std::string &name, int sl, RObj nw, int64_t seq) {
+    RSlot &p = entry(name, seq);
+    if (!p.has[sl]) {
+      p.o[sl] = std::move(nw);
+      p.has[sl] = true;
+      return p;
+    }
+    RObj &sv = p.o[sl];
+    if (sv.supp && !nw.supp) {   // the primary mapping takes over the supplementary's record
+      generalize(nw);
+      generalize(sv);
+      emit(2, nw.id, sv.id);
+      for (int64_t h : sv.hashes) nw.add_hash(h);
+      sv = std::move(nw);
+    } else if (!sv.general && !nw.general) {
+      sv.upd = true;
+      for (int64_t h : nw.hashes) sv.add_hash(h);
+    } else {
+      generalize(sv);
+      generalize(nw);
+      emit(2, sv.id, nw.id);
+      for (int64_t h : nw.hashes) sv.add_hash(h);
     }
     return p;
   }
-  // write_pair (SR:134-165): both records to the first instance's dataset files, once per name
-  int write_pair(const std::string &name, const RInst &a, const RInst &b, int64_t *w, bool ra = false,
-                 bool rb = false) {
-    if (!written.insert(name).second) return 0;
-    const RInst *ab[2] = {&a, &b};
-    const bool re[2] = {ra, rb};
-    for (int s = 0; s < 2; ++s) {
-      int64_t *o = w + 7 * s;
-      o[0] = a.ds;
-      o[1] = s;
-      o[2] = ab[s]->job;
-      o[3] = ab[s]->ds;
-      o[4] = ab[s]->scope;
-      o[5] = ab[s]->row;
-      o[6] = re[s] ? 1 : 0;
+  // add_anonymized_read_pair_to_collection_from_alignment (AM:320-348) with record rec (its object
+  // nw, rec_supp / rec_sa: flags), then pair_unmapped_or_non_pileup_pairs_and_write (SR:375-406)
+  int passthrough(const std::string &name, int sl, RObj nw, const RInst &rec, bool rec_supp, int64_t seq,
+                  int64_t *w) {
+    auto it = to_pair.find(name);
+    const bool known = it != to_pair.end();
+    RSlot &p = entry(name, seq);
+    if (!p.has[sl]) {
+      p.o[sl] = std::move(nw);
+      p.has[sl] = true;
     }
-    return 2;
+    if (known) {
+      RObj &o = p.o[sl];
+      if (!rec_supp && o.supp) {
+        generalize(o);
+        emit(4, o.id, rec.job, rec.ds, rec.row);
+        o.supp = false;
+      }
+      if (rec_supp) o.add_hash(record_id(rec.job, rec.ds, rec.row));
+    }
+    if (p.has[0] && p.has[1] && p.o[0].complete() && p.o[1].complete()) {
+      apply(p.o[0]);
+      apply(p.o[1]);
+      return write_pair(name, p.o[0], p.o[1], w);
+    }
+    return 0;
   }
 };
 
@@ -911,49 +1178,119 @@ GANON_HOST_API int ganon_resolver_contig(ganon_resolver *r, int32_t job, int64_t
                                          const int64_t *op_rows, const char *op_names, const int64_t *op_name_off,
                                          const int32_t *op_name_len, int64_t n_left, const int64_t *left,
                                          const char *left_names, const int64_t *left_name_off,
-                                         const int32_t *left_name_len, int32_t *out_n, int64_t *out_w) {
-  if (!r || n_ops < 0 || n_left < 0 || (n_ops > 0 && (!ops || !op_rows || !op_names || !op_name_off ||
-                                                       !op_name_len || !out_n || !out_w)) ||
-      (n_left > 0 && (!left || !left_names || !left_name_off || !left_name_len))) {
+                                         const int32_t *left_name_len, int64_t n_objs, const int64_t *objs,
+                                         const int64_t *obj_rows, int32_t *out_n, int64_t *out_w) {
+  if (!r || n_ops < 0 || n_left < 0 || n_objs < 0 ||
+      (n_ops > 0 && (!ops || !op_rows || !op_names || !op_name_off || !op_name_len || !out_n || !out_w)) ||
+      (n_left > 0 && (!left || !left_names || !left_name_off || !left_name_len)) || (n_objs > 0 && (!objs || !obj_rows))) {
     g_err = "resolver: bad argument";
     return GANON_PLAN_E_ARG;
   }
   try {
     const int64_t base = (int64_t)job << 32;
+    auto object = [&](int64_t k) {   // a plan object (ganon_plan_view.objs) as the resolver follows it
+      const int64_t *o = objs + 10 * k;
+      RObj x;
+      x.general = true;
+      x.id = base | k;
+      x.ds = (int32_t)o[1];
+      x.supp = o[4] < 0;
+      x.has_sa = (o[9] & 2) != 0;
+      x.n_sa = (int32_t)(o[9] >> 8);
+      for (int64_t h = 0; h < o[8]; ++h) x.add_hash(record_id(job, o[1], obj_rows[o[7] + h]));
+      return x;
+    };
     for (int64_t i = 0; i < n_ops; ++i) {
       const int32_t *e = ops + 7 * i;
       const std::string name(op_names + op_name_off[i], (size_t)op_name_len[i]);
       const RInst inst{job, e[4], e[5], op_rows[i]};
+      const int64_t seq = base | (int64_t)(uint32_t)e[6];
       out_n[i] = 0;
       if (e[0] == 3) {   // a complete pair in one scope: this op (slot 0) and the next (slot 1)
         if (i + 1 >= n_ops || ops[7 * (i + 1)] != 3) {
           g_err = "resolver: unpaired pair event";
           return GANON_PLAN_E_ARG;
         }
-        const RInst other{job, ops[7 * (i + 1) + 4], ops[7 * (i + 1) + 5], op_rows[i + 1]};
-        out_n[i] = r->write_pair(name, inst, other, out_w + 14 * i);
+        RObj a = plain_obj(inst);
+        RObj b = plain_obj(RInst{job, ops[7 * (i + 1) + 4], ops[7 * (i + 1) + 5], op_rows[i + 1]});
+        out_n[i] = r->write_pair(name, a, b, out_w + 14 * i);
         out_n[i + 1] = 0;
         ++i;
         continue;
       }
-      if (e[0] != 4 && e[0] != 5) {
+      if (e[0] == 4) {   // anonymize_window's consumer (SR:320-360) for an incomplete plain pair
+        RSlot &p = r->add_or_update(name, e[3], plain_obj(inst), seq);
+        if (p.has[0] && p.has[1] && p.o[0].complete() && p.o[1].complete()) {
+          r->apply(p.o[0]);
+          r->apply(p.o[1]);
+          out_n[i] = r->write_pair(name, p.o[0], p.o[1], out_w + 14 * i);
+          r->to_pair.erase(name);
+        }
+        continue;
+      }
+      if (e[0] == 5) {
+        out_n[i] = r->passthrough(name, e[3], plain_obj(inst), inst, false, seq, out_w + 14 * i);
+        continue;
+      }
+      if (e[0] == 7) {
+        if (op_rows[i] < 0 || op_rows[i] >= n_objs) {
+          g_err = "resolver: object index out of range";
+          return GANON_PLAN_E_ARG;
+        }
+        const int64_t *o = objs + 10 * op_rows[i];
+        RObj x = object(op_rows[i]);
+        out_n[i] = r->passthrough(name, e[3], std::move(x), RInst{job, o[1], -1, o[3]}, (o[9] & 1) != 0, seq,
+                                  out_w + 14 * i);
+        continue;
+      }
+      if (e[0] != 6 || !(e[2] & 1)) {
         g_err = "resolver: not a placeholder event";
         return GANON_PLAN_E_ARG;
       }
-      RSlot &p = r->store_first(name, e[3], inst, base | (int64_t)(uint32_t)e[6], e[0] == 4);
-      if (p.has[0] && p.has[1]) {
-        const RInst a = p.p[0], b = p.p[1];
-        out_n[i] = r->write_pair(name, a, b, out_w + 14 * i, p.upd[0], p.upd[1]);
-        if (e[0] == 4) r->to_pair.erase(name);   // anonymize_window pops a written pair (SR:360)
+      // the objects of one yield of a complex name (AM:489-532 + SR:304-361)
+      const int n = (e[2] >> 1) & 3;
+      if (n < 1 || i + n > n_ops) {
+        g_err = "resolver: bad object group";
+        return GANON_PLAN_E_ARG;
       }
+      RObj x[2];
+      int sl[2];
+      for (int k = 0; k < n; ++k) {
+        const int64_t oi = op_rows[i + k];
+        if (oi < 0 || oi >= n_objs || ops[7 * (i + k)] != 6) {
+          g_err = "resolver: bad object group";
+          return GANON_PLAN_E_ARG;
+        }
+        x[k] = object(oi);
+        sl[k] = ops[7 * (i + k) + 3];
+        out_n[i + k] = 0;
+      }
+      int64_t *w = out_w + 14 * i;
+      if (n == 2 && x[0].complete() && x[1].complete()) {
+        out_n[i] = r->write_pair(name, x[0], x[1], w);
+      } else {
+        for (int k = 0; k < n; ++k) r->add_or_update(name, sl[k], std::move(x[k]), seq);
+        RSlot &p = r->to_pair[name];
+        if (p.has[0] && p.has[1] && p.o[0].complete() && p.o[1].complete()) {
+          r->apply(p.o[0]);
+          r->apply(p.o[1]);
+          out_n[i] = r->write_pair(name, p.o[0], p.o[1], w);
+          r->to_pair.erase(name);
+        }
+      }
+      i += n - 1;
     }
     for (int64_t k = 0; k < n_left; ++k) {
       const int64_t *l = left + 11 * k;
       const std::string name(left_names + left_name_off[k], (size_t)left_name_len[k]);
       for (int s = 0; s < 2; ++s)
         if (l[1 + 4 * s]) {
-          RSlot &p = r->store_first(name, s, RInst{job, l[2 + 4 * s], l[3 + 4 * s], l[4 + 4 * s]}, base | l[0]);
-          if (l[9 + s]) p.upd[s] = true;
+          RSlot &p = r->entry(name, base | l[0]);
+          if (!p.has[s]) {
+            p.o[s] = plain_obj(RInst{job, l[2 + 4 * s], l[3 + 4 * s], l[4 + 4 * s]});
+            p.has[s] = true;
+          }
+          if (l[9 + s] && !p.o[s].general) p.o[s].upd = true;
         }
     }
   } catch (const std::bad_alloc &) {
@@ -963,6 +1300,16 @@ GANON_HOST_API int ganon_resolver_contig(ganon_resolver *r, int32_t job, int64_t
   return GANON_PLAN_OK;
 }
 
+GANON_HOST_API int64_t ganon_resolver_take_log(ganon_resolver *r, int64_t *out, int64_t cap) {
+  if (!r) return GANON_PLAN_E_ARG;
+  const int64_t n = (int64_t)r->log.size() / 8;
+  if (out && cap >= n) {
+    std::copy(r->log.begin(), r->log.end(), out);
+    r->log.clear();
+  }
+  return n;
+}
+
 GANON_HOST_API int64_t ganon_resolver_pending(ganon_resolver *r, int64_t *out, int64_t cap) {
   if (!r) return GANON_PLAN_E_ARG;
   int64_t n = 0;
@@ -970,12 +1317,19 @@ GANON_HOST_API int64_t ganon_resolver_pending(ganon_resolver *r, int64_t *out, i
     for (int s = 0; s < 2; ++s)
       if (kv.second.has[s]) {
         if (out && n < cap) {
-          const RInst &i = kv.second.p[s];
-          int64_t *o = out + 4 * n;
-          o[0] = i.job;
-          o[1] = i.ds;
-          o[2] = i.scope;
-          o[3] = i.row;
+          const RObj &o = kv.second.o[s];
+          int64_t *d = out + 4 * n;
+          if (o.general) {
+            d[0] = -1;
+            d[1] = o.ds;
+            d[2] = -2;
+            d[3] = o.id;
+          } else {
+            d[0] = o.inst.job;
+            d[1] = o.inst.ds;
+            d[2] = o.inst.scope;
+            d[3] = o.inst.row;
+          }
         }
         ++n;
       }
@@ -992,48 +1346,62 @@ GANON_HOST_API int ganon_resolver_finish(ganon_resolver *r, int64_t n_cand, cons
     return GANON_PLAN_E_ARG;
   }
   *n_tail = 0;
-  // pair_unmapped_mates (SR:561-600) runs only when something is left to pair (SR:752)
-  if (!r->to_pair.empty()) {
-    for (int64_t k = 0; k < n_cand; ++k) {
-      const int64_t *c = cand + 7 * k;
-      if (c[2] < 0) {   // this window's fetch(first - 1, last) raises (pysam region check)
-        g_err = "start out of range (" + std::to_string(c[3]) + ")";
-        return GANON_PLAN_E_VALUE;
-      }
-      const std::string name(names + name_off[k], (size_t)name_len[k]);
-      if (!r->to_pair.count(name)) continue;
-      if (c[5]) {
-        g_err = "read '" + name + "' has no SEQ; the reference cannot upper-case it";
-        return GANON_PLAN_E_TYPE;
-      }
-      if (c[4] < 0) {
-        g_err = "read '" + name + "' has neither the READ1 nor the READ2 flag; the reference cannot store it (SURVEY Q8)";
-        return GANON_PLAN_E_TYPE;
-      }
-      RSlot &p = r->store_first(name, (int)c[4], RInst{c[0], c[2], -1, c[3]}, INT64_MAX);
-      if (p.has[0] && p.has[1]) {
-        const RInst a = p.p[0], b = p.p[1];
-        *n_tail += r->write_pair(name, a, b, tail + 7 * *n_tail, p.upd[0], p.upd[1]);
+  try {
+    // pair_unmapped_mates (SR:561-600) runs only when something is left to pair (SR:752)
+    if (!r->to_pair.empty()) {
+      for (int64_t k = 0; k < n_cand; ++k) {
+        const int64_t *c = cand + 7 * k;
+        if (c[2] < 0) {   // this window's fetch(first - 1, last) raises (pysam region check)
+          g_err = "start out of range (" + std::to_string(c[3]) + ")";
+          return GANON_PLAN_E_VALUE;
+        }
+        const std::string name(names + name_off[k], (size_t)name_len[k]);
+        if (!r->to_pair.count(name)) continue;
+        if (c[5]) {
+          g_err = "read '" + name + "' has no SEQ; the reference cannot upper-case it";
+          return GANON_PLAN_E_TYPE;
+        }
+        if (c[4] < 0) {
+          g_err = "read '" + name + "' has neither the READ1 nor the READ2 flag; the reference cannot store it (SURVEY Q8)";
+          return GANON_PLAN_E_TYPE;
+        }
+        const RInst rec{c[0], c[2], -1, c[3]};
+        *n_tail += r->passthrough(name, (int)c[4], plain_obj(rec), rec, false, INT64_MAX, tail + 7 * *n_tail);
       }
     }
+    for (const std::string &k : r->written) r->to_pair.erase(k);
+    std::vector<std::pair<int64_t, RSlot *>> rest;
+    for (auto &kv : r->to_pair) rest.emplace_back(kv.second.seq, &kv.second);
+    std::stable_sort(rest.begin(), rest.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
+    n_single[0] = n_single[1] = 0;
+    for (auto &e : rest) {   // write_single_end_reads (SR:603-622): the READ1 object if any
+      const int sl = e.second->has[0] ? 0 : 1;
+      RObj &o = e.second->o[sl];
+      if (o.supp) continue;
+      int64_t *dst = (o.ds == 0 ? single0 : single1) + 5 * n_single[o.ds];
+      if (o.general) {
+        r->apply(o);
+        const int64_t serial = r->next_serial++;
+        r->emit(5, o.id, serial);
+        dst[0] = -1;
+        dst[1] = o.ds;
+        dst[2] = -2;
+        dst[3] = serial;
+        dst[4] = 0;
+      } else {
+        dst[0] = o.inst.job;
+        dst[1] = o.inst.ds;
+        dst[2] = o.inst.scope;
+        dst[3] = o.inst.row;
+        dst[4] = o.upd ? 1 : 0;
+      }
+      ++n_single[o.ds];
+    }
+    *write_single_end = r->to_pair.empty() ? 0 : 1;
+  } catch (const std::bad_alloc &) {
+    g_err = "out of memory";
+    return GANON_PLAN_E_NOMEM;
   }
-  for (const std::string &k : r->written) r->to_pair.erase(k);
-  std::vector<std::pair<int64_t, const RSlot *>> rest;
-  for (const auto &kv : r->to_pair) rest.emplace_back(kv.second.seq, &kv.second);
-  std::stable_sort(rest.begin(), rest.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
-  n_single[0] = n_single[1] = 0;
-  for (const auto &e : rest) {
-    const int sl = e.second->has[0] ? 0 : 1;
-    const RInst &i = e.second->p[sl];
-    int64_t *dst = (i.ds == 0 ? single0 : single1) + 5 * n_single[i.ds];
-    dst[0] = i.job;
-    dst[1] = i.ds;
-    dst[2] = i.scope;
-    dst[3] = i.row;
-    dst[4] = e.second->upd[sl] ? 1 : 0;
-    ++n_single[i.ds];
-  }
-  *write_single_end = r->to_pair.empty() ? 0 : 1;
   return GANON_PLAN_OK;
 }
 

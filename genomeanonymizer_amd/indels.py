@@ -43,19 +43,26 @@ class IndelCall:
     ref_allele: str
 
 
+def apply_indel(seq: bytearray, qual_fwd: List[int], irp: int, c: IndelCall):
+    """mask_or_modify_indel (AM:178-203) on (ASCII seq, forward qualities). Raises ValueError like
+    the reference when the lengths diverge."""
+    if c.variant_type is VariantType.INS:
+        seq = seq[:irp] + seq[irp + c.length:]
+        qual_fwd = qual_fwd[:irp] + qual_fwd[irp + c.length:]
+    elif c.variant_type is VariantType.DEL:
+        avg = int(float(sum(qual_fwd)) / len(qual_fwd)) if qual_fwd else _nan_int()
+        seq = seq[:irp] + bytearray(c.ref_allele.encode()) + seq[irp:]
+        qual_fwd = qual_fwd[:irp] + [avg] * c.length + qual_fwd[irp:]
+    if len(seq) != len(qual_fwd):
+        raise ValueError("Length of the modified qualities does not match the length of the modified sequence")
+    return seq, qual_fwd
+
+
 def apply_leftovers(seq: bytearray, qual_fwd: List[int], edits: List[Tuple[int, IndelCall]]):
     """mask_or_anonymize_left_over_variants + mask_or_modify_indel on (ASCII seq, forward
-    qualities). Raises ValueError like the reference when lengths diverge."""
+    qualities)."""
     for irp, c in sorted(edits, key=lambda e: e[1].variant_type.value):
-        if c.variant_type is VariantType.INS:
-            seq = seq[:irp] + seq[irp + c.length:]
-            qual_fwd = qual_fwd[:irp] + qual_fwd[irp + c.length:]
-        elif c.variant_type is VariantType.DEL:
-            avg = int(float(sum(qual_fwd)) / len(qual_fwd)) if qual_fwd else _nan_int()
-            seq = seq[:irp] + bytearray(c.ref_allele.encode()) + seq[irp:]
-            qual_fwd = qual_fwd[:irp] + [avg] * c.length + qual_fwd[irp:]
-        if len(seq) != len(qual_fwd):
-            raise ValueError("Length of the modified qualities does not match the length of the modified sequence")
+        seq, qual_fwd = apply_indel(seq, qual_fwd, irp, c)
     return seq, qual_fwd
 
 

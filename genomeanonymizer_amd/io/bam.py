@@ -165,6 +165,58 @@ class ReadTable:
                 raise ValueError(f"bad aux type in record {i}")
         return False
 
+    def may_be_complex(self) -> bool:
+        """Any secondary / supplementary record or SA tag candidate (cheap pre-check)."""
+        return bool(np.any(self.flag & (FLAG_SECONDARY | FLAG_SUPPLEMENTARY))) or self._sa_candidates().size > 0
+
+    def _sa_candidates(self) -> np.ndarray:
+        a = self.aux
+        if len(a) < 3:
+            return np.zeros(0, np.int64)
+        hit = np.nonzero((a[:-2] == ord("S")) & (a[1:-1] == ord("A")) & (a[2:] == ord("Z")))[0]
+        if not len(hit):
+            return np.zeros(0, np.int64)
+        rows = np.searchsorted(self.aux_off, hit, side="right") - 1
+        return np.unique(rows[(rows >= 0)])
+
+    def tag_value(self, i: int, tag: bytes):
+        """The value of a Z/H/A or integer tag of record ``i`` (None without it)."""
+        a = self.aux[self.aux_off[i]:self.aux_off[i] + self.aux_len[i]].tobytes()
+        j = 0
+        sizes = {ord(c): s for c, s in zip("AcCsSiIf", (1, 1, 1, 2, 2, 4, 4, 4))}
+        while j + 3 <= len(a):
+            t, ty = a[j:j + 2], a[j + 2]
+            j += 3
+            if ty in (ord("Z"), ord("H")):
+                k = a.index(b"\x00", j)
+                if t == tag:
+                    return a[j:k].decode()
+                j = k + 1
+            elif ty in sizes:
+                if t == tag:
+                    return a[j:j + sizes[ty]]
+                j += sizes[ty]
+            elif ty == ord("B"):
+                sub = a[j]
+                cnt = int.from_bytes(a[j + 1:j + 5], "little")
+                j += 5 + sizes[sub] * cnt
+            else:
+                raise ValueError(f"bad aux type in record {i}")
+        return None
+
+    def sa_count(self) -> np.ndarray:
+        """Per record: entries of its SA tag (``len(tag.rstrip(';').split(';'))``, AM:103-106), -1
+        without one (cached)."""
+        c = getattr(self, "_sa", None)
+        if c is None:
+            c = np.full(self.n, -1, np.int32)
+            for r in self._sa_candidates().tolist():
+                v = self.tag_value(r, b"SA")
+                if isinstance(v, str):
+                    c[r] = len(v.rstrip(";").split(";"))
+            self._sa = c
+        return c
+
     def cigar_of(self, i: int) -> np.ndarray:
         o = int(self.cig_off[i])
         return self.cigar[o:o + int(self.n_cigar[i])]

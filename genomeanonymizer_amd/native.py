@@ -95,6 +95,18 @@ BATCH_ARRAYS = {
 _PTR_OF = {np.int32: _i32p, np.int64: _i64p, np.uint8: _u8p, np.uint32: _u32p}
 
 
+def indel_view(arrays: dict) -> dict:
+    """The batch as the indel tally sees it: ``indel_incid_off``/``indel_incid_read`` (when the
+    plan leaves later alignments of a read out, anonymizer_methods.build_batch) replace the
+    incidence CSR."""
+    if "indel_incid_off" not in arrays:
+        return arrays
+    a = dict(arrays)
+    a["scope_incid_off"] = arrays["indel_incid_off"]
+    a["incid_read"] = arrays["indel_incid_read"]
+    return a
+
+
 def make_c_batch(arrays: dict, with_ref: bool = True) -> GanonBatch:
     """Build a GanonBatch over numpy arrays (kept alive by the caller's dict). ``with_ref`` False:
     the reference is resident on the device, ``ref_nt16`` may be absent."""
@@ -203,7 +215,7 @@ EXPORTED_HOST_SYMBOLS = (
     "ganon_bam_reader_open", "ganon_bam_reader_set_window", "ganon_bam_reader_has_index", "ganon_bam_reader_header",
     "ganon_bam_reader_contig", "ganon_bam_reader_close",
     "ganon_resolver_create", "ganon_resolver_free", "ganon_resolver_contig", "ganon_resolver_pending",
-    "ganon_resolver_finish",
+    "ganon_resolver_finish", "ganon_resolver_take_log",
 )
 
 
@@ -537,7 +549,8 @@ class DeviceBatch:
 
     def indel_tally(self, arrays: dict) -> "DeviceIndels":
         """Plan the germline indel tally of this batch (``arrays`` = the batch it was uploaded from)."""
-        b = make_c_batch(arrays)
+        iv = indel_view(arrays)
+        b = make_c_batch(iv)
         h = _p()
         self.m._check(self.m._lib.ganon_indel_upload(self.m._h, C.byref(b), self.h, C.byref(h)), "ganon_indel_upload")
         return DeviceIndels(self.m, h)
@@ -602,7 +615,8 @@ class PlanTable(C.Structure):
     """Mirror of ``ganon_plan_table`` (include/ganon_host.h)."""
     _fields_ = [("n", C.c_int64), ("tid", _i32p), ("pos", _i32p), ("end", _i32p), ("flag", _i32p),
                 ("l_seq", _i32p), ("n_cigar", _i32p), ("names", _p), ("name_off", _i64p), ("name_len", _i32p),
-                ("n_ref", C.c_int32), ("ref_len", _i64p), ("tid_of_contig", _i32p), ("mate_tid", _i32p)]
+                ("n_ref", C.c_int32), ("ref_len", _i64p), ("tid_of_contig", _i32p), ("mate_tid", _i32p),
+                ("n_sa", _i32p)]
 
 
 class PlanInput(C.Structure):
@@ -619,7 +633,9 @@ class PlanView(C.Structure):
                 ("t_rows", _i64p), ("n_rows", _i64p), ("n_events", C.c_int64), ("events", _i32p),
                 ("event_rows", _i64p), ("n_stats", C.c_int64), ("stats", _i32p),
                 ("n_single", C.c_int64 * 2), ("single", _i64p * 2), ("write_single_end", C.c_int32),
-                ("n_left", C.c_int64), ("left", _i64p), ("n_cand", C.c_int64), ("cand", _i64p)]
+                ("n_left", C.c_int64), ("left", _i64p), ("n_cand", C.c_int64), ("cand", _i64p),
+                ("n_objs", C.c_int64), ("objs", _i64p), ("n_obj_rows", C.c_int64), ("obj_rows", _i64p),
+                ("n_skip", C.c_int64), ("skip", _i64p)]
 
 
 PLAN_E_VALUE, PLAN_E_TYPE, PLAN_E_UNSUPPORTED = -10, -11, -12
@@ -660,6 +676,8 @@ def plan_sample(tables, contig_names, contig_lens, win_contig, win_first, win_la
         idx = {nm: i for i, nm in enumerate(t.ref_names)}
         pt.tid_of_contig = arr([idx.get(c, -1) for c in contig_names], np.int32)
         pt.mate_tid = arr(t.mate_tid, np.int32)
+        if only_contig is not None or t.may_be_complex():
+            pt.n_sa = arr(t.sa_count(), np.int32)
     inp.n_contigs = len(contig_names)
     inp.contig_len = arr(contig_lens, np.int64)
     blob = b"".join(c.encode() + b"\0" for c in contig_names) or b"\0"
@@ -710,6 +728,9 @@ def plan_sample(tables, contig_names, contig_lens, win_contig, win_first, win_la
         out["write_single_end"] = bool(v.write_single_end)
         out["left"] = _np_copy(v.left, 11 * int(v.n_left), np.int64).reshape(-1, 11)
         out["cand"] = _np_copy(v.cand, 5 * int(v.n_cand), np.int64).reshape(-1, 5)
+        out["objs"] = _np_copy(v.objs, 10 * int(v.n_objs), np.int64).reshape(-1, 10)
+        out["obj_rows"] = _np_copy(v.obj_rows, int(v.n_obj_rows), np.int64)
+        out["skip"] = _np_copy(v.skip, 3 * int(v.n_skip), np.int64).reshape(-1, 3)
     finally:
         lib.ganon_plan_free(h)
     return out
@@ -745,12 +766,16 @@ class Resolver:
         raise GanonError(f"resolver failed ({rc}): {msg}")
 
     def contig(self, job: int, ops: np.ndarray, op_rows: np.ndarray, op_names: list, left: np.ndarray,
-               left_names: list):
-        """Returns (n_writes per op, writes [n_ops, 2, 7])."""
+               left_names: list, objs: np.ndarray = None, obj_rows: np.ndarray = None):
+        """Returns (n_writes per op, writes [n_ops, 2, 7]); ``objs``/``obj_rows``: the plan's
+        objects of complex names (their log: ``take_log``)."""
         keep = []
         ops = np.ascontiguousarray(ops, np.int32).reshape(-1, 7)
         rows = np.ascontiguousarray(op_rows, np.int64)
         left = np.ascontiguousarray(left, np.int64).reshape(-1, 11)
+        objs = np.ascontiguousarray(np.zeros((0, 10), np.int64) if objs is None else objs, np.int64).reshape(-1, 10)
+        obj_rows = np.ascontiguousarray(np.zeros(0, np.int64) if obj_rows is None else obj_rows, np.int64)
+        keep += [objs, obj_rows]
         n = len(ops)
         out_n = np.zeros(max(n, 1), np.int32)
         out_w = np.zeros((max(n, 1), 2, 7), np.int64)
@@ -758,10 +783,18 @@ class Resolver:
         ln, lo, ll = _names_args(left_names, keep)
         rc = self._lib.ganon_resolver_contig(self._h, int(job), n, ops.ctypes.data_as(_i32p), rows.ctypes.data_as(_i64p),
                                              on, oo, ol, len(left), left.ctypes.data_as(_i64p), ln, lo, ll,
+                                             len(objs), objs.ctypes.data_as(_i64p), obj_rows.ctypes.data_as(_i64p),
                                              out_n.ctypes.data_as(_i32p), out_w.ctypes.data_as(_i64p))
         if rc != 0:
             self._err(rc)
         return out_n[:n], out_w[:n]
+
+    def take_log(self) -> np.ndarray:
+        """The object log entries made since the last call ([n, 8] int64, include/ganon_host.h)."""
+        n = self._lib.ganon_resolver_take_log(self._h, None, 0)
+        out = np.zeros((max(n, 1), 8), np.int64)
+        self._lib.ganon_resolver_take_log(self._h, out.ctypes.data_as(_i64p), n)
+        return out[:n]
 
     def pending(self) -> np.ndarray:
         k = self._lib.ganon_resolver_pending(self._h, None, 0)
@@ -847,7 +880,9 @@ def host_lib():
     lib.ganon_resolver_create.argtypes = [C.POINTER(_p)]
     lib.ganon_resolver_free.argtypes = [_p]
     lib.ganon_resolver_contig.argtypes = [_p, C.c_int32, C.c_int64, _i32p, _i64p, _p, _i64p, _i32p, C.c_int64, _i64p,
-                                          _p, _i64p, _i32p, _i32p, _i64p]
+                                          _p, _i64p, _i32p, C.c_int64, _i64p, _i64p, _i32p, _i64p]
+    lib.ganon_resolver_take_log.argtypes = [_p, _i64p, C.c_int64]
+    lib.ganon_resolver_take_log.restype = C.c_int64
     lib.ganon_resolver_pending.argtypes = [_p, _i64p, C.c_int64]
     lib.ganon_resolver_pending.restype = C.c_int64
     lib.ganon_resolver_finish.argtypes = [_p, C.c_int64, _i64p, _p, _i64p, _i32p, _i64p, _i64p, _i64p, _i64p,

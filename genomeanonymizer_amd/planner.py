@@ -237,7 +237,9 @@ class SamplePlanner:
     native = False
     # ---- input checks --------------------------------------------------------------------
     def _check_supported(self, names: bool = True) -> None:
-        for ds, t in enumerate(self.tables):
+        # the native planner plans complex names in contig mode and refuses them in whole-sample
+        # mode itself (csrc/ganon_plan.cpp); this Python restatement does not plan them
+        for ds, t in enumerate(self.tables if not self.native else ()):
             if np.any(t.flag & (FLAG_SECONDARY | FLAG_SUPPLEMENTARY)):
                 raise UnsupportedInput("secondary/supplementary alignments are not supported yet "
                                        "(reference: AnonymizedRead supplementary bookkeeping, AM:98-137)")
@@ -589,7 +591,8 @@ class NativeSamplePlanner(SamplePlanner):
         res = native.plan_sample(self.tables, refs, list(self.fasta.lengths),
                                  [cidx[x.sequence] for x in w], [x.first for x in w], [x.last for x in w],
                                  only_contig=self.only_contig)
-        self.contig_exports = {"left": res["left"], "cand": res["cand"]}
+        self.contig_exports = {"left": res["left"], "cand": res["cand"], "objs": res["objs"],
+                               "obj_rows": res["obj_rows"]}
         T, N = self.tables
         t_rows, n_rows = res["t_rows"], res["n_rows"]
         to, no = res["scope_t_off"], res["scope_n_off"]
@@ -611,8 +614,10 @@ class NativeSamplePlanner(SamplePlanner):
                 self.stats_events.append(("scope", val))
         single = {d: [(d, r, s) for r, s, _ in res["single"][d].tolist()] for d in (0, 1)}
         reapply = {d: [x for _, _, x in res["single"][d].tolist()] for d in (0, 1)}
-        return Plan(self.scopes, None, single, self.stats_events, res["write_single_end"], single_reapply=reapply,
+        plan = Plan(self.scopes, None, single, self.stats_events, res["write_single_end"], single_reapply=reapply,
                     events=res["events"], event_rows=res["event_rows"])
+        plan.skip = res["skip"]
+        return plan
 
 
 class ContigPlanner(NativeSamplePlanner):

@@ -34,6 +34,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import native
+from . import objects
 from .anonymizer_methods import CompleteGermlineAnonymizer, MaskResult
 from .io.bam import BamReader, ReadTable
 from .io.fasta import FastaRef
@@ -75,14 +76,51 @@ class Job:
         ev, rows = self.plan.io_arrays()
         self.events, self.event_rows = ev, rows
         self.ph = np.nonzero(ev[:, 0] >= 3)[0]
+        self.plain_ph = self.ph[ev[self.ph, 0] <= 5]   # kinds 6 / 7 carry objects of complex names
         self.left = ex["left"]
         self.cand = ex["cand"]
+        self.objs, self.obj_rows = ex["objs"], ex["obj_rows"]
         self.masked_scope = [np.full(t.n, -1, np.int64) for t in self.tables]
         written = self._mask_instances()
         self.res: MaskResult = anonymizer.anonymize(planner, self.plan, written=written)
         t3 = time.time()
         self.fmt = FastqFormatter(self.tables, self.res, anonymizer.format_fastq)
+        self.cx = self._complex_ingredients()
         self.timing = {"decode_s": t1 - t0, "plan_s": t2 - t1, "mask_s": t3 - t2}
+
+    def _complex_incidences(self):
+        """(dataset, row, scope) of every alignment of a complex name's object in a scope."""
+        O = self.objs
+        out = []
+        for k in np.nonzero(O[:, 0] >= 0)[0].tolist() if len(O) else []:
+            sc, ds, a_off, a_n = int(O[k, 0]), int(O[k, 1]), int(O[k, 5]), int(O[k, 6])
+            for a in self.obj_rows[a_off:a_off + a_n].tolist():
+                out.append((ds, a, sc))
+        return sorted(set(out))
+
+    def _complex_ingredients(self) -> Optional[dict]:
+        """What objects.Replay needs of this job's complex names: their records and, per (alignment,
+        scope), the bases the device masked and the indel left-overs."""
+        O = self.objs
+        if not len(O):
+            return None
+        rec = {}
+        for k in range(len(O)):
+            ds, c, base, a_off, a_n = int(O[k, 1]), int(O[k, 3]), int(O[k, 4]), int(O[k, 5]), int(O[k, 6])
+            for r in [c, base] + self.obj_rows[a_off:a_off + a_n].tolist():
+                if r >= 0 and (ds, r) not in rec:
+                    rec[(ds, r)] = objects.record_of(self.tables[ds], r)
+        masks, indels = {}, {}
+        for ds, a, sc in self._complex_incidences():
+            r = rec[(ds, a)]
+            nib = self.res.masked_nib(self.tables, ds, a, sc)
+            d = objects.mask_diffs(r, objects.decode_nt16(self.res.seq_out, nib, len(r.seq)))
+            if d:
+                masks[(ds, a, sc)] = d
+            e = self.res.leftovers.get((ds, a, sc))
+            if e:
+                indels[(ds, a, sc)] = list(e)
+        return {"objs": O, "obj_rows": self.obj_rows, "rec": rec, "masks": masks, "indels": indels}
 
     # -- which masked copy of each read the device produces --------------------------------------
     def _mask_instances(self):
@@ -92,7 +130,7 @@ class Job:
         parts = []
         w = ev[:, 0] == 1
         parts.append((ev[w, 4].astype(np.int64), rows[w], ev[w, 5].astype(np.int64)))
-        p = self.ph
+        p = self.plain_ph
         parts.append((ev[p, 4].astype(np.int64), rows[p], ev[p, 5].astype(np.int64)))
         L = self.left
         for s in (0, 1):
@@ -112,7 +150,12 @@ class Job:
             key = ds * (1 << 40) + rw
             _, first = np.unique(key, return_index=True)
             keep[first] = True
-        return ds[keep], rw[keep], sc[keep]
+        ds, rw, sc = ds[keep], rw[keep], sc[keep]
+        cx = self._complex_incidences()     # every (alignment, scope) of a complex name: one copy each
+        if cx:
+            c = np.array(cx, np.int64)
+            ds, rw, sc = np.concatenate([ds, c[:, 0]]), np.concatenate([rw, c[:, 1]]), np.concatenate([sc, c[:, 2]])
+        return ds, rw, sc
 
     def check_instance(self, ds: int, row: int, scope: int) -> None:
         if scope >= 0 and self.masked_scope[ds][row] != scope:
@@ -140,6 +183,11 @@ class Job:
         ops = ev[p]
         op_rows = rows[p]
         op_ds = ops[:, 4].astype(np.int64)
+        plain = ops[:, 0] <= 5
+        O = self.objs
+        op_name_rows = op_rows.copy()
+        if len(O) and not np.all(plain):   # objects: the name of their creator
+            op_name_rows[~plain] = O[op_rows[~plain], 3]
         L = self.left
         left_ds = np.where(L[:, 1] == 1, L[:, 2], L[:, 6]) if len(L) else np.zeros(0, np.int64)
         left_row = np.where(L[:, 1] == 1, L[:, 4], L[:, 8]) if len(L) else np.zeros(0, np.int64)
@@ -154,7 +202,7 @@ class Job:
         for i, nm in zip(idx.tolist(), _names_ds(self.tables, C[idx, 1], C[idx, 2])):
             cand_names[i] = nm
         # carried records: every instance the resolution may write outside this job
-        inst = [(ops[:, 4].astype(np.int64), op_rows, ops[:, 5].astype(np.int64))]
+        inst = [(ops[plain, 4].astype(np.int64), op_rows[plain], ops[plain, 5].astype(np.int64))]
         for s in (0, 1):
             h = L[:, 1 + 4 * s] == 1 if len(L) else np.zeros(0, bool)
             inst.append((L[h, 2 + 4 * s], L[h, 4 + 4 * s], L[h, 3 + 4 * s]))
@@ -163,6 +211,7 @@ class Job:
         rw = np.concatenate([x[1] for x in inst]).astype(np.int64)
         sc = np.concatenate([x[2] for x in inst]).astype(np.int64)
         carry: Dict[Key, bytes] = {}
+        info: dict = {}
         if len(ds):
             key = np.stack([ds, sc, rw], axis=1)
             _, first = np.unique(key, axis=0, return_index=True)
@@ -173,17 +222,24 @@ class Job:
             for i, b in zip(first.tolist(), recs):
                 inst = (int(ds[i]), int(rw[i]), int(sc[i]))
                 carry[(self.job, inst[0], inst[2], inst[1], 0)] = b
+                info[(self.job, inst[0], inst[1])] = int(self.tables[inst[0]].flag[inst[1]])
                 if inst in self.res.leftovers:   # written later with its left-overs applied twice
                     carry[(self.job, inst[0], inst[2], inst[1], 1)] = self.fmt.edited_bytes(inst, 1)
+                    # the record before its edits and the edits (objects.Replay, complex names)
+                    carry[(self.job, inst[0], inst[2], inst[1], 2)] = self.fmt._native(
+                        np.array([inst[0]]), np.array([inst[1]]), np.array([inst[2]]))
+                    info[(self.job, inst[0], inst[2], inst[1])] = list(self.res.leftovers[inst])
         return {
             "job": self.job, "ops": ops, "op_rows": op_rows,
-            "op_names": _names_ds(self.tables, op_ds, op_rows),
+            "op_names": _names_ds(self.tables, op_ds, op_name_rows),
             "left": L, "left_names": _names_ds(self.tables, left_ds, left_row),
-            "cand": cand, "cand_names": cand_names, "carry": carry,
+            "cand": cand, "cand_names": cand_names, "carry": carry, "carry_info": info,
+            "objs": O, "obj_rows": self.obj_rows, "cx": self.cx,
         }
 
     # -- output ----------------------------------------------------------------------------------
-    def output(self, out_n: np.ndarray, out_w: np.ndarray, carry: Dict[Key, bytes], block: int) -> List[bytes]:
+    def output(self, out_n: np.ndarray, out_w: np.ndarray, carry: Dict[Key, bytes], block: int,
+               replay: "objects.Replay" = None) -> List[bytes]:
         """The job's bytes per output file (tumor .1, .2, normal .1, .2) with the resolved writes of
         its placeholder events spliced into its I/O log."""
         ev, rows = self.events, self.event_rows
@@ -215,9 +271,10 @@ class Job:
         wr = fin[:, 0] == 1
         fin[~wr, 6] = 0
         reap = fin[:, 6].astype(np.int64)
-        ext = wr & (fjob != self.job)
+        gen = wr & (fin[:, 5] == -2)        # an object of a complex name (objects.Replay)
+        ext = wr & ((fjob != self.job) | gen)
         loc = wr & ~ext
-        chk = np.nonzero(loc & (fin[:, 5] >= 0))[0]
+        chk = np.nonzero(loc & (fin[:, 5] >= 0))[0]   # plain local writes only (gen is ext)
         if len(chk):
             d, r, sc = fin[chk, 4].astype(np.int64), frow[chk], fin[chk, 5].astype(np.int64)
             ms = np.where(d == 0, self.masked_scope[0][np.where(d == 0, r, 0)] if self.tables[0].n else -1,
@@ -231,6 +288,10 @@ class Job:
         rec_len[li] = self.record_lengths(fin[li, 4], frow[li], fin[li, 5], reap[li])
         ext_bytes: Dict[int, bytes] = {}
         for i in np.nonzero(ext)[0].tolist():
+            if gen[i]:
+                ext_bytes[i] = replay.take(int(frow[i]))
+                rec_len[i] = len(ext_bytes[i])
+                continue
             b = carry.get((int(fjob[i]), int(fin[i, 4]), int(fin[i, 5]), int(frow[i]), int(reap[i])))
             if b is None and reap[i]:   # a carried record without left-overs: the same bytes
                 b = carry.get((int(fjob[i]), int(fin[i, 4]), int(fin[i, 5]), int(frow[i]), 0))
@@ -325,6 +386,8 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
     contigs = list(fasta.references)
     resolver = native.Resolver()
     carry: Dict[Key, bytes] = {}
+    carry_info: dict = {}
+    replay = objects.Replay(carry, carry_info)
     cands: List[np.ndarray] = []
     cand_names: List[bytes] = []
     base = [0, 0, 0, 0]
@@ -360,9 +423,12 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
                 e = g["exp"]
                 if e is None:
                     continue
-                out_n, out_w = resolver.contig(e["job"], e["ops"], e["op_rows"], e["op_names"], e["left"],
-                                               e["left_names"])
                 carry.update(e["carry"])
+                carry_info.update(e["carry_info"])
+                replay.add_job(e["job"], e["cx"])
+                out_n, out_w = resolver.contig(e["job"], e["ops"], e["op_rows"], e["op_names"], e["left"],
+                                               e["left_names"], e["objs"], e["obj_rows"])
+                replay.run(resolver.take_log())
                 cands.append(e["cand"])
                 cand_names.extend(e["cand_names"])
                 if job is not None and e["job"] == job.job:
@@ -371,7 +437,7 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
             data = [b"", b"", b"", b""]
             if job is not None:
                 try:
-                    data = job.output(mine[0], mine[1], carry, block_size)
+                    data = job.output(mine[0], mine[1], carry, block_size, replay)
                     stats_rows.append((job.job, job.stats()))
                 except BaseException as e:
                     failure, err = e, repr(e)
@@ -388,21 +454,30 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
                 base[f] += sum(g["sizes"][f] for g in sizes)
             # carried records still reachable: pending pairs and the end-of-sample candidates
             pend = resolver.pending()
+            replay.settle(pend)
             live = set(map(tuple, pend.tolist()))
             for c in cands:
                 for r in c[c[:, 2] >= 0].tolist() if len(c) else []:
                     live.add((r[0], r[2], -1, r[3]))
             for k in [k for k in carry if k[:4] not in live]:
                 del carry[k]
+            live_rows = {(k[0], k[1], k[3]) for k in live}
+            for k in [k for k in carry_info if (k if len(k) == 3 else (k[0], k[1], k[3])) not in live_rows
+                      or (len(k) == 4 and k not in live)]:
+                del carry_info[k]
+            replay.written.clear()     # serials of the other ranks' jobs
             job = None
             timing["resolve_s"] += t1 - t0
             timing["write_s"] += time.time() - t1
         # ---- end of the sample: pair_unmapped_mates, single ends (SR:561-622) ----
         cand = np.concatenate(cands) if cands else np.zeros((0, 7), np.int64)
         tail, single, wse = resolver.finish(cand, cand_names)
+        replay.run(resolver.take_log())
         if rank == 0:
             per_file: List[List[bytes]] = [[], [], [], []]
             def carried(k):
+                if k[2] == -2:
+                    return replay.take(k[3])
                 b = carry.get(k)
                 return b if b is not None else carry[k[:4] + (0,)]
             for w in tail.tolist():

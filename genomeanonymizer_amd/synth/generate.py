@@ -61,6 +61,8 @@ class ScenarioConfig:
     unplaced_frac: float = 0.0      # of the unmapped mates: unplaced (tid -1)
     cross_contig_pairs: int = 0     # per sample: pairs with mates on two different contigs
     bam_index: bool = False         # also write <bam>.bai
+    chimeric_frac: float = 0.0      # per mapped 150M read: split into a primary + a hard-clipped supplementary (SA tags)
+    secondary_frac: float = 0.0     # per mapped read: an extra secondary alignment (flag 0x100) elsewhere
 
 
 @dataclasses.dataclass
@@ -218,6 +220,49 @@ def _base_events(ev):
     return [i for i, e in enumerate(ev) if e[0] != "D"]
 
 
+def _add_split_alignments(recs, cfg, models, rng):
+    """BWA-style extra alignments: a mapped all-M read becomes a primary (aligned head, soft-clipped
+    tail) plus a supplementary record of its tail elsewhere (hard-clipped head, flag 0x800), each with
+    an SA tag naming the other; or it gains a secondary alignment (flag 0x100, full sequence)
+    elsewhere. The tail's bases are the read's own (they mismatch their new reference site)."""
+    out = []
+    names = [m.spec.name for m in models]
+    for r in recs:
+        if r.flag & 4 or r.tid < 0 or len(r.cigar) != 1 or r.cigar[0][0] != "M":
+            out.append(r)
+            continue
+        L = len(r.seq)
+        x = rng.random()
+        if x < cfg.chimeric_frac and L > 60:
+            k = int(rng.integers(30, L - 30))
+            if rng.random() < 0.5:            # near the primary (same scope / section) or anywhere
+                ti = r.tid
+                lo = max(0, r.pos - 3000)
+                spos = int(rng.integers(lo, max(lo + 1, min(models[ti].spec.length - (L - k) - 2, r.pos + 3000))))
+            else:
+                ti = int(rng.integers(0, len(models)))
+                spos = int(rng.integers(0, models[ti].spec.length - (L - k) - 2))
+            strand = "-" if r.flag & 16 else "+"
+            s_rev = bool(rng.random() < 0.5)      # the tail may align on either strand
+            sstrand = "-" if s_rev else "+"
+            prim = BamRecord(r.name, r.flag, r.tid, r.pos, r.mapq, [("M", k), ("S", L - k)], r.mate_tid, r.mate_pos,
+                             r.tlen, r.seq, r.qual,
+                             [("SA", "Z", f"{names[ti]},{spos + 1},{sstrand},{k}H{L - k}M,60,0;")])
+            supp = BamRecord(r.name, (r.flag & ~0x12) | 0x800 | (0x10 if s_rev else 0), ti, spos, 60,
+                             [("H", k), ("M", L - k)], r.mate_tid, r.mate_pos, 0, r.seq[k:], list(r.qual)[k:],
+                             [("SA", "Z", f"{names[r.tid]},{r.pos + 1},{strand},{k}M{L - k}S,{r.mapq},0;")])
+            out += [prim, supp]
+        elif x < cfg.chimeric_frac + cfg.secondary_frac:
+            ti = r.mate_tid if r.mate_tid >= 0 else r.tid    # BWA-style: near the mate's contig
+            spos = int(rng.integers(0, models[ti].spec.length - L - 2))
+            sec = BamRecord(r.name, r.flag | 0x100, ti, spos, 0, [("M", L)], r.mate_tid, r.mate_pos, 0, r.seq,
+                            list(r.qual))
+            out += [r, sec]
+        else:
+            out.append(r)
+    return out
+
+
 def generate(cfg: ScenarioConfig, outdir: str) -> Dict[str, str]:
     """Write ``ref.fa``(+fai), ``tumor.bam``, ``normal.bam``, ``variants.vcf``,
     ``samples.tsv`` and ``truth.json`` into ``outdir``. Returns the paths."""
@@ -351,8 +396,10 @@ def generate(cfg: ScenarioConfig, outdir: str) -> Dict[str, str]:
                                   rng.integers(2, 41, len(sa)).tolist()))
             recs.append(BamRecord(name, fb, tb, pb, 60, ob, ta, pa, 0, "".join(sb),
                                   rng.integers(2, 41, len(sb)).tolist()))
+        if cfg.chimeric_frac or cfg.secondary_frac:
+            recs = _add_split_alignments(recs, cfg, models, rng)
         recs.sort(key=lambda r: (r.tid if r.tid >= 0 else 1 << 30, r.pos, bool(r.flag & 4), r.name,
-                                 r.flag & 0xC0))
+                                 r.flag & 0xC0, r.flag & 0x900))
         path = os.path.join(outdir, "tumor.bam" if sample == "T" else "normal.bam")
         write_bam(path, contig_lens, recs, index=cfg.bam_index)
         paths[sample] = path
@@ -400,7 +447,10 @@ def fuzz_scenario(seed: int) -> ScenarioConfig:
                           germline_snp_per_kb=float(rng.uniform(3, 10)),
                           germline_indel_per_kb=float(rng.uniform(1, 4)), hom_fraction=0.3,
                           softclip_frac=0.05, unmapped_mate_frac=0.05, n_base_frac=0.03,
-                          unplaced_frac=0.4, cross_contig_pairs=int(rng.integers(5, 30)))
+                          unplaced_frac=0.4, cross_contig_pairs=int(rng.integers(5, 30)),
+                          # seeds >= 1000: BWA-style supplementary (SA) and secondary alignments too
+                          chimeric_frac=0.15 if seed >= 2000 else 0.03 if seed >= 1000 else 0.0,
+                          secondary_frac=0.08 if seed >= 2000 else 0.02 if seed >= 1000 else 0.0)
 
 
 def scenario(name: str) -> ScenarioConfig:

@@ -122,6 +122,9 @@ typedef struct ganon_plan_table {  /* one sample, file order (columns of a ganon
   const int64_t *ref_len;          /* [n_ref] BAM header lengths                            */
   const int32_t *tid_of_contig;    /* [n_contigs] this BAM's tid of each FASTA contig, -1 none */
   const int32_t *mate_tid;         /* per record; read only in contig mode                    */
+  const int32_t *n_sa;             /* per record: entries of its SA tag, -1 without one; NULL = none.
+                                      Records with an SA tag or the SECONDARY / SUPPLEMENTARY flag make
+                                      their name "complex" (contig mode only; see ganon_plan_view.objs) */
 } ganon_plan_table;
 typedef struct ganon_plan_input {
   ganon_plan_table tables[2];      /* 0 tumor, 1 normal                                      */
@@ -172,6 +175,24 @@ typedef struct ganon_plan_view {
   int64_t n_cand;
   const int64_t *cand;       /* 5 per record: window, dataset (-1: this window's fetch raises), row,
                                 slot (-1: no READ1/READ2 flag), 1 if the record has no SEQ */
+  /* contig mode, complex names (a record with an SA tag, or a secondary / supplementary alignment):
+   * the reference's AnonymizedRead objects (anonymizer_methods.py:84-287) of such a name are planned
+   * here and resolved sample-wide. objs: 10 int64 per object: scope (-1: created by a pass-through),
+   * dataset, slot, creator row (the alignment that created it: orientation, SA count), base row (the
+   * first non-supplementary alignment, whose sequence it holds; -1: still supplementary), offset and
+   * count in obj_rows of its alignments in the scope (registration order), offset and count in
+   * obj_rows of the supplementary records it recorded, creator info (bit 0 supplementary, bit 1 has an
+   * SA tag, bits 8.. SA entries). Events kind 6: the objects of one yield of a complex name (e[2] bit 0
+   * first event of the group, bits 1..2 objects in the group; e[3] slot, e[4] dataset, e[5] scope,
+   * e[6] clock, row = object index); kind 7: a pass-through record of a complex name (row = object).
+   * skip: 3 per incidence (scope, dataset, row) left out of the indel tally (a later alignment of a
+   * read already met in the scope: seen_read_alns, variation_classifier.py:196-207). */
+  int64_t n_objs;
+  const int64_t *objs;
+  int64_t n_obj_rows;
+  const int64_t *obj_rows;
+  int64_t n_skip;
+  const int64_t *skip;
 } ganon_plan_view;
 /* Returns GANON_PLAN_OK or a GANON_PLAN_E_* code (message: ganon_plan_last_error()). */
 GANON_HOST_API int ganon_plan_run(const ganon_plan_input *in, ganon_plan **out);
@@ -195,9 +216,20 @@ GANON_HOST_API int ganon_resolver_contig(ganon_resolver *r, int32_t job, int64_t
                                          const int64_t *op_rows, const char *op_names, const int64_t *op_name_off,
                                          const int32_t *op_name_len, int64_t n_left, const int64_t *left,
                                          const char *left_names, const int64_t *left_name_off,
-                                         const int32_t *left_name_len, int32_t *out_n, int64_t *out_w);
-/* Pending instances (4 int64 each: job, dataset, scope, row); returns the count (all of them when
- * cap >= count, else only the count). */
+                                         const int32_t *left_name_len, int64_t n_objs, const int64_t *objs,
+                                         const int64_t *obj_rows, int32_t *out_n, int64_t *out_w);
+/* Complex names (ganon_plan_view.objs): an object is identified by (job << 32) | index for the plan's
+ * objects, or 1 << 62 | k for a plain instance the resolver had to follow as an object. A write of an
+ * object is (file dataset, slot, -1, dataset, -2, serial, 0); what it writes follows from the object
+ * log, 8 int64 per entry, in order: (1, id, job, dataset, scope, row, reapply, 0) a plain instance
+ * becomes object id; (2, dst, src) update_anonymized_read_from_other(dst, src) (AM:281-287);
+ * (3, id) mask_or_anonymize_left_over_variants if flagged (AM:254-270); (4, id, job, dataset, row)
+ * update_from_primary_mapping with that record (AM:142-149); (5, id, serial) the object is written.
+ * ganon_resolver_take_log copies the entries made since the last call and returns their count (all of
+ * them, and clears the log, when cap >= count). */
+GANON_HOST_API int64_t ganon_resolver_take_log(ganon_resolver *r, int64_t *out, int64_t cap);
+/* Pending instances (4 int64 each: job, dataset, scope, row; an object: -1, dataset, -2, id); returns
+ * the count (all of them when cap >= count, else only the count). */
 GANON_HOST_API int64_t ganon_resolver_pending(ganon_resolver *r, int64_t *out, int64_t cap);
 /* cand: 7 int64 per record (job, window, dataset, row, slot, no-SEQ flag, 0) in window order, with
  * names. tail (14 int64 per candidate) receives the writes of pair_unmapped_mates (count n_tail);

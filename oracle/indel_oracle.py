@@ -68,14 +68,18 @@ class _Call:
 def indel_records(a: dict) -> List[tuple]:
     n_scopes = len(a["scope_span_start"])
     inc_off = a["scope_incid_off"]
+    # tallied reads: the batch's indel CSR when the plan leaves later alignments out (seen_read_alns)
+    t_off = a.get("indel_incid_off", inc_off)
+    t_read = a.get("indel_incid_read", a["incid_read"])
     out: List[tuple] = []
     seq_cache: Dict[int, str] = {}
     end_cache: Dict[int, int] = {}
     for s in range(n_scopes):
         reads = a["incid_read"][int(inc_off[s]):int(inc_off[s + 1])].astype(np.int64)
-        order = np.argsort(a["ref_start"][reads], kind="stable")
+        tallied = t_read[int(t_off[s]):int(t_off[s + 1])].astype(np.int64)
+        order = np.argsort(a["ref_start"][tallied], kind="stable")
         calls: Dict[int, List[_Call]] = {}
-        for r in reads[order].tolist():
+        for r in tallied[order].tolist():
             c0 = int(a["cig_off"][r])
             cig = a["cigar"][c0:c0 + int(a["n_cig"][r])].tolist()
             if not any((w & 0xF) in (1, 2) for w in cig):

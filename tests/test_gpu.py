@@ -226,6 +226,16 @@ def test_hip_pipeline_matches_reference(name, whole, tmp_path, hip_built, monkey
     assert bad == {}
 
 
+@pytest.mark.parametrize("name", ["fuzz1001", "fuzz2000", "fuzz2003"])
+def test_hip_pipeline_split_alignments_match_reference(name, tmp_path, hip_built, monkeypatch):
+    """Supplementary (SA) and secondary alignments through the streamed HIP product: one device copy
+    per (alignment, scope), the object log replayed over them (objects.py); the reference's files."""
+    from genomeanonymizer_amd.anonymizer_methods import CompleteGermlineAnonymizer
+    monkeypatch.setenv("GANON_WHOLE_SAMPLE", "0")
+    bad = run_pipeline_vs_golden(name, str(tmp_path / name), CompleteGermlineAnonymizer(device=0))
+    assert bad == {}
+
+
 def test_hip_streaming_matches_whole_sample_many_contigs(tmp_path, hip_built, monkeypatch):
     """The streamed product (per-contig decode, contig-mode plans, one HIP batch per contig with the
     genome resident, cross-contig resolution) against the whole-sample product on a 12-contig

@@ -33,6 +33,29 @@ def test_pipeline_with_oracle_matches_reference(name, whole, tmp_path, monkeypat
     assert bad == {}
 
 
+@pytest.mark.parametrize("name", ["fuzz1001", "fuzz2000", "fuzz2003"])
+def test_pipeline_split_alignments_match_reference(name, tmp_path, monkeypatch):
+    """Supplementary alignments with SA tags (chimeric reads, the tail on either strand, near the
+    primary or on another contig) and secondary alignments: the reference's AnonymizedRead object
+    model (creator orientation, primary promotion, supplementary-coordinate masks, left-over
+    merges; objects.py) through the streamed product, against the reference's own files."""
+    from pyoracle import OracleEngine
+    from genomeanonymizer_amd.anonymizer_methods import CompleteGermlineAnonymizer
+    monkeypatch.setenv("GANON_WHOLE_SAMPLE", "0")
+    bad = run_pipeline_vs_golden(name, str(tmp_path / name), CompleteGermlineAnonymizer(engine=OracleEngine()))
+    assert bad == {}
+
+
+def test_whole_sample_refuses_split_alignments(tmp_path, monkeypatch):
+    """The whole-sample planner does not restate the object model: it refuses such input loudly."""
+    from pyoracle import OracleEngine
+    from genomeanonymizer_amd.anonymizer_methods import CompleteGermlineAnonymizer
+    from genomeanonymizer_amd.planner import UnsupportedInput
+    monkeypatch.setenv("GANON_WHOLE_SAMPLE", "1")
+    with pytest.raises(UnsupportedInput):
+        run_pipeline_vs_golden("fuzz1001", str(tmp_path / "w"), CompleteGermlineAnonymizer(engine=OracleEngine()))
+
+
 def test_oracle_known_answers():
     """Hand-built scope: TN SNV masked, T-only kept, N base ignored, kept variant kept."""
     from pyoracle import OracleEngine

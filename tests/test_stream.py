@@ -13,7 +13,7 @@ import pytest
 import torch.multiprocessing as mp
 
 
-def _scenario(seed: int, n_contigs: int = 4):
+def _scenario(seed: int, n_contigs: int = 4, split: bool = False):
     from genomeanonymizer_amd.synth.generate import ContigSpec, ScenarioConfig
     rng = np.random.default_rng(seed)
     contigs = []
@@ -31,7 +31,8 @@ def _scenario(seed: int, n_contigs: int = 4):
     return ScenarioConfig(name=f"s{seed}", seed=seed, contigs=contigs, germline_snp_per_kb=5.0,
                           germline_indel_per_kb=1.0, hom_fraction=0.3, softclip_frac=0.05,
                           unmapped_mate_frac=0.04, n_base_frac=0.03, unplaced_frac=0.4, cross_contig_pairs=15,
-                          bam_index=bool(seed % 2))
+                          bam_index=bool(seed % 2), chimeric_frac=0.1 if split else 0.0,
+                          secondary_frac=0.05 if split else 0.0)
 
 
 def _outputs(prefixes, stats_path):
@@ -153,11 +154,13 @@ def _rank_worker(rank, world, port, paths, outdir, q):
         dist.destroy_process_group()
 
 
-def test_three_ranks_match_one_rank(tmp_path):
-    """3 ranks over 5 contigs (the last round leaves a rank idle): the files equal one rank's."""
+@pytest.mark.parametrize("split", [False, True], ids=["plain", "split_alignments"])
+def test_three_ranks_match_one_rank(split, tmp_path):
+    """3 ranks over 5 contigs (the last round leaves a rank idle): the files equal one rank's; with
+    supplementary / secondary alignments the objects of complex names cross the ranks' contigs."""
     from test_distributed import _free_port
     from genomeanonymizer_amd.synth.generate import generate
-    paths = generate(_scenario(23, n_contigs=5), str(tmp_path / "in"))
+    paths = generate(_scenario(23, n_contigs=5, split=split), str(tmp_path / "in"))
     one = _run(paths, str(tmp_path / "one"), False)
     stats_one = one.pop("stats")
     os.remove(paths["N"] + ".statistics.txt")

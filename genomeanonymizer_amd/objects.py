@@ -118,12 +118,14 @@ class State:
         """mask_or_anonymize_left_over_variants when flagged (AM:254-270)."""
         if not self.flag:
             return
+        self.flag = False
+        if self.seq is None:          # content never written (Replay._plain_object)
+            return
         for kind, pos, x in sorted(self.left, key=lambda e: _TYPE_ORDER[e[0]]):
             if kind == "S":
                 self.put(pos, x)
             else:
                 self.seq, self.qual = apply_indel(self.seq, self.qual, pos, x)
-        self.flag = False
 
     def absorb(self, other: "State") -> None:
         """update_anonymized_read_from_other (AM:281-287)."""
@@ -134,6 +136,9 @@ class State:
 
     def fastq(self) -> bytes:
         """get_anonymized_fastq_record (AM:215-243) with the creator's orientation."""
+        if self.seq is None:
+            from .planner import UnsupportedInput
+            raise UnsupportedInput("a read met in two scopes of one contig would be written from its second copy")
         seq = bytes(self.seq)
         if self.qual is None:
             raise TypeError(f"read {self.name.decode()!r} has no qualities")
@@ -217,13 +222,17 @@ class Replay:
         return st
 
     def _plain_object(self, job: int, ds: int, scope: int, row: int, upd: int) -> State:
-        flag = self.carry_info[(job, ds, row)]
         edits = self.carry_info.get((job, ds, scope, row), [])
-        raw = self.carry.get((job, ds, scope, row, 2)) if edits else None
-        name, seq, mate, qual = decode_fastq(raw if raw is not None else self.carry[(job, ds, scope, row, 0)],
-                                             bool(flag & 0x10))
-        rev = bool(flag & 0x10)
-        st = State(bytearray(seq), qual[::-1] if rev else qual, rev, name, mate)
+        rec = self.carry.get((job, ds, scope, row, 2 if edits else 0))
+        if rec is None:
+            # a copy of a read met in a second scope: never written (stream.Job.check_instance), it
+            # can only lend its left-over flag / list to the object it updates
+            st = State(None, None, False, b"", 0)
+        else:
+            flag = self.carry_info[(job, ds, row)]
+            rev = bool(flag & 0x10)
+            name, seq, mate, qual = decode_fastq(rec, rev)
+            st = State(bytearray(seq), qual[::-1] if rev else qual, rev, name, mate)
         st.left = [(call.variant_type, irp, call) for irp, call in edits]
         st.flag = bool(st.left)
         if scope >= 0:

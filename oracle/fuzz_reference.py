@@ -87,13 +87,14 @@ def main():
                                                           [(t_out, n_out)], True, 2)
                 res[mode] = files(t_out, n_out, paths["N"] + ".statistics.txt")
             except Exception as e:
-                res[mode] = {"error": type(e).__name__ + ": " + str(e)[:200]}
+                res[mode] = {"error": type(e).__name__, "message": str(e)[:200]}
         for mode, got in res.items():
-            diff = sorted(k for k in set(ref) | set(got) if ref.get(k) != got.get(k))
+            diff = sorted(k for k in set(ref) | set(got) if k != "message" and ref.get(k) != got.get(k))
             if diff:
                 bad += 1
                 print(f"seed {seed} mode {'whole' if mode == '1' else 'stream'}: differs in {diff}"
-                      + (f" ({got.get('error') or ref.get('error')})" if 'error' in diff else ""), flush=True)
+                      + (f" ({got.get('error')}: {got.get('message')} / reference {ref.get('error')})"
+                         if 'error' in diff else ""), flush=True)
                 for k in diff:
                     if k == "error":
                         continue

@@ -36,6 +36,8 @@ _REF = (1 << 0) | (1 << 2) | (1 << 3) | (1 << 7) | (1 << 8)     # M D N = X
 _QRY = (1 << 0) | (1 << 1) | (1 << 4) | (1 << 7) | (1 << 8)     # M I S = X
 _TYPE_ORDER = {"S": VariantType.SNV.value, VariantType.DEL: VariantType.DEL.value,
                VariantType.INS: VariantType.INS.value}
+_COMP = bytes.maketrans(b"ACGTN", b"TGCAN")
+_PHRED = bytes((b + 33) & 0xFF for b in range(256))
 
 Key = Tuple[int, int, int]            # (job, dataset, row)
 
@@ -51,11 +53,11 @@ class Record:
     def reverse(self) -> bool:
         return bool(self.flag & 0x10)
 
-    def forward_qual(self) -> Optional[List[int]]:
+    def forward_qual(self) -> Optional[bytes]:
+        """get_forward_qualities (bytes; a list once an indel edits it)."""
         if self.qual is None:
             return None
-        q = list(self.qual)
-        return q[::-1] if self.reverse else q
+        return self.qual[::-1] if self.reverse else self.qual
 
     def columns(self, idx: np.ndarray) -> np.ndarray:
         """Reference column of each aligned query position (a CIGAR walk)."""
@@ -80,11 +82,30 @@ def decode_nt16(buf: np.ndarray, nib0: int, n: int) -> bytes:
 
 
 def record_of(table, row: int) -> Record:
-    L = int(table.l_seq[row])
-    q = table.qual[int(table.qual_off[row]):int(table.qual_off[row]) + L]
-    qual = None if (L == 0 or q[0] == 0xFF) else q.tobytes()
-    return Record(table.name(row).encode(), int(table.flag[row]), int(table.pos[row]), table.cigar_of(row).copy(),
-                  decode_nt16(table.seq, 2 * int(table.seq_off[row]), L), qual)
+    return records_of(table, [row])[row]
+
+
+def records_of(table, rows) -> Dict[int, Record]:
+    """Records of many rows of a ReadTable, the sequences decoded in one pass."""
+    rows = np.asarray(sorted(set(int(r) for r in rows)), np.int64)
+    if not len(rows):
+        return {}
+    L = table.l_seq[rows].astype(np.int64)
+    start = np.concatenate([[0], np.cumsum(L)[:-1]])
+    nib = np.repeat(2 * table.seq_off[rows].astype(np.int64) - start, L) + np.arange(int(L.sum()), dtype=np.int64)
+    b = table.seq[nib >> 1]
+    blob = NT16[np.where(nib & 1, b & 0xF, b >> 4)].tobytes()
+    qb = table.qual.tobytes()
+    nb = table.names_blob.tobytes()
+    cig = table.cigar
+    out = {}
+    for r, l, s0 in zip(rows.tolist(), L.tolist(), start.tolist()):
+        qo = int(table.qual_off[r])
+        qual = None if (l == 0 or qb[qo] == 0xFF) else qb[qo:qo + l]
+        no, co = int(table.name_off[r]), int(table.cig_off[r])
+        out[r] = Record(nb[no:no + int(table.name_len[r])], int(table.flag[r]), int(table.pos[r]),
+                        cig[co:co + int(table.n_cigar[r])].copy(), blob[s0:s0 + l], qual)
+    return out
 
 
 def mask_diffs(rec: Record, masked: bytes) -> List[Tuple[int, int, int, int]]:
@@ -125,7 +146,8 @@ class State:
             if kind == "S":
                 self.put(pos, x)
             else:
-                self.seq, self.qual = apply_indel(self.seq, self.qual, pos, x)
+                self.seq, q = apply_indel(self.seq, list(self.qual), pos, x)
+                self.qual = bytes(q)
 
     def absorb(self, other: "State") -> None:
         """update_anonymized_read_from_other (AM:281-287)."""
@@ -142,15 +164,14 @@ class State:
         seq = bytes(self.seq)
         if self.qual is None:
             raise TypeError(f"read {self.name.decode()!r} has no qualities")
-        qual = self.qual
+        qual = bytes(self.qual)
         if self.reverse:
-            try:
-                seq = bytes(_REVERSES[c] for c in reversed(seq))
-            except KeyError:
-                raise TypeError(f"reverse read {self.name.decode()!r} has a base outside ACGTN (SURVEY Q7)") from None
+            if seq.translate(None, b"ACGTN"):
+                raise TypeError(f"reverse read {self.name.decode()!r} has a base outside ACGTN (SURVEY Q7)")
+            seq = seq[::-1].translate(_COMP)
             qual = qual[::-1]
         return (b"@" + self.name + b"/" + str(self.mate).encode() + b"\n" + seq + b"\n+\n" +
-                bytes(q + 33 for q in qual) + b"\n")
+                qual.translate(_PHRED) + b"\n")
 
 
 def decode_fastq(rec: bytes, reverse: bool) -> Tuple[bytes, bytes, int, bytes, List[int]]:
@@ -159,8 +180,8 @@ def decode_fastq(rec: bytes, reverse: bool) -> Tuple[bytes, bytes, int, bytes, L
     head, seq, _, qual = rec.rstrip(b"\n").split(b"\n")
     name, mate = head[1:].rsplit(b"/", 1)
     if reverse:
-        seq = bytes(_REVERSES[c] for c in reversed(seq))
-    return name, seq, int(mate), [c - 33 for c in qual]
+        seq = seq[::-1].translate(_COMP)
+    return name, seq, int(mate), bytes((c - 33) & 0xFF for c in qual)
 
 
 class Replay:
@@ -177,6 +198,7 @@ class Replay:
 
     def add_job(self, job: int, cx: Optional[dict]) -> None:
         if cx is not None and len(cx["objs"]):
+            cx = dict(cx, objs_l=cx["objs"].tolist(), rows_l=cx["obj_rows"].tolist())
             self.jobs[job] = cx
 
     # -- object creation ------------------------------------------------------------------------
@@ -186,13 +208,13 @@ class Replay:
             return r
         flag = self.carry_info[(job, ds, row)]
         name, seq, _, qual = decode_fastq(self.carry[(job, ds, -1, row, 0)], bool(flag & 0x10))
-        return Record(name, flag, -1, np.zeros(0, np.uint32), seq, bytes(qual))
+        return Record(name, flag, -1, np.zeros(0, np.uint32), seq, qual)
 
     def _plan_object(self, gid: int) -> State:
         job, k = gid >> 32, gid & 0xFFFFFFFF
         cx = self.jobs[job]
-        scope, ds, _, c, base, a_off, a_n = (int(x) for x in cx["objs"][k][:7])
-        aligns = cx["obj_rows"][a_off:a_off + a_n].tolist()
+        scope, ds, _, c, base, a_off, a_n = cx["objs_l"][k][:7]
+        aligns = cx["rows_l"][a_off:a_off + a_n]
         crec = cx["rec"][(ds, c)]
         brec = cx["rec"][(ds, base)] if base >= 0 else crec
         q = brec.forward_qual()

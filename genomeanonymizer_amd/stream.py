@@ -91,12 +91,13 @@ class Job:
     def _complex_incidences(self):
         """(dataset, row, scope) of every alignment of a complex name's object in a scope."""
         O = self.objs
-        out = []
-        for k in np.nonzero(O[:, 0] >= 0)[0].tolist() if len(O) else []:
-            sc, ds, a_off, a_n = int(O[k, 0]), int(O[k, 1]), int(O[k, 5]), int(O[k, 6])
-            for a in self.obj_rows[a_off:a_off + a_n].tolist():
-                out.append((ds, a, sc))
-        return sorted(set(out))
+        if not len(O):
+            return []
+        O = O[O[:, 0] >= 0]
+        n = O[:, 6]
+        idx = np.repeat(O[:, 5] - np.concatenate([[0], np.cumsum(n)[:-1]]), n) + np.arange(int(n.sum()))
+        trip = np.stack([np.repeat(O[:, 1], n), self.obj_rows[idx], np.repeat(O[:, 0], n)], axis=1)
+        return [tuple(t) for t in np.unique(trip, axis=0).tolist()]
 
     def _complex_ingredients(self) -> Optional[dict]:
         """What objects.Replay needs of this job's complex names: their records and, per (alignment,
@@ -105,21 +106,46 @@ class Job:
         if not len(O):
             return None
         rec = {}
-        for k in range(len(O)):
-            ds, c, base, a_off, a_n = int(O[k, 1]), int(O[k, 3]), int(O[k, 4]), int(O[k, 5]), int(O[k, 6])
-            for r in [c, base] + self.obj_rows[a_off:a_off + a_n].tolist():
-                if r >= 0 and (ds, r) not in rec:
-                    rec[(ds, r)] = objects.record_of(self.tables[ds], r)
+        for ds in (0, 1):
+            m = O[:, 1] == ds
+            if not np.any(m):
+                continue
+            rows = [O[m, 3], O[m, 4][O[m, 4] >= 0]]
+            rows += [self.obj_rows[a:a + n] for a, n in zip(O[m, 5].tolist(), O[m, 6].tolist())]
+            for r, v in objects.records_of(self.tables[ds], np.concatenate(rows)).items():
+                rec[(ds, r)] = v
         masks, indels = {}, {}
-        for ds, a, sc in self._complex_incidences():
-            r = rec[(ds, a)]
-            nib = self.res.masked_nib(self.tables, ds, a, sc)
-            d = objects.mask_diffs(r, objects.decode_nt16(self.res.seq_out, nib, len(r.seq)))
-            if d:
-                masks[(ds, a, sc)] = d
-            e = self.res.leftovers.get((ds, a, sc))
-            if e:
-                indels[(ds, a, sc)] = list(e)
+        inc = self._complex_incidences()
+        if inc:
+            # every incidence's masked copy against its record, one vectorised compare
+            T = self.tables
+            I = np.array(inc, np.int64)
+            L = np.array([int(T[d].l_seq[a]) for d, a, _ in inc], np.int64)
+            onib = np.array([2 * int(T[d].seq_off[a]) for d, a, _ in inc], np.int64)
+            mnib = np.array([self.res.masked_nib(T, d, a, sc) for d, a, sc in inc], np.int64)
+            start = np.concatenate([[0], np.cumsum(L)[:-1]])
+            k = np.arange(int(L.sum()), dtype=np.int64) - np.repeat(start, L)
+            src = np.concatenate([T[0].seq, T[1].seq]) if T[1].n else T[0].seq
+            base1 = len(T[0].seq)
+            on = np.repeat(onib + 2 * base1 * (I[:, 0] == 1), L) + k
+            mn = np.repeat(mnib, L) + k
+            ob = src[on >> 1]
+            ov = np.where(on & 1, ob & 0xF, ob >> 4)
+            mb = self.res.seq_out[mn >> 1]
+            mv = np.where(mn & 1, mb & 0xF, mb >> 4)
+            hit = np.nonzero(ov != mv)[0]
+            owner = np.searchsorted(start, hit, side="right") - 1
+            for i in np.unique(owner).tolist():
+                ds, a, sc = inc[i]
+                sel = hit[owner == i]
+                idx = sel - start[i]
+                cols = rec[(ds, a)].columns(idx)
+                masks[(ds, a, sc)] = list(zip(cols.tolist(), idx.tolist(), objects.NT16[mv[sel]].tolist(),
+                                              objects.NT16[ov[sel]].tolist()))
+            for ds, a, sc in inc:
+                e = self.res.leftovers.get((ds, a, sc))
+                if e:
+                    indels[(ds, a, sc)] = list(e)
         return {"objs": O, "obj_rows": self.obj_rows, "rec": rec, "masks": masks, "indels": indels}
 
     # -- which masked copy of each read the device produces --------------------------------------

@@ -1059,8 +1059,12 @@ struct ganon_resolver {
   std::vector<int64_t> log;     // 8 per entry (include/ganon_host.h)
   int64_t next_gid = (int64_t)1 << 62;
   int64_t next_serial = 0;
+  // the content of a written name's objects can no longer reach a file: their operations are not
+  // logged (the control state is kept: to_pair entries still count for SR:725 and the candidates)
+  bool quiet = false;
 
   void emit(int64_t op, int64_t id, int64_t a = 0, int64_t b = 0, int64_t c = 0, int64_t d = 0, int64_t e = 0) {
+    if (quiet) return;
     log.insert(log.end(), {op, id, a, b, c, d, e, 0});
   }
   void generalize(RObj &o) {
@@ -1206,6 +1210,7 @@ GANON_HOST_API int ganon_resolver_contig(ganon_resolver *r, int32_t job, int64_t
       const RInst inst{job, e[4], e[5], op_rows[i]};
       const int64_t seq = base | (int64_t)(uint32_t)e[6];
       out_n[i] = 0;
+      r->quiet = r->written.count(name) != 0;
       if (e[0] == 3) {   // a complete pair in one scope: this op (slot 0) and the next (slot 1)
         if (i + 1 >= n_ops || ops[7 * (i + 1)] != 3) {
           g_err = "resolver: unpaired pair event";
@@ -1313,7 +1318,8 @@ GANON_HOST_API int64_t ganon_resolver_take_log(ganon_resolver *r, int64_t *out, 
 GANON_HOST_API int64_t ganon_resolver_pending(ganon_resolver *r, int64_t *out, int64_t cap) {
   if (!r) return GANON_PLAN_E_ARG;
   int64_t n = 0;
-  for (const auto &kv : r->to_pair)
+  for (const auto &kv : r->to_pair) {
+    if (r->written.count(kv.first)) continue;   // dropped at the sample's end, never written again
     for (int s = 0; s < 2; ++s)
       if (kv.second.has[s]) {
         if (out && n < cap) {
@@ -1333,6 +1339,7 @@ GANON_HOST_API int64_t ganon_resolver_pending(ganon_resolver *r, int64_t *out, i
         }
         ++n;
       }
+  }
   return n;
 }
 
@@ -1366,9 +1373,11 @@ GANON_HOST_API int ganon_resolver_finish(ganon_resolver *r, int64_t n_cand, cons
           return GANON_PLAN_E_TYPE;
         }
         const RInst rec{c[0], c[2], -1, c[3]};
+        r->quiet = r->written.count(name) != 0;
         *n_tail += r->passthrough(name, (int)c[4], plain_obj(rec), rec, false, INT64_MAX, tail + 7 * *n_tail);
       }
     }
+    r->quiet = false;
     for (const std::string &k : r->written) r->to_pair.erase(k);
     std::vector<std::pair<int64_t, RSlot *>> rest;
     for (auto &kv : r->to_pair) rest.emplace_back(kv.second.seq, &kv.second);

@@ -88,16 +88,22 @@ class Job:
         self.cx = self._complex_ingredients()
         self.timing = {"decode_s": t1 - t0, "plan_s": t2 - t1, "mask_s": t3 - t2}
 
-    def _complex_incidences(self):
-        """(dataset, row, scope) of every alignment of a complex name's object in a scope."""
+    def _complex_incidences(self) -> np.ndarray:
+        """(dataset, row, scope) of every alignment of a complex name's object in a scope, [n, 3]."""
+        c = getattr(self, "_cx_inc", None)
+        if c is not None:
+            return c
         O = self.objs
         if not len(O):
-            return []
-        O = O[O[:, 0] >= 0]
-        n = O[:, 6]
-        idx = np.repeat(O[:, 5] - np.concatenate([[0], np.cumsum(n)[:-1]]), n) + np.arange(int(n.sum()))
-        trip = np.stack([np.repeat(O[:, 1], n), self.obj_rows[idx], np.repeat(O[:, 0], n)], axis=1)
-        return [tuple(t) for t in np.unique(trip, axis=0).tolist()]
+            c = np.zeros((0, 3), np.int64)
+        else:
+            O = O[O[:, 0] >= 0]
+            n = O[:, 6]
+            idx = np.repeat(O[:, 5] - np.concatenate([[0], np.cumsum(n)[:-1]]), n) + np.arange(int(n.sum()))
+            trip = np.stack([np.repeat(O[:, 1], n), self.obj_rows[idx], np.repeat(O[:, 0], n)], axis=1)
+            c = np.unique(trip, axis=0) if len(trip) else np.zeros((0, 3), np.int64)
+        self._cx_inc = c
+        return c
 
     def _complex_ingredients(self) -> Optional[dict]:
         """What objects.Replay needs of this job's complex names: their records and, per (alignment,
@@ -115,14 +121,21 @@ class Job:
             for r, v in objects.records_of(self.tables[ds], np.concatenate(rows)).items():
                 rec[(ds, r)] = v
         masks, indels = {}, {}
-        inc = self._complex_incidences()
-        if inc:
+        I = self._complex_incidences()
+        if len(I):
             # every incidence's masked copy against its record, one vectorised compare
             T = self.tables
-            I = np.array(inc, np.int64)
-            L = np.array([int(T[d].l_seq[a]) for d, a, _ in inc], np.int64)
-            onib = np.array([2 * int(T[d].seq_off[a]) for d, a, _ in inc], np.int64)
-            mnib = np.array([self.res.masked_nib(T, d, a, sc) for d, a, sc in inc], np.int64)
+            d0 = I[:, 0] == 0
+            r0, r1 = np.where(d0, I[:, 1], 0), np.where(d0, 0, I[:, 1])
+            pick = lambda f: np.where(d0, getattr(T[0], f)[r0] if T[0].n else 0,
+                                      getattr(T[1], f)[r1] if T[1].n else 0).astype(np.int64)
+            L = pick("l_seq")
+            onib = 2 * pick("seq_off")
+            mnib = 2 * (np.where(d0, self.res.seq_base[0], self.res.seq_base[1]) + onib // 2)
+            for i, key in enumerate(map(tuple, I.tolist())):
+                o = self.res.dup_off.get(key) if self.res.dup_off else None
+                if o is not None:
+                    mnib[i] = 2 * o
             start = np.concatenate([[0], np.cumsum(L)[:-1]])
             k = np.arange(int(L.sum()), dtype=np.int64) - np.repeat(start, L)
             src = np.concatenate([T[0].seq, T[1].seq]) if T[1].n else T[0].seq
@@ -135,6 +148,7 @@ class Job:
             mv = np.where(mn & 1, mb & 0xF, mb >> 4)
             hit = np.nonzero(ov != mv)[0]
             owner = np.searchsorted(start, hit, side="right") - 1
+            inc = I.tolist()
             for i in np.unique(owner).tolist():
                 ds, a, sc = inc[i]
                 sel = hit[owner == i]
@@ -142,10 +156,11 @@ class Job:
                 cols = rec[(ds, a)].columns(idx)
                 masks[(ds, a, sc)] = list(zip(cols.tolist(), idx.tolist(), objects.NT16[mv[sel]].tolist(),
                                               objects.NT16[ov[sel]].tolist()))
-            for ds, a, sc in inc:
-                e = self.res.leftovers.get((ds, a, sc))
-                if e:
-                    indels[(ds, a, sc)] = list(e)
+            if self.res.leftovers:
+                incset = set(map(tuple, inc))
+                for k, e in self.res.leftovers.items():
+                    if e and k in incset:
+                        indels[k] = list(e)
         return {"objs": O, "obj_rows": self.obj_rows, "rec": rec, "masks": masks, "indels": indels}
 
     # -- which masked copy of each read the device produces --------------------------------------
@@ -177,9 +192,8 @@ class Job:
             _, first = np.unique(key, return_index=True)
             keep[first] = True
         ds, rw, sc = ds[keep], rw[keep], sc[keep]
-        cx = self._complex_incidences()     # every (alignment, scope) of a complex name: one copy each
-        if cx:
-            c = np.array(cx, np.int64)
+        c = self._complex_incidences()      # every (alignment, scope) of a complex name: one copy each
+        if len(c):
             ds, rw, sc = np.concatenate([ds, c[:, 0]]), np.concatenate([rw, c[:, 1]]), np.concatenate([sc, c[:, 2]])
         return ds, rw, sc
 

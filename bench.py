@@ -282,7 +282,8 @@ def main() -> None:
     ap.add_argument("--windows", type=int, default=None)
     ap.add_argument("--germline", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--unroll", type=int, default=2, help="group kernel chunk width in 16-base blocks (1/2/4/8)")
+    ap.add_argument("--unroll", type=int, default=0,
+                    help="group kernel chunk width in 16-base blocks (1/2/4/8; 0 auto: 1 for long reads, else 2)")
     ap.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive measurement")
     ap.add_argument("--target", type=int, default=None, help="GANON_PARAM_GROUP_TARGET (cost units per group)")
     ap.add_argument("--no-fastq", action="store_true", help="skip the FASTQ formatter measurement")

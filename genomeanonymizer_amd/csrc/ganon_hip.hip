@@ -1466,13 +1466,14 @@ GANON_API int ganon_ctx_set_variant(ganon_ctx *ctx, int variant) {
 GANON_API int ganon_ctx_set_param(ganon_ctx *ctx, int param, int value) {
   if (!ctx) return GANON_E_ARG;
   if (param == GANON_PARAM_GROUP_UNROLL) {
-    if (value != 1 && value != 2 && value != 4 && value != 8)
-      return fail(ctx, GANON_E_ARG, "group unroll must be 1, 2, 4 or 8 (got %d)", value);
+    if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8)
+      return fail(ctx, GANON_E_ARG, "group unroll must be 0 (auto), 1, 2, 4 or 8 (got %d)", value);
     ctx->group_unroll = value;
     return GANON_OK;
   }
   if (param == GANON_PARAM_GROUP_TARGET) {
-    if (value < 16 || value > 65536) return fail(ctx, GANON_E_ARG, "group target must be in [16, 65536] (got %d)", value);
+    if (value != 0 && (value < 16 || value > 65536))
+      return fail(ctx, GANON_E_ARG, "group target must be 0 (auto) or in [16, 65536] (got %d)", value);
     ctx->group_target = value;
     return GANON_OK;
   }
@@ -1577,7 +1578,9 @@ GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
   // 2. masking: the fused group kernel writes every byte of out (its pieces tile [0, seq_bytes))
   if (db->n_groups) {
     KernelScope ks(ctx, "k_group_fused");
-    const int u = ctx->group_unroll;
+    // 16-base chunks per thread: long reads (short segments between indels) waste less with one
+    // (profiles/r02/sweep_c5.jsonl); short reads run best with two (sweep_c3.jsonl)
+    const int u = ctx->group_unroll ? ctx->group_unroll : db->long_mode ? 1 : 2;
     auto kern = u == 2 ? k_group<2, true> : u == 4 ? k_group<4, true> : u == 8 ? k_group<8, true> : k_group<1, true>;
     const GrpBatch GB{B.seq, B.ref, B.keep_code, B.ref2, B.keep_pos, B.span_start, B.span_len};
     kern<<<db->n_groups, kGrpThreads, 0, st>>>(GB, static_cast<const int4 *>(db->b_groups.p),

@@ -1173,6 +1173,7 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db, const int64_t *host_incid_off) {
     db->long_mode = ctx->prep_long == 1 || (ctx->prep_long != 0 && max_seg > 1);
     db->flat_mode = !db->long_mode && max_seg <= 1 && (ctx->prep_long == -1 || ctx->prep_long == 2);
     db->region_per_incid = (int64_t)((max_len + 47) / 48);
+    if (!ctx->group_target) db->group_target = db->long_mode ? 1408 : 704;   // auto (sweep_c5 / sweep_c3)
     if ((double)db->n_incid * (double)db->region_per_incid > 4e9)
       return fail(ctx, GANON_E_ARG, "batch too large: %lld incidences of reads up to %llu bases (split it)",
                   (long long)db->n_incid, max_len);
@@ -1184,6 +1185,7 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db, const int64_t *host_incid_off) {
   if ((rc = check_launch(ctx, "k_prep_incid_check/k_prep_seen_check")) || (rc = check_err(ctx, db))) return rc;
   // 3. groups (their number follows from the host's CSR offsets), then a counting emit pass sizes
   //    the segment records and overflow regions
+  if (db->group_target <= 0) db->group_target = 704;
   const long long w = weight_of(db->group_target);
   int64_t ng = ns ? (host_incid_off[ns - 1] + w * (ns - 1)) / db->group_target + 1 : 0;
   db->scost = nullptr;

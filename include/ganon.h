@@ -112,12 +112,13 @@ enum {
 };
 GANON_API int ganon_ctx_set_variant(ganon_ctx *ctx, int variant);
 /* Tuning knobs (results never depend on them). GANON_PARAM_GROUP_UNROLL: 16-base chunks each
- * thread of the group kernels loads at once (chunk = 16 x value bases): 1, 2 (default), 4 or 8.
+ * thread of the group kernels loads at once (chunk = 16 x value bases): 1, 2, 4 or 8; 0 (default)
+ * = 1 in long-read prep mode, else 2.
  * GANON_PARAM_GROUP_SKIP is for phase timing only and DOES change results: bit 0 leaves out
  * the classification, bit 1 the chunk scan, bit 2 the partition copy of the group kernels, bit 3
  * the per-scope count stores.
  * Keep it 0 in production. GANON_PARAM_GROUP_TARGET: segments per scope group (read at
- * upload, in cost units: segments plus 3 per scope; default 704). GANON_PARAM_NT_COPY: non-temporal stores for the fused partition copy
+ * upload, in cost units: segments plus 3 per scope; 0 (default) = 1408 in long-read prep mode, else 704). GANON_PARAM_NT_COPY: non-temporal stores for the fused partition copy
  * (default 1). GANON_PARAM_REF2: group kernels read a 2-bit copy of the reference for segments
  * whose reference range is all ACGT (1, default) or the nt16 reference only (0).
  * GANON_PARAM_FASTQ_KD: FASTQ formatter kernel: 0 (default) / 9 / 10 = 16-byte units, 2 / 1 / 3 per lane;

@@ -341,12 +341,17 @@ class Job:
             ext_bytes[i] = b
             rec_len[i] = len(b)
         order = native.io_replay(fin[:, :7].astype(np.int32), np.where(wr, rec_len, 0), block)
+        # every local record of the four files in ONE formatter call, then split per file
+        les = [order[f][~ext[order[f]]] for f in range(4)]
+        allr = np.concatenate(les)
+        blob = self.fmt.format_arrays(fin[allr, 4], frow[allr], fin[allr, 5], reap[allr]) if len(allr) else b""
+        cut = np.concatenate([[0], np.cumsum([int(rec_len[x].sum()) for x in les])])
         out = []
         for f in range(4):
             e = order[f]
             is_ext = ext[e]
-            le = e[~is_ext]
-            data = self.fmt.format_arrays(fin[le, 4], frow[le], fin[le, 5], reap[le]) if len(le) else b""
+            le = les[f]
+            data = blob[cut[f]:cut[f + 1]]
             if not np.any(is_ext):
                 out.append(data)
                 continue

@@ -30,6 +30,8 @@ STAT_HEADER = ["#SEQ", "#FIRST", "#LAST", "#SNV", "#DEL", "#INS", "#DUP", "#INV"
 
 
 _NT16_BYTES = np.frombuffer(NT16.encode(), np.uint8)
+_COMP = bytes.maketrans(b"ACGTN", b"TGCAN")
+_PHRED = bytes((b + 33) & 0xFF for b in range(256))
 
 
 def _decode(buf: np.ndarray, nib0: int, n: int) -> bytearray:
@@ -118,22 +120,20 @@ class FastqFormatter:
             seq = _decode(self.res.seq_out, nib0, L)
         else:
             seq = _decode(t.seq, 2 * int(t.seq_off[row]), L)
-        q = t.qual[int(t.qual_off[row]):int(t.qual_off[row]) + L].tolist()
+        q = t.qual[int(t.qual_off[row]):int(t.qual_off[row]) + L].tobytes()
         rev = bool(t.is_reverse[row])
-        qual_fwd = q[::-1] if rev else q
+        qual_fwd = list(q[::-1] if rev else q)
         for _ in range(times):   # mask_or_anonymize_left_over_variants, once more when re-flagged
             seq, qual_fwd = apply_leftovers(seq, qual_fwd, edits)
+        seq = bytes(seq)
+        qual = bytes(qual_fwd)
         if rev:
-            try:
-                seq = bytearray(_REVERSES[c] for c in reversed(seq))
-            except KeyError:
+            if seq.translate(None, b"ACGTN"):
                 raise TypeError(f"reverse read {t.name(row)!r} has a base outside ACGTN (SURVEY Q7)")
-            qual = qual_fwd[::-1]
-        else:
-            qual = qual_fwd
+            seq = seq[::-1].translate(_COMP)
+            qual = qual[::-1]
         mate = 1 if t.flag[row] & 0x40 else 2
-        return (f"@{t.name(row)}/{mate}\n".encode() + bytes(seq) + b"\n+\n" +
-                bytes(x + 33 for x in qual) + b"\n")
+        return f"@{t.name(row)}/{mate}\n".encode() + seq + b"\n+\n" + qual.translate(_PHRED) + b"\n"
 
     def format_arrays(self, ds: np.ndarray, row: np.ndarray, sc: np.ndarray, reapply=None) -> bytes:
         """Records in the given order: every unedited record in ONE formatter call, the rare

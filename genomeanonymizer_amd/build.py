@@ -82,7 +82,7 @@ def build_hip(force: bool = False) -> str:
     return HIP_LIB
 
 
-HOST_SOURCES = ("ganon_host.cpp", "ganon_plan.cpp")
+HOST_SOURCES = ("ganon_host.cpp", "ganon_plan.cpp", "ganon_objects.cpp")
 
 
 def build_host(force: bool = False) -> str:

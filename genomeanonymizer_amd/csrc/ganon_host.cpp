@@ -739,3 +739,51 @@ GANON_HOST_API void ganon_pack_nt16(const char *ascii, int64_t n, uint8_t *out) 
     out[i >> 1] = (uint8_t)((lut[(uint8_t)ascii[i]] << 4) | lut[(uint8_t)ascii[i + 1]]);
   if (n & 1) out[n >> 1] = (uint8_t)(lut[(uint8_t)ascii[n - 1]] << 4);
 }
+
+// ---- SA tag entries per record (the object model's n_supplementaries, AM:103-106) ----
+GANON_HOST_API int ganon_aux_sa_count(const uint8_t *aux, const int64_t *aux_off, const int32_t *aux_len, int64_t n,
+                                      int32_t *out) {
+  if (n < 0 || (n > 0 && (!aux_off || !aux_len || !out))) return -1;
+  auto size_of = [](uint8_t t) -> int {
+    switch (t) {
+      case 'A': case 'c': case 'C': return 1;
+      case 's': case 'S': return 2;
+      case 'i': case 'I': case 'f': return 4;
+      default: return 0;
+    }
+  };
+  for (int64_t r = 0; r < n; ++r) {
+    out[r] = -1;
+    const uint8_t *a = aux + aux_off[r];
+    const int64_t len = aux_len[r];
+    int64_t j = 0;
+    while (j + 3 <= len) {
+      const uint8_t t0 = a[j], t1 = a[j + 1], ty = a[j + 2];
+      j += 3;
+      if (ty == 'Z' || ty == 'H') {
+        int64_t k = j;
+        while (k < len && a[k]) ++k;
+        if (t0 == 'S' && t1 == 'A' && ty == 'Z') {
+          // len(value.rstrip(';').split(';'))
+          int64_t e = k;
+          while (e > j && a[e - 1] == ';') --e;
+          int32_t c = 1;
+          for (int64_t x = j; x < e; ++x) c += a[x] == ';';
+          out[r] = c;
+        }
+        j = k + 1;
+      } else if (ty == 'B') {
+        if (j + 5 > len) break;
+        const int sz = size_of(a[j]);
+        int32_t cnt;
+        std::memcpy(&cnt, a + j + 1, 4);
+        j += 5 + (int64_t)sz * cnt;
+      } else {
+        const int sz = size_of(ty);
+        if (!sz) break;   // malformed: leave the rest
+        j += sz;
+      }
+    }
+  }
+  return 0;
+}

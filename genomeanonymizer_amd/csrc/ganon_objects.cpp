@@ -1,0 +1,665 @@
+// ganon_objects.cpp — content of the AnonymizedRead objects of complex names (secondary /
+// supplementary alignments, SA tags), part of libganon_host.so; C ABI in include/ganon_host.h
+// (ganon_objects_*, ganon_blob_*).
+//
+// The native planner (ganon_plan.cpp) decides which objects exist and the resolver logs what happens
+// to them sample-wide; this replays that log over the device's masked copies:
+//   object state      sequence + forward qualities of the base record (update_from_primary_mapping,
+//                     anonymizer_methods.py:142-149), the creator's orientation and mate (AM:84-117)
+//   SNV masks         written at the query position of the alignment that found them (AM:548-554):
+//                     directly once the object holds a primary mapping, else as left-overs; one per
+//                     (column, allele) and read — the last alignment in pileup order (a dict, variants.py:64-65)
+//   left-overs        mask_or_anonymize_left_over_variants (AM:254-270): stable by variant type,
+//                     SNV np.put (IndexError), mask_or_modify_indel (AM:178-203, ValueError)
+//   merges            update_anonymized_read_from_other (AM:281-287)
+//   output            get_anonymized_fastq_record (AM:215-243): reverse complement (Q7 TypeError)
+//                     and reversed forward qualities when the creator is reverse
+// genomeanonymizer_amd/objects.py is the Python restatement the tests compare with.
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <new>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/ganon_host.h"
+
+namespace {
+
+thread_local std::string g_oerr;
+
+struct OErr {
+  int code;
+  std::string msg;
+};
+[[noreturn]] void oraise(int code, const std::string &m) { throw OErr{code, m}; }
+
+constexpr char kNt16[] = "=ACMGRSVTWYHKDBN";
+
+// ---- a little byte writer / reader for the packed blob ----
+struct Writer {
+  std::vector<uint8_t> b;
+  void i64(int64_t v) {
+    const size_t o = b.size();
+    b.resize(o + 8);
+    std::memcpy(b.data() + o, &v, 8);
+  }
+  void bytes(const void *p, size_t n) {
+    const size_t o = b.size();
+    b.resize(o + n);
+    if (n) std::memcpy(b.data() + o, p, n);
+  }
+};
+struct Reader {
+  const uint8_t *p, *e;
+  int64_t i64() {
+    if (e - p < 8) oraise(GANON_PLAN_E_ARG, "objects: truncated blob");
+    int64_t v;
+    std::memcpy(&v, p, 8);
+    p += 8;
+    return v;
+  }
+  std::string str(int64_t n) {
+    if (n < 0 || e - p < n) oraise(GANON_PLAN_E_ARG, "objects: truncated blob");
+    std::string s(reinterpret_cast<const char *>(p), (size_t)n);
+    p += n;
+    return s;
+  }
+};
+
+struct Rec {                 // one BAM record
+  std::string name, seq;     // seq: ASCII, BAM orientation
+  std::string qual;          // BAM order (valid if has_qual)
+  bool has_qual = false;
+  int32_t flag = 0, pos = 0;
+  std::vector<uint32_t> cigar;
+  bool reverse() const { return (flag & 0x10) != 0; }
+  std::string fwd_qual() const {
+    std::string q = qual;
+    if (reverse()) std::reverse(q.begin(), q.end());
+    return q;
+  }
+};
+
+struct Mask {
+  int64_t col;
+  int32_t idx;
+  uint8_t base, alt;
+};
+
+struct Item {                // one left-over: 1 SNV (pos, base), 2 DEL / 3 INS (irp, length, allele)
+  int type;
+  int64_t pos;
+  uint8_t base = 0;
+  int64_t length = 0;
+  std::string ref;
+};
+
+struct State {
+  bool has_seq = true;
+  std::string seq;
+  std::string qual;          // forward qualities
+  bool has_qual = true;
+  std::vector<Item> left;
+  bool flag = false;
+  bool reverse = false;
+  std::string name;
+  int mate = 1;
+
+  void put(int64_t pos, uint8_t base) {   // np.put(..., mode='raise')
+    const int64_t n = (int64_t)seq.size();
+    if (pos < -n || pos >= n)
+      oraise(GANON_PLAN_E_INDEX, "index " + std::to_string(pos) + " is out of bounds for axis 0 with size " +
+                                     std::to_string(n));
+    seq[(size_t)(pos < 0 ? pos + n : pos)] = (char)base;
+  }
+  static std::string slice(const std::string &s, int64_t a, int64_t b) {   // python s[a:b], a, b >= 0
+    const int64_t n = (int64_t)s.size();
+    a = std::min(std::max<int64_t>(a, 0), n);
+    b = std::min(std::max<int64_t>(b, 0), n);
+    return b > a ? s.substr((size_t)a, (size_t)(b - a)) : std::string();
+  }
+  void indel(const Item &it) {
+    if (it.type == 3) {
+      seq = slice(seq, 0, it.pos) + slice(seq, it.pos + it.length, (int64_t)seq.size());
+      qual = slice(qual, 0, it.pos) + slice(qual, it.pos + it.length, (int64_t)qual.size());
+    } else {
+      if (qual.empty()) oraise(GANON_PLAN_E_VALUE, "cannot convert float NaN to integer");
+      int64_t sum = 0;
+      for (unsigned char c : qual) sum += c;
+      const int64_t avg = (int64_t)((double)sum / (double)qual.size());
+      seq = slice(seq, 0, it.pos) + it.ref + slice(seq, it.pos, (int64_t)seq.size());
+      qual = slice(qual, 0, it.pos) + std::string((size_t)std::max<int64_t>(it.length, 0), (char)(uint8_t)avg) +
+             slice(qual, it.pos, (int64_t)qual.size());
+    }
+    if (seq.size() != qual.size())
+      oraise(GANON_PLAN_E_VALUE, "Length of the modified qualities does not match the length of the modified sequence");
+  }
+  void apply() {
+    if (!flag) return;
+    flag = false;
+    if (!has_seq) return;   // a second-scope copy: never written (objects.Replay._plain_object)
+    std::vector<const Item *> order;
+    order.reserve(left.size());
+    for (const Item &it : left) order.push_back(&it);
+    std::stable_sort(order.begin(), order.end(), [](const Item *a, const Item *b) { return a->type < b->type; });
+    for (const Item *it : order) {
+      if (it->type == 1) put(it->pos, it->base);
+      else indel(*it);
+    }
+  }
+  void absorb(const State &o) {
+    if (o.flag) left.insert(left.end(), o.left.begin(), o.left.end());
+    if (!left.empty()) flag = true;
+  }
+  std::string fastq() const {
+    if (!has_seq) oraise(GANON_PLAN_E_UNSUPPORTED, "a read met in two scopes of one contig would be written from its second copy");
+    if (!has_qual) oraise(GANON_PLAN_E_TYPE, "read '" + name + "' has no qualities");
+    std::string s = seq, q = qual;
+    if (reverse) {
+      for (char &c : s) {
+        switch (c) {
+          case 'A': c = 'T'; break;
+          case 'C': c = 'G'; break;
+          case 'G': c = 'C'; break;
+          case 'T': c = 'A'; break;
+          case 'N': break;
+          default: oraise(GANON_PLAN_E_TYPE, "reverse read '" + name + "' has a base outside ACGTN (SURVEY Q7)");
+        }
+      }
+      std::reverse(s.begin(), s.end());
+      std::reverse(q.begin(), q.end());
+    }
+    for (char &c : q) c = (char)(uint8_t)((uint8_t)c + 33);
+    std::string out;
+    out.reserve(name.size() + s.size() + q.size() + 8);
+    out += '@';
+    out += name;
+    out += '/';
+    out += (char)('0' + mate);
+    out += '\n';
+    out += s;
+    out += "\n+\n";
+    out += q;
+    out += '\n';
+    return out;
+  }
+};
+
+int64_t key3(int64_t ds, int64_t row) { return (ds << 40) | row; }
+
+struct IncKey {
+  int64_t ds, row, scope;
+  bool operator<(const IncKey &o) const {
+    return ds != o.ds ? ds < o.ds : row != o.row ? row < o.row : scope < o.scope;
+  }
+};
+
+struct Job {
+  std::vector<int64_t> objs, obj_rows;
+  std::unordered_map<int64_t, Rec> rec;            // key3(ds, row)
+  std::map<IncKey, std::vector<Mask>> masks;
+  std::map<IncKey, std::vector<Item>> indels;
+};
+
+std::vector<int64_t> ref_cols(const Rec &r, const std::vector<int32_t> &idx) {
+  std::vector<int64_t> out(idx.size(), -1);
+  int64_t rp = r.pos, qp = 0;
+  for (uint32_t c : r.cigar) {
+    const int op = (int)(c & 0xF);
+    const int64_t n = c >> 4;
+    const bool ref = op == 0 || op == 2 || op == 3 || op == 7 || op == 8;
+    const bool qry = op == 0 || op == 1 || op == 4 || op == 7 || op == 8;
+    if (ref && qry)
+      for (size_t i = 0; i < idx.size(); ++i)
+        if (idx[i] >= qp && idx[i] < qp + n) out[i] = rp + (idx[i] - qp);
+    if (ref) rp += n;
+    if (qry) qp += n;
+  }
+  return out;
+}
+
+}  // namespace
+
+struct ganon_blob {
+  std::vector<uint8_t> data;
+};
+
+struct ganon_objects {
+  std::unordered_map<int32_t, Job> jobs;
+  std::unordered_map<int64_t, State> states;
+  struct Plain {
+    int32_t flag;
+    std::string fastq;
+    std::vector<Item> edits;
+  };
+  std::map<IncKey, Plain> plain;                   // key (job, ds, row) with scope in IncKey.scope... see key
+  std::unordered_map<int64_t, std::string> written;
+
+  static IncKey pkey(int64_t job, int64_t ds, int64_t scope, int64_t row) {
+    return IncKey{(job << 2) | ds, row, scope};
+  }
+
+  State plan_object(int64_t gid) {
+    const int32_t job = (int32_t)(gid >> 32);
+    const int64_t k = gid & 0xFFFFFFFFll;
+    auto jt = jobs.find(job);
+    if (jt == jobs.end() || k < 0 || 10 * k + 9 >= (int64_t)jt->second.objs.size())
+      oraise(GANON_PLAN_E_ARG, "objects: unknown object " + std::to_string(gid));
+    Job &J = jt->second;
+    const int64_t *o = J.objs.data() + 10 * k;
+    const int64_t scope = o[0], ds = o[1], c = o[3], base = o[4], a_off = o[5], a_n = o[6];
+    const Rec &cr = J.rec.at(key3(ds, c));
+    const Rec &br = base >= 0 ? J.rec.at(key3(ds, base)) : cr;
+    State st;
+    st.seq = br.seq;
+    st.has_qual = br.has_qual;
+    st.qual = br.has_qual ? br.fwd_qual() : std::string();
+    st.reverse = cr.reverse();
+    st.name = cr.name;
+    st.mate = (cr.flag & 0x40) ? 1 : 2;
+    if (scope < 0) return st;
+    // one mask per (column, allele): the read's last alignment at that column (file order)
+    struct Best {
+      int64_t row;
+      int32_t idx;
+      uint8_t base;
+    };
+    std::map<std::pair<int64_t, int>, Best> best;
+    for (int64_t i = 0; i < a_n; ++i) {
+      const int64_t a = J.obj_rows[(size_t)(a_off + i)];
+      auto mt = J.masks.find(IncKey{ds, a, scope});
+      if (mt == J.masks.end()) continue;
+      for (const Mask &m : mt->second) {
+        auto key = std::make_pair(m.col, (int)m.alt);
+        auto it = best.find(key);
+        if (it == best.end() || a > it->second.row) best[key] = Best{a, m.idx, m.base};
+      }
+    }
+    // (column, row) order, as objects.Replay sorts
+    std::vector<std::pair<std::pair<int64_t, int64_t>, Best>> ms;
+    for (const auto &kv : best) ms.push_back({{kv.first.first, kv.second.row}, kv.second});
+    std::sort(ms.begin(), ms.end(), [](const auto &a, const auto &b) {
+      if (a.first != b.first) return a.first < b.first;
+      return a.second.idx < b.second.idx;
+    });
+    const bool primary = base >= 0;
+    for (const auto &m : ms) {
+      if (primary && m.first.first >= br.pos) st.put(m.second.idx, m.second.base);
+      else st.left.push_back(Item{1, m.second.idx, m.second.base, 0, std::string()});
+    }
+    auto it = J.indels.find(IncKey{ds, c, scope});
+    if (it != J.indels.end()) st.left.insert(st.left.end(), it->second.begin(), it->second.end());
+    st.flag = !st.left.empty();
+    if (primary) st.apply();   // mask_left_over_variants_in_pair before the scope yields it (AM:495, 523)
+    return st;
+  }
+
+  State &state(int64_t gid) {
+    auto it = states.find(gid);
+    if (it != states.end()) return it->second;
+    if (gid >= ((int64_t)1 << 62)) oraise(GANON_PLAN_E_ARG, "objects: unknown object " + std::to_string(gid));
+    return states.emplace(gid, plan_object(gid)).first->second;
+  }
+
+  // a formatted plain record back to (name, BAM-orientation bases, mate, BAM-order qualities)
+  static void decode(const std::string &rec, bool reverse, std::string &name, std::string &seq, int &mate,
+                     std::string &qual) {
+    size_t a = rec.find('\n'), b = rec.find('\n', a + 1), c = rec.find('\n', b + 1), d = rec.find('\n', c + 1);
+    if (rec.empty() || rec[0] != '@' || a == std::string::npos || b == std::string::npos || c == std::string::npos)
+      oraise(GANON_PLAN_E_ARG, "objects: bad carried record");
+    if (d == std::string::npos) d = rec.size();
+    const std::string head = rec.substr(1, a - 1);
+    const size_t sl = head.rfind('/');
+    name = head.substr(0, sl);
+    mate = sl == std::string::npos ? 1 : std::atoi(head.c_str() + sl + 1);
+    seq = rec.substr(a + 1, b - a - 1);
+    qual = rec.substr(c + 1, d - c - 1);
+    for (char &q : qual) q = (char)(uint8_t)((uint8_t)q - 33);
+    if (reverse) {
+      for (char &x : seq) x = x == 'A' ? 'T' : x == 'C' ? 'G' : x == 'G' ? 'C' : x == 'T' ? 'A' : x;
+      std::reverse(seq.begin(), seq.end());
+    }
+  }
+
+  State plain_object(int64_t job, int64_t ds, int64_t scope, int64_t row, bool upd) {
+    State st;
+    auto it = plain.find(pkey(job, ds, scope, row));
+    if (it == plain.end()) {
+      st.has_seq = false;   // never written: it can only lend its flag / list
+    } else {
+      const Plain &P = it->second;
+      const bool rev = (P.flag & 0x10) != 0;
+      std::string qual;
+      decode(P.fastq, rev, st.name, st.seq, st.mate, qual);
+      if (rev) std::reverse(qual.begin(), qual.end());
+      st.qual = qual;
+      st.reverse = rev;
+      st.left = P.edits;
+    }
+    st.flag = !st.left.empty();
+    if (scope >= 0) st.apply();
+    if (upd) st.flag = !st.left.empty();
+    return st;
+  }
+
+  void update(State &st, int64_t job, int64_t ds, int64_t row) {
+    auto jt = jobs.find((int32_t)job);
+    if (jt != jobs.end()) {
+      auto rt = jt->second.rec.find(key3(ds, row));
+      if (rt != jt->second.rec.end()) {
+        st.seq = rt->second.seq;
+        st.has_qual = rt->second.has_qual;
+        st.qual = rt->second.has_qual ? rt->second.fwd_qual() : std::string();
+        st.has_seq = true;
+        return;
+      }
+    }
+    auto it = plain.find(pkey(job, ds, -1, row));
+    if (it == plain.end()) oraise(GANON_PLAN_E_ARG, "objects: record of update_from_primary_mapping not carried");
+    std::string name, qual;
+    int mate;
+    const bool rev = (it->second.flag & 0x10) != 0;
+    decode(it->second.fastq, rev, name, st.seq, mate, qual);
+    if (rev) std::reverse(qual.begin(), qual.end());
+    st.qual = qual;
+    st.has_qual = true;
+    st.has_seq = true;
+  }
+};
+
+namespace {
+template <typename F>
+int guard(F &&f) {
+  try {
+    f();
+  } catch (const OErr &e) {
+    g_oerr = e.msg;
+    return e.code;
+  } catch (const std::bad_alloc &) {
+    g_oerr = "out of memory";
+    return GANON_PLAN_E_NOMEM;
+  } catch (const std::out_of_range &) {
+    g_oerr = "objects: inconsistent ingredients";
+    return GANON_PLAN_E_ARG;
+  }
+  return GANON_PLAN_OK;
+}
+}  // namespace
+
+GANON_HOST_API const char *ganon_objects_last_error(void) { return g_oerr.c_str(); }
+
+GANON_HOST_API int ganon_objects_pack(const ganon_objects_src *src, ganon_blob **out) {
+  if (!src || !out) return GANON_PLAN_E_ARG;
+  *out = nullptr;
+  ganon_blob *b = new ganon_blob();
+  const int rc = guard([&] {
+    Writer w;
+    w.i64(src->n_objs);
+    w.bytes(src->objs, (size_t)(10 * src->n_objs) * 8);
+    w.i64(src->n_obj_rows);
+    w.bytes(src->obj_rows, (size_t)src->n_obj_rows * 8);
+    // records: creator, base and every alignment of each object
+    std::vector<int64_t> need;
+    for (int64_t k = 0; k < src->n_objs; ++k) {
+      const int64_t *o = src->objs + 10 * k;
+      need.push_back(key3(o[1], o[3]));
+      if (o[4] >= 0) need.push_back(key3(o[1], o[4]));
+      for (int64_t i = 0; i < o[6]; ++i) need.push_back(key3(o[1], src->obj_rows[o[5] + i]));
+    }
+    std::sort(need.begin(), need.end());
+    need.erase(std::unique(need.begin(), need.end()), need.end());
+    w.i64((int64_t)need.size());
+    for (int64_t kk : need) {
+      const int ds = (int)(kk >> 40);
+      const int64_t r = kk & (((int64_t)1 << 40) - 1);
+      const ganon_objects_table &t = src->tables[ds];
+      if (ds < 0 || ds > 1 || r < 0 || r >= t.n) oraise(GANON_PLAN_E_ARG, "objects: record out of range");
+      const int32_t L = t.l_seq[r];
+      std::string seq((size_t)std::max(L, 0), 'N');
+      for (int32_t i = 0; i < L; ++i) {
+        const uint8_t x = t.seq[t.seq_off[r] + (i >> 1)];
+        seq[(size_t)i] = kNt16[(i & 1) ? (x & 15) : (x >> 4)];
+      }
+      const bool hq = L > 0 && t.qual[t.qual_off[r]] != 0xFF;
+      w.i64(ds);
+      w.i64(r);
+      w.i64(t.flag[r]);
+      w.i64(t.pos[r]);
+      w.i64(t.name_len[r]);
+      w.bytes(t.names + t.name_off[r], (size_t)t.name_len[r]);
+      w.i64(t.n_cigar[r]);
+      w.bytes(t.cigar + t.cig_off[r], (size_t)t.n_cigar[r] * 4);
+      w.i64(L);
+      w.bytes(seq.data(), seq.size());
+      w.i64(hq ? 1 : 0);
+      if (hq) w.bytes(t.qual + t.qual_off[r], (size_t)L);
+    }
+    // masks: where each copy differs from its record, with the reference column
+    Writer mw;
+    int64_t n_masks = 0;
+    for (int64_t i = 0; i < src->n_inc; ++i) {
+      const int64_t ds = src->inc[3 * i], r = src->inc[3 * i + 1], sc = src->inc[3 * i + 2];
+      const ganon_objects_table &t = src->tables[ds];
+      const int32_t L = t.l_seq[r];
+      const int64_t o = 2 * t.seq_off[r], m = src->inc_nib[i];
+      std::vector<int32_t> idx;
+      std::vector<uint8_t> nv, ov;
+      for (int32_t q = 0; q < L; ++q) {
+        const uint8_t a = t.seq[(o + q) >> 1], bb = src->masked[(m + q) >> 1];
+        const int av = ((o + q) & 1) ? (a & 15) : (a >> 4);
+        const int bv = ((m + q) & 1) ? (bb & 15) : (bb >> 4);
+        if (av != bv) {
+          idx.push_back(q);
+          nv.push_back((uint8_t)kNt16[bv]);
+          ov.push_back((uint8_t)kNt16[av]);
+        }
+      }
+      if (idx.empty()) continue;
+      Rec tmp;
+      tmp.pos = t.pos[r];
+      tmp.cigar.assign(t.cigar + t.cig_off[r], t.cigar + t.cig_off[r] + t.n_cigar[r]);
+      const std::vector<int64_t> cols = ref_cols(tmp, idx);
+      for (size_t k = 0; k < idx.size(); ++k) {
+        mw.i64(ds);
+        mw.i64(r);
+        mw.i64(sc);
+        mw.i64(cols[k]);
+        mw.i64(idx[k]);
+        mw.i64(nv[k]);
+        mw.i64(ov[k]);
+        ++n_masks;
+      }
+    }
+    w.i64(n_masks);
+    w.bytes(mw.b.data(), mw.b.size());
+    w.i64(src->n_ind);
+    for (int64_t i = 0; i < src->n_ind; ++i) {
+      for (int k = 0; k < 6; ++k) w.i64(src->ind[6 * i + k]);
+      w.i64(src->ind_ref_len[i]);
+      w.bytes(src->ind_ref + src->ind_ref_off[i], (size_t)src->ind_ref_len[i]);
+    }
+    b->data = std::move(w.b);
+  });
+  if (rc) {
+    delete b;
+    return rc;
+  }
+  *out = b;
+  return GANON_PLAN_OK;
+}
+
+GANON_HOST_API int64_t ganon_blob_size(const ganon_blob *b) { return b ? (int64_t)b->data.size() : 0; }
+GANON_HOST_API const uint8_t *ganon_blob_data(const ganon_blob *b) { return b ? b->data.data() : nullptr; }
+GANON_HOST_API void ganon_blob_free(ganon_blob *b) { delete b; }
+
+GANON_HOST_API int ganon_objects_create(ganon_objects **out) {
+  if (!out) return GANON_PLAN_E_ARG;
+  try {
+    *out = new ganon_objects();
+  } catch (const std::bad_alloc &) {
+    return GANON_PLAN_E_NOMEM;
+  }
+  return GANON_PLAN_OK;
+}
+
+GANON_HOST_API void ganon_objects_free(ganon_objects *o) { delete o; }
+
+GANON_HOST_API int ganon_objects_add_job(ganon_objects *o, int32_t job, const uint8_t *blob, int64_t size) {
+  if (!o || (size > 0 && !blob) || size < 0) return GANON_PLAN_E_ARG;
+  return guard([&] {
+    Reader rd{blob, blob + size};
+    Job J;
+    const int64_t n_objs = rd.i64();
+    J.objs.resize((size_t)(10 * n_objs));
+    for (auto &v : J.objs) v = rd.i64();
+    const int64_t n_rows = rd.i64();
+    J.obj_rows.resize((size_t)n_rows);
+    for (auto &v : J.obj_rows) v = rd.i64();
+    const int64_t n_rec = rd.i64();
+    for (int64_t i = 0; i < n_rec; ++i) {
+      Rec r;
+      const int64_t ds = rd.i64(), row = rd.i64();
+      r.flag = (int32_t)rd.i64();
+      r.pos = (int32_t)rd.i64();
+      r.name = rd.str(rd.i64());
+      const int64_t nc = rd.i64();
+      const std::string cg = rd.str(4 * nc);
+      r.cigar.resize((size_t)nc);
+      if (nc) std::memcpy(r.cigar.data(), cg.data(), (size_t)(4 * nc));
+      r.seq = rd.str(rd.i64());
+      r.has_qual = rd.i64() != 0;
+      if (r.has_qual) r.qual = rd.str((int64_t)r.seq.size());
+      J.rec.emplace(key3(ds, row), std::move(r));
+    }
+    const int64_t n_masks = rd.i64();
+    for (int64_t i = 0; i < n_masks; ++i) {
+      const int64_t ds = rd.i64(), row = rd.i64(), sc = rd.i64();
+      Mask m;
+      m.col = rd.i64();
+      m.idx = (int32_t)rd.i64();
+      m.base = (uint8_t)rd.i64();
+      m.alt = (uint8_t)rd.i64();
+      J.masks[IncKey{ds, row, sc}].push_back(m);
+    }
+    const int64_t n_ind = rd.i64();
+    for (int64_t i = 0; i < n_ind; ++i) {
+      const int64_t ds = rd.i64(), row = rd.i64(), sc = rd.i64();
+      Item it;
+      it.pos = rd.i64();
+      it.type = (int)rd.i64();
+      it.length = rd.i64();
+      it.ref = rd.str(rd.i64());
+      J.indels[IncKey{ds, row, sc}].push_back(std::move(it));
+    }
+    if (n_objs) o->jobs[job] = std::move(J);
+  });
+}
+
+GANON_HOST_API int ganon_objects_add_plain(ganon_objects *o, int64_t job, int64_t ds, int64_t scope, int64_t row,
+                                           int32_t flag, const char *fastq, int64_t len, int64_t n_ind,
+                                           const int64_t *ind, const char *ind_ref, const int64_t *ind_ref_off,
+                                           const int32_t *ind_ref_len) {
+  if (!o || !fastq || len < 0 || n_ind < 0 || (n_ind > 0 && (!ind || !ind_ref || !ind_ref_off || !ind_ref_len)))
+    return GANON_PLAN_E_ARG;
+  return guard([&] {
+    ganon_objects::Plain P;
+    P.flag = flag;
+    P.fastq.assign(fastq, (size_t)len);
+    for (int64_t i = 0; i < n_ind; ++i) {
+      Item it;
+      it.pos = ind[3 * i];
+      it.type = (int)ind[3 * i + 1];
+      it.length = ind[3 * i + 2];
+      it.ref.assign(ind_ref + ind_ref_off[i], (size_t)ind_ref_len[i]);
+      P.edits.push_back(std::move(it));
+    }
+    o->plain[ganon_objects::pkey(job, ds, scope, row)] = std::move(P);
+  });
+}
+
+GANON_HOST_API int ganon_objects_run(ganon_objects *o, int64_t n, const int64_t *log) {
+  if (!o || n < 0 || (n > 0 && !log)) return GANON_PLAN_E_ARG;
+  return guard([&] {
+    for (int64_t i = 0; i < n; ++i) {
+      const int64_t *e = log + 8 * i;
+      switch (e[0]) {
+        case 1:
+          o->states[e[1]] = o->plain_object(e[2], e[3], e[4], e[5], e[6] != 0);
+          break;
+        case 2: {
+          State &src = o->state(e[2]);
+          o->state(e[1]).absorb(src);
+          break;
+        }
+        case 3:
+          o->state(e[1]).apply();
+          break;
+        case 4:
+          o->update(o->state(e[1]), e[2], e[3], e[4]);
+          break;
+        case 5:
+          o->written[e[2]] = o->state(e[1]).fastq();
+          break;
+        default:
+          oraise(GANON_PLAN_E_ARG, "objects: bad log entry " + std::to_string(e[0]));
+      }
+    }
+  });
+}
+
+GANON_HOST_API int64_t ganon_objects_take(ganon_objects *o, int64_t serial, char *out, int64_t cap) {
+  if (!o) return GANON_PLAN_E_ARG;
+  auto it = o->written.find(serial);
+  if (it == o->written.end()) return -1;
+  const int64_t n = (int64_t)it->second.size();
+  if (out && cap >= n) {
+    std::memcpy(out, it->second.data(), (size_t)n);
+    o->written.erase(it);
+  }
+  return n;
+}
+
+GANON_HOST_API int64_t ganon_objects_take_all(ganon_objects *o, int64_t *serials, int64_t *lens, char *buf,
+                                              int64_t cap, int64_t *total) {
+  if (!o || !total) return GANON_PLAN_E_ARG;
+  int64_t n = 0, bytes = 0;
+  for (const auto &kv : o->written) {
+    ++n;
+    bytes += (int64_t)kv.second.size();
+  }
+  *total = bytes;
+  if (!serials || !lens || !buf || cap < bytes) return n;
+  int64_t k = 0, off = 0;
+  for (const auto &kv : o->written) {
+    serials[k] = kv.first;
+    lens[k] = (int64_t)kv.second.size();
+    std::memcpy(buf + off, kv.second.data(), kv.second.size());
+    off += lens[k];
+    ++k;
+  }
+  o->written.clear();
+  return n;
+}
+
+GANON_HOST_API int ganon_objects_settle(ganon_objects *o, int64_t n_live, const int64_t *live_ids) {
+  if (!o || n_live < 0 || (n_live > 0 && !live_ids)) return GANON_PLAN_E_ARG;
+  return guard([&] {
+    std::unordered_map<int64_t, char> live;
+    for (int64_t i = 0; i < n_live; ++i) live[live_ids[i]] = 1;
+    for (const auto &kv : live) {
+      const int64_t gid = kv.first;
+      if (gid < ((int64_t)1 << 62) && o->jobs.count((int32_t)(gid >> 32))) o->state(gid);
+    }
+    for (auto it = o->states.begin(); it != o->states.end();) {
+      if (!live.count(it->first)) it = o->states.erase(it);
+      else ++it;
+    }
+    o->jobs.clear();
+    o->plain.clear();
+    o->written.clear();
+  });
+}

@@ -210,10 +210,13 @@ class ReadTable:
         c = getattr(self, "_sa", None)
         if c is None:
             c = np.full(self.n, -1, np.int32)
-            for r in self._sa_candidates().tolist():
-                v = self.tag_value(r, b"SA")
-                if isinstance(v, str):
-                    c[r] = len(v.rstrip(";").split(";"))
+            if self.n and self._sa_candidates().size:
+                aux = np.ascontiguousarray(self.aux)
+                off = np.ascontiguousarray(self.aux_off, np.int64)
+                ln = np.ascontiguousarray(self.aux_len, np.int32)
+                native.host_lib().ganon_aux_sa_count(aux.ctypes.data_as(native._u8p), off.ctypes.data_as(native._i64p),
+                                                     ln.ctypes.data_as(native._i32p), self.n,
+                                                     c.ctypes.data_as(native._i32p))
             self._sa = c
         return c
 

@@ -215,7 +215,10 @@ EXPORTED_HOST_SYMBOLS = (
     "ganon_bam_reader_open", "ganon_bam_reader_set_window", "ganon_bam_reader_has_index", "ganon_bam_reader_header",
     "ganon_bam_reader_contig", "ganon_bam_reader_close",
     "ganon_resolver_create", "ganon_resolver_free", "ganon_resolver_contig", "ganon_resolver_pending",
-    "ganon_resolver_finish", "ganon_resolver_take_log",
+    "ganon_resolver_finish", "ganon_resolver_take_log", "ganon_objects_pack", "ganon_blob_size", "ganon_blob_data",
+    "ganon_blob_free", "ganon_objects_create", "ganon_objects_free", "ganon_objects_add_job", "ganon_objects_add_plain",
+    "ganon_objects_run", "ganon_objects_take", "ganon_objects_settle", "ganon_objects_last_error",
+    "ganon_objects_take_all", "ganon_aux_sa_count",
 )
 
 
@@ -638,7 +641,7 @@ class PlanView(C.Structure):
                 ("n_skip", C.c_int64), ("skip", _i64p)]
 
 
-PLAN_E_VALUE, PLAN_E_TYPE, PLAN_E_UNSUPPORTED = -10, -11, -12
+PLAN_E_VALUE, PLAN_E_TYPE, PLAN_E_UNSUPPORTED, PLAN_E_INDEX = -10, -11, -12, -13
 
 
 def _np_copy(ptr, n: int, dtype) -> np.ndarray:
@@ -834,6 +837,163 @@ class Resolver:
             pass
 
 
+class ObjectsTable(C.Structure):
+    """Mirror of ``ganon_objects_table`` (include/ganon_host.h)."""
+    _fields_ = [("n", C.c_int64), ("flag", _i32p), ("pos", _i32p), ("l_seq", _i32p), ("n_cigar", _i32p),
+                ("name_len", _i32p), ("seq_off", _i64p), ("qual_off", _i64p), ("name_off", _i64p),
+                ("cig_off", _i64p), ("seq", _u8p), ("qual", _u8p), ("names", _p), ("cigar", _u32p)]
+
+
+class ObjectsSrc(C.Structure):
+    _fields_ = [("tables", ObjectsTable * 2), ("n_objs", C.c_int64), ("objs", _i64p), ("n_obj_rows", C.c_int64),
+                ("obj_rows", _i64p), ("n_inc", C.c_int64), ("inc", _i64p), ("inc_nib", _i64p), ("masked", _u8p),
+                ("n_ind", C.c_int64), ("ind", _i64p), ("ind_ref", _p), ("ind_ref_off", _i64p),
+                ("ind_ref_len", _i32p)]
+
+
+def _indel_args(entries, keep: list):
+    """(n, ind int64 array, ref blob, offsets, lengths) of left-over entries [(prefix..., irp, call)]."""
+    rows, refs = [], []
+    for pre, irp, call in entries:
+        rows.append(list(pre) + [int(irp), int(call.variant_type.value), int(call.length)])
+        refs.append(call.ref_allele.encode())
+    width = len(rows[0]) if rows else 1
+    ind = np.ascontiguousarray(np.array(rows, np.int64).reshape(-1, width) if rows else np.zeros((1, width), np.int64))
+    lens = np.array([len(r) for r in refs] or [0], np.int32)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.int64)]).astype(np.int64)
+    blob = np.frombuffer(b"".join(refs) + b"\0", np.uint8).copy()
+    keep += [ind, lens, offs, blob]
+    return len(rows), ind.ctypes.data_as(_i64p), blob.ctypes.data_as(_p), offs.ctypes.data_as(_i64p), \
+        lens.ctypes.data_as(_i32p)
+
+
+def objects_pack(tables, objs: np.ndarray, obj_rows: np.ndarray, inc: np.ndarray, inc_nib: np.ndarray,
+                 masked: np.ndarray, leftovers: dict) -> bytes:
+    """``ganon_objects_pack``: one contig plan's complex-name ingredients as a blob (objects.py)."""
+    lib = host_lib()
+    keep = []
+
+    def arr(a, dt):
+        a = np.ascontiguousarray(a, dtype=dt)
+        if a.size == 0:
+            a = np.zeros(1, dt)
+        keep.append(a)
+        return a.ctypes.data_as(_PTR_OF[dt])
+
+    src = ObjectsSrc()
+    for d, t in enumerate(tables):
+        ot = src.tables[d]
+        ot.n = t.n
+        for f in ("flag", "pos", "l_seq", "n_cigar", "name_len"):
+            setattr(ot, f, arr(getattr(t, f), np.int32))
+        for f in ("seq_off", "qual_off", "name_off", "cig_off"):
+            setattr(ot, f, arr(getattr(t, f), np.int64))
+        ot.seq = arr(t.seq, np.uint8)
+        ot.qual = arr(t.qual, np.uint8)
+        nb = np.ascontiguousarray(t.names_blob if len(t.names_blob) else np.zeros(1, np.uint8))
+        keep.append(nb)
+        ot.names = nb.ctypes.data_as(_p)
+        ot.cigar = arr(t.cigar, np.uint32)
+    src.n_objs = len(objs)
+    src.objs = arr(objs, np.int64)
+    src.n_obj_rows = len(obj_rows)
+    src.obj_rows = arr(obj_rows, np.int64)
+    src.n_inc = len(inc)
+    src.inc = arr(inc, np.int64)
+    src.inc_nib = arr(inc_nib, np.int64)
+    src.masked = arr(masked, np.uint8)
+    entries = [((d, r, sc), irp, call) for (d, r, sc), lst in leftovers.items() for irp, call in lst]
+    src.n_ind, src.ind, src.ind_ref, src.ind_ref_off, src.ind_ref_len = _indel_args(entries, keep)
+    h = _p()
+    rc = lib.ganon_objects_pack(C.byref(src), C.byref(h))
+    if rc != 0:
+        raise GanonError(f"ganon_objects_pack failed ({rc}): {lib.ganon_objects_last_error().decode(errors='replace')}")
+    try:
+        n = lib.ganon_blob_size(h)
+        return C.string_at(lib.ganon_blob_data(h), n) if n else b""
+    finally:
+        lib.ganon_blob_free(h)
+
+
+class ObjectStore:
+    """``ganon_objects_*``: the content replay of the resolver log in libganon_host.so (objects.py
+    restates it in Python)."""
+
+    def __init__(self):
+        self._lib = host_lib()
+        h = _p()
+        if self._lib.ganon_objects_create(C.byref(h)) != 0:
+            raise GanonError("ganon_objects_create failed")
+        self._h = h
+
+    def _check(self, rc: int) -> None:
+        if rc == 0:
+            return
+        msg = self._lib.ganon_objects_last_error().decode(errors="replace")
+        if rc == PLAN_E_VALUE:
+            raise ValueError(msg)
+        if rc == PLAN_E_TYPE:
+            raise TypeError(msg)
+        if rc == PLAN_E_INDEX:
+            raise IndexError(msg)
+        if rc == PLAN_E_UNSUPPORTED:
+            from .planner import UnsupportedInput
+            raise UnsupportedInput(msg)
+        raise GanonError(f"objects failed ({rc}): {msg}")
+
+    def add_job(self, job: int, blob: bytes) -> None:
+        self._check(self._lib.ganon_objects_add_job(self._h, int(job), blob, len(blob)))
+
+    def add_plain(self, job, ds, scope, row, flag, fastq: bytes, edits) -> None:
+        keep = []
+        n, ind, ref, ro, rl = _indel_args([((), irp, call) for irp, call in edits], keep)
+        self._check(self._lib.ganon_objects_add_plain(self._h, int(job), int(ds), int(scope), int(row), int(flag),
+                                                      fastq, len(fastq), n, ind, ref, ro, rl))
+
+    def run(self, log: np.ndarray) -> None:
+        lg = np.ascontiguousarray(log, np.int64).reshape(-1, 8)
+        if len(lg):
+            self._check(self._lib.ganon_objects_run(self._h, len(lg), lg.ctypes.data_as(_i64p)))
+
+    def take_all(self) -> dict:
+        """serial -> FASTQ bytes of every object written since the last call."""
+        tot = C.c_int64(0)
+        n = self._lib.ganon_objects_take_all(self._h, None, None, None, 0, C.byref(tot))
+        if n <= 0:
+            return {}
+        ser = np.zeros(n, np.int64)
+        lens = np.zeros(n, np.int64)
+        buf = C.create_string_buffer(max(tot.value, 1))
+        self._lib.ganon_objects_take_all(self._h, ser.ctypes.data_as(_i64p), lens.ctypes.data_as(_i64p), buf,
+                                         tot.value, C.byref(tot))
+        raw = buf.raw
+        off = np.concatenate([[0], np.cumsum(lens)]).tolist()
+        return {s: raw[off[i]:off[i + 1]] for i, s in enumerate(ser.tolist())}
+
+    def take(self, serial: int) -> bytes:
+        n = self._lib.ganon_objects_take(self._h, int(serial), None, 0)
+        if n < 0:
+            raise KeyError(serial)
+        buf = C.create_string_buffer(max(int(n), 1))
+        self._lib.ganon_objects_take(self._h, int(serial), buf, int(n))
+        return buf.raw[:n]
+
+    def settle(self, live_ids: np.ndarray) -> None:
+        ids = np.ascontiguousarray(live_ids, np.int64)
+        self._check(self._lib.ganon_objects_settle(self._h, len(ids), ids.ctypes.data_as(_i64p) if len(ids) else None))
+
+    def close(self) -> None:
+        if self._h:
+            self._lib.ganon_objects_free(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def io_replay(events: np.ndarray, rec_len: np.ndarray, block: int):
     """``ganon_io_replay``: per output file (dataset * 2 + slot) the write-event indices in the
     order they reach the file."""
@@ -881,6 +1041,25 @@ def host_lib():
     lib.ganon_resolver_free.argtypes = [_p]
     lib.ganon_resolver_contig.argtypes = [_p, C.c_int32, C.c_int64, _i32p, _i64p, _p, _i64p, _i32p, C.c_int64, _i64p,
                                           _p, _i64p, _i32p, C.c_int64, _i64p, _i64p, _i32p, _i64p]
+    lib.ganon_objects_pack.argtypes = [C.POINTER(ObjectsSrc), C.POINTER(_p)]
+    lib.ganon_blob_size.argtypes = [_p]
+    lib.ganon_blob_size.restype = C.c_int64
+    lib.ganon_blob_data.argtypes = [_p]
+    lib.ganon_blob_data.restype = C.c_void_p
+    lib.ganon_blob_free.argtypes = [_p]
+    lib.ganon_objects_create.argtypes = [C.POINTER(_p)]
+    lib.ganon_objects_free.argtypes = [_p]
+    lib.ganon_objects_add_job.argtypes = [_p, C.c_int32, C.c_char_p, C.c_int64]
+    lib.ganon_objects_add_plain.argtypes = [_p, C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_int32, C.c_char_p,
+                                            C.c_int64, C.c_int64, _i64p, _p, _i64p, _i32p]
+    lib.ganon_objects_run.argtypes = [_p, C.c_int64, _i64p]
+    lib.ganon_objects_take.argtypes = [_p, C.c_int64, C.c_char_p, C.c_int64]
+    lib.ganon_objects_take.restype = C.c_int64
+    lib.ganon_objects_settle.argtypes = [_p, C.c_int64, _i64p]
+    lib.ganon_objects_take_all.argtypes = [_p, _i64p, _i64p, C.c_char_p, C.c_int64, C.POINTER(C.c_int64)]
+    lib.ganon_objects_take_all.restype = C.c_int64
+    lib.ganon_aux_sa_count.argtypes = [_u8p, _i64p, _i32p, C.c_int64, _i32p]
+    lib.ganon_objects_last_error.restype = C.c_char_p
     lib.ganon_resolver_take_log.argtypes = [_p, _i64p, C.c_int64]
     lib.ganon_resolver_take_log.restype = C.c_int64
     lib.ganon_resolver_pending.argtypes = [_p, _i64p, C.c_int64]

@@ -299,6 +299,49 @@ class Replay:
         for gid in [g for g in self.states if g not in live]:
             del self.states[gid]
         self.jobs.clear()
+        self.written.clear()     # serials of other ranks' jobs (this rank's were taken)
+
+    def take(self, serial: int) -> bytes:
+        return self.written.pop(serial)
+
+
+class NativeReplay:
+    """The same replay in libganon_host.so (``native.ObjectStore``, csrc/ganon_objects.cpp): the
+    product's; the job ingredients travel as the packed blob of ``native.objects_pack``."""
+
+    native = True
+
+    def __init__(self, carry: dict, carry_info: dict):
+        from . import native
+        self.carry, self.carry_info = carry, carry_info
+        self.store = native.ObjectStore()
+        self.written: Dict[int, bytes] = {}
+
+    def add_job(self, job: int, cx: Optional[bytes]) -> None:
+        if cx:
+            self.store.add_job(job, cx)
+
+    def run(self, log: np.ndarray) -> None:
+        if not len(log):
+            return
+        # plain instances the log turns into objects (1) or promotes from (4): their carried records
+        for op, _, a, b, c, d, _, _ in log[(log[:, 0] == 1) | (log[:, 0] == 4)].tolist():
+            if op == 1:
+                edits = self.carry_info.get((a, b, c, d), [])
+                rec = self.carry.get((a, b, c, d, 2 if edits else 0))
+                if rec is not None:
+                    self.store.add_plain(a, b, c, d, self.carry_info[(a, b, d)], rec, edits)
+            else:
+                rec = self.carry.get((a, b, -1, c, 0))
+                if rec is not None:
+                    self.store.add_plain(a, b, -1, c, self.carry_info[(a, b, c)], rec, [])
+        self.store.run(log)
+        self.written.update(self.store.take_all())
+
+    def settle(self, pending: np.ndarray) -> None:
+        live = pending[pending[:, 2] == -2, 3] if len(pending) else np.zeros(0, np.int64)
+        self.store.settle(live)
+        self.written.clear()
 
     def take(self, serial: int) -> bytes:
         return self.written.pop(serial)

@@ -105,12 +105,23 @@ class Job:
         self._cx_inc = c
         return c
 
-    def _complex_ingredients(self) -> Optional[dict]:
-        """What objects.Replay needs of this job's complex names: their records and, per (alignment,
-        scope), the bases the device masked and the indel left-overs."""
+    def _complex_ingredients(self):
+        """What the object replay needs of this job's complex names: their records and, per
+        (alignment, scope), the bases the device masked and the indel left-overs — the packed blob of
+        ``native.objects_pack`` (objects.NativeReplay), or Python objects (objects.Replay,
+        GANON_OBJECTS=python)."""
         O = self.objs
         if not len(O):
             return None
+        if os.environ.get("GANON_OBJECTS", "native") != "python":
+            I = self._complex_incidences()
+            T = self.tables
+            nib = np.zeros(len(I), np.int64)
+            for i, (d, a, sc) in enumerate(I.tolist()):
+                nib[i] = self.res.masked_nib(T, d, a, sc)
+            incs = set(map(tuple, I.tolist()))
+            left = {k: v for k, v in self.res.leftovers.items() if v and k in incs}
+            return native.objects_pack(T, O, self.obj_rows, I, nib, self.res.seq_out, left)
         rec = {}
         for ds in (0, 1):
             m = O[:, 1] == ds
@@ -432,7 +443,7 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
     resolver = native.Resolver()
     carry: Dict[Key, bytes] = {}
     carry_info: dict = {}
-    replay = objects.Replay(carry, carry_info)
+    replay = (objects.Replay if os.environ.get("GANON_OBJECTS") == "python" else objects.NativeReplay)(carry, carry_info)
     cands: List[np.ndarray] = []
     cand_names: List[bytes] = []
     base = [0, 0, 0, 0]
@@ -510,7 +521,6 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
             for k in [k for k in carry_info if (k if len(k) == 3 else (k[0], k[1], k[3])) not in live_rows
                       or (len(k) == 4 and k not in live)]:
                 del carry_info[k]
-            replay.written.clear()     # serials of the other ranks' jobs
             job = None
             timing["resolve_s"] += t1 - t0
             timing["write_s"] += time.time() - t1

@@ -66,6 +66,10 @@ GANON_HOST_API const char *ganon_host_last_error(void);
  * first record). The returned ganon_bam carries the full reference list and is released with
  * ganon_bam_close. The reader header view has n_records = 0. */
 typedef struct ganon_bam_reader ganon_bam_reader;
+/* entries of each record's SA tag (len(tag.rstrip(';').split(';')), anonymizer_methods.py:103-106),
+ * -1 without one, from the aux blob of a ganon_bam_view */
+GANON_HOST_API int ganon_aux_sa_count(const uint8_t *aux, const int64_t *aux_off, const int32_t *aux_len, int64_t n,
+                                      int32_t *out);
 GANON_HOST_API int ganon_bam_reader_open(const char *path, int threads, ganon_bam_reader **out);
 GANON_HOST_API int ganon_bam_reader_has_index(const ganon_bam_reader *reader);
 /* Compressed bytes read and inflated per step (default 32 MiB, at least 128 KiB). */
@@ -110,7 +114,8 @@ enum {
   GANON_PLAN_E_NOMEM = -3,
   GANON_PLAN_E_VALUE = -10,        /* the reference raises ValueError (region errors Q4, Q10, ...) */
   GANON_PLAN_E_TYPE = -11,         /* the reference raises TypeError (Q8, reads without SEQ, ...)  */
-  GANON_PLAN_E_UNSUPPORTED = -12   /* input this build does not restate                           */
+  GANON_PLAN_E_UNSUPPORTED = -12,  /* input this build does not restate                           */
+  GANON_PLAN_E_INDEX = -13         /* the reference raises IndexError (np.put out of range)        */
 };
 typedef struct ganon_plan_table {  /* one sample, file order (columns of a ganon_bam_view) */
   int64_t n;
@@ -240,6 +245,73 @@ GANON_HOST_API int ganon_resolver_finish(ganon_resolver *r, int64_t n_cand, cons
                                          const int64_t *name_off, const int32_t *name_len, int64_t *tail,
                                          int64_t *n_tail, int64_t *single0, int64_t *single1, int64_t *n_single,
                                          int32_t *write_single_end);
+
+/* ---- Objects of complex names (the content side of the resolver log) ---------------------------
+ * AnonymizedRead content (anonymizer_methods.py:84-287): sequence and forward qualities of the base
+ * record, SNV masks written at the query position of the alignment that found them (directly once
+ * the object holds a primary mapping, else as left-overs), left-over lists applied stable by variant
+ * type, update_anonymized_read_from_other, update_from_primary_mapping, the FASTQ record with the
+ * creator's orientation (genomeanonymizer_amd/objects.py is the Python restatement the tests compare).
+ *
+ * ganon_objects_pack: what one contig plan's objects need, as one self-contained blob (it travels
+ * between ranks): the plan objects, their records (name, flag, position, CIGAR, bases, qualities),
+ * the bases the device changed in every (alignment, scope) copy (with their reference columns) and
+ * the indel left-overs. */
+typedef struct ganon_objects_table {   /* one sample's records of the contig (ReadTable columns) */
+  int64_t n;
+  const int32_t *flag, *pos, *l_seq, *n_cigar, *name_len;
+  const int64_t *seq_off, *qual_off, *name_off, *cig_off;
+  const uint8_t *seq;                  /* nt16, 2 per byte, BAM layout                            */
+  const uint8_t *qual;                 /* BAM order; first byte 0xFF = missing                    */
+  const char *names;
+  const uint32_t *cigar;
+} ganon_objects_table;
+typedef struct ganon_objects_src {
+  ganon_objects_table tables[2];
+  int64_t n_objs;
+  const int64_t *objs;                 /* ganon_plan_view.objs (10 per object)                    */
+  int64_t n_obj_rows;
+  const int64_t *obj_rows;
+  int64_t n_inc;
+  const int64_t *inc;                  /* (dataset, row, scope) per masked copy                   */
+  const int64_t *inc_nib;              /* nibble index of that copy in masked                     */
+  const uint8_t *masked;               /* the device output                                       */
+  int64_t n_ind;
+  const int64_t *ind;                  /* 6 per left-over: dataset, row, scope, in_read_pos, type
+                                          (2 DEL, 3 INS), length                                  */
+  const char *ind_ref;                 /* reference allele of each (ind_ref_off / ind_ref_len)    */
+  const int64_t *ind_ref_off;
+  const int32_t *ind_ref_len;
+} ganon_objects_src;
+typedef struct ganon_blob ganon_blob;
+GANON_HOST_API int ganon_objects_pack(const ganon_objects_src *src, ganon_blob **out);
+GANON_HOST_API int64_t ganon_blob_size(const ganon_blob *b);
+GANON_HOST_API const uint8_t *ganon_blob_data(const ganon_blob *b);
+GANON_HOST_API void ganon_blob_free(ganon_blob *b);
+typedef struct ganon_objects ganon_objects;
+GANON_HOST_API int ganon_objects_create(ganon_objects **out);
+GANON_HOST_API void ganon_objects_free(ganon_objects *o);
+/* a packed job (its object ids are job << 32 | index) */
+GANON_HOST_API int ganon_objects_add_job(ganon_objects *o, int32_t job, const uint8_t *blob, int64_t size);
+/* a plain instance's content for log entries 1 / 4: its formatted record (writer.py), BAM flag and
+ * indel left-overs (n_ind entries of 3: in_read_pos, type, length, with reference alleles) */
+GANON_HOST_API int ganon_objects_add_plain(ganon_objects *o, int64_t job, int64_t ds, int64_t scope, int64_t row,
+                                           int32_t flag, const char *fastq, int64_t len, int64_t n_ind,
+                                           const int64_t *ind, const char *ind_ref, const int64_t *ind_ref_off,
+                                           const int32_t *ind_ref_len);
+/* replay resolver log entries (ganon_resolver_take_log); GANON_PLAN_OK or the reference's error
+ * (E_INDEX / E_TYPE / E_VALUE / E_UNSUPPORTED, message: ganon_objects_last_error) */
+GANON_HOST_API int ganon_objects_run(ganon_objects *o, int64_t n, const int64_t *log);
+/* bytes of written object `serial` (returns the size; copies and forgets it when cap >= size; -1:
+ * unknown serial) */
+GANON_HOST_API int64_t ganon_objects_take(ganon_objects *o, int64_t serial, char *out, int64_t cap);
+/* after a round: create the pending objects of the added jobs, drop every other state and the jobs */
+/* every written object at once: returns their count, *total their bytes; fills serials / lens / buf
+ * (and forgets them) when cap >= *total */
+GANON_HOST_API int64_t ganon_objects_take_all(ganon_objects *o, int64_t *serials, int64_t *lens, char *buf,
+                                              int64_t cap, int64_t *total);
+GANON_HOST_API int ganon_objects_settle(ganon_objects *o, int64_t n_live, const int64_t *live_ids);
+GANON_HOST_API const char *ganon_objects_last_error(void);
 
 /* Order in which the write events of an I/O log (ganon_plan_view.events layout, 7 ints each)
  * reach the four FASTQ files (tumor .1, tumor .2, normal .1, normal .2 = file dataset * 2 + slot):

@@ -33,15 +33,18 @@ def test_pipeline_with_oracle_matches_reference(name, whole, tmp_path, monkeypat
     assert bad == {}
 
 
+@pytest.mark.parametrize("impl", ["native", "python"])
 @pytest.mark.parametrize("name", ["fuzz1001", "fuzz2000", "fuzz2003"])
-def test_pipeline_split_alignments_match_reference(name, tmp_path, monkeypatch):
+def test_pipeline_split_alignments_match_reference(name, impl, tmp_path, monkeypatch):
     """Supplementary alignments with SA tags (chimeric reads, the tail on either strand, near the
     primary or on another contig) and secondary alignments: the reference's AnonymizedRead object
     model (creator orientation, primary promotion, supplementary-coordinate masks, left-over
-    merges; objects.py) through the streamed product, against the reference's own files."""
+    merges) through the streamed product, against the reference's own files — with the product's
+    object replay (csrc/ganon_objects.cpp) and its Python restatement (objects.Replay)."""
     from pyoracle import OracleEngine
     from genomeanonymizer_amd.anonymizer_methods import CompleteGermlineAnonymizer
     monkeypatch.setenv("GANON_WHOLE_SAMPLE", "0")
+    monkeypatch.setenv("GANON_OBJECTS", impl)
     bad = run_pipeline_vs_golden(name, str(tmp_path / name), CompleteGermlineAnonymizer(engine=OracleEngine()))
     assert bad == {}
 

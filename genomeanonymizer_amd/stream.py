@@ -445,6 +445,7 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
     carry_info: dict = {}
     replay = (objects.Replay if os.environ.get("GANON_OBJECTS") == "python" else objects.NativeReplay)(carry, carry_info)
     cands: List[np.ndarray] = []
+    carry_floor = 0
     cand_names: List[bytes] = []
     base = [0, 0, 0, 0]
     stats_rows: List[Tuple[int, Dict[str, List[int]]]] = []
@@ -508,19 +509,22 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
                 if data[f]:
                     os.pwrite(fds[f], data[f], off)
                 base[f] += sum(g["sizes"][f] for g in sizes)
-            # carried records still reachable: pending pairs and the end-of-sample candidates
-            pend = resolver.pending()
-            replay.settle(pend)
-            live = set(map(tuple, pend.tolist()))
-            for c in cands:
-                for r in c[c[:, 2] >= 0].tolist() if len(c) else []:
-                    live.add((r[0], r[2], -1, r[3]))
-            for k in [k for k in carry if k[:4] not in live]:
-                del carry[k]
-            live_rows = {(k[0], k[1], k[3]) for k in live}
-            for k in [k for k in carry_info if (k if len(k) == 3 else (k[0], k[1], k[3])) not in live_rows
-                      or (len(k) == 4 and k not in live)]:
-                del carry_info[k]
+            # carried records still reachable: pending pairs and the end-of-sample candidates (pruned
+            # when the carry has doubled or every 16 rounds: each pass walks the whole carry)
+            if len(carry) > max(200_000, 2 * carry_floor) or rnd % 16 == 15:
+                pend = resolver.pending()
+                replay.settle(pend)
+                live = set(map(tuple, pend.tolist()))
+                for c in cands:
+                    for r in c[c[:, 2] >= 0].tolist() if len(c) else []:
+                        live.add((r[0], r[2], -1, r[3]))
+                for k in [k for k in carry if k[:4] not in live]:
+                    del carry[k]
+                live_rows = {(k[0], k[1], k[3]) for k in live}
+                for k in [k for k in carry_info if (k if len(k) == 3 else (k[0], k[1], k[3])) not in live_rows
+                          or (len(k) == 4 and k not in live)]:
+                    del carry_info[k]
+                carry_floor = len(carry)
             job = None
             timing["resolve_s"] += t1 - t0
             timing["write_s"] += time.time() - t1

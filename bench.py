@@ -288,8 +288,9 @@ def main() -> None:
     ap.add_argument("--target", type=int, default=None, help="GANON_PARAM_GROUP_TARGET (cost units per group)")
     ap.add_argument("--no-fastq", action="store_true", help="skip the FASTQ formatter measurement")
     ap.add_argument("--indel-sort", type=int, default=0, help="GANON_PARAM_INDEL_SORT: 0 segmented, 1 global")
-    ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_r01.json"),
-                    help="PMC summary (tools/pmc_summary.py) for the traffic field, if present")
+    ap.add_argument("--pmc", default=None,
+                    help="PMC step summary (tools/pmc_step.py) for the traffic field; default "
+                         "profiles/r02/pmc_step_<config>.json when present")
     args = ap.parse_args()
     for k, v in CONFIGS[args.config]["defaults"].items():
         if getattr(args, k) is None:
@@ -417,12 +418,14 @@ def main() -> None:
     pass_ms = sum(v["avg_ms"] * v["launches"] for v in per_kernel.values()) / args.steps
     alg_total = algorithmic_bytes(arr)
     achieved = alg_total / (pass_ms * 1e-3) / 1e9
-    traffic = None
-    if os.path.exists(args.pmc):
+    traffic = dom_traffic = None
+    pmc_path = args.pmc or os.path.join(REPO, "profiles", "r02", f"pmc_step_{args.config}.json")
+    if os.path.exists(pmc_path):
         try:
-            pmc = json.load(open(args.pmc))
+            pmc = json.load(open(pmc_path))
             if pmc.get("reads") == args.reads and pmc.get("config") == args.config:
                 traffic = pmc.get("step_hbm_bytes")
+                dom_traffic = pmc.get("kernels", {}).get("k_group", {}).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
 
@@ -456,6 +459,7 @@ def main() -> None:
                      "dominant": {"kernel": dom, "algorithmic_bytes_per_launch": dom_bytes,
                                   "avg_launch_ms": round(dom_ms, 5),
                                   "achieved": round(dom_bytes / (dom_ms * 1e-3) / 1e9, 1),
+                                  "traffic": dom_traffic if "k_group" in dom else None,
                                   "frac": round(dom_bytes / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}},
         "pass": {"kernel_ms": round(pass_ms, 4), "algorithmic_bytes": alg_total,
                  "prep_ms": round(sum(v["avg_ms"] * v["launches"] for n, v in per_kernel.items()

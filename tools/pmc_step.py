@@ -1,0 +1,67 @@
+#!/usr/bin/env python3
+"""HBM bytes per launch of every kernel of one bench step, from tools/gpu_pmc_step.sh's passes.
+
+Read bytes = 32 * RDREQ_32B + 64 * RDREQ_64B + 128 * RDREQ_128B (L2-to-fabric read requests by size,
+summed over the L2 channels); write bytes = 64 * WRREQ_64B + 32 * (WRREQ - WRREQ_64B); FETCH_SIZE /
+WRITE_SIZE (KB) beside them (on gfx950 FETCH_SIZE tallies 128-B requests at 64 B,
+MI355X_MICROARCH.md). Kernels are matched to bench.py's names by substring. ``step_hbm_bytes`` (the
+bench's ``roofline.traffic``) sums the kernels of one step: device prep, group kernel, finish and the
+indel tally, each at its launches per step.
+
+usage: pmc_step.py TAG CONFIG READS OUT.json
+"""
+import collections
+import csv
+import glob
+import json
+import re
+import sys
+
+STEP_KERNELS = ("k_prep", "k_group", "k_finish", "k_indel", "k_tile_large", "k_mask_large", "rocprim")
+
+
+def short(name: str) -> str:
+    m = re.search(r"\b(k_[A-Za-z0-9_]+)", name)
+    if m:
+        return m.group(1)
+    return "rocprim:" + name.split("(")[0][-60:] if "rocprim" in name else name[:60]
+
+
+def main():
+    tag, config, reads, out = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4]
+    tot = collections.defaultdict(float)
+    n = collections.Counter()
+    for d in glob.glob(f"gpurun_out/pmc_{tag}_p*"):
+        for f in glob.glob(d + "/**/*counter_collection.csv", recursive=True):
+            for r in csv.DictReader(open(f)):
+                key = (short(r["Kernel_Name"]), r["Counter_Name"])
+                tot[key] += float(r["Counter_Value"])
+                n[key] += 1
+    kern = collections.defaultdict(dict)
+    for (k, c), v in tot.items():
+        kern[k][c] = v / n[(k, c)]
+    # launches per step from the kernel trace (the PMC runs use --steps 3 --warmup 1 = 4 runs + 1 for
+    # the profiled pass, so counts per launch are means; launches per step from the stats run)
+    res = {"config": config, "reads": reads, "kernels": {}}
+    step = 0.0
+    for k, vals in sorted(kern.items()):
+        rd = 32 * vals.get("TCC_EA0_RDREQ_32B", 0) + 64 * vals.get("TCC_EA0_RDREQ_64B", 0) + \
+            128 * vals.get("TCC_EA0_RDREQ_128B", 0)
+        wr64 = vals.get("TCC_EA0_WRREQ_64B", 0)
+        wr = 64 * wr64 + 32 * (vals.get("TCC_EA0_WRREQ", 0) - wr64)
+        res["kernels"][k] = {"hbm_read_bytes_per_launch": int(rd), "hbm_write_bytes_per_launch": int(wr),
+                             "hbm_bytes_per_launch": int(rd + wr), "fetch_size_kb": vals.get("FETCH_SIZE"),
+                             "write_size_kb": vals.get("WRITE_SIZE"), "counters_per_launch": vals}
+        if any(s in k for s in STEP_KERNELS):
+            step += rd + wr
+    res["step_hbm_bytes"] = int(step)
+    res["method"] = ("TCC_EA0_RDREQ_{32B,64B,128B} x size + TCC_EA0_WRREQ{,_64B}; three rocprofv3 --pmc passes "
+                     "(tools/gpu_pmc_step.sh) over bench.py --steps 3, mean over dispatches; step = prep + group + "
+                     "finish + indel kernels, one launch each")
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps({k: v["hbm_bytes_per_launch"] for k, v in res["kernels"].items()}))
+    print("step_hbm_bytes", res["step_hbm_bytes"])
+
+
+if __name__ == "__main__":
+    main()

@@ -17,14 +17,22 @@ import json
 import re
 import sys
 
-STEP_KERNELS = ("k_prep", "k_group", "k_finish", "k_indel", "k_tile_large", "k_mask_large", "rocprim")
+# kernels of one ganon_batch_run + ganon_indel_run (validation, k_prep_reads, the reference copies and
+# the record download run at upload / download only)
+STEP_KERNELS = {"k_prep_groups", "k_prep_emit", "k_prep_emit_flat", "k_prep_emit_waves", "k_prep_long_groups",
+                "k_prep_long_mid", "k_prep_linemap", "k_prep_pieces", "k_group", "k_finish", "k_tile_large",
+                "k_mask_large", "k_indel_mark", "k_indel_count", "k_indel_emit", "k_indel_segs", "k_indel_runs",
+                "k_indel_classify", "rocprim_sort", "rocprim_scan", "rocprim_other"}
 
 
 def short(name: str) -> str:
     m = re.search(r"\b(k_[A-Za-z0-9_]+)", name)
     if m:
         return m.group(1)
-    return "rocprim:" + name.split("(")[0][-60:] if "rocprim" in name else name[:60]
+    if "rocprim" in name:
+        return "rocprim_sort" if ("sort" in name or "radix" in name) else "rocprim_scan" if "scan" in name \
+            else "rocprim_other"
+    return name[:60]
 
 
 def main():
@@ -52,12 +60,13 @@ def main():
         res["kernels"][k] = {"hbm_read_bytes_per_launch": int(rd), "hbm_write_bytes_per_launch": int(wr),
                              "hbm_bytes_per_launch": int(rd + wr), "fetch_size_kb": vals.get("FETCH_SIZE"),
                              "write_size_kb": vals.get("WRITE_SIZE"), "counters_per_launch": vals}
-        if any(s in k for s in STEP_KERNELS):
+        if k in STEP_KERNELS:
             step += rd + wr
     res["step_hbm_bytes"] = int(step)
+    res["step_kernels"] = sorted(k for k in res["kernels"] if k in STEP_KERNELS)
     res["method"] = ("TCC_EA0_RDREQ_{32B,64B,128B} x size + TCC_EA0_WRREQ{,_64B}; three rocprofv3 --pmc passes "
-                     "(tools/gpu_pmc_step.sh) over bench.py --steps 3, mean over dispatches; step = prep + group + "
-                     "finish + indel kernels, one launch each")
+                     "(tools/gpu_pmc_step.sh) over bench.py --steps 3, mean over dispatches; step = the kernels of "
+                     "one ganon_batch_run + ganon_indel_run (step_kernels), one launch each")
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps({k: v["hbm_bytes_per_launch"] for k, v in res["kernels"].items()}))
     print("step_hbm_bytes", res["step_hbm_bytes"])

@@ -304,7 +304,6 @@ constexpr int kGrpThreads = 256;
 #endif
 constexpr int kGrpTile = 256;        // segment records staged per tile
 constexpr int kGrpStack = 80;        // key ranges pending (bisection depth <= 64)
-constexpr int kGrpPatch = 512;       // in-partition masks of one list pass (<= its observations)
 constexpr int kGrpMap = 4096;        // chunk -> segment map entries (larger tiles binary-search)
 constexpr int kGrpQuad = 256;        // lists up to this size are matched without sorting
 constexpr unsigned long long kEmpty = ~0ull;
@@ -322,14 +321,18 @@ struct GrpBatch {
   const int32_t *keep_pos, *span_start, *span_len;
 };
 
-struct GrpShared {
+// OBS: observations held in LDS before a list overflows into the group's global region (512; 1024
+// for deep-coverage batches, ganon_batch_run picks it); the in-partition mask list has the same size.
+template <int OBS>
+struct GrpSharedT {
+  static constexpr int kObs = OBS;
   int4 rec[kGrpTile];               // segment records (layout at kSegMine)
   int pre[kGrpTile];
   uint8_t cmap[kGrpMap];            // staged segment of each chunk (tiles of <= kGrpMap chunks)
   int wsum[kGrpThreads / 64];
-  unsigned long long key[kGrpObs];   // observation list
-  unsigned long long pay[kGrpObs];
-  unsigned long long patch[kGrpPatch];   // nibble index << 4 | (from ^ to)
+  unsigned long long key[OBS];      // observation list
+  unsigned long long pay[OBS];
+  unsigned long long patch[OBS];    // nibble index << 4 | (from ^ to)
   unsigned long long stk_lo[kGrpStack], stk_hi[kGrpStack];
   int stk_mode[kGrpStack];
   unsigned long long kmin, kmax;
@@ -353,7 +356,8 @@ struct PatchSink {
   __device__ bool inside(int64_t byte) const { return (byte >= p0 && byte < p1) || (byte >= q0 && byte < q1); }
 };
 
-__device__ __forceinline__ void sink_patch(GrpShared &sh, const PatchSink &k, int64_t nib, int c, int rc) {
+template <class SH>
+__device__ __forceinline__ void sink_patch(SH &sh, const PatchSink &k, int64_t nib, int c, int rc) {
   const unsigned long long e = ((unsigned long long)nib << 4) | (unsigned long long)(c ^ rc);
   if (k.fused) {
     const int64_t byte = nib >> 1;
@@ -364,7 +368,7 @@ __device__ __forceinline__ void sink_patch(GrpShared &sh, const PatchSink &k, in
     }
     if (k.lds) {
       const int i = atomicAdd(&sh.n_patch, 1);
-      if (i < kGrpPatch) sh.patch[i] = e;
+      if (i < SH::kObs) sh.patch[i] = e;
       return;
     }
   }
@@ -401,23 +405,25 @@ __device__ __forceinline__ unsigned gtab_home(unsigned long long key, int tsize)
   return (unsigned)(((h >> 32) * (unsigned long long)tsize) >> 32);
 }
 
-__device__ __forceinline__ void grp_count(GrpShared &sh, int s_local, int calls, int bases);
+template <class SH>
+__device__ __forceinline__ void grp_count(SH &sh, int s_local, int calls, int bases);
 
 // payload: nibble index:48 | ref:4 | dataset:1 | mine:1
-__device__ __forceinline__ void grp_observe(GrpShared &sh, const GrpRange &R, const GrpGlobal &gg,
+template <class SH>
+__device__ __forceinline__ void grp_observe(SH &sh, const GrpRange &R, const GrpGlobal &gg,
                                             unsigned long long key, int64_t nib, int rc, int ds, uint32_t mine) {
   if (key < R.lo || key >= R.hi) return;
   const unsigned long long pay = (unsigned long long)nib | ((unsigned long long)rc << 48) |
                                  ((unsigned long long)ds << 52) | ((unsigned long long)mine << 53);
   const int k = atomicAdd(&sh.n_obs, 1);
-  if (k < kGrpObs) {
+  if (k < SH::kObs) {
     sh.key[k] = key;
     sh.pay[k] = pay;
   } else {
     // past the LDS list: straight into the group's global region (no second scan)
-    if (k - kGrpObs < gg.cap - kGrpObs) {
-      gg.aux->okey[gg.off + (k - kGrpObs)] = key;
-      gg.aux->opay[gg.off + (k - kGrpObs)] = pay;
+    if (k - SH::kObs < gg.cap - SH::kObs) {
+      gg.aux->okey[gg.off + (k - SH::kObs)] = key;
+      gg.aux->opay[gg.off + (k - SH::kObs)] = pay;
     }
   }
 }
@@ -454,7 +460,8 @@ __device__ __forceinline__ void copy_windows(const uint8_t *__restrict__ src, ui
 
 // Stage records [c0, c0 + nh) in LDS with the exclusive prefix of their chunk counts;
 // returns the tile's chunk total.
-__device__ __forceinline__ int grp_tile(GrpShared &sh, const int4 *__restrict__ rec4, int64_t c0, int nh,
+template <class SH>
+__device__ __forceinline__ int grp_tile(SH &sh, const int4 *__restrict__ rec4, int64_t c0, int nh,
                                         int chunk) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t ix = c0 + (tid < nh ? tid : nh - 1);
@@ -495,7 +502,8 @@ __device__ __forceinline__ int grp_tile(GrpShared &sh, const int4 *__restrict__ 
 }
 
 // The staged segment owning chunk t (largest j with pre[j] <= t).
-__device__ __forceinline__ int grp_find(const GrpShared &sh, int nh, int total, int t) {
+template <class SH>
+__device__ __forceinline__ int grp_find(const SH &sh, int nh, int total, int t) {
   if (total <= kGrpMap) return sh.cmap[t];
   int lo = 0, hi = nh - 1;
   while (lo < hi) {
@@ -510,8 +518,8 @@ __device__ __forceinline__ int grp_find(const GrpShared &sh, int nh, int total, 
 // is 16 * K bases: each thread loads the 2K + 1 sequence dwords and 2K + 1 reference dwords
 // covering its chunk at once (one memory round trip per chunk), then takes the K 16-base
 // windows out of registers with static indices.
-template <int K, bool REF2>
-__device__ __forceinline__ void grp_scan(const GrpBatch &B, GrpShared &sh, const GrpRange &R, const GrpGlobal &gg,
+template <int K, bool REF2, class SH>
+__device__ __forceinline__ void grp_scan(const GrpBatch &B, SH &sh, const GrpRange &R, const GrpGlobal &gg,
                                          int64_t i_begin, int64_t i_end, const int4 *__restrict__ rec4, int skip) {
   const int tid = threadIdx.x;
   for (int64_t c0 = i_begin; c0 < i_end; c0 += kGrpTile) {
@@ -610,7 +618,8 @@ __device__ __forceinline__ void lds_bitonic(unsigned long long *key, unsigned lo
 // observation against the whole list (no sort, no barrier); longer lists are sorted and one
 // thread takes each run of equal keys. count: add calls/bases to the per-scope and workgroup
 // totals (off for a re-run that only re-applies masks).
-__device__ __forceinline__ void grp_count(GrpShared &sh, int s_local, int calls, int bases) {
+template <class SH>
+__device__ __forceinline__ void grp_count(SH &sh, int s_local, int calls, int bases) {
   if (calls) {
     atomicAdd(&sh.cnt_calls[s_local], calls);
     atomicAdd(&sh.blk_calls, calls);
@@ -621,7 +630,8 @@ __device__ __forceinline__ void grp_count(GrpShared &sh, int s_local, int calls,
   }
 }
 
-__device__ __forceinline__ void grp_classify(const GrpBatch &B, GrpShared &sh, int n, int s_begin,
+template <class SH>
+__device__ __forceinline__ void grp_classify(const GrpBatch &B, SH &sh, int n, int s_begin,
                                              const PatchSink &sink, bool count) {
   const int tid = threadIdx.x;
   if (n <= kGrpQuad) {
@@ -668,7 +678,8 @@ __device__ __forceinline__ void grp_classify(const GrpBatch &B, GrpShared &sh, i
 // Overflow path: n observations of one key range sit in the group's global region. Aggregate
 // them in a hash table of distinct keys (workgroup-scope atomics in L2), count the TN calls
 // (minus the kept variant), and mask the observations of reads the scopes write.
-__device__ __forceinline__ void grp_global(const GrpBatch &B, GrpShared &sh, const GrpGlobal &gg, int n,
+template <class SH>
+__device__ __forceinline__ void grp_global(const GrpBatch &B, SH &sh, const GrpGlobal &gg, int n,
                                            int s_begin, const PatchSink &sink) {
   const int tid = opaque_tid();
   const int tsize = max(2 * n, 64);
@@ -780,7 +791,8 @@ __device__ __forceinline__ void grp_global(const GrpBatch &B, GrpShared &sh, con
 // Fused: apply the sorted in-partition list (nibble << 4 | from ^ to) with one plain byte store
 // per masked byte, out[b] ^ mask — the partition copy and earlier masks of that byte were
 // stored by this workgroup and have drained (read back from L2).
-__device__ __forceinline__ void grp_patch_bytes(const GrpBatch &B, GrpShared &sh, int np, uint8_t *out) {
+template <class SH>
+__device__ __forceinline__ void grp_patch_bytes(const GrpBatch &B, SH &sh, int np, uint8_t *out) {
   for (int i = threadIdx.x; i < np; i += kGrpThreads) {
     const unsigned long long e = sh.patch[i];
     const int64_t byte = (int64_t)(e >> 5);
@@ -799,12 +811,12 @@ __device__ __forceinline__ void grp_patch_bytes(const GrpBatch &B, GrpShared &sh
 // {seg_end lo, hi, seg_mid lo, hi}, {partition piece A begin lo, hi, end lo, hi} (bytes; fused
 // only), {global region offset lo, hi, capacity, 0}, {piece B begin lo, hi, end lo, hi};
 // segments [seg_begin, seg_mid) have an all-ACGT reference range (2-bit reference).
-template <int U, bool FUSED>
-__global__ void __launch_bounds__(kGrpThreads, (U == 1 ? 6 : U == 2 ? GANON_K2_BLOCKS : U == 4 ? 5 : 4)) k_group(const GrpBatch B, const int4 *__restrict__ groups,
+template <int U, bool FUSED, int OBS>
+__global__ void __launch_bounds__(kGrpThreads, (OBS > 512 ? 4 : U == 1 ? 6 : U == 2 ? GANON_K2_BLOCKS : U == 4 ? 5 : 4)) k_group(const GrpBatch B, const int4 *__restrict__ groups,
                                                        const int4 *__restrict__ rec4,
                                                        uint8_t *__restrict__ out, const GrpAux *__restrict__ aux,
                                                        int skip, int nt_copy) {
-  __shared__ GrpShared sh;
+  __shared__ GrpSharedT<OBS> sh;
   const int tid = threadIdx.x;
   const int4 g0 = groups[kGrpRec * blockIdx.x];
   const int4 g1 = groups[kGrpRec * blockIdx.x + 1];
@@ -873,13 +885,13 @@ __global__ void __launch_bounds__(kGrpThreads, (U == 1 ? 6 : U == 2 ? GANON_K2_B
     if (skip & kSkipClassify) continue;
     const int n = sh.n_obs;
     if (tid == 0 && n > kGrpQuad)   // path counters (ganon_batch_path_counts): sorted list, region, split
-      atomicAdd(&aux->paths[n <= kGrpObs ? 0 : n <= gg.cap ? 1 : 2], 1ull);
-    if (n > kGrpObs) {
+      atomicAdd(&aux->paths[n <= OBS ? 0 : n <= gg.cap ? 1 : 2], 1ull);
+    if (n > OBS) {
       if (n <= gg.cap) {
         // the list joins the region's tail: n observations contiguous in the region
-        for (int i = opaque_tid(); i < kGrpObs; i += kGrpThreads) {
-          aux->okey[gg.off + (n - kGrpObs) + i] = sh.key[i];
-          aux->opay[gg.off + (n - kGrpObs) + i] = sh.pay[i];
+        for (int i = opaque_tid(); i < OBS; i += kGrpThreads) {
+          aux->okey[gg.off + (n - OBS) + i] = sh.key[i];
+          aux->opay[gg.off + (n - OBS) + i] = sh.pay[i];
         }
         __builtin_amdgcn_s_waitcnt(0);   // region stores at L2 before the barrier
         __syncthreads();
@@ -892,7 +904,7 @@ __global__ void __launch_bounds__(kGrpThreads, (U == 1 ? 6 : U == 2 ? GANON_K2_B
       __builtin_amdgcn_s_waitcnt(0);
       __syncthreads();
       for (int i = opaque_tid(); i < gg.cap; i += kGrpThreads) {
-        const unsigned long long k = i < kGrpObs ? sh.key[i] : ld_l2(aux->okey + gg.off + (i - kGrpObs));
+        const unsigned long long k = i < OBS ? sh.key[i] : ld_l2(aux->okey + gg.off + (i - OBS));
         atomicMin(&sh.kmin, k);
         atomicMax(&sh.kmax, k);
       }
@@ -1362,6 +1374,15 @@ int load_batch(ganon_ctx *ctx, ganon_dbatch *db, const ganon_batch *b, const gan
   // bytes outside every read are never written by the masking kernels: make them defined
   HIP_OR_FAIL(hipMemsetAsync(db->out, 0, (size_t)b->seq_bytes + 16, ctx->stream));
   if ((rc = ganon_prep::plan(ctx, db, b->scope_incid_off))) return rc;
+  {
+    // deep coverage (aligned bases per position of the scopes' spans): its groups' observation lists
+    // outgrow 512 entries and would take the global-region path (profiles/r02/pmc_step_c3)
+    double span = 0.0, bases = 0.0;
+    for (int32_t s = 0; s < b->n_scopes; ++s) span += (double)b->scope_span_len[s];
+    for (int32_t r = 0; r < b->n_reads; ++r) bases += (double)b->read_len[r];
+    const double mean_len = b->n_reads ? bases / b->n_reads : 0.0;
+    db->deep = !db->long_mode && span > 0.0 && (double)b->n_incid * mean_len >= 16.0 * span;
+  }
   if ((rc = plan_huge(ctx, db, b))) return rc;
   const GrpAux a{db->scope_calls,
                  db->scope_bases,
@@ -1501,6 +1522,12 @@ GANON_API int ganon_ctx_set_param(ganon_ctx *ctx, int param, int value) {
     ctx->prep_long = value;
     return GANON_OK;
   }
+  if (param == GANON_PARAM_GROUP_OBS) {
+    if (value != 0 && value != 512 && value != 1024)
+      return fail(ctx, GANON_E_ARG, "group observation list: 0 (auto), 512 or 1024 (got %d)", value);
+    ctx->group_obs = value;
+    return GANON_OK;
+  }
   if (param == GANON_PARAM_NT_COPY) {
     ctx->nt_copy = value != 0;
     return GANON_OK;
@@ -1581,7 +1608,10 @@ GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
     // 16-base chunks per thread: long reads (short segments between indels) waste less with one
     // (profiles/r02/sweep_c5.jsonl); short reads run best with two (sweep_c3.jsonl)
     const int u = ctx->group_unroll ? ctx->group_unroll : db->long_mode ? 1 : 2;
-    auto kern = u == 2 ? k_group<2, true> : u == 4 ? k_group<4, true> : u == 8 ? k_group<8, true> : k_group<1, true>;
+    const int obs = ctx->group_obs ? ctx->group_obs : db->deep ? 1024 : 512;
+    auto kern = obs == 1024 ? (u == 1 ? k_group<1, true, 1024> : k_group<2, true, 1024>)
+                            : u == 2 ? k_group<2, true, 512> : u == 4 ? k_group<4, true, 512>
+                            : u == 8 ? k_group<8, true, 512> : k_group<1, true, 512>;
     const GrpBatch GB{B.seq, B.ref, B.keep_code, B.ref2, B.keep_pos, B.span_start, B.span_len};
     kern<<<db->n_groups, kGrpThreads, 0, st>>>(GB, static_cast<const int4 *>(db->b_groups.p),
                                                static_cast<const int4 *>(db->b_seg4.p), db->out, db->aux,

@@ -202,19 +202,24 @@ def test_hip_configs2_density_matches_oracle(masker, oracle):
     arr, info = config2_batch(n_reads=2_400_000, genome=6_000_000, n_contigs=2, n_windows=600,
                               n_germline=162_000, seed=12, window_spacing=10_000)
     assert info["germline_snps"] > 150_000
+    from genomeanonymizer_amd import native
     o_out, o_calls, o_bases, o_tot = oracle.mask(arr)
     db = masker.upload(arr)
     try:
-        db.run()
-        out, calls, bases, tot = db.download()
-        paths = db.path_counts()
+        runs = {}
+        for obs in (512, 0):          # the 512-entry lists (region path forced) and the auto choice
+            masker.set_param(native.PARAM_GROUP_OBS, obs)
+            db.run()
+            runs[obs] = db.download() + (db.path_counts(),)
     finally:
+        masker.set_param(native.PARAM_GROUP_OBS, 0)
         db.free()
-    assert np.array_equal(calls, o_calls)
-    assert np.array_equal(bases, o_bases)
-    assert np.array_equal(out, o_out)
+    for obs, (out, calls, bases, tot, paths) in runs.items():
+        assert np.array_equal(calls, o_calls), obs
+        assert np.array_equal(bases, o_bases), obs
+        assert np.array_equal(out, o_out), obs
     assert o_bases.sum() > 100_000
-    assert paths["region_passes"] > 0, paths
+    assert runs[512][4]["region_passes"] > 0, runs[512][4]
 
 
 @pytest.mark.parametrize("whole", [False, True], ids=["streaming", "whole_sample"])

@@ -26,9 +26,12 @@ def main():
     arr, _ = bench.make_batch(args, 0)
     m = native.HipMasker(0)
     ref = m.upload_reference(arr["ref_nt16"])
-    settings = [(u, t) for t in (352, 704, 1408) for u in (1, 2, 4)]
+    mode = sys.argv[3] if len(sys.argv) > 3 else "grid"
+    settings = [(u, t) for t in (352, 704, 1408) for u in (1, 2, 4)] if mode == "grid" else [(0, 0)]
+    obs_list = (512, 1024) if mode == "obs" else (0,)
     ref_tot, best, db, cur_t = None, None, None, None
-    for u, t in settings:
+    for (u, t), obs in [(x, o) for x in settings for o in obs_list]:
+        m.set_param(native.PARAM_GROUP_OBS, obs)
         m.set_param(native.PARAM_GROUP_UNROLL, u)
         if t != cur_t:                   # the target applies at upload
             if db is not None:
@@ -54,7 +57,7 @@ def main():
         m.set_profiling(False)
         tot = db.totals()[:2].tolist()
         ref_tot = ref_tot or tot
-        line = {"config": cfg, "unroll": u, "target": t, "ms_per_step": round(ms, 4),
+        line = {"config": cfg, "unroll": u, "target": t, "obs": obs, "ms_per_step": round(ms, 4),
                 "kernels_ms": {k: round(v, 4) for k, v in kt.items()}, "totals": tot, "same": tot == ref_tot}
         print(json.dumps(line), flush=True)
         if best is None or ms < best[0]:

@@ -140,7 +140,6 @@ struct ganon_dbatch {
   // long-read mode (a read with more than one aligned segment): groups cut on the prefix of segments
   // per scope (scost, upload) instead of the CSR offsets, and emitted one wave per incidence
   bool long_mode = false;
-  bool deep = false;            // deep coverage: the group kernel keeps 1024 observations in LDS
   bool flat_mode = false;   // every read has at most one aligned segment: one record per incidence, in place
   int64_t *scost = nullptr;
   int64_t n_seg = 0, region = 0, far_cap = 0, n_written = 0, region_per_incid = 0;

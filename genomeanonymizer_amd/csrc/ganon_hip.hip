@@ -1374,15 +1374,7 @@ int load_batch(ganon_ctx *ctx, ganon_dbatch *db, const ganon_batch *b, const gan
   // bytes outside every read are never written by the masking kernels: make them defined
   HIP_OR_FAIL(hipMemsetAsync(db->out, 0, (size_t)b->seq_bytes + 16, ctx->stream));
   if ((rc = ganon_prep::plan(ctx, db, b->scope_incid_off))) return rc;
-  {
-    // deep coverage (aligned bases per position of the scopes' spans): its groups' observation lists
-    // outgrow 512 entries and would take the global-region path (profiles/r02/pmc_step_c3)
-    double span = 0.0, bases = 0.0;
-    for (int32_t s = 0; s < b->n_scopes; ++s) span += (double)b->scope_span_len[s];
-    for (int32_t r = 0; r < b->n_reads; ++r) bases += (double)b->read_len[r];
-    const double mean_len = b->n_reads ? bases / b->n_reads : 0.0;
-    db->deep = !db->long_mode && span > 0.0 && (double)b->n_incid * mean_len >= 16.0 * span;
-  }
+
   if ((rc = plan_huge(ctx, db, b))) return rc;
   const GrpAux a{db->scope_calls,
                  db->scope_bases,
@@ -1608,7 +1600,9 @@ GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
     // 16-base chunks per thread: long reads (short segments between indels) waste less with one
     // (profiles/r02/sweep_c5.jsonl); short reads run best with two (sweep_c3.jsonl)
     const int u = ctx->group_unroll ? ctx->group_unroll : db->long_mode ? 1 : 2;
-    const int obs = ctx->group_obs ? ctx->group_obs : db->deep ? 1024 : 512;
+    // 512 unless forced: the 1024-entry list (4 workgroups per CU instead of 6) measured slower on
+    // c3 too (3.19 vs 2.84 ms, profiles/r02/sweep_c3_obs.jsonl) — occupancy outweighs the region path
+    const int obs = ctx->group_obs ? ctx->group_obs : 512;
     auto kern = obs == 1024 ? (u == 1 ? k_group<1, true, 1024> : k_group<2, true, 1024>)
                             : u == 2 ? k_group<2, true, 512> : u == 4 ? k_group<4, true, 512>
                             : u == 8 ? k_group<8, true, 512> : k_group<1, true, 512>;

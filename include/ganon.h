@@ -138,8 +138,7 @@ enum { GANON_PARAM_GROUP_UNROLL = 1, GANON_PARAM_GROUP_SKIP = 2, GANON_PARAM_GRO
        GANON_PARAM_NT_COPY = 4, GANON_PARAM_REF2 = 5, GANON_PARAM_FASTQ_SKIP = 6, GANON_PARAM_FASTQ_KD = 7,
        GANON_PARAM_INDEL_SORT = 8, GANON_PARAM_PREP_LONG = 9, GANON_PARAM_GROUP_OBS = 10 };
 /* GANON_PARAM_GROUP_OBS: observations a group keeps in LDS before its list overflows into the global
- * region: 512 or 1024; 0 (default) = 1024 for deep-coverage short-read batches (incidences x mean read
- * length >= 16 x the scopes' total span, decided at upload), else 512. */
+ * region: 512 (0, default) or 1024 (fewer resident workgroups; slower on every measured config). */
 GANON_API int ganon_ctx_set_param(ganon_ctx *ctx, int param, int value);
 /* When on, ganon_batch_run records a HIP event pair around each kernel it launches. */
 GANON_API int ganon_ctx_set_profiling(ganon_ctx *ctx, int enabled);

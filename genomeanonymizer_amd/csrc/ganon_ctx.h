@@ -30,6 +30,7 @@ struct ganon_ctx {
   int fq_kd = 0;               // GANON_PARAM_FASTQ_KD (0: quad kernel, 2 quads per lane; 3: dword kernel)
   int indel_sort = 0;          // GANON_PARAM_INDEL_SORT
   int group_obs = 0;           // GANON_PARAM_GROUP_OBS (0 auto, 512, 1024)
+  int prep_unroll = 0;         // GANON_PARAM_PREP_UNROLL (0 auto = 2, 1, 2, 4)
   std::string err;
   struct Rec { std::string name; hipEvent_t e0, e1; };
   std::vector<Rec> recs;

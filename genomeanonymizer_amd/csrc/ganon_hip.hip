@@ -1514,6 +1514,12 @@ GANON_API int ganon_ctx_set_param(ganon_ctx *ctx, int param, int value) {
     ctx->prep_long = value;
     return GANON_OK;
   }
+  if (param == GANON_PARAM_PREP_UNROLL) {
+    if (value != 0 && value != 1 && value != 2 && value != 4)
+      return fail(ctx, GANON_E_ARG, "prep unroll: 0 (auto), 1, 2 or 4 (got %d)", value);
+    ctx->prep_unroll = value;
+    return GANON_OK;
+  }
   if (param == GANON_PARAM_GROUP_OBS) {
     if (value != 0 && value != 512 && value != 1024)
       return fail(ctx, GANON_E_ARG, "group observation list: 0 (auto), 512 or 1024 (got %d)", value);

@@ -702,6 +702,8 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_emit(const Raw R, const l
 // segment, or in a huge scope, leaves a zero-length record the group kernel skips). A group whose
 // records all have an all-ACGT reference range is read through the 2-bit reference (clean part =
 // the whole range), any other group through the nt16 reference.
+// kFlatU: incidences per thread and trip (GANON_PARAM_PREP_UNROLL)
+template <int kFlatU>
 __global__ void __launch_bounds__(kPrepThreads) k_prep_emit_flat(const Raw R, const longlong2 *__restrict__ gmeta,
                                                                  int n_groups, const uint64_t *__restrict__ bad,
                                                                  int64_t n_blk, long long region_per_incid,
@@ -731,18 +733,18 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_emit_flat(const Raw R, co
   __syncthreads();
   unsigned long long mn0 = kNone, mn1 = kNone;
   bool dirty = false;
-  // two incidences per thread and trip, their loads issued together (the chain incidence -> read
+  // kFlatU incidences per thread and trip, their loads issued together (the chain incidence -> read
   // fields -> CIGAR -> reference block bitmap is latency bound)
-  for (long long base = i0; base < i1; base += 2 * kPrepThreads) {
-    EmitInc e[2];
-    int jj[2];
+  for (long long base = i0; base < i1; base += kFlatU * kPrepThreads) {
+    EmitInc e[kFlatU];
+    int jj[kFlatU];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < kFlatU; ++u) {
       const long long i = base + tid + kPrepThreads * u;
       e[u].r = i < i1 ? R.incid_read[i] : -1;
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < kFlatU; ++u) {
       const int rr = e[u].r >= 0 ? e[u].r : 0;
       e[u].cg = R.cigar + R.cig_off[rr];
       e[u].ncig = e[u].r >= 0 ? R.n_cig[rr] : 0;
@@ -754,9 +756,9 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_emit_flat(const Raw R, co
       jj[u] = lds_upper(off, ns, base + tid + kPrepThreads * u);
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) e[u].w0 = e[u].ncig > 0 ? e[u].cg[0] : 0u;
+    for (int u = 0; u < kFlatU; ++u) e[u].w0 = e[u].ncig > 0 ? e[u].cg[0] : 0u;
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < kFlatU; ++u) {
       if (e[u].r < 0) continue;
       const EmitInc &x = e[u];
       const int j = jj[u];
@@ -1088,7 +1090,9 @@ int launch_emit(ganon_ctx *ctx, ganon_dbatch *db, const Raw &R, int write) {
     return check_launch(ctx, "k_prep_emit (long)");
   }
   if (db->flat_mode) {
-    hipLaunchKernelGGL(k_prep_emit_flat, dim3((unsigned)db->n_groups), dim3(kPrepThreads), 0, ctx->stream, R,
+    auto flat = ctx->prep_unroll == 4 ? k_prep_emit_flat<4> : ctx->prep_unroll == 1 ? k_prep_emit_flat<1>
+                                                                                   : k_prep_emit_flat<2>;
+    hipLaunchKernelGGL(flat, dim3((unsigned)db->n_groups), dim3(kPrepThreads), 0, ctx->stream, R,
                        static_cast<const longlong2 *>(db->b_gs0.p), db->n_groups, db->ref->bad, db->ref->n_blk,
                        (long long)db->region_per_incid, static_cast<int4 *>(db->b_seg4.p),
                        static_cast<int4 *>(db->b_groups.p), static_cast<unsigned long long *>(db->b_lo.p), line_map(db),

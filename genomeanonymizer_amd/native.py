@@ -197,6 +197,7 @@ PARAM_FASTQ_KD = 7       # include/ganon.h GANON_PARAM_FASTQ_KD
 PARAM_INDEL_SORT = 8     # include/ganon.h GANON_PARAM_INDEL_SORT (0 segmented, 1 global)
 PARAM_PREP_LONG = 9      # include/ganon.h GANON_PARAM_PREP_LONG (-1 auto, 0 never, 1 always; at upload)
 PARAM_GROUP_OBS = 10     # include/ganon.h GANON_PARAM_GROUP_OBS (0 auto, 512, 1024)
+PARAM_PREP_UNROLL = 11   # include/ganon.h GANON_PARAM_PREP_UNROLL (0 auto, 1, 2, 4)
 
 EXPORTED_HIP_SYMBOLS = (
     "ganon_ctx_create", "ganon_ctx_destroy", "ganon_last_error", "ganon_abi_version",

@@ -136,7 +136,10 @@ GANON_API int ganon_ctx_set_variant(ganon_ctx *ctx, int variant);
  * when it applies; 0: the two-pass per-group emit. Same results. */
 enum { GANON_PARAM_GROUP_UNROLL = 1, GANON_PARAM_GROUP_SKIP = 2, GANON_PARAM_GROUP_TARGET = 3,
        GANON_PARAM_NT_COPY = 4, GANON_PARAM_REF2 = 5, GANON_PARAM_FASTQ_SKIP = 6, GANON_PARAM_FASTQ_KD = 7,
-       GANON_PARAM_INDEL_SORT = 8, GANON_PARAM_PREP_LONG = 9, GANON_PARAM_GROUP_OBS = 10 };
+       GANON_PARAM_INDEL_SORT = 8, GANON_PARAM_PREP_LONG = 9, GANON_PARAM_GROUP_OBS = 10,
+       GANON_PARAM_PREP_UNROLL = 11 };
+/* GANON_PARAM_PREP_UNROLL: incidences each thread of the one-segment prep emit takes per trip (1, 2,
+ * 4; 0 = default). */
 /* GANON_PARAM_GROUP_OBS: observations a group keeps in LDS before its list overflows into the global
  * region: 512 (0, default) or 1024 (fewer resident workgroups; slower on every measured config). */
 GANON_API int ganon_ctx_set_param(ganon_ctx *ctx, int param, int value);

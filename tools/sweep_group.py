@@ -29,9 +29,15 @@ def main():
     mode = sys.argv[3] if len(sys.argv) > 3 else "grid"
     settings = [(u, t) for t in (352, 704, 1408) for u in (1, 2, 4)] if mode == "grid" else [(0, 0)]
     obs_list = (512, 1024) if mode == "obs" else (0,)
+    pu_list = (1, 2, 4) if mode == "prep" else (0,)
+    if mode == "prep":
+        obs_list = pu_list
     ref_tot, best, db, cur_t = None, None, None, None
     for (u, t), obs in [(x, o) for x in settings for o in obs_list]:
-        m.set_param(native.PARAM_GROUP_OBS, obs)
+        if mode == "prep":
+            m.set_param(native.PARAM_PREP_UNROLL, obs)
+        else:
+            m.set_param(native.PARAM_GROUP_OBS, obs)
         m.set_param(native.PARAM_GROUP_UNROLL, u)
         if t != cur_t:                   # the target applies at upload
             if db is not None:

@@ -52,7 +52,7 @@ def _worker(rank, world, port, name, workdir, q, engine="oracle", fail_rank=-1):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name,index", [("edge", True), ("tiny", False)])
+@pytest.mark.parametrize("name,index", [("edge", True), ("tiny", False), ("fuzz2003", False)])
 def test_two_rank_contig_shards_match_reference(name, index, tmp_path):
     from helpers import GOLDEN, run_pipeline_vs_golden
     from genomeanonymizer_amd.synth.generate import generate, scenario

@@ -13,7 +13,7 @@ from test_distributed import _free_port, _worker
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("name", ["edge", "config1"])
+@pytest.mark.parametrize("name", ["edge", "config1", "fuzz2003"])
 def test_two_rank_hip_contig_shards_match_reference(name, tmp_path, hip_built):
     import gzip
     from helpers import GOLDEN

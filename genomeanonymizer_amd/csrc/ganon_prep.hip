@@ -702,6 +702,8 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_emit(const Raw R, const l
 // segment, or in a huge scope, leaves a zero-length record the group kernel skips). A group whose
 // records all have an all-ACGT reference range is read through the 2-bit reference (clean part =
 // the whole range), any other group through the nt16 reference.
+constexpr unsigned long long kLongReadLen = 1000;   // auto prep: long-read mode above this read length
+
 // kFlatU: incidences per thread and trip (GANON_PARAM_PREP_UNROLL)
 template <int kFlatU>
 __global__ void __launch_bounds__(kPrepThreads) k_prep_emit_flat(const Raw R, const longlong2 *__restrict__ gmeta,
@@ -1174,7 +1176,10 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db, const int64_t *host_incid_off) {
     HIP_OR_FAIL(hipStreamSynchronize(st));
     // prep mode: long (a read with several segments, or forced), one-segment (every read has at most
     // one: the default for short reads), or the two-pass short emit (GANON_PARAM_PREP_LONG 0)
-    db->long_mode = ctx->prep_long == 1 || (ctx->prep_long != 0 && max_seg > 1);
+    // auto: the long-read prep (a wave per incidence) only for long reads; short reads with indels
+    // (several segments, a few per cent of the reads) take the two-pass emit — the long prep took
+    // 11.3 ms instead of ~0.2 on a planner-built 2 M-read batch (profiles/r02/planner_batch_bench.json)
+    db->long_mode = ctx->prep_long == 1 || (ctx->prep_long == -1 && max_seg > 1 && max_len > kLongReadLen);
     db->flat_mode = !db->long_mode && max_seg <= 1 && (ctx->prep_long == -1 || ctx->prep_long == 2);
     db->region_per_incid = (int64_t)((max_len + 47) / 48);
     if (!ctx->group_target) db->group_target = db->long_mode ? 1408 : 704;   // auto (sweep_c5 / sweep_c3)

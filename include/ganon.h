@@ -131,9 +131,11 @@ GANON_API int ganon_ctx_set_variant(ganon_ctx *ctx, int variant);
  * sorts every observation in one global sort of 64-bit scope|position keys (1). Same records.
  * GANON_PARAM_PREP_LONG (read at upload): which device prep builds the segment records. -1 (default):
  * the long-read prep (groups cut on the prefix of aligned segments per scope, one wave per incidence
- * walking its CIGAR) when a read of the batch has more than one segment, else the one-segment prep
- * (one record per incidence at its own index); 1: always the long-read prep; 2: the one-segment prep
- * when it applies; 0: the two-pass per-group emit. Same results. */
+ * walking its CIGAR) when a read of the batch has more than one segment and reads are longer than
+ * 1000 bases; the one-segment prep (one record per incidence at its own index) when no read has more
+ * than one segment; else (short reads with indels) the two-pass per-group emit; 1: always the
+ * long-read prep; 2: the one-segment prep when it applies; 0: the two-pass per-group emit. Same
+ * results. */
 enum { GANON_PARAM_GROUP_UNROLL = 1, GANON_PARAM_GROUP_SKIP = 2, GANON_PARAM_GROUP_TARGET = 3,
        GANON_PARAM_NT_COPY = 4, GANON_PARAM_REF2 = 5, GANON_PARAM_FASTQ_SKIP = 6, GANON_PARAM_FASTQ_KD = 7,
        GANON_PARAM_INDEL_SORT = 8, GANON_PARAM_PREP_LONG = 9, GANON_PARAM_GROUP_OBS = 10,

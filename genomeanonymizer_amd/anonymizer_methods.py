@@ -98,40 +98,49 @@ def build_batch(plan: Plan, tables: Tuple[ReadTable, ReadTable], fasta: FastaRef
     incid_off = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
     incid = (np.concatenate([np.concatenate([bidx[0][sc.t_rows], bidx[1][sc.n_rows]]) for sc in scopes]).astype(np.int32)
              if scopes else np.zeros(0, np.int32))
-    seq_parts = [T.seq, N.seq]
-    dup_off: Dict[Tuple[int, int, int], int] = {}
-    dup_rows = []
-    extra = {k: [] for k in ("ref_start", "read_len", "seq_off", "cig_off", "n_cig", "dataset")}
+    # the same read masked in another scope: a copy of its record, the one that scope's
+    # incidence points at (first occurrence per (dataset, row, scope); vectorised)
+    cand = np.nonzero(~first)[0]
+    cand = cand[ws[b[cand]] != loc[w_sc[cand]]]
+    if len(cand):
+        trip = np.stack([w_ds[cand], w_row[cand], w_sc[cand]], axis=1)
+        _, fi = np.unique(trip, axis=0, return_index=True)
+        cand = cand[np.sort(fi)]
+    d_ds, d_row, d_sc = w_ds[cand], w_row[cand], w_sc[cand]
+    nd = len(cand)
+    d0 = d_ds == 0
+    r0, r1 = np.where(d0, d_row, 0), np.where(d0, 0, d_row)
+    pick = lambda f: np.where(d0, getattr(T, f)[r0] if T.n else 0, getattr(N, f)[r1] if N.n else 0).astype(np.int64)
+    d_len = pick("l_seq")
+    nbytes = (d_len + 1) // 2
     n_seq = len(T.seq) + len(N.seq)
-    ex_ws = []
-    for i in np.nonzero(~first)[0].tolist():        # the same read masked in another scope
-        d, r, sid = int(w_ds[i]), int(w_row[i]), int(w_sc[i])
-        if (d, r, sid) in dup_off or ws[b[i]] == loc[sid]:
-            continue
-        t = tables[d]
-        nbytes = (int(t.l_seq[r]) + 1) // 2
-        o = int(t.seq_off[r])
-        seq_parts.append(t.seq[o:o + nbytes])
-        dup_off[(d, r, sid)] = n_seq
-        k = int(loc[sid])
-        seg = incid[incid_off[k]:incid_off[k + 1]]
-        hit = np.nonzero(seg == b[i])[0]
-        seg[hit] = n_reads + len(dup_rows)
-        extra["ref_start"].append(int(t.pos[r]))
-        extra["read_len"].append(int(t.l_seq[r]))
-        extra["seq_off"].append(n_seq)
-        extra["cig_off"].append(int(t.cig_off[r]) + cig_base[d])
-        extra["n_cig"].append(int(t.n_cigar[r]))
-        extra["dataset"].append(d)
-        ex_ws.append(k)
-        dup_rows.append((d, r))
-        n_seq += nbytes
-    if dup_rows:
-        for f, dt in (("ref_start", np.int32), ("read_len", np.int32), ("seq_off", np.int64), ("cig_off", np.int64),
-                      ("n_cig", np.int32), ("dataset", np.uint8)):
-            arr[f] = np.concatenate([arr[f], np.array(extra[f], dt)])
-        ws = np.concatenate([ws, np.array(ex_ws, np.int32)])
-    arr["seq_nt16"] = np.ascontiguousarray(np.concatenate(seq_parts).astype(np.uint8))
+    d_seq = n_seq + np.concatenate([[0], np.cumsum(nbytes)[:-1]]).astype(np.int64) if nd else np.zeros(0, np.int64)
+    d_k = loc[d_sc]
+    d_idx = n_reads + np.arange(nd, dtype=np.int64)          # batch read index of each copy
+    if nd:
+        src = np.repeat(np.where(d0, 0, len(T.seq)) + pick("seq_off"), nbytes) + \
+            (np.arange(int(nbytes.sum())) - np.repeat(np.concatenate([[0], np.cumsum(nbytes)[:-1]]), nbytes))
+        seq_all = np.concatenate([T.seq, N.seq, np.concatenate([T.seq, N.seq])[src]])
+        # re-point the copy's scope incidences at the copy
+        inc_k = np.repeat(np.arange(len(scopes), dtype=np.int64), counts)
+        M = n_reads + nd + 1
+        dkey = d_k * M + b[cand]
+        order = np.argsort(dkey, kind="stable")
+        ikey = inc_k * M + incid
+        pos = np.minimum(np.searchsorted(dkey[order], ikey), nd - 1)
+        hit = dkey[order][pos] == ikey
+        incid = incid.copy()
+        incid[hit] = d_idx[order][pos[hit]].astype(np.int32)
+        for f, v, dt in (("ref_start", pick("pos"), np.int32), ("read_len", d_len, np.int32), ("seq_off", d_seq, np.int64),
+                         ("cig_off", pick("cig_off") + np.where(d0, cig_base[0], cig_base[1]), np.int64),
+                         ("n_cig", pick("n_cigar"), np.int32), ("dataset", d_ds, np.uint8)):
+            arr[f] = np.concatenate([arr[f], v.astype(dt)])
+        ws = np.concatenate([ws, d_k.astype(np.int32)])
+    else:
+        seq_all = np.concatenate([T.seq, N.seq])
+    dup_off = dict(zip(zip(d_ds.tolist(), d_row.tolist(), d_sc.tolist()), d_seq.tolist()))
+    dup_rows = list(zip(d_ds.tolist(), d_row.tolist()))
+    arr["seq_nt16"] = np.ascontiguousarray(seq_all.astype(np.uint8))
     arr["write_scope"] = ws
     arr["scope_incid_off"] = incid_off
     arr["incid_read"] = incid
@@ -139,14 +148,25 @@ def build_batch(plan: Plan, tables: Tuple[ReadTable, ReadTable], fasta: FastaRef
     if skip is not None and len(skip):
         # seen_read_alns (variation_classifier.py:196-207): later alignments of a read in a scope
         # are tallied for SNVs but not for indels
-        drop = np.zeros(len(incid), bool)
-        for sid, d, r in skip.tolist():
-            k = int(loc[sid]) if sid < len(plan.scopes) else -1
-            if k < 0:
-                continue
-            br = n_reads + dup_rows.index((d, r)) if (d, r, sid) in dup_off else int(bidx[d][r])
-            seg = incid[incid_off[k]:incid_off[k + 1]]
-            drop[incid_off[k] + np.nonzero(seg == br)[0]] = True
+        s_sc, s_ds, s_row = (np.asarray(skip[:, j], np.int64) for j in range(3))
+        ok = s_sc < len(plan.scopes)
+        s_sc, s_ds, s_row = s_sc[ok], s_ds[ok], s_row[ok]
+        s_k = loc[s_sc]
+        ok = s_k >= 0
+        s_sc, s_ds, s_row, s_k = s_sc[ok], s_ds[ok], s_row[ok], s_k[ok]
+        br = np.where(s_ds == 0, bidx[0][np.where(s_ds == 0, s_row, 0)] if T.n else -1,
+                      bidx[1][np.where(s_ds == 1, s_row, 0)] if N.n else -1)
+        if nd:    # a read copied into that scope: the copy
+            key3 = lambda a, b_, c: (c * 2 + a) * (max(T.n, N.n) + 1) + b_
+            dk3 = key3(d_ds, d_row, d_sc)
+            o3 = np.argsort(dk3)
+            sk3 = key3(s_ds, s_row, s_sc)
+            p3 = np.minimum(np.searchsorted(dk3[o3], sk3), nd - 1)
+            h3 = dk3[o3][p3] == sk3
+            br = np.where(h3, d_idx[o3][p3], br)
+        inc_k = np.repeat(np.arange(len(scopes), dtype=np.int64), counts)
+        M = n_reads + nd + 1
+        drop = np.isin(inc_k * M + incid, s_k * M + br)
         kept = np.diff(np.concatenate([[0], np.cumsum(~drop)])[incid_off])
         arr["indel_incid_off"] = np.concatenate([[0], np.cumsum(kept)]).astype(np.int64)
         arr["indel_incid_read"] = incid[~drop]

@@ -787,3 +787,136 @@ GANON_HOST_API int ganon_aux_sa_count(const uint8_t *aux, const int64_t *aux_off
   }
   return 0;
 }
+
+// ---------------------------------------------------------------------------------------------
+// Indel left-overs on formatted records: mask_or_anonymize_left_over_variants (AM:254-270, edits
+// stably sorted by VariantType value, offsets not shifted between edits) and
+// mask_or_modify_indel (AM:178-203) on the stored-orientation sequence and the *forward-oriented*
+// qualities, then get_anonymized_fastq_record (AM:205-243) again. The input record is
+// the unedited one the formatter wrote, so the stored sequence and qualities are recovered from it.
+GANON_HOST_API int ganon_fastq_edit(int64_t n, const char *recs, const int64_t *rec_off, const uint8_t *reverse,
+                                    const int32_t *times, const int64_t *edit_off, const int64_t *edits,
+                                    const char *alleles, const int64_t *allele_off, char *out, int64_t cap,
+                                    int64_t *out_len, int64_t *bad) {
+  if (n < 0 || (n > 0 && (!recs || !rec_off || !reverse || !times || !edit_off || !out_len || !bad)) ||
+      (n > 0 && edit_off[n] > edit_off[0] && (!edits || !allele_off)))
+    return -1;
+  *bad = -1;
+  uint8_t kComp[256] = {};
+  kComp['A'] = 'T', kComp['C'] = 'G', kComp['G'] = 'C', kComp['T'] = 'A', kComp['N'] = 'N';
+  std::string seq, s2;
+  std::vector<int64_t> qual, q2;
+  std::vector<int64_t> order;
+  int64_t w = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    const char *r = recs + rec_off[i];
+    const int64_t rl = rec_off[i + 1] - rec_off[i];
+    const char *e1 = (const char *)memchr(r, '\n', (size_t)rl);
+    if (!e1) return -1;
+    const int64_t hl = e1 - r + 1;                      // "@name/m\n"
+    const int64_t L = (rl - hl - 4) / 2;                // seq \n + \n qual \n
+    if (L < 0 || hl + 2 * L + 4 != rl) return -1;
+    const char *ps = r + hl, *pq = ps + L + 3;
+    const bool rev = reverse[i] != 0;
+    seq.assign(ps, (size_t)L);
+    qual.resize((size_t)L);
+    for (int64_t k = 0; k < L; ++k) qual[k] = (uint8_t)(pq[k] - 33);
+    if (rev) {                                          // printed = revcomp(stored), qualities stored order
+      std::reverse(seq.begin(), seq.end());
+      for (auto &c : seq) c = (char)kComp[(uint8_t)c];
+      std::reverse(qual.begin(), qual.end());           // forward-oriented qualities (Q1)
+    }
+    order.clear();
+    for (int64_t e = edit_off[i]; e < edit_off[i + 1]; ++e) order.push_back(e);
+    std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return edits[3 * a + 1] < edits[3 * b + 1]; });
+    for (int t = 0; t < times[i]; ++t) {
+      for (int64_t e : order) {
+        const int64_t type = edits[3 * e + 1], len = edits[3 * e + 2];
+        const int64_t S = (int64_t)seq.size(), Q = (int64_t)qual.size();
+        auto clampp = [](int64_t p, int64_t size) { return p < 0 ? std::max<int64_t>(0, p + size) : std::min(p, size); };
+        const int64_t irp = edits[3 * e];
+        if (type == 3) {                                // INS: seq[:irp] + seq[irp + len:]
+          const int64_t a = clampp(irp, S), b = clampp(irp + len, S);
+          s2.assign(seq, 0, (size_t)a);
+          s2.append(seq, (size_t)b, std::string::npos);
+          const int64_t qa = clampp(irp, Q), qb = clampp(irp + len, Q);
+          q2.assign(qual.begin(), qual.begin() + qa);
+          q2.insert(q2.end(), qual.begin() + qb, qual.end());
+          seq.swap(s2);
+          qual.swap(q2);
+        } else if (type == 2) {                         // DEL: ref allele and `len` average qualities at irp
+          if (Q == 0) {
+            *bad = i;
+            return 3;                                   // int(nan): ValueError
+          }
+          int64_t sum = 0;
+          for (int64_t v : qual) sum += v;
+          const int64_t avg = (int64_t)((double)sum / (double)Q);
+          const int64_t a = clampp(irp, S), qa = clampp(irp, Q);
+          seq.insert((size_t)a, alleles + allele_off[e], (size_t)(allele_off[e + 1] - allele_off[e]));
+          qual.insert(qual.begin() + qa, (size_t)std::max<int64_t>(0, len), avg);
+        }
+        if (seq.size() != qual.size()) {
+          *bad = i;
+          return 2;                                     // lengths diverge: ValueError
+        }
+      }
+    }
+    const int64_t L2 = (int64_t)seq.size();
+    for (int64_t v : qual)
+      if (v < 0 || v > 255) {                           // bytes(qual) refuses it
+        *bad = i;
+        return 2;
+      }
+    if (rev) {
+      for (auto c : seq)
+        if (!kComp[(uint8_t)c]) {
+          *bad = i;
+          return 1;                                     // reverse complement of a non-ACGTN base (Q7)
+        }
+      std::reverse(seq.begin(), seq.end());
+      for (auto &c : seq) c = (char)kComp[(uint8_t)c];
+      std::reverse(qual.begin(), qual.end());
+    }
+    const int64_t need = hl + 2 * L2 + 4;
+    if (w + need > cap) return -2;
+    char *o = out + w;
+    memcpy(o, r, (size_t)hl);
+    o += hl;
+    memcpy(o, seq.data(), (size_t)L2);
+    o += L2;
+    memcpy(o, "\n+\n", 3);
+    o += 3;
+    for (int64_t k = 0; k < L2; ++k) o[k] = (char)((qual[k] + 33) & 0xFF);
+    o += L2;
+    *o = '\n';
+    out_len[i] = need;
+    w += need;
+  }
+  return 0;
+}
+
+// Byte ranges of `src` back to back into `dst` (the output stage's splice of pre-formatted
+// records); threads for large copies. Returns the bytes written, -1 on bad arguments.
+GANON_HOST_API int64_t ganon_gather_ranges(const char *src, int64_t src_len, int64_t n, const int64_t *off,
+                                           const int64_t *len, char *dst, int64_t cap) {
+  if (n < 0 || (n > 0 && (!src || !off || !len || !dst))) return -1;
+  std::vector<int64_t> at((size_t)n + 1, 0);
+  for (int64_t i = 0; i < n; ++i) {
+    if (off[i] < 0 || len[i] < 0 || off[i] + len[i] > src_len) return -1;
+    at[i + 1] = at[i] + len[i];
+  }
+  if (at[n] > cap) return -1;
+  auto work = [&](int64_t a, int64_t b) {
+    for (int64_t i = a; i < b; ++i) memcpy(dst + at[i], src + off[i], (size_t)len[i]);
+  };
+  const int nt = (int)std::min<int64_t>(8, std::max<int64_t>(1, at[n] >> 23));   // one thread per 8 MiB
+  if (nt == 1) {
+    work(0, n);
+  } else {
+    std::vector<std::thread> pool;
+    for (int t = 0; t < nt; ++t) pool.emplace_back(work, n * t / nt, n * (t + 1) / nt);
+    for (auto &th : pool) th.join();
+  }
+  return at[n];
+}

@@ -10,7 +10,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
-from typing import Optional
+from typing import Optional, Tuple
 
 import numpy as np
 
@@ -220,7 +220,7 @@ EXPORTED_HOST_SYMBOLS = (
     "ganon_resolver_finish", "ganon_resolver_take_log", "ganon_objects_pack", "ganon_blob_size", "ganon_blob_data",
     "ganon_blob_free", "ganon_objects_create", "ganon_objects_free", "ganon_objects_add_job", "ganon_objects_add_plain",
     "ganon_objects_run", "ganon_objects_take", "ganon_objects_settle", "ganon_objects_last_error",
-    "ganon_objects_take_all", "ganon_aux_sa_count",
+    "ganon_objects_take_all", "ganon_aux_sa_count", "ganon_fastq_edit", "ganon_gather_ranges",
 )
 
 
@@ -432,6 +432,61 @@ def host_format_fastq(recs: dict) -> bytes:
     out = C.create_string_buffer(max(n_bytes, 1))
     w = host_lib().ganon_fastq_format(*a, out, n_bytes)
     return out.raw[:_fastq_result(w, lambda: "host formatter")]
+
+
+_new_bytes = C.pythonapi.PyBytes_FromStringAndSize
+_new_bytes.restype = C.py_object
+_new_bytes.argtypes = [C.c_void_p, C.c_ssize_t]
+
+
+def gather_ranges(src: bytes, off: np.ndarray, length: np.ndarray) -> bytes:
+    """libganon_host.so ganon_gather_ranges: src[off[i]:off[i] + length[i]] back to back."""
+    off = np.ascontiguousarray(off, np.int64)
+    length = np.ascontiguousarray(length, np.int64)
+    total = int(length.sum())
+    out = _new_bytes(None, total)      # a fresh, unshared bytes object the library fills in place
+    w = host_lib().ganon_gather_ranges(src, len(src), len(off), off.ctypes.data_as(_i64p),
+                                       length.ctypes.data_as(_i64p), out, total)
+    if w != total:
+        raise GanonError("gather_ranges: range outside the source")
+    return out
+
+
+class FastqEditError(GanonError):
+    """ganon_fastq_edit refused record ``index``: code 1 = reverse read with a base outside ACGTN
+    (SURVEY Q7), 2 = sequence/quality lengths diverge, 3 = DEL on a read without qualities."""
+
+    def __init__(self, code: int, index: int):
+        super().__init__(f"record {index}: left-over edit failed (code {code})")
+        self.code, self.index = code, index
+
+
+def fastq_edit(recs: bytes, rec_off: np.ndarray, reverse: np.ndarray, times: np.ndarray, edit_off: np.ndarray,
+               edits: np.ndarray, alleles: bytes, allele_off: np.ndarray, cap: int) -> Tuple[bytes, np.ndarray]:
+    """libganon_host.so ganon_fastq_edit: the indel left-overs applied to unedited records (host
+    side of row A4). Returns (edited records back to back, per-record lengths)."""
+    n = len(reverse)
+    rec_off = np.ascontiguousarray(rec_off, np.int64)
+    reverse = np.ascontiguousarray(reverse, np.uint8)
+    times = np.ascontiguousarray(times, np.int32)
+    edit_off = np.ascontiguousarray(edit_off, np.int64)
+    edits = np.ascontiguousarray(edits, np.int64).reshape(-1)
+    allele_off = np.ascontiguousarray(allele_off, np.int64)
+    if len(rec_off) != n + 1 or len(edit_off) != n + 1 or len(edits) != 3 * int(edit_off[-1]) or \
+            len(allele_off) != int(edit_off[-1]) + 1:
+        raise GanonError("fastq_edit: inconsistent array sizes")
+    out = C.create_string_buffer(max(int(cap), 1))
+    out_len = np.zeros(n, np.int64)
+    bad = C.c_int64(-1)
+    P = lambda a, t: a.ctypes.data_as(t)
+    rc = host_lib().ganon_fastq_edit(n, recs, P(rec_off, _i64p), P(reverse, _u8p), P(times, _i32p),
+                                     P(edit_off, _i64p), P(edits, _i64p), alleles, P(allele_off, _i64p),
+                                     C.cast(out, _p), int(cap), P(out_len, _i64p), C.byref(bad))
+    if rc > 0:
+        raise FastqEditError(rc, int(bad.value))
+    if rc < 0:
+        raise GanonError("fastq_edit: output too small" if rc == -2 else "fastq_edit: bad arguments")
+    return out.raw[:int(out_len.sum())], out_len
 
 
 class DeviceFastq:
@@ -1061,6 +1116,10 @@ def host_lib():
     lib.ganon_objects_take_all.argtypes = [_p, _i64p, _i64p, C.c_char_p, C.c_int64, C.POINTER(C.c_int64)]
     lib.ganon_objects_take_all.restype = C.c_int64
     lib.ganon_aux_sa_count.argtypes = [_u8p, _i64p, _i32p, C.c_int64, _i32p]
+    lib.ganon_gather_ranges.argtypes = [C.c_char_p, C.c_int64, C.c_int64, _i64p, _i64p, C.c_char_p, C.c_int64]
+    lib.ganon_gather_ranges.restype = C.c_int64
+    lib.ganon_fastq_edit.argtypes = [C.c_int64, C.c_char_p, _i64p, _u8p, _i32p, _i64p, _i64p, C.c_char_p, _i64p,
+                                     _p, C.c_int64, _i64p, _i64p]
     lib.ganon_objects_last_error.restype = C.c_char_p
     lib.ganon_resolver_take_log.argtypes = [_p, _i64p, C.c_int64]
     lib.ganon_resolver_take_log.restype = C.c_int64

@@ -85,8 +85,37 @@ class Job:
         self.res: MaskResult = anonymizer.anonymize(planner, self.plan, written=written)
         t3 = time.time()
         self.fmt = FastqFormatter(self.tables, self.res, anonymizer.format_fastq)
+        # every read once, as its masked copy (or unmasked): the records this job can write
+        self.fmt.preformat(*self._format_instances())
+        t4 = time.time()
         self.cx = self._complex_ingredients()
-        self.timing = {"decode_s": t1 - t0, "plan_s": t2 - t1, "mask_s": t3 - t2}
+        self.timing = {"decode_s": t1 - t0, "plan_s": t2 - t1, "mask_s": t3 - t2, "format_s": t4 - t3}
+
+    def _format_instances(self):
+        """Every read once as its masked copy (or unmasked), plus the unmasked records the events,
+        unwritten pairs and candidates name for reads masked elsewhere."""
+        ds, rw, sc = [], [], []
+        for d in (0, 1):
+            n = self.tables[d].n
+            ds.append(np.full(n, d, np.int64))
+            rw.append(np.arange(n, dtype=np.int64))
+            sc.append(self.masked_scope[d])
+        ev, rows = self.events, self.event_rows
+        m = ((ev[:, 0] == 1) | ((ev[:, 0] >= 3) & (ev[:, 0] <= 5))) & (ev[:, 5] < 0)
+        ds.append(ev[m, 4].astype(np.int64))
+        rw.append(rows[m].astype(np.int64))
+        L = self.left
+        for s_ in (0, 1):
+            h = (L[:, 1 + 4 * s_] == 1) & (L[:, 3 + 4 * s_] < 0) if len(L) else np.zeros(0, bool)
+            ds.append(L[h, 2 + 4 * s_].astype(np.int64))
+            rw.append(L[h, 4 + 4 * s_].astype(np.int64))
+        C = self.cand
+        cm = C[:, 1] >= 0 if len(C) else np.zeros(0, bool)
+        ds.append(C[cm, 1].astype(np.int64))
+        rw.append(C[cm, 2].astype(np.int64))
+        n_extra = sum(len(x) for x in ds[2:])
+        sc.append(np.full(n_extra, -1, np.int64))
+        return np.concatenate(ds), np.concatenate(rw), np.concatenate(sc)
 
     def _complex_incidences(self) -> np.ndarray:
         """(dataset, row, scope) of every alignment of a complex name's object in a scope, [n, 3]."""
@@ -105,6 +134,26 @@ class Job:
         self._cx_inc = c
         return c
 
+    def _masked_nibs(self, I: np.ndarray) -> np.ndarray:
+        """MaskResult.masked_nib of every (dataset, row, scope) row of ``I``, vectorised."""
+        T = self.tables
+        d0 = I[:, 0] == 0
+        r0, r1 = np.where(d0, I[:, 1], 0), np.where(d0, 0, I[:, 1])
+        off = np.where(d0, T[0].seq_off[r0] if T[0].n else 0, T[1].seq_off[r1] if T[1].n else 0).astype(np.int64)
+        nib = 2 * (np.where(d0, self.res.seq_base[0], self.res.seq_base[1]) + off)
+        dup = self.res.dup_off
+        if dup and len(I):
+            k = np.array(list(dup.keys()), np.int64).reshape(-1, 3)
+            v = np.array(list(dup.values()), np.int64)
+            M = max(T[0].n, T[1].n) + 1
+            dk = (k[:, 2] * 2 + k[:, 0]) * M + k[:, 1]
+            o = np.argsort(dk)
+            ik = (I[:, 2] * 2 + I[:, 0]) * M + I[:, 1]
+            p = np.minimum(np.searchsorted(dk[o], ik), len(dk) - 1)
+            hit = dk[o][p] == ik
+            nib[hit] = 2 * v[o][p[hit]]
+        return nib
+
     def _complex_ingredients(self):
         """What the object replay needs of this job's complex names: their records and, per
         (alignment, scope), the bases the device masked and the indel left-overs — the packed blob of
@@ -116,9 +165,7 @@ class Job:
         if os.environ.get("GANON_OBJECTS", "native") != "python":
             I = self._complex_incidences()
             T = self.tables
-            nib = np.zeros(len(I), np.int64)
-            for i, (d, a, sc) in enumerate(I.tolist()):
-                nib[i] = self.res.masked_nib(T, d, a, sc)
+            nib = self._masked_nibs(I)
             incs = set(map(tuple, I.tolist()))
             left = {k: v for k, v in self.res.leftovers.items() if v and k in incs}
             return native.objects_pack(T, O, self.obj_rows, I, nib, self.res.seq_out, left)
@@ -142,11 +189,7 @@ class Job:
                                       getattr(T[1], f)[r1] if T[1].n else 0).astype(np.int64)
             L = pick("l_seq")
             onib = 2 * pick("seq_off")
-            mnib = 2 * (np.where(d0, self.res.seq_base[0], self.res.seq_base[1]) + onib // 2)
-            for i, key in enumerate(map(tuple, I.tolist())):
-                o = self.res.dup_off.get(key) if self.res.dup_off else None
-                if o is not None:
-                    mnib[i] = 2 * o
+            mnib = self._masked_nibs(I)
             start = np.concatenate([[0], np.cumsum(L)[:-1]])
             k = np.arange(int(L.sum()), dtype=np.int64) - np.repeat(start, L)
             src = np.concatenate([T[0].seq, T[1].seq]) if T[1].n else T[0].seq
@@ -270,16 +313,20 @@ class Job:
             ok = np.array([sc[i] < 0 or self.masked_scope[ds[i]][rw[i]] == sc[i] for i in first.tolist()], bool)
             first = first[ok] if len(first) else first
             recs = self.format_records(ds[first], rw[first], sc[first])
+            edited = []
             for i, b in zip(first.tolist(), recs):
                 inst = (int(ds[i]), int(rw[i]), int(sc[i]))
                 carry[(self.job, inst[0], inst[2], inst[1], 0)] = b
                 info[(self.job, inst[0], inst[1])] = int(self.tables[inst[0]].flag[inst[1]])
-                if inst in self.res.leftovers:   # written later with its left-overs applied twice
-                    carry[(self.job, inst[0], inst[2], inst[1], 1)] = self.fmt.edited_bytes(inst, 1)
-                    # the record before its edits and the edits (objects.Replay, complex names)
-                    carry[(self.job, inst[0], inst[2], inst[1], 2)] = self.fmt._native(
-                        np.array([inst[0]]), np.array([inst[1]]), np.array([inst[2]]))
-                    info[(self.job, inst[0], inst[2], inst[1])] = list(self.res.leftovers[inst])
+                if inst in self.res.leftovers:
+                    edited.append(inst)
+            # written later with its left-overs applied twice; the record before its edits and the
+            # edits (objects.Replay, complex names)
+            self.fmt.prepare_edited(edited, [1] * len(edited))
+            for inst, b in zip(edited, self.fmt.unedited(edited)):
+                carry[(self.job, inst[0], inst[2], inst[1], 1)] = self.fmt.edited_bytes(inst, 1)
+                carry[(self.job, inst[0], inst[2], inst[1], 2)] = b
+                info[(self.job, inst[0], inst[2], inst[1])] = list(self.res.leftovers[inst])
         return {
             "job": self.job, "ops": ops, "op_rows": op_rows,
             "op_names": _names_ds(self.tables, op_ds, op_name_rows),
@@ -430,7 +477,7 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
     paths = [f"{tumor_out}.1.fastq", f"{tumor_out}.2.fastq", f"{normal_out}.1.fastq", f"{normal_out}.2.fastq"]
     if block_size is None:
         block_size = _writer.io_block_size(os.path.dirname(os.path.abspath(tumor_out)))
-    timing = {"decode_s": 0.0, "plan_s": 0.0, "mask_s": 0.0, "resolve_s": 0.0, "write_s": 0.0, "jobs": 0,
+    timing = {"decode_s": 0.0, "plan_s": 0.0, "mask_s": 0.0, "format_s": 0.0, "resolve_s": 0.0, "write_s": 0.0, "jobs": 0,
               "reads": 0}
     failure: Optional[BaseException] = None
     if rank == 0:
@@ -461,7 +508,7 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
                 try:
                     job = Job(jid, contigs[jid], readers, fasta, windows, anonymizer)
                     exp = job.exports()
-                    for k in ("decode_s", "plan_s", "mask_s"):
+                    for k in ("decode_s", "plan_s", "mask_s", "format_s"):
                         timing[k] += job.timing[k]
                     timing["jobs"] += 1
                     timing["reads"] += int(job.tables[0].n + job.tables[1].n)

@@ -7,7 +7,7 @@
   and the qualities printed in the BAM's stored order for every read (they are
   loaded forward-oriented and reversed once more on output). Bulk formatting runs on the
   GPU (``ganon_fastq_format_hip`` through the masking engine) or in libganon_host.so; the
-  rare indel-edited records are formatted here.
+  rare indel-edited records get their left-overs applied by ``native.fastq_edit``.
 * the statistics file of ``AnonymizedVariantsStatistics.write_statistics`` (SR:175-242).
 """
 from __future__ import annotations
@@ -19,26 +19,12 @@ import numpy as np
 
 from . import native
 from .anonymizer_methods import MaskResult
-from .indels import apply_leftovers
+from .variants import VariantType
 from .io.bam import ReadTable
 from .planner import Plan
 
-NT16 = "=ACMGRSVTWYHKDBN"
-_REVERSES = {ord("A"): ord("T"), ord("C"): ord("G"), ord("G"): ord("C"), ord("T"): ord("A"), ord("N"): ord("N")}
 OUTSIDE_WINDOWS = "outside_windows,-,-,-"
 STAT_HEADER = ["#SEQ", "#FIRST", "#LAST", "#SNV", "#DEL", "#INS", "#DUP", "#INV", "#CNV", "#TRA", "#SGL"]
-
-
-_NT16_BYTES = np.frombuffer(NT16.encode(), np.uint8)
-_COMP = bytes.maketrans(b"ACGTN", b"TGCAN")
-_PHRED = bytes((b + 33) & 0xFF for b in range(256))
-
-
-def _decode(buf: np.ndarray, nib0: int, n: int) -> bytearray:
-    i = nib0 + np.arange(n, dtype=np.int64)
-    b = buf[i >> 1]
-    c = np.where(i & 1, b & 0xF, b >> 4)
-    return bytearray(_NT16_BYTES[c].tobytes())
 
 
 class FastqFormatter:
@@ -57,6 +43,7 @@ class FastqFormatter:
         self._name_base = (0, len(tables[0].names_blob))
         self.edited: Dict[Tuple[int, int, int], bytes] = {}   # indel-edited records (write_fastqs)
         self.edited2: Dict[Tuple[int, int, int], bytes] = {}  # the same with the left-overs applied twice
+        self._pre = None     # (sorted instance keys, offsets, lengths, bytes) of preformat()
 
     @staticmethod
     def _key(ds, row, sc):
@@ -95,6 +82,15 @@ class FastqFormatter:
     def _native(self, ds, row, sc) -> bytes:
         if len(ds) == 0:
             return b""
+        pre = self._pre
+        if pre is not None:      # slices of the job's pre-formatted records
+            k = self._key(ds, row, sc)
+            pos = np.minimum(np.searchsorted(pre[0], k), len(pre[0]) - 1)
+            if np.array_equal(pre[0][pos], k):
+                return native.gather_ranges(pre[3], pre[1][pos], pre[2][pos])
+        return self._format(ds, row, sc)
+
+    def _format(self, ds, row, sc) -> bytes:
         try:
             return self.backend(self.records_arrays(ds, row, sc))
         except native.FastqBadRecord as e:
@@ -102,38 +98,97 @@ class FastqFormatter:
             raise TypeError(f"reverse read {self.tables[d].name(r)!r} has a base outside ACGTN: the "
                             "reference's reverse complement fails on it (SURVEY Q7)") from None
 
+    def preformat(self, ds, row, sc) -> None:
+        """Format the instances a job can write in ONE formatter call (the device round trip costs
+        more than the bytes); later record runs are sliced out of it. A reverse read with a base
+        outside ACGTN is left out (its error is raised only if it is written, as in the
+        reference); after a few such reads the job formats on demand."""
+        ds, row, sc = (np.asarray(x, np.int64) for x in (ds, row, sc))
+        key = self._key(ds, row, sc)
+        key, first = np.unique(key, return_index=True)
+        ds, row, sc = ds[first], row[first], sc[first]
+        for _ in range(4):
+            if len(ds) == 0:
+                return
+            try:
+                data = self.backend(self.records_arrays(ds, row, sc))
+            except native.FastqBadRecord as e:
+                keep = np.ones(len(ds), bool)
+                keep[e.index] = False
+                ds, row, sc, key = ds[keep], row[keep], sc[keep], key[keep]
+                continue
+            ln = self._plain_lengths(ds, row)
+            self._pre = (key, np.concatenate([[0], np.cumsum(ln)[:-1]]).astype(np.int64), ln, data)
+            return
+
     def edited_bytes(self, inst, reapply: int = 0) -> bytes:
         """Record of an instance with left-over edits, applied once or (reapply) twice (cached)."""
         cache = self.edited2 if reapply else self.edited
         b = cache.get(inst)
         if b is None:
-            b = self._edited(inst, self.res.leftovers[inst], 2 if reapply else 1)
-            cache[inst] = b
+            self.prepare_edited([inst], [reapply])
+            b = cache[inst]
         return b
 
-    def _edited(self, inst, edits, times: int = 1) -> bytes:
-        ds, row, sc = inst
-        t = self.tables[ds]
-        L = int(t.l_seq[row])
-        if sc >= 0:
-            nib0 = 2 * (self.res.seq_base[ds] + int(t.seq_off[row]))
-            seq = _decode(self.res.seq_out, nib0, L)
-        else:
-            seq = _decode(t.seq, 2 * int(t.seq_off[row]), L)
-        q = t.qual[int(t.qual_off[row]):int(t.qual_off[row]) + L].tobytes()
-        rev = bool(t.is_reverse[row])
-        qual_fwd = list(q[::-1] if rev else q)
-        for _ in range(times):   # mask_or_anonymize_left_over_variants, once more when re-flagged
-            seq, qual_fwd = apply_leftovers(seq, qual_fwd, edits)
-        seq = bytes(seq)
-        qual = bytes(qual_fwd)
-        if rev:
-            if seq.translate(None, b"ACGTN"):
-                raise TypeError(f"reverse read {t.name(row)!r} has a base outside ACGTN (SURVEY Q7)")
-            seq = seq[::-1].translate(_COMP)
-            qual = qual[::-1]
-        mate = 1 if t.flag[row] & 0x40 else 2
-        return f"@{t.name(row)}/{mate}\n".encode() + seq + b"\n+\n" + qual.translate(_PHRED) + b"\n"
+    def prepare_edited(self, insts: Sequence[Tuple[int, int, int]], reapply: Sequence[int]) -> None:
+        """Format the edited records of ``insts`` not cached yet in one batch: the unedited records
+        in one formatter call, the left-overs applied by ``native.fastq_edit`` (AM:178-203, 254-270)."""
+        todo, seen = [], set()
+        for inst, re_ in zip(insts, reapply):
+            k = (inst, int(bool(re_)))
+            if k not in seen and inst not in (self.edited2 if re_ else self.edited):
+                seen.add(k)
+                todo.append(k)
+        if not todo:
+            return
+        a = np.array([x[0] for x in todo], np.int64).reshape(-1, 3)
+        ds, row, sc = a[:, 0], a[:, 1], a[:, 2]
+        plain = self._native(ds, row, sc)
+        rec_off = np.concatenate([[0], np.cumsum(self._plain_lengths(ds, row))])
+        T, N = self.tables
+        rev = np.where(ds == 0, T.is_reverse[np.where(ds == 0, row, 0)] if T.n else 0,
+                       N.is_reverse[np.where(ds == 1, row, 0)] if N.n else 0).astype(np.uint8)
+        times = np.array([2 if r else 1 for _, r in todo], np.int32)
+        edits, alleles, edit_off, allele_off, extra = [], [], [0], [0], 0
+        left = self.res.leftovers
+        for (inst, r) in todo:
+            for irp, c in left[inst]:
+                al = c.ref_allele.encode() if c.variant_type is VariantType.DEL else b""
+                edits.append((irp, c.variant_type.value, c.length))
+                alleles.append(al)
+                allele_off.append(allele_off[-1] + len(al))
+                extra += (2 if r else 1) * (len(al) + max(c.length, 0))
+            edit_off.append(len(edits))
+        try:
+            data, lens = native.fastq_edit(plain, rec_off, rev, times, np.array(edit_off, np.int64),
+                                           np.array(edits, np.int64).reshape(-1, 3), b"".join(alleles),
+                                           np.array(allele_off, np.int64), len(plain) + extra)
+        except native.FastqEditError as e:
+            (d, r_, _), _r = todo[e.index]
+            if e.code == 1:
+                raise TypeError(f"reverse read {self.tables[d].name(r_)!r} has a base outside ACGTN (SURVEY Q7)") from None
+            if e.code == 3:
+                raise ValueError("cannot convert float NaN to integer") from None
+            raise ValueError("Length of the modified qualities does not match the length of the modified sequence") from None
+        off = np.concatenate([[0], np.cumsum(lens)]).tolist()
+        for j, (inst, r) in enumerate(todo):
+            (self.edited2 if r else self.edited)[inst] = data[off[j]:off[j + 1]]
+
+    def _plain_lengths(self, ds, row) -> np.ndarray:
+        T, N = self.tables
+        r0, r1 = np.where(ds == 0, row, 0), np.where(ds == 1, row, 0)
+        nl = np.where(ds == 0, T.name_len[r0] if T.n else 0, N.name_len[r1] if N.n else 0).astype(np.int64)
+        ls = np.where(ds == 0, T.l_seq[r0] if T.n else 0, N.l_seq[r1] if N.n else 0).astype(np.int64)
+        return nl + 8 + 2 * ls
+
+    def unedited(self, insts: Sequence[Tuple[int, int, int]]) -> List[bytes]:
+        """The records of ``insts`` before their left-over edits, one formatter call."""
+        if not insts:
+            return []
+        a = np.array(insts, np.int64).reshape(-1, 3)
+        data = self._native(a[:, 0], a[:, 1], a[:, 2])
+        off = np.concatenate([[0], np.cumsum(self._plain_lengths(a[:, 0], a[:, 1]))]).tolist()
+        return [data[off[j]:off[j + 1]] for j in range(len(a))]
 
     def format_arrays(self, ds: np.ndarray, row: np.ndarray, sc: np.ndarray, reapply=None) -> bytes:
         """Records in the given order: every unedited record in ONE formatter call, the rare
@@ -159,6 +214,7 @@ class FastqFormatter:
         ls = np.where(ds == 0, T.l_seq[np.where(ds == 0, row, 0)], N.l_seq[np.where(ds == 1, row, 0)])
         rl = np.where(keep, nl.astype(np.int64) + 8 + 2 * ls.astype(np.int64), 0)
         off = np.concatenate([[0], np.cumsum(rl)])      # byte offset in `data` of each record
+        self.prepare_edited([(int(ds[i]), int(row[i]), int(sc[i])) for i in ed.tolist()], reapply[ed].tolist())
         parts, prev = [], 0
         for i in ed.tolist():
             parts.append(data[off[prev]:off[i]])
@@ -186,7 +242,9 @@ class FastqFormatter:
             keys = self._key(ds, row, sc)
             lk = self._key(*zip(*left.keys()))
             re_ = np.zeros(len(ds), np.int64) if reapply is None else np.asarray(reapply, np.int64)
-            for i in np.nonzero(np.isin(keys, lk))[0].tolist():
+            ed = np.nonzero(np.isin(keys, lk))[0]
+            self.prepare_edited([(int(ds[i]), int(row[i]), int(sc[i])) for i in ed.tolist()], re_[ed].tolist())
+            for i in ed.tolist():
                 out[i] = len(self.edited_bytes((int(ds[i]), int(row[i]), int(sc[i])), int(re_[i])))
         return out
 

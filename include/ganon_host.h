@@ -95,6 +95,30 @@ GANON_HOST_API int64_t ganon_fastq_format(int64_t n, const uint8_t *const *seq_b
                                           const char *names, const int64_t *name_off, const int32_t *name_len,
                                           const uint8_t *mate, char *out, int64_t cap);
 
+/* Indel left-overs applied to formatted records (replaces the per-record host loop of
+ * AnonymizedRead.mask_or_anonymize_left_over_variants, anonymizer_methods.py:254-270, and
+ * mask_or_modify_indel, :178-203, then get_anonymized_fastq_record, :205-243). Record i is
+ * rec[rec_off[i] .. rec_off[i+1]) as ganon_fastq_format wrote it without edits; reverse[i] its
+ * BAM strand; its edits e in [edit_off[i], edit_off[i+1]) are (edits[3e] read position,
+ * edits[3e+1] VariantType value: 2 DEL, 3 INS, others only length-checked, edits[3e+2] length),
+ * a DEL inserting alleles[allele_off[e] .. allele_off[e+1]); stably sorted by type and applied
+ * times[i] times to the stored-orientation sequence and the forward-oriented
+ * qualities (Q1, Q6). Writes the edited records back to back into `out` (cap bytes), lengths in
+ * out_len. Returns 0; 1 = reverse read with a base outside ACGTN after its edits (Q7, the
+ * reference's KeyError), 2 = sequence and quality lengths diverge (ValueError), 3 = a DEL on a
+ * read without qualities (int(nan), ValueError), with *bad = the record; -1 bad arguments or
+ * malformed record, -2 `cap` too small. */
+GANON_HOST_API int ganon_fastq_edit(int64_t n, const char *recs, const int64_t *rec_off, const uint8_t *reverse,
+                                    const int32_t *times, const int64_t *edit_off, const int64_t *edits,
+                                    const char *alleles, const int64_t *allele_off, char *out, int64_t cap,
+                                    int64_t *out_len, int64_t *bad);
+
+/* Copy the byte ranges src[off[i] .. off[i] + len[i]) back to back into dst (cap bytes): the
+ * output stage slicing records out of a job's pre-formatted FASTQ blob. Returns the bytes
+ * written, or -1 for a range outside src_len or a too-small cap. */
+GANON_HOST_API int64_t ganon_gather_ranges(const char *src, int64_t src_len, int64_t n, const int64_t *off,
+                                           const int64_t *len, char *dst, int64_t cap);
+
 /* Upper-case a FASTA slice and pack it to nt16 nibbles (2 per byte, high first). Bytes
  * outside "=ACMGRSVTWYHKDBN" (after upper-casing) become N (15). `out` has (n+1)/2 bytes. */
 GANON_HOST_API void ganon_pack_nt16(const char *ascii, int64_t n, uint8_t *out);

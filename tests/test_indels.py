@@ -190,3 +190,87 @@ def test_hip_indel_long_reads_match_oracle(hip_built):
         db.free()
     finally:
         m.close()
+
+
+def _py_edit(seq: bytes, qual: bytes, rev: bool, edits, times: int):
+    """The per-record host loop the writer used before ganon_fastq_edit (indels.apply_leftovers,
+    AM:178-203 / 254-270): stored sequence, forward-oriented qualities (Q1), then the record."""
+    from genomeanonymizer_amd.indels import apply_leftovers
+    s, q = bytearray(seq), list(qual[::-1] if rev else qual)
+    for _ in range(times):
+        s, q = apply_leftovers(s, q, edits)
+    s, q = bytes(s), bytes(q)
+    if rev:
+        if s.translate(None, b"ACGTN"):
+            raise TypeError("Q7")
+        s, q = s[::-1].translate(bytes.maketrans(b"ACGTN", b"TGCAN")), q[::-1]
+    return s, q
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_native_fastq_edit_matches_host_loop(seed):
+    """ganon_fastq_edit (libganon_host.so) against the Python loop on random records and edits,
+    including out-of-range positions, DEL alleles of the wrong length, non-ACGTN alleles on
+    reverse reads (Q7), empty reads (int(nan)) and the doubled application (Q16)."""
+    from genomeanonymizer_amd import native
+    from genomeanonymizer_amd.indels import IndelCall
+    from genomeanonymizer_amd.variants import VariantType
+    rng = np.random.default_rng(seed)
+    comp = bytes.maketrans(b"ACGTN", b"TGCAN")
+    cases = []
+    for i in range(400):
+        rev = bool(rng.integers(2))
+        L = int(rng.integers(0, 40)) if rng.random() < 0.9 else 0
+        alpha = b"ACGTN" if rev else b"=ACMGRSVTWYHKDBN"
+        seq = bytes(rng.choice(list(alpha), L).tolist()) if L else b""
+        qual = bytes(rng.integers(0, 94, L).tolist())
+        edits = []
+        for _ in range(int(rng.integers(1, 4))):
+            t = VariantType.DEL if rng.random() < 0.5 else VariantType.INS
+            n = int(rng.integers(1, 6))
+            irp = int(rng.integers(0, L + 5))
+            if t is VariantType.DEL:
+                k = n if rng.random() < 0.9 else n + 1
+                ref = "".join(rng.choice(list("ACGT" if rng.random() < 0.95 else "ACGM"), k).tolist())
+            else:
+                ref = "A"
+            edits.append((irp, IndelCall(irp, irp + 1, t, n, "A", ref)))
+        times = int(rng.integers(1, 3))
+        try:
+            want = _py_edit(seq, qual, rev, edits, times)
+        except TypeError:
+            want = 1
+        except ValueError as e:
+            want = 3 if "NaN" in str(e) else 2
+        printed = (seq[::-1].translate(comp) if rev else seq)
+        name = f"r{i}".encode()
+        rec = b"@" + name + b"/1\n" + printed + b"\n+\n" + bytes((b + 33) & 0xFF for b in qual) + b"\n"
+        cases.append((rec, rev, edits, times, want))
+    # one batch per case keeps the first-error semantics per record; plus one batch of all good ones
+    good = [c for c in cases if not isinstance(c[4], int)]
+    for batch in [[c] for c in cases] + [good]:
+        recs = b"".join(c[0] for c in batch)
+        rec_off = np.concatenate([[0], np.cumsum([len(c[0]) for c in batch])])
+        ed, al, eo, ao, extra = [], [], [0], [0], 0
+        for c in batch:
+            for irp, x in c[2]:
+                a = x.ref_allele.encode() if x.variant_type is VariantType.DEL else b""
+                ed.append((irp, x.variant_type.value, x.length))
+                al.append(a)
+                ao.append(ao[-1] + len(a))
+                extra += c[3] * (len(a) + x.length)
+            eo.append(len(ed))
+        try:
+            data, lens = native.fastq_edit(recs, rec_off, np.array([c[1] for c in batch], np.uint8),
+                                           np.array([c[3] for c in batch], np.int32), np.array(eo, np.int64),
+                                           np.array(ed, np.int64), b"".join(al), np.array(ao, np.int64),
+                                           len(recs) + extra)
+        except native.FastqEditError as e:
+            assert len(batch) == 1 and batch[0][4] == e.code, (batch[0], e.code)
+            continue
+        off = np.concatenate([[0], np.cumsum(lens)])
+        for j, c in enumerate(batch):
+            assert not isinstance(c[4], int), c
+            s, q = c[4]
+            name = c[0][:c[0].index(b"\n") + 1]
+            assert data[off[j]:off[j + 1]] == name + s + b"\n+\n" + bytes((b + 33) & 0xFF for b in q) + b"\n"

@@ -35,13 +35,24 @@ def main():
     modes = sys.argv[3].split(",") if len(sys.argv) > 3 else ["stream", "whole"]
     for mode in modes:
         runs = []
-        for _ in range(2):    # the first run pays one-time costs (module loads, device init)
+        for it in range(2):    # the first run pays one-time costs (module loads, device init)
+            prof = None
+            if it == 1 and os.environ.get("E2E_PROFILE"):   # cProfile of the timed run -> E2E_PROFILE path
+                import cProfile
+                prof = cProfile.Profile()
+                prof.enable()
             t1 = time.time()
             tim = sr.anonymize_genome(windows, os.path.join(d, "tumor.bam"), os.path.join(d, "normal.bam"),
                                       os.path.join(d, "ref.fa"), anon, os.path.join(out, f"tumor_{mode}"),
                                       os.path.join(out, f"normal_{mode}"), True, 16, fasta=fasta,
                                       streaming=(mode == "stream"))
             tim["wall_s"] = time.time() - t1
+            if prof is not None:
+                import pstats
+                prof.disable()
+                with open(f"{os.environ['E2E_PROFILE']}_{mode}.txt", "w") as f:
+                    pstats.Stats(prof, stream=f).sort_stats("cumulative").print_stats(60)
+                    pstats.Stats(prof, stream=f).sort_stats("tottime").print_stats(40)
             runs.append(tim)
         tim = runs[-1]
         res[mode] = {"reads": tim["reads"], "stages_s": {k: round(v, 3) for k, v in tim.items() if k.endswith("_s")},

@@ -8,6 +8,7 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -36,7 +37,36 @@ struct ganon_ctx {
   std::vector<Rec> recs;
   std::vector<hipEvent_t> pool;
   std::vector<ganon_kernel_time> last_times;
+  // device blocks of released one-shot buffers (FASTQ formatter), reused by size on ctx->stream
+  std::multimap<size_t, void *> dcache;
+  size_t dcache_bytes = 0;
 };
+
+// A device block of at least `bytes` from the context's cache (at most 2x larger), else hipMalloc.
+inline hipError_t ctx_dmalloc(ganon_ctx *ctx, void **p, size_t bytes, size_t *got) {
+  auto it = ctx->dcache.lower_bound(bytes);
+  if (it != ctx->dcache.end() && it->first <= 2 * bytes + (1u << 16)) {
+    *p = it->second;
+    *got = it->first;
+    ctx->dcache_bytes -= it->first;
+    ctx->dcache.erase(it);
+    return hipSuccess;
+  }
+  *got = bytes;
+  return hipMalloc(p, bytes);
+}
+
+// Return a block to the cache (stream order makes its reuse safe: every user runs on ctx->stream),
+// or free it when the cache holds 1 GiB already.
+inline void ctx_dfree(ganon_ctx *ctx, void *p, size_t bytes) {
+  if (!p) return;
+  if (ctx && ctx->dcache_bytes + bytes <= (size_t(1) << 30)) {
+    ctx->dcache.emplace(bytes, p);
+    ctx->dcache_bytes += bytes;
+  } else {
+    hipFree(p);
+  }
+}
 
 // Device sequence buffers of an uploaded masking batch (defined in ganon_hip.hip): the input
 // (BAM nt16 layout) and the masked output, both `bytes` long.

@@ -969,7 +969,7 @@ __global__ void __launch_bounds__(kFqThreads) k_fq_dense(const FqBufs bufs, cons
 // ---- host side ---------------------------------------------------------------------------
 
 struct ganon_fastq {
-  std::vector<void *> allocs;
+  std::vector<std::pair<void *, size_t>> allocs;
   int64_t n = 0, nb = 0, n_tiles = 0;
   uint64_t total = 0;
   FqBufs bufs{};
@@ -989,14 +989,15 @@ template <typename T>
 int fq_alloc(ganon_ctx *ctx, ganon_fastq *f, T **p, size_t count) {
   *p = nullptr;
   const size_t bytes = std::max<size_t>(count, 1) * sizeof(T) + 128;
-  hipError_t e = hipMalloc(reinterpret_cast<void **>(p), bytes);
+  size_t got = 0;
+  hipError_t e = ctx_dmalloc(ctx, reinterpret_cast<void **>(p), bytes, &got);
   if (e != hipSuccess) return fail(ctx, GANON_E_NOMEM, "hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
-  f->allocs.push_back(*p);
+  f->allocs.emplace_back(*p, got);
   return GANON_OK;
 }
 
-void fq_release(ganon_fastq *f) {
-  for (void *p : f->allocs) hipFree(p);
+void fq_release(ganon_ctx *ctx, ganon_fastq *f) {
+  for (auto &a : f->allocs) ctx_dfree(ctx, a.first, a.second);
   f->allocs.clear();
 }
 
@@ -1028,7 +1029,7 @@ GANON_API int ganon_fastq_upload(ganon_ctx *ctx, const ganon_fastq_records *in, 
   ganon_fastq *f = new ganon_fastq();
   f->n = n;
   auto bail = [&](int rc) {
-    fq_release(f);
+    fq_release(ctx, f);
     delete f;
     return rc;
   };
@@ -1215,7 +1216,7 @@ GANON_API int64_t ganon_fastq_download(ganon_ctx *ctx, ganon_fastq *f, char *out
 GANON_API int ganon_fastq_free(ganon_ctx *ctx, ganon_fastq *f) {
   if (!f) return GANON_E_ARG;
   if (ctx) hipSetDevice(ctx->device);
-  fq_release(f);
+  fq_release(ctx, f);
   delete f;
   return GANON_OK;
 }

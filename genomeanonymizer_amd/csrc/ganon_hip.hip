@@ -1455,6 +1455,7 @@ GANON_API int ganon_ctx_destroy(ganon_ctx *ctx) {
     hipEventDestroy(r.e1);
   }
   for (auto e : ctx->pool) hipEventDestroy(e);
+  for (auto &b : ctx->dcache) hipFree(b.second);
   delete ctx;
   return GANON_OK;
 }

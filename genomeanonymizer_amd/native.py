@@ -29,6 +29,10 @@ class GanonError(RuntimeError):
 
 
 _p = C.c_void_p
+# a fresh, unshared bytes object of n bytes (contents undefined) for a library to fill in place
+_new_bytes = C.pythonapi.PyBytes_FromStringAndSize
+_new_bytes.restype = C.py_object
+_new_bytes.argtypes = [C.c_void_p, C.c_ssize_t]
 _i32p = C.POINTER(C.c_int32)
 _i64p = C.POINTER(C.c_int64)
 _u8p = C.POINTER(C.c_uint8)
@@ -346,9 +350,10 @@ class HipMasker:
         """One-shot ``ganon_fastq_format_hip`` (the host formatter's arguments)."""
         a = _fastq_args(recs)
         n_bytes = fastq_bytes(recs)
-        out = C.create_string_buffer(max(n_bytes, 1))
+        out = _new_bytes(None, n_bytes)    # filled in place: no zero-fill, no copy out
         w = self._lib.ganon_fastq_format_hip(self._h, *a, out, n_bytes)
-        return out.raw[:_fastq_result(w, lambda: self._lib.ganon_last_error(self._h).decode(errors="replace"))]
+        w = _fastq_result(w, lambda: self._lib.ganon_last_error(self._h).decode(errors="replace"))
+        return out if w == n_bytes else out[:w]
 
 
 class FastqBadRecord(GanonError):
@@ -429,14 +434,9 @@ def host_format_fastq(recs: dict) -> bytes:
     """libganon_host.so ganon_fastq_format over a ``fastq_records`` dict (same contract)."""
     a = _fastq_args(recs)
     n_bytes = fastq_bytes(recs)
-    out = C.create_string_buffer(max(n_bytes, 1))
-    w = host_lib().ganon_fastq_format(*a, out, n_bytes)
-    return out.raw[:_fastq_result(w, lambda: "host formatter")]
-
-
-_new_bytes = C.pythonapi.PyBytes_FromStringAndSize
-_new_bytes.restype = C.py_object
-_new_bytes.argtypes = [C.c_void_p, C.c_ssize_t]
+    out = _new_bytes(None, n_bytes)
+    w = _fastq_result(host_lib().ganon_fastq_format(*a, out, n_bytes), lambda: "host formatter")
+    return out if w == n_bytes else out[:w]
 
 
 def gather_ranges(src: bytes, off: np.ndarray, length: np.ndarray) -> bytes:

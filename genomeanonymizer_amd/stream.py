@@ -29,6 +29,7 @@ from __future__ import annotations
 
 import os
 import time
+from concurrent.futures import ThreadPoolExecutor
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -59,15 +60,27 @@ def _names_ds(tables, ds: np.ndarray, rows: np.ndarray) -> List[bytes]:
     return out
 
 
+def decode_contig(readers, contig: str):
+    """The contig's records of both BAMs (io.bam.BamReader.contig; the inflate runs in native
+    threads without the GIL, so a prefetch thread overlaps it with the previous job)."""
+    return tuple(r.contig(r.tid_of(contig)) for r in readers)
+
+
 class Job:
     """Phase 1 of one contig: decode, plan, mask; then, once resolved, its output bytes."""
 
     def __init__(self, job: int, contig: str, readers, fasta: FastaRef, windows: Sequence[Window],
-                 anonymizer: CompleteGermlineAnonymizer):
+                 anonymizer: CompleteGermlineAnonymizer, tables=None):
+        """``tables``: the job's decoded records when the caller prefetched them (a
+        ``concurrent.futures.Future`` or the tuple); decode_s is then the time spent waiting."""
         self.job = job
         self.contig = contig
         t0 = time.time()
-        self.tables = tuple(r.contig(r.tid_of(contig)) for r in readers)
+        if tables is None:
+            tables = decode_contig(readers, contig)
+        elif hasattr(tables, "result"):
+            tables = tables.result()
+        self.tables = tables
         t1 = time.time()
         planner = ContigPlanner(self.tables[0], self.tables[1], fasta, windows, job)
         self.plan: Plan = planner.run()
@@ -498,6 +511,10 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
     stats_rows: List[Tuple[int, Dict[str, List[int]]]] = []
     totals = np.zeros(8, np.int64)
     n_rounds = (len(contigs) + world - 1) // world
+    # the next job's decode runs in a thread while this job plans, masks and writes (bounded: one
+    # job ahead); GANON_PREFETCH=0 decodes in line
+    pool = ThreadPoolExecutor(1) if os.environ.get("GANON_PREFETCH", "1") != "0" else None
+    ahead = None
     try:
         for rnd in range(n_rounds):
             jid = rnd * world + rank
@@ -506,7 +523,12 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
             err = None
             if failure is None and jid < len(contigs):
                 try:
-                    job = Job(jid, contigs[jid], readers, fasta, windows, anonymizer)
+                    tables = None
+                    if pool is not None:
+                        tables = ahead if ahead is not None else pool.submit(decode_contig, readers, contigs[jid])
+                        ahead = (pool.submit(decode_contig, readers, contigs[jid + world])
+                                 if jid + world < len(contigs) else None)
+                    job = Job(jid, contigs[jid], readers, fasta, windows, anonymizer, tables)
                     exp = job.exports()
                     for k in ("decode_s", "plan_s", "mask_s", "format_s"):
                         timing[k] += job.timing[k]
@@ -607,6 +629,8 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
                         merged[key] = list(counts)
             write_statistics(normal_stats_path or f"{normal_bam}.statistics.txt", merged)
     finally:
+        if pool is not None:      # a prefetch still running (a failed job) ends before its reader closes
+            pool.shutdown(wait=True)
         for fd in fds:
             os.close(fd)
         for r in readers:

@@ -61,31 +61,45 @@ def _names_ds(tables, ds: np.ndarray, rows: np.ndarray) -> List[bytes]:
 
 
 def decode_contig(readers, contig: str):
-    """The contig's records of both BAMs (io.bam.BamReader.contig; the inflate runs in native
-    threads without the GIL, so a prefetch thread overlaps it with the previous job)."""
+    """The contig's records of both BAMs (io.bam.BamReader.contig)."""
     return tuple(r.contig(r.tid_of(contig)) for r in readers)
+
+
+def prepare_job(job: int, contig: str, readers, fasta: FastaRef, windows: Sequence[Window]):
+    """Decode and plan one job: what the prefetch thread runs for the next job while the current one
+    masks and writes (the BGZF inflate and ganon_plan_run are native and run without the GIL).
+    Returns (tables, planner, plan, decode seconds, plan seconds)."""
+    t0 = time.time()
+    tables = decode_contig(readers, contig)
+    t1 = time.time()
+    planner = ContigPlanner(tables[0], tables[1], fasta, windows, job)
+    plan = planner.run()
+    return tables, planner, plan, t1 - t0, time.time() - t1
 
 
 class Job:
     """Phase 1 of one contig: decode, plan, mask; then, once resolved, its output bytes."""
 
     def __init__(self, job: int, contig: str, readers, fasta: FastaRef, windows: Sequence[Window],
-                 anonymizer: CompleteGermlineAnonymizer, tables=None):
-        """``tables``: the job's decoded records when the caller prefetched them (a
-        ``concurrent.futures.Future`` or the tuple); decode_s is then the time spent waiting."""
+                 anonymizer: CompleteGermlineAnonymizer, prepared=None):
+        """``prepared``: ``prepare_job``'s result when the caller prefetched it (a
+        ``concurrent.futures.Future``); decode_s + plan_s are then the time spent waiting for it and
+        prefetch_s the decode + plan time the thread spent."""
         self.job = job
         self.contig = contig
         t0 = time.time()
-        if tables is None:
-            tables = decode_contig(readers, contig)
-        elif hasattr(tables, "result"):
-            tables = tables.result()
+        if prepared is None:
+            tables, planner, plan, _, t_plan = prepare_job(job, contig, readers, fasta, windows)
+            t1 = time.time()
+            t_dec, t_pl, hidden = t1 - t0 - t_plan, t_plan, 0.0
+        else:
+            tables, planner, plan, a, b = prepared.result()
+            t1 = time.time()
+            t_dec, t_pl, hidden = t1 - t0, 0.0, a + b
         self.tables = tables
-        t1 = time.time()
-        planner = ContigPlanner(self.tables[0], self.tables[1], fasta, windows, job)
-        self.plan: Plan = planner.run()
+        self.plan: Plan = plan
         ex = planner.contig_exports
-        t2 = time.time()
+        t2 = t1
         ev, rows = self.plan.io_arrays()
         self.events, self.event_rows = ev, rows
         self.ph = np.nonzero(ev[:, 0] >= 3)[0]
@@ -102,7 +116,8 @@ class Job:
         self.fmt.preformat(*self._format_instances())
         t4 = time.time()
         self.cx = self._complex_ingredients()
-        self.timing = {"decode_s": t1 - t0, "plan_s": t2 - t1, "mask_s": t3 - t2, "format_s": t4 - t3}
+        self.timing = {"decode_s": t_dec, "plan_s": t_pl, "mask_s": t3 - t2, "format_s": t4 - t3,
+                       "prefetch_s": hidden}
 
     def _format_instances(self):
         """Every read once as its masked copy (or unmasked), plus the unmasked records the events,
@@ -490,7 +505,7 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
     paths = [f"{tumor_out}.1.fastq", f"{tumor_out}.2.fastq", f"{normal_out}.1.fastq", f"{normal_out}.2.fastq"]
     if block_size is None:
         block_size = _writer.io_block_size(os.path.dirname(os.path.abspath(tumor_out)))
-    timing = {"decode_s": 0.0, "plan_s": 0.0, "mask_s": 0.0, "format_s": 0.0, "resolve_s": 0.0, "write_s": 0.0, "jobs": 0,
+    timing = {"decode_s": 0.0, "plan_s": 0.0, "mask_s": 0.0, "format_s": 0.0, "prefetch_s": 0.0, "resolve_s": 0.0, "write_s": 0.0, "jobs": 0,
               "reads": 0}
     failure: Optional[BaseException] = None
     if rank == 0:
@@ -523,14 +538,16 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
             err = None
             if failure is None and jid < len(contigs):
                 try:
-                    tables = None
+                    pre = None
                     if pool is not None:
-                        tables = ahead if ahead is not None else pool.submit(decode_contig, readers, contigs[jid])
-                        ahead = (pool.submit(decode_contig, readers, contigs[jid + world])
-                                 if jid + world < len(contigs) else None)
-                    job = Job(jid, contigs[jid], readers, fasta, windows, anonymizer, tables)
+                        pre = ahead if ahead is not None else pool.submit(prepare_job, jid, contigs[jid], readers,
+                                                                           fasta, windows)
+                        nj = jid + world
+                        ahead = (pool.submit(prepare_job, nj, contigs[nj], readers, fasta, windows)
+                                 if nj < len(contigs) else None)
+                    job = Job(jid, contigs[jid], readers, fasta, windows, anonymizer, pre)
                     exp = job.exports()
-                    for k in ("decode_s", "plan_s", "mask_s", "format_s"):
+                    for k in ("decode_s", "plan_s", "mask_s", "format_s", "prefetch_s"):
                         timing[k] += job.timing[k]
                     timing["jobs"] += 1
                     timing["reads"] += int(job.tables[0].n + job.tables[1].n)

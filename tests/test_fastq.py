@@ -170,3 +170,51 @@ def test_hip_formatter_config2_size_properties(masker):
     exp = native.host_format_fastq(recs)
     assert len(got) == native.fastq_bytes(recs)
     assert got == exp
+
+
+# ---- CPU: the output stage's per-job pre-formatting (writer.FastqFormatter.preformat) ----------
+
+def _toy_tables():
+    """Two small read tables (tumor 5 reads, normal 3) with one reverse tumor read holding an IUPAC
+    base: formatting it is the reference's KeyError (Q7) — but only if it is written."""
+    from types import SimpleNamespace
+    rng = np.random.default_rng(7)
+    tabs = []
+    for ds, n in ((0, 5), (1, 3)):
+        L = rng.integers(5, 40, n).astype(np.int32)
+        seq_off = np.concatenate([[0], np.cumsum((L + 1) // 2)[:-1]]).astype(np.int64)
+        seq = rng.choice(np.array([0x12, 0x48, 0x81, 0x24, 0xF1], np.uint8), int(((L + 1) // 2).sum()))
+        qual_off = np.concatenate([[0], np.cumsum(L)[:-1]]).astype(np.int64)
+        qual = rng.integers(2, 41, int(L.sum()), dtype=np.uint8)
+        names = [f"r{ds}_{i}".encode() for i in range(n)]
+        blob = np.frombuffer(b"".join(names), np.uint8)
+        name_len = np.array([len(x) for x in names], np.int32)
+        rev = (np.arange(n) % 2).astype(np.uint8)
+        if ds == 0:
+            seq[seq_off[1]] = 0x31            # read 1 (reverse): an 'M' first base
+        t = SimpleNamespace(n=n, seq=seq, qual=qual, names_blob=blob, seq_off=seq_off, l_seq=L, qual_off=qual_off,
+                            name_len=name_len, name_off=np.concatenate([[0], np.cumsum(name_len)[:-1]]).astype(np.int64),
+                            flag=np.where(np.arange(n) % 2, 0x80, 0x40).astype(np.int64), is_reverse=rev)
+        t.name = (lambda t_: (lambda r: bytes(t_.names_blob[t_.name_off[r]:t_.name_off[r] + t_.name_len[r]]).decode()))(t)
+        tabs.append(t)
+    res = SimpleNamespace(seq_out=np.zeros(1, np.uint8), seq_base=(0, 0), leftovers={})
+    return tuple(tabs), res
+
+
+def test_preformat_slices_match_direct_formatting_and_defer_q7():
+    from genomeanonymizer_amd.writer import FastqFormatter
+    tables, res = _toy_tables()
+    ds = np.array([0] * 5 + [1] * 3, np.int64)
+    row = np.array([0, 1, 2, 3, 4, 0, 1, 2], np.int64)
+    sc = np.full(8, -1, np.int64)
+    direct = FastqFormatter(tables, res)
+    pre = FastqFormatter(tables, res)
+    pre.preformat(ds, row, sc)
+    assert pre._pre is not None and len(pre._pre[0]) == 7        # the Q7 read left out, not raised
+    good = np.array([0, 2, 3, 4, 5, 6, 7])
+    order = good[::-1]                                            # any order, any subset
+    assert pre._native(ds[order], row[order], sc[order]) == direct._native(ds[order], row[order], sc[order])
+    with pytest.raises(TypeError, match="r0_1"):                  # raised when it is written
+        pre._native(ds[:3], row[:3], sc[:3])
+    assert pre.unedited([(1, 2, -1), (0, 4, -1)]) == [direct._native(np.array([1]), np.array([2]), np.array([-1])),
+                                                      direct._native(np.array([0]), np.array([4]), np.array([-1]))]

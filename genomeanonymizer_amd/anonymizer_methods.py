@@ -250,12 +250,13 @@ class CompleteGermlineAnonymizer:
         fmt = getattr(self.engine, "format_fastq", None)
         return fmt(recs) if fmt is not None else native.host_format_fastq(recs)
 
-    def anonymize(self, planner: SamplePlanner, plan: Plan, scope_ids=None, written=None) -> MaskResult:
-        """Mask all scopes of ``plan`` (or the contig shard ``scope_ids``) in one device batch.
-        Per-scope counts come back indexed by plan scope id (zero outside the shard)."""
+    def anonymize(self, planner: SamplePlanner, plan: Plan, scope_ids=None, written=None, batch=None) -> MaskResult:
+        """Mask all scopes of ``plan`` (or the contig shard ``scope_ids``) in one device batch
+        (``batch``: build_batch's result when the caller built it already). Per-scope counts come
+        back indexed by plan scope id (zero outside the shard)."""
         tables = planner.tables
         fasta = planner.fasta
-        arrays, meta = build_batch(plan, tables, fasta, scope_ids, written)
+        arrays, meta = batch if batch is not None else build_batch(plan, tables, fasta, scope_ids, written)
         out, b_calls, b_bases, totals, irecs = self.engine.mask(arrays, indels=True)
         calls = np.zeros(len(plan.scopes), np.int32)
         bases = np.zeros(len(plan.scopes), np.int32)

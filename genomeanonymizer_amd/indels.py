@@ -21,6 +21,9 @@ from .variants import VariantType
 NT16 = "=ACMGRSVTWYHKDBN"
 
 
+_NT16_BYTES = np.frombuffer(NT16.encode(), np.uint8)
+
+
 def query_sequence(t: ReadTable, row: int) -> str:
     L = int(t.l_seq[row])
     o = int(t.seq_off[row])
@@ -28,7 +31,7 @@ def query_sequence(t: ReadTable, row: int) -> str:
     nib = np.empty(2 * len(b), np.uint8)
     nib[0::2] = b >> 4
     nib[1::2] = b & 0xF
-    return "".join(NT16[c] for c in nib[:L])
+    return _NT16_BYTES[nib[:L]].tobytes().decode()
 
 
 @dataclasses.dataclass

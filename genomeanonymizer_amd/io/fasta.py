@@ -62,6 +62,6 @@ class FastaRef:
                 offs[n] = nib
                 parts.append(buf)
                 nib += 2 * len(buf)
+            self._nib_off = offs      # before _packed: another thread may test _packed meanwhile
             self._packed = np.concatenate(parts) if parts else np.zeros(0, np.uint8)
-            self._nib_off = offs
         return self._packed, self._nib_off

@@ -36,7 +36,7 @@ import numpy as np
 
 from . import native
 from . import objects
-from .anonymizer_methods import CompleteGermlineAnonymizer, MaskResult
+from .anonymizer_methods import CompleteGermlineAnonymizer, MaskResult, build_batch
 from .io.bam import BamReader, ReadTable
 from .io.fasta import FastaRef
 from .planner import ContigPlanner, Plan, Window, UnsupportedInput
@@ -65,41 +65,22 @@ def decode_contig(readers, contig: str):
     return tuple(r.contig(r.tid_of(contig)) for r in readers)
 
 
-def prepare_job(job: int, contig: str, readers, fasta: FastaRef, windows: Sequence[Window]):
-    """Decode and plan one job: what the prefetch thread runs for the next job while the current one
-    masks and writes (the BGZF inflate and ganon_plan_run are native and run without the GIL).
-    Returns (tables, planner, plan, decode seconds, plan seconds)."""
-    t0 = time.time()
-    tables = decode_contig(readers, contig)
-    t1 = time.time()
-    planner = ContigPlanner(tables[0], tables[1], fasta, windows, job)
-    plan = planner.run()
-    return tables, planner, plan, t1 - t0, time.time() - t1
+class JobPrep:
+    """The host stage of one contig before the device: decode (io.bam), plan (ganon_plan_run), the
+    masked instance of every read and the device batch (anonymizer_methods.build_batch). The
+    streamed loop runs it for the next contig in a prefetch thread while the current one masks,
+    formats and writes (the BGZF inflate and the planner are native and drop the GIL)."""
 
-
-class Job:
-    """Phase 1 of one contig: decode, plan, mask; then, once resolved, its output bytes."""
-
-    def __init__(self, job: int, contig: str, readers, fasta: FastaRef, windows: Sequence[Window],
-                 anonymizer: CompleteGermlineAnonymizer, prepared=None):
-        """``prepared``: ``prepare_job``'s result when the caller prefetched it (a
-        ``concurrent.futures.Future``); decode_s + plan_s are then the time spent waiting for it and
-        prefetch_s the decode + plan time the thread spent."""
+    def __init__(self, job: int, contig: str, readers, fasta: FastaRef, windows: Sequence[Window]):
         self.job = job
         self.contig = contig
         t0 = time.time()
-        if prepared is None:
-            tables, planner, plan, _, t_plan = prepare_job(job, contig, readers, fasta, windows)
-            t1 = time.time()
-            t_dec, t_pl, hidden = t1 - t0 - t_plan, t_plan, 0.0
-        else:
-            tables, planner, plan, a, b = prepared.result()
-            t1 = time.time()
-            t_dec, t_pl, hidden = t1 - t0, 0.0, a + b
-        self.tables = tables
-        self.plan: Plan = plan
-        ex = planner.contig_exports
-        t2 = t1
+        self.tables = decode_contig(readers, contig)
+        t1 = time.time()
+        self.planner = ContigPlanner(self.tables[0], self.tables[1], fasta, windows, job)
+        self.plan: Plan = self.planner.run()
+        ex = self.planner.contig_exports
+        t2 = time.time()
         ev, rows = self.plan.io_arrays()
         self.events, self.event_rows = ev, rows
         self.ph = np.nonzero(ev[:, 0] >= 3)[0]
@@ -108,15 +89,90 @@ class Job:
         self.cand = ex["cand"]
         self.objs, self.obj_rows = ex["objs"], ex["obj_rows"]
         self.masked_scope = [np.full(t.n, -1, np.int64) for t in self.tables]
-        written = self._mask_instances()
-        self.res: MaskResult = anonymizer.anonymize(planner, self.plan, written=written)
+        self.written = self._mask_instances()
+        self.batch = build_batch(self.plan, self.tables, fasta, None, self.written)
+        self.prep_timing = (t1 - t0, t2 - t1, time.time() - t2)
+
+    # -- which masked copy of each read the device produces --------------------------------------
+    def _mask_instances(self):
+        """One masked scope per read: its local write, else its first placeholder, else its
+        unwritten-pair entry (the instance the sample-wide state can store first)."""
+        ev, rows = self.events, self.event_rows
+        parts = []
+        w = ev[:, 0] == 1
+        parts.append((ev[w, 4].astype(np.int64), rows[w], ev[w, 5].astype(np.int64)))
+        p = self.plain_ph
+        parts.append((ev[p, 4].astype(np.int64), rows[p], ev[p, 5].astype(np.int64)))
+        L = self.left
+        for s in (0, 1):
+            h = L[:, 1 + 4 * s] == 1 if len(L) else np.zeros(0, bool)
+            parts.append((L[h, 2 + 4 * s], L[h, 4 + 4 * s], L[h, 3 + 4 * s]))
+        ds = np.concatenate([x[0] for x in parts]).astype(np.int64)
+        rw = np.concatenate([x[1] for x in parts]).astype(np.int64)
+        sc = np.concatenate([x[2] for x in parts]).astype(np.int64)
+        m = sc >= 0
+        ds, rw, sc = ds[m], rw[m], sc[m]
+        for d in (0, 1):
+            sel = ds == d
+            r, s = rw[sel][::-1], sc[sel][::-1]        # reversed: the first occurrence wins
+            self.masked_scope[d][r] = s
+        keep = np.zeros(len(ds), bool)
+        if len(ds):
+            key = ds * (1 << 40) + rw
+            _, first = np.unique(key, return_index=True)
+            keep[first] = True
+        ds, rw, sc = ds[keep], rw[keep], sc[keep]
+        c = self._complex_incidences()      # every (alignment, scope) of a complex name: one copy each
+        if len(c):
+            ds, rw, sc = np.concatenate([ds, c[:, 0]]), np.concatenate([rw, c[:, 1]]), np.concatenate([sc, c[:, 2]])
+        return ds, rw, sc
+
+    def _complex_incidences(self) -> np.ndarray:
+        """(dataset, row, scope) of every alignment of a complex name's object in a scope, [n, 3]."""
+        c = getattr(self, "_cx_inc", None)
+        if c is not None:
+            return c
+        O = self.objs
+        if not len(O):
+            c = np.zeros((0, 3), np.int64)
+        else:
+            O = O[O[:, 0] >= 0]
+            n = O[:, 6]
+            idx = np.repeat(O[:, 5] - np.concatenate([[0], np.cumsum(n)[:-1]]), n) + np.arange(int(n.sum()))
+            trip = np.stack([np.repeat(O[:, 1], n), self.obj_rows[idx], np.repeat(O[:, 0], n)], axis=1)
+            c = np.unique(trip, axis=0) if len(trip) else np.zeros((0, 3), np.int64)
+        self._cx_inc = c
+        return c
+
+
+class Job(JobPrep):
+    """One contig: its JobPrep stage, then mask + format on the device; once resolved, its output
+    bytes."""
+
+    def __init__(self, job: int, contig: str, readers, fasta: FastaRef, windows: Sequence[Window],
+                 anonymizer: CompleteGermlineAnonymizer, prepared=None):
+        """``prepared``: a ``concurrent.futures.Future`` of this job's JobPrep when the caller
+        prefetched it; decode_s is then the time spent waiting for it and prefetch_s the time the
+        thread spent (decode + plan + batch)."""
+        t0 = time.time()
+        if prepared is None:
+            JobPrep.__init__(self, job, contig, readers, fasta, windows)
+            t_dec, t_pl, t_b = self.prep_timing
+            hidden = 0.0
+        else:
+            self.__dict__.update(prepared.result().__dict__)
+            t_dec, t_pl, t_b = time.time() - t0, 0.0, 0.0
+            hidden = sum(self.prep_timing)
+        t2 = time.time()
+        self.res: MaskResult = anonymizer.anonymize(self.planner, self.plan, written=self.written, batch=self.batch)
+        self.batch = None
         t3 = time.time()
         self.fmt = FastqFormatter(self.tables, self.res, anonymizer.format_fastq)
         # every read once, as its masked copy (or unmasked): the records this job can write
         self.fmt.preformat(*self._format_instances())
         t4 = time.time()
         self.cx = self._complex_ingredients()
-        self.timing = {"decode_s": t_dec, "plan_s": t_pl, "mask_s": t3 - t2, "format_s": t4 - t3,
+        self.timing = {"decode_s": t_dec, "plan_s": t_pl, "mask_s": t3 - t2 + t_b, "format_s": t4 - t3,
                        "prefetch_s": hidden}
 
     def _format_instances(self):
@@ -144,23 +200,6 @@ class Job:
         n_extra = sum(len(x) for x in ds[2:])
         sc.append(np.full(n_extra, -1, np.int64))
         return np.concatenate(ds), np.concatenate(rw), np.concatenate(sc)
-
-    def _complex_incidences(self) -> np.ndarray:
-        """(dataset, row, scope) of every alignment of a complex name's object in a scope, [n, 3]."""
-        c = getattr(self, "_cx_inc", None)
-        if c is not None:
-            return c
-        O = self.objs
-        if not len(O):
-            c = np.zeros((0, 3), np.int64)
-        else:
-            O = O[O[:, 0] >= 0]
-            n = O[:, 6]
-            idx = np.repeat(O[:, 5] - np.concatenate([[0], np.cumsum(n)[:-1]]), n) + np.arange(int(n.sum()))
-            trip = np.stack([np.repeat(O[:, 1], n), self.obj_rows[idx], np.repeat(O[:, 0], n)], axis=1)
-            c = np.unique(trip, axis=0) if len(trip) else np.zeros((0, 3), np.int64)
-        self._cx_inc = c
-        return c
 
     def _masked_nibs(self, I: np.ndarray) -> np.ndarray:
         """MaskResult.masked_nib of every (dataset, row, scope) row of ``I``, vectorised."""
@@ -245,40 +284,6 @@ class Job:
                         indels[k] = list(e)
         return {"objs": O, "obj_rows": self.obj_rows, "rec": rec, "masks": masks, "indels": indels}
 
-    # -- which masked copy of each read the device produces --------------------------------------
-    def _mask_instances(self):
-        """One masked scope per read: its local write, else its first placeholder, else its
-        unwritten-pair entry (the instance the sample-wide state can store first)."""
-        ev, rows = self.events, self.event_rows
-        parts = []
-        w = ev[:, 0] == 1
-        parts.append((ev[w, 4].astype(np.int64), rows[w], ev[w, 5].astype(np.int64)))
-        p = self.plain_ph
-        parts.append((ev[p, 4].astype(np.int64), rows[p], ev[p, 5].astype(np.int64)))
-        L = self.left
-        for s in (0, 1):
-            h = L[:, 1 + 4 * s] == 1 if len(L) else np.zeros(0, bool)
-            parts.append((L[h, 2 + 4 * s], L[h, 4 + 4 * s], L[h, 3 + 4 * s]))
-        ds = np.concatenate([x[0] for x in parts]).astype(np.int64)
-        rw = np.concatenate([x[1] for x in parts]).astype(np.int64)
-        sc = np.concatenate([x[2] for x in parts]).astype(np.int64)
-        m = sc >= 0
-        ds, rw, sc = ds[m], rw[m], sc[m]
-        for d in (0, 1):
-            sel = ds == d
-            r, s = rw[sel][::-1], sc[sel][::-1]        # reversed: the first occurrence wins
-            self.masked_scope[d][r] = s
-        keep = np.zeros(len(ds), bool)
-        if len(ds):
-            key = ds * (1 << 40) + rw
-            _, first = np.unique(key, return_index=True)
-            keep[first] = True
-        ds, rw, sc = ds[keep], rw[keep], sc[keep]
-        c = self._complex_incidences()      # every (alignment, scope) of a complex name: one copy each
-        if len(c):
-            ds, rw, sc = np.concatenate([ds, c[:, 0]]), np.concatenate([rw, c[:, 1]]), np.concatenate([sc, c[:, 2]])
-        return ds, rw, sc
-
     def check_instance(self, ds: int, row: int, scope: int) -> None:
         if scope >= 0 and self.masked_scope[ds][row] != scope:
             raise UnsupportedInput(
@@ -335,8 +340,7 @@ class Job:
         carry: Dict[Key, bytes] = {}
         info: dict = {}
         if len(ds):
-            key = np.stack([ds, sc, rw], axis=1)
-            _, first = np.unique(key, axis=0, return_index=True)
+            _, first = np.unique(FastqFormatter._key(ds, rw, sc), return_index=True)
             first = np.sort(first)
             ok = np.array([sc[i] < 0 or self.masked_scope[ds[i]][rw[i]] == sc[i] for i in first.tolist()], bool)
             first = first[ok] if len(first) else first
@@ -540,10 +544,10 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
                 try:
                     pre = None
                     if pool is not None:
-                        pre = ahead if ahead is not None else pool.submit(prepare_job, jid, contigs[jid], readers,
+                        pre = ahead if ahead is not None else pool.submit(JobPrep, jid, contigs[jid], readers,
                                                                            fasta, windows)
                         nj = jid + world
-                        ahead = (pool.submit(prepare_job, nj, contigs[nj], readers, fasta, windows)
+                        ahead = (pool.submit(JobPrep, nj, contigs[nj], readers, fasta, windows)
                                  if nj < len(contigs) else None)
                     job = Job(jid, contigs[jid], readers, fasta, windows, anonymizer, pre)
                     exp = job.exports()

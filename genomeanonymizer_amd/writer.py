@@ -44,6 +44,7 @@ class FastqFormatter:
         self.edited: Dict[Tuple[int, int, int], bytes] = {}   # indel-edited records (write_fastqs)
         self.edited2: Dict[Tuple[int, int, int], bytes] = {}  # the same with the left-overs applied twice
         self._pre = None     # (sorted instance keys, offsets, lengths, bytes) of preformat()
+        self._left_keys = None   # sorted keys of the instances with left-over edits
 
     @staticmethod
     def _key(ds, row, sc):
@@ -78,6 +79,19 @@ class FastqFormatter:
     def records(self, recs: Sequence[Tuple[int, int, int]]) -> dict:
         a = np.array(recs, np.int64).reshape(-1, 3)
         return self.records_arrays(a[:, 0], a[:, 1], a[:, 2])
+
+    def _edited_index(self, ds, row, sc) -> np.ndarray:
+        """Indices of the instances that carry left-over edits."""
+        left = self.res.leftovers
+        if not left or len(ds) == 0:
+            return np.zeros(0, np.int64)
+        if self._left_keys is None or len(self._left_keys) != len(left):
+            a = np.array(list(left.keys()), np.int64).reshape(-1, 3)
+            self._left_keys = np.sort(self._key(a[:, 0], a[:, 1], a[:, 2]))
+        lk = self._left_keys
+        k = self._key(ds, row, sc)
+        pos = np.minimum(np.searchsorted(lk, k), len(lk) - 1)
+        return np.nonzero(lk[pos] == k)[0]
 
     def _native(self, ds, row, sc) -> bytes:
         if len(ds) == 0:
@@ -198,12 +212,7 @@ class FastqFormatter:
         row = np.asarray(row, np.int64)
         sc = np.asarray(sc, np.int64)
         reapply = np.zeros(len(ds), np.int64) if reapply is None else np.asarray(reapply, np.int64)
-        left = self.res.leftovers
-        if not left:
-            return self._native(ds, row, sc)
-        keys = self._key(ds, row, sc)
-        lk = self._key(*zip(*left.keys()))
-        ed = np.nonzero(np.isin(keys, lk))[0]
+        ed = self._edited_index(ds, row, sc)
         if len(ed) == 0:
             return self._native(ds, row, sc)
         keep = np.ones(len(ds), bool)
@@ -237,12 +246,9 @@ class FastqFormatter:
         nl = np.where(ds == 0, T.name_len[r0] if T.n else 0, N.name_len[r1] if N.n else 0).astype(np.int64)
         ls = np.where(ds == 0, T.l_seq[r0] if T.n else 0, N.l_seq[r1] if N.n else 0).astype(np.int64)
         out = nl + 8 + 2 * ls
-        left = self.res.leftovers
-        if left and len(ds):
-            keys = self._key(ds, row, sc)
-            lk = self._key(*zip(*left.keys()))
+        ed = self._edited_index(ds, row, sc)
+        if len(ed):
             re_ = np.zeros(len(ds), np.int64) if reapply is None else np.asarray(reapply, np.int64)
-            ed = np.nonzero(np.isin(keys, lk))[0]
             self.prepare_edited([(int(ds[i]), int(row[i]), int(sc[i])) for i in ed.tolist()], re_[ed].tolist())
             for i in ed.tolist():
                 out[i] = len(self.edited_bytes((int(ds[i]), int(row[i]), int(sc[i])), int(re_[i])))

@@ -417,19 +417,23 @@ class Job(JobPrep):
         li = np.nonzero(loc)[0]
         rec_len[li] = self.record_lengths(fin[li, 4], frow[li], fin[li, 5], reap[li])
         ext_bytes: Dict[int, bytes] = {}
-        for i in np.nonzero(ext)[0].tolist():
-            if gen[i]:
-                ext_bytes[i] = replay.take(int(frow[i]))
-                rec_len[i] = len(ext_bytes[i])
-                continue
-            b = carry.get((int(fjob[i]), int(fin[i, 4]), int(fin[i, 5]), int(frow[i]), int(reap[i])))
-            if b is None and reap[i]:   # a carried record without left-overs: the same bytes
-                b = carry.get((int(fjob[i]), int(fin[i, 4]), int(fin[i, 5]), int(frow[i]), 0))
-            if b is None:
-                raise UnsupportedInput("a record written across contigs was not carried (its mate fields disagree "
-                                       "with where its records are)")
+        xi = np.nonzero(ext)[0]
+        xl = []
+        for i, g, jb, d, sc_, r, re_ in zip(xi.tolist(), gen[xi].tolist(), fjob[xi].tolist(), fin[xi, 4].tolist(),
+                                             fin[xi, 5].tolist(), frow[xi].tolist(), reap[xi].tolist()):
+            if g:
+                b = replay.take(r)
+            else:
+                b = carry.get((jb, d, sc_, r, re_))
+                if b is None and re_:   # a carried record without left-overs: the same bytes
+                    b = carry.get((jb, d, sc_, r, 0))
+                if b is None:
+                    raise UnsupportedInput("a record written across contigs was not carried (its mate fields "
+                                           "disagree with where its records are)")
             ext_bytes[i] = b
-            rec_len[i] = len(b)
+            xl.append(len(b))
+        if len(xi):
+            rec_len[xi] = xl
         order = native.io_replay(fin[:, :7].astype(np.int32), np.where(wr, rec_len, 0), block)
         # every local record of the four files in ONE formatter call, then split per file
         les = [order[f][~ext[order[f]]] for f in range(4)]
@@ -448,12 +452,13 @@ class Job(JobPrep):
             off = np.concatenate([[0], np.cumsum(rec_len[le])])
             parts, prev_local = [], 0
             pos = np.nonzero(is_ext)[0]
-            for j, p in enumerate(pos.tolist()):
+            offl = off.tolist()
+            for j, (p, ei) in enumerate(zip(pos.tolist(), e[pos].tolist())):
                 n_local_before = p - j
-                parts.append(data[off[prev_local]:off[n_local_before]])
-                parts.append(ext_bytes[int(e[p])])
+                parts.append(data[offl[prev_local]:offl[n_local_before]])
+                parts.append(ext_bytes[ei])
                 prev_local = n_local_before
-            parts.append(data[off[prev_local]:])
+            parts.append(data[offl[prev_local]:])
             out.append(b"".join(parts))
         return out
 

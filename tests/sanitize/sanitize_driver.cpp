@@ -7,6 +7,8 @@
 //   sanitize_driver bam FILE...                 decode each file (malformed ones must fail cleanly)
 //   sanitize_driver plan T.bam N.bam SPEC       plan a pair, replay its I/O log, format every record
 //   sanitize_driver oracle SEED                 mask a random batch (single- and multi-threaded)
+//   sanitize_driver edit SEED                   indel left-overs on random (and malformed) records, range gathers
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -241,10 +243,62 @@ static int run_oracle(int seed) {
   return 0;
 }
 
+// Random records (some truncated or with a missing newline) and edits (positions past the read,
+// negative lengths, empty reads) through ganon_fastq_edit; range gathers in and out of bounds.
+static int run_edit(int seed) {
+  std::mt19937_64 rng((uint64_t)seed);
+  const char *bases = "ACGTNMR=";
+  int ok = 0, refused = 0;
+  for (int it = 0; it < 3000; ++it) {
+    const int L = (int)(rng() % 40);
+    const bool rev = rng() & 1;
+    std::string rec = "@r" + std::to_string(it) + "/1\n";
+    for (int k = 0; k < L; ++k) rec += bases[rng() % (rev ? 5 : 8)];
+    rec += "\n+\n";
+    for (int k = 0; k < L; ++k) rec += (char)(33 + rng() % 60);
+    rec += "\n";
+    if (rng() % 10 == 0) rec.resize(rng() % (rec.size() + 1));   // malformed: truncated
+    const int ne = 1 + (int)(rng() % 3);
+    std::vector<int64_t> edits, aoff{0};
+    std::string alleles;
+    for (int e = 0; e < ne; ++e) {
+      const int64_t type = 2 + (int64_t)(rng() % 2), len = (int64_t)(rng() % 7) - 1;
+      edits.push_back((int64_t)(rng() % (L + 6)) - 1);
+      edits.push_back(type);
+      edits.push_back(len);
+      const int al = type == 2 ? (int)std::max<int64_t>(0, len + (int64_t)(rng() % 2)) : 0;
+      for (int k = 0; k < al; ++k) alleles += bases[rng() % 4];
+      aoff.push_back((int64_t)alleles.size());
+    }
+    const int64_t rec_off[2] = {0, (int64_t)rec.size()}, edit_off[2] = {0, ne};
+    const uint8_t r8 = rev;
+    const int32_t times = 1 + (int32_t)(rng() % 2);
+    std::vector<char> out(rec.size() + 2 * (alleles.size() + 8 * ne) + 64);
+    int64_t out_len = 0, bad = -1;
+    const int rc = ganon_fastq_edit(1, rec.data(), rec_off, &r8, &times, edit_off, edits.data(), alleles.data(),
+                                    aoff.data(), out.data(), (int64_t)out.size(), &out_len, &bad);
+    if (rc == 0) {
+      if (out_len < 0 || out_len > (int64_t)out.size()) return 1;
+      ++ok;
+    } else {
+      ++refused;
+    }
+  }
+  std::string src(1000, 'x');
+  std::vector<int64_t> off{0, 10, 990}, len{5, 20, 10};
+  std::vector<char> dst(64);
+  if (ganon_gather_ranges(src.data(), (int64_t)src.size(), 3, off.data(), len.data(), dst.data(), 64) != 35) return 1;
+  len[2] = 11;   // one byte past the source
+  if (ganon_gather_ranges(src.data(), (int64_t)src.size(), 3, off.data(), len.data(), dst.data(), 64) != -1) return 1;
+  std::printf("edit ok=%d refused=%d\n", ok, refused);
+  return 0;
+}
+
 int main(int argc, char **argv) {
   if (argc >= 2 && !std::strcmp(argv[1], "bam")) return run_bam(argc - 2, argv + 2);
   if (argc >= 5 && !std::strcmp(argv[1], "plan")) return run_plan(argv + 2);
   if (argc >= 3 && !std::strcmp(argv[1], "oracle")) return run_oracle(std::atoi(argv[2]));
+  if (argc >= 3 && !std::strcmp(argv[1], "edit")) return run_edit(std::atoi(argv[2]));
   std::fprintf(stderr, "usage: sanitize_driver bam FILE... | plan T.bam N.bam SPEC | oracle SEED\n");
   return 2;
 }

@@ -118,3 +118,12 @@ def test_malformed_bam_files_are_rejected_cleanly(driver, tmp_path):
     assert f"decoded " in out
     dec, rej = out.strip().split("\n")[-1].split()[1::2]
     assert int(rej) >= 14
+
+
+def test_fastq_edit_and_gather_under_sanitizers(driver):
+    """ganon_fastq_edit on random, truncated and oddly edited records, ganon_gather_ranges in and out
+    of bounds: no sanitizer report, malformed input refused with an error code."""
+    for seed in (1, 2):
+        out = _run(driver, "edit", str(seed))
+        ok, refused = (int(x.split("=")[1]) for x in out.split()[1:3])
+        assert ok > 1000 and refused > 100, out       # both paths exercised

@@ -514,7 +514,7 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
     paths = [f"{tumor_out}.1.fastq", f"{tumor_out}.2.fastq", f"{normal_out}.1.fastq", f"{normal_out}.2.fastq"]
     if block_size is None:
         block_size = _writer.io_block_size(os.path.dirname(os.path.abspath(tumor_out)))
-    timing = {"decode_s": 0.0, "plan_s": 0.0, "mask_s": 0.0, "format_s": 0.0, "prefetch_s": 0.0, "resolve_s": 0.0, "write_s": 0.0, "jobs": 0,
+    timing = {"decode_s": 0.0, "plan_s": 0.0, "mask_s": 0.0, "format_s": 0.0, "prefetch_s": 0.0, "resolve_s": 0.0, "write_s": 0.0, "prunes": 0, "jobs": 0,
               "reads": 0}
     failure: Optional[BaseException] = None
     if rank == 0:
@@ -530,6 +530,8 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
     replay = (objects.Replay if os.environ.get("GANON_OBJECTS") == "python" else objects.NativeReplay)(carry, carry_info)
     cands: List[np.ndarray] = []
     carry_floor = 0
+    cand_live: set = set()
+    prune_min = int(os.environ.get("GANON_CARRY_PRUNE_MIN", "200000"))   # carried records before a prune
     cand_names: List[bytes] = []
     base = [0, 0, 0, 0]
     stats_rows: List[Tuple[int, Dict[str, List[int]]]] = []
@@ -582,6 +584,9 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
                                                e["left_names"], e["objs"], e["obj_rows"])
                 replay.run(resolver.take_log())
                 cands.append(e["cand"])
+                c = e["cand"]
+                if len(c):      # candidates stay live to the end of the sample
+                    cand_live.update((r[0], r[2], -1, r[3]) for r in c[c[:, 2] >= 0].tolist())
                 cand_names.extend(e["cand_names"])
                 if job is not None and e["job"] == job.job:
                     mine = (out_n, out_w)
@@ -606,20 +611,23 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
                 base[f] += sum(g["sizes"][f] for g in sizes)
             # carried records still reachable: pending pairs and the end-of-sample candidates (pruned
             # when the carry has doubled or every 16 rounds: each pass walks the whole carry)
-            if len(carry) > max(200_000, 2 * carry_floor) or rnd % 16 == 15:
+            # (the objects of complex names are settled every 16 rounds; the carry walk runs only when
+            # the carry has doubled, so its cost stays proportional to what it inserts)
+            grow = len(carry) > max(prune_min, 2 * carry_floor)
+            if grow or rnd % 16 == 15:
                 pend = resolver.pending()
                 replay.settle(pend)
-                live = set(map(tuple, pend.tolist()))
-                for c in cands:
-                    for r in c[c[:, 2] >= 0].tolist() if len(c) else []:
-                        live.add((r[0], r[2], -1, r[3]))
-                for k in [k for k in carry if k[:4] not in live]:
-                    del carry[k]
-                live_rows = {(k[0], k[1], k[3]) for k in live}
-                for k in [k for k in carry_info if (k if len(k) == 3 else (k[0], k[1], k[3])) not in live_rows
-                          or (len(k) == 4 and k not in live)]:
-                    del carry_info[k]
-                carry_floor = len(carry)
+                if grow:
+                    live = set(map(tuple, pend.tolist()))
+                    live |= cand_live
+                    for k in [k for k in carry if k[:4] not in live]:
+                        del carry[k]
+                    live_rows = {(k[0], k[1], k[3]) for k in live}
+                    for k in [k for k in carry_info if (k if len(k) == 3 else (k[0], k[1], k[3])) not in live_rows
+                              or (len(k) == 4 and k not in live)]:
+                        del carry_info[k]
+                    carry_floor = len(carry)
+                    timing["prunes"] += 1
             job = None
             timing["resolve_s"] += t1 - t0
             timing["write_s"] += time.time() - t1

@@ -120,8 +120,12 @@ def test_streaming_matches_whole_sample(seed, tmp_path):
     assert any(k.endswith(".single_end.fastq") for k in whole)
 
 
-def test_streaming_many_contigs_matches_whole_sample(tmp_path):
-    """12 contigs (a tiled sample): per-contig offsets and the carried state over many rounds."""
+@pytest.mark.parametrize("prune_min", [None, 0], ids=["default", "prune_on_growth"])
+def test_streaming_many_contigs_matches_whole_sample(prune_min, tmp_path, monkeypatch):
+    """12 contigs (a tiled sample): per-contig offsets and the carried state over many rounds; with
+    GANON_CARRY_PRUNE_MIN=0 the carried records are pruned whenever they have doubled."""
+    if prune_min is not None:
+        monkeypatch.setenv("GANON_CARRY_PRUNE_MIN", str(prune_min))
     from genomeanonymizer_amd.synth.generate import generate, scenario
     from genomeanonymizer_amd.synth.tile import tile_sample
     base = generate(scenario("tiny"), str(tmp_path / "base"))

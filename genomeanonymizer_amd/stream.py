@@ -71,11 +71,12 @@ class JobPrep:
     streamed loop runs it for the next contig in a prefetch thread while the current one masks,
     formats and writes (the BGZF inflate and the planner are native and drop the GIL)."""
 
-    def __init__(self, job: int, contig: str, readers, fasta: FastaRef, windows: Sequence[Window]):
+    def __init__(self, job: int, contig: str, readers, fasta: FastaRef, windows: Sequence[Window], tables=None):
+        """``tables``: the decoded records when a decode thread produced them (a Future)."""
         self.job = job
         self.contig = contig
         t0 = time.time()
-        self.tables = decode_contig(readers, contig)
+        self.tables = decode_contig(readers, contig) if tables is None else tables.result()
         t1 = time.time()
         self.planner = ContigPlanner(self.tables[0], self.tables[1], fasta, windows, job)
         self.plan: Plan = self.planner.run()
@@ -537,10 +538,21 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
     stats_rows: List[Tuple[int, Dict[str, List[int]]]] = []
     totals = np.zeros(8, np.int64)
     n_rounds = (len(contigs) + world - 1) // world
-    # the next job's decode runs in a thread while this job plans, masks and writes (bounded: one
-    # job ahead); GANON_PREFETCH=0 decodes in line
-    pool = ThreadPoolExecutor(1) if os.environ.get("GANON_PREFETCH", "1") != "0" else None
-    ahead = None
+    # look-ahead: a decode thread reads the next contigs in order (one BamReader stream) and
+    # `depth` threads plan and batch them (JobPrep) while this job masks, formats and writes;
+    # GANON_PREFETCH = depth (default 2, 0: everything in line). Bounded: depth jobs ahead.
+    depth = int(os.environ.get("GANON_PREFETCH", "2"))
+    dec_pool = ThreadPoolExecutor(1) if depth > 0 else None
+    pool = ThreadPoolExecutor(depth) if depth > 0 else None
+    ahead: Dict[int, object] = {}
+
+    def submit_upto(j_last: int) -> None:
+        j = max(ahead) + world if ahead else rank
+        while j <= min(j_last, len(contigs) - 1):
+            if j not in ahead:
+                dec = dec_pool.submit(decode_contig, readers, contigs[j])
+                ahead[j] = pool.submit(JobPrep, j, contigs[j], readers, fasta, windows, dec)
+            j += world
     try:
         for rnd in range(n_rounds):
             jid = rnd * world + rank
@@ -551,11 +563,8 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
                 try:
                     pre = None
                     if pool is not None:
-                        pre = ahead if ahead is not None else pool.submit(JobPrep, jid, contigs[jid], readers,
-                                                                           fasta, windows)
-                        nj = jid + world
-                        ahead = (pool.submit(JobPrep, nj, contigs[nj], readers, fasta, windows)
-                                 if nj < len(contigs) else None)
+                        submit_upto(jid + depth * world)
+                        pre = ahead.pop(jid)
                     job = Job(jid, contigs[jid], readers, fasta, windows, anonymizer, pre)
                     exp = job.exports()
                     for k in ("decode_s", "plan_s", "mask_s", "format_s", "prefetch_s"):
@@ -663,8 +672,11 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
                         merged[key] = list(counts)
             write_statistics(normal_stats_path or f"{normal_bam}.statistics.txt", merged)
     finally:
-        if pool is not None:      # a prefetch still running (a failed job) ends before its reader closes
+        if pool is not None:      # prefetches still running (a failed job) end before their reader closes
+            for f in ahead.values():
+                f.cancel()
             pool.shutdown(wait=True)
+            dec_pool.shutdown(wait=True)
         for fd in fds:
             os.close(fd)
         for r in readers:

@@ -222,12 +222,14 @@ class FastqFormatter:
         nl = np.where(ds == 0, T.name_len[np.where(ds == 0, row, 0)], N.name_len[np.where(ds == 1, row, 0)])
         ls = np.where(ds == 0, T.l_seq[np.where(ds == 0, row, 0)], N.l_seq[np.where(ds == 1, row, 0)])
         rl = np.where(keep, nl.astype(np.int64) + 8 + 2 * ls.astype(np.int64), 0)
-        off = np.concatenate([[0], np.cumsum(rl)])      # byte offset in `data` of each record
-        self.prepare_edited([(int(ds[i]), int(row[i]), int(sc[i])) for i in ed.tolist()], reapply[ed].tolist())
+        off = np.concatenate([[0], np.cumsum(rl)]).tolist()      # byte offset in `data` of each record
+        insts = list(zip(ds[ed].tolist(), row[ed].tolist(), sc[ed].tolist()))
+        re_ = reapply[ed].tolist()
+        self.prepare_edited(insts, re_)
         parts, prev = [], 0
-        for i in ed.tolist():
+        for i, inst, r in zip(ed.tolist(), insts, re_):
             parts.append(data[off[prev]:off[i]])
-            parts.append(self.edited_bytes((int(ds[i]), int(row[i]), int(sc[i])), int(reapply[i])))
+            parts.append((self.edited2 if r else self.edited)[inst])
             prev = i + 1
         parts.append(data[off[prev]:])
         return b"".join(parts)
@@ -249,9 +251,10 @@ class FastqFormatter:
         ed = self._edited_index(ds, row, sc)
         if len(ed):
             re_ = np.zeros(len(ds), np.int64) if reapply is None else np.asarray(reapply, np.int64)
-            self.prepare_edited([(int(ds[i]), int(row[i]), int(sc[i])) for i in ed.tolist()], re_[ed].tolist())
-            for i in ed.tolist():
-                out[i] = len(self.edited_bytes((int(ds[i]), int(row[i]), int(sc[i])), int(re_[i])))
+            insts = list(zip(ds[ed].tolist(), row[ed].tolist(), sc[ed].tolist()))
+            rl = re_[ed].tolist()
+            self.prepare_edited(insts, rl)
+            out[ed] = [len((self.edited2 if r else self.edited)[inst]) for inst, r in zip(insts, rl)]
         return out
 
 

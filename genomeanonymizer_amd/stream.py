@@ -545,14 +545,14 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
     dec_pool = ThreadPoolExecutor(1) if depth > 0 else None
     pool = ThreadPoolExecutor(depth) if depth > 0 else None
     ahead: Dict[int, object] = {}
+    next_job = [rank]          # the next of this rank's jobs to submit (in order: one BAM stream)
 
     def submit_upto(j_last: int) -> None:
-        j = max(ahead) + world if ahead else rank
-        while j <= min(j_last, len(contigs) - 1):
-            if j not in ahead:
-                dec = dec_pool.submit(decode_contig, readers, contigs[j])
-                ahead[j] = pool.submit(JobPrep, j, contigs[j], readers, fasta, windows, dec)
-            j += world
+        while next_job[0] <= min(j_last, len(contigs) - 1):
+            j = next_job[0]
+            dec = dec_pool.submit(decode_contig, readers, contigs[j])
+            ahead[j] = pool.submit(JobPrep, j, contigs[j], readers, fasta, windows, dec)
+            next_job[0] += world
     try:
         for rnd in range(n_rounds):
             jid = rnd * world + rank

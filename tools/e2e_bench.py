@@ -4,7 +4,10 @@ planner -> GPU masking + indel tally -> GPU FASTQ formatting -> files), the path
 CLI runs: the streamed path (per contig, bounded memory; the default) and the whole-sample path.
 Prints one JSON line with per-stage seconds, reads/s and the process's peak RSS per mode.
 
-    python tools/e2e_bench.py DIR   # DIR holds tumor.bam normal.bam ref.fa variants.vcf (tools/e2e_data.py)
+    python tools/e2e_bench.py DIR [OUTDIR] [stream,whole]   # DIR: tumor.bam normal.bam ref.fa variants.vcf
+                                                             # (tools/e2e_data.py)
+    E2E_PROFILE=PREFIX ...   # cProfile of the timed run of each mode -> PREFIX_<mode>.txt (main thread)
+    GANON_PREFETCH=N ...     # look-ahead planning threads of the streamed path (0: in line)
 """
 import json
 import os

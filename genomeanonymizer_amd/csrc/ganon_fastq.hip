@@ -707,7 +707,7 @@ __device__ __forceinline__ const uint32_t *fq_clamp(uintptr_t a, uintptr_t lo, u
   return reinterpret_cast<const uint32_t *>(a < lo ? lo : a > hi ? hi : a);
 }
 
-template <int KQ>
+template <int KQ, bool ALIGN5 = true>
 __global__ void __launch_bounds__(kFqThreads) k_fq_quad(const FqBufs bufs, const FqRec *__restrict__ recs,
                                                         const uint64_t *__restrict__ off,
                                                         const int64_t *__restrict__ tile_first, int64_t n,
@@ -886,16 +886,27 @@ __global__ void __launch_bounds__(kFqThreads) k_fq_quad(const FqBufs bufs, const
       for (int d = 0; d < 4; ++d) m[d] = full ? 0xFFFFFFFFu : fq_dmask(J[j] + 4 * d, len[j]);
       if (f == 0) {
         const uint32_t sel = rev ? (par[j] ? 0x04010502u : 0x00040105u) : (par[j] ? 0x02050104u : 0x05010400u);
+        const uint64_t tlo = rev ? kRevLo : kFwdLo, thi = rev ? kRevHi : kFwdHi;
+        // window bytes [sh + 2d, sh + 2d + 4) for d = 0..3 (reversed: sh + 6 - 2d) from five byte
+        // alignments instead of a 3-way dword select per output dword
+        const uint32_t w0 = __builtin_amdgcn_alignbyte(dw[j][1], dw[j][0], sh[j]);
+        const uint32_t w1 = __builtin_amdgcn_alignbyte(dw[j][2], dw[j][1], sh[j]);
+        const uint32_t w2 = __builtin_amdgcn_alignbyte(dw[j][3], dw[j][2], sh[j]);
+        const uint32_t h0 = __builtin_amdgcn_alignbyte(w1, w0, 2), h1 = __builtin_amdgcn_alignbyte(w2, w1, 2);
+        const uint32_t win[4] = {rev ? h1 : w0, rev ? w1 : h0, rev ? h0 : w1, rev ? w0 : h1};
 #pragma unroll
         for (int d = 0; d < 4; ++d) {
-          const uint32_t o = sh[j] + (rev ? 6 - 2 * d : 2 * d);   // window byte offset (<= 9)
-          const uint32_t kk = o >> 2;
-          const uint32_t lo_w = kk == 0 ? dw[j][0] : kk == 1 ? dw[j][1] : dw[j][2];
-          const uint32_t hi_w = kk == 0 ? dw[j][1] : kk == 1 ? dw[j][2] : dw[j][3];
-          const uint32_t w = __builtin_amdgcn_alignbyte(hi_w, lo_w, o & 3);
+          uint32_t w = win[d];
+          if constexpr (!ALIGN5) {   // round-1 select per output dword (A/B: GANON_PARAM_FASTQ_KD 11)
+            const uint32_t o = sh[j] + (rev ? 6 - 2 * d : 2 * d);
+            const uint32_t kk = o >> 2;
+            const uint32_t lo_w = kk == 0 ? dw[j][0] : kk == 1 ? dw[j][1] : dw[j][2];
+            const uint32_t hi_w = kk == 0 ? dw[j][1] : kk == 1 ? dw[j][2] : dw[j][3];
+            w = __builtin_amdgcn_alignbyte(hi_w, lo_w, o & 3);
+          }
           const uint32_t hiN = (w >> 4) & 0x0F0F0F0Fu, loN = w & 0x0F0F0F0Fu;
           const uint32_t cc = __builtin_amdgcn_perm(loN, hiN, sel);
-          x[d] = rev ? nt16_lut(cc, kRevLo, kRevHi) : nt16_lut(cc, kFwdLo, kFwdHi);
+          x[d] = nt16_lut(cc, tlo, thi);
           const uint32_t y = x[d] | ~m[d];
           if (rev && ((y - 0x01010101u) & ~y & 0x80808080u)) bad = min(bad, (unsigned long long)(r0 + k));
         }
@@ -1170,7 +1181,7 @@ GANON_API int ganon_fastq_run(ganon_ctx *ctx, ganon_fastq *f) {
     // virtual dwords per lane per round: a tile holds ~2,100 of them (2,048 tile dwords plus the
     // dwords neighbouring fields share), so the width sets the number of dependent load rounds
     const int kd = ctx->fq_kd;
-    auto kern = kd == 0 ? k_fq_quad<2> : kd == 9 ? k_fq_quad<1> : kd == 10 ? k_fq_quad<3>
+    auto kern = kd == 0 ? k_fq_quad<2> : kd == 9 ? k_fq_quad<1> : kd == 10 ? k_fq_quad<3> : kd == 11 ? k_fq_quad<2, false>
               : kd == 1 ? k_fq_format<1> : kd == 2 ? k_fq_format<2> : kd == 3 ? k_fq_format<3>
               : kd == 5 ? k_fq_format<5> : kd == 6 ? k_fq_format<6> : kd == 8 ? k_fq_format<8> : k_fq_format<4>;
     hipLaunchKernelGGL(kern, dim3((unsigned)f->n_tiles), dim3(kFqThreads), 0, ctx->stream, f->bufs, f->recs,

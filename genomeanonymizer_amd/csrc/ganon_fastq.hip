@@ -247,11 +247,15 @@ struct FqField {
   int a, b, ia, ib;
 };
 
+// int64 clamps written out: HIP's min/max templates on int64_t compile to f64 conversions here
+__device__ __forceinline__ int64_t lo64(int64_t a, int64_t b) { return a < b ? a : b; }
+__device__ __forceinline__ int64_t hi64(int64_t a, int64_t b) { return a < b ? b : a; }
+
 __device__ __forceinline__ FqField fq_field(int64_t P0, uint32_t fa, uint32_t len) {
   FqField F;
-  const int64_t a = max<int64_t>(P0 + fa, 0), b = min<int64_t>(P0 + fa + len, kFqTile);
-  F.a = (int)min<int64_t>(a, kFqTile);
-  F.b = (int)max<int64_t>(b, (int64_t)F.a);
+  const int64_t a = hi64(P0 + fa, 0), b = lo64(P0 + fa + len, kFqTile);
+  F.a = (int)lo64(a, kFqTile);
+  F.b = (int)hi64(b, (int64_t)F.a);
   F.ia = (F.a + 3) & ~3;
   F.ib = F.b & ~3;
   return F;
@@ -410,7 +414,7 @@ __device__ __forceinline__ void fq_tile_by_records(uint8_t *smem, const FqBufs &
   uint64_t *s_off = reinterpret_cast<uint64_t *>(smem + kFqTile + kFqStage * sizeof(FqRec));
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   for (int64_t sb = r0; sb <= rl; sb += kFqStage) {
-    const int ns = (int)min<int64_t>(kFqStage, rl - sb + 1);
+    const int ns = (int)lo64(kFqStage, rl - sb + 1);
     if (sb != r0) __syncthreads();   // the previous batch of staged records is done
     for (int k = threadIdx.x; k < ns; k += kFqThreads) s_rec[k] = recs[sb + k];
     for (int k = threadIdx.x; k <= ns; k += kFqThreads) s_off[k] = off[sb + k];
@@ -707,6 +711,8 @@ __device__ __forceinline__ const uint32_t *fq_clamp(uintptr_t a, uintptr_t lo, u
   return reinterpret_cast<const uint32_t *>(a < lo ? lo : a > hi ? hi : a);
 }
 
+typedef __attribute__((address_space(1))) const uint32_t GU32;
+
 template <int KQ, bool ALIGN5 = true>
 __global__ void __launch_bounds__(kFqThreads) k_fq_quad(const FqBufs bufs, const FqRec *__restrict__ recs,
                                                         const uint64_t *__restrict__ off,
@@ -819,7 +825,7 @@ __global__ void __launch_bounds__(kFqThreads) k_fq_quad(const FqBufs bufs, const
   for (int vb = 0; vb < ((skip & 32) ? 0 : V); vb += kFqThreads * KQ) {
     uint32_t key[KQ], dw[KQ][5], sh[KQ], par[KQ], flg[KQ];
     int tq[KQ], J[KQ], len[KQ];
-    const uint32_t *ad[KQ][5];
+    const GU32 *ad[KQ][5];   // global address space: global_load, not flat (no LDS wait coupling)
 #pragma unroll
     for (int j = 0; j < KQ; ++j) {
       const int v = vb + j * kFqThreads + t;
@@ -827,7 +833,7 @@ __global__ void __launch_bounds__(kFqThreads) k_fq_quad(const FqBufs bufs, const
       sh[j] = par[j] = flg[j] = 0;
       tq[j] = J[j] = len[j] = 0;
 #pragma unroll
-      for (int k = 0; k < 5; ++k) ad[j][k] = reinterpret_cast<const uint32_t *>(bufs.names);
+      for (int k = 0; k < 5; ++k) ad[j][k] = reinterpret_cast<const GU32 *>((uintptr_t)bufs.names);
       if (v >= V) continue;
       const uint32_t kf = map[v];
       key[j] = kf;
@@ -857,7 +863,7 @@ __global__ void __launch_bounds__(kFqThreads) k_fq_quad(const FqBufs bufs, const
       const int a = start - (start & 3);
 #pragma unroll
       for (int k = 0; k < 5; ++k)
-        ad[j][k] = reinterpret_cast<const uint32_t *>(A0 + (uint64_t)(uint32_t)min(max(a + 4 * k, 0), hi));
+        ad[j][k] = reinterpret_cast<const GU32 *>(A0 + (uint64_t)(uint32_t)min(max(a + 4 * k, 0), hi));
     }
 #pragma unroll
     for (int j = 0; j < KQ; ++j) {

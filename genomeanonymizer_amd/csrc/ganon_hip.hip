@@ -39,6 +39,15 @@ using namespace ganon_dev;
 
 namespace {
 
+// Buffers reached through GrpAux (device memory holding pointers) as address-space-1 pointers:
+// global_* memory ops instead of flat_* on the overflow, far-list and per-scope-count paths.
+template <class T>
+__device__ __forceinline__ __attribute__((address_space(1))) T *gp(T *p) {
+  return (__attribute__((address_space(1))) T *)(uintptr_t)p;
+}
+typedef __attribute__((address_space(1))) unsigned long long GU64;
+typedef __attribute__((address_space(1))) unsigned int GU32;
+
 __device__ __forceinline__ int nib_at(const uint8_t *__restrict__ buf, int64_t i) {
   const uint8_t b = buf[i >> 1];
   return (i & 1) ? (b & 0xF) : (b >> 4);
@@ -362,8 +371,8 @@ __device__ __forceinline__ void sink_patch(SH &sh, const PatchSink &k, int64_t n
   if (k.fused) {
     const int64_t byte = nib >> 1;
     if (!k.inside(byte)) {
-      const unsigned long long i = atomicAdd(k.aux->far_count, 1ull);
-      if (i < (unsigned long long)k.aux->far_cap) k.aux->far[i] = e;
+      const unsigned long long i = __hip_atomic_fetch_add(gp(k.aux->far_count), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (i < (unsigned long long)k.aux->far_cap) gp(k.aux->far)[i] = e;
       return;
     }
     if (k.lds) {
@@ -388,6 +397,12 @@ __device__ __forceinline__ unsigned long long ld_l2(const unsigned long long *p)
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // sc1: past the CU's L1
 }
 __device__ __forceinline__ unsigned int ld_l2(const unsigned int *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long ld_l2(const GU64 *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned int ld_l2(const GU32 *p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -422,8 +437,8 @@ __device__ __forceinline__ void grp_observe(SH &sh, const GrpRange &R, const Grp
   } else {
     // past the LDS list: straight into the group's global region (no second scan)
     if (k - SH::kObs < gg.cap - SH::kObs) {
-      gg.aux->okey[gg.off + (k - SH::kObs)] = key;
-      gg.aux->opay[gg.off + (k - SH::kObs)] = pay;
+      gp(gg.aux->okey)[gg.off + (k - SH::kObs)] = key;
+      gp(gg.aux->opay)[gg.off + (k - SH::kObs)] = pay;
     }
   }
 }
@@ -683,9 +698,9 @@ __device__ __forceinline__ void grp_global(const GrpBatch &B, SH &sh, const GrpG
                                            int s_begin, const PatchSink &sink) {
   const int tid = opaque_tid();
   const int tsize = max(2 * n, 64);
-  unsigned long long *tk = gg.aux->tkey + 2 * gg.off;
-  unsigned int *tf = gg.aux->tflag + 2 * gg.off;
-  unsigned long long *okey = gg.aux->okey + gg.off, *opay = gg.aux->opay + gg.off;
+  GU64 *tk = gp(gg.aux->tkey) + 2 * gg.off;
+  GU32 *tf = gp(gg.aux->tflag) + 2 * gg.off;
+  GU64 *okey = gp(gg.aux->okey) + gg.off, *opay = gp(gg.aux->opay) + gg.off;
   for (int i = tid; i < tsize; i += kGrpThreads) {
     tk[i] = kEmpty;
     tf[i] = 0;
@@ -857,12 +872,12 @@ __global__ void __launch_bounds__(kGrpThreads, (OBS > 512 ? 4 : U == 1 ? 6 : U =
       // workgroup's partial totals (k_finish sums them)
       for (int i = opaque_tid(); i < ((skip & kSkipCounts) ? 0 : s_end - s_begin); i += kGrpThreads) {
         if (B.span_len[s_begin + i] > kGrpMaxSpan) continue;
-        aux->scope_calls[s_begin + i] = sh.cnt_calls[i];
-        aux->scope_bases[s_begin + i] = sh.cnt_bases[i];
+        gp(aux->scope_calls)[s_begin + i] = sh.cnt_calls[i];
+        gp(aux->scope_bases)[s_begin + i] = sh.cnt_bases[i];
       }
       if (tid == 0) {
-        aux->part[2 * blockIdx.x] = sh.blk_calls;
-        aux->part[2 * blockIdx.x + 1] = sh.blk_bases;
+        gp(aux->part)[2 * blockIdx.x] = sh.blk_calls;
+        gp(aux->part)[2 * blockIdx.x + 1] = sh.blk_bases;
       }
       break;
     }
@@ -885,13 +900,13 @@ __global__ void __launch_bounds__(kGrpThreads, (OBS > 512 ? 4 : U == 1 ? 6 : U =
     if (skip & kSkipClassify) continue;
     const int n = sh.n_obs;
     if (tid == 0 && n > kGrpQuad)   // path counters (ganon_batch_path_counts): sorted list, region, split
-      atomicAdd(&aux->paths[n <= OBS ? 0 : n <= gg.cap ? 1 : 2], 1ull);
+      __hip_atomic_fetch_add(gp(aux->paths) + (n <= OBS ? 0 : n <= gg.cap ? 1 : 2), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (n > OBS) {
       if (n <= gg.cap) {
         // the list joins the region's tail: n observations contiguous in the region
         for (int i = opaque_tid(); i < OBS; i += kGrpThreads) {
-          aux->okey[gg.off + (n - OBS) + i] = sh.key[i];
-          aux->opay[gg.off + (n - OBS) + i] = sh.pay[i];
+          gp(aux->okey)[gg.off + (n - OBS) + i] = sh.key[i];
+          gp(aux->opay)[gg.off + (n - OBS) + i] = sh.pay[i];
         }
         __builtin_amdgcn_s_waitcnt(0);   // region stores at L2 before the barrier
         __syncthreads();
@@ -904,7 +919,7 @@ __global__ void __launch_bounds__(kGrpThreads, (OBS > 512 ? 4 : U == 1 ? 6 : U =
       __builtin_amdgcn_s_waitcnt(0);
       __syncthreads();
       for (int i = opaque_tid(); i < gg.cap; i += kGrpThreads) {
-        const unsigned long long k = i < OBS ? sh.key[i] : ld_l2(aux->okey + gg.off + (i - OBS));
+        const unsigned long long k = i < OBS ? sh.key[i] : ld_l2(gp(aux->okey) + gg.off + (i - OBS));
         atomicMin(&sh.kmin, k);
         atomicMax(&sh.kmax, k);
       }

@@ -1,14 +1,18 @@
 #!/usr/bin/env python3
 """Benchmark of the germline-masking hot path on BASELINE.json configs[1].
 
-One step = everything it takes to anonymize one resident raw batch: ``ganon_batch_run`` =
-the device prep (CIGAR walk of every (scope, read) incidence into aligned segments, scope groups,
-output partition pieces — rebuilt from the raw ganon_batch arrays on every run,
-csrc/ganon_prep.hip) + SNV tally -> TN classification -> overwrite for every scope and the copy of
-every other read (k_group, k_finish), then ``ganon_indel_run`` = the germline indel tally (no
-launch when no read has an I/D op, as in the config-2 synthetic reads). The batch is the config-2
-layout (10 M synthetic 150 bp tumor+normal reads on a 3.0 Gb genome with 1 M germline SNPs and a
-1 M-window VCF; genomeanonymizer_amd/synth/batch.py) copied to HBM once as raw SoA arrays.
+One step = everything a freshly arrived raw batch needs to be anonymized, starting from its raw
+SoA arrays in HBM: ``ganon_batch_replan`` = the device plan of a fresh batch (one scan that
+validates every read and scope, writes read ends and segments per read, the scope-group table and
+the output-partition candidates; one synchronization for the prep mode and buffer sizes), then
+``ganon_batch_run`` = the device prep (CIGAR walk of every (scope, read) incidence into aligned
+segments with the incidence checks, output partition pieces, csrc/ganon_prep.hip) + SNV tally ->
+TN classification -> overwrite for every scope and the copy of every other read (k_group,
+k_finish) + the write-scope check, then the germline indel tally when the scan found I/D ops (none
+in the config-2 synthetic reads: no launch). Nothing derived survives from one step to the next
+(the 3 GB batch is also far larger than the 256 MB MALL). The batch is the config-2 layout (10 M
+synthetic 150 bp tumor+normal reads on a 3.0 Gb genome with 1 M germline SNPs and a 1 M-window
+VCF; genomeanonymizer_amd/synth/batch.py) copied to HBM once as raw SoA arrays.
 Multi-GPU (torchrun): every rank owns its own config-2 shard (per-contig sharding makes shards
 independent; weak scaling) and the only collective is the int64 totals all-reduce over RCCL of
 each step, overlapped with the next step's kernels (double-buffered).
@@ -36,7 +40,7 @@ sys.path.insert(0, REPO)
 
 HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 GROUP_MAX_SPAN = 1 << 20                # kGrpMaxSpan: widest scope of the group kernels
-PREP_KERNELS = ("prep_groups", "prep_emit", "prep_pieces")
+PREP_KERNELS = ("prep_scan", "prep_groups", "prep_emit", "prep_pieces", "prep_seen_check")
 
 
 def kernel_class(name: str) -> str:
@@ -106,13 +110,14 @@ def kernel_bytes(arr) -> dict:
     return out
 
 
-def cpu_baseline(arr, n_reads: int, budget_s: float = 10.0, threads: int = 16) -> dict:
+def cpu_baseline(arr, n_reads: int, budget_s: float = 10.0, threads: int = 0) -> dict:
     """SURVEY §8(d) ref-cpu-N and ref-cpu-1: the C oracle (the reference's per-scope classify +
     mask restated in C) over the same resident batch, on `threads` host threads (scope shards;
     16 = one GPU's CPU share on the box) and on one thread, each for about budget_s / 2."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     from pyoracle import OracleEngine
     eng = OracleEngine()
+    threads = threads or int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
 
     def rate(th: int):
         eng.threads = th
@@ -126,7 +131,15 @@ def cpu_baseline(arr, n_reads: int, budget_s: float = 10.0, threads: int = 16) -
 
     mt, mt_runs, mt_s = rate(threads)
     st, st_runs, st_s = rate(1)
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as fh:
+            model = next((ln.split(":", 1)[1].strip() for ln in fh if ln.startswith("model name")), "")
+    except OSError:
+        pass
     return {"value": round(mt, 1), "unit": "reads/s", "cores": threads, "kind": "port",
+            "host": {"nproc": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)), "cpu_model": model,
+                     "threads_used": threads, "why": "the GPU box's CPU share per GPU (OMP_NUM_THREADS)"},
             "sample": f"oracle/ganon_oracle.c (C restatement of the reference's per-scope classify+mask) over "
                       f"the whole {n_reads}-read batch: {threads} threads x{mt_runs} ({mt_s:.1f} s); one thread "
                       f"{st:.0f} reads/s x{st_runs} ({st_s:.1f} s); reference Python calibration: 1,196 reads/s "
@@ -269,6 +282,71 @@ def pcie_bench(masker, db, arr, args, torch) -> dict:
                     "validation/plan + run + D2H of the masked bases, per batch"}
 
 
+def _child_json(cmd, env_extra: dict, timeout: int) -> dict:
+    """Run a measurement in a child process (its own peak RSS and device context) and parse the
+    last JSON line it prints."""
+    import subprocess
+    env = dict(os.environ, **env_extra)
+    t = time.perf_counter()
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
+    if r.returncode != 0:
+        return {"error": f"exit {r.returncode}: {r.stderr[-600:]}"}
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    out["child_wall_s"] = round(time.perf_counter() - t, 2)
+    return out
+
+
+def e2e_lines(args) -> dict:
+    """the product pipeline file to file (BAM decode -> native planner -> HIP
+    masking + indel tally -> HIP FASTQ formatting -> FASTQ files; tools/e2e_bench.py, streamed path)
+    on a synthetic paired-BAM pair (synth/fastpair.py: 150 bp reads, germline SNPs + deletions,
+    window VCF, .bai), and the same pipeline on the CPU (the C oracle masks on the host's cores, the
+    host C++ formatter formats) on a bounded sample. Run in child processes before this process
+    touches the GPU. The whole-sample path runs once on the same input: its files must equal the
+    streamed ones."""
+    import shutil
+    import tempfile
+    from genomeanonymizer_amd.synth.fastpair import make_pair
+    d = tempfile.mkdtemp(prefix="ganon_e2e_")
+    res = {}
+    try:
+        t = time.perf_counter()
+        inp = os.path.join(d, "in")
+        make_pair(inp, n_contigs=args.e2e_contigs, pairs_per_contig=args.e2e_pairs)
+        gen_s = time.perf_counter() - t
+        tool = os.path.join(REPO, "tools", "e2e_bench.py")
+        hip = _child_json([sys.executable, tool, inp, os.path.join(d, "out"), "stream,whole"],
+                          {"E2E_RUNS": str(args.e2e_runs)}, 900)
+        st = hip.get("stream", {})
+        res["e2e"] = {
+            "value": st.get("reads_per_s"), "unit": "reads/s", "bases_per_sec": st.get("bases_per_s"),
+            "reads": st.get("reads"), "wall_s": st.get("stages_s", {}).get("wall_s"),
+            "wall_s_runs": st.get("wall_s_runs"), "stages_s": st.get("stages_s"),
+            "peak_rss_mb": st.get("peak_rss_mb"), "output_bytes": st.get("output_bytes"),
+            "whole_sample": {k: hip.get("whole", {}).get(k) for k in ("reads_per_s", "stages_s", "peak_rss_mb")},
+            "files_equal_whole_sample": hip.get("stream_equals_whole"),
+            "workload": f"synth/fastpair.py: {args.e2e_contigs} contigs x 2 Mb, {args.e2e_pairs} pairs per contig "
+                        f"and sample (150 bp, FR), 1 germline het SNP/kb + 0.1 het deletion/kb in tumor and normal, "
+                        f"a somatic window SNV every 20 kb; streamed product, files written to local disk",
+            "generate_s": round(gen_s, 1), "error": hip.get("error")}
+        # the CPU path on a bounded sample (the first contigs)
+        cpu_in = os.path.join(d, "cpu_in")
+        make_pair(cpu_in, n_contigs=args.e2e_cpu_contigs, pairs_per_contig=args.e2e_pairs, seed=8)
+        cores = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
+        cpu = _child_json([sys.executable, tool, cpu_in, os.path.join(d, "cpu_out"), "stream"],
+                          {"E2E_ENGINE": "oracle", "E2E_THREADS": str(cores), "E2E_RUNS": "1"}, 900)
+        cs = cpu.get("stream", {})
+        res["cpu_e2e"] = {"value": cs.get("reads_per_s"), "unit": "reads/s", "bases_per_sec": cs.get("bases_per_s"),
+                          "reads": cs.get("reads"), "cores": cores, "kind": "port",
+                          "stages_s": cs.get("stages_s"), "error": cpu.get("error"),
+                          "sample": f"the same pipeline with the C oracle masking on {cores} host threads, the "
+                                    f"indel restatement (Python) and the host C++ formatter, "
+                                    f"{args.e2e_cpu_contigs} contigs of the same shape"}
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+    return res
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -288,6 +366,15 @@ def main() -> None:
     ap.add_argument("--target", type=int, default=None, help="GANON_PARAM_GROUP_TARGET (cost units per group)")
     ap.add_argument("--no-fastq", action="store_true", help="skip the FASTQ formatter measurement")
     ap.add_argument("--indel-sort", type=int, default=0, help="GANON_PARAM_INDEL_SORT: 0 segmented, 1 global")
+    ap.add_argument("--fuse-emit", type=int, default=0,
+                    help="GANON_PARAM_FUSE_EMIT: 1 the group kernel builds its records, 0 the separate emit kernel")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (BAM -> FASTQ) line")
+    ap.add_argument("--e2e-contigs", type=int, default=24)
+    ap.add_argument("--e2e-pairs", type=int, default=23_000, help="pairs per contig and sample")
+    ap.add_argument("--e2e-cpu-contigs", type=int, default=2)
+    ap.add_argument("--e2e-runs", type=int, default=2, help="timed end-to-end runs after a warm run")
+    ap.add_argument("--resident", action="store_true",
+                    help="round-2 step: run only, the plan made once at upload (not a fresh batch)")
     ap.add_argument("--pmc", default=None,
                     help="PMC step summary (tools/pmc_step.py) for the traffic field; default "
                          "profiles/r02/pmc_step_<config>.json when present")
@@ -296,9 +383,11 @@ def main() -> None:
         if getattr(args, k) is None:
             setattr(args, k, v)
 
-    import torch
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
+    # end to end first: child processes, before this process initialises the GPU (N = 1 only)
+    e2e = e2e_lines(args) if world == 1 and not args.no_e2e else {}
+    import torch
     local = int(os.environ.get("LOCAL_RANK", 0))
     dev = local % max(1, torch.cuda.device_count())   # == local on a node with a GPU per rank
     torch.cuda.set_device(dev)
@@ -323,12 +412,15 @@ def main() -> None:
     if args.target:
         masker.set_param(native.PARAM_GROUP_TARGET, args.target)
     masker.set_param(native.PARAM_INDEL_SORT, args.indel_sort)
+    masker.set_param(native.PARAM_FUSE_EMIT, args.fuse_emit)
     stream = torch.cuda.current_stream()
     masker.set_stream(stream.cuda_stream)
     t_up = time.perf_counter()
     ref = masker.upload_reference(arr["ref_nt16"])      # the genome stays resident (ganon_ref_upload)
     db = masker.upload({k: v for k, v in arr.items() if k != "ref_nt16"}, ref=ref)
-    ind = db.indel_tally(arr)      # germline indel tally, part of every step
+    shape = db.shape()
+    # germline indel tally: part of every step when the device scan found I/D ops
+    ind = db.indel_tally(arr) if shape["id_ops"] else None
     t_up = time.perf_counter() - t_up
     # totals all-reduce (RCCL) of every step, double-buffered: the reduction of step i runs beside
     # step i + 1's kernels; a buffer is reused only after its previous reduction completed
@@ -337,8 +429,11 @@ def main() -> None:
     host_reduce = dist is not None and dist.get_backend() != "nccl"
 
     def step(i: int):
+        if not args.resident:
+            db.replan()     # a fresh batch: the plan from the raw arrays, every step
         db.run()
-        ind.run()
+        if ind is not None:
+            ind.run()
         if dist is not None:
             if host_reduce:
                 dist.all_reduce(torch.from_numpy(db.totals()))
@@ -379,8 +474,11 @@ def main() -> None:
     masker.set_profiling(True)
     ktimes: dict = {}
     for _ in range(args.steps):
+        if not args.resident:
+            db.replan()
         db.run()
-        ind.run()
+        if ind is not None:
+            ind.run()
         db.sync()
         for name, launches, ms in db.kernel_times():
             k = ktimes.setdefault(name, [0, 0.0])
@@ -389,11 +487,25 @@ def main() -> None:
     masker.set_profiling(False)
     pcie = None if args.no_pcie else pcie_bench(masker, db, arr, args, torch)
     fastq = None if args.no_fastq else fastq_bench(masker, db, arr, args, torch, rank)
-    totals = db.totals()
+    # the run-only step of round 2 (plan kept from the previous step), for comparison
+    run_only_ms = None
+    if not args.resident:
+        db.replan()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(args.steps):
+            db.run()
+        torch.cuda.synchronize()
+        run_only_ms = (time.perf_counter() - t) / args.steps * 1e3
+    totals = db.totals()     # (also reports any check the runs made: a bad batch raises here)
     batch_info = db.info()
-    irecs = ind.download()
-    indel_info = ind.info()
-    ind.free()
+    if ind is not None:
+        irecs = ind.download()
+        indel_info = ind.info()
+        ind.free()
+    else:
+        irecs = np.zeros(0, native.INDEL_REC)
+        indel_info = {"observations": 0, "emitted": 0, "incidences": 0}
     if dist is not None and host_reduce:
         t_host = torch.from_numpy(totals.copy())
         dist.all_reduce(t_host)
@@ -461,6 +573,10 @@ def main() -> None:
                                   "achieved": round(dom_bytes / (dom_ms * 1e-3) / 1e9, 1),
                                   "traffic": dom_traffic if "k_group" in dom else None,
                                   "frac": round(dom_bytes / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}},
+        "step_kind": "resident batch, plan kept (run only)" if args.resident else
+                     "fresh batch: device plan (replan) + run every step",
+        "run_only_ms_per_step": round(run_only_ms, 4) if run_only_ms else None,
+        "batch_shape": shape,
         "pass": {"kernel_ms": round(pass_ms, 4), "algorithmic_bytes": alg_total,
                  "prep_ms": round(sum(v["avg_ms"] * v["launches"] for n, v in per_kernel.items()
                                       if n in PREP_KERNELS) / args.steps, 4),
@@ -471,6 +587,7 @@ def main() -> None:
                   "masked_calls": int((irecs["kind"] == native.INDEL_CALL).sum()),
                   "support_records": int((irecs["kind"] == native.INDEL_SUPPORT).sum()),
                   "ms_per_step": round(indel_ms, 4)},
+        "e2e": e2e.get("e2e"),
         "pcie_inclusive": pcie,
         "fastq": fastq,
         "totals": {k: int(v) for k, v in zip(native.TOTAL_NAMES, job_totals)},
@@ -479,6 +596,11 @@ def main() -> None:
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(arr, info["reads"])
+        cb = result["cpu_baseline"]
+        fmt_rate = (fastq or {}).get("cpu_host_formatter", {}).get("value")
+        if fmt_rate:   # ref-cpu-1 with FASTQ formatting: mask then format, one core
+            cb["single_core_mask_plus_format"] = round(1.0 / (1.0 / cb["single_core_value"] + 1.0 / fmt_rate), 1)
+        cb["e2e"] = e2e.get("cpu_e2e")
     elif rank == 0:
         result["cpu_baseline"] = None
     if rank == 0:

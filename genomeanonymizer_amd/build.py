@@ -76,7 +76,7 @@ def build_hip(force: bool = False) -> str:
             os.replace(obj + ".tmp", obj)
     if failed:
         raise RuntimeError(f"build failed: {' '.join(failed)}")
-    tmp = HIP_LIB + ".tmp"
+    tmp = f"{HIP_LIB}.{os.getpid()}.tmp"
     _run([_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs)
     os.replace(tmp, HIP_LIB)
     return HIP_LIB
@@ -89,7 +89,7 @@ def build_host(force: bool = False) -> str:
     srcs = [os.path.join(CSRC, s) for s in HOST_SOURCES]
     hdr = os.path.join(REPO, "include", "ganon_host.h")
     if force or _stale(HOST_LIB, srcs + [hdr, __file__]):
-        tmp = HOST_LIB + ".tmp"
+        tmp = f"{HOST_LIB}.{os.getpid()}.tmp"
         _run(["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-fvisibility=hidden", "-pthread",
               "-o", tmp] + srcs + ["-lz"])
         os.replace(tmp, HOST_LIB)
@@ -101,7 +101,7 @@ def build_oracle(force: bool = False) -> str:
     hdr = os.path.join(REPO, "include", "ganon.h")
     os.makedirs(os.path.dirname(ORACLE_LIB), exist_ok=True)
     if force or _stale(ORACLE_LIB, [src, hdr, __file__]):
-        tmp = ORACLE_LIB + ".tmp"
+        tmp = f"{ORACLE_LIB}.{os.getpid()}.tmp"
         _run(["gcc", "-O2", "-std=c11", "-fPIC", "-shared", "-pthread", "-o", tmp, src])
         os.replace(tmp, ORACLE_LIB)
     return ORACLE_LIB

@@ -77,9 +77,22 @@ struct GrpAux {
   unsigned long long *paths;                    // [0] sorted lists, [1] region passes, [2] key-range splits
   unsigned long long *okey, *opay, *tkey;       // overflow regions
   unsigned int *tflag;
+  // the fused one-segment emit (k_group EMIT): the raw arrays each tile's records are built from,
+  // the group table of the batch scan, the incidence checks' outputs
+  const longlong2 *gmeta;
+  int32_t n_groups, n_scopes, n_reads, pad;
+  int64_t n_incid, region_per_incid, n_blk;
+  const int64_t *incid_off, *seq_off, *cig_off, *ref_off;
+  const int32_t *incid_read, *ref_start, *read_len, *n_cig, *write_scope, *read_end, *span_start, *span_len;
+  const uint8_t *dataset;
+  const uint32_t *cigar;
+  const uint64_t *bad;                          // non-ACGT 64-base blocks of the reference
+  unsigned long long *ws_part;                  // [group] write-scope hash sums
+  struct PrepErr *err;
 };
 
-// First error the device validation found (upload only).
+// First error the device validation found: per-read and per-scope checks at plan time, incidence
+// and write-scope checks during the run (reported by ganon_batch_download).
 struct PrepErr {
   int code;         // 0 none, else a PrepErrKind
   int pad;
@@ -90,6 +103,64 @@ enum PrepErrKind {
   kErrReadSeq = 1, kErrReadCigar, kErrReadDataset, kErrReadWriteScope, kErrReadLong, kErrCigarOp, kErrReadPos,
   kErrScopeOff, kErrScopeSpan, kErrScopeRef, kErrScopeKeep, kErrIncidRead, kErrIncidSpan, kErrWriteScopeMissing
 };
+
+// ---- device helpers shared by the prep kernels (ganon_prep.hip) and the group kernel's fused emit
+#ifdef __HIPCC__
+__device__ __forceinline__ void report(PrepErr *err, int kind, long long index, long long a = 0, long long b = 0) {
+  if (atomicCAS(&err->code, 0, kind) == 0) {
+    err->index = index;
+    err->a = a;
+    err->b = b;
+  }
+}
+
+__device__ __forceinline__ bool is_aligned_op(int op) { return op == 0 || op == 7 || op == 8; }
+
+// Aligned runs of a read (M/=/X ops, cut at kSegMaxLen, clipped to the read length): f(q, p, n)
+// with query offset q, contig position p, length n — the host planner's segments_of, round 1.
+template <typename F>
+__device__ __forceinline__ void walk_segments(const uint32_t *__restrict__ cig, int nc, int L, int ref_start, uint32_t w0,
+                                              F &&f) {
+  int q = 0, p = ref_start;
+  for (int k = 0; k < nc && q < L; ++k) {
+    const uint32_t w = k == 0 ? w0 : cig[k];   // (the first word is loaded early by the caller)
+    const int op = (int)(w & 0xF);
+    const int len = (int)(w >> 4);
+    if (is_aligned_op(op)) {
+      const int n = min(len, L - q);
+      for (int o = 0; o < n; o += kSegMaxLen) f(q + o, p + o, min(kSegMaxLen, n - o));
+      q += len;
+      p += len;
+    } else if (op == 1 || op == 4) {
+      q += len;
+    } else if (op == 2 || op == 3) {
+      p += len;
+    }
+  }
+}
+
+// Is the reference range [rnib, rnib + n) free of non-ACGT codes (every 64-base block clean)?
+__device__ __forceinline__ bool ref_clean(const uint64_t *__restrict__ bad, int64_t n_blk, int64_t rnib, int n) {
+  const int64_t k0 = rnib >> 6, k1 = (rnib + n - 1) >> 6;
+  if (k1 >= n_blk) return false;
+  for (int64_t wd = k0 >> 6; wd <= (k1 >> 6); ++wd) {
+    const int lo = wd == (k0 >> 6) ? (int)(k0 & 63) : 0;
+    const int hi = wd == (k1 >> 6) ? (int)(k1 & 63) : 63;
+    const uint64_t mask = (hi == 63 ? ~0ull : ((1ull << (hi + 1)) - 1)) & ~((1ull << lo) - 1);
+    if (bad[wd] & mask) return false;
+  }
+  return true;
+}
+
+
+__device__ __forceinline__ unsigned long long ws_hash(int r) {
+  unsigned long long z = (unsigned long long)(uint32_t)r + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+#endif
 
 // Grow-only device buffer (+128 bytes of padding: the group kernels load up to 68 bytes past a
 // chunk start, the patch atomics touch whole dwords).
@@ -120,18 +191,21 @@ struct ganon_dbatch {
   ganon_dev::DBuf b_ref_start, b_read_len, b_seq_off, b_cig_off, b_n_cig, b_dataset, b_write_scope, b_seq, b_cigar,
       b_incid_off, b_incid_read, b_span_start, b_span_len, b_ref_off, b_keep_pos, b_keep_code;
   // derived layer
+  ganon_dev::DBuf b_part;                                          // k_prep_scan per-block partials
   ganon_dev::DBuf b_nseg, b_scost, b_scan_tmp, b_slots, b_slot0;   // segments per read; long-read mode: group
                                                                   // costs, dirty flags, first slot per incidence
-  ganon_dev::DBuf b_read_end, b_seen, b_cursor, b_gs0, b_lo, b_linemap, b_groups, b_seg4, b_grp_part, b_far, b_gokey, b_gopay, b_gtkey, b_gtflag, b_out,
+  ganon_dev::DBuf b_wspart;                                        // per-group write-scope hash sums
+  ganon_dev::DBuf b_read_end, b_cursor, b_gs0, b_lo, b_linemap, b_groups, b_seg4, b_grp_part, b_far, b_gokey, b_gopay, b_gtkey, b_gtflag, b_out,
       b_scope_calls, b_scope_bases, b_small;   // b_small: totals, static totals, counters, acc, status, errors
   uint8_t *out = nullptr;
   int32_t *scope_calls = nullptr, *scope_bases = nullptr;
   unsigned long long *totals = nullptr, *static_totals = nullptr, *acc = nullptr, *far_count = nullptr;
   int32_t *counters = nullptr;          // [0] rare small (unused), [1] rare tiles
-  int32_t *status = nullptr;            // sticky device error bits (1: far-mask list overflow)
+  int32_t *status = nullptr;            // sticky device error bits (1: far-mask list overflow, 2: write-scope sums)
   ganon_dev::PrepErr *err = nullptr;
-  unsigned long long *plan_info = nullptr;   // [0] far nibbles, [1] huge scopes, [2] written reads, [3] longest read,
-                                             // [4] most segments of one read
+  unsigned long long *plan_info = nullptr;   // [0] I/D ops, [1] huge scopes, [2] written reads, [3] longest read,
+                                             // [4] most segments of one read, [5] short-read groups,
+                                             // [6] write-scope hash sum (k_finish compares)
   unsigned long long *paths = nullptr;       // GrpAux::paths (since upload)
   unsigned long long *cursor = nullptr;      // k_prep_emit allocation counters and their bases (b_cursor)
   ganon_dev::GrpAux *aux = nullptr;
@@ -141,8 +215,14 @@ struct ganon_dbatch {
   // per scope (scost, upload) instead of the CSR offsets, and emitted one wave per incidence
   bool long_mode = false;
   bool flat_mode = false;   // every read has at most one aligned segment: one record per incidence, in place
+  bool fused_emit = false;  // this run's group kernel builds the records itself (flat mode, set by the run)
   int64_t *scost = nullptr;
-  int64_t n_seg = 0, region = 0, far_cap = 0, n_written = 0, region_per_incid = 0;
+  int64_t n_seg = 0, region = 0, far_cap = 0, n_written = 0, region_per_incid = 0, n_id_ops = 0;
+  int64_t max_len = 0, max_seg = 0;         // longest read, most aligned segments of one read (plan)
+  int64_t far_cap_alloc = 0;                 // capacity of b_far (kept across batches, grown on overflow)
+  std::vector<unsigned long long> cursor_h;  // emit sub-counter bases (host copy of an async upload)
+  ganon_dev::GrpAux aux_h{};                 // host copies of the async uploads of a plan
+  unsigned long long static_h[GANON_N_TOTALS] = {0};
   // huge scopes (> kGrpMaxSpan positions): tile path, planned on the host at upload
   std::vector<void *> huge_allocs;
   ganon_dev::Tile *tiles_h = nullptr;
@@ -157,12 +237,18 @@ struct ganon_dbatch {
 
 namespace ganon_prep {
 
-// Validate the raw layer on the device, plan the derived layer (group count, segment count,
-// overflow regions, far-mask capacity) and size its buffers. Synchronous (upload time).
-int plan(ganon_ctx *ctx, ganon_dbatch *db, const int64_t *host_incid_off);
+// Validate the raw layer on the device and plan the derived layer (prep mode, group count, segment
+// count, overflow regions) from it: one scan over the raw arrays and one synchronization (two more
+// in the two-pass and long-read modes). Everything a freshly arrived raw batch needs before its
+// first run (upload, reload, ganon_batch_replan).
+int plan(ganon_ctx *ctx, ganon_dbatch *db);
 // Rebuild every derived array from the raw layer (async on the stream): the first half of
 // every ganon_batch_run.
 int run(ganon_ctx *ctx, ganon_dbatch *db);
+// The write-scope sums disagreed (k_finish status bit 2): find the read (async; then batch_error).
+int ws_diag(ganon_ctx *ctx, ganon_dbatch *db);
+// Synchronize and report the first error the device checks recorded (GANON_E_ARG) or GANON_OK.
+int batch_error(ganon_ctx *ctx, ganon_dbatch *db);
 // Grow-only allocation of count elements of T.
 int grow(ganon_ctx *ctx, ganon_dev::DBuf &b, size_t bytes);
 template <typename T>

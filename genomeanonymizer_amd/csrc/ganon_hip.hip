@@ -311,6 +311,9 @@ constexpr int kGrpThreads = 256;
 #ifndef GANON_K2_BLOCKS
 #define GANON_K2_BLOCKS 6   // resident workgroups per CU the K = 2 instance is compiled for
 #endif
+#ifndef GANON_KE_BLOCKS
+#define GANON_KE_BLOCKS 6   // ... and its fused-emit instance
+#endif
 constexpr int kGrpTile = 256;        // segment records staged per tile
 constexpr int kGrpStack = 80;        // key ranges pending (bisection depth <= 64)
 constexpr int kGrpMap = 4096;        // chunk -> segment map entries (larger tiles binary-search)
@@ -349,6 +352,9 @@ struct GrpSharedT {
   int blk_calls, blk_bases;         // this workgroup's contribution to the totals
   int cnt_calls[kGrpMaxScopes];     // per-scope counts, written out once at the end
   int cnt_bases[kGrpMaxScopes];
+  int off32[kGrpMaxScopes + 1];     // fused emit: the group's scope offsets from its first incidence
+  unsigned long long hsum;          // fused emit: the group's write-scope hash sum
+  uint8_t clean[kGrpTile];          // fused emit: the staged record's reference range is all ACGT
 };
 
 struct GrpRange {
@@ -473,17 +479,83 @@ __device__ __forceinline__ void copy_windows(const uint8_t *__restrict__ src, ui
   }
 }
 
+// Where a fused-emit tile builds its records from (k_group EMIT).
+struct EmitTile {
+  const GrpAux *aux;
+  int64_t i_begin;   // the group's first incidence
+  int s_begin, ns;
+  bool first;        // the group's first pass over its records: the write-scope sums count it
+};
+
+// The fused one-segment emit (flat prep mode; k_prep_emit_flat's record for incidence i, built in
+// the group kernel instead of written to HBM and read back): the incidence checks (read index
+// before any gather through it, the read inside its scope's span), the write-scope hash of a read
+// met in its write scope, its one aligned segment as a record (zero-length: none, a huge scope or
+// a failed check) and whether its reference range is all ACGT (the 2-bit reference).
+__device__ __forceinline__ int4 emit_record(const EmitTile &E, const int *off32, int64_t i, bool &clean,
+                                           unsigned long long *hsum) {
+  const GrpAux *A = E.aux;
+  clean = false;
+  const int rd = gp(A->incid_read)[i];
+  const int j = [&] {   // the staged scope of incidence i (largest j with off32[j] <= i - i_begin)
+    const int x = (int)(i - E.i_begin);
+    int lo = 0, hi = E.ns - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (off32[mid] <= x) lo = mid;
+      else hi = mid - 1;
+    }
+    return lo;
+  }();
+  int4 rec = make_int4(0, 0, 0, j);
+  if (rd < 0 || rd >= A->n_reads) {
+    report(A->err, kErrIncidRead, i, rd);
+    return rec;
+  }
+  const int s = E.s_begin + j;
+  const int64_t co = gp(A->cig_off)[rd];
+  const int nc = gp(A->n_cig)[rd], L = gp(A->read_len)[rd], rs = gp(A->ref_start)[rd], re = gp(A->read_end)[rd];
+  const int64_t so = gp(A->seq_off)[rd];
+  const int ds = gp(A->dataset)[rd], wsc = gp(A->write_scope)[rd];
+  const uint32_t w0 = nc > 0 ? gp(A->cigar)[co] : 0u;
+  const int ss = gp(A->span_start)[s], sl = gp(A->span_len)[s];
+  const int64_t r0 = gp(A->ref_off)[s] - ss;
+  if (rs < ss || re > ss + sl) {
+    report(A->err, kErrIncidSpan, s, rd);
+    return rec;
+  }
+  const bool mine = wsc == s;
+  if (mine && E.first) atomicAdd(hsum, ws_hash(rd));   // (LDS: no register lives across the kernel)
+  if (sl > kGrpMaxSpan) return rec;   // huge scope: the tile path
+  const uint32_t fl = ((uint32_t)ds << 30) | (mine ? kSegMine : 0u);
+  walk_segments(A->cigar + co, nc, L, rs, w0, [&](int q, int p, int n) {
+    const uint64_t sq = (uint64_t)(2 * so + q), rf = (uint64_t)(r0 + p);
+    const uint32_t z = (uint32_t)((sq >> 32) & 0xFF) | ((uint32_t)((rf >> 32) & 0xFF) << 8) | ((uint32_t)n << 16) | fl;
+    rec = make_int4((int)(uint32_t)sq, (int)(uint32_t)rf, (int)z, (int)((uint32_t)j | ((uint32_t)(p - ss) << 12)));
+    clean = ref_clean(A->bad, A->n_blk, (int64_t)rf, n);
+  });
+  return rec;
+}
+
 // Stage records [c0, c0 + nh) in LDS with the exclusive prefix of their chunk counts;
-// returns the tile's chunk total.
-template <class SH>
+// returns the tile's chunk total. EMIT: the records are built from the incidences (emit_record).
+template <bool EMIT, class SH>
 __device__ __forceinline__ int grp_tile(SH &sh, const int4 *__restrict__ rec4, int64_t c0, int nh,
-                                        int chunk) {
+                                        int chunk, const EmitTile &E) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t ix = c0 + (tid < nh ? tid : nh - 1);
-  const int4 r = rec4[ix];
+  int4 r;
+  bool cl = false;
+  if constexpr (EMIT) {
+    r = make_int4(0, 0, 0, 0);
+    if (tid < nh) r = emit_record(E, sh.off32, c0 + tid, cl, &sh.hsum);
+  } else {
+    const int64_t ix = c0 + (tid < nh ? tid : nh - 1);
+    r = rec4[ix];
+  }
   int nck = 0;
   if (tid < nh) {
     sh.rec[tid] = r;
+    if constexpr (EMIT) sh.clean[tid] = cl;
     nck = ((((uint32_t)r.z >> 16) & kSegMaxLen) + chunk - 1) / chunk;
   }
   // wave inclusive scan: DPP row_shr within each 16-lane row, then the row totals (no lane-index
@@ -529,20 +601,14 @@ __device__ __forceinline__ int grp_find(const SH &sh, int nh, int total, int t) 
   return lo;
 }
 
-// Stream every chunk of every segment of the group, feeding observations in range R. A chunk
-// is 16 * K bases: each thread loads the 2K + 1 sequence dwords and 2K + 1 reference dwords
-// covering its chunk at once (one memory round trip per chunk), then takes the K 16-base
-// windows out of registers with static indices.
+// One chunk (16 * K bases) of staged record j: each thread loads the 2K + 1 sequence dwords and
+// the K + 1 (2-bit) or 2K + 1 (nt16) reference dwords covering it at once (one memory round trip
+// per chunk), then takes the K 16-base windows out of registers with static indices.
 template <int K, bool REF2, class SH>
-__device__ __forceinline__ void grp_scan(const GrpBatch &B, SH &sh, const GrpRange &R, const GrpGlobal &gg,
-                                         int64_t i_begin, int64_t i_end, const int4 *__restrict__ rec4, int skip) {
-  const int tid = threadIdx.x;
-  for (int64_t c0 = i_begin; c0 < i_end; c0 += kGrpTile) {
-    const int nh = (int)((i_end - c0) < kGrpTile ? (i_end - c0) : kGrpTile);
-    int total = grp_tile(sh, rec4, c0, nh, 16 * K);
-    if (skip & kSkipChunks) total = 0;
-    for (int t = tid; t < total; t += kGrpThreads) {
-      const int j = grp_find(sh, nh, total, t);
+__device__ __forceinline__ void grp_chunk(const GrpBatch &B, SH &sh, const GrpRange &R, const GrpGlobal &gg, int t,
+                                          int j) {
+  {
+    {
       const int4 r = sh.rec[j];
       const uint32_t rz = (uint32_t)r.z;
       const int L = (int)((rz >> 16) & kSegMaxLen);
@@ -595,6 +661,30 @@ __device__ __forceinline__ void grp_scan(const GrpBatch &B, SH &sh, const GrpRan
           const unsigned long long key = sk | ((unsigned long long)(pos_seg + qi + k) << 4) | (unsigned long long)c;
           grp_observe(sh, R, gg, key, sn + 16 * i + k, rc, ds_, rz >> 31);
         }
+      }
+    }
+  }
+}
+
+// Stream every chunk of every segment of the group, feeding observations in range R. EMIT: the
+// records come from the incidences (grp_tile) and each wave reads the 2-bit reference when every
+// record it meets has an all-ACGT reference range, else the nt16 one.
+template <int K, bool REF2, bool EMIT, class SH>
+__device__ __forceinline__ void grp_scan(const GrpBatch &B, SH &sh, const GrpRange &R, const GrpGlobal &gg,
+                                         int64_t i_begin, int64_t i_end, const int4 *__restrict__ rec4, int skip,
+                                         const EmitTile &E) {
+  const int tid = threadIdx.x;
+  for (int64_t c0 = i_begin; c0 < i_end; c0 += kGrpTile) {
+    const int nh = (int)((i_end - c0) < kGrpTile ? (i_end - c0) : kGrpTile);
+    int total = grp_tile<EMIT>(sh, rec4, c0, nh, 16 * K, E);
+    if (skip & kSkipChunks) total = 0;
+    for (int t = tid; t < total; t += kGrpThreads) {
+      const int j = grp_find(sh, nh, total, t);
+      if constexpr (EMIT) {
+        if (B.ref2 && __all(sh.clean[j])) grp_chunk<K, true>(B, sh, R, gg, t, j);
+        else grp_chunk<K, false>(B, sh, R, gg, t, j);
+      } else {
+        grp_chunk<K, REF2>(B, sh, R, gg, t, j);
       }
     }
     __syncthreads();
@@ -826,21 +916,48 @@ __device__ __forceinline__ void grp_patch_bytes(const GrpBatch &B, SH &sh, int n
 // {seg_end lo, hi, seg_mid lo, hi}, {partition piece A begin lo, hi, end lo, hi} (bytes; fused
 // only), {global region offset lo, hi, capacity, 0}, {piece B begin lo, hi, end lo, hi};
 // segments [seg_begin, seg_mid) have an all-ACGT reference range (2-bit reference).
-template <int U, bool FUSED, int OBS>
-__global__ void __launch_bounds__(kGrpThreads, (OBS > 512 ? 4 : U == 1 ? 6 : U == 2 ? GANON_K2_BLOCKS : U == 4 ? 5 : 4)) k_group(const GrpBatch B, const int4 *__restrict__ groups,
+// EMIT (one-segment prep mode): the group's scopes and incidences come from the batch scan's group
+// table, its overflow region in closed form, its records from its incidences (emit_record): the
+// prep's emit kernel and its 16-byte records in HBM are gone; the write-scope hash sum of the
+// group is written at the end.
+template <int U, bool FUSED, int OBS, bool EMIT = false>
+__global__ void __launch_bounds__(kGrpThreads, (OBS > 512 ? 4 : U == 1 ? 6 : U == 2 ? (EMIT ? GANON_KE_BLOCKS : GANON_K2_BLOCKS) : U == 4 ? 5 : 4)) k_group(const GrpBatch B, const int4 *__restrict__ groups,
                                                        const int4 *__restrict__ rec4,
                                                        uint8_t *__restrict__ out, const GrpAux *__restrict__ aux,
                                                        int skip, int nt_copy) {
   __shared__ GrpSharedT<OBS> sh;
   const int tid = threadIdx.x;
-  const int4 g0 = groups[kGrpRec * blockIdx.x];
-  const int4 g1 = groups[kGrpRec * blockIdx.x + 1];
   const int4 g2 = groups[kGrpRec * blockIdx.x + 2];
-  const int4 g3 = groups[kGrpRec * blockIdx.x + 3];
   const int4 g4 = groups[kGrpRec * blockIdx.x + 4];
-  const GrpGlobal gg{aux, i64_of(g3.x, g3.y), g3.z};
-  const int s_begin = g0.x, s_end = g0.y;
-  const int64_t i_begin = i64_of(g0.z, g0.w), i_end = i64_of(g1.x, g1.y), i_mid = i64_of(g1.z, g1.w);
+  int s_begin, s_end;
+  int64_t i_begin, i_end, i_mid;
+  GrpGlobal gg;
+  if constexpr (EMIT) {
+    const int g = (int)blockIdx.x;
+    const longlong2 m0 = aux->gmeta[g];
+    const longlong2 m1 = g + 1 < aux->n_groups ? aux->gmeta[g + 1] : make_longlong2(aux->n_scopes, aux->n_incid);
+    s_begin = (int)m0.x;
+    s_end = (int)m1.x;
+    i_begin = m0.y;
+    i_end = m1.y;
+    i_mid = i_end;
+    const int64_t rpi = aux->region_per_incid;
+    gg = GrpGlobal{aux, i_begin * rpi + (int64_t)kGrpObs * g,
+                   (int)min((i_end - i_begin) * rpi + kGrpObs, (long long)(INT32_MAX / 2))};
+    for (int t = tid; t <= s_end - s_begin; t += kGrpThreads)
+      sh.off32[t] = (int)(gp(aux->incid_off)[s_begin + t] - i_begin);
+  } else {
+    const int4 g0 = groups[kGrpRec * blockIdx.x];
+    const int4 g1 = groups[kGrpRec * blockIdx.x + 1];
+    const int4 g3 = groups[kGrpRec * blockIdx.x + 3];
+    gg = GrpGlobal{aux, i64_of(g3.x, g3.y), g3.z};
+    s_begin = g0.x;
+    s_end = g0.y;
+    i_begin = i64_of(g0.z, g0.w);
+    i_end = i64_of(g1.x, g1.y);
+    i_mid = i64_of(g1.z, g1.w);
+  }
+  const EmitTile E{aux, i_begin, s_begin, s_end - s_begin, true};
   const PatchSink sink{out, i64_of(g2.x, g2.y), i64_of(g2.z, g2.w), i64_of(g4.x, g4.y), i64_of(g4.z, g4.w),
                        aux, FUSED, FUSED};
   // the partition pieces, whole 16-byte windows (the buffers are padded past seq_bytes); the
@@ -853,6 +970,7 @@ __global__ void __launch_bounds__(kGrpThreads, (OBS > 512 ? 4 : U == 1 ? 6 : U =
   }
   if (tid == 0) {
     sh.top = 0;
+    sh.hsum = 0ull;
     sh.stk_lo[0] = 0ull;
     sh.stk_hi[0] = ~0ull;
     sh.stk_mode[0] = kModeCollect;
@@ -864,6 +982,7 @@ __global__ void __launch_bounds__(kGrpThreads, (OBS > 512 ? 4 : U == 1 ? 6 : U =
     sh.cnt_calls[i] = 0;
     sh.cnt_bases[i] = 0;
   }
+  bool first_pass = true;   // (the first key range is the whole one: every record once)
   for (;;) {
     __syncthreads();
     const int top = sh.top;
@@ -879,6 +998,8 @@ __global__ void __launch_bounds__(kGrpThreads, (OBS > 512 ? 4 : U == 1 ? 6 : U =
         gp(aux->part)[2 * blockIdx.x] = sh.blk_calls;
         gp(aux->part)[2 * blockIdx.x + 1] = sh.blk_bases;
       }
+      if constexpr (EMIT)   // the group's write-scope hash sum (k_finish compares the batch's)
+        if (tid == 0) gp(aux->ws_part)[blockIdx.x] = sh.hsum;
       break;
     }
     const GrpRange R{sh.stk_lo[top], sh.stk_hi[top], sh.stk_mode[top]};
@@ -890,12 +1011,16 @@ __global__ void __launch_bounds__(kGrpThreads, (OBS > 512 ? 4 : U == 1 ? 6 : U =
       sh.kmax = 0ull;
     }
     __syncthreads();
-    if (B.ref2) {
-      grp_scan<U, true>(B, sh, R, gg, i_begin, i_mid, rec4, skip);
-      grp_scan<U, false>(B, sh, R, gg, i_mid, i_end, rec4, skip);
+    if constexpr (EMIT) {
+      const EmitTile Ep{E.aux, E.i_begin, E.s_begin, E.ns, first_pass};
+      grp_scan<U, false, true>(B, sh, R, gg, i_begin, i_end, rec4, skip, Ep);
+    } else if (B.ref2) {
+      grp_scan<U, true, false>(B, sh, R, gg, i_begin, i_mid, rec4, skip, E);
+      grp_scan<U, false, false>(B, sh, R, gg, i_mid, i_end, rec4, skip, E);
     } else {
-      grp_scan<U, false>(B, sh, R, gg, i_begin, i_end, rec4, skip);
+      grp_scan<U, false, false>(B, sh, R, gg, i_begin, i_end, rec4, skip, E);
     }
+    first_pass = false;
     // (grp_scan ends on a barrier)
     if (skip & kSkipClassify) continue;
     const int n = sh.n_obs;
@@ -971,7 +1096,9 @@ __global__ void __launch_bounds__(kBlock) k_finish(const unsigned long long *__r
                                                    const unsigned long long *__restrict__ static_totals,
                                                    int32_t *counters, unsigned long long *far_count,
                                                    int32_t *status, unsigned long long *acc,
-                                                   unsigned long long *totals) {
+                                                   unsigned long long *totals,
+                                                   const unsigned long long *__restrict__ ws_part,
+                                                   const unsigned long long *__restrict__ ws_expect) {
   const int64_t gtid = blockIdx.x * (int64_t)kBlock + threadIdx.x, gstride = (int64_t)gridDim.x * kBlock;
   const unsigned long long far_n = *far_count;
   const int64_t n_far = far_n < (unsigned long long)far_cap ? (int64_t)far_n : far_cap;
@@ -983,33 +1110,40 @@ __global__ void __launch_bounds__(kBlock) k_finish(const unsigned long long *__r
     atomicXor(reinterpret_cast<uint32_t *>(out) + (byte >> 2), (uint32_t)(e & 15) << sh);
   }
   long long c = 0, b = 0;
+  unsigned long long h = 0;   // write-scope hash sums of the emit paths (one per group)
   for (int64_t i = gtid; i < n_groups; i += gstride) {
     c += grp_part[2 * i];
     b += grp_part[2 * i + 1];
+    h += ws_part[i];
   }
   for (int64_t i = gtid; i < n_large; i += gstride) {
     c += scope_calls[large_ids[i]];
     b += scope_bases[large_ids[i]];
   }
-  __shared__ long long part[2][kWaves];
+  __shared__ long long part[3][kWaves];
   __shared__ int last;
   for (int o = 32; o > 0; o >>= 1) {
     c += __shfl_xor(c, o);
     b += __shfl_xor(b, o);
+    h += __shfl_xor(h, o);
   }
   if ((threadIdx.x & 63) == 0) {
     part[0][threadIdx.x >> 6] = c;
     part[1][threadIdx.x >> 6] = b;
+    part[2][threadIdx.x >> 6] = (long long)h;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
     c = b = 0;
+    h = 0;
     for (int w = 0; w < kWaves; ++w) {
       c += part[0][w];
       b += part[1][w];
+      h += (unsigned long long)part[2][w];
     }
     if (c) atomicAdd(&acc[0], (unsigned long long)c);
     if (b) atomicAdd(&acc[1], (unsigned long long)b);
+    if (h) atomicAdd(&acc[4], h);
     __threadfence();
     last = atomicAdd(&acc[2], 1ull) == gridDim.x - 1;
   }
@@ -1018,13 +1152,19 @@ __global__ void __launch_bounds__(kBlock) k_finish(const unsigned long long *__r
   __threadfence();
   const unsigned long long sc = atomicExch(&acc[0], 0ull), sb = atomicExch(&acc[1], 0ull);
   atomicExch(&acc[2], 0ull);
+  // every written read met once in its write scope (k_prep_scan's sum vs the emit paths')
+  if (atomicExch(&acc[4], 0ull) != *ws_expect) atomicOr(status, 2);
   for (int k = 0; k < GANON_N_TOTALS; ++k) totals[k] = static_totals[k];
   totals[GANON_T_MASKED_SNV_CALLS] += sc;
   totals[GANON_T_MASKED_BASES] += sb;
   totals[GANON_T_RARE_SCOPES] += (unsigned long long)(atomicExch(&counters[0], 0) + atomicExch(&counters[1], 0));
-  // more far masks than the planned capacity (cannot happen for a batch planned at upload): the
-  // masks past it were dropped — download reports the run as failed instead of unmasked bases
-  if (atomicExch(far_count, 0ull) > (unsigned long long)far_cap) atomicOr(status, 1);
+  // more far masks than the list holds: the masks past it were dropped — ganon_batch_download grows
+  // the list to the count kept in acc[3] and runs the batch again
+  const unsigned long long n_far_all = atomicExch(far_count, 0ull);
+  if (n_far_all > (unsigned long long)far_cap) {
+    atomicOr(status, 1);
+    atomicMax(&acc[3], n_far_all);
+  }
 }
 // One workgroup per 16 Ki-position tile of a large scope: tally -> TN table (global).
 template <int TB>
@@ -1130,6 +1270,8 @@ using ganon_detail::KernelScope;
 
 namespace {
 
+constexpr int64_t kFarMaxEntries = int64_t(1) << 30;   // far-mask list entries at most (8 GiB)
+
 size_t tile_lds_bytes(int tb) { return (size_t)kTile * tb + kTile / 2 + 16 * sizeof(int); }
 
 void free_buf(DBuf &b) {
@@ -1160,9 +1302,10 @@ void free_batch(ganon_dbatch *db) {
   DBuf *bufs[] = {&db->b_ref_start, &db->b_read_len, &db->b_seq_off, &db->b_cig_off, &db->b_n_cig, &db->b_dataset,
                   &db->b_write_scope, &db->b_seq, &db->b_cigar, &db->b_incid_off, &db->b_incid_read,
                   &db->b_span_start, &db->b_span_len, &db->b_ref_off, &db->b_keep_pos, &db->b_keep_code,
-                  &db->b_read_end, &db->b_seen, &db->b_cursor, &db->b_gs0, &db->b_lo, &db->b_linemap, &db->b_groups,
+                  &db->b_read_end, &db->b_wspart, &db->b_cursor, &db->b_gs0, &db->b_lo, &db->b_linemap, &db->b_groups,
                   &db->b_seg4, &db->b_grp_part, &db->b_far, &db->b_gokey, &db->b_gopay, &db->b_gtkey, &db->b_gtflag,
-                  &db->b_out, &db->b_scope_calls, &db->b_scope_bases, &db->b_small};
+                  &db->b_out, &db->b_scope_calls, &db->b_scope_bases, &db->b_small, &db->b_part, &db->b_nseg,
+                  &db->b_scost, &db->b_scan_tmp, &db->b_slots, &db->b_slot0};
   for (DBuf *b : bufs) free_buf(*b);
   free_huge(db);
   free_ref(db->own_ref);
@@ -1308,6 +1451,119 @@ int plan_huge(ganon_ctx *ctx, ganon_dbatch *db, const ganon_batch *b) {
   return GANON_OK;
 }
 
+// Host copies of the arrays plan_huge reads, for a batch planned from its device arrays alone
+// (ganon_batch_replan of a batch with scopes wider than the group kernels': rare).
+struct HostCopy {
+  std::vector<int32_t> ref_start, n_cig, write_scope, incid_read, span_start, span_len;
+  std::vector<int64_t> cig_off, incid_off;
+  std::vector<uint32_t> cigar;
+  ganon_batch b{};
+};
+
+template <typename T>
+int d2h_vec(ganon_ctx *ctx, std::vector<T> &v, const T *src, size_t n) {
+  v.resize(n);
+  if (n) HIP_OR_FAIL(hipMemcpyAsync(v.data(), src, n * sizeof(T), hipMemcpyDeviceToHost, ctx->stream));
+  return GANON_OK;
+}
+
+int host_copy(ganon_ctx *ctx, const ganon_dbatch *db, HostCopy &h) {
+  const DevBatch &B = db->B;
+  int rc;
+  if ((rc = d2h_vec(ctx, h.ref_start, B.ref_start, (size_t)db->n_reads)) ||
+      (rc = d2h_vec(ctx, h.n_cig, B.n_cig, (size_t)db->n_reads)) ||
+      (rc = d2h_vec(ctx, h.write_scope, B.write_scope, (size_t)db->n_reads)) ||
+      (rc = d2h_vec(ctx, h.cig_off, B.cig_off, (size_t)db->n_reads)) ||
+      (rc = d2h_vec(ctx, h.cigar, B.cigar, (size_t)db->n_cigar_ops)) ||
+      (rc = d2h_vec(ctx, h.incid_off, B.incid_off, (size_t)db->n_scopes + 1)) ||
+      (rc = d2h_vec(ctx, h.incid_read, B.incid_read, (size_t)db->n_incid)) ||
+      (rc = d2h_vec(ctx, h.span_start, B.span_start, (size_t)db->n_scopes)) ||
+      (rc = d2h_vec(ctx, h.span_len, B.span_len, (size_t)db->n_scopes)))
+    return rc;
+  HIP_OR_FAIL(hipStreamSynchronize(ctx->stream));
+  ganon_batch &b = h.b;
+  b.n_reads = db->n_reads;
+  b.n_scopes = db->n_scopes;
+  b.n_incid = db->n_incid;
+  b.n_cigar_ops = db->n_cigar_ops;
+  b.ref_start = h.ref_start.data();
+  b.n_cig = h.n_cig.data();
+  b.write_scope = h.write_scope.data();
+  b.cig_off = h.cig_off.data();
+  b.cigar = h.cigar.data();
+  b.scope_incid_off = h.incid_off.data();
+  b.incid_read = h.incid_read.data();
+  b.scope_span_start = h.span_start.data();
+  b.scope_span_len = h.span_len.data();
+  return GANON_OK;
+}
+
+// Plan a batch whose raw arrays are on the device (ganon_prep::plan: validation, prep mode, sizes),
+// the huge-scope tiles (from `host`, or host copies), and upload the group kernels' aux pointers
+// and the static totals (async).
+int prepare(ganon_ctx *ctx, ganon_dbatch *db, const ganon_batch *host) {
+  int rc;
+  HIP_OR_FAIL(hipMemsetAsync(db->status, 0, sizeof(int32_t), ctx->stream));
+  HIP_OR_FAIL(hipMemsetAsync(db->acc + 3, 0, sizeof(unsigned long long), ctx->stream));
+  if ((rc = ganon_prep::plan(ctx, db))) return rc;
+  if (db->n_huge_scopes && !host) {
+    HostCopy h;
+    if ((rc = host_copy(ctx, db, h)) || (rc = plan_huge(ctx, db, &h.b))) return rc;
+  } else if ((rc = plan_huge(ctx, db, host))) {
+    return rc;
+  }
+  GrpAux &a = db->aux_h;
+  a = GrpAux{};
+  a.scope_calls = db->scope_calls;
+  a.scope_bases = db->scope_bases;
+  a.part = static_cast<int32_t *>(db->b_grp_part.p);
+  a.far = static_cast<unsigned long long *>(db->b_far.p);
+  a.far_count = db->far_count;
+  a.far_cap = db->far_cap;
+  a.paths = db->paths;
+  a.okey = static_cast<unsigned long long *>(db->b_gokey.p);
+  a.opay = static_cast<unsigned long long *>(db->b_gopay.p);
+  a.tkey = static_cast<unsigned long long *>(db->b_gtkey.p);
+  a.tflag = static_cast<unsigned int *>(db->b_gtflag.p);
+  // the fused one-segment emit
+  const DevBatch &B = db->B;
+  a.gmeta = static_cast<const longlong2 *>(db->b_gs0.p);
+  a.n_groups = db->n_groups;
+  a.n_scopes = db->n_scopes;
+  a.n_reads = db->n_reads;
+  a.n_incid = db->n_incid;
+  a.region_per_incid = db->region_per_incid;
+  a.n_blk = db->ref->n_blk;
+  a.incid_off = B.incid_off;
+  a.seq_off = B.seq_off;
+  a.cig_off = B.cig_off;
+  a.ref_off = B.ref_off;
+  a.incid_read = B.incid_read;
+  a.ref_start = B.ref_start;
+  a.read_len = B.read_len;
+  a.n_cig = B.n_cig;
+  a.write_scope = B.write_scope;
+  a.read_end = B.read_end;
+  a.span_start = B.span_start;
+  a.span_len = B.span_len;
+  a.dataset = B.dataset;
+  a.cigar = B.cigar;
+  a.bad = db->ref->bad;
+  a.ws_part = static_cast<unsigned long long *>(db->b_wspart.p);
+  a.err = db->err;
+  unsigned long long *st = db->static_h;
+  std::fill(st, st + GANON_N_TOTALS, 0ull);
+  st[GANON_T_READS_IN] = (unsigned long long)db->n_reads;
+  st[GANON_T_READS_WRITTEN] = (unsigned long long)db->n_written;
+  st[GANON_T_SCOPES] = (unsigned long long)db->n_scopes;
+  st[GANON_T_LARGE_TILES] = (unsigned long long)db->n_tiles_h;
+  // (from db-resident host copies: the next plan of db synchronizes before it rewrites them)
+  HIP_OR_FAIL(hipMemcpyAsync(db->aux, &db->aux_h, sizeof db->aux_h, hipMemcpyHostToDevice, ctx->stream));
+  HIP_OR_FAIL(hipMemcpyAsync(db->static_totals, st, GANON_N_TOTALS * sizeof(unsigned long long), hipMemcpyHostToDevice,
+                             ctx->stream));
+  return GANON_OK;
+}
+
 // Copy a host batch into db (grow-only buffers), validate and plan it on the device.
 int load_batch(ganon_ctx *ctx, ganon_dbatch *db, const ganon_batch *b, const ganon_ref *shared) {
   if (b->n_reads < 0 || b->n_scopes < 0 || b->n_incid < 0 || b->seq_bytes < 0 || b->n_cigar_ops < 0 || b->ref_bytes < 0)
@@ -1366,17 +1622,17 @@ int load_batch(ganon_ctx *ctx, ganon_dbatch *db, const ganon_batch *b, const gan
   D.ref2 = db->ref->ref2;
   // small device state: totals, static totals, acc, far count, plan info (u64); counters, status;
   // the first validation error; the group kernels' aux pointers
-  constexpr size_t kU64 = 8 + 8 + 4 + 1 + 6 + 4;
+  constexpr size_t kU64 = 8 + 8 + 5 + 1 + 8 + 4;
   constexpr size_t kSmallBytes = kU64 * 8 + 8 * 4 + sizeof(PrepErr) + sizeof(GrpAux) + 64;
   uint8_t *sm = nullptr;
   if ((rc = ganon_prep::grow_n(ctx, db->b_small, kSmallBytes, &sm))) return rc;
   auto *u = reinterpret_cast<unsigned long long *>(sm);
   db->totals = u;
   db->static_totals = u + 8;
-  db->acc = u + 16;
-  db->far_count = u + 20;
-  db->plan_info = u + 21;
-  db->paths = u + 27;
+  db->acc = u + 16;        // [0] calls, [1] bases, [2] ticket, [3] far masks needed, [4] write-scope sum
+  db->far_count = u + 21;
+  db->plan_info = u + 22;
+  db->paths = u + 30;
   db->counters = reinterpret_cast<int32_t *>(u + kU64);
   db->status = db->counters + 4;
   db->err = reinterpret_cast<PrepErr *>(sm + kU64 * 8 + 8 * 4);
@@ -1388,28 +1644,7 @@ int load_batch(ganon_ctx *ctx, ganon_dbatch *db, const ganon_batch *b, const gan
     return rc;
   // bytes outside every read are never written by the masking kernels: make them defined
   HIP_OR_FAIL(hipMemsetAsync(db->out, 0, (size_t)b->seq_bytes + 16, ctx->stream));
-  if ((rc = ganon_prep::plan(ctx, db, b->scope_incid_off))) return rc;
-
-  if ((rc = plan_huge(ctx, db, b))) return rc;
-  const GrpAux a{db->scope_calls,
-                 db->scope_bases,
-                 static_cast<int32_t *>(db->b_grp_part.p),
-                 static_cast<unsigned long long *>(db->b_far.p),
-                 db->far_count,
-                 db->far_cap,
-                 db->paths,
-                 static_cast<unsigned long long *>(db->b_gokey.p),
-                 static_cast<unsigned long long *>(db->b_gopay.p),
-                 static_cast<unsigned long long *>(db->b_gtkey.p),
-                 static_cast<unsigned int *>(db->b_gtflag.p)};
-  unsigned long long st[GANON_N_TOTALS] = {0};
-  st[GANON_T_READS_IN] = (unsigned long long)b->n_reads;
-  st[GANON_T_READS_WRITTEN] = (unsigned long long)db->n_written;
-  st[GANON_T_SCOPES] = (unsigned long long)b->n_scopes;
-  st[GANON_T_LARGE_TILES] = (unsigned long long)db->n_tiles_h;
-  // (both from stack memory: synchronized below before returning)
-  HIP_OR_FAIL(hipMemcpyAsync(db->aux, &a, sizeof a, hipMemcpyHostToDevice, ctx->stream));
-  HIP_OR_FAIL(hipMemcpyAsync(db->static_totals, st, sizeof st, hipMemcpyHostToDevice, ctx->stream));
+  if ((rc = prepare(ctx, db, b))) return rc;
   HIP_OR_FAIL(hipStreamSynchronize(ctx->stream));
   return GANON_OK;
 }
@@ -1548,6 +1783,15 @@ GANON_API int ganon_ctx_set_param(ganon_ctx *ctx, int param, int value) {
     ctx->nt_copy = value != 0;
     return GANON_OK;
   }
+  if (param == GANON_PARAM_FUSE_EMIT) {
+    ctx->fuse_emit = value != 0;
+    return GANON_OK;
+  }
+  if (param == GANON_PARAM_FAR_INIT) {
+    if (value < 0) return fail(ctx, GANON_E_ARG, "far-mask list capacity must be >= 0");
+    ctx->far_init = value;
+    return GANON_OK;
+  }
   if (param == GANON_PARAM_GROUP_SKIP) {
     ctx->group_skip = value & (kSkipClassify | kSkipChunks | kSkipCopy | kSkipCounts);
     return GANON_OK;
@@ -1599,18 +1843,46 @@ GANON_API int ganon_batch_reload(ganon_ctx *ctx, ganon_dbatch *db, const ganon_b
   return rc;
 }
 
-GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
-  if (!ctx || !db) return fail(ctx, GANON_E_ARG, "null argument");
-  HIP_OR_FAIL(hipSetDevice(ctx->device));
+namespace {
+// A new profiled step: the event pairs of the previous one go back to the pool.
+void new_step(ganon_ctx *ctx) {
   for (auto &r : ctx->recs) {
     ctx->pool.push_back(r.e0);
     ctx->pool.push_back(r.e1);
   }
   ctx->recs.clear();
+}
+}  // namespace
+
+GANON_API int ganon_batch_replan(ganon_ctx *ctx, ganon_dbatch *db) {
+  if (!ctx || !db) return fail(ctx, GANON_E_ARG, "null argument");
+  if (!db->b_small.p) return fail(ctx, GANON_E_STATE, "replan of a batch that was never loaded");
+  HIP_OR_FAIL(hipSetDevice(ctx->device));
+  new_step(ctx);
+  ctx->step_open = true;   // the next run's kernels join this step's timings
+  int rc = prepare(ctx, db, nullptr);
+  if (rc) {
+    db->n_groups = 0;
+    db->ran = false;
+  }
+  return rc;
+}
+
+GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
+  if (!ctx || !db) return fail(ctx, GANON_E_ARG, "null argument");
+  HIP_OR_FAIL(hipSetDevice(ctx->device));
+  if (!ctx->step_open) new_step(ctx);
+  ctx->step_open = false;
   hipStream_t st = ctx->stream;
   DevBatch B = db->B;
   if (!ctx->ref2) B.ref2 = nullptr;   // group kernels then read the nt16 reference only
   int rc;
+  // 16-base chunks per thread: long reads (short segments between indels) waste less with one
+  // (profiles/r02/sweep_c5.jsonl); short reads run best with two (sweep_c3.jsonl)
+  const int u = ctx->group_unroll ? ctx->group_unroll : db->long_mode ? 1 : 2;
+  // one-segment prep mode: the group kernel builds its records from the incidences (no emit kernel,
+  // no records in HBM); GANON_PARAM_FUSE_EMIT 0 keeps the separate emit for A/B
+  db->fused_emit = db->flat_mode && u == 2 && ctx->fuse_emit;
   // 1. derived layer from the raw SoA
   if ((rc = ganon_prep::run(ctx, db))) return rc;
   if (db->n_huge_scopes) {
@@ -1621,13 +1893,11 @@ GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
   // 2. masking: the fused group kernel writes every byte of out (its pieces tile [0, seq_bytes))
   if (db->n_groups) {
     KernelScope ks(ctx, "k_group_fused");
-    // 16-base chunks per thread: long reads (short segments between indels) waste less with one
-    // (profiles/r02/sweep_c5.jsonl); short reads run best with two (sweep_c3.jsonl)
-    const int u = ctx->group_unroll ? ctx->group_unroll : db->long_mode ? 1 : 2;
     // 512 unless forced: the 1024-entry list (4 workgroups per CU instead of 6) measured slower on
     // c3 too (3.19 vs 2.84 ms, profiles/r02/sweep_c3_obs.jsonl) — occupancy outweighs the region path
     const int obs = ctx->group_obs ? ctx->group_obs : 512;
-    auto kern = obs == 1024 ? (u == 1 ? k_group<1, true, 1024> : k_group<2, true, 1024>)
+    auto kern = db->fused_emit ? (obs == 1024 ? k_group<2, true, 1024, true> : k_group<2, true, 512, true>)
+                : obs == 1024 ? (u == 1 ? k_group<1, true, 1024> : k_group<2, true, 1024>)
                             : u == 2 ? k_group<2, true, 512> : u == 4 ? k_group<4, true, 512>
                             : u == 8 ? k_group<8, true, 512> : k_group<1, true, 512>;
     const GrpBatch GB{B.seq, B.ref, B.keep_code, B.ref2, B.keep_pos, B.span_start, B.span_len};
@@ -1670,7 +1940,8 @@ GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
     k_finish<<<64, kBlock, 0, st>>>(static_cast<const unsigned long long *>(db->b_far.p), db->n_groups ? db->far_cap : 0,
                                     db->out, static_cast<const int32_t *>(db->b_grp_part.p), db->n_groups,
                                     db->large_ids, db->n_huge_scopes, db->scope_calls, db->scope_bases,
-                                    db->static_totals, db->counters, db->far_count, db->status, db->acc, db->totals);
+                                    db->static_totals, db->counters, db->far_count, db->status, db->acc, db->totals,
+                                    static_cast<const unsigned long long *>(db->b_wspart.p), db->plan_info + 6);
     if ((rc = check_launch(ctx, "k_finish"))) return rc;
   }
   db->ran = true;
@@ -1715,8 +1986,40 @@ GANON_API int ganon_batch_download(ganon_ctx *ctx, ganon_dbatch *db, uint8_t *se
   if (!db->ran) return fail(ctx, GANON_E_STATE, "download before run");
   HIP_OR_FAIL(hipSetDevice(ctx->device));
   hipStream_t st = ctx->stream;
+  int rc;
+  // the checks made during the run (incidences, write scopes)
+  if ((rc = ganon_prep::batch_error(ctx, db))) return rc;
   int32_t status = 0;
+  unsigned long long far_need = 0;
   HIP_OR_FAIL(hipMemcpyAsync(&status, db->status, sizeof status, hipMemcpyDeviceToHost, st));
+  HIP_OR_FAIL(hipMemcpyAsync(&far_need, db->acc + 3, sizeof far_need, hipMemcpyDeviceToHost, st));
+  HIP_OR_FAIL(hipStreamSynchronize(st));
+  if (status & 2) {
+    // a written read its write scope does not list (or lists twice): name it
+    if ((rc = ganon_prep::ws_diag(ctx, db)) || (rc = ganon_prep::batch_error(ctx, db))) return rc;
+    return fail(ctx, GANON_E_ARG, "a written read is not listed exactly once by its write scope");
+  }
+  if (status & 1) {
+    // the far-mask list overflowed: grow it to the count the run needed and run again (the list
+    // keeps its capacity for later batches)
+    if ((int64_t)far_need > kFarMaxEntries)
+      return fail(ctx, GANON_E_NOMEM, "far-mask list: %llu entries needed (max %lld)", far_need, (long long)kFarMaxEntries);
+    unsigned long long *far = nullptr;
+    const int64_t cap = std::min<int64_t>(kFarMaxEntries, (int64_t)far_need + (int64_t)far_need / 4 + 1024);
+    if ((rc = ganon_prep::grow_n(ctx, db->b_far, (size_t)cap, &far))) return rc;
+    db->far_cap = db->far_cap_alloc = cap;
+    db->aux_h.far = far;
+    db->aux_h.far_cap = cap;
+    HIP_OR_FAIL(hipMemcpyAsync(db->aux, &db->aux_h, sizeof db->aux_h, hipMemcpyHostToDevice, st));
+    HIP_OR_FAIL(hipMemsetAsync(db->status, 0, sizeof(int32_t), st));
+    HIP_OR_FAIL(hipMemsetAsync(db->acc + 3, 0, sizeof(unsigned long long), st));
+    const bool prof = ctx->profiling;
+    ctx->profiling = false;
+    rc = ganon_batch_run(ctx, db);
+    ctx->profiling = prof;
+    if (rc) return rc;
+    HIP_OR_FAIL(hipMemcpyAsync(&status, db->status, sizeof status, hipMemcpyDeviceToHost, st));
+  }
   if (seq_out && db->seq_bytes)
     HIP_OR_FAIL(hipMemcpyAsync(seq_out, db->out, (size_t)db->seq_bytes, hipMemcpyDeviceToHost, st));
   if (scope_calls_out && db->n_scopes)
@@ -1726,7 +2029,7 @@ GANON_API int ganon_batch_download(ganon_ctx *ctx, ganon_dbatch *db, uint8_t *se
   if (totals_out)
     HIP_OR_FAIL(hipMemcpyAsync(totals_out, db->totals, GANON_N_TOTALS * 8, hipMemcpyDeviceToHost, st));
   HIP_OR_FAIL(hipStreamSynchronize(st));
-  if (status & 1) return fail(ctx, GANON_E_STATE, "far-mask list overflowed its planned capacity: output invalid");
+  if (status & 1) return fail(ctx, GANON_E_STATE, "far-mask list overflowed after growing: output invalid");
   return GANON_OK;
 }
 
@@ -1773,6 +2076,15 @@ GANON_API int ganon_batch_info(ganon_dbatch *db, int64_t *info) {
   info[5] = db->n_large_written_h;
   info[6] = db->region;
   info[7] = db->n_written;
+  return GANON_OK;
+}
+
+GANON_API int ganon_batch_shape(ganon_dbatch *db, int64_t *shape) {
+  if (!db || !shape) return GANON_E_ARG;
+  shape[0] = db->n_id_ops;
+  shape[1] = db->max_len;
+  shape[2] = db->max_seg;
+  shape[3] = db->long_mode ? 1 : db->flat_mode ? 2 : 0;
   return GANON_OK;
 }
 

@@ -74,52 +74,6 @@ struct Raw {
   int64_t n_incid, seq_bytes, n_cigar_ops, ref_nibs;
 };
 
-__device__ __forceinline__ void report(PrepErr *err, int kind, long long index, long long a = 0, long long b = 0) {
-  if (atomicCAS(&err->code, 0, kind) == 0) {
-    err->index = index;
-    err->a = a;
-    err->b = b;
-  }
-}
-
-__device__ __forceinline__ bool is_aligned_op(int op) { return op == 0 || op == 7 || op == 8; }
-
-// Aligned runs of a read (M/=/X ops, cut at kSegMaxLen, clipped to the read length): f(q, p, n)
-// with query offset q, contig position p, length n — the host planner's segments_of, round 1.
-template <typename F>
-__device__ __forceinline__ void walk_segments(const uint32_t *__restrict__ cig, int nc, int L, int ref_start, uint32_t w0,
-                                              F &&f) {
-  int q = 0, p = ref_start;
-  for (int k = 0; k < nc && q < L; ++k) {
-    const uint32_t w = k == 0 ? w0 : cig[k];   // (the first word is loaded early by the caller)
-    const int op = (int)(w & 0xF);
-    const int len = (int)(w >> 4);
-    if (is_aligned_op(op)) {
-      const int n = min(len, L - q);
-      for (int o = 0; o < n; o += kSegMaxLen) f(q + o, p + o, min(kSegMaxLen, n - o));
-      q += len;
-      p += len;
-    } else if (op == 1 || op == 4) {
-      q += len;
-    } else if (op == 2 || op == 3) {
-      p += len;
-    }
-  }
-}
-
-// Is the reference range [rnib, rnib + n) free of non-ACGT codes (every 64-base block clean)?
-__device__ __forceinline__ bool ref_clean(const uint64_t *__restrict__ bad, int64_t n_blk, int64_t rnib, int n) {
-  const int64_t k0 = rnib >> 6, k1 = (rnib + n - 1) >> 6;
-  if (k1 >= n_blk) return false;
-  for (int64_t wd = k0 >> 6; wd <= (k1 >> 6); ++wd) {
-    const int lo = wd == (k0 >> 6) ? (int)(k0 & 63) : 0;
-    const int hi = wd == (k1 >> 6) ? (int)(k1 & 63) : 63;
-    const uint64_t mask = (hi == 63 ? ~0ull : ((1ull << (hi + 1)) - 1)) & ~((1ull << lo) - 1);
-    if (bad[wd] & mask) return false;
-  }
-  return true;
-}
-
 // ---- reference blocks -----------------------------------------------------------------------
 // Bit k of bad: 64-base block k (32 bytes of nt16) holds a code other than A, C, G, T.
 __global__ void __launch_bounds__(kPrepThreads) k_ref_blocks(const uint8_t *__restrict__ ref, int64_t bytes,
@@ -142,65 +96,273 @@ __global__ void __launch_bounds__(kPrepThreads) k_ref_blocks(const uint8_t *__re
   }
 }
 
-// ---- per read (upload: validation) --------------------------------------------------------
-__global__ void __launch_bounds__(kPrepThreads) k_prep_reads(const Raw R, PrepErr *err, int32_t *__restrict__ read_end,
-                                                             int32_t *__restrict__ nseg, unsigned long long *written) {
-  int n_written = 0, max_len = 0, max_seg = 0;
-  for (int64_t r = blockIdx.x * (int64_t)kPrepThreads + threadIdx.x; r < R.n_reads;
-       r += (int64_t)gridDim.x * kPrepThreads) {
-    const int L = R.read_len[r];
-    const int nc = R.n_cig[r];
-    const int64_t co = R.cig_off[r];
-    const int rs = R.ref_start[r];
-    const int64_t so = R.seq_off[r];
-    const int ws = R.write_scope[r];
-    if (L < 0 || so < 0 || so + ((int64_t)L + 1) / 2 > R.seq_bytes) { report(err, kErrReadSeq, r); continue; }
-    if (nc < 0 || co < 0 || co + nc > R.n_cigar_ops) { report(err, kErrReadCigar, r); continue; }
-    if (R.dataset[r] > 1) report(err, kErrReadDataset, r);
-    if (ws < -1 || ws >= R.n_scopes) report(err, kErrReadWriteScope, r, ws);
-    if (L >= (1 << 24)) report(err, kErrReadLong, r);
-    n_written += ws >= 0;
-    max_len = max(max_len, L);
-    int64_t rl = 0;
-    for (int k = 0; k < nc; ++k) {
-      const uint32_t w = R.cigar[co + k];
-      const int op = (int)(w & 0xF);
-      if (op > 8) { report(err, kErrCigarOp, r, op); break; }
-      if (is_aligned_op(op) || op == 2 || op == 3) rl += w >> 4;
-    }
-    if (rs < 0 || rs + rl > INT32_MAX) { report(err, kErrReadPos, r); continue; }
-    read_end[r] = (int32_t)(rs + (rl > 0 ? rl : 1));
-    int ns = 0;   // segments of the read (walk_segments)
-    if (nc <= (int)(R.n_cigar_ops - co)) walk_segments(R.cigar + co, nc, L, rs, nc ? R.cigar[co] : 0u, [&](int, int, int) { ++ns; });
-    nseg[r] = ns;
-    max_seg = max(max_seg, ns);
-  }
-  for (int o = 32; o > 0; o >>= 1) {
-    n_written += __shfl_xor(n_written, o);
-    max_len = max(max_len, __shfl_xor(max_len, o));
-    max_seg = max(max_seg, __shfl_xor(max_seg, o));
-  }
-  if ((threadIdx.x & 63) == 0 && n_written) atomicAdd(written, (unsigned long long)n_written);
-  if ((threadIdx.x & 63) == 0 && max_len) atomicMax(written + 1, (unsigned long long)max_len);
-  if ((threadIdx.x & 63) == 0 && max_seg) atomicMax(written + 2, (unsigned long long)max_seg);
+// Scope groups: the scopes whose cost prefix (incidences + `weight` per scope, no scan needed: the
+// CSR offsets are that prefix) falls in one bucket of `target` units. The weight bounds a group to
+// 256 scopes. A bucket skipped over by a scope with many incidences is an empty group.
+__device__ __forceinline__ int64_t group_of(const int64_t *__restrict__ incid_off, int64_t s, long long weight,
+                                            long long target, const int64_t *__restrict__ cost) {
+  return cost ? cost[s] / target : (incid_off[s] + weight * s) / target;
 }
 
-// ---- per scope (upload: validation) --------------------------------------------------------
-__global__ void __launch_bounds__(kPrepThreads) k_prep_scope_check(const Raw R, PrepErr *err,
-                                                                   unsigned long long *huge) {
-  int n_huge = 0;
-  for (int64_t s = blockIdx.x * (int64_t)kPrepThreads + threadIdx.x; s < R.n_scopes;
-       s += (int64_t)gridDim.x * kPrepThreads) {
-    const int64_t i0 = R.incid_off[s], i1 = R.incid_off[s + 1];
-    if (i0 < 0 || i1 < i0 || i1 > R.n_incid) report(err, kErrScopeOff, s);
-    const int64_t ss = R.span_start[s], sl = R.span_len[s];
-    if (ss < 0 || sl < 0) report(err, kErrScopeSpan, s);
-    if (R.ref_off[s] < 0 || R.ref_off[s] + sl > R.ref_nibs) report(err, kErrScopeRef, s);
-    if (R.keep_code[s] > 15) report(err, kErrScopeKeep, s);
-    n_huge += sl > kGrpMaxSpan;
+// ---- the batch scan: every per-read and per-scope check, one pass over the raw arrays ----------
+// Replaces round 2's four check kernels, the segments-per-read pass and the far-capacity pass
+// (k_prep_reads / k_prep_scope_check / k_prep_incid_check / k_prep_seen_check / k_prep_farcap):
+// one coalesced read of each per-read and per-scope array. Read blocks validate every read field
+// before any load that depends on it, write read_end (bam_endpos) and the aligned segments per
+// read, and fold the read into its write scope's group candidate (the lowest buffer offset of
+// the reads a group writes, per dataset; short-read groups, closed form from the CSR offsets);
+// scope blocks validate the scope arrays and write the group table (first scope and incidence of
+// each group). Per-block partial sums (no same-address atomics: a batch-wide counter hit once
+// per wave serialised k_prep_reads at 0.8 ms) go to `part`, reduced by k_prep_reduce. The
+// incidence checks (read index, span containment) and the write-scope check need the scope of
+// each incidence: the emit kernels make them where they walk the incidences anyway, and
+// k_prep_seen_check runs after the masking kernels (neither can fault: the emit kernels range-check
+// before they gather). Their errors are reported by ganon_batch_download.
+enum { kPartWritten = 0, kPartMaxLen, kPartMaxSeg, kPartIdOps, kPartHuge, kPartWsHash, kParts };
+
+// The write-scope check without a per-read mark: every written read r contributes ws_hash(r) once
+// from the batch scan and once from the emit path that meets it in its write scope; the sums
+// (64-bit, wrapping, order-free) agree iff every written read is listed by its write scope (up to
+// a 2^-64 collision: a read listed twice in its write scope and another one missing give
+// different sums). k_finish compares them; on a mismatch ganon_batch_download runs
+// k_prep_ws_diag to name the read.
+// Sum of v over the block (256 threads); the result in every thread.
+__device__ __forceinline__ unsigned long long block_sum_u64(unsigned long long v, unsigned long long *ws) {
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t lo = __shfl_xor((uint32_t)v, o), hi = __shfl_xor((uint32_t)(v >> 32), o);
+    v += ((unsigned long long)hi << 32) | lo;
   }
-  for (int o = 32; o > 0; o >>= 1) n_huge += __shfl_xor(n_huge, o);
-  if ((threadIdx.x & 63) == 0 && n_huge) atomicAdd(huge, (unsigned long long)n_huge);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = v;
+  __syncthreads();
+  unsigned long long t = 0;
+  for (int w = 0; w < kWaves; ++w) t += ws[w];
+  return t;
+}
+#ifndef GANON_SCAN_U
+#define GANON_SCAN_U 4   // reads per thread of k_prep_scan (loads issued together)
+#endif
+constexpr int kScanReadsPerBlock = GANON_SCAN_U * kPrepThreads;
+constexpr int kScanScopesPerBlock = 4 * kPrepThreads;
+
+struct ScanOut {
+  int32_t *read_end;
+  unsigned long long *lo;     // [2 g_bound] group candidates (kNone-initialised), short-read groups
+  longlong2 *gmeta;           // [g_bound] first scope and incidence of each short-read group
+  int64_t g_bound;            // group count bound: (n_incid + weight (n_scopes - 1)) / target + 1
+  unsigned long long *part;   // [kParts x blocks]
+};
+
+__device__ __forceinline__ unsigned long long shfl64(unsigned long long v, int lane) {
+  const uint32_t lo = __shfl((uint32_t)v, lane), hi = __shfl((uint32_t)(v >> 32), lane);
+  return ((unsigned long long)hi << 32) | lo;
+}
+
+// Wave-aggregated atomicMin of (key -> value) pairs (kNone keys absent): one atomic per distinct
+// key in the wave (a wave of reads in buffer order meets one or two groups per dataset).
+__device__ __forceinline__ void wave_min_by_key(unsigned long long *__restrict__ dst, unsigned long long key,
+                                                unsigned long long val) {
+  const int lane = threadIdx.x & 63;
+  unsigned long long m = __ballot(key != kNone);
+  while (m) {
+    const int l = __ffsll((long long)m) - 1;
+    const unsigned long long k0 = shfl64(key, l);
+    const bool same = key == k0;
+    unsigned long long v = same ? val : kNone;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const unsigned long long x = shfl64(v, lane ^ o);
+      v = x < v ? x : v;
+    }
+    if (lane == l) atomicMin(dst + k0, v);
+    m &= ~__ballot(same);
+  }
+}
+
+__device__ __forceinline__ void block_parts(unsigned long long (&acc)[kParts], unsigned long long *__restrict__ part) {
+  __shared__ unsigned long long ws[kWaves][kParts];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < kParts; ++k) {
+    unsigned long long v = acc[k];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const unsigned long long x = shfl64(v, lane ^ o);
+      v = (k == kPartMaxLen || k == kPartMaxSeg) ? (x > v ? x : v) : v + x;
+    }
+    if (lane == 0) ws[wave][k] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < kParts) {
+    const int k = threadIdx.x;
+    unsigned long long v = 0;
+    for (int w = 0; w < kWaves; ++w)
+      v = (k == kPartMaxLen || k == kPartMaxSeg) ? (ws[w][k] > v ? ws[w][k] : v) : v + ws[w][k];
+    part[(int64_t)kParts * blockIdx.x + k] = v;
+  }
+}
+
+__global__ void __launch_bounds__(kPrepThreads) k_prep_scan(const Raw R, PrepErr *err, ScanOut O, long long weight,
+                                                            long long target, int read_blocks) {
+  unsigned long long acc[kParts] = {0, 0, 0, 0, 0, 0};
+  const int tid = threadIdx.x;
+  if ((int)blockIdx.x < read_blocks) {
+    // kScanU reads per thread, each load stage issued for all of them before any is used (the chain
+    // read fields -> first CIGAR word -> the write scope's CSR offset is latency bound)
+    constexpr int kScanU = kScanReadsPerBlock / kPrepThreads;
+    const int64_t r0 = (int64_t)blockIdx.x * kScanReadsPerBlock;
+    const int64_t r1 = min(r0 + kScanReadsPerBlock, (int64_t)R.n_reads);
+    int L[kScanU], nc[kScanU], rs[kScanU], ws[kScanU], ds[kScanU];
+    int64_t co[kScanU], so[kScanU];
+    bool ok[kScanU];
+#pragma unroll
+    for (int u = 0; u < kScanU; ++u) {
+      const int64_t r = r0 + tid + kPrepThreads * u;
+      ok[u] = r < r1;
+      const int64_t rr = ok[u] ? r : r0;
+      L[u] = R.read_len[rr];
+      nc[u] = R.n_cig[rr];
+      co[u] = R.cig_off[rr];
+      rs[u] = R.ref_start[rr];
+      so[u] = R.seq_off[rr];
+      ws[u] = R.write_scope[rr];
+      ds[u] = R.dataset[rr];
+    }
+    uint32_t w0[kScanU];
+    int64_t goff[kScanU];
+#pragma unroll
+    for (int u = 0; u < kScanU; ++u) {
+      const int64_t r = r0 + tid + kPrepThreads * u;
+      if (!ok[u]) continue;
+      if (L[u] < 0 || so[u] < 0 || so[u] + ((int64_t)L[u] + 1) / 2 > R.seq_bytes) { report(err, kErrReadSeq, r); ok[u] = false; }
+      else if (nc[u] < 0 || co[u] < 0 || co[u] + nc[u] > R.n_cigar_ops) { report(err, kErrReadCigar, r); ok[u] = false; }
+      if (ds[u] > 1) report(err, kErrReadDataset, r);
+      if (ws[u] < -1 || ws[u] >= R.n_scopes) { report(err, kErrReadWriteScope, r, ws[u]); ok[u] = false; }
+      if (L[u] >= (1 << 24)) report(err, kErrReadLong, r);
+    }
+#pragma unroll
+    for (int u = 0; u < kScanU; ++u) {
+      w0[u] = ok[u] && nc[u] > 0 ? R.cigar[co[u]] : 0u;
+      goff[u] = ok[u] && ws[u] >= 0 ? R.incid_off[ws[u]] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < kScanU; ++u) {
+      const int64_t r = r0 + tid + kPrepThreads * u;
+      unsigned long long ckey = kNone, cval = 0;
+      if (ok[u]) {
+        acc[kPartWritten] += ws[u] >= 0;
+        if (ws[u] >= 0) acc[kPartWsHash] += ws_hash((int)r);
+        acc[kPartMaxLen] = max(acc[kPartMaxLen], (unsigned long long)L[u]);
+        // one walk: reference length (bam_endpos), aligned segments as walk_segments cuts them,
+        // I/D ops (the indel tally's observations)
+        int64_t rl = 0;
+        int q = 0, ns = 0, nid = 0;
+        bool good = true;
+        for (int k = 0; k < nc[u]; ++k) {
+          const uint32_t w = k == 0 ? w0[u] : R.cigar[co[u] + k];
+          const int op = (int)(w & 0xF);
+          const int len = (int)(w >> 4);
+          if (op > 8) { report(err, kErrCigarOp, r, op); good = false; break; }
+          if (is_aligned_op(op)) {
+            if (q < L[u]) ns += (min(len, L[u] - q) + kSegMaxLen - 1) / kSegMaxLen;
+            q += len;
+            rl += len;
+          } else if (op == 1 || op == 4) {
+            q += len;
+          } else if (op == 2 || op == 3) {
+            rl += len;
+          }
+          nid += op == 1 || op == 2;
+        }
+        if (good && (rs[u] < 0 || rs[u] + rl > INT32_MAX)) { report(err, kErrReadPos, r); good = false; }
+        if (good) {
+          O.read_end[r] = (int32_t)(rs[u] + (rl > 0 ? rl : 1));
+          acc[kPartMaxSeg] = max(acc[kPartMaxSeg], (unsigned long long)ns);
+          acc[kPartIdOps] += (unsigned long long)nid;
+          if (ws[u] >= 0 && L[u] > 0 && ds[u] <= 1) {
+            int64_t g = (goff[u] + weight * ws[u]) / target;   // group_of, short-read groups
+            g = g < 0 ? 0 : (g >= O.g_bound ? O.g_bound - 1 : g);
+            ckey = 2 * (unsigned long long)g + (unsigned long long)ds[u];
+            cval = (unsigned long long)so[u];
+          }
+        }
+      }
+      wave_min_by_key(O.lo, ckey, cval);
+    }
+  } else {
+    const int64_t s0 = (int64_t)(blockIdx.x - read_blocks) * kScanScopesPerBlock;
+    const int64_t s1 = min(s0 + kScanScopesPerBlock, (int64_t)R.n_scopes);
+    for (int64_t s = s0 + tid; s < s1; s += kPrepThreads) {
+      const int64_t i0 = R.incid_off[s], i1 = R.incid_off[s + 1];
+      if (i0 < 0 || i1 < i0 || i1 > R.n_incid) report(err, kErrScopeOff, s);
+      const int64_t ss = R.span_start[s], sl = R.span_len[s];
+      if (ss < 0 || sl < 0) report(err, kErrScopeSpan, s);
+      if (R.ref_off[s] < 0 || R.ref_off[s] + sl > R.ref_nibs) report(err, kErrScopeRef, s);
+      if (R.keep_code[s] > 15) report(err, kErrScopeKeep, s);
+      acc[kPartHuge] += sl > kGrpMaxSpan;
+      // the group table: every bucket from the previous scope's (exclusive) to this scope's starts
+      // here (clamped: offsets are only known valid after this kernel)
+      int64_t b = group_of(R.incid_off, s, weight, target, nullptr);
+      int64_t bp = s == 0 ? -1 : group_of(R.incid_off, s - 1, weight, target, nullptr);
+      b = min(b, O.g_bound - 1);
+      bp = max(bp, (int64_t)-1);
+      const longlong2 m = make_longlong2(s, i0);
+      for (int64_t x = bp + 1; x <= b; ++x) O.gmeta[x] = m;
+    }
+  }
+  block_parts(acc, O.part);
+}
+
+// plan_info: [0] I/D ops, [1] huge scopes, [2] written reads, [3] longest read, [4] most segments of
+// one read, [5] short-read groups (bucket of the last scope + 1), [6] write-scope hash sum.
+__global__ void __launch_bounds__(kPrepThreads) k_prep_reduce(const Raw R, const unsigned long long *__restrict__ part,
+                                                              int n_blocks, long long weight, long long target,
+                                                              int64_t g_bound, unsigned long long *__restrict__ info) {
+  unsigned long long acc[kParts] = {0, 0, 0, 0, 0, 0};
+  for (int b = threadIdx.x; b < n_blocks; b += kPrepThreads) {
+#pragma unroll
+    for (int k = 0; k < kParts; ++k) {
+      const unsigned long long v = part[(int64_t)kParts * b + k];
+      acc[k] = (k == kPartMaxLen || k == kPartMaxSeg) ? (v > acc[k] ? v : acc[k]) : acc[k] + v;
+    }
+  }
+  __shared__ unsigned long long out[kParts];
+  // block_parts writes part[blockIdx.x = 0]: reduce into LDS instead
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __shared__ unsigned long long ws[kWaves][kParts];
+#pragma unroll
+  for (int k = 0; k < kParts; ++k) {
+    unsigned long long v = acc[k];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const unsigned long long x = shfl64(v, lane ^ o);
+      v = (k == kPartMaxLen || k == kPartMaxSeg) ? (x > v ? x : v) : v + x;
+    }
+    if (lane == 0) ws[wave][k] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < kParts) {
+    const int k = threadIdx.x;
+    unsigned long long v = 0;
+    for (int w = 0; w < kWaves; ++w)
+      v = (k == kPartMaxLen || k == kPartMaxSeg) ? (ws[w][k] > v ? ws[w][k] : v) : v + ws[w][k];
+    out[k] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    info[0] = out[kPartIdOps];
+    info[1] = out[kPartHuge];
+    info[2] = out[kPartWritten];
+    info[3] = out[kPartMaxLen];
+    info[4] = out[kPartMaxSeg];
+    info[6] = out[kPartWsHash];
+    int64_t ng = 0;
+    if (R.n_scopes > 0) {
+      ng = group_of(R.incid_off, R.n_scopes - 1, weight, target, nullptr) + 1;
+      ng = ng < 1 ? 1 : (ng > g_bound ? g_bound : ng);
+    }
+    info[5] = (unsigned long long)ng;
+  }
 }
 
 // Largest j in [0, n) with off[j] <= i (off nondecreasing, off[0] <= i).
@@ -214,19 +376,45 @@ __device__ __forceinline__ int lds_upper(const long long *off, int n, long long 
   return lo;
 }
 
-__global__ void __launch_bounds__(kPrepThreads) k_prep_seen_check(const Raw R, const uint8_t *__restrict__ seen,
-                                                                  PrepErr *err) {
+// Long-read mode only: aligned segments per read (walk_segments' cuts), for the segment-weighted
+// groups and the record slots.
+__global__ void __launch_bounds__(kPrepThreads) k_prep_nseg(const Raw R, int32_t *__restrict__ nseg) {
   for (int64_t r = blockIdx.x * (int64_t)kPrepThreads + threadIdx.x; r < R.n_reads;
-       r += (int64_t)gridDim.x * kPrepThreads)
-    if (R.write_scope[r] >= 0 && !seen[r]) report(err, kErrWriteScopeMissing, r, R.write_scope[r]);
+       r += (int64_t)gridDim.x * kPrepThreads) {
+    const int nc = R.n_cig[r];
+    int ns = 0;
+    walk_segments(R.cigar + R.cig_off[r], nc, R.read_len[r], R.ref_start[r], nc ? R.cigar[R.cig_off[r]] : 0u,
+                  [&](int, int, int) { ++ns; });
+    nseg[r] = ns;
+  }
 }
 
-// Scope groups: the scopes whose cost prefix (incidences + `weight` per scope, no scan needed: the
-// CSR offsets are that prefix) falls in one bucket of `target` units. The weight bounds a group to
-// 256 scopes. A bucket skipped over by a scope with many incidences is an empty group.
-__device__ __forceinline__ int64_t group_of(const int64_t *__restrict__ incid_off, int64_t s, long long weight,
-                                            long long target, const int64_t *__restrict__ cost) {
-  return cost ? cost[s] / target : (incid_off[s] + weight * s) / target;
+// The write-scope sums disagreed (k_finish): name a written read its write scope does not list.
+__global__ void __launch_bounds__(kPrepThreads) k_prep_ws_diag(const Raw R, PrepErr *err) {
+  for (int64_t r = blockIdx.x * (int64_t)kPrepThreads + threadIdx.x; r < R.n_reads;
+       r += (int64_t)gridDim.x * kPrepThreads) {
+    const int ws = R.write_scope[r];
+    if (ws < 0) continue;
+    int n = 0;
+    for (int64_t i = R.incid_off[ws]; i < R.incid_off[ws + 1]; ++i) n += R.incid_read[i] == (int)r;
+    if (n != 1) report(err, kErrWriteScopeMissing, r, ws);
+  }
+}
+
+// The incidence checks of the emit paths: read index in range (before any gather through it) and
+// the read inside its scope's span. False = the incidence contributes nothing (the batch is
+// reported invalid).
+__device__ __forceinline__ bool incid_ok(const Raw &R, const int32_t *__restrict__ read_end, PrepErr *err, int64_t i,
+                                         int64_t s, int r, int ss, int se) {
+  if (r < 0 || r >= R.n_reads) {
+    report(err, kErrIncidRead, i, r);
+    return false;
+  }
+  if (R.ref_start[r] < ss || read_end[r] > se) {
+    report(err, kErrIncidSpan, s, r);
+    return false;
+  }
+  return true;
 }
 
 // Long-read mode (upload): cost of scope s = its incidences' segments + weight (exclusive prefix next).
@@ -239,23 +427,11 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_scope_cost(const Raw R, c
       continue;
     }
     int64_t c = weight;
-    for (int64_t i = R.incid_off[s]; i < R.incid_off[s + 1]; ++i) c += nseg[R.incid_read[i]];
-    cost[s] = c;
-  }
-}
-
-// Upload only: every incidence's read index and span, and the write scope of every written read.
-__global__ void __launch_bounds__(kPrepThreads) k_prep_incid_check(const Raw R, const int32_t *__restrict__ read_end,
-                                                                   PrepErr *err, uint8_t *__restrict__ seen) {
-  for (int64_t s = blockIdx.x * (int64_t)kPrepThreads + threadIdx.x; s < R.n_scopes;
-       s += (int64_t)gridDim.x * kPrepThreads) {
-    const int ss = R.span_start[s], se = R.span_start[s] + R.span_len[s];
     for (int64_t i = R.incid_off[s]; i < R.incid_off[s + 1]; ++i) {
       const int r = R.incid_read[i];
-      if (r < 0 || r >= R.n_reads) { report(err, kErrIncidRead, i, r); continue; }
-      if (R.ref_start[r] < ss || read_end[r] > se) { report(err, kErrIncidSpan, s, r); continue; }
-      if (R.write_scope[r] == s) seen[r] = 1;
+      if (r >= 0 && r < R.n_reads) c += nseg[r];
     }
+    cost[s] = c;
   }
 }
 
@@ -355,6 +531,15 @@ __device__ void map_mark(const LineMap &M, unsigned long long key, uint32_t c) {
   }
 }
 
+// Flat mode: the candidates k_prep_scan folded per group mark their lines.
+__global__ void __launch_bounds__(kPrepThreads) k_prep_mark(const unsigned long long *__restrict__ lo, int n_cand,
+                                                            LineMap M) {
+  for (int64_t c = blockIdx.x * (int64_t)kPrepThreads + threadIdx.x; c < n_cand; c += (int64_t)gridDim.x * kPrepThreads) {
+    const unsigned long long k = lo[c];
+    if (k != kNone) map_mark(M, k, (uint32_t)c);
+  }
+}
+
 // l1 / l2 from l0 (thread per l1 word).
 __global__ void __launch_bounds__(kPrepThreads) k_prep_linemap(LineMap M) {
   for (int64_t w1 = blockIdx.x * (int64_t)kPrepThreads + threadIdx.x; w1 < M.n1; w1 += (int64_t)gridDim.x * kPrepThreads) {
@@ -395,30 +580,6 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_pieces(const unsigned lon
     }
     groups[kGrpRec * (c >> 1) + 2 + 2 * (c & 1)] = pc;
   }
-}
-
-__device__ __forceinline__ int64_t rec_lo(const int4 &x) { return (int64_t)(((uint64_t)(uint32_t)x.y << 32) | (uint32_t)x.x); }
-__device__ __forceinline__ int64_t rec_hi(const int4 &x) { return (int64_t)(((uint64_t)(uint32_t)x.w << 32) | (uint32_t)x.z); }
-
-// Upload only: nibbles of written reads outside their group's pieces (the far-mask capacity).
-__global__ void __launch_bounds__(kPrepThreads) k_prep_farcap(const Raw R, long long weight, long long target,
-                                                              const int64_t *__restrict__ cost,
-                                                              const int4 *__restrict__ groups,
-                                                              unsigned long long *far_nibs) {
-  unsigned long long acc = 0;
-  for (int64_t r = blockIdx.x * (int64_t)kPrepThreads + threadIdx.x; r < R.n_reads;
-       r += (int64_t)gridDim.x * kPrepThreads) {
-    const int ws = R.write_scope[r];
-    if (ws < 0 || R.read_len[r] == 0 || R.span_len[ws] > kGrpMaxSpan) continue;
-    const int64_t g = group_of(R.incid_off, ws, weight, target, cost);
-    const int4 A = groups[kGrpRec * g + 2], Bp = groups[kGrpRec * g + 4];
-    const int64_t r0 = R.seq_off[r], r1 = r0 + ((int64_t)R.read_len[r] + 1) / 2;
-    const int64_t in = max((int64_t)0, min(r1, rec_hi(A)) - max(r0, rec_lo(A))) +
-                       max((int64_t)0, min(r1, rec_hi(Bp)) - max(r0, rec_lo(Bp)));
-    acc += (unsigned long long)(2 * ((r1 - r0) - in));
-  }
-  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
-  if ((threadIdx.x & 63) == 0 && acc) atomicAdd(far_nibs, acc);
 }
 
 // Block-wide exclusive scan of two counters (256 threads).
@@ -473,17 +634,30 @@ constexpr int kEmitUnroll = 2;   // incidences per thread and trip
 struct EmitInc {                 // one incidence of a trip, in registers
   const uint32_t *cg;
   int64_t so;
-  int r, j, ncig, L, rs, ds, wsc;
+  int r, j, ncig, L, rs, re, ds, wsc;
   uint32_t w0;
 };
 
+// What the emit kernels need for the incidence checks (incid_ok) and the write-scope marks.
+struct Checks {
+  const int32_t *read_end;
+  unsigned long long *ws_part;   // [group] write-scope hash sum of the group's mine incidences
+  PrepErr *err;
+};
+
 // The read side of a trip (needs no scope lookup: issued before the scope staging is waited for).
-__device__ __forceinline__ void emit_load_reads(const Raw &R, long long base, long long i1, EmitInc (&e)[kEmitUnroll]) {
+// An incidence whose read index is out of range is reported and dropped before any gather.
+__device__ __forceinline__ void emit_load_reads(const Raw &R, const Checks &C, long long base, long long i1,
+                                                EmitInc (&e)[kEmitUnroll]) {
   const int tid = threadIdx.x;
 #pragma unroll
   for (int u = 0; u < kEmitUnroll; ++u) {
     const long long i = base + tid + kPrepThreads * u;
     e[u].r = i < i1 ? R.incid_read[i] : -1;
+    if (i < i1 && (e[u].r < 0 || e[u].r >= R.n_reads)) {
+      report(C.err, kErrIncidRead, i, e[u].r);
+      e[u].r = -1;
+    }
   }
 #pragma unroll
   for (int u = 0; u < kEmitUnroll; ++u) {
@@ -492,6 +666,7 @@ __device__ __forceinline__ void emit_load_reads(const Raw &R, long long base, lo
     e[u].ncig = e[u].r >= 0 ? R.n_cig[rr] : 0;
     e[u].L = R.read_len[rr];
     e[u].rs = R.ref_start[rr];
+    e[u].re = C.read_end[rr];
     e[u].so = R.seq_off[rr];
     e[u].ds = R.dataset[rr];
     e[u].wsc = R.write_scope[rr];
@@ -500,28 +675,38 @@ __device__ __forceinline__ void emit_load_reads(const Raw &R, long long base, lo
   for (int u = 0; u < kEmitUnroll; ++u) e[u].w0 = e[u].ncig > 0 ? e[u].cg[0] : 0u;
 }
 
-// The scope side: local scope index by binary search in the staged offsets; huge scopes drop out.
-__device__ __forceinline__ void emit_resolve(const long long *off, const uint8_t *huge, int ns, long long base,
-                                             EmitInc (&e)[kEmitUnroll], bool keep_huge) {
+// The scope side: local scope index by binary search in the staged offsets; a read outside its
+// scope's span is reported and dropped; `hsum` (if given) adds the write-scope hash of the reads met
+// in their write scope; huge scopes drop out unless kept.
+__device__ __forceinline__ void emit_resolve(const long long *off, const uint8_t *huge, const int *sstart,
+                                             const int *send, int s0, int ns, long long base, EmitInc (&e)[kEmitUnroll],
+                                             bool keep_huge, const Checks &C, unsigned long long *hsum) {
 #pragma unroll
   for (int u = 0; u < kEmitUnroll; ++u) {
     e[u].j = 0;
     if (e[u].r < 0) continue;
-    e[u].j = lds_upper(off, ns, base + threadIdx.x + kPrepThreads * u);
-    if (!keep_huge && huge[e[u].j]) e[u].r = -1;
+    const int j = lds_upper(off, ns, base + threadIdx.x + kPrepThreads * u);
+    e[u].j = j;
+    if (e[u].rs < sstart[j] || e[u].re > send[j]) {
+      report(C.err, kErrIncidSpan, s0 + j, e[u].r);
+      e[u].r = -1;
+      continue;
+    }
+    if (hsum && e[u].wsc == s0 + j) *hsum += ws_hash(e[u].r);
+    if (!keep_huge && huge[j]) e[u].r = -1;
   }
 }
 
 __global__ void __launch_bounds__(kPrepThreads) k_prep_emit(const Raw R, const longlong2 *__restrict__ gmeta,
                                                             int n_groups, int write, const uint64_t *__restrict__ bad,
-                                                            int64_t n_blk, long long region_per_incid,
-                                                            int32_t *__restrict__ read_end, int4 *__restrict__ seg4,
+                                                            int64_t n_blk, long long region_per_incid, const Checks C,
+                                                            int4 *__restrict__ seg4,
                                                             int4 *__restrict__ groups, unsigned long long *__restrict__ lo,
                                                             LineMap M, unsigned long long *__restrict__ cursor,
                                                             const unsigned long long *__restrict__ cursor_base) {
   __shared__ long long off[kGrpMaxScopes + 1];
   __shared__ long long ref0[kGrpMaxScopes];
-  __shared__ int sstart[kGrpMaxScopes];
+  __shared__ int sstart[kGrpMaxScopes], send[kGrpMaxScopes];
   __shared__ uint8_t huge[kGrpMaxScopes];
   __shared__ int ws[2 * kWaves];
   __shared__ unsigned long long lmin[2], gbase;
@@ -536,6 +721,7 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_emit(const Raw R, const l
   for (int t = tid; t <= ns; t += kPrepThreads) off[t] = R.incid_off[s0 + t];
   for (int t = tid; t < ns; t += kPrepThreads) {
     sstart[t] = R.span_start[s0 + t];
+    send[t] = R.span_start[s0 + t] + R.span_len[s0 + t];
     ref0[t] = R.ref_off[s0 + t] - R.span_start[s0 + t];
     huge[t] = R.span_len[s0 + t] > kGrpMaxSpan;
   }
@@ -546,12 +732,13 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_emit(const Raw R, const l
   for (int u = 0; u < kEmitUnroll; ++u) cnt[u] = 0;   // an empty group runs no trip
   int tot_c = 0, tot_d = 0, ec = 0, ed = 0;   // group totals; (one trip) this thread's offsets
   unsigned long long mn0 = kNone, mn1 = kNone;   // this thread's candidates
+  unsigned long long hsum = 0;                    // write-scope hash of this thread's mine incidences
   // ---- pass 1: count
   for (long long base = i0; base < i1; base += kPrepThreads * kEmitUnroll) {   // uniform trip count
     EmitInc e[kEmitUnroll];
-    emit_load_reads(R, base, i1, e);
+    emit_load_reads(R, C, base, i1, e);
     __syncthreads();   // (first trip: the scope staging)
-    emit_resolve(off, huge, ns, base, e, true);
+    emit_resolve(off, huge, sstart, send, s0, ns, base, e, true, C, &hsum);
     int tnc = 0, tnd = 0;
 #pragma unroll
     for (int u = 0; u < kEmitUnroll; ++u) {
@@ -563,7 +750,6 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_emit(const Raw R, const l
         if (x.ds) mn1 = min(mn1, (unsigned long long)x.so);
         else mn0 = min(mn0, (unsigned long long)x.so);
       }
-      // (read_end, bam_endpos, is the upload's: k_prep_reads writes it once per batch)
       if (huge[x.j]) continue;
       const uint32_t fl = ((uint32_t)x.ds << 30) | (mine ? kSegMine : 0u);
       const int64_t qnib = 2 * x.so, r0 = ref0[x.j];
@@ -589,6 +775,11 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_emit(const Raw R, const l
     ed += tot_d;
     tot_c += tc;
     tot_d += td;
+  }
+  {
+    __shared__ unsigned long long hws[kWaves];
+    const unsigned long long h = block_sum_u64(hsum, hws);
+    if (tid == 0) C.ws_part[g] = h;
   }
   // ---- candidates: wave reductions, one LDS atomic per wave
   for (int o = 32; o > 0; o >>= 1) {
@@ -621,8 +812,8 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_emit(const Raw R, const l
       EmitInc e[kEmitUnroll];
       const bool reload = !one_trip || cnt[0] > 1 || cnt[1] > 1;
       if (reload) {
-        emit_load_reads(R, base, i1, e);
-        emit_resolve(off, huge, ns, base, e, false);
+        emit_load_reads(R, C, base, i1, e);
+        emit_resolve(off, huge, sstart, send, s0, ns, base, e, false, C, nullptr);
       }
       if (one_trip) {
 #pragma unroll
@@ -704,19 +895,19 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_emit(const Raw R, const l
 // the whole range), any other group through the nt16 reference.
 constexpr unsigned long long kLongReadLen = 1000;   // auto prep: long-read mode above this read length
 
-// kFlatU: incidences per thread and trip (GANON_PARAM_PREP_UNROLL)
+// kFlatU: incidences per thread and trip (GANON_PARAM_PREP_UNROLL). The group candidates come from
+// k_prep_scan (closed-form groups); this kernel makes the incidence checks, marks the reads met in
+// their write scope and writes the records and group records 0, 1 and 3.
 template <int kFlatU>
 __global__ void __launch_bounds__(kPrepThreads) k_prep_emit_flat(const Raw R, const longlong2 *__restrict__ gmeta,
                                                                  int n_groups, const uint64_t *__restrict__ bad,
                                                                  int64_t n_blk, long long region_per_incid,
-                                                                 int4 *__restrict__ seg4, int4 *__restrict__ groups,
-                                                                 unsigned long long *__restrict__ lo, LineMap M,
-                                                                 int write) {
+                                                                 const Checks C, int4 *__restrict__ seg4,
+                                                                 int4 *__restrict__ groups) {
   __shared__ long long off[kGrpMaxScopes + 1];
   __shared__ long long ref0[kGrpMaxScopes];
-  __shared__ int sstart[kGrpMaxScopes];
+  __shared__ int sstart[kGrpMaxScopes], send[kGrpMaxScopes];
   __shared__ uint8_t huge[kGrpMaxScopes];
-  __shared__ unsigned long long lmin[2];
   __shared__ int s_dirty;
   const int tid = threadIdx.x;
   const int g = blockIdx.x;
@@ -727,14 +918,14 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_emit_flat(const Raw R, co
   for (int t = tid; t <= ns; t += kPrepThreads) off[t] = R.incid_off[s0 + t];
   for (int t = tid; t < ns; t += kPrepThreads) {
     sstart[t] = R.span_start[s0 + t];
+    send[t] = R.span_start[s0 + t] + R.span_len[s0 + t];
     ref0[t] = R.ref_off[s0 + t] - R.span_start[s0 + t];
     huge[t] = R.span_len[s0 + t] > kGrpMaxSpan;
   }
-  if (tid < 2) lmin[tid] = kNone;
   if (tid == 0) s_dirty = 0;
   __syncthreads();
-  unsigned long long mn0 = kNone, mn1 = kNone;
   bool dirty = false;
+  unsigned long long hsum = 0;
   // kFlatU incidences per thread and trip, their loads issued together (the chain incidence -> read
   // fields -> CIGAR -> reference block bitmap is latency bound)
   for (long long base = i0; base < i1; base += kFlatU * kPrepThreads) {
@@ -744,6 +935,10 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_emit_flat(const Raw R, co
     for (int u = 0; u < kFlatU; ++u) {
       const long long i = base + tid + kPrepThreads * u;
       e[u].r = i < i1 ? R.incid_read[i] : -1;
+      if (i < i1 && (e[u].r < 0 || e[u].r >= R.n_reads)) {
+        report(C.err, kErrIncidRead, i, e[u].r);
+        e[u].r = -2;   // in range of the group, no read: a zero-length record
+      }
     }
 #pragma unroll
     for (int u = 0; u < kFlatU; ++u) {
@@ -752,6 +947,7 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_emit_flat(const Raw R, co
       e[u].ncig = e[u].r >= 0 ? R.n_cig[rr] : 0;
       e[u].L = R.read_len[rr];
       e[u].rs = R.ref_start[rr];
+      e[u].re = C.read_end[rr];
       e[u].so = R.seq_off[rr];
       e[u].ds = R.dataset[rr];
       e[u].wsc = R.write_scope[rr];
@@ -761,17 +957,18 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_emit_flat(const Raw R, co
     for (int u = 0; u < kFlatU; ++u) e[u].w0 = e[u].ncig > 0 ? e[u].cg[0] : 0u;
 #pragma unroll
     for (int u = 0; u < kFlatU; ++u) {
-      if (e[u].r < 0) continue;
+      if (e[u].r == -1) continue;   // past the group
       const EmitInc &x = e[u];
       const int j = jj[u];
-      const bool mine = x.wsc == s0 + j;
-      if (mine && x.L > 0) {
-        if (x.ds) mn1 = min(mn1, (unsigned long long)x.so);
-        else mn0 = min(mn0, (unsigned long long)x.so);
-      }
-      if (!write) continue;
       int4 rec = make_int4(0, 0, 0, j);   // zero-length: no chunks
-      if (!huge[j]) {
+      bool ok = x.r >= 0;
+      if (ok && (x.rs < sstart[j] || x.re > send[j])) {
+        report(C.err, kErrIncidSpan, s0 + j, x.r);
+        ok = false;
+      }
+      const bool mine = ok && x.wsc == s0 + j;
+      if (mine) hsum += ws_hash(x.r);
+      if (ok && !huge[j]) {
         const uint32_t fl = ((uint32_t)x.ds << 30) | (mine ? kSegMine : 0u);
         const int64_t qnib = 2 * x.so, r0 = ref0[j];
         const int ss = sstart[j];
@@ -785,21 +982,11 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_emit_flat(const Raw R, co
       seg4[base + tid + kPrepThreads * u] = rec;
     }
   }
-  for (int o = 32; o > 0; o >>= 1) {
-    mn0 = min(mn0, (unsigned long long)__shfl_xor(mn0, o));
-    mn1 = min(mn1, (unsigned long long)__shfl_xor(mn1, o));
-  }
-  if ((tid & 63) == 0) {
-    if (mn0 != kNone) atomicMin(&lmin[0], mn0);
-    if (mn1 != kNone) atomicMin(&lmin[1], mn1);
-  }
   if (__any(dirty) && (tid & 63) == 0) s_dirty = 1;
-  __syncthreads();
-  if (tid < 2) {
-    lo[2 * (int64_t)g + tid] = lmin[tid];
-    if (lmin[tid] != kNone) map_mark(M, lmin[tid], (uint32_t)(2 * g + tid));
-  }
+  __shared__ unsigned long long hws[kWaves];
+  const unsigned long long h = block_sum_u64(hsum, hws);   // (its barriers order s_dirty too)
   if (tid == 0) {
+    C.ws_part[g] = h;
     const int64_t seg_b = i0, seg_e = i1, mid = s_dirty ? seg_b : seg_e;
     const int64_t region = i0 * region_per_incid + (int64_t)kGrpObs * g;
     const int cap = (int)min((i1 - i0) * region_per_incid + kGrpObs, (long long)(INT32_MAX / 2));
@@ -885,18 +1072,23 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_long_groups(const Raw R, 
                                                                    unsigned long long *__restrict__ cursor,
                                                                    const unsigned long long *__restrict__ cursor_base,
                                                                    unsigned long long *__restrict__ dirty,
-                                                                   int64_t *__restrict__ slot0, int write) {
+                                                                   int64_t *__restrict__ slot0, const Checks C,
+                                                                   int write) {
   for (int64_t g = blockIdx.x * (int64_t)kPrepThreads + threadIdx.x; g < n_groups;
        g += (int64_t)gridDim.x * kPrepThreads) {
     const longlong2 m0 = gmeta[g];
     const longlong2 m1 = g + 1 < n_groups ? gmeta[g + 1] : make_longlong2(R.n_scopes, R.n_incid);
     const int s0 = (int)m0.x, s1 = (int)m1.x;
     const long long i0 = m0.y, i1 = m1.y;
-    unsigned long long count = 0, mn[2] = {kNone, kNone};
+    unsigned long long count = 0, mn[2] = {kNone, kNone}, hsum = 0;
     for (int s = s0; s < s1; ++s) {
-      if (R.span_len[s] > kGrpMaxSpan) continue;   // huge scope: tile path
+      const int ss = R.span_start[s], se = ss + R.span_len[s];
+      const bool big = R.span_len[s] > kGrpMaxSpan;   // huge scope: tile path
       for (int64_t i = R.incid_off[s]; i < R.incid_off[s + 1]; ++i) {
         const int r = R.incid_read[i];
+        if (!incid_ok(R, C.read_end, C.err, i, s, r, ss, se)) continue;
+        if (R.write_scope[r] == s) hsum += ws_hash(r);
+        if (big) continue;
         count += (unsigned long long)nseg[r];
         if (R.write_scope[r] == s && R.read_len[r] > 0) {
           const int d = R.dataset[r];
@@ -914,9 +1106,11 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_long_groups(const Raw R, 
       int64_t x = seg_b;
       for (int s = s0; s < s1; ++s) {
         if (R.span_len[s] > kGrpMaxSpan) continue;
+        const int ss = R.span_start[s], se = ss + R.span_len[s];
         for (int64_t i = R.incid_off[s]; i < R.incid_off[s + 1]; ++i) {
+          const int r = R.incid_read[i];
           slot0[i] = x;
-          x += nseg[R.incid_read[i]];
+          if (r >= 0 && r < R.n_reads && R.ref_start[r] >= ss && C.read_end[r] <= se) x += nseg[r];
         }
       }
     }
@@ -930,6 +1124,7 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_long_groups(const Raw R, 
     groups[kGrpRec * g + 1] = make_int4((int)(uint32_t)seg_e, (int)(uint32_t)((uint64_t)seg_e >> 32), 0, 0);
     groups[kGrpRec * g + 3] = make_int4((int)(uint32_t)region, (int)(uint32_t)((uint64_t)region >> 32), cap, 0);
     dirty[g] = 0;
+    C.ws_part[g] = hsum;
   }
 }
 
@@ -941,6 +1136,7 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_emit_waves(const Raw R, c
                                                                   const uint64_t *__restrict__ bad, int64_t n_blk,
                                                                   const int64_t *__restrict__ slot0,
                                                                   unsigned long long *__restrict__ dirty,
+                                                                  const int32_t *__restrict__ read_end,
                                                                   int4 *__restrict__ seg4) {
   const int64_t nw = (int64_t)gridDim.x * kWaves;
   for (int64_t i = blockIdx.x * (int64_t)kWaves + (threadIdx.x >> 6); i < R.n_incid; i += nw) {
@@ -954,6 +1150,9 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_emit_waves(const Raw R, c
     if (R.span_len[s] > kGrpMaxSpan) continue;
     const int64_t g = group_of(R.incid_off, s, 0, target, cost);
     const int r = R.incid_read[i];
+    // the incidence checks of k_prep_long_groups (reported there): skipped alike
+    if (r < 0 || r >= R.n_reads || R.ref_start[r] < R.span_start[s] || read_end[r] > R.span_start[s] + R.span_len[s])
+      continue;
     wave_walk(R, r, R.write_scope[r] == s, s - (int)gmeta[g].x, R.span_start[s], R.ref_off[s] - R.span_start[s], bad,
               n_blk, slot0[i], dirty + g, seg4);
   }
@@ -1023,17 +1222,9 @@ const char *err_text(int kind) {
     case kErrScopeKeep: return "scope %lld: keep_code > 15";
     case kErrIncidRead: return "incidence %lld: read %lld out of range";
     case kErrIncidSpan: return "scope %lld: read %lld outside its span";
-    case kErrWriteScopeMissing: return "read %lld: write_scope %lld does not contain it";
+    case kErrWriteScopeMissing: return "read %lld: write_scope %lld does not list it exactly once";
     default: return "invalid batch (%lld)";
   }
-}
-
-int check_err(ganon_ctx *ctx, ganon_dbatch *db) {
-  PrepErr e{};
-  HIP_OR_FAIL(hipMemcpyAsync(&e, db->err, sizeof e, hipMemcpyDeviceToHost, ctx->stream));
-  HIP_OR_FAIL(hipStreamSynchronize(ctx->stream));
-  if (e.code) return fail(ctx, GANON_E_ARG, err_text(e.code), e.index, e.a, e.b);
-  return GANON_OK;
 }
 
 // The line map over the batch's output buffer (b_linemap: l0 | l1 | l2 | hash keys | hash values).
@@ -1060,6 +1251,10 @@ int64_t line_map_words(const ganon_dbatch *db) {
   return M.n0 + M.n1 + M.n2 + 2 * M.hsize;
 }
 
+Checks checks_of(const ganon_dbatch *db) {
+  return Checks{db->B.read_end, static_cast<unsigned long long *>(db->b_wspart.p), db->err};
+}
+
 int launch_groups(ganon_ctx *ctx, ganon_dbatch *db, const Raw &R) {
   KernelScope ks(ctx, "prep_groups");
   if (db->n_groups)   // the line map, marked by the emit kernel
@@ -1081,11 +1276,11 @@ int launch_emit(ganon_ctx *ctx, ganon_dbatch *db, const Raw &R, int write) {
                        static_cast<const longlong2 *>(db->b_gs0.p), db->n_groups, (long long)db->region_per_incid,
                        static_cast<const int32_t *>(db->b_nseg.p), static_cast<int4 *>(db->b_groups.p),
                        static_cast<unsigned long long *>(db->b_lo.p), line_map(db), db->cursor, db->cursor + kCursors,
-                       dirty, slot0, write);
+                       dirty, slot0, checks_of(db), write);
     if (write) {
       hipLaunchKernelGGL(k_prep_emit_waves, dim3(grid_for(db->n_incid * 64)), dim3(kPrepThreads), 0, ctx->stream, R,
                          db->scost, (long long)db->group_target, static_cast<const longlong2 *>(db->b_gs0.p),
-                         db->ref->bad, db->ref->n_blk, slot0, dirty, static_cast<int4 *>(db->b_seg4.p));
+                         db->ref->bad, db->ref->n_blk, slot0, dirty, db->B.read_end, static_cast<int4 *>(db->b_seg4.p));
       hipLaunchKernelGGL(k_prep_long_mid, dim3(gg), dim3(kPrepThreads), 0, ctx->stream, db->n_groups, dirty,
                          static_cast<int4 *>(db->b_groups.p));
     }
@@ -1096,15 +1291,13 @@ int launch_emit(ganon_ctx *ctx, ganon_dbatch *db, const Raw &R, int write) {
                                                                                    : k_prep_emit_flat<2>;
     hipLaunchKernelGGL(flat, dim3((unsigned)db->n_groups), dim3(kPrepThreads), 0, ctx->stream, R,
                        static_cast<const longlong2 *>(db->b_gs0.p), db->n_groups, db->ref->bad, db->ref->n_blk,
-                       (long long)db->region_per_incid, static_cast<int4 *>(db->b_seg4.p),
-                       static_cast<int4 *>(db->b_groups.p), static_cast<unsigned long long *>(db->b_lo.p), line_map(db),
-                       write);
+                       (long long)db->region_per_incid, checks_of(db), static_cast<int4 *>(db->b_seg4.p),
+                       static_cast<int4 *>(db->b_groups.p));
     return check_launch(ctx, "k_prep_emit_flat");
   }
   hipLaunchKernelGGL(k_prep_emit, dim3((unsigned)db->n_groups), dim3(kPrepThreads), 0, ctx->stream, R,
                      static_cast<const longlong2 *>(db->b_gs0.p), db->n_groups, write, db->ref->bad, db->ref->n_blk,
-                     (long long)db->region_per_incid, const_cast<int32_t *>(db->B.read_end),
-                     static_cast<int4 *>(db->b_seg4.p), static_cast<int4 *>(db->b_groups.p),
+                     (long long)db->region_per_incid, checks_of(db), static_cast<int4 *>(db->b_seg4.p), static_cast<int4 *>(db->b_groups.p),
                      static_cast<unsigned long long *>(db->b_lo.p), line_map(db), db->cursor, db->cursor + kCursors);
   return check_launch(ctx, "k_prep_emit");
 }
@@ -1115,6 +1308,11 @@ int launch_pieces(ganon_ctx *ctx, ganon_dbatch *db) {
   if (!db->n_groups) return GANON_OK;
   KernelScope ks(ctx, "prep_pieces");
   const LineMap M = line_map(db);
+  if (db->flat_mode) {   // the candidates of k_prep_scan mark their lines
+    HIP_OR_FAIL(hipMemsetAsync(db->b_linemap.p, 0, (size_t)line_map_words(db) * 8, st));
+    hipLaunchKernelGGL(k_prep_mark, dim3(grid_for(n_cand)), dim3(kPrepThreads), 0, st,
+                       static_cast<const unsigned long long *>(db->b_lo.p), n_cand, M);
+  }
   hipLaunchKernelGGL(k_prep_linemap, dim3(grid_for(M.n1)), dim3(kPrepThreads), 0, st, M);
   hipLaunchKernelGGL(k_prep_pieces, dim3(grid_for(n_cand)), dim3(kPrepThreads), 0, st,
                      static_cast<const unsigned long long *>(db->b_lo.p), n_cand, M, db->seq_bytes,
@@ -1129,13 +1327,14 @@ namespace ganon_prep {
 int grow(ganon_ctx *ctx, DBuf &b, size_t bytes) {
   const size_t need = bytes + 128;
   if (b.p && b.bytes >= need) return GANON_OK;
+  const size_t old = b.bytes;
   if (b.p) {
     hipStreamSynchronize(ctx->stream);   // a previous run may still read it
     hipFree(b.p);
     b.p = nullptr;
     b.bytes = 0;
   }
-  const size_t alloc = std::max(need, b.bytes + b.bytes / 4);   // some headroom for reloads
+  const size_t alloc = std::max(need, old + old / 4);   // some headroom for reloads
   hipError_t e = hipMalloc(&b.p, alloc);
   if (e != hipSuccess) {
     b.p = nullptr;
@@ -1145,61 +1344,77 @@ int grow(ganon_ctx *ctx, DBuf &b, size_t bytes) {
   return GANON_OK;
 }
 
-int plan(ganon_ctx *ctx, ganon_dbatch *db, const int64_t *host_incid_off) {
+int plan(ganon_ctx *ctx, ganon_dbatch *db) {
   hipStream_t st = ctx->stream;
   int rc;
   const int64_t nr = db->n_reads, ns = db->n_scopes;
-  int32_t *read_end = nullptr;
-  if ((rc = grow_n(ctx, db->b_read_end, nr, &read_end))) return rc;
+  int32_t *read_end = nullptr, *nseg = nullptr;
+  if ((rc = grow_n(ctx, db->b_read_end, (size_t)std::max<int64_t>(nr, 1), &read_end)) ||
+      (rc = grow_n(ctx, db->b_cursor, 4 * kCursors, &db->cursor)))
+    return rc;
   db->B.read_end = read_end;
-  uint8_t *seen = nullptr;
-  if ((rc = grow_n(ctx, db->b_seen, nr, &seen))) return rc;
-  if ((rc = grow_n(ctx, db->b_cursor, 4 * kCursors, &db->cursor))) return rc;   // counters, then bases
+  db->ran = false;
+  db->n_groups = 0;
   const Raw R = raw_of(db);
-  HIP_OR_FAIL(hipMemsetAsync(db->err, 0, sizeof(PrepErr), st));
-  HIP_OR_FAIL(hipMemsetAsync(db->plan_info, 0, 6 * sizeof(unsigned long long), st));
-  int32_t *nseg = nullptr;
-  if ((rc = grow_n(ctx, db->b_nseg, nr, &nseg))) return rc;
-  HIP_OR_FAIL(hipMemsetAsync(seen, 0, (size_t)std::max<int64_t>(nr, 1), st));
-  // 1. per-read and per-scope checks (every later kernel relies on them)
-  if (nr) hipLaunchKernelGGL(k_prep_reads, dim3(grid_for(nr)), dim3(kPrepThreads), 0, st, R, db->err, read_end, nseg,
-                             db->plan_info + 2);
-  if (ns) hipLaunchKernelGGL(k_prep_scope_check, dim3(grid_for(ns)), dim3(kPrepThreads), 0, st, R, db->err,
-                             db->plan_info + 1);
-  if ((rc = check_launch(ctx, "k_prep_reads/k_prep_scope_check")) || (rc = check_err(ctx, db))) return rc;
+  // short-read groups (one-segment and two-pass emits) in closed form from the CSR offsets; the
+  // long-read prep cuts its own from the segments per scope below
+  const int tgt0 = ctx->group_target ? ctx->group_target : 704;
+  const long long w0 = weight_of(tgt0);
+  const int64_t g_bound = ns ? (db->n_incid + w0 * (ns - 1)) / tgt0 + 1 : 1;
+  longlong2 *gm = nullptr;
+  unsigned long long *lo = nullptr, *part = nullptr;
+  const int64_t rb = (nr + kScanReadsPerBlock - 1) / kScanReadsPerBlock;
+  const int64_t sb = (ns + kScanScopesPerBlock - 1) / kScanScopesPerBlock;
+  const int64_t nb = std::max<int64_t>(1, rb + sb);
+  if (nb > INT32_MAX) return fail(ctx, GANON_E_ARG, "batch too large");
+  if ((rc = grow_n(ctx, db->b_gs0, (size_t)g_bound, &gm)) || (rc = grow_n(ctx, db->b_lo, 2 * (size_t)g_bound, &lo)) ||
+      (rc = grow_n(ctx, db->b_part, (size_t)kParts * nb, &part)))
+    return rc;
   {
-    // overflow-region observations per incidence: the longest read's ceil(L / 48) (>= the round-1
-    // bound of aligned bases / 48 per group)
-    unsigned long long max_len = 0, max_seg = 0;
-    HIP_OR_FAIL(hipMemcpyAsync(&max_len, db->plan_info + 3, sizeof max_len, hipMemcpyDeviceToHost, st));
-    HIP_OR_FAIL(hipMemcpyAsync(&max_seg, db->plan_info + 4, sizeof max_seg, hipMemcpyDeviceToHost, st));
-    HIP_OR_FAIL(hipStreamSynchronize(st));
-    // prep mode: long (a read with several segments, or forced), one-segment (every read has at most
-    // one: the default for short reads), or the two-pass short emit (GANON_PARAM_PREP_LONG 0)
-    // auto: the long-read prep (a wave per incidence) only for long reads; short reads with indels
-    // (several segments, a few per cent of the reads) take the two-pass emit — the long prep took
-    // 11.3 ms instead of ~0.2 on a planner-built 2 M-read batch (profiles/r02/planner_batch_bench.json)
-    db->long_mode = ctx->prep_long == 1 || (ctx->prep_long == -1 && max_seg > 1 && max_len > kLongReadLen);
-    db->flat_mode = !db->long_mode && max_seg <= 1 && (ctx->prep_long == -1 || ctx->prep_long == 2);
-    db->region_per_incid = (int64_t)((max_len + 47) / 48);
-    if (!ctx->group_target) db->group_target = db->long_mode ? 1408 : 704;   // auto (sweep_c5 / sweep_c3)
-    if ((double)db->n_incid * (double)db->region_per_incid > 4e9)
-      return fail(ctx, GANON_E_ARG, "batch too large: %lld incidences of reads up to %llu bases (split it)",
-                  (long long)db->n_incid, max_len);
+    // 1. the batch scan: every per-read and per-scope check, read ends, segments per read, the group
+    //    table and candidates of the short-read modes, per-block partials; then their reduction
+    KernelScope ks(ctx, "prep_scan");
+    HIP_OR_FAIL(hipMemsetAsync(db->err, 0, sizeof(PrepErr), st));
+    HIP_OR_FAIL(hipMemsetAsync(lo, 0xFF, 2 * (size_t)g_bound * sizeof(unsigned long long), st));
+    hipLaunchKernelGGL(k_prep_scan, dim3((unsigned)nb), dim3(kPrepThreads), 0, st, R, db->err,
+                       ScanOut{read_end, lo, gm, g_bound, part}, w0, (long long)tgt0, (int)rb);
+    hipLaunchKernelGGL(k_prep_reduce, dim3(1), dim3(kPrepThreads), 0, st, R, part, (int)nb, w0, (long long)tgt0, g_bound,
+                       db->plan_info);
+    if ((rc = check_launch(ctx, "k_prep_scan"))) return rc;
   }
-  // 2. incidences, write scopes
-  if (ns) hipLaunchKernelGGL(k_prep_incid_check, dim3(grid_for(ns)), dim3(kPrepThreads), 0, st, R, read_end, db->err,
-                             seen);
-  if (nr) hipLaunchKernelGGL(k_prep_seen_check, dim3(grid_for(nr)), dim3(kPrepThreads), 0, st, R, seen, db->err);
-  if ((rc = check_launch(ctx, "k_prep_incid_check/k_prep_seen_check")) || (rc = check_err(ctx, db))) return rc;
-  // 3. groups (their number follows from the host's CSR offsets), then a counting emit pass sizes
-  //    the segment records and overflow regions
-  if (db->group_target <= 0) db->group_target = 704;
+  // 2. the one synchronization of a fresh batch: its first error and its shape
+  unsigned long long info[6] = {0, 0, 0, 0, 0, 0};
+  PrepErr e{};
+  HIP_OR_FAIL(hipMemcpyAsync(info, db->plan_info, sizeof info, hipMemcpyDeviceToHost, st));
+  HIP_OR_FAIL(hipMemcpyAsync(&e, db->err, sizeof e, hipMemcpyDeviceToHost, st));
+  HIP_OR_FAIL(hipStreamSynchronize(st));
+  if (e.code) return fail(ctx, GANON_E_ARG, err_text(e.code), e.index, e.a, e.b);
+  const unsigned long long max_len = info[3], max_seg = info[4];
+  // prep mode: long (a read with several segments, or forced), one-segment (every read has at most
+  // one: the default for short reads), or the two-pass short emit (GANON_PARAM_PREP_LONG 0)
+  // auto: the long-read prep (a wave per incidence) only for long reads; short reads with indels
+  // (several segments, a few per cent of the reads) take the two-pass emit — the long prep took
+  // 11.3 ms instead of ~0.2 on a planner-built 2 M-read batch (profiles/r02/planner_batch_bench.json)
+  db->long_mode = ctx->prep_long == 1 || (ctx->prep_long == -1 && max_seg > 1 && max_len > kLongReadLen);
+  db->flat_mode = !db->long_mode && max_seg <= 1 && (ctx->prep_long == -1 || ctx->prep_long == 2);
+  // overflow-region observations per incidence: the longest read's ceil(L / 48)
+  db->region_per_incid = (int64_t)((max_len + 47) / 48);
+  db->group_target = ctx->group_target ? ctx->group_target : db->long_mode ? 1408 : 704;   // auto (sweep_c5 / sweep_c3)
+  db->n_id_ops = (int64_t)info[0];
+  db->max_len = (int64_t)max_len;
+  db->max_seg = (int64_t)max_seg;
+  db->n_huge_scopes = (int32_t)info[1];
+  db->n_written = (int64_t)info[2];
+  if ((double)db->n_incid * (double)db->region_per_incid > 4e9)
+    return fail(ctx, GANON_E_ARG, "batch too large: %lld incidences of reads up to %llu bases (split it)",
+                (long long)db->n_incid, max_len);
   const long long w = weight_of(db->group_target);
-  int64_t ng = ns ? (host_incid_off[ns - 1] + w * (ns - 1)) / db->group_target + 1 : 0;
+  int64_t ng = ns ? (int64_t)info[5] : 0;   // closed-form groups of the target used by the scan
   db->scost = nullptr;
   if (db->long_mode && ns) {
     // groups cut on the prefix of segments per scope: cost[s] = segments of its incidences + w
+    if ((rc = grow_n(ctx, db->b_nseg, (size_t)std::max<int64_t>(nr, 1), &nseg))) return rc;
+    if (nr) hipLaunchKernelGGL(k_prep_nseg, dim3(grid_for(nr)), dim3(kPrepThreads), 0, st, R, nseg);
     int64_t *cost = nullptr;
     if ((rc = grow_n(ctx, db->b_scost, (size_t)ns + 1, &cost))) return rc;
     hipLaunchKernelGGL(k_prep_scope_cost, dim3(grid_for(ns + 1)), dim3(kPrepThreads), 0, st, R, nseg, w, cost);
@@ -1219,6 +1434,8 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db, const int64_t *host_incid_off) {
     if ((rc = grow_n(ctx, db->b_slots, (size_t)ng, &sl)) ||
         (rc = grow_n(ctx, db->b_slot0, (size_t)std::max<int64_t>(db->n_incid, 1), &s0p)))
       return rc;
+  } else if (ns && db->group_target != tgt0) {
+    return fail(ctx, GANON_E_STATE, "group target changed during the plan");
   }
   if (ng > INT32_MAX / kGrpRec) return fail(ctx, GANON_E_ARG, "batch too large: %lld scope groups", (long long)ng);
   db->n_groups = (int32_t)ng;
@@ -1226,45 +1443,45 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db, const int64_t *host_incid_off) {
   int4 *grp = nullptr;
   unsigned long long *u64 = nullptr;
   uint32_t *u32 = nullptr;
-  longlong2 *gm = nullptr;
-  if ((rc = grow_n(ctx, db->b_gs0, ng, &gm)) || (rc = grow_n(ctx, db->b_groups, (size_t)kGrpRec * ng, &grp)) ||
+  // (short-read modes: ng <= g_bound, so the scan's group table and candidates stay in place)
+  if ((rc = grow_n(ctx, db->b_gs0, (size_t)std::max<int64_t>(ng, 1), &gm)) ||
+      (rc = grow_n(ctx, db->b_groups, (size_t)kGrpRec * ng, &grp)) ||
       (rc = grow_n(ctx, db->b_grp_part, 2 * (size_t)ng, &p32)) ||
-      (rc = grow_n(ctx, db->b_lo, 2 * (size_t)ng, &u64)) ||
+      (rc = grow_n(ctx, db->b_wspart, (size_t)std::max<int64_t>(ng, 1), &u64)) ||
+      (rc = grow_n(ctx, db->b_lo, 2 * (size_t)std::max<int64_t>(ng, 1), &u64)) ||
       (rc = grow_n(ctx, db->b_linemap, (size_t)line_map_words(db), &u64)))
     return rc;
-  HIP_OR_FAIL(hipMemsetAsync(db->cursor + kCursors, 0, kCursors * sizeof(unsigned long long), st));
-  if ((rc = launch_groups(ctx, db, R)) || (rc = launch_emit(ctx, db, R, 0)) || (rc = launch_pieces(ctx, db))) return rc;
-  if (ng && nr)
-    hipLaunchKernelGGL(k_prep_farcap, dim3(grid_for(nr)), dim3(kPrepThreads), 0, st, R, w, (long long)db->group_target,
-                       db->long_mode ? db->scost : nullptr, static_cast<const int4 *>(db->b_groups.p), db->plan_info);
-  if ((rc = check_launch(ctx, "k_prep_farcap"))) return rc;
-  unsigned long long info[4] = {0, 0, 0, 0};
-  std::vector<unsigned long long> cur(2 * kCursors, 0);
-  HIP_OR_FAIL(hipMemcpyAsync(info, db->plan_info, sizeof info, hipMemcpyDeviceToHost, st));
-  HIP_OR_FAIL(hipMemcpyAsync(cur.data(), db->cursor, kCursors * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
-  HIP_OR_FAIL(hipStreamSynchronize(st));
-  // sub-counter bases: exclusive prefix of the counting pass's totals (groups with more segments
-  // than incidences only; deterministic per sub-counter)
-  unsigned long long tseg = 0;
-  for (int k = 0; k < kCursors; ++k) {
-    cur[kCursors + k] = tseg;
-    tseg += cur[k];
+  int64_t extra_seg = 0;
+  if (!db->flat_mode && ng) {
+    // two-pass and long-read emits: a counting pass sizes the records of groups with more segments
+    // than incidences (sub-counter bases: exclusive prefix of the pass's totals, deterministic)
+    HIP_OR_FAIL(hipMemsetAsync(db->cursor + kCursors, 0, kCursors * sizeof(unsigned long long), st));
+    if ((rc = launch_groups(ctx, db, R)) || (rc = launch_emit(ctx, db, R, 0))) return rc;
+    std::vector<unsigned long long> cur(2 * kCursors, 0);
+    HIP_OR_FAIL(hipMemcpyAsync(cur.data(), db->cursor, kCursors * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+    HIP_OR_FAIL(hipStreamSynchronize(st));
+    unsigned long long tseg = 0;
+    for (int k = 0; k < kCursors; ++k) {
+      cur[kCursors + k] = tseg;
+      tseg += cur[k];
+    }
+    db->cursor_h.assign(cur.begin() + kCursors, cur.end());
+    HIP_OR_FAIL(hipMemcpyAsync(db->cursor + kCursors, db->cursor_h.data(), kCursors * sizeof(unsigned long long),
+                               hipMemcpyHostToDevice, st));
+    extra_seg = (int64_t)tseg;
   }
-  HIP_OR_FAIL(hipMemcpyAsync(db->cursor + kCursors, cur.data() + kCursors, kCursors * sizeof(unsigned long long),
-                             hipMemcpyHostToDevice, st));
-  HIP_OR_FAIL(hipStreamSynchronize(st));
-  db->n_seg = db->n_incid + (int64_t)tseg;   // record slots: one per incidence, then the long groups
+  db->n_seg = db->n_incid + extra_seg;   // record slots: one per incidence, then the long groups
   db->region = db->n_incid * db->region_per_incid + (int64_t)kGrpObs * ng;
-  // far masks: at most one per nibble of a written read outside its group's pieces. That bound is
-  // exact but loose (masks are the TN-mismatching nibbles only), and a batch whose scopes are not
-  // in genome order can put most written bytes outside their pieces: the list is capped at 2^28
-  // entries (2 GiB); a run that needs more reports it (k_finish status) instead of dropping masks
-  db->far_cap = std::min<int64_t>((int64_t)info[0], kFarMax);
-  db->n_huge_scopes = (int32_t)info[1];
-  db->n_written = (int64_t)info[2];
+  // far masks (bytes a group masks outside its own pieces, applied by k_finish): the list keeps its
+  // capacity across batches; a run that needs more reports the count (k_finish) and
+  // ganon_batch_download grows the list and runs again — no counting pass, no synchronization here
+  const int64_t far_want = ctx->far_init > 0 ? (int64_t)ctx->far_init
+                                             : std::min<int64_t>(kFarMax, std::max<int64_t>(int64_t(1) << 16, db->n_reads / 8));
+  db->far_cap = std::max<int64_t>(db->far_cap_alloc, far_want);
   int4 *s4 = nullptr;
-  if ((rc = grow_n(ctx, db->b_seg4, (size_t)db->n_seg, &s4))) return rc;
+  if ((rc = grow_n(ctx, db->b_seg4, (size_t)std::max<int64_t>(db->n_seg, 1), &s4))) return rc;
   if ((rc = grow_n(ctx, db->b_far, (size_t)db->far_cap, &u64))) return rc;
+  db->far_cap_alloc = db->far_cap;
   if ((rc = grow_n(ctx, db->b_gokey, (size_t)db->region, &u64)) || (rc = grow_n(ctx, db->b_gopay, (size_t)db->region, &u64)) ||
       (rc = grow_n(ctx, db->b_gtkey, 2 * (size_t)db->region + 64, &u64)) ||
       (rc = grow_n(ctx, db->b_gtflag, 2 * (size_t)db->region + 64, &u32)))
@@ -1276,8 +1493,26 @@ int run(ganon_ctx *ctx, ganon_dbatch *db) {
   const Raw R = raw_of(db);
   int rc;
   if (!db->n_groups) return GANON_OK;
+  if (db->flat_mode) {   // the scan's group table is in place
+    if ((rc = launch_pieces(ctx, db))) return rc;
+    return db->fused_emit ? GANON_OK : launch_emit(ctx, db, R, 1);   // (fused: the group kernel emits)
+  }
   if ((rc = launch_groups(ctx, db, R)) || (rc = launch_emit(ctx, db, R, 1))) return rc;
   return launch_pieces(ctx, db);
+}
+
+int ws_diag(ganon_ctx *ctx, ganon_dbatch *db) {
+  hipLaunchKernelGGL(k_prep_ws_diag, dim3(grid_for(db->n_reads)), dim3(kPrepThreads), 0, ctx->stream, raw_of(db),
+                     db->err);
+  return check_launch(ctx, "k_prep_ws_diag");
+}
+
+int batch_error(ganon_ctx *ctx, ganon_dbatch *db) {
+  PrepErr e{};
+  HIP_OR_FAIL(hipMemcpyAsync(&e, db->err, sizeof e, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_OR_FAIL(hipStreamSynchronize(ctx->stream));
+  if (e.code) return fail(ctx, GANON_E_ARG, err_text(e.code), e.index, e.a, e.b);
+  return GANON_OK;
 }
 
 }  // namespace ganon_prep

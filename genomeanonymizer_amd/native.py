@@ -156,6 +156,7 @@ def hip_lib():
     lib.ganon_batch_upload.argtypes = [_p, C.POINTER(GanonBatch), C.POINTER(_p)]
     lib.ganon_batch_upload_ref.argtypes = [_p, C.POINTER(GanonBatch), _p, C.POINTER(_p)]
     lib.ganon_batch_reload.argtypes = [_p, _p, C.POINTER(GanonBatch)]
+    lib.ganon_batch_replan.argtypes = [_p, _p]
     lib.ganon_ref_upload.argtypes = [_p, _u8p, C.c_int64, C.POINTER(_p)]
     lib.ganon_ref_free.argtypes = [_p, _p]
     lib.ganon_batch_run.argtypes = [_p, _p]
@@ -166,6 +167,7 @@ def hip_lib():
     lib.ganon_batch_copy_totals.argtypes = [_p, _p, _p]
     lib.ganon_last_kernel_times.argtypes = [_p, C.POINTER(KernelTime), C.c_int]
     lib.ganon_batch_info.argtypes = [_p, _i64p]
+    lib.ganon_batch_shape.argtypes = [_p, _i64p]
     lib.ganon_batch_path_counts.argtypes = [_p, _p, _i64p]
     lib.ganon_fastq_upload.argtypes = [_p, C.POINTER(GanonFastqRecords), C.POINTER(_p)]
     lib.ganon_fastq_run.argtypes = [_p, _p]
@@ -185,7 +187,7 @@ def hip_lib():
     lib.ganon_indel_download.restype = C.c_int64
     lib.ganon_indel_info.argtypes = [_p, _i64p]
     lib.ganon_indel_free.argtypes = [_p, _p]
-    if lib.ganon_abi_version() != 3:
+    if lib.ganon_abi_version() != 4:
         raise GanonError("libganon_hip.so ABI version mismatch")
     _hip = lib
     return lib
@@ -202,13 +204,16 @@ PARAM_INDEL_SORT = 8     # include/ganon.h GANON_PARAM_INDEL_SORT (0 segmented, 
 PARAM_PREP_LONG = 9      # include/ganon.h GANON_PARAM_PREP_LONG (-1 auto, 0 never, 1 always; at upload)
 PARAM_GROUP_OBS = 10     # include/ganon.h GANON_PARAM_GROUP_OBS (0 auto, 512, 1024)
 PARAM_PREP_UNROLL = 11   # include/ganon.h GANON_PARAM_PREP_UNROLL (0 auto, 1, 2, 4)
+PARAM_FAR_INIT = 12      # include/ganon.h GANON_PARAM_FAR_INIT (first far-mask list capacity; 0 auto)
+PARAM_FUSE_EMIT = 13     # include/ganon.h GANON_PARAM_FUSE_EMIT (1: the group kernel emits its records)
 
 EXPORTED_HIP_SYMBOLS = (
     "ganon_ctx_create", "ganon_ctx_destroy", "ganon_last_error", "ganon_abi_version",
     "ganon_ctx_set_stream", "ganon_ctx_set_profiling", "ganon_ctx_set_variant", "ganon_ctx_set_param", "ganon_mask_batch",
-    "ganon_ref_upload", "ganon_ref_free", "ganon_batch_upload", "ganon_batch_upload_ref", "ganon_batch_reload",
+    "ganon_ref_upload", "ganon_ref_free", "ganon_batch_upload", "ganon_batch_upload_ref", "ganon_batch_reload", "ganon_batch_replan",
     "ganon_batch_run", "ganon_batch_sync", "ganon_batch_download", "ganon_batch_free",
     "ganon_batch_device_totals", "ganon_batch_copy_totals", "ganon_last_kernel_times", "ganon_batch_info",
+    "ganon_batch_shape",
     "ganon_batch_path_counts",
     "ganon_fastq_upload", "ganon_fastq_run", "ganon_fastq_bytes", "ganon_fastq_device_output",
     "ganon_fastq_download", "ganon_fastq_free", "ganon_fastq_format_hip",
@@ -553,6 +558,11 @@ class DeviceBatch:
         self.seq_bytes = b.seq_bytes
         self.n_scopes = b.n_scopes
 
+    def replan(self) -> None:
+        """ganon_batch_replan: plan the device arrays again exactly as a fresh upload would
+        (validation scan, prep mode, sizes; one synchronization)."""
+        self.m._check(self.m._lib.ganon_batch_replan(self.m._h, self.h), "ganon_batch_replan")
+
     def run(self) -> None:
         self.m._check(self.m._lib.ganon_batch_run(self.m._h, self.h), "ganon_batch_run")
 
@@ -595,6 +605,13 @@ class DeviceBatch:
         keys = ("groups", "segments", "huge_scopes", "huge_tiles", "far_capacity", "huge_written_reads",
                 "overflow_region", "written_reads")
         return dict(zip(keys, a.tolist()))
+
+    def shape(self) -> dict:
+        """ganon_batch_shape: what the device scan of the last plan found."""
+        a = np.zeros(4, np.int64)
+        self.m._check(self.m._lib.ganon_batch_shape(self.h, _ptr(a, _i64p)), "batch_shape")
+        return {"id_ops": int(a[0]), "max_len": int(a[1]), "max_seg": int(a[2]),
+                "prep_mode": ("two_pass", "long_read", "one_segment")[int(a[3])]}
 
     def kernel_times(self) -> list:
         arr = (KernelTime * 32)()

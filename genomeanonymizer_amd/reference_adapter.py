@@ -405,7 +405,10 @@ class GpuCompleteGermlineAnonymizer:
 
     def anonymize(self, variant_to_keep, tumor_normal_pileup, ref_genome,
                   stats_recorder=None) -> Generator[list, None, None]:
-        columns = [tuple(p) for p in tumor_normal_pileup]
+        # pysam columns are views of the pileup engine's live buffer (the next step of the iterator
+        # overwrites them): every column is copied while it is current, its reads as
+        # (alignment, query_position) — pysam's PileupRead.alignment is a copy of the record
+        columns = [tuple(None if c is None else _ColumnSnapshot(c) for c in p) for p in tumor_normal_pileup]
         _, snv_calls, indel_calls = self._device_calls(columns, variant_to_keep, ref_genome)
         # the kept window variant is never masked nor counted (AM:546-547): SNVs on the device,
         # indels here (their identity includes the allele)
@@ -440,6 +443,24 @@ class GpuCompleteGermlineAnonymizer:
             self._mask_left_overs(pair[PAIR_1_IDX], pair[PAIR_2_IDX])
             yield pair
         self.reset()
+
+
+class _ReadSnapshot:
+    __slots__ = ("alignment", "query_position")
+
+    def __init__(self, pr):
+        self.alignment = pr.alignment
+        self.query_position = pr.query_position
+
+
+class _ColumnSnapshot:
+    """The parts of a pysam PileupColumn the adapter reads, copied while the column is current."""
+    __slots__ = ("reference_pos", "reference_name", "pileups")
+
+    def __init__(self, col):
+        self.reference_pos = col.reference_pos
+        self.reference_name = col.reference_name
+        self.pileups = [_ReadSnapshot(pr) for pr in col.pileups]
 
 
 def _supplementary_hash(aln, model) -> str:

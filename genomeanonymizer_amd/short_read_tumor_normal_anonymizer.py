@@ -68,7 +68,8 @@ def anonymize_genome(windows_in_sample: List[Window], tumor_bam_file: str, norma
         write_statistics(f"{normal_bam_file}.statistics.txt", statistics_rows(plan, res))
     t4 = time.time()
     timing = {"decode_s": t1 - t0, "plan_s": t2 - t1, "mask_s": t3 - t2, "write_s": t4 - t3,
-              "reads": int(tumor.n + normal.n), "scopes": len(plan.scopes)}
+              "reads": int(tumor.n + normal.n), "bases": int(tumor.l_seq.sum() + normal.l_seq.sum()),
+              "scopes": len(plan.scopes)}
     log.info("Anonymization complete for samples %s and %s: %s", tumor_output_fastq, normal_output_fastq, timing)
     return timing
 

@@ -516,7 +516,7 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
     if block_size is None:
         block_size = _writer.io_block_size(os.path.dirname(os.path.abspath(tumor_out)))
     timing = {"decode_s": 0.0, "plan_s": 0.0, "mask_s": 0.0, "format_s": 0.0, "prefetch_s": 0.0, "resolve_s": 0.0, "write_s": 0.0, "prunes": 0, "jobs": 0,
-              "reads": 0}
+              "reads": 0, "bases": 0}
     failure: Optional[BaseException] = None
     if rank == 0:
         for p in paths:
@@ -571,6 +571,7 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
                         timing[k] += job.timing[k]
                     timing["jobs"] += 1
                     timing["reads"] += int(job.tables[0].n + job.tables[1].n)
+                    timing["bases"] += int(job.tables[0].l_seq.sum(dtype=np.int64) + job.tables[1].l_seq.sum(dtype=np.int64))
                     totals += np.asarray(job.res.totals, np.int64)[:8]
                 except BaseException as e:   # every rank must reach the gathers
                     failure, err = e, repr(e)
@@ -613,10 +614,14 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
                 if failure is not None:
                     raise failure
                 raise RuntimeError(f"another rank failed: {errs[0]}")
+            try:
+                for f in range(4):
+                    off = base[f] + sum(sizes[r]["sizes"][f] for r in range(rank))
+                    if data[f]:
+                        os.pwrite(fds[f], data[f], off)
+            except BaseException as e:   # reported at the next exchange (every rank reaches it)
+                failure = failure or e
             for f in range(4):
-                off = base[f] + sum(sizes[r]["sizes"][f] for r in range(rank))
-                if data[f]:
-                    os.pwrite(fds[f], data[f], off)
                 base[f] += sum(g["sizes"][f] for g in sizes)
             # carried records still reachable: pending pairs and the end-of-sample candidates (pruned
             # when the carry has doubled or every 16 rounds: each pass walks the whole carry)
@@ -641,27 +646,39 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
             timing["resolve_s"] += t1 - t0
             timing["write_s"] += time.time() - t1
         # ---- end of the sample: pair_unmapped_mates, single ends (SR:561-622) ----
-        cand = np.concatenate(cands) if cands else np.zeros((0, 7), np.int64)
-        tail, single, wse = resolver.finish(cand, cand_names)
-        replay.run(resolver.take_log())
-        if rank == 0:
-            per_file: List[List[bytes]] = [[], [], [], []]
-            def carried(k):
-                if k[2] == -2:
-                    return replay.take(k[3])
-                b = carry.get(k)
-                return b if b is not None else carry[k[:4] + (0,)]
-            for w in tail.tolist():
-                per_file[2 * w[0] + w[1]].append(carried((w[2], w[3], w[4], w[5], w[6])))
-            for f in range(4):
-                blob = b"".join(per_file[f])
-                if blob:
-                    os.pwrite(fds[f], blob, base[f])
-            if wse:
-                for d, prefix in enumerate((tumor_out, normal_out)):
-                    with open(f"{prefix}.single_end.fastq", "wb") as fh:
-                        fh.write(b"".join(carried(tuple(x)) for x in single[d].tolist()))
-        all_stats = comm.allgather(stats_rows)
+        err = repr(failure) if failure is not None else None
+        if failure is None:
+            try:
+                cand = np.concatenate(cands) if cands else np.zeros((0, 7), np.int64)
+                tail, single, wse = resolver.finish(cand, cand_names)
+                replay.run(resolver.take_log())
+                if rank == 0:
+                    per_file: List[List[bytes]] = [[], [], [], []]
+
+                    def carried(k):
+                        if k[2] == -2:
+                            return replay.take(k[3])
+                        b = carry.get(k)
+                        return b if b is not None else carry[k[:4] + (0,)]
+                    for w in tail.tolist():
+                        per_file[2 * w[0] + w[1]].append(carried((w[2], w[3], w[4], w[5], w[6])))
+                    for f in range(4):
+                        blob = b"".join(per_file[f])
+                        if blob:
+                            os.pwrite(fds[f], blob, base[f])
+                    if wse:
+                        for d, prefix in enumerate((tumor_out, normal_out)):
+                            with open(f"{prefix}.single_end.fastq", "wb") as fh:
+                                fh.write(b"".join(carried(tuple(x)) for x in single[d].tolist()))
+            except BaseException as e:   # every rank reaches the gather below, then all raise
+                failure, err = e, repr(e)
+        gathered = comm.allgather({"stats": stats_rows, "err": err})
+        errs = [g["err"] for g in gathered if g["err"] is not None]
+        if errs:
+            if failure is not None:
+                raise failure
+            raise RuntimeError(f"another rank failed: {errs[0]}")
+        all_stats = [g["stats"] for g in gathered]
         if rank == 0 and record_statistics:
             merged: Dict[str, List[int]] = {OUTSIDE_WINDOWS: [0] * 8}
             for _, rows in sorted((x for part in all_stats for x in part), key=lambda t: t[0]):

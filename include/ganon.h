@@ -35,7 +35,7 @@
 #define GANON_API __attribute__((visibility("default")))
 #endif
 
-#define GANON_ABI_VERSION 3
+#define GANON_ABI_VERSION 4
 
 enum {
   GANON_OK = 0,
@@ -140,7 +140,14 @@ GANON_API int ganon_ctx_set_variant(ganon_ctx *ctx, int variant);
 enum { GANON_PARAM_GROUP_UNROLL = 1, GANON_PARAM_GROUP_SKIP = 2, GANON_PARAM_GROUP_TARGET = 3,
        GANON_PARAM_NT_COPY = 4, GANON_PARAM_REF2 = 5, GANON_PARAM_FASTQ_SKIP = 6, GANON_PARAM_FASTQ_KD = 7,
        GANON_PARAM_INDEL_SORT = 8, GANON_PARAM_PREP_LONG = 9, GANON_PARAM_GROUP_OBS = 10,
-       GANON_PARAM_PREP_UNROLL = 11 };
+       GANON_PARAM_PREP_UNROLL = 11, GANON_PARAM_FAR_INIT = 12, GANON_PARAM_FUSE_EMIT = 13 };
+/* GANON_PARAM_FUSE_EMIT: in the one-segment prep mode the group kernel builds each tile's segment
+ * records from the incidences itself (1) instead of reading those the prep's emit kernel wrote to
+ * HBM (0, default: the in-kernel gathers stall the group kernel more than the emit kernel costs,
+ * DESIGN.md 4a). Same results. */
+/* GANON_PARAM_FAR_INIT: first capacity of a batch's far-mask list (entries; 0 = auto, n_reads / 8 but
+ * at least 65536). A run that needs more is run again by ganon_batch_download with the list grown
+ * to the count it needed (testing knob: 1 forces that path). */
 /* GANON_PARAM_PREP_UNROLL: incidences each thread of the one-segment prep emit takes per trip (1, 2,
  * 4; 0 = default). */
 /* GANON_PARAM_GROUP_OBS: observations a group keeps in LDS before its list overflows into the global
@@ -164,17 +171,23 @@ GANON_API int ganon_ref_upload(ganon_ctx *ctx, const uint8_t *ref_nt16, int64_t 
 GANON_API int ganon_ref_free(ganon_ctx *ctx, ganon_ref *ref);
 
 /* Device-resident path (streaming, benchmarks, multi-GPU shards). Upload copies only the raw
- * ganon_batch arrays to HBM and validates and plans them on the device (synchronous). Every
- * ganon_batch_run first rebuilds the derived layer (per-read CIGAR walk into aligned segments,
- * scope groups, output partitions) from those raw arrays on the device, then masks: a run does
- * all the work of anonymizing the batch. ganon_batch_upload uploads the batch's own reference;
+ * ganon_batch arrays to HBM and plans them on the device: one scan validates every read and scope
+ * and sizes the derived layer (one synchronization). Every ganon_batch_run rebuilds the derived
+ * layer (per-incidence CIGAR walk into aligned segments, output partitions) from those raw arrays
+ * on the device, then masks. The incidence checks (read index, read inside its scope's span) and
+ * the write-scope check run inside the run; their errors (GANON_E_ARG) are returned by
+ * ganon_batch_download. ganon_batch_upload uploads the batch's own reference;
  * ganon_batch_upload_ref uses a resident one. ganon_batch_reload replaces the contents of an
  * uploaded batch with another host batch, reusing its device buffers (grow-only) and its
- * reference (resident, or the new batch's own) — the double-buffered streaming path. */
+ * reference (resident, or the new batch's own) — the double-buffered streaming path.
+ * ganon_batch_replan plans the batch's device arrays again from scratch, exactly as a fresh upload
+ * of the same contents would (for arrays another stream or kernel wrote in place, and for timing
+ * what a fresh batch costs: replan + run). Since ABI 4. */
 GANON_API int ganon_batch_upload(ganon_ctx *ctx, const ganon_batch *batch, ganon_dbatch **out);
 GANON_API int ganon_batch_upload_ref(ganon_ctx *ctx, const ganon_batch *batch, const ganon_ref *ref,
                                      ganon_dbatch **out);
 GANON_API int ganon_batch_reload(ganon_ctx *ctx, ganon_dbatch *db, const ganon_batch *batch);
+GANON_API int ganon_batch_replan(ganon_ctx *ctx, ganon_dbatch *db);
 GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db);      /* async on the stream */
 GANON_API int ganon_batch_sync(ganon_ctx *ctx);
 GANON_API int ganon_batch_download(ganon_ctx *ctx, ganon_dbatch *db, uint8_t *seq_out_nt16,
@@ -199,6 +212,10 @@ GANON_API int ganon_last_kernel_times(ganon_ctx *ctx, ganon_kernel_time *out, in
  * path), huge-scope tiles, far-mask capacity (nibbles), reads written by huge scopes, overflow-region
  * entries, written reads]. */
 GANON_API int ganon_batch_info(ganon_dbatch *db, int64_t *info8);
+/* Shape of the planned batch, from the device scan: [I/D CIGAR ops (0: the indel tally has nothing
+ * to do), longest read, most aligned segments of one read, prep mode (0 two-pass, 1 long-read,
+ * 2 one-segment)]. Since ABI 4. */
+GANON_API int ganon_batch_shape(ganon_dbatch *db, int64_t *shape4);
 /* How often the group kernel took its rarer paths since upload (synchronous): [lists of more than
  * 256 observations classified after an LDS sort, lists of more than 512 classified from the
  * group's global overflow region, key-range splits of an overflowing region, 0]. */

@@ -190,14 +190,33 @@ class PileupRead:
         self.query_position = qpos
 
 
-class PileupColumn:
-    __slots__ = ("reference_id", "reference_name", "reference_pos", "pileups")
+class _PileupCursor:
+    """State shared by the columns of one pileup iterator. pysam's PileupColumn reads its reads
+    from the pileup engine's live buffer, which the next step of the iterator overwrites: a column
+    kept past that step shows other reads (or raises once the iterator finished). The stub makes
+    that misuse loud: ``pileups`` of a column the iterator has moved past raises."""
+    __slots__ = ("gen",)
 
-    def __init__(self, tid, name, pos, pileups):
+    def __init__(self):
+        self.gen = 0
+
+
+class PileupColumn:
+    __slots__ = ("reference_id", "reference_name", "reference_pos", "_pileups", "_cursor", "_gen")
+
+    def __init__(self, tid, name, pos, pileups, cursor=None):
         self.reference_id = tid
         self.reference_name = name
         self.reference_pos = pos
-        self.pileups = pileups
+        self._pileups = pileups
+        self._cursor = cursor
+        self._gen = cursor.gen if cursor is not None else 0
+
+    @property
+    def pileups(self):
+        if self._cursor is not None and self._cursor.gen != self._gen:
+            raise ValueError("PileupColumn accessed after its iterator moved on (pysam: live pileup buffer)")
+        return self._pileups
 
     @property
     def nsegments(self):
@@ -304,17 +323,22 @@ def _pileup_columns(reads, tid, name):
     active: List[AlignedSegment] = []
     n = len(reads)
     pos = reads[0].reference_start if reads else 0
-    while i < n or active:
-        while i < n and reads[i].reference_start <= pos:
-            active.append(reads[i]); i += 1
-        active = [r for r in active if r._end > pos]
-        if active:
-            yield PileupColumn(tid, name, pos, [PileupRead(r, _qpos_at(r, pos)) for r in active])
-            pos += 1
-        elif i < n:
-            pos = reads[i].reference_start
-        else:
-            break
+    cur = _PileupCursor()
+    try:
+        while i < n or active:
+            while i < n and reads[i].reference_start <= pos:
+                active.append(reads[i]); i += 1
+            active = [r for r in active if r._end > pos]
+            if active:
+                yield PileupColumn(tid, name, pos, [PileupRead(r, _qpos_at(r, pos)) for r in active], cur)
+                cur.gen += 1     # the engine's buffer moves on
+                pos += 1
+            elif i < n:
+                pos = reads[i].reference_start
+            else:
+                break
+    finally:
+        cur.gen += 1
 
 
 class FastaFile:

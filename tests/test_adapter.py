@@ -93,3 +93,17 @@ def test_adapter_matches_reference_on_gpu(name, hip_built):
         check(name, run_adapter(name, m))
     finally:
         m.close()
+
+
+def test_stub_pileup_columns_are_live_views():
+    """pysam's PileupColumn is a view of the pileup engine's live buffer: the stub raises when a
+    column is read after its iterator moved on, so a consumer that stores columns (the pattern the
+    adapter snapshots against) fails here instead of reading another column's reads."""
+    pysam = _pysam()
+    d = os.path.join(GOLD, "snv")
+    T = pysam.AlignmentFile(os.path.join(d, "t.bam"))
+    contig = T.references[0]
+    cols = list(T.pileup(reference=contig, start=0, end=T.lengths[0], stepper="nofilter"))
+    assert len(cols) > 2
+    with pytest.raises(ValueError):
+        cols[0].pileups

@@ -18,7 +18,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, name, workdir, q, engine="oracle", fail_rank=-1):
+def _worker(rank, world, port, name, workdir, q, engine="oracle", fail_rank=-1, fail_stage="job"):
     import sys
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [repo, os.path.join(repo, "oracle"), os.path.join(repo, "tests")]
@@ -44,7 +44,11 @@ def _worker(rank, world, port, name, workdir, q, engine="oracle", fail_rank=-1):
         if rank == fail_rank:
             def boom(*a, **k):
                 raise RuntimeError("injected failure")
-            anon.anonymize = boom
+            if fail_stage == "tail":      # the end-of-sample stage (pair_unmapped_mates, single ends)
+                from genomeanonymizer_amd import native
+                native.Resolver.finish = boom
+            else:
+                anon.anonymize = boom
         tot = anonymize_genome_sharded(windows, paths["T"], paths["N"], paths["ref"], name_output(paths["T"]),
                                        name_output(paths["N"]), True, anon, dist)
         q.put((rank, tot))
@@ -80,16 +84,19 @@ def test_two_rank_contig_shards_match_reference(name, index, tmp_path):
     assert open(paths["N"] + ".statistics.txt").read() == open(os.path.join(GOLDEN, name, "normal.statistics.txt")).read()
 
 
-def test_a_failing_rank_stops_every_rank(tmp_path):
-    """A rank that raises still reaches the error-flag all-reduce: the other rank raises too
-    instead of waiting in a collective forever (distributed.py)."""
+@pytest.mark.parametrize("fail_rank,stage", [(1, "job"), (0, "tail")])
+def test_a_failing_rank_stops_every_rank(tmp_path, fail_rank, stage):
+    """A rank that raises — in a contig job, or rank 0 in the end-of-sample stage — still reaches
+    the next exchange with its error flag: the other rank raises too instead of waiting in a
+    collective forever (ADVICE r1 distributed.py, r2 stream.py)."""
     from genomeanonymizer_amd.synth.generate import generate, scenario
     workdir = str(tmp_path / "tiny")
     generate(scenario("tiny"), os.path.join(workdir, "in"))
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, "tiny", workdir, q, "oracle", 1)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, "tiny", workdir, q, "oracle", fail_rank, stage))
+             for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:

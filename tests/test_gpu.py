@@ -536,3 +536,82 @@ def test_two_pass_prep_matches_oracle(masker_twopass, oracle, seed):
     bad = [r for r in _all_reads_equal(arr, out, o_out) if in_batch[r] or arr["write_scope"][r] >= 0]
     assert bad == []
     assert np.array_equal(calls, o_calls) and np.array_equal(bases, o_bases)
+
+
+def test_replan_is_a_fresh_upload(masker, oracle):
+    """ganon_batch_replan plans the resident raw arrays again from scratch (the bench's fresh-batch
+    step): after reloading another batch and replanning, every run equals a one-shot mask; repeated
+    replans leave nothing behind."""
+    from genomeanonymizer_amd.synth.batch import config2_batch, random_batch
+    a, _ = config2_batch(n_reads=150_000, genome=40_000_000, n_windows=12_000, n_germline=30_000, seed=21)
+    b = random_batch(41, n_scopes=60, rare_frac=0.2, wide_scopes=3)
+    want_a, want_b = masker.mask(a), masker.mask(b)
+    db = masker.upload(a)
+    try:
+        for arr, want in ((a, want_a), (b, want_b), (a, want_a)):
+            if db.seq_bytes != len(arr["seq_nt16"]) or arr is b:
+                db.reload(arr)
+            for _ in range(3):
+                db.replan()
+                db.run()
+            got = db.download()
+            for k in range(4):
+                assert np.array_equal(got[k], want[k]), k
+            assert db.shape()["prep_mode"] == "one_segment" or arr is b
+    finally:
+        db.free()
+    o_out, o_calls, o_bases, _ = oracle.mask(a)
+    assert np.array_equal(want_a[0], o_out) and np.array_equal(want_a[1], o_calls)
+
+
+def test_far_list_overflow_grows_and_reruns(hip_built, oracle):
+    """A far-mask list too small for the run (GANON_PARAM_FAR_INIT 1): k_finish reports the count it
+    needed, ganon_batch_download grows the list and runs again — the bytes equal the oracle's."""
+    from genomeanonymizer_amd import native
+    from genomeanonymizer_amd.synth.batch import config2_batch, relayout
+    arr, _ = config2_batch(n_reads=200_000, genome=60_000_000, n_windows=20_000, n_germline=40_000, seed=8)
+    sh = relayout(arr, np.random.default_rng(3).permutation(len(arr["read_len"])))
+    o_out, o_calls, o_bases, _ = oracle.mask(sh)
+    m = native.HipMasker(0)
+    try:
+        m.set_param(native.PARAM_FAR_INIT, 1)
+        db = m.upload(sh)
+        try:
+            assert db.info()["far_capacity"] == 1
+            db.run()
+            out, calls, bases, tot = db.download()
+            assert db.info()["far_capacity"] > 1
+        finally:
+            db.free()
+    finally:
+        m.close()
+    assert o_bases.sum() > 10
+    assert np.array_equal(out, o_out) and np.array_equal(calls, o_calls) and np.array_equal(bases, o_bases)
+
+
+def test_incidence_errors_are_reported_by_download(masker):
+    """The incidence checks run inside the device prep of every run: a read listed outside its
+    scope's span, or a read index out of range, fails the download (GANON_E_ARG), never a fault."""
+    from genomeanonymizer_amd import native
+    from genomeanonymizer_amd.synth.batch import random_batch
+    arr = random_batch(5, n_scopes=16)
+    bad = dict(arr)
+    bad["incid_read"] = arr["incid_read"].copy()
+    bad["incid_read"][3] = len(arr["read_len"]) + 100
+    db = masker.upload(bad)
+    try:
+        db.run()
+        with pytest.raises(native.GanonError, match="out of range"):
+            db.download()
+    finally:
+        db.free()
+    bad = dict(arr)
+    bad["write_scope"] = arr["write_scope"].copy()
+    r = int(np.nonzero(arr["write_scope"] >= 0)[0][0])
+    others = [s for s in range(len(arr["scope_span_len"])) if s != arr["write_scope"][r]]
+    # a scope that does not list read r (the write-scope check after the masking kernels)
+    lists = {s: set(arr["incid_read"][arr["scope_incid_off"][s]:arr["scope_incid_off"][s + 1]].tolist()) for s in others}
+    s_bad = next(s for s in others if r not in lists[s])
+    bad["write_scope"][r] = s_bad
+    with pytest.raises(native.GanonError, match="does not list it exactly once"):
+        masker.mask(bad)

@@ -2,15 +2,19 @@
 """End-to-end timing of the product pipeline on one tumor/normal pair (BAM decode -> native
 planner -> GPU masking + indel tally -> GPU FASTQ formatting -> files), the path a user of the
 CLI runs: the streamed path (per contig, bounded memory; the default) and the whole-sample path.
-Prints one JSON line with per-stage seconds, reads/s and the process's peak RSS per mode.
+Prints one JSON line with per-stage seconds, reads/s, bases/s and the process's peak RSS per mode.
 
     python tools/e2e_bench.py DIR [OUTDIR] [stream,whole]   # DIR: tumor.bam normal.bam ref.fa variants.vcf
-                                                             # (tools/e2e_data.py)
+                                                             # (tools/e2e_data.py, synth/fastpair.py)
+    E2E_ENGINE=oracle ...    # the CPU path: the C oracle (E2E_THREADS threads) masks, the host C++
+                             # formatter formats (bench.py's CPU end-to-end baseline; test infrastructure)
+    E2E_RUNS=N ...           # timed runs per mode after one untimed warm run (default 1)
     E2E_PROFILE=PREFIX ...   # cProfile of the timed run of each mode -> PREFIX_<mode>.txt (main thread)
     GANON_PREFETCH=N ...     # look-ahead planning threads of the streamed path (0: in line)
 """
 import json
 import os
+import resource
 import sys
 import time
 
@@ -18,12 +22,31 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 
+def _engine():
+    from genomeanonymizer_amd.anonymizer_methods import CompleteGermlineAnonymizer
+    if os.environ.get("E2E_ENGINE", "hip") == "oracle":
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        from pyoracle import OracleEngine
+        from genomeanonymizer_amd import native
+
+        class CpuEngine(OracleEngine):
+            """The C oracle's masking + the host C++ formatter (libganon_host.so)."""
+
+            def format_fastq(self, recs):
+                return native.host_format_fastq(recs)
+        eng = CpuEngine()
+        eng.threads = int(os.environ.get("E2E_THREADS", "16"))
+        return CompleteGermlineAnonymizer(engine=eng)
+    anon = CompleteGermlineAnonymizer(device=0)
+    anon.engine   # context creation outside the timed stages
+    return anon
+
+
 def main():
     d = sys.argv[1]
     out = sys.argv[2] if len(sys.argv) > 2 else os.path.join(REPO, "gpurun_out", "e2e")
     os.makedirs(out, exist_ok=True)
     from genomeanonymizer_amd import short_read_tumor_normal_anonymizer as sr
-    from genomeanonymizer_amd.anonymizer_methods import CompleteGermlineAnonymizer
     from genomeanonymizer_amd.io.fasta import FastaRef
     from genomeanonymizer_amd.io.vcf import read_vcf
     from genomeanonymizer_amd.planner import get_windows
@@ -31,16 +54,15 @@ def main():
     fasta = FastaRef(os.path.join(d, "ref.fa"))
     windows = get_windows(read_vcf(os.path.join(d, "variants.vcf")), dict(fasta.index))
     t_win = time.time() - t0
-    anon = CompleteGermlineAnonymizer(device=0)
-    anon.engine   # context creation outside the timed stages
-    import resource
-    res = {"windows_s": round(t_win, 3)}
+    anon = _engine()
+    res = {"windows_s": round(t_win, 3), "engine": os.environ.get("E2E_ENGINE", "hip")}
     modes = sys.argv[3].split(",") if len(sys.argv) > 3 else ["stream", "whole"]
+    n_timed = int(os.environ.get("E2E_RUNS", "1"))
     for mode in modes:
         runs = []
-        for it in range(2):    # the first run pays one-time costs (module loads, device init)
+        for it in range(1 + n_timed):    # the first run pays one-time costs (module loads, device init)
             prof = None
-            if it == 1 and os.environ.get("E2E_PROFILE"):   # cProfile of the timed run -> E2E_PROFILE path
+            if it == n_timed and os.environ.get("E2E_PROFILE"):   # cProfile of the last timed run
                 import cProfile
                 prof = cProfile.Profile()
                 prof.enable()
@@ -57,11 +79,18 @@ def main():
                     pstats.Stats(prof, stream=f).sort_stats("cumulative").print_stats(60)
                     pstats.Stats(prof, stream=f).sort_stats("tottime").print_stats(40)
             runs.append(tim)
-        tim = runs[-1]
-        res[mode] = {"reads": tim["reads"], "stages_s": {k: round(v, 3) for k, v in tim.items() if k.endswith("_s")},
-                     "reads_per_s": round(tim["reads"] / tim["wall_s"], 1),
+        timed = runs[1:]
+        best = min(timed, key=lambda t: t["wall_s"])
+        bases = int(best.get("bases", 0))
+        res[mode] = {"reads": best["reads"], "bases": bases,
+                     "stages_s": {k: round(v, 3) for k, v in best.items() if k.endswith("_s")},
+                     "reads_per_s": round(best["reads"] / best["wall_s"], 1),
+                     "bases_per_s": round(bases / best["wall_s"], 1),
+                     "wall_s_runs": [round(t["wall_s"], 3) for t in timed],
                      "peak_rss_mb": resource.getrusage(resource.RUSAGE_SELF).ru_maxrss // 1024,
-                     "first_run_wall_s": round(runs[0]["wall_s"], 3)}
+                     "first_run_wall_s": round(runs[0]["wall_s"], 3),
+                     "output_bytes": sum(os.path.getsize(os.path.join(out, f"{x}_{mode}{s}"))
+                                         for x in ("tumor", "normal") for s in (".1.fastq", ".2.fastq"))}
         print(json.dumps({mode: res[mode]}), file=sys.stderr, flush=True)
     if "stream" in res and "whole" in res:
         same = all(open(os.path.join(out, f"{x}_stream{s}"), "rb").read() ==

@@ -86,20 +86,13 @@ def run_anonymizer(argv=None) -> None:
     if world > 1:
         import torch
         import torch.distributed as dist
-        from .distributed import anonymize_genome_sharded
-        from .io.fasta import FastaRef
-        from .io.vcf import read_vcf
-        from .planner import get_windows
+        from .distributed import run_pairs_sharded
         torch.cuda.set_device(device)
         dist.init_process_group("nccl", device_id=torch.device("cuda", device))
-        rank = dist.get_rank()
-        fa = FastaRef(config.reference)
-        for vcf, (t, n), (to, no) in zip(vcfs, samples, outputs):
-            windows = get_windows(read_vcf(vcf), fa.index)
-            tot = anonymize_genome_sharded(windows, t, n, config.reference, to, no, bool(config.record_statistics),
-                                           anonymizer, dist, threads=max(1, config.cpu))
-            if rank == 0:
-                logging.info("sample %s/%s totals %s", t, n, tot)
+        # one pair per GPU when there are enough pairs, else each pair's contigs over all GPUs
+        tots = run_pairs_sharded(vcfs, samples, config.reference, anonymizer, outputs, bool(config.record_statistics),
+                                 dist, threads=max(1, config.cpu))
+        logging.info("rank %d totals %s", dist.get_rank(), tots)
         dist.destroy_process_group()
     else:
         run_short_read_tumor_normal_anonymizer(vcfs, samples, config.reference, anonymizer, outputs,

@@ -18,12 +18,14 @@ same flow one FASTA contig ("job") at a time:
 5. replay the job's I/O log (the reference's per-section append handles) and write its
    bytes at the job's offset of each output file; the files grow in contig order.
 
-Multi-GPU: ``world`` ranks take the contigs round-robin in FASTA order (the north
-star's policy); round i processes jobs i*world .. i*world+world-1 in parallel, one per rank, each on
-its own GPU; one gather of the placeholders / carried records and one of the byte counts per round
-(gloo over the host) let every rank resolve and place its own job, so each rank decodes, plans,
-masks, formats and writes only its contigs. No data-path collective touches the masked bases.
-Memory: one job per rank plus the carried records of names still unpaired.
+Steps 1-3 and the formatting run on the job's owner rank; step 4 runs in a coordinator thread of
+rank 0 (``_Coordinator``) that takes the contigs in FASTA order as their exports arrive and answers
+the owner with its resolved writes and its offsets in the files; the owner assembles and writes its
+bytes (step 5) itself. Multi-GPU (distributed.py): the contigs are sharded over the
+ranks (round-robin or LPT), each rank works through its own contigs with no lock-step; only the
+cross-contig pairing state and the records it may write travel, to rank 0 and back to the owner.
+No data-path collective touches the masked bases. Memory: GANON_PENDING jobs per rank waiting for
+their resolution plus the prefetched ones, and the carried records of names still unpaired.
 """
 from __future__ import annotations
 
@@ -369,10 +371,22 @@ class Job(JobPrep):
         }
 
     # -- output ----------------------------------------------------------------------------------
-    def output(self, out_n: np.ndarray, out_w: np.ndarray, carry: Dict[Key, bytes], block: int,
-               replay: "objects.Replay" = None) -> List[bytes]:
+    def local_sizes(self) -> List[int]:
+        """Bytes of the job's own (non-placeholder) writes per output file (tumor .1, .2, normal .1,
+        .2): with the resolved placeholder writes, the coordinator places the job in the files."""
+        ev, rows = self.events, self.event_rows
+        w = np.nonzero(ev[:, 0] == 1)[0]
+        if not len(w):
+            return [0, 0, 0, 0]
+        ln = self.record_lengths(ev[w, 4], rows[w], ev[w, 5], ev[w, 6])
+        f = 2 * ev[w, 2].astype(np.int64) + ev[w, 3]
+        return [int(x) for x in np.bincount(f, weights=ln, minlength=4).astype(np.int64)[:4]]
+
+    def output(self, out_n: np.ndarray, out_w: np.ndarray, ext_list: List[bytes], block: int) -> List[bytes]:
         """The job's bytes per output file (tumor .1, .2, normal .1, .2) with the resolved writes of
-        its placeholder events spliced into its I/O log."""
+        its placeholder events spliced into its I/O log; ``ext_list``: the bytes of the resolved writes
+        of records of other contigs (and objects of complex names), in event order (the
+        coordinator's ``resolve``)."""
         ev, rows = self.events, self.event_rows
         n = len(ev)
         is_ph = ev[:, 0] >= 3
@@ -417,24 +431,12 @@ class Job(JobPrep):
         rec_len = np.zeros(nf, np.int64)
         li = np.nonzero(loc)[0]
         rec_len[li] = self.record_lengths(fin[li, 4], frow[li], fin[li, 5], reap[li])
-        ext_bytes: Dict[int, bytes] = {}
         xi = np.nonzero(ext)[0]
-        xl = []
-        for i, g, jb, d, sc_, r, re_ in zip(xi.tolist(), gen[xi].tolist(), fjob[xi].tolist(), fin[xi, 4].tolist(),
-                                             fin[xi, 5].tolist(), frow[xi].tolist(), reap[xi].tolist()):
-            if g:
-                b = replay.take(r)
-            else:
-                b = carry.get((jb, d, sc_, r, re_))
-                if b is None and re_:   # a carried record without left-overs: the same bytes
-                    b = carry.get((jb, d, sc_, r, 0))
-                if b is None:
-                    raise UnsupportedInput("a record written across contigs was not carried (its mate fields "
-                                           "disagree with where its records are)")
-            ext_bytes[i] = b
-            xl.append(len(b))
+        if len(xi) != len(ext_list):
+            raise RuntimeError(f"job {self.job}: {len(xi)} writes from other contigs, {len(ext_list)} resolved")
+        ext_bytes: Dict[int, bytes] = dict(zip(xi.tolist(), ext_list))
         if len(xi):
-            rec_len[xi] = xl
+            rec_len[xi] = [len(b) for b in ext_list]
         order = native.io_replay(fin[:, :7].astype(np.int32), np.where(wr, rec_len, 0), block)
         # every local record of the four files in ONE formatter call, then split per file
         les = [order[f][~ext[order[f]]] for f in range(4)]
@@ -465,6 +467,10 @@ class Job(JobPrep):
 
     def stats(self) -> Dict[str, List[int]]:
         return statistics_rows(self.plan, self.res)
+
+    def release_device(self) -> None:
+        """The job's exports are out: nothing on the device is needed to write it any more."""
+        self.batch = None
 
 
 class _Comm:
@@ -502,21 +508,136 @@ class _Comm:
         return t.cpu().numpy()
 
 
+class _Coordinator:
+    """The sample-wide pairing state (rank 0): resolves the contigs in FASTA order as their exports
+    arrive — ``native.Resolver`` over the placeholder events, the object replay of complex names,
+    the carried records — and answers each job's owner with its resolved writes, the bytes of those
+    writing records of other contigs, and the offsets of the job's bytes in the four files (their
+    sizes follow from the owner's own write sizes and the resolved writes: no round trip). At the
+    end it writes the tail (``pair_unmapped_mates``) and the single ends (SR:561-622)."""
+
+    def __init__(self, fds, paths_single, block_size: int):
+        self.fds = fds
+        self.paths_single = paths_single
+        self.block = block_size
+        self.resolver = native.Resolver()
+        self.carry: Dict[Key, bytes] = {}
+        self.carry_info: dict = {}
+        self.replay = (objects.Replay if os.environ.get("GANON_OBJECTS") == "python" else objects.NativeReplay)(
+            self.carry, self.carry_info)
+        self.cands: List[np.ndarray] = []
+        self.cand_live: set = set()
+        self.cand_names: List[bytes] = []
+        self.carry_floor = 0
+        self.prune_min = int(os.environ.get("GANON_CARRY_PRUNE_MIN", "200000"))   # carried records before a prune
+        self.base = [0, 0, 0, 0]
+        self.prunes = 0
+        self.resolve_s = 0.0
+
+    def _bytes_of(self, jb: int, d: int, sc: int, r: int, re_: int) -> bytes:
+        if sc == -2:        # an object of a complex name (objects.Replay)
+            return self.replay.take(r)
+        b = self.carry.get((jb, d, sc, r, re_))
+        if b is None and re_:   # a carried record without left-overs: the same bytes
+            b = self.carry.get((jb, d, sc, r, 0))
+        if b is None:
+            raise UnsupportedInput("a record written across contigs was not carried (its mate fields "
+                                   "disagree with where its records are)")
+        return b
+
+    def resolve(self, exp: dict, k: int) -> dict:
+        t0 = time.time()
+        e = exp
+        self.carry.update(e["carry"])
+        self.carry_info.update(e["carry_info"])
+        self.replay.add_job(e["job"], e["cx"])
+        out_n, out_w = self.resolver.contig(e["job"], e["ops"], e["op_rows"], e["op_names"], e["left"],
+                                            e["left_names"], e["objs"], e["obj_rows"])
+        self.replay.run(self.resolver.take_log())
+        c = e["cand"]
+        self.cands.append(c)
+        if len(c):      # candidates stay live to the end of the sample
+            self.cand_live.update((r[0], r[2], -1, r[3]) for r in c[c[:, 2] >= 0].tolist())
+        self.cand_names.extend(e["cand_names"])
+        # the job's resolved writes: bytes of those from other contigs (in event order), file sizes
+        sizes = list(e["local_sizes"])
+        ext: List[bytes] = []
+        job = e["job"]
+        for i in range(len(out_n)):
+            for w in out_w[i, :int(out_n[i])].tolist():
+                f, jb, d, sc, r, re_ = 2 * w[0] + w[1], w[2], w[3], w[4], w[5], w[6]
+                b = self._bytes_of(jb, d, sc, r, re_)
+                if jb != job or sc == -2:
+                    ext.append(b)
+                sizes[f] += len(b)
+        offsets = list(self.base)
+        for f in range(4):
+            self.base[f] += sizes[f]
+        # carried records still reachable: pending pairs and the end-of-sample candidates (pruned
+        # when the carry has doubled; the objects of complex names are settled every 16 jobs)
+        grow = len(self.carry) > max(self.prune_min, 2 * self.carry_floor)
+        if grow or k % 16 == 15:
+            pend = self.resolver.pending()
+            self.replay.settle(pend)
+            if grow:
+                live = set(map(tuple, pend.tolist()))
+                live |= self.cand_live
+                for key in [key for key in self.carry if key[:4] not in live]:
+                    del self.carry[key]
+                live_rows = {(x[0], x[1], x[3]) for x in live}
+                for key in [key for key in self.carry_info
+                            if (key if len(key) == 3 else (key[0], key[1], key[3])) not in live_rows
+                            or (len(key) == 4 and key not in live)]:
+                    del self.carry_info[key]
+                self.carry_floor = len(self.carry)
+                self.prunes += 1
+        self.resolve_s += time.time() - t0
+        return {"job": job, "out_n": out_n, "out_w": out_w, "ext": ext, "offsets": offsets, "sizes": sizes,
+                "err": None}
+
+    def finish(self, rank0_fds) -> None:
+        """End of the sample: pair_unmapped_mates, single ends (SR:561-622)."""
+        cand = np.concatenate(self.cands) if self.cands else np.zeros((0, 7), np.int64)
+        tail, single, wse = self.resolver.finish(cand, self.cand_names)
+        self.replay.run(self.resolver.take_log())
+        per_file: List[List[bytes]] = [[], [], [], []]
+
+        def carried(k):
+            if k[2] == -2:
+                return self.replay.take(k[3])
+            b = self.carry.get(k)
+            return b if b is not None else self.carry[k[:4] + (0,)]
+        for w in tail.tolist():
+            per_file[2 * w[0] + w[1]].append(carried((w[2], w[3], w[4], w[5], w[6])))
+        for f in range(4):
+            blob = b"".join(per_file[f])
+            if blob:
+                os.pwrite(rank0_fds[f], blob, self.base[f])
+        if wse:
+            for d, path in enumerate(self.paths_single):
+                with open(path, "wb") as fh:
+                    fh.write(b"".join(carried(tuple(x)) for x in single[d].tolist()))
+
+    def close(self) -> None:
+        self.resolver.close()
+
+
 def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam: str, fasta: FastaRef,
                                anonymizer: CompleteGermlineAnonymizer, tumor_out: str, normal_out: str,
                                record_statistics: bool, threads: int = 8, dist=None,
                                normal_stats_path: Optional[str] = None, block_size: Optional[int] = None,
                                window_bytes: int = 0) -> dict:
     """One tumor/normal pair, contig by contig (single rank when ``dist`` is None, else the
-    ranks of the initialised torch.distributed world). Output files, statistics and errors are
-    the reference's (SR:625-760)."""
+    ranks of the initialised torch.distributed world, each on its own contigs: distributed.py).
+    Output files, statistics and errors are the reference's (SR:625-760)."""
+    from .distributed import Link, assign_contigs
     comm = _Comm(dist)
     rank, world = comm.rank, comm.world
     paths = [f"{tumor_out}.1.fastq", f"{tumor_out}.2.fastq", f"{normal_out}.1.fastq", f"{normal_out}.2.fastq"]
     if block_size is None:
         block_size = _writer.io_block_size(os.path.dirname(os.path.abspath(tumor_out)))
-    timing = {"decode_s": 0.0, "plan_s": 0.0, "mask_s": 0.0, "format_s": 0.0, "prefetch_s": 0.0, "resolve_s": 0.0, "write_s": 0.0, "prunes": 0, "jobs": 0,
-              "reads": 0, "bases": 0}
+    timing = {"decode_s": 0.0, "plan_s": 0.0, "mask_s": 0.0, "format_s": 0.0, "prefetch_s": 0.0, "resolve_s": 0.0,
+              "write_s": 0.0, "wait_s": 0.0, "prunes": 0, "jobs": 0, "reads": 0, "bases": 0}
     failure: Optional[BaseException] = None
     if rank == 0:
         for p in paths:
@@ -525,159 +646,122 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
     fds = [os.open(p, os.O_WRONLY) for p in paths]
     readers = (BamReader(tumor_bam, threads, window_bytes), BamReader(normal_bam, threads, window_bytes))
     contigs = list(fasta.references)
-    resolver = native.Resolver()
-    carry: Dict[Key, bytes] = {}
-    carry_info: dict = {}
-    replay = (objects.Replay if os.environ.get("GANON_OBJECTS") == "python" else objects.NativeReplay)(carry, carry_info)
-    cands: List[np.ndarray] = []
-    carry_floor = 0
-    cand_live: set = set()
-    prune_min = int(os.environ.get("GANON_CARRY_PRUNE_MIN", "200000"))   # carried records before a prune
-    cand_names: List[bytes] = []
-    base = [0, 0, 0, 0]
+    owner = assign_contigs(list(fasta.lengths), world)
+    mine = [j for j in range(len(contigs)) if owner[j] == rank]
+    link = Link(dist)
+    coord = _Coordinator(fds, (f"{tumor_out}.single_end.fastq", f"{normal_out}.single_end.fastq"), block_size) \
+        if rank == 0 else None
+    coord_exc: List[Optional[BaseException]] = [None]
     stats_rows: List[Tuple[int, Dict[str, List[int]]]] = []
     totals = np.zeros(8, np.int64)
-    n_rounds = (len(contigs) + world - 1) // world
-    # look-ahead: a decode thread reads the next contigs in order (one BamReader stream) and
-    # `depth` threads plan and batch them (JobPrep) while this job masks, formats and writes;
-    # GANON_PREFETCH = depth (default 2, 0: everything in line). Bounded: depth jobs ahead.
+
+    def coordinate() -> None:
+        """Rank 0's coordinator thread: every job in FASTA order, as its export arrives."""
+        err = None
+        try:
+            for k in range(len(contigs)):
+                o = owner[k]
+                exp = link.recv_export(o)
+                if exp.get("err") is not None:   # the owner failed: its error is its own to report
+                    err = exp["err"]
+                    break
+                link.send_resolution(o, coord.resolve(exp, k))
+            if err is None:
+                coord.finish(fds)
+        except BaseException as e:   # reported to every owner still waiting
+            coord_exc[0] = e
+            err = repr(e)
+        if err is not None:
+            for r in range(world):   # every worker still waiting for a resolution stops
+                link.send_resolution(r, {"err": err})
+
+    import threading
+    coord_thread = threading.Thread(target=coordinate, name="ganon-coordinator", daemon=True) if rank == 0 else None
+    if coord_thread is not None:
+        coord_thread.start()
+    # look-ahead: a decode thread reads this rank's next contigs in order (one BamReader stream) and
+    # `depth` threads plan and batch them (JobPrep) while the current one masks, formats and writes;
+    # GANON_PREFETCH = depth (default 2, 0: everything in line). At most `pend_max` jobs wait for
+    # their resolution (GANON_PENDING, default 4): memory is bounded by them and the prefetched jobs.
     depth = int(os.environ.get("GANON_PREFETCH", "2"))
+    pend_max = max(1, int(os.environ.get("GANON_PENDING", "4")))
     dec_pool = ThreadPoolExecutor(1) if depth > 0 else None
     pool = ThreadPoolExecutor(depth) if depth > 0 else None
     ahead: Dict[int, object] = {}
-    next_job = [rank]          # the next of this rank's jobs to submit (in order: one BAM stream)
+    nxt = [0]                  # index in `mine` of the next job to submit
 
-    def submit_upto(j_last: int) -> None:
-        while next_job[0] <= min(j_last, len(contigs) - 1):
-            j = next_job[0]
+    def submit_upto(i_last: int) -> None:
+        while nxt[0] <= min(i_last, len(mine) - 1):
+            j = mine[nxt[0]]
             dec = dec_pool.submit(decode_contig, readers, contigs[j])
             ahead[j] = pool.submit(JobPrep, j, contigs[j], readers, fasta, windows, dec)
-            next_job[0] += world
-    try:
-        for rnd in range(n_rounds):
-            jid = rnd * world + rank
-            job = None
-            exp = None
-            err = None
-            if failure is None and jid < len(contigs):
-                try:
-                    pre = None
-                    if pool is not None:
-                        submit_upto(jid + depth * world)
-                        pre = ahead.pop(jid)
-                    job = Job(jid, contigs[jid], readers, fasta, windows, anonymizer, pre)
-                    exp = job.exports()
-                    for k in ("decode_s", "plan_s", "mask_s", "format_s", "prefetch_s"):
-                        timing[k] += job.timing[k]
-                    timing["jobs"] += 1
-                    timing["reads"] += int(job.tables[0].n + job.tables[1].n)
-                    timing["bases"] += int(job.tables[0].l_seq.sum(dtype=np.int64) + job.tables[1].l_seq.sum(dtype=np.int64))
-                    totals += np.asarray(job.res.totals, np.int64)[:8]
-                except BaseException as e:   # every rank must reach the gathers
-                    failure, err = e, repr(e)
-            gathered = comm.allgather({"exp": exp, "err": err})
-            errs = [g["err"] for g in gathered if g["err"] is not None]
-            if errs:
-                if failure is not None:
-                    raise failure
-                raise RuntimeError(f"another rank failed: {errs[0]}")
-            t0 = time.time()
-            mine = None
-            for g in gathered:
-                e = g["exp"]
-                if e is None:
-                    continue
-                carry.update(e["carry"])
-                carry_info.update(e["carry_info"])
-                replay.add_job(e["job"], e["cx"])
-                out_n, out_w = resolver.contig(e["job"], e["ops"], e["op_rows"], e["op_names"], e["left"],
-                                               e["left_names"], e["objs"], e["obj_rows"])
-                replay.run(resolver.take_log())
-                cands.append(e["cand"])
-                c = e["cand"]
-                if len(c):      # candidates stay live to the end of the sample
-                    cand_live.update((r[0], r[2], -1, r[3]) for r in c[c[:, 2] >= 0].tolist())
-                cand_names.extend(e["cand_names"])
-                if job is not None and e["job"] == job.job:
-                    mine = (out_n, out_w)
-            t1 = time.time()
-            data = [b"", b"", b"", b""]
-            if job is not None:
-                try:
-                    data = job.output(mine[0], mine[1], carry, block_size, replay)
-                    stats_rows.append((job.job, job.stats()))
-                except BaseException as e:
-                    failure, err = e, repr(e)
-            sizes = comm.allgather({"sizes": [len(d) for d in data], "err": err})
-            errs = [g["err"] for g in sizes if g["err"] is not None]
-            if errs:
-                if failure is not None:
-                    raise failure
-                raise RuntimeError(f"another rank failed: {errs[0]}")
-            try:
-                for f in range(4):
-                    off = base[f] + sum(sizes[r]["sizes"][f] for r in range(rank))
-                    if data[f]:
-                        os.pwrite(fds[f], data[f], off)
-            except BaseException as e:   # reported at the next exchange (every rank reaches it)
-                failure = failure or e
-            for f in range(4):
-                base[f] += sum(g["sizes"][f] for g in sizes)
-            # carried records still reachable: pending pairs and the end-of-sample candidates (pruned
-            # when the carry has doubled or every 16 rounds: each pass walks the whole carry)
-            # (the objects of complex names are settled every 16 rounds; the carry walk runs only when
-            # the carry has doubled, so its cost stays proportional to what it inserts)
-            grow = len(carry) > max(prune_min, 2 * carry_floor)
-            if grow or rnd % 16 == 15:
-                pend = resolver.pending()
-                replay.settle(pend)
-                if grow:
-                    live = set(map(tuple, pend.tolist()))
-                    live |= cand_live
-                    for k in [k for k in carry if k[:4] not in live]:
-                        del carry[k]
-                    live_rows = {(k[0], k[1], k[3]) for k in live}
-                    for k in [k for k in carry_info if (k if len(k) == 3 else (k[0], k[1], k[3])) not in live_rows
-                              or (len(k) == 4 and k not in live)]:
-                        del carry_info[k]
-                    carry_floor = len(carry)
-                    timing["prunes"] += 1
-            job = None
-            timing["resolve_s"] += t1 - t0
-            timing["write_s"] += time.time() - t1
-        # ---- end of the sample: pair_unmapped_mates, single ends (SR:561-622) ----
-        err = repr(failure) if failure is not None else None
-        if failure is None:
-            try:
-                cand = np.concatenate(cands) if cands else np.zeros((0, 7), np.int64)
-                tail, single, wse = resolver.finish(cand, cand_names)
-                replay.run(resolver.take_log())
-                if rank == 0:
-                    per_file: List[List[bytes]] = [[], [], [], []]
+            nxt[0] += 1
 
-                    def carried(k):
-                        if k[2] == -2:
-                            return replay.take(k[3])
-                        b = carry.get(k)
-                        return b if b is not None else carry[k[:4] + (0,)]
-                    for w in tail.tolist():
-                        per_file[2 * w[0] + w[1]].append(carried((w[2], w[3], w[4], w[5], w[6])))
-                    for f in range(4):
-                        blob = b"".join(per_file[f])
-                        if blob:
-                            os.pwrite(fds[f], blob, base[f])
-                    if wse:
-                        for d, prefix in enumerate((tumor_out, normal_out)):
-                            with open(f"{prefix}.single_end.fastq", "wb") as fh:
-                                fh.write(b"".join(carried(tuple(x)) for x in single[d].tolist()))
-            except BaseException as e:   # every rank reaches the gather below, then all raise
-                failure, err = e, repr(e)
+    pending: "List[Job]" = []
+
+    def finish_oldest() -> None:
+        nonlocal failure
+        t0 = time.time()
+        res = link.recv_resolution()
+        timing["wait_s"] += time.time() - t0
+        if res.get("err") is not None:
+            raise RuntimeError(f"another rank failed: {res['err']}")
+        job = pending.pop(0)
+        if res["job"] != job.job:
+            raise RuntimeError(f"resolution of job {res['job']} for job {job.job}")
+        t1 = time.time()
+        data = job.output(res["out_n"], res["out_w"], res["ext"], block_size)
+        for f in range(4):
+            if len(data[f]) != res["sizes"][f]:
+                raise RuntimeError(f"job {job.job}: {len(data[f])} bytes for file {f}, {res['sizes'][f]} planned")
+            if data[f]:
+                os.pwrite(fds[f], data[f], res["offsets"][f])
+        stats_rows.append((job.job, job.stats()))
+        timing["write_s"] += time.time() - t1
+
+    try:
+        try:
+            for i, j in enumerate(mine):
+                pre = None
+                if pool is not None:
+                    submit_upto(i + depth)
+                    pre = ahead.pop(j)
+                job = Job(j, contigs[j], readers, fasta, windows, anonymizer, pre)
+                exp = job.exports()
+                exp["local_sizes"] = job.local_sizes()
+                exp["err"] = None
+                for k in ("decode_s", "plan_s", "mask_s", "format_s", "prefetch_s"):
+                    timing[k] += job.timing[k]
+                timing["jobs"] += 1
+                timing["reads"] += int(job.tables[0].n + job.tables[1].n)
+                timing["bases"] += int(job.tables[0].l_seq.sum(dtype=np.int64) + job.tables[1].l_seq.sum(dtype=np.int64))
+                totals += np.asarray(job.res.totals, np.int64)[:8]
+                link.send_export(exp)
+                job.release_device()
+                pending.append(job)
+                while len(pending) >= pend_max:
+                    finish_oldest()
+            while pending:
+                finish_oldest()
+        except BaseException as e:   # every rank reaches the exchange below with its error
+            failure = e
+            # the coordinator may be waiting for this rank's next export: tell it
+            link.send_export({"err": repr(e)})
+        if coord_thread is not None:
+            coord_thread.join()
+            timing["resolve_s"] = coord.resolve_s
+            timing["prunes"] = coord.prunes
+            if coord_exc[0] is not None:   # rank 0 reports the coordinator's own error
+                failure = coord_exc[0]
+        err = repr(failure) if failure is not None else None
         gathered = comm.allgather({"stats": stats_rows, "err": err})
         errs = [g["err"] for g in gathered if g["err"] is not None]
         if errs:
             if failure is not None:
                 raise failure
             raise RuntimeError(f"another rank failed: {errs[0]}")
+        if failure is None:
+            link.drain()
         all_stats = [g["stats"] for g in gathered]
         if rank == 0 and record_statistics:
             merged: Dict[str, List[int]] = {OUTSIDE_WINDOWS: [0] * 8}
@@ -698,7 +782,8 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
             os.close(fd)
         for r in readers:
             r.close()
-        resolver.close()
+        if coord is not None:
+            coord.close()
     totals = comm.allreduce_totals(totals)
     timing["totals"] = {k: int(v) for k, v in zip(("masked_snv_calls", "masked_bases", "reads_in", "reads_written",
                                                    "scopes", "rare_scopes", "large_tiles", "reserved"), totals)}

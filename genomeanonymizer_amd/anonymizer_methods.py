@@ -40,6 +40,7 @@ class MaskResult:
     totals: np.ndarray
     arrays: dict                           # the device batch (kept for tests/bench)
     dup_off: Dict[Tuple[int, int, int], int] = dataclasses.field(default_factory=dict)
+    device_gen: int = -1                   # the engine's job batch holding this result (format_fastq_batch)
 
     def masked_nib(self, tables, ds: int, row: int, scope: int) -> int:
         """Nibble offset in seq_out of read (ds, row) as masked by ``scope``."""
@@ -250,6 +251,12 @@ class CompleteGermlineAnonymizer:
         fmt = getattr(self.engine, "format_fastq", None)
         return fmt(recs) if fmt is not None else native.host_format_fastq(recs)
 
+    def format_fastq_batch(self, recs: dict, gen: int):
+        """The same records formatted from the engine's resident job batch (its masked output and
+        input bases, no upload of the sequences), or None when that batch has moved on."""
+        fmt = getattr(self.engine, "format_fastq_batch", None)
+        return fmt(recs, gen) if fmt is not None else None
+
     def anonymize(self, planner: SamplePlanner, plan: Plan, scope_ids=None, written=None, batch=None) -> MaskResult:
         """Mask all scopes of ``plan`` (or the contig shard ``scope_ids``) in one device batch
         (``batch``: build_batch's result when the caller built it already). Per-scope counts come
@@ -258,13 +265,14 @@ class CompleteGermlineAnonymizer:
         fasta = planner.fasta
         arrays, meta = batch if batch is not None else build_batch(plan, tables, fasta, scope_ids, written)
         out, b_calls, b_bases, totals, irecs = self.engine.mask(arrays, indels=True)
+        gen = getattr(self.engine, "job_gen", -1)
         calls = np.zeros(len(plan.scopes), np.int32)
         bases = np.zeros(len(plan.scopes), np.int32)
         calls[meta["scope_ids"]] = b_calls
         bases[meta["scope_ids"]] = b_bases
         indel_counts, leftovers = indel_results(irecs, meta, plan, tables, fasta)
         return MaskResult(out, meta["seq_base"], {}, calls, bases, indel_counts, leftovers, totals, arrays,
-                          meta["dup_off"])
+                          meta["dup_off"], gen)
 
 
 ANONYMIZER_ALGORITHMS = {CompleteGermlineAnonymizer.name: CompleteGermlineAnonymizer}

@@ -251,6 +251,8 @@ class HipMasker:
         self._h = h
         self.device = device
         self._ref = None            # (the host array, its DeviceRef): the genome stays resident
+        self._job_db = None         # the device batch of the last mask(indels=True), reloaded per job
+        self.job_gen = 0            # increments with every job batch: a MaskResult's batch is live while equal
 
     def resident_reference(self, ref_nt16: np.ndarray) -> "DeviceRef":
         """The packed genome in HBM, uploaded once per array object (stream.py masks one contig
@@ -267,6 +269,9 @@ class HipMasker:
             raise GanonError(f"{what} failed ({rc}): {msg}")
 
     def close(self) -> None:
+        if getattr(self, "_job_db", None) is not None:
+            self._job_db.free()
+            self._job_db = None
         if getattr(self, "_ref", None) is not None:
             self._ref[1].free()
             self._ref = None
@@ -299,18 +304,31 @@ class HipMasker:
         """Synchronous one-shot: returns (seq_out, scope_calls, scope_bases, totals), plus the
         germline indel records (``INDEL_REC``, sorted) when ``indels``."""
         if indels:
-            db = self.upload(arrays, ref=self.resident_reference(arrays["ref_nt16"]))
-            try:
-                t = db.indel_tally(arrays)
+            # one device batch per context, reloaded job after job (grow-only buffers: no allocation
+            # once the largest job has been seen); it stays valid — for formatting from the device
+            # (format_fastq_batch) — until the next job
+            ref = self.resident_reference(arrays["ref_nt16"])
+            self.job_gen += 1
+            db = self._job_db
+            if db is None:
+                db = self._job_db = self.upload(arrays, ref=ref)
+            else:
                 try:
-                    db.run()
+                    db.reload(arrays)
+                except GanonError:
+                    self._job_db = None
+                    db.free()
+                    raise
+            t = db.indel_tally(arrays) if db.shape()["id_ops"] else None   # (no I/D op: nothing to tally)
+            try:
+                db.run()
+                if t is not None:
                     t.run()
-                    res = db.download()
-                    recs = t.download()
-                finally:
-                    t.free()
+                res = db.download()
+                recs = t.download() if t is not None else np.zeros(0, INDEL_REC)
             finally:
-                db.free()
+                if t is not None:
+                    t.free()
             return res + (recs,)
         b = make_c_batch(arrays)
         out = np.empty(b.seq_bytes, np.uint8)
@@ -350,6 +368,32 @@ class HipMasker:
         self._check(self._lib.ganon_fastq_upload(self._h, C.byref(c), C.byref(h)), "ganon_fastq_upload")
         del keep
         return DeviceFastq(self, h)
+
+    def format_fastq_batch(self, recs: dict, gen: int) -> Optional[bytes]:
+        """Format records whose sequences are in the last job batch (``recs`` as FastqFormatter
+        builds them: buffer 0 = that batch's masked output, 1 / 2 = the tumor / normal blobs, which
+        are the batch's input at offsets 0 / ``recs['seq_base1']``), reading the bases in place on
+        the device: no upload of the sequences. None when the batch is no longer job ``gen``'s."""
+        db = self._job_db
+        if db is None or gen != self.job_gen:
+            return None
+        r = dict(recs)
+        sel = recs["seq_sel"]
+        r["seq_nib_off"] = recs["seq_nib_off"] + np.where(sel == 2, 2 * int(recs["seq_base1"]), 0).astype(np.int64)
+        r["seq_sel"] = np.minimum(sel, 1).astype(np.uint8)
+        c, keep = _c_fastq_records(r, seq_batch=db)
+        h = _p()
+        self._check(self._lib.ganon_fastq_upload(self._h, C.byref(c), C.byref(h)), "ganon_fastq_upload")
+        del keep
+        try:
+            self._check(self._lib.ganon_fastq_run(self._h, h), "ganon_fastq_run")
+            n_bytes = int(self._lib.ganon_fastq_bytes(h))
+            out = _new_bytes(None, n_bytes)      # filled in place
+            w = self._lib.ganon_fastq_download(self._h, h, out, n_bytes)
+            w = _fastq_result(w, lambda: self._lib.ganon_last_error(self._h).decode(errors="replace"))
+        finally:
+            self._lib.ganon_fastq_free(self._h, h)
+        return out if w == n_bytes else out[:w]
 
     def format_fastq(self, recs: dict) -> bytes:
         """One-shot ``ganon_fastq_format_hip`` (the host formatter's arguments)."""

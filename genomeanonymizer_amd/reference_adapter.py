@@ -215,6 +215,7 @@ class GpuCompleteGermlineAnonymizer:
         self._engine = engine
         self.model = model or default_model()
         self.anonymized_reads: Dict[str, List[Optional[object]]] = {}
+        self._built: set = set()      # alignments whose AnonymizedRead was built once this scope
 
     @property
     def engine(self):
@@ -225,6 +226,7 @@ class GpuCompleteGermlineAnonymizer:
 
     def reset(self) -> None:
         self.anonymized_reads = {}
+        self._built = set()
 
     # -- 1 + 2: the scope as a device batch ------------------------------------------------------
     def _device_calls(self, columns, variant_to_keep, ref_genome):
@@ -357,10 +359,19 @@ class GpuCompleteGermlineAnonymizer:
 
     # -- 3: the reference's per-scope control flow ---------------------------------------------
     def _add_from_alignment(self, aln, ds: int) -> None:
-        """add_anonymized_read_pair_to_collection_from_alignment (AM:320-349)."""
+        """add_anonymized_read_pair_to_collection_from_alignment (AM:320-349). The reference builds
+        a new AnonymizedRead at every column (Q13) and keeps it only when the pair slot is empty;
+        here it is built when it is kept, or the first time an alignment is met (so that whatever
+        the constructor would raise is raised at the same column) — a long read meets ~10^4
+        columns."""
         pair = self.anonymized_reads.get(aln.query_name)
-        new = self.model.anonymized_read(aln, ds)
-        idx = new.get_pair_idx()
+        key = self._key(ds, aln)
+        idx = PAIR_1_IDX if aln.flag & 0x40 else PAIR_2_IDX if aln.flag & 0x80 else None
+        new = None
+        if key not in self._built or pair is None or pair[idx] is None:
+            self._built.add(key)
+            new = self.model.anonymized_read(aln, ds)
+            idx = new.get_pair_idx()
         if pair is None:
             pair = self.anonymized_reads[aln.query_name] = [None, None]
             pair[idx] = new

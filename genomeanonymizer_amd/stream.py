@@ -170,7 +170,8 @@ class Job(JobPrep):
         self.res: MaskResult = anonymizer.anonymize(self.planner, self.plan, written=self.written, batch=self.batch)
         self.batch = None
         t3 = time.time()
-        self.fmt = FastqFormatter(self.tables, self.res, anonymizer.format_fastq)
+        self.fmt = FastqFormatter(self.tables, self.res, anonymizer.format_fastq,
+                                  getattr(anonymizer, "format_fastq_batch", None))
         # every read once, as its masked copy (or unmasked): the records this job can write
         self.fmt.preformat(*self._format_instances())
         t4 = time.time()

@@ -32,10 +32,13 @@ class FastqFormatter:
     HIP formatter of the masking engine's device (``HipMasker.format_fastq``) in the product,
     the host library's ``ganon_fastq_format`` when no engine formatter is given."""
 
-    def __init__(self, tables: Tuple[ReadTable, ReadTable], res: MaskResult, backend=None):
+    def __init__(self, tables: Tuple[ReadTable, ReadTable], res: MaskResult, backend=None, device_backend=None):
+        """``device_backend(recs, gen)``: formats from the engine's resident job batch while it still
+        holds ``res`` (preformat only; None = not available)."""
         self.tables = tables
         self.res = res
         self.backend = backend or native.host_format_fastq
+        self.device_backend = device_backend
         # buffers: 0 = device output, 1 = tumor BAM seq, 2 = normal BAM seq
         self._seq_bufs = [res.seq_out, tables[0].seq, tables[1].seq]
         self._qual_bufs = [tables[0].qual, tables[1].qual]
@@ -125,7 +128,13 @@ class FastqFormatter:
             if len(ds) == 0:
                 return
             try:
-                data = self.backend(self.records_arrays(ds, row, sc))
+                data = None
+                if self.device_backend is not None:   # the bases in place on the device
+                    recs = self.records_arrays(ds, row, sc)
+                    recs["seq_base1"] = len(self.tables[0].seq)
+                    data = self.device_backend(recs, self.res.device_gen)
+                if data is None:
+                    data = self.backend(self.records_arrays(ds, row, sc))
             except native.FastqBadRecord as e:
                 keep = np.ones(len(ds), bool)
                 keep[e.index] = False

@@ -132,7 +132,58 @@ def make(name: str, arr: dict, seed: int) -> dict:
             "counts": {k: sum(e["counts"].get(k, 0) for e in expected) for k in ("SNV", "DEL", "INS")}}
 
 
+def make_long(name: str, seed: int, n_reads: int = 8, genome: int = 36_000, len_range=(10_000, 16_000)) -> dict:
+    """Long reads (SURVEY §8(d) C5 shape): a ``longread_batch`` of 10-30 kb reads with 1-3 bp indels
+    every ~20 bases, soft clips up to 2 kb, substitutions and IUPAC reference codes, on ONE contig,
+    paired two by two within each dataset (FR, mate fields set); every window scope (window
+    +-1000; the pileup takes whole read extents, so the scopes span tens of kb and share reads) is
+    run through the unmodified reference. Germline indels (the same indel in a tumor and a normal
+    read) occur, so the yielded records carry the reference's indel edits too."""
+    from genomeanonymizer_amd.synth.batch import longread_batch
+    from genomeanonymizer_amd.synth.bamwriter import BamRecord, write_bam, write_fasta
+    arr, info = longread_batch(seed, n_reads=n_reads, genome=genome, len_range=len_range)
+    dest = os.path.join(REPO, "tests", "golden", "adapter", name)
+    os.makedirs(dest, exist_ok=True)
+    rng = np.random.default_rng(seed)
+    ref_seq = "".join(NT16[c] for c in _nibbles(arr["ref_nt16"], 0, genome))
+    write_fasta(os.path.join(dest, "ref.fa"), [("c0", ref_seq)])
+    n = len(arr["read_len"])
+    recs = {0: [], 1: []}
+    for ds in (0, 1):
+        rows = [r for r in range(n) if int(arr["dataset"][r]) == ds]
+        rng.shuffle(rows)
+        for k in range(0, len(rows), 2):
+            grp = rows[k:k + 2]
+            for m, r in enumerate(grp):
+                mate = grp[1 - m] if len(grp) == 2 else r
+                name_ = f"d{ds}p{k // 2}" if len(grp) == 2 else f"d{ds}u{k}"
+                L = int(arr["read_len"][r])
+                seq = "".join(NT16[c] for c in _nibbles(arr["seq_nt16"], 2 * int(arr["seq_off"][r]), L))
+                rev = m == 1 and set(seq) <= set("ACGTN")
+                flag = 1 | (64 if m == 0 else 128) | (16 if rev else 0) | (32 if (m == 0 and len(grp) == 2) else 0)
+                cig = arr["cigar"][arr["cig_off"][r]:arr["cig_off"][r] + arr["n_cig"][r]]
+                ops = [("MIDNSHP=X"[int(w) & 0xF], int(w) >> 4) for w in cig]
+                qual = rng.integers(20, 24, L).tolist()
+                recs[ds].append(BamRecord(name_, flag, 0, int(arr["ref_start"][r]), 60, ops, 0,
+                                          int(arr["ref_start"][mate]), 0, seq, qual))
+    for ds, fn in ((0, "t.bam"), (1, "n.bam")):
+        write_bam(os.path.join(dest, fn), [("c0", genome)], sorted(recs[ds], key=lambda x: x.pos))
+    scopes = []
+    for s in range(len(arr["scope_span_len"])):
+        kp = int(arr["keep_pos"][s])                  # the window's variant (0-based)
+        scopes.append(["c0", kp - 1000, kp + 1001, [kp, NT16[int(arr["keep_code"][s])], ref_seq[kp].upper()]])
+    expected = run_reference(dest, scopes)
+    json.dump(scopes, open(os.path.join(dest, "scopes.json"), "w"))
+    json.dump(expected, open(os.path.join(dest, "expected.json"), "w"))
+    return {"reads": n, "scopes": len(scopes), "pairs": sum(len(e["pairs"]) for e in expected),
+            "cigar_ops": int(len(arr["cigar"])), "max_span": info["max_span"],
+            "counts": {k: sum(e["counts"].get(k, 0) for e in expected) for k in ("SNV", "DEL", "INS")}}
+
+
 if __name__ == "__main__":
     from genomeanonymizer_amd.synth.batch import indel_batch, random_batch
-    print("snv", make("snv", random_batch(404, n_scopes=24, rare_frac=0.1, wide_scopes=1), 404))
-    print("indel", make("indel", indel_batch(505, n_scopes=16), 505))
+    if "long" in sys.argv[1:]:
+        print("long", make_long("long", 601))
+    else:
+        print("snv", make("snv", random_batch(404, n_scopes=24, rare_frac=0.1, wide_scopes=1), 404))
+        print("indel", make("indel", indel_batch(505, n_scopes=16), 505))

@@ -37,7 +37,7 @@ _BAM_CACHE: Dict[str, tuple] = {}
 class AlignedSegment:
     __slots__ = ("query_name", "flag", "reference_id", "reference_start", "mapping_quality",
                  "_cigar", "next_reference_id", "next_reference_start", "template_length",
-                 "query_sequence", "_qual", "_tags", "_header", "_end")
+                 "query_sequence", "_qual", "_tags", "_header", "_end", "_cigarstring")
 
     # -- flags ------------------------------------------------------------------------
     @property
@@ -72,7 +72,10 @@ class AlignedSegment:
     def cigarstring(self):
         if not self._cigar:
             return None
-        return "".join(f"{n}{CIGAR_OPS[op]}" for op, n in self._cigar)
+        cs = getattr(self, "_cigarstring", None)
+        if cs is None:
+            cs = self._cigarstring = "".join(f"{n}{CIGAR_OPS[op]}" for op, n in self._cigar)   # (never changes)
+        return cs
 
     @property
     def cigartuples(self):
@@ -317,20 +320,49 @@ class AlignmentFile:
         return _pileup_columns(reads, tid, contig)
 
 
+class _QposWalker:
+    """_qpos_at for increasing reference positions of one read, walking its CIGAR once."""
+    __slots__ = ("cig", "k", "rp", "qp")
+
+    def __init__(self, aln):
+        self.cig = aln._cigar
+        self.k = 0
+        self.rp = aln.reference_start
+        self.qp = 0
+
+    def at(self, refpos: int):
+        while self.k < len(self.cig):
+            op, n = self.cig[self.k]
+            if op in (0, 7, 8):
+                if refpos < self.rp + n:
+                    return self.qp + (refpos - self.rp) if refpos >= self.rp else None
+                self.rp += n
+                self.qp += n
+            elif op in (1, 4):
+                self.qp += n
+            elif op in (2, 3):
+                if refpos < self.rp + n:
+                    return None
+                self.rp += n
+            self.k += 1
+        return None
+
+
 def _pileup_columns(reads, tid, name):
     # reads are in file (= push) order; a read contributes to [start, end) columns
     i = 0
     active: List[AlignedSegment] = []
+    walkers: Dict[int, _QposWalker] = {}
     n = len(reads)
     pos = reads[0].reference_start if reads else 0
     cur = _PileupCursor()
     try:
         while i < n or active:
             while i < n and reads[i].reference_start <= pos:
-                active.append(reads[i]); i += 1
+                active.append(reads[i]); walkers[id(reads[i])] = _QposWalker(reads[i]); i += 1
             active = [r for r in active if r._end > pos]
             if active:
-                yield PileupColumn(tid, name, pos, [PileupRead(r, _qpos_at(r, pos)) for r in active], cur)
+                yield PileupColumn(tid, name, pos, [PileupRead(r, walkers[id(r)].at(pos)) for r in active], cur)
                 cur.gen += 1     # the engine's buffer moves on
                 pos += 1
             elif i < n:

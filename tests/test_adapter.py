@@ -78,14 +78,14 @@ def check(name, got):
         assert g["pairs"] == e["pairs"], s
 
 
-@pytest.mark.parametrize("name", ["snv", "indel"])
+@pytest.mark.parametrize("name", ["snv", "indel", "long"])
 def test_adapter_matches_reference_with_oracle_engine(name):
     from pyoracle import OracleEngine
     check(name, run_adapter(name, OracleEngine()))
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["snv", "indel"])
+@pytest.mark.parametrize("name", ["snv", "indel", "long"])
 def test_adapter_matches_reference_on_gpu(name, hip_built):
     from genomeanonymizer_amd import native
     m = native.HipMasker(0)

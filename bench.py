@@ -366,8 +366,8 @@ def main() -> None:
     ap.add_argument("--target", type=int, default=None, help="GANON_PARAM_GROUP_TARGET (cost units per group)")
     ap.add_argument("--no-fastq", action="store_true", help="skip the FASTQ formatter measurement")
     ap.add_argument("--indel-sort", type=int, default=0, help="GANON_PARAM_INDEL_SORT: 0 segmented, 1 global")
-    ap.add_argument("--fuse-emit", type=int, default=0,
-                    help="GANON_PARAM_FUSE_EMIT: 1 the group kernel builds its records, 0 the separate emit kernel")
+    ap.add_argument("--prep-unroll", type=int, default=0, help="GANON_PARAM_PREP_UNROLL: incidences per thread "
+                    "and trip of the one-segment emit (0 auto, 1, 2, 4)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (BAM -> FASTQ) line")
     ap.add_argument("--e2e-contigs", type=int, default=24)
     ap.add_argument("--e2e-pairs", type=int, default=23_000, help="pairs per contig and sample")
@@ -377,7 +377,7 @@ def main() -> None:
                     help="round-2 step: run only, the plan made once at upload (not a fresh batch)")
     ap.add_argument("--pmc", default=None,
                     help="PMC step summary (tools/pmc_step.py) for the traffic field; default "
-                         "profiles/r02/pmc_step_<config>.json when present")
+                         "profiles/r03/pmc_step_<config>.json when present")
     args = ap.parse_args()
     for k, v in CONFIGS[args.config]["defaults"].items():
         if getattr(args, k) is None:
@@ -412,7 +412,7 @@ def main() -> None:
     if args.target:
         masker.set_param(native.PARAM_GROUP_TARGET, args.target)
     masker.set_param(native.PARAM_INDEL_SORT, args.indel_sort)
-    masker.set_param(native.PARAM_FUSE_EMIT, args.fuse_emit)
+    masker.set_param(native.PARAM_PREP_UNROLL, args.prep_unroll)
     stream = torch.cuda.current_stream()
     masker.set_stream(stream.cuda_stream)
     t_up = time.perf_counter()
@@ -531,7 +531,7 @@ def main() -> None:
     alg_total = algorithmic_bytes(arr)
     achieved = alg_total / (pass_ms * 1e-3) / 1e9
     traffic = dom_traffic = None
-    pmc_path = args.pmc or os.path.join(REPO, "profiles", "r02", f"pmc_step_{args.config}.json")
+    pmc_path = args.pmc or os.path.join(REPO, "profiles", "r03", f"pmc_step_{args.config}.json")
     if os.path.exists(pmc_path):
         try:
             pmc = json.load(open(pmc_path))

@@ -16,6 +16,7 @@ masking path: a missing HIP library or device raises ``GanonError``.
 from __future__ import annotations
 
 import dataclasses
+import threading
 from typing import Dict, Optional, Tuple
 
 import numpy as np
@@ -238,6 +239,9 @@ class CompleteGermlineAnonymizer:
     def __init__(self, device: int = 0, engine=None):
         self.device = device
         self._engine = engine
+        # one caller of the engine at a time (the streamed path formats on a writer thread while the
+        # next contig masks; the engine's context is not thread-safe)
+        self.lock = threading.RLock()
 
     @property
     def engine(self):
@@ -249,13 +253,19 @@ class CompleteGermlineAnonymizer:
         """FASTQ records on the masking engine's device (``ganon_fastq_format_hip``); an engine
         without a formatter (none in the product) leaves them to libganon_host.so."""
         fmt = getattr(self.engine, "format_fastq", None)
-        return fmt(recs) if fmt is not None else native.host_format_fastq(recs)
+        if fmt is None:
+            return native.host_format_fastq(recs)
+        with self.lock:
+            return fmt(recs)
 
     def format_fastq_batch(self, recs: dict, gen: int):
         """The same records formatted from the engine's resident job batch (its masked output and
         input bases, no upload of the sequences), or None when that batch has moved on."""
         fmt = getattr(self.engine, "format_fastq_batch", None)
-        return fmt(recs, gen) if fmt is not None else None
+        if fmt is None:
+            return None
+        with self.lock:
+            return fmt(recs, gen)
 
     def anonymize(self, planner: SamplePlanner, plan: Plan, scope_ids=None, written=None, batch=None) -> MaskResult:
         """Mask all scopes of ``plan`` (or the contig shard ``scope_ids``) in one device batch
@@ -264,8 +274,9 @@ class CompleteGermlineAnonymizer:
         tables = planner.tables
         fasta = planner.fasta
         arrays, meta = batch if batch is not None else build_batch(plan, tables, fasta, scope_ids, written)
-        out, b_calls, b_bases, totals, irecs = self.engine.mask(arrays, indels=True)
-        gen = getattr(self.engine, "job_gen", -1)
+        with self.lock:
+            out, b_calls, b_bases, totals, irecs = self.engine.mask(arrays, indels=True)
+            gen = getattr(self.engine, "job_gen", -1)
         calls = np.zeros(len(plan.scopes), np.int32)
         bases = np.zeros(len(plan.scopes), np.int32)
         calls[meta["scope_ids"]] = b_calls

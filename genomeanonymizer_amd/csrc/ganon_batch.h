@@ -77,18 +77,6 @@ struct GrpAux {
   unsigned long long *paths;                    // [0] sorted lists, [1] region passes, [2] key-range splits
   unsigned long long *okey, *opay, *tkey;       // overflow regions
   unsigned int *tflag;
-  // the fused one-segment emit (k_group EMIT): the raw arrays each tile's records are built from,
-  // the group table of the batch scan, the incidence checks' outputs
-  const longlong2 *gmeta;
-  int32_t n_groups, n_scopes, n_reads, pad;
-  int64_t n_incid, region_per_incid, n_blk;
-  const int64_t *incid_off, *seq_off, *cig_off, *ref_off;
-  const int32_t *incid_read, *ref_start, *read_len, *n_cig, *write_scope, *read_end, *span_start, *span_len;
-  const uint8_t *dataset;
-  const uint32_t *cigar;
-  const uint64_t *bad;                          // non-ACGT 64-base blocks of the reference
-  unsigned long long *ws_part;                  // [group] write-scope hash sums
-  struct PrepErr *err;
 };
 
 // First error the device validation found: per-read and per-scope checks at plan time, incidence
@@ -104,7 +92,7 @@ enum PrepErrKind {
   kErrScopeOff, kErrScopeSpan, kErrScopeRef, kErrScopeKeep, kErrIncidRead, kErrIncidSpan, kErrWriteScopeMissing
 };
 
-// ---- device helpers shared by the prep kernels (ganon_prep.hip) and the group kernel's fused emit
+// ---- device helpers shared by the prep kernels (ganon_prep.hip) and the group kernels
 #ifdef __HIPCC__
 __device__ __forceinline__ void report(PrepErr *err, int kind, long long index, long long a = 0, long long b = 0) {
   if (atomicCAS(&err->code, 0, kind) == 0) {
@@ -215,7 +203,6 @@ struct ganon_dbatch {
   // per scope (scost, upload) instead of the CSR offsets, and emitted one wave per incidence
   bool long_mode = false;
   bool flat_mode = false;   // every read has at most one aligned segment: one record per incidence, in place
-  bool fused_emit = false;  // this run's group kernel builds the records itself (flat mode, set by the run)
   int64_t *scost = nullptr;
   int64_t n_seg = 0, region = 0, far_cap = 0, n_written = 0, region_per_incid = 0, n_id_ops = 0;
   int64_t max_len = 0, max_seg = 0;         // longest read, most aligned segments of one read (plan)

@@ -33,7 +33,6 @@ struct ganon_ctx {
   int group_obs = 0;           // GANON_PARAM_GROUP_OBS (0 auto, 512, 1024)
   int prep_unroll = 0;         // GANON_PARAM_PREP_UNROLL (0 auto = 2, 1, 2, 4)
   int far_init = 0;            // GANON_PARAM_FAR_INIT (0 auto)
-  int fuse_emit = 0;           // GANON_PARAM_FUSE_EMIT (off: measured slower)
   bool step_open = false;      // ganon_batch_replan started a profiled step the next run continues
   std::string err;
   struct Rec { std::string name; hipEvent_t e0, e1; };

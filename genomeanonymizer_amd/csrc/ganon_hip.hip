@@ -311,9 +311,6 @@ constexpr int kGrpThreads = 256;
 #ifndef GANON_K2_BLOCKS
 #define GANON_K2_BLOCKS 6   // resident workgroups per CU the K = 2 instance is compiled for
 #endif
-#ifndef GANON_KE_BLOCKS
-#define GANON_KE_BLOCKS 6   // ... and its fused-emit instance
-#endif
 constexpr int kGrpTile = 256;        // segment records staged per tile
 constexpr int kGrpStack = 80;        // key ranges pending (bisection depth <= 64)
 constexpr int kGrpMap = 4096;        // chunk -> segment map entries (larger tiles binary-search)
@@ -352,9 +349,6 @@ struct GrpSharedT {
   int blk_calls, blk_bases;         // this workgroup's contribution to the totals
   int cnt_calls[kGrpMaxScopes];     // per-scope counts, written out once at the end
   int cnt_bases[kGrpMaxScopes];
-  int off32[kGrpMaxScopes + 1];     // fused emit: the group's scope offsets from its first incidence
-  unsigned long long hsum;          // fused emit: the group's write-scope hash sum
-  uint8_t clean[kGrpTile];          // fused emit: the staged record's reference range is all ACGT
 };
 
 struct GrpRange {
@@ -479,83 +473,15 @@ __device__ __forceinline__ void copy_windows(const uint8_t *__restrict__ src, ui
   }
 }
 
-// Where a fused-emit tile builds its records from (k_group EMIT).
-struct EmitTile {
-  const GrpAux *aux;
-  int64_t i_begin;   // the group's first incidence
-  int s_begin, ns;
-  bool first;        // the group's first pass over its records: the write-scope sums count it
-};
-
-// The fused one-segment emit (flat prep mode; k_prep_emit_flat's record for incidence i, built in
-// the group kernel instead of written to HBM and read back): the incidence checks (read index
-// before any gather through it, the read inside its scope's span), the write-scope hash of a read
-// met in its write scope, its one aligned segment as a record (zero-length: none, a huge scope or
-// a failed check) and whether its reference range is all ACGT (the 2-bit reference).
-__device__ __forceinline__ int4 emit_record(const EmitTile &E, const int *off32, int64_t i, bool &clean,
-                                           unsigned long long *hsum) {
-  const GrpAux *A = E.aux;
-  clean = false;
-  const int rd = gp(A->incid_read)[i];
-  const int j = [&] {   // the staged scope of incidence i (largest j with off32[j] <= i - i_begin)
-    const int x = (int)(i - E.i_begin);
-    int lo = 0, hi = E.ns - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (off32[mid] <= x) lo = mid;
-      else hi = mid - 1;
-    }
-    return lo;
-  }();
-  int4 rec = make_int4(0, 0, 0, j);
-  if (rd < 0 || rd >= A->n_reads) {
-    report(A->err, kErrIncidRead, i, rd);
-    return rec;
-  }
-  const int s = E.s_begin + j;
-  const int64_t co = gp(A->cig_off)[rd];
-  const int nc = gp(A->n_cig)[rd], L = gp(A->read_len)[rd], rs = gp(A->ref_start)[rd], re = gp(A->read_end)[rd];
-  const int64_t so = gp(A->seq_off)[rd];
-  const int ds = gp(A->dataset)[rd], wsc = gp(A->write_scope)[rd];
-  const uint32_t w0 = nc > 0 ? gp(A->cigar)[co] : 0u;
-  const int ss = gp(A->span_start)[s], sl = gp(A->span_len)[s];
-  const int64_t r0 = gp(A->ref_off)[s] - ss;
-  if (rs < ss || re > ss + sl) {
-    report(A->err, kErrIncidSpan, s, rd);
-    return rec;
-  }
-  const bool mine = wsc == s;
-  if (mine && E.first) atomicAdd(hsum, ws_hash(rd));   // (LDS: no register lives across the kernel)
-  if (sl > kGrpMaxSpan) return rec;   // huge scope: the tile path
-  const uint32_t fl = ((uint32_t)ds << 30) | (mine ? kSegMine : 0u);
-  walk_segments(A->cigar + co, nc, L, rs, w0, [&](int q, int p, int n) {
-    const uint64_t sq = (uint64_t)(2 * so + q), rf = (uint64_t)(r0 + p);
-    const uint32_t z = (uint32_t)((sq >> 32) & 0xFF) | ((uint32_t)((rf >> 32) & 0xFF) << 8) | ((uint32_t)n << 16) | fl;
-    rec = make_int4((int)(uint32_t)sq, (int)(uint32_t)rf, (int)z, (int)((uint32_t)j | ((uint32_t)(p - ss) << 12)));
-    clean = ref_clean(A->bad, A->n_blk, (int64_t)rf, n);
-  });
-  return rec;
-}
-
 // Stage records [c0, c0 + nh) in LDS with the exclusive prefix of their chunk counts;
-// returns the tile's chunk total. EMIT: the records are built from the incidences (emit_record).
-template <bool EMIT, class SH>
-__device__ __forceinline__ int grp_tile(SH &sh, const int4 *__restrict__ rec4, int64_t c0, int nh,
-                                        int chunk, const EmitTile &E) {
+// returns the tile's chunk total.
+template <class SH>
+__device__ __forceinline__ int grp_tile(SH &sh, const int4 *__restrict__ rec4, int64_t c0, int nh, int chunk) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  int4 r;
-  bool cl = false;
-  if constexpr (EMIT) {
-    r = make_int4(0, 0, 0, 0);
-    if (tid < nh) r = emit_record(E, sh.off32, c0 + tid, cl, &sh.hsum);
-  } else {
-    const int64_t ix = c0 + (tid < nh ? tid : nh - 1);
-    r = rec4[ix];
-  }
+  const int4 r = rec4[c0 + (tid < nh ? tid : nh - 1)];
   int nck = 0;
   if (tid < nh) {
     sh.rec[tid] = r;
-    if constexpr (EMIT) sh.clean[tid] = cl;
     nck = ((((uint32_t)r.z >> 16) & kSegMaxLen) + chunk - 1) / chunk;
   }
   // wave inclusive scan: DPP row_shr within each 16-lane row, then the row totals (no lane-index
@@ -666,26 +592,18 @@ __device__ __forceinline__ void grp_chunk(const GrpBatch &B, SH &sh, const GrpRa
   }
 }
 
-// Stream every chunk of every segment of the group, feeding observations in range R. EMIT: the
-// records come from the incidences (grp_tile) and each wave reads the 2-bit reference when every
-// record it meets has an all-ACGT reference range, else the nt16 one.
-template <int K, bool REF2, bool EMIT, class SH>
+// Stream every chunk of every segment of the group, feeding observations in range R.
+template <int K, bool REF2, class SH>
 __device__ __forceinline__ void grp_scan(const GrpBatch &B, SH &sh, const GrpRange &R, const GrpGlobal &gg,
-                                         int64_t i_begin, int64_t i_end, const int4 *__restrict__ rec4, int skip,
-                                         const EmitTile &E) {
+                                         int64_t i_begin, int64_t i_end, const int4 *__restrict__ rec4, int skip) {
   const int tid = threadIdx.x;
   for (int64_t c0 = i_begin; c0 < i_end; c0 += kGrpTile) {
     const int nh = (int)((i_end - c0) < kGrpTile ? (i_end - c0) : kGrpTile);
-    int total = grp_tile<EMIT>(sh, rec4, c0, nh, 16 * K, E);
+    int total = grp_tile(sh, rec4, c0, nh, 16 * K);
     if (skip & kSkipChunks) total = 0;
     for (int t = tid; t < total; t += kGrpThreads) {
       const int j = grp_find(sh, nh, total, t);
-      if constexpr (EMIT) {
-        if (B.ref2 && __all(sh.clean[j])) grp_chunk<K, true>(B, sh, R, gg, t, j);
-        else grp_chunk<K, false>(B, sh, R, gg, t, j);
-      } else {
-        grp_chunk<K, REF2>(B, sh, R, gg, t, j);
-      }
+      grp_chunk<K, REF2>(B, sh, R, gg, t, j);
     }
     __syncthreads();
   }
@@ -916,48 +834,21 @@ __device__ __forceinline__ void grp_patch_bytes(const GrpBatch &B, SH &sh, int n
 // {seg_end lo, hi, seg_mid lo, hi}, {partition piece A begin lo, hi, end lo, hi} (bytes; fused
 // only), {global region offset lo, hi, capacity, 0}, {piece B begin lo, hi, end lo, hi};
 // segments [seg_begin, seg_mid) have an all-ACGT reference range (2-bit reference).
-// EMIT (one-segment prep mode): the group's scopes and incidences come from the batch scan's group
-// table, its overflow region in closed form, its records from its incidences (emit_record): the
-// prep's emit kernel and its 16-byte records in HBM are gone; the write-scope hash sum of the
-// group is written at the end.
-template <int U, bool FUSED, int OBS, bool EMIT = false>
-__global__ void __launch_bounds__(kGrpThreads, (OBS > 512 ? 4 : U == 1 ? 6 : U == 2 ? (EMIT ? GANON_KE_BLOCKS : GANON_K2_BLOCKS) : U == 4 ? 5 : 4)) k_group(const GrpBatch B, const int4 *__restrict__ groups,
+template <int U, bool FUSED, int OBS>
+__global__ void __launch_bounds__(kGrpThreads, (OBS > 512 ? 4 : U == 1 ? 6 : U == 2 ? GANON_K2_BLOCKS : U == 4 ? 5 : 4)) k_group(const GrpBatch B, const int4 *__restrict__ groups,
                                                        const int4 *__restrict__ rec4,
                                                        uint8_t *__restrict__ out, const GrpAux *__restrict__ aux,
                                                        int skip, int nt_copy) {
   __shared__ GrpSharedT<OBS> sh;
   const int tid = threadIdx.x;
+  const int4 g0 = groups[kGrpRec * blockIdx.x];
+  const int4 g1 = groups[kGrpRec * blockIdx.x + 1];
   const int4 g2 = groups[kGrpRec * blockIdx.x + 2];
+  const int4 g3 = groups[kGrpRec * blockIdx.x + 3];
   const int4 g4 = groups[kGrpRec * blockIdx.x + 4];
-  int s_begin, s_end;
-  int64_t i_begin, i_end, i_mid;
-  GrpGlobal gg;
-  if constexpr (EMIT) {
-    const int g = (int)blockIdx.x;
-    const longlong2 m0 = aux->gmeta[g];
-    const longlong2 m1 = g + 1 < aux->n_groups ? aux->gmeta[g + 1] : make_longlong2(aux->n_scopes, aux->n_incid);
-    s_begin = (int)m0.x;
-    s_end = (int)m1.x;
-    i_begin = m0.y;
-    i_end = m1.y;
-    i_mid = i_end;
-    const int64_t rpi = aux->region_per_incid;
-    gg = GrpGlobal{aux, i_begin * rpi + (int64_t)kGrpObs * g,
-                   (int)min((i_end - i_begin) * rpi + kGrpObs, (long long)(INT32_MAX / 2))};
-    for (int t = tid; t <= s_end - s_begin; t += kGrpThreads)
-      sh.off32[t] = (int)(gp(aux->incid_off)[s_begin + t] - i_begin);
-  } else {
-    const int4 g0 = groups[kGrpRec * blockIdx.x];
-    const int4 g1 = groups[kGrpRec * blockIdx.x + 1];
-    const int4 g3 = groups[kGrpRec * blockIdx.x + 3];
-    gg = GrpGlobal{aux, i64_of(g3.x, g3.y), g3.z};
-    s_begin = g0.x;
-    s_end = g0.y;
-    i_begin = i64_of(g0.z, g0.w);
-    i_end = i64_of(g1.x, g1.y);
-    i_mid = i64_of(g1.z, g1.w);
-  }
-  const EmitTile E{aux, i_begin, s_begin, s_end - s_begin, true};
+  const GrpGlobal gg{aux, i64_of(g3.x, g3.y), g3.z};
+  const int s_begin = g0.x, s_end = g0.y;
+  const int64_t i_begin = i64_of(g0.z, g0.w), i_end = i64_of(g1.x, g1.y), i_mid = i64_of(g1.z, g1.w);
   const PatchSink sink{out, i64_of(g2.x, g2.y), i64_of(g2.z, g2.w), i64_of(g4.x, g4.y), i64_of(g4.z, g4.w),
                        aux, FUSED, FUSED};
   // the partition pieces, whole 16-byte windows (the buffers are padded past seq_bytes); the
@@ -970,7 +861,6 @@ __global__ void __launch_bounds__(kGrpThreads, (OBS > 512 ? 4 : U == 1 ? 6 : U =
   }
   if (tid == 0) {
     sh.top = 0;
-    sh.hsum = 0ull;
     sh.stk_lo[0] = 0ull;
     sh.stk_hi[0] = ~0ull;
     sh.stk_mode[0] = kModeCollect;
@@ -982,7 +872,6 @@ __global__ void __launch_bounds__(kGrpThreads, (OBS > 512 ? 4 : U == 1 ? 6 : U =
     sh.cnt_calls[i] = 0;
     sh.cnt_bases[i] = 0;
   }
-  bool first_pass = true;   // (the first key range is the whole one: every record once)
   for (;;) {
     __syncthreads();
     const int top = sh.top;
@@ -998,8 +887,6 @@ __global__ void __launch_bounds__(kGrpThreads, (OBS > 512 ? 4 : U == 1 ? 6 : U =
         gp(aux->part)[2 * blockIdx.x] = sh.blk_calls;
         gp(aux->part)[2 * blockIdx.x + 1] = sh.blk_bases;
       }
-      if constexpr (EMIT)   // the group's write-scope hash sum (k_finish compares the batch's)
-        if (tid == 0) gp(aux->ws_part)[blockIdx.x] = sh.hsum;
       break;
     }
     const GrpRange R{sh.stk_lo[top], sh.stk_hi[top], sh.stk_mode[top]};
@@ -1011,16 +898,12 @@ __global__ void __launch_bounds__(kGrpThreads, (OBS > 512 ? 4 : U == 1 ? 6 : U =
       sh.kmax = 0ull;
     }
     __syncthreads();
-    if constexpr (EMIT) {
-      const EmitTile Ep{E.aux, E.i_begin, E.s_begin, E.ns, first_pass};
-      grp_scan<U, false, true>(B, sh, R, gg, i_begin, i_end, rec4, skip, Ep);
-    } else if (B.ref2) {
-      grp_scan<U, true, false>(B, sh, R, gg, i_begin, i_mid, rec4, skip, E);
-      grp_scan<U, false, false>(B, sh, R, gg, i_mid, i_end, rec4, skip, E);
+    if (B.ref2) {
+      grp_scan<U, true>(B, sh, R, gg, i_begin, i_mid, rec4, skip);
+      grp_scan<U, false>(B, sh, R, gg, i_mid, i_end, rec4, skip);
     } else {
-      grp_scan<U, false, false>(B, sh, R, gg, i_begin, i_end, rec4, skip, E);
+      grp_scan<U, false>(B, sh, R, gg, i_begin, i_end, rec4, skip);
     }
-    first_pass = false;
     // (grp_scan ends on a barrier)
     if (skip & kSkipClassify) continue;
     const int n = sh.n_obs;
@@ -1525,32 +1408,6 @@ int prepare(ganon_ctx *ctx, ganon_dbatch *db, const ganon_batch *host) {
   a.opay = static_cast<unsigned long long *>(db->b_gopay.p);
   a.tkey = static_cast<unsigned long long *>(db->b_gtkey.p);
   a.tflag = static_cast<unsigned int *>(db->b_gtflag.p);
-  // the fused one-segment emit
-  const DevBatch &B = db->B;
-  a.gmeta = static_cast<const longlong2 *>(db->b_gs0.p);
-  a.n_groups = db->n_groups;
-  a.n_scopes = db->n_scopes;
-  a.n_reads = db->n_reads;
-  a.n_incid = db->n_incid;
-  a.region_per_incid = db->region_per_incid;
-  a.n_blk = db->ref->n_blk;
-  a.incid_off = B.incid_off;
-  a.seq_off = B.seq_off;
-  a.cig_off = B.cig_off;
-  a.ref_off = B.ref_off;
-  a.incid_read = B.incid_read;
-  a.ref_start = B.ref_start;
-  a.read_len = B.read_len;
-  a.n_cig = B.n_cig;
-  a.write_scope = B.write_scope;
-  a.read_end = B.read_end;
-  a.span_start = B.span_start;
-  a.span_len = B.span_len;
-  a.dataset = B.dataset;
-  a.cigar = B.cigar;
-  a.bad = db->ref->bad;
-  a.ws_part = static_cast<unsigned long long *>(db->b_wspart.p);
-  a.err = db->err;
   unsigned long long *st = db->static_h;
   std::fill(st, st + GANON_N_TOTALS, 0ull);
   st[GANON_T_READS_IN] = (unsigned long long)db->n_reads;
@@ -1783,10 +1640,6 @@ GANON_API int ganon_ctx_set_param(ganon_ctx *ctx, int param, int value) {
     ctx->nt_copy = value != 0;
     return GANON_OK;
   }
-  if (param == GANON_PARAM_FUSE_EMIT) {
-    ctx->fuse_emit = value != 0;
-    return GANON_OK;
-  }
   if (param == GANON_PARAM_FAR_INIT) {
     if (value < 0) return fail(ctx, GANON_E_ARG, "far-mask list capacity must be >= 0");
     ctx->far_init = value;
@@ -1880,9 +1733,6 @@ GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
   // 16-base chunks per thread: long reads (short segments between indels) waste less with one
   // (profiles/r02/sweep_c5.jsonl); short reads run best with two (sweep_c3.jsonl)
   const int u = ctx->group_unroll ? ctx->group_unroll : db->long_mode ? 1 : 2;
-  // one-segment prep mode: the group kernel builds its records from the incidences (no emit kernel,
-  // no records in HBM); GANON_PARAM_FUSE_EMIT 0 keeps the separate emit for A/B
-  db->fused_emit = db->flat_mode && u == 2 && ctx->fuse_emit;
   // 1. derived layer from the raw SoA
   if ((rc = ganon_prep::run(ctx, db))) return rc;
   if (db->n_huge_scopes) {
@@ -1896,8 +1746,7 @@ GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
     // 512 unless forced: the 1024-entry list (4 workgroups per CU instead of 6) measured slower on
     // c3 too (3.19 vs 2.84 ms, profiles/r02/sweep_c3_obs.jsonl) — occupancy outweighs the region path
     const int obs = ctx->group_obs ? ctx->group_obs : 512;
-    auto kern = db->fused_emit ? (obs == 1024 ? k_group<2, true, 1024, true> : k_group<2, true, 512, true>)
-                : obs == 1024 ? (u == 1 ? k_group<1, true, 1024> : k_group<2, true, 1024>)
+    auto kern = obs == 1024 ? (u == 1 ? k_group<1, true, 1024> : k_group<2, true, 1024>)
                             : u == 2 ? k_group<2, true, 512> : u == 4 ? k_group<4, true, 512>
                             : u == 8 ? k_group<8, true, 512> : k_group<1, true, 512>;
     const GrpBatch GB{B.seq, B.ref, B.keep_code, B.ref2, B.keep_pos, B.span_start, B.span_len};

@@ -10,33 +10,36 @@
 // records — one per aligned run: (query nibble, reference nibble, length, dataset, whether this
 // scope writes the read) — that k_group (ganon_hip.hip) streams in 16-base chunks.
 //
-// Kernels (integer work, HBM/latency bound, no MFMA), in launch order:
-//   (upload only) k_prep_reads / k_prep_scope_check / k_prep_incid_check / k_prep_seen_check:
-//                   every check of the round-1 host validation, on the device (no host loop);
-//   k_prep_groups   thread per scope: groups are the scopes whose (incidences + 3 per scope) prefix
-//                   — the CSR offsets themselves, no scan — falls in one bucket of group_target
-//                   units; the weight caps a group at 256 scopes;
-//   k_prep_emit     workgroup per group: scope metadata staged in LDS, each thread walks two
-//                   incidences' CIGARs (loads issued together), counts clean/dirty segments around
-//                   a block scan, takes the group's record range and overflow region from one of
-//                   256 allocation counters (bases fixed at upload), and writes the records (single-segment ones kept in registers
-//                   from the count); all-ACGT-reference segments fill the range from the front,
-//                   the others from the back (the group kernel reads the front part through the
-//                   2-bit reference); read_end; the lowest buffer offset of the reads the group
-//                   writes, per dataset (LDS atomicMin);
+// Kernels (integer work, HBM/latency bound, no MFMA), in launch order. Plan (ganon_batch_replan /
+// the upload; one host synchronization):
+//   k_prep_scan + k_prep_reduce  one pass over the raw per-read and per-scope arrays: every check of
+//                   the host validation, read_end, the batch shape (longest read, segments per
+//                   read, I/D ops, written reads, huge scopes, write-scope hash sum) as per-block
+//                   partials, and the group table of the short-read modes — groups are the scopes
+//                   whose (incidences + weight per scope) prefix, the CSR offsets themselves, falls
+//                   in one bucket of group_target units (the weight caps a group at 256 scopes);
+//   (long-read mode) k_prep_nseg + k_prep_scope_cost + exclusive scan: groups cut on the
+//                   segments-per-scope prefix instead;
+//   (two-pass and long modes) k_prep_groups + a counting emit: record ranges of groups with more
+//                   segments than incidences.
+// Run (ganon_batch_run):
 //   k_prep_emit_flat (every read with at most one aligned segment: short reads, the default then):
-//                   thread per incidence, its one record at the slot of its own index — no count
-//                   pass, no scan, no allocation; a group is read through the 2-bit reference unless
-//                   one of its records touches a non-ACGT block;
-//   k_prep_emit_long (long-read mode, a read with more than one aligned segment in the batch):
-//                   groups cut on the segments-per-scope prefix computed at upload, the record count
-//                   from the segments per read, one wave per incidence over the whole batch walking
-//                   its CIGAR 64 ops at a time (wave prefix sums of the query / reference deltas and
-//                   of the record counts) into deterministic slots — one walk, no atomics;
-//   k_prep_linemap + k_prep_pieces  the candidates mark their 128-byte lines in a 3-level
-//                   bitmap (ties on a line through a small hash table); each candidate's piece runs
-//                   from its line to the next marked one, so the pieces tile the output buffer —
-//                   each group copies at most two pieces. No sort.
+//                   workgroup per group, thread per incidence, its one record at the slot of its own
+//                   index — no count pass, no scan, no allocation; the incidence checks, the
+//                   write-scope hash sum and the group's partition candidates (lowest buffer offset
+//                   of the reads it writes, per dataset) marked in the line map; a group is read
+//                   through the 2-bit reference unless one of its records touches a non-ACGT block;
+//   k_prep_emit     (two-pass: short reads with indels) workgroup per group: counts clean/dirty
+//                   segments around a block scan, takes the group's record range (its own incidence
+//                   indices, or one of 256 allocation counters), writes the records —
+//                   all-ACGT-reference segments from the front, the others from the back;
+//   k_prep_long_groups + k_prep_emit_waves + k_prep_long_mid (long reads): one wave per incidence
+//                   walks its CIGAR 64 ops at a time (wave prefix sums of the query / reference
+//                   deltas and of the record counts) into deterministic slots — no atomics;
+//   k_prep_linemap + k_prep_pieces  the candidates' 128-byte lines form a 3-level bitmap (ties on a
+//                   line through a small hash table); each candidate's piece runs from its line to
+//                   the next marked one, so the pieces tile the output buffer — each group copies at
+//                   most two pieces. No sort.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -108,16 +111,14 @@ __device__ __forceinline__ int64_t group_of(const int64_t *__restrict__ incid_of
 // Replaces round 2's four check kernels, the segments-per-read pass and the far-capacity pass
 // (k_prep_reads / k_prep_scope_check / k_prep_incid_check / k_prep_seen_check / k_prep_farcap):
 // one coalesced read of each per-read and per-scope array. Read blocks validate every read field
-// before any load that depends on it, write read_end (bam_endpos) and the aligned segments per
-// read, and fold the read into its write scope's group candidate (the lowest buffer offset of
-// the reads a group writes, per dataset; short-read groups, closed form from the CSR offsets);
-// scope blocks validate the scope arrays and write the group table (first scope and incidence of
-// each group). Per-block partial sums (no same-address atomics: a batch-wide counter hit once
-// per wave serialised k_prep_reads at 0.8 ms) go to `part`, reduced by k_prep_reduce. The
-// incidence checks (read index, span containment) and the write-scope check need the scope of
-// each incidence: the emit kernels make them where they walk the incidences anyway, and
-// k_prep_seen_check runs after the masking kernels (neither can fault: the emit kernels range-check
-// before they gather). Their errors are reported by ganon_batch_download.
+// before any load that depends on it, write read_end (bam_endpos) and count the aligned segments
+// and I/D ops per read; scope blocks validate the scope arrays and write the group table (first
+// scope and incidence of each short-read group, closed form from the CSR offsets). Per-block
+// partial sums (no same-address atomics: a batch-wide counter hit once per wave serialised
+// k_prep_reads at 0.8 ms) go to `part`, reduced by k_prep_reduce. The incidence checks (read
+// index, span containment) and the write-scope check need the scope of each incidence: the emit
+// kernels make them where they walk the incidences anyway (neither can fault: they range-check
+// before they gather); ganon_batch_download reports their errors.
 enum { kPartWritten = 0, kPartMaxLen, kPartMaxSeg, kPartIdOps, kPartHuge, kPartWsHash, kParts };
 
 // The write-scope check without a per-read mark: every written read r contributes ws_hash(r) once
@@ -147,7 +148,6 @@ constexpr int kScanScopesPerBlock = 4 * kPrepThreads;
 
 struct ScanOut {
   int32_t *read_end;
-  unsigned long long *lo;     // [2 g_bound] group candidates (kNone-initialised), short-read groups
   longlong2 *gmeta;           // [g_bound] first scope and incidence of each short-read group
   int64_t g_bound;            // group count bound: (n_incid + weight (n_scopes - 1)) / target + 1
   unsigned long long *part;   // [kParts x blocks]
@@ -156,27 +156,6 @@ struct ScanOut {
 __device__ __forceinline__ unsigned long long shfl64(unsigned long long v, int lane) {
   const uint32_t lo = __shfl((uint32_t)v, lane), hi = __shfl((uint32_t)(v >> 32), lane);
   return ((unsigned long long)hi << 32) | lo;
-}
-
-// Wave-aggregated atomicMin of (key -> value) pairs (kNone keys absent): one atomic per distinct
-// key in the wave (a wave of reads in buffer order meets one or two groups per dataset).
-__device__ __forceinline__ void wave_min_by_key(unsigned long long *__restrict__ dst, unsigned long long key,
-                                                unsigned long long val) {
-  const int lane = threadIdx.x & 63;
-  unsigned long long m = __ballot(key != kNone);
-  while (m) {
-    const int l = __ffsll((long long)m) - 1;
-    const unsigned long long k0 = shfl64(key, l);
-    const bool same = key == k0;
-    unsigned long long v = same ? val : kNone;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const unsigned long long x = shfl64(v, lane ^ o);
-      v = x < v ? x : v;
-    }
-    if (lane == l) atomicMin(dst + k0, v);
-    m &= ~__ballot(same);
-  }
 }
 
 __device__ __forceinline__ void block_parts(unsigned long long (&acc)[kParts], unsigned long long *__restrict__ part) {
@@ -208,7 +187,7 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_scan(const Raw R, PrepErr
   const int tid = threadIdx.x;
   if ((int)blockIdx.x < read_blocks) {
     // kScanU reads per thread, each load stage issued for all of them before any is used (the chain
-    // read fields -> first CIGAR word -> the write scope's CSR offset is latency bound)
+    // read fields -> first CIGAR word is latency bound)
     constexpr int kScanU = kScanReadsPerBlock / kPrepThreads;
     const int64_t r0 = (int64_t)blockIdx.x * kScanReadsPerBlock;
     const int64_t r1 = min(r0 + kScanReadsPerBlock, (int64_t)R.n_reads);
@@ -229,7 +208,6 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_scan(const Raw R, PrepErr
       ds[u] = R.dataset[rr];
     }
     uint32_t w0[kScanU];
-    int64_t goff[kScanU];
 #pragma unroll
     for (int u = 0; u < kScanU; ++u) {
       const int64_t r = r0 + tid + kPrepThreads * u;
@@ -241,14 +219,10 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_scan(const Raw R, PrepErr
       if (L[u] >= (1 << 24)) report(err, kErrReadLong, r);
     }
 #pragma unroll
-    for (int u = 0; u < kScanU; ++u) {
-      w0[u] = ok[u] && nc[u] > 0 ? R.cigar[co[u]] : 0u;
-      goff[u] = ok[u] && ws[u] >= 0 ? R.incid_off[ws[u]] : 0;
-    }
+    for (int u = 0; u < kScanU; ++u) w0[u] = ok[u] && nc[u] > 0 ? R.cigar[co[u]] : 0u;
 #pragma unroll
     for (int u = 0; u < kScanU; ++u) {
       const int64_t r = r0 + tid + kPrepThreads * u;
-      unsigned long long ckey = kNone, cval = 0;
       if (ok[u]) {
         acc[kPartWritten] += ws[u] >= 0;
         if (ws[u] >= 0) acc[kPartWsHash] += ws_hash((int)r);
@@ -279,15 +253,8 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_scan(const Raw R, PrepErr
           O.read_end[r] = (int32_t)(rs[u] + (rl > 0 ? rl : 1));
           acc[kPartMaxSeg] = max(acc[kPartMaxSeg], (unsigned long long)ns);
           acc[kPartIdOps] += (unsigned long long)nid;
-          if (ws[u] >= 0 && L[u] > 0 && ds[u] <= 1) {
-            int64_t g = (goff[u] + weight * ws[u]) / target;   // group_of, short-read groups
-            g = g < 0 ? 0 : (g >= O.g_bound ? O.g_bound - 1 : g);
-            ckey = 2 * (unsigned long long)g + (unsigned long long)ds[u];
-            cval = (unsigned long long)so[u];
-          }
         }
       }
-      wave_min_by_key(O.lo, ckey, cval);
     }
   } else {
     const int64_t s0 = (int64_t)(blockIdx.x - read_blocks) * kScanScopesPerBlock;
@@ -528,15 +495,6 @@ __device__ void map_mark(const LineMap &M, unsigned long long key, uint32_t c) {
       atomicMax(&M.hval[h], v);
       return;
     }
-  }
-}
-
-// Flat mode: the candidates k_prep_scan folded per group mark their lines.
-__global__ void __launch_bounds__(kPrepThreads) k_prep_mark(const unsigned long long *__restrict__ lo, int n_cand,
-                                                            LineMap M) {
-  for (int64_t c = blockIdx.x * (int64_t)kPrepThreads + threadIdx.x; c < n_cand; c += (int64_t)gridDim.x * kPrepThreads) {
-    const unsigned long long k = lo[c];
-    if (k != kNone) map_mark(M, k, (uint32_t)c);
   }
 }
 
@@ -895,20 +853,23 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_emit(const Raw R, const l
 // the whole range), any other group through the nt16 reference.
 constexpr unsigned long long kLongReadLen = 1000;   // auto prep: long-read mode above this read length
 
-// kFlatU: incidences per thread and trip (GANON_PARAM_PREP_UNROLL). The group candidates come from
-// k_prep_scan (closed-form groups); this kernel makes the incidence checks, marks the reads met in
-// their write scope and writes the records and group records 0, 1 and 3.
+// kFlatU: incidences per thread and trip (GANON_PARAM_PREP_UNROLL). Besides the records and group
+// records 0, 1 and 3 the kernel makes the incidence checks, sums the write-scope hashes of the
+// reads met in their write scope and marks the group's partition candidates (the lowest buffer
+// offset of the reads it writes, per dataset) in the line map.
 template <int kFlatU>
 __global__ void __launch_bounds__(kPrepThreads) k_prep_emit_flat(const Raw R, const longlong2 *__restrict__ gmeta,
                                                                  int n_groups, const uint64_t *__restrict__ bad,
                                                                  int64_t n_blk, long long region_per_incid,
                                                                  const Checks C, int4 *__restrict__ seg4,
-                                                                 int4 *__restrict__ groups) {
+                                                                 int4 *__restrict__ groups,
+                                                                 unsigned long long *__restrict__ lo, LineMap M) {
   __shared__ long long off[kGrpMaxScopes + 1];
   __shared__ long long ref0[kGrpMaxScopes];
   __shared__ int sstart[kGrpMaxScopes], send[kGrpMaxScopes];
   __shared__ uint8_t huge[kGrpMaxScopes];
   __shared__ int s_dirty;
+  __shared__ unsigned long long lmin[2];
   const int tid = threadIdx.x;
   const int g = blockIdx.x;
   const longlong2 m0 = gmeta[g];
@@ -923,9 +884,10 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_emit_flat(const Raw R, co
     huge[t] = R.span_len[s0 + t] > kGrpMaxSpan;
   }
   if (tid == 0) s_dirty = 0;
+  if (tid < 2) lmin[tid] = kNone;
   __syncthreads();
   bool dirty = false;
-  unsigned long long hsum = 0;
+  unsigned long long hsum = 0, mn0 = kNone, mn1 = kNone;
   // kFlatU incidences per thread and trip, their loads issued together (the chain incidence -> read
   // fields -> CIGAR -> reference block bitmap is latency bound)
   for (long long base = i0; base < i1; base += kFlatU * kPrepThreads) {
@@ -967,7 +929,13 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_emit_flat(const Raw R, co
         ok = false;
       }
       const bool mine = ok && x.wsc == s0 + j;
-      if (mine) hsum += ws_hash(x.r);
+      if (mine) {
+        hsum += ws_hash(x.r);
+        if (x.L > 0) {
+          if (x.ds) mn1 = min(mn1, (unsigned long long)x.so);
+          else mn0 = min(mn0, (unsigned long long)x.so);
+        }
+      }
       if (ok && !huge[j]) {
         const uint32_t fl = ((uint32_t)x.ds << 30) | (mine ? kSegMine : 0u);
         const int64_t qnib = 2 * x.so, r0 = ref0[j];
@@ -983,8 +951,20 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_emit_flat(const Raw R, co
     }
   }
   if (__any(dirty) && (tid & 63) == 0) s_dirty = 1;
+  for (int o = 32; o > 0; o >>= 1) {
+    mn0 = min(mn0, (unsigned long long)__shfl_xor(mn0, o));
+    mn1 = min(mn1, (unsigned long long)__shfl_xor(mn1, o));
+  }
+  if ((tid & 63) == 0) {
+    if (mn0 != kNone) atomicMin(&lmin[0], mn0);
+    if (mn1 != kNone) atomicMin(&lmin[1], mn1);
+  }
   __shared__ unsigned long long hws[kWaves];
-  const unsigned long long h = block_sum_u64(hsum, hws);   // (its barriers order s_dirty too)
+  const unsigned long long h = block_sum_u64(hsum, hws);   // (its barriers order s_dirty and lmin too)
+  if (tid < 2) {
+    lo[2 * (int64_t)g + tid] = lmin[tid];
+    if (lmin[tid] != kNone) map_mark(M, lmin[tid], (uint32_t)(2 * g + tid));
+  }
   if (tid == 0) {
     C.ws_part[g] = h;
     const int64_t seg_b = i0, seg_e = i1, mid = s_dirty ? seg_b : seg_e;
@@ -1292,7 +1272,8 @@ int launch_emit(ganon_ctx *ctx, ganon_dbatch *db, const Raw &R, int write) {
     hipLaunchKernelGGL(flat, dim3((unsigned)db->n_groups), dim3(kPrepThreads), 0, ctx->stream, R,
                        static_cast<const longlong2 *>(db->b_gs0.p), db->n_groups, db->ref->bad, db->ref->n_blk,
                        (long long)db->region_per_incid, checks_of(db), static_cast<int4 *>(db->b_seg4.p),
-                       static_cast<int4 *>(db->b_groups.p));
+                       static_cast<int4 *>(db->b_groups.p), static_cast<unsigned long long *>(db->b_lo.p),
+                       line_map(db));
     return check_launch(ctx, "k_prep_emit_flat");
   }
   hipLaunchKernelGGL(k_prep_emit, dim3((unsigned)db->n_groups), dim3(kPrepThreads), 0, ctx->stream, R,
@@ -1308,11 +1289,6 @@ int launch_pieces(ganon_ctx *ctx, ganon_dbatch *db) {
   if (!db->n_groups) return GANON_OK;
   KernelScope ks(ctx, "prep_pieces");
   const LineMap M = line_map(db);
-  if (db->flat_mode) {   // the candidates of k_prep_scan mark their lines
-    HIP_OR_FAIL(hipMemsetAsync(db->b_linemap.p, 0, (size_t)line_map_words(db) * 8, st));
-    hipLaunchKernelGGL(k_prep_mark, dim3(grid_for(n_cand)), dim3(kPrepThreads), 0, st,
-                       static_cast<const unsigned long long *>(db->b_lo.p), n_cand, M);
-  }
   hipLaunchKernelGGL(k_prep_linemap, dim3(grid_for(M.n1)), dim3(kPrepThreads), 0, st, M);
   hipLaunchKernelGGL(k_prep_pieces, dim3(grid_for(n_cand)), dim3(kPrepThreads), 0, st,
                      static_cast<const unsigned long long *>(db->b_lo.p), n_cand, M, db->seq_bytes,
@@ -1362,22 +1338,20 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db) {
   const long long w0 = weight_of(tgt0);
   const int64_t g_bound = ns ? (db->n_incid + w0 * (ns - 1)) / tgt0 + 1 : 1;
   longlong2 *gm = nullptr;
-  unsigned long long *lo = nullptr, *part = nullptr;
+  unsigned long long *part = nullptr;
   const int64_t rb = (nr + kScanReadsPerBlock - 1) / kScanReadsPerBlock;
   const int64_t sb = (ns + kScanScopesPerBlock - 1) / kScanScopesPerBlock;
   const int64_t nb = std::max<int64_t>(1, rb + sb);
   if (nb > INT32_MAX) return fail(ctx, GANON_E_ARG, "batch too large");
-  if ((rc = grow_n(ctx, db->b_gs0, (size_t)g_bound, &gm)) || (rc = grow_n(ctx, db->b_lo, 2 * (size_t)g_bound, &lo)) ||
-      (rc = grow_n(ctx, db->b_part, (size_t)kParts * nb, &part)))
+  if ((rc = grow_n(ctx, db->b_gs0, (size_t)g_bound, &gm)) || (rc = grow_n(ctx, db->b_part, (size_t)kParts * nb, &part)))
     return rc;
   {
-    // 1. the batch scan: every per-read and per-scope check, read ends, segments per read, the group
-    //    table and candidates of the short-read modes, per-block partials; then their reduction
+    // 1. the batch scan: every per-read and per-scope check, read ends, the group table of the
+    //    short-read modes, per-block partials; then their reduction
     KernelScope ks(ctx, "prep_scan");
     HIP_OR_FAIL(hipMemsetAsync(db->err, 0, sizeof(PrepErr), st));
-    HIP_OR_FAIL(hipMemsetAsync(lo, 0xFF, 2 * (size_t)g_bound * sizeof(unsigned long long), st));
     hipLaunchKernelGGL(k_prep_scan, dim3((unsigned)nb), dim3(kPrepThreads), 0, st, R, db->err,
-                       ScanOut{read_end, lo, gm, g_bound, part}, w0, (long long)tgt0, (int)rb);
+                       ScanOut{read_end, gm, g_bound, part}, w0, (long long)tgt0, (int)rb);
     hipLaunchKernelGGL(k_prep_reduce, dim3(1), dim3(kPrepThreads), 0, st, R, part, (int)nb, w0, (long long)tgt0, g_bound,
                        db->plan_info);
     if ((rc = check_launch(ctx, "k_prep_scan"))) return rc;
@@ -1443,7 +1417,7 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db) {
   int4 *grp = nullptr;
   unsigned long long *u64 = nullptr;
   uint32_t *u32 = nullptr;
-  // (short-read modes: ng <= g_bound, so the scan's group table and candidates stay in place)
+  // (short-read modes: ng <= g_bound, so the scan's group table stays in place)
   if ((rc = grow_n(ctx, db->b_gs0, (size_t)std::max<int64_t>(ng, 1), &gm)) ||
       (rc = grow_n(ctx, db->b_groups, (size_t)kGrpRec * ng, &grp)) ||
       (rc = grow_n(ctx, db->b_grp_part, 2 * (size_t)ng, &p32)) ||
@@ -1493,11 +1467,15 @@ int run(ganon_ctx *ctx, ganon_dbatch *db) {
   const Raw R = raw_of(db);
   int rc;
   if (!db->n_groups) return GANON_OK;
-  if (db->flat_mode) {   // the scan's group table is in place
-    if ((rc = launch_pieces(ctx, db))) return rc;
-    return db->fused_emit ? GANON_OK : launch_emit(ctx, db, R, 1);   // (fused: the group kernel emits)
+  if (db->flat_mode) {   // the scan's group table is in place; the emit marks the line map
+    {
+      KernelScope ks(ctx, "prep_emit");
+      HIP_OR_FAIL(hipMemsetAsync(db->b_linemap.p, 0, (size_t)line_map_words(db) * 8, ctx->stream));
+    }
+    if ((rc = launch_emit(ctx, db, R, 1))) return rc;
+  } else if ((rc = launch_groups(ctx, db, R)) || (rc = launch_emit(ctx, db, R, 1))) {
+    return rc;
   }
-  if ((rc = launch_groups(ctx, db, R)) || (rc = launch_emit(ctx, db, R, 1))) return rc;
   return launch_pieces(ctx, db);
 }
 

@@ -205,7 +205,6 @@ PARAM_PREP_LONG = 9      # include/ganon.h GANON_PARAM_PREP_LONG (-1 auto, 0 nev
 PARAM_GROUP_OBS = 10     # include/ganon.h GANON_PARAM_GROUP_OBS (0 auto, 512, 1024)
 PARAM_PREP_UNROLL = 11   # include/ganon.h GANON_PARAM_PREP_UNROLL (0 auto, 1, 2, 4)
 PARAM_FAR_INIT = 12      # include/ganon.h GANON_PARAM_FAR_INIT (first far-mask list capacity; 0 auto)
-PARAM_FUSE_EMIT = 13     # include/ganon.h GANON_PARAM_FUSE_EMIT (1: the group kernel emits its records)
 
 EXPORTED_HIP_SYMBOLS = (
     "ganon_ctx_create", "ganon_ctx_destroy", "ganon_last_error", "ganon_abi_version",

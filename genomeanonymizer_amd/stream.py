@@ -30,6 +30,7 @@ their resolution plus the prefetched ones, and the carried records of names stil
 from __future__ import annotations
 
 import os
+import threading
 import time
 from concurrent.futures import ThreadPoolExecutor
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -638,7 +639,7 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
     if block_size is None:
         block_size = _writer.io_block_size(os.path.dirname(os.path.abspath(tumor_out)))
     timing = {"decode_s": 0.0, "plan_s": 0.0, "mask_s": 0.0, "format_s": 0.0, "prefetch_s": 0.0, "resolve_s": 0.0,
-              "write_s": 0.0, "wait_s": 0.0, "prunes": 0, "jobs": 0, "reads": 0, "bases": 0}
+              "write_s": 0.0, "wait_s": 0.0, "writer_wait_s": 0.0, "prunes": 0, "jobs": 0, "reads": 0, "bases": 0}
     failure: Optional[BaseException] = None
     if rank == 0:
         for p in paths:
@@ -676,7 +677,6 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
             for r in range(world):   # every worker still waiting for a resolution stops
                 link.send_resolution(r, {"err": err})
 
-    import threading
     coord_thread = threading.Thread(target=coordinate, name="ganon-coordinator", daemon=True) if rank == 0 else None
     if coord_thread is not None:
         coord_thread.start()
@@ -698,27 +698,46 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
             ahead[j] = pool.submit(JobPrep, j, contigs[j], readers, fasta, windows, dec)
             nxt[0] += 1
 
-    pending: "List[Job]" = []
+    # the writer thread: each exported job, in order, waits for its resolution, splices its bytes and
+    # writes them at their offsets while the main thread masks and formats the next contigs (the
+    # splice is numpy and native code, the writes are pwrite: both mostly outside the GIL).
+    # GANON_WRITER=0 writes in line.
+    writer = ThreadPoolExecutor(1) if os.environ.get("GANON_WRITER", "1") != "0" else None
+    pending: list = []          # futures of the writer (or jobs, in line)
+    writer_failed = threading.Event()
+
+    def finish(job: "Job") -> None:
+        if writer_failed.is_set():   # an earlier job failed: its resolution may never come
+            return
+        try:
+            t0 = time.time()
+            res = link.recv_resolution()
+            timing["wait_s"] += time.time() - t0
+            if res.get("err") is not None:
+                raise RuntimeError(f"another rank failed: {res['err']}")
+            if res["job"] != job.job:
+                raise RuntimeError(f"resolution of job {res['job']} for job {job.job}")
+            t1 = time.time()
+            data = job.output(res["out_n"], res["out_w"], res["ext"], block_size)
+            for f in range(4):
+                if len(data[f]) != res["sizes"][f]:
+                    raise RuntimeError(f"job {job.job}: {len(data[f])} bytes for file {f}, {res['sizes'][f]} planned")
+                if data[f]:
+                    os.pwrite(fds[f], data[f], res["offsets"][f])
+            stats_rows.append((job.job, job.stats()))
+            timing["write_s"] += time.time() - t1
+        except BaseException:
+            writer_failed.set()
+            raise
 
     def finish_oldest() -> None:
-        nonlocal failure
-        t0 = time.time()
-        res = link.recv_resolution()
-        timing["wait_s"] += time.time() - t0
-        if res.get("err") is not None:
-            raise RuntimeError(f"another rank failed: {res['err']}")
-        job = pending.pop(0)
-        if res["job"] != job.job:
-            raise RuntimeError(f"resolution of job {res['job']} for job {job.job}")
-        t1 = time.time()
-        data = job.output(res["out_n"], res["out_w"], res["ext"], block_size)
-        for f in range(4):
-            if len(data[f]) != res["sizes"][f]:
-                raise RuntimeError(f"job {job.job}: {len(data[f])} bytes for file {f}, {res['sizes'][f]} planned")
-            if data[f]:
-                os.pwrite(fds[f], data[f], res["offsets"][f])
-        stats_rows.append((job.job, job.stats()))
-        timing["write_s"] += time.time() - t1
+        p = pending.pop(0)
+        if writer is None:
+            finish(p)
+        else:
+            t0 = time.time()
+            p.result()
+            timing["writer_wait_s"] += time.time() - t0
 
     try:
         try:
@@ -739,7 +758,7 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
                 totals += np.asarray(job.res.totals, np.int64)[:8]
                 link.send_export(exp)
                 job.release_device()
-                pending.append(job)
+                pending.append(job if writer is None else writer.submit(finish, job))
                 while len(pending) >= pend_max:
                     finish_oldest()
             while pending:
@@ -748,6 +767,12 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
             failure = e
             # the coordinator may be waiting for this rank's next export: tell it
             link.send_export({"err": repr(e)})
+            if writer is not None:   # jobs not started yet are dropped; the running one gets the error
+                writer_failed.set()
+                for p in pending:
+                    p.cancel()
+                writer.shutdown(wait=True)
+                writer = None
         if coord_thread is not None:
             coord_thread.join()
             timing["resolve_s"] = coord.resolve_s
@@ -774,6 +799,8 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
                         merged[key] = list(counts)
             write_statistics(normal_stats_path or f"{normal_bam}.statistics.txt", merged)
     finally:
+        if writer is not None:
+            writer.shutdown(wait=True)
         if pool is not None:      # prefetches still running (a failed job) end before their reader closes
             for f in ahead.values():
                 f.cancel()

@@ -140,11 +140,7 @@ GANON_API int ganon_ctx_set_variant(ganon_ctx *ctx, int variant);
 enum { GANON_PARAM_GROUP_UNROLL = 1, GANON_PARAM_GROUP_SKIP = 2, GANON_PARAM_GROUP_TARGET = 3,
        GANON_PARAM_NT_COPY = 4, GANON_PARAM_REF2 = 5, GANON_PARAM_FASTQ_SKIP = 6, GANON_PARAM_FASTQ_KD = 7,
        GANON_PARAM_INDEL_SORT = 8, GANON_PARAM_PREP_LONG = 9, GANON_PARAM_GROUP_OBS = 10,
-       GANON_PARAM_PREP_UNROLL = 11, GANON_PARAM_FAR_INIT = 12, GANON_PARAM_FUSE_EMIT = 13 };
-/* GANON_PARAM_FUSE_EMIT: in the one-segment prep mode the group kernel builds each tile's segment
- * records from the incidences itself (1) instead of reading those the prep's emit kernel wrote to
- * HBM (0, default: the in-kernel gathers stall the group kernel more than the emit kernel costs,
- * DESIGN.md 4a). Same results. */
+       GANON_PARAM_PREP_UNROLL = 11, GANON_PARAM_FAR_INIT = 12 };
 /* GANON_PARAM_FAR_INIT: first capacity of a batch's far-mask list (entries; 0 = auto, n_reads / 8 but
  * at least 65536). A run that needs more is run again by ganon_batch_download with the list grown
  * to the count it needed (testing knob: 1 forces that path). */

@@ -17,9 +17,9 @@ import json
 import re
 import sys
 
-# kernels of one ganon_batch_run + ganon_indel_run (validation, k_prep_reads, the reference copies and
-# the record download run at upload / download only)
-STEP_KERNELS = {"k_prep_groups", "k_prep_emit", "k_prep_emit_flat", "k_prep_emit_waves", "k_prep_long_groups",
+# kernels of one fresh-batch step: ganon_batch_replan + ganon_batch_run + ganon_indel_run (the
+# reference copies and the record download run at upload / download only)
+STEP_KERNELS = {"k_prep_scan", "k_prep_reduce", "k_prep_nseg", "k_prep_scope_cost", "k_prep_groups", "k_prep_emit", "k_prep_emit_flat", "k_prep_emit_waves", "k_prep_long_groups",
                 "k_prep_long_mid", "k_prep_linemap", "k_prep_pieces", "k_group", "k_finish", "k_tile_large",
                 "k_mask_large", "k_indel_mark", "k_indel_count", "k_indel_emit", "k_indel_segs", "k_indel_runs",
                 "k_indel_classify", "rocprim_sort", "rocprim_scan", "rocprim_other"}
@@ -66,7 +66,7 @@ def main():
     res["step_kernels"] = sorted(k for k in res["kernels"] if k in STEP_KERNELS)
     res["method"] = ("TCC_EA0_RDREQ_{32B,64B,128B} x size + TCC_EA0_WRREQ{,_64B}; three rocprofv3 --pmc passes "
                      "(tools/gpu_pmc_step.sh) over bench.py --steps 3, mean over dispatches; step = the kernels of "
-                     "one ganon_batch_run + ganon_indel_run (step_kernels), one launch each")
+                     "one fresh-batch step, replan + run + indel tally (step_kernels), one launch each")
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps({k: v["hbm_bytes_per_launch"] for k, v in res["kernels"].items()}))
     print("step_hbm_bytes", res["step_hbm_bytes"])

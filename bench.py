@@ -156,10 +156,13 @@ CONFIGS = {
            "generator": "genomeanonymizer_amd.synth.batch.config2_batch", "seed": 3,
            "workload": "SURVEY C3 density: {reads} 150 bp reads (~60x tumor+normal) on {genome} bp, "
                        "1 germline het SNP per kb, a window every 10 kb, resident in HBM"},
+    # (longread_batch places its own sites: a germline het SNP per kb and a window every 10 kb of
+    # `genome`; --windows / --germline do not apply)
     "c5": {"defaults": {"reads": 20_000, "genome": 200_000_000, "windows": 0, "germline": 0},
            "generator": "genomeanonymizer_amd.synth.batch.longread_batch", "seed": 7,
-           "workload": "SURVEY C5: {reads} ONT-like reads 10-100 kb (5 % indels, soft clips) on {genome} bp, "
-                       "germline het SNP per kb, a window every 10 kb (scopes to ~200 kb), resident in HBM"},
+           "workload": "SURVEY C5 shape: {reads} ONT-like reads 10-100 kb (5 % indels, soft clips) on {genome} bp "
+                       "with {c5_germline} germline het SNPs (1 per kb; configs[4] names 1 M on 3 Gb) and "
+                       "{c5_windows} windows (1 per 10 kb, scopes to ~200 kb), resident in HBM"},
 }
 
 
@@ -315,36 +318,83 @@ def e2e_lines(args) -> dict:
         make_pair(inp, n_contigs=args.e2e_contigs, pairs_per_contig=args.e2e_pairs)
         gen_s = time.perf_counter() - t
         tool = os.path.join(REPO, "tools", "e2e_bench.py")
-        hip = _child_json([sys.executable, tool, inp, os.path.join(d, "out"), "stream,whole"],
+        # one process: the streamed and the whole-sample paths (their files must be equal)
+        one = _child_json([sys.executable, tool, inp, os.path.join(d, "out"), "stream,whole"],
                           {"E2E_RUNS": str(args.e2e_runs)}, 900)
+        # the product's host work over P processes sharing the GPU (the multi-rank path, gloo)
+        hip = one
+        if args.e2e_workers > 1:
+            hip = _child_json([sys.executable, tool, inp, os.path.join(d, "out_w"), "stream"],
+                              {"E2E_RUNS": str(args.e2e_runs), "E2E_WORKERS": str(args.e2e_workers)}, 900)
         st = hip.get("stream", {})
+        same = None
+        if args.e2e_workers > 1 and "error" not in hip and "error" not in one:
+            same = all(open(os.path.join(d, "out_w", f"{x}_stream{sfx}"), "rb").read() ==
+                       open(os.path.join(d, "out", f"{x}_whole{sfx}"), "rb").read()
+                       for x in ("tumor", "normal") for sfx in (".1.fastq", ".2.fastq"))
+        elif args.e2e_workers <= 1:
+            same = one.get("stream_equals_whole")
+        o1 = one.get("stream", {})
         res["e2e"] = {
             "value": st.get("reads_per_s"), "unit": "reads/s", "bases_per_sec": st.get("bases_per_s"),
-            "reads": st.get("reads"), "wall_s": st.get("stages_s", {}).get("wall_s"),
-            "wall_s_runs": st.get("wall_s_runs"), "stages_s": st.get("stages_s"),
-            "peak_rss_mb": st.get("peak_rss_mb"), "output_bytes": st.get("output_bytes"),
-            "whole_sample": {k: hip.get("whole", {}).get(k) for k in ("reads_per_s", "stages_s", "peak_rss_mb")},
-            "files_equal_whole_sample": hip.get("stream_equals_whole"),
+            "reads": st.get("reads"), "workers": args.e2e_workers, "wall_s": st.get("stages_s", {}).get("wall_s"),
+            "wall_s_runs": st.get("wall_s_runs"), "stages_s_rank0": st.get("stages_s"),
+            "peak_rss_mb_rank0": st.get("peak_rss_mb"), "output_bytes": st.get("output_bytes"),
+            "one_process": {"reads_per_s": o1.get("reads_per_s"), "stages_s": o1.get("stages_s"),
+                            "peak_rss_mb": o1.get("peak_rss_mb")},
+            "whole_sample": {k: one.get("whole", {}).get(k) for k in ("reads_per_s", "stages_s", "peak_rss_mb")},
+            "files_equal_whole_sample": same,
             "workload": f"synth/fastpair.py: {args.e2e_contigs} contigs x 2 Mb, {args.e2e_pairs} pairs per contig "
                         f"and sample (150 bp, FR), 1 germline het SNP/kb + 0.1 het deletion/kb in tumor and normal, "
-                        f"a somatic window SNV every 20 kb; streamed product, files written to local disk",
-            "generate_s": round(gen_s, 1), "error": hip.get("error")}
+                        f"a somatic window SNV every 20 kb; streamed product in {args.e2e_workers} processes sharing "
+                        f"the GPU (contigs sharded as over ranks, 16 / {args.e2e_workers} decode threads each), "
+                        f"files written to local disk",
+            "generate_s": round(gen_s, 1), "error": hip.get("error") or one.get("error")}
         # the CPU path on a bounded sample (the first contigs)
         cpu_in = os.path.join(d, "cpu_in")
         make_pair(cpu_in, n_contigs=args.e2e_cpu_contigs, pairs_per_contig=args.e2e_pairs, seed=8)
         cores = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
+        wk = max(1, args.e2e_workers)
         cpu = _child_json([sys.executable, tool, cpu_in, os.path.join(d, "cpu_out"), "stream"],
-                          {"E2E_ENGINE": "oracle", "E2E_THREADS": str(cores), "E2E_RUNS": "1"}, 900)
+                          {"E2E_ENGINE": "oracle", "E2E_THREADS": str(max(1, cores // wk)), "E2E_RUNS": "1",
+                           "E2E_WORKERS": str(wk)}, 900)
         cs = cpu.get("stream", {})
         res["cpu_e2e"] = {"value": cs.get("reads_per_s"), "unit": "reads/s", "bases_per_sec": cs.get("bases_per_s"),
-                          "reads": cs.get("reads"), "cores": cores, "kind": "port",
+                          "reads": cs.get("reads"), "cores": cores, "kind": "port", "workers": wk,
                           "stages_s": cs.get("stages_s"), "error": cpu.get("error"),
-                          "sample": f"the same pipeline with the C oracle masking on {cores} host threads, the "
+                          "sample": f"the same pipeline ({wk} processes) with the C oracle masking on {cores} host "
+                                    f"threads in all, the "
                                     f"indel restatement (Python) and the host C++ formatter, "
                                     f"{args.e2e_cpu_contigs} contigs of the same shape"}
     finally:
         shutil.rmtree(d, ignore_errors=True)
     return res
+
+
+# the SURVEY §8(d) shapes timed beside the metric's line (child processes, before this process
+# initialises the GPU): C3 density at a quarter of its size, C5 long reads at half of the reads
+SIDE_CONFIGS = {
+    "c3": ["--reads", "10000000", "--genome", "25000000", "--windows", "2500", "--germline", "25000",
+           "--steps", "10", "--warmup", "3"],
+    "c5": ["--reads", "10000", "--genome", "100000000", "--steps", "5", "--warmup", "2"],
+}
+
+
+def side_config_lines(args) -> dict:
+    """The c3 and c5 lines, each a child bench.py run (the same fresh-batch step and roofline), reduced
+    to the fields a reader compares."""
+    out = {}
+    for name, extra in SIDE_CONFIGS.items():
+        r = _child_json([sys.executable, os.path.abspath(__file__), "--config", name, "--no-e2e", "--no-pcie",
+                         "--no-fastq", "--no-cpu-baseline", "--no-side-configs"] + extra, {}, 600)
+        if "error" in r:
+            out[name] = {"error": r["error"]}
+            continue
+        out[name] = {k: r.get(k) for k in ("value", "unit", "bases_per_sec", "ms_per_step", "run_only_ms_per_step",
+                                           "roofline", "batch_shape", "indel", "child_wall_s")}
+        out[name]["workload"] = r.get("config", {}).get("workload")
+        out[name]["kernels_ms"] = {k: v.get("avg_ms") for k, v in r.get("pass", {}).get("kernels", {}).items()}
+    return out
 
 
 def main() -> None:
@@ -369,10 +419,13 @@ def main() -> None:
     ap.add_argument("--prep-unroll", type=int, default=0, help="GANON_PARAM_PREP_UNROLL: incidences per thread "
                     "and trip of the one-segment emit (0 auto, 1, 2, 4)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (BAM -> FASTQ) line")
+    ap.add_argument("--no-side-configs", action="store_true", help="skip the c3 / c5 lines (child runs)")
     ap.add_argument("--e2e-contigs", type=int, default=24)
     ap.add_argument("--e2e-pairs", type=int, default=23_000, help="pairs per contig and sample")
-    ap.add_argument("--e2e-cpu-contigs", type=int, default=2)
+    ap.add_argument("--e2e-cpu-contigs", type=int, default=4)
     ap.add_argument("--e2e-runs", type=int, default=2, help="timed end-to-end runs after a warm run")
+    ap.add_argument("--e2e-workers", type=int, default=8,
+                    help="processes sharing the GPU in the end-to-end line (the multi-rank path over gloo)")
     ap.add_argument("--resident", action="store_true",
                     help="round-2 step: run only, the plan made once at upload (not a fresh batch)")
     ap.add_argument("--pmc", default=None,
@@ -387,6 +440,7 @@ def main() -> None:
     world = int(os.environ.get("WORLD_SIZE", 1))
     # end to end first: child processes, before this process initialises the GPU (N = 1 only)
     e2e = e2e_lines(args) if world == 1 and not args.no_e2e else {}
+    side = side_config_lines(args) if world == 1 and args.config == "c2" and not args.no_side_configs else None
     import torch
     local = int(os.environ.get("LOCAL_RANK", 0))
     dev = local % max(1, torch.cuda.device_count())   # == local on a node with a GPU per rank
@@ -559,7 +613,8 @@ def main() -> None:
         "vs_baseline": None,
         "dtype": "u8",
         "data": f"synthetic ({cfg['generator']}, seed {cfg['seed']}+rank)",
-        "config": {"workload": cfg["workload"].format(**vars(args)), "name": args.config,
+        "config": {"workload": cfg["workload"].format(**vars(args), c5_germline=args.genome // 1000,
+                                                     c5_windows=args.genome // 10_000), "name": args.config,
                    "reads_per_gpu": info["reads"], "mean_read_len": round(mean_len, 1),
                    "scopes_per_gpu": info["scopes"], "incidences_per_gpu": info.get("incidences"),
                    "window_scopes": info.get("window_scopes"), "union_scopes": info.get("union_scopes"),
@@ -588,6 +643,7 @@ def main() -> None:
                   "support_records": int((irecs["kind"] == native.INDEL_SUPPORT).sum()),
                   "ms_per_step": round(indel_ms, 4)},
         "e2e": e2e.get("e2e"),
+        "side_configs": side,
         "pcie_inclusive": pcie,
         "fastq": fastq,
         "totals": {k: int(v) for k, v in zip(native.TOTAL_NAMES, job_totals)},

@@ -17,7 +17,7 @@ from __future__ import annotations
 
 import dataclasses
 import threading
-from typing import Dict, Optional, Tuple
+from typing import Callable, Dict, Optional, Tuple
 
 import numpy as np
 
@@ -31,7 +31,7 @@ from .variants import VariantType, kept_snv
 
 @dataclasses.dataclass
 class MaskResult:
-    seq_out: np.ndarray                    # masked copy of the batch's seq blob
+    _seq: Optional[np.ndarray]             # masked copy of the batch's seq blob (None: not fetched yet)
     seq_base: Tuple[int, int]              # byte offset of the tumor / normal blob in seq_out
     batch_index: Dict[Tuple[int, int], int]
     scope_snv_calls: np.ndarray            # [n_scopes] masked TN SNV calls
@@ -42,6 +42,17 @@ class MaskResult:
     arrays: dict                           # the device batch (kept for tests/bench)
     dup_off: Dict[Tuple[int, int, int], int] = dataclasses.field(default_factory=dict)
     device_gen: int = -1                   # the engine's job batch holding this result (format_fastq_batch)
+    seq_fetch: Optional[Callable[[], np.ndarray]] = None   # downloads _seq while that batch holds it
+
+    @property
+    def seq_out(self) -> np.ndarray:
+        """The masked bases; fetched from the device on first use when the mask left them there."""
+        if self._seq is None:
+            if self.seq_fetch is None:
+                raise RuntimeError("masked bases were not kept")
+            self._seq = self.seq_fetch()
+            self.seq_fetch = None
+        return self._seq
 
     def masked_nib(self, tables, ds: int, row: int, scope: int) -> int:
         """Nibble offset in seq_out of read (ds, row) as masked by ``scope``."""
@@ -267,23 +278,36 @@ class CompleteGermlineAnonymizer:
         with self.lock:
             return fmt(recs, gen)
 
-    def anonymize(self, planner: SamplePlanner, plan: Plan, scope_ids=None, written=None, batch=None) -> MaskResult:
+    def anonymize(self, planner: SamplePlanner, plan: Plan, scope_ids=None, written=None, batch=None,
+                  lazy_seq: bool = False) -> MaskResult:
         """Mask all scopes of ``plan`` (or the contig shard ``scope_ids``) in one device batch
         (``batch``: build_batch's result when the caller built it already). Per-scope counts come
-        back indexed by plan scope id (zero outside the shard)."""
+        back indexed by plan scope id (zero outside the shard). ``lazy_seq``: leave the masked bases
+        on the device (MaskResult.seq_out downloads them on first use, valid until the engine's next
+        job; the streamed path formats from the device and rarely needs them)."""
         tables = planner.tables
         fasta = planner.fasta
         arrays, meta = batch if batch is not None else build_batch(plan, tables, fasta, scope_ids, written)
+        fetch = None
         with self.lock:
-            out, b_calls, b_bases, totals, irecs = self.engine.mask(arrays, indels=True)
-            gen = getattr(self.engine, "job_gen", -1)
+            if lazy_seq and hasattr(self.engine, "job_seq"):
+                out, b_calls, b_bases, totals, irecs = self.engine.mask(arrays, indels=True, fetch_seq=False)
+                gen = self.engine.job_gen
+                eng, lock = self.engine, self.lock
+
+                def fetch():
+                    with lock:
+                        return eng.job_seq(gen)
+            else:
+                out, b_calls, b_bases, totals, irecs = self.engine.mask(arrays, indels=True)
+                gen = getattr(self.engine, "job_gen", -1)
         calls = np.zeros(len(plan.scopes), np.int32)
         bases = np.zeros(len(plan.scopes), np.int32)
         calls[meta["scope_ids"]] = b_calls
         bases[meta["scope_ids"]] = b_bases
         indel_counts, leftovers = indel_results(irecs, meta, plan, tables, fasta)
         return MaskResult(out, meta["seq_base"], {}, calls, bases, indel_counts, leftovers, totals, arrays,
-                          meta["dup_off"], gen)
+                          meta["dup_off"], gen, fetch)
 
 
 ANONYMIZER_ALGORITHMS = {CompleteGermlineAnonymizer.name: CompleteGermlineAnonymizer}

@@ -8,7 +8,9 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <memory>
 #include <thread>
+#include <utility>
 #include <vector>
 
 #include "../../include/ganon_host.h"
@@ -21,6 +23,30 @@ thread_local std::string g_err;
 inline void copy_bytes(void *dst, const void *src, size_t n) {
   if (n) std::memcpy(dst, src, n);
 }
+
+// A vector whose resize / sized construction leaves new elements uninitialised: the decoder's
+// buffers are written in full before they are read (zero-filling them was one more serial pass over
+// every inflated byte).
+template <class T>
+struct NoInit : std::allocator<T> {
+  template <class U>
+  struct rebind {
+    using other = NoInit<U>;
+  };
+  NoInit() = default;
+  template <class U>
+  NoInit(const NoInit<U> &) noexcept {}
+  template <class U>
+  void construct(U *p) noexcept {
+    ::new (static_cast<void *>(p)) U;
+  }
+  template <class U, class... A>
+  void construct(U *p, A &&...a) {
+    ::new (static_cast<void *>(p)) U(std::forward<A>(a)...);
+  }
+};
+template <class T>
+using RawVec = std::vector<T, NoInit<T>>;
 
 struct Block {
   int64_t in_off;   // compressed payload offset in the file buffer
@@ -49,11 +75,11 @@ struct ganon_bam {
   std::string err;
   std::vector<char> ref_names;
   std::vector<int64_t> ref_name_off, ref_len;
-  std::vector<int32_t> tid, pos, end, flag, mapq, l_seq, n_cigar, mate_tid, mate_pos, tlen, name_len, aux_len;
-  std::vector<int64_t> name_off, cig_off, seq_off, qual_off, aux_off;
-  std::vector<char> names;
-  std::vector<uint32_t> cigar;
-  std::vector<uint8_t> seq, qual, aux;
+  RawVec<int32_t> tid, pos, end, flag, mapq, l_seq, n_cigar, mate_tid, mate_pos, tlen, name_len, aux_len;
+  RawVec<int64_t> name_off, cig_off, seq_off, qual_off, aux_off;
+  RawVec<char> names;
+  RawVec<uint32_t> cigar;
+  RawVec<uint8_t> seq, qual, aux;
 };
 
 static int set_err(const std::string &m) {
@@ -282,7 +308,7 @@ static int bam_open_impl(const char *path, int threads, ganon_bam **out) {
   std::fseek(fh, 0, SEEK_END);
   const long fsize = std::ftell(fh);
   std::fseek(fh, 0, SEEK_SET);
-  std::vector<uint8_t> file((size_t)std::max(0L, fsize));
+  RawVec<uint8_t> file((size_t)std::max(0L, fsize));
   if (fsize > 0 && std::fread(file.data(), 1, (size_t)fsize, fh) != (size_t)fsize) {
     std::fclose(fh);
     return set_err("short read");
@@ -301,7 +327,7 @@ static int bam_open_impl(const char *path, int threads, ganon_bam **out) {
     total += isize;
     off += blen;
   }
-  std::vector<uint8_t> data((size_t)total);
+  RawVec<uint8_t> data((size_t)total);
   if (!inflate_blocks(file.data(), blocks, 0, blocks.size(), data.data(), threads))
     return set_err("BGZF inflate failed");
   file.clear();
@@ -405,10 +431,10 @@ inline int64_t tid_order(int32_t t) { return t < 0 ? (int64_t)INT32_MAX : (int64
 // Reads and inflates complete BGZF blocks starting at file offset coff (at most R->chunk compressed
 // bytes). Appends the inflated bytes to data and one (data offset, file offset) pair per non-empty
 // block to bmap. Returns the file offset after the last complete block, or -1 on error.
-int64_t read_blocks(ganon_bam_reader *R, int64_t coff, int64_t step, std::vector<uint8_t> &data,
+int64_t read_blocks(ganon_bam_reader *R, int64_t coff, int64_t step, RawVec<uint8_t> &data,
                     std::vector<std::pair<int64_t, int64_t>> &bmap) {
   const int64_t want = std::min<int64_t>(std::max<int64_t>(step, 1 << 17), R->fsize - coff);
-  std::vector<uint8_t> comp((size_t)want);
+  RawVec<uint8_t> comp((size_t)want);
   if (std::fseek(R->fh, (long)coff, SEEK_SET) != 0 || std::fread(comp.data(), 1, (size_t)want, R->fh) != (size_t)want)
     return set_err("short read");
   std::vector<Block> blocks;
@@ -448,11 +474,11 @@ int64_t voff_at(const std::vector<std::pair<int64_t, int64_t>> &bmap, int64_t x)
 // record met (kTidEnd when none) so that an index start can be validated. hint: expected compressed
 // bytes of the sequence (index span) or 0; the step read and inflated at a time starts there (or at
 // 1 MiB) and doubles up to the reader's window, so a small sequence never inflates a whole window.
-int scan_tid(ganon_bam_reader *R, int64_t voff, int32_t tid, int64_t hint, std::vector<uint8_t> &kept,
+int scan_tid(ganon_bam_reader *R, int64_t voff, int32_t tid, int64_t hint, RawVec<uint8_t> &kept,
              int64_t &next_voff, int32_t &next_tid, int32_t &first_tid) {
   int64_t step = std::min<int64_t>(hint > 0 ? hint + (1 << 16) : (1 << 20), R->chunk);
   int64_t coff = voff >> 16;
-  std::vector<uint8_t> data;
+  RawVec<uint8_t> data;
   std::vector<std::pair<int64_t, int64_t>> bmap;
   int64_t dpos = (int64_t)(voff & 0xFFFF);
   bool seen = false;
@@ -477,6 +503,11 @@ int scan_tid(ganon_bam_reader *R, int64_t voff, int32_t tid, int64_t hint, std::
     coff = read_blocks(R, coff, step, data, bmap);
     if (coff < 0) return -1;
     step = std::min<int64_t>(2 * step, R->chunk);
+    int64_t run0 = -1;   // first byte of the current run of `tid` records (copied to kept at once)
+    auto flush = [&]() {
+      if (run0 >= 0) kept.insert(kept.end(), data.begin() + run0, data.begin() + dpos);
+      run0 = -1;
+    };
     for (;;) {
       if (dpos + 4 > (int64_t)data.size()) break;
       int32_t bs, rtid;
@@ -486,15 +517,17 @@ int scan_tid(ganon_bam_reader *R, int64_t voff, int32_t tid, int64_t hint, std::
       std::memcpy(&rtid, &data[(size_t)dpos + 4], 4);
       if (first_tid == kTidEnd) first_tid = rtid;
       if (rtid == tid) {
-        kept.insert(kept.end(), data.begin() + dpos, data.begin() + dpos + 4 + bs);
+        if (run0 < 0) run0 = dpos;
         seen = true;
       } else if (seen || tid_order(rtid) > tid_order(tid)) {
+        flush();
         next_voff = voff_at(bmap, dpos);
         next_tid = rtid;
         return 0;
       }
       dpos += 4 + bs;
     }
+    flush();
   }
 }
 
@@ -571,7 +604,7 @@ int reader_open_impl(const char *path, int threads, ganon_bam_reader **out) {
   std::fseek(R->fh, 0, SEEK_END);
   R->fsize = (int64_t)std::ftell(R->fh);
   // header: inflate block windows until it is complete
-  std::vector<uint8_t> data;
+  RawVec<uint8_t> data;
   std::vector<std::pair<int64_t, int64_t>> bmap;
   int64_t coff = 0, p = 0;
   for (;;) {
@@ -629,7 +662,7 @@ GANON_HOST_API int ganon_bam_reader_contig(ganon_bam_reader *R, int32_t tid, gan
   *out = nullptr;
   if (tid < 0 || tid >= (int32_t)R->header.ref_len.size()) return set_err("tid out of range");
   try {
-    std::vector<uint8_t> kept;
+    RawVec<uint8_t> kept;
     int64_t next_voff = -1;
     int32_t next_tid = kTidEnd, first_tid = kTidEnd;
     bool done = false;

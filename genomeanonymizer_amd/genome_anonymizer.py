@@ -9,7 +9,9 @@ Outputs next to the inputs: re.sub('.bam|.sam|.cram', '.anonymized', path) + .1/
 
 Multi-GPU: launch under ``torchrun --nproc-per-node N`` (or set WORLD_SIZE/RANK/LOCAL_RANK):
 contigs are sharded round-robin over the ranks; each rank decodes, masks and writes its own
-contigs at their offsets of the shared output files (distributed.py, stream.py).
+contigs at their offsets of the shared output files (distributed.py, stream.py). More ranks than
+GPUs (e.g. 4 per GPU) spread the host work (decode, planning, output) over more processes: rank r
+uses GPU LOCAL_RANK % GPUs and the ranks talk over gloo instead of RCCL.
 """
 from __future__ import annotations
 
@@ -81,14 +83,21 @@ def run_anonymizer(argv=None) -> None:
     vcfs, samples, outputs = read_samples(join_dir_file(config.directory, config.samples), config.directory)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    device = config.device if config.device is not None else local
-    anonymizer = CompleteGermlineAnonymizer(device=device)
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    n_dev = 1
     if world > 1:
         import torch
+        n_dev = max(1, torch.cuda.device_count())   # (counting devices does not initialise the GPU)
+    device = config.device if config.device is not None else local % n_dev
+    anonymizer = CompleteGermlineAnonymizer(device=device)
+    if world > 1:
         import torch.distributed as dist
         from .distributed import run_pairs_sharded
-        torch.cuda.set_device(device)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        if local_world > n_dev:   # ranks share a GPU: RCCL takes one rank per device
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(device)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
         # one pair per GPU when there are enough pairs, else each pair's contigs over all GPUs
         tots = run_pairs_sharded(vcfs, samples, config.reference, anonymizer, outputs, bool(config.record_statistics),
                                  dist, threads=max(1, config.cpu))

@@ -299,9 +299,10 @@ class HipMasker:
     def set_profiling(self, on: bool) -> None:
         self._check(self._lib.ganon_ctx_set_profiling(self._h, 1 if on else 0), "set_profiling")
 
-    def mask(self, arrays: dict, indels: bool = False):
+    def mask(self, arrays: dict, indels: bool = False, fetch_seq: bool = True):
         """Synchronous one-shot: returns (seq_out, scope_calls, scope_bases, totals), plus the
-        germline indel records (``INDEL_REC``, sorted) when ``indels``."""
+        germline indel records (``INDEL_REC``, sorted) when ``indels``. ``fetch_seq`` False (job
+        path): seq_out is None, the masked bases stay in the job batch (``job_seq``)."""
         if indels:
             # one device batch per context, reloaded job after job (grow-only buffers: no allocation
             # once the largest job has been seen); it stays valid — for formatting from the device
@@ -323,7 +324,7 @@ class HipMasker:
                 db.run()
                 if t is not None:
                     t.run()
-                res = db.download()
+                res = db.download(with_seq=fetch_seq)
                 recs = t.download() if t is not None else np.zeros(0, INDEL_REC)
             finally:
                 if t is not None:
@@ -337,6 +338,15 @@ class HipMasker:
         self._check(self._lib.ganon_mask_batch(self._h, C.byref(b), _ptr(out, _u8p), _ptr(calls, _i32p),
                                                _ptr(bases, _i32p), _ptr(tot, _i64p)), "ganon_mask_batch")
         return out, calls, bases, tot
+
+    def job_seq(self, gen: int) -> np.ndarray:
+        """The masked bases of job ``gen`` from the job batch (it holds only the last job's)."""
+        db = self._job_db
+        if db is None or gen != self.job_gen:
+            raise GanonError(f"the masked bases of job {gen} are no longer on the device (job {self.job_gen} is)")
+        out = np.empty(db.seq_bytes, np.uint8)
+        db.download_seq(out)
+        return out
 
     # -- device-resident path ------------------------------------------------------------
     def upload(self, arrays: dict, ref: "DeviceRef" = None) -> "DeviceBatch":
@@ -612,13 +622,15 @@ class DeviceBatch:
     def sync(self) -> None:
         self.m._check(self.m._lib.ganon_batch_sync(self.m._h), "ganon_batch_sync")
 
-    def download(self):
-        out = np.empty(self.seq_bytes, np.uint8)
+    def download(self, with_seq: bool = True):
+        """(masked bases or None, per-scope calls, per-scope bases, totals)."""
+        out = np.empty(self.seq_bytes, np.uint8) if with_seq else None
         calls = np.zeros(self.n_scopes, np.int32)
         bases = np.zeros(self.n_scopes, np.int32)
         tot = np.zeros(GANON_N_TOTALS, np.int64)
-        self.m._check(self.m._lib.ganon_batch_download(self.m._h, self.h, _ptr(out, _u8p), _ptr(calls, _i32p),
-                                                       _ptr(bases, _i32p), _ptr(tot, _i64p)), "download")
+        self.m._check(self.m._lib.ganon_batch_download(self.m._h, self.h, _ptr(out, _u8p) if with_seq else None,
+                                                       _ptr(calls, _i32p), _ptr(bases, _i32p), _ptr(tot, _i64p)),
+                      "download")
         return out, calls, bases, tot
 
     def download_seq(self, out: np.ndarray) -> None:

@@ -168,13 +168,18 @@ class Job(JobPrep):
             t_dec, t_pl, t_b = time.time() - t0, 0.0, 0.0
             hidden = sum(self.prep_timing)
         t2 = time.time()
-        self.res: MaskResult = anonymizer.anonymize(self.planner, self.plan, written=self.written, batch=self.batch)
+        self.res: MaskResult = anonymizer.anonymize(self.planner, self.plan, written=self.written, batch=self.batch,
+                                                    lazy_seq=True)
         self.batch = None
         t3 = time.time()
         self.fmt = FastqFormatter(self.tables, self.res, anonymizer.format_fastq,
                                   getattr(anonymizer, "format_fastq_batch", None))
-        # every read once, as its masked copy (or unmasked): the records this job can write
-        self.fmt.preformat(*self._format_instances())
+        # every read once, as its masked copy (or unmasked): the records this job can write. The
+        # masked bases stay on the device unless a later stage needs them on the host (records left
+        # to on-demand formatting, complex names' objects): fetched now, while the engine's job
+        # batch still holds them
+        if not self.fmt.preformat(*self._format_instances()) or len(self.objs):
+            _ = self.res.seq_out
         t4 = time.time()
         self.cx = self._complex_ingredients()
         self.timing = {"decode_s": t_dec, "plan_s": t_pl, "mask_s": t3 - t2 + t_b, "format_s": t4 - t3,

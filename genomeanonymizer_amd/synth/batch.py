@@ -652,12 +652,13 @@ def config2_batch(n_reads: int = 10_000_000, genome: int = 3_000_000_000, n_cont
     gstart = cstart[rc] + rpos
     n = len(rpos)
     # bases: reference + germline het alts on haplotype 1 + 0.1 % errors
-    codes = np.empty((n, L), np.uint8)
-    step = 1_000_000
-    offs = np.arange(L, dtype=np.int64)
-    for a in range(0, n, step):
-        b = min(n, a + step)
-        codes[a:b] = ref_codes(gstart[a:b, None] + offs[None, :])
+    # (the genome one code per byte, each read's codes one row of a sliding-window view: a row copy
+    # per read instead of a per-base gather)
+    nib = np.empty(2 * len(ref), np.uint8)
+    nib[0::2] = ref >> 4
+    nib[1::2] = ref & 0xF
+    codes = np.lib.stride_tricks.sliding_window_view(nib, L)[gstart]
+    del nib
     lo = np.searchsorted(gsnp, gstart)
     hi = np.searchsorted(gsnp, gstart + L)
     cnt = hi - lo

@@ -39,8 +39,6 @@ class FastqFormatter:
         self.res = res
         self.backend = backend or native.host_format_fastq
         self.device_backend = device_backend
-        # buffers: 0 = device output, 1 = tumor BAM seq, 2 = normal BAM seq
-        self._seq_bufs = [res.seq_out, tables[0].seq, tables[1].seq]
         self._qual_bufs = [tables[0].qual, tables[1].qual]
         self._names = tables[0].names_blob.tobytes() + tables[1].names_blob.tobytes()
         self._name_base = (0, len(tables[0].names_blob))
@@ -49,12 +47,19 @@ class FastqFormatter:
         self._pre = None     # (sorted instance keys, offsets, lengths, bytes) of preformat()
         self._left_keys = None   # sorted keys of the instances with left-over edits
 
+    @property
+    def _seq_bufs(self) -> list:
+        """Sequence buffers: 0 = the masked output (fetched from the device on first use), 1 / 2 =
+        the tumor / normal BAM bases."""
+        return [self.res.seq_out, self.tables[0].seq, self.tables[1].seq]
+
     @staticmethod
     def _key(ds, row, sc):
         return ((np.asarray(sc, np.int64) + 1) << 33) | (np.asarray(ds, np.int64) << 32) | np.asarray(row, np.int64)
 
-    def records_arrays(self, ds: np.ndarray, row: np.ndarray, sc: np.ndarray) -> dict:
-        """The record arrays of instances ``(dataset, row, write scope | -1)``."""
+    def records_arrays(self, ds: np.ndarray, row: np.ndarray, sc: np.ndarray, seq_bufs: bool = True) -> dict:
+        """The record arrays of instances ``(dataset, row, write scope | -1)`` (``seq_bufs`` False:
+        without the host sequence buffers, for the device formatter that reads them in place)."""
         n = len(ds)
         T, N = self.tables
         ds = np.asarray(ds, np.int64)
@@ -71,7 +76,7 @@ class FastqFormatter:
         flag = pick("flag", np.int64)
         name_off = pick("name_off", np.int64) + np.where(t0, self._name_base[0], self._name_base[1])
         return {
-            "seq_bufs": self._seq_bufs, "seq_sel": seq_sel, "seq_nib_off": (2 * byte_off).astype(np.int64),
+            "seq_bufs": self._seq_bufs if seq_bufs else None, "seq_sel": seq_sel, "seq_nib_off": (2 * byte_off).astype(np.int64),
             "seq_len": seq_len, "reverse": pick("is_reverse", np.uint8),
             "qual_bufs": self._qual_bufs, "qual_sel": ds.astype(np.uint8), "qual_off": pick("qual_off", np.int64),
             "qual_len": seq_len.copy(), "qual_rev": np.zeros(n, np.uint8),   # stored order for every read (Q1)
@@ -115,22 +120,24 @@ class FastqFormatter:
             raise TypeError(f"reverse read {self.tables[d].name(r)!r} has a base outside ACGTN: the "
                             "reference's reverse complement fails on it (SURVEY Q7)") from None
 
-    def preformat(self, ds, row, sc) -> None:
+    def preformat(self, ds, row, sc) -> bool:
         """Format the instances a job can write in ONE formatter call (the device round trip costs
         more than the bytes); later record runs are sliced out of it. A reverse read with a base
         outside ACGTN is left out (its error is raised only if it is written, as in the
-        reference); after a few such reads the job formats on demand."""
+        reference); after a few such reads the job formats on demand. True when every instance was
+        formatted (no later record run needs the masked bases on the host)."""
         ds, row, sc = (np.asarray(x, np.int64) for x in (ds, row, sc))
         key = self._key(ds, row, sc)
         key, first = np.unique(key, return_index=True)
         ds, row, sc = ds[first], row[first], sc[first]
+        n_all = len(ds)
         for _ in range(4):
             if len(ds) == 0:
-                return
+                return n_all == 0
             try:
                 data = None
                 if self.device_backend is not None:   # the bases in place on the device
-                    recs = self.records_arrays(ds, row, sc)
+                    recs = self.records_arrays(ds, row, sc, seq_bufs=False)
                     recs["seq_base1"] = len(self.tables[0].seq)
                     data = self.device_backend(recs, self.res.device_gen)
                 if data is None:
@@ -142,7 +149,8 @@ class FastqFormatter:
                 continue
             ln = self._plain_lengths(ds, row)
             self._pre = (key, np.concatenate([[0], np.cumsum(ln)[:-1]]).astype(np.int64), ln, data)
-            return
+            return len(ds) == n_all
+        return False
 
     def edited_bytes(self, inst, reapply: int = 0) -> bytes:
         """Record of an instance with left-over edits, applied once or (reapply) twice (cached)."""

@@ -11,6 +11,9 @@ Prints one JSON line with per-stage seconds, reads/s, bases/s and the process's 
     E2E_RUNS=N ...           # timed runs per mode after one untimed warm run (default 1)
     E2E_PROFILE=PREFIX ...   # cProfile of the timed run of each mode -> PREFIX_<mode>.txt (main thread)
     GANON_PREFETCH=N ...     # look-ahead planning threads of the streamed path (0: in line)
+    E2E_WORKERS=P ...        # the streamed path in P processes sharing the GPU (torch.distributed.run,
+                             # gloo; the contigs sharded over them as over the ranks of a multi-GPU run,
+                             # host decode threads 16 / P each); wall = the slowest rank's
 """
 import json
 import os
@@ -37,12 +40,36 @@ def _engine():
         eng = CpuEngine()
         eng.threads = int(os.environ.get("E2E_THREADS", "16"))
         return CompleteGermlineAnonymizer(engine=eng)
-    anon = CompleteGermlineAnonymizer(device=0)
+    anon = CompleteGermlineAnonymizer(device=int(os.environ.get("GANON_DEVICE", "0")))
     anon.engine   # context creation outside the timed stages
     return anon
 
 
+def _relaunch(workers: int) -> None:
+    """This script again under torch.distributed.run with ``workers`` ranks (a child process: this
+    one has not touched the GPU); exits with its code."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={workers}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    sys.exit(subprocess.call(cmd))
+
+
 def main():
+    workers = int(os.environ.get("E2E_WORKERS", "1"))
+    if workers > 1 and "RANK" not in os.environ:
+        _relaunch(workers)
+    dist = None
+    rank = 0
+    if workers > 1:
+        import torch
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+        rank = dist.get_rank()
+        os.environ.setdefault("GANON_DEVICE", str(int(os.environ.get("LOCAL_RANK", 0)) % max(1, torch.cuda.device_count())))
     d = sys.argv[1]
     out = sys.argv[2] if len(sys.argv) > 2 else os.path.join(REPO, "gpurun_out", "e2e")
     os.makedirs(out, exist_ok=True)
@@ -57,6 +84,9 @@ def main():
     anon = _engine()
     res = {"windows_s": round(t_win, 3), "engine": os.environ.get("E2E_ENGINE", "hip")}
     modes = sys.argv[3].split(",") if len(sys.argv) > 3 else ["stream", "whole"]
+    if dist is not None and modes != ["stream"]:
+        sys.exit("E2E_WORKERS > 1 runs the streamed path only")
+    threads = max(1, 16 // workers)
     n_timed = int(os.environ.get("E2E_RUNS", "1"))
     for mode in modes:
         runs = []
@@ -66,16 +96,35 @@ def main():
                 import cProfile
                 prof = cProfile.Profile()
                 prof.enable()
+            # a run writes new files: the previous run's outputs go first (truncating 0.7 GB of
+            # files inside the timed region cost ~75 ms)
+            if rank == 0:
+                for x in ("tumor", "normal"):
+                    for sfx in (".1.fastq", ".2.fastq", ".single_end.fastq"):
+                        try:
+                            os.unlink(os.path.join(out, f"{x}_{mode}{sfx}"))
+                        except FileNotFoundError:
+                            pass
+            if dist is not None:
+                dist.barrier()
             t1 = time.time()
             tim = sr.anonymize_genome(windows, os.path.join(d, "tumor.bam"), os.path.join(d, "normal.bam"),
                                       os.path.join(d, "ref.fa"), anon, os.path.join(out, f"tumor_{mode}"),
-                                      os.path.join(out, f"normal_{mode}"), True, 16, fasta=fasta,
-                                      streaming=(mode == "stream"))
+                                      os.path.join(out, f"normal_{mode}"), True, threads, fasta=fasta,
+                                      streaming=(mode == "stream"), dist=dist)
             tim["wall_s"] = time.time() - t1
+            if dist is not None:   # the slowest rank's wall; reads and bases of all ranks
+                import torch
+                w = torch.tensor([tim["wall_s"]], dtype=torch.float64)
+                dist.all_reduce(w, op=dist.ReduceOp.MAX)
+                rb = torch.tensor([tim["reads"], tim.get("bases", 0)], dtype=torch.int64)
+                dist.all_reduce(rb)
+                tim["wall_s"], tim["reads"], tim["bases"] = float(w[0]), int(rb[0]), int(rb[1])
             if prof is not None:
                 import pstats
                 prof.disable()
-                with open(f"{os.environ['E2E_PROFILE']}_{mode}.txt", "w") as f:
+                sfx = f"_r{rank}" if dist is not None else ""
+                with open(f"{os.environ['E2E_PROFILE']}_{mode}{sfx}.txt", "w") as f:
                     pstats.Stats(prof, stream=f).sort_stats("cumulative").print_stats(60)
                     pstats.Stats(prof, stream=f).sort_stats("tottime").print_stats(40)
             runs.append(tim)
@@ -88,16 +137,21 @@ def main():
                      "bases_per_s": round(bases / best["wall_s"], 1),
                      "wall_s_runs": [round(t["wall_s"], 3) for t in timed],
                      "peak_rss_mb": resource.getrusage(resource.RUSAGE_SELF).ru_maxrss // 1024,
+                     "workers": workers,
                      "first_run_wall_s": round(runs[0]["wall_s"], 3),
                      "output_bytes": sum(os.path.getsize(os.path.join(out, f"{x}_{mode}{s}"))
                                          for x in ("tumor", "normal") for s in (".1.fastq", ".2.fastq"))}
-        print(json.dumps({mode: res[mode]}), file=sys.stderr, flush=True)
+        if rank == 0:
+            print(json.dumps({mode: res[mode]}), file=sys.stderr, flush=True)
     if "stream" in res and "whole" in res:
         same = all(open(os.path.join(out, f"{x}_stream{s}"), "rb").read() ==
                    open(os.path.join(out, f"{x}_whole{s}"), "rb").read()
                    for x in ("tumor", "normal") for s in (".1.fastq", ".2.fastq"))
         res["stream_equals_whole"] = same
-    print(json.dumps(res))
+    if rank == 0:
+        print(json.dumps(res))
+    if dist is not None:
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

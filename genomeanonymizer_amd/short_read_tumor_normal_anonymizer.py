@@ -9,7 +9,9 @@ arguments and output files:
 By default a sample streams contig by contig with bounded memory (stream.py: per-contig decode,
 plan, one device batch, cross-contig pairing resolution, output at the contig's file offsets);
 GANON_WHOLE_SAMPLE=1 selects the whole-sample path below (one plan and one device batch for the
-sample), kept as the second implementation the tests compare against.
+sample), kept as the second implementation the tests compare against; a sample with secondary /
+supplementary alignments or SA tags (the object model of DESIGN §1c, planned per contig only) goes
+to the streamed path from there, which writes the same files.
 """
 from __future__ import annotations
 
@@ -34,6 +36,12 @@ def name_output(sample: str) -> str:
     return re.sub(".bam|.sam|.cram", ".anonymized", sample)
 
 
+def has_split_alignments(table: ReadTable) -> bool:
+    """Any secondary (0x100) or supplementary (0x800) record or SA tag (the reference's
+    AnonymizedRead object model, AM:84-287)."""
+    return bool(table.n) and (bool(((table.flag & 0x900) != 0).any()) or bool((table.sa_count() >= 0).any()))
+
+
 def get_ref_idxs(fasta: FastaRef) -> Dict[str, int]:
     return dict(fasta.index)
 
@@ -56,6 +64,12 @@ def anonymize_genome(windows_in_sample: List[Window], tumor_bam_file: str, norma
     t0 = time.time()
     tumor = ReadTable(tumor_bam_file, threads=available_threads)
     normal = ReadTable(normal_bam_file, threads=available_threads)
+    if has_split_alignments(tumor) or has_split_alignments(normal):
+        log.info("secondary / supplementary alignments or SA tags: the sample streams contig by contig")
+        from .stream import anonymize_genome_streaming
+        return anonymize_genome_streaming(windows_in_sample, tumor_bam_file, normal_bam_file, fasta, anonymizer,
+                                          tumor_output_fastq, normal_output_fastq, record_statistics,
+                                          available_threads)
     t1 = time.time()
     planner = make_planner(tumor, normal, fasta, windows_in_sample)
     plan = planner.run()

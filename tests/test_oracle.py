@@ -49,14 +49,15 @@ def test_pipeline_split_alignments_match_reference(name, impl, tmp_path, monkeyp
     assert bad == {}
 
 
-def test_whole_sample_refuses_split_alignments(tmp_path, monkeypatch):
-    """The whole-sample planner does not restate the object model: it refuses such input loudly."""
+def test_whole_mode_streams_split_alignments(tmp_path, monkeypatch):
+    """The whole-sample planner does not restate the object model: a sample with secondary /
+    supplementary alignments or SA tags goes to the streamed path, and the files are the
+    reference's (fuzz golden with split alignments)."""
     from pyoracle import OracleEngine
     from genomeanonymizer_amd.anonymizer_methods import CompleteGermlineAnonymizer
-    from genomeanonymizer_amd.planner import UnsupportedInput
     monkeypatch.setenv("GANON_WHOLE_SAMPLE", "1")
-    with pytest.raises(UnsupportedInput):
-        run_pipeline_vs_golden("fuzz1001", str(tmp_path / "w"), CompleteGermlineAnonymizer(engine=OracleEngine()))
+    bad = run_pipeline_vs_golden("fuzz1001", str(tmp_path / "w"), CompleteGermlineAnonymizer(engine=OracleEngine()))
+    assert bad == {}
 
 
 def test_oracle_known_answers():

@@ -416,6 +416,8 @@ def main() -> None:
     ap.add_argument("--target", type=int, default=None, help="GANON_PARAM_GROUP_TARGET (cost units per group)")
     ap.add_argument("--no-fastq", action="store_true", help="skip the FASTQ formatter measurement")
     ap.add_argument("--indel-sort", type=int, default=0, help="GANON_PARAM_INDEL_SORT: 0 segmented, 1 global")
+    ap.add_argument("--spec-plan", type=int, default=1, help="GANON_PARAM_SPEC_PLAN: 1 speculative replans "
+                    "(no host synchronization inside the step), 0 the replan waits for the scan")
     ap.add_argument("--prep-unroll", type=int, default=0, help="GANON_PARAM_PREP_UNROLL: incidences per thread "
                     "and trip of the one-segment emit (0 auto, 1, 2, 4)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (BAM -> FASTQ) line")
@@ -467,6 +469,7 @@ def main() -> None:
         masker.set_param(native.PARAM_GROUP_TARGET, args.target)
     masker.set_param(native.PARAM_INDEL_SORT, args.indel_sort)
     masker.set_param(native.PARAM_PREP_UNROLL, args.prep_unroll)
+    masker.set_param(native.PARAM_SPEC_PLAN, args.spec_plan)
     stream = torch.cuda.current_stream()
     masker.set_stream(stream.cuda_stream)
     t_up = time.perf_counter()
@@ -629,7 +632,9 @@ def main() -> None:
                                   "traffic": dom_traffic if "k_group" in dom else None,
                                   "frac": round(dom_bytes / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}},
         "step_kind": "resident batch, plan kept (run only)" if args.resident else
-                     "fresh batch: device plan (replan) + run every step",
+                     ("fresh batch: device plan (replan: validation scan, group table, shape checks) + run every "
+                      "step; " + ("speculative replan (the run is enqueued behind the scan, which gates it)"
+                                  if args.spec_plan else "the replan waits for the scan")),
         "run_only_ms_per_step": round(run_only_ms, 4) if run_only_ms else None,
         "batch_shape": shape,
         "pass": {"kernel_ms": round(pass_ms, 4), "algorithmic_bytes": alg_total,

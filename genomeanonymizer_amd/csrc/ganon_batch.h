@@ -199,6 +199,12 @@ struct ganon_dbatch {
   ganon_dev::GrpAux *aux = nullptr;
   // plan of the current contents (device prep, sized at upload)
   int32_t n_groups = 0, group_target = 512;
+  // speculative replan (GANON_PARAM_SPEC_PLAN): the last full plan was one-segment mode without huge
+  // scopes for these sizes, so a replan of the same sizes launches its run without waiting for the
+  // scan; the device checks the assumption (plan_info[7]) and ganon_batch_download plans and runs
+  // again when it failed
+  bool spec = false, spec_ready = false;
+  int64_t spec_sizes[3] = {-1, -1, -1};
   // long-read mode (a read with more than one aligned segment): groups cut on the prefix of segments
   // per scope (scost, upload) instead of the CSR offsets, and emitted one wave per incidence
   bool long_mode = false;
@@ -228,7 +234,7 @@ namespace ganon_prep {
 // count, overflow regions) from it: one scan over the raw arrays and one synchronization (two more
 // in the two-pass and long-read modes). Everything a freshly arrived raw batch needs before its
 // first run (upload, reload, ganon_batch_replan).
-int plan(ganon_ctx *ctx, ganon_dbatch *db);
+int plan(ganon_ctx *ctx, ganon_dbatch *db, bool allow_spec);
 // Rebuild every derived array from the raw layer (async on the stream): the first half of
 // every ganon_batch_run.
 int run(ganon_ctx *ctx, ganon_dbatch *db);

@@ -31,6 +31,7 @@ struct ganon_ctx {
   int fq_kd = 0;               // GANON_PARAM_FASTQ_KD (0: quad kernel, 2 quads per lane; 3: dword kernel)
   int indel_sort = 0;          // GANON_PARAM_INDEL_SORT
   int group_obs = 0;           // GANON_PARAM_GROUP_OBS (0 auto, 512, 1024)
+  int spec_plan = 1;           // GANON_PARAM_SPEC_PLAN (1: speculative replans, 0: every plan synchronizes)
   int prep_unroll = 0;         // GANON_PARAM_PREP_UNROLL (0 auto = 2, 1, 2, 4)
   int far_init = 0;            // GANON_PARAM_FAR_INIT (0 auto)
   bool step_open = false;      // ganon_batch_replan started a profiled step the next run continues

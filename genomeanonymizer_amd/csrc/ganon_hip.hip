@@ -838,9 +838,18 @@ template <int U, bool FUSED, int OBS>
 __global__ void __launch_bounds__(kGrpThreads, (OBS > 512 ? 4 : U == 1 ? 6 : U == 2 ? GANON_K2_BLOCKS : U == 4 ? 5 : 4)) k_group(const GrpBatch B, const int4 *__restrict__ groups,
                                                        const int4 *__restrict__ rec4,
                                                        uint8_t *__restrict__ out, const GrpAux *__restrict__ aux,
-                                                       int skip, int nt_copy) {
+                                                       int skip, int nt_copy, const unsigned long long *__restrict__ gate) {
   __shared__ GrpSharedT<OBS> sh;
   const int tid = threadIdx.x;
+  // one-segment mode launches for the group bound: blocks past the scan's count (gate[5]) add
+  // nothing; no block runs on a batch the scan rejected (gate[7])
+  if (gate && (gate[7] || blockIdx.x >= gate[5])) {
+    if (tid == 0) {
+      gp(aux->part)[2 * blockIdx.x] = 0;
+      gp(aux->part)[2 * blockIdx.x + 1] = 0;
+    }
+    return;
+  }
   const int4 g0 = groups[kGrpRec * blockIdx.x];
   const int4 g1 = groups[kGrpRec * blockIdx.x + 1];
   const int4 g2 = groups[kGrpRec * blockIdx.x + 2];
@@ -981,7 +990,7 @@ __global__ void __launch_bounds__(kBlock) k_finish(const unsigned long long *__r
                                                    int32_t *status, unsigned long long *acc,
                                                    unsigned long long *totals,
                                                    const unsigned long long *__restrict__ ws_part,
-                                                   const unsigned long long *__restrict__ ws_expect) {
+                                                   const unsigned long long *__restrict__ plan_info) {
   const int64_t gtid = blockIdx.x * (int64_t)kBlock + threadIdx.x, gstride = (int64_t)gridDim.x * kBlock;
   const unsigned long long far_n = *far_count;
   const int64_t n_far = far_n < (unsigned long long)far_cap ? (int64_t)far_n : far_cap;
@@ -1035,9 +1044,14 @@ __global__ void __launch_bounds__(kBlock) k_finish(const unsigned long long *__r
   __threadfence();
   const unsigned long long sc = atomicExch(&acc[0], 0ull), sb = atomicExch(&acc[1], 0ull);
   atomicExch(&acc[2], 0ull);
-  // every written read met once in its write scope (k_prep_scan's sum vs the emit paths')
-  if (atomicExch(&acc[4], 0ull) != *ws_expect) atomicOr(status, 2);
+  // every written read met once in its write scope (k_prep_scan's sum vs the emit paths'); a gated
+  // run (plan_info[7]: a speculative plan the batch did not fit, or an invalid batch) ran no
+  // one-segment kernel: ganon_batch_download plans and runs it again (or reports the error)
+  const unsigned long long hs = atomicExch(&acc[4], 0ull);
+  if (plan_info[7]) atomicOr(status, 4);
+  else if (hs != plan_info[6]) atomicOr(status, 2);
   for (int k = 0; k < GANON_N_TOTALS; ++k) totals[k] = static_totals[k];
+  totals[GANON_T_READS_WRITTEN] = plan_info[2];
   totals[GANON_T_MASKED_SNV_CALLS] += sc;
   totals[GANON_T_MASKED_BASES] += sb;
   totals[GANON_T_RARE_SCOPES] += (unsigned long long)(atomicExch(&counters[0], 0) + atomicExch(&counters[1], 0));
@@ -1384,11 +1398,12 @@ int host_copy(ganon_ctx *ctx, const ganon_dbatch *db, HostCopy &h) {
 // Plan a batch whose raw arrays are on the device (ganon_prep::plan: validation, prep mode, sizes),
 // the huge-scope tiles (from `host`, or host copies), and upload the group kernels' aux pointers
 // and the static totals (async).
-int prepare(ganon_ctx *ctx, ganon_dbatch *db, const ganon_batch *host) {
+int prepare(ganon_ctx *ctx, ganon_dbatch *db, const ganon_batch *host, bool allow_spec = false) {
   int rc;
   HIP_OR_FAIL(hipMemsetAsync(db->status, 0, sizeof(int32_t), ctx->stream));
   HIP_OR_FAIL(hipMemsetAsync(db->acc + 3, 0, sizeof(unsigned long long), ctx->stream));
-  if ((rc = ganon_prep::plan(ctx, db))) return rc;
+  if ((rc = ganon_prep::plan(ctx, db, allow_spec))) return rc;
+  if (db->spec) return GANON_OK;   // the previous plan's tiles (none), aux pointers and static totals
   if (db->n_huge_scopes && !host) {
     HostCopy h;
     if ((rc = host_copy(ctx, db, h)) || (rc = plan_huge(ctx, db, &h.b))) return rc;
@@ -1501,7 +1516,7 @@ int load_batch(ganon_ctx *ctx, ganon_dbatch *db, const ganon_batch *b, const gan
     return rc;
   // bytes outside every read are never written by the masking kernels: make them defined
   HIP_OR_FAIL(hipMemsetAsync(db->out, 0, (size_t)b->seq_bytes + 16, ctx->stream));
-  if ((rc = prepare(ctx, db, b))) return rc;
+  if ((rc = prepare(ctx, db, b, ctx->spec_plan == 2))) return rc;   // (2: testing knob)
   HIP_OR_FAIL(hipStreamSynchronize(ctx->stream));
   return GANON_OK;
 }
@@ -1640,6 +1655,11 @@ GANON_API int ganon_ctx_set_param(ganon_ctx *ctx, int param, int value) {
     ctx->nt_copy = value != 0;
     return GANON_OK;
   }
+  if (param == GANON_PARAM_SPEC_PLAN) {
+    if (value < 0 || value > 2) return fail(ctx, GANON_E_ARG, "speculative plans: 0, 1 or 2 (got %d)", value);
+    ctx->spec_plan = value;
+    return GANON_OK;
+  }
   if (param == GANON_PARAM_FAR_INIT) {
     if (value < 0) return fail(ctx, GANON_E_ARG, "far-mask list capacity must be >= 0");
     ctx->far_init = value;
@@ -1713,7 +1733,9 @@ GANON_API int ganon_batch_replan(ganon_ctx *ctx, ganon_dbatch *db) {
   HIP_OR_FAIL(hipSetDevice(ctx->device));
   new_step(ctx);
   ctx->step_open = true;   // the next run's kernels join this step's timings
-  int rc = prepare(ctx, db, nullptr);
+  // (speculative: an upload or reload plans in full — its caller reads the shape at once, e.g. the
+  // I/D op count that decides the indel tally)
+  int rc = prepare(ctx, db, nullptr, true);
   if (rc) {
     db->n_groups = 0;
     db->ran = false;
@@ -1752,7 +1774,7 @@ GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
     const GrpBatch GB{B.seq, B.ref, B.keep_code, B.ref2, B.keep_pos, B.span_start, B.span_len};
     kern<<<db->n_groups, kGrpThreads, 0, st>>>(GB, static_cast<const int4 *>(db->b_groups.p),
                                                static_cast<const int4 *>(db->b_seg4.p), db->out, db->aux,
-                                               ctx->group_skip, ctx->nt_copy);
+                                               ctx->group_skip, ctx->nt_copy, db->flat_mode ? db->plan_info : nullptr);
     if ((rc = check_launch(ctx, "k_group"))) return rc;
   } else if (db->seq_bytes) {
     KernelScope ks(ctx, "copy_seq");
@@ -1790,7 +1812,7 @@ GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
                                     db->out, static_cast<const int32_t *>(db->b_grp_part.p), db->n_groups,
                                     db->large_ids, db->n_huge_scopes, db->scope_calls, db->scope_bases,
                                     db->static_totals, db->counters, db->far_count, db->status, db->acc, db->totals,
-                                    static_cast<const unsigned long long *>(db->b_wspart.p), db->plan_info + 6);
+                                    static_cast<const unsigned long long *>(db->b_wspart.p), db->plan_info);
     if ((rc = check_launch(ctx, "k_finish"))) return rc;
   }
   db->ran = true;
@@ -1843,6 +1865,23 @@ GANON_API int ganon_batch_download(ganon_ctx *ctx, ganon_dbatch *db, uint8_t *se
   HIP_OR_FAIL(hipMemcpyAsync(&status, db->status, sizeof status, hipMemcpyDeviceToHost, st));
   HIP_OR_FAIL(hipMemcpyAsync(&far_need, db->acc + 3, sizeof far_need, hipMemcpyDeviceToHost, st));
   HIP_OR_FAIL(hipStreamSynchronize(st));
+  if (status & 4) {
+    // a speculative replan the batch did not fit (a read with several segments, a longer read, a
+    // huge scope): plan it in full and run it again
+    const int sp = ctx->spec_plan;
+    const bool prof = ctx->profiling;
+    ctx->spec_plan = 0;
+    ctx->profiling = false;
+    rc = prepare(ctx, db, nullptr);
+    if (!rc) rc = ganon_batch_run(ctx, db);
+    ctx->spec_plan = sp;
+    ctx->profiling = prof;
+    if (rc) return rc;
+    if ((rc = ganon_prep::batch_error(ctx, db))) return rc;
+    HIP_OR_FAIL(hipMemcpyAsync(&status, db->status, sizeof status, hipMemcpyDeviceToHost, st));
+    HIP_OR_FAIL(hipMemcpyAsync(&far_need, db->acc + 3, sizeof far_need, hipMemcpyDeviceToHost, st));
+    HIP_OR_FAIL(hipStreamSynchronize(st));
+  }
   if (status & 2) {
     // a written read its write scope does not list (or lists twice): name it
     if ((rc = ganon_prep::ws_diag(ctx, db)) || (rc = ganon_prep::batch_error(ctx, db))) return rc;

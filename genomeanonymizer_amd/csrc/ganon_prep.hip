@@ -281,10 +281,14 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_scan(const Raw R, PrepErr
 }
 
 // plan_info: [0] I/D ops, [1] huge scopes, [2] written reads, [3] longest read, [4] most segments of
-// one read, [5] short-read groups (bucket of the last scope + 1), [6] write-scope hash sum.
+// one read, [5] short-read groups (bucket of the last scope + 1), [6] write-scope hash sum, [7] the
+// run's gate: nonzero when the one-segment kernels must not run — the scan found an invalid field,
+// or (speculative replan, spec_rpi > 0) the batch is not what the plan launched for: a read with
+// several segments, a longer read than the overflow regions were cut for, a huge scope.
 __global__ void __launch_bounds__(kPrepThreads) k_prep_reduce(const Raw R, const unsigned long long *__restrict__ part,
                                                               int n_blocks, long long weight, long long target,
-                                                              int64_t g_bound, unsigned long long *__restrict__ info) {
+                                                              int64_t g_bound, unsigned long long *__restrict__ info,
+                                                              const PrepErr *__restrict__ err, long long spec_rpi) {
   unsigned long long acc[kParts] = {0, 0, 0, 0, 0, 0};
   for (int b = threadIdx.x; b < n_blocks; b += kPrepThreads) {
 #pragma unroll
@@ -329,6 +333,9 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_reduce(const Raw R, const
       ng = ng < 1 ? 1 : (ng > g_bound ? g_bound : ng);
     }
     info[5] = (unsigned long long)ng;
+    const unsigned long long rpi = (out[kPartMaxLen] + 47) / 48;
+    const bool spec_bad = spec_rpi > 0 && (out[kPartMaxSeg] > 1 || rpi > (unsigned long long)spec_rpi || out[kPartHuge] > 0);
+    info[7] = (err->code != 0 ? 1ull : 0ull) | (spec_bad ? 2ull : 0ull);
   }
 }
 
@@ -514,7 +521,12 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_linemap(LineMap M) {
 // Piece of candidate c: slot d = c & 1 of group c >> 1. No candidate at all: candidate 0 (group
 // 0, dataset 0) copies the whole buffer.
 __global__ void __launch_bounds__(kPrepThreads) k_prep_pieces(const unsigned long long *__restrict__ lo, int n_cand,
-                                                              LineMap M, int64_t seq_bytes, int4 *__restrict__ groups) {
+                                                              LineMap M, int64_t seq_bytes, int4 *__restrict__ groups,
+                                                              const unsigned long long *__restrict__ gate) {
+  if (gate) {   // one-segment mode: the candidates of the scan's groups only
+    if (gate[7]) return;
+    n_cand = (int)min((unsigned long long)n_cand, 2 * gate[5]);
+  }
   for (int64_t c = blockIdx.x * (int64_t)kPrepThreads + threadIdx.x; c < n_cand; c += (int64_t)gridDim.x * kPrepThreads) {
     const unsigned long long k = lo[c];
     int4 pc = piece(0, 0);
@@ -863,7 +875,8 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_emit_flat(const Raw R, co
                                                                  int64_t n_blk, long long region_per_incid,
                                                                  const Checks C, int4 *__restrict__ seg4,
                                                                  int4 *__restrict__ groups,
-                                                                 unsigned long long *__restrict__ lo, LineMap M) {
+                                                                 unsigned long long *__restrict__ lo, LineMap M,
+                                                                 const unsigned long long *__restrict__ gate) {
   __shared__ long long off[kGrpMaxScopes + 1];
   __shared__ long long ref0[kGrpMaxScopes];
   __shared__ int sstart[kGrpMaxScopes], send[kGrpMaxScopes];
@@ -872,8 +885,15 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_emit_flat(const Raw R, co
   __shared__ unsigned long long lmin[2];
   const int tid = threadIdx.x;
   const int g = blockIdx.x;
+  // launched for the group bound: past the scan's group count (gate[5]) a block only clears its
+  // write-scope sum; nothing runs on a batch the scan rejected (gate[7])
+  if (gate[7]) return;
+  if ((unsigned long long)g >= gate[5]) {
+    if (tid == 0) C.ws_part[g] = 0;
+    return;
+  }
   const longlong2 m0 = gmeta[g];
-  const longlong2 m1 = g + 1 < n_groups ? gmeta[g + 1] : make_longlong2(R.n_scopes, R.n_incid);
+  const longlong2 m1 = (unsigned long long)g + 1 < gate[5] ? gmeta[g + 1] : make_longlong2(R.n_scopes, R.n_incid);
   const int s0 = (int)m0.x, s1 = (int)m1.x, ns = s1 - s0;
   const long long i0 = m0.y, i1 = m1.y;
   for (int t = tid; t <= ns; t += kPrepThreads) off[t] = R.incid_off[s0 + t];
@@ -1273,7 +1293,7 @@ int launch_emit(ganon_ctx *ctx, ganon_dbatch *db, const Raw &R, int write) {
                        static_cast<const longlong2 *>(db->b_gs0.p), db->n_groups, db->ref->bad, db->ref->n_blk,
                        (long long)db->region_per_incid, checks_of(db), static_cast<int4 *>(db->b_seg4.p),
                        static_cast<int4 *>(db->b_groups.p), static_cast<unsigned long long *>(db->b_lo.p),
-                       line_map(db));
+                       line_map(db), static_cast<const unsigned long long *>(db->plan_info));
     return check_launch(ctx, "k_prep_emit_flat");
   }
   hipLaunchKernelGGL(k_prep_emit, dim3((unsigned)db->n_groups), dim3(kPrepThreads), 0, ctx->stream, R,
@@ -1292,7 +1312,7 @@ int launch_pieces(ganon_ctx *ctx, ganon_dbatch *db) {
   hipLaunchKernelGGL(k_prep_linemap, dim3(grid_for(M.n1)), dim3(kPrepThreads), 0, st, M);
   hipLaunchKernelGGL(k_prep_pieces, dim3(grid_for(n_cand)), dim3(kPrepThreads), 0, st,
                      static_cast<const unsigned long long *>(db->b_lo.p), n_cand, M, db->seq_bytes,
-                     static_cast<int4 *>(db->b_groups.p));
+                     static_cast<int4 *>(db->b_groups.p), db->flat_mode ? db->plan_info : nullptr);
   return check_launch(ctx, "k_prep_pieces");
 }
 
@@ -1320,7 +1340,7 @@ int grow(ganon_ctx *ctx, DBuf &b, size_t bytes) {
   return GANON_OK;
 }
 
-int plan(ganon_ctx *ctx, ganon_dbatch *db) {
+int plan(ganon_ctx *ctx, ganon_dbatch *db, bool allow_spec) {
   hipStream_t st = ctx->stream;
   int rc;
   const int64_t nr = db->n_reads, ns = db->n_scopes;
@@ -1330,13 +1350,21 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db) {
     return rc;
   db->B.read_end = read_end;
   db->ran = false;
-  db->n_groups = 0;
   const Raw R = raw_of(db);
   // short-read groups (one-segment and two-pass emits) in closed form from the CSR offsets; the
   // long-read prep cuts its own from the segments per scope below
   const int tgt0 = ctx->group_target ? ctx->group_target : 704;
   const long long w0 = weight_of(tgt0);
   const int64_t g_bound = ns ? (db->n_incid + w0 * (ns - 1)) / tgt0 + 1 : 1;
+  // speculative: the last full plan of db found a one-segment batch without huge scopes of these
+  // sizes; the run launches for the same shape at once and the scan's reduction checks it (gate)
+  const bool spec = allow_spec && ctx->spec_plan && db->spec_ready && db->spec_sizes[0] == nr && db->spec_sizes[1] == ns &&
+                    db->spec_sizes[2] == db->n_incid && db->group_target == tgt0 && db->flat_mode;
+  db->spec = spec;
+  if (!spec) {
+    db->n_groups = 0;
+    db->spec_ready = false;
+  }
   longlong2 *gm = nullptr;
   unsigned long long *part = nullptr;
   const int64_t rb = (nr + kScanReadsPerBlock - 1) / kScanReadsPerBlock;
@@ -1353,9 +1381,11 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db) {
     hipLaunchKernelGGL(k_prep_scan, dim3((unsigned)nb), dim3(kPrepThreads), 0, st, R, db->err,
                        ScanOut{read_end, gm, g_bound, part}, w0, (long long)tgt0, (int)rb);
     hipLaunchKernelGGL(k_prep_reduce, dim3(1), dim3(kPrepThreads), 0, st, R, part, (int)nb, w0, (long long)tgt0, g_bound,
-                       db->plan_info);
+                       db->plan_info, static_cast<const PrepErr *>(db->err),
+                       spec ? (long long)db->region_per_incid : 0ll);
     if ((rc = check_launch(ctx, "k_prep_scan"))) return rc;
   }
+  if (spec) return GANON_OK;   // the previous plan's mode, sizes and buffers; errors at download
   // 2. the one synchronization of a fresh batch: its first error and its shape
   unsigned long long info[6] = {0, 0, 0, 0, 0, 0};
   PrepErr e{};
@@ -1411,6 +1441,9 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db) {
   } else if (ns && db->group_target != tgt0) {
     return fail(ctx, GANON_E_STATE, "group target changed during the plan");
   }
+  // one-segment mode launches for the group bound (blocks past the scan's count return at once):
+  // a speculative replan of the same sizes then needs no count from the host
+  if (db->flat_mode && ns) ng = g_bound;
   if (ng > INT32_MAX / kGrpRec) return fail(ctx, GANON_E_ARG, "batch too large: %lld scope groups", (long long)ng);
   db->n_groups = (int32_t)ng;
   int32_t *p32 = nullptr;
@@ -1460,6 +1493,10 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db) {
       (rc = grow_n(ctx, db->b_gtkey, 2 * (size_t)db->region + 64, &u64)) ||
       (rc = grow_n(ctx, db->b_gtflag, 2 * (size_t)db->region + 64, &u32)))
     return rc;
+  db->spec_ready = db->flat_mode && db->n_huge_scopes == 0;
+  db->spec_sizes[0] = nr;
+  db->spec_sizes[1] = ns;
+  db->spec_sizes[2] = db->n_incid;
   return GANON_OK;
 }
 

@@ -205,6 +205,7 @@ PARAM_PREP_LONG = 9      # include/ganon.h GANON_PARAM_PREP_LONG (-1 auto, 0 nev
 PARAM_GROUP_OBS = 10     # include/ganon.h GANON_PARAM_GROUP_OBS (0 auto, 512, 1024)
 PARAM_PREP_UNROLL = 11   # include/ganon.h GANON_PARAM_PREP_UNROLL (0 auto, 1, 2, 4)
 PARAM_FAR_INIT = 12      # include/ganon.h GANON_PARAM_FAR_INIT (first far-mask list capacity; 0 auto)
+PARAM_SPEC_PLAN = 13     # include/ganon.h GANON_PARAM_SPEC_PLAN (1 speculative replans, 0 synchronous)
 
 EXPORTED_HIP_SYMBOLS = (
     "ganon_ctx_create", "ganon_ctx_destroy", "ganon_last_error", "ganon_abi_version",
@@ -613,7 +614,8 @@ class DeviceBatch:
 
     def replan(self) -> None:
         """ganon_batch_replan: plan the device arrays again exactly as a fresh upload would
-        (validation scan, prep mode, sizes; one synchronization)."""
+        (validation scan, prep mode, sizes; speculative — no synchronization — when the previous
+        plan's one-segment shape still applies; errors then come from download)."""
         self.m._check(self.m._lib.ganon_batch_replan(self.m._h, self.h), "ganon_batch_replan")
 
     def run(self) -> None:

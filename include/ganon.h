@@ -140,7 +140,10 @@ GANON_API int ganon_ctx_set_variant(ganon_ctx *ctx, int variant);
 enum { GANON_PARAM_GROUP_UNROLL = 1, GANON_PARAM_GROUP_SKIP = 2, GANON_PARAM_GROUP_TARGET = 3,
        GANON_PARAM_NT_COPY = 4, GANON_PARAM_REF2 = 5, GANON_PARAM_FASTQ_SKIP = 6, GANON_PARAM_FASTQ_KD = 7,
        GANON_PARAM_INDEL_SORT = 8, GANON_PARAM_PREP_LONG = 9, GANON_PARAM_GROUP_OBS = 10,
-       GANON_PARAM_PREP_UNROLL = 11, GANON_PARAM_FAR_INIT = 12 };
+       GANON_PARAM_PREP_UNROLL = 11, GANON_PARAM_FAR_INIT = 12, GANON_PARAM_SPEC_PLAN = 13 };
+/* GANON_PARAM_SPEC_PLAN: 1 (default) speculative replans (ganon_batch_replan), 0 every plan
+ * synchronizes for the scan's result, 2 (testing knob) reloads speculate too — their caller must
+ * not read the shape before the download. Same results. */
 /* GANON_PARAM_FAR_INIT: first capacity of a batch's far-mask list (entries; 0 = auto, n_reads / 8 but
  * at least 65536). A run that needs more is run again by ganon_batch_download with the list grown
  * to the count it needed (testing knob: 1 forces that path). */
@@ -178,7 +181,15 @@ GANON_API int ganon_ref_free(ganon_ctx *ctx, ganon_ref *ref);
  * reference (resident, or the new batch's own) — the double-buffered streaming path.
  * ganon_batch_replan plans the batch's device arrays again from scratch, exactly as a fresh upload
  * of the same contents would (for arrays another stream or kernel wrote in place, and for timing
- * what a fresh batch costs: replan + run). Since ABI 4. */
+ * what a fresh batch costs: replan + run). Since ABI 4. A replan is speculative (no
+ * synchronization: the scan and the run are enqueued back to back) when the batch's previous plan
+ * found every read with at most one aligned segment and no scope wider than 2^20 positions, for
+ * the same read / scope / incidence counts (GANON_PARAM_SPEC_PLAN 0 turns this off): the scan's
+ * reduction checks that the new contents fit that plan and gates the run's kernels; a batch that
+ * does not fit (or fails validation) runs nothing, and ganon_batch_download then plans it in full
+ * and runs it again (or returns the validation error) — the results are those of a full plan
+ * either way. After a speculative replan, ganon_batch_info / ganon_batch_shape report the previous
+ * full plan until the next download. */
 GANON_API int ganon_batch_upload(ganon_ctx *ctx, const ganon_batch *batch, ganon_dbatch **out);
 GANON_API int ganon_batch_upload_ref(ganon_ctx *ctx, const ganon_batch *batch, const ganon_ref *ref,
                                      ganon_dbatch **out);

@@ -564,6 +564,68 @@ def test_replan_is_a_fresh_upload(masker, oracle):
     assert np.array_equal(want_a[0], o_out) and np.array_equal(want_a[1], o_calls)
 
 
+def _two_segment_copy(arr: dict, r: int) -> dict:
+    """arr with read r's CIGAR replaced by 70M 5I 75M (same query length, shorter on the reference:
+    two aligned segments, the read stays inside its scopes)."""
+    b = {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in arr.items()}
+    assert int(b["n_cig"][r]) == 1 and int(b["read_len"][r]) == 150
+    b["cig_off"][r] = len(b["cigar"])
+    b["n_cig"][r] = 3
+    b["cigar"] = np.concatenate([b["cigar"], np.array([70 << 4, (5 << 4) | 1, 75 << 4], np.uint32)])
+    return b
+
+
+def test_speculative_replan_and_fallback(hip_built):
+    """A replan after a one-segment plan of the same sizes is speculative (no synchronization); the
+    scan's reduction gates the run. A batch that does not fit (a read with two segments) or fails
+    validation runs nothing; ganon_batch_download plans it in full and runs it again, or returns the
+    validation error. GANON_PARAM_SPEC_PLAN 2 makes reloads speculate too (the testing knob)."""
+    from genomeanonymizer_amd import native
+    from genomeanonymizer_amd.synth.batch import config2_batch
+    a, _ = config2_batch(n_reads=120_000, genome=30_000_000, n_windows=10_000, n_germline=25_000, seed=33)
+    cand = np.nonzero((a["write_scope"] >= 0) & (a["n_cig"] == 1) & (a["read_len"] == 150))[0]
+    r = int(cand[len(cand) // 3])
+    b = _two_segment_copy(a, r)
+    bad = {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in a.items()}
+    bad["seq_off"][r] = len(bad["seq_nt16"]) + 10
+    m = native.HipMasker(0)
+    try:
+        want_a, want_b = m.mask(a), m.mask(b)
+        m.set_param(native.PARAM_SPEC_PLAN, 2)
+        db = m.upload(a)
+        try:
+            db.run()
+            got = db.download()
+            assert all(np.array_equal(got[k], want_a[k]) for k in range(4))
+            assert db.shape()["prep_mode"] == "one_segment"
+            db.reload(b)          # speculative: the gate stops the run, download plans b in full
+            db.run()
+            got = db.download()
+            assert all(np.array_equal(got[k], want_b[k]) for k in range(4))
+            assert db.shape()["prep_mode"] == "two_pass" and db.shape()["max_seg"] == 2
+            db.reload(a)          # b's plan was not one-segment: a full plan
+            db.run()
+            got = db.download()
+            assert all(np.array_equal(got[k], want_a[k]) for k in range(4))
+            for _ in range(3):    # speculative replans of the same contents
+                db.replan()
+                db.run()
+            got = db.download()
+            assert all(np.array_equal(got[k], want_a[k]) for k in range(4))
+            db.reload(bad)        # speculative, invalid: nothing runs, download names the read
+            db.run()
+            with pytest.raises(native.GanonError, match="read"):
+                db.download()
+            db.reload(a)
+            db.run()
+            got = db.download()
+            assert all(np.array_equal(got[k], want_a[k]) for k in range(4))
+        finally:
+            db.free()
+    finally:
+        m.close()
+
+
 def test_far_list_overflow_grows_and_reruns(hip_built, oracle):
     """A far-mask list too small for the run (GANON_PARAM_FAR_INIT 1): k_finish reports the count it
     needed, ganon_batch_download grows the list and runs again — the bytes equal the oracle's."""

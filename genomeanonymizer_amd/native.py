@@ -258,6 +258,9 @@ class HipMasker:
         """The packed genome in HBM, uploaded once per array object (stream.py masks one contig
         batch after another against the same genome)."""
         if self._ref is None or self._ref[0] is not ref_nt16:
+            if getattr(self, "_job_db", None) is not None:   # it reads the reference being replaced
+                self._job_db.free()
+                self._job_db = None
             if self._ref is not None:
                 self._ref[1].free()
             self._ref = (ref_nt16, self.upload_reference(ref_nt16))

@@ -204,7 +204,7 @@ struct ganon_dbatch {
   // scan; the device checks the assumption (plan_info[7]) and ganon_batch_download plans and runs
   // again when it failed
   bool spec = false, spec_ready = false;
-  int64_t spec_sizes[3] = {-1, -1, -1};
+  int64_t spec_sizes[4] = {-1, -1, -1, -1};   // reads, scopes, incidences, group target of that plan
   // long-read mode (a read with more than one aligned segment): groups cut on the prefix of segments
   // per scope (scost, upload) instead of the CSR offsets, and emitted one wave per incidence
   bool long_mode = false;

@@ -1403,7 +1403,14 @@ int prepare(ganon_ctx *ctx, ganon_dbatch *db, const ganon_batch *host, bool allo
   HIP_OR_FAIL(hipMemsetAsync(db->status, 0, sizeof(int32_t), ctx->stream));
   HIP_OR_FAIL(hipMemsetAsync(db->acc + 3, 0, sizeof(unsigned long long), ctx->stream));
   if ((rc = ganon_prep::plan(ctx, db, allow_spec))) return rc;
-  if (db->spec) return GANON_OK;   // the previous plan's tiles (none), aux pointers and static totals
+  if (db->spec) {
+    // the previous plan's tiles (none), aux pointers and static totals, unchanged on the host; copied
+    // again (a reload clears the device's small state)
+    HIP_OR_FAIL(hipMemcpyAsync(db->aux, &db->aux_h, sizeof db->aux_h, hipMemcpyHostToDevice, ctx->stream));
+    HIP_OR_FAIL(hipMemcpyAsync(db->static_totals, db->static_h, GANON_N_TOTALS * sizeof(unsigned long long),
+                               hipMemcpyHostToDevice, ctx->stream));
+    return GANON_OK;
+  }
   if (db->n_huge_scopes && !host) {
     HostCopy h;
     if ((rc = host_copy(ctx, db, h)) || (rc = plan_huge(ctx, db, &h.b))) return rc;

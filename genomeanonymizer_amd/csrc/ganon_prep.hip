@@ -1359,7 +1359,7 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db, bool allow_spec) {
   // speculative: the last full plan of db found a one-segment batch without huge scopes of these
   // sizes; the run launches for the same shape at once and the scan's reduction checks it (gate)
   const bool spec = allow_spec && ctx->spec_plan && db->spec_ready && db->spec_sizes[0] == nr && db->spec_sizes[1] == ns &&
-                    db->spec_sizes[2] == db->n_incid && db->group_target == tgt0 && db->flat_mode;
+                    db->spec_sizes[2] == db->n_incid && db->spec_sizes[3] == tgt0 && db->flat_mode;
   db->spec = spec;
   if (!spec) {
     db->n_groups = 0;
@@ -1497,6 +1497,7 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db, bool allow_spec) {
   db->spec_sizes[0] = nr;
   db->spec_sizes[1] = ns;
   db->spec_sizes[2] = db->n_incid;
+  db->spec_sizes[3] = tgt0;
   return GANON_OK;
 }
 

@@ -949,6 +949,180 @@ __global__ void __launch_bounds__(kFqThreads) k_fq_quad(const FqBufs bufs, const
   }
 }
 
+// ---- row variant (GANON_PARAM_FASTQ_KD 12) -----------------------------------------------------
+// No virtual map: one thread per record stages its three field extents (tile offset, source,
+// length) and its constant bytes; then each field is formatted in one flat pass over (record,
+// 8-byte unit) pairs — a record's units are G consecutive lanes, G the tile's widest extent of that
+// field rounded up to a power of two (20 of 32 lanes carry a 150-byte field, 5-7 of 8 a read
+// name). A unit is two tile dwords: three aligned source dwords (clamped into the field's own
+// aligned extent: bytes outside the field are masked off anyway), two v_alignbyte, the transform
+// (+33 per byte for qualities, two v_perm nibble selects and the 16-entry table for bases, byte
+// reversal for reversed fields) and two LDS stores — plain for dwords inside the field, masked OR
+// for the dwords it shares with a neighbour or a constant. Per unit that is ~1/3 of the quad
+// variant's address and map work.
+struct FqRow {
+  uint64_t src[3];   // bases: 2 * byte address + first nibble; qualities / name: address of byte 0
+  int32_t fo[3];     // tile offset of the field's first byte (< 0: it starts in an earlier tile)
+  uint32_t len[3];
+  uint32_t rev;      // bit 0 bases reversed, bit 1 qualities reversed
+  uint32_t pad;
+};
+static_assert(sizeof(FqRow) == 56, "FqRow layout");
+
+__device__ __forceinline__ uint32_t fq_bmask(int j, int len) {   // bytes j..j+3 of a field inside [0, len)
+  const int lo = max(0, -j), hi = min(4, len - j);
+  return hi > lo ? (0xFFFFFFFFu >> (8 * (4 - (hi - lo)))) << (8 * lo) : 0u;
+}
+
+// Field f (0 bases, 1 qualities, 2 name) of every staged record: units u of record k.
+template <int F>
+__device__ __forceinline__ void fq_rows_field(const FqRow *rows, int ns, int lg, uint32_t *tile32, int64_t r0,
+                                              unsigned long long &bad) {
+  const int G = 1 << lg;
+  for (int vl = threadIdx.x; vl < (ns << lg); vl += kFqThreads) {
+    const int k = vl >> lg, u = vl & (G - 1);
+    const int fo = rows[k].fo[F];
+    const int len = (int)rows[k].len[F];
+    const int T = ((fo >> 3) + u) * 8;           // tile byte of the unit (8-aligned)
+    if (T < 0 || T >= kFqTile || T >= fo + len || len == 0) continue;
+    const int i0 = T - fo;                       // field byte of the unit's first byte (>= -7)
+    const bool rev = F == 0 ? (rows[k].rev & 1) : F == 1 ? ((rows[k].rev >> 1) & 1) : false;
+    const uint64_t src = rows[k].src[F];
+    uint32_t x0, x1;
+    if (F == 0) {
+      // nibbles of the 8 bases, ascending: [n_lo, n_lo + 8)
+      const int64_t nlo = (int64_t)src + (rev ? (int64_t)(len - 8 - i0) : (int64_t)i0);
+      const uint64_t fb0 = src >> 1, fb1 = ((uint64_t)src + len - 1) >> 1;   // the field's bytes
+      const uint64_t A0 = fb0 & ~(uint64_t)3;
+      const int hi = (int)((fb1 - A0) >> 2);
+      const int64_t B = nlo >> 1;                                            // first byte (may precede the field)
+      const int64_t rel = B - (int64_t)A0;                                   // >= -4
+      const int di = (int)((rel + 8) >> 2) - 2, sh = (int)((rel + 8) & 3);
+      const GU32 *base = reinterpret_cast<const GU32 *>(A0);
+      const uint32_t d0 = __builtin_nontemporal_load(base + min(max(di, 0), hi));
+      const uint32_t d1 = __builtin_nontemporal_load(base + min(max(di + 1, 0), hi));
+      const uint32_t d2 = __builtin_nontemporal_load(base + min(max(di + 2, 0), hi));
+      const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh), w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+      const uint32_t h0 = __builtin_amdgcn_alignbyte(w1, w0, 2);   // bytes B + 2 .. B + 5
+      const uint32_t par = (uint32_t)(nlo & 1);
+      const uint32_t sel = rev ? (par ? 0x04010502u : 0x00040105u) : (par ? 0x02050104u : 0x05010400u);
+      const uint64_t tlo = rev ? kRevLo : kFwdLo, thi = rev ? kRevHi : kFwdHi;
+      const uint32_t a = rev ? h0 : w0, b = rev ? w0 : h0;   // reversed: the upper nibbles first
+      const uint32_t ca = __builtin_amdgcn_perm(a & 0x0F0F0F0Fu, (a >> 4) & 0x0F0F0F0Fu, sel);
+      const uint32_t cb = __builtin_amdgcn_perm(b & 0x0F0F0F0Fu, (b >> 4) & 0x0F0F0F0Fu, sel);
+      x0 = nt16_lut(ca, tlo, thi);
+      x1 = nt16_lut(cb, tlo, thi);
+      if (rev) {
+        const uint32_t y0 = x0 | ~fq_bmask(i0, len), y1 = x1 | ~fq_bmask(i0 + 4, len);
+        if (((y0 - 0x01010101u) & ~y0 & 0x80808080u) | ((y1 - 0x01010101u) & ~y1 & 0x80808080u))
+          bad = min(bad, (unsigned long long)(r0 + k));
+      }
+    } else {
+      // bytes [j_lo, j_lo + 8) of the field, ascending (reversed qualities: read backwards)
+      const int jlo = rev ? len - 8 - i0 : i0;
+      const uint64_t A0 = src & ~(uint64_t)3;
+      const int hi = (int)(((src & 3) + (uint64_t)len - 1) >> 2);
+      const int rel = (int)(src & 3) + jlo;                                  // >= -7
+      const int di = ((rel + 8) >> 2) - 2, sh = (rel + 8) & 3;
+      const GU32 *base = reinterpret_cast<const GU32 *>(A0);
+      const uint32_t d0 = __builtin_nontemporal_load(base + min(max(di, 0), hi));
+      const uint32_t d1 = __builtin_nontemporal_load(base + min(max(di + 1, 0), hi));
+      const uint32_t d2 = __builtin_nontemporal_load(base + min(max(di + 2, 0), hi));
+      uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh), w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+      if (rev) {
+        const uint32_t t = __builtin_bswap32(w1);
+        w1 = __builtin_bswap32(w0);
+        w0 = t;
+      }
+      x0 = F == 1 ? add33(w0) : w0;
+      x1 = F == 1 ? add33(w1) : w1;
+    }
+    const uint32_t m0 = fq_bmask(i0, len), m1 = fq_bmask(i0 + 4, len);
+    uint32_t *t32 = tile32 + (T >> 2);
+    if (m0 == 0xFFFFFFFFu) t32[0] = x0;
+    else if (m0) atomicOr(t32, x0 & m0);
+    if (m1 == 0xFFFFFFFFu) t32[1] = x1;
+    else if (m1) atomicOr(t32 + 1, x1 & m1);
+  }
+}
+
+__global__ void __launch_bounds__(kFqThreads) k_fq_rows(const FqBufs bufs, const FqRec *__restrict__ recs,
+                                                        const uint64_t *__restrict__ off,
+                                                        const int64_t *__restrict__ tile_first, int64_t n,
+                                                        uint64_t total, uint8_t *__restrict__ out,
+                                                        unsigned long long *__restrict__ err, int skip,
+                                                        int *__restrict__ dense_list,
+                                                        unsigned int *__restrict__ dense_count) {
+  __shared__ __attribute__((aligned(16))) uint8_t tile[kFqTile];
+  __shared__ FqRow rows[kFqStage];
+  __shared__ int s_lg[3];
+  const uint64_t t0 = (uint64_t)blockIdx.x * kFqTile;
+  const int64_t r0 = tile_first[blockIdx.x];
+  const int64_t rl = (t0 + kFqTile < total) ? tile_first[blockIdx.x + 1] : n - 1;
+  const int t = threadIdx.x;
+  uint32_t *tile32 = reinterpret_cast<uint32_t *>(tile);
+  if (rl - r0 + 1 > kFqStage) {   // left to k_fq_dense
+    if (t == 0) dense_list[atomicAdd(dense_count, 1u)] = (int)blockIdx.x;
+    return;
+  }
+  const int ns = (int)(rl - r0 + 1);
+  // 1. zero the tile; one thread per record: its row, its constant bytes, the field widths
+  reinterpret_cast<uint4 *>(tile)[t] = make_uint4(0, 0, 0, 0);
+  reinterpret_cast<uint4 *>(tile)[t + kFqThreads] = make_uint4(0, 0, 0, 0);
+  if (t < 3) s_lg[t] = 0;
+  __syncthreads();
+  if (t < ns) {
+    const FqRec R = recs[r0 + t];
+    const int64_t P0 = (int64_t)off[r0 + t] - (int64_t)t0;   // > -2^31: a record is < 2^31 bytes
+    const uint32_t NL = (uint32_t)(R.name >> 48), L = R.len, Q = R.qlen;
+    const uint32_t mate = (uint32_t)((R.qual >> 48) & 0xFF);
+    FqRow w;
+    w.src[0] = 2 * (uint64_t)(uintptr_t)pick4(bufs.seq, (uint32_t)(R.seq >> 56) & 3) + (R.seq & kOff56);
+    w.src[1] = (uint64_t)(uintptr_t)(pick4(bufs.qual, (uint32_t)(R.qual >> 56) & 3) + (R.qual & kOff48));
+    w.src[2] = (uint64_t)(uintptr_t)(bufs.names + (R.name & kOff48));
+    w.fo[0] = (int32_t)(P0 + NL + 4);
+    w.fo[1] = (int32_t)(P0 + NL + 7 + L);
+    w.fo[2] = (int32_t)(P0 + 1);
+    w.len[0] = L;
+    w.len[1] = Q;
+    w.len[2] = NL;
+    w.rev = (uint32_t)((R.seq >> 58) & 1) | ((uint32_t)((R.seq >> 59) & 1) << 1);
+    w.pad = 0;
+    rows[t] = w;
+#pragma unroll
+    for (int f = 0; f < 3; ++f) {   // units (8-byte) the field spans, as a power-of-two exponent
+      const int units = w.len[f] ? ((w.fo[f] + (int)w.len[f] + 7) >> 3) - (w.fo[f] >> 3) : 0;
+      int lg = 0;
+      while ((1 << lg) < units) ++lg;
+      atomicMax(&s_lg[f], lg);
+    }
+    const int64_t o[8] = {0, NL + 1, NL + 2, NL + 3, NL + 4 + L, NL + 5 + L, NL + 6 + L, NL + 7 + L + Q};
+    const uint32_t x[8] = {'@', '/', (mate + '0') & 0xFF, '\n', '\n', '+', '\n', '\n'};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int64_t p = P0 + o[e];
+      if (p >= 0 && p < kFqTile) atomicOr(&tile32[p >> 2], x[e] << (8 * (p & 3)));
+    }
+  }
+  __syncthreads();
+  unsigned long long bad = ~0ull;
+  if (!(skip & 32)) {
+    fq_rows_field<0>(rows, ns, s_lg[0], tile32, r0, bad);
+    fq_rows_field<1>(rows, ns, s_lg[1], tile32, r0, bad);
+    fq_rows_field<2>(rows, ns, s_lg[2], tile32, r0, bad);
+  }
+  if (bad != ~0ull) atomicMin(err, bad);
+  __syncthreads();
+  if (skip & 2) return;
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int q = 0; q < kFqTile / (16 * kFqThreads); ++q) {
+    const int p = (q * kFqThreads + t) * 16;
+    if (t0 + p >= total) break;
+    __builtin_nontemporal_store(*reinterpret_cast<const u32x4 *>(tile + p), reinterpret_cast<u32x4 *>(out + t0 + p));
+  }
+}
+
 // Tiles touched by more than kFqStage records (records of a few dozen bytes), listed by
 // k_fq_format: built in LDS record by record (one wave per record), a fixed grid looping over
 // the list.
@@ -1187,7 +1361,8 @@ GANON_API int ganon_fastq_run(ganon_ctx *ctx, ganon_fastq *f) {
     // virtual dwords per lane per round: a tile holds ~2,100 of them (2,048 tile dwords plus the
     // dwords neighbouring fields share), so the width sets the number of dependent load rounds
     const int kd = ctx->fq_kd;
-    auto kern = kd == 0 ? k_fq_quad<2> : kd == 9 ? k_fq_quad<1> : kd == 10 ? k_fq_quad<3> : kd == 11 ? k_fq_quad<2, false>
+    auto kern = kd == 0 ? k_fq_quad<2> : kd == 12 ? k_fq_rows : kd == 9 ? k_fq_quad<1> : kd == 10 ? k_fq_quad<3>
+              : kd == 11 ? k_fq_quad<2, false>
               : kd == 1 ? k_fq_format<1> : kd == 2 ? k_fq_format<2> : kd == 3 ? k_fq_format<3>
               : kd == 5 ? k_fq_format<5> : kd == 6 ? k_fq_format<6> : kd == 8 ? k_fq_format<8> : k_fq_format<4>;
     hipLaunchKernelGGL(kern, dim3((unsigned)f->n_tiles), dim3(kFqThreads), 0, ctx->stream, f->bufs, f->recs,

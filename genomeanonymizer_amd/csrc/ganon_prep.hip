@@ -181,11 +181,65 @@ __device__ __forceinline__ void block_parts(unsigned long long (&acc)[kParts], u
   }
 }
 
+// One read's CIGAR walked by a whole wave, 64 ops at a time (long reads: thousands of ops, a serial
+// chain of dependent loads for one thread): the reference length (bam_endpos), the aligned
+// segments as walk_segments cuts them (per-lane query offsets from a wave prefix sum, the
+// read-length clip), the I/D ops; bad_op = the first op code above 8 (the walk stops there), or -1.
+struct CigarWalk {
+  long long rl;
+  int ns, nid, bad_op;
+};
+
+__device__ __forceinline__ CigarWalk wave_cigar_walk(const uint32_t *__restrict__ cg, int nc, int L) {
+  const int lane = threadIdx.x & 63;
+  CigarWalk W{0, 0, 0, -1};
+  int q = 0;
+  for (int base = 0; base < nc; base += 64) {
+    const int k = base + lane;
+    const uint32_t w = k < nc ? cg[k] : 0u;   // padding lanes: a 0M op, which adds nothing
+    const int op = (int)(w & 0xF), len = (int)(w >> 4);
+    const unsigned long long badm = __ballot(op > 8);
+    if (badm) {
+      W.bad_op = __shfl(op, __ffsll((long long)badm) - 1);
+      return W;
+    }
+    const bool al = is_aligned_op(op);
+    const int dq = (al || op == 1 || op == 4) ? len : 0;
+    int incl = dq;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int x = __shfl_up(incl, o);
+      if (lane >= o) incl += x;
+    }
+    const int q0 = q + incl - dq;
+    int seg = (al && q0 < L) ? (min(len, L - q0) + kSegMaxLen - 1) / kSegMaxLen : 0;
+    int id = (op == 1 || op == 2) ? 1 : 0;
+    long long dr = (al || op == 2 || op == 3) ? (long long)len : 0ll;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      seg += __shfl_xor(seg, o);
+      id += __shfl_xor(id, o);
+      dr += __shfl_xor(dr, o);
+    }
+    W.ns += seg;
+    W.nid += id;
+    W.rl += dr;
+    q += __shfl(incl, 63);
+  }
+  return W;
+}
+
+constexpr int kScanLongCigar = 48;   // reads with more CIGAR ops are walked by a wave (k_prep_scan)
+
 __global__ void __launch_bounds__(kPrepThreads) k_prep_scan(const Raw R, PrepErr *err, ScanOut O, long long weight,
                                                             long long target, int read_blocks) {
   unsigned long long acc[kParts] = {0, 0, 0, 0, 0, 0};
   const int tid = threadIdx.x;
+  __shared__ int s_long[kScanReadsPerBlock];   // reads of the block left to the wave walk
+  __shared__ int s_nlong;
   if ((int)blockIdx.x < read_blocks) {
+    if (tid == 0) s_nlong = 0;
+    __syncthreads();
     // kScanU reads per thread, each load stage issued for all of them before any is used (the chain
     // read fields -> first CIGAR word is latency bound)
     constexpr int kScanU = kScanReadsPerBlock / kPrepThreads;
@@ -227,6 +281,10 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_scan(const Raw R, PrepErr
         acc[kPartWritten] += ws[u] >= 0;
         if (ws[u] >= 0) acc[kPartWsHash] += ws_hash((int)r);
         acc[kPartMaxLen] = max(acc[kPartMaxLen], (unsigned long long)L[u]);
+        if (nc[u] > kScanLongCigar) {   // a long read: the wave walk below
+          s_long[atomicAdd(&s_nlong, 1)] = (int)(r - r0);
+          continue;
+        }
         // one walk: reference length (bam_endpos), aligned segments as walk_segments cuts them,
         // I/D ops (the indel tally's observations)
         int64_t rl = 0;
@@ -254,6 +312,24 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_scan(const Raw R, PrepErr
           acc[kPartMaxSeg] = max(acc[kPartMaxSeg], (unsigned long long)ns);
           acc[kPartIdOps] += (unsigned long long)nid;
         }
+      }
+    }
+    __syncthreads();
+    // the long reads, one wave each (their read-level checks passed above)
+    const int nl = s_nlong;
+    for (int j = tid >> 6; j < nl; j += kPrepThreads / 64) {
+      const int64_t r = r0 + s_long[j];
+      const int rs_ = R.ref_start[r];
+      const CigarWalk W = wave_cigar_walk(R.cigar + R.cig_off[r], R.n_cig[r], R.read_len[r]);
+      if ((tid & 63) != 0) continue;
+      if (W.bad_op >= 0) {
+        report(err, kErrCigarOp, r, W.bad_op);
+      } else if (rs_ < 0 || rs_ + W.rl > INT32_MAX) {
+        report(err, kErrReadPos, r);
+      } else {
+        O.read_end[r] = (int32_t)(rs_ + (W.rl > 0 ? W.rl : 1));
+        acc[kPartMaxSeg] = max(acc[kPartMaxSeg], (unsigned long long)W.ns);
+        acc[kPartIdOps] += (unsigned long long)W.nid;
       }
     }
   } else {
@@ -351,15 +427,12 @@ __device__ __forceinline__ int lds_upper(const long long *off, int n, long long 
 }
 
 // Long-read mode only: aligned segments per read (walk_segments' cuts), for the segment-weighted
-// groups and the record slots.
+// groups and the record slots; one wave per read (wave_cigar_walk).
 __global__ void __launch_bounds__(kPrepThreads) k_prep_nseg(const Raw R, int32_t *__restrict__ nseg) {
-  for (int64_t r = blockIdx.x * (int64_t)kPrepThreads + threadIdx.x; r < R.n_reads;
-       r += (int64_t)gridDim.x * kPrepThreads) {
-    const int nc = R.n_cig[r];
-    int ns = 0;
-    walk_segments(R.cigar + R.cig_off[r], nc, R.read_len[r], R.ref_start[r], nc ? R.cigar[R.cig_off[r]] : 0u,
-                  [&](int, int, int) { ++ns; });
-    nseg[r] = ns;
+  const int64_t n_waves = (int64_t)gridDim.x * (kPrepThreads / 64);
+  for (int64_t r = (blockIdx.x * (int64_t)kPrepThreads + threadIdx.x) >> 6; r < R.n_reads; r += n_waves) {
+    const CigarWalk W = wave_cigar_walk(R.cigar + R.cig_off[r], R.n_cig[r], R.read_len[r]);
+    if ((threadIdx.x & 63) == 0) nseg[r] = W.ns;
   }
 }
 
@@ -1418,7 +1491,7 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db, bool allow_spec) {
   if (db->long_mode && ns) {
     // groups cut on the prefix of segments per scope: cost[s] = segments of its incidences + w
     if ((rc = grow_n(ctx, db->b_nseg, (size_t)std::max<int64_t>(nr, 1), &nseg))) return rc;
-    if (nr) hipLaunchKernelGGL(k_prep_nseg, dim3(grid_for(nr)), dim3(kPrepThreads), 0, st, R, nseg);
+    if (nr) hipLaunchKernelGGL(k_prep_nseg, dim3(grid_for(nr * 64)), dim3(kPrepThreads), 0, st, R, nseg);
     int64_t *cost = nullptr;
     if ((rc = grow_n(ctx, db->b_scost, (size_t)ns + 1, &cost))) return rc;
     hipLaunchKernelGGL(k_prep_scope_cost, dim3(grid_for(ns + 1)), dim3(kPrepThreads), 0, st, R, nseg, w, cost);

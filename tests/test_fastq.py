@@ -83,10 +83,11 @@ def test_bad_for_reverse_flags_non_acgtn_reads():
 
 # ---- GPU: the HIP formatter ----------------------------------------------------------------
 
-@pytest.fixture(scope="module", params=[0, 9, 11, 3], ids=["quad2", "quad1", "quad2_select", "dword3"])
+@pytest.fixture(scope="module", params=[0, 12, 9, 11, 3], ids=["quad2", "rows", "quad1", "quad2_select", "dword3"])
 def masker(hip_built, request):
     """Every HIP formatter test runs on the quad kernel (GANON_PARAM_FASTQ_KD 0, the default; 9 = one
-    quad per lane; 11 = the per-dword base select of round 1) and on the dword kernel (3)."""
+    quad per lane; 11 = the per-dword base select of round 1), the record-row kernel (12) and the
+    dword kernel (3)."""
     m = native.HipMasker(0)
     m.set_param(native.PARAM_FASTQ_KD, request.param)
     yield m

@@ -40,7 +40,7 @@ sys.path.insert(0, REPO)
 
 HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 GROUP_MAX_SPAN = 1 << 20                # kGrpMaxSpan: widest scope of the group kernels
-PREP_KERNELS = ("prep_scan", "prep_groups", "prep_emit", "prep_pieces", "prep_seen_check")
+PREP_KERNELS = ("prep_scan", "prep_scan_long", "prep_groups", "prep_emit", "prep_pieces")
 
 
 def kernel_class(name: str) -> str:

@@ -180,6 +180,7 @@ struct ganon_dbatch {
       b_incid_off, b_incid_read, b_span_start, b_span_len, b_ref_off, b_keep_pos, b_keep_code;
   // derived layer
   ganon_dev::DBuf b_part;                                          // k_prep_scan per-block partials
+  ganon_dev::DBuf b_long;                                          // k_prep_scan's list of long-CIGAR reads
   ganon_dev::DBuf b_nseg, b_scost, b_scan_tmp, b_slots, b_slot0;   // segments per read; long-read mode: group
                                                                   // costs, dirty flags, first slot per incidence
   ganon_dev::DBuf b_wspart;                                        // per-group write-scope hash sums

@@ -1201,7 +1201,7 @@ void free_batch(ganon_dbatch *db) {
                   &db->b_span_start, &db->b_span_len, &db->b_ref_off, &db->b_keep_pos, &db->b_keep_code,
                   &db->b_read_end, &db->b_wspart, &db->b_cursor, &db->b_gs0, &db->b_lo, &db->b_linemap, &db->b_groups,
                   &db->b_seg4, &db->b_grp_part, &db->b_far, &db->b_gokey, &db->b_gopay, &db->b_gtkey, &db->b_gtflag,
-                  &db->b_out, &db->b_scope_calls, &db->b_scope_bases, &db->b_small, &db->b_part, &db->b_nseg,
+                  &db->b_out, &db->b_scope_calls, &db->b_scope_bases, &db->b_small, &db->b_part, &db->b_long, &db->b_nseg,
                   &db->b_scost, &db->b_scan_tmp, &db->b_slots, &db->b_slot0};
   for (DBuf *b : bufs) free_buf(*b);
   free_huge(db);

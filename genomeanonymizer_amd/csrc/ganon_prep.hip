@@ -148,6 +148,8 @@ constexpr int kScanScopesPerBlock = 4 * kPrepThreads;
 
 struct ScanOut {
   int32_t *read_end;
+  int32_t *long_list;         // reads with more than kScanLongCigar CIGAR ops (k_prep_scan_long walks them)
+  unsigned int *long_count;
   longlong2 *gmeta;           // [g_bound] first scope and incidence of each short-read group
   int64_t g_bound;            // group count bound: (n_incid + weight (n_scopes - 1)) / target + 1
   unsigned long long *part;   // [kParts x blocks]
@@ -229,17 +231,14 @@ __device__ __forceinline__ CigarWalk wave_cigar_walk(const uint32_t *__restrict_
   return W;
 }
 
-constexpr int kScanLongCigar = 48;   // reads with more CIGAR ops are walked by a wave (k_prep_scan)
+constexpr int kScanLongCigar = 48;   // reads with more CIGAR ops are walked by a wave (k_prep_scan_long)
+constexpr int kLongGrid = 4096;      // workgroups of k_prep_scan_long at most (4 waves each)
 
 __global__ void __launch_bounds__(kPrepThreads) k_prep_scan(const Raw R, PrepErr *err, ScanOut O, long long weight,
                                                             long long target, int read_blocks) {
   unsigned long long acc[kParts] = {0, 0, 0, 0, 0, 0};
   const int tid = threadIdx.x;
-  __shared__ int s_long[kScanReadsPerBlock];   // reads of the block left to the wave walk
-  __shared__ int s_nlong;
   if ((int)blockIdx.x < read_blocks) {
-    if (tid == 0) s_nlong = 0;
-    __syncthreads();
     // kScanU reads per thread, each load stage issued for all of them before any is used (the chain
     // read fields -> first CIGAR word is latency bound)
     constexpr int kScanU = kScanReadsPerBlock / kPrepThreads;
@@ -281,8 +280,8 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_scan(const Raw R, PrepErr
         acc[kPartWritten] += ws[u] >= 0;
         if (ws[u] >= 0) acc[kPartWsHash] += ws_hash((int)r);
         acc[kPartMaxLen] = max(acc[kPartMaxLen], (unsigned long long)L[u]);
-        if (nc[u] > kScanLongCigar) {   // a long read: the wave walk below
-          s_long[atomicAdd(&s_nlong, 1)] = (int)(r - r0);
+        if (nc[u] > kScanLongCigar) {   // a long read: k_prep_scan_long walks it with a wave
+          O.long_list[atomicAdd(O.long_count, 1u)] = (int32_t)r;
           continue;
         }
         // one walk: reference length (bam_endpos), aligned segments as walk_segments cuts them,
@@ -314,24 +313,6 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_scan(const Raw R, PrepErr
         }
       }
     }
-    __syncthreads();
-    // the long reads, one wave each (their read-level checks passed above)
-    const int nl = s_nlong;
-    for (int j = tid >> 6; j < nl; j += kPrepThreads / 64) {
-      const int64_t r = r0 + s_long[j];
-      const int rs_ = R.ref_start[r];
-      const CigarWalk W = wave_cigar_walk(R.cigar + R.cig_off[r], R.n_cig[r], R.read_len[r]);
-      if ((tid & 63) != 0) continue;
-      if (W.bad_op >= 0) {
-        report(err, kErrCigarOp, r, W.bad_op);
-      } else if (rs_ < 0 || rs_ + W.rl > INT32_MAX) {
-        report(err, kErrReadPos, r);
-      } else {
-        O.read_end[r] = (int32_t)(rs_ + (W.rl > 0 ? W.rl : 1));
-        acc[kPartMaxSeg] = max(acc[kPartMaxSeg], (unsigned long long)W.ns);
-        acc[kPartIdOps] += (unsigned long long)W.nid;
-      }
-    }
   } else {
     const int64_t s0 = (int64_t)(blockIdx.x - read_blocks) * kScanScopesPerBlock;
     const int64_t s1 = min(s0 + kScanScopesPerBlock, (int64_t)R.n_scopes);
@@ -356,6 +337,31 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_scan(const Raw R, PrepErr
   block_parts(acc, O.part);
 }
 
+// The long reads k_prep_scan listed (their read-level checks passed there), one wave each: read_end,
+// segments, I/D ops into per-block partials after the scan's (k_prep_reduce sums both). Launched
+// after the plan's synchronization found some (a second, small reduction follows): short-read
+// batches never pay for it.
+__global__ void __launch_bounds__(kPrepThreads) k_prep_scan_long(const Raw R, PrepErr *err, ScanOut O, int n_long) {
+  unsigned long long acc[kParts] = {0, 0, 0, 0, 0, 0};
+  const int64_t n_waves = (int64_t)gridDim.x * (kPrepThreads / 64);
+  for (int64_t j = (blockIdx.x * (int64_t)kPrepThreads + threadIdx.x) >> 6; j < n_long; j += n_waves) {
+    const int64_t r = O.long_list[j];
+    const int rs_ = R.ref_start[r];
+    const CigarWalk W = wave_cigar_walk(R.cigar + R.cig_off[r], R.n_cig[r], R.read_len[r]);
+    if ((threadIdx.x & 63) != 0) continue;
+    if (W.bad_op >= 0) {
+      report(err, kErrCigarOp, r, W.bad_op);
+    } else if (rs_ < 0 || rs_ + W.rl > INT32_MAX) {
+      report(err, kErrReadPos, r);
+    } else {
+      O.read_end[r] = (int32_t)(rs_ + (W.rl > 0 ? W.rl : 1));
+      acc[kPartMaxSeg] = max(acc[kPartMaxSeg], (unsigned long long)W.ns);
+      acc[kPartIdOps] += (unsigned long long)W.nid;
+    }
+  }
+  block_parts(acc, O.part);
+}
+
 // plan_info: [0] I/D ops, [1] huge scopes, [2] written reads, [3] longest read, [4] most segments of
 // one read, [5] short-read groups (bucket of the last scope + 1), [6] write-scope hash sum, [7] the
 // run's gate: nonzero when the one-segment kernels must not run — the scan found an invalid field,
@@ -364,7 +370,8 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_scan(const Raw R, PrepErr
 __global__ void __launch_bounds__(kPrepThreads) k_prep_reduce(const Raw R, const unsigned long long *__restrict__ part,
                                                               int n_blocks, long long weight, long long target,
                                                               int64_t g_bound, unsigned long long *__restrict__ info,
-                                                              const PrepErr *__restrict__ err, long long spec_rpi) {
+                                                              const PrepErr *__restrict__ err, long long spec_rpi,
+                                                              const unsigned int *__restrict__ long_count) {
   unsigned long long acc[kParts] = {0, 0, 0, 0, 0, 0};
   for (int b = threadIdx.x; b < n_blocks; b += kPrepThreads) {
 #pragma unroll
@@ -410,7 +417,8 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_reduce(const Raw R, const
     }
     info[5] = (unsigned long long)ng;
     const unsigned long long rpi = (out[kPartMaxLen] + 47) / 48;
-    const bool spec_bad = spec_rpi > 0 && (out[kPartMaxSeg] > 1 || rpi > (unsigned long long)spec_rpi || out[kPartHuge] > 0);
+    const bool spec_bad = spec_rpi > 0 && (out[kPartMaxSeg] > 1 || rpi > (unsigned long long)spec_rpi ||
+                                           out[kPartHuge] > 0 || *long_count > 0);
     info[7] = (err->code != 0 ? 1ull : 0ull) | (spec_bad ? 2ull : 0ull);
   }
 }
@@ -1444,27 +1452,51 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db, bool allow_spec) {
   const int64_t sb = (ns + kScanScopesPerBlock - 1) / kScanScopesPerBlock;
   const int64_t nb = std::max<int64_t>(1, rb + sb);
   if (nb > INT32_MAX) return fail(ctx, GANON_E_ARG, "batch too large");
-  if ((rc = grow_n(ctx, db->b_gs0, (size_t)g_bound, &gm)) || (rc = grow_n(ctx, db->b_part, (size_t)kParts * nb, &part)))
+  // partials: the scan's blocks, then up to kLongGrid blocks of k_prep_scan_long, then its counter
+  int32_t *long_list = nullptr;
+  if ((rc = grow_n(ctx, db->b_gs0, (size_t)g_bound, &gm)) ||
+      (rc = grow_n(ctx, db->b_part, (size_t)kParts * (nb + kLongGrid) + 1, &part)) ||
+      (rc = grow_n(ctx, db->b_long, (size_t)std::max<int64_t>(nr, 1), &long_list)))
     return rc;
+  auto *long_count = reinterpret_cast<unsigned int *>(part + (size_t)kParts * (nb + kLongGrid));
+  const ScanOut O{read_end, long_list, long_count, gm, g_bound, part};
   {
     // 1. the batch scan: every per-read and per-scope check, read ends, the group table of the
     //    short-read modes, per-block partials; then their reduction
     KernelScope ks(ctx, "prep_scan");
     HIP_OR_FAIL(hipMemsetAsync(db->err, 0, sizeof(PrepErr), st));
-    hipLaunchKernelGGL(k_prep_scan, dim3((unsigned)nb), dim3(kPrepThreads), 0, st, R, db->err,
-                       ScanOut{read_end, gm, g_bound, part}, w0, (long long)tgt0, (int)rb);
+    HIP_OR_FAIL(hipMemsetAsync(long_count, 0, sizeof(unsigned int), st));
+    hipLaunchKernelGGL(k_prep_scan, dim3((unsigned)nb), dim3(kPrepThreads), 0, st, R, db->err, O, w0, (long long)tgt0,
+                       (int)rb);
     hipLaunchKernelGGL(k_prep_reduce, dim3(1), dim3(kPrepThreads), 0, st, R, part, (int)nb, w0, (long long)tgt0, g_bound,
                        db->plan_info, static_cast<const PrepErr *>(db->err),
-                       spec ? (long long)db->region_per_incid : 0ll);
+                       spec ? (long long)db->region_per_incid : 0ll, static_cast<const unsigned int *>(long_count));
     if ((rc = check_launch(ctx, "k_prep_scan"))) return rc;
   }
   if (spec) return GANON_OK;   // the previous plan's mode, sizes and buffers; errors at download
   // 2. the one synchronization of a fresh batch: its first error and its shape
   unsigned long long info[6] = {0, 0, 0, 0, 0, 0};
   PrepErr e{};
+  unsigned int n_long = 0;
   HIP_OR_FAIL(hipMemcpyAsync(info, db->plan_info, sizeof info, hipMemcpyDeviceToHost, st));
   HIP_OR_FAIL(hipMemcpyAsync(&e, db->err, sizeof e, hipMemcpyDeviceToHost, st));
+  HIP_OR_FAIL(hipMemcpyAsync(&n_long, long_count, sizeof n_long, hipMemcpyDeviceToHost, st));
   HIP_OR_FAIL(hipStreamSynchronize(st));
+  if (!e.code && n_long) {
+    // reads with long CIGARs: a wave each, then the reduction again over both sets of partials
+    KernelScope ks(ctx, "prep_scan_long");
+    const unsigned gl = (unsigned)std::min<int64_t>(kLongGrid, ((int64_t)n_long + 3) / 4);
+    ScanOut OL = O;
+    OL.part = part + (size_t)kParts * nb;
+    hipLaunchKernelGGL(k_prep_scan_long, dim3(gl), dim3(kPrepThreads), 0, st, R, db->err, OL, (int)n_long);
+    hipLaunchKernelGGL(k_prep_reduce, dim3(1), dim3(kPrepThreads), 0, st, R, part, (int)(nb + gl), w0, (long long)tgt0,
+                       g_bound, db->plan_info, static_cast<const PrepErr *>(db->err), 0ll,
+                       static_cast<const unsigned int *>(long_count));
+    if ((rc = check_launch(ctx, "k_prep_scan_long"))) return rc;
+    HIP_OR_FAIL(hipMemcpyAsync(info, db->plan_info, sizeof info, hipMemcpyDeviceToHost, st));
+    HIP_OR_FAIL(hipMemcpyAsync(&e, db->err, sizeof e, hipMemcpyDeviceToHost, st));
+    HIP_OR_FAIL(hipStreamSynchronize(st));
+  }
   if (e.code) return fail(ctx, GANON_E_ARG, err_text(e.code), e.index, e.a, e.b);
   const unsigned long long max_len = info[3], max_seg = info[4];
   // prep mode: long (a read with several segments, or forced), one-segment (every read has at most

@@ -190,7 +190,11 @@ struct ganon_dbatch {
   int32_t *scope_calls = nullptr, *scope_bases = nullptr;
   unsigned long long *totals = nullptr, *static_totals = nullptr, *acc = nullptr, *far_count = nullptr;
   int32_t *counters = nullptr;          // [0] rare small (unused), [1] rare tiles
-  int32_t *status = nullptr;            // sticky device error bits (1: far-mask list overflow, 2: write-scope sums)
+  int32_t *status = nullptr;            // device status bits of the run (1: far-mask list overflow, 2: write-scope
+                                        // sums, 4: gated by the plan); cleared with the other flags per plan
+  unsigned int *long_count = nullptr;   // reads the scan left to k_prep_scan_long
+  unsigned long long *far_need = nullptr;   // far masks a run needed (k_finish)
+  size_t flags_bytes = 0;               // err .. far_need: one memset per plan
   ganon_dev::PrepErr *err = nullptr;
   unsigned long long *plan_info = nullptr;   // [0] I/D ops, [1] huge scopes, [2] written reads, [3] longest read,
                                              // [4] most segments of one read, [5] short-read groups,

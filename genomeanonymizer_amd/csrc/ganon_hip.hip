@@ -988,6 +988,7 @@ __global__ void __launch_bounds__(kBlock) k_finish(const unsigned long long *__r
                                                    const unsigned long long *__restrict__ static_totals,
                                                    int32_t *counters, unsigned long long *far_count,
                                                    int32_t *status, unsigned long long *acc,
+                                                   unsigned long long *far_need,
                                                    unsigned long long *totals,
                                                    const unsigned long long *__restrict__ ws_part,
                                                    const unsigned long long *__restrict__ plan_info) {
@@ -1056,11 +1057,11 @@ __global__ void __launch_bounds__(kBlock) k_finish(const unsigned long long *__r
   totals[GANON_T_MASKED_BASES] += sb;
   totals[GANON_T_RARE_SCOPES] += (unsigned long long)(atomicExch(&counters[0], 0) + atomicExch(&counters[1], 0));
   // more far masks than the list holds: the masks past it were dropped — ganon_batch_download grows
-  // the list to the count kept in acc[3] and runs the batch again
+  // the list to the count kept in far_need and runs the batch again
   const unsigned long long n_far_all = atomicExch(far_count, 0ull);
   if (n_far_all > (unsigned long long)far_cap) {
     atomicOr(status, 1);
-    atomicMax(&acc[3], n_far_all);
+    atomicMax(far_need, n_far_all);
   }
 }
 // One workgroup per 16 Ki-position tile of a large scope: tally -> TN table (global).
@@ -1400,9 +1401,7 @@ int host_copy(ganon_ctx *ctx, const ganon_dbatch *db, HostCopy &h) {
 // and the static totals (async).
 int prepare(ganon_ctx *ctx, ganon_dbatch *db, const ganon_batch *host, bool allow_spec = false) {
   int rc;
-  HIP_OR_FAIL(hipMemsetAsync(db->status, 0, sizeof(int32_t), ctx->stream));
-  HIP_OR_FAIL(hipMemsetAsync(db->acc + 3, 0, sizeof(unsigned long long), ctx->stream));
-  if ((rc = ganon_prep::plan(ctx, db, allow_spec))) return rc;
+  if ((rc = ganon_prep::plan(ctx, db, allow_spec))) return rc;   // (it clears the step's flags first)
   if (db->spec) {
     // the previous plan's tiles (none), aux pointers and static totals, unchanged on the host; copied
     // again (a reload clears the device's small state)
@@ -1502,7 +1501,10 @@ int load_batch(ganon_ctx *ctx, ganon_dbatch *db, const ganon_batch *b, const gan
   // small device state: totals, static totals, acc, far count, plan info (u64); counters, status;
   // the first validation error; the group kernels' aux pointers
   constexpr size_t kU64 = 8 + 8 + 5 + 1 + 8 + 4;
-  constexpr size_t kSmallBytes = kU64 * 8 + 8 * 4 + sizeof(PrepErr) + sizeof(GrpAux) + 64;
+  // the per-plan flags (first error, status bits, long-read count, far masks needed) are adjacent:
+  // one memset clears them at the start of every plan
+  constexpr size_t kFlags = sizeof(PrepErr) + 16;
+  constexpr size_t kSmallBytes = kU64 * 8 + 8 * 4 + kFlags + sizeof(GrpAux) + 64;
   uint8_t *sm = nullptr;
   if ((rc = ganon_prep::grow_n(ctx, db->b_small, kSmallBytes, &sm))) return rc;
   auto *u = reinterpret_cast<unsigned long long *>(sm);
@@ -1513,9 +1515,12 @@ int load_batch(ganon_ctx *ctx, ganon_dbatch *db, const ganon_batch *b, const gan
   db->plan_info = u + 22;
   db->paths = u + 30;
   db->counters = reinterpret_cast<int32_t *>(u + kU64);
-  db->status = db->counters + 4;
   db->err = reinterpret_cast<PrepErr *>(sm + kU64 * 8 + 8 * 4);
-  db->aux = reinterpret_cast<GrpAux *>(sm + kU64 * 8 + 8 * 4 + sizeof(PrepErr));
+  db->status = reinterpret_cast<int32_t *>(db->err + 1);
+  db->long_count = reinterpret_cast<unsigned int *>(db->status + 1);
+  db->far_need = reinterpret_cast<unsigned long long *>(db->long_count + 1);
+  db->flags_bytes = kFlags;
+  db->aux = reinterpret_cast<GrpAux *>(sm + kU64 * 8 + 8 * 4 + kFlags);
   HIP_OR_FAIL(hipMemsetAsync(sm, 0, kSmallBytes, ctx->stream));
   if ((rc = ganon_prep::grow_n(ctx, db->b_scope_calls, b->n_scopes, &db->scope_calls)) ||
       (rc = ganon_prep::grow_n(ctx, db->b_scope_bases, b->n_scopes, &db->scope_bases)) ||
@@ -1818,7 +1823,8 @@ GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
     k_finish<<<64, kBlock, 0, st>>>(static_cast<const unsigned long long *>(db->b_far.p), db->n_groups ? db->far_cap : 0,
                                     db->out, static_cast<const int32_t *>(db->b_grp_part.p), db->n_groups,
                                     db->large_ids, db->n_huge_scopes, db->scope_calls, db->scope_bases,
-                                    db->static_totals, db->counters, db->far_count, db->status, db->acc, db->totals,
+                                    db->static_totals, db->counters, db->far_count, db->status, db->acc, db->far_need,
+                                    db->totals,
                                     static_cast<const unsigned long long *>(db->b_wspart.p), db->plan_info);
     if ((rc = check_launch(ctx, "k_finish"))) return rc;
   }
@@ -1870,7 +1876,7 @@ GANON_API int ganon_batch_download(ganon_ctx *ctx, ganon_dbatch *db, uint8_t *se
   int32_t status = 0;
   unsigned long long far_need = 0;
   HIP_OR_FAIL(hipMemcpyAsync(&status, db->status, sizeof status, hipMemcpyDeviceToHost, st));
-  HIP_OR_FAIL(hipMemcpyAsync(&far_need, db->acc + 3, sizeof far_need, hipMemcpyDeviceToHost, st));
+  HIP_OR_FAIL(hipMemcpyAsync(&far_need, db->far_need, sizeof far_need, hipMemcpyDeviceToHost, st));
   HIP_OR_FAIL(hipStreamSynchronize(st));
   if (status & 4) {
     // a speculative replan the batch did not fit (a read with several segments, a longer read, a
@@ -1886,7 +1892,7 @@ GANON_API int ganon_batch_download(ganon_ctx *ctx, ganon_dbatch *db, uint8_t *se
     if (rc) return rc;
     if ((rc = ganon_prep::batch_error(ctx, db))) return rc;
     HIP_OR_FAIL(hipMemcpyAsync(&status, db->status, sizeof status, hipMemcpyDeviceToHost, st));
-    HIP_OR_FAIL(hipMemcpyAsync(&far_need, db->acc + 3, sizeof far_need, hipMemcpyDeviceToHost, st));
+    HIP_OR_FAIL(hipMemcpyAsync(&far_need, db->far_need, sizeof far_need, hipMemcpyDeviceToHost, st));
     HIP_OR_FAIL(hipStreamSynchronize(st));
   }
   if (status & 2) {
@@ -1907,7 +1913,7 @@ GANON_API int ganon_batch_download(ganon_ctx *ctx, ganon_dbatch *db, uint8_t *se
     db->aux_h.far_cap = cap;
     HIP_OR_FAIL(hipMemcpyAsync(db->aux, &db->aux_h, sizeof db->aux_h, hipMemcpyHostToDevice, st));
     HIP_OR_FAIL(hipMemsetAsync(db->status, 0, sizeof(int32_t), st));
-    HIP_OR_FAIL(hipMemsetAsync(db->acc + 3, 0, sizeof(unsigned long long), st));
+    HIP_OR_FAIL(hipMemsetAsync(db->far_need, 0, sizeof(unsigned long long), st));
     const bool prof = ctx->profiling;
     ctx->profiling = false;
     rc = ganon_batch_run(ctx, db);

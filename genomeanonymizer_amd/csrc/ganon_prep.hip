@@ -152,7 +152,8 @@ struct ScanOut {
   unsigned int *long_count;
   longlong2 *gmeta;           // [g_bound] first scope and incidence of each short-read group
   int64_t g_bound;            // group count bound: (n_incid + weight (n_scopes - 1)) / target + 1
-  unsigned long long *part;   // [kParts x blocks]
+  unsigned long long *part;   // [kParts][part_stride]: partial k of block b at part[k * part_stride + b]
+  int64_t part_stride;
 };
 
 __device__ __forceinline__ unsigned long long shfl64(unsigned long long v, int lane) {
@@ -160,7 +161,8 @@ __device__ __forceinline__ unsigned long long shfl64(unsigned long long v, int l
   return ((unsigned long long)hi << 32) | lo;
 }
 
-__device__ __forceinline__ void block_parts(unsigned long long (&acc)[kParts], unsigned long long *__restrict__ part) {
+__device__ __forceinline__ void block_parts(unsigned long long (&acc)[kParts], unsigned long long *__restrict__ part,
+                                            int64_t stride) {
   __shared__ unsigned long long ws[kWaves][kParts];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
@@ -179,7 +181,7 @@ __device__ __forceinline__ void block_parts(unsigned long long (&acc)[kParts], u
     unsigned long long v = 0;
     for (int w = 0; w < kWaves; ++w)
       v = (k == kPartMaxLen || k == kPartMaxSeg) ? (ws[w][k] > v ? ws[w][k] : v) : v + ws[w][k];
-    part[(int64_t)kParts * blockIdx.x + k] = v;
+    part[stride * k + blockIdx.x] = v;
   }
 }
 
@@ -334,7 +336,7 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_scan(const Raw R, PrepErr
       for (int64_t x = bp + 1; x <= b; ++x) O.gmeta[x] = m;
     }
   }
-  block_parts(acc, O.part);
+  block_parts(acc, O.part, O.part_stride);
 }
 
 // The long reads k_prep_scan listed (their read-level checks passed there), one wave each: read_end,
@@ -359,7 +361,7 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_scan_long(const Raw R, Pr
       acc[kPartIdOps] += (unsigned long long)W.nid;
     }
   }
-  block_parts(acc, O.part);
+  block_parts(acc, O.part, O.part_stride);
 }
 
 // plan_info: [0] I/D ops, [1] huge scopes, [2] written reads, [3] longest read, [4] most segments of
@@ -367,23 +369,26 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_scan_long(const Raw R, Pr
 // run's gate: nonzero when the one-segment kernels must not run — the scan found an invalid field,
 // or (speculative replan, spec_rpi > 0) the batch is not what the plan launched for: a read with
 // several segments, a longer read than the overflow regions were cut for, a huge scope.
-__global__ void __launch_bounds__(kPrepThreads) k_prep_reduce(const Raw R, const unsigned long long *__restrict__ part,
-                                                              int n_blocks, long long weight, long long target,
-                                                              int64_t g_bound, unsigned long long *__restrict__ info,
-                                                              const PrepErr *__restrict__ err, long long spec_rpi,
-                                                              const unsigned int *__restrict__ long_count) {
+constexpr int kReduceThreads = 1024;
+
+__global__ void __launch_bounds__(kReduceThreads) k_prep_reduce(const Raw R, const unsigned long long *__restrict__ part,
+                                                                int64_t stride, int n_blocks, long long weight,
+                                                                long long target, int64_t g_bound,
+                                                                unsigned long long *__restrict__ info,
+                                                                const PrepErr *__restrict__ err, long long spec_rpi,
+                                                                const unsigned int *__restrict__ long_count) {
+  // partials of one kind contiguous (block_parts): every load coalesced, 1024 threads in flight
   unsigned long long acc[kParts] = {0, 0, 0, 0, 0, 0};
-  for (int b = threadIdx.x; b < n_blocks; b += kPrepThreads) {
 #pragma unroll
-    for (int k = 0; k < kParts; ++k) {
-      const unsigned long long v = part[(int64_t)kParts * b + k];
+  for (int k = 0; k < kParts; ++k)
+    for (int b = threadIdx.x; b < n_blocks; b += kReduceThreads) {
+      const unsigned long long v = part[stride * k + b];
       acc[k] = (k == kPartMaxLen || k == kPartMaxSeg) ? (v > acc[k] ? v : acc[k]) : acc[k] + v;
     }
-  }
   __shared__ unsigned long long out[kParts];
-  // block_parts writes part[blockIdx.x = 0]: reduce into LDS instead
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  __shared__ unsigned long long ws[kWaves][kParts];
+  constexpr int kRW = kReduceThreads / 64;
+  __shared__ unsigned long long ws[kRW][kParts];
 #pragma unroll
   for (int k = 0; k < kParts; ++k) {
     unsigned long long v = acc[k];
@@ -398,7 +403,7 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_reduce(const Raw R, const
   if (threadIdx.x < kParts) {
     const int k = threadIdx.x;
     unsigned long long v = 0;
-    for (int w = 0; w < kWaves; ++w)
+    for (int w = 0; w < kRW; ++w)
       v = (k == kPartMaxLen || k == kPartMaxSeg) ? (ws[w][k] > v ? ws[w][k] : v) : v + ws[w][k];
     out[k] = v;
   }
@@ -586,16 +591,17 @@ __device__ void map_mark(const LineMap &M, unsigned long long key, uint32_t c) {
   }
 }
 
-// l1 / l2 from l0 (thread per l1 word).
+// l1 / l2 from l0: a wave per l1 word, one l0 word per lane, the l1 word is the wave's ballot.
 __global__ void __launch_bounds__(kPrepThreads) k_prep_linemap(LineMap M) {
-  for (int64_t w1 = blockIdx.x * (int64_t)kPrepThreads + threadIdx.x; w1 < M.n1; w1 += (int64_t)gridDim.x * kPrepThreads) {
-    unsigned long long b = 0;
-    for (int k = 0; k < 64; ++k) {
-      const int64_t w = (w1 << 6) + k;
-      if (w < M.n0 && M.l0[w]) b |= 1ull << k;
+  const int lane = threadIdx.x & 63;
+  const int64_t n_waves = (int64_t)gridDim.x * (kPrepThreads / 64);
+  for (int64_t w1 = (blockIdx.x * (int64_t)kPrepThreads + threadIdx.x) >> 6; w1 < M.n1; w1 += n_waves) {
+    const int64_t w = (w1 << 6) + lane;
+    const unsigned long long b = __ballot(w < M.n0 && M.l0[w] != 0);
+    if (lane == 0) {
+      M.l1[w1] = b;
+      if (b) atomicOr(&M.l2[w1 >> 6], 1ull << (w1 & 63));
     }
-    M.l1[w1] = b;
-    if (b) atomicOr(&M.l2[w1 >> 6], 1ull << (w1 & 63));
   }
 }
 
@@ -1390,7 +1396,7 @@ int launch_pieces(ganon_ctx *ctx, ganon_dbatch *db) {
   if (!db->n_groups) return GANON_OK;
   KernelScope ks(ctx, "prep_pieces");
   const LineMap M = line_map(db);
-  hipLaunchKernelGGL(k_prep_linemap, dim3(grid_for(M.n1)), dim3(kPrepThreads), 0, st, M);
+  hipLaunchKernelGGL(k_prep_linemap, dim3(grid_for(M.n1 * 64)), dim3(kPrepThreads), 0, st, M);
   hipLaunchKernelGGL(k_prep_pieces, dim3(grid_for(n_cand)), dim3(kPrepThreads), 0, st,
                      static_cast<const unsigned long long *>(db->b_lo.p), n_cand, M, db->seq_bytes,
                      static_cast<int4 *>(db->b_groups.p), db->flat_mode ? db->plan_info : nullptr);
@@ -1452,24 +1458,24 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db, bool allow_spec) {
   const int64_t sb = (ns + kScanScopesPerBlock - 1) / kScanScopesPerBlock;
   const int64_t nb = std::max<int64_t>(1, rb + sb);
   if (nb > INT32_MAX) return fail(ctx, GANON_E_ARG, "batch too large");
-  // partials: the scan's blocks, then up to kLongGrid blocks of k_prep_scan_long, then its counter
+  // partials (SoA, one row per kind): the scan's blocks, then up to kLongGrid blocks of k_prep_scan_long
   int32_t *long_list = nullptr;
   if ((rc = grow_n(ctx, db->b_gs0, (size_t)g_bound, &gm)) ||
-      (rc = grow_n(ctx, db->b_part, (size_t)kParts * (nb + kLongGrid) + 1, &part)) ||
+      (rc = grow_n(ctx, db->b_part, (size_t)kParts * (nb + kLongGrid), &part)) ||
       (rc = grow_n(ctx, db->b_long, (size_t)std::max<int64_t>(nr, 1), &long_list)))
     return rc;
-  auto *long_count = reinterpret_cast<unsigned int *>(part + (size_t)kParts * (nb + kLongGrid));
-  const ScanOut O{read_end, long_list, long_count, gm, g_bound, part};
+  unsigned int *long_count = db->long_count;
+  const int64_t pstride = nb + kLongGrid;
+  const ScanOut O{read_end, long_list, long_count, gm, g_bound, part, pstride};
   {
     // 1. the batch scan: every per-read and per-scope check, read ends, the group table of the
     //    short-read modes, per-block partials; then their reduction
     KernelScope ks(ctx, "prep_scan");
-    HIP_OR_FAIL(hipMemsetAsync(db->err, 0, sizeof(PrepErr), st));
-    HIP_OR_FAIL(hipMemsetAsync(long_count, 0, sizeof(unsigned int), st));
+    HIP_OR_FAIL(hipMemsetAsync(db->err, 0, db->flags_bytes, st));   // error, status, long reads, far need
     hipLaunchKernelGGL(k_prep_scan, dim3((unsigned)nb), dim3(kPrepThreads), 0, st, R, db->err, O, w0, (long long)tgt0,
                        (int)rb);
-    hipLaunchKernelGGL(k_prep_reduce, dim3(1), dim3(kPrepThreads), 0, st, R, part, (int)nb, w0, (long long)tgt0, g_bound,
-                       db->plan_info, static_cast<const PrepErr *>(db->err),
+    hipLaunchKernelGGL(k_prep_reduce, dim3(1), dim3(kReduceThreads), 0, st, R, part, pstride, (int)nb, w0, (long long)tgt0,
+                       g_bound, db->plan_info, static_cast<const PrepErr *>(db->err),
                        spec ? (long long)db->region_per_incid : 0ll, static_cast<const unsigned int *>(long_count));
     if ((rc = check_launch(ctx, "k_prep_scan"))) return rc;
   }
@@ -1487,10 +1493,10 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db, bool allow_spec) {
     KernelScope ks(ctx, "prep_scan_long");
     const unsigned gl = (unsigned)std::min<int64_t>(kLongGrid, ((int64_t)n_long + 3) / 4);
     ScanOut OL = O;
-    OL.part = part + (size_t)kParts * nb;
+    OL.part = part + nb;   // (blocks nb.. of every kind)
     hipLaunchKernelGGL(k_prep_scan_long, dim3(gl), dim3(kPrepThreads), 0, st, R, db->err, OL, (int)n_long);
-    hipLaunchKernelGGL(k_prep_reduce, dim3(1), dim3(kPrepThreads), 0, st, R, part, (int)(nb + gl), w0, (long long)tgt0,
-                       g_bound, db->plan_info, static_cast<const PrepErr *>(db->err), 0ll,
+    hipLaunchKernelGGL(k_prep_reduce, dim3(1), dim3(kReduceThreads), 0, st, R, part, pstride, (int)(nb + gl), w0,
+                       (long long)tgt0, g_bound, db->plan_info, static_cast<const PrepErr *>(db->err), 0ll,
                        static_cast<const unsigned int *>(long_count));
     if ((rc = check_launch(ctx, "k_prep_scan_long"))) return rc;
     HIP_OR_FAIL(hipMemcpyAsync(info, db->plan_info, sizeof info, hipMemcpyDeviceToHost, st));

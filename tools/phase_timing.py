@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--config", default="c2", help="bench.py workload (c2, c3, c5)")
     ap.add_argument("--reads", type=int, default=None)
     ap.add_argument("--genome", type=int, default=None)
+    ap.add_argument("--windows", type=int, default=None)
+    ap.add_argument("--germline", type=int, default=None)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--configs", default="0:1:0,0:2:0,0:2:1,0:2:2,0:2:4",
@@ -29,7 +31,6 @@ def main():
     args = ap.parse_args()
     from genomeanonymizer_amd import native
     import bench
-    args.windows = args.germline = None
     for k, v in bench.CONFIGS[args.config]["defaults"].items():
         if getattr(args, k) is None:
             setattr(args, k, v)

@@ -345,7 +345,7 @@ struct GrpSharedT {
   unsigned long long stk_lo[kGrpStack], stk_hi[kGrpStack];
   int stk_mode[kGrpStack];
   unsigned long long kmin, kmax;
-  int top, n_obs, n_patch;
+  int top, n_obs, n_patch, n_filt;
   int blk_calls, blk_bases;         // this workgroup's contribution to the totals
   int cnt_calls[kGrpMaxScopes];     // per-scope counts, written out once at the end
   int cnt_bases[kGrpMaxScopes];
@@ -423,11 +423,34 @@ __device__ __forceinline__ unsigned gtab_home(unsigned long long key, int tsize)
 template <class SH>
 __device__ __forceinline__ void grp_count(SH &sh, int s_local, int calls, int bases);
 
+// Per-dataset Bloom bitmaps of the pass's observation keys, in the patch list's LDS (unused while a
+// pass scans): a key seen in only one dataset can never be a TN call, so a list that overflows the
+// LDS list is first filtered by them (grp_filter) — a 60x scope's sequencing errors, which are
+// almost all single-dataset, then mostly drop out and the rest fits in LDS.
+constexpr int kBloomBits = 16384;   // per dataset: the two take the 4 KiB of the 512-entry patch list
+__device__ __forceinline__ uint32_t bloom_hash(unsigned long long key) {
+  return (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> 40);
+}
+template <class SH>
+__device__ __forceinline__ uint32_t *bloom_of(SH &sh) {
+  static_assert(sizeof(sh.patch) * 8 >= 2 * kBloomBits, "Bloom bitmaps live in the patch list");
+  return reinterpret_cast<uint32_t *>(sh.patch);
+}
+template <class SH>
+__device__ __forceinline__ bool bloom_both(SH &sh, unsigned long long key) {
+  const uint32_t h = bloom_hash(key) & (kBloomBits - 1), *b = bloom_of(sh);
+  return ((b[h >> 5] & b[(kBloomBits + h) >> 5]) >> (h & 31)) & 1u;
+}
+
 // payload: nibble index:48 | ref:4 | dataset:1 | mine:1
 template <class SH>
 __device__ __forceinline__ void grp_observe(SH &sh, const GrpRange &R, const GrpGlobal &gg,
                                             unsigned long long key, int64_t nib, int rc, int ds, uint32_t mine) {
   if (key < R.lo || key >= R.hi) return;
+  {
+    const uint32_t h = (bloom_hash(key) & (kBloomBits - 1)) + (uint32_t)ds * kBloomBits;
+    atomicOr(bloom_of(sh) + (h >> 5), 1u << (h & 31));
+  }
   const unsigned long long pay = (unsigned long long)nib | ((unsigned long long)rc << 48) |
                                  ((unsigned long long)ds << 52) | ((unsigned long long)mine << 53);
   const int k = atomicAdd(&sh.n_obs, 1);
@@ -698,6 +721,66 @@ __device__ __forceinline__ void grp_classify(const GrpBatch &B, SH &sh, int n, i
   }
 }
 
+// An overflowing list (n > OBS: OBS in LDS, the rest in the group's global region) filtered by the
+// pass's Bloom bitmaps: the LDS list is compacted in place to its keys seen in both datasets (a key
+// seen in one can never be a TN call; the bitmaps have no false negatives), the region's surviving
+// observations are appended after it as far as OBS. Returns all survivors; sh.n_obs = the LDS
+// list's. The region itself is left as it was.
+template <class SH>
+__device__ __forceinline__ int grp_filter(SH &sh, const GrpGlobal &gg, int n) {
+  constexpr int kPer = SH::kObs / kGrpThreads;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  __builtin_amdgcn_s_waitcnt(0);   // the scan's region stores at L2
+  __syncthreads();
+  unsigned long long k[kPer], p[kPer];
+  bool keep[kPer];
+  int cnt = 0;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int i = tid + j * kGrpThreads;
+    k[j] = sh.key[i];
+    p[j] = sh.pay[i];
+    keep[j] = bloom_both(sh, k[j]);
+    cnt += keep[j] ? 1 : 0;
+  }
+  int incl = cnt;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int x = __shfl_up(incl, o);
+    if (lane >= o) incl += x;
+  }
+  if (lane == 63) sh.wsum[wave] = incl;
+  if (tid == 0) sh.n_filt = 0;
+  __syncthreads();   // (every thread holds its entries: the list can be rewritten)
+  int base = incl - cnt, total = 0;
+#pragma unroll
+  for (int w = 0; w < kGrpThreads / 64; ++w) {
+    const int v = sh.wsum[w];
+    base += w < wave ? v : 0;
+    total += v;
+  }
+#pragma unroll
+  for (int j = 0; j < kPer; ++j)
+    if (keep[j]) {
+      sh.key[base] = k[j];
+      sh.pay[base] = p[j];
+      ++base;
+    }
+  if (tid == 0) sh.n_obs = total;
+  GU64 *okey = gp(gg.aux->okey) + gg.off, *opay = gp(gg.aux->opay) + gg.off;
+  for (int i = opaque_tid(); i < n - SH::kObs; i += kGrpThreads) {
+    const unsigned long long key = ld_l2(okey + i);
+    if (!bloom_both(sh, key)) continue;
+    const int slot = total + atomicAdd(&sh.n_filt, 1);
+    if (slot < SH::kObs) {
+      sh.key[slot] = key;
+      sh.pay[slot] = ld_l2(opay + i);
+    }
+  }
+  __syncthreads();
+  return total + sh.n_filt;
+}
+
 // Overflow path: n observations of one key range sit in the group's global region. Aggregate
 // them in a hash table of distinct keys (workgroup-scope atomics in L2), count the TN calls
 // (minus the kept variant), and mask the observations of reads the scopes write.
@@ -899,6 +982,7 @@ __global__ void __launch_bounds__(kGrpThreads, (OBS > 512 ? 4 : U == 1 ? 6 : U =
       break;
     }
     const GrpRange R{sh.stk_lo[top], sh.stk_hi[top], sh.stk_mode[top]};
+    for (int i = tid; i < 2 * kBloomBits / 32; i += kGrpThreads) bloom_of(sh)[i] = 0u;
     __syncthreads();
     if (tid == 0) {
       sh.top = top - 1;
@@ -915,15 +999,38 @@ __global__ void __launch_bounds__(kGrpThreads, (OBS > 512 ? 4 : U == 1 ? 6 : U =
     }
     // (grp_scan ends on a barrier)
     if (skip & kSkipClassify) continue;
-    const int n = sh.n_obs;
+    int n = sh.n_obs;
     if (tid == 0 && n > kGrpQuad)   // path counters (ganon_batch_path_counts): sorted list, region, split
       __hip_atomic_fetch_add(gp(aux->paths) + (n <= OBS ? 0 : n <= gg.cap ? 1 : 2), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (n > OBS) {
       if (n <= gg.cap) {
-        // the list joins the region's tail: n observations contiguous in the region
-        for (int i = opaque_tid(); i < OBS; i += kGrpThreads) {
-          gp(aux->okey)[gg.off + (n - OBS) + i] = sh.key[i];
-          gp(aux->opay)[gg.off + (n - OBS) + i] = sh.pay[i];
+        // drop the observations whose key was not seen in both datasets (Bloom bitmaps): when the
+        // rest fits in the LDS list, it is classified there like a short list
+        const int m = grp_filter(sh, gg, n);
+        if (m <= OBS) {
+          if (tid == 0)   // (counted as a region pass above too)
+            __hip_atomic_fetch_add(gp(aux->paths) + 3, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          grp_classify(B, sh, m, s_begin, sink, true);
+          if (sink.lds) {
+            __builtin_amdgcn_s_waitcnt(0);
+            __syncthreads();
+            const int np = sh.n_patch;
+            if (np) {
+              lds_bitonic(sh.patch, nullptr, np);
+              grp_patch_bytes(B, sh, np, out);
+              __builtin_amdgcn_s_waitcnt(0);
+            }
+            if (tid == 0) sh.n_patch = 0;
+          }
+          continue;
+        }
+        // the list (its kept part: m - survivors of the region beyond it) joins the region's
+        // tail: the region's own entries are untouched
+        const int ml = sh.n_obs;   // (grp_filter: the kept part of the LDS list)
+        n = (n - OBS) + ml;
+        for (int i = opaque_tid(); i < ml; i += kGrpThreads) {
+          gp(aux->okey)[gg.off + (n - ml) + i] = sh.key[i];
+          gp(aux->opay)[gg.off + (n - ml) + i] = sh.pay[i];
         }
         __builtin_amdgcn_s_waitcnt(0);   // region stores at L2 before the barrier
         __syncthreads();

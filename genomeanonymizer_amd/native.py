@@ -682,7 +682,8 @@ class DeviceBatch:
         """ganon_batch_path_counts: the group kernel's rarer paths taken since upload."""
         a = np.zeros(4, np.int64)
         self.m._check(self.m._lib.ganon_batch_path_counts(self.m._h, self.h, _ptr(a, _i64p)), "path_counts")
-        return {"sorted_lists": int(a[0]), "region_passes": int(a[1]), "key_range_splits": int(a[2])}
+        return {"sorted_lists": int(a[0]), "overflowing_lists": int(a[1]), "key_range_splits": int(a[2]),
+                "filtered_into_lds": int(a[3])}
 
     def indel_tally(self, arrays: dict) -> "DeviceIndels":
         """Plan the germline indel tally of this batch (``arrays`` = the batch it was uploaded from)."""

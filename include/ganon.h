@@ -224,8 +224,9 @@ GANON_API int ganon_batch_info(ganon_dbatch *db, int64_t *info8);
  * 2 one-segment)]. Since ABI 4. */
 GANON_API int ganon_batch_shape(ganon_dbatch *db, int64_t *shape4);
 /* How often the group kernel took its rarer paths since upload (synchronous): [lists of more than
- * 256 observations classified after an LDS sort, lists of more than 512 classified from the
- * group's global overflow region, key-range splits of an overflowing region, 0]. */
+ * 256 observations classified after an LDS sort, lists of more than 512 (overflowing into the
+ * group's global region), key-range splits of an overflowing region, overflowing lists the Bloom
+ * filter brought back into LDS (no region pass)]. */
 GANON_API int ganon_batch_path_counts(ganon_ctx *ctx, ganon_dbatch *db, int64_t *out4);
 
 /* ---- FASTQ record formatter ------------------------------------------

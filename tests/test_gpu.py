@@ -139,7 +139,7 @@ def test_dense_scopes_match_oracle(masker, oracle, seed, keep, err):
     assert np.array_equal(calls, o_calls)
     assert np.array_equal(bases, o_bases)
     assert np.array_equal(out, o_out)
-    assert paths["region_passes"] > 0, paths
+    assert paths["overflowing_lists"] > 0, paths
     assert (paths["key_range_splits"] > 0) == (err > 0.04), paths
 
 
@@ -219,7 +219,29 @@ def test_hip_configs2_density_matches_oracle(masker, oracle):
         assert np.array_equal(bases, o_bases), obs
         assert np.array_equal(out, o_out), obs
     assert o_bases.sum() > 100_000
-    assert runs[512][4]["region_passes"] > 0, runs[512][4]
+    assert runs[512][4]["overflowing_lists"] > 0, runs[512][4]
+
+
+def test_hip_deep_coverage_filter_matches_oracle(masker, oracle):
+    """SURVEY C3 density (60x tumor + normal, a germline het SNP per kb, 0.1 % sequencing errors,
+    a window every 10 kb): gap union scopes of ~4,000 reads overflow the 512-entry LDS list; the
+    pass's Bloom bitmaps drop the single-dataset keys (sequencing errors) and most such lists are
+    classified in LDS instead of the global region (GrpShared patch area reused)."""
+    from genomeanonymizer_amd.synth.batch import config2_batch
+    arr, info = config2_batch(n_reads=2_000_000, genome=5_000_000, n_contigs=2, n_windows=500,
+                              n_germline=5_000, seed=31, window_spacing=10_000)
+    o_out, o_calls, o_bases, _ = oracle.mask(arr)
+    db = masker.upload(arr)
+    try:
+        db.run()
+        out, calls, bases, _ = db.download()
+        paths = db.path_counts()
+    finally:
+        db.free()
+    assert np.array_equal(calls, o_calls)
+    assert np.array_equal(bases, o_bases)
+    assert np.array_equal(out, o_out)
+    assert paths["overflowing_lists"] > 0 and paths["filtered_into_lds"] > 0, paths
 
 
 @pytest.mark.parametrize("whole", [False, True], ids=["streaming", "whole_sample"])

@@ -427,6 +427,9 @@ __device__ __forceinline__ void grp_count(SH &sh, int s_local, int calls, int ba
 // pass scans): a key seen in only one dataset can never be a TN call, so a list that overflows the
 // LDS list is first filtered by them (grp_filter) — a 60x scope's sequencing errors, which are
 // almost all single-dataset, then mostly drop out and the rest fits in LDS.
+#ifndef GANON_GRP_BLOOM
+#define GANON_GRP_BLOOM 1   // 0: no Bloom filtering (A/B builds)
+#endif
 constexpr int kBloomBits = 16384;   // per dataset: the two take the 4 KiB of the 512-entry patch list
 __device__ __forceinline__ uint32_t bloom_hash(unsigned long long key) {
   return (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> 40);
@@ -447,7 +450,7 @@ template <class SH>
 __device__ __forceinline__ void grp_observe(SH &sh, const GrpRange &R, const GrpGlobal &gg,
                                             unsigned long long key, int64_t nib, int rc, int ds, uint32_t mine) {
   if (key < R.lo || key >= R.hi) return;
-  {
+  if (GANON_GRP_BLOOM) {
     const uint32_t h = (bloom_hash(key) & (kBloomBits - 1)) + (uint32_t)ds * kBloomBits;
     atomicOr(bloom_of(sh) + (h >> 5), 1u << (h & 31));
   }
@@ -982,7 +985,8 @@ __global__ void __launch_bounds__(kGrpThreads, (OBS > 512 ? 4 : U == 1 ? 6 : U =
       break;
     }
     const GrpRange R{sh.stk_lo[top], sh.stk_hi[top], sh.stk_mode[top]};
-    for (int i = tid; i < 2 * kBloomBits / 32; i += kGrpThreads) bloom_of(sh)[i] = 0u;
+    if (GANON_GRP_BLOOM)
+      for (int i = tid; i < 2 * kBloomBits / 32; i += kGrpThreads) bloom_of(sh)[i] = 0u;
     __syncthreads();
     if (tid == 0) {
       sh.top = top - 1;
@@ -1006,7 +1010,7 @@ __global__ void __launch_bounds__(kGrpThreads, (OBS > 512 ? 4 : U == 1 ? 6 : U =
       if (n <= gg.cap) {
         // drop the observations whose key was not seen in both datasets (Bloom bitmaps): when the
         // rest fits in the LDS list, it is classified there like a short list
-        const int m = grp_filter(sh, gg, n);
+        const int m = GANON_GRP_BLOOM ? grp_filter(sh, gg, n) : OBS + 1;
         if (m <= OBS) {
           if (tid == 0)   // (counted as a region pass above too)
             __hip_atomic_fetch_add(gp(aux->paths) + 3, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1026,7 +1030,7 @@ __global__ void __launch_bounds__(kGrpThreads, (OBS > 512 ? 4 : U == 1 ? 6 : U =
         }
         // the list (its kept part: m - survivors of the region beyond it) joins the region's
         // tail: the region's own entries are untouched
-        const int ml = sh.n_obs;   // (grp_filter: the kept part of the LDS list)
+        const int ml = GANON_GRP_BLOOM ? sh.n_obs : OBS;   // (grp_filter: the kept part of the LDS list)
         n = (n - OBS) + ml;
         for (int i = opaque_tid(); i < ml; i += kGrpThreads) {
           gp(aux->okey)[gg.off + (n - ml) + i] = sh.key[i];

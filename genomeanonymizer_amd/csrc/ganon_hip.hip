@@ -423,10 +423,11 @@ __device__ __forceinline__ unsigned gtab_home(unsigned long long key, int tsize)
 template <class SH>
 __device__ __forceinline__ void grp_count(SH &sh, int s_local, int calls, int bases);
 
-// Per-dataset Bloom bitmaps of the pass's observation keys, in the patch list's LDS (unused while a
-// pass scans): a key seen in only one dataset can never be a TN call, so a list that overflows the
-// LDS list is first filtered by them (grp_filter) — a 60x scope's sequencing errors, which are
-// almost all single-dataset, then mostly drop out and the rest fits in LDS.
+// Per-dataset Bloom bitmaps of an overflowing pass's observation keys, built from the stored
+// observations in the patch list's LDS (unused until the classification): a key seen in only one
+// dataset can never be a TN call, so a list that overflows the LDS list is first filtered by them
+// (grp_filter) — a 60x scope's sequencing errors, almost all single-dataset, then mostly drop out
+// and the rest fits in LDS. Passes that do not overflow (every configs[1] group) pay nothing.
 #ifndef GANON_GRP_BLOOM
 #define GANON_GRP_BLOOM 1   // 0: no Bloom filtering (A/B builds)
 #endif
@@ -450,10 +451,6 @@ template <class SH>
 __device__ __forceinline__ void grp_observe(SH &sh, const GrpRange &R, const GrpGlobal &gg,
                                             unsigned long long key, int64_t nib, int rc, int ds, uint32_t mine) {
   if (key < R.lo || key >= R.hi) return;
-  if (GANON_GRP_BLOOM) {
-    const uint32_t h = (bloom_hash(key) & (kBloomBits - 1)) + (uint32_t)ds * kBloomBits;
-    atomicOr(bloom_of(sh) + (h >> 5), 1u << (h & 31));
-  }
   const unsigned long long pay = (unsigned long long)nib | ((unsigned long long)rc << 48) |
                                  ((unsigned long long)ds << 52) | ((unsigned long long)mine << 53);
   const int k = atomicAdd(&sh.n_obs, 1);
@@ -730,10 +727,21 @@ __device__ __forceinline__ void grp_classify(const GrpBatch &B, SH &sh, int n, i
 // observations are appended after it as far as OBS. Returns all survivors; sh.n_obs = the LDS
 // list's. The region itself is left as it was.
 template <class SH>
-__device__ __forceinline__ int grp_filter(SH &sh, const GrpGlobal &gg, int n) {
+__device__ __attribute__((noinline)) int grp_filter(SH &sh, const GrpGlobal &gg, int n) {
   constexpr int kPer = SH::kObs / kGrpThreads;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  GU64 *okey = gp(gg.aux->okey) + gg.off, *opay = gp(gg.aux->opay) + gg.off;
+  uint32_t *bloom = bloom_of(sh);
+  for (int i = tid; i < 2 * kBloomBits / 32; i += kGrpThreads) bloom[i] = 0u;
   __builtin_amdgcn_s_waitcnt(0);   // the scan's region stores at L2
+  __syncthreads();
+  // the bitmaps: every stored observation's key, by dataset (payload bit 52)
+  for (int i = opaque_tid(); i < n; i += kGrpThreads) {
+    const unsigned long long key = i < SH::kObs ? sh.key[i] : ld_l2(okey + (i - SH::kObs));
+    const unsigned long long pay = i < SH::kObs ? sh.pay[i] : ld_l2(opay + (i - SH::kObs));
+    const uint32_t h = (bloom_hash(key) & (kBloomBits - 1)) + (uint32_t)((pay >> 52) & 1) * kBloomBits;
+    atomicOr(bloom + (h >> 5), 1u << (h & 31));
+  }
   __syncthreads();
   unsigned long long k[kPer], p[kPer];
   bool keep[kPer];
@@ -770,7 +778,6 @@ __device__ __forceinline__ int grp_filter(SH &sh, const GrpGlobal &gg, int n) {
       ++base;
     }
   if (tid == 0) sh.n_obs = total;
-  GU64 *okey = gp(gg.aux->okey) + gg.off, *opay = gp(gg.aux->opay) + gg.off;
   for (int i = opaque_tid(); i < n - SH::kObs; i += kGrpThreads) {
     const unsigned long long key = ld_l2(okey + i);
     if (!bloom_both(sh, key)) continue;
@@ -985,8 +992,6 @@ __global__ void __launch_bounds__(kGrpThreads, (OBS > 512 ? 4 : U == 1 ? 6 : U =
       break;
     }
     const GrpRange R{sh.stk_lo[top], sh.stk_hi[top], sh.stk_mode[top]};
-    if (GANON_GRP_BLOOM)
-      for (int i = tid; i < 2 * kBloomBits / 32; i += kGrpThreads) bloom_of(sh)[i] = 0u;
     __syncthreads();
     if (tid == 0) {
       sh.top = top - 1;

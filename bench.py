@@ -417,6 +417,8 @@ def main() -> None:
     ap.add_argument("--no-fastq", action="store_true", help="skip the FASTQ formatter measurement")
     ap.add_argument("--indel-sort", type=int, default=0, help="GANON_PARAM_INDEL_SORT: 0 segmented, 1 global")
     ap.add_argument("--fastq-kd", type=int, default=None, help="GANON_PARAM_FASTQ_KD (formatter kernel A/B)")
+    ap.add_argument("--pipeline", type=int, default=1,
+                    help="resident batches stepped round-robin, each in its own context and HIP stream")
     ap.add_argument("--spec-plan", type=int, default=1, help="GANON_PARAM_SPEC_PLAN: 1 speculative replans "
                     "(no host synchronization inside the step), 0 the replan waits for the scan")
     ap.add_argument("--prep-unroll", type=int, default=0, help="GANON_PARAM_PREP_UNROLL: incidences per thread "
@@ -481,6 +483,24 @@ def main() -> None:
     shape = db.shape()
     # germline indel tally: part of every step when the device scan found I/D ops
     ind = db.indel_tally(arr) if shape["id_ops"] else None
+    # --pipeline S: S resident batches, each in its own context on its own HIP stream, stepped
+    # round-robin: a batch's plan (latency-bound scan and emit) runs beside another's group kernel
+    # (bandwidth-bound). Every batch still gets its full fresh step; the timed region holds the
+    # same number of steps.
+    slots = [(masker, stream, db, ind)]
+    for _ in range(1, args.pipeline):
+        m2 = native.HipMasker(dev)
+        for prm, val in ((native.PARAM_GROUP_UNROLL, args.unroll), (native.PARAM_INDEL_SORT, args.indel_sort),
+                         (native.PARAM_PREP_UNROLL, args.prep_unroll), (native.PARAM_SPEC_PLAN, args.spec_plan)):
+            m2.set_param(prm, val)
+        if args.target:
+            m2.set_param(native.PARAM_GROUP_TARGET, args.target)
+        st2 = torch.cuda.Stream()
+        m2.set_stream(st2.cuda_stream)
+        r2 = m2.upload_reference(arr["ref_nt16"])
+        d2 = m2.upload({k: v for k, v in arr.items() if k != "ref_nt16"}, ref=r2)
+        slots.append((m2, st2, d2, d2.indel_tally(arr) if shape["id_ops"] else None))
+        slots[-1] = slots[-1] + (r2,)
     t_up = time.perf_counter() - t_up
     # totals all-reduce (RCCL) of every step, double-buffered: the reduction of step i runs beside
     # step i + 1's kernels; a buffer is reused only after its previous reduction completed
@@ -489,20 +509,22 @@ def main() -> None:
     host_reduce = dist is not None and dist.get_backend() != "nccl"
 
     def step(i: int):
+        _, st_i, db_i, ind_i = slots[i % len(slots)][:4]
         if not args.resident:
-            db.replan()     # a fresh batch: the plan from the raw arrays, every step
-        db.run()
-        if ind is not None:
-            ind.run()
+            db_i.replan()     # a fresh batch: the plan from the raw arrays, every step
+        db_i.run()
+        if ind_i is not None:
+            ind_i.run()
         if dist is not None:
             if host_reduce:
-                dist.all_reduce(torch.from_numpy(db.totals()))
+                dist.all_reduce(torch.from_numpy(db_i.totals()))
                 return
             b = i & 1
             if works[b] is not None:
                 works[b].wait()
-            db.copy_totals_to(tots[b].data_ptr())
-            works[b] = dist.all_reduce(tots[b], async_op=True)
+            with torch.cuda.stream(st_i):   # (the reduction is ordered after this batch's kernels)
+                db_i.copy_totals_to(tots[b].data_ptr())
+                works[b] = dist.all_reduce(tots[b], async_op=True)
 
     def drain():
         for b in range(2):
@@ -577,6 +599,14 @@ def main() -> None:
         job_totals = tots[0].cpu().numpy()
     else:
         job_totals = totals
+    for sl in slots[1:]:
+        if not (sl[2].totals() == totals).all():
+            raise RuntimeError("pipelined batches disagree")
+        if sl[3] is not None:
+            sl[3].free()
+        sl[2].free()
+        sl[4].free()
+        sl[0].close()
     db.free()
     ref.free()
 
@@ -627,7 +657,8 @@ def main() -> None:
                    "reads_per_gpu": info["reads"], "mean_read_len": round(mean_len, 1),
                    "scopes_per_gpu": info["scopes"], "incidences_per_gpu": info.get("incidences"),
                    "window_scopes": info.get("window_scopes"), "union_scopes": info.get("union_scopes"),
-                   "passthrough_reads": info.get("passthrough_reads"), "parallelism": f"contig-shard x{world}"},
+                   "passthrough_reads": info.get("passthrough_reads"), "parallelism": f"contig-shard x{world}",
+                   "pipeline": args.pipeline},
         "roofline": {"bound": "hbm", "kernel": "step: " + " + ".join(per_kernel), "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                      "traffic": traffic, "algorithmic_bytes_per_launch": alg_total,
@@ -640,7 +671,9 @@ def main() -> None:
         "step_kind": "resident batch, plan kept (run only)" if args.resident else
                      ("fresh batch: device plan (replan: validation scan, group table, shape checks) + run every "
                       "step; " + ("speculative replan (the run is enqueued behind the scan, which gates it)"
-                                  if args.spec_plan else "the replan waits for the scan")),
+                                  if args.spec_plan else "the replan waits for the scan")
+                      + (f"; {args.pipeline} resident batches stepped round-robin, each on its own HIP stream"
+                         if args.pipeline > 1 else "")),
         "run_only_ms_per_step": round(run_only_ms, 4) if run_only_ms else None,
         "batch_shape": shape,
         "pass": {"kernel_ms": round(pass_ms, 4), "algorithmic_bytes": alg_total,

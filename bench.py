@@ -417,7 +417,7 @@ def main() -> None:
     ap.add_argument("--no-fastq", action="store_true", help="skip the FASTQ formatter measurement")
     ap.add_argument("--indel-sort", type=int, default=0, help="GANON_PARAM_INDEL_SORT: 0 segmented, 1 global")
     ap.add_argument("--fastq-kd", type=int, default=None, help="GANON_PARAM_FASTQ_KD (formatter kernel A/B)")
-    ap.add_argument("--pipeline", type=int, default=1,
+    ap.add_argument("--pipeline", type=int, default=3,
                     help="resident batches stepped round-robin, each in its own context and HIP stream")
     ap.add_argument("--spec-plan", type=int, default=1, help="GANON_PARAM_SPEC_PLAN: 1 speculative replans "
                     "(no host synchronization inside the step), 0 the replan waits for the scan")
@@ -552,6 +552,17 @@ def main() -> None:
         dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
     dt = float(dt_t.item())
 
+    # the same steps on one batch and one stream (no overlap between batches), for comparison
+    one_stream_ms = None
+    if len(slots) > 1:
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for i in range(args.steps):
+            step(i * len(slots))
+        drain()
+        torch.cuda.synchronize()
+        one_stream_ms = (time.perf_counter() - t) / args.steps * 1e3
+
     # per-kernel durations: the same steps again with a HIP event pair around each launch
     masker.set_profiling(True)
     ktimes: dict = {}
@@ -675,6 +686,7 @@ def main() -> None:
                       + (f"; {args.pipeline} resident batches stepped round-robin, each on its own HIP stream"
                          if args.pipeline > 1 else "")),
         "run_only_ms_per_step": round(run_only_ms, 4) if run_only_ms else None,
+        "one_stream_ms_per_step": round(one_stream_ms, 4) if one_stream_ms else None,
         "batch_shape": shape,
         "pass": {"kernel_ms": round(pass_ms, 4), "algorithmic_bytes": alg_total,
                  "prep_ms": round(sum(v["avg_ms"] * v["launches"] for n, v in per_kernel.items()

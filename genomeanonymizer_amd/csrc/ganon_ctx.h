@@ -14,6 +14,9 @@
 
 #include "../../include/ganon.h"
 
+struct ganon_inflate_state;                       // ganon_inflate.hip: grow-only device buffers
+void ganon_inflate_free(ganon_inflate_state *st);
+
 struct ganon_ctx {
   int device = 0;
   hipStream_t own = nullptr;
@@ -43,6 +46,7 @@ struct ganon_ctx {
   // device blocks of released one-shot buffers (FASTQ formatter), reused by size on ctx->stream
   std::multimap<size_t, void *> dcache;
   size_t dcache_bytes = 0;
+  ganon_inflate_state *inflate = nullptr;   // BGZF inflate buffers (first ganon_inflate)
 };
 
 // A device block of at least `bytes` from the context's cache (at most 2x larger), else hipMalloc.

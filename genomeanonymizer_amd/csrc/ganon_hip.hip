@@ -1706,6 +1706,7 @@ GANON_API int ganon_ctx_destroy(ganon_ctx *ctx) {
   }
   for (auto e : ctx->pool) hipEventDestroy(e);
   for (auto &b : ctx->dcache) hipFree(b.second);
+  ganon_inflate_free(ctx->inflate);
   delete ctx;
   return GANON_OK;
 }

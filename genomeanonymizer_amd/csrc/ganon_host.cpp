@@ -421,6 +421,9 @@ struct ganon_bam_reader {
   std::vector<int64_t> index_end;    // per tid: virtual offset past its last record (-1 unknown)
   int64_t cur_voff = -1;             // forward cursor: the first record not yet consumed
   int32_t cur_tid = 0;
+  ganon_inflate_fn inflater = nullptr;   // ganon_bam_reader_set_inflater: block windows inflated by it
+  void *inflater_user = nullptr;
+  int64_t inflater_min = 64;             // ... when they hold at least this many blocks
 };
 
 namespace {
@@ -456,8 +459,22 @@ int64_t read_blocks(ganon_bam_reader *R, int64_t coff, int64_t step, RawVec<uint
   if (off == 0) return set_err("truncated BGZF block");
   const size_t base = data.size();
   data.resize(base + (size_t)total);
-  if (!inflate_blocks(comp.data(), blocks, 0, blocks.size(), data.data() + base, R->threads))
+  if (R->inflater && (int64_t)blocks.size() >= R->inflater_min) {
+    const size_t nb = blocks.size();
+    std::vector<int64_t> in_off(nb), out_off(nb);
+    std::vector<int32_t> in_len(nb), out_len(nb);
+    for (size_t i = 0; i < nb; ++i) {
+      in_off[i] = blocks[i].in_off;
+      in_len[i] = blocks[i].in_len;
+      out_off[i] = blocks[i].out_off;
+      out_len[i] = blocks[i].out_len;
+    }
+    if (R->inflater(R->inflater_user, comp.data(), off, in_off.data(), in_len.data(), out_off.data(), out_len.data(),
+                    (int64_t)nb, data.data() + base, total) != 0)
+      return set_err("BGZF inflate failed (inflater)");
+  } else if (!inflate_blocks(comp.data(), blocks, 0, blocks.size(), data.data() + base, R->threads)) {
     return set_err("BGZF inflate failed");
+  }
   for (size_t i = 0; i < blocks.size(); ++i) bmap.emplace_back((int64_t)base + blocks[i].out_off, bcoff[i]);
   return coff + off;
 }
@@ -647,6 +664,15 @@ GANON_HOST_API int ganon_bam_reader_open(const char *path, int threads, ganon_ba
 GANON_HOST_API int ganon_bam_reader_set_window(ganon_bam_reader *R, int64_t bytes) {
   if (!R) return set_err("null argument");
   R->chunk = std::max<int64_t>(bytes, 1 << 17);   // at least two maximal BGZF blocks
+  return 0;
+}
+
+GANON_HOST_API int ganon_bam_reader_set_inflater(ganon_bam_reader *R, ganon_inflate_fn fn, void *user,
+                                                 int64_t min_blocks) {
+  if (!R || min_blocks < 1) return set_err("ganon_bam_reader_set_inflater: bad arguments");
+  R->inflater = fn;
+  R->inflater_user = fn ? user : nullptr;
+  R->inflater_min = min_blocks;
   return 0;
 }
 

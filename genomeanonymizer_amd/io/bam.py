@@ -229,9 +229,10 @@ class BamReader:
     """One BAM file read a reference sequence at a time (``ganon_bam_reader``, include/
     ganon_host.h): the bounded-memory counterpart of ``ReadTable(path)``. ``contig(tid)`` returns a
     ReadTable of that sequence's records only (file order, full reference list); the reader seeks
-    through ``<bam>.bai`` when present, else streams forward."""
+    through ``<bam>.bai`` when present, else streams forward. ``inflater``: a native.GpuInflater
+    that inflates the reader's BGZF block windows instead of its zlib threads."""
 
-    def __init__(self, path: str, threads: int = 8, window: int = 0):
+    def __init__(self, path: str, threads: int = 8, window: int = 0, inflater=None):
         lib = native.host_lib()
         h = C.c_void_p()
         rc = lib.ganon_bam_reader_open(os.fsencode(path), int(threads), C.byref(h))
@@ -241,6 +242,9 @@ class BamReader:
         self.path = path
         if window:
             lib.ganon_bam_reader_set_window(h, int(window))
+        self.inflater = inflater   # (kept alive: the reader calls into its context)
+        if inflater is not None:   # a native.GpuInflater: block windows inflate on the GPU
+            lib.ganon_bam_reader_set_inflater(h, inflater.fn, inflater.handle, inflater.min_blocks)
         v = native.BamView()
         lib.ganon_bam_reader_header(h, C.byref(v))
         off = _arr(v.ref_name_off, v.n_ref, np.int64)

@@ -187,6 +187,8 @@ def hip_lib():
     lib.ganon_indel_download.restype = C.c_int64
     lib.ganon_indel_info.argtypes = [_p, _i64p]
     lib.ganon_indel_free.argtypes = [_p, _p]
+    lib.ganon_inflate.argtypes = [_p, _u8p, C.c_int64, _i64p, _i32p, _i64p, _i32p, C.c_int64, _u8p, C.c_int64,
+                                  _i64p]
     if lib.ganon_abi_version() != 4:
         raise GanonError("libganon_hip.so ABI version mismatch")
     _hip = lib
@@ -218,6 +220,7 @@ EXPORTED_HIP_SYMBOLS = (
     "ganon_fastq_upload", "ganon_fastq_run", "ganon_fastq_bytes", "ganon_fastq_device_output",
     "ganon_fastq_download", "ganon_fastq_free", "ganon_fastq_format_hip",
     "ganon_indel_upload", "ganon_indel_run", "ganon_indel_download", "ganon_indel_info", "ganon_indel_free",
+    "ganon_inflate", "ganon_inflate_hostcb",
 )
 EXPORTED_HOST_SYMBOLS = (
     "ganon_bam_open", "ganon_bam_view_get", "ganon_bam_error", "ganon_bam_close",
@@ -230,11 +233,65 @@ EXPORTED_HOST_SYMBOLS = (
     "ganon_blob_free", "ganon_objects_create", "ganon_objects_free", "ganon_objects_add_job", "ganon_objects_add_plain",
     "ganon_objects_run", "ganon_objects_take", "ganon_objects_settle", "ganon_objects_last_error",
     "ganon_objects_take_all", "ganon_aux_sa_count", "ganon_fastq_edit", "ganon_gather_ranges",
+    "ganon_bam_reader_set_inflater",
 )
 
 
 def _ptr(a: np.ndarray, ty):
     return a.ctypes.data_as(ty) if a is not None else None
+
+
+class GpuInflater:
+    """BGZF inflate on the GPU (``ganon_inflate``, include/ganon.h): a device
+    context of its own (own stream, own grow-only buffers), used by one thread at a time — the
+    BamReader decode thread hands it its block windows (``BamReader(..., inflater=)``)."""
+
+    def __init__(self, device: int = 0, min_blocks: int = 64):
+        lib = hip_lib()
+        self._lib = lib
+        h = _p()
+        if lib.ganon_ctx_create(int(device), C.byref(h)) != 0:
+            raise GanonError(f"ganon_ctx_create(device={device}) failed: no usable gfx950 device")
+        self._h = h
+        self.device = device
+        self.min_blocks = int(min_blocks)
+        self.fn = C.cast(lib.ganon_inflate_hostcb, _p)   # the reader's callback, user = the context
+
+    @property
+    def handle(self):
+        return self._h
+
+    def inflate(self, comp: np.ndarray, in_off: np.ndarray, in_len: np.ndarray, out_len: np.ndarray) -> np.ndarray:
+        """Inflate raw DEFLATE payloads comp[in_off[i]:+in_len[i]] (each to out_len[i] bytes),
+        concatenated; raises GanonError naming the first bad block."""
+        comp = np.ascontiguousarray(comp, np.uint8)
+        in_off = np.ascontiguousarray(in_off, np.int64)
+        in_len = np.ascontiguousarray(in_len, np.int32)
+        out_len = np.ascontiguousarray(out_len, np.int32)
+        out_off = np.zeros(len(out_len), np.int64)
+        if len(out_len) > 1:
+            np.cumsum(out_len[:-1], out=out_off[1:])
+        total = int(out_len.sum()) if len(out_len) else 0
+        out = np.empty(total, np.uint8)
+        bad = np.full(1, -1, np.int64)
+        rc = self._lib.ganon_inflate(self._h, _ptr(comp, _u8p), len(comp), _ptr(in_off, _i64p), _ptr(in_len, _i32p),
+                                     _ptr(out_off, _i64p), _ptr(out_len, _i32p), len(out_len), _ptr(out, _u8p),
+                                     total, _ptr(bad, _i64p))
+        if rc != 0:
+            msg = self._lib.ganon_last_error(self._h).decode(errors="replace")
+            raise GanonError(f"ganon_inflate failed ({rc}, block {int(bad[0])}): {msg}")
+        return out
+
+    def close(self) -> None:
+        if self._h:
+            self._lib.ganon_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class HipMasker:
@@ -1161,6 +1218,7 @@ def host_lib():
     lib.ganon_bam_reader_header.argtypes = [_p, C.POINTER(BamView)]
     lib.ganon_bam_reader_contig.argtypes = [_p, C.c_int32, C.POINTER(_p)]
     lib.ganon_bam_reader_close.argtypes = [_p]
+    lib.ganon_bam_reader_set_inflater.argtypes = [_p, _p, _p, C.c_int64]
     lib.ganon_host_last_error.restype = C.c_char_p
     lib.ganon_fastq_format.restype = C.c_int64
     lib.ganon_fastq_format.argtypes = [C.c_int64, C.POINTER(_u8p), _u8p, _i64p, _i32p, _u8p, C.POINTER(_u8p),

@@ -651,7 +651,13 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
             open(p, "wb").close()
     comm.barrier()
     fds = [os.open(p, os.O_WRONLY) for p in paths]
-    readers = (BamReader(tumor_bam, threads, window_bytes), BamReader(normal_bam, threads, window_bytes))
+    # GANON_GPU_INFLATE=1: the decode thread's BGZF windows inflate on this rank's GPU (one context
+    # of its own, shared by both readers: they are only used by that thread, one at a time)
+    inflater = None
+    if os.environ.get("GANON_GPU_INFLATE", "0") == "1":
+        inflater = native.GpuInflater(anonymizer.device)
+    readers = (BamReader(tumor_bam, threads, window_bytes, inflater),
+               BamReader(normal_bam, threads, window_bytes, inflater))
     contigs = list(fasta.references)
     owner = assign_contigs(list(fasta.lengths), world)
     mine = [j for j in range(len(contigs)) if owner[j] == rank]

@@ -337,4 +337,19 @@ GANON_API int64_t ganon_indel_download(ganon_ctx *ctx, ganon_indels *t, ganon_in
 GANON_API int ganon_indel_info(const ganon_indels *t, int64_t *info8);
 GANON_API int ganon_indel_free(ganon_ctx *ctx, ganon_indels *t);
 
+/* ---- BGZF inflate (input decode offload) ---------------------------------
+ * Replaces the zlib inflate behind AlignmentFile.fetch / pileup (pileup_io.pyx:12-17 via htslib's
+ * bgzf_read): n_blocks raw DEFLATE payloads (RFC 1951; BGZF blocks, at most 64 KiB in and out each)
+ * at comp[in_off[i], + in_len[i]) inflate to out[out_off[i], + out_len[i]) (out_len = the block's
+ * ISIZE). Host buffers in and out (synchronous: H2D, one workgroup per block, D2H); the device
+ * buffers are kept by the context. GANON_E_ARG with *first_bad = the block when a stream is invalid
+ * or does not inflate to its ISIZE. ganon_inflate_hostcb has the host BAM reader's inflater
+ * signature (include/ganon_host.h ganon_bam_reader_set_inflater, user = the context). Since ABI 4. */
+GANON_API int ganon_inflate(ganon_ctx *ctx, const uint8_t *comp, int64_t comp_len, const int64_t *in_off,
+                            const int32_t *in_len, const int64_t *out_off, const int32_t *out_len,
+                            int64_t n_blocks, uint8_t *out, int64_t out_total, int64_t *first_bad);
+GANON_API int ganon_inflate_hostcb(void *ctx, const uint8_t *comp, int64_t comp_len, const int64_t *in_off,
+                                   const int32_t *in_len, const int64_t *out_off, const int32_t *out_len,
+                                   int64_t n_blocks, uint8_t *out, int64_t out_total);
+
 #endif /* GANON_H */

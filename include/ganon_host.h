@@ -74,6 +74,16 @@ GANON_HOST_API int ganon_bam_reader_open(const char *path, int threads, ganon_ba
 GANON_HOST_API int ganon_bam_reader_has_index(const ganon_bam_reader *reader);
 /* Compressed bytes read and inflated per step (default 32 MiB, at least 128 KiB). */
 GANON_HOST_API int ganon_bam_reader_set_window(ganon_bam_reader *reader, int64_t bytes);
+/* Block inflater for the reader's windows: inflates n_blocks raw DEFLATE payloads at
+ * comp[in_off[i], + in_len[i]) to out[out_off[i], + out_len[i]); 0 on success. The signature of
+ * ganon_inflate_hostcb (include/ganon.h: the GPU inflate, user = a ganon_ctx). Windows of at least
+ * min_blocks blocks go to it, smaller ones to the reader's zlib threads; fn NULL restores zlib for
+ * all. The reader is not thread-safe; neither need fn be for one reader. */
+typedef int (*ganon_inflate_fn)(void *user, const uint8_t *comp, int64_t comp_len, const int64_t *in_off,
+                                const int32_t *in_len, const int64_t *out_off, const int32_t *out_len,
+                                int64_t n_blocks, uint8_t *out, int64_t out_total);
+GANON_HOST_API int ganon_bam_reader_set_inflater(ganon_bam_reader *reader, ganon_inflate_fn fn, void *user,
+                                                 int64_t min_blocks);
 GANON_HOST_API int ganon_bam_reader_header(ganon_bam_reader *reader, ganon_bam_view *view);
 GANON_HOST_API int ganon_bam_reader_contig(ganon_bam_reader *reader, int32_t tid, ganon_bam **out);
 GANON_HOST_API void ganon_bam_reader_close(ganon_bam_reader *reader);

@@ -6,15 +6,18 @@
 // payloads here instead of to zlib on its threads (ganon_bam_reader_set_inflater).
 //
 // One 64-lane workgroup per block, and the wave decodes it as ONE decoder: Huffman decoding is a
-// serial bit stream, so every lane runs the same symbol loop on the same (wave-uniform, mostly
-// scalar) state, and the lanes split only the byte work — the payload is pulled into an 8 KiB LDS
-// ring 4 KiB at a time, an LZ77 match of length L is copied by all 64 lanes at once (periodic
-// source index w - dist + (j mod dist), so even an overlapping match has no intra-copy dependence)
-// and a stored block is copied straight from global memory. The 64 KiB output window stays in LDS
-// and is written out coalesced at the end. 76 KiB of LDS: two blocks decode per CU, 512 on the
-// chip. Stored, fixed- and dynamic-Huffman blocks; canonical codes through a 9-bit lookup table
-// with a bit-by-bit canonical walk for longer codes. Every read and write is range-checked: a
-// malformed stream sets the block's status and stops it, never faults.
+// serial bit stream, so every lane runs the same symbol loop on the same wave-uniform state (kept
+// in scalar registers, scalar branches: readfirstlane at the loop head tells the compiler so), and
+// the lanes split only the byte work. Per code: one LDS read of a 10-bit lookup table (a canonical
+// bit walk for longer codes); per ~57 bits, one LDS read of three payload dwords. The payload comes
+// through a 2 KiB LDS ring filled 1 KiB at a time by the lanes; the output goes through a 32 KiB
+// LDS ring (DEFLATE's whole back-reference window): a match of length L is copied by all lanes at
+// once (periodic source index w - dist + (j mod dist): even an overlapping match has no intra-copy
+// dependence), and every completed 4 KiB of the ring is written to the block's output by the lanes
+// (coalesced dword stores). ~39 KiB of LDS: four blocks decode per CU, 1024 on the chip — the
+// decoders are latency-bound, so the count of them in flight is the throughput. Stored, fixed-
+// and dynamic-Huffman blocks. Every read and write is range-checked (output against the block's
+// ISIZE): a malformed stream sets the block's status and stops it, never faults.
 // Written from RFC 1951 and the BGZF section of the SAM specification.
 #include <hip/hip_runtime.h>
 
@@ -30,10 +33,13 @@ using ganon_detail::check_launch;
 using ganon_detail::fail;
 
 constexpr int kInfThreads = 64;
-constexpr int kWin = 65536;          // BGZF: at most 64 KiB of output and of payload per block
-constexpr int kRing = 8192;          // payload ring (LDS), refilled kRing/2 bytes at a time
+constexpr int kWin = 65536;          // BGZF: at most 64 KiB of output per block
+constexpr int kRing = 2048;          // payload ring (LDS), refilled kRing/2 bytes at a time
 constexpr int kRingHalf = kRing / 2;
-constexpr int kFastBits = 9;         // Huffman lookup table width
+constexpr int kOutRing = 32768;      // output ring: DEFLATE's 32 KiB back-reference window
+constexpr int kFlush = 4096;         // output written out per completed chunk of the ring
+constexpr int kFastBits = 10;        // Huffman lookup table width
+constexpr uint32_t kFastMask = (1u << kFastBits) - 1;
 
 // Canonical Huffman code: counts per length, symbols by (length, value), a kFastBits lookup table
 // of (symbol | length << 9) for codes of at most kFastBits bits (0: longer code or none).
@@ -44,56 +50,85 @@ struct Huff {
 };
 
 struct InfShared {
-  uint8_t out[kWin];
+  uint8_t out[kOutRing];
   uint8_t ring[kRing];
   Huff lit, dist;
   uint16_t lens[19 + 288 + 32];   // code-length code, then literal/length + distance lengths
 };
 
-constexpr uint16_t kLenBase[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31, 35, 43, 51, 59, 67, 83, 99,
-                                   115, 131, 163, 195, 227, 258};
-constexpr uint8_t kLenExtra[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
-constexpr uint16_t kDistBase[30] = {1, 2, 3, 4, 5, 7, 9, 13, 17, 25, 33, 49, 65, 97, 129, 193, 257, 385, 513, 769,
-                                    1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
-constexpr uint8_t kDistExtra[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11,
-                                    12, 12, 13, 13};
 constexpr uint8_t kClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
 enum { kInfOk = 0, kInfBadBlock = 1, kInfBadCode = 2, kInfOverrun = 3, kInfBadDist = 4, kInfSize = 5 };
 
+// The decoder below is host-callable too (NL = 1 lane, no barriers): tools/inflate_host_check.cpp
+// runs the same code against zlib without a GPU.
+#if defined(__HIP_DEVICE_COMPILE__)
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+  return (uint64_t)(uint32_t)uni((int)(uint32_t)v) | ((uint64_t)(uint32_t)uni((int)(uint32_t)(v >> 32)) << 32);
+}
+// LDS operations of one wave complete in issue order, so a lane reading what another lane of the
+// same (single-wave) workgroup stored earlier needs only the compiler kept from reordering them
+#define INF_WAVE_ORDER() __asm__ __volatile__("" ::: "memory")
+#else
+inline int uni(int v) { return v; }
+inline uint64_t uni64(uint64_t v) { return v; }
+#define INF_WAVE_ORDER() ((void)0)
+#endif
+#define INF_FN __host__ __device__
 
 // LSB-first bit reader. Payload bytes [filled - kRing, filled) are in the LDS ring (index & mask);
 // top_up (wave-uniform: every lane calls it together) keeps at least kRingHalf bytes ahead of pos.
+template <int NL>
 struct Bits {
   const uint8_t *g;   // the block's payload in global memory
   uint8_t *ring;
   int n, pos, filled, lane;
   uint64_t buf;
   int cnt;
-  __device__ void top_up() {
+  INF_FN void top_up() {
     if (filled < n && filled - pos < kRingHalf) {
-      __syncthreads();   // earlier ring reads are done before their slots are overwritten
-      const int e = min(filled + kRingHalf, n);
-      for (int k = filled + lane; k < e; k += kInfThreads) ring[k & (kRing - 1)] = g[k];
+      INF_WAVE_ORDER();   // earlier ring reads are issued before their slots are overwritten
+      const int e = filled + kRingHalf < n ? filled + kRingHalf : n;
+      for (int k0 = filled; k0 < e; k0 += NL) {   // (a uniform loop: the state stays scalar)
+        const int k = k0 + lane;
+        if (k < e) ring[k & (kRing - 1)] = g[k];
+      }
       filled = e;
-      __syncthreads();
+      INF_WAVE_ORDER();
     }
   }
-  __device__ void refill() {
-    if (cnt > 56) return;
+  // Tops the bit buffer up to 57..64 bits (or the end of the payload) with one LDS round trip:
+  // the three aligned ring dwords under the next 8 bytes.
+  INF_FN void refill() {
+    if (cnt > 56 || pos >= n) return;
     top_up();
-    while (cnt <= 56 && pos < n) {
-      buf |= (uint64_t)(uint32_t)uni(ring[pos & (kRing - 1)]) << cnt;
-      ++pos;
-      cnt += 8;
-    }
+    const uint32_t *rw = reinterpret_cast<const uint32_t *>(ring);
+    constexpr int kWm = kRing / 4 - 1;
+    const int w = pos >> 2;
+    const uint32_t w0 = (uint32_t)uni((int)rw[w & kWm]), w1 = (uint32_t)uni((int)rw[(w + 1) & kWm]),
+                   w2 = (uint32_t)uni((int)rw[(w + 2) & kWm]);
+    const int sh = 8 * (pos & 3);
+    const uint64_t lo = (uint64_t)w0 | ((uint64_t)w1 << 32), hi = (uint64_t)w2;
+    const uint64_t v = sh ? (lo >> sh) | (hi << (64 - sh)) : lo;   // payload bytes pos .. pos + 7
+    int nb = (64 - cnt) >> 3;
+    if (nb > n - pos) nb = n - pos;
+    buf |= (nb == 8 ? v : v & ((1ull << (8 * nb)) - 1)) << cnt;
+    cnt += 8 * nb;
+    pos += nb;
   }
-  __device__ bool need(int k) {
+  INF_FN bool need(int k) {
     if (cnt < k) refill();
     return cnt >= k;
   }
-  __device__ uint32_t take(int k) {   // (need(k) checked by the caller)
+  // the decoder state is wave-uniform: say so to the compiler (scalar registers, scalar branches)
+  INF_FN void uniform() {
+    pos = uni(pos);
+    filled = uni(filled);
+    cnt = uni(cnt);
+    buf = uni64(buf);
+  }
+  INF_FN uint32_t take(int k) {   // (need(k) checked by the caller)
     const uint32_t v = k ? (uint32_t)(buf & ((1ull << k) - 1)) : 0u;
     buf >>= k;
     cnt -= k;
@@ -101,11 +136,13 @@ struct Bits {
   }
 };
 
-__device__ __forceinline__ uint32_t rev_bits(uint32_t v, int n) { return __builtin_bitreverse32(v) >> (32 - n); }
+INF_FN inline uint32_t rev_bits(uint32_t v, int n) { return __builtin_bitreverse32(v) >> (32 - n); }
 
 // Build h from n code lengths; false on an over-subscribed code (an incomplete one is allowed:
-// RFC 1951 permits a single distance code). Wave-uniform: every lane writes the same values.
-__device__ bool huff_build(Huff &h, const uint16_t *len, int n) {
+// RFC 1951 permits a single distance code). Counts and symbols: every lane writes the same values;
+// the lookup table: split over the lanes.
+template <int NL>
+__attribute__((noinline)) INF_FN bool huff_build(Huff &h, const uint16_t *len, int n, int lane) {
   uint32_t cnt[16];
   for (int l = 0; l < 16; ++l) cnt[l] = 0;
   for (int s = 0; s < n; ++s) {
@@ -128,25 +165,30 @@ __device__ bool huff_build(Huff &h, const uint16_t *len, int n) {
     const int l = uni(len[s]);
     if (l) h.symbol[offs[l]++] = (uint16_t)s;
   }
-  for (int i = 0; i < (1 << kFastBits); ++i) h.fast[i] = 0;
-  // canonical codes of lengths <= kFastBits into the table (bit-reversed: the stream's bit order)
+  for (int i = lane; i < (1 << kFastBits); i += NL) h.fast[i] = 0;
+  INF_WAVE_ORDER();
+  // canonical codes of lengths <= kFastBits into the table (bit-reversed: the stream's bit order);
+  // the 2^(kFastBits - l) entries of a code are split over the lanes
   int code = 0, idx = 0;
   for (int l = 1; l <= kFastBits; ++l) {
     for (uint32_t k = 0; k < cnt[l]; ++k, ++idx, ++code) {
       const uint32_t r = rev_bits((uint32_t)code, l);
       const uint16_t e = (uint16_t)(uni(h.symbol[idx]) | (l << 9));
-      for (uint32_t f = r; f < (1u << kFastBits); f += 1u << l) h.fast[f] = e;
+      for (uint32_t f = r + ((uint32_t)lane << l); f < (1u << kFastBits); f += (uint32_t)NL << l) h.fast[f] = e;
     }
     code <<= 1;
   }
+  INF_WAVE_ORDER();
   return true;
 }
 
-// One symbol; -1 on an invalid code or a stream that ends inside it.
-__device__ int huff_decode(const Huff &h, Bits &b) {
+// One symbol through the table (header code-length codes); -1 on an invalid code or a stream
+// that ends inside it.
+template <int NL>
+INF_FN int huff_decode(const Huff &h, Bits<NL> &b) {
   b.refill();
   if (b.cnt >= kFastBits || b.pos >= b.n) {
-    const int e = uni(h.fast[b.buf & ((1u << kFastBits) - 1)]);
+    const int e = uni(h.fast[b.buf & kFastMask]);
     const int l = e >> 9;
     if (l && l <= b.cnt) {
       b.take(l);
@@ -168,11 +210,58 @@ __device__ int huff_decode(const Huff &h, Bits &b) {
   return -1;
 }
 
-// Decode one block's payload (n bytes at g) into S.out; returns the bytes written or -status.
-// Wave-uniform: all 64 lanes run it together.
-__device__ int inflate_wave(InfShared &S, const uint8_t *g, int n, int lane) {
-  Bits b{g, S.ring, n, 0, 0, lane, 0ull, 0};
-  int w = 0;
+// A code the kFastBits table does not finish (longer, or near the end of the payload): the
+// canonical walk (RFC 1951 3.2.2) over the cnt valid bits of buf. Returns sym | length << 16, -1.
+__attribute__((noinline)) INF_FN int huff_slow(const Huff &h, uint64_t buf, int cnt) {
+  int code = 0, first = 0, index = 0;
+  for (int l = 1; l < 16 && l <= cnt; ++l) {
+    code |= (int)((buf >> (l - 1)) & 1);
+    const int count = uni(h.count[l]);
+    if (code - count < first) return uni(h.symbol[index + (code - first)]) | (l << 16);
+    index += count;
+    first += count;
+    first <<= 1;
+    code <<= 1;
+  }
+  return -1;
+}
+
+// Output bytes [from, to) of the ring to dst (the block's output), by the lanes.
+template <int NL>
+INF_FN void flush_out(const uint8_t *ring, uint8_t *dst, int from, int to, int lane) {
+  INF_WAVE_ORDER();   // the ring bytes (lane 0's literals, every lane's copies) are issued
+  // dword stores over the aligned middle when the chunk does not wrap the ring
+  int a = from;
+  const int a4 = (from + 3) & ~3, b4 = to & ~3;
+  const bool words = (((uintptr_t)(dst + a4)) & 3) == 0 && a4 < b4 &&
+                     (a4 & (kOutRing - 1)) + (b4 - a4) <= kOutRing;
+  if (words) {
+    for (int k0 = from; k0 < a4; k0 += NL) {
+      const int k = k0 + lane;
+      if (k < a4) dst[k] = ring[k & (kOutRing - 1)];
+    }
+    const uint32_t *rw = reinterpret_cast<const uint32_t *>(ring + (a4 & (kOutRing - 1)));
+    uint32_t *dw = reinterpret_cast<uint32_t *>(dst + a4);
+    const int nw = (b4 - a4) >> 2;
+    for (int k0 = 0; k0 < nw; k0 += NL) {
+      const int k = k0 + lane;
+      if (k < nw) dw[k] = rw[k];
+    }
+    a = b4;
+  }
+  for (int k0 = a; k0 < to; k0 += NL) {
+    const int k = k0 + lane;
+    if (k < to) dst[k] = ring[k & (kOutRing - 1)];
+  }
+}
+
+// Decode one block's payload (n bytes at g) into dst (cap = the block's ISIZE bytes, never more);
+// returns the bytes decoded or -status. Wave-uniform: all 64 lanes run it together.
+template <int NL>
+INF_FN int inflate_wave(InfShared &S, const uint8_t *g, int n, uint8_t *dst, int cap, int lane) {
+  Bits<NL> b{g, S.ring, n, 0, 0, lane, 0ull, 0};
+  constexpr int M = kOutRing - 1;
+  int w = 0, flushed = 0;
   for (;;) {
     if (!b.need(3)) return -kInfOverrun;
     const int final_ = (int)b.take(1);
@@ -182,24 +271,36 @@ __device__ int inflate_wave(InfShared &S, const uint8_t *g, int n, int lane) {
       if (!b.need(32)) return -kInfOverrun;
       const int ln = (int)b.take(16), nl = (int)b.take(16);
       if ((ln ^ 0xFFFF) != nl) return -kInfBadBlock;
-      if (w + ln > kWin) return -kInfSize;
+      if (w + ln > cap) return -kInfSize;
       int k = 0;
       for (; k < ln && b.cnt >= 8; ++k, ++w) {   // bytes already in the bit buffer
         const uint8_t v = (uint8_t)b.take(8);
-        if (lane == 0) S.out[w] = v;
+        if (lane == 0) S.out[w & M] = v;
       }
-      const int rest = ln - k;
+      int rest = ln - k;
       if (b.pos + rest > n) return -kInfOverrun;
-      for (int j = lane; j < rest; j += kInfThreads) S.out[w + j] = g[b.pos + j];
-      w += rest;
-      b.pos += rest;
+      while (rest > 0) {   // the rest from global memory, a flush chunk at a time
+        const int piece = rest < kFlush ? rest : kFlush;
+        for (int j0 = 0; j0 < piece; j0 += NL) {
+          const int j = j0 + lane;
+          if (j < piece) S.out[(w + j) & M] = g[b.pos + j];
+        }
+        w += piece;
+        b.pos += piece;
+        rest -= piece;
+        if (w - flushed >= kFlush) {
+          const int to = w & ~(kFlush - 1);
+          flush_out<NL>(S.out, dst, flushed, to, lane);
+          flushed = to;
+        }
+      }
       if (b.filled < b.pos) b.filled = b.pos;
     } else if (type == 1 || type == 2) {
       if (type == 1) {   // fixed codes
         for (int s = 0; s < 288; ++s) S.lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8;
         for (int s = 0; s < 30; ++s) S.lens[288 + s] = 5;
-        huff_build(S.lit, S.lens, 288);
-        huff_build(S.dist, S.lens + 288, 30);
+        huff_build<NL>(S.lit, S.lens, 288, lane);
+        huff_build<NL>(S.dist, S.lens + 288, 30, lane);
       } else {           // dynamic codes
         if (!b.need(14)) return -kInfOverrun;
         const int nlen = (int)b.take(5) + 257, ndist = (int)b.take(5) + 1, ncode = (int)b.take(4) + 4;
@@ -209,7 +310,7 @@ __device__ int inflate_wave(InfShared &S, const uint8_t *g, int n, int lane) {
           if (!b.need(3)) return -kInfOverrun;
           S.lens[kClOrder[i]] = (uint16_t)b.take(3);
         }
-        if (!huff_build(S.dist, S.lens, 19)) return -kInfBadCode;   // (the code-length code, in dist)
+        if (!huff_build<NL>(S.dist, S.lens, 19, lane)) return -kInfBadCode;   // (the code-length code, in dist)
         // the literal/length and distance code lengths, after the code-length code's 19 slots
         uint16_t *ll = S.lens + 19;
         int k = 0;
@@ -236,48 +337,118 @@ __device__ int inflate_wave(InfShared &S, const uint8_t *g, int n, int lane) {
           while (rep--) ll[k++] = (uint16_t)val;
         }
         if (uni(ll[256]) == 0) return -kInfBadCode;   // no end-of-block code
-        if (!huff_build(S.lit, ll, nlen)) return -kInfBadCode;
-        if (!huff_build(S.dist, ll + nlen, ndist)) return -kInfBadCode;
+        if (!huff_build<NL>(S.lit, ll, nlen, lane)) return -kInfBadCode;
+        if (!huff_build<NL>(S.dist, ll + nlen, ndist, lane)) return -kInfBadCode;
       }
+      // the symbol loop: errors leave it through `err` (a single exit, and only uniform inner
+      // loops, keep the control flow and so the state scalar)
+      const uint16_t *lfast = S.lit.fast, *dfast = S.dist.fast;
+      int err = 0;
       for (;;) {
-        const int sym = huff_decode(S.lit, b);
-        if (sym < 0) return -kInfBadCode;
-        if (sym < 256) {
-          if (w >= kWin) return -kInfSize;
-          if (lane == 0) S.out[w] = (uint8_t)sym;
-          ++w;
-          continue;
-        }
-        if (sym == 256) break;
-        const int li = sym - 257;
-        if (li >= 29) return -kInfBadCode;
-        if (!b.need(kLenExtra[li])) return -kInfOverrun;
-        const int len = kLenBase[li] + (int)b.take(kLenExtra[li]);
-        const int ds = huff_decode(S.dist, b);
-        if (ds < 0 || ds >= 30) return -kInfBadCode;
-        if (!b.need(kDistExtra[ds])) return -kInfOverrun;
-        const int dist = kDistBase[ds] + (int)b.take(kDistExtra[ds]);
-        if (dist > w) return -kInfBadDist;
-        if (w + len > kWin) return -kInfSize;
-        __syncthreads();   // lane 0's literals and the last copy are visible to every lane
-        const uint8_t *src = S.out + (w - dist);
-        if (dist >= len) {
-          for (int j = lane; j < len; j += kInfThreads) S.out[w + j] = src[j];
-        } else {           // overlapping: out[w + j] = out[w - dist + j mod dist]
-          int r = lane % dist;
-          const int step = kInfThreads % dist;
-          for (int j = lane; j < len; j += kInfThreads) {
-            S.out[w + j] = src[r];
-            r += step;
-            if (r >= dist) r -= dist;
+        b.uniform();
+        w = uni(w);
+        flushed = uni(flushed);
+        if (b.cnt < 15) b.refill();
+        int e = uni(lfast[b.buf & kFastMask]);
+        int l = e >> 9;
+        if (l == 0 || l > b.cnt) {
+          e = uni(huff_slow(S.lit, b.buf, b.cnt));
+          if (e < 0) {
+            err = kInfBadCode;
+            break;
           }
+          l = e >> 16;
         }
-        w += len;
+        const int sym = e & 511;
+        b.buf >>= l;
+        b.cnt -= l;
+        if (sym < 256) {
+          if (w >= cap) {
+            err = kInfSize;
+            break;
+          }
+#ifdef INF_MARK
+          __asm__ volatile("; MARK_LITERAL");
+#endif
+          if (lane == 0) S.out[w & M] = (uint8_t)sym;
+          ++w;
+        } else {
+          if (sym == 256) break;
+          const int li = sym - 257;
+          if (li >= 29) {
+            err = kInfBadCode;
+            break;
+          }
+          if (b.cnt < 33) b.refill();   // length extra (<= 5) + distance code (<= 15) + extra (<= 13)
+          // RFC 1951 3.2.5 length codes: base 3 + li below 8, then 4..7 << extra (+ 3); 258 alone
+          const int le = li < 8 || li == 28 ? 0 : (li - 4) >> 2;
+          const int lb = li < 8 ? 3 + li : li == 28 ? 258 : ((4 + (li & 3)) << le) + 3;
+          int d = uni(dfast[(b.buf >> le) & kFastMask]);
+          int dl = d >> 9;
+          if (b.cnt < le) {
+            err = kInfOverrun;
+            break;
+          }
+          const int len = lb + (int)(b.buf & ((1u << le) - 1));
+          b.buf >>= le;
+          b.cnt -= le;
+          if (dl == 0 || dl > b.cnt) {
+            d = uni(huff_slow(S.dist, b.buf, b.cnt));
+            if (d < 0) {
+              err = kInfBadCode;
+              break;
+            }
+            dl = d >> 16;
+          }
+          const int ds = d & 511;
+          b.buf >>= dl;
+          b.cnt -= dl;
+          // distance codes: base 1 + ds below 4, then 2..3 << extra (+ 1)
+          const int de = ds < 4 ? 0 : (ds - 2) >> 1;
+          if (ds >= 30 || b.cnt < de) {
+            err = ds >= 30 ? kInfBadCode : kInfOverrun;
+            break;
+          }
+          const int dist = (ds < 4 ? 1 + ds : ((2 + (ds & 1)) << de) + 1) + (int)(b.buf & ((1u << de) - 1));
+          b.buf >>= de;
+          b.cnt -= de;
+          if (dist > w || w + len > cap) {
+            err = dist > w ? kInfBadDist : kInfSize;
+            break;
+          }
+          INF_WAVE_ORDER();   // lane 0's literals and the last copy are read by every lane
+          if (dist >= len) {
+            for (int j0 = 0; j0 < len; j0 += NL) {
+              const int j = j0 + lane;
+              if (j < len) S.out[(w + j) & M] = S.out[(w - dist + j) & M];
+            }
+          } else {           // overlapping: out[w + j] = out[w - dist + j mod dist]
+            // lane mod dist, lane < 64 (exact: (lane + 1/2) / dist is >= 1/(2 dist) from an integer)
+            const int q = (int)(((float)lane + 0.5f) / (float)dist);
+            int r = lane - q * dist;
+            const int step = NL % dist;
+            for (int j0 = 0; j0 < len; j0 += NL) {
+              if (j0 + lane < len) S.out[(w + j0 + lane) & M] = S.out[(w - dist + r) & M];
+              r += step;
+              if (r >= dist) r -= dist;
+            }
+          }
+          w += len;
+        }
+        if (w - flushed >= kFlush) {   // (at most kFlush + 257 bytes are ever unflushed)
+          const int to = w & ~(kFlush - 1);
+          flush_out<NL>(S.out, dst, flushed, to, lane);
+          flushed = to;
+        }
       }
+      if (err) return -err;
     } else {
       return -kInfBadBlock;
     }
-    if (final_) return w;
+    if (final_) {
+      flush_out<NL>(S.out, dst, flushed, w, lane);
+      return w;
+    }
   }
 }
 
@@ -295,26 +466,14 @@ __global__ void __launch_bounds__(kInfThreads) k_inflate(const uint8_t *__restri
   for (int64_t i = blockIdx.x; i < n_blocks; i += gridDim.x) {
     const int64_t io = in_off[i], oo = out_off[i];
     const int il = in_len[i], ol = out_len[i];
-    const bool ok = io >= 0 && il >= 0 && il <= kWin && io + il <= comp_len && oo >= 0 && ol >= 0 && ol <= kWin &&
+    const bool ok = io >= 0 && il >= 0 && io + il <= comp_len && oo >= 0 && ol >= 0 && ol <= kWin &&
                     oo + ol <= out_total;
     if (!ok) {
       if (t == 0) status[i] = kInfSize;
       continue;
     }
-    const int r = inflate_wave(S, comp + io, il, t);
+    const int r = inflate_wave<kInfThreads>(S, comp + io, il, out + oo, ol, t);
     if (t == 0) status[i] = r < 0 ? -r : (r == ol ? kInfOk : kInfSize);
-    __syncthreads();
-    if (r == ol) {
-      uint8_t *o = out + oo;
-      int k0 = 0;
-      if ((oo & 3) == 0) {   // aligned: dword stores
-        const int n4 = ol >> 2;
-        for (int k = t; k < n4; k += kInfThreads)
-          reinterpret_cast<uint32_t *>(o)[k] = reinterpret_cast<const uint32_t *>(S.out)[k];
-        k0 = n4 << 2;
-      }
-      for (int k = k0 + t; k < ol; k += kInfThreads) o[k] = S.out[k];
-    }
     __syncthreads();   // (S is reused by the next block)
   }
 }
@@ -384,14 +543,24 @@ GANON_API int ganon_inflate(ganon_ctx *ctx, const uint8_t *comp, int64_t comp_le
       hipMemcpyAsync(st->out_len, out_len, nb * 4, hipMemcpyHostToDevice, s) != hipSuccess)
     return fail(ctx, GANON_E_DEVICE, "ganon_inflate: host-to-device copy failed");
   const unsigned grid = (unsigned)std::min<int64_t>(n_blocks, 1 << 16);
+  if (ctx->profiling) {   // a profiled call: ganon_last_kernel_times reports k_inflate alone
+    for (auto &r : ctx->recs) {
+      ctx->pool.push_back(r.e0);
+      ctx->pool.push_back(r.e1);
+    }
+    ctx->recs.clear();
+  }
+  {
+  ganon_detail::KernelScope ks(ctx, "k_inflate");
   hipLaunchKernelGGL(k_inflate, dim3(grid), dim3(kInfThreads), 0, s, st->comp, comp_len, st->in_off, st->in_len,
                      st->out_off, st->out_len, n_blocks, st->out, out_total, st->status);
+  }
   if ((rc = check_launch(ctx, "k_inflate"))) return rc;
   std::vector<int32_t> stat(nb);
   if (hipMemcpyAsync(out, st->out, (size_t)out_total, hipMemcpyDeviceToHost, s) != hipSuccess ||
-      hipMemcpyAsync(stat.data(), st->status, nb * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
-      hipStreamSynchronize(s) != hipSuccess)
+      hipMemcpyAsync(stat.data(), st->status, nb * 4, hipMemcpyDeviceToHost, s) != hipSuccess)
     return fail(ctx, GANON_E_DEVICE, "ganon_inflate: device-to-host copy failed");
+  if ((rc = ganon_batch_sync(ctx))) return rc;   // (collects the kernel time when profiling)
   for (size_t i = 0; i < nb; ++i)
     if (stat[i]) {
       if (first_bad) *first_bad = (int64_t)i;

@@ -261,6 +261,15 @@ class GpuInflater:
     def handle(self):
         return self._h
 
+    def set_profiling(self, on: bool) -> None:
+        self._lib.ganon_ctx_set_profiling(self._h, 1 if on else 0)
+
+    def kernel_ms(self) -> float:
+        """k_inflate's time in the last profiled inflate (HIP events on the context's stream)."""
+        arr = (KernelTime * 4)()
+        n = self._lib.ganon_last_kernel_times(self._h, arr, 4)
+        return sum(float(arr[i].ms) for i in range(min(n, 4)) if arr[i].name == b"k_inflate")
+
     def inflate(self, comp: np.ndarray, in_off: np.ndarray, in_len: np.ndarray, out_len: np.ndarray) -> np.ndarray:
         """Inflate raw DEFLATE payloads comp[in_off[i]:+in_len[i]] (each to out_len[i] bytes),
         concatenated; raises GanonError naming the first bad block."""

@@ -45,11 +45,11 @@ def _zlib_streams():
         b"",
         b"A",
         bytes(rng.integers(0, 256, 65536, dtype=np.uint8)),                      # incompressible
-        bytes(rng.choice(list(b"ACGTN"), 65536, p=[.3, .2, .2, .29, .01])),      # bases
+        rng.choice(np.frombuffer(b"ACGTN", np.uint8), 65536, p=[.3, .2, .2, .29, .01]).tobytes(),   # bases
         b"\x00" * 65536,                                                          # one long run
         (b"@read_%d\nACGTACGTTTGA\n+\nIIIIHHHG#\n" * 2500)[:65536],              # FASTQ-like repeats
         bytes(rng.integers(30, 42, 40000, dtype=np.uint8)),                      # qualities
-        bytes(np.repeat(rng.integers(0, 256, 3000, dtype=np.uint8), rng.integers(1, 40, 3000)))[:65536],
+        np.repeat(rng.integers(0, 256, 3000, dtype=np.uint8), rng.integers(1, 40, 3000)).tobytes()[:65536],
     ]
     out = []
     for t in texts:
@@ -59,7 +59,7 @@ def _zlib_streams():
             c = zlib.compressobj(level, zlib.DEFLATED, -15, 9, strategy)
             out.append((c.compress(t) + c.flush(), t))
     # several deflate blocks in one stream (flushes), a stored block between Huffman ones
-    t = bytes(rng.choice(list(b"ACGT"), 60000))
+    t = rng.choice(np.frombuffer(b"ACGT", np.uint8), 60000).tobytes()
     c = zlib.compressobj(6, zlib.DEFLATED, -15)
     parts = [c.compress(t[:20000]), c.flush(zlib.Z_FULL_FLUSH), c.compress(t[20000:40000]),
              c.flush(zlib.Z_SYNC_FLUSH), c.compress(t[40000:]), c.flush()]
@@ -127,6 +127,53 @@ def test_reader_inflater_hook_matches_zlib_threads(tmp_path):
     R.close()
 
 
+def _bad_cases(rng):
+    t = rng.choice(np.frombuffer(b"ACGT", np.uint8), 30000).tobytes()
+    good = zlib.compress(t, 6)[2:-4]
+    return t, good, [
+        (good, len(t) + 1),                                    # ISIZE disagrees
+        (good[:len(good) // 2], len(t)),                       # truncated
+        (b"\x07" + good[1:], len(t)),                          # BTYPE 3 (reserved)
+        (bytes([0x01, 0x05, 0x00, 0x00, 0x00]) + b"abcde", 5),  # stored LEN/NLEN mismatch
+        (bytes(rng.integers(0, 256, 4000, dtype=np.uint8)), 65536),   # noise
+    ]
+
+
+@pytest.fixture(scope="module")
+def host_check(tmp_path_factory):
+    """tools/inflate_host_check.cpp built with hipcc: the kernel's decoder source run on the host."""
+    import shutil
+    import subprocess
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("hipcc is not available")
+    root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+    exe = str(tmp_path_factory.mktemp("ihc") / "inflate_host_check")
+    subprocess.run([hipcc, "-O2", "-std=c++17", "--offload-arch=gfx950", "-x", "hip",
+                    os.path.join(root, "tools", "inflate_host_check.cpp"), "-o", exe], check=True)
+    d = tmp_path_factory.mktemp("ihc_io")
+
+    def run(streams):
+        comp, in_off, in_len, out_len = _soa(streams)
+        comp.tofile(d / "comp.bin")
+        meta = np.stack([in_off, in_len.astype(np.int64), out_len.astype(np.int64)], 1).ravel()
+        np.concatenate([[len(streams)], meta]).astype(np.int64).tofile(d / "meta.bin")
+        r = subprocess.run([exe, str(d / "comp.bin"), str(d / "meta.bin"), str(d / "out.bin")], check=True,
+                           capture_output=True, text=True)
+        return [int(x) for x in r.stdout.split()], open(d / "out.bin", "rb").read()
+    return run
+
+
+def test_decoder_source_matches_zlib_on_host(host_check):
+    streams = _zlib_streams()
+    status, out = host_check(streams)
+    assert status == [0] * len(streams)
+    assert out == b"".join(t for _, t in streams)
+    _, _, bad = _bad_cases(np.random.default_rng(3))
+    status, _ = host_check([(s, b"\x00" * n) for s, n in bad])
+    assert all(x != 0 for x in status)
+
+
 def test_zlib_streams_cover_every_block_type():
     """The fixture streams hold stored (BTYPE 0), fixed (1) and dynamic (2) first blocks."""
     kinds = {(s[0] >> 1) & 3 for s, _ in _zlib_streams() if s}
@@ -168,16 +215,7 @@ def test_gpu_inflate_real_bgzf_blocks(gpu_inflater, tmp_path):
 @pytest.mark.gpu
 def test_gpu_inflate_rejects_bad_streams(gpu_inflater):
     from genomeanonymizer_amd import native
-    rng = np.random.default_rng(3)
-    t = bytes(rng.choice(list(b"ACGT"), 30000))
-    good = zlib.compress(t, 6)[2:-4]
-    cases = [
-        (good, len(t) + 1),                                    # ISIZE disagrees
-        (good[:len(good) // 2], len(t)),                       # truncated
-        (b"\x07" + good[1:], len(t)),                          # BTYPE 3 (reserved)
-        (bytes([0x01, 0x05, 0x00, 0x00, 0x00]) + b"abcde", 5),  # stored LEN/NLEN mismatch
-        (bytes(rng.integers(0, 256, 4000, dtype=np.uint8)), 65536),   # noise
-    ]
+    t, good, cases = _bad_cases(np.random.default_rng(3))
     for k, (s, n) in enumerate(cases):
         streams = [(good, t), (s, b"\x00" * n)]
         comp, in_off, in_len, out_len = _soa(streams)

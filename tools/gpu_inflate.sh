@@ -12,7 +12,7 @@ tail -3 gpurun_out/inflate_tests.log
 timeout -k 10 300 python tools/inflate_bench.py ${INF_ARGS:-} > gpurun_out/inflate_bench.json 2> gpurun_out/inflate_bench.err \
   || { tail -20 gpurun_out/inflate_bench.err; exit 1; }
 cat gpurun_out/inflate_bench.json
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/inf_prof -o inf -- python3 tools/inflate_bench.py --no-cpu \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/inf_prof -o inf -- python3 tools/inflate_bench.py --no-cpu \
   > gpurun_out/inflate_prof.log 2>&1 || { tail -20 gpurun_out/inflate_prof.log; exit 1; }
 find gpurun_out/inf_prof -name '*kernel_stats.csv' -exec cat {} \;
 echo "exit=0"

@@ -90,10 +90,15 @@ struct Bits {
     if (filled < n && filled - pos < kRingHalf) {
       INF_WAVE_ORDER();   // earlier ring reads are issued before their slots are overwritten
       const int e = filled + kRingHalf < n ? filled + kRingHalf : n;
-      for (int k0 = filled; k0 < e; k0 += NL) {   // (a uniform loop: the state stays scalar)
-        const int k = k0 + lane;
-        if (k < e) ring[k & (kRing - 1)] = g[k];
-      }
+      // kRingHalf / NL consecutive bytes per lane, all loads issued before the first store
+      constexpr int kPer = kRingHalf / NL;
+      const int k0 = filled + lane * kPer;
+      uint8_t v[kPer];
+#pragma unroll
+      for (int i = 0; i < kPer; ++i) v[i] = k0 + i < e ? g[k0 + i] : 0;
+#pragma unroll
+      for (int i = 0; i < kPer; ++i)
+        if (k0 + i < e) ring[(k0 + i) & (kRing - 1)] = v[i];
       filled = e;
       INF_WAVE_ORDER();
     }
@@ -372,6 +377,16 @@ INF_FN int inflate_wave(InfShared &S, const uint8_t *g, int n, uint8_t *dst, int
 #endif
           if (lane == 0) S.out[w & M] = (uint8_t)sym;
           ++w;
+          // a second literal in the same iteration when its code is in the table and the bits
+          // are there (literal runs: half the loop overhead)
+          const int e2 = uni(lfast[b.buf & kFastMask]);
+          const int l2 = e2 >> 9, s2 = e2 & 511;
+          if (l2 && l2 <= b.cnt && s2 < 256 && w < cap) {
+            if (lane == 0) S.out[w & M] = (uint8_t)s2;
+            ++w;
+            b.buf >>= l2;
+            b.cnt -= l2;
+          }
         } else {
           if (sym == 256) break;
           const int li = sym - 257;

@@ -653,9 +653,11 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
     fds = [os.open(p, os.O_WRONLY) for p in paths]
     # GANON_GPU_INFLATE=1: the decode thread's BGZF windows inflate on this rank's GPU (one context
     # of its own, shared by both readers: they are only used by that thread, one at a time)
+    # (GANON_GPU_INFLATE_MIN: the fewest blocks a window needs to go to the GPU, default 512 — one
+    # block takes ~12 ms on its wave, so only large windows pay off: DESIGN §4e)
     inflater = None
     if os.environ.get("GANON_GPU_INFLATE", "0") == "1":
-        inflater = native.GpuInflater(anonymizer.device)
+        inflater = native.GpuInflater(anonymizer.device, int(os.environ.get("GANON_GPU_INFLATE_MIN", "512")))
     readers = (BamReader(tumor_bam, threads, window_bytes, inflater),
                BamReader(normal_bam, threads, window_bytes, inflater))
     contigs = list(fasta.references)

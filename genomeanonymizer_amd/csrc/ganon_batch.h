@@ -184,6 +184,9 @@ struct ganon_dbatch {
   ganon_dev::DBuf b_nseg, b_scost, b_scan_tmp, b_slots, b_slot0;   // segments per read; long-read mode: group
                                                                   // costs, dirty flags, first slot per incidence
   ganon_dev::DBuf b_wspart;                                        // per-group write-scope hash sums
+  ganon_dev::DBuf b_order;                                         // group launch order (k_prep_order_*), then per-block class counts
+  int64_t max_scope_incid = 0;                                     // most incidences of one scope (host, at load)
+  bool ordered = false;                                            // the run launches groups in b_order's order
   ganon_dev::DBuf b_read_end, b_cursor, b_gs0, b_lo, b_linemap, b_groups, b_seg4, b_grp_part, b_far, b_gokey, b_gopay, b_gtkey, b_gtflag, b_out,
       b_scope_calls, b_scope_bases, b_small;   // b_small: totals, static totals, counters, acc, status, errors
   uint8_t *out = nullptr;

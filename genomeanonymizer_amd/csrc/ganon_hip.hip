@@ -931,23 +931,31 @@ template <int U, bool FUSED, int OBS>
 __global__ void __launch_bounds__(kGrpThreads, (OBS > 512 ? 4 : U == 1 ? 6 : U == 2 ? GANON_K2_BLOCKS : U == 4 ? 5 : 4)) k_group(const GrpBatch B, const int4 *__restrict__ groups,
                                                        const int4 *__restrict__ rec4,
                                                        uint8_t *__restrict__ out, const GrpAux *__restrict__ aux,
-                                                       int skip, int nt_copy, const unsigned long long *__restrict__ gate) {
+                                                       int skip, int nt_copy, const unsigned long long *__restrict__ gate,
+                                                       const int32_t *__restrict__ order) {
   __shared__ GrpSharedT<OBS> sh;
   const int tid = threadIdx.x;
+  // the group this block runs: order[] (k_prep_order, longest first) when the batch has groups of
+  // very unequal cost, else blockIdx (order[0] = -1); partials stay at the block's own slot
+  int gid = blockIdx.x;
+  if (order) {
+    const int o0 = order[0];
+    if (o0 >= 0) gid = blockIdx.x ? order[blockIdx.x] : o0;
+  }
   // one-segment mode launches for the group bound: blocks past the scan's count (gate[5]) add
   // nothing; no block runs on a batch the scan rejected (gate[7])
-  if (gate && (gate[7] || blockIdx.x >= gate[5])) {
+  if (gate && (gate[7] || (unsigned long long)gid >= gate[5])) {
     if (tid == 0) {
       gp(aux->part)[2 * blockIdx.x] = 0;
       gp(aux->part)[2 * blockIdx.x + 1] = 0;
     }
     return;
   }
-  const int4 g0 = groups[kGrpRec * blockIdx.x];
-  const int4 g1 = groups[kGrpRec * blockIdx.x + 1];
-  const int4 g2 = groups[kGrpRec * blockIdx.x + 2];
-  const int4 g3 = groups[kGrpRec * blockIdx.x + 3];
-  const int4 g4 = groups[kGrpRec * blockIdx.x + 4];
+  const int4 g0 = groups[kGrpRec * gid];
+  const int4 g1 = groups[kGrpRec * gid + 1];
+  const int4 g2 = groups[kGrpRec * gid + 2];
+  const int4 g3 = groups[kGrpRec * gid + 3];
+  const int4 g4 = groups[kGrpRec * gid + 4];
   const GrpGlobal gg{aux, i64_of(g3.x, g3.y), g3.z};
   const int s_begin = g0.x, s_end = g0.y;
   const int64_t i_begin = i64_of(g0.z, g0.w), i_end = i64_of(g1.x, g1.y), i_mid = i64_of(g1.z, g1.w);
@@ -1319,7 +1327,7 @@ void free_batch(ganon_dbatch *db) {
                   &db->b_read_end, &db->b_wspart, &db->b_cursor, &db->b_gs0, &db->b_lo, &db->b_linemap, &db->b_groups,
                   &db->b_seg4, &db->b_grp_part, &db->b_far, &db->b_gokey, &db->b_gopay, &db->b_gtkey, &db->b_gtflag,
                   &db->b_out, &db->b_scope_calls, &db->b_scope_bases, &db->b_small, &db->b_part, &db->b_long, &db->b_nseg,
-                  &db->b_scost, &db->b_scan_tmp, &db->b_slots, &db->b_slot0};
+                  &db->b_scost, &db->b_scan_tmp, &db->b_slots, &db->b_slot0, &db->b_order};
   for (DBuf *b : bufs) free_buf(*b);
   free_huge(db);
   free_ref(db->own_ref);
@@ -1576,10 +1584,13 @@ int load_batch(ganon_ctx *ctx, ganon_dbatch *db, const ganon_batch *b, const gan
   if (b->scope_incid_off[0] != 0 || b->scope_incid_off[b->n_scopes] != b->n_incid)
     return fail(ctx, GANON_E_ARG, "scope_incid_off must start at 0 and end at n_incid");
   if (2 * b->seq_bytes >= (int64_t(1) << 39)) return fail(ctx, GANON_E_ARG, "sequence over 2^39 bases");
+  int64_t max_si = 0;   // (the group kernel's launch order: ganon_prep launch_pieces)
+  for (int32_t s = 0; s < b->n_scopes; ++s) max_si = std::max(max_si, b->scope_incid_off[s + 1] - b->scope_incid_off[s]);
   if (b->n_incid >= INT32_MAX) return fail(ctx, GANON_E_ARG, "more than 2^31-1 incidences");
   int rc;
   HIP_OR_FAIL(hipStreamSynchronize(ctx->stream));   // a previous run of db may still read its buffers
   db->ran = false;
+  db->max_scope_incid = max_si;
   if (shared) {
     db->ref = shared;
   } else {
@@ -1903,7 +1914,8 @@ GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
     const GrpBatch GB{B.seq, B.ref, B.keep_code, B.ref2, B.keep_pos, B.span_start, B.span_len};
     kern<<<db->n_groups, kGrpThreads, 0, st>>>(GB, static_cast<const int4 *>(db->b_groups.p),
                                                static_cast<const int4 *>(db->b_seg4.p), db->out, db->aux,
-                                               ctx->group_skip, ctx->nt_copy, db->flat_mode ? db->plan_info : nullptr);
+                                               ctx->group_skip, ctx->nt_copy, db->flat_mode ? db->plan_info : nullptr,
+                                               db->ordered ? static_cast<const int32_t *>(db->b_order.p) : nullptr);
     if ((rc = check_launch(ctx, "k_group"))) return rc;
   } else if (db->seq_bytes) {
     KernelScope ks(ctx, "copy_seq");

@@ -1390,6 +1390,105 @@ int launch_emit(ganon_ctx *ctx, ganon_dbatch *db, const Raw &R, int write) {
   return check_launch(ctx, "k_prep_emit");
 }
 
+// Launch order of the group kernel. A scope with more incidences than the group target is a group
+// of its own — at 60x coverage up to ~12x the others (8 k incidences against 704) — and
+// in scope order such a group can start among the last and run on alone at the end. When a group
+// costs more than twice the target, order[] lists the groups by descending cost in power-of-two
+// classes (longest processing time first; the empty groups of skipped buckets and the blocks past
+// the scan's count last); else order[0] = -1 and the blocks run in group order. Two passes over the
+// group table (just written: L2), a block per 256 groups, no atomics outside LDS and no memset:
+// per-block class counts, then every block finds its classes' offsets from all blocks' counts and
+// scatters its groups. Launched only for batches that can hold such a group (launch_pieces).
+constexpr int kOrderThreads = 256;
+constexpr int kOrderClasses = 32;
+constexpr int kOrderRow = kOrderClasses + 1;   // per-block row: class counts, then the block's max cost
+
+__device__ __forceinline__ int order_class(long long c, long long target) {
+  if (c <= 0) return kOrderClasses - 1;
+  const unsigned long long x = (unsigned long long)(c * 8 / target) + 1;   // eighths of a target, + 1
+  const int lg = 63 - __clzll((long long)x);
+  return kOrderClasses - 2 - min(lg, kOrderClasses - 2);
+}
+
+__device__ __forceinline__ long long order_cost(const int4 *__restrict__ groups, int64_t g, int64_t ng) {
+  if (g >= ng) return 0;
+  const int4 a = groups[kGrpRec * g], b = groups[kGrpRec * g + 1];
+  const int64_t end = (int64_t)(uint32_t)b.x | ((int64_t)b.y << 32), beg = (int64_t)(uint32_t)a.z | ((int64_t)a.w << 32);
+  return end - beg;
+}
+
+__device__ __forceinline__ int64_t order_groups(const unsigned long long *__restrict__ gate, int64_t n_groups) {
+  return gate ? (gate[7] ? 0 : min(n_groups, (int64_t)gate[5])) : n_groups;
+}
+
+__global__ void __launch_bounds__(kOrderThreads) k_prep_order_count(const int4 *__restrict__ groups, int64_t n_groups,
+                                                                     const unsigned long long *__restrict__ gate,
+                                                                     long long target, uint32_t *__restrict__ rows) {
+  __shared__ unsigned int hist[kOrderClasses];
+  __shared__ unsigned int bmax;
+  const int t = threadIdx.x;
+  const int64_t ng = order_groups(gate, n_groups);
+  if (t < kOrderClasses) hist[t] = 0;
+  if (t == 0) bmax = 0;
+  __syncthreads();
+  const int64_t g = (int64_t)blockIdx.x * kOrderThreads + t;
+  if (g < n_groups) {
+    const long long c = order_cost(groups, g, ng);
+    atomicAdd(&hist[order_class(c, target)], 1u);
+    atomicMax(&bmax, (unsigned int)min(c, (long long)UINT32_MAX));
+  }
+  __syncthreads();
+  if (t < kOrderClasses) rows[(int64_t)blockIdx.x * kOrderRow + t] = hist[t];
+  if (t == 0) rows[(int64_t)blockIdx.x * kOrderRow + kOrderClasses] = bmax;
+}
+
+__global__ void __launch_bounds__(kOrderThreads) k_prep_order_scatter(const int4 *__restrict__ groups, int64_t n_groups,
+                                                                       const unsigned long long *__restrict__ gate,
+                                                                       long long target, const uint32_t *__restrict__ rows,
+                                                                       int n_blocks, int32_t *__restrict__ order) {
+  __shared__ unsigned int tot[kOrderClasses], pre[kOrderClasses];
+  __shared__ unsigned int gmax;
+  const int t = threadIdx.x;
+  const int64_t ng = order_groups(gate, n_groups);
+  // column t of the per-block rows (classes, then the largest cost): all blocks' sum / max and the
+  // sum over the blocks before this one; independent loads, eight in flight
+  if (t <= kOrderClasses) {
+    unsigned int all = 0, before = 0;
+    const int me = (int)blockIdx.x;
+#pragma unroll 8
+    for (int k = 0; k < n_blocks; ++k) {
+      const unsigned int v = rows[(int64_t)k * kOrderRow + t];
+      if (t == kOrderClasses) {
+        all = max(all, v);
+      } else {
+        all += v;
+        before += k < me ? v : 0u;
+      }
+    }
+    if (t == kOrderClasses) {
+      gmax = all;
+    } else {
+      tot[t] = all;
+      pre[t] = before;
+    }
+  }
+  __syncthreads();
+  if ((long long)gmax <= 2 * target) {
+    if (blockIdx.x == 0 && t == 0) order[0] = -1;
+    return;
+  }
+  if (t == 0) {
+    unsigned int run = 0;
+    for (int k = 0; k < kOrderClasses; ++k) {
+      pre[k] += run;
+      run += tot[k];
+    }
+  }
+  __syncthreads();
+  const int64_t g = (int64_t)blockIdx.x * kOrderThreads + t;
+  if (g < n_groups) order[atomicAdd(&pre[order_class(order_cost(groups, g, ng), target)], 1u)] = (int32_t)g;
+}
+
 int launch_pieces(ganon_ctx *ctx, ganon_dbatch *db) {
   hipStream_t st = ctx->stream;
   const int n_cand = 2 * db->n_groups;
@@ -1400,6 +1499,19 @@ int launch_pieces(ganon_ctx *ctx, ganon_dbatch *db) {
   hipLaunchKernelGGL(k_prep_pieces, dim3(grid_for(n_cand)), dim3(kPrepThreads), 0, st,
                      static_cast<const unsigned long long *>(db->b_lo.p), n_cand, M, db->seq_bytes,
                      static_cast<int4 *>(db->b_groups.p), db->flat_mode ? db->plan_info : nullptr);
+  // launch order (k_prep_order_*): long reads, or a scope with more than twice the target's
+  // incidences (the host's count at load); otherwise the group kernel runs in group order
+  db->ordered = db->long_mode || db->max_scope_incid > 2 * (int64_t)db->group_target;
+  if (db->ordered) {
+    const int nb = (int)((db->n_groups + kOrderThreads - 1) / kOrderThreads);
+    const int4 *g = static_cast<const int4 *>(db->b_groups.p);
+    const unsigned long long *gate = db->flat_mode ? db->plan_info : nullptr;
+    uint32_t *rows = static_cast<uint32_t *>(db->b_order.p) + (size_t)db->n_groups + 1;
+    hipLaunchKernelGGL(k_prep_order_count, dim3(nb), dim3(kOrderThreads), 0, st, g, (int64_t)db->n_groups, gate,
+                       (long long)db->group_target, rows);
+    hipLaunchKernelGGL(k_prep_order_scatter, dim3(nb), dim3(kOrderThreads), 0, st, g, (int64_t)db->n_groups, gate,
+                       (long long)db->group_target, rows, nb, static_cast<int32_t *>(db->b_order.p));
+  }
   return check_launch(ctx, "k_prep_pieces");
 }
 
@@ -1565,6 +1677,8 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db, bool allow_spec) {
   if ((rc = grow_n(ctx, db->b_gs0, (size_t)std::max<int64_t>(ng, 1), &gm)) ||
       (rc = grow_n(ctx, db->b_groups, (size_t)kGrpRec * ng, &grp)) ||
       (rc = grow_n(ctx, db->b_grp_part, 2 * (size_t)ng, &p32)) ||
+      (rc = grow_n(ctx, db->b_order, (size_t)ng + 1 + (size_t)kOrderRow * ((ng + kOrderThreads - 1) / kOrderThreads),
+                   &p32)) ||
       (rc = grow_n(ctx, db->b_wspart, (size_t)std::max<int64_t>(ng, 1), &u64)) ||
       (rc = grow_n(ctx, db->b_lo, 2 * (size_t)std::max<int64_t>(ng, 1), &u64)) ||
       (rc = grow_n(ctx, db->b_linemap, (size_t)line_map_words(db), &u64)))

@@ -1403,11 +1403,14 @@ constexpr int kOrderThreads = 256;
 constexpr int kOrderClasses = 32;
 constexpr int kOrderRow = kOrderClasses + 1;   // per-block row: class counts, then the block's max cost
 
+// class of a group: the big ones (over twice the target) by power of two, longest first; every other
+// group in one class, so that those keep their neighbours (the partition copies and the reference
+// lines of consecutive groups are adjacent); the empty ones last
 __device__ __forceinline__ int order_class(long long c, long long target) {
   if (c <= 0) return kOrderClasses - 1;
-  const unsigned long long x = (unsigned long long)(c * 8 / target) + 1;   // eighths of a target, + 1
-  const int lg = 63 - __clzll((long long)x);
-  return kOrderClasses - 2 - min(lg, kOrderClasses - 2);
+  if (c <= 2 * target) return kOrderClasses - 2;
+  const int lg = 63 - __clzll((long long)(c / (2 * target)));   // 0 .. : twice the target << lg
+  return kOrderClasses - 3 - min(lg, kOrderClasses - 3);
 }
 
 __device__ __forceinline__ long long order_cost(const int4 *__restrict__ groups, int64_t g, int64_t ng) {

@@ -500,6 +500,8 @@ struct ganon_inflate_state {
   int64_t *in_off = nullptr, *out_off = nullptr;
   int32_t *in_len = nullptr, *out_len = nullptr, *status = nullptr;
   size_t comp_cap = 0, out_cap = 0, blk_cap = 0;
+  hipStream_t copy = nullptr;           // copies of a chunked call (the kernels run on ctx->stream)
+  std::vector<hipEvent_t> ev;           // two per chunk
 };
 
 namespace {
@@ -551,13 +553,6 @@ GANON_API int ganon_inflate(ganon_ctx *ctx, const uint8_t *comp, int64_t comp_le
     st->blk_cap = c1;
   }
   hipStream_t s = ctx->stream;
-  if (hipMemcpyAsync(st->comp, comp, (size_t)comp_len, hipMemcpyHostToDevice, s) != hipSuccess ||
-      hipMemcpyAsync(st->in_off, in_off, nb * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
-      hipMemcpyAsync(st->out_off, out_off, nb * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
-      hipMemcpyAsync(st->in_len, in_len, nb * 4, hipMemcpyHostToDevice, s) != hipSuccess ||
-      hipMemcpyAsync(st->out_len, out_len, nb * 4, hipMemcpyHostToDevice, s) != hipSuccess)
-    return fail(ctx, GANON_E_DEVICE, "ganon_inflate: host-to-device copy failed");
-  const unsigned grid = (unsigned)std::min<int64_t>(n_blocks, 1 << 16);
   if (ctx->profiling) {   // a profiled call: ganon_last_kernel_times reports k_inflate alone
     for (auto &r : ctx->recs) {
       ctx->pool.push_back(r.e0);
@@ -565,17 +560,72 @@ GANON_API int ganon_inflate(ganon_ctx *ctx, const uint8_t *comp, int64_t comp_le
     }
     ctx->recs.clear();
   }
-  {
-  ganon_detail::KernelScope ks(ctx, "k_inflate");
-  hipLaunchKernelGGL(k_inflate, dim3(grid), dim3(kInfThreads), 0, s, st->comp, comp_len, st->in_off, st->in_len,
-                     st->out_off, st->out_len, n_blocks, st->out, out_total, st->status);
+  // Chunks of kChunk blocks (about one wave of decoders on the chip) when the blocks lie in file
+  // order: the payload of chunk c + 1 goes up and the output of chunk c - 1 comes down on a copy
+  // stream while chunk c decodes; otherwise one chunk.
+  constexpr int64_t kChunk = 1024;
+  bool ordered = true;
+  for (size_t i = 1; i < nb && ordered; ++i)
+    ordered = in_off[i] >= in_off[i - 1] + in_len[i - 1] && out_off[i] >= out_off[i - 1] + out_len[i - 1];
+  const int64_t n_chunks = ordered ? (n_blocks + kChunk - 1) / kChunk : 1;
+  auto span_in = [&](int64_t b0, int64_t b1, int64_t &lo, int64_t &hi) {
+    lo = ordered ? in_off[b0] : 0;
+    hi = ordered ? in_off[b1 - 1] + in_len[b1 - 1] : comp_len;
+  };
+  auto span_out = [&](int64_t b0, int64_t b1, int64_t &lo, int64_t &hi) {
+    lo = ordered ? out_off[b0] : 0;
+    hi = ordered ? out_off[b1 - 1] + out_len[b1 - 1] : out_total;
+  };
+  if (ordered && (in_off[0] < 0 || in_off[nb - 1] + in_len[nb - 1] > comp_len || out_off[0] < 0 ||
+                  out_off[nb - 1] + out_len[nb - 1] > out_total))
+    return fail(ctx, GANON_E_ARG, "ganon_inflate: block ranges outside the buffers");
+  if (!st->copy && hipStreamCreateWithFlags(&st->copy, hipStreamNonBlocking) != hipSuccess)
+    return fail(ctx, GANON_E_DEVICE, "ganon_inflate: stream creation failed");
+  while ((int64_t)st->ev.size() < 2 * n_chunks) {
+    hipEvent_t e;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
+      return fail(ctx, GANON_E_DEVICE, "ganon_inflate: event creation failed");
+    st->ev.push_back(e);
   }
-  if ((rc = check_launch(ctx, "k_inflate"))) return rc;
+  hipStream_t cs = st->copy;
+  bool okc = hipMemcpyAsync(st->in_off, in_off, nb * 8, hipMemcpyHostToDevice, cs) == hipSuccess &&
+             hipMemcpyAsync(st->out_off, out_off, nb * 8, hipMemcpyHostToDevice, cs) == hipSuccess &&
+             hipMemcpyAsync(st->in_len, in_len, nb * 4, hipMemcpyHostToDevice, cs) == hipSuccess &&
+             hipMemcpyAsync(st->out_len, out_len, nb * 4, hipMemcpyHostToDevice, cs) == hipSuccess;
+  auto d2h = [&](int64_t c) {
+    const int64_t b0 = c * kChunk, b1 = std::min(n_blocks, b0 + kChunk);
+    int64_t lo, hi;
+    span_out(b0, b1, lo, hi);
+    return hipStreamWaitEvent(cs, st->ev[2 * c + 1], 0) == hipSuccess &&
+           (hi <= lo || hipMemcpyAsync(out + lo, st->out + lo, (size_t)(hi - lo), hipMemcpyDeviceToHost, cs) == hipSuccess);
+  };
+  for (int64_t c = 0; c < n_chunks && okc; ++c) {
+    const int64_t b0 = c * kChunk, b1 = std::min(n_blocks, b0 + kChunk);
+    int64_t lo, hi;
+    span_in(b0, b1, lo, hi);
+    okc = (hi <= lo || hipMemcpyAsync(st->comp + lo, comp + lo, (size_t)(hi - lo), hipMemcpyHostToDevice, cs) == hipSuccess) &&
+          hipEventRecord(st->ev[2 * c], cs) == hipSuccess && hipStreamWaitEvent(s, st->ev[2 * c], 0) == hipSuccess;
+    if (!okc) break;
+    {
+      ganon_detail::KernelScope ks(ctx, "k_inflate");
+      const unsigned grid = (unsigned)std::min<int64_t>(b1 - b0, 1 << 16);
+      hipLaunchKernelGGL(k_inflate, dim3(grid), dim3(kInfThreads), 0, s, st->comp, comp_len, st->in_off + b0,
+                         st->in_len + b0, st->out_off + b0, st->out_len + b0, b1 - b0, st->out, out_total,
+                         st->status + b0);
+    }
+    if ((rc = check_launch(ctx, "k_inflate"))) return rc;
+    okc = hipEventRecord(st->ev[2 * c + 1], s) == hipSuccess && (c == 0 || d2h(c - 1));
+  }
   std::vector<int32_t> stat(nb);
-  if (hipMemcpyAsync(out, st->out, (size_t)out_total, hipMemcpyDeviceToHost, s) != hipSuccess ||
-      hipMemcpyAsync(stat.data(), st->status, nb * 4, hipMemcpyDeviceToHost, s) != hipSuccess)
-    return fail(ctx, GANON_E_DEVICE, "ganon_inflate: device-to-host copy failed");
-  if ((rc = ganon_batch_sync(ctx))) return rc;   // (collects the kernel time when profiling)
+  okc = okc && d2h(n_chunks - 1) &&
+        hipMemcpyAsync(stat.data(), st->status, nb * 4, hipMemcpyDeviceToHost, cs) == hipSuccess &&
+        hipStreamSynchronize(cs) == hipSuccess;
+  if (!okc) {
+    hipStreamSynchronize(cs);
+    hipStreamSynchronize(s);
+    return fail(ctx, GANON_E_DEVICE, "ganon_inflate: copy failed");
+  }
+  if ((rc = ganon_batch_sync(ctx))) return rc;   // (collects the kernel times when profiling)
   for (size_t i = 0; i < nb; ++i)
     if (stat[i]) {
       if (first_bad) *first_bad = (int64_t)i;
@@ -593,6 +643,11 @@ GANON_API int ganon_inflate_hostcb(void *ctx, const uint8_t *comp, int64_t comp_
 
 void ganon_inflate_free(ganon_inflate_state *st) {
   if (!st) return;
+  if (st->copy) {
+    hipStreamSynchronize(st->copy);
+    hipStreamDestroy(st->copy);
+  }
+  for (hipEvent_t e : st->ev) hipEventDestroy(e);
   for (void *p : {(void *)st->comp, (void *)st->out, (void *)st->in_off, (void *)st->out_off, (void *)st->in_len,
                   (void *)st->out_len, (void *)st->status})
     if (p) hipFree(p);

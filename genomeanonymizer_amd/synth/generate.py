@@ -476,6 +476,18 @@ def scenario(name: str) -> ScenarioConfig:
             germline_snp_per_kb=6.0, germline_indel_per_kb=1.0, hom_fraction=0.3,
             softclip_frac=0.05, unmapped_mate_frac=0.02, n_base_frac=0.05, iupac_sites=2,
             lowercase_frac=0.05, n_ref_runs=2, unplaced_frac=0.3, cross_contig_pairs=25)
+    if name == "long1":
+        # Long paired reads (SURVEY §8(d) C5 in miniature, pinned file to file by the reference run):
+        # 4-6 kb reads, 12 kb fragments, dense germline indels (hap-1 reads carry 20-40 I/D ops, many
+        # over the 48-op threshold of the device's long-CIGAR walk), 1 % substitution errors, soft clips.
+        return ScenarioConfig(
+            name="long1", seed=41,
+            contigs=[ContigSpec("lr1", 60_000, 24, windows=[6000, 20000, 41000], keep_windows=1),
+                     ContigSpec("lr2", 40_000, 14, windows=[15000])],
+            read_len=5000, insert_mean=12_000.0, insert_sd=1500.0,
+            germline_snp_per_kb=3.0, germline_indel_per_kb=6.0, hom_fraction=0.5,
+            error_rate=0.01, softclip_frac=0.2, n_base_frac=0.2, unmapped_mate_frac=0.05,
+            unplaced_frac=0.3, cross_contig_pairs=3)
     if name == "tiny":
         return ScenarioConfig(
             name="tiny", seed=3,

@@ -435,6 +435,24 @@ def fuzz_scenario(seed: int) -> ScenarioConfig:
     """Random small multi-contig pair (oracle/fuzz_reference.py; goldens tests/golden/fuzz<seed>)."""
     rng = np.random.default_rng(seed)
     contigs = []
+    if seed >= 9000:
+        # long paired reads: 2-8 kb, dense germline indels (long CIGARs), 0.5-2 % substitution errors
+        rl = int(rng.integers(2000, 8001))
+        for c in range(int(rng.integers(1, 3))):
+            L = int(rng.integers(30_000, 60_000))
+            wins, x = [], 1500 + int(rng.integers(0, 3000))
+            while x < L - 1500 and len(wins) < 4:
+                wins.append(x)
+                x += 2003 + int(rng.integers(0, 12000))
+            contigs.append(ContigSpec(f"c{c}", L, int(rng.integers(8, 24)), windows=wins,
+                                      keep_windows=int(rng.integers(0, 2))))
+        return ScenarioConfig(name=f"fuzz{seed}", seed=seed, contigs=contigs, read_len=rl,
+                              insert_mean=float(2 * rl + rng.integers(500, 4000)), insert_sd=float(rl / 8),
+                              germline_snp_per_kb=float(rng.uniform(1, 6)),
+                              germline_indel_per_kb=float(rng.uniform(2, 8)), hom_fraction=0.4,
+                              error_rate=float(rng.uniform(0.005, 0.02)), softclip_frac=0.2,
+                              unmapped_mate_frac=0.05, n_base_frac=0.2, unplaced_frac=0.4,
+                              cross_contig_pairs=int(rng.integers(0, 4)))
     for c in range(int(rng.integers(2, 4))):
         L = int(rng.integers(6_000, 14_000))
         wins, x = [], 1001 + int(rng.integers(0, 1500))

@@ -91,7 +91,7 @@ def build_host(force: bool = False) -> str:
     if force or _stale(HOST_LIB, srcs + [hdr, __file__]):
         tmp = f"{HOST_LIB}.{os.getpid()}.tmp"
         _run(["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-fvisibility=hidden", "-pthread",
-              "-o", tmp] + srcs + ["-lz"])
+              "-o", tmp] + srcs + ["-lz", "-ldl"])
         os.replace(tmp, HOST_LIB)
     return HOST_LIB
 

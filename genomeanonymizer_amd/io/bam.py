@@ -32,11 +32,29 @@ def _arr(ptr, n, dtype):
     return np.ctypeslib.as_array(ptr, shape=(n,)).astype(dtype, copy=True)
 
 
-def _blob(ptr, n, dtype=np.uint8):
+class _Decoded:
+    """Owns one native ``ganon_bam`` (decoded records); released when the last array viewing its
+    memory is gone."""
+    __slots__ = ("h", "__weakref__")
+
+    def __init__(self, h):
+        self.h = h
+
+    def __del__(self):
+        if self.h:
+            native.host_lib().ganon_bam_close(self.h)
+            self.h = None
+
+
+def _view(ptr, n, dtype, owner: _Decoded):
+    """A writable numpy view of n elements of native memory (no copy); the view keeps `owner`, and
+    with it the native buffers, alive."""
     if n == 0:
         return np.zeros(0, dtype)
     addr = ptr if isinstance(ptr, int) else C.cast(ptr, C.c_void_p).value
-    return np.frombuffer(C.string_at(addr, n * np.dtype(dtype).itemsize), dtype=dtype).copy()
+    buf = (C.c_char * (n * np.dtype(dtype).itemsize)).from_address(addr)
+    buf._owner = owner
+    return np.frombuffer(buf, dtype=dtype)
 
 
 class ReadTable:
@@ -44,7 +62,7 @@ class ReadTable:
 
     def __init__(self, path: str, threads: int = 8, handle=None):
         """Decode the whole file, or take the records of an open ``ganon_bam`` handle (one
-        reference sequence from ``BamReader.contig``); the handle is released here."""
+        reference sequence from ``BamReader.contig``); the table owns the handle from here on."""
         lib = native.host_lib()
         if handle is None:
             h = C.c_void_p()
@@ -53,15 +71,15 @@ class ReadTable:
                 raise native.GanonError(f"cannot decode {path}: {lib.ganon_host_last_error().decode()}")
         else:
             h = handle
-        try:
-            v = native.BamView()
-            lib.ganon_bam_view_get(h, C.byref(v))
-            self._load(path, v)
-        finally:
-            lib.ganon_bam_close(h)
+        owner = _Decoded(h)
+        v = native.BamView()
+        lib.ganon_bam_view_get(h, C.byref(v))
+        self._load(path, v, owner)
         self._finish()
 
-    def _load(self, path: str, v) -> None:
+    def _load(self, path: str, v, owner: _Decoded) -> None:
+        """Per-record columns are copied (small); the byte blobs (names, CIGAR words, sequences,
+        qualities, aux) are views of the decoder's buffers, which `owner` frees with the last view."""
         n = int(v.n_records)
         self.path = path
         self.n = n
@@ -76,11 +94,11 @@ class ReadTable:
             setattr(self, f, _arr(getattr(v, f), n, np.int32))
         for f in ("name_off", "cig_off", "seq_off", "qual_off", "aux_off"):
             setattr(self, f, _arr(getattr(v, f), n, np.int64))
-        self.names_blob = _blob(v.names, int(v.names_bytes))
-        self.cigar = _blob(v.cigar, int(v.cigar_ops), np.uint32).copy()
-        self.seq = _blob(v.seq, int(v.seq_bytes)).copy()
-        self.qual = _blob(v.qual, int(v.qual_bytes)).copy()
-        self.aux = _blob(v.aux, int(v.aux_bytes)).copy()
+        self.names_blob = _view(v.names, int(v.names_bytes), np.uint8, owner)
+        self.cigar = _view(v.cigar, int(v.cigar_ops), np.uint32, owner)
+        self.seq = _view(v.seq, int(v.seq_bytes), np.uint8, owner)
+        self.qual = _view(v.qual, int(v.qual_bytes), np.uint8, owner)
+        self.aux = _view(v.aux, int(v.aux_bytes), np.uint8, owner)
 
     def _finish(self) -> None:
         self._names: Optional[List[str]] = None

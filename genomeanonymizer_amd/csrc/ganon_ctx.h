@@ -144,6 +144,28 @@ inline int check_launch(ganon_ctx *ctx, const char *what) {
 
 }  // namespace ganon_detail
 
+namespace ganon_wave {
+
+// Inclusive prefix sum over the 64 lanes of a wave (every lane active): DPP row_shr steps inside
+// each 16-lane row, then the lower rows' totals through readlane — no LDS crossbar round trips and
+// no lane-index arithmetic (a __shfl_up ladder is six ds_bpermute trips per scan). Used by the
+// wave-per-read CIGAR walks, where it sits on the critical path of every 64 ops.
+__device__ __forceinline__ int incl_sum(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);   // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);   // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);   // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);   // row_shr:8
+  const int r0 = __builtin_amdgcn_readlane(v, 15), r1 = __builtin_amdgcn_readlane(v, 31),
+            r2 = __builtin_amdgcn_readlane(v, 47);
+  const int row = (int)(threadIdx.x & 63) >> 4;
+  return v + (row >= 1 ? r0 : 0) + (row >= 2 ? r1 : 0) + (row >= 3 ? r2 : 0);
+}
+
+// The wave's total from an inclusive sum (lane 63), wave-uniform.
+__device__ __forceinline__ int last(int incl) { return __builtin_amdgcn_readlane(incl, 63); }
+
+}  // namespace ganon_wave
+
 #define HIP_OR_FAIL(call)                                                                          \
   do {                                                                                             \
     hipError_t e_ = (call);                                                                        \

@@ -99,13 +99,8 @@ __device__ __forceinline__ int nib(const uint8_t *__restrict__ seq, int64_t byte
 }
 
 __device__ __forceinline__ int wave_excl_scan(int v, int lane) {
-  int x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(x, o);
-    if (lane >= o) x += y;
-  }
-  return x - v;
+  (void)lane;
+  return ganon_wave::incl_sum(v) - v;
 }
 
 // The reference's offsets of a read's ops, 64 CIGAR ops per step of one wave: pos = reference
@@ -141,8 +136,8 @@ __device__ __forceinline__ void walk_block(const GanonReadView &V, int r, int k0
     c[j].is_id = k < nc && (op == 1 || op == 2);
     c[j].pos = rcarry + wave_excl_scan(radv, lane);
     c[j].irp = qcarry + wave_excl_scan(qadv, lane);
-    rcarry = __shfl(c[j].pos + radv, 63);
-    qcarry = __shfl(c[j].irp + qadv, 63);
+    rcarry = ganon_wave::last(c[j].pos + radv);
+    qcarry = ganon_wave::last(c[j].irp + qadv);
   }
   f(c);
 }

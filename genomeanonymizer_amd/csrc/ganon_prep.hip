@@ -198,6 +198,9 @@ __device__ __forceinline__ CigarWalk wave_cigar_walk(const uint32_t *__restrict_
   const int lane = threadIdx.x & 63;
   CigarWalk W{0, 0, 0, -1};
   int q = 0;
+  // per-lane sums, reduced once after the walk: only the query offset is a prefix
+  int seg = 0, id = 0;
+  long long dr = 0;
   for (int base = 0; base < nc; base += 64) {
     const int k = base + lane;
     const uint32_t w = k < nc ? cg[k] : 0u;   // padding lanes: a 0M op, which adds nothing
@@ -205,31 +208,26 @@ __device__ __forceinline__ CigarWalk wave_cigar_walk(const uint32_t *__restrict_
     const unsigned long long badm = __ballot(op > 8);
     if (badm) {
       W.bad_op = __shfl(op, __ffsll((long long)badm) - 1);
-      return W;
+      break;
     }
     const bool al = is_aligned_op(op);
     const int dq = (al || op == 1 || op == 4) ? len : 0;
-    int incl = dq;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int x = __shfl_up(incl, o);
-      if (lane >= o) incl += x;
-    }
+    const int incl = ganon_wave::incl_sum(dq);
     const int q0 = q + incl - dq;
-    int seg = (al && q0 < L) ? (min(len, L - q0) + kSegMaxLen - 1) / kSegMaxLen : 0;
-    int id = (op == 1 || op == 2) ? 1 : 0;
-    long long dr = (al || op == 2 || op == 3) ? (long long)len : 0ll;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      seg += __shfl_xor(seg, o);
-      id += __shfl_xor(id, o);
-      dr += __shfl_xor(dr, o);
-    }
-    W.ns += seg;
-    W.nid += id;
-    W.rl += dr;
-    q += __shfl(incl, 63);
+    seg += (al && q0 < L) ? (min(len, L - q0) + kSegMaxLen - 1) / kSegMaxLen : 0;
+    id += (op == 1 || op == 2) ? 1 : 0;
+    dr += (al || op == 2 || op == 3) ? (long long)len : 0ll;
+    q += ganon_wave::last(incl);
   }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    seg += __shfl_xor(seg, o);
+    id += __shfl_xor(id, o);
+    dr += __shfl_xor(dr, o);
+  }
+  W.ns = seg;
+  W.nid = id;
+  W.rl = dr;
   return W;
 }
 
@@ -1113,25 +1111,11 @@ __device__ __forceinline__ void wave_walk(const Raw &R, int r, bool mine, int jl
     const bool al = is_aligned_op(op);
     const int dq = (al || op == 1 || op == 4) ? len : 0;
     const int dp = (al || op == 2 || op == 3) ? len : 0;
-    const int q_ex0 = q, p_ex0 = p;
-    int iq = dq, ip = dp;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int xq = __shfl_up(iq, o), xp = __shfl_up(ip, o);
-      if (lane >= o) {
-        iq += xq;
-        ip += xp;
-      }
-    }
-    const int q0 = q_ex0 + iq - dq, p0 = p_ex0 + ip - dp;
+    const int iq = ganon_wave::incl_sum(dq), ip = ganon_wave::incl_sum(dp);
+    const int q0 = q + iq - dq, p0 = p + ip - dp;
     const int n = (al && q0 < L) ? min(len, L - q0) : 0;
     const int c = (n + kSegMaxLen - 1) / kSegMaxLen;   // pieces
-    int ic = c;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int x = __shfl_up(ic, o);
-      if (lane >= o) ic += x;
-    }
+    const int ic = ganon_wave::incl_sum(c);
     int64_t pc = slot + ic - c;
     for (int o = 0; o < n; o += kSegMaxLen) {
       const int m = min(kSegMaxLen, n - o);
@@ -1141,9 +1125,9 @@ __device__ __forceinline__ void wave_walk(const Raw &R, int r, bool mine, int jl
                              (int)((uint32_t)jl | ((uint32_t)(p0 + o - ss) << 12)));
       any_dirty |= !ref_clean(bad, n_blk, (int64_t)rf, m);
     }
-    slot += __shfl(ic, 63);
-    q += __shfl(iq, 63);
-    p += __shfl(ip, 63);
+    slot += ganon_wave::last(ic);
+    q += ganon_wave::last(iq);
+    p += ganon_wave::last(ip);
   }
   if (__any(any_dirty) && lane == 0) atomicOr(dirty, 1ull);
 }

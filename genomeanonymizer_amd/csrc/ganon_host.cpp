@@ -1026,3 +1026,5 @@ GANON_HOST_API int64_t ganon_gather_ranges(const char *src, int64_t src_len, int
   }
   return at[n];
 }
+
+GANON_HOST_API const char *ganon_host_inflate_backend(void) { return libdeflate() ? "libdeflate" : "zlib"; }

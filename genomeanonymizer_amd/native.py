@@ -224,7 +224,7 @@ EXPORTED_HIP_SYMBOLS = (
 )
 EXPORTED_HOST_SYMBOLS = (
     "ganon_bam_open", "ganon_bam_view_get", "ganon_bam_error", "ganon_bam_close",
-    "ganon_host_last_error", "ganon_fastq_format", "ganon_pack_nt16",
+    "ganon_host_last_error", "ganon_host_inflate_backend", "ganon_fastq_format", "ganon_pack_nt16",
     "ganon_plan_run", "ganon_plan_view_get", "ganon_plan_free", "ganon_plan_last_error", "ganon_io_replay",
     "ganon_bam_reader_open", "ganon_bam_reader_set_window", "ganon_bam_reader_has_index", "ganon_bam_reader_header",
     "ganon_bam_reader_contig", "ganon_bam_reader_close",
@@ -1232,6 +1232,7 @@ def host_lib():
     lib.ganon_bam_reader_close.argtypes = [_p]
     lib.ganon_bam_reader_set_inflater.argtypes = [_p, _p, _p, C.c_int64]
     lib.ganon_host_last_error.restype = C.c_char_p
+    lib.ganon_host_inflate_backend.restype = C.c_char_p
     lib.ganon_fastq_format.restype = C.c_int64
     lib.ganon_fastq_format.argtypes = [C.c_int64, C.POINTER(_u8p), _u8p, _i64p, _i32p, _u8p, C.POINTER(_u8p),
                                        _u8p, _i64p, _i32p, _u8p, C.c_char_p, _i64p, _i32p, _u8p, C.c_char_p,

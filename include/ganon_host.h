@@ -59,6 +59,9 @@ GANON_HOST_API int ganon_bam_view_get(ganon_bam *bam, ganon_bam_view *view);
 GANON_HOST_API const char *ganon_bam_error(ganon_bam *bam);
 GANON_HOST_API void ganon_bam_close(ganon_bam *bam);
 GANON_HOST_API const char *ganon_host_last_error(void);
+/* The host BGZF inflater in use: "libdeflate" (the system libdeflate.so.0, loaded at run time) or
+ * "zlib" (no libdeflate, or GANON_INFLATE=zlib in the environment at the first decode). */
+GANON_HOST_API const char *ganon_host_inflate_backend(void);
 
 /* Contig reader: bounded-memory decode of one reference sequence at a time (the records of BAM tid
  * `tid`, file order). Seeks through the BAM index (<path>.bai or <path minus .bam>.bai) when one

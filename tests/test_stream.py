@@ -303,3 +303,66 @@ def test_one_pair_per_rank(tmp_path):
     for p in pairs:
         got = _outputs((p["out"] + "/tumor", p["out"] + "/normal"), p["N"] + ".statistics.txt")
         assert got == one
+
+
+_DIGEST = r"""
+import hashlib, sys
+sys.path.insert(0, sys.argv[1])
+from genomeanonymizer_amd import native
+from genomeanonymizer_amd.io.bam import BamReader, ReadTable
+h = hashlib.sha256()
+for path in sys.argv[2:]:
+    full = ReadTable(path, threads=3)
+    R = BamReader(path, threads=2, window=1 << 17)
+    for t in [full] + [R.contig(i) for i in range(len(full.ref_names))]:
+        for f in ("pos", "end", "flag", "l_seq", "n_cigar", "name_len", "cigar", "seq", "qual", "aux", "names_blob"):
+            h.update(getattr(t, f).tobytes())
+    R.close()
+print(native.host_lib().ganon_host_inflate_backend().decode(), h.hexdigest())
+"""
+
+
+def test_libdeflate_and_zlib_inflaters_decode_alike(tmp_path):
+    """The host inflater (the system libdeflate when present, else zlib; GANON_INFLATE=zlib forces
+    zlib) decodes every field alike, whole-file and contig by contig; the views of the decoder's
+    buffers outlive the reader."""
+    import subprocess
+    import sys
+    from genomeanonymizer_amd.synth.generate import generate, scenario
+    paths = generate(dataclasses.replace(scenario("edge"), bam_index=True), str(tmp_path / "in"))
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = {}
+    for mode in ("default", "zlib"):
+        env = dict(os.environ)
+        env.pop("GANON_INFLATE", None)
+        if mode == "zlib":
+            env["GANON_INFLATE"] = "zlib"
+        r = subprocess.run([sys.executable, "-c", _DIGEST, repo, paths["T"], paths["N"]], env=env,
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        out[mode] = r.stdout.split()
+    assert out["zlib"][0] == "zlib"
+    if os.path.exists("/usr/lib/x86_64-linux-gnu/libdeflate.so.0"):
+        assert out["default"][0] == "libdeflate"
+    assert out["default"][1] == out["zlib"][1]
+
+
+def test_decoded_blobs_are_views_kept_alive(tmp_path):
+    """ReadTable's byte blobs are views of the native decoder's buffers: they stay valid after the
+    table and its reader are gone (the owner is freed with the last view)."""
+    import gc
+    from genomeanonymizer_amd.io.bam import BamReader
+    from genomeanonymizer_amd.synth.generate import generate, scenario
+    paths = generate(scenario("tiny"), str(tmp_path / "in"))
+    R = BamReader(paths["T"], threads=2)
+    t = R.contig(0)
+    seq, qual, names = t.seq, t.qual, t.names_blob
+    ref = (seq.copy(), qual.copy(), names.copy())
+    assert not seq.flags.owndata
+    del t
+    R.close()
+    del R
+    gc.collect()
+    junk = [np.full(1 << 16, 0xAB, np.uint8) for _ in range(64)]   # reuse of freed memory would show
+    assert np.array_equal(seq, ref[0]) and np.array_equal(qual, ref[1]) and np.array_equal(names, ref[2])
+    del junk

@@ -1,6 +1,7 @@
 // ganon_host.cpp — BGZF/BAM decoder to SoA columns and FASTQ formatter (libganon_host.so).
 // See include/ganon_host.h. Written from the SAM/BAM v1 specification.
 #include <dlfcn.h>
+#include <sys/mman.h>
 #include <zlib.h>
 
 #include <algorithm>
@@ -49,6 +50,31 @@ struct NoInit : std::allocator<T> {
 };
 template <class T>
 using RawVec = std::vector<T, NoInit<T>>;
+
+// Large decoder buffers are first touched by the decoder itself: ask for transparent huge pages on
+// them (THP "madvise" mode) so that a chromosome-sized contig does not take a 4 KiB page fault per
+// page of every buffer it fills (measured: a 1 GB contig spent more time faulting its buffers in
+// than inflating). No effect on small buffers or where THP is off.
+inline void huge_advise(void *p, size_t bytes) {
+  constexpr uintptr_t kHuge = 2u << 20;
+  if (bytes < 4 * kHuge) return;
+  const uintptr_t a = ((uintptr_t)p + kHuge - 1) & ~(kHuge - 1), e = ((uintptr_t)p + bytes) & ~(kHuge - 1);
+  if (e > a) madvise(reinterpret_cast<void *>(a), e - a, MADV_HUGEPAGE);
+}
+
+template <class T>
+void huge_resize(RawVec<T> &v, size_t n) {
+  const bool grow = n > v.capacity();
+  v.resize(n);
+  if (grow) huge_advise(v.data(), v.capacity() * sizeof(T));
+}
+
+template <class T>
+void huge_reserve(RawVec<T> &v, size_t n) {
+  if (n <= v.capacity()) return;
+  v.reserve(n);
+  huge_advise(v.data(), v.capacity() * sizeof(T));
+}
 
 struct Block {
   int64_t in_off;   // compressed payload offset in the file buffer
@@ -282,13 +308,13 @@ int records_to_columns(const uint8_t *d, int64_t p, int64_t n, ganon_bam *bam, i
   }
   for (auto *v : {&bam->tid, &bam->pos, &bam->end, &bam->flag, &bam->mapq, &bam->l_seq, &bam->n_cigar, &bam->mate_tid,
                   &bam->mate_pos, &bam->tlen, &bam->name_len, &bam->aux_len})
-    v->resize((size_t)nr);
-  for (auto *v : {&bam->name_off, &bam->cig_off, &bam->seq_off, &bam->qual_off, &bam->aux_off}) v->resize((size_t)nr);
-  bam->names.resize((size_t)o_name[nr]);
-  bam->cigar.resize((size_t)o_cig[nr]);
-  bam->seq.resize((size_t)o_seq[nr]);
-  bam->qual.resize((size_t)o_qual[nr]);
-  bam->aux.resize((size_t)o_aux[nr]);
+    huge_resize(*v, (size_t)nr);
+  for (auto *v : {&bam->name_off, &bam->cig_off, &bam->seq_off, &bam->qual_off, &bam->aux_off}) huge_resize(*v, (size_t)nr);
+  huge_resize(bam->names, (size_t)o_name[nr]);
+  huge_resize(bam->cigar, (size_t)o_cig[nr]);
+  huge_resize(bam->seq, (size_t)o_seq[nr]);
+  huge_resize(bam->qual, (size_t)o_qual[nr]);
+  huge_resize(bam->aux, (size_t)o_aux[nr]);
   run_chunks([&](int64_t i0, int64_t i1) {
     for (int64_t i = i0; i < i1; ++i) {
       const uint8_t *r = d + rec[i] + 4;
@@ -505,7 +531,7 @@ int64_t read_blocks(ganon_bam_reader *R, int64_t coff, int64_t step, RawVec<uint
   }
   if (off == 0) return set_err("truncated BGZF block");
   const size_t base = data.size();
-  data.resize(base + (size_t)total);
+  huge_resize(data, base + (size_t)total);
   if (R->inflater && (int64_t)blocks.size() >= R->inflater_min) {
     const size_t nb = blocks.size();
     std::vector<int64_t> in_off(nb), out_off(nb);
@@ -524,6 +550,24 @@ int64_t read_blocks(ganon_bam_reader *R, int64_t coff, int64_t step, RawVec<uint
   }
   for (size_t i = 0; i < blocks.size(); ++i) bmap.emplace_back((int64_t)base + blocks[i].out_off, bcoff[i]);
   return coff + off;
+}
+
+// memcpy split over up to `threads` threads for large runs (a contig's records are copied out of
+// each inflated window once; one thread copying and faulting in a GB-sized buffer was a third of the
+// decode of a chromosome-sized contig).
+void parallel_copy(uint8_t *dst, const uint8_t *src, size_t n, int threads) {
+  constexpr size_t kPer = 4u << 20;
+  const int nt = (int)std::min<size_t>((size_t)std::max(1, std::min(threads, 16)), (n + kPer - 1) / kPer);
+  if (nt <= 1) {
+    copy_bytes(dst, src, n);
+    return;
+  }
+  const size_t per = (n + nt - 1) / nt;
+  std::vector<std::thread> pool;
+  for (int t = 1; t < nt; ++t)
+    pool.emplace_back([=] { copy_bytes(dst + t * per, src + t * per, std::min(per, n - std::min(n, t * per))); });
+  copy_bytes(dst, src, std::min(per, n));
+  for (auto &th : pool) th.join();
 }
 
 int64_t voff_at(const std::vector<std::pair<int64_t, int64_t>> &bmap, int64_t x) {
@@ -569,7 +613,12 @@ int scan_tid(ganon_bam_reader *R, int64_t voff, int32_t tid, int64_t hint, RawVe
     step = std::min<int64_t>(2 * step, R->chunk);
     int64_t run0 = -1;   // first byte of the current run of `tid` records (copied to kept at once)
     auto flush = [&]() {
-      if (run0 >= 0) kept.insert(kept.end(), data.begin() + run0, data.begin() + dpos);
+      if (run0 >= 0) {
+        const size_t n = (size_t)(dpos - run0), at = kept.size();
+        if (at + n > kept.capacity()) huge_reserve(kept, std::max(2 * kept.capacity(), at + n));
+        kept.resize(at + n);
+        parallel_copy(kept.data() + at, data.data() + run0, n, R->threads);
+      }
       run0 = -1;
     };
     for (;;) {
@@ -746,6 +795,9 @@ GANON_HOST_API int ganon_bam_reader_contig(ganon_bam_reader *R, int32_t tid, gan
       } else {
         const int64_t e = R->index_end[(size_t)tid];
         const int64_t hint = e > beg ? (e >> 16) - (beg >> 16) : 0;
+        // the sequence's records, inflated, at ~3.5x their compressed span (address space only: an
+        // underestimate just grows the buffer)
+        huge_reserve(kept, (size_t)hint * 7 / 2 + (1 << 20));
         if (scan_tid(R, beg, tid, hint, kept, next_voff, next_tid, first_tid) != 0) return -1;
         done = first_tid == tid;   // a stale index falls back to the forward scan
         if (!done) kept.clear();

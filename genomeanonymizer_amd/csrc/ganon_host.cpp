@@ -485,6 +485,7 @@ GANON_HOST_API void ganon_bam_close(ganon_bam *b) { delete b; }
 struct ganon_bam_reader {
   FILE *fh = nullptr;
   int64_t fsize = 0;
+  const uint8_t *map = nullptr;      // the whole file mapped read-only (nullptr: fread per window)
   int threads = 8;
   int64_t chunk = 32 << 20;          // compressed bytes read per step
   ganon_bam header;                  // reference list only
@@ -510,16 +511,27 @@ inline int64_t tid_order(int32_t t) { return t < 0 ? (int64_t)INT32_MAX : (int64
 int64_t read_blocks(ganon_bam_reader *R, int64_t coff, int64_t step, RawVec<uint8_t> &data,
                     std::vector<std::pair<int64_t, int64_t>> &bmap) {
   const int64_t want = std::min<int64_t>(std::max<int64_t>(step, 1 << 17), R->fsize - coff);
-  RawVec<uint8_t> comp((size_t)want);
-  if (std::fseek(R->fh, (long)coff, SEEK_SET) != 0 || std::fread(comp.data(), 1, (size_t)want, R->fh) != (size_t)want)
-    return set_err("short read");
+  // the window's compressed bytes: in place in the file mapping (the inflate threads read the page
+  // cache directly; no serial copy, no fresh buffer to fault in per window), else read into a buffer
+  RawVec<uint8_t> buf;
+  const uint8_t *comp;
+  if (R->map) {
+    comp = R->map + coff;
+    const uintptr_t pg = 4096, a = (uintptr_t)comp & ~(pg - 1);
+    madvise(reinterpret_cast<void *>(a), (size_t)((uintptr_t)comp + want - a), MADV_WILLNEED);
+  } else {
+    buf.resize((size_t)want);
+    if (std::fseek(R->fh, (long)coff, SEEK_SET) != 0 || std::fread(buf.data(), 1, (size_t)want, R->fh) != (size_t)want)
+      return set_err("short read");
+    comp = buf.data();
+  }
   std::vector<Block> blocks;
   std::vector<int64_t> bcoff;
   int64_t off = 0, total = 0;
   while (off < want) {
     int64_t blen, in_rel;
     int32_t in_len, isize;
-    const int rc = parse_block(&comp[(size_t)off], want - off, blen, in_rel, in_len, isize);
+    const int rc = parse_block(comp + off, want - off, blen, in_rel, in_len, isize);
     if (rc < 0) return -1;
     if (rc == 0) break;
     if (isize > 0) {
@@ -542,10 +554,10 @@ int64_t read_blocks(ganon_bam_reader *R, int64_t coff, int64_t step, RawVec<uint
       out_off[i] = blocks[i].out_off;
       out_len[i] = blocks[i].out_len;
     }
-    if (R->inflater(R->inflater_user, comp.data(), off, in_off.data(), in_len.data(), out_off.data(), out_len.data(),
+    if (R->inflater(R->inflater_user, comp, off, in_off.data(), in_len.data(), out_off.data(), out_len.data(),
                     (int64_t)nb, data.data() + base, total) != 0)
       return set_err("BGZF inflate failed (inflater)");
-  } else if (!inflate_blocks(comp.data(), blocks, 0, blocks.size(), data.data() + base, R->threads)) {
+  } else if (!inflate_blocks(comp, blocks, 0, blocks.size(), data.data() + base, R->threads)) {
     return set_err("BGZF inflate failed");
   }
   for (size_t i = 0; i < blocks.size(); ++i) bmap.emplace_back((int64_t)base + blocks[i].out_off, bcoff[i]);
@@ -716,6 +728,10 @@ int reader_open_impl(const char *path, int threads, ganon_bam_reader **out) {
   }
   std::fseek(R->fh, 0, SEEK_END);
   R->fsize = (int64_t)std::ftell(R->fh);
+  if (R->fsize > 0 && !std::getenv("GANON_NO_MMAP")) {   // (GANON_NO_MMAP=1: fread per window, A/B)
+    void *m = mmap(nullptr, (size_t)R->fsize, PROT_READ, MAP_PRIVATE, fileno(R->fh), 0);
+    if (m != MAP_FAILED) R->map = static_cast<const uint8_t *>(m);
+  }
   // header: inflate block windows until it is complete
   RawVec<uint8_t> data;
   std::vector<std::pair<int64_t, int64_t>> bmap;
@@ -827,6 +843,7 @@ GANON_HOST_API int ganon_bam_reader_contig(ganon_bam_reader *R, int32_t tid, gan
 
 GANON_HOST_API void ganon_bam_reader_close(ganon_bam_reader *R) {
   if (!R) return;
+  if (R->map) munmap(const_cast<uint8_t *>(R->map), (size_t)R->fsize);
   if (R->fh) std::fclose(R->fh);
   delete R;
 }

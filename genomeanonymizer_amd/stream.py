@@ -63,6 +63,14 @@ def _names_ds(tables, ds: np.ndarray, rows: np.ndarray) -> List[bytes]:
     return out
 
 
+def _pwrite_all(fd: int, data, offset: int) -> None:
+    """os.pwrite until every byte is written (a single call may write fewer bytes)."""
+    mv = memoryview(data)
+    done = 0
+    while done < len(mv):
+        done += os.pwrite(fd, mv[done:], offset + done)
+
+
 def decode_contig(readers, contig: str):
     """The contig's records of both BAMs (io.bam.BamReader.contig)."""
     return tuple(r.contig(r.tid_of(contig)) for r in readers)
@@ -716,6 +724,7 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
     # splice is numpy and native code, the writes are pwrite: both mostly outside the GIL).
     # GANON_WRITER=0 writes in line.
     writer = ThreadPoolExecutor(1) if os.environ.get("GANON_WRITER", "1") != "0" else None
+    file_pool = ThreadPoolExecutor(4)
     pending: list = []          # futures of the writer (or jobs, in line)
     writer_failed = threading.Event()
 
@@ -735,8 +744,11 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
             for f in range(4):
                 if len(data[f]) != res["sizes"][f]:
                     raise RuntimeError(f"job {job.job}: {len(data[f])} bytes for file {f}, {res['sizes'][f]} planned")
-                if data[f]:
-                    os.pwrite(fds[f], data[f], res["offsets"][f])
+            # the four files written concurrently (pwrite drops the GIL; a file system serialises
+            # buffered writes per file, not across files)
+            futs = [file_pool.submit(_pwrite_all, fds[f], data[f], res["offsets"][f]) for f in range(4) if data[f]]
+            for fu in futs:
+                fu.result()
             stats_rows.append((job.job, job.stats()))
             timing["write_s"] += time.time() - t1
         except BaseException:
@@ -814,6 +826,7 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
     finally:
         if writer is not None:
             writer.shutdown(wait=True)
+        file_pool.shutdown(wait=True)
         if pool is not None:      # prefetches still running (a failed job) end before their reader closes
             for f in ahead.values():
                 f.cancel()

@@ -11,6 +11,7 @@ Prints one JSON line with per-stage seconds, reads/s, bases/s and the process's 
     E2E_RUNS=N ...           # timed runs per mode after one untimed warm run (default 1)
     E2E_PROFILE=PREFIX ...   # cProfile of the timed run of each mode -> PREFIX_<mode>.txt (main thread)
     GANON_PREFETCH=N ...     # look-ahead planning threads of the streamed path (0: in line)
+    E2E_DECODE_THREADS=T ... # host decode threads per process (default 16 / E2E_WORKERS)
     E2E_WORKERS=P ...        # the streamed path in P processes sharing the GPU (torch.distributed.run,
                              # gloo; the contigs sharded over them as over the ranks of a multi-GPU run,
                              # host decode threads 16 / P each); wall = the slowest rank's
@@ -86,7 +87,7 @@ def main():
     modes = sys.argv[3].split(",") if len(sys.argv) > 3 else ["stream", "whole"]
     if dist is not None and modes != ["stream"]:
         sys.exit("E2E_WORKERS > 1 runs the streamed path only")
-    threads = max(1, 16 // workers)
+    threads = int(os.environ.get("E2E_DECODE_THREADS", "0")) or max(1, 16 // workers)
     n_timed = int(os.environ.get("E2E_RUNS", "1"))
     for mode in modes:
         runs = []

@@ -506,6 +506,17 @@ def scenario(name: str) -> ScenarioConfig:
             germline_snp_per_kb=3.0, germline_indel_per_kb=6.0, hom_fraction=0.5,
             error_rate=0.01, softclip_frac=0.2, n_base_frac=0.2, unmapped_mate_frac=0.05,
             unplaced_frac=0.3, cross_contig_pairs=3)
+    if name == "long2":
+        # configs[4]-length reads file to file: 15 kb paired reads (ONT-like 2 % substitutions, dense
+        # germline indels: ~100-200 CIGAR ops per read), 34 kb fragments
+        return ScenarioConfig(
+            name="long2", seed=43,
+            contigs=[ContigSpec("ont1", 150_000, 10, windows=[20000, 70000, 120000], keep_windows=1),
+                     ContigSpec("ont2", 90_000, 5, windows=[45000])],
+            read_len=15_000, insert_mean=34_000.0, insert_sd=3000.0,
+            germline_snp_per_kb=2.0, germline_indel_per_kb=5.0, hom_fraction=0.5,
+            error_rate=0.02, softclip_frac=0.3, n_base_frac=0.3, unmapped_mate_frac=0.05,
+            unplaced_frac=0.5, cross_contig_pairs=2)
     if name == "tiny":
         return ScenarioConfig(
             name="tiny", seed=3,

@@ -535,6 +535,14 @@ GANON_API int ganon_inflate(ganon_ctx *ctx, const uint8_t *comp, int64_t comp_le
                                                                       !out_len || !out)))
     return fail(ctx, GANON_E_ARG, "ganon_inflate: bad arguments");
   if (!n_blocks) return GANON_OK;
+  // every block inside both buffers before any span is computed from them: the host copies of a
+  // chunk are sized from its first and last block only
+  for (int64_t i = 0; i < n_blocks; ++i)
+    if (in_off[i] < 0 || in_len[i] < 0 || out_off[i] < 0 || out_len[i] < 0 || in_off[i] + in_len[i] > comp_len ||
+        out_off[i] + out_len[i] > out_total) {
+      if (first_bad) *first_bad = i;
+      return fail(ctx, GANON_E_ARG, "ganon_inflate: block %lld lies outside the buffers", (long long)i);
+    }
   if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, GANON_E_DEVICE, "hipSetDevice failed");
   if (!ctx->inflate) ctx->inflate = new ganon_inflate_state();
   ganon_inflate_state *st = ctx->inflate;
@@ -613,7 +621,12 @@ GANON_API int ganon_inflate(ganon_ctx *ctx, const uint8_t *comp, int64_t comp_le
                          st->in_len + b0, st->out_off + b0, st->out_len + b0, b1 - b0, st->out, out_total,
                          st->status + b0);
     }
-    if ((rc = check_launch(ctx, "k_inflate"))) return rc;
+    if ((rc = check_launch(ctx, "k_inflate"))) {
+      // copies from / into the caller's buffers may still be queued: they end before it gets them back
+      hipStreamSynchronize(cs);
+      hipStreamSynchronize(s);
+      return rc;
+    }
     okc = hipEventRecord(st->ev[2 * c + 1], s) == hipSuccess && (c == 0 || d2h(c - 1));
   }
   std::vector<int32_t> stat(nb);

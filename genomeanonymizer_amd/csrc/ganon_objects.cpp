@@ -156,7 +156,7 @@ struct State {
     if (!left.empty()) flag = true;
   }
   std::string fastq() const {
-    if (!has_seq) oraise(GANON_PLAN_E_UNSUPPORTED, "a read met in two scopes of one contig would be written from its second copy");
+    if (!has_seq) oraise(GANON_PLAN_E_ARG, "internal: an object made from a masked copy that was not carried");
     if (!has_qual) oraise(GANON_PLAN_E_TYPE, "read '" + name + "' has no qualities");
     std::string s = seq, q = qual;
     if (reverse) {

@@ -138,7 +138,7 @@ class Planner {
   std::vector<int64_t> single_[2];    // (row, scope, reapply) triples
   bool write_single_end_ = false;
   std::vector<int64_t> left_;         // contig mode: 11 per unwritten pair (include/ganon_host.h)
-  std::vector<int64_t> cand_;         // contig mode: 5 per pair_unmapped_mates candidate
+  std::vector<int64_t> cand_;         // contig mode: 6 per pair_unmapped_mates candidate
   std::vector<int64_t> objs_;         // contig mode: 10 per object of a complex name
   std::vector<int64_t> obj_rows_;
   std::vector<int64_t> skip_;         // (scope, ds, row) left out of the indel tally
@@ -158,6 +158,7 @@ class Planner {
   bool cmode_ = false;
   std::vector<uint8_t> cross_;        // per name id (contig mode)
   std::vector<uint8_t> cx_;           // per name id: complex (SA tag / secondary / supplementary record)
+  std::vector<uint8_t> slot_seen_;    // per name id: mate slots of its plain records (contig mode)
   std::unordered_set<int64_t> written_;
   int32_t next_hid_ = 0;
 
@@ -189,19 +190,26 @@ class Planner {
       if (cmode_) {
         cross_.resize(ids.size(), 0);
         cx_.resize(ids.size(), 0);
+        slot_seen_.resize(ids.size(), 0);
         for (int64_t r = 0; r < t.n; ++r) {
           const size_t nm = (size_t)nid_[d][r];
           if (t.tid[r] < 0 || t.mate_tid[r] != t.tid[r]) cross_[nm] = 1;
+          // two plain records of one mate (a duplicated record): the reference keeps one object per
+          // mate and scope, which the object model of complex names restates (AM:320-348)
+          const int ms = complex_rec(d, r) ? -1 : tab_[d].mate_idx(r);
+          if (ms >= 0) {
+            if (slot_seen_[nm] & (1 << ms)) cx_[nm] = cross_[nm] = 1;
+            slot_seen_[nm] |= (uint8_t)(1 << ms);
+          }
           if (complex_rec(d, r)) {
-            // a secondary alignment off its mate's contig: the name's other records may be planned
-            // as local elsewhere, where nothing tells that this object exists
-            if ((t.flag[r] & kFlagSecondary) && t.mate_tid[r] >= 0 && t.mate_tid[r] != t.tid[r])
-              raise(GANON_PLAN_E_UNSUPPORTED, "secondary alignment of '" + tab_[d].name(r) +
-                                                  "' on another reference sequence than its mate");
+            // (a secondary alignment off its mate's contig is settled sample-wide: the caller forces
+            // its name cross on the mate's contig when it comes later, ganon_resolver_mark_written
+            // covers a mate's contig planned before)
             cx_[nm] = 1;
             cross_[nm] = 1;
           }
         }
+        if (d == 1) force_cross(ids);
       } else {
         for (int64_t r = 0; r < t.n; ++r)
           if (complex_rec(d, r))
@@ -218,6 +226,13 @@ class Planner {
                                       " read names occur in both the tumor and the normal BAM; the reference keys "
                                       "reads by name only and mixes such reads (SURVEY Q10)");
       }
+    }
+  }
+
+  void force_cross(const std::unordered_map<std::string_view, int64_t> &ids) {
+    for (int64_t k = 0; k < in_->n_force; ++k) {
+      auto it = ids.find(std::string_view(in_->force_names + in_->force_off[k], (size_t)in_->force_len[k]));
+      if (it != ids.end()) cross_[(size_t)it->second] = 1;
     }
   }
 
@@ -848,17 +863,17 @@ class Planner {
         try {
           fetch(ds, in_->win_contig[w], true, in_->win_first[w] - 1, true, in_->win_last[w], rows);
         } catch (const PlanError &) {
-          cand_.insert(cand_.end(), {w, -1, in_->win_first[w] - 1, -1, 0});   // raises if reached
+          cand_.insert(cand_.end(), {w, -1, in_->win_first[w] - 1, -1, 0, 0});   // raises if reached
           break;
         }
         for (int64_t r : rows) {
           if (!tab_[ds].unmapped(r)) continue;
           const int64_t nm = nid_[ds][(size_t)r];
           if (!cross_[(size_t)nm] && !pending.count(nm)) continue;
-          if (complex_rec(ds, r))
-            raise(GANON_PLAN_E_UNSUPPORTED, "unmapped secondary / supplementary record or SA tag ('" +
-                                                tab_[ds].name(r) + "')");
-          cand_.insert(cand_.end(), {w, ds, r, tab_[ds].mate_idx(r), in_->tables[ds].l_seq[r] == 0 ? 1 : 0});
+          // the AnonymizedRead this record creates or updates at the end of the sample (AM:98-108)
+          const int32_t nsa = n_sa(ds, r);
+          const int64_t info = (supp_rec(ds, r) ? 1 : 0) | (nsa >= 0 ? 2 : 0) | ((int64_t)std::max(nsa, 0) << 8);
+          cand_.insert(cand_.end(), {w, ds, r, tab_[ds].mate_idx(r), in_->tables[ds].l_seq[r] == 0 ? 1 : 0, info});
         }
       }
     }
@@ -915,6 +930,10 @@ GANON_HOST_API int ganon_plan_run(const ganon_plan_input *in, ganon_plan **out) 
                           (in->tables[0].n > 0 && !in->tables[0].mate_tid) ||
                           (in->tables[1].n > 0 && !in->tables[1].mate_tid))) {
     g_err = "contig mode: bad contig or missing mate_tid";
+    return GANON_PLAN_E_ARG;
+  }
+  if (in->n_force < 0 || (in->n_force > 0 && (!in->contig_mode || !in->force_names || !in->force_off || !in->force_len))) {
+    g_err = "bad forced cross names";
     return GANON_PLAN_E_ARG;
   }
   for (int32_t w = 0; w < in->n_windows; ++w)
@@ -987,7 +1006,7 @@ GANON_HOST_API int ganon_plan_view_get(const ganon_plan *pl, ganon_plan_view *v)
   v->write_single_end = p.write_single_end_ ? 1 : 0;
   v->n_left = (int64_t)p.left_.size() / 11;
   v->left = p.left_.data();
-  v->n_cand = (int64_t)p.cand_.size() / 5;
+  v->n_cand = (int64_t)p.cand_.size() / 6;
   v->cand = p.cand_.data();
   v->n_objs = (int64_t)p.objs_.size() / 10;
   v->objs = p.objs_.data();
@@ -1305,6 +1324,27 @@ GANON_HOST_API int ganon_resolver_contig(ganon_resolver *r, int32_t job, int64_t
   return GANON_PLAN_OK;
 }
 
+GANON_HOST_API int64_t ganon_resolver_mark_written(ganon_resolver *r, int64_t n, const char *names,
+                                                   const int64_t *name_off, const int32_t *name_len) {
+  if (!r || n < 0 || (n > 0 && (!names || !name_off || !name_len))) {
+    g_err = "resolver: bad argument";
+    return GANON_PLAN_E_ARG;
+  }
+  int64_t marked = 0;
+  try {
+    for (int64_t k = 0; k < n; ++k) {
+      std::string name(names + name_off[k], (size_t)name_len[k]);
+      if (r->to_pair.count(name) || r->written.count(name)) continue;
+      r->written.insert(std::move(name));
+      ++marked;
+    }
+  } catch (const std::bad_alloc &) {
+    g_err = "out of memory";
+    return GANON_PLAN_E_NOMEM;
+  }
+  return marked;
+}
+
 GANON_HOST_API int64_t ganon_resolver_take_log(ganon_resolver *r, int64_t *out, int64_t cap) {
   if (!r) return GANON_PLAN_E_ARG;
   const int64_t n = (int64_t)r->log.size() / 8;
@@ -1374,7 +1414,15 @@ GANON_HOST_API int ganon_resolver_finish(ganon_resolver *r, int64_t n_cand, cons
         }
         const RInst rec{c[0], c[2], -1, c[3]};
         r->quiet = r->written.count(name) != 0;
-        *n_tail += r->passthrough(name, (int)c[4], plain_obj(rec), rec, false, INT64_MAX, tail + 7 * *n_tail);
+        // an unmapped record flagged supplementary or carrying an SA tag creates an object with that
+        // state (AnonymizedRead.__init__, AM:98-108): incomplete until its primary / supplementaries
+        RObj nw = plain_obj(rec);
+        const bool rsupp = (c[6] & 1) != 0;
+        nw.supp = rsupp;
+        nw.has_sa = (c[6] & 2) != 0;
+        nw.n_sa = (int32_t)(c[6] >> 8);
+        if (rsupp && nw.has_sa) nw.add_hash(record_id(rec.job, rec.ds, rec.row));
+        *n_tail += r->passthrough(name, (int)c[4], std::move(nw), rec, rsupp, INT64_MAX, tail + 7 * *n_tail);
       }
     }
     r->quiet = false;

@@ -134,7 +134,12 @@ def anonymize_genome_sharded(windows: List[Window], tumor_bam: str, normal_bam: 
     anonymizer = anonymizer or CompleteGermlineAnonymizer(device=int(os.environ.get("LOCAL_RANK", 0)))
     timing = anonymize_genome_streaming(windows, tumor_bam, normal_bam, FastaRef(ref_file), anonymizer, tumor_out,
                                         normal_out, record_statistics, threads, dist=dist)
+    global LAST_TIMING
+    LAST_TIMING = timing
     return timing["totals"]
+
+
+LAST_TIMING: dict = {}   # the stage timing of this process's last anonymize_genome_sharded (tests, tools)
 
 
 def run_pairs_sharded(vcfs: Sequence[str], samples: Sequence[tuple], ref_file: str,

@@ -84,13 +84,15 @@ def run_anonymizer(argv=None) -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    # launched by torchrun (any world size, one included): the process-group path
+    launched = world > 1 or ("RANK" in os.environ and "MASTER_ADDR" in os.environ)
     n_dev = 1
-    if world > 1:
+    if launched:
         import torch
         n_dev = max(1, torch.cuda.device_count())   # (counting devices does not initialise the GPU)
     device = config.device if config.device is not None else local % n_dev
     anonymizer = CompleteGermlineAnonymizer(device=device)
-    if world > 1:
+    if launched:
         import torch.distributed as dist
         from .distributed import run_pairs_sharded
         if local_world > n_dev:   # ranks share a GPU: RCCL takes one rank per device
@@ -98,6 +100,8 @@ def run_anonymizer(argv=None) -> None:
         else:
             torch.cuda.set_device(device)
             dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        logging.info("rank %d of %d: process group backend %s", dist.get_rank(), dist.get_world_size(),
+                     dist.get_backend())
         # one pair per GPU when there are enough pairs, else each pair's contigs over all GPUs
         tots = run_pairs_sharded(vcfs, samples, config.reference, anonymizer, outputs, bool(config.record_statistics),
                                  dist, threads=max(1, config.cpu))

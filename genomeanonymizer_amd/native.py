@@ -229,7 +229,7 @@ EXPORTED_HOST_SYMBOLS = (
     "ganon_bam_reader_open", "ganon_bam_reader_set_window", "ganon_bam_reader_has_index", "ganon_bam_reader_header",
     "ganon_bam_reader_contig", "ganon_bam_reader_close",
     "ganon_resolver_create", "ganon_resolver_free", "ganon_resolver_contig", "ganon_resolver_pending",
-    "ganon_resolver_finish", "ganon_resolver_take_log", "ganon_objects_pack", "ganon_blob_size", "ganon_blob_data",
+    "ganon_resolver_finish", "ganon_resolver_take_log", "ganon_resolver_mark_written", "ganon_objects_pack", "ganon_blob_size", "ganon_blob_data",
     "ganon_blob_free", "ganon_objects_create", "ganon_objects_free", "ganon_objects_add_job", "ganon_objects_add_plain",
     "ganon_objects_run", "ganon_objects_take", "ganon_objects_settle", "ganon_objects_last_error",
     "ganon_objects_take_all", "ganon_aux_sa_count", "ganon_fastq_edit", "ganon_gather_ranges",
@@ -830,7 +830,8 @@ class PlanInput(C.Structure):
     _fields_ = [("tables", PlanTable * 2), ("n_contigs", C.c_int32), ("contig_len", _i64p),
                 ("contig_names", _p), ("contig_name_off", _i64p), ("n_windows", C.c_int32),
                 ("win_contig", _i32p), ("win_first", _i64p), ("win_last", _i64p),
-                ("contig_mode", C.c_int32), ("only_contig", C.c_int32)]
+                ("contig_mode", C.c_int32), ("only_contig", C.c_int32), ("n_force", C.c_int64),
+                ("force_names", _p), ("force_off", _i64p), ("force_len", _i32p)]
 
 
 class PlanView(C.Structure):
@@ -854,11 +855,13 @@ def _np_copy(ptr, n: int, dtype) -> np.ndarray:
     return np.ctypeslib.as_array(ptr, shape=(int(n),)).astype(dtype, copy=True)
 
 
-def plan_sample(tables, contig_names, contig_lens, win_contig, win_first, win_last, only_contig=None) -> dict:
+def plan_sample(tables, contig_names, contig_lens, win_contig, win_first, win_last, only_contig=None,
+                force_names=()) -> dict:
     """``ganon_plan_run`` over two ReadTables (io/bam.py) and the variant windows. Returns the
     plan's column arrays (copies); raises ValueError / TypeError / planner.UnsupportedInput as
     the reference's own code would (message from the library). ``only_contig``: contig mode for
-    that FASTA contig (tables holding its records only), see include/ganon_host.h."""
+    that FASTA contig (tables holding its records only), see include/ganon_host.h; ``force_names``
+    (bytes): names planned as cross names there (``ganon_plan_input.force_names``)."""
     lib = host_lib()
     keep = []
 
@@ -899,6 +902,10 @@ def plan_sample(tables, contig_names, contig_lens, win_contig, win_first, win_la
     inp.win_last = arr(win_last, np.int64)
     inp.contig_mode = 0 if only_contig is None else 1
     inp.only_contig = -1 if only_contig is None else int(only_contig)
+    force_names = list(force_names)
+    if force_names:
+        inp.n_force = len(force_names)
+        inp.force_names, inp.force_off, inp.force_len = _names_args(force_names, keep)
     h = _p()
     rc = lib.ganon_plan_run(C.byref(inp), C.byref(h))
     if rc != 0:
@@ -934,7 +941,7 @@ def plan_sample(tables, contig_names, contig_lens, win_contig, win_first, win_la
         out["single"] = [_np_copy(v.single[d], 3 * int(v.n_single[d]), np.int64).reshape(-1, 3) for d in (0, 1)]
         out["write_single_end"] = bool(v.write_single_end)
         out["left"] = _np_copy(v.left, 11 * int(v.n_left), np.int64).reshape(-1, 11)
-        out["cand"] = _np_copy(v.cand, 5 * int(v.n_cand), np.int64).reshape(-1, 5)
+        out["cand"] = _np_copy(v.cand, 6 * int(v.n_cand), np.int64).reshape(-1, 6)
         out["objs"] = _np_copy(v.objs, 10 * int(v.n_objs), np.int64).reshape(-1, 10)
         out["obj_rows"] = _np_copy(v.obj_rows, int(v.n_obj_rows), np.int64)
         out["skip"] = _np_copy(v.skip, 3 * int(v.n_skip), np.int64).reshape(-1, 3)
@@ -995,6 +1002,18 @@ class Resolver:
         if rc != 0:
             self._err(rc)
         return out_n[:n], out_w[:n]
+
+    def mark_written(self, names: list) -> int:
+        """``ganon_resolver_mark_written``: the names it has no state for count as written (their
+        contig planned them locally and wrote them); returns how many were marked."""
+        if not names:
+            return 0
+        keep = []
+        nb, no, nl = _names_args(list(names), keep)
+        rc = self._lib.ganon_resolver_mark_written(self._h, len(names), nb, no, nl)
+        if rc < 0:
+            self._err(rc)
+        return int(rc)
 
     def take_log(self) -> np.ndarray:
         """The object log entries made since the last call ([n, 8] int64, include/ganon_host.h)."""
@@ -1270,6 +1289,8 @@ def host_lib():
     lib.ganon_fastq_edit.argtypes = [C.c_int64, C.c_char_p, _i64p, _u8p, _i32p, _i64p, _i64p, C.c_char_p, _i64p,
                                      _p, C.c_int64, _i64p, _i64p]
     lib.ganon_objects_last_error.restype = C.c_char_p
+    lib.ganon_resolver_mark_written.argtypes = [_p, C.c_int64, _p, _i64p, _i32p]
+    lib.ganon_resolver_mark_written.restype = C.c_int64
     lib.ganon_resolver_take_log.argtypes = [_p, _i64p, C.c_int64]
     lib.ganon_resolver_take_log.restype = C.c_int64
     lib.ganon_resolver_pending.argtypes = [_p, _i64p, C.c_int64]

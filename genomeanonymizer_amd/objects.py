@@ -159,8 +159,8 @@ class State:
     def fastq(self) -> bytes:
         """get_anonymized_fastq_record (AM:215-243) with the creator's orientation."""
         if self.seq is None:
-            from .planner import UnsupportedInput
-            raise UnsupportedInput("a read met in two scopes of one contig would be written from its second copy")
+            # every masked copy a resolution can name is carried (stream.JobPrep._mask_instances)
+            raise RuntimeError("internal: an object made from a masked copy that was not carried")
         seq = bytes(self.seq)
         if self.qual is None:
             raise TypeError(f"read {self.name.decode()!r} has no qualities")
@@ -247,8 +247,7 @@ class Replay:
         edits = self.carry_info.get((job, ds, scope, row), [])
         rec = self.carry.get((job, ds, scope, row, 2 if edits else 0))
         if rec is None:
-            # a copy of a read met in a second scope: never written (stream.Job.check_instance), it
-            # can only lend its left-over flag / list to the object it updates
+            # not carried: only a copy no write can name (fastq() refuses it)
             st = State(None, None, False, b"", 0)
         else:
             flag = self.carry_info[(job, ds, row)]

@@ -582,6 +582,7 @@ class NativeSamplePlanner(SamplePlanner):
 
     native = True
     only_contig: Optional[int] = None   # contig mode (ContigPlanner)
+    force_names: Sequence[bytes] = ()   # contig mode: names planned as cross names (ContigPlanner)
 
     def run(self) -> Plan:
         from . import native
@@ -590,7 +591,7 @@ class NativeSamplePlanner(SamplePlanner):
         w = self.windows
         res = native.plan_sample(self.tables, refs, list(self.fasta.lengths),
                                  [cidx[x.sequence] for x in w], [x.first for x in w], [x.last for x in w],
-                                 only_contig=self.only_contig)
+                                 only_contig=self.only_contig, force_names=self.force_names)
         self.contig_exports = {"left": res["left"], "cand": res["cand"], "objs": res["objs"],
                                "obj_rows": res["obj_rows"]}
         T, N = self.tables
@@ -624,11 +625,14 @@ class ContigPlanner(NativeSamplePlanner):
     """Contig mode of the native planner (include/ganon_host.h ``contig_mode``): plans one FASTA
     contig from tables holding only that contig's records. Pairing operations on names with a
     record on another sequence become placeholder events (kinds 3/4/5) for stream.py's resolver;
-    ``contig_exports`` holds the contig's unwritten pairs and pair_unmapped_mates candidates."""
+    ``contig_exports`` holds the contig's unwritten pairs and pair_unmapped_mates candidates.
+    ``force_names``: names to plan as cross names although their records here say nothing of
+    another sequence (secondary alignments elsewhere whose mate is on this contig, stream.py)."""
 
     def __init__(self, tumor: ReadTable, normal: ReadTable, fasta: FastaRef, windows: Sequence[Window],
-                 contig_index: int):
+                 contig_index: int, force_names: Sequence[bytes] = ()):
         self.only_contig = int(contig_index)
+        self.force_names = sorted(force_names)
         super().__init__(tumor, normal, fasta, windows)
 
 

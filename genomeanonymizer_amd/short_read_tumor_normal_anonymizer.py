@@ -25,7 +25,7 @@ from .anonymizer_methods import CompleteGermlineAnonymizer
 from .io.bam import ReadTable
 from .io.fasta import FastaRef
 from .io.vcf import read_vcf
-from .planner import Window, get_windows, make_planner
+from .planner import UnsupportedInput, Window, get_windows, make_planner
 from .writer import statistics_rows, write_fastqs, write_statistics
 
 log = logging.getLogger("genomeanonymizer_amd")
@@ -72,7 +72,14 @@ def anonymize_genome(windows_in_sample: List[Window], tumor_bam_file: str, norma
                                           available_threads)
     t1 = time.time()
     planner = make_planner(tumor, normal, fasta, windows_in_sample)
-    plan = planner.run()
+    try:
+        plan = planner.run()
+    except UnsupportedInput as e:   # e.g. a duplicated record: the streamed path's object model has it
+        log.info("%s: the sample streams contig by contig", e)
+        from .stream import anonymize_genome_streaming
+        return anonymize_genome_streaming(windows_in_sample, tumor_bam_file, normal_bam_file, fasta, anonymizer,
+                                          tumor_output_fastq, normal_output_fastq, record_statistics,
+                                          available_threads)
     t2 = time.time()
     res = anonymizer.anonymize(planner, plan)
     t3 = time.time()

@@ -32,7 +32,7 @@ from __future__ import annotations
 import os
 import threading
 import time
-from concurrent.futures import ThreadPoolExecutor
+from concurrent.futures import Future, ThreadPoolExecutor
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -42,7 +42,7 @@ from . import objects
 from .anonymizer_methods import CompleteGermlineAnonymizer, MaskResult, build_batch
 from .io.bam import BamReader, ReadTable
 from .io.fasta import FastaRef
-from .planner import ContigPlanner, Plan, Window, UnsupportedInput
+from .planner import ContigPlanner, Plan, Window
 from . import writer as _writer
 from .writer import OUTSIDE_WINDOWS, FastqFormatter, statistics_rows, write_statistics
 
@@ -68,12 +68,65 @@ def _pwrite_all(fd: int, data, offset: int) -> None:
     mv = memoryview(data)
     done = 0
     while done < len(mv):
-        done += os.pwrite(fd, mv[done:], offset + done)
+        n = os.pwrite(fd, mv[done:], offset + done)
+        if n <= 0:
+            raise OSError(f"pwrite wrote nothing at offset {offset + done}")
+        done += n
 
 
-def decode_contig(readers, contig: str):
-    """The contig's records of both BAMs (io.bam.BamReader.contig)."""
-    return tuple(r.contig(r.tid_of(contig)) for r in readers)
+def decode_contig(readers, contig: str, secondaries: "Optional[SecondaryIndex]" = None, job: int = -1):
+    """The contig's records of both BAMs (io.bam.BamReader.contig); with ``secondaries``, the
+    secondary alignments among them whose mate is on another contig are published there before the
+    tables are handed on (the decode runs in job order, so every later job's plan sees them)."""
+    tables = tuple(r.contig(r.tid_of(contig)) for r in readers)
+    if secondaries is not None:
+        secondaries.publish(job, secondaries.scan(tables))
+    return tables
+
+
+class SecondaryIndex:
+    """Secondary alignments off their mate's contig (flag 0x100, mate_tid != tid). Their name's
+    other records say nothing of them, so the contig holding the mate plans that name locally unless
+    told (the reference keeps one pairing state per name for the whole sample, SR:134-165,
+    AM:320-389): a job planned after such a secondary's contig plans the name as a cross name
+    (``forced_for``); a job planned before it wrote the name itself, which the coordinator marks in
+    the resolver when it meets the secondary (``ganon_resolver_mark_written``). The coordinator
+    checks every export against the secondaries of the jobs before it and asks the owner to plan
+    a job again when one was published too late (another rank decoded it)."""
+
+    def __init__(self, readers, contigs: Sequence[str]):
+        idx = {c: i for i, c in enumerate(contigs)}
+        # FASTA job of every BAM tid, per sample (-1: not a FASTA contig)
+        self.job_of_tid = [np.array([idx.get(n, -1) for n in r.ref_names] + [-1], np.int64) for r in readers]
+        self.lock = threading.Lock()
+        self.by_mate: Dict[int, Dict[bytes, int]] = {}   # mate job -> name -> lowest source job
+
+    def scan(self, tables) -> List[Tuple[bytes, int]]:
+        """(name, mate job) of each off-contig secondary alignment of ``tables``."""
+        out: List[Tuple[bytes, int]] = []
+        for d, t in enumerate(tables):
+            if not t.n:
+                continue
+            sel = np.nonzero(((t.flag & 0x100) != 0) & (t.mate_tid >= 0) & (t.mate_tid != t.tid))[0]
+            if not len(sel):
+                continue
+            mj = self.job_of_tid[d][np.minimum(t.mate_tid[sel], len(self.job_of_tid[d]) - 1)]
+            keep = mj >= 0
+            for nm, j in zip(_names(t, sel[keep]), mj[keep].tolist()):
+                out.append((nm, int(j)))
+        return out
+
+    def publish(self, job: int, pairs: List[Tuple[bytes, int]]) -> None:
+        with self.lock:
+            for nm, mj in pairs:
+                d = self.by_mate.setdefault(mj, {})
+                if d.get(nm, 1 << 62) > job:
+                    d[nm] = job
+
+    def forced_for(self, job: int) -> List[bytes]:
+        """Names of published secondaries of earlier jobs whose mate is on ``job``."""
+        with self.lock:
+            return sorted(nm for nm, src in self.by_mate.get(job, {}).items() if src < job)
 
 
 class JobPrep:
@@ -82,14 +135,21 @@ class JobPrep:
     streamed loop runs it for the next contig in a prefetch thread while the current one masks,
     formats and writes (the BGZF inflate and the planner are native and drop the GIL)."""
 
-    def __init__(self, job: int, contig: str, readers, fasta: FastaRef, windows: Sequence[Window], tables=None):
-        """``tables``: the decoded records when a decode thread produced them (a Future)."""
+    def __init__(self, job: int, contig: str, readers, fasta: FastaRef, windows: Sequence[Window], tables=None,
+                 secondaries: Optional[SecondaryIndex] = None, force: Optional[Sequence[bytes]] = None):
+        """``tables``: the decoded records when a decode thread produced them (a Future);
+        ``secondaries``: the run's SecondaryIndex; ``force``: names to plan as cross names (a job
+        planned again), else the secondaries published for this job."""
         self.job = job
         self.contig = contig
         t0 = time.time()
-        self.tables = decode_contig(readers, contig) if tables is None else tables.result()
+        self.tables = decode_contig(readers, contig, secondaries, job) if tables is None else tables.result()
         t1 = time.time()
-        self.planner = ContigPlanner(self.tables[0], self.tables[1], fasta, windows, job)
+        if force is None:
+            force = secondaries.forced_for(job) if secondaries is not None else []
+        self.forced = sorted(set(force))
+        self.offsec = secondaries.scan(self.tables) if secondaries is not None else []
+        self.planner = ContigPlanner(self.tables[0], self.tables[1], fasta, windows, job, self.forced)
         self.plan: Plan = self.planner.run()
         ex = self.planner.contig_exports
         t2 = time.time()
@@ -107,8 +167,11 @@ class JobPrep:
 
     # -- which masked copy of each read the device produces --------------------------------------
     def _mask_instances(self):
-        """One masked scope per read: its local write, else its first placeholder, else its
-        unwritten-pair entry (the instance the sample-wide state can store first)."""
+        """Every masked copy a write of this job or of the sample-wide resolution may name: each
+        read's local write, its placeholders and unwritten-pair entries (a cross name's read met in
+        two scopes of the contig: one copy per scope, build_batch). ``masked_scope`` per read is the
+        first of them (its local write, else its first placeholder, else its unwritten-pair entry):
+        the copy formatted when nothing names another."""
         ev, rows = self.events, self.event_rows
         parts = []
         w = ev[:, 0] == 1
@@ -130,10 +193,10 @@ class JobPrep:
             self.masked_scope[d][r] = s
         keep = np.zeros(len(ds), bool)
         if len(ds):
-            key = ds * (1 << 40) + rw
-            _, first = np.unique(key, return_index=True)
-            keep[first] = True
+            _, first = np.unique(FastqFormatter._key(ds, rw, sc), return_index=True)
+            keep[np.sort(first)] = True     # every distinct copy, first occurrences first
         ds, rw, sc = ds[keep], rw[keep], sc[keep]
+        self.masked_keys = np.unique(FastqFormatter._key(ds, rw, sc))
         c = self._complex_incidences()      # every (alignment, scope) of a complex name: one copy each
         if len(c):
             ds, rw, sc = np.concatenate([ds, c[:, 0]]), np.concatenate([rw, c[:, 1]]), np.concatenate([sc, c[:, 2]])
@@ -162,13 +225,13 @@ class Job(JobPrep):
     bytes."""
 
     def __init__(self, job: int, contig: str, readers, fasta: FastaRef, windows: Sequence[Window],
-                 anonymizer: CompleteGermlineAnonymizer, prepared=None):
+                 anonymizer: CompleteGermlineAnonymizer, prepared=None, secondaries: Optional[SecondaryIndex] = None):
         """``prepared``: a ``concurrent.futures.Future`` of this job's JobPrep when the caller
         prefetched it; decode_s is then the time spent waiting for it and prefetch_s the time the
         thread spent (decode + plan + batch)."""
         t0 = time.time()
         if prepared is None:
-            JobPrep.__init__(self, job, contig, readers, fasta, windows)
+            JobPrep.__init__(self, job, contig, readers, fasta, windows, secondaries=secondaries)
             t_dec, t_pl, t_b = self.prep_timing
             hidden = 0.0
         else:
@@ -176,18 +239,21 @@ class Job(JobPrep):
             t_dec, t_pl, t_b = time.time() - t0, 0.0, 0.0
             hidden = sum(self.prep_timing)
         t2 = time.time()
-        self.res: MaskResult = anonymizer.anonymize(self.planner, self.plan, written=self.written, batch=self.batch,
-                                                    lazy_seq=True)
-        self.batch = None
-        t3 = time.time()
-        self.fmt = FastqFormatter(self.tables, self.res, anonymizer.format_fastq,
-                                  getattr(anonymizer, "format_fastq_batch", None))
-        # every read once, as its masked copy (or unmasked): the records this job can write. The
-        # masked bases stay on the device unless a later stage needs them on the host (records left
-        # to on-demand formatting, complex names' objects): fetched now, while the engine's job
-        # batch still holds them
-        if not self.fmt.preformat(*self._format_instances()) or len(self.objs):
-            _ = self.res.seq_out
+        # the device part in one hold of the engine: a job planned again on the writer thread
+        # (SecondaryIndex) must not take the engine's job batch between this mask and its format
+        with anonymizer.lock:
+            self.res: MaskResult = anonymizer.anonymize(self.planner, self.plan, written=self.written,
+                                                        batch=self.batch, lazy_seq=True)
+            self.batch = None
+            t3 = time.time()
+            self.fmt = FastqFormatter(self.tables, self.res, anonymizer.format_fastq,
+                                      getattr(anonymizer, "format_fastq_batch", None))
+            # every read once, as its masked copy (or unmasked): the records this job can write. The
+            # masked bases stay on the device unless a later stage needs them on the host (records
+            # left to on-demand formatting, complex names' objects): fetched now, while the engine's
+            # job batch still holds them
+            if not self.fmt.preformat(*self._format_instances()) or len(self.objs):
+                _ = self.res.seq_out
         t4 = time.time()
         self.cx = self._complex_ingredients()
         self.timing = {"decode_s": t_dec, "plan_s": t_pl, "mask_s": t3 - t2 + t_b, "format_s": t4 - t3,
@@ -217,7 +283,28 @@ class Job(JobPrep):
         rw.append(C[cm, 2].astype(np.int64))
         n_extra = sum(len(x) for x in ds[2:])
         sc.append(np.full(n_extra, -1, np.int64))
+        # the further masked copies of reads met in two scopes (cross names)
+        mk = self.masked_keys
+        if len(mk):
+            m_sc = (mk >> 33) - 1
+            m_ds = (mk >> 32) & 1
+            m_rw = mk & 0xFFFFFFFF
+            other = np.nonzero(np.where(m_ds == 0, self.masked_scope[0][np.where(m_ds == 0, m_rw, 0)] if self.tables[0].n else -1,
+                                        self.masked_scope[1][np.where(m_ds == 1, m_rw, 0)] if self.tables[1].n else -1)
+                               != m_sc)[0]
+            ds.append(m_ds[other])
+            rw.append(m_rw[other])
+            sc.append(m_sc[other])
         return np.concatenate(ds), np.concatenate(rw), np.concatenate(sc)
+
+    def is_masked(self, ds, row, sc) -> np.ndarray:
+        """Whether the device masked copy (dataset, row, scope) (vectorised; scope -1: unmasked)."""
+        k = FastqFormatter._key(ds, row, sc)
+        mk = self.masked_keys
+        if not len(mk):
+            return np.asarray(sc) < 0
+        pos = np.minimum(np.searchsorted(mk, k), len(mk) - 1)
+        return (np.asarray(sc) < 0) | (mk[pos] == k)
 
     def _masked_nibs(self, I: np.ndarray) -> np.ndarray:
         """MaskResult.masked_nib of every (dataset, row, scope) row of ``I``, vectorised."""
@@ -303,10 +390,9 @@ class Job(JobPrep):
         return {"objs": O, "obj_rows": self.obj_rows, "rec": rec, "masks": masks, "indels": indels}
 
     def check_instance(self, ds: int, row: int, scope: int) -> None:
-        if scope >= 0 and self.masked_scope[ds][row] != scope:
-            raise UnsupportedInput(
-                f"read {self.tables[ds].name(row)!r} would be written from two scopes of {self.contig!r} "
-                "(mate fields that disagree with where its records are)")
+        if scope >= 0 and not bool(self.is_masked(np.array([ds]), np.array([row]), np.array([scope]))[0]):
+            raise RuntimeError(f"internal: read {self.tables[ds].name(row)!r} written from scope {scope} of "
+                               f"{self.contig!r}, a copy the device did not mask")
 
     # -- exports for the resolution ---------------------------------------------------------------
     def record_lengths(self, ds, row, sc, reapply=None) -> np.ndarray:
@@ -341,7 +427,7 @@ class Job(JobPrep):
         cand = np.zeros((len(C), 7), np.int64)
         if len(C):
             cand[:, 0] = self.job
-            cand[:, 1:6] = C
+            cand[:, 1:7] = C
         cand_names = [b""] * len(C)
         idx = np.nonzero(cm)[0]
         for i, nm in zip(idx.tolist(), _names_ds(self.tables, C[idx, 1], C[idx, 2])):
@@ -360,8 +446,7 @@ class Job(JobPrep):
         if len(ds):
             _, first = np.unique(FastqFormatter._key(ds, rw, sc), return_index=True)
             first = np.sort(first)
-            ok = np.array([sc[i] < 0 or self.masked_scope[ds[i]][rw[i]] == sc[i] for i in first.tolist()], bool)
-            first = first[ok] if len(first) else first
+            first = first[self.is_masked(ds[first], rw[first], sc[first])] if len(first) else first
             recs = self.format_records(ds[first], rw[first], sc[first])
             edited = []
             for i, b in zip(first.tolist(), recs):
@@ -383,6 +468,7 @@ class Job(JobPrep):
             "left": L, "left_names": _names_ds(self.tables, left_ds, left_row),
             "cand": cand, "cand_names": cand_names, "carry": carry, "carry_info": info,
             "objs": O, "obj_rows": self.obj_rows, "cx": self.cx,
+            "forced": self.forced, "offsec": self.offsec,
         }
 
     # -- output ----------------------------------------------------------------------------------
@@ -437,9 +523,7 @@ class Job(JobPrep):
         chk = np.nonzero(loc & (fin[:, 5] >= 0))[0]   # plain local writes only (gen is ext)
         if len(chk):
             d, r, sc = fin[chk, 4].astype(np.int64), frow[chk], fin[chk, 5].astype(np.int64)
-            ms = np.where(d == 0, self.masked_scope[0][np.where(d == 0, r, 0)] if self.tables[0].n else -1,
-                          self.masked_scope[1][np.where(d == 1, r, 0)] if self.tables[1].n else -1)
-            bad = np.nonzero(ms != sc)[0]
+            bad = np.nonzero(~self.is_masked(d, r, sc))[0]
             if len(bad):
                 i = int(chk[bad[0]])
                 self.check_instance(int(fin[i, 4]), int(frow[i]), int(fin[i, 5]))
@@ -548,6 +632,17 @@ class _Coordinator:
         self.base = [0, 0, 0, 0]
         self.prunes = 0
         self.resolve_s = 0.0
+        self.need_force: Dict[int, set] = {}   # job -> names its plan must treat as cross (SecondaryIndex)
+        self.redos = 0
+        self.marked = 0
+
+    def missing_force(self, exp: dict, k: int) -> List[bytes]:
+        """Names job k's plan had to plan as cross names but did not (a secondary of an earlier job,
+        decoded on another rank after this job was planned): the owner plans it again with them."""
+        need = self.need_force.get(k)
+        if not need:
+            return []
+        return sorted(need - set(exp.get("forced", ())))
 
     def _bytes_of(self, jb: int, d: int, sc: int, r: int, re_: int) -> bytes:
         if sc == -2:        # an object of a complex name (objects.Replay)
@@ -556,13 +651,22 @@ class _Coordinator:
         if b is None and re_:   # a carried record without left-overs: the same bytes
             b = self.carry.get((jb, d, sc, r, 0))
         if b is None:
-            raise UnsupportedInput("a record written across contigs was not carried (its mate fields "
-                                   "disagree with where its records are)")
+            raise RuntimeError(f"internal: record {(jb, d, sc, r)} written across contigs was not carried")
         return b
 
     def resolve(self, exp: dict, k: int) -> dict:
         t0 = time.time()
         e = exp
+        # off-contig secondaries of this job: a mate's contig before it planned the name locally and
+        # wrote it (unless the resolver holds the name: pending, or planned as cross there); a mate's
+        # contig after it must plan the name as a cross name
+        before = [nm for nm, mj in e.get("offsec", ()) if mj < k]
+        if before:
+            self.marked += self.resolver.mark_written(sorted(set(before)))
+        for nm, mj in e.get("offsec", ()):
+            if mj > k:
+                self.need_force.setdefault(mj, set()).add(nm)
+        self.need_force.pop(k, None)
         self.carry.update(e["carry"])
         self.carry_info.update(e["carry_info"])
         self.replay.add_job(e["job"], e["cx"])
@@ -627,7 +731,7 @@ class _Coordinator:
         for f in range(4):
             blob = b"".join(per_file[f])
             if blob:
-                os.pwrite(rank0_fds[f], blob, self.base[f])
+                _pwrite_all(rank0_fds[f], blob, self.base[f])
         if wse:
             for d, path in enumerate(self.paths_single):
                 with open(path, "wb") as fh:
@@ -677,26 +781,62 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
     coord_exc: List[Optional[BaseException]] = [None]
     stats_rows: List[Tuple[int, Dict[str, List[int]]]] = []
     totals = np.zeros(8, np.int64)
+    totals_lock = threading.Lock()
+    secondaries = SecondaryIndex(readers, contigs)
+
+    stash: Dict[int, list] = {}      # exports an owner sent after the job it is planning again
+
+    def recv_export(o: int) -> dict:
+        q = stash.get(o)
+        return q.pop(0) if q else link.recv_export(o)
+
+    def recv_redo(o: int, k: int) -> dict:
+        while True:
+            m = link.recv_export(o)
+            if m.get("err") is not None or m.get("redo_of") == k:
+                return m
+            stash.setdefault(o, []).append(m)
 
     def coordinate() -> None:
-        """Rank 0's coordinator thread: every job in FASTA order, as its export arrives."""
+        """Rank 0's coordinator thread: every job in FASTA order, as its export arrives. When it
+        stops on an error, every rank with a job still unresolved gets the error and answers with
+        an error export of its own (stream loop below); the exports it sent in between are received
+        and dropped, so no send is left without its receive."""
         err = None
+        k = 0
+        failed_owner = -1
         try:
             for k in range(len(contigs)):
                 o = owner[k]
-                exp = link.recv_export(o)
+                exp = recv_export(o)
+                while exp.get("err") is None:
+                    miss = coord.missing_force(exp, k)
+                    if not miss:
+                        break
+                    coord.redos += 1
+                    link.send_resolution(o, {"job": k, "redo": sorted(set(miss) | set(exp.get("forced", ()))),
+                                             "err": None})
+                    exp = recv_redo(o, k)
                 if exp.get("err") is not None:   # the owner failed: its error is its own to report
                     err = exp["err"]
+                    failed_owner = o
                     break
                 link.send_resolution(o, coord.resolve(exp, k))
+                k += 1
             if err is None:
                 coord.finish(fds)
         except BaseException as e:   # reported to every owner still waiting
             coord_exc[0] = e
             err = repr(e)
         if err is not None:
-            for r in range(world):   # every worker still waiting for a resolution stops
+            waiting = sorted({owner[j] for j in range(k, len(contigs))})
+            for r in waiting:        # every worker with a job not resolved stops
                 link.send_resolution(r, {"err": err})
+            for r in waiting:        # ... and answers with its error: drop what it sent before
+                if r == failed_owner:
+                    continue
+                while recv_export(r).get("err") is None:
+                    pass
 
     coord_thread = threading.Thread(target=coordinate, name="ganon-coordinator", daemon=True) if rank == 0 else None
     if coord_thread is not None:
@@ -715,8 +855,8 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
     def submit_upto(i_last: int) -> None:
         while nxt[0] <= min(i_last, len(mine) - 1):
             j = mine[nxt[0]]
-            dec = dec_pool.submit(decode_contig, readers, contigs[j])
-            ahead[j] = pool.submit(JobPrep, j, contigs[j], readers, fasta, windows, dec)
+            dec = dec_pool.submit(decode_contig, readers, contigs[j], secondaries, j)
+            ahead[j] = pool.submit(JobPrep, j, contigs[j], readers, fasta, windows, dec, secondaries)
             nxt[0] += 1
 
     # the writer thread: each exported job, in order, waits for its resolution, splices its bytes and
@@ -728,12 +868,38 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
     pending: list = []          # futures of the writer (or jobs, in line)
     writer_failed = threading.Event()
 
+    redo_readers: list = []
+
+    def redo(job: "Job", force: List[bytes]) -> "Job":
+        """Plan, mask and format ``job`` again with ``force`` planned as cross names (its own
+        readers: the decode thread owns the others) and send its export in place of the first."""
+        if not redo_readers:
+            redo_readers.extend(BamReader(p, threads, window_bytes) for p in (tumor_bam, normal_bam))
+        prep = JobPrep(job.job, job.contig, redo_readers, fasta, windows, secondaries=secondaries, force=force)
+        done = Future()
+        done.set_result(prep)
+        j2 = Job(job.job, job.contig, redo_readers, fasta, windows, anonymizer, done)
+        exp = j2.exports()
+        exp["local_sizes"] = j2.local_sizes()
+        exp["err"] = None
+        exp["redo_of"] = job.job
+        with totals_lock:
+            totals[:] += np.asarray(j2.res.totals, np.int64)[:8] - np.asarray(job.res.totals, np.int64)[:8]
+        link.send_export(exp)
+        j2.release_device()
+        return j2
+
     def finish(job: "Job") -> None:
         if writer_failed.is_set():   # an earlier job failed: its resolution may never come
             return
         try:
             t0 = time.time()
             res = link.recv_resolution()
+            while res.get("redo") is not None and res.get("err") is None:
+                if res["job"] != job.job:
+                    raise RuntimeError(f"redo of job {res['job']} for job {job.job}")
+                job = redo(job, res["redo"])
+                res = link.recv_resolution()
             timing["wait_s"] += time.time() - t0
             if res.get("err") is not None:
                 raise RuntimeError(f"another rank failed: {res['err']}")
@@ -771,7 +937,7 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
                 if pool is not None:
                     submit_upto(i + depth)
                     pre = ahead.pop(j)
-                job = Job(j, contigs[j], readers, fasta, windows, anonymizer, pre)
+                job = Job(j, contigs[j], readers, fasta, windows, anonymizer, pre, secondaries)
                 exp = job.exports()
                 exp["local_sizes"] = job.local_sizes()
                 exp["err"] = None
@@ -780,7 +946,8 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
                 timing["jobs"] += 1
                 timing["reads"] += int(job.tables[0].n + job.tables[1].n)
                 timing["bases"] += int(job.tables[0].l_seq.sum(dtype=np.int64) + job.tables[1].l_seq.sum(dtype=np.int64))
-                totals += np.asarray(job.res.totals, np.int64)[:8]
+                with totals_lock:
+                    totals[:] += np.asarray(job.res.totals, np.int64)[:8]
                 link.send_export(exp)
                 job.release_device()
                 pending.append(job if writer is None else writer.submit(finish, job))
@@ -802,6 +969,8 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
             coord_thread.join()
             timing["resolve_s"] = coord.resolve_s
             timing["prunes"] = coord.prunes
+            timing["redos"] = coord.redos
+            timing["marked_written"] = coord.marked
             if coord_exc[0] is not None:   # rank 0 reports the coordinator's own error
                 failure = coord_exc[0]
         err = repr(failure) if failure is not None else None
@@ -835,6 +1004,8 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
         for fd in fds:
             os.close(fd)
         for r in readers:
+            r.close()
+        for r in redo_readers:
             r.close()
         if coord is not None:
             coord.close()

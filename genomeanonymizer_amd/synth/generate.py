@@ -63,6 +63,9 @@ class ScenarioConfig:
     bam_index: bool = False         # also write <bam>.bai
     chimeric_frac: float = 0.0      # per mapped 150M read: split into a primary + a hard-clipped supplementary (SA tags)
     secondary_frac: float = 0.0     # per mapped read: an extra secondary alignment (flag 0x100) elsewhere
+    secondary_anywhere: bool = False  # secondaries on any contig (else near the mate's contig, BWA-style)
+    unmapped_complex_frac: float = 0.0  # of the placed-unmapped mates: flagged secondary / supplementary or SA-tagged
+    duplicate_frac: float = 0.0     # per record: written twice (a duplicated record, e.g. a BAM merged twice)
 
 
 @dataclasses.dataclass
@@ -254,6 +257,8 @@ def _add_split_alignments(recs, cfg, models, rng):
             out += [prim, supp]
         elif x < cfg.chimeric_frac + cfg.secondary_frac:
             ti = r.mate_tid if r.mate_tid >= 0 else r.tid    # BWA-style: near the mate's contig
+            if cfg.secondary_anywhere:      # e.g. a repeat copy on another chromosome
+                ti = int(rng.integers(0, len(models)))
             spos = int(rng.integers(0, models[ti].spec.length - L - 2))
             sec = BamRecord(r.name, r.flag | 0x100, ti, spos, 0, [("M", L)], r.mate_tid, r.mate_pos, 0, r.seq,
                             list(r.qual))
@@ -373,8 +378,19 @@ def generate(cfg: ScenarioConfig, outdir: str) -> Dict[str, str]:
                         recs.append(BamRecord(name, lflag, ti, lpos, 60, lops, -1, -1, 0, "".join(lseq), lq))
                         recs.append(BamRecord(name, rflag, -1, -1, 0, [], -1, -1, 0, "".join(useq), uq))
                         continue
+                    tags = []
+                    if cfg.unmapped_complex_frac and rng.random() < cfg.unmapped_complex_frac:
+                        # an unmapped record the reference still turns into an object with
+                        # supplementary state (AM:98-108): flagged secondary / supplementary, or an SA tag
+                        kind = int(rng.integers(0, 3))
+                        if kind == 0:
+                            rflag |= 0x100
+                        elif kind == 1:
+                            rflag |= 0x800
+                        else:
+                            tags = [("SA", "Z", f"{models[ti].spec.name},{lpos + 1},+,{cfg.read_len}M,0,0;")]
                     recs.append(BamRecord(name, lflag, ti, lpos, 60, lops, ti, lpos, 0, "".join(lseq), lq))
-                    recs.append(BamRecord(name, rflag, ti, lpos, 0, [], ti, lpos, 0, "".join(useq), uq))
+                    recs.append(BamRecord(name, rflag, ti, lpos, 0, [], ti, lpos, 0, "".join(useq), uq, tags))
                 else:
                     recs.append(BamRecord(name, lflag, ti, lpos, 60, lops, ti, rpos, tlen, "".join(lseq), lq))
                     recs.append(BamRecord(name, rflag, ti, rpos, 60, rops, ti, lpos, -tlen, "".join(rseq), rq))
@@ -398,6 +414,8 @@ def generate(cfg: ScenarioConfig, outdir: str) -> Dict[str, str]:
                                   rng.integers(2, 41, len(sb)).tolist()))
         if cfg.chimeric_frac or cfg.secondary_frac:
             recs = _add_split_alignments(recs, cfg, models, rng)
+        if cfg.duplicate_frac:
+            recs = [x for r in recs for x in ((r, r) if rng.random() < cfg.duplicate_frac else (r,))]
         recs.sort(key=lambda r: (r.tid if r.tid >= 0 else 1 << 30, r.pos, bool(r.flag & 4), r.name,
                                  r.flag & 0xC0, r.flag & 0x900))
         path = os.path.join(outdir, "tumor.bam" if sample == "T" else "normal.bam")
@@ -466,9 +484,15 @@ def fuzz_scenario(seed: int) -> ScenarioConfig:
                           germline_indel_per_kb=float(rng.uniform(1, 4)), hom_fraction=0.3,
                           softclip_frac=0.05, unmapped_mate_frac=0.05, n_base_frac=0.03,
                           unplaced_frac=0.4, cross_contig_pairs=int(rng.integers(5, 30)),
-                          # seeds >= 1000: BWA-style supplementary (SA) and secondary alignments too
+                          # seeds >= 1000: BWA-style supplementary (SA) and secondary alignments too;
+                          # seeds >= 3000: secondaries on any contig (off their mate's contig) and
+                          # placed-unmapped mates that are secondary / supplementary / SA-tagged
                           chimeric_frac=0.15 if seed >= 2000 else 0.03 if seed >= 1000 else 0.0,
-                          secondary_frac=0.08 if seed >= 2000 else 0.02 if seed >= 1000 else 0.0)
+                          secondary_frac=0.08 if seed >= 2000 else 0.02 if seed >= 1000 else 0.0,
+                          secondary_anywhere=seed >= 3000,
+                          unmapped_complex_frac=0.4 if seed >= 3000 else 0.0,
+                          # seeds >= 3500: duplicated records too
+                          duplicate_frac=0.02 if seed >= 3500 else 0.0)
 
 
 def scenario(name: str) -> ScenarioConfig:

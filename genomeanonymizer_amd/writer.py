@@ -47,11 +47,11 @@ class FastqFormatter:
         self._pre = None     # (sorted instance keys, offsets, lengths, bytes) of preformat()
         self._left_keys = None   # sorted keys of the instances with left-over edits
 
-    @property
-    def _seq_bufs(self) -> list:
-        """Sequence buffers: 0 = the masked output (fetched from the device on first use), 1 / 2 =
-        the tumor / normal BAM bases."""
-        return [self.res.seq_out, self.tables[0].seq, self.tables[1].seq]
+    def _seq_bufs(self, masked: bool = True) -> list:
+        """Sequence buffers: 0 = the masked output (fetched from the device on first use, only when
+        some record reads it: ``masked``), 1 / 2 = the tumor / normal BAM bases."""
+        m = self.res.seq_out if masked else np.zeros(1, np.uint8)
+        return [m, self.tables[0].seq, self.tables[1].seq]
 
     @staticmethod
     def _key(ds, row, sc):
@@ -72,17 +72,34 @@ class FastqFormatter:
         seq_off_t = pick("seq_off", np.int64)
         base = np.where(t0, self.res.seq_base[0], self.res.seq_base[1])
         byte_off = np.where(sc >= 0, base + seq_off_t, seq_off_t)
+        if getattr(self.res, "dup_off", None) and n:   # a read masked in a further scope: that scope's copy
+            dk, dv = self._dup_index()
+            k = self._key(ds, row, sc)
+            pos = np.minimum(np.searchsorted(dk, k), len(dk) - 1)
+            hit = (dk[pos] == k) & (sc >= 0)
+            byte_off = np.where(hit, dv[pos], byte_off)
         seq_len = pick("l_seq", np.int32)
         flag = pick("flag", np.int64)
         name_off = pick("name_off", np.int64) + np.where(t0, self._name_base[0], self._name_base[1])
         return {
-            "seq_bufs": self._seq_bufs if seq_bufs else None, "seq_sel": seq_sel, "seq_nib_off": (2 * byte_off).astype(np.int64),
+            "seq_bufs": self._seq_bufs(bool((seq_sel == 0).any())) if seq_bufs else None, "seq_sel": seq_sel,
+            "seq_nib_off": (2 * byte_off).astype(np.int64),
             "seq_len": seq_len, "reverse": pick("is_reverse", np.uint8),
             "qual_bufs": self._qual_bufs, "qual_sel": ds.astype(np.uint8), "qual_off": pick("qual_off", np.int64),
             "qual_len": seq_len.copy(), "qual_rev": np.zeros(n, np.uint8),   # stored order for every read (Q1)
             "names": self._names, "name_len": pick("name_len", np.int32), "name_off": name_off,
             "mate": np.where(flag & 0x40, 1, 2).astype(np.uint8),
         }
+
+    def _dup_index(self):
+        """Sorted instance keys of the further masked copies and their byte offsets in seq_out."""
+        if getattr(self, "_dup", None) is None:
+            k = np.array(list(self.res.dup_off.keys()), np.int64).reshape(-1, 3)
+            v = np.array(list(self.res.dup_off.values()), np.int64)
+            key = self._key(k[:, 0], k[:, 1], k[:, 2])
+            o = np.argsort(key)
+            self._dup = (key[o], v[o])
+        return self._dup
 
     def records(self, recs: Sequence[Tuple[int, int, int]]) -> dict:
         a = np.array(recs, np.int64).reshape(-1, 3)

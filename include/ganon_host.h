@@ -188,6 +188,14 @@ typedef struct ganon_plan_input {
    * (view.cand). */
   int32_t contig_mode;
   int32_t only_contig;
+  /* Contig mode: names planned as cross names although every record of theirs on this contig says
+   * otherwise (n_force names at force_off / force_len; NULL / 0 = none). The caller lists the names of
+   * secondary alignments on earlier contigs whose mate is on this one: the reference's pairing state
+   * for such a name may hold that alignment's object when this contig's records arrive. */
+  int64_t n_force;
+  const char *force_names;
+  const int64_t *force_off;
+  const int32_t *force_len;
 } ganon_plan_input;
 typedef struct ganon_plan ganon_plan;
 typedef struct ganon_plan_view {
@@ -215,8 +223,10 @@ typedef struct ganon_plan_view {
   const int64_t *left;       /* 11 per unwritten pair: clock, has0, ds0, scope0, row0, has1, ds1, scope1, row1,
                                 reapply0, reapply1 */
   int64_t n_cand;
-  const int64_t *cand;       /* 5 per record: window, dataset (-1: this window's fetch raises), row,
-                                slot (-1: no READ1/READ2 flag), 1 if the record has no SEQ */
+  const int64_t *cand;       /* 6 per record: window, dataset (-1: this window's fetch raises), row,
+                                slot (-1: no READ1/READ2 flag), 1 if the record has no SEQ, object info
+                                of the record (bit 0 supplementary, bit 1 has an SA tag, bits 8.. SA
+                                entries: the AnonymizedRead it creates, AM:98-108) */
   /* contig mode, complex names (a record with an SA tag, or a secondary / supplementary alignment):
    * the reference's AnonymizedRead objects (anonymizer_methods.py:84-287) of such a name are planned
    * here and resolved sample-wide. objs: 10 int64 per object: scope (-1: created by a pass-through),
@@ -273,8 +283,13 @@ GANON_HOST_API int64_t ganon_resolver_take_log(ganon_resolver *r, int64_t *out, 
 /* Pending instances (4 int64 each: job, dataset, scope, row; an object: -1, dataset, -2, id); returns
  * the count (all of them when cap >= count, else only the count). */
 GANON_HOST_API int64_t ganon_resolver_pending(ganon_resolver *r, int64_t *out, int64_t cap);
-/* cand: 7 int64 per record (job, window, dataset, row, slot, no-SEQ flag, 0) in window order, with
- * names. tail (14 int64 per candidate) receives the writes of pair_unmapped_mates (count n_tail);
+/* Names written on an earlier contig by a plan that did not treat them as cross names (an off-contig
+ * secondary alignment met later names one: its name's other records said nothing of it). Every name
+ * the resolver has no state for is marked written; returns how many were marked. */
+GANON_HOST_API int64_t ganon_resolver_mark_written(ganon_resolver *r, int64_t n, const char *names,
+                                                   const int64_t *name_off, const int32_t *name_len);
+/* cand: 7 int64 per record (job, window, dataset, row, slot, no-SEQ flag, object info as in
+ * ganon_plan_view.cand) in window order, with names. tail (14 int64 per candidate) receives the writes of pair_unmapped_mates (count n_tail);
  * single[d] (5 int64 per record: job, dataset, scope, row, reapply; capacity = ganon_resolver_pending
  * count) the single ends in dictionary order (counts n_single[2]). Returns GANON_PLAN_OK or GANON_PLAN_E_VALUE / _TYPE with the
  * reference's error (message: ganon_plan_last_error). */

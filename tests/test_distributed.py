@@ -51,13 +51,17 @@ def _worker(rank, world, port, name, workdir, q, engine="oracle", fail_rank=-1, 
                 anon.anonymize = boom
         tot = anonymize_genome_sharded(windows, paths["T"], paths["N"], paths["ref"], name_output(paths["T"]),
                                        name_output(paths["N"]), True, anon, dist)
-        q.put((rank, tot))
+        from genomeanonymizer_amd import distributed
+        q.put((rank, (tot, distributed.LAST_TIMING.get("redos", 0))))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name,index", [("edge", True), ("tiny", False), ("fuzz2003", False)])
-def test_two_rank_contig_shards_match_reference(name, index, tmp_path):
+@pytest.mark.parametrize("name,index,world", [("edge", True, 2), ("tiny", False, 2), ("fuzz2003", False, 2),
+                                              ("fuzz3000", False, 2), ("fuzz3008", True, 3)])
+def test_two_rank_contig_shards_match_reference(name, index, world, tmp_path):
+    """fuzz3000 / fuzz3008 put secondaries off their mate's contig on another rank than the mate:
+    the coordinator has the owner plan such a contig again (SecondaryIndex, stream.py)."""
     from helpers import GOLDEN, run_pipeline_vs_golden
     from genomeanonymizer_amd.synth.generate import generate, scenario
     import gzip
@@ -67,14 +71,16 @@ def test_two_rank_contig_shards_match_reference(name, index, tmp_path):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, name, workdir, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, name, workdir, q)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
         p.join(300)
     assert all(p.exitcode == 0 for p in procs)
-    results = dict(q.get() for _ in range(2))
-    assert results[0] == results[1]            # totals are all-reduced
+    results = dict(q.get() for _ in range(world))
+    assert all(results[r][0] == results[0][0] for r in range(world))   # totals are all-reduced
+    if name.startswith("fuzz3"):      # a contig planned again (rank 0's coordinator counts them)
+        assert results[0][1] > 0
     from genomeanonymizer_amd.short_read_tumor_normal_anonymizer import name_output
     for tag, pre in (("tumor", name_output(paths["T"])), ("normal", name_output(paths["N"]))):
         for suf in (".1.fastq", ".2.fastq", ".single_end.fastq"):
@@ -106,4 +112,29 @@ def test_a_failing_rank_stops_every_rank(tmp_path, fail_rank, stage):
         if p.is_alive():
             p.kill()
     assert alive == [False, False]
+    assert all(p.exitcode != 0 for p in procs)
+
+
+def test_middle_rank_failure_with_ranks_still_exporting(tmp_path):
+    """3 ranks over 6 contigs; rank 1 fails in its first job while ranks 0 and 2 are still exporting
+    later contigs. The coordinator stops at rank 1's contig, sends the error only to the ranks with
+    jobs left, and receives every export sent before their error answers (ADVICE r3 stream.py): all
+    three processes end with an error, none hangs in a pending send."""
+    from test_stream import _scenario
+    from genomeanonymizer_amd.synth.generate import generate
+    workdir = str(tmp_path / "six")
+    generate(_scenario(23, n_contigs=6, split=False), os.path.join(workdir, "in"))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 3, port, "six", workdir, q, "oracle", 1, "job")) for r in range(3)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(180)
+    alive = [p.is_alive() for p in procs]
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    assert alive == [False, False, False]
     assert all(p.exitcode != 0 for p in procs)

@@ -253,12 +253,16 @@ def test_hip_pipeline_matches_reference(name, whole, tmp_path, hip_built, monkey
     assert bad == {}
 
 
-@pytest.mark.parametrize("name", ["fuzz1001", "fuzz2000", "fuzz2003"])
-def test_hip_pipeline_split_alignments_match_reference(name, tmp_path, hip_built, monkeypatch):
+@pytest.mark.parametrize("whole", [False, True], ids=["streaming", "whole_sample"])
+@pytest.mark.parametrize("name", ["fuzz1001", "fuzz2000", "fuzz2003", "fuzz3000", "fuzz3008"])
+def test_hip_pipeline_split_alignments_match_reference(name, whole, tmp_path, hip_built, monkeypatch):
     """Supplementary (SA) and secondary alignments through the streamed HIP product: one device copy
-    per (alignment, scope), the object log replayed over them (objects.py); the reference's files."""
+    per (alignment, scope), the object log replayed over them (objects.py); the reference's files.
+    fuzz3000 / fuzz3008: secondaries off their mate's contig, second-scope copies of cross names,
+    unmapped supplementary / secondary / SA-tagged mates in the end-of-sample tail. Whole-sample
+    mode hands such samples to the streamed path."""
     from genomeanonymizer_amd.anonymizer_methods import CompleteGermlineAnonymizer
-    monkeypatch.setenv("GANON_WHOLE_SAMPLE", "0")
+    monkeypatch.setenv("GANON_WHOLE_SAMPLE", "1" if whole else "0")
     bad = run_pipeline_vs_golden(name, str(tmp_path / name), CompleteGermlineAnonymizer(device=0))
     assert bad == {}
 

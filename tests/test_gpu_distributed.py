@@ -43,3 +43,30 @@ def test_two_rank_hip_contig_shards_match_reference(name, tmp_path, hip_built):
             if os.path.exists(gp):
                 assert open(pre + suf, "rb").read() == gzip.open(gp).read(), tag + suf
     assert open(paths["N"] + ".statistics.txt").read() == open(os.path.join(GOLDEN, name, "normal.statistics.txt")).read()
+
+
+def test_cli_rccl_process_group_world_one(tmp_path, hip_built):
+    """The CLI as torchrun starts it (RANK / WORLD_SIZE / MASTER_* set) with one rank: the nccl
+    (RCCL) process group is created before any GPU call, the sample goes through the sharded
+    streamed path (coordinator, Link over the gloo side group) and the int64 totals are all-reduced
+    on a CUDA tensor by RCCL (stream._Comm.allreduce_totals). Files equal the reference's."""
+    import gzip
+    import subprocess
+    import sys
+    from helpers import GOLDEN, REPO
+    from genomeanonymizer_amd.synth.generate import generate, scenario
+    d = str(tmp_path / "rccl")
+    paths = generate(scenario("fuzz3000"), d)
+    env = dict(os.environ, PYTHONPATH=REPO, GANON_IO_BLOCK="4096", RANK="0", WORLD_SIZE="1", LOCAL_RANK="0",
+               LOCAL_WORLD_SIZE="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    r = subprocess.run([sys.executable, "-m", "genomeanonymizer_amd.genome_anonymizer", "-d", d, "-s", "samples.tsv",
+                        "-r", paths["ref"], "--record_statistics", "-c", "4", "-v", "2"], env=env,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "process group backend nccl" in r.stderr, r.stderr[-2000:]
+    for tag in ("tumor", "normal"):
+        for suf in (".1.fastq", ".2.fastq", ".single_end.fastq"):
+            gp = os.path.join(GOLDEN, "fuzz3000", f"{tag}{suf}.gz")
+            assert open(os.path.join(d, f"{tag}.anonymized{suf}"), "rb").read() == gzip.open(gp).read(), tag + suf
+    assert open(paths["N"] + ".statistics.txt").read() == \
+        open(os.path.join(GOLDEN, "fuzz3000", "normal.statistics.txt")).read()

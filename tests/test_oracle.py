@@ -34,13 +34,16 @@ def test_pipeline_with_oracle_matches_reference(name, whole, tmp_path, monkeypat
 
 
 @pytest.mark.parametrize("impl", ["native", "python"])
-@pytest.mark.parametrize("name", ["fuzz1001", "fuzz2000", "fuzz2003"])
+@pytest.mark.parametrize("name", ["fuzz1001", "fuzz2000", "fuzz2003", "fuzz3000", "fuzz3008"])
 def test_pipeline_split_alignments_match_reference(name, impl, tmp_path, monkeypatch):
     """Supplementary alignments with SA tags (chimeric reads, the tail on either strand, near the
     primary or on another contig) and secondary alignments: the reference's AnonymizedRead object
     model (creator orientation, primary promotion, supplementary-coordinate masks, left-over
     merges) through the streamed product, against the reference's own files — with the product's
-    object replay (csrc/ganon_objects.cpp) and its Python restatement (objects.Replay)."""
+    object replay (csrc/ganon_objects.cpp) and its Python restatement (objects.Replay). Seeds >= 3000
+    add secondaries off their mate's contig (forced cross names, names marked written), reads of
+    cross names written from a second scope's copy, and placed-unmapped mates flagged secondary /
+    supplementary or SA-tagged among the end-of-sample candidates."""
     from pyoracle import OracleEngine
     from genomeanonymizer_amd.anonymizer_methods import CompleteGermlineAnonymizer
     monkeypatch.setenv("GANON_WHOLE_SAMPLE", "0")
@@ -49,14 +52,15 @@ def test_pipeline_split_alignments_match_reference(name, impl, tmp_path, monkeyp
     assert bad == {}
 
 
-def test_whole_mode_streams_split_alignments(tmp_path, monkeypatch):
+@pytest.mark.parametrize("name", ["fuzz1001", "fuzz3000"])
+def test_whole_mode_streams_split_alignments(name, tmp_path, monkeypatch):
     """The whole-sample planner does not restate the object model: a sample with secondary /
     supplementary alignments or SA tags goes to the streamed path, and the files are the
     reference's (fuzz golden with split alignments)."""
     from pyoracle import OracleEngine
     from genomeanonymizer_amd.anonymizer_methods import CompleteGermlineAnonymizer
     monkeypatch.setenv("GANON_WHOLE_SAMPLE", "1")
-    bad = run_pipeline_vs_golden("fuzz1001", str(tmp_path / "w"), CompleteGermlineAnonymizer(engine=OracleEngine()))
+    bad = run_pipeline_vs_golden(name, str(tmp_path / "w"), CompleteGermlineAnonymizer(engine=OracleEngine()))
     assert bad == {}
 
 

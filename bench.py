@@ -166,16 +166,28 @@ CONFIGS = {
 }
 
 
-def make_batch(args, rank: int):
+def batch_reads(args, k: int) -> int:
+    """Reads of pipeline batch k: the configured count -2 % / +-0 / +2 % in turn (mean = the
+    configured count over every three batches), so consecutive batches differ in reads, scopes and
+    incidences."""
+    if args.batches * args.pipeline <= 1:
+        return args.reads
+    return args.reads + ((k % 3) - 1) * (args.reads // 50)
+
+
+def make_batch(args, rank: int, k: int = 0):
+    """Batch k of this rank: the same sample (genome, germline sites, windows: the config's seed +
+    rank) with its own reads (read seed) and read count (batch_reads); c5: its own long-read batch."""
     from genomeanonymizer_amd.synth.batch import config2_batch, longread_batch
     if args.config == "c5":
-        return longread_batch(seed=7 + rank, n_reads=args.reads, genome=args.genome)
+        return longread_batch(seed=7 + rank + 100 * k, n_reads=args.reads, genome=args.genome)
     seed = CONFIGS[args.config]["seed"] + rank
+    rs = 1000 * seed + k
     if args.config == "c3":
-        return config2_batch(n_reads=args.reads, genome=args.genome, n_contigs=4, n_windows=args.windows,
-                             n_germline=args.germline, seed=seed, window_spacing=10_000)
-    return config2_batch(n_reads=args.reads, genome=args.genome, n_windows=args.windows,
-                         n_germline=args.germline, seed=seed)
+        return config2_batch(n_reads=batch_reads(args, k), genome=args.genome, n_contigs=4, n_windows=args.windows,
+                             n_germline=args.germline, seed=seed, window_spacing=10_000, read_seed=rs)
+    return config2_batch(n_reads=batch_reads(args, k), genome=args.genome, n_windows=args.windows,
+                         n_germline=args.germline, seed=seed, read_seed=rs)
 
 
 def fastq_bench(masker, db, arr, args, torch, rank: int) -> dict:
@@ -418,7 +430,10 @@ def main() -> None:
     ap.add_argument("--indel-sort", type=int, default=0, help="GANON_PARAM_INDEL_SORT: 0 segmented, 1 global")
     ap.add_argument("--fastq-kd", type=int, default=None, help="GANON_PARAM_FASTQ_KD (formatter kernel A/B)")
     ap.add_argument("--pipeline", type=int, default=3,
-                    help="resident batches stepped round-robin, each in its own context and HIP stream")
+                    help="contexts stepped round-robin, each with its own HIP stream")
+    ap.add_argument("--batches", type=int, default=2,
+                    help="resident raw batches per context, stepped in turn: every step plans a batch of other "
+                         "read / scope / incidence counts than the context's previous one (c5: 1)")
     ap.add_argument("--spec-plan", type=int, default=1, help="GANON_PARAM_SPEC_PLAN: 1 speculative replans "
                     "(no host synchronization inside the step), 0 the replan waits for the scan")
     ap.add_argument("--prep-unroll", type=int, default=0, help="GANON_PARAM_PREP_UNROLL: incidences per thread "
@@ -440,6 +455,8 @@ def main() -> None:
     for k, v in CONFIGS[args.config]["defaults"].items():
         if getattr(args, k) is None:
             setattr(args, k, v)
+    if args.config == "c5" or args.resident:
+        args.batches = 1
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
@@ -463,45 +480,53 @@ def main() -> None:
     from genomeanonymizer_amd import native
     from genomeanonymizer_amd.synth.batch import algorithmic_bytes
 
+    # --pipeline S contexts x --batches B resident raw batches: S * B batches of the same sample with
+    # their own reads and read counts (make_batch). Step i runs context i % S on its batch
+    # (i // S) % B: every step plans a batch of other counts than that context's previous plan (a
+    # new batch arriving), and a context's plan (latency-bound scan and emit) runs beside another
+    # context's group kernel (bandwidth-bound)
+    n_b = args.pipeline * args.batches
     t_gen = time.perf_counter()
-    arr, info = make_batch(args, rank)
+    batches = [make_batch(args, rank, k) for k in range(n_b)]
     t_gen = time.perf_counter() - t_gen
-    masker = native.HipMasker(dev)
-    masker.set_param(native.PARAM_GROUP_UNROLL, args.unroll)
-    if args.target:
-        masker.set_param(native.PARAM_GROUP_TARGET, args.target)
-    masker.set_param(native.PARAM_INDEL_SORT, args.indel_sort)
-    masker.set_param(native.PARAM_PREP_UNROLL, args.prep_unroll)
-    masker.set_param(native.PARAM_SPEC_PLAN, args.spec_plan)
-    if args.fastq_kd is not None:
-        masker.set_param(native.PARAM_FASTQ_KD, args.fastq_kd)
-    stream = torch.cuda.current_stream()
-    masker.set_stream(stream.cuda_stream)
+    arr, info = batches[0]
     t_up = time.perf_counter()
-    ref = masker.upload_reference(arr["ref_nt16"])      # the genome stays resident (ganon_ref_upload)
-    db = masker.upload({k: v for k, v in arr.items() if k != "ref_nt16"}, ref=ref)
-    shape = db.shape()
-    # germline indel tally: part of every step when the device scan found I/D ops
-    ind = db.indel_tally(arr) if shape["id_ops"] else None
-    # --pipeline S: S resident batches, each in its own context on its own HIP stream, stepped
-    # round-robin: a batch's plan (latency-bound scan and emit) runs beside another's group kernel
-    # (bandwidth-bound). Every batch still gets its full fresh step; the timed region holds the
-    # same number of steps.
-    slots = [(masker, stream, db, ind)]
-    for _ in range(1, args.pipeline):
-        m2 = native.HipMasker(dev)
+    slots = []
+    shape = None
+    for si in range(args.pipeline):
+        m = native.HipMasker(dev)
         for prm, val in ((native.PARAM_GROUP_UNROLL, args.unroll), (native.PARAM_INDEL_SORT, args.indel_sort),
                          (native.PARAM_PREP_UNROLL, args.prep_unroll), (native.PARAM_SPEC_PLAN, args.spec_plan)):
-            m2.set_param(prm, val)
+            m.set_param(prm, val)
         if args.target:
-            m2.set_param(native.PARAM_GROUP_TARGET, args.target)
-        st2 = torch.cuda.Stream()
-        m2.set_stream(st2.cuda_stream)
-        r2 = m2.upload_reference(arr["ref_nt16"])
-        d2 = m2.upload({k: v for k, v in arr.items() if k != "ref_nt16"}, ref=r2)
-        slots.append((m2, st2, d2, d2.indel_tally(arr) if shape["id_ops"] else None))
-        slots[-1] = slots[-1] + (r2,)
+            m.set_param(native.PARAM_GROUP_TARGET, args.target)
+        if args.fastq_kd is not None:
+            m.set_param(native.PARAM_FASTQ_KD, args.fastq_kd)
+        st = torch.cuda.current_stream() if si == 0 else torch.cuda.Stream()
+        m.set_stream(st.cuda_stream)
+        mine = [batches[si + args.pipeline * b] for b in range(args.batches)]
+        # the genome stays resident (ganon_ref_upload), shared by the context's batches of one sample
+        r = m.upload_reference(mine[0][0]["ref_nt16"]) if args.config != "c5" or args.batches == 1 else None
+        dbs, inds = [], []
+        for a, _ in mine:
+            if r is None:
+                r = m.upload_reference(a["ref_nt16"])
+            d = m.upload({k: v for k, v in a.items() if k != "ref_nt16"}, ref=r)
+            sh = d.shape()
+            shape = shape or sh
+            dbs.append(d)
+            # germline indel tally: part of every step when the device scan found I/D ops
+            inds.append(d.indel_tally(a) if sh["id_ops"] else None)
+        slots.append({"m": m, "st": st, "ref": r, "dbs": dbs, "inds": inds, "arrs": [a for a, _ in mine],
+                      "reads": [i["reads"] for _, i in mine]})
+    masker, stream, db, ind = slots[0]["m"], slots[0]["st"], slots[0]["dbs"][0], slots[0]["inds"][0]
+    ref = slots[0]["ref"]
     t_up = time.perf_counter() - t_up
+
+    def pick(i: int):
+        sl = slots[i % len(slots)]
+        b = (i // len(slots)) % args.batches
+        return sl, b
     # totals all-reduce (RCCL) of every step, double-buffered: the reduction of step i runs beside
     # step i + 1's kernels; a buffer is reused only after its previous reduction completed
     tots = [torch.zeros(8, dtype=torch.int64, device="cuda") for _ in range(2)]
@@ -509,7 +534,8 @@ def main() -> None:
     host_reduce = dist is not None and dist.get_backend() != "nccl"
 
     def step(i: int):
-        _, st_i, db_i, ind_i = slots[i % len(slots)][:4]
+        sl, b = pick(i)
+        st_i, db_i, ind_i = sl["st"], sl["dbs"][b], sl["inds"][b]
         if not args.resident:
             db_i.replan()     # a fresh batch: the plan from the raw arrays, every step
         db_i.run()
@@ -538,6 +564,7 @@ def main() -> None:
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
+    gated0 = sum(d.gated_runs() for sl in slots for d in sl["dbs"])
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -547,12 +574,18 @@ def main() -> None:
     if dist is not None:
         dist.barrier()
     dt = time.perf_counter() - t0
+    # every timed step really ran: a speculative plan a batch did not fit runs nothing (its download
+    # would plan it again), so such a step must not count
+    gated = sum(d.gated_runs() for sl in slots for d in sl["dbs"]) - gated0
+    if gated:
+        raise RuntimeError(f"{gated} timed steps ran nothing (speculative plans their batches did not fit)")
+    reads_timed = sum(pick(i)[0]["reads"][pick(i)[1]] for i in range(args.steps))
     dt_t = torch.tensor([dt], dtype=torch.float64, device="cpu" if host_reduce else "cuda")
     if dist is not None:
         dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
     dt = float(dt_t.item())
 
-    # the same steps on one batch and one stream (no overlap between batches), for comparison
+    # the same steps on one context and one stream (its batches in turn, no overlap), for comparison
     one_stream_ms = None
     if len(slots) > 1:
         torch.cuda.synchronize()
@@ -562,18 +595,36 @@ def main() -> None:
         drain()
         torch.cuda.synchronize()
         one_stream_ms = (time.perf_counter() - t) / args.steps * 1e3
+    # the same pipelined steps with every plan synchronous (GANON_PARAM_SPEC_PLAN 0: the host waits
+    # for each scan before it launches the run), for comparison
+    sync_ms = None
+    if not args.resident and args.spec_plan:
+        for sl in slots:
+            sl["m"].set_param(native.PARAM_SPEC_PLAN, 0)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for i in range(args.steps):
+            step(i)
+        drain()
+        torch.cuda.synchronize()
+        sync_ms = (time.perf_counter() - t) / args.steps * 1e3
+        for sl in slots:
+            sl["m"].set_param(native.PARAM_SPEC_PLAN, args.spec_plan)
 
-    # per-kernel durations: the same steps again with a HIP event pair around each launch
+    # per-kernel durations: context 0's steps again (its batches in turn) with a HIP event pair
+    # around each launch
     masker.set_profiling(True)
     ktimes: dict = {}
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        b = i % args.batches
+        db_i, ind_i = slots[0]["dbs"][b], slots[0]["inds"][b]
         if not args.resident:
-            db.replan()
-        db.run()
-        if ind is not None:
-            ind.run()
-        db.sync()
-        for name, launches, ms in db.kernel_times():
+            db_i.replan()
+        db_i.run()
+        if ind_i is not None:
+            ind_i.run()
+        db_i.sync()
+        for name, launches, ms in db_i.kernel_times():
             k = ktimes.setdefault(name, [0, 0.0])
             k[0] += launches
             k[1] += ms
@@ -610,18 +661,42 @@ def main() -> None:
         job_totals = tots[0].cpu().numpy()
     else:
         job_totals = totals
-    for sl in slots[1:]:
-        if not (sl[2].totals() == totals).all():
-            raise RuntimeError("pipelined batches disagree")
-        if sl[3] is not None:
-            sl[3].free()
-        sl[2].free()
-        sl[4].free()
-        sl[0].close()
+    # every batch's last (speculative) result equals a full synchronous plan + run of it
+    per_batch = []
+    for sl in slots:
+        spec_tots = []
+        for rnd in range(2):    # (round 0 leaves every batch planned after another: round 1 is a new-batch plan)
+            spec_tots = []
+            for d in sl["dbs"]:
+                d.replan()
+                d.run()
+                g0 = d.gated_runs()
+                spec_tots.append((d.totals(), g0))
+        sl["m"].set_param(native.PARAM_SPEC_PLAN, 0)
+        for d, (spec_tot, g0) in zip(sl["dbs"], spec_tots):
+            d.replan()
+            d.run()
+            if not (d.totals() == spec_tot).all():
+                raise RuntimeError("a speculative step's totals differ from its batch's full plan")
+            per_batch.append({"reads": int(spec_tot[2]), "written": int(spec_tot[3]), "scopes": int(spec_tot[4]),
+                              "masked_snv_calls": int(spec_tot[0]), "gated_runs_since_upload": g0})
+    for sl in slots:
+        for x in sl["inds"]:
+            if x is not None and x is not ind:
+                x.free()
+        for d in sl["dbs"]:
+            if d is not db:
+                d.free()
+        if sl is not slots[0]:
+            sl["ref"].free()
+            sl["m"].close()
     db.free()
     ref.free()
 
-    kb = kernel_bytes(arr)
+    # algorithmic bytes of the profiled steps: context 0's batches, one step each in turn
+    prof_arrs = slots[0]["arrs"]
+    kbs = [kernel_bytes(a) for a in prof_arrs]
+    kb = {k: sum(x[k] for x in kbs) // len(kbs) for k in kbs[0]}
     kb.update(indel_bytes(arr, indel_info["observations"], indel_info["emitted"]))
     per_kernel = {n: {"launches": c, "avg_ms": ms / c} for n, (c, ms) in ktimes.items()}
     # the dominant kernel: the longest one the algorithmic bytes are counted for (the group kernel;
@@ -632,7 +707,7 @@ def main() -> None:
     dom_bytes = kb.get(kernel_class(dom), 0)
     dom_ms = per_kernel[dom]["avg_ms"]
     pass_ms = sum(v["avg_ms"] * v["launches"] for v in per_kernel.values()) / args.steps
-    alg_total = algorithmic_bytes(arr)
+    alg_total = sum(algorithmic_bytes(a) for a in prof_arrs) // len(prof_arrs)
     achieved = alg_total / (pass_ms * 1e-3) / 1e9
     traffic = dom_traffic = None
     pmc_path = args.pmc or os.path.join(REPO, "profiles", "r03", f"pmc_step_{args.config}.json")
@@ -645,8 +720,8 @@ def main() -> None:
         except Exception:
             traffic = None
 
-    reads_total = info["reads"] * world
-    value = reads_total * args.steps / dt
+    reads_total = reads_timed * world
+    value = reads_total / dt
     mean_len = float(arr["read_len"].astype(np.int64).mean()) if len(arr["read_len"]) else 0.0
     cfg = CONFIGS[args.config]
     result = {
@@ -680,11 +755,16 @@ def main() -> None:
                                   "traffic": dom_traffic if "k_group" in dom else None,
                                   "frac": round(dom_bytes / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}},
         "step_kind": "resident batch, plan kept (run only)" if args.resident else
-                     ("fresh batch: device plan (replan: validation scan, group table, shape checks) + run every "
-                      "step; " + ("speculative replan (the run is enqueued behind the scan, which gates it)"
-                                  if args.spec_plan else "the replan waits for the scan")
-                      + (f"; {args.pipeline} resident batches stepped round-robin, each on its own HIP stream"
-                         if args.pipeline > 1 else "")),
+                     (f"fresh batch: device plan (replan: validation scan, group table, shape checks) + run every "
+                      f"step, over {n_b} resident raw batches of the sample with their own reads ({args.pipeline} "
+                      f"contexts on their own HIP streams x {args.batches} batches each, stepped in turn; read counts "
+                      f"{sorted(set(batch_reads(args, k) for k in range(n_b)))}): every plan is of other read / scope / "
+                      f"incidence counts than its context's previous one; "
+                      + ("speculative plan (the run is enqueued behind the scan, buffers sized on the host from the "
+                         "batch's counts for the context's last shape; the scan gates the run; gated timed steps: 0)"
+                         if args.spec_plan else "the plan waits for the scan")),
+        "batches": per_batch,
+        "sync_plan_ms_per_step": round(sync_ms, 4) if sync_ms else None,
         "run_only_ms_per_step": round(run_only_ms, 4) if run_only_ms else None,
         "one_stream_ms_per_step": round(one_stream_ms, 4) if one_stream_ms else None,
         "batch_shape": shape,

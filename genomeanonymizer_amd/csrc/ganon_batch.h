@@ -203,6 +203,7 @@ struct ganon_dbatch {
                                              // [4] most segments of one read, [5] short-read groups,
                                              // [6] write-scope hash sum (k_finish compares)
   unsigned long long *paths = nullptr;       // GrpAux::paths (since upload)
+  unsigned long long *gated = nullptr;       // runs stopped by a speculative plan's gate (since upload)
   unsigned long long *cursor = nullptr;      // k_prep_emit allocation counters and their bases (b_cursor)
   ganon_dev::GrpAux *aux = nullptr;
   // plan of the current contents (device prep, sized at upload)
@@ -212,6 +213,7 @@ struct ganon_dbatch {
   // scan; the device checks the assumption (plan_info[7]) and ganon_batch_download plans and runs
   // again when it failed
   bool spec = false, spec_ready = false;
+  bool spec_sized = false;   // the speculation sized this plan's buffers for new counts (ctx->spec_*)
   int64_t spec_sizes[4] = {-1, -1, -1, -1};   // reads, scopes, incidences, group target of that plan
   // long-read mode (a read with more than one aligned segment): groups cut on the prefix of segments
   // per scope (scost, upload) instead of the CSR offsets, and emitted one wave per incidence

@@ -35,6 +35,12 @@ struct ganon_ctx {
   int indel_sort = 0;          // GANON_PARAM_INDEL_SORT
   int group_obs = 0;           // GANON_PARAM_GROUP_OBS (0 auto, 512, 1024)
   int spec_plan = 1;           // GANON_PARAM_SPEC_PLAN (1: speculative replans, 0: every plan synchronizes)
+  // the shape of this context's last full plan when a replan of a batch of other sizes may assume it
+  // (one-segment mode, no huge scope): its overflow-region entries per incidence and group target
+  bool spec_shape_ok = false;
+  const void *last_plan = nullptr;   // the batch this context planned last
+  int64_t spec_rpi = 0;
+  int spec_tgt = 0;
   int prep_unroll = 0;         // GANON_PARAM_PREP_UNROLL (0 auto = 2, 1, 2, 4)
   int far_init = 0;            // GANON_PARAM_FAR_INIT (0 auto)
   bool step_open = false;      // ganon_batch_replan started a profiled step the next run continues

@@ -1115,7 +1115,8 @@ __global__ void __launch_bounds__(kBlock) k_finish(const unsigned long long *__r
                                                    unsigned long long *far_need,
                                                    unsigned long long *totals,
                                                    const unsigned long long *__restrict__ ws_part,
-                                                   const unsigned long long *__restrict__ plan_info) {
+                                                   const unsigned long long *__restrict__ plan_info,
+                                                   unsigned long long *gated) {
   const int64_t gtid = blockIdx.x * (int64_t)kBlock + threadIdx.x, gstride = (int64_t)gridDim.x * kBlock;
   const unsigned long long far_n = *far_count;
   const int64_t n_far = far_n < (unsigned long long)far_cap ? (int64_t)far_n : far_cap;
@@ -1173,8 +1174,12 @@ __global__ void __launch_bounds__(kBlock) k_finish(const unsigned long long *__r
   // run (plan_info[7]: a speculative plan the batch did not fit, or an invalid batch) ran no
   // one-segment kernel: ganon_batch_download plans and runs it again (or reports the error)
   const unsigned long long hs = atomicExch(&acc[4], 0ull);
-  if (plan_info[7]) atomicOr(status, 4);
-  else if (hs != plan_info[6]) atomicOr(status, 2);
+  if (plan_info[7]) {
+    atomicOr(status, 4);
+    atomicAdd(gated, 1ull);   // (cumulative since upload: ganon_batch_gated_runs)
+  } else if (hs != plan_info[6]) {
+    atomicOr(status, 2);
+  }
   for (int k = 0; k < GANON_N_TOTALS; ++k) totals[k] = static_totals[k];
   totals[GANON_T_READS_WRITTEN] = plan_info[2];
   totals[GANON_T_MASKED_SNV_CALLS] += sc;
@@ -1526,7 +1531,7 @@ int host_copy(ganon_ctx *ctx, const ganon_dbatch *db, HostCopy &h) {
 int prepare(ganon_ctx *ctx, ganon_dbatch *db, const ganon_batch *host, bool allow_spec = false) {
   int rc;
   if ((rc = ganon_prep::plan(ctx, db, allow_spec))) return rc;   // (it clears the step's flags first)
-  if (db->spec) {
+  if (db->spec && !db->spec_sized) {
     // the previous plan's tiles (none), aux pointers and static totals, unchanged on the host; copied
     // again (a reload clears the device's small state)
     HIP_OR_FAIL(hipMemcpyAsync(db->aux, &db->aux_h, sizeof db->aux_h, hipMemcpyHostToDevice, ctx->stream));
@@ -1627,7 +1632,7 @@ int load_batch(ganon_ctx *ctx, ganon_dbatch *db, const ganon_batch *b, const gan
   D.ref2 = db->ref->ref2;
   // small device state: totals, static totals, acc, far count, plan info (u64); counters, status;
   // the first validation error; the group kernels' aux pointers
-  constexpr size_t kU64 = 8 + 8 + 5 + 1 + 8 + 4;
+  constexpr size_t kU64 = 8 + 8 + 5 + 1 + 8 + 4 + 1;
   // the per-plan flags (first error, status bits, long-read count, far masks needed) are adjacent:
   // one memset clears them at the start of every plan
   constexpr size_t kFlags = sizeof(PrepErr) + 16;
@@ -1641,6 +1646,7 @@ int load_batch(ganon_ctx *ctx, ganon_dbatch *db, const ganon_batch *b, const gan
   db->far_count = u + 21;
   db->plan_info = u + 22;
   db->paths = u + 30;
+  db->gated = u + 34;      // runs a speculative plan's gate stopped (cumulative)
   db->counters = reinterpret_cast<int32_t *>(u + kU64);
   db->err = reinterpret_cast<PrepErr *>(sm + kU64 * 8 + 8 * 4);
   db->status = reinterpret_cast<int32_t *>(db->err + 1);
@@ -1954,7 +1960,7 @@ GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
                                     db->large_ids, db->n_huge_scopes, db->scope_calls, db->scope_bases,
                                     db->static_totals, db->counters, db->far_count, db->status, db->acc, db->far_need,
                                     db->totals,
-                                    static_cast<const unsigned long long *>(db->b_wspart.p), db->plan_info);
+                                    static_cast<const unsigned long long *>(db->b_wspart.p), db->plan_info, db->gated);
     if ((rc = check_launch(ctx, "k_finish"))) return rc;
   }
   db->ran = true;
@@ -2085,6 +2091,17 @@ GANON_API int ganon_batch_copy_totals(ganon_ctx *ctx, ganon_dbatch *db, void *de
   HIP_OR_FAIL(hipSetDevice(ctx->device));
   HIP_OR_FAIL(hipMemcpyAsync(dev_dst, db->totals, GANON_N_TOTALS * sizeof(int64_t), hipMemcpyDeviceToDevice,
                              ctx->stream));
+  return GANON_OK;
+}
+
+GANON_API int ganon_batch_gated_runs(ganon_ctx *ctx, ganon_dbatch *db, int64_t *out) {
+  if (!ctx || !db || !out) return fail(ctx, GANON_E_ARG, "null argument");
+  if (!db->gated) return fail(ctx, GANON_E_STATE, "batch never loaded");
+  HIP_OR_FAIL(hipSetDevice(ctx->device));
+  unsigned long long g = 0;
+  HIP_OR_FAIL(hipMemcpyAsync(&g, db->gated, sizeof g, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_OR_FAIL(hipStreamSynchronize(ctx->stream));
+  *out = (int64_t)g;
   return GANON_OK;
 }
 

@@ -493,6 +493,7 @@ struct ganon_bam_reader {
   bool has_index = false;
   std::vector<int64_t> index_beg;    // per tid: virtual offset of its first record, -1 = no records
   std::vector<int64_t> index_end;    // per tid: virtual offset past its last record (-1 unknown)
+  std::vector<std::vector<int64_t>> linear;   // per tid: the linear index (first record of each 16 kb window)
   int64_t cur_voff = -1;             // forward cursor: the first record not yet consumed
   int32_t cur_tid = 0;
   ganon_inflate_fn inflater = nullptr;   // ganon_bam_reader_set_inflater: block windows inflated by it
@@ -656,6 +657,88 @@ int scan_tid(ganon_bam_reader *R, int64_t voff, int32_t tid, int64_t hint, RawVe
   }
 }
 
+// Record end (bam_endpos: pos + reference length, pos + 1 without one or when unmapped) of the
+// record at d (block_size first).
+int64_t record_end(const uint8_t *d) {
+  int32_t pos, l_rn_mq_bin, flag_nc;
+  std::memcpy(&pos, d + 8, 4);
+  std::memcpy(&l_rn_mq_bin, d + 12, 4);
+  std::memcpy(&flag_nc, d + 16, 4);
+  const int l_rn = l_rn_mq_bin & 0xFF, nc = flag_nc & 0xFFFF, flag = (int)((uint32_t)flag_nc >> 16);
+  int64_t rl = 0;
+  if (!(flag & 4)) {
+    const uint8_t *cg = d + 36 + l_rn;
+    for (int k = 0; k < nc; ++k) {
+      uint32_t w;
+      std::memcpy(&w, cg + 4 * k, 4);
+      const int op = w & 0xF;
+      if (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) rl += w >> 4;
+    }
+  }
+  return (int64_t)pos + (rl > 0 ? rl : 1);
+}
+
+// Streams from virtual offset voff: keeps the records of `tid` overlapping [beg, end) (htslib's
+// region semantics: pos < end and bam_endpos > beg), in file order; stops at the first record of
+// another sequence or at pos >= end. Runs of kept records are copied to kept at once.
+int scan_region(ganon_bam_reader *R, int64_t voff, int32_t tid, int64_t beg, int64_t end, int64_t hint,
+                RawVec<uint8_t> &kept) {
+  int64_t step = std::min<int64_t>(hint > 0 ? hint + (1 << 16) : (1 << 20), R->chunk);
+  int64_t coff = voff >> 16;
+  RawVec<uint8_t> data;
+  std::vector<std::pair<int64_t, int64_t>> bmap;
+  int64_t dpos = (int64_t)(voff & 0xFFFF);
+  for (;;) {
+    if (coff >= R->fsize) {
+      if (dpos < (int64_t)data.size()) return set_err("truncated BAM record");
+      return 0;
+    }
+    if (dpos > 0 && !data.empty()) {
+      const int64_t cut = std::min<int64_t>(dpos, (int64_t)data.size());
+      data.erase(data.begin(), data.begin() + cut);
+      dpos -= cut;
+      for (auto &e : bmap) e.first -= cut;
+      size_t k = 0;
+      while (k + 1 < bmap.size() && bmap[k + 1].first <= 0) ++k;
+      bmap.erase(bmap.begin(), bmap.begin() + (long)k);
+    }
+    coff = read_blocks(R, coff, step, data, bmap);
+    if (coff < 0) return -1;
+    step = std::min<int64_t>(2 * step, R->chunk);
+    int64_t run0 = -1;
+    auto flush = [&]() {
+      if (run0 >= 0) {
+        const size_t n = (size_t)(dpos - run0), at = kept.size();
+        if (at + n > kept.capacity()) huge_reserve(kept, std::max(2 * kept.capacity(), at + n));
+        kept.resize(at + n);
+        parallel_copy(kept.data() + at, data.data() + run0, n, R->threads);
+      }
+      run0 = -1;
+    };
+    for (;;) {
+      if (dpos + 4 > (int64_t)data.size()) break;
+      int32_t bs, rtid, rpos;
+      std::memcpy(&bs, &data[(size_t)dpos], 4);
+      if (bs < 32) return set_err("bad record size");
+      if (dpos + 4 + bs > (int64_t)data.size()) break;
+      std::memcpy(&rtid, &data[(size_t)dpos + 4], 4);
+      std::memcpy(&rpos, &data[(size_t)dpos + 8], 4);
+      if (rtid != tid || rpos >= end) {
+        if (tid_order(rtid) < tid_order(tid)) return set_err("BAM index points before its sequence");
+        flush();
+        return 0;
+      }
+      if (record_end(&data[(size_t)dpos]) > beg) {
+        if (run0 < 0) run0 = dpos;
+      } else {
+        flush();
+      }
+      dpos += 4 + bs;
+    }
+    flush();
+  }
+}
+
 void load_index(ganon_bam_reader *R, const std::string &bam_path) {
   std::vector<std::string> cands{bam_path + ".bai"};
   if (bam_path.size() > 4 && bam_path.compare(bam_path.size() - 4, 4, ".bam") == 0)
@@ -681,6 +764,7 @@ void load_index(ganon_bam_reader *R, const std::string &bam_path) {
         n_ref != (int32_t)R->header.ref_len.size())
       continue;
     std::vector<int64_t> beg((size_t)n_ref, -1), end((size_t)n_ref, -1);
+    std::vector<std::vector<int64_t>> lin((size_t)n_ref);
     bool ok = true;
     for (int32_t r = 0; r < n_ref && ok; ++r) {
       int32_t n_bin;
@@ -706,6 +790,8 @@ void load_index(ganon_bam_reader *R, const std::string &bam_path) {
       }
       int32_t n_intv;
       if (!ok || !rd(&n_intv, 4) || n_intv < 0 || p + 8ull * (size_t)n_intv > b.size()) { ok = false; break; }
+      lin[(size_t)r].resize((size_t)n_intv);
+      if (n_intv) std::memcpy(lin[(size_t)r].data(), &b[p], 8ull * (size_t)n_intv);
       p += 8ull * (size_t)n_intv;
       beg[(size_t)r] = pseudo >= 0 ? pseudo : lo;
       end[(size_t)r] = pseudo >= 0 ? pseudo_end : hi;
@@ -713,6 +799,7 @@ void load_index(ganon_bam_reader *R, const std::string &bam_path) {
     if (!ok) continue;
     R->index_beg = std::move(beg);
     R->index_end = std::move(end);
+    R->linear = std::move(lin);
     R->has_index = true;
     return;
   }
@@ -838,6 +925,48 @@ GANON_HOST_API int ganon_bam_reader_contig(ganon_bam_reader *R, int32_t tid, gan
     return 0;
   } catch (const std::bad_alloc &) {
     return set_err("out of memory decoding a BAM sequence");
+  }
+}
+
+GANON_HOST_API int ganon_bam_reader_region(ganon_bam_reader *R, int32_t tid, int64_t beg, int64_t end,
+                                           ganon_bam **out) {
+  if (!R || !out) return set_err("null argument");
+  *out = nullptr;
+  if (tid < 0 || tid >= (int32_t)R->header.ref_len.size()) return set_err("tid out of range");
+  if (!R->has_index) return set_err("region reads need the BAM index");
+  if (beg < 0 || end < beg) return set_err("bad region");
+  try {
+    RawVec<uint8_t> kept;
+    const int64_t first = R->index_beg[(size_t)tid];
+    if (first >= 0 && end > beg) {
+      // the first record that can overlap beg: the linear index entry of its 16 kb window (the
+      // nearest filled one before it), never before the sequence's first record
+      int64_t voff = first;
+      const std::vector<int64_t> &lin = R->linear[(size_t)tid];
+      for (int64_t w = std::min<int64_t>(beg >> 14, (int64_t)lin.size() - 1); w >= 0; --w)
+        if (lin[(size_t)w] > 0) {
+          voff = std::max(voff, lin[(size_t)w]);
+          break;
+        }
+      const int64_t e = R->index_end[(size_t)tid];
+      const int64_t span = e > voff ? (e >> 16) - (voff >> 16) : 0;
+      const int64_t len = R->header.ref_len[(size_t)tid];
+      const int64_t hint = len > 0 ? std::min<int64_t>(span, span * (end - beg) / len + (1 << 20)) : 0;
+      huge_reserve(kept, (size_t)hint * 7 / 2 + (1 << 20));
+      if (scan_region(R, voff, tid, beg, end, hint, kept) != 0) return -1;
+    }
+    auto *bam = new ganon_bam();
+    bam->ref_names = R->header.ref_names;
+    bam->ref_name_off = R->header.ref_name_off;
+    bam->ref_len = R->header.ref_len;
+    if (records_to_columns(kept.data(), 0, (int64_t)kept.size(), bam, R->threads) != 0) {
+      delete bam;
+      return -1;
+    }
+    *out = bam;
+    return 0;
+  } catch (const std::bad_alloc &) {
+    return set_err("out of memory decoding a BAM region");
   }
 }
 

@@ -96,6 +96,7 @@ class Planner {
 
   void run() {
     cmode_ = in_->contig_mode != 0;
+    jmode_ = cmode_ && in_->sec_hi >= 0;
     name_ids();
     const std::vector<Section> secs = sections();
     for (const Section &w : secs) {
@@ -156,6 +157,9 @@ class Planner {
   std::unordered_map<int64_t, PairSlot> to_pair_;
   uint64_t pair_seq_ = 0;             // clock: to_pair insertions and placeholder events
   bool cmode_ = false;
+  bool jmode_ = false;                // job mode: sections [sec_lo, sec_hi) of the contig
+  int64_t xlo_ = 0, xhi_ = 0;         // job mode: records outside [xlo_, xhi_) other jobs may meet
+  std::vector<uint8_t> job_win_;      // per window: one of the job's sections (job mode)
   std::vector<uint8_t> cross_;        // per name id (contig mode)
   std::vector<uint8_t> cx_;           // per name id: complex (SA tag / secondary / supplementary record)
   std::vector<uint8_t> slot_seen_;    // per name id: mate slots of its plain records (contig mode)
@@ -168,6 +172,21 @@ class Planner {
 
   // names -> ids; the same name in both samples is the reference's silent mix-up (Q10)
   void name_ids() {
+    if (jmode_) {
+      // the reach of the neighbouring jobs into this one: a gap section's scopes pile up the union of
+      // its read clusters (pileup_io.pyx:124-298), up to the furthest end of a record starting before
+      // this job (previous job) or from the first start of a record ending after it (next job); a
+      // record there may be met by both jobs
+      xlo_ = in_->reg_lo;
+      xhi_ = in_->reg_hi;
+      for (int d = 0; d < 2; ++d) {
+        const ganon_plan_table &t = in_->tables[d];
+        for (int64_t r = 0; r < t.n; ++r) {
+          if (t.pos[r] < in_->reg_lo) xlo_ = std::max<int64_t>(xlo_, t.end[r]);
+          if (t.end[r] > in_->reg_hi) xhi_ = std::min<int64_t>(xhi_, t.pos[r]);
+        }
+      }
+    }
     std::unordered_map<std::string_view, int64_t> ids;
     ids.reserve((size_t)(in_->tables[0].n + in_->tables[1].n));
     int64_t tumor_ids = 0;
@@ -194,6 +213,10 @@ class Planner {
         for (int64_t r = 0; r < t.n; ++r) {
           const size_t nm = (size_t)nid_[d][r];
           if (t.tid[r] < 0 || t.mate_tid[r] != t.tid[r]) cross_[nm] = 1;
+          // job mode: a record another job's pileups may reach, or a mate another job reads
+          if (jmode_ && (t.pos[r] < xlo_ || t.end[r] > xhi_ || t.mate_pos[r] < in_->reg_lo ||
+                         t.mate_pos[r] >= in_->reg_hi))
+            cross_[nm] = 1;
           // two plain records of one mate (a duplicated record): the reference keeps one object per
           // mate and scope, which the object model of complex names restates (AM:320-348)
           const int ms = complex_rec(d, r) ? -1 : tab_[d].mate_idx(r);
@@ -237,7 +260,7 @@ class Planner {
   }
 
   // ---- sections (SR:245-276) ----
-  std::vector<Section> sections() const {
+  std::vector<Section> sections() {
     std::vector<std::vector<int32_t>> by_seq((size_t)in_->n_contigs);
     for (int32_t w = 0; w < in_->n_windows; ++w) by_seq[(size_t)in_->win_contig[w]].push_back(w);
     std::vector<Section> out;
@@ -261,6 +284,14 @@ class Planner {
       if (a.first != b.first) return a.first < b.first;
       return a.last < b.last;
     });
+    if (jmode_) {   // (contig mode: out holds the one contig's sections, in order)
+      if (in_->sec_lo < 0 || in_->sec_hi > (int32_t)out.size() || in_->sec_lo > in_->sec_hi)
+        raise(GANON_PLAN_E_VALUE, "job sections out of range");
+      out = std::vector<Section>(out.begin() + in_->sec_lo, out.begin() + in_->sec_hi);
+      job_win_.assign((size_t)in_->n_windows, 0);
+      for (const Section &w : out)
+        if (w.window >= 0) job_win_[(size_t)w.window] = 1;
+    }
     return out;
   }
 
@@ -859,6 +890,7 @@ class Planner {
     std::vector<int64_t> rows;
     for (int32_t w = 0; w < in_->n_windows; ++w) {
       if (in_->win_contig[w] != in_->only_contig) continue;
+      if (jmode_ && !job_win_[(size_t)w]) continue;
       for (int ds = 0; ds < 2; ++ds) {
         try {
           fetch(ds, in_->win_contig[w], true, in_->win_first[w] - 1, true, in_->win_last[w], rows);
@@ -928,7 +960,9 @@ GANON_HOST_API int ganon_plan_run(const ganon_plan_input *in, ganon_plan **out) 
   }
   if (in->contig_mode && (in->only_contig < 0 || in->only_contig >= in->n_contigs ||
                           (in->tables[0].n > 0 && !in->tables[0].mate_tid) ||
-                          (in->tables[1].n > 0 && !in->tables[1].mate_tid))) {
+                          (in->tables[1].n > 0 && !in->tables[1].mate_tid) ||
+                          (in->sec_hi >= 0 && ((in->tables[0].n > 0 && !in->tables[0].mate_pos) ||
+                                               (in->tables[1].n > 0 && !in->tables[1].mate_pos))))) {
     g_err = "contig mode: bad contig or missing mate_tid";
     return GANON_PLAN_E_ARG;
   }
@@ -1032,6 +1066,7 @@ namespace {
 
 struct RInst {
   int64_t job, ds, scope, row;
+  int64_t rid = -1;   // the record's identity for the supplementary hashes (-1: (job, ds, row))
 };
 
 // One AnonymizedRead of the sample-wide state: a plain instance (its masked copy in one scope and
@@ -1069,6 +1104,10 @@ struct RSlot {
 };
 
 int64_t record_id(int64_t job, int64_t ds, int64_t row) { return (job << 40) | (ds << 39) | row; }
+// A record's identity for get_supplementary_hash_from_aln (AM:61-62, the set of supplementary records
+// an object recorded): the caller's content id when given (a record two jobs' tables both hold is
+// one record), else its row in its job.
+int64_t record_id(const RInst &i) { return i.rid >= 0 ? i.rid : record_id(i.job, i.ds, i.row); }
 
 }  // namespace
 
@@ -1174,7 +1213,7 @@ struct ganon_resolver {
         emit(4, o.id, rec.job, rec.ds, rec.row);
         o.supp = false;
       }
-      if (rec_supp) o.add_hash(record_id(rec.job, rec.ds, rec.row));
+      if (rec_supp) o.add_hash(record_id(rec));
     }
     if (p.has[0] && p.has[1] && p.o[0].complete() && p.o[1].complete()) {
       apply(p.o[0]);
@@ -1202,7 +1241,8 @@ GANON_HOST_API int ganon_resolver_contig(ganon_resolver *r, int32_t job, int64_t
                                          const int32_t *op_name_len, int64_t n_left, const int64_t *left,
                                          const char *left_names, const int64_t *left_name_off,
                                          const int32_t *left_name_len, int64_t n_objs, const int64_t *objs,
-                                         const int64_t *obj_rows, int32_t *out_n, int64_t *out_w) {
+                                         const int64_t *obj_rows, const int64_t *obj_ids, int32_t *out_n,
+                                         int64_t *out_w) {
   if (!r || n_ops < 0 || n_left < 0 || n_objs < 0 ||
       (n_ops > 0 && (!ops || !op_rows || !op_names || !op_name_off || !op_name_len || !out_n || !out_w)) ||
       (n_left > 0 && (!left || !left_names || !left_name_off || !left_name_len)) || (n_objs > 0 && (!objs || !obj_rows))) {
@@ -1220,7 +1260,8 @@ GANON_HOST_API int ganon_resolver_contig(ganon_resolver *r, int32_t job, int64_t
       x.supp = o[4] < 0;
       x.has_sa = (o[9] & 2) != 0;
       x.n_sa = (int32_t)(o[9] >> 8);
-      for (int64_t h = 0; h < o[8]; ++h) x.add_hash(record_id(job, o[1], obj_rows[o[7] + h]));
+      for (int64_t h = 0; h < o[8]; ++h)
+        x.add_hash(obj_ids && obj_ids[o[7] + h] >= 0 ? obj_ids[o[7] + h] : record_id(job, o[1], obj_rows[o[7] + h]));
       return x;
     };
     for (int64_t i = 0; i < n_ops; ++i) {
@@ -1263,8 +1304,8 @@ GANON_HOST_API int ganon_resolver_contig(ganon_resolver *r, int32_t job, int64_t
         }
         const int64_t *o = objs + 10 * op_rows[i];
         RObj x = object(op_rows[i]);
-        out_n[i] = r->passthrough(name, e[3], std::move(x), RInst{job, o[1], -1, o[3]}, (o[9] & 1) != 0, seq,
-                                  out_w + 14 * i);
+        const RInst rec{job, o[1], -1, o[3], obj_ids ? obj_ids[o[5]] : -1};   // (o[5]: the creator's entry)
+        out_n[i] = r->passthrough(name, e[3], std::move(x), rec, (o[9] & 1) != 0, seq, out_w + 14 * i);
         continue;
       }
       if (e[0] != 6 || !(e[2] & 1)) {
@@ -1397,7 +1438,7 @@ GANON_HOST_API int ganon_resolver_finish(ganon_resolver *r, int64_t n_cand, cons
     // pair_unmapped_mates (SR:561-600) runs only when something is left to pair (SR:752)
     if (!r->to_pair.empty()) {
       for (int64_t k = 0; k < n_cand; ++k) {
-        const int64_t *c = cand + 7 * k;
+        const int64_t *c = cand + 8 * k;
         if (c[2] < 0) {   // this window's fetch(first - 1, last) raises (pysam region check)
           g_err = "start out of range (" + std::to_string(c[3]) + ")";
           return GANON_PLAN_E_VALUE;
@@ -1412,7 +1453,7 @@ GANON_HOST_API int ganon_resolver_finish(ganon_resolver *r, int64_t n_cand, cons
           g_err = "read '" + name + "' has neither the READ1 nor the READ2 flag; the reference cannot store it (SURVEY Q8)";
           return GANON_PLAN_E_TYPE;
         }
-        const RInst rec{c[0], c[2], -1, c[3]};
+        const RInst rec{c[0], c[2], -1, c[3], c[7]};
         r->quiet = r->written.count(name) != 0;
         // an unmapped record flagged supplementary or carrying an SA tag creates an object with that
         // state (AnonymizedRead.__init__, AM:98-108): incomplete until its primary / supplementaries
@@ -1421,7 +1462,7 @@ GANON_HOST_API int ganon_resolver_finish(ganon_resolver *r, int64_t n_cand, cons
         nw.supp = rsupp;
         nw.has_sa = (c[6] & 2) != 0;
         nw.n_sa = (int32_t)(c[6] >> 8);
-        if (rsupp && nw.has_sa) nw.add_hash(record_id(rec.job, rec.ds, rec.row));
+        if (rsupp && nw.has_sa) nw.add_hash(record_id(rec));
         *n_tail += r->passthrough(name, (int)c[4], std::move(nw), rec, rsupp, INT64_MAX, tail + 7 * *n_tail);
       }
     }

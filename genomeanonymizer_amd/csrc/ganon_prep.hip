@@ -1526,6 +1526,77 @@ int grow(ganon_ctx *ctx, DBuf &b, size_t bytes) {
   return GANON_OK;
 }
 
+// Buffers of a plan with ng scope groups (the full plan once it knows the shape; a speculative plan
+// of new counts from the shape it assumes).
+int size_plan(ganon_ctx *ctx, ganon_dbatch *db, int64_t ng, int tgt0, const Raw &R) {
+  hipStream_t st = ctx->stream;
+  int rc;
+  longlong2 *gm = nullptr;
+  if (ng > INT32_MAX / kGrpRec) return fail(ctx, GANON_E_ARG, "batch too large: %lld scope groups", (long long)ng);
+  db->n_groups = (int32_t)ng;
+  int32_t *p32 = nullptr;
+  int4 *grp = nullptr;
+  unsigned long long *u64 = nullptr;
+  uint32_t *u32 = nullptr;
+  // (short-read modes: ng <= g_bound, so the scan's group table stays in place)
+  if ((rc = grow_n(ctx, db->b_gs0, (size_t)std::max<int64_t>(ng, 1), &gm)) ||
+      (rc = grow_n(ctx, db->b_groups, (size_t)kGrpRec * ng, &grp)) ||
+      (rc = grow_n(ctx, db->b_grp_part, 2 * (size_t)ng, &p32)) ||
+      (rc = grow_n(ctx, db->b_order, (size_t)ng + 1 + (size_t)kOrderRow * ((ng + kOrderThreads - 1) / kOrderThreads),
+                   &p32)) ||
+      (rc = grow_n(ctx, db->b_wspart, (size_t)std::max<int64_t>(ng, 1), &u64)) ||
+      (rc = grow_n(ctx, db->b_lo, 2 * (size_t)std::max<int64_t>(ng, 1), &u64)) ||
+      (rc = grow_n(ctx, db->b_linemap, (size_t)line_map_words(db), &u64)))
+    return rc;
+  int64_t extra_seg = 0;
+  if (!db->flat_mode && ng) {
+    // two-pass and long-read emits: a counting pass sizes the records of groups with more segments
+    // than incidences (sub-counter bases: exclusive prefix of the pass's totals, deterministic)
+    HIP_OR_FAIL(hipMemsetAsync(db->cursor + kCursors, 0, kCursors * sizeof(unsigned long long), st));
+    if ((rc = launch_groups(ctx, db, R)) || (rc = launch_emit(ctx, db, R, 0))) return rc;
+    std::vector<unsigned long long> cur(2 * kCursors, 0);
+    HIP_OR_FAIL(hipMemcpyAsync(cur.data(), db->cursor, kCursors * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+    HIP_OR_FAIL(hipStreamSynchronize(st));
+    unsigned long long tseg = 0;
+    for (int k = 0; k < kCursors; ++k) {
+      cur[kCursors + k] = tseg;
+      tseg += cur[k];
+    }
+    db->cursor_h.assign(cur.begin() + kCursors, cur.end());
+    HIP_OR_FAIL(hipMemcpyAsync(db->cursor + kCursors, db->cursor_h.data(), kCursors * sizeof(unsigned long long),
+                               hipMemcpyHostToDevice, st));
+    extra_seg = (int64_t)tseg;
+  }
+  db->n_seg = db->n_incid + extra_seg;   // record slots: one per incidence, then the long groups
+  db->region = db->n_incid * db->region_per_incid + (int64_t)kGrpObs * ng;
+  // far masks (bytes a group masks outside its own pieces, applied by k_finish): the list keeps its
+  // capacity across batches; a run that needs more reports the count (k_finish) and
+  // ganon_batch_download grows the list and runs again — no counting pass, no synchronization here
+  const int64_t far_want = ctx->far_init > 0 ? (int64_t)ctx->far_init
+                                             : std::min<int64_t>(kFarMax, std::max<int64_t>(int64_t(1) << 16, db->n_reads / 8));
+  db->far_cap = std::max<int64_t>(db->far_cap_alloc, far_want);
+  int4 *s4 = nullptr;
+  if ((rc = grow_n(ctx, db->b_seg4, (size_t)std::max<int64_t>(db->n_seg, 1), &s4))) return rc;
+  if ((rc = grow_n(ctx, db->b_far, (size_t)db->far_cap, &u64))) return rc;
+  db->far_cap_alloc = db->far_cap;
+  if ((rc = grow_n(ctx, db->b_gokey, (size_t)db->region, &u64)) || (rc = grow_n(ctx, db->b_gopay, (size_t)db->region, &u64)) ||
+      (rc = grow_n(ctx, db->b_gtkey, 2 * (size_t)db->region + 64, &u64)) ||
+      (rc = grow_n(ctx, db->b_gtflag, 2 * (size_t)db->region + 64, &u32)))
+    return rc;
+  db->spec_ready = db->flat_mode && db->n_huge_scopes == 0;
+  db->spec_sizes[0] = db->n_reads;
+  db->spec_sizes[1] = db->n_scopes;
+  db->spec_sizes[2] = db->n_incid;
+  db->spec_sizes[3] = tgt0;
+  if (!db->spec) {   // a full plan: the shape a new batch of this context may assume
+    ctx->spec_shape_ok = db->spec_ready;
+    ctx->spec_rpi = db->region_per_incid;
+    ctx->spec_tgt = tgt0;
+  }
+  return GANON_OK;
+}
+
+
 int plan(ganon_ctx *ctx, ganon_dbatch *db, bool allow_spec) {
   hipStream_t st = ctx->stream;
   int rc;
@@ -1543,14 +1614,22 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db, bool allow_spec) {
   const long long w0 = weight_of(tgt0);
   const int64_t g_bound = ns ? (db->n_incid + w0 * (ns - 1)) / tgt0 + 1 : 1;
   // speculative: the last full plan of db found a one-segment batch without huge scopes of these
-  // sizes; the run launches for the same shape at once and the scan's reduction checks it (gate)
-  const bool spec = allow_spec && ctx->spec_plan && db->spec_ready && db->spec_sizes[0] == nr && db->spec_sizes[1] == ns &&
-                    db->spec_sizes[2] == db->n_incid && db->spec_sizes[3] == tgt0 && db->flat_mode;
+  // sizes, or (other sizes: a new batch) the context's last full plan did; the run launches for that
+  // shape at once (buffers sized on the host from the counts) and the scan's reduction checks it (gate)
+  // ("same": the context's previous plan was of this batch — a replan of its contents in place)
+  const bool same = db->spec_ready && db->spec_sizes[0] == nr && db->spec_sizes[1] == ns &&
+                    db->spec_sizes[2] == db->n_incid && db->spec_sizes[3] == tgt0 && db->flat_mode &&
+                    ctx->last_plan == db;
+  ctx->last_plan = db;
+  const bool sized = !same && ctx->spec_shape_ok && ctx->spec_tgt == tgt0 && ctx->prep_long == -1;
+  const bool spec = allow_spec && ctx->spec_plan && (same || sized);
   db->spec = spec;
+  db->spec_sized = spec && sized;
   if (!spec) {
     db->n_groups = 0;
     db->spec_ready = false;
   }
+  const int64_t spec_rpi = !spec ? 0 : db->spec_sized ? ctx->spec_rpi : db->region_per_incid;
   longlong2 *gm = nullptr;
   unsigned long long *part = nullptr;
   const int64_t rb = (nr + kScanReadsPerBlock - 1) / kScanReadsPerBlock;
@@ -1575,10 +1654,26 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db, bool allow_spec) {
                        (int)rb);
     hipLaunchKernelGGL(k_prep_reduce, dim3(1), dim3(kReduceThreads), 0, st, R, part, pstride, (int)nb, w0, (long long)tgt0,
                        g_bound, db->plan_info, static_cast<const PrepErr *>(db->err),
-                       spec ? (long long)db->region_per_incid : 0ll, static_cast<const unsigned int *>(long_count));
+                       (long long)spec_rpi, static_cast<const unsigned int *>(long_count));
     if ((rc = check_launch(ctx, "k_prep_scan"))) return rc;
   }
-  if (spec) return GANON_OK;   // the previous plan's mode, sizes and buffers; errors at download
+  if (spec && !db->spec_sized) return GANON_OK;   // the previous plan's mode, sizes and buffers; errors at download
+  if (spec) {
+    // a new batch assumed to have the context's last shape: one-segment mode, no huge scope, reads no
+    // longer than that plan's; what the scan alone knows (the written reads, the I/D ops) stays on
+    // the device (prepare copies the written count into the static totals)
+    db->long_mode = false;
+    db->flat_mode = true;
+    db->region_per_incid = spec_rpi;
+    db->group_target = tgt0;
+    db->n_id_ops = 0;
+    db->max_len = 48 * spec_rpi;
+    db->max_seg = 1;
+    db->n_huge_scopes = 0;
+    db->n_written = -1;
+    db->scost = nullptr;
+    return size_plan(ctx, db, ns ? g_bound : 0, tgt0, R);
+  }
   // 2. the one synchronization of a fresh batch: its first error and its shape
   unsigned long long info[6] = {0, 0, 0, 0, 0, 0};
   PrepErr e{};
@@ -1654,63 +1749,7 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db, bool allow_spec) {
   // one-segment mode launches for the group bound (blocks past the scan's count return at once):
   // a speculative replan of the same sizes then needs no count from the host
   if (db->flat_mode && ns) ng = g_bound;
-  if (ng > INT32_MAX / kGrpRec) return fail(ctx, GANON_E_ARG, "batch too large: %lld scope groups", (long long)ng);
-  db->n_groups = (int32_t)ng;
-  int32_t *p32 = nullptr;
-  int4 *grp = nullptr;
-  unsigned long long *u64 = nullptr;
-  uint32_t *u32 = nullptr;
-  // (short-read modes: ng <= g_bound, so the scan's group table stays in place)
-  if ((rc = grow_n(ctx, db->b_gs0, (size_t)std::max<int64_t>(ng, 1), &gm)) ||
-      (rc = grow_n(ctx, db->b_groups, (size_t)kGrpRec * ng, &grp)) ||
-      (rc = grow_n(ctx, db->b_grp_part, 2 * (size_t)ng, &p32)) ||
-      (rc = grow_n(ctx, db->b_order, (size_t)ng + 1 + (size_t)kOrderRow * ((ng + kOrderThreads - 1) / kOrderThreads),
-                   &p32)) ||
-      (rc = grow_n(ctx, db->b_wspart, (size_t)std::max<int64_t>(ng, 1), &u64)) ||
-      (rc = grow_n(ctx, db->b_lo, 2 * (size_t)std::max<int64_t>(ng, 1), &u64)) ||
-      (rc = grow_n(ctx, db->b_linemap, (size_t)line_map_words(db), &u64)))
-    return rc;
-  int64_t extra_seg = 0;
-  if (!db->flat_mode && ng) {
-    // two-pass and long-read emits: a counting pass sizes the records of groups with more segments
-    // than incidences (sub-counter bases: exclusive prefix of the pass's totals, deterministic)
-    HIP_OR_FAIL(hipMemsetAsync(db->cursor + kCursors, 0, kCursors * sizeof(unsigned long long), st));
-    if ((rc = launch_groups(ctx, db, R)) || (rc = launch_emit(ctx, db, R, 0))) return rc;
-    std::vector<unsigned long long> cur(2 * kCursors, 0);
-    HIP_OR_FAIL(hipMemcpyAsync(cur.data(), db->cursor, kCursors * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
-    HIP_OR_FAIL(hipStreamSynchronize(st));
-    unsigned long long tseg = 0;
-    for (int k = 0; k < kCursors; ++k) {
-      cur[kCursors + k] = tseg;
-      tseg += cur[k];
-    }
-    db->cursor_h.assign(cur.begin() + kCursors, cur.end());
-    HIP_OR_FAIL(hipMemcpyAsync(db->cursor + kCursors, db->cursor_h.data(), kCursors * sizeof(unsigned long long),
-                               hipMemcpyHostToDevice, st));
-    extra_seg = (int64_t)tseg;
-  }
-  db->n_seg = db->n_incid + extra_seg;   // record slots: one per incidence, then the long groups
-  db->region = db->n_incid * db->region_per_incid + (int64_t)kGrpObs * ng;
-  // far masks (bytes a group masks outside its own pieces, applied by k_finish): the list keeps its
-  // capacity across batches; a run that needs more reports the count (k_finish) and
-  // ganon_batch_download grows the list and runs again — no counting pass, no synchronization here
-  const int64_t far_want = ctx->far_init > 0 ? (int64_t)ctx->far_init
-                                             : std::min<int64_t>(kFarMax, std::max<int64_t>(int64_t(1) << 16, db->n_reads / 8));
-  db->far_cap = std::max<int64_t>(db->far_cap_alloc, far_want);
-  int4 *s4 = nullptr;
-  if ((rc = grow_n(ctx, db->b_seg4, (size_t)std::max<int64_t>(db->n_seg, 1), &s4))) return rc;
-  if ((rc = grow_n(ctx, db->b_far, (size_t)db->far_cap, &u64))) return rc;
-  db->far_cap_alloc = db->far_cap;
-  if ((rc = grow_n(ctx, db->b_gokey, (size_t)db->region, &u64)) || (rc = grow_n(ctx, db->b_gopay, (size_t)db->region, &u64)) ||
-      (rc = grow_n(ctx, db->b_gtkey, 2 * (size_t)db->region + 64, &u64)) ||
-      (rc = grow_n(ctx, db->b_gtflag, 2 * (size_t)db->region + 64, &u32)))
-    return rc;
-  db->spec_ready = db->flat_mode && db->n_huge_scopes == 0;
-  db->spec_sizes[0] = nr;
-  db->spec_sizes[1] = ns;
-  db->spec_sizes[2] = db->n_incid;
-  db->spec_sizes[3] = tgt0;
-  return GANON_OK;
+  return size_plan(ctx, db, ng, tgt0, R);
 }
 
 int run(ganon_ctx *ctx, ganon_dbatch *db) {

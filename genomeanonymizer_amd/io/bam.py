@@ -289,6 +289,19 @@ class BamReader:
                                     f"{lib.ganon_host_last_error().decode()}")
         return ReadTable(self.path, handle=h)
 
+    def region(self, tid: int, beg: int, end: int) -> ReadTable:
+        """The records of BAM sequence ``tid`` overlapping [beg, end) (0-based, htslib's fetch
+        semantics), through the index (``ganon_bam_reader_region``; an index is required)."""
+        if tid < 0:
+            return self.empty()
+        lib = native.host_lib()
+        h = C.c_void_p()
+        rc = lib.ganon_bam_reader_region(self._h, int(tid), int(beg), int(end), C.byref(h))
+        if rc != 0:
+            raise native.GanonError(f"cannot decode {self.path} sequence {tid} [{beg}, {end}): "
+                                    f"{lib.ganon_host_last_error().decode()}")
+        return ReadTable(self.path, handle=h)
+
     def empty(self) -> ReadTable:
         """A table with no records and this file's reference list."""
         t = ReadTable.__new__(ReadTable)

@@ -169,6 +169,7 @@ def hip_lib():
     lib.ganon_batch_info.argtypes = [_p, _i64p]
     lib.ganon_batch_shape.argtypes = [_p, _i64p]
     lib.ganon_batch_path_counts.argtypes = [_p, _p, _i64p]
+    lib.ganon_batch_gated_runs.argtypes = [_p, _p, _i64p]
     lib.ganon_fastq_upload.argtypes = [_p, C.POINTER(GanonFastqRecords), C.POINTER(_p)]
     lib.ganon_fastq_run.argtypes = [_p, _p]
     lib.ganon_fastq_bytes.argtypes = [_p]
@@ -216,7 +217,7 @@ EXPORTED_HIP_SYMBOLS = (
     "ganon_batch_run", "ganon_batch_sync", "ganon_batch_download", "ganon_batch_free",
     "ganon_batch_device_totals", "ganon_batch_copy_totals", "ganon_last_kernel_times", "ganon_batch_info",
     "ganon_batch_shape",
-    "ganon_batch_path_counts",
+    "ganon_batch_path_counts", "ganon_batch_gated_runs",
     "ganon_fastq_upload", "ganon_fastq_run", "ganon_fastq_bytes", "ganon_fastq_device_output",
     "ganon_fastq_download", "ganon_fastq_free", "ganon_fastq_format_hip",
     "ganon_indel_upload", "ganon_indel_run", "ganon_indel_download", "ganon_indel_info", "ganon_indel_free",
@@ -227,7 +228,7 @@ EXPORTED_HOST_SYMBOLS = (
     "ganon_host_last_error", "ganon_host_inflate_backend", "ganon_fastq_format", "ganon_pack_nt16",
     "ganon_plan_run", "ganon_plan_view_get", "ganon_plan_free", "ganon_plan_last_error", "ganon_io_replay",
     "ganon_bam_reader_open", "ganon_bam_reader_set_window", "ganon_bam_reader_has_index", "ganon_bam_reader_header",
-    "ganon_bam_reader_contig", "ganon_bam_reader_close",
+    "ganon_bam_reader_contig", "ganon_bam_reader_region", "ganon_bam_reader_close",
     "ganon_resolver_create", "ganon_resolver_free", "ganon_resolver_contig", "ganon_resolver_pending",
     "ganon_resolver_finish", "ganon_resolver_take_log", "ganon_resolver_mark_written", "ganon_objects_pack", "ganon_blob_size", "ganon_blob_data",
     "ganon_blob_free", "ganon_objects_create", "ganon_objects_free", "ganon_objects_add_job", "ganon_objects_add_plain",
@@ -754,6 +755,13 @@ class DeviceBatch:
         return {"sorted_lists": int(a[0]), "overflowing_lists": int(a[1]), "key_range_splits": int(a[2]),
                 "filtered_into_lds": int(a[3])}
 
+    def gated_runs(self) -> int:
+        """ganon_batch_gated_runs: runs since upload whose speculative plan the batch did not fit
+        (they ran nothing; the download planned and ran the batch in full)."""
+        a = np.zeros(1, np.int64)
+        self.m._check(self.m._lib.ganon_batch_gated_runs(self.m._h, self.h, _ptr(a, _i64p)), "gated_runs")
+        return int(a[0])
+
     def indel_tally(self, arrays: dict) -> "DeviceIndels":
         """Plan the germline indel tally of this batch (``arrays`` = the batch it was uploaded from)."""
         iv = indel_view(arrays)
@@ -823,7 +831,7 @@ class PlanTable(C.Structure):
     _fields_ = [("n", C.c_int64), ("tid", _i32p), ("pos", _i32p), ("end", _i32p), ("flag", _i32p),
                 ("l_seq", _i32p), ("n_cigar", _i32p), ("names", _p), ("name_off", _i64p), ("name_len", _i32p),
                 ("n_ref", C.c_int32), ("ref_len", _i64p), ("tid_of_contig", _i32p), ("mate_tid", _i32p),
-                ("n_sa", _i32p)]
+                ("mate_pos", _i32p), ("n_sa", _i32p)]
 
 
 class PlanInput(C.Structure):
@@ -831,7 +839,8 @@ class PlanInput(C.Structure):
                 ("contig_names", _p), ("contig_name_off", _i64p), ("n_windows", C.c_int32),
                 ("win_contig", _i32p), ("win_first", _i64p), ("win_last", _i64p),
                 ("contig_mode", C.c_int32), ("only_contig", C.c_int32), ("n_force", C.c_int64),
-                ("force_names", _p), ("force_off", _i64p), ("force_len", _i32p)]
+                ("force_names", _p), ("force_off", _i64p), ("force_len", _i32p),
+                ("sec_lo", C.c_int32), ("sec_hi", C.c_int32), ("reg_lo", C.c_int64), ("reg_hi", C.c_int64)]
 
 
 class PlanView(C.Structure):
@@ -856,12 +865,13 @@ def _np_copy(ptr, n: int, dtype) -> np.ndarray:
 
 
 def plan_sample(tables, contig_names, contig_lens, win_contig, win_first, win_last, only_contig=None,
-                force_names=()) -> dict:
+                force_names=(), job=None) -> dict:
     """``ganon_plan_run`` over two ReadTables (io/bam.py) and the variant windows. Returns the
     plan's column arrays (copies); raises ValueError / TypeError / planner.UnsupportedInput as
     the reference's own code would (message from the library). ``only_contig``: contig mode for
     that FASTA contig (tables holding its records only), see include/ganon_host.h; ``force_names``
-    (bytes): names planned as cross names there (``ganon_plan_input.force_names``)."""
+    (bytes): names planned as cross names there (``ganon_plan_input.force_names``); ``job``:
+    (first section, end section, region start, region end) of job mode (``ganon_plan_input.sec_lo``)."""
     lib = host_lib()
     keep = []
 
@@ -886,6 +896,7 @@ def plan_sample(tables, contig_names, contig_lens, win_contig, win_first, win_la
         idx = {nm: i for i, nm in enumerate(t.ref_names)}
         pt.tid_of_contig = arr([idx.get(c, -1) for c in contig_names], np.int32)
         pt.mate_tid = arr(t.mate_tid, np.int32)
+        pt.mate_pos = arr(t.mate_pos, np.int32)
         if only_contig is not None or t.may_be_complex():
             pt.n_sa = arr(t.sa_count(), np.int32)
     inp.n_contigs = len(contig_names)
@@ -902,6 +913,7 @@ def plan_sample(tables, contig_names, contig_lens, win_contig, win_first, win_la
     inp.win_last = arr(win_last, np.int64)
     inp.contig_mode = 0 if only_contig is None else 1
     inp.only_contig = -1 if only_contig is None else int(only_contig)
+    inp.sec_lo, inp.sec_hi, inp.reg_lo, inp.reg_hi = (-1, -1, 0, 0) if job is None else tuple(int(x) for x in job)
     force_names = list(force_names)
     if force_names:
         inp.n_force = len(force_names)
@@ -980,7 +992,7 @@ class Resolver:
         raise GanonError(f"resolver failed ({rc}): {msg}")
 
     def contig(self, job: int, ops: np.ndarray, op_rows: np.ndarray, op_names: list, left: np.ndarray,
-               left_names: list, objs: np.ndarray = None, obj_rows: np.ndarray = None):
+               left_names: list, objs: np.ndarray = None, obj_rows: np.ndarray = None, obj_ids: np.ndarray = None):
         """Returns (n_writes per op, writes [n_ops, 2, 7]); ``objs``/``obj_rows``: the plan's
         objects of complex names (their log: ``take_log``)."""
         keep = []
@@ -989,7 +1001,10 @@ class Resolver:
         left = np.ascontiguousarray(left, np.int64).reshape(-1, 11)
         objs = np.ascontiguousarray(np.zeros((0, 10), np.int64) if objs is None else objs, np.int64).reshape(-1, 10)
         obj_rows = np.ascontiguousarray(np.zeros(0, np.int64) if obj_rows is None else obj_rows, np.int64)
-        keep += [objs, obj_rows]
+        ids = None if obj_ids is None else np.ascontiguousarray(obj_ids, np.int64)
+        if ids is not None and len(ids) != len(obj_rows):
+            raise ValueError("obj_ids: one per obj_rows entry")
+        keep += [objs, obj_rows, ids]
         n = len(ops)
         out_n = np.zeros(max(n, 1), np.int32)
         out_w = np.zeros((max(n, 1), 2, 7), np.int64)
@@ -998,6 +1013,7 @@ class Resolver:
         rc = self._lib.ganon_resolver_contig(self._h, int(job), n, ops.ctypes.data_as(_i32p), rows.ctypes.data_as(_i64p),
                                              on, oo, ol, len(left), left.ctypes.data_as(_i64p), ln, lo, ll,
                                              len(objs), objs.ctypes.data_as(_i64p), obj_rows.ctypes.data_as(_i64p),
+                                             None if ids is None or not len(ids) else ids.ctypes.data_as(_i64p),
                                              out_n.ctypes.data_as(_i32p), out_w.ctypes.data_as(_i64p))
         if rc != 0:
             self._err(rc)
@@ -1032,7 +1048,7 @@ class Resolver:
         """Returns (tail writes [n, 7], single ends per dataset [m, 5] (job, ds, scope, row,
         reapply), write_single_end)."""
         keep = []
-        cand = np.ascontiguousarray(cand, np.int64).reshape(-1, 7)
+        cand = np.ascontiguousarray(cand, np.int64).reshape(-1, 8)
         n_pend = self._lib.ganon_resolver_pending(self._h, None, 0)
         tail = np.zeros((max(2 * len(cand), 1), 7), np.int64)
         s0 = np.zeros((max(n_pend, 1), 5), np.int64)
@@ -1248,6 +1264,7 @@ def host_lib():
     lib.ganon_bam_reader_set_window.argtypes = [_p, C.c_int64]
     lib.ganon_bam_reader_header.argtypes = [_p, C.POINTER(BamView)]
     lib.ganon_bam_reader_contig.argtypes = [_p, C.c_int32, C.POINTER(_p)]
+    lib.ganon_bam_reader_region.argtypes = [_p, C.c_int32, C.c_int64, C.c_int64, C.POINTER(_p)]
     lib.ganon_bam_reader_close.argtypes = [_p]
     lib.ganon_bam_reader_set_inflater.argtypes = [_p, _p, _p, C.c_int64]
     lib.ganon_host_last_error.restype = C.c_char_p
@@ -1265,7 +1282,7 @@ def host_lib():
     lib.ganon_resolver_create.argtypes = [C.POINTER(_p)]
     lib.ganon_resolver_free.argtypes = [_p]
     lib.ganon_resolver_contig.argtypes = [_p, C.c_int32, C.c_int64, _i32p, _i64p, _p, _i64p, _i32p, C.c_int64, _i64p,
-                                          _p, _i64p, _i32p, C.c_int64, _i64p, _i64p, _i32p, _i64p]
+                                          _p, _i64p, _i32p, C.c_int64, _i64p, _i64p, _i64p, _i32p, _i64p]
     lib.ganon_objects_pack.argtypes = [C.POINTER(ObjectsSrc), C.POINTER(_p)]
     lib.ganon_blob_size.argtypes = [_p]
     lib.ganon_blob_size.restype = C.c_int64

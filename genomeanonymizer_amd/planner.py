@@ -583,6 +583,7 @@ class NativeSamplePlanner(SamplePlanner):
     native = True
     only_contig: Optional[int] = None   # contig mode (ContigPlanner)
     force_names: Sequence[bytes] = ()   # contig mode: names planned as cross names (ContigPlanner)
+    job: Optional[Tuple[int, int, int, int]] = None   # job mode: sections [lo, hi) of the contig, region
 
     def run(self) -> Plan:
         from . import native
@@ -591,7 +592,7 @@ class NativeSamplePlanner(SamplePlanner):
         w = self.windows
         res = native.plan_sample(self.tables, refs, list(self.fasta.lengths),
                                  [cidx[x.sequence] for x in w], [x.first for x in w], [x.last for x in w],
-                                 only_contig=self.only_contig, force_names=self.force_names)
+                                 only_contig=self.only_contig, force_names=self.force_names, job=self.job)
         self.contig_exports = {"left": res["left"], "cand": res["cand"], "objs": res["objs"],
                                "obj_rows": res["obj_rows"]}
         T, N = self.tables
@@ -630,9 +631,12 @@ class ContigPlanner(NativeSamplePlanner):
     another sequence (secondary alignments elsewhere whose mate is on this contig, stream.py)."""
 
     def __init__(self, tumor: ReadTable, normal: ReadTable, fasta: FastaRef, windows: Sequence[Window],
-                 contig_index: int, force_names: Sequence[bytes] = ()):
+                 contig_index: int, force_names: Sequence[bytes] = (), job: Optional[Tuple[int, int, int, int]] = None):
+        """``job``: (first section, end section, region start, region end): job mode, a run of the
+        contig's sections planned from the records overlapping the region (stream.py)."""
         self.only_contig = int(contig_index)
         self.force_names = sorted(force_names)
+        self.job = job
         super().__init__(tumor, normal, fasta, windows)
 
 

@@ -29,6 +29,7 @@ their resolution plus the prefetched ones, and the carried records of names stil
 """
 from __future__ import annotations
 
+import dataclasses
 import os
 import threading
 import time
@@ -42,7 +43,7 @@ from . import objects
 from .anonymizer_methods import CompleteGermlineAnonymizer, MaskResult, build_batch
 from .io.bam import BamReader, ReadTable
 from .io.fasta import FastaRef
-from .planner import ContigPlanner, Plan, Window
+from .planner import ContigPlanner, Plan, Window, get_genome_sections
 from . import writer as _writer
 from .writer import OUTSIDE_WINDOWS, FastqFormatter, statistics_rows, write_statistics
 
@@ -74,47 +75,179 @@ def _pwrite_all(fd: int, data, offset: int) -> None:
         done += n
 
 
-def decode_contig(readers, contig: str, secondaries: "Optional[SecondaryIndex]" = None, job: int = -1):
-    """The contig's records of both BAMs (io.bam.BamReader.contig); with ``secondaries``, the
-    secondary alignments among them whose mate is on another contig are published there before the
-    tables are handed on (the decode runs in job order, so every later job's plan sees them)."""
-    tables = tuple(r.contig(r.tid_of(contig)) for r in readers)
+@dataclasses.dataclass(frozen=True)
+class JobSpec:
+    """One unit of the streamed sample: a FASTA contig, or a run of consecutive sections of it (job
+    mode). The reference's unit of work is the section (anonymize_genome, SR:660-697); a run of
+    sections is planned from the records overlapping ``region``, the union of its sections' region
+    queries (the jobs of a contig tile it)."""
+    index: int
+    contig: str
+    cidx: int                                   # FASTA index of the contig
+    sections: Optional[Tuple[int, int]] = None  # [first, end) in the contig's section order; None = all
+    region: Optional[Tuple[int, int]] = None    # [beg, end), 0-based: the records decoded
+    length: int = 0                             # bases (sharding weight)
+
+    def label(self) -> str:
+        return self.contig if self.region is None else f"{self.contig}:{self.region[0]}-{self.region[1]}"
+
+
+def plan_jobs(fasta: FastaRef, windows: Sequence[Window], job_bp: int, indexed: bool) -> List[JobSpec]:
+    """The sample's jobs in FASTA then section order. ``job_bp`` > 0 and indexed BAMs: each contig
+    longer than job_bp is cut at section boundaries into runs of about job_bp bases (a short tail
+    joins the run before it); else one job per contig. A contig whose sections do not tile it (the
+    reference's region errors) stays whole."""
+    refs, lens = list(fasta.references), list(fasta.lengths)
+    if job_bp <= 0 or not indexed:
+        return [JobSpec(i, c, i, None, None, int(L)) for i, (c, L) in enumerate(zip(refs, lens))]
+    by: Dict[str, List[Window]] = {c: [] for c in refs}
+    for w in get_genome_sections(windows, fasta):
+        by[w.sequence].append(w)
+    out: List[JobSpec] = []
+    for ci, (c, L) in enumerate(zip(refs, lens)):
+        ss = by[c]
+        tiles = (len(ss) > 1 and ss[0].first == 1 and ss[-1].last == L - 1 and
+                 all(w.first <= w.last for w in ss) and
+                 all(ss[k].first == ss[k - 1].last + 1 for k in range(1, len(ss))))
+        cuts = [0]
+        if tiles and L > job_bp:
+            acc = 0
+            for k, w in enumerate(ss):
+                acc += w.last - w.first + 1
+                if acc >= job_bp and k + 1 < len(ss):
+                    cuts.append(k + 1)
+                    acc = 0
+            if len(cuts) > 1 and ss[-1].last - ss[cuts[-1]].first + 1 < job_bp // 2:
+                cuts.pop()
+        if len(cuts) == 1:
+            out.append(JobSpec(len(out), c, ci, None, None, int(L)))
+            continue
+        cuts.append(len(ss))
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            lo = 0 if a == 0 else ss[a].first - 1
+            hi = int(L) if b == len(ss) else ss[b - 1].last
+            out.append(JobSpec(len(out), c, ci, (a, b), (lo, hi), hi - lo))
+    return out
+
+
+def decode_job(readers, spec: JobSpec, secondaries: "Optional[SecondaryIndex]" = None):
+    """The job's records of both BAMs (io.bam.BamReader.contig, or .region in job mode); with
+    ``secondaries``, the secondary alignments among them whose mate another job reads are published
+    there before the tables are handed on (the decode runs in job order, so every later job's plan
+    sees them)."""
+    if spec.region is None:
+        tables = tuple(r.contig(r.tid_of(spec.contig)) for r in readers)
+    else:
+        # the scopes of a gap section pile up the union of its read clusters (pileup_io.pyx:124-298,
+        # SR:523-534), which reaches past the job's range by a read's extent: the records overlapping
+        # [lo, hi) fix the range the job's pileups can touch; read with a margin, again if it was short
+        lo, hi = spec.region
+        m = int(os.environ.get("GANON_JOB_MARGIN", "4096"))
+        tables = tuple(r.region(r.tid_of(spec.contig), max(0, lo - m), hi + m) for r in readers)
+        need_lo, need_hi = lo, hi
+        for t in tables:
+            if t.n:
+                sel = (np.asarray(t.pos) < hi) & (np.asarray(t.end) > lo) & ((np.asarray(t.flag) & 4) == 0)
+                if sel.any():
+                    need_lo = min(need_lo, int(np.asarray(t.pos)[sel].min()))
+                    need_hi = max(need_hi, int(np.asarray(t.end)[sel].max()))
+        if need_lo < lo - m or need_hi > hi + m:
+            tables = tuple(r.region(r.tid_of(spec.contig), need_lo, need_hi) for r in readers)
     if secondaries is not None:
-        secondaries.publish(job, secondaries.scan(tables))
+        secondaries.publish(spec.index, secondaries.scan(tables, spec.index)[0])
     return tables
 
 
-class SecondaryIndex:
-    """Secondary alignments off their mate's contig (flag 0x100, mate_tid != tid). Their name's
-    other records say nothing of them, so the contig holding the mate plans that name locally unless
-    told (the reference keeps one pairing state per name for the whole sample, SR:134-165,
-    AM:320-389): a job planned after such a secondary's contig plans the name as a cross name
-    (``forced_for``); a job planned before it wrote the name itself, which the coordinator marks in
-    the resolver when it meets the secondary (``ganon_resolver_mark_written``). The coordinator
-    checks every export against the secondaries of the jobs before it and asks the owner to plan
-    a job again when one was published too late (another rank decoded it)."""
+def content_ids(table: ReadTable, rows: np.ndarray) -> np.ndarray:
+    """A record's identity for the supplementary records an object recorded
+    (get_supplementary_hash_from_aln: reference, start, CIGAR, sequence, qualities, flag; AM:61-62):
+    a 63-bit mix of its sequence, position, flag, length and CIGAR words, so that a record two jobs'
+    tables both hold is one record (vectorised)."""
+    rows = np.asarray(rows, np.int64)
+    if not len(rows):
+        return np.zeros(0, np.int64)
+    M = np.uint64(0xFFFFFFFFFFFFFFFF)
 
-    def __init__(self, readers, contigs: Sequence[str]):
-        idx = {c: i for i, c in enumerate(contigs)}
-        # FASTA job of every BAM tid, per sample (-1: not a FASTA contig)
-        self.job_of_tid = [np.array([idx.get(n, -1) for n in r.ref_names] + [-1], np.int64) for r in readers]
+    def mix(x):
+        x = (x + np.uint64(0x9E3779B97F4A7C15)) & M
+        x = ((x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)) & M
+        x = ((x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)) & M
+        return x ^ (x >> np.uint64(31))
+
+    with np.errstate(over="ignore"):
+        u = lambda a: np.asarray(a, np.int64).astype(np.uint64)
+        h = mix(u(table.tid[rows]) << np.uint64(32) | (u(table.pos[rows]) & np.uint64(0xFFFFFFFF)))
+        h = mix(h ^ (u(table.flag[rows]) << np.uint64(40) | u(table.l_seq[rows])))
+        nc = np.asarray(table.n_cigar[rows], np.int64)
+        co = np.asarray(table.cig_off[rows], np.int64)
+        tot = int(nc.sum())
+        if tot:
+            idx = np.repeat(co - np.concatenate([[0], np.cumsum(nc)[:-1]]), nc) + np.arange(tot)
+            w = mix(u(table.cigar[idx]) + u(np.arange(tot) - np.repeat(np.concatenate([[0], np.cumsum(nc)[:-1]]), nc)))
+            acc = np.zeros(len(rows), np.uint64)
+            np.add.at(acc, np.repeat(np.arange(len(rows)), nc), w)
+            h = mix(h ^ acc)
+    return (h >> np.uint64(1)).astype(np.int64)
+
+
+class SecondaryIndex:
+    """Secondary alignments whose mate another job reads (flag 0x100; the mate on another contig,
+    or in job mode in another run of sections). Their name's other records say nothing of them, so
+    the job holding the mate plans that name locally unless told (the reference keeps one pairing
+    state per name for the whole sample, SR:134-165, AM:320-389): a job planned after such a
+    secondary's job plans the name as a cross name (``forced_for``); a job planned before it wrote
+    the name itself, which the coordinator marks in the resolver when it meets the secondary
+    (``ganon_resolver_mark_written``). The coordinator checks every export against the secondaries
+    of the jobs before it and asks the owner to plan a job again when one was published too late
+    (another rank decoded it)."""
+
+    def __init__(self, readers, jobs: Sequence[JobSpec]):
+        contigs: Dict[str, int] = {}
+        for j in jobs:
+            contigs.setdefault(j.contig, j.cidx)
+        # FASTA contig of every BAM tid, per sample (-1: not a FASTA contig)
+        self.contig_of_tid = [np.array([contigs.get(n, -1) for n in r.ref_names] + [-1], np.int64) for r in readers]
+        n_c = max(contigs.values()) + 1 if contigs else 0
+        self.starts: List[np.ndarray] = [np.zeros(0, np.int64)] * n_c   # per contig: its jobs' region starts
+        self.ids: List[np.ndarray] = [np.zeros(0, np.int64)] * n_c
+        for c in range(n_c):
+            js = [j for j in jobs if j.cidx == c]
+            self.starts[c] = np.array([j.region[0] if j.region else 0 for j in js], np.int64)
+            self.ids[c] = np.array([j.index for j in js], np.int64)
         self.lock = threading.Lock()
         self.by_mate: Dict[int, Dict[bytes, int]] = {}   # mate job -> name -> lowest source job
 
-    def scan(self, tables) -> List[Tuple[bytes, int]]:
-        """(name, mate job) of each off-contig secondary alignment of ``tables``."""
+    def job_of(self, ds: int, tid: np.ndarray, pos: np.ndarray) -> np.ndarray:
+        """The job reading position pos of BAM tid (-1: none)."""
+        ct = self.contig_of_tid[ds]
+        c = ct[np.where((tid >= 0) & (tid < len(ct) - 1), tid, len(ct) - 1)]
+        out = np.full(len(tid), -1, np.int64)
+        for ci in np.unique(c[c >= 0]).tolist():
+            sel = np.nonzero(c == ci)[0]
+            k = np.searchsorted(self.starts[ci], pos[sel], side="right") - 1
+            out[sel] = self.ids[ci][np.maximum(k, 0)]
+        return out
+
+    def scan(self, tables, job: int) -> Tuple[List[Tuple[bytes, int]], List[bytes]]:
+        """(name, mate job) of each secondary alignment of ``tables`` whose mate another job reads,
+        and the names of all its secondary alignments (complex names of the job already)."""
         out: List[Tuple[bytes, int]] = []
+        own: List[bytes] = []
         for d, t in enumerate(tables):
             if not t.n:
                 continue
-            sel = np.nonzero(((t.flag & 0x100) != 0) & (t.mate_tid >= 0) & (t.mate_tid != t.tid))[0]
+            sec = np.nonzero((t.flag & 0x100) != 0)[0]
+            if not len(sec):
+                continue
+            own.extend(_names(t, sec))
+            sel = sec[np.asarray(t.mate_tid[sec]) >= 0]
             if not len(sel):
                 continue
-            mj = self.job_of_tid[d][np.minimum(t.mate_tid[sel], len(self.job_of_tid[d]) - 1)]
-            keep = mj >= 0
+            mj = self.job_of(d, np.asarray(t.mate_tid[sel], np.int64), np.asarray(t.mate_pos[sel], np.int64))
+            keep = (mj >= 0) & (mj != job)
             for nm, j in zip(_names(t, sel[keep]), mj[keep].tolist()):
                 out.append((nm, int(j)))
-        return out
+        return out, own
 
     def publish(self, job: int, pairs: List[Tuple[bytes, int]]) -> None:
         with self.lock:
@@ -124,7 +257,7 @@ class SecondaryIndex:
                     d[nm] = job
 
     def forced_for(self, job: int) -> List[bytes]:
-        """Names of published secondaries of earlier jobs whose mate is on ``job``."""
+        """Names of published secondaries of earlier jobs whose mate this job reads."""
         with self.lock:
             return sorted(nm for nm, src in self.by_mate.get(job, {}).items() if src < job)
 
@@ -135,21 +268,23 @@ class JobPrep:
     streamed loop runs it for the next contig in a prefetch thread while the current one masks,
     formats and writes (the BGZF inflate and the planner are native and drop the GIL)."""
 
-    def __init__(self, job: int, contig: str, readers, fasta: FastaRef, windows: Sequence[Window], tables=None,
+    def __init__(self, spec: JobSpec, readers, fasta: FastaRef, windows: Sequence[Window], tables=None,
                  secondaries: Optional[SecondaryIndex] = None, force: Optional[Sequence[bytes]] = None):
         """``tables``: the decoded records when a decode thread produced them (a Future);
         ``secondaries``: the run's SecondaryIndex; ``force``: names to plan as cross names (a job
         planned again), else the secondaries published for this job."""
-        self.job = job
-        self.contig = contig
+        self.spec = spec
+        self.job = spec.index
+        self.contig = spec.label()
         t0 = time.time()
-        self.tables = decode_contig(readers, contig, secondaries, job) if tables is None else tables.result()
+        self.tables = decode_job(readers, spec, secondaries) if tables is None else tables.result()
         t1 = time.time()
         if force is None:
-            force = secondaries.forced_for(job) if secondaries is not None else []
+            force = secondaries.forced_for(self.job) if secondaries is not None else []
         self.forced = sorted(set(force))
-        self.offsec = secondaries.scan(self.tables) if secondaries is not None else []
-        self.planner = ContigPlanner(self.tables[0], self.tables[1], fasta, windows, job, self.forced)
+        self.offsec, self.own_sec = secondaries.scan(self.tables, self.job) if secondaries is not None else ([], [])
+        job_arg = None if spec.sections is None else (spec.sections[0], spec.sections[1], spec.region[0], spec.region[1])
+        self.planner = ContigPlanner(self.tables[0], self.tables[1], fasta, windows, spec.cidx, self.forced, job_arg)
         self.plan: Plan = self.planner.run()
         ex = self.planner.contig_exports
         t2 = time.time()
@@ -224,14 +359,14 @@ class Job(JobPrep):
     """One contig: its JobPrep stage, then mask + format on the device; once resolved, its output
     bytes."""
 
-    def __init__(self, job: int, contig: str, readers, fasta: FastaRef, windows: Sequence[Window],
+    def __init__(self, spec: JobSpec, readers, fasta: FastaRef, windows: Sequence[Window],
                  anonymizer: CompleteGermlineAnonymizer, prepared=None, secondaries: Optional[SecondaryIndex] = None):
         """``prepared``: a ``concurrent.futures.Future`` of this job's JobPrep when the caller
         prefetched it; decode_s is then the time spent waiting for it and prefetch_s the time the
         thread spent (decode + plan + batch)."""
         t0 = time.time()
         if prepared is None:
-            JobPrep.__init__(self, job, contig, readers, fasta, windows, secondaries=secondaries)
+            JobPrep.__init__(self, spec, readers, fasta, windows, secondaries=secondaries)
             t_dec, t_pl, t_b = self.prep_timing
             hidden = 0.0
         else:
@@ -424,10 +559,15 @@ class Job(JobPrep):
         left_row = np.where(L[:, 1] == 1, L[:, 4], L[:, 8]) if len(L) else np.zeros(0, np.int64)
         C = self.cand
         cm = C[:, 1] >= 0 if len(C) else np.zeros(0, bool)
-        cand = np.zeros((len(C), 7), np.int64)
+        cand = np.zeros((len(C), 8), np.int64)
         if len(C):
             cand[:, 0] = self.job
             cand[:, 1:7] = C
+            cand[:, 7] = -1
+            for d in (0, 1):   # identities of the records that create objects with supplementary state
+                sel = np.nonzero((C[:, 1] == d) & (C[:, 5] != 0))[0]
+                if len(sel):
+                    cand[sel, 7] = content_ids(self.tables[d], C[sel, 2])
         cand_names = [b""] * len(C)
         idx = np.nonzero(cm)[0]
         for i, nm in zip(idx.tolist(), _names_ds(self.tables, C[idx, 1], C[idx, 2])):
@@ -468,8 +608,22 @@ class Job(JobPrep):
             "left": L, "left_names": _names_ds(self.tables, left_ds, left_row),
             "cand": cand, "cand_names": cand_names, "carry": carry, "carry_info": info,
             "objs": O, "obj_rows": self.obj_rows, "cx": self.cx,
-            "forced": self.forced, "offsec": self.offsec,
+            "obj_ids": self._obj_ids(), "forced": self.forced, "offsec": self.offsec, "own_sec": self.own_sec,
         }
+
+    def _obj_ids(self) -> Optional[np.ndarray]:
+        """content_ids of every obj_rows entry (the records of each object: alignments, then the
+        supplementary records it recorded; all of its dataset)."""
+        O = self.objs
+        if not len(O):
+            return None
+        ds = np.repeat(O[:, 1], O[:, 6] + O[:, 8])
+        ids = np.zeros(len(self.obj_rows), np.int64)
+        for d in (0, 1):
+            sel = np.nonzero(ds == d)[0]
+            if len(sel):
+                ids[sel] = content_ids(self.tables[d], self.obj_rows[sel])
+        return ids
 
     # -- output ----------------------------------------------------------------------------------
     def local_sizes(self) -> List[int]:
@@ -642,7 +796,7 @@ class _Coordinator:
         need = self.need_force.get(k)
         if not need:
             return []
-        return sorted(need - set(exp.get("forced", ())))
+        return sorted(need - set(exp.get("forced", ())) - set(exp.get("own_sec", ())))
 
     def _bytes_of(self, jb: int, d: int, sc: int, r: int, re_: int) -> bytes:
         if sc == -2:        # an object of a complex name (objects.Replay)
@@ -671,7 +825,7 @@ class _Coordinator:
         self.carry_info.update(e["carry_info"])
         self.replay.add_job(e["job"], e["cx"])
         out_n, out_w = self.resolver.contig(e["job"], e["ops"], e["op_rows"], e["op_names"], e["left"],
-                                            e["left_names"], e["objs"], e["obj_rows"])
+                                            e["left_names"], e["objs"], e["obj_rows"], e.get("obj_ids"))
         self.replay.run(self.resolver.take_log())
         c = e["cand"]
         self.cands.append(c)
@@ -716,7 +870,7 @@ class _Coordinator:
 
     def finish(self, rank0_fds) -> None:
         """End of the sample: pair_unmapped_mates, single ends (SR:561-622)."""
-        cand = np.concatenate(self.cands) if self.cands else np.zeros((0, 7), np.int64)
+        cand = np.concatenate(self.cands) if self.cands else np.zeros((0, 8), np.int64)
         tail, single, wse = self.resolver.finish(cand, self.cand_names)
         self.replay.run(self.resolver.take_log())
         per_file: List[List[bytes]] = [[], [], [], []]
@@ -772,9 +926,12 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
         inflater = native.GpuInflater(anonymizer.device, int(os.environ.get("GANON_GPU_INFLATE_MIN", "512")))
     readers = (BamReader(tumor_bam, threads, window_bytes, inflater),
                BamReader(normal_bam, threads, window_bytes, inflater))
-    contigs = list(fasta.references)
-    owner = assign_contigs(list(fasta.lengths), world)
-    mine = [j for j in range(len(contigs)) if owner[j] == rank]
+    # jobs: contigs, or runs of sections of about GANON_JOB_BP bases (default 4 Mb; 0 = whole
+    # contigs) when both BAMs are indexed
+    job_bp = int(os.environ.get("GANON_JOB_BP", str(4_000_000)))
+    jobs = plan_jobs(fasta, windows, job_bp, all(r.has_index for r in readers))
+    owner = assign_contigs([j.length for j in jobs], world)
+    mine = [j for j in range(len(jobs)) if owner[j] == rank]
     link = Link(dist)
     coord = _Coordinator(fds, (f"{tumor_out}.single_end.fastq", f"{normal_out}.single_end.fastq"), block_size) \
         if rank == 0 else None
@@ -782,7 +939,7 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
     stats_rows: List[Tuple[int, Dict[str, List[int]]]] = []
     totals = np.zeros(8, np.int64)
     totals_lock = threading.Lock()
-    secondaries = SecondaryIndex(readers, contigs)
+    secondaries = SecondaryIndex(readers, jobs)
 
     stash: Dict[int, list] = {}      # exports an owner sent after the job it is planning again
 
@@ -806,7 +963,7 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
         k = 0
         failed_owner = -1
         try:
-            for k in range(len(contigs)):
+            for k in range(len(jobs)):
                 o = owner[k]
                 exp = recv_export(o)
                 while exp.get("err") is None:
@@ -829,7 +986,7 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
             coord_exc[0] = e
             err = repr(e)
         if err is not None:
-            waiting = sorted({owner[j] for j in range(k, len(contigs))})
+            waiting = sorted({owner[j] for j in range(k, len(jobs))})
             for r in waiting:        # every worker with a job not resolved stops
                 link.send_resolution(r, {"err": err})
             for r in waiting:        # ... and answers with its error: drop what it sent before
@@ -855,8 +1012,8 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
     def submit_upto(i_last: int) -> None:
         while nxt[0] <= min(i_last, len(mine) - 1):
             j = mine[nxt[0]]
-            dec = dec_pool.submit(decode_contig, readers, contigs[j], secondaries, j)
-            ahead[j] = pool.submit(JobPrep, j, contigs[j], readers, fasta, windows, dec, secondaries)
+            dec = dec_pool.submit(decode_job, readers, jobs[j], secondaries)
+            ahead[j] = pool.submit(JobPrep, jobs[j], readers, fasta, windows, dec, secondaries)
             nxt[0] += 1
 
     # the writer thread: each exported job, in order, waits for its resolution, splices its bytes and
@@ -875,10 +1032,10 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
         readers: the decode thread owns the others) and send its export in place of the first."""
         if not redo_readers:
             redo_readers.extend(BamReader(p, threads, window_bytes) for p in (tumor_bam, normal_bam))
-        prep = JobPrep(job.job, job.contig, redo_readers, fasta, windows, secondaries=secondaries, force=force)
+        prep = JobPrep(job.spec, redo_readers, fasta, windows, secondaries=secondaries, force=force)
         done = Future()
         done.set_result(prep)
-        j2 = Job(job.job, job.contig, redo_readers, fasta, windows, anonymizer, done)
+        j2 = Job(job.spec, redo_readers, fasta, windows, anonymizer, done)
         exp = j2.exports()
         exp["local_sizes"] = j2.local_sizes()
         exp["err"] = None
@@ -937,15 +1094,19 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
                 if pool is not None:
                     submit_upto(i + depth)
                     pre = ahead.pop(j)
-                job = Job(j, contigs[j], readers, fasta, windows, anonymizer, pre, secondaries)
+                job = Job(jobs[j], readers, fasta, windows, anonymizer, pre, secondaries)
                 exp = job.exports()
                 exp["local_sizes"] = job.local_sizes()
                 exp["err"] = None
                 for k in ("decode_s", "plan_s", "mask_s", "format_s", "prefetch_s"):
                     timing[k] += job.timing[k]
                 timing["jobs"] += 1
-                timing["reads"] += int(job.tables[0].n + job.tables[1].n)
-                timing["bases"] += int(job.tables[0].l_seq.sum(dtype=np.int64) + job.tables[1].l_seq.sum(dtype=np.int64))
+                # (job mode: the records starting in the job's range; the margin's belong to its neighbours)
+                for t in job.tables:
+                    own = slice(None) if job.spec.region is None else \
+                        (np.asarray(t.pos) >= job.spec.region[0]) & (np.asarray(t.pos) < job.spec.region[1])
+                    timing["reads"] += int(np.count_nonzero(np.ones(t.n, bool)[own]))
+                    timing["bases"] += int(np.asarray(t.l_seq)[own].sum(dtype=np.int64))
                 with totals_lock:
                     totals[:] += np.asarray(job.res.totals, np.int64)[:8]
                 link.send_export(exp)

@@ -605,12 +605,22 @@ def _random_genome(rng, total: int) -> np.ndarray:
     return lut[raw]
 
 
+_SITES_CACHE: Dict[tuple, tuple] = {}
+
+
 def config2_batch(n_reads: int = 10_000_000, genome: int = 3_000_000_000, n_contigs: int = 24,
                   n_windows: int = 1_000_000, n_germline: int = 1_000_000, read_len: int = 150,
-                  seed: int = 2, window_spacing: int = 2500) -> Tuple[Dict[str, np.ndarray], dict]:
-    """Vectorised BASELINE configs[1] batch. Returns (arrays, info)."""
-    rng = np.random.default_rng(seed)
+                  seed: int = 2, window_spacing: int = 2500, read_seed: int = None) -> Tuple[Dict[str, np.ndarray], dict]:
+    """Vectorised BASELINE configs[1] batch. Returns (arrays, info). ``read_seed``: the reads come
+    from their own generator (the genome, germline sites and windows from ``seed``, generated once
+    per process and shared): batches of other reads on the same sample."""
     L = read_len
+    key = (seed, genome, n_contigs, n_windows, n_germline, window_spacing)
+    if read_seed is not None and key in _SITES_CACHE:
+        clen, cstart, ref, gsnp, galt, win_contig, win_pos = _SITES_CACHE[key]
+        return _config2_reads(np.random.default_rng(read_seed), n_reads, L, n_contigs, clen, cstart, ref, gsnp, galt,
+                              win_contig, win_pos)
+    rng = np.random.default_rng(seed)
     # contigs: 24 of decreasing length summing to `genome`, each starting on a byte boundary
     w = np.linspace(2.0, 1.0, n_contigs)
     clen = np.floor(w / w.sum() * genome).astype(np.int64)
@@ -636,6 +646,17 @@ def config2_batch(n_reads: int = 10_000_000, genome: int = 3_000_000_000, n_cont
         win_pos.append(pos)
     win_contig = np.concatenate(win_contig)
     win_pos = np.concatenate(win_pos)
+    if read_seed is not None:
+        _SITES_CACHE[key] = (clen, cstart, ref, gsnp, galt, win_contig, win_pos)
+        rng = np.random.default_rng(read_seed)
+    return _config2_reads(rng, n_reads, L, n_contigs, clen, cstart, ref, gsnp, galt, win_contig, win_pos)
+
+
+def _config2_reads(rng, n_reads, L, n_contigs, clen, cstart, ref, gsnp, galt, win_contig, win_pos):
+    def ref_codes(gpos: np.ndarray) -> np.ndarray:
+        b = ref[gpos >> 1]
+        return np.where(gpos & 1, b & 0xF, b >> 4).astype(np.uint8)
+
     # reads: FR pairs, half tumor half normal
     n_pairs = n_reads // 2
     pc = rng.choice(n_contigs, size=n_pairs, p=clen / clen.sum())

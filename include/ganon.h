@@ -184,8 +184,11 @@ GANON_API int ganon_ref_free(ganon_ctx *ctx, ganon_ref *ref);
  * what a fresh batch costs: replan + run). Since ABI 4. A replan is speculative (no
  * synchronization: the scan and the run are enqueued back to back) when the batch's previous plan
  * found every read with at most one aligned segment and no scope wider than 2^20 positions, for
- * the same read / scope / incidence counts (GANON_PARAM_SPEC_PLAN 0 turns this off): the scan's
- * reduction checks that the new contents fit that plan and gates the run's kernels; a batch that
+ * the same read / scope / incidence counts, or — a batch of other counts — when the context's last
+ * full plan found that shape (the new batch is assumed to have it: its buffers are sized on the host
+ * from its counts, the overflow regions for reads no longer than that plan's) (GANON_PARAM_SPEC_PLAN
+ * 0 turns this off): the scan's reduction checks that the new contents fit that plan and gates the
+ * run's kernels; a batch that
  * does not fit (or fails validation) runs nothing, and ganon_batch_download then plans it in full
  * and runs it again (or returns the validation error) — the results are those of a full plan
  * either way. After a speculative replan, ganon_batch_info / ganon_batch_shape report the previous
@@ -228,6 +231,9 @@ GANON_API int ganon_batch_shape(ganon_dbatch *db, int64_t *shape4);
  * group's global region), key-range splits of an overflowing region, overflowing lists the Bloom
  * filter brought back into LDS (no region pass)]. */
 GANON_API int ganon_batch_path_counts(ganon_ctx *ctx, ganon_dbatch *db, int64_t *out4);
+/* Runs since upload whose speculative plan the batch did not fit (their kernels ran nothing; the
+ * next ganon_batch_download planned and ran the batch in full). Synchronous. Since ABI 4. */
+GANON_API int ganon_batch_gated_runs(ganon_ctx *ctx, ganon_dbatch *db, int64_t *out);
 
 /* ---- FASTQ record formatter ------------------------------------------
  * Replaces, for many reads at once, AnonymizedRead.get_anonymized_fastq_record

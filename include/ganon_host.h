@@ -89,6 +89,12 @@ GANON_HOST_API int ganon_bam_reader_set_inflater(ganon_bam_reader *reader, ganon
                                                  int64_t min_blocks);
 GANON_HOST_API int ganon_bam_reader_header(ganon_bam_reader *reader, ganon_bam_view *view);
 GANON_HOST_API int ganon_bam_reader_contig(ganon_bam_reader *reader, int32_t tid, ganon_bam **out);
+/* The records of tid overlapping [beg, end) (0-based; htslib's region semantics: pos < end and
+ * bam_endpos > beg, placed unmapped records at [pos, pos + 1)), file order, through the index's
+ * linear offsets (an index is required): what the reference's fetch(contig, beg, end) returns
+ * (pileup_io.pyx:138-139, short_read_tumor_normal_anonymizer.py:570-573). */
+GANON_HOST_API int ganon_bam_reader_region(ganon_bam_reader *reader, int32_t tid, int64_t beg, int64_t end,
+                                           ganon_bam **out);
 GANON_HOST_API void ganon_bam_reader_close(ganon_bam_reader *reader);
 
 /* FASTQ formatter. For record i:
@@ -164,6 +170,7 @@ typedef struct ganon_plan_table {  /* one sample, file order (columns of a ganon
   const int64_t *ref_len;          /* [n_ref] BAM header lengths                            */
   const int32_t *tid_of_contig;    /* [n_contigs] this BAM's tid of each FASTA contig, -1 none */
   const int32_t *mate_tid;         /* per record; read only in contig mode                    */
+  const int32_t *mate_pos;         /* per record; read only in job mode (ganon_plan_input.sec_hi) */
   const int32_t *n_sa;             /* per record: entries of its SA tag, -1 without one; NULL = none.
                                       Records with an SA tag or the SECONDARY / SUPPLEMENTARY flag make
                                       their name "complex" (contig mode only; see ganon_plan_view.objs) */
@@ -196,6 +203,14 @@ typedef struct ganon_plan_input {
   const char *force_names;
   const int64_t *force_off;
   const int32_t *force_len;
+  /* Job mode (contig mode with sec_hi >= 0): plan only sections [sec_lo, sec_hi) of the contig (its
+   * sections in get_genome_sections order, SR:245-276) from tables holding the records overlapping
+   * [reg_lo, reg_hi), the union of those sections' region queries (the jobs of a contig tile it, so
+   * a record overlapping another job's range is in both tables). Names with a record reaching outside
+   * the range, or whose mate starts outside it, are cross names too; the candidates are the windows
+   * of these sections only. */
+  int32_t sec_lo, sec_hi;
+  int64_t reg_lo, reg_hi;
 } ganon_plan_input;
 typedef struct ganon_plan ganon_plan;
 typedef struct ganon_plan_view {
@@ -262,14 +277,18 @@ typedef struct ganon_resolver ganon_resolver;
 GANON_HOST_API int ganon_resolver_create(ganon_resolver **out);
 GANON_HOST_API void ganon_resolver_free(ganon_resolver *r);
 /* ops: the placeholder events of job's plan (7 int32 each, plan layout) with their rows and read
- * names; left: the plan's unwritten pairs (11 int64 each) with names. out_n[i] receives the number of
- * writes op i makes (0 or 2), out_w 14 int64 per op. */
+ * names; left: the plan's unwritten pairs (11 int64 each) with names. obj_ids (NULL, or one per
+ * obj_rows entry, -1 = none): content identities of the objects' records, for the supplementary
+ * records an object recorded (get_supplementary_hash_from_aln, AM:61-62): a record the tables of two
+ * jobs both hold (job mode) is one record. out_n[i] receives the number of writes op i makes (0 or
+ * 2), out_w 14 int64 per op. */
 GANON_HOST_API int ganon_resolver_contig(ganon_resolver *r, int32_t job, int64_t n_ops, const int32_t *ops,
                                          const int64_t *op_rows, const char *op_names, const int64_t *op_name_off,
                                          const int32_t *op_name_len, int64_t n_left, const int64_t *left,
                                          const char *left_names, const int64_t *left_name_off,
                                          const int32_t *left_name_len, int64_t n_objs, const int64_t *objs,
-                                         const int64_t *obj_rows, int32_t *out_n, int64_t *out_w);
+                                         const int64_t *obj_rows, const int64_t *obj_ids, int32_t *out_n,
+                                         int64_t *out_w);
 /* Complex names (ganon_plan_view.objs): an object is identified by (job << 32) | index for the plan's
  * objects, or 1 << 62 | k for a plain instance the resolver had to follow as an object. A write of an
  * object is (file dataset, slot, -1, dataset, -2, serial, 0); what it writes follows from the object
@@ -288,8 +307,8 @@ GANON_HOST_API int64_t ganon_resolver_pending(ganon_resolver *r, int64_t *out, i
  * the resolver has no state for is marked written; returns how many were marked. */
 GANON_HOST_API int64_t ganon_resolver_mark_written(ganon_resolver *r, int64_t n, const char *names,
                                                    const int64_t *name_off, const int32_t *name_len);
-/* cand: 7 int64 per record (job, window, dataset, row, slot, no-SEQ flag, object info as in
- * ganon_plan_view.cand) in window order, with names. tail (14 int64 per candidate) receives the writes of pair_unmapped_mates (count n_tail);
+/* cand: 8 int64 per record (job, window, dataset, row, slot, no-SEQ flag, object info as in
+ * ganon_plan_view.cand, content identity or -1) in window order, with names. tail (14 int64 per candidate) receives the writes of pair_unmapped_mates (count n_tail);
  * single[d] (5 int64 per record: job, dataset, scope, row, reapply; capacity = ganon_resolver_pending
  * count) the single ends in dictionary order (counts n_single[2]). Returns GANON_PLAN_OK or GANON_PLAN_E_VALUE / _TYPE with the
  * reference's error (message: ganon_plan_last_error). */

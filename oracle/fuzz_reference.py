@@ -24,8 +24,12 @@ sys.path[:0] = [REPO, HERE]
 
 
 def scenario(seed: int):
+    """FUZZ_INDEX=1: the BAMs get a .bai (the product's job mode then cuts contigs into runs of
+    sections of GANON_JOB_BP bases)."""
+    import dataclasses
     from genomeanonymizer_amd.synth.generate import fuzz_scenario
-    return fuzz_scenario(seed)
+    sc = fuzz_scenario(seed)
+    return dataclasses.replace(sc, bam_index=True) if os.environ.get("FUZZ_INDEX") == "1" else sc
 
 
 def run_ref(paths, work):

@@ -24,15 +24,18 @@ def input_digests(paths) -> dict:
     return d
 
 
-def run_pipeline_vs_golden(name: str, workdir: str, anonymizer, block_size: int = 4096):
+def run_pipeline_vs_golden(name: str, workdir: str, anonymizer, block_size: int = 4096, bam_index: bool = False):
     """Regenerate the scenario's inputs, run the product pipeline, compare every output
-    file with the reference's. Returns a dict of mismatches (empty = byte-identical)."""
+    file with the reference's. Returns a dict of mismatches (empty = byte-identical).
+    ``bam_index``: write .bai files too (the streamed path's job mode reads regions through them)."""
+    import dataclasses
     from genomeanonymizer_amd.synth.generate import generate, scenario
     from genomeanonymizer_amd import short_read_tumor_normal_anonymizer as sr
     from genomeanonymizer_amd import writer
     meta = json.load(open(os.path.join(GOLDEN, name, "meta.json")))
     shutil.rmtree(workdir, ignore_errors=True)
-    paths = generate(scenario(name), os.path.join(workdir, "in"))
+    sc = dataclasses.replace(scenario(name), bam_index=True) if bam_index else scenario(name)
+    paths = generate(sc, os.path.join(workdir, "in"))
     assert input_digests(paths) == meta["inputs_sha256"], "synthetic generator drifted from the fixtures"
     t_out, n_out = sr.name_output(paths["T"]), sr.name_output(paths["N"])
     orig = writer.io_block_size

@@ -138,3 +138,32 @@ def test_middle_rank_failure_with_ranks_still_exporting(tmp_path):
             p.kill()
     assert alive == [False, False, False]
     assert all(p.exitcode != 0 for p in procs)
+
+
+def test_three_rank_job_mode_matches_reference(tmp_path, monkeypatch):
+    """Job mode over 3 ranks: ~2.5 kb runs of sections of each contig sharded over the ranks (region
+    decode, secondaries whose mate another rank's job reads: planned again), files = the reference's."""
+    import dataclasses
+    import gzip
+    from helpers import GOLDEN
+    from genomeanonymizer_amd.synth.generate import generate, scenario
+    from genomeanonymizer_amd.short_read_tumor_normal_anonymizer import name_output
+    monkeypatch.setenv("GANON_JOB_BP", "2500")
+    name = "fuzz3008"
+    workdir = str(tmp_path / name)
+    paths = generate(dataclasses.replace(scenario(name), bam_index=True), os.path.join(workdir, "in"))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 3, port, name, workdir, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(300)
+    assert all(p.exitcode == 0 for p in procs)
+    for tag, pre in (("tumor", name_output(paths["T"])), ("normal", name_output(paths["N"]))):
+        for suf in (".1.fastq", ".2.fastq", ".single_end.fastq"):
+            gp = os.path.join(GOLDEN, name, f"{tag}{suf}.gz")
+            if os.path.exists(gp):
+                assert open(pre + suf, "rb").read() == gzip.open(gp).read(), tag + suf
+    assert open(paths["N"] + ".statistics.txt").read() == open(os.path.join(GOLDEN, name, "normal.statistics.txt")).read()

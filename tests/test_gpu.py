@@ -267,6 +267,17 @@ def test_hip_pipeline_split_alignments_match_reference(name, whole, tmp_path, hi
     assert bad == {}
 
 
+@pytest.mark.parametrize("name", ["config1", "fuzz3008", "long1"])
+def test_hip_job_mode_matches_reference(name, tmp_path, hip_built, monkeypatch):
+    """Job mode through the HIP product: contigs cut into ~2.5 kb runs of sections (region decode with
+    a margin, one device batch per job, cross names resolved in job order); the reference's files."""
+    from genomeanonymizer_amd.anonymizer_methods import CompleteGermlineAnonymizer
+    monkeypatch.setenv("GANON_WHOLE_SAMPLE", "0")
+    monkeypatch.setenv("GANON_JOB_BP", "2500")
+    bad = run_pipeline_vs_golden(name, str(tmp_path / name), CompleteGermlineAnonymizer(device=0), bam_index=True)
+    assert bad == {}
+
+
 def test_hip_streaming_matches_whole_sample_many_contigs(tmp_path, hip_built, monkeypatch):
     """The streamed product (per-contig decode, contig-mode plans, one HIP batch per contig with the
     genome resident, cross-contig resolution) against the whole-sample product on a 12-contig
@@ -599,6 +610,51 @@ def _two_segment_copy(arr: dict, r: int) -> dict:
     b["n_cig"][r] = 3
     b["cigar"] = np.concatenate([b["cigar"], np.array([70 << 4, (5 << 4) | 1, 75 << 4], np.uint32)])
     return b
+
+
+def test_speculative_plan_of_new_counts(hip_built):
+    """Batches of other read / scope / incidence counts than the context's last plan speculate too
+    (buffers sized from their counts, the context's last shape assumed, the scan gating the run):
+    two resident batches of one sample replanned in turn give exactly their full plans' results;
+    a batch that does not fit that shape (a read with two segments) runs nothing, counts one gated
+    run, and its download plans and runs it in full."""
+    from genomeanonymizer_amd import native
+    from genomeanonymizer_amd.synth.batch import config2_batch
+    kw = dict(genome=30_000_000, n_windows=10_000, n_germline=25_000, seed=34)
+    a, _ = config2_batch(n_reads=120_000, read_seed=1, **kw)
+    b, _ = config2_batch(n_reads=124_000, read_seed=2, **kw)
+    assert len(a["read_len"]) != len(b["read_len"]) and len(a["incid_read"]) != len(b["incid_read"])
+    cand = np.nonzero((b["write_scope"] >= 0) & (b["n_cig"] == 1) & (b["read_len"] == 150))[0]
+    c = _two_segment_copy(b, int(cand[len(cand) // 2]))
+    m = native.HipMasker(0)
+    try:
+        want = [m.mask(x) for x in (a, b, c)]
+        ref = m.upload_reference(a["ref_nt16"])
+        dbs = [m.upload({k: v for k, v in x.items() if k != "ref_nt16"}, ref=ref) for x in (a, b, c)]
+        try:
+            for _ in range(3):            # a, b, a, b, ...: every replan is of other counts
+                for k in (0, 1):
+                    dbs[k].replan()
+                    dbs[k].run()
+                    got = dbs[k].download()
+                    assert all(np.array_equal(got[j], want[k][j]) for j in range(4))
+            assert dbs[0].gated_runs() == 0 and dbs[1].gated_runs() == 0
+            dbs[1].replan()               # (the context's last full shape: one-segment)
+            dbs[1].run()
+            dbs[2].replan()               # speculative; its two-segment read stops the run
+            dbs[2].run()
+            assert dbs[2].gated_runs() == 1
+            got = dbs[2].download()
+            assert all(np.array_equal(got[j], want[2][j]) for j in range(4))
+            assert dbs[2].shape()["max_seg"] == 2
+            got = dbs[1].download()
+            assert all(np.array_equal(got[j], want[1][j]) for j in range(4))
+        finally:
+            for d in dbs:
+                d.free()
+            ref.free()
+    finally:
+        m.close()
 
 
 def test_speculative_replan_and_fallback(hip_built):

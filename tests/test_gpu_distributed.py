@@ -13,7 +13,7 @@ from test_distributed import _free_port, _worker
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("name", ["edge", "config1", "fuzz2003"])
+@pytest.mark.parametrize("name", ["edge", "config1", "fuzz2003", "fuzz3008"])
 def test_two_rank_hip_contig_shards_match_reference(name, tmp_path, hip_built):
     import gzip
     from helpers import GOLDEN
@@ -34,7 +34,7 @@ def test_two_rank_hip_contig_shards_match_reference(name, tmp_path, hip_built):
         if p.is_alive():
             p.kill()
     assert codes == [0, 0], codes
-    results = dict(q.get() for _ in range(2))
+    results = {r: v[0] for r, v in (q.get() for _ in range(2))}   # (totals, redos)
     assert results[0] == results[1]            # totals are all-reduced
     assert results[0]["masked_snv_calls"] > 0
     for tag, pre in (("tumor", name_output(paths["T"])), ("normal", name_output(paths["N"]))):

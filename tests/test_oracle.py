@@ -146,3 +146,23 @@ def test_oracle_is_buffer_layout_invariant():
         o2, c2, b2, _ = e.mask(other)
         assert np.array_equal(c2, calls) and np.array_equal(b2, bases)
         assert np.array_equal(o2[np.repeat(other["seq_off"], nb) + rel], out[np.repeat(arr["seq_off"], nb) + rel])
+
+
+@pytest.mark.parametrize("name", ["edge", "config1", "fuzz9", "fuzz2003", "fuzz3000", "fuzz3008", "long1", "fuzz9001"])
+def test_job_mode_matches_reference(name, tmp_path, monkeypatch):
+    """Job mode (stream.plan_jobs): indexed BAMs, contigs cut into runs of sections of ~2.5 kb, each
+    decoded by a region query with a margin, planned alone (names reaching another job's range or
+    pileups are cross names), resolved in job order; the files are the reference's. Long reads
+    (long1, fuzz9001) are longer than the jobs."""
+    from pyoracle import OracleEngine
+    from genomeanonymizer_amd.anonymizer_methods import CompleteGermlineAnonymizer
+    monkeypatch.setenv("GANON_WHOLE_SAMPLE", "0")
+    monkeypatch.setenv("GANON_JOB_BP", "2500")
+    jobs = []
+    from genomeanonymizer_amd import stream
+    orig = stream.plan_jobs
+    monkeypatch.setattr(stream, "plan_jobs", lambda *a, **k: jobs.extend(orig(*a, **k)) or jobs)
+    bad = run_pipeline_vs_golden(name, str(tmp_path / name), CompleteGermlineAnonymizer(engine=OracleEngine()),
+                                 bam_index=True)
+    assert bad == {}
+    assert sum(j.region is not None for j in jobs) >= 2, jobs     # contigs were cut

@@ -366,3 +366,28 @@ def test_decoded_blobs_are_views_kept_alive(tmp_path):
     junk = [np.full(1 << 16, 0xAB, np.uint8) for _ in range(64)]   # reuse of freed memory would show
     assert np.array_equal(seq, ref[0]) and np.array_equal(qual, ref[1]) and np.array_equal(names, ref[2])
     del junk
+
+
+def test_region_reader_matches_fetch(tmp_path):
+    """ganon_bam_reader_region (BAI linear index, htslib overlap semantics, placed unmapped records
+    at [pos, pos + 1)) against the whole-file table's fetch on random regions of a multi-window BAM."""
+    from genomeanonymizer_amd.io.bam import BamReader, ReadTable
+    from genomeanonymizer_amd.synth.fastpair import make_pair
+    d = str(tmp_path / "in")
+    make_pair(d, n_contigs=2, contig_len=400_000, pairs_per_contig=20_000, window_every=20_000)
+    rng = np.random.default_rng(3)
+    for key in ("tumor", "normal"):
+        path = os.path.join(d, f"{key}.bam")
+        full = ReadTable(path)
+        rd = BamReader(path, 4)
+        assert rd.has_index
+        for tid, (name, L) in enumerate(zip(full.ref_names, full.ref_lens)):
+            for _ in range(20):
+                a = int(rng.integers(0, L))
+                b = int(min(L, a + rng.integers(0, 60_000)))
+                exp = full.fetch(name, a, b)
+                got = rd.region(tid, a, b)
+                assert got.n == len(exp)
+                assert np.array_equal(np.asarray(got.pos), np.asarray(full.pos)[exp])
+                assert np.array_equal(np.asarray(got.flag), np.asarray(full.flag)[exp])
+        rd.close()

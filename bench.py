@@ -362,6 +362,29 @@ def e2e_lines(args) -> dict:
                         f"the GPU (contigs sharded as over ranks, 16 / {args.e2e_workers} decode threads each), "
                         f"files written to local disk",
             "generate_s": round(gen_s, 1), "error": hip.get("error") or one.get("error")}
+        # chromosome-scale contigs: 2 x 40 Mb, ~10 M reads (configs[1]'s read count), the contigs cut
+        # into runs of sections (job mode) over the same processes
+        if args.e2e_chrom_pairs > 0:
+            t = time.perf_counter()
+            cin = os.path.join(d, "chrom_in")
+            make_pair(cin, n_contigs=2, contig_len=40_000_000, pairs_per_contig=args.e2e_chrom_pairs,
+                      window_every=20_000, seed=9)
+            cgen = time.perf_counter() - t
+            ch = _child_json([sys.executable, tool, cin, os.path.join(d, "chrom_out"), "stream"],
+                             {"E2E_RUNS": "1", "E2E_WORKERS": str(args.e2e_workers)}, 900)
+            cs = ch.get("stream", {})
+            res["e2e"]["chromosome_scale"] = {
+                "value": cs.get("reads_per_s"), "unit": "reads/s", "bases_per_sec": cs.get("bases_per_s"),
+                "reads": cs.get("reads"), "workers": args.e2e_workers, "wall_s": cs.get("stages_s", {}).get("wall_s"),
+                "stages_s_rank0": cs.get("stages_s"), "peak_rss_mb_rank0": cs.get("peak_rss_mb"),
+                "output_bytes": cs.get("output_bytes"), "jobs": cs.get("jobs"), "generate_s": round(cgen, 1),
+                "workload": f"synth/fastpair.py: 2 contigs x 40 Mb, {args.e2e_chrom_pairs} pairs per contig and sample "
+                            f"(150 bp, FR), germline SNPs/deletions as above, a window every 20 kb; contigs cut into "
+                            f"runs of sections of GANON_JOB_BP (default 4 Mb) read by BAI region queries, sharded over "
+                            f"{args.e2e_workers} processes sharing the GPU",
+                "error": ch.get("error")}
+            shutil.rmtree(cin, ignore_errors=True)
+            shutil.rmtree(os.path.join(d, "chrom_out"), ignore_errors=True)
         # the CPU path on a bounded sample (the first contigs)
         cpu_in = os.path.join(d, "cpu_in")
         make_pair(cpu_in, n_contigs=args.e2e_cpu_contigs, pairs_per_contig=args.e2e_pairs, seed=8)
@@ -444,6 +467,8 @@ def main() -> None:
     ap.add_argument("--e2e-pairs", type=int, default=23_000, help="pairs per contig and sample")
     ap.add_argument("--e2e-cpu-contigs", type=int, default=4)
     ap.add_argument("--e2e-runs", type=int, default=2, help="timed end-to-end runs after a warm run")
+    ap.add_argument("--e2e-chrom-pairs", type=int, default=1_250_000,
+                    help="pairs per contig and sample of the chromosome-scale end-to-end line (2 x 40 Mb; 0: skip)")
     ap.add_argument("--e2e-workers", type=int, default=8,
                     help="processes sharing the GPU in the end-to-end line (the multi-rank path over gloo)")
     ap.add_argument("--resident", action="store_true",

@@ -24,6 +24,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <deque>
 #include <string>
 #include <string_view>
 #include <unordered_map>
@@ -79,6 +80,134 @@ struct PairSlot {
   uint64_t seq = 0;   // insertion order (dict order: a deleted key re-inserted goes last)
 };
 
+// Read names -> dense ids: an open-addressing table of ids keyed by a 64-bit hash of the name bytes,
+// the name compared on a hash hit (no per-name allocation: the planner meets every record's name).
+class NameTable {
+ public:
+  void reserve(size_t n) {
+    size_t cap = 64;
+    while (cap < 2 * n + 2) cap <<= 1;
+    slot_.assign(cap, Entry{0, -1});
+    mask_ = cap - 1;
+    str_.clear();
+    str_.reserve(n);
+  }
+  size_t size() const { return str_.size(); }
+  static uint64_t hash_of(std::string_view s) {
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ (uint64_t)s.size();
+    const char *p = s.data();
+    size_t n = s.size();
+    while (n >= 8) {
+      uint64_t v;
+      std::memcpy(&v, p, 8);
+      h = mix(h ^ v) + 0x632BE59BD9B4E019ull;
+      p += 8;
+      n -= 8;
+    }
+    uint64_t v = 0;
+    std::memcpy(&v, p, n);
+    return mix(h ^ v ^ ((uint64_t)n << 59));
+  }
+  void prefetch(uint64_t h) const { __builtin_prefetch(&slot_[(size_t)h & mask_]); }
+  // the id of the name (hash h), inserted when new (*added set)
+  int64_t get(std::string_view nm, uint64_t h, bool *added) {
+    for (size_t i = (size_t)h & mask_;; i = (i + 1) & mask_) {
+      Entry &e = slot_[i];
+      if (e.id < 0) {
+        if (2 * (str_.size() + 1) > slot_.size()) {   // (reserve() sizes for every record: rare)
+          grow();
+          return get(nm, h, added);
+        }
+        e.hash = h;
+        e.id = (int64_t)str_.size();
+        str_.push_back(nm);
+        *added = true;
+        return e.id;
+      }
+      if (e.hash == h && str_[(size_t)e.id] == nm) {
+        *added = false;
+        return e.id;
+      }
+    }
+  }
+  int64_t find(std::string_view nm) const {
+    if (slot_.empty()) return -1;
+    const uint64_t h = hash_of(nm);
+    for (size_t i = (size_t)h & mask_;; i = (i + 1) & mask_) {
+      const Entry &e = slot_[i];
+      if (e.id < 0) return -1;
+      if (e.hash == h && str_[(size_t)e.id] == nm) return e.id;
+    }
+  }
+
+ private:
+  struct Entry {
+    uint64_t hash;
+    int64_t id;   // -1: empty
+  };
+  static uint64_t mix(uint64_t x) {
+    x ^= x >> 32;
+    x *= 0xD6E8FEB86659FD93ull;
+    x ^= x >> 32;
+    return x;
+  }
+  void grow() {
+    std::vector<Entry> old;
+    old.swap(slot_);
+    slot_.assign(old.size() * 2, Entry{0, -1});
+    mask_ = slot_.size() - 1;
+    for (const Entry &e : old)
+      if (e.id >= 0)
+        for (size_t i = (size_t)e.hash & mask_;; i = (i + 1) & mask_)
+          if (slot_[i].id < 0) {
+            slot_[i] = e;
+            break;
+          }
+  }
+  std::vector<Entry> slot_;
+  std::vector<std::string_view> str_;
+  size_t mask_ = 0;
+};
+
+// to_pair_anonymized_reads keyed by dense name id: the entry of a name (-1 none) in a pool in
+// insertion order (an erased entry stays dead in the pool; a name stored again gets a new one).
+class PairTable {
+ public:
+  void resize(size_t n) { at_.assign(n, -1); }
+  PairSlot *find(int64_t name) {
+    const int64_t i = at_[(size_t)name];
+    return i < 0 ? nullptr : &pool_[(size_t)i];
+  }
+  bool count(int64_t name) const { return at_[(size_t)name] >= 0; }
+  PairSlot &emplace(int64_t name) {
+    at_[(size_t)name] = (int64_t)pool_.size();
+    pool_.emplace_back();
+    names_.push_back(name);
+    ++live_;
+    return pool_.back();
+  }
+  void erase(int64_t name) {
+    const int64_t i = at_[(size_t)name];
+    if (i < 0) return;
+    names_[(size_t)i] = -1;
+    at_[(size_t)name] = -1;
+    --live_;
+  }
+  bool empty() const { return live_ == 0; }
+  size_t size() const { return live_; }
+  template <class F>
+  void for_each(F &&f) const {
+    for (size_t i = 0; i < pool_.size(); ++i)
+      if (names_[i] >= 0) f(names_[i], pool_[i]);
+  }
+
+ private:
+  std::vector<int64_t> at_;
+  std::deque<PairSlot> pool_;   // (stable references across insertions)
+  std::deque<int64_t> names_;   // name of each pool entry, -1 erased
+  size_t live_ = 0;
+};
+
 struct ScopeRec {
   int32_t contig, window;
   int64_t first, last, span_start, span_end;
@@ -115,10 +244,11 @@ class Planner {
       return;
     }
     if (!to_pair_.empty()) pair_unmapped_mates();
-    for (int64_t k : written_) to_pair_.erase(k);
+    for (size_t k = 0; k < written_.size(); ++k)
+      if (written_[k]) to_pair_.erase((int64_t)k);
     std::vector<std::pair<uint64_t, const PairSlot *>> rest;
     rest.reserve(to_pair_.size());
-    for (const auto &kv : to_pair_) rest.emplace_back(kv.second.seq, &kv.second);
+    to_pair_.for_each([&](int64_t, const PairSlot &p) { rest.emplace_back(p.seq, &p); });
     std::sort(rest.begin(), rest.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
     for (const auto &e : rest) {
       const int sl = e.second->has[0] ? 0 : 1;
@@ -154,7 +284,8 @@ class Planner {
   const ganon_plan_input *in_;
   Table tab_[2];
   std::vector<int64_t> nid_[2];       // name id per row
-  std::unordered_map<int64_t, PairSlot> to_pair_;
+  NameTable names_;
+  PairTable to_pair_;
   uint64_t pair_seq_ = 0;             // clock: to_pair insertions and placeholder events
   bool cmode_ = false;
   bool jmode_ = false;                // job mode: sections [sec_lo, sec_hi) of the contig
@@ -163,7 +294,8 @@ class Planner {
   std::vector<uint8_t> cross_;        // per name id (contig mode)
   std::vector<uint8_t> cx_;           // per name id: complex (SA tag / secondary / supplementary record)
   std::vector<uint8_t> slot_seen_;    // per name id: mate slots of its plain records (contig mode)
-  std::unordered_set<int64_t> written_;
+  std::vector<uint8_t> written_;      // per name id: written_read_ids
+  std::vector<int32_t> where_;        // per name id: scratch of yield_sequence (-1)
   int32_t next_hid_ = 0;
 
   std::string contig_name(int32_t c) const {
@@ -187,23 +319,28 @@ class Planner {
         }
       }
     }
-    std::unordered_map<std::string_view, int64_t> ids;
+    NameTable &ids = names_;
     ids.reserve((size_t)(in_->tables[0].n + in_->tables[1].n));
     int64_t tumor_ids = 0;
     for (int d = 0; d < 2; ++d) {
       const ganon_plan_table &t = in_->tables[d];
       nid_[d].resize((size_t)t.n);
       int64_t shared = 0;
-      for (int64_t r = 0; r < t.n; ++r) {
-        std::string_view nm(t.names + t.name_off[r], (size_t)t.name_len[r]);
-        auto it = ids.find(nm);
-        if (it == ids.end()) {
-          const int64_t id = (int64_t)ids.size();
-          ids.emplace(nm, id);
+      // hashes of a run of records first, their table lines prefetched, then the lookups
+      constexpr int64_t kRun = 32;
+      uint64_t hs[kRun];
+      for (int64_t r0 = 0; r0 < t.n; r0 += kRun) {
+        const int64_t n = std::min<int64_t>(kRun, t.n - r0);
+        for (int64_t k = 0; k < n; ++k) {
+          hs[k] = NameTable::hash_of(std::string_view(t.names + t.name_off[r0 + k], (size_t)t.name_len[r0 + k]));
+          ids.prefetch(hs[k]);
+        }
+        for (int64_t k = 0; k < n; ++k) {
+          const int64_t r = r0 + k;
+          bool added;
+          const int64_t id = ids.get(std::string_view(t.names + t.name_off[r], (size_t)t.name_len[r]), hs[k], &added);
           nid_[d][r] = id;
-        } else {
-          nid_[d][r] = it->second;
-          if (d == 1 && it->second < tumor_ids) ++shared;
+          if (!added && d == 1 && id < tumor_ids) ++shared;
         }
       }
       if (cmode_) {
@@ -240,7 +377,12 @@ class Planner {
                                             "streaming (contig) path only (record '" + tab_[d].name(r) + "')");
       }
       if (d == 0) tumor_ids = (int64_t)ids.size();
-      else if (shared) {
+      else {
+        to_pair_.resize(ids.size());
+        written_.assign(ids.size(), 0);
+        where_.assign(ids.size(), -1);
+      }
+      if (d == 1 && shared) {
         // count distinct shared names like the Python set intersection
         std::unordered_set<int64_t> s;
         for (int64_t r = 0; r < t.n; ++r)
@@ -252,10 +394,10 @@ class Planner {
     }
   }
 
-  void force_cross(const std::unordered_map<std::string_view, int64_t> &ids) {
+  void force_cross(const NameTable &ids) {
     for (int64_t k = 0; k < in_->n_force; ++k) {
-      auto it = ids.find(std::string_view(in_->force_names + in_->force_off[k], (size_t)in_->force_len[k]));
-      if (it != ids.end()) cross_[(size_t)it->second] = 1;
+      const int64_t id = ids.find(std::string_view(in_->force_names + in_->force_off[k], (size_t)in_->force_len[k]));
+      if (id >= 0) cross_[(size_t)id] = 1;
     }
   }
 
@@ -417,7 +559,8 @@ class Planner {
 
   void write_pair(const Inst &i0, const Inst &i1, int32_t hid, bool r0 = false, bool r1 = false) {
     const int64_t name = nid_[i0.ds][(size_t)i0.row];
-    if (!written_.insert(name).second) return;
+    if (written_[(size_t)name]) return;
+    written_[(size_t)name] = 1;
     log_write(hid, i0.ds, 0, i0, r0);
     log_write(hid, i0.ds, 1, i1, r1);
   }
@@ -427,12 +570,12 @@ class Planner {
   PairSlot &store_first(const Inst &inst, bool update = false) {
     const int64_t name = nid_[inst.ds][(size_t)inst.row];
     const int sl = slot(inst.ds, inst.row);
-    auto it = to_pair_.find(name);
-    if (it == to_pair_.end()) {
-      it = to_pair_.emplace(name, PairSlot{}).first;
-      it->second.seq = pair_seq_++;
+    PairSlot *pp = to_pair_.find(name);
+    if (!pp) {
+      pp = &to_pair_.emplace(name);
+      pp->seq = pair_seq_++;
     }
-    PairSlot &p = it->second;
+    PairSlot &p = *pp;
     if (!p.has[sl]) {
       p.p[sl] = inst;
       p.has[sl] = true;
@@ -575,22 +718,22 @@ class Planner {
     eps.clear();
     order.clear();
     std::vector<int64_t> pair_rank;
-    std::unordered_map<int64_t, int32_t> where;
-    std::unordered_map<int64_t, int32_t> cx_where;
+    std::vector<int32_t> &where = where_;   // per name: its pair / complex registrations (-1), reset below
+    std::vector<int64_t> cx_names;
     std::vector<std::vector<int32_t>> cx_regs;
-    where.reserve(reg.size());
     for (int32_t gi = 0; gi < (int32_t)reg.size(); ++gi) {
       const Reg &g = reg[(size_t)gi];
       const int64_t name = nid_[g.ds][(size_t)g.row];
       const int sl = slot(g.ds, g.row);
       if (cx(g.ds, g.row)) {
-        auto it = cx_where.find(name);
-        if (it == cx_where.end()) {
-          cx_where.emplace(name, (int32_t)cx_regs.size());
+        const int32_t wi = where[(size_t)name];
+        if (wi < 0) {
+          where[(size_t)name] = (int32_t)cx_regs.size();
+          cx_names.push_back(name);
           cx_regs.emplace_back();
           cx_regs.back().push_back(gi);
         } else {
-          std::vector<int32_t> &v = cx_regs[(size_t)it->second];
+          std::vector<int32_t> &v = cx_regs[(size_t)wi];
           // seen_read_alns: only a read's first alignment in the scope contributes indels
           bool seen = false;
           for (int32_t x : v) seen = seen || slot(reg[(size_t)x].ds, reg[(size_t)x].row) == sl;
@@ -600,15 +743,15 @@ class Planner {
         continue;
       }
       const int64_t e = in_->tables[g.ds].end[g.row];
-      auto it = where.find(name);
+      const int32_t wi = where[(size_t)name];
       YPair *p;
-      if (it == where.end()) {
-        where.emplace(name, (int32_t)pairs.size());
+      if (wi < 0) {
+        where[(size_t)name] = (int32_t)pairs.size();
         pairs.push_back(YPair{name, {}, {false, false}, e});
         pair_rank.push_back(gi);
         p = &pairs.back();
       } else {
-        p = &pairs[(size_t)it->second];
+        p = &pairs[(size_t)wi];
         p->max_end = std::max(p->max_end, e);
       }
       if (p->has[sl])
@@ -617,6 +760,8 @@ class Planner {
       p->p[sl] = Inst{g.ds, sid, g.row};
       p->has[sl] = true;
     }
+    for (const YPair &p : pairs) where[(size_t)p.name] = -1;   // (a name is plain or complex in every scope)
+    for (int64_t nm : cx_names) where[(size_t)nm] = -1;
     std::vector<YItem> items;
     for (int32_t k = 0; k < (int32_t)pairs.size(); ++k) {
       const YPair &p = pairs[(size_t)k];
@@ -723,13 +868,12 @@ class Planner {
         placeholder(4, hid, p.has[0] ? 0 : 1, inst);
         continue;
       }
-      store_first(inst, true);
+      PairSlot &ps = store_first(inst, true);
       const int64_t name = nid_[inst.ds][(size_t)inst.row];
-      auto it = to_pair_.find(name);
-      if (it->second.has[0] && it->second.has[1]) {
-        const Inst a = it->second.p[0], b = it->second.p[1];
-        write_pair(a, b, hid, it->second.upd[0], it->second.upd[1]);
-        to_pair_.erase(it);
+      if (ps.has[0] && ps.has[1]) {
+        const Inst a = ps.p[0], b = ps.p[1];
+        write_pair(a, b, hid, ps.upd[0], ps.upd[1]);
+        to_pair_.erase(name);
       }
     }
     close_handle(hid);
@@ -867,12 +1011,12 @@ class Planner {
   // ---- contig mode: what the sample-wide resolution needs from this contig ----
   void export_contig() {
     std::vector<std::pair<uint64_t, const PairSlot *>> rest;
-    std::unordered_set<int64_t> pending;
-    for (const auto &kv : to_pair_) {
-      if (written_.count(kv.first)) continue;   // dropped at the sample's end anyway
-      rest.emplace_back(kv.second.seq, &kv.second);
-      pending.insert(kv.first);
-    }
+    std::vector<uint8_t> pending(written_.size(), 0);
+    to_pair_.for_each([&](int64_t name, const PairSlot &p) {
+      if (written_[(size_t)name]) return;   // dropped at the sample's end anyway
+      rest.emplace_back(p.seq, &p);
+      pending[(size_t)name] = 1;
+    });
     std::sort(rest.begin(), rest.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
     for (const auto &e : rest) {
       const PairSlot &p = *e.second;
@@ -901,7 +1045,7 @@ class Planner {
         for (int64_t r : rows) {
           if (!tab_[ds].unmapped(r)) continue;
           const int64_t nm = nid_[ds][(size_t)r];
-          if (!cross_[(size_t)nm] && !pending.count(nm)) continue;
+          if (!cross_[(size_t)nm] && !pending[(size_t)nm]) continue;
           // the AnonymizedRead this record creates or updates at the end of the sample (AM:98-108)
           const int32_t nsa = n_sa(ds, r);
           const int64_t info = (supp_rec(ds, r) ? 1 : 0) | (nsa >= 0 ? 2 : 0) | ((int64_t)std::max(nsa, 0) << 8);

@@ -101,9 +101,13 @@ def run_short_read_tumor_normal_anonymizer(vcf_variants_per_sample: Sequence[str
                                            output_filenames: Sequence[Tuple[str, str]], record_statistics: bool,
                                            cpus: int = 1, enhance_parallelization: bool = False,
                                            dist=None) -> List[dict]:
-    """SR:889-967. Samples run one after another on the GPU (each is one device batch);
-    ``cpus`` sets the host decode threads. The reference's enhanced mode crashes whenever a
-    sample is split; here it is accepted and has no effect."""
+    """SR:889-967. Several pairs run concurrently like the reference's process pool (SR:944-961):
+    min(cpus, pairs) processes (GANON_PAIR_WORKERS overrides; 1 = in turn), each with its own HIP
+    context on the anonymizer's device, the host threads split as the reference splits
+    ``processes_by_sample``; a pair's own work (decode, plan, mask, format, files) is unchanged.
+    One pair, a distributed run or an anonymizer with a custom engine (tests) run in this process.
+    The reference's enhanced mode crashes whenever a sample is split; here it is
+    accepted and has no effect."""
     if enhance_parallelization:
         log.warning("--enhanced_multiprocessing has no effect in this build (the reference's mode is broken, "
                     "SURVEY Q12)")
@@ -112,8 +116,31 @@ def run_short_read_tumor_normal_anonymizer(vcf_variants_per_sample: Sequence[str
     inputs = []
     for vcf, samples, outs in zip(vcf_variants_per_sample, tumor_normal_samples, output_filenames):
         inputs.append((get_windows(read_vcf(vcf), ref_idx), samples, outs))
+    workers = int(os.environ.get("GANON_PAIR_WORKERS", str(min(max(1, int(cpus)), len(inputs)))))
+    if workers > 1 and len(inputs) > 1 and dist is None and getattr(anonymizer, "_engine", None) is None:
+        import multiprocessing as mp
+        from concurrent.futures import ProcessPoolExecutor
+        # (processes_by_sample, SR:945-946)
+        threads = 1 if cpus <= len(inputs) else max(1, int(cpus) // len(inputs))
+        # spawned: a forked child of a process that touched the GPU cannot use it
+        with ProcessPoolExecutor(max_workers=min(workers, len(inputs)), mp_context=mp.get_context("spawn")) as ex:
+            futs = [ex.submit(_anonymize_pair, windows, t_bam, n_bam, ref_genome_file, anonymizer.device, t_out, n_out,
+                              record_statistics, threads)
+                    for windows, (t_bam, n_bam), (t_out, n_out) in inputs]
+            return [f.result() for f in futs]
     timings = []
     for windows, (t_bam, n_bam), (t_out, n_out) in inputs:
         timings.append(anonymize_genome(windows, t_bam, n_bam, ref_genome_file, anonymizer, t_out, n_out,
                                         record_statistics, max(1, int(cpus)), fasta=fasta, dist=dist))
     return timings
+
+
+def _anonymize_pair(windows, t_bam, n_bam, ref_genome_file, device, t_out, n_out, record_statistics, threads) -> dict:
+    """One pair in a pool process (its own HIP context on ``device``)."""
+    anon = CompleteGermlineAnonymizer(device=device)
+    try:
+        return anonymize_genome(windows, t_bam, n_bam, ref_genome_file, anon, t_out, n_out, record_statistics, threads)
+    finally:
+        eng = getattr(anon, "_engine", None)
+        if eng is not None and hasattr(eng, "close"):
+            eng.close()

@@ -318,6 +318,40 @@ def test_cli_matches_reference(tmp_path, hip_built):
     assert open(paths["N"] + ".statistics.txt").read() == open(os.path.join(GOLDEN, "edge", "normal.statistics.txt")).read()
 
 
+def test_cli_concurrent_pairs(tmp_path, hip_built):
+    """-s listing several pairs: they run concurrently, one process and HIP context each on the one
+    GPU (the reference's process pool, SR:944-961); every pair's files are the reference's."""
+    import gzip
+    import os
+    import shutil
+    import subprocess
+    import sys
+    from helpers import GOLDEN, REPO
+    from genomeanonymizer_amd.synth.generate import generate, scenario
+    d = str(tmp_path / "pairs")
+    paths = generate(scenario("edge"), os.path.join(d, "a"))
+    for sub in ("b", "c"):
+        os.makedirs(os.path.join(d, sub))
+        for f in ("tumor.bam", "normal.bam", "variants.vcf"):
+            shutil.copy(os.path.join(d, "a", f), os.path.join(d, sub, f))
+    with open(os.path.join(d, "samples.tsv"), "w") as fh:
+        fh.write("#tumor\tnormal\tvcf\n")
+        for sub in ("a", "b", "c"):
+            fh.write(f"{sub}/tumor.bam\t{sub}/normal.bam\t{sub}/variants.vcf\n")
+    env = dict(os.environ, PYTHONPATH=REPO, GANON_IO_BLOCK="4096")
+    r = subprocess.run([sys.executable, "-m", "genomeanonymizer_amd.genome_anonymizer", "-d", d, "-s", "samples.tsv",
+                        "-r", paths["ref"], "--record_statistics", "-c", "6"], env=env, capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    for sub in ("a", "b", "c"):
+        for tag in ("tumor", "normal"):
+            for suf in (".1.fastq", ".2.fastq", ".single_end.fastq"):
+                gp = os.path.join(GOLDEN, "edge", f"{tag}{suf}.gz")
+                assert open(os.path.join(d, sub, f"{tag}.anonymized{suf}"), "rb").read() == gzip.open(gp).read()
+        assert open(os.path.join(d, sub, "normal.bam.statistics.txt")).read() == \
+            open(os.path.join(GOLDEN, "edge", "normal.statistics.txt")).read()
+
+
 def test_hip_config2_matches_oracle(masker, oracle):
     """BASELINE configs[1] layout at 2 M reads: every byte and count equal to the oracle."""
     from genomeanonymizer_amd.synth.batch import config2_batch

@@ -118,9 +118,9 @@ def main():
                 import torch
                 w = torch.tensor([tim["wall_s"]], dtype=torch.float64)
                 dist.all_reduce(w, op=dist.ReduceOp.MAX)
-                rb = torch.tensor([tim["reads"], tim.get("bases", 0)], dtype=torch.int64)
+                rb = torch.tensor([tim["reads"], tim.get("bases", 0), tim.get("jobs", 0)], dtype=torch.int64)
                 dist.all_reduce(rb)
-                tim["wall_s"], tim["reads"], tim["bases"] = float(w[0]), int(rb[0]), int(rb[1])
+                tim["wall_s"], tim["reads"], tim["bases"], tim["jobs"] = float(w[0]), int(rb[0]), int(rb[1]), int(rb[2])
             if prof is not None:
                 import pstats
                 prof.disable()
@@ -132,7 +132,7 @@ def main():
         timed = runs[1:]
         best = min(timed, key=lambda t: t["wall_s"])
         bases = int(best.get("bases", 0))
-        res[mode] = {"reads": best["reads"], "bases": bases,
+        res[mode] = {"reads": best["reads"], "bases": bases, "jobs": best.get("jobs"),
                      "stages_s": {k: round(v, 3) for k, v in best.items() if k.endswith("_s")},
                      "reads_per_s": round(best["reads"] / best["wall_s"], 1),
                      "bases_per_s": round(bases / best["wall_s"], 1),

@@ -77,10 +77,13 @@ class Link:
         self.q_exp: "queue.Queue" = queue.Queue()
         self.q_res: "queue.Queue" = queue.Queue()
         self._inflight: list = []
+        self.sent_bytes = 0       # pickled payload bytes this rank sent / received over gloo
+        self.recv_bytes = 0
 
     def _send(self, obj, dst: int, tag: int) -> None:
         import torch
         payload = pickle.dumps(obj, protocol=pickle.HIGHEST_PROTOCOL)
+        self.sent_bytes += len(payload)
         n = torch.tensor([len(payload)], dtype=torch.int64)
         t = torch.frombuffer(bytearray(payload), dtype=torch.uint8)
         w1 = self.dist.isend(n, dst, group=self.group, tag=tag)
@@ -95,6 +98,7 @@ class Link:
         self.dist.recv(n, src, group=self.group, tag=tag)
         t = torch.empty(int(n.item()), dtype=torch.uint8)
         self.dist.recv(t, src, group=self.group, tag=tag)
+        self.recv_bytes += int(n.item())
         return pickle.loads(t.numpy().tobytes())
 
     # worker side

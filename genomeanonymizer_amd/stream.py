@@ -1170,6 +1170,8 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
             r.close()
         if coord is not None:
             coord.close()
+    timing["exchange_sent_bytes"] = link.sent_bytes
+    timing["exchange_recv_bytes"] = link.recv_bytes
     totals = comm.allreduce_totals(totals)
     timing["totals"] = {k: int(v) for k, v in zip(("masked_snv_calls", "masked_bases", "reads_in", "reads_written",
                                                    "scopes", "rare_scopes", "large_tiles", "reserved"), totals)}

@@ -391,3 +391,60 @@ def test_region_reader_matches_fetch(tmp_path):
                 assert np.array_equal(np.asarray(got.pos), np.asarray(full.pos)[exp])
                 assert np.array_equal(np.asarray(got.flag), np.asarray(full.flag)[exp])
         rd.close()
+
+
+def _rank_worker_timing(rank, world, port, paths, outdir, q):
+    """_rank_worker, reporting the rank's exchange bytes and rank 0's coordinator seconds."""
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [repo, os.path.join(repo, "oracle"), os.path.join(repo, "tests")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from pyoracle import OracleEngine
+        from genomeanonymizer_amd.anonymizer_methods import CompleteGermlineAnonymizer
+        from genomeanonymizer_amd import distributed
+        from genomeanonymizer_amd.io.fasta import FastaRef
+        from genomeanonymizer_amd.io.vcf import read_vcf
+        from genomeanonymizer_amd.planner import get_windows
+        windows = get_windows(read_vcf(paths["vcf"]), FastaRef(paths["ref"]).index)
+        distributed.anonymize_genome_sharded(windows, paths["T"], paths["N"], paths["ref"], os.path.join(outdir, "tumor"),
+                                             os.path.join(outdir, "normal"), True,
+                                             CompleteGermlineAnonymizer(engine=OracleEngine()), dist)
+        t = distributed.LAST_TIMING
+        q.put((rank, {k: t.get(k) for k in ("exchange_sent_bytes", "exchange_recv_bytes", "resolve_s", "jobs",
+                                             "reads", "wait_s")}))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_four_ranks_24_contigs_exchange(tmp_path):
+    """4 ranks over a 24-contig sample (cross-contig, unplaced and unmapped mates): the files equal one
+    rank's; every rank's exchange with rank 0's coordinator (pickled exports and resolutions over
+    gloo) and the coordinator's resolve time are reported."""
+    from test_distributed import _free_port
+    from genomeanonymizer_amd.synth.generate import generate
+    paths = generate(_scenario(41, n_contigs=24), str(tmp_path / "in"))
+    one = _run(paths, str(tmp_path / "one"), False)
+    stats_one = one.pop("stats")
+    os.remove(paths["N"] + ".statistics.txt")
+    out = str(tmp_path / "four")
+    os.makedirs(out)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_worker_timing, args=(r, 4, port, paths, out, q)) for r in range(4)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(300)
+    assert [p.exitcode for p in procs] == [0] * 4
+    rep = dict(q.get() for _ in range(4))
+    print("4-rank exchange:", rep)
+    assert sum(r["jobs"] for r in rep.values()) == 24
+    assert rep[0]["resolve_s"] is not None and rep[0]["exchange_recv_bytes"] > 0
+    assert all(rep[r]["exchange_sent_bytes"] > 0 for r in (1, 2, 3))
+    four = _outputs((os.path.join(out, "tumor"), os.path.join(out, "normal")), paths["N"] + ".statistics.txt")
+    assert four.pop("stats") == stats_one
+    assert four == one

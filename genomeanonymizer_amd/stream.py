@@ -65,14 +65,21 @@ def _names_ds(tables, ds: np.ndarray, rows: np.ndarray) -> List[bytes]:
 
 
 def _pwrite_all(fd: int, data, offset: int) -> None:
-    """os.pwrite until every byte is written (a single call may write fewer bytes)."""
-    mv = memoryview(data)
-    done = 0
-    while done < len(mv):
-        n = os.pwrite(fd, mv[done:], offset + done)
+    """Write ``data`` (a bytes-like object, or a list of them written back to back with pwritev, no
+    join) at ``offset`` until every byte is written (a single call may write fewer bytes)."""
+    parts = [memoryview(x).cast("B") for x in (data if isinstance(data, list) else [data])]
+    parts = [x for x in parts if len(x)]
+    while parts:
+        batch = parts[:512]   # (IOV_MAX is 1024)
+        n = os.pwritev(fd, batch, offset)
         if n <= 0:
-            raise OSError(f"pwrite wrote nothing at offset {offset + done}")
-        done += n
+            raise OSError(f"pwritev wrote nothing at offset {offset}")
+        offset += n
+        k = 0
+        while k < len(batch) and n >= len(batch[k]):
+            n -= len(batch[k])
+            k += 1
+        parts = ([batch[k][n:]] if k < len(batch) else []) + batch[k + 1:] + parts[len(batch):]
 
 
 @dataclasses.dataclass(frozen=True)
@@ -639,9 +646,9 @@ class Job(JobPrep):
 
     def output(self, out_n: np.ndarray, out_w: np.ndarray, ext_list: List[bytes], block: int) -> List[bytes]:
         """The job's bytes per output file (tumor .1, .2, normal .1, .2) with the resolved writes of
-        its placeholder events spliced into its I/O log; ``ext_list``: the bytes of the resolved writes
-        of records of other contigs (and objects of complex names), in event order (the
-        coordinator's ``resolve``)."""
+        its placeholder events spliced into its I/O log, each as a list of buffers written back to back
+        (no join); ``ext_list``: the bytes of the resolved writes of records of other contigs (and
+        objects of complex names), in event order (the coordinator's ``resolve``)."""
         ev, rows = self.events, self.event_rows
         n = len(ev)
         is_ph = ev[:, 0] >= 3
@@ -697,13 +704,14 @@ class Job(JobPrep):
         blob = self.fmt.format_arrays(fin[allr, 4], frow[allr], fin[allr, 5], reap[allr]) if len(allr) else b""
         cut = np.concatenate([[0], np.cumsum([int(rec_len[x].sum()) for x in les])])
         out = []
+        mv = memoryview(blob)
         for f in range(4):
             e = order[f]
             is_ext = ext[e]
             le = les[f]
-            data = blob[cut[f]:cut[f + 1]]
+            data = mv[cut[f]:cut[f + 1]]
             if not np.any(is_ext):
-                out.append(data)
+                out.append([data])
                 continue
             off = np.concatenate([[0], np.cumsum(rec_len[le])])
             parts, prev_local = [], 0
@@ -715,7 +723,7 @@ class Job(JobPrep):
                 parts.append(ext_bytes[ei])
                 prev_local = n_local_before
             parts.append(data[offl[prev_local]:])
-            out.append(b"".join(parts))
+            out.append(parts)
         return out
 
     def stats(self) -> Dict[str, List[int]]:
@@ -1065,11 +1073,13 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
             t1 = time.time()
             data = job.output(res["out_n"], res["out_w"], res["ext"], block_size)
             for f in range(4):
-                if len(data[f]) != res["sizes"][f]:
-                    raise RuntimeError(f"job {job.job}: {len(data[f])} bytes for file {f}, {res['sizes'][f]} planned")
+                nb = sum(len(x) for x in data[f])
+                if nb != res["sizes"][f]:
+                    raise RuntimeError(f"job {job.job}: {nb} bytes for file {f}, {res['sizes'][f]} planned")
             # the four files written concurrently (pwrite drops the GIL; a file system serialises
             # buffered writes per file, not across files)
-            futs = [file_pool.submit(_pwrite_all, fds[f], data[f], res["offsets"][f]) for f in range(4) if data[f]]
+            futs = [file_pool.submit(_pwrite_all, fds[f], data[f], res["offsets"][f]) for f in range(4)
+                    if any(len(x) for x in data[f])]
             for fu in futs:
                 fu.result()
             stats_rows.append((job.job, job.stats()))

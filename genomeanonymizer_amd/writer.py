@@ -65,9 +65,9 @@ class FastqFormatter:
         ds = np.asarray(ds, np.int64)
         row = np.asarray(row, np.int64)
         sc = np.asarray(sc, np.int64)
-        t0, t1 = ds == 0, ds == 1
-        r0, r1 = np.where(t0, row, 0), np.where(t1, row, 0)
-        pick = lambda f, dt: np.where(t0, getattr(T, f)[r0], getattr(N, f)[r1]).astype(dt)
+        t0 = ds == 0
+        g = row + ds * T.n          # row in the concatenated tumor + normal columns
+        pick = lambda f, dt: self._column(f, dt)[g]
         seq_sel = np.where(sc >= 0, 0, 1 + ds).astype(np.uint8)
         seq_off_t = pick("seq_off", np.int64)
         base = np.where(t0, self.res.seq_base[0], self.res.seq_base[1])
@@ -90,6 +90,16 @@ class FastqFormatter:
             "names": self._names, "name_len": pick("name_len", np.int32), "name_off": name_off,
             "mate": np.where(flag & 0x40, 1, 2).astype(np.uint8),
         }
+
+    def _column(self, f: str, dt) -> np.ndarray:
+        """Column f of the tumor then the normal table, as dt (made once per job)."""
+        cols = self.__dict__.setdefault("_cols", {})
+        c = cols.get(f)
+        if c is None:
+            T, N = self.tables
+            c = np.concatenate([np.asarray(getattr(T, f)), np.asarray(getattr(N, f))]).astype(dt, copy=False)
+            cols[f] = c
+        return c
 
     def _dup_index(self):
         """Sorted instance keys of the further masked copies and their byte offsets in seq_out."""

@@ -461,6 +461,8 @@ def main() -> None:
                     "(no host synchronization inside the step), 0 the replan waits for the scan")
     ap.add_argument("--prep-unroll", type=int, default=0, help="GANON_PARAM_PREP_UNROLL: incidences per thread "
                     "and trip of the one-segment emit (0 auto, 1, 2, 4)")
+    ap.add_argument("--fused-flat", type=int, default=1, help="GANON_PARAM_FUSED_FLAT: 1 the group kernel makes "
+                    "the one-segment records from the scan's read descriptors, 0 the record pass")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (BAM -> FASTQ) line")
     ap.add_argument("--no-side-configs", action="store_true", help="skip the c3 / c5 lines (child runs)")
     ap.add_argument("--e2e-contigs", type=int, default=24)
@@ -521,7 +523,8 @@ def main() -> None:
     for si in range(args.pipeline):
         m = native.HipMasker(dev)
         for prm, val in ((native.PARAM_GROUP_UNROLL, args.unroll), (native.PARAM_INDEL_SORT, args.indel_sort),
-                         (native.PARAM_PREP_UNROLL, args.prep_unroll), (native.PARAM_SPEC_PLAN, args.spec_plan)):
+                         (native.PARAM_PREP_UNROLL, args.prep_unroll), (native.PARAM_SPEC_PLAN, args.spec_plan),
+                         (native.PARAM_FUSED_FLAT, args.fused_flat)):
             m.set_param(prm, val)
         if args.target:
             m.set_param(native.PARAM_GROUP_TARGET, args.target)

@@ -43,6 +43,15 @@ constexpr uint32_t kSegMine = 1u << 31;     // the segment's read is written by 
 //   [2] {piece A begin lo, hi, end lo, hi}       [3] {overflow region lo, hi, capacity, 0}
 //   [4] {piece B begin lo, hi, end lo, hi}
 // segments [seg_begin, seg_mid) have an all-ACGT reference range (2-bit reference).
+// read descriptor (int4, 16 bytes; k_prep_scan writes one per read of at most kScanLongCigar CIGAR
+// ops that passed its checks): everything the fused one-segment group kernel gathers per incidence.
+//   x = query nibble of the read's first aligned segment, bits 0-31 (2 seq_off + q),
+//   y = its contig position p (ref_start when the read has no segment),
+//   z = query nibble bits 32-39 | length << 8 (14 bits; 0: no segment) | dataset << 22 | wide << 23 |
+//       (p - ref_start) << 24 (4 bits) | (read_end - p - length) << 28 (4 bits),
+//   w = write scope.
+// wide: one of the two deltas did not fit (the span check then reads ref_start and read_end).
+constexpr uint32_t kDescWide = 1u << 23;
 
 // Device view of a batch (all pointers device-resident).
 struct DevBatch {
@@ -67,6 +76,15 @@ struct Tile {
   int64_t hi;
 };
 
+// First error the device validation found: per-read and per-scope checks at plan time, incidence
+// and write-scope checks during the run (reported by ganon_batch_download).
+struct PrepErr {
+  int code;         // 0 none, else a PrepErrKind
+  int pad;
+  long long index;  // read / scope / incidence
+  long long a, b;
+};
+
 // Rarely used outputs and scratch of the group kernels, read through one pointer (device
 // memory) so that their addresses do not occupy scalar registers for the whole kernel.
 struct GrpAux {
@@ -77,15 +95,15 @@ struct GrpAux {
   unsigned long long *paths;                    // [0] sorted lists, [1] region passes, [2] key-range splits
   unsigned long long *okey, *opay, *tkey;       // overflow regions
   unsigned int *tflag;
-};
-
-// First error the device validation found: per-read and per-scope checks at plan time, incidence
-// and write-scope checks during the run (reported by ganon_batch_download).
-struct PrepErr {
-  int code;         // 0 none, else a PrepErrKind
-  int pad;
-  long long index;  // read / scope / incidence
-  long long a, b;
+  // fused one-segment mode: the group kernel makes its segment records from the incidences and the
+  // read descriptors itself (incidence checks, write-scope hash sums per group)
+  const int32_t *incid_read, *ref_start, *read_end;
+  const int4 *desc;
+  const int64_t *incid_off, *ref_off;
+  const uint8_t *sdirty;                        // per scope: its reference span holds a non-ACGT block
+  int32_t n_reads, pad_;
+  PrepErr *err;
+  unsigned long long *ws_part;
 };
 enum PrepErrKind {
   kErrReadSeq = 1, kErrReadCigar, kErrReadDataset, kErrReadWriteScope, kErrReadLong, kErrCigarOp, kErrReadPos,
@@ -219,6 +237,13 @@ struct ganon_dbatch {
   // per scope (scost, upload) instead of the CSR offsets, and emitted one wave per incidence
   bool long_mode = false;
   bool flat_mode = false;   // every read has at most one aligned segment: one record per incidence, in place
+  // fused one-segment mode (GANON_PARAM_FUSED_FLAT, default on): no record pass — the scan writes a
+  // descriptor per read (b_desc) and the partition candidates (b_cand: per group and dataset, the
+  // complement of the lowest buffer offset written, atomicMax), the group kernel makes each
+  // incidence's record in LDS. Off for batches with long-CIGAR reads (the scan does not describe them).
+  bool fused = false;
+  ganon_dev::DBuf b_desc, b_cand, b_sdirty;
+  unsigned long long *cand = nullptr;   // the scan's candidates of this plan (null: the emit marks them)
   int64_t *scost = nullptr;
   int64_t n_seg = 0, region = 0, far_cap = 0, n_written = 0, region_per_incid = 0, n_id_ops = 0;
   int64_t max_len = 0, max_seg = 0;         // longest read, most aligned segments of one read (plan)

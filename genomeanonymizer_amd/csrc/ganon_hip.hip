@@ -349,6 +349,8 @@ struct GrpSharedT {
   int blk_calls, blk_bases;         // this workgroup's contribution to the totals
   int cnt_calls[kGrpMaxScopes];     // per-scope counts, written out once at the end
   int cnt_bases[kGrpMaxScopes];
+  int wdirty[kGrpThreads / 64];     // fused one-segment mode: a wave's records need the nt16 reference
+  unsigned long long hsum;          // ... and the write-scope hash sum of the group's mine incidences
 };
 
 struct GrpRange {
@@ -496,17 +498,11 @@ __device__ __forceinline__ void copy_windows(const uint8_t *__restrict__ src, ui
   }
 }
 
-// Stage records [c0, c0 + nh) in LDS with the exclusive prefix of their chunk counts;
-// returns the tile's chunk total.
+// The staged tile's chunk map: the exclusive prefix of the records' chunk counts (nck: this
+// thread's record) and the chunk -> record map; returns the tile's chunk total.
 template <class SH>
-__device__ __forceinline__ int grp_tile(SH &sh, const int4 *__restrict__ rec4, int64_t c0, int nh, int chunk) {
+__device__ __forceinline__ int grp_tile_map(SH &sh, int nck) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int4 r = rec4[c0 + (tid < nh ? tid : nh - 1)];
-  int nck = 0;
-  if (tid < nh) {
-    sh.rec[tid] = r;
-    nck = ((((uint32_t)r.z >> 16) & kSegMaxLen) + chunk - 1) / chunk;
-  }
   // wave inclusive scan: DPP row_shr within each 16-lane row, then the row totals (no lane-index
   // registers: shuffle index arithmetic hoisted out of the tile loop cost 9 VGPRs and spills)
   int incl = nck;
@@ -534,6 +530,135 @@ __device__ __forceinline__ int grp_tile(SH &sh, const int4 *__restrict__ rec4, i
   if (total <= kGrpMap)
     for (int k = 0; k < nck; ++k) sh.cmap[pre + k] = (uint8_t)tid;
   __syncthreads();
+  return total;
+}
+
+// Stage records [c0, c0 + nh) in LDS with the exclusive prefix of their chunk counts;
+// returns the tile's chunk total.
+template <class SH>
+__device__ __forceinline__ int grp_tile(SH &sh, const int4 *__restrict__ rec4, int64_t c0, int nh, int chunk) {
+  const int tid = threadIdx.x;
+  const int4 r = rec4[c0 + (tid < nh ? tid : nh - 1)];
+  int nck = 0;
+  if (tid < nh) {
+    sh.rec[tid] = r;
+    nck = ((((uint32_t)r.z >> 16) & kSegMaxLen) + chunk - 1) / chunk;
+  }
+  return grp_tile_map(sh, nck);
+}
+
+// ---- fused one-segment mode: records made in LDS ------------------------------------------
+// A one-segment batch (every read at most one aligned segment) needs no record pass over HBM:
+// k_prep_scan wrote a 16-byte descriptor per read (its segment's query nibble, contig position and
+// length, dataset, write scope, ganon_batch.h), and each tile here turns incidences [c0, c0 + nh)
+// into the records k_prep_emit_flat used to write — scope by binary search in the staged scope
+// table, the span check, the write-scope mark (and, on the group's first pass, the incidence checks
+// and the write-scope hash sum). The group's scopes sit in the patch list's LDS (unused while chunks
+// stream; staged again before every pass, the classification reuses it), 16 bytes each. A tile reads
+// the 2-bit reference unless one of its records lies in a scope whose reference span holds a
+// non-ACGT block (the record pass decided this per group; both copies give the same bases where
+// the 2-bit one is read).
+struct FlatScope {
+  int off;                  // first incidence, relative to the group's
+  int sstart;               // span start
+  unsigned long long pk;    // ref_off - span_start (42-bit signed) | min(span_len, 2^20 + 1) << 42 | dirty << 63
+};
+static_assert(sizeof(FlatScope) * kGrpMaxScopes <= sizeof(unsigned long long) * kGrpObs,
+              "the scope table fits the patch list");
+
+template <class SH>
+__device__ __forceinline__ FlatScope *flat_scopes(SH &sh) {
+  return reinterpret_cast<FlatScope *>(sh.patch);
+}
+
+// Scope s of a group whose incidences start at i_begin (a thread per scope: at most kGrpMaxScopes,
+// the group's workgroup size).
+static_assert(kGrpMaxScopes <= kGrpThreads, "one staging thread per scope of a group");
+__device__ __forceinline__ FlatScope flat_load(const GrpBatch &B, const GrpAux *__restrict__ aux, int s, int64_t i_begin) {
+  const int64_t off = aux->incid_off[s], ro = aux->ref_off[s];
+  const int ss = B.span_start[s], sl = B.span_len[s];
+  const bool dirty = aux->sdirty[s] != 0;   // (k_prep_scan)
+  FlatScope f;
+  f.off = (int)(off - i_begin);
+  f.sstart = ss;
+  f.pk = ((unsigned long long)(ro - ss) & ((1ull << 42) - 1)) | ((unsigned long long)min(sl, kGrpMaxSpan + 1) << 42) |
+         ((unsigned long long)dirty << 63);
+  return f;
+}
+
+// r: incidence c0 + tid's read (loaded a tile ahead by grp_scan_flat).
+template <class SH>
+__device__ __forceinline__ int grp_tile_flat(SH &sh, const GrpBatch &B, const GrpAux *__restrict__ aux, int64_t c0,
+                                             int nh, int chunk, int s_begin, int ns, int64_t i_begin, bool first,
+                                             int r, bool &clean) {
+  const int tid = threadIdx.x;
+  const FlatScope *sc = flat_scopes(sh);
+  int nck = 0;
+  bool dirty = false;
+  unsigned long long hsum = 0;
+  if (tid < nh) {
+    const int64_t i = c0 + tid;
+    const int il = (int)(i - i_begin);
+    int lo = 0, hi = ns - 1;   // the incidence's scope: largest j with off[j] <= il
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (sc[mid].off <= il) lo = mid;
+      else hi = mid - 1;
+    }
+    const int j = lo;
+    int4 rec = make_int4(0, 0, 0, j);   // zero length: no chunks
+    if (r < 0 || r >= aux->n_reads) {
+      if (first) report(aux->err, kErrIncidRead, i, r);
+    } else {
+      const int4 d = aux->desc[r];
+      const FlatScope S = sc[j];
+      const uint32_t z = (uint32_t)d.z;
+      const int n = (int)((z >> 8) & kSegMaxLen), p = d.y;
+      int rs, re;
+      if (z & kDescWide) {
+        rs = aux->ref_start[r];
+        re = aux->read_end[r];
+      } else {
+        rs = p - (int)((z >> 24) & 15);
+        re = p + n + (int)(z >> 28);
+      }
+      int sl = (int)((S.pk >> 42) & ((1ull << 21) - 1));
+      const bool huge = sl > kGrpMaxSpan;
+      if (huge) sl = B.span_len[s_begin + j];
+      if (rs < S.sstart || (int64_t)re > (int64_t)S.sstart + sl) {
+        if (first) report(aux->err, kErrIncidSpan, s_begin + j, r);
+      } else {
+        const bool mine = d.w == s_begin + j;
+        if (first && mine) hsum += ws_hash(r);
+        if (!huge && n > 0) {
+          const int64_t r0 = (int64_t)(S.pk << 22) >> 22;
+          const uint64_t sq = (uint64_t)(uint32_t)d.x | ((uint64_t)(z & 0xFF) << 32);
+          const uint64_t rf = (uint64_t)(r0 + p);
+          const uint32_t rz = (uint32_t)((sq >> 32) & 0xFF) | ((uint32_t)((rf >> 32) & 0xFF) << 8) |
+                              ((uint32_t)n << 16) | (((z >> 22) & 1u) << 30) | (mine ? kSegMine : 0u);
+          rec = make_int4((int)(uint32_t)sq, (int)(uint32_t)rf, (int)rz,
+                          (int)((uint32_t)j | ((uint32_t)(p - S.sstart) << 12)));
+          dirty = (S.pk >> 63) != 0;
+          nck = (n + chunk - 1) / chunk;
+        }
+      }
+    }
+    sh.rec[tid] = rec;
+  }
+  if (first) {   // the tile's write-scope hashes into the group's sum (uniform branch)
+    for (int o = 32; o > 0; o >>= 1) {
+      const uint32_t lo = __shfl_xor((uint32_t)hsum, o), hi = __shfl_xor((uint32_t)(hsum >> 32), o);
+      hsum += ((unsigned long long)hi << 32) | lo;
+    }
+    if ((tid & 63) == 0 && hsum) atomicAdd(&sh.hsum, hsum);
+  }
+  const unsigned long long dm = __ballot(dirty);
+  if ((tid & 63) == 0) sh.wdirty[tid >> 6] = dm != 0ull;
+  const int total = grp_tile_map(sh, nck);
+  int any = 0;
+#pragma unroll
+  for (int w = 0; w < kGrpThreads / 64; ++w) any |= sh.wdirty[w];
+  clean = any == 0;
   return total;
 }
 
@@ -627,6 +752,33 @@ __device__ __forceinline__ void grp_scan(const GrpBatch &B, SH &sh, const GrpRan
     for (int t = tid; t < total; t += kGrpThreads) {
       const int j = grp_find(sh, nh, total, t);
       grp_chunk<K, REF2>(B, sh, R, gg, t, j);
+    }
+    __syncthreads();
+  }
+}
+
+// Fused one-segment mode: the same stream over records made from incidences [i_begin, i_end) tile
+// by tile (grp_tile_flat), each tile through the 2-bit reference when all of its records allow.
+template <int K, class SH>
+__device__ __forceinline__ void grp_scan_flat(const GrpBatch &B, SH &sh, const GrpRange &R, const GrpGlobal &gg,
+                                              const GrpAux *__restrict__ aux, int64_t i_begin, int64_t i_end,
+                                              int s_begin, int ns, bool first, int skip, int r_first) {
+  const int tid = threadIdx.x;
+  // each tile's incidence reads are loaded while the previous tile streams (one dependent load,
+  // the descriptor, left per tile); the first tile's by the caller
+  int r_next = r_first;
+  for (int64_t c0 = i_begin; c0 < i_end; c0 += kGrpTile) {
+    const int nh = (int)((i_end - c0) < kGrpTile ? (i_end - c0) : kGrpTile);
+    const int r = r_next;
+    const int64_t in = c0 + kGrpTile + tid;
+    r_next = in < i_end ? aux->incid_read[in] : -1;
+    bool clean;
+    int total = grp_tile_flat(sh, B, aux, c0, nh, 16 * K, s_begin, ns, i_begin, first, r, clean);
+    if (skip & kSkipChunks) total = 0;
+    if (clean && B.ref2) {
+      for (int t = tid; t < total; t += kGrpThreads) grp_chunk<K, true>(B, sh, R, gg, t, grp_find(sh, nh, total, t));
+    } else {
+      for (int t = tid; t < total; t += kGrpThreads) grp_chunk<K, false>(B, sh, R, gg, t, grp_find(sh, nh, total, t));
     }
     __syncthreads();
   }
@@ -927,7 +1079,9 @@ __device__ __forceinline__ void grp_patch_bytes(const GrpBatch &B, SH &sh, int n
 // {seg_end lo, hi, seg_mid lo, hi}, {partition piece A begin lo, hi, end lo, hi} (bytes; fused
 // only), {global region offset lo, hi, capacity, 0}, {piece B begin lo, hi, end lo, hi};
 // segments [seg_begin, seg_mid) have an all-ACGT reference range (2-bit reference).
-template <int U, bool FUSED, int OBS>
+// FLAT: fused one-segment mode (records from incidences and read descriptors, grp_tile_flat; rec4
+// unused; group record 1's mid ignored).
+template <int U, bool FUSED, int OBS, bool FLAT>
 __global__ void __launch_bounds__(kGrpThreads, (OBS > 512 ? 4 : U == 1 ? 6 : U == 2 ? GANON_K2_BLOCKS : U == 4 ? 5 : 4)) k_group(const GrpBatch B, const int4 *__restrict__ groups,
                                                        const int4 *__restrict__ rec4,
                                                        uint8_t *__restrict__ out, const GrpAux *__restrict__ aux,
@@ -965,6 +1119,14 @@ __global__ void __launch_bounds__(kGrpThreads, (OBS > 512 ? 4 : U == 1 ? 6 : U =
   // stores drain while the scan runs (s_waitcnt before the mask stores). (Copying tile by tile,
   // each time up to the tile's written reads so that the scan's loads hit L2, read 0.34 GB less
   // per c2 launch but took 0.55 instead of 0.54 ms in the same build: DESIGN 5.)
+  // (FLAT: the first pass's scope table and first tile's reads are loaded before the copy, which
+  // hides their latency)
+  FlatScope fs{};
+  int r_first = -1;
+  if constexpr (FLAT) {
+    if (tid < s_end - s_begin) fs = flat_load(B, aux, s_begin + tid, i_begin);
+    if (i_begin + tid < i_end) r_first = aux->incid_read[i_begin + tid];
+  }
   if (FUSED && !(skip & kSkipCopy)) {
     copy_windows(B.seq, out, sink.p0, sink.p1, nt_copy);
     copy_windows(B.seq, out, sink.q0, sink.q1, nt_copy);
@@ -977,11 +1139,13 @@ __global__ void __launch_bounds__(kGrpThreads, (OBS > 512 ? 4 : U == 1 ? 6 : U =
     sh.n_patch = 0;
     sh.blk_calls = 0;
     sh.blk_bases = 0;
+    sh.hsum = 0;
   }
   for (int i = tid; i < kGrpMaxScopes; i += kGrpThreads) {
     sh.cnt_calls[i] = 0;
     sh.cnt_bases[i] = 0;
   }
+  bool first = true;   // (FLAT) the group's first pass makes the incidence checks and the hash sum
   for (;;) {
     __syncthreads();
     const int top = sh.top;
@@ -996,6 +1160,7 @@ __global__ void __launch_bounds__(kGrpThreads, (OBS > 512 ? 4 : U == 1 ? 6 : U =
       if (tid == 0) {
         gp(aux->part)[2 * blockIdx.x] = sh.blk_calls;
         gp(aux->part)[2 * blockIdx.x + 1] = sh.blk_bases;
+        if (FLAT) gp(aux->ws_part)[gid] = sh.hsum;
       }
       break;
     }
@@ -1008,7 +1173,17 @@ __global__ void __launch_bounds__(kGrpThreads, (OBS > 512 ? 4 : U == 1 ? 6 : U =
       sh.kmax = 0ull;
     }
     __syncthreads();
-    if (B.ref2) {
+    if constexpr (FLAT) {
+      // the scope table (patch list space: the previous pass's classification is done with it)
+      if (!first) {   // (loaded again: a pass after a key-range split)
+        if (tid < s_end - s_begin) fs = flat_load(B, aux, s_begin + opaque_tid(), i_begin);
+        r_first = i_begin + tid < i_end ? aux->incid_read[i_begin + opaque_tid()] : -1;
+      }
+      if (tid < s_end - s_begin) flat_scopes(sh)[tid] = fs;
+      __syncthreads();
+      grp_scan_flat<U>(B, sh, R, gg, aux, i_begin, i_end, s_begin, s_end - s_begin, first, skip, r_first);
+      first = false;
+    } else if (B.ref2) {
       grp_scan<U, true>(B, sh, R, gg, i_begin, i_mid, rec4, skip);
       grp_scan<U, false>(B, sh, R, gg, i_mid, i_end, rec4, skip);
     } else {
@@ -1558,6 +1733,16 @@ int prepare(ganon_ctx *ctx, ganon_dbatch *db, const ganon_batch *host, bool allo
   a.opay = static_cast<unsigned long long *>(db->b_gopay.p);
   a.tkey = static_cast<unsigned long long *>(db->b_gtkey.p);
   a.tflag = static_cast<unsigned int *>(db->b_gtflag.p);
+  a.incid_read = db->B.incid_read;
+  a.ref_start = db->B.ref_start;
+  a.read_end = db->B.read_end;
+  a.desc = static_cast<const int4 *>(db->b_desc.p);
+  a.incid_off = db->B.incid_off;
+  a.ref_off = db->B.ref_off;
+  a.sdirty = static_cast<const uint8_t *>(db->b_sdirty.p);
+  a.n_reads = db->n_reads;
+  a.err = db->err;
+  a.ws_part = static_cast<unsigned long long *>(db->b_wspart.p);
   unsigned long long *st = db->static_h;
   std::fill(st, st + GANON_N_TOTALS, 0ull);
   st[GANON_T_READS_IN] = (unsigned long long)db->n_reads;
@@ -1806,6 +1991,11 @@ GANON_API int ganon_ctx_set_param(ganon_ctx *ctx, int param, int value) {
     ctx->spec_plan = value;
     return GANON_OK;
   }
+  if (param == GANON_PARAM_FUSED_FLAT) {
+    if (value != 0 && value != 1) return fail(ctx, GANON_E_ARG, "fused one-segment mode: 0 or 1 (got %d)", value);
+    ctx->fused_flat = value;
+    return GANON_OK;
+  }
   if (param == GANON_PARAM_FAR_INIT) {
     if (value < 0) return fail(ctx, GANON_E_ARG, "far-mask list capacity must be >= 0");
     ctx->far_init = value;
@@ -1914,9 +2104,13 @@ GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
     // 512 unless forced: the 1024-entry list (4 workgroups per CU instead of 6) measured slower on
     // c3 too (3.19 vs 2.84 ms, profiles/r02/sweep_c3_obs.jsonl) — occupancy outweighs the region path
     const int obs = ctx->group_obs ? ctx->group_obs : 512;
-    auto kern = obs == 1024 ? (u == 1 ? k_group<1, true, 1024> : k_group<2, true, 1024>)
-                            : u == 2 ? k_group<2, true, 512> : u == 4 ? k_group<4, true, 512>
-                            : u == 8 ? k_group<8, true, 512> : k_group<1, true, 512>;
+    auto kern = db->fused
+                    ? (obs == 1024 ? (u == 1 ? k_group<1, true, 1024, true> : k_group<2, true, 1024, true>)
+                                   : u == 2 ? k_group<2, true, 512, true> : u == 4 ? k_group<4, true, 512, true>
+                                   : u == 8 ? k_group<8, true, 512, true> : k_group<1, true, 512, true>)
+                    : (obs == 1024 ? (u == 1 ? k_group<1, true, 1024, false> : k_group<2, true, 1024, false>)
+                                   : u == 2 ? k_group<2, true, 512, false> : u == 4 ? k_group<4, true, 512, false>
+                                   : u == 8 ? k_group<8, true, 512, false> : k_group<1, true, 512, false>);
     const GrpBatch GB{B.seq, B.ref, B.keep_code, B.ref2, B.keep_pos, B.span_start, B.span_len};
     kern<<<db->n_groups, kGrpThreads, 0, st>>>(GB, static_cast<const int4 *>(db->b_groups.p),
                                                static_cast<const int4 *>(db->b_seg4.p), db->out, db->aux,
@@ -2131,7 +2325,7 @@ GANON_API int ganon_batch_shape(ganon_dbatch *db, int64_t *shape) {
   shape[0] = db->n_id_ops;
   shape[1] = db->max_len;
   shape[2] = db->max_seg;
-  shape[3] = db->long_mode ? 1 : db->flat_mode ? 2 : 0;
+  shape[3] = db->long_mode ? 1 : db->flat_mode ? (db->fused ? 3 : 2) : 0;
   return GANON_OK;
 }
 

@@ -154,11 +154,44 @@ struct ScanOut {
   int64_t g_bound;            // group count bound: (n_incid + weight (n_scopes - 1)) / target + 1
   unsigned long long *part;   // [kParts][part_stride]: partial k of block b at part[k * part_stride + b]
   int64_t part_stride;
+  int4 *desc;                 // fused one-segment mode: [n_reads] read descriptors (ganon_batch.h), or null
+  unsigned long long *cand;   // and [2 g_bound] partition candidates: ~(lowest written offset), atomicMax
+  uint8_t *sdirty;            // and [n_scopes]: the scope's reference span holds a non-ACGT block
+  const uint64_t *bad;
+  int64_t n_blk;
 };
+
 
 __device__ __forceinline__ unsigned long long shfl64(unsigned long long v, int lane) {
   const uint32_t lo = __shfl((uint32_t)v, lane), hi = __shfl((uint32_t)(v >> 32), lane);
   return ((unsigned long long)hi << 32) | lo;
+}
+
+// Partition candidate of a written read (fused one-segment mode): group g's candidate in dataset d
+// is the lowest buffer offset of the reads it writes — the reads whose write scope falls in g. A
+// wave's lanes hold consecutive reads (tumor and normal interleaved by position), so a wave meets
+// few distinct (group, dataset) keys: one device-scope atomic per key and wave — the first
+// pending lane leads, the lanes holding its key reduce their offsets across the wave, the leader
+// stores. key < 0: no candidate. Every lane of the wave calls.
+__device__ __forceinline__ void scan_candidate(unsigned long long *__restrict__ cand, long long key, int64_t so) {
+  const unsigned long long v = ~(unsigned long long)so;   // (complements: the largest wins)
+  const int lane = threadIdx.x & 63;
+  unsigned long long pending = __ballot(key >= 0);
+  while (pending) {
+    const int leader = __ffsll((long long)pending) - 1;
+    const uint32_t klo = __builtin_amdgcn_readlane((uint32_t)key, leader),
+                   khi = __builtin_amdgcn_readlane((uint32_t)((unsigned long long)key >> 32), leader);
+    const long long lk = (long long)(((unsigned long long)khi << 32) | klo);
+    const bool same = key == lk;
+    unsigned long long x = same ? v : 0ull;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const unsigned long long y = shfl64(x, lane ^ o);
+      x = y > x ? y : x;
+    }
+    if (lane == leader) atomicMax(&cand[lk], x);
+    pending &= ~__ballot(same);
+  }
 }
 
 __device__ __forceinline__ void block_parts(unsigned long long (&acc)[kParts], unsigned long long *__restrict__ part,
@@ -234,7 +267,10 @@ __device__ __forceinline__ CigarWalk wave_cigar_walk(const uint32_t *__restrict_
 constexpr int kScanLongCigar = 48;   // reads with more CIGAR ops are walked by a wave (k_prep_scan_long)
 constexpr int kLongGrid = 4096;      // workgroups of k_prep_scan_long at most (4 waves each)
 
-__global__ void __launch_bounds__(kPrepThreads) k_prep_scan(const Raw R, PrepErr *err, ScanOut O, long long weight,
+#ifndef GANON_SCAN_BLOCKS
+#define GANON_SCAN_BLOCKS 1   // resident workgroups per CU k_prep_scan is compiled for (1: no bound)
+#endif
+__global__ void __launch_bounds__(kPrepThreads, GANON_SCAN_BLOCKS) k_prep_scan(const Raw R, PrepErr *err, ScanOut O, long long weight,
                                                             long long target, int read_blocks) {
   unsigned long long acc[kParts] = {0, 0, 0, 0, 0, 0};
   const int tid = threadIdx.x;
@@ -271,8 +307,28 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_scan(const Raw R, PrepErr
       if (ws[u] < -1 || ws[u] >= R.n_scopes) { report(err, kErrReadWriteScope, r, ws[u]); ok[u] = false; }
       if (L[u] >= (1 << 24)) report(err, kErrReadLong, r);
     }
+    // (fused one-segment mode) the CSR offset of each written read's write scope (incidence counts
+    // are below 2^31: load_batch) gives its group: the partition candidates, before the walks
+    int wo[kScanU];
 #pragma unroll
-    for (int u = 0; u < kScanU; ++u) w0[u] = ok[u] && nc[u] > 0 ? R.cigar[co[u]] : 0u;
+    for (int u = 0; u < kScanU; ++u) {
+      w0[u] = ok[u] && nc[u] > 0 ? R.cigar[co[u]] : 0u;
+      wo[u] = O.cand && ok[u] && ws[u] >= 0 && L[u] > 0 ? (int)R.incid_off[ws[u]] : -1;
+    }
+    if (O.cand) {
+#pragma unroll
+      for (int u = 0; u < kScanU; ++u) {
+        long long key = -1;
+        if (wo[u] >= 0) {
+          // group_of, the offset loaded above (32-bit division when it fits)
+          const uint64_t x = (uint64_t)wo[u] + (uint64_t)weight * (uint64_t)ws[u];
+          int64_t g = x >> 32 ? (int64_t)(x / (uint64_t)target) : (int64_t)((uint32_t)x / (uint32_t)target);
+          g = g < 0 ? 0 : (g > O.g_bound - 1 ? O.g_bound - 1 : g);
+          key = 2 * g + (ds[u] & 1);
+        }
+        scan_candidate(O.cand, key, so[u]);
+      }
+    }
 #pragma unroll
     for (int u = 0; u < kScanU; ++u) {
       const int64_t r = r0 + tid + kPrepThreads * u;
@@ -285,9 +341,11 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_scan(const Raw R, PrepErr
           continue;
         }
         // one walk: reference length (bam_endpos), aligned segments as walk_segments cuts them,
-        // I/D ops (the indel tally's observations)
+        // I/D ops (the indel tally's observations); the first segment for the descriptor
         int64_t rl = 0;
         int q = 0, ns = 0, nid = 0;
+        int fq = 0, fn = 0;
+        int fp = 0;
         bool good = true;
         for (int k = 0; k < nc[u]; ++k) {
           const uint32_t w = k == 0 ? w0[u] : R.cigar[co[u] + k];
@@ -295,7 +353,14 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_scan(const Raw R, PrepErr
           const int len = (int)(w >> 4);
           if (op > 8) { report(err, kErrCigarOp, r, op); good = false; break; }
           if (is_aligned_op(op)) {
-            if (q < L[u]) ns += (min(len, L[u] - q) + kSegMaxLen - 1) / kSegMaxLen;
+            if (q < L[u]) {
+              if (ns == 0) {
+                fq = q;
+                fp = (int)rl;
+                fn = min(min(len, L[u] - q), kSegMaxLen);
+              }
+              ns += (min(len, L[u] - q) + kSegMaxLen - 1) / kSegMaxLen;
+            }
             q += len;
             rl += len;
           } else if (op == 1 || op == 4) {
@@ -307,9 +372,19 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_scan(const Raw R, PrepErr
         }
         if (good && (rs[u] < 0 || rs[u] + rl > INT32_MAX)) { report(err, kErrReadPos, r); good = false; }
         if (good) {
-          O.read_end[r] = (int32_t)(rs[u] + (rl > 0 ? rl : 1));
+          const int re = (int32_t)(rs[u] + (rl > 0 ? rl : 1));
+          O.read_end[r] = re;
           acc[kPartMaxSeg] = max(acc[kPartMaxSeg], (unsigned long long)ns);
           acc[kPartIdOps] += (unsigned long long)nid;
+          if (O.desc) {
+            const uint64_t sq = (uint64_t)(2 * so[u] + fq);
+            const int p = (int)(rs[u] + fp);
+            const int d1 = p - rs[u], d2 = re - p - fn;
+            const bool wide = d1 > 15 || d2 < 0 || d2 > 15;
+            const uint32_t z = (uint32_t)((sq >> 32) & 0xFF) | ((uint32_t)fn << 8) | ((uint32_t)ds[u] << 22) |
+                               (wide ? kDescWide : ((uint32_t)d1 << 24) | ((uint32_t)d2 << 28));
+            O.desc[r] = make_int4((int)(uint32_t)sq, p, (int)z, ws[u]);
+          }
         }
       }
     }
@@ -324,6 +399,10 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_scan(const Raw R, PrepErr
       if (R.ref_off[s] < 0 || R.ref_off[s] + sl > R.ref_nibs) report(err, kErrScopeRef, s);
       if (R.keep_code[s] > 15) report(err, kErrScopeKeep, s);
       acc[kPartHuge] += sl > kGrpMaxSpan;
+      if (O.sdirty) {   // (huge scopes: the tile path; a bad slice: reported above)
+        const int64_t ro = R.ref_off[s];
+        O.sdirty[s] = sl > 0 && sl <= kGrpMaxSpan && ro >= 0 && ro + sl <= R.ref_nibs && !ref_clean(O.bad, O.n_blk, ro, (int)sl);
+      }
       // the group table: every bucket from the previous scope's (exclusive) to this scope's starts
       // here (clamped: offsets are only known valid after this kernel)
       int64_t b = group_of(R.incid_off, s, weight, target, nullptr);
@@ -634,6 +713,42 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_pieces(const unsigned lon
       if (!any) pc = piece(0, seq_bytes);
     }
     groups[kGrpRec * (c >> 1) + 2 + 2 * (c & 1)] = pc;
+  }
+}
+
+// Fused one-segment mode, thread per group (the scan's group bound): group records 0, 1 and 3 in
+// closed form from the scan's group table (every segment slot is the incidence's own; the group
+// kernel picks the reference copy per tile), the candidates the scan found (lo, line map marks),
+// and a zero write-scope sum for the groups past the scan's count (the group kernel writes the
+// others'). Nothing on a gated run.
+__global__ void __launch_bounds__(kPrepThreads) k_prep_cands(const Raw R, const longlong2 *__restrict__ gmeta,
+                                                             int n_groups, long long region_per_incid,
+                                                             const unsigned long long *__restrict__ cand,
+                                                             unsigned long long *__restrict__ lo, int4 *__restrict__ groups,
+                                                             LineMap M, unsigned long long *__restrict__ ws_part,
+                                                             const unsigned long long *__restrict__ gate) {
+  const int64_t g = blockIdx.x * (int64_t)kPrepThreads + threadIdx.x;
+  if (g >= n_groups || gate[7]) return;
+  if ((unsigned long long)g >= gate[5]) {
+    ws_part[g] = 0;
+    return;
+  }
+  const longlong2 m0 = gmeta[g];
+  const longlong2 m1 = (unsigned long long)g + 1 < gate[5] ? gmeta[g + 1] : make_longlong2(R.n_scopes, R.n_incid);
+  const int s0 = (int)m0.x, s1 = (int)m1.x;
+  const int64_t i0 = m0.y, i1 = m1.y;
+  const int64_t region = i0 * region_per_incid + (int64_t)kGrpObs * g;
+  const int cap = (int)min((i1 - i0) * region_per_incid + kGrpObs, (long long)(INT32_MAX / 2));
+  groups[kGrpRec * g] = make_int4(s0, s1, (int)(uint32_t)i0, (int)(uint32_t)((uint64_t)i0 >> 32));
+  groups[kGrpRec * g + 1] = make_int4((int)(uint32_t)i1, (int)(uint32_t)((uint64_t)i1 >> 32), (int)(uint32_t)i1,
+                                      (int)(uint32_t)((uint64_t)i1 >> 32));
+  groups[kGrpRec * g + 3] = make_int4((int)(uint32_t)region, (int)(uint32_t)((uint64_t)region >> 32), cap, 0);
+#pragma unroll
+  for (int d = 0; d < 2; ++d) {
+    const unsigned long long c = cand[2 * g + d];
+    const unsigned long long k = c ? ~c : kNone;
+    lo[2 * g + d] = k;
+    if (k != kNone) map_mark(M, k, (uint32_t)(2 * g + d));
   }
 }
 
@@ -1576,7 +1691,8 @@ int size_plan(ganon_ctx *ctx, ganon_dbatch *db, int64_t ng, int tgt0, const Raw 
                                              : std::min<int64_t>(kFarMax, std::max<int64_t>(int64_t(1) << 16, db->n_reads / 8));
   db->far_cap = std::max<int64_t>(db->far_cap_alloc, far_want);
   int4 *s4 = nullptr;
-  if ((rc = grow_n(ctx, db->b_seg4, (size_t)std::max<int64_t>(db->n_seg, 1), &s4))) return rc;
+  // (fused one-segment mode: no records in HBM)
+  if ((rc = grow_n(ctx, db->b_seg4, db->fused ? 1 : (size_t)std::max<int64_t>(db->n_seg, 1), &s4))) return rc;
   if ((rc = grow_n(ctx, db->b_far, (size_t)db->far_cap, &u64))) return rc;
   db->far_cap_alloc = db->far_cap;
   if ((rc = grow_n(ctx, db->b_gokey, (size_t)db->region, &u64)) || (rc = grow_n(ctx, db->b_gopay, (size_t)db->region, &u64)) ||
@@ -1617,9 +1733,12 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db, bool allow_spec) {
   // sizes, or (other sizes: a new batch) the context's last full plan did; the run launches for that
   // shape at once (buffers sized on the host from the counts) and the scan's reduction checks it (gate)
   // ("same": the context's previous plan was of this batch — a replan of its contents in place)
+  // fused one-segment mode: the scan describes the reads and finds the partition candidates when the
+  // batch may be planned in that mode (not after the context's last full plan found another shape)
+  const bool want_fused = ctx->fused_flat && (ctx->prep_long == -1 || ctx->prep_long == 2) && !ctx->last_full_nonflat;
   const bool same = db->spec_ready && db->spec_sizes[0] == nr && db->spec_sizes[1] == ns &&
                     db->spec_sizes[2] == db->n_incid && db->spec_sizes[3] == tgt0 && db->flat_mode &&
-                    ctx->last_plan == db;
+                    ctx->last_plan == db && db->fused == want_fused;
   ctx->last_plan = db;
   const bool sized = !same && ctx->spec_shape_ok && ctx->spec_tgt == tgt0 && ctx->prep_long == -1;
   const bool spec = allow_spec && ctx->spec_plan && (same || sized);
@@ -1629,6 +1748,7 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db, bool allow_spec) {
     db->n_groups = 0;
     db->spec_ready = false;
   }
+  db->fused = want_fused;   // (until the full plan's shape says otherwise)
   const int64_t spec_rpi = !spec ? 0 : db->spec_sized ? ctx->spec_rpi : db->region_per_incid;
   longlong2 *gm = nullptr;
   unsigned long long *part = nullptr;
@@ -1642,14 +1762,24 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db, bool allow_spec) {
       (rc = grow_n(ctx, db->b_part, (size_t)kParts * (nb + kLongGrid), &part)) ||
       (rc = grow_n(ctx, db->b_long, (size_t)std::max<int64_t>(nr, 1), &long_list)))
     return rc;
+  unsigned long long *cand = nullptr;
+  int4 *desc = nullptr;
+  uint8_t *sdirty = nullptr;
+  if (db->fused && ((rc = grow_n(ctx, db->b_desc, (size_t)std::max<int64_t>(nr, 1), &desc)) ||
+                    (rc = grow_n(ctx, db->b_cand, 2 * (size_t)g_bound, &cand)) ||
+                    (rc = grow_n(ctx, db->b_sdirty, (size_t)std::max<int64_t>(ns, 1), &sdirty))))
+    return rc;
+  db->cand = cand;
   unsigned int *long_count = db->long_count;
   const int64_t pstride = nb + kLongGrid;
-  const ScanOut O{read_end, long_list, long_count, gm, g_bound, part, pstride};
+  const ScanOut O{read_end, long_list, long_count, gm, g_bound, part, pstride, desc, cand,
+                  sdirty, db->ref->bad, db->ref->n_blk};
   {
     // 1. the batch scan: every per-read and per-scope check, read ends, the group table of the
     //    short-read modes, per-block partials; then their reduction
     KernelScope ks(ctx, "prep_scan");
     HIP_OR_FAIL(hipMemsetAsync(db->err, 0, db->flags_bytes, st));   // error, status, long reads, far need
+    if (cand) HIP_OR_FAIL(hipMemsetAsync(cand, 0, 2 * (size_t)g_bound * sizeof *cand, st));
     hipLaunchKernelGGL(k_prep_scan, dim3((unsigned)nb), dim3(kPrepThreads), 0, st, R, db->err, O, w0, (long long)tgt0,
                        (int)rb);
     hipLaunchKernelGGL(k_prep_reduce, dim3(1), dim3(kReduceThreads), 0, st, R, part, pstride, (int)nb, w0, (long long)tgt0,
@@ -1706,6 +1836,10 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db, bool allow_spec) {
   // 11.3 ms instead of ~0.2 on a planner-built 2 M-read batch (profiles/r02/planner_batch_bench.json)
   db->long_mode = ctx->prep_long == 1 || (ctx->prep_long == -1 && max_seg > 1 && max_len > kLongReadLen);
   db->flat_mode = !db->long_mode && max_seg <= 1 && (ctx->prep_long == -1 || ctx->prep_long == 2);
+  // fused: the scan described every read (none left to the wave walk)
+  db->fused = db->fused && db->flat_mode && n_long == 0;
+  if (!db->fused) db->cand = nullptr;
+  ctx->last_full_nonflat = !db->flat_mode;
   // overflow-region observations per incidence: the longest read's ceil(L / 48)
   db->region_per_incid = (int64_t)((max_len + 47) / 48);
   db->group_target = ctx->group_target ? ctx->group_target : db->long_mode ? 1408 : 704;   // auto (sweep_c5 / sweep_c3)
@@ -1761,7 +1895,18 @@ int run(ganon_ctx *ctx, ganon_dbatch *db) {
       KernelScope ks(ctx, "prep_emit");
       HIP_OR_FAIL(hipMemsetAsync(db->b_linemap.p, 0, (size_t)line_map_words(db) * 8, ctx->stream));
     }
-    if ((rc = launch_emit(ctx, db, R, 1))) return rc;
+    if (db->fused) {
+      // no records: group records, candidates and line map marks from the scan's results
+      KernelScope ks(ctx, "prep_cands");
+      hipLaunchKernelGGL(k_prep_cands, dim3(grid_for(db->n_groups, INT32_MAX)), dim3(kPrepThreads), 0, ctx->stream, R,
+                         static_cast<const longlong2 *>(db->b_gs0.p), db->n_groups, (long long)db->region_per_incid,
+                         static_cast<const unsigned long long *>(db->cand), static_cast<unsigned long long *>(db->b_lo.p),
+                         static_cast<int4 *>(db->b_groups.p), line_map(db), static_cast<unsigned long long *>(db->b_wspart.p),
+                         static_cast<const unsigned long long *>(db->plan_info));
+      if ((rc = check_launch(ctx, "k_prep_cands"))) return rc;
+    } else if ((rc = launch_emit(ctx, db, R, 1))) {
+      return rc;
+    }
   } else if ((rc = launch_groups(ctx, db, R)) || (rc = launch_emit(ctx, db, R, 1))) {
     return rc;
   }

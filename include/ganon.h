@@ -140,7 +140,12 @@ GANON_API int ganon_ctx_set_variant(ganon_ctx *ctx, int variant);
 enum { GANON_PARAM_GROUP_UNROLL = 1, GANON_PARAM_GROUP_SKIP = 2, GANON_PARAM_GROUP_TARGET = 3,
        GANON_PARAM_NT_COPY = 4, GANON_PARAM_REF2 = 5, GANON_PARAM_FASTQ_SKIP = 6, GANON_PARAM_FASTQ_KD = 7,
        GANON_PARAM_INDEL_SORT = 8, GANON_PARAM_PREP_LONG = 9, GANON_PARAM_GROUP_OBS = 10,
-       GANON_PARAM_PREP_UNROLL = 11, GANON_PARAM_FAR_INIT = 12, GANON_PARAM_SPEC_PLAN = 13 };
+       GANON_PARAM_PREP_UNROLL = 11, GANON_PARAM_FAR_INIT = 12, GANON_PARAM_SPEC_PLAN = 13,
+       GANON_PARAM_FUSED_FLAT = 14 };
+/* GANON_PARAM_FUSED_FLAT: 1 (default) a one-segment batch (no read of more than one aligned segment,
+ * none of more than 48 CIGAR ops) builds no segment records in HBM — the plan's scan writes a 16-byte
+ * descriptor per read and the partition candidates, and the group kernel makes each incidence's
+ * record in LDS; 0 the record pass (the one-segment prep emit). Same results. */
 /* GANON_PARAM_SPEC_PLAN: 1 (default) speculative replans (ganon_batch_replan), 0 every plan
  * synchronizes for the scan's result, 2 (testing knob) reloads speculate too — their caller must
  * not read the shape before the download. Same results. */
@@ -224,7 +229,7 @@ GANON_API int ganon_last_kernel_times(ganon_ctx *ctx, ganon_kernel_time *out, in
 GANON_API int ganon_batch_info(ganon_dbatch *db, int64_t *info8);
 /* Shape of the planned batch, from the device scan: [I/D CIGAR ops (0: the indel tally has nothing
  * to do), longest read, most aligned segments of one read, prep mode (0 two-pass, 1 long-read,
- * 2 one-segment)]. Since ABI 4. */
+ * 2 one-segment, 3 one-segment fused: GANON_PARAM_FUSED_FLAT)]. Since ABI 4. */
 GANON_API int ganon_batch_shape(ganon_dbatch *db, int64_t *shape4);
 /* How often the group kernel took its rarer paths since upload (synchronous): [lists of more than
  * 256 observations classified after an LDS sort, lists of more than 512 (overflowing into the

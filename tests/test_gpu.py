@@ -628,7 +628,7 @@ def test_replan_is_a_fresh_upload(masker, oracle):
             got = db.download()
             for k in range(4):
                 assert np.array_equal(got[k], want[k]), k
-            assert db.shape()["prep_mode"] == "one_segment" or arr is b
+            assert db.shape()["prep_mode"].startswith("one_segment") or arr is b
     finally:
         db.free()
     o_out, o_calls, o_bases, _ = oracle.mask(a)
@@ -713,7 +713,7 @@ def test_speculative_replan_and_fallback(hip_built):
             db.run()
             got = db.download()
             assert all(np.array_equal(got[k], want_a[k]) for k in range(4))
-            assert db.shape()["prep_mode"] == "one_segment"
+            assert db.shape()["prep_mode"].startswith("one_segment")   # (fused after a flat plan)
             db.reload(b)          # speculative: the gate stops the run, download plans b in full
             db.run()
             got = db.download()
@@ -765,6 +765,67 @@ def test_far_list_overflow_grows_and_reruns(hip_built, oracle):
         m.close()
     assert o_bases.sum() > 10
     assert np.array_equal(out, o_out) and np.array_equal(calls, o_calls) and np.array_equal(bases, o_bases)
+
+
+def _recigar(arr: dict, r: int, ops) -> dict:
+    """arr with read r's CIGAR replaced by ops ((length, op code) pairs)."""
+    b = {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in arr.items()}
+    b["cig_off"][r] = len(b["cigar"])
+    b["n_cig"][r] = len(ops)
+    b["cigar"] = np.concatenate([b["cigar"], np.array([(n << 4) | op for n, op in ops], np.uint32)])
+    return b
+
+
+def test_fused_one_segment_matches_record_pass(hip_built, oracle):
+    """GANON_PARAM_FUSED_FLAT 1 (default): a one-segment batch builds no records in HBM — the scan's
+    read descriptors and candidates feed the group kernel, which makes each incidence's record in LDS.
+    Byte-equal to the record pass (PARAM 0) and the oracle on: a configs[1]-shaped batch; reads whose
+    segment starts or ends more than 15 positions inside their reference span (the descriptor's wide
+    form: 16D134M16S, 16S134M16D); a reference with N bases inside written reads' scopes (tiles that
+    read the nt16 copy); a permuted buffer layout (candidates from unordered offsets); and the
+    incidence errors, reported by the download in both modes."""
+    from genomeanonymizer_amd import native
+    from genomeanonymizer_amd.synth.batch import config2_batch, relayout
+    a, _ = config2_batch(n_reads=160_000, genome=40_000_000, n_windows=14_000, n_germline=40_000, seed=52)
+    wr = np.nonzero((a["write_scope"] >= 0) & (a["n_cig"] == 1) & (a["read_len"] == 150))[0]
+    b = _recigar(a, int(wr[100]), [(16, 2), (134, 0), (16, 4)])
+    b = _recigar(b, int(wr[5000]), [(16, 4), (134, 0), (16, 2)])
+    b = _recigar(b, int(wr[9000]), [(3, 2), (147, 0), (3, 4)])
+    c = {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in a.items()}
+    for r in wr[::997][:40]:   # N bases in the reference under written reads
+        s = int(c["write_scope"][r])
+        nib = int(c["scope_ref_off"][s]) + int(c["ref_start"][r]) - int(c["scope_span_start"][s]) + 20
+        c["ref_nt16"][nib // 2: nib // 2 + 4] = 0xFF
+    d = relayout(a, np.random.default_rng(5).permutation(len(a["read_len"])))
+    fused, rec = native.HipMasker(0), native.HipMasker(0)
+    rec.set_param(native.PARAM_FUSED_FLAT, 0)
+    try:
+        for name, x in (("plain", a), ("wide", b), ("nref", c), ("layout", d)):
+            o = oracle.mask(x)
+            got_f, got_r = fused.mask(x), rec.mask(x)
+            for k in range(3):
+                assert np.array_equal(got_f[k], got_r[k]), (name, k)
+                assert np.array_equal(got_f[k], o[k]), (name, k)
+            assert np.array_equal(got_f[3], got_r[3]), name
+            db = fused.upload(x)
+            try:
+                assert db.shape()["prep_mode"] == "one_segment_fused", name
+            finally:
+                db.free()
+        assert o[2].sum() > 0
+        for m in (fused, rec):
+            bad = {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in a.items()}
+            bad["incid_read"][7] = len(a["read_len"]) + 3
+            with pytest.raises(native.GanonError, match="out of range"):
+                m.mask(bad)
+            bad = {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in a.items()}
+            far = int(wr[np.nonzero(a["ref_start"][wr] > 500_000)[0][0]])
+            bad["ref_start"][far] -= 100_000   # outside every scope that lists it
+            with pytest.raises(native.GanonError, match="outside its span"):
+                m.mask(bad)
+    finally:
+        fused.close()
+        rec.close()
 
 
 def test_incidence_errors_are_reported_by_download(masker):

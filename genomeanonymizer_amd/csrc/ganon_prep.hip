@@ -44,6 +44,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <type_traits>
 
 #include <rocprim/device/device_scan.hpp>
 
@@ -156,9 +157,6 @@ struct ScanOut {
   int64_t part_stride;
   int4 *desc;                 // fused one-segment mode: [n_reads] read descriptors (ganon_batch.h), or null
   unsigned long long *cand;   // and [2 g_bound] partition candidates: ~(lowest written offset), atomicMax
-  uint8_t *sdirty;            // and [n_scopes]: the scope's reference span holds a non-ACGT block
-  const uint64_t *bad;
-  int64_t n_blk;
 };
 
 
@@ -270,43 +268,55 @@ constexpr int kLongGrid = 4096;      // workgroups of k_prep_scan_long at most (
 #ifndef GANON_SCAN_BLOCKS
 #define GANON_SCAN_BLOCKS 1   // resident workgroups per CU k_prep_scan is compiled for (1: no bound)
 #endif
+// NARROW: sequence bytes and CIGAR ops below 2^31 (every configs[1]-sized batch): the offsets are
+// kept as 32 bits once checked (fewer live registers across the walks: occupancy).
+template <bool NARROW>
 __global__ void __launch_bounds__(kPrepThreads, GANON_SCAN_BLOCKS) k_prep_scan(const Raw R, PrepErr *err, ScanOut O, long long weight,
                                                             long long target, int read_blocks) {
   unsigned long long acc[kParts] = {0, 0, 0, 0, 0, 0};
   const int tid = threadIdx.x;
   if ((int)blockIdx.x < read_blocks) {
+    typedef typename std::conditional<NARROW, uint32_t, int64_t>::type Off;
+    uint32_t n_wr = 0, mx_len = 0, mx_seg = 0, n_id = 0;   // (per thread: 32 bits are enough)
+    unsigned long long hsum = 0;
     // kScanU reads per thread, each load stage issued for all of them before any is used (the chain
     // read fields -> first CIGAR word is latency bound)
     constexpr int kScanU = kScanReadsPerBlock / kPrepThreads;
     const int64_t r0 = (int64_t)blockIdx.x * kScanReadsPerBlock;
     const int64_t r1 = min(r0 + kScanReadsPerBlock, (int64_t)R.n_reads);
     int L[kScanU], nc[kScanU], rs[kScanU], ws[kScanU], ds[kScanU];
-    int64_t co[kScanU], so[kScanU];
+    Off co[kScanU], so[kScanU];
     bool ok[kScanU];
+    {
+      int64_t co64[kScanU], so64[kScanU];
 #pragma unroll
-    for (int u = 0; u < kScanU; ++u) {
-      const int64_t r = r0 + tid + kPrepThreads * u;
-      ok[u] = r < r1;
-      const int64_t rr = ok[u] ? r : r0;
-      L[u] = R.read_len[rr];
-      nc[u] = R.n_cig[rr];
-      co[u] = R.cig_off[rr];
-      rs[u] = R.ref_start[rr];
-      so[u] = R.seq_off[rr];
-      ws[u] = R.write_scope[rr];
-      ds[u] = R.dataset[rr];
+      for (int u = 0; u < kScanU; ++u) {
+        const int64_t r = r0 + tid + kPrepThreads * u;
+        ok[u] = r < r1;
+        const int64_t rr = ok[u] ? r : r0;
+        L[u] = R.read_len[rr];
+        nc[u] = R.n_cig[rr];
+        co64[u] = R.cig_off[rr];
+        rs[u] = R.ref_start[rr];
+        so64[u] = R.seq_off[rr];
+        ws[u] = R.write_scope[rr];
+        ds[u] = R.dataset[rr];
+      }
+#pragma unroll
+      for (int u = 0; u < kScanU; ++u) {
+        const int64_t r = r0 + tid + kPrepThreads * u;
+        if (ok[u]) {
+          if (L[u] < 0 || so64[u] < 0 || so64[u] + ((int64_t)L[u] + 1) / 2 > R.seq_bytes) { report(err, kErrReadSeq, r); ok[u] = false; }
+          else if (nc[u] < 0 || co64[u] < 0 || co64[u] + nc[u] > R.n_cigar_ops) { report(err, kErrReadCigar, r); ok[u] = false; }
+          if (ds[u] > 1) report(err, kErrReadDataset, r);
+          if (ws[u] < -1 || ws[u] >= R.n_scopes) { report(err, kErrReadWriteScope, r, ws[u]); ok[u] = false; }
+          if (L[u] >= (1 << 24)) report(err, kErrReadLong, r);
+        }
+        co[u] = ok[u] ? (Off)co64[u] : (Off)0;   // (checked: in range)
+        so[u] = ok[u] ? (Off)so64[u] : (Off)0;
+      }
     }
     uint32_t w0[kScanU];
-#pragma unroll
-    for (int u = 0; u < kScanU; ++u) {
-      const int64_t r = r0 + tid + kPrepThreads * u;
-      if (!ok[u]) continue;
-      if (L[u] < 0 || so[u] < 0 || so[u] + ((int64_t)L[u] + 1) / 2 > R.seq_bytes) { report(err, kErrReadSeq, r); ok[u] = false; }
-      else if (nc[u] < 0 || co[u] < 0 || co[u] + nc[u] > R.n_cigar_ops) { report(err, kErrReadCigar, r); ok[u] = false; }
-      if (ds[u] > 1) report(err, kErrReadDataset, r);
-      if (ws[u] < -1 || ws[u] >= R.n_scopes) { report(err, kErrReadWriteScope, r, ws[u]); ok[u] = false; }
-      if (L[u] >= (1 << 24)) report(err, kErrReadLong, r);
-    }
     // (fused one-segment mode) the CSR offset of each written read's write scope (incidence counts
     // are below 2^31: load_batch) gives its group: the partition candidates, before the walks
     int wo[kScanU];
@@ -326,16 +336,16 @@ __global__ void __launch_bounds__(kPrepThreads, GANON_SCAN_BLOCKS) k_prep_scan(c
           g = g < 0 ? 0 : (g > O.g_bound - 1 ? O.g_bound - 1 : g);
           key = 2 * g + (ds[u] & 1);
         }
-        scan_candidate(O.cand, key, so[u]);
+        scan_candidate(O.cand, key, (int64_t)so[u]);
       }
     }
 #pragma unroll
     for (int u = 0; u < kScanU; ++u) {
       const int64_t r = r0 + tid + kPrepThreads * u;
       if (ok[u]) {
-        acc[kPartWritten] += ws[u] >= 0;
-        if (ws[u] >= 0) acc[kPartWsHash] += ws_hash((int)r);
-        acc[kPartMaxLen] = max(acc[kPartMaxLen], (unsigned long long)L[u]);
+        n_wr += ws[u] >= 0;
+        if (ws[u] >= 0) hsum += ws_hash((int)r);
+        mx_len = max(mx_len, (uint32_t)L[u]);
         if (nc[u] > kScanLongCigar) {   // a long read: k_prep_scan_long walks it with a wave
           O.long_list[atomicAdd(O.long_count, 1u)] = (int32_t)r;
           continue;
@@ -374,10 +384,10 @@ __global__ void __launch_bounds__(kPrepThreads, GANON_SCAN_BLOCKS) k_prep_scan(c
         if (good) {
           const int re = (int32_t)(rs[u] + (rl > 0 ? rl : 1));
           O.read_end[r] = re;
-          acc[kPartMaxSeg] = max(acc[kPartMaxSeg], (unsigned long long)ns);
-          acc[kPartIdOps] += (unsigned long long)nid;
+          mx_seg = max(mx_seg, (uint32_t)ns);
+          n_id += (uint32_t)nid;
           if (O.desc) {
-            const uint64_t sq = (uint64_t)(2 * so[u] + fq);
+            const uint64_t sq = 2 * (uint64_t)so[u] + (uint64_t)fq;
             const int p = (int)(rs[u] + fp);
             const int d1 = p - rs[u], d2 = re - p - fn;
             const bool wide = d1 > 15 || d2 < 0 || d2 > 15;
@@ -388,6 +398,11 @@ __global__ void __launch_bounds__(kPrepThreads, GANON_SCAN_BLOCKS) k_prep_scan(c
         }
       }
     }
+    acc[kPartWritten] = n_wr;
+    acc[kPartWsHash] = hsum;
+    acc[kPartMaxLen] = mx_len;
+    acc[kPartMaxSeg] = mx_seg;
+    acc[kPartIdOps] = n_id;
   } else {
     const int64_t s0 = (int64_t)(blockIdx.x - read_blocks) * kScanScopesPerBlock;
     const int64_t s1 = min(s0 + kScanScopesPerBlock, (int64_t)R.n_scopes);
@@ -399,10 +414,7 @@ __global__ void __launch_bounds__(kPrepThreads, GANON_SCAN_BLOCKS) k_prep_scan(c
       if (R.ref_off[s] < 0 || R.ref_off[s] + sl > R.ref_nibs) report(err, kErrScopeRef, s);
       if (R.keep_code[s] > 15) report(err, kErrScopeKeep, s);
       acc[kPartHuge] += sl > kGrpMaxSpan;
-      if (O.sdirty) {   // (huge scopes: the tile path; a bad slice: reported above)
-        const int64_t ro = R.ref_off[s];
-        O.sdirty[s] = sl > 0 && sl <= kGrpMaxSpan && ro >= 0 && ro + sl <= R.ref_nibs && !ref_clean(O.bad, O.n_blk, ro, (int)sl);
-      }
+
       // the group table: every bucket from the previous scope's (exclusive) to this scope's starts
       // here (clamped: offsets are only known valid after this kernel)
       int64_t b = group_of(R.incid_off, s, weight, target, nullptr);
@@ -720,15 +732,23 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_pieces(const unsigned lon
 // closed form from the scan's group table (every segment slot is the incidence's own; the group
 // kernel picks the reference copy per tile), the candidates the scan found (lo, line map marks),
 // and a zero write-scope sum for the groups past the scan's count (the group kernel writes the
-// others'). Nothing on a gated run.
+// others'); and thread per scope: whether the scope's reference span holds a non-ACGT block (its
+// records then read the nt16 reference). Nothing on a gated run.
 __global__ void __launch_bounds__(kPrepThreads) k_prep_cands(const Raw R, const longlong2 *__restrict__ gmeta,
                                                              int n_groups, long long region_per_incid,
                                                              const unsigned long long *__restrict__ cand,
                                                              unsigned long long *__restrict__ lo, int4 *__restrict__ groups,
                                                              LineMap M, unsigned long long *__restrict__ ws_part,
-                                                             const unsigned long long *__restrict__ gate) {
+                                                             const unsigned long long *__restrict__ gate,
+                                                             uint8_t *__restrict__ sdirty, const uint64_t *__restrict__ bad,
+                                                             int64_t n_blk) {
   const int64_t g = blockIdx.x * (int64_t)kPrepThreads + threadIdx.x;
-  if (g >= n_groups || gate[7]) return;
+  if (gate[7]) return;
+  if (g < R.n_scopes) {   // (huge scopes: the tile path; slices were validated by the scan)
+    const int64_t sl = R.span_len[g], ro = R.ref_off[g];
+    sdirty[g] = sl > 0 && sl <= kGrpMaxSpan && !ref_clean(bad, n_blk, ro, (int)sl);
+  }
+  if (g >= n_groups) return;
   if ((unsigned long long)g >= gate[5]) {
     ws_part[g] = 0;
     return;
@@ -1764,7 +1784,7 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db, bool allow_spec) {
     return rc;
   unsigned long long *cand = nullptr;
   int4 *desc = nullptr;
-  uint8_t *sdirty = nullptr;
+  uint8_t *sdirty = nullptr;   // (k_prep_cands)
   if (db->fused && ((rc = grow_n(ctx, db->b_desc, (size_t)std::max<int64_t>(nr, 1), &desc)) ||
                     (rc = grow_n(ctx, db->b_cand, 2 * (size_t)g_bound, &cand)) ||
                     (rc = grow_n(ctx, db->b_sdirty, (size_t)std::max<int64_t>(ns, 1), &sdirty))))
@@ -1772,16 +1792,16 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db, bool allow_spec) {
   db->cand = cand;
   unsigned int *long_count = db->long_count;
   const int64_t pstride = nb + kLongGrid;
-  const ScanOut O{read_end, long_list, long_count, gm, g_bound, part, pstride, desc, cand,
-                  sdirty, db->ref->bad, db->ref->n_blk};
+  const ScanOut O{read_end, long_list, long_count, gm, g_bound, part, pstride, desc, cand};
   {
     // 1. the batch scan: every per-read and per-scope check, read ends, the group table of the
     //    short-read modes, per-block partials; then their reduction
     KernelScope ks(ctx, "prep_scan");
     HIP_OR_FAIL(hipMemsetAsync(db->err, 0, db->flags_bytes, st));   // error, status, long reads, far need
     if (cand) HIP_OR_FAIL(hipMemsetAsync(cand, 0, 2 * (size_t)g_bound * sizeof *cand, st));
-    hipLaunchKernelGGL(k_prep_scan, dim3((unsigned)nb), dim3(kPrepThreads), 0, st, R, db->err, O, w0, (long long)tgt0,
-                       (int)rb);
+    const bool narrow = db->seq_bytes < INT32_MAX && db->n_cigar_ops < INT32_MAX;
+    hipLaunchKernelGGL(narrow ? k_prep_scan<true> : k_prep_scan<false>, dim3((unsigned)nb), dim3(kPrepThreads), 0, st, R,
+                       db->err, O, w0, (long long)tgt0, (int)rb);
     hipLaunchKernelGGL(k_prep_reduce, dim3(1), dim3(kReduceThreads), 0, st, R, part, pstride, (int)nb, w0, (long long)tgt0,
                        g_bound, db->plan_info, static_cast<const PrepErr *>(db->err),
                        (long long)spec_rpi, static_cast<const unsigned int *>(long_count));
@@ -1898,11 +1918,13 @@ int run(ganon_ctx *ctx, ganon_dbatch *db) {
     if (db->fused) {
       // no records: group records, candidates and line map marks from the scan's results
       KernelScope ks(ctx, "prep_cands");
-      hipLaunchKernelGGL(k_prep_cands, dim3(grid_for(db->n_groups, INT32_MAX)), dim3(kPrepThreads), 0, ctx->stream, R,
-                         static_cast<const longlong2 *>(db->b_gs0.p), db->n_groups, (long long)db->region_per_incid,
-                         static_cast<const unsigned long long *>(db->cand), static_cast<unsigned long long *>(db->b_lo.p),
-                         static_cast<int4 *>(db->b_groups.p), line_map(db), static_cast<unsigned long long *>(db->b_wspart.p),
-                         static_cast<const unsigned long long *>(db->plan_info));
+      hipLaunchKernelGGL(k_prep_cands, dim3(grid_for(std::max<int64_t>(db->n_groups, db->n_scopes), INT32_MAX)),
+                         dim3(kPrepThreads), 0, ctx->stream, R, static_cast<const longlong2 *>(db->b_gs0.p), db->n_groups,
+                         (long long)db->region_per_incid, static_cast<const unsigned long long *>(db->cand),
+                         static_cast<unsigned long long *>(db->b_lo.p), static_cast<int4 *>(db->b_groups.p), line_map(db),
+                         static_cast<unsigned long long *>(db->b_wspart.p),
+                         static_cast<const unsigned long long *>(db->plan_info), static_cast<uint8_t *>(db->b_sdirty.p),
+                         db->ref->bad, db->ref->n_blk);
       if ((rc = check_launch(ctx, "k_prep_cands"))) return rc;
     } else if ((rc = launch_emit(ctx, db, R, 1))) {
       return rc;

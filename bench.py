@@ -477,7 +477,7 @@ def main() -> None:
                     help="round-2 step: run only, the plan made once at upload (not a fresh batch)")
     ap.add_argument("--pmc", default=None,
                     help="PMC step summary (tools/pmc_step.py) for the traffic field; default "
-                         "profiles/r03/pmc_step_<config>.json when present")
+                         "profiles/r04 (else r03)/pmc_step_<config>.json when present")
     args = ap.parse_args()
     for k, v in CONFIGS[args.config]["defaults"].items():
         if getattr(args, k) is None:
@@ -738,15 +738,20 @@ def main() -> None:
     alg_total = sum(algorithmic_bytes(a) for a in prof_arrs) // len(prof_arrs)
     achieved = alg_total / (pass_ms * 1e-3) / 1e9
     traffic = dom_traffic = None
-    pmc_path = args.pmc or os.path.join(REPO, "profiles", "r03", f"pmc_step_{args.config}.json")
-    if os.path.exists(pmc_path):
-        try:
-            pmc = json.load(open(pmc_path))
-            if pmc.get("reads") == args.reads and pmc.get("config") == args.config:
-                traffic = pmc.get("step_hbm_bytes")
-                dom_traffic = pmc.get("kernels", {}).get("k_group", {}).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    # the newest round's PMC summary of this config and size (tools/gpu_pmc_r04.sh)
+    pmc_paths = [args.pmc] if args.pmc else [os.path.join(REPO, "profiles", r, f"pmc_step_{args.config}.json")
+                                             for r in ("r04", "r03")]
+    pmc_used = None
+    for pmc_path in pmc_paths:
+        if traffic is None and os.path.exists(pmc_path):
+            try:
+                pmc = json.load(open(pmc_path))
+                if pmc.get("reads") == args.reads and pmc.get("config") == args.config:
+                    traffic = pmc.get("step_hbm_bytes")
+                    dom_traffic = pmc.get("kernels", {}).get("k_group", {}).get("hbm_bytes_per_launch")
+                    pmc_used = os.path.relpath(pmc_path, REPO)
+            except Exception:
+                traffic = None
 
     reads_total = reads_timed * world
     value = reads_total / dt
@@ -775,7 +780,7 @@ def main() -> None:
                    "pipeline": args.pipeline},
         "roofline": {"bound": "hbm", "kernel": "step: " + " + ".join(per_kernel), "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                     "traffic": traffic, "algorithmic_bytes_per_launch": alg_total,
+                     "traffic": traffic, "traffic_source": pmc_used, "algorithmic_bytes_per_launch": alg_total,
                      "avg_launch_ms": round(pass_ms, 5),
                      "dominant": {"kernel": dom, "algorithmic_bytes_per_launch": dom_bytes,
                                   "avg_launch_ms": round(dom_ms, 5),

@@ -52,6 +52,15 @@ constexpr uint32_t kSegMine = 1u << 31;     // the segment's read is written by 
 //   w = write scope.
 // wide: one of the two deltas did not fit (the span check then reads ref_start and read_end).
 constexpr uint32_t kDescWide = 1u << 23;
+// long-read mode: read record (int4; k_prep_read_recs, at b_rbase[read] + k for the read's k-th
+// aligned-segment piece, in CIGAR order): x = query nibble bits 0-31, y = contig position,
+// z = query nibble bits 32-39 | length << 16 (14 bits) | dataset << 30, w = 0 — a segment record
+// without its scope's fields. incidence record (int4; k_prep_long_groups): x = the incidence's
+// first slot in its group's slot space (its read's records follow), y = scope local | mine << 31,
+// z / w = b_rbase of its read (lo, hi). (The reference copy is chosen per tile from the scopes'
+// flags: a per-segment flag moved nothing on C5, profiles/r04/c5_ab.) The group kernel's slot t of a group: the incidence with the
+// largest first slot <= t, its read record t - x. Long-read group records: [0] seg_begin = 0,
+// [1] seg_end = the group's slot count, seg_mid = its first incidence; [3].w = its incidence count.
 
 // Device view of a batch (all pointers device-resident).
 struct DevBatch {
@@ -101,6 +110,7 @@ struct GrpAux {
   const int4 *desc;
   const int64_t *incid_off, *ref_off;
   const uint8_t *sdirty;                        // per scope: its reference span holds a non-ACGT block
+  const int4 *inc4, *rrec;                      // long-read mode: incidence and read records
   int32_t n_reads, pad_;
   PrepErr *err;
   unsigned long long *ws_part;
@@ -243,6 +253,11 @@ struct ganon_dbatch {
   // incidence's record in LDS. Off for batches with long-CIGAR reads (the scan does not describe them).
   bool fused = false;
   ganon_dev::DBuf b_desc, b_cand, b_sdirty;
+  // long-read mode: segment records once per read (b_rrec at b_rbase[read]) and per incidence its
+  // first slot in its group, scope and write mark (b_inc4); the group kernel reads the read's
+  // records for every scope that lists it
+  ganon_dev::DBuf b_inc4, b_rbase, b_rrec;
+  int64_t n_rrec = 0, n_long_seg = 0;
   unsigned long long *cand = nullptr;   // the scan's candidates of this plan (null: the emit marks them)
   int64_t *scost = nullptr;
   int64_t n_seg = 0, region = 0, far_cap = 0, n_written = 0, region_per_incid = 0, n_id_ops = 0;

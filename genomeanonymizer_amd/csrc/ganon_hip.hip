@@ -757,16 +757,103 @@ __device__ __forceinline__ void grp_scan(const GrpBatch &B, SH &sh, const GrpRan
   }
 }
 
+// Long-read mode: slots [c0, c0 + nh) of a group whose incidences are [inc0, inc0 + n_inc): the
+// incidence owning slot t (largest first slot <= t: incidences without records share their
+// successor's first slot and lose to it), its read's record t - first slot, completed with the
+// scope's fields from the staged scope table (reference offset, span start, reference flag) and
+// the incidence's write mark. A tile of a 10-100 kb read's incidence reads 256 consecutive read
+// records (one coalesced load). long_fetch issues a tile's loads; grp_scan_long issues the next
+// tile's before it streams the current one, so their latency overlaps the chunk loads.
+// itab: the group's incidence records staged in LDS after the scope table (ns + n_inc <= the
+// table's 256 entries: every C5 group), else null (looked up in global memory).
+struct LongFetch {
+  int4 rr;   // the read record
+  int iy;    // the incidence record's y: scope local | mine << 31
+};
+
+__device__ __forceinline__ LongFetch long_fetch(const GrpAux *__restrict__ aux, int64_t c0, int nh, int64_t inc0,
+                                                int n_inc, const int4 *itab) {
+  LongFetch f{make_int4(0, 0, 0, 0), 0};
+  const int tid = threadIdx.x;
+  if (tid < nh) {
+    const int64_t t = c0 + tid;
+    const int4 *it = itab ? itab : aux->inc4 + inc0;
+    int lo = 0, hi = n_inc - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if ((int64_t)it[mid].x <= t) lo = mid;
+      else hi = mid - 1;
+    }
+    const int4 I = it[lo];
+    const int64_t rb = (int64_t)((uint64_t)(uint32_t)I.z | ((uint64_t)(uint32_t)I.w << 32));
+    f.rr = aux->rrec[rb + (t - (int64_t)(uint32_t)I.x)];
+    f.iy = I.y;
+  }
+  return f;
+}
+
+template <class SH>
+__device__ __forceinline__ int grp_tile_long(SH &sh, const LongFetch &F, int nh, int chunk, bool &clean) {
+  const int tid = threadIdx.x;
+  const FlatScope *sc = flat_scopes(sh);
+  int nck = 0;
+  bool dirty = false;
+  if (tid < nh) {
+    const int j = F.iy & 0xFFF;
+    const FlatScope S = sc[j];
+    const uint32_t z = (uint32_t)F.rr.z;
+    const int n = (int)((z >> 16) & kSegMaxLen), p = F.rr.y;
+    const int64_t r0 = (int64_t)(S.pk << 22) >> 22;
+    const uint64_t rf = (uint64_t)(r0 + p);
+    const uint32_t rz = (z & 0xFFu) | ((uint32_t)((rf >> 32) & 0xFF) << 8) | ((uint32_t)n << 16) | (z & (1u << 30)) |
+                        ((uint32_t)F.iy & kSegMine);
+    sh.rec[tid] = make_int4(F.rr.x, (int)(uint32_t)rf, (int)rz, (int)((uint32_t)j | ((uint32_t)(p - S.sstart) << 12)));
+    dirty = (S.pk >> 63) != 0;
+    nck = (n + chunk - 1) / chunk;
+  }
+  const unsigned long long dm = __ballot(dirty);
+  if ((tid & 63) == 0) sh.wdirty[tid >> 6] = dm != 0ull;
+  const int total = grp_tile_map(sh, nck);
+  int any = 0;
+#pragma unroll
+  for (int w = 0; w < kGrpThreads / 64; ++w) any |= sh.wdirty[w];
+  clean = any == 0;
+  return total;
+}
+
+template <int K, class SH>
+__device__ __forceinline__ void grp_scan_long(const GrpBatch &B, SH &sh, const GrpRange &R, const GrpGlobal &gg,
+                                              const GrpAux *__restrict__ aux, int64_t i_begin, int64_t i_end,
+                                              int64_t inc0, int n_inc, const int4 *itab, int skip) {
+  const int tid = threadIdx.x;
+  const auto tile_n = [&](int64_t c0) { return (int)((i_end - c0) < kGrpTile ? (i_end - c0) : kGrpTile); };
+  LongFetch next = i_begin < i_end ? long_fetch(aux, i_begin, tile_n(i_begin), inc0, n_inc, itab) : LongFetch{};
+  for (int64_t c0 = i_begin; c0 < i_end; c0 += kGrpTile) {
+    const int nh = tile_n(c0);
+    const LongFetch cur = next;
+    if (c0 + kGrpTile < i_end) next = long_fetch(aux, c0 + kGrpTile, tile_n(c0 + kGrpTile), inc0, n_inc, itab);
+    bool clean;
+    int total = grp_tile_long(sh, cur, nh, 16 * K, clean);
+    if (skip & kSkipChunks) total = 0;
+    if (clean && B.ref2) {
+      for (int t = tid; t < total; t += kGrpThreads) grp_chunk<K, true>(B, sh, R, gg, t, grp_find(sh, nh, total, t));
+    } else {
+      for (int t = tid; t < total; t += kGrpThreads) grp_chunk<K, false>(B, sh, R, gg, t, grp_find(sh, nh, total, t));
+    }
+    __syncthreads();
+  }
+}
+
 // Fused one-segment mode: the same stream over records made from incidences [i_begin, i_end) tile
 // by tile (grp_tile_flat), each tile through the 2-bit reference when all of its records allow.
 template <int K, class SH>
 __device__ __forceinline__ void grp_scan_flat(const GrpBatch &B, SH &sh, const GrpRange &R, const GrpGlobal &gg,
                                               const GrpAux *__restrict__ aux, int64_t i_begin, int64_t i_end,
-                                              int s_begin, int ns, bool first, int skip, int r_first) {
+                                              int s_begin, int ns, bool first, int skip) {
   const int tid = threadIdx.x;
   // each tile's incidence reads are loaded while the previous tile streams (one dependent load,
-  // the descriptor, left per tile); the first tile's by the caller
-  int r_next = r_first;
+  // the descriptor, left per tile); the first tile's by the caller (staged in sh.rec[tid].x)
+  int r_next = sh.rec[tid].x;
   for (int64_t c0 = i_begin; c0 < i_end; c0 += kGrpTile) {
     const int nh = (int)((i_end - c0) < kGrpTile ? (i_end - c0) : kGrpTile);
     const int r = r_next;
@@ -1080,8 +1167,9 @@ __device__ __forceinline__ void grp_patch_bytes(const GrpBatch &B, SH &sh, int n
 // only), {global region offset lo, hi, capacity, 0}, {piece B begin lo, hi, end lo, hi};
 // segments [seg_begin, seg_mid) have an all-ACGT reference range (2-bit reference).
 // FLAT: fused one-segment mode (records from incidences and read descriptors, grp_tile_flat; rec4
-// unused; group record 1's mid ignored).
-template <int U, bool FUSED, int OBS, bool FLAT>
+// unused; group record 1's mid ignored). LONG: long-read mode (records from the read records and
+// incidence records, grp_tile_long; rec4 unused).
+template <int U, bool FUSED, int OBS, bool FLAT, bool LONG = false>
 __global__ void __launch_bounds__(kGrpThreads, (OBS > 512 ? 4 : U == 1 ? 6 : U == 2 ? GANON_K2_BLOCKS : U == 4 ? 5 : 4)) k_group(const GrpBatch B, const int4 *__restrict__ groups,
                                                        const int4 *__restrict__ rec4,
                                                        uint8_t *__restrict__ out, const GrpAux *__restrict__ aux,
@@ -1123,14 +1211,30 @@ __global__ void __launch_bounds__(kGrpThreads, (OBS > 512 ? 4 : U == 1 ? 6 : U =
   // hides their latency)
   FlatScope fs{};
   int r_first = -1;
-  if constexpr (FLAT) {
+  int4 inc_rec{};   // (LONG) this thread's incidence record, staged after the scope table
+  const bool inc_lds = LONG && (s_end - s_begin) + g3.w <= kGrpMaxScopes;
+  if constexpr (FLAT || LONG) {
     if (tid < s_end - s_begin) fs = flat_load(B, aux, s_begin + tid, i_begin);
+  }
+  if constexpr (LONG) {
+    if (inc_lds && tid < g3.w) inc_rec = aux->inc4[i_mid + tid];
+  }
+  if constexpr (FLAT) {
     if (i_begin + tid < i_end) r_first = aux->incid_read[i_begin + tid];
   }
   if (FUSED && !(skip & kSkipCopy)) {
     copy_windows(B.seq, out, sink.p0, sink.p1, nt_copy);
     copy_windows(B.seq, out, sink.q0, sink.q1, nt_copy);
   }
+  // (staged for the first pass now: registers carried into the pass loop would stay live through
+  // the classification and spill)
+  if constexpr (FLAT || LONG) {
+    if (tid < s_end - s_begin) flat_scopes(sh)[tid] = fs;
+  }
+  if constexpr (LONG) {
+    if (inc_lds && tid < g3.w) reinterpret_cast<int4 *>(flat_scopes(sh) + (s_end - s_begin))[tid] = inc_rec;
+  }
+  if constexpr (FLAT) sh.rec[tid].x = r_first;   // (read by the first tile before it writes sh.rec)
   if (tid == 0) {
     sh.top = 0;
     sh.stk_lo[0] = 0ull;
@@ -1175,13 +1279,23 @@ __global__ void __launch_bounds__(kGrpThreads, (OBS > 512 ? 4 : U == 1 ? 6 : U =
     __syncthreads();
     if constexpr (FLAT) {
       // the scope table (patch list space: the previous pass's classification is done with it)
-      if (!first) {   // (loaded again: a pass after a key-range split)
-        if (tid < s_end - s_begin) fs = flat_load(B, aux, s_begin + opaque_tid(), i_begin);
-        r_first = i_begin + tid < i_end ? aux->incid_read[i_begin + opaque_tid()] : -1;
+      if (!first) {   // (staged again: a pass after a key-range split)
+        if (tid < s_end - s_begin) flat_scopes(sh)[tid] = flat_load(B, aux, s_begin + opaque_tid(), i_begin);
+        sh.rec[tid].x = i_begin + tid < i_end ? aux->incid_read[i_begin + opaque_tid()] : -1;
       }
-      if (tid < s_end - s_begin) flat_scopes(sh)[tid] = fs;
       __syncthreads();
-      grp_scan_flat<U>(B, sh, R, gg, aux, i_begin, i_end, s_begin, s_end - s_begin, first, skip, r_first);
+      grp_scan_flat<U>(B, sh, R, gg, aux, i_begin, i_end, s_begin, s_end - s_begin, first, skip);
+      first = false;
+    } else if constexpr (LONG) {
+      const int ns = s_end - s_begin;
+      int4 *itab = reinterpret_cast<int4 *>(flat_scopes(sh) + ns);
+      if (!first) {   // (staged again: a pass after a key-range split)
+        if (tid < ns) flat_scopes(sh)[tid] = flat_load(B, aux, s_begin + opaque_tid(), i_begin);
+        if (inc_lds && tid < g3.w) itab[tid] = aux->inc4[i_mid + opaque_tid()];
+      }
+      __syncthreads();
+      // (i_mid: the group's first incidence, g3.w: its incidence count)
+      grp_scan_long<U>(B, sh, R, gg, aux, i_begin, i_end, i_mid, g3.w, inc_lds ? itab : nullptr, skip);
       first = false;
     } else if (B.ref2) {
       grp_scan<U, true>(B, sh, R, gg, i_begin, i_mid, rec4, skip);
@@ -1507,7 +1621,8 @@ void free_batch(ganon_dbatch *db) {
                   &db->b_read_end, &db->b_wspart, &db->b_cursor, &db->b_gs0, &db->b_lo, &db->b_linemap, &db->b_groups,
                   &db->b_seg4, &db->b_grp_part, &db->b_far, &db->b_gokey, &db->b_gopay, &db->b_gtkey, &db->b_gtflag,
                   &db->b_out, &db->b_scope_calls, &db->b_scope_bases, &db->b_small, &db->b_part, &db->b_long, &db->b_nseg,
-                  &db->b_scost, &db->b_scan_tmp, &db->b_slots, &db->b_slot0, &db->b_order};
+                  &db->b_scost, &db->b_scan_tmp, &db->b_slots, &db->b_slot0, &db->b_order, &db->b_desc, &db->b_cand,
+                  &db->b_sdirty, &db->b_inc4, &db->b_rbase, &db->b_rrec};
   for (DBuf *b : bufs) free_buf(*b);
   free_huge(db);
   free_ref(db->own_ref);
@@ -1740,6 +1855,8 @@ int prepare(ganon_ctx *ctx, ganon_dbatch *db, const ganon_batch *host, bool allo
   a.incid_off = db->B.incid_off;
   a.ref_off = db->B.ref_off;
   a.sdirty = static_cast<const uint8_t *>(db->b_sdirty.p);
+  a.inc4 = static_cast<const int4 *>(db->b_inc4.p);
+  a.rrec = static_cast<const int4 *>(db->b_rrec.p);
   a.n_reads = db->n_reads;
   a.err = db->err;
   a.ws_part = static_cast<unsigned long long *>(db->b_wspart.p);
@@ -2108,6 +2225,10 @@ GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
                     ? (obs == 1024 ? (u == 1 ? k_group<1, true, 1024, true> : k_group<2, true, 1024, true>)
                                    : u == 2 ? k_group<2, true, 512, true> : u == 4 ? k_group<4, true, 512, true>
                                    : u == 8 ? k_group<8, true, 512, true> : k_group<1, true, 512, true>)
+                : db->long_mode
+                    ? (obs == 1024 ? (u == 1 ? k_group<1, true, 1024, false, true> : k_group<2, true, 1024, false, true>)
+                                   : u == 2 ? k_group<2, true, 512, false, true> : u == 4 ? k_group<4, true, 512, false, true>
+                                   : u == 8 ? k_group<8, true, 512, false, true> : k_group<1, true, 512, false, true>)
                     : (obs == 1024 ? (u == 1 ? k_group<1, true, 1024, false> : k_group<2, true, 1024, false>)
                                    : u == 2 ? k_group<2, true, 512, false> : u == 4 ? k_group<4, true, 512, false>
                                    : u == 8 ? k_group<8, true, 512, false> : k_group<1, true, 512, false>);

@@ -75,10 +75,13 @@ struct IndelObs {       // one I/D op of one incidence
   uint32_t ord;         // unfiltered slot: incidence order, then op order (registration order)
 };
 
-// Candidate map: 2 bits per genome position (bit 0: one read has an I/D op there, bit 1: two or
-// more). An observation at a position with bit 1 clear is alone at its (scope, position) in every
-// scope, so it cannot be part of a tumor AND normal call or change the rank of one: it is not
-// emitted (GANON_PARAM_INDEL_SORT 0).
+// Candidate map: 2 bits per genome position (bit 0: a tumor read has an I/D op there, bit 1: a
+// normal read has). A TN call at (scope, pos) needs a tumor and a normal read with an op at pos, so
+// a position missing either bit has no TN call in any scope; the other calls at such a position
+// only matter as the rank of a TN call there (registration order among the calls at pos), and
+// there is none. Its observations are not emitted (GANON_PARAM_INDEL_SORT 0); every observation
+// at a position with both bits is, so the ranks are those of the full tally. (Round 3 kept every
+// position two reads of any dataset shared: at C5's 5 % indel errors about twice as many.)
 
 
 // Sort keys. Segmented (default): one segment per scope, 32-bit key = segment parity << 31 |
@@ -142,26 +145,21 @@ __device__ __forceinline__ void walk_block(const GanonReadView &V, int r, int k0
   f(c);
 }
 
-// Candidate marking: one wave per block of a read with an I/D op (each read once, whatever its scopes).
+// Candidate marking: one wave per block of a read with an I/D op (each read once, whatever its
+// scopes): its dataset's bit at every op position (no-return atomics, nothing waits on them).
 __global__ void __launch_bounds__(kIndelThreads) k_indel_mark(const GanonReadView V, const IndelRead *__restrict__ reads,
                                                               int64_t n_reads, uint32_t *__restrict__ map) {
   const int lane = threadIdx.x & 63;
   const int64_t w = (int64_t)blockIdx.x * kIndelWaves + (threadIdx.x >> 6);
   if (w >= n_reads) return;
   const IndelRead e = reads[w];
+  const uint32_t ds = V.dataset[e.read] & 1u;
   walk_block(V, e.read, e.k0, e.pos0, 0, lane, [&](const CigarStep (&c)[kWalkJ]) {
-    uint32_t old[kWalkJ], bit[kWalkJ];
-    int64_t word[kWalkJ];
 #pragma unroll
     for (int j = 0; j < kWalkJ; ++j) {
       const int64_t g = e.cbase + c[j].pos;
-      word[j] = g >> 4;
-      bit[j] = 1u << (2 * (g & 15));
-      old[j] = c[j].is_id ? atomicOr(map + word[j], bit[j]) : 0u;
+      if (c[j].is_id) atomicOr(map + (g >> 4), 1u << (2 * (g & 15) + ds));
     }
-#pragma unroll
-    for (int j = 0; j < kWalkJ; ++j)
-      if (c[j].is_id && (old[j] & bit[j])) atomicOr(map + word[j], bit[j] << 1);
   });
 }
 
@@ -173,7 +171,7 @@ __device__ __forceinline__ void cand_bits(const uint32_t *__restrict__ map, int6
   for (int j = 0; j < kWalkJ; ++j) mw[j] = c[j].is_id ? map[(cbase + c[j].pos) >> 4] : 0u;
 #pragma unroll
   for (int j = 0; j < kWalkJ; ++j)
-    hit[j] = c[j].is_id && ((mw[j] >> (2 * ((cbase + c[j].pos) & 15) + 1)) & 1);
+    hit[j] = c[j].is_id && ((mw[j] >> (2 * ((cbase + c[j].pos) & 15))) & 3) == 3;   // tumor and normal
 }
 
 // Candidate observations per listed incidence (filtered emission slots come from their scan).

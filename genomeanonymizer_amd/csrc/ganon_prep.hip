@@ -1217,69 +1217,68 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_emit_flat(const Raw R, co
   }
 }
 
-// ---- long-read mode: one wave per incidence ---------------------------------------------------
-// A read with thousands of CIGAR ops (long reads with indel errors) walked by one thread is a
-// serial chain of dependent loads; here a wave walks it 64 ops at a time: per-lane query / reference
-// deltas, wave prefix sums for each op's (q, p), the read-length clip (ops at or past the read
-// length give nothing, as walk_segments stops there), per-lane segment pieces and a wave prefix of
-// the piece counts. The slots are deterministic: the incidence's records follow the group's
-// earlier incidences (k_prep_long_groups wrote each incidence's first slot from the segments per
-// read) in op order, so the walk needs no cursor and no atomics. A group all of whose records have
-// an all-ACGT reference range is read through the 2-bit reference by the group kernel (its clean
-// part is the whole range); a group with any other record is read through the nt16 reference (its
-// clean part is empty) — the wave that finds one flags the group.
-__device__ __forceinline__ void wave_walk(const Raw &R, int r, bool mine, int jl, int ss, int64_t r0ref,
-                                          const uint64_t *__restrict__ bad, int64_t n_blk, int64_t slot0,
-                                          unsigned long long *dirty, int4 *__restrict__ seg4) {
+// ---- long-read mode: segment records once per read -------------------------------------------
+// A 10-100 kb read with 5 % indel errors has thousands of aligned segments, and it sits in several
+// scopes (windows every 10 kb): round 3 wrote its records once per (scope, read) incidence, ~4x the
+// read's own (1.8 GB per C5 batch of 20 k reads), and the group kernel read them back. The records
+// do not depend on the scope except through its reference offset, span start and write mark, so
+// they are written once per read here (b_rrec, read records) and the group kernel adds those
+// fields when it stages a tile (grp_tile_long). One wave walks a read 64 CIGAR ops at a time:
+// per-lane query / reference deltas, wave prefix sums for each op's (q, p), the read-length clip
+// (ops at or past the read length give nothing, as walk_segments stops there), per-lane pieces of
+// kSegMaxLen and a wave prefix of the piece counts — deterministic slots from b_rbase (the
+// exclusive prefix of the segments per read), no atomics.
+__global__ void __launch_bounds__(kPrepThreads) k_prep_read_recs(const Raw R, const int64_t *__restrict__ rbase,
+                                                                 int4 *__restrict__ rrec) {
   const int lane = threadIdx.x & 63;
-  const int nc = R.n_cig[r], L = R.read_len[r];
-  const int64_t co = R.cig_off[r];
-  const uint32_t fl = ((uint32_t)R.dataset[r] << 30) | (mine ? kSegMine : 0u);
-  const int64_t qnib = 2 * R.seq_off[r];
-  int q = 0, p = R.ref_start[r];   // carries (wave-uniform)
-  int64_t slot = slot0;
-  bool any_dirty = false;
-  for (int base = 0; base < nc && q < L; base += 64) {
-    const int k = base + lane;
-    const uint32_t w = k < nc ? R.cigar[co + k] : 0u;
-    const int op = (int)(w & 0xF), len = (int)(w >> 4);
-    const bool al = is_aligned_op(op);
-    const int dq = (al || op == 1 || op == 4) ? len : 0;
-    const int dp = (al || op == 2 || op == 3) ? len : 0;
-    const int iq = ganon_wave::incl_sum(dq), ip = ganon_wave::incl_sum(dp);
-    const int q0 = q + iq - dq, p0 = p + ip - dp;
-    const int n = (al && q0 < L) ? min(len, L - q0) : 0;
-    const int c = (n + kSegMaxLen - 1) / kSegMaxLen;   // pieces
-    const int ic = ganon_wave::incl_sum(c);
-    int64_t pc = slot + ic - c;
-    for (int o = 0; o < n; o += kSegMaxLen) {
-      const int m = min(kSegMaxLen, n - o);
-      const uint64_t sq = (uint64_t)(qnib + q0 + o), rf = (uint64_t)(r0ref + p0 + o);
-      const uint32_t z = (uint32_t)((sq >> 32) & 0xFF) | ((uint32_t)((rf >> 32) & 0xFF) << 8) | ((uint32_t)m << 16) | fl;
-      seg4[pc++] = make_int4((int)(uint32_t)sq, (int)(uint32_t)rf, (int)z,
-                             (int)((uint32_t)jl | ((uint32_t)(p0 + o - ss) << 12)));
-      any_dirty |= !ref_clean(bad, n_blk, (int64_t)rf, m);
+  const int64_t nw = (int64_t)gridDim.x * kWaves;
+  for (int64_t r = (blockIdx.x * (int64_t)kPrepThreads + threadIdx.x) >> 6; r < R.n_reads; r += nw) {
+    const int nc = R.n_cig[r], L = R.read_len[r];
+    const int64_t co = R.cig_off[r];
+    const uint32_t fl = (uint32_t)R.dataset[r] << 30;
+    const int64_t qnib = 2 * R.seq_off[r];
+    int q = 0, p = R.ref_start[r];   // carries (wave-uniform)
+    int64_t slot = rbase[r];
+    for (int base = 0; base < nc && q < L; base += 64) {
+      const int k = base + lane;
+      const uint32_t w = k < nc ? R.cigar[co + k] : 0u;
+      const int op = (int)(w & 0xF), len = (int)(w >> 4);
+      const bool al = is_aligned_op(op);
+      const int dq = (al || op == 1 || op == 4) ? len : 0;
+      const int dp = (al || op == 2 || op == 3) ? len : 0;
+      const int iq = ganon_wave::incl_sum(dq), ip = ganon_wave::incl_sum(dp);
+      const int q0 = q + iq - dq, p0 = p + ip - dp;
+      const int n = (al && q0 < L) ? min(len, L - q0) : 0;
+      const int c = (n + kSegMaxLen - 1) / kSegMaxLen;   // pieces
+      const int ic = ganon_wave::incl_sum(c);
+      int64_t pc = slot + ic - c;
+      for (int o = 0; o < n; o += kSegMaxLen) {
+        const int m = min(kSegMaxLen, n - o);
+        const uint64_t sq = (uint64_t)(qnib + q0 + o);
+        rrec[pc++] = make_int4((int)(uint32_t)sq, p0 + o, (int)((uint32_t)((sq >> 32) & 0xFF) | ((uint32_t)m << 16) | fl), 0);
+      }
+      slot += ganon_wave::last(ic);
+      q += ganon_wave::last(iq);
+      p += ganon_wave::last(ip);
     }
-    slot += ganon_wave::last(ic);
-    q += ganon_wave::last(iq);
-    p += ganon_wave::last(ip);
   }
-  if (__any(any_dirty) && lane == 0) atomicOr(dirty, 1ull);
 }
 
-// Long-read mode, per group (thread per group): the record count from the segments per read (no
-// walk), the record range as k_prep_emit takes it, each incidence's first slot, the candidates,
-// group records 0 and 3, and the group's dirty flag reset. Long-read groups hold few incidences.
+// Long-read mode, per group (thread per group): each incidence's first slot in the group's slot
+// space (the segments of the group's earlier incidences; no walk: the segments per read), scope and
+// write mark and its read's record base (incidence records, b_inc4), the incidence checks, the
+// group records (slot range, first incidence and count, overflow region), the candidates, the
+// write-scope hash sum, and per scope whether its reference span holds a non-ACGT block.
+// Long-read groups hold few incidences.
 __global__ void __launch_bounds__(kPrepThreads) k_prep_long_groups(const Raw R, const longlong2 *__restrict__ gmeta,
                                                                    int n_groups, long long region_per_incid,
                                                                    const int32_t *__restrict__ nseg,
+                                                                   const int64_t *__restrict__ rbase,
                                                                    int4 *__restrict__ groups,
                                                                    unsigned long long *__restrict__ lo, LineMap M,
-                                                                   unsigned long long *__restrict__ cursor,
-                                                                   const unsigned long long *__restrict__ cursor_base,
-                                                                   unsigned long long *__restrict__ dirty,
-                                                                   int64_t *__restrict__ slot0, const Checks C,
-                                                                   int write) {
+                                                                   int4 *__restrict__ inc4, uint8_t *__restrict__ sdirty,
+                                                                   const uint64_t *__restrict__ bad, int64_t n_blk,
+                                                                   const Checks C) {
   for (int64_t g = blockIdx.x * (int64_t)kPrepThreads + threadIdx.x; g < n_groups;
        g += (int64_t)gridDim.x * kPrepThreads) {
     const longlong2 m0 = gmeta[g];
@@ -1288,35 +1287,23 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_long_groups(const Raw R, 
     const long long i0 = m0.y, i1 = m1.y;
     unsigned long long count = 0, mn[2] = {kNone, kNone}, hsum = 0;
     for (int s = s0; s < s1; ++s) {
-      const int ss = R.span_start[s], se = ss + R.span_len[s];
-      const bool big = R.span_len[s] > kGrpMaxSpan;   // huge scope: tile path
+      const int ss = R.span_start[s], sl = R.span_len[s], se = ss + sl;
+      const bool big = sl > kGrpMaxSpan;   // huge scope: tile path
+      sdirty[s] = !big && sl > 0 && !ref_clean(bad, n_blk, R.ref_off[s], sl);
       for (int64_t i = R.incid_off[s]; i < R.incid_off[s + 1]; ++i) {
         const int r = R.incid_read[i];
-        if (!incid_ok(R, C.read_end, C.err, i, s, r, ss, se)) continue;
-        if (R.write_scope[r] == s) hsum += ws_hash(r);
+        const bool ok = incid_ok(R, C.read_end, C.err, i, s, r, ss, se);
+        const bool mine = ok && R.write_scope[r] == s;
+        const int64_t rb = ok ? rbase[r] : 0;
+        inc4[i] = make_int4((int)count, (int)((uint32_t)(s - s0) | (mine ? kSegMine : 0u)), (int)(uint32_t)rb,
+                            (int)(uint32_t)((uint64_t)rb >> 32));
+        if (!ok) continue;
+        if (mine) hsum += ws_hash(r);
         if (big) continue;
         count += (unsigned long long)nseg[r];
-        if (R.write_scope[r] == s && R.read_len[r] > 0) {
+        if (mine && R.read_len[r] > 0) {
           const int d = R.dataset[r];
           mn[d] = min(mn[d], (unsigned long long)R.seq_off[r]);
-        }
-      }
-    }
-    int64_t seg_b = i0;
-    if ((long long)count > i1 - i0) {
-      const int k = (int)(g % kCursors);
-      seg_b = (int64_t)(R.n_incid + cursor_base[k] + atomicAdd(&cursor[k], count));
-    }
-    const int64_t seg_e = seg_b + (int64_t)count;
-    if (write) {
-      int64_t x = seg_b;
-      for (int s = s0; s < s1; ++s) {
-        if (R.span_len[s] > kGrpMaxSpan) continue;
-        const int ss = R.span_start[s], se = ss + R.span_len[s];
-        for (int64_t i = R.incid_off[s]; i < R.incid_off[s + 1]; ++i) {
-          const int r = R.incid_read[i];
-          slot0[i] = x;
-          if (r >= 0 && r < R.n_reads && R.ref_start[r] >= ss && C.read_end[r] <= se) x += nseg[r];
         }
       }
     }
@@ -1326,58 +1313,12 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_long_groups(const Raw R, 
     }
     const int64_t region = i0 * region_per_incid + (int64_t)kGrpObs * g;
     const int cap = (int)min((i1 - i0) * region_per_incid + kGrpObs, (long long)(INT32_MAX / 2));
-    groups[kGrpRec * g] = make_int4(s0, s1, (int)(uint32_t)seg_b, (int)(uint32_t)((uint64_t)seg_b >> 32));
-    groups[kGrpRec * g + 1] = make_int4((int)(uint32_t)seg_e, (int)(uint32_t)((uint64_t)seg_e >> 32), 0, 0);
-    groups[kGrpRec * g + 3] = make_int4((int)(uint32_t)region, (int)(uint32_t)((uint64_t)region >> 32), cap, 0);
-    dirty[g] = 0;
+    groups[kGrpRec * g] = make_int4(s0, s1, 0, 0);
+    groups[kGrpRec * g + 1] = make_int4((int)(uint32_t)count, (int)(uint32_t)(count >> 32), (int)(uint32_t)i0,
+                                        (int)(uint32_t)((uint64_t)i0 >> 32));
+    groups[kGrpRec * g + 3] = make_int4((int)(uint32_t)region, (int)(uint32_t)((uint64_t)region >> 32), cap,
+                                        (int)(i1 - i0));
     C.ws_part[g] = hsum;
-  }
-}
-
-// Long-read mode: the records, one wave per incidence over the whole batch (a long-read group holds
-// one or two incidences: waves per group would idle). The scope of incidence i by binary search in
-// the CSR offsets, its group in closed form (group_of).
-__global__ void __launch_bounds__(kPrepThreads) k_prep_emit_waves(const Raw R, const int64_t *__restrict__ cost,
-                                                                  long long target, const longlong2 *__restrict__ gmeta,
-                                                                  const uint64_t *__restrict__ bad, int64_t n_blk,
-                                                                  const int64_t *__restrict__ slot0,
-                                                                  unsigned long long *__restrict__ dirty,
-                                                                  const int32_t *__restrict__ read_end,
-                                                                  int4 *__restrict__ seg4) {
-  const int64_t nw = (int64_t)gridDim.x * kWaves;
-  for (int64_t i = blockIdx.x * (int64_t)kWaves + (threadIdx.x >> 6); i < R.n_incid; i += nw) {
-    int64_t a = 0, b = R.n_scopes - 1;   // last scope with incid_off[s] <= i
-    while (a < b) {
-      const int64_t mid = (a + b + 1) >> 1;
-      if (R.incid_off[mid] <= i) a = mid;
-      else b = mid - 1;
-    }
-    const int s = (int)a;
-    if (R.span_len[s] > kGrpMaxSpan) continue;
-    const int64_t g = group_of(R.incid_off, s, 0, target, cost);
-    const int r = R.incid_read[i];
-    // the incidence checks of k_prep_long_groups (reported there): skipped alike
-    if (r < 0 || r >= R.n_reads || R.ref_start[r] < R.span_start[s] || read_end[r] > R.span_start[s] + R.span_len[s])
-      continue;
-    wave_walk(R, r, R.write_scope[r] == s, s - (int)gmeta[g].x, R.span_start[s], R.ref_off[s] - R.span_start[s], bad,
-              n_blk, slot0[i], dirty + g, seg4);
-  }
-}
-
-// Long-read mode: each group's clean part (group record 1's mid): the whole range, or nothing.
-__global__ void __launch_bounds__(kPrepThreads) k_prep_long_mid(int n_groups, const unsigned long long *__restrict__ dirty,
-                                                                int4 *__restrict__ groups) {
-  for (int64_t g = blockIdx.x * (int64_t)kPrepThreads + threadIdx.x; g < n_groups;
-       g += (int64_t)gridDim.x * kPrepThreads) {
-    const int4 A = groups[kGrpRec * g];
-    const int4 Bq = groups[kGrpRec * g + 1];
-    if (dirty[g]) {   // mid = seg_b
-      groups[kGrpRec * g + 1].z = A.z;
-      groups[kGrpRec * g + 1].w = A.w;
-    } else {          // mid = seg_e
-      groups[kGrpRec * g + 1].z = Bq.x;
-      groups[kGrpRec * g + 1].w = Bq.y;
-    }
   }
 }
 
@@ -1475,22 +1416,17 @@ int launch_emit(ganon_ctx *ctx, ganon_dbatch *db, const Raw &R, int write) {
   if (!db->n_groups) return GANON_OK;
   KernelScope ks(ctx, "prep_emit");
   if (db->long_mode) {
-    const unsigned gg = grid_for(db->n_groups);
-    auto *dirty = static_cast<unsigned long long *>(db->b_slots.p);
-    auto *slot0 = static_cast<int64_t *>(db->b_slot0.p);
-    hipLaunchKernelGGL(k_prep_long_groups, dim3(gg), dim3(kPrepThreads), 0, ctx->stream, R,
+    // (write 0: the plan's counting pass is not needed in this mode)
+    if (!write) return GANON_OK;
+    hipLaunchKernelGGL(k_prep_long_groups, dim3(grid_for(db->n_groups)), dim3(kPrepThreads), 0, ctx->stream, R,
                        static_cast<const longlong2 *>(db->b_gs0.p), db->n_groups, (long long)db->region_per_incid,
-                       static_cast<const int32_t *>(db->b_nseg.p), static_cast<int4 *>(db->b_groups.p),
-                       static_cast<unsigned long long *>(db->b_lo.p), line_map(db), db->cursor, db->cursor + kCursors,
-                       dirty, slot0, checks_of(db), write);
-    if (write) {
-      hipLaunchKernelGGL(k_prep_emit_waves, dim3(grid_for(db->n_incid * 64)), dim3(kPrepThreads), 0, ctx->stream, R,
-                         db->scost, (long long)db->group_target, static_cast<const longlong2 *>(db->b_gs0.p),
-                         db->ref->bad, db->ref->n_blk, slot0, dirty, db->B.read_end, static_cast<int4 *>(db->b_seg4.p));
-      hipLaunchKernelGGL(k_prep_long_mid, dim3(gg), dim3(kPrepThreads), 0, ctx->stream, db->n_groups, dirty,
-                         static_cast<int4 *>(db->b_groups.p));
-    }
-    return check_launch(ctx, "k_prep_emit (long)");
+                       static_cast<const int32_t *>(db->b_nseg.p), static_cast<const int64_t *>(db->b_rbase.p),
+                       static_cast<int4 *>(db->b_groups.p), static_cast<unsigned long long *>(db->b_lo.p), line_map(db),
+                       static_cast<int4 *>(db->b_inc4.p), static_cast<uint8_t *>(db->b_sdirty.p), db->ref->bad,
+                       db->ref->n_blk, checks_of(db));
+    hipLaunchKernelGGL(k_prep_read_recs, dim3(grid_for(db->n_reads * 64)), dim3(kPrepThreads), 0, ctx->stream, R,
+                       static_cast<const int64_t *>(db->b_rbase.p), static_cast<int4 *>(db->b_rrec.p));
+    return check_launch(ctx, "k_prep_long_groups / k_prep_read_recs");
   }
   if (db->flat_mode) {
     auto flat = ctx->prep_unroll == 4 ? k_prep_emit_flat<4> : ctx->prep_unroll == 1 ? k_prep_emit_flat<1>
@@ -1684,9 +1620,10 @@ int size_plan(ganon_ctx *ctx, ganon_dbatch *db, int64_t ng, int tgt0, const Raw 
       (rc = grow_n(ctx, db->b_linemap, (size_t)line_map_words(db), &u64)))
     return rc;
   int64_t extra_seg = 0;
-  if (!db->flat_mode && ng) {
-    // two-pass and long-read emits: a counting pass sizes the records of groups with more segments
-    // than incidences (sub-counter bases: exclusive prefix of the pass's totals, deterministic)
+  if (!db->flat_mode && !db->long_mode && ng) {
+    // two-pass emit: a counting pass sizes the records of groups with more segments than
+    // incidences (sub-counter bases: exclusive prefix of the pass's totals, deterministic); the
+    // long-read mode keeps its records per read (b_rrec, sized by the plan)
     HIP_OR_FAIL(hipMemsetAsync(db->cursor + kCursors, 0, kCursors * sizeof(unsigned long long), st));
     if ((rc = launch_groups(ctx, db, R)) || (rc = launch_emit(ctx, db, R, 0))) return rc;
     std::vector<unsigned long long> cur(2 * kCursors, 0);
@@ -1702,7 +1639,7 @@ int size_plan(ganon_ctx *ctx, ganon_dbatch *db, int64_t ng, int tgt0, const Raw 
                                hipMemcpyHostToDevice, st));
     extra_seg = (int64_t)tseg;
   }
-  db->n_seg = db->n_incid + extra_seg;   // record slots: one per incidence, then the long groups
+  db->n_seg = db->long_mode ? db->n_long_seg : db->n_incid + extra_seg;   // record slots (long: virtual)
   db->region = db->n_incid * db->region_per_incid + (int64_t)kGrpObs * ng;
   // far masks (bytes a group masks outside its own pieces, applied by k_finish): the list keeps its
   // capacity across batches; a run that needs more reports the count (k_finish) and
@@ -1711,8 +1648,9 @@ int size_plan(ganon_ctx *ctx, ganon_dbatch *db, int64_t ng, int tgt0, const Raw 
                                              : std::min<int64_t>(kFarMax, std::max<int64_t>(int64_t(1) << 16, db->n_reads / 8));
   db->far_cap = std::max<int64_t>(db->far_cap_alloc, far_want);
   int4 *s4 = nullptr;
-  // (fused one-segment mode: no records in HBM)
-  if ((rc = grow_n(ctx, db->b_seg4, db->fused ? 1 : (size_t)std::max<int64_t>(db->n_seg, 1), &s4))) return rc;
+  // (fused one-segment and long-read modes: no per-incidence records in HBM)
+  if ((rc = grow_n(ctx, db->b_seg4, db->fused || db->long_mode ? 1 : (size_t)std::max<int64_t>(db->n_seg, 1), &s4)))
+    return rc;
   if ((rc = grow_n(ctx, db->b_far, (size_t)db->far_cap, &u64))) return rc;
   db->far_cap_alloc = db->far_cap;
   if ((rc = grow_n(ctx, db->b_gokey, (size_t)db->region, &u64)) || (rc = grow_n(ctx, db->b_gopay, (size_t)db->region, &u64)) ||
@@ -1882,20 +1820,34 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db, bool allow_spec) {
     if ((rc = grow_n(ctx, db->b_scost, (size_t)ns + 1, &cost))) return rc;
     hipLaunchKernelGGL(k_prep_scope_cost, dim3(grid_for(ns + 1)), dim3(kPrepThreads), 0, st, R, nseg, w, cost);
     if ((rc = check_launch(ctx, "k_prep_scope_cost"))) return rc;
-    size_t tb = 0;
+    // and the read records' bases (exclusive prefix of the segments per read, 64-bit)
+    int64_t *rbase = nullptr;
+    if ((rc = grow_n(ctx, db->b_rbase, (size_t)std::max<int64_t>(nr, 1), &rbase))) return rc;
+    size_t tb = 0, tb2 = 0;
     HIP_OR_FAIL(rocprim::exclusive_scan(nullptr, tb, cost, cost, (int64_t)0, (size_t)ns + 1, rocprim::plus<int64_t>(), st));
+    if (nr) HIP_OR_FAIL(rocprim::exclusive_scan(nullptr, tb2, nseg, rbase, (int64_t)0, (size_t)nr, rocprim::plus<int64_t>(), st));
+    tb = std::max(tb, tb2);
     void *tmp = nullptr;
     if ((rc = grow_n(ctx, db->b_scan_tmp, tb, reinterpret_cast<uint8_t **>(&tmp)))) return rc;
     HIP_OR_FAIL(rocprim::exclusive_scan(tmp, tb, cost, cost, (int64_t)0, (size_t)ns + 1, rocprim::plus<int64_t>(), st));
-    int64_t last = 0;
-    HIP_OR_FAIL(hipMemcpyAsync(&last, cost + ns - 1, sizeof last, hipMemcpyDeviceToHost, st));
+    int64_t last[2] = {0, 0}, rb_last = 0;   // the last scope's cost prefix, and the total
+    int32_t ns_last = 0;
+    HIP_OR_FAIL(hipMemcpyAsync(last, cost + ns - 1, sizeof last, hipMemcpyDeviceToHost, st));
+    if (nr) {
+      HIP_OR_FAIL(rocprim::exclusive_scan(tmp, tb, nseg, rbase, (int64_t)0, (size_t)nr, rocprim::plus<int64_t>(), st));
+      HIP_OR_FAIL(hipMemcpyAsync(&rb_last, rbase + nr - 1, sizeof rb_last, hipMemcpyDeviceToHost, st));
+      HIP_OR_FAIL(hipMemcpyAsync(&ns_last, nseg + nr - 1, sizeof ns_last, hipMemcpyDeviceToHost, st));
+    }
     HIP_OR_FAIL(hipStreamSynchronize(st));
     db->scost = cost;
-    ng = last / db->group_target + 1;
-    unsigned long long *sl = nullptr;
-    int64_t *s0p = nullptr;
-    if ((rc = grow_n(ctx, db->b_slots, (size_t)ng, &sl)) ||
-        (rc = grow_n(ctx, db->b_slot0, (size_t)std::max<int64_t>(db->n_incid, 1), &s0p)))
+    ng = last[0] / db->group_target + 1;
+    db->n_rrec = rb_last + ns_last;
+    db->n_long_seg = last[1] - w * ns;   // segments over the incidences (the group kernel's slots)
+    int4 *i4 = nullptr, *rr = nullptr;
+    uint8_t *sd = nullptr;
+    if ((rc = grow_n(ctx, db->b_inc4, (size_t)std::max<int64_t>(db->n_incid, 1), &i4)) ||
+        (rc = grow_n(ctx, db->b_rrec, (size_t)std::max<int64_t>(db->n_rrec, 1), &rr)) ||
+        (rc = grow_n(ctx, db->b_sdirty, (size_t)ns, &sd)))
       return rc;
   } else if (ns && db->group_target != tgt0) {
     return fail(ctx, GANON_E_STATE, "group target changed during the plan");

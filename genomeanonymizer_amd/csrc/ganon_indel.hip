@@ -13,11 +13,15 @@
 // Design: integer work, no MFMA. Observations are rare in short-read batches and
 // dense in long-read ones (5 % indel errors: ~10^8 per C5 batch), so the tally is a sort rather
 // than an LDS table:
-//   k_indel_emit      one wave per (scope, read) incidence with an I/D op; lanes take 64 CIGAR ops
-//                     at a time, wave prefix sums give each op its reference position and read
-//                     offset, I/D lanes write a 16-byte observation and a 32-bit sort key
-//                     (pos - span_start, plus the scope segment's parity in bit 31) at
-//                     ballot-compacted slots fixed at upload by a host scan (scope-major);
+//   candidates        (default) k_indel_mark sets a tumor / normal bit per genome position of every
+//                     read's I/D ops; k_indel_rcount + k_indel_remit walk each read once (a wave per
+//                     block of 256 CIGAR ops: lanes take 64 ops at a time, wave prefix sums give each
+//                     op its reference position and read offset) and list its ops at positions
+//                     with both bits (ballot-compacted, read-major);
+//   k_indel_expand    one wave per (scope, read) incidence: its read's candidates as 16-byte
+//                     observations with a 32-bit sort key (pos - span_start, plus the scope
+//                     segment's parity in bit 31), scope-major (GANON_PARAM_INDEL_SORT 1:
+//                     k_indel_emit walks every incidence and writes all its ops at the host's slots);
 //   radix sort        rocPRIM segmented pairs (key, observation index), one segment per scope
 //                     with observations, position bits only (GANON_PARAM_INDEL_SORT 1: one
 //                     global sort of 64-bit scope|position keys instead);
@@ -62,9 +66,21 @@ struct IndelInc {       // one block of one incidence with an I/D op (host plan)
   int64_t cbase;        // genome nibble index of the read's contig start (candidate map)
 };
 
-struct IndelRead {      // one block of one read with an I/D op (candidate marking)
-  int32_t read, k0, pos0, pad;
+struct IndelRead {      // one block of one read with an I/D op (candidate marking, per-read candidates)
+  int32_t read, k0, pos0, irp0;
+  int32_t nid0, pad;    // I/D ops of the read before the block
   int64_t cbase;
+};
+
+struct IndelIncR {      // one (scope, read) incidence with an I/D op (the filtered path, per incidence)
+  int32_t read;
+  uint32_t scope_par;   // scope | segment parity << 31
+  int32_t rfirst, rnb;  // the read's blocks in the read list (its candidates: rcand[roff[rfirst]..roff[rfirst + rnb]])
+  int64_t obs_base;     // the incidence's first unfiltered slot (registration order)
+};
+
+struct IndelCand {      // one candidate I/D op of a read (scope-free part of an observation)
+  int32_t pos, irp, type_len, ord;   // ord: the op's index among the read's I/D ops
 };
 
 struct IndelObs {       // one I/D op of one incidence
@@ -174,14 +190,54 @@ __device__ __forceinline__ void cand_bits(const uint32_t *__restrict__ map, int6
     hit[j] = c[j].is_id && ((mw[j] >> (2 * ((cbase + c[j].pos) & 15))) & 3) == 3;   // tumor and normal
 }
 
-// Candidate observations per listed incidence (filtered emission slots come from their scan).
-__global__ void __launch_bounds__(kIndelThreads) k_indel_count(const GanonReadView V, const IndelInc *__restrict__ list,
-                                                               int64_t n_list, const uint32_t *__restrict__ map,
-                                                               int32_t *__restrict__ cnt) {
+// The unfiltered path (GANON_PARAM_INDEL_SORT 1, one global sort): every I/D op of every listed
+// incidence block at the host's slots.
+template <typename KeyT>
+__global__ void __launch_bounds__(kIndelThreads) k_indel_emit(const GanonReadView V, const IndelInc *__restrict__ list,
+                                                              int64_t n_list, int pos_bits, IndelObs *__restrict__ obs,
+                                                              KeyT *__restrict__ keys, uint32_t *__restrict__ vals) {
   const int lane = threadIdx.x & 63;
   const int64_t w = (int64_t)blockIdx.x * kIndelWaves + (threadIdx.x >> 6);
   if (w >= n_list) return;
   const IndelInc e = list[w];
+  const int scope = (int)(e.scope_par & 0x7FFFFFFFu);
+  const int span0 = V.span_start[scope];
+  int64_t slot = e.obs_off;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  walk_block(V, e.read, e.k0, e.pos0, e.irp0, lane, [&](const CigarStep (&c)[kWalkJ]) {
+#pragma unroll
+    for (int j = 0; j < kWalkJ; ++j) {
+      const unsigned long long m = __ballot(c[j].is_id);
+      if (c[j].is_id) {
+        const int64_t o = slot + __popcll(m & below);
+        IndelObs ob;
+        ob.read = e.read;
+        ob.irp = c[j].irp;
+        ob.scope = scope;
+        ob.type_len = (c[j].len << 1) | (c[j].op == 1 ? 1 : 0);
+        ob.ord = (uint32_t)o;
+        obs[o] = ob;
+        keys[o] = make_key<KeyT>(e.scope_par, pos_bits, (uint32_t)(c[j].pos - span0));
+        vals[o] = (uint32_t)o;
+      }
+      slot += __popcll(m);
+    }
+  });
+}
+
+// ---- filtered path, per read (round 4) -------------------------------------------------------
+// A read's candidate ops (those at positions where a tumor and a normal read have an I/D op) do not
+// depend on the scope: they are found once per read block (k_indel_rcount / k_indel_remit, the
+// CIGAR walked twice per read instead of twice per (scope, read) incidence, ~4 per C5 read) into a
+// read-major candidate list, and every incidence's observations are a coalesced copy of its read's
+// entries with the scope's key (k_indel_expand).
+__global__ void __launch_bounds__(kIndelThreads) k_indel_rcount(const GanonReadView V, const IndelRead *__restrict__ reads,
+                                                                int64_t n_reads, const uint32_t *__restrict__ map,
+                                                                int32_t *__restrict__ cnt) {
+  const int lane = threadIdx.x & 63;
+  const int64_t w = (int64_t)blockIdx.x * kIndelWaves + (threadIdx.x >> 6);
+  if (w >= n_reads) return;
+  const IndelRead e = reads[w];
   int total = 0;
   walk_block(V, e.read, e.k0, e.pos0, e.irp0, lane, [&](const CigarStep (&c)[kWalkJ]) {
     bool hit[kWalkJ];
@@ -192,49 +248,70 @@ __global__ void __launch_bounds__(kIndelThreads) k_indel_count(const GanonReadVi
   if (lane == 0) cnt[w] = total;
 }
 
-// FILTER: slots from the candidate scan (off[w]), only candidate ops; else the host's slots.
-template <typename KeyT, bool FILTER>
-__global__ void __launch_bounds__(kIndelThreads) k_indel_emit(const GanonReadView V, const IndelInc *__restrict__ list,
-                                                              int64_t n_list, int pos_bits, const uint32_t *__restrict__ map,
-                                                              const int32_t *__restrict__ off, IndelObs *__restrict__ obs,
-                                                              KeyT *__restrict__ keys, uint32_t *__restrict__ vals) {
+__global__ void __launch_bounds__(kIndelThreads) k_indel_remit(const GanonReadView V, const IndelRead *__restrict__ reads,
+                                                               int64_t n_reads, const uint32_t *__restrict__ map,
+                                                               const int32_t *__restrict__ roff,
+                                                               IndelCand *__restrict__ rcand) {
   const int lane = threadIdx.x & 63;
   const int64_t w = (int64_t)blockIdx.x * kIndelWaves + (threadIdx.x >> 6);
-  if (w >= n_list) return;
-  const IndelInc e = list[w];
-  const int scope = (int)(e.scope_par & 0x7FFFFFFFu);
-  const int span0 = V.span_start[scope];
-  int64_t slot = FILTER ? (int64_t)off[w] : e.obs_off;
-  int64_t ord = e.obs_off;
+  if (w >= n_reads) return;
+  const IndelRead e = reads[w];
+  int64_t slot = roff[w];
+  int ord = e.nid0;
   const unsigned long long below = (1ull << lane) - 1ull;
   walk_block(V, e.read, e.k0, e.pos0, e.irp0, lane, [&](const CigarStep (&c)[kWalkJ]) {
     bool keep[kWalkJ];
-    if (FILTER) {
-      cand_bits(map, e.cbase, c, keep);
-    } else {
-#pragma unroll
-      for (int j = 0; j < kWalkJ; ++j) keep[j] = c[j].is_id;
-    }
+    cand_bits(map, e.cbase, c, keep);
 #pragma unroll
     for (int j = 0; j < kWalkJ; ++j) {
       const unsigned long long m_all = __ballot(c[j].is_id);
       const unsigned long long m = __ballot(keep[j]);
-      if (keep[j]) {
-        const int64_t o = slot + __popcll(m & below);
-        IndelObs ob;
-        ob.read = e.read;
-        ob.irp = c[j].irp;
-        ob.scope = scope;
-        ob.type_len = (c[j].len << 1) | (c[j].op == 1 ? 1 : 0);
-        ob.ord = (uint32_t)(ord + __popcll(m_all & below));
-        obs[o] = ob;
-        keys[o] = make_key<KeyT>(e.scope_par, pos_bits, (uint32_t)(c[j].pos - span0));
-        vals[o] = (uint32_t)o;
-      }
+      if (keep[j])
+        rcand[slot + __popcll(m & below)] = IndelCand{c[j].pos, c[j].irp, (c[j].len << 1) | (c[j].op == 1 ? 1 : 0),
+                                                      ord + (int)__popcll(m_all & below)};
       slot += __popcll(m);
       ord += __popcll(m_all);
     }
   });
+}
+
+// Observations per incidence: its read's candidates (thread per incidence).
+__global__ void k_indel_icount(const IndelIncR *__restrict__ inc, int64_t n_inc, const int32_t *__restrict__ roff,
+                               int32_t *__restrict__ cnt) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= n_inc) return;
+  const IndelIncR e = inc[i];
+  cnt[i] = roff[e.rfirst + e.rnb] - roff[e.rfirst];
+}
+
+// One wave per incidence: its read's candidate entries with the scope's key, 64 at a time.
+template <typename KeyT>
+__global__ void __launch_bounds__(kIndelThreads) k_indel_expand(const GanonReadView V, const IndelIncR *__restrict__ inc,
+                                                                int64_t n_inc, int pos_bits,
+                                                                const int32_t *__restrict__ roff,
+                                                                const IndelCand *__restrict__ rcand,
+                                                                const int32_t *__restrict__ off, IndelObs *__restrict__ obs,
+                                                                KeyT *__restrict__ keys, uint32_t *__restrict__ vals) {
+  const int lane = threadIdx.x & 63;
+  const int64_t w = (int64_t)blockIdx.x * kIndelWaves + (threadIdx.x >> 6);
+  if (w >= n_inc) return;
+  const IndelIncR e = inc[w];
+  const int scope = (int)(e.scope_par & 0x7FFFFFFFu);
+  const int span0 = V.span_start[scope];
+  const int64_t a = roff[e.rfirst], n = roff[e.rfirst + e.rnb] - a, o0 = off[w];
+  for (int64_t k = lane; k < n; k += 64) {
+    const IndelCand c = rcand[a + k];
+    const int64_t o = o0 + k;
+    IndelObs ob;
+    ob.read = e.read;
+    ob.irp = c.irp;
+    ob.scope = scope;
+    ob.type_len = c.type_len;
+    ob.ord = (uint32_t)(e.obs_base + c.ord);
+    obs[o] = ob;
+    keys[o] = make_key<KeyT>(e.scope_par, pos_bits, (uint32_t)(c.pos - span0));
+    vals[o] = (uint32_t)o;
+  }
 }
 
 // Segment offsets of the filtered observations: seg_off[k] = off[first listed incidence of k].
@@ -474,9 +551,15 @@ struct ganon_indels {
   IndelRead *rdist = nullptr;         // distinct reads with an I/D op (candidate marking)
   uint32_t *map = nullptr;            // candidate map, 2 bits per genome position
   int64_t map_words = 0;
-  int32_t *cnt = nullptr;             // [n_list + 1] candidate observations per listed incidence
-  int32_t *off = nullptr;             // [n_list + 1] their exclusive scan; off[n_list] = count
-  int32_t *seg_first = nullptr;       // [n_seg + 1] first listed incidence of each segment
+  int32_t *cnt = nullptr;             // [n_list + 1] candidate observations per incidence (ilist)
+  int32_t *off = nullptr;             // [n_list + 1] their exclusive scan; off[n_ilist] = count
+  IndelIncR *ilist = nullptr;         // incidences with an I/D op (filtered path)
+  int64_t n_ilist = 0;
+  int32_t *rcnt = nullptr;            // [n_rdist + 1] candidates per read block, then their scan (roff)
+  int32_t *roff = nullptr;
+  IndelCand *rcand = nullptr;         // the reads' candidate ops, read-major
+  int64_t n_rcand_cap = 0;
+  int32_t *seg_first = nullptr;       // [n_seg + 1] first ilist incidence of each segment
   int32_t *seg_off = nullptr;         // [n_seg + 1] observation offsets of the segments
   int32_t *nval = nullptr;            // [1] n_obs (unfiltered runs)
   IndelObs *obs = nullptr;
@@ -494,7 +577,7 @@ struct ganon_indels {
   ganon_indel_rec *recs = nullptr;
   int64_t recs_cap = 0;
   bool ran = false;
-  const int32_t *n_dev() const { return global ? nval : off + n_list; }
+  const int32_t *n_dev() const { return global ? nval : off + n_ilist; }
 };
 
 namespace {
@@ -535,7 +618,12 @@ hipError_t sort_pairs(ganon_indels *t, void *temp, size_t &bytes, bool global, h
 }
 
 hipError_t scan_counts(ganon_indels *t, void *temp, size_t &bytes, hipStream_t st) {
-  return rocprim::exclusive_scan(temp, bytes, t->cnt, t->off, 0, (size_t)(t->n_list + 1), rocprim::plus<int32_t>(),
+  return rocprim::exclusive_scan(temp, bytes, t->cnt, t->off, 0, (size_t)(t->n_ilist + 1), rocprim::plus<int32_t>(),
+                                 st);
+}
+
+hipError_t scan_read_counts(ganon_indels *t, void *temp, size_t &bytes, hipStream_t st) {
+  return rocprim::exclusive_scan(temp, bytes, t->rcnt, t->roff, 0, (size_t)(t->n_rdist + 1), rocprim::plus<int32_t>(),
                                  st);
 }
 
@@ -547,14 +635,23 @@ int run_tally(ganon_ctx *ctx, ganon_indels *t) {
   const unsigned lgrid = (unsigned)((t->n_list + kIndelWaves - 1) / kIndelWaves);
   HIP_OR_FAIL(hipMemsetAsync(t->counters, 0, 2 * sizeof(unsigned long long), ctx->stream));
   HIP_OR_FAIL(hipMemsetAsync(t->run_count, 0, sizeof(unsigned int), ctx->stream));
+  const unsigned rgrid = (unsigned)((t->n_rdist + kIndelWaves - 1) / kIndelWaves);
   if (filter) {
+    // per read block: the map, then its candidate ops (count, scan, list); per incidence: counts
+    // from the read's, their scan, the segments
     KernelScope ks(ctx, "indel_candidates");
     HIP_OR_FAIL(hipMemsetAsync(t->map, 0, (size_t)t->map_words * 4, ctx->stream));
-    hipLaunchKernelGGL(k_indel_mark, dim3((unsigned)((t->n_rdist + kIndelWaves - 1) / kIndelWaves)),
-                       dim3(kIndelThreads), 0, ctx->stream, t->V, t->rdist, t->n_rdist, t->map);
-    hipLaunchKernelGGL(k_indel_count, dim3(lgrid), dim3(kIndelThreads), 0, ctx->stream, t->V, t->list, t->n_list,
-                       t->map, t->cnt);
+    hipLaunchKernelGGL(k_indel_mark, dim3(rgrid), dim3(kIndelThreads), 0, ctx->stream, t->V, t->rdist, t->n_rdist, t->map);
+    hipLaunchKernelGGL(k_indel_rcount, dim3(rgrid), dim3(kIndelThreads), 0, ctx->stream, t->V, t->rdist, t->n_rdist,
+                       t->map, t->rcnt);
     size_t bytes = t->temp_bytes;
+    if (scan_read_counts(t, t->temp, bytes, ctx->stream) != hipSuccess)
+      return fail(ctx, GANON_E_DEVICE, "indel read scan failed");
+    hipLaunchKernelGGL(k_indel_remit, dim3(rgrid), dim3(kIndelThreads), 0, ctx->stream, t->V, t->rdist, t->n_rdist,
+                       t->map, t->roff, t->rcand);
+    hipLaunchKernelGGL(k_indel_icount, dim3((unsigned)((t->n_ilist + 255) / 256)), dim3(256), 0, ctx->stream, t->ilist,
+                       t->n_ilist, t->roff, t->cnt);
+    bytes = t->temp_bytes;
     if (scan_counts(t, t->temp, bytes, ctx->stream) != hipSuccess) return fail(ctx, GANON_E_DEVICE, "indel scan failed");
     hipLaunchKernelGGL(k_indel_segs, dim3((unsigned)((t->n_seg + 256) / 256)), dim3(256), 0, ctx->stream,
                        t->seg_first, t->n_seg, t->off, t->seg_off);
@@ -563,11 +660,12 @@ int run_tally(ganon_ctx *ctx, ganon_indels *t) {
   {
     KernelScope ks(ctx, "k_indel_emit");
     if (filter)
-      hipLaunchKernelGGL((k_indel_emit<KeyT, true>), dim3(lgrid), dim3(kIndelThreads), 0, ctx->stream, t->V, t->list,
-                         t->n_list, t->pos_bits, t->map, t->off, t->obs, static_cast<KeyT *>(t->keys[0]), t->vals[0]);
+      hipLaunchKernelGGL(k_indel_expand<KeyT>, dim3((unsigned)((t->n_ilist + kIndelWaves - 1) / kIndelWaves)),
+                         dim3(kIndelThreads), 0, ctx->stream, t->V, t->ilist, t->n_ilist, t->pos_bits, t->roff, t->rcand,
+                         t->off, t->obs, static_cast<KeyT *>(t->keys[0]), t->vals[0]);
     else
-      hipLaunchKernelGGL((k_indel_emit<KeyT, false>), dim3(lgrid), dim3(kIndelThreads), 0, ctx->stream, t->V, t->list,
-                         t->n_list, t->pos_bits, t->map, t->off, t->obs, static_cast<KeyT *>(t->keys[0]), t->vals[0]);
+      hipLaunchKernelGGL(k_indel_emit<KeyT>, dim3(lgrid), dim3(kIndelThreads), 0, ctx->stream, t->V, t->list, t->n_list,
+                         t->pos_bits, t->obs, static_cast<KeyT *>(t->keys[0]), t->vals[0]);
     if ((rc = check_launch(ctx, "k_indel_emit"))) return rc;
   }
   {
@@ -642,39 +740,48 @@ GANON_API int ganon_indel_upload(ganon_ctx *ctx, const ganon_batch *b, const gan
     const Blk &x = blks[(size_t)(blk_of[r] + i)];
     return (i + 1 < n_blk(r) ? blks[(size_t)(blk_of[r] + i + 1)].nid0 : nid[r]) - x.nid0;
   };
-  std::vector<IndelInc> list;
+  std::vector<IndelInc> list;            // per incidence block (the unfiltered global-sort path)
+  std::vector<IndelIncR> ilist;          // per incidence (the filtered path)
   std::vector<IndelRead> rdist;          // each read with an I/D op once (first incidence's contig)
-  std::vector<uint8_t> seen(b->n_reads, 0);
-  std::vector<int32_t> seg_first;        // first list entry of each segment, then the list size
-  int64_t n_obs = 0;
+  std::vector<int32_t> rfirst(b->n_reads, -1), rnb(b->n_reads, 0);   // a read's blocks in rdist
+  std::vector<int32_t> seg_first;        // first ilist entry of each segment, then the list size
+  int64_t n_obs = 0, n_rcand = 0;
   int32_t max_span = 0;
   for (int32_t s = 0; s < b->n_scopes; ++s) {
     max_span = std::max(max_span, b->scope_span_len[s]);
     const uint32_t par = (uint32_t)(seg_first.size() & 1) << 31;
     const int64_t cbase = b->scope_ref_off[s] - b->scope_span_start[s];   // contig start, genome nibbles
-    const size_t before = list.size();
+    const size_t before = ilist.size();
     for (int64_t i = b->scope_incid_off[s]; i < b->scope_incid_off[s + 1]; ++i) {
       const int32_t r = b->incid_read[i];
       if (!nid[r]) continue;
+      const bool first = rfirst[r] < 0;
+      if (first) rfirst[r] = (int32_t)rdist.size();
       for (int k = 0; k < n_blk(r); ++k) {
         const int ids = blk_ids(r, k);
         if (!ids) continue;
         const Blk &x = blks[(size_t)(blk_of[r] + k)];
         list.push_back(IndelInc{r, (uint32_t)s | par, x.k0, x.pos0, x.irp0, 0, n_obs + x.nid0, cbase});
-        if (!seen[r]) rdist.push_back(IndelRead{r, x.k0, x.pos0, 0, cbase});
+        if (first) {
+          rdist.push_back(IndelRead{r, x.k0, x.pos0, x.irp0, x.nid0, 0, cbase});
+          ++rnb[r];
+        }
       }
-      seen[r] = 1;
+      if (first) n_rcand += nid[r];
+      ilist.push_back(IndelIncR{r, (uint32_t)s | par, rfirst[r], rnb[r], n_obs});
       n_obs += nid[r];
     }
-    if (list.size() > before) seg_first.push_back((int32_t)before);
+    if (ilist.size() > before) seg_first.push_back((int32_t)before);
   }
-  seg_first.push_back((int32_t)list.size());
+  seg_first.push_back((int32_t)ilist.size());
   if (n_obs >= (int64_t)INT32_MAX) return fail(ctx, GANON_E_ARG, "indel upload: %lld observations (max 2^31-1)", (long long)n_obs);
   ganon_indels *t = new ganon_indels();
   t->V = V;
   t->n_obs = n_obs;
   t->n_list = (int64_t)list.size();
+  t->n_ilist = (int64_t)ilist.size();
   t->n_rdist = (int64_t)rdist.size();
+  t->n_rcand_cap = n_rcand;
   t->n_seg = (int32_t)seg_first.size() - 1;
   t->pos_bits = bits_for((int64_t)max_span);
   t->key_bits = t->pos_bits + bits_for(std::max<int64_t>((int64_t)b->n_scopes - 1, 1));
@@ -692,6 +799,10 @@ GANON_API int ganon_indel_upload(ganon_ctx *ctx, const ganon_batch *b, const gan
     if ((rc = ind_alloc(ctx, t, &t->map, (size_t)t->map_words))) return bail(rc);
     if ((rc = ind_alloc(ctx, t, &t->cnt, list.size() + 1))) return bail(rc);
     if ((rc = ind_alloc(ctx, t, &t->off, list.size() + 1))) return bail(rc);
+    if ((rc = ind_alloc(ctx, t, &t->ilist, ilist.size()))) return bail(rc);
+    if ((rc = ind_alloc(ctx, t, &t->rcnt, rdist.size() + 1))) return bail(rc);
+    if ((rc = ind_alloc(ctx, t, &t->roff, rdist.size() + 1))) return bail(rc);
+    if ((rc = ind_alloc(ctx, t, &t->rcand, (size_t)n_rcand))) return bail(rc);
     if ((rc = ind_alloc(ctx, t, &t->seg_first, seg_first.size()))) return bail(rc);
     if ((rc = ind_alloc(ctx, t, &t->seg_off, seg_first.size()))) return bail(rc);
     if ((rc = ind_alloc(ctx, t, &t->nval, 1))) return bail(rc);
@@ -707,22 +818,26 @@ GANON_API int ganon_indel_upload(ganon_ctx *ctx, const ganon_batch *b, const gan
     if ((rc = ind_alloc(ctx, t, &t->run_list, (size_t)n_obs / 2 + 1))) return bail(rc);
     if ((rc = ind_alloc(ctx, t, &t->run_count, 1))) return bail(rc);
     // temp storage: the largest of the two sorts and the count scan
-    size_t seg_bytes = 0, glob_bytes = 0, scan_bytes = 0;
+    size_t seg_bytes = 0, glob_bytes = 0, scan_bytes = 0, rscan_bytes = 0;
     if (sort_pairs<uint32_t>(t, nullptr, seg_bytes, false, ctx->stream, nullptr) != hipSuccess ||
         sort_pairs<unsigned long long>(t, nullptr, glob_bytes, true, ctx->stream, nullptr) != hipSuccess ||
-        scan_counts(t, nullptr, scan_bytes, ctx->stream) != hipSuccess)
+        scan_counts(t, nullptr, scan_bytes, ctx->stream) != hipSuccess ||
+        scan_read_counts(t, nullptr, rscan_bytes, ctx->stream) != hipSuccess)
       return bail(fail(ctx, GANON_E_DEVICE, "indel upload: radix sort / scan sizing failed"));
-    t->temp_bytes = std::max(std::max(seg_bytes, glob_bytes), scan_bytes);
+    t->temp_bytes = std::max(std::max(seg_bytes, glob_bytes), std::max(scan_bytes, rscan_bytes));
     if ((rc = ind_alloc(ctx, t, reinterpret_cast<uint8_t **>(&t->temp), t->temp_bytes))) return bail(rc);
     const int32_t nv = (int32_t)n_obs;
     hipError_t e = hipMemcpyAsync(t->list, list.data(), list.size() * sizeof(IndelInc), hipMemcpyHostToDevice, ctx->stream);
     if (e == hipSuccess)
       e = hipMemcpyAsync(t->rdist, rdist.data(), rdist.size() * sizeof(IndelRead), hipMemcpyHostToDevice, ctx->stream);
     if (e == hipSuccess)
+      e = hipMemcpyAsync(t->ilist, ilist.data(), ilist.size() * sizeof(IndelIncR), hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess)
       e = hipMemcpyAsync(t->seg_first, seg_first.data(), seg_first.size() * sizeof(int32_t), hipMemcpyHostToDevice,
                          ctx->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(t->nval, &nv, sizeof nv, hipMemcpyHostToDevice, ctx->stream);
-    if (e == hipSuccess) e = hipMemsetAsync(t->cnt + list.size(), 0, sizeof(int32_t), ctx->stream);   // scan tail
+    if (e == hipSuccess) e = hipMemsetAsync(t->cnt + ilist.size(), 0, sizeof(int32_t), ctx->stream);   // scan tails
+    if (e == hipSuccess) e = hipMemsetAsync(t->rcnt + rdist.size(), 0, sizeof(int32_t), ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     if (e != hipSuccess) return bail(fail(ctx, GANON_E_DEVICE, "indel upload copy failed: %s", hipGetErrorString(e)));
   }

@@ -18,7 +18,7 @@ def main():
     a = argparse.Namespace(config="c2", reads=None, genome=None, windows=None, germline=None)
     for k, v in bench.CONFIGS["c2"]["defaults"].items():
         setattr(a, k, v)
-    arr, info = bench.make_batch(a, 0)
+    arr, info = bench.make_batch(a, 0, 0)
     m = native.HipMasker(0)
     torch.cuda.set_device(0)
     m.set_stream(torch.cuda.current_stream().cuda_stream)

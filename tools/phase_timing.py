@@ -34,7 +34,7 @@ def main():
     for k, v in bench.CONFIGS[args.config]["defaults"].items():
         if getattr(args, k) is None:
             setattr(args, k, v)
-    arr, info = bench.make_batch(args, 0)
+    arr, info = bench.make_batch(args, 0, 0)
     m = native.HipMasker(0)
     cfgs = []
     for c in args.configs.split(","):

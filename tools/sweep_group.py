@@ -23,7 +23,7 @@ def main():
     cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
     args = argparse.Namespace(config=cfg, **bench.CONFIGS[cfg]["defaults"])
-    arr, _ = bench.make_batch(args, 0)
+    arr, _ = bench.make_batch(args, 0, 0)
     m = native.HipMasker(0)
     ref = m.upload_reference(arr["ref_nt16"])
     mode = sys.argv[3] if len(sys.argv) > 3 else "grid"

@@ -155,6 +155,7 @@ struct ScanOut {
   int64_t g_bound;            // group count bound: (n_incid + weight (n_scopes - 1)) / target + 1
   unsigned long long *part;   // [kParts][part_stride]: partial k of block b at part[k * part_stride + b]
   int64_t part_stride;
+  int32_t *nseg;              // k_prep_scan_long: aligned segments of each long read (long-read mode), or null
   int4 *desc;                 // fused one-segment mode: [n_reads] read descriptors (ganon_batch.h), or null
   unsigned long long *cand;   // and [2 g_bound] partition candidates: ~(lowest written offset), atomicMax
 };
@@ -446,6 +447,7 @@ __global__ void __launch_bounds__(kPrepThreads) k_prep_scan_long(const Raw R, Pr
       report(err, kErrReadPos, r);
     } else {
       O.read_end[r] = (int32_t)(rs_ + (W.rl > 0 ? W.rl : 1));
+      if (O.nseg) O.nseg[r] = W.ns;   // (the long-read mode's segments per read: no second walk)
       acc[kPartMaxSeg] = max(acc[kPartMaxSeg], (unsigned long long)W.ns);
       acc[kPartIdOps] += (unsigned long long)W.nid;
     }
@@ -529,12 +531,26 @@ __device__ __forceinline__ int lds_upper(const long long *off, int n, long long 
 }
 
 // Long-read mode only: aligned segments per read (walk_segments' cuts), for the segment-weighted
-// groups and the record slots; one wave per read (wave_cigar_walk).
+// groups and the record slots — the reads of at most kScanLongCigar ops, a thread each
+// (k_prep_scan_long wrote the long reads' counts during its walk).
 __global__ void __launch_bounds__(kPrepThreads) k_prep_nseg(const Raw R, int32_t *__restrict__ nseg) {
-  const int64_t n_waves = (int64_t)gridDim.x * (kPrepThreads / 64);
-  for (int64_t r = (blockIdx.x * (int64_t)kPrepThreads + threadIdx.x) >> 6; r < R.n_reads; r += n_waves) {
-    const CigarWalk W = wave_cigar_walk(R.cigar + R.cig_off[r], R.n_cig[r], R.read_len[r]);
-    if ((threadIdx.x & 63) == 0) nseg[r] = W.ns;
+  for (int64_t r = blockIdx.x * (int64_t)kPrepThreads + threadIdx.x; r < R.n_reads; r += (int64_t)gridDim.x * kPrepThreads) {
+    const int nc = R.n_cig[r];
+    if (nc > kScanLongCigar) continue;
+    const int L = R.read_len[r];
+    const uint32_t *cg = R.cigar + R.cig_off[r];
+    int q = 0, ns = 0;
+    for (int k = 0; k < nc && q < L; ++k) {
+      const uint32_t w = cg[k];
+      const int op = (int)(w & 0xF), len = (int)(w >> 4);
+      if (is_aligned_op(op)) {
+        ns += (min(len, L - q) + kSegMaxLen - 1) / kSegMaxLen;
+        q += len;
+      } else if (op == 1 || op == 4) {
+        q += len;
+      }
+    }
+    nseg[r] = ns;
   }
 }
 
@@ -1730,7 +1746,7 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db, bool allow_spec) {
   db->cand = cand;
   unsigned int *long_count = db->long_count;
   const int64_t pstride = nb + kLongGrid;
-  const ScanOut O{read_end, long_list, long_count, gm, g_bound, part, pstride, desc, cand};
+  const ScanOut O{read_end, long_list, long_count, gm, g_bound, part, pstride, nullptr, desc, cand};
   {
     // 1. the batch scan: every per-read and per-scope check, read ends, the group table of the
     //    short-read modes, per-block partials; then their reduction
@@ -1776,6 +1792,7 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db, bool allow_spec) {
     const unsigned gl = (unsigned)std::min<int64_t>(kLongGrid, ((int64_t)n_long + 3) / 4);
     ScanOut OL = O;
     OL.part = part + nb;   // (blocks nb.. of every kind)
+    if ((rc = grow_n(ctx, db->b_nseg, (size_t)std::max<int64_t>(nr, 1), &OL.nseg))) return rc;
     hipLaunchKernelGGL(k_prep_scan_long, dim3(gl), dim3(kPrepThreads), 0, st, R, db->err, OL, (int)n_long);
     hipLaunchKernelGGL(k_prep_reduce, dim3(1), dim3(kReduceThreads), 0, st, R, part, pstride, (int)(nb + gl), w0,
                        (long long)tgt0, g_bound, db->plan_info, static_cast<const PrepErr *>(db->err), 0ll,
@@ -1815,7 +1832,8 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db, bool allow_spec) {
   if (db->long_mode && ns) {
     // groups cut on the prefix of segments per scope: cost[s] = segments of its incidences + w
     if ((rc = grow_n(ctx, db->b_nseg, (size_t)std::max<int64_t>(nr, 1), &nseg))) return rc;
-    if (nr) hipLaunchKernelGGL(k_prep_nseg, dim3(grid_for(nr * 64)), dim3(kPrepThreads), 0, st, R, nseg);
+    // (the short reads; k_prep_scan_long wrote the long reads' counts)
+    if (nr) hipLaunchKernelGGL(k_prep_nseg, dim3(grid_for(nr)), dim3(kPrepThreads), 0, st, R, nseg);
     int64_t *cost = nullptr;
     if ((rc = grow_n(ctx, db->b_scost, (size_t)ns + 1, &cost))) return rc;
     hipLaunchKernelGGL(k_prep_scope_cost, dim3(grid_for(ns + 1)), dim3(kPrepThreads), 0, st, R, nseg, w, cost);

@@ -18,6 +18,7 @@ def main():
     a = argparse.Namespace(config="c2", reads=None, genome=None, windows=None, germline=None)
     for k, v in bench.CONFIGS["c2"]["defaults"].items():
         setattr(a, k, v)
+    a.batches = a.pipeline = 1   # (one batch of the configured size)
     arr, info = bench.make_batch(a, 0, 0)
     m = native.HipMasker(0)
     torch.cuda.set_device(0)

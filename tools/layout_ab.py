@@ -26,6 +26,7 @@ def main():
     for k, v in bench.CONFIGS[a.config]["defaults"].items():
         if getattr(a, k) is None:
             setattr(a, k, v)
+    a.batches = a.pipeline = 1   # (one batch of the configured size)
     arr, _ = bench.make_batch(a, 0, 0)
     dm = dataset_major(arr)
     m = native.HipMasker(0)

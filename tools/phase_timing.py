@@ -34,6 +34,7 @@ def main():
     for k, v in bench.CONFIGS[args.config]["defaults"].items():
         if getattr(args, k) is None:
             setattr(args, k, v)
+    args.batches = args.pipeline = 1   # (one batch of the configured size)
     arr, info = bench.make_batch(args, 0, 0)
     m = native.HipMasker(0)
     cfgs = []

@@ -23,6 +23,7 @@ def main():
     cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
     args = argparse.Namespace(config=cfg, **bench.CONFIGS[cfg]["defaults"])
+    args.batches = args.pipeline = 1   # (one batch of the configured size)
     arr, _ = bench.make_batch(args, 0, 0)
     m = native.HipMasker(0)
     ref = m.upload_reference(arr["ref_nt16"])

@@ -1206,7 +1206,9 @@ __global__ void __launch_bounds__(kGrpThreads, (OBS > 512 ? 4 : U == 1 ? 6 : U =
   // the partition pieces, whole 16-byte windows (the buffers are padded past seq_bytes); the
   // stores drain while the scan runs (s_waitcnt before the mask stores). (Copying tile by tile,
   // each time up to the tile's written reads so that the scan's loads hit L2, read 0.34 GB less
-  // per c2 launch but took 0.55 instead of 0.54 ms in the same build: DESIGN 5.)
+  // per c2 launch but took 0.55 instead of 0.54 ms in the same build: DESIGN 5. Round 4 tried it
+  // again in the fused one-segment kernel, each tile first copying the piece up to its last segment
+  // byte: 0.665-0.679 vs 0.618 ms per pipelined c2 step, profiles/r04/tile_copy_ab.)
   // (FLAT: the first pass's scope table and first tile's reads are loaded before the copy, which
   // hides their latency)
   FlatScope fs{};

@@ -949,6 +949,328 @@ __global__ void __launch_bounds__(kFqThreads) k_fq_quad(const FqBufs bufs, const
   }
 }
 
+// ---- span variant (GANON_PARAM_FASTQ_KD 13 / 14 / 15) ------------------------------------------
+// The quad kernel's units with their per-unit setup moved into the descriptor phase. Within one
+// field span every unit's source window moves by a fixed step (16 bytes, 8 for the nt16 bases,
+// negative on reversed fields), so the byte shift, the nibble parity and the aligned window start
+// of unit 0 are computed once per span by the record's thread; a unit adds i * step and clamps its
+// five dword offsets with one v_med3 each. Partial units (a field's first and last) build their byte
+// masks from two thresholds; the reverse-complement error test is folded over the unit's four
+// dwords; the nt16 table blend takes its byte mask from v_perm's constant selectors. TM base tiles
+// (8 KiB each) per workgroup: per-tile setup (descriptor scan, barriers, dispatch) is paid once per
+// TM tiles; a workgroup with more than 64 * TM records lists its base tiles for k_fq_dense.
+struct FqSpanS {
+  uint64_t base;   // 4-byte-aligned address of the field's first source byte (bases: of its first nibble)
+  int32_t a0;      // offset (from base) of unit 0's first aligned source dword
+  int32_t hi;      // offset of the field's last aligned source dword
+  int32_t j0;      // field index of unit 0's first byte (-15..0, or the bytes before the tile)
+  int32_t len;     // field length
+  uint16_t td0;    // first tile quad
+  uint16_t vs;     // first virtual quad
+  uint32_t info;   // byte shift | parity << 2 | reverse << 3 | field << 4 (0 bases, 1 qualities, 2 name) |
+                   // window step per unit (int8) << 8
+};
+static_assert(sizeof(FqSpanS) == 32, "FqSpanS layout");
+
+constexpr int kFqDirectMap = 24;   // span kernel: fields of at most this many quads write their map entries
+
+template <int TM>
+struct FqSpanCfg {
+  static constexpr int kTile = TM * kFqTile;
+  static constexpr int kStage = TM * kFqStage;
+  static constexpr int kMap = TM * kFqQMap;
+  static constexpr size_t kSmem = kTile + kMap * sizeof(uint16_t) + 3 * kStage * sizeof(FqSpanS);
+  static_assert(kMap >= kTile / 16 + 3 * kStage, "virtual quad map");
+  static_assert(kMap * sizeof(uint16_t) == 8 * TM * kFqThreads, "TM uint2 of the map per thread");
+};
+
+__device__ __forceinline__ int med3i(int x, int lo, int hi) { return min(max(x, lo), hi); }   // v_med3_i32
+
+// bytes [4d, 4d + 4) of a unit, as a dword mask, that lie in [lo, hi) (unit byte positions)
+__device__ __forceinline__ uint32_t fq_rmask(int lo, int hi, int d) {
+  const uint32_t ge = (uint32_t)(~0ull << med3i(8 * (lo - 4 * d), 0, 32));
+  const uint32_t lt = ~(uint32_t)(~0ull << med3i(8 * (hi - 4 * d), 0, 32));
+  return ge & lt;
+}
+
+// nt16 codes (one per byte, 0..15) -> table bytes; the bit-3 blend mask from v_perm selectors
+// 0x0C (byte 0x00) / 0x0D (byte 0xFF)
+__device__ __forceinline__ uint32_t nt16_lut2(uint32_t c, uint64_t lo, uint64_t hi) {
+  const uint32_t sel = c & 0x07070707u;
+  const uint32_t a = __builtin_amdgcn_perm((uint32_t)(lo >> 32), (uint32_t)lo, sel);
+  const uint32_t b = __builtin_amdgcn_perm((uint32_t)(hi >> 32), (uint32_t)hi, sel);
+  const uint32_t m = __builtin_amdgcn_perm(0u, 0u, ((c >> 3) & 0x01010101u) | 0x0C0C0C0Cu);
+  return (b & m) | (a & ~m);
+}
+
+template <int KQ, int TM, bool LEAN = false>
+__global__ void __launch_bounds__(kFqThreads, TM == 1 ? 8 : 4) k_fq_span(const FqBufs bufs, const FqRec *__restrict__ recs,
+                                                        const uint64_t *__restrict__ off,
+                                                        const int64_t *__restrict__ tile_first, int64_t n,
+                                                        uint64_t total, uint8_t *__restrict__ out,
+                                                        unsigned long long *__restrict__ err, int skip,
+                                                        int *__restrict__ dense_list,
+                                                        unsigned int *__restrict__ dense_count,
+                                                        int64_t n_tiles) {
+  using C = FqSpanCfg<TM>;
+  constexpr int TT = C::kTile;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[C::kSmem];
+  __shared__ unsigned long long s_w[kFqThreads / 64];
+  const int64_t tb = (int64_t)blockIdx.x * TM;   // first base tile
+  const uint64_t t0 = (uint64_t)tb * kFqTile;
+  const int64_t r0 = tile_first[tb];
+  const int64_t rl = (t0 + TT < total) ? tile_first[tb + TM] : n - 1;
+  const int t = threadIdx.x;
+  unsigned long long bad = ~0ull;
+  uint8_t *tile = smem;
+  uint32_t *tile32 = reinterpret_cast<uint32_t *>(smem);
+  if (rl - r0 + 1 > C::kStage) {   // left to k_fq_dense, base tile by base tile
+    if (t < TM && tb + t < n_tiles) dense_list[atomicAdd(dense_count, 1u)] = (int)(tb + t);
+    return;
+  }
+  const int ns = (int)(rl - r0 + 1);
+  uint16_t *map = reinterpret_cast<uint16_t *>(smem + TT);
+  FqSpanS *spans = reinterpret_cast<FqSpanS *>(smem + TT + C::kMap * sizeof(uint16_t));
+  // 1. zero tile and map; one thread per record: its three field spans in tile quads
+#pragma unroll
+  for (int k = 0; k < 2 * TM; ++k) reinterpret_cast<uint4 *>(tile)[t + k * kFqThreads] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+  for (int k = 0; k < TM; ++k) reinterpret_cast<uint2 *>(map)[t + k * kFqThreads] = make_uint2(0, 0);
+  unsigned long long cnt = 0;   // quads touched: bases | qualities << 16 | name << 32
+  FqSpanS sp[3];
+  int64_t P0 = 0;
+  uint32_t NL = 0, L = 0, Q = 0, mate = 0;
+  if (t < ns) {
+    const FqRec R = recs[r0 + t];
+    P0 = (int64_t)off[r0 + t] - (int64_t)t0;
+    NL = (uint32_t)(R.name >> 48);
+    L = R.len;
+    Q = R.qlen;
+    mate = (uint32_t)((R.qual >> 48) & 0xFF);
+    const uint32_t fa[3] = {NL + 4, NL + 7 + L, 1u}, len[3] = {L, Q, NL};
+    const uint32_t rev[3] = {(uint32_t)(R.seq >> 58) & 1, (uint32_t)(R.seq >> 59) & 1, 0u};
+    const uint64_t src[3] = {2 * (uint64_t)(uintptr_t)pick4(bufs.seq, (uint32_t)(R.seq >> 56) & 3) + (R.seq & kOff56),
+                             (uint64_t)(uintptr_t)(pick4(bufs.qual, (uint32_t)(R.qual >> 56) & 3) + (R.qual & kOff48)),
+                             (uint64_t)(uintptr_t)(bufs.names + (R.name & kOff48))};
+#pragma unroll
+    for (int f = 0; f < 3; ++f) {
+      const int64_t fs = P0 + fa[f];
+      const int a = (int)lo64(hi64(fs, 0), TT), b = (int)hi64(lo64(fs + len[f], TT), (int64_t)a);
+      const int q0 = a >> 4, q1 = (b + 15) >> 4;
+      const int j0 = (int)(16 * (int64_t)q0 - fs);
+      const int L_ = (int)len[f];
+      const int rel0 = rev[f] ? L_ - 16 - j0 : j0;   // unit 0's window start in field units
+      int start0, hi;
+      uint64_t base;
+      uint32_t par = 0;
+      if (f == 0) {   // nibble units: src = 2 * byte address + first nibble
+        const int n_off = (int)(src[0] & 7) + rel0;
+        par = (uint32_t)(n_off & 1);
+        start0 = n_off >> 1;
+        hi = (((int)(src[0] & 7) + L_ - 1) >> 1) & ~3;
+        base = (src[0] >> 1) & ~(uint64_t)3;
+      } else {
+        start0 = (int)(src[f] & 3) + rel0;
+        hi = ((int)(src[f] & 3) + L_ - 1) & ~3;
+        base = src[f] & ~(uint64_t)3;
+      }
+      const uint32_t sh = (uint32_t)start0 & 3;
+      sp[f].base = base;
+      sp[f].a0 = start0 - (int)sh;
+      sp[f].hi = hi;
+      sp[f].j0 = j0;
+      sp[f].len = L_;
+      sp[f].td0 = (uint16_t)q0;
+      const int step = (f == 0 ? 8 : 16) * (rev[f] ? -1 : 1);   // window move per unit (bytes)
+      sp[f].info = sh | (par << 2) | (rev[f] << 3) | ((uint32_t)f << 4) | (((uint32_t)step & 0xFF) << 8);
+      sp[f].vs = 0;
+      spans[f * C::kStage + t] = sp[f];   // (vs once the scan is done)
+      cnt |= (unsigned long long)(b > a ? q1 - q0 : 0) << (16 * f);
+    }
+    // a field of more than kFqDirectMap quads: the map is filled forward, not written per record
+    const uint32_t cmax = max(max((uint32_t)(cnt & 0xFFFF), (uint32_t)((cnt >> 16) & 0xFFFF)), (uint32_t)((cnt >> 32) & 0xFFFF));
+    cnt |= (unsigned long long)(cmax > kFqDirectMap) << 48;
+  }
+  unsigned long long tot;
+  const unsigned long long pre = block_excl_scan(cnt, s_w, tot);   // (its barrier: tile and map are zero)
+  if (skip & 8) return;
+  const int V0 = (int)(tot & 0xFFFF), V1 = V0 + (int)((tot >> 16) & 0xFFFF), V = V1 + (int)((tot >> 32) & 0xFFFF);
+  const bool direct = (tot >> 48) == 0;   // block-uniform
+  if (t < ns) {
+    const int base[3] = {0, V0, V1};
+#pragma unroll
+    for (int f = 0; f < 3; ++f) {
+      const int c = (int)((cnt >> (16 * f)) & 0xFFFF);
+      const int v = base[f] + (int)((pre >> (16 * f)) & 0xFFFF);
+      spans[f * C::kStage + t].vs = (uint16_t)v;
+      const uint16_t key = (uint16_t)(f * C::kStage + t);
+      if (direct) {
+        for (int u = 0; u < c; ++u) map[v + u] = key;
+      } else if (c > 0) {
+        map[v] = key;
+      }
+    }
+    const int64_t o[8] = {0, NL + 1, NL + 2, NL + 3, NL + 4 + L, NL + 5 + L, NL + 6 + L, NL + 7 + L + Q};
+    const uint32_t x[8] = {'@', '/', (mate + '0') & 0xFF, '\n', '\n', '+', '\n', '\n'};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int64_t p = P0 + o[e];
+      if (p >= 0 && p < TT) atomicOr(&tile32[p >> 2], x[e] << (8 * (p & 3)));
+    }
+  }
+  __syncthreads();
+  // 2. fill forward (prefix max over the virtual quads): thread t owns map[4TM t, 4TM t + 4TM)
+  if (!direct) {
+    uint32_t *mw = reinterpret_cast<uint32_t *>(map) + 2 * TM * t;
+    uint32_t v[4 * TM];
+#pragma unroll
+    for (int k = 0; k < 2 * TM; ++k) {
+      const uint32_t w = mw[k];
+      v[2 * k] = w & 0xFFFF;
+      v[2 * k + 1] = w >> 16;
+    }
+    uint32_t mx = 0;
+#pragma unroll
+    for (int i = 0; i < 4 * TM; ++i) mx = max(mx, v[i]);
+    uint32_t inc = mx;
+    const int lane = t & 63;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t u = __shfl_up(inc, o);
+      if (lane >= o) inc = max(inc, u);
+    }
+    __syncthreads();   // s_w reused
+    if (lane == 63) s_w[t >> 6] = inc;
+    __syncthreads();
+    uint32_t pm = __shfl_up(inc, 1);
+    if (lane == 0) pm = 0;
+    for (int w = 0; w < (t >> 6); ++w) pm = max(pm, (uint32_t)s_w[w]);
+#pragma unroll
+    for (int i = 0; i < 4 * TM; ++i) {
+      pm = max(pm, v[i]);
+      v[i] = pm;
+    }
+#pragma unroll
+    for (int k = 0; k < 2 * TM; ++k) mw[k] = v[2 * k] | v[2 * k + 1] << 16;
+    __syncthreads();
+  }
+  if (skip & 16) return;
+  // 3. units: KQ virtual quads per lane at a time
+#pragma unroll 1
+  for (int vb = 0; vb < ((skip & 32) ? 0 : V); vb += kFqThreads * KQ) {
+    uint32_t key[KQ], dw[KQ][5], info[KQ];
+    int tq[KQ], J[KQ], len[KQ];
+#pragma unroll
+    for (int j = 0; j < KQ; ++j) {   // each unit's loads issued as soon as its addresses exist
+      const int v = vb + j * kFqThreads + t;
+      key[j] = 0xFFFFu;
+      info[j] = 0;
+      tq[j] = J[j] = len[j] = 0;
+      dw[j][0] = dw[j][1] = dw[j][2] = dw[j][3] = dw[j][4] = 0;
+      if (v >= V) continue;
+      const uint32_t kf = map[v];
+      key[j] = kf;
+      const FqSpanS S = spans[kf];
+      const int i = v - S.vs;
+      tq[j] = S.td0 + i;
+      J[j] = S.j0 + 16 * i;
+      len[j] = S.len;
+      info[j] = S.info;
+      const int a = S.a0 + __mul24(((int)(S.info << 16)) >> 24, i);   // + i * step
+      const int nd = ((S.info >> 4) & 3) != 0 ? 5 : 3;
+      if (skip & 1) {
+        dw[j][0] = dw[j][1] = dw[j][2] = dw[j][3] = dw[j][4] = 0x11111111u;
+        continue;
+      }
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        if (k >= nd) break;
+        int o;
+        asm("v_med3_i32 %0, %1, 0, %2" : "=v"(o) : "v"(a + 4 * k), "v"(S.hi));
+        dw[j][k] = __builtin_nontemporal_load(reinterpret_cast<const GU32 *>(S.base + (uint64_t)(uint32_t)o));
+      }
+    }
+    if (LEAN) {   // only the loaded dwords live across the load wait: the unit's span fields again
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int j = 0; j < KQ; ++j) {
+        const int v = vb + j * kFqThreads + t;
+        if (v >= V) continue;
+        const uint32_t kf = map[v];
+        const FqSpanS &S = spans[kf];
+        const int i = v - S.vs;
+        tq[j] = S.td0 + i;
+        J[j] = S.j0 + 16 * i;
+        len[j] = S.len;
+        info[j] = S.info;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < KQ; ++j) {
+      if (key[j] == 0xFFFFu) continue;
+      const int f = (info[j] >> 4) & 3, k = key[j] % C::kStage;
+      const uint32_t sh = info[j] & 3, par = (info[j] >> 2) & 1;
+      const bool rev = (info[j] >> 3) & 1;
+      const bool full = J[j] >= 0 && J[j] + 16 <= len[j];
+      uint32_t x[4];
+      if (f == 0) {
+        const uint32_t sel = rev ? (par ? 0x04010502u : 0x00040105u) : (par ? 0x02050104u : 0x05010400u);
+        const uint64_t tlo = rev ? kRevLo : kFwdLo, thi = rev ? kRevHi : kFwdHi;
+        const uint32_t w0 = __builtin_amdgcn_alignbyte(dw[j][1], dw[j][0], sh);
+        const uint32_t w1 = __builtin_amdgcn_alignbyte(dw[j][2], dw[j][1], sh);
+        const uint32_t w2 = __builtin_amdgcn_alignbyte(dw[j][3], dw[j][2], sh);
+        const uint32_t h0 = __builtin_amdgcn_alignbyte(w1, w0, 2), h1 = __builtin_amdgcn_alignbyte(w2, w1, 2);
+        const uint32_t win[4] = {rev ? h1 : w0, rev ? w1 : h0, rev ? h0 : w1, rev ? w0 : h1};
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          const uint32_t w = win[d];
+          const uint32_t hiN = (w >> 4) & 0x0F0F0F0Fu, loN = w & 0x0F0F0F0Fu;
+          x[d] = nt16_lut2(__builtin_amdgcn_perm(loN, hiN, sel), tlo, thi);
+        }
+        if (rev) {   // a zero byte (no complement) inside the field: the reference's KeyError (Q7)
+          uint32_t z = 0;
+          const int lo = -J[j], hb = len[j] - J[j];
+#pragma unroll
+          for (int d = 0; d < 4; ++d) {
+            const uint32_t y = full ? x[d] : x[d] | ~fq_rmask(lo, hb, d);
+            z |= (y - 0x01010101u) & ~y & 0x80808080u;
+          }
+          if (z) bad = min(bad, (unsigned long long)(r0 + k));
+        }
+      } else {
+        uint32_t we[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) we[e] = __builtin_amdgcn_alignbyte(dw[j][e + 1], dw[j][e], sh);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          const uint32_t y = rev ? __builtin_bswap32(we[3 - d]) : we[d];
+          x[d] = f == 1 ? add33(y) : y;
+        }
+      }
+      if (full) {
+        reinterpret_cast<uint4 *>(tile)[tq[j]] = make_uint4(x[0], x[1], x[2], x[3]);
+      } else {
+        const int lo = -J[j], hb = len[j] - J[j];
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          const uint32_t m = fq_rmask(lo, hb, d);
+          if (m == 0xFFFFFFFFu) tile32[4 * tq[j] + d] = x[d];
+          else if (m) atomicOr(&tile32[4 * tq[j] + d], x[d] & m);
+        }
+      }
+    }
+  }
+  if (bad != ~0ull) atomicMin(err, bad);
+  __syncthreads();
+  if (skip & 2) return;
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int q = 0; q < TT / (16 * kFqThreads); ++q) {
+    const int p = (q * kFqThreads + t) * 16;
+    if (t0 + p >= total) break;
+    __builtin_nontemporal_store(*reinterpret_cast<const u32x4 *>(tile + p), reinterpret_cast<u32x4 *>(out + t0 + p));
+  }
+}
+
 // ---- row variant (GANON_PARAM_FASTQ_KD 12) -----------------------------------------------------
 // No virtual map: one thread per record stages its three field extents (tile offset, source,
 // length) and its constant bytes; then each field is formatted in one flat pass over (record,
@@ -1365,9 +1687,18 @@ GANON_API int ganon_fastq_run(ganon_ctx *ctx, ganon_fastq *f) {
               : kd == 11 ? k_fq_quad<2, false>
               : kd == 1 ? k_fq_format<1> : kd == 2 ? k_fq_format<2> : kd == 3 ? k_fq_format<3>
               : kd == 5 ? k_fq_format<5> : kd == 6 ? k_fq_format<6> : kd == 8 ? k_fq_format<8> : k_fq_format<4>;
-    hipLaunchKernelGGL(kern, dim3((unsigned)f->n_tiles), dim3(kFqThreads), 0, ctx->stream, f->bufs, f->recs,
-                       f->off, f->tile_first, f->n, f->total, f->out, f->err, ctx->fq_skip, f->dense_list,
-                       f->dense_count);
+    if (kd >= 13 && kd <= 18) {   // span kernels: TM base tiles per workgroup
+      const int tm = (kd == 13 || kd == 16) ? 1 : 2;
+      auto sk = kd == 13 ? k_fq_span<2, 1> : kd == 14 ? k_fq_span<2, 2> : kd == 15 ? k_fq_span<1, 2>
+              : kd == 16 ? k_fq_span<3, 1, true> : kd == 17 ? k_fq_span<4, 2, true> : k_fq_span<5, 2, true>;
+      hipLaunchKernelGGL(sk, dim3((unsigned)((f->n_tiles + tm - 1) / tm)), dim3(kFqThreads), 0, ctx->stream, f->bufs,
+                         f->recs, f->off, f->tile_first, f->n, f->total, f->out, f->err, ctx->fq_skip, f->dense_list,
+                         f->dense_count, f->n_tiles);
+    } else {
+      hipLaunchKernelGGL(kern, dim3((unsigned)f->n_tiles), dim3(kFqThreads), 0, ctx->stream, f->bufs, f->recs,
+                         f->off, f->tile_first, f->n, f->total, f->out, f->err, ctx->fq_skip, f->dense_list,
+                         f->dense_count);
+    }
     hipLaunchKernelGGL(k_fq_dense, dim3(kFqDenseGrid), dim3(kFqThreads), 0, ctx->stream, f->bufs, f->recs, f->off,
                        f->tile_first, f->n, f->total, f->out, f->err, f->dense_list, f->dense_count);
     if ((rc = check_launch(ctx, "k_fq_format"))) return rc;

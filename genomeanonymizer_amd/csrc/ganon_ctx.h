@@ -31,7 +31,7 @@ struct ganon_ctx {
   int ref2 = 1;                // GANON_PARAM_REF2
   int fq_skip = 0;             // GANON_PARAM_FASTQ_SKIP (profiling only)
   int prep_long = -1;          // GANON_PARAM_PREP_LONG (-1 auto, 0 never, 1 always)
-  int fq_kd = 0;               // GANON_PARAM_FASTQ_KD (0: quad kernel, 2 quads per lane; 3: dword kernel)
+  int fq_kd = 0;               // GANON_PARAM_FASTQ_KD (0: span kernel, 3 units per lane; 16: quad kernel)
   int indel_sort = 0;          // GANON_PARAM_INDEL_SORT
   int group_obs = 0;           // GANON_PARAM_GROUP_OBS (0 auto, 512, 1024)
   int spec_plan = 1;           // GANON_PARAM_SPEC_PLAN (1: speculative replans, 0: every plan synchronizes)

@@ -11,16 +11,16 @@
 // Design: byte work, HBM-bound. A run is four launches:
 //   k_fq_bsum   record-length sums per block of 2048 records
 //   k_fq_bscan  one workgroup: exclusive scan of the block sums (also resets the error slot)
-//   k_fq_off    record output offsets (u64) + for every 16 KiB output tile the record that
+//   k_fq_off    record output offsets (u64) + for every 8 KiB output tile the record that
 //               holds its first byte
-//   k_fq_format one workgroup per 16 KiB output tile, records staged in LDS. Lanes own
-//               consecutive output dwords (every store instruction writes 256 contiguous
-//               bytes, each line once); a per-lane record cursor walks forward. A dword inside
-//               one field is built from two aligned dword loads: names as they are,
-//               qualities + 33 per byte (SWAR, byte-reversed for reversed qualities), bases
-//               as four nibbles through two v_perm table lookups (reverse complement likewise,
-//               with a zero-byte test for the Q7 error); dwords across fields are built byte
-//               by byte. KD dwords per lane are loaded before any is used.
+//   k_fq_span   (default) one workgroup per 8 KiB output tile, assembled in LDS and stored
+//               with full-line 16-byte stores: per record its three field spans (staged once by
+//               the record's thread), a virtual map of 16-byte units filled forward, then every
+//               unit's source dwords loaded in one round (3 units per lane), transformed (names
+//               as they are, qualities + 33 per byte, bases as nibbles through two v_perm table
+//               lookups, reverse complement with a zero-byte test for the Q7 error) and written.
+//   k_fq_quad / k_fq_rows / k_fq_format: earlier designs kept as A/B instances
+//               (GANON_PARAM_FASTQ_KD); k_fq_dense takes tiles with more than 64 records.
 #include "ganon_ctx.h"
 
 #include <algorithm>
@@ -687,7 +687,7 @@ __global__ void __launch_bounds__(kFqThreads) k_fq_format(const FqBufs bufs, con
   }
 }
 
-// ---- quad variant (GANON_PARAM_FASTQ_KD 0 / 9 / 10) -----------------------------------------------
+// ---- quad variant (GANON_PARAM_FASTQ_KD 16 / 9 / 10; the default up to round 4) --------------------
 // The same tile design with 16-byte units: a virtual unit is one 16-byte-aligned tile quad of one
 // field, so the map / span lookup and the address arithmetic are paid once per 16 output bytes
 // instead of once per 4 (the dword kernel above is VALU-bound: without loads and stores it still
@@ -949,16 +949,21 @@ __global__ void __launch_bounds__(kFqThreads) k_fq_quad(const FqBufs bufs, const
   }
 }
 
-// ---- span variant (GANON_PARAM_FASTQ_KD 13 / 14 / 15) ------------------------------------------
+// ---- span variant (GANON_PARAM_FASTQ_KD 0, the default / 13 / 14) ------------------------------
 // The quad kernel's units with their per-unit setup moved into the descriptor phase. Within one
 // field span every unit's source window moves by a fixed step (16 bytes, 8 for the nt16 bases,
 // negative on reversed fields), so the byte shift, the nibble parity and the aligned window start
 // of unit 0 are computed once per span by the record's thread; a unit adds i * step and clamps its
 // five dword offsets with one v_med3 each. Partial units (a field's first and last) build their byte
 // masks from two thresholds; the reverse-complement error test is folded over the unit's four
-// dwords; the nt16 table blend takes its byte mask from v_perm's constant selectors. TM base tiles
-// (8 KiB each) per workgroup: per-tile setup (descriptor scan, barriers, dispatch) is paid once per
-// TM tiles; a workgroup with more than 64 * TM records lists its base tiles for k_fq_dense.
+// dwords; the nt16 table blend takes its byte mask from v_perm's constant selectors. The kernel is
+// latency-bound (eight 4-wave workgroups per CU, each a chain of dependent rounds: tile_first ->
+// records -> spans -> source loads -> tile stores), so a unit's loads are issued as soon as its
+// addresses exist and, with LEAN, only the loaded dwords stay live across the wait (the span fields
+// are re-read from LDS after it): 3 units per lane fit 64 VGPRs and cover a c2 tile's ~600 units in
+// one load round. TM base tiles (8 KiB each) per workgroup (TM = 2 measured slower:
+// fewer resident workgroups); a workgroup with more than 64 * TM records lists its base tiles for
+// k_fq_dense.
 struct FqSpanS {
   uint64_t base;   // 4-byte-aligned address of the field's first source byte (bases: of its first nibble)
   int32_t a0;      // offset (from base) of unit 0's first aligned source dword
@@ -971,8 +976,6 @@ struct FqSpanS {
                    // window step per unit (int8) << 8
 };
 static_assert(sizeof(FqSpanS) == 32, "FqSpanS layout");
-
-constexpr int kFqDirectMap = 24;   // span kernel: fields of at most this many quads write their map entries
 
 template <int TM>
 struct FqSpanCfg {
@@ -1016,6 +1019,7 @@ __global__ void __launch_bounds__(kFqThreads, TM == 1 ? 8 : 4) k_fq_span(const F
   constexpr int TT = C::kTile;
   __shared__ __attribute__((aligned(16))) uint8_t smem[C::kSmem];
   __shared__ unsigned long long s_w[kFqThreads / 64];
+  __shared__ uint32_t s_m[kFqThreads / 64];   // fill-forward wave maxima (s_w is still being read)
   const int64_t tb = (int64_t)blockIdx.x * TM;   // first base tile
   const uint64_t t0 = (uint64_t)tb * kFqTile;
   const int64_t r0 = tile_first[tb];
@@ -1083,32 +1087,22 @@ __global__ void __launch_bounds__(kFqThreads, TM == 1 ? 8 : 4) k_fq_span(const F
       sp[f].td0 = (uint16_t)q0;
       const int step = (f == 0 ? 8 : 16) * (rev[f] ? -1 : 1);   // window move per unit (bytes)
       sp[f].info = sh | (par << 2) | (rev[f] << 3) | ((uint32_t)f << 4) | (((uint32_t)step & 0xFF) << 8);
-      sp[f].vs = 0;
-      spans[f * C::kStage + t] = sp[f];   // (vs once the scan is done)
       cnt |= (unsigned long long)(b > a ? q1 - q0 : 0) << (16 * f);
     }
-    // a field of more than kFqDirectMap quads: the map is filled forward, not written per record
-    const uint32_t cmax = max(max((uint32_t)(cnt & 0xFFFF), (uint32_t)((cnt >> 16) & 0xFFFF)), (uint32_t)((cnt >> 32) & 0xFFFF));
-    cnt |= (unsigned long long)(cmax > kFqDirectMap) << 48;
   }
   unsigned long long tot;
   const unsigned long long pre = block_excl_scan(cnt, s_w, tot);   // (its barrier: tile and map are zero)
   if (skip & 8) return;
   const int V0 = (int)(tot & 0xFFFF), V1 = V0 + (int)((tot >> 16) & 0xFFFF), V = V1 + (int)((tot >> 32) & 0xFFFF);
-  const bool direct = (tot >> 48) == 0;   // block-uniform
   if (t < ns) {
     const int base[3] = {0, V0, V1};
 #pragma unroll
     for (int f = 0; f < 3; ++f) {
       const int c = (int)((cnt >> (16 * f)) & 0xFFFF);
       const int v = base[f] + (int)((pre >> (16 * f)) & 0xFFFF);
-      spans[f * C::kStage + t].vs = (uint16_t)v;
-      const uint16_t key = (uint16_t)(f * C::kStage + t);
-      if (direct) {
-        for (int u = 0; u < c; ++u) map[v + u] = key;
-      } else if (c > 0) {
-        map[v] = key;
-      }
+      sp[f].vs = (uint16_t)v;
+      spans[f * C::kStage + t] = sp[f];
+      if (c > 0) map[v] = (uint16_t)(f * C::kStage + t);
     }
     const int64_t o[8] = {0, NL + 1, NL + 2, NL + 3, NL + 4 + L, NL + 5 + L, NL + 6 + L, NL + 7 + L + Q};
     const uint32_t x[8] = {'@', '/', (mate + '0') & 0xFF, '\n', '\n', '+', '\n', '\n'};
@@ -1120,7 +1114,7 @@ __global__ void __launch_bounds__(kFqThreads, TM == 1 ? 8 : 4) k_fq_span(const F
   }
   __syncthreads();
   // 2. fill forward (prefix max over the virtual quads): thread t owns map[4TM t, 4TM t + 4TM)
-  if (!direct) {
+  {
     uint32_t *mw = reinterpret_cast<uint32_t *>(map) + 2 * TM * t;
     uint32_t v[4 * TM];
 #pragma unroll
@@ -1138,12 +1132,11 @@ __global__ void __launch_bounds__(kFqThreads, TM == 1 ? 8 : 4) k_fq_span(const F
       const uint32_t u = __shfl_up(inc, o);
       if (lane >= o) inc = max(inc, u);
     }
-    __syncthreads();   // s_w reused
-    if (lane == 63) s_w[t >> 6] = inc;
+    if (lane == 63) s_m[t >> 6] = inc;
     __syncthreads();
     uint32_t pm = __shfl_up(inc, 1);
     if (lane == 0) pm = 0;
-    for (int w = 0; w < (t >> 6); ++w) pm = max(pm, (uint32_t)s_w[w]);
+    for (int w = 0; w < (t >> 6); ++w) pm = max(pm, s_m[w]);
 #pragma unroll
     for (int i = 0; i < 4 * TM; ++i) {
       pm = max(pm, v[i]);
@@ -1683,14 +1676,13 @@ GANON_API int ganon_fastq_run(ganon_ctx *ctx, ganon_fastq *f) {
     // virtual dwords per lane per round: a tile holds ~2,100 of them (2,048 tile dwords plus the
     // dwords neighbouring fields share), so the width sets the number of dependent load rounds
     const int kd = ctx->fq_kd;
-    auto kern = kd == 0 ? k_fq_quad<2> : kd == 12 ? k_fq_rows : kd == 9 ? k_fq_quad<1> : kd == 10 ? k_fq_quad<3>
+    auto kern = kd == 16 ? k_fq_quad<2> : kd == 12 ? k_fq_rows : kd == 9 ? k_fq_quad<1> : kd == 10 ? k_fq_quad<3>
               : kd == 11 ? k_fq_quad<2, false>
               : kd == 1 ? k_fq_format<1> : kd == 2 ? k_fq_format<2> : kd == 3 ? k_fq_format<3>
               : kd == 5 ? k_fq_format<5> : kd == 6 ? k_fq_format<6> : kd == 8 ? k_fq_format<8> : k_fq_format<4>;
-    if (kd >= 13 && kd <= 18) {   // span kernels: TM base tiles per workgroup
-      const int tm = (kd == 13 || kd == 16) ? 1 : 2;
-      auto sk = kd == 13 ? k_fq_span<2, 1> : kd == 14 ? k_fq_span<2, 2> : kd == 15 ? k_fq_span<1, 2>
-              : kd == 16 ? k_fq_span<3, 1, true> : kd == 17 ? k_fq_span<4, 2, true> : k_fq_span<5, 2, true>;
+    if (kd == 0 || kd == 13 || kd == 14) {   // span kernels (default: 3 units per lane, one 8 KiB tile)
+      const int tm = kd == 14 ? 2 : 1;
+      auto sk = kd == 0 ? k_fq_span<3, 1, true> : kd == 13 ? k_fq_span<2, 1> : k_fq_span<2, 2>;
       hipLaunchKernelGGL(sk, dim3((unsigned)((f->n_tiles + tm - 1) / tm)), dim3(kFqThreads), 0, ctx->stream, f->bufs,
                          f->recs, f->off, f->tile_first, f->n, f->total, f->out, f->err, ctx->fq_skip, f->dense_list,
                          f->dense_count, f->n_tiles);

@@ -121,9 +121,11 @@ GANON_API int ganon_ctx_set_variant(ganon_ctx *ctx, int variant);
  * upload, in cost units: segments plus 3 per scope; 0 (default) = 1408 in long-read prep mode, else 704). GANON_PARAM_NT_COPY: non-temporal stores for the fused partition copy
  * (default 1). GANON_PARAM_REF2: group kernels read a 2-bit copy of the reference for segments
  * whose reference range is all ACGT (1, default) or the nt16 reference only (0).
- * GANON_PARAM_FASTQ_KD: FASTQ formatter kernel: 0 (default) / 9 / 10 = 16-byte units, 2 / 1 / 3 per lane;
- *   11 = 16-byte units, 2 per lane, bases windows selected per output dword (A/B instance);
- *   1-6 or 8 = the dword kernel with that many output dwords per lane at once.
+ * GANON_PARAM_FASTQ_KD: FASTQ formatter kernel: 0 (default) = 16-byte units with per-span window
+ *   setup, 3 per lane in one load round; 13 / 14 = the same, 2 per lane, one / two 8 KiB tiles per
+ *   workgroup; 16 / 9 / 10 = 16-byte units with per-unit setup (the default up to round 4), 2 / 1 / 3
+ *   per lane; 11 = 16-byte units, 2 per lane, bases windows selected per output dword (A/B instance);
+ *   12 = record rows; 1-6 or 8 = the dword kernel with that many output dwords per lane at once.
  * GANON_PARAM_FASTQ_SKIP (phase timing only, changes results): bit 0 leaves out the
  * formatter's source loads, bit 1 its stores; bits 3-6 stop after the descriptor scan / after the
  * dword map / leave out the interior pass / leave out the edge and constant bytes.

@@ -83,14 +83,13 @@ def test_bad_for_reverse_flags_non_acgtn_reads():
 
 # ---- GPU: the HIP formatter ----------------------------------------------------------------
 
-@pytest.fixture(scope="module", params=[0, 13, 14, 15, 16, 17, 18, 12, 9, 11, 3],
-                ids=["quad2", "span_t1", "span_t2", "span1_t2", "span_direct", "span1_direct", "span_direct_t2",
-                     "rows", "quad1", "quad2_select", "dword3"])
+@pytest.fixture(scope="module", params=[0, 13, 14, 16, 12, 9, 11, 3],
+                ids=["span3", "span2", "span2_t2", "quad2", "rows", "quad1", "quad2_select", "dword3"])
 def masker(hip_built, request):
-    """Every HIP formatter test runs on the quad kernel (GANON_PARAM_FASTQ_KD 0, the default; 9 = one
-    quad per lane; 11 = the per-dword base select of round 1), the span kernel (13: one 8 KiB tile
-    per workgroup, 14 / 15: two, with 2 / 1 units per lane), the record-row kernel (12) and the
-    dword kernel (3)."""
+    """Every HIP formatter test runs on the span kernel (GANON_PARAM_FASTQ_KD 0, the default: 3 units
+    per lane; 13 / 14: 2 per lane, one / two 8 KiB tiles per workgroup), the quad kernel (16, the
+    default up to round 4; 9 = one quad per lane; 11 = the per-dword base select of round 1), the
+    record-row kernel (12) and the dword kernel (3)."""
     m = native.HipMasker(0)
     m.set_param(native.PARAM_FASTQ_KD, request.param)
     yield m

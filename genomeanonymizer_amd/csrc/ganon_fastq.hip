@@ -1006,7 +1006,7 @@ __device__ __forceinline__ uint32_t nt16_lut2(uint32_t c, uint64_t lo, uint64_t 
   return (b & m) | (a & ~m);
 }
 
-template <int KQ, int TM, bool LEAN = false>
+template <int KQ, int TM, bool LEAN = false, bool SEARCH = false>
 __global__ void __launch_bounds__(kFqThreads, TM == 1 ? 8 : 4) k_fq_span(const FqBufs bufs, const FqRec *__restrict__ recs,
                                                         const uint64_t *__restrict__ off,
                                                         const int64_t *__restrict__ tile_first, int64_t n,
@@ -1038,8 +1038,10 @@ __global__ void __launch_bounds__(kFqThreads, TM == 1 ? 8 : 4) k_fq_span(const F
   // 1. zero tile and map; one thread per record: its three field spans in tile quads
 #pragma unroll
   for (int k = 0; k < 2 * TM; ++k) reinterpret_cast<uint4 *>(tile)[t + k * kFqThreads] = make_uint4(0, 0, 0, 0);
+  if (!SEARCH) {
 #pragma unroll
-  for (int k = 0; k < TM; ++k) reinterpret_cast<uint2 *>(map)[t + k * kFqThreads] = make_uint2(0, 0);
+    for (int k = 0; k < TM; ++k) reinterpret_cast<uint2 *>(map)[t + k * kFqThreads] = make_uint2(0, 0);
+  }
   unsigned long long cnt = 0;   // quads touched: bases | qualities << 16 | name << 32
   FqSpanS sp[3];
   int64_t P0 = 0;
@@ -1102,7 +1104,7 @@ __global__ void __launch_bounds__(kFqThreads, TM == 1 ? 8 : 4) k_fq_span(const F
       const int v = base[f] + (int)((pre >> (16 * f)) & 0xFFFF);
       sp[f].vs = (uint16_t)v;
       spans[f * C::kStage + t] = sp[f];
-      if (c > 0) map[v] = (uint16_t)(f * C::kStage + t);
+      if (!SEARCH && c > 0) map[v] = (uint16_t)(f * C::kStage + t);
     }
     const int64_t o[8] = {0, NL + 1, NL + 2, NL + 3, NL + 4 + L, NL + 5 + L, NL + 6 + L, NL + 7 + L + Q};
     const uint32_t x[8] = {'@', '/', (mate + '0') & 0xFF, '\n', '\n', '+', '\n', '\n'};
@@ -1113,8 +1115,9 @@ __global__ void __launch_bounds__(kFqThreads, TM == 1 ? 8 : 4) k_fq_span(const F
     }
   }
   __syncthreads();
-  // 2. fill forward (prefix max over the virtual quads): thread t owns map[4TM t, 4TM t + 4TM)
-  {
+  // 2. fill forward (prefix max over the virtual quads): thread t owns map[4TM t, 4TM t + 4TM).
+  //    SEARCH: no map; a unit finds its span by a binary search over the field's span starts
+  if (!SEARCH) {
     uint32_t *mw = reinterpret_cast<uint32_t *>(map) + 2 * TM * t;
     uint32_t v[4 * TM];
 #pragma unroll
@@ -1160,7 +1163,20 @@ __global__ void __launch_bounds__(kFqThreads, TM == 1 ? 8 : 4) k_fq_span(const F
       tq[j] = J[j] = len[j] = 0;
       dw[j][0] = dw[j][1] = dw[j][2] = dw[j][3] = dw[j][4] = 0;
       if (v >= V) continue;
-      const uint32_t kf = map[v];
+      uint32_t kf;
+      if (SEARCH) {   // the last record of the unit's field whose span starts at or before v
+        const int f = v < V0 ? 0 : v < V1 ? 1 : 2;
+        const FqSpanS *fs = spans + f * C::kStage;
+        int k = 0;
+#pragma unroll
+        for (int st = C::kStage / 2; st > 0; st >>= 1) {
+          const int c = k + st;
+          if (c < ns && (int)fs[c].vs <= v) k = c;
+        }
+        kf = (uint32_t)(f * C::kStage + k);
+      } else {
+        kf = map[v];
+      }
       key[j] = kf;
       const FqSpanS S = spans[kf];
       const int i = v - S.vs;
@@ -1188,8 +1204,7 @@ __global__ void __launch_bounds__(kFqThreads, TM == 1 ? 8 : 4) k_fq_span(const F
       for (int j = 0; j < KQ; ++j) {
         const int v = vb + j * kFqThreads + t;
         if (v >= V) continue;
-        const uint32_t kf = map[v];
-        const FqSpanS &S = spans[kf];
+        const FqSpanS &S = spans[key[j]];
         const int i = v - S.vs;
         tq[j] = S.td0 + i;
         J[j] = S.j0 + 16 * i;
@@ -1680,9 +1695,10 @@ GANON_API int ganon_fastq_run(ganon_ctx *ctx, ganon_fastq *f) {
               : kd == 11 ? k_fq_quad<2, false>
               : kd == 1 ? k_fq_format<1> : kd == 2 ? k_fq_format<2> : kd == 3 ? k_fq_format<3>
               : kd == 5 ? k_fq_format<5> : kd == 6 ? k_fq_format<6> : kd == 8 ? k_fq_format<8> : k_fq_format<4>;
-    if (kd == 0 || kd == 13 || kd == 14) {   // span kernels (default: 3 units per lane, one 8 KiB tile)
+    if (kd == 0 || kd == 13 || kd == 14 || kd == 15) {   // span kernels (default: 3 units per lane, one 8 KiB tile)
       const int tm = kd == 14 ? 2 : 1;
-      auto sk = kd == 0 ? k_fq_span<3, 1, true> : kd == 13 ? k_fq_span<2, 1> : k_fq_span<2, 2>;
+      auto sk = kd == 0 ? k_fq_span<3, 1, true> : kd == 13 ? k_fq_span<2, 1> : kd == 14 ? k_fq_span<2, 2>
+              : k_fq_span<3, 1, true, true>;
       hipLaunchKernelGGL(sk, dim3((unsigned)((f->n_tiles + tm - 1) / tm)), dim3(kFqThreads), 0, ctx->stream, f->bufs,
                          f->recs, f->off, f->tile_first, f->n, f->total, f->out, f->err, ctx->fq_skip, f->dense_list,
                          f->dense_count, f->n_tiles);

@@ -96,19 +96,13 @@ GANON_API const char *ganon_last_error(ganon_ctx *ctx);
 GANON_API int ganon_abi_version(void);
 /* Use an external hipStream_t (e.g. torch's current stream); NULL = the ctx's own. */
 GANON_API int ganon_ctx_set_stream(ganon_ctx *ctx, void *hip_stream);
-/* Small-scope kernel. Since ABI 3 the fused group kernel (GANON_VARIANT_DEFAULT =
- * GANON_VARIANT_GROUP_FUSED: one workgroup per group of consecutive scopes copies its line-aligned
- * pieces of the output and masks with byte stores) is the only one; the round-1 A/B kernels
- * (BLOCK, WAVE, COPYPATCH, GROUP, PERSIST) were retired and ganon_ctx_set_variant rejects them
- * with GANON_E_ARG. The enum values are kept so that old callers get that error, not another. */
+/* Group kernel selection. Since ABI 3 the fused group kernel (one workgroup per group of
+ * consecutive scopes copies its line-aligned pieces of the output and masks with byte stores) is
+ * the only one: GANON_VARIANT_DEFAULT and GANON_VARIANT_GROUP_FUSED both select it; any other value
+ * (the round-1 A/B kernels 1-4 and 6 were retired) is rejected with GANON_E_ARG. */
 enum {
   GANON_VARIANT_DEFAULT = 0,
-  GANON_VARIANT_BLOCK = 1,
-  GANON_VARIANT_WAVE = 2,
-  GANON_VARIANT_COPYPATCH = 3,
-  GANON_VARIANT_GROUP = 4,
-  GANON_VARIANT_GROUP_FUSED = 5,
-  GANON_VARIANT_PERSIST = 6
+  GANON_VARIANT_GROUP_FUSED = 5
 };
 GANON_API int ganon_ctx_set_variant(ganon_ctx *ctx, int variant);
 /* Tuning knobs (results never depend on them). GANON_PARAM_GROUP_UNROLL: 16-base chunks each

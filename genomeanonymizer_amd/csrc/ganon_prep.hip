@@ -468,14 +468,26 @@ __global__ void __launch_bounds__(kReduceThreads) k_prep_reduce(const Raw R, con
                                                                 unsigned long long *__restrict__ info,
                                                                 const PrepErr *__restrict__ err, long long spec_rpi,
                                                                 const unsigned int *__restrict__ long_count) {
-  // partials of one kind contiguous (block_parts): every load coalesced, 1024 threads in flight
+  // partials of one kind contiguous (block_parts): every load coalesced, 1024 threads in flight,
+  // kReduceU blocks of every kind loaded per thread before any is added (a loop of dependent
+  // single loads took ~50 us for configs[1]'s 11 k blocks: one HBM latency per iteration)
+  constexpr int kReduceU = 8;
   unsigned long long acc[kParts] = {0, 0, 0, 0, 0, 0};
+  for (int b0 = threadIdx.x; b0 < n_blocks; b0 += kReduceU * kReduceThreads) {
+    unsigned long long v[kParts][kReduceU];
 #pragma unroll
-  for (int k = 0; k < kParts; ++k)
-    for (int b = threadIdx.x; b < n_blocks; b += kReduceThreads) {
-      const unsigned long long v = part[stride * k + b];
-      acc[k] = (k == kPartMaxLen || k == kPartMaxSeg) ? (v > acc[k] ? v : acc[k]) : acc[k] + v;
-    }
+    for (int k = 0; k < kParts; ++k)
+#pragma unroll
+      for (int u = 0; u < kReduceU; ++u) {
+        const int b = b0 + u * kReduceThreads;
+        v[k][u] = b < n_blocks ? part[stride * k + b] : 0ull;
+      }
+#pragma unroll
+    for (int k = 0; k < kParts; ++k)
+#pragma unroll
+      for (int u = 0; u < kReduceU; ++u)
+        acc[k] = (k == kPartMaxLen || k == kPartMaxSeg) ? (v[k][u] > acc[k] ? v[k][u] : acc[k]) : acc[k] + v[k][u];
+  }
   __shared__ unsigned long long out[kParts];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   constexpr int kRW = kReduceThreads / 64;

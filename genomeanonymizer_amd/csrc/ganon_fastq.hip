@@ -1006,7 +1006,7 @@ __device__ __forceinline__ uint32_t nt16_lut2(uint32_t c, uint64_t lo, uint64_t 
   return (b & m) | (a & ~m);
 }
 
-template <int KQ, int TM, bool LEAN = false, bool SEARCH = false>
+template <int KQ, int TM, bool LEAN = false, int MAP = 0>   // MAP: 0 filled map, 1 binary search, 2 coarse map
 __global__ void __launch_bounds__(kFqThreads, TM == 1 ? 8 : 4) k_fq_span(const FqBufs bufs, const FqRec *__restrict__ recs,
                                                         const uint64_t *__restrict__ off,
                                                         const int64_t *__restrict__ tile_first, int64_t n,
@@ -1038,7 +1038,7 @@ __global__ void __launch_bounds__(kFqThreads, TM == 1 ? 8 : 4) k_fq_span(const F
   // 1. zero tile and map; one thread per record: its three field spans in tile quads
 #pragma unroll
   for (int k = 0; k < 2 * TM; ++k) reinterpret_cast<uint4 *>(tile)[t + k * kFqThreads] = make_uint4(0, 0, 0, 0);
-  if (!SEARCH) {
+  if (MAP == 0) {
 #pragma unroll
     for (int k = 0; k < TM; ++k) reinterpret_cast<uint2 *>(map)[t + k * kFqThreads] = make_uint2(0, 0);
   }
@@ -1104,7 +1104,9 @@ __global__ void __launch_bounds__(kFqThreads, TM == 1 ? 8 : 4) k_fq_span(const F
       const int v = base[f] + (int)((pre >> (16 * f)) & 0xFFFF);
       sp[f].vs = (uint16_t)v;
       spans[f * C::kStage + t] = sp[f];
-      if (!SEARCH && c > 0) map[v] = (uint16_t)(f * C::kStage + t);
+      if (MAP == 0 && c > 0) map[v] = (uint16_t)(f * C::kStage + t);
+      if (MAP == 2)   // coarse map: the span holding unit 8b, for the blocks b whose first unit is ours
+        for (int b = (v + 7) >> 3; 8 * b < v + c; ++b) map[b] = (uint16_t)(f * C::kStage + t);
     }
     const int64_t o[8] = {0, NL + 1, NL + 2, NL + 3, NL + 4 + L, NL + 5 + L, NL + 6 + L, NL + 7 + L + Q};
     const uint32_t x[8] = {'@', '/', (mate + '0') & 0xFF, '\n', '\n', '+', '\n', '\n'};
@@ -1116,8 +1118,9 @@ __global__ void __launch_bounds__(kFqThreads, TM == 1 ? 8 : 4) k_fq_span(const F
   }
   __syncthreads();
   // 2. fill forward (prefix max over the virtual quads): thread t owns map[4TM t, 4TM t + 4TM).
-  //    SEARCH: no map; a unit finds its span by a binary search over the field's span starts
-  if (!SEARCH) {
+  //    MAP 1: no map; a unit finds its span by a binary search over the field's span starts.
+  //    MAP 2: one entry per 8 units (written per record above); a unit walks forward from it
+  if (MAP == 0) {
     uint32_t *mw = reinterpret_cast<uint32_t *>(map) + 2 * TM * t;
     uint32_t v[4 * TM];
 #pragma unroll
@@ -1164,7 +1167,15 @@ __global__ void __launch_bounds__(kFqThreads, TM == 1 ? 8 : 4) k_fq_span(const F
       dw[j][0] = dw[j][1] = dw[j][2] = dw[j][3] = dw[j][4] = 0;
       if (v >= V) continue;
       uint32_t kf;
-      if (SEARCH) {   // the last record of the unit's field whose span starts at or before v
+      if (MAP == 2) {   // from the span of unit 8 * (v / 8), forward over the spans starting <= v
+        kf = map[v >> 3];
+        for (;;) {
+          const uint32_t kt = kf % C::kStage;
+          const uint32_t nx = (int)kt + 1 < ns ? kf + 1 : (kf - kt) + C::kStage;
+          if (nx >= 3u * C::kStage || (int)spans[nx].vs > v) break;
+          kf = nx;
+        }
+      } else if (MAP == 1) {   // the last record of the unit's field whose span starts at or before v
         const int f = v < V0 ? 0 : v < V1 ? 1 : 2;
         const FqSpanS *fs = spans + f * C::kStage;
         int k = 0;
@@ -1695,10 +1706,10 @@ GANON_API int ganon_fastq_run(ganon_ctx *ctx, ganon_fastq *f) {
               : kd == 11 ? k_fq_quad<2, false>
               : kd == 1 ? k_fq_format<1> : kd == 2 ? k_fq_format<2> : kd == 3 ? k_fq_format<3>
               : kd == 5 ? k_fq_format<5> : kd == 6 ? k_fq_format<6> : kd == 8 ? k_fq_format<8> : k_fq_format<4>;
-    if (kd == 0 || kd == 13 || kd == 14 || kd == 15) {   // span kernels (default: 3 units per lane, one 8 KiB tile)
+    if (kd == 0 || (kd >= 13 && kd <= 15) || kd == 17) {   // span kernels (default: 3 units per lane, one 8 KiB tile)
       const int tm = kd == 14 ? 2 : 1;
       auto sk = kd == 0 ? k_fq_span<3, 1, true> : kd == 13 ? k_fq_span<2, 1> : kd == 14 ? k_fq_span<2, 2>
-              : k_fq_span<3, 1, true, true>;
+              : kd == 15 ? k_fq_span<3, 1, true, 1> : k_fq_span<3, 1, true, 2>;
       hipLaunchKernelGGL(sk, dim3((unsigned)((f->n_tiles + tm - 1) / tm)), dim3(kFqThreads), 0, ctx->stream, f->bufs,
                          f->recs, f->off, f->tile_first, f->n, f->total, f->out, f->err, ctx->fq_skip, f->dense_list,
                          f->dense_count, f->n_tiles);

@@ -2077,10 +2077,10 @@ GANON_API int ganon_ctx_set_param(ganon_ctx *ctx, int param, int value) {
     return GANON_OK;
   }
   if (param == GANON_PARAM_FASTQ_KD) {
-    if (value < 0 || value > 16 || value == 7)
+    if (value < 0 || value > 17 || value == 7)
       return fail(ctx, GANON_E_ARG,
                   "FASTQ kernel: 0 (spans, 3 units per lane), 13 / 14 (spans, 2 per lane, 8 / 16 KiB tiles), "
-                  "15 (as 0, span found by binary search instead of the filled map), "
+                  "15 / 17 (as 0, span found by binary search / from a map entry per 8 units), "
                   "16 / 9 / 10 (quads, 2 / 1 / 3 per lane), 11 (quads, per-dword base select), "
                   "12 (record rows), dwords per lane 1-6 or 8");
     ctx->fq_kd = value;

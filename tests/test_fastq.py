@@ -83,8 +83,9 @@ def test_bad_for_reverse_flags_non_acgtn_reads():
 
 # ---- GPU: the HIP formatter ----------------------------------------------------------------
 
-@pytest.fixture(scope="module", params=[0, 15, 13, 14, 16, 12, 9, 11, 3],
-                ids=["span3", "span3_search", "span2", "span2_t2", "quad2", "rows", "quad1", "quad2_select", "dword3"])
+@pytest.fixture(scope="module", params=[0, 15, 17, 13, 14, 16, 12, 9, 11, 3],
+                ids=["span3", "span3_search", "span3_coarse", "span2", "span2_t2", "quad2", "rows", "quad1",
+                     "quad2_select", "dword3"])
 def masker(hip_built, request):
     """Every HIP formatter test runs on the span kernel (GANON_PARAM_FASTQ_KD 0, the default: 3 units
     per lane; 13 / 14: 2 per lane, one / two 8 KiB tiles per workgroup), the quad kernel (16, the

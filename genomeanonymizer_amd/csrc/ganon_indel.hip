@@ -353,6 +353,9 @@ __device__ bool normal_covers(const GanonReadView &V, int scope, int pos) {
   return false;
 }
 
+#ifndef GANON_CLS_DIAG
+#define GANON_CLS_DIAG 0   // phase timing builds only (tools/build_variant.py): 1 no normal-column check,
+#endif                     // 2 no pass 2, 3 run extents only — all change results
 template <typename KeyT>
 __device__ void classify_run(const GanonReadView &V, const KeyT *__restrict__ keys, const uint32_t *__restrict__ vals,
                              int64_t n, int pos_bits, const IndelObs *__restrict__ obs, uint8_t *__restrict__ flags,
@@ -361,6 +364,9 @@ __device__ void classify_run(const GanonReadView &V, const KeyT *__restrict__ ke
   const KeyT key = keys[j0];
   int64_t j1 = j0 + 1;
   while (j1 < n && keys[j1] == key) ++j1;
+#if GANON_CLS_DIAG == 3
+  if (j1 > j0) return;   // (phase timing builds only: results change)
+#endif
   const int scope = obs[vals[j0]].scope;
   const unsigned long long kNone = ~0ull;
   bool any_tn = false;
@@ -390,8 +396,11 @@ __device__ void classify_run(const GanonReadView &V, const KeyT *__restrict__ ke
     }
   }
   if (!any_tn) return;
+#if GANON_CLS_DIAG == 2
+  return;
+#endif
   const int pos = V.span_start[scope] + (int)((unsigned long long)key & ((1ull << pos_bits) - 1ull));
-  if (!normal_covers(V, scope, pos)) {
+  if (GANON_CLS_DIAG != 1 && !normal_covers(V, scope, pos)) {
     for (int64_t a = j0; a < j1; ++a) flags[a] = 0;
     return;
   }

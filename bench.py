@@ -152,6 +152,15 @@ CONFIGS = {
            "generator": "genomeanonymizer_amd.synth.batch.config2_batch", "seed": 2,
            "workload": "BASELINE configs[1]: {reads}-read 150 bp tumor+normal batch, {germline} germline SNPs, "
                        "{windows}-window VCF, {genome} bp / 24 contigs, resident in HBM"},
+    # configs[1] with realistic CIGARs (verdict r04 item 1): germline het deletions 0.1/kb and
+    # sequencing indels 1.5e-4/base, so that ~3 % of the reads carry an I/D op and the germline indel
+    # tally runs in every step
+    "c2id": {"defaults": {"reads": 10_000_000, "genome": 3_000_000_000, "windows": 1_000_000, "germline": 1_000_000},
+             "generator": "genomeanonymizer_amd.synth.batch.config2_batch(germline_del_per_kb=0.1, "
+                          "seq_indel_per_base=1.5e-4)", "seed": 2,
+             "workload": "BASELINE configs[1] with indel CIGARs: {reads}-read 150 bp tumor+normal batch, {germline} "
+                         "germline SNPs + germline het deletions 0.1/kb + sequencing indels 1.5e-4/base (~3 % of "
+                         "the reads aM dD/I bM), {windows}-window VCF, {genome} bp / 24 contigs, resident in HBM"},
     "c3": {"defaults": {"reads": 40_000_000, "genome": 100_000_000, "windows": 10_000, "germline": 100_000},
            "generator": "genomeanonymizer_amd.synth.batch.config2_batch", "seed": 3,
            "workload": "SURVEY C3 density: {reads} 150 bp reads (~60x tumor+normal) on {genome} bp, "
@@ -186,8 +195,9 @@ def make_batch(args, rank: int, k: int = 0):
     if args.config == "c3":
         return config2_batch(n_reads=batch_reads(args, k), genome=args.genome, n_contigs=4, n_windows=args.windows,
                              n_germline=args.germline, seed=seed, window_spacing=10_000, read_seed=rs)
+    idp = {"germline_del_per_kb": 0.1, "seq_indel_per_base": 1.5e-4} if args.config == "c2id" else {}
     return config2_batch(n_reads=batch_reads(args, k), genome=args.genome, n_windows=args.windows,
-                         n_germline=args.germline, seed=seed, read_seed=rs)
+                         n_germline=args.germline, seed=seed, read_seed=rs, **idp)
 
 
 def fastq_bench(masker, db, arr, args, torch, rank: int) -> dict:
@@ -407,8 +417,10 @@ def e2e_lines(args) -> dict:
 
 
 # the SURVEY §8(d) shapes timed beside the metric's line (child processes, before this process
-# initialises the GPU): C3 density at a quarter of its size, C5 long reads at half of the reads
+# initialises the GPU): configs[1] with indel CIGARs at full size, C3 density at a quarter of its
+# size, C5 long reads at half of the reads
 SIDE_CONFIGS = {
+    "c2id": ["--steps", "20", "--warmup", "5"],
     "c3": ["--reads", "10000000", "--genome", "25000000", "--windows", "2500", "--germline", "25000",
            "--steps", "10", "--warmup", "3"],
     "c5": ["--reads", "10000", "--genome", "100000000", "--steps", "5", "--warmup", "2"],

@@ -51,7 +51,14 @@ constexpr uint32_t kSegMine = 1u << 31;     // the segment's read is written by 
 //       (p - ref_start) << 24 (4 bits) | (read_end - p - length) << 28 (4 bits),
 //   w = write scope.
 // wide: one of the two deltas did not fit (the span check then reads ref_start and read_end).
+// A read of 2..kFusedMaxSeg aligned segments (a short read with an I/D/N op, round 5) is always wide
+// and keeps every segment in the extras list instead: x = index of its first extras record, y = its
+// first segment's contig position, z = length << 8 | dataset << 22 | wide | (segments - 1) << 24
+// (3 bits; the query nibble is the extras record's). Extras record (int4, k_prep_scan, at
+// x + k for the read's k-th segment): x = query nibble bits 0-31, y = contig position,
+// z = query nibble bits 32-39 | length << 8, w = 0.
 constexpr uint32_t kDescWide = 1u << 23;
+constexpr int kFusedMaxSeg = 8;   // most aligned segments of a read the fused one-segment mode takes
 // long-read mode: read record (int4; k_prep_read_recs, at b_rbase[read] + k for the read's k-th
 // aligned-segment piece, in CIGAR order): x = query nibble bits 0-31, y = contig position,
 // z = query nibble bits 32-39 | length << 16 (14 bits) | dataset << 30, w = 0 — a segment record
@@ -111,6 +118,11 @@ struct GrpAux {
   const int64_t *incid_off, *ref_off;
   const uint8_t *sdirty;                        // per scope: its reference span holds a non-ACGT block
   const int4 *inc4, *rrec;                      // long-read mode: incidence and read records
+  // fused mode, multi-segment reads: the extras records (k_prep_scan) and, per group, the entries of
+  // its incidences with further segments (k_group's first pass, at the group's first incidence:
+  // x = the read's extras index, y = scope local | further segments << 12 | dataset << 15 | mine << 31)
+  const int4 *xrec;
+  int2 *xlist;
   int32_t n_reads, pad_;
   PrepErr *err;
   unsigned long long *ws_part;
@@ -253,6 +265,13 @@ struct ganon_dbatch {
   // incidence's record in LDS. Off for batches with long-CIGAR reads (the scan does not describe them).
   bool fused = false;
   ganon_dev::DBuf b_desc, b_cand, b_sdirty;
+  // ... and reads of several aligned segments (at most kFusedMaxSeg): their segments as extras records
+  // (b_xrec, allocated by the scan with a counter, capacity xcap records: a plan that needs more grows
+  // it and scans again, a speculative one is gated), the group kernel's per-group entries (b_xlist)
+  ganon_dev::DBuf b_xrec, b_xlist, b_xcnt;
+  int64_t xcap = 0;
+  unsigned int *xcount = nullptr;       // the scan's allocation counters (b_xcnt: one stripe of xcap / 64
+                                        // records per counter, one 128-byte line each; cleared per plan)
   // long-read mode: segment records once per read (b_rrec at b_rbase[read]) and per incidence its
   // first slot in its group, scope and write mark (b_inc4); the group kernel reads the read's
   // records for every scope that lists it

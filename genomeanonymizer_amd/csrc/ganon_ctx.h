@@ -43,8 +43,8 @@ struct ganon_ctx {
   int spec_tgt = 0;
   int prep_unroll = 0;         // GANON_PARAM_PREP_UNROLL (0 auto = 2, 1, 2, 4)
   int far_init = 0;            // GANON_PARAM_FAR_INIT (0 auto)
+  int xrec_init = 0;           // GANON_PARAM_XREC_INIT (0 auto)
   int fused_flat = 1;          // GANON_PARAM_FUSED_FLAT (1: one-segment records made in the group kernel)
-  bool last_full_nonflat = false;   // this context's last full plan was not one-segment mode
   bool step_open = false;      // ganon_batch_replan started a profiled step the next run continues
   std::string err;
   struct Rec { std::string name; hipEvent_t e0, e1; };

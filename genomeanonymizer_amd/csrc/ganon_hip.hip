@@ -351,6 +351,7 @@ struct GrpSharedT {
   int cnt_bases[kGrpMaxScopes];
   int wdirty[kGrpThreads / 64];     // fused one-segment mode: a wave's records need the nt16 reference
   unsigned long long hsum;          // ... and the write-scope hash sum of the group's mine incidences
+  int n_xent, n_xtile;              // ... and its incidences with further segments (entries), an extras tile's records
 };
 
 struct GrpRange {
@@ -614,10 +615,16 @@ __device__ __forceinline__ int grp_tile_flat(SH &sh, const GrpBatch &B, const Gr
       const FlatScope S = sc[j];
       const uint32_t z = (uint32_t)d.z;
       const int n = (int)((z >> 8) & kSegMaxLen), p = d.y;
-      int rs, re;
+      int rs, re, nx = 0;
+      uint64_t sq = (uint64_t)(uint32_t)d.x | ((uint64_t)(z & 0xFF) << 32);
       if (z & kDescWide) {
+        // (a multi-segment read: its first segment's query nibble from its first extras record)
+        nx = (int)((z >> 24) & 7);
+        int4 e0 = make_int4(0, 0, 0, 0);
+        if (nx) e0 = aux->xrec[(uint32_t)d.x];
         rs = aux->ref_start[r];
         re = aux->read_end[r];
+        if (nx) sq = (uint64_t)(uint32_t)e0.x | ((uint64_t)((uint32_t)e0.z & 0xFF) << 32);
       } else {
         rs = p - (int)((z >> 24) & 15);
         re = p + n + (int)(z >> 28);
@@ -632,8 +639,12 @@ __device__ __forceinline__ int grp_tile_flat(SH &sh, const GrpBatch &B, const Gr
         if (first && mine) hsum += ws_hash(r);
         if (!huge && n > 0) {
           const int64_t r0 = (int64_t)(S.pk << 22) >> 22;
-          const uint64_t sq = (uint64_t)(uint32_t)d.x | ((uint64_t)(z & 0xFF) << 32);
           const uint64_t rf = (uint64_t)(r0 + p);
+          if (first && nx) {   // its further segments: an entry in the group's list (streamed after the incidences)
+            const int k = atomicAdd(&sh.n_xent, 1);
+            aux->xlist[i_begin + k] = make_int2(d.x, (int)((uint32_t)j | ((uint32_t)nx << 12) | (((z >> 22) & 1u) << 15) |
+                                                           (mine ? 0x80000000u : 0u)));
+          }
           const uint32_t rz = (uint32_t)((sq >> 32) & 0xFF) | ((uint32_t)((rf >> 32) & 0xFF) << 8) |
                               ((uint32_t)n << 16) | (((z >> 22) & 1u) << 30) | (mine ? kSegMine : 0u);
           rec = make_int4((int)(uint32_t)sq, (int)(uint32_t)rf, (int)rz,
@@ -844,6 +855,11 @@ __device__ __forceinline__ void grp_scan_long(const GrpBatch &B, SH &sh, const G
   }
 }
 
+template <int K, class SH>
+__device__ __forceinline__ void grp_scan_extra(const GrpBatch &B, SH &sh, const GrpRange &R,
+                                                         const GrpGlobal &gg, const GrpAux *__restrict__ aux,
+                                                         int64_t i_begin, int n_e, int skip);
+
 // Fused one-segment mode: the same stream over records made from incidences [i_begin, i_end) tile
 // by tile (grp_tile_flat), each tile through the 2-bit reference when all of its records allow.
 template <int K, class SH>
@@ -868,6 +884,93 @@ __device__ __forceinline__ void grp_scan_flat(const GrpBatch &B, SH &sh, const G
       for (int t = tid; t < total; t += kGrpThreads) grp_chunk<K, false>(B, sh, R, gg, t, grp_find(sh, nh, total, t));
     }
     __syncthreads();
+  }
+  // multi-segment reads (short reads with an I/D/N op): their further segments, from the entries the
+  // first pass listed — a segment's observations are those of any other record of its scope, so they
+  // may come after the incidences
+  if (first) {   // (the entries' stores at L2 before any thread reads them back)
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+  }
+  const int n_e = sh.n_xent;
+  if (n_e) grp_scan_extra<K>(B, sh, R, gg, aux, i_begin, n_e, skip);
+}
+
+// Block-wide exclusive prefix sum of v (every thread calls; ends on a barrier); *total = the sum.
+template <class SH>
+__device__ __forceinline__ int blk_excl_sum(SH &sh, int v, int *total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int incl = ganon_wave::incl_sum(v);
+  if (lane == 63) sh.wsum[wave] = incl;
+  __syncthreads();
+  int base = 0, t = 0;
+#pragma unroll
+  for (int w = 0; w < kGrpThreads / 64; ++w) {
+    const int x = sh.wsum[w];
+    base += w < wave ? x : 0;
+    t += x;
+  }
+  *total = t;
+  __syncthreads();   // (sh.wsum is free again)
+  return base + incl - v;
+}
+
+// The fused mode's extras tiles: the group's n_e entries (an incidence of a multi-segment read each:
+// its read's extras index, scope, further segments, dataset, write mark) expanded into the records
+// of their further segments, as many whole entries per tile as fit its kGrpTile records (an entry
+// has at most kFusedMaxSeg - 1), then streamed like any tile.
+template <int K, class SH>
+__device__ __forceinline__ void grp_scan_extra(const GrpBatch &B, SH &sh, const GrpRange &R,
+                                                         const GrpGlobal &gg, const GrpAux *__restrict__ aux,
+                                                         int64_t i_begin, int n_e, int skip) {
+  const int tid = opaque_tid();
+  const FlatScope *sc = flat_scopes(sh);
+  const unsigned long long *xl = reinterpret_cast<const unsigned long long *>(aux->xlist) + i_begin;
+  for (int e0 = 0; e0 < n_e;) {
+    const int m = min(n_e - e0, kGrpTile);
+    unsigned long long ent = 0;
+    if (tid < m) ent = ld_l2(xl + e0 + tid);   // (written by this workgroup's first pass: read past L1)
+    const uint32_t ey = (uint32_t)(ent >> 32);
+    const int nx = tid < m ? (int)((ey >> 12) & 7) : 0;
+    int total;
+    const int pre = blk_excl_sum(sh, nx, &total);
+    const bool fit = tid < m && pre + nx <= kGrpTile;
+    if (fit) {
+      const int j = (int)(ey & 0xFFF);
+      const FlatScope S = sc[j];
+      const int64_t r0 = (int64_t)(S.pk << 22) >> 22;
+      const uint32_t xi = (uint32_t)ent;
+      const uint32_t hi = (((ey >> 15) & 1u) << 30) | (ey & kSegMine);
+      for (int k = 0; k < nx; ++k) {
+        const int4 e = aux->xrec[xi + 1 + k];
+        const uint32_t z = (uint32_t)e.z;
+        const int n = (int)((z >> 8) & kSegMaxLen), p = e.y;
+        const uint64_t rf = (uint64_t)(r0 + p);
+        const uint32_t rz = (z & 0xFFu) | ((uint32_t)((rf >> 32) & 0xFF) << 8) | ((uint32_t)n << 16) | hi;
+        sh.rec[pre + k] = make_int4(e.x, (int)(uint32_t)rf, (int)rz, (int)((uint32_t)j | ((uint32_t)(p - S.sstart) << 12)));
+      }
+    }
+    const int used = __syncthreads_count(fit);   // (the fitting entries are a prefix: every nx >= 1)
+    if (fit && tid == used - 1) sh.n_xtile = pre + nx;
+    __syncthreads();
+    const int nh = sh.n_xtile;
+    int nck = 0;
+    bool dirty = false;
+    if (tid < nh) {
+      const int4 r = sh.rec[tid];
+      nck = ((((uint32_t)r.z >> 16) & kSegMaxLen) + 16 * K - 1) / (16 * K);
+      dirty = (sc[r.w & 0xFFF].pk >> 63) != 0;
+    }
+    const bool clean = !__syncthreads_or(dirty);
+    int tot = grp_tile_map(sh, nck);
+    if (skip & kSkipChunks) tot = 0;
+    if (clean && B.ref2) {
+      for (int t = tid; t < tot; t += kGrpThreads) grp_chunk<K, true>(B, sh, R, gg, t, grp_find(sh, nh, tot, t));
+    } else {
+      for (int t = tid; t < tot; t += kGrpThreads) grp_chunk<K, false>(B, sh, R, gg, t, grp_find(sh, nh, tot, t));
+    }
+    __syncthreads();
+    e0 += used;
   }
 }
 
@@ -1246,6 +1349,7 @@ __global__ void __launch_bounds__(kGrpThreads, (OBS > 512 ? 4 : U == 1 ? 6 : U =
     sh.blk_calls = 0;
     sh.blk_bases = 0;
     sh.hsum = 0;
+    sh.n_xent = 0;
   }
   for (int i = tid; i < kGrpMaxScopes; i += kGrpThreads) {
     sh.cnt_calls[i] = 0;
@@ -1624,7 +1728,7 @@ void free_batch(ganon_dbatch *db) {
                   &db->b_seg4, &db->b_grp_part, &db->b_far, &db->b_gokey, &db->b_gopay, &db->b_gtkey, &db->b_gtflag,
                   &db->b_out, &db->b_scope_calls, &db->b_scope_bases, &db->b_small, &db->b_part, &db->b_long, &db->b_nseg,
                   &db->b_scost, &db->b_scan_tmp, &db->b_slots, &db->b_slot0, &db->b_order, &db->b_desc, &db->b_cand,
-                  &db->b_sdirty, &db->b_inc4, &db->b_rbase, &db->b_rrec};
+                  &db->b_sdirty, &db->b_inc4, &db->b_rbase, &db->b_rrec, &db->b_xrec, &db->b_xlist, &db->b_xcnt};
   for (DBuf *b : bufs) free_buf(*b);
   free_huge(db);
   free_ref(db->own_ref);
@@ -1859,6 +1963,8 @@ int prepare(ganon_ctx *ctx, ganon_dbatch *db, const ganon_batch *host, bool allo
   a.sdirty = static_cast<const uint8_t *>(db->b_sdirty.p);
   a.inc4 = static_cast<const int4 *>(db->b_inc4.p);
   a.rrec = static_cast<const int4 *>(db->b_rrec.p);
+  a.xrec = static_cast<const int4 *>(db->b_xrec.p);
+  a.xlist = static_cast<int2 *>(db->b_xlist.p);
   a.n_reads = db->n_reads;
   a.err = db->err;
   a.ws_part = static_cast<unsigned long long *>(db->b_wspart.p);
@@ -2115,6 +2221,11 @@ GANON_API int ganon_ctx_set_param(ganon_ctx *ctx, int param, int value) {
   if (param == GANON_PARAM_FUSED_FLAT) {
     if (value != 0 && value != 1) return fail(ctx, GANON_E_ARG, "fused one-segment mode: 0 or 1 (got %d)", value);
     ctx->fused_flat = value;
+    return GANON_OK;
+  }
+  if (param == GANON_PARAM_XREC_INIT) {
+    if (value < 0) return fail(ctx, GANON_E_ARG, "extras list capacity must be >= 0");
+    ctx->xrec_init = value;
     return GANON_OK;
   }
   if (param == GANON_PARAM_FAR_INIT) {
@@ -2450,7 +2561,8 @@ GANON_API int ganon_batch_shape(ganon_dbatch *db, int64_t *shape) {
   shape[0] = db->n_id_ops;
   shape[1] = db->max_len;
   shape[2] = db->max_seg;
-  shape[3] = db->long_mode ? 1 : db->flat_mode ? (db->fused ? 3 : 2) : 0;
+  // (4: fused with multi-segment reads, found by a full plan; a speculative plan reports 3)
+  shape[3] = db->long_mode ? 1 : db->flat_mode ? (db->fused ? (db->max_seg > 1 && !db->spec ? 4 : 3) : 2) : 0;
   return GANON_OK;
 }
 

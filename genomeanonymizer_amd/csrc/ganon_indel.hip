@@ -92,7 +92,11 @@ struct IndelObs {       // one I/D op of one incidence
 };
 
 // Candidate map: 2 bits per genome position (bit 0: a tumor read has an I/D op there, bit 1: a
-// normal read has). A TN call at (scope, pos) needs a tumor and a normal read with an op at pos, so
+// normal read has) — or, when the batch has far fewer I/D ops than the genome has positions (a
+// short-read batch: ~3e5 ops on 3 Gb), 2 bits per cell of a hashed map of at least 64 cells per
+// op (map_cell): cleared per run in microseconds instead of a 750 MB memset. A collision can only
+// add a position (its observations are then emitted and classified, and it holds no TN call: one of
+// its datasets had no op there); no position with both bits is ever lost. A TN call at (scope, pos) needs a tumor and a normal read with an op at pos, so
 // a position missing either bit has no TN call in any scope; the other calls at such a position
 // only matter as the rank of a TN call there (registration order among the calls at pos), and
 // there is none. Its observations are not emitted (GANON_PARAM_INDEL_SORT 0); every observation
@@ -107,6 +111,12 @@ template <typename KeyT>
 __device__ __forceinline__ KeyT make_key(uint32_t scope_par, int pos_bits, uint32_t rel) {
   if constexpr (sizeof(KeyT) == 4) return (scope_par & 0x80000000u) | rel;
   else return ((unsigned long long)(scope_par & 0x7FFFFFFFu) << pos_bits) | rel;
+}
+
+// Map cell of genome nibble g: g itself (dense map, shift 0) or the top bits of a multiplicative
+// hash (hashed map of 2^(64 - shift) cells).
+__device__ __forceinline__ uint64_t map_cell(int64_t g, int shift) {
+  return shift ? ((uint64_t)g * 0x9E3779B97F4A7C15ull) >> shift : (uint64_t)g;
 }
 
 constexpr int kIndelWaves = 4;
@@ -164,7 +174,7 @@ __device__ __forceinline__ void walk_block(const GanonReadView &V, int r, int k0
 // Candidate marking: one wave per block of a read with an I/D op (each read once, whatever its
 // scopes): its dataset's bit at every op position (no-return atomics, nothing waits on them).
 __global__ void __launch_bounds__(kIndelThreads) k_indel_mark(const GanonReadView V, const IndelRead *__restrict__ reads,
-                                                              int64_t n_reads, uint32_t *__restrict__ map) {
+                                                              int64_t n_reads, uint32_t *__restrict__ map, int shift) {
   const int lane = threadIdx.x & 63;
   const int64_t w = (int64_t)blockIdx.x * kIndelWaves + (threadIdx.x >> 6);
   if (w >= n_reads) return;
@@ -173,21 +183,25 @@ __global__ void __launch_bounds__(kIndelThreads) k_indel_mark(const GanonReadVie
   walk_block(V, e.read, e.k0, e.pos0, 0, lane, [&](const CigarStep (&c)[kWalkJ]) {
 #pragma unroll
     for (int j = 0; j < kWalkJ; ++j) {
-      const int64_t g = e.cbase + c[j].pos;
+      const uint64_t g = map_cell(e.cbase + c[j].pos, shift);
       if (c[j].is_id) atomicOr(map + (g >> 4), 1u << (2 * (g & 15) + ds));
     }
   });
 }
 
 // Candidate bits of kWalkJ steps, their map words loaded together.
-__device__ __forceinline__ void cand_bits(const uint32_t *__restrict__ map, int64_t cbase,
+__device__ __forceinline__ void cand_bits(const uint32_t *__restrict__ map, int shift, int64_t cbase,
                                           const CigarStep (&c)[kWalkJ], bool (&hit)[kWalkJ]) {
   uint32_t mw[kWalkJ];
+  uint64_t g[kWalkJ];
 #pragma unroll
-  for (int j = 0; j < kWalkJ; ++j) mw[j] = c[j].is_id ? map[(cbase + c[j].pos) >> 4] : 0u;
+  for (int j = 0; j < kWalkJ; ++j) {
+    g[j] = map_cell(cbase + c[j].pos, shift);
+    mw[j] = c[j].is_id ? map[g[j] >> 4] : 0u;
+  }
 #pragma unroll
   for (int j = 0; j < kWalkJ; ++j)
-    hit[j] = c[j].is_id && ((mw[j] >> (2 * ((cbase + c[j].pos) & 15))) & 3) == 3;   // tumor and normal
+    hit[j] = c[j].is_id && ((mw[j] >> (2 * (g[j] & 15))) & 3) == 3;   // tumor and normal
 }
 
 // The unfiltered path (GANON_PARAM_INDEL_SORT 1, one global sort): every I/D op of every listed
@@ -233,7 +247,7 @@ __global__ void __launch_bounds__(kIndelThreads) k_indel_emit(const GanonReadVie
 // entries with the scope's key (k_indel_expand).
 __global__ void __launch_bounds__(kIndelThreads) k_indel_rcount(const GanonReadView V, const IndelRead *__restrict__ reads,
                                                                 int64_t n_reads, const uint32_t *__restrict__ map,
-                                                                int32_t *__restrict__ cnt) {
+                                                                int shift, int32_t *__restrict__ cnt) {
   const int lane = threadIdx.x & 63;
   const int64_t w = (int64_t)blockIdx.x * kIndelWaves + (threadIdx.x >> 6);
   if (w >= n_reads) return;
@@ -241,7 +255,7 @@ __global__ void __launch_bounds__(kIndelThreads) k_indel_rcount(const GanonReadV
   int total = 0;
   walk_block(V, e.read, e.k0, e.pos0, e.irp0, lane, [&](const CigarStep (&c)[kWalkJ]) {
     bool hit[kWalkJ];
-    cand_bits(map, e.cbase, c, hit);
+    cand_bits(map, shift, e.cbase, c, hit);
 #pragma unroll
     for (int j = 0; j < kWalkJ; ++j) total += __popcll(__ballot(hit[j]));
   });
@@ -250,7 +264,7 @@ __global__ void __launch_bounds__(kIndelThreads) k_indel_rcount(const GanonReadV
 
 __global__ void __launch_bounds__(kIndelThreads) k_indel_remit(const GanonReadView V, const IndelRead *__restrict__ reads,
                                                                int64_t n_reads, const uint32_t *__restrict__ map,
-                                                               const int32_t *__restrict__ roff,
+                                                               int shift, const int32_t *__restrict__ roff,
                                                                IndelCand *__restrict__ rcand) {
   const int lane = threadIdx.x & 63;
   const int64_t w = (int64_t)blockIdx.x * kIndelWaves + (threadIdx.x >> 6);
@@ -261,7 +275,7 @@ __global__ void __launch_bounds__(kIndelThreads) k_indel_remit(const GanonReadVi
   const unsigned long long below = (1ull << lane) - 1ull;
   walk_block(V, e.read, e.k0, e.pos0, e.irp0, lane, [&](const CigarStep (&c)[kWalkJ]) {
     bool keep[kWalkJ];
-    cand_bits(map, e.cbase, c, keep);
+    cand_bits(map, shift, e.cbase, c, keep);
 #pragma unroll
     for (int j = 0; j < kWalkJ; ++j) {
       const unsigned long long m_all = __ballot(c[j].is_id);
@@ -311,6 +325,97 @@ __global__ void __launch_bounds__(kIndelThreads) k_indel_expand(const GanonReadV
     obs[o] = ob;
     keys[o] = make_key<KeyT>(e.scope_par, pos_bits, (uint32_t)(c.pos - span0));
     vals[o] = (uint32_t)o;
+  }
+}
+
+// ---- short reads (round 5): a thread per read and per incidence ---------------------------------
+// A 150 bp read with an indel has 3 CIGAR ops: a wave per read block (above) left 61 of its 64 lanes
+// idle, and the ~3e5 indel reads of a c2id batch cost ~0.09 ms per walk kernel in wave launches
+// alone. Batches whose reads with I/D ops all have at most kThreadWalkOps ops walk them a thread
+// each; the same op order, positions and counts as walk_block.
+constexpr int kThreadWalkOps = 32;
+
+template <typename F>
+__device__ __forceinline__ void thread_walk(const GanonReadView &V, const IndelRead &e, F &&f) {
+  const int nc = V.n_cig[e.read];
+  const uint32_t *__restrict__ cig = V.cigar + V.cig_off[e.read];
+  int pos = e.pos0, irp = e.irp0;
+  for (int k = e.k0; k < nc; ++k) {
+    const uint32_t w = cig[k];
+    const int op = (int)(w & 0xF), len = (int)(w >> 4);
+    if (op == 1 || op == 2) f(pos, irp, op, len);
+    pos += (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) ? len : 0;
+    irp += (op == 0 || op == 1 || op == 3 || op == 4 || op == 5 || op == 7 || op == 8) ? len : 0;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_indel_mark_t(const GanonReadView V, const IndelRead *__restrict__ reads,
+                                                      int64_t n_reads, uint32_t *__restrict__ map, int shift) {
+  const int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (w >= n_reads) return;
+  const IndelRead e = reads[w];
+  const uint32_t ds = V.dataset[e.read] & 1u;
+  thread_walk(V, e, [&](int pos, int, int, int) {
+    const uint64_t g = map_cell(e.cbase + pos, shift);
+    atomicOr(map + (g >> 4), 1u << (2 * (g & 15) + ds));
+  });
+}
+
+__device__ __forceinline__ bool cand_bit(const uint32_t *__restrict__ map, int shift, int64_t gpos) {
+  const uint64_t g = map_cell(gpos, shift);
+  return ((map[g >> 4] >> (2 * (g & 15))) & 3) == 3;
+}
+
+__global__ void __launch_bounds__(256) k_indel_rcount_t(const GanonReadView V, const IndelRead *__restrict__ reads,
+                                                        int64_t n_reads, const uint32_t *__restrict__ map, int shift,
+                                                        int32_t *__restrict__ cnt) {
+  const int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (w >= n_reads) return;
+  const IndelRead e = reads[w];
+  int total = 0;
+  thread_walk(V, e, [&](int pos, int, int, int) { total += cand_bit(map, shift, e.cbase + pos) ? 1 : 0; });
+  cnt[w] = total;
+}
+
+__global__ void __launch_bounds__(256) k_indel_remit_t(const GanonReadView V, const IndelRead *__restrict__ reads,
+                                                       int64_t n_reads, const uint32_t *__restrict__ map, int shift,
+                                                       const int32_t *__restrict__ roff, IndelCand *__restrict__ rcand) {
+  const int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (w >= n_reads) return;
+  const IndelRead e = reads[w];
+  int64_t slot = roff[w];
+  int ord = e.nid0;
+  thread_walk(V, e, [&](int pos, int irp, int op, int len) {
+    if (cand_bit(map, shift, e.cbase + pos)) rcand[slot++] = IndelCand{pos, irp, (len << 1) | (op == 1 ? 1 : 0), ord};
+    ++ord;
+  });
+}
+
+template <typename KeyT>
+__global__ void __launch_bounds__(256) k_indel_expand_t(const GanonReadView V, const IndelIncR *__restrict__ inc,
+                                                        int64_t n_inc, int pos_bits, const int32_t *__restrict__ roff,
+                                                        const IndelCand *__restrict__ rcand,
+                                                        const int32_t *__restrict__ off, IndelObs *__restrict__ obs,
+                                                        KeyT *__restrict__ keys, uint32_t *__restrict__ vals) {
+  const int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (w >= n_inc) return;
+  const IndelIncR e = inc[w];
+  const int64_t a = roff[e.rfirst], n = roff[e.rfirst + e.rnb] - a;
+  if (!n) return;
+  const int scope = (int)(e.scope_par & 0x7FFFFFFFu);
+  const int span0 = V.span_start[scope];
+  const int64_t o0 = off[w];
+  for (int64_t k = 0; k < n; ++k) {
+    const IndelCand c = rcand[a + k];
+    IndelObs ob;
+    ob.read = e.read;
+    ob.irp = c.irp;
+    ob.scope = scope;
+    ob.type_len = c.type_len;
+    ob.ord = (uint32_t)(e.obs_base + c.ord);
+    obs[o0 + k] = ob;
+    keys[o0 + k] = make_key<KeyT>(e.scope_par, pos_bits, (uint32_t)(c.pos - span0));
+    vals[o0 + k] = (uint32_t)(o0 + k);
   }
 }
 
@@ -558,8 +663,10 @@ struct ganon_indels {
   bool global = false;                // strategy of the last run (GANON_PARAM_INDEL_SORT 1)
   IndelInc *list = nullptr;
   IndelRead *rdist = nullptr;         // distinct reads with an I/D op (candidate marking)
-  uint32_t *map = nullptr;            // candidate map, 2 bits per genome position
+  uint32_t *map = nullptr;            // candidate map, 2 bits per genome position or hashed cell
   int64_t map_words = 0;
+  int map_shift = 0;                  // 0: dense (a cell per genome position), else hashed (map_cell)
+  bool thread_walk = false;           // every read with an I/D op has at most kThreadWalkOps CIGAR ops
   int32_t *cnt = nullptr;             // [n_list + 1] candidate observations per incidence (ilist)
   int32_t *off = nullptr;             // [n_list + 1] their exclusive scan; off[n_ilist] = count
   IndelIncR *ilist = nullptr;         // incidences with an I/D op (filtered path)
@@ -650,14 +757,27 @@ int run_tally(ganon_ctx *ctx, ganon_indels *t) {
     // from the read's, their scan, the segments
     KernelScope ks(ctx, "indel_candidates");
     HIP_OR_FAIL(hipMemsetAsync(t->map, 0, (size_t)t->map_words * 4, ctx->stream));
-    hipLaunchKernelGGL(k_indel_mark, dim3(rgrid), dim3(kIndelThreads), 0, ctx->stream, t->V, t->rdist, t->n_rdist, t->map);
-    hipLaunchKernelGGL(k_indel_rcount, dim3(rgrid), dim3(kIndelThreads), 0, ctx->stream, t->V, t->rdist, t->n_rdist,
-                       t->map, t->rcnt);
+    const unsigned tgrid = (unsigned)((t->n_rdist + 255) / 256);
+    if (t->thread_walk) {
+      hipLaunchKernelGGL(k_indel_mark_t, dim3(tgrid), dim3(256), 0, ctx->stream, t->V, t->rdist, t->n_rdist, t->map,
+                         t->map_shift);
+      hipLaunchKernelGGL(k_indel_rcount_t, dim3(tgrid), dim3(256), 0, ctx->stream, t->V, t->rdist, t->n_rdist, t->map,
+                         t->map_shift, t->rcnt);
+    } else {
+      hipLaunchKernelGGL(k_indel_mark, dim3(rgrid), dim3(kIndelThreads), 0, ctx->stream, t->V, t->rdist, t->n_rdist,
+                         t->map, t->map_shift);
+      hipLaunchKernelGGL(k_indel_rcount, dim3(rgrid), dim3(kIndelThreads), 0, ctx->stream, t->V, t->rdist, t->n_rdist,
+                         t->map, t->map_shift, t->rcnt);
+    }
     size_t bytes = t->temp_bytes;
     if (scan_read_counts(t, t->temp, bytes, ctx->stream) != hipSuccess)
       return fail(ctx, GANON_E_DEVICE, "indel read scan failed");
-    hipLaunchKernelGGL(k_indel_remit, dim3(rgrid), dim3(kIndelThreads), 0, ctx->stream, t->V, t->rdist, t->n_rdist,
-                       t->map, t->roff, t->rcand);
+    if (t->thread_walk)
+      hipLaunchKernelGGL(k_indel_remit_t, dim3(tgrid), dim3(256), 0, ctx->stream, t->V, t->rdist, t->n_rdist, t->map,
+                         t->map_shift, t->roff, t->rcand);
+    else
+      hipLaunchKernelGGL(k_indel_remit, dim3(rgrid), dim3(kIndelThreads), 0, ctx->stream, t->V, t->rdist, t->n_rdist,
+                         t->map, t->map_shift, t->roff, t->rcand);
     hipLaunchKernelGGL(k_indel_icount, dim3((unsigned)((t->n_ilist + 255) / 256)), dim3(256), 0, ctx->stream, t->ilist,
                        t->n_ilist, t->roff, t->cnt);
     bytes = t->temp_bytes;
@@ -668,7 +788,11 @@ int run_tally(ganon_ctx *ctx, ganon_indels *t) {
   }
   {
     KernelScope ks(ctx, "k_indel_emit");
-    if (filter)
+    if (filter && t->thread_walk)
+      hipLaunchKernelGGL(k_indel_expand_t<KeyT>, dim3((unsigned)((t->n_ilist + 255) / 256)), dim3(256), 0, ctx->stream,
+                         t->V, t->ilist, t->n_ilist, t->pos_bits, t->roff, t->rcand, t->off, t->obs,
+                         static_cast<KeyT *>(t->keys[0]), t->vals[0]);
+    else if (filter)
       hipLaunchKernelGGL(k_indel_expand<KeyT>, dim3((unsigned)((t->n_ilist + kIndelWaves - 1) / kIndelWaves)),
                          dim3(kIndelThreads), 0, ctx->stream, t->V, t->ilist, t->n_ilist, t->pos_bits, t->roff, t->rcand,
                          t->off, t->obs, static_cast<KeyT *>(t->keys[0]), t->vals[0]);
@@ -713,6 +837,7 @@ GANON_API int ganon_indel_upload(ganon_ctx *ctx, const ganon_batch *b, const gan
     return fail(ctx, GANON_E_ARG, "indel upload: host batch does not match the device batch");
   // per read: I/D ops (the host CIGARs were validated by ganon_batch_upload)
   std::vector<int32_t> nid(b->n_reads, 0);
+  int32_t max_nc_id = 0;   // most CIGAR ops of a read with an I/D op (the thread-walk kernels' bound)
   for (int32_t r = 0; r < b->n_reads; ++r) {
     const uint32_t *c = b->cigar + b->cig_off[r];
     int32_t k = 0;
@@ -721,6 +846,7 @@ GANON_API int ganon_indel_upload(ganon_ctx *ctx, const ganon_batch *b, const gan
       k += (op == 1 || op == 2);
     }
     nid[r] = k;
+    if (k) max_nc_id = std::max(max_nc_id, b->n_cig[r]);
   }
   // per read with an I/D op: the reference's running offsets at every kWalkOps-th op, and the I/D
   // ops before it (process_indels arithmetic, variation_classifier.py:52-141)
@@ -795,6 +921,19 @@ GANON_API int ganon_indel_upload(ganon_ctx *ctx, const ganon_batch *b, const gan
   t->pos_bits = bits_for((int64_t)max_span);
   t->key_bits = t->pos_bits + bits_for(std::max<int64_t>((int64_t)b->n_scopes - 1, 1));
   t->map_words = (2 * b->ref_bytes + 64) / 16 + 1;
+  {
+    const char *tw = getenv("GANON_INDEL_WAVE_WALK");   // (A/B: 1 keeps the wave-per-block walks)
+    t->thread_walk = max_nc_id <= kThreadWalkOps && !(tw && tw[0] == '1');
+    // hashed map: 2^k cells, at least 64 per candidate-marking op, when that is smaller than the
+    // genome's positions (env GANON_INDEL_DENSE_MAP=1: always dense, A/B)
+    int k = 12;
+    while (k < 40 && (int64_t(1) << k) < 64 * std::max<int64_t>(n_rcand, 1)) ++k;
+    const char *dense = getenv("GANON_INDEL_DENSE_MAP");
+    if ((int64_t(1) << k) / 16 + 1 < t->map_words && !(dense && dense[0] == '1')) {
+      t->map_words = (int64_t(1) << k) / 16;
+      t->map_shift = 64 - k;
+    }
+  }
   int rc = GANON_OK;
   auto bail = [&](int code) {
     ind_release(t);

@@ -210,6 +210,7 @@ PARAM_PREP_UNROLL = 11   # include/ganon.h GANON_PARAM_PREP_UNROLL (0 auto, 1, 2
 PARAM_FAR_INIT = 12      # include/ganon.h GANON_PARAM_FAR_INIT (first far-mask list capacity; 0 auto)
 PARAM_SPEC_PLAN = 13     # include/ganon.h GANON_PARAM_SPEC_PLAN (1 speculative replans, 0 synchronous)
 PARAM_FUSED_FLAT = 14    # include/ganon.h GANON_PARAM_FUSED_FLAT (1 one-segment records in the group kernel, 0 record pass)
+PARAM_XREC_INIT = 15     # include/ganon.h GANON_PARAM_XREC_INIT (first extras list capacity; 0 auto)
 
 EXPORTED_HIP_SYMBOLS = (
     "ganon_ctx_create", "ganon_ctx_destroy", "ganon_last_error", "ganon_abi_version",
@@ -742,7 +743,8 @@ class DeviceBatch:
         a = np.zeros(4, np.int64)
         self.m._check(self.m._lib.ganon_batch_shape(self.h, _ptr(a, _i64p)), "batch_shape")
         return {"id_ops": int(a[0]), "max_len": int(a[1]), "max_seg": int(a[2]),
-                "prep_mode": ("two_pass", "long_read", "one_segment", "one_segment_fused")[int(a[3])]}
+                "prep_mode": ("two_pass", "long_read", "one_segment", "one_segment_fused",
+                              "multi_segment_fused")[int(a[3])]}
 
     def kernel_times(self) -> list:
         arr = (KernelTime * 32)()

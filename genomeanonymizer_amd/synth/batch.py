@@ -610,16 +610,23 @@ _SITES_CACHE: Dict[tuple, tuple] = {}
 
 def config2_batch(n_reads: int = 10_000_000, genome: int = 3_000_000_000, n_contigs: int = 24,
                   n_windows: int = 1_000_000, n_germline: int = 1_000_000, read_len: int = 150,
-                  seed: int = 2, window_spacing: int = 2500, read_seed: int = None) -> Tuple[Dict[str, np.ndarray], dict]:
+                  seed: int = 2, window_spacing: int = 2500, read_seed: int = None,
+                  germline_del_per_kb: float = 0.0, seq_indel_per_base: float = 0.0) -> Tuple[Dict[str, np.ndarray], dict]:
     """Vectorised BASELINE configs[1] batch. Returns (arrays, info). ``read_seed``: the reads come
     from their own generator (the genome, germline sites and windows from ``seed``, generated once
-    per process and shared): batches of other reads on the same sample."""
+    per process and shared): batches of other reads on the same sample.
+
+    Realistic CIGARs (the ``c2id`` shape): ``germline_del_per_kb`` het deletions of 1-3 bp per kb of
+    genome (on haplotype 1 of tumor and normal alike, as synth/fastpair.py plants them: a read of
+    haplotype 1 over one is ``aM dD bM``), and ``seq_indel_per_base`` sequencing indels of 1-3 bp
+    (a read with one is ``aM dI/D bM``). Zero (the default) keeps every read ``150M``."""
     L = read_len
     key = (seed, genome, n_contigs, n_windows, n_germline, window_spacing)
+    idp = (germline_del_per_kb, seq_indel_per_base)
     if read_seed is not None and key in _SITES_CACHE:
         clen, cstart, ref, gsnp, galt, win_contig, win_pos = _SITES_CACHE[key]
         return _config2_reads(np.random.default_rng(read_seed), n_reads, L, n_contigs, clen, cstart, ref, gsnp, galt,
-                              win_contig, win_pos)
+                              win_contig, win_pos, idp)
     rng = np.random.default_rng(seed)
     # contigs: 24 of decreasing length summing to `genome`, each starting on a byte boundary
     w = np.linspace(2.0, 1.0, n_contigs)
@@ -649,10 +656,44 @@ def config2_batch(n_reads: int = 10_000_000, genome: int = 3_000_000_000, n_cont
     if read_seed is not None:
         _SITES_CACHE[key] = (clen, cstart, ref, gsnp, galt, win_contig, win_pos)
         rng = np.random.default_rng(read_seed)
-    return _config2_reads(rng, n_reads, L, n_contigs, clen, cstart, ref, gsnp, galt, win_contig, win_pos)
+    return _config2_reads(rng, n_reads, L, n_contigs, clen, cstart, ref, gsnp, galt, win_contig, win_pos, idp)
 
 
-def _config2_reads(rng, n_reads, L, n_contigs, clen, cstart, ref, gsnp, galt, win_contig, win_pos):
+def _read_indels(rng, n, L, gstart, hap, del_per_kb, seq_per_base, genome_seed):
+    """Per read (offset a, length d, kind: 0 none, 1 deletion, 2 insertion) for the c2id shape:
+    germline het deletions (a deterministic site set of the genome: hash of the 1-kb bin, so every
+    batch of the sample sees the same sites) on haplotype-1 reads, then sequencing indels on reads
+    without one."""
+    a = np.zeros(n, np.int64)
+    d = np.zeros(n, np.int64)
+    kind = np.zeros(n, np.int8)
+    if del_per_kb > 0:
+        # sites: bin b of 1 kb holds a deletion iff hash(b) < del_per_kb; position and length from the hash
+        def h(x):
+            x = (x.astype(np.uint64) + np.uint64(genome_seed) * np.uint64(0x9E3779B97F4A7C15)) & np.uint64(2**64 - 1)
+            x ^= x >> np.uint64(31)
+            x *= np.uint64(0xBF58476D1CE4E5B9)
+            x ^= x >> np.uint64(29)
+            return x
+        with np.errstate(over="ignore"):
+            for b in (gstart // 1000, gstart // 1000 + 1):   # a 150 bp read touches at most two bins
+                hv = h(b)
+                has = (hv >> np.uint64(40)).astype(np.float64) / float(1 << 24) < del_per_kb
+                site = b * 1000 + ((hv & np.uint64(0xFFFF)).astype(np.int64) % 1000)
+                ln = 1 + ((hv >> np.uint64(16)) & np.uint64(3)).astype(np.int64) % 3
+                off = site - gstart
+                ok = has & hap & (kind == 0) & (off >= 10) & (off <= L - 10)
+                a[ok], d[ok], kind[ok] = off[ok], ln[ok], 1
+    if seq_per_base > 0:
+        hit = (rng.random(n) < seq_per_base * L) & (kind == 0)
+        k = int(hit.sum())
+        a[hit] = rng.integers(10, L - 10, k)
+        d[hit] = rng.integers(1, 4, k)
+        kind[hit] = np.where(rng.random(k) < 0.5, 1, 2)
+    return a, d, kind
+
+
+def _config2_reads(rng, n_reads, L, n_contigs, clen, cstart, ref, gsnp, galt, win_contig, win_pos, idp=(0.0, 0.0)):
     def ref_codes(gpos: np.ndarray) -> np.ndarray:
         b = ref[gpos >> 1]
         return np.where(gpos & 1, b & 0xF, b >> 4).astype(np.uint8)
@@ -672,22 +713,40 @@ def _config2_reads(rng, n_reads, L, n_contigs, clen, cstart, ref, gsnp, galt, wi
     rc, rpos, rds, hap = rc[order], rpos[order], rds[order], hap[order]
     gstart = cstart[rc] + rpos
     n = len(rpos)
+    del_kb, seq_pb = idp
+    with_id = del_kb > 0 or seq_pb > 0
+    ia, idd, ikind = _read_indels(rng, n, L, gstart, hap, del_kb, seq_pb, int(cstart[-1]) + len(ref)) if with_id \
+        else (None, None, None)
+    W = L + 3 if with_id else L    # (a deletion's read takes up to 3 reference bases past L)
     # bases: reference + germline het alts on haplotype 1 + 0.1 % errors
     # (the genome one code per byte, each read's codes one row of a sliding-window view: a row copy
     # per read instead of a per-base gather)
-    nib = np.empty(2 * len(ref), np.uint8)
-    nib[0::2] = ref >> 4
-    nib[1::2] = ref & 0xF
-    codes = np.lib.stride_tricks.sliding_window_view(nib, L)[gstart]
+    nib = np.zeros(2 * len(ref) + 4, np.uint8)
+    nib[0:2 * len(ref):2] = ref >> 4
+    nib[1:2 * len(ref):2] = ref & 0xF
+    codes = np.lib.stride_tricks.sliding_window_view(nib, W)[gstart]
     del nib
     lo = np.searchsorted(gsnp, gstart)
-    hi = np.searchsorted(gsnp, gstart + L)
+    hi = np.searchsorted(gsnp, gstart + W)
     cnt = hi - lo
     rid = np.repeat(np.arange(n), cnt)
     k = np.arange(int(cnt.sum())) - np.repeat(np.cumsum(cnt) - cnt, cnt)
     sidx = lo[rid] + k
     carry = hap[rid]
     codes[rid[carry], (gsnp[sidx] - gstart[rid])[carry]] = galt[sidx][carry]
+    span = np.full(n, L, np.int64)
+    if with_id:
+        # the indel reads' rows: a deletion skips d reference columns at a, an insertion puts d
+        # random bases there (column index -1) and shifts the rest
+        sel = np.nonzero(ikind > 0)[0]
+        j = np.arange(L)[None, :]
+        aa, dd, kk = ia[sel][:, None], idd[sel][:, None], ikind[sel][:, None]
+        col = np.where(kk == 1, j + dd * (j >= aa), np.where(j < aa, j, np.where(j < aa + dd, -1, j - dd)))
+        rows = np.take_along_axis(codes[sel], np.maximum(col, 0), axis=1)
+        rows = np.where(col < 0, ACGT[rng.integers(0, 4, rows.shape)], rows).astype(np.uint8)
+        codes = codes[:, :L].copy()
+        codes[sel] = rows
+        span[sel] = np.where(ikind[sel] == 1, L + idd[sel], L - idd[sel])
     n_err = int(n * L * 0.001)
     er = rng.integers(0, n, n_err)
     eo = rng.integers(0, L, n_err)
@@ -695,7 +754,7 @@ def _config2_reads(rng, n_reads, L, n_contigs, clen, cstart, ref, gsnp, galt, wi
     seq = ((codes[:, 0::2] << 4) | codes[:, 1::2]).reshape(-1)
     del codes
     # scopes: windows first (in contig/position order), then gap union scopes
-    rend = rpos + L
+    rend = rpos + span
     key = rc * (1 << 40) + rpos
     span = L
     wkey_lo = win_contig * (1 << 40) + (win_pos - 1000 - span)
@@ -767,14 +826,31 @@ def _config2_reads(rng, n_reads, L, n_contigs, clen, cstart, ref, gsnp, galt, wi
     s_start, s_end, s_contig = s_start[order], s_end[order], s_contig[order]
     keep_pos, keep_code = keep_pos[order], keep_code[order]
     ws = np.where(ws >= 0, new_id[np.maximum(ws, 0)], -1).astype(np.int32)
+    if with_id:
+        # aM dD (L-a)M or aM dI (L-a-d)M; every other read L M
+        n_cig = np.where(ikind > 0, 3, 1).astype(np.int32)
+        cig_off = np.concatenate([[0], np.cumsum(n_cig)[:-1]]).astype(np.int64)
+        cigar = np.empty(int(n_cig.sum()), np.uint32)
+        plain = ikind == 0
+        cigar[cig_off[plain]] = (L << 4) | 0
+        s = np.nonzero(~plain)[0]
+        o = cig_off[s]
+        dl = ikind[s] == 1
+        cigar[o] = (ia[s] << 4).astype(np.uint32)
+        cigar[o + 1] = ((idd[s] << 4) | np.where(dl, 2, 1)).astype(np.uint32)
+        cigar[o + 2] = (np.where(dl, L - ia[s], L - ia[s] - idd[s]) << 4).astype(np.uint32)
+    else:
+        n_cig = np.ones(n, np.int32)
+        cig_off = np.arange(n, dtype=np.int64)
+        cigar = np.full(n, (L << 4) | 0, np.uint32)
     arr = {
         "ref_start": rpos.astype(np.int32),
         "read_len": np.full(n, L, np.int32),
         "seq_off": (np.arange(n, dtype=np.int64) * (L // 2)),
         "seq_nt16": seq,
-        "cig_off": np.arange(n, dtype=np.int64),
-        "n_cig": np.ones(n, np.int32),
-        "cigar": np.full(n, (L << 4) | 0, np.uint32),
+        "cig_off": cig_off,
+        "n_cig": n_cig,
+        "cigar": cigar,
         "dataset": rds.astype(np.uint8),
         "write_scope": ws,
         "scope_incid_off": incid_off,
@@ -790,6 +866,8 @@ def _config2_reads(rng, n_reads, L, n_contigs, clen, cstart, ref, gsnp, galt, wi
             "union_scopes": int(len(u_ids)), "incidences": int(len(inc_read)),
             "passthrough_reads": int((ws < 0).sum()), "genome": int(clen.sum()), "contigs": n_contigs,
             "germline_snps": int(len(gsnp))}
+    if with_id:
+        info["indel_reads"] = int((ikind > 0).sum())
     return arr, info
 
 

@@ -137,11 +137,17 @@ enum { GANON_PARAM_GROUP_UNROLL = 1, GANON_PARAM_GROUP_SKIP = 2, GANON_PARAM_GRO
        GANON_PARAM_NT_COPY = 4, GANON_PARAM_REF2 = 5, GANON_PARAM_FASTQ_SKIP = 6, GANON_PARAM_FASTQ_KD = 7,
        GANON_PARAM_INDEL_SORT = 8, GANON_PARAM_PREP_LONG = 9, GANON_PARAM_GROUP_OBS = 10,
        GANON_PARAM_PREP_UNROLL = 11, GANON_PARAM_FAR_INIT = 12, GANON_PARAM_SPEC_PLAN = 13,
-       GANON_PARAM_FUSED_FLAT = 14 };
-/* GANON_PARAM_FUSED_FLAT: 1 (default) a one-segment batch (no read of more than one aligned segment,
+       GANON_PARAM_FUSED_FLAT = 14, GANON_PARAM_XREC_INIT = 15 };
+/* GANON_PARAM_XREC_INIT: first capacity of a batch's extras list (the fused mode's records of reads
+ * with 2-8 aligned segments; 0 = auto, n_reads / 8 but at least 65536). A plan that needs more grows
+ * it to the count and scans again; a speculative run that needs more is gated (testing knob: 1
+ * forces both paths). */
+/* GANON_PARAM_FUSED_FLAT: 1 (default) a batch of short reads (no read of more than 8 aligned segments,
  * none of more than 48 CIGAR ops) builds no segment records in HBM — the plan's scan writes a 16-byte
- * descriptor per read and the partition candidates, and the group kernel makes each incidence's
- * record in LDS; 0 the record pass (the one-segment prep emit). Same results. */
+ * descriptor per read (and the segments of reads with several: short reads with I/D/N ops, round 5)
+ * and the partition candidates, and the group kernel makes each incidence's records in LDS; 0 the
+ * record pass (the one-segment prep emit; the two-pass emit for reads of several segments). Same
+ * results. */
 /* GANON_PARAM_SPEC_PLAN: 1 (default) speculative replans (ganon_batch_replan), 0 every plan
  * synchronizes for the scan's result, 2 (testing knob) reloads speculate too — their caller must
  * not read the shape before the download. Same results. */
@@ -184,7 +190,8 @@ GANON_API int ganon_ref_free(ganon_ctx *ctx, ganon_ref *ref);
  * of the same contents would (for arrays another stream or kernel wrote in place, and for timing
  * what a fresh batch costs: replan + run). Since ABI 4. A replan is speculative (no
  * synchronization: the scan and the run are enqueued back to back) when the batch's previous plan
- * found every read with at most one aligned segment and no scope wider than 2^20 positions, for
+ * found every read with at most one aligned segment (at most 8 short-read segments in the fused
+ * mode, GANON_PARAM_FUSED_FLAT: short reads with I/D/N ops) and no scope wider than 2^20 positions, for
  * the same read / scope / incidence counts, or — a batch of other counts — when the context's last
  * full plan found that shape (the new batch is assumed to have it: its buffers are sized on the host
  * from its counts, the overflow regions for reads no longer than that plan's) (GANON_PARAM_SPEC_PLAN
@@ -225,7 +232,9 @@ GANON_API int ganon_last_kernel_times(ganon_ctx *ctx, ganon_kernel_time *out, in
 GANON_API int ganon_batch_info(ganon_dbatch *db, int64_t *info8);
 /* Shape of the planned batch, from the device scan: [I/D CIGAR ops (0: the indel tally has nothing
  * to do), longest read, most aligned segments of one read, prep mode (0 two-pass, 1 long-read,
- * 2 one-segment, 3 one-segment fused: GANON_PARAM_FUSED_FLAT)]. Since ABI 4. */
+ * 2 one-segment, 3 one-segment fused: GANON_PARAM_FUSED_FLAT, 4 the same with reads of 2-8 aligned
+ * segments, the fused mode's multi-segment records (a full plan; a speculative one reports 3))].
+ * Since ABI 4. */
 GANON_API int ganon_batch_shape(ganon_dbatch *db, int64_t *shape4);
 /* How often the group kernel took its rarer paths since upload (synchronous): [lists of more than
  * 256 observations classified after an LDS sort, lists of more than 512 (overflowing into the

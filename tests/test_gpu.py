@@ -646,12 +646,17 @@ def _two_segment_copy(arr: dict, r: int) -> dict:
     return b
 
 
+# 9 aligned segments (query 150, 142 on the reference): one more than the fused mode takes
+NINE_SEG = [(16, 0), (1, 1)] * 8 + [(14, 0)]
+
+
 def test_speculative_plan_of_new_counts(hip_built):
     """Batches of other read / scope / incidence counts than the context's last plan speculate too
     (buffers sized from their counts, the context's last shape assumed, the scan gating the run):
-    two resident batches of one sample replanned in turn give exactly their full plans' results;
-    a batch that does not fit that shape (a read with two segments) runs nothing, counts one gated
-    run, and its download plans and runs it in full."""
+    two resident batches of one sample replanned in turn give exactly their full plans' results; a
+    batch with a two-segment read fits the fused shape (round 5: no gate); a batch that does not fit
+    (a read of nine aligned segments) runs nothing, counts one gated run, and its download plans and
+    runs it in full."""
     from genomeanonymizer_amd import native
     from genomeanonymizer_amd.synth.batch import config2_batch
     kw = dict(genome=30_000_000, n_windows=10_000, n_germline=25_000, seed=34)
@@ -659,12 +664,14 @@ def test_speculative_plan_of_new_counts(hip_built):
     b, _ = config2_batch(n_reads=124_000, read_seed=2, **kw)
     assert len(a["read_len"]) != len(b["read_len"]) and len(a["incid_read"]) != len(b["incid_read"])
     cand = np.nonzero((b["write_scope"] >= 0) & (b["n_cig"] == 1) & (b["read_len"] == 150))[0]
-    c = _two_segment_copy(b, int(cand[len(cand) // 2]))
+    c = _recigar(b, int(cand[len(cand) // 2]), NINE_SEG)
+    c2 = _two_segment_copy(b, int(cand[len(cand) // 3]))
     m = native.HipMasker(0)
     try:
-        want = [m.mask(x) for x in (a, b, c)]
+        want = [m.mask(x) for x in (a, b, c, c2)]
         ref = m.upload_reference(a["ref_nt16"])
-        dbs = [m.upload({k: v for k, v in x.items() if k != "ref_nt16"}, ref=ref) for x in (a, b, c)]
+        dbs = [m.upload({k: v for k, v in x.items() if k != "ref_nt16"}, ref=ref) for x in (a, b, c, c2)]
+        assert dbs[3].shape()["prep_mode"] == "multi_segment_fused"
         try:
             for _ in range(3):            # a, b, a, b, ...: every replan is of other counts
                 for k in (0, 1):
@@ -675,12 +682,17 @@ def test_speculative_plan_of_new_counts(hip_built):
             assert dbs[0].gated_runs() == 0 and dbs[1].gated_runs() == 0
             dbs[1].replan()               # (the context's last full shape: one-segment)
             dbs[1].run()
-            dbs[2].replan()               # speculative; its two-segment read stops the run
+            dbs[3].replan()               # speculative; a two-segment read fits the fused shape
+            dbs[3].run()
+            got = dbs[3].download()
+            assert dbs[3].gated_runs() == 0
+            assert all(np.array_equal(got[j], want[3][j]) for j in range(4))
+            dbs[2].replan()               # speculative; its nine-segment read stops the run
             dbs[2].run()
             assert dbs[2].gated_runs() == 1
             got = dbs[2].download()
             assert all(np.array_equal(got[j], want[2][j]) for j in range(4))
-            assert dbs[2].shape()["max_seg"] == 2
+            assert dbs[2].shape()["max_seg"] == 9 and dbs[2].shape()["prep_mode"] == "two_pass"
             got = dbs[1].download()
             assert all(np.array_equal(got[j], want[1][j]) for j in range(4))
         finally:
@@ -695,18 +707,20 @@ def test_speculative_replan_and_fallback(hip_built):
     """A replan after a one-segment plan of the same sizes is speculative (no synchronization); the
     scan's reduction gates the run. A batch that does not fit (a read with two segments) or fails
     validation runs nothing; ganon_batch_download plans it in full and runs it again, or returns the
-    validation error. GANON_PARAM_SPEC_PLAN 2 makes reloads speculate too (the testing knob)."""
+    validation error. A read with two segments fits the fused shape (round 5) and runs as speculated;
+    one with nine does not. GANON_PARAM_SPEC_PLAN 2 makes reloads speculate too (the testing knob)."""
     from genomeanonymizer_amd import native
     from genomeanonymizer_amd.synth.batch import config2_batch
     a, _ = config2_batch(n_reads=120_000, genome=30_000_000, n_windows=10_000, n_germline=25_000, seed=33)
     cand = np.nonzero((a["write_scope"] >= 0) & (a["n_cig"] == 1) & (a["read_len"] == 150))[0]
     r = int(cand[len(cand) // 3])
-    b = _two_segment_copy(a, r)
+    b = _recigar(a, r, NINE_SEG)
+    b2 = _two_segment_copy(a, r)
     bad = {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in a.items()}
     bad["seq_off"][r] = len(bad["seq_nt16"]) + 10
     m = native.HipMasker(0)
     try:
-        want_a, want_b = m.mask(a), m.mask(b)
+        want_a, want_b, want_b2 = m.mask(a), m.mask(b), m.mask(b2)
         m.set_param(native.PARAM_SPEC_PLAN, 2)
         db = m.upload(a)
         try:
@@ -714,11 +728,16 @@ def test_speculative_replan_and_fallback(hip_built):
             got = db.download()
             assert all(np.array_equal(got[k], want_a[k]) for k in range(4))
             assert db.shape()["prep_mode"].startswith("one_segment")   # (fused after a flat plan)
+            db.reload(b2)         # speculative, fits: two segments in the fused mode
+            db.run()
+            got = db.download()
+            assert all(np.array_equal(got[k], want_b2[k]) for k in range(4))
+            assert db.gated_runs() == 0
             db.reload(b)          # speculative: the gate stops the run, download plans b in full
             db.run()
             got = db.download()
             assert all(np.array_equal(got[k], want_b[k]) for k in range(4))
-            assert db.shape()["prep_mode"] == "two_pass" and db.shape()["max_seg"] == 2
+            assert db.shape()["prep_mode"] == "two_pass" and db.shape()["max_seg"] == 9
             db.reload(a)          # b's plan was not one-segment: a full plan
             db.run()
             got = db.download()
@@ -826,6 +845,95 @@ def test_fused_one_segment_matches_record_pass(hip_built, oracle):
     finally:
         fused.close()
         rec.close()
+
+
+def test_fused_multi_segment_matches_record_pass(hip_built, oracle):
+    """Short reads with I/D/N ops in the fused mode (round 5): the scan writes every segment of a read
+    of 2-8 aligned segments as an extras record, the group kernel lists each such incidence on its
+    first pass and streams the further segments after the group's incidences. Byte-equal to the
+    record pass (the two-pass emit) and to the oracle on: a c2id-shaped batch (germline het deletions
+    and sequencing indels, ~3 % of the reads aM dD/I bM); hand-made CIGARs of 2-8 segments (N skips,
+    =/X runs, several I/D ops, a leading soft clip) with N bases in the reference under some of them;
+    a shuffled buffer layout; a batch with a nine-segment read (the two-pass emit in both contexts);
+    and the extras list grown from a capacity of 1 (GANON_PARAM_XREC_INIT 1: the plan scans again)."""
+    from genomeanonymizer_amd import native
+    from genomeanonymizer_amd.synth.batch import config2_batch, relayout
+    a, info = config2_batch(n_reads=200_000, genome=60_000_000, n_windows=20_000, n_germline=60_000, seed=61,
+                            germline_del_per_kb=0.1, seq_indel_per_base=1.5e-4)
+    assert 0.02 < info["indel_reads"] / info["reads"] < 0.05
+    wr = np.nonzero((a["write_scope"] >= 0) & (a["n_cig"] == 1) & (a["read_len"] == 150))[0]
+    shapes = [[(30, 0), (2, 2), (30, 0), (2, 1), (30, 0), (2, 2), (30, 0), (2, 1), (26, 0)],   # 5 segments
+              [(50, 0), (20, 3), (80, 0), (20, 1)],                                         # N skip
+              [(70, 7), (80, 8)],                                                           # = then X
+              [(17, 0), (1, 1)] * 7 + [(24, 0)],                                            # 8 segments
+              [(5, 4), (60, 0), (3, 1), (40, 0), (2, 2), (42, 0)]]                          # soft clip first
+    b = a
+    hand = []
+    for k, r in enumerate(wr[37::211][:200]):
+        b = _recigar(b, int(r), shapes[k % len(shapes)])
+        hand.append(int(r))
+    c = {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in b.items()}
+    for r in hand[::7]:   # N bases in the reference under multi-segment written reads
+        s = int(c["write_scope"][r])
+        nib = int(c["scope_ref_off"][s]) + int(c["ref_start"][r]) - int(c["scope_span_start"][s]) + 90
+        c["ref_nt16"][nib // 2: nib // 2 + 3] = 0xFF
+    d = relayout(b, np.random.default_rng(7).permutation(len(b["read_len"])))
+    e = _recigar(b, int(wr[12345]), NINE_SEG)
+    fused, rec, tiny = native.HipMasker(0), native.HipMasker(0), native.HipMasker(0)
+    rec.set_param(native.PARAM_FUSED_FLAT, 0)
+    tiny.set_param(native.PARAM_XREC_INIT, 1)
+    try:
+        for name, x, mode in (("c2id", a, "multi_segment_fused"), ("hand", b, "multi_segment_fused"),
+                              ("nref", c, "multi_segment_fused"), ("layout", d, "multi_segment_fused"),
+                              ("nine", e, "two_pass")):
+            o = oracle.mask(x)
+            got_f, got_r = fused.mask(x), rec.mask(x)
+            for k in range(3):
+                assert np.array_equal(got_f[k], got_r[k]), (name, k)
+                assert np.array_equal(got_f[k], o[k]), (name, k)
+            assert np.array_equal(got_f[3], got_r[3]), name
+            db = fused.upload(x)
+            try:
+                assert db.shape()["prep_mode"] == mode, name
+            finally:
+                db.free()
+            if name in ("c2id", "nref"):
+                got_t = tiny.mask(x)
+                assert all(np.array_equal(got_t[k], got_f[k]) for k in range(4)), name
+        assert o[2].sum() > 0
+    finally:
+        fused.close()
+        rec.close()
+        tiny.close()
+
+
+def test_fused_multi_segment_speculative_batches(hip_built):
+    """c2id-shaped batches of other counts replanned in turn on one context (the bench's step): every
+    plan speculates (no gated run) and every result equals the batch's full plan."""
+    from genomeanonymizer_amd import native
+    from genomeanonymizer_amd.synth.batch import config2_batch
+    kw = dict(genome=40_000_000, n_windows=12_000, n_germline=40_000, seed=62, germline_del_per_kb=0.1,
+              seq_indel_per_base=1.5e-4)
+    xs = [config2_batch(n_reads=n, read_seed=k, **kw)[0] for k, n in enumerate((150_000, 153_000, 147_000))]
+    m = native.HipMasker(0)
+    try:
+        want = [m.mask(x) for x in xs]
+        ref = m.upload_reference(xs[0]["ref_nt16"])
+        dbs = [m.upload({k: v for k, v in x.items() if k != "ref_nt16"}, ref=ref) for x in xs]
+        try:
+            for _ in range(3):
+                for k, db in enumerate(dbs):
+                    db.replan()
+                    db.run()
+                    got = db.download()
+                    assert all(np.array_equal(got[j], want[k][j]) for j in range(4)), k
+            assert all(db.gated_runs() == 0 for db in dbs)
+        finally:
+            for db in dbs:
+                db.free()
+            ref.free()
+    finally:
+        m.close()
 
 
 def test_incidence_errors_are_reported_by_download(masker):

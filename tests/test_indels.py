@@ -167,6 +167,33 @@ def test_hip_indel_known_answers_and_random_batches(hip_built):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("env", [{}, {"GANON_INDEL_WAVE_WALK": "1"}, {"GANON_INDEL_DENSE_MAP": "1"}],
+                         ids=["thread_walk_hashed", "wave_walk", "dense_map"])
+def test_hip_indel_short_read_paths_match_oracle(env, hip_built, monkeypatch):
+    """Short-read batches (round 5): the candidate walks and the incidence expansion take a thread per
+    read / incidence, and the candidate map is hashed (2 bits per cell, 64 cells per op: a collision
+    can only add a position). Equal to the oracle, and to the wave-per-block walks and the dense
+    genome map (the A/B switches, read at indel upload), on dense indel batches and on a c2id-shaped
+    batch (germline het deletions + sequencing indels, ~3 % of the reads)."""
+    import indel_oracle
+    from genomeanonymizer_amd import native
+    from genomeanonymizer_amd.synth.batch import config2_batch, indel_batch
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    c2id, _ = config2_batch(n_reads=60_000, genome=6_000_000, n_windows=1_800, n_germline=6_000, seed=71,
+                            germline_del_per_kb=0.3, seq_indel_per_base=3e-4)
+    m = native.HipMasker(0)
+    try:
+        for arr in (indel_batch(5), indel_batch(6, indel_per_kb=30.0), c2id):
+            want = native.indel_records_array(indel_oracle.indel_records(arr))
+            assert len(want) > 20
+            *_, got = m.mask(arr, indels=True)
+            assert np.array_equal(got, want)
+    finally:
+        m.close()
+
+
+@pytest.mark.gpu
 def test_hip_indel_long_reads_match_oracle(hip_built):
     """C5 shape: 10-100 kb reads with ~5 % indel errors — ~10^5 observations, chance TN calls."""
     import indel_oracle

@@ -307,11 +307,12 @@ def pcie_bench(masker, db, arr, args, torch) -> dict:
                     "validation/plan + run + D2H of the masked bases, per batch"}
 
 
-def _child_json(cmd, env_extra: dict, timeout: int) -> dict:
+def _child_json(cmd, env_extra: dict, timeout: int, drop=()) -> dict:
     """Run a measurement in a child process (its own peak RSS and device context) and parse the
-    last JSON line it prints."""
+    last JSON line it prints (``drop``: variables of this environment the child must not see)."""
     import subprocess
-    env = dict(os.environ, **env_extra)
+    env = {k: v for k, v in os.environ.items() if k not in drop}
+    env.update(env_extra)
     t = time.perf_counter()
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
     if r.returncode != 0:
@@ -372,29 +373,51 @@ def e2e_lines(args) -> dict:
                         f"the GPU (contigs sharded as over ranks, 16 / {args.e2e_workers} decode threads each), "
                         f"files written to local disk",
             "generate_s": round(gen_s, 1), "error": hip.get("error") or one.get("error")}
-        # chromosome-scale contigs: 2 x 40 Mb, ~10 M reads (configs[1]'s read count), the contigs cut
-        # into runs of sections (job mode) over the same processes
+        # chromosome-scale contigs at configs[2] density (verdict r04 items 2-3): 2 x 20 Mb at 30x per
+        # sample (2 M pairs per contig and sample: 16 M reads, scopes ~860 reads deep), the contigs cut
+        # into runs of sections (job mode) over the same processes; then the same input in ONE process
+        # in contig mode (GANON_JOB_BP=0: one job per contig, an independent plan) — its files must
+        # equal the sharded run's
         if args.e2e_chrom_pairs > 0:
             t = time.perf_counter()
             cin = os.path.join(d, "chrom_in")
-            make_pair(cin, n_contigs=2, contig_len=40_000_000, pairs_per_contig=args.e2e_chrom_pairs,
+            make_pair(cin, n_contigs=2, contig_len=args.e2e_chrom_len, pairs_per_contig=args.e2e_chrom_pairs,
                       window_every=20_000, seed=9)
             cgen = time.perf_counter() - t
+            cov = 2 * args.e2e_chrom_pairs * 150 / args.e2e_chrom_len
             ch = _child_json([sys.executable, tool, cin, os.path.join(d, "chrom_out"), "stream"],
-                             {"E2E_RUNS": "1", "E2E_WORKERS": str(args.e2e_workers)}, 900)
+                             {"E2E_RUNS": "1", "E2E_WORKERS": str(args.e2e_workers), "E2E_DISK_PROBE": "1"}, 900)
             cs = ch.get("stream", {})
+            env1 = {"E2E_RUNS": "1", "GANON_JOB_BP": "0"}
+            one = _child_json([sys.executable, tool, cin, os.path.join(d, "chrom_one"), "stream"], env1, 900,
+                              drop=("E2E_WORKERS",))
+            same = None
+            if "error" not in ch and "error" not in one:
+                same = all(open(os.path.join(d, "chrom_out", f"{x}_stream{sfx}"), "rb").read() ==
+                           open(os.path.join(d, "chrom_one", f"{x}_stream{sfx}"), "rb").read()
+                           for x in ("tumor", "normal") for sfx in (".1.fastq", ".2.fastq", ".single_end.fastq"))
+            o1 = one.get("stream", {})
             res["e2e"]["chromosome_scale"] = {
                 "value": cs.get("reads_per_s"), "unit": "reads/s", "bases_per_sec": cs.get("bases_per_s"),
                 "reads": cs.get("reads"), "workers": args.e2e_workers, "wall_s": cs.get("stages_s", {}).get("wall_s"),
+                "critical_path_s_rank0": cs.get("critical_path_s_rank0"),
                 "stages_s_rank0": cs.get("stages_s"), "peak_rss_mb_rank0": cs.get("peak_rss_mb"),
                 "output_bytes": cs.get("output_bytes"), "jobs": cs.get("jobs"), "generate_s": round(cgen, 1),
-                "workload": f"synth/fastpair.py: 2 contigs x 40 Mb, {args.e2e_chrom_pairs} pairs per contig and sample "
-                            f"(150 bp, FR), germline SNPs/deletions as above, a window every 20 kb; contigs cut into "
-                            f"runs of sections of GANON_JOB_BP (default 4 Mb) read by BAI region queries, sharded over "
+                "disk": ch.get("disk"),
+                "files_equal": same,
+                "files_equal_against": {"what": "the same input in one process, contig mode (GANON_JOB_BP=0: one job "
+                                                "per contig), E2E_WORKERS unset", "reads_per_s": o1.get("reads_per_s"),
+                                        "wall_s": o1.get("stages_s", {}).get("wall_s"),
+                                        "peak_rss_mb": o1.get("peak_rss_mb"), "error": one.get("error")},
+                "workload": f"synth/fastpair.py: 2 contigs x {args.e2e_chrom_len // 1_000_000} Mb, {args.e2e_chrom_pairs} "
+                            f"pairs per contig and sample ({cov:.0f}x per sample, configs[2] density; 150 bp, FR), "
+                            f"germline SNPs/deletions as above, a window every 20 kb; contigs cut into runs of sections "
+                            f"of GANON_JOB_BP (default 4 Mb) read by BAI region queries, sharded over "
                             f"{args.e2e_workers} processes sharing the GPU",
                 "error": ch.get("error")}
             shutil.rmtree(cin, ignore_errors=True)
             shutil.rmtree(os.path.join(d, "chrom_out"), ignore_errors=True)
+            shutil.rmtree(os.path.join(d, "chrom_one"), ignore_errors=True)
         # the CPU path on a bounded sample (the first contigs)
         cpu_in = os.path.join(d, "cpu_in")
         make_pair(cpu_in, n_contigs=args.e2e_cpu_contigs, pairs_per_contig=args.e2e_pairs, seed=8)
@@ -481,8 +504,10 @@ def main() -> None:
     ap.add_argument("--e2e-pairs", type=int, default=23_000, help="pairs per contig and sample")
     ap.add_argument("--e2e-cpu-contigs", type=int, default=4)
     ap.add_argument("--e2e-runs", type=int, default=2, help="timed end-to-end runs after a warm run")
-    ap.add_argument("--e2e-chrom-pairs", type=int, default=1_250_000,
-                    help="pairs per contig and sample of the chromosome-scale end-to-end line (2 x 40 Mb; 0: skip)")
+    ap.add_argument("--e2e-chrom-pairs", type=int, default=2_000_000,
+                    help="pairs per contig and sample of the chromosome-scale end-to-end line (2 contigs of "
+                         "--e2e-chrom-len; default 30x per sample, configs[2] density; 0: skip)")
+    ap.add_argument("--e2e-chrom-len", type=int, default=20_000_000)
     ap.add_argument("--e2e-workers", type=int, default=8,
                     help="processes sharing the GPU in the end-to-end line (the multi-rank path over gloo)")
     ap.add_argument("--resident", action="store_true",

@@ -115,8 +115,8 @@ class AnonymizedRead:
 
     def update_from_primary_mapping(self, aln) -> None:
         if aln.is_supplementary:
-            raise ValueError("Trying to update AnonymizedRead using a supplementary alignment: "
-                             "The update should always be called only if the primary mapping appears")
+            raise ValueError("update_from_primary_mapping got a supplementary alignment (only the primary "
+                             "record may supply the sequence and qualities)")
         self._set_from(aln)
         self.is_supplementary = False
 
@@ -141,20 +141,19 @@ class AnonymizedRead:
             seq = np.concatenate((seq[:irp], ref, seq[irp:]))
             qual = qual[:irp] + array.array("B", [int(np.mean(qual))] * v.length) + qual[irp:]
         if len(seq) != len(qual):
-            raise ValueError("Length of the modified qualities does not match the length of the modified sequence")
+            raise ValueError(f"left-over edits left {len(seq)} bases but {len(qual)} qualities")
         self.anonymized_sequence_array, self.anonymized_qualities_array = seq, qual
 
     def add_left_over_variant(self, irp: int, v) -> None:
         if not self.is_supplementary and v.variant_type == self._vt.SNV:
-            raise ValueError(f"Trying to add left over SNV variant to AnonymizedRead {self.query_name} containing "
-                             f"a primary mapping\n all SNVs can be masked already")
+            raise ValueError(f"{self.query_name}: an SNV left-over on a read that holds its primary record "
+                             f"(its SNVs are masked directly)")
         self.left_over_variants_to_mask.append((irp, v))
         self.has_left_overs_to_mask = True
 
     def mask_or_anonymize_left_over_variants(self) -> None:
         if self.is_supplementary:
-            raise ValueError(f"Trying to mask left over variants in AnonymizedRead {self.query_name} "
-                             f"without a primary mapping")
+            raise ValueError(f"{self.query_name}: left-over edits applied before the primary record was met")
         self.left_over_variants_to_mask.sort(key=lambda x: x[1].variant_type.value)
         for irp, v in self.left_over_variants_to_mask:
             if v.variant_type == self._vt.SNV:

@@ -66,6 +66,7 @@ def anonymize_genome(windows_in_sample: List[Window], tumor_bam_file: str, norma
     normal = ReadTable(normal_bam_file, threads=available_threads)
     if has_split_alignments(tumor) or has_split_alignments(normal):
         log.info("secondary / supplementary alignments or SA tags: the sample streams contig by contig")
+        del tumor, normal   # (the streamed path decodes job by job: do not hold the whole sample too)
         from .stream import anonymize_genome_streaming
         return anonymize_genome_streaming(windows_in_sample, tumor_bam_file, normal_bam_file, fasta, anonymizer,
                                           tumor_output_fastq, normal_output_fastq, record_statistics,
@@ -76,6 +77,7 @@ def anonymize_genome(windows_in_sample: List[Window], tumor_bam_file: str, norma
         plan = planner.run()
     except UnsupportedInput as e:   # e.g. a duplicated record: the streamed path's object model has it
         log.info("%s: the sample streams contig by contig", e)
+        del tumor, normal, planner   # (the whole-sample tables would double the RSS)
         from .stream import anonymize_genome_streaming
         return anonymize_genome_streaming(windows_in_sample, tumor_bam_file, normal_bam_file, fasta, anonymizer,
                                           tumor_output_fastq, normal_output_fastq, record_statistics,

@@ -217,8 +217,10 @@ class SecondaryIndex:
         n_c = max(contigs.values()) + 1 if contigs else 0
         self.starts: List[np.ndarray] = [np.zeros(0, np.int64)] * n_c   # per contig: its jobs' region starts
         self.ids: List[np.ndarray] = [np.zeros(0, np.int64)] * n_c
-        for c in range(n_c):
-            js = [j for j in jobs if j.cidx == c]
+        by_c: Dict[int, list] = {}   # one pass over the jobs (a scaffold-level FASTA has ~1e5 contigs)
+        for j in jobs:
+            by_c.setdefault(j.cidx, []).append(j)
+        for c, js in by_c.items():
             self.starts[c] = np.array([j.region[0] if j.region else 0 for j in js], np.int64)
             self.ids[c] = np.array([j.index for j in js], np.int64)
         self.lock = threading.Lock()
@@ -609,10 +611,15 @@ class Job(JobPrep):
                 carry[(self.job, inst[0], inst[2], inst[1], 1)] = self.fmt.edited_bytes(inst, 1)
                 carry[(self.job, inst[0], inst[2], inst[1], 2)] = b
                 info[(self.job, inst[0], inst[2], inst[1])] = list(self.res.leftovers[inst])
+        op_names = _names_ds(self.tables, op_ds, op_name_rows)
+        left_names = _names_ds(self.tables, left_ds, left_row)
+        # (redo_needed) names planned as cross names here: those of plain placeholder events (kinds
+        # 3-5; the object events 6/7 and the unwritten pairs can be local names)
+        self.cross_names = {nm for nm, pl in zip(op_names, plain.tolist()) if pl}
         return {
             "job": self.job, "ops": ops, "op_rows": op_rows,
-            "op_names": _names_ds(self.tables, op_ds, op_name_rows),
-            "left": L, "left_names": _names_ds(self.tables, left_ds, left_row),
+            "op_names": op_names,
+            "left": L, "left_names": left_names,
             "cand": cand, "cand_names": cand_names, "carry": carry, "carry_info": info,
             "objs": O, "obj_rows": self.obj_rows, "cx": self.cx,
             "obj_ids": self._obj_ids(), "forced": self.forced, "offsec": self.offsec, "own_sec": self.own_sec,
@@ -733,6 +740,25 @@ class Job(JobPrep):
         """The job's exports are out: nothing on the device is needed to write it any more."""
         self.batch = None
 
+    def redo_needed(self, force: Sequence[bytes]) -> List[bytes]:
+        """The names of ``force`` whose forcing changes this job's plan: not forced already, present in
+        its records (a name it never meets plans the same), and planned as a local name (a name already
+        cross here — a placeholder event or an unwritten pair of its export — plans the same).
+        Call after exports()."""
+        new = sorted(set(force) - set(self.forced) - getattr(self, "cross_names", set()))
+        if not new:
+            return []
+        out = []
+        for t in self.tables:
+            if not len(new) or t.n == 0:
+                continue
+            blob = b"\0" + t.names_blob.tobytes()   # (BAM names: NUL-terminated, back to back)
+            keep = []
+            for nm in new:
+                (out if blob.find(b"\0" + nm + b"\0") >= 0 else keep).append(nm)
+            new = keep
+        return sorted(out)
+
 
 class _Comm:
     """Host-side gathers for the per-round exchange (gloo group over torch.distributed)."""
@@ -796,6 +822,7 @@ class _Coordinator:
         self.resolve_s = 0.0
         self.need_force: Dict[int, set] = {}   # job -> names its plan must treat as cross (SecondaryIndex)
         self.redos = 0
+        self.redos_unchanged = 0   # redo requests the owner answered without planning again
         self.marked = 0
 
     def missing_force(self, exp: dict, k: int) -> List[bytes]:
@@ -981,7 +1008,13 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
                     coord.redos += 1
                     link.send_resolution(o, {"job": k, "redo": sorted(set(miss) | set(exp.get("forced", ()))),
                                              "err": None})
-                    exp = recv_redo(o, k)
+                    re_exp = recv_redo(o, k)
+                    if re_exp.get("unchanged") and re_exp.get("err") is None:
+                        # the owner found nothing to plan again: the first export stands
+                        coord.redos_unchanged += 1
+                        exp["forced"] = re_exp["forced"]
+                    else:
+                        exp = re_exp
                 if exp.get("err") is not None:   # the owner failed: its error is its own to report
                     err = exp["err"]
                     failed_owner = o
@@ -1038,6 +1071,14 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
     def redo(job: "Job", force: List[bytes]) -> "Job":
         """Plan, mask and format ``job`` again with ``force`` planned as cross names (its own
         readers: the decode thread owns the others) and send its export in place of the first."""
+        if not job.redo_needed(force):
+            # every name it would force is absent from the job or already a cross name there: the
+            # plan would not change — tell the coordinator to keep the export it has (ADVICE r04)
+            timing["redos_skipped"] = timing.get("redos_skipped", 0) + 1
+            link.send_export({"redo_of": job.job, "unchanged": True, "forced": sorted(set(force) | set(job.forced)),
+                              "err": None})
+            job.forced = sorted(set(force) | set(job.forced))
+            return job
         if not redo_readers:
             redo_readers.extend(BamReader(p, threads, window_bytes) for p in (tumor_bam, normal_bam))
         prep = JobPrep(job.spec, redo_readers, fasta, windows, secondaries=secondaries, force=force)
@@ -1097,6 +1138,7 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
             p.result()
             timing["writer_wait_s"] += time.time() - t0
 
+    t_loop0 = time.time()
     try:
         try:
             for i, j in enumerate(mine):
@@ -1105,6 +1147,7 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
                     submit_upto(i + depth)
                     pre = ahead.pop(j)
                 job = Job(jobs[j], readers, fasta, windows, anonymizer, pre, secondaries)
+                t_exp0 = time.time()
                 exp = job.exports()
                 exp["local_sizes"] = job.local_sizes()
                 exp["err"] = None
@@ -1121,11 +1164,14 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
                     totals[:] += np.asarray(job.res.totals, np.int64)[:8]
                 link.send_export(exp)
                 job.release_device()
+                timing["export_s"] = timing.get("export_s", 0.0) + time.time() - t_exp0
                 pending.append(job if writer is None else writer.submit(finish, job))
                 while len(pending) >= pend_max:
                     finish_oldest()
+            t_drain0 = time.time()
             while pending:
                 finish_oldest()
+            timing["drain_s"] = time.time() - t_drain0
         except BaseException as e:   # every rank reaches the exchange below with its error
             failure = e
             # the coordinator may be waiting for this rank's next export: tell it
@@ -1141,6 +1187,7 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
             timing["resolve_s"] = coord.resolve_s
             timing["prunes"] = coord.prunes
             timing["redos"] = coord.redos
+            timing["redos_unchanged"] = coord.redos_unchanged
             timing["marked_written"] = coord.marked
             if coord_exc[0] is not None:   # rank 0 reports the coordinator's own error
                 failure = coord_exc[0]
@@ -1186,4 +1233,14 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
     timing["totals"] = {k: int(v) for k, v in zip(("masked_snv_calls", "masked_bases", "reads_in", "reads_written",
                                                    "scopes", "rare_scopes", "large_tiles", "reserved"), totals)}
     comm.barrier()
+    # this rank's main thread, stage by stage: what its wall is made of (the thread-time sums above
+    # overlap; these do not): waiting for the job's prefetched decode + plan, its mask (batch build
+    # included) and format on the device, the export, waiting for a writer slot, the last jobs'
+    # writes, then the coordinator, the statistics and the final exchanges
+    loop = time.time() - t_loop0
+    cp = {"wait_decode_plan": timing["decode_s"] + timing["plan_s"], "mask": timing["mask_s"],
+          "format": timing["format_s"], "export": timing.get("export_s", 0.0),
+          "wait_writer": timing["writer_wait_s"] - timing.get("drain_s", 0.0), "drain_writes": timing.get("drain_s", 0.0)}
+    cp["tail"] = max(0.0, loop - sum(cp.values()))
+    timing["critical_path"] = {k: round(v, 3) for k, v in cp.items()}
     return timing

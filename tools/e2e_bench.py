@@ -15,6 +15,8 @@ Prints one JSON line with per-stage seconds, reads/s, bases/s and the process's 
     E2E_WORKERS=P ...        # the streamed path in P processes sharing the GPU (torch.distributed.run,
                              # gloo; the contigs sharded over them as over the ranks of a multi-GPU run,
                              # host decode threads 16 / P each); wall = the slowest rank's
+    E2E_DISK_PROBE=1 ...     # also time 2 GiB of pwrite into OUTDIR (4 files at once, as the product
+                             # writes; page cache, then with fsync): the box's write bandwidth
 """
 import json
 import os
@@ -44,6 +46,35 @@ def _engine():
     anon = CompleteGermlineAnonymizer(device=int(os.environ.get("GANON_DEVICE", "0")))
     anon.engine   # context creation outside the timed stages
     return anon
+
+
+def disk_probe(out: str, total: int = 2 << 30) -> dict:
+    """Write bandwidth of OUTDIR's file system as the product sees it: four files written at once in
+    16 MiB pwrites (the page cache: what an un-synced run's wall pays), then the same with an fsync
+    of each file (the device)."""
+    from concurrent.futures import ThreadPoolExecutor
+    buf = os.urandom(16 << 20)
+    res = {}
+    for sync in (False, True):
+        paths = [os.path.join(out, f"_probe{k}") for k in range(4)]
+        fds = [os.open(p, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644) for p in paths]
+
+        def one(fd):
+            for o in range(0, total // 4, len(buf)):
+                os.pwrite(fd, buf, o)
+            if sync:
+                os.fsync(fd)
+        t = time.time()
+        with ThreadPoolExecutor(4) as ex:
+            list(ex.map(one, fds))
+        dt = time.time() - t
+        for fd, p in zip(fds, paths):
+            os.close(fd)
+            os.unlink(p)
+        res["fsync_gb_per_s" if sync else "page_cache_gb_per_s"] = round(total / dt / 1e9, 2)
+    res["bytes"] = total
+    res["dir"] = out
+    return res
 
 
 def _relaunch(workers: int) -> None:
@@ -139,6 +170,8 @@ def main():
                      "wall_s_runs": [round(t["wall_s"], 3) for t in timed],
                      "peak_rss_mb": resource.getrusage(resource.RUSAGE_SELF).ru_maxrss // 1024,
                      "workers": workers,
+                     "critical_path_s_rank0": best.get("critical_path"),
+                     "redos": best.get("redos"), "redos_unchanged": best.get("redos_unchanged"),
                      "first_run_wall_s": round(runs[0]["wall_s"], 3),
                      "output_bytes": sum(os.path.getsize(os.path.join(out, f"{x}_{mode}{s}"))
                                          for x in ("tumor", "normal") for s in (".1.fastq", ".2.fastq"))}
@@ -149,6 +182,8 @@ def main():
                    open(os.path.join(out, f"{x}_whole{s}"), "rb").read()
                    for x in ("tumor", "normal") for s in (".1.fastq", ".2.fastq"))
         res["stream_equals_whole"] = same
+    if rank == 0 and os.environ.get("E2E_DISK_PROBE") == "1":
+        res["disk"] = disk_probe(out)
     if rank == 0:
         print(json.dumps(res))
     if dist is not None:

@@ -393,8 +393,10 @@ def e2e_lines(args) -> dict:
                               drop=("E2E_WORKERS",))
             same = None
             if "error" not in ch and "error" not in one:
-                same = all(open(os.path.join(d, "chrom_out", f"{x}_stream{sfx}"), "rb").read() ==
-                           open(os.path.join(d, "chrom_one", f"{x}_stream{sfx}"), "rb").read()
+                def rd(p):   # (a sample without single ends writes no single-end file)
+                    return open(p, "rb").read() if os.path.exists(p) else None
+                same = all(rd(os.path.join(d, "chrom_out", f"{x}_stream{sfx}")) ==
+                           rd(os.path.join(d, "chrom_one", f"{x}_stream{sfx}"))
                            for x in ("tumor", "normal") for sfx in (".1.fastq", ".2.fastq", ".single_end.fastq"))
             o1 = one.get("stream", {})
             res["e2e"]["chromosome_scale"] = {

@@ -351,7 +351,8 @@ struct GrpSharedT {
   int cnt_bases[kGrpMaxScopes];
   int wdirty[kGrpThreads / 64];     // fused one-segment mode: a wave's records need the nt16 reference
   unsigned long long hsum;          // ... and the write-scope hash sum of the group's mine incidences
-  int n_xent, n_xtile;              // ... and its incidences with further segments (entries), an extras tile's records
+  int n_xent, n_xrec, n_xtile;      // ... and its incidences with further segments (entries), their records, an
+                                    // extras tile's records
 };
 
 struct GrpRange {
@@ -587,11 +588,19 @@ __device__ __forceinline__ FlatScope flat_load(const GrpBatch &B, const GrpAux *
   return f;
 }
 
-// r: incidence c0 + tid's read (loaded a tile ahead by grp_scan_flat).
+template <class SH>
+__device__ __forceinline__ int blk_excl_sum(SH &sh, int v, int *total);
+template <class SH>
+__device__ __attribute__((noinline)) int grp_xexpand(SH &sh, const GrpAux *__restrict__ aux, int64_t i_begin, int e0, int n_e,
+                                           int base, int *n_rec);
+
+// r: incidence c0 + tid's read (loaded a tile ahead by grp_scan_flat). last: the group's last
+// incidence tile — when the further segments of the group's multi-segment reads fit in its free
+// slots, they join it (merged: no extras tile after it); nh grows by their records.
 template <class SH>
 __device__ __forceinline__ int grp_tile_flat(SH &sh, const GrpBatch &B, const GrpAux *__restrict__ aux, int64_t c0,
-                                             int nh, int chunk, int s_begin, int ns, int64_t i_begin, bool first,
-                                             int r, bool &clean) {
+                                             int &nh, int chunk, int s_begin, int ns, int64_t i_begin, bool first,
+                                             int r, bool &clean, bool last, bool &merged) {
   const int tid = threadIdx.x;
   const FlatScope *sc = flat_scopes(sh);
   int nck = 0;
@@ -642,6 +651,7 @@ __device__ __forceinline__ int grp_tile_flat(SH &sh, const GrpBatch &B, const Gr
           const uint64_t rf = (uint64_t)(r0 + p);
           if (first && nx) {   // its further segments: an entry in the group's list (streamed after the incidences)
             const int k = atomicAdd(&sh.n_xent, 1);
+            atomicAdd(&sh.n_xrec, nx);
             aux->xlist[i_begin + k] = make_int2(d.x, (int)((uint32_t)j | ((uint32_t)nx << 12) | (((z >> 22) & 1u) << 15) |
                                                            (mine ? 0x80000000u : 0u)));
           }
@@ -662,6 +672,22 @@ __device__ __forceinline__ int grp_tile_flat(SH &sh, const GrpBatch &B, const Gr
       hsum += ((unsigned long long)hi << 32) | lo;
     }
     if ((tid & 63) == 0 && hsum) atomicAdd(&sh.hsum, hsum);
+  }
+  if (last) {   // (uniform) the group's further segments into this tile's free slots when they fit
+    if (first) __builtin_amdgcn_s_waitcnt(0);   // (this tile's entries at L2 before the barrier)
+    __syncthreads();
+    const int ne = sh.n_xent, nr = sh.n_xrec;
+    if (ne && nh + nr <= kGrpTile) {
+      int got;
+      grp_xexpand(sh, aux, i_begin, 0, ne, nh, &got);   // (every entry fits: ends on a barrier)
+      if (tid >= nh && tid < nh + nr) {
+        const int4 x = sh.rec[tid];
+        nck = ((((uint32_t)x.z >> 16) & kSegMaxLen) + chunk - 1) / chunk;
+        dirty = (flat_scopes(sh)[x.w & 0xFFF].pk >> 63) != 0;
+      }
+      nh += nr;
+      merged = true;
+    }
   }
   const unsigned long long dm = __ballot(dirty);
   if ((tid & 63) == 0) sh.wdirty[tid >> 6] = dm != 0ull;
@@ -870,24 +896,28 @@ __device__ __forceinline__ void grp_scan_flat(const GrpBatch &B, SH &sh, const G
   // each tile's incidence reads are loaded while the previous tile streams (one dependent load,
   // the descriptor, left per tile); the first tile's by the caller (staged in sh.rec[tid].x)
   int r_next = sh.rec[tid].x;
+  bool merged = false;
   for (int64_t c0 = i_begin; c0 < i_end; c0 += kGrpTile) {
     const int nh = (int)((i_end - c0) < kGrpTile ? (i_end - c0) : kGrpTile);
     const int r = r_next;
     const int64_t in = c0 + kGrpTile + tid;
     r_next = in < i_end ? aux->incid_read[in] : -1;
     bool clean;
-    int total = grp_tile_flat(sh, B, aux, c0, nh, 16 * K, s_begin, ns, i_begin, first, r, clean);
+    int nt = nh;   // (the last tile may take the extras records too)
+    int total = grp_tile_flat(sh, B, aux, c0, nt, 16 * K, s_begin, ns, i_begin, first, r, clean, c0 + kGrpTile >= i_end,
+                              merged);
     if (skip & kSkipChunks) total = 0;
     if (clean && B.ref2) {
-      for (int t = tid; t < total; t += kGrpThreads) grp_chunk<K, true>(B, sh, R, gg, t, grp_find(sh, nh, total, t));
+      for (int t = tid; t < total; t += kGrpThreads) grp_chunk<K, true>(B, sh, R, gg, t, grp_find(sh, nt, total, t));
     } else {
-      for (int t = tid; t < total; t += kGrpThreads) grp_chunk<K, false>(B, sh, R, gg, t, grp_find(sh, nh, total, t));
+      for (int t = tid; t < total; t += kGrpThreads) grp_chunk<K, false>(B, sh, R, gg, t, grp_find(sh, nt, total, t));
     }
     __syncthreads();
   }
   // multi-segment reads (short reads with an I/D/N op): their further segments, from the entries the
   // first pass listed — a segment's observations are those of any other record of its scope, so they
-  // may come after the incidences
+  // may come after the incidences: in the last tile's free slots (merged), else in extras tiles
+  if (merged) return;
   if (first) {   // (the entries' stores at L2 before any thread reads them back)
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
@@ -919,41 +949,58 @@ __device__ __forceinline__ int blk_excl_sum(SH &sh, int v, int *total) {
 // its read's extras index, scope, further segments, dataset, write mark) expanded into the records
 // of their further segments, as many whole entries per tile as fit its kGrpTile records (an entry
 // has at most kFusedMaxSeg - 1), then streamed like any tile.
+// Entries [e0, e0 + min(n_e - e0, kGrpTile)) of the group's list expanded into the records of their
+// further segments at sh.rec[base + ...]: as many whole entries as fit the tile (every entry has 1 to
+// kFusedMaxSeg - 1 records, so the fitting ones are a prefix). Returns the entries taken; *n_rec = the
+// records written. Every thread calls; ends on a barrier.
+template <class SH>
+__device__ __attribute__((noinline)) int grp_xexpand(SH &sh, const GrpAux *__restrict__ aux, int64_t i_begin, int e0, int n_e,
+                                           int base, int *n_rec) {
+  const int tid = opaque_tid();
+  const FlatScope *sc = flat_scopes(sh);
+  const unsigned long long *xl = reinterpret_cast<const unsigned long long *>(aux->xlist) + i_begin;
+  const int m = min(n_e - e0, kGrpTile);
+  unsigned long long ent = 0;
+  if (tid < m) ent = ld_l2(xl + e0 + tid);   // (written by this workgroup's first pass: read past L1)
+  const uint32_t ey = (uint32_t)(ent >> 32);
+  const int nx = tid < m ? (int)((ey >> 12) & 7) : 0;
+  int total;
+  const int pre = base + blk_excl_sum(sh, nx, &total);
+  const bool fit = tid < m && pre + nx <= kGrpTile;
+  if (fit) {
+    const int j = (int)(ey & 0xFFF);
+    const FlatScope S = sc[j];
+    const int64_t r0 = (int64_t)(S.pk << 22) >> 22;
+    const uint32_t xi = (uint32_t)ent;
+    const uint32_t hi = (((ey >> 15) & 1u) << 30) | (ey & kSegMine);
+    for (int k = 0; k < nx; ++k) {
+      const int4 e = aux->xrec[xi + 1 + k];
+      const uint32_t z = (uint32_t)e.z;
+      const int n = (int)((z >> 8) & kSegMaxLen), p = e.y;
+      const uint64_t rf = (uint64_t)(r0 + p);
+      const uint32_t rz = (z & 0xFFu) | ((uint32_t)((rf >> 32) & 0xFF) << 8) | ((uint32_t)n << 16) | hi;
+      sh.rec[pre + k] = make_int4(e.x, (int)(uint32_t)rf, (int)rz, (int)((uint32_t)j | ((uint32_t)(p - S.sstart) << 12)));
+    }
+  }
+  const int used = __syncthreads_count(fit);
+  if (fit && tid == used - 1) sh.n_xtile = pre + nx - base;
+  __syncthreads();
+  *n_rec = sh.n_xtile;
+  return used;
+}
+
+// The fused mode's extras tiles (the further segments that did not fit the group's last tile): the
+// group's n_e entries (an incidence of a multi-segment read each: its read's extras index, scope,
+// further segments, dataset, write mark) expanded tile by tile, then streamed like any tile.
 template <int K, class SH>
 __device__ __forceinline__ void grp_scan_extra(const GrpBatch &B, SH &sh, const GrpRange &R,
                                                          const GrpGlobal &gg, const GrpAux *__restrict__ aux,
                                                          int64_t i_begin, int n_e, int skip) {
   const int tid = opaque_tid();
   const FlatScope *sc = flat_scopes(sh);
-  const unsigned long long *xl = reinterpret_cast<const unsigned long long *>(aux->xlist) + i_begin;
   for (int e0 = 0; e0 < n_e;) {
-    const int m = min(n_e - e0, kGrpTile);
-    unsigned long long ent = 0;
-    if (tid < m) ent = ld_l2(xl + e0 + tid);   // (written by this workgroup's first pass: read past L1)
-    const uint32_t ey = (uint32_t)(ent >> 32);
-    const int nx = tid < m ? (int)((ey >> 12) & 7) : 0;
-    int total;
-    const int pre = blk_excl_sum(sh, nx, &total);
-    const bool fit = tid < m && pre + nx <= kGrpTile;
-    if (fit) {
-      const int j = (int)(ey & 0xFFF);
-      const FlatScope S = sc[j];
-      const int64_t r0 = (int64_t)(S.pk << 22) >> 22;
-      const uint32_t xi = (uint32_t)ent;
-      const uint32_t hi = (((ey >> 15) & 1u) << 30) | (ey & kSegMine);
-      for (int k = 0; k < nx; ++k) {
-        const int4 e = aux->xrec[xi + 1 + k];
-        const uint32_t z = (uint32_t)e.z;
-        const int n = (int)((z >> 8) & kSegMaxLen), p = e.y;
-        const uint64_t rf = (uint64_t)(r0 + p);
-        const uint32_t rz = (z & 0xFFu) | ((uint32_t)((rf >> 32) & 0xFF) << 8) | ((uint32_t)n << 16) | hi;
-        sh.rec[pre + k] = make_int4(e.x, (int)(uint32_t)rf, (int)rz, (int)((uint32_t)j | ((uint32_t)(p - S.sstart) << 12)));
-      }
-    }
-    const int used = __syncthreads_count(fit);   // (the fitting entries are a prefix: every nx >= 1)
-    if (fit && tid == used - 1) sh.n_xtile = pre + nx;
-    __syncthreads();
-    const int nh = sh.n_xtile;
+    int nh;
+    const int used = grp_xexpand(sh, aux, i_begin, e0, n_e, 0, &nh);
     int nck = 0;
     bool dirty = false;
     if (tid < nh) {
@@ -1350,6 +1397,7 @@ __global__ void __launch_bounds__(kGrpThreads, (OBS > 512 ? 4 : U == 1 ? 6 : U =
     sh.blk_bases = 0;
     sh.hsum = 0;
     sh.n_xent = 0;
+    sh.n_xrec = 0;
   }
   for (int i = tid; i < kGrpMaxScopes; i += kGrpThreads) {
     sh.cnt_calls[i] = 0;

@@ -24,7 +24,8 @@ from __future__ import annotations
 import os
 import pickle
 import queue
-from typing import List, Sequence
+import threading
+from typing import Dict, List, Optional, Sequence
 
 import numpy as np
 
@@ -127,6 +128,169 @@ class Link:
             w1.wait()
             w2.wait()
         self._inflight = []
+
+
+class SecondaryExchange:
+    """Off-contig secondary alignments published across ranks before any job is planned (round 5;
+    ADVICE r04: without it, a job whose mate-side names another rank's later decode forced was planned,
+    masked and formatted again — serially, while the coordinator waited: on a 4-rank CPU probe with 1 %
+    of the pairs carrying such a secondary, 2 of 3 jobs were planned twice and the run took 4x the
+    one-process wall).
+
+    Every rank reports each of its jobs once its decode thread has read it (DECODED: the job's
+    (name, mate job) secondaries, or an error) to rank 0, whose registry keeps the decode frontier —
+    the first job not decoded yet — and the secondaries by mate job. Job j may be planned once every
+    job before it is decoded (only an earlier job's secondary can force a name on j: a later one's is
+    marked written by the coordinator instead): rank 0 then sends j's owner a PERMIT with the names to
+    plan as cross names. Each job is reported exactly once (a failing rank reports its remaining jobs
+    as errors) and permitted exactly once (after an error, every job not permitted yet gets the error),
+    so every receive has its send. Ranks couple only through their decode progress."""
+
+    DECODED, PERMIT = 13, 14
+
+    def __init__(self, dist, owner: Sequence[int]):
+        self.dist = dist
+        self.rank, self.world = dist.get_rank(), dist.get_world_size()
+        self.group = dist.new_group(backend="gloo")
+        self.owner = list(owner)
+        self.n = len(owner)
+        self.mine = [j for j in range(self.n) if owner[j] == self.rank]
+        # locks: report_lock (the reported set), reg_lock (rank 0's registry; taken before io_lock),
+        # io_lock (a leaf: isends and their in-flight list)
+        self.report_lock = threading.Lock()
+        self.io_lock = threading.Lock()
+        self.reported: set = set()
+        self._inflight: list = []
+        self.cv = threading.Condition()
+        self.permits: Dict[int, object] = {}
+        self.threads: List[threading.Thread] = []
+        self.wait_s = 0.0
+        if self.rank == 0:
+            self.reg_lock = threading.Lock()
+            self.decoded = [False] * self.n
+            self.frontier = 0
+            self.next_permit = 0
+            self.failed: Optional[str] = None
+            self.by_mate: Dict[int, Dict[bytes, int]] = {}
+            with self.reg_lock:
+                self._advance()
+            for r in range(1, self.world):
+                cnt = sum(1 for o in owner if o == r)
+                if cnt:
+                    self.threads.append(threading.Thread(target=self._receive_reports, args=(r, cnt), daemon=True,
+                                                         name=f"ganon-secx-{r}"))
+        elif self.mine:
+            self.threads.append(threading.Thread(target=self._receive_permits, daemon=True, name="ganon-secx-permits"))
+        for t in self.threads:
+            t.start()
+
+    # transport (pickled objects as uint8 tensors, a length message first; as Link)
+    def _send(self, obj, dst: int, tag: int) -> None:
+        import torch
+        payload = pickle.dumps(obj, protocol=pickle.HIGHEST_PROTOCOL)
+        n = torch.tensor([len(payload)], dtype=torch.int64)
+        t = torch.frombuffer(bytearray(payload), dtype=torch.uint8)
+        with self.io_lock:
+            w1 = self.dist.isend(n, dst, group=self.group, tag=tag)
+            w2 = self.dist.isend(t, dst, group=self.group, tag=tag)
+            self._inflight.append((w1, w2, n, t))
+            self._inflight = [x for x in self._inflight if not (x[0].is_completed() and x[1].is_completed())]
+
+    def _recv(self, src: int, tag: int):
+        import torch
+        n = torch.zeros(1, dtype=torch.int64)
+        self.dist.recv(n, src, group=self.group, tag=tag)
+        t = torch.empty(int(n.item()), dtype=torch.uint8)
+        self.dist.recv(t, src, group=self.group, tag=tag)
+        return pickle.loads(t.numpy().tobytes())
+
+    # worker side
+    def report(self, job: int, pairs) -> None:
+        """Job ``job`` decoded (its decode thread): its secondaries whose mate another job reads."""
+        self._report({"job": job, "pairs": list(pairs)})
+
+    def fail(self, err: str) -> None:
+        """This rank failed: every job of it not reported yet is reported as the error."""
+        for j in self.mine:
+            self._report({"job": j, "err": err})
+
+    def _report(self, msg: dict) -> None:
+        with self.report_lock:
+            if msg["job"] in self.reported:
+                return
+            self.reported.add(msg["job"])
+        if self.rank == 0:
+            with self.reg_lock:
+                self._on_report(msg)
+        else:
+            self._send(msg, 0, self.DECODED)
+
+    def permit(self, job: int) -> List[bytes]:
+        """Block until every job before ``job`` is decoded (on any rank); the names of the secondaries
+        of earlier jobs whose mate ``job`` reads. Raises when a rank failed first."""
+        import time
+        t0 = time.time()
+        with self.cv:
+            while job not in self.permits:
+                self.cv.wait()
+            v = self.permits.pop(job)
+        self.wait_s += time.time() - t0
+        if isinstance(v, str):
+            raise RuntimeError(f"another rank failed: {v}")
+        return v
+
+    def _deliver(self, msg: dict) -> None:
+        with self.cv:
+            self.permits[msg["job"]] = msg["err"] if msg.get("err") is not None else msg["names"]
+            self.cv.notify_all()
+
+    def _receive_permits(self) -> None:
+        for _ in self.mine:
+            self._deliver(self._recv(0, self.PERMIT))
+
+    # registry (rank 0)
+    def _receive_reports(self, r: int, cnt: int) -> None:
+        for _ in range(cnt):
+            msg = self._recv(r, self.DECODED)
+            with self.reg_lock:
+                self._on_report(msg)
+
+    def _on_report(self, msg: dict) -> None:   # (reg_lock held)
+        if msg.get("err") is not None:
+            self.failed = self.failed or msg["err"]
+        else:
+            self.decoded[msg["job"]] = True
+            for nm, mj in msg["pairs"]:
+                d = self.by_mate.setdefault(int(mj), {})
+                if d.get(nm, 1 << 62) > msg["job"]:
+                    d[nm] = msg["job"]
+        self._advance()
+
+    def _advance(self) -> None:
+        while self.frontier < self.n and self.decoded[self.frontier]:
+            self.frontier += 1
+        while self.next_permit < self.n and (self.failed is not None or self.next_permit <= self.frontier):
+            j = self.next_permit
+            self.next_permit += 1
+            if self.failed is not None:
+                msg = {"job": j, "err": self.failed}
+            else:
+                msg = {"job": j, "names": sorted(nm for nm, src in self.by_mate.get(j, {}).items() if src < j)}
+            if self.owner[j] == 0:
+                self._deliver(msg)
+            else:
+                self._send(msg, self.owner[j], self.PERMIT)
+
+    def close(self, timeout: Optional[float] = None) -> None:
+        """Join the receiving threads and wait for every send (a normal end: each has its receive)."""
+        for t in self.threads:
+            t.join(timeout)
+        if timeout is None:
+            with self.io_lock:
+                for w1, w2, _, _ in self._inflight:
+                    w1.wait()
+                    w2.wait()
+                self._inflight = []
 
 
 def anonymize_genome_sharded(windows: List[Window], tumor_bam: str, normal_bam: str, ref_file: str,

@@ -225,6 +225,9 @@ class SecondaryIndex:
             self.ids[c] = np.array([j.index for j in js], np.int64)
         self.lock = threading.Lock()
         self.by_mate: Dict[int, Dict[bytes, int]] = {}   # mate job -> name -> lowest source job
+        # several ranks: distributed.SecondaryExchange — every job's secondaries reach every later
+        # job's plan whichever rank decodes them (a plan waits until every earlier job is decoded)
+        self.remote = None
 
     def job_of(self, ds: int, tid: np.ndarray, pos: np.ndarray) -> np.ndarray:
         """The job reading position pos of BAM tid (-1: none)."""
@@ -264,11 +267,15 @@ class SecondaryIndex:
                 d = self.by_mate.setdefault(mj, {})
                 if d.get(nm, 1 << 62) > job:
                     d[nm] = job
+        if self.remote is not None:
+            self.remote.report(job, pairs)
 
     def forced_for(self, job: int) -> List[bytes]:
-        """Names of published secondaries of earlier jobs whose mate this job reads."""
+        """Names of published secondaries of earlier jobs whose mate this job reads (several ranks:
+        once every earlier job is decoded, on any rank)."""
+        remote = self.remote.permit(job) if self.remote is not None else []
         with self.lock:
-            return sorted(nm for nm, src in self.by_mate.get(job, {}).items() if src < job)
+            return sorted(set(remote) | {nm for nm, src in self.by_mate.get(job, {}).items() if src < job})
 
 
 class JobPrep:
@@ -975,6 +982,11 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
     totals = np.zeros(8, np.int64)
     totals_lock = threading.Lock()
     secondaries = SecondaryIndex(readers, jobs)
+    xchg = None
+    if world > 1 and os.environ.get("GANON_SEC_EXCHANGE", "1") != "0":
+        from .distributed import SecondaryExchange
+        xchg = SecondaryExchange(dist, owner)
+        secondaries.remote = xchg
 
     stash: Dict[int, list] = {}      # exports an owner sent after the job it is planning again
 
@@ -1174,6 +1186,8 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
             timing["drain_s"] = time.time() - t_drain0
         except BaseException as e:   # every rank reaches the exchange below with its error
             failure = e
+            if xchg is not None:     # plans waiting for this rank's decodes get the error
+                xchg.fail(repr(e))
             # the coordinator may be waiting for this rank's next export: tell it
             link.send_export({"err": repr(e)})
             if writer is not None:   # jobs not started yet are dropped; the running one gets the error
@@ -1192,6 +1206,11 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
             if coord_exc[0] is not None:   # rank 0 reports the coordinator's own error
                 failure = coord_exc[0]
         err = repr(failure) if failure is not None else None
+        if xchg is not None:
+            if failure is not None:
+                xchg.fail(err)
+            xchg.close(None if failure is None else 60.0)
+            timing["permit_wait_s"] = round(xchg.wait_s, 3)
         gathered = comm.allgather({"stats": stats_rows, "err": err})
         errs = [g["err"] for g in gathered if g["err"] is not None]
         if errs:

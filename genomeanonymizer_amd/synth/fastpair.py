@@ -11,7 +11,10 @@ a het germline SNP per ``1000 / snp_per_kb`` bases and a 1-3 bp het germline del
 germline variants the path masks); a somatic SNV window variant every ``window_every`` bases from
 5,000 (the VCF; tumor reads carry it at AF 0.4); FR pairs with insert N(300, 30), flags 99/147 or
 83/163, 0.1 % substitution errors, phred uniform in [2, 40], a 5-20 base soft clip on 2 % of the
-reads; tumor and normal read names disjoint.
+reads; tumor and normal read names disjoint. ``sec_frac``: that fraction of the pairs of
+every contig also has a secondary alignment of its read 1 (flag 0x100, 150M, the read's bases) at a
+random position of another contig, its mate fields naming the primary mate — the aligner output
+that makes the streamed path plan a job again when another rank decodes the secondary.
 """
 from __future__ import annotations
 
@@ -155,8 +158,9 @@ def _reads(rng, c: _Contig, n_pairs: int, read_len: int, tumor: bool, err: float
     return pos, end, cig, ncig, base, flag, mate, tlen
 
 
-def _encode(tid: int, pos, end, cig, ncig, base, flag, mpos, tlen, names: np.ndarray, qual) -> bytes:
-    """BAM records (fixed read and name length) back to back."""
+def _encode(tid: int, pos, end, cig, ncig, base, flag, mpos, tlen, names: np.ndarray, qual, mtid=None) -> bytes:
+    """BAM records (fixed read and name length) back to back (``mtid``: per-record mate
+    reference, default the record's own)."""
     n, read_len = base.shape
     nl = names.shape[1] + 1
     size = 36 + nl + 4 * ncig + (read_len + 1) // 2 + read_len
@@ -170,7 +174,7 @@ def _encode(tid: int, pos, end, cig, ncig, base, flag, mpos, tlen, names: np.nda
     hdr["ncig"] = ncig
     hdr["flag"] = flag
     hdr["lseq"] = read_len
-    hdr["nref"] = tid
+    hdr["nref"] = tid if mtid is None else mtid
     hdr["npos"] = mpos
     hdr["tlen"] = tlen
     codes = _CODE[base]
@@ -281,7 +285,7 @@ def _write_bam(path: str, contigs: List[Tuple[str, int]], per_contig, level: int
 def make_pair(outdir: str, n_contigs: int = 24, contig_len: int = 2_000_000, pairs_per_contig: int = 23_000,
               read_len: int = 150, seed: int = 7, snp_per_kb: float = 1.0, del_per_kb: float = 0.1,
               window_every: int = 20_000, err: float = 0.001, clip_frac: float = 0.02, level: int = 1,
-              threads: int = 16) -> Dict[str, str]:
+              threads: int = 16, sec_frac: float = 0.0) -> Dict[str, str]:
     os.makedirs(outdir, exist_ok=True)
     rng = np.random.default_rng(seed)
     names = [f"chr{i + 1}" for i in range(n_contigs)]
@@ -319,22 +323,45 @@ def make_pair(outdir: str, n_contigs: int = 24, contig_len: int = 2_000_000, pai
         fh.write("#tumor\tnormal\tvcf\ntumor.bam\tnormal.bam\tvariants.vcf\n")
     with ThreadPoolExecutor(threads) as pool:
         for tag, tumor in (("T", True), ("N", False)):
-            per = []
+            recs = []   # per contig: the record columns, secondaries from other contigs appended below
             for tid, c in enumerate(contigs):
                 pos, end, cig, ncig, base, flag, mate, tlen = _reads(rng, c, pairs_per_contig, read_len, tumor, err,
                                                                      clip_frac)
-                order = np.argsort(pos, kind="stable")
-                inv = np.empty_like(order)
-                inv[order] = np.arange(len(order))
                 pair_id = np.arange(len(pos)) // 2
                 nm = np.frombuffer(b"".join(f"{tag}{tid:03d}:{p:08d}".encode() for p in range(pairs_per_contig)),
                                    np.uint8).reshape(pairs_per_contig, -1)[pair_id]
                 qual = rng.integers(2, 41, base.shape, dtype=np.uint8)
-                o = order
-                blob = _encode(tid, pos[o], end[o], cig[o], ncig[o], base[o], flag[o], pos[mate][o], tlen[o], nm[o],
-                               qual[o])
-                nl = nm.shape[1] + 1
-                sz = 36 + nl + 4 * ncig[o] + (read_len + 1) // 2 + read_len
-                per.append((blob, sz, pos[o], end[o]))
+                recs.append({"pos": pos, "end": end, "cig": cig, "ncig": ncig, "base": base, "flag": flag,
+                             "mpos": pos[mate], "tlen": tlen, "nm": nm, "qual": qual,
+                             "mtid": np.full(len(pos), tid, np.int64)})
+            if sec_frac > 0 and len(contigs) > 1:
+                add = [[] for _ in contigs]
+                for tid, r in enumerate(recs):
+                    k = int(pairs_per_contig * sec_frac)
+                    i = 2 * rng.choice(pairs_per_contig, k, replace=False)
+                    i = np.where(r["flag"][i] & 0x40, i, i + 1)          # the pair's read 1
+                    dst = (tid + 1 + rng.integers(0, len(contigs) - 1, k)) % len(contigs)
+                    for t in np.unique(dst).tolist():
+                        sel = i[dst == t]
+                        L = contigs[t].length
+                        sp = rng.integers(0, L - read_len - 1, len(sel))
+                        cg = np.zeros((len(sel), 3), np.uint32)
+                        cg[:, 0] = read_len << 4
+                        add[t].append({"pos": sp, "end": sp + read_len, "cig": cg, "ncig": np.ones(len(sel), np.int64),
+                                       "base": r["base"][sel], "flag": r["flag"][sel] | 0x100,
+                                       "mpos": r["mpos"][sel], "tlen": np.zeros(len(sel), np.int64),
+                                       "nm": r["nm"][sel], "qual": r["qual"][sel],
+                                       "mtid": np.full(len(sel), tid, np.int64)})
+                for t, extra in enumerate(add):
+                    if extra:
+                        recs[t] = {k: np.concatenate([recs[t][k]] + [e[k] for e in extra]) for k in recs[t]}
+            per = []
+            for tid, r in enumerate(recs):
+                o = np.argsort(r["pos"], kind="stable")
+                blob = _encode(tid, r["pos"][o], r["end"][o], r["cig"][o], r["ncig"][o], r["base"][o], r["flag"][o],
+                               r["mpos"][o], r["tlen"][o], r["nm"][o], r["qual"][o], r["mtid"][o])
+                nl = r["nm"].shape[1] + 1
+                sz = 36 + nl + 4 * r["ncig"][o] + (read_len + 1) // 2 + read_len
+                per.append((blob, sz, r["pos"][o], r["end"][o]))
             _write_bam(paths[tag], [(n, c.length) for n, c in zip(names, contigs)], per, level, pool)
     return paths

@@ -10,6 +10,9 @@ run_short_read_tumor_normal_anonymizer of the reference and through this build's
 oracle standing in for the device, streamed and whole-sample), every output file compared.
 
 usage: python oracle/fuzz_reference.py SEED [SEED ...]
+       FUZZ_FASTPAIR=N_CONTIGS,CONTIG_LEN,PAIRS,SEC_FRAC python oracle/fuzz_reference.py SEED ...
+       (the sample from synth/fastpair.py instead: the end-to-end bench's input shape, with SEC_FRAC
+       of the pairs given an off-contig secondary alignment of read 1; BAMs indexed)
 """
 from __future__ import annotations
 
@@ -76,7 +79,14 @@ def main():
     bad = 0
     for seed in [int(x) for x in sys.argv[1:]]:
         work = tempfile.mkdtemp(prefix=f"ganon_fuzz_{seed}_")
-        paths = generate(scenario(seed), os.path.join(work, "in"))
+        fp = os.environ.get("FUZZ_FASTPAIR")
+        if fp:
+            from genomeanonymizer_amd.synth.fastpair import make_pair
+            nc, cl, pp, sf = fp.split(",")
+            paths = make_pair(os.path.join(work, "in"), n_contigs=int(nc), contig_len=int(cl), pairs_per_contig=int(pp),
+                              seed=seed, sec_frac=float(sf), window_every=max(5000, int(cl) // 20))
+        else:
+            paths = generate(scenario(seed), os.path.join(work, "in"))
         try:
             ref = files(*run_ref(paths, work), os.path.join(work, "ref_stats.txt"))
         except Exception as e:   # the reference raising is an outcome the product must match too

@@ -57,11 +57,16 @@ def _worker(rank, world, port, name, workdir, q, engine="oracle", fail_rank=-1, 
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name,index,world", [("edge", True, 2), ("tiny", False, 2), ("fuzz2003", False, 2),
-                                              ("fuzz3000", False, 2), ("fuzz3008", True, 3)])
-def test_two_rank_contig_shards_match_reference(name, index, world, tmp_path):
-    """fuzz3000 / fuzz3008 put secondaries off their mate's contig on another rank than the mate:
-    the coordinator has the owner plan such a contig again (SecondaryIndex, stream.py)."""
+@pytest.mark.parametrize("name,index,world,xchg", [("edge", True, 2, "1"), ("tiny", False, 2, "1"),
+                                                   ("fuzz2003", False, 2, "1"), ("fuzz3000", False, 2, "1"),
+                                                   ("fuzz3008", True, 3, "1"), ("fuzz3000", False, 2, "0"),
+                                                   ("fuzz3008", True, 3, "0")])
+def test_two_rank_contig_shards_match_reference(name, index, world, xchg, tmp_path, monkeypatch):
+    """fuzz3000 / fuzz3008 put secondaries off their mate's contig on another rank than the mate.
+    With the secondary exchange (distributed.SecondaryExchange, default) every plan knows the earlier
+    jobs' secondaries from every rank: no job is planned twice. Without it (GANON_SEC_EXCHANGE=0) the
+    coordinator has the owner plan such a job again (the redo protocol, stream.py)."""
+    monkeypatch.setenv("GANON_SEC_EXCHANGE", xchg)
     from helpers import GOLDEN, run_pipeline_vs_golden
     from genomeanonymizer_amd.synth.generate import generate, scenario
     import gzip
@@ -79,8 +84,8 @@ def test_two_rank_contig_shards_match_reference(name, index, world, tmp_path):
     assert all(p.exitcode == 0 for p in procs)
     results = dict(q.get() for _ in range(world))
     assert all(results[r][0] == results[0][0] for r in range(world))   # totals are all-reduced
-    if name.startswith("fuzz3"):      # a contig planned again (rank 0's coordinator counts them)
-        assert results[0][1] > 0
+    if name.startswith("fuzz3"):      # jobs planned again (rank 0's coordinator counts them)
+        assert (results[0][1] > 0) == (xchg == "0")
     from genomeanonymizer_amd.short_read_tumor_normal_anonymizer import name_output
     for tag, pre in (("tumor", name_output(paths["T"])), ("normal", name_output(paths["N"]))):
         for suf in (".1.fastq", ".2.fastq", ".single_end.fastq"):

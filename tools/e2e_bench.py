@@ -145,7 +145,12 @@ def main():
                                       os.path.join(out, f"normal_{mode}"), True, threads, fasta=fasta,
                                       streaming=(mode == "stream"), dist=dist)
             tim["wall_s"] = time.time() - t1
-            if dist is not None:   # the slowest rank's wall; reads and bases of all ranks
+            if dist is not None:   # every rank's exchange and waits, then the slowest rank's wall
+                per_rank = [None] * dist.get_world_size()
+                dist.all_gather_object(per_rank, {k: tim.get(k) for k in (
+                    "wall_s", "exchange_sent_bytes", "exchange_recv_bytes", "wait_s", "writer_wait_s", "jobs",
+                    "decode_s", "mask_s", "format_s", "write_s", "redos_skipped", "critical_path")})
+                tim["per_rank"] = per_rank
                 import torch
                 w = torch.tensor([tim["wall_s"]], dtype=torch.float64)
                 dist.all_reduce(w, op=dist.ReduceOp.MAX)
@@ -171,6 +176,8 @@ def main():
                      "peak_rss_mb": resource.getrusage(resource.RUSAGE_SELF).ru_maxrss // 1024,
                      "workers": workers,
                      "critical_path_s_rank0": best.get("critical_path"),
+                     "per_rank": best.get("per_rank"),
+                     "coordinator_busy_s": best.get("resolve_s"),
                      "redos": best.get("redos"), "redos_unchanged": best.get("redos_unchanged"),
                      "first_run_wall_s": round(runs[0]["wall_s"], 3),
                      "output_bytes": sum(os.path.getsize(os.path.join(out, f"{x}_{mode}{s}"))

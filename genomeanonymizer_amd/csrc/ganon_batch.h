@@ -51,13 +51,16 @@ constexpr uint32_t kSegMine = 1u << 31;     // the segment's read is written by 
 //       (p - ref_start) << 24 (4 bits) | (read_end - p - length) << 28 (4 bits),
 //   w = write scope.
 // wide: one of the two deltas did not fit (the span check then reads ref_start and read_end).
-// A read of 2..kFusedMaxSeg aligned segments (a short read with an I/D/N op, round 5) is always wide
-// and keeps every segment in the extras list instead: x = index of its first extras record, y = its
-// first segment's contig position, z = length << 8 | dataset << 22 | wide | (segments - 1) << 24
-// (3 bits; the query nibble is the extras record's). Extras record (int4, k_prep_scan, at
-// x + k for the read's k-th segment): x = query nibble bits 0-31, y = contig position,
-// z = query nibble bits 32-39 | length << 8, w = 0.
+// A read of 2..kFusedMaxSeg aligned segments (a short read with an I/D/N op, round 5) is described the
+// same way by its FIRST segment, with kDescMulti (bit 7: query nibbles are below 2^39, so bit 7 of the
+// high byte is free) and its further segment count in bits 28-30 instead of the end delta (its span
+// end is checked when its further segments are expanded). Its further segments are in the extras
+// list (k_prep_scan) at xidx[read]: a header {ref_start, read_end, 0, 0}, then one record per further
+// segment (int4: x = query nibble bits 0-31, y = contig position, z = query nibble bits 32-38 |
+// length << 8, w = 0). Round 5's first layout pointed the descriptor at the extras list, and every
+// tile waited for one more dependent load round (c2id k_group 0.56 vs c2 0.49 ms).
 constexpr uint32_t kDescWide = 1u << 23;
+constexpr uint32_t kDescMulti = 1u << 7;
 constexpr int kFusedMaxSeg = 8;   // most aligned segments of a read the fused one-segment mode takes
 // long-read mode: read record (int4; k_prep_read_recs, at b_rbase[read] + k for the read's k-th
 // aligned-segment piece, in CIGAR order): x = query nibble bits 0-31, y = contig position,
@@ -122,6 +125,7 @@ struct GrpAux {
   // its incidences with further segments (k_group's first pass, at the group's first incidence:
   // x = the read's extras index, y = scope local | further segments << 12 | dataset << 15 | mine << 31)
   const int4 *xrec;
+  const int32_t *xidx;                          // per multi-segment read: its extras header's index
   int2 *xlist;
   int32_t n_reads, pad_;
   PrepErr *err;
@@ -268,7 +272,7 @@ struct ganon_dbatch {
   // ... and reads of several aligned segments (at most kFusedMaxSeg): their segments as extras records
   // (b_xrec, allocated by the scan with a counter, capacity xcap records: a plan that needs more grows
   // it and scans again, a speculative one is gated), the group kernel's per-group entries (b_xlist)
-  ganon_dev::DBuf b_xrec, b_xlist, b_xcnt;
+  ganon_dev::DBuf b_xrec, b_xlist, b_xcnt, b_xidx;
   int64_t xcap = 0;
   unsigned int *xcount = nullptr;       // the scan's allocation counters (b_xcnt: one stripe of xcap / 64
                                         // records per counter, one 128-byte line each; cleared per plan)

@@ -592,7 +592,7 @@ template <class SH>
 __device__ __forceinline__ int blk_excl_sum(SH &sh, int v, int *total);
 template <class SH>
 __device__ __attribute__((noinline)) int grp_xexpand(SH &sh, const GrpAux *__restrict__ aux, int64_t i_begin, int e0, int n_e,
-                                           int base, int *n_rec);
+                                           int base, int *n_rec, int s_begin, bool first);
 
 // r: incidence c0 + tid's read (loaded a tile ahead by grp_scan_flat). last: the group's last
 // incidence tile — when the further segments of the group's multi-segment reads fit in its free
@@ -624,19 +624,18 @@ __device__ __forceinline__ int grp_tile_flat(SH &sh, const GrpBatch &B, const Gr
       const FlatScope S = sc[j];
       const uint32_t z = (uint32_t)d.z;
       const int n = (int)((z >> 8) & kSegMaxLen), p = d.y;
-      int rs, re, nx = 0;
-      uint64_t sq = (uint64_t)(uint32_t)d.x | ((uint64_t)(z & 0xFF) << 32);
+      // (a multi-segment read: the first segment's end here, the read's end when its further
+      // segments are expanded)
+      const bool multi = (z & kDescMulti) != 0;
+      const int nx = multi ? (int)((z >> 28) & 7) : 0;
+      const uint64_t sq = (uint64_t)(uint32_t)d.x | ((uint64_t)(z & 0x7F) << 32);
+      int rs, re;
       if (z & kDescWide) {
-        // (a multi-segment read: its first segment's query nibble from its first extras record)
-        nx = (int)((z >> 24) & 7);
-        int4 e0 = make_int4(0, 0, 0, 0);
-        if (nx) e0 = aux->xrec[(uint32_t)d.x];
         rs = aux->ref_start[r];
-        re = aux->read_end[r];
-        if (nx) sq = (uint64_t)(uint32_t)e0.x | ((uint64_t)((uint32_t)e0.z & 0xFF) << 32);
+        re = multi ? p + n : aux->read_end[r];
       } else {
         rs = p - (int)((z >> 24) & 15);
-        re = p + n + (int)(z >> 28);
+        re = p + n + (multi ? 0 : (int)(z >> 28));
       }
       int sl = (int)((S.pk >> 42) & ((1ull << 21) - 1));
       const bool huge = sl > kGrpMaxSpan;
@@ -652,10 +651,10 @@ __device__ __forceinline__ int grp_tile_flat(SH &sh, const GrpBatch &B, const Gr
           if (first && nx) {   // its further segments: an entry in the group's list (streamed after the incidences)
             const int k = atomicAdd(&sh.n_xent, 1);
             atomicAdd(&sh.n_xrec, nx);
-            aux->xlist[i_begin + k] = make_int2(d.x, (int)((uint32_t)j | ((uint32_t)nx << 12) | (((z >> 22) & 1u) << 15) |
-                                                           (mine ? 0x80000000u : 0u)));
+            aux->xlist[i_begin + k] = make_int2(r, (int)((uint32_t)j | ((uint32_t)nx << 12) | (((z >> 22) & 1u) << 15) |
+                                                        (mine ? 0x80000000u : 0u)));
           }
-          const uint32_t rz = (uint32_t)((sq >> 32) & 0xFF) | ((uint32_t)((rf >> 32) & 0xFF) << 8) |
+          const uint32_t rz = (uint32_t)((sq >> 32) & 0x7F) | ((uint32_t)((rf >> 32) & 0xFF) << 8) |
                               ((uint32_t)n << 16) | (((z >> 22) & 1u) << 30) | (mine ? kSegMine : 0u);
           rec = make_int4((int)(uint32_t)sq, (int)(uint32_t)rf, (int)rz,
                           (int)((uint32_t)j | ((uint32_t)(p - S.sstart) << 12)));
@@ -679,7 +678,7 @@ __device__ __forceinline__ int grp_tile_flat(SH &sh, const GrpBatch &B, const Gr
     const int ne = sh.n_xent, nr = sh.n_xrec;
     if (ne && nh + nr <= kGrpTile) {
       int got;
-      grp_xexpand(sh, aux, i_begin, 0, ne, nh, &got);   // (every entry fits: ends on a barrier)
+      grp_xexpand(sh, aux, i_begin, 0, ne, nh, &got, s_begin, first);   // (every entry fits: ends on a barrier)
       if (tid >= nh && tid < nh + nr) {
         const int4 x = sh.rec[tid];
         nck = ((((uint32_t)x.z >> 16) & kSegMaxLen) + chunk - 1) / chunk;
@@ -884,7 +883,7 @@ __device__ __forceinline__ void grp_scan_long(const GrpBatch &B, SH &sh, const G
 template <int K, class SH>
 __device__ __forceinline__ void grp_scan_extra(const GrpBatch &B, SH &sh, const GrpRange &R,
                                                          const GrpGlobal &gg, const GrpAux *__restrict__ aux,
-                                                         int64_t i_begin, int n_e, int skip);
+                                                         int64_t i_begin, int n_e, int skip, int s_begin, bool first);
 
 // Fused one-segment mode: the same stream over records made from incidences [i_begin, i_end) tile
 // by tile (grp_tile_flat), each tile through the 2-bit reference when all of its records allow.
@@ -923,7 +922,7 @@ __device__ __forceinline__ void grp_scan_flat(const GrpBatch &B, SH &sh, const G
     __syncthreads();
   }
   const int n_e = sh.n_xent;
-  if (n_e) grp_scan_extra<K>(B, sh, R, gg, aux, i_begin, n_e, skip);
+  if (n_e) grp_scan_extra<K>(B, sh, R, gg, aux, i_begin, n_e, skip, s_begin, first);
 }
 
 // Block-wide exclusive prefix sum of v (every thread calls; ends on a barrier); *total = the sum.
@@ -955,7 +954,7 @@ __device__ __forceinline__ int blk_excl_sum(SH &sh, int v, int *total) {
 // records written. Every thread calls; ends on a barrier.
 template <class SH>
 __device__ __attribute__((noinline)) int grp_xexpand(SH &sh, const GrpAux *__restrict__ aux, int64_t i_begin, int e0, int n_e,
-                                           int base, int *n_rec) {
+                                           int base, int *n_rec, int s_begin, bool first) {
   const int tid = opaque_tid();
   const FlatScope *sc = flat_scopes(sh);
   const unsigned long long *xl = reinterpret_cast<const unsigned long long *>(aux->xlist) + i_begin;
@@ -971,14 +970,21 @@ __device__ __attribute__((noinline)) int grp_xexpand(SH &sh, const GrpAux *__res
     const int j = (int)(ey & 0xFFF);
     const FlatScope S = sc[j];
     const int64_t r0 = (int64_t)(S.pk << 22) >> 22;
-    const uint32_t xi = (uint32_t)ent;
+    const int r = (int)(uint32_t)ent;
+    const uint32_t xi = (uint32_t)aux->xidx[r];
     const uint32_t hi = (((ey >> 15) & 1u) << 30) | (ey & kSegMine);
+    // the read's span check (the tile checked its first segment's end only): a read reaching past
+    // its scope's span is the batch's error, and its further segments stream nothing
+    const int4 h = aux->xrec[xi];
+    const int sl = (int)((S.pk >> 42) & ((1ull << 21) - 1));   // (entries are never made in huge scopes)
+    const bool in_span = h.x >= S.sstart && (int64_t)h.y <= (int64_t)S.sstart + sl;
+    if (!in_span && first) report(aux->err, kErrIncidSpan, s_begin + j, r);
     for (int k = 0; k < nx; ++k) {
       const int4 e = aux->xrec[xi + 1 + k];
       const uint32_t z = (uint32_t)e.z;
-      const int n = (int)((z >> 8) & kSegMaxLen), p = e.y;
+      const int n = in_span ? (int)((z >> 8) & kSegMaxLen) : 0, p = e.y;
       const uint64_t rf = (uint64_t)(r0 + p);
-      const uint32_t rz = (z & 0xFFu) | ((uint32_t)((rf >> 32) & 0xFF) << 8) | ((uint32_t)n << 16) | hi;
+      const uint32_t rz = (z & 0x7Fu) | ((uint32_t)((rf >> 32) & 0xFF) << 8) | ((uint32_t)n << 16) | hi;
       sh.rec[pre + k] = make_int4(e.x, (int)(uint32_t)rf, (int)rz, (int)((uint32_t)j | ((uint32_t)(p - S.sstart) << 12)));
     }
   }
@@ -995,12 +1001,12 @@ __device__ __attribute__((noinline)) int grp_xexpand(SH &sh, const GrpAux *__res
 template <int K, class SH>
 __device__ __forceinline__ void grp_scan_extra(const GrpBatch &B, SH &sh, const GrpRange &R,
                                                          const GrpGlobal &gg, const GrpAux *__restrict__ aux,
-                                                         int64_t i_begin, int n_e, int skip) {
+                                                         int64_t i_begin, int n_e, int skip, int s_begin, bool first) {
   const int tid = opaque_tid();
   const FlatScope *sc = flat_scopes(sh);
   for (int e0 = 0; e0 < n_e;) {
     int nh;
-    const int used = grp_xexpand(sh, aux, i_begin, e0, n_e, 0, &nh);
+    const int used = grp_xexpand(sh, aux, i_begin, e0, n_e, 0, &nh, s_begin, first);
     int nck = 0;
     bool dirty = false;
     if (tid < nh) {
@@ -1776,7 +1782,7 @@ void free_batch(ganon_dbatch *db) {
                   &db->b_seg4, &db->b_grp_part, &db->b_far, &db->b_gokey, &db->b_gopay, &db->b_gtkey, &db->b_gtflag,
                   &db->b_out, &db->b_scope_calls, &db->b_scope_bases, &db->b_small, &db->b_part, &db->b_long, &db->b_nseg,
                   &db->b_scost, &db->b_scan_tmp, &db->b_slots, &db->b_slot0, &db->b_order, &db->b_desc, &db->b_cand,
-                  &db->b_sdirty, &db->b_inc4, &db->b_rbase, &db->b_rrec, &db->b_xrec, &db->b_xlist, &db->b_xcnt};
+                  &db->b_sdirty, &db->b_inc4, &db->b_rbase, &db->b_rrec, &db->b_xrec, &db->b_xlist, &db->b_xcnt, &db->b_xidx};
   for (DBuf *b : bufs) free_buf(*b);
   free_huge(db);
   free_ref(db->own_ref);
@@ -2012,6 +2018,7 @@ int prepare(ganon_ctx *ctx, ganon_dbatch *db, const ganon_batch *host, bool allo
   a.inc4 = static_cast<const int4 *>(db->b_inc4.p);
   a.rrec = static_cast<const int4 *>(db->b_rrec.p);
   a.xrec = static_cast<const int4 *>(db->b_xrec.p);
+  a.xidx = static_cast<const int32_t *>(db->b_xidx.p);
   a.xlist = static_cast<int2 *>(db->b_xlist.p);
   a.n_reads = db->n_reads;
   a.err = db->err;

@@ -158,6 +158,7 @@ struct ScanOut {
   int32_t *nseg;              // k_prep_scan_long: aligned segments of each long read (long-read mode), or null
   int4 *desc;                 // fused one-segment mode: [n_reads] read descriptors (ganon_batch.h), or null
   unsigned long long *cand;   // and [2 g_bound] partition candidates: ~(lowest written offset), atomicMax
+  int32_t *xidx;              // (per multi-segment read: its extras header)
   int4 *xrec;                 // and the extras records of reads of 2..kFusedMaxSeg segments: kXStripes
   unsigned int *xcount;       // stripes of xper records each, stripe k's count at xcount[kXStride * k]
   uint32_t xper;
@@ -455,19 +456,31 @@ __global__ void __launch_bounds__(kPrepThreads, GANON_SCAN_BLOCKS) k_prep_scan(c
         const int nc_r = R.n_cig[r], L_r = R.read_len[r], rs_r = R.ref_start[r], ds_r = R.dataset[r], ws_r = R.write_scope[r];
         const uint32_t *cg = R.cigar + co_r;
         int k = 0, p0 = 0, n0 = 0;
+        uint64_t sq0 = 0;
         // (the segment count is the first loop's; a stripe that overflows writes nothing past it)
         walk_segments(cg, nc_r, L_r, rs_r, cg[0], [&](int qq, int p, int n) {
           const uint64_t sq = 2 * (uint64_t)so_r + (uint64_t)qq;
-          if ((uint64_t)idx + k < s1)
-            O.xrec[idx + k] = make_int4((int)(uint32_t)sq, p, (int)(((uint32_t)(sq >> 32) & 0xFF) | ((uint32_t)n << 8)), 0);
-          if (k == 0) {
+          if (k == 0) {   // (the descriptor's)
+            sq0 = sq;
             p0 = p;
             n0 = n;
+          } else if ((uint64_t)idx + k < s1) {
+            O.xrec[idx + k] = make_int4((int)(uint32_t)sq, p, (int)(((uint32_t)(sq >> 32) & 0x7F) | ((uint32_t)n << 8)), 0);
           }
           ++k;
         });
-        const uint32_t z = ((uint32_t)n0 << 8) | ((uint32_t)(ds_r & 1) << 22) | kDescWide | ((uint32_t)(k - 1) << 24);
-        O.desc[r] = make_int4((int)idx, p0, (int)z, ws_r);
+        int64_t rl = 0;   // the read's end (bam_endpos) for the header: its span is checked there
+        for (int c = 0; c < nc_r; ++c) {
+          const uint32_t w = cg[c];
+          const int op = (int)(w & 0xF);
+          if (is_aligned_op(op) || op == 2 || op == 3) rl += (int64_t)(w >> 4);
+        }
+        if ((uint64_t)idx < s1) O.xrec[idx] = make_int4(rs_r, (int)(rs_r + (rl > 0 ? rl : 1)), 0, 0);
+        O.xidx[r] = (int32_t)idx;
+        const int d1 = p0 - rs_r;
+        const uint32_t z = ((uint32_t)(sq0 >> 32) & 0x7F) | kDescMulti | ((uint32_t)n0 << 8) | ((uint32_t)(ds_r & 1) << 22) |
+                           (d1 > 15 ? kDescWide : (uint32_t)d1 << 24) | ((uint32_t)(k - 1) << 28);
+        O.desc[r] = make_int4((int)(uint32_t)sq0, p0, (int)z, ws_r);
       }
     }
     acc[kPartWritten] = n_wr;
@@ -1837,6 +1850,7 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db, bool allow_spec) {
   unsigned long long *cand = nullptr;
   int4 *desc = nullptr, *xrec = nullptr;
   int2 *xlist = nullptr;
+  int32_t *xidx = nullptr;
   uint8_t *sdirty = nullptr;   // (k_prep_cands)
   if (db->fused) {
     // extras records of multi-segment reads: the list keeps its capacity (at least one per 8 reads)
@@ -1847,7 +1861,8 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db, bool allow_spec) {
         (rc = grow_n(ctx, db->b_cand, 2 * (size_t)g_bound, &cand)) ||
         (rc = grow_n(ctx, db->b_sdirty, (size_t)std::max<int64_t>(ns, 1), &sdirty)) ||
         (rc = grow_n(ctx, db->b_xrec, (size_t)xwant, &xrec)) ||
-        (rc = grow_n(ctx, db->b_xlist, (size_t)std::max<int64_t>(db->n_incid, 1), &xlist)))
+        (rc = grow_n(ctx, db->b_xlist, (size_t)std::max<int64_t>(db->n_incid, 1), &xlist)) ||
+        (rc = grow_n(ctx, db->b_xidx, (size_t)std::max<int64_t>(nr, 1), &xidx)))
       return rc;
     db->xcap = std::min<int64_t>(INT32_MAX, (int64_t)((db->b_xrec.bytes - 128) / sizeof(int4)));
     if (ctx->xrec_init > 0 && db->xcap > xwant) db->xcap = xwant;   // (testing knob: the capacity asked for)
@@ -1856,7 +1871,7 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db, bool allow_spec) {
   unsigned int *long_count = db->long_count;
   const int64_t pstride = nb + kLongGrid;
   if ((rc = grow_n(ctx, db->b_xcnt, (size_t)kXStripes * kXStride, &db->xcount))) return rc;
-  const ScanOut O{read_end, long_list, long_count, gm, g_bound, part, pstride, nullptr, desc, cand, xrec, db->xcount,
+  const ScanOut O{read_end, long_list, long_count, gm, g_bound, part, pstride, nullptr, desc, cand, xidx, xrec, db->xcount,
                   (uint32_t)(xrec ? db->xcap / kXStripes : 0)};
   // the speculation's segment bound: a fused plan takes multi-segment reads, the record pass does not
   const int spec_maxseg = db->fused ? kFusedMaxSeg : 1;

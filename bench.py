@@ -338,6 +338,7 @@ def e2e_lines(args) -> dict:
     try:
         t = time.perf_counter()
         inp = os.path.join(d, "in")
+        stage("e2e: generating the 24-contig pair")
         make_pair(inp, n_contigs=args.e2e_contigs, pairs_per_contig=args.e2e_pairs)
         gen_s = time.perf_counter() - t
         tool = os.path.join(REPO, "tools", "e2e_bench.py")
@@ -381,10 +382,12 @@ def e2e_lines(args) -> dict:
         if args.e2e_chrom_pairs > 0:
             t = time.perf_counter()
             cin = os.path.join(d, "chrom_in")
+            stage("e2e: generating the chromosome-scale pair")
             make_pair(cin, n_contigs=2, contig_len=args.e2e_chrom_len, pairs_per_contig=args.e2e_chrom_pairs,
                       window_every=20_000, seed=9)
             cgen = time.perf_counter() - t
             cov = 2 * args.e2e_chrom_pairs * 150 / args.e2e_chrom_len
+            stage("e2e: chromosome-scale runs")
             ch = _child_json([sys.executable, tool, cin, os.path.join(d, "chrom_out"), "stream"],
                              {"E2E_RUNS": "1", "E2E_WORKERS": str(args.e2e_workers), "E2E_DISK_PROBE": "1"}, 900)
             cs = ch.get("stream", {})
@@ -421,6 +424,7 @@ def e2e_lines(args) -> dict:
             shutil.rmtree(os.path.join(d, "chrom_out"), ignore_errors=True)
             shutil.rmtree(os.path.join(d, "chrom_one"), ignore_errors=True)
         # the CPU path on a bounded sample (the first contigs)
+        stage("e2e: the CPU pipeline")
         cpu_in = os.path.join(d, "cpu_in")
         make_pair(cpu_in, n_contigs=args.e2e_cpu_contigs, pairs_per_contig=args.e2e_pairs, seed=8)
         cores = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
@@ -457,6 +461,7 @@ def side_config_lines(args) -> dict:
     to the fields a reader compares."""
     out = {}
     for name, extra in SIDE_CONFIGS.items():
+        stage(f"side config {name} (child bench run)")
         r = _child_json([sys.executable, os.path.abspath(__file__), "--config", name, "--no-e2e", "--no-pcie",
                          "--no-fastq", "--no-cpu-baseline", "--no-side-configs"] + extra, {}, 600)
         if "error" in r:
@@ -469,7 +474,29 @@ def side_config_lines(args) -> dict:
     return out
 
 
+_STAGE = ["start", time.time()]
+
+
+def stage(name: str) -> None:
+    """Name the bench's current stage (the heartbeat reports it)."""
+    _STAGE[0], _STAGE[1] = name, time.time()
+    print(f"[bench] {name}", file=sys.stderr, flush=True)
+
+
+def _heartbeat(every: float = 30.0) -> None:
+    """A line on stderr every `every` seconds while the bench runs (its child runs and data generation
+    print nothing for minutes; a runner that takes a silent command for a hung one must not kill it)."""
+    import threading
+
+    def beat():
+        while True:
+            time.sleep(every)
+            print(f"[bench] ... {_STAGE[0]} ({time.time() - _STAGE[1]:.0f} s)", file=sys.stderr, flush=True)
+    threading.Thread(target=beat, daemon=True, name="bench-heartbeat").start()
+
+
 def main() -> None:
+    _heartbeat()
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -501,6 +528,8 @@ def main() -> None:
     ap.add_argument("--fused-flat", type=int, default=1, help="GANON_PARAM_FUSED_FLAT: 1 the group kernel makes "
                     "the one-segment records from the scan's read descriptors, 0 the record pass")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (BAM -> FASTQ) line")
+    ap.add_argument("--indel-tally", type=int, default=1, help="diagnostic: 0 leaves the germline indel tally out of "
+                    "the step (the line then says so in step_kind; never the metric's setting)")
     ap.add_argument("--no-side-configs", action="store_true", help="skip the c3 / c5 lines (child runs)")
     ap.add_argument("--e2e-contigs", type=int, default=24)
     ap.add_argument("--e2e-pairs", type=int, default=23_000, help="pairs per contig and sample")
@@ -527,8 +556,13 @@ def main() -> None:
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     # end to end first: child processes, before this process initialises the GPU (N = 1 only)
+    if world == 1 and not args.no_e2e:
+        stage("end-to-end lines (child processes)")
     e2e = e2e_lines(args) if world == 1 and not args.no_e2e else {}
+    if world == 1 and args.config == "c2" and not args.no_side_configs:
+        stage("side configs (child bench runs)")
     side = side_config_lines(args) if world == 1 and args.config == "c2" and not args.no_side_configs else None
+    stage(f"{args.config}: generating {args.pipeline * args.batches} batches")
     import torch
     local = int(os.environ.get("LOCAL_RANK", 0))
     dev = local % max(1, torch.cuda.device_count())   # == local on a node with a GPU per rank
@@ -583,7 +617,7 @@ def main() -> None:
             shape = shape or sh
             dbs.append(d)
             # germline indel tally: part of every step when the device scan found I/D ops
-            inds.append(d.indel_tally(a) if sh["id_ops"] else None)
+            inds.append(d.indel_tally(a) if sh["id_ops"] and args.indel_tally else None)
         slots.append({"m": m, "st": st, "ref": r, "dbs": dbs, "inds": inds, "arrs": [a for a, _ in mine],
                       "reads": [i["reads"] for _, i in mine]})
     masker, stream, db, ind = slots[0]["m"], slots[0]["st"], slots[0]["dbs"][0], slots[0]["inds"][0]
@@ -625,6 +659,7 @@ def main() -> None:
                 works[b].wait()
                 works[b] = None
 
+    stage("warmup and timed steps")
     for i in range(args.warmup):
         step(i)
     drain()
@@ -634,8 +669,11 @@ def main() -> None:
     gated0 = sum(d.gated_runs() for sl in slots for d in sl["dbs"])
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    host_s = 0.0   # host time inside step(): the launches (a host-bound step shows host_s ~ dt)
     for i in range(args.steps):
+        th = time.perf_counter()
         step(i)
+        host_s += time.perf_counter() - th
     drain()
     torch.cuda.synchronize()
     if dist is not None:
@@ -696,6 +734,7 @@ def main() -> None:
             k[0] += launches
             k[1] += ms
     masker.set_profiling(False)
+    stage("pcie / fastq / cpu baseline")
     pcie = None if args.no_pcie else pcie_bench(masker, db, arr, args, torch)
     fastq = None if args.no_fastq else fastq_bench(masker, db, arr, args, torch, rank)
     # the run-only step of round 2 (plan kept from the previous step), for comparison
@@ -826,7 +865,8 @@ def main() -> None:
                                   "achieved": round(dom_bytes / (dom_ms * 1e-3) / 1e9, 1),
                                   "traffic": dom_traffic if "k_group" in dom else None,
                                   "frac": round(dom_bytes / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}},
-        "step_kind": "resident batch, plan kept (run only)" if args.resident else
+        "step_kind": ("DIAGNOSTIC: the indel tally left out; " if not args.indel_tally else "") +
+                     ("resident batch, plan kept (run only)" if args.resident else
                      (f"fresh batch: device plan (replan: validation scan, group table, shape checks) + run every "
                       f"step, over {n_b} resident raw batches of the sample with their own reads ({args.pipeline} "
                       f"contexts on their own HIP streams x {args.batches} batches each, stepped in turn; read counts "
@@ -834,8 +874,9 @@ def main() -> None:
                       f"incidence counts than its context's previous one; "
                       + ("speculative plan (the run is enqueued behind the scan, buffers sized on the host from the "
                          "batch's counts for the context's last shape; the scan gates the run; gated timed steps: 0)"
-                         if args.spec_plan else "the plan waits for the scan")),
+                         if args.spec_plan else "the plan waits for the scan"))),
         "batches": per_batch,
+        "host_launch_ms_per_step": round(host_s / args.steps * 1e3, 4),
         "sync_plan_ms_per_step": round(sync_ms, 4) if sync_ms else None,
         "run_only_ms_per_step": round(run_only_ms, 4) if run_only_ms else None,
         "one_stream_ms_per_step": round(one_stream_ms, 4) if one_stream_ms else None,

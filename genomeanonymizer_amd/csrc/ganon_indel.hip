@@ -420,10 +420,23 @@ __global__ void __launch_bounds__(256) k_indel_expand_t(const GanonReadView V, c
 }
 
 // Segment offsets of the filtered observations: seg_off[k] = off[first listed incidence of k].
+// Also marks every segment's first element in segbits: a run of equal keys never crosses a segment
+// boundary. (The 32-bit key's parity bit alone told adjacent segments apart, but the filter empties
+// segments, and two segments of one parity with one empty between them met in one run when the last
+// key of the first equalled the first of the second: a missed TN call or a wrong rank — found by
+// tools/indel_ab.py on a 10 M-read c2id batch, round 5.)
 __global__ void k_indel_segs(const int32_t *__restrict__ seg_first, int32_t n_seg, const int32_t *__restrict__ off,
-                             int32_t *__restrict__ seg_off) {
+                             int32_t *__restrict__ seg_off, uint32_t *__restrict__ segbits) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k <= n_seg) seg_off[k] = off[seg_first[k]];
+  if (k <= n_seg) {
+    const int32_t o = off[seg_first[k]];
+    seg_off[k] = o;
+    atomicOr(segbits + (o >> 5), 1u << (o & 31));
+  }
+}
+
+__device__ __forceinline__ bool seg_start(const uint32_t *__restrict__ segbits, int64_t j) {
+  return segbits && ((segbits[j >> 5] >> (j & 31)) & 1u);
 }
 
 // Exact call identity of two observations at the same (scope, pos): type, length, allele.
@@ -449,26 +462,21 @@ __device__ __forceinline__ unsigned long long reg_key(const GanonReadView &V, co
   return ((unsigned long long)(uint32_t)V.ref_start[o.read] << 32) | o.ord;
 }
 
-__device__ bool normal_covers(const GanonReadView &V, int scope, int pos) {
-  const int64_t i1 = V.incid_off[scope + 1];
-  for (int64_t i = V.incid_off[scope]; i < i1; ++i) {
-    const int r = V.incid_read[i];
-    if (V.dataset[r] == 1 && V.ref_start[r] <= pos && pos < V.read_end[r]) return true;
-  }
-  return false;
-}
-
 #ifndef GANON_CLS_DIAG
 #define GANON_CLS_DIAG 0   // phase timing builds only (tools/build_variant.py): 1 no normal-column check,
 #endif                     // 2 no pass 2, 3 run extents only — all change results
+// Pass 1 of a run (a thread each): call heads, TN state, first registered support; a run with a TN
+// call goes to tn_list for the normal-column check and pass 2 (k_indel_tn, a wave each: the check
+// scans the scope's incidences, a serial loop of dependent gathers for one thread — round 5).
 template <typename KeyT>
 __device__ void classify_run(const GanonReadView &V, const KeyT *__restrict__ keys, const uint32_t *__restrict__ vals,
                              int64_t n, int pos_bits, const IndelObs *__restrict__ obs, uint8_t *__restrict__ flags,
                              int32_t *__restrict__ rank, unsigned long long *__restrict__ repk, int64_t j0,
-                             unsigned long long *__restrict__ n_rec) {
+                             unsigned long long *__restrict__ n_rec, int64_t *__restrict__ tn_list,
+                             unsigned int *__restrict__ tn_count, const uint32_t *__restrict__ segbits) {
   const KeyT key = keys[j0];
   int64_t j1 = j0 + 1;
-  while (j1 < n && keys[j1] == key) ++j1;
+  while (j1 < n && keys[j1] == key && !seg_start(segbits, j1)) ++j1;
 #if GANON_CLS_DIAG == 3
   if (j1 > j0) return;   // (phase timing builds only: results change)
 #endif
@@ -504,8 +512,47 @@ __device__ void classify_run(const GanonReadView &V, const KeyT *__restrict__ ke
 #if GANON_CLS_DIAG == 2
   return;
 #endif
+  (void)n_rec;
+  tn_list[atomicAdd(tn_count, 1u)] = j0;
+}
+
+// A run with a TN call (a wave each): the normal pileup column check over the scope's incidences,
+// 64 at a time; then lane 0 ranks the masked calls and marks their records (pass 2).
+template <typename KeyT>
+__device__ void classify_tn(const GanonReadView &V, const KeyT *__restrict__ keys, const uint32_t *__restrict__ vals,
+                            int64_t n, int pos_bits, const IndelObs *__restrict__ obs, uint8_t *__restrict__ flags,
+                            int32_t *__restrict__ rank, const unsigned long long *__restrict__ repk, int64_t j0,
+                            unsigned long long *__restrict__ n_rec, const uint32_t *__restrict__ segbits) {
+  const int lane = threadIdx.x & 63;
+  const KeyT key = keys[j0];
+  int64_t j1 = j0 + 1;   // the run's end, 64 keys at a time
+  for (;; j1 += 64) {
+    const bool other = j1 + lane >= n || keys[j1 + lane] != key || seg_start(segbits, j1 + lane);
+    const unsigned long long m = __ballot(other);
+    if (m) {
+      j1 += __ffsll((long long)m) - 1;
+      break;
+    }
+  }
+  const int scope = obs[vals[j0]].scope;
   const int pos = V.span_start[scope] + (int)((unsigned long long)key & ((1ull << pos_bits) - 1ull));
-  if (GANON_CLS_DIAG != 1 && !normal_covers(V, scope, pos)) {
+  bool covered = GANON_CLS_DIAG == 1;
+  if (!covered) {
+    const int64_t i0 = V.incid_off[scope], i1 = V.incid_off[scope + 1];
+    for (int64_t b = i0; b < i1; b += 64) {
+      bool c = false;
+      if (b + lane < i1) {
+        const int r = V.incid_read[b + lane];
+        c = V.dataset[r] == 1 && V.ref_start[r] <= pos && pos < V.read_end[r];
+      }
+      if (__any(c)) {
+        covered = true;
+        break;
+      }
+    }
+  }
+  if (lane != 0) return;
+  if (!covered) {
     for (int64_t a = j0; a < j1; ++a) flags[a] = 0;
     return;
   }
@@ -553,7 +600,8 @@ constexpr int kRunChunk = 256 * kRunPer;
 template <typename KeyT>
 __global__ void __launch_bounds__(256) k_indel_runs(const KeyT *__restrict__ keys, const int32_t *__restrict__ n_dev,
                                                     uint8_t *__restrict__ flags, int32_t *__restrict__ run_list,
-                                                    unsigned int *__restrict__ run_count) {
+                                                    unsigned int *__restrict__ run_count,
+                                                    const uint32_t *__restrict__ segbits) {
   const int64_t n = *n_dev;
   __shared__ unsigned int wsum[4];
   __shared__ unsigned int base;
@@ -566,7 +614,9 @@ __global__ void __launch_bounds__(256) k_indel_runs(const KeyT *__restrict__ key
     if (j < n) {
       flags[j] = 0;
       const KeyT k = keys[j];
-      if ((j == 0 || keys[j - 1] != k) && j + 1 < n && keys[j + 1] == k) heads |= 1u << i;
+      if ((j == 0 || keys[j - 1] != k || seg_start(segbits, j)) && j + 1 < n && keys[j + 1] == k &&
+          !seg_start(segbits, j + 1))
+        heads |= 1u << i;
     }
   }
   const unsigned int cnt = __popc(heads);
@@ -606,11 +656,33 @@ __global__ void __launch_bounds__(256) k_indel_classify(const GanonReadView V, c
                                                         unsigned long long *__restrict__ repk,
                                                         const int32_t *__restrict__ run_list,
                                                         const unsigned int *__restrict__ run_count,
-                                                        unsigned long long *__restrict__ n_rec) {
+                                                        unsigned long long *__restrict__ n_rec, int64_t *__restrict__ tn_list,
+                                                        unsigned int *__restrict__ tn_count,
+                                                        const uint32_t *__restrict__ segbits) {
   const int64_t n = *n_dev;
   const unsigned int n_runs = *run_count;
   for (unsigned int ri = blockIdx.x * blockDim.x + threadIdx.x; ri < n_runs; ri += gridDim.x * blockDim.x)
-    classify_run<KeyT>(V, keys, vals, n, pos_bits, obs, flags, rank, repk, run_list[ri], n_rec);
+    classify_run<KeyT>(V, keys, vals, n, pos_bits, obs, flags, rank, repk, run_list[ri], n_rec, tn_list, tn_count,
+                       segbits);
+}
+
+// The runs with a TN call, a wave each (grid-stride over the device-side count).
+template <typename KeyT>
+__global__ void __launch_bounds__(256) k_indel_tn(const GanonReadView V, const KeyT *__restrict__ keys,
+                                                  const uint32_t *__restrict__ vals, const int32_t *__restrict__ n_dev,
+                                                  int pos_bits, const IndelObs *__restrict__ obs,
+                                                  uint8_t *__restrict__ flags, int32_t *__restrict__ rank,
+                                                  const unsigned long long *__restrict__ repk,
+                                                  const int64_t *__restrict__ tn_list,
+                                                  const unsigned int *__restrict__ tn_count,
+                                                  unsigned long long *__restrict__ n_rec,
+                                                  const uint32_t *__restrict__ segbits) {
+  const int64_t n = *n_dev;
+  const unsigned int n_tn = *tn_count;
+  const unsigned int n_waves = gridDim.x * (blockDim.x / 64);
+  for (unsigned int w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; w < n_tn; w += n_waves) {
+    classify_tn<KeyT>(V, keys, vals, n, pos_bits, obs, flags, rank, repk, tn_list[w], n_rec, segbits);
+  }
 }
 
 
@@ -661,6 +733,12 @@ struct ganon_indels {
   int32_t n_seg = 0;                  // scopes with observations (segments of the sort)
   int pos_bits = 1, key_bits = 2;
   bool global = false;                // strategy of the last run (GANON_PARAM_INDEL_SORT 1)
+  // the filtered observations sorted by one global radix sort of 64-bit (scope, position) keys (the
+  // short-read batches, round 5) instead of rocPRIM's segmented sort, whose partitioning copies the
+  // segment counts to the host and SYNCHRONIZES the stream: the host waited ~1 ms per c2id step for
+  // every queued kernel of its context, so the pipelined contexts ran one after another
+  bool gsort = false;
+  bool key64 = false;                 // the last run's keys are 64-bit (global or gsort)
   IndelInc *list = nullptr;
   IndelRead *rdist = nullptr;         // distinct reads with an I/D op (candidate marking)
   uint32_t *map = nullptr;            // candidate map, 2 bits per genome position or hashed cell
@@ -687,7 +765,9 @@ struct ganon_indels {
   unsigned long long *repk = nullptr;
   unsigned long long *counters = nullptr;   // [0] records (classify), [1] write slots
   int32_t *run_list = nullptr;        // first element of each run of >1 observations
-  unsigned int *run_count = nullptr;
+  unsigned int *run_count = nullptr;  // [0] runs, [1] runs with a TN call
+  int64_t *tn_list = nullptr;         // runs with a TN call: their first element
+  uint32_t *segbits = nullptr;        // (segmented sort) bit j: element j starts a segment
   void *temp = nullptr;
   size_t temp_bytes = 0;
   ganon_indel_rec *recs = nullptr;
@@ -749,8 +829,10 @@ int run_tally(ganon_ctx *ctx, ganon_indels *t) {
   const int64_t n = t->n_obs;   // capacity
   const bool filter = !t->global;
   const unsigned lgrid = (unsigned)((t->n_list + kIndelWaves - 1) / kIndelWaves);
+  if (filter && t->key64)   // (one global sort of the capacity: the slots past the filtered count sort last)
+    HIP_OR_FAIL(hipMemsetAsync(t->keys[0], 0xFF, (size_t)t->n_obs * sizeof(unsigned long long), ctx->stream));
   HIP_OR_FAIL(hipMemsetAsync(t->counters, 0, 2 * sizeof(unsigned long long), ctx->stream));
-  HIP_OR_FAIL(hipMemsetAsync(t->run_count, 0, sizeof(unsigned int), ctx->stream));
+  HIP_OR_FAIL(hipMemsetAsync(t->run_count, 0, 2 * sizeof(unsigned int), ctx->stream));
   const unsigned rgrid = (unsigned)((t->n_rdist + kIndelWaves - 1) / kIndelWaves);
   if (filter) {
     // per read block: the map, then its candidate ops (count, scan, list); per incidence: counts
@@ -782,8 +864,11 @@ int run_tally(ganon_ctx *ctx, ganon_indels *t) {
                        t->n_ilist, t->roff, t->cnt);
     bytes = t->temp_bytes;
     if (scan_counts(t, t->temp, bytes, ctx->stream) != hipSuccess) return fail(ctx, GANON_E_DEVICE, "indel scan failed");
-    hipLaunchKernelGGL(k_indel_segs, dim3((unsigned)((t->n_seg + 256) / 256)), dim3(256), 0, ctx->stream,
-                       t->seg_first, t->n_seg, t->off, t->seg_off);
+    if (!t->key64) {
+      HIP_OR_FAIL(hipMemsetAsync(t->segbits, 0, ((size_t)t->n_obs / 32 + 2) * sizeof(uint32_t), ctx->stream));
+      hipLaunchKernelGGL(k_indel_segs, dim3((unsigned)((t->n_seg + 256) / 256)), dim3(256), 0, ctx->stream,
+                         t->seg_first, t->n_seg, t->off, t->seg_off, t->segbits);
+    }
     if ((rc = check_launch(ctx, "indel_candidates"))) return rc;
   }
   {
@@ -805,7 +890,7 @@ int run_tally(ganon_ctx *ctx, ganon_indels *t) {
     KernelScope ks(ctx, "indel_sort");
     size_t bytes = t->temp_bytes;
     int sel = 0;
-    if (sort_pairs<KeyT>(t, t->temp, bytes, t->global, ctx->stream, &sel) != hipSuccess)
+    if (sort_pairs<KeyT>(t, t->temp, bytes, t->key64, ctx->stream, &sel) != hipSuccess)
       return fail(ctx, GANON_E_DEVICE, "indel radix sort failed");
     if (sel < 0) return fail(ctx, GANON_E_DEVICE, "indel radix sort: key/value buffers diverged");
     t->sorted_sel = sel;
@@ -813,14 +898,21 @@ int run_tally(ganon_ctx *ctx, ganon_indels *t) {
   {
     KernelScope ks(ctx, "k_indel_classify");
     const KeyT *keys = static_cast<const KeyT *>(t->keys[t->sorted_sel]);
+    // (segment starts: the segmented sort's filtered path only; 64-bit keys hold the whole scope)
+    const uint32_t *segbits = filter && !t->key64 ? t->segbits : nullptr;
     hipLaunchKernelGGL(k_indel_runs<KeyT>, dim3((unsigned)((n + kRunChunk - 1) / kRunChunk)), dim3(256), 0,
-                       ctx->stream, keys, t->n_dev(), t->flags, t->run_list, t->run_count);
+                       ctx->stream, keys, t->n_dev(), t->flags, t->run_list, t->run_count, segbits);
     // runs <= n / 2 (the counts stay on the device): one thread per possible run, the threads past
     // the count leave at once
     const unsigned grid = (unsigned)std::max<int64_t>(1, (n / 2 + 255) / 256);   // (n = 1: one idle workgroup)
     hipLaunchKernelGGL(k_indel_classify<KeyT>, dim3(grid), dim3(256), 0, ctx->stream, t->V, keys,
                        t->vals[t->sorted_sel], t->n_dev(), t->pos_bits, t->obs, t->flags, t->rank, t->repk,
-                       t->run_list, t->run_count, t->counters);
+                       t->run_list, t->run_count, t->counters, t->tn_list, t->run_count + 1, segbits);
+    // runs with a TN call: a wave each (at most one per two observations; waves past the count leave)
+    const unsigned tgrid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n / 2 + 3) / 4, 4096));
+    hipLaunchKernelGGL(k_indel_tn<KeyT>, dim3(tgrid), dim3(256), 0, ctx->stream, t->V, keys, t->vals[t->sorted_sel],
+                       t->n_dev(), t->pos_bits, t->obs, t->flags, t->rank, t->repk, t->tn_list, t->run_count + 1,
+                       t->counters, segbits);
     if ((rc = check_launch(ctx, "k_indel_classify"))) return rc;
   }
   return GANON_OK;
@@ -924,6 +1016,8 @@ GANON_API int ganon_indel_upload(ganon_ctx *ctx, const ganon_batch *b, const gan
   {
     const char *tw = getenv("GANON_INDEL_WAVE_WALK");   // (A/B: 1 keeps the wave-per-block walks)
     t->thread_walk = max_nc_id <= kThreadWalkOps && !(tw && tw[0] == '1');
+    const char *ss = getenv("GANON_INDEL_SEGSORT");   // (A/B: 1 keeps the segmented sort)
+    t->gsort = t->thread_walk && !(ss && ss[0] == '1');
     // hashed map: 2^k cells, at least 64 per candidate-marking op, when that is smaller than the
     // genome's positions (env GANON_INDEL_DENSE_MAP=1: always dense, A/B)
     int k = 12;
@@ -964,7 +1058,9 @@ GANON_API int ganon_indel_upload(ganon_ctx *ctx, const ganon_batch *b, const gan
     if ((rc = ind_alloc(ctx, t, &t->repk, (size_t)n_obs))) return bail(rc);
     if ((rc = ind_alloc(ctx, t, &t->counters, 2))) return bail(rc);
     if ((rc = ind_alloc(ctx, t, &t->run_list, (size_t)n_obs / 2 + 1))) return bail(rc);
-    if ((rc = ind_alloc(ctx, t, &t->run_count, 1))) return bail(rc);
+    if ((rc = ind_alloc(ctx, t, &t->run_count, 2))) return bail(rc);
+    if ((rc = ind_alloc(ctx, t, &t->tn_list, (size_t)n_obs / 2 + 1))) return bail(rc);
+    if ((rc = ind_alloc(ctx, t, &t->segbits, (size_t)n_obs / 32 + 2))) return bail(rc);
     // temp storage: the largest of the two sorts and the count scan
     size_t seg_bytes = 0, glob_bytes = 0, scan_bytes = 0, rscan_bytes = 0;
     if (sort_pairs<uint32_t>(t, nullptr, seg_bytes, false, ctx->stream, nullptr) != hipSuccess ||
@@ -1001,7 +1097,8 @@ GANON_API int ganon_indel_run(ganon_ctx *ctx, ganon_indels *t) {
   t->n_candidates = -1;
   if (t->n_obs == 0) return GANON_OK;
   t->global = ctx->indel_sort != 0;
-  return t->global ? run_tally<unsigned long long>(ctx, t) : run_tally<uint32_t>(ctx, t);
+  t->key64 = t->global || t->gsort;
+  return t->key64 ? run_tally<unsigned long long>(ctx, t) : run_tally<uint32_t>(ctx, t);
 }
 
 GANON_API int64_t ganon_indel_download(ganon_ctx *ctx, ganon_indels *t, ganon_indel_rec *out, int64_t cap) {
@@ -1030,7 +1127,7 @@ GANON_API int64_t ganon_indel_download(ganon_ctx *ctx, ganon_indels *t, ganon_in
   const unsigned grid = (unsigned)((n + 255) / 256);
   e = hipMemsetAsync(t->counters + 1, 0, sizeof(unsigned long long), ctx->stream);
   if (e != hipSuccess) return fail(ctx, GANON_E_DEVICE, "indel download: %s", hipGetErrorString(e));
-  if (t->global)
+  if (t->key64)
     hipLaunchKernelGGL(k_indel_write<unsigned long long>, dim3(grid), dim3(256), 0, ctx->stream, t->V,
                        static_cast<const unsigned long long *>(t->keys[t->sorted_sel]), t->vals[t->sorted_sel],
                        t->n_dev(), t->pos_bits, t->obs, t->flags, t->rank, t->counters + 1, t->recs);
@@ -1050,7 +1147,7 @@ GANON_API int ganon_indel_info(const ganon_indels *t, int64_t *info8) {
   if (!t || !info8) return GANON_E_ARG;
   info8[0] = t->n_obs;
   info8[1] = t->n_list;
-  info8[2] = t->global ? t->key_bits : t->pos_bits;
+  info8[2] = t->key64 ? t->key_bits : t->pos_bits;
   info8[3] = t->n_records;
   info8[4] = t->n_candidates;
   info8[5] = t->n_rdist;

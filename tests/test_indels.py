@@ -167,14 +167,16 @@ def test_hip_indel_known_answers_and_random_batches(hip_built):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("env", [{}, {"GANON_INDEL_WAVE_WALK": "1"}, {"GANON_INDEL_DENSE_MAP": "1"}],
-                         ids=["thread_walk_hashed", "wave_walk", "dense_map"])
+@pytest.mark.parametrize("env", [{}, {"GANON_INDEL_WAVE_WALK": "1"}, {"GANON_INDEL_DENSE_MAP": "1"},
+                                 {"GANON_INDEL_SEGSORT": "1"}],
+                         ids=["thread_walk_hashed_gsort", "wave_walk", "dense_map", "segmented_sort"])
 def test_hip_indel_short_read_paths_match_oracle(env, hip_built, monkeypatch):
     """Short-read batches (round 5): the candidate walks and the incidence expansion take a thread per
-    read / incidence, and the candidate map is hashed (2 bits per cell, 64 cells per op: a collision
-    can only add a position). Equal to the oracle, and to the wave-per-block walks and the dense
-    genome map (the A/B switches, read at indel upload), on dense indel batches and on a c2id-shaped
-    batch (germline het deletions + sequencing indels, ~3 % of the reads)."""
+    read / incidence, the candidate map is hashed (2 bits per cell, 64 cells per op: a collision can
+    only add a position), and the filtered observations are sorted by one global 64-bit radix sort (no
+    host synchronization). Equal to the oracle, and to the wave-per-block walks, the dense genome map
+    and the segmented sort (the A/B switches, read at indel upload), on dense indel batches and on a
+    c2id-shaped batch (germline het deletions + sequencing indels, ~3 % of the reads)."""
     import indel_oracle
     from genomeanonymizer_amd import native
     from genomeanonymizer_amd.synth.batch import config2_batch, indel_batch
@@ -191,6 +193,48 @@ def test_hip_indel_short_read_paths_match_oracle(env, hip_built, monkeypatch):
             assert np.array_equal(got, want)
     finally:
         m.close()
+
+
+def empty_segment_batch():
+    """Three scopes of one contig, each call at the same position relative to its span: scopes 0 and 2
+    hold a TN deletion (a tumor and a normal read), scope 1 a tumor-only one that the T∧N candidate
+    filter removes — so scope 1's sort segment is empty and scopes 0 and 2 (one segment parity) meet in
+    the sorted array with equal 32-bit keys (round 5's segmented-sort bug, tools/indel_ab.py)."""
+    ref = "ACGTACGTAC" * 30
+    reads = []
+    for s, base in ((0, 5), (1, 105), (2, 205)):
+        allele = ref[base:base + 8] + ref[base + 10:base + 22]
+        reads.append(([s], base, "8M2D12M", allele, 0, s))
+        if s != 1:
+            reads.append(([s], base, "8M2D12M", allele, 1, s))
+    return scope_batch(ref, reads, n_scopes=3)
+
+
+def test_indel_oracle_empty_segment_batch():
+    import indel_oracle
+    recs = indel_oracle.indel_records(empty_segment_batch())
+    calls = sorted((r[0], r[1]) for r in recs if r[5] == 0)
+    assert calls == [(0, 13), (2, 213)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("env", [{}, {"GANON_INDEL_SEGSORT": "1"}, {"GANON_INDEL_WAVE_WALK": "1"}],
+                         ids=["global_sort", "segmented_sort", "wave_walk"])
+def test_hip_indel_runs_never_cross_scopes(env, hip_built, monkeypatch):
+    """Equal sort keys of two scopes whose segments an emptied segment separates stay two runs: the
+    segmented path marks every segment's first element (k_indel_segs) and a run stops there."""
+    import indel_oracle
+    from genomeanonymizer_amd import native
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    arr = empty_segment_batch()
+    want = native.indel_records_array(indel_oracle.indel_records(arr))
+    m = native.HipMasker(0)
+    try:
+        *_, got = m.mask(arr, indels=True)
+    finally:
+        m.close()
+    assert np.array_equal(got, want)
 
 
 @pytest.mark.gpu

@@ -431,7 +431,9 @@ __global__ void k_indel_segs(const int32_t *__restrict__ seg_first, int32_t n_se
   if (k <= n_seg) {
     const int32_t o = off[seg_first[k]];
     seg_off[k] = o;
-    atomicOr(segbits + (o >> 5), 1u << (o & 31));
+    // (non-empty segments only: the empty ones share their successor's start, and thousands of
+    // atomics on one word serialised the kernel — 0.3 ms on c2id)
+    if (k < n_seg && off[seg_first[k + 1]] > o) atomicOr(segbits + (o >> 5), 1u << (o & 31));
   }
 }
 
@@ -465,15 +467,24 @@ __device__ __forceinline__ unsigned long long reg_key(const GanonReadView &V, co
 #ifndef GANON_CLS_DIAG
 #define GANON_CLS_DIAG 0   // phase timing builds only (tools/build_variant.py): 1 no normal-column check,
 #endif                     // 2 no pass 2, 3 run extents only — all change results
-// Pass 1 of a run (a thread each): call heads, TN state, first registered support; a run with a TN
-// call goes to tn_list for the normal-column check and pass 2 (k_indel_tn, a wave each: the check
-// scans the scope's incidences, a serial loop of dependent gathers for one thread — round 5).
+__device__ bool normal_covers(const GanonReadView &V, int scope, int pos) {
+  const int64_t i1 = V.incid_off[scope + 1];
+  for (int64_t i = V.incid_off[scope]; i < i1; ++i) {
+    const int r = V.incid_read[i];
+    if (V.dataset[r] == 1 && V.ref_start[r] <= pos && pos < V.read_end[r]) return true;
+  }
+  return false;
+}
+
+// One run (a thread each): call heads, TN state, first registered support; the normal pileup column;
+// ranks and records of the masked calls. (Round 5 tried the column check a wave per TN run: no gain
+// on c2id, and long-read runs lost the thread-per-run parallelism of their second pass: c5 classify
+// 0.72 -> 3.8 ms. Not kept.)
 template <typename KeyT>
 __device__ void classify_run(const GanonReadView &V, const KeyT *__restrict__ keys, const uint32_t *__restrict__ vals,
                              int64_t n, int pos_bits, const IndelObs *__restrict__ obs, uint8_t *__restrict__ flags,
                              int32_t *__restrict__ rank, unsigned long long *__restrict__ repk, int64_t j0,
-                             unsigned long long *__restrict__ n_rec, int64_t *__restrict__ tn_list,
-                             unsigned int *__restrict__ tn_count, const uint32_t *__restrict__ segbits) {
+                             unsigned long long *__restrict__ n_rec, const uint32_t *__restrict__ segbits) {
   const KeyT key = keys[j0];
   int64_t j1 = j0 + 1;
   while (j1 < n && keys[j1] == key && !seg_start(segbits, j1)) ++j1;
@@ -512,47 +523,8 @@ __device__ void classify_run(const GanonReadView &V, const KeyT *__restrict__ ke
 #if GANON_CLS_DIAG == 2
   return;
 #endif
-  (void)n_rec;
-  tn_list[atomicAdd(tn_count, 1u)] = j0;
-}
-
-// A run with a TN call (a wave each): the normal pileup column check over the scope's incidences,
-// 64 at a time; then lane 0 ranks the masked calls and marks their records (pass 2).
-template <typename KeyT>
-__device__ void classify_tn(const GanonReadView &V, const KeyT *__restrict__ keys, const uint32_t *__restrict__ vals,
-                            int64_t n, int pos_bits, const IndelObs *__restrict__ obs, uint8_t *__restrict__ flags,
-                            int32_t *__restrict__ rank, const unsigned long long *__restrict__ repk, int64_t j0,
-                            unsigned long long *__restrict__ n_rec, const uint32_t *__restrict__ segbits) {
-  const int lane = threadIdx.x & 63;
-  const KeyT key = keys[j0];
-  int64_t j1 = j0 + 1;   // the run's end, 64 keys at a time
-  for (;; j1 += 64) {
-    const bool other = j1 + lane >= n || keys[j1 + lane] != key || seg_start(segbits, j1 + lane);
-    const unsigned long long m = __ballot(other);
-    if (m) {
-      j1 += __ffsll((long long)m) - 1;
-      break;
-    }
-  }
-  const int scope = obs[vals[j0]].scope;
   const int pos = V.span_start[scope] + (int)((unsigned long long)key & ((1ull << pos_bits) - 1ull));
-  bool covered = GANON_CLS_DIAG == 1;
-  if (!covered) {
-    const int64_t i0 = V.incid_off[scope], i1 = V.incid_off[scope + 1];
-    for (int64_t b = i0; b < i1; b += 64) {
-      bool c = false;
-      if (b + lane < i1) {
-        const int r = V.incid_read[b + lane];
-        c = V.dataset[r] == 1 && V.ref_start[r] <= pos && pos < V.read_end[r];
-      }
-      if (__any(c)) {
-        covered = true;
-        break;
-      }
-    }
-  }
-  if (lane != 0) return;
-  if (!covered) {
+  if (GANON_CLS_DIAG != 1 && !normal_covers(V, scope, pos)) {
     for (int64_t a = j0; a < j1; ++a) flags[a] = 0;
     return;
   }
@@ -656,35 +628,13 @@ __global__ void __launch_bounds__(256) k_indel_classify(const GanonReadView V, c
                                                         unsigned long long *__restrict__ repk,
                                                         const int32_t *__restrict__ run_list,
                                                         const unsigned int *__restrict__ run_count,
-                                                        unsigned long long *__restrict__ n_rec, int64_t *__restrict__ tn_list,
-                                                        unsigned int *__restrict__ tn_count,
+                                                        unsigned long long *__restrict__ n_rec,
                                                         const uint32_t *__restrict__ segbits) {
   const int64_t n = *n_dev;
   const unsigned int n_runs = *run_count;
   for (unsigned int ri = blockIdx.x * blockDim.x + threadIdx.x; ri < n_runs; ri += gridDim.x * blockDim.x)
-    classify_run<KeyT>(V, keys, vals, n, pos_bits, obs, flags, rank, repk, run_list[ri], n_rec, tn_list, tn_count,
-                       segbits);
+    classify_run<KeyT>(V, keys, vals, n, pos_bits, obs, flags, rank, repk, run_list[ri], n_rec, segbits);
 }
-
-// The runs with a TN call, a wave each (grid-stride over the device-side count).
-template <typename KeyT>
-__global__ void __launch_bounds__(256) k_indel_tn(const GanonReadView V, const KeyT *__restrict__ keys,
-                                                  const uint32_t *__restrict__ vals, const int32_t *__restrict__ n_dev,
-                                                  int pos_bits, const IndelObs *__restrict__ obs,
-                                                  uint8_t *__restrict__ flags, int32_t *__restrict__ rank,
-                                                  const unsigned long long *__restrict__ repk,
-                                                  const int64_t *__restrict__ tn_list,
-                                                  const unsigned int *__restrict__ tn_count,
-                                                  unsigned long long *__restrict__ n_rec,
-                                                  const uint32_t *__restrict__ segbits) {
-  const int64_t n = *n_dev;
-  const unsigned int n_tn = *tn_count;
-  const unsigned int n_waves = gridDim.x * (blockDim.x / 64);
-  for (unsigned int w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; w < n_tn; w += n_waves) {
-    classify_tn<KeyT>(V, keys, vals, n, pos_bits, obs, flags, rank, repk, tn_list[w], n_rec, segbits);
-  }
-}
-
 
 // Records in device order (slots from an atomic counter; the host sorts them).
 template <typename KeyT>
@@ -765,8 +715,7 @@ struct ganon_indels {
   unsigned long long *repk = nullptr;
   unsigned long long *counters = nullptr;   // [0] records (classify), [1] write slots
   int32_t *run_list = nullptr;        // first element of each run of >1 observations
-  unsigned int *run_count = nullptr;  // [0] runs, [1] runs with a TN call
-  int64_t *tn_list = nullptr;         // runs with a TN call: their first element
+  unsigned int *run_count = nullptr;
   uint32_t *segbits = nullptr;        // (segmented sort) bit j: element j starts a segment
   void *temp = nullptr;
   size_t temp_bytes = 0;
@@ -793,6 +742,14 @@ void ind_release(ganon_indels *t) {
   t->allocs.clear();
 }
 
+// rocPRIM's default segmented config partitions the segments by size once there are 3,000 or more,
+// and the partitioning copies the small / medium / large counts to the host with a stream
+// synchronization: every segmented sort waited for its context's whole queue (the host ~1 ms per c2id
+// step, round 5). This config never partitions (the threshold is out of reach) and still sorts short
+// segments a warp each (unpartitioned warp sort).
+using SegSortConfig = rocprim::segmented_radix_sort_config<7, rocprim::kernel_config<256, 16>,
+                                                           rocprim::WarpSortConfig<32, 4, 256, 0xFFFFFFFFu>, true>;
+
 // Segmented (filtered observations, device segment offsets) or one global sort (all observations).
 // num_items is the capacity: the filtered count stays on the device, the segments bound the work.
 template <typename KeyT>
@@ -803,7 +760,7 @@ hipError_t sort_pairs(ganon_indels *t, void *temp, size_t &bytes, bool global, h
   if (global)
     e = rocprim::radix_sort_pairs(temp, bytes, K, Vb, (unsigned int)t->n_obs, 0u, (unsigned int)t->key_bits, st);
   else
-    e = rocprim::segmented_radix_sort_pairs(temp, bytes, K, Vb, (unsigned int)t->n_obs, (unsigned int)t->n_seg,
+    e = rocprim::segmented_radix_sort_pairs<SegSortConfig>(temp, bytes, K, Vb, (unsigned int)t->n_obs, (unsigned int)t->n_seg,
                                             t->seg_off, t->seg_off + 1, 0u, (unsigned int)t->pos_bits, st);
   if (sel) {
     const int ks = K.current() == static_cast<KeyT *>(t->keys[0]) ? 0 : 1;
@@ -832,7 +789,7 @@ int run_tally(ganon_ctx *ctx, ganon_indels *t) {
   if (filter && t->key64)   // (one global sort of the capacity: the slots past the filtered count sort last)
     HIP_OR_FAIL(hipMemsetAsync(t->keys[0], 0xFF, (size_t)t->n_obs * sizeof(unsigned long long), ctx->stream));
   HIP_OR_FAIL(hipMemsetAsync(t->counters, 0, 2 * sizeof(unsigned long long), ctx->stream));
-  HIP_OR_FAIL(hipMemsetAsync(t->run_count, 0, 2 * sizeof(unsigned int), ctx->stream));
+  HIP_OR_FAIL(hipMemsetAsync(t->run_count, 0, sizeof(unsigned int), ctx->stream));
   const unsigned rgrid = (unsigned)((t->n_rdist + kIndelWaves - 1) / kIndelWaves);
   if (filter) {
     // per read block: the map, then its candidate ops (count, scan, list); per incidence: counts
@@ -907,12 +864,7 @@ int run_tally(ganon_ctx *ctx, ganon_indels *t) {
     const unsigned grid = (unsigned)std::max<int64_t>(1, (n / 2 + 255) / 256);   // (n = 1: one idle workgroup)
     hipLaunchKernelGGL(k_indel_classify<KeyT>, dim3(grid), dim3(256), 0, ctx->stream, t->V, keys,
                        t->vals[t->sorted_sel], t->n_dev(), t->pos_bits, t->obs, t->flags, t->rank, t->repk,
-                       t->run_list, t->run_count, t->counters, t->tn_list, t->run_count + 1, segbits);
-    // runs with a TN call: a wave each (at most one per two observations; waves past the count leave)
-    const unsigned tgrid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n / 2 + 3) / 4, 4096));
-    hipLaunchKernelGGL(k_indel_tn<KeyT>, dim3(tgrid), dim3(256), 0, ctx->stream, t->V, keys, t->vals[t->sorted_sel],
-                       t->n_dev(), t->pos_bits, t->obs, t->flags, t->rank, t->repk, t->tn_list, t->run_count + 1,
-                       t->counters, segbits);
+                       t->run_list, t->run_count, t->counters, segbits);
     if ((rc = check_launch(ctx, "k_indel_classify"))) return rc;
   }
   return GANON_OK;
@@ -1058,8 +1010,7 @@ GANON_API int ganon_indel_upload(ganon_ctx *ctx, const ganon_batch *b, const gan
     if ((rc = ind_alloc(ctx, t, &t->repk, (size_t)n_obs))) return bail(rc);
     if ((rc = ind_alloc(ctx, t, &t->counters, 2))) return bail(rc);
     if ((rc = ind_alloc(ctx, t, &t->run_list, (size_t)n_obs / 2 + 1))) return bail(rc);
-    if ((rc = ind_alloc(ctx, t, &t->run_count, 2))) return bail(rc);
-    if ((rc = ind_alloc(ctx, t, &t->tn_list, (size_t)n_obs / 2 + 1))) return bail(rc);
+    if ((rc = ind_alloc(ctx, t, &t->run_count, 1))) return bail(rc);
     if ((rc = ind_alloc(ctx, t, &t->segbits, (size_t)n_obs / 32 + 2))) return bail(rc);
     // temp storage: the largest of the two sorts and the count scan
     size_t seg_bytes = 0, glob_bytes = 0, scan_bytes = 0, rscan_bytes = 0;

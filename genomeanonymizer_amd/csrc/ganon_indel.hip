@@ -39,6 +39,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <string>
 #include <vector>
 
 #include "../../include/ganon.h"
@@ -334,6 +335,7 @@ __global__ void __launch_bounds__(kIndelThreads) k_indel_expand(const GanonReadV
 // alone. Batches whose reads with I/D ops all have at most kThreadWalkOps ops walk them a thread
 // each; the same op order, positions and counts as walk_block.
 constexpr int kThreadWalkOps = 32;
+constexpr int64_t kTsortMax = 4096;   // (k_indel_tsort) most observations of one scope
 
 template <typename F>
 __device__ __forceinline__ void thread_walk(const GanonReadView &V, const IndelRead &e, F &&f) {
@@ -366,24 +368,40 @@ __device__ __forceinline__ bool cand_bit(const uint32_t *__restrict__ map, int s
   return ((map[g >> 4] >> (2 * (g & 15))) & 3) == 3;
 }
 
-__global__ void __launch_bounds__(256) k_indel_rcount_t(const GanonReadView V, const IndelRead *__restrict__ reads,
-                                                        int64_t n_reads, const uint32_t *__restrict__ map, int shift,
-                                                        int32_t *__restrict__ cnt) {
-  const int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (w >= n_reads) return;
-  const IndelRead e = reads[w];
-  int total = 0;
-  thread_walk(V, e, [&](int pos, int, int, int) { total += cand_bit(map, shift, e.cbase + pos) ? 1 : 0; });
-  cnt[w] = total;
-}
-
-__global__ void __launch_bounds__(256) k_indel_remit_t(const GanonReadView V, const IndelRead *__restrict__ reads,
+// Count, place and list in one kernel (thread walks): each read's candidates at a block-aggregated
+// allocation (one atomic per block) instead of a count kernel, a device scan and a list kernel;
+// rstart / rcnt per read (the list is read-major within a block, blocks in any order: a read's
+// candidates stay contiguous and in op order, which is all the expansion needs).
+__global__ void __launch_bounds__(256) k_indel_rlist_t(const GanonReadView V, const IndelRead *__restrict__ reads,
                                                        int64_t n_reads, const uint32_t *__restrict__ map, int shift,
-                                                       const int32_t *__restrict__ roff, IndelCand *__restrict__ rcand) {
+                                                       int32_t *__restrict__ rstart, int32_t *__restrict__ rcnt,
+                                                       unsigned int *__restrict__ total, IndelCand *__restrict__ rcand) {
+  __shared__ int wsum[4];
+  __shared__ unsigned int base;
   const int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  IndelRead e{};
+  int cnt = 0;
+  if (w < n_reads) {
+    e = reads[w];
+    thread_walk(V, e, [&](int pos, int, int, int) { cnt += cand_bit(map, shift, e.cbase + pos) ? 1 : 0; });
+  }
+  const int incl = ganon_wave::incl_sum(cnt);
+  if (lane == 63) wsum[wave] = incl;
+  __syncthreads();
+  int wbase = 0, btot = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    wbase += k < wave ? wsum[k] : 0;
+    btot += wsum[k];
+  }
+  if (threadIdx.x == 0) base = btot ? atomicAdd(total, (unsigned int)btot) : 0u;
+  __syncthreads();
   if (w >= n_reads) return;
-  const IndelRead e = reads[w];
-  int64_t slot = roff[w];
+  int64_t slot = (int64_t)base + wbase + incl - cnt;
+  rstart[w] = (int32_t)slot;
+  rcnt[w] = cnt;
+  if (!cnt) return;
   int ord = e.nid0;
   thread_walk(V, e, [&](int pos, int irp, int op, int len) {
     if (cand_bit(map, shift, e.cbase + pos)) rcand[slot++] = IndelCand{pos, irp, (len << 1) | (op == 1 ? 1 : 0), ord};
@@ -391,16 +409,26 @@ __global__ void __launch_bounds__(256) k_indel_remit_t(const GanonReadView V, co
   });
 }
 
+// Observations per incidence from the thread walks' per-read counts (every short read is one block).
+__global__ void k_indel_icount_t(const IndelIncR *__restrict__ inc, int64_t n_inc, const int32_t *__restrict__ rcnt,
+                                 int32_t *__restrict__ cnt) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= n_inc) return;
+  cnt[i] = rcnt[inc[i].rfirst];
+}
+
 template <typename KeyT>
 __global__ void __launch_bounds__(256) k_indel_expand_t(const GanonReadView V, const IndelIncR *__restrict__ inc,
                                                         int64_t n_inc, int pos_bits, const int32_t *__restrict__ roff,
+                                                        const int32_t *__restrict__ rcnt,
                                                         const IndelCand *__restrict__ rcand,
                                                         const int32_t *__restrict__ off, IndelObs *__restrict__ obs,
                                                         KeyT *__restrict__ keys, uint32_t *__restrict__ vals) {
   const int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (w >= n_inc) return;
   const IndelIncR e = inc[w];
-  const int64_t a = roff[e.rfirst], n = roff[e.rfirst + e.rnb] - a;
+  // (roff: the read's start; rcnt: its count — k_indel_rlist_t, every short read one block)
+  const int64_t a = roff[e.rfirst], n = rcnt[e.rfirst];
   if (!n) return;
   const int scope = (int)(e.scope_par & 0x7FFFFFFFu);
   const int span0 = V.span_start[scope];
@@ -437,6 +465,30 @@ __global__ void k_indel_segs(const int32_t *__restrict__ seg_first, int32_t n_se
   }
 }
 
+// Short-read batches (round 5): the filtered observations are already scope-major in registration
+// order (incidence, then op order), so sorting each scope's few observations by position in place — a
+// stable insertion sort, a thread per segment — is the whole sort. (rocPRIM's segmented sort cost
+// 0.17 ms on c2id's ~2e5 mostly empty segments, a global 64-bit radix sort of the capacity 0.09 ms.)
+template <typename KeyT>
+__global__ void __launch_bounds__(256) k_indel_tsort(KeyT *__restrict__ keys, uint32_t *__restrict__ vals,
+                                                     const int32_t *__restrict__ seg_off, int32_t n_seg) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n_seg) return;
+  const int32_t a = seg_off[k], b = seg_off[k + 1];
+  for (int32_t i = a + 1; i < b; ++i) {
+    const KeyT kk = keys[i];
+    const uint32_t vv = vals[i];
+    int32_t j = i - 1;
+    while (j >= a && keys[j] > kk) {
+      keys[j + 1] = keys[j];
+      vals[j + 1] = vals[j];
+      --j;
+    }
+    keys[j + 1] = kk;
+    vals[j + 1] = vv;
+  }
+}
+
 __device__ __forceinline__ bool seg_start(const uint32_t *__restrict__ segbits, int64_t j) {
   return segbits && ((segbits[j >> 5] >> (j & 31)) & 1u);
 }
@@ -467,11 +519,20 @@ __device__ __forceinline__ unsigned long long reg_key(const GanonReadView &V, co
 #ifndef GANON_CLS_DIAG
 #define GANON_CLS_DIAG 0   // phase timing builds only (tools/build_variant.py): 1 no normal-column check,
 #endif                     // 2 no pass 2, 3 run extents only — all change results
+// Does a normal read of the scope cover pos? Eight incidences per round, their loads issued together
+// (one incidence per round was a chain of dependent gathers per TN run).
 __device__ bool normal_covers(const GanonReadView &V, int scope, int pos) {
+  constexpr int kU = 8;
   const int64_t i1 = V.incid_off[scope + 1];
-  for (int64_t i = V.incid_off[scope]; i < i1; ++i) {
-    const int r = V.incid_read[i];
-    if (V.dataset[r] == 1 && V.ref_start[r] <= pos && pos < V.read_end[r]) return true;
+  for (int64_t i = V.incid_off[scope]; i < i1; i += kU) {
+    int r[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) r[u] = i + u < i1 ? V.incid_read[i + u] : -1;
+    bool hit = false;
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+      if (r[u] >= 0) hit |= V.dataset[r[u]] == 1 && V.ref_start[r[u]] <= pos && pos < V.read_end[r[u]];
+    if (hit) return true;
   }
   return false;
 }
@@ -688,6 +749,7 @@ struct ganon_indels {
   // segment counts to the host and SYNCHRONIZES the stream: the host waited ~1 ms per c2id step for
   // every queued kernel of its context, so the pipelined contexts ran one after another
   bool gsort = false;
+  bool tsort = false;                 // short reads: the in-place segment sort (k_indel_tsort), 32-bit keys
   bool key64 = false;                 // the last run's keys are 64-bit (global or gsort)
   IndelInc *list = nullptr;
   IndelRead *rdist = nullptr;         // distinct reads with an I/D op (candidate marking)
@@ -800,26 +862,25 @@ int run_tally(ganon_ctx *ctx, ganon_indels *t) {
     if (t->thread_walk) {
       hipLaunchKernelGGL(k_indel_mark_t, dim3(tgrid), dim3(256), 0, ctx->stream, t->V, t->rdist, t->n_rdist, t->map,
                          t->map_shift);
-      hipLaunchKernelGGL(k_indel_rcount_t, dim3(tgrid), dim3(256), 0, ctx->stream, t->V, t->rdist, t->n_rdist, t->map,
-                         t->map_shift, t->rcnt);
+      // count + place + list in one kernel (its allocation counter: counters[1], idle until download)
+      hipLaunchKernelGGL(k_indel_rlist_t, dim3(tgrid), dim3(256), 0, ctx->stream, t->V, t->rdist, t->n_rdist, t->map,
+                         t->map_shift, t->roff, t->rcnt, reinterpret_cast<unsigned int *>(t->counters + 1), t->rcand);
+      hipLaunchKernelGGL(k_indel_icount_t, dim3((unsigned)((t->n_ilist + 255) / 256)), dim3(256), 0, ctx->stream,
+                         t->ilist, t->n_ilist, t->rcnt, t->cnt);
     } else {
       hipLaunchKernelGGL(k_indel_mark, dim3(rgrid), dim3(kIndelThreads), 0, ctx->stream, t->V, t->rdist, t->n_rdist,
                          t->map, t->map_shift);
       hipLaunchKernelGGL(k_indel_rcount, dim3(rgrid), dim3(kIndelThreads), 0, ctx->stream, t->V, t->rdist, t->n_rdist,
                          t->map, t->map_shift, t->rcnt);
-    }
-    size_t bytes = t->temp_bytes;
-    if (scan_read_counts(t, t->temp, bytes, ctx->stream) != hipSuccess)
-      return fail(ctx, GANON_E_DEVICE, "indel read scan failed");
-    if (t->thread_walk)
-      hipLaunchKernelGGL(k_indel_remit_t, dim3(tgrid), dim3(256), 0, ctx->stream, t->V, t->rdist, t->n_rdist, t->map,
-                         t->map_shift, t->roff, t->rcand);
-    else
+      size_t rb = t->temp_bytes;
+      if (scan_read_counts(t, t->temp, rb, ctx->stream) != hipSuccess)
+        return fail(ctx, GANON_E_DEVICE, "indel read scan failed");
       hipLaunchKernelGGL(k_indel_remit, dim3(rgrid), dim3(kIndelThreads), 0, ctx->stream, t->V, t->rdist, t->n_rdist,
                          t->map, t->map_shift, t->roff, t->rcand);
-    hipLaunchKernelGGL(k_indel_icount, dim3((unsigned)((t->n_ilist + 255) / 256)), dim3(256), 0, ctx->stream, t->ilist,
-                       t->n_ilist, t->roff, t->cnt);
-    bytes = t->temp_bytes;
+      hipLaunchKernelGGL(k_indel_icount, dim3((unsigned)((t->n_ilist + 255) / 256)), dim3(256), 0, ctx->stream,
+                         t->ilist, t->n_ilist, t->roff, t->cnt);
+    }
+    size_t bytes = t->temp_bytes;
     if (scan_counts(t, t->temp, bytes, ctx->stream) != hipSuccess) return fail(ctx, GANON_E_DEVICE, "indel scan failed");
     if (!t->key64) {
       HIP_OR_FAIL(hipMemsetAsync(t->segbits, 0, ((size_t)t->n_obs / 32 + 2) * sizeof(uint32_t), ctx->stream));
@@ -832,7 +893,7 @@ int run_tally(ganon_ctx *ctx, ganon_indels *t) {
     KernelScope ks(ctx, "k_indel_emit");
     if (filter && t->thread_walk)
       hipLaunchKernelGGL(k_indel_expand_t<KeyT>, dim3((unsigned)((t->n_ilist + 255) / 256)), dim3(256), 0, ctx->stream,
-                         t->V, t->ilist, t->n_ilist, t->pos_bits, t->roff, t->rcand, t->off, t->obs,
+                         t->V, t->ilist, t->n_ilist, t->pos_bits, t->roff, t->rcnt, t->rcand, t->off, t->obs,
                          static_cast<KeyT *>(t->keys[0]), t->vals[0]);
     else if (filter)
       hipLaunchKernelGGL(k_indel_expand<KeyT>, dim3((unsigned)((t->n_ilist + kIndelWaves - 1) / kIndelWaves)),
@@ -845,12 +906,19 @@ int run_tally(ganon_ctx *ctx, ganon_indels *t) {
   }
   {
     KernelScope ks(ctx, "indel_sort");
-    size_t bytes = t->temp_bytes;
-    int sel = 0;
-    if (sort_pairs<KeyT>(t, t->temp, bytes, t->key64, ctx->stream, &sel) != hipSuccess)
-      return fail(ctx, GANON_E_DEVICE, "indel radix sort failed");
-    if (sel < 0) return fail(ctx, GANON_E_DEVICE, "indel radix sort: key/value buffers diverged");
-    t->sorted_sel = sel;
+    if (filter && t->tsort) {
+      hipLaunchKernelGGL(k_indel_tsort<KeyT>, dim3((unsigned)((t->n_seg + 255) / 256)), dim3(256), 0, ctx->stream,
+                         static_cast<KeyT *>(t->keys[0]), t->vals[0], t->seg_off, t->n_seg);
+      if ((rc = check_launch(ctx, "k_indel_tsort"))) return rc;
+      t->sorted_sel = 0;
+    } else {
+      size_t bytes = t->temp_bytes;
+      int sel = 0;
+      if (sort_pairs<KeyT>(t, t->temp, bytes, t->key64, ctx->stream, &sel) != hipSuccess)
+        return fail(ctx, GANON_E_DEVICE, "indel radix sort failed");
+      if (sel < 0) return fail(ctx, GANON_E_DEVICE, "indel radix sort: key/value buffers diverged");
+      t->sorted_sel = sel;
+    }
   }
   {
     KernelScope ks(ctx, "k_indel_classify");
@@ -926,8 +994,10 @@ GANON_API int ganon_indel_upload(ganon_ctx *ctx, const ganon_batch *b, const gan
   std::vector<int32_t> seg_first;        // first ilist entry of each segment, then the list size
   int64_t n_obs = 0, n_rcand = 0;
   int32_t max_span = 0;
+  int64_t max_seg_obs = 0;   // most observations of one scope before the filter (k_indel_tsort's bound)
   for (int32_t s = 0; s < b->n_scopes; ++s) {
     max_span = std::max(max_span, b->scope_span_len[s]);
+    const int64_t obs_before = n_obs;
     const uint32_t par = (uint32_t)(seg_first.size() & 1) << 31;
     const int64_t cbase = b->scope_ref_off[s] - b->scope_span_start[s];   // contig start, genome nibbles
     const size_t before = ilist.size();
@@ -951,6 +1021,7 @@ GANON_API int ganon_indel_upload(ganon_ctx *ctx, const ganon_batch *b, const gan
       n_obs += nid[r];
     }
     if (ilist.size() > before) seg_first.push_back((int32_t)before);
+    max_seg_obs = std::max(max_seg_obs, n_obs - obs_before);
   }
   seg_first.push_back((int32_t)ilist.size());
   if (n_obs >= (int64_t)INT32_MAX) return fail(ctx, GANON_E_ARG, "indel upload: %lld observations (max 2^31-1)", (long long)n_obs);
@@ -968,8 +1039,13 @@ GANON_API int ganon_indel_upload(ganon_ctx *ctx, const ganon_batch *b, const gan
   {
     const char *tw = getenv("GANON_INDEL_WAVE_WALK");   // (A/B: 1 keeps the wave-per-block walks)
     t->thread_walk = max_nc_id <= kThreadWalkOps && !(tw && tw[0] == '1');
-    const char *ss = getenv("GANON_INDEL_SEGSORT");   // (A/B: 1 keeps the segmented sort)
-    t->gsort = t->thread_walk && !(ss && ss[0] == '1');
+    // short reads: the in-place segment sort while no scope has more than kTsortMax observations
+    // before the filter (its worst case is quadratic); GANON_INDEL_SORTMODE (A/B): seg = rocPRIM's
+    // segmented sort, global = one 64-bit radix sort of the capacity
+    const char *sm = getenv("GANON_INDEL_SORTMODE");
+    const std::string mode = sm ? sm : "";
+    t->tsort = t->thread_walk && max_seg_obs <= kTsortMax && mode.empty();
+    t->gsort = t->thread_walk && !t->tsort && mode != "seg";
     // hashed map: 2^k cells, at least 64 per candidate-marking op, when that is smaller than the
     // genome's positions (env GANON_INDEL_DENSE_MAP=1: always dense, A/B)
     int k = 12;

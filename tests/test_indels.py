@@ -168,15 +168,16 @@ def test_hip_indel_known_answers_and_random_batches(hip_built):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("env", [{}, {"GANON_INDEL_WAVE_WALK": "1"}, {"GANON_INDEL_DENSE_MAP": "1"},
-                                 {"GANON_INDEL_SEGSORT": "1"}],
-                         ids=["thread_walk_hashed_gsort", "wave_walk", "dense_map", "segmented_sort"])
+                                 {"GANON_INDEL_SORTMODE": "seg"}, {"GANON_INDEL_SORTMODE": "global"}],
+                         ids=["thread_walk_hashed_tsort", "wave_walk", "dense_map", "segmented_sort", "global_sort"])
 def test_hip_indel_short_read_paths_match_oracle(env, hip_built, monkeypatch):
     """Short-read batches (round 5): the candidate walks and the incidence expansion take a thread per
     read / incidence, the candidate map is hashed (2 bits per cell, 64 cells per op: a collision can
-    only add a position), and the filtered observations are sorted by one global 64-bit radix sort (no
-    host synchronization). Equal to the oracle, and to the wave-per-block walks, the dense genome map
-    and the segmented sort (the A/B switches, read at indel upload), on dense indel batches and on a
-    c2id-shaped batch (germline het deletions + sequencing indels, ~3 % of the reads)."""
+    only add a position), and the filtered observations, already scope-major, are sorted in place per
+    scope (k_indel_tsort). Equal to the oracle, and to the wave-per-block walks, the dense genome map,
+    rocPRIM's segmented sort and one global 64-bit sort (the A/B switches, read at indel upload), on
+    dense indel batches and on a c2id-shaped batch (germline het deletions + sequencing indels, ~3 % of
+    the reads)."""
     import indel_oracle
     from genomeanonymizer_amd import native
     from genomeanonymizer_amd.synth.batch import config2_batch, indel_batch
@@ -218,8 +219,9 @@ def test_indel_oracle_empty_segment_batch():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("env", [{}, {"GANON_INDEL_SEGSORT": "1"}, {"GANON_INDEL_WAVE_WALK": "1"}],
-                         ids=["global_sort", "segmented_sort", "wave_walk"])
+@pytest.mark.parametrize("env", [{}, {"GANON_INDEL_SORTMODE": "seg"}, {"GANON_INDEL_SORTMODE": "global"},
+                                 {"GANON_INDEL_WAVE_WALK": "1"}],
+                         ids=["segment_sort", "segmented_sort", "global_sort", "wave_walk"])
 def test_hip_indel_runs_never_cross_scopes(env, hip_built, monkeypatch):
     """Equal sort keys of two scopes whose segments an emptied segment separates stay two runs: the
     segmented path marks every segment's first element (k_indel_segs) and a run stops there."""

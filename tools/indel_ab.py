@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """A/B of the indel tally's strategies on one batch (GPU): the default (short reads: thread walks,
-hashed map, global 64-bit sort) against GANON_INDEL_SEGSORT=1 / GANON_INDEL_WAVE_WALK=1 /
+hashed map, in-place segment sort) against GANON_INDEL_SORTMODE=seg|global / GANON_INDEL_WAVE_WALK=1 /
 GANON_INDEL_DENSE_MAP=1 (read at indel upload). Prints the record counts and the first differences.
 
     python tools/indel_ab.py [READS=10000000]
@@ -25,9 +25,10 @@ def main():
     m = native.HipMasker(0)
     db = m.upload(arr)
     out = {}
-    for name, env in (("default", {}), ("segsort", {"GANON_INDEL_SEGSORT": "1"}),
+    for name, env in (("default", {}), ("segsort", {"GANON_INDEL_SORTMODE": "seg"}),
+                      ("globalsort", {"GANON_INDEL_SORTMODE": "global"}),
                       ("wave_walk", {"GANON_INDEL_WAVE_WALK": "1"}), ("dense_map", {"GANON_INDEL_DENSE_MAP": "1"})):
-        for k in ("GANON_INDEL_SEGSORT", "GANON_INDEL_WAVE_WALK", "GANON_INDEL_DENSE_MAP"):
+        for k in ("GANON_INDEL_SORTMODE", "GANON_INDEL_WAVE_WALK", "GANON_INDEL_DENSE_MAP"):
             os.environ.pop(k, None)
         os.environ.update(env)
         t = db.indel_tally(arr)

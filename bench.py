@@ -417,8 +417,8 @@ def e2e_lines(args) -> dict:
                 "workload": f"synth/fastpair.py: 2 contigs x {args.e2e_chrom_len // 1_000_000} Mb, {args.e2e_chrom_pairs} "
                             f"pairs per contig and sample ({cov:.0f}x per sample, configs[2] density; 150 bp, FR), "
                             f"germline SNPs/deletions as above, a window every 20 kb; contigs cut into runs of sections "
-                            f"of GANON_JOB_BP (default 4 Mb) read by BAI region queries, sharded over "
-                            f"{args.e2e_workers} processes sharing the GPU",
+                            f"(job mode: about 6 jobs per process, at most 4 Mb each) read by BAI region queries, "
+                            f"sharded over {args.e2e_workers} processes sharing the GPU",
                 "error": ch.get("error")}
             shutil.rmtree(cin, ignore_errors=True)
             shutil.rmtree(os.path.join(d, "chrom_out"), ignore_errors=True)

@@ -99,6 +99,13 @@ class JobSpec:
         return self.contig if self.region is None else f"{self.contig}:{self.region[0]}-{self.region[1]}"
 
 
+def auto_job_bp(genome_len: int, world: int) -> int:
+    """Job size when GANON_JOB_BP is unset: 4 Mb, or less so that each of the ``world`` ranks gets
+    about GANON_JOBS_PER_RANK (6) jobs, but at least 256 kb."""
+    per_rank = max(1, int(os.environ.get("GANON_JOBS_PER_RANK", "6")))
+    return int(min(4_000_000, max(256_000, genome_len // max(1, per_rank * world))))
+
+
 def plan_jobs(fasta: FastaRef, windows: Sequence[Window], job_bp: int, indexed: bool) -> List[JobSpec]:
     """The sample's jobs in FASTA then section order. ``job_bp`` > 0 and indexed BAMs: each contig
     longer than job_bp is cut at section boundaries into runs of about job_bp bases (a short tail
@@ -970,7 +977,11 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
                BamReader(normal_bam, threads, window_bytes, inflater))
     # jobs: contigs, or runs of sections of about GANON_JOB_BP bases (default 4 Mb; 0 = whole
     # contigs) when both BAMs are indexed
-    job_bp = int(os.environ.get("GANON_JOB_BP", str(4_000_000)))
+    # (unset: 4 Mb, or smaller so that every rank gets about GANON_JOBS_PER_RANK jobs (default 6, at
+    # least 256 kb each): 2 x 20 Mb over 8 ranks made 10 jobs of 4 Mb, two ranks ran two each and
+    # the rest idled half the wall — round 5's 30x chromosome-scale line)
+    job_bp = int(os.environ.get("GANON_JOB_BP", "0") or 0) if "GANON_JOB_BP" in os.environ else \
+        auto_job_bp(sum(int(L) for L in fasta.lengths), world)
     jobs = plan_jobs(fasta, windows, job_bp, all(r.has_index for r in readers))
     owner = assign_contigs([j.length for j in jobs], world)
     mine = [j for j in range(len(jobs)) if owner[j] == rank]

@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -38,7 +39,10 @@ constexpr int kRing = 2048;          // payload ring (LDS), refilled kRing/2 byt
 constexpr int kRingHalf = kRing / 2;
 constexpr int kOutRing = 32768;      // output ring: DEFLATE's 32 KiB back-reference window
 constexpr int kFlush = 4096;         // output written out per completed chunk of the ring
-constexpr int kFastBits = 10;        // Huffman lookup table width
+#ifndef INF_FAST_BITS
+#define INF_FAST_BITS 10
+#endif
+constexpr int kFastBits = INF_FAST_BITS;   // Huffman lookup table width
 constexpr uint32_t kFastMask = (1u << kFastBits) - 1;
 
 // Canonical Huffman code: counts per length, symbols by (length, value), a kFastBits lookup table
@@ -49,11 +53,16 @@ struct Huff {
   uint16_t fast[1 << kFastBits];
 };
 
+constexpr int kRoundK = 4;        // token rounds: kRoundK x 64 bit offsets decoded at once
+constexpr int kRoundMaxM = 8;     // ... at most this many matches per round
+constexpr int kRoundOut = 2048;   // ... and about this many output bytes (+ one match)
+
 struct InfShared {
   uint8_t out[kOutRing];
   uint8_t ring[kRing];
   Huff lit, dist;
   uint16_t lens[19 + 288 + 32];   // code-length code, then literal/length + distance lengths
+  int4 mrec[kRoundMaxM];          // a round's matches: bit offset, output offset, length, distance
 };
 
 constexpr uint8_t kClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
@@ -76,6 +85,9 @@ inline uint64_t uni64(uint64_t v) { return v; }
 #define INF_WAVE_ORDER() ((void)0)
 #endif
 #define INF_FN __host__ __device__
+// (the decoder state must stay in registers: a helper left out of line takes its reference arguments
+// to the stack, and every access of the bit reader becomes a scratch round trip)
+#define INF_INL __host__ __device__ __attribute__((always_inline)) inline
 
 // LSB-first bit reader. Payload bytes [filled - kRing, filled) are in the LDS ring (index & mask);
 // top_up (wave-uniform: every lane calls it together) keeps at least kRingHalf bytes ahead of pos.
@@ -86,8 +98,10 @@ struct Bits {
   int n, pos, filled, lane;
   uint64_t buf;
   int cnt;
-  INF_FN void top_up() {
-    if (filled < n && filled - pos < kRingHalf) {
+  INF_INL void top_up() {
+    // (refilled 64 bytes early: a token round rewinds pos by up to 8 bytes of the bit buffer, and
+    // those must still be in the ring)
+    if (filled < n && filled - pos < kRingHalf - 64) {
       INF_WAVE_ORDER();   // earlier ring reads are issued before their slots are overwritten
       const int e = filled + kRingHalf < n ? filled + kRingHalf : n;
       // kRingHalf / NL consecutive bytes per lane, all loads issued before the first store
@@ -105,7 +119,7 @@ struct Bits {
   }
   // Tops the bit buffer up to 57..64 bits (or the end of the payload) with one LDS round trip:
   // the three aligned ring dwords under the next 8 bytes.
-  INF_FN void refill() {
+  INF_INL void refill() {
     if (cnt > 56 || pos >= n) return;
     top_up();
     const uint32_t *rw = reinterpret_cast<const uint32_t *>(ring);
@@ -122,18 +136,18 @@ struct Bits {
     cnt += 8 * nb;
     pos += nb;
   }
-  INF_FN bool need(int k) {
+  INF_INL bool need(int k) {
     if (cnt < k) refill();
     return cnt >= k;
   }
   // the decoder state is wave-uniform: say so to the compiler (scalar registers, scalar branches)
-  INF_FN void uniform() {
+  INF_INL void uniform() {
     pos = uni(pos);
     filled = uni(filled);
     cnt = uni(cnt);
     buf = uni64(buf);
   }
-  INF_FN uint32_t take(int k) {   // (need(k) checked by the caller)
+  INF_INL uint32_t take(int k) {   // (need(k) checked by the caller)
     const uint32_t v = k ? (uint32_t)(buf & ((1ull << k) - 1)) : 0u;
     buf >>= k;
     cnt -= k;
@@ -190,7 +204,7 @@ __attribute__((noinline)) INF_FN bool huff_build(Huff &h, const uint16_t *len, i
 // One symbol through the table (header code-length codes); -1 on an invalid code or a stream
 // that ends inside it.
 template <int NL>
-INF_FN int huff_decode(const Huff &h, Bits<NL> &b) {
+INF_INL int huff_decode(const Huff &h, Bits<NL> &b) {
   b.refill();
   if (b.cnt >= kFastBits || b.pos >= b.n) {
     const int e = uni(h.fast[b.buf & kFastMask]);
@@ -233,7 +247,7 @@ __attribute__((noinline)) INF_FN int huff_slow(const Huff &h, uint64_t buf, int 
 
 // Output bytes [from, to) of the ring to dst (the block's output), by the lanes.
 template <int NL>
-INF_FN void flush_out(const uint8_t *ring, uint8_t *dst, int from, int to, int lane) {
+INF_INL void flush_out(const uint8_t *ring, uint8_t *dst, int from, int to, int lane) {
   INF_WAVE_ORDER();   // the ring bytes (lane 0's literals, every lane's copies) are issued
   // dword stores over the aligned middle when the chunk does not wrap the ring
   int a = from;
@@ -260,13 +274,296 @@ INF_FN void flush_out(const uint8_t *ring, uint8_t *dst, int from, int to, int l
   }
 }
 
+
+// Copy of a match: out[w + j] = out[w - dist + j], j < len, by all lanes at once (a periodic source
+// index for an overlapping match: out[w + j] = out[w - dist + (j mod dist)]).
+template <int NL>
+INF_INL void copy_match(InfShared &S, int w, int len, int dist, int lane) {
+  constexpr int M = kOutRing - 1;
+  INF_WAVE_ORDER();   // the literals and the last copy are read by every lane
+  if (dist >= len) {
+    for (int j0 = 0; j0 < len; j0 += NL) {
+      const int j = j0 + lane;
+      if (j < len) S.out[(w + j) & M] = S.out[(w - dist + j) & M];
+    }
+  } else {
+    // lane mod dist, lane < 64 (exact: (lane + 1/2) / dist is >= 1/(2 dist) from an integer)
+    const int q = (int)(((float)lane + 0.5f) / (float)dist);
+    int r = lane - q * dist;
+    const int step = NL % dist;
+    for (int j0 = 0; j0 < len; j0 += NL) {
+      if (j0 + lane < len) S.out[(w + j0 + lane) & M] = S.out[(w - dist + r) & M];
+      r += step;
+      if (r >= dist) r -= dist;
+    }
+  }
+}
+
+// ---- token rounds ------------------------------------------------------------------------------
+// The scalar symbol loop pays one dependent LDS lookup and ~20 scalar instructions per code, and a
+// wave issues one instruction per 4 cycles: ~400 cycles per literal. A round instead decodes, on
+// every lane, the token (literal, or length + distance with their extra bits) that WOULD start at
+// each of the next kRoundK x 64 bit offsets — independent lookups, issued together. The true token
+// boundaries are then a scalar chain through those lanes (readlane: offset -> offset + the token's
+// bit length), a handful of scalar instructions per token; the round's literals are written by
+// their lanes at once, its matches copied in stream order. A token the tables cannot finish (a
+// code longer than kFastBits, the end-of-block code, bits past the payload, an invalid code) stops
+// the chain: the scalar loop decodes that one token, with every check, and rounds resume.
+constexpr uint32_t kTokMatch = 1u << 15, kTokStop = 1u << 16;
+// (tuning build, -DINF_PROF: cycles of each part of a round, summed per wave, tools/inflate_prof.py)
+#if defined(INF_PROF)
+__device__ unsigned long long g_inf_prof[6];
+#endif
+#if defined(INF_PROF) && defined(__HIP_DEVICE_COMPILE__)
+#define INF_T() ((uint64_t)__builtin_amdgcn_s_memtime())
+#define INF_ACC(i, t0) (prof[i] += INF_T() - (t0))
+#else
+#define INF_T() ((uint64_t)0)
+#define INF_ACC(i, t0) ((void)(t0))
+#endif
+#ifdef INF_STATS
+long long inf_stats[8];
+#endif
+
+// The tokens at bits B0 + 64 k (k < kRoundK) of the payload (the ring holds them): bits 0-5 the
+// token's length in bits, 6-14 its output length, kTokMatch, kTokStop, 24-31 a literal's byte;
+// d[k] a match's distance. Branch-free, so that the LDS reads of every k are in flight together:
+// the ring words (the same shift for every k), then the literal/length codes, then the distance
+// codes (looked up for literals too, and ignored).
+INF_INL void lane_tokens(const InfShared &S, uint32_t B0, uint32_t nbits, uint32_t *t, uint32_t *d) {
+  const uint32_t *rw = reinterpret_cast<const uint32_t *>(S.ring);
+  constexpr int kWm = kRing / 4 - 1;
+  const uint32_t wd = B0 >> 5;
+  const int sh = (int)(B0 & 31);
+  uint32_t wv[2 * kRoundK + 1];
+#pragma unroll
+  for (int i = 0; i < 2 * kRoundK + 1; ++i) wv[i] = rw[(wd + (uint32_t)i) & kWm];
+  uint64_t bits[kRoundK];
+  int e[kRoundK];
+#pragma unroll
+  for (int k = 0; k < kRoundK; ++k) {
+    const uint64_t lo = (uint64_t)wv[2 * k] | ((uint64_t)wv[2 * k + 1] << 32);
+    bits[k] = (lo >> sh) | (((uint64_t)wv[2 * k + 2] << 1) << (63 - sh));   // (sh = 0: no high word)
+    e[k] = S.lit.fast[bits[k] & kFastMask];
+  }
+  int len[kRoundK], lbits[kRoundK], dd[kRoundK];
+  uint64_t b2[kRoundK];
+#pragma unroll
+  for (int k = 0; k < kRoundK; ++k) {
+    const int l = e[k] >> 9, sym = e[k] & 511;
+    const int li = sym > 256 ? sym - 257 : 0;   // RFC 1951 3.2.5 length codes
+    const int le = li < 8 || li >= 28 ? 0 : (li - 4) >> 2;
+    const int lb = li < 8 ? 3 + li : li == 28 ? 258 : ((4 + (li & 3)) << le) + 3;
+    len[k] = lb + (int)((bits[k] >> l) & ((1u << le) - 1));
+    lbits[k] = l + le;
+    b2[k] = bits[k] >> lbits[k];
+    dd[k] = S.dist.fast[b2[k] & kFastMask];
+  }
+#pragma unroll
+  for (int k = 0; k < kRoundK; ++k) {
+    const int l = e[k] >> 9, sym = e[k] & 511;
+    const int dl = dd[k] >> 9, ds = dd[k] & 511;
+    const int de = ds < 4 ? 0 : (ds - 2) >> 1;
+    const uint32_t dv = (uint32_t)(ds < 4 ? 1 + ds : ((2 + (ds & 1)) << de) + 1) +
+                        (uint32_t)((b2[k] >> dl) & ((1u << de) - 1));
+    const bool lit = l && sym < 256;
+    const bool match = l && sym > 256 && sym < 257 + 29 && dl && ds < 30;
+    uint32_t tok = lit ? (uint32_t)l | (1u << 6) | ((uint32_t)sym << 24)
+                 : match ? (uint32_t)(lbits[k] + dl + de) | ((uint32_t)len[k] << 6) | kTokMatch : kTokStop;
+    if ((uint64_t)B0 + 64 * k + (tok & 63) > nbits) tok = kTokStop;
+    t[k] = tok;
+    d[k] = dv;
+  }
+}
+
+// The tokens of one round. On the device each lane holds its kRoundK offsets in registers, the
+// chain reads them with readlane and writes each literal's output offset back with writelane; the
+// host build (NL = 1) keeps all kRoundK x 64 in arrays.
+template <int NL>
+struct RoundToks {
+  uint32_t t[kRoundK][64], d[kRoundK][64];
+  int pos[kRoundK][64];
+  INF_FN void fill(const InfShared &S, uint32_t P, uint32_t nbits, int) {
+    for (int l = 0; l < 64; ++l) {
+      uint32_t tt[kRoundK], dd[kRoundK];
+      lane_tokens(S, P + (uint32_t)l, nbits, tt, dd);
+      for (int k = 0; k < kRoundK; ++k) {
+        t[k][l] = tt[k];
+        d[k][l] = dd[k];
+      }
+    }
+  }
+  // The chain through the literals of k from offset xk: each one's output offset recorded, its bit
+  // set in m. Stops at offset 64, at `lim` bytes of output, or at a match / stop token (returned).
+  INF_FN uint32_t chain(int k, int &xk, int &out, int lim, uint64_t &m) {
+    uint32_t tk = 0;
+    while (xk < 64 && out < lim) {
+      tk = t[k][xk];
+      if (tk & (kTokStop | kTokMatch)) break;
+      pos[k][xk] = out;
+      m |= 1ull << xk;
+      ++out;
+      xk += (int)(tk & 63);
+    }
+    return tk;
+  }
+  INF_FN uint32_t dist(int k, int l) const { return d[k][l]; }
+  template <class F>
+  INF_FN void each_literal(const uint64_t (&lm)[kRoundK], int, F &&f) const {
+    for (int k = 0; k < kRoundK; ++k)
+      for (int l = 0; l < 64; ++l)
+        if ((lm[k] >> l) & 1) f(64 * k + l, pos[k][l], (uint8_t)(t[k][l] >> 24));
+  }
+};
+#if defined(__HIP_DEVICE_COMPILE__)
+template <>
+struct RoundToks<64> {
+  uint32_t t[kRoundK], d[kRoundK];
+  int pos[kRoundK];
+  __device__ void fill(const InfShared &S, uint32_t P, uint32_t nbits, int lane) {
+    lane_tokens(S, P + (uint32_t)lane, nbits, t, d);
+  }
+  // (the literal loop in scalar instructions: a readlane, a test, a writelane, a bit set, three adds)
+  __device__ uint32_t chain(int k, int &xk, int &out, int lim, uint64_t &m) {
+    uint32_t tk, tmp;
+    int p = pos[k];
+    xk = uni(xk);   // (wave-uniform: the compiler must see scalars for the asm's SGPR operands)
+    out = uni(out);
+    lim = uni(lim);
+    m = uni64(m);
+    // (the offset lives in m0 inside the loop: writelane may take m0 as its lane select beside an
+    // SGPR value, where a second SGPR would break the one-SGPR operand limit)
+    __asm__ __volatile__(
+        "s_mov_b32 %[tk], 0\n\t"
+        "s_mov_b32 m0, %[xk]\n"
+        "1:\n\t"
+        "s_cmp_lt_i32 m0, 64\n\t"
+        "s_cbranch_scc0 2f\n\t"
+        "s_cmp_lt_i32 %[out], %[lim]\n\t"
+        "s_cbranch_scc0 2f\n\t"
+        "v_readlane_b32 %[tk], %[tv], m0\n\t"
+        "s_and_b32 %[tmp], %[tk], 0x18000\n\t"
+        "s_cbranch_scc1 2f\n\t"
+        "v_writelane_b32 %[p], %[out], m0\n\t"
+        "s_bitset1_b64 %[m], m0\n\t"
+        "s_and_b32 %[tmp], %[tk], 63\n\t"
+        "s_add_i32 %[out], %[out], 1\n\t"
+        "s_add_i32 m0, m0, %[tmp]\n\t"
+        "s_branch 1b\n"
+        "2:\n\t"
+        "s_mov_b32 %[xk], m0"
+        : [tk] "=&s"(tk), [tmp] "=&s"(tmp), [xk] "+s"(xk), [out] "+s"(out), [m] "+s"(m), [p] "+v"(p)
+        : [tv] "v"(t[k]), [lim] "s"(lim)
+        : "scc", "m0");
+    pos[k] = p;
+    return tk;
+  }
+  __device__ uint32_t dist(int k, int l) const { return (uint32_t)__builtin_amdgcn_readlane((int)d[k], l); }
+  template <class F>
+  __device__ void each_literal(const uint64_t (&lm)[kRoundK], int lane, F &&f) const {
+#pragma unroll
+    for (int k = 0; k < kRoundK; ++k)
+      if ((lm[k] >> lane) & 1) f(64 * k + lane, pos[k], (uint8_t)(t[k] >> 24));
+  }
+};
+#endif
+
+// Rounds from bit P until a token needs the scalar loop (returned true) or the round limits end
+// them (false: another round). Advances P and w; flushes completed output chunks.
+template <int NL>
+INF_INL bool inflate_round(InfShared &S, RoundToks<NL> &R, uint32_t &P, int &w, int &flushed, uint32_t nbits,
+                          int cap, uint8_t *dst, int lane, uint64_t *prof) {
+  constexpr int M = kOutRing - 1;
+  uint64_t t0 = INF_T();
+  R.fill(S, P, nbits, lane);
+  INF_ACC(0, t0);
+#if defined(INF_PROF) && defined(__HIP_DEVICE_COMPILE__)
+  prof[4] += 1;
+#endif
+  t0 = INF_T();
+  uint64_t lm[kRoundK];
+  int nm = 0, out = 0, x = 0, maxd = 0;
+  bool need_scalar = false, stop = false;
+  // output this round may produce: kRoundOut (+ one match), never past the block's ISIZE
+  const int room = cap - w, lim = room < kRoundOut ? room : kRoundOut;
+#pragma unroll
+  for (int k = 0; k < kRoundK; ++k) {
+    lm[k] = 0;
+    if (stop) continue;
+    int xk = x - 64 * k;
+    uint64_t m = 0;
+    for (;;) {
+      const uint32_t t = R.chain(k, xk, out, lim, m);
+      if (!(t & (kTokStop | kTokMatch))) break;   // offset 64 or the output limit
+      const int ol = (int)((t >> 6) & 511);
+      const int dv = (int)R.dist(k, xk);
+      // a token for the scalar loop (a code the tables cannot finish, end of block, an invalid
+      // code, bits past the payload, a bad distance, output past ISIZE), or a full record list
+      if ((t & kTokStop) || dv > w + out || out + ol > room || nm == kRoundMaxM) {
+        need_scalar = (t & kTokStop) || dv > w + out || out + ol > room;
+        stop = true;
+        break;
+      }
+      if (lane == 0) S.mrec[nm] = make_int4(xk + 64 * k, out, ol, dv);
+      ++nm;
+      maxd = dv > maxd ? dv : maxd;
+      out += ol;
+      xk += (int)(t & 63);
+    }
+    lm[k] = m;
+    x = xk + 64 * k;
+    if (out >= lim) stop = true;
+  }
+  INF_WAVE_ORDER();   // the match records are read by every lane
+  INF_ACC(1, t0);
+  t0 = INF_T();
+#if defined(INF_STATS) && !defined(__HIP_DEVICE_COMPILE__)
+  inf_stats[0]++; inf_stats[1] += out; inf_stats[2] += nm; inf_stats[3] += need_scalar; inf_stats[4] += x;
+#endif
+  if (nm == 0 || maxd + out <= kOutRing) {
+    // no match reads a ring slot a later literal of the round overwrites: literals first
+    R.each_literal(lm, lane, [&](int, int pos, uint8_t v) { S.out[(w + pos) & M] = v; });
+    for (int j = 0; j < nm; ++j) {
+      const int4 mr = S.mrec[j];
+      copy_match<NL>(S, w + mr.y, mr.z, mr.w, lane);
+    }
+  } else {   // stream order: the literals before each match, then the match
+    int xprev = -1;
+    for (int j = 0; j <= nm; ++j) {
+      const int4 mr = j < nm ? S.mrec[j] : make_int4(1 << 30, 0, 0, 0);
+      R.each_literal(lm, lane, [&](int xl, int pos, uint8_t v) {
+        if (xl > xprev && xl < mr.x) S.out[(w + pos) & M] = v;
+      });
+      if (j < nm) copy_match<NL>(S, w + mr.y, mr.z, mr.w, lane);
+      xprev = mr.x;
+    }
+  }
+  w += out;
+  P += (uint32_t)x;
+  if (w - flushed >= kFlush) {
+    const int to = w & ~(kFlush - 1);
+    flush_out<NL>(S.out, dst, flushed, to, lane);
+    flushed = to;
+  }
+  INF_ACC(2, t0);
+  return need_scalar || x == 0;
+}
+
 // Decode one block's payload (n bytes at g) into dst (cap = the block's ISIZE bytes, never more);
 // returns the bytes decoded or -status. Wave-uniform: all 64 lanes run it together.
-template <int NL>
+template <int NL, bool ROUNDS = true>
 INF_FN int inflate_wave(InfShared &S, const uint8_t *g, int n, uint8_t *dst, int cap, int lane) {
+  // the block's arguments are wave-uniform: say so (an out-of-line call passes them in vector
+  // registers, and every branch on them would run under exec masks)
+  n = uni(n);
+  cap = uni(cap);
+  g = reinterpret_cast<const uint8_t *>(uni64(reinterpret_cast<uint64_t>(g)));
+  dst = reinterpret_cast<uint8_t *>(uni64(reinterpret_cast<uint64_t>(dst)));
   Bits<NL> b{g, S.ring, n, 0, 0, lane, 0ull, 0};
   constexpr int M = kOutRing - 1;
   int w = 0, flushed = 0;
+  uint64_t prof[6] = {0, 0, 0, 0, 0, 0};
+  const uint64_t t_block = INF_T();
   for (;;) {
     if (!b.need(3)) return -kInfOverrun;
     const int final_ = (int)b.take(1);
@@ -353,9 +650,37 @@ INF_FN int inflate_wave(InfShared &S, const uint8_t *g, int n, uint8_t *dst, int
         b.uniform();
         w = uni(w);
         flushed = uni(flushed);
+        if (ROUNDS) {   // token rounds up to the next token the scalar code below must decode
+          uint32_t P = (uint32_t)(8 * b.pos - b.cnt);
+          for (;;) {
+            b.pos = (int)(P >> 3);
+            b.top_up();
+            RoundToks<NL> R;
+            const bool sc = inflate_round<NL>(S, R, P, w, flushed, 8u * (uint32_t)n, cap, dst, lane, prof);
+            P = (uint32_t)uni((int)P);
+            w = uni(w);
+            flushed = uni(flushed);
+            if (sc) break;
+          }
+          // the bit reader at P again
+          b.pos = (int)(P >> 3);
+          b.buf = 0;
+          b.cnt = 0;
+          b.top_up();
+          b.refill();
+          b.take((int)(P & 7));
+          b.uniform();
+        }
         if (b.cnt < 15) b.refill();
         int e = uni(lfast[b.buf & kFastMask]);
         int l = e >> 9;
+#if defined(INF_STATS) && !defined(__HIP_DEVICE_COMPILE__)
+        if (ROUNDS) {
+          if (l == 0) inf_stats[5]++;
+          else if ((e & 511) == 256) inf_stats[6]++;
+          else inf_stats[7]++;
+        }
+#endif
         if (l == 0 || l > b.cnt) {
           e = uni(huff_slow(S.lit, b.buf, b.cnt));
           if (e < 0) {
@@ -431,23 +756,7 @@ INF_FN int inflate_wave(InfShared &S, const uint8_t *g, int n, uint8_t *dst, int
             err = dist > w ? kInfBadDist : kInfSize;
             break;
           }
-          INF_WAVE_ORDER();   // lane 0's literals and the last copy are read by every lane
-          if (dist >= len) {
-            for (int j0 = 0; j0 < len; j0 += NL) {
-              const int j = j0 + lane;
-              if (j < len) S.out[(w + j) & M] = S.out[(w - dist + j) & M];
-            }
-          } else {           // overlapping: out[w + j] = out[w - dist + j mod dist]
-            // lane mod dist, lane < 64 (exact: (lane + 1/2) / dist is >= 1/(2 dist) from an integer)
-            const int q = (int)(((float)lane + 0.5f) / (float)dist);
-            int r = lane - q * dist;
-            const int step = NL % dist;
-            for (int j0 = 0; j0 < len; j0 += NL) {
-              if (j0 + lane < len) S.out[(w + j0 + lane) & M] = S.out[(w - dist + r) & M];
-              r += step;
-              if (r >= dist) r -= dist;
-            }
-          }
+          copy_match<NL>(S, w, len, dist, lane);
           w += len;
         }
         if (w - flushed >= kFlush) {   // (at most kFlush + 257 bytes are ever unflushed)
@@ -462,6 +771,11 @@ INF_FN int inflate_wave(InfShared &S, const uint8_t *g, int n, uint8_t *dst, int
     }
     if (final_) {
       flush_out<NL>(S.out, dst, flushed, w, lane);
+#if defined(INF_PROF) && defined(__HIP_DEVICE_COMPILE__)
+      prof[3] += INF_T() - t_block;
+      if (lane == 0)
+        for (int i = 0; i < 6; ++i) atomicAdd(&g_inf_prof[i], (unsigned long long)prof[i]);
+#endif
       return w;
     }
   }
@@ -469,6 +783,7 @@ INF_FN int inflate_wave(InfShared &S, const uint8_t *g, int n, uint8_t *dst, int
 
 // Block i: payload comp[in_off[i], + in_len[i]) -> out[out_off[i], + out_len[i]) (its ISIZE);
 // status[i] = 0 or the failure (a length other than ISIZE included).
+template <bool ROUNDS>
 __global__ void __launch_bounds__(kInfThreads) k_inflate(const uint8_t *__restrict__ comp, int64_t comp_len,
                                                          const int64_t *__restrict__ in_off,
                                                          const int32_t *__restrict__ in_len,
@@ -487,7 +802,7 @@ __global__ void __launch_bounds__(kInfThreads) k_inflate(const uint8_t *__restri
       if (t == 0) status[i] = kInfSize;
       continue;
     }
-    const int r = inflate_wave<kInfThreads>(S, comp + io, il, out + oo, ol, t);
+    const int r = inflate_wave<kInfThreads, ROUNDS>(S, comp + io, il, out + oo, ol, t);
     if (t == 0) status[i] = r < 0 ? -r : (r == ol ? kInfOk : kInfSize);
     __syncthreads();   // (S is reused by the next block)
   }
@@ -617,7 +932,9 @@ GANON_API int ganon_inflate(ganon_ctx *ctx, const uint8_t *comp, int64_t comp_le
     {
       ganon_detail::KernelScope ks(ctx, "k_inflate");
       const unsigned grid = (unsigned)std::min<int64_t>(b1 - b0, 1 << 16);
-      hipLaunchKernelGGL(k_inflate, dim3(grid), dim3(kInfThreads), 0, s, st->comp, comp_len, st->in_off + b0,
+      // (GANON_INFLATE_ROUNDS=0: the scalar symbol loop alone, A/B)
+      static const bool rounds = !(std::getenv("GANON_INFLATE_ROUNDS") && std::getenv("GANON_INFLATE_ROUNDS")[0] == '0');
+      hipLaunchKernelGGL(rounds ? k_inflate<true> : k_inflate<false>, dim3(grid), dim3(kInfThreads), 0, s, st->comp, comp_len, st->in_off + b0,
                          st->in_len + b0, st->out_off + b0, st->out_len + b0, b1 - b0, st->out, out_total,
                          st->status + b0);
     }
@@ -666,3 +983,13 @@ void ganon_inflate_free(ganon_inflate_state *st) {
     if (p) hipFree(p);
   delete st;
 }
+
+#if defined(INF_PROF)
+// (tuning build only) the summed round cycles since the last call: fill, chain, emit, block total,
+// rounds; then zeroed
+GANON_API int ganon_inflate_prof_read(unsigned long long *out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_inf_prof), sizeof(unsigned long long) * 6) != hipSuccess) return -1;
+  unsigned long long z[6] = {0, 0, 0, 0, 0, 0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_inf_prof), z, sizeof z) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -139,23 +139,26 @@ def main():
                             pass
             if dist is not None:
                 dist.barrier()
-            t1 = time.time()
+            t1, c1 = time.time(), os.times()
             tim = sr.anonymize_genome(windows, os.path.join(d, "tumor.bam"), os.path.join(d, "normal.bam"),
                                       os.path.join(d, "ref.fa"), anon, os.path.join(out, f"tumor_{mode}"),
                                       os.path.join(out, f"normal_{mode}"), True, threads, fasta=fasta,
                                       streaming=(mode == "stream"), dist=dist)
             tim["wall_s"] = time.time() - t1
+            c2 = os.times()   # this process's CPU time over the run (all its threads)
+            tim["cpu_s"] = (c2.user - c1.user) + (c2.system - c1.system)
             if dist is not None:   # every rank's exchange and waits, then the slowest rank's wall
                 per_rank = [None] * dist.get_world_size()
                 dist.all_gather_object(per_rank, {k: tim.get(k) for k in (
                     "wall_s", "exchange_sent_bytes", "exchange_recv_bytes", "wait_s", "writer_wait_s", "jobs",
-                    "decode_s", "mask_s", "format_s", "write_s", "redos_skipped", "critical_path")})
+                    "decode_s", "mask_s", "format_s", "write_s", "redos_skipped", "critical_path", "cpu_s")})
                 tim["per_rank"] = per_rank
                 import torch
                 w = torch.tensor([tim["wall_s"]], dtype=torch.float64)
                 dist.all_reduce(w, op=dist.ReduceOp.MAX)
                 rb = torch.tensor([tim["reads"], tim.get("bases", 0), tim.get("jobs", 0)], dtype=torch.int64)
                 dist.all_reduce(rb)
+                tim["cpu_s"] = sum(p["cpu_s"] for p in per_rank)
                 tim["wall_s"], tim["reads"], tim["bases"], tim["jobs"] = float(w[0]), int(rb[0]), int(rb[1]), int(rb[2])
             if prof is not None:
                 import pstats
@@ -180,6 +183,9 @@ def main():
                      "coordinator_busy_s": best.get("resolve_s"),
                      "redos": best.get("redos"), "redos_unchanged": best.get("redos_unchanged"),
                      "first_run_wall_s": round(runs[0]["wall_s"], 3),
+                     # host CPU seconds of all ranks over the run, and the cores that kept busy
+                     "cpu_s": round(best["cpu_s"], 2), "cores_busy": round(best["cpu_s"] / best["wall_s"], 2),
+                     "cpus_available": len(os.sched_getaffinity(0)),
                      "output_bytes": sum(os.path.getsize(os.path.join(out, f"{x}_{mode}{s}"))
                                          for x in ("tumor", "normal") for s in (".1.fastq", ".2.fastq"))}
         if rank == 0:

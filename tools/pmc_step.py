@@ -22,7 +22,8 @@ import sys
 STEP_KERNELS = {"k_prep_scan", "k_prep_cands", "k_prep_order_count", "k_prep_order_scatter", "k_prep_scan_long", "k_prep_reduce", "k_prep_nseg", "k_prep_scope_cost", "k_prep_groups", "k_prep_emit", "k_prep_emit_flat", "k_prep_emit_waves", "k_prep_long_groups",
                 "k_prep_long_mid", "k_prep_read_recs", "k_prep_linemap", "k_prep_pieces", "k_group", "k_finish", "k_tile_large",
                 "k_mask_large", "k_indel_mark", "k_indel_count", "k_indel_emit", "k_indel_segs", "k_indel_runs",
-                "k_indel_rcount", "k_indel_remit", "k_indel_icount", "k_indel_expand",
+                "k_indel_rcount", "k_indel_remit", "k_indel_icount", "k_indel_expand", "k_indel_mark_t",
+                "k_indel_rlist_t", "k_indel_icount_t", "k_indel_expand_t", "k_indel_tsort",
                 "k_indel_classify", "rocprim_sort", "rocprim_scan", "rocprim_other"}
 
 

@@ -545,7 +545,7 @@ def main() -> None:
                     help="round-2 step: run only, the plan made once at upload (not a fresh batch)")
     ap.add_argument("--pmc", default=None,
                     help="PMC step summary (tools/pmc_step.py) for the traffic field; default "
-                         "profiles/r04 (else r03)/pmc_step_<config>.json when present")
+                         "profiles/r05 (else r04, r03)/pmc_step_<config>.json when present")
     args = ap.parse_args()
     for k, v in CONFIGS[args.config]["defaults"].items():
         if getattr(args, k) is None:
@@ -816,9 +816,9 @@ def main() -> None:
     alg_total = sum(algorithmic_bytes(a) for a in prof_arrs) // len(prof_arrs)
     achieved = alg_total / (pass_ms * 1e-3) / 1e9
     traffic = dom_traffic = None
-    # the newest round's PMC summary of this config and size (tools/gpu_pmc_r04.sh)
+    # the newest round's PMC summary of this config and size (tools/gpu_pmc_r05.sh, r04, r03)
     pmc_paths = [args.pmc] if args.pmc else [os.path.join(REPO, "profiles", r, f"pmc_step_{args.config}.json")
-                                             for r in ("r04", "r03")]
+                                             for r in ("r05", "r04", "r03")]
     pmc_used = None
     for pmc_path in pmc_paths:
         if traffic is None and os.path.exists(pmc_path):

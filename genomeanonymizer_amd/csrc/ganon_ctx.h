@@ -6,6 +6,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include <cstdarg>
 #include <cstdio>
 #include <map>
@@ -147,6 +149,14 @@ struct KernelScope {
 inline int check_launch(ganon_ctx *ctx, const char *what) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(ctx, GANON_E_DEVICE, "launch of %s failed: %s", what, hipGetErrorString(e));
+  // (GANON_SYNC_CHECK=1, debugging only: wait for every checked launch, so that a kernel's fault
+  // is reported under its own name)
+  static const bool sync_check = [] {
+    const char *v = std::getenv("GANON_SYNC_CHECK");
+    return v && v[0] == '1';
+  }();
+  if (sync_check && (e = hipDeviceSynchronize()) != hipSuccess)
+    return fail(ctx, GANON_E_DEVICE, "%s failed: %s", what, hipGetErrorString(e));
   return GANON_OK;
 }
 

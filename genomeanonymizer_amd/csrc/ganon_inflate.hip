@@ -6,16 +6,14 @@
 // payloads here instead of to zlib on its threads (ganon_bam_reader_set_inflater).
 //
 // One 64-lane workgroup per block, and the wave decodes it as ONE decoder: Huffman decoding is a
-// serial bit stream, so every lane runs the same symbol loop on the same wave-uniform state (kept
-// in scalar registers, scalar branches: readfirstlane at the loop head tells the compiler so), and
-// the lanes split only the byte work. Per code: one LDS read of a 10-bit lookup table (a canonical
-// bit walk for longer codes); per ~57 bits, one LDS read of three payload dwords. The payload comes
-// through a 2 KiB LDS ring filled 1 KiB at a time by the lanes; the output goes through a 32 KiB
-// LDS ring (DEFLATE's whole back-reference window): a match of length L is copied by all lanes at
-// once (periodic source index w - dist + (j mod dist): even an overlapping match has no intra-copy
-// dependence), and every completed 4 KiB of the ring is written to the block's output by the lanes
-// (coalesced dword stores). ~39 KiB of LDS: four blocks decode per CU, 1024 on the chip — the
-// decoders are latency-bound, so the count of them in flight is the throughput. Stored, fixed-
+// serial bit stream. Token rounds (round 5, below): every lane decodes the token that would start
+// at one of the next 256 bit offsets, a scalar chain through them (readlane) finds the true token
+// boundaries, the literals are written by their lanes at once and the matches copied in stream
+// order by all lanes (periodic source index w - dist + (j mod dist): even an overlapping match has
+// no intra-copy dependence); tokens the tables cannot finish go through the scalar symbol loop.
+// The payload comes through a 2 KiB LDS ring; the output through an 8 KiB LDS ring written out to
+// the block's output every completed 1 KiB, and matches further back than 4 KiB read the written
+// output from global memory. ~16 KiB of LDS per decoder: ten blocks decode per CU. Stored, fixed-
 // and dynamic-Huffman blocks. Every read and write is range-checked (output against the block's
 // ISIZE): a malformed stream sets the block's status and stops it, never faults.
 // Written from RFC 1951 and the BGZF section of the SAM specification.
@@ -37,8 +35,14 @@ constexpr int kInfThreads = 64;
 constexpr int kWin = 65536;          // BGZF: at most 64 KiB of output per block
 constexpr int kRing = 2048;          // payload ring (LDS), refilled kRing/2 bytes at a time
 constexpr int kRingHalf = kRing / 2;
-constexpr int kOutRing = 32768;      // output ring: DEFLATE's 32 KiB back-reference window
-constexpr int kFlush = 4096;         // output written out per completed chunk of the ring
+// Output: an 8 KiB LDS ring of the latest output, written out to the block's output every
+// completed kFlush bytes; a match reaching further back than kNear reads the block's output in
+// global memory (written out and fenced by then). Round 5: the ring held DEFLATE's whole 32 KiB
+// window (40 KiB of LDS per decoder, 4 decoders per CU, one wave per SIMD: every dependent
+// instruction of the serial decoder waited out its latency alone); 16 KiB per decoder fits 10.
+constexpr int kOutRing = 8192;
+constexpr int kFlush = 1024;
+constexpr int kNear = 4096;
 #ifndef INF_FAST_BITS
 #define INF_FAST_BITS 10
 #endif
@@ -272,16 +276,26 @@ INF_INL void flush_out(const uint8_t *ring, uint8_t *dst, int from, int to, int 
     const int k = k0 + lane;
     if (k < to) dst[k] = ring[k & (kOutRing - 1)];
   }
+  // far matches read these bytes back from global memory (other lanes of this wave): the stores
+  // complete before any later load
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+#endif
 }
 
 
 // Copy of a match: out[w + j] = out[w - dist + j], j < len, by all lanes at once (a periodic source
 // index for an overlapping match: out[w + j] = out[w - dist + (j mod dist)]).
 template <int NL>
-INF_INL void copy_match(InfShared &S, int w, int len, int dist, int lane) {
+INF_INL void copy_match(InfShared &S, const uint8_t *dst, int w, int len, int dist, int lane) {
   constexpr int M = kOutRing - 1;
   INF_WAVE_ORDER();   // the literals and the last copy are read by every lane
-  if (dist >= len) {
+  if (dist > kNear) {   // (far: its source is written out; dist > kNear >= len, no overlap)
+    for (int j0 = 0; j0 < len; j0 += NL) {
+      const int j = j0 + lane;
+      if (j < len) S.out[(w + j) & M] = dst[w - dist + j];
+    }
+  } else if (dist >= len) {
     for (int j0 = 0; j0 < len; j0 += NL) {
       const int j = j0 + lane;
       if (j < len) S.out[(w + j) & M] = S.out[(w - dist + j) & M];
@@ -506,7 +520,7 @@ INF_INL bool inflate_round(InfShared &S, RoundToks<NL> &R, uint32_t &P, int &w, 
       }
       if (lane == 0) S.mrec[nm] = make_int4(xk + 64 * k, out, ol, dv);
       ++nm;
-      maxd = dv > maxd ? dv : maxd;
+      if (dv <= kNear && dv > maxd) maxd = dv;   // (far matches read global memory)
       out += ol;
       xk += (int)(t & 63);
     }
@@ -525,7 +539,7 @@ INF_INL bool inflate_round(InfShared &S, RoundToks<NL> &R, uint32_t &P, int &w, 
     R.each_literal(lm, lane, [&](int, int pos, uint8_t v) { S.out[(w + pos) & M] = v; });
     for (int j = 0; j < nm; ++j) {
       const int4 mr = S.mrec[j];
-      copy_match<NL>(S, w + mr.y, mr.z, mr.w, lane);
+      copy_match<NL>(S, dst, w + mr.y, mr.z, mr.w, lane);
     }
   } else {   // stream order: the literals before each match, then the match
     int xprev = -1;
@@ -534,7 +548,7 @@ INF_INL bool inflate_round(InfShared &S, RoundToks<NL> &R, uint32_t &P, int &w, 
       R.each_literal(lm, lane, [&](int xl, int pos, uint8_t v) {
         if (xl > xprev && xl < mr.x) S.out[(w + pos) & M] = v;
       });
-      if (j < nm) copy_match<NL>(S, w + mr.y, mr.z, mr.w, lane);
+      if (j < nm) copy_match<NL>(S, dst, w + mr.y, mr.z, mr.w, lane);
       xprev = mr.x;
     }
   }
@@ -756,7 +770,7 @@ INF_FN int inflate_wave(InfShared &S, const uint8_t *g, int n, uint8_t *dst, int
             err = dist > w ? kInfBadDist : kInfSize;
             break;
           }
-          copy_match<NL>(S, w, len, dist, lane);
+          copy_match<NL>(S, dst, w, len, dist, lane);
           w += len;
         }
         if (w - flushed >= kFlush) {   // (at most kFlush + 257 bytes are ever unflushed)
@@ -883,10 +897,10 @@ GANON_API int ganon_inflate(ganon_ctx *ctx, const uint8_t *comp, int64_t comp_le
     }
     ctx->recs.clear();
   }
-  // Chunks of kChunk blocks (about one wave of decoders on the chip) when the blocks lie in file
+  // Chunks of kChunk blocks (about one round of decoders on the chip: 10 per CU) when the blocks lie in file
   // order: the payload of chunk c + 1 goes up and the output of chunk c - 1 comes down on a copy
   // stream while chunk c decodes; otherwise one chunk.
-  constexpr int64_t kChunk = 1024;
+  constexpr int64_t kChunk = 2560;
   bool ordered = true;
   for (size_t i = 1; i < nb && ordered; ++i)
     ordered = in_off[i] >= in_off[i - 1] + in_len[i - 1] && out_off[i] >= out_off[i - 1] + out_len[i - 1];

@@ -248,9 +248,9 @@ class GpuInflater:
     """BGZF inflate on the GPU (``ganon_inflate``, include/ganon.h): a device
     context of its own (own stream, own grow-only buffers), used by one thread at a time — the
     BamReader decode thread hands it its block windows (``BamReader(..., inflater=)``). Windows
-    of fewer than ``min_blocks`` blocks stay on the reader's zlib threads: the decoder is one wave
-    per block and latency-bound (~12 ms per 64 KiB block, 1024 blocks in flight), so a call pays
-    off only when it carries hundreds of blocks."""
+    of fewer than ``min_blocks`` blocks stay on the reader's host threads: the decoder is one wave
+    per block (token rounds, ten blocks per CU, 2,560 in flight; a 64 KiB block takes several ms on
+    its wave), so a call pays off only when it carries hundreds of blocks."""
 
     def __init__(self, device: int = 0, min_blocks: int = 512):
         lib = hip_lib()

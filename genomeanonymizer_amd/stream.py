@@ -966,12 +966,15 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
             open(p, "wb").close()
     comm.barrier()
     fds = [os.open(p, os.O_WRONLY) for p in paths]
-    # GANON_GPU_INFLATE=1: the decode thread's BGZF windows inflate on this rank's GPU (one context
-    # of its own, shared by both readers: they are only used by that thread, one at a time)
-    # (GANON_GPU_INFLATE_MIN: the fewest blocks a window needs to go to the GPU, default 512 — one
-    # block takes ~12 ms on its wave, so only large windows pay off: DESIGN §4e)
+    # The decode thread's BGZF windows inflate on this rank's GPU (one context of its own, shared by
+    # both readers: they are only used by that thread, one at a time) whenever the masking engine is
+    # the GPU's (round 5: the token-round kernel made it the faster decoder at chromosome scale, 8.0e6
+    # vs 5.9e6 reads/s on the 30x line); GANON_GPU_INFLATE=0 / 1 forces it off / on.
+    # (GANON_GPU_INFLATE_MIN: the fewest blocks a window needs to go to the GPU, default 512 — a
+    # block takes milliseconds on its wave, so only large windows pay off)
     inflater = None
-    if os.environ.get("GANON_GPU_INFLATE", "0") == "1":
+    gi = os.environ.get("GANON_GPU_INFLATE", "auto")
+    if gi == "1" or (gi == "auto" and (anonymizer._engine is None or isinstance(anonymizer._engine, native.HipMasker))):
         inflater = native.GpuInflater(anonymizer.device, int(os.environ.get("GANON_GPU_INFLATE_MIN", "512")))
     readers = (BamReader(tumor_bam, threads, window_bytes, inflater),
                BamReader(normal_bam, threads, window_bytes, inflater))
@@ -1255,6 +1258,8 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
             r.close()
         for r in redo_readers:
             r.close()
+        if inflater is not None:   # (after its readers: the device context goes with it)
+            inflater.close()
         if coord is not None:
             coord.close()
     timing["exchange_sent_bytes"] = link.sent_bytes

@@ -260,9 +260,9 @@ class BamReader:
         self.path = path
         if window:
             lib.ganon_bam_reader_set_window(h, int(window))
-        self.inflater = inflater   # (kept alive: the reader calls into its context)
-        if inflater is not None:   # a native.GpuInflater: block windows inflate on the GPU
-            lib.ganon_bam_reader_set_inflater(h, inflater.fn, inflater.handle, inflater.min_blocks)
+        self.inflater = None
+        if inflater is not None:
+            self.set_inflater(inflater)
         v = native.BamView()
         lib.ganon_bam_reader_header(h, C.byref(v))
         off = _arr(v.ref_name_off, v.n_ref, np.int64)
@@ -270,6 +270,12 @@ class BamReader:
         self.ref_names: List[str] = [C.string_at(raw + int(o)).decode() for o in off]
         self.ref_lens = _arr(v.ref_len, v.n_ref, np.int64)
         self.has_index = bool(lib.ganon_bam_reader_has_index(h))
+
+    def set_inflater(self, inflater) -> None:
+        """Block windows inflate on the GPU from now on (a native.GpuInflater, kept alive here: the
+        reader calls into its context)."""
+        native.host_lib().ganon_bam_reader_set_inflater(self._h, inflater.fn, inflater.handle, inflater.min_blocks)
+        self.inflater = inflater
 
     def tid_of(self, contig: str) -> int:
         try:

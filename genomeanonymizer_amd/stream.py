@@ -101,8 +101,10 @@ class JobSpec:
 
 def auto_job_bp(genome_len: int, world: int) -> int:
     """Job size when GANON_JOB_BP is unset: 4 Mb, or less so that each of the ``world`` ranks gets
-    about GANON_JOBS_PER_RANK (6) jobs, but at least 256 kb."""
-    per_rank = max(1, int(os.environ.get("GANON_JOBS_PER_RANK", "6")))
+    about GANON_JOBS_PER_RANK (3) jobs, but at least 256 kb. (The 30x chromosome-scale line, 8
+    ranks: 3 jobs per rank 6.67e6 reads/s, 6 6.42e6, 12 6.55e6 — more jobs add plan waits for the
+    decode frontier of the jobs before them; the 24-contig line keeps one job per 2 Mb contig.)"""
+    per_rank = max(1, int(os.environ.get("GANON_JOBS_PER_RANK", "3")))
     return int(min(4_000_000, max(256_000, genome_len // max(1, per_rank * world))))
 
 
@@ -966,26 +968,31 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
             open(p, "wb").close()
     comm.barrier()
     fds = [os.open(p, os.O_WRONLY) for p in paths]
-    # The decode thread's BGZF windows inflate on this rank's GPU (one context of its own, shared by
-    # both readers: they are only used by that thread, one at a time) whenever the masking engine is
-    # the GPU's (round 5: the token-round kernel made it the faster decoder at chromosome scale, 8.0e6
-    # vs 5.9e6 reads/s on the 30x line); GANON_GPU_INFLATE=0 / 1 forces it off / on.
-    # (GANON_GPU_INFLATE_MIN: the fewest blocks a window needs to go to the GPU, default 512 — a
-    # block takes milliseconds on its wave, so only large windows pay off)
-    inflater = None
-    gi = os.environ.get("GANON_GPU_INFLATE", "auto")
-    if gi == "1" or (gi == "auto" and (anonymizer._engine is None or isinstance(anonymizer._engine, native.HipMasker))):
-        inflater = native.GpuInflater(anonymizer.device, int(os.environ.get("GANON_GPU_INFLATE_MIN", "512")))
-    readers = (BamReader(tumor_bam, threads, window_bytes, inflater),
-               BamReader(normal_bam, threads, window_bytes, inflater))
+    readers = (BamReader(tumor_bam, threads, window_bytes), BamReader(normal_bam, threads, window_bytes))
     # jobs: contigs, or runs of sections of about GANON_JOB_BP bases (default 4 Mb; 0 = whole
     # contigs) when both BAMs are indexed
-    # (unset: 4 Mb, or smaller so that every rank gets about GANON_JOBS_PER_RANK jobs (default 6, at
+    # (unset: 4 Mb, or smaller so that every rank gets about GANON_JOBS_PER_RANK jobs (default 3, at
     # least 256 kb each): 2 x 20 Mb over 8 ranks made 10 jobs of 4 Mb, two ranks ran two each and
     # the rest idled half the wall — round 5's 30x chromosome-scale line)
     job_bp = int(os.environ.get("GANON_JOB_BP", "0") or 0) if "GANON_JOB_BP" in os.environ else \
         auto_job_bp(sum(int(L) for L in fasta.lengths), world)
     jobs = plan_jobs(fasta, windows, job_bp, all(r.has_index for r in readers))
+    # The decode thread's BGZF windows inflate on this rank's GPU (one context of its own, shared by
+    # both readers: they are only used by that thread, one at a time) when the masking engine is the
+    # GPU's and a job's reads come in windows of at least GANON_GPU_INFLATE_MIN blocks (default 512,
+    # ~18 MB compressed: a block takes milliseconds on its wave, so only large windows pay off, and
+    # the context costs its setup) — round 5: the token-round kernel made it the faster decoder at
+    # chromosome scale (30x line: 6.28e6 -> 6.93e6 and 5.87e6 -> 8.04e6 reads/s on two boxes, 22 %
+    # less host CPU). GANON_GPU_INFLATE=0 / 1 forces it off / on.
+    inflater = None
+    gi = os.environ.get("GANON_GPU_INFLATE", "auto")
+    min_blocks = int(os.environ.get("GANON_GPU_INFLATE_MIN", "512"))
+    gpu_engine = anonymizer._engine is None or isinstance(anonymizer._engine, native.HipMasker)
+    big_jobs = max(os.path.getsize(p) for p in (tumor_bam, normal_bam)) / max(1, len(jobs)) >= min_blocks * 36_000
+    if gi == "1" or (gi == "auto" and gpu_engine and big_jobs):
+        inflater = native.GpuInflater(anonymizer.device, min_blocks)
+        for r in readers:
+            r.set_inflater(inflater)
     owner = assign_contigs([j.length for j in jobs], world)
     mine = [j for j in range(len(jobs)) if owner[j] == rank]
     link = Link(dist)

@@ -535,8 +535,8 @@ def main() -> None:
     ap.add_argument("--e2e-pairs", type=int, default=23_000, help="pairs per contig and sample")
     ap.add_argument("--e2e-cpu-contigs", type=int, default=4)
     ap.add_argument("--e2e-runs", type=int, default=3,
-                    help="timed end-to-end runs after a warm run (the best is the line; all are in wall_s_runs: the
-                    709 MB of output writes make single runs spread 0.32-0.58 s on one box)")
+                    help="timed end-to-end runs after a warm run (the best is the line; all are in wall_s_runs: "
+                         "the 709 MB of output writes make single runs spread 0.32-0.58 s on one box)")
     ap.add_argument("--e2e-chrom-pairs", type=int, default=2_000_000,
                     help="pairs per contig and sample of the chromosome-scale end-to-end line (2 contigs of "
                          "--e2e-chrom-len; default 30x per sample, configs[2] density; 0: skip)")

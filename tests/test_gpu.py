@@ -352,6 +352,35 @@ def test_cli_concurrent_pairs(tmp_path, hip_built):
             open(os.path.join(GOLDEN, "edge", "normal.statistics.txt")).read()
 
 
+def test_cli_concurrent_pairs_error_reaches_caller(tmp_path, hip_built):
+    """A pair that fails inside the process pool (GANON_PAIR_WORKERS=2: spawned children, a HIP context
+    each) fails the run: its error comes back through the pool to the CLI, which exits non-zero and
+    names it."""
+    import os
+    import shutil
+    import subprocess
+    import sys
+    from helpers import REPO
+    from genomeanonymizer_amd.synth.generate import generate, scenario
+    d = str(tmp_path / "pairs")
+    generate(scenario("edge"), os.path.join(d, "a"))
+    os.makedirs(os.path.join(d, "b"))
+    for f in ("normal.bam", "variants.vcf"):
+        shutil.copy(os.path.join(d, "a", f), os.path.join(d, "b", f))
+    with open(os.path.join(d, "b", "tumor.bam"), "wb") as fh:   # not a BGZF file
+        fh.write(b"this is not a BAM file" * 64)
+    with open(os.path.join(d, "samples.tsv"), "w") as fh:
+        fh.write("#tumor\tnormal\tvcf\n")
+        for sub in ("a", "b"):
+            fh.write(f"{sub}/tumor.bam\t{sub}/normal.bam\t{sub}/variants.vcf\n")
+    env = dict(os.environ, PYTHONPATH=REPO, GANON_PAIR_WORKERS="2")
+    r = subprocess.run([sys.executable, "-m", "genomeanonymizer_amd.genome_anonymizer", "-d", d, "-s", "samples.tsv",
+                        "-r", os.path.join(d, "a", "ref.fa"), "-c", "2"], env=env, capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode != 0
+    assert "b/tumor.bam" in r.stderr or "BGZF" in r.stderr, r.stderr[-2000:]
+
+
 def test_hip_config2_matches_oracle(masker, oracle):
     """BASELINE configs[1] layout at 2 M reads: every byte and count equal to the oracle."""
     from genomeanonymizer_amd.synth.batch import config2_batch

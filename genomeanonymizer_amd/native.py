@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import time
 from typing import Optional, Tuple
 
 import numpy as np
@@ -466,16 +467,24 @@ class HipMasker:
         sel = recs["seq_sel"]
         r["seq_nib_off"] = recs["seq_nib_off"] + np.where(sel == 2, 2 * int(recs["seq_base1"]), 0).astype(np.int64)
         r["seq_sel"] = np.minimum(sel, 1).astype(np.uint8)
+        t0 = time.perf_counter()
         c, keep = _c_fastq_records(r, seq_batch=db)
         h = _p()
         self._check(self._lib.ganon_fastq_upload(self._h, C.byref(c), C.byref(h)), "ganon_fastq_upload")
         del keep
         try:
+            t1 = time.perf_counter()
             self._check(self._lib.ganon_fastq_run(self._h, h), "ganon_fastq_run")
             n_bytes = int(self._lib.ganon_fastq_bytes(h))
             out = _new_bytes(None, n_bytes)      # filled in place
+            t2 = time.perf_counter()
             w = self._lib.ganon_fastq_download(self._h, h, out, n_bytes)
             w = _fastq_result(w, lambda: self._lib.ganon_last_error(self._h).decode(errors="replace"))
+            t3 = time.perf_counter()
+            FQ_TIMES["upload_s"] += t1 - t0   # (where a job's formatting goes: the stream's timing)
+            FQ_TIMES["run_s"] += t2 - t1
+            FQ_TIMES["download_s"] += t3 - t2
+            FQ_TIMES["bytes"] += n_bytes
         finally:
             self._lib.ganon_fastq_free(self._h, h)
         return out if w == n_bytes else out[:w]
@@ -499,6 +508,9 @@ class FastqBadRecord(GanonError):
 
 
 FASTQ_FAILED = -(1 << 63) + 1   # include/ganon.h GANON_FASTQ_FAILED
+
+# per process: the device formatter's record upload, run (kernels + sync) and download of the bytes
+FQ_TIMES = {"upload_s": 0.0, "run_s": 0.0, "download_s": 0.0, "bytes": 0}
 
 
 def _fastq_result(w: int, err) -> int:

@@ -151,7 +151,7 @@ def main():
                 per_rank = [None] * dist.get_world_size()
                 dist.all_gather_object(per_rank, {k: tim.get(k) for k in (
                     "wall_s", "exchange_sent_bytes", "exchange_recv_bytes", "wait_s", "writer_wait_s", "jobs",
-                    "decode_s", "mask_s", "format_s", "write_s", "redos_skipped", "critical_path", "cpu_s")})
+                    "decode_s", "mask_s", "format_s", "write_s", "redos_skipped", "critical_path", "cpu_s", "fastq_device")})
                 tim["per_rank"] = per_rank
                 import torch
                 w = torch.tensor([tim["wall_s"]], dtype=torch.float64)
@@ -179,6 +179,7 @@ def main():
                      "peak_rss_mb": resource.getrusage(resource.RUSAGE_SELF).ru_maxrss // 1024,
                      "workers": workers,
                      "critical_path_s_rank0": best.get("critical_path"),
+                     "fastq_device_rank0": best.get("fastq_device"),
                      "per_rank": best.get("per_rank"),
                      "coordinator_busy_s": best.get("resolve_s"),
                      "redos": best.get("redos"), "redos_unchanged": best.get("redos_unchanged"),

@@ -61,6 +61,37 @@ def assign_samples(n_samples: int, world: int) -> List[int]:
     return [i % max(1, world) for i in range(n_samples)]
 
 
+# Side gloo groups of the streamed path (Link, SecondaryExchange), kept for the next run of this
+# process once a run has ended cleanly on every rank: creating one took 0.13-0.33 s per rank and run
+# on the 8-rank chromosome-scale line (`groups_s`), ~10 % of its wall. Keyed by purpose and the
+# default process group (a group of a destroyed world is never reused); a run that failed anywhere
+# returns nothing, so the next run makes fresh groups and no message of the failed one is left to
+# meet it. Every rank takes and returns the same groups in the same order (the error state it
+# returns on is the run's final all-gathered one), so new_group stays collective.
+_SIDE_GROUPS: dict = {}
+
+
+def _world_key(dist):
+    try:
+        pg = dist.distributed_c10d._get_default_group()
+    except Exception:   # pragma: no cover
+        pg = None
+    return id(pg), pg
+
+
+def take_side_group(dist, purpose: str):
+    k, _ = _world_key(dist)
+    hit = _SIDE_GROUPS.pop((purpose, k), None)
+    return hit[0] if hit is not None else dist.new_group(backend="gloo")
+
+
+def return_side_group(dist, purpose: str, group, clean: bool) -> None:
+    if group is None or not clean:
+        return
+    k, pg = _world_key(dist)
+    _SIDE_GROUPS[(purpose, k)] = (group, pg)   # (pg kept: its id cannot be reused while cached)
+
+
 class Link:
     """Messages between each rank's worker (its main thread) and the coordinator (a thread of rank
     0): exports go to rank 0, resolutions come back to the job's owner, in job order per rank (FIFO
@@ -74,7 +105,7 @@ class Link:
         self.dist = dist
         self.rank = dist.get_rank() if dist is not None else 0
         self.world = dist.get_world_size() if dist is not None else 1
-        self.group = dist.new_group(backend="gloo") if dist is not None and self.world > 1 else None
+        self.group = take_side_group(dist, "link") if dist is not None and self.world > 1 else None
         self.q_exp: "queue.Queue" = queue.Queue()
         self.q_res: "queue.Queue" = queue.Queue()
         self._inflight: list = []
@@ -151,7 +182,7 @@ class SecondaryExchange:
     def __init__(self, dist, owner: Sequence[int]):
         self.dist = dist
         self.rank, self.world = dist.get_rank(), dist.get_world_size()
-        self.group = dist.new_group(backend="gloo")
+        self.group = take_side_group(dist, "secondary")
         self.owner = list(owner)
         self.n = len(owner)
         self.mine = [j for j in range(self.n) if owner[j] == self.rank]

@@ -955,6 +955,7 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
     ranks of the initialised torch.distributed world, each on its own contigs: distributed.py).
     Output files, statistics and errors are the reference's (SR:625-760)."""
     from .distributed import Link, assign_contigs
+    t_start = time.time()
     comm = _Comm(dist)
     rank, world = comm.rank, comm.world
     paths = [f"{tumor_out}.1.fastq", f"{tumor_out}.2.fastq", f"{normal_out}.1.fastq", f"{normal_out}.2.fastq"]
@@ -995,7 +996,9 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
             r.set_inflater(inflater)
     owner = assign_contigs([j.length for j in jobs], world)
     mine = [j for j in range(len(jobs)) if owner[j] == rank]
+    t_g = time.time()
     link = Link(dist)
+    timing_groups = time.time() - t_g
     coord = _Coordinator(fds, (f"{tumor_out}.single_end.fastq", f"{normal_out}.single_end.fastq"), block_size) \
         if rank == 0 else None
     coord_exc: List[Optional[BaseException]] = [None]
@@ -1006,7 +1009,9 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
     xchg = None
     if world > 1 and os.environ.get("GANON_SEC_EXCHANGE", "1") != "0":
         from .distributed import SecondaryExchange
+        t_g = time.time()
         xchg = SecondaryExchange(dist, owner)
+        timing_groups += time.time() - t_g
         secondaries.remote = xchg
 
     stash: Dict[int, list] = {}      # exports an owner sent after the job it is planning again
@@ -1172,6 +1177,8 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
             timing["writer_wait_s"] += time.time() - t0
 
     t_loop0 = time.time()
+    timing["setup_s"] = t_loop0 - t_start   # (readers, job plan, exchange groups, inflater, coordinator)
+    timing["groups_s"] = timing_groups
     fq0 = dict(native.FQ_TIMES)
     try:
         try:
@@ -1241,6 +1248,12 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
             raise RuntimeError(f"another rank failed: {errs[0]}")
         if failure is None:
             link.drain()
+        # every rank ended cleanly: the side groups serve this process's next run (distributed.py)
+        if dist is not None and world > 1:
+            from .distributed import return_side_group
+            return_side_group(dist, "link", link.group, True)
+            if xchg is not None:
+                return_side_group(dist, "secondary", xchg.group, True)
         all_stats = [g["stats"] for g in gathered]
         if rank == 0 and record_statistics:
             merged: Dict[str, List[int]] = {OUTSIDE_WINDOWS: [0] * 8}

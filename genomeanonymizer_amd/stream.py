@@ -1225,6 +1225,7 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
                     p.cancel()
                 writer.shutdown(wait=True)
                 writer = None
+        t_tail = time.time()   # (the tail's parts: tail_s below)
         if coord_thread is not None:
             coord_thread.join()
             timing["resolve_s"] = coord.resolve_s
@@ -1234,13 +1235,19 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
             timing["marked_written"] = coord.marked
             if coord_exc[0] is not None:   # rank 0 reports the coordinator's own error
                 failure = coord_exc[0]
+        tails = {"coordinator_join": time.time() - t_tail}
         err = repr(failure) if failure is not None else None
+        t_tail = time.time()
         if xchg is not None:
             if failure is not None:
                 xchg.fail(err)
             xchg.close(None if failure is None else 60.0)
             timing["permit_wait_s"] = round(xchg.wait_s, 3)
+        tails["exchange_close"] = time.time() - t_tail
+        t_tail = time.time()
         gathered = comm.allgather({"stats": stats_rows, "err": err})
+        tails["gather"] = time.time() - t_tail
+        t_tail = time.time()
         errs = [g["err"] for g in gathered if g["err"] is not None]
         if errs:
             if failure is not None:
@@ -1264,6 +1271,8 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
                     else:
                         merged[key] = list(counts)
             write_statistics(normal_stats_path or f"{normal_bam}.statistics.txt", merged)
+        tails["drain_stats"] = time.time() - t_tail
+        t_tail = time.time()
     finally:
         if writer is not None:
             writer.shutdown(wait=True)
@@ -1283,12 +1292,18 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
             inflater.close()
         if coord is not None:
             coord.close()
+    if "tails" in locals():
+        tails["close"] = time.time() - t_tail
+        t_tail = time.time()
     timing["exchange_sent_bytes"] = link.sent_bytes
     timing["exchange_recv_bytes"] = link.recv_bytes
     totals = comm.allreduce_totals(totals)
     timing["totals"] = {k: int(v) for k, v in zip(("masked_snv_calls", "masked_bases", "reads_in", "reads_written",
                                                    "scopes", "rare_scopes", "large_tiles", "reserved"), totals)}
     comm.barrier()
+    if "tails" in locals():
+        tails["totals_barrier"] = time.time() - t_tail
+        timing["tail_parts"] = {k: round(v, 3) for k, v in tails.items()}
     # this rank's main thread, stage by stage: what its wall is made of (the thread-time sums above
     # overlap; these do not): waiting for the job's prefetched decode + plan, its mask (batch build
     # included) and format on the device, the export, waiting for a writer slot, the last jobs'

@@ -99,6 +99,14 @@ class JobSpec:
         return self.contig if self.region is None else f"{self.contig}:{self.region[0]}-{self.region[1]}"
 
 
+_INFLATERS: Dict[Tuple[int, int], "native.GpuInflater"] = {}   # (device, min blocks) -> this process's inflater
+
+
+def _close_all(objs) -> None:
+    for o in objs:
+        o.close()
+
+
 def auto_job_bp(genome_len: int, world: int) -> int:
     """Job size when GANON_JOB_BP is unset: 4 Mb, or less so that each of the ``world`` ranks gets
     about GANON_JOBS_PER_RANK (3) jobs, but at least 256 kb. (The 30x chromosome-scale line, 8
@@ -991,7 +999,11 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
     gpu_engine = anonymizer._engine is None or isinstance(anonymizer._engine, native.HipMasker)
     big_jobs = max(os.path.getsize(p) for p in (tumor_bam, normal_bam)) / max(1, len(jobs)) >= min_blocks * 36_000
     if gi == "1" or (gi == "auto" and gpu_engine and big_jobs):
-        inflater = native.GpuInflater(anonymizer.device, min_blocks)
+        # (one per device and process, kept for the next run: its context's teardown was part of
+        # every run's tail)
+        inflater = _INFLATERS.get((anonymizer.device, min_blocks))
+        if inflater is None:
+            inflater = _INFLATERS[(anonymizer.device, min_blocks)] = native.GpuInflater(anonymizer.device, min_blocks)
         for r in readers:
             r.set_inflater(inflater)
     owner = assign_contigs([j.length for j in jobs], world)
@@ -1284,12 +1296,9 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
             dec_pool.shutdown(wait=True)
         for fd in fds:
             os.close(fd)
-        for r in readers:
-            r.close()
-        for r in redo_readers:
-            r.close()
-        if inflater is not None:   # (after its readers: the device context goes with it)
-            inflater.close()
+        # the readers' file mappings go on a thread of their own (unmapping a chromosome's BAM
+        # took part of every rank's tail; nothing waits for it)
+        threading.Thread(target=_close_all, args=(list(readers) + list(redo_readers),), daemon=True).start()
         if coord is not None:
             coord.close()
     if "tails" in locals():

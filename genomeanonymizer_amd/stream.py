@@ -99,6 +99,7 @@ class JobSpec:
         return self.contig if self.region is None else f"{self.contig}:{self.region[0]}-{self.region[1]}"
 
 
+DECODE_TIMES = {"decode_s": 0.0}   # per process (one decode thread per streamed run)
 _INFLATERS: Dict[Tuple[int, int], "native.GpuInflater"] = {}   # (device, min blocks) -> this process's inflater
 
 
@@ -159,6 +160,7 @@ def decode_job(readers, spec: JobSpec, secondaries: "Optional[SecondaryIndex]" =
     ``secondaries``, the secondary alignments among them whose mate another job reads are published
     there before the tables are handed on (the decode runs in job order, so every later job's plan
     sees them)."""
+    t0 = time.time()
     if spec.region is None:
         tables = tuple(r.contig(r.tid_of(spec.contig)) for r in readers)
     else:
@@ -179,6 +181,7 @@ def decode_job(readers, spec: JobSpec, secondaries: "Optional[SecondaryIndex]" =
             tables = tuple(r.region(r.tid_of(spec.contig), need_lo, need_hi) for r in readers)
     if secondaries is not None:
         secondaries.publish(spec.index, secondaries.scan(tables, spec.index)[0])
+    DECODE_TIMES["decode_s"] += time.time() - t0   # (the decode thread's busy time)
     return tables
 
 
@@ -426,6 +429,8 @@ class Job(JobPrep):
         self.cx = self._complex_ingredients()
         self.timing = {"decode_s": t_dec, "plan_s": t_pl, "mask_s": t3 - t2 + t_b, "format_s": t4 - t3,
                        "prefetch_s": hidden}
+        # the prefetch thread's parts: waiting for the decode thread, the plan, the batch build
+        self.prep_parts = self.prep_timing if prepared is not None else (0.0, 0.0, 0.0)
 
     def _format_instances(self):
         """Every read once as its masked copy (or unmasked), plus the unmasked records the events,
@@ -1192,6 +1197,7 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
     timing["setup_s"] = t_loop0 - t_start   # (readers, job plan, exchange groups, inflater, coordinator)
     timing["groups_s"] = timing_groups
     fq0 = dict(native.FQ_TIMES)
+    dec0 = DECODE_TIMES["decode_s"]
     try:
         try:
             for i, j in enumerate(mine):
@@ -1206,6 +1212,9 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
                 exp["err"] = None
                 for k in ("decode_s", "plan_s", "mask_s", "format_s", "prefetch_s"):
                     timing[k] += job.timing[k]
+                pp = timing.setdefault("prep_parts", {"decode_wait": 0.0, "plan": 0.0, "batch": 0.0})
+                for k, v in zip(("decode_wait", "plan", "batch"), job.prep_parts):
+                    pp[k] = round(pp[k] + v, 3)
                 timing["jobs"] += 1
                 # (job mode: the records starting in the job's range; the margin's belong to its neighbours)
                 for t in job.tables:
@@ -1324,6 +1333,7 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
     cp["tail"] = max(0.0, loop - sum(cp.values()))
     timing["critical_path"] = {k: round(v, 3) for k, v in cp.items()}
     # the device formatter's share of "format": record upload, run, download of the bytes
+    timing["decode_thread_s"] = round(DECODE_TIMES["decode_s"] - dec0, 3)
     timing["fastq_device"] = {k: round(native.FQ_TIMES[k] - fq0[k], 3) if k != "bytes" else native.FQ_TIMES[k] - fq0[k]
                               for k in native.FQ_TIMES}
     return timing

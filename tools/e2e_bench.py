@@ -152,7 +152,7 @@ def main():
                 dist.all_gather_object(per_rank, {k: tim.get(k) for k in (
                     "wall_s", "exchange_sent_bytes", "exchange_recv_bytes", "wait_s", "writer_wait_s", "jobs",
                     "decode_s", "mask_s", "format_s", "write_s", "redos_skipped", "critical_path", "cpu_s", "fastq_device",
-                    "setup_s", "groups_s", "tail_parts")})
+                    "setup_s", "groups_s", "tail_parts", "prep_parts", "decode_thread_s", "prefetch_s")})
                 tim["per_rank"] = per_rank
                 import torch
                 w = torch.tensor([tim["wall_s"]], dtype=torch.float64)

@@ -100,7 +100,15 @@ class JobSpec:
 
 
 DECODE_TIMES = {"decode_s": 0.0}   # per process (one decode thread per streamed run)
-_INFLATERS: Dict[Tuple[int, int], "native.GpuInflater"] = {}   # (device, min blocks) -> this process's inflater
+_SAMPLE_POOL: list = []
+
+
+def _sample_pool():
+    """Two threads reading a job's tumor and normal BAM at once (one per process)."""
+    if not _SAMPLE_POOL:
+        _SAMPLE_POOL.append(ThreadPoolExecutor(2, thread_name_prefix="ganon-sample"))
+    return _SAMPLE_POOL[0]
+_INFLATERS: Dict[Tuple[int, int, int], "native.GpuInflater"] = {}   # (device, min blocks, sample) -> inflater
 
 
 def _close_all(objs) -> None:
@@ -161,15 +169,19 @@ def decode_job(readers, spec: JobSpec, secondaries: "Optional[SecondaryIndex]" =
     there before the tables are handed on (the decode runs in job order, so every later job's plan
     sees them)."""
     t0 = time.time()
+    # the two samples' BAMs are read at once (round 5: the decode thread bounded the 30x line's ranks;
+    # each reader has its own threads and, with GPU inflate, its own inflater context; the native
+    # reads drop the GIL)
+    both = _sample_pool().map if len(readers) == 2 and os.environ.get("GANON_DECODE_PAIR", "1") != "0" else map
     if spec.region is None:
-        tables = tuple(r.contig(r.tid_of(spec.contig)) for r in readers)
+        tables = tuple(both(lambda r: r.contig(r.tid_of(spec.contig)), readers))
     else:
         # the scopes of a gap section pile up the union of its read clusters (pileup_io.pyx:124-298,
         # SR:523-534), which reaches past the job's range by a read's extent: the records overlapping
         # [lo, hi) fix the range the job's pileups can touch; read with a margin, again if it was short
         lo, hi = spec.region
         m = int(os.environ.get("GANON_JOB_MARGIN", "4096"))
-        tables = tuple(r.region(r.tid_of(spec.contig), max(0, lo - m), hi + m) for r in readers)
+        tables = tuple(both(lambda r: r.region(r.tid_of(spec.contig), max(0, lo - m), hi + m), readers))
         need_lo, need_hi = lo, hi
         for t in tables:
             if t.n:
@@ -178,7 +190,7 @@ def decode_job(readers, spec: JobSpec, secondaries: "Optional[SecondaryIndex]" =
                     need_lo = min(need_lo, int(np.asarray(t.pos)[sel].min()))
                     need_hi = max(need_hi, int(np.asarray(t.end)[sel].max()))
         if need_lo < lo - m or need_hi > hi + m:
-            tables = tuple(r.region(r.tid_of(spec.contig), need_lo, need_hi) for r in readers)
+            tables = tuple(both(lambda r: r.region(r.tid_of(spec.contig), need_lo, need_hi), readers))
     if secondaries is not None:
         secondaries.publish(spec.index, secondaries.scan(tables, spec.index)[0])
     DECODE_TIMES["decode_s"] += time.time() - t0   # (the decode thread's busy time)
@@ -1004,9 +1016,8 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
     job_bp = int(os.environ.get("GANON_JOB_BP", "0") or 0) if "GANON_JOB_BP" in os.environ else \
         auto_job_bp(sum(int(L) for L in fasta.lengths), world)
     jobs = plan_jobs(fasta, windows, job_bp, all(r.has_index for r in readers))
-    # The decode thread's BGZF windows inflate on this rank's GPU (one context of its own, shared by
-    # both readers: they are only used by that thread, one at a time) when the masking engine is the
-    # GPU's and a job's reads come in windows of at least GANON_GPU_INFLATE_MIN blocks (default 512,
+    # The readers' BGZF windows inflate on this rank's GPU (a context of its own per reader: the two
+    # samples decode at once) when the masking engine is the GPU's and a job's reads come in windows of at least GANON_GPU_INFLATE_MIN blocks (default 512,
     # ~18 MB compressed: a block takes milliseconds on its wave, so only large windows pay off, and
     # the context costs its setup) — round 5: the token-round kernel made it the faster decoder at
     # chromosome scale (30x line: 6.28e6 -> 6.93e6 and 5.87e6 -> 8.04e6 reads/s on two boxes, 22 %
@@ -1017,12 +1028,13 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
     gpu_engine = anonymizer._engine is None or isinstance(anonymizer._engine, native.HipMasker)
     big_jobs = max(os.path.getsize(p) for p in (tumor_bam, normal_bam)) / max(1, len(jobs)) >= min_blocks * 36_000
     if gi == "1" or (gi == "auto" and gpu_engine and big_jobs):
-        # (one per device and process, kept for the next run: its context's teardown was part of
-        # every run's tail)
-        inflater = _INFLATERS.get((anonymizer.device, min_blocks))
-        if inflater is None:
-            inflater = _INFLATERS[(anonymizer.device, min_blocks)] = native.GpuInflater(anonymizer.device, min_blocks)
-        for r in readers:
+        # (per device, sample and process, kept for the next run: their teardown was part of every
+        # run's tail)
+        for i, r in enumerate(readers):
+            inflater = _INFLATERS.get((anonymizer.device, min_blocks, i))
+            if inflater is None:
+                inflater = _INFLATERS[(anonymizer.device, min_blocks, i)] = native.GpuInflater(anonymizer.device,
+                                                                                             min_blocks)
             r.set_inflater(inflater)
     owner = assign_contigs([j.length for j in jobs], world)
     mine = [j for j in range(len(jobs)) if owner[j] == rank]

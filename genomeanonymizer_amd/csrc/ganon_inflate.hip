@@ -447,10 +447,37 @@ struct RoundToks<64> {
     m = uni64(m);
     // (the offset lives in m0 inside the loop: writelane may take m0 as its lane select beside an
     // SGPR value, where a second SGPR would break the one-SGPR operand limit)
+    // (with room for a whole k of literals — at most 64 — the output limit is not tested per
+    // literal, and the loop takes two literals per branch back)
     __asm__ __volatile__(
         "s_mov_b32 %[tk], 0\n\t"
-        "s_mov_b32 m0, %[xk]\n"
+        "s_mov_b32 m0, %[xk]\n\t"
+        "s_sub_i32 %[tmp], %[lim], %[out]\n\t"
+        "s_cmp_lt_i32 %[tmp], 64\n\t"
+        "s_cbranch_scc1 3f\n"
         "1:\n\t"
+        "s_cmp_lt_i32 m0, 64\n\t"
+        "s_cbranch_scc0 2f\n\t"
+        "v_readlane_b32 %[tk], %[tv], m0\n\t"
+        "s_and_b32 %[tmp], %[tk], 0x18000\n\t"
+        "s_cbranch_scc1 2f\n\t"
+        "v_writelane_b32 %[p], %[out], m0\n\t"
+        "s_bitset1_b64 %[m], m0\n\t"
+        "s_and_b32 %[tmp], %[tk], 63\n\t"
+        "s_add_i32 %[out], %[out], 1\n\t"
+        "s_add_i32 m0, m0, %[tmp]\n\t"
+        "s_cmp_lt_i32 m0, 64\n\t"
+        "s_cbranch_scc0 2f\n\t"
+        "v_readlane_b32 %[tk], %[tv], m0\n\t"
+        "s_and_b32 %[tmp], %[tk], 0x18000\n\t"
+        "s_cbranch_scc1 2f\n\t"
+        "v_writelane_b32 %[p], %[out], m0\n\t"
+        "s_bitset1_b64 %[m], m0\n\t"
+        "s_and_b32 %[tmp], %[tk], 63\n\t"
+        "s_add_i32 %[out], %[out], 1\n\t"
+        "s_add_i32 m0, m0, %[tmp]\n\t"
+        "s_branch 1b\n"
+        "3:\n\t"
         "s_cmp_lt_i32 m0, 64\n\t"
         "s_cbranch_scc0 2f\n\t"
         "s_cmp_lt_i32 %[out], %[lim]\n\t"
@@ -463,7 +490,7 @@ struct RoundToks<64> {
         "s_and_b32 %[tmp], %[tk], 63\n\t"
         "s_add_i32 %[out], %[out], 1\n\t"
         "s_add_i32 m0, m0, %[tmp]\n\t"
-        "s_branch 1b\n"
+        "s_branch 3b\n"
         "2:\n\t"
         "s_mov_b32 %[xk], m0"
         : [tk] "=&s"(tk), [tmp] "=&s"(tmp), [xk] "+s"(xk), [out] "+s"(out), [m] "+s"(m), [p] "+v"(p)

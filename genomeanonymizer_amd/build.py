@@ -43,7 +43,8 @@ def _run(cmd) -> None:
         raise RuntimeError(f"build failed: {' '.join(cmd)}")
 
 
-HIP_SOURCES = ("ganon_hip.hip", "ganon_prep.hip", "ganon_fastq.hip", "ganon_indel.hip", "ganon_inflate.hip")
+HIP_SOURCES = ("ganon_hip.hip", "ganon_prep.hip", "ganon_fastq.hip", "ganon_indel.hip", "ganon_inflate.hip",
+               "ganon_bam.hip")
 
 
 def build_hip(force: bool = False) -> str:

@@ -1,0 +1,506 @@
+// ganon_bam.hip — BAM records to column arrays on MI355X (gfx950), part of libganon_hip.so; C ABI in
+// include/ganon.h (ganon_bam_columns). SURVEY §8(f)4, its second half: the record walk after the
+// inflate, which libganon_host.so does on the host (records_to_columns, csrc/ganon_host.cpp; the
+// column view ganon_bam_view of include/ganon_host.h) and the reference gets from htslib's bam_read1
+// behind AlignmentFile.fetch / pileup (pileup_io.pyx:12-17). The input is the inflated stream in
+// device memory — k_inflate's output where the inflate ran on the device (ganon_inflate_device_output)
+// — so the decoded records never cross PCIe.
+//
+// Record boundaries. Record k + 1 starts 4 + block_size(k) bytes after record k: a chain that one
+// thread would walk at one dependent load per record. The stream [p, n) is cut into kChunk-byte
+// chunks; chunk c holds the records that start in [p + c kChunk, p + (c + 1) kChunk). One thread per
+// chunk guesses the chunk's first record start (the first offset from which kProbe chained records
+// look like BAM records: sizes, reference ids, name terminator, read length against the block size)
+// and walks the chain to the chunk's end: its record count and exit (the first start at or past the
+// chunk's end). The guesses are then proven: chunk 0 starts at p, and a chunk whose guess equals its
+// predecessor's exit holds exactly the true records when its predecessor does — so by induction every
+// chunk before the first failing one is exact. A failing chunk whose predecessor passed is walked
+// again from that predecessor's exit, and the host repeats check and fix until no chunk fails (each
+// round fixes at least the first failing chunk; none needed a fix on any BAM tried, see `fixes`).
+// The exact walk checks what the host decoder checks (block_size >= 32, the record inside the
+// stream), the per-record pass the rest (read length and CIGAR inside the block): same errors.
+//
+// Columns. Per-record sizes (name bytes kept with a NUL, CIGAR ops, packed sequence bytes, quality
+// bytes, aux bytes), five exclusive scans (rocPRIM) for the blob offsets, then a wave per record:
+// lanes 0-35 load the record's size and fixed fields once (broadcast by readlane), lane 0 writes the
+// scalar columns, the wave copies name / CIGAR / sequence / quality / aux bytes lane-strided and sums
+// the reference length of its CIGAR ops for bam_endpos. Bytes are copied as bytes: BAM fields are
+// not aligned in the stream.
+#include <hip/hip_runtime.h>
+#include <rocprim/device/device_scan.hpp>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "../../include/ganon.h"
+#include "ganon_ctx.h"
+
+using ganon_detail::check_launch;
+using ganon_detail::fail;
+
+namespace {
+
+constexpr int kBamThreads = 256;
+constexpr int64_t kChunk = 4096;     // stream bytes per chunk (~12 short-read records)
+constexpr int kProbe = 4;            // chained plausible records that make a guess
+constexpr int64_t kGuessSpan = 3 * kChunk;   // guess search window from the chunk start
+
+__device__ __forceinline__ uint32_t rd32(const uint8_t *__restrict__ d, int64_t o) {
+  return (uint32_t)d[o] | ((uint32_t)d[o + 1] << 8) | ((uint32_t)d[o + 2] << 16) | ((uint32_t)d[o + 3] << 24);
+}
+
+// Does a BAM record plausibly start at o? (guesses only: a wrong guess is caught by the check)
+__device__ __forceinline__ bool plausible(const uint8_t *__restrict__ d, int64_t o, int64_t n, int64_t &next) {
+  if (o + 36 > n) return false;
+  const int32_t bs = (int32_t)rd32(d, o);
+  if (bs < 32 || o + 4 + (int64_t)bs > n) return false;
+  const int32_t tid = (int32_t)rd32(d, o + 4), pos = (int32_t)rd32(d, o + 8);
+  const int l_rn = d[o + 12];
+  const int ncig = (int)(d[o + 16] | (d[o + 17] << 8));
+  const int32_t lseq = (int32_t)rd32(d, o + 20);
+  const int32_t mtid = (int32_t)rd32(d, o + 24), mpos = (int32_t)rd32(d, o + 28);
+  if (tid < -1 || pos < -1 || mtid < -1 || mpos < -1 || l_rn < 1 || lseq < 0) return false;
+  if (32 + (int64_t)l_rn + 4LL * ncig + ((int64_t)lseq + 1) / 2 + lseq > bs) return false;
+  if (d[o + 4 + 32 + l_rn - 1] != 0) return false;
+  next = o + 4 + bs;
+  return true;
+}
+
+__device__ __forceinline__ bool chain_plausible(const uint8_t *__restrict__ d, int64_t o, int64_t n) {
+  for (int k = 0; k < kProbe && o < n; ++k) {
+    int64_t next;
+    if (!plausible(d, o, n, next)) return false;
+    o = next;
+  }
+  return true;
+}
+
+struct Chunks {
+  int64_t *entry, *exitp, *cnt;
+  int32_t *bad;     // 1: truncated size field, 2: bad block_size (the walk stopped there)
+  uint8_t *flag;    // the chunk's entry is not its predecessor's exit
+  unsigned long long *info;   // [failing chunks, first failing chunk, first bad chunk]
+};
+
+// Walk chunk c's chain from e (a record start, or < 0 for none): count and exit.
+__device__ __forceinline__ void walk(const uint8_t *__restrict__ d, int64_t p, int64_t n, int64_t c, int64_t e,
+                                     const Chunks &K) {
+  const int64_t ce = min(n, p + (c + 1) * kChunk);
+  int64_t s = e, k = 0;
+  int b = 0;
+  if (s >= 0) {
+    while (s < ce) {
+      if (s + 4 > n) {
+        b = 1;
+        break;
+      }
+      const int32_t bs = (int32_t)rd32(d, s);
+      if (bs < 32 || s + 4 + (int64_t)bs > n) {
+        b = 2;
+        break;
+      }
+      s += 4 + (int64_t)bs;
+      ++k;
+    }
+  }
+  K.entry[c] = e;
+  K.exitp[c] = b ? -2 : (e >= 0 ? s : -1);
+  K.cnt[c] = k;
+  K.bad[c] = b;
+}
+
+// mode 0: every chunk guesses its entry (chunk 0: p) and walks; mode 1: failing chunks whose
+// predecessor passed walk again from the predecessor's exit.
+__global__ void __launch_bounds__(kBamThreads) k_bam_walk(const uint8_t *__restrict__ d, int64_t p, int64_t n,
+                                                          int64_t n_chunks, Chunks K, int mode) {
+  const int64_t c = (int64_t)blockIdx.x * kBamThreads + threadIdx.x;
+  if (c >= n_chunks) return;
+  if (mode == 1) {
+    if (c == 0 || !K.flag[c] || K.flag[c - 1]) return;
+    walk(d, p, n, c, K.exitp[c - 1], K);
+    return;
+  }
+  int64_t e = -1;
+  if (c == 0) {
+    e = p;
+  } else {
+    const int64_t cs = p + c * kChunk, lim = min(n, cs + kGuessSpan);
+    for (int64_t o = cs; o < lim; ++o)
+      if (chain_plausible(d, o, n)) {
+        e = o;
+        break;
+      }
+    if (e < 0 && lim == n) e = n;   // (no record starts in the rest of the stream: a guess too)
+  }
+  walk(d, p, n, c, e, K);
+}
+
+__global__ void __launch_bounds__(kBamThreads) k_bam_check(int64_t n_chunks, Chunks K) {
+  const int64_t c = (int64_t)blockIdx.x * kBamThreads + threadIdx.x;
+  if (c >= n_chunks) return;
+  const int64_t e = K.entry[c];
+  const bool f = c > 0 && (e < 0 || e != K.exitp[c - 1]);
+  K.flag[c] = f ? 1 : 0;
+  if (f) {
+    __hip_atomic_fetch_add(K.info, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_min(K.info + 1, (unsigned long long)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (K.bad[c]) __hip_atomic_fetch_min(K.info + 2, (unsigned long long)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The record offsets: each chunk's chain again, from its proven entry, at its records' base index.
+__global__ void __launch_bounds__(kBamThreads) k_bam_offsets(const uint8_t *__restrict__ d, int64_t p, int64_t n,
+                                                             int64_t n_chunks, const int64_t *__restrict__ entry,
+                                                             const int64_t *__restrict__ base,
+                                                             int64_t *__restrict__ rec) {
+  const int64_t c = (int64_t)blockIdx.x * kBamThreads + threadIdx.x;
+  if (c >= n_chunks) return;
+  const int64_t ce = min(n, p + (c + 1) * kChunk);
+  int64_t s = entry[c], i = base[c];
+  if (s < 0) return;
+  while (s < ce) {
+    rec[i++] = s;
+    s += 4 + (int64_t)(int32_t)rd32(d, s);
+  }
+}
+
+struct Sizes {
+  int64_t *name, *cig, *seq, *qual, *aux;   // [nr + 1] each (the last entry 0: the scan's total)
+};
+
+// Per record: the blob bytes it takes (records_to_columns' first pass), or the first bad record.
+__global__ void __launch_bounds__(kBamThreads) k_bam_sizes(const uint8_t *__restrict__ d, const int64_t *__restrict__ rec,
+                                                           int64_t nr, Sizes S, unsigned long long *__restrict__ first_bad) {
+  const int64_t i = (int64_t)blockIdx.x * kBamThreads + threadIdx.x;
+  if (i >= nr) return;
+  const int64_t o = rec[i];
+  const int32_t bs = (int32_t)rd32(d, o);
+  const uint8_t *r = d + o + 4;
+  const int l_rn = r[8];
+  const int ncig = (int)(r[12] | (r[13] << 8));
+  const int32_t lseq = (int32_t)rd32(r, 16);
+  const int64_t need = 32 + (int64_t)l_rn + 4LL * ncig + ((int64_t)lseq + 1) / 2 + lseq;
+  if (lseq < 0 || need > bs) {
+    __hip_atomic_fetch_min(first_bad, (unsigned long long)i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    S.name[i] = S.cig[i] = S.seq[i] = S.qual[i] = S.aux[i] = 0;
+    return;
+  }
+  S.name[i] = l_rn + ((l_rn == 0 || r[32 + l_rn - 1] != 0) ? 1 : 0);
+  S.cig[i] = ncig;
+  S.seq[i] = ((int64_t)lseq + 1) / 2;
+  S.qual[i] = lseq;
+  S.aux[i] = bs - need;
+}
+
+}  // namespace
+
+struct ganon_bam_dcols {
+  ganon_bam_cols v{};          // device pointers
+  void *block = nullptr;        // one allocation for the per-record columns
+  void *blobs = nullptr;        // one allocation for the blobs
+  uint8_t *stream = nullptr;    // the device copy of a host stream (on_host)
+  int64_t fixes = 0;            // check/fix rounds that found failing chunks
+};
+
+namespace {
+
+__global__ void __launch_bounds__(kBamThreads) k_bam_scatter(const uint8_t *__restrict__ d, const int64_t *__restrict__ rec,
+                                                             int64_t nr, ganon_bam_cols V) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * (kBamThreads / 64);
+  uint8_t *cig8 = reinterpret_cast<uint8_t *>(V.cigar);
+  for (int64_t i = ((int64_t)blockIdx.x * kBamThreads + threadIdx.x) >> 6; i < nr; i += nw) {
+    const int64_t o = rec[i];
+    const int hb = lane < 36 ? (int)d[o + lane] : 0;   // block_size + the fixed fields
+    auto b = [&](int k) { return (uint32_t)__builtin_amdgcn_readlane(hb, k) & 0xFFu; };
+    auto w32 = [&](int k) { return b(k) | (b(k + 1) << 8) | (b(k + 2) << 16) | (b(k + 3) << 24); };
+    const int32_t bs = (int32_t)w32(0);
+    const int l_rn = (int)b(12);
+    const int ncig = (int)(b(16) | (b(17) << 8));
+    const int flag = (int)(b(18) | (b(19) << 8));
+    const int32_t lseq = (int32_t)w32(20);
+    const int32_t pos = (int32_t)w32(8);
+    const uint8_t *r = d + o + 4;
+    const int64_t o_name = V.name_off[i], o_cig = V.cig_off[i], o_seq = V.seq_off[i], o_qual = V.qual_off[i],
+                  o_aux = V.aux_off[i];
+    // name (+ NUL when the record's own is missing)
+    for (int k = lane; k < l_rn; k += 64) V.names[o_name + k] = (char)r[32 + k];
+    if (lane == 0 && V.name_off[i + 1] - o_name > l_rn) V.names[o_name + l_rn] = 0;
+    int64_t q = 32 + l_rn;
+    // CIGAR words (bytes) and the reference length of M / D / N / = / X
+    for (int k = lane; k < 4 * ncig; k += 64) cig8[4 * o_cig + k] = r[q + k];
+    unsigned long long rl = 0;
+    for (int k = lane; k < ncig; k += 64) {
+      const uint32_t w = rd32(r, q + 4LL * k);
+      const int op = (int)(w & 0xF);
+      if (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) rl += w >> 4;
+    }
+    for (int s = 32; s > 0; s >>= 1) {
+      const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)rl, s), hi = (uint32_t)__shfl_xor((int)(uint32_t)(rl >> 32), s);
+      rl += ((unsigned long long)hi << 32) | lo;
+    }
+    q += 4LL * ncig;
+    const int64_t nseq = ((int64_t)lseq + 1) / 2;
+    for (int64_t k = lane; k < nseq; k += 64) V.seq[o_seq + k] = r[q + k];
+    q += nseq;
+    for (int64_t k = lane; k < lseq; k += 64) V.qual[o_qual + k] = r[q + k];
+    q += lseq;
+    const int64_t na = bs - q;
+    for (int64_t k = lane; k < na; k += 64) V.aux[o_aux + k] = r[q + k];
+    if (lane == 0) {
+      const int64_t rlen = (flag & 4) ? 0 : (int64_t)rl;
+      V.tid[i] = (int32_t)w32(4);
+      V.pos[i] = pos;
+      V.end[i] = (int32_t)(pos + (rlen > 0 ? rlen : 1));
+      V.flag[i] = flag;
+      V.mapq[i] = (int)b(13);
+      V.l_seq[i] = lseq;
+      V.n_cigar[i] = ncig;
+      V.mate_tid[i] = (int32_t)w32(24);
+      V.mate_pos[i] = (int32_t)w32(28);
+      V.tlen[i] = (int32_t)w32(32);
+      V.name_len[i] = l_rn > 0 ? l_rn - 1 : 0;
+      V.aux_len[i] = (int32_t)na;
+    }
+  }
+}
+
+unsigned grid_of(int64_t n) { return (unsigned)std::max<int64_t>(1, (n + kBamThreads - 1) / kBamThreads); }
+
+template <typename T>
+T *carve(uint8_t *&at, int64_t count) {
+  T *p = reinterpret_cast<T *>(at);
+  at += ((count * (int64_t)sizeof(T) + 255) / 256) * 256;
+  return p;
+}
+
+int columns(ganon_ctx *ctx, const uint8_t *d, int64_t p, int64_t n, ganon_bam_dcols *H) {
+  hipStream_t s = ctx->stream;
+  const int64_t n_chunks = n > p ? (n - p + kChunk - 1) / kChunk : 0;
+  int rc;
+  // chunk arrays and the scan's temporary space, one block
+  std::vector<void *> tmp;
+  auto dalloc = [&](size_t bytes) -> void * {
+    void *q = nullptr;
+    if (hipMalloc(&q, std::max<size_t>(bytes, 256)) != hipSuccess) return nullptr;
+    tmp.push_back(q);
+    return q;
+  };
+  struct Free {
+    std::vector<void *> &t;
+    hipStream_t s;
+    ~Free() {
+      if (!t.empty()) hipStreamSynchronize(s);
+      for (void *q : t) hipFree(q);
+    }
+  } free_tmp{tmp, s};
+  Chunks K{};
+  int64_t *base = nullptr;
+  if (n_chunks) {
+    const int64_t nc = n_chunks;
+    K.entry = static_cast<int64_t *>(dalloc(nc * 8));
+    K.exitp = static_cast<int64_t *>(dalloc(nc * 8));
+    K.cnt = static_cast<int64_t *>(dalloc((nc + 1) * 8));
+    base = static_cast<int64_t *>(dalloc((nc + 1) * 8));
+    K.bad = static_cast<int32_t *>(dalloc(nc * 4));
+    K.flag = static_cast<uint8_t *>(dalloc(nc));
+    K.info = static_cast<unsigned long long *>(dalloc(3 * 8));
+    if (!K.entry || !K.exitp || !K.cnt || !base || !K.bad || !K.flag || !K.info)
+      return fail(ctx, GANON_E_DEVICE, "ganon_bam_columns: device allocation failed");
+    {
+      ganon_detail::KernelScope ks(ctx, "k_bam_walk");
+      hipLaunchKernelGGL(k_bam_walk, dim3(grid_of(nc)), dim3(kBamThreads), 0, s, d, p, n, nc, K, 0);
+    }
+    if ((rc = check_launch(ctx, "k_bam_walk"))) return rc;
+    for (int64_t round = 0;; ++round) {
+      const unsigned long long init[3] = {0ull, ~0ull, ~0ull};
+      unsigned long long info[3];
+      HIP_OR_FAIL(hipMemcpyAsync(K.info, init, sizeof init, hipMemcpyHostToDevice, s));
+      {
+        ganon_detail::KernelScope ks(ctx, "k_bam_check");
+        hipLaunchKernelGGL(k_bam_check, dim3(grid_of(nc)), dim3(kBamThreads), 0, s, nc, K);
+      }
+      if ((rc = check_launch(ctx, "k_bam_check"))) return rc;
+      HIP_OR_FAIL(hipMemcpyAsync(info, K.info, sizeof info, hipMemcpyDeviceToHost, s));
+      HIP_OR_FAIL(hipStreamSynchronize(s));
+      // every chunk before the first failing one is exact: a bad walk there is the stream's error
+      if (info[2] != ~0ull && info[2] < info[1])
+        return fail(ctx, GANON_E_ARG, "ganon_bam_columns: bad record size (chunk %lld)", (long long)info[2]);
+      if (info[0] == 0) break;
+      if (round > nc) return fail(ctx, GANON_E_DEVICE, "ganon_bam_columns: record chain did not settle");
+      ++H->fixes;
+      {
+        ganon_detail::KernelScope ks(ctx, "k_bam_walk_fix");
+        hipLaunchKernelGGL(k_bam_walk, dim3(grid_of(nc)), dim3(kBamThreads), 0, s, d, p, n, nc, K, 1);
+      }
+      if ((rc = check_launch(ctx, "k_bam_walk_fix"))) return rc;
+    }
+    HIP_OR_FAIL(hipMemsetAsync(K.cnt + nc, 0, 8, s));
+    size_t tb = 0;
+    HIP_OR_FAIL(rocprim::exclusive_scan(nullptr, tb, K.cnt, base, (int64_t)0, (size_t)(nc + 1), rocprim::plus<int64_t>(), s));
+    void *tsc = dalloc(tb);
+    if (!tsc) return fail(ctx, GANON_E_DEVICE, "ganon_bam_columns: device allocation failed");
+    HIP_OR_FAIL(rocprim::exclusive_scan(tsc, tb, K.cnt, base, (int64_t)0, (size_t)(nc + 1), rocprim::plus<int64_t>(), s));
+  }
+  int64_t nr = 0;
+  if (n_chunks) {
+    HIP_OR_FAIL(hipMemcpyAsync(&nr, base + n_chunks, 8, hipMemcpyDeviceToHost, s));
+    HIP_OR_FAIL(hipStreamSynchronize(s));
+  }
+  // per-record columns: 12 int32 + 6 int64 (5 offsets of nr + 1, the record offsets) + the sizes
+  ganon_bam_cols &V = H->v;
+  V.n_records = nr;
+  {
+    const int64_t m = nr + 1;
+    const int64_t bytes = 12 * (((m * 4) + 255) / 256 * 256) + 11 * (((m * 8) + 255) / 256 * 256);
+    if (hipMalloc(&H->block, (size_t)std::max<int64_t>(bytes, 256)) != hipSuccess)
+      return fail(ctx, GANON_E_DEVICE, "ganon_bam_columns: device allocation of %lld bytes failed", (long long)bytes);
+    uint8_t *at = static_cast<uint8_t *>(H->block);
+    for (int32_t **f : {&V.tid, &V.pos, &V.end, &V.flag, &V.mapq, &V.l_seq, &V.n_cigar, &V.mate_tid, &V.mate_pos, &V.tlen,
+                        &V.name_len, &V.aux_len})
+      *f = carve<int32_t>(at, m);
+    for (int64_t **f : {&V.name_off, &V.cig_off, &V.seq_off, &V.qual_off, &V.aux_off, &V.rec_off}) *f = carve<int64_t>(at, m);
+    Sizes S{carve<int64_t>(at, m), carve<int64_t>(at, m), carve<int64_t>(at, m), carve<int64_t>(at, m),
+            carve<int64_t>(at, m)};
+    unsigned long long *first_bad = static_cast<unsigned long long *>(dalloc(8));
+    if (!first_bad) return fail(ctx, GANON_E_DEVICE, "ganon_bam_columns: device allocation failed");
+    const unsigned long long none = ~0ull;
+    HIP_OR_FAIL(hipMemcpyAsync(first_bad, &none, 8, hipMemcpyHostToDevice, s));
+    if (nr) {
+      ganon_detail::KernelScope ks(ctx, "k_bam_offsets");
+      hipLaunchKernelGGL(k_bam_offsets, dim3(grid_of(n_chunks)), dim3(kBamThreads), 0, s, d, p, n, n_chunks, K.entry, base,
+                         V.rec_off);
+    }
+    if ((rc = check_launch(ctx, "k_bam_offsets"))) return rc;
+    for (int64_t *z : {S.name, S.cig, S.seq, S.qual, S.aux}) HIP_OR_FAIL(hipMemsetAsync(z + nr, 0, 8, s));
+    if (nr) {
+      ganon_detail::KernelScope ks(ctx, "k_bam_sizes");
+      hipLaunchKernelGGL(k_bam_sizes, dim3(grid_of(nr)), dim3(kBamThreads), 0, s, d, V.rec_off, nr, S, first_bad);
+    }
+    if ((rc = check_launch(ctx, "k_bam_sizes"))) return rc;
+    size_t tb = 0;
+    HIP_OR_FAIL(rocprim::exclusive_scan(nullptr, tb, S.name, V.name_off, (int64_t)0, (size_t)m, rocprim::plus<int64_t>(), s));
+    void *tsc = dalloc(tb);
+    if (!tsc) return fail(ctx, GANON_E_DEVICE, "ganon_bam_columns: device allocation failed");
+    {
+      ganon_detail::KernelScope ks(ctx, "bam_scans");
+      const std::pair<int64_t *, int64_t *> io[5] = {{S.name, V.name_off}, {S.cig, V.cig_off}, {S.seq, V.seq_off},
+                                                     {S.qual, V.qual_off}, {S.aux, V.aux_off}};
+      for (const auto &x : io)
+        HIP_OR_FAIL(rocprim::exclusive_scan(tsc, tb, x.first, x.second, (int64_t)0, (size_t)m, rocprim::plus<int64_t>(), s));
+    }
+    unsigned long long bad_rec = ~0ull;
+    int64_t tot[5];
+    HIP_OR_FAIL(hipMemcpyAsync(&bad_rec, first_bad, 8, hipMemcpyDeviceToHost, s));
+    int64_t *offs[5] = {V.name_off, V.cig_off, V.seq_off, V.qual_off, V.aux_off};
+    for (int k = 0; k < 5; ++k) HIP_OR_FAIL(hipMemcpyAsync(&tot[k], offs[k] + nr, 8, hipMemcpyDeviceToHost, s));
+    HIP_OR_FAIL(hipStreamSynchronize(s));
+    if (bad_rec != ~0ull)
+      return fail(ctx, GANON_E_ARG, "ganon_bam_columns: record %lld: fields exceed block size", (long long)bad_rec);
+    V.names_bytes = tot[0];
+    V.cigar_ops = tot[1];
+    V.seq_bytes = tot[2];
+    V.qual_bytes = tot[3];
+    V.aux_bytes = tot[4];
+  }
+  {
+    const int64_t rb = ((V.names_bytes + 255) / 256 + (4 * V.cigar_ops + 255) / 256 + (V.seq_bytes + 255) / 256 +
+                        (V.qual_bytes + 255) / 256 + (V.aux_bytes + 255) / 256) * 256;
+    if (hipMalloc(&H->blobs, (size_t)std::max<int64_t>(rb, 256)) != hipSuccess)
+      return fail(ctx, GANON_E_DEVICE, "ganon_bam_columns: device allocation of %lld bytes failed", (long long)rb);
+    uint8_t *at = static_cast<uint8_t *>(H->blobs);
+    V.names = carve<char>(at, V.names_bytes);
+    V.cigar = carve<uint32_t>(at, V.cigar_ops);
+    V.seq = carve<uint8_t>(at, V.seq_bytes);
+    V.qual = carve<uint8_t>(at, V.qual_bytes);
+    V.aux = carve<uint8_t>(at, V.aux_bytes);
+  }
+  if (nr) {
+    ganon_detail::KernelScope ks(ctx, "k_bam_scatter");
+    const unsigned grid = (unsigned)std::min<int64_t>((nr + 3) / 4, 1 << 16);
+    hipLaunchKernelGGL(k_bam_scatter, dim3(grid), dim3(kBamThreads), 0, s, d, V.rec_off, nr, V);
+  }
+  if ((rc = check_launch(ctx, "k_bam_scatter"))) return rc;
+  return ganon_batch_sync(ctx);   // (collects the kernel times when profiling)
+}
+
+void release(ganon_bam_dcols *H) {
+  if (!H) return;
+  hipFree(H->block);
+  hipFree(H->blobs);
+  hipFree(H->stream);
+  delete H;
+}
+
+}  // namespace
+
+GANON_API int ganon_bam_columns(ganon_ctx *ctx, const uint8_t *stream, int64_t p, int64_t n, int on_host,
+                                ganon_bam_dcols **out) {
+  if (!ctx || !out || p < 0 || n < p || (n > 0 && !stream))
+    return fail(ctx, GANON_E_ARG, "ganon_bam_columns: bad arguments");
+  *out = nullptr;
+  if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, GANON_E_DEVICE, "hipSetDevice failed");
+  auto *H = new ganon_bam_dcols();
+  const uint8_t *d = stream;
+  if (on_host && n > 0) {
+    if (hipMalloc(&H->stream, (size_t)n) != hipSuccess) {
+      release(H);
+      return fail(ctx, GANON_E_DEVICE, "ganon_bam_columns: device allocation of %lld bytes failed", (long long)n);
+    }
+    if (hipMemcpyAsync(H->stream, stream, (size_t)n, hipMemcpyHostToDevice, ctx->stream) != hipSuccess) {
+      hipStreamSynchronize(ctx->stream);
+      release(H);
+      return fail(ctx, GANON_E_DEVICE, "ganon_bam_columns: stream copy failed");
+    }
+    d = H->stream;
+  }
+  const int rc = columns(ctx, d, p, n, H);
+  if (rc) {
+    hipStreamSynchronize(ctx->stream);
+    release(H);
+    return rc;
+  }
+  *out = H;
+  return GANON_OK;
+}
+
+GANON_API int ganon_bam_dcols_get(const ganon_bam_dcols *c, ganon_bam_cols *device_view, int64_t *fixes) {
+  if (!c || !device_view) return GANON_E_ARG;
+  *device_view = c->v;
+  if (fixes) *fixes = c->fixes;
+  return GANON_OK;
+}
+
+GANON_API int ganon_bam_dcols_download(ganon_ctx *ctx, const ganon_bam_dcols *c, const ganon_bam_cols *host) {
+  if (!ctx || !c || !host) return fail(ctx, GANON_E_ARG, "ganon_bam_dcols_download: bad arguments");
+  const ganon_bam_cols &V = c->v;
+  const int64_t nr = V.n_records;
+  hipStream_t s = ctx->stream;
+  auto cp = [&](void *dst, const void *src, int64_t bytes) {
+    return !dst || bytes <= 0 || hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDeviceToHost, s) == hipSuccess;
+  };
+  bool ok = true;
+  const std::pair<int32_t *, const int32_t *> i32[12] = {
+      {host->tid, V.tid}, {host->pos, V.pos}, {host->end, V.end}, {host->flag, V.flag}, {host->mapq, V.mapq},
+      {host->l_seq, V.l_seq}, {host->n_cigar, V.n_cigar}, {host->mate_tid, V.mate_tid}, {host->mate_pos, V.mate_pos},
+      {host->tlen, V.tlen}, {host->name_len, V.name_len}, {host->aux_len, V.aux_len}};
+  for (const auto &x : i32) ok = ok && cp(x.first, x.second, nr * 4);
+  const std::pair<int64_t *, const int64_t *> i64[6] = {{host->name_off, V.name_off}, {host->cig_off, V.cig_off},
+                                                        {host->seq_off, V.seq_off},   {host->qual_off, V.qual_off},
+                                                        {host->aux_off, V.aux_off},   {host->rec_off, V.rec_off}};
+  for (const auto &x : i64) ok = ok && cp(x.first, x.second, nr * 8);
+  ok = ok && cp(host->names, V.names, V.names_bytes) && cp(host->cigar, V.cigar, 4 * V.cigar_ops) &&
+       cp(host->seq, V.seq, V.seq_bytes) && cp(host->qual, V.qual, V.qual_bytes) && cp(host->aux, V.aux, V.aux_bytes);
+  if (!ok || hipStreamSynchronize(s) != hipSuccess) {
+    hipStreamSynchronize(s);
+    return fail(ctx, GANON_E_DEVICE, "ganon_bam_dcols_download: copy failed");
+  }
+  return GANON_OK;
+}
+
+GANON_API int ganon_bam_dcols_free(ganon_ctx *ctx, ganon_bam_dcols *c) {
+  if (ctx) hipStreamSynchronize(ctx->stream);
+  release(c);
+  return GANON_OK;
+}

@@ -856,6 +856,7 @@ struct ganon_inflate_state {
   int64_t *in_off = nullptr, *out_off = nullptr;
   int32_t *in_len = nullptr, *out_len = nullptr, *status = nullptr;
   size_t comp_cap = 0, out_cap = 0, blk_cap = 0;
+  int64_t last_out = -1;                // out_total of the last successful call (ganon_inflate_device_output)
   hipStream_t copy = nullptr;           // copies of a chunked call (the kernels run on ctx->stream)
   std::vector<hipEvent_t> ev;           // two per chunk
 };
@@ -905,6 +906,7 @@ GANON_API int ganon_inflate(ganon_ctx *ctx, const uint8_t *comp, int64_t comp_le
   const size_t nb = (size_t)n_blocks;
   size_t cap_blk = st->blk_cap;
   int rc;
+  st->last_out = -1;
   if ((rc = grow_dev(ctx, &st->comp, st->comp_cap, (size_t)comp_len)) ||
       (rc = grow_dev(ctx, &st->out, st->out_cap, (size_t)out_total)))
     return rc;
@@ -1002,6 +1004,16 @@ GANON_API int ganon_inflate(ganon_ctx *ctx, const uint8_t *comp, int64_t comp_le
       if (first_bad) *first_bad = (int64_t)i;
       return fail(ctx, GANON_E_ARG, "BGZF block %lld: invalid DEFLATE stream (code %d)", (long long)i, stat[i]);
     }
+  st->last_out = out_total;
+  return GANON_OK;
+}
+
+GANON_API int ganon_inflate_device_output(ganon_ctx *ctx, const uint8_t **out, int64_t *bytes) {
+  if (!ctx || !out || !bytes) return fail(ctx, GANON_E_ARG, "ganon_inflate_device_output: bad arguments");
+  if (!ctx->inflate || ctx->inflate->last_out < 0)
+    return fail(ctx, GANON_E_ARG, "ganon_inflate_device_output: no successful inflate on this context");
+  *out = ctx->inflate->out;
+  *bytes = ctx->inflate->last_out;
   return GANON_OK;
 }
 

@@ -89,7 +89,7 @@ class ReadTable:
         for o in ref_name_off:
             self.ref_names.append(C.string_at(raw + int(o)).decode())
         self.ref_lens = _arr(v.ref_len, v.n_ref, np.int64)
-        for f in ("tid", "pos", "end", "flag", "mapq", "l_seq", "n_cigar", "mate_tid", "mate_pos", "name_len",
+        for f in ("tid", "pos", "end", "flag", "mapq", "l_seq", "n_cigar", "mate_tid", "mate_pos", "tlen", "name_len",
                   "aux_len"):
             setattr(self, f, _arr(getattr(v, f), n, np.int32))
         for f in ("name_off", "cig_off", "seq_off", "qual_off", "aux_off"):
@@ -313,7 +313,7 @@ class BamReader:
         t = ReadTable.__new__(ReadTable)
         t.path, t.n = self.path, 0
         t.ref_names, t.ref_lens = list(self.ref_names), self.ref_lens.copy()
-        for f in ("tid", "pos", "end", "flag", "mapq", "l_seq", "n_cigar", "mate_tid", "mate_pos", "name_len",
+        for f in ("tid", "pos", "end", "flag", "mapq", "l_seq", "n_cigar", "mate_tid", "mate_pos", "tlen", "name_len",
                   "aux_len"):
             setattr(t, f, np.zeros(0, np.int32))
         for f in ("name_off", "cig_off", "seq_off", "qual_off", "aux_off"):

@@ -11,7 +11,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 import time
-from typing import Optional, Tuple
+from typing import Dict, Optional, Tuple
 
 import numpy as np
 
@@ -37,6 +37,10 @@ _new_bytes.argtypes = [C.c_void_p, C.c_ssize_t]
 _i32p = C.POINTER(C.c_int32)
 _i64p = C.POINTER(C.c_int64)
 _u8p = C.POINTER(C.c_uint8)
+# ganon_bam_cols member order (include/ganon.h)
+BAM_I32_COLS = ("tid", "pos", "end", "flag", "mapq", "l_seq", "n_cigar", "mate_tid", "mate_pos", "tlen", "name_len",
+                "aux_len")
+BAM_I64_COLS = ("name_off", "cig_off", "seq_off", "qual_off", "aux_off", "rec_off")
 _u32p = C.POINTER(C.c_uint32)
 
 
@@ -191,6 +195,11 @@ def hip_lib():
     lib.ganon_indel_free.argtypes = [_p, _p]
     lib.ganon_inflate.argtypes = [_p, _u8p, C.c_int64, _i64p, _i32p, _i64p, _i32p, C.c_int64, _u8p, C.c_int64,
                                   _i64p]
+    lib.ganon_inflate_device_output.argtypes = [_p, C.POINTER(_p), _i64p]
+    lib.ganon_bam_columns.argtypes = [_p, _p, C.c_int64, C.c_int64, C.c_int, C.POINTER(_p)]
+    lib.ganon_bam_dcols_get.argtypes = [_p, C.POINTER(BamCols), _i64p]
+    lib.ganon_bam_dcols_download.argtypes = [_p, _p, C.POINTER(BamCols)]
+    lib.ganon_bam_dcols_free.argtypes = [_p, _p]
     if lib.ganon_abi_version() != 4:
         raise GanonError("libganon_hip.so ABI version mismatch")
     _hip = lib
@@ -224,7 +233,8 @@ EXPORTED_HIP_SYMBOLS = (
     "ganon_fastq_upload", "ganon_fastq_run", "ganon_fastq_bytes", "ganon_fastq_device_output",
     "ganon_fastq_download", "ganon_fastq_free", "ganon_fastq_format_hip",
     "ganon_indel_upload", "ganon_indel_run", "ganon_indel_download", "ganon_indel_info", "ganon_indel_free",
-    "ganon_inflate", "ganon_inflate_hostcb",
+    "ganon_inflate", "ganon_inflate_hostcb", "ganon_inflate_device_output",
+    "ganon_bam_columns", "ganon_bam_dcols_get", "ganon_bam_dcols_download", "ganon_bam_dcols_free",
 )
 EXPORTED_HOST_SYMBOLS = (
     "ganon_bam_open", "ganon_bam_view_get", "ganon_bam_error", "ganon_bam_close",
@@ -243,6 +253,56 @@ EXPORTED_HOST_SYMBOLS = (
 
 def _ptr(a: np.ndarray, ty):
     return a.ctypes.data_as(ty) if a is not None else None
+
+
+class BamCols(C.Structure):
+    """Mirror of ``ganon_bam_cols`` (include/ganon.h): device pointers, or host arrays for a download."""
+    _fields_ = [("n_records", C.c_int64)] + [(f, _i32p) for f in BAM_I32_COLS] + [(f, _i64p) for f in BAM_I64_COLS] + [
+        ("names", _p), ("names_bytes", C.c_int64), ("cigar", _p), ("cigar_ops", C.c_int64),
+        ("seq", _p), ("seq_bytes", C.c_int64), ("qual", _p), ("qual_bytes", C.c_int64),
+        ("aux", _p), ("aux_bytes", C.c_int64)]
+
+
+def bam_columns_device(ctx, stream, p: int, n: int, on_host: bool) -> Tuple[Dict[str, np.ndarray], int]:
+    """``ganon_bam_columns`` on context ``ctx`` (a ``ganon_ctx`` handle): the records at stream[p, n)
+    decoded to columns on the device, downloaded as numpy arrays named as ``io.bam.ReadTable``'s
+    (blobs: names_blob, cigar, seq, qual, aux; plus rec_off). ``stream`` is a host uint8 array
+    (``on_host``) or a device address. Returns (columns, boundary fix rounds)."""
+    lib = hip_lib()
+    h = _p()
+    if on_host:
+        arr = np.ascontiguousarray(stream, np.uint8)
+        addr = arr.ctypes.data
+    else:
+        addr = int(stream)
+    rc = lib.ganon_bam_columns(ctx, _p(addr), int(p), int(n), 1 if on_host else 0, C.byref(h))
+    if rc != 0:
+        raise GanonError(f"ganon_bam_columns failed ({rc}): {lib.ganon_last_error(ctx).decode(errors='replace')}")
+    try:
+        dv = BamCols()
+        fixes = C.c_int64(0)
+        lib.ganon_bam_dcols_get(h, C.byref(dv), C.byref(fixes))
+        nr = int(dv.n_records)
+        cols: Dict[str, np.ndarray] = {}
+        hv = BamCols()
+        hv.n_records = nr
+        for f in BAM_I32_COLS:
+            cols[f] = np.empty(nr, np.int32)
+            setattr(hv, f, _ptr(cols[f], _i32p))
+        for f in BAM_I64_COLS:
+            cols[f] = np.empty(nr, np.int64)
+            setattr(hv, f, _ptr(cols[f], _i64p))
+        for f, key, dt, cnt in (("names", "names_blob", np.uint8, "names_bytes"), ("cigar", "cigar", np.uint32, "cigar_ops"),
+                                ("seq", "seq", np.uint8, "seq_bytes"), ("qual", "qual", np.uint8, "qual_bytes"),
+                                ("aux", "aux", np.uint8, "aux_bytes")):
+            cols[key] = np.empty(int(getattr(dv, cnt)), dt)
+            setattr(hv, f, _p(cols[key].ctypes.data))
+            setattr(hv, cnt, int(getattr(dv, cnt)))
+        if lib.ganon_bam_dcols_download(ctx, h, C.byref(hv)) != 0:
+            raise GanonError(f"ganon_bam_dcols_download failed: {lib.ganon_last_error(ctx).decode(errors='replace')}")
+        return cols, int(fixes.value)
+    finally:
+        lib.ganon_bam_dcols_free(ctx, h)
 
 
 class GpuInflater:
@@ -297,6 +357,22 @@ class GpuInflater:
             msg = self._lib.ganon_last_error(self._h).decode(errors="replace")
             raise GanonError(f"ganon_inflate failed ({rc}, block {int(bad[0])}): {msg}")
         return out
+
+    def device_output(self) -> Tuple[int, int]:
+        """(device address, bytes) of the last inflate's output, still on the device
+        (``ganon_inflate_device_output``): valid until the next ``inflate``."""
+        addr, nb = _p(), C.c_int64(0)
+        if self._lib.ganon_inflate_device_output(self._h, C.byref(addr), C.byref(nb)) != 0:
+            raise GanonError(self._lib.ganon_last_error(self._h).decode(errors="replace"))
+        return int(addr.value or 0), int(nb.value)
+
+    def bam_columns(self, p: int, n: int) -> Tuple[Dict[str, np.ndarray], int]:
+        """The BAM records at [p, n) of the last inflate's output, decoded to columns on the device
+        where the inflate left them (``ganon_bam_columns``, include/ganon.h)."""
+        addr, nb = self.device_output()
+        if not 0 <= p <= n <= nb:
+            raise GanonError(f"bam_columns: [{p}, {n}) outside the inflated {nb} bytes")
+        return bam_columns_device(self._h, addr, p, n, on_host=False)
 
     def close(self) -> None:
         if self._h:

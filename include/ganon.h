@@ -368,4 +368,43 @@ GANON_API int ganon_inflate_hostcb(void *ctx, const uint8_t *comp, int64_t comp_
                                    const int32_t *in_len, const int64_t *out_off, const int32_t *out_len,
                                    int64_t n_blocks, uint8_t *out, int64_t out_total);
 
+/* The device copy of the last successful ganon_inflate's output on this context (out_total bytes,
+ * block i at out_off[i]): valid until the context's next ganon_inflate. Lets the record walk below
+ * run on the inflated stream where it already lies. */
+GANON_API int ganon_inflate_device_output(ganon_ctx *ctx, const uint8_t **out, int64_t *bytes);
+
+/* ---- BAM records -> columns on the device (the record walk after the inflate) ----
+ * Replaces, for a stream the device holds, libganon_host.so's record walk (records_to_columns in
+ * csrc/ganon_host.cpp, the ganon_bam_view of include/ganon_host.h) — what the reference gets from
+ * htslib's bam_read1 behind AlignmentFile.fetch / pileup (pileup_io.pyx:12-17). The records lie back
+ * to back at stream[p, n) (p: the first record, after the BAM header); stream is a device pointer,
+ * or a host pointer with on_host = 1 (copied to the device first). The columns are those of
+ * ganon_bam_view, same values and blob layout (record order = stream order; name blob with one NUL
+ * per name; bam_endpos in `end`), plus rec_off = each record's offset in the stream; they stay in
+ * device memory, owned by the handle. Errors as the host decoder's: GANON_E_ARG on a bad record size
+ * or fields that exceed a record's block size. Since ABI 4 (round 5). */
+typedef struct ganon_bam_cols {
+  int64_t n_records;
+  int32_t *tid, *pos, *end, *flag, *mapq, *l_seq, *n_cigar, *mate_tid, *mate_pos, *tlen, *name_len, *aux_len;
+  int64_t *name_off, *cig_off, *seq_off, *qual_off, *aux_off, *rec_off;
+  char *names;
+  int64_t names_bytes;
+  uint32_t *cigar;
+  int64_t cigar_ops;
+  uint8_t *seq;
+  int64_t seq_bytes;
+  uint8_t *qual;
+  int64_t qual_bytes;
+  uint8_t *aux;
+  int64_t aux_bytes;
+} ganon_bam_cols;
+typedef struct ganon_bam_dcols ganon_bam_dcols;
+GANON_API int ganon_bam_columns(ganon_ctx *ctx, const uint8_t *stream, int64_t p, int64_t n, int on_host,
+                                ganon_bam_dcols **out);
+/* The device pointers and sizes; *fixes = the boundary check rounds that found a wrong guess. */
+GANON_API int ganon_bam_dcols_get(const ganon_bam_dcols *c, ganon_bam_cols *device_view, int64_t *fixes);
+/* Copy the columns to host arrays sized from ganon_bam_dcols_get's counts (NULL members skipped). */
+GANON_API int ganon_bam_dcols_download(ganon_ctx *ctx, const ganon_bam_dcols *c, const ganon_bam_cols *host);
+GANON_API int ganon_bam_dcols_free(ganon_ctx *ctx, ganon_bam_dcols *c);
+
 #endif /* GANON_H */

@@ -531,6 +531,8 @@ def main() -> None:
     ap.add_argument("--indel-tally", type=int, default=1, help="diagnostic: 0 leaves the germline indel tally out of "
                     "the step (the line then says so in step_kind; never the metric's setting)")
     ap.add_argument("--no-side-configs", action="store_true", help="skip the c3 / c5 lines (child runs)")
+    ap.add_argument("--no-bam-decode", action="store_true",
+                    help="skip the device BAM record walk line (tools/bam_cols_bench.py, a child run)")
     ap.add_argument("--e2e-contigs", type=int, default=24)
     ap.add_argument("--e2e-pairs", type=int, default=23_000, help="pairs per contig and sample")
     ap.add_argument("--e2e-cpu-contigs", type=int, default=4)
@@ -564,6 +566,10 @@ def main() -> None:
     if world == 1 and args.config == "c2" and not args.no_side_configs:
         stage("side configs (child bench runs)")
     side = side_config_lines(args) if world == 1 and args.config == "c2" and not args.no_side_configs else None
+    bam_decode = None
+    if world == 1 and args.config == "c2" and not args.no_bam_decode:
+        stage("device BAM record walk (child run)")
+        bam_decode = _child_json([sys.executable, os.path.join(REPO, "tools", "bam_cols_bench.py")], {}, 600)
     stage(f"{args.config}: generating {args.pipeline * args.batches} batches")
     import torch
     local = int(os.environ.get("LOCAL_RANK", 0))
@@ -895,6 +901,7 @@ def main() -> None:
                   "ms_per_step": round(indel_ms, 4)},
         "e2e": e2e.get("e2e"),
         "side_configs": side,
+        "bam_decode": bam_decode,
         "pcie_inclusive": pcie,
         "fastq": fastq,
         "totals": {k: int(v) for k, v in zip(native.TOTAL_NAMES, job_totals)},

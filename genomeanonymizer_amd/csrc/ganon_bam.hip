@@ -8,15 +8,15 @@
 //
 // Record boundaries. Record k + 1 starts 4 + block_size(k) bytes after record k: a chain that one
 // thread would walk at one dependent load per record. The stream [p, n) is cut into kChunk-byte
-// chunks; chunk c holds the records that start in [p + c kChunk, p + (c + 1) kChunk). One thread per
+// chunks; chunk c holds the records that start in [p + c kChunk, p + (c + 1) kChunk). A wave per
 // chunk guesses the chunk's first record start (the first offset from which kProbe chained records
 // look like BAM records: sizes, reference ids, name terminator, read length against the block size)
-// and walks the chain to the chunk's end: its record count and exit (the first start at or past the
+// and one lane walks the chain to the chunk's end: its record count and exit (the first start at or past the
 // chunk's end). The guesses are then proven: chunk 0 starts at p, and a chunk whose guess equals its
 // predecessor's exit holds exactly the true records when its predecessor does — so by induction every
 // chunk before the first failing one is exact. A failing chunk whose predecessor passed is walked
 // again from that predecessor's exit, and the host repeats check and fix until no chunk fails (each
-// round fixes at least the first failing chunk; none needed a fix on any BAM tried, see `fixes`).
+// round fixes at least the first failing run of chunks; `fixes` counts the failing chunks met).
 // The exact walk checks what the host decoder checks (block_size >= 32, the record inside the
 // stream), the per-record pass the rest (read length and CIGAR inside the block): same errors.
 //
@@ -42,24 +42,51 @@ using ganon_detail::fail;
 namespace {
 
 constexpr int kBamThreads = 256;
-constexpr int64_t kChunk = 4096;     // stream bytes per chunk (~12 short-read records)
+constexpr int64_t kChunk = 2048;     // stream bytes per chunk (~6 short-read records)
 constexpr int kProbe = 4;            // chained plausible records that make a guess
-constexpr int64_t kGuessSpan = 3 * kChunk;   // guess search window from the chunk start
+constexpr int64_t kGuessSpan = 2 * kChunk;   // guess search window from the chunk start
 
 __device__ __forceinline__ uint32_t rd32(const uint8_t *__restrict__ d, int64_t o) {
   return (uint32_t)d[o] | ((uint32_t)d[o + 1] << 8) | ((uint32_t)d[o + 2] << 16) | ((uint32_t)d[o + 3] << 24);
 }
 
+// 32 bits at any byte offset o of the stream [0, n) from the two aligned dwords that hold them
+// (alignbyte): half the load instructions of four byte loads — the guess and the walk are bound
+// by the texture path's per-instruction cost, not by bytes. Bytes near the stream's end, where the
+// second dword would pass it, are read one by one.
+__device__ __forceinline__ uint32_t ld32(const uint8_t *__restrict__ d, int64_t o, int64_t n) {
+  const int64_t a = o & ~(int64_t)3;
+  if (a + 8 > n) return rd32(d, o);
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(d + a);
+  return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(o & 3));
+}
+
 // Does a BAM record plausibly start at o? (guesses only: a wrong guess is caught by the check)
 __device__ __forceinline__ bool plausible(const uint8_t *__restrict__ d, int64_t o, int64_t n, int64_t &next) {
-  if (o + 36 > n) return false;
-  const int32_t bs = (int32_t)rd32(d, o);
+  if (o + 40 > n) {   // (the stream's last bytes: byte loads)
+    if (o + 36 > n) return false;
+  }
+  uint32_t h[9];   // block_size and the fixed fields, [o, o + 36)
+  if (o + 40 <= n) {
+    const int64_t a = o & ~(int64_t)3;
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(d + a);
+    uint32_t x[10];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) x[k] = w[k];
+    const uint32_t sh = (uint32_t)(o & 3);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) h[k] = __builtin_amdgcn_alignbyte(x[k + 1], x[k], sh);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) h[k] = rd32(d, o + 4 * k);
+  }
+  const int32_t bs = (int32_t)h[0];
   if (bs < 32 || o + 4 + (int64_t)bs > n) return false;
-  const int32_t tid = (int32_t)rd32(d, o + 4), pos = (int32_t)rd32(d, o + 8);
-  const int l_rn = d[o + 12];
-  const int ncig = (int)(d[o + 16] | (d[o + 17] << 8));
-  const int32_t lseq = (int32_t)rd32(d, o + 20);
-  const int32_t mtid = (int32_t)rd32(d, o + 24), mpos = (int32_t)rd32(d, o + 28);
+  const int32_t tid = (int32_t)h[1], pos = (int32_t)h[2];
+  const int l_rn = (int)(h[3] & 0xFF);
+  const int ncig = (int)(h[4] & 0xFFFF);
+  const int32_t lseq = (int32_t)h[5];
+  const int32_t mtid = (int32_t)h[6], mpos = (int32_t)h[7];
   if (tid < -1 || pos < -1 || mtid < -1 || mpos < -1 || l_rn < 1 || lseq < 0) return false;
   if (32 + (int64_t)l_rn + 4LL * ncig + ((int64_t)lseq + 1) / 2 + lseq > bs) return false;
   if (d[o + 4 + 32 + l_rn - 1] != 0) return false;
@@ -95,7 +122,7 @@ __device__ __forceinline__ void walk(const uint8_t *__restrict__ d, int64_t p, i
         b = 1;
         break;
       }
-      const int32_t bs = (int32_t)rd32(d, s);
+      const int32_t bs = (int32_t)ld32(d, s, n);
       if (bs < 32 || s + 4 + (int64_t)bs > n) {
         b = 2;
         break;
@@ -110,30 +137,41 @@ __device__ __forceinline__ void walk(const uint8_t *__restrict__ d, int64_t p, i
   K.bad[c] = b;
 }
 
-// mode 0: every chunk guesses its entry (chunk 0: p) and walks; mode 1: failing chunks whose
-// predecessor passed walk again from the predecessor's exit.
-__global__ void __launch_bounds__(kBamThreads) k_bam_walk(const uint8_t *__restrict__ d, int64_t p, int64_t n,
-                                                          int64_t n_chunks, Chunks K, int mode) {
-  const int64_t c = (int64_t)blockIdx.x * kBamThreads + threadIdx.x;
-  if (c >= n_chunks) return;
-  if (mode == 1) {
-    if (c == 0 || !K.flag[c] || K.flag[c - 1]) return;
-    walk(d, p, n, c, K.exitp[c - 1], K);
-    return;
-  }
+// Every chunk's guess and walk, a wave per chunk: the lanes test 64 consecutive candidate offsets at
+// once (their first loads coalesced: a thread per chunk testing one offset after another made the
+// byte loads of 64 lanes touch 64 cache lines apiece, 2.5 ms per 254 MB), the first plausible one
+// (ballot) is the guess, and lane 0 walks the chain.
+__global__ void __launch_bounds__(kBamThreads) k_bam_guess(const uint8_t *__restrict__ d, int64_t p, int64_t n,
+                                                           int64_t n_chunks, Chunks K) {
+  const int lane = threadIdx.x & 63;
+  const int64_t c = ((int64_t)blockIdx.x * kBamThreads + threadIdx.x) >> 6;
+  if (c >= n_chunks) return;   // (wave-uniform)
   int64_t e = -1;
   if (c == 0) {
     e = p;
   } else {
     const int64_t cs = p + c * kChunk, lim = min(n, cs + kGuessSpan);
-    for (int64_t o = cs; o < lim; ++o)
-      if (chain_plausible(d, o, n)) {
-        e = o;
+    for (int64_t o0 = cs; o0 < lim; o0 += 64) {
+      const int64_t o = o0 + lane;
+      const unsigned long long m = __ballot(o < lim && chain_plausible(d, o, n));
+      if (m) {
+        e = o0 + __builtin_ctzll(m);
         break;
       }
+    }
     if (e < 0 && lim == n) e = n;   // (no record starts in the rest of the stream: a guess too)
   }
-  walk(d, p, n, c, e, K);
+  if (lane == 0) walk(d, p, n, c, e, K);
+}
+
+// A run of failing chunks whose predecessor passed, walked again from the predecessor's exit chunk
+// after chunk by one thread (a long read's record covers several chunks that found no start: one
+// round for the run).
+__global__ void __launch_bounds__(kBamThreads) k_bam_fix(const uint8_t *__restrict__ d, int64_t p, int64_t n,
+                                                         int64_t n_chunks, Chunks K) {
+  const int64_t c = (int64_t)blockIdx.x * kBamThreads + threadIdx.x;
+  if (c >= n_chunks || c == 0 || !K.flag[c] || K.flag[c - 1]) return;
+  for (int64_t cc = c; cc < n_chunks && (cc == c || K.flag[cc]); ++cc) walk(d, p, n, cc, K.exitp[cc - 1], K);
 }
 
 __global__ void __launch_bounds__(kBamThreads) k_bam_check(int64_t n_chunks, Chunks K) {
@@ -161,7 +199,7 @@ __global__ void __launch_bounds__(kBamThreads) k_bam_offsets(const uint8_t *__re
   if (s < 0) return;
   while (s < ce) {
     rec[i++] = s;
-    s += 4 + (int64_t)(int32_t)rd32(d, s);
+    s += 4 + (int64_t)(int32_t)ld32(d, s, n);
   }
 }
 
@@ -197,10 +235,11 @@ __global__ void __launch_bounds__(kBamThreads) k_bam_sizes(const uint8_t *__rest
 
 struct ganon_bam_dcols {
   ganon_bam_cols v{};          // device pointers
-  void *block = nullptr;        // one allocation for the per-record columns
-  void *blobs = nullptr;        // one allocation for the blobs
+  void *block = nullptr;        // one block for the per-record columns
+  void *blobs = nullptr;        // one block for the blobs
   uint8_t *stream = nullptr;    // the device copy of a host stream (on_host)
-  int64_t fixes = 0;            // check/fix rounds that found failing chunks
+  size_t block_bytes = 0, blobs_bytes = 0, stream_bytes = 0;   // (context cache blocks)
+  int64_t fixes = 0;            // failing chunks met by the checks (summed over the rounds)
 };
 
 namespace {
@@ -224,15 +263,36 @@ __global__ void __launch_bounds__(kBamThreads) k_bam_scatter(const uint8_t *__re
     const uint8_t *r = d + o + 4;
     const int64_t o_name = V.name_off[i], o_cig = V.cig_off[i], o_seq = V.seq_off[i], o_qual = V.qual_off[i],
                   o_aux = V.aux_off[i];
-    // name (+ NUL when the record's own is missing)
-    for (int k = lane; k < l_rn; k += 64) V.names[o_name + k] = (char)r[32 + k];
-    if (lane == 0 && V.name_off[i + 1] - o_name > l_rn) V.names[o_name + l_rn] = 0;
-    int64_t q = 32 + l_rn;
-    // CIGAR words (bytes) and the reference length of M / D / N / = / X
-    for (int k = lane; k < 4 * ncig; k += 64) cig8[4 * o_cig + k] = r[q + k];
+    const int nseq = (int)(((int64_t)lseq + 1) / 2);
+    const int e_name = l_rn, e_cig = e_name + 4 * ncig, e_seq = e_cig + nseq, e_qual = e_seq + lseq;
+    const int body = bs - 32, na = body - e_qual;   // name .. aux: one byte stream, five blobs
+    // each blob's destination less its first body index (wave-uniform): a byte's destination is
+    // base[segment] + its body index
+    uint8_t *const d_name = reinterpret_cast<uint8_t *>(V.names) + o_name, *const d_cig = cig8 + 4 * o_cig - e_name,
+                   *const d_seq = V.seq + o_seq - e_cig, *const d_qual = V.qual + o_qual - e_seq,
+                   *const d_aux = V.aux + o_aux - e_qual;
+    // the body bytes, four loads in flight per lane before their stores
+    for (int k0 = 0; k0 < body; k0 += 4 * 64) {
+      uint8_t v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int k = k0 + 64 * u + lane;
+        v[u] = k < body ? r[32 + k] : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int k = k0 + 64 * u + lane;
+        if (k < body) {
+          uint8_t *base = k < e_name ? d_name : k < e_cig ? d_cig : k < e_seq ? d_seq : k < e_qual ? d_qual : d_aux;
+          base[k] = v[u];
+        }
+      }
+    }
+    if (lane == 0 && V.name_off[i + 1] - o_name > l_rn) V.names[o_name + l_rn] = 0;   // (a name without its NUL)
+    // the reference length of the M / D / N / = / X ops (bam_endpos)
     unsigned long long rl = 0;
     for (int k = lane; k < ncig; k += 64) {
-      const uint32_t w = rd32(r, q + 4LL * k);
+      const uint32_t w = rd32(r, 32 + e_name + 4LL * k);
       const int op = (int)(w & 0xF);
       if (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) rl += w >> 4;
     }
@@ -240,14 +300,6 @@ __global__ void __launch_bounds__(kBamThreads) k_bam_scatter(const uint8_t *__re
       const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)rl, s), hi = (uint32_t)__shfl_xor((int)(uint32_t)(rl >> 32), s);
       rl += ((unsigned long long)hi << 32) | lo;
     }
-    q += 4LL * ncig;
-    const int64_t nseq = ((int64_t)lseq + 1) / 2;
-    for (int64_t k = lane; k < nseq; k += 64) V.seq[o_seq + k] = r[q + k];
-    q += nseq;
-    for (int64_t k = lane; k < lseq; k += 64) V.qual[o_qual + k] = r[q + k];
-    q += lseq;
-    const int64_t na = bs - q;
-    for (int64_t k = lane; k < na; k += 64) V.aux[o_aux + k] = r[q + k];
     if (lane == 0) {
       const int64_t rlen = (flag & 4) ? 0 : (int64_t)rl;
       V.tid[i] = (int32_t)w32(4);
@@ -279,22 +331,23 @@ int columns(ganon_ctx *ctx, const uint8_t *d, int64_t p, int64_t n, ganon_bam_dc
   hipStream_t s = ctx->stream;
   const int64_t n_chunks = n > p ? (n - p + kChunk - 1) / kChunk : 0;
   int rc;
-  // chunk arrays and the scan's temporary space, one block
-  std::vector<void *> tmp;
+  // chunk arrays and the scans' temporary space from the context's block cache (stream-ordered
+  // reuse: no hipMalloc / hipFree, which synchronize, once a call of this size has run)
+  std::vector<std::pair<void *, size_t>> tmp;
   auto dalloc = [&](size_t bytes) -> void * {
     void *q = nullptr;
-    if (hipMalloc(&q, std::max<size_t>(bytes, 256)) != hipSuccess) return nullptr;
-    tmp.push_back(q);
+    size_t got = 0;
+    if (ctx_dmalloc(ctx, &q, std::max<size_t>(bytes, 256), &got) != hipSuccess) return nullptr;
+    tmp.emplace_back(q, got);
     return q;
   };
   struct Free {
-    std::vector<void *> &t;
-    hipStream_t s;
+    ganon_ctx *ctx;
+    std::vector<std::pair<void *, size_t>> &t;
     ~Free() {
-      if (!t.empty()) hipStreamSynchronize(s);
-      for (void *q : t) hipFree(q);
+      for (auto &q : t) ctx_dfree(ctx, q.first, q.second);
     }
-  } free_tmp{tmp, s};
+  } free_tmp{ctx, tmp};
   Chunks K{};
   int64_t *base = nullptr;
   if (n_chunks) {
@@ -309,10 +362,10 @@ int columns(ganon_ctx *ctx, const uint8_t *d, int64_t p, int64_t n, ganon_bam_dc
     if (!K.entry || !K.exitp || !K.cnt || !base || !K.bad || !K.flag || !K.info)
       return fail(ctx, GANON_E_DEVICE, "ganon_bam_columns: device allocation failed");
     {
-      ganon_detail::KernelScope ks(ctx, "k_bam_walk");
-      hipLaunchKernelGGL(k_bam_walk, dim3(grid_of(nc)), dim3(kBamThreads), 0, s, d, p, n, nc, K, 0);
+      ganon_detail::KernelScope ks(ctx, "k_bam_guess");
+      hipLaunchKernelGGL(k_bam_guess, dim3(grid_of(64 * nc)), dim3(kBamThreads), 0, s, d, p, n, nc, K);
     }
-    if ((rc = check_launch(ctx, "k_bam_walk"))) return rc;
+    if ((rc = check_launch(ctx, "k_bam_guess"))) return rc;
     for (int64_t round = 0;; ++round) {
       const unsigned long long init[3] = {0ull, ~0ull, ~0ull};
       unsigned long long info[3];
@@ -329,12 +382,12 @@ int columns(ganon_ctx *ctx, const uint8_t *d, int64_t p, int64_t n, ganon_bam_dc
         return fail(ctx, GANON_E_ARG, "ganon_bam_columns: bad record size (chunk %lld)", (long long)info[2]);
       if (info[0] == 0) break;
       if (round > nc) return fail(ctx, GANON_E_DEVICE, "ganon_bam_columns: record chain did not settle");
-      ++H->fixes;
+      H->fixes += (int64_t)info[0];
       {
-        ganon_detail::KernelScope ks(ctx, "k_bam_walk_fix");
-        hipLaunchKernelGGL(k_bam_walk, dim3(grid_of(nc)), dim3(kBamThreads), 0, s, d, p, n, nc, K, 1);
+        ganon_detail::KernelScope ks(ctx, "k_bam_fix");
+        hipLaunchKernelGGL(k_bam_fix, dim3(grid_of(nc)), dim3(kBamThreads), 0, s, d, p, n, nc, K);
       }
-      if ((rc = check_launch(ctx, "k_bam_walk_fix"))) return rc;
+      if ((rc = check_launch(ctx, "k_bam_fix"))) return rc;
     }
     HIP_OR_FAIL(hipMemsetAsync(K.cnt + nc, 0, 8, s));
     size_t tb = 0;
@@ -354,7 +407,7 @@ int columns(ganon_ctx *ctx, const uint8_t *d, int64_t p, int64_t n, ganon_bam_dc
   {
     const int64_t m = nr + 1;
     const int64_t bytes = 12 * (((m * 4) + 255) / 256 * 256) + 11 * (((m * 8) + 255) / 256 * 256);
-    if (hipMalloc(&H->block, (size_t)std::max<int64_t>(bytes, 256)) != hipSuccess)
+    if (ctx_dmalloc(ctx, &H->block, (size_t)std::max<int64_t>(bytes, 256), &H->block_bytes) != hipSuccess)
       return fail(ctx, GANON_E_DEVICE, "ganon_bam_columns: device allocation of %lld bytes failed", (long long)bytes);
     uint8_t *at = static_cast<uint8_t *>(H->block);
     for (int32_t **f : {&V.tid, &V.pos, &V.end, &V.flag, &V.mapq, &V.l_seq, &V.n_cigar, &V.mate_tid, &V.mate_pos, &V.tlen,
@@ -407,7 +460,7 @@ int columns(ganon_ctx *ctx, const uint8_t *d, int64_t p, int64_t n, ganon_bam_dc
   {
     const int64_t rb = ((V.names_bytes + 255) / 256 + (4 * V.cigar_ops + 255) / 256 + (V.seq_bytes + 255) / 256 +
                         (V.qual_bytes + 255) / 256 + (V.aux_bytes + 255) / 256) * 256;
-    if (hipMalloc(&H->blobs, (size_t)std::max<int64_t>(rb, 256)) != hipSuccess)
+    if (ctx_dmalloc(ctx, &H->blobs, (size_t)std::max<int64_t>(rb, 256), &H->blobs_bytes) != hipSuccess)
       return fail(ctx, GANON_E_DEVICE, "ganon_bam_columns: device allocation of %lld bytes failed", (long long)rb);
     uint8_t *at = static_cast<uint8_t *>(H->blobs);
     V.names = carve<char>(at, V.names_bytes);
@@ -425,11 +478,11 @@ int columns(ganon_ctx *ctx, const uint8_t *d, int64_t p, int64_t n, ganon_bam_dc
   return ganon_batch_sync(ctx);   // (collects the kernel times when profiling)
 }
 
-void release(ganon_bam_dcols *H) {
+void release(ganon_ctx *ctx, ganon_bam_dcols *H) {
   if (!H) return;
-  hipFree(H->block);
-  hipFree(H->blobs);
-  hipFree(H->stream);
+  ctx_dfree(ctx, H->block, H->block_bytes);
+  ctx_dfree(ctx, H->blobs, H->blobs_bytes);
+  ctx_dfree(ctx, H->stream, H->stream_bytes);
   delete H;
 }
 
@@ -439,18 +492,30 @@ GANON_API int ganon_bam_columns(ganon_ctx *ctx, const uint8_t *stream, int64_t p
                                 ganon_bam_dcols **out) {
   if (!ctx || !out || p < 0 || n < p || (n > 0 && !stream))
     return fail(ctx, GANON_E_ARG, "ganon_bam_columns: bad arguments");
+  if (!on_host && (reinterpret_cast<uintptr_t>(stream) & 3))   // (the walks read aligned dwords)
+    return fail(ctx, GANON_E_ARG, "ganon_bam_columns: a device stream must be 4-byte aligned");
   *out = nullptr;
   if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, GANON_E_DEVICE, "hipSetDevice failed");
+  if (ctx->profiling) {   // a profiled call: ganon_last_kernel_times reports this call's kernels alone
+    hipStreamSynchronize(ctx->stream);
+    for (auto &r : ctx->recs) {
+      ctx->pool.push_back(r.e0);
+      ctx->pool.push_back(r.e1);
+    }
+    ctx->recs.clear();
+  }
   auto *H = new ganon_bam_dcols();
   const uint8_t *d = stream;
   if (on_host && n > 0) {
-    if (hipMalloc(&H->stream, (size_t)n) != hipSuccess) {
-      release(H);
+    if (ctx_dmalloc(ctx, reinterpret_cast<void **>(&H->stream), (size_t)n, &H->stream_bytes) != hipSuccess) {
+      release(ctx, H);
       return fail(ctx, GANON_E_DEVICE, "ganon_bam_columns: device allocation of %lld bytes failed", (long long)n);
     }
-    if (hipMemcpyAsync(H->stream, stream, (size_t)n, hipMemcpyHostToDevice, ctx->stream) != hipSuccess) {
+    // (waited for: the kernel events that follow time the record walk, not the copy)
+    if (hipMemcpyAsync(H->stream, stream, (size_t)n, hipMemcpyHostToDevice, ctx->stream) != hipSuccess ||
+        hipStreamSynchronize(ctx->stream) != hipSuccess) {
       hipStreamSynchronize(ctx->stream);
-      release(H);
+      release(ctx, H);
       return fail(ctx, GANON_E_DEVICE, "ganon_bam_columns: stream copy failed");
     }
     d = H->stream;
@@ -458,7 +523,7 @@ GANON_API int ganon_bam_columns(ganon_ctx *ctx, const uint8_t *stream, int64_t p
   const int rc = columns(ctx, d, p, n, H);
   if (rc) {
     hipStreamSynchronize(ctx->stream);
-    release(H);
+    release(ctx, H);
     return rc;
   }
   *out = H;
@@ -501,6 +566,6 @@ GANON_API int ganon_bam_dcols_download(ganon_ctx *ctx, const ganon_bam_dcols *c,
 
 GANON_API int ganon_bam_dcols_free(ganon_ctx *ctx, ganon_bam_dcols *c) {
   if (ctx) hipStreamSynchronize(ctx->stream);
-  release(c);
+  release(ctx, c);
   return GANON_OK;
 }

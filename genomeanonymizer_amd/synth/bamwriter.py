@@ -208,3 +208,24 @@ def write_vcf(path: str, contigs: Sequence[Tuple[str, int]],
         fh.write("#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\n")
         for c, p, i, r, a in records:
             fh.write(f"{c}\t{p}\t{i}\t{r}\t{a}\t.\tPASS\t.\n")
+
+
+def first_record_offset(d: bytes) -> int:
+    """Offset of the first record of an inflated BAM stream (after magic, header text and the
+    reference list, SAM spec §4.2)."""
+    if d[:4] != b"BAM\x01":
+        raise ValueError("not an inflated BAM stream")
+    p = 8 + int.from_bytes(d[4:8], "little")
+    n_ref = int.from_bytes(d[p:p + 4], "little")
+    p += 4
+    for _ in range(n_ref):
+        p += 4 + int.from_bytes(d[p:p + 4], "little") + 4
+    return p
+
+
+def write_bgzf(path: str, data: bytes, level: int = 6) -> None:
+    """``data`` as a BGZF file (level 0: stored blocks)."""
+    w = BgzfWriter(path, level)
+    w.write(data)
+    w.close()
+

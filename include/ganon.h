@@ -377,8 +377,8 @@ GANON_API int ganon_inflate_device_output(ganon_ctx *ctx, const uint8_t **out, i
  * Replaces, for a stream the device holds, libganon_host.so's record walk (records_to_columns in
  * csrc/ganon_host.cpp, the ganon_bam_view of include/ganon_host.h) — what the reference gets from
  * htslib's bam_read1 behind AlignmentFile.fetch / pileup (pileup_io.pyx:12-17). The records lie back
- * to back at stream[p, n) (p: the first record, after the BAM header); stream is a device pointer,
- * or a host pointer with on_host = 1 (copied to the device first). The columns are those of
+ * to back at stream[p, n) (p: the first record, after the BAM header); stream is a 4-byte aligned
+ * device pointer, or a host pointer with on_host = 1 (copied to the device first). The columns are those of
  * ganon_bam_view, same values and blob layout (record order = stream order; name blob with one NUL
  * per name; bam_endpos in `end`), plus rec_off = each record's offset in the stream; they stay in
  * device memory, owned by the handle. Errors as the host decoder's: GANON_E_ARG on a bad record size
@@ -401,10 +401,11 @@ typedef struct ganon_bam_cols {
 typedef struct ganon_bam_dcols ganon_bam_dcols;
 GANON_API int ganon_bam_columns(ganon_ctx *ctx, const uint8_t *stream, int64_t p, int64_t n, int on_host,
                                 ganon_bam_dcols **out);
-/* The device pointers and sizes; *fixes = the boundary check rounds that found a wrong guess. */
+/* The device pointers and sizes; *fixes = the stream chunks whose first record start was guessed wrong. */
 GANON_API int ganon_bam_dcols_get(const ganon_bam_dcols *c, ganon_bam_cols *device_view, int64_t *fixes);
 /* Copy the columns to host arrays sized from ganon_bam_dcols_get's counts (NULL members skipped). */
 GANON_API int ganon_bam_dcols_download(ganon_ctx *ctx, const ganon_bam_dcols *c, const ganon_bam_cols *host);
+/* (with the context that made it: its device blocks return to that context's cache) */
 GANON_API int ganon_bam_dcols_free(ganon_ctx *ctx, ganon_bam_dcols *c);
 
 #endif /* GANON_H */

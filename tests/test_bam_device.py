@@ -21,14 +21,8 @@ BLOBS = ("names_blob", "cigar", "seq", "qual", "aux")
 
 
 def first_record(d: bytes) -> int:
-    """Offset of the first record of an inflated BAM stream (after magic, text and references)."""
-    assert d[:4] == b"BAM\x01"
-    p = 8 + int.from_bytes(d[4:8], "little")
-    n_ref = int.from_bytes(d[p:p + 4], "little")
-    p += 4
-    for _ in range(n_ref):
-        p += 4 + int.from_bytes(d[p:p + 4], "little") + 4
-    return p
+    from genomeanonymizer_amd.synth.bamwriter import first_record_offset
+    return first_record_offset(d)
 
 
 def inflated(path: str):
@@ -89,10 +83,8 @@ def adversarial_stream(seed: int = 5, n: int = 3000) -> bytes:
 
 
 def write_raw_bam(path: str, stream: bytes, level: int = 1) -> None:
-    from genomeanonymizer_amd.synth.bamwriter import BgzfWriter
-    w = BgzfWriter(path, level)
-    w.write(stream)
-    w.close()
+    from genomeanonymizer_amd.synth.bamwriter import write_bgzf
+    write_bgzf(path, stream, level)
 
 
 def test_first_record_offset_and_adversarial_stream_decode_on_host(tmp_path):

@@ -244,76 +244,119 @@ struct ganon_bam_dcols {
 
 namespace {
 
-__global__ void __launch_bounds__(kBamThreads) k_bam_scatter(const uint8_t *__restrict__ d, const int64_t *__restrict__ rec,
-                                                             int64_t nr, ganon_bam_cols V) {
-  const int lane = threadIdx.x & 63;
-  const int64_t nw = (int64_t)gridDim.x * (kBamThreads / 64);
+// Record i's columns and blob bytes, by one wave; src(k) = byte k of the record (its block_size
+// field first), from global memory or from the block's LDS copy.
+template <class Src>
+__device__ __forceinline__ void scatter_record(const ganon_bam_cols &V, int64_t i, int lane, Src src) {
   uint8_t *cig8 = reinterpret_cast<uint8_t *>(V.cigar);
-  for (int64_t i = ((int64_t)blockIdx.x * kBamThreads + threadIdx.x) >> 6; i < nr; i += nw) {
+  const int hb = lane < 36 ? (int)src(lane) : 0;   // block_size + the fixed fields
+  auto b = [&](int k) { return (uint32_t)__builtin_amdgcn_readlane(hb, k) & 0xFFu; };
+  auto w32 = [&](int k) { return b(k) | (b(k + 1) << 8) | (b(k + 2) << 16) | (b(k + 3) << 24); };
+  const int32_t bs = (int32_t)w32(0);
+  const int l_rn = (int)b(12);
+  const int ncig = (int)(b(16) | (b(17) << 8));
+  const int flag = (int)(b(18) | (b(19) << 8));
+  const int32_t lseq = (int32_t)w32(20);
+  const int32_t pos = (int32_t)w32(8);
+  const int64_t o_name = V.name_off[i], o_cig = V.cig_off[i], o_seq = V.seq_off[i], o_qual = V.qual_off[i],
+                o_aux = V.aux_off[i];
+  const int nseq = (int)(((int64_t)lseq + 1) / 2);
+  const int e_name = l_rn, e_cig = e_name + 4 * ncig, e_seq = e_cig + nseq, e_qual = e_seq + lseq;
+  const int body = bs - 32, na = body - e_qual;   // name .. aux: one byte stream, five blobs
+  // each blob's destination less its first body index (wave-uniform): a byte's destination is
+  // base[segment] + its body index
+  uint8_t *const d_name = reinterpret_cast<uint8_t *>(V.names) + o_name, *const d_cig = cig8 + 4 * o_cig - e_name,
+                 *const d_seq = V.seq + o_seq - e_cig, *const d_qual = V.qual + o_qual - e_seq,
+                 *const d_aux = V.aux + o_aux - e_qual;
+  // the body bytes, four loads in flight per lane before their stores
+  for (int k0 = 0; k0 < body; k0 += 4 * 64) {
+    uint8_t v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = k0 + 64 * u + lane;
+      v[u] = k < body ? src(36 + k) : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = k0 + 64 * u + lane;
+      if (k < body) {
+        uint8_t *base = k < e_name ? d_name : k < e_cig ? d_cig : k < e_seq ? d_seq : k < e_qual ? d_qual : d_aux;
+        base[k] = v[u];
+      }
+    }
+  }
+  if (lane == 0 && V.name_off[i + 1] - o_name > l_rn) V.names[o_name + l_rn] = 0;   // (a name without its NUL)
+  // the reference length of the M / D / N / = / X ops (bam_endpos)
+  unsigned long long rl = 0;
+  for (int k = lane; k < ncig; k += 64) {
+    const int64_t q = 36 + e_name + 4LL * k;
+    const uint32_t w = (uint32_t)src(q) | ((uint32_t)src(q + 1) << 8) | ((uint32_t)src(q + 2) << 16) | ((uint32_t)src(q + 3) << 24);
+    const int op = (int)(w & 0xF);
+    if (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) rl += w >> 4;
+  }
+  for (int s = 32; s > 0; s >>= 1) {
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)rl, s), hi = (uint32_t)__shfl_xor((int)(uint32_t)(rl >> 32), s);
+    rl += ((unsigned long long)hi << 32) | lo;
+  }
+  if (lane == 0) {
+    const int64_t rlen = (flag & 4) ? 0 : (int64_t)rl;
+    V.tid[i] = (int32_t)w32(4);
+    V.pos[i] = pos;
+    V.end[i] = (int32_t)(pos + (rlen > 0 ? rlen : 1));
+    V.flag[i] = flag;
+    V.mapq[i] = (int)b(13);
+    V.l_seq[i] = lseq;
+    V.n_cigar[i] = ncig;
+    V.mate_tid[i] = (int32_t)w32(24);
+    V.mate_pos[i] = (int32_t)w32(28);
+    V.tlen[i] = (int32_t)w32(32);
+    V.name_len[i] = l_rn > 0 ? l_rn - 1 : 0;
+    V.aux_len[i] = (int32_t)na;
+  }
+}
+
+constexpr int kScatRecs = 16;      // records per workgroup (four per wave)
+constexpr int kStage = 16384;      // LDS bytes staged per workgroup
+
+// A wave per record. The workgroup's run of kScatRecs records (back to back in the stream) is first
+// copied to LDS with coalesced aligned dword loads, then each wave reads its record's bytes from
+// there (a byte per lane per instruction from global memory, BAM fields being unaligned, cost the
+// texture path as much as the stores); a run longer than the LDS copy reads global memory.
+__global__ void __launch_bounds__(kBamThreads) k_bam_scatter(const uint8_t *__restrict__ d, int64_t n,
+                                                             const int64_t *__restrict__ rec, int64_t nr,
+                                                             ganon_bam_cols V) {
+  __shared__ uint32_t stage[kStage / 4];
+  const int64_t i0 = (int64_t)blockIdx.x * kScatRecs;
+  if (i0 >= nr) return;
+  const int64_t i1 = min(nr, i0 + kScatRecs);
+  const int64_t s0 = rec[i0], s1 = i1 < nr ? rec[i1] : n;   // (records lie back to back up to n)
+  const int64_t a0 = s0 & ~(int64_t)3;
+  const bool fits = s1 - a0 <= kStage;
+  if (fits) {
+    const int nw = (int)((s1 - a0 + 3) >> 2);
+    for (int w = threadIdx.x; w < nw; w += kBamThreads) {
+      const int64_t a = a0 + 4LL * w;
+      uint32_t v;
+      if (a + 4 <= n) {
+        v = *reinterpret_cast<const uint32_t *>(d + a);
+      } else {
+        v = 0;
+        for (int k = 0; k < 4; ++k)
+          if (a + k < n) v |= (uint32_t)d[a + k] << (8 * k);
+      }
+      stage[w] = v;
+    }
+  }
+  __syncthreads();
+  const uint8_t *sb = reinterpret_cast<const uint8_t *>(stage);
+  const int lane = threadIdx.x & 63;
+  for (int64_t i = i0 + (threadIdx.x >> 6); i < i1; i += kBamThreads / 64) {
     const int64_t o = rec[i];
-    const int hb = lane < 36 ? (int)d[o + lane] : 0;   // block_size + the fixed fields
-    auto b = [&](int k) { return (uint32_t)__builtin_amdgcn_readlane(hb, k) & 0xFFu; };
-    auto w32 = [&](int k) { return b(k) | (b(k + 1) << 8) | (b(k + 2) << 16) | (b(k + 3) << 24); };
-    const int32_t bs = (int32_t)w32(0);
-    const int l_rn = (int)b(12);
-    const int ncig = (int)(b(16) | (b(17) << 8));
-    const int flag = (int)(b(18) | (b(19) << 8));
-    const int32_t lseq = (int32_t)w32(20);
-    const int32_t pos = (int32_t)w32(8);
-    const uint8_t *r = d + o + 4;
-    const int64_t o_name = V.name_off[i], o_cig = V.cig_off[i], o_seq = V.seq_off[i], o_qual = V.qual_off[i],
-                  o_aux = V.aux_off[i];
-    const int nseq = (int)(((int64_t)lseq + 1) / 2);
-    const int e_name = l_rn, e_cig = e_name + 4 * ncig, e_seq = e_cig + nseq, e_qual = e_seq + lseq;
-    const int body = bs - 32, na = body - e_qual;   // name .. aux: one byte stream, five blobs
-    // each blob's destination less its first body index (wave-uniform): a byte's destination is
-    // base[segment] + its body index
-    uint8_t *const d_name = reinterpret_cast<uint8_t *>(V.names) + o_name, *const d_cig = cig8 + 4 * o_cig - e_name,
-                   *const d_seq = V.seq + o_seq - e_cig, *const d_qual = V.qual + o_qual - e_seq,
-                   *const d_aux = V.aux + o_aux - e_qual;
-    // the body bytes, four loads in flight per lane before their stores
-    for (int k0 = 0; k0 < body; k0 += 4 * 64) {
-      uint8_t v[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int k = k0 + 64 * u + lane;
-        v[u] = k < body ? r[32 + k] : 0;
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int k = k0 + 64 * u + lane;
-        if (k < body) {
-          uint8_t *base = k < e_name ? d_name : k < e_cig ? d_cig : k < e_seq ? d_seq : k < e_qual ? d_qual : d_aux;
-          base[k] = v[u];
-        }
-      }
-    }
-    if (lane == 0 && V.name_off[i + 1] - o_name > l_rn) V.names[o_name + l_rn] = 0;   // (a name without its NUL)
-    // the reference length of the M / D / N / = / X ops (bam_endpos)
-    unsigned long long rl = 0;
-    for (int k = lane; k < ncig; k += 64) {
-      const uint32_t w = rd32(r, 32 + e_name + 4LL * k);
-      const int op = (int)(w & 0xF);
-      if (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) rl += w >> 4;
-    }
-    for (int s = 32; s > 0; s >>= 1) {
-      const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)rl, s), hi = (uint32_t)__shfl_xor((int)(uint32_t)(rl >> 32), s);
-      rl += ((unsigned long long)hi << 32) | lo;
-    }
-    if (lane == 0) {
-      const int64_t rlen = (flag & 4) ? 0 : (int64_t)rl;
-      V.tid[i] = (int32_t)w32(4);
-      V.pos[i] = pos;
-      V.end[i] = (int32_t)(pos + (rlen > 0 ? rlen : 1));
-      V.flag[i] = flag;
-      V.mapq[i] = (int)b(13);
-      V.l_seq[i] = lseq;
-      V.n_cigar[i] = ncig;
-      V.mate_tid[i] = (int32_t)w32(24);
-      V.mate_pos[i] = (int32_t)w32(28);
-      V.tlen[i] = (int32_t)w32(32);
-      V.name_len[i] = l_rn > 0 ? l_rn - 1 : 0;
-      V.aux_len[i] = (int32_t)na;
+    if (fits) {
+      const int base = (int)(o - a0);
+      scatter_record(V, i, lane, [&](int64_t k) { return sb[base + k]; });
+    } else {
+      scatter_record(V, i, lane, [&](int64_t k) { return d[o + k]; });
     }
   }
 }
@@ -471,8 +514,8 @@ int columns(ganon_ctx *ctx, const uint8_t *d, int64_t p, int64_t n, ganon_bam_dc
   }
   if (nr) {
     ganon_detail::KernelScope ks(ctx, "k_bam_scatter");
-    const unsigned grid = (unsigned)std::min<int64_t>((nr + 3) / 4, 1 << 16);
-    hipLaunchKernelGGL(k_bam_scatter, dim3(grid), dim3(kBamThreads), 0, s, d, V.rec_off, nr, V);
+    const unsigned grid = (unsigned)((nr + kScatRecs - 1) / kScatRecs);
+    hipLaunchKernelGGL(k_bam_scatter, dim3(grid), dim3(kBamThreads), 0, s, d, n, V.rec_off, nr, V);
   }
   if ((rc = check_launch(ctx, "k_bam_scatter"))) return rc;
   return ganon_batch_sync(ctx);   // (collects the kernel times when profiling)

@@ -203,3 +203,94 @@ def test_device_columns_errors_match_host(ctx, tmp_path):
     d = np.frombuffer(hdr + b"".join(good), np.uint8)
     cols, _ = native.bam_columns_device(ctx.handle, d, len(hdr), len(d), on_host=True)
     assert len(cols["pos"]) == 50
+
+
+def _walk_chunks(d: bytes, p: int, chunk: int, probe: int = 4, span: int = None):
+    """Host restatement of ganon_bam_columns' boundary proof (csrc/ganon_bam.hip: k_bam_guess,
+    k_bam_check, k_bam_fix) at a small chunk size: guesses, exact-by-induction check, run fixes.
+    Returns (record offsets, failing chunks met)."""
+    n = len(d)
+    span = span or 2 * chunk
+    i32 = lambda o: int.from_bytes(d[o:o + 4], "little", signed=True)
+
+    def plausible(o):
+        if o + 36 > n:
+            return None
+        bs = i32(o)
+        if bs < 32 or o + 4 + bs > n:
+            return None
+        tid, pos, l_rn = i32(o + 4), i32(o + 8), d[o + 12]
+        ncig = d[o + 16] | (d[o + 17] << 8)
+        lseq, mtid, mpos = i32(o + 20), i32(o + 24), i32(o + 28)
+        if min(tid, pos, mtid, mpos) < -1 or l_rn < 1 or lseq < 0:
+            return None
+        if 32 + l_rn + 4 * ncig + (lseq + 1) // 2 + lseq > bs or d[o + 4 + 32 + l_rn - 1] != 0:
+            return None
+        return o + 4 + bs
+
+    def chain(o):
+        for _ in range(probe):
+            if o >= n:
+                return True
+            o = plausible(o)
+            if o is None:
+                return False
+        return True
+
+    nc = (n - p + chunk - 1) // chunk
+    entry, exitp = [0] * nc, [0] * nc
+
+    def walk(c, e):
+        ce = min(n, p + (c + 1) * chunk)
+        s = e
+        while 0 <= s < ce:
+            s += 4 + i32(s)
+        entry[c], exitp[c] = e, (s if e >= 0 else -1)
+
+    for c in range(nc):
+        if c == 0:
+            e = p
+        else:
+            cs = p + c * chunk
+            lim = min(n, cs + span)
+            e = next((o for o in range(cs, lim) if chain(o)), n if lim == n else -1)
+        walk(c, e)
+    fixes = 0
+    while True:
+        flag = [c > 0 and (entry[c] < 0 or entry[c] != exitp[c - 1]) for c in range(nc)]
+        if not any(flag):
+            break
+        fixes += sum(flag)
+        for c in range(1, nc):
+            if flag[c] and not flag[c - 1]:
+                cc = c
+                while cc < nc and (cc == c or flag[cc]):
+                    walk(cc, exitp[cc - 1])
+                    cc += 1
+    recs = []
+    for c in range(nc):
+        ce = min(n, p + (c + 1) * chunk)
+        s = entry[c]
+        while 0 <= s < ce:
+            recs.append(s)
+            s += 4 + i32(s)
+    return recs, fixes
+
+
+def test_chunk_proof_restatement_finds_every_record():
+    """The boundary algorithm itself, on the host: wrong guesses (aux holding record chains, long
+    records, chunks without a record start) are all caught and fixed, and the records found are the
+    sequential walk's, for several chunk sizes."""
+    s = adversarial_stream(seed=11, n=250)
+    p = len(_header([("c1", 10**6), ("c2", 2 * 10**6), ("c3", 500)]))
+    seq, o = [], p
+    while o < len(s):
+        seq.append(o)
+        o += 4 + int.from_bytes(s[o:o + 4], "little", signed=True)
+    assert o == len(s)
+    total_fixes = 0
+    for chunk in (97, 256, 1024, 2048):
+        recs, fixes = _walk_chunks(s, p, chunk)
+        assert recs == seq, chunk
+        total_fixes += fixes
+    assert total_fixes > 0

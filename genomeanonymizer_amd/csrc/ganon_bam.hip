@@ -43,7 +43,8 @@ namespace {
 
 constexpr int kBamThreads = 256;
 constexpr int64_t kChunk = 2048;     // stream bytes per chunk (~6 short-read records)
-constexpr int kProbe = 4;            // chained plausible records that make a guess
+constexpr int kProbe = 2;            // chained plausible records that make a guess (4: 0.23 vs 0.18 ms per 254 MB,
+                                     // 506 vs 610 wrong guesses: each one costs a re-walk of a chunk, not a result)
 constexpr int64_t kGuessSpan = 2 * kChunk;   // guess search window from the chunk start
 
 __device__ __forceinline__ uint32_t rd32(const uint8_t *__restrict__ d, int64_t o) {

@@ -239,6 +239,14 @@ def fastq_bench(masker, db, arr, args, torch, rank: int) -> dict:
     head = f.download()[:64]   # also checks the error slot (no bad record)
     f.free()
     n = len(recs["seq_len"])
+    # HBM bytes of the format kernel from the newest PMC summary of this record count taken on these
+    # formatter sources (tools/gpu_pmc_fastq.sh -> tools/pmc_step.py ... fastq)
+    pmc, pmc_src, pmc_note = pmc_summary("fastq", n, kind="fastq")
+    fq_traffic = None
+    if pmc is not None:
+        fq_traffic = max((v.get("hbm_bytes_per_launch", 0) for k, v in pmc.get("kernels", {}).items()
+                          if k.startswith("k_fq_span") or k.startswith("k_fq_quad") or k.startswith("k_fq_format")),
+                         default=None)
     alg = fq_bytes(recs)
     fmt_k = kt.get("k_fq_format", [1, float("nan")])
     k_ms = fmt_k[1] / fmt_k[0]
@@ -265,7 +273,8 @@ def fastq_bench(masker, db, arr, args, torch, rank: int) -> dict:
         "roofline": {"bound": "hbm", "kernel": "k_fq_format", "achieved": round(k_alg / (k_ms * 1e-3) / 1e9, 1),
                      "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(k_alg / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
-                     "algorithmic_bytes_per_launch": k_alg, "avg_launch_ms": round(k_ms, 5)},
+                     "algorithmic_bytes_per_launch": k_alg, "avg_launch_ms": round(k_ms, 5),
+                     "traffic": fq_traffic, "traffic_source": pmc_src, "traffic_note": pmc_note},
         "cpu_host_formatter": {"value": round(host_rps, 1), "unit": "records/s", "cores": 1,
                                "kind": "host C++ (libganon_host.so ganon_fastq_format)",
                                "sample": f"first {m} records, {reps} passes"},
@@ -394,14 +403,28 @@ def e2e_lines(args) -> dict:
             env1 = {"E2E_RUNS": "1", "GANON_JOB_BP": "0"}
             one = _child_json([sys.executable, tool, cin, os.path.join(d, "chrom_one"), "stream"], env1, 900,
                               drop=("E2E_WORKERS",))
-            same = None
-            if "error" not in ch and "error" not in one:
-                def rd(p):   # (a sample without single ends writes no single-end file)
-                    return open(p, "rb").read() if os.path.exists(p) else None
-                same = all(rd(os.path.join(d, "chrom_out", f"{x}_stream{sfx}")) ==
-                           rd(os.path.join(d, "chrom_one", f"{x}_stream{sfx}"))
+            def rd(p):   # (a sample without single ends writes no single-end file)
+                return open(p, "rb").read() if os.path.exists(p) else None
+
+            def files_equal(a: str, b: str) -> bool:
+                return all(rd(os.path.join(d, a, f"{x}_stream{sfx}")) == rd(os.path.join(d, b, f"{x}_stream{sfx}"))
                            for x in ("tumor", "normal") for sfx in (".1.fastq", ".2.fastq", ".single_end.fastq"))
+            same = files_equal("chrom_out", "chrom_one") if "error" not in ch and "error" not in one else None
+            # the same input through the CPU pipeline (the C oracle masks on the host's cores, the indel
+            # restatement tallies, the host C++ formatter formats; verdict r05 item 1): the GPU run's files
+            # must equal it byte for byte — a shared planner or kernel bug of the two HIP runs cannot hide
+            orc, same_oracle = {}, None
+            if not args.no_e2e_oracle:
+                stage("e2e: chromosome-scale oracle leg (CPU)")
+                cores = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
+                wk = max(1, args.e2e_workers)
+                orc = _child_json([sys.executable, tool, cin, os.path.join(d, "chrom_oracle"), "stream"],
+                                  {"E2E_ENGINE": "oracle", "E2E_RUNS": "0", "E2E_WORKERS": str(wk),
+                                   "E2E_THREADS": str(max(1, cores // wk))}, 1200)
+                if "error" not in ch and "error" not in orc:
+                    same_oracle = files_equal("chrom_out", "chrom_oracle")
             o1 = one.get("stream", {})
+            oo = orc.get("stream", {})
             res["e2e"]["chromosome_scale"] = {
                 "value": cs.get("reads_per_s"), "unit": "reads/s", "bases_per_sec": cs.get("bases_per_s"),
                 "reads": cs.get("reads"), "workers": args.e2e_workers, "wall_s": cs.get("stages_s", {}).get("wall_s"),
@@ -410,6 +433,14 @@ def e2e_lines(args) -> dict:
                 "output_bytes": cs.get("output_bytes"), "jobs": cs.get("jobs"), "generate_s": round(cgen, 1),
                 "disk": ch.get("disk"),
                 "files_equal": same,
+                "files_equal_oracle": same_oracle,
+                "oracle_leg": {"what": "the same input through the CPU pipeline: the C oracle masking (oracle/ganon_oracle.c), "
+                                       "the indel restatement (oracle/indel_oracle.py) and the host C++ formatter, same "
+                                       "planner, same processes", "reads_per_s": oo.get("reads_per_s"),
+                               "wall_s": oo.get("stages_s", {}).get("wall_s"), "error": orc.get("error"),
+                               "skipped": bool(args.no_e2e_oracle)},
+                "cpu_us_per_read": round(cs["cpu_s"] / cs["reads"] * 1e6, 3) if cs.get("cpu_s") and cs.get("reads") else None,
+                "cores_busy": cs.get("cores_busy"),
                 "files_equal_against": {"what": "the same input in one process, contig mode (GANON_JOB_BP=0: one job "
                                                 "per contig), E2E_WORKERS unset", "reads_per_s": o1.get("reads_per_s"),
                                         "wall_s": o1.get("stages_s", {}).get("wall_s"),
@@ -423,6 +454,7 @@ def e2e_lines(args) -> dict:
             shutil.rmtree(cin, ignore_errors=True)
             shutil.rmtree(os.path.join(d, "chrom_out"), ignore_errors=True)
             shutil.rmtree(os.path.join(d, "chrom_one"), ignore_errors=True)
+            shutil.rmtree(os.path.join(d, "chrom_oracle"), ignore_errors=True)
         # the CPU path on a bounded sample (the first contigs)
         stage("e2e: the CPU pipeline")
         cpu_in = os.path.join(d, "cpu_in")
@@ -472,6 +504,77 @@ def side_config_lines(args) -> dict:
         out[name]["workload"] = r.get("config", {}).get("workload")
         out[name]["kernels_ms"] = {k: v.get("avg_ms") for k, v in r.get("pass", {}).get("kernels", {}).items()}
     return out
+
+
+def summary(r: dict) -> dict:
+    """The line's headline figures in a few hundred bytes: the metric's step and its roofline, the
+    side configs, the formatter, the device record walk, the end-to-end lines with their parity flags
+    and the CPU baseline (every figure also sits, with its details, earlier in the line)."""
+    def short(msg):
+        return msg[-200:] if isinstance(msg, str) else msg
+
+    def rf(x):
+        x = x or {}
+        dm = x.get("dominant") or {}
+        return {"frac": x.get("frac"), "dominant": dm.get("kernel"), "dominant_frac": dm.get("frac"),
+                "traffic": x.get("traffic"), "traffic_source": x.get("traffic_source")}
+    out = {"c2": {"value": r.get("value"), "ms_per_step": r.get("ms_per_step"), "roofline": rf(r.get("roofline"))}}
+    for k, v in (r.get("side_configs") or {}).items():
+        out[k] = {"error": v["error"][:200]} if "error" in v else \
+            {"value": v.get("value"), "ms_per_step": v.get("ms_per_step"), "roofline": rf(v.get("roofline"))}
+    fq = r.get("fastq") or {}
+    if fq:
+        fr = fq.get("roofline", {})
+        out["fastq"] = {"ms_per_run": fq.get("ms_per_run"), "kernel_ms": fr.get("avg_launch_ms"), "frac": fr.get("frac"),
+                        "traffic": fr.get("traffic"), "traffic_source": fr.get("traffic_source")}
+    bd = r.get("bam_decode") or {}
+    if bd:
+        out["bam_decode"] = {"records_per_s": bd.get("value"), "device_ms": bd.get("device_ms"),
+                             "columns_equal_host_decoder": bd.get("columns_equal_host_decoder"), "error": short(bd.get("error"))}
+    e = r.get("e2e") or {}
+    if e:
+        out["e2e"] = {"value": e.get("value"), "files_equal_whole_sample": e.get("files_equal_whole_sample"),
+                      "error": short(e.get("error"))}
+        c = e.get("chromosome_scale") or {}
+        if c:
+            out["e2e_chromosome_scale"] = {"value": c.get("value"), "reads": c.get("reads"), "wall_s": c.get("wall_s"),
+                                           "files_equal": c.get("files_equal"),
+                                           "files_equal_oracle": c.get("files_equal_oracle"),
+                                           "cpu_us_per_read": c.get("cpu_us_per_read"), "error": short(c.get("error")),
+                                           "oracle_error": short((c.get("oracle_leg") or {}).get("error"))}
+    cb = r.get("cpu_baseline") or {}
+    if cb:
+        out["cpu_baseline"] = {"value": cb.get("value"), "cores": cb.get("cores"),
+                               "single_core_value": cb.get("single_core_value"),
+                               "e2e_value": (cb.get("e2e") or {}).get("value")}
+    return out
+
+
+def pmc_summary(config: str, reads: int, explicit: str = None, kind: str = "mask"):
+    """The newest PMC summary under profiles/ of this config and size whose kernel-sources digest
+    (genomeanonymizer_amd.build.sources_digest, recorded by tools/pmc_step.py) equals the sources this
+    bench runs: PMC bytes of older kernels are not cited. Returns (summary, path, note)."""
+    import glob
+    from genomeanonymizer_amd.build import sources_digest
+    want = sources_digest(kind)
+    name = f"pmc_step_{config}.json" if kind == "mask" else f"pmc_{config}.json"
+    paths = [explicit] if explicit else sorted(glob.glob(os.path.join(REPO, "profiles", "r*", name)), reverse=True)
+    note = f"no PMC summary of {config} at {reads} under profiles/"
+    for p in paths:
+        try:
+            pmc = json.load(open(p))
+        except (OSError, ValueError):
+            continue
+        if pmc.get("config") != config or pmc.get("reads") != reads:
+            continue
+        rel = os.path.relpath(p, REPO)
+        if pmc.get("sources_digest") != want:
+            if note.startswith("no PMC"):
+                note = (f"{rel} was taken on other kernel sources (digest {pmc.get('sources_digest')}, this build "
+                        f"{want}): not cited")
+            continue
+        return pmc, rel, None
+    return None, None, note
 
 
 _STAGE = ["start", time.time()]
@@ -543,13 +646,15 @@ def main() -> None:
                     help="pairs per contig and sample of the chromosome-scale end-to-end line (2 contigs of "
                          "--e2e-chrom-len; default 30x per sample, configs[2] density; 0: skip)")
     ap.add_argument("--e2e-chrom-len", type=int, default=20_000_000)
+    ap.add_argument("--no-e2e-oracle", action="store_true",
+                    help="skip the chromosome-scale line's CPU-oracle leg (files_equal_oracle)")
     ap.add_argument("--e2e-workers", type=int, default=8,
                     help="processes sharing the GPU in the end-to-end line (the multi-rank path over gloo)")
     ap.add_argument("--resident", action="store_true",
                     help="round-2 step: run only, the plan made once at upload (not a fresh batch)")
     ap.add_argument("--pmc", default=None,
-                    help="PMC step summary (tools/pmc_step.py) for the traffic field; default "
-                         "profiles/r05 (else r04, r03)/pmc_step_<config>.json when present")
+                    help="PMC step summary (tools/pmc_step.py) for the traffic field; default the newest "
+                         "profiles/r*/pmc_step_<config>.json of this size taken on these kernel sources")
     args = ap.parse_args()
     for k, v in CONFIGS[args.config]["defaults"].items():
         if getattr(args, k) is None:
@@ -824,20 +929,11 @@ def main() -> None:
     alg_total = sum(algorithmic_bytes(a) for a in prof_arrs) // len(prof_arrs)
     achieved = alg_total / (pass_ms * 1e-3) / 1e9
     traffic = dom_traffic = None
-    # the newest round's PMC summary of this config and size (tools/gpu_pmc_r05.sh, r04, r03)
-    pmc_paths = [args.pmc] if args.pmc else [os.path.join(REPO, "profiles", r, f"pmc_step_{args.config}.json")
-                                             for r in ("r05", "r04", "r03")]
-    pmc_used = None
-    for pmc_path in pmc_paths:
-        if traffic is None and os.path.exists(pmc_path):
-            try:
-                pmc = json.load(open(pmc_path))
-                if pmc.get("reads") == args.reads and pmc.get("config") == args.config:
-                    traffic = pmc.get("step_hbm_bytes")
-                    dom_traffic = pmc.get("kernels", {}).get("k_group", {}).get("hbm_bytes_per_launch")
-                    pmc_used = os.path.relpath(pmc_path, REPO)
-            except Exception:
-                traffic = None
+    # the newest PMC summary of this config and size taken on these kernel sources (tools/pmc_step.py)
+    pmc, pmc_used, pmc_note = pmc_summary(args.config, args.reads, args.pmc)
+    if pmc is not None:
+        traffic = pmc.get("step_hbm_bytes")
+        dom_traffic = pmc.get("kernels", {}).get("k_group", {}).get("hbm_bytes_per_launch")
 
     reads_total = reads_timed * world
     value = reads_total / dt
@@ -866,7 +962,8 @@ def main() -> None:
                    "pipeline": args.pipeline},
         "roofline": {"bound": "hbm", "kernel": "step: " + " + ".join(per_kernel), "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                     "traffic": traffic, "traffic_source": pmc_used, "algorithmic_bytes_per_launch": alg_total,
+                     "traffic": traffic, "traffic_source": pmc_used, "traffic_note": pmc_note,
+                     "algorithmic_bytes_per_launch": alg_total,
                      "avg_launch_ms": round(pass_ms, 5),
                      "dominant": {"kernel": dom, "algorithmic_bytes_per_launch": dom_bytes,
                                   "avg_launch_ms": round(dom_ms, 5),
@@ -918,6 +1015,8 @@ def main() -> None:
     elif rank == 0:
         result["cpu_baseline"] = None
     if rank == 0:
+        # last: the compact figures a reader compares (a runner that keeps only the line's tail keeps these)
+        result["summary"] = summary(result)
         print(json.dumps(result), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -108,6 +108,28 @@ def build_oracle(force: bool = False) -> str:
     return ORACLE_LIB
 
 
+# the sources a PMC summary describes (tools/pmc_step.py, tools/fq_pmc_summary.py record their digest;
+# bench.py cites a summary only while the digest still matches: PMC bytes of older kernels are not
+# evidence for these)
+DIGEST_SOURCES = {
+    "mask": ("csrc/ganon_hip.hip", "csrc/ganon_prep.hip", "csrc/ganon_indel.hip", "csrc/ganon_ctx.h",
+             "csrc/ganon_batch.h", "../include/ganon.h"),
+    "fastq": ("csrc/ganon_fastq.hip", "csrc/ganon_ctx.h", "csrc/ganon_batch.h", "../include/ganon.h"),
+}
+
+
+def sources_digest(kind: str = "mask") -> str:
+    """sha256 over the kernel sources of ``kind`` (DIGEST_SOURCES), in a fixed order."""
+    import hashlib
+    h = hashlib.sha256()
+    for rel in DIGEST_SOURCES[kind]:
+        p = os.path.normpath(os.path.join(PKG, rel))
+        h.update(os.path.basename(p).encode() + b"\0")
+        with open(p, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def build_all(force: bool = False) -> None:
     build_host(force)
     build_oracle(force)

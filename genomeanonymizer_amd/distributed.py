@@ -81,6 +81,9 @@ def _world_key(dist):
 
 def take_side_group(dist, purpose: str):
     k, _ = _world_key(dist)
+    # groups cached under another (destroyed) world are released: they are never reused
+    for key in [x for x in _SIDE_GROUPS if x[1] != k]:
+        _SIDE_GROUPS.pop(key, None)
     hit = _SIDE_GROUPS.pop((purpose, k), None)
     return hit[0] if hit is not None else dist.new_group(backend="gloo")
 
@@ -258,12 +261,17 @@ class SecondaryExchange:
 
     def permit(self, job: int) -> List[bytes]:
         """Block until every job before ``job`` is decoded (on any rank); the names of the secondaries
-        of earlier jobs whose mate ``job`` reads. Raises when a rank failed first."""
+        of earlier jobs whose mate ``job`` reads. Raises when a rank failed first, when this rank's
+        receiver thread failed (it delivers its error), or after GANON_PERMIT_TIMEOUT seconds (1800)."""
         import time
         t0 = time.time()
+        limit = float(os.environ.get("GANON_PERMIT_TIMEOUT", "1800"))
         with self.cv:
             while job not in self.permits:
-                self.cv.wait()
+                left = limit - (time.time() - t0)
+                if left <= 0:
+                    raise RuntimeError(f"secondary exchange: no permit for job {job} after {limit:.0f} s")
+                self.cv.wait(left)
             v = self.permits.pop(job)
         self.wait_s += time.time() - t0
         if isinstance(v, str):
@@ -276,15 +284,29 @@ class SecondaryExchange:
             self.cv.notify_all()
 
     def _receive_permits(self) -> None:
-        for _ in self.mine:
-            self._deliver(self._recv(0, self.PERMIT))
+        got = set()
+        try:
+            for _ in self.mine:
+                msg = self._recv(0, self.PERMIT)
+                got.add(msg["job"])
+                self._deliver(msg)
+        except Exception as e:   # noqa: BLE001  (a daemon thread: its error must reach permit())
+            err = f"secondary exchange: receiving permits failed: {e!r}"
+            for j in self.mine:
+                if j not in got:
+                    self._deliver({"job": j, "err": err})
 
     # registry (rank 0)
     def _receive_reports(self, r: int, cnt: int) -> None:
-        for _ in range(cnt):
-            msg = self._recv(r, self.DECODED)
+        try:
+            for _ in range(cnt):
+                msg = self._recv(r, self.DECODED)
+                with self.reg_lock:
+                    self._on_report(msg)
+        except Exception as e:   # noqa: BLE001  (every job not permitted yet gets the error)
             with self.reg_lock:
-                self._on_report(msg)
+                self.failed = self.failed or f"secondary exchange: reports of rank {r} lost: {e!r}"
+                self._advance()
 
     def _on_report(self, msg: dict) -> None:   # (reg_lock held)
         if msg.get("err") is not None:
@@ -309,6 +331,11 @@ class SecondaryExchange:
                 msg = {"job": j, "names": sorted(nm for nm, src in self.by_mate.get(j, {}).items() if src < j)}
             if self.owner[j] == 0:
                 self._deliver(msg)
+            elif self.failed is not None:
+                try:    # (the transport may be what failed: the owner's receiver then fails on its own)
+                    self._send(msg, self.owner[j], self.PERMIT)
+                except Exception:   # noqa: BLE001
+                    pass
             else:
                 self._send(msg, self.owner[j], self.PERMIT)
 

@@ -33,7 +33,7 @@ import dataclasses
 import os
 import threading
 import time
-from concurrent.futures import Future, ThreadPoolExecutor
+from concurrent.futures import Future, ThreadPoolExecutor, wait
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -111,6 +111,15 @@ def _sample_pool():
 _INFLATERS: Dict[Tuple[int, int, int], "native.GpuInflater"] = {}   # (device, min blocks, sample) -> inflater
 
 
+def _map_samples(fn, readers) -> list:
+    """``fn`` over the samples' readers on the sample pool. Every call finishes before the first error
+    is raised: a failing sample must not leave the other sample's native read running inside a reader
+    (or an inflater context) that the failure path then closes or hands to the next run."""
+    futs = [_sample_pool().submit(fn, r) for r in readers]
+    wait(futs)
+    return [f.result() for f in futs]
+
+
 def _close_all(objs) -> None:
     for o in objs:
         o.close()
@@ -172,7 +181,7 @@ def decode_job(readers, spec: JobSpec, secondaries: "Optional[SecondaryIndex]" =
     # the two samples' BAMs are read at once (round 5: the decode thread bounded the 30x line's ranks;
     # each reader has its own threads and, with GPU inflate, its own inflater context; the native
     # reads drop the GIL)
-    both = _sample_pool().map if len(readers) == 2 and os.environ.get("GANON_DECODE_PAIR", "1") != "0" else map
+    both = _map_samples if len(readers) == 2 and os.environ.get("GANON_DECODE_PAIR", "1") != "0" else map
     if spec.region is None:
         tables = tuple(both(lambda r: r.contig(r.tid_of(spec.contig)), readers))
     else:
@@ -1299,6 +1308,15 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
             if coord_exc[0] is not None:   # rank 0 reports the coordinator's own error
                 failure = coord_exc[0]
         tails = {"coordinator_join": time.time() - t_tail}
+        if failure is None:
+            # every send of this rank has its receive on a clean run (rank 0's coordinator took every
+            # export before it joined; this rank's worker took every resolution): wait for them BEFORE the
+            # final gather, so that a failed drain is part of the gathered error state and every rank
+            # decides alike whether its side groups serve the next run
+            try:
+                link.drain()
+            except Exception as e:   # noqa: BLE001
+                failure = e
         err = repr(failure) if failure is not None else None
         t_tail = time.time()
         if xchg is not None:
@@ -1316,8 +1334,6 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
             if failure is not None:
                 raise failure
             raise RuntimeError(f"another rank failed: {errs[0]}")
-        if failure is None:
-            link.drain()
         # every rank ended cleanly: the side groups serve this process's next run (distributed.py)
         if dist is not None and world > 1:
             from .distributed import return_side_group

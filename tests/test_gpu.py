@@ -505,6 +505,51 @@ def test_hip_fastq_full_size_matches_host_formatter(masker, c2_full):
     assert got == want
 
 
+def test_hip_config2_indel_cigars_full_size_matches_oracle(oracle, hip_built):
+    """BASELINE configs[1] at full size with realistic CIGARs (the bench's c2id line: 10 M reads,
+    germline het deletions 0.1/kb and sequencing indels 1.5e-4/base, ~3 % of the reads aM dD/I bM),
+    through the multi-segment fused path plus the germline indel tally, exactly as the bench steps
+    it (upload, then speculative replans on a context that planned another batch in between), against
+    the C oracle (every byte, per-scope calls and bases) and the indel restatement (every record).
+    A parity bug of round 5 showed only at this size (runs crossing emptied sort segments)."""
+    import indel_oracle
+    from genomeanonymizer_amd import native
+    from genomeanonymizer_amd.synth.batch import config2_batch
+    arr, info = config2_batch(germline_del_per_kb=0.1, seq_indel_per_base=1.5e-4)
+    assert info["reads"] == 10_000_000 and info["indel_reads"] > 200_000
+    o_out, o_calls, o_bases, _ = oracle.mask(arr)
+    want_ind = native.indel_records_array(indel_oracle.indel_records(arr))
+    assert len(want_ind) > 1000 and o_calls.sum() > 0
+    small, _ = config2_batch(n_reads=150_000, genome=40_000_000, n_windows=12_000, n_germline=30_000, seed=77)
+    m = native.HipMasker(0)
+    try:
+        ref = m.upload_reference(arr["ref_nt16"])
+        db = m.upload({k: v for k, v in arr.items() if k != "ref_nt16"}, ref=ref)
+        other = m.upload(small)
+        assert db.shape()["prep_mode"] == "multi_segment_fused"
+        ind = db.indel_tally(arr)
+        for step in range(3):   # upload plan, then two fresh speculative replans after another batch's
+            if step:
+                other.replan()
+                other.run()
+                db.replan()
+            db.run()
+            ind.run()
+            out, calls, bases, tot = db.download()
+            got_ind = ind.download()
+            assert np.array_equal(calls, o_calls), step
+            assert np.array_equal(bases, o_bases), step
+            assert np.array_equal(out, o_out), step
+            assert tot[1] == bases.sum() and tot[2] == info["reads"], step
+            assert np.array_equal(got_ind, want_ind), step
+        ind.free()
+        other.free()
+        db.free()
+        ref.free()
+    finally:
+        m.close()
+
+
 @pytest.mark.parametrize("seed", [11, 12, 13])
 def test_hip_pipeline_matches_oracle_pipeline_on_random_scenarios(seed, tmp_path, hip_built):
     """Differential end-to-end check beyond the three golden scenarios: randomized samples with

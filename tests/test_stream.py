@@ -448,3 +448,27 @@ def test_four_ranks_24_contigs_exchange(tmp_path):
     four = _outputs((os.path.join(out, "tumor"), os.path.join(out, "normal")), paths["N"] + ".statistics.txt")
     assert four.pop("stats") == stats_one
     assert four == one
+
+
+def test_one_corrupt_sample_fails_cleanly_and_the_next_run_is_right(tmp_path):
+    """a job's tumor and normal BAMs are read at once on the sample pool. Only the tumor
+    BAM is corrupt, past the header (a BGZF block of its second contig): the run raises the reader's
+    inflate error once the normal sample's read of that job has finished (stream._map_samples waits for
+    both before raising, so the failure path never closes a reader a read is still inside), and the
+    next runs in the same process — the same sample pool — write equal files streamed and whole."""
+    from genomeanonymizer_amd import native
+    from genomeanonymizer_amd.synth.fastpair import make_pair
+    paths = make_pair(str(tmp_path / "in"), n_contigs=3, contig_len=400_000, pairs_per_contig=4_000, seed=3)
+    bad = dict(paths)
+    bad["T"] = str(tmp_path / "bad_tumor.bam")
+    data = bytearray(open(paths["T"], "rb").read())
+    assert len(data) > 2 << 20     # (the reader's header read takes the first MiB)
+    mid = len(data) * 6 // 10
+    data[mid:mid + 4096] = bytes(4096)
+    open(bad["T"], "wb").write(bytes(data))
+    shutil.copy(paths["T"] + ".bai", bad["T"] + ".bai")
+    with pytest.raises(native.GanonError, match="inflate|BGZF|block"):
+        _run(bad, str(tmp_path / "bad"), False)
+    whole = _run(paths, str(tmp_path / "whole"), True)
+    streamed = _run(paths, str(tmp_path / "stream"), False)
+    assert whole == streamed

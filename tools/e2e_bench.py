@@ -8,7 +8,7 @@ Prints one JSON line with per-stage seconds, reads/s, bases/s and the process's 
                                                              # (tools/e2e_data.py, synth/fastpair.py)
     E2E_ENGINE=oracle ...    # the CPU path: the C oracle (E2E_THREADS threads) masks, the host C++
                              # formatter formats (bench.py's CPU end-to-end baseline; test infrastructure)
-    E2E_RUNS=N ...           # timed runs per mode after one untimed warm run (default 1)
+    E2E_RUNS=N ...           # timed runs per mode after one untimed warm run (default 1; 0: one run only)
     E2E_PROFILE=PREFIX ...   # cProfile of the timed run of each mode -> PREFIX_<mode>.txt (main thread)
     GANON_PREFETCH=N ...     # look-ahead planning threads of the streamed path (0: in line)
     E2E_DECODE_THREADS=T ... # host decode threads per process (default 16 / E2E_WORKERS)
@@ -169,7 +169,7 @@ def main():
                     pstats.Stats(prof, stream=f).sort_stats("cumulative").print_stats(60)
                     pstats.Stats(prof, stream=f).sort_stats("tottime").print_stats(40)
             runs.append(tim)
-        timed = runs[1:]
+        timed = runs[1:] or runs   # (E2E_RUNS=0: the one run, a parity leg)
         best = min(timed, key=lambda t: t["wall_s"])
         bases = int(best.get("bases", 0))
         res[mode] = {"reads": best["reads"], "bases": bases, "jobs": best.get("jobs"),

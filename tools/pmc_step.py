@@ -8,12 +8,13 @@ MI355X_MICROARCH.md). Kernels are matched to bench.py's names by substring. ``st
 bench's ``roofline.traffic``) sums the kernels of one step: device prep, group kernel, finish and the
 indel tally, each at its launches per step.
 
-usage: pmc_step.py TAG CONFIG READS OUT.json
+usage: pmc_step.py TAG CONFIG READS OUT.json      (CONFIG fastq: the formatter's kernels, READS = records)
 """
 import collections
 import csv
 import glob
 import json
+import os
 import re
 import sys
 
@@ -60,7 +61,11 @@ def main():
         kern[k][c] = v / n[(k, c)]
     # launches per step from the kernel trace (the PMC runs use --steps 3 --warmup 1 = 4 runs + 1 for
     # the profiled pass, so counts per launch are means; launches per step from the stats run)
-    res = {"config": config, "reads": reads, "kernels": {}}
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from genomeanonymizer_amd.build import sources_digest
+    # the kernels these counters describe: bench.py cites the summary only while the digest matches
+    kind = "fastq" if config == "fastq" else "mask"   # (fastq: tools/gpu_pmc_fastq.sh, the formatter's kernels)
+    res = {"config": config, "reads": reads, "sources_digest": sources_digest(kind), "kernels": {}}
     step = 0.0
     for k, vals in sorted(kern.items()):
         rd = 32 * vals.get("TCC_EA0_RDREQ_32B", 0) + 64 * vals.get("TCC_EA0_RDREQ_64B", 0) + \
@@ -70,7 +75,7 @@ def main():
         res["kernels"][k] = {"hbm_read_bytes_per_launch": int(rd), "hbm_write_bytes_per_launch": int(wr),
                              "hbm_bytes_per_launch": int(rd + wr), "fetch_size_kb": vals.get("FETCH_SIZE"),
                              "write_size_kb": vals.get("WRITE_SIZE"), "counters_per_launch": vals}
-        if k in STEP_KERNELS:
+        if (k.startswith("k_fq") if kind == "fastq" else k in STEP_KERNELS):
             step += rd + wr
     # the step's memsets: fills under 64 MB (the upload's output-buffer clear is ~0.75 GB) over the
     # group kernel's dispatches (one per step); the upload's small clears are counted too (an upper bound)
@@ -78,7 +83,8 @@ def main():
     res["memset_bytes_per_step"] = int(memset)
     step += memset
     res["step_hbm_bytes"] = int(step)
-    res["step_kernels"] = sorted(k for k in res["kernels"] if k in STEP_KERNELS)
+    res["step_kernels"] = sorted(k for k in res["kernels"]
+                                 if (k.startswith("k_fq") if kind == "fastq" else k in STEP_KERNELS))
     res["method"] = ("TCC_EA0_RDREQ_{32B,64B,128B} x size + TCC_EA0_WRREQ{,_64B}; three rocprofv3 --pmc passes "
                      "(tools/gpu_pmc_step.sh) over bench.py --steps 3, mean over dispatches; step = the kernels of "
                      "one fresh-batch step, replan + run + indel tally (step_kernels), one launch each, plus "

@@ -123,6 +123,34 @@ __device__ __forceinline__ uint64_t map_cell(int64_t g, int shift) {
 constexpr int kIndelWaves = 4;
 constexpr int kIndelThreads = 64 * kIndelWaves;
 
+// Bounds-checked builds (tools/build_variant.py ichk -DGANON_INDEL_CHECK=1; verdict r05 item 2): every
+// index a kernel of the tally dereferences is checked against its buffer's capacity first; a failing
+// check records its source line in g_indel_chk (first one wins) and the thread leaves instead of
+// touching memory, and ganon_indel_download reports the line. Default builds compile the checks away.
+#ifndef GANON_INDEL_CHECK
+#define GANON_INDEL_CHECK 0
+#endif
+// capacities the checks compare against: [0] observations, [1] read candidates, [2] records,
+// [3] reads, [4] scopes, [5] incidence blocks (list), [6] filtered incidences (ilist), [7] read blocks
+__device__ long long g_indel_cap[8];
+__device__ unsigned int g_indel_chk[2];   // [0] first failing line, [1] failures
+#if GANON_INDEL_CHECK
+#define ICHK_RET(cond, ...)                                   \
+  do {                                                        \
+    if (!(cond)) {                                            \
+      atomicCAS(&g_indel_chk[0], 0u, (unsigned int)__LINE__); \
+      atomicAdd(&g_indel_chk[1], 1u);                         \
+      return __VA_ARGS__;                                     \
+    }                                                         \
+  } while (0)
+#else
+#define ICHK_RET(cond, ...) \
+  do {                      \
+  } while (0)
+#endif
+#define ICHK(cond) ICHK_RET(cond)
+#define IN_CAP(i, k) ((long long)(i) >= 0 && (long long)(i) < g_indel_cap[k])
+
 __device__ __forceinline__ int nib(const uint8_t *__restrict__ seq, int64_t byte_off, int i) {
   const uint8_t b = seq[byte_off + (i >> 1)];
   return (i & 1) ? (b & 0xF) : (b >> 4);
@@ -180,6 +208,7 @@ __global__ void __launch_bounds__(kIndelThreads) k_indel_mark(const GanonReadVie
   const int64_t w = (int64_t)blockIdx.x * kIndelWaves + (threadIdx.x >> 6);
   if (w >= n_reads) return;
   const IndelRead e = reads[w];
+  ICHK(IN_CAP(e.read, 3));
   const uint32_t ds = V.dataset[e.read] & 1u;
   walk_block(V, e.read, e.k0, e.pos0, 0, lane, [&](const CigarStep (&c)[kWalkJ]) {
 #pragma unroll
@@ -216,6 +245,7 @@ __global__ void __launch_bounds__(kIndelThreads) k_indel_emit(const GanonReadVie
   if (w >= n_list) return;
   const IndelInc e = list[w];
   const int scope = (int)(e.scope_par & 0x7FFFFFFFu);
+  ICHK(IN_CAP(e.read, 3) && IN_CAP(scope, 4));
   const int span0 = V.span_start[scope];
   int64_t slot = e.obs_off;
   const unsigned long long below = (1ull << lane) - 1ull;
@@ -225,6 +255,7 @@ __global__ void __launch_bounds__(kIndelThreads) k_indel_emit(const GanonReadVie
       const unsigned long long m = __ballot(c[j].is_id);
       if (c[j].is_id) {
         const int64_t o = slot + __popcll(m & below);
+        ICHK(IN_CAP(o, 0));
         IndelObs ob;
         ob.read = e.read;
         ob.irp = c[j].irp;
@@ -253,6 +284,7 @@ __global__ void __launch_bounds__(kIndelThreads) k_indel_rcount(const GanonReadV
   const int64_t w = (int64_t)blockIdx.x * kIndelWaves + (threadIdx.x >> 6);
   if (w >= n_reads) return;
   const IndelRead e = reads[w];
+  ICHK(IN_CAP(e.read, 3));
   int total = 0;
   walk_block(V, e.read, e.k0, e.pos0, e.irp0, lane, [&](const CigarStep (&c)[kWalkJ]) {
     bool hit[kWalkJ];
@@ -281,6 +313,7 @@ __global__ void __launch_bounds__(kIndelThreads) k_indel_remit(const GanonReadVi
     for (int j = 0; j < kWalkJ; ++j) {
       const unsigned long long m_all = __ballot(c[j].is_id);
       const unsigned long long m = __ballot(keep[j]);
+      ICHK(!keep[j] || IN_CAP(slot + __popcll(m & below), 1));
       if (keep[j])
         rcand[slot + __popcll(m & below)] = IndelCand{c[j].pos, c[j].irp, (c[j].len << 1) | (c[j].op == 1 ? 1 : 0),
                                                       ord + (int)__popcll(m_all & below)};
@@ -296,6 +329,7 @@ __global__ void k_indel_icount(const IndelIncR *__restrict__ inc, int64_t n_inc,
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i >= n_inc) return;
   const IndelIncR e = inc[i];
+  ICHK(e.rfirst >= 0 && e.rnb >= 0 && (long long)e.rfirst + e.rnb <= g_indel_cap[7]);
   cnt[i] = roff[e.rfirst + e.rnb] - roff[e.rfirst];
 }
 
@@ -312,9 +346,11 @@ __global__ void __launch_bounds__(kIndelThreads) k_indel_expand(const GanonReadV
   if (w >= n_inc) return;
   const IndelIncR e = inc[w];
   const int scope = (int)(e.scope_par & 0x7FFFFFFFu);
+  ICHK(IN_CAP(scope, 4) && IN_CAP(e.read, 3) && e.rfirst >= 0 && (long long)e.rfirst + e.rnb <= g_indel_cap[7]);
   const int span0 = V.span_start[scope];
   const int64_t a = roff[e.rfirst], n = roff[e.rfirst + e.rnb] - a, o0 = off[w];
   for (int64_t k = lane; k < n; k += 64) {
+    ICHK(IN_CAP(a + k, 1) && IN_CAP(o0 + k, 0));
     const IndelCand c = rcand[a + k];
     const int64_t o = o0 + k;
     IndelObs ob;
@@ -356,6 +392,7 @@ __global__ void __launch_bounds__(256) k_indel_mark_t(const GanonReadView V, con
   const int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (w >= n_reads) return;
   const IndelRead e = reads[w];
+  ICHK(IN_CAP(e.read, 3));
   const uint32_t ds = V.dataset[e.read] & 1u;
   thread_walk(V, e, [&](int pos, int, int, int) {
     const uint64_t g = map_cell(e.cbase + pos, shift);
@@ -404,7 +441,10 @@ __global__ void __launch_bounds__(256) k_indel_rlist_t(const GanonReadView V, co
   if (!cnt) return;
   int ord = e.nid0;
   thread_walk(V, e, [&](int pos, int irp, int op, int len) {
-    if (cand_bit(map, shift, e.cbase + pos)) rcand[slot++] = IndelCand{pos, irp, (len << 1) | (op == 1 ? 1 : 0), ord};
+    if (cand_bit(map, shift, e.cbase + pos)) {
+      ICHK(IN_CAP(slot, 1));
+      rcand[slot++] = IndelCand{pos, irp, (len << 1) | (op == 1 ? 1 : 0), ord};
+    }
     ++ord;
   });
 }
@@ -414,6 +454,7 @@ __global__ void k_indel_icount_t(const IndelIncR *__restrict__ inc, int64_t n_in
                                  int32_t *__restrict__ cnt) {
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i >= n_inc) return;
+  ICHK(IN_CAP(inc[i].rfirst, 7));
   cnt[i] = rcnt[inc[i].rfirst];
 }
 
@@ -427,12 +468,14 @@ __global__ void __launch_bounds__(256) k_indel_expand_t(const GanonReadView V, c
   const int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (w >= n_inc) return;
   const IndelIncR e = inc[w];
+  ICHK(IN_CAP(e.rfirst, 7) && IN_CAP(e.read, 3));
   // (roff: the read's start; rcnt: its count — k_indel_rlist_t, every short read one block)
   const int64_t a = roff[e.rfirst], n = rcnt[e.rfirst];
   if (!n) return;
   const int scope = (int)(e.scope_par & 0x7FFFFFFFu);
   const int span0 = V.span_start[scope];
   const int64_t o0 = off[w];
+  ICHK(IN_CAP(scope, 4) && (n == 0 || (IN_CAP(a, 1) && IN_CAP(a + n - 1, 1) && IN_CAP(o0, 0) && IN_CAP(o0 + n - 1, 0))));
   for (int64_t k = 0; k < n; ++k) {
     const IndelCand c = rcand[a + k];
     IndelObs ob;
@@ -457,7 +500,9 @@ __global__ void k_indel_segs(const int32_t *__restrict__ seg_first, int32_t n_se
                              int32_t *__restrict__ seg_off, uint32_t *__restrict__ segbits) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k <= n_seg) {
+    ICHK(seg_first[k] >= 0 && seg_first[k] <= g_indel_cap[6]);
     const int32_t o = off[seg_first[k]];
+    ICHK(o >= 0 && o <= g_indel_cap[0]);
     seg_off[k] = o;
     // (non-empty segments only: the empty ones share their successor's start, and thousands of
     // atomics on one word serialised the kernel — 0.3 ms on c2id)
@@ -475,6 +520,7 @@ __global__ void __launch_bounds__(256) k_indel_tsort(KeyT *__restrict__ keys, ui
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n_seg) return;
   const int32_t a = seg_off[k], b = seg_off[k + 1];
+  ICHK(a >= 0 && a <= b && b <= g_indel_cap[0]);
   for (int32_t i = a + 1; i < b; ++i) {
     const KeyT kk = keys[i];
     const uint32_t vv = vals[i];
@@ -498,6 +544,7 @@ __device__ bool same_call(const GanonReadView &V, const IndelObs &a, const Indel
   if (a.type_len != b.type_len) return false;
   const int len = a.type_len >> 1;
   const int alen = (a.type_len & 1) ? len : 2;
+  ICHK_RET(IN_CAP(a.read, 3) && IN_CAP(b.read, 3) && a.irp >= 0 && b.irp >= 0, false);
   const int La = V.read_len[a.read], Lb = V.read_len[b.read];
   // python slice [irp, irp + alen) clipped to the read
   const int na = max(0, min(La, a.irp + alen) - a.irp);
@@ -528,6 +575,8 @@ __device__ bool normal_covers(const GanonReadView &V, int scope, int pos) {
     int r[kU];
 #pragma unroll
     for (int u = 0; u < kU; ++u) r[u] = i + u < i1 ? V.incid_read[i + u] : -1;
+#pragma unroll
+    for (int u = 0; u < kU; ++u) ICHK_RET(r[u] < 0 || IN_CAP(r[u], 3), false);
     bool hit = false;
 #pragma unroll
     for (int u = 0; u < kU; ++u)
@@ -546,9 +595,17 @@ __device__ void classify_run(const GanonReadView &V, const KeyT *__restrict__ ke
                              int64_t n, int pos_bits, const IndelObs *__restrict__ obs, uint8_t *__restrict__ flags,
                              int32_t *__restrict__ rank, unsigned long long *__restrict__ repk, int64_t j0,
                              unsigned long long *__restrict__ n_rec, const uint32_t *__restrict__ segbits) {
+  ICHK(j0 >= 0 && j0 < n && n <= g_indel_cap[0]);
   const KeyT key = keys[j0];
   int64_t j1 = j0 + 1;
   while (j1 < n && keys[j1] == key && !seg_start(segbits, j1)) ++j1;
+#if GANON_INDEL_CHECK
+  for (int64_t a = j0; a < j1; ++a) {
+    ICHK(IN_CAP(vals[a], 0));
+    const IndelObs o = obs[vals[a]];
+    ICHK(IN_CAP(o.read, 3) && IN_CAP(o.scope, 4) && o.irp >= 0);
+  }
+#endif
 #if GANON_CLS_DIAG == 3
   if (j1 > j0) return;   // (phase timing builds only: results change)
 #endif
@@ -636,6 +693,7 @@ __global__ void __launch_bounds__(256) k_indel_runs(const KeyT *__restrict__ key
                                                     unsigned int *__restrict__ run_count,
                                                     const uint32_t *__restrict__ segbits) {
   const int64_t n = *n_dev;
+  ICHK(n >= 0 && n <= g_indel_cap[0]);
   __shared__ unsigned int wsum[4];
   __shared__ unsigned int base;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -709,7 +767,9 @@ __global__ void __launch_bounds__(256) k_indel_write(const GanonReadView V, cons
   if (j >= *n_dev) return;
   const uint8_t f = flags[j];
   if (!f) return;
+  ICHK(IN_CAP(vals[j], 0));
   const IndelObs o = obs[vals[j]];
+  ICHK(IN_CAP(o.scope, 4));
   ganon_indel_rec rec;
   rec.scope = o.scope;
   rec.pos = V.span_start[o.scope] + (int)((unsigned long long)keys[j] & ((1ull << pos_bits) - 1ull));
@@ -719,6 +779,7 @@ __global__ void __launch_bounds__(256) k_indel_write(const GanonReadView V, cons
   rec.read = o.read;
   rec.in_read_pos = o.irp;
   unsigned long long w = atomicAdd(slot, (unsigned long long)((f & 1) + (f >> 1)));
+  ICHK(IN_CAP(w + (f & 1) + (f >> 1) - 1, 2));
   if (f & 1) {
     rec.kind = GANON_INDEL_CALL;
     out[w++] = rec;
@@ -727,6 +788,20 @@ __global__ void __launch_bounds__(256) k_indel_write(const GanonReadView V, cons
     rec.kind = GANON_INDEL_SUPPORT;
     out[w] = rec;
   }
+}
+
+// Checked builds: a failed bounds check of any tally kernel so far (its source line), else GANON_OK.
+int indel_check_result(ganon_ctx *ctx) {
+#if GANON_INDEL_CHECK
+  unsigned int chk[2] = {0, 0};
+  if (hipMemcpyFromSymbol(chk, HIP_SYMBOL(g_indel_chk), sizeof chk, 0, hipMemcpyDeviceToHost) != hipSuccess)
+    return fail(ctx, GANON_E_DEVICE, "indel check: reading the check word failed");
+  if (chk[0])
+    return fail(ctx, GANON_E_DEVICE, "indel bounds check failed at ganon_indel.hip:%u (%u failures)", chk[0], chk[1]);
+#else
+  (void)ctx;
+#endif
+  return GANON_OK;
 }
 
 int bits_for(int64_t v) {   // bits to hold 0..v
@@ -852,6 +927,14 @@ int run_tally(ganon_ctx *ctx, ganon_indels *t) {
     HIP_OR_FAIL(hipMemsetAsync(t->keys[0], 0xFF, (size_t)t->n_obs * sizeof(unsigned long long), ctx->stream));
   HIP_OR_FAIL(hipMemsetAsync(t->counters, 0, 2 * sizeof(unsigned long long), ctx->stream));
   HIP_OR_FAIL(hipMemsetAsync(t->run_count, 0, sizeof(unsigned int), ctx->stream));
+#if GANON_INDEL_CHECK   // (checked builds: the capacities every index is checked against; one context at a time)
+  {
+    const long long caps[8] = {t->n_obs, t->n_rcand_cap, t->recs_cap, t->V.n_reads, t->V.n_scopes, t->n_list, t->n_ilist,
+                               t->n_rdist};
+    HIP_OR_FAIL(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_indel_cap), caps, sizeof caps, 0, hipMemcpyHostToDevice, ctx->stream));
+    HIP_OR_FAIL(hipStreamSynchronize(ctx->stream));   // (caps is a stack array)
+  }
+#endif
   const unsigned rgrid = (unsigned)((t->n_rdist + kIndelWaves - 1) / kIndelWaves);
   if (filter) {
     // per read block: the map, then its candidate ops (count, scan, list); per incidence: counts
@@ -1143,6 +1226,7 @@ GANON_API int64_t ganon_indel_download(ganon_ctx *ctx, ganon_indels *t, ganon_in
   if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
   t->n_candidates = cand;
   if (e != hipSuccess) return fail(ctx, GANON_E_DEVICE, "indel download: %s", hipGetErrorString(e));
+  if (int crc = indel_check_result(ctx)) return crc;
   t->n_records = (int64_t)total;
   if (!out || cap < (int64_t)total || total == 0) return (int64_t)total;
   if (t->recs_cap < (int64_t)total) {
@@ -1154,6 +1238,15 @@ GANON_API int64_t ganon_indel_download(ganon_ctx *ctx, ganon_indels *t, ganon_in
   const unsigned grid = (unsigned)((n + 255) / 256);
   e = hipMemsetAsync(t->counters + 1, 0, sizeof(unsigned long long), ctx->stream);
   if (e != hipSuccess) return fail(ctx, GANON_E_DEVICE, "indel download: %s", hipGetErrorString(e));
+#if GANON_INDEL_CHECK
+  {
+    const long long rcap = t->recs_cap;
+    e = hipMemcpyToSymbolAsync(HIP_SYMBOL(g_indel_cap), &rcap, sizeof rcap, 2 * sizeof(long long), hipMemcpyHostToDevice,
+                               ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) return fail(ctx, GANON_E_DEVICE, "indel download: %s", hipGetErrorString(e));
+  }
+#endif
   if (t->key64)
     hipLaunchKernelGGL(k_indel_write<unsigned long long>, dim3(grid), dim3(256), 0, ctx->stream, t->V,
                        static_cast<const unsigned long long *>(t->keys[t->sorted_sel]), t->vals[t->sorted_sel],
@@ -1167,6 +1260,7 @@ GANON_API int64_t ganon_indel_download(ganon_ctx *ctx, ganon_indels *t, ganon_in
   e = hipMemcpyAsync(out, t->recs, (size_t)total * sizeof(ganon_indel_rec), hipMemcpyDeviceToHost, ctx->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
   if (e != hipSuccess) return fail(ctx, GANON_E_DEVICE, "indel download: %s", hipGetErrorString(e));
+  if ((rc = indel_check_result(ctx))) return rc;
   return (int64_t)total;
 }
 

@@ -1308,15 +1308,6 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
             if coord_exc[0] is not None:   # rank 0 reports the coordinator's own error
                 failure = coord_exc[0]
         tails = {"coordinator_join": time.time() - t_tail}
-        if failure is None:
-            # every send of this rank has its receive on a clean run (rank 0's coordinator took every
-            # export before it joined; this rank's worker took every resolution): wait for them BEFORE the
-            # final gather, so that a failed drain is part of the gathered error state and every rank
-            # decides alike whether its side groups serve the next run
-            try:
-                link.drain()
-            except Exception as e:   # noqa: BLE001
-                failure = e
         err = repr(failure) if failure is not None else None
         t_tail = time.time()
         if xchg is not None:
@@ -1334,12 +1325,24 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
             if failure is not None:
                 raise failure
             raise RuntimeError(f"another rank failed: {errs[0]}")
-        # every rank ended cleanly: the side groups serve this process's next run (distributed.py)
+        # every rank ended cleanly: its sends all have their receives (a failed run never drains: a
+        # failed rank stops receiving). The side groups serve this process's next run only when every
+        # rank drained (one more small gather, so that all ranks cache alike and the next
+        # run's new_group calls stay collective)
+        drain_err = None
+        try:
+            link.drain()
+        except Exception as e:   # noqa: BLE001
+            drain_err = e
         if dist is not None and world > 1:
-            from .distributed import return_side_group
-            return_side_group(dist, "link", link.group, True)
-            if xchg is not None:
-                return_side_group(dist, "secondary", xchg.group, True)
+            drained = comm.allgather(drain_err is None)
+            if all(drained):
+                from .distributed import return_side_group
+                return_side_group(dist, "link", link.group, True)
+                if xchg is not None:
+                    return_side_group(dist, "secondary", xchg.group, True)
+        if drain_err is not None:
+            raise drain_err
         all_stats = [g["stats"] for g in gathered]
         if rank == 0 and record_statistics:
             merged: Dict[str, List[int]] = {OUTSIDE_WINDOWS: [0] * 8}

@@ -10,6 +10,8 @@ Prints one JSON line with per-stage seconds, reads/s, bases/s and the process's 
                              # formatter formats (bench.py's CPU end-to-end baseline; test infrastructure)
     E2E_RUNS=N ...           # timed runs per mode after one untimed warm run (default 1; 0: one run only)
     E2E_PROFILE=PREFIX ...   # cProfile of the timed run of each mode -> PREFIX_<mode>.txt (main thread)
+    E2E_SAMPLE=PREFIX ...    # CPU attribution of the last timed run, every thread (tools/cpu_sampler.py)
+                             # -> PREFIX_<mode>_r<rank>.json
     GANON_PREFETCH=N ...     # look-ahead planning threads of the streamed path (0: in line)
     E2E_DECODE_THREADS=T ... # host decode threads per process (default 16 / E2E_WORKERS)
     E2E_WORKERS=P ...        # the streamed path in P processes sharing the GPU (torch.distributed.run,
@@ -139,12 +141,20 @@ def main():
                             pass
             if dist is not None:
                 dist.barrier()
+            sampler = None
+            if it == n_timed and os.environ.get("E2E_SAMPLE"):   # CPU attribution of the last timed run
+                sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+                from cpu_sampler import Sampler
+                sampler = Sampler().__enter__()
             t1, c1 = time.time(), os.times()
             tim = sr.anonymize_genome(windows, os.path.join(d, "tumor.bam"), os.path.join(d, "normal.bam"),
                                       os.path.join(d, "ref.fa"), anon, os.path.join(out, f"tumor_{mode}"),
                                       os.path.join(out, f"normal_{mode}"), True, threads, fasta=fasta,
                                       streaming=(mode == "stream"), dist=dist)
             tim["wall_s"] = time.time() - t1
+            if sampler is not None:
+                sampler.__exit__(None, None, None)
+                sampler.report(f"{os.environ['E2E_SAMPLE']}_{mode}_r{rank}.json")
             c2 = os.times()   # this process's CPU time over the run (all its threads)
             tim["cpu_s"] = (c2.user - c1.user) + (c2.system - c1.system)
             if dist is not None:   # every rank's exchange and waits, then the slowest rank's wall

@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -74,6 +75,19 @@ void huge_reserve(RawVec<T> &v, size_t n) {
   if (n <= v.capacity()) return;
   v.reserve(n);
   huge_advise(v.data(), v.capacity() * sizeof(T));
+}
+
+// Decoder phase clocks (ganon_host_phase_times): wall nanoseconds of the calling threads, summed over
+// calls and threads — where a reader's decode time goes (tools/e2e_bench.py reports them per rank).
+enum { kPhParse, kPhInflate, kPhWalk, kPhCopy, kPhRecWalk, kPhSizes, kPhColumns, kPhN };
+std::atomic<long long> g_phase_ns[kPhN];
+using PhClock = std::chrono::steady_clock;
+// charge the time since t to phase ph and restart t
+inline void lap(int ph, PhClock::time_point &t) {
+  const auto now = PhClock::now();
+  g_phase_ns[ph].fetch_add((long long)std::chrono::duration_cast<std::chrono::nanoseconds>(now - t).count(),
+                           std::memory_order_relaxed);
+  t = now;
 }
 
 struct Block {
@@ -255,6 +269,7 @@ int records_to_columns(const uint8_t *d, int64_t p, int64_t n, ganon_bam *bam, i
   const int nt = std::max(1, std::min(threads, 64));
   // ---- records: boundaries (sequential), sizes + offsets, then columns in parallel ----
   std::vector<int64_t> rec;   // offset of each record's block_size field
+  auto tph = PhClock::now();
   while (p < n) {
     int32_t bs;
     if (p + 4 > n) return set_err("truncated record size");
@@ -267,6 +282,7 @@ int records_to_columns(const uint8_t *d, int64_t p, int64_t n, ganon_bam *bam, i
   // per record: name bytes kept, CIGAR ops, sequence length, aux bytes
   std::vector<int64_t> o_name(nr + 1), o_cig(nr + 1), o_seq(nr + 1), o_qual(nr + 1), o_aux(nr + 1);
   std::atomic<int64_t> first_bad{INT64_MAX};
+  lap(kPhRecWalk, tph);
   auto run_chunks = [&](auto &&fn) {
     std::vector<std::thread> ts;
     const int64_t per = (nr + nt - 1) / std::max(nt, 1);
@@ -315,6 +331,7 @@ int records_to_columns(const uint8_t *d, int64_t p, int64_t n, ganon_bam *bam, i
   huge_resize(bam->seq, (size_t)o_seq[nr]);
   huge_resize(bam->qual, (size_t)o_qual[nr]);
   huge_resize(bam->aux, (size_t)o_aux[nr]);
+  lap(kPhSizes, tph);
   run_chunks([&](int64_t i0, int64_t i1) {
     for (int64_t i = i0; i < i1; ++i) {
       const uint8_t *r = d + rec[i] + 4;
@@ -369,6 +386,7 @@ int records_to_columns(const uint8_t *d, int64_t p, int64_t n, ganon_bam *bam, i
       copy_bytes(bam->aux.data() + o_aux[i], r + q, (size_t)(bs - q));
     }
   });
+  lap(kPhColumns, tph);
   return 0;
 }
 
@@ -511,6 +529,7 @@ inline int64_t tid_order(int32_t t) { return t < 0 ? (int64_t)INT32_MAX : (int64
 // block to bmap. Returns the file offset after the last complete block, or -1 on error.
 int64_t read_blocks(ganon_bam_reader *R, int64_t coff, int64_t step, RawVec<uint8_t> &data,
                     std::vector<std::pair<int64_t, int64_t>> &bmap) {
+  auto tph = PhClock::now();
   const int64_t want = std::min<int64_t>(std::max<int64_t>(step, 1 << 17), R->fsize - coff);
   // the window's compressed bytes: in place in the file mapping (the inflate threads read the page
   // cache directly; no serial copy, no fresh buffer to fault in per window), else read into a buffer
@@ -545,6 +564,7 @@ int64_t read_blocks(ganon_bam_reader *R, int64_t coff, int64_t step, RawVec<uint
   if (off == 0) return set_err("truncated BGZF block");
   const size_t base = data.size();
   huge_resize(data, base + (size_t)total);
+  lap(kPhParse, tph);
   if (R->inflater && (int64_t)blocks.size() >= R->inflater_min) {
     const size_t nb = blocks.size();
     std::vector<int64_t> in_off(nb), out_off(nb);
@@ -561,6 +581,7 @@ int64_t read_blocks(ganon_bam_reader *R, int64_t coff, int64_t step, RawVec<uint
   } else if (!inflate_blocks(comp, blocks, 0, blocks.size(), data.data() + base, R->threads)) {
     return set_err("BGZF inflate failed");
   }
+  lap(kPhInflate, tph);
   for (size_t i = 0; i < blocks.size(); ++i) bmap.emplace_back((int64_t)base + blocks[i].out_off, bcoff[i]);
   return coff + off;
 }
@@ -625,12 +646,15 @@ int scan_tid(ganon_bam_reader *R, int64_t voff, int32_t tid, int64_t hint, RawVe
     if (coff < 0) return -1;
     step = std::min<int64_t>(2 * step, R->chunk);
     int64_t run0 = -1;   // first byte of the current run of `tid` records (copied to kept at once)
+    auto tw = PhClock::now();
     auto flush = [&]() {
       if (run0 >= 0) {
+        lap(kPhWalk, tw);
         const size_t n = (size_t)(dpos - run0), at = kept.size();
         if (at + n > kept.capacity()) huge_reserve(kept, std::max(2 * kept.capacity(), at + n));
         kept.resize(at + n);
         parallel_copy(kept.data() + at, data.data() + run0, n, R->threads);
+        lap(kPhCopy, tw);
       }
       run0 = -1;
     };
@@ -654,6 +678,7 @@ int scan_tid(ganon_bam_reader *R, int64_t voff, int32_t tid, int64_t hint, RawVe
       dpos += 4 + bs;
     }
     flush();
+    lap(kPhWalk, tw);
   }
 }
 
@@ -706,12 +731,15 @@ int scan_region(ganon_bam_reader *R, int64_t voff, int32_t tid, int64_t beg, int
     if (coff < 0) return -1;
     step = std::min<int64_t>(2 * step, R->chunk);
     int64_t run0 = -1;
+    auto tw = PhClock::now();
     auto flush = [&]() {
       if (run0 >= 0) {
+        lap(kPhWalk, tw);
         const size_t n = (size_t)(dpos - run0), at = kept.size();
         if (at + n > kept.capacity()) huge_reserve(kept, std::max(2 * kept.capacity(), at + n));
         kept.resize(at + n);
         parallel_copy(kept.data() + at, data.data() + run0, n, R->threads);
+        lap(kPhCopy, tw);
       }
       run0 = -1;
     };
@@ -736,6 +764,7 @@ int scan_region(ganon_bam_reader *R, int64_t voff, int32_t tid, int64_t beg, int
       dpos += 4 + bs;
     }
     flush();
+    lap(kPhWalk, tw);
   }
 }
 
@@ -1202,17 +1231,21 @@ GANON_HOST_API int ganon_fastq_edit(int64_t n, const char *recs, const int64_t *
 
 // Byte ranges of `src` back to back into `dst` (the output stage's splice of pre-formatted
 // records); threads for large copies. Returns the bytes written, -1 on bad arguments.
-GANON_HOST_API int64_t ganon_gather_ranges(const char *src, int64_t src_len, int64_t n, const int64_t *off,
-                                           const int64_t *len, char *dst, int64_t cap) {
-  if (n < 0 || (n > 0 && (!src || !off || !len || !dst))) return -1;
+static int64_t gather_impl(const char *const *src, const int64_t *src_len, int n_src, int64_t n, const uint8_t *sel,
+                           const int64_t *off, const int64_t *len, char *dst, int64_t cap) {
+  if (n < 0 || (n > 0 && (!off || !len || !dst))) return -1;
+  for (int k = 0; k < n_src; ++k)
+    if (n > 0 && !src[k] && src_len[k] > 0) return -1;
   std::vector<int64_t> at((size_t)n + 1, 0);
   for (int64_t i = 0; i < n; ++i) {
-    if (off[i] < 0 || len[i] < 0 || off[i] + len[i] > src_len) return -1;
+    const int k = sel ? sel[i] : 0;
+    if (k >= n_src || off[i] < 0 || len[i] < 0 || off[i] + len[i] > src_len[k]) return -1;
     at[i + 1] = at[i] + len[i];
   }
   if (at[n] > cap) return -1;
   auto work = [&](int64_t a, int64_t b) {
-    for (int64_t i = a; i < b; ++i) memcpy(dst + at[i], src + off[i], (size_t)len[i]);
+    for (int64_t i = a; i < b; ++i)
+      if (len[i]) memcpy(dst + at[i], src[sel ? sel[i] : 0] + off[i], (size_t)len[i]);
   };
   const int nt = (int)std::min<int64_t>(8, std::max<int64_t>(1, at[n] >> 23));   // one thread per 8 MiB
   if (nt == 1) {
@@ -1223,6 +1256,28 @@ GANON_HOST_API int64_t ganon_gather_ranges(const char *src, int64_t src_len, int
     for (auto &th : pool) th.join();
   }
   return at[n];
+}
+
+GANON_HOST_API int64_t ganon_gather_ranges(const char *src, int64_t src_len, int64_t n, const int64_t *off,
+                                           const int64_t *len, char *dst, int64_t cap) {
+  if (n > 0 && !src) return -1;
+  return gather_impl(&src, &src_len, 1, n, nullptr, off, len, dst, cap);
+}
+
+GANON_HOST_API int64_t ganon_gather_ranges2(const char *src0, int64_t len0, const char *src1, int64_t len1, int64_t n,
+                                            const uint8_t *sel, const int64_t *off, const int64_t *len, char *dst,
+                                            int64_t cap) {
+  if (n > 0 && !sel) return -1;
+  const char *src[2] = {src0, src1};
+  const int64_t sl[2] = {len0, len1};
+  return gather_impl(src, sl, 2, n, sel, off, len, dst, cap);
+}
+
+GANON_HOST_API int ganon_host_phase_times(double *out, int n, int reset) {
+  const int k = std::min(n, (int)kPhN);
+  for (int i = 0; i < k; ++i)
+    out[i] = (reset ? g_phase_ns[i].exchange(0) : g_phase_ns[i].load()) * 1e-9;
+  return (int)kPhN;
 }
 
 GANON_HOST_API const char *ganon_host_inflate_backend(void) { return libdeflate() ? "libdeflate" : "zlib"; }

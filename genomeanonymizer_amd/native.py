@@ -246,7 +246,7 @@ EXPORTED_HOST_SYMBOLS = (
     "ganon_resolver_finish", "ganon_resolver_take_log", "ganon_resolver_mark_written", "ganon_objects_pack", "ganon_blob_size", "ganon_blob_data",
     "ganon_blob_free", "ganon_objects_create", "ganon_objects_free", "ganon_objects_add_job", "ganon_objects_add_plain",
     "ganon_objects_run", "ganon_objects_take", "ganon_objects_settle", "ganon_objects_last_error",
-    "ganon_objects_take_all", "ganon_aux_sa_count", "ganon_fastq_edit", "ganon_gather_ranges",
+    "ganon_objects_take_all", "ganon_aux_sa_count", "ganon_fastq_edit", "ganon_gather_ranges", "ganon_gather_ranges2", "ganon_host_phase_times",
     "ganon_bam_reader_set_inflater",
 )
 
@@ -672,6 +672,30 @@ def gather_ranges(src: bytes, off: np.ndarray, length: np.ndarray) -> bytes:
     if w != total:
         raise GanonError("gather_ranges: range outside the source")
     return out
+
+
+def gather_ranges2(src0: bytes, src1: bytes, sel: np.ndarray, off: np.ndarray, length: np.ndarray) -> bytes:
+    """libganon_host.so ganon_gather_ranges2: range i from src0 (sel 0) or src1 (sel 1), back to back."""
+    sel = np.ascontiguousarray(sel, np.uint8)
+    off = np.ascontiguousarray(off, np.int64)
+    length = np.ascontiguousarray(length, np.int64)
+    total = int(length.sum())
+    out = _new_bytes(None, total)
+    w = host_lib().ganon_gather_ranges2(src0, len(src0), src1, len(src1), len(off), sel.ctypes.data_as(_u8p),
+                                        off.ctypes.data_as(_i64p), length.ctypes.data_as(_i64p), out, total)
+    if w != total:
+        raise GanonError("gather_ranges2: bad selector or range outside its source")
+    return out
+
+
+DECODE_PHASES = ("parse", "inflate", "region_walk", "kept_copy", "record_walk", "sizes", "columns")
+
+
+def decode_phase_times(reset: bool = False) -> dict:
+    """ganon_host_phase_times: seconds the BAM readers' calling threads spent per decode phase."""
+    out = (C.c_double * 16)()
+    n = host_lib().ganon_host_phase_times(out, 16, int(reset))
+    return {DECODE_PHASES[i] if i < len(DECODE_PHASES) else f"p{i}": round(out[i], 4) for i in range(min(n, 16))}
 
 
 class FastqEditError(GanonError):
@@ -1394,6 +1418,11 @@ def host_lib():
     lib.ganon_aux_sa_count.argtypes = [_u8p, _i64p, _i32p, C.c_int64, _i32p]
     lib.ganon_gather_ranges.argtypes = [C.c_char_p, C.c_int64, C.c_int64, _i64p, _i64p, C.c_char_p, C.c_int64]
     lib.ganon_gather_ranges.restype = C.c_int64
+    lib.ganon_gather_ranges2.argtypes = [C.c_char_p, C.c_int64, C.c_char_p, C.c_int64, C.c_int64, _u8p, _i64p, _i64p,
+                                         C.c_char_p, C.c_int64]
+    lib.ganon_gather_ranges2.restype = C.c_int64
+    lib.ganon_host_phase_times.argtypes = [C.POINTER(C.c_double), C.c_int, C.c_int]
+    lib.ganon_host_phase_times.restype = C.c_int
     lib.ganon_fastq_edit.argtypes = [C.c_int64, C.c_char_p, _i64p, _u8p, _i32p, _i64p, _i64p, C.c_char_p, _i64p,
                                      _p, C.c_int64, _i64p, _i64p]
     lib.ganon_objects_last_error.restype = C.c_char_p

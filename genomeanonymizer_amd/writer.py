@@ -261,22 +261,39 @@ class FastqFormatter:
             return self._native(ds, row, sc)
         keep = np.ones(len(ds), bool)
         keep[ed] = False
-        data = self._native(ds[keep], row[keep], sc[keep])
-        T, N = self.tables
-        nl = np.where(ds == 0, T.name_len[np.where(ds == 0, row, 0)], N.name_len[np.where(ds == 1, row, 0)])
-        ls = np.where(ds == 0, T.l_seq[np.where(ds == 0, row, 0)], N.l_seq[np.where(ds == 1, row, 0)])
-        rl = np.where(keep, nl.astype(np.int64) + 8 + 2 * ls.astype(np.int64), 0)
-        off = np.concatenate([[0], np.cumsum(rl)]).tolist()      # byte offset in `data` of each record
         insts = list(zip(ds[ed].tolist(), row[ed].tolist(), sc[ed].tolist()))
         re_ = reapply[ed].tolist()
         self.prepare_edited(insts, re_)
-        parts, prev = [], 0
-        for i, inst, r in zip(ed.tolist(), insts, re_):
-            parts.append(data[off[prev]:off[i]])
-            parts.append((self.edited2 if r else self.edited)[inst])
-            prev = i + 1
-        parts.append(data[off[prev]:])
-        return b"".join(parts)
+        eb = [(self.edited2 if r else self.edited)[inst] for inst, r in zip(insts, re_)]
+        # ONE copy of every record into its place: the unedited ones straight out of the job's
+        # pre-formatted blob (or of one formatter call), the edited ones out of their small
+        # concatenation (slicing and joining the whole output in Python copied it twice more: the
+        # writer thread's largest CPU cost at 30x, tools/cpu_sampler.py)
+        sel = np.zeros(len(ds), np.uint8)
+        sel[ed] = 1
+        off = np.zeros(len(ds), np.int64)
+        ln = np.zeros(len(ds), np.int64)
+        e_len = np.array([len(b) for b in eb], np.int64)
+        off[ed] = np.concatenate([[0], np.cumsum(e_len)[:-1]])
+        ln[ed] = e_len
+        kd, kr, ks = ds[keep], row[keep], sc[keep]
+        src, k_off, k_len = self._ranges(kd, kr, ks)
+        off[keep] = k_off
+        ln[keep] = k_len
+        return native.gather_ranges2(src, b"".join(eb), sel, off, ln)
+
+    def _ranges(self, ds, row, sc):
+        """(source bytes, offsets, lengths) of the records of ``ds, row, sc`` (unedited): ranges of
+        the pre-formatted blob when it holds every one, else one formatter call's output."""
+        pre = self._pre
+        if pre is not None and len(ds):
+            k = self._key(ds, row, sc)
+            pos = np.minimum(np.searchsorted(pre[0], k), len(pre[0]) - 1)
+            if np.array_equal(pre[0][pos], k):
+                return pre[3], pre[1][pos], pre[2][pos]
+        data = self._format(ds, row, sc) if len(ds) else b""
+        ln = self._plain_lengths(ds, row)
+        return data, np.concatenate([[0], np.cumsum(ln)[:-1]]).astype(np.int64) if len(ds) else ln, ln
 
     def format(self, recs: Sequence[Tuple[int, int, int]], reapply=None) -> bytes:
         a = np.array(recs, np.int64).reshape(-1, 3)

@@ -138,6 +138,20 @@ GANON_HOST_API int ganon_fastq_edit(int64_t n, const char *recs, const int64_t *
 GANON_HOST_API int64_t ganon_gather_ranges(const char *src, int64_t src_len, int64_t n, const int64_t *off,
                                            const int64_t *len, char *dst, int64_t cap);
 
+/* The same from two sources: range i is src0[off[i] ..) when sel[i] == 0, src1[off[i] ..) when 1 (the
+ * output stage splicing a job's few indel-edited records in among its pre-formatted ones with one
+ * copy). Returns the bytes written, or -1 for a bad selector, a range outside its source or a
+ * too-small cap. */
+GANON_HOST_API int64_t ganon_gather_ranges2(const char *src0, int64_t len0, const char *src1, int64_t len1, int64_t n,
+                                            const uint8_t *sel, const int64_t *off, const int64_t *len, char *dst,
+                                            int64_t cap);
+
+/* Decoder phase clocks: wall seconds the reader's calling threads spent per phase since the last
+ * reset (parse of BGZF headers, inflate, record walk of the region scan, copies of kept runs, the
+ * columns' record walk, sizes pass, columns pass), summed over calls and threads; out[0..n). Returns
+ * the number of phases. Diagnostics (tools/e2e_bench.py). */
+GANON_HOST_API int ganon_host_phase_times(double *out, int n, int reset);
+
 /* Upper-case a FASTA slice and pack it to nt16 nibbles (2 per byte, high first). Bytes
  * outside "=ACMGRSVTWYHKDBN" (after upper-casing) become N (15). `out` has (n+1)/2 bytes. */
 GANON_HOST_API void ganon_pack_nt16(const char *ascii, int64_t n, uint8_t *out);

@@ -146,12 +146,15 @@ def main():
                 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
                 from cpu_sampler import Sampler
                 sampler = Sampler().__enter__()
+            from genomeanonymizer_amd import native as _nat
+            _nat.decode_phase_times(reset=True)
             t1, c1 = time.time(), os.times()
             tim = sr.anonymize_genome(windows, os.path.join(d, "tumor.bam"), os.path.join(d, "normal.bam"),
                                       os.path.join(d, "ref.fa"), anon, os.path.join(out, f"tumor_{mode}"),
                                       os.path.join(out, f"normal_{mode}"), True, threads, fasta=fasta,
                                       streaming=(mode == "stream"), dist=dist)
             tim["wall_s"] = time.time() - t1
+            tim["decode_phases"] = _nat.decode_phase_times()
             if sampler is not None:
                 sampler.__exit__(None, None, None)
                 sampler.report(f"{os.environ['E2E_SAMPLE']}_{mode}_r{rank}.json")
@@ -162,7 +165,7 @@ def main():
                 dist.all_gather_object(per_rank, {k: tim.get(k) for k in (
                     "wall_s", "exchange_sent_bytes", "exchange_recv_bytes", "wait_s", "writer_wait_s", "jobs",
                     "decode_s", "mask_s", "format_s", "write_s", "redos_skipped", "critical_path", "cpu_s", "fastq_device",
-                    "setup_s", "groups_s", "tail_parts", "prep_parts", "decode_thread_s", "prefetch_s")})
+                    "setup_s", "groups_s", "tail_parts", "prep_parts", "decode_thread_s", "prefetch_s", "decode_phases")})
                 tim["per_rank"] = per_rank
                 import torch
                 w = torch.tensor([tim["wall_s"]], dtype=torch.float64)
@@ -191,6 +194,7 @@ def main():
                      "workers": workers,
                      "critical_path_s_rank0": best.get("critical_path"),
                      "fastq_device_rank0": best.get("fastq_device"),
+                     "decode_phases_rank0": best.get("decode_phases"),
                      "per_rank": best.get("per_rank"),
                      "coordinator_busy_s": best.get("resolve_s"),
                      "redos": best.get("redos"), "redos_unchanged": best.get("redos_unchanged"),

@@ -2195,6 +2195,21 @@ GANON_API int ganon_ctx_destroy(ganon_ctx *ctx) {
 
 GANON_API const char *ganon_last_error(ganon_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
+GANON_API int ganon_pinned_alloc(int64_t bytes, void **out) {
+  if (!out || bytes < 0) return GANON_E_ARG;
+  *out = nullptr;
+  if (hipHostMalloc(out, (size_t)std::max<int64_t>(bytes, 1), hipHostMallocDefault) != hipSuccess) {
+    *out = nullptr;
+    return GANON_E_NOMEM;
+  }
+  return GANON_OK;
+}
+
+GANON_API int ganon_pinned_free(void *p) {
+  if (p) hipHostFree(p);
+  return GANON_OK;
+}
+
 GANON_API int ganon_ctx_set_stream(ganon_ctx *ctx, void *hip_stream) {
   if (!ctx) return GANON_E_ARG;
   ctx->stream = hip_stream ? reinterpret_cast<hipStream_t>(hip_stream) : ctx->own;

@@ -264,20 +264,26 @@ int parse_header(const uint8_t *d, int64_t n, ganon_bam *bam, int64_t &p) {
   return 1;
 }
 
-// Column arrays of the records packed back to back in d[p, n) (each: block_size + body).
-int records_to_columns(const uint8_t *d, int64_t p, int64_t n, ganon_bam *bam, int threads) {
+// Column arrays of the records packed back to back in d[p, n) (each: block_size + body), or, with
+// `known`, of the records at those offsets of d (the reader's scans walked and checked them already:
+// their records stay in place in the scan's buffer, no boundary walk and no copy of the kept runs).
+int records_to_columns(const uint8_t *d, int64_t p, int64_t n, ganon_bam *bam, int threads,
+                       const std::vector<int64_t> *known = nullptr) {
   const int nt = std::max(1, std::min(threads, 64));
   // ---- records: boundaries (sequential), sizes + offsets, then columns in parallel ----
-  std::vector<int64_t> rec;   // offset of each record's block_size field
+  std::vector<int64_t> own;   // offset of each record's block_size field
   auto tph = PhClock::now();
-  while (p < n) {
-    int32_t bs;
-    if (p + 4 > n) return set_err("truncated record size");
-    std::memcpy(&bs, d + p, 4);
-    if (bs < 32 || p + 4 + bs > n) return set_err("bad record size");
-    rec.push_back(p);
-    p += 4 + bs;
+  if (!known) {
+    while (p < n) {
+      int32_t bs;
+      if (p + 4 > n) return set_err("truncated record size");
+      std::memcpy(&bs, d + p, 4);
+      if (bs < 32 || p + 4 + bs > n) return set_err("bad record size");
+      own.push_back(p);
+      p += 4 + bs;
+    }
   }
+  const std::vector<int64_t> &rec = known ? *known : own;
   const int64_t nr = (int64_t)rec.size();
   // per record: name bytes kept, CIGAR ops, sequence length, aux bytes
   std::vector<int64_t> o_name(nr + 1), o_cig(nr + 1), o_seq(nr + 1), o_qual(nr + 1), o_aux(nr + 1);
@@ -586,24 +592,6 @@ int64_t read_blocks(ganon_bam_reader *R, int64_t coff, int64_t step, RawVec<uint
   return coff + off;
 }
 
-// memcpy split over up to `threads` threads for large runs (a contig's records are copied out of
-// each inflated window once; one thread copying and faulting in a GB-sized buffer was a third of the
-// decode of a chromosome-sized contig).
-void parallel_copy(uint8_t *dst, const uint8_t *src, size_t n, int threads) {
-  constexpr size_t kPer = 4u << 20;
-  const int nt = (int)std::min<size_t>((size_t)std::max(1, std::min(threads, 16)), (n + kPer - 1) / kPer);
-  if (nt <= 1) {
-    copy_bytes(dst, src, n);
-    return;
-  }
-  const size_t per = (n + nt - 1) / nt;
-  std::vector<std::thread> pool;
-  for (int t = 1; t < nt; ++t)
-    pool.emplace_back([=] { copy_bytes(dst + t * per, src + t * per, std::min(per, n - std::min(n, t * per))); });
-  copy_bytes(dst, src, std::min(per, n));
-  for (auto &th : pool) th.join();
-}
-
 int64_t voff_at(const std::vector<std::pair<int64_t, int64_t>> &bmap, int64_t x) {
   auto it = std::upper_bound(bmap.begin(), bmap.end(), std::make_pair(x, INT64_MAX));
   if (it == bmap.begin()) return -1;
@@ -616,12 +604,16 @@ int64_t voff_at(const std::vector<std::pair<int64_t, int64_t>> &bmap, int64_t x)
 // record met (kTidEnd when none) so that an index start can be validated. hint: expected compressed
 // bytes of the sequence (index span) or 0; the step read and inflated at a time starts there (or at
 // 1 MiB) and doubles up to the reader's window, so a small sequence never inflates a whole window.
-int scan_tid(ganon_bam_reader *R, int64_t voff, int32_t tid, int64_t hint, RawVec<uint8_t> &kept,
-             int64_t &next_voff, int32_t &next_tid, int32_t &first_tid) {
+int scan_tid(ganon_bam_reader *R, int64_t voff, int32_t tid, int64_t hint, RawVec<uint8_t> &data,
+             std::vector<int64_t> &recs, int64_t &next_voff, int32_t &next_tid, int32_t &first_tid) {
+  // (the records stay where they were inflated: `data` grows by every window and only the offsets of
+  // the sequence's records are kept — round 6; the windows' consumed bytes used to be dropped and the
+  // kept runs copied into a second buffer, then walked again to find their boundaries)
   int64_t step = std::min<int64_t>(hint > 0 ? hint + (1 << 16) : (1 << 20), R->chunk);
   int64_t coff = voff >> 16;
-  RawVec<uint8_t> data;
   std::vector<std::pair<int64_t, int64_t>> bmap;
+  data.clear();
+  recs.clear();
   int64_t dpos = (int64_t)(voff & 0xFFFF);
   bool seen = false;
   first_tid = kTidEnd;
@@ -632,32 +624,10 @@ int scan_tid(ganon_bam_reader *R, int64_t voff, int32_t tid, int64_t hint, RawVe
       next_tid = kTidEnd;
       return 0;
     }
-    // drop consumed bytes (keep the block map entries still needed for offsets >= dpos)
-    if (dpos > 0 && !data.empty()) {
-      const int64_t cut = std::min<int64_t>(dpos, (int64_t)data.size());
-      data.erase(data.begin(), data.begin() + cut);
-      dpos -= cut;
-      for (auto &e : bmap) e.first -= cut;
-      size_t k = 0;
-      while (k + 1 < bmap.size() && bmap[k + 1].first <= 0) ++k;
-      bmap.erase(bmap.begin(), bmap.begin() + (long)k);
-    }
     coff = read_blocks(R, coff, step, data, bmap);
     if (coff < 0) return -1;
     step = std::min<int64_t>(2 * step, R->chunk);
-    int64_t run0 = -1;   // first byte of the current run of `tid` records (copied to kept at once)
     auto tw = PhClock::now();
-    auto flush = [&]() {
-      if (run0 >= 0) {
-        lap(kPhWalk, tw);
-        const size_t n = (size_t)(dpos - run0), at = kept.size();
-        if (at + n > kept.capacity()) huge_reserve(kept, std::max(2 * kept.capacity(), at + n));
-        kept.resize(at + n);
-        parallel_copy(kept.data() + at, data.data() + run0, n, R->threads);
-        lap(kPhCopy, tw);
-      }
-      run0 = -1;
-    };
     for (;;) {
       if (dpos + 4 > (int64_t)data.size()) break;
       int32_t bs, rtid;
@@ -667,17 +637,16 @@ int scan_tid(ganon_bam_reader *R, int64_t voff, int32_t tid, int64_t hint, RawVe
       std::memcpy(&rtid, &data[(size_t)dpos + 4], 4);
       if (first_tid == kTidEnd) first_tid = rtid;
       if (rtid == tid) {
-        if (run0 < 0) run0 = dpos;
+        recs.push_back(dpos);
         seen = true;
       } else if (seen || tid_order(rtid) > tid_order(tid)) {
-        flush();
         next_voff = voff_at(bmap, dpos);
         next_tid = rtid;
+        lap(kPhWalk, tw);
         return 0;
       }
       dpos += 4 + bs;
     }
-    flush();
     lap(kPhWalk, tw);
   }
 }
@@ -707,42 +676,23 @@ int64_t record_end(const uint8_t *d) {
 // region semantics: pos < end and bam_endpos > beg), in file order; stops at the first record of
 // another sequence or at pos >= end. Runs of kept records are copied to kept at once.
 int scan_region(ganon_bam_reader *R, int64_t voff, int32_t tid, int64_t beg, int64_t end, int64_t hint,
-                RawVec<uint8_t> &kept) {
+                RawVec<uint8_t> &data, std::vector<int64_t> &recs) {
+  // (records stay in place in `data`, their offsets in recs: as scan_tid)
   int64_t step = std::min<int64_t>(hint > 0 ? hint + (1 << 16) : (1 << 20), R->chunk);
   int64_t coff = voff >> 16;
-  RawVec<uint8_t> data;
   std::vector<std::pair<int64_t, int64_t>> bmap;
+  data.clear();
+  recs.clear();
   int64_t dpos = (int64_t)(voff & 0xFFFF);
   for (;;) {
     if (coff >= R->fsize) {
       if (dpos < (int64_t)data.size()) return set_err("truncated BAM record");
       return 0;
     }
-    if (dpos > 0 && !data.empty()) {
-      const int64_t cut = std::min<int64_t>(dpos, (int64_t)data.size());
-      data.erase(data.begin(), data.begin() + cut);
-      dpos -= cut;
-      for (auto &e : bmap) e.first -= cut;
-      size_t k = 0;
-      while (k + 1 < bmap.size() && bmap[k + 1].first <= 0) ++k;
-      bmap.erase(bmap.begin(), bmap.begin() + (long)k);
-    }
     coff = read_blocks(R, coff, step, data, bmap);
     if (coff < 0) return -1;
     step = std::min<int64_t>(2 * step, R->chunk);
-    int64_t run0 = -1;
     auto tw = PhClock::now();
-    auto flush = [&]() {
-      if (run0 >= 0) {
-        lap(kPhWalk, tw);
-        const size_t n = (size_t)(dpos - run0), at = kept.size();
-        if (at + n > kept.capacity()) huge_reserve(kept, std::max(2 * kept.capacity(), at + n));
-        kept.resize(at + n);
-        parallel_copy(kept.data() + at, data.data() + run0, n, R->threads);
-        lap(kPhCopy, tw);
-      }
-      run0 = -1;
-    };
     for (;;) {
       if (dpos + 4 > (int64_t)data.size()) break;
       int32_t bs, rtid, rpos;
@@ -753,17 +703,12 @@ int scan_region(ganon_bam_reader *R, int64_t voff, int32_t tid, int64_t beg, int
       std::memcpy(&rpos, &data[(size_t)dpos + 8], 4);
       if (rtid != tid || rpos >= end) {
         if (tid_order(rtid) < tid_order(tid)) return set_err("BAM index points before its sequence");
-        flush();
+        lap(kPhWalk, tw);
         return 0;
       }
-      if (record_end(&data[(size_t)dpos]) > beg) {
-        if (run0 < 0) run0 = dpos;
-      } else {
-        flush();
-      }
+      if (record_end(&data[(size_t)dpos]) > beg) recs.push_back(dpos);
       dpos += 4 + bs;
     }
-    flush();
     lap(kPhWalk, tw);
   }
 }
@@ -916,7 +861,8 @@ GANON_HOST_API int ganon_bam_reader_contig(ganon_bam_reader *R, int32_t tid, gan
   *out = nullptr;
   if (tid < 0 || tid >= (int32_t)R->header.ref_len.size()) return set_err("tid out of range");
   try {
-    RawVec<uint8_t> kept;
+    RawVec<uint8_t> data;
+    std::vector<int64_t> recs;
     int64_t next_voff = -1;
     int32_t next_tid = kTidEnd, first_tid = kTidEnd;
     bool done = false;
@@ -927,17 +873,17 @@ GANON_HOST_API int ganon_bam_reader_contig(ganon_bam_reader *R, int32_t tid, gan
       } else {
         const int64_t e = R->index_end[(size_t)tid];
         const int64_t hint = e > beg ? (e >> 16) - (beg >> 16) : 0;
-        // the sequence's records, inflated, at ~3.5x their compressed span (address space only: an
+        // the sequence's blocks, inflated, at ~3.5x their compressed span (address space only: an
         // underestimate just grows the buffer)
-        huge_reserve(kept, (size_t)hint * 7 / 2 + (1 << 20));
-        if (scan_tid(R, beg, tid, hint, kept, next_voff, next_tid, first_tid) != 0) return -1;
+        huge_reserve(data, (size_t)hint * 7 / 2 + (4 << 20));
+        if (scan_tid(R, beg, tid, hint, data, recs, next_voff, next_tid, first_tid) != 0) return -1;
         done = first_tid == tid;   // a stale index falls back to the forward scan
-        if (!done) kept.clear();
+        if (!done) recs.clear();
       }
     }
     if (!done) {
       const bool forward = R->cur_voff >= 0 && tid_order(R->cur_tid) <= tid_order(tid);
-      if (scan_tid(R, forward ? R->cur_voff : R->data_voff, tid, 0, kept, next_voff, next_tid, first_tid) != 0)
+      if (scan_tid(R, forward ? R->cur_voff : R->data_voff, tid, 0, data, recs, next_voff, next_tid, first_tid) != 0)
         return -1;
       R->cur_voff = next_voff;
       R->cur_tid = next_tid;
@@ -946,7 +892,7 @@ GANON_HOST_API int ganon_bam_reader_contig(ganon_bam_reader *R, int32_t tid, gan
     bam->ref_names = R->header.ref_names;
     bam->ref_name_off = R->header.ref_name_off;
     bam->ref_len = R->header.ref_len;
-    if (records_to_columns(kept.data(), 0, (int64_t)kept.size(), bam, R->threads) != 0) {
+    if (records_to_columns(data.data(), 0, (int64_t)data.size(), bam, R->threads, &recs) != 0) {
       delete bam;
       return -1;
     }
@@ -965,7 +911,8 @@ GANON_HOST_API int ganon_bam_reader_region(ganon_bam_reader *R, int32_t tid, int
   if (!R->has_index) return set_err("region reads need the BAM index");
   if (beg < 0 || end < beg) return set_err("bad region");
   try {
-    RawVec<uint8_t> kept;
+    RawVec<uint8_t> data;
+    std::vector<int64_t> recs;
     const int64_t first = R->index_beg[(size_t)tid];
     if (first >= 0 && end > beg) {
       // the first record that can overlap beg: the linear index entry of its 16 kb window (the
@@ -981,14 +928,14 @@ GANON_HOST_API int ganon_bam_reader_region(ganon_bam_reader *R, int32_t tid, int
       const int64_t span = e > voff ? (e >> 16) - (voff >> 16) : 0;
       const int64_t len = R->header.ref_len[(size_t)tid];
       const int64_t hint = len > 0 ? std::min<int64_t>(span, span * (end - beg) / len + (1 << 20)) : 0;
-      huge_reserve(kept, (size_t)hint * 7 / 2 + (1 << 20));
-      if (scan_region(R, voff, tid, beg, end, hint, kept) != 0) return -1;
+      huge_reserve(data, (size_t)hint * 7 / 2 + (4 << 20));
+      if (scan_region(R, voff, tid, beg, end, hint, data, recs) != 0) return -1;
     }
     auto *bam = new ganon_bam();
     bam->ref_names = R->header.ref_names;
     bam->ref_name_off = R->header.ref_name_off;
     bam->ref_len = R->header.ref_len;
-    if (records_to_columns(kept.data(), 0, (int64_t)kept.size(), bam, R->threads) != 0) {
+    if (records_to_columns(data.data(), 0, (int64_t)data.size(), bam, R->threads, &recs) != 0) {
       delete bam;
       return -1;
     }

@@ -10,6 +10,8 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import threading
+import weakref
 import time
 from typing import Dict, Optional, Tuple
 
@@ -180,7 +182,9 @@ def hip_lib():
     lib.ganon_fastq_bytes.argtypes = [_p]
     lib.ganon_fastq_bytes.restype = C.c_int64
     lib.ganon_fastq_device_output.argtypes = [_p, C.POINTER(_p)]
-    lib.ganon_fastq_download.argtypes = [_p, _p, C.c_char_p, C.c_int64]
+    lib.ganon_fastq_download.argtypes = [_p, _p, C.c_void_p, C.c_int64]
+    lib.ganon_pinned_alloc.argtypes = [C.c_int64, C.POINTER(_p)]
+    lib.ganon_pinned_free.argtypes = [_p]
     lib.ganon_fastq_download.restype = C.c_int64
     lib.ganon_fastq_free.argtypes = [_p, _p]
     lib.ganon_fastq_format_hip.restype = C.c_int64
@@ -235,6 +239,7 @@ EXPORTED_HIP_SYMBOLS = (
     "ganon_indel_upload", "ganon_indel_run", "ganon_indel_download", "ganon_indel_info", "ganon_indel_free",
     "ganon_inflate", "ganon_inflate_hostcb", "ganon_inflate_device_output",
     "ganon_bam_columns", "ganon_bam_dcols_get", "ganon_bam_dcols_download", "ganon_bam_dcols_free",
+    "ganon_pinned_alloc", "ganon_pinned_free",
 )
 EXPORTED_HOST_SYMBOLS = (
     "ganon_bam_open", "ganon_bam_view_get", "ganon_bam_error", "ganon_bam_close",
@@ -384,6 +389,48 @@ class GpuInflater:
             self.close()
         except Exception:
             pass
+
+
+class PinnedPool:
+    """Page-locked host blocks (ganon_pinned_alloc) handed out as numpy uint8 views and taken back when
+    the last view is gone (weakref.finalize on the block): the device formatter's records of a job
+    land in one by DMA — into pageable memory the runtime staged every byte through a host copy,
+    ~1 CPU-second per 5 GB of FASTQ (tools/cpu_sampler.py on the 30x line). Free blocks are kept for
+    reuse up to ``keep`` bytes; sizes are rounded to 16 MiB."""
+
+    def __init__(self, keep: int = 2 << 30):
+        self.keep = keep
+        self.free: list = []          # (capacity, address)
+        self.lock = threading.Lock()
+
+    def take(self, n: int) -> np.ndarray:
+        cap = max(16 << 20, -(-n // (16 << 20)) * (16 << 20))
+        addr = None
+        with self.lock:
+            best = None
+            for i, (c, a) in enumerate(self.free):
+                if cap <= c <= 2 * cap and (best is None or c < self.free[best][0]):
+                    best = i
+            if best is not None:
+                cap, addr = self.free.pop(best)
+        if addr is None:
+            ptr = _p()
+            if hip_lib().ganon_pinned_alloc(cap, C.byref(ptr)) != 0 or not ptr.value:
+                return np.empty(n, np.uint8)      # (no page-locked memory left: pageable)
+            addr = ptr.value
+        block = (C.c_uint8 * cap).from_address(addr)
+        weakref.finalize(block, self._give_back, cap, addr)
+        return np.frombuffer(block, np.uint8, count=n)
+
+    def _give_back(self, cap: int, addr: int) -> None:
+        with self.lock:
+            if sum(c for c, _ in self.free) + cap <= self.keep:
+                self.free.append((cap, addr))
+                return
+        hip_lib().ganon_pinned_free(_p(addr))
+
+
+PINNED = PinnedPool()
 
 
 class HipMasker:
@@ -552,9 +599,10 @@ class HipMasker:
             t1 = time.perf_counter()
             self._check(self._lib.ganon_fastq_run(self._h, h), "ganon_fastq_run")
             n_bytes = int(self._lib.ganon_fastq_bytes(h))
-            out = _new_bytes(None, n_bytes)      # filled in place
+            # page-locked: the records come down by DMA (a numpy view; the job's pre-formatted blob)
+            out = PINNED.take(n_bytes) if n_bytes >= (8 << 20) else _new_bytes(None, n_bytes)
             t2 = time.perf_counter()
-            w = self._lib.ganon_fastq_download(self._h, h, out, n_bytes)
+            w = self._lib.ganon_fastq_download(self._h, h, _addr(out), n_bytes)
             w = _fastq_result(w, lambda: self._lib.ganon_last_error(self._h).decode(errors="replace"))
             t3 = time.perf_counter()
             FQ_TIMES["upload_s"] += t1 - t0   # (where a job's formatting goes: the stream's timing)
@@ -661,27 +709,35 @@ def host_format_fastq(recs: dict) -> bytes:
     return out if w == n_bytes else out[:w]
 
 
-def gather_ranges(src: bytes, off: np.ndarray, length: np.ndarray) -> bytes:
-    """libganon_host.so ganon_gather_ranges: src[off[i]:off[i] + length[i]] back to back."""
+def _addr(buf) -> int:
+    """Address of a bytes object's or a contiguous numpy array's data."""
+    if isinstance(buf, np.ndarray):
+        return buf.ctypes.data
+    return C.cast(C.c_char_p(buf), C.c_void_p).value or 0
+
+
+def gather_ranges(src, off: np.ndarray, length: np.ndarray) -> bytes:
+    """libganon_host.so ganon_gather_ranges: src[off[i]:off[i] + length[i]] back to back (src: bytes or a
+    uint8 array)."""
     off = np.ascontiguousarray(off, np.int64)
     length = np.ascontiguousarray(length, np.int64)
     total = int(length.sum())
     out = _new_bytes(None, total)      # a fresh, unshared bytes object the library fills in place
-    w = host_lib().ganon_gather_ranges(src, len(src), len(off), off.ctypes.data_as(_i64p),
+    w = host_lib().ganon_gather_ranges(_addr(src), len(src), len(off), off.ctypes.data_as(_i64p),
                                        length.ctypes.data_as(_i64p), out, total)
     if w != total:
         raise GanonError("gather_ranges: range outside the source")
     return out
 
 
-def gather_ranges2(src0: bytes, src1: bytes, sel: np.ndarray, off: np.ndarray, length: np.ndarray) -> bytes:
+def gather_ranges2(src0, src1, sel: np.ndarray, off: np.ndarray, length: np.ndarray) -> bytes:
     """libganon_host.so ganon_gather_ranges2: range i from src0 (sel 0) or src1 (sel 1), back to back."""
     sel = np.ascontiguousarray(sel, np.uint8)
     off = np.ascontiguousarray(off, np.int64)
     length = np.ascontiguousarray(length, np.int64)
     total = int(length.sum())
     out = _new_bytes(None, total)
-    w = host_lib().ganon_gather_ranges2(src0, len(src0), src1, len(src1), len(off), sel.ctypes.data_as(_u8p),
+    w = host_lib().ganon_gather_ranges2(_addr(src0), len(src0), _addr(src1), len(src1), len(off), sel.ctypes.data_as(_u8p),
                                         off.ctypes.data_as(_i64p), length.ctypes.data_as(_i64p), out, total)
     if w != total:
         raise GanonError("gather_ranges2: bad selector or range outside its source")
@@ -756,7 +812,7 @@ class DeviceFastq:
 
     def download(self) -> bytes:
         out = C.create_string_buffer(max(self.n_bytes, 1))
-        w = self.m._lib.ganon_fastq_download(self.m._h, self.h, out, self.n_bytes)
+        w = self.m._lib.ganon_fastq_download(self.m._h, self.h, _addr(out), self.n_bytes)
         return out.raw[:_fastq_result(w, lambda: self.m._lib.ganon_last_error(self.m._h).decode(errors="replace"))]
 
     def kernel_times(self) -> list:
@@ -1416,9 +1472,9 @@ def host_lib():
     lib.ganon_objects_take_all.argtypes = [_p, _i64p, _i64p, C.c_char_p, C.c_int64, C.POINTER(C.c_int64)]
     lib.ganon_objects_take_all.restype = C.c_int64
     lib.ganon_aux_sa_count.argtypes = [_u8p, _i64p, _i32p, C.c_int64, _i32p]
-    lib.ganon_gather_ranges.argtypes = [C.c_char_p, C.c_int64, C.c_int64, _i64p, _i64p, C.c_char_p, C.c_int64]
+    lib.ganon_gather_ranges.argtypes = [C.c_void_p, C.c_int64, C.c_int64, _i64p, _i64p, C.c_char_p, C.c_int64]
     lib.ganon_gather_ranges.restype = C.c_int64
-    lib.ganon_gather_ranges2.argtypes = [C.c_char_p, C.c_int64, C.c_char_p, C.c_int64, C.c_int64, _u8p, _i64p, _i64p,
+    lib.ganon_gather_ranges2.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_int64, _u8p, _i64p, _i64p,
                                          C.c_char_p, C.c_int64]
     lib.ganon_gather_ranges2.restype = C.c_int64
     lib.ganon_host_phase_times.argtypes = [C.POINTER(C.c_double), C.c_int, C.c_int]

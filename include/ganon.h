@@ -93,6 +93,11 @@ typedef struct ganon_batch {
 GANON_API int ganon_ctx_create(int device, ganon_ctx **out);
 GANON_API int ganon_ctx_destroy(ganon_ctx *ctx);
 GANON_API const char *ganon_last_error(ganon_ctx *ctx);
+/* Page-locked host memory (hipHostMalloc) for the host side of large device copies: the FASTQ
+ * records a job formats on the device land in it by DMA, with no staging copy on the host's cores.
+ * Returns GANON_OK or GANON_E_NOMEM. */
+GANON_API int ganon_pinned_alloc(int64_t bytes, void **out);
+GANON_API int ganon_pinned_free(void *p);
 GANON_API int ganon_abi_version(void);
 /* Use an external hipStream_t (e.g. torch's current stream); NULL = the ctx's own. */
 GANON_API int ganon_ctx_set_stream(ganon_ctx *ctx, void *hip_stream);

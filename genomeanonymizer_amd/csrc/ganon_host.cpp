@@ -520,6 +520,10 @@ struct ganon_bam_reader {
   std::vector<std::vector<int64_t>> linear;   // per tid: the linear index (first record of each 16 kb window)
   int64_t cur_voff = -1;             // forward cursor: the first record not yet consumed
   int32_t cur_tid = 0;
+  ganon_buf_alloc_fn balloc = nullptr;   // ganon_bam_reader_set_buffer_alloc: the scans' inflated bytes in
+  ganon_buf_free_fn bfree = nullptr;     // a page-locked buffer kept across scans (pbuf, pcap)
+  uint8_t *pbuf = nullptr;
+  int64_t pcap = 0;
   ganon_inflate_fn inflater = nullptr;   // ganon_bam_reader_set_inflater: block windows inflated by it
   void *inflater_user = nullptr;
   int64_t inflater_min = 64;             // ... when they hold at least this many blocks
@@ -527,13 +531,62 @@ struct ganon_bam_reader {
 
 namespace {
 
+// The inflated bytes of one scan: the reader's page-locked buffer when it has a buffer allocator
+// (the GPU inflater's device-to-host copies then land by DMA, with no staging copy on the host's
+// cores; the buffer is reused by the reader's next scan: the columns are copied out of it), else a
+// fresh huge-page buffer.
+struct ScanBuf {
+  ganon_bam_reader *R;
+  RawVec<uint8_t> own;
+  size_t n = 0;
+  bool pinned;
+  explicit ScanBuf(ganon_bam_reader *r) : R(r), pinned(r->balloc != nullptr) {}
+  uint8_t *data() { return pinned ? R->pbuf : own.data(); }
+  size_t size() const { return pinned ? n : own.size(); }
+  bool empty() const { return size() == 0; }
+  void clear() {
+    if (pinned) n = 0;
+    else own.clear();
+  }
+  uint8_t &operator[](size_t i) { return data()[i]; }
+  bool grow(size_t m) {   // (pinned) capacity for m bytes, contents kept
+    if ((int64_t)m <= R->pcap) return true;
+    const size_t cap = std::max(m, (size_t)(2 * R->pcap));
+    void *p = nullptr;
+    if (R->balloc((int64_t)cap, &p) != 0 || !p) return false;
+    if (n) std::memcpy(p, R->pbuf, n);
+    if (R->pbuf) R->bfree(R->pbuf);
+    R->pbuf = static_cast<uint8_t *>(p);
+    R->pcap = (int64_t)cap;
+    return true;
+  }
+  void reserve(size_t c) {
+    if (pinned) {
+      if (!grow(c)) throw std::bad_alloc();
+    } else {
+      huge_reserve(own, c);
+    }
+  }
+  void resize(size_t m) {
+    if (pinned) {
+      if (!grow(m)) throw std::bad_alloc();
+      n = m;
+    } else {
+      huge_resize(own, m);
+    }
+  }
+};
+inline void buf_resize(RawVec<uint8_t> &v, size_t m) { huge_resize(v, m); }
+inline void buf_resize(ScanBuf &v, size_t m) { v.resize(m); }
+
 constexpr int32_t kTidEnd = INT32_MAX;
 inline int64_t tid_order(int32_t t) { return t < 0 ? (int64_t)INT32_MAX : (int64_t)t; }   // unplaced last
 
 // Reads and inflates complete BGZF blocks starting at file offset coff (at most R->chunk compressed
 // bytes). Appends the inflated bytes to data and one (data offset, file offset) pair per non-empty
 // block to bmap. Returns the file offset after the last complete block, or -1 on error.
-int64_t read_blocks(ganon_bam_reader *R, int64_t coff, int64_t step, RawVec<uint8_t> &data,
+template <class Buf>
+int64_t read_blocks(ganon_bam_reader *R, int64_t coff, int64_t step, Buf &data,
                     std::vector<std::pair<int64_t, int64_t>> &bmap) {
   auto tph = PhClock::now();
   const int64_t want = std::min<int64_t>(std::max<int64_t>(step, 1 << 17), R->fsize - coff);
@@ -569,7 +622,7 @@ int64_t read_blocks(ganon_bam_reader *R, int64_t coff, int64_t step, RawVec<uint
   }
   if (off == 0) return set_err("truncated BGZF block");
   const size_t base = data.size();
-  huge_resize(data, base + (size_t)total);
+  buf_resize(data, base + (size_t)total);
   lap(kPhParse, tph);
   if (R->inflater && (int64_t)blocks.size() >= R->inflater_min) {
     const size_t nb = blocks.size();
@@ -604,7 +657,7 @@ int64_t voff_at(const std::vector<std::pair<int64_t, int64_t>> &bmap, int64_t x)
 // record met (kTidEnd when none) so that an index start can be validated. hint: expected compressed
 // bytes of the sequence (index span) or 0; the step read and inflated at a time starts there (or at
 // 1 MiB) and doubles up to the reader's window, so a small sequence never inflates a whole window.
-int scan_tid(ganon_bam_reader *R, int64_t voff, int32_t tid, int64_t hint, RawVec<uint8_t> &data,
+int scan_tid(ganon_bam_reader *R, int64_t voff, int32_t tid, int64_t hint, ScanBuf &data,
              std::vector<int64_t> &recs, int64_t &next_voff, int32_t &next_tid, int32_t &first_tid) {
   // (the records stay where they were inflated: `data` grows by every window and only the offsets of
   // the sequence's records are kept — round 6; the windows' consumed bytes used to be dropped and the
@@ -676,7 +729,7 @@ int64_t record_end(const uint8_t *d) {
 // region semantics: pos < end and bam_endpos > beg), in file order; stops at the first record of
 // another sequence or at pos >= end. Runs of kept records are copied to kept at once.
 int scan_region(ganon_bam_reader *R, int64_t voff, int32_t tid, int64_t beg, int64_t end, int64_t hint,
-                RawVec<uint8_t> &data, std::vector<int64_t> &recs) {
+                ScanBuf &data, std::vector<int64_t> &recs) {
   // (records stay in place in `data`, their offsets in recs: as scan_tid)
   int64_t step = std::min<int64_t>(hint > 0 ? hint + (1 << 16) : (1 << 20), R->chunk);
   int64_t coff = voff >> 16;
@@ -840,6 +893,17 @@ GANON_HOST_API int ganon_bam_reader_set_window(ganon_bam_reader *R, int64_t byte
   return 0;
 }
 
+GANON_HOST_API int ganon_bam_reader_set_buffer_alloc(ganon_bam_reader *R, ganon_buf_alloc_fn alloc,
+                                                     ganon_buf_free_fn free_fn) {
+  if (!R || (!alloc) != (!free_fn)) return set_err("ganon_bam_reader_set_buffer_alloc: bad arguments");
+  if (R->pbuf) R->bfree(R->pbuf);
+  R->pbuf = nullptr;
+  R->pcap = 0;
+  R->balloc = alloc;
+  R->bfree = free_fn;
+  return 0;
+}
+
 GANON_HOST_API int ganon_bam_reader_set_inflater(ganon_bam_reader *R, ganon_inflate_fn fn, void *user,
                                                  int64_t min_blocks) {
   if (!R || min_blocks < 1) return set_err("ganon_bam_reader_set_inflater: bad arguments");
@@ -861,7 +925,7 @@ GANON_HOST_API int ganon_bam_reader_contig(ganon_bam_reader *R, int32_t tid, gan
   *out = nullptr;
   if (tid < 0 || tid >= (int32_t)R->header.ref_len.size()) return set_err("tid out of range");
   try {
-    RawVec<uint8_t> data;
+    ScanBuf data(R);
     std::vector<int64_t> recs;
     int64_t next_voff = -1;
     int32_t next_tid = kTidEnd, first_tid = kTidEnd;
@@ -875,7 +939,7 @@ GANON_HOST_API int ganon_bam_reader_contig(ganon_bam_reader *R, int32_t tid, gan
         const int64_t hint = e > beg ? (e >> 16) - (beg >> 16) : 0;
         // the sequence's blocks, inflated, at ~3.5x their compressed span (address space only: an
         // underestimate just grows the buffer)
-        huge_reserve(data, (size_t)hint * 7 / 2 + (4 << 20));
+        data.reserve((size_t)hint * 7 / 2 + (4 << 20));
         if (scan_tid(R, beg, tid, hint, data, recs, next_voff, next_tid, first_tid) != 0) return -1;
         done = first_tid == tid;   // a stale index falls back to the forward scan
         if (!done) recs.clear();
@@ -911,7 +975,7 @@ GANON_HOST_API int ganon_bam_reader_region(ganon_bam_reader *R, int32_t tid, int
   if (!R->has_index) return set_err("region reads need the BAM index");
   if (beg < 0 || end < beg) return set_err("bad region");
   try {
-    RawVec<uint8_t> data;
+    ScanBuf data(R);
     std::vector<int64_t> recs;
     const int64_t first = R->index_beg[(size_t)tid];
     if (first >= 0 && end > beg) {
@@ -928,7 +992,7 @@ GANON_HOST_API int ganon_bam_reader_region(ganon_bam_reader *R, int32_t tid, int
       const int64_t span = e > voff ? (e >> 16) - (voff >> 16) : 0;
       const int64_t len = R->header.ref_len[(size_t)tid];
       const int64_t hint = len > 0 ? std::min<int64_t>(span, span * (end - beg) / len + (1 << 20)) : 0;
-      huge_reserve(data, (size_t)hint * 7 / 2 + (4 << 20));
+      data.reserve((size_t)hint * 7 / 2 + (4 << 20));
       if (scan_region(R, voff, tid, beg, end, hint, data, recs) != 0) return -1;
     }
     auto *bam = new ganon_bam();
@@ -949,6 +1013,7 @@ GANON_HOST_API int ganon_bam_reader_region(ganon_bam_reader *R, int32_t tid, int
 GANON_HOST_API void ganon_bam_reader_close(ganon_bam_reader *R) {
   if (!R) return;
   if (R->map) munmap(const_cast<uint8_t *>(R->map), (size_t)R->fsize);
+  if (R->pbuf) R->bfree(R->pbuf);
   if (R->fh) std::fclose(R->fh);
   delete R;
 }

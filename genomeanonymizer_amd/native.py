@@ -252,7 +252,7 @@ EXPORTED_HOST_SYMBOLS = (
     "ganon_blob_free", "ganon_objects_create", "ganon_objects_free", "ganon_objects_add_job", "ganon_objects_add_plain",
     "ganon_objects_run", "ganon_objects_take", "ganon_objects_settle", "ganon_objects_last_error",
     "ganon_objects_take_all", "ganon_aux_sa_count", "ganon_fastq_edit", "ganon_gather_ranges", "ganon_gather_ranges2", "ganon_host_phase_times",
-    "ganon_bam_reader_set_inflater",
+    "ganon_bam_reader_set_inflater", "ganon_bam_reader_set_buffer_alloc",
 )
 
 
@@ -710,9 +710,11 @@ def host_format_fastq(recs: dict) -> bytes:
 
 
 def _addr(buf) -> int:
-    """Address of a bytes object's or a contiguous numpy array's data."""
+    """Address of a bytes object's, a ctypes array's or a contiguous numpy array's data."""
     if isinstance(buf, np.ndarray):
         return buf.ctypes.data
+    if isinstance(buf, C.Array):
+        return C.addressof(buf)
     return C.cast(C.c_char_p(buf), C.c_void_p).value or 0
 
 
@@ -1477,6 +1479,7 @@ def host_lib():
     lib.ganon_gather_ranges2.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_int64, _u8p, _i64p, _i64p,
                                          C.c_char_p, C.c_int64]
     lib.ganon_gather_ranges2.restype = C.c_int64
+    lib.ganon_bam_reader_set_buffer_alloc.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
     lib.ganon_host_phase_times.argtypes = [C.POINTER(C.c_double), C.c_int, C.c_int]
     lib.ganon_host_phase_times.restype = C.c_int
     lib.ganon_fastq_edit.argtypes = [C.c_int64, C.c_char_p, _i64p, _u8p, _i32p, _i64p, _i64p, C.c_char_p, _i64p,

@@ -87,6 +87,14 @@ typedef int (*ganon_inflate_fn)(void *user, const uint8_t *comp, int64_t comp_le
                                 int64_t n_blocks, uint8_t *out, int64_t out_total);
 GANON_HOST_API int ganon_bam_reader_set_inflater(ganon_bam_reader *reader, ganon_inflate_fn fn, void *user,
                                                  int64_t min_blocks);
+/* Where the reader's scans put their inflated bytes: a buffer from alloc (grown through it, freed
+ * through free_fn, kept across the reader's scans) instead of fresh pageable memory — with
+ * ganon_pinned_alloc / ganon_pinned_free (include/ganon.h) the GPU inflater's device-to-host copies
+ * go by DMA. alloc returns 0 on success. NULL, NULL restores fresh buffers. */
+typedef int (*ganon_buf_alloc_fn)(int64_t bytes, void **out);
+typedef int (*ganon_buf_free_fn)(void *p);
+GANON_HOST_API int ganon_bam_reader_set_buffer_alloc(ganon_bam_reader *reader, ganon_buf_alloc_fn alloc,
+                                                     ganon_buf_free_fn free_fn);
 GANON_HOST_API int ganon_bam_reader_header(ganon_bam_reader *reader, ganon_bam_view *view);
 GANON_HOST_API int ganon_bam_reader_contig(ganon_bam_reader *reader, int32_t tid, ganon_bam **out);
 /* The records of tid overlapping [beg, end) (0-based; htslib's region semantics: pos < end and

@@ -368,9 +368,35 @@ def test_decoded_blobs_are_views_kept_alive(tmp_path):
     del junk
 
 
-def test_region_reader_matches_fetch(tmp_path):
+def _python_buffer_alloc():
+    """A ganon_buf_alloc_fn / ganon_buf_free_fn pair over ctypes buffers (the page-locked allocator's
+    stand-in on the CPU), with the live blocks and the number of allocations."""
+    import ctypes as C
+    live, calls = {}, [0]
+    AF = C.CFUNCTYPE(C.c_int, C.c_int64, C.POINTER(C.c_void_p))
+    FF = C.CFUNCTYPE(C.c_int, C.c_void_p)
+
+    def alloc(n, out):
+        b = C.create_string_buffer(int(n))
+        live[C.addressof(b)] = b
+        out[0] = C.addressof(b)
+        calls[0] += 1
+        return 0
+
+    def free(p):
+        live.pop(p, None)
+        return 0
+    return AF(alloc), FF(free), live, calls
+
+
+@pytest.mark.parametrize("scan_buffer", ["fresh", "reader_owned"])
+def test_region_reader_matches_fetch(scan_buffer, tmp_path):
     """ganon_bam_reader_region (BAI linear index, htslib overlap semantics, placed unmapped records
-    at [pos, pos + 1)) against the whole-file table's fetch on random regions of a multi-window BAM."""
+    at [pos, pos + 1)) against the whole-file table's fetch on random regions of a multi-window BAM;
+    with the scans' bytes in fresh buffers, and in one buffer the reader keeps and reuses across its
+    scans (ganon_bam_reader_set_buffer_alloc: page-locked with the GPU inflater)."""
+    import ctypes as C
+    from genomeanonymizer_amd import native
     from genomeanonymizer_amd.io.bam import BamReader, ReadTable
     from genomeanonymizer_amd.synth.fastpair import make_pair
     d = str(tmp_path / "in")
@@ -380,6 +406,10 @@ def test_region_reader_matches_fetch(tmp_path):
         path = os.path.join(d, f"{key}.bam")
         full = ReadTable(path)
         rd = BamReader(path, 4)
+        if scan_buffer == "reader_owned":
+            af, ff, live, calls = _python_buffer_alloc()
+            rd._keep_alloc = (af, ff)
+            native.host_lib().ganon_bam_reader_set_buffer_alloc(rd._h, C.cast(af, C.c_void_p), C.cast(ff, C.c_void_p))
         assert rd.has_index
         for tid, (name, L) in enumerate(zip(full.ref_names, full.ref_lens)):
             for _ in range(20):
@@ -390,7 +420,14 @@ def test_region_reader_matches_fetch(tmp_path):
                 assert got.n == len(exp)
                 assert np.array_equal(np.asarray(got.pos), np.asarray(full.pos)[exp])
                 assert np.array_equal(np.asarray(got.flag), np.asarray(full.flag)[exp])
+                assert np.array_equal(np.asarray(got.qual), np.concatenate([np.asarray(full.qual)[
+                    int(full.qual_off[i]):int(full.qual_off[i]) + int(full.l_seq[i])] for i in exp]) if len(exp)
+                    else np.zeros(0, np.uint8))
+            # contig scans use the same buffer
+            assert rd.contig(tid).n == int((np.asarray(full.tid) == tid).sum())
         rd.close()
+        if scan_buffer == "reader_owned":
+            assert calls[0] >= 1 and not live    # grown through the allocator, freed at close
 
 
 def _rank_worker_timing(rank, world, port, paths, outdir, q):

@@ -134,7 +134,22 @@ def auto_job_bp(genome_len: int, world: int) -> int:
     return int(min(4_000_000, max(256_000, genome_len // max(1, per_rank * world))))
 
 
-def plan_jobs(fasta: FastaRef, windows: Sequence[Window], job_bp: int, indexed: bool) -> List[JobSpec]:
+def job_targets(genome_len: int, job_bp: int, world: int, taper: float):
+    """Target length of job k (a function): ``job_bp`` each, except that with several ranks the first
+    and the last ``world`` jobs — every rank's first and last job under round-robin ownership — are
+    ``taper`` x shorter and the jobs between them longer by what those give up. A rank's first job's
+    decode + plan is waited for with nothing to overlap it, and its last job's format + write drains
+    alone: shorter ones shorten both ends of every rank's pipeline (GANON_JOB_TAPER, default 0.5;
+    1 = equal jobs)."""
+    n = max(1, int(round(genome_len / max(1, job_bp))))
+    if world <= 1 or taper >= 1.0 or n < 3 * world:
+        return lambda k: job_bp
+    small = max(1, int(job_bp * taper))
+    mid = max(small, (genome_len - 2 * world * small) // max(1, n - 2 * world))
+    return lambda k: small if k < world or k >= n - world else mid
+
+
+def plan_jobs(fasta: FastaRef, windows: Sequence[Window], job_bp: int, indexed: bool, target=None) -> List[JobSpec]:
     """The sample's jobs in FASTA then section order. ``job_bp`` > 0 and indexed BAMs: each contig
     longer than job_bp is cut at section boundaries into runs of about job_bp bases (a short tail
     joins the run before it); else one job per contig. A contig whose sections do not tile it (the
@@ -152,14 +167,15 @@ def plan_jobs(fasta: FastaRef, windows: Sequence[Window], job_bp: int, indexed: 
                  all(w.first <= w.last for w in ss) and
                  all(ss[k].first == ss[k - 1].last + 1 for k in range(1, len(ss))))
         cuts = [0]
+        tgt = target or (lambda k: job_bp)     # (job_targets: the k-th job's length)
         if tiles and L > job_bp:
             acc = 0
             for k, w in enumerate(ss):
                 acc += w.last - w.first + 1
-                if acc >= job_bp and k + 1 < len(ss):
+                if acc >= tgt(len(out) + len(cuts) - 1) and k + 1 < len(ss):
                     cuts.append(k + 1)
                     acc = 0
-            if len(cuts) > 1 and ss[-1].last - ss[cuts[-1]].first + 1 < job_bp // 2:
+            if len(cuts) > 1 and ss[-1].last - ss[cuts[-1]].first + 1 < tgt(len(out) + len(cuts) - 1) // 2:
                 cuts.pop()
         if len(cuts) == 1:
             out.append(JobSpec(len(out), c, ci, None, None, int(L)))
@@ -1024,7 +1040,9 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
     # the rest idled half the wall — round 5's 30x chromosome-scale line)
     job_bp = int(os.environ.get("GANON_JOB_BP", "0") or 0) if "GANON_JOB_BP" in os.environ else \
         auto_job_bp(sum(int(L) for L in fasta.lengths), world)
-    jobs = plan_jobs(fasta, windows, job_bp, all(r.has_index for r in readers))
+    genome_len = sum(int(L) for L in fasta.lengths)
+    jobs = plan_jobs(fasta, windows, job_bp, all(r.has_index for r in readers),
+                     job_targets(genome_len, job_bp, world, float(os.environ.get("GANON_JOB_TAPER", "1"))))
     # The readers' BGZF windows inflate on this rank's GPU (a context of its own per reader: the two
     # samples decode at once) when the masking engine is the GPU's and a job's reads come in windows of at least GANON_GPU_INFLATE_MIN blocks (default 512,
     # ~18 MB compressed: a block takes milliseconds on its wave, so only large windows pay off, and

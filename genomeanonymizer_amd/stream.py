@@ -473,7 +473,8 @@ class Job(JobPrep):
             # masked bases stay on the device unless a later stage needs them on the host (records
             # left to on-demand formatting, complex names' objects): fetched now, while the engine's
             # job batch still holds them
-            if not self.fmt.preformat(*self._format_instances()) or len(self.objs):
+            nb = self.tables[0].n + self.tables[1].n   # (_format_instances: every read once first)
+            if not self.fmt.preformat(*self._format_instances(), n_base=nb) or len(self.objs):
                 _ = self.res.seq_out
         t4 = time.time()
         self.cx = self._complex_ingredients()

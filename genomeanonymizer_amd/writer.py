@@ -13,7 +13,7 @@
 from __future__ import annotations
 
 import itertools
-from typing import Dict, List, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -25,6 +25,17 @@ from .planner import Plan
 
 OUTSIDE_WINDOWS = "outside_windows,-,-,-"
 STAT_HEADER = ["#SEQ", "#FIRST", "#LAST", "#SNV", "#DEL", "#INS", "#DUP", "#INV", "#CNV", "#TRA", "#SGL"]
+
+
+class _Pre:
+    """A job's pre-formatted records (FastqFormatter.preformat): ``base`` (or None) the masked scope
+    of every read's own copy, in row order (tumor then normal), its record at index row (+ the tumor
+    rows); ``keys`` the sorted instance keys of the other records, at indices len(base) + rank;
+    ``off`` / ``len`` each record's range in ``data`` (bytes, or a page-locked uint8 array)."""
+    __slots__ = ("base", "keys", "off", "len", "data")
+
+    def __init__(self, base, keys, off, ln, data):
+        self.base, self.keys, self.off, self.len, self.data = base, keys, off, ln, data
 
 
 class FastqFormatter:
@@ -44,7 +55,7 @@ class FastqFormatter:
         self._name_base = (0, len(tables[0].names_blob))
         self.edited: Dict[Tuple[int, int, int], bytes] = {}   # indel-edited records (write_fastqs)
         self.edited2: Dict[Tuple[int, int, int], bytes] = {}  # the same with the left-overs applied twice
-        self._pre = None     # (sorted instance keys, offsets, lengths, bytes) of preformat()
+        self._pre = None     # preformat()'s blob: _Pre
         self._left_keys = None   # sorted keys of the instances with left-over edits
 
     def _seq_bufs(self, masked: bool = True) -> list:
@@ -128,15 +139,40 @@ class FastqFormatter:
         pos = np.minimum(np.searchsorted(lk, k), len(lk) - 1)
         return np.nonzero(lk[pos] == k)[0]
 
+    def _locate(self, ds, row, sc) -> Optional[np.ndarray]:
+        """Indices in the pre-formatted blob of the records (ds, row, sc), or None when one is not in it.
+        A read's own copy (its masked scope, or unmasked) is found by its row directly; other copies by
+        a search of the few extra keys."""
+        pre = self._pre
+        if pre is None or len(ds) == 0:
+            return None
+        ds = np.asarray(ds, np.int64)
+        row = np.asarray(row, np.int64)
+        sc = np.asarray(sc, np.int64)
+        if pre.base is None:
+            k = self._key(ds, row, sc)
+            pos = np.minimum(np.searchsorted(pre.keys, k), len(pre.keys) - 1)
+            return pos if np.array_equal(pre.keys[pos], k) else None
+        g = row + ds * self.tables[0].n
+        idx = g.copy()
+        miss = np.nonzero(pre.base[g] != sc)[0]
+        if len(miss):
+            if not len(pre.keys):
+                return None
+            k = self._key(ds[miss], row[miss], sc[miss])
+            pos = np.minimum(np.searchsorted(pre.keys, k), len(pre.keys) - 1)
+            if not np.array_equal(pre.keys[pos], k):
+                return None
+            idx[miss] = len(pre.base) + pos
+        return idx
+
     def _native(self, ds, row, sc) -> bytes:
         if len(ds) == 0:
             return b""
-        pre = self._pre
-        if pre is not None:      # slices of the job's pre-formatted records
-            k = self._key(ds, row, sc)
-            pos = np.minimum(np.searchsorted(pre[0], k), len(pre[0]) - 1)
-            if np.array_equal(pre[0][pos], k):
-                return native.gather_ranges(pre[3], pre[1][pos], pre[2][pos])
+        idx = self._locate(ds, row, sc)
+        if idx is not None:      # slices of the job's pre-formatted records
+            pre = self._pre
+            return native.gather_ranges(pre.data, pre.off[idx], pre.len[idx])
         return self._format(ds, row, sc)
 
     def _format(self, ds, row, sc) -> bytes:
@@ -147,13 +183,21 @@ class FastqFormatter:
             raise TypeError(f"reverse read {self.tables[d].name(r)!r} has a base outside ACGTN: the "
                             "reference's reverse complement fails on it (SURVEY Q7)") from None
 
-    def preformat(self, ds, row, sc) -> bool:
+    def preformat(self, ds, row, sc, n_base: int = 0) -> bool:
         """Format the instances a job can write in ONE formatter call (the device round trip costs
         more than the bytes); later record runs are sliced out of it. A reverse read with a base
         outside ACGTN is left out (its error is raised only if it is written, as in the
         reference); after a few such reads the job formats on demand. True when every instance was
-        formatted (no later record run needs the masked bases on the host)."""
+        formatted (no later record run needs the masked bases on the host).
+
+        ``n_base``: the first n_base instances are every read of the tumor then the normal table once,
+        in row order (Job._format_instances): they are formatted in that order and found by row, the
+        rest are de-duplicated against them and searched by key (sorting every instance key of a job
+        and searching them cost the 30x line ~0.8 CPU-s, tools/cpu_sampler.py)."""
         ds, row, sc = (np.asarray(x, np.int64) for x in (ds, row, sc))
+        T, N = self.tables
+        if n_base and n_base == T.n + N.n and len(ds) >= n_base and self._preformat_base(ds, row, sc, n_base):
+            return True
         key = self._key(ds, row, sc)
         key, first = np.unique(key, return_index=True)
         ds, row, sc = ds[first], row[first], sc[first]
@@ -175,9 +219,37 @@ class FastqFormatter:
                 ds, row, sc, key = ds[keep], row[keep], sc[keep], key[keep]
                 continue
             ln = self._plain_lengths(ds, row)
-            self._pre = (key, np.concatenate([[0], np.cumsum(ln)[:-1]]).astype(np.int64), ln, data)
+            self._pre = _Pre(None, key, np.concatenate([[0], np.cumsum(ln)[:-1]]).astype(np.int64), ln, data)
             return len(ds) == n_all
         return False
+
+    def _preformat_base(self, ds, row, sc, nb: int) -> bool:
+        """preformat's structured case (no record refused by the formatter; else False, nothing kept)."""
+        base_sc = sc[:nb]
+        e_ds, e_row, e_sc = ds[nb:], row[nb:], sc[nb:]
+        if len(e_ds):   # extras that are not a read's own copy, once each, by key
+            own = base_sc[e_row + e_ds * self.tables[0].n] == e_sc
+            e_ds, e_row, e_sc = e_ds[~own], e_row[~own], e_sc[~own]
+            ekey, first = np.unique(self._key(e_ds, e_row, e_sc), return_index=True)
+            e_ds, e_row, e_sc = e_ds[first], e_row[first], e_sc[first]
+        else:
+            ekey = np.zeros(0, np.int64)
+        a_ds = np.concatenate([ds[:nb], e_ds])
+        a_row = np.concatenate([row[:nb], e_row])
+        a_sc = np.concatenate([base_sc, e_sc])
+        try:
+            data = None
+            if self.device_backend is not None:
+                recs = self.records_arrays(a_ds, a_row, a_sc, seq_bufs=False)
+                recs["seq_base1"] = len(self.tables[0].seq)
+                data = self.device_backend(recs, self.res.device_gen)
+            if data is None:
+                data = self.backend(self.records_arrays(a_ds, a_row, a_sc))
+        except native.FastqBadRecord:
+            return False
+        ln = self._plain_lengths(a_ds, a_row)
+        self._pre = _Pre(base_sc.copy(), ekey, np.concatenate([[0], np.cumsum(ln)[:-1]]).astype(np.int64), ln, data)
+        return True
 
     def edited_bytes(self, inst, reapply: int = 0) -> bytes:
         """Record of an instance with left-over edits, applied once or (reapply) twice (cached)."""
@@ -285,12 +357,10 @@ class FastqFormatter:
     def _ranges(self, ds, row, sc):
         """(source bytes, offsets, lengths) of the records of ``ds, row, sc`` (unedited): ranges of
         the pre-formatted blob when it holds every one, else one formatter call's output."""
-        pre = self._pre
-        if pre is not None and len(ds):
-            k = self._key(ds, row, sc)
-            pos = np.minimum(np.searchsorted(pre[0], k), len(pre[0]) - 1)
-            if np.array_equal(pre[0][pos], k):
-                return pre[3], pre[1][pos], pre[2][pos]
+        idx = self._locate(ds, row, sc)
+        if idx is not None:
+            pre = self._pre
+            return pre.data, pre.off[idx], pre.len[idx]
         data = self._format(ds, row, sc) if len(ds) else b""
         ln = self._plain_lengths(ds, row)
         return data, np.concatenate([[0], np.cumsum(ln)[:-1]]).astype(np.int64) if len(ds) else ln, ln

@@ -664,6 +664,13 @@ def _check_fastq(recs: dict) -> None:
             raise GanonError(f"FASTQ record array {k} must be C-contiguous {np.dtype(dt)}")
 
 
+def _names_ptr(names):
+    """The names blob (bytes or a uint8 array) as the formatter's char pointer, without a copy."""
+    if isinstance(names, np.ndarray) and names.dtype == np.uint8 and names.flags["C_CONTIGUOUS"]:
+        return C.cast(_addr(names), C.c_char_p)    # (alive in the caller's record dict)
+    return names if isinstance(names, bytes) else bytes(names)
+
+
 def _fastq_args(recs: dict) -> tuple:
     """The host formatter's argument list (minus out/cap) over a ``fastq_records`` dict."""
     _check_fastq(recs)
@@ -672,7 +679,7 @@ def _fastq_args(recs: dict) -> tuple:
     P = lambda k, t: recs[k].ctypes.data_as(t)
     return (len(recs["seq_len"]), seq_ptrs, P("seq_sel", _u8p), P("seq_nib_off", _i64p), P("seq_len", _i32p),
             P("reverse", _u8p), qual_ptrs, P("qual_sel", _u8p), P("qual_off", _i64p), P("qual_len", _i32p),
-            P("qual_rev", _u8p), bytes(recs["names"]), P("name_off", _i64p), P("name_len", _i32p),
+            P("qual_rev", _u8p), _names_ptr(recs["names"]), P("name_off", _i64p), P("name_len", _i32p),
             P("mate", _u8p))
 
 
@@ -692,9 +699,11 @@ def _c_fastq_records(recs: dict, seq_batch=None):
     qp = (_u8p * len(recs["qual_bufs"]))(*[b.ctypes.data_as(_u8p) for b in recs["qual_bufs"]])
     keep.append(qp)
     c.qual_buf = qp
-    names = bytes(recs["names"])
+    names = recs["names"]
+    if not isinstance(names, (bytes, np.ndarray)):
+        names = bytes(names)
     keep.append(names)
-    c.names = names
+    c.names = C.cast(_addr(names), C.c_char_p)     # (in place: a job's names blob is not copied)
     for k, dt in FASTQ_ARRAYS.items():
         setattr(c, k, recs[k].ctypes.data_as(_PTR_OF[dt]))
     return c, keep

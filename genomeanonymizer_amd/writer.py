@@ -51,7 +51,7 @@ class FastqFormatter:
         self.backend = backend or native.host_format_fastq
         self.device_backend = device_backend
         self._qual_bufs = [tables[0].qual, tables[1].qual]
-        self._names = tables[0].names_blob.tobytes() + tables[1].names_blob.tobytes()
+        self._names = np.concatenate([np.asarray(tables[0].names_blob, np.uint8), np.asarray(tables[1].names_blob, np.uint8)])
         self._name_base = (0, len(tables[0].names_blob))
         self.edited: Dict[Tuple[int, int, int], bytes] = {}   # indel-edited records (write_fastqs)
         self.edited2: Dict[Tuple[int, int, int], bytes] = {}  # the same with the left-overs applied twice

@@ -214,7 +214,7 @@ def test_preformat_slices_match_direct_formatting_and_defer_q7():
     direct = FastqFormatter(tables, res)
     pre = FastqFormatter(tables, res)
     pre.preformat(ds, row, sc)
-    assert pre._pre is not None and len(pre._pre[0]) == 7        # the Q7 read left out, not raised
+    assert pre._pre is not None and len(pre._pre.keys) == 7      # the Q7 read left out, not raised
     good = np.array([0, 2, 3, 4, 5, 6, 7])
     order = good[::-1]                                            # any order, any subset
     assert pre._native(ds[order], row[order], sc[order]) == direct._native(ds[order], row[order], sc[order])
@@ -222,3 +222,28 @@ def test_preformat_slices_match_direct_formatting_and_defer_q7():
         pre._native(ds[:3], row[:3], sc[:3])
     assert pre.unedited([(1, 2, -1), (0, 4, -1)]) == [direct._native(np.array([1]), np.array([2]), np.array([-1])),
                                                       direct._native(np.array([0]), np.array([4]), np.array([-1]))]
+
+
+def test_preformat_by_row_matches_direct_formatting():
+    """preformat's structured case (Job._format_instances: every read once in row order, then further
+    copies): the reads' own records found by row, the others by key — duplicates of a read's own copy
+    dropped — equal to formatting directly, in any order; a refused read falls back to the keyed case."""
+    from genomeanonymizer_amd.writer import FastqFormatter
+    tables, res = _toy_tables()
+    tables[0].seq[tables[0].seq_off[1]] = 0x12        # (no Q7 read: the structured case holds)
+    nb = tables[0].n + tables[1].n
+    ds = np.array([0] * 5 + [1] * 3 + [0, 1, 0, 0], np.int64)
+    row = np.array([0, 1, 2, 3, 4, 0, 1, 2, 2, 1, 3, 2], np.int64)
+    sc = np.array([-1] * 8 + [-1, -1, -1, -1], np.int64)
+    sc[nb:] = [-1, -1, -1, -1]
+    direct = FastqFormatter(tables, res)
+    pre = FastqFormatter(tables, res)
+    assert pre.preformat(ds, row, sc, n_base=nb)
+    assert pre._pre.base is not None and len(pre._pre.keys) == 0      # every extra is a read's own copy
+    order = np.random.default_rng(1).permutation(nb)
+    assert pre._native(ds[order], row[order], sc[order]) == direct._native(ds[order], row[order], sc[order])
+    # the Q7 read: refused by the formatter -> the keyed case, the read left out
+    tables2, res2 = _toy_tables()
+    pre2 = FastqFormatter(tables2, res2)
+    pre2.preformat(ds, row, sc, n_base=nb)
+    assert pre2._pre.base is None and len(pre2._pre.keys) == 7

@@ -420,7 +420,7 @@ int columns(ganon_ctx *ctx, const uint8_t *d, int64_t p, int64_t n, ganon_bam_dc
       }
       if ((rc = check_launch(ctx, "k_bam_check"))) return rc;
       HIP_OR_FAIL(hipMemcpyAsync(info, K.info, sizeof info, hipMemcpyDeviceToHost, s));
-      HIP_OR_FAIL(hipStreamSynchronize(s));
+      HIP_OR_FAIL(ganon_detail::sync_stream(s));
       // every chunk before the first failing one is exact: a bad walk there is the stream's error
       if (info[2] != ~0ull && info[2] < info[1])
         return fail(ctx, GANON_E_ARG, "ganon_bam_columns: bad record size (chunk %lld)", (long long)info[2]);
@@ -443,7 +443,7 @@ int columns(ganon_ctx *ctx, const uint8_t *d, int64_t p, int64_t n, ganon_bam_dc
   int64_t nr = 0;
   if (n_chunks) {
     HIP_OR_FAIL(hipMemcpyAsync(&nr, base + n_chunks, 8, hipMemcpyDeviceToHost, s));
-    HIP_OR_FAIL(hipStreamSynchronize(s));
+    HIP_OR_FAIL(ganon_detail::sync_stream(s));
   }
   // per-record columns: 12 int32 + 6 int64 (5 offsets of nr + 1, the record offsets) + the sizes
   ganon_bam_cols &V = H->v;
@@ -492,7 +492,7 @@ int columns(ganon_ctx *ctx, const uint8_t *d, int64_t p, int64_t n, ganon_bam_dc
     HIP_OR_FAIL(hipMemcpyAsync(&bad_rec, first_bad, 8, hipMemcpyDeviceToHost, s));
     int64_t *offs[5] = {V.name_off, V.cig_off, V.seq_off, V.qual_off, V.aux_off};
     for (int k = 0; k < 5; ++k) HIP_OR_FAIL(hipMemcpyAsync(&tot[k], offs[k] + nr, 8, hipMemcpyDeviceToHost, s));
-    HIP_OR_FAIL(hipStreamSynchronize(s));
+    HIP_OR_FAIL(ganon_detail::sync_stream(s));
     if (bad_rec != ~0ull)
       return fail(ctx, GANON_E_ARG, "ganon_bam_columns: record %lld: fields exceed block size", (long long)bad_rec);
     V.names_bytes = tot[0];
@@ -541,7 +541,7 @@ GANON_API int ganon_bam_columns(ganon_ctx *ctx, const uint8_t *stream, int64_t p
   *out = nullptr;
   if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, GANON_E_DEVICE, "hipSetDevice failed");
   if (ctx->profiling) {   // a profiled call: ganon_last_kernel_times reports this call's kernels alone
-    hipStreamSynchronize(ctx->stream);
+    ganon_detail::sync_stream(ctx->stream);
     for (auto &r : ctx->recs) {
       ctx->pool.push_back(r.e0);
       ctx->pool.push_back(r.e1);
@@ -557,8 +557,8 @@ GANON_API int ganon_bam_columns(ganon_ctx *ctx, const uint8_t *stream, int64_t p
     }
     // (waited for: the kernel events that follow time the record walk, not the copy)
     if (hipMemcpyAsync(H->stream, stream, (size_t)n, hipMemcpyHostToDevice, ctx->stream) != hipSuccess ||
-        hipStreamSynchronize(ctx->stream) != hipSuccess) {
-      hipStreamSynchronize(ctx->stream);
+        ganon_detail::sync_stream(ctx->stream) != hipSuccess) {
+      ganon_detail::sync_stream(ctx->stream);
       release(ctx, H);
       return fail(ctx, GANON_E_DEVICE, "ganon_bam_columns: stream copy failed");
     }
@@ -566,7 +566,7 @@ GANON_API int ganon_bam_columns(ganon_ctx *ctx, const uint8_t *stream, int64_t p
   }
   const int rc = columns(ctx, d, p, n, H);
   if (rc) {
-    hipStreamSynchronize(ctx->stream);
+    ganon_detail::sync_stream(ctx->stream);
     release(ctx, H);
     return rc;
   }
@@ -601,15 +601,15 @@ GANON_API int ganon_bam_dcols_download(ganon_ctx *ctx, const ganon_bam_dcols *c,
   for (const auto &x : i64) ok = ok && cp(x.first, x.second, nr * 8);
   ok = ok && cp(host->names, V.names, V.names_bytes) && cp(host->cigar, V.cigar, 4 * V.cigar_ops) &&
        cp(host->seq, V.seq, V.seq_bytes) && cp(host->qual, V.qual, V.qual_bytes) && cp(host->aux, V.aux, V.aux_bytes);
-  if (!ok || hipStreamSynchronize(s) != hipSuccess) {
-    hipStreamSynchronize(s);
+  if (!ok || ganon_detail::sync_stream(s) != hipSuccess) {
+    ganon_detail::sync_stream(s);
     return fail(ctx, GANON_E_DEVICE, "ganon_bam_dcols_download: copy failed");
   }
   return GANON_OK;
 }
 
 GANON_API int ganon_bam_dcols_free(ganon_ctx *ctx, ganon_bam_dcols *c) {
-  if (ctx) hipStreamSynchronize(ctx->stream);
+  if (ctx) ganon_detail::sync_stream(ctx->stream);
   release(ctx, c);
   return GANON_OK;
 }

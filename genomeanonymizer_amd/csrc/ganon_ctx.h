@@ -6,7 +6,9 @@
 
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstdlib>
+#include <thread>
 
 #include <cstdarg>
 #include <cstdio>
@@ -158,6 +160,36 @@ inline int check_launch(ganon_ctx *ctx, const char *what) {
   if (sync_check && (e = hipDeviceSynchronize()) != hipSuccess)
     return fail(ctx, GANON_E_DEVICE, "%s failed: %s", what, hipGetErrorString(e));
   return GANON_OK;
+}
+
+// Wait for the work queued on stream s without keeping a core busy: an event recorded on s and
+// polled with sleeps of 2-100 us. HIP's own waits spin or yield, and with eight processes on one GPU
+// (the end-to-end line) the waiting threads took cores from the decode and output threads of the
+// GPU's host CPU share. GANON_SLEEP_SYNC=0: hipStreamSynchronize (A/B). One event per host thread
+// and device.
+inline hipError_t sync_stream(hipStream_t s) {
+  static const bool sleepy = [] {
+    const char *v = std::getenv("GANON_SLEEP_SYNC");
+    return !(v && v[0] == '0');
+  }();
+  if (!sleepy) return hipStreamSynchronize(s);
+  thread_local hipEvent_t ev = nullptr;
+  thread_local int ev_dev = -1;
+  int dev = 0;
+  hipError_t r = hipGetDevice(&dev);
+  if (r != hipSuccess) return r;
+  if (!ev || ev_dev != dev) {
+    if ((r = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return r;
+    ev_dev = dev;
+  }
+  if ((r = hipEventRecord(ev, s)) != hipSuccess) return r;
+  unsigned us = 2;
+  for (;;) {
+    r = hipEventQuery(ev);
+    if (r != hipErrorNotReady) return r;
+    std::this_thread::sleep_for(std::chrono::microseconds(us));
+    us = us < 100 ? 2 * us : 100;
+  }
 }
 
 }  // namespace ganon_detail

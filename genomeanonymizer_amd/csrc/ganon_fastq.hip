@@ -1671,7 +1671,7 @@ GANON_API int ganon_fastq_upload(ganon_ctx *ctx, const ganon_fastq_records *in, 
     HIP_OR_FAIL(hipMemcpyAsync(f->len, len.data(), len.size() * sizeof(uint32_t), hipMemcpyHostToDevice, ctx->stream));
   }
   HIP_OR_FAIL(hipMemsetAsync(f->err, 0xFF, sizeof(unsigned long long), ctx->stream));
-  HIP_OR_FAIL(hipStreamSynchronize(ctx->stream));   // the host staging vectors die here
+  HIP_OR_FAIL(ganon_detail::sync_stream(ctx->stream));   // the host staging vectors die here
   *out = f;
   return GANON_OK;
 }
@@ -1740,7 +1740,7 @@ GANON_API int64_t ganon_fastq_download(ganon_ctx *ctx, ganon_fastq *f, char *out
   unsigned long long bad = ~0ull;
   if (f->n && hipMemcpyAsync(&bad, f->err, sizeof bad, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess)
     return fail(ctx, GANON_E_DEVICE, "error-slot copy failed"), kFailed;
-  if (hipStreamSynchronize(ctx->stream) != hipSuccess) return fail(ctx, GANON_E_DEVICE, "formatter run failed"), kFailed;
+  if (ganon_detail::sync_stream(ctx->stream) != hipSuccess) return fail(ctx, GANON_E_DEVICE, "formatter run failed"), kFailed;
   if (bad != ~0ull) {
     fail(ctx, GANON_E_ARG, "record %llu: reverse read with a base outside ACGTN (SURVEY Q7)", bad);
     return -(int64_t)bad - 1;
@@ -1750,7 +1750,7 @@ GANON_API int64_t ganon_fastq_download(ganon_ctx *ctx, ganon_fastq *f, char *out
     return INT64_MIN;
   }
   if (f->total && (hipMemcpyAsync(out, f->out, f->total, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
-                   hipStreamSynchronize(ctx->stream) != hipSuccess))
+                   ganon_detail::sync_stream(ctx->stream) != hipSuccess))
     return fail(ctx, GANON_E_DEVICE, "output copy failed"), kFailed;
   return (int64_t)f->total;
 }

@@ -1842,7 +1842,7 @@ int ref_create(ganon_ctx *ctx, const uint8_t *nt16, int64_t bytes, ganon_ref **o
     rc = check_launch(ctx, "k_ref2");
   }
   if (!rc) rc = ganon_ref_blocks(ctx, r);
-  if (!rc && hipStreamSynchronize(ctx->stream) != hipSuccess) rc = fail(ctx, GANON_E_DEVICE, "reference upload sync failed");
+  if (!rc && ganon_detail::sync_stream(ctx->stream) != hipSuccess) rc = fail(ctx, GANON_E_DEVICE, "reference upload sync failed");
   if (rc) {
     free_ref(r);
     return rc;
@@ -1957,7 +1957,7 @@ int host_copy(ganon_ctx *ctx, const ganon_dbatch *db, HostCopy &h) {
       (rc = d2h_vec(ctx, h.span_start, B.span_start, (size_t)db->n_scopes)) ||
       (rc = d2h_vec(ctx, h.span_len, B.span_len, (size_t)db->n_scopes)))
     return rc;
-  HIP_OR_FAIL(hipStreamSynchronize(ctx->stream));
+  HIP_OR_FAIL(ganon_detail::sync_stream(ctx->stream));
   ganon_batch &b = h.b;
   b.n_reads = db->n_reads;
   b.n_scopes = db->n_scopes;
@@ -2058,7 +2058,7 @@ int load_batch(ganon_ctx *ctx, ganon_dbatch *db, const ganon_batch *b, const gan
   for (int32_t s = 0; s < b->n_scopes; ++s) max_si = std::max(max_si, b->scope_incid_off[s + 1] - b->scope_incid_off[s]);
   if (b->n_incid >= INT32_MAX) return fail(ctx, GANON_E_ARG, "more than 2^31-1 incidences");
   int rc;
-  HIP_OR_FAIL(hipStreamSynchronize(ctx->stream));   // a previous run of db may still read its buffers
+  HIP_OR_FAIL(ganon_detail::sync_stream(ctx->stream));   // a previous run of db may still read its buffers
   db->ran = false;
   db->max_scope_incid = max_si;
   if (shared) {
@@ -2127,7 +2127,7 @@ int load_batch(ganon_ctx *ctx, ganon_dbatch *db, const ganon_batch *b, const gan
   // bytes outside every read are never written by the masking kernels: make them defined
   HIP_OR_FAIL(hipMemsetAsync(db->out, 0, (size_t)b->seq_bytes + 16, ctx->stream));
   if ((rc = prepare(ctx, db, b, ctx->spec_plan == 2))) return rc;   // (2: testing knob)
-  HIP_OR_FAIL(hipStreamSynchronize(ctx->stream));
+  HIP_OR_FAIL(ganon_detail::sync_stream(ctx->stream));
   return GANON_OK;
 }
 
@@ -2138,7 +2138,7 @@ int upload_common(ganon_ctx *ctx, const ganon_batch *b, const ganon_ref *ref, ga
   ganon_dbatch *db = new ganon_dbatch();
   int rc = load_batch(ctx, db, b, ref);
   if (rc) {
-    hipStreamSynchronize(ctx->stream);
+    ganon_detail::sync_stream(ctx->stream);
     free_batch(db);
     delete db;
     return rc;
@@ -2179,7 +2179,7 @@ GANON_API int ganon_ctx_destroy(ganon_ctx *ctx) {
   if (!ctx) return GANON_E_ARG;
   hipSetDevice(ctx->device);
   if (ctx->own) {
-    hipStreamSynchronize(ctx->own);
+    ganon_detail::sync_stream(ctx->own);
     hipStreamDestroy(ctx->own);
   }
   for (auto &r : ctx->recs) {
@@ -2326,7 +2326,7 @@ GANON_API int ganon_ref_free(ganon_ctx *ctx, ganon_ref *ref) {
   if (!ref) return GANON_E_ARG;
   if (ctx) {
     hipSetDevice(ctx->device);
-    hipStreamSynchronize(ctx->stream);
+    ganon_detail::sync_stream(ctx->stream);
   }
   free_ref(ref);
   return GANON_OK;
@@ -2469,7 +2469,7 @@ GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
 
 GANON_API int ganon_batch_sync(ganon_ctx *ctx) {
   if (!ctx) return GANON_E_ARG;
-  HIP_OR_FAIL(hipStreamSynchronize(ctx->stream));
+  HIP_OR_FAIL(ganon_detail::sync_stream(ctx->stream));
   if (ctx->profiling) {
     ctx->last_times.clear();
     for (auto &r : ctx->recs) {
@@ -2512,7 +2512,7 @@ GANON_API int ganon_batch_download(ganon_ctx *ctx, ganon_dbatch *db, uint8_t *se
   unsigned long long far_need = 0;
   HIP_OR_FAIL(hipMemcpyAsync(&status, db->status, sizeof status, hipMemcpyDeviceToHost, st));
   HIP_OR_FAIL(hipMemcpyAsync(&far_need, db->far_need, sizeof far_need, hipMemcpyDeviceToHost, st));
-  HIP_OR_FAIL(hipStreamSynchronize(st));
+  HIP_OR_FAIL(ganon_detail::sync_stream(st));
   if (status & 4) {
     // a speculative replan the batch did not fit (a read with several segments, a longer read, a
     // huge scope): plan it in full and run it again
@@ -2528,7 +2528,7 @@ GANON_API int ganon_batch_download(ganon_ctx *ctx, ganon_dbatch *db, uint8_t *se
     if ((rc = ganon_prep::batch_error(ctx, db))) return rc;
     HIP_OR_FAIL(hipMemcpyAsync(&status, db->status, sizeof status, hipMemcpyDeviceToHost, st));
     HIP_OR_FAIL(hipMemcpyAsync(&far_need, db->far_need, sizeof far_need, hipMemcpyDeviceToHost, st));
-    HIP_OR_FAIL(hipStreamSynchronize(st));
+    HIP_OR_FAIL(ganon_detail::sync_stream(st));
   }
   if (status & 2) {
     // a written read its write scope does not list (or lists twice): name it
@@ -2564,7 +2564,7 @@ GANON_API int ganon_batch_download(ganon_ctx *ctx, ganon_dbatch *db, uint8_t *se
     HIP_OR_FAIL(hipMemcpyAsync(scope_bases_out, db->scope_bases, (size_t)db->n_scopes * 4, hipMemcpyDeviceToHost, st));
   if (totals_out)
     HIP_OR_FAIL(hipMemcpyAsync(totals_out, db->totals, GANON_N_TOTALS * 8, hipMemcpyDeviceToHost, st));
-  HIP_OR_FAIL(hipStreamSynchronize(st));
+  HIP_OR_FAIL(ganon_detail::sync_stream(st));
   if (status & 1) return fail(ctx, GANON_E_STATE, "far-mask list overflowed after growing: output invalid");
   return GANON_OK;
 }
@@ -2573,7 +2573,7 @@ GANON_API int ganon_batch_free(ganon_ctx *ctx, ganon_dbatch *db) {
   if (!db) return GANON_E_ARG;
   if (ctx) {
     hipSetDevice(ctx->device);
-    hipStreamSynchronize(ctx->stream);
+    ganon_detail::sync_stream(ctx->stream);
   }
   free_batch(db);
   delete db;
@@ -2600,7 +2600,7 @@ GANON_API int ganon_batch_gated_runs(ganon_ctx *ctx, ganon_dbatch *db, int64_t *
   HIP_OR_FAIL(hipSetDevice(ctx->device));
   unsigned long long g = 0;
   HIP_OR_FAIL(hipMemcpyAsync(&g, db->gated, sizeof g, hipMemcpyDeviceToHost, ctx->stream));
-  HIP_OR_FAIL(hipStreamSynchronize(ctx->stream));
+  HIP_OR_FAIL(ganon_detail::sync_stream(ctx->stream));
   *out = (int64_t)g;
   return GANON_OK;
 }
@@ -2609,7 +2609,7 @@ GANON_API int ganon_batch_path_counts(ganon_ctx *ctx, ganon_dbatch *db, int64_t 
   if (!ctx || !db || !out4) return fail(ctx, GANON_E_ARG, "null argument");
   HIP_OR_FAIL(hipSetDevice(ctx->device));
   HIP_OR_FAIL(hipMemcpyAsync(out4, db->paths, 4 * sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
-  HIP_OR_FAIL(hipStreamSynchronize(ctx->stream));
+  HIP_OR_FAIL(ganon_detail::sync_stream(ctx->stream));
   return GANON_OK;
 }
 

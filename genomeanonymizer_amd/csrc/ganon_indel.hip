@@ -932,7 +932,7 @@ int run_tally(ganon_ctx *ctx, ganon_indels *t) {
     const long long caps[8] = {t->n_obs, t->n_rcand_cap, t->recs_cap, t->V.n_reads, t->V.n_scopes, t->n_list, t->n_ilist,
                                t->n_rdist};
     HIP_OR_FAIL(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_indel_cap), caps, sizeof caps, 0, hipMemcpyHostToDevice, ctx->stream));
-    HIP_OR_FAIL(hipStreamSynchronize(ctx->stream));   // (caps is a stack array)
+    HIP_OR_FAIL(ganon_detail::sync_stream(ctx->stream));   // (caps is a stack array)
   }
 #endif
   const unsigned rgrid = (unsigned)((t->n_rdist + kIndelWaves - 1) / kIndelWaves);
@@ -1192,7 +1192,7 @@ GANON_API int ganon_indel_upload(ganon_ctx *ctx, const ganon_batch *b, const gan
     if (e == hipSuccess) e = hipMemcpyAsync(t->nval, &nv, sizeof nv, hipMemcpyHostToDevice, ctx->stream);
     if (e == hipSuccess) e = hipMemsetAsync(t->cnt + ilist.size(), 0, sizeof(int32_t), ctx->stream);   // scan tails
     if (e == hipSuccess) e = hipMemsetAsync(t->rcnt + rdist.size(), 0, sizeof(int32_t), ctx->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e == hipSuccess) e = ganon_detail::sync_stream(ctx->stream);
     if (e != hipSuccess) return bail(fail(ctx, GANON_E_DEVICE, "indel upload copy failed: %s", hipGetErrorString(e)));
   }
   *out = t;
@@ -1223,7 +1223,7 @@ GANON_API int64_t ganon_indel_download(ganon_ctx *ctx, ganon_indels *t, ganon_in
   int32_t cand = 0;
   hipError_t e = hipMemcpyAsync(&total, t->counters, sizeof total, hipMemcpyDeviceToHost, ctx->stream);
   if (e == hipSuccess) e = hipMemcpyAsync(&cand, t->n_dev(), sizeof cand, hipMemcpyDeviceToHost, ctx->stream);
-  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (e == hipSuccess) e = ganon_detail::sync_stream(ctx->stream);
   t->n_candidates = cand;
   if (e != hipSuccess) return fail(ctx, GANON_E_DEVICE, "indel download: %s", hipGetErrorString(e));
   if (int crc = indel_check_result(ctx)) return crc;
@@ -1243,7 +1243,7 @@ GANON_API int64_t ganon_indel_download(ganon_ctx *ctx, ganon_indels *t, ganon_in
     const long long rcap = t->recs_cap;
     e = hipMemcpyToSymbolAsync(HIP_SYMBOL(g_indel_cap), &rcap, sizeof rcap, 2 * sizeof(long long), hipMemcpyHostToDevice,
                                ctx->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e == hipSuccess) e = ganon_detail::sync_stream(ctx->stream);
     if (e != hipSuccess) return fail(ctx, GANON_E_DEVICE, "indel download: %s", hipGetErrorString(e));
   }
 #endif
@@ -1258,7 +1258,7 @@ GANON_API int64_t ganon_indel_download(ganon_ctx *ctx, ganon_indels *t, ganon_in
   int rc = check_launch(ctx, "k_indel_write");
   if (rc) return rc;
   e = hipMemcpyAsync(out, t->recs, (size_t)total * sizeof(ganon_indel_rec), hipMemcpyDeviceToHost, ctx->stream);
-  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (e == hipSuccess) e = ganon_detail::sync_stream(ctx->stream);
   if (e != hipSuccess) return fail(ctx, GANON_E_DEVICE, "indel download: %s", hipGetErrorString(e));
   if ((rc = indel_check_result(ctx))) return rc;
   return (int64_t)total;
@@ -1281,7 +1281,7 @@ GANON_API int ganon_indel_free(ganon_ctx *ctx, ganon_indels *t) {
   if (!t) return GANON_OK;
   if (ctx) {
     hipSetDevice(ctx->device);
-    hipStreamSynchronize(ctx->stream);
+    ganon_detail::sync_stream(ctx->stream);
   }
   ind_release(t);
   delete t;

@@ -867,7 +867,7 @@ template <typename T>
 int grow_dev(ganon_ctx *ctx, T **p, size_t &cap, size_t need) {
   if (*p && cap >= need) return GANON_OK;
   if (*p) {
-    hipStreamSynchronize(ctx->stream);
+    ganon_detail::sync_stream(ctx->stream);
     hipFree(*p);
     *p = nullptr;
   }
@@ -983,8 +983,8 @@ GANON_API int ganon_inflate(ganon_ctx *ctx, const uint8_t *comp, int64_t comp_le
     }
     if ((rc = check_launch(ctx, "k_inflate"))) {
       // copies from / into the caller's buffers may still be queued: they end before it gets them back
-      hipStreamSynchronize(cs);
-      hipStreamSynchronize(s);
+      ganon_detail::sync_stream(cs);
+      ganon_detail::sync_stream(s);
       return rc;
     }
     okc = hipEventRecord(st->ev[2 * c + 1], s) == hipSuccess && (c == 0 || d2h(c - 1));
@@ -992,10 +992,10 @@ GANON_API int ganon_inflate(ganon_ctx *ctx, const uint8_t *comp, int64_t comp_le
   std::vector<int32_t> stat(nb);
   okc = okc && d2h(n_chunks - 1) &&
         hipMemcpyAsync(stat.data(), st->status, nb * 4, hipMemcpyDeviceToHost, cs) == hipSuccess &&
-        hipStreamSynchronize(cs) == hipSuccess;
+        ganon_detail::sync_stream(cs) == hipSuccess;
   if (!okc) {
-    hipStreamSynchronize(cs);
-    hipStreamSynchronize(s);
+    ganon_detail::sync_stream(cs);
+    ganon_detail::sync_stream(s);
     return fail(ctx, GANON_E_DEVICE, "ganon_inflate: copy failed");
   }
   if ((rc = ganon_batch_sync(ctx))) return rc;   // (collects the kernel times when profiling)
@@ -1027,7 +1027,7 @@ GANON_API int ganon_inflate_hostcb(void *ctx, const uint8_t *comp, int64_t comp_
 void ganon_inflate_free(ganon_inflate_state *st) {
   if (!st) return;
   if (st->copy) {
-    hipStreamSynchronize(st->copy);
+    ganon_detail::sync_stream(st->copy);
     hipStreamDestroy(st->copy);
   }
   for (hipEvent_t e : st->ev) hipEventDestroy(e);

@@ -1706,7 +1706,7 @@ int grow(ganon_ctx *ctx, DBuf &b, size_t bytes) {
   if (b.p && b.bytes >= need) return GANON_OK;
   const size_t old = b.bytes;
   if (b.p) {
-    hipStreamSynchronize(ctx->stream);   // a previous run may still read it
+    ganon_detail::sync_stream(ctx->stream);   // a previous run may still read it
     hipFree(b.p);
     b.p = nullptr;
     b.bytes = 0;
@@ -1752,7 +1752,7 @@ int size_plan(ganon_ctx *ctx, ganon_dbatch *db, int64_t ng, int tgt0, const Raw 
     if ((rc = launch_groups(ctx, db, R)) || (rc = launch_emit(ctx, db, R, 0))) return rc;
     std::vector<unsigned long long> cur(2 * kCursors, 0);
     HIP_OR_FAIL(hipMemcpyAsync(cur.data(), db->cursor, kCursors * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
-    HIP_OR_FAIL(hipStreamSynchronize(st));
+    HIP_OR_FAIL(ganon_detail::sync_stream(st));
     unsigned long long tseg = 0;
     for (int k = 0; k < kCursors; ++k) {
       cur[kCursors + k] = tseg;
@@ -1918,7 +1918,7 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db, bool allow_spec) {
   HIP_OR_FAIL(hipMemcpyAsync(&n_long, long_count, sizeof n_long, hipMemcpyDeviceToHost, st));
   if (db->fused)
     HIP_OR_FAIL(hipMemcpyAsync(xc.data(), db->xcount, xc.size() * sizeof(unsigned int), hipMemcpyDeviceToHost, st));
-  HIP_OR_FAIL(hipStreamSynchronize(st));
+  HIP_OR_FAIL(ganon_detail::sync_stream(st));
   if (!e.code && n_long) {
     // reads with long CIGARs: a wave each, then the reduction again over both sets of partials
     KernelScope ks(ctx, "prep_scan_long");
@@ -1934,7 +1934,7 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db, bool allow_spec) {
     if ((rc = check_launch(ctx, "k_prep_scan_long"))) return rc;
     HIP_OR_FAIL(hipMemcpyAsync(info, db->plan_info, sizeof info, hipMemcpyDeviceToHost, st));
     HIP_OR_FAIL(hipMemcpyAsync(&e, db->err, sizeof e, hipMemcpyDeviceToHost, st));
-    HIP_OR_FAIL(hipStreamSynchronize(st));
+    HIP_OR_FAIL(ganon_detail::sync_stream(st));
   }
   if (e.code) return fail(ctx, GANON_E_ARG, err_text(e.code), e.index, e.a, e.b);
   const unsigned long long max_len = info[3], max_seg = info[4];
@@ -2003,7 +2003,7 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db, bool allow_spec) {
       HIP_OR_FAIL(hipMemcpyAsync(&rb_last, rbase + nr - 1, sizeof rb_last, hipMemcpyDeviceToHost, st));
       HIP_OR_FAIL(hipMemcpyAsync(&ns_last, nseg + nr - 1, sizeof ns_last, hipMemcpyDeviceToHost, st));
     }
-    HIP_OR_FAIL(hipStreamSynchronize(st));
+    HIP_OR_FAIL(ganon_detail::sync_stream(st));
     db->scost = cost;
     ng = last[0] / db->group_target + 1;
     db->n_rrec = rb_last + ns_last;
@@ -2061,7 +2061,7 @@ int ws_diag(ganon_ctx *ctx, ganon_dbatch *db) {
 int batch_error(ganon_ctx *ctx, ganon_dbatch *db) {
   PrepErr e{};
   HIP_OR_FAIL(hipMemcpyAsync(&e, db->err, sizeof e, hipMemcpyDeviceToHost, ctx->stream));
-  HIP_OR_FAIL(hipStreamSynchronize(ctx->stream));
+  HIP_OR_FAIL(ganon_detail::sync_stream(ctx->stream));
   if (e.code) return fail(ctx, GANON_E_ARG, err_text(e.code), e.index, e.a, e.b);
   return GANON_OK;
 }

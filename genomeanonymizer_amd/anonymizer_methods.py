@@ -62,6 +62,20 @@ class MaskResult:
         return 2 * o
 
 
+def _seq_buffer(parts, extra=None) -> np.ndarray:
+    """The batch's bases (the tables' blobs back to back, then the further copies) in one page-locked
+    block when the GPU engine is loaded (native.PINNED: the batch upload then goes by DMA instead of
+    through the runtime's staging copies), else in fresh memory."""
+    parts = [np.asarray(p, np.uint8) for p in parts] + ([np.asarray(extra, np.uint8)] if extra is not None else [])
+    n = sum(len(p) for p in parts)
+    out = native.PINNED.take(n) if n >= (8 << 20) and native.hip_loaded() else np.empty(n, np.uint8)
+    at = 0
+    for p in parts:
+        out[at:at + len(p)] = p
+        at += len(p)
+    return out
+
+
 def build_batch(plan: Plan, tables: Tuple[ReadTable, ReadTable], fasta: FastaRef,
                 scope_ids=None, written=None) -> Tuple[dict, dict]:
     """Lay the plan's scopes (all, or the subset ``scope_ids`` of one contig shard) out as
@@ -133,7 +147,7 @@ def build_batch(plan: Plan, tables: Tuple[ReadTable, ReadTable], fasta: FastaRef
     if nd:
         src = np.repeat(np.where(d0, 0, len(T.seq)) + pick("seq_off"), nbytes) + \
             (np.arange(int(nbytes.sum())) - np.repeat(np.concatenate([[0], np.cumsum(nbytes)[:-1]]), nbytes))
-        seq_all = np.concatenate([T.seq, N.seq, np.concatenate([T.seq, N.seq])[src]])
+        seq_all = _seq_buffer([T.seq, N.seq], np.concatenate([T.seq, N.seq])[src])
         # re-point the copy's scope incidences at the copy
         inc_k = np.repeat(np.arange(len(scopes), dtype=np.int64), counts)
         M = n_reads + nd + 1
@@ -150,10 +164,10 @@ def build_batch(plan: Plan, tables: Tuple[ReadTable, ReadTable], fasta: FastaRef
             arr[f] = np.concatenate([arr[f], v.astype(dt)])
         ws = np.concatenate([ws, d_k.astype(np.int32)])
     else:
-        seq_all = np.concatenate([T.seq, N.seq])
+        seq_all = _seq_buffer([T.seq, N.seq])
     dup_off = dict(zip(zip(d_ds.tolist(), d_row.tolist(), d_sc.tolist()), d_seq.tolist()))
     dup_rows = list(zip(d_ds.tolist(), d_row.tolist()))
-    arr["seq_nt16"] = np.ascontiguousarray(seq_all.astype(np.uint8))
+    arr["seq_nt16"] = seq_all
     arr["write_scope"] = ws
     arr["scope_incid_off"] = incid_off
     arr["incid_read"] = incid

@@ -21,6 +21,8 @@
 //   k_finish: far masks, totals.
 // The reference genome is resident (ganon_ref): nt16 + a 2-bit copy + a non-ACGT block map.
 #include <hip/hip_runtime.h>
+#include <map>
+#include <mutex>
 
 #include <algorithm>
 #include <cstdarg>
@@ -2195,18 +2197,52 @@ GANON_API int ganon_ctx_destroy(ganon_ctx *ctx) {
 
 GANON_API const char *ganon_last_error(ganon_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
+// Page-locked blocks are cached per process (up to 8 GiB): pinning and unpinning hundreds of MB per
+// reader and run (the readers' scan buffers, the FASTQ blobs) cost more than the copies they save.
+namespace {
+std::mutex g_pin_mu;
+std::multimap<size_t, void *> g_pin_free;   // capacity -> block
+std::map<void *, size_t> g_pin_cap;         // every live or cached block's capacity
+size_t g_pin_cached = 0;
+constexpr size_t kPinCacheMax = size_t(8) << 30;
+}  // namespace
+
 GANON_API int ganon_pinned_alloc(int64_t bytes, void **out) {
   if (!out || bytes < 0) return GANON_E_ARG;
   *out = nullptr;
-  if (hipHostMalloc(out, (size_t)std::max<int64_t>(bytes, 1), hipHostMallocDefault) != hipSuccess) {
+  const size_t want = (size_t)std::max<int64_t>(bytes, 1);
+  {
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    auto it = g_pin_free.lower_bound(want);
+    if (it != g_pin_free.end() && it->first <= 2 * want + (size_t(16) << 20)) {
+      *out = it->second;
+      g_pin_cached -= it->first;
+      g_pin_free.erase(it);
+      return GANON_OK;
+    }
+  }
+  const size_t cap = (want + (size_t(2) << 20) - 1) & ~((size_t(2) << 20) - 1);
+  if (hipHostMalloc(out, cap, hipHostMallocDefault) != hipSuccess) {
     *out = nullptr;
     return GANON_E_NOMEM;
   }
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  g_pin_cap[*out] = cap;
   return GANON_OK;
 }
 
 GANON_API int ganon_pinned_free(void *p) {
-  if (p) hipHostFree(p);
+  if (!p) return GANON_OK;
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  auto it = g_pin_cap.find(p);
+  if (it == g_pin_cap.end()) return GANON_E_ARG;
+  if (g_pin_cached + it->second <= kPinCacheMax) {
+    g_pin_free.emplace(it->second, p);
+    g_pin_cached += it->second;
+  } else {
+    g_pin_cap.erase(it);
+    hipHostFree(p);
+  }
   return GANON_OK;
 }
 

@@ -142,6 +142,14 @@ _hip = None
 _host = None
 
 
+_HIP_CONTEXTS = [0]   # HipMasker contexts created in this process (page-locked buffers need a GPU)
+
+
+def hip_loaded() -> bool:
+    """Whether this process drives the GPU (a HipMasker exists): page-locked staging only then."""
+    return _HIP_CONTEXTS[0] > 0
+
+
 def hip_lib():
     """Load libganon_hip.so (raises GanonError if it is missing)."""
     global _hip
@@ -392,41 +400,23 @@ class GpuInflater:
 
 
 class PinnedPool:
-    """Page-locked host blocks (ganon_pinned_alloc) handed out as numpy uint8 views and taken back when
-    the last view is gone (weakref.finalize on the block): the device formatter's records of a job
-    land in one by DMA — into pageable memory the runtime staged every byte through a host copy,
-    ~1 CPU-second per 5 GB of FASTQ (tools/cpu_sampler.py on the 30x line). Free blocks are kept for
-    reuse up to ``keep`` bytes; sizes are rounded to 16 MiB."""
-
-    def __init__(self, keep: int = 2 << 30):
-        self.keep = keep
-        self.free: list = []          # (capacity, address)
-        self.lock = threading.Lock()
+    """Page-locked host blocks (ganon_pinned_alloc: cached per process in libganon_hip.so) handed out
+    as numpy uint8 views and given back when the last view is gone (weakref.finalize on the block):
+    the device formatter's records of a job land in one by DMA — into pageable memory the runtime
+    staged every byte through a host copy, ~1 CPU-second per 5 GB of FASTQ (tools/cpu_sampler.py on
+    the 30x line). Sizes are rounded to 16 MiB so that blocks are reused across jobs."""
 
     def take(self, n: int) -> np.ndarray:
         cap = max(16 << 20, -(-n // (16 << 20)) * (16 << 20))
-        addr = None
-        with self.lock:
-            best = None
-            for i, (c, a) in enumerate(self.free):
-                if cap <= c <= 2 * cap and (best is None or c < self.free[best][0]):
-                    best = i
-            if best is not None:
-                cap, addr = self.free.pop(best)
-        if addr is None:
-            ptr = _p()
-            if hip_lib().ganon_pinned_alloc(cap, C.byref(ptr)) != 0 or not ptr.value:
-                return np.empty(n, np.uint8)      # (no page-locked memory left: pageable)
-            addr = ptr.value
-        block = (C.c_uint8 * cap).from_address(addr)
-        weakref.finalize(block, self._give_back, cap, addr)
+        ptr = _p()
+        if hip_lib().ganon_pinned_alloc(cap, C.byref(ptr)) != 0 or not ptr.value:
+            return np.empty(n, np.uint8)      # (no page-locked memory left: pageable)
+        block = (C.c_uint8 * cap).from_address(ptr.value)
+        weakref.finalize(block, PinnedPool._give_back, ptr.value)
         return np.frombuffer(block, np.uint8, count=n)
 
-    def _give_back(self, cap: int, addr: int) -> None:
-        with self.lock:
-            if sum(c for c, _ in self.free) + cap <= self.keep:
-                self.free.append((cap, addr))
-                return
+    @staticmethod
+    def _give_back(addr: int) -> None:
         hip_lib().ganon_pinned_free(_p(addr))
 
 
@@ -445,6 +435,7 @@ class HipMasker:
             raise GanonError(f"ganon_ctx_create(device={device}) failed with {rc}: "
                              "no usable gfx950 device (there is no CPU fallback)")
         self._h = h
+        _HIP_CONTEXTS[0] += 1
         self.device = device
         self._ref = None            # (the host array, its DeviceRef): the genome stays resident
         self._job_db = None         # the device batch of the last mask(indels=True), reloaded per job

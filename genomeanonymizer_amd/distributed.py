@@ -21,6 +21,7 @@ on the default ``nccl`` group.
 """
 from __future__ import annotations
 
+import atexit
 import os
 import pickle
 import queue
@@ -79,11 +80,33 @@ def _world_key(dist):
     return id(pg), pg
 
 
+def release_side_groups(dist=None, stale_only_for=None) -> None:
+    """Destroy the cached side groups (all of them, or those not of world key ``stale_only_for``). Called
+    before the default group goes (genome_anonymizer.py, tools/e2e_bench.py) and at exit: a cached
+    gloo group left to the interpreter's teardown destroyed its threads while joinable
+    ("terminate called without an active exception" after a clean 8-rank run, round 6)."""
+    if dist is None:
+        try:
+            import torch.distributed as dist
+        except Exception:   # pragma: no cover
+            return
+    for key in list(_SIDE_GROUPS):
+        if stale_only_for is not None and key[1] == stale_only_for:
+            continue
+        group, _ = _SIDE_GROUPS.pop(key)
+        try:
+            dist.destroy_process_group(group)
+        except Exception:   # noqa: BLE001  (its world is gone already)
+            pass
+
+
+atexit.register(release_side_groups)
+
+
 def take_side_group(dist, purpose: str):
     k, _ = _world_key(dist)
     # groups cached under another (destroyed) world are released: they are never reused
-    for key in [x for x in _SIDE_GROUPS if x[1] != k]:
-        _SIDE_GROUPS.pop(key, None)
+    release_side_groups(dist, stale_only_for=k)
     hit = _SIDE_GROUPS.pop((purpose, k), None)
     return hit[0] if hit is not None else dist.new_group(backend="gloo")
 

@@ -106,6 +106,8 @@ def run_anonymizer(argv=None) -> None:
         tots = run_pairs_sharded(vcfs, samples, config.reference, anonymizer, outputs, bool(config.record_statistics),
                                  dist, threads=max(1, config.cpu))
         logging.info("rank %d totals %s", dist.get_rank(), tots)
+        from .distributed import release_side_groups
+        release_side_groups(dist)
         dist.destroy_process_group()
     else:
         run_short_read_tumor_normal_anonymizer(vcfs, samples, config.reference, anonymizer, outputs,

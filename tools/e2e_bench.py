@@ -216,6 +216,8 @@ def main():
     if rank == 0:
         print(json.dumps(res))
     if dist is not None:
+        from genomeanonymizer_amd.distributed import release_side_groups
+        release_side_groups(dist)
         dist.destroy_process_group()
 
 

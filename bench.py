@@ -397,8 +397,10 @@ def e2e_lines(args) -> dict:
             cgen = time.perf_counter() - t
             cov = 2 * args.e2e_chrom_pairs * 150 / args.e2e_chrom_len
             stage("e2e: chromosome-scale runs")
+            # (a warm run, then two timed runs: the best is the value, both are in wall_s_runs; single runs
+            # spread ~2-4 % on one box)
             ch = _child_json([sys.executable, tool, cin, os.path.join(d, "chrom_out"), "stream"],
-                             {"E2E_RUNS": "1", "E2E_WORKERS": str(args.e2e_workers), "E2E_DISK_PROBE": "1"}, 900)
+                             {"E2E_RUNS": "2", "E2E_WORKERS": str(args.e2e_workers), "E2E_DISK_PROBE": "1"}, 900)
             cs = ch.get("stream", {})
             env1 = {"E2E_RUNS": "1", "GANON_JOB_BP": "0"}
             one = _child_json([sys.executable, tool, cin, os.path.join(d, "chrom_one"), "stream"], env1, 900,
@@ -428,7 +430,7 @@ def e2e_lines(args) -> dict:
             res["e2e"]["chromosome_scale"] = {
                 "value": cs.get("reads_per_s"), "unit": "reads/s", "bases_per_sec": cs.get("bases_per_s"),
                 "reads": cs.get("reads"), "workers": args.e2e_workers, "wall_s": cs.get("stages_s", {}).get("wall_s"),
-                "critical_path_s_rank0": cs.get("critical_path_s_rank0"),
+                "wall_s_runs": cs.get("wall_s_runs"), "critical_path_s_rank0": cs.get("critical_path_s_rank0"),
                 "stages_s_rank0": cs.get("stages_s"), "peak_rss_mb_rank0": cs.get("peak_rss_mb"),
                 "output_bytes": cs.get("output_bytes"), "jobs": cs.get("jobs"), "generate_s": round(cgen, 1),
                 "disk": ch.get("disk"),

@@ -2,6 +2,7 @@
 // See include/ganon_host.h. Written from the SAM/BAM v1 specification.
 #include <dlfcn.h>
 #include <sys/mman.h>
+#include <unistd.h>
 #include <zlib.h>
 
 #include <algorithm>
@@ -524,6 +525,8 @@ struct ganon_bam_reader {
   ganon_buf_free_fn bfree = nullptr;     // a page-locked buffer kept across scans (pbuf, pcap)
   uint8_t *pbuf = nullptr;
   int64_t pcap = 0;
+  uint8_t *cbuf = nullptr;               // (with balloc) the compressed windows for the GPU inflater,
+  int64_t ccap = 0;                      // read by pread into page-locked memory
   ganon_inflate_fn inflater = nullptr;   // ganon_bam_reader_set_inflater: block windows inflated by it
   void *inflater_user = nullptr;
   int64_t inflater_min = 64;             // ... when they hold at least this many blocks
@@ -594,7 +597,27 @@ int64_t read_blocks(ganon_bam_reader *R, int64_t coff, int64_t step, Buf &data,
   // cache directly; no serial copy, no fresh buffer to fault in per window), else read into a buffer
   RawVec<uint8_t> buf;
   const uint8_t *comp;
-  if (R->map) {
+  if (R->balloc && R->inflater && want >= R->inflater_min * 16384) {
+    // a window for the GPU inflater: read into the reader's page-locked buffer (its upload then goes
+    // by DMA; through the file mapping, every page faulted into this process and was copied again
+    // by the runtime's staging, and unmapping the touched pages was most of the readers' close)
+    if (want > R->ccap) {
+      void *p = nullptr;
+      const int64_t cap = std::max<int64_t>(want, 2 * R->ccap);
+      if (R->balloc(cap, &p) != 0 || !p) return set_err("page-locked window allocation failed");
+      if (R->cbuf) R->bfree(R->cbuf);
+      R->cbuf = static_cast<uint8_t *>(p);
+      R->ccap = cap;
+    }
+    const int fd = fileno(R->fh);
+    int64_t got = 0;
+    while (got < want) {
+      const ssize_t r = pread(fd, R->cbuf + got, (size_t)(want - got), (off_t)(coff + got));
+      if (r <= 0) return set_err("short read");
+      got += r;
+    }
+    comp = R->cbuf;
+  } else if (R->map) {
     comp = R->map + coff;
     const uintptr_t pg = 4096, a = (uintptr_t)comp & ~(pg - 1);
     madvise(reinterpret_cast<void *>(a), (size_t)((uintptr_t)comp + want - a), MADV_WILLNEED);
@@ -897,8 +920,9 @@ GANON_HOST_API int ganon_bam_reader_set_buffer_alloc(ganon_bam_reader *R, ganon_
                                                      ganon_buf_free_fn free_fn) {
   if (!R || (!alloc) != (!free_fn)) return set_err("ganon_bam_reader_set_buffer_alloc: bad arguments");
   if (R->pbuf) R->bfree(R->pbuf);
-  R->pbuf = nullptr;
-  R->pcap = 0;
+  if (R->cbuf) R->bfree(R->cbuf);
+  R->pbuf = R->cbuf = nullptr;
+  R->pcap = R->ccap = 0;
   R->balloc = alloc;
   R->bfree = free_fn;
   return 0;
@@ -1014,6 +1038,7 @@ GANON_HOST_API void ganon_bam_reader_close(ganon_bam_reader *R) {
   if (!R) return;
   if (R->map) munmap(const_cast<uint8_t *>(R->map), (size_t)R->fsize);
   if (R->pbuf) R->bfree(R->pbuf);
+  if (R->cbuf) R->bfree(R->cbuf);
   if (R->fh) std::fclose(R->fh);
   delete R;
 }

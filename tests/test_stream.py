@@ -509,3 +509,48 @@ def test_one_corrupt_sample_fails_cleanly_and_the_next_run_is_right(tmp_path):
     whole = _run(paths, str(tmp_path / "whole"), True)
     streamed = _run(paths, str(tmp_path / "stream"), False)
     assert whole == streamed
+
+
+def test_reader_with_inflater_and_buffer_alloc_reads_windows_into_its_buffer(tmp_path):
+    """The GPU-inflater configuration of the reader on the CPU: windows for the inflater are read by
+    pread into the reader's allocator-provided buffer (page-locked with the GPU inflater) and handed to
+    the inflater callback (here zlib in Python); region reads equal the whole-file table's fetch, and
+    the buffers go back through the allocator at close."""
+    import ctypes as C
+    import zlib
+    from genomeanonymizer_amd import native
+    from genomeanonymizer_amd.io.bam import BamReader, ReadTable
+    from genomeanonymizer_amd.synth.fastpair import make_pair
+    d = str(tmp_path / "in")
+    make_pair(d, n_contigs=2, contig_len=400_000, pairs_per_contig=20_000, window_every=20_000)
+    INF = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint8), C.c_int64, C.POINTER(C.c_int64),
+                      C.POINTER(C.c_int32), C.POINTER(C.c_int64), C.POINTER(C.c_int32), C.c_int64,
+                      C.POINTER(C.c_uint8), C.c_int64)
+    calls = [0]
+
+    def inflate(user, comp, comp_len, in_off, in_len, out_off, out_len, n, out, out_total):
+        calls[0] += 1
+        base_in, base_out = C.addressof(comp.contents), C.addressof(out.contents)
+        for i in range(n):
+            o = zlib.decompress(C.string_at(base_in + in_off[i], in_len[i]), -15)
+            if len(o) != out_len[i]:
+                return 1
+            C.memmove(base_out + out_off[i], o, len(o))
+        return 0
+    cb = INF(inflate)
+    path = os.path.join(d, "tumor.bam")
+    full = ReadTable(path)
+    rd = BamReader(path, 4)
+    af, ff, live, allocs = _python_buffer_alloc()
+    lib = native.host_lib()
+    lib.ganon_bam_reader_set_buffer_alloc(rd._h, C.cast(af, C.c_void_p), C.cast(ff, C.c_void_p))
+    lib.ganon_bam_reader_set_inflater(rd._h, C.cast(cb, C.c_void_p), None, 1)
+    for tid, (name, L) in enumerate(zip(full.ref_names, full.ref_lens)):
+        for a, b in ((0, int(L)), (1000, 200_000), (150_000, 390_000)):
+            exp = full.fetch(name, a, b)
+            got = rd.region(tid, a, b)
+            assert got.n == len(exp)
+            assert np.array_equal(np.asarray(got.pos), np.asarray(full.pos)[exp])
+    assert calls[0] > 0 and allocs[0] >= 2     # (the scan buffer and the compressed-window buffer)
+    rd.close()
+    assert not live

@@ -28,12 +28,14 @@
 // not aligned in the stream.
 #include <hip/hip_runtime.h>
 #include <rocprim/device/device_scan.hpp>
+#include <rocprim/device/device_select.hpp>
 
 #include <algorithm>
 #include <cstring>
 #include <vector>
 
 #include "../../include/ganon.h"
+#include "../../include/ganon_host.h"
 #include "ganon_ctx.h"
 
 using ganon_detail::check_launch;
@@ -108,22 +110,35 @@ struct Chunks {
   int64_t *entry, *exitp, *cnt;
   int32_t *bad;     // 1: truncated size field, 2: bad block_size (the walk stopped there)
   uint8_t *flag;    // the chunk's entry is not its predecessor's exit
-  unsigned long long *info;   // [failing chunks, first failing chunk, first bad chunk]
+  unsigned long long *info;   // [failing chunks, first failing chunk, first bad chunk, first cut record]
+  int64_t *tailp;   // (cut mode) the start of the record the stream's end cuts, -1 none
+  bool cut;         // cut mode: the stream may end inside a record (a window of a region read); that
+                    // record and the bytes after it are not records — the chain ends at its start
 };
 
 // Walk chunk c's chain from e (a record start, or < 0 for none): count and exit.
 __device__ __forceinline__ void walk(const uint8_t *__restrict__ d, int64_t p, int64_t n, int64_t c, int64_t e,
                                      const Chunks &K) {
   const int64_t ce = min(n, p + (c + 1) * kChunk);
-  int64_t s = e, k = 0;
+  int64_t s = e, k = 0, t = -1;
   int b = 0;
   if (s >= 0) {
     while (s < ce) {
       if (s + 4 > n) {
+        if (K.cut) {   // (the chain ends here: every later chunk holds no record, entry = exit = n)
+          t = s;
+          s = n;
+          break;
+        }
         b = 1;
         break;
       }
       const int32_t bs = (int32_t)ld32(d, s, n);
+      if (bs >= 32 && s + 4 + (int64_t)bs > n && K.cut) {
+        t = s;
+        s = n;
+        break;
+      }
       if (bs < 32 || s + 4 + (int64_t)bs > n) {
         b = 2;
         break;
@@ -132,6 +147,7 @@ __device__ __forceinline__ void walk(const uint8_t *__restrict__ d, int64_t p, i
       ++k;
     }
   }
+  if (K.cut) K.tailp[c] = t;
   K.entry[c] = e;
   K.exitp[c] = b ? -2 : (e >= 0 ? s : -1);
   K.cnt[c] = k;
@@ -186,6 +202,9 @@ __global__ void __launch_bounds__(kBamThreads) k_bam_check(int64_t n_chunks, Chu
     __hip_atomic_fetch_min(K.info + 1, (unsigned long long)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if (K.bad[c]) __hip_atomic_fetch_min(K.info + 2, (unsigned long long)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // (read once no chunk fails: then every chunk is exact and at most one ends the chain at a cut)
+  if (K.cut && K.tailp[c] >= 0)
+    __hip_atomic_fetch_min(K.info + 3, (unsigned long long)K.tailp[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // The record offsets: each chunk's chain again, from its proven entry, at its records' base index.
@@ -199,9 +218,53 @@ __global__ void __launch_bounds__(kBamThreads) k_bam_offsets(const uint8_t *__re
   int64_t s = entry[c], i = base[c];
   if (s < 0) return;
   while (s < ce) {
+    if (s + 4 > n) break;   // (cut mode: the record the stream's end cuts is not one)
+    const int64_t bs = (int64_t)(int32_t)ld32(d, s, n);
+    if (s + 4 + bs > n) break;
     rec[i++] = s;
-    s += 4 + (int64_t)(int32_t)ld32(d, s, n);
+    s += 4 + bs;
   }
+}
+
+inline __device__ int64_t tid_order_d(int32_t t) { return t < 0 ? (int64_t)INT32_MAX : (int64_t)t; }
+
+// A region read's records (ganon_bam_reader_region's scan_region, csrc/ganon_host.cpp): the window's
+// records run from the region's first candidate; the region ends at the first record of another
+// sequence or at pos >= end (info[0] = its index; info[1] = the same when that record's sequence
+// comes before the region's: the index pointed before its sequence); a record before it is kept when
+// bam_endpos > beg (htslib's overlap test). info[2] = 1: a record's CIGAR passes its block (the host
+// decoder reports it).
+__global__ void __launch_bounds__(kBamThreads) k_region_keep(const uint8_t *__restrict__ d, int64_t n,
+                                                             const int64_t *__restrict__ rec, int64_t nr, int32_t tid,
+                                                             int64_t beg, int64_t end, uint8_t *__restrict__ keep,
+                                                             unsigned long long *__restrict__ info) {
+  const int64_t i = (int64_t)blockIdx.x * kBamThreads + threadIdx.x;
+  if (i >= nr) return;
+  const int64_t o = rec[i];
+  const int32_t bs = (int32_t)rd32(d, o), rtid = (int32_t)rd32(d, o + 4), rpos = (int32_t)rd32(d, o + 8);
+  if (rtid != tid || (int64_t)rpos >= end) {
+    keep[i] = 0;
+    __hip_atomic_fetch_min(info, (unsigned long long)i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid_order_d(rtid) < tid_order_d(tid))
+      __hip_atomic_fetch_min(info + 1, (unsigned long long)i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  const int l_rn = d[o + 12];
+  const int nc = (int)(d[o + 16] | (d[o + 17] << 8));
+  const int flag = (int)(d[o + 18] | (d[o + 19] << 8));
+  if (36 + (int64_t)l_rn + 4LL * nc > 4 + (int64_t)bs) {
+    keep[i] = 1;
+    info[2] = 1;   // (plain store of a constant: any writer's value is the same)
+    return;
+  }
+  int64_t rl = 0;
+  if (!(flag & 4))
+    for (int k = 0; k < nc; ++k) {
+      const uint32_t w = rd32(d, o + 36 + l_rn + 4LL * k);
+      const int op = (int)(w & 0xF);
+      if (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) rl += w >> 4;
+    }
+  keep[i] = (int64_t)rpos + (rl > 0 ? rl : 1) > beg ? 1 : 0;
 }
 
 struct Sizes {
@@ -240,6 +303,7 @@ struct ganon_bam_dcols {
   void *blobs = nullptr;        // one block for the blobs
   uint8_t *stream = nullptr;    // the device copy of a host stream (on_host)
   size_t block_bytes = 0, blobs_bytes = 0, stream_bytes = 0;   // (context cache blocks)
+  int64_t blobs_used = 0;       // bytes of the blob block the carve uses
   int64_t fixes = 0;            // failing chunks met by the checks (summed over the rounds)
 };
 
@@ -371,7 +435,18 @@ T *carve(uint8_t *&at, int64_t count) {
   return p;
 }
 
-int columns(ganon_ctx *ctx, const uint8_t *d, int64_t p, int64_t n, ganon_bam_dcols *H) {
+// A region read's request (ganon_region_decode): the records of sequence tid overlapping [beg, end)
+// from the window's first record on. status out: 1 the region ends inside the window (the columns
+// are its records'), 0 it goes on past the window, 2 declined — the window holds a malformed record
+// or the index pointed before the sequence: the host's walk reports those.
+struct RegionReq {
+  int32_t tid;
+  int64_t beg, end;
+  bool at_eof;   // the window ends at the end of the file
+  int status;
+};
+
+int columns(ganon_ctx *ctx, const uint8_t *d, int64_t p, int64_t n, ganon_bam_dcols *H, RegionReq *rg = nullptr) {
   hipStream_t s = ctx->stream;
   const int64_t n_chunks = n > p ? (n - p + kChunk - 1) / kChunk : 0;
   int rc;
@@ -394,6 +469,7 @@ int columns(ganon_ctx *ctx, const uint8_t *d, int64_t p, int64_t n, ganon_bam_dc
   } free_tmp{ctx, tmp};
   Chunks K{};
   int64_t *base = nullptr;
+  unsigned long long tail = ~0ull;   // (cut mode) the record the window's end cuts
   if (n_chunks) {
     const int64_t nc = n_chunks;
     K.entry = static_cast<int64_t *>(dalloc(nc * 8));
@@ -402,8 +478,10 @@ int columns(ganon_ctx *ctx, const uint8_t *d, int64_t p, int64_t n, ganon_bam_dc
     base = static_cast<int64_t *>(dalloc((nc + 1) * 8));
     K.bad = static_cast<int32_t *>(dalloc(nc * 4));
     K.flag = static_cast<uint8_t *>(dalloc(nc));
-    K.info = static_cast<unsigned long long *>(dalloc(3 * 8));
-    if (!K.entry || !K.exitp || !K.cnt || !base || !K.bad || !K.flag || !K.info)
+    K.info = static_cast<unsigned long long *>(dalloc(4 * 8));
+    K.cut = rg != nullptr;
+    K.tailp = rg ? static_cast<int64_t *>(dalloc(nc * 8)) : nullptr;
+    if (!K.entry || !K.exitp || !K.cnt || !base || !K.bad || !K.flag || !K.info || (rg && !K.tailp))
       return fail(ctx, GANON_E_DEVICE, "ganon_bam_columns: device allocation failed");
     {
       ganon_detail::KernelScope ks(ctx, "k_bam_guess");
@@ -411,8 +489,8 @@ int columns(ganon_ctx *ctx, const uint8_t *d, int64_t p, int64_t n, ganon_bam_dc
     }
     if ((rc = check_launch(ctx, "k_bam_guess"))) return rc;
     for (int64_t round = 0;; ++round) {
-      const unsigned long long init[3] = {0ull, ~0ull, ~0ull};
-      unsigned long long info[3];
+      const unsigned long long init[4] = {0ull, ~0ull, ~0ull, ~0ull};
+      unsigned long long info[4];
       HIP_OR_FAIL(hipMemcpyAsync(K.info, init, sizeof init, hipMemcpyHostToDevice, s));
       {
         ganon_detail::KernelScope ks(ctx, "k_bam_check");
@@ -422,9 +500,17 @@ int columns(ganon_ctx *ctx, const uint8_t *d, int64_t p, int64_t n, ganon_bam_dc
       HIP_OR_FAIL(hipMemcpyAsync(info, K.info, sizeof info, hipMemcpyDeviceToHost, s));
       HIP_OR_FAIL(ganon_detail::sync_stream(s));
       // every chunk before the first failing one is exact: a bad walk there is the stream's error
-      if (info[2] != ~0ull && info[2] < info[1])
+      if (info[2] != ~0ull && info[2] < info[1]) {
+        if (rg) {
+          rg->status = 2;
+          return GANON_OK;
+        }
         return fail(ctx, GANON_E_ARG, "ganon_bam_columns: bad record size (chunk %lld)", (long long)info[2]);
-      if (info[0] == 0) break;
+      }
+      if (info[0] == 0) {
+        tail = info[3];
+        break;
+      }
       if (round > nc) return fail(ctx, GANON_E_DEVICE, "ganon_bam_columns: record chain did not settle");
       H->fixes += (int64_t)info[0];
       {
@@ -445,6 +531,61 @@ int columns(ganon_ctx *ctx, const uint8_t *d, int64_t p, int64_t n, ganon_bam_dc
     HIP_OR_FAIL(hipMemcpyAsync(&nr, base + n_chunks, 8, hipMemcpyDeviceToHost, s));
     HIP_OR_FAIL(ganon_detail::sync_stream(s));
   }
+  // A region read: the window's records up to the region's end, those overlapping [beg, end) kept
+  // (a stream compaction of their offsets); the columns below are built for those alone.
+  int64_t *sel = nullptr;
+  if (rg) {
+    if (rg->at_eof && tail != ~0ull) {   // the file ends inside a record: the host's error
+      rg->status = 2;
+      return GANON_OK;
+    }
+    int64_t *all = static_cast<int64_t *>(dalloc((size_t)(nr + 1) * 8));
+    uint8_t *keep = static_cast<uint8_t *>(dalloc((size_t)nr + 1));
+    unsigned long long *ri = static_cast<unsigned long long *>(dalloc(3 * 8));
+    sel = static_cast<int64_t *>(dalloc((size_t)(nr + 1) * 8));
+    int64_t *cnt = static_cast<int64_t *>(dalloc(8));
+    if (!all || !keep || !ri || !sel || !cnt) return fail(ctx, GANON_E_DEVICE, "ganon_region_decode: device allocation failed");
+    const unsigned long long init[3] = {~0ull, ~0ull, 0ull};
+    unsigned long long info[3] = {~0ull, ~0ull, 0ull};
+    HIP_OR_FAIL(hipMemcpyAsync(ri, init, sizeof init, hipMemcpyHostToDevice, s));
+    if (nr) {
+      {
+        ganon_detail::KernelScope ks(ctx, "k_bam_offsets");
+        hipLaunchKernelGGL(k_bam_offsets, dim3(grid_of(n_chunks)), dim3(kBamThreads), 0, s, d, p, n, n_chunks, K.entry,
+                           base, all);
+      }
+      if ((rc = check_launch(ctx, "k_bam_offsets"))) return rc;
+      {
+        ganon_detail::KernelScope ks(ctx, "k_region_keep");
+        hipLaunchKernelGGL(k_region_keep, dim3(grid_of(nr)), dim3(kBamThreads), 0, s, d, n, all, nr, rg->tid, rg->beg,
+                           rg->end, keep, ri);
+      }
+      if ((rc = check_launch(ctx, "k_region_keep"))) return rc;
+      HIP_OR_FAIL(hipMemcpyAsync(info, ri, sizeof info, hipMemcpyDeviceToHost, s));
+      HIP_OR_FAIL(ganon_detail::sync_stream(s));
+    }
+    if (info[2] || (info[1] != ~0ull && info[1] == info[0])) {
+      rg->status = 2;
+      return GANON_OK;
+    }
+    if (info[0] == ~0ull && (!rg->at_eof || tail != ~0ull)) {   // the region goes on past the window
+      rg->status = 0;
+      return GANON_OK;
+    }
+    const int64_t cut = info[0] == ~0ull ? nr : (int64_t)info[0];
+    int64_t nk = 0;
+    if (cut > 0) {
+      size_t tb = 0;
+      HIP_OR_FAIL(rocprim::select(nullptr, tb, all, keep, sel, cnt, (size_t)cut, s));
+      void *tsel = dalloc(tb);
+      if (!tsel) return fail(ctx, GANON_E_DEVICE, "ganon_region_decode: device allocation failed");
+      HIP_OR_FAIL(rocprim::select(tsel, tb, all, keep, sel, cnt, (size_t)cut, s));
+      HIP_OR_FAIL(hipMemcpyAsync(&nk, cnt, 8, hipMemcpyDeviceToHost, s));
+      HIP_OR_FAIL(ganon_detail::sync_stream(s));
+    }
+    nr = nk;
+    rg->status = 1;
+  }
   // per-record columns: 12 int32 + 6 int64 (5 offsets of nr + 1, the record offsets) + the sizes
   ganon_bam_cols &V = H->v;
   V.n_records = nr;
@@ -464,12 +605,16 @@ int columns(ganon_ctx *ctx, const uint8_t *d, int64_t p, int64_t n, ganon_bam_dc
     if (!first_bad) return fail(ctx, GANON_E_DEVICE, "ganon_bam_columns: device allocation failed");
     const unsigned long long none = ~0ull;
     HIP_OR_FAIL(hipMemcpyAsync(first_bad, &none, 8, hipMemcpyHostToDevice, s));
-    if (nr) {
-      ganon_detail::KernelScope ks(ctx, "k_bam_offsets");
-      hipLaunchKernelGGL(k_bam_offsets, dim3(grid_of(n_chunks)), dim3(kBamThreads), 0, s, d, p, n, n_chunks, K.entry, base,
-                         V.rec_off);
+    if (sel) {
+      if (nr) HIP_OR_FAIL(hipMemcpyAsync(V.rec_off, sel, (size_t)nr * 8, hipMemcpyDeviceToDevice, s));
+    } else {
+      if (nr) {
+        ganon_detail::KernelScope ks(ctx, "k_bam_offsets");
+        hipLaunchKernelGGL(k_bam_offsets, dim3(grid_of(n_chunks)), dim3(kBamThreads), 0, s, d, p, n, n_chunks, K.entry,
+                           base, V.rec_off);
+      }
+      if ((rc = check_launch(ctx, "k_bam_offsets"))) return rc;
     }
-    if ((rc = check_launch(ctx, "k_bam_offsets"))) return rc;
     for (int64_t *z : {S.name, S.cig, S.seq, S.qual, S.aux}) HIP_OR_FAIL(hipMemsetAsync(z + nr, 0, 8, s));
     if (nr) {
       ganon_detail::KernelScope ks(ctx, "k_bam_sizes");
@@ -493,8 +638,13 @@ int columns(ganon_ctx *ctx, const uint8_t *d, int64_t p, int64_t n, ganon_bam_dc
     int64_t *offs[5] = {V.name_off, V.cig_off, V.seq_off, V.qual_off, V.aux_off};
     for (int k = 0; k < 5; ++k) HIP_OR_FAIL(hipMemcpyAsync(&tot[k], offs[k] + nr, 8, hipMemcpyDeviceToHost, s));
     HIP_OR_FAIL(ganon_detail::sync_stream(s));
-    if (bad_rec != ~0ull)
+    if (bad_rec != ~0ull) {
+      if (rg) {
+        rg->status = 2;
+        return GANON_OK;
+      }
       return fail(ctx, GANON_E_ARG, "ganon_bam_columns: record %lld: fields exceed block size", (long long)bad_rec);
+    }
     V.names_bytes = tot[0];
     V.cigar_ops = tot[1];
     V.seq_bytes = tot[2];
@@ -512,6 +662,7 @@ int columns(ganon_ctx *ctx, const uint8_t *d, int64_t p, int64_t n, ganon_bam_dc
     V.seq = carve<uint8_t>(at, V.seq_bytes);
     V.qual = carve<uint8_t>(at, V.qual_bytes);
     V.aux = carve<uint8_t>(at, V.aux_bytes);
+    H->blobs_used = rb;
   }
   if (nr) {
     ganon_detail::KernelScope ks(ctx, "k_bam_scatter");
@@ -612,4 +763,85 @@ GANON_API int ganon_bam_dcols_free(ganon_ctx *ctx, ganon_bam_dcols *c) {
   if (ctx) ganon_detail::sync_stream(ctx->stream);
   release(ctx, c);
   return GANON_OK;
+}
+
+// ---- a region read decoded on the device (the reader's region decoder, ganon_bam_reader_region) ----
+GANON_API int ganon_region_decode(void *user, const uint8_t *comp, int64_t comp_len, const int64_t *in_off,
+                                  const int32_t *in_len, const int64_t *out_off, const int32_t *out_len,
+                                  int64_t n_blocks, uint8_t *out, int64_t out_total, int64_t p0, int32_t tid,
+                                  int64_t beg, int64_t end, int at_eof, ganon_bam_view *cols, void **block) {
+  ganon_ctx *ctx = static_cast<ganon_ctx *>(user);
+  if (!ctx || !cols || !block || (out_total > 0 && !out) || p0 < 0) return -1;
+  *block = nullptr;
+  if (ganon_inflate_impl(ctx, comp, comp_len, in_off, in_len, out_off, out_len, n_blocks, nullptr, out_total, nullptr))
+    return -1;   // (the inflate failed: ctx->err)
+  const uint8_t *dout = nullptr;
+  int64_t bytes = 0;
+  if (ganon_inflate_device_output(ctx, &dout, &bytes) || bytes != out_total) return -1;
+  hipStream_t s = ctx->stream;
+  // the host's walk goes on from the inflated window: its bytes to `out`
+  auto raw = [&]() -> int {
+    if (out_total > 0 && (hipMemcpyAsync(out, dout, (size_t)out_total, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                          ganon_detail::sync_stream(s) != hipSuccess)) {
+      ganon_detail::sync_stream(s);
+      return fail(ctx, -1, "ganon_region_decode: copy failed");
+    }
+    return 0;
+  };
+  if (p0 > out_total) return raw();
+  auto *H = new ganon_bam_dcols();
+  RegionReq rq{tid, beg, end, at_eof != 0, 0};
+  const int rc = columns(ctx, dout, p0, out_total, H, &rq);
+  if (rc || rq.status != 1) {   // (a device failure, too, leaves the window to the host)
+    ganon_detail::sync_stream(s);
+    release(ctx, H);
+    return raw();
+  }
+  // the columns to one page-locked block, laid out as the device block's first 17 columns and the
+  // blob block: two copies by DMA
+  const ganon_bam_cols &V = H->v;
+  const int64_t m = V.n_records + 1;
+  const int64_t prefix = 12 * (((m * 4) + 255) / 256 * 256) + 5 * (((m * 8) + 255) / 256 * 256);
+  void *hb = nullptr;
+  if (ganon_pinned_alloc(prefix + H->blobs_used + 256, &hb) != 0 || !hb) {
+    release(ctx, H);
+    return raw();
+  }
+  uint8_t *h8 = static_cast<uint8_t *>(hb);
+  if (hipMemcpyAsync(h8, H->block, (size_t)prefix, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      (H->blobs_used > 0 &&
+       hipMemcpyAsync(h8 + prefix, H->blobs, (size_t)H->blobs_used, hipMemcpyDeviceToHost, s) != hipSuccess) ||
+      ganon_detail::sync_stream(s) != hipSuccess) {
+    ganon_detail::sync_stream(s);
+    release(ctx, H);
+    ganon_pinned_free(hb);
+    return raw();
+  }
+  ganon_bam_cols hv{};
+  uint8_t *at = h8;
+  for (int32_t **f : {&hv.tid, &hv.pos, &hv.end, &hv.flag, &hv.mapq, &hv.l_seq, &hv.n_cigar, &hv.mate_tid, &hv.mate_pos,
+                      &hv.tlen, &hv.name_len, &hv.aux_len})
+    *f = carve<int32_t>(at, m);
+  for (int64_t **f : {&hv.name_off, &hv.cig_off, &hv.seq_off, &hv.qual_off, &hv.aux_off}) *f = carve<int64_t>(at, m);
+  at = h8 + prefix;
+  hv.names = carve<char>(at, V.names_bytes);
+  hv.cigar = carve<uint32_t>(at, V.cigar_ops);
+  hv.seq = carve<uint8_t>(at, V.seq_bytes);
+  hv.qual = carve<uint8_t>(at, V.qual_bytes);
+  hv.aux = carve<uint8_t>(at, V.aux_bytes);
+  *cols = ganon_bam_view{};
+  cols->n_records = V.n_records;
+  cols->tid = hv.tid, cols->pos = hv.pos, cols->end = hv.end, cols->flag = hv.flag, cols->mapq = hv.mapq;
+  cols->l_seq = hv.l_seq, cols->n_cigar = hv.n_cigar, cols->mate_tid = hv.mate_tid, cols->mate_pos = hv.mate_pos;
+  cols->tlen = hv.tlen, cols->name_len = hv.name_len, cols->aux_len = hv.aux_len;
+  cols->name_off = hv.name_off, cols->cig_off = hv.cig_off, cols->seq_off = hv.seq_off, cols->qual_off = hv.qual_off;
+  cols->aux_off = hv.aux_off;
+  cols->names = hv.names, cols->names_bytes = V.names_bytes;
+  cols->cigar = hv.cigar, cols->cigar_ops = V.cigar_ops;
+  cols->seq = hv.seq, cols->seq_bytes = V.seq_bytes;
+  cols->qual = hv.qual, cols->qual_bytes = V.qual_bytes;
+  cols->aux = hv.aux, cols->aux_bytes = V.aux_bytes;
+  release(ctx, H);
+  *block = hb;
+  return 1;
 }

@@ -20,6 +20,10 @@
 
 struct ganon_inflate_state;                       // ganon_inflate.hip: grow-only device buffers
 void ganon_inflate_free(ganon_inflate_state *st);
+// ganon_inflate; out == nullptr: the output stays in device memory (ganon_inflate_device_output)
+int ganon_inflate_impl(ganon_ctx *ctx, const uint8_t *comp, int64_t comp_len, const int64_t *in_off,
+                       const int32_t *in_len, const int64_t *out_off, const int32_t *out_len, int64_t n_blocks,
+                       uint8_t *out, int64_t out_total, int64_t *first_bad);
 
 struct ganon_ctx {
   int device = 0;

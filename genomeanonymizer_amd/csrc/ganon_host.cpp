@@ -80,8 +80,10 @@ void huge_reserve(RawVec<T> &v, size_t n) {
 
 // Decoder phase clocks (ganon_host_phase_times): wall nanoseconds of the calling threads, summed over
 // calls and threads — where a reader's decode time goes (tools/e2e_bench.py reports them per rank).
-enum { kPhParse, kPhInflate, kPhWalk, kPhCopy, kPhRecWalk, kPhSizes, kPhColumns, kPhN };
+enum { kPhParse, kPhInflate, kPhWalk, kPhCopy, kPhRecWalk, kPhSizes, kPhColumns, kPhDevice, kPhN };
 std::atomic<long long> g_phase_ns[kPhN];
+// region reads the device decoder finished, and those it handed back to the host's walk
+std::atomic<long long> g_dev_regions{0}, g_dev_fallbacks{0};
 using PhClock = std::chrono::steady_clock;
 // charge the time since t to phase ph and restart t
 inline void lap(int ph, PhClock::time_point &t) {
@@ -168,6 +170,17 @@ struct ganon_bam {
   RawVec<char> names;
   RawVec<uint32_t> cigar;
   RawVec<uint8_t> seq, qual, aux;
+  // (a region decoded on the device, ganon_bam_reader_set_region_decoder) the record columns lie in
+  // one block from the decoder, freed with ext_free; the vectors above stay empty
+  void *ext_block = nullptr;
+  ganon_buf_free_fn ext_free = nullptr;
+  ganon_bam_view ext{};
+  ganon_bam() = default;
+  ganon_bam(const ganon_bam &) = delete;
+  ganon_bam &operator=(const ganon_bam &) = delete;
+  ~ganon_bam() {
+    if (ext_block && ext_free) ext_free(ext_block);
+  }
 };
 
 static int set_err(const std::string &m) {
@@ -461,6 +474,14 @@ GANON_HOST_API int ganon_bam_open(const char *path, int threads, ganon_bam **out
 
 GANON_HOST_API int ganon_bam_view_get(ganon_bam *b, ganon_bam_view *v) {
   if (!b || !v) return set_err("null argument");
+  if (b->ext_block) {
+    *v = b->ext;
+    v->n_ref = (int32_t)b->ref_len.size();
+    v->ref_names = b->ref_names.data();
+    v->ref_name_off = b->ref_name_off.data();
+    v->ref_len = b->ref_len.data();
+    return 0;
+  }
   v->n_records = (int64_t)b->tid.size();
   v->n_ref = (int32_t)b->ref_len.size();
   v->ref_names = b->ref_names.data();
@@ -530,6 +551,10 @@ struct ganon_bam_reader {
   ganon_inflate_fn inflater = nullptr;   // ganon_bam_reader_set_inflater: block windows inflated by it
   void *inflater_user = nullptr;
   int64_t inflater_min = 64;             // ... when they hold at least this many blocks
+  ganon_region_fn rdec = nullptr;        // ganon_bam_reader_set_region_decoder: a region read's first
+  void *rdec_user = nullptr;             // window decoded whole by it (at least rdec_min blocks)
+  int64_t rdec_min = 64;
+  ganon_buf_free_fn rdec_release = nullptr;
 };
 
 namespace {
@@ -585,19 +610,32 @@ inline void buf_resize(ScanBuf &v, size_t m) { v.resize(m); }
 constexpr int32_t kTidEnd = INT32_MAX;
 inline int64_t tid_order(int32_t t) { return t < 0 ? (int64_t)INT32_MAX : (int64_t)t; }   // unplaced last
 
+// A region read's first window offered to the reader's region decoder: the records from byte p0 of
+// the window's inflated bytes; done = the decoder returned the region's columns (cols, block).
+struct RegionCall {
+  int32_t tid;
+  int64_t beg, end, p0;
+  bool done = false;
+  ganon_bam_view cols{};
+  void *block = nullptr;
+};
+
 // Reads and inflates complete BGZF blocks starting at file offset coff (at most R->chunk compressed
 // bytes). Appends the inflated bytes to data and one (data offset, file offset) pair per non-empty
-// block to bmap. Returns the file offset after the last complete block, or -1 on error.
+// block to bmap. Returns the file offset after the last complete block, or -1 on error. With rq and
+// a region decoder, a window of enough blocks goes to the decoder (rq->done: the region is decoded,
+// data holds nothing of it).
 template <class Buf>
 int64_t read_blocks(ganon_bam_reader *R, int64_t coff, int64_t step, Buf &data,
-                    std::vector<std::pair<int64_t, int64_t>> &bmap) {
+                    std::vector<std::pair<int64_t, int64_t>> &bmap, RegionCall *rq = nullptr) {
   auto tph = PhClock::now();
   const int64_t want = std::min<int64_t>(std::max<int64_t>(step, 1 << 17), R->fsize - coff);
+  const bool dev = rq && R->rdec;   // (then the decoder inflates the window if it holds enough blocks)
   // the window's compressed bytes: in place in the file mapping (the inflate threads read the page
   // cache directly; no serial copy, no fresh buffer to fault in per window), else read into a buffer
   RawVec<uint8_t> buf;
   const uint8_t *comp;
-  if (R->balloc && R->inflater && want >= R->inflater_min * 16384) {
+  if (R->balloc && ((R->inflater && want >= R->inflater_min * 16384) || (dev && want >= R->rdec_min * 16384))) {
     // a window for the GPU inflater: read into the reader's page-locked buffer (its upload then goes
     // by DMA; through the file mapping, every page faulted into this process and was copied again
     // by the runtime's staging, and unmapping the touched pages was most of the readers' close)
@@ -647,7 +685,29 @@ int64_t read_blocks(ganon_bam_reader *R, int64_t coff, int64_t step, Buf &data,
   const size_t base = data.size();
   buf_resize(data, base + (size_t)total);
   lap(kPhParse, tph);
-  if (R->inflater && (int64_t)blocks.size() >= R->inflater_min) {
+  if (dev && (int64_t)blocks.size() >= R->rdec_min) {
+    const size_t nb = blocks.size();
+    std::vector<int64_t> in_off(nb), out_off(nb);
+    std::vector<int32_t> in_len(nb), out_len(nb);
+    for (size_t i = 0; i < nb; ++i) {
+      in_off[i] = blocks[i].in_off;
+      in_len[i] = blocks[i].in_len;
+      out_off[i] = blocks[i].out_off;
+      out_len[i] = blocks[i].out_len;
+    }
+    const int at_eof = coff + off >= R->fsize ? 1 : 0;
+    const int r = R->rdec(R->rdec_user, comp, off, in_off.data(), in_len.data(), out_off.data(), out_len.data(),
+                          (int64_t)nb, data.data() + base, total, rq->p0 + (int64_t)base, rq->tid, rq->beg, rq->end,
+                          at_eof, &rq->cols, &rq->block);
+    lap(kPhDevice, tph);
+    if (r < 0) return set_err("BGZF inflate failed (region decoder)");
+    if (r == 1) {
+      rq->done = true;
+      g_dev_regions.fetch_add(1, std::memory_order_relaxed);
+      return coff + off;
+    }
+    g_dev_fallbacks.fetch_add(1, std::memory_order_relaxed);
+  } else if (R->inflater && (int64_t)blocks.size() >= R->inflater_min) {
     const size_t nb = blocks.size();
     std::vector<int64_t> in_off(nb), out_off(nb);
     std::vector<int32_t> in_len(nb), out_len(nb);
@@ -752,7 +812,7 @@ int64_t record_end(const uint8_t *d) {
 // region semantics: pos < end and bam_endpos > beg), in file order; stops at the first record of
 // another sequence or at pos >= end. Runs of kept records are copied to kept at once.
 int scan_region(ganon_bam_reader *R, int64_t voff, int32_t tid, int64_t beg, int64_t end, int64_t hint,
-                ScanBuf &data, std::vector<int64_t> &recs) {
+                ScanBuf &data, std::vector<int64_t> &recs, RegionCall *rq = nullptr, int64_t dev_step = 0) {
   // (records stay in place in `data`, their offsets in recs: as scan_tid)
   int64_t step = std::min<int64_t>(hint > 0 ? hint + (1 << 16) : (1 << 20), R->chunk);
   int64_t coff = voff >> 16;
@@ -760,13 +820,19 @@ int scan_region(ganon_bam_reader *R, int64_t voff, int32_t tid, int64_t beg, int
   data.clear();
   recs.clear();
   int64_t dpos = (int64_t)(voff & 0xFFFF);
+  if (rq) {
+    rq->p0 = dpos;
+    if (dev_step > 0) step = dev_step;
+  }
   for (;;) {
     if (coff >= R->fsize) {
       if (dpos < (int64_t)data.size()) return set_err("truncated BAM record");
       return 0;
     }
-    coff = read_blocks(R, coff, step, data, bmap);
+    coff = read_blocks(R, coff, step, data, bmap, rq);
     if (coff < 0) return -1;
+    if (rq && rq->done) return 0;
+    rq = nullptr;   // (the first window only)
     step = std::min<int64_t>(2 * step, R->chunk);
     auto tw = PhClock::now();
     for (;;) {
@@ -937,6 +1003,16 @@ GANON_HOST_API int ganon_bam_reader_set_inflater(ganon_bam_reader *R, ganon_infl
   return 0;
 }
 
+GANON_HOST_API int ganon_bam_reader_set_region_decoder(ganon_bam_reader *R, ganon_region_fn fn, void *user,
+                                                       int64_t min_blocks, ganon_buf_free_fn release) {
+  if (!R || min_blocks < 1 || (fn && !release)) return set_err("ganon_bam_reader_set_region_decoder: bad arguments");
+  R->rdec = fn;
+  R->rdec_user = fn ? user : nullptr;
+  R->rdec_min = min_blocks;
+  R->rdec_release = fn ? release : nullptr;
+  return 0;
+}
+
 GANON_HOST_API int ganon_bam_reader_has_index(const ganon_bam_reader *R) { return R && R->has_index ? 1 : 0; }
 
 GANON_HOST_API int ganon_bam_reader_header(ganon_bam_reader *R, ganon_bam_view *v) {
@@ -1001,6 +1077,7 @@ GANON_HOST_API int ganon_bam_reader_region(ganon_bam_reader *R, int32_t tid, int
   try {
     ScanBuf data(R);
     std::vector<int64_t> recs;
+    RegionCall rq{tid, beg, end, 0};
     const int64_t first = R->index_beg[(size_t)tid];
     if (first >= 0 && end > beg) {
       // the first record that can overlap beg: the linear index entry of its 16 kb window (the
@@ -1016,13 +1093,29 @@ GANON_HOST_API int ganon_bam_reader_region(ganon_bam_reader *R, int32_t tid, int
       const int64_t span = e > voff ? (e >> 16) - (voff >> 16) : 0;
       const int64_t len = R->header.ref_len[(size_t)tid];
       const int64_t hint = len > 0 ? std::min<int64_t>(span, span * (end - beg) / len + (1 << 20)) : 0;
-      data.reserve((size_t)hint * 7 / 2 + (4 << 20));
-      if (scan_region(R, voff, tid, beg, end, hint, data, recs) != 0) return -1;
+      // (with a region decoder the first window is the whole region's estimated span: the span from
+      // voff covers [beg, len) — plus 1/32 and 1 MiB of margin, and two blocks past a sequence's end
+      // for the next record that ends the region)
+      int64_t dev_step = 0;
+      if (R->rdec) {
+        const int64_t rest = std::max<int64_t>(1, len - beg);
+        dev_step = std::min<int64_t>({span + (1 << 17), span * std::min<int64_t>(end - beg, rest) / rest * 33 / 32 + (1 << 20),
+                                      16 * R->chunk});
+      }
+      if (!R->rdec) data.reserve((size_t)hint * 7 / 2 + (4 << 20));
+      if (scan_region(R, voff, tid, beg, end, hint, data, recs, R->rdec ? &rq : nullptr, dev_step) != 0) return -1;
     }
     auto *bam = new ganon_bam();
     bam->ref_names = R->header.ref_names;
     bam->ref_name_off = R->header.ref_name_off;
     bam->ref_len = R->header.ref_len;
+    if (rq.done) {
+      bam->ext = rq.cols;
+      bam->ext_block = rq.block;
+      bam->ext_free = R->rdec_release;
+      *out = bam;
+      return 0;
+    }
     if (records_to_columns(data.data(), 0, (int64_t)data.size(), bam, R->threads, &recs) != 0) {
       delete bam;
       return -1;
@@ -1314,7 +1407,10 @@ GANON_HOST_API int ganon_host_phase_times(double *out, int n, int reset) {
   const int k = std::min(n, (int)kPhN);
   for (int i = 0; i < k; ++i)
     out[i] = (reset ? g_phase_ns[i].exchange(0) : g_phase_ns[i].load()) * 1e-9;
-  return (int)kPhN;
+  // then two counts: region reads the device decoder finished / handed back to the host's walk
+  if (n > kPhN) out[kPhN] = (double)(reset ? g_dev_regions.exchange(0) : g_dev_regions.load());
+  if (n > kPhN + 1) out[kPhN + 1] = (double)(reset ? g_dev_fallbacks.exchange(0) : g_dev_fallbacks.load());
+  return (int)kPhN + 2;
 }
 
 GANON_HOST_API const char *ganon_host_inflate_backend(void) { return libdeflate() ? "libdeflate" : "zlib"; }

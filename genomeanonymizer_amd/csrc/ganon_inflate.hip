@@ -883,13 +883,15 @@ int grow_dev(ganon_ctx *ctx, T **p, size_t &cap, size_t need) {
 
 }  // namespace
 
-GANON_API int ganon_inflate(ganon_ctx *ctx, const uint8_t *comp, int64_t comp_len, const int64_t *in_off,
-                            const int32_t *in_len, const int64_t *out_off, const int32_t *out_len, int64_t n_blocks,
-                            uint8_t *out, int64_t out_total, int64_t *first_bad) {
+// ganon_inflate; out == nullptr keeps the output in device memory only (ganon_inflate_device_output:
+// the device region decode of ganon_bam.hip walks it there)
+int ganon_inflate_impl(ganon_ctx *ctx, const uint8_t *comp, int64_t comp_len, const int64_t *in_off,
+                       const int32_t *in_len, const int64_t *out_off, const int32_t *out_len, int64_t n_blocks,
+                       uint8_t *out, int64_t out_total, int64_t *first_bad) {
   if (!ctx) return GANON_E_ARG;
   if (first_bad) *first_bad = -1;
   if (n_blocks < 0 || comp_len < 0 || out_total < 0 || (n_blocks && (!comp || !in_off || !in_len || !out_off ||
-                                                                      !out_len || !out)))
+                                                                      !out_len)))
     return fail(ctx, GANON_E_ARG, "ganon_inflate: bad arguments");
   if (!n_blocks) return GANON_OK;
   // every block inside both buffers before any span is computed from them: the host copies of a
@@ -963,7 +965,8 @@ GANON_API int ganon_inflate(ganon_ctx *ctx, const uint8_t *comp, int64_t comp_le
     int64_t lo, hi;
     span_out(b0, b1, lo, hi);
     return hipStreamWaitEvent(cs, st->ev[2 * c + 1], 0) == hipSuccess &&
-           (hi <= lo || hipMemcpyAsync(out + lo, st->out + lo, (size_t)(hi - lo), hipMemcpyDeviceToHost, cs) == hipSuccess);
+           (!out || hi <= lo ||
+            hipMemcpyAsync(out + lo, st->out + lo, (size_t)(hi - lo), hipMemcpyDeviceToHost, cs) == hipSuccess);
   };
   for (int64_t c = 0; c < n_chunks && okc; ++c) {
     const int64_t b0 = c * kChunk, b1 = std::min(n_blocks, b0 + kChunk);
@@ -1006,6 +1009,13 @@ GANON_API int ganon_inflate(ganon_ctx *ctx, const uint8_t *comp, int64_t comp_le
     }
   st->last_out = out_total;
   return GANON_OK;
+}
+
+GANON_API int ganon_inflate(ganon_ctx *ctx, const uint8_t *comp, int64_t comp_len, const int64_t *in_off,
+                            const int32_t *in_len, const int64_t *out_off, const int32_t *out_len, int64_t n_blocks,
+                            uint8_t *out, int64_t out_total, int64_t *first_bad) {
+  if (ctx && n_blocks > 0 && !out) return fail(ctx, GANON_E_ARG, "ganon_inflate: bad arguments");
+  return ganon_inflate_impl(ctx, comp, comp_len, in_off, in_len, out_off, out_len, n_blocks, out, out_total, first_bad);
 }
 
 GANON_API int ganon_inflate_device_output(ganon_ctx *ctx, const uint8_t **out, int64_t *bytes) {

@@ -276,12 +276,18 @@ class BamReader:
         reader calls into its context)."""
         native.host_lib().ganon_bam_reader_set_inflater(self._h, inflater.fn, inflater.handle, inflater.min_blocks)
         self.inflater = inflater
-        if os.environ.get("GANON_PINNED_SCAN", "1") != "0":
+        if isinstance(inflater, native.GpuInflater) and os.environ.get("GANON_PINNED_SCAN", "1") != "0":
             # the scans' inflated bytes in one page-locked buffer kept by the reader: the inflater's
             # device-to-host copies go by DMA instead of through the runtime's staging copies
             hl = native.hip_lib()
             native.host_lib().ganon_bam_reader_set_buffer_alloc(
                 self._h, C.cast(hl.ganon_pinned_alloc, C.c_void_p), C.cast(hl.ganon_pinned_free, C.c_void_p))
+            if os.environ.get("GANON_DEVICE_REGION", "1") != "0":
+                # region reads: the first window inflated, walked and filtered on the device, the
+                # kept records' columns back by DMA (no host record walk or column copies; DESIGN §4f)
+                native.host_lib().ganon_bam_reader_set_region_decoder(
+                    self._h, inflater.region_fn, inflater.handle, inflater.min_blocks,
+                    C.cast(hl.ganon_pinned_free, C.c_void_p))
 
     def tid_of(self, contig: str) -> int:
         try:

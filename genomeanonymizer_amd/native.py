@@ -212,7 +212,7 @@ def hip_lib():
     lib.ganon_bam_dcols_get.argtypes = [_p, C.POINTER(BamCols), _i64p]
     lib.ganon_bam_dcols_download.argtypes = [_p, _p, C.POINTER(BamCols)]
     lib.ganon_bam_dcols_free.argtypes = [_p, _p]
-    if lib.ganon_abi_version() != 4:
+    if lib.ganon_abi_version() != 5:
         raise GanonError("libganon_hip.so ABI version mismatch")
     _hip = lib
     return lib
@@ -247,7 +247,7 @@ EXPORTED_HIP_SYMBOLS = (
     "ganon_indel_upload", "ganon_indel_run", "ganon_indel_download", "ganon_indel_info", "ganon_indel_free",
     "ganon_inflate", "ganon_inflate_hostcb", "ganon_inflate_device_output",
     "ganon_bam_columns", "ganon_bam_dcols_get", "ganon_bam_dcols_download", "ganon_bam_dcols_free",
-    "ganon_pinned_alloc", "ganon_pinned_free",
+    "ganon_pinned_alloc", "ganon_pinned_free", "ganon_region_decode",
 )
 EXPORTED_HOST_SYMBOLS = (
     "ganon_bam_open", "ganon_bam_view_get", "ganon_bam_error", "ganon_bam_close",
@@ -260,7 +260,7 @@ EXPORTED_HOST_SYMBOLS = (
     "ganon_blob_free", "ganon_objects_create", "ganon_objects_free", "ganon_objects_add_job", "ganon_objects_add_plain",
     "ganon_objects_run", "ganon_objects_take", "ganon_objects_settle", "ganon_objects_last_error",
     "ganon_objects_take_all", "ganon_aux_sa_count", "ganon_fastq_edit", "ganon_gather_ranges", "ganon_gather_ranges2", "ganon_host_phase_times",
-    "ganon_bam_reader_set_inflater", "ganon_bam_reader_set_buffer_alloc",
+    "ganon_bam_reader_set_inflater", "ganon_bam_reader_set_buffer_alloc", "ganon_bam_reader_set_region_decoder",
 )
 
 
@@ -336,6 +336,7 @@ class GpuInflater:
         self.device = device
         self.min_blocks = int(min_blocks)
         self.fn = C.cast(lib.ganon_inflate_hostcb, _p)   # the reader's callback, user = the context
+        self.region_fn = C.cast(lib.ganon_region_decode, _p)   # the reader's region decoder, same user
 
     @property
     def handle(self):
@@ -746,7 +747,9 @@ def gather_ranges2(src0, src1, sel: np.ndarray, off: np.ndarray, length: np.ndar
     return out
 
 
-DECODE_PHASES = ("parse", "inflate", "region_walk", "kept_copy", "record_walk", "sizes", "columns")
+# (then two counts: region reads the device decoder finished, and those it handed back to the host)
+DECODE_PHASES = ("parse", "inflate", "region_walk", "kept_copy", "record_walk", "sizes", "columns", "device_region",
+                 "device_regions", "device_fallbacks")
 
 
 def decode_phase_times(reset: bool = False) -> dict:
@@ -1480,6 +1483,7 @@ def host_lib():
                                          C.c_char_p, C.c_int64]
     lib.ganon_gather_ranges2.restype = C.c_int64
     lib.ganon_bam_reader_set_buffer_alloc.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.ganon_bam_reader_set_region_decoder.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p]
     lib.ganon_host_phase_times.argtypes = [C.POINTER(C.c_double), C.c_int, C.c_int]
     lib.ganon_host_phase_times.restype = C.c_int
     lib.ganon_fastq_edit.argtypes = [C.c_int64, C.c_char_p, _i64p, _u8p, _i32p, _i64p, _i64p, C.c_char_p, _i64p,

@@ -35,7 +35,7 @@
 #define GANON_API __attribute__((visibility("default")))
 #endif
 
-#define GANON_ABI_VERSION 4
+#define GANON_ABI_VERSION 5
 
 enum {
   GANON_OK = 0,
@@ -412,5 +412,23 @@ GANON_API int ganon_bam_dcols_get(const ganon_bam_dcols *c, ganon_bam_cols *devi
 GANON_API int ganon_bam_dcols_download(ganon_ctx *ctx, const ganon_bam_dcols *c, const ganon_bam_cols *host);
 /* (with the context that made it: its device blocks return to that context's cache) */
 GANON_API int ganon_bam_dcols_free(ganon_ctx *ctx, ganon_bam_dcols *c);
+
+/* A region read's window decoded on the device: the reader's region decoder (ganon_region_fn of
+ * include/ganon_host.h, user = a ganon_ctx; libganon_host.so's ganon_bam_reader_region, the
+ * reference's AlignmentFile.fetch(contig, beg, end), short_read_tumor_normal_anonymizer.py:570-573).
+ * Inflates the window's BGZF blocks (as ganon_inflate) and keeps them in device memory; walks the
+ * records from byte p0 (the window may end inside a record); the region ends at the first record of
+ * another sequence or with pos >= end; records with bam_endpos > beg are kept. Returns 1 when the
+ * region ends inside the window: *cols = the kept records' columns (ganon_bam_view's record fields
+ * and blobs, same values and layout as the host decoder's) in one page-locked block *block, freed
+ * with ganon_pinned_free. Returns 0 when the region goes on past the window, or the window holds
+ * what the host decoder must report (a malformed record, an index that points before the
+ * sequence): out[0, out_total) then holds the inflated window for the host's walk. -1: the inflate
+ * failed. Since ABI 5 (round 6). */
+struct ganon_bam_view;
+GANON_API int ganon_region_decode(void *user, const uint8_t *comp, int64_t comp_len, const int64_t *in_off,
+                                  const int32_t *in_len, const int64_t *out_off, const int32_t *out_len,
+                                  int64_t n_blocks, uint8_t *out, int64_t out_total, int64_t p0, int32_t tid,
+                                  int64_t beg, int64_t end, int at_eof, struct ganon_bam_view *cols, void **block);
 
 #endif /* GANON_H */

@@ -95,6 +95,19 @@ typedef int (*ganon_buf_alloc_fn)(int64_t bytes, void **out);
 typedef int (*ganon_buf_free_fn)(void *p);
 GANON_HOST_API int ganon_bam_reader_set_buffer_alloc(ganon_bam_reader *reader, ganon_buf_alloc_fn alloc,
                                                      ganon_buf_free_fn free_fn);
+/* Region decoder (ganon_region_decode of include/ganon.h, user = a ganon_ctx): a region read's
+ * first window of at least min_blocks blocks goes to it whole — inflated, walked and filtered on the
+ * device, the kept records' columns back in one block the returned table owns (release(block) at
+ * ganon_bam_close). It returns 1 with *cols / *block when the region ends inside the window, 0 after
+ * writing the inflated window to out (the reader's walk goes on from there), -1 on an inflate error.
+ * The window is then sized to the region's index span (up to 16x the reader's window). fn NULL
+ * turns it off. */
+typedef int (*ganon_region_fn)(void *user, const uint8_t *comp, int64_t comp_len, const int64_t *in_off,
+                               const int32_t *in_len, const int64_t *out_off, const int32_t *out_len,
+                               int64_t n_blocks, uint8_t *out, int64_t out_total, int64_t p0, int32_t tid,
+                               int64_t beg, int64_t end, int at_eof, ganon_bam_view *cols, void **block);
+GANON_HOST_API int ganon_bam_reader_set_region_decoder(ganon_bam_reader *reader, ganon_region_fn fn, void *user,
+                                                       int64_t min_blocks, ganon_buf_free_fn release);
 GANON_HOST_API int ganon_bam_reader_header(ganon_bam_reader *reader, ganon_bam_view *view);
 GANON_HOST_API int ganon_bam_reader_contig(ganon_bam_reader *reader, int32_t tid, ganon_bam **out);
 /* The records of tid overlapping [beg, end) (0-based; htslib's region semantics: pos < end and

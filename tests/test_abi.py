@@ -37,7 +37,7 @@ def test_host_library_exports_header():
 def test_abi_version_and_struct_layout(hip_built):
     from genomeanonymizer_amd import native
     lib = native.hip_lib()
-    assert lib.ganon_abi_version() == 4
+    assert lib.ganon_abi_version() == 5
     # ganon_batch: 2 int32 + 4 int64 + 17 pointers, naturally aligned
     assert ctypes.sizeof(native.GanonBatch) == 8 + 32 + 17 * 8
     # ganon_fastq_records: int64 + 2 int32 + 15 pointers

@@ -554,3 +554,92 @@ def test_reader_with_inflater_and_buffer_alloc_reads_windows_into_its_buffer(tmp
     assert calls[0] > 0 and allocs[0] >= 2     # (the scan buffer and the compressed-window buffer)
     rd.close()
     assert not live
+
+
+def test_reader_region_decoder_protocol(tmp_path):
+    """The device region decoder's protocol on the CPU (ganon_bam_reader_set_region_decoder, include/
+    ganon_host.h; the GPU's ganon_region_decode is checked in tests/test_region_device.py): a Python
+    decoder that either returns a region's columns in a block of its own (here: another reader's
+    decode, laid out in one buffer) or declines after inflating the window into `out` (the reader's
+    walk then goes on from there). Both ways the tables equal the plain reader's, the decoder sees the
+    region and the window's first record offset, and every block goes back through release when its
+    table closes."""
+    import ctypes as C
+    import gc
+    import zlib
+    from genomeanonymizer_amd import native
+    from genomeanonymizer_amd.io.bam import BamReader
+    from genomeanonymizer_amd.synth.fastpair import make_pair
+    d = str(tmp_path / "in")
+    make_pair(d, n_contigs=2, contig_len=400_000, pairs_per_contig=20_000, window_every=20_000)
+    path = os.path.join(d, "tumor.bam")
+    ref, helper = BamReader(path, 4), BamReader(path, 4)
+    u8p, i64p, i32p = C.POINTER(C.c_uint8), C.POINTER(C.c_int64), C.POINTER(C.c_int32)
+    REG = C.CFUNCTYPE(C.c_int, C.c_void_p, u8p, C.c_int64, i64p, i32p, i64p, i32p, C.c_int64, u8p, C.c_int64,
+                      C.c_int64, C.c_int32, C.c_int64, C.c_int64, C.c_int, C.POINTER(native.BamView),
+                      C.POINTER(C.c_void_p))
+    FF = C.CFUNCTYPE(C.c_int, C.c_void_p)
+    live, seen, mode = {}, [], ["done"]
+    cols_i32 = ("tid", "pos", "end", "flag", "mapq", "l_seq", "n_cigar", "mate_tid", "mate_pos", "tlen", "name_len",
+                "aux_len")
+    cols_i64 = ("name_off", "cig_off", "seq_off", "qual_off", "aux_off")
+    blobs = (("names", "names_blob", "names_bytes"), ("cigar", "cigar", "cigar_ops"), ("seq", "seq", "seq_bytes"),
+             ("qual", "qual", "qual_bytes"), ("aux", "aux", "aux_bytes"))
+
+    def decode(user, comp, comp_len, in_off, in_len, out_off, out_len, n, out, out_total, p0, tid, beg, end,
+               at_eof, cols, block):
+        seen.append((tid, beg, end, p0, mode[0]))
+        if mode[0] == "decline":
+            base_in, base_out = C.addressof(comp.contents), C.addressof(out.contents)
+            for i in range(n):
+                o = zlib.decompress(C.string_at(base_in + in_off[i], in_len[i]), -15)
+                C.memmove(base_out + out_off[i], o, len(o))
+            return 0
+        t = helper.region(tid, beg, end)
+        parts = [np.ascontiguousarray(getattr(t, f)) for f in cols_i32 + cols_i64] + \
+            [np.ascontiguousarray(getattr(t, a)) for _, a, _ in blobs]
+        offs, size = [], 0
+        for a in parts:
+            offs.append(size)
+            size += (a.nbytes + 255) // 256 * 256
+        buf = C.create_string_buffer(max(size, 1))
+        base = C.addressof(buf)
+        for a, o in zip(parts, offs):
+            if a.nbytes:
+                C.memmove(base + o, a.ctypes.data, a.nbytes)
+        v = cols.contents
+        v.n_records = t.n
+        for k, f in enumerate(cols_i32 + cols_i64):
+            setattr(v, f, C.cast(base + offs[k], type(getattr(v, f))))
+        for j, (f, a, nb) in enumerate(blobs):
+            k = len(cols_i32) + len(cols_i64) + j
+            setattr(v, f, C.cast(base + offs[k], type(getattr(v, f))) if f != "names" else base + offs[k])
+            setattr(v, nb, int(getattr(t, a).size))
+        live[base] = buf
+        block[0] = base
+        return 1
+
+    def release(p):
+        live.pop(p, None)
+        return 0
+    dec, rel = REG(decode), FF(release)
+    rd = BamReader(path, 4)
+    lib = native.host_lib()
+    lib.ganon_bam_reader_set_region_decoder(rd._h, C.cast(dec, C.c_void_p), None, 1, C.cast(rel, C.c_void_p))
+    for m in ("done", "decline"):
+        mode[0] = m
+        for tid, L in enumerate(ref.ref_lens):
+            for a, b in ((0, int(L)), (1000, 200_000), (150_000, 390_000), (399_000, int(L) + 5)):
+                exp, got = ref.region(tid, a, b), rd.region(tid, a, b)
+                assert got.n == exp.n and got.n > 0
+                for f in cols_i32 + cols_i64 + ("names_blob", "cigar", "seq", "qual", "aux"):
+                    assert np.array_equal(np.asarray(getattr(got, f)), np.asarray(getattr(exp, f))), (m, f)
+                assert seen[-1][:3] == (tid, a, b)
+        del got, exp
+        gc.collect()
+        assert not live                     # (each table's block released with its last view)
+    assert {s[4] for s in seen} == {"done", "decline"}
+    assert all(s[3] >= 0 for s in seen)
+    rd.close()
+    ref.close()
+    helper.close()

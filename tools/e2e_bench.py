@@ -211,6 +211,20 @@ def main():
                    open(os.path.join(out, f"{x}_whole{s}"), "rb").read()
                    for x in ("tumor", "normal") for s in (".1.fastq", ".2.fastq"))
         res["stream_equals_whole"] = same
+    if rank == 0 and os.environ.get("E2E_DIGEST") == "1":   # (outside the timed runs: A/B parity of settings)
+        import hashlib
+        dig = hashlib.sha1()
+        for mode in res:
+            if not isinstance(res[mode], dict):
+                continue
+            for x in ("tumor", "normal"):
+                for sfx in (".1.fastq", ".2.fastq", ".single_end.fastq"):
+                    p = os.path.join(out, f"{x}_{mode}{sfx}")
+                    if os.path.exists(p):
+                        with open(p, "rb") as f:
+                            for blk in iter(lambda: f.read(1 << 24), b""):
+                                dig.update(blk)
+        res["output_sha1"] = dig.hexdigest()
     if rank == 0 and os.environ.get("E2E_DISK_PROBE") == "1":
         res["disk"] = disk_probe(out)
     if rank == 0:

@@ -497,7 +497,7 @@ int columns(ganon_ctx *ctx, const uint8_t *d, int64_t p, int64_t n, ganon_bam_dc
         hipLaunchKernelGGL(k_bam_check, dim3(grid_of(nc)), dim3(kBamThreads), 0, s, nc, K);
       }
       if ((rc = check_launch(ctx, "k_bam_check"))) return rc;
-      HIP_OR_FAIL(hipMemcpyAsync(info, K.info, sizeof info, hipMemcpyDeviceToHost, s));
+      HIP_OR_FAIL(ganon_detail::readback(info, K.info, sizeof info, s));
       HIP_OR_FAIL(ganon_detail::sync_stream(s));
       // every chunk before the first failing one is exact: a bad walk there is the stream's error
       if (info[2] != ~0ull && info[2] < info[1]) {
@@ -528,7 +528,7 @@ int columns(ganon_ctx *ctx, const uint8_t *d, int64_t p, int64_t n, ganon_bam_dc
   }
   int64_t nr = 0;
   if (n_chunks) {
-    HIP_OR_FAIL(hipMemcpyAsync(&nr, base + n_chunks, 8, hipMemcpyDeviceToHost, s));
+    HIP_OR_FAIL(ganon_detail::readback(&nr, base + n_chunks, 8, s));
     HIP_OR_FAIL(ganon_detail::sync_stream(s));
   }
   // A region read: the window's records up to the region's end, those overlapping [beg, end) kept
@@ -561,7 +561,7 @@ int columns(ganon_ctx *ctx, const uint8_t *d, int64_t p, int64_t n, ganon_bam_dc
                            rg->end, keep, ri);
       }
       if ((rc = check_launch(ctx, "k_region_keep"))) return rc;
-      HIP_OR_FAIL(hipMemcpyAsync(info, ri, sizeof info, hipMemcpyDeviceToHost, s));
+      HIP_OR_FAIL(ganon_detail::readback(info, ri, sizeof info, s));
       HIP_OR_FAIL(ganon_detail::sync_stream(s));
     }
     if (info[2] || (info[1] != ~0ull && info[1] == info[0])) {
@@ -580,7 +580,7 @@ int columns(ganon_ctx *ctx, const uint8_t *d, int64_t p, int64_t n, ganon_bam_dc
       void *tsel = dalloc(tb);
       if (!tsel) return fail(ctx, GANON_E_DEVICE, "ganon_region_decode: device allocation failed");
       HIP_OR_FAIL(rocprim::select(tsel, tb, all, keep, sel, cnt, (size_t)cut, s));
-      HIP_OR_FAIL(hipMemcpyAsync(&nk, cnt, 8, hipMemcpyDeviceToHost, s));
+      HIP_OR_FAIL(ganon_detail::readback(&nk, cnt, 8, s));
       HIP_OR_FAIL(ganon_detail::sync_stream(s));
     }
     nr = nk;
@@ -634,9 +634,9 @@ int columns(ganon_ctx *ctx, const uint8_t *d, int64_t p, int64_t n, ganon_bam_dc
     }
     unsigned long long bad_rec = ~0ull;
     int64_t tot[5];
-    HIP_OR_FAIL(hipMemcpyAsync(&bad_rec, first_bad, 8, hipMemcpyDeviceToHost, s));
+    HIP_OR_FAIL(ganon_detail::readback(&bad_rec, first_bad, 8, s));
     int64_t *offs[5] = {V.name_off, V.cig_off, V.seq_off, V.qual_off, V.aux_off};
-    for (int k = 0; k < 5; ++k) HIP_OR_FAIL(hipMemcpyAsync(&tot[k], offs[k] + nr, 8, hipMemcpyDeviceToHost, s));
+    for (int k = 0; k < 5; ++k) HIP_OR_FAIL(ganon_detail::readback(&tot[k], offs[k] + nr, 8, s));
     HIP_OR_FAIL(ganon_detail::sync_stream(s));
     if (bad_rec != ~0ull) {
       if (rg) {

@@ -196,6 +196,17 @@ inline hipError_t sync_stream(hipStream_t s) {
   }
 }
 
+// A device-to-host copy into pageable host memory (a status word, a count, a small array): the
+// runtime stages such a copy and waits for the stream inside the call, spinning a core while the
+// stream's kernels run. The sleep poll waits for the stream first, so the copy finds it idle
+// (round 6: the region decoder's readbacks behind the inflate had cost up to 0.5 CPU-s per process
+// of the end-to-end line).
+inline hipError_t readback(void *dst, const void *src, size_t bytes, hipStream_t s) {
+  hipError_t e = sync_stream(s);
+  if (e != hipSuccess) return e;
+  return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s);
+}
+
 }  // namespace ganon_detail
 
 namespace ganon_wave {

@@ -1738,7 +1738,7 @@ GANON_API int64_t ganon_fastq_download(ganon_ctx *ctx, ganon_fastq *f, char *out
   if (!ctx || !f || (!out && f->total)) return kFailed;
   if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, GANON_E_DEVICE, "hipSetDevice failed"), kFailed;
   unsigned long long bad = ~0ull;
-  if (f->n && hipMemcpyAsync(&bad, f->err, sizeof bad, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess)
+  if (f->n && ganon_detail::readback(&bad, f->err, sizeof bad, ctx->stream) != hipSuccess)
     return fail(ctx, GANON_E_DEVICE, "error-slot copy failed"), kFailed;
   if (ganon_detail::sync_stream(ctx->stream) != hipSuccess) return fail(ctx, GANON_E_DEVICE, "formatter run failed"), kFailed;
   if (bad != ~0ull) {

@@ -1942,7 +1942,7 @@ struct HostCopy {
 template <typename T>
 int d2h_vec(ganon_ctx *ctx, std::vector<T> &v, const T *src, size_t n) {
   v.resize(n);
-  if (n) HIP_OR_FAIL(hipMemcpyAsync(v.data(), src, n * sizeof(T), hipMemcpyDeviceToHost, ctx->stream));
+  if (n) HIP_OR_FAIL(ganon_detail::readback(v.data(), src, n * sizeof(T), ctx->stream));
   return GANON_OK;
 }
 
@@ -2205,6 +2205,7 @@ std::multimap<size_t, void *> g_pin_free;   // capacity -> block
 std::map<void *, size_t> g_pin_cap;         // every live or cached block's capacity
 size_t g_pin_cached = 0;
 constexpr size_t kPinCacheMax = size_t(8) << 30;
+int64_t g_pin_stats[4] = {0, 0, 0, 0};      // blocks pinned anew, their bytes, seconds in hipHostMalloc, cache hits
 }  // namespace
 
 GANON_API int ganon_pinned_alloc(int64_t bytes, void **out) {
@@ -2215,6 +2216,7 @@ GANON_API int ganon_pinned_alloc(int64_t bytes, void **out) {
     std::lock_guard<std::mutex> lk(g_pin_mu);
     auto it = g_pin_free.lower_bound(want);
     if (it != g_pin_free.end() && it->first <= 2 * want + (size_t(16) << 20)) {
+      g_pin_stats[3] += 1;
       *out = it->second;
       g_pin_cached -= it->first;
       g_pin_free.erase(it);
@@ -2222,12 +2224,24 @@ GANON_API int ganon_pinned_alloc(int64_t bytes, void **out) {
     }
   }
   const size_t cap = (want + (size_t(2) << 20) - 1) & ~((size_t(2) << 20) - 1);
+  const auto t0 = std::chrono::steady_clock::now();
   if (hipHostMalloc(out, cap, hipHostMallocDefault) != hipSuccess) {
     *out = nullptr;
     return GANON_E_NOMEM;
   }
+  const int64_t ns = (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
   std::lock_guard<std::mutex> lk(g_pin_mu);
   g_pin_cap[*out] = cap;
+  g_pin_stats[0] += 1;
+  g_pin_stats[1] += (int64_t)cap;
+  g_pin_stats[2] += ns;
+  return GANON_OK;
+}
+
+GANON_API int ganon_pinned_stats(int64_t *out4) {
+  if (!out4) return GANON_E_ARG;
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  for (int k = 0; k < 4; ++k) out4[k] = g_pin_stats[k];
   return GANON_OK;
 }
 
@@ -2546,8 +2560,8 @@ GANON_API int ganon_batch_download(ganon_ctx *ctx, ganon_dbatch *db, uint8_t *se
   if ((rc = ganon_prep::batch_error(ctx, db))) return rc;
   int32_t status = 0;
   unsigned long long far_need = 0;
-  HIP_OR_FAIL(hipMemcpyAsync(&status, db->status, sizeof status, hipMemcpyDeviceToHost, st));
-  HIP_OR_FAIL(hipMemcpyAsync(&far_need, db->far_need, sizeof far_need, hipMemcpyDeviceToHost, st));
+  HIP_OR_FAIL(ganon_detail::readback(&status, db->status, sizeof status, st));
+  HIP_OR_FAIL(ganon_detail::readback(&far_need, db->far_need, sizeof far_need, st));
   HIP_OR_FAIL(ganon_detail::sync_stream(st));
   if (status & 4) {
     // a speculative replan the batch did not fit (a read with several segments, a longer read, a
@@ -2562,8 +2576,8 @@ GANON_API int ganon_batch_download(ganon_ctx *ctx, ganon_dbatch *db, uint8_t *se
     ctx->profiling = prof;
     if (rc) return rc;
     if ((rc = ganon_prep::batch_error(ctx, db))) return rc;
-    HIP_OR_FAIL(hipMemcpyAsync(&status, db->status, sizeof status, hipMemcpyDeviceToHost, st));
-    HIP_OR_FAIL(hipMemcpyAsync(&far_need, db->far_need, sizeof far_need, hipMemcpyDeviceToHost, st));
+    HIP_OR_FAIL(ganon_detail::readback(&status, db->status, sizeof status, st));
+    HIP_OR_FAIL(ganon_detail::readback(&far_need, db->far_need, sizeof far_need, st));
     HIP_OR_FAIL(ganon_detail::sync_stream(st));
   }
   if (status & 2) {
@@ -2590,7 +2604,7 @@ GANON_API int ganon_batch_download(ganon_ctx *ctx, ganon_dbatch *db, uint8_t *se
     rc = ganon_batch_run(ctx, db);
     ctx->profiling = prof;
     if (rc) return rc;
-    HIP_OR_FAIL(hipMemcpyAsync(&status, db->status, sizeof status, hipMemcpyDeviceToHost, st));
+    HIP_OR_FAIL(ganon_detail::readback(&status, db->status, sizeof status, st));
   }
   if (seq_out && db->seq_bytes)
     HIP_OR_FAIL(hipMemcpyAsync(seq_out, db->out, (size_t)db->seq_bytes, hipMemcpyDeviceToHost, st));
@@ -2635,7 +2649,7 @@ GANON_API int ganon_batch_gated_runs(ganon_ctx *ctx, ganon_dbatch *db, int64_t *
   if (!db->gated) return fail(ctx, GANON_E_STATE, "batch never loaded");
   HIP_OR_FAIL(hipSetDevice(ctx->device));
   unsigned long long g = 0;
-  HIP_OR_FAIL(hipMemcpyAsync(&g, db->gated, sizeof g, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_OR_FAIL(ganon_detail::readback(&g, db->gated, sizeof g, ctx->stream));
   HIP_OR_FAIL(ganon_detail::sync_stream(ctx->stream));
   *out = (int64_t)g;
   return GANON_OK;
@@ -2644,7 +2658,7 @@ GANON_API int ganon_batch_gated_runs(ganon_ctx *ctx, ganon_dbatch *db, int64_t *
 GANON_API int ganon_batch_path_counts(ganon_ctx *ctx, ganon_dbatch *db, int64_t *out4) {
   if (!ctx || !db || !out4) return fail(ctx, GANON_E_ARG, "null argument");
   HIP_OR_FAIL(hipSetDevice(ctx->device));
-  HIP_OR_FAIL(hipMemcpyAsync(out4, db->paths, 4 * sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+  HIP_OR_FAIL(ganon_detail::readback(out4, db->paths, 4 * sizeof(int64_t), ctx->stream));
   HIP_OR_FAIL(ganon_detail::sync_stream(ctx->stream));
   return GANON_OK;
 }

@@ -80,7 +80,8 @@ void huge_reserve(RawVec<T> &v, size_t n) {
 
 // Decoder phase clocks (ganon_host_phase_times): wall nanoseconds of the calling threads, summed over
 // calls and threads — where a reader's decode time goes (tools/e2e_bench.py reports them per rank).
-enum { kPhParse, kPhInflate, kPhWalk, kPhCopy, kPhRecWalk, kPhSizes, kPhColumns, kPhDevice, kPhN };
+enum { kPhParse, kPhInflate, kPhWalk, kPhCopy, kPhRecWalk, kPhSizes, kPhColumns, kPhDevice, kPhRead, kPhDeviceCpu,
+       kPhN };
 std::atomic<long long> g_phase_ns[kPhN];
 // region reads the device decoder finished, and those it handed back to the host's walk
 std::atomic<long long> g_dev_regions{0}, g_dev_fallbacks{0};
@@ -655,6 +656,7 @@ int64_t read_blocks(ganon_bam_reader *R, int64_t coff, int64_t step, Buf &data,
       got += r;
     }
     comp = R->cbuf;
+    lap(kPhRead, tph);
   } else if (R->map) {
     comp = R->map + coff;
     const uintptr_t pg = 4096, a = (uintptr_t)comp & ~(pg - 1);
@@ -696,10 +698,15 @@ int64_t read_blocks(ganon_bam_reader *R, int64_t coff, int64_t step, Buf &data,
       out_len[i] = blocks[i].out_len;
     }
     const int at_eof = coff + off >= R->fsize ? 1 : 0;
+    timespec c0{}, c1{};
+    clock_gettime(CLOCK_THREAD_CPUTIME_ID, &c0);
     const int r = R->rdec(R->rdec_user, comp, off, in_off.data(), in_len.data(), out_off.data(), out_len.data(),
                           (int64_t)nb, data.data() + base, total, rq->p0 + (int64_t)base, rq->tid, rq->beg, rq->end,
                           at_eof, &rq->cols, &rq->block);
     lap(kPhDevice, tph);
+    clock_gettime(CLOCK_THREAD_CPUTIME_ID, &c1);
+    g_phase_ns[kPhDeviceCpu].fetch_add((c1.tv_sec - c0.tv_sec) * 1000000000LL + (c1.tv_nsec - c0.tv_nsec),
+                                       std::memory_order_relaxed);
     if (r < 0) return set_err("BGZF inflate failed (region decoder)");
     if (r == 1) {
       rq->done = true;

@@ -1221,8 +1221,8 @@ GANON_API int64_t ganon_indel_download(ganon_ctx *ctx, ganon_indels *t, ganon_in
   }
   unsigned long long total = 0;
   int32_t cand = 0;
-  hipError_t e = hipMemcpyAsync(&total, t->counters, sizeof total, hipMemcpyDeviceToHost, ctx->stream);
-  if (e == hipSuccess) e = hipMemcpyAsync(&cand, t->n_dev(), sizeof cand, hipMemcpyDeviceToHost, ctx->stream);
+  hipError_t e = ganon_detail::readback(&total, t->counters, sizeof total, ctx->stream);
+  if (e == hipSuccess) e = ganon_detail::readback(&cand, t->n_dev(), sizeof cand, ctx->stream);
   if (e == hipSuccess) e = ganon_detail::sync_stream(ctx->stream);
   t->n_candidates = cand;
   if (e != hipSuccess) return fail(ctx, GANON_E_DEVICE, "indel download: %s", hipGetErrorString(e));

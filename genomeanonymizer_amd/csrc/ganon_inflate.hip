@@ -994,7 +994,7 @@ int ganon_inflate_impl(ganon_ctx *ctx, const uint8_t *comp, int64_t comp_len, co
   }
   std::vector<int32_t> stat(nb);
   okc = okc && d2h(n_chunks - 1) &&
-        hipMemcpyAsync(stat.data(), st->status, nb * 4, hipMemcpyDeviceToHost, cs) == hipSuccess &&
+        ganon_detail::readback(stat.data(), st->status, nb * 4, cs) == hipSuccess &&
         ganon_detail::sync_stream(cs) == hipSuccess;
   if (!okc) {
     ganon_detail::sync_stream(cs);

@@ -1751,7 +1751,7 @@ int size_plan(ganon_ctx *ctx, ganon_dbatch *db, int64_t ng, int tgt0, const Raw 
     HIP_OR_FAIL(hipMemsetAsync(db->cursor + kCursors, 0, kCursors * sizeof(unsigned long long), st));
     if ((rc = launch_groups(ctx, db, R)) || (rc = launch_emit(ctx, db, R, 0))) return rc;
     std::vector<unsigned long long> cur(2 * kCursors, 0);
-    HIP_OR_FAIL(hipMemcpyAsync(cur.data(), db->cursor, kCursors * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+    HIP_OR_FAIL(ganon_detail::readback(cur.data(), db->cursor, kCursors * sizeof(unsigned long long), st));
     HIP_OR_FAIL(ganon_detail::sync_stream(st));
     unsigned long long tseg = 0;
     for (int k = 0; k < kCursors; ++k) {
@@ -1913,11 +1913,11 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db, bool allow_spec) {
   PrepErr e{};
   unsigned int n_long = 0;
   std::vector<unsigned int> xc((size_t)kXStripes * kXStride, 0u);
-  HIP_OR_FAIL(hipMemcpyAsync(info, db->plan_info, sizeof info, hipMemcpyDeviceToHost, st));
-  HIP_OR_FAIL(hipMemcpyAsync(&e, db->err, sizeof e, hipMemcpyDeviceToHost, st));
-  HIP_OR_FAIL(hipMemcpyAsync(&n_long, long_count, sizeof n_long, hipMemcpyDeviceToHost, st));
+  HIP_OR_FAIL(ganon_detail::readback(info, db->plan_info, sizeof info, st));
+  HIP_OR_FAIL(ganon_detail::readback(&e, db->err, sizeof e, st));
+  HIP_OR_FAIL(ganon_detail::readback(&n_long, long_count, sizeof n_long, st));
   if (db->fused)
-    HIP_OR_FAIL(hipMemcpyAsync(xc.data(), db->xcount, xc.size() * sizeof(unsigned int), hipMemcpyDeviceToHost, st));
+    HIP_OR_FAIL(ganon_detail::readback(xc.data(), db->xcount, xc.size() * sizeof(unsigned int), st));
   HIP_OR_FAIL(ganon_detail::sync_stream(st));
   if (!e.code && n_long) {
     // reads with long CIGARs: a wave each, then the reduction again over both sets of partials
@@ -1932,8 +1932,8 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db, bool allow_spec) {
                        static_cast<const unsigned int *>(long_count), spec_maxseg,
                        static_cast<const unsigned int *>(db->xcount), (unsigned int)O.xper);
     if ((rc = check_launch(ctx, "k_prep_scan_long"))) return rc;
-    HIP_OR_FAIL(hipMemcpyAsync(info, db->plan_info, sizeof info, hipMemcpyDeviceToHost, st));
-    HIP_OR_FAIL(hipMemcpyAsync(&e, db->err, sizeof e, hipMemcpyDeviceToHost, st));
+    HIP_OR_FAIL(ganon_detail::readback(info, db->plan_info, sizeof info, st));
+    HIP_OR_FAIL(ganon_detail::readback(&e, db->err, sizeof e, st));
     HIP_OR_FAIL(ganon_detail::sync_stream(st));
   }
   if (e.code) return fail(ctx, GANON_E_ARG, err_text(e.code), e.index, e.a, e.b);
@@ -1997,11 +1997,11 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db, bool allow_spec) {
     HIP_OR_FAIL(rocprim::exclusive_scan(tmp, tb, cost, cost, (int64_t)0, (size_t)ns + 1, rocprim::plus<int64_t>(), st));
     int64_t last[2] = {0, 0}, rb_last = 0;   // the last scope's cost prefix, and the total
     int32_t ns_last = 0;
-    HIP_OR_FAIL(hipMemcpyAsync(last, cost + ns - 1, sizeof last, hipMemcpyDeviceToHost, st));
+    HIP_OR_FAIL(ganon_detail::readback(last, cost + ns - 1, sizeof last, st));
     if (nr) {
       HIP_OR_FAIL(rocprim::exclusive_scan(tmp, tb, nseg, rbase, (int64_t)0, (size_t)nr, rocprim::plus<int64_t>(), st));
-      HIP_OR_FAIL(hipMemcpyAsync(&rb_last, rbase + nr - 1, sizeof rb_last, hipMemcpyDeviceToHost, st));
-      HIP_OR_FAIL(hipMemcpyAsync(&ns_last, nseg + nr - 1, sizeof ns_last, hipMemcpyDeviceToHost, st));
+      HIP_OR_FAIL(ganon_detail::readback(&rb_last, rbase + nr - 1, sizeof rb_last, st));
+      HIP_OR_FAIL(ganon_detail::readback(&ns_last, nseg + nr - 1, sizeof ns_last, st));
     }
     HIP_OR_FAIL(ganon_detail::sync_stream(st));
     db->scost = cost;
@@ -2060,7 +2060,7 @@ int ws_diag(ganon_ctx *ctx, ganon_dbatch *db) {
 
 int batch_error(ganon_ctx *ctx, ganon_dbatch *db) {
   PrepErr e{};
-  HIP_OR_FAIL(hipMemcpyAsync(&e, db->err, sizeof e, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_OR_FAIL(ganon_detail::readback(&e, db->err, sizeof e, ctx->stream));
   HIP_OR_FAIL(ganon_detail::sync_stream(ctx->stream));
   if (e.code) return fail(ctx, GANON_E_ARG, err_text(e.code), e.index, e.a, e.b);
   return GANON_OK;

@@ -193,6 +193,7 @@ def hip_lib():
     lib.ganon_fastq_download.argtypes = [_p, _p, C.c_void_p, C.c_int64]
     lib.ganon_pinned_alloc.argtypes = [C.c_int64, C.POINTER(_p)]
     lib.ganon_pinned_free.argtypes = [_p]
+    lib.ganon_pinned_stats.argtypes = [_i64p]
     lib.ganon_fastq_download.restype = C.c_int64
     lib.ganon_fastq_free.argtypes = [_p, _p]
     lib.ganon_fastq_format_hip.restype = C.c_int64
@@ -247,7 +248,7 @@ EXPORTED_HIP_SYMBOLS = (
     "ganon_indel_upload", "ganon_indel_run", "ganon_indel_download", "ganon_indel_info", "ganon_indel_free",
     "ganon_inflate", "ganon_inflate_hostcb", "ganon_inflate_device_output",
     "ganon_bam_columns", "ganon_bam_dcols_get", "ganon_bam_dcols_download", "ganon_bam_dcols_free",
-    "ganon_pinned_alloc", "ganon_pinned_free", "ganon_region_decode",
+    "ganon_pinned_alloc", "ganon_pinned_free", "ganon_pinned_stats", "ganon_region_decode",
 )
 EXPORTED_HOST_SYMBOLS = (
     "ganon_bam_open", "ganon_bam_view_get", "ganon_bam_error", "ganon_bam_close",
@@ -749,7 +750,18 @@ def gather_ranges2(src0, src1, sel: np.ndarray, off: np.ndarray, length: np.ndar
 
 # (then two counts: region reads the device decoder finished, and those it handed back to the host)
 DECODE_PHASES = ("parse", "inflate", "region_walk", "kept_copy", "record_walk", "sizes", "columns", "device_region",
-                 "device_regions", "device_fallbacks")
+                 "read", "device_region_cpu", "device_regions", "device_fallbacks")
+
+
+def pinned_stats() -> dict:
+    """ganon_pinned_stats: the process's page-locked blocks pinned anew (count, bytes, seconds) and
+    the requests its cache served (an empty dict without the HIP library loaded)."""
+    if _hip is None:
+        return {}
+    out = np.zeros(4, np.int64)
+    hip_lib().ganon_pinned_stats(_ptr(out, _i64p))
+    return {"new_blocks": int(out[0]), "new_bytes": int(out[1]), "pin_s": round(out[2] * 1e-9, 4),
+            "cache_hits": int(out[3])}
 
 
 def decode_phase_times(reset: bool = False) -> dict:

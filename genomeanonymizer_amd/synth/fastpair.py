@@ -282,14 +282,9 @@ def _write_bam(path: str, contigs: List[Tuple[str, int]], per_contig, level: int
     return len(st)
 
 
-def make_pair(outdir: str, n_contigs: int = 24, contig_len: int = 2_000_000, pairs_per_contig: int = 23_000,
-              read_len: int = 150, seed: int = 7, snp_per_kb: float = 1.0, del_per_kb: float = 0.1,
-              window_every: int = 20_000, err: float = 0.001, clip_frac: float = 0.02, level: int = 1,
-              threads: int = 16, sec_frac: float = 0.0) -> Dict[str, str]:
-    os.makedirs(outdir, exist_ok=True)
-    rng = np.random.default_rng(seed)
-    names = [f"chr{i + 1}" for i in range(n_contigs)]
-    contigs = [_Contig(rng, contig_len, snp_per_kb, del_per_kb, window_every) for _ in names]
+def write_reference(outdir: str, names: List[str], contigs: List[_Contig]) -> Dict[str, str]:
+    """ref.fa (+ .fai), the window VCF and samples.tsv of a synthetic pair; the paths, with the BAM
+    paths the caller writes."""
     paths = {"ref": os.path.join(outdir, "ref.fa"), "vcf": os.path.join(outdir, "variants.vcf"),
              "T": os.path.join(outdir, "tumor.bam"), "N": os.path.join(outdir, "normal.bam")}
     # FASTA (60 columns) + .fai
@@ -321,6 +316,18 @@ def make_pair(outdir: str, n_contigs: int = 24, contig_len: int = 2_000_000, pai
                              for i, p in enumerate(c.windows.tolist())))
     with open(os.path.join(outdir, "samples.tsv"), "w") as fh:
         fh.write("#tumor\tnormal\tvcf\ntumor.bam\tnormal.bam\tvariants.vcf\n")
+    return paths
+
+
+def make_pair(outdir: str, n_contigs: int = 24, contig_len: int = 2_000_000, pairs_per_contig: int = 23_000,
+              read_len: int = 150, seed: int = 7, snp_per_kb: float = 1.0, del_per_kb: float = 0.1,
+              window_every: int = 20_000, err: float = 0.001, clip_frac: float = 0.02, level: int = 1,
+              threads: int = 16, sec_frac: float = 0.0) -> Dict[str, str]:
+    os.makedirs(outdir, exist_ok=True)
+    rng = np.random.default_rng(seed)
+    names = [f"chr{i + 1}" for i in range(n_contigs)]
+    contigs = [_Contig(rng, contig_len, snp_per_kb, del_per_kb, window_every) for _ in names]
+    paths = write_reference(outdir, names, contigs)
     with ThreadPoolExecutor(threads) as pool:
         for tag, tumor in (("T", True), ("N", False)):
             recs = []   # per contig: the record columns, secondaries from other contigs appended below

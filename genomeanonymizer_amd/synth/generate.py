@@ -495,6 +495,25 @@ def fuzz_scenario(seed: int) -> ScenarioConfig:
                           duplicate_frac=0.02 if seed >= 3500 else 0.0)
 
 
+# Golden inputs made by synth/longpair.py instead of a ScenarioConfig (the long-read end-to-end
+# line's shape at golden size; always BAI-indexed)
+LONGPAIR_GOLDEN = {"longpair": dict(n_contigs=2, contig_len=600_000, pairs_per_contig=12, seed=1,
+                                    window_every=30_000)}
+
+
+def make_inputs(name: str, outdir: str, bam_index: bool = False) -> Dict[str, str]:
+    """The inputs of golden scenario ``name``: generate(scenario(name)) (``bam_index``: with .bai
+    files), or synth/longpair.py for the names of LONGPAIR_GOLDEN."""
+    if name in LONGPAIR_GOLDEN:
+        from .longpair import make_long_pair
+        return make_long_pair(outdir, **LONGPAIR_GOLDEN[name])
+    sc = scenario(name)
+    if bam_index:
+        import dataclasses
+        sc = dataclasses.replace(sc, bam_index=True)
+    return generate(sc, outdir)
+
+
 def scenario(name: str) -> ScenarioConfig:
     if name.startswith("fuzz"):
         return fuzz_scenario(int(name[4:]))

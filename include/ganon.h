@@ -98,6 +98,9 @@ GANON_API const char *ganon_last_error(ganon_ctx *ctx);
  * Returns GANON_OK or GANON_E_NOMEM. */
 GANON_API int ganon_pinned_alloc(int64_t bytes, void **out);
 GANON_API int ganon_pinned_free(void *p);
+/* The process's page-locked block counters since it started: out4 = {blocks pinned anew, their bytes,
+ * nanoseconds spent pinning them (hipHostMalloc), requests served from the cache}. */
+GANON_API int ganon_pinned_stats(int64_t *out4);
 GANON_API int ganon_abi_version(void);
 /* Use an external hipStream_t (e.g. torch's current stream); NULL = the ctx's own. */
 GANON_API int ganon_ctx_set_stream(ganon_ctx *ctx, void *hip_stream);

@@ -13,6 +13,9 @@ usage: python oracle/fuzz_reference.py SEED [SEED ...]
        FUZZ_FASTPAIR=N_CONTIGS,CONTIG_LEN,PAIRS,SEC_FRAC python oracle/fuzz_reference.py SEED ...
        (the sample from synth/fastpair.py instead: the end-to-end bench's input shape, with SEC_FRAC
        of the pairs given an off-contig secondary alignment of read 1; BAMs indexed)
+       FUZZ_LONGPAIR=N_CONTIGS,CONTIG_LEN,PAIRS python oracle/fuzz_reference.py SEED ...
+       (synth/longpair.py: the long-read end-to-end line's shape — 10-100 kb paired reads with
+       soft clips, sequencing and germline indels; BAMs indexed)
 """
 from __future__ import annotations
 
@@ -80,7 +83,13 @@ def main():
     for seed in [int(x) for x in sys.argv[1:]]:
         work = tempfile.mkdtemp(prefix=f"ganon_fuzz_{seed}_")
         fp = os.environ.get("FUZZ_FASTPAIR")
-        if fp:
+        lp = os.environ.get("FUZZ_LONGPAIR")
+        if lp:
+            from genomeanonymizer_amd.synth.longpair import make_long_pair
+            nc, cl, pp = lp.split(",")
+            paths = make_long_pair(os.path.join(work, "in"), n_contigs=int(nc), contig_len=int(cl),
+                                   pairs_per_contig=int(pp), seed=seed, window_every=max(5000, int(cl) // 20))
+        elif fp:
             from genomeanonymizer_amd.synth.fastpair import make_pair
             nc, cl, pp, sf = fp.split(",")
             paths = make_pair(os.path.join(work, "in"), n_contigs=int(nc), contig_len=int(cl), pairs_per_contig=int(pp),

@@ -76,7 +76,7 @@ def _digest_inputs(paths) -> dict:
 
 def run_reference(scenario_name: str, golden_root: str) -> dict:
     sys.path.insert(0, REPO)
-    from genomeanonymizer_amd.synth.generate import generate, scenario
+    from genomeanonymizer_amd.synth.generate import make_inputs
 
     work = tempfile.mkdtemp(prefix=f"ganon_ref_{scenario_name}_")
     mod_dir = os.path.join(work, "_mods")
@@ -89,7 +89,7 @@ def run_reference(scenario_name: str, golden_root: str) -> dict:
             sys.path.insert(0, p)
 
     inputs = os.path.join(work, "in")
-    paths = generate(scenario(scenario_name), inputs)
+    paths = make_inputs(scenario_name, inputs)
 
     from src.GenomeAnonymizer.anonymizer_methods import CompleteGermlineAnonymizer
     from src.GenomeAnonymizer.short_read_tumor_normal_anonymizer import (
@@ -125,7 +125,7 @@ def run_reference(scenario_name: str, golden_root: str) -> dict:
         files["normal.statistics.txt"] = hashlib.sha256(fi.read()).hexdigest()
     meta = {"scenario": scenario_name, "inputs_sha256": _digest_inputs(paths),
             "outputs_sha256": files, "reference_seconds": round(elapsed, 2),
-            "generator": "genomeanonymizer_amd.synth.generate.scenario(%r)" % scenario_name,
+            "generator": "genomeanonymizer_amd.synth.generate.make_inputs(%r)" % scenario_name,
             "entry": "run_short_read_tumor_normal_anonymizer(..., CompleteGermlineAnonymizer(), "
                      "record_statistics=True, cpus=1, enhance_parallelization=False)"}
     with open(os.path.join(dest, "meta.json"), "w") as fh:

@@ -28,14 +28,12 @@ def run_pipeline_vs_golden(name: str, workdir: str, anonymizer, block_size: int 
     """Regenerate the scenario's inputs, run the product pipeline, compare every output
     file with the reference's. Returns a dict of mismatches (empty = byte-identical).
     ``bam_index``: write .bai files too (the streamed path's job mode reads regions through them)."""
-    import dataclasses
-    from genomeanonymizer_amd.synth.generate import generate, scenario
+    from genomeanonymizer_amd.synth.generate import make_inputs
     from genomeanonymizer_amd import short_read_tumor_normal_anonymizer as sr
     from genomeanonymizer_amd import writer
     meta = json.load(open(os.path.join(GOLDEN, name, "meta.json")))
     shutil.rmtree(workdir, ignore_errors=True)
-    sc = dataclasses.replace(scenario(name), bam_index=True) if bam_index else scenario(name)
-    paths = generate(sc, os.path.join(workdir, "in"))
+    paths = make_inputs(name, os.path.join(workdir, "in"), bam_index)
     assert input_digests(paths) == meta["inputs_sha256"], "synthetic generator drifted from the fixtures"
     t_out, n_out = sr.name_output(paths["T"]), sr.name_output(paths["N"])
     orig = writer.io_block_size

@@ -245,7 +245,8 @@ def test_hip_deep_coverage_filter_matches_oracle(masker, oracle):
 
 
 @pytest.mark.parametrize("whole", [False, True], ids=["streaming", "whole_sample"])
-@pytest.mark.parametrize("name", ["tiny", "edge", "config1", "fuzz5", "fuzz9", "long1", "fuzz9001", "long2"])
+@pytest.mark.parametrize("name", ["tiny", "edge", "config1", "fuzz5", "fuzz9", "long1", "fuzz9001", "long2",
+                                  "longpair"])
 def test_hip_pipeline_matches_reference(name, whole, tmp_path, hip_built, monkeypatch):
     from genomeanonymizer_amd.anonymizer_methods import CompleteGermlineAnonymizer
     monkeypatch.setenv("GANON_WHOLE_SAMPLE", "1" if whole else "0")

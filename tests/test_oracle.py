@@ -24,7 +24,8 @@ def test_oracle_matches_reference_per_scope(seed):
 
 
 @pytest.mark.parametrize("whole", [False, True], ids=["streaming", "whole_sample"])
-@pytest.mark.parametrize("name", ["tiny", "edge", "config1", "fuzz5", "fuzz9", "long1", "fuzz9001", "long2"])
+@pytest.mark.parametrize("name", ["tiny", "edge", "config1", "fuzz5", "fuzz9", "long1", "fuzz9001", "long2",
+                                  "longpair"])
 def test_pipeline_with_oracle_matches_reference(name, whole, tmp_path, monkeypatch):
     from pyoracle import OracleEngine
     from genomeanonymizer_amd.anonymizer_methods import CompleteGermlineAnonymizer

@@ -148,6 +148,7 @@ def main():
                 sampler = Sampler().__enter__()
             from genomeanonymizer_amd import native as _nat
             _nat.decode_phase_times(reset=True)
+            pin0 = _nat.pinned_stats()
             t1, c1 = time.time(), os.times()
             tim = sr.anonymize_genome(windows, os.path.join(d, "tumor.bam"), os.path.join(d, "normal.bam"),
                                       os.path.join(d, "ref.fa"), anon, os.path.join(out, f"tumor_{mode}"),
@@ -155,6 +156,8 @@ def main():
                                       streaming=(mode == "stream"), dist=dist)
             tim["wall_s"] = time.time() - t1
             tim["decode_phases"] = _nat.decode_phase_times()
+            pin1 = _nat.pinned_stats()
+            tim["pinned"] = {k: round(pin1[k] - pin0.get(k, 0), 4) for k in pin1}
             if sampler is not None:
                 sampler.__exit__(None, None, None)
                 sampler.report(f"{os.environ['E2E_SAMPLE']}_{mode}_r{rank}.json")
@@ -165,7 +168,8 @@ def main():
                 dist.all_gather_object(per_rank, {k: tim.get(k) for k in (
                     "wall_s", "exchange_sent_bytes", "exchange_recv_bytes", "wait_s", "writer_wait_s", "jobs",
                     "decode_s", "mask_s", "format_s", "write_s", "redos_skipped", "critical_path", "cpu_s", "fastq_device",
-                    "setup_s", "groups_s", "tail_parts", "prep_parts", "decode_thread_s", "prefetch_s", "decode_phases")})
+                    "setup_s", "groups_s", "tail_parts", "prep_parts", "decode_thread_s", "prefetch_s", "decode_phases",
+                    "pinned")})
                 tim["per_rank"] = per_rank
                 import torch
                 w = torch.tensor([tim["wall_s"]], dtype=torch.float64)

@@ -63,6 +63,14 @@ struct ganon_ctx {
   std::multimap<size_t, void *> dcache;
   size_t dcache_bytes = 0;
   ganon_inflate_state *inflate = nullptr;   // BGZF inflate buffers (first ganon_inflate)
+  // GANON_INDEL_FORK=1: the indel tally of a batch runs on a side stream forked after the batch's
+  // prep (fork_ev, recorded by ganon_batch_run before the group kernel) and joined back (join_ev), so
+  // that its latency-bound launches overlap the bandwidth-bound group kernel (they read only the
+  // prep's outputs and the raw reads)
+  int indel_fork = -1;          // -1: read from the environment at first use
+  hipStream_t side = nullptr;
+  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+  const void *fork_db = nullptr;   // the batch fork_ev belongs to (nullptr: none pending)
 };
 
 // A device block of at least `bytes` from the context's cache (at most 2x larger), else hipMalloc.

@@ -2189,6 +2189,12 @@ GANON_API int ganon_ctx_destroy(ganon_ctx *ctx) {
     hipEventDestroy(r.e1);
   }
   for (auto e : ctx->pool) hipEventDestroy(e);
+  if (ctx->side) {
+    ganon_detail::sync_stream(ctx->side);
+    hipStreamDestroy(ctx->side);
+  }
+  if (ctx->fork_ev) hipEventDestroy(ctx->fork_ev);
+  if (ctx->join_ev) hipEventDestroy(ctx->join_ev);
   for (auto &b : ctx->dcache) hipFree(b.second);
   ganon_inflate_free(ctx->inflate);
   delete ctx;
@@ -2445,6 +2451,15 @@ GANON_API int ganon_batch_run(ganon_ctx *ctx, ganon_dbatch *db) {
   const int u = ctx->group_unroll ? ctx->group_unroll : db->long_mode ? 1 : 2;
   // 1. derived layer from the raw SoA
   if ((rc = ganon_prep::run(ctx, db))) return rc;
+  if (ctx->indel_fork < 0) {
+    const char *v = std::getenv("GANON_INDEL_FORK");
+    ctx->indel_fork = v && v[0] == '1' ? 1 : 0;
+  }
+  if (ctx->indel_fork) {   // (the fork point of this batch's indel tally: its inputs are final here)
+    if (!ctx->fork_ev) HIP_OR_FAIL(hipEventCreateWithFlags(&ctx->fork_ev, hipEventDisableTiming));
+    HIP_OR_FAIL(hipEventRecord(ctx->fork_ev, st));
+    ctx->fork_db = db;
+  }
   if (db->n_huge_scopes) {
     // huge scopes are counted with atomics (tiles)
     HIP_OR_FAIL(hipMemsetAsync(db->scope_calls, 0, (size_t)db->n_scopes * sizeof(int32_t), st));

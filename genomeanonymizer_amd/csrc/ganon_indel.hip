@@ -815,6 +815,7 @@ int bits_for(int64_t v) {   // bits to hold 0..v
 struct ganon_indels {
   std::vector<void *> allocs;
   GanonReadView V{};
+  const void *db = nullptr;           // the device batch it tallies (the fork point, ctx->fork_db)
   int64_t n_obs = 0, n_list = 0, n_rdist = 0, n_records = -1, n_candidates = -1;
   int32_t n_seg = 0;                  // scopes with observations (segments of the sort)
   int pos_bits = 1, key_bits = 2;
@@ -1110,6 +1111,7 @@ GANON_API int ganon_indel_upload(ganon_ctx *ctx, const ganon_batch *b, const gan
   if (n_obs >= (int64_t)INT32_MAX) return fail(ctx, GANON_E_ARG, "indel upload: %lld observations (max 2^31-1)", (long long)n_obs);
   ganon_indels *t = new ganon_indels();
   t->V = V;
+  t->db = db;
   t->n_obs = n_obs;
   t->n_list = (int64_t)list.size();
   t->n_ilist = (int64_t)ilist.size();
@@ -1208,7 +1210,21 @@ GANON_API int ganon_indel_run(ganon_ctx *ctx, ganon_indels *t) {
   if (t->n_obs == 0) return GANON_OK;
   t->global = ctx->indel_sort != 0;
   t->key64 = t->global || t->gsort;
-  return t->key64 ? run_tally<unsigned long long>(ctx, t) : run_tally<uint32_t>(ctx, t);
+  if (!(ctx->indel_fork > 0 && ctx->fork_db && ctx->fork_db == t->db))
+    return t->key64 ? run_tally<unsigned long long>(ctx, t) : run_tally<uint32_t>(ctx, t);
+  // on the side stream from the batch's fork point, joined back into the context's stream (every
+  // later operation of the context — downloads, the next plan — waits for the tally)
+  ctx->fork_db = nullptr;
+  if (!ctx->side) HIP_OR_FAIL(hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
+  if (!ctx->join_ev) HIP_OR_FAIL(hipEventCreateWithFlags(&ctx->join_ev, hipEventDisableTiming));
+  const hipStream_t main = ctx->stream;
+  HIP_OR_FAIL(hipStreamWaitEvent(ctx->side, ctx->fork_ev, 0));
+  ctx->stream = ctx->side;
+  const int rc = t->key64 ? run_tally<unsigned long long>(ctx, t) : run_tally<uint32_t>(ctx, t);
+  ctx->stream = main;
+  HIP_OR_FAIL(hipEventRecord(ctx->join_ev, ctx->side));
+  HIP_OR_FAIL(hipStreamWaitEvent(main, ctx->join_ev, 0));
+  return rc;
 }
 
 GANON_API int64_t ganon_indel_download(ganon_ctx *ctx, ganon_indels *t, ganon_indel_rec *out, int64_t cap) {

@@ -67,6 +67,9 @@ def main():
                                             "jobs": r["jobs"], "wait_s": round(r["wait_s"], 3),
                                             "wall_s": round(r["wall_s"], 3)} for r in m["per_rank"]],
                "critical_path_s_rank0": m.get("critical_path_s_rank0"),
+               # every rank's wall split (stream.py critical_path) and rank 0's tail, part by part
+               "critical_path_s_per_rank": [r.get("critical_path") for r in m["per_rank"]],
+               "tail_parts_s_per_rank": [r.get("tail_parts") for r in m["per_rank"]],
                "one_process_contig_mode": {"wall_s": one["stream"]["stages_s"]["wall_s"],
                                            "reads_per_s": one["stream"]["reads_per_s"]},
                "files_equal_one_process": same, "host": {"nproc": os.cpu_count()}}

@@ -23,12 +23,19 @@ def main():
     cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
     args = argparse.Namespace(config=cfg, **bench.CONFIGS[cfg]["defaults"])
+    # SWEEP_SHAPE="reads=10000000,genome=25000000,...": the shape of a bench side line instead of the
+    # config's defaults; SWEEP_TARGETS / SWEEP_UNROLL: comma lists for the grid
+    for kv in filter(None, os.environ.get("SWEEP_SHAPE", "").split(",")):
+        k, v = kv.split("=")
+        setattr(args, k, int(v))
     args.batches = args.pipeline = 1   # (one batch of the configured size)
     arr, _ = bench.make_batch(args, 0, 0)
     m = native.HipMasker(0)
     ref = m.upload_reference(arr["ref_nt16"])
     mode = sys.argv[3] if len(sys.argv) > 3 else "grid"
-    settings = [(u, t) for t in (352, 704, 1408) for u in (1, 2, 4)] if mode == "grid" else [(0, 0)]
+    tl = [int(x) for x in os.environ.get("SWEEP_TARGETS", "352,704,1408").split(",")]
+    ul = [int(x) for x in os.environ.get("SWEEP_UNROLL", "1,2,4").split(",")]
+    settings = [(u, t) for t in tl for u in ul] if mode == "grid" else [(0, 0)]
     obs_list = (512, 1024) if mode == "obs" else (0,)
     pu_list = (1, 2, 4) if mode == "prep" else (0,)
     if mode == "prep":

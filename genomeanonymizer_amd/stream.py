@@ -55,6 +55,57 @@ def _names(table: ReadTable, rows: np.ndarray) -> List[bytes]:
     return [nb[o:o + n].tobytes() for o, n in zip(table.name_off[rows].tolist(), table.name_len[rows].tolist())]
 
 
+_NK = (np.uint64(0x9E3779B97F4A7C15), np.uint64(0xC2B2AE3D27D4EB4F), np.uint64(0x165667B19E3779F9))
+
+
+def _name_keys(blob: np.ndarray, off: np.ndarray, ln: np.ndarray) -> np.ndarray:
+    """A 64-bit key per name (blob[off:off + ln]): its length with its first and last eight bytes
+    (shorter names: their bytes, zero-padded). Equal names have equal keys; the rare unequal names with
+    equal keys are told apart by the caller's byte comparison."""
+    buf = np.zeros(len(blob) + 16, np.uint8)
+    buf[:len(blob)] = blob
+    off = off.astype(np.int64)
+    ln = ln.astype(np.int64)
+    idx = np.arange(8, dtype=np.int64)
+    first = buf[off[:, None] + idx]
+    first[idx[None, :] >= ln[:, None]] = 0
+    last = buf[np.maximum(off, off + ln - 8)[:, None] + idx]
+    last[idx[None, :] >= ln[:, None]] = 0
+    w0 = first.view(np.uint64).ravel()
+    w1 = last.view(np.uint64).ravel()
+    with np.errstate(over="ignore"):
+        return (w0 * _NK[0]) ^ (w1 * _NK[1]) ^ (ln.astype(np.uint64) * _NK[2])
+
+
+def _names_present(table: ReadTable, names: Sequence[bytes]) -> set:
+    """The names of ``names`` that some record of ``table`` carries: one vectorized pass over the
+    table's names (keys, then a byte comparison of the key hits) instead of a search of the names
+    blob per name (5,362 blob searches took 14.9 s of a 2-rank CPU run's 22.8 s, `redo_needed`)."""
+    if not len(names) or table.n == 0:
+        return set()
+    cand = list(names)
+    cb = np.frombuffer(b"".join(cand), np.uint8)
+    cl = np.array([len(x) for x in cand], np.int64)
+    co = np.concatenate([[0], np.cumsum(cl)[:-1]]).astype(np.int64)
+    ck = _name_keys(cb, co, cl)
+    tk = _name_keys(table.names_blob, table.name_off, table.name_len)
+    hit = np.isin(ck, tk)
+    if not hit.any():
+        return set()
+    order = np.argsort(tk, kind="stable")
+    sk = tk[order]
+    nb = table.names_blob
+    out = set()
+    for i in np.nonzero(hit)[0].tolist():
+        lo, hi = np.searchsorted(sk, ck[i], "left"), np.searchsorted(sk, ck[i], "right")
+        for r in order[lo:hi].tolist():
+            o, n = int(table.name_off[r]), int(table.name_len[r])
+            if nb[o:o + n].tobytes() == cand[i]:
+                out.add(cand[i])
+                break
+    return out
+
+
 def _names_ds(tables, ds: np.ndarray, rows: np.ndarray) -> List[bytes]:
     out: List[bytes] = [b""] * len(ds)
     for d in (0, 1):
@@ -833,11 +884,9 @@ class Job(JobPrep):
         for t in self.tables:
             if not len(new) or t.n == 0:
                 continue
-            blob = b"\0" + t.names_blob.tobytes()   # (BAM names: NUL-terminated, back to back)
-            keep = []
-            for nm in new:
-                (out if blob.find(b"\0" + nm + b"\0") >= 0 else keep).append(nm)
-            new = keep
+            found = _names_present(t, new)
+            out.extend(nm for nm in new if nm in found)
+            new = [nm for nm in new if nm not in found]
         return sorted(out)
 
 

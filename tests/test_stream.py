@@ -368,6 +368,29 @@ def test_decoded_blobs_are_views_kept_alive(tmp_path):
     del junk
 
 
+def test_names_present_equals_blob_search(tmp_path):
+    """stream._names_present (one vectorized pass, Job.redo_needed) finds exactly the names a search
+    of the NUL-separated names blob finds: present names, absent ones, prefixes and extensions of
+    present names, names of every length around the 8-byte key words, empty input."""
+    from genomeanonymizer_amd import stream
+    from genomeanonymizer_amd.io.bam import BamReader
+    from genomeanonymizer_amd.synth.generate import generate, scenario
+    paths = generate(scenario("fuzz3000"), str(tmp_path / "in"))
+    R = BamReader(paths["T"], threads=2)
+    t = R.contig(0)
+    present = stream._names(t, np.arange(t.n))
+    rng = np.random.default_rng(7)
+    pick = [present[i] for i in rng.choice(len(present), 200, replace=False)]
+    probes = pick + [p[:-1] for p in pick[:40]] + [p + b"x" for p in pick[:40]] + \
+        [b"q" * k for k in range(1, 20)] + [p[:8] for p in pick[:20]] + [b"no_such_read_%d" % i for i in range(50)]
+    blob = b"\0" + t.names_blob.tobytes()
+    want = {nm for nm in probes if blob.find(b"\0" + nm + b"\0") >= 0}
+    assert stream._names_present(t, probes) == want
+    assert set(pick) <= want
+    assert stream._names_present(t, []) == set()
+    R.close()
+
+
 def _python_buffer_alloc():
     """A ganon_buf_alloc_fn / ganon_buf_free_fn pair over ctypes buffers (the page-locked allocator's
     stand-in on the CPU), with the live blocks and the number of allocations."""

@@ -337,6 +337,24 @@ class SecondaryIndex:
         # several ranks: distributed.SecondaryExchange — every job's secondaries reach every later
         # job's plan whichever rank decodes them (a plan waits until every earlier job is decoded)
         self.remote = None
+        # speculative plans checked against their permit, and how many had to be planned again:
+        # when at least half of them were (secondaries common in the data), later jobs wait for
+        # their permit before planning instead (GANON_SPEC_PLAN=1 / 0 forces either way)
+        self.spec_checked = 0
+        self.spec_redone = 0
+
+    def speculate(self) -> bool:
+        """Plan the next job at once with the names known here (True) or wait for its permit."""
+        mode = os.environ.get("GANON_SPEC_PLAN", "auto")
+        if mode in ("0", "1"):
+            return mode == "1"
+        with self.lock:
+            return self.spec_checked < 2 or 2 * self.spec_redone < self.spec_checked
+
+    def note_spec(self, redone: bool) -> None:
+        with self.lock:
+            self.spec_checked += 1
+            self.spec_redone += bool(redone)
 
     def job_of(self, ds: int, tid: np.ndarray, pos: np.ndarray) -> np.ndarray:
         """The job reading position pos of BAM tid (-1: none)."""
@@ -415,7 +433,8 @@ class JobPrep:
         # permitted names change its plan is planned again there). Waiting for it here put the decode
         # frontier of all earlier jobs on every plan's critical path (up to 0.6 s per rank on the 30x
         # line's later ranks, with no secondary in the data).
-        self.speculative = force is None and secondaries is not None and secondaries.remote is not None
+        self.speculative = force is None and secondaries is not None and secondaries.remote is not None and \
+            secondaries.speculate()
         if force is None:
             force = (secondaries.forced_local(self.job) if self.speculative else secondaries.forced_for(self.job)) \
                 if secondaries is not None else []
@@ -1315,7 +1334,9 @@ def anonymize_genome_streaming(windows: List[Window], tumor_bam: str, normal_bam
                     t_p = time.time()
                     full = secondaries.forced_for(job.job)
                     timing["permit_check_s"] = timing.get("permit_check_s", 0.0) + time.time() - t_p
-                    if job.redo_needed(full):   # planned again with them, on the redo readers
+                    redo = job.redo_needed(full)
+                    secondaries.note_spec(bool(redo))
+                    if redo:   # planned again with them, on the redo readers
                         timing["spec_replans"] = timing.get("spec_replans", 0) + 1
                         job.release_device()
                         if not redo_readers:

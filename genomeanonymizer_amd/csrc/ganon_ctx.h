@@ -33,7 +33,7 @@ struct ganon_ctx {
   int variant = GANON_VARIANT_DEFAULT;
   int group_unroll = 0;        // GANON_PARAM_GROUP_UNROLL (0 auto: 1 for long reads, else 2)
   int group_skip = 0;          // GANON_PARAM_GROUP_SKIP (profiling only)
-  int group_target = 0;        // GANON_PARAM_GROUP_TARGET (0 auto: 704 short reads, 1408 long-read mode), cost units per group (segments + a
+  int group_target = 0;        // GANON_PARAM_GROUP_TARGET (0 auto: 704 short reads, 2816 long-read mode), cost units per group (segments + a
                                // per-scope weight of 3: ~512 segments on configs[1], two staging tiles)
   int nt_copy = 1;             // GANON_PARAM_NT_COPY
   int ref2 = 1;                // GANON_PARAM_REF2

@@ -1964,7 +1964,7 @@ int plan(ganon_ctx *ctx, ganon_dbatch *db, bool allow_spec) {
   if (!db->fused) db->cand = nullptr;
   // overflow-region observations per incidence: the longest read's ceil(L / 48)
   db->region_per_incid = (int64_t)((max_len + 47) / 48);
-  db->group_target = ctx->group_target ? ctx->group_target : db->long_mode ? 1408 : 704;   // auto (sweep_c5 / sweep_c3)
+  db->group_target = ctx->group_target ? ctx->group_target : db->long_mode ? 2816 : 704;   // auto (profiles/r06/sweep: c5 2816 1.99 vs 1408 2.08 ms, c3 704)
   db->n_id_ops = (int64_t)info[0];
   db->max_len = (int64_t)max_len;
   db->max_seg = (int64_t)max_seg;

@@ -639,14 +639,15 @@ def test_long_prep_config2_matches_oracle(masker_long, oracle):
 
 def test_long_reads_c5_shape_groups_are_balanced(masker, oracle):
     """C5-shaped batch (reads of thousands of CIGAR ops): the long-read prep cuts groups on
-    segments, so no group holds more than a few times the target, and results equal the oracle."""
+    segments, so no group holds more than a few times the target (2816 segments in long-read mode
+    since round 6: groups average at most twice that), and results equal the oracle."""
     from genomeanonymizer_amd.synth.batch import longread_batch
     arr, info = longread_batch(7, n_reads=400)
     o_out, o_calls, o_bases, _ = oracle.mask(arr)
     db = masker.upload(arr)
     try:
         bi = db.info()
-        assert bi["groups"] * 512 >= bi["segments"] // 4, bi
+        assert bi["groups"] * 2 * 2816 >= bi["segments"], bi
         db.run()
         out, calls, bases, tot = db.download()
     finally:

@@ -380,8 +380,14 @@ __device__ __forceinline__ void scatter_record(const ganon_bam_cols &V, int64_t 
   }
 }
 
-constexpr int kScatRecs = 16;      // records per workgroup (four per wave)
-constexpr int kStage = 16384;      // LDS bytes staged per workgroup
+#ifndef GANON_SCAT_RECS
+#define GANON_SCAT_RECS 16         // (A/B builds: tools/build_variant.py)
+#endif
+#ifndef GANON_SCAT_STAGE
+#define GANON_SCAT_STAGE 16384
+#endif
+constexpr int kScatRecs = GANON_SCAT_RECS;    // records per workgroup (four per wave)
+constexpr int kStage = GANON_SCAT_STAGE;      // LDS bytes staged per workgroup
 
 // A wave per record. The workgroup's run of kScatRecs records (back to back in the stream) is first
 // copied to LDS with coalesced aligned dword loads, then each wave reads its record's bytes from

@@ -381,12 +381,12 @@ __device__ __forceinline__ void scatter_record(const ganon_bam_cols &V, int64_t 
 }
 
 #ifndef GANON_SCAT_RECS
-#define GANON_SCAT_RECS 16         // (A/B builds: tools/build_variant.py)
+#define GANON_SCAT_RECS 32         // (profiles/r06/bam_sr: 8 0.643, 16 0.615, 32 0.598, 64 0.836 ms)
 #endif
 #ifndef GANON_SCAT_STAGE
 #define GANON_SCAT_STAGE 16384
 #endif
-constexpr int kScatRecs = GANON_SCAT_RECS;    // records per workgroup (four per wave)
+constexpr int kScatRecs = GANON_SCAT_RECS;    // records per workgroup (eight per wave)
 constexpr int kStage = GANON_SCAT_STAGE;      // LDS bytes staged per workgroup
 
 // A wave per record. The workgroup's run of kScatRecs records (back to back in the stream) is first
